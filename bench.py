@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Kafka records/sec delivered to the GPU with a commit after every batch.
+
+BASELINE.json metric "Kafka records/sec to GPU with per-batch commit, at
+1/2/4/8 MI355X".  Configurations (BASELINE.json ``configs``):
+
+  * N = 1 : config 2 -- 1x MI355X, num_workers=4, 8-partition topic,
+            fixed-width float32 records (256 x f32 = 1 KiB), pinned ring +
+            hipMemcpyAsync on a side stream, gfx950 collate kernel -> bf16;
+  * N > 1 : config 3 -- one process per GPU (torchrun), 8 partitions per rank
+            (64 at N = 8), static rank sharding, auto_commit lock-stepped by an
+            RCCL all-reduce over xGMI every step.
+
+A step = one batch of ``--batch-size`` records per rank consumed from the
+synthetic broker, packed in pinned memory, copied to the GPU, collated to
+bf16 by the HIP kernel, handed to the user, and its offsets committed (the
+commit of batch k happens when batch k+1 is requested, as in the reference's
+auto_commit).  Records are synthetic Kafka RecordBatch v2 records produced
+into the shared-memory broker before timing (a retained backlog).
+Weak scaling: per-rank work is fixed as N grows.
+
+Usage: python bench.py [--gpus N --steps K --warmup W]
+  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+BASELINE_METRIC = "Kafka records/sec to GPU with per-batch commit, at 1/2/4/8 MI355X"
+# reference measured on config 2's shape without a GPU (bs=256, 1 KiB f32[256], nw=4)
+BASELINE_VALUE = 337237.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--batch-size", type=int, default=256)
+    ap.add_argument("--dim", type=int, default=256, help="float32 elements per record")
+    ap.add_argument("--workers", type=int, default=4)
+    ap.add_argument("--partitions-per-gpu", type=int, default=8)
+    ap.add_argument("--slots-per-worker", type=int, default=4)
+    ap.add_argument("--prefetch", type=int, default=2)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "f16", "f32"])
+    ap.add_argument("--records-per-batch", type=int, default=64, help="Kafka RecordBatch size in the log")
+    ap.add_argument("--no-crc", action="store_true", help="skip CRC32C verification (kafka-python check_crcs)")
+    ap.add_argument("--device", default=None, help="override device (e.g. cpu for a dry run)")
+    ap.add_argument("--stats", action="store_true", help="print loader stats to stderr")
+    return ap.parse_args()
+
+
+def main() -> int:
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        print(f"[bench] warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
+    from torchkafka_amd.broker import SyntheticBroker
+    from torchkafka_amd.parallel import shard_partitions
+
+    dtype = {"bf16": torch.bfloat16, "fp8": torch.float8_e4m3fn, "f16": torch.float16, "f32": torch.float32}[args.dtype]
+    device = torch.device(args.device) if args.device else torch.device("cuda", local_rank)
+
+    class Records(KafkaDataset):
+        schema = FixedWidth(torch.float32, (args.dim,))
+
+    # --- broker: one per job (all ranks of a torchrun share the agent's pid and port)
+    tag = f"{os.getppid()}-{os.environ.get('MASTER_PORT', '0')}" if world > 1 else f"{os.getpid()}"
+    url = f"shm://tkbench-{tag}"
+    n_parts = args.partitions_per_gpu * world
+    B = args.batch_size
+    broker = SyntheticBroker.create(url, log_capacity=1 << 34, index_capacity=1 << 22)
+    broker.create_topic("bench", n_parts)
+    # backlog per owned partition: every batch the timed loop and the warm-up consume, plus what the
+    # workers prefetch into their ring slots, with headroom
+    mine = shard_partitions(n_parts, rank, world)
+    batches = args.warmup + args.steps + args.workers * (args.slots_per_worker + 2)
+    per_part = int(math.ceil(batches * B * 1.25 / max(1, len(mine)))) + B
+    t_fill = time.perf_counter()
+    broker.fill("bench", per_part, "fixed_f32", size=args.dim, partitions=mine,
+                records_per_batch=args.records_per_batch, threads=min(16, len(mine)))
+    t_fill = time.perf_counter() - t_fill
+
+    if world > 1:
+        # no CUDA touched yet: the loader forks its workers before HIP is initialised
+        dist.init_process_group("nccl" if device.type == "cuda" else "gloo")
+
+    loader = DeviceLoader(
+        Records.placeholder(), B, num_workers=args.workers, device=device, dtype=dtype,
+        slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
+        worker_init_fn=Records.init_worker("bench", bootstrap_servers=url, group_id="bench",
+                                           auto_offset_reset="earliest", check_crcs=not args.no_crc),
+    )
+    it = iter(auto_commit(loader))
+    x = next(it)  # forks workers, initialises HIP/RCCL
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier(device_ids=[local_rank] if device.type == "cuda" else None)
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+
+    for _ in range(max(0, args.warmup - 1)):
+        x = next(it)
+    sync()
+    loader.stats.reset()
+    t0 = time.perf_counter()
+    rows = 0
+    for _ in range(args.steps):
+        x = next(it)
+        rows += x.shape[0]
+    sync()
+    elapsed = time.perf_counter() - t0
+    stats = loader.stats.summary()
+
+    # whole-job aggregate: records of every rank over the slowest rank's time
+    if world > 1:
+        t = torch.tensor([elapsed, float(rows)], dtype=torch.float64,
+                         device=device if device.type == "cuda" else "cpu")
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed, total_rows = float(tmax[0]), float(t[1])
+    else:
+        total_rows = float(rows)
+    value = total_rows / elapsed
+
+    # check what landed on the device: the last batch's records must be this rank's partitions
+    xf = x.float()
+    parts = set(int(p) for p in xf[:, 1].tolist())
+    assert parts <= set(mine), f"rank {rank} received foreign partitions {parts - set(mine)}"
+
+    it.close()  # normal end of the auto_commit generator: final commit + worker shutdown
+    if world > 1:
+        dist.barrier(device_ids=[local_rank] if device.type == "cuda" else None)
+    committed = broker.committed_offsets("bench", "bench")
+    if rank == 0:
+        if args.stats:
+            print(json.dumps({"loader_stats": stats, "fill_s": t_fill, "committed_sample": dict(list(committed.items())[:4])}),
+                  file=sys.stderr)
+        out = {
+            "metric": BASELINE_METRIC,
+            "value": round(value, 1),
+            "unit": "records/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1000, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_VALUE, 3),
+            "dtype": args.dtype,
+            "data": "synthetic (Kafka RecordBatch v2 records in the shared-memory broker, random-free deterministic f32)",
+            "config": {
+                "model": f"KafkaDataset FixedWidth f32[{args.dim}] ({args.dim * 4} B records) -> {args.dtype} via gfx950 collate",
+                "global_batch": B * world,
+                "seq_len": args.dim,
+                "parallelism": f"dp{world}",
+                "partitions": n_parts,
+                "num_workers": args.workers,
+                "commit": "auto_commit per batch" + (", RCCL lockstep" if world > 1 else ""),
+                "bytes_per_step_per_gpu": B * args.dim * 4,
+                "gb_per_s": round(value * args.dim * 4 / 1e9, 3),
+                "commit_p99_us": round(stats["commit_p99_us"], 2),
+            },
+        }
+        print(json.dumps(out))
+    loader.close()
+    if world > 1:
+        dist.barrier(device_ids=[local_rank] if device.type == "cuda" else None)
+        dist.destroy_process_group()
+    if rank == 0:
+        broker.destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

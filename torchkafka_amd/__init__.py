@@ -1,0 +1,26 @@
+"""torchkafka_amd: Kafka -> PyTorch streaming for AMD Instinct MI355X (gfx950).
+
+Public API of Bendabir/torch-kafka (``KafkaDataset``, ``auto_commit``; reference
+src/__init__.py:17-18) plus the MI355X device path (``DeviceLoader``), the
+synthetic broker and a kafka-python compatible client.  ``import torchkafka``
+is an alias of this package.
+"""
+from .loader import DeviceLoader, KafkaBatch, auto_commit
+from .models import FixedWidth, JsonArray, KafkaDataset, VarLen
+
+__version__ = "1.2.0+mi355x.1"
+
+__all__ = ["KafkaDataset", "auto_commit", "DeviceLoader", "KafkaBatch", "FixedWidth", "VarLen", "JsonArray",
+           "SyntheticBroker", "KafkaConsumer", "KafkaProducer"]
+
+
+def __getattr__(name):
+    if name == "SyntheticBroker":
+        from .broker import SyntheticBroker
+
+        return SyntheticBroker
+    if name in ("KafkaConsumer", "KafkaProducer"):
+        from . import client
+
+        return getattr(client, name)
+    raise AttributeError(name)

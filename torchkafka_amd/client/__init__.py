@@ -1,0 +1,12 @@
+"""kafka-python compatible client over the synthetic broker."""
+from .consumer import KafkaConsumer
+from .errors import (
+    CommitFailedError, CorruptRecordException, KafkaConfigurationError, KafkaError, NoBrokersAvailable,
+    OffsetOutOfRangeError,
+)
+from .producer import KafkaProducer
+from .records import ConsumerRecord, OffsetAndMetadata, RecordMetadata, TopicPartition
+
+__all__ = ["KafkaConsumer", "KafkaProducer", "ConsumerRecord", "TopicPartition", "OffsetAndMetadata",
+           "RecordMetadata", "KafkaError", "CommitFailedError", "CorruptRecordException", "NoBrokersAvailable",
+           "OffsetOutOfRangeError", "KafkaConfigurationError"]

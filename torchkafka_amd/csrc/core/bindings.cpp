@@ -1,0 +1,492 @@
+// pybind11 bindings of the host native core: module `torchkafka_amd._tkcore`.
+// No HIP here (imported in forked workers); device work lives in `_tkhip`.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "broker.h"
+#include "consumer.h"
+#include "crc32c.h"
+#include "record_batch.h"
+#include "ring.h"
+
+namespace py = pybind11;
+using namespace tk;
+
+namespace {
+
+py::object bytes_or_none(const uint8_t* p, int32_t len) {
+  if (!p || len < 0) return py::none();
+  return py::bytes(reinterpret_cast<const char*>(p), size_t(len));
+}
+
+py::tuple record_tuple(const RecordView& r, int ts_type) {
+  py::list headers;
+  if (r.header_count > 0) {
+    for (const auto& h : parse_headers(r)) {
+      headers.append(py::make_tuple(py::str(reinterpret_cast<const char*>(h.key), size_t(h.key_len)),
+                                    bytes_or_none(h.value, h.value_len)));
+    }
+  }
+  return py::make_tuple(r.offset, r.timestamp, ts_type, bytes_or_none(r.key, r.key_len),
+                        bytes_or_none(r.value, r.value_len), headers, py::none(), r.key_len, r.value_len,
+                        r.header_bytes);
+}
+
+struct PyFetcher {
+  Fetcher f;
+  size_t rr = 0;
+  PyFetcher(std::shared_ptr<Broker> b, bool crc) : f(std::move(b), crc) {}
+};
+
+struct PyRing {
+  std::unique_ptr<Ring> r;
+  std::vector<uint32_t> cursor;
+  std::vector<uint8_t> done;
+  uint32_t rr = 0;
+  explicit PyRing(std::unique_ptr<Ring> ring) : r(std::move(ring)) {
+    cursor.assign(r->n_workers(), 0);
+    done.assign(r->n_workers(), 0);
+  }
+};
+
+std::vector<RecordIn> to_records(const std::vector<py::object>& values, const std::vector<py::object>& keys,
+                                 const std::vector<int64_t>& timestamps, const std::vector<py::object>& headers,
+                                 std::vector<std::string>& keep, std::vector<std::vector<HeaderView>>& hkeep) {
+  const size_t n = values.size();
+  if (keys.size() != n || timestamps.size() != n || headers.size() != n)
+    throw std::invalid_argument("values/keys/timestamps/headers length mismatch");
+  keep.reserve(n * 2 + 16);
+  hkeep.resize(n);
+  std::vector<RecordIn> recs(n);
+  auto hold = [&](const py::object& o, const uint8_t** p, int32_t* len) {
+    if (o.is_none()) { *p = nullptr; *len = -1; return; }
+    keep.emplace_back(o.cast<std::string>());
+    *p = reinterpret_cast<const uint8_t*>(keep.back().data());
+    *len = int32_t(keep.back().size());
+  };
+  for (size_t i = 0; i < n; ++i) {
+    RecordIn& r = recs[i];
+    r.timestamp = timestamps[i];
+    hold(keys[i], &r.key, &r.key_len);
+    hold(values[i], &r.value, &r.value_len);
+    r.headers = nullptr;
+    r.header_count = 0;
+    if (!headers[i].is_none()) {
+      for (auto item : headers[i].cast<py::list>()) {
+        auto t = item.cast<py::tuple>();
+        HeaderView h;
+        keep.emplace_back(t[0].cast<std::string>());
+        h.key = reinterpret_cast<const uint8_t*>(keep.back().data());
+        h.key_len = int32_t(keep.back().size());
+        hold(py::reinterpret_borrow<py::object>(t[1]), &h.value, &h.value_len);
+        hkeep[i].push_back(h);
+      }
+      r.headers = hkeep[i].data();
+      r.header_count = int32_t(hkeep[i].size());
+    }
+  }
+  return recs;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_tkcore, m) {
+  m.doc() = "torchkafka_amd host native core: RecordBatch codec, shm broker, fetcher, packers, slot ring";
+
+  static py::exception<KafkaError> kafka_error(m, "KafkaError", PyExc_RuntimeError);
+  static py::exception<CommitFailed> commit_failed(m, "CommitFailedError", kafka_error.ptr());
+  static py::exception<CorruptRecord> corrupt(m, "CorruptRecordException", kafka_error.ptr());
+  static py::exception<OffsetOutOfRange> oor(m, "OffsetOutOfRangeError", kafka_error.ptr());
+  static py::exception<InjectedFetchError> fetch_err(m, "InjectedFetchError", kafka_error.ptr());
+  py::register_exception_translator([](std::exception_ptr p) {
+    try {
+      if (p) std::rethrow_exception(p);
+    } catch (const CommitFailed& e) {
+      py::set_error(commit_failed, e.what());
+    } catch (const CorruptRecord& e) {
+      py::set_error(corrupt, e.what());
+    } catch (const OffsetOutOfRange& e) {
+      py::set_error(oor, e.what());
+    } catch (const InjectedFetchError& e) {
+      py::set_error(fetch_err, e.what());
+    } catch (const KafkaError& e) {
+      py::set_error(kafka_error, e.what());
+    }
+  });
+
+  // ---- codec
+  m.def("crc32c", [](py::bytes b) {
+    std::string s = b;
+    return crc32c(s.data(), s.size());
+  });
+  m.def("crc32c_hw", &crc32c_hw);
+  m.def(
+      "encode_batch",
+      [](int64_t base_offset, std::vector<py::object> values, std::vector<py::object> keys,
+         std::vector<int64_t> timestamps, std::vector<py::object> headers) {
+        std::vector<std::string> keep;
+        std::vector<std::vector<HeaderView>> hkeep;
+        auto recs = to_records(values, keys, timestamps, headers, keep, hkeep);
+        int64_t min_ts = timestamps.empty() ? 0 : *std::min_element(timestamps.begin(), timestamps.end());
+        std::string out(batch_encoded_size(recs.data(), recs.size(), min_ts), '\0');
+        size_t n = encode_batch(reinterpret_cast<uint8_t*>(&out[0]), base_offset, recs.data(), recs.size());
+        out.resize(n);
+        return py::bytes(out);
+      },
+      py::arg("base_offset"), py::arg("values"), py::arg("keys"), py::arg("timestamps"), py::arg("headers"));
+  m.def(
+      "decode_batches",
+      [](py::bytes data, bool check_crcs) {
+        std::string s = data;
+        const uint8_t* p = reinterpret_cast<const uint8_t*>(s.data());
+        size_t left = s.size();
+        py::list out;
+        while (left >= kBatchHeaderBytes) {
+          BatchHeader h = parse_batch_header(p, left);
+          if (check_crcs && !verify_batch_crc(p, h)) throw CorruptRecord("batch failed CRC check");
+          RecordIter it(p, h);
+          RecordView r;
+          while (it.next(&r)) out.append(record_tuple(r, h.timestamp_type()));
+          p += h.total_size();
+          left -= h.total_size();
+        }
+        return out;
+      },
+      py::arg("data"), py::arg("check_crcs") = true);
+  m.def("parse_json_f32", [](py::bytes b) {
+    std::string s = b;
+    std::vector<float> v(s.size() / 2 + 2);
+    int64_t n = parse_json_f32(s.data(), s.size(), v.data(), int64_t(v.size()));
+    if (n < 0) throw std::invalid_argument("not a flat numeric JSON array");
+    v.resize(size_t(n));
+    return v;
+  });
+  m.def("json_array_len", [](py::bytes b) {
+    std::string s = b;
+    return json_array_len(s.data(), s.size());
+  });
+
+  // ---- broker
+  py::class_<Broker, std::shared_ptr<Broker>>(m, "Broker")
+      .def(py::init([](const std::string& url, bool create, uint32_t max_topics, uint32_t max_partitions,
+                       uint32_t max_groups, uint64_t log_capacity, uint64_t index_capacity, uint32_t rebalance_delay_ms) {
+             BrokerConfig c;
+             c.max_topics = max_topics;
+             c.max_partitions = max_partitions;
+             c.max_groups = max_groups;
+             c.default_log_capacity = log_capacity;
+             c.default_index_capacity = index_capacity;
+             c.group_initial_rebalance_delay_ms = rebalance_delay_ms;
+             return std::make_shared<Broker>(url, create, c);
+           }),
+           py::arg("url"), py::arg("create") = false, py::arg("max_topics") = 256, py::arg("max_partitions") = 4096,
+           py::arg("max_groups") = 64, py::arg("log_capacity") = uint64_t(256) << 20,
+           py::arg("index_capacity") = uint64_t(1) << 20, py::arg("group_initial_rebalance_delay_ms") = 100)
+      .def_static("url_to_dir", &Broker::url_to_dir)
+      .def_property_readonly("dir", &Broker::dir)
+      .def_property_readonly("group_initial_rebalance_delay_ms",
+                             [](Broker& b) { return b.meta().group_initial_rebalance_delay_ms; })
+      .def("create_topic",
+           [](Broker& b, const std::string& name, uint32_t n, uint64_t cap, uint64_t icap) {
+             TopicInfo t = b.create_topic(name, n, cap, icap);
+             return py::make_tuple(t.index, t.n_partitions, t.first_pidx);
+           },
+           py::arg("name"), py::arg("num_partitions"), py::arg("log_capacity") = 0, py::arg("index_capacity") = 0)
+      .def("find_topic",
+           [](Broker& b, const std::string& name) -> py::object {
+             TopicInfo t;
+             if (!b.find_topic(name, &t)) return py::none();
+             return py::make_tuple(t.index, t.n_partitions, t.first_pidx);
+           })
+      .def("topics",
+           [](Broker& b) {
+             py::list l;
+             for (auto& t : b.topics()) l.append(py::make_tuple(t.name, t.index, t.n_partitions, t.first_pidx));
+             return l;
+           })
+      .def("partition_of",
+           [](Broker& b, uint32_t pidx) {
+             auto& P = b.part(pidx);
+             return py::make_tuple(P.topic_index, P.partition);
+           })
+      .def("high_watermark", [](Broker& b, uint32_t p) { return b.part(p).high_watermark.load(); })
+      .def("log_start_offset", [](Broker& b, uint32_t p) { return b.part(p).log_start_offset.load(); })
+      .def("log_bytes", [](Broker& b, uint32_t p) { return b.part(p).log_end_pos.load(); })
+      .def("partition_stats",
+           [](Broker& b, uint32_t p) {
+             auto& P = b.part(p);
+             py::dict d;
+             d["fetch_calls"] = P.fetch_calls.load();
+             d["bytes_fetched"] = P.bytes_fetched.load();
+             d["records_produced"] = P.records_produced.load();
+             d["batches"] = P.n_batches.load();
+             d["log_bytes"] = P.log_end_pos.load();
+             return d;
+           })
+      .def(
+          "append",
+          [](Broker& b, uint32_t pidx, std::vector<py::object> values, std::vector<py::object> keys,
+             std::vector<int64_t> timestamps, std::vector<py::object> headers) {
+            std::vector<std::string> keep;
+            std::vector<std::vector<HeaderView>> hkeep;
+            auto recs = to_records(values, keys, timestamps, headers, keep, hkeep);
+            py::gil_scoped_release nogil;
+            return b.append(pidx, recs.data(), recs.size());
+          },
+          py::arg("pidx"), py::arg("values"), py::arg("keys"), py::arg("timestamps"), py::arg("headers"))
+      .def(
+          "fill_synthetic",
+          [](Broker& b, std::vector<uint32_t> pidxs, int64_t n, int kind, int64_t a, int64_t bb, uint32_t rpb,
+             uint64_t seed, int threads) {
+            py::gil_scoped_release nogil;
+            b.fill_synthetic(pidxs, n, kind, a, bb, rpb, seed, threads);
+          },
+          py::arg("pidxs"), py::arg("n_records"), py::arg("kind"), py::arg("size_a"), py::arg("size_b") = 0,
+          py::arg("records_per_batch") = 64, py::arg("seed") = 0, py::arg("threads") = 1)
+      .def("delete_records", &Broker::delete_records)
+      .def("group_index", &Broker::group_index, py::arg("group"), py::arg("create") = true)
+      .def("group_name", &Broker::group_name)
+      .def("join_group", &Broker::join_group)
+      .def("leave_group", &Broker::leave_group)
+      .def("member_id", &Broker::member_id)
+      .def("poll_group",
+           [](Broker& b, uint32_t g, int slot, uint64_t mid) {
+             GroupView v = b.poll_group(g, slot, mid);
+             return py::make_tuple(v.generation, v.state, v.member_active, v.assignment);
+           })
+      .def("commit",
+           [](Broker& b, uint32_t g, int slot, uint64_t mid, uint32_t gen,
+              std::vector<std::tuple<uint32_t, int64_t, std::string>> entries) {
+             std::vector<CommitEntry> es;
+             es.reserve(entries.size());
+             for (auto& e : entries) es.push_back(CommitEntry{std::get<0>(e), std::get<1>(e), std::get<2>(e)});
+             b.commit(g, slot, mid, gen, es);
+           })
+      .def("committed",
+           [](Broker& b, uint32_t g, uint32_t pidx) {
+             std::string meta;
+             int64_t off = b.committed(g, pidx, &meta);
+             return py::make_tuple(off, py::str(meta));
+           })
+      .def("commit_count", &Broker::commit_count)
+      .def("inject_commit_failures", &Broker::inject_commit_failures)
+      .def("reset_group_offsets", &Broker::reset_group_offsets)
+      .def("set_fetch_delay", &Broker::set_fetch_delay)
+      .def("inject_fetch_errors", &Broker::inject_fetch_errors);
+
+  // ---- fetcher
+  py::class_<PyFetcher>(m, "Fetcher")
+      .def(py::init<std::shared_ptr<Broker>, bool>(), py::arg("broker"), py::arg("check_crcs") = true)
+      .def("assign", [](PyFetcher& f, std::vector<uint32_t> p, std::vector<int64_t> pos) { f.f.assign(p, pos); })
+      .def("assigned", [](PyFetcher& f) {
+        py::list l;
+        for (auto& p : f.f.parts()) l.append(p.pidx);
+        return l;
+      })
+      .def("positions",
+           [](PyFetcher& f) {
+             py::dict d;
+             for (auto& p : f.f.parts()) d[py::int_(p.pidx)] = p.position;
+             return d;
+           })
+      .def("position", [](PyFetcher& f, uint32_t pidx) -> py::object {
+        size_t i = f.f.find(pidx);
+        if (i == size_t(-1)) return py::none();
+        return py::int_(f.f.parts()[i].position);
+      })
+      .def("seek", [](PyFetcher& f, uint32_t pidx, int64_t off) {
+        size_t i = f.f.find(pidx);
+        if (i == size_t(-1)) throw std::invalid_argument("partition is not assigned");
+        auto& fp = f.f.parts()[i];
+        fp.position = off;
+        fp.batch_hint = -1;
+      })
+      .def("pause", [](PyFetcher& f, uint32_t pidx, bool paused) {
+        size_t i = f.f.find(pidx);
+        if (i == size_t(-1)) throw std::invalid_argument("partition is not assigned");
+        f.f.parts()[i].paused = paused;
+      })
+      .def("has_data", [](PyFetcher& f) {
+        for (auto& p : f.f.parts())
+          if (!p.paused && f.f.has_data(p)) return true;
+        return false;
+      })
+      .def(
+          "poll_records",
+          [](PyFetcher& f, int64_t max_records) {
+            // Non-blocking: one round-robin pass, returns [(pidx, [record tuples])].
+            py::list out;
+            auto& parts = f.f.parts();
+            int64_t left = max_records;
+            for (size_t k = 0; k < parts.size() && left > 0; ++k) {
+              FetchPart& fp = parts[(f.rr + k) % parts.size()];
+              if (fp.paused) continue;
+              py::list recs;
+              Broker& b = f.f.broker();
+              (void)b;
+              f.f.scan(fp, size_t(left), [&](const RecordView& r) {
+                recs.append(record_tuple(r, 0));
+                return kTake;
+              });
+              if (py::len(recs)) {
+                left -= int64_t(py::len(recs));
+                out.append(py::make_tuple(fp.pidx, recs));
+              }
+            }
+            if (!parts.empty()) f.rr = (f.rr + 1) % parts.size();
+            return out;
+          },
+          py::arg("max_records"))
+      .def(
+          "fill_slot",
+          [](PyFetcher& f, py::object ring_obj, uint32_t gslot, int kind, int elem_size, int64_t row_elems,
+             int64_t min_len, int64_t max_len, bool truncate, bool skip_bad, int64_t batch_rows, int64_t timeout_ms) {
+            PyRing& ring = ring_obj.cast<PyRing&>();
+            PackSpec s;
+            s.kind = kind;
+            s.elem_size = elem_size;
+            s.row_elems = row_elems;
+            s.min_len = min_len;
+            s.max_len = max_len;
+            s.truncate = truncate;
+            s.skip_bad = skip_bad;
+            FillOutcome o;
+            {
+              py::gil_scoped_release nogil;
+              o = fill_slot(f.f, *ring.r, gslot, s, batch_rows, timeout_ms, &f.rr);
+            }
+            return py::make_tuple(o.rows, o.scanned, o.timed_out, o.shutdown);
+          },
+          py::arg("ring"), py::arg("gslot"), py::arg("kind"), py::arg("elem_size"), py::arg("row_elems"),
+          py::arg("min_len"), py::arg("max_len"), py::arg("truncate"), py::arg("skip_bad"), py::arg("batch_rows"),
+          py::arg("timeout_ms"));
+
+  // ---- ring
+  py::class_<PyRing>(m, "Ring")
+      .def_static("create",
+                  [](const std::string& name, uint32_t nw, uint32_t spw, uint64_t cap) {
+                    return new PyRing(Ring::create(name, nw, spw, cap));
+                  })
+      .def_static("open", [](const std::string& name) { return new PyRing(Ring::open(name)); })
+      .def_property_readonly("name", [](PyRing& r) { return r.r->name(); })
+      .def_property_readonly("base_address", [](PyRing& r) { return reinterpret_cast<uintptr_t>(r.r->base()); })
+      .def_property_readonly("total_bytes", [](PyRing& r) { return r.r->total_bytes(); })
+      .def_property_readonly("n_workers", [](PyRing& r) { return r.r->n_workers(); })
+      .def_property_readonly("slots_per_worker", [](PyRing& r) { return r.r->slots_per_worker(); })
+      .def_property_readonly("n_slots", [](PyRing& r) { return r.r->n_slots(); })
+      .def_property_readonly("payload_capacity", [](PyRing& r) { return r.r->payload_capacity(); })
+      .def("gslot", [](PyRing& r, uint32_t w, uint32_t i) { return r.r->gslot(w, i); })
+      .def("payload_address", [](PyRing& r, uint32_t g) { return reinterpret_cast<uintptr_t>(r.r->payload(g)); })
+      .def("payload_view",
+           [](PyRing& r, uint32_t g) {
+             return py::memoryview::from_memory(r.r->payload(g), ssize_t(r.r->payload_capacity()), false);
+           })
+      .def("slot_summary",
+           [](PyRing& r, uint32_t g) {
+             SlotHeader* h = r.r->slot(g);
+             return py::make_tuple(h->n_rows, h->flags, h->payload_bytes, h->values_offset, h->max_row_len,
+                                   h->total_elems, h->worker, h->kind, h->src_dtype);
+           })
+      .def("slot_info",
+           [](PyRing& r, uint32_t g) {
+             SlotHeader* h = r.r->slot(g);
+             py::dict d;
+             d["state"] = h->state.load();
+             d["worker"] = h->worker;
+             d["seq"] = h->seq;
+             d["n_rows"] = h->n_rows;
+             d["flags"] = h->flags;
+             d["kind"] = h->kind;
+             d["payload_bytes"] = h->payload_bytes;
+             d["values_offset"] = h->values_offset;
+             d["values_bytes"] = h->values_bytes;
+             d["max_row_len"] = h->max_row_len;
+             d["total_elems"] = h->total_elems;
+             d["n_scanned"] = h->n_scanned;
+             d["row_bytes"] = h->row_bytes;
+             d["t_fill_start_ns"] = h->t_fill_start_ns;
+             d["t_ready_ns"] = h->t_ready_ns;
+             d["error"] = std::string(h->err, h->err_len);
+             return d;
+           })
+      .def("watermarks",
+           [](PyRing& r, uint32_t g) {
+             SlotHeader* h = r.r->slot(g);
+             py::list l;
+             for (uint32_t i = 0; i < h->n_parts; ++i)
+               l.append(py::make_tuple(h->wm[i].pidx, h->wm[i].first_offset, h->wm[i].next_offset, h->wm[i].count));
+             return l;
+           })
+      .def("set_slot",
+           [](PyRing& r, uint32_t g, uint32_t n_rows, uint32_t flags, uint32_t kind, uint64_t payload_bytes,
+              uint64_t values_offset, int64_t max_row_len, int64_t total_elems, int64_t n_scanned,
+              std::vector<std::tuple<uint32_t, int64_t, int64_t, uint32_t>> wms) {
+             SlotHeader* h = r.r->slot(g);
+             if (wms.size() > size_t(kMaxSlotParts)) throw std::invalid_argument("too many watermarks");
+             if (payload_bytes > r.r->payload_capacity()) throw std::invalid_argument("payload exceeds slot");
+             h->n_rows = n_rows;
+             h->flags = flags;
+             h->err_len = 0;
+             h->kind = kind;
+             h->payload_bytes = payload_bytes;
+             h->values_offset = values_offset;
+             h->values_bytes = payload_bytes - values_offset;
+             h->max_row_len = max_row_len;
+             h->total_elems = total_elems;
+             h->n_scanned = n_scanned;
+             h->n_parts = uint32_t(wms.size());
+             for (size_t i = 0; i < wms.size(); ++i)
+               h->wm[i] = Watermark{std::get<0>(wms[i]), std::get<3>(wms[i]), std::get<1>(wms[i]), std::get<2>(wms[i])};
+           })
+      .def("set_slot_sample",
+           [](PyRing& r, uint32_t g, int32_t dtype, std::vector<int64_t> shape) {
+             SlotHeader* h = r.r->slot(g);
+             if (shape.size() > 8) throw std::invalid_argument("sample rank > 8");
+             h->src_dtype = dtype;
+             h->ndim = int32_t(shape.size());
+             for (size_t i = 0; i < shape.size(); ++i) h->shape[i] = shape[i];
+           })
+      .def("slot_sample",
+           [](PyRing& r, uint32_t g) {
+             SlotHeader* h = r.r->slot(g);
+             std::vector<int64_t> shape(h->shape, h->shape + h->ndim);
+             return py::make_tuple(h->src_dtype, shape);
+           })
+      .def("set_flags", [](PyRing& r, uint32_t g, uint32_t flags) { r.r->slot(g)->flags |= flags; })
+      .def("set_error",
+           [](PyRing& r, uint32_t g, const std::string& msg) {
+             SlotHeader* h = r.r->slot(g);
+             const size_t n = std::min(msg.size(), sizeof(h->err));
+             std::memcpy(h->err, msg.data(), n);
+             h->err_len = uint32_t(n);
+             h->flags |= kSlotError;
+           })
+      .def("set_worker_pid", [](PyRing& r, uint32_t w, int64_t pid) { r.r->header()->worker_pid[w].store(pid); })
+      .def("worker_pid", [](PyRing& r, uint32_t w) { return r.r->header()->worker_pid[w].load(); })
+      .def("worker_acquire",
+           [](PyRing& r, uint32_t w, uint32_t i, int64_t timeout_ms) {
+             py::gil_scoped_release nogil;
+             return r.r->worker_acquire(w, i, timeout_ms);
+           })
+      .def("worker_publish", [](PyRing& r, uint32_t g) { r.r->worker_publish(g); })
+      .def(
+          "main_acquire",
+          [](PyRing& r, int64_t timeout_ms, bool in_order) {
+            py::gil_scoped_release nogil;
+            return r.r->main_acquire(r.cursor.data(), &r.rr, r.done.data(), in_order, timeout_ms);
+          },
+          py::arg("timeout_ms"), py::arg("in_order") = false)
+      .def("mark_done", [](PyRing& r, uint32_t w) { r.done.at(w) = 1; })
+      .def("is_done", [](PyRing& r, uint32_t w) { return bool(r.done.at(w)); })
+      .def("main_release", [](PyRing& r, uint32_t g) { r.r->main_release(g); })
+      .def("shutdown", [](PyRing& r) { r.r->shutdown(); })
+      .def("is_shutdown", [](PyRing& r) { return bool(r.r->header()->shutdown.load()); })
+      .def("unlink", [](PyRing& r) { r.r->unlink(); });
+
+  m.attr("SLOT_EOS") = int(kSlotEOS);
+  m.attr("SLOT_ERROR") = int(kSlotError);
+  m.attr("PACK_FIXED") = int(kPackFixed);
+  m.attr("PACK_VARLEN") = int(kPackVarlen);
+  m.attr("PACK_JSON_F32") = int(kPackJsonF32);
+  m.attr("SLOT_HEADER_BYTES") = kSlotHeaderBytes;
+}

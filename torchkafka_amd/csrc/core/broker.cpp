@@ -1,0 +1,697 @@
+#include "broker.h"
+
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/file.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cmath>
+#include <thread>
+
+namespace tk {
+
+// ------------------------------------------------------------ robust mutex
+void init_robust_mutex(pthread_mutex_t* m) {
+  pthread_mutexattr_t a;
+  pthread_mutexattr_init(&a);
+  pthread_mutexattr_setpshared(&a, PTHREAD_PROCESS_SHARED);
+  pthread_mutexattr_setrobust(&a, PTHREAD_MUTEX_ROBUST);
+  pthread_mutex_init(m, &a);
+  pthread_mutexattr_destroy(&a);
+}
+
+RobustLock::RobustLock(pthread_mutex_t* m) : m_(m) {
+  int rc = pthread_mutex_lock(m_);
+  if (rc == EOWNERDEAD) {
+    // The previous owner died inside the critical section.  Every critical
+    // section below publishes with a final atomic store, so the protected
+    // state is consistent up to the last publish; adopt the lock.
+    pthread_mutex_consistent(m_);
+  } else if (rc != 0) {
+    errno = rc;
+    throw_errno("pthread_mutex_lock");
+  }
+}
+RobustLock::~RobustLock() { pthread_mutex_unlock(m_); }
+
+// ------------------------------------------------------------ helpers
+namespace {
+
+void mkdir_p(const std::string& path) {
+  std::string cur;
+  for (size_t i = 0; i < path.size(); ++i) {
+    cur.push_back(path[i]);
+    if ((path[i] == '/' && i > 0) || i + 1 == path.size()) {
+      if (mkdir(cur.c_str(), 0777) != 0 && errno != EEXIST) throw_errno("mkdir " + cur);
+    }
+  }
+}
+
+struct Layout {
+  size_t topics, parts, groups, owners, offsets, total;
+};
+
+Layout layout_for(uint32_t max_topics, uint32_t max_parts, uint32_t max_groups) {
+  Layout L;
+  size_t off = align_up(sizeof(MetaHeader), 4096);
+  L.topics = off;
+  off = align_up(off + sizeof(TopicEntry) * max_topics, 4096);
+  L.parts = off;
+  off = align_up(off + sizeof(PartitionEntry) * max_parts, 4096);
+  L.groups = off;
+  off = align_up(off + sizeof(GroupEntry) * max_groups, 4096);
+  L.owners = off;
+  off = align_up(off + sizeof(int16_t) * size_t(max_groups) * max_parts, 4096);
+  L.offsets = off;
+  off = align_up(off + sizeof(OffsetEntry) * size_t(max_groups) * max_parts, 4096);
+  L.total = off;
+  return L;
+}
+
+void* map_file(const std::string& path, size_t len, bool create_size) {
+  int fd = open(path.c_str(), O_RDWR | O_CREAT, 0666);
+  if (fd < 0) throw_errno("open " + path);
+  if (create_size) {
+    struct stat st;
+    if (fstat(fd, &st) != 0) { close(fd); throw_errno("fstat " + path); }
+    if (size_t(st.st_size) < len && ftruncate(fd, off_t(len)) != 0) {
+      close(fd);
+      throw_errno("ftruncate " + path);
+    }
+  }
+  void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) throw_errno("mmap " + path);
+  return p;
+}
+
+std::string part_path(const std::string& dir, uint32_t pidx, const char* ext) {
+  char buf[32];
+  snprintf(buf, sizeof(buf), "/p%05u.%s", pidx, ext);
+  return dir + buf;
+}
+
+bool pid_alive(int32_t pid) {
+  if (pid <= 0) return false;
+  if (kill(pid, 0) == 0) return true;
+  return errno == EPERM;
+}
+
+inline uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------ construction
+std::string Broker::url_to_dir(const std::string& url) {
+  const std::string shm = "shm://", file = "file://";
+  if (url.rfind(shm, 0) == 0) {
+    std::string name = url.substr(shm.size());
+    if (name.empty() || name.find('/') != std::string::npos || name == "." || name == "..")
+      throw std::invalid_argument("bad shm broker name in '" + url + "'");
+    return "/dev/shm/torchkafka/" + name;
+  }
+  if (url.rfind(file, 0) == 0) return url.substr(file.size());
+  return url;
+}
+
+Broker::Broker(const std::string& url, bool create, const BrokerConfig& cfg) : dir_(url_to_dir(url)) {
+  if (create) mkdir_p(dir_);
+  struct stat st;
+  if (stat(dir_.c_str(), &st) != 0) throw KafkaError("NoBrokersAvailable: no broker at '" + url + "'");
+  map_meta(create, cfg);
+  maps_.resize(meta_->max_partitions);
+}
+
+Broker::~Broker() {
+  for (auto& m : maps_) {
+    if (m.log) munmap(m.log, m.log_len);
+    if (m.idx) munmap(m.idx, m.idx_len);
+  }
+  if (meta_map_) munmap(meta_map_, meta_len_);
+}
+
+void Broker::map_meta(bool create, const BrokerConfig& cfg) {
+  const std::string lock_path = dir_ + "/lock", meta_path = dir_ + "/meta";
+  int lfd = open(lock_path.c_str(), O_RDWR | (create ? O_CREAT : 0), 0666);
+  if (lfd < 0) throw KafkaError("NoBrokersAvailable: cannot open broker at '" + dir_ + "'");
+  if (flock(lfd, LOCK_EX) != 0) { close(lfd); throw_errno("flock"); }
+  struct Unlock {
+    int fd;
+    ~Unlock() { flock(fd, LOCK_UN); close(fd); }
+  } unlock{lfd};
+
+  int fd = open(meta_path.c_str(), O_RDWR | (create ? O_CREAT : 0), 0666);
+  if (fd < 0) throw KafkaError("NoBrokersAvailable: broker meta missing in '" + dir_ + "'");
+  struct stat st;
+  fstat(fd, &st);
+  if (st.st_size == 0) {
+    if (!create) { close(fd); throw KafkaError("NoBrokersAvailable: broker not initialised"); }
+    Layout L = layout_for(cfg.max_topics, cfg.max_partitions, cfg.max_groups);
+    if (ftruncate(fd, off_t(L.total)) != 0) { close(fd); throw_errno("ftruncate meta"); }
+    void* p = mmap(nullptr, L.total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) throw_errno("mmap meta");
+    meta_map_ = static_cast<uint8_t*>(p);
+    meta_len_ = L.total;
+    meta_ = reinterpret_cast<MetaHeader*>(meta_map_);
+    meta_->magic = kBrokerMagic;
+    meta_->version = kBrokerVersion;
+    meta_->max_topics = cfg.max_topics;
+    meta_->max_partitions = cfg.max_partitions;
+    meta_->max_groups = cfg.max_groups;
+    meta_->group_initial_rebalance_delay_ms = cfg.group_initial_rebalance_delay_ms;
+    meta_->default_log_capacity = cfg.default_log_capacity;
+    meta_->default_index_capacity = cfg.default_index_capacity;
+    init_robust_mutex(&meta_->lock);
+    auto* parts = reinterpret_cast<PartitionEntry*>(meta_map_ + L.parts);
+    for (uint32_t i = 0; i < cfg.max_partitions; ++i) init_robust_mutex(&parts[i].lock);
+    auto* offs = reinterpret_cast<OffsetEntry*>(meta_map_ + L.offsets);
+    for (size_t i = 0; i < size_t(cfg.max_groups) * cfg.max_partitions; ++i) offs[i].offset.store(-1);
+    auto* own = reinterpret_cast<int16_t*>(meta_map_ + L.owners);
+    std::fill(own, own + size_t(cfg.max_groups) * cfg.max_partitions, int16_t(-1));
+    meta_->ready.store(1, std::memory_order_release);
+  } else {
+    MetaHeader hdr;
+    if (pread(fd, &hdr, sizeof(uint64_t) + 8 + 16, 0) < 0) { close(fd); throw_errno("read meta"); }
+    if (hdr.magic != kBrokerMagic || hdr.version != kBrokerVersion) {
+      close(fd);
+      throw KafkaError("broker directory '" + dir_ + "' has an incompatible format");
+    }
+    Layout L = layout_for(hdr.max_topics, hdr.max_partitions, hdr.max_groups);
+    void* p = mmap(nullptr, L.total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) throw_errno("mmap meta");
+    meta_map_ = static_cast<uint8_t*>(p);
+    meta_len_ = L.total;
+    meta_ = reinterpret_cast<MetaHeader*>(meta_map_);
+  }
+  Layout L = layout_for(meta_->max_topics, meta_->max_partitions, meta_->max_groups);
+  topics_ = reinterpret_cast<TopicEntry*>(meta_map_ + L.topics);
+  parts_ = reinterpret_cast<PartitionEntry*>(meta_map_ + L.parts);
+  groups_ = reinterpret_cast<GroupEntry*>(meta_map_ + L.groups);
+  owners_ = reinterpret_cast<int16_t*>(meta_map_ + L.owners);
+  offsets_ = reinterpret_cast<OffsetEntry*>(meta_map_ + L.offsets);
+}
+
+// ------------------------------------------------------------ topics
+TopicInfo Broker::create_topic(const std::string& name, uint32_t n_partitions, uint64_t log_capacity,
+                               uint64_t index_capacity) {
+  if (name.empty() || name.size() >= kNameLen) throw std::invalid_argument("bad topic name");
+  if (n_partitions == 0) throw std::invalid_argument("a topic needs at least one partition");
+  TopicInfo info;
+  {
+    RobustLock l(&meta_->lock);
+    if (find_topic(name, &info)) return info;
+    const uint32_t ti = meta_->n_topics.load();
+    const uint32_t first = meta_->n_partitions.load();
+    if (ti >= meta_->max_topics) throw KafkaError("broker topic table full");
+    if (first + n_partitions > meta_->max_partitions) throw KafkaError("broker partition table full");
+    if (!log_capacity) log_capacity = meta_->default_log_capacity;
+    if (!index_capacity) index_capacity = meta_->default_index_capacity;
+    for (uint32_t i = 0; i < n_partitions; ++i) {
+      const uint32_t pidx = first + i;
+      PartitionEntry& P = parts_[pidx];
+      P.high_watermark.store(0);
+      P.log_start_offset.store(0);
+      P.log_end_pos.store(0);
+      P.n_batches.store(0);
+      P.log_capacity = log_capacity;
+      P.index_capacity = index_capacity;
+      P.topic_index = ti;
+      P.partition = i;
+      P.fetch_delay_ns.store(0);
+      P.fetch_errors.store(0);
+      // Create (sparse) backing files now so readers can map them.
+      void* a = map_file(part_path(dir_, pidx, "log"), log_capacity, true);
+      munmap(a, log_capacity);
+      void* b = map_file(part_path(dir_, pidx, "idx"), index_capacity * sizeof(IndexEntry), true);
+      munmap(b, index_capacity * sizeof(IndexEntry));
+    }
+    TopicEntry& T = topics_[ti];
+    std::memset(T.name, 0, kNameLen);
+    std::memcpy(T.name, name.data(), name.size());
+    T.n_partitions = n_partitions;
+    T.first_pidx = first;
+    T.log_capacity = log_capacity;
+    T.index_capacity = index_capacity;
+    meta_->n_partitions.store(first + n_partitions, std::memory_order_release);
+    meta_->n_topics.store(ti + 1, std::memory_order_release);
+    info.index = ti;
+    info.n_partitions = n_partitions;
+    info.first_pidx = first;
+    info.name = name;
+  }
+  return info;
+}
+
+bool Broker::find_topic(const std::string& name, TopicInfo* out) const {
+  const uint32_t n = meta_->n_topics.load(std::memory_order_acquire);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (name == topics_[i].name) {
+      out->index = i;
+      out->n_partitions = topics_[i].n_partitions;
+      out->first_pidx = topics_[i].first_pidx;
+      out->name = name;
+      return true;
+    }
+  }
+  return false;
+}
+
+std::vector<TopicInfo> Broker::topics() const {
+  std::vector<TopicInfo> v;
+  const uint32_t n = meta_->n_topics.load(std::memory_order_acquire);
+  for (uint32_t i = 0; i < n; ++i)
+    v.push_back(TopicInfo{i, topics_[i].n_partitions, topics_[i].first_pidx, topics_[i].name});
+  return v;
+}
+
+PartitionEntry& Broker::part(uint32_t pidx) {
+  if (pidx >= meta_->n_partitions.load(std::memory_order_acquire)) throw std::out_of_range("bad partition index");
+  return parts_[pidx];
+}
+const PartitionEntry& Broker::part(uint32_t pidx) const {
+  if (pidx >= meta_->n_partitions.load(std::memory_order_acquire)) throw std::out_of_range("bad partition index");
+  return parts_[pidx];
+}
+
+Broker::Mapped& Broker::mapped(uint32_t pidx) {
+  Mapped& m = maps_.at(pidx);
+  if (__atomic_load_n(&m.idx, __ATOMIC_ACQUIRE)) return m;
+  std::lock_guard<std::mutex> g(maps_mu_);
+  if (!m.idx) {
+    const PartitionEntry& P = part(pidx);
+    m.log_len = P.log_capacity;
+    m.idx_len = P.index_capacity * sizeof(IndexEntry);
+    m.log = static_cast<uint8_t*>(map_file(part_path(dir_, pidx, "log"), m.log_len, false));
+    auto* idx = static_cast<IndexEntry*>(map_file(part_path(dir_, pidx, "idx"), m.idx_len, false));
+    __atomic_store_n(&m.idx, idx, __ATOMIC_RELEASE);
+  }
+  return m;
+}
+
+const uint8_t* Broker::log_base(uint32_t pidx) { return mapped(pidx).log; }
+const IndexEntry* Broker::index_base(uint32_t pidx) { return mapped(pidx).idx; }
+
+int64_t Broker::find_batch(uint32_t pidx, int64_t offset, int64_t hint) {
+  const PartitionEntry& P = part(pidx);
+  const IndexEntry* idx = mapped(pidx).idx;
+  const int64_t nb = int64_t(P.n_batches.load(std::memory_order_acquire));
+  auto contains = [&](int64_t i) {
+    return i >= 0 && i < nb && idx[i].base_offset <= offset && offset <= idx[i].base_offset + idx[i].last_offset_delta;
+  };
+  if (contains(hint)) return hint;
+  if (contains(hint + 1)) return hint + 1;
+  int64_t lo = 0, hi = nb;  // first entry with base_offset > offset
+  while (lo < hi) {
+    int64_t mid = (lo + hi) / 2;
+    if (idx[mid].base_offset <= offset) lo = mid + 1; else hi = mid;
+  }
+  int64_t i = lo - 1;
+  if (!contains(i)) throw OffsetOutOfRange("offset " + std::to_string(offset) + " not in log");
+  return i;
+}
+
+// ------------------------------------------------------------ produce
+int64_t Broker::append(uint32_t pidx, const RecordIn* recs, size_t n) {
+  if (n == 0) throw std::invalid_argument("empty batch");
+  PartitionEntry& P = part(pidx);
+  Mapped& m = mapped(pidx);
+  int64_t min_ts = recs[0].timestamp;
+  for (size_t i = 1; i < n; ++i) min_ts = std::min(min_ts, recs[i].timestamp);
+  const size_t size = batch_encoded_size(recs, n, min_ts);
+  RobustLock l(&P.lock);
+  const uint64_t pos = P.log_end_pos.load(std::memory_order_relaxed);
+  const uint64_t nb = P.n_batches.load(std::memory_order_relaxed);
+  if (pos + size > P.log_capacity)
+    throw KafkaError("partition log full (capacity " + std::to_string(P.log_capacity) + " bytes)");
+  if (nb >= P.index_capacity) throw KafkaError("partition index full");
+  const int64_t base = P.high_watermark.load(std::memory_order_relaxed);
+  const size_t wrote = encode_batch(m.log + pos, base, recs, n);
+  int64_t max_ts = recs[0].timestamp;
+  for (size_t i = 1; i < n; ++i) max_ts = std::max(max_ts, recs[i].timestamp);
+  m.idx[nb] = IndexEntry{base, pos, uint32_t(wrote), int32_t(n - 1), max_ts};
+  P.log_end_pos.store(pos + wrote, std::memory_order_release);
+  P.n_batches.store(nb + 1, std::memory_order_release);
+  P.records_produced.fetch_add(n, std::memory_order_relaxed);
+  P.high_watermark.store(base + int64_t(n), std::memory_order_release);
+  return base;
+}
+
+void Broker::delete_records(uint32_t pidx, int64_t before_offset) {
+  PartitionEntry& P = part(pidx);
+  RobustLock l(&P.lock);
+  const int64_t hw = P.high_watermark.load();
+  int64_t v = std::min(before_offset, hw);
+  if (v > P.log_start_offset.load()) P.log_start_offset.store(v, std::memory_order_release);
+}
+
+// Synthetic record generators.  Values are a deterministic
+// function of (partition, offset) so any consumer can verify what it got.
+//   kind 0 FIXED_F32   : size_a floats; v[0]=offset, v[1]=partition, v[j]=pattern
+//   kind 1 JSON_F32    : JSON array text of L in [size_a, size_b] numbers "%.2f"
+//   kind 2 BYTES       : L in [size_a, size_b] bytes of a (p, o) pattern
+//   kind 3 TOKENS_I32  : L in [size_a, size_b] int32 token ids
+//   kind 4 VARLEN_F32  : L in [size_a, size_b] raw float32
+namespace {
+
+inline float synth_f32(uint32_t p, int64_t o, int64_t j) {
+  return float(int64_t((uint64_t(o) * 31u + uint64_t(j) * 7u + p * 13u) % 2001u) - 1000) * 0.0625f;
+}
+
+inline int64_t synth_len(uint64_t seed, uint32_t p, int64_t o, int64_t lo, int64_t hi) {
+  if (hi <= lo) return lo;
+  return lo + int64_t(mix64(seed ^ (uint64_t(p) << 40) ^ uint64_t(o)) % uint64_t(hi - lo + 1));
+}
+
+size_t gen_value(std::vector<uint8_t>& buf, int kind, uint32_t p, int64_t o, int64_t a, int64_t b,
+                 uint64_t seed) {
+  switch (kind) {
+    case 0: {
+      buf.resize(size_t(a) * 4);
+      float* v = reinterpret_cast<float*>(buf.data());
+      if (a > 0) v[0] = float(o);
+      if (a > 1) v[1] = float(p);
+      for (int64_t j = 2; j < a; ++j) v[j] = synth_f32(p, o, j);
+      return buf.size();
+    }
+    case 1: {
+      const int64_t L = synth_len(seed, p, o, a, b);
+      buf.resize(size_t(L) * 12 + 2);
+      char* s = reinterpret_cast<char*>(buf.data());
+      size_t n = 0;
+      s[n++] = '[';
+      for (int64_t j = 0; j < L; ++j) {
+        if (j) { s[n++] = ','; s[n++] = ' '; }
+        // value in [-50.00, 50.99] with two decimals, cheap exact formatting
+        int64_t cents = int64_t(mix64(seed + uint64_t(o) * 1315423911u + uint64_t(j) * 2654435761u + p) % 10100) - 5000;
+        if (cents < 0) { s[n++] = '-'; cents = -cents; }
+        int64_t ip = cents / 100, fp = cents % 100;
+        if (ip >= 10) s[n++] = char('0' + ip / 10);
+        s[n++] = char('0' + ip % 10);
+        s[n++] = '.';
+        s[n++] = char('0' + fp / 10);
+        s[n++] = char('0' + fp % 10);
+      }
+      s[n++] = ']';
+      buf.resize(n);
+      return n;
+    }
+    case 2: {
+      const int64_t L = synth_len(seed, p, o, a, b);
+      buf.resize(size_t(L));
+      uint64_t pat = mix64((uint64_t(p) << 48) ^ uint64_t(o) ^ seed);
+      size_t i = 0;
+      for (; i + 8 <= buf.size(); i += 8) std::memcpy(buf.data() + i, &pat, 8);
+      for (; i < buf.size(); ++i) buf[i] = uint8_t(pat >> (8 * (i & 7)));
+      return buf.size();
+    }
+    case 3: {
+      const int64_t L = synth_len(seed, p, o, a, b);
+      buf.resize(size_t(L) * 4);
+      int32_t* t = reinterpret_cast<int32_t*>(buf.data());
+      for (int64_t j = 0; j < L; ++j) t[j] = int32_t((uint64_t(o) * 977u + uint64_t(j) * 131u + p * 7u) % 50000u);
+      return buf.size();
+    }
+    case 4: {
+      const int64_t L = synth_len(seed, p, o, a, b);
+      buf.resize(size_t(L) * 4);
+      float* v = reinterpret_cast<float*>(buf.data());
+      for (int64_t j = 0; j < L; ++j) v[j] = synth_f32(p, o, j);
+      return buf.size();
+    }
+    default:
+      throw std::invalid_argument("unknown synthetic record kind");
+  }
+}
+
+}  // namespace
+
+void Broker::fill_synthetic(const std::vector<uint32_t>& pidxs, int64_t n_records, int kind, int64_t size_a,
+                            int64_t size_b, uint32_t records_per_batch, uint64_t seed, int n_threads) {
+  if (records_per_batch == 0) records_per_batch = 1;
+  for (uint32_t pidx : pidxs) { part(pidx); mapped(pidx); }
+  std::atomic<size_t> next{0};
+  std::exception_ptr err;
+  std::mutex err_mu;
+  auto work = [&]() {
+    std::vector<std::vector<uint8_t>> vals(records_per_batch);
+    std::vector<RecordIn> recs(records_per_batch);
+    try {
+      for (;;) {
+        const size_t k = next.fetch_add(1);
+        if (k >= pidxs.size()) break;
+        const uint32_t pidx = pidxs[k];
+        const uint32_t p = parts_[pidx].partition;
+        int64_t done = 0;
+        while (done < n_records) {
+          const int64_t base = parts_[pidx].high_watermark.load();
+          const size_t n = size_t(std::min<int64_t>(records_per_batch, n_records - done));
+          for (size_t i = 0; i < n; ++i) {
+            const int64_t o = base + int64_t(i);
+            size_t len = gen_value(vals[i], kind, p, o, size_a, size_b, seed);
+            recs[i] = RecordIn{1700000000000LL + o, nullptr, -1, vals[i].data(), int32_t(len), nullptr, 0};
+          }
+          append(pidx, recs.data(), n);
+          done += int64_t(n);
+        }
+      }
+    } catch (...) {
+      std::lock_guard<std::mutex> g(err_mu);
+      if (!err) err = std::current_exception();
+    }
+  };
+  n_threads = std::max(1, std::min<int>(n_threads, int(pidxs.size())));
+  std::vector<std::thread> ts;
+  for (int i = 1; i < n_threads; ++i) ts.emplace_back(work);
+  work();
+  for (auto& t : ts) t.join();
+  if (err) std::rethrow_exception(err);
+}
+
+// ------------------------------------------------------------ groups
+GroupEntry& Broker::group(uint32_t g) const {
+  if (g >= meta_->n_groups.load(std::memory_order_acquire)) throw std::out_of_range("bad group index");
+  return groups_[g];
+}
+int16_t* Broker::owners(uint32_t g) const { return owners_ + size_t(g) * meta_->max_partitions; }
+OffsetEntry& Broker::offset_entry(uint32_t g, uint32_t pidx) const {
+  if (pidx >= meta_->max_partitions) throw std::out_of_range("bad partition index");
+  return offsets_[size_t(g) * meta_->max_partitions + pidx];
+}
+
+uint32_t Broker::group_index(const std::string& name, bool create) {
+  if (name.empty() || name.size() >= kNameLen) throw std::invalid_argument("bad group id");
+  auto scan = [&]() -> int64_t {
+    const uint32_t n = meta_->n_groups.load(std::memory_order_acquire);
+    for (uint32_t i = 0; i < n; ++i)
+      if (name == groups_[i].name) return i;
+    return -1;
+  };
+  int64_t g = scan();
+  if (g >= 0 || !create) {
+    if (g < 0) throw KafkaError("unknown group '" + name + "'");
+    return uint32_t(g);
+  }
+  RobustLock l(&meta_->lock);
+  g = scan();
+  if (g >= 0) return uint32_t(g);
+  const uint32_t n = meta_->n_groups.load();
+  if (n >= meta_->max_groups) throw KafkaError("broker group table full");
+  GroupEntry& G = groups_[n];
+  std::memset(G.name, 0, kNameLen);
+  std::memcpy(G.name, name.data(), name.size());
+  G.generation.store(0);
+  G.state.store(kGroupEmpty);
+  G.next_member_id = 0;
+  for (auto& m : G.members) m.active.store(0);
+  meta_->n_groups.store(n + 1, std::memory_order_release);
+  return n;
+}
+
+std::string Broker::group_name(uint32_t g) const { return group(g).name; }
+
+uint64_t Broker::member_id(uint32_t g, int slot) const { return group(g).members[slot].member_id; }
+
+bool Broker::expire_members_locked(GroupEntry& G, int64_t now) {
+  bool changed = false;
+  for (auto& M : G.members) {
+    if (!M.active.load()) continue;
+    const bool dead = !pid_alive(M.pid);
+    const bool stale = now - M.last_poll_ns.load() > M.max_poll_interval_ns;
+    if (dead || stale) {
+      M.active.store(0);
+      changed = true;
+    }
+  }
+  G.last_expiry_check_ns.store(now);
+  return changed;
+}
+
+void Broker::assign_locked(GroupEntry& G, uint32_t g) {
+  // Range assignor (kafka-python's default): per topic, members subscribed to
+  // it sorted by member id; partition count split into contiguous ranges.
+  int16_t* own = owners(g);
+  std::fill(own, own + meta_->max_partitions, int16_t(-1));
+  const uint32_t nt = meta_->n_topics.load();
+  for (uint32_t t = 0; t < nt; ++t) {
+    std::vector<std::pair<uint64_t, int>> subs;
+    for (int s = 0; s < kMaxMembers; ++s) {
+      const MemberEntry& M = G.members[s];
+      if (!M.active.load()) continue;
+      for (uint32_t i = 0; i < M.n_topics; ++i)
+        if (M.topics[i] == t) { subs.emplace_back(M.member_id, s); break; }
+    }
+    if (subs.empty()) continue;
+    std::sort(subs.begin(), subs.end());
+    const uint32_t np = topics_[t].n_partitions, first = topics_[t].first_pidx;
+    const uint32_t m = uint32_t(subs.size()), per = np / m, extra = np % m;
+    uint32_t p = 0;
+    for (uint32_t k = 0; k < m; ++k) {
+      const uint32_t cnt = per + (k < extra ? 1 : 0);
+      for (uint32_t c = 0; c < cnt; ++c) own[first + p++] = int16_t(subs[k].second);
+    }
+  }
+}
+
+void Broker::rebalance_locked(GroupEntry& G, uint32_t g, int64_t now, bool immediate) {
+  int active = 0;
+  for (auto& M : G.members) active += M.active.load() ? 1 : 0;
+  if (active == 0) {
+    int16_t* own = owners(g);
+    std::fill(own, own + meta_->max_partitions, int16_t(-1));
+    G.generation.fetch_add(1);
+    G.state.store(kGroupEmpty);
+    return;
+  }
+  const uint32_t st = G.state.load();
+  if (st == kGroupEmpty && !immediate && meta_->group_initial_rebalance_delay_ms > 0) {
+    G.prepare_deadline_ns = now + int64_t(meta_->group_initial_rebalance_delay_ms) * 1000000LL;
+    G.state.store(kGroupPreparing);
+    return;
+  }
+  if (st == kGroupPreparing && !immediate && now < G.prepare_deadline_ns) return;
+  assign_locked(G, g);
+  G.generation.fetch_add(1);
+  G.state.store(kGroupStable, std::memory_order_release);
+}
+
+int Broker::join_group(uint32_t g, const std::vector<uint32_t>& topic_indices, int64_t session_timeout_ms,
+                       int64_t max_poll_interval_ms) {
+  if (topic_indices.size() > size_t(kMaxSubscribedTopics)) throw std::invalid_argument("too many topics");
+  GroupEntry& G = group(g);
+  RobustLock l(&meta_->lock);
+  const int64_t now = now_ns();
+  expire_members_locked(G, now);
+  int slot = -1;
+  for (int s = 0; s < kMaxMembers; ++s)
+    if (!G.members[s].active.load()) { slot = s; break; }
+  if (slot < 0) throw KafkaError("consumer group '" + std::string(G.name) + "' is full");
+  MemberEntry& M = G.members[slot];
+  M.pid = int32_t(getpid());
+  M.last_poll_ns.store(now);
+  M.session_timeout_ns = session_timeout_ms * 1000000LL;
+  M.max_poll_interval_ns = max_poll_interval_ms * 1000000LL;
+  M.member_id = ++G.next_member_id;
+  M.n_topics = uint32_t(topic_indices.size());
+  for (size_t i = 0; i < topic_indices.size(); ++i) M.topics[i] = topic_indices[i];
+  M.active.store(1, std::memory_order_release);
+  rebalance_locked(G, g, now, false);
+  return slot;
+}
+
+void Broker::leave_group(uint32_t g, int slot, uint64_t mid) {
+  GroupEntry& G = group(g);
+  RobustLock l(&meta_->lock);
+  MemberEntry& M = G.members[slot];
+  if (!M.active.load() || M.member_id != mid) return;
+  M.active.store(0);
+  rebalance_locked(G, g, now_ns(), true);
+}
+
+GroupView Broker::poll_group(uint32_t g, int slot, uint64_t mid) {
+  GroupEntry& G = group(g);
+  GroupView v{};
+  MemberEntry& M = G.members[slot];
+  const int64_t now = now_ns();
+  if (M.active.load() && M.member_id == mid) M.last_poll_ns.store(now);
+  RobustLock l(&meta_->lock);
+  if (now - G.last_expiry_check_ns.load() > 50000000LL && expire_members_locked(G, now))
+    rebalance_locked(G, g, now, true);
+  if (G.state.load() == kGroupPreparing && now >= G.prepare_deadline_ns) rebalance_locked(G, g, now, false);
+  v.member_active = M.active.load() && M.member_id == mid;
+  v.generation = G.generation.load();
+  v.state = G.state.load();
+  if (v.member_active && v.state == kGroupStable) {
+    const int16_t* own = owners(g);
+    const uint32_t np = meta_->n_partitions.load();
+    for (uint32_t p = 0; p < np; ++p)
+      if (own[p] == slot) v.assignment.push_back(p);
+  }
+  return v;
+}
+
+void Broker::commit(uint32_t g, int slot, uint64_t mid, uint32_t generation, const std::vector<CommitEntry>& entries) {
+  GroupEntry& G = group(g);
+  int32_t inj = G.inject_commit_failures.load();
+  while (inj > 0) {
+    if (G.inject_commit_failures.compare_exchange_weak(inj, inj - 1))
+      throw CommitFailed("CommitFailedError: injected commit failure");
+  }
+  if (slot >= 0) {
+    RobustLock l(&meta_->lock);
+    MemberEntry& M = G.members[slot];
+    if (!M.active.load() || M.member_id != mid)
+      throw CommitFailed("CommitFailedError: member is no longer part of the group (rebalanced)");
+    const int64_t now = now_ns();
+    if (now - M.last_poll_ns.load() > M.max_poll_interval_ns) {
+      M.active.store(0);
+      rebalance_locked(G, g, now, true);
+      throw CommitFailed("CommitFailedError: time between polls exceeded max_poll_interval_ms");
+    }
+    if (G.state.load() != kGroupStable || G.generation.load() != generation)
+      throw CommitFailed("CommitFailedError: the group has rebalanced (generation " +
+                         std::to_string(G.generation.load()) + ", member had " + std::to_string(generation) + ")");
+  } else if (G.state.load(std::memory_order_acquire) != kGroupEmpty) {
+    throw CommitFailed("CommitFailedError: group has active members; commit from a non-member rejected");
+  }
+  const int64_t wall = wall_ms();
+  for (const auto& e : entries) {
+    OffsetEntry& O = offset_entry(g, e.pidx);
+    const size_t ml = std::min(e.metadata.size(), sizeof(O.metadata));
+    std::memcpy(O.metadata, e.metadata.data(), ml);
+    O.meta_len = int32_t(ml);
+    O.commit_wall_ms.store(wall, std::memory_order_relaxed);
+    O.offset.store(e.offset, std::memory_order_release);
+    O.seq.fetch_add(1, std::memory_order_release);
+  }
+  G.n_commits.fetch_add(1, std::memory_order_relaxed);
+}
+
+int64_t Broker::committed(uint32_t g, uint32_t pidx, std::string* metadata) const {
+  const OffsetEntry& O = offset_entry(g, pidx);
+  const int64_t off = O.offset.load(std::memory_order_acquire);
+  if (metadata && off >= 0) metadata->assign(O.metadata, size_t(O.meta_len));
+  return off;
+}
+
+uint64_t Broker::commit_count(uint32_t g) const { return group(g).n_commits.load(); }
+
+void Broker::inject_commit_failures(uint32_t g, int32_t n) { group(g).inject_commit_failures.store(n); }
+
+void Broker::reset_group_offsets(uint32_t g) {
+  group(g);
+  for (uint32_t p = 0; p < meta_->max_partitions; ++p) offset_entry(g, p).offset.store(-1);
+}
+
+}  // namespace tk

@@ -1,0 +1,238 @@
+// Synthetic Kafka broker living in shared memory (or a persistent directory).
+//
+// Role: stands in for the Kafka cluster the reference talks to through
+// kafka-python (reference kafka_dataset.py:21-22,206).  It keeps
+// the exact semantics the reference's commit protocol depends on:
+//   * partitioned append-only logs of RecordBatch v2 bytes (zero-copy fetch);
+//   * per-(group, partition) committed offsets that survive process restarts
+//     when the broker directory is on disk (the "checkpoint");
+//   * consumer groups with range assignment, generations and rebalances, so
+//     a stale member's commit fails with CommitFailedError (B14);
+//   * fault injection: commit failures, slow and failing fetches (D3/D4/D8 tests).
+//
+// Layout of a broker directory:
+//   lock          flock()ed while the meta file is created
+//   meta          MetaHeader | TopicEntry[] | PartitionEntry[] | GroupEntry[] |
+//                 owners int16[groups][partitions] | OffsetEntry[groups][partitions]
+//   pNNNNN.log    RecordBatch bytes of global partition NNNNN (sparse, mmap'ed)
+//   pNNNNN.idx    IndexEntry per batch (base offset -> file position)
+// Every process maps the files MAP_SHARED; cross-process synchronisation uses
+// atomics in the mapping plus robust process-shared pthread mutexes.
+#pragma once
+#include <pthread.h>
+
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "record_batch.h"
+
+namespace tk {
+
+constexpr uint64_t kBrokerMagic = 0x31304B4F5242544BULL;  // "TKBROK01"
+constexpr uint32_t kBrokerVersion = 1;
+constexpr int kMaxMembers = 64;
+constexpr int kMaxSubscribedTopics = 16;
+constexpr int kNameLen = 160;
+
+struct BrokerConfig {
+  uint32_t max_topics = 256;
+  uint32_t max_partitions = 4096;
+  uint32_t max_groups = 64;
+  uint64_t default_log_capacity = 256ull << 20;   // bytes per partition (sparse)
+  uint64_t default_index_capacity = 1u << 20;     // batches per partition
+  uint32_t group_initial_rebalance_delay_ms = 100;
+};
+
+struct alignas(64) MetaHeader {
+  uint64_t magic;
+  uint32_t version;
+  std::atomic<uint32_t> ready;
+  uint32_t max_topics, max_partitions, max_groups, group_initial_rebalance_delay_ms;
+  uint64_t default_log_capacity, default_index_capacity;
+  std::atomic<uint32_t> n_topics, n_partitions, n_groups, pad0;
+  pthread_mutex_t lock;  // topic/group creation, membership changes
+};
+
+struct alignas(64) TopicEntry {
+  char name[kNameLen];
+  uint32_t n_partitions;
+  uint32_t first_pidx;
+  uint64_t log_capacity;
+  uint64_t index_capacity;
+};
+
+struct IndexEntry {
+  int64_t base_offset;
+  uint64_t pos;
+  uint32_t size;
+  int32_t last_offset_delta;
+  int64_t max_timestamp;
+};
+static_assert(sizeof(IndexEntry) == 32, "index entry layout");
+
+struct alignas(64) PartitionEntry {
+  pthread_mutex_t lock;                   // producer append lock
+  std::atomic<int64_t> high_watermark;    // next offset to be produced
+  std::atomic<int64_t> log_start_offset;  // first retained offset
+  std::atomic<uint64_t> log_end_pos;      // bytes used in the .log file
+  std::atomic<uint64_t> n_batches;        // published index entries
+  uint64_t log_capacity, index_capacity;
+  uint32_t topic_index, partition;
+  // fault injection & metrics
+  std::atomic<int64_t> fetch_delay_ns;
+  std::atomic<int32_t> fetch_errors;
+  std::atomic<uint32_t> pad1;
+  std::atomic<uint64_t> fetch_calls, bytes_fetched, records_produced;
+};
+
+struct alignas(64) MemberEntry {
+  std::atomic<uint32_t> active;
+  int32_t pid;
+  std::atomic<int64_t> last_poll_ns;
+  int64_t session_timeout_ns;
+  int64_t max_poll_interval_ns;
+  uint64_t member_id;
+  uint32_t n_topics;
+  uint32_t topics[kMaxSubscribedTopics];
+};
+
+enum GroupState : uint32_t { kGroupEmpty = 0, kGroupPreparing = 1, kGroupStable = 2 };
+
+struct alignas(64) GroupEntry {
+  char name[kNameLen];
+  std::atomic<uint32_t> generation;
+  std::atomic<uint32_t> state;
+  int64_t prepare_deadline_ns;
+  uint64_t next_member_id;
+  std::atomic<int32_t> inject_commit_failures;
+  std::atomic<int32_t> pad;
+  std::atomic<uint64_t> n_commits;
+  std::atomic<int64_t> last_expiry_check_ns;
+  MemberEntry members[kMaxMembers];
+};
+
+struct alignas(64) OffsetEntry {
+  std::atomic<int64_t> offset;  // -1 = nothing committed
+  std::atomic<uint64_t> seq;
+  std::atomic<int64_t> commit_wall_ms;
+  int32_t meta_len;
+  char metadata[36];
+};
+
+struct TopicInfo {
+  uint32_t index, n_partitions, first_pidx;
+  std::string name;
+};
+
+struct CommitEntry {
+  uint32_t pidx;
+  int64_t offset;
+  std::string metadata;
+};
+
+struct GroupView {
+  uint32_t generation;
+  uint32_t state;
+  bool member_active;       // false: this member was evicted / left
+  std::vector<uint32_t> assignment;  // global partition indices (sorted)
+};
+
+class Broker {
+ public:
+  // url: "shm://name" -> /dev/shm/torchkafka/name ; "file:///abs/dir" or a plain path.
+  static std::string url_to_dir(const std::string& url);
+  Broker(const std::string& url, bool create, const BrokerConfig& cfg);
+  ~Broker();
+  Broker(const Broker&) = delete;
+  Broker& operator=(const Broker&) = delete;
+
+  const std::string& dir() const { return dir_; }
+  const MetaHeader& meta() const { return *meta_; }
+
+  // ---- topics
+  TopicInfo create_topic(const std::string& name, uint32_t n_partitions, uint64_t log_capacity = 0,
+                         uint64_t index_capacity = 0);
+  bool find_topic(const std::string& name, TopicInfo* out) const;
+  std::vector<TopicInfo> topics() const;
+  PartitionEntry& part(uint32_t pidx);
+  const PartitionEntry& part(uint32_t pidx) const;
+
+  // ---- log access (zero-copy)
+  const uint8_t* log_base(uint32_t pidx);
+  const IndexEntry* index_base(uint32_t pidx);
+  // Index of the batch containing `offset` (requires log_start <= offset < hw), hint = last result.
+  int64_t find_batch(uint32_t pidx, int64_t offset, int64_t hint) ;
+
+  // ---- produce: appends one batch, returns its base offset.
+  int64_t append(uint32_t pidx, const RecordIn* recs, size_t n);
+  // Synthetic generator (see SyntheticSpec in broker.cpp): fills n records per partition.
+  void fill_synthetic(const std::vector<uint32_t>& pidxs, int64_t n_records, int kind, int64_t size_a,
+                      int64_t size_b, uint32_t records_per_batch, uint64_t seed, int n_threads);
+  void delete_records(uint32_t pidx, int64_t before_offset);
+
+  // ---- groups / offsets
+  uint32_t group_index(const std::string& group, bool create = true);
+  std::string group_name(uint32_t g) const;
+  // Joins (subscribe mode).  Returns member slot.
+  int join_group(uint32_t g, const std::vector<uint32_t>& topic_indices, int64_t session_timeout_ms,
+                 int64_t max_poll_interval_ms);
+  void leave_group(uint32_t g, int member_slot, uint64_t member_id);
+  uint64_t member_id(uint32_t g, int slot) const;
+  GroupView poll_group(uint32_t g, int member_slot, uint64_t member_id);
+  // member_slot < 0: manual-assignment ("simple") consumer.
+  void commit(uint32_t g, int member_slot, uint64_t member_id, uint32_t generation,
+              const std::vector<CommitEntry>& entries);
+  int64_t committed(uint32_t g, uint32_t pidx, std::string* metadata = nullptr) const;
+  uint64_t commit_count(uint32_t g) const;
+  void inject_commit_failures(uint32_t g, int32_t n);
+  void reset_group_offsets(uint32_t g);
+
+  // ---- fault injection
+  void set_fetch_delay(uint32_t pidx, int64_t delay_ns) { part(pidx).fetch_delay_ns.store(delay_ns); }
+  void inject_fetch_errors(uint32_t pidx, int32_t n) { part(pidx).fetch_errors.store(n); }
+
+ private:
+  struct Mapped {
+    uint8_t* log = nullptr;
+    IndexEntry* idx = nullptr;
+    size_t log_len = 0, idx_len = 0;
+  };
+  void map_meta(bool create, const BrokerConfig& cfg);
+  Mapped& mapped(uint32_t pidx);
+  GroupEntry& group(uint32_t g) const;
+  int16_t* owners(uint32_t g) const;
+  OffsetEntry& offset_entry(uint32_t g, uint32_t pidx) const;
+  void rebalance_locked(GroupEntry& G, uint32_t g, int64_t now, bool immediate);
+  void assign_locked(GroupEntry& G, uint32_t g);
+  bool expire_members_locked(GroupEntry& G, int64_t now);
+
+  std::string dir_;
+  int meta_fd_ = -1;
+  uint8_t* meta_map_ = nullptr;
+  size_t meta_len_ = 0;
+  MetaHeader* meta_ = nullptr;
+  TopicEntry* topics_ = nullptr;
+  PartitionEntry* parts_ = nullptr;
+  GroupEntry* groups_ = nullptr;
+  int16_t* owners_ = nullptr;
+  OffsetEntry* offsets_ = nullptr;
+  std::vector<Mapped> maps_;
+  std::mutex maps_mu_;
+};
+
+// Locks a robust process-shared mutex, recovering it if its owner died.
+class RobustLock {
+ public:
+  explicit RobustLock(pthread_mutex_t* m);
+  ~RobustLock();
+
+ private:
+  pthread_mutex_t* m_;
+};
+void init_robust_mutex(pthread_mutex_t* m);
+
+}  // namespace tk

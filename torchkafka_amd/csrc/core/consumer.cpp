@@ -1,0 +1,329 @@
+#include "consumer.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <limits>
+
+namespace tk {
+
+void Fetcher::assign(const std::vector<uint32_t>& pidxs, const std::vector<int64_t>& positions) {
+  if (pidxs.size() != positions.size()) throw std::invalid_argument("assign: size mismatch");
+  std::vector<FetchPart> np;
+  for (size_t i = 0; i < pidxs.size(); ++i) {
+    b_->part(pidxs[i]);  // validates
+    FetchPart fp;
+    fp.pidx = pidxs[i];
+    fp.position = positions[i];
+    // keep decode caches of partitions that stay assigned at the same position
+    for (const auto& old : parts_)
+      if (old.pidx == fp.pidx && old.position == fp.position) {
+        fp.batch_hint = old.batch_hint;
+        fp.verified_base = old.verified_base;
+        fp.paused = old.paused;
+      }
+    np.push_back(fp);
+  }
+  parts_ = std::move(np);
+}
+
+size_t Fetcher::find(uint32_t pidx) const {
+  for (size_t i = 0; i < parts_.size(); ++i)
+    if (parts_[i].pidx == pidx) return i;
+  return size_t(-1);
+}
+
+bool Fetcher::has_data(const FetchPart& fp) {
+  const PartitionEntry& P = b_->part(fp.pidx);
+  const int64_t hw = P.high_watermark.load(std::memory_order_acquire);
+  if (fp.position > hw || fp.position < P.log_start_offset.load(std::memory_order_acquire))
+    throw OffsetOutOfRange("OffsetOutOfRangeError: position " + std::to_string(fp.position) +
+                           " outside [" + std::to_string(P.log_start_offset.load()) + ", " + std::to_string(hw) +
+                           "] of partition index " + std::to_string(fp.pidx));
+  return fp.position < hw;
+}
+
+// ------------------------------------------------------------ JSON
+namespace {
+
+inline bool is_ws(char c) { return c == ' ' || c == '\n' || c == '\t' || c == '\r'; }
+inline bool is_digit(char c) { return c >= '0' && c <= '9'; }
+
+const double kPow10[] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                         1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+// Parses one JSON number (or NaN/Infinity/-Infinity, which Python's json accepts).
+// Returns the end pointer or nullptr.
+const char* parse_number(const char* p, const char* e, double* out) {
+  const char* start = p;
+  bool neg = false;
+  if (p < e && *p == '-') { neg = true; ++p; }
+  if (p < e && (*p == 'N' || *p == 'I')) {
+    if (e - p >= 3 && std::memcmp(p, "NaN", 3) == 0 && !neg) { *out = std::numeric_limits<double>::quiet_NaN(); return p + 3; }
+    if (e - p >= 8 && std::memcmp(p, "Infinity", 8) == 0) {
+      *out = neg ? -std::numeric_limits<double>::infinity() : std::numeric_limits<double>::infinity();
+      return p + 8;
+    }
+    return nullptr;
+  }
+  uint64_t mant = 0;
+  int nd = 0, exp10 = 0;
+  bool any = false, truncated = false;
+  while (p < e && is_digit(*p)) {
+    const int d = *p++ - '0';
+    any = true;
+    if (mant == 0 && d == 0) continue;
+    if (nd < 19) { mant = mant * 10 + uint64_t(d); ++nd; } else { ++exp10; truncated = true; }
+  }
+  if (p < e && *p == '.') {
+    ++p;
+    bool frac = false;
+    while (p < e && is_digit(*p)) {
+      const int d = *p++ - '0';
+      frac = true;
+      if (mant == 0 && d == 0) { --exp10; continue; }
+      if (nd < 19) { mant = mant * 10 + uint64_t(d); ++nd; --exp10; } else { truncated = true; }
+    }
+    if (!frac) return nullptr;
+    any = true;
+  }
+  if (!any) return nullptr;
+  if (p < e && (*p == 'e' || *p == 'E')) {
+    ++p;
+    bool eneg = false;
+    if (p < e && (*p == '+' || *p == '-')) eneg = *p++ == '-';
+    if (p >= e || !is_digit(*p)) return nullptr;
+    int ev = 0;
+    while (p < e && is_digit(*p)) { if (ev < 100000) ev = ev * 10 + (*p - '0'); ++p; }
+    exp10 += eneg ? -ev : ev;
+  }
+  double v;
+  if (!truncated && mant <= (1ull << 53) && exp10 >= -22 && exp10 <= 22) {
+    // Clinger's fast path: both operands exact, one correctly rounded op.
+    v = exp10 < 0 ? double(mant) / kPow10[-exp10] : double(mant) * kPow10[exp10];
+    if (neg) v = -v;
+  } else {
+    char buf[128];
+    const size_t len = std::min<size_t>(size_t(p - start), sizeof(buf) - 1);
+    std::memcpy(buf, start, len);
+    buf[len] = 0;
+    v = std::strtod(buf, nullptr);
+  }
+  *out = v;
+  return p;
+}
+
+}  // namespace
+
+int64_t parse_json_f32(const char* s, size_t n, float* out, int64_t cap) {
+  const char* p = s;
+  const char* e = s + n;
+  while (p < e && is_ws(*p)) ++p;
+  if (p >= e || *p != '[') return -1;
+  ++p;
+  while (p < e && is_ws(*p)) ++p;
+  int64_t k = 0;
+  if (p < e && *p == ']') {
+    ++p;
+  } else {
+    for (;;) {
+      while (p < e && is_ws(*p)) ++p;
+      double v;
+      p = parse_number(p, e, &v);
+      if (!p) return -1;
+      if (k >= cap) return -2;
+      out[k++] = float(v);
+      while (p < e && is_ws(*p)) ++p;
+      if (p >= e) return -1;
+      if (*p == ',') { ++p; continue; }
+      if (*p == ']') { ++p; break; }
+      return -1;
+    }
+  }
+  while (p < e && is_ws(*p)) ++p;
+  return p == e ? k : -1;
+}
+
+int64_t json_array_len(const char* s, size_t n) {
+  const char* p = s;
+  const char* e = s + n;
+  while (p < e && is_ws(*p)) ++p;
+  if (p >= e || *p != '[') return -1;
+  ++p;
+  int64_t k = 0;
+  bool in_tok = false;
+  for (; p < e; ++p) {
+    if (*p == ']') return in_tok ? k + 1 : k;
+    if (*p == ',') { if (!in_tok) return -1; ++k; in_tok = false; }
+    else if (!is_ws(*p)) in_tok = true;
+  }
+  return -1;
+}
+
+// ------------------------------------------------------------ fill
+FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, int64_t B, int64_t timeout_ms,
+                      size_t* rr) {
+  SlotHeader* h = ring.slot(g);
+  uint8_t* pay = ring.payload(g);
+  const uint64_t cap = ring.payload_capacity();
+  auto& parts = f.parts();
+  FillOutcome out;
+  h->n_rows = 0;
+  h->n_parts = 0;
+  h->flags = 0;
+  h->kind = uint32_t(spec.kind);
+  h->err_len = 0;
+  h->max_row_len = 0;
+  h->total_elems = 0;
+  h->n_scanned = 0;
+  h->src_dtype = -1;
+  h->ndim = 0;
+  h->t_fill_start_ns = now_ns();
+  if (B <= 0) throw std::invalid_argument("batch size must be positive");
+
+  const bool fixed = spec.kind == kPackFixed;
+  const uint64_t row_bytes = fixed ? uint64_t(spec.row_elems) * uint64_t(spec.elem_size) : 0;
+  uint64_t values_off = 0;
+  int32_t* offs = nullptr;
+  if (fixed) {
+    if (uint64_t(B) * row_bytes > cap) throw std::invalid_argument("ring slot too small for the batch");
+  } else {
+    values_off = align_up(uint64_t(B + 1) * 4, 256);
+    if (values_off >= cap) throw std::invalid_argument("ring slot too small for the batch offsets");
+    offs = reinterpret_cast<int32_t*>(pay);
+    offs[0] = 0;
+  }
+  uint8_t* vals = pay + values_off;
+  const uint64_t vcap = cap - values_off;
+  uint64_t vused = 0;
+  int64_t rows = 0, elems = 0, max_len = 0, scanned = 0;
+  std::vector<int> wm_of(parts.size(), -1);
+  size_t cur_part = 0;
+  bool slot_full = false;
+
+  auto touch = [&](const RecordView& r) {
+    int k = wm_of[cur_part];
+    if (k < 0) {
+      if (h->n_parts >= uint32_t(kMaxSlotParts)) throw std::runtime_error("too many partitions in one slot");
+      k = int(h->n_parts++);
+      wm_of[cur_part] = k;
+      h->wm[k].pidx = parts[cur_part].pidx;
+      h->wm[k].count = 0;
+      h->wm[k].first_offset = parts[cur_part].position;
+    }
+    h->wm[k].count++;
+    h->wm[k].next_offset = r.offset + 1;
+    ++scanned;
+  };
+  auto bad = [&](const RecordView& r, const char* why) -> int {
+    if (!spec.skip_bad)
+      throw CorruptRecord(std::string("record at offset ") + std::to_string(r.offset) + ": " + why);
+    touch(r);
+    return kTake;
+  };
+
+  auto visit = [&](const RecordView& r) -> int {
+    if (r.value == nullptr) { touch(r); return kTake; }  // null value == `_process` returned None
+    if (fixed) {
+      if (uint64_t(r.value_len) != row_bytes) return bad(r, "value size does not match the fixed-width schema");
+      std::memcpy(vals + uint64_t(rows) * row_bytes, r.value, row_bytes);
+      touch(r);
+      ++rows;
+      return rows == B ? kTakeStop : kTake;
+    }
+    int64_t len;
+    uint64_t nbytes;
+    if (spec.kind == kPackVarlen) {
+      if (r.value_len % spec.elem_size) return bad(r, "value size is not a multiple of the element size");
+      len = r.value_len / spec.elem_size;
+      if (len < spec.min_len) { touch(r); return kTake; }
+      if (spec.max_len >= 0 && len > spec.max_len) {
+        if (!spec.truncate) { touch(r); return kTake; }
+        len = spec.max_len;
+      }
+      nbytes = uint64_t(len) * uint64_t(spec.elem_size);
+      if (vused + nbytes > vcap) {
+        if (rows == 0) throw std::runtime_error("a single record exceeds the ring slot capacity");
+        slot_full = true;
+        return kStopBefore;
+      }
+      std::memcpy(vals + vused, r.value, nbytes);
+    } else {  // JSON -> f32
+      float* dst = reinterpret_cast<float*>(vals + vused);
+      const int64_t room = int64_t((vcap - vused) / 4);
+      len = parse_json_f32(reinterpret_cast<const char*>(r.value), size_t(r.value_len), dst, room);
+      if (len == -2) {
+        if (rows == 0) throw std::runtime_error("a single record exceeds the ring slot capacity");
+        slot_full = true;
+        return kStopBefore;
+      }
+      if (len < 0) return bad(r, "value is not a flat numeric JSON array");
+      if (len < spec.min_len) { touch(r); return kTake; }
+      if (spec.max_len >= 0 && len > spec.max_len) {
+        if (!spec.truncate) { touch(r); return kTake; }
+        len = spec.max_len;
+      }
+      nbytes = uint64_t(len) * 4;
+    }
+    vused += nbytes;
+    elems += len;
+    if (elems > INT32_MAX) throw std::runtime_error("slot exceeds int32 element offsets");
+    max_len = std::max(max_len, len);
+    offs[rows + 1] = int32_t(elems);
+    touch(r);
+    ++rows;
+    return rows == B ? kTakeStop : kTake;
+  };
+
+  const int64_t idle_ns = timeout_ms < 0 ? INT64_MAX : timeout_ms * 1000000LL;
+  int64_t last_progress = now_ns();
+  int64_t backoff_ns = 20000;
+  bool stop = false;
+  while (rows < B && !stop && !parts.empty()) {
+    bool progress = false;
+    for (size_t k = 0; k < parts.size() && rows < B; ++k) {
+      cur_part = (*rr + k) % parts.size();
+      FetchPart& fp = parts[cur_part];
+      if (fp.paused) continue;
+      size_t n;
+      try {
+        n = f.scan(fp, 1u << 20, visit);
+      } catch (const OffsetOutOfRange&) {
+        if (rows == 0 && scanned == 0) throw;  // nothing packed yet: let the caller reset positions
+        stop = true;                           // keep what is packed; the reset happens on the next fill
+        break;
+      }
+      if (n) progress = true;
+      if (slot_full) {  // the next record does not fit: close the batch early
+        stop = true;
+        break;
+      }
+    }
+    *rr = (*rr + 1) % std::max<size_t>(parts.size(), 1);
+    if (rows >= B || stop) break;
+    if (progress) {
+      last_progress = now_ns();
+      backoff_ns = 20000;
+      continue;
+    }
+    if (ring.header()->shutdown.load(std::memory_order_acquire)) { out.shutdown = true; break; }
+    const int64_t now = now_ns();
+    if (now - last_progress >= idle_ns) { out.timed_out = true; break; }
+    const int64_t sl = std::min<int64_t>(backoff_ns, idle_ns - (now - last_progress));
+    timespec ts{time_t(sl / 1000000000LL), long(sl % 1000000000LL)};
+    nanosleep(&ts, nullptr);
+    backoff_ns = std::min<int64_t>(backoff_ns * 2, 1000000);
+  }
+  h->n_rows = uint32_t(rows);
+  h->row_bytes = uint32_t(row_bytes);
+  h->values_offset = values_off;
+  h->values_bytes = fixed ? uint64_t(rows) * row_bytes : vused;
+  h->payload_bytes = values_off + h->values_bytes;
+  h->max_row_len = fixed ? spec.row_elems : max_len;
+  h->total_elems = fixed ? rows * spec.row_elems : elems;
+  h->n_scanned = scanned;
+  out.rows = rows;
+  out.scanned = scanned;
+  return out;
+}
+
+}  // namespace tk

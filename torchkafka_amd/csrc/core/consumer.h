@@ -1,0 +1,142 @@
+// Consumer-side native core: partition fetch/decode and the batch packers.
+//
+// The reference's hot loop is kafka-python's per-record iterator feeding a
+// Python `_process` (kafka_dataset.py:156-162), then torch.stack in the
+// DataLoader.  Here the same work for schema-declared records is
+// one native call per batch: walk RecordBatches straight out of the broker's
+// mapped log (CRC-checked once per batch), apply the None-skip filter, and
+// pack values into a pinned ring slot as either a dense [rows, D] block or a
+// CSR (int32 row offsets + values) for variable-length rows.
+#pragma once
+#include <memory>
+#include <vector>
+
+#include "broker.h"
+#include "record_batch.h"
+#include "ring.h"
+
+namespace tk {
+
+struct FetchPart {
+  uint32_t pidx;
+  int64_t position;
+  int64_t batch_hint = -1;
+  int64_t verified_base = INT64_MIN;
+  bool paused = false;
+};
+
+// What the visitor returns for each record.
+enum VisitAction : int { kTake = 0, kTakeStop = 1, kStopBefore = 2 };
+
+class Fetcher {
+ public:
+  Fetcher(std::shared_ptr<Broker> b, bool check_crcs) : b_(std::move(b)), check_crcs_(check_crcs) {}
+  Broker& broker() { return *b_; }
+  std::vector<FetchPart>& parts() { return parts_; }
+  void assign(const std::vector<uint32_t>& pidxs, const std::vector<int64_t>& positions);
+  size_t find(uint32_t pidx) const;  // index into parts(), or npos
+  bool check_crcs() const { return check_crcs_; }
+
+  // Visits up to `max_records` records of one partition at/after its position
+  // without blocking.  Applies fetch fault injection.  Returns records taken.
+  template <class F>
+  size_t scan(FetchPart& fp, size_t max_records, F&& visit);
+
+  // Throws OffsetOutOfRange when position is outside [log_start, hw].
+  bool has_data(const FetchPart& fp);
+
+ private:
+  std::shared_ptr<Broker> b_;
+  bool check_crcs_;
+  std::vector<FetchPart> parts_;
+};
+
+// ------------------------------------------------------------ packers
+enum PackKind : int { kPackFixed = 0, kPackVarlen = 1, kPackJsonF32 = 2 };
+
+struct PackSpec {
+  int kind = kPackFixed;
+  int elem_size = 4;        // bytes per stored element (fixed/var-len); JSON emits f32
+  int64_t row_elems = 0;    // fixed-width: elements per row
+  int64_t min_len = 0;      // var-len/JSON: shorter rows are skipped (the reference's `_process -> None`)
+  int64_t max_len = -1;     // var-len/JSON: longer rows truncated (truncate) or skipped
+  int truncate = 1;
+  int skip_bad = 0;         // malformed rows: 1 = skip, 0 = raise
+};
+
+struct FillOutcome {
+  int64_t rows = 0;
+  int64_t scanned = 0;
+  bool timed_out = false;
+  bool shutdown = false;
+};
+
+// Fills one ring slot with up to `batch_rows` rows, blocking until the batch
+// is full, `timeout_ms` passes without new data (-1 = forever) or shutdown.
+// Writes header fields (rows, watermarks, layout) but does not publish.
+FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t gslot, const PackSpec& spec, int64_t batch_rows,
+                      int64_t timeout_ms, size_t* rr_cursor);
+
+// Numeric JSON array -> float32 (correctly rounded as Python float()+float32 cast).
+// Returns elements parsed, or -1 when the text is not a flat numeric array.
+int64_t parse_json_f32(const char* s, size_t n, float* out, int64_t cap);
+// Element count of a flat numeric JSON array without converting (-1 if malformed).
+int64_t json_array_len(const char* s, size_t n);
+
+// ------------------------------------------------------------ template impl
+template <class F>
+size_t Fetcher::scan(FetchPart& fp, size_t max_records, F&& visit) {
+  Broker& b = *b_;
+  PartitionEntry& P = b.part(fp.pidx);
+  const int64_t delay = P.fetch_delay_ns.load(std::memory_order_relaxed);
+  if (delay > 0) {
+    timespec ts{time_t(delay / 1000000000LL), long(delay % 1000000000LL)};
+    nanosleep(&ts, nullptr);
+  }
+  int32_t errs = P.fetch_errors.load(std::memory_order_relaxed);
+  while (errs > 0) {
+    if (P.fetch_errors.compare_exchange_weak(errs, errs - 1))
+      throw InjectedFetchError("KafkaError: injected fetch failure on partition " + std::to_string(fp.pidx));
+  }
+  P.fetch_calls.fetch_add(1, std::memory_order_relaxed);
+  if (!has_data(fp)) return 0;
+  const int64_t hw = P.high_watermark.load(std::memory_order_acquire);
+  const uint8_t* log = b.log_base(fp.pidx);
+  const IndexEntry* idx = b.index_base(fp.pidx);
+  size_t taken = 0;
+  uint64_t bytes = 0;
+  while (taken < max_records && fp.position < hw) {
+    const int64_t bi = b.find_batch(fp.pidx, fp.position, fp.batch_hint);
+    fp.batch_hint = bi;
+    const IndexEntry e = idx[bi];
+    const uint8_t* bp = log + e.pos;
+    const BatchHeader h = parse_batch_header(bp, e.size);
+    if (check_crcs_ && fp.verified_base != h.base_offset) {
+      if (!verify_batch_crc(bp, h))
+        throw CorruptRecord("Record batch at offset " + std::to_string(h.base_offset) + " failed CRC check");
+      fp.verified_base = h.base_offset;
+    }
+    bytes += e.size;
+    RecordIter it(bp, h);
+    RecordView r;
+    while (it.next(&r)) {
+      if (r.offset < fp.position) continue;
+      const int act = visit(r);
+      if (act == kStopBefore) {
+        P.bytes_fetched.fetch_add(bytes, std::memory_order_relaxed);
+        return taken;
+      }
+      fp.position = r.offset + 1;
+      ++taken;
+      if (act == kTakeStop || taken >= max_records) {
+        P.bytes_fetched.fetch_add(bytes, std::memory_order_relaxed);
+        return taken;
+      }
+    }
+    if (fp.position < h.next_offset()) fp.position = h.next_offset();
+  }
+  P.bytes_fetched.fetch_add(bytes, std::memory_order_relaxed);
+  return taken;
+}
+
+}  // namespace tk

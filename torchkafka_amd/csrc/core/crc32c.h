@@ -1,0 +1,18 @@
+// CRC32C (Castagnoli) as used by Kafka RecordBatch v2 (the `crc` field covers
+// attributes .. end of batch).  Hardware path: SSE4.2 `crc32` with three
+// interleaved streams combined by GF(2) shifting; portable slicing-by-8 table
+// fallback when the CPU lacks SSE4.2.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+
+namespace tk {
+
+// crc32c(data) with the standard init/final xor (0xFFFFFFFF).
+uint32_t crc32c(const void* data, size_t n);
+// Continue a running crc (value as returned by crc32c over a prefix).
+uint32_t crc32c_extend(uint32_t crc, const void* data, size_t n);
+// True if the hardware (SSE4.2) path is in use.
+bool crc32c_hw();
+
+}  // namespace tk

@@ -1,0 +1,106 @@
+// pybind11 bindings of the device half: module `torchkafka_amd._tkhip`.
+// Tensors cross the boundary as raw device pointers (Tensor.data_ptr()) and
+// streams as hipStream_t handles (torch.cuda.Stream.cuda_stream), so the
+// module does not link against libtorch and builds with plain hipcc.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "collate.h"
+#include "dtypes.h"
+#include "engine.h"
+
+namespace py = pybind11;
+using namespace tkh;
+
+namespace {
+template <typename T>
+T* ptr(uintptr_t p) { return reinterpret_cast<T*>(p); }
+hipStream_t stream_of(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+}  // namespace
+
+PYBIND11_MODULE(_tkhip, m) {
+  m.doc() = "torchkafka_amd gfx950 device path: H2D engine + collate kernels";
+
+  m.def("device_info", [](int dev) {
+    hipDeviceProp_t p;
+    hipError_t e = hipGetDeviceProperties(&p, dev);
+    if (e != hipSuccess) throw std::runtime_error(hipGetErrorString(e));
+    py::dict d;
+    d["name"] = std::string(p.name);
+    d["gcn_arch"] = std::string(p.gcnArchName);
+    d["cus"] = p.multiProcessorCount;
+    d["warp_size"] = p.warpSize;
+    d["total_mem"] = p.totalGlobalMem;
+    d["lds_per_block"] = p.sharedMemPerBlock;
+    return d;
+  });
+
+  m.def(
+      "collate_fixed",
+      [](uintptr_t src, int src_dt, uintptr_t dst, int dst_dt, int64_t rows, int64_t row, uintptr_t shift,
+         uintptr_t scale, uintptr_t stream) {
+        launch_fixed(ptr<const void>(src), src_dt, ptr<void>(dst), dst_dt, rows, row, ptr<const float>(shift),
+                     ptr<const float>(scale), stream_of(stream));
+      },
+      py::arg("src"), py::arg("src_dtype"), py::arg("dst"), py::arg("dst_dtype"), py::arg("rows"), py::arg("row"),
+      py::arg("shift") = 0, py::arg("scale") = 0, py::arg("stream") = 0);
+
+  m.def(
+      "collate_varlen",
+      [](uintptr_t offs, uintptr_t vals, int src_dt, uintptr_t out, int dst_dt, int64_t rows, int64_t L, double pad,
+         uintptr_t lengths, uintptr_t mask, uintptr_t stream) {
+        launch_varlen(ptr<const int32_t>(offs), ptr<const void>(vals), src_dt, ptr<void>(out), dst_dt, rows, L, pad,
+                      ptr<int64_t>(lengths), ptr<uint8_t>(mask), stream_of(stream));
+      },
+      py::arg("offsets"), py::arg("values"), py::arg("src_dtype"), py::arg("out"), py::arg("dst_dtype"),
+      py::arg("rows"), py::arg("L"), py::arg("pad") = 0.0, py::arg("lengths") = 0, py::arg("mask") = 0,
+      py::arg("stream") = 0);
+
+  py::class_<Engine>(m, "Engine")
+      .def(py::init<int, int, size_t>(), py::arg("device"), py::arg("n_slots"), py::arg("staging_bytes"))
+      .def_property_readonly("device", &Engine::device)
+      .def_property_readonly("n_slots", &Engine::n_slots)
+      .def_property_readonly("staging_stride", &Engine::staging_stride)
+      .def_property_readonly("copy_stream", [](Engine& e) { return reinterpret_cast<uintptr_t>(e.copy_stream()); })
+      .def("staging_address", [](Engine& e, int s) { return reinterpret_cast<uintptr_t>(e.staging(s)); })
+      .def("register_host", [](Engine& e, uintptr_t p, size_t n) { e.register_host(ptr<void>(p), n); })
+      .def("unregister_host", &Engine::unregister_host)
+      .def_property_readonly("host_registered", &Engine::host_registered)
+      .def("h2d", [](Engine& e, int s, uintptr_t host, size_t n) { e.h2d(s, ptr<const void>(host), n); })
+      .def("h2d_complete", &Engine::h2d_complete)
+      .def("wait_h2d",
+           [](Engine& e, int s) {
+             py::gil_scoped_release nogil;
+             e.wait_h2d(s);
+           })
+      .def("collate_fixed",
+           [](Engine& e, int s, uintptr_t stream, size_t voff, int src_dt, uintptr_t dst, int dst_dt, int64_t rows,
+              int64_t row, uintptr_t shift, uintptr_t scale) {
+             e.collate_fixed(s, stream_of(stream), voff, src_dt, ptr<void>(dst), dst_dt, rows, row,
+                             ptr<const float>(shift), ptr<const float>(scale));
+           })
+      .def("collate_varlen",
+           [](Engine& e, int s, uintptr_t stream, size_t voff, int src_dt, uintptr_t out, int dst_dt, int64_t rows,
+              int64_t L, double pad, uintptr_t lengths, uintptr_t mask) {
+             e.collate_varlen(s, stream_of(stream), voff, src_dt, ptr<void>(out), dst_dt, rows, L, pad,
+                              ptr<int64_t>(lengths), ptr<uint8_t>(mask));
+           })
+      .def("copy_raw",
+           [](Engine& e, int s, uintptr_t stream, size_t off, uintptr_t dst, size_t n) {
+             e.copy_raw(s, stream_of(stream), off, ptr<void>(dst), n);
+           })
+      .def("synchronize", [](Engine& e) {
+        py::gil_scoped_release nogil;
+        e.synchronize();
+      });
+
+  m.attr("F32") = int(kF32);
+  m.attr("F16") = int(kF16);
+  m.attr("BF16") = int(kBF16);
+  m.attr("FP8E4M3") = int(kFP8E4M3);
+  m.attr("U8") = int(kU8);
+  m.attr("I8") = int(kI8);
+  m.attr("I32") = int(kI32);
+  m.attr("I64") = int(kI64);
+}

@@ -1,0 +1,20 @@
+// Host-side launchers of the gfx950 collate kernels (collate.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace tkh {
+
+// Dense [rows, row] -> [rows, row] cast with optional fused (x - shift) * scale.
+void launch_fixed(const void* src, int src_dt, void* dst, int dst_dt, int64_t rows, int64_t row, const float* shift,
+                  const float* scale, hipStream_t stream);
+
+// CSR (int32 offsets[rows+1] in elements, values 16B-aligned) -> padded
+// [rows, L] with `pad`; optional int64 lengths[rows] and uint8 mask[rows, L].
+void launch_varlen(const int32_t* offs, const void* vals, int src_dt, void* out, int dst_dt, int64_t rows, int64_t L,
+                   double pad, int64_t* lengths, uint8_t* mask, hipStream_t stream);
+
+}  // namespace tkh

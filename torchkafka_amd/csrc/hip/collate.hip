@@ -1,0 +1,265 @@
+// CDNA4 (gfx950) collate kernels: the device half of the batch collate that
+// the reference leaves to torch's CPU `default_collate`.
+//
+// Both kernels are HBM/L2-bandwidth-bound element-wise work; the design
+// follows the memory-bound playbook of cdna_hip_programming.md:
+//   * 64-wide waves, 256-thread blocks, 16-byte-per-lane global accesses
+//     (Guideline 13) and grid-stride loops capped at ~2048 blocks (Guideline 11);
+//   * conversions bit-exact with torch (dtypes.h), optional per-feature affine
+//     normalisation fused into the same pass (no second read of the batch);
+//   * the variable-length pad kernel stages each row chunk through LDS with
+//     aligned 16-byte loads, so unaligned CSR row starts never turn into
+//     narrow global loads, and reads LDS through a padded layout (one dword
+//     of padding per 32 bytes) that keeps the per-lane 8-element reads free
+//     of bank conflicts (MI355X_MICROARCH.md §LDS: ds_read_b32 banks (a/4)%32).
+#include <hip/hip_runtime.h>
+
+#include "collate.h"
+#include "dtypes.h"
+
+namespace tkh {
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kEPT = 8;                   // elements per thread
+constexpr int kChunk = kThreads * kEPT;   // var-len: output elements per block
+
+template <typename T, int N>
+struct alignas(sizeof(T) * N >= 16 ? 16 : sizeof(T) * N) Vec {
+  T v[N];
+};
+
+// ---------------------------------------------------------------- conversion
+template <typename S, typename D, bool IntPath>
+struct Conv;
+
+template <typename S, typename D>
+struct Conv<S, D, false> {  // float destination
+  __device__ __forceinline__ static D apply(S s, float shift, float scale, bool affine) {
+    float x = to_f32<S>(s);
+    if (affine) x = (x - shift) * scale;
+    return Store<D>::cvt(x);
+  }
+};
+template <typename S, typename D>
+struct Conv<S, D, true> {  // integer destination (token ids etc.)
+  __device__ __forceinline__ static D apply(S s, float, float, bool) { return D(int64_t(s)); }
+};
+
+template <typename D> struct IsIntDst { static constexpr bool value = false; };
+template <> struct IsIntDst<int32_t> { static constexpr bool value = true; };
+template <> struct IsIntDst<int64_t> { static constexpr bool value = true; };
+template <> struct IsIntDst<uint8_t> { static constexpr bool value = true; };
+
+// ---------------------------------------------------------------- fixed width
+// dst[i] = conv(src[i]) over a dense [rows, D] block; vector path needs
+// D % 8 == 0 and both pointers 16-byte aligned (checked on the host).
+template <typename S, typename D, bool AFFINE>
+__global__ __launch_bounds__(kThreads) void fixed_vec_kernel(const S* __restrict__ src, D* __restrict__ dst,
+                                                             int64_t n_groups, int64_t row, const float* __restrict__ shift,
+                                                             const float* __restrict__ scale) {
+  using C = Conv<S, D, IsIntDst<D>::value>;
+  const int64_t stride = int64_t(gridDim.x) * kThreads;
+  for (int64_t g = int64_t(blockIdx.x) * kThreads + threadIdx.x; g < n_groups; g += stride) {
+    const int64_t e = g * kEPT;
+    const Vec<S, kEPT> in = *reinterpret_cast<const Vec<S, kEPT>*>(src + e);
+    Vec<D, kEPT> out;
+    if constexpr (AFFINE) {
+      const int64_t d = e % row;
+      const Vec<float, kEPT> sh = *reinterpret_cast<const Vec<float, kEPT>*>(shift + d);
+      const Vec<float, kEPT> sc = *reinterpret_cast<const Vec<float, kEPT>*>(scale + d);
+#pragma unroll
+      for (int k = 0; k < kEPT; ++k) out.v[k] = C::apply(in.v[k], sh.v[k], sc.v[k], true);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kEPT; ++k) out.v[k] = C::apply(in.v[k], 0.f, 1.f, false);
+    }
+    *reinterpret_cast<Vec<D, kEPT>*>(dst + e) = out;
+  }
+}
+
+template <typename S, typename D, bool AFFINE>
+__global__ __launch_bounds__(kThreads) void fixed_scalar_kernel(const S* __restrict__ src, D* __restrict__ dst,
+                                                                int64_t n, int64_t row, const float* __restrict__ shift,
+                                                                const float* __restrict__ scale) {
+  using C = Conv<S, D, IsIntDst<D>::value>;
+  const int64_t stride = int64_t(gridDim.x) * kThreads;
+  for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < n; i += stride) {
+    if constexpr (AFFINE) {
+      const int64_t d = i % row;
+      dst[i] = C::apply(src[i], shift[d], scale[d], true);
+    } else {
+      dst[i] = C::apply(src[i], 0.f, 1.f, false);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- var-len pad
+// Padded LDS byte address: one dword of padding after every 32 bytes.
+__device__ __forceinline__ uint32_t lds_pad(uint32_t b) { return b + ((b >> 5) << 2); }
+
+template <typename S, typename D>
+__global__ __launch_bounds__(kThreads) void varlen_pad_kernel(const int32_t* __restrict__ offs,
+                                                              const uint8_t* __restrict__ vals, D* __restrict__ out,
+                                                              int64_t L, D pad, int64_t* __restrict__ lengths,
+                                                              uint8_t* __restrict__ mask, int vec_store_ok) {
+  using C = Conv<S, D, IsIntDst<D>::value>;
+  constexpr uint32_t kStageBytes = kChunk * sizeof(S) + 32;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kStageBytes + (kStageBytes / 32) * 4 + 16];
+
+  const int64_t r = blockIdx.y;
+  const int64_t c0 = int64_t(blockIdx.x) * kChunk;
+  const int32_t beg = offs[r];
+  const int64_t len = int64_t(offs[r + 1]) - beg;
+  const int64_t nreal = len - c0 < 0 ? 0 : (len - c0 > kChunk ? kChunk : len - c0);
+
+  uint32_t shift_b = 0;
+  if (nreal > 0) {
+    const uint64_t sb = (uint64_t(beg) + uint64_t(c0)) * sizeof(S);
+    const uint64_t ab = sb & ~uint64_t(15);
+    const uint64_t eb = (sb + uint64_t(nreal) * sizeof(S) + 15) & ~uint64_t(15);
+    shift_b = uint32_t(sb - ab);
+    const uint32_t nv = uint32_t((eb - ab) >> 4);
+    for (uint32_t i = threadIdx.x; i < nv; i += kThreads) {
+      const uint4 v = *reinterpret_cast<const uint4*>(vals + ab + (uint64_t(i) << 4));
+      // 16 aligned bytes never straddle a 32-byte padding boundary, but the
+      // padded address is only 4-byte aligned: store dwords, not one b128.
+      uint32_t* d = reinterpret_cast<uint32_t*>(lds + lds_pad(i << 4));
+      d[0] = v.x;
+      d[1] = v.y;
+      d[2] = v.z;
+      d[3] = v.w;
+    }
+  }
+  __syncthreads();
+
+  const int64_t j0 = c0 + int64_t(threadIdx.x) * kEPT;
+  if (j0 >= L) return;
+  Vec<D, kEPT> o;
+#pragma unroll
+  for (int k = 0; k < kEPT; ++k) {
+    const int64_t local = int64_t(threadIdx.x) * kEPT + k;
+    if (local < nreal) {
+      const S s = *reinterpret_cast<const S*>(lds + lds_pad(shift_b + uint32_t(local) * sizeof(S)));
+      o.v[k] = C::apply(s, 0.f, 1.f, false);
+    } else {
+      o.v[k] = pad;
+    }
+  }
+  D* orow = out + r * L;
+  if (vec_store_ok && j0 + kEPT <= L) {
+    *reinterpret_cast<Vec<D, kEPT>*>(orow + j0) = o;
+  } else {
+#pragma unroll
+    for (int k = 0; k < kEPT; ++k)
+      if (j0 + k < L) orow[j0 + k] = o.v[k];
+  }
+  if (mask) {
+    uint8_t* mrow = mask + r * L;
+#pragma unroll
+    for (int k = 0; k < kEPT; ++k)
+      if (j0 + k < L) mrow[j0 + k] = uint8_t((j0 + k) < len);  // j < L already bounds len
+  }
+  if (lengths && blockIdx.x == 0 && threadIdx.x == 0) lengths[r] = len < L ? len : L;
+}
+
+int grid_for(int64_t work_items) {
+  int64_t g = (work_items + kThreads - 1) / kThreads;
+  if (g < 1) g = 1;
+  if (g > 2048) g = 2048;
+  return int(g);
+}
+
+template <typename S, typename D>
+void launch_fixed_t(const void* src, void* dst, int64_t rows, int64_t row, const float* shift, const float* scale,
+                    hipStream_t stream) {
+  const int64_t n = rows * row;
+  if (n == 0) return;
+  const bool affine = shift != nullptr;
+  const bool vec = (row % kEPT == 0) && (reinterpret_cast<uintptr_t>(src) % 16 == 0) &&
+                   (reinterpret_cast<uintptr_t>(dst) % 16 == 0) &&
+                   (!affine || (reinterpret_cast<uintptr_t>(shift) % 16 == 0 && reinterpret_cast<uintptr_t>(scale) % 16 == 0));
+  if (vec) {
+    const int64_t groups = n / kEPT;
+    const int grid = grid_for(groups);
+    if (affine)
+      hipLaunchKernelGGL((fixed_vec_kernel<S, D, true>), dim3(grid), dim3(kThreads), 0, stream,
+                         static_cast<const S*>(src), static_cast<D*>(dst), groups, row, shift, scale);
+    else
+      hipLaunchKernelGGL((fixed_vec_kernel<S, D, false>), dim3(grid), dim3(kThreads), 0, stream,
+                         static_cast<const S*>(src), static_cast<D*>(dst), groups, row, shift, scale);
+  } else {
+    const int grid = grid_for(n);
+    if (affine)
+      hipLaunchKernelGGL((fixed_scalar_kernel<S, D, true>), dim3(grid), dim3(kThreads), 0, stream,
+                         static_cast<const S*>(src), static_cast<D*>(dst), n, row, shift, scale);
+    else
+      hipLaunchKernelGGL((fixed_scalar_kernel<S, D, false>), dim3(grid), dim3(kThreads), 0, stream,
+                         static_cast<const S*>(src), static_cast<D*>(dst), n, row, shift, scale);
+  }
+}
+
+template <typename S, typename D>
+void launch_varlen_t(const int32_t* offs, const void* vals, void* out, int64_t rows, int64_t L, double pad,
+                     int64_t* lengths, uint8_t* mask, hipStream_t stream) {
+  if (rows == 0 || L == 0) {
+    return;
+  }
+  if (rows > 65535) throw std::runtime_error("varlen collate: more than 65535 rows per batch");
+  D padv;
+  if constexpr (IsIntDst<D>::value) padv = D(int64_t(pad)); else padv = Store<D>::cvt(float(pad));
+  const int vec_ok = (L % kEPT == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0);
+  dim3 grid(unsigned((L + kChunk - 1) / kChunk), unsigned(rows));
+  hipLaunchKernelGGL((varlen_pad_kernel<S, D>), grid, dim3(kThreads), 0, stream, offs,
+                     static_cast<const uint8_t*>(vals), static_cast<D*>(out), L, padv, lengths, mask, vec_ok);
+}
+
+#define TK_DISPATCH_DST(S, FN, ...)                                                    \
+  switch (dst_dt) {                                                                    \
+    case kF32: FN<S, float>(__VA_ARGS__); break;                                       \
+    case kF16: FN<S, _Float16>(__VA_ARGS__); break;                                    \
+    case kBF16: FN<S, __bf16>(__VA_ARGS__); break;                                     \
+    case kFP8E4M3: FN<S, fp8e4m3>(__VA_ARGS__); break;                                 \
+    case kI32: FN<S, int32_t>(__VA_ARGS__); break;                                     \
+    case kI64: FN<S, int64_t>(__VA_ARGS__); break;                                     \
+    default: throw std::invalid_argument("collate: unsupported destination dtype");    \
+  }
+
+#define TK_DISPATCH_SRC(FN, ...)                                                       \
+  switch (src_dt) {                                                                    \
+    case kF32: TK_DISPATCH_DST(float, FN, __VA_ARGS__) break;                          \
+    case kF16: TK_DISPATCH_DST(_Float16, FN, __VA_ARGS__) break;                       \
+    case kBF16: TK_DISPATCH_DST(__bf16, FN, __VA_ARGS__) break;                        \
+    case kU8: TK_DISPATCH_DST(uint8_t, FN, __VA_ARGS__) break;                         \
+    case kI8: TK_DISPATCH_DST(int8_t, FN, __VA_ARGS__) break;                          \
+    case kI32: TK_DISPATCH_DST(int32_t, FN, __VA_ARGS__) break;                        \
+    case kI64: TK_DISPATCH_DST(int64_t, FN, __VA_ARGS__) break;                        \
+    default: throw std::invalid_argument("collate: unsupported source dtype");         \
+  }
+
+bool is_float_dt(int dt) { return dt == kF32 || dt == kF16 || dt == kBF16 || dt == kFP8E4M3; }
+
+}  // namespace
+
+void launch_fixed(const void* src, int src_dt, void* dst, int dst_dt, int64_t rows, int64_t row, const float* shift,
+                  const float* scale, hipStream_t stream) {
+  if (!is_float_dt(dst_dt) && is_float_dt(src_dt))
+    throw std::invalid_argument("collate: float records cannot be cast to an integer dtype");
+  if (shift && !is_float_dt(dst_dt)) throw std::invalid_argument("collate: normalisation needs a float dtype");
+  TK_DISPATCH_SRC(launch_fixed_t, src, dst, rows, row, shift, scale, stream)
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("fixed collate launch: ") + hipGetErrorString(e));
+}
+
+void launch_varlen(const int32_t* offs, const void* vals, int src_dt, void* out, int dst_dt, int64_t rows, int64_t L,
+                   double pad, int64_t* lengths, uint8_t* mask, hipStream_t stream) {
+  if (!is_float_dt(dst_dt) && is_float_dt(src_dt))
+    throw std::invalid_argument("collate: float records cannot be cast to an integer dtype");
+  if (reinterpret_cast<uintptr_t>(vals) % 16) throw std::invalid_argument("varlen collate: values must be 16B aligned");
+  TK_DISPATCH_SRC(launch_varlen_t, offs, vals, out, rows, L, pad, lengths, mask, stream)
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("varlen collate launch: ") + hipGetErrorString(e));
+}
+
+}  // namespace tkh

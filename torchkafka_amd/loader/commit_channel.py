@@ -1,0 +1,86 @@
+"""Main -> worker commit requests through shared memory (replaces signals for auto_commit).
+
+The reference asks a worker to commit with SIGUSR1 (kafka_dataset.py:235-239)
+and the worker commits its consumer *position*, which already includes every
+prefetched batch (B10/D3); after the stream ends the default action of the
+signal kills the worker (D4).  Here the main process publishes, per worker,
+the cumulative number of that worker's samples the user has finished with;
+the worker maps the count to the consumer positions it recorded when it
+produced that sample and commits exactly those.  Workers acknowledge, so the
+main process can wait for the final commit before tearing workers down.
+"""
+from __future__ import annotations
+
+import time
+from multiprocessing import shared_memory
+
+import numpy as np
+
+_REQ, _ACK, _HDR = 0, 1, 2
+
+
+class CommitChannel:
+    def __init__(self, num_workers: int, batch_size: int):
+        if num_workers < 1 or batch_size < 1:
+            raise ValueError("commit channel needs num_workers >= 1 and batch_size >= 1")
+        self.num_workers = num_workers
+        self.batch_size = batch_size
+        self._shm = shared_memory.SharedMemory(create=True, size=8 * (_HDR + 2 * num_workers))
+        self._owner = True
+        self._arr = np.ndarray((_HDR + 2 * num_workers,), dtype=np.int64, buffer=self._shm.buf)
+        self._arr[:] = 0
+        self._arr[0] = num_workers
+        self._arr[1] = batch_size
+
+    # pickling (spawn workers): re-attach by name, never unlink from a worker
+    def __getstate__(self):
+        return {"name": self._shm.name, "num_workers": self.num_workers, "batch_size": self.batch_size}
+
+    def __setstate__(self, st):
+        self.num_workers = st["num_workers"]
+        self.batch_size = st["batch_size"]
+        self._shm = shared_memory.SharedMemory(name=st["name"])
+        try:  # the creating process owns the segment's lifetime
+            from multiprocessing import resource_tracker
+
+            resource_tracker.unregister(self._shm._name, "shared_memory")  # type: ignore[attr-defined]
+        except Exception:  # noqa: BLE001
+            pass
+        self._owner = False
+        self._arr = np.ndarray((_HDR + 2 * self.num_workers,), dtype=np.int64, buffer=self._shm.buf)
+
+    def _i(self, w: int, which: int) -> int:
+        return _HDR + 2 * w + which
+
+    def request(self, worker: int, samples: int) -> None:
+        self._arr[self._i(worker, _REQ)] = samples
+
+    def requested(self, worker: int) -> int:
+        return int(self._arr[self._i(worker, _REQ)])
+
+    def ack(self, worker: int, samples: int) -> None:
+        self._arr[self._i(worker, _ACK)] = samples
+
+    def acked(self, worker: int) -> int:
+        return int(self._arr[self._i(worker, _ACK)])
+
+    def wait_acks(self, timeout: float = 5.0, alive=None) -> bool:
+        """Waits until every worker acknowledged its latest request; ``alive(w)`` can cut a dead worker short."""
+        deadline = time.monotonic() + timeout
+        while True:
+            pending = [w for w in range(self.num_workers) if self.acked(w) < self.requested(w)
+                       and (alive is None or alive(w))]
+            if not pending:
+                return True
+            if time.monotonic() >= deadline:
+                return False
+            time.sleep(0.001)
+
+    def close(self) -> None:
+        try:
+            self._arr = None
+            self._shm.close()
+            if self._owner:
+                self._shm.unlink()
+        except Exception:  # noqa: BLE001
+            pass

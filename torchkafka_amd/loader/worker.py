@@ -1,0 +1,219 @@
+"""DeviceLoader worker process: consume records and pack batches into pinned ring slots.
+
+One process per worker (forked before the parent touches HIP, or spawned);
+it never initialises the GPU.  Two paths:
+
+* **native** (dataset declares a ``schema`` and the consumer is the synthetic
+  broker's): one ``Fetcher.fill_slot`` call per batch decodes RecordBatches
+  straight out of the broker log, applies the schema's None-skip filter and
+  packs values into the slot; no Python per record.
+* **generic** (any ``_process``): the reference's per-record loop
+  (kafka_dataset.py:156-162) runs unchanged, and the samples are stacked
+  directly into the slot's pinned memory (dense) or written as CSR
+  (variable-length 1-D samples), with per-partition offset watermarks.
+
+Errors are shipped to the main process in a slot marked SLOT_ERROR.
+"""
+from __future__ import annotations
+
+import os
+import random
+import traceback
+
+import numpy as np
+import torch
+
+from ..ops.native import core
+
+_DT_CODE = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.float8_e4m3fn: 3, torch.uint8: 4,
+            torch.int8: 5, torch.int32: 6, torch.int64: 7}
+
+
+class _StopWorker(Exception):
+    pass
+
+
+def _set_worker_info(worker_id: int, num_workers: int, seed: int, dataset) -> None:
+    from torch.utils.data._utils import worker as _w
+
+    _w._worker_info = _w.WorkerInfo(id=worker_id, num_workers=num_workers, seed=seed, dataset=dataset)
+
+
+def worker_main(ring, ring_name: str, worker_id: int, num_workers: int, dataset, worker_init_fn, cfg: dict) -> None:
+    """Entry point of a DeviceLoader worker process."""
+    if ring is None:
+        ring = core().Ring.open(ring_name)
+    ring.set_worker_pid(worker_id, os.getpid())
+    spw = ring.slots_per_worker
+    state = {"i": 0, "g": None}
+    try:
+        torch.set_num_threads(1)
+        seed = int(cfg.get("base_seed", 0)) + worker_id
+        random.seed(seed)
+        torch.manual_seed(seed)
+        np.random.seed(seed % (2**32))
+        _set_worker_info(worker_id, num_workers, seed, dataset)
+        if worker_init_fn is not None:
+            worker_init_fn(worker_id)
+        consumer = getattr(dataset, "_consumer", None)
+        if consumer is None:
+            raise RuntimeError(
+                "DeviceLoader worker has no consumer: build the dataset with placeholder() and pass "
+                "worker_init_fn=YourDataset.init_worker(topic, ...)")
+        dataset._worker_id = worker_id
+        if cfg["sharding"] == "static":
+            topics = sorted(consumer.subscription() or [])
+            if not topics:
+                raise RuntimeError("static sharding needs the consumer to be created with its topics")
+            consumer.assign_shard(topics, cfg["rank"], cfg["world_size"], worker_id, num_workers)
+        if cfg["native"] and getattr(consumer, "_fetcher", None) is not None and dataset.schema is not None:
+            _native_loop(ring, worker_id, spw, consumer, dataset.schema, cfg, state)
+        else:
+            _generic_loop(ring, worker_id, spw, consumer, dataset, cfg, state)
+    except _StopWorker:
+        return
+    except BaseException:  # noqa: BLE001 - everything goes to the main process
+        msg = f"Caught exception in DeviceLoader worker {worker_id} (pid {os.getpid()}):\n{traceback.format_exc()}"
+        try:
+            g = state["g"]
+            if g is None:
+                if not ring.worker_acquire(worker_id, state["i"], 10000):
+                    return
+                g = ring.gslot(worker_id, state["i"])
+            ring.set_slot(g, 0, 0, 0, 0, 0, 0, 0, 0, [])
+            ring.set_error(g, msg)
+            ring.worker_publish(g)
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def _acquire(ring, worker_id: int, state: dict) -> int:
+    if not ring.worker_acquire(worker_id, state["i"], -1):
+        raise _StopWorker
+    g = ring.gslot(worker_id, state["i"])
+    state["g"] = g
+    return g
+
+
+def _publish(ring, worker_id: int, spw: int, state: dict) -> None:
+    ring.worker_publish(state["g"])
+    state["g"] = None
+    state["i"] = (state["i"] + 1) % spw
+
+
+def _consumer_timeout_ms(consumer) -> int:
+    t = getattr(consumer, "config", {}).get("consumer_timeout_ms", float("inf"))
+    return -1 if t == float("inf") else int(t)
+
+
+def _native_loop(ring, worker_id, spw, consumer, schema, cfg, state) -> None:
+    from ..client.errors import OffsetOutOfRangeError
+
+    kind, elem, row_elems, min_len, max_len, trunc, skip_bad = schema.native_spec()
+    bs = int(cfg["batch_size"])
+    timeout = _consumer_timeout_ms(consumer)
+    fetcher = consumer._fetcher
+    if not fetcher.assigned() and cfg["sharding"] == "static":
+        g = _acquire(ring, worker_id, state)  # nothing to read, ever: end of stream right away
+        ring.set_slot(g, 0, core().SLOT_EOS, kind, 0, 0, 0, 0, 0, [])
+        _publish(ring, worker_id, spw, state)
+        return
+    while True:
+        g = _acquire(ring, worker_id, state)
+        consumer._ensure_group()
+        while True:
+            try:
+                rows, _scanned, timed_out, shut = fetcher.fill_slot(ring, g, kind, elem, row_elems, min_len,
+                                                                    max_len, trunc, skip_bad, bs, timeout)
+                break
+            except OffsetOutOfRangeError:
+                # retention moved past a position: reset it like the consumer would and refill this slot
+                b = consumer._b
+                for p in fetcher.assigned():
+                    pos = fetcher.position(p)
+                    if not b.log_start_offset(p) <= pos <= b.high_watermark(p):
+                        fetcher.seek(p, consumer._reset_position(p))
+        if shut:
+            raise _StopWorker
+        if timed_out:
+            ring.set_flags(g, core().SLOT_EOS)
+        _publish(ring, worker_id, spw, state)
+        if timed_out:
+            return
+
+
+def _generic_loop(ring, worker_id, spw, consumer, dataset, cfg, state) -> None:
+    bs = int(cfg["batch_size"])
+    broker = getattr(consumer, "_broker", None)
+    cap = ring.payload_capacity
+    samples: list = []
+    wm: dict = {}  # pidx -> [first, next, count]
+    first_pos: dict = {}
+
+    def pidx_of(rec):
+        if broker is None:
+            raise RuntimeError("DeviceLoader's generic path needs the synthetic-broker consumer")
+        return broker.pidx(rec.topic, rec.partition)
+
+    def flush(eos: bool) -> None:
+        g = _acquire(ring, worker_id, state)
+        view = ring.payload_view(g)
+        wms = [(p, v[0], v[1], v[2]) for p, v in wm.items()]
+        if samples:
+            s0 = samples[0]
+            if not isinstance(s0, torch.Tensor):
+                raise TypeError(f"DeviceLoader samples must be tensors, got {type(s0).__name__}")
+            dt = s0.dtype
+            code = _DT_CODE.get(dt)
+            if code is None:
+                raise TypeError(f"unsupported sample dtype {dt}")
+            same = all(s.shape == s0.shape and s.dtype == dt for s in samples)
+            esize = s0.element_size()
+            if same:
+                nbytes = len(samples) * s0.numel() * esize
+                if nbytes > cap:
+                    raise RuntimeError(f"batch of {nbytes} bytes exceeds the ring slot ({cap}); raise slot_bytes")
+                dst = torch.frombuffer(view, dtype=dt, count=len(samples) * s0.numel()).view(len(samples), *s0.shape)
+                torch.stack(samples, out=dst)
+                ring.set_slot(g, len(samples), core().SLOT_EOS if eos else 0, core().PACK_FIXED, nbytes, 0,
+                              s0.numel(), len(samples) * s0.numel(), len(samples), wms)
+                ring.set_slot_sample(g, code, list(s0.shape))
+            else:
+                if any(s.dim() != 1 or s.dtype != dt for s in samples):
+                    raise TypeError("DeviceLoader needs equal-shape samples or 1-D variable-length samples")
+                n = len(samples)
+                voff = (4 * (n + 1) + 255) // 256 * 256
+                lens = [s.numel() for s in samples]
+                total = sum(lens)
+                nbytes = voff + total * esize
+                if nbytes > cap:
+                    raise RuntimeError(f"batch of {nbytes} bytes exceeds the ring slot ({cap}); raise slot_bytes")
+                offs = torch.frombuffer(view, dtype=torch.int32, count=n + 1)
+                offs[0] = 0
+                offs[1:] = torch.tensor(lens, dtype=torch.int64).cumsum(0).to(torch.int32)
+                vals = torch.frombuffer(view, dtype=dt, count=total, offset=voff)
+                torch.cat(samples, out=vals)
+                ring.set_slot(g, n, core().SLOT_EOS if eos else 0, core().PACK_VARLEN, nbytes, voff, max(lens),
+                              total, n, wms)
+                ring.set_slot_sample(g, code, [])
+        else:
+            ring.set_slot(g, 0, core().SLOT_EOS if eos else 0, 0, 0, 0, 0, 0, 0, wms)
+        _publish(ring, worker_id, spw, state)
+        samples.clear()
+        wm.clear()
+
+    for record in consumer:
+        p = pidx_of(record)
+        ent = wm.get(p)
+        if ent is None:
+            ent = wm[p] = [first_pos.get(p, record.offset), record.offset + 1, 0]
+        ent[1] = record.offset + 1
+        ent[2] += 1
+        first_pos[p] = record.offset + 1
+        data = dataset._process(record)
+        if data is None:
+            continue
+        samples.append(data)
+        if len(samples) == bs:
+            flush(False)
+    flush(True)

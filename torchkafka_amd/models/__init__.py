@@ -1,0 +1,5 @@
+"""Dataset classes: the reference's KafkaDataset plus declarative record schemas."""
+from .kafka_dataset import KafkaDataset
+from .schema import FixedWidth, JsonArray, VarLen
+
+__all__ = ["KafkaDataset", "FixedWidth", "VarLen", "JsonArray"]

@@ -1,0 +1,280 @@
+"""KafkaDataset: an IterableDataset streaming Kafka records (reference R1-R12).
+
+Behaviour-compatible with ``src/kafka_dataset.py`` of Bendabir/torch-kafka:
+same constructor/placeholder/new_consumer/init_worker/commit/commit_worker/
+close API, same error types and messages (B2, B3, B5, B12, B13, B22), same
+log messages and levels on logger ``torchkafka.kafka_dataset``,
+same forced ``enable_auto_commit=False`` (B1), same None-skip (B6) and the
+same POSIX-signal commit protocol for users who call ``commit_worker``.
+
+Deliberate fixes, each covered by a test:
+  D3  exact multi-worker commits: with :func:`auto_commit` the main process
+      tells each worker how many of its samples the user has finished
+      (shared-memory commit channel) and the worker commits the consumer
+      positions recorded at that sample, not its prefetched position;
+  D4  the commit handler stays installed after the stream ends, so a late
+      commit request can no longer kill the worker with SIGUSR1;
+  D6  ``init_worker`` returns a picklable object (works under spawn);
+  D7  using a forked consumer in a worker raises a clear error;
+  D8  commit requests are applied while the consumer idles on empty partitions.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import signal
+import sys
+import threading
+from collections import deque
+
+from torch.utils.data import IterableDataset, get_worker_info
+
+from ..client.errors import COMMIT_FAILED_ERRORS
+from ..client.records import OffsetAndMetadata, TopicPartition
+
+_logger = logging.getLogger("torchkafka.kafka_dataset")
+
+
+def _platform_commit_signal():
+    # kafka_dataset.py:47-55 -- SIGUSR1 on Linux; SIGINT on macOS/Windows; anything else is unsupported.
+    if sys.platform in {"linux", "linux2"}:
+        return signal.SIGUSR1
+    if sys.platform in {"darwin", "win32", "win64"}:
+        return signal.SIGINT
+    raise RuntimeError(f"Unsupported platform '{sys.platform}'.")
+
+
+class _WorkerInit:
+    """Picklable ``worker_init_fn`` built by :meth:`KafkaDataset.init_worker` (fixes D6)."""
+
+    def __init__(self, cls, args, kwargs):
+        self.cls, self.args, self.kwargs = cls, args, kwargs
+
+    def __call__(self, worker_id: int) -> None:
+        worker_info = get_worker_info()
+        if worker_info is None:
+            raise RuntimeError("Custom initialization should be used for multiprocessing only.")
+        dataset = worker_info.dataset
+        dataset._consumer = self.cls.new_consumer(*self.args, **self.kwargs)
+        dataset._consumer_pid = os.getpid()
+        dataset._worker_id = worker_id
+
+    def __repr__(self):
+        return f"{self.cls.__name__}.init_worker{self.args!r}"
+
+
+class KafkaDataset(IterableDataset):
+    """PyTorch dataset that streams data from Kafka (single- or multi-process DataLoader).
+
+    Subclass it and implement ``_process(record)`` (return ``None`` to skip a
+    record), or declare ``schema = FixedWidth(...) / VarLen(...) /
+    JsonArray(...)`` to get a default ``_process`` plus the native
+    :class:`~torchkafka_amd.loader.DeviceLoader` fast path.  All constructor
+    arguments go to the Kafka consumer; auto commit is always disabled.
+    """
+
+    _torchkafka_dataset = True  # duck-type marker for auto_commit (fixes D2)
+    _COMMIT_SIGNAL = _platform_commit_signal()
+    schema = None
+
+    def __init__(self, *args, **kwargs):
+        self._worker_id = None
+        self._commit_required = False
+        self._commit_channel = None
+        self._consumer_pid = os.getpid()
+        if kwargs.get("_is_placeholder", False):
+            self._consumer = None
+        else:
+            if len(args) == 0:
+                raise ValueError(
+                    "No topic was provided. "
+                    "Please use the placeholder() method "
+                    "to create a dataset without consumer."
+                )
+            self._consumer = self.new_consumer(*args, **kwargs)
+
+    def __del__(self):
+        self.close()
+
+    def close(self):
+        """Close the Kafka consumer without committing the offsets (B16)."""
+        consumer = getattr(self, "_consumer", None)
+        if consumer is not None and getattr(self, "_consumer_pid", os.getpid()) == os.getpid():
+            consumer.close(autocommit=False)
+        self._commit_required = False
+
+    # ------------------------------------------------------------------ commit protocol
+    def commit(self, signum=None, stack=None):  # pylint: disable=unused-argument
+        """Commit the consumer offsets.  Main process: commit now.  Worker: signal-handler entry point."""
+        if self._consumer is None:
+            raise RuntimeError("Consumer is not initialized.")
+        if self._worker_id is None:
+            self._commit_if_required(force=True)
+        elif signum is not None:
+            if signum != self._COMMIT_SIGNAL:
+                raise ValueError(f"Worker {self._worker_id} received a bad signal ({signum}).")
+            self._commit_required = True
+        else:
+            raise RuntimeError("Direct commit should not be used with multiprocessing.")
+
+    def _do_commit(self, offsets=None) -> bool:
+        if self._worker_id is None:
+            _logger.debug("Committing offsets.")
+        else:
+            _logger.info("Committing offsets on worker %d.", self._worker_id)
+        try:
+            if offsets is None:
+                self._consumer.commit()
+            else:
+                self._consumer.commit(offsets=offsets)
+        except COMMIT_FAILED_ERRORS:
+            if self._worker_id is None:
+                _logger.error("Commit failed.")
+            else:
+                _logger.error("Commit failed on worker %d.", self._worker_id)
+            return False
+        else:
+            if self._worker_id is None:
+                _logger.debug("Committed offsets.")
+            else:
+                _logger.debug("Committed offsets on worker %d.", self._worker_id)
+            return True
+        finally:
+            self._commit_required = False
+
+    def _commit_if_required(self, force: bool = False):
+        if not force and not self._commit_required:
+            return
+        self._do_commit()
+
+    # ------------------------------------------------------------------ exact commit channel (D3/D8)
+    def _service_channel(self) -> None:
+        ch = self._commit_channel
+        if ch is None or self._worker_id is None:
+            return
+        with self._channel_lock:
+            req = ch.requested(self._worker_id)
+            if req <= self._channel_done:
+                return
+            snap = None
+            while self._snapshots and self._snapshots[0][0] <= req:
+                snap = self._snapshots.popleft()
+            if snap is not None:
+                offsets = {TopicPartition(t, p): OffsetAndMetadata(o, "") for (t, p), o in snap[1].items()}
+                if offsets:
+                    self._do_commit(offsets)
+                # a failed commit is logged and not retried, as in the reference (B14)
+                self._channel_done = snap[0]
+            ch.ack(self._worker_id, req)
+
+    def _channel_keepalive(self) -> None:
+        """After the stream ended in a worker: keep serving commit requests (final batch, D4)."""
+        stop = self._channel_stop
+
+        def run():
+            while not stop.wait(0.005):
+                try:
+                    self._service_channel()
+                except Exception:  # noqa: BLE001 - the worker is winding down
+                    _logger.exception("final commit failed on worker %s", self._worker_id)
+                    return
+
+        threading.Thread(target=run, name="torchkafka-final-commit", daemon=True).start()
+
+    # ------------------------------------------------------------------ iteration
+    def __iter__(self):
+        if self._consumer is None:
+            raise RuntimeError("Consumer is not initialized.")
+        in_worker = self._worker_id is not None
+        if not in_worker and get_worker_info() is not None and self._consumer_pid != os.getpid():
+            raise RuntimeError(
+                "This KafkaDataset's consumer was created in the parent process and inherited by a "
+                "DataLoader worker. Use KafkaDataset.placeholder() together with "
+                "worker_init_fn=KafkaDataset.init_worker(...)."
+            )
+        ch = self._commit_channel if in_worker else None
+        if in_worker:
+            signal.signal(self._COMMIT_SIGNAL, self.commit)
+            if ch is not None:
+                if getattr(self, "_channel_stop", None) is not None:
+                    self._channel_stop.set()
+                self._channel_lock = threading.Lock()
+                self._channel_stop = threading.Event()
+                self._snapshots = deque()
+                self._channel_done = 0
+                hooks = getattr(self._consumer, "_idle_hooks", None)
+                if hooks is not None and self._service_channel not in hooks:
+                    hooks.append(self._service_channel)
+        bs = ch.batch_size if ch is not None else 0
+        positions: dict = {}
+        yielded = 0
+        for record in self._consumer:
+            if ch is not None:
+                positions[(record.topic, record.partition)] = record.offset + 1
+            data = self._process(record)
+            if data is not None:
+                yielded += 1
+                if ch is not None and yielded % bs == 0:
+                    with self._channel_lock:
+                        self._snapshots.append((yielded, dict(positions)))
+                yield data
+            if in_worker:
+                self._commit_if_required()
+                if ch is not None:
+                    self._service_channel()
+        if ch is not None:
+            with self._channel_lock:
+                self._snapshots.append((yielded, dict(positions)))
+            self._service_channel()
+            self._channel_keepalive()
+        # D4: the reference resets the handler to SIG_DFL here, so a commit
+        # signal that arrives afterwards kills the worker.  Keep it installed.
+
+    def _process(self, record):
+        """Map a Kafka record to a sample, or ``None`` to skip it."""
+        if self.schema is not None:
+            return self.schema.process(record)
+        raise NotImplementedError()
+
+    # ------------------------------------------------------------------ factories
+    @classmethod
+    def new_consumer(cls, *args, **kwargs):
+        """Build a consumer with auto-commit disabled (B1).  Override to force settings."""
+        if len(args) == 0:
+            raise ValueError("Cannot create a consumer without topic.")
+        kwargs["enable_auto_commit"] = False
+        if "_is_placeholder" in kwargs:
+            del kwargs["_is_placeholder"]
+        return _make_consumer(*args, **kwargs)
+
+    @classmethod
+    def init_worker(cls, *args, **kwargs):
+        """``worker_init_fn`` that gives every DataLoader worker its own consumer."""
+        return _WorkerInit(cls, args, kwargs)
+
+    @classmethod
+    def commit_worker(cls, worker):
+        """Ask a DataLoader worker process to commit its offsets (POSIX signal, B9)."""
+        os.kill(worker.pid, cls._COMMIT_SIGNAL)
+
+    @classmethod
+    def placeholder(cls):
+        """A consumer-less dataset for multi-worker DataLoaders."""
+        return cls(_is_placeholder=True)
+
+
+def _make_consumer(*topics, **kwargs):
+    """Synthetic-broker consumer, or kafka-python's when installed and pointed at a real cluster."""
+    from ..broker.synthetic import is_synthetic_url
+
+    servers = kwargs.get("bootstrap_servers")
+    if not is_synthetic_url(servers) and not os.environ.get("TORCHKAFKA_BROKER"):
+        try:  # pragma: no cover - kafka-python is not installed in this image
+            from kafka import KafkaConsumer as _KP  # type: ignore
+
+            return _KP(*topics, **kwargs)
+        except ImportError:
+            pass
+    from ..client.consumer import KafkaConsumer
+
+    return KafkaConsumer(*topics, **kwargs)

@@ -1,0 +1,114 @@
+"""Batch collate on device (gfx950 HIP kernels) and the matching torch references.
+
+Standalone entry points on device tensors (used by tests and by users who
+already hold CSR/dense batches on the GPU); the DeviceLoader drives the same
+kernels through the H2D engine on its pinned staging buffers.
+"""
+from __future__ import annotations
+
+import torch
+
+from .native import hip
+
+DTYPE_CODE = {
+    torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.float8_e4m3fn: 3, torch.uint8: 4,
+    torch.int8: 5, torch.int32: 6, torch.int64: 7,
+}
+CODE_DTYPE = {v: k for k, v in DTYPE_CODE.items()}
+FLOAT_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float8_e4m3fn)
+
+
+def _code(dt: torch.dtype) -> int:
+    try:
+        return DTYPE_CODE[dt]
+    except KeyError:
+        raise TypeError(f"collate: unsupported dtype {dt}") from None
+
+
+def _stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def normalize_params(normalize, row: int, device) -> tuple[torch.Tensor, torch.Tensor] | None:
+    """(mean, std) -> device (shift, scale) f32 vectors of length ``row`` (scale = 1/std)."""
+    if normalize is None:
+        return None
+    mean, std = normalize
+    mean = torch.as_tensor(mean, dtype=torch.float32).flatten()
+    std = torch.as_tensor(std, dtype=torch.float32).flatten()
+    mean = mean.expand(row) if mean.numel() == 1 else mean
+    std = std.expand(row) if std.numel() == 1 else std
+    if mean.numel() != row or std.numel() != row:
+        raise ValueError(f"normalize mean/std must have 1 or {row} elements")
+    return mean.contiguous().to(device), (1.0 / std).contiguous().to(device)
+
+
+def collate_fixed(src: torch.Tensor, dtype: torch.dtype, normalize=None) -> torch.Tensor:
+    """Casts a dense ``[rows, *shape]`` device batch to ``dtype`` with optional fused (x-mean)/std."""
+    if src.device.type != "cuda":
+        return reference_fixed(src, dtype, normalize)
+    src = src.contiguous()
+    rows = src.shape[0]
+    row = src[0].numel() if rows else 0
+    out = torch.empty(src.shape, dtype=dtype, device=src.device)
+    prm = normalize_params(normalize, row, src.device)
+    shift, scale = (prm[0].data_ptr(), prm[1].data_ptr()) if prm is not None else (0, 0)
+    hip().collate_fixed(src.data_ptr(), _code(src.dtype), out.data_ptr(), _code(dtype), rows, row, shift, scale,
+                        _stream_ptr(src.device))
+    return out
+
+
+def collate_varlen(offsets: torch.Tensor, values: torch.Tensor, dtype: torch.dtype, L: int | None = None,
+                   pad_value: float = 0, return_mask: bool = False):
+    """CSR (``offsets`` int32 [rows+1], ``values`` [nnz]) -> padded ``[rows, L]`` + lengths (+ mask)."""
+    rows = offsets.numel() - 1
+    lens = offsets[1:] - offsets[:-1]
+    if L is None:
+        L = int(lens.max().item()) if rows else 0
+    if values.device.type != "cuda":
+        return reference_varlen(offsets, values, dtype, L, pad_value, return_mask)
+    if offsets.dtype != torch.int32:
+        raise TypeError("offsets must be int32")
+    dev = values.device
+    # the kernel stages 16-byte aligned windows: give it an aligned copy with slack
+    esz = values.element_size()
+    buf = torch.zeros(values.numel() * esz + 64, dtype=torch.uint8, device=dev)
+    buf[: values.numel() * esz].copy_(values.contiguous().view(torch.uint8).flatten())
+    out = torch.empty((rows, L), dtype=dtype, device=dev)
+    lengths = torch.empty(rows, dtype=torch.int64, device=dev)
+    mask = torch.empty((rows, L), dtype=torch.bool, device=dev) if return_mask else None
+    hip().collate_varlen(offsets.contiguous().data_ptr(), buf.data_ptr(), _code(values.dtype), out.data_ptr(),
+                         _code(dtype), rows, L, float(pad_value), lengths.data_ptr(),
+                         mask.data_ptr() if mask is not None else 0, _stream_ptr(dev))
+    return (out, lengths, mask) if return_mask else (out, lengths)
+
+
+# ----------------------------------------------------------------------------- torch references
+def reference_fixed(src: torch.Tensor, dtype: torch.dtype, normalize=None) -> torch.Tensor:
+    if normalize is None:
+        return src.to(dtype)
+    row = src[0].numel() if src.shape[0] else 0
+    prm = normalize_params(normalize, row, src.device)
+    x = src.reshape(src.shape[0], -1).to(torch.float32)
+    x = (x - prm[0]) * prm[1]
+    return x.to(dtype).reshape(src.shape)
+
+
+def reference_varlen(offsets: torch.Tensor, values: torch.Tensor, dtype: torch.dtype, L: int,
+                     pad_value: float = 0, return_mask: bool = False):
+    rows = offsets.numel() - 1
+    offs = offsets.to(torch.int64).cpu()
+    lens = (offs[1:] - offs[:-1]).clamp(max=L)
+    if dtype in FLOAT_DTYPES:
+        out = torch.full((rows, L), float(pad_value), dtype=torch.float32, device=values.device).to(dtype)
+    else:
+        out = torch.full((rows, L), int(pad_value), dtype=torch.int64, device=values.device).to(dtype)
+    for r in range(rows):
+        n = int(lens[r])
+        if n:
+            out[r, :n] = values[int(offs[r]): int(offs[r]) + n].to(dtype)
+    lengths = lens.to(values.device)
+    if return_mask:
+        mask = torch.arange(L, device=values.device)[None, :] < lengths[:, None]
+        return out, lengths, mask
+    return out, lengths

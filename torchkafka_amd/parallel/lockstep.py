@@ -1,0 +1,75 @@
+"""Cross-rank lockstep for streaming DDP.
+
+The reference has no notion of ranks: under torchrun every rank's consumers
+would join one group and run at their own pace, so one rank running out of
+records (or lagging) leaves the others hanging in the next gradient
+all-reduce, and offsets committed by a fast rank describe a step the job as
+a whole never finished.
+
+:class:`Lockstep` makes every loader step a collective decision: each rank
+contributes ``[have_batch, step, -step]`` and one all-reduce(MIN) tells all
+ranks whether *every* rank has a batch for this step (so they continue or
+stop together) and checks that they are on the same step.  Because the
+collective completes only when every rank has reached step k, it is also the
+barrier after which batch k-1's offsets may be committed on every rank.
+
+On ROCm the ``nccl`` backend is RCCL: the 24-byte all-reduce rides xGMI and is
+latency-bound, so it is issued on a private side stream (never behind the
+user's queued compute) and read back through pinned memory.  With ``gloo``
+(CPU tests) the same code runs on host tensors.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class LockstepError(RuntimeError):
+    pass
+
+
+class Lockstep:
+    def __init__(self, group=None, device: torch.device | None = None):
+        if not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("Lockstep needs an initialised torch.distributed process group")
+        self.group = group
+        self.world_size = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        backend = dist.get_backend(group)
+        self.on_device = backend == "nccl"
+        if self.on_device:
+            if device is None or device.type != "cuda":
+                device = torch.device("cuda", torch.cuda.current_device())
+            self.device = device
+            self._stream = torch.cuda.Stream(device=device)
+            self._dev = torch.zeros(3, dtype=torch.int64, device=device)
+            self._h_in = torch.zeros(3, dtype=torch.int64).pin_memory()
+            self._h_out = torch.zeros(3, dtype=torch.int64).pin_memory()
+        else:
+            self.device = torch.device("cpu")
+            self._buf = torch.zeros(3, dtype=torch.int64)
+        self.collectives = 0
+
+    def _allreduce_min(self, a: int, b: int, c: int) -> tuple[int, int, int]:
+        self.collectives += 1
+        if not self.on_device:
+            self._buf[0], self._buf[1], self._buf[2] = a, b, c
+            dist.all_reduce(self._buf, op=dist.ReduceOp.MIN, group=self.group)
+            return int(self._buf[0]), int(self._buf[1]), int(self._buf[2])
+        self._h_in[0], self._h_in[1], self._h_in[2] = a, b, c
+        with torch.cuda.stream(self._stream):
+            self._dev.copy_(self._h_in, non_blocking=True)
+            dist.all_reduce(self._dev, op=dist.ReduceOp.MIN, group=self.group)
+            self._h_out.copy_(self._dev, non_blocking=True)
+        self._stream.synchronize()
+        return int(self._h_out[0]), int(self._h_out[1]), int(self._h_out[2])
+
+    def agree(self, have_batch: bool, step: int) -> bool:
+        """True iff every rank has a batch for ``step``.  Raises if ranks disagree on the step."""
+        have, lo, neg_hi = self._allreduce_min(1 if have_batch else 0, step, -step)
+        if lo != -neg_hi:
+            raise LockstepError(f"ranks are out of step: min step {lo}, max step {-neg_hi} (this rank: {step})")
+        return bool(have)
+
+    def barrier(self) -> None:
+        self._allreduce_min(0, 0, 0)

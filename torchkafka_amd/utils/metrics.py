@@ -1,0 +1,91 @@
+"""Loader metrics: the reference has no timers or counters at all.
+
+Cheap per-batch accounting kept on the hot path (a few integer adds):
+records/bytes delivered, host time spent waiting for a ring slot vs issuing
+the copy+collate, and commit latency samples for p50/p99 reporting.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+
+def percentile(samples, q: float) -> float:
+    if not samples:
+        return float("nan")
+    s = sorted(samples)
+    k = (len(s) - 1) * q / 100.0
+    lo = int(k)
+    hi = min(lo + 1, len(s) - 1)
+    return s[lo] + (s[hi] - s[lo]) * (k - lo)
+
+
+@dataclass
+class LoaderStats:
+    batches: int = 0
+    records: int = 0
+    payload_bytes: int = 0
+    wait_ns: int = 0
+    issue_ns: int = 0
+    commits: int = 0
+    commit_failures: int = 0
+    commit_ns: list = field(default_factory=list)
+    started: float = field(default_factory=time.perf_counter)
+    max_commit_samples: int = 100000
+
+    def record_batch(self, rows: int, nbytes: int, wait_ns: int, issue_ns: int) -> None:
+        self.batches += 1
+        self.records += rows
+        self.payload_bytes += nbytes
+        self.wait_ns += wait_ns
+        self.issue_ns += issue_ns
+
+    def record_commit(self, ns: int) -> None:
+        self.commits += 1
+        if len(self.commit_ns) < self.max_commit_samples:
+            self.commit_ns.append(ns)
+
+    def reset(self) -> None:
+        self.__init__()
+
+    def summary(self) -> dict:
+        el = time.perf_counter() - self.started
+        c_us = [x / 1e3 for x in self.commit_ns]
+        return {
+            "batches": self.batches,
+            "records": self.records,
+            "bytes": self.payload_bytes,
+            "elapsed_s": el,
+            "records_per_s": self.records / el if el > 0 else float("nan"),
+            "host_wait_us_per_batch": self.wait_ns / 1e3 / max(self.batches, 1),
+            "host_issue_us_per_batch": self.issue_ns / 1e3 / max(self.batches, 1),
+            "commits": self.commits,
+            "commit_failures": self.commit_failures,
+            "commit_p50_us": percentile(c_us, 50),
+            "commit_p99_us": percentile(c_us, 99),
+        }
+
+
+class StageTimer:
+    """Named wall-clock stage accumulator (``with timer('h2d'): ...``)."""
+
+    def __init__(self):
+        self.totals: dict[str, float] = {}
+        self.counts: dict[str, int] = {}
+
+    def __call__(self, name: str):
+        timer = self
+
+        class _Ctx:
+            def __enter__(self):
+                self.t = time.perf_counter()
+
+            def __exit__(self, *exc):
+                timer.totals[name] = timer.totals.get(name, 0.0) + time.perf_counter() - self.t
+                timer.counts[name] = timer.counts.get(name, 0) + 1
+
+        return _Ctx()
+
+    def report(self) -> dict:
+        return {k: {"total_s": v, "count": self.counts[k], "mean_us": v / self.counts[k] * 1e6}
+                for k, v in self.totals.items()}
