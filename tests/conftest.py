@@ -34,7 +34,7 @@ def broker():
 
     url = f"shm://tktest-{os.getpid()}-{uuid.uuid4().hex[:8]}"
     b = SyntheticBroker.create(url, log_capacity=64 << 20, index_capacity=1 << 16,
-                               group_initial_rebalance_delay_ms=50)
+                               group_initial_rebalance_delay_ms=300)
     try:
         yield b
     finally:

@@ -1,0 +1,417 @@
+"""Behaviour compatibility with the reference KafkaDataset / auto_commit
+and the deliberate fixes of its defects (§2.7, D1-D8).  CPU only, torch DataLoader paths."""
+import json
+import logging
+import os
+import signal
+import threading
+import time
+
+import pytest
+import torch
+from torch.utils.data import DataLoader
+
+from torchkafka_amd import KafkaDataset, auto_commit
+from torchkafka_amd.client.errors import CommitFailedError, IllegalStateError, NoBrokersAvailable
+
+
+class Rand8(KafkaDataset):
+    """README.md:36-44."""
+
+    def _process(self, record):
+        return torch.rand(8)
+
+
+class OffsetSkip5(KafkaDataset):
+    """Returns the record offset; None for offset % 5 == 4."""
+
+    def _process(self, record):
+        return None if record.offset % 5 == 4 else torch.tensor(record.offset)
+
+
+class PartOffset(KafkaDataset):
+    def _process(self, record):
+        return torch.tensor([record.partition, record.offset])
+
+
+class MinSize(KafkaDataset):
+    """README.md:62-80: extra constructor state that must survive into workers."""
+
+    def __init__(self, min_size: int, *args, **kwargs):
+        self.min_size = min_size
+        super().__init__(*args, **kwargs)
+
+    @classmethod
+    def placeholder(cls, min_size: int):
+        return cls(min_size, _is_placeholder=True)
+
+    def _process(self, record):
+        elements = json.loads(record.value)
+        if len(elements) < self.min_size:
+            return None
+        return torch.tensor(elements[: self.min_size], dtype=torch.float32)
+
+
+def kw(broker, **extra):
+    d = dict(bootstrap_servers=broker.url, group_id="group_1", auto_offset_reset="earliest",
+             consumer_timeout_ms=200)
+    d.update(extra)
+    return d
+
+
+def produce_offsets(broker, topic="topic", n=12, partitions=1):
+    broker.create_topic(topic, partitions)
+    for p in range(partitions):
+        broker.produce(topic, [f"{p}:{i}".encode() for i in range(n)], partition=p)
+
+
+# ------------------------------------------------------------------------------------------ B1-B5
+def test_b1_auto_commit_forced_off(broker):
+    produce_offsets(broker)
+    ds = Rand8("topic", **kw(broker, enable_auto_commit=True))
+    assert ds._consumer.config["enable_auto_commit"] is False
+
+
+def test_b2_no_topic():
+    with pytest.raises(ValueError) as e:
+        Rand8()
+    assert str(e.value) == ("No topic was provided. Please use the placeholder() method "
+                            "to create a dataset without consumer.")
+
+
+def test_b3_new_consumer_without_topic():
+    with pytest.raises(ValueError, match="^Cannot create a consumer without topic.$"):
+        Rand8.new_consumer(bootstrap_servers="shm://x")
+
+
+def test_b4_placeholder_flag_not_forwarded(broker):
+    produce_offsets(broker)
+    # the synthetic consumer rejects unknown configs, so a leaked _is_placeholder would raise
+    c = Rand8.new_consumer("topic", _is_placeholder=False, **kw(broker))
+    assert "_is_placeholder" not in c.config
+
+
+def test_b5_placeholder_has_no_consumer():
+    ds = Rand8.placeholder()
+    with pytest.raises(RuntimeError, match="^Consumer is not initialized.$"):
+        next(iter(ds))
+    with pytest.raises(RuntimeError, match="^Consumer is not initialized.$"):
+        ds.commit()
+
+
+# ------------------------------------------------------------------------------------------ B6-B8
+def test_b6_b7_none_skip_and_commit_timing(broker):
+    produce_offsets(broker, n=12)
+    ds = OffsetSkip5("topic", **kw(broker))
+    dl = DataLoader(ds, batch_size=4)
+    gen = auto_commit(dl)
+    seen, commits = [], []
+    for batch in gen:
+        seen.append(batch.tolist())
+        commits.append(broker.committed("group_1", "topic", 0))
+    # batches [0..3], [5..8], [10, 11]; the commit of batch k happens when k+1 is requested
+    assert seen == [[0, 1, 2, 3], [5, 6, 7, 8], [10, 11]]
+    assert commits == [None, 4, 9]
+    assert broker.committed("group_1", "topic", 0) == 12  # final batch committed at normal end (B8, B27)
+
+
+def test_b8_break_does_not_commit_last_batch(broker):
+    produce_offsets(broker, n=12)
+    ds = OffsetSkip5("topic", **kw(broker))
+    for i, batch in enumerate(auto_commit(DataLoader(ds, batch_size=4))):
+        if i == 1:
+            break
+    assert broker.committed("group_1", "topic", 0) == 4
+
+
+# ------------------------------------------------------------------------------------------ B12-B16
+def test_b12_b13_worker_commit_entry_point(broker):
+    produce_offsets(broker)
+    ds = Rand8("topic", **kw(broker))
+    next(iter(ds))  # join the group and consume a record (in "main" mode)
+    ds._worker_id = 3
+    with pytest.raises(ValueError, match=r"^Worker 3 received a bad signal \(12\).$"):
+        ds.commit(12, None)
+    with pytest.raises(RuntimeError, match="^Direct commit should not be used with multiprocessing.$"):
+        ds.commit()
+    ds.commit(ds._COMMIT_SIGNAL, None)
+    assert ds._commit_required is True
+    ds._commit_if_required()
+    assert ds._commit_required is False
+    assert broker.commit_count("group_1") == 1
+
+
+def test_b14_commit_failed_is_logged_and_swallowed(broker, caplog):
+    produce_offsets(broker, n=8)
+    ds = OffsetSkip5("topic", **kw(broker))
+    broker.inject_commit_failures("group_1", 1)
+    caplog.set_level(logging.DEBUG, logger="torchkafka.kafka_dataset")
+    batches = [b.tolist() for b in auto_commit(DataLoader(ds, batch_size=4))]
+    assert batches == [[0, 1, 2, 3], [5, 6, 7]]
+    msgs = [(r.levelname, r.getMessage()) for r in caplog.records if r.name == "torchkafka.kafka_dataset"]
+    assert ("ERROR", "Commit failed.") in msgs
+    assert ("DEBUG", "Committing offsets.") in msgs and ("DEBUG", "Committed offsets.") in msgs
+    assert broker.committed("group_1", "topic", 0) == 8  # the next commit succeeded
+    # worker wording (B26)
+    caplog.clear()
+    ds._worker_id = 2
+    broker.inject_commit_failures("group_1", 1)
+    ds._commit_if_required(force=True)
+    assert [(r.levelname, r.getMessage()) for r in caplog.records] == [
+        ("INFO", "Committing offsets on worker 2."), ("ERROR", "Commit failed on worker 2.")]
+    assert ds._commit_required is False
+
+
+def test_b15_other_commit_errors_propagate(broker):
+    produce_offsets(broker)
+    ds = Rand8("topic", **kw(broker, group_id=None))
+    with pytest.raises(AssertionError, match="Requires group_id"):
+        for _ in auto_commit(DataLoader(ds, batch_size=4)):
+            pass
+
+
+def test_b16_close_never_commits(broker):
+    produce_offsets(broker)
+    ds = Rand8("topic", **kw(broker))
+    next(iter(DataLoader(ds, batch_size=4)))
+    ds.close()
+    assert broker.committed("group_1", "topic", 0) is None
+
+
+def test_b17_handler_installed_lazily_and_kept(broker):
+    produce_offsets(broker, n=4)
+    ds = Rand8("topic", **kw(broker))
+    ds._worker_id = 0  # simulate a worker in this process
+    sig = ds._COMMIT_SIGNAL
+    old = signal.getsignal(sig)
+    try:
+        signal.signal(sig, signal.SIG_DFL)
+        gen = iter(ds)
+        assert signal.getsignal(sig) == signal.SIG_DFL  # not at iter()
+        next(gen)
+        assert signal.getsignal(sig) == ds.commit  # at the first next()
+        list(gen)
+        assert signal.getsignal(sig) == ds.commit  # D4: not reset to SIG_DFL on exhaustion
+    finally:
+        signal.signal(sig, old)
+
+
+# ------------------------------------------------------------------------------------------ B18-B19, D1-D2
+def test_b18_type_error_is_lazy():
+    gen = auto_commit([1, 2, 3])
+    with pytest.raises(TypeError, match="^A DataLoader must be provided.$"):
+        next(gen)
+
+
+def test_b19_non_kafka_dataset_passthrough():
+    data = list(auto_commit(DataLoader(list(range(10)), batch_size=4)))
+    assert [d.tolist() for d in data] == [[0, 1, 2, 3], [4, 5, 6, 7], [8, 9]]
+
+
+def test_d1_d2_package_importable_and_marker_detection(broker):
+    import torchkafka
+    import torchkafka_amd
+
+    assert torchkafka.KafkaDataset is torchkafka_amd.KafkaDataset
+    assert torchkafka.auto_commit is torchkafka_amd.auto_commit
+
+    class Foreign(torch.utils.data.IterableDataset):
+        """A KafkaDataset-like class from another import path (the D2 situation)."""
+
+        _torchkafka_dataset = True
+
+        def __init__(self):
+            self.commits = 0
+
+        def __iter__(self):
+            yield from (torch.tensor(i) for i in range(8))
+
+        def commit(self):
+            self.commits += 1
+
+    ds = Foreign()
+    list(auto_commit(DataLoader(ds, batch_size=4)))
+    assert ds.commits == 2
+
+
+# ------------------------------------------------------------------------------------------ multi-worker
+def test_b21_workers_are_group_members_exactly_once(broker):
+    produce_offsets(broker, n=20, partitions=4)
+    ds = PartOffset.placeholder()
+    dl = DataLoader(ds, batch_size=5, num_workers=2,
+                    worker_init_fn=PartOffset.init_worker("topic", **kw(broker, consumer_timeout_ms=500)))
+    rows = torch.cat([b for b in auto_commit(dl)]).tolist()
+    assert sorted(map(tuple, rows)) == [(p, o) for p in range(4) for o in range(20)]
+    assert broker.committed_offsets("group_1", "topic") == {p: 20 for p in range(4)}
+
+
+def test_d3_exact_commit_with_prefetch(broker):
+    """Reference: after the user consumed offsets 0..3, worker 0 committed position 12 (B10, X2)."""
+    produce_offsets(broker, n=24, partitions=2)
+    ds = PartOffset.placeholder()
+    dl = DataLoader(ds, batch_size=4, num_workers=2, prefetch_factor=2,
+                    worker_init_fn=PartOffset.init_worker("topic", **kw(broker, consumer_timeout_ms=1000)))
+    gen = auto_commit(dl)
+    first = next(gen)
+    p = int(first[0, 0])
+    second = next(gen)  # the user finished `first`: its worker commits exactly through it
+    deadline = time.time() + 5
+    while broker.committed("group_1", "topic", p) is None and time.time() < deadline:
+        time.sleep(0.005)
+    assert broker.committed("group_1", "topic", p) == int(first[-1, 1]) + 1 == 4
+    rest = [second] + list(gen)
+    total = torch.cat([first] + rest)
+    assert total.shape[0] == 48
+    assert broker.committed_offsets("group_1", "topic") == {0: 24, 1: 24}
+
+
+def test_d4_d5_uneven_workers_no_signal_death(broker):
+    """Worker 0 runs dry early: attribution stays right and no worker is killed (reference D4/D5)."""
+    broker.create_topic("topic", 2)
+    broker.produce("topic", [b"x"] * 4, partition=0)
+    broker.produce("topic", [b"y"] * 40, partition=1)
+    ds = PartOffset.placeholder()
+    dl = DataLoader(ds, batch_size=4, num_workers=2,
+                    worker_init_fn=PartOffset.init_worker("topic", **kw(broker, consumer_timeout_ms=700)))
+    out = list(auto_commit(dl))
+    assert sum(b.shape[0] for b in out) == 44
+    assert broker.committed_offsets("group_1", "topic") == {0: 4, 1: 40}
+
+
+def test_d4_commit_worker_signal_after_stream_end_is_harmless(broker):
+    broker.create_topic("topic", 2)
+    broker.produce("topic", [b"x"] * 4, partition=0)
+    broker.produce("topic", [b"y"] * 400, partition=1)
+    ds = PartOffset.placeholder()
+    dl = DataLoader(ds, batch_size=4, num_workers=2, prefetch_factor=1,
+                    worker_init_fn=PartOffset.init_worker("topic", **kw(broker, consumer_timeout_ms=300)))
+    it = iter(dl)
+    batches = [next(it) for _ in range(4)]
+    time.sleep(0.8)  # the worker owning partition 0 has exhausted its stream by now
+    for w in it._workers:
+        try:
+            KafkaDataset.commit_worker(w)
+        except ProcessLookupError:  # that worker already exited normally
+            pass
+    time.sleep(0.2)
+    # reference: "DataLoader worker (pid ...) is killed by signal: User defined signal 1"
+    assert all(w.is_alive() or w.exitcode == 0 for w in it._workers)
+    rest = list(it)
+    # nothing was committed here, so the exited member's partition is re-read after the rebalance
+    # (Kafka's at-least-once); every record is still delivered
+    assert {tuple(r) for b in batches + rest for r in b.tolist()} == \
+        {(0, o) for o in range(4)} | {(1, o) for o in range(400)}
+
+
+def test_d6_init_worker_picklable_under_spawn(broker):
+    produce_offsets(broker, n=8, partitions=2)
+    ds = PartOffset.placeholder()
+    dl = DataLoader(ds, batch_size=4, num_workers=2, multiprocessing_context="spawn",
+                    worker_init_fn=PartOffset.init_worker("topic", **kw(broker, consumer_timeout_ms=1500)))
+    rows = torch.cat(list(auto_commit(dl)))
+    assert rows.shape[0] == 16
+    assert broker.committed_offsets("group_1", "topic") == {0: 8, 1: 8}
+
+
+def test_d7_forked_consumer_is_an_error(broker):
+    produce_offsets(broker)
+    ds = Rand8("topic", **kw(broker))  # not a placeholder
+    dl = DataLoader(ds, batch_size=4, num_workers=1)
+    with pytest.raises((RuntimeError, IllegalStateError), match="placeholder"):
+        list(dl)
+
+
+def test_d8_commit_applied_while_partition_idle(broker):
+    produce_offsets(broker, n=8)
+    ds = OffsetSkip5.placeholder()
+    dl = DataLoader(ds, batch_size=3, num_workers=1,
+                    worker_init_fn=OffsetSkip5.init_worker("topic", **kw(broker, consumer_timeout_ms=2500)))
+    gen = auto_commit(dl)
+    b1 = next(gen)
+    b2 = next(gen)  # offsets 0,1,2 | 3,5,6 ; record 7 then the stream idles
+    assert b1.tolist() == [0, 1, 2] and b2.tolist() == [3, 5, 6]
+    result = {}
+
+    def pull():
+        result["rest"] = list(gen)  # requests batch 3 -> commit request for b2; blocks while the worker idles
+
+    t = threading.Thread(target=pull)
+    t.start()
+    deadline = time.time() + 2.0
+    while broker.committed("group_1", "topic", 0) != 7 and time.time() < deadline:
+        time.sleep(0.01)
+    committed_while_idle = broker.committed("group_1", "topic", 0)
+    t.join(10)
+    assert committed_while_idle == 7  # reference: only after the next record arrives (B28)
+    assert [b.tolist() for b in result["rest"]] == [[7]]
+    assert broker.committed("group_1", "topic", 0) == 8
+
+
+def test_b22_init_worker_outside_worker():
+    fn = Rand8.init_worker("topic", bootstrap_servers="shm://nowhere")
+    with pytest.raises(RuntimeError, match="^Custom initialization should be used for multiprocessing only.$"):
+        fn(0)
+
+
+def test_b23_worker_init_error_deferred_to_first_batch():
+    ds = Rand8.placeholder()
+    dl = DataLoader(ds, batch_size=4, num_workers=1,
+                    worker_init_fn=Rand8.init_worker("topic", bootstrap_servers="shm://no-such-broker-b23"))
+    with pytest.raises(NoBrokersAvailable):
+        next(iter(dl))
+
+
+def test_b24_subclass_state_survives_into_workers(broker):
+    broker.create_topic("topic", 1)
+    broker.produce("topic", [json.dumps(list(range(n))).encode() for n in (1, 5, 2, 7, 3, 6)])
+    ds = MinSize.placeholder(3)
+    dl = DataLoader(ds, batch_size=2, num_workers=1,
+                    worker_init_fn=MinSize.init_worker("topic", **kw(broker)))
+    rows = torch.cat(list(auto_commit(dl)))
+    assert rows.tolist() == [[0, 1, 2]] * 4
+
+
+def test_b25_collate_of_lists_matches_torch(broker):
+    class Lists(KafkaDataset):
+        def _process(self, record):
+            return json.loads(record.value)
+
+    broker.create_topic("topic", 1)
+    broker.produce("topic", [b"[1, 2]", b"[1, 2]", b"[1, 2]", b"[1]"])
+    ds = Lists("topic", **kw(broker))
+    it = iter(DataLoader(ds, batch_size=3))
+    first = next(it)
+    assert [t.tolist() for t in first] == [[1, 1, 1], [2, 2, 2]]  # transposed list (default_collate)
+    ds2 = Lists("topic", **kw(broker, group_id="other"))
+    with pytest.raises(RuntimeError, match="each element in list of batch should be of equal size"):
+        list(DataLoader(ds2, batch_size=4))
+
+
+def test_platform_signal():
+    import sys
+
+    if sys.platform.startswith("linux"):
+        assert KafkaDataset._COMMIT_SIGNAL == signal.SIGUSR1
+
+
+def test_schema_default_process(broker):
+    from torchkafka_amd import FixedWidth
+
+    class Vec(KafkaDataset):
+        schema = FixedWidth(torch.float32, (4,))
+
+    broker.create_topic("topic", 1)
+    broker.produce("topic", [torch.arange(4, dtype=torch.float32).numpy().tobytes(), None])
+    out = list(auto_commit(DataLoader(Vec("topic", **kw(broker)), batch_size=2)))
+    assert [b.tolist() for b in out] == [[[0.0, 1.0, 2.0, 3.0]]]
+    assert broker.committed("group_1", "topic", 0) == 2
+
+
+def test_readme_rand8_multiprocess(broker):
+    produce_offsets(broker, n=10, partitions=2)
+    dataset = Rand8.placeholder()
+    dataloader = DataLoader(dataset, batch_size=4, num_workers=2,
+                            worker_init_fn=Rand8.init_worker("topic", **kw(broker, consumer_timeout_ms=400)))
+    n = sum(b.shape[0] for b in auto_commit(dataloader))
+    assert n == 20
+    assert broker.committed_offsets("group_1", "topic") == {0: 10, 1: 10}

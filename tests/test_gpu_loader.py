@@ -141,31 +141,6 @@ def test_generic_process_path_on_device(broker):
     assert broker.committed_offsets("g", "t") == {0: 90, 1: 90}
 
 
-def test_lockstep_nccl_world1(broker):
-    import os
-
-    import torch.distributed as dist
-
-    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
-    from torchkafka_amd.parallel import Lockstep
-
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29533")
-    dist.init_process_group("nccl", rank=0, world_size=1)
-    try:
-        lk = Lockstep(device=torch.device("cuda", 0))
-        assert lk.agree(True, 0) and not lk.agree(False, 1)
-        broker.create_topic("t", 2)
-        broker.fill("t", 64, "fixed_f32", size=8)
-        DS = _dataset(FixedWidth(torch.float32, (8,)))
-        dl = DeviceLoader(DS.placeholder(), 16, num_workers=1, device="cuda:0", world_size=1, rank=0,
-                          worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id="g",
-                                                        auto_offset_reset="earliest", consumer_timeout_ms=300))
-        assert sum(x.shape[0] for x in auto_commit(dl)) == 128
-    finally:
-        dist.destroy_process_group()
-
-
 def test_smoke_entry():
     import __graft_entry__
 

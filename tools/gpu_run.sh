@@ -14,12 +14,13 @@ step() {  # step <name> <timeout> <cmd...>
   case $rc in 124|134|137|139) echo "fatal rc=$rc in $name: stopping"; exit $rc;; esac
   return 0
 }
-STEPS=${STEPS:-"build smoke pytest bench prof"}
+STEPS=${STEPS:-"build smoke bench prof nccl pytest"}
 for s in $STEPS; do
   case $s in
     build)  step build 600 python -c "import __graft_entry__ as g; g.build()" ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    pytest) step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    pytest) step pytest_gpu 600 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=150 --timeout-method=thread ;;
+    nccl)   step nccl_probe 120 python tools/nccl_probe.py ;;
     bench)  step bench 600 python bench.py --stats ;;
     bench8) step bench_fp8 600 python bench.py --stats --dtype fp8 ;;
     prof)   (cd /tmp && export TMPDIR=/tmp && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$OLDPWD/bench.py" --steps 200) ;;

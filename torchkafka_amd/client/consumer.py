@@ -179,7 +179,7 @@ class KafkaConsumer:
             self._buffer = deque(r for r in self._buffer if r[0] in keep)
         self._assignment = pidxs
 
-    def _ensure_group(self) -> None:
+    def _ensure_group(self, block: bool = True) -> None:
         """Joins / follows the consumer group (subscription mode).  kafka-python's coordinator poll."""
         if self._manual or not self._subscription:
             return
@@ -208,7 +208,18 @@ class KafkaConsumer:
         if state != _GROUP_STABLE:
             if self._assignment:
                 self._set_assignment([])
-            return
+            # kafka-python joins the group synchronously (ensure_active_group blocks):
+            # wait out the initial rebalance delay instead of returning an empty assignment
+            if not block:
+                return
+            deadline = time.monotonic() + 60.0
+            while state != _GROUP_STABLE and time.monotonic() < deadline:
+                time.sleep(0.005)
+                gen, state, active, assignment = self._b.poll_group(self._g, self._member_slot, self._member_id)
+                if not active:
+                    return self._ensure_group()
+            if state != _GROUP_STABLE:
+                return
         if gen != self._generation:
             self._generation = gen
             old = set(self._assignment)

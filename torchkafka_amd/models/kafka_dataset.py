@@ -25,6 +25,7 @@ import os
 import signal
 import sys
 import threading
+import time
 from collections import deque
 
 from torch.utils.data import IterableDataset, get_worker_info
@@ -167,19 +168,45 @@ class KafkaDataset(IterableDataset):
                 self._channel_done = snap[0]
             ch.ack(self._worker_id, req)
 
-    def _channel_keepalive(self) -> None:
-        """After the stream ended in a worker: keep serving commit requests (final batch, D4)."""
-        stop = self._channel_stop
+    def _start_committer(self) -> None:
+        """Background servicing of commit requests while the generator is suspended.
+
+        A DataLoader worker spends most of its time outside ``__iter__`` (blocked on
+        its index queue once it has prefetched ``prefetch_factor`` batches), where
+        the reference's in-loop check never runs (B9/B28).  The generator holds
+        ``_consumer_lock`` whenever it runs, so this thread only touches the
+        consumer while the generator is suspended or finished.
+        """
+        if getattr(self, "_committer", None) is not None:
+            return
 
         def run():
-            while not stop.wait(0.005):
-                try:
-                    self._service_channel()
-                except Exception:  # noqa: BLE001 - the worker is winding down
-                    _logger.exception("final commit failed on worker %s", self._worker_id)
-                    return
+            while True:
+                time.sleep(0.002)
+                if self._consumer_lock.acquire(blocking=False):
+                    try:
+                        self._service_channel()
+                    except Exception:  # noqa: BLE001 - keep serving; the error is logged
+                        _logger.exception("commit request failed on worker %s", self._worker_id)
+                    finally:
+                        self._consumer_lock.release()
 
-        threading.Thread(target=run, name="torchkafka-final-commit", daemon=True).start()
+        self._committer = threading.Thread(target=run, name="torchkafka-committer", daemon=True)
+        self._committer.start()
+        # A non-persistent DataLoader worker exits right after the main process has
+        # seen its end of stream -- which is after the main process requested the
+        # commit of that worker's last batch.  Serve that request on the way out.
+        import multiprocessing.util as mpu
+
+        self._channel_finalizer = mpu.Finalize(self, KafkaDataset._final_service, args=(self,), exitpriority=100)
+
+    @staticmethod
+    def _final_service(ds) -> None:
+        try:
+            with ds._consumer_lock:
+                ds._service_channel()
+        except Exception:  # noqa: BLE001 - the process is exiting
+            _logger.exception("final commit failed on worker %s", ds._worker_id)
 
     # ------------------------------------------------------------------ iteration
     def __iter__(self):
@@ -195,40 +222,56 @@ class KafkaDataset(IterableDataset):
         ch = self._commit_channel if in_worker else None
         if in_worker:
             signal.signal(self._COMMIT_SIGNAL, self.commit)
-            if ch is not None:
-                if getattr(self, "_channel_stop", None) is not None:
-                    self._channel_stop.set()
-                self._channel_lock = threading.Lock()
-                self._channel_stop = threading.Event()
-                self._snapshots = deque()
-                self._channel_done = 0
-                hooks = getattr(self._consumer, "_idle_hooks", None)
-                if hooks is not None and self._service_channel not in hooks:
-                    hooks.append(self._service_channel)
-        bs = ch.batch_size if ch is not None else 0
+        if ch is None:
+            yield from self._records(in_worker)
+            return
+        if getattr(self, "_consumer_lock", None) is None:
+            self._consumer_lock = threading.Lock()
+            self._channel_lock = threading.Lock()
+        with self._channel_lock:
+            self._snapshots = deque()
+            self._channel_done = 0
+        hooks = getattr(self._consumer, "_idle_hooks", None)
+        if hooks is not None and self._service_channel not in hooks:
+            hooks.append(self._service_channel)
+        self._start_committer()
+        cl = self._consumer_lock
+        bs = ch.batch_size
         positions: dict = {}
         yielded = 0
-        for record in self._consumer:
-            if ch is not None:
+        cl.acquire()
+        try:
+            for record in self._consumer:
                 positions[(record.topic, record.partition)] = record.offset + 1
-            data = self._process(record)
-            if data is not None:
-                yielded += 1
-                if ch is not None and yielded % bs == 0:
-                    with self._channel_lock:
-                        self._snapshots.append((yielded, dict(positions)))
-                yield data
-            if in_worker:
+                data = self._process(record)
+                if data is not None:
+                    yielded += 1
+                    if yielded % bs == 0:
+                        with self._channel_lock:
+                            self._snapshots.append((yielded, dict(positions)))
+                    cl.release()
+                    try:
+                        yield data
+                    finally:
+                        cl.acquire()
                 self._commit_if_required()
-                if ch is not None:
-                    self._service_channel()
-        if ch is not None:
+                self._service_channel()
             with self._channel_lock:
                 self._snapshots.append((yielded, dict(positions)))
             self._service_channel()
-            self._channel_keepalive()
+        finally:
+            cl.release()
         # D4: the reference resets the handler to SIG_DFL here, so a commit
         # signal that arrives afterwards kills the worker.  Keep it installed.
+
+    def _records(self, in_worker: bool):
+        """The reference's record loop (kafka_dataset.py:147-171) without the commit channel."""
+        for record in self._consumer:
+            data = self._process(record)
+            if data is not None:
+                yield data
+            if in_worker:
+                self._commit_if_required()
 
     def _process(self, record):
         """Map a Kafka record to a sample, or ``None`` to skip it."""
