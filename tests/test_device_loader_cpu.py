@@ -1,0 +1,255 @@
+"""DeviceLoader semantics on the CPU device: ring, workers, exact commits, sharding, errors."""
+import os
+
+import pytest
+import torch
+
+from conftest import synth_f32
+from torchkafka_amd import DeviceLoader, FixedWidth, JsonArray, KafkaDataset, VarLen, auto_commit
+from torchkafka_amd.loader import WorkerError
+
+
+class Vec16(KafkaDataset):
+    schema = FixedWidth(torch.float32, (16,))
+
+
+class Vec16Lenient(KafkaDataset):
+    schema = FixedWidth(torch.float32, (16,), skip_bad=True)
+
+
+class Json(KafkaDataset):
+    schema = JsonArray(min_len=3)
+
+
+class Tokens(KafkaDataset):
+    schema = VarLen(torch.int32, max_len=20)
+
+
+class Doubled(KafkaDataset):
+    def _process(self, record):
+        t = torch.frombuffer(bytearray(record.value), dtype=torch.float32)
+        return None if int(t[0]) % 4 == 0 else t * 2
+
+
+class Ragged(KafkaDataset):
+    def _process(self, record):
+        n = int(record.offset % 5)
+        return torch.arange(n, dtype=torch.int64) + record.offset
+
+
+class Crashy(KafkaDataset):
+    def _process(self, record):
+        if record.offset == 5:
+            os._exit(3)
+        return torch.zeros(2)
+
+
+def init(ds_cls, broker, topic="t", group="g", **kw):
+    d = dict(bootstrap_servers=broker.url, group_id=group, auto_offset_reset="earliest", consumer_timeout_ms=250)
+    d.update(kw)
+    return ds_cls.init_worker(topic, **d)
+
+
+def loader(ds_cls, broker, bs, workers=2, topic="t", group="g", consumer_kw=None, **kw):
+    return DeviceLoader(ds_cls.placeholder(), bs, num_workers=workers, device="cpu",
+                        worker_init_fn=init(ds_cls, broker, topic, group, **(consumer_kw or {})), **kw)
+
+
+def check_rows(x):
+    for row in x:
+        o, p = int(row[0]), int(row[1])
+        assert row.tolist() == [synth_f32(p, o, j) for j in range(x.shape[1])]
+
+
+@pytest.mark.parametrize("workers", [1, 2, 4])
+def test_fixed_width_all_records_once(broker, workers):
+    broker.create_topic("t", 4)
+    broker.fill("t", 250, "fixed_f32", size=16, records_per_batch=32)
+    seen = set()
+    for x in auto_commit(loader(Vec16, broker, 64, workers)):
+        assert x.dtype == torch.float32 and x.shape[1] == 16
+        check_rows(x)
+        for o, p in x[:, :2].long().tolist():
+            assert (p, o) not in seen
+            seen.add((p, o))
+    assert len(seen) == 1000
+    assert broker.committed_offsets("g", "t") == {p: 250 for p in range(4)}
+
+
+def test_exact_commit_of_each_finished_batch(broker):
+    broker.create_topic("t", 2)
+    broker.fill("t", 100, "fixed_f32", size=16)
+    dl = loader(Vec16, broker, 20, workers=2, return_info=True, slots_per_worker=4)
+    gen = auto_commit(dl)
+    b1 = next(gen)
+    assert broker.committed_offsets("g", "t") == {0: None, 1: None}  # nothing finished yet
+    next(gen)
+    expect = {pidx: nxt for pidx, _f, nxt, _c in b1.watermarks}
+    got = {broker.pidx("t", p): o for p, o in broker.committed_offsets("g", "t").items() if o is not None}
+    assert got == expect  # exactly batch 1, despite the workers having prefetched further
+    gen.close()  # like a `break`: the second batch is not committed
+    assert {broker.pidx("t", p): o for p, o in broker.committed_offsets("g", "t").items() if o is not None} == expect
+
+
+def test_manual_mode_and_commit(broker):
+    broker.create_topic("t", 1)
+    broker.fill("t", 50, "fixed_f32", size=16)
+    dl = loader(Vec16, broker, 10, workers=1)
+    it = iter(dl)
+    next(it), next(it)
+    assert broker.committed("g", "t", 0) is None  # plain iteration never commits
+    dl.commit()
+    assert broker.committed("g", "t", 0) == 20
+    it.close()
+
+
+def test_resume_from_committed_offsets(broker):
+    broker.create_topic("t", 1)
+    broker.fill("t", 60, "fixed_f32", size=16)
+    gen = auto_commit(loader(Vec16, broker, 10, workers=1))
+    first = [next(gen) for _ in range(3)]
+    gen.close()  # batches 1 and 2 committed, batch 3 not
+    assert broker.committed("g", "t", 0) == 20
+    rest = torch.cat(list(auto_commit(loader(Vec16, broker, 10, workers=1))))
+    assert rest[:, 0].long().tolist() == list(range(20, 60))  # batch 3 is re-delivered (at-least-once)
+    assert torch.equal(first[2], rest[:10])
+
+
+def test_drop_last_and_in_order(broker):
+    broker.create_topic("t", 2)
+    broker.fill("t", 35, "fixed_f32", size=16)
+    xs = list(auto_commit(loader(Vec16, broker, 10, workers=2, drop_last=True, in_order=True)))
+    assert all(x.shape[0] == 10 for x in xs) and len(xs) == 6
+    assert broker.committed_offsets("g", "t") == {0: 35, 1: 35}  # dropped records still consumed
+
+
+def test_bad_record_raises_in_main(broker):
+    broker.create_topic("t", 1)
+    broker.fill("t", 5, "fixed_f32", size=16)
+    broker.produce("t", [b"short"])
+    with pytest.raises(WorkerError, match="does not match the fixed-width schema"):
+        list(loader(Vec16, broker, 4, workers=1))
+
+
+def test_skip_bad_and_nulls_are_skipped_but_committed(broker):
+    broker.create_topic("t", 1)
+    broker.fill("t", 5, "fixed_f32", size=16)
+    broker.produce("t", [b"short", None])
+    broker.fill("t", 3, "fixed_f32", size=16)
+    xs = torch.cat(list(auto_commit(loader(Vec16Lenient, broker, 4, workers=1))))
+    assert xs[:, 0].long().tolist() == [0, 1, 2, 3, 4, 7, 8, 9]
+    assert broker.committed("g", "t", 0) == 10
+
+
+def test_json_min_len_filter(broker):
+    from torchkafka_amd.client import KafkaConsumer
+
+    broker.create_topic("t", 2)
+    broker.fill("t", 80, "json_f32", size=0, max_size=9)
+    rows = {}
+    for x, lens in auto_commit(loader(Json, broker, 16, workers=2, dtype=torch.float32)):
+        assert x.shape[1] % 8 == 0  # pad_multiple
+        for i in range(x.shape[0]):
+            n = int(lens[i])
+            assert n >= 3
+            assert bool((x[i, n:] == 0).all())
+            rows.setdefault(n, []).append(tuple(x[i, :n].tolist()))
+    ref = {}
+    c = KafkaConsumer("t", bootstrap_servers=broker.url, auto_offset_reset="earliest", consumer_timeout_ms=100)
+    for r in c:
+        t = Json.schema.process(r)
+        if t is not None:
+            ref.setdefault(t.numel(), []).append(tuple(t.tolist()))
+    assert {k: sorted(v) for k, v in rows.items()} == {k: sorted(v) for k, v in ref.items()}
+    assert broker.committed_offsets("g", "t") == {0: 80, 1: 80}
+
+
+def test_varlen_tokens_truncate_and_pad(broker):
+    broker.create_topic("t", 1)
+    broker.fill("t", 40, "tokens_i32", size=1, max_size=40)
+    n = 0
+    for x, lens, mask in loader(Tokens, broker, 8, workers=1, dtype=torch.int64, pad_value=-1, return_mask=True):
+        assert x.dtype == torch.int64 and int(lens.max()) <= 20
+        assert torch.equal(mask, torch.arange(x.shape[1])[None, :] < lens[:, None])
+        assert bool((x[~mask] == -1).all())
+        n += x.shape[0]
+    assert n == 40
+
+
+def test_generic_process_path_dense_and_ragged(broker):
+    broker.create_topic("t", 2)
+    broker.fill("t", 40, "fixed_f32", size=8)
+    xs = torch.cat(list(auto_commit(loader(Doubled, broker, 6, workers=2))))
+    assert xs.shape == (60, 8)
+    assert bool(((xs[:, 0] / 2) % 4 != 0).all())
+    assert broker.committed_offsets("g", "t") == {0: 40, 1: 40}
+    total = 0
+    for x, lens in auto_commit(loader(Ragged, broker, 7, workers=1, group="g2")):
+        for i in range(x.shape[0]):
+            n = int(lens[i])
+            off = int(x[i, 0]) if n else None
+            if n:
+                assert x[i, :n].tolist() == list(range(off, off + n))
+        total += x.shape[0]
+    assert total == 80
+
+
+def test_worker_death_is_detected(broker):
+    broker.create_topic("t", 1)
+    broker.fill("t", 20, "fixed_f32", size=2)
+    with pytest.raises(WorkerError, match="exited unexpectedly"):
+        list(loader(Crashy, broker, 4, workers=1))
+
+
+def test_more_workers_than_partitions(broker):
+    broker.create_topic("t", 2)
+    broker.fill("t", 30, "fixed_f32", size=16)
+    xs = torch.cat(list(auto_commit(loader(Vec16, broker, 8, workers=5))))
+    assert xs.shape[0] == 60
+
+
+def test_static_sharding_across_ranks(broker):
+    broker.create_topic("t", 8)
+    broker.fill("t", 20, "fixed_f32", size=16)
+    owned = {}
+    for rank in range(2):
+        dl = loader(Vec16, broker, 16, workers=2, rank=rank, world_size=2, lockstep=False)
+        parts = set()
+        for x in auto_commit(dl):
+            parts |= set(x[:, 1].long().tolist())
+        owned[rank] = parts
+    assert owned[0] == {0, 2, 4, 6} and owned[1] == {1, 3, 5, 7}
+    assert broker.committed_offsets("g", "t") == {p: 20 for p in range(8)}
+
+
+def test_group_sharding_mode(broker):
+    broker.create_topic("t", 4)
+    broker.fill("t", 25, "fixed_f32", size=16)
+    xs = torch.cat(list(loader(Vec16, broker, 10, workers=2, sharding="group", consumer_kw={"consumer_timeout_ms": 600})))
+    assert sorted(map(tuple, xs[:, :2].long().tolist())) == sorted((o, p) for p in range(4) for o in range(25))
+
+
+def test_normalize_and_bf16_on_cpu(broker):
+    broker.create_topic("t", 1)
+    broker.fill("t", 16, "fixed_f32", size=16)
+    mean, std = torch.arange(16.0), torch.full((16,), 2.0)
+    x = torch.cat(list(loader(Vec16, broker, 16, workers=1, normalize=(mean, std))))
+    raw = torch.tensor([[synth_f32(0, o, j) for j in range(16)] for o in range(16)])
+    assert torch.allclose(x, (raw - mean) / std)
+    xb = torch.cat(list(loader(Vec16, broker, 16, workers=1, dtype=torch.bfloat16, group="g3")))
+    assert xb.dtype == torch.bfloat16 and torch.equal(xb, raw.to(torch.bfloat16))
+
+
+def test_stats_and_commit_latency(broker):
+    broker.create_topic("t", 2)
+    broker.fill("t", 64, "fixed_f32", size=16)
+    dl = loader(Vec16, broker, 16, workers=2)
+    list(auto_commit(dl))
+    s = dl.stats.summary()
+    assert s["records"] == 128 and s["batches"] == 8 and s["commits"] >= 8
+    assert s["commit_p99_us"] > 0
+
+
+def test_len_is_undefined(broker):
+    with pytest.raises(TypeError):
+        len(DeviceLoader(Vec16.placeholder(), 4, num_workers=1, device="cpu"))
