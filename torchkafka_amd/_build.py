@@ -95,8 +95,11 @@ def hipcc() -> str:
 
 def build_hip(force: bool = False, verbose: bool = False) -> Path:
     src_dir = CSRC / "hip"
-    srcs = sorted(src_dir.glob("*.hip")) + sorted(src_dir.glob("*.cpp"))
-    deps = srcs + sorted(src_dir.glob("*.h"))
+    core_dir = CSRC / "core"
+    # the main-process step driver embeds the host core (ring, broker) to commit natively
+    core_srcs = [p for p in sorted(core_dir.glob("*.cpp")) if p.name != "bindings.cpp"]
+    srcs = sorted(src_dir.glob("*.hip")) + sorted(src_dir.glob("*.cpp")) + core_srcs
+    deps = srcs + sorted(src_dir.glob("*.h")) + sorted(core_dir.glob("*.h"))
     out = hip_target()
     if not force and out.exists() and out.stat().st_mtime >= _newest(deps):
         return out
@@ -104,16 +107,17 @@ def build_hip(force: bool = False, verbose: bool = False) -> Path:
     obj_dir.mkdir(parents=True, exist_ok=True)
     cc = hipcc()
     flags = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}", "-DNDEBUG",
-             "-Wno-unused-result", *_py_includes(), f"-I{src_dir}"]
+             "-Wno-unused-result", *_py_includes(), f"-I{src_dir}", f"-I{core_dir}"]
     objs, jobs = [], []
     for s in srcs:
-        o = obj_dir / (s.stem + ".o")
+        o = obj_dir / ((("core_" if s.parent == core_dir else "") + s.stem) + ".o")
         objs.append(o)
         lang = ["-x", "hip"] if s.suffix == ".hip" else []
         jobs.append([cc, *flags, *lang, "-c", str(s), "-o", str(o)])
     _compile_all(jobs)
     tmp = out.with_suffix(".tmp.so")
-    _run([cc, "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs), f"-L{ROCM}/lib", "-lamdhip64"])
+    _run([cc, "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs), f"-L{ROCM}/lib", "-lamdhip64",
+          "-lpthread", "-lrt"])
     os.replace(tmp, out)
     if verbose:
         print(f"[torchkafka_amd] built {out.name} for {ARCH}")

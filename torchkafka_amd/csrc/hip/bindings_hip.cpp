@@ -9,6 +9,7 @@
 #include "collate.h"
 #include "dtypes.h"
 #include "engine.h"
+#include "driver.h"
 
 namespace py = pybind11;
 using namespace tkh;
@@ -94,6 +95,79 @@ PYBIND11_MODULE(_tkhip, m) {
         py::gil_scoped_release nogil;
         e.synchronize();
       });
+
+  py::class_<MainDriver>(m, "MainDriver")
+      .def(py::init([](Engine* e, const std::string& ring, const std::string& url, const std::string& group,
+                       int prefetch, bool in_order, int src_dt) {
+             return new MainDriver(e, ring, url, group, prefetch, in_order, src_dt);
+           }),
+           py::keep_alive<1, 2>(), py::arg("engine"), py::arg("ring_name"), py::arg("broker_url"), py::arg("group"),
+           py::arg("prefetch"), py::arg("in_order"), py::arg("default_src_dtype"))
+      .def_property_readonly("can_commit", &MainDriver::can_commit)
+      .def("step_fixed",
+           [](MainDriver& d, uintptr_t stream, int dst_dt, uintptr_t dst, int64_t row, uintptr_t shift,
+              uintptr_t scale, bool auto_commit, int64_t timeout_ms) {
+             int cs = 0;
+             int64_t r;
+             {
+               py::gil_scoped_release nogil;
+               r = d.step_fixed(stream_of(stream), dst_dt, ptr<void>(dst), row, ptr<const float>(shift),
+                                ptr<const float>(scale), auto_commit, timeout_ms, &cs, &d.last);
+             }
+             return py::make_tuple(r, cs);
+           })
+      .def("next_slot",
+           [](MainDriver& d, int64_t timeout_ms) -> py::tuple {
+             int r;
+             {
+               py::gil_scoped_release nogil;
+               r = d.next_slot(timeout_ms, &d.last);
+             }
+             if (r < 0) return py::make_tuple(r);
+             const SlotView& v = d.last;
+             return py::make_tuple(r, v.n_rows, v.kind, v.max_row_len, v.total_elems, v.src_dtype, v.shape,
+                                   v.payload_bytes);
+           })
+      .def("collate_fixed_last",
+           [](MainDriver& d, uintptr_t stream, int dst_dt, uintptr_t dst, int64_t row, uintptr_t shift,
+              uintptr_t scale) {
+             d.collate_fixed(d.last, stream_of(stream), dst_dt, ptr<void>(dst), row, ptr<const float>(shift),
+                             ptr<const float>(scale));
+           })
+      .def("collate_varlen_last",
+           [](MainDriver& d, uintptr_t stream, int dst_dt, uintptr_t out, int64_t L, double pad, uintptr_t lengths,
+              uintptr_t mask) {
+             d.collate_varlen(d.last, stream_of(stream), dst_dt, ptr<void>(out), L, pad, ptr<int64_t>(lengths),
+                              ptr<uint8_t>(mask));
+           })
+      .def("last_watermarks",
+           [](MainDriver& d) {
+             py::list l;
+             for (const auto& w : d.last.wms) l.append(py::make_tuple(w.pidx, w.first_offset, w.next_offset, w.count));
+             return l;
+           })
+      .def("deliver_last", [](MainDriver& d) { d.deliver(d.last); })
+      .def("finish_delivered", &MainDriver::finish_delivered)
+      .def("add_finished",
+           [](MainDriver& d, std::vector<std::tuple<uint32_t, int64_t, int64_t, uint32_t>> wms) {
+             std::vector<tk::Watermark> v;
+             for (auto& w : wms) v.push_back(tk::Watermark{std::get<0>(w), std::get<3>(w), std::get<1>(w), std::get<2>(w)});
+             d.add_finished(v);
+           })
+      .def("commit_pending", &MainDriver::commit_pending)
+      .def("committed", &MainDriver::committed)
+      .def("take_pending", &MainDriver::take_pending)
+      .def("error", &MainDriver::error)
+      .def("worker_done", &MainDriver::worker_done)
+      .def("stats",
+           [](MainDriver& d) {
+             py::dict s;
+             s["commits"] = d.commits();
+             s["commit_failures"] = d.commit_failures();
+             s["commit_ns"] = d.commit_ns();
+             return s;
+           })
+      .def("reset_stats", &MainDriver::reset_stats);
 
   m.attr("F32") = int(kF32);
   m.attr("F16") = int(kF16);

@@ -1,0 +1,183 @@
+#include "driver.h"
+
+#include <algorithm>
+
+namespace tkh {
+
+MainDriver::MainDriver(Engine* engine, const std::string& ring_name, const std::string& broker_url,
+                       const std::string& group, int prefetch, bool in_order, int default_src_dt)
+    : eng_(engine), prefetch_(std::max(0, prefetch)), in_order_(in_order), default_src_dt_(default_src_dt) {
+  ring_ = tk::Ring::open(ring_name);
+  if (int(ring_->n_slots()) > eng_->n_slots()) throw std::invalid_argument("driver: engine has fewer slots than ring");
+  cursor_.assign(ring_->n_workers(), 0);
+  done_.assign(ring_->n_workers(), 0);
+  if (!broker_url.empty() && !group.empty()) {
+    broker_ = std::make_shared<tk::Broker>(broker_url, false, tk::BrokerConfig{});
+    group_ = broker_->group_index(group, true);
+  }
+  commit_ns_.reserve(1 << 16);
+}
+
+MainDriver::~MainDriver() = default;
+
+void MainDriver::release_completed() {
+  if (inflight_.empty()) return;
+  size_t k = 0;
+  for (int64_t g : inflight_) {
+    if (eng_->h2d_complete(int(g)))
+      ring_->main_release(uint32_t(g));
+    else
+      inflight_[k++] = g;
+  }
+  inflight_.resize(k);
+}
+
+int MainDriver::poll_one(bool block, int64_t timeout_ms) {
+  for (;;) {
+    const int64_t g = ring_->main_acquire(cursor_.data(), &rr_, done_.data(), in_order_, block ? timeout_ms : 0);
+    if (g == -2) return -2;
+    if (g < 0) return -1;
+    tk::SlotHeader* h = ring_->slot(uint32_t(g));
+    if (h->flags & tk::kSlotError) {
+      error_.assign(h->err, h->err_len);
+      ring_->main_release(uint32_t(g));
+      return -3;
+    }
+    if (h->flags & tk::kSlotEOS) done_.at(h->worker) = 1;
+    SlotView v;
+    v.g = g;
+    v.n_rows = h->n_rows;
+    v.flags = h->flags;
+    v.kind = h->kind;
+    v.worker = h->worker;
+    v.payload_bytes = h->payload_bytes;
+    v.values_offset = h->values_offset;
+    v.max_row_len = h->max_row_len;
+    v.total_elems = h->total_elems;
+    v.n_scanned = h->n_scanned;
+    v.src_dtype = h->src_dtype >= 0 ? h->src_dtype : default_src_dt_;
+    if (h->src_dtype >= 0) v.shape.assign(h->shape, h->shape + h->ndim);
+    v.wms.assign(h->wm, h->wm + h->n_parts);
+    if (v.n_rows == 0) {
+      // empty (end-of-stream) slot: keep its watermarks in delivery order
+      ring_->main_release(uint32_t(g));
+      if (!v.wms.empty()) {
+        v.g = -1;
+        staged_.push_back(std::move(v));
+        return 1;
+      }
+      if (!block) return 0;
+      continue;
+    }
+    eng_->h2d(int(g), ring_->payload(uint32_t(g)), v.payload_bytes);
+    inflight_.push_back(g);
+    staged_.push_back(std::move(v));
+    return 1;
+  }
+}
+
+int MainDriver::next_slot(int64_t timeout_ms, SlotView* out) {
+  release_completed();
+  for (;;) {
+    // keep `prefetch` batches beyond the one handed out in flight to the device
+    while (int(staged_.size()) < prefetch_ + 1) {
+      int r = poll_one(false, 0);
+      if (r == -3) return -3;
+      if (r <= 0) break;
+    }
+    if (staged_.empty()) {
+      int r = poll_one(true, timeout_ms);
+      if (r < 0) return r;
+      if (r == 0) return -1;
+    }
+    SlotView v = std::move(staged_.front());
+    staged_.pop_front();
+    if (v.g < 0) {  // empty slot: its watermarks ride on the next delivered batch
+      carry_.insert(carry_.end(), v.wms.begin(), v.wms.end());
+      continue;
+    }
+    if (!carry_.empty()) {
+      v.wms.insert(v.wms.begin(), carry_.begin(), carry_.end());
+      carry_.clear();
+    }
+    *out = std::move(v);
+    return 1;
+  }
+}
+
+void MainDriver::collate_fixed(const SlotView& v, hipStream_t stream, int dst_dt, void* dst, int64_t row,
+                               const float* shift, const float* scale) {
+  const int src_dt = v.src_dtype;
+  eng_->collate_fixed(int(v.g), stream, v.values_offset, src_dt, dst, dst_dt, v.n_rows, row, shift, scale);
+}
+
+void MainDriver::collate_varlen(const SlotView& v, hipStream_t stream, int dst_dt, void* out, int64_t L, double pad,
+                                int64_t* lengths, uint8_t* mask) {
+  eng_->collate_varlen(int(v.g), stream, v.values_offset, v.src_dtype, out, dst_dt, v.n_rows, L, pad, lengths, mask);
+}
+
+void MainDriver::deliver(const SlotView& v) { delivered_ = v.wms; }
+
+void MainDriver::add_finished(const std::vector<tk::Watermark>& wms) {
+  for (const auto& w : wms) {
+    auto it = pending_.find(w.pidx);
+    if (it == pending_.end() || w.next_offset > it->second) pending_[w.pidx] = w.next_offset;
+  }
+}
+
+void MainDriver::finish_delivered() {
+  add_finished(delivered_);
+  delivered_.clear();
+}
+
+int MainDriver::commit_pending() {
+  if (pending_.empty()) return 0;
+  if (!broker_) throw std::runtime_error("DeviceLoader cannot commit: no group_id / broker");
+  const int64_t t0 = tk::now_ns();
+  entries_.clear();
+  for (const auto& kv : pending_) entries_.push_back(tk::CommitEntry{kv.first, kv.second, std::string()});
+  int status = 1;
+  try {
+    broker_->commit(group_, -1, 0, 0, entries_);
+    for (const auto& kv : pending_) committed_[kv.first] = kv.second;
+    ++commits_;
+  } catch (const tk::CommitFailed&) {
+    ++commit_failures_;
+    status = -1;
+  }
+  pending_.clear();
+  if (commit_ns_.size() < (1u << 20)) commit_ns_.push_back(tk::now_ns() - t0);
+  return status;
+}
+
+int64_t MainDriver::step_fixed(hipStream_t stream, int dst_dt, void* dst, int64_t row, const float* shift,
+                               const float* scale, bool auto_commit, int64_t timeout_ms, int* commit_status,
+                               SlotView* out) {
+  *commit_status = 0;
+  finish_delivered();  // asking for the next batch finishes the previous one
+  if (auto_commit) *commit_status = commit_pending();
+  int r = next_slot(timeout_ms, out);
+  if (r < 0) return r;
+  collate_fixed(*out, stream, dst_dt, dst, row, shift, scale);
+  delivered_ = out->wms;
+  return out->n_rows;
+}
+
+std::vector<std::pair<uint32_t, int64_t>> MainDriver::committed() const {
+  std::vector<std::pair<uint32_t, int64_t>> v(committed_.begin(), committed_.end());
+  std::sort(v.begin(), v.end());
+  return v;
+}
+
+std::vector<std::pair<uint32_t, int64_t>> MainDriver::take_pending() {
+  std::vector<std::pair<uint32_t, int64_t>> v(pending_.begin(), pending_.end());
+  pending_.clear();
+  return v;
+}
+
+void MainDriver::reset_stats() {
+  commits_ = commit_failures_ = 0;
+  commit_ns_.clear();
+}
+
+}  // namespace tkh

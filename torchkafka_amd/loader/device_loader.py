@@ -73,6 +73,7 @@ class _Run:
         self.ring = core().Ring.create(self.name, L.num_workers, L.slots_per_worker, L._slot_capacity())
         self.procs: list = []
         self.engine = None
+        self.driver = None
         self.payload_addr = [self.ring.payload_address(g) for g in range(self.ring.n_slots)]
         self.staged: deque = deque()       # (g, summary, wms) with H2D issued (or CPU: just acquired)
         self.inflight: list = []           # slots whose H2D may still be reading host memory
@@ -95,6 +96,9 @@ class _Run:
                 self.engine = hip().Engine(L.device.index if L.device.index is not None else torch.cuda.current_device(),
                                            self.ring.n_slots, self.ring.payload_capacity)
                 self.engine.register_host(self.ring.base_address, self.ring.total_bytes)
+                url, group = L._commit_target_url()
+                self.driver = hip().MainDriver(self.engine, self.name, url, group, L.prefetch, L.in_order,
+                                               L._default_src_code())
         except BaseException:
             self.close()
             raise
@@ -103,6 +107,12 @@ class _Run:
     def _check_workers(self) -> None:
         for w, p in enumerate(self.procs):
             if not self.done[w] and not p.is_alive():
+                raise WorkerError(f"DeviceLoader worker {w} (pid {p.pid}) exited unexpectedly "
+                                  f"with exit code {p.exitcode}")
+
+    def _check_workers_native(self) -> None:
+        for w, p in enumerate(self.procs):
+            if not p.is_alive() and not self.driver.worker_done(w):
                 raise WorkerError(f"DeviceLoader worker {w} (pid {p.pid}) exited unexpectedly "
                                   f"with exit code {p.exitcode}")
 
@@ -169,6 +179,7 @@ class _Run:
             if p.is_alive():
                 p.terminate()
                 p.join(timeout=5)
+        self.driver = None
         if self.engine is not None:
             try:
                 self.engine.synchronize()
@@ -278,6 +289,24 @@ class DeviceLoader:
                 servers = servers if servers is not None else cons.config.get("bootstrap_servers")
         return group_id, servers
 
+    def _commit_target_url(self) -> tuple[str, str]:
+        if self._group_id is None or self._servers is None:
+            return "", ""
+        from ..broker.synthetic import resolve_url
+
+        try:
+            return resolve_url(self._servers), str(self._group_id)
+        except Exception:  # noqa: BLE001 - not a synthetic broker: commits go through Python
+            return "", ""
+
+    def _default_src_code(self) -> int:
+        s = self.schema
+        if s is None:
+            return -1
+        if getattr(s, "kind", None) == 2:
+            return DTYPE_CODE[torch.float32]
+        return DTYPE_CODE[s.dtype]
+
     def _slot_capacity(self) -> int:
         if self.slot_bytes is not None:
             return int(self.slot_bytes)
@@ -319,6 +348,9 @@ class DeviceLoader:
                 except BaseException:
                     run.close()
                     raise
+        if run.driver is not None and lock is None and self._fast_path_ok():
+            yield from self._iterate_fast(run, auto_commit)
+            return
         finished = self._pending_wms
         prev = None
         step = 0
@@ -367,8 +399,78 @@ class DeviceLoader:
             return (wms, ev)
         return (wms, None)
 
+    def _fast_path_ok(self) -> bool:
+        s = self.schema
+        return (s is not None and getattr(s, "kind", None) == 0 and self.native and not self.return_info
+                and not self.drop_last and self.commit_on == "host")
+
+    def _iterate_fast(self, run: _Run, auto_commit: bool):
+        """Fixed-width records on the GPU: one native call per batch (slot, H2D, collate, exact commit)."""
+        drv = run.driver
+        s = self.schema
+        B, shape, row = self.batch_size, tuple(s.shape), s.row_elems
+        dst_dt = self._out_dtype(s.dtype)
+        dst_code = DTYPE_CODE[dst_dt]
+        prm = self._norm_params(row)
+        shift, scale = (prm[0].data_ptr(), prm[1].data_ptr()) if prm is not None else (0, 0)
+        dev = self.device
+        stats = self.stats
+        empty = torch.empty
+        debug = _ds_logger.isEnabledFor(logging.DEBUG)
+        completed = False
+        try:
+            while True:
+                t0 = time.perf_counter_ns()
+                out = empty((B, *shape), dtype=dst_dt, device=dev)
+                r, cs = drv.step_fixed(torch.cuda.current_stream(dev).cuda_stream, dst_code, out.data_ptr(), row,
+                                       shift, scale, auto_commit, 100)
+                if cs:
+                    self._log_commit(cs, debug)
+                if r > 0:
+                    stats.batches += 1
+                    stats.records += r
+                    stats.issue_ns += time.perf_counter_ns() - t0
+                    yield out if r == B else out[:r]
+                elif r == -2:
+                    break
+                elif r == -3:
+                    raise WorkerError(drv.error())
+                else:
+                    run._check_workers_native()
+                    if self.timeout > 0 and time.perf_counter_ns() - t0 > self.timeout * 1e9:
+                        raise TimeoutError(f"DeviceLoader timed out after {self.timeout}s waiting for a batch")
+            completed = True
+        finally:
+            if completed and auto_commit:
+                drv.finish_delivered()
+                self._log_commit(drv.commit_pending(), debug)
+            elif not auto_commit:
+                # manual mode: keep every yielded batch committable by DeviceLoader.commit()
+                drv.finish_delivered()
+                pend = drv.take_pending()
+                if pend:
+                    self._pending_wms.append(([(p, 0, o, 0) for p, o in pend], None))
+            self._absorb_driver_stats(drv)
+            run.close()
+
+    def _log_commit(self, status: int, debug: bool) -> None:
+        if status == -1:
+            _ds_logger.error("Commit failed.")
+        elif status == 1 and debug:
+            _ds_logger.debug("Committed offsets.")
+
+    def _absorb_driver_stats(self, drv) -> None:
+        st = drv.stats()
+        self.stats.commits += st["commits"]
+        self.stats.commit_failures += st["commit_failures"]
+        self.stats.commit_ns.extend(st["commit_ns"])
+        self._committed.update(dict(drv.committed()))
+        drv.reset_stats()
+
     def _next_item(self, run: _Run):
         """Returns (batch, watermarks) or None at end of stream."""
+        if run.driver is not None:
+            return self._next_item_driver(run)
         t0 = time.perf_counter_ns()
         if run.engine is not None:
             run.release_completed()
@@ -398,6 +500,64 @@ class DeviceLoader:
             run.carry = []
         self.stats.record_batch(n_rows, summ[2], t1 - t0, time.perf_counter_ns() - t1)
         return batch, wms
+
+    def _next_item_driver(self, run: _Run):
+        drv = run.driver
+        t0 = time.perf_counter_ns()
+        while True:
+            res = drv.next_slot(100)
+            r = res[0]
+            if r == -2:
+                return None
+            if r == -3:
+                raise WorkerError(drv.error())
+            if r == -1:
+                run._check_workers_native()
+                if self.timeout > 0 and time.perf_counter_ns() - t0 > self.timeout * 1e9:
+                    raise TimeoutError(f"DeviceLoader timed out after {self.timeout}s waiting for a batch")
+                continue
+            _, n_rows, kind, max_len, total, src_code, shape, payload_bytes = res
+            wms = drv.last_watermarks()
+            if self.drop_last and n_rows < self.batch_size:
+                run.carry.extend(wms)
+                continue
+            if run.carry:
+                wms = run.carry + wms
+                run.carry = []
+            break
+        t1 = time.perf_counter_ns()
+        src_dt = CODE_DTYPE[src_code]
+        dst_dt = self._out_dtype(src_dt)
+        if (dst_dt in FLOAT_DTYPES) != (src_dt in FLOAT_DTYPES) and src_dt in FLOAT_DTYPES:
+            raise TypeError(f"cannot collate {src_dt} records to {dst_dt}")
+        dev = self.device
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        lengths = mask = None
+        fixed = kind == core().PACK_FIXED
+        if fixed:
+            if not shape:
+                shape = tuple(self.schema.shape)
+            row = int(max_len) if max_len else 1
+            out = torch.empty((n_rows, *shape), dtype=dst_dt, device=dev)
+            prm = self._norm_params(row)
+            shift, scale = (prm[0].data_ptr(), prm[1].data_ptr()) if prm is not None else (0, 0)
+            drv.collate_fixed_last(stream, DTYPE_CODE[dst_dt], out.data_ptr(), row, shift, scale)
+        else:
+            L = self.pad_to if self.pad_to is not None else int(max_len)
+            if self.pad_to is None and self.pad_multiple > 1:
+                L = (L + self.pad_multiple - 1) // self.pad_multiple * self.pad_multiple
+            out = torch.empty((n_rows, L), dtype=dst_dt, device=dev)
+            lengths = torch.empty(n_rows, dtype=torch.int64, device=dev)
+            mask = torch.empty((n_rows, L), dtype=torch.bool, device=dev) if self.return_mask else None
+            drv.collate_varlen_last(stream, DTYPE_CODE[dst_dt], out.data_ptr(), L, float(self.pad_value),
+                                    lengths.data_ptr(), mask.data_ptr() if mask is not None else 0)
+        self.stats.record_batch(n_rows, payload_bytes, t1 - t0, time.perf_counter_ns() - t1)
+        n_rec = sum(w[3] for w in wms)
+        if self.return_info:
+            return KafkaBatch(out, lengths, mask, wms, n_rec), wms
+        if fixed:
+            return out, wms
+        return ((out, lengths, mask) if self.return_mask else (out, lengths)), wms
 
     # ------------------------------------------------------------------ collate
     def _collate(self, run: _Run, g: int, summ, wms):
@@ -515,6 +675,11 @@ class DeviceLoader:
 
     def commit(self) -> None:
         """Commits every batch yielded so far (manual mode)."""
+        run = self._run
+        if run is not None and run.driver is not None and not run.closed:
+            run.driver.finish_delivered()
+            self._log_commit(run.driver.commit_pending(), _ds_logger.isEnabledFor(logging.DEBUG))
+            self._absorb_driver_stats(run.driver)
         self._commit_finished(wait=True)
 
     def committed_offsets(self) -> dict[int, int]:
