@@ -52,6 +52,10 @@ def parse():
     ap.add_argument("--no-crc", action="store_true", help="skip CRC32C verification (kafka-python check_crcs)")
     ap.add_argument("--device", default=None, help="override device (e.g. cpu for a dry run)")
     ap.add_argument("--stats", action="store_true", help="print loader stats to stderr")
+    ap.add_argument("--in-order", action="store_true", help="strict worker round-robin delivery")
+    ap.add_argument("--h2d", default="dma", choices=["dma", "zerocopy"])
+    ap.add_argument("--copy-streams", type=int, default=4)
+    ap.add_argument("--lockstep-depth", type=int, default=2)
     return ap.parse_args()
 
 
@@ -101,6 +105,7 @@ def main() -> int:
     loader = DeviceLoader(
         Records.placeholder(), B, num_workers=args.workers, device=device, dtype=dtype,
         slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
+        in_order=args.in_order, h2d=args.h2d, copy_streams=args.copy_streams, lockstep_depth=args.lockstep_depth,
         worker_init_fn=Records.init_worker("bench", bootstrap_servers=url, group_id="bench",
                                            auto_offset_reset="earliest", check_crcs=not args.no_crc),
     )
@@ -120,7 +125,7 @@ def main() -> int:
     for _ in range(max(0, args.warmup - 1)):
         x = next(it)
     sync()
-    loader.stats.reset()
+    loader.reset_stats()
     t0 = time.perf_counter()
     rows = 0
     for _ in range(args.steps):
@@ -128,7 +133,7 @@ def main() -> int:
         rows += x.shape[0]
     sync()
     elapsed = time.perf_counter() - t0
-    stats = loader.stats.summary()
+    stats = loader.stats_summary()
 
     # whole-job aggregate: records of every rank over the slowest rank's time
     if world > 1:
@@ -176,6 +181,7 @@ def main() -> int:
                 "partitions": n_parts,
                 "num_workers": args.workers,
                 "commit": "auto_commit per batch" + (", RCCL lockstep" if world > 1 else ""),
+                "h2d": args.h2d,
                 "bytes_per_step_per_gpu": B * args.dim * 4,
                 "gb_per_s": round(value * args.dim * 4 / 1e9, 3),
                 "commit_p99_us": round(stats["commit_p99_us"], 2),

@@ -45,6 +45,41 @@ def test_fixed_f32_exact_records_and_commits(broker, workers):
     assert broker.committed_offsets("g", "t") == {p: 300 for p in range(6)}
 
 
+@pytest.mark.parametrize("h2d,streams", [("dma", 1), ("dma", 4), ("zerocopy", 4)])
+def test_h2d_modes_deliver_identical_batches(broker, h2d, streams):
+    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
+
+    broker.create_topic("t", 4)
+    broker.fill("t", 400, "fixed_f32", size=64, records_per_batch=37)
+    DS = _dataset(FixedWidth(torch.float32, (64,)))
+    dl = DeviceLoader(DS.placeholder(), 50, num_workers=2, device="cuda:0", h2d=h2d, copy_streams=streams,
+                      slots_per_worker=3, prefetch=3,
+                      worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    rows = []
+    for x in auto_commit(dl):
+        _expected_rows(x)
+        rows += [tuple(r) for r in x[:, :2].long().tolist()]
+    assert len(rows) == len(set(rows)) == 1600
+    assert broker.committed_offsets("g", "t") == {p: 400 for p in range(4)}
+
+
+def test_commit_on_device_waits_for_user_work(broker):
+    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
+
+    broker.create_topic("t", 1)
+    broker.fill("t", 64, "fixed_f32", size=16)
+    DS = _dataset(FixedWidth(torch.float32, (16,)))
+    dl = DeviceLoader(DS.placeholder(), 16, num_workers=1, device="cuda:0", commit_on="device",
+                      worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    n = 0
+    for x in auto_commit(dl):
+        torch.cuda._sleep(2_000_000)  # the user's step keeps the GPU busy
+        n += x.shape[0]
+    assert n == 64 and broker.committed("g", "t", 0) == 64
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float8_e4m3fn])
 def test_fixed_cast_on_device_matches_cpu_path(broker, dtype):
     from torchkafka_amd import DeviceLoader, FixedWidth

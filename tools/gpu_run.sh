@@ -21,8 +21,17 @@ for s in $STEPS; do
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     pytest) step pytest_gpu 600 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=150 --timeout-method=thread ;;
     nccl)   step nccl_probe 120 python tools/nccl_probe.py ;;
+    lockcheck) step lockstep_check 300 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29631 tools/lockstep_check.py ;;
     bench)  step bench 600 python bench.py --stats ;;
     bench8) step bench_fp8 600 python bench.py --stats --dtype fp8 ;;
+    benchlong) step bench_long 600 python bench.py --stats --steps 4000 --warmup 100 ;;
+    benchnocrc) step bench_nocrc 600 python bench.py --stats --steps 4000 --warmup 100 --no-crc ;;
+    benchzc) step bench_zc 600 python bench.py --stats --steps 4000 --warmup 100 --h2d zerocopy ;;
+    benchs1) step bench_s1 600 python bench.py --stats --steps 4000 --warmup 100 --copy-streams 1 ;;
+    benchw8) step bench_w8 600 python bench.py --stats --steps 4000 --warmup 100 --workers 8 ;;
+    benchnont) TORCHKAFKA_NT_COPY=0 step bench_nont 600 python bench.py --stats --steps 4000 --warmup 100 ;;
+    benchbs) step bench_bs1024 600 python bench.py --stats --steps 2000 --warmup 100 --batch-size 1024 ;;
+    profcopy) (cd /tmp && export TMPDIR=/tmp && step profcopy 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profcopy" -o run -- python3 "$OLDPWD/bench.py" --steps 1000) ;;
     prof)   (cd /tmp && export TMPDIR=/tmp && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$OLDPWD/bench.py" --steps 200) ;;
   esac
 done

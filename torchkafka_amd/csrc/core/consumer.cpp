@@ -4,6 +4,10 @@
 #include <cstdlib>
 #include <limits>
 
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
+
 namespace tk {
 
 void Fetcher::assign(const std::vector<uint32_t>& pidxs, const std::vector<int64_t>& positions) {
@@ -41,6 +45,51 @@ bool Fetcher::has_data(const FetchPart& fp) {
                            "] of partition index " + std::to_string(fp.pidx));
   return fp.position < hw;
 }
+
+// ------------------------------------------------------------ streaming copy
+namespace {
+
+// Copies record values into a ring slot.  The slot is never read again by
+// this CPU -- the GPU's DMA engine reads it -- so 32-byte-aligned
+// destinations use non-temporal stores: no read-for-ownership of the
+// destination lines and no eviction of the log data being decoded.  Ordering:
+// Ring::worker_publish issues an sfence before the slot's release store.
+#if defined(__x86_64__)
+__attribute__((target("avx2"))) void copy_nt_avx2(uint8_t* dst, const uint8_t* src, size_t n) {
+  size_t i = 0;
+  for (; i + 128 <= n; i += 128) {
+    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i));
+    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 32));
+    const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 64));
+    const __m256i d = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 96));
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i), a);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 32), b);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 64), c);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 96), d);
+  }
+  for (; i + 32 <= n; i += 32)
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i),
+                        _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i)));
+  if (i < n) std::memcpy(dst + i, src + i, n - i);
+}
+bool nt_enabled() {
+  const char* e = std::getenv("TORCHKAFKA_NT_COPY");
+  return __builtin_cpu_supports("avx2") && !(e && e[0] == '0');
+}
+const bool g_avx2 = nt_enabled();
+#endif
+
+inline void copy_to_slot(uint8_t* dst, const uint8_t* src, size_t n) {
+#if defined(__x86_64__)
+  if (n >= 256 && g_avx2 && (reinterpret_cast<uintptr_t>(dst) & 31) == 0) {
+    copy_nt_avx2(dst, src, n);
+    return;
+  }
+#endif
+  std::memcpy(dst, src, n);
+}
+
+}  // namespace
 
 // ------------------------------------------------------------ JSON
 namespace {
@@ -225,7 +274,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
     if (r.value == nullptr) { touch(r); return kTake; }  // null value == `_process` returned None
     if (fixed) {
       if (uint64_t(r.value_len) != row_bytes) return bad(r, "value size does not match the fixed-width schema");
-      std::memcpy(vals + uint64_t(rows) * row_bytes, r.value, row_bytes);
+      copy_to_slot(vals + uint64_t(rows) * row_bytes, r.value, row_bytes);
       touch(r);
       ++rows;
       return rows == B ? kTakeStop : kTake;
@@ -246,7 +295,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
         slot_full = true;
         return kStopBefore;
       }
-      std::memcpy(vals + vused, r.value, nbytes);
+      copy_to_slot(vals + vused, r.value, nbytes);
     } else {  // JSON -> f32
       float* dst = reinterpret_cast<float*>(vals + vused);
       const int64_t room = int64_t((vcap - vused) / 4);

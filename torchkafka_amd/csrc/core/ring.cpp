@@ -108,6 +108,9 @@ bool Ring::worker_acquire(uint32_t worker, uint32_t i, int64_t timeout_ms) {
 
 void Ring::worker_publish(uint32_t g) {
   SlotHeader* s = slot(g);
+#if defined(__x86_64__)
+  __builtin_ia32_sfence();  // order the packer's non-temporal stores before the release below
+#endif
   s->t_ready_ns = now_ns();
   s->state.store(kSlotReady, std::memory_order_release);
   hdr_->ready_seq.fetch_add(1, std::memory_order_acq_rel);

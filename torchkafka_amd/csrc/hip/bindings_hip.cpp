@@ -10,11 +10,39 @@
 #include "dtypes.h"
 #include "engine.h"
 #include "driver.h"
+#include "rccl_lockstep.h"
 
 namespace py = pybind11;
 using namespace tkh;
 
 namespace {
+// Lockstep transport backed by a Python callable (e.g. a gloo all_reduce): lets the
+// native driver's pipelined protocol run multi-rank where RCCL cannot (several
+// ranks on one GPU, CPU tests).  Each issue() performs the collective at once.
+class PyLockstep : public LockstepTransport {
+ public:
+  explicit PyLockstep(py::function fn) : fn_(std::move(fn)) {}
+  int issue(int64_t a, int64_t b, int64_t c) override {
+    py::gil_scoped_acquire gil;
+    py::tuple r = fn_(a, b, c);
+    const int t = int(next_++ % 64);
+    res_[t][0] = r[0].cast<int64_t>();
+    res_[t][1] = r[1].cast<int64_t>();
+    res_[t][2] = r[2].cast<int64_t>();
+    return t;
+  }
+  void wait(int t, int64_t out[3]) override {
+    out[0] = res_[t][0];
+    out[1] = res_[t][1];
+    out[2] = res_[t][2];
+  }
+
+ private:
+  py::function fn_;
+  uint64_t next_ = 0;
+  int64_t res_[64][3];
+};
+
 template <typename T>
 T* ptr(uintptr_t p) { return reinterpret_cast<T*>(p); }
 hipStream_t stream_of(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
@@ -59,7 +87,14 @@ PYBIND11_MODULE(_tkhip, m) {
       py::arg("stream") = 0);
 
   py::class_<Engine>(m, "Engine")
-      .def(py::init<int, int, size_t>(), py::arg("device"), py::arg("n_slots"), py::arg("staging_bytes"))
+      .def(py::init<int, int, size_t, int, int>(), py::arg("device"), py::arg("n_slots"), py::arg("staging_bytes"),
+           py::arg("n_streams") = 4, py::arg("mode") = int(kH2DDma))
+      .def_property_readonly("mode", &Engine::mode)
+      .def("wait_copy",
+           [](Engine& e, int s) {
+             py::gil_scoped_release nogil;
+             e.wait_copy(s);
+           })
       .def_property_readonly("device", &Engine::device)
       .def_property_readonly("n_slots", &Engine::n_slots)
       .def_property_readonly("staging_stride", &Engine::staging_stride)
@@ -95,6 +130,26 @@ PYBIND11_MODULE(_tkhip, m) {
         py::gil_scoped_release nogil;
         e.synchronize();
       });
+
+  py::class_<LockstepTransport>(m, "LockstepTransport");
+  py::class_<PyLockstep, LockstepTransport>(m, "PyLockstep").def(py::init<py::function>(), py::arg("allreduce_min"));
+  py::class_<RcclLockstep, LockstepTransport>(m, "RcclLockstep")
+      .def(py::init([](const std::string& lib, py::bytes id, int rank, int world, int device, int slots) {
+             return new RcclLockstep(lib, std::string(id), rank, world, device, slots);
+           }),
+           py::arg("lib_path"), py::arg("unique_id"), py::arg("rank"), py::arg("world_size"), py::arg("device"),
+           py::arg("slots"))
+      .def_static("unique_id", [](const std::string& lib) { return py::bytes(RcclLockstep::unique_id(lib)); })
+      .def("allreduce_min",
+           [](RcclLockstep& l, int64_t a, int64_t b, int64_t c) {
+             int64_t r[3];
+             {
+               py::gil_scoped_release nogil;
+               l.wait(l.issue(a, b, c), r);
+             }
+             return py::make_tuple(r[0], r[1], r[2]);
+           })
+      .def_property_readonly("issued", &RcclLockstep::issued);
 
   py::class_<MainDriver>(m, "MainDriver")
       .def(py::init([](Engine* e, const std::string& ring, const std::string& url, const std::string& group,
@@ -147,7 +202,19 @@ PYBIND11_MODULE(_tkhip, m) {
              return l;
            })
       .def("deliver_last", [](MainDriver& d) { d.deliver(d.last); })
-      .def("finish_delivered", &MainDriver::finish_delivered)
+      .def("discard_last",
+           [](MainDriver& d) {
+             py::gil_scoped_release nogil;
+             d.discard(d.last);
+           })
+      .def("finish_delivered", [](MainDriver& d, uintptr_t fence) { d.finish_delivered(stream_of(fence)); },
+           py::arg("fence_stream") = 0)
+      .def("set_commit_on_device", &MainDriver::set_commit_on_device)
+      .def("drain_fenced",
+           [](MainDriver& d, bool wait) {
+             py::gil_scoped_release nogil;
+             d.drain_fenced(wait);
+           })
       .def("add_finished",
            [](MainDriver& d, std::vector<std::tuple<uint32_t, int64_t, int64_t, uint32_t>> wms) {
              std::vector<tk::Watermark> v;
@@ -165,10 +232,24 @@ PYBIND11_MODULE(_tkhip, m) {
              s["commits"] = d.commits();
              s["commit_failures"] = d.commit_failures();
              s["commit_ns"] = d.commit_ns();
+             s["fill_ns"] = d.fill_ns_;
+             s["fills"] = d.fills_;
+             s["blocked_ns"] = d.blocked_ns_;
+             s["blocked_calls"] = d.blocked_calls_;
+             s["ready_age_ns"] = d.ready_age_ns_;
              return s;
            })
-      .def("reset_stats", &MainDriver::reset_stats);
+      .def("reset_stats", &MainDriver::reset_stats)
+      .def("enable_lockstep", &MainDriver::enable_lockstep, py::keep_alive<1, 2>())
+      .def("finish_lockstep",
+           [](MainDriver& d) {
+             py::gil_scoped_release nogil;
+             d.finish_lockstep();
+           })
+      .def_property_readonly("lockstep_enabled", &MainDriver::lockstep_enabled);
 
+  m.attr("H2D_DMA") = int(kH2DDma);
+  m.attr("H2D_ZERO_COPY") = int(kH2DZeroCopy);
   m.attr("F32") = int(kF32);
   m.attr("F16") = int(kF16);
   m.attr("BF16") = int(kBF16);

@@ -18,18 +18,21 @@ MainDriver::MainDriver(Engine* engine, const std::string& ring_name, const std::
   commit_ns_.reserve(1 << 16);
 }
 
-MainDriver::~MainDriver() = default;
+MainDriver::~MainDriver() {
+  for (auto& f : fenced_) hipEventDestroy(std::get<0>(f));
+  for (auto e : event_pool_) hipEventDestroy(e);
+}
 
+// Host slots whose collate kernel ran are handed back to their worker.  Kernels
+// run in hand-out order on the user's stream, so the scan stops at the first
+// incomplete one (one event query per batch in steady state).
 void MainDriver::release_completed() {
-  if (inflight_.empty()) return;
   size_t k = 0;
-  for (int64_t g : inflight_) {
-    if (eng_->h2d_complete(int(g)))
-      ring_->main_release(uint32_t(g));
-    else
-      inflight_[k++] = g;
+  while (k < handed_.size() && eng_->slot_done(int(handed_[k]))) {
+    ring_->main_release(uint32_t(handed_[k]));
+    ++k;
   }
-  inflight_.resize(k);
+  if (k) handed_.erase(handed_.begin(), handed_.begin() + long(k));
 }
 
 int MainDriver::poll_one(bool block, int64_t timeout_ms) {
@@ -44,6 +47,9 @@ int MainDriver::poll_one(bool block, int64_t timeout_ms) {
       return -3;
     }
     if (h->flags & tk::kSlotEOS) done_.at(h->worker) = 1;
+    fill_ns_ += h->t_ready_ns - h->t_fill_start_ns;
+    ready_age_ns_ += tk::now_ns() - h->t_ready_ns;
+    ++fills_;
     SlotView v;
     v.g = g;
     v.n_rows = h->n_rows;
@@ -70,14 +76,110 @@ int MainDriver::poll_one(bool block, int64_t timeout_ms) {
       continue;
     }
     eng_->h2d(int(g), ring_->payload(uint32_t(g)), v.payload_bytes);
-    inflight_.push_back(g);
     staged_.push_back(std::move(v));
     return 1;
   }
 }
 
+int MainDriver::data_staged() const {
+  int n = 0;
+  for (const auto& v : staged_) n += v.g >= 0 ? 1 : 0;
+  return n;
+}
+
+bool MainDriver::all_done() const {
+  for (auto d : done_)
+    if (!d) return false;
+  return true;
+}
+
+bool MainDriver::pop_data(SlotView* out) {
+  while (!staged_.empty()) {
+    SlotView v = std::move(staged_.front());
+    staged_.pop_front();
+    if (v.g < 0) {
+      carry_.insert(carry_.end(), v.wms.begin(), v.wms.end());
+      continue;
+    }
+    if (!carry_.empty()) {
+      v.wms.insert(v.wms.begin(), carry_.begin(), carry_.end());
+      carry_.clear();
+    }
+    *out = std::move(v);
+    return true;
+  }
+  return false;
+}
+
+void MainDriver::enable_lockstep(LockstepTransport* ls, int depth) {
+  ls_ = ls;
+  depth_ = std::max(0, depth);
+  step_ = issued_ = 0;
+  delivered_index_ = -1;
+  stopped_ = false;
+  tickets_.clear();
+  finished_q_.clear();
+}
+
+// Step k may be delivered only if every rank has a batch for it.  The
+// agreement for step j is issued at step max(0, j - depth); its completion
+// proves every rank reached that step, i.e. finished every batch < j - depth,
+// which is what may be committed once it is read.
+int MainDriver::next_slot_lockstep(int64_t timeout_ms, SlotView* out) {
+  if (stopped_) return -2;
+  while (int(staged_.size()) < prefetch_ + 1) {
+    int r = poll_one(false, 0);
+    if (r == -3) return -3;
+    if (r <= 0) break;
+  }
+  while (issued_ <= step_ + depth_) {
+    const int need = int(issued_ - step_) + 1;
+    while (data_staged() < need && !all_done()) {
+      const int64_t t0 = tk::now_ns();
+      int r = poll_one(true, timeout_ms);
+      blocked_ns_ += tk::now_ns() - t0;
+      ++blocked_calls_;
+      if (r == -3) return -3;
+      if (r == -2) break;
+      if (r <= 0) return -1;  // timed out: the caller checks worker health and calls again
+    }
+    const bool have = data_staged() >= need;
+    tickets_.emplace_back(issued_, ls_->issue(have ? 1 : 0, issued_, -issued_));
+    ++issued_;
+  }
+  const auto front = tickets_.front();
+  tickets_.pop_front();
+  int64_t res[3];
+  ls_->wait(front.second, res);
+  if (res[1] != -res[2])
+    throw std::runtime_error("lockstep: ranks are out of step (min " + std::to_string(res[1]) + ", max " +
+                             std::to_string(-res[2]) + ")");
+  while (!finished_q_.empty() && finished_q_.front().first < front.first - depth_) {
+    add_finished(finished_q_.front().second);
+    finished_q_.pop_front();
+  }
+  if (res[0] == 0) {
+    stopped_ = true;
+    return -2;
+  }
+  if (!pop_data(out)) throw std::logic_error("lockstep: agreed on a batch that is not staged");
+  delivered_index_ = step_++;
+  return 1;
+}
+
+void MainDriver::finish_lockstep() {
+  drain_fenced(true);
+  if (!ls_) return;
+  int64_t res[3];
+  ls_->wait(ls_->issue(0, 0, 0), res);  // every rank has stopped at the same step
+  for (auto& f : finished_q_) add_finished(f.second);
+  finished_q_.clear();
+}
+
 int MainDriver::next_slot(int64_t timeout_ms, SlotView* out) {
   release_completed();
+  if (!fenced_.empty()) drain_fenced(false);
+  if (ls_) return next_slot_lockstep(timeout_ms, out);
   for (;;) {
     // keep `prefetch` batches beyond the one handed out in flight to the device
     while (int(staged_.size()) < prefetch_ + 1) {
@@ -86,7 +188,10 @@ int MainDriver::next_slot(int64_t timeout_ms, SlotView* out) {
       if (r <= 0) break;
     }
     if (staged_.empty()) {
+      const int64_t t0 = tk::now_ns();
       int r = poll_one(true, timeout_ms);
+      blocked_ns_ += tk::now_ns() - t0;
+      ++blocked_calls_;
       if (r < 0) return r;
       if (r == 0) return -1;
     }
@@ -109,14 +214,22 @@ void MainDriver::collate_fixed(const SlotView& v, hipStream_t stream, int dst_dt
                                const float* shift, const float* scale) {
   const int src_dt = v.src_dtype;
   eng_->collate_fixed(int(v.g), stream, v.values_offset, src_dt, dst, dst_dt, v.n_rows, row, shift, scale);
+  handed_.push_back(v.g);
 }
 
 void MainDriver::collate_varlen(const SlotView& v, hipStream_t stream, int dst_dt, void* out, int64_t L, double pad,
                                 int64_t* lengths, uint8_t* mask) {
   eng_->collate_varlen(int(v.g), stream, v.values_offset, v.src_dtype, out, dst_dt, v.n_rows, L, pad, lengths, mask);
+  handed_.push_back(v.g);
 }
 
 void MainDriver::deliver(const SlotView& v) { delivered_ = v.wms; }
+
+void MainDriver::discard(const SlotView& v) {
+  if (v.g < 0) return;
+  eng_->wait_copy(int(v.g));
+  ring_->main_release(uint32_t(v.g));
+}
 
 void MainDriver::add_finished(const std::vector<tk::Watermark>& wms) {
   for (const auto& w : wms) {
@@ -125,12 +238,49 @@ void MainDriver::add_finished(const std::vector<tk::Watermark>& wms) {
   }
 }
 
-void MainDriver::finish_delivered() {
-  add_finished(delivered_);
+void MainDriver::stage_finished(int64_t index, std::vector<tk::Watermark>&& wms) {
+  if (ls_)
+    finished_q_.emplace_back(index, std::move(wms));
+  else
+    add_finished(wms);
+}
+
+void MainDriver::finish_delivered(hipStream_t fence) {
+  if (delivered_.empty()) return;
+  if (commit_on_device_) {
+    hipEvent_t ev;
+    if (event_pool_.empty()) {
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+        throw std::runtime_error("driver: hipEventCreate failed");
+    } else {
+      ev = event_pool_.back();
+      event_pool_.pop_back();
+    }
+    if (hipEventRecord(ev, fence) != hipSuccess) throw std::runtime_error("driver: hipEventRecord failed");
+    fenced_.emplace_back(ev, delivered_index_, std::move(delivered_));
+  } else {
+    stage_finished(delivered_index_, std::move(delivered_));
+  }
   delivered_.clear();
 }
 
+void MainDriver::drain_fenced(bool wait) {
+  while (!fenced_.empty()) {
+    auto& f = fenced_.front();
+    hipEvent_t ev = std::get<0>(f);
+    if (wait) {
+      if (hipEventSynchronize(ev) != hipSuccess) throw std::runtime_error("driver: hipEventSynchronize failed");
+    } else if (hipEventQuery(ev) != hipSuccess) {
+      break;  // in order: a later batch is never committed before an earlier one
+    }
+    stage_finished(std::get<1>(f), std::move(std::get<2>(f)));
+    event_pool_.push_back(ev);
+    fenced_.pop_front();
+  }
+}
+
 int MainDriver::commit_pending() {
+  drain_fenced(false);
   if (pending_.empty()) return 0;
   if (!broker_) throw std::runtime_error("DeviceLoader cannot commit: no group_id / broker");
   const int64_t t0 = tk::now_ns();
@@ -154,7 +304,7 @@ int64_t MainDriver::step_fixed(hipStream_t stream, int dst_dt, void* dst, int64_
                                const float* scale, bool auto_commit, int64_t timeout_ms, int* commit_status,
                                SlotView* out) {
   *commit_status = 0;
-  finish_delivered();  // asking for the next batch finishes the previous one
+  finish_delivered(stream);  // asking for the next batch finishes the previous one
   if (auto_commit) *commit_status = commit_pending();
   int r = next_slot(timeout_ms, out);
   if (r < 0) return r;
@@ -177,6 +327,7 @@ std::vector<std::pair<uint32_t, int64_t>> MainDriver::take_pending() {
 
 void MainDriver::reset_stats() {
   commits_ = commit_failures_ = 0;
+  fill_ns_ = fills_ = blocked_ns_ = blocked_calls_ = ready_age_ns_ = 0;
   commit_ns_.clear();
 }
 

@@ -18,6 +18,7 @@
 
 #include "broker.h"
 #include "engine.h"
+#include "rccl_lockstep.h"
 #include "ring.h"
 
 namespace tkh {
@@ -48,7 +49,14 @@ class MainDriver {
                       int64_t* lengths, uint8_t* mask);
 
   void deliver(const SlotView& v);   // batch handed to the user
-  void finish_delivered();           // the user is done with every delivered batch
+  void discard(const SlotView& v);   // consumed but not handed out (drop_last): free its slot
+  // The user is done with every delivered batch.  With commit-on-device, `fence`
+  // (the user's stream) gets an event and the batch only becomes committable
+  // once the GPU has executed everything the user queued for it.
+  void finish_delivered(hipStream_t fence = nullptr);
+  void set_commit_on_device(bool on) { commit_on_device_ = on; }
+  // Moves fenced batches whose GPU work completed to the committable stage.
+  void drain_fenced(bool wait);
   void add_finished(const std::vector<tk::Watermark>& wms);
   // Commits every finished batch.  Returns 0 nothing to do, 1 committed, -1 CommitFailedError.
   int commit_pending();
@@ -68,11 +76,33 @@ class MainDriver {
   const std::vector<int64_t>& commit_ns() const { return commit_ns_; }
   void reset_stats();
 
+  // Cross-rank lockstep over RCCL, pipelined `depth` steps ahead (ls is owned by the caller).
+  void enable_lockstep(LockstepTransport* ls, int depth);
+  // End of a lock-stepped iteration: barrier, then every finished batch becomes committable.
+  void finish_lockstep();
+  bool lockstep_enabled() const { return ls_ != nullptr; }
+
   SlotView last;  // the slot most recently returned by next_slot / step_fixed
 
  private:
   int poll_one(bool block, int64_t timeout_ms);
   void release_completed();
+  int next_slot_lockstep(int64_t timeout_ms, SlotView* out);
+  int data_staged() const;
+  bool all_done() const;
+  bool pop_data(SlotView* out);
+
+  void stage_finished(int64_t index, std::vector<tk::Watermark>&& wms);
+  bool commit_on_device_ = false;
+  std::deque<std::tuple<hipEvent_t, int64_t, std::vector<tk::Watermark>>> fenced_;
+  std::vector<hipEvent_t> event_pool_;
+
+  LockstepTransport* ls_ = nullptr;
+  int depth_ = 2;
+  int64_t step_ = 0, issued_ = 0, delivered_index_ = -1;
+  bool stopped_ = false;
+  std::deque<std::pair<int64_t, int>> tickets_;
+  std::deque<std::pair<int64_t, std::vector<tk::Watermark>>> finished_q_;
 
   Engine* eng_;
   std::unique_ptr<tk::Ring> ring_;
@@ -85,7 +115,7 @@ class MainDriver {
   std::vector<uint8_t> done_;
   uint32_t rr_ = 0;
   std::deque<SlotView> staged_;
-  std::vector<int64_t> inflight_;
+  std::deque<int64_t> handed_;  // slots whose collate was launched, in launch order
   std::vector<tk::Watermark> carry_;
   std::vector<tk::Watermark> delivered_;
   std::unordered_map<uint32_t, int64_t> pending_;
@@ -93,6 +123,10 @@ class MainDriver {
   std::vector<tk::CommitEntry> entries_;
   std::string error_;
   uint64_t commits_ = 0, commit_failures_ = 0;
+ public:
+  // profiling counters (ns): worker fill time of delivered slots, main time blocked on the ring
+  int64_t fill_ns_ = 0, fills_ = 0, blocked_ns_ = 0, blocked_calls_ = 0, ready_age_ns_ = 0;
+ private:
   std::vector<int64_t> commit_ns_;
 };
 

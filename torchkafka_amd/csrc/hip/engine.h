@@ -7,42 +7,66 @@
 
 namespace tkh {
 
+// How a ring slot's bytes reach the collate kernel.
+enum H2DMode : int {
+  kH2DDma = 0,       // hipMemcpyAsync (SDMA engine) into a device staging buffer, then the kernel
+  kH2DZeroCopy = 1,  // the kernel reads the pinned slot straight over PCIe (no copy, no staging)
+};
+
 class Engine {
  public:
-  Engine(int device, int n_slots, size_t staging_bytes);
+  Engine(int device, int n_slots, size_t staging_bytes, int n_streams = 4, int mode = kH2DDma);
   ~Engine();
   Engine(const Engine&) = delete;
   Engine& operator=(const Engine&) = delete;
 
   int device() const { return device_; }
   int n_slots() const { return n_slots_; }
+  int mode() const { return mode_; }
   size_t staging_stride() const { return stride_; }
   void* staging(int s) const { return static_cast<uint8_t*>(staging_) + stride_ * size_t(s); }
-  hipStream_t copy_stream() const { return copy_stream_; }
+  hipStream_t stream_of_slot(int s) const { return streams_[size_t(s) % streams_.size()]; }
 
   void register_host(void* p, size_t len);
   void unregister_host();
   bool host_registered() const { return host_ptr_ != nullptr; }
 
+  // DMA mode: start the slot's copy (its stream runs the slot's kernel after it).
+  // Zero-copy mode: no-op.  `host` must lie in the registered region.
   void h2d(int s, const void* host, size_t nbytes);
-  bool h2d_complete(int s);
-  void wait_h2d(int s);
-  void collate_fixed(int s, hipStream_t stream, size_t values_offset, int src_dt, void* dst, int dst_dt, int64_t rows,
+  // True once the slot's kernel completed: the host slot and its staging buffer are reusable.
+  bool slot_done(int s);
+  void wait_slot(int s);
+  void wait_copy(int s);  // DMA mode: the slot's copy has finished reading host memory
+  // Launch the collate of slot `s` on the user's stream (after the slot's copy in DMA mode).
+  void collate_fixed(int s, hipStream_t user, size_t values_offset, int src_dt, void* dst, int dst_dt, int64_t rows,
                      int64_t row, const float* shift, const float* scale);
-  void collate_varlen(int s, hipStream_t stream, size_t values_offset, int src_dt, void* out, int dst_dt, int64_t rows,
+  void collate_varlen(int s, hipStream_t user, size_t values_offset, int src_dt, void* out, int dst_dt, int64_t rows,
                       int64_t L, double pad, int64_t* lengths, uint8_t* mask);
-  void copy_raw(int s, hipStream_t stream, size_t offset, void* dst, size_t nbytes);
+  void copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes);
   void synchronize();
+
+  // legacy names used by tests
+  bool h2d_complete(int s) { return slot_done(s); }
+  void wait_h2d(int s) { wait_slot(s); }
+  hipStream_t copy_stream() const { return streams_[0]; }
 
  private:
   void check_slot(int s) const;
+  const uint8_t* src_base(int s) const;  // where slot s's payload is read from by kernels
+  void begin(int s, hipStream_t user);
+  void finish(int s, hipStream_t user);
+
   int device_;
   int n_slots_;
+  int mode_;
   size_t stride_ = 0;
   void* staging_ = nullptr;
-  hipStream_t copy_stream_ = nullptr;
-  std::vector<hipEvent_t> h2d_done_, consumed_;
+  std::vector<hipStream_t> streams_;
+  std::vector<hipEvent_t> done_, copied_;
+  std::vector<const uint8_t*> host_src_;  // per slot: host payload pointer given at h2d()
   void* host_ptr_ = nullptr;
+  uint8_t* host_dev_ = nullptr;           // device view of the registered host region (zero-copy)
   size_t host_len_ = 0;
 };
 

@@ -1,15 +1,22 @@
-// H2D engine: pinned-ring registration, side-stream hipMemcpyAsync, per-slot
-// events and the collate launches.
+// H2D engine: pinned-ring registration, side-stream copies, collate launches.
 //
-// Per ring slot s the engine owns a device staging buffer staging[s] and two
-// events:
-//   h2d_done[s]  recorded on the copy stream after the H2D copy of slot s;
-//                the compute stream waits on it before the collate kernel and
-//                the host polls it to recycle the host slot early (the pinned
-//                slot is free as soon as the DMA read it, not after the kernel);
-//   consumed[s]  recorded on the compute stream after the collate kernel;
-//                the copy stream waits on it before overwriting staging[s].
-// No allocation, no synchronisation in the per-batch path (Guideline 9).
+// DMA mode (default): when a slot is acquired -- `prefetch` batches before
+// the user asks for it -- its payload is copied by hipMemcpyAsync into
+// staging[s] on copy stream streams[s % J] and copied[s] is recorded there.
+// Slots on different copy streams use different SDMA queues, so copies run
+// concurrently (one stream alone measured ~12 us per 256 KiB on MI355X).
+// When the batch is handed out, the user's stream waits on copied[s], the
+// collate kernel runs on the user's stream (ordered after the user's prior
+// work, so a recycled output block is never overwritten early) and done[s]
+// is recorded.  The host slot is released once done[s] completed; a staging
+// buffer is therefore only rewritten after its previous kernel has run.
+//
+// Zero-copy mode: no copy; the kernel reads the pinned slot directly through
+// its device mapping (hipHostRegisterMapped) over PCIe.
+//
+// Per batch the host issues memcpyAsync + eventRecord (prefetch) and
+// streamWaitEvent + launch + eventRecord (hand-out); zero-copy mode only the
+// last two.  No allocation, no synchronisation (Guideline 9).
 #include <hip/hip_runtime.h>
 
 #include <stdexcept>
@@ -27,28 +34,32 @@ namespace tkh {
     if (_e != hipSuccess) throw std::runtime_error(std::string(#expr) + ": " + hipGetErrorString(_e)); \
   } while (0)
 
-Engine::Engine(int device, int n_slots, size_t staging_bytes) : device_(device), n_slots_(n_slots) {
+Engine::Engine(int device, int n_slots, size_t staging_bytes, int n_streams, int mode)
+    : device_(device), n_slots_(n_slots), mode_(mode) {
   if (n_slots <= 0) throw std::invalid_argument("engine: n_slots must be positive");
+  if (mode != kH2DDma && mode != kH2DZeroCopy) throw std::invalid_argument("engine: bad h2d mode");
+  if (n_streams < 1) n_streams = 1;
+  if (n_streams > n_slots) n_streams = n_slots;
   TKH_CHECK(hipSetDevice(device_));
-  TKH_CHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+  streams_.resize(size_t(n_streams));
+  for (auto& st : streams_) TKH_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   stride_ = (staging_bytes + 256 + 4095) / 4096 * 4096;
-  TKH_CHECK(hipMalloc(&staging_, stride_ * size_t(n_slots)));
-  h2d_done_.resize(size_t(n_slots));
-  consumed_.resize(size_t(n_slots));
-  for (int i = 0; i < n_slots; ++i) {
-    TKH_CHECK(hipEventCreateWithFlags(&h2d_done_[size_t(i)], hipEventDisableTiming));
-    TKH_CHECK(hipEventCreateWithFlags(&consumed_[size_t(i)], hipEventDisableTiming));
-  }
+  if (mode_ == kH2DDma) TKH_CHECK(hipMalloc(&staging_, stride_ * size_t(n_slots)));
+  done_.resize(size_t(n_slots));
+  for (auto& e : done_) TKH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  copied_.resize(size_t(n_slots));
+  for (auto& e : copied_) TKH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  host_src_.assign(size_t(n_slots), nullptr);
 }
 
 Engine::~Engine() {
   hipSetDevice(device_);
-  hipStreamSynchronize(copy_stream_);
+  for (auto st : streams_) hipStreamSynchronize(st);
   if (host_ptr_) hipHostUnregister(host_ptr_);
-  for (auto e : h2d_done_) hipEventDestroy(e);
-  for (auto e : consumed_) hipEventDestroy(e);
+  for (auto e : done_) hipEventDestroy(e);
+  for (auto e : copied_) hipEventDestroy(e);
   if (staging_) hipFree(staging_);
-  hipStreamDestroy(copy_stream_);
+  for (auto st : streams_) hipStreamDestroy(st);
 }
 
 void Engine::check_slot(int s) const {
@@ -58,67 +69,97 @@ void Engine::check_slot(int s) const {
 void Engine::register_host(void* p, size_t len) {
   if (host_ptr_) throw std::runtime_error("engine: a host region is already registered");
   TKH_CHECK(hipSetDevice(device_));
-  TKH_CHECK(hipHostRegister(p, len, hipHostRegisterDefault));
+  TKH_CHECK(hipHostRegister(p, len, hipHostRegisterMapped));
+  void* dev = nullptr;
+  TKH_CHECK(hipHostGetDevicePointer(&dev, p, 0));
   host_ptr_ = p;
+  host_dev_ = static_cast<uint8_t*>(dev);
   host_len_ = len;
 }
 
 void Engine::unregister_host() {
   if (!host_ptr_) return;
-  TKH_CHECK(hipStreamSynchronize(copy_stream_));
+  synchronize();
   TKH_CHECK(hipHostUnregister(host_ptr_));
   host_ptr_ = nullptr;
+  host_dev_ = nullptr;
   host_len_ = 0;
 }
 
 void Engine::h2d(int s, const void* host, size_t nbytes) {
   check_slot(s);
+  const auto* h = static_cast<const uint8_t*>(host);
+  if (host_ptr_ && (h < static_cast<uint8_t*>(host_ptr_) || h + nbytes > static_cast<uint8_t*>(host_ptr_) + host_len_))
+    throw std::invalid_argument("engine: slot payload outside the registered host region");
+  host_src_[size_t(s)] = h;
+  if (mode_ == kH2DZeroCopy) {
+    if (!host_dev_) throw std::runtime_error("engine: zero-copy mode needs a registered host region");
+    return;
+  }
   if (nbytes + 256 > stride_) throw std::invalid_argument("engine: copy larger than the staging buffer");
-  // staging[s] may still be read by the previous batch's collate kernel
-  TKH_CHECK(hipStreamWaitEvent(copy_stream_, consumed_[size_t(s)], 0));
-  if (nbytes) TKH_CHECK(hipMemcpyAsync(staging(s), host, nbytes, hipMemcpyHostToDevice, copy_stream_));
-  TKH_CHECK(hipEventRecord(h2d_done_[size_t(s)], copy_stream_));
+  hipStream_t st = stream_of_slot(s);
+  if (nbytes) TKH_CHECK(hipMemcpyAsync(staging(s), host, nbytes, hipMemcpyHostToDevice, st));
+  TKH_CHECK(hipEventRecord(copied_[size_t(s)], st));
 }
 
-bool Engine::h2d_complete(int s) {
+const uint8_t* Engine::src_base(int s) const {
+  if (mode_ == kH2DDma) return static_cast<const uint8_t*>(staging(s));
+  const uint8_t* h = host_src_[size_t(s)];
+  if (!h) throw std::runtime_error("engine: slot has no payload (h2d not called)");
+  return host_dev_ + (h - static_cast<const uint8_t*>(host_ptr_));
+}
+
+bool Engine::slot_done(int s) {
   check_slot(s);
-  hipError_t e = hipEventQuery(h2d_done_[size_t(s)]);
+  hipError_t e = hipEventQuery(done_[size_t(s)]);
   if (e == hipSuccess) return true;
   if (e == hipErrorNotReady) return false;
-  throw std::runtime_error(std::string("engine: h2d event: ") + hipGetErrorString(e));
+  throw std::runtime_error(std::string("engine: slot event: ") + hipGetErrorString(e));
 }
 
-void Engine::wait_h2d(int s) {
+void Engine::wait_slot(int s) {
   check_slot(s);
-  TKH_CHECK(hipEventSynchronize(h2d_done_[size_t(s)]));
+  TKH_CHECK(hipEventSynchronize(done_[size_t(s)]));
 }
 
-void Engine::collate_fixed(int s, hipStream_t stream, size_t values_offset, int src_dt, void* dst, int dst_dt,
+void Engine::wait_copy(int s) {
+  check_slot(s);
+  if (mode_ == kH2DDma) TKH_CHECK(hipEventSynchronize(copied_[size_t(s)]));
+}
+
+void Engine::begin(int s, hipStream_t user) {
+  if (mode_ == kH2DDma) TKH_CHECK(hipStreamWaitEvent(user, copied_[size_t(s)], 0));
+}
+
+void Engine::finish(int s, hipStream_t user) { TKH_CHECK(hipEventRecord(done_[size_t(s)], user)); }
+
+void Engine::collate_fixed(int s, hipStream_t user, size_t values_offset, int src_dt, void* dst, int dst_dt,
                            int64_t rows, int64_t row, const float* shift, const float* scale) {
   check_slot(s);
-  TKH_CHECK(hipStreamWaitEvent(stream, h2d_done_[size_t(s)], 0));
-  launch_fixed(static_cast<uint8_t*>(staging(s)) + values_offset, src_dt, dst, dst_dt, rows, row, shift, scale, stream);
-  TKH_CHECK(hipEventRecord(consumed_[size_t(s)], stream));
+  begin(s, user);
+  launch_fixed(src_base(s) + values_offset, src_dt, dst, dst_dt, rows, row, shift, scale, user);
+  finish(s, user);
 }
 
-void Engine::collate_varlen(int s, hipStream_t stream, size_t values_offset, int src_dt, void* out, int dst_dt,
+void Engine::collate_varlen(int s, hipStream_t user, size_t values_offset, int src_dt, void* out, int dst_dt,
                             int64_t rows, int64_t L, double pad, int64_t* lengths, uint8_t* mask) {
   check_slot(s);
-  TKH_CHECK(hipStreamWaitEvent(stream, h2d_done_[size_t(s)], 0));
-  auto* base = static_cast<uint8_t*>(staging(s));
+  const uint8_t* base = src_base(s);
+  begin(s, user);
   launch_varlen(reinterpret_cast<const int32_t*>(base), base + values_offset, src_dt, out, dst_dt, rows, L, pad,
-                lengths, mask, stream);
-  TKH_CHECK(hipEventRecord(consumed_[size_t(s)], stream));
+                lengths, mask, user);
+  finish(s, user);
 }
 
-void Engine::copy_raw(int s, hipStream_t stream, size_t offset, void* dst, size_t nbytes) {
+void Engine::copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes) {
   check_slot(s);
-  TKH_CHECK(hipStreamWaitEvent(stream, h2d_done_[size_t(s)], 0));
-  if (nbytes)
-    TKH_CHECK(hipMemcpyAsync(dst, static_cast<uint8_t*>(staging(s)) + offset, nbytes, hipMemcpyDeviceToDevice, stream));
-  TKH_CHECK(hipEventRecord(consumed_[size_t(s)], stream));
+  begin(s, user);
+  if (nbytes) TKH_CHECK(hipMemcpyAsync(dst, src_base(s) + offset, nbytes, hipMemcpyDefault, user));
+  finish(s, user);
 }
 
-void Engine::synchronize() { TKH_CHECK(hipStreamSynchronize(copy_stream_)); }
+void Engine::synchronize() {
+  for (auto st : streams_) TKH_CHECK(hipStreamSynchronize(st));
+}
 
 }  // namespace tkh

@@ -1,0 +1,124 @@
+#include "rccl_lockstep.h"
+
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <stdexcept>
+
+namespace tkh {
+
+struct RcclApi {
+  void* lib = nullptr;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+namespace {
+
+#define TKH_HIP(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess) throw std::runtime_error(std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+RcclApi* load_api(const std::string& path) {
+  // Prefer the instance already in the process (torch's), then the given path, then the system one.
+  void* lib = dlopen(path.c_str(), RTLD_NOW | RTLD_NOLOAD | RTLD_GLOBAL);
+  if (!lib) lib = dlopen(path.c_str(), RTLD_NOW | RTLD_GLOBAL);
+  if (!lib) lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!lib) throw std::runtime_error(std::string("cannot load RCCL: ") + dlerror());
+  auto* api = new RcclApi();
+  api->lib = lib;
+  auto sym = [&](const char* name) {
+    void* p = dlsym(lib, name);
+    if (!p) throw std::runtime_error(std::string("RCCL symbol missing: ") + name);
+    return p;
+  };
+  api->GetUniqueId = reinterpret_cast<decltype(api->GetUniqueId)>(sym("ncclGetUniqueId"));
+  api->CommInitRank = reinterpret_cast<decltype(api->CommInitRank)>(sym("ncclCommInitRank"));
+  api->AllReduce = reinterpret_cast<decltype(api->AllReduce)>(sym("ncclAllReduce"));
+  api->CommDestroy = reinterpret_cast<decltype(api->CommDestroy)>(sym("ncclCommDestroy"));
+  api->GetErrorString = reinterpret_cast<decltype(api->GetErrorString)>(sym("ncclGetErrorString"));
+  return api;
+}
+
+void check(RcclApi* api, ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + api->GetErrorString(r));
+}
+
+}  // namespace
+
+std::string RcclLockstep::unique_id(const std::string& lib_path) {
+  RcclApi* api = load_api(lib_path);
+  ncclUniqueId id;
+  check(api, api->GetUniqueId(&id), "ncclGetUniqueId");
+  delete api;  // the library stays loaded (no dlclose)
+  return std::string(id.internal, sizeof(id.internal));
+}
+
+RcclLockstep::RcclLockstep(const std::string& lib_path, const std::string& id, int rank, int world, int device,
+                           int slots)
+    : rank_(rank), world_(world), device_(device), slots_(slots < 2 ? 2 : slots) {
+  if (id.size() != NCCL_UNIQUE_ID_BYTES) throw std::invalid_argument("RCCL unique id must be 128 bytes");
+  api_ = load_api(lib_path);
+  TKH_HIP(hipSetDevice(device_));
+  TKH_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  TKH_HIP(hipMalloc(reinterpret_cast<void**>(&d_), sizeof(int64_t) * 6 * size_t(slots_)));
+  TKH_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_in_), sizeof(int64_t) * 3 * size_t(slots_), hipHostMallocDefault));
+  TKH_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_out_), sizeof(int64_t) * 3 * size_t(slots_), hipHostMallocDefault));
+  ev_.resize(size_t(slots_));
+  for (auto& e : ev_) TKH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  ncclUniqueId uid;
+  std::memcpy(uid.internal, id.data(), NCCL_UNIQUE_ID_BYTES);
+  ncclComm_t comm = nullptr;
+  check(api_, api_->CommInitRank(&comm, world_, uid, rank_), "ncclCommInitRank");
+  comm_ = comm;
+}
+
+RcclLockstep::~RcclLockstep() {
+  hipSetDevice(device_);
+  if (stream_) hipStreamSynchronize(stream_);
+  if (comm_) api_->CommDestroy(static_cast<ncclComm_t>(comm_));
+  for (auto e : ev_) hipEventDestroy(e);
+  if (d_) hipFree(d_);
+  if (h_in_) hipHostFree(h_in_);
+  if (h_out_) hipHostFree(h_out_);
+  if (stream_) hipStreamDestroy(stream_);
+  delete api_;
+}
+
+int RcclLockstep::issue(int64_t a, int64_t b, int64_t c) {
+  const int s = int(issued_ % uint64_t(slots_));
+  // the slot's previous round trip must be complete before its buffers are reused
+  TKH_HIP(hipEventSynchronize(ev_[size_t(s)]));
+  int64_t* hin = h_in_ + 3 * s;
+  int64_t* hout = h_out_ + 3 * s;
+  int64_t* din = d_ + 6 * s;
+  int64_t* dout = din + 3;
+  hin[0] = a;
+  hin[1] = b;
+  hin[2] = c;
+  TKH_HIP(hipMemcpyAsync(din, hin, 3 * sizeof(int64_t), hipMemcpyHostToDevice, stream_));
+  check(api_, api_->AllReduce(din, dout, 3, ncclInt64, ncclMin, static_cast<ncclComm_t>(comm_), stream_),
+        "ncclAllReduce");
+  TKH_HIP(hipMemcpyAsync(hout, dout, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, stream_));
+  TKH_HIP(hipEventRecord(ev_[size_t(s)], stream_));
+  ++issued_;
+  return s;
+}
+
+bool RcclLockstep::ready(int t) { return hipEventQuery(ev_.at(size_t(t))) == hipSuccess; }
+
+void RcclLockstep::wait(int t, int64_t out[3]) {
+  TKH_HIP(hipEventSynchronize(ev_.at(size_t(t))));
+  const int64_t* hout = h_out_ + 3 * t;
+  out[0] = hout[0];
+  out[1] = hout[1];
+  out[2] = hout[2];
+}
+
+}  // namespace tkh

@@ -1,0 +1,64 @@
+// Native RCCL lockstep collective for multi-GPU streaming.
+//
+// One tiny all-reduce(MIN) of int64 [have_batch, step, -step] per loader step
+// decides, for every rank at once, whether all ranks have a batch for that
+// step (so they continue or stop together) and proves they are on the same
+// step.  Issued from C++ on a private HIP stream -- never behind the user's
+// queued compute -- and pipelined `depth` steps ahead, so the host never
+// waits on the ~10-30 us xGMI round trip: the result for step k was issued
+// at step k - depth and is normally complete when it is read.
+//
+// RCCL is resolved with dlopen() against the librccl that torch already
+// loaded (same library instance as torch.distributed's "nccl" backend); the
+// communicator is our own, bootstrapped from a unique id the caller
+// broadcasts through torch.distributed.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace tkh {
+
+struct RcclApi;
+
+// A pipelined all-reduce(MIN) of three int64 per step: issue() returns a ticket, wait() its result.
+class LockstepTransport {
+ public:
+  virtual ~LockstepTransport() = default;
+  virtual int issue(int64_t a, int64_t b, int64_t c) = 0;
+  virtual void wait(int ticket, int64_t out[3]) = 0;
+};
+
+class RcclLockstep : public LockstepTransport {
+ public:
+  // Generates a unique id (rank 0) -- 128 opaque bytes.
+  static std::string unique_id(const std::string& lib_path);
+  RcclLockstep(const std::string& lib_path, const std::string& id, int rank, int world, int device, int slots);
+  ~RcclLockstep();
+  RcclLockstep(const RcclLockstep&) = delete;
+  RcclLockstep& operator=(const RcclLockstep&) = delete;
+
+  // Enqueues all-reduce(MIN) of {a, b, c}; returns a ticket.
+  int issue(int64_t a, int64_t b, int64_t c) override;
+  // Waits for a ticket's result.
+  void wait(int ticket, int64_t out[3]) override;
+  bool ready(int ticket);
+  int world() const { return world_; }
+  int rank() const { return rank_; }
+  uint64_t issued() const { return issued_; }
+
+ private:
+  RcclApi* api_ = nullptr;
+  void* comm_ = nullptr;
+  int rank_, world_, device_, slots_;
+  hipStream_t stream_ = nullptr;
+  int64_t* d_ = nullptr;       // device [slots][2][3]: in, out
+  int64_t* h_in_ = nullptr;    // pinned [slots][3]
+  int64_t* h_out_ = nullptr;   // pinned [slots][3]
+  std::vector<hipEvent_t> ev_;
+  uint64_t issued_ = 0;
+};
+
+}  // namespace tkh

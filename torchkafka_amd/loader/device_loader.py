@@ -49,6 +49,22 @@ log = logging.getLogger(__name__)
 _ds_logger = logging.getLogger("torchkafka.kafka_dataset")
 
 
+def _host_allreduce_min(group):
+    """all-reduce(MIN) of three int64 over a CPU (gloo) group, for the driver's PyLockstep transport."""
+    import torch.distributed as dist
+
+    if dist.get_backend(group) != "gloo":
+        group = dist.new_group(backend="gloo")  # collective: every rank builds its loader iterator
+    buf = torch.zeros(3, dtype=torch.int64)
+
+    def allreduce_min(a: int, b: int, c: int):
+        buf[0], buf[1], buf[2] = a, b, c
+        dist.all_reduce(buf, op=dist.ReduceOp.MIN, group=group)
+        return int(buf[0]), int(buf[1]), int(buf[2])
+
+    return allreduce_min
+
+
 class KafkaBatch(NamedTuple):
     """Batch plus provenance (``return_info=True``)."""
 
@@ -74,6 +90,7 @@ class _Run:
         self.procs: list = []
         self.engine = None
         self.driver = None
+        self.rccl = None
         self.payload_addr = [self.ring.payload_address(g) for g in range(self.ring.n_slots)]
         self.staged: deque = deque()       # (g, summary, wms) with H2D issued (or CPU: just acquired)
         self.inflight: list = []           # slots whose H2D may still be reading host memory
@@ -93,12 +110,14 @@ class _Run:
                 self.procs.append(p)
             if L.device.type == "cuda":
                 # only after the fork: workers never inherit an initialised HIP runtime state they would use
-                self.engine = hip().Engine(L.device.index if L.device.index is not None else torch.cuda.current_device(),
-                                           self.ring.n_slots, self.ring.payload_capacity)
+                dev = L.device.index if L.device.index is not None else torch.cuda.current_device()
+                mode = hip().H2D_ZERO_COPY if L.h2d == "zerocopy" else hip().H2D_DMA
+                self.engine = hip().Engine(dev, self.ring.n_slots, self.ring.payload_capacity, L.copy_streams, mode)
                 self.engine.register_host(self.ring.base_address, self.ring.total_bytes)
                 url, group = L._commit_target_url()
                 self.driver = hip().MainDriver(self.engine, self.name, url, group, L.prefetch, L.in_order,
                                                L._default_src_code())
+                self.driver.set_commit_on_device(L.commit_on == "device")
         except BaseException:
             self.close()
             raise
@@ -180,6 +199,7 @@ class _Run:
                 p.terminate()
                 p.join(timeout=5)
         self.driver = None
+        self.rccl = None
         if self.engine is not None:
             try:
                 self.engine.synchronize()
@@ -216,7 +236,12 @@ class DeviceLoader:
         pad_to / pad_multiple / pad_value / return_mask: variable-length padding controls.
         commit_on: ``"host"`` (commit when the next batch is requested, as the reference) or
             ``"device"`` (additionally wait until the GPU finished the user's work on the batch).
-        lockstep: synchronise steps and commits across ranks when torch.distributed is initialised.
+        lockstep: synchronise steps and commits across ranks when torch.distributed is initialised
+            (``True``: native RCCL on GPUs, gloo on CPU; ``"host"``: a gloo transport even on GPUs;
+            ``"always"``: also at world size 1).
+        lockstep_depth: steps the per-step agreement is issued ahead (hides the collective's latency).
+        h2d: ``"dma"`` (hipMemcpyAsync into device staging on ``copy_streams`` side streams, issued
+            ``prefetch`` batches ahead) or ``"zerocopy"`` (the collate kernel reads pinned host memory).
     """
 
     def __init__(self, dataset, batch_size: int = 256, *, num_workers: int = 4, worker_init_fn=None,
@@ -226,7 +251,8 @@ class DeviceLoader:
                  return_info: bool = False, slot_bytes: int | None = None, native: bool = True,
                  multiprocessing_context: str = "fork", commit_on: str = "host", lockstep: bool = True,
                  rank: int | None = None, world_size: int | None = None, timeout: float = 0,
-                 group_id: str | None = None, bootstrap_servers=None, base_seed: int | None = None):
+                 group_id: str | None = None, bootstrap_servers=None, base_seed: int | None = None,
+                 lockstep_depth: int = 2, h2d: str = "dma", copy_streams: int = 4):
         if batch_size < 1:
             raise ValueError("batch_size must be >= 1")
         if num_workers < 1:
@@ -262,6 +288,11 @@ class DeviceLoader:
         self.multiprocessing_context = multiprocessing_context
         self.commit_on = commit_on
         self.lockstep = lockstep
+        self.lockstep_depth = max(0, int(lockstep_depth))
+        if h2d not in ("dma", "zerocopy"):
+            raise ValueError("h2d must be 'dma' (hipMemcpyAsync on side streams) or 'zerocopy'")
+        self.h2d = h2d
+        self.copy_streams = max(1, int(copy_streams))
         r, w = dist_rank_world()
         self.rank = r if rank is None else int(rank)
         self.world_size = w if world_size is None else int(world_size)
@@ -337,19 +368,27 @@ class DeviceLoader:
         # fork the workers first: the lockstep below initialises HIP in this process
         run = self._run = _Run(self)
         lock = None
-        if self.lockstep and self.world_size > 1:
-            import torch.distributed as dist
+        try:
+            want = self.lockstep and (self.world_size > 1 or self.lockstep == "always")
+            if want:
+                import torch.distributed as dist
 
-            if dist.is_available() and dist.is_initialized():
-                from ..parallel.lockstep import Lockstep
+                if dist.is_available() and dist.is_initialized():
+                    if run.driver is not None:
+                        if dist.get_backend(process_group) == "nccl" and self.lockstep != "host":
+                            run.rccl = self._make_rccl_lockstep(process_group)
+                        else:
+                            run.rccl = hip().PyLockstep(_host_allreduce_min(process_group))
+                        run.driver.enable_lockstep(run.rccl, self.lockstep_depth)
+                    else:
+                        from ..parallel.lockstep import Lockstep
 
-                try:
-                    lock = Lockstep(process_group, self.device if self.device.type == "cuda" else None)
-                except BaseException:
-                    run.close()
-                    raise
-        if run.driver is not None and lock is None and self._fast_path_ok():
-            yield from self._iterate_fast(run, auto_commit)
+                        lock = Lockstep(process_group, None)
+        except BaseException:
+            run.close()
+            raise
+        if run.driver is not None:
+            yield from self._iterate_driver(run, auto_commit)
             return
         finished = self._pending_wms
         prev = None
@@ -402,10 +441,57 @@ class DeviceLoader:
     def _fast_path_ok(self) -> bool:
         s = self.schema
         return (s is not None and getattr(s, "kind", None) == 0 and self.native and not self.return_info
-                and not self.drop_last and self.commit_on == "host")
+                and not self.drop_last)
 
-    def _iterate_fast(self, run: _Run, auto_commit: bool):
-        """Fixed-width records on the GPU: one native call per batch (slot, H2D, collate, exact commit)."""
+    def _make_rccl_lockstep(self, process_group):
+        """Native RCCL communicator for the per-step lockstep (id broadcast through torch.distributed)."""
+        import torch.distributed as dist
+
+        lib = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+        rank = dist.get_rank(process_group)
+        world = dist.get_world_size(process_group)
+        uid = [hip().RcclLockstep.unique_id(lib) if rank == 0 else None]
+        src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
+        dist.broadcast_object_list(uid, src=src, group=process_group, device=self.device)
+        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        return hip().RcclLockstep(lib, uid[0], rank, world, dev, self.lockstep_depth + 2)
+
+    def _iterate_driver(self, run: _Run, auto_commit: bool):
+        """GPU iteration through the native step driver (one native call per fixed-width batch)."""
+        drv = run.driver
+        debug = _ds_logger.isEnabledFor(logging.DEBUG)
+        completed = False
+        try:
+            if self._fast_path_ok():
+                yield from self._fast_loop(run, auto_commit, debug)
+            else:
+                while True:
+                    # asking for the next batch finishes the previous one
+                    drv.finish_delivered(torch.cuda.current_stream(self.device).cuda_stream)
+                    if auto_commit:
+                        self._log_commit(drv.commit_pending(), debug)
+                    item = self._next_item_driver(run)
+                    if item is None:
+                        break
+                    drv.deliver_last()
+                    yield item[0]
+            completed = True
+        finally:
+            drv.finish_delivered(torch.cuda.current_stream(self.device).cuda_stream)
+            if completed:
+                drv.finish_lockstep()
+            drv.drain_fenced(True)
+            if completed and auto_commit:
+                self._log_commit(drv.commit_pending(), debug)
+            elif not auto_commit:
+                # manual mode: keep every yielded batch committable by DeviceLoader.commit()
+                pend = drv.take_pending()
+                if pend:
+                    self._pending_wms.append(([(p, 0, o, 0) for p, o in pend], None))
+            self._absorb_driver_stats(drv)
+            run.close()
+
+    def _fast_loop(self, run: _Run, auto_commit: bool, debug: bool):
         drv = run.driver
         s = self.schema
         B, shape, row = self.batch_size, tuple(s.shape), s.row_elems
@@ -416,42 +502,29 @@ class DeviceLoader:
         dev = self.device
         stats = self.stats
         empty = torch.empty
-        debug = _ds_logger.isEnabledFor(logging.DEBUG)
-        completed = False
-        try:
-            while True:
-                t0 = time.perf_counter_ns()
-                out = empty((B, *shape), dtype=dst_dt, device=dev)
-                r, cs = drv.step_fixed(torch.cuda.current_stream(dev).cuda_stream, dst_code, out.data_ptr(), row,
-                                       shift, scale, auto_commit, 100)
-                if cs:
-                    self._log_commit(cs, debug)
-                if r > 0:
-                    stats.batches += 1
-                    stats.records += r
-                    stats.issue_ns += time.perf_counter_ns() - t0
-                    yield out if r == B else out[:r]
-                elif r == -2:
-                    break
-                elif r == -3:
-                    raise WorkerError(drv.error())
-                else:
-                    run._check_workers_native()
-                    if self.timeout > 0 and time.perf_counter_ns() - t0 > self.timeout * 1e9:
-                        raise TimeoutError(f"DeviceLoader timed out after {self.timeout}s waiting for a batch")
-            completed = True
-        finally:
-            if completed and auto_commit:
-                drv.finish_delivered()
-                self._log_commit(drv.commit_pending(), debug)
-            elif not auto_commit:
-                # manual mode: keep every yielded batch committable by DeviceLoader.commit()
-                drv.finish_delivered()
-                pend = drv.take_pending()
-                if pend:
-                    self._pending_wms.append(([(p, 0, o, 0) for p, o in pend], None))
-            self._absorb_driver_stats(drv)
-            run.close()
+        raw_stream = torch._C._cuda_getCurrentRawStream
+        dev_index = dev.index
+        out_shape = (B, *shape)
+        step = drv.step_fixed
+        while True:
+            t0 = time.perf_counter_ns()
+            out = empty(out_shape, dtype=dst_dt, device=dev)
+            r, cs = step(raw_stream(dev_index), dst_code, out.data_ptr(), row, shift, scale, auto_commit, 100)
+            if cs:
+                self._log_commit(cs, debug)
+            if r > 0:
+                stats.batches += 1
+                stats.records += r
+                stats.issue_ns += time.perf_counter_ns() - t0
+                yield out if r == B else out[:r]
+            elif r == -2:
+                return
+            elif r == -3:
+                raise WorkerError(drv.error())
+            else:
+                run._check_workers_native()
+                if self.timeout > 0 and time.perf_counter_ns() - t0 > self.timeout * 1e9:
+                    raise TimeoutError(f"DeviceLoader timed out after {self.timeout}s waiting for a batch")
 
     def _log_commit(self, status: int, debug: bool) -> None:
         if status == -1:
@@ -461,6 +534,10 @@ class DeviceLoader:
 
     def _absorb_driver_stats(self, drv) -> None:
         st = drv.stats()
+        self.stats.worker_fill_ns += st["fill_ns"]
+        self.stats.worker_fills += st["fills"]
+        self.stats.wait_ns += st["blocked_ns"]
+        self.stats.ready_age_ns += st["ready_age_ns"]
         self.stats.commits += st["commits"]
         self.stats.commit_failures += st["commit_failures"]
         self.stats.commit_ns.extend(st["commit_ns"])
@@ -519,11 +596,10 @@ class DeviceLoader:
             _, n_rows, kind, max_len, total, src_code, shape, payload_bytes = res
             wms = drv.last_watermarks()
             if self.drop_last and n_rows < self.batch_size:
-                run.carry.extend(wms)
+                drv.discard_last()     # consumed but not handed out: finished right away
+                drv.deliver_last()
+                drv.finish_delivered()
                 continue
-            if run.carry:
-                wms = run.carry + wms
-                run.carry = []
             break
         t1 = time.perf_counter_ns()
         src_dt = CODE_DTYPE[src_code]
@@ -677,10 +753,25 @@ class DeviceLoader:
         """Commits every batch yielded so far (manual mode)."""
         run = self._run
         if run is not None and run.driver is not None and not run.closed:
-            run.driver.finish_delivered()
+            run.driver.finish_delivered(torch.cuda.current_stream(self.device).cuda_stream)
+            run.driver.drain_fenced(True)
             self._log_commit(run.driver.commit_pending(), _ds_logger.isEnabledFor(logging.DEBUG))
             self._absorb_driver_stats(run.driver)
         self._commit_finished(wait=True)
+
+    def reset_stats(self) -> None:
+        """Zeroes the loader's counters (and the native driver's) -- e.g. after warm-up."""
+        self.stats.reset()
+        run = self._run
+        if run is not None and run.driver is not None and not run.closed:
+            run.driver.reset_stats()
+
+    def stats_summary(self) -> dict:
+        """Counters so far, including the native driver's (commits, worker fill times, blocking)."""
+        run = self._run
+        if run is not None and run.driver is not None and not run.closed:
+            self._absorb_driver_stats(run.driver)
+        return self.stats.summary()
 
     def committed_offsets(self) -> dict[int, int]:
         return dict(self._committed)

@@ -30,6 +30,9 @@ class LoaderStats:
     commits: int = 0
     commit_failures: int = 0
     commit_ns: list = field(default_factory=list)
+    worker_fill_ns: int = 0
+    worker_fills: int = 0
+    ready_age_ns: int = 0
     started: float = field(default_factory=time.perf_counter)
     max_commit_samples: int = 100000
 
@@ -59,6 +62,8 @@ class LoaderStats:
             "records_per_s": self.records / el if el > 0 else float("nan"),
             "host_wait_us_per_batch": self.wait_ns / 1e3 / max(self.batches, 1),
             "host_issue_us_per_batch": self.issue_ns / 1e3 / max(self.batches, 1),
+            "worker_fill_us_per_batch": self.worker_fill_ns / 1e3 / max(self.worker_fills, 1),
+            "ready_age_us_per_batch": self.ready_age_ns / 1e3 / max(self.worker_fills, 1),
             "commits": self.commits,
             "commit_failures": self.commit_failures,
             "commit_p50_us": percentile(c_us, 50),
