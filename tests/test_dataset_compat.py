@@ -303,7 +303,21 @@ def test_d4_commit_worker_signal_after_stream_end_is_harmless(broker):
         {(0, o) for o in range(4)} | {(1, o) for o in range(400)}
 
 
-def test_d6_init_worker_picklable_under_spawn(broker):
+def test_d6_init_worker_picklable_under_spawn():
+    import uuid
+
+    from torchkafka_amd.broker import SyntheticBroker
+
+    # spawned workers need ~1-2 s to start: use Kafka's default 3 s initial rebalance delay so both
+    # join the first generation (otherwise the late joiner triggers a rebalance and re-delivery)
+    broker = SyntheticBroker.create(f"shm://tkd6-{uuid.uuid4().hex[:8]}", group_initial_rebalance_delay_ms=3000)
+    try:
+        _d6_body(broker)
+    finally:
+        broker.destroy()
+
+
+def _d6_body(broker):
     produce_offsets(broker, n=8, partitions=2)
     ds = PartOffset.placeholder()
     dl = DataLoader(ds, batch_size=4, num_workers=2, multiprocessing_context="spawn",

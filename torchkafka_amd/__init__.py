@@ -5,6 +5,8 @@ src/__init__.py:17-18) plus the MI355X device path (``DeviceLoader``), the
 synthetic broker and a kafka-python compatible client.  ``import torchkafka``
 is an alias of this package.
 """
+import numpy.random  # noqa: F401  -- import eagerly: a lazy import racing a DataLoader fork deadlocks/crashes workers
+
 from .loader import DeviceLoader, KafkaBatch, auto_commit
 from .models import FixedWidth, JsonArray, KafkaDataset, VarLen
 

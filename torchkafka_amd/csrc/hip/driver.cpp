@@ -9,6 +9,12 @@ MainDriver::MainDriver(Engine* engine, const std::string& ring_name, const std::
     : eng_(engine), prefetch_(std::max(0, prefetch)), in_order_(in_order), default_src_dt_(default_src_dt) {
   ring_ = tk::Ring::open(ring_name);
   if (int(ring_->n_slots()) > eng_->n_slots()) throw std::invalid_argument("driver: engine has fewer slots than ring");
+  // Pin THIS mapping of the ring: it is the one whose addresses the copies use
+  // (another mapping of the same shm object has different virtual addresses).
+  if (!eng_->host_registered()) {
+    eng_->register_host(ring_->base(), ring_->total_bytes());
+    registered_ = true;
+  }
   cursor_.assign(ring_->n_workers(), 0);
   done_.assign(ring_->n_workers(), 0);
   if (!broker_url.empty() && !group.empty()) {
@@ -19,6 +25,12 @@ MainDriver::MainDriver(Engine* engine, const std::string& ring_name, const std::
 }
 
 MainDriver::~MainDriver() {
+  if (registered_) {
+    try {
+      eng_->unregister_host();  // before ring_'s mapping goes away
+    } catch (...) {
+    }
+  }
   for (auto& f : fenced_) hipEventDestroy(std::get<0>(f));
   for (auto e : event_pool_) hipEventDestroy(e);
 }

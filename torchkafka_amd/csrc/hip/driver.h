@@ -105,6 +105,7 @@ class MainDriver {
   std::deque<std::pair<int64_t, std::vector<tk::Watermark>>> finished_q_;
 
   Engine* eng_;
+  bool registered_ = false;
   std::unique_ptr<tk::Ring> ring_;
   std::shared_ptr<tk::Broker> broker_;
   uint32_t group_ = 0;

@@ -109,9 +109,11 @@ def _multi_worker(dataloader: DataLoader, final_commit_timeout: float):
             consumed[w] += _batch_len(batch, bs)
             channel.request(w, consumed[w])
         # normal end: make sure every worker committed its final batch before shutdown
+        channel.close_requests()
         if not channel.wait_acks(final_commit_timeout, alive):
             log.warning("auto_commit: some workers did not acknowledge their final commit")
     finally:
+        channel.close_requests()  # a worker waiting to serve a last request may exit now
         try:
             batches._shutdown_workers()  # type: ignore[attr-defined]
         except Exception:  # noqa: BLE001

@@ -16,7 +16,8 @@ from multiprocessing import shared_memory
 
 import numpy as np
 
-_REQ, _ACK, _HDR = 0, 1, 2
+_REQ, _ACK, _HDR = 0, 1, 3
+_CLOSING = 2  # header word: the main process will send no further requests
 
 
 class CommitChannel:
@@ -63,6 +64,13 @@ class CommitChannel:
 
     def acked(self, worker: int) -> int:
         return int(self._arr[self._i(worker, _ACK)])
+
+    def close_requests(self) -> None:
+        """No more requests will come (end of iteration or the user broke out of the loop)."""
+        self._arr[_CLOSING] = 1
+
+    def closing(self) -> bool:
+        return bool(self._arr[_CLOSING])
 
     def wait_acks(self, timeout: float = 5.0, alive=None) -> bool:
         """Waits until every worker acknowledged its latest request; ``alive(w)`` can cut a dead worker short."""

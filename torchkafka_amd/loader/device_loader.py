@@ -113,7 +113,6 @@ class _Run:
                 dev = L.device.index if L.device.index is not None else torch.cuda.current_device()
                 mode = hip().H2D_ZERO_COPY if L.h2d == "zerocopy" else hip().H2D_DMA
                 self.engine = hip().Engine(dev, self.ring.n_slots, self.ring.payload_capacity, L.copy_streams, mode)
-                self.engine.register_host(self.ring.base_address, self.ring.total_bytes)
                 url, group = L._commit_target_url()
                 self.driver = hip().MainDriver(self.engine, self.name, url, group, L.prefetch, L.in_order,
                                                L._default_src_code())
@@ -198,15 +197,14 @@ class _Run:
             if p.is_alive():
                 p.terminate()
                 p.join(timeout=5)
-        self.driver = None
-        self.rccl = None
         if self.engine is not None:
             try:
                 self.engine.synchronize()
-                self.engine.unregister_host()
             except Exception:  # noqa: BLE001
                 log.exception("engine teardown failed")
-            self.engine = None
+        self.driver = None  # unregisters its pinned ring mapping
+        self.rccl = None
+        self.engine = None
         try:
             self.ring.unlink()
         except Exception:  # noqa: BLE001

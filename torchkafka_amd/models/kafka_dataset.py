@@ -201,8 +201,27 @@ class KafkaDataset(IterableDataset):
         self._channel_finalizer = mpu.Finalize(self, KafkaDataset._final_service, args=(self,), exitpriority=100)
 
     @staticmethod
-    def _final_service(ds) -> None:
+    def _final_service(ds, max_wait: float = 60.0) -> None:
+        """Worker exit hook: serve the commit of this worker's last batch.
+
+        The DataLoader may shut a worker down as soon as its end of stream is
+        seen -- possibly before the main process has even yielded that
+        worker's final batch -- so wait (bounded) until the main process has
+        requested everything this worker produced or announced it is done.
+        """
+        ch = ds._commit_channel
+        parent = os.getppid()
+        deadline = time.monotonic() + max_wait
         try:
+            while True:
+                with ds._consumer_lock:
+                    ds._service_channel()
+                total = getattr(ds, "_final_yielded", None)
+                if ch is None or total is None or ch.acked(ds._worker_id) >= total or ch.closing():
+                    break
+                if os.getppid() != parent or time.monotonic() > deadline:
+                    break
+                time.sleep(0.002)
             with ds._consumer_lock:
                 ds._service_channel()
         except Exception:  # noqa: BLE001 - the process is exiting
@@ -231,6 +250,7 @@ class KafkaDataset(IterableDataset):
         with self._channel_lock:
             self._snapshots = deque()
             self._channel_done = 0
+            self._final_yielded = None
         hooks = getattr(self._consumer, "_idle_hooks", None)
         if hooks is not None and self._service_channel not in hooks:
             hooks.append(self._service_channel)
@@ -258,6 +278,7 @@ class KafkaDataset(IterableDataset):
                 self._service_channel()
             with self._channel_lock:
                 self._snapshots.append((yielded, dict(positions)))
+            self._final_yielded = yielded
             self._service_channel()
         finally:
             cl.release()
