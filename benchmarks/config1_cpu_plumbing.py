@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""BASELINE config 1: single-process KafkaDataset on CPU, 1-partition topic, batch_size=4,
+``_process -> torch.rand(8)`` -- the reference's README example, plumbing only (no GPU).
+
+Path measured: synthetic broker -> KafkaConsumer iteration -> KafkaDataset.__iter__ /
+``_process`` -> torch DataLoader (num_workers=0, default_collate) -> auto_commit (one
+commit per batch).  Reference yardstick: 108,521 records/s on the same
+shape with an in-memory fake consumer.
+
+Usage: python benchmarks/config1_cpu_plumbing.py [--records N]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+YARDSTICK = 108521.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--records", type=int, default=200000)
+    ap.add_argument("--batch-size", type=int, default=4)
+    args = ap.parse_args()
+
+    import torch
+    from torch.utils.data import DataLoader
+
+    from torchkafka_amd import KafkaDataset, auto_commit
+    from torchkafka_amd.broker import SyntheticBroker
+
+    torch.set_num_threads(1)
+
+    class MyDataset(KafkaDataset):
+        def _process(self, record):
+            return torch.rand(8)
+
+    url = f"shm://tkcfg1-{os.getpid()}"
+    b = SyntheticBroker.create(url)
+    try:
+        b.create_topic("topic", 1)
+        b.fill("topic", args.records, "bytes", size=16, records_per_batch=500)
+        ds = MyDataset("topic", group_id="group_1", bootstrap_servers=url, auto_offset_reset="earliest",
+                       consumer_timeout_ms=200)
+        dl = DataLoader(ds, batch_size=args.batch_size)
+        n = 0
+        t0 = None
+        for i, batch in enumerate(auto_commit(dl)):
+            if i == 100:
+                t0 = time.perf_counter()
+                n = 0
+            n += batch.shape[0]
+        # the stream end includes one consumer_timeout_ms wait; exclude it
+        el = time.perf_counter() - t0 - 0.2
+        assert b.committed("group_1", "topic", 0) == args.records
+        v = n / el
+        print(json.dumps({"config": 1, "metric": "records/s (CPU plumbing, per-batch commit)", "value": round(v),
+                          "batch_size": args.batch_size, "records": n, "vs_yardstick": round(v / YARDSTICK, 3)}))
+    finally:
+        b.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""BASELINE config 4: variable-length JSON records, on-device pad/stack -> bf16 (HIP collate), batch 256.
+
+Records are JSON arrays of 16..256 numbers ("[-12.34, 5.06, ...]", ~1 KiB of text on
+average), as in the reference README's ``json.loads(record.value)`` example.  Workers
+parse them natively (C++ JSON -> CSR float32 in the pinned ring) and the gfx950
+var-len kernel pads/stacks/casts on the GPU.  The reference cannot collate this at
+all (variable-length lists fail default_collate).
+
+Usage: python benchmarks/config4_json_varlen.py [--steps K] [--device cuda:0]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--batch-size", type=int, default=256)
+    ap.add_argument("--workers", type=int, default=4)
+    ap.add_argument("--partitions", type=int, default=8)
+    ap.add_argument("--min-len", type=int, default=16)
+    ap.add_argument("--max-len", type=int, default=256)
+    ap.add_argument("--device", default="cuda:0")
+    args = ap.parse_args()
+
+    import torch
+
+    from torchkafka_amd import DeviceLoader, JsonArray, KafkaDataset, auto_commit
+    from torchkafka_amd.broker import SyntheticBroker
+
+    class Json(KafkaDataset):
+        schema = JsonArray()
+
+    url = f"shm://tkcfg4-{os.getpid()}"
+    b = SyntheticBroker.create(url, log_capacity=1 << 33)
+    try:
+        b.create_topic("json", args.partitions)
+        B = args.batch_size
+        per_part = int(math.ceil((args.steps + args.warmup + 8 * args.workers) * B * 1.3 / args.partitions))
+        t = time.perf_counter()
+        b.fill("json", per_part, "json_f32", size=args.min_len, max_size=args.max_len, threads=args.partitions)
+        fill_s = time.perf_counter() - t
+        dl = DeviceLoader(Json.placeholder(), B, num_workers=args.workers, device=args.device, dtype=torch.bfloat16,
+                          worker_init_fn=Json.init_worker("json", bootstrap_servers=url, group_id="cfg4",
+                                                          auto_offset_reset="earliest"))
+        it = iter(auto_commit(dl))
+        for _ in range(args.warmup):
+            x, lens = next(it)
+        if x.is_cuda:
+            torch.cuda.synchronize()
+        dl.reset_stats()
+        t0 = time.perf_counter()
+        rows = 0
+        elems = 0
+        for _ in range(args.steps):
+            x, lens = next(it)
+            rows += x.shape[0]
+        if x.is_cuda:
+            torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        st = dl.stats_summary()
+        it.close()
+        text_bytes = b.partition_stats("json", 0)["log_bytes"] / max(1, b.end_offset("json", 0))
+        print(json.dumps({"config": 4, "metric": "JSON records/s to GPU (bf16 padded), per-batch commit",
+                          "value": round(rows / el), "ms_per_step": round(el / args.steps * 1e3, 4),
+                          "batch_size": B, "avg_record_bytes": round(text_bytes), "last_batch_shape": list(x.shape),
+                          "device": args.device, "fill_s": round(fill_s, 2), "loader": st}))
+    finally:
+        b.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -21,7 +21,7 @@ for s in $STEPS; do
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     pytest) step pytest_gpu 600 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=150 --timeout-method=thread ;;
     nccl)   step nccl_probe 120 python tools/nccl_probe.py ;;
-    lockcheck) step lockstep_check 300 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29631 tools/lockstep_check.py ;;
+    lockcheck) step lockstep_check 150 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29631 tools/lockstep_check.py ;;
     bench)  step bench 600 python bench.py --stats ;;
     bench8) step bench_fp8 600 python bench.py --stats --dtype fp8 ;;
     benchlong) step bench_long 600 python bench.py --stats --steps 4000 --warmup 100 ;;

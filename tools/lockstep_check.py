@@ -15,6 +15,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    import faulthandler
+
+    faulthandler.dump_traceback_later(75, exit=True)  # a hang prints every thread's stack
     import torch
     import torch.distributed as dist
 
@@ -42,8 +45,10 @@ def main():
                           worker_init_fn=Vec.init_worker("t", bootstrap_servers=url, group_id=group,
                                                          auto_offset_reset="earliest", consumer_timeout_ms=500))
         steps, parts = 0, set()
+        print(f"[rank {rank}] depth {depth}: iterating", flush=True)
         for x in auto_commit(dl):
             steps += 1
+            print(f"[rank {rank}] depth {depth}: step {steps}", flush=True)
             parts |= set(x[:, 1].long().tolist())
         torch.cuda.synchronize()
         dist.barrier()

@@ -118,6 +118,8 @@ class KafkaConsumer:
         self._assignment: list[int] = []          # global partition indices
         self._paused: set[int] = set()
         self._buffer: deque = deque()
+        self._tp_cache: dict[int, TopicPartition] = {}
+        self._position: dict[int, int] = {}
         self._idle_hooks: list[Callable[[], None]] = []
         self._iter_deadline = None
         self._last_auto_commit = time.monotonic()
@@ -142,7 +144,17 @@ class KafkaConsumer:
             )
 
     def _tp(self, pidx: int) -> TopicPartition:
-        return self._broker.tp_of(pidx)
+        tp = self._tp_cache.get(pidx)
+        if tp is None:
+            tp = self._tp_cache[pidx] = self._broker.tp_of(pidx)
+        return tp
+
+    def _sync_positions(self) -> None:
+        """Consumed (returned-to-user) positions follow kafka-python: they advance as records are
+        returned, not as they are fetched.  Partitions without buffered records take the fetch position."""
+        buffered = {r[0] for r in self._buffer}
+        fetch = self._fetcher.positions()
+        self._position = {p: (self._position.get(p, fetch[p]) if p in buffered else fetch[p]) for p in fetch}
 
     def _pidx(self, tp: TopicPartition) -> int:
         return self._broker.pidx(tp.topic, tp.partition)
@@ -178,6 +190,7 @@ class KafkaConsumer:
             keep = set(pidxs)
             self._buffer = deque(r for r in self._buffer if r[0] in keep)
         self._assignment = pidxs
+        self._sync_positions()
 
     def _ensure_group(self, block: bool = True) -> None:
         """Joins / follows the consumer group (subscription mode).  kafka-python's coordinator poll."""
@@ -204,6 +217,7 @@ class KafkaConsumer:
             self._assignment = []
             self._fetcher.assign([], [])
             self._buffer.clear()
+            self._position = {}
             return self._ensure_group()
         if state != _GROUP_STABLE:
             if self._assignment:
@@ -232,6 +246,7 @@ class KafkaConsumer:
                 keep = set(pidxs)
                 self._buffer = deque(r for r in self._buffer if r[0] in keep)
             self._assignment = pidxs
+            self._sync_positions()
             if set(pidxs) != old:
                 log.debug("group %s generation %d assignment %s", self.config["group_id"], gen,
                           [self._tp(p) for p in pidxs])
@@ -245,16 +260,18 @@ class KafkaConsumer:
                 pos = self._fetcher.position(p)
                 if pos is not None and not lo <= pos <= hi:
                     self._fetcher.seek(p, self._reset_position(p))
+                    self._position[p] = self._fetcher.position(p)
             chunks = self._fetcher.poll_records(max_records)
         n = 0
+        buf = self._buffer
         for pidx, recs in chunks:
-            for r in recs:
-                self._buffer.append((pidx, r))
+            buf.extend((pidx, r) for r in recs)
             n += len(recs)
         return n
 
     def _make_record(self, pidx: int, r) -> ConsumerRecord:
-        tp = self._tp(pidx)
+        self._position[pidx] = r[0] + 1
+        tp = self._tp_cache.get(pidx) or self._tp(pidx)
         key, value = r[3], r[4]
         kd, vd = self.config["key_deserializer"], self.config["value_deserializer"]
         if kd is not None and key is not None:
@@ -341,10 +358,10 @@ class KafkaConsumer:
     def position(self, partition: TopicPartition) -> int:
         self._check_open()
         self._ensure_group()
-        pos = self._fetcher.position(self._pidx(partition))
-        if pos is None:
+        p = self._pidx(partition)
+        if p not in self._assignment:
             raise IllegalStateError(f"Partition {partition} is not assigned")
-        return pos
+        return self._position.get(p, self._fetcher.position(p))
 
     def seek(self, partition: TopicPartition, offset: int) -> None:
         self._check_open()
@@ -353,6 +370,7 @@ class KafkaConsumer:
         p = self._pidx(partition)
         self._fetcher.seek(p, int(offset))
         self._buffer = deque(r for r in self._buffer if r[0] != p)
+        self._position[p] = int(offset)
 
     def seek_to_beginning(self, *partitions) -> None:
         for tp in partitions or self.assignment():
@@ -460,11 +478,7 @@ class KafkaConsumer:
     # ------------------------------------------------------------------ commits
     def _consumed_offsets(self) -> dict[int, int]:
         """Positions of assigned partitions, excluding records still in the iteration buffer."""
-        pos = dict(self._fetcher.positions())
-        for pidx, r in self._buffer:
-            if r[0] < pos.get(pidx, r[0] + 1):
-                pos[pidx] = r[0]
-        return pos
+        return {p: self._position.get(p, 0) for p in self._assignment}
 
     def commit(self, offsets: dict | None = None) -> None:
         """Synchronously commits ``offsets`` (default: every consumed position).  Requires group_id."""
