@@ -38,7 +38,8 @@ def main():
         schema = FixedWidth(torch.float32, (8,))
 
     results = {}
-    for depth in (0, 2, 5):
+    depths = [int(d) for d in os.environ.get("LOCKCHECK_DEPTHS", "0,2,5").split(",")]
+    for depth in depths:
         group = f"g{depth}"
         dl = DeviceLoader(Vec.placeholder(), 10, num_workers=2, device="cuda:0", lockstep="host",
                           lockstep_depth=depth,

@@ -65,6 +65,8 @@ PYBIND11_MODULE(_tkhip, m) {
     return d;
   });
 
+  m.def("api_bench", &api_bench, py::arg("device") = 0, py::arg("iters") = 10000);
+
   m.def(
       "collate_fixed",
       [](uintptr_t src, int src_dt, uintptr_t dst, int dst_dt, int64_t rows, int64_t row, uintptr_t shift,

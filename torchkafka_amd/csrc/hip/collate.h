@@ -5,6 +5,8 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <utility>
+#include <vector>
 
 namespace tkh {
 
@@ -16,5 +18,7 @@ void launch_fixed(const void* src, int src_dt, void* dst, int dst_dt, int64_t ro
 // [rows, L] with `pad`; optional int64 lengths[rows] and uint8 mask[rows, L].
 void launch_varlen(const int32_t* offs, const void* vals, int src_dt, void* out, int dst_dt, int64_t rows, int64_t L,
                    double pad, int64_t* lengths, uint8_t* mask, hipStream_t stream);
+
+std::vector<std::pair<std::string, double>> api_bench(int device, int iters);
 
 }  // namespace tkh

@@ -15,6 +15,10 @@
 #include <hip/hip_runtime.h>
 
 #include "collate.h"
+
+#include <chrono>
+#include <string>
+#include <vector>
 #include "dtypes.h"
 
 namespace tkh {
@@ -260,6 +264,47 @@ void launch_varlen(const int32_t* offs, const void* vals, int src_dt, void* out,
   TK_DISPATCH_SRC(launch_varlen_t, offs, vals, out, rows, L, pad, lengths, mask, stream)
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("varlen collate launch: ") + hipGetErrorString(e));
+}
+
+__global__ void empty_kernel() {}
+
+// Host cost (ns per call, averaged over `iters`) of the HIP calls on the per-batch path.
+std::vector<std::pair<std::string, double>> api_bench(int device, int iters) {
+  std::vector<std::pair<std::string, double>> out;
+  hipSetDevice(device);
+  hipStream_t st;
+  hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  hipEvent_t ev;
+  hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  void* d = nullptr;
+  void* h = nullptr;
+  hipMalloc(&d, 1 << 20);
+  hipHostMalloc(&h, 1 << 20, hipHostMallocDefault);
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto time_it = [&](const char* name, auto&& fn) {
+    hipStreamSynchronize(st);
+    auto t0 = now();
+    for (int i = 0; i < iters; ++i) fn(i);
+    auto t1 = now();
+    hipStreamSynchronize(st);
+    out.emplace_back(name, std::chrono::duration<double, std::nano>(t1 - t0).count() / iters);
+  };
+  time_it("hipLaunchKernel(empty)", [&](int) { hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, st); });
+  time_it("hipEventRecord", [&](int) { hipEventRecord(ev, st); });
+  time_it("hipEventQuery", [&](int) { (void)hipEventQuery(ev); });
+  time_it("hipStreamWaitEvent", [&](int) { hipStreamWaitEvent(st, ev, 0); });
+  time_it("hipMemcpyAsync(4KiB pinned H2D)", [&](int) { hipMemcpyAsync(d, h, 4096, hipMemcpyHostToDevice, st); });
+  time_it("hipMemcpyAsync(256KiB pinned H2D)", [&](int) { hipMemcpyAsync(d, h, 262144, hipMemcpyHostToDevice, st); });
+  time_it("hipGetLastError", [&](int) { (void)hipGetLastError(); });
+  time_it("launch_fixed(256x256 f32->bf16)", [&](int) {
+    launch_fixed(h, kF32, d, kBF16, 256, 256, nullptr, nullptr, st);
+  });
+  hipStreamSynchronize(st);
+  hipFree(d);
+  hipHostFree(h);
+  hipEventDestroy(ev);
+  hipStreamDestroy(st);
+  return out;
 }
 
 }  // namespace tkh

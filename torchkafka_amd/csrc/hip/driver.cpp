@@ -1,6 +1,25 @@
 #include "driver.h"
 
+#include <unistd.h>
+
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
+namespace {
+const bool g_trace = [] {
+  const char* e = std::getenv("TORCHKAFKA_DRIVER_TRACE");
+  return e && e[0] == '1';
+}();
+}  // namespace
+#define DTRACE(...)                                       \
+  do {                                                    \
+    if (g_trace) {                                        \
+      std::fprintf(stderr, "[driver %d] ", int(getpid())); \
+      std::fprintf(stderr, __VA_ARGS__);                  \
+      std::fputc('\n', stderr);                           \
+    }                                                     \
+  } while (0)
 
 namespace tkh {
 
@@ -58,7 +77,10 @@ int MainDriver::poll_one(bool block, int64_t timeout_ms) {
       ring_->main_release(uint32_t(g));
       return -3;
     }
-    if (h->flags & tk::kSlotEOS) done_.at(h->worker) = 1;
+    if (h->flags & tk::kSlotEOS) {
+      done_.at(h->worker) = 1;
+      DTRACE("EOS from worker %u (rows %u)", h->worker, h->n_rows);
+    }
     fill_ns_ += h->t_ready_ns - h->t_fill_start_ns;
     ready_age_ns_ += tk::now_ns() - h->t_ready_ns;
     ++fills_;
@@ -126,55 +148,90 @@ bool MainDriver::pop_data(SlotView* out) {
 void MainDriver::enable_lockstep(LockstepTransport* ls, int depth) {
   ls_ = ls;
   depth_ = std::max(0, depth);
-  step_ = issued_ = 0;
+  step_ = granted_ = 0;
   delivered_index_ = -1;
-  stopped_ = false;
+  stopped_ = no_more_credit_ = false;
   tickets_.clear();
   finished_q_.clear();
 }
 
-// Step k may be delivered only if every rank has a batch for it.  The
-// agreement for step j is issued at step max(0, j - depth); its completion
-// proves every rank reached that step, i.e. finished every batch < j - depth,
-// which is what may be committed once it is read.
+// Cross-rank lockstep as a credit protocol.  Ranks deliver batch indices in
+// the same order; `granted_` is the index below which every rank is known to
+// hold a batch.  An agreement carries each rank's count of batches it holds
+// beyond `granted_` (what is staged now -- never a wait on data that a worker
+// cannot publish while its ring slots are all staged here), or -1 if its
+// stream has ended and it holds none.  MIN over ranks extends `granted_`; -1
+// means no further credit will ever come, so all ranks stop at the same
+// index.  A new agreement is issued while `depth` credits remain, so its
+// round trip overlaps the delivery of those batches.  Every decision depends
+// only on (step_, granted_) and agreement results, which are identical on all
+// ranks, so the collective sequences stay aligned.  Completion of an
+// agreement issued at step s proves every rank reached s: batches < s are
+// finished everywhere and become committable.
+int64_t MainDriver::credit_value() const {
+  const int64_t beyond = int64_t(data_staged()) - (granted_ - step_);
+  if (beyond > 0) return beyond;
+  return all_done() ? -1 : 0;
+}
+
+void MainDriver::issue_agreement() {
+  const int64_t v = credit_value();
+  DTRACE("step %ld issue agreement base=%ld value=%ld staged=%d", long(step_), long(granted_), long(v),
+         data_staged());
+  tickets_.push_back(Ticket{step_, granted_, ls_->issue(v, step_, -step_)});
+}
+
+void MainDriver::settle_agreement() {
+  const Ticket t = tickets_.front();
+  tickets_.pop_front();
+  int64_t res[3];
+  ls_->wait(t.ticket, res);
+  if (res[1] != -res[2])
+    throw std::runtime_error("lockstep: ranks are out of step (min " + std::to_string(res[1]) + ", max " +
+                             std::to_string(-res[2]) + ")");
+  while (!finished_q_.empty() && finished_q_.front().first < t.step) {
+    add_finished(finished_q_.front().second);
+    finished_q_.pop_front();
+  }
+  if (res[0] < 0)
+    no_more_credit_ = true;
+  else
+    granted_ = std::max(granted_, t.base + res[0]);
+  DTRACE("step %ld settled agreement from step %ld: min=%ld granted=%ld", long(step_), long(t.step), long(res[0]),
+         long(granted_));
+}
+
 int MainDriver::next_slot_lockstep(int64_t timeout_ms, SlotView* out) {
   if (stopped_) return -2;
-  while (int(staged_.size()) < prefetch_ + 1) {
+  // stage everything already published (non-blocking): these are the credits this rank can offer
+  for (;;) {
     int r = poll_one(false, 0);
     if (r == -3) return -3;
     if (r <= 0) break;
   }
-  while (issued_ <= step_ + depth_) {
-    const int need = int(issued_ - step_) + 1;
-    while (data_staged() < need && !all_done()) {
-      const int64_t t0 = tk::now_ns();
-      int r = poll_one(true, timeout_ms);
-      blocked_ns_ += tk::now_ns() - t0;
-      ++blocked_calls_;
-      if (r == -3) return -3;
-      if (r == -2) break;
-      if (r <= 0) return -1;  // timed out: the caller checks worker health and calls again
+  if (tickets_.empty() && !no_more_credit_ && granted_ - step_ <= depth_ && step_ < granted_) issue_agreement();
+  while (step_ >= granted_) {
+    if (no_more_credit_) {
+      stopped_ = true;
+      return -2;
     }
-    const bool have = data_staged() >= need;
-    tickets_.emplace_back(issued_, ls_->issue(have ? 1 : 0, issued_, -issued_));
-    ++issued_;
+    bool starved = false;
+    if (tickets_.empty()) {
+      if (data_staged() == 0 && !all_done()) {
+        // nothing to offer yet: give this rank's workers a moment before spending a collective round
+        const int64_t t0 = tk::now_ns();
+        int r = poll_one(true, timeout_ms);
+        blocked_ns_ += tk::now_ns() - t0;
+        ++blocked_calls_;
+        if (r == -3) return -3;
+        starved = (r == -1 || r == 0);
+      }
+      issue_agreement();  // value 0 when still starved: the other ranks wait with us, nobody hangs
+    }
+    settle_agreement();
+    if (starved && step_ >= granted_) return -1;  // let the caller check worker health, then call again
   }
-  const auto front = tickets_.front();
-  tickets_.pop_front();
-  int64_t res[3];
-  ls_->wait(front.second, res);
-  if (res[1] != -res[2])
-    throw std::runtime_error("lockstep: ranks are out of step (min " + std::to_string(res[1]) + ", max " +
-                             std::to_string(-res[2]) + ")");
-  while (!finished_q_.empty() && finished_q_.front().first < front.first - depth_) {
-    add_finished(finished_q_.front().second);
-    finished_q_.pop_front();
-  }
-  if (res[0] == 0) {
-    stopped_ = true;
-    return -2;
-  }
-  if (!pop_data(out)) throw std::logic_error("lockstep: agreed on a batch that is not staged");
+  if (!pop_data(out)) throw std::logic_error("lockstep: granted a batch that is not staged");
   delivered_index_ = step_++;
   return 1;
 }
@@ -182,6 +239,7 @@ int MainDriver::next_slot_lockstep(int64_t timeout_ms, SlotView* out) {
 void MainDriver::finish_lockstep() {
   drain_fenced(true);
   if (!ls_) return;
+  while (!tickets_.empty()) settle_agreement();  // every rank issued the same agreements
   int64_t res[3];
   ls_->wait(ls_->issue(0, 0, 0), res);  // every rank has stopped at the same step
   for (auto& f : finished_q_) add_finished(f.second);

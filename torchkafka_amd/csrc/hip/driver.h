@@ -97,11 +97,19 @@ class MainDriver {
   std::deque<std::tuple<hipEvent_t, int64_t, std::vector<tk::Watermark>>> fenced_;
   std::vector<hipEvent_t> event_pool_;
 
+  struct Ticket {
+    int64_t step;   // step at which it was issued
+    int64_t base;   // granted_ at issue time
+    int ticket;
+  };
+  int64_t credit_value() const;
+  void issue_agreement();
+  void settle_agreement();
   LockstepTransport* ls_ = nullptr;
   int depth_ = 2;
-  int64_t step_ = 0, issued_ = 0, delivered_index_ = -1;
-  bool stopped_ = false;
-  std::deque<std::pair<int64_t, int>> tickets_;
+  int64_t step_ = 0, granted_ = 0, delivered_index_ = -1;
+  bool stopped_ = false, no_more_credit_ = false;
+  std::deque<Ticket> tickets_;
   std::deque<std::pair<int64_t, std::vector<tk::Watermark>>> finished_q_;
 
   Engine* eng_;
