@@ -43,6 +43,8 @@ from ..ops.collate import CODE_DTYPE, DTYPE_CODE, FLOAT_DTYPES, normalize_params
 from ..ops.native import core, hip
 from ..parallel.sharding import dist_rank_world
 from ..utils.metrics import LoaderStats
+from ..utils.tracing import enabled as _roctx_enabled
+from ..utils.tracing import trace_range
 from .worker import worker_main
 
 log = logging.getLogger(__name__)
@@ -490,6 +492,23 @@ class DeviceLoader:
             run.close()
 
     def _fast_loop(self, run: _Run, auto_commit: bool, debug: bool):
+        if _roctx_enabled():
+            yield from self._fast_loop_traced(run, auto_commit, debug)
+            return
+        yield from self._fast_loop_plain(run, auto_commit, debug)
+
+    def _fast_loop_traced(self, run: _Run, auto_commit: bool, debug: bool):
+        """The fast loop with one roctx range per step (``TORCHKAFKA_ROCTX=1``)."""
+        gen = self._fast_loop_plain(run, auto_commit, debug)
+        while True:
+            with trace_range("torchkafka.next_batch"):
+                try:
+                    x = next(gen)
+                except StopIteration:
+                    return
+            yield x
+
+    def _fast_loop_plain(self, run: _Run, auto_commit: bool, debug: bool):
         drv = run.driver
         s = self.schema
         B, shape, row = self.batch_size, tuple(s.shape), s.row_elems
