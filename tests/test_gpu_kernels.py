@@ -126,3 +126,68 @@ def test_extension_is_native():
     assert mod.__file__.endswith(".so")
     info = mod.device_info(0)
     assert "gfx950" in info["gcn_arch"], info
+
+
+# ----------------------------------------------------------------------------- property-based (hypothesis)
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+_GPU_SETTINGS = settings(max_examples=40, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+
+
+@_GPU_SETTINGS
+@given(st.integers(0, 300), st.integers(1, 700), st.sampled_from(FLOATS), st.integers(0, 2 ** 16))
+def test_fixed_property(rows, row, dst, seed):
+    from torchkafka_amd.ops.collate import collate_fixed
+
+    src = special_f32(max(rows * row, 1), seed=seed)[: rows * row].view(rows, row)
+    out = collate_fixed(src.cuda(), dst)
+    assert_same(out, src.to(dst))
+
+
+@_GPU_SETTINGS
+@given(st.lists(st.integers(0, 5000), min_size=1, max_size=64), st.sampled_from(FLOATS),
+       st.one_of(st.none(), st.integers(1, 6000)), st.integers(0, 2 ** 16))
+def test_varlen_property(lens, dst, L, seed):
+    """Any length distribution (L=0 rows, one huge row, truncation) pads exactly like the torch reference."""
+    from torchkafka_amd.ops.collate import collate_varlen, reference_varlen
+
+    offs = torch.zeros(len(lens) + 1, dtype=torch.int32)
+    offs[1:] = torch.tensor(lens).cumsum(0).to(torch.int32)
+    vals = special_f32(max(int(offs[-1]), 1), seed=seed)[: int(offs[-1])]
+    width = L if L is not None else max(max(lens), 1)
+    out, ln, mask = collate_varlen(offs.cuda(), vals.cuda(), dst, L=width, pad_value=0.5, return_mask=True)
+    r_out, r_ln, r_mask = reference_varlen(offs, vals, dst, width, pad_value=0.5, return_mask=True)
+    assert_same(out, r_out)
+    assert torch.equal(ln.cpu(), r_ln)
+    assert torch.equal(mask.cpu(), r_mask)
+
+
+_SERIAL_SCRIPT = r"""
+import torch
+from torchkafka_amd.ops.collate import collate_fixed, collate_varlen, reference_varlen
+src = torch.randn(257, 333)
+assert torch.equal(collate_fixed(src.cuda(), torch.bfloat16).cpu().view(torch.int16),
+                   src.to(torch.bfloat16).view(torch.int16))
+lens = torch.tensor([0, 4097, 1, 300, 2048])
+offs = torch.zeros(6, dtype=torch.int32); offs[1:] = lens.cumsum(0).to(torch.int32)
+vals = torch.randn(int(offs[-1]))
+out, ln = collate_varlen(offs.cuda(), vals.cuda(), torch.float16, L=4097)
+r, rl = reference_varlen(offs, vals, torch.float16, 4097)
+assert torch.equal(out.cpu().view(torch.int16), r.view(torch.int16)) and torch.equal(ln.cpu(), rl)
+print("OK")
+"""
+
+
+def test_kernels_under_serialized_launches():
+    """re-run the kernels with launches serialised (AMD_SERIALIZE_KERNEL / HIP_LAUNCH_BLOCKING)
+    so a missing stream dependency cannot hide behind asynchrony."""
+    import os
+    import subprocess
+    import sys
+
+    env = dict(os.environ, AMD_SERIALIZE_KERNEL="3", AMD_SERIALIZE_COPY="3", HIP_LAUNCH_BLOCKING="1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _SERIAL_SCRIPT], env=env, cwd=root, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stderr[-2000:]
