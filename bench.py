@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--device", default=None, help="override device (e.g. cpu for a dry run)")
     ap.add_argument("--stats", action="store_true", help="print loader stats to stderr")
     ap.add_argument("--in-order", action="store_true", help="strict worker round-robin delivery")
-    ap.add_argument("--h2d", default="dma", choices=["dma", "zerocopy"])
+    ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy"])
     ap.add_argument("--copy-streams", type=int, default=4)
     ap.add_argument("--lockstep-depth", type=int, default=2)
     return ap.parse_args()
@@ -181,7 +181,7 @@ def main() -> int:
                 "partitions": n_parts,
                 "num_workers": args.workers,
                 "commit": "auto_commit per batch" + (", RCCL lockstep" if world > 1 else ""),
-                "h2d": args.h2d,
+                "h2d": loader._resolve_h2d(loader._slot_capacity()),
                 "bytes_per_step_per_gpu": B * args.dim * 4,
                 "gb_per_s": round(value * args.dim * 4 / 1e9, 3),
                 "commit_p99_us": round(stats["commit_p99_us"], 2),

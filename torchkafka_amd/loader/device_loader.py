@@ -113,7 +113,8 @@ class _Run:
             if L.device.type == "cuda":
                 # only after the fork: workers never inherit an initialised HIP runtime state they would use
                 dev = L.device.index if L.device.index is not None else torch.cuda.current_device()
-                mode = hip().H2D_ZERO_COPY if L.h2d == "zerocopy" else hip().H2D_DMA
+                mode = hip().H2D_ZERO_COPY if L._resolve_h2d(self.ring.payload_capacity) == "zerocopy" \
+                    else hip().H2D_DMA
                 self.engine = hip().Engine(dev, self.ring.n_slots, self.ring.payload_capacity, L.copy_streams, mode)
                 url, group = L._commit_target_url()
                 self.driver = hip().MainDriver(self.engine, self.name, url, group, L.prefetch, L.in_order,
@@ -241,7 +242,10 @@ class DeviceLoader:
             ``"always"``: also at world size 1).
         lockstep_depth: steps the per-step agreement is issued ahead (hides the collective's latency).
         h2d: ``"dma"`` (hipMemcpyAsync into device staging on ``copy_streams`` side streams, issued
-            ``prefetch`` batches ahead) or ``"zerocopy"`` (the collate kernel reads pinned host memory).
+            ``prefetch`` batches ahead), ``"zerocopy"`` (the collate kernel reads pinned host memory over
+            PCIe: two HIP calls per batch instead of five, but the read runs on the compute stream) or
+            ``"auto"`` (default: zero-copy for slots up to ``ZERO_COPY_MAX_BYTES``, where a batch is
+            latency-bound; DMA above, where copy/compute overlap matters).
     """
 
     def __init__(self, dataset, batch_size: int = 256, *, num_workers: int = 4, worker_init_fn=None,
@@ -252,7 +256,7 @@ class DeviceLoader:
                  multiprocessing_context: str = "fork", commit_on: str = "host", lockstep: bool = True,
                  rank: int | None = None, world_size: int | None = None, timeout: float = 0,
                  group_id: str | None = None, bootstrap_servers=None, base_seed: int | None = None,
-                 lockstep_depth: int = 2, h2d: str = "dma", copy_streams: int = 4):
+                 lockstep_depth: int = 2, h2d: str = "auto", copy_streams: int = 4):
         if batch_size < 1:
             raise ValueError("batch_size must be >= 1")
         if num_workers < 1:
@@ -289,8 +293,8 @@ class DeviceLoader:
         self.commit_on = commit_on
         self.lockstep = lockstep
         self.lockstep_depth = max(0, int(lockstep_depth))
-        if h2d not in ("dma", "zerocopy"):
-            raise ValueError("h2d must be 'dma' (hipMemcpyAsync on side streams) or 'zerocopy'")
+        if h2d not in ("auto", "dma", "zerocopy"):
+            raise ValueError("h2d must be 'auto', 'dma' (hipMemcpyAsync on side streams) or 'zerocopy'")
         self.h2d = h2d
         self.copy_streams = max(1, int(copy_streams))
         r, w = dist_rank_world()
@@ -329,6 +333,14 @@ class DeviceLoader:
             return resolve_url(self._servers), str(self._group_id)
         except Exception:  # noqa: BLE001 - not a synthetic broker: commits go through Python
             return "", ""
+
+    #: largest slot payload that ``h2d="auto"`` moves with zero-copy reads (above: DMA on side streams)
+    ZERO_COPY_MAX_BYTES = 1 << 20
+
+    def _resolve_h2d(self, slot_payload_bytes: int) -> str:
+        if self.h2d != "auto":
+            return self.h2d
+        return "zerocopy" if slot_payload_bytes <= self.ZERO_COPY_MAX_BYTES else "dma"
 
     def _default_src_code(self) -> int:
         s = self.schema
