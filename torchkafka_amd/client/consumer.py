@@ -23,6 +23,7 @@ import logging
 import os
 import time
 from collections import deque
+
 from typing import Callable, Iterable
 
 from ..broker.synthetic import open_broker, resolve_url
@@ -34,6 +35,7 @@ from .errors import (
 )
 from .records import ConsumerRecord, OffsetAndMetadata, TopicPartition
 
+_getpid = os.getpid
 log = logging.getLogger(__name__)
 
 _GROUP_STABLE = 2
@@ -252,8 +254,12 @@ class KafkaConsumer:
                           [self._tp(p) for p in pidxs])
 
     def _fetch_into_buffer(self, max_records: int) -> int:
+        tps = self._tp_cache
+        for p in self._assignment:
+            if p not in tps:
+                self._tp(p)
         try:
-            chunks = self._fetcher.poll_records(max_records)
+            recs = self._fetcher.poll_consumer_records(max_records, ConsumerRecord, tps)
         except OffsetOutOfRangeError:
             for p in self._assignment:
                 lo, hi = self._b.log_start_offset(p), self._b.high_watermark(p)
@@ -261,24 +267,19 @@ class KafkaConsumer:
                 if pos is not None and not lo <= pos <= hi:
                     self._fetcher.seek(p, self._reset_position(p))
                     self._position[p] = self._fetcher.position(p)
-            chunks = self._fetcher.poll_records(max_records)
-        n = 0
-        buf = self._buffer
-        for pidx, recs in chunks:
-            buf.extend((pidx, r) for r in recs)
-            n += len(recs)
-        return n
-
-    def _make_record(self, pidx: int, r) -> ConsumerRecord:
-        self._position[pidx] = r[0] + 1
-        tp = self._tp_cache.get(pidx) or self._tp(pidx)
-        key, value = r[3], r[4]
+            recs = self._fetcher.poll_consumer_records(max_records, ConsumerRecord, tps)
         kd, vd = self.config["key_deserializer"], self.config["value_deserializer"]
-        if kd is not None and key is not None:
-            key = kd(key)
-        if vd is not None and value is not None:
-            value = vd(value)
-        return ConsumerRecord(tp.topic, tp.partition, r[0], r[1], r[2], key, value, r[5], r[6], r[7], r[8], r[9])
+        if kd is not None or vd is not None:
+            # kafka-python deserializes while parsing fetched records (before iteration)
+            recs = [(p, r._replace(key=kd(r.key) if kd is not None and r.key is not None else r.key,
+                                   value=vd(r.value) if vd is not None and r.value is not None else r.value))
+                    for p, r in recs]
+        self._buffer.extend(recs)
+        return len(recs)
+
+    def _make_record(self, pidx: int, r: ConsumerRecord) -> ConsumerRecord:
+        self._position[pidx] = r.offset + 1
+        return r
 
     def _maybe_auto_commit(self) -> None:
         if self.config["enable_auto_commit"] and self._g is not None:
@@ -454,6 +455,11 @@ class KafkaConsumer:
 
     def __next__(self) -> ConsumerRecord:
         """Blocks for the next record; StopIteration after ``consumer_timeout_ms`` without one."""
+        buf = self._buffer
+        if buf and not self._closed and self._pid == _getpid():
+            pidx, r = buf.popleft()  # hot path: one record from the fetched buffer
+            self._position[pidx] = r[2] + 1
+            return r
         self._check_open()
         timeout = self.config["consumer_timeout_ms"]
         deadline = None if timeout == float("inf") else time.monotonic() + timeout / 1000.0
@@ -484,6 +490,15 @@ class KafkaConsumer:
         """Synchronously commits ``offsets`` (default: every consumed position).  Requires group_id."""
         self._check_open()
         assert self.config["group_id"] is not None, "Requires group_id"
+        if offsets is None and isinstance(self._assignment, list):
+            if self._manual or not self._subscription:
+                self._b.commit_positions(self._g, -1, 0, 0, self._assignment, self._position)
+            else:
+                if self._member_slot < 0:
+                    raise CommitFailedError("CommitFailedError: consumer is not part of an active group")
+                self._b.commit_positions(self._g, self._member_slot, self._member_id, self._generation,
+                                         self._assignment, self._position)
+            return
         if offsets is None:
             entries = [(p, int(o), "") for p, o in self._consumed_offsets().items()]
         else:

@@ -262,6 +262,21 @@ PYBIND11_MODULE(_tkcore, m) {
              for (auto& e : entries) es.push_back(CommitEntry{std::get<0>(e), std::get<1>(e), std::get<2>(e)});
              b.commit(g, slot, mid, gen, es);
            })
+      .def("commit_positions",
+           [](Broker& b, uint32_t g, int slot, uint64_t mid, uint32_t gen, py::list assignment, py::dict positions) {
+             // The consumer's default commit: every assigned partition at its consumed position
+             // (0 when nothing was consumed yet), without building Python entry tuples.
+             std::vector<CommitEntry> es;
+             es.reserve(py::len(assignment));
+             for (py::handle h : assignment) {
+               PyObject* v = PyDict_GetItem(positions.ptr(), h.ptr());  // borrowed
+               const int64_t off = v ? PyLong_AsLongLong(v) : 0;
+               if (off == -1 && PyErr_Occurred()) throw py::error_already_set();
+               es.push_back(CommitEntry{h.cast<uint32_t>(), off, std::string()});
+             }
+             if (es.empty()) return;
+             b.commit(g, slot, mid, gen, es);
+           })
       .def("committed",
            [](Broker& b, uint32_t g, uint32_t pidx) {
              std::string meta;
@@ -337,6 +352,64 @@ PYBIND11_MODULE(_tkcore, m) {
             return out;
           },
           py::arg("max_records"))
+      .def(
+          "poll_consumer_records",
+          [](PyFetcher& f, int64_t max_records, py::object record_cls, py::dict tps) {
+            // Like poll_records, but builds the kafka-python ConsumerRecord namedtuples here:
+            // returns [(pidx, ConsumerRecord)], one flat list, in fetch order.  `tps` maps
+            // pidx -> TopicPartition for every assigned partition.
+            if (!PyType_Check(record_cls.ptr()) || !PyType_IsSubtype(reinterpret_cast<PyTypeObject*>(record_cls.ptr()),
+                                                                     &PyTuple_Type))
+              throw std::invalid_argument("record_cls must be a tuple subclass (namedtuple)");
+            PyTypeObject* cls = reinterpret_cast<PyTypeObject*>(record_cls.ptr());
+            py::list out;
+            auto& parts = f.f.parts();
+            int64_t left = max_records;
+            py::object none = py::none();
+            for (size_t k = 0; k < parts.size() && left > 0; ++k) {
+              FetchPart& fp = parts[(f.rr + k) % parts.size()];
+              if (fp.paused) continue;
+              py::object tp = tps[py::int_(fp.pidx)];
+              py::object topic = tp.attr("__getitem__")(0), part = tp.attr("__getitem__")(1);
+              py::int_ pidx(fp.pidx);
+              size_t got = f.f.scan(fp, size_t(left), [&](const RecordView& r) {
+                // tuple_subtype_new's layout: allocate the namedtuple directly and fill its items
+                PyObject* o = cls->tp_alloc(cls, 12);
+                if (!o) throw py::error_already_set();
+                py::list headers;
+                if (r.header_count > 0) {
+                  for (const auto& h : parse_headers(r)) {
+                    headers.append(py::make_tuple(py::str(reinterpret_cast<const char*>(h.key), size_t(h.key_len)),
+                                                  bytes_or_none(h.value, h.value_len)));
+                  }
+                }
+                PyObject* items[12] = {
+                    topic.inc_ref().ptr(),
+                    part.inc_ref().ptr(),
+                    PyLong_FromLongLong(r.offset),
+                    PyLong_FromLongLong(r.timestamp),
+                    PyLong_FromLong(0),
+                    bytes_or_none(r.key, r.key_len).release().ptr(),
+                    bytes_or_none(r.value, r.value_len).release().ptr(),
+                    headers.release().ptr(),
+                    none.inc_ref().ptr(),
+                    PyLong_FromLong(r.key_len),
+                    PyLong_FromLong(r.value_len),
+                    PyLong_FromLong(r.header_bytes),
+                };
+                for (int i = 0; i < 12; ++i) PyTuple_SET_ITEM(o, i, items[i]);
+                PyObject* pair = PyTuple_New(2);
+                PyTuple_SET_ITEM(pair, 0, pidx.inc_ref().ptr());
+                PyTuple_SET_ITEM(pair, 1, o);
+                out.append(py::reinterpret_steal<py::object>(pair));
+                return kTake;
+              });
+              left -= int64_t(got);
+            }
+            if (!parts.empty()) f.rr = (f.rr + 1) % parts.size();
+            return out;
+          },
+          py::arg("max_records"), py::arg("record_cls"), py::arg("tps"))
       .def(
           "fill_slot",
           [](PyFetcher& f, py::object ring_obj, uint32_t gslot, int kind, int elem_size, int64_t row_elems,

@@ -110,7 +110,7 @@ class KafkaDataset(IterableDataset):
         if self._consumer is None:
             raise RuntimeError("Consumer is not initialized.")
         if self._worker_id is None:
-            self._commit_if_required(force=True)
+            self._do_commit()  # forced: _commit_if_required(force=True)
         elif signum is not None:
             if signum != self._COMMIT_SIGNAL:
                 raise ValueError(f"Worker {self._worker_id} received a bad signal ({signum}).")
