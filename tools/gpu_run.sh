@@ -33,8 +33,11 @@ for s in $STEPS; do
     benchw8) step bench_w8 600 python bench.py --stats --steps 4000 --warmup 100 --workers 8 ;;
     benchnont) TORCHKAFKA_NT_COPY=0 step bench_nont 600 python bench.py --stats --steps 4000 --warmup 100 ;;
     benchbs) step bench_bs1024 600 python bench.py --stats --steps 2000 --warmup 100 --batch-size 1024 ;;
-    profcopy) (cd /tmp && export TMPDIR=/tmp && step profcopy 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profcopy" -o run -- python3 "$OLDPWD/bench.py" --steps 1000) ;;
-    prof)   (cd /tmp && export TMPDIR=/tmp && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$OLDPWD/bench.py" --steps 200) ;;
+    kbench) step kernel_bench 300 python tools/kernel_bench.py ;;
+    pmc)    (cd /tmp && export TMPDIR=/tmp && step pmc_bytes 300 rocprofv3 --pmc FETCH_SIZE WRITE_SIZE --output-format csv -d "$OUT/pmc_bytes" -o run -- python3 "$OLDPWD/tools/kernel_bench.py" --quick) || exit $?
+            (cd /tmp && export TMPDIR=/tmp && step pmc_lds 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAVES --output-format csv -d "$OUT/pmc_lds" -o run -- python3 "$OLDPWD/tools/kernel_bench.py" --quick) || exit $? ;;
+    profcopy) (cd /tmp && export TMPDIR=/tmp && step profcopy 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profcopy" -o run -- python3 "$OLDPWD/bench.py" --steps 1000) || exit $? ;;
+    prof)   (cd /tmp && export TMPDIR=/tmp && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$OLDPWD/bench.py" --steps 200) || exit $? ;;
   esac
 done
 echo "=== done"

@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""Device-resident throughput of the gfx950 collate kernels vs PyTorch's own kernels.
+
+Inputs already live in HBM, so this measures the kernels alone (the loader's H2D is
+measured by bench.py).  For each case it prints µs per call and the effective HBM
+bandwidth (bytes read + bytes written) / time, next to the equivalent PyTorch op
+(``Tensor.to`` for the cast, an index_put-based pad for var-len).
+
+Usage: python tools/kernel_bench.py [--quick] [--iters N]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, iters):
+    import torch
+
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) * 1000.0 / iters  # µs
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true", help="fewer iterations (for counter collection)")
+    ap.add_argument("--iters", type=int, default=200)
+    args = ap.parse_args()
+    iters = 20 if args.quick else args.iters
+
+    import torch
+
+    from torchkafka_amd.ops.collate import collate_fixed, collate_varlen
+    from torchkafka_amd.ops.native import hip
+
+    hip()
+    dev = torch.device("cuda", 0)
+    out = []
+
+    fixed_cases = [("config2 batch 256x256 f32->bf16", 256, 256, torch.bfloat16),
+                   ("256x256 f32->fp8e4m3", 256, 256, torch.float8_e4m3fn),
+                   ("bs1024 1024x256 f32->bf16", 1024, 256, torch.bfloat16),
+                   ("config5 8x262144 f32->bf16 (8 MiB)", 8, 262144, torch.bfloat16),
+                   ("64x262144 f32->bf16 (64 MiB)", 64, 262144, torch.bfloat16),
+                   ("256x262144 f32->bf16 (256 MiB)", 256, 262144, torch.bfloat16)]
+    for name, rows, row, dt in fixed_cases:
+        src = torch.randn(rows, row, device=dev)
+        t_ours = timeit(lambda: collate_fixed(src, dt), iters)
+        t_torch = timeit(lambda: src.to(dt), iters)
+        nbytes = src.numel() * 4 + src.numel() * torch.empty((), dtype=dt).element_size()
+        out.append({"kernel": "fixed", "case": name, "us": round(t_ours, 2), "GBps": round(nbytes / t_ours / 1e3, 1),
+                    "torch_us": round(t_torch, 2), "torch_GBps": round(nbytes / t_torch / 1e3, 1)})
+
+    g = torch.Generator().manual_seed(0)
+    var_cases = [("config4 256 rows, L~U(0,512) f32->bf16", 256, 512), ("256 rows, L~U(0,8192)", 256, 8192),
+                 ("4096 rows, L~U(0,4096)", 4096, 4096)]
+    for name, rows, lmax in var_cases:
+        lens = torch.randint(0, lmax + 1, (rows,), generator=g)
+        offs = torch.zeros(rows + 1, dtype=torch.int32)
+        offs[1:] = lens.cumsum(0).to(torch.int32)
+        vals = torch.randn(int(offs[-1]), device=dev)
+        offs_d = offs.to(dev)
+        L = int(lens.max())
+        esz_in = vals.numel() * 4
+        nbytes = esz_in + rows * L * 2
+
+        buf = torch.zeros(vals.numel() * 4 + 64, dtype=torch.uint8, device=dev)
+        buf[: vals.numel() * 4].copy_(vals.view(torch.uint8))
+        o = torch.empty((rows, L), dtype=torch.bfloat16, device=dev)
+        ln = torch.empty(rows, dtype=torch.int64, device=dev)
+        mod = hip()
+        stream = torch.cuda.current_stream(dev).cuda_stream
+
+        def ours():
+            mod.collate_varlen(offs_d.data_ptr(), buf.data_ptr(), 0, o.data_ptr(), 2, rows, L, 0.0, ln.data_ptr(), 0,
+                               stream)
+
+        row_idx = torch.repeat_interleave(torch.arange(rows, device=dev), lens.to(dev))
+        col_idx = torch.arange(vals.numel(), device=dev) - offs_d[:-1].long().repeat_interleave(lens.to(dev))
+
+        def torch_pad():
+            t = torch.zeros((rows, L), dtype=torch.bfloat16, device=dev)
+            t[row_idx, col_idx] = vals.to(torch.bfloat16)
+            return t
+
+        # numerics check once
+        ours()
+        assert torch.equal(o.view(torch.int16), torch_pad().view(torch.int16))
+        _ = collate_varlen(offs_d, vals, torch.bfloat16, L=L)
+        t_ours = timeit(ours, iters)
+        t_torch = timeit(torch_pad, iters)
+        out.append({"kernel": "varlen", "case": name, "us": round(t_ours, 2), "GBps": round(nbytes / t_ours / 1e3, 1),
+                    "torch_us": round(t_torch, 2), "torch_GBps": round(nbytes / t_torch / 1e3, 1)})
+
+    for r in out:
+        print(json.dumps(r))
+
+
+if __name__ == "__main__":
+    main()
