@@ -3,6 +3,8 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <deque>
+
 #include "broker.h"
 #include "consumer.h"
 #include "crc32c.h"
@@ -51,11 +53,12 @@ struct PyRing {
 
 std::vector<RecordIn> to_records(const std::vector<py::object>& values, const std::vector<py::object>& keys,
                                  const std::vector<int64_t>& timestamps, const std::vector<py::object>& headers,
-                                 std::vector<std::string>& keep, std::vector<std::vector<HeaderView>>& hkeep) {
+                                 std::deque<std::string>& keep, std::vector<std::vector<HeaderView>>& hkeep) {
+  // `keep` is a deque: growing it never moves the strings that RecordIn/HeaderView point into
+  // (a vector would, and short strings keep their bytes inline).
   const size_t n = values.size();
   if (keys.size() != n || timestamps.size() != n || headers.size() != n)
     throw std::invalid_argument("values/keys/timestamps/headers length mismatch");
-  keep.reserve(n * 2 + 16);
   hkeep.resize(n);
   std::vector<RecordIn> recs(n);
   auto hold = [&](const py::object& o, const uint8_t** p, int32_t* len) {
@@ -124,7 +127,7 @@ PYBIND11_MODULE(_tkcore, m) {
       "encode_batch",
       [](int64_t base_offset, std::vector<py::object> values, std::vector<py::object> keys,
          std::vector<int64_t> timestamps, std::vector<py::object> headers) {
-        std::vector<std::string> keep;
+        std::deque<std::string> keep;
         std::vector<std::vector<HeaderView>> hkeep;
         auto recs = to_records(values, keys, timestamps, headers, keep, hkeep);
         int64_t min_ts = timestamps.empty() ? 0 : *std::min_element(timestamps.begin(), timestamps.end());
@@ -227,7 +230,7 @@ PYBIND11_MODULE(_tkcore, m) {
           "append",
           [](Broker& b, uint32_t pidx, std::vector<py::object> values, std::vector<py::object> keys,
              std::vector<int64_t> timestamps, std::vector<py::object> headers) {
-            std::vector<std::string> keep;
+            std::deque<std::string> keep;
             std::vector<std::vector<HeaderView>> hkeep;
             auto recs = to_records(values, keys, timestamps, headers, keep, hkeep);
             py::gil_scoped_release nogil;

@@ -103,10 +103,15 @@ def reference_varlen(offsets: torch.Tensor, values: torch.Tensor, dtype: torch.d
         out = torch.full((rows, L), float(pad_value), dtype=torch.float32, device=values.device).to(dtype)
     else:
         out = torch.full((rows, L), int(pad_value), dtype=torch.int64, device=values.device).to(dtype)
-    for r in range(rows):
-        n = int(lens[r])
-        if n:
-            out[r, :n] = values[int(offs[r]): int(offs[r]) + n].to(dtype)
+    if rows and int(lens.sum()):
+        # vectorised scatter (no per-row Python loop): element j of row r lands at out[r, j]
+        dev = values.device
+        lens_d, starts = lens.to(dev), offs[:-1].to(dev)
+        row_idx = torch.repeat_interleave(torch.arange(rows, device=dev), lens_d)
+        first = torch.cumsum(lens_d, 0) - lens_d  # position of each row's first element in the gather
+        col_idx = torch.arange(int(lens.sum()), device=dev) - torch.repeat_interleave(first, lens_d)
+        src_idx = torch.repeat_interleave(starts, lens_d) + col_idx
+        out[row_idx, col_idx] = values[src_idx].to(dtype)
     lengths = lens.to(values.device)
     if return_mask:
         mask = torch.arange(L, device=values.device)[None, :] < lengths[:, None]
