@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--device", default=None, help="override device (e.g. cpu for a dry run)")
     ap.add_argument("--stats", action="store_true", help="print loader stats to stderr")
     ap.add_argument("--in-order", action="store_true", help="strict worker round-robin delivery")
+    ap.add_argument("--event-every", type=int, default=None)
     ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy"])
     ap.add_argument("--copy-streams", type=int, default=4)
     ap.add_argument("--lockstep-depth", type=int, default=2)
@@ -106,6 +107,7 @@ def main() -> int:
         Records.placeholder(), B, num_workers=args.workers, device=device, dtype=dtype,
         slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
         in_order=args.in_order, h2d=args.h2d, copy_streams=args.copy_streams, lockstep_depth=args.lockstep_depth,
+        event_every=args.event_every,
         worker_init_fn=Records.init_worker("bench", bootstrap_servers=url, group_id="bench",
                                            auto_offset_reset="earliest", check_crcs=not args.no_crc),
     )

@@ -13,7 +13,8 @@ def special_f32(n: int, seed: int = 0) -> torch.Tensor:
     specials = torch.tensor([0.0, -0.0, float("inf"), float("-inf"), float("nan"), 1e-40, -1e-42, 448.0, 449.0,
                              464.0, 479.9, 480.0, 65504.0, 65520.0, 3.0e38, 2 ** -9, 2 ** -10, 0.0009765625,
                              1.0 + 2 ** -8, 1.0 + 3 * 2 ** -9, -3.5, 2 ** -6, 2 ** -7 * 1.5])
-    x[: specials.numel()] = specials
+    k = min(n, specials.numel())
+    x[:k] = specials[:k]
     return x
 
 
@@ -74,6 +75,20 @@ def test_fixed_other_sources(src_dt, dst):
         src = torch.randint(max(info.min, -1000), min(info.max, 1000), (33, 64), dtype=torch.int64).to(src_dt)
     out = collate_fixed(src.cuda(), dst)
     assert_same(out, src.to(dst))
+
+
+@pytest.mark.parametrize("rows", [1024, 1031])
+def test_fixed_unrolled_tiles(rows):
+    """>= 256*256*4 groups: the 4-deep unrolled kernel, including a ragged last tile."""
+    from torchkafka_amd.ops.collate import collate_fixed
+
+    src = special_f32(rows * 2048, seed=rows).view(rows, 2048)
+    for dt in (torch.bfloat16, torch.float8_e4m3fn):
+        assert_same(collate_fixed(src.cuda(), dt), src.to(dt))
+    mean, std = torch.randn(2048), torch.rand(2048) + 0.5
+    from torchkafka_amd.ops.collate import reference_fixed
+    assert_same(collate_fixed(src.cuda(), torch.bfloat16, normalize=(mean, std)),
+                reference_fixed(src, torch.bfloat16, normalize=(mean, std)))
 
 
 def test_fixed_large_grid_stride():

@@ -45,15 +45,16 @@ def test_fixed_f32_exact_records_and_commits(broker, workers):
     assert broker.committed_offsets("g", "t") == {p: 300 for p in range(6)}
 
 
-@pytest.mark.parametrize("h2d,streams", [("dma", 1), ("dma", 4), ("zerocopy", 4)])
-def test_h2d_modes_deliver_identical_batches(broker, h2d, streams):
+@pytest.mark.parametrize("h2d,streams,every", [("dma", 1, 1), ("dma", 4, 1), ("zerocopy", 4, 1), ("dma", 4, 3),
+                                               ("zerocopy", 2, 5)])
+def test_h2d_modes_deliver_identical_batches(broker, h2d, streams, every):
     from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
 
     broker.create_topic("t", 4)
     broker.fill("t", 400, "fixed_f32", size=64, records_per_batch=37)
     DS = _dataset(FixedWidth(torch.float32, (64,)))
     dl = DeviceLoader(DS.placeholder(), 50, num_workers=2, device="cuda:0", h2d=h2d, copy_streams=streams,
-                      slots_per_worker=3, prefetch=3,
+                      slots_per_worker=3, prefetch=3, event_every=every,
                       worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id="g",
                                                     auto_offset_reset="earliest", consumer_timeout_ms=300))
     rows = []
@@ -180,3 +181,31 @@ def test_smoke_entry():
     import __graft_entry__
 
     __graft_entry__.smoke()
+
+
+def test_batched_events_with_stream_switches(broker):
+    """Slots without their own completion event are released by a later event on the SAME
+    stream; switching the user's stream must first cover them on the old one."""
+    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
+
+    broker.create_topic("t", 2)
+    broker.fill("t", 320, "fixed_f32", size=16, records_per_batch=20)
+    DS = _dataset(FixedWidth(torch.float32, (16,)))
+    dl = DeviceLoader(DS.placeholder(), 16, num_workers=2, device="cuda:0", event_every=4, slots_per_worker=2,
+                      worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    rows = []
+    it = iter(auto_commit(dl))
+    i = 0
+    while True:
+        with torch.cuda.stream(streams[(i // 3) % 2]):
+            try:
+                x = next(it)
+            except StopIteration:
+                break
+            torch.cuda._sleep(200_000)
+            rows += [tuple(r) for r in x[:, :2].long().tolist()]
+        i += 1
+    assert len(rows) == len(set(rows)) == 640
+    assert broker.committed_offsets("g", "t") == {0: 320, 1: 320}

@@ -32,10 +32,15 @@ for s in $STEPS; do
     benchs1) step bench_s1 600 python bench.py --stats --steps 4000 --warmup 100 --copy-streams 1 ;;
     benchw8) step bench_w8 600 python bench.py --stats --steps 4000 --warmup 100 --workers 8 ;;
     benchnont) TORCHKAFKA_NT_COPY=0 step bench_nont 600 python bench.py --stats --steps 4000 --warmup 100 ;;
+    benchee1) step bench_ee1 600 python bench.py --stats --steps 4000 --warmup 100 --event-every 1 ;;
+    benchee4) step bench_ee4 600 python bench.py --stats --steps 4000 --warmup 100 --event-every 4 ;;
+    benchdma) step bench_dma 600 python bench.py --stats --steps 4000 --warmup 100 --h2d dma ;;
     benchbs) step bench_bs1024 600 python bench.py --stats --steps 2000 --warmup 100 --batch-size 1024 ;;
     kbench) step kernel_bench 300 python tools/kernel_bench.py ;;
-    pmc)    (cd /tmp && export TMPDIR=/tmp && step pmc_bytes 300 rocprofv3 --pmc FETCH_SIZE WRITE_SIZE --output-format csv -d "$OUT/pmc_bytes" -o run -- python3 "$OLDPWD/tools/kernel_bench.py" --quick) || exit $?
-            (cd /tmp && export TMPDIR=/tmp && step pmc_lds 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAVES --output-format csv -d "$OUT/pmc_lds" -o run -- python3 "$OLDPWD/tools/kernel_bench.py" --quick) || exit $? ;;
+    kprof)  (cd /tmp && export TMPDIR=/tmp && step kprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kprof" -o run -- python3 "$OLDPWD/tools/kernel_bench.py" --quick) || exit $? ;;
+    # TCC has 4 slots per pass: FETCH_SIZE costs 3, WRITE_SIZE 2 (MI355X_MICROARCH.md) -> two passes
+    pmc)    (cd /tmp && export TMPDIR=/tmp && step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 "$OLDPWD/tools/kernel_bench.py" --quick) || exit $?
+            (cd /tmp && export TMPDIR=/tmp && step pmc_write 300 rocprofv3 --pmc WRITE_SIZE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_INSTS_VMEM_WR --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$OLDPWD/tools/kernel_bench.py" --quick) || exit $? ;;
     profcopy) (cd /tmp && export TMPDIR=/tmp && step profcopy 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profcopy" -o run -- python3 "$OLDPWD/bench.py" --steps 1000) || exit $? ;;
     prof)   (cd /tmp && export TMPDIR=/tmp && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$OLDPWD/bench.py" --steps 200) || exit $? ;;
   esac

@@ -21,6 +21,17 @@ void futex_wake_all(std::atomic<uint32_t>* addr) {
   syscall(SYS_futex, reinterpret_cast<uint32_t*>(addr), FUTEX_WAKE, INT_MAX, nullptr, nullptr, 0);
 }
 
+void bump_and_wake(std::atomic<uint32_t>* seq, std::atomic<uint32_t>* waiters) {
+  seq->fetch_add(1, std::memory_order_seq_cst);
+  if (waiters->load(std::memory_order_seq_cst) != 0) futex_wake_all(seq);
+}
+
+void wait_seq(std::atomic<uint32_t>* seq, std::atomic<uint32_t>* waiters, uint32_t seen, int64_t timeout_ns) {
+  waiters->fetch_add(1, std::memory_order_seq_cst);
+  if (seq->load(std::memory_order_seq_cst) == seen) futex_wait(seq, seen, timeout_ns);
+  waiters->fetch_sub(1, std::memory_order_seq_cst);
+}
+
 std::unique_ptr<Ring> Ring::create(const std::string& name, uint32_t n_workers, uint32_t slots_per_worker,
                                    uint64_t payload_capacity) {
   if (n_workers == 0 || n_workers > kMaxWorkers) throw std::invalid_argument("ring: bad worker count");
@@ -48,7 +59,12 @@ std::unique_ptr<Ring> Ring::create(const std::string& name, uint32_t n_workers, 
   h->total_bytes = total;
   h->shutdown.store(0);
   h->ready_seq.store(0);
-  for (int w = 0; w < kMaxWorkers; ++w) { h->free_seq[w].store(0); h->worker_pid[w].store(0); }
+  h->ready_waiters.store(0);
+  for (int w = 0; w < kMaxWorkers; ++w) {
+    h->free_seq[w].store(0);
+    h->free_waiters[w].store(0);
+    h->worker_pid[w].store(0);
+  }
   for (uint32_t s = 0; s < n_workers * slots_per_worker; ++s) {
     SlotHeader* sh = r->slot(s);
     sh->state.store(kSlotFree);
@@ -102,7 +118,7 @@ bool Ring::worker_acquire(uint32_t worker, uint32_t i, int64_t timeout_ms) {
     }
     const int64_t now = now_ns();
     if (now >= deadline) return false;
-    futex_wait(&hdr_->free_seq[worker], seq, std::min<int64_t>(deadline - now, 100000000LL));
+    wait_seq(&hdr_->free_seq[worker], &hdr_->free_waiters[worker], seq, std::min<int64_t>(deadline - now, 100000000LL));
   }
 }
 
@@ -113,8 +129,7 @@ void Ring::worker_publish(uint32_t g) {
 #endif
   s->t_ready_ns = now_ns();
   s->state.store(kSlotReady, std::memory_order_release);
-  hdr_->ready_seq.fetch_add(1, std::memory_order_acq_rel);
-  futex_wake_all(&hdr_->ready_seq);
+  bump_and_wake(&hdr_->ready_seq, &hdr_->ready_waiters);
 }
 
 int64_t Ring::main_acquire(uint32_t* cursor, uint32_t* rr, const uint8_t* done, bool in_order, int64_t timeout_ms) {
@@ -145,7 +160,7 @@ int64_t Ring::main_acquire(uint32_t* cursor, uint32_t* rr, const uint8_t* done, 
       cpu_relax();
       continue;
     }
-    futex_wait(&hdr_->ready_seq, seq, std::min<int64_t>(deadline - now, 20000000LL));
+    wait_seq(&hdr_->ready_seq, &hdr_->ready_waiters, seq, std::min<int64_t>(deadline - now, 20000000LL));
   }
 }
 
@@ -153,8 +168,7 @@ void Ring::main_release(uint32_t g) {
   SlotHeader* s = slot(g);
   const uint32_t w = s->worker;
   s->state.store(kSlotFree, std::memory_order_release);
-  hdr_->free_seq[w].fetch_add(1, std::memory_order_acq_rel);
-  futex_wake_all(&hdr_->free_seq[w]);
+  bump_and_wake(&hdr_->free_seq[w], &hdr_->free_waiters[w]);
 }
 
 void Ring::shutdown() {

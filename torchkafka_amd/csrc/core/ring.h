@@ -68,7 +68,9 @@ struct alignas(64) RingHeader {
   uint64_t slot_stride, payload_capacity, total_bytes;
   std::atomic<uint32_t> shutdown;
   std::atomic<uint32_t> ready_seq;  // futex: bumped on every publish
+  std::atomic<uint32_t> ready_waiters;  // main blocked in futex_wait on ready_seq (0/1)
   alignas(64) std::atomic<uint32_t> free_seq[kMaxWorkers];  // futex per worker: bumped on release
+  alignas(64) std::atomic<uint32_t> free_waiters[kMaxWorkers];  // worker blocked on free_seq[w]
   alignas(64) std::atomic<int64_t> worker_pid[kMaxWorkers];
 };
 
@@ -118,5 +120,11 @@ class Ring {
 // futex helpers on a shared mapping (non-private futexes).
 void futex_wait(std::atomic<uint32_t>* addr, uint32_t expected, int64_t timeout_ns);
 void futex_wake_all(std::atomic<uint32_t>* addr);
+
+// Bumps `seq` and wakes its waiters, skipping the syscall when nobody sleeps on it.
+// Pairs with wait_seq(): both sides use seq_cst, so either the waker sees the
+// waiter's registration or the waiter sees the new sequence value (no lost wakeup).
+void bump_and_wake(std::atomic<uint32_t>* seq, std::atomic<uint32_t>* waiters);
+void wait_seq(std::atomic<uint32_t>* seq, std::atomic<uint32_t>* waiters, uint32_t seen, int64_t timeout_ns);
 
 }  // namespace tk

@@ -239,9 +239,16 @@ PYBIND11_MODULE(_tkhip, m) {
              s["blocked_ns"] = d.blocked_ns_;
              s["blocked_calls"] = d.blocked_calls_;
              s["ready_age_ns"] = d.ready_age_ns_;
+             s["phase_commit_ns"] = d.ph_commit_ns_;
+             s["phase_next_ns"] = d.ph_next_ns_;
+             s["phase_launch_ns"] = d.ph_launch_ns_;
+             s["phase_steps"] = d.ph_steps_;
+             s["events"] = d.events_;
              return s;
            })
       .def("reset_stats", &MainDriver::reset_stats)
+      .def("set_event_every", &MainDriver::set_event_every, py::arg("n"))
+      .def_property_readonly("event_every", &MainDriver::event_every)
       .def("enable_lockstep", &MainDriver::enable_lockstep, py::keep_alive<1, 2>())
       .def("finish_lockstep",
            [](MainDriver& d) {

@@ -59,27 +59,43 @@ template <> struct IsIntDst<uint8_t> { static constexpr bool value = true; };
 // ---------------------------------------------------------------- fixed width
 // dst[i] = conv(src[i]) over a dense [rows, D] block; vector path needs
 // D % 8 == 0 and both pointers 16-byte aligned (checked on the host).
-template <typename S, typename D, bool AFFINE>
+// Each thread owns U groups of kEPT elements per iteration, spaced kThreads groups
+// apart so every wave access stays one contiguous 64-lane span; all U loads are
+// issued before the first convert, so a wave keeps U x 16-32 B per lane in flight
+// (a large stream needs that memory-level parallelism to approach HBM rate; small
+// batches use U = 1 so they still spread over many CUs).
+template <typename S, typename D, bool AFFINE, int U>
 __global__ __launch_bounds__(kThreads) void fixed_vec_kernel(const S* __restrict__ src, D* __restrict__ dst,
                                                              int64_t n_groups, int64_t row, const float* __restrict__ shift,
                                                              const float* __restrict__ scale) {
   using C = Conv<S, D, IsIntDst<D>::value>;
-  const int64_t stride = int64_t(gridDim.x) * kThreads;
-  for (int64_t g = int64_t(blockIdx.x) * kThreads + threadIdx.x; g < n_groups; g += stride) {
-    const int64_t e = g * kEPT;
-    const Vec<S, kEPT> in = *reinterpret_cast<const Vec<S, kEPT>*>(src + e);
-    Vec<D, kEPT> out;
-    if constexpr (AFFINE) {
-      const int64_t d = e % row;
-      const Vec<float, kEPT> sh = *reinterpret_cast<const Vec<float, kEPT>*>(shift + d);
-      const Vec<float, kEPT> sc = *reinterpret_cast<const Vec<float, kEPT>*>(scale + d);
+  const int64_t tile = int64_t(kThreads) * U;
+  const int64_t stride = int64_t(gridDim.x) * tile;
+  for (int64_t base = int64_t(blockIdx.x) * tile + threadIdx.x; base < n_groups; base += stride) {
+    Vec<S, kEPT> in[U];
 #pragma unroll
-      for (int k = 0; k < kEPT; ++k) out.v[k] = C::apply(in.v[k], sh.v[k], sc.v[k], true);
-    } else {
-#pragma unroll
-      for (int k = 0; k < kEPT; ++k) out.v[k] = C::apply(in.v[k], 0.f, 1.f, false);
+    for (int u = 0; u < U; ++u) {
+      const int64_t g = base + int64_t(u) * kThreads;
+      if (g < n_groups) in[u] = *reinterpret_cast<const Vec<S, kEPT>*>(src + g * kEPT);
     }
-    *reinterpret_cast<Vec<D, kEPT>*>(dst + e) = out;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t g = base + int64_t(u) * kThreads;
+      if (g >= n_groups) break;
+      const int64_t e = g * kEPT;
+      Vec<D, kEPT> out;
+      if constexpr (AFFINE) {
+        const int64_t d = e % row;
+        const Vec<float, kEPT> sh = *reinterpret_cast<const Vec<float, kEPT>*>(shift + d);
+        const Vec<float, kEPT> sc = *reinterpret_cast<const Vec<float, kEPT>*>(scale + d);
+#pragma unroll
+        for (int k = 0; k < kEPT; ++k) out.v[k] = C::apply(in[u].v[k], sh.v[k], sc.v[k], true);
+      } else {
+#pragma unroll
+        for (int k = 0; k < kEPT; ++k) out.v[k] = C::apply(in[u].v[k], 0.f, 1.f, false);
+      }
+      *reinterpret_cast<Vec<D, kEPT>*>(dst + e) = out;
+    }
   }
 }
 
@@ -186,13 +202,27 @@ void launch_fixed_t(const void* src, void* dst, int64_t rows, int64_t row, const
                    (!affine || (reinterpret_cast<uintptr_t>(shift) % 16 == 0 && reinterpret_cast<uintptr_t>(scale) % 16 == 0));
   if (vec) {
     const int64_t groups = n / kEPT;
-    const int grid = grid_for(groups);
-    if (affine)
-      hipLaunchKernelGGL((fixed_vec_kernel<S, D, true>), dim3(grid), dim3(kThreads), 0, stream,
-                         static_cast<const S*>(src), static_cast<D*>(dst), groups, row, shift, scale);
-    else
-      hipLaunchKernelGGL((fixed_vec_kernel<S, D, false>), dim3(grid), dim3(kThreads), 0, stream,
-                         static_cast<const S*>(src), static_cast<D*>(dst), groups, row, shift, scale);
+    // U = 4 once there is at least one full 4-deep tile per CU (256 CUs); below that U = 1
+    constexpr int64_t kBigGroups = int64_t(256) * kThreads * 4;
+    const bool big = groups >= kBigGroups;
+    const int grid = big ? grid_for((groups + 3) / 4) : grid_for(groups);
+    const S* s = static_cast<const S*>(src);
+    D* d = static_cast<D*>(dst);
+    if (affine) {
+      if (big)
+        hipLaunchKernelGGL((fixed_vec_kernel<S, D, true, 4>), dim3(grid), dim3(kThreads), 0, stream, s, d, groups, row,
+                           shift, scale);
+      else
+        hipLaunchKernelGGL((fixed_vec_kernel<S, D, true, 1>), dim3(grid), dim3(kThreads), 0, stream, s, d, groups, row,
+                           shift, scale);
+    } else {
+      if (big)
+        hipLaunchKernelGGL((fixed_vec_kernel<S, D, false, 4>), dim3(grid), dim3(kThreads), 0, stream, s, d, groups,
+                           row, shift, scale);
+      else
+        hipLaunchKernelGGL((fixed_vec_kernel<S, D, false, 1>), dim3(grid), dim3(kThreads), 0, stream, s, d, groups,
+                           row, shift, scale);
+    }
   } else {
     const int grid = grid_for(n);
     if (affine)

@@ -57,13 +57,59 @@ MainDriver::~MainDriver() {
 // Host slots whose collate kernel ran are handed back to their worker.  Kernels
 // run in hand-out order on the user's stream, so the scan stops at the first
 // incomplete one (one event query per batch in steady state).
+// With batched events only some slots carry one; a completed event also completes
+// every slot launched before it on that stream (note_handed keeps one stream per run).
 void MainDriver::release_completed() {
   size_t k = 0;
-  while (k < handed_.size() && eng_->slot_done(int(handed_[k]))) {
-    ring_->main_release(uint32_t(handed_[k]));
-    ++k;
+  while (k < handed_.size()) {
+    size_t e = k;
+    while (e < handed_.size() && !handed_[e].ev) ++e;  // next slot with an event
+    if (e == handed_.size() || !eng_->slot_done(int(handed_[e].g))) break;
+    for (; k <= e; ++k) ring_->main_release(uint32_t(handed_[k].g));
   }
   if (k) handed_.erase(handed_.begin(), handed_.begin() + long(k));
+}
+
+void MainDriver::cover_handed() {
+  if (unevented_ == 0 || handed_.empty()) return;
+  // the newest handed slot has no event: one recorded now on its stream covers it and
+  // every unevented slot before it (they all ran on last_stream_)
+  Handed& h = handed_.back();
+  eng_->record_done(int(h.g), last_stream_);
+  h.ev = true;
+  unevented_ = 0;
+  ++events_;
+}
+
+void MainDriver::note_handed(int64_t g, hipStream_t stream, bool* record) {
+  if (stream != last_stream_) {
+    cover_handed();  // earlier unevented slots ran on the previous stream
+    last_stream_ = stream;
+  }
+  *record = (unevented_ + 1 >= event_every_);
+  if (*record) {
+    unevented_ = 0;
+    ++events_;
+  } else {
+    ++unevented_;
+  }
+  handed_.push_back(Handed{g, *record});
+}
+
+int MainDriver::poll_blocking(int64_t timeout_ms) {
+  // Workers may be waiting for slots the GPU still reads: cover them with an event and keep
+  // releasing while waiting, so a full ring drains without a round trip through the caller.
+  cover_handed();
+  const int64_t deadline = timeout_ms < 0 ? INT64_MAX : tk::now_ns() + timeout_ms * 1000000LL;
+  for (;;) {
+    const int64_t now = tk::now_ns();
+    const int64_t left_ms = deadline == INT64_MAX ? -1 : std::max<int64_t>(0, (deadline - now) / 1000000LL);
+    const int64_t slice = handed_.empty() ? left_ms : (left_ms < 0 ? 1 : std::min<int64_t>(left_ms, 1));
+    const int r = poll_one(true, slice);
+    if (r != -1) return r;
+    release_completed();
+    if (tk::now_ns() >= deadline) return -1;
+  }
 }
 
 int MainDriver::poll_one(bool block, int64_t timeout_ms) {
@@ -220,7 +266,7 @@ int MainDriver::next_slot_lockstep(int64_t timeout_ms, SlotView* out) {
       if (data_staged() == 0 && !all_done()) {
         // nothing to offer yet: give this rank's workers a moment before spending a collective round
         const int64_t t0 = tk::now_ns();
-        int r = poll_one(true, timeout_ms);
+        int r = poll_blocking(timeout_ms);
         blocked_ns_ += tk::now_ns() - t0;
         ++blocked_calls_;
         if (r == -3) return -3;
@@ -259,7 +305,7 @@ int MainDriver::next_slot(int64_t timeout_ms, SlotView* out) {
     }
     if (staged_.empty()) {
       const int64_t t0 = tk::now_ns();
-      int r = poll_one(true, timeout_ms);
+      int r = poll_blocking(timeout_ms);
       blocked_ns_ += tk::now_ns() - t0;
       ++blocked_calls_;
       if (r < 0) return r;
@@ -282,15 +328,18 @@ int MainDriver::next_slot(int64_t timeout_ms, SlotView* out) {
 
 void MainDriver::collate_fixed(const SlotView& v, hipStream_t stream, int dst_dt, void* dst, int64_t row,
                                const float* shift, const float* scale) {
-  const int src_dt = v.src_dtype;
-  eng_->collate_fixed(int(v.g), stream, v.values_offset, src_dt, dst, dst_dt, v.n_rows, row, shift, scale);
-  handed_.push_back(v.g);
+  bool record;
+  note_handed(v.g, stream, &record);
+  eng_->collate_fixed(int(v.g), stream, v.values_offset, v.src_dtype, dst, dst_dt, v.n_rows, row, shift, scale,
+                      record);
 }
 
 void MainDriver::collate_varlen(const SlotView& v, hipStream_t stream, int dst_dt, void* out, int64_t L, double pad,
                                 int64_t* lengths, uint8_t* mask) {
-  eng_->collate_varlen(int(v.g), stream, v.values_offset, v.src_dtype, out, dst_dt, v.n_rows, L, pad, lengths, mask);
-  handed_.push_back(v.g);
+  bool record;
+  note_handed(v.g, stream, &record);
+  eng_->collate_varlen(int(v.g), stream, v.values_offset, v.src_dtype, out, dst_dt, v.n_rows, L, pad, lengths, mask,
+                       record);
 }
 
 void MainDriver::deliver(const SlotView& v) { delivered_ = v.wms; }
@@ -374,12 +423,19 @@ int64_t MainDriver::step_fixed(hipStream_t stream, int dst_dt, void* dst, int64_
                                const float* scale, bool auto_commit, int64_t timeout_ms, int* commit_status,
                                SlotView* out) {
   *commit_status = 0;
+  const int64_t t0 = tk::now_ns();
   finish_delivered(stream);  // asking for the next batch finishes the previous one
   if (auto_commit) *commit_status = commit_pending();
+  const int64_t t1 = tk::now_ns();
   int r = next_slot(timeout_ms, out);
+  const int64_t t2 = tk::now_ns();
+  ph_commit_ns_ += t1 - t0;
+  ph_next_ns_ += t2 - t1;
   if (r < 0) return r;
   collate_fixed(*out, stream, dst_dt, dst, row, shift, scale);
   delivered_ = out->wms;
+  ph_launch_ns_ += tk::now_ns() - t2;
+  ++ph_steps_;
   return out->n_rows;
 }
 
@@ -398,6 +454,7 @@ std::vector<std::pair<uint32_t, int64_t>> MainDriver::take_pending() {
 void MainDriver::reset_stats() {
   commits_ = commit_failures_ = 0;
   fill_ns_ = fills_ = blocked_ns_ = blocked_calls_ = ready_age_ns_ = 0;
+  ph_commit_ns_ = ph_next_ns_ = ph_launch_ns_ = ph_steps_ = events_ = 0;
   commit_ns_.clear();
 }
 

@@ -84,9 +84,18 @@ class MainDriver {
 
   SlotView last;  // the slot most recently returned by next_slot / step_fixed
 
+  // Completion events are recorded for one handed-out slot in `n` (>= 1); the others are
+  // released when a later event on the same stream completes.  An event is always recorded
+  // before the driver blocks and when the user's stream changes.
+  void set_event_every(int n) { event_every_ = n < 1 ? 1 : n; }
+  int event_every() const { return event_every_; }
+
  private:
   int poll_one(bool block, int64_t timeout_ms);
   void release_completed();
+  void note_handed(int64_t g, hipStream_t stream, bool* record);  // decides whether slot g records its event
+  void cover_handed();  // records an event for the newest handed slot without one
+  int poll_blocking(int64_t timeout_ms);  // blocks for a slot, releasing completed ones meanwhile
   int next_slot_lockstep(int64_t timeout_ms, SlotView* out);
   int data_staged() const;
   bool all_done() const;
@@ -124,7 +133,13 @@ class MainDriver {
   std::vector<uint8_t> done_;
   uint32_t rr_ = 0;
   std::deque<SlotView> staged_;
-  std::deque<int64_t> handed_;  // slots whose collate was launched, in launch order
+  struct Handed {
+    int64_t g;
+    bool ev;  // its own completion event was recorded
+  };
+  std::deque<Handed> handed_;  // slots whose collate was launched, in launch order
+  hipStream_t last_stream_ = nullptr;
+  int event_every_ = 1, unevented_ = 0;
   std::vector<tk::Watermark> carry_;
   std::vector<tk::Watermark> delivered_;
   std::unordered_map<uint32_t, int64_t> pending_;
@@ -135,6 +150,8 @@ class MainDriver {
  public:
   // profiling counters (ns): worker fill time of delivered slots, main time blocked on the ring
   int64_t fill_ns_ = 0, fills_ = 0, blocked_ns_ = 0, blocked_calls_ = 0, ready_age_ns_ = 0;
+  // step_fixed phases (ns): finish+commit of the previous batch, slot acquisition/release, collate launch
+  int64_t ph_commit_ns_ = 0, ph_next_ns_ = 0, ph_launch_ns_ = 0, ph_steps_ = 0, events_ = 0;
  private:
   std::vector<int64_t> commit_ns_;
 };

@@ -39,10 +39,13 @@ class Engine {
   void wait_slot(int s);
   void wait_copy(int s);  // DMA mode: the slot's copy has finished reading host memory
   // Launch the collate of slot `s` on the user's stream (after the slot's copy in DMA mode).
+  // `record` = false skips the slot's completion event: a later slot's event on the same
+  // stream (record_done) then stands for it (the driver batches events this way).
   void collate_fixed(int s, hipStream_t user, size_t values_offset, int src_dt, void* dst, int dst_dt, int64_t rows,
-                     int64_t row, const float* shift, const float* scale);
+                     int64_t row, const float* shift, const float* scale, bool record = true);
   void collate_varlen(int s, hipStream_t user, size_t values_offset, int src_dt, void* out, int dst_dt, int64_t rows,
-                      int64_t L, double pad, int64_t* lengths, uint8_t* mask);
+                      int64_t L, double pad, int64_t* lengths, uint8_t* mask, bool record = true);
+  void record_done(int s, hipStream_t user) { finish(s, user); }
   void copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes);
   void synchronize();
 

@@ -134,21 +134,21 @@ void Engine::begin(int s, hipStream_t user) {
 void Engine::finish(int s, hipStream_t user) { TKH_CHECK(hipEventRecord(done_[size_t(s)], user)); }
 
 void Engine::collate_fixed(int s, hipStream_t user, size_t values_offset, int src_dt, void* dst, int dst_dt,
-                           int64_t rows, int64_t row, const float* shift, const float* scale) {
+                           int64_t rows, int64_t row, const float* shift, const float* scale, bool record) {
   check_slot(s);
   begin(s, user);
   launch_fixed(src_base(s) + values_offset, src_dt, dst, dst_dt, rows, row, shift, scale, user);
-  finish(s, user);
+  if (record) finish(s, user);
 }
 
 void Engine::collate_varlen(int s, hipStream_t user, size_t values_offset, int src_dt, void* out, int dst_dt,
-                            int64_t rows, int64_t L, double pad, int64_t* lengths, uint8_t* mask) {
+                            int64_t rows, int64_t L, double pad, int64_t* lengths, uint8_t* mask, bool record) {
   check_slot(s);
   const uint8_t* base = src_base(s);
   begin(s, user);
   launch_varlen(reinterpret_cast<const int32_t*>(base), base + values_offset, src_dt, out, dst_dt, rows, L, pad,
                 lengths, mask, user);
-  finish(s, user);
+  if (record) finish(s, user);
 }
 
 void Engine::copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes) {

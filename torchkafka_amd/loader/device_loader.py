@@ -120,6 +120,7 @@ class _Run:
                 self.driver = hip().MainDriver(self.engine, self.name, url, group, L.prefetch, L.in_order,
                                                L._default_src_code())
                 self.driver.set_commit_on_device(L.commit_on == "device")
+                self.driver.set_event_every(L._event_every(self.ring.n_slots))
         except BaseException:
             self.close()
             raise
@@ -246,6 +247,8 @@ class DeviceLoader:
             PCIe: two HIP calls per batch instead of five, but the read runs on the compute stream) or
             ``"auto"`` (default: zero-copy for slots up to ``ZERO_COPY_MAX_BYTES``, where a batch is
             latency-bound; DMA above, where copy/compute overlap matters).
+        event_every: record a slot-completion event for one batch in k (default: ring slots / 8,
+            at most 4); slots in between are released with the next event on the same stream.
     """
 
     def __init__(self, dataset, batch_size: int = 256, *, num_workers: int = 4, worker_init_fn=None,
@@ -256,7 +259,8 @@ class DeviceLoader:
                  multiprocessing_context: str = "fork", commit_on: str = "host", lockstep: bool = True,
                  rank: int | None = None, world_size: int | None = None, timeout: float = 0,
                  group_id: str | None = None, bootstrap_servers=None, base_seed: int | None = None,
-                 lockstep_depth: int = 2, h2d: str = "auto", copy_streams: int = 4):
+                 lockstep_depth: int = 2, h2d: str = "auto", copy_streams: int = 4,
+                 event_every: int | None = None):
         if batch_size < 1:
             raise ValueError("batch_size must be >= 1")
         if num_workers < 1:
@@ -297,6 +301,7 @@ class DeviceLoader:
             raise ValueError("h2d must be 'auto', 'dma' (hipMemcpyAsync on side streams) or 'zerocopy'")
         self.h2d = h2d
         self.copy_streams = max(1, int(copy_streams))
+        self.event_every = None if event_every is None else max(1, int(event_every))
         r, w = dist_rank_world()
         self.rank = r if rank is None else int(rank)
         self.world_size = w if world_size is None else int(world_size)
@@ -336,6 +341,13 @@ class DeviceLoader:
 
     #: largest slot payload that ``h2d="auto"`` moves with zero-copy reads (above: DMA on side streams)
     ZERO_COPY_MAX_BYTES = 1 << 20
+
+    def _event_every(self, n_slots: int) -> int:
+        """Slots per completion event: one ``hipEventRecord`` per batch costs ~1.3 µs of host time,
+        so with a deep ring only every k-th batch records one (k <= n_slots / 8 keeps workers fed)."""
+        if self.event_every is not None:
+            return self.event_every
+        return max(1, min(4, n_slots // 8))
 
     def _resolve_h2d(self, slot_payload_bytes: int) -> str:
         if self.h2d != "auto":
@@ -567,6 +579,11 @@ class DeviceLoader:
         self.stats.worker_fills += st["fills"]
         self.stats.wait_ns += st["blocked_ns"]
         self.stats.ready_age_ns += st["ready_age_ns"]
+        self.stats.phase_commit_ns += st["phase_commit_ns"]
+        self.stats.phase_next_ns += st["phase_next_ns"]
+        self.stats.phase_launch_ns += st["phase_launch_ns"]
+        self.stats.phase_steps += st["phase_steps"]
+        self.stats.events += st["events"]
         self.stats.commits += st["commits"]
         self.stats.commit_failures += st["commit_failures"]
         self.stats.commit_ns.extend(st["commit_ns"])

@@ -33,6 +33,11 @@ class LoaderStats:
     worker_fill_ns: int = 0
     worker_fills: int = 0
     ready_age_ns: int = 0
+    phase_commit_ns: int = 0   # native step driver: finish + commit of the previous batch
+    phase_next_ns: int = 0     # native step driver: slot release/acquire (+H2D issue)
+    phase_launch_ns: int = 0   # native step driver: collate launch (+event)
+    phase_steps: int = 0
+    events: int = 0            # completion events recorded (batched: fewer than batches)
     started: float = field(default_factory=time.perf_counter)
     max_commit_samples: int = 100000
 
@@ -64,6 +69,10 @@ class LoaderStats:
             "host_issue_us_per_batch": self.issue_ns / 1e3 / max(self.batches, 1),
             "worker_fill_us_per_batch": self.worker_fill_ns / 1e3 / max(self.worker_fills, 1),
             "ready_age_us_per_batch": self.ready_age_ns / 1e3 / max(self.worker_fills, 1),
+            "native_commit_us_per_step": self.phase_commit_ns / 1e3 / max(self.phase_steps, 1),
+            "native_next_us_per_step": self.phase_next_ns / 1e3 / max(self.phase_steps, 1),
+            "native_launch_us_per_step": self.phase_launch_ns / 1e3 / max(self.phase_steps, 1),
+            "events_per_batch": self.events / max(self.batches, 1),
             "commits": self.commits,
             "commit_failures": self.commit_failures,
             "commit_p50_us": percentile(c_us, 50),
