@@ -2,8 +2,10 @@
 
 * ``_tkcore``  host C++17 (g++): RecordBatch codec, shm broker, fetcher,
   packers, slot ring.  No HIP: it is imported inside forked loader workers.
-* ``_tkhip``   HIP for gfx950 (hipcc --offload-arch=gfx950): collate kernels
-  and the H2D engine.  Built with plain hipcc -- no hipify step, no CUDA shim.
+* ``_tkhip``   HIP for gfx950 (hipcc --offload-arch=gfx950): collate kernels,
+  the H2D engine, the step driver and the RCCL lockstep.  Built with hipcc -- no
+  hipify step, no CUDA shim -- against the installed PyTorch (torch's pybind11;
+  libtorch for the batch allocation in torch_step.cpp).
 
 Both land next to this file so the built ``.so`` travel with the repository
 snapshot to the GPU box.  Run ``python -m torchkafka_amd._build`` (or
@@ -31,6 +33,18 @@ def _py_includes() -> list[str]:
     import pybind11
 
     return [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+
+
+def _torch_paths() -> tuple[Path, Path]:
+    """(include, lib) of the installed PyTorch: the device module links libtorch for
+    step_fixed_tensor and must use torch's bundled pybind11 for every binding."""
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    if spec is None or spec.origin is None:
+        raise RuntimeError("the gfx950 extension needs PyTorch (ROCm build) installed")
+    root = Path(spec.origin).parent
+    return root / "include", root / "lib"
 
 
 def core_target() -> Path:
@@ -106,18 +120,25 @@ def build_hip(force: bool = False, verbose: bool = False) -> Path:
     obj_dir = BUILD / f"hip-{ARCH}"
     obj_dir.mkdir(parents=True, exist_ok=True)
     cc = hipcc()
+    t_inc, t_lib = _torch_paths()
+    # torch's include dir first: its bundled pybind11 is the one every binding in this module uses
     flags = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}", "-DNDEBUG",
-             "-Wno-unused-result", *_py_includes(), f"-I{src_dir}", f"-I{core_dir}"]
+             "-Wno-unused-result", f"-I{t_inc}", f"-I{sysconfig.get_paths()['include']}", f"-I{src_dir}",
+             f"-I{core_dir}"]
+    torch_flags = [f"-I{t_inc / 'torch' / 'csrc' / 'api' / 'include'}", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1",
+                   "-DTORCH_API_INCLUDE_EXTENSION_H", "-D_GLIBCXX_USE_CXX11_ABI=1", "-Wno-deprecated-declarations"]
     objs, jobs = [], []
     for s in srcs:
         o = obj_dir / ((("core_" if s.parent == core_dir else "") + s.stem) + ".o")
         objs.append(o)
         lang = ["-x", "hip"] if s.suffix == ".hip" else []
-        jobs.append([cc, *flags, *lang, "-c", str(s), "-o", str(o)])
+        extra = torch_flags if s.name == "torch_step.cpp" else []
+        jobs.append([cc, *flags, *extra, *lang, "-c", str(s), "-o", str(o)])
     _compile_all(jobs)
     tmp = out.with_suffix(".tmp.so")
     _run([cc, "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs), f"-L{ROCM}/lib", "-lamdhip64",
-          "-lpthread", "-lrt"])
+          f"-L{t_lib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch", "-ltorch_python",
+          f"-Wl,-rpath,{t_lib}", "-lpthread", "-lrt"])
     os.replace(tmp, out)
     if verbose:
         print(f"[torchkafka_amd] built {out.name} for {ARCH}")

@@ -1,7 +1,8 @@
 // pybind11 bindings of the device half: module `torchkafka_amd._tkhip`.
 // Tensors cross the boundary as raw device pointers (Tensor.data_ptr()) and
-// streams as hipStream_t handles (torch.cuda.Stream.cuda_stream), so the
-// module does not link against libtorch and builds with plain hipcc.
+// streams as hipStream_t handles (torch.cuda.Stream.cuda_stream).  The one
+// exception is torch_step.cpp (step_fixed_tensor), which allocates the batch
+// through libtorch; the module therefore builds against torch's pybind11.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -14,6 +15,10 @@
 
 namespace py = pybind11;
 using namespace tkh;
+
+namespace tkh {
+void register_torch_step(py::module_& m);  // torch_step.cpp
+}
 
 namespace {
 // Lockstep transport backed by a Python callable (e.g. a gloo all_reduce): lets the
@@ -256,6 +261,8 @@ PYBIND11_MODULE(_tkhip, m) {
              d.finish_lockstep();
            })
       .def_property_readonly("lockstep_enabled", &MainDriver::lockstep_enabled);
+
+  register_torch_step(m);
 
   m.attr("H2D_DMA") = int(kH2DDma);
   m.attr("H2D_ZERO_COPY") = int(kH2DZeroCopy);

@@ -161,6 +161,23 @@ int MainDriver::poll_one(bool block, int64_t timeout_ms) {
   }
 }
 
+// Pull the headers of the slots the next acquisition will look at into this core's
+// cache while the caller runs Python: they were written by worker processes on other
+// cores, and reading them cold costs several cross-core transfers per batch.  Only
+// READY slots are touched, so a worker still filling a slot never loses its lines.
+void MainDriver::prefetch_ready() const {
+  const uint32_t nw = ring_->n_workers(), spw = ring_->slots_per_worker();
+  for (uint32_t w = 0; w < nw; ++w) {
+    if (done_[w]) continue;
+    const tk::SlotHeader* h = ring_->slot(w * spw + cursor_[w]);
+    if (h->state.load(std::memory_order_relaxed) != tk::kSlotReady) continue;
+    const char* p = reinterpret_cast<const char*>(h);
+    __builtin_prefetch(p + 64);
+    __builtin_prefetch(p + 128);
+    __builtin_prefetch(reinterpret_cast<const char*>(&h->wm[0]));
+  }
+}
+
 int MainDriver::data_staged() const {
   int n = 0;
   for (const auto& v : staged_) n += v.g >= 0 ? 1 : 0;
@@ -434,6 +451,7 @@ int64_t MainDriver::step_fixed(hipStream_t stream, int dst_dt, void* dst, int64_
   if (r < 0) return r;
   collate_fixed(*out, stream, dst_dt, dst, row, shift, scale);
   delivered_ = out->wms;
+  prefetch_ready();
   ph_launch_ns_ += tk::now_ns() - t2;
   ++ph_steps_;
   return out->n_rows;

@@ -98,6 +98,7 @@ class MainDriver {
   int poll_blocking(int64_t timeout_ms);  // blocks for a slot, releasing completed ones meanwhile
   int next_slot_lockstep(int64_t timeout_ms, SlotView* out);
   int data_staged() const;
+  void prefetch_ready() const;
   bool all_done() const;
   bool pop_data(SlotView* out);
 

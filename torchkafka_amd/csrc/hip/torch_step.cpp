@@ -1,0 +1,64 @@
+// The fixed-width fast path with the output tensor allocated here, in C++, from
+// PyTorch's HIP caching allocator on the caller's current stream.
+//
+// Per batch the Python loop used to pay for torch.empty(...) through the Python
+// argument parser (~1.7 µs on the MI355X host), plus stream and data_ptr lookups.
+// at::empty + THPVariable_Wrap cost a fraction of that, and the batch keeps the
+// allocator's ordinary stream semantics (freed tensors are reused on the stream
+// they were allocated on).  This is the only translation unit that sees libtorch
+// headers.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/csrc/autograd/python_variable.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "driver.h"
+#include "dtypes.h"
+
+namespace py = pybind11;
+
+namespace tkh {
+
+namespace {
+at::ScalarType scalar_type_of(int code) {
+  switch (code) {
+    case kF32: return at::kFloat;
+    case kF16: return at::kHalf;
+    case kBF16: return at::kBFloat16;
+    case kFP8E4M3: return at::kFloat8_e4m3fn;
+    case kU8: return at::kByte;
+    case kI8: return at::kChar;
+    case kI32: return at::kInt;
+    case kI64: return at::kLong;
+    default: throw std::invalid_argument("step_fixed_tensor: unsupported dtype code");
+  }
+}
+}  // namespace
+
+void register_torch_step(py::module_& m) {
+  m.def(
+      "step_fixed_tensor",
+      [](MainDriver& d, int device, std::vector<int64_t> shape, int dst_dt, int64_t row, uintptr_t shift,
+         uintptr_t scale, bool auto_commit, int64_t timeout_ms) -> py::tuple {
+        const auto dev = c10::DeviceIndex(device);
+        hipStream_t stream = c10::hip::getCurrentHIPStream(dev).stream();
+        at::Tensor out = at::empty(shape, at::TensorOptions().dtype(scalar_type_of(dst_dt)).device(at::kCUDA, dev));
+        int cs = 0;
+        int64_t r;
+        {
+          py::gil_scoped_release nogil;
+          r = d.step_fixed(stream, dst_dt, out.data_ptr(), row, reinterpret_cast<const float*>(shift),
+                           reinterpret_cast<const float*>(scale), auto_commit, timeout_ms, &cs, &d.last);
+        }
+        if (r <= 0) return py::make_tuple(r, cs, py::none());
+        if (r < shape[0]) out = out.narrow(0, 0, r);
+        return py::make_tuple(r, cs, py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(out))));
+      },
+      py::arg("driver"), py::arg("device"), py::arg("shape"), py::arg("dst_dt"), py::arg("row"), py::arg("shift"),
+      py::arg("scale"), py::arg("auto_commit"), py::arg("timeout_ms"),
+      "finish+commit the previous batch, take the next slot and collate it into a new tensor "
+      "allocated on the current stream -> (rows, commit_status, tensor | None)");
+}
+
+}  // namespace tkh

@@ -542,22 +542,21 @@ class DeviceLoader:
         shift, scale = (prm[0].data_ptr(), prm[1].data_ptr()) if prm is not None else (0, 0)
         dev = self.device
         stats = self.stats
-        empty = torch.empty
-        raw_stream = torch._C._cuda_getCurrentRawStream
         dev_index = dev.index
-        out_shape = (B, *shape)
-        step = drv.step_fixed
+        out_shape = [B, *shape]
+        # one native call per batch: allocate (torch caching allocator, current stream),
+        # finish + commit the previous batch, take the next slot, launch the collate
+        step = hip().step_fixed_tensor
         while True:
             t0 = time.perf_counter_ns()
-            out = empty(out_shape, dtype=dst_dt, device=dev)
-            r, cs = step(raw_stream(dev_index), dst_code, out.data_ptr(), row, shift, scale, auto_commit, 100)
+            r, cs, out = step(drv, dev_index, out_shape, dst_code, row, shift, scale, auto_commit, 100)
             if cs:
                 self._log_commit(cs, debug)
             if r > 0:
                 stats.batches += 1
                 stats.records += r
                 stats.issue_ns += time.perf_counter_ns() - t0
-                yield out if r == B else out[:r]
+                yield out
             elif r == -2:
                 return
             elif r == -3:
