@@ -183,7 +183,7 @@ def main() -> int:
                 "partitions": n_parts,
                 "num_workers": args.workers,
                 "commit": "auto_commit per batch" + (", RCCL lockstep" if world > 1 else ""),
-                "h2d": loader._resolve_h2d(loader._slot_capacity()),
+                "h2d": loader._resolve_h2d(loader._slot_capacity()) if device.type == "cuda" else "n/a (cpu)",
                 "bytes_per_step_per_gpu": B * args.dim * 4,
                 "gb_per_s": round(value * args.dim * 4 / 1e9, 3),
                 "commit_p99_us": round(stats["commit_p99_us"], 2),

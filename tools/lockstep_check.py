@@ -3,7 +3,8 @@
 Launch: python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port P \
             tools/lockstep_check.py [--transport host|rccl]
 Every rank uses cuda:0 for the device path; the per-step agreement goes through
-gloo (``lockstep="host"``), since RCCL refuses two ranks on one GPU.  Rank r owns
+gloo (``lockstep="host"``) by default.  ``LOCKCHECK_TRANSPORT=rccl`` tries the native
+RCCL transport instead (two ranks on one GPU: only if RCCL accepts that).  Rank r owns
 partitions {r, r + world}; the last rank has the least data, so every rank must
 stop at its batch count, and only batches all ranks finished may be committed.
 """
@@ -41,7 +42,8 @@ def main():
     depths = [int(d) for d in os.environ.get("LOCKCHECK_DEPTHS", "0,2,5").split(",")]
     for depth in depths:
         group = f"g{depth}"
-        dl = DeviceLoader(Vec.placeholder(), 10, num_workers=2, device="cuda:0", lockstep="host",
+        dl = DeviceLoader(Vec.placeholder(), 10, num_workers=2, device="cuda:0",
+                          lockstep=os.environ.get("LOCKCHECK_TRANSPORT", "host"),
                           lockstep_depth=depth,
                           worker_init_fn=Vec.init_worker("t", bootstrap_servers=url, group_id=group,
                                                          auto_offset_reset="earliest", consumer_timeout_ms=500))
