@@ -120,6 +120,31 @@ def test_varlen_pad_matches_reference(dst):
     assert torch.equal(mask.cpu(), r_mask)
 
 
+@pytest.mark.parametrize("src_dt,dst", [(torch.bfloat16, torch.float32), (torch.float16, torch.bfloat16),
+                                        (torch.uint8, torch.int32), (torch.int64, torch.int32),
+                                        (torch.int8, torch.float16)])
+def test_varlen_narrow_and_wide_sources(src_dt, dst):
+    """1/2-byte sources take the LDS-staged kernel (row starts not dword-aligned), 4/8-byte the direct one."""
+    from torchkafka_amd.ops.collate import collate_varlen, reference_varlen
+
+    g = torch.Generator().manual_seed(11)
+    lens = torch.randint(0, 3000, (37,), generator=g)
+    lens[0], lens[1] = 0, 2049
+    offs = torch.zeros(38, dtype=torch.int32)
+    offs[1:] = lens.cumsum(0).to(torch.int32)
+    n = int(offs[-1])
+    if src_dt.is_floating_point:
+        vals = torch.randn(n, generator=g).to(src_dt)
+    else:
+        info = torch.iinfo(src_dt)
+        vals = torch.randint(max(info.min, -100), min(info.max, 100), (n,), generator=g, dtype=torch.int64).to(src_dt)
+    L = int(lens.max()) + 5
+    out, ln, mask = collate_varlen(offs.cuda(), vals.cuda(), dst, L=L, pad_value=3, return_mask=True)
+    r_out, r_ln, r_mask = reference_varlen(offs, vals, dst, L, pad_value=3, return_mask=True)
+    assert_same(out, r_out)
+    assert torch.equal(ln.cpu(), r_ln) and torch.equal(mask.cpu(), r_mask)
+
+
 def test_varlen_truncating_width():
     from torchkafka_amd.ops.collate import collate_varlen, reference_varlen
 

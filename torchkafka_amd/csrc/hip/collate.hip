@@ -7,11 +7,15 @@
 //     (Guideline 13) and grid-stride loops capped at ~2048 blocks (Guideline 11);
 //   * conversions bit-exact with torch (dtypes.h), optional per-feature affine
 //     normalisation fused into the same pass (no second read of the batch);
-//   * the variable-length pad kernel stages each row chunk through LDS with
-//     aligned 16-byte loads, so unaligned CSR row starts never turn into
-//     narrow global loads, and reads LDS through a padded layout (one dword
-//     of padding per 32 bytes) that keeps the per-lane 8-element reads free
-//     of bank conflicts (MI355X_MICROARCH.md §LDS: ds_read_b32 banks (a/4)%32).
+//   * variable-length pad, 4/8-byte sources: each lane loads its 8 elements
+//     with dword-aligned global_load_dwordx4 (full width on gfx950 wherever a
+//     CSR row starts), no LDS and no barrier;
+//   * variable-length pad, 1/2-byte sources (row starts not dword-aligned):
+//     the row chunk is staged through LDS with aligned 16-byte global loads
+//     and read back through a padded layout (one dword per 32 bytes): lane t
+//     reads dword 9t + c, a conflict-free ds_read_b32 pattern; the staging
+//     ds_write_b32s are at most 2-way, which costs no extra cycle on CDNA4
+//     (MI355X_MICROARCH.md §LDS).
 #include <hip/hip_runtime.h>
 
 #include "collate.h"
@@ -234,6 +238,52 @@ void launch_fixed_t(const void* src, void* dst, int64_t rows, int64_t row, const
   }
 }
 
+// Direct variant for 4- and 8-byte sources (f32 JSON values, i32/i64 token ids): a row's
+// elements are dword-aligned wherever the row starts, and gfx950 serves dword-aligned
+// global_load_dwordx4 at full width, so each lane loads its 8 elements straight from
+// global memory (2-4 x 16 B, one contiguous span per wave) with no LDS round trip or
+// barrier.  1- and 2-byte sources keep the LDS-staged kernel above (their row starts
+// are not dword-aligned).
+template <typename S>
+struct alignas(4) LoadVec {  // 8 source elements with only dword alignment
+  typedef S type __attribute__((ext_vector_type(8), aligned(4)));
+};
+
+template <typename S, typename D>
+__global__ __launch_bounds__(kThreads) void varlen_direct_kernel(const int32_t* __restrict__ offs,
+                                                                 const S* __restrict__ vals, D* __restrict__ out,
+                                                                 int64_t L, D pad, int64_t* __restrict__ lengths,
+                                                                 uint8_t* __restrict__ mask, int vec_store_ok) {
+  static_assert(sizeof(S) >= 4, "direct var-len loads need dword-sized elements");
+  using C = Conv<S, D, IsIntDst<D>::value>;
+  const int64_t r = blockIdx.y;
+  const int64_t j0 = int64_t(blockIdx.x) * kChunk + int64_t(threadIdx.x) * kEPT;
+  const int32_t beg = offs[r];
+  const int64_t len = int64_t(offs[r + 1]) - beg;
+  if (lengths && blockIdx.x == 0 && threadIdx.x == 0) lengths[r] = len < L ? len : L;
+  if (j0 >= L) return;
+  const S* row = vals + beg;
+  D* orow = out + r * L;
+  if (j0 + kEPT <= len && vec_store_ok) {
+    // interior of a row (len <= L so j0 + 8 <= L too): load, convert in pairs, one 16 B store
+    const typename LoadVec<S>::type v = *reinterpret_cast<const typename LoadVec<S>::type*>(row + j0);
+    Vec<D, kEPT> o;
+#pragma unroll
+    for (int k = 0; k < kEPT; ++k) o.v[k] = C::apply(v[k], 0.f, 1.f, false);
+    *reinterpret_cast<Vec<D, kEPT>*>(orow + j0) = o;
+  } else {
+#pragma unroll
+    for (int k = 0; k < kEPT; ++k)
+      if (j0 + k < L) orow[j0 + k] = (j0 + k < len) ? C::apply(row[j0 + k], 0.f, 1.f, false) : pad;
+  }
+  if (mask) {
+    uint8_t* mrow = mask + r * L;
+#pragma unroll
+    for (int k = 0; k < kEPT; ++k)
+      if (j0 + k < L) mrow[j0 + k] = uint8_t((j0 + k) < len);
+  }
+}
+
 template <typename S, typename D>
 void launch_varlen_t(const int32_t* offs, const void* vals, void* out, int64_t rows, int64_t L, double pad,
                      int64_t* lengths, uint8_t* mask, hipStream_t stream) {
@@ -245,8 +295,13 @@ void launch_varlen_t(const int32_t* offs, const void* vals, void* out, int64_t r
   if constexpr (IsIntDst<D>::value) padv = D(int64_t(pad)); else padv = Store<D>::cvt(float(pad));
   const int vec_ok = (L % kEPT == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0);
   dim3 grid(unsigned((L + kChunk - 1) / kChunk), unsigned(rows));
-  hipLaunchKernelGGL((varlen_pad_kernel<S, D>), grid, dim3(kThreads), 0, stream, offs,
-                     static_cast<const uint8_t*>(vals), static_cast<D*>(out), L, padv, lengths, mask, vec_ok);
+  if constexpr (sizeof(S) >= 4) {
+    hipLaunchKernelGGL((varlen_direct_kernel<S, D>), grid, dim3(kThreads), 0, stream, offs,
+                       static_cast<const S*>(vals), static_cast<D*>(out), L, padv, lengths, mask, vec_ok);
+  } else {
+    hipLaunchKernelGGL((varlen_pad_kernel<S, D>), grid, dim3(kThreads), 0, stream, offs,
+                       static_cast<const uint8_t*>(vals), static_cast<D*>(out), L, padv, lengths, mask, vec_ok);
+  }
 }
 
 #define TK_DISPATCH_DST(S, FN, ...)                                                    \
