@@ -62,28 +62,31 @@ def main():
                     "torch_us": round(t_torch, 2), "torch_GBps": round(nbytes / t_torch / 1e3, 1)})
 
     g = torch.Generator().manual_seed(0)
-    var_cases = [("config4 256 rows, L~U(0,512) f32->bf16", 256, 512), ("256 rows, L~U(0,8192)", 256, 8192),
-                 ("4096 rows, L~U(0,4096)", 4096, 4096)]
-    for name, rows, lmax in var_cases:
+    var_cases = [("config4 256 rows, L~U(0,512) f32->bf16", 256, 512, torch.float32),
+                 ("256 rows, L~U(0,8192) f32->bf16", 256, 8192, torch.float32),
+                 ("4096 rows, L~U(0,4096) f32->bf16", 4096, 4096, torch.float32),
+                 ("LDS-staged: 4096 rows, L~U(0,4096) bf16->bf16", 4096, 4096, torch.bfloat16)]
+    src_code = {torch.float32: 0, torch.bfloat16: 2}
+    for name, rows, lmax, sdt in var_cases:
         lens = torch.randint(0, lmax + 1, (rows,), generator=g)
         offs = torch.zeros(rows + 1, dtype=torch.int32)
         offs[1:] = lens.cumsum(0).to(torch.int32)
-        vals = torch.randn(int(offs[-1]), device=dev)
+        vals = torch.randn(int(offs[-1]), device=dev).to(sdt)
         offs_d = offs.to(dev)
         L = int(lens.max())
-        esz_in = vals.numel() * 4
-        nbytes = esz_in + rows * L * 2
+        esz = vals.element_size()
+        nbytes = vals.numel() * esz + rows * L * 2
 
-        buf = torch.zeros(vals.numel() * 4 + 64, dtype=torch.uint8, device=dev)
-        buf[: vals.numel() * 4].copy_(vals.view(torch.uint8))
+        buf = torch.zeros(vals.numel() * esz + 64, dtype=torch.uint8, device=dev)
+        buf[: vals.numel() * esz].copy_(vals.view(torch.uint8))
         o = torch.empty((rows, L), dtype=torch.bfloat16, device=dev)
         ln = torch.empty(rows, dtype=torch.int64, device=dev)
         mod = hip()
         stream = torch.cuda.current_stream(dev).cuda_stream
 
         def ours():
-            mod.collate_varlen(offs_d.data_ptr(), buf.data_ptr(), 0, o.data_ptr(), 2, rows, L, 0.0, ln.data_ptr(), 0,
-                               stream)
+            mod.collate_varlen(offs_d.data_ptr(), buf.data_ptr(), src_code[sdt], o.data_ptr(), 2, rows, L, 0.0,
+                               ln.data_ptr(), 0, stream)
 
         row_idx = torch.repeat_interleave(torch.arange(rows, device=dev), lens.to(dev))
         col_idx = torch.arange(vals.numel(), device=dev) - offs_d[:-1].long().repeat_interleave(lens.to(dev))

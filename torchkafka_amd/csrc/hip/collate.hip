@@ -12,10 +12,10 @@
 //     CSR row starts), no LDS and no barrier;
 //   * variable-length pad, 1/2-byte sources (row starts not dword-aligned):
 //     the row chunk is staged through LDS with aligned 16-byte global loads
-//     and read back through a padded layout (one dword per 32 bytes): lane t
-//     reads dword 9t + c, a conflict-free ds_read_b32 pattern; the staging
-//     ds_write_b32s are at most 2-way, which costs no extra cycle on CDNA4
-//     (MI355X_MICROARCH.md §LDS).
+//     and read back through a padded layout (one dword after every lane's
+//     8-element chunk): lane t reads dword (2*sizeof(S)+1)*t + c, an odd
+//     stride, so each 32-lane read group hits 32 distinct banks
+//     (MI355X_MICROARCH.md §LDS: ds_read_b32/u16/u8 bank = (a/4) mod 32).
 #include <hip/hip_runtime.h>
 
 #include "collate.h"
@@ -120,8 +120,14 @@ __global__ __launch_bounds__(kThreads) void fixed_scalar_kernel(const S* __restr
 }
 
 // ---------------------------------------------------------------- var-len pad
-// Padded LDS byte address: one dword of padding after every 32 bytes.
-__device__ __forceinline__ uint32_t lds_pad(uint32_t b) { return b + ((b >> 5) << 2); }
+// Padded LDS byte address: one dword of padding after every lane chunk (kEPT elements,
+// 8 * sizeof(S) bytes), so lane t's k-th ds_read lands on dword (2 * sizeof(S) + 1) * t + c:
+// an odd stride, hence a different bank for each of the 32 lanes of a read group.
+template <typename S>
+__device__ __forceinline__ uint32_t lds_pad(uint32_t b) {
+  constexpr uint32_t kLaneBytes = kEPT * sizeof(S);
+  return b + (b / kLaneBytes) * 4;
+}
 
 template <typename S, typename D>
 __global__ __launch_bounds__(kThreads) void varlen_pad_kernel(const int32_t* __restrict__ offs,
@@ -130,7 +136,7 @@ __global__ __launch_bounds__(kThreads) void varlen_pad_kernel(const int32_t* __r
                                                               uint8_t* __restrict__ mask, int vec_store_ok) {
   using C = Conv<S, D, IsIntDst<D>::value>;
   constexpr uint32_t kStageBytes = kChunk * sizeof(S) + 32;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kStageBytes + (kStageBytes / 32) * 4 + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kStageBytes + (kStageBytes / (kEPT * sizeof(S)) + 1) * 4 + 16];
 
   const int64_t r = blockIdx.y;
   const int64_t c0 = int64_t(blockIdx.x) * kChunk;
@@ -147,13 +153,13 @@ __global__ __launch_bounds__(kThreads) void varlen_pad_kernel(const int32_t* __r
     const uint32_t nv = uint32_t((eb - ab) >> 4);
     for (uint32_t i = threadIdx.x; i < nv; i += kThreads) {
       const uint4 v = *reinterpret_cast<const uint4*>(vals + ab + (uint64_t(i) << 4));
-      // 16 aligned bytes never straddle a 32-byte padding boundary, but the
-      // padded address is only 4-byte aligned: store dwords, not one b128.
-      uint32_t* d = reinterpret_cast<uint32_t*>(lds + lds_pad(i << 4));
-      d[0] = v.x;
-      d[1] = v.y;
-      d[2] = v.z;
-      d[3] = v.w;
+      // the padded addresses are only 4-byte aligned and, for 1-byte sources, a pad
+      // falls inside the 16 bytes: store each dword at its own padded address
+      const uint32_t b = i << 4;
+      *reinterpret_cast<uint32_t*>(lds + lds_pad<S>(b)) = v.x;
+      *reinterpret_cast<uint32_t*>(lds + lds_pad<S>(b + 4)) = v.y;
+      *reinterpret_cast<uint32_t*>(lds + lds_pad<S>(b + 8)) = v.z;
+      *reinterpret_cast<uint32_t*>(lds + lds_pad<S>(b + 12)) = v.w;
     }
   }
   __syncthreads();
@@ -165,7 +171,7 @@ __global__ __launch_bounds__(kThreads) void varlen_pad_kernel(const int32_t* __r
   for (int k = 0; k < kEPT; ++k) {
     const int64_t local = int64_t(threadIdx.x) * kEPT + k;
     if (local < nreal) {
-      const S s = *reinterpret_cast<const S*>(lds + lds_pad(shift_b + uint32_t(local) * sizeof(S)));
+      const S s = *reinterpret_cast<const S*>(lds + lds_pad<S>(shift_b + uint32_t(local) * sizeof(S)));
       o.v[k] = C::apply(s, 0.f, 1.f, false);
     } else {
       o.v[k] = pad;
@@ -270,6 +276,12 @@ __global__ __launch_bounds__(kThreads) void varlen_direct_kernel(const int32_t* 
     Vec<D, kEPT> o;
 #pragma unroll
     for (int k = 0; k < kEPT; ++k) o.v[k] = C::apply(v[k], 0.f, 1.f, false);
+    *reinterpret_cast<Vec<D, kEPT>*>(orow + j0) = o;
+  } else if (j0 >= len && vec_store_ok && j0 + kEPT <= L) {
+    // all padding (typically half of a batch padded to its longest row): one vector store
+    Vec<D, kEPT> o;
+#pragma unroll
+    for (int k = 0; k < kEPT; ++k) o.v[k] = pad;
     *reinterpret_cast<Vec<D, kEPT>*>(orow + j0) = o;
   } else {
 #pragma unroll
