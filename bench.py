@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy"])
     ap.add_argument("--copy-streams", type=int, default=4)
     ap.add_argument("--lockstep-depth", type=int, default=2)
+    ap.add_argument("--no-numa", action="store_true", help="do not bind ranks to their GPU's NUMA node")
     return ap.parse_args()
 
 
@@ -75,6 +76,11 @@ def main() -> int:
     from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
     from torchkafka_amd.broker import SyntheticBroker
     from torchkafka_amd.parallel import shard_partitions
+    from torchkafka_amd.utils.topology import bind_to_gpu_numa
+
+    if not args.device and not args.no_numa:
+        # the broker log this rank fills, its ring and its workers all live on its GPU's socket
+        bind_to_gpu_numa(local_rank)
 
     dtype = {"bf16": torch.bfloat16, "fp8": torch.float8_e4m3fn, "f16": torch.float16, "f32": torch.float32}[args.dtype]
     device = torch.device(args.device) if args.device else torch.device("cuda", local_rank)
@@ -107,7 +113,7 @@ def main() -> int:
         Records.placeholder(), B, num_workers=args.workers, device=device, dtype=dtype,
         slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
         in_order=args.in_order, h2d=args.h2d, copy_streams=args.copy_streams, lockstep_depth=args.lockstep_depth,
-        event_every=args.event_every,
+        event_every=args.event_every, numa_bind=not args.no_numa,
         worker_init_fn=Records.init_worker("bench", bootstrap_servers=url, group_id="bench",
                                            auto_offset_reset="earliest", check_crcs=not args.no_crc),
     )

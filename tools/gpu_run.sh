@@ -19,7 +19,7 @@ for s in $STEPS; do
   case $s in
     build)  step build 600 python -c "import __graft_entry__ as g; g.build()" ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    pytest) step pytest_gpu 600 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=150 --timeout-method=thread ;;
+    pytest) step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     nccl)   step nccl_probe 120 python tools/nccl_probe.py ;;
     overhead) step host_overhead 120 python tools/host_overhead.py ;;
     lockcheck5) TORCHKAFKA_DRIVER_TRACE=1 LOCKCHECK_DEPTHS=5 step lockstep_check5 150 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29632 tools/lockstep_check.py ;;
@@ -28,6 +28,7 @@ for s in $STEPS; do
     bench)  step bench 600 python bench.py --stats ;;
     bench8) step bench_fp8 600 python bench.py --stats --dtype fp8 ;;
     benchlong) step bench_long 600 python bench.py --stats --steps 4000 --warmup 100 ;;
+    benchnonuma) step bench_nonuma 600 python bench.py --stats --steps 4000 --warmup 100 --no-numa ;;
     benchnocrc) step bench_nocrc 600 python bench.py --stats --steps 4000 --warmup 100 --no-crc ;;
     benchzc) step bench_zc 600 python bench.py --stats --steps 4000 --warmup 100 --h2d zerocopy ;;
     benchs1) step bench_s1 600 python bench.py --stats --steps 4000 --warmup 100 --copy-streams 1 ;;
@@ -37,6 +38,9 @@ for s in $STEPS; do
     benchee4) step bench_ee4 600 python bench.py --stats --steps 4000 --warmup 100 --event-every 4 ;;
     benchdma) step bench_dma 600 python bench.py --stats --steps 4000 --warmup 100 --h2d dma ;;
     benchbs) step bench_bs1024 600 python bench.py --stats --steps 2000 --warmup 100 --batch-size 1024 ;;
+    config1) step config1 300 python benchmarks/config1_cpu_plumbing.py ;;
+    config4) step config4 300 python benchmarks/config4_json_varlen.py ;;
+    config5) step config5 300 python benchmarks/config5_large_messages.py ;;
     kbench) step kernel_bench 300 python tools/kernel_bench.py ;;
     kprof)  (cd /tmp && export TMPDIR=/tmp && step kprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kprof" -o run -- python3 "$OLDPWD/tools/kernel_bench.py" --quick) || exit $? ;;
     # TCC has 4 slots per pass: FETCH_SIZE costs 3, WRITE_SIZE 2 (MI355X_MICROARCH.md) -> two passes

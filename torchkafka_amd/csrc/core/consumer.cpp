@@ -1,6 +1,10 @@
 #include "consumer.h"
 
+#include <sys/mman.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cerrno>
 #include <cstdlib>
 #include <limits>
 
@@ -19,12 +23,14 @@ void Fetcher::assign(const std::vector<uint32_t>& pidxs, const std::vector<int64
     fp.pidx = pidxs[i];
     fp.position = positions[i];
     // keep decode caches of partitions that stay assigned at the same position
-    for (const auto& old : parts_)
+    for (const auto& old : parts_) {
+      if (old.pidx == fp.pidx) fp.populated_end = old.populated_end;
       if (old.pidx == fp.pidx && old.position == fp.position) {
         fp.batch_hint = old.batch_hint;
         fp.verified_base = old.verified_base;
         fp.paused = old.paused;
       }
+    }
     np.push_back(fp);
   }
   parts_ = std::move(np);
@@ -44,6 +50,22 @@ bool Fetcher::has_data(const FetchPart& fp) {
                            " outside [" + std::to_string(P.log_start_offset.load()) + ", " + std::to_string(hw) +
                            "] of partition index " + std::to_string(fp.pidx));
   return fp.position < hw;
+}
+
+void Fetcher::prefault(FetchPart& fp, const uint8_t* log, uint64_t pos, uint64_t log_end) {
+  static const long page = sysconf(_SC_PAGESIZE);
+  const uint64_t pg = uint64_t(page > 0 ? page : 4096);
+  const uint64_t lo = std::max<uint64_t>(pos, fp.populated_end) & ~(pg - 1);
+  const uint64_t hi = std::min<uint64_t>(pos + kPrefaultBytes, (log_end + pg - 1) & ~(pg - 1));
+  if (hi > lo && prefault_ok_) {
+#ifdef MADV_POPULATE_READ
+    if (madvise(const_cast<uint8_t*>(log) + lo, hi - lo, MADV_POPULATE_READ) != 0 && errno == EINVAL)
+      prefault_ok_ = false;  // kernel < 5.14: fall back to faulting pages on first touch
+#else
+    prefault_ok_ = false;
+#endif
+  }
+  fp.populated_end = std::max<uint64_t>(hi, pos + 1);
 }
 
 // ------------------------------------------------------------ streaming copy

@@ -42,6 +42,7 @@ from ..client.errors import COMMIT_FAILED_ERRORS
 from ..ops.collate import CODE_DTYPE, DTYPE_CODE, FLOAT_DTYPES, normalize_params
 from ..ops.native import core, hip
 from ..parallel.sharding import dist_rank_world
+from ..utils import topology
 from ..utils.metrics import LoaderStats
 from ..utils.tracing import enabled as _roctx_enabled
 from ..utils.tracing import trace_range
@@ -99,6 +100,10 @@ class _Run:
         self.done = [False] * L.num_workers
         self.carry: list = []              # watermarks of consumed-but-undelivered records
         self.closed = False
+        if L.numa_bind and L.device.type == "cuda" and L.device.index is not None:
+            # before the fork: the workers inherit the mask, and the ring pages they first-touch land on
+            # the GPU's socket (utils/topology.py)
+            topology.bind_to_gpu_numa(L.device.index)
         ctx = mp.get_context(L.multiprocessing_context)
         cfg = L._worker_cfg()
         pass_ring = L.multiprocessing_context == "fork"
@@ -116,6 +121,8 @@ class _Run:
                 mode = hip().H2D_ZERO_COPY if L._resolve_h2d(self.ring.payload_capacity) == "zerocopy" \
                     else hip().H2D_DMA
                 self.engine = hip().Engine(dev, self.ring.n_slots, self.ring.payload_capacity, L.copy_streams, mode)
+                if L.numa_bind:
+                    topology.check_device(dev)
                 url, group = L._commit_target_url()
                 self.driver = hip().MainDriver(self.engine, self.name, url, group, L.prefetch, L.in_order,
                                                L._default_src_code())
@@ -250,6 +257,9 @@ class DeviceLoader:
             latency-bound; DMA above, where copy/compute overlap matters).
         event_every: record a slot-completion event for one batch in k (default: ring slots / 4,
             at most 4); slots in between are released with the next event on the same stream.
+        numa_bind: before forking the workers, restrict this process (and so the workers) to the CPUs
+            of the socket the target GPU is attached to (no-op on single-socket hosts or when
+            ``TORCHKAFKA_NUMA=0``); see ``utils/topology.py``.
     """
 
     def __init__(self, dataset, batch_size: int = 256, *, num_workers: int = 4, worker_init_fn=None,
@@ -261,7 +271,7 @@ class DeviceLoader:
                  rank: int | None = None, world_size: int | None = None, timeout: float = 0,
                  group_id: str | None = None, bootstrap_servers=None, base_seed: int | None = None,
                  lockstep_depth: int = 2, h2d: str = "auto", copy_streams: int = 4,
-                 event_every: int | None = None):
+                 event_every: int | None = None, numa_bind: bool = True):
         if batch_size < 1:
             raise ValueError("batch_size must be >= 1")
         if num_workers < 1:
@@ -303,6 +313,7 @@ class DeviceLoader:
         self.h2d = h2d
         self.copy_streams = max(1, int(copy_streams))
         self.event_every = None if event_every is None else max(1, int(event_every))
+        self.numa_bind = bool(numa_bind)
         r, w = dist_rank_world()
         self.rank = r if rank is None else int(rank)
         self.world_size = w if world_size is None else int(world_size)
