@@ -39,8 +39,8 @@ BASELINE_VALUE = 337237.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--batch-size", type=int, default=256)
     ap.add_argument("--dim", type=int, default=256, help="float32 elements per record")
     ap.add_argument("--workers", type=int, default=4)
@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy"])
     ap.add_argument("--copy-streams", type=int, default=4)
     ap.add_argument("--lockstep-depth", type=int, default=2)
+    ap.add_argument("--coalesce", type=int, default=4, help="staged batches collated per kernel launch")
     ap.add_argument("--no-numa", action="store_true", help="do not bind ranks to their GPU's NUMA node")
     return ap.parse_args()
 
@@ -113,7 +114,7 @@ def main() -> int:
         Records.placeholder(), B, num_workers=args.workers, device=device, dtype=dtype,
         slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
         in_order=args.in_order, h2d=args.h2d, copy_streams=args.copy_streams, lockstep_depth=args.lockstep_depth,
-        event_every=args.event_every, numa_bind=not args.no_numa,
+        event_every=args.event_every, numa_bind=not args.no_numa, coalesce=args.coalesce,
         worker_init_fn=Records.init_worker("bench", bootstrap_servers=url, group_id="bench",
                                            auto_offset_reset="earliest", check_crcs=not args.no_crc),
     )

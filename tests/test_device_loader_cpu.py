@@ -253,3 +253,37 @@ def test_stats_and_commit_latency(broker):
 def test_len_is_undefined(broker):
     with pytest.raises(TypeError):
         len(DeviceLoader(Vec16.placeholder(), 4, num_workers=1, device="cpu"))
+
+
+def test_state_dict_round_trip_resumes_exactly(broker):
+    """Checkpoint = committed offsets; load_state_dict rewinds the group to them."""
+    import json
+
+    broker.create_topic("t", 2)
+    broker.fill("t", 200, "fixed_f32", size=16, records_per_batch=10)
+    dl = loader(Vec16, broker, 20, workers=1)
+    it = iter(auto_commit(dl))
+    seen = []
+    for _ in range(5):
+        seen.append(next(it))
+    next(it)  # finishes (and commits) the 5th batch
+    it.close()
+    state = json.loads(json.dumps(dl.state_dict()))  # survives a JSON checkpoint
+    assert state["group_id"] == "g"
+    snap = {int(p): o for p, o in state["offsets"]["t"].items()}
+    assert sum(snap.values()) >= 100
+    # keep consuming: the group moves past the checkpoint
+    for _ in auto_commit(loader(Vec16, broker, 20, workers=1)):
+        pass
+    assert broker.committed_offsets("g", "t") == {0: 200, 1: 200}
+    # resume from the checkpoint: the first records delivered are exactly the checkpoint's positions
+    dl2 = loader(Vec16, broker, 20, workers=1)
+    dl2.load_state_dict(state)
+    assert broker.committed_offsets("g", "t") == snap
+    firsts = {}
+    for x in auto_commit(dl2):
+        for o, p in x[:, :2].long().tolist():
+            firsts.setdefault(p, o)
+    assert firsts == {p: o for p, o in snap.items() if o < 200}
+    with pytest.raises(ValueError):
+        dl2.load_state_dict({"version": 2, "offsets": {}})

@@ -209,3 +209,66 @@ def test_batched_events_with_stream_switches(broker):
         i += 1
     assert len(rows) == len(set(rows)) == 640
     assert broker.committed_offsets("g", "t") == {0: 320, 1: 320}
+
+
+@pytest.mark.parametrize("h2d,coalesce,dtype", [("zerocopy", 4, torch.float32), ("zerocopy", 8, torch.bfloat16),
+                                                ("dma", 4, torch.float32), ("zerocopy", 2, torch.float8_e4m3fn)])
+def test_coalesced_launches_deliver_identical_batches(broker, h2d, coalesce, dtype):
+    """Batches staged together are collated by one group launch and handed out one per request."""
+    import time
+
+    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
+
+    broker.create_topic("t", 4)
+    broker.fill("t", 480, "fixed_f32", size=64, records_per_batch=40)
+    DS = _dataset(FixedWidth(torch.float32, (64,)))
+    dl = DeviceLoader(DS.placeholder(), 48, num_workers=2, device="cuda:0", h2d=h2d, slots_per_worker=6, prefetch=2,
+                      coalesce=coalesce, dtype=dtype,
+                      worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    rows = []
+    for i, x in enumerate(auto_commit(dl)):
+        if i % 8 == 0:
+            time.sleep(0.02)  # a slow user step: the ring fills up and the next request forms a group
+        assert x.dtype == dtype and x.shape[1] == 64
+        if dtype == torch.float32:
+            _expected_rows(x)
+        # offsets above 256 are not exact in bf16/fp8: identify rows by (step, index) there
+        rows += [tuple(r) for r in x[:, :2].long().tolist()] if dtype == torch.float32 else \
+            [(i, j) for j in range(x.shape[0])]
+    assert len(rows) == len(set(rows)) == 1920
+    assert dl.stats.groups > 0
+    assert broker.committed_offsets("g", "t") == {p: 480 for p in range(4)}
+
+
+def test_coalesced_batch_consumed_on_another_stream(broker):
+    """A batch collated by a group launch on stream A and delivered while the user is on stream B:
+    B must wait for the group kernel (it is queued behind 20 ms of GPU work on A)."""
+    import time
+
+    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
+
+    broker.create_topic("t", 2)
+    broker.fill("t", 256, "fixed_f32", size=256, records_per_batch=32)
+    DS = _dataset(FixedWidth(torch.float32, (256,)))
+    dl = DeviceLoader(DS.placeholder(), 32, num_workers=2, device="cuda:0", h2d="zerocopy", slots_per_worker=8,
+                      coalesce=8, worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id="g",
+                                                               auto_offset_reset="earliest", consumer_timeout_ms=300))
+    a, b = torch.cuda.Stream(), torch.cuda.Stream()
+    it = iter(auto_commit(dl))
+    with torch.cuda.stream(a):
+        x = next(it)
+        time.sleep(0.1)                # every slot fills
+        torch.cuda._sleep(20_000_000)  # stream A busy for ~20 ms: the group kernel waits behind it
+        x = next(it)                   # group launch on A
+    copies = []
+    with torch.cuda.stream(b):
+        for x in it:
+            copies.append(x.clone())   # runs on B right away unless B waits for the group
+    torch.cuda.synchronize()
+    n = 64
+    for y in copies:
+        _expected_rows(y)
+        n += y.shape[0]
+    assert n == 512
+    assert dl.stats.groups > 0

@@ -19,6 +19,7 @@ for s in $STEPS; do
   case $s in
     build)  step build 600 python -c "import __graft_entry__ as g; g.build()" ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    pytestloader) step pytest_loader 300 python -u -m pytest tests/test_gpu_loader.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     pytest) step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     nccl)   step nccl_probe 120 python tools/nccl_probe.py ;;
     overhead) step host_overhead 120 python tools/host_overhead.py ;;
@@ -29,6 +30,9 @@ for s in $STEPS; do
     bench8) step bench_fp8 600 python bench.py --stats --dtype fp8 ;;
     benchlong) step bench_long 600 python bench.py --stats --steps 4000 --warmup 100 ;;
     benchnonuma) step bench_nonuma 600 python bench.py --stats --steps 4000 --warmup 100 --no-numa ;;
+    benchc1) step bench_c1 600 python bench.py --stats --steps 4000 --warmup 100 --coalesce 1 ;;
+    benchc8) step bench_c8 600 python bench.py --stats --steps 4000 --warmup 100 --coalesce 8 ;;
+    benchw8c8) step bench_w8c8 600 python bench.py --stats --steps 4000 --warmup 100 --coalesce 8 --workers 8 ;;
     benchnocrc) step bench_nocrc 600 python bench.py --stats --steps 4000 --warmup 100 --no-crc ;;
     benchzc) step bench_zc 600 python bench.py --stats --steps 4000 --warmup 100 --h2d zerocopy ;;
     benchs1) step bench_s1 600 python bench.py --stats --steps 4000 --warmup 100 --copy-streams 1 ;;

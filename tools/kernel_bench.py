@@ -2,9 +2,11 @@
 """Device-resident throughput of the gfx950 collate kernels vs PyTorch's own kernels.
 
 Inputs already live in HBM, so this measures the kernels alone (the loader's H2D is
-measured by bench.py).  For each case it prints µs per call and the effective HBM
-bandwidth (bytes read + bytes written) / time, next to the equivalent PyTorch op
-(``Tensor.to`` for the cast, an index_put-based pad for var-len).
+measured by bench.py).  For each case it prints the device time per call (``gpu_us``:
+calls captured in a HIP graph and replayed, so host launch cost is excluded) and the
+effective HBM bandwidth (bytes read + bytes written) / time, next to the equivalent
+PyTorch op (``Tensor.to`` for the cast, an index_put-based pad for var-len); ``eager_us``
+is the wall time per eager call including the Python wrapper and launch.
 
 Usage: python tools/kernel_bench.py [--quick] [--iters N]
 """
@@ -29,6 +31,36 @@ def timeit(fn, iters):
     e.record()
     e.synchronize()
     return s.elapsed_time(e) * 1000.0 / iters  # µs
+
+
+def timeit_graph(fn, iters, per_graph=20):
+    """Device time per call: `per_graph` calls captured in one HIP graph, replayed, so the host's
+    per-launch cost (Python wrapper + hipLaunchKernel) is out of the measurement."""
+    import torch
+
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(per_graph):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    reps = max(1, iters // per_graph)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        g.replay()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) * 1000.0 / (reps * per_graph)
 
 
 def main():
@@ -57,9 +89,12 @@ def main():
         src = torch.randn(rows, row, device=dev)
         t_ours = timeit(lambda: collate_fixed(src, dt), iters)
         t_torch = timeit(lambda: src.to(dt), iters)
+        g_ours = timeit_graph(lambda: collate_fixed(src, dt), iters)
+        g_torch = timeit_graph(lambda: src.to(dt), iters)
         nbytes = src.numel() * 4 + src.numel() * torch.empty((), dtype=dt).element_size()
-        out.append({"kernel": "fixed", "case": name, "us": round(t_ours, 2), "GBps": round(nbytes / t_ours / 1e3, 1),
-                    "torch_us": round(t_torch, 2), "torch_GBps": round(nbytes / t_torch / 1e3, 1)})
+        out.append({"kernel": "fixed", "case": name, "gpu_us": round(g_ours, 2), "GBps": round(nbytes / g_ours / 1e3, 1),
+                    "torch_gpu_us": round(g_torch, 2), "torch_GBps": round(nbytes / g_torch / 1e3, 1),
+                    "eager_us": round(t_ours, 2), "torch_eager_us": round(t_torch, 2)})
 
     g = torch.Generator().manual_seed(0)
     var_cases = [("config4 256 rows, L~U(0,512) f32->bf16", 256, 512, torch.float32),
@@ -102,8 +137,13 @@ def main():
         _ = collate_varlen(offs_d, vals, torch.bfloat16, L=L)
         t_ours = timeit(ours, iters)
         t_torch = timeit(torch_pad, iters)
-        out.append({"kernel": "varlen", "case": name, "us": round(t_ours, 2), "GBps": round(nbytes / t_ours / 1e3, 1),
-                    "torch_us": round(t_torch, 2), "torch_GBps": round(nbytes / t_torch / 1e3, 1)})
+        g_ours = timeit_graph(lambda: mod.collate_varlen(offs_d.data_ptr(), buf.data_ptr(), src_code[sdt], o.data_ptr(),
+                                                          2, rows, L, 0.0, ln.data_ptr(), 0,
+                                                          torch.cuda.current_stream(dev).cuda_stream), iters)
+        g_torch = timeit_graph(torch_pad, iters)
+        out.append({"kernel": "varlen", "case": name, "gpu_us": round(g_ours, 2), "GBps": round(nbytes / g_ours / 1e3, 1),
+                    "torch_gpu_us": round(g_torch, 2), "torch_GBps": round(nbytes / g_torch / 1e3, 1),
+                    "eager_us": round(t_ours, 2), "torch_eager_us": round(t_torch, 2)})
 
     for r in out:
         print(json.dumps(r))

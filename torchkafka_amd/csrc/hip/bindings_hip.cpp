@@ -249,11 +249,14 @@ PYBIND11_MODULE(_tkhip, m) {
              s["phase_launch_ns"] = d.ph_launch_ns_;
              s["phase_steps"] = d.ph_steps_;
              s["events"] = d.events_;
+             s["groups"] = d.groups();
              return s;
            })
       .def("reset_stats", &MainDriver::reset_stats)
       .def("set_event_every", &MainDriver::set_event_every, py::arg("n"))
       .def_property_readonly("event_every", &MainDriver::event_every)
+      .def("set_coalesce", &MainDriver::set_coalesce, py::arg("n"))
+      .def_property_readonly("coalesce", &MainDriver::coalesce)
       .def("enable_lockstep", &MainDriver::enable_lockstep, py::keep_alive<1, 2>())
       .def("finish_lockstep",
            [](MainDriver& d) {

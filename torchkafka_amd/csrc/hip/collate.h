@@ -19,6 +19,11 @@ void launch_fixed(const void* src, int src_dt, void* dst, int dst_dt, int64_t ro
 void launch_varlen(const int32_t* offs, const void* vals, int src_dt, void* out, int dst_dt, int64_t rows, int64_t L,
                    double pad, int64_t* lengths, uint8_t* mask, hipStream_t stream);
 
+// Up to kMaxGroup dense casts (consecutive batches, same dtypes and row width) in one launch.
+constexpr int kMaxGroup = 8;
+void launch_fixed_group(const void* const* srcs, int src_dt, void* const* dsts, int dst_dt, const int64_t* rows, int n,
+                        int64_t row, const float* shift, const float* scale, hipStream_t stream);
+
 std::vector<std::pair<std::string, double>> api_bench(int device, int iters);
 
 }  // namespace tkh

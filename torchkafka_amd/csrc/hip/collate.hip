@@ -20,6 +20,7 @@
 
 #include "collate.h"
 
+#include <algorithm>
 #include <chrono>
 #include <string>
 #include <vector>
@@ -244,6 +245,80 @@ void launch_fixed_t(const void* src, void* dst, int64_t rows, int64_t row, const
   }
 }
 
+// Coalesced launch: up to kMaxGroup ring slots (consecutive batches) collated by one
+// kernel, block range [k * bps, (k + 1) * bps) serving slot k.  One launch replaces k
+// (host: ~3-4 us of hipLaunchKernel + bookkeeping per batch), and in zero-copy mode
+// k x 256 KiB of PCIe reads are in flight at once instead of 256 KiB: a 256 KiB
+// zero-copy read is latency-bound at ~37 GB/s, 1 MiB reaches ~50 GB/s (measured,
+// profiles/r01_s3_baseline/register_probe.log).
+struct FixedGroupArgs {
+  const void* src[kMaxGroup];
+  void* dst[kMaxGroup];
+  int64_t groups[kMaxGroup];  // kEPT-element groups of slot k
+  int n;
+  int bps;                    // blocks per slot
+};
+
+template <typename S, typename D, bool AFFINE>
+__global__ __launch_bounds__(kThreads) void fixed_group_kernel(FixedGroupArgs a, int64_t row,
+                                                               const float* __restrict__ shift,
+                                                               const float* __restrict__ scale) {
+  using C = Conv<S, D, IsIntDst<D>::value>;
+  const int k = int(blockIdx.x) / a.bps;
+  const int b = int(blockIdx.x) - k * a.bps;
+  const S* __restrict__ src = static_cast<const S*>(a.src[k]);
+  D* __restrict__ dst = static_cast<D*>(a.dst[k]);
+  const int64_t n_groups = a.groups[k];
+  const int64_t stride = int64_t(a.bps) * kThreads;
+  for (int64_t g = int64_t(b) * kThreads + threadIdx.x; g < n_groups; g += stride) {
+    const Vec<S, kEPT> in = *reinterpret_cast<const Vec<S, kEPT>*>(src + g * kEPT);
+    const int64_t e = g * kEPT;
+    Vec<D, kEPT> out;
+    if constexpr (AFFINE) {
+      const int64_t d = e % row;
+      const Vec<float, kEPT> sh = *reinterpret_cast<const Vec<float, kEPT>*>(shift + d);
+      const Vec<float, kEPT> sc = *reinterpret_cast<const Vec<float, kEPT>*>(scale + d);
+#pragma unroll
+      for (int j = 0; j < kEPT; ++j) out.v[j] = C::apply(in.v[j], sh.v[j], sc.v[j], true);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kEPT; ++j) out.v[j] = C::apply(in.v[j], 0.f, 1.f, false);
+    }
+    *reinterpret_cast<Vec<D, kEPT>*>(dst + e) = out;
+  }
+}
+
+template <typename S, typename D>
+void launch_fixed_group_t(const void* const* srcs, void* const* dsts, const int64_t* rows, int n, int64_t row,
+                          const float* shift, const float* scale, hipStream_t stream) {
+  const bool affine = shift != nullptr;
+  bool vec = (row % kEPT == 0) &&
+             (!affine || (reinterpret_cast<uintptr_t>(shift) % 16 == 0 && reinterpret_cast<uintptr_t>(scale) % 16 == 0));
+  int64_t max_groups = 0;
+  for (int k = 0; k < n && vec; ++k) {
+    vec = reinterpret_cast<uintptr_t>(srcs[k]) % 16 == 0 && reinterpret_cast<uintptr_t>(dsts[k]) % 16 == 0;
+    max_groups = std::max<int64_t>(max_groups, rows[k] * row / kEPT);
+  }
+  if (!vec || max_groups == 0) {  // unaligned or odd rows: one ordinary launch per slot
+    for (int k = 0; k < n; ++k) launch_fixed_t<S, D>(srcs[k], dsts[k], rows[k], row, shift, scale, stream);
+    return;
+  }
+  FixedGroupArgs a{};
+  a.n = n;
+  for (int k = 0; k < n; ++k) {
+    a.src[k] = srcs[k];
+    a.dst[k] = dsts[k];
+    a.groups[k] = rows[k] * row / kEPT;
+  }
+  // every lane's load in flight at once up to ~2048 blocks in total
+  a.bps = int(std::max<int64_t>(1, std::min<int64_t>((max_groups + kThreads - 1) / kThreads, 2048 / n)));
+  const dim3 grid(unsigned(a.bps * n));
+  if (affine)
+    hipLaunchKernelGGL((fixed_group_kernel<S, D, true>), grid, dim3(kThreads), 0, stream, a, row, shift, scale);
+  else
+    hipLaunchKernelGGL((fixed_group_kernel<S, D, false>), grid, dim3(kThreads), 0, stream, a, row, shift, scale);
+}
+
 // Direct variant for 4- and 8-byte sources (f32 JSON values, i32/i64 token ids): a row's
 // elements are dword-aligned wherever the row starts, and gfx950 serves dword-aligned
 // global_load_dwordx4 at full width, so each lane loads its 8 elements straight from
@@ -361,6 +436,17 @@ void launch_varlen(const int32_t* offs, const void* vals, int src_dt, void* out,
   TK_DISPATCH_SRC(launch_varlen_t, offs, vals, out, rows, L, pad, lengths, mask, stream)
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("varlen collate launch: ") + hipGetErrorString(e));
+}
+
+void launch_fixed_group(const void* const* srcs, int src_dt, void* const* dsts, int dst_dt, const int64_t* rows, int n,
+                        int64_t row, const float* shift, const float* scale, hipStream_t stream) {
+  if (n < 1 || n > kMaxGroup) throw std::invalid_argument("collate: group size out of range");
+  if (!is_float_dt(dst_dt) && is_float_dt(src_dt))
+    throw std::invalid_argument("collate: float records cannot be cast to an integer dtype");
+  if (shift && !is_float_dt(dst_dt)) throw std::invalid_argument("collate: normalisation needs a float dtype");
+  TK_DISPATCH_SRC(launch_fixed_group_t, srcs, dsts, rows, n, row, shift, scale, stream)
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("fixed group collate launch: ") + hipGetErrorString(e));
 }
 
 __global__ void empty_kernel() {}

@@ -1,5 +1,7 @@
 #include "driver.h"
 
+#include "consumer.h"
+
 #include <unistd.h>
 
 #include <algorithm>
@@ -457,6 +459,98 @@ int64_t MainDriver::step_fixed(hipStream_t stream, int dst_dt, void* dst, int64_
   return out->n_rows;
 }
 
+int64_t MainDriver::step_group_begin(hipStream_t stream, bool auto_commit, int64_t timeout_ms, int* commit_status,
+                                     std::vector<int64_t>* group_rows, std::shared_ptr<void>* pre_out) {
+  *commit_status = 0;
+  group_rows->clear();
+  group_idx_.clear();
+  const int64_t t0 = tk::now_ns();
+  finish_delivered(stream);  // asking for the next batch finishes the previous one
+  if (auto_commit) *commit_status = commit_pending();
+  const int64_t t1 = tk::now_ns();
+  if (!ls_ && coalesce_ > 1) {
+    // stage what the workers already published, so a group can form (never blocks)
+    while (int(staged_.size()) < prefetch_ + coalesce_) {
+      const int r = poll_one(false, 0);
+      if (r == -3) return -3;
+      if (r <= 0) break;
+    }
+  }
+  const int r = next_slot(timeout_ms, &last);
+  const int64_t t2 = tk::now_ns();
+  ph_commit_ns_ += t1 - t0;
+  ph_next_ns_ += t2 - t1;
+  if (r < 0) return r;
+  if (last.pre) {
+    // collated by an earlier group launch; a consumer on another stream waits for that kernel
+    if (last.pre_stream != stream) eng_->stream_wait_done(int(last.pre_event_slot), stream);
+    *pre_out = std::move(last.pre_out);
+    delivered_ = last.wms;
+    prefetch_ready();
+    ++ph_steps_;
+    return last.n_rows;
+  }
+  group_rows->push_back(last.n_rows);
+  if (last.kind == uint32_t(tk::kPackFixed)) {
+    for (size_t i = 0; i < staged_.size() && int(group_rows->size()) < coalesce_; ++i) {
+      const SlotView& v = staged_[i];
+      if (v.g < 0) continue;  // watermark-only slot: rides on the next delivered batch
+      if (v.pre || v.kind != last.kind || v.src_dtype != last.src_dtype || v.max_row_len != last.max_row_len ||
+          v.shape != last.shape || v.n_rows == 0)
+        break;
+      group_idx_.push_back(i);
+      group_rows->push_back(v.n_rows);
+    }
+  }
+  return last.n_rows;
+}
+
+void MainDriver::step_group_launch(hipStream_t stream, int dst_dt, void* const* dsts, int64_t row,
+                                   const float* shift, const float* scale,
+                                   std::vector<std::shared_ptr<void>>&& handles) {
+  const int64_t t0 = tk::now_ns();
+  const int n = 1 + int(group_idx_.size());
+  if (int(handles.size()) != n - 1) throw std::invalid_argument("driver: group handles do not match the group");
+  int slots[kMaxGroup];
+  size_t voffs[kMaxGroup];
+  int64_t rows[kMaxGroup];
+  slots[0] = int(last.g);
+  voffs[0] = last.values_offset;
+  rows[0] = last.n_rows;
+  for (int k = 1; k < n; ++k) {
+    const SlotView& v = staged_[group_idx_[size_t(k - 1)]];
+    slots[k] = int(v.g);
+    voffs[k] = v.values_offset;
+    rows[k] = v.n_rows;
+  }
+  if (n == 1) {
+    collate_fixed(last, stream, dst_dt, dsts[0], row, shift, scale);
+  } else {
+    if (stream != last_stream_) {
+      cover_handed();
+      last_stream_ = stream;
+    }
+    eng_->collate_fixed_group(slots, n, stream, voffs, last.src_dtype, dsts, dst_dt, rows, row, shift, scale);
+    // one completion event (after the group kernel, on the last slot) releases every slot of the group
+    for (int k = 0; k < n; ++k) handed_.push_back(Handed{slots[k], k == n - 1});
+    unevented_ = 0;
+    ++events_;
+    ++groups_;
+    for (int k = 1; k < n; ++k) {
+      SlotView& v = staged_[group_idx_[size_t(k - 1)]];
+      v.pre = true;
+      v.pre_stream = stream;
+      v.pre_event_slot = slots[n - 1];
+      v.pre_out = std::move(handles[size_t(k - 1)]);
+    }
+  }
+  group_idx_.clear();
+  delivered_ = last.wms;
+  prefetch_ready();
+  ph_launch_ns_ += tk::now_ns() - t0;
+  ++ph_steps_;
+}
+
 std::vector<std::pair<uint32_t, int64_t>> MainDriver::committed() const {
   std::vector<std::pair<uint32_t, int64_t>> v(committed_.begin(), committed_.end());
   std::sort(v.begin(), v.end());
@@ -472,7 +566,7 @@ std::vector<std::pair<uint32_t, int64_t>> MainDriver::take_pending() {
 void MainDriver::reset_stats() {
   commits_ = commit_failures_ = 0;
   fill_ns_ = fills_ = blocked_ns_ = blocked_calls_ = ready_age_ns_ = 0;
-  ph_commit_ns_ = ph_next_ns_ = ph_launch_ns_ = ph_steps_ = events_ = 0;
+  ph_commit_ns_ = ph_next_ns_ = ph_launch_ns_ = ph_steps_ = events_ = groups_ = 0;
   commit_ns_.clear();
 }
 

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "broker.h"
+#include "collate.h"
 #include "engine.h"
 #include "rccl_lockstep.h"
 #include "ring.h"
@@ -31,6 +32,11 @@ struct SlotView {
   int32_t src_dtype = -1;
   std::vector<int64_t> shape;
   std::vector<tk::Watermark> wms;
+  // coalesced fast path: collated ahead of delivery by a group launch
+  bool pre = false;
+  hipStream_t pre_stream = nullptr;
+  int64_t pre_event_slot = -1;        // slot whose completion event follows the group kernel
+  std::shared_ptr<void> pre_out;      // the output tensor (opaque here: libtorch stays in torch_step.cpp)
 };
 
 class MainDriver {
@@ -66,6 +72,22 @@ class MainDriver {
   // Returns n_rows (>0), or -1 timeout, -2 end, -3 error; *commit_status as commit_pending().
   int64_t step_fixed(hipStream_t stream, int dst_dt, void* dst, int64_t row, const float* shift, const float* scale,
                      bool auto_commit, int64_t timeout_ms, int* commit_status, SlotView* out);
+
+  // Coalesced fast path, two phases around the caller's output allocation:
+  //   begin:  finish+commit the previous batch, take the next one.  If it was collated by an
+  //           earlier group launch, *pre_out receives its tensor and nothing is launched.
+  //           Otherwise *group_rows lists the rows of the batches to collate now: the one being
+  //           returned, then up to coalesce-1 already-staged fixed-width batches behind it.
+  //   launch: one kernel collates the group into dsts[k]; handles[k-1] (k >= 1) ride with the
+  //           staged batches until they are delivered.
+  // Returns n_rows (>0), or -1 timeout, -2 end, -3 error.
+  int64_t step_group_begin(hipStream_t stream, bool auto_commit, int64_t timeout_ms, int* commit_status,
+                           std::vector<int64_t>* group_rows, std::shared_ptr<void>* pre_out);
+  void step_group_launch(hipStream_t stream, int dst_dt, void* const* dsts, int64_t row, const float* shift,
+                         const float* scale, std::vector<std::shared_ptr<void>>&& handles);
+  void set_coalesce(int n) { coalesce_ = n < 1 ? 1 : (n > kMaxGroup ? kMaxGroup : n); }
+  int coalesce() const { return coalesce_; }
+  int64_t groups() const { return groups_; }
 
   const std::vector<tk::Watermark>& delivered() const { return delivered_; }
   std::vector<std::pair<uint32_t, int64_t>> committed() const;
@@ -155,6 +177,9 @@ class MainDriver {
   int64_t ph_commit_ns_ = 0, ph_next_ns_ = 0, ph_launch_ns_ = 0, ph_steps_ = 0, events_ = 0;
  private:
   std::vector<int64_t> commit_ns_;
+  int coalesce_ = 1;
+  int64_t groups_ = 0;
+  std::vector<size_t> group_idx_;  // staged_ indices of the batches behind `last` in the pending group
 };
 
 }  // namespace tkh

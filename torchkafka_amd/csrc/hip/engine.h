@@ -45,6 +45,13 @@ class Engine {
                      int64_t row, const float* shift, const float* scale, bool record = true);
   void collate_varlen(int s, hipStream_t user, size_t values_offset, int src_dt, void* out, int dst_dt, int64_t rows,
                       int64_t L, double pad, int64_t* lengths, uint8_t* mask, bool record = true);
+  // Consecutive fixed-width slots collated by one kernel (collate.h launch_fixed_group);
+  // the completion event of the last slot is recorded (it stands for all of them).
+  void collate_fixed_group(const int* slots, int n, hipStream_t user, const size_t* values_offsets, int src_dt,
+                           void* const* dsts, int dst_dt, const int64_t* rows, int64_t row, const float* shift,
+                           const float* scale);
+  // `user` waits for slot s's completion event (a batch collated on another stream).
+  void stream_wait_done(int s, hipStream_t user);
   void record_done(int s, hipStream_t user) { finish(s, user); }
   void copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes);
   void synchronize();

@@ -141,6 +141,25 @@ void Engine::collate_fixed(int s, hipStream_t user, size_t values_offset, int sr
   if (record) finish(s, user);
 }
 
+void Engine::collate_fixed_group(const int* slots, int n, hipStream_t user, const size_t* values_offsets, int src_dt,
+                                 void* const* dsts, int dst_dt, const int64_t* rows, int64_t row, const float* shift,
+                                 const float* scale) {
+  if (n < 1 || n > kMaxGroup) throw std::invalid_argument("engine: bad group size");
+  const void* srcs[kMaxGroup];
+  for (int k = 0; k < n; ++k) {
+    check_slot(slots[k]);
+    begin(slots[k], user);
+    srcs[k] = src_base(slots[k]) + values_offsets[k];
+  }
+  launch_fixed_group(srcs, src_dt, dsts, dst_dt, rows, n, row, shift, scale, user);
+  finish(slots[n - 1], user);
+}
+
+void Engine::stream_wait_done(int s, hipStream_t user) {
+  check_slot(s);
+  TKH_CHECK(hipStreamWaitEvent(user, done_[size_t(s)], 0));
+}
+
 void Engine::collate_varlen(int s, hipStream_t user, size_t values_offset, int src_dt, void* out, int dst_dt,
                             int64_t rows, int64_t L, double pad, int64_t* lengths, uint8_t* mask, bool record) {
   check_slot(s);

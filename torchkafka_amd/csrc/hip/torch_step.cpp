@@ -14,6 +14,7 @@
 #include <pybind11/stl.h>
 
 #include "driver.h"
+#include "collate.h"
 #include "dtypes.h"
 
 namespace py = pybind11;
@@ -59,6 +60,57 @@ void register_torch_step(py::module_& m) {
       py::arg("scale"), py::arg("auto_commit"), py::arg("timeout_ms"),
       "finish+commit the previous batch, take the next slot and collate it into a new tensor "
       "allocated on the current stream -> (rows, commit_status, tensor | None)");
+
+  // Coalesced variant: when several fixed-width batches are already staged, one allocation and
+  // one kernel launch serve up to driver.coalesce of them; the following calls return the
+  // pre-collated tensors without any HIP call (MainDriver::step_group_begin/launch).
+  m.def(
+      "step_fixed_group_tensor",
+      [](MainDriver& d, int device, std::vector<int64_t> shape, int dst_dt, int64_t row, uintptr_t shift,
+         uintptr_t scale, bool auto_commit, int64_t timeout_ms) -> py::tuple {
+        const auto dev = c10::DeviceIndex(device);
+        hipStream_t stream = c10::hip::getCurrentHIPStream(dev).stream();
+        int cs = 0;
+        int64_t r;
+        std::vector<int64_t> rows;
+        std::shared_ptr<void> pre;
+        {
+          py::gil_scoped_release nogil;
+          r = d.step_group_begin(stream, auto_commit, timeout_ms, &cs, &rows, &pre);
+        }
+        if (r <= 0) return py::make_tuple(r, cs, py::none());
+        at::Tensor out;
+        if (pre) {
+          out = *static_cast<at::Tensor*>(pre.get());
+        } else {
+          int64_t total = 0;
+          for (auto x : rows) total += x;
+          std::vector<int64_t> all_shape(shape);
+          all_shape[0] = total;
+          at::Tensor all =
+              at::empty(all_shape, at::TensorOptions().dtype(scalar_type_of(dst_dt)).device(at::kCUDA, dev));
+          void* dsts[kMaxGroup];
+          std::vector<std::shared_ptr<void>> handles;
+          handles.reserve(rows.size());
+          int64_t off = 0;
+          for (size_t k = 0; k < rows.size(); ++k) {
+            at::Tensor t = rows.size() == 1 ? all : all.narrow(0, off, rows[k]);
+            dsts[k] = t.data_ptr();
+            if (k == 0)
+              out = t;
+            else
+              handles.emplace_back(new at::Tensor(std::move(t)), [](void* p) { delete static_cast<at::Tensor*>(p); });
+            off += rows[k];
+          }
+          py::gil_scoped_release nogil;
+          d.step_group_launch(stream, dst_dt, dsts, row, reinterpret_cast<const float*>(shift),
+                              reinterpret_cast<const float*>(scale), std::move(handles));
+        }
+        return py::make_tuple(r, cs, py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(out))));
+      },
+      py::arg("driver"), py::arg("device"), py::arg("shape"), py::arg("dst_dt"), py::arg("row"), py::arg("shift"),
+      py::arg("scale"), py::arg("auto_commit"), py::arg("timeout_ms"),
+      "coalesced step_fixed_tensor: up to driver.coalesce staged batches collated by one launch");
 }
 
 }  // namespace tkh

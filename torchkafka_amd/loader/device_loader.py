@@ -128,6 +128,7 @@ class _Run:
                                                L._default_src_code())
                 self.driver.set_commit_on_device(L.commit_on == "device")
                 self.driver.set_event_every(L._event_every(self.ring.n_slots))
+                self.driver.set_coalesce(L.coalesce)
         except BaseException:
             self.close()
             raise
@@ -257,6 +258,9 @@ class DeviceLoader:
             latency-bound; DMA above, where copy/compute overlap matters).
         event_every: record a slot-completion event for one batch in k (default: ring slots / 4,
             at most 4); slots in between are released with the next event on the same stream.
+        coalesce: fixed-width batches that are already staged when the next one is requested are
+            collated together, up to this many per kernel launch (one allocation, one launch, one
+            completion event); the following requests return them without a HIP call.  1 disables.
         numa_bind: before forking the workers, restrict this process (and so the workers) to the CPUs
             of the socket the target GPU is attached to (no-op on single-socket hosts or when
             ``TORCHKAFKA_NUMA=0``); see ``utils/topology.py``.
@@ -271,7 +275,7 @@ class DeviceLoader:
                  rank: int | None = None, world_size: int | None = None, timeout: float = 0,
                  group_id: str | None = None, bootstrap_servers=None, base_seed: int | None = None,
                  lockstep_depth: int = 2, h2d: str = "auto", copy_streams: int = 4,
-                 event_every: int | None = None, numa_bind: bool = True):
+                 event_every: int | None = None, numa_bind: bool = True, coalesce: int = 4):
         if batch_size < 1:
             raise ValueError("batch_size must be >= 1")
         if num_workers < 1:
@@ -314,6 +318,7 @@ class DeviceLoader:
         self.copy_streams = max(1, int(copy_streams))
         self.event_every = None if event_every is None else max(1, int(event_every))
         self.numa_bind = bool(numa_bind)
+        self.coalesce = max(1, min(8, int(coalesce)))
         r, w = dist_rank_world()
         self.rank = r if rank is None else int(rank)
         self.world_size = w if world_size is None else int(world_size)
@@ -561,7 +566,7 @@ class DeviceLoader:
         out_shape = [B, *shape]
         # one native call per batch: allocate (torch caching allocator, current stream),
         # finish + commit the previous batch, take the next slot, launch the collate
-        step = hip().step_fixed_tensor
+        step = hip().step_fixed_group_tensor if self.coalesce > 1 else hip().step_fixed_tensor
         while True:
             t0 = time.perf_counter_ns()
             r, cs, out = step(drv, dev_index, out_shape, dst_code, row, shift, scale, auto_commit, 100)
@@ -598,6 +603,7 @@ class DeviceLoader:
         self.stats.phase_launch_ns += st["phase_launch_ns"]
         self.stats.phase_steps += st["phase_steps"]
         self.stats.events += st["events"]
+        self.stats.groups += st.get("groups", 0)
         self.stats.commits += st["commits"]
         self.stats.commit_failures += st["commit_failures"]
         self.stats.commit_ns.extend(st["commit_ns"])
@@ -835,6 +841,38 @@ class DeviceLoader:
 
     def committed_offsets(self) -> dict[int, int]:
         return dict(self._committed)
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    def state_dict(self) -> dict:
+        """Committed positions for a model checkpoint (the committed offsets ARE the
+        checkpoint).  ``{"version": 1, "group_id": g, "offsets": {topic: {partition: offset}}}``
+        -- JSON-serialisable.  Under DDP each rank reports the partitions it consumed and committed;
+        save one per rank or all-gather them."""
+        b = self._broker()
+        offsets: dict[str, dict[int, int]] = {}
+        for pidx, off in sorted(self.committed_offsets().items()):
+            tp = b.tp_of(pidx)
+            offsets.setdefault(tp.topic, {})[tp.partition] = int(off)
+        return {"version": 1, "group_id": self._group_id, "offsets": offsets}
+
+    def load_state_dict(self, state: dict) -> None:
+        """Resumes from a checkpoint's offsets: they are committed for the group (an administrative
+        commit, as ``kafka-consumer-groups --reset-offsets`` does), so the next iteration's workers
+        start exactly there, like consumers restarting after a crash.  Call before iterating."""
+        from ..client.records import TopicPartition
+
+        if self._run is not None and not self._run.closed:
+            raise RuntimeError("load_state_dict() must be called before iterating the loader")
+        if int(state.get("version", 1)) != 1:
+            raise ValueError(f"unsupported DeviceLoader state version {state.get('version')}")
+        group = state.get("group_id") or self._group_id
+        if group is None:
+            raise RuntimeError("load_state_dict needs a group_id (in the state or the loader)")
+        b = self._broker()
+        offs = {TopicPartition(t, int(p)): int(o) for t, parts in state["offsets"].items() for p, o in parts.items()}
+        if offs:
+            b.commit(group, offs)
+        self._committed.update({b.pidx(tp.topic, tp.partition): o for tp, o in offs.items()})
 
     def close(self) -> None:
         if self._run is not None:

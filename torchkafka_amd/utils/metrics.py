@@ -38,6 +38,7 @@ class LoaderStats:
     phase_launch_ns: int = 0   # native step driver: collate launch (+event)
     phase_steps: int = 0
     events: int = 0            # completion events recorded (batched: fewer than batches)
+    groups: int = 0            # coalesced launches (several batches collated by one kernel)
     started: float = field(default_factory=time.perf_counter)
     max_commit_samples: int = 100000
 
@@ -73,6 +74,7 @@ class LoaderStats:
             "native_next_us_per_step": self.phase_next_ns / 1e3 / max(self.phase_steps, 1),
             "native_launch_us_per_step": self.phase_launch_ns / 1e3 / max(self.phase_steps, 1),
             "events_per_batch": self.events / max(self.batches, 1),
+            "group_launches_per_batch": self.groups / max(self.batches, 1),
             "commits": self.commits,
             "commit_failures": self.commit_failures,
             "commit_p50_us": percentile(c_us, 50),
