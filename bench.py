@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--stats", action="store_true", help="print loader stats to stderr")
     ap.add_argument("--in-order", action="store_true", help="strict worker round-robin delivery")
     ap.add_argument("--event-every", type=int, default=None)
-    ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy"])
+    ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy", "direct"])
     ap.add_argument("--copy-streams", type=int, default=4)
     ap.add_argument("--lockstep-depth", type=int, default=2)
     ap.add_argument("--coalesce", type=int, default=4, help="staged batches collated per kernel launch")

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--slots-per-worker", type=int, default=2)
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy", "direct"])
     args = ap.parse_args()
 
     import torch
@@ -56,7 +57,7 @@ def main():
         fill_s = time.perf_counter() - t
         dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
         dl = DeviceLoader(Big.placeholder(), B, num_workers=args.workers, device=args.device, dtype=dtype,
-                          slots_per_worker=args.slots_per_worker, prefetch=1,
+                          slots_per_worker=args.slots_per_worker, prefetch=1, h2d=args.h2d,
                           worker_init_fn=Big.init_worker("big", bootstrap_servers=url, group_id="cfg5",
                                                          auto_offset_reset="earliest"))
         it = iter(auto_commit(dl))

@@ -272,3 +272,74 @@ def test_coalesced_batch_consumed_on_another_stream(broker):
         n += y.shape[0]
     assert n == 512
     assert dl.stats.groups > 0
+
+
+def _produce_random(broker, topic, n_parts, n_per_part, nbytes, seed=0):
+    import random
+
+    rng = random.Random(seed)
+    for p in range(n_parts):
+        vals, keys = [], []
+        for _ in range(n_per_part):
+            vals.append(bytes(rng.getrandbits(8) for _ in range(nbytes)))
+            keys.append(b"k" * rng.randrange(0, 9))  # shifts every value's alignment in the log
+        broker.produce(topic, vals, partition=p, keys=keys)
+
+
+@pytest.mark.parametrize("shape,src,dst,norm", [
+    ((256,), torch.float32, torch.bfloat16, False),
+    ((13,), torch.float32, torch.float32, False),       # 52-byte rows: partial last lane
+    ((700,), torch.float32, torch.bfloat16, False),     # 2800-byte rows: three 1 KiB wave segments
+    ((40,), torch.bfloat16, torch.float32, False),      # 2-byte source elements
+    ((48,), torch.uint8, torch.float16, False),         # 1-byte source elements
+    ((64,), torch.float32, torch.bfloat16, True),       # fused normalisation
+])
+def test_direct_log_gather_matches_copy_path(broker, shape, src, dst, norm):
+    """h2d='direct' (rows gathered from the pinned broker log at any byte alignment) delivers
+    bit-identical batches to the copying zero-copy path, with the same commits."""
+    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
+
+    numel = 1
+    for d in shape:
+        numel *= d
+    esize = torch.empty((), dtype=src).element_size()
+    broker.create_topic("t", 3)
+    _produce_random(broker, "t", 3, 70, numel * esize)
+    DS = _dataset(FixedWidth(src, shape))
+    normalize = (0.5, 2.0) if norm else None
+    outs = {}
+    for mode in ("zerocopy", "direct"):
+        dl = DeviceLoader(DS.placeholder(), 32, num_workers=1, device="cuda:0", dtype=dst, h2d=mode, in_order=True,
+                          normalize=normalize, coalesce=4,
+                          worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id=f"g-{mode}",
+                                                        auto_offset_reset="earliest", consumer_timeout_ms=300))
+        xs = [x.clone() for x in auto_commit(dl)]
+        outs[mode] = torch.cat(xs)
+        assert broker.committed_offsets(f"g-{mode}", "t") == {0: 70, 1: 70, 2: 70}
+        if mode == "direct":
+            assert dl.stats.log_bytes_registered > 0
+    a, b = outs["zerocopy"], outs["direct"]
+    assert a.shape == b.shape == (210, *shape)
+    ai = a.view(torch.int16) if a.element_size() == 2 else a.view(torch.int32) if a.element_size() == 4 else a
+    bi = b.view(torch.int16) if b.element_size() == 2 else b.view(torch.int32) if b.element_size() == 4 else b
+    assert torch.equal(ai, bi)
+
+
+def test_direct_log_gather_values(broker):
+    """Direct mode against known record contents (the synthetic f32 generator), several workers."""
+    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
+
+    broker.create_topic("t", 6)
+    broker.fill("t", 300, "fixed_f32", size=32, records_per_batch=50)
+    DS = _dataset(FixedWidth(torch.float32, (32,)))
+    dl = DeviceLoader(DS.placeholder(), 64, num_workers=3, device="cuda:0", h2d="direct",
+                      worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    seen = set()
+    for x in auto_commit(dl):
+        _expected_rows(x)
+        for o, p in x[:, :2].cpu().long().tolist():
+            assert (p, o) not in seen
+            seen.add((p, o))
+    assert len(seen) == 1800
+    assert broker.committed_offsets("g", "t") == {p: 300 for p in range(6)}

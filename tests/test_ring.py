@@ -119,3 +119,51 @@ def test_fill_slot_native_pack(broker):
         assert rows == 50 and timed_out
     finally:
         r.unlink()
+
+
+def test_gather_slot_locates_every_value_in_the_log(broker):
+    """kPackGatherFixed (h2d='direct'): one (pidx << 44 | byte offset) per row, pointing at exactly
+    the record value the copying packer would have written, with per-partition log extents."""
+    import struct
+
+    from torchkafka_amd.client.consumer import KafkaConsumer
+    from torchkafka_amd.ops.native import core
+
+    broker.create_topic("g", 3)
+    rng = __import__("random").Random(5)
+    for p in range(3):
+        vals = [bytes(rng.getrandbits(8) for _ in range(40)) for _ in range(30)]
+        keys = [b"k" * rng.randrange(0, 7) for _ in range(30)]  # vary the value alignment in the log
+        broker.produce("g", vals, partition=p, keys=keys)
+    ring = core().Ring.create(f"/tkgather-{os.getpid()}", 1, 2, 1 << 16)
+    try:
+        c = KafkaConsumer("g", bootstrap_servers=broker.url, group_id="x", auto_offset_reset="earliest")
+        c.assign_shard(["g"], 0, 1, 0, 1)
+        assert ring.worker_acquire(0, 0, 1000)
+        g = ring.gslot(0, 0)
+        rows, scanned, _, _ = c._fetcher.fill_slot(ring, g, core().PACK_FIXED, 4, 10, 0, -1, True, False, 64, 100,
+                                                    True)
+        assert rows == 64
+        summ = ring.slot_summary(g)
+        assert summ[7] == core().PACK_GATHER_FIXED and summ[2] == 64 * 8
+        ents = struct.unpack("<64Q", bytes(ring.payload_view(g)[: 64 * 8]))
+        b = broker.native
+        tps = {broker.pidx("g", p): p for p in range(3)}
+        got = [(tps[e >> 44], e & ((1 << 44) - 1)) for e in ents]
+        # reference: the same records through the copying consumer path
+        c2 = KafkaConsumer("g", bootstrap_servers=broker.url, group_id="y", auto_offset_reset="earliest",
+                           consumer_timeout_ms=100)
+        c2.assign_shard(["g"], 0, 1, 0, 1)
+        by_tp = {}
+        for r in c2:
+            by_tp.setdefault(r.partition, []).append(r.value)
+        seen = {p: 0 for p in range(3)}
+        for p, off in got:
+            assert b.read_log(broker.pidx("g", p), off, 40) == by_tp[p][seen[p]]
+            seen[p] += 1
+        ext = dict(zip([w[0] for w in ring.watermarks(g)], ring.slot_info(g).get("log_end", [])))
+        for pidx, end in ext.items():
+            assert end == max(off + 40 for p, off in got if broker.pidx("g", p) == pidx)
+    finally:
+        ring.shutdown()
+        ring.unlink()

@@ -33,6 +33,11 @@ for s in $STEPS; do
     benchc1) step bench_c1 600 python bench.py --stats --steps 4000 --warmup 100 --coalesce 1 ;;
     benchc8) step bench_c8 600 python bench.py --stats --steps 4000 --warmup 100 --coalesce 8 ;;
     benchw8c8) step bench_w8c8 600 python bench.py --stats --steps 4000 --warmup 100 --coalesce 8 --workers 8 ;;
+    benchdirect) step bench_direct 600 python bench.py --stats --steps 4000 --warmup 100 --h2d direct ;;
+    benchdirectc8) step bench_direct_c8 600 python bench.py --stats --steps 4000 --warmup 100 --h2d direct --coalesce 8 ;;
+    benchdirectw8) step bench_direct_w8 600 python bench.py --stats --steps 4000 --warmup 100 --h2d direct --workers 8 ;;
+    pytestdirect) step pytest_direct 300 python -u -m pytest tests/test_gpu_loader.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread -k "direct" ;;
+    benchnospin) TORCHKAFKA_WORKER_SPIN_US=0 step bench_nospin 600 python bench.py --stats --steps 4000 --warmup 100 ;;
     benchnocrc) step bench_nocrc 600 python bench.py --stats --steps 4000 --warmup 100 --no-crc ;;
     benchzc) step bench_zc 600 python bench.py --stats --steps 4000 --warmup 100 --h2d zerocopy ;;
     benchs1) step bench_s1 600 python bench.py --stats --steps 4000 --warmup 100 --copy-streams 1 ;;
@@ -45,6 +50,8 @@ for s in $STEPS; do
     config1) step config1 300 python benchmarks/config1_cpu_plumbing.py ;;
     config4) step config4 300 python benchmarks/config4_json_varlen.py ;;
     config5) step config5 300 python benchmarks/config5_large_messages.py ;;
+    config5direct) step config5_direct 300 python benchmarks/config5_large_messages.py --h2d direct ;;
+    config5w8) step config5_w8 300 python benchmarks/config5_large_messages.py --workers 8 ;;
     kbench) step kernel_bench 300 python tools/kernel_bench.py ;;
     kprof)  (cd /tmp && export TMPDIR=/tmp && step kprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kprof" -o run -- python3 "$OLDPWD/tools/kernel_bench.py" --quick) || exit $? ;;
     # TCC has 4 slots per pass: FETCH_SIZE costs 3, WRITE_SIZE 2 (MI355X_MICROARCH.md) -> two passes

@@ -215,6 +215,12 @@ PYBIND11_MODULE(_tkcore, m) {
       .def("high_watermark", [](Broker& b, uint32_t p) { return b.part(p).high_watermark.load(); })
       .def("log_start_offset", [](Broker& b, uint32_t p) { return b.part(p).log_start_offset.load(); })
       .def("log_bytes", [](Broker& b, uint32_t p) { return b.part(p).log_end_pos.load(); })
+      .def("read_log",
+           [](Broker& b, uint32_t p, uint64_t off, uint64_t n) {
+             if (off + n > b.part(p).log_end_pos.load()) throw std::out_of_range("read_log beyond the log end");
+             return py::bytes(reinterpret_cast<const char*>(b.log_base(p)) + off, n);
+           },
+           py::arg("pidx"), py::arg("offset"), py::arg("n"), "raw bytes of a partition log (tests, tools)")
       .def("partition_stats",
            [](Broker& b, uint32_t p) {
              auto& P = b.part(p);
@@ -416,9 +422,11 @@ PYBIND11_MODULE(_tkcore, m) {
       .def(
           "fill_slot",
           [](PyFetcher& f, py::object ring_obj, uint32_t gslot, int kind, int elem_size, int64_t row_elems,
-             int64_t min_len, int64_t max_len, bool truncate, bool skip_bad, int64_t batch_rows, int64_t timeout_ms) {
+             int64_t min_len, int64_t max_len, bool truncate, bool skip_bad, int64_t batch_rows, int64_t timeout_ms,
+             bool gather) {
             PyRing& ring = ring_obj.cast<PyRing&>();
             PackSpec s;
+            s.gather = gather;
             s.kind = kind;
             s.elem_size = elem_size;
             s.row_elems = row_elems;
@@ -435,7 +443,7 @@ PYBIND11_MODULE(_tkcore, m) {
           },
           py::arg("ring"), py::arg("gslot"), py::arg("kind"), py::arg("elem_size"), py::arg("row_elems"),
           py::arg("min_len"), py::arg("max_len"), py::arg("truncate"), py::arg("skip_bad"), py::arg("batch_rows"),
-          py::arg("timeout_ms"));
+          py::arg("timeout_ms"), py::arg("gather") = false);
 
   // ---- ring
   py::class_<PyRing>(m, "Ring")
@@ -483,6 +491,7 @@ PYBIND11_MODULE(_tkcore, m) {
              d["t_fill_start_ns"] = h->t_fill_start_ns;
              d["t_ready_ns"] = h->t_ready_ns;
              d["error"] = std::string(h->err, h->err_len);
+             d["log_end"] = std::vector<uint64_t>(h->log_end, h->log_end + h->n_parts);
              return d;
            })
       .def("watermarks",
@@ -538,6 +547,7 @@ PYBIND11_MODULE(_tkcore, m) {
              h->flags |= kSlotError;
            })
       .def("set_worker_pid", [](PyRing& r, uint32_t w, int64_t pid) { r.r->header()->worker_pid[w].store(pid); })
+      .def("set_worker_spin_ns", [](PyRing& r, int64_t ns) { r.r->set_worker_spin_ns(ns); })
       .def("worker_pid", [](PyRing& r, uint32_t w) { return r.r->header()->worker_pid[w].load(); })
       .def("worker_acquire",
            [](PyRing& r, uint32_t w, uint32_t i, int64_t timeout_ms) {
@@ -564,5 +574,6 @@ PYBIND11_MODULE(_tkcore, m) {
   m.attr("PACK_FIXED") = int(kPackFixed);
   m.attr("PACK_VARLEN") = int(kPackVarlen);
   m.attr("PACK_JSON_F32") = int(kPackJsonF32);
+  m.attr("PACK_GATHER_FIXED") = int(kPackGatherFixed);
   m.attr("SLOT_HEADER_BYTES") = kSlotHeaderBytes;
 }

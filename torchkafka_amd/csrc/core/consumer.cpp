@@ -238,10 +238,11 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   const uint64_t cap = ring.payload_capacity();
   auto& parts = f.parts();
   FillOutcome out;
+  const bool gather = spec.kind == kPackFixed && spec.gather;
   h->n_rows = 0;
   h->n_parts = 0;
   h->flags = 0;
-  h->kind = uint32_t(spec.kind);
+  h->kind = uint32_t(gather ? kPackGatherFixed : spec.kind);
   h->err_len = 0;
   h->max_row_len = 0;
   h->total_elems = 0;
@@ -255,7 +256,14 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   const uint64_t row_bytes = fixed ? uint64_t(spec.row_elems) * uint64_t(spec.elem_size) : 0;
   uint64_t values_off = 0;
   int32_t* offs = nullptr;
-  if (fixed) {
+  uint64_t* gat = nullptr;
+  std::vector<const uint8_t*> log_of;
+  if (gather) {
+    if (uint64_t(B) * 8 > cap) throw std::invalid_argument("ring slot too small for the batch's gather table");
+    gat = reinterpret_cast<uint64_t*>(pay);
+    log_of.reserve(parts.size());
+    for (const auto& fp : parts) log_of.push_back(f.broker().log_base(fp.pidx));
+  } else if (fixed) {
     if (uint64_t(B) * row_bytes > cap) throw std::invalid_argument("ring slot too small for the batch");
   } else {
     values_off = align_up(uint64_t(B + 1) * 4, 256);
@@ -280,6 +288,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
       h->wm[k].pidx = parts[cur_part].pidx;
       h->wm[k].count = 0;
       h->wm[k].first_offset = parts[cur_part].position;
+      h->log_end[k] = 0;
     }
     h->wm[k].count++;
     h->wm[k].next_offset = r.offset + 1;
@@ -296,6 +305,15 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
     if (r.value == nullptr) { touch(r); return kTake; }  // null value == `_process` returned None
     if (fixed) {
       if (uint64_t(r.value_len) != row_bytes) return bad(r, "value size does not match the fixed-width schema");
+      if (gather) {
+        const uint64_t off = uint64_t(r.value - log_of[cur_part]);
+        gat[rows] = (uint64_t(parts[cur_part].pidx) << kGatherShift) | off;
+        touch(r);
+        uint64_t& e = h->log_end[wm_of[cur_part]];
+        e = std::max<uint64_t>(e, off + row_bytes);
+        ++rows;
+        return rows == B ? kTakeStop : kTake;
+      }
       copy_to_slot(vals + uint64_t(rows) * row_bytes, r.value, row_bytes);
       touch(r);
       ++rows;
@@ -387,7 +405,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   h->n_rows = uint32_t(rows);
   h->row_bytes = uint32_t(row_bytes);
   h->values_offset = values_off;
-  h->values_bytes = fixed ? uint64_t(rows) * row_bytes : vused;
+  h->values_bytes = gather ? uint64_t(rows) * 8 : (fixed ? uint64_t(rows) * row_bytes : vused);
   h->payload_bytes = values_off + h->values_bytes;
   h->max_row_len = fixed ? spec.row_elems : max_len;
   h->total_elems = fixed ? rows * spec.row_elems : elems;

@@ -62,7 +62,14 @@ class Fetcher {
 };
 
 // ------------------------------------------------------------ packers
-enum PackKind : int { kPackFixed = 0, kPackVarlen = 1, kPackJsonF32 = 2 };
+enum PackKind : int { kPackFixed = 0, kPackVarlen = 1, kPackJsonF32 = 2, kPackGatherFixed = 3 };
+
+// kPackGatherFixed: the slot holds no values, only one uint64 per row locating the row's value
+// inside the broker log it was fetched from, (pidx << kGatherShift) | byte offset.  The main
+// process pins the logs in place and the collate kernel gathers rows straight out of them
+// (DeviceLoader h2d="direct"): the worker never copies the payload.
+constexpr int kGatherShift = 44;
+constexpr uint64_t kGatherOffsetMask = (uint64_t(1) << kGatherShift) - 1;
 
 struct PackSpec {
   int kind = kPackFixed;
@@ -72,6 +79,7 @@ struct PackSpec {
   int64_t max_len = -1;     // var-len/JSON: longer rows truncated (truncate) or skipped
   int truncate = 1;
   int skip_bad = 0;         // malformed rows: 1 = skip, 0 = raise
+  int gather = 0;           // fixed-width: emit log locations (kPackGatherFixed) instead of values
 };
 
 struct FillOutcome {

@@ -105,9 +105,16 @@ SlotHeader* Ring::slot(uint32_t g) const {
   return reinterpret_cast<SlotHeader*>(base_ + hdr_bytes + uint64_t(g) * hdr_->slot_stride);
 }
 
+// A worker whose sub-ring is full spins for up to spin_ns_ (200 µs) before sleeping on the futex.
+// With workers ahead of the consumer (the common case), a slot comes back every few µs; if
+// the worker slept instead, every main_release would pay a futex_wake syscall (~1-2 µs) on the
+// main thread's per-batch path, plus the worker's wake-up latency.  Workers run on their own
+// cores (one per worker), so the spin costs no one else's time.
 bool Ring::worker_acquire(uint32_t worker, uint32_t i, int64_t timeout_ms) {
   SlotHeader* s = slot(gslot(worker, i));
-  const int64_t deadline = timeout_ms < 0 ? INT64_MAX : now_ns() + timeout_ms * 1000000LL;
+  const int64_t start = now_ns();
+  const int64_t deadline = timeout_ms < 0 ? INT64_MAX : start + timeout_ms * 1000000LL;
+  const int64_t spin_until = std::min(deadline, start + spin_ns_);
   for (;;) {
     if (hdr_->shutdown.load(std::memory_order_acquire)) return false;
     const uint32_t seq = hdr_->free_seq[worker].load(std::memory_order_acquire);
@@ -118,6 +125,10 @@ bool Ring::worker_acquire(uint32_t worker, uint32_t i, int64_t timeout_ms) {
     }
     const int64_t now = now_ns();
     if (now >= deadline) return false;
+    if (now < spin_until) {
+      for (int k = 0; k < 64; ++k) cpu_relax();
+      continue;
+    }
     wait_seq(&hdr_->free_seq[worker], &hdr_->free_waiters[worker], seq, std::min<int64_t>(deadline - now, 100000000LL));
   }
 }

@@ -59,6 +59,8 @@ struct alignas(64) SlotHeader {
   int64_t shape[8];
   char err[2048];
   Watermark wm[kMaxSlotParts];
+  // direct (log-gather) slots: bytes of wm[k]'s partition log referenced by this slot, [0, log_end[k])
+  uint64_t log_end[kMaxSlotParts];
 };
 static_assert(sizeof(SlotHeader) <= kSlotHeaderBytes, "slot header too large");
 
@@ -106,9 +108,12 @@ class Ring {
   void main_release(uint32_t gslot);    // INFLIGHT/READY -> FREE (+wake worker)
   void shutdown();
   void unlink();
+  // Worker side: how long worker_acquire spins on a full sub-ring before sleeping (ns).
+  void set_worker_spin_ns(int64_t ns) { spin_ns_ = ns < 0 ? 0 : ns; }
 
  private:
   Ring() = default;
+  int64_t spin_ns_ = 200000;
   std::string name_;
   int fd_ = -1;
   uint8_t* base_ = nullptr;

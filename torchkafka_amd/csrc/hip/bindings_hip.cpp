@@ -250,12 +250,16 @@ PYBIND11_MODULE(_tkhip, m) {
              s["phase_steps"] = d.ph_steps_;
              s["events"] = d.events_;
              s["groups"] = d.groups();
+             s["log_bytes_registered"] = d.log_bytes_registered();
+             s["log_register_ns"] = d.log_register_ns();
              return s;
            })
       .def("reset_stats", &MainDriver::reset_stats)
       .def("set_event_every", &MainDriver::set_event_every, py::arg("n"))
       .def_property_readonly("event_every", &MainDriver::event_every)
       .def("set_coalesce", &MainDriver::set_coalesce, py::arg("n"))
+      .def("enable_direct", &MainDriver::enable_direct)
+      .def_property_readonly("direct", &MainDriver::direct)
       .def_property_readonly("coalesce", &MainDriver::coalesce)
       .def("enable_lockstep", &MainDriver::enable_lockstep, py::keep_alive<1, 2>())
       .def("finish_lockstep",

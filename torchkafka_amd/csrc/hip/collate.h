@@ -24,6 +24,12 @@ constexpr int kMaxGroup = 8;
 void launch_fixed_group(const void* const* srcs, int src_dt, void* const* dsts, int dst_dt, const int64_t* rows, int n,
                         int64_t row, const float* shift, const float* scale, hipStream_t stream);
 
+// Fixed-width rows gathered from pinned broker logs: ents[k][i] = (pidx << 44) | byte offset,
+// bases[pidx] = device address of partition pidx's log.  Rows of `row_bytes` at any alignment.
+void launch_gather_group(const uint64_t* const* ents, int src_dt, void* const* dsts, int dst_dt, const int64_t* rows,
+                         int n, const uint64_t* bases, int64_t row_bytes, const float* shift, const float* scale,
+                         hipStream_t stream);
+
 std::vector<std::pair<std::string, double>> api_bench(int device, int iters);
 
 }  // namespace tkh

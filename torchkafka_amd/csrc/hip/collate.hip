@@ -319,6 +319,123 @@ void launch_fixed_group_t(const void* const* srcs, void* const* dsts, const int6
     hipLaunchKernelGGL((fixed_group_kernel<S, D, false>), grid, dim3(kThreads), 0, stream, a, row, shift, scale);
 }
 
+// ---------------------------------------------------------------- log gather (h2d="direct")
+// Rows are gathered straight out of the broker's partition logs, pinned in place by the main
+// process: the worker only wrote one uint64 per row, (pidx << 44) | byte offset of the value in
+// that partition's log (consumer.h kPackGatherFixed).  Record values sit at arbitrary byte
+// offsets (RecordBatch v2 varint headers precede them), so one wave per row:
+//   * lane l loads the 16-byte-aligned chunk l of the row's span (one contiguous 1 KiB+ wave
+//     access, coalesced into full PCIe reads), lane 63 also loads the chunk after it;
+//   * the next lane's chunk comes over a lane shuffle (no second PCIe read of any byte);
+//   * the misalignment s = 4q + r is wave-uniform: dword q selects the window, v_alignbyte_b32
+//     shifts by r bytes, giving 16 aligned bytes per lane -> 16/sizeof(S) elements, converted
+//     and stored (16 B per lane for f32 -> bf16 ... 8 B).
+struct GatherGroupArgs {
+  const uint64_t* ent[kMaxGroup];  // per slot: gather table (zero-copy view of the ring slot)
+  void* dst[kMaxGroup];
+  int32_t first[kMaxGroup + 1];    // prefix sum of rows: slot k owns global rows [first[k], first[k+1])
+  int n;
+};
+
+__device__ __forceinline__ uint32_t shfl_down1(uint32_t v) {
+  // lane l receives lane l+1's value (lane 63 gets its own; it loads its successor itself)
+  const int lane = int(threadIdx.x & 63);
+  const int src = lane == 63 ? lane : lane + 1;
+  return uint32_t(__builtin_amdgcn_ds_bpermute(src << 2, int(v)));
+}
+
+template <typename S, typename D, bool AFFINE>
+__global__ __launch_bounds__(kThreads) void gather_fixed_kernel(GatherGroupArgs a, const uint64_t* __restrict__ bases,
+                                                                int64_t row_bytes, const float* __restrict__ shift,
+                                                                const float* __restrict__ scale) {
+  using C = Conv<S, D, IsIntDst<D>::value>;
+  constexpr int kPer = 16 / int(sizeof(S));  // source elements per lane per segment
+  const int lane = int(threadIdx.x & 63);
+  const int64_t row_elems = row_bytes / int64_t(sizeof(S));
+  const int64_t total = a.first[a.n];
+  const int64_t waves = int64_t(gridDim.x) * (kThreads / 64);
+  const bool vec_store = ((row_elems * int64_t(sizeof(D))) % (kPer * int64_t(sizeof(D)))) == 0;
+  for (int64_t gr = int64_t(blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6); gr < total; gr += waves) {
+    int k = 0;
+    while (k + 1 < a.n && gr >= a.first[k + 1]) ++k;
+    const int64_t r = gr - a.first[k];
+    const uint64_t e = a.ent[k][r];
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(bases[e >> 44]) + (e & ((uint64_t(1) << 44) - 1));
+    const uint32_t s = uint32_t(reinterpret_cast<uintptr_t>(src) & 15);
+    const uint4* A = reinterpret_cast<const uint4*>(src - s);
+    const uint32_t q = s >> 2, rb = s & 3;
+    D* drow = static_cast<D*>(a.dst[k]) + r * row_elems;
+    for (int64_t seg = 0; seg < row_bytes; seg += 1024) {
+      const int64_t rem = row_bytes - seg;              // row bytes left from this segment on
+      const int64_t need = int64_t(s) + rem;            // source bytes needed from A + seg on
+      const uint4* Aseg = A + seg / 16;
+      uint4 c = {0u, 0u, 0u, 0u};
+      if (int64_t(lane) * 16 < need) c = Aseg[lane];
+      uint4 nx;
+      nx.x = shfl_down1(c.x);
+      nx.y = shfl_down1(c.y);
+      nx.z = shfl_down1(c.z);
+      nx.w = shfl_down1(c.w);
+      if (lane == 63) {
+        nx = {0u, 0u, 0u, 0u};
+        if (int64_t(64) * 16 < need) nx = Aseg[64];
+      }
+      const int64_t o = int64_t(lane) * 16;             // this lane's output bytes [o, o + 16) of the segment
+      if (o >= rem) continue;
+      const uint32_t w[8] = {c.x, c.y, c.z, c.w, nx.x, nx.y, nx.z, nx.w};
+      uint32_t out4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        // q is wave-uniform: the selects resolve to one path per row
+        const uint32_t lo = q == 0 ? w[j] : q == 1 ? w[j + 1] : q == 2 ? w[j + 2] : w[j + 3];
+        const uint32_t hi = q == 0 ? w[j + 1] : q == 1 ? w[j + 2] : q == 2 ? w[j + 3] : w[j + 4];
+        out4[j] = __builtin_amdgcn_alignbyte(hi, lo, rb);
+      }
+      S sv[kPer];
+      __builtin_memcpy(sv, out4, 16);
+      const int64_t e0 = (seg + o) / int64_t(sizeof(S));  // first element of this lane in the row
+      const int nel = rem - o >= 16 ? kPer : int((rem - o) / int64_t(sizeof(S)));
+      Vec<D, kPer> ov;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        if constexpr (AFFINE)
+          ov.v[j] = C::apply(sv[j], j < nel ? shift[e0 + j] : 0.f, j < nel ? scale[e0 + j] : 1.f, true);
+        else
+          ov.v[j] = C::apply(sv[j], 0.f, 1.f, false);
+      }
+      if (nel == kPer && vec_store) {
+        *reinterpret_cast<Vec<D, kPer>*>(drow + e0) = ov;
+      } else {
+        for (int j = 0; j < nel; ++j) drow[e0 + j] = ov.v[j];
+      }
+    }
+  }
+}
+
+template <typename S, typename D>
+void launch_gather_group_t(const uint64_t* const* ents, void* const* dsts, const int64_t* rows, int n,
+                           const uint64_t* bases, int64_t row_bytes, const float* shift, const float* scale,
+                           hipStream_t stream) {
+  GatherGroupArgs a{};
+  a.n = n;
+  a.first[0] = 0;
+  for (int k = 0; k < n; ++k) {
+    a.ent[k] = ents[k];
+    a.dst[k] = dsts[k];
+    a.first[k + 1] = a.first[k] + int32_t(rows[k]);
+  }
+  const int64_t total = a.first[n];
+  if (total == 0) return;
+  constexpr int kWavesPerBlock = kThreads / 64;
+  const int grid = int(std::min<int64_t>((total + kWavesPerBlock - 1) / kWavesPerBlock, 4096));
+  if (shift)
+    hipLaunchKernelGGL((gather_fixed_kernel<S, D, true>), dim3(grid), dim3(kThreads), 0, stream, a, bases, row_bytes,
+                       shift, scale);
+  else
+    hipLaunchKernelGGL((gather_fixed_kernel<S, D, false>), dim3(grid), dim3(kThreads), 0, stream, a, bases,
+                       row_bytes, shift, scale);
+}
+
 // Direct variant for 4- and 8-byte sources (f32 JSON values, i32/i64 token ids): a row's
 // elements are dword-aligned wherever the row starts, and gfx950 serves dword-aligned
 // global_load_dwordx4 at full width, so each lane loads its 8 elements straight from
@@ -447,6 +564,21 @@ void launch_fixed_group(const void* const* srcs, int src_dt, void* const* dsts, 
   TK_DISPATCH_SRC(launch_fixed_group_t, srcs, dsts, rows, n, row, shift, scale, stream)
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("fixed group collate launch: ") + hipGetErrorString(e));
+}
+
+void launch_gather_group(const uint64_t* const* ents, int src_dt, void* const* dsts, int dst_dt, const int64_t* rows,
+                         int n, const uint64_t* bases, int64_t row_bytes, const float* shift, const float* scale,
+                         hipStream_t stream) {
+  if (n < 1 || n > kMaxGroup) throw std::invalid_argument("collate: group size out of range");
+  if (!is_float_dt(dst_dt) && is_float_dt(src_dt))
+    throw std::invalid_argument("collate: float records cannot be cast to an integer dtype");
+  if (shift && !is_float_dt(dst_dt)) throw std::invalid_argument("collate: normalisation needs a float dtype");
+  int64_t total = 0;
+  for (int k = 0; k < n; ++k) total += rows[k];
+  if (total > INT32_MAX) throw std::invalid_argument("gather collate: too many rows");
+  TK_DISPATCH_SRC(launch_gather_group_t, ents, dsts, rows, n, bases, row_bytes, shift, scale, stream)
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("gather collate launch: ") + hipGetErrorString(e));
 }
 
 __global__ void empty_kernel() {}

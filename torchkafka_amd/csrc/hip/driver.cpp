@@ -46,6 +46,10 @@ MainDriver::MainDriver(Engine* engine, const std::string& ring_name, const std::
 }
 
 MainDriver::~MainDriver() {
+  // pinned log ranges first: the kernels that read them completed (slots drained by the caller)
+  if (!reg_ptrs_.empty()) hipDeviceSynchronize();
+  for (void* p : reg_ptrs_) hipHostUnregister(p);
+  if (bases_dev_) hipFree(bases_dev_);
   if (registered_) {
     try {
       eng_->unregister_host();  // before ring_'s mapping goes away
@@ -140,6 +144,7 @@ int MainDriver::poll_one(bool block, int64_t timeout_ms) {
     v.worker = h->worker;
     v.payload_bytes = h->payload_bytes;
     v.values_offset = h->values_offset;
+    v.row_bytes = h->row_bytes;
     v.max_row_len = h->max_row_len;
     v.total_elems = h->total_elems;
     v.n_scanned = h->n_scanned;
@@ -156,6 +161,14 @@ int MainDriver::poll_one(bool block, int64_t timeout_ms) {
       }
       if (!block) return 0;
       continue;
+    }
+    if (v.kind == uint32_t(tk::kPackGatherFixed)) {
+      if (!direct_) {
+        error_ = "DeviceLoader: a worker produced a log-gather slot but direct mode is off";
+        return -3;
+      }
+      // pin every log range this slot's rows live in before any kernel may read them
+      for (uint32_t k = 0; k < h->n_parts; ++k) ensure_log(h->wm[k].pidx, h->log_end[k]);
     }
     eng_->h2d(int(g), ring_->payload(uint32_t(g)), v.payload_bytes);
     staged_.push_back(std::move(v));
@@ -345,10 +358,74 @@ int MainDriver::next_slot(int64_t timeout_ms, SlotView* out) {
   }
 }
 
+void MainDriver::enable_direct() {
+  if (!broker_) throw std::runtime_error("DeviceLoader h2d='direct' needs the synthetic broker (group_id + URL)");
+  if (direct_) return;
+  const uint32_t np = broker_->meta().max_partitions;
+  reg_end_.assign(np, 0);
+  if (hipMalloc(reinterpret_cast<void**>(&bases_dev_), size_t(np) * sizeof(uint64_t)) != hipSuccess)
+    throw std::runtime_error("driver: hipMalloc(log base table) failed");
+  if (hipMemset(bases_dev_, 0, size_t(np) * sizeof(uint64_t)) != hipSuccess)
+    throw std::runtime_error("driver: hipMemset failed");
+  direct_ = true;
+}
+
+void MainDriver::ensure_log(uint32_t pidx, uint64_t end) {
+  if (pidx >= reg_end_.size()) throw std::out_of_range("driver: partition index beyond the broker's table");
+  if (end <= reg_end_[pidx]) return;
+  const int64_t t0 = tk::now_ns();
+  const uint8_t* base = broker_->log_base(pidx);
+  const uint64_t cap = broker_->part(pidx).log_capacity;
+  if (end > cap) throw std::runtime_error("driver: slot references bytes beyond the partition log");
+  // Everything already written (a retained backlog is pinned once, at its first use), then whole
+  // chunks, so a growing log pays one registration per 64 MiB.  Pinning costs ~13 GB/s of fresh
+  // shm pages on the MI355X host (profiles/*/register_probe2.log): it is what bounds this mode
+  // on a log that grows faster than that.
+  const uint64_t written = broker_->part(pidx).log_end_pos.load(std::memory_order_acquire);
+  uint64_t hi = (std::max(end, written) + kLogChunk - 1) / kLogChunk * kLogChunk;
+  if (hi > cap) hi = cap;
+  const uint64_t lo = reg_end_[pidx];
+  void* p = const_cast<uint8_t*>(base) + lo;
+  if (hipHostRegister(p, hi - lo, hipHostRegisterMapped) != hipSuccess)
+    throw std::runtime_error("driver: hipHostRegister of a partition log failed");
+  reg_ptrs_.push_back(p);
+  void* dp = nullptr;
+  if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess || dp != p)
+    throw std::runtime_error("driver: h2d='direct' needs device addresses of pinned host memory to equal host "
+                             "addresses (unified addressing)");
+  if (lo == 0) {
+    const uint64_t b = reinterpret_cast<uint64_t>(base);
+    if (hipMemcpy(bases_dev_ + pidx, &b, sizeof(b), hipMemcpyHostToDevice) != hipSuccess)
+      throw std::runtime_error("driver: log base table update failed");
+  }
+  reg_end_[pidx] = hi;
+  reg_total_ += hi - lo;
+  reg_ns_ += tk::now_ns() - t0;
+  DTRACE("pinned log of partition %u: [%lu, %lu)", pidx, (unsigned long)lo, (unsigned long)hi);
+}
+
+void MainDriver::launch_group(const int* slots, const int64_t* rows, const size_t* voffs, int n, const SlotView& v,
+                              hipStream_t stream, int dst_dt, void* const* dsts, int64_t row, const float* shift,
+                              const float* scale) {
+  if (v.kind == uint32_t(tk::kPackGatherFixed))
+    eng_->collate_gather_group(slots, n, stream, v.src_dtype, dsts, dst_dt, rows, int64_t(v.row_bytes), bases_dev_,
+                               shift, scale);
+  else
+    eng_->collate_fixed_group(slots, n, stream, voffs, v.src_dtype, dsts, dst_dt, rows, row, shift, scale);
+}
+
 void MainDriver::collate_fixed(const SlotView& v, hipStream_t stream, int dst_dt, void* dst, int64_t row,
                                const float* shift, const float* scale) {
   bool record;
   note_handed(v.g, stream, &record);
+  if (v.kind == uint32_t(tk::kPackGatherFixed)) {
+    const int slot = int(v.g);
+    const int64_t rows = v.n_rows;
+    void* d = dst;
+    eng_->collate_gather_group(&slot, 1, stream, v.src_dtype, &d, dst_dt, &rows, int64_t(v.row_bytes), bases_dev_,
+                               shift, scale, record);
+    return;
+  }
   eng_->collate_fixed(int(v.g), stream, v.values_offset, v.src_dtype, dst, dst_dt, v.n_rows, row, shift, scale,
                       record);
 }
@@ -491,12 +568,12 @@ int64_t MainDriver::step_group_begin(hipStream_t stream, bool auto_commit, int64
     return last.n_rows;
   }
   group_rows->push_back(last.n_rows);
-  if (last.kind == uint32_t(tk::kPackFixed)) {
+  if (last.kind == uint32_t(tk::kPackFixed) || last.kind == uint32_t(tk::kPackGatherFixed)) {
     for (size_t i = 0; i < staged_.size() && int(group_rows->size()) < coalesce_; ++i) {
       const SlotView& v = staged_[i];
       if (v.g < 0) continue;  // watermark-only slot: rides on the next delivered batch
       if (v.pre || v.kind != last.kind || v.src_dtype != last.src_dtype || v.max_row_len != last.max_row_len ||
-          v.shape != last.shape || v.n_rows == 0)
+          v.row_bytes != last.row_bytes || v.shape != last.shape || v.n_rows == 0)
         break;
       group_idx_.push_back(i);
       group_rows->push_back(v.n_rows);
@@ -530,7 +607,7 @@ void MainDriver::step_group_launch(hipStream_t stream, int dst_dt, void* const* 
       cover_handed();
       last_stream_ = stream;
     }
-    eng_->collate_fixed_group(slots, n, stream, voffs, last.src_dtype, dsts, dst_dt, rows, row, shift, scale);
+    launch_group(slots, rows, voffs, n, last, stream, dst_dt, dsts, row, shift, scale);
     // one completion event (after the group kernel, on the last slot) releases every slot of the group
     for (int k = 0; k < n; ++k) handed_.push_back(Handed{slots[k], k == n - 1});
     unevented_ = 0;
@@ -567,6 +644,8 @@ void MainDriver::reset_stats() {
   commits_ = commit_failures_ = 0;
   fill_ns_ = fills_ = blocked_ns_ = blocked_calls_ = ready_age_ns_ = 0;
   ph_commit_ns_ = ph_next_ns_ = ph_launch_ns_ = ph_steps_ = events_ = groups_ = 0;
+  reg_ns_ = 0;
+  reg_total_ = 0;
   commit_ns_.clear();
 }
 

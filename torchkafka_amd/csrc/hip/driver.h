@@ -28,6 +28,7 @@ struct SlotView {
   int64_t g = -1;
   uint32_t n_rows = 0, flags = 0, kind = 0, worker = 0;
   uint64_t payload_bytes = 0, values_offset = 0;
+  uint32_t row_bytes = 0;
   int64_t max_row_len = 0, total_elems = 0, n_scanned = 0;
   int32_t src_dtype = -1;
   std::vector<int64_t> shape;
@@ -86,6 +87,15 @@ class MainDriver {
   void step_group_launch(hipStream_t stream, int dst_dt, void* const* dsts, int64_t row, const float* shift,
                          const float* scale, std::vector<std::shared_ptr<void>>&& handles);
   void set_coalesce(int n) { coalesce_ = n < 1 ? 1 : (n > kMaxGroup ? kMaxGroup : n); }
+
+  // h2d="direct": the workers' slots hold log locations (kPackGatherFixed); the driver pins each
+  // partition log in place (hipHostRegister, kLogChunk at a time, just ahead of what a slot
+  // references) and keeps a device table of their addresses for the gather kernel.
+  static constexpr uint64_t kLogChunk = uint64_t(64) << 20;
+  void enable_direct();
+  bool direct() const { return direct_; }
+  uint64_t log_bytes_registered() const { return reg_total_; }
+  int64_t log_register_ns() const { return reg_ns_; }
   int coalesce() const { return coalesce_; }
   int64_t groups() const { return groups_; }
 
@@ -179,6 +189,16 @@ class MainDriver {
   std::vector<int64_t> commit_ns_;
   int coalesce_ = 1;
   int64_t groups_ = 0;
+  void ensure_log(uint32_t pidx, uint64_t end);
+  void launch_group(const int* slots, const int64_t* rows, const size_t* voffs, int n, const SlotView& v,
+                    hipStream_t stream, int dst_dt, void* const* dsts, int64_t row, const float* shift,
+                    const float* scale);
+  bool direct_ = false;
+  uint64_t* bases_dev_ = nullptr;
+  std::vector<uint64_t> reg_end_;        // per pidx: bytes of its log pinned (and device-mapped)
+  std::vector<void*> reg_ptrs_;          // registered ranges, unregistered at teardown
+  uint64_t reg_total_ = 0;
+  int64_t reg_ns_ = 0;
   std::vector<size_t> group_idx_;  // staged_ indices of the batches behind `last` in the pending group
 };
 

@@ -50,6 +50,11 @@ class Engine {
   void collate_fixed_group(const int* slots, int n, hipStream_t user, const size_t* values_offsets, int src_dt,
                            void* const* dsts, int dst_dt, const int64_t* rows, int64_t row, const float* shift,
                            const float* scale);
+  // Log-gather slots (h2d="direct"): each slot's payload is its gather table; rows are read from
+  // the pinned broker logs through `bases` (device table, one address per partition index).
+  void collate_gather_group(const int* slots, int n, hipStream_t user, int src_dt, void* const* dsts, int dst_dt,
+                            const int64_t* rows, int64_t row_bytes, const uint64_t* bases, const float* shift,
+                            const float* scale, bool record = true);
   // `user` waits for slot s's completion event (a batch collated on another stream).
   void stream_wait_done(int s, hipStream_t user);
   void record_done(int s, hipStream_t user) { finish(s, user); }

@@ -155,6 +155,20 @@ void Engine::collate_fixed_group(const int* slots, int n, hipStream_t user, cons
   finish(slots[n - 1], user);
 }
 
+void Engine::collate_gather_group(const int* slots, int n, hipStream_t user, int src_dt, void* const* dsts, int dst_dt,
+                                  const int64_t* rows, int64_t row_bytes, const uint64_t* bases, const float* shift,
+                                  const float* scale, bool record) {
+  if (n < 1 || n > kMaxGroup) throw std::invalid_argument("engine: bad group size");
+  const uint64_t* ents[kMaxGroup];
+  for (int k = 0; k < n; ++k) {
+    check_slot(slots[k]);
+    begin(slots[k], user);
+    ents[k] = reinterpret_cast<const uint64_t*>(src_base(slots[k]));
+  }
+  launch_gather_group(ents, src_dt, dsts, dst_dt, rows, n, bases, row_bytes, shift, scale, user);
+  if (record) finish(slots[n - 1], user);
+}
+
 void Engine::stream_wait_done(int s, hipStream_t user) {
   check_slot(s);
   TKH_CHECK(hipStreamWaitEvent(user, done_[size_t(s)], 0));

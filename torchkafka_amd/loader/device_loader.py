@@ -118,7 +118,7 @@ class _Run:
             if L.device.type == "cuda":
                 # only after the fork: workers never inherit an initialised HIP runtime state they would use
                 dev = L.device.index if L.device.index is not None else torch.cuda.current_device()
-                mode = hip().H2D_ZERO_COPY if L._resolve_h2d(self.ring.payload_capacity) == "zerocopy" \
+                mode = hip().H2D_ZERO_COPY if L._resolve_h2d(self.ring.payload_capacity) in ("zerocopy", "direct") \
                     else hip().H2D_DMA
                 self.engine = hip().Engine(dev, self.ring.n_slots, self.ring.payload_capacity, L.copy_streams, mode)
                 if L.numa_bind:
@@ -129,6 +129,8 @@ class _Run:
                 self.driver.set_commit_on_device(L.commit_on == "device")
                 self.driver.set_event_every(L._event_every(self.ring.n_slots))
                 self.driver.set_coalesce(L.coalesce)
+                if L._direct():
+                    self.driver.enable_direct()
         except BaseException:
             self.close()
             raise
@@ -255,7 +257,12 @@ class DeviceLoader:
             ``prefetch`` batches ahead), ``"zerocopy"`` (the collate kernel reads pinned host memory over
             PCIe: two HIP calls per batch instead of five, but the read runs on the compute stream) or
             ``"auto"`` (default: zero-copy for slots up to ``ZERO_COPY_MAX_BYTES``, where a batch is
-            latency-bound; DMA above, where copy/compute overlap matters).
+            latency-bound; DMA above, where copy/compute overlap matters) or ``"direct"`` (experimental;
+            fixed-width schemas on the synthetic broker: workers only locate each row in the broker log,
+            the main process pins the logs in place and the collate kernel gathers rows straight out of
+            them over PCIe, so no worker copies the payload.  Measured slower than "zerocopy" on MI355X
+            (docs/PERFORMANCE.md): the CPU CRC pass still dominates a worker, the gather kernel pays a
+            second dependent PCIe round trip, and pinning new log pages runs at ~13 GB/s).
         event_every: record a slot-completion event for one batch in k (default: ring slots / 4,
             at most 4); slots in between are released with the next event on the same stream.
         coalesce: fixed-width batches that are already staged when the next one is requested are
@@ -312,8 +319,8 @@ class DeviceLoader:
         self.commit_on = commit_on
         self.lockstep = lockstep
         self.lockstep_depth = max(0, int(lockstep_depth))
-        if h2d not in ("auto", "dma", "zerocopy"):
-            raise ValueError("h2d must be 'auto', 'dma' (hipMemcpyAsync on side streams) or 'zerocopy'")
+        if h2d not in ("auto", "dma", "zerocopy", "direct"):
+            raise ValueError("h2d must be 'auto', 'dma' (hipMemcpyAsync on side streams), 'zerocopy' or 'direct'")
         self.h2d = h2d
         self.copy_streams = max(1, int(copy_streams))
         self.event_every = None if event_every is None else max(1, int(event_every))
@@ -390,7 +397,20 @@ class DeviceLoader:
 
     def _worker_cfg(self) -> dict:
         return {"batch_size": self.batch_size, "sharding": self.sharding, "rank": self.rank,
-                "world_size": self.world_size, "native": self.native, "base_seed": self.base_seed}
+                "world_size": self.world_size, "native": self.native, "base_seed": self.base_seed,
+                "gather": self._direct()}
+
+    def _direct(self) -> bool:
+        """h2d='direct': fixed-width rows gathered by the kernel straight from the pinned broker logs."""
+        if self.h2d != "direct":
+            return False
+        if self.device.type != "cuda" or not self._fast_path_ok():
+            raise ValueError("h2d='direct' needs a CUDA device, a FixedWidth schema, native=True, "
+                             "return_info=False and drop_last=False")
+        if self._commit_target_url()[0] == "":
+            raise ValueError("h2d='direct' needs the synthetic broker (bootstrap_servers shm:// or file://) "
+                             "and a group_id")
+        return True
 
     def _out_dtype(self, src: torch.dtype) -> torch.dtype:
         if self.dtype is not None:
@@ -604,6 +624,8 @@ class DeviceLoader:
         self.stats.phase_steps += st["phase_steps"]
         self.stats.events += st["events"]
         self.stats.groups += st.get("groups", 0)
+        self.stats.log_bytes_registered = st.get("log_bytes_registered", 0)
+        self.stats.log_register_ns = st.get("log_register_ns", 0)
         self.stats.commits += st["commits"]
         self.stats.commit_failures += st["commit_failures"]
         self.stats.commit_ns.extend(st["commit_ns"])

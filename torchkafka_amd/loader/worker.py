@@ -44,6 +44,8 @@ def worker_main(ring, ring_name: str, worker_id: int, num_workers: int, dataset,
     if ring is None:
         ring = core().Ring.open(ring_name)
     ring.set_worker_pid(worker_id, os.getpid())
+    # spin (µs) on a full sub-ring before sleeping: keeps futex wakes off the main thread's path
+    ring.set_worker_spin_ns(int(os.environ.get("TORCHKAFKA_WORKER_SPIN_US", "200")) * 1000)
     spw = ring.slots_per_worker
     state = {"i": 0, "g": None}
     try:
@@ -113,6 +115,7 @@ def _native_loop(ring, worker_id, spw, consumer, schema, cfg, state) -> None:
     bs = int(cfg["batch_size"])
     timeout = _consumer_timeout_ms(consumer)
     fetcher = consumer._fetcher
+    gather = bool(cfg.get("gather")) and kind == core().PACK_FIXED
     if not fetcher.assigned() and cfg["sharding"] == "static":
         g = _acquire(ring, worker_id, state)  # nothing to read, ever: end of stream right away
         ring.set_slot(g, 0, core().SLOT_EOS, kind, 0, 0, 0, 0, 0, [])
@@ -124,7 +127,8 @@ def _native_loop(ring, worker_id, spw, consumer, schema, cfg, state) -> None:
         while True:
             try:
                 rows, _scanned, timed_out, shut = fetcher.fill_slot(ring, g, kind, elem, row_elems, min_len,
-                                                                    max_len, trunc, skip_bad, bs, timeout)
+                                                                    max_len, trunc, skip_bad, bs, timeout,
+                                                                    gather)
                 break
             except OffsetOutOfRangeError:
                 # retention moved past a position: reset it like the consumer would and refill this slot

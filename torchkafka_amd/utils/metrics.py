@@ -39,6 +39,8 @@ class LoaderStats:
     phase_steps: int = 0
     events: int = 0            # completion events recorded (batched: fewer than batches)
     groups: int = 0            # coalesced launches (several batches collated by one kernel)
+    log_bytes_registered: int = 0  # h2d="direct": broker log bytes pinned in place so far
+    log_register_ns: int = 0
     started: float = field(default_factory=time.perf_counter)
     max_commit_samples: int = 100000
 
@@ -75,6 +77,8 @@ class LoaderStats:
             "native_launch_us_per_step": self.phase_launch_ns / 1e3 / max(self.phase_steps, 1),
             "events_per_batch": self.events / max(self.batches, 1),
             "group_launches_per_batch": self.groups / max(self.batches, 1),
+            "log_mib_pinned": self.log_bytes_registered / 2**20,
+            "log_pin_ms": self.log_register_ns / 1e6,
             "commits": self.commits,
             "commit_failures": self.commit_failures,
             "commit_p50_us": percentile(c_us, 50),
