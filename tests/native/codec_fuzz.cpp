@@ -1,0 +1,106 @@
+// Host-sanitizer fuzz test of the RecordBatch v2 codec, CRC32C and the JSON parser
+// (built with -fsanitize=address,undefined by tools/sanitize.sh).  Every decode of a randomly
+// corrupted batch must either throw CorruptRecord or stay inside the buffer; ASan turns an
+// out-of-bounds read into a failure.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "consumer.h"
+#include "crc32c.h"
+#include "record_batch.h"
+
+using namespace tk;
+
+#define CHECK(c)                                                                  \
+  do {                                                                            \
+    if (!(c)) {                                                                   \
+      std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #c);   \
+      std::abort();                                                               \
+    }                                                                             \
+  } while (0)
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? std::atoi(argv[1]) : 3000;
+  std::mt19937_64 rng(12345);
+  uint64_t decoded = 0, rejected = 0;
+  for (int it = 0; it < iters; ++it) {
+    const int n = 1 + int(rng() % 20);
+    std::vector<std::vector<uint8_t>> keys(n), vals(n), hk(n), hv(n);
+    std::vector<HeaderView> hdrs(n);
+    std::vector<RecordIn> recs(n);
+    for (int i = 0; i < n; ++i) {
+      keys[i].resize(rng() % 9);
+      vals[i].resize(rng() % 300);
+      for (auto& c : vals[i]) c = uint8_t(rng());
+      hk[i].assign(rng() % 5, 'h');
+      hv[i].assign(rng() % 5, 'v');
+      hdrs[i] = HeaderView{hk[i].data(), int32_t(hk[i].size()), hv[i].data(), int32_t(hv[i].size())};
+      const bool null_key = rng() % 3 == 0, null_val = rng() % 5 == 0;
+      recs[i] = RecordIn{int64_t(1000 + i), null_key ? nullptr : keys[i].data(), null_key ? -1 : int32_t(keys[i].size()),
+                         null_val ? nullptr : vals[i].data(), null_val ? -1 : int32_t(vals[i].size()),
+                         rng() % 2 ? &hdrs[i] : nullptr, 0};
+      recs[i].header_count = recs[i].headers ? 1 : 0;
+    }
+    const size_t sz = batch_encoded_size(recs.data(), n, 1000);
+    std::vector<uint8_t> buf(sz);
+    CHECK(encode_batch(buf.data(), int64_t(it) * 100, recs.data(), n) == sz);
+    // clean decode round trip
+    BatchHeader h = parse_batch_header(buf.data(), buf.size());
+    CHECK(verify_batch_crc(buf.data(), h));
+    RecordIter ri(buf.data(), h);
+    RecordView rv;
+    int k = 0;
+    while (ri.next(&rv)) {
+      CHECK(rv.value_len == recs[k].value_len);
+      if (rv.value_len > 0) CHECK(std::memcmp(rv.value, recs[k].value, size_t(rv.value_len)) == 0);
+      ++k;
+    }
+    CHECK(k == n);
+    // corrupt 1-4 bytes (header or body) and decode from an exact-size heap copy
+    std::vector<uint8_t> bad(buf);
+    const int flips = 1 + int(rng() % 4);
+    for (int f = 0; f < flips; ++f) bad[rng() % bad.size()] ^= uint8_t(1 + rng() % 255);
+    uint8_t* p = static_cast<uint8_t*>(std::malloc(bad.size()));
+    std::memcpy(p, bad.data(), bad.size());
+    try {
+      BatchHeader hb = parse_batch_header(p, bad.size());
+      if (hb.total_size() <= bad.size()) {
+        (void)verify_batch_crc(p, hb);
+        RecordIter rb(p, hb);
+        RecordView r2;
+        while (rb.next(&r2)) {
+          if (r2.value_len > 0) CHECK(r2.value >= p && r2.value + r2.value_len <= p + bad.size());
+          if (r2.header_count > 0) (void)parse_headers(r2);
+        }
+      }
+      ++decoded;
+    } catch (const CorruptRecord&) {
+      ++rejected;
+    } catch (const std::exception&) {
+      ++rejected;
+    }
+    std::free(p);
+    // CRC32C: extend() over splits equals one pass
+    const size_t cut = bad.size() ? rng() % bad.size() : 0;
+    CHECK(crc32c_extend(crc32c(bad.data(), cut), bad.data() + cut, bad.size() - cut) == crc32c(bad.data(), bad.size()));
+  }
+  // JSON parser on random printable strings and on mutated arrays
+  std::vector<float> out(512);
+  const char alphabet[] = "[],.-+eE0123456789 NaInfity";
+  for (int it = 0; it < iters * 4; ++it) {
+    const size_t len = rng() % 64;
+    char* s = static_cast<char*>(std::malloc(len ? len : 1));
+    for (size_t i = 0; i < len; ++i) s[i] = alphabet[rng() % (sizeof(alphabet) - 1)];
+    const int64_t got = parse_json_f32(s, len, out.data(), int64_t(out.size()));
+    CHECK(got >= -2 && got <= int64_t(out.size()));
+    const int64_t n2 = json_array_len(s, len);
+    CHECK(n2 >= -1);
+    std::free(s);
+  }
+  std::printf("codec fuzz: %d batches, %llu corrupted decodes survived, %llu rejected; JSON fuzz ok\n", iters,
+              (unsigned long long)decoded, (unsigned long long)rejected);
+  return 0;
+}

@@ -1,0 +1,25 @@
+#!/bin/bash
+# Host sanitizer runs of the native core: ThreadSanitizer over the ring protocol,
+# the futex hand-offs and the broker/fetcher/packer pipeline; AddressSanitizer + UBSan over the
+# same stress test and a codec/CRC/JSON fuzz test.  Host code only -- GPU sanitizers are not
+# available on this pool.  Usage: tools/sanitize.sh [outdir]
+set -euo pipefail
+cd "$(dirname "$0")/.."
+OUT=${1:-build/sanitize}
+mkdir -p "$OUT"
+CORE=torchkafka_amd/csrc/core
+SRCS="$CORE/ring.cpp $CORE/broker.cpp $CORE/consumer.cpp $CORE/record_batch.cpp $CORE/crc32c.cpp"
+CXX=${CXX:-g++}
+COMMON="-std=c++17 -O1 -g -fno-omit-frame-pointer -I$CORE -pthread"
+$CXX $COMMON -fsanitize=thread tests/native/ring_stress.cpp $SRCS -o "$OUT/ring_stress_tsan" -lrt
+$CXX $COMMON -fsanitize=address,undefined -fno-sanitize-recover=undefined tests/native/ring_stress.cpp $SRCS \
+    -o "$OUT/ring_stress_asan" -lrt
+$CXX $COMMON -fsanitize=address,undefined -fno-sanitize-recover=undefined tests/native/codec_fuzz.cpp $SRCS \
+    -o "$OUT/codec_fuzz_asan" -lrt
+export TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1"
+export ASAN_OPTIONS="halt_on_error=1 detect_leaks=1"
+export UBSAN_OPTIONS="halt_on_error=1 print_stacktrace=1"
+echo "== tsan ring_stress"; "$OUT/ring_stress_tsan" 4 3 ${TK_SAN_BATCHES:-2000}
+echo "== asan ring_stress"; "$OUT/ring_stress_asan" 4 3 ${TK_SAN_BATCHES:-2000}
+echo "== asan codec_fuzz"; "$OUT/codec_fuzz_asan" ${TK_SAN_FUZZ:-3000}
+echo "sanitizers: all clean"

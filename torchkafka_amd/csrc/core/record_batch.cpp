@@ -161,7 +161,7 @@ size_t encode_batch(uint8_t* out, int64_t base_offset, const RecordIn* recs, siz
     for (int32_t h = 0; h < r.header_count; ++h) {
       const HeaderView& hv = r.headers[h];
       p = put_varint(p, hv.key_len);
-      std::memcpy(p, hv.key, size_t(hv.key_len));
+      if (hv.key_len > 0) std::memcpy(p, hv.key, size_t(hv.key_len));  // empty key: pointer may be null
       p += hv.key_len;
       p = put_varint(p, hv.value_len);
       if (hv.value_len > 0) { std::memcpy(p, hv.value, size_t(hv.value_len)); p += hv.value_len; }
