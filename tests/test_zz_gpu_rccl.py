@@ -42,3 +42,25 @@ def test_native_rccl_lockstep_driver_world1(broker):
             assert broker.committed_offsets(f"g{depth}", "t") == {0: 95, 1: 95}
     finally:
         dist.destroy_process_group()
+
+
+def test_rccl_lockstep_transport_failure_detection_plumbing():
+    """The native transport's bounded wait (failure detection) at world size 1: results come back,
+    the timeout is settable and nothing is aborted.  (A dead peer cannot be staged on a 1-GPU box;
+    the timeout/abort path is exercised by multi-GPU runs.)"""
+    import os
+
+    import torch
+
+    from torchkafka_amd.ops.native import hip
+
+    lib = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    uid = hip().RcclLockstep.unique_id(lib)
+    ls = hip().RcclLockstep(lib, uid, 0, 1, 0, 3)
+    assert ls.timeout_ms == 600000
+    ls.set_timeout_ms(2000)
+    assert ls.timeout_ms == 2000
+    for i in range(10):
+        assert ls.allreduce_min(i, -i, 7) == (i, -i, 7)
+    assert not ls.aborted
+    del ls

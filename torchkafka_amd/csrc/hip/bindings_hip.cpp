@@ -156,7 +156,10 @@ PYBIND11_MODULE(_tkhip, m) {
              }
              return py::make_tuple(r[0], r[1], r[2]);
            })
-      .def_property_readonly("issued", &RcclLockstep::issued);
+      .def_property_readonly("issued", &RcclLockstep::issued)
+      .def("set_timeout_ms", &RcclLockstep::set_timeout_ms, py::arg("ms"))
+      .def_property_readonly("timeout_ms", &RcclLockstep::timeout_ms)
+      .def_property_readonly("aborted", &RcclLockstep::aborted);
 
   py::class_<MainDriver>(m, "MainDriver")
       .def(py::init([](Engine* e, const std::string& ring, const std::string& url, const std::string& group,

@@ -3,8 +3,10 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
 
 namespace tkh {
 
@@ -14,6 +16,8 @@ struct RcclApi {
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;                         // optional
+  ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;  // optional
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
 };
 
@@ -43,6 +47,8 @@ RcclApi* load_api(const std::string& path) {
   api->AllReduce = reinterpret_cast<decltype(api->AllReduce)>(sym("ncclAllReduce"));
   api->CommDestroy = reinterpret_cast<decltype(api->CommDestroy)>(sym("ncclCommDestroy"));
   api->GetErrorString = reinterpret_cast<decltype(api->GetErrorString)>(sym("ncclGetErrorString"));
+  api->CommAbort = reinterpret_cast<decltype(api->CommAbort)>(dlsym(lib, "ncclCommAbort"));
+  api->CommGetAsyncError = reinterpret_cast<decltype(api->CommGetAsyncError)>(dlsym(lib, "ncclCommGetAsyncError"));
   return api;
 }
 
@@ -81,8 +87,8 @@ RcclLockstep::RcclLockstep(const std::string& lib_path, const std::string& id, i
 
 RcclLockstep::~RcclLockstep() {
   hipSetDevice(device_);
-  if (stream_) hipStreamSynchronize(stream_);
-  if (comm_) api_->CommDestroy(static_cast<ncclComm_t>(comm_));
+  if (!aborted_ && stream_) hipStreamSynchronize(stream_);
+  if (comm_) api_->CommDestroy(static_cast<ncclComm_t>(comm_));  // null once aborted
   for (auto e : ev_) hipEventDestroy(e);
   if (d_) hipFree(d_);
   if (h_in_) hipHostFree(h_in_);
@@ -91,10 +97,44 @@ RcclLockstep::~RcclLockstep() {
   delete api_;
 }
 
+void RcclLockstep::wait_event(int t, const char* what) {
+  hipEvent_t ev = ev_.at(size_t(t));
+  hipError_t e = hipEventQuery(ev);
+  if (e == hipSuccess) return;
+  if (aborted_) throw std::runtime_error("lockstep: the RCCL communicator was aborted after a failure");
+  // spin briefly (the round trip is normally done), then poll with short sleeps, checking
+  // RCCL's asynchronous error state and the deadline
+  const auto t0 = std::chrono::steady_clock::now();
+  int spins = 0;
+  for (;;) {
+    e = hipEventQuery(ev);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+    if (++spins < 2000) continue;
+    const auto el = std::chrono::steady_clock::now() - t0;
+    const int64_t ms = std::chrono::duration_cast<std::chrono::milliseconds>(el).count();
+    ncclResult_t async = ncclSuccess;
+    if (api_->CommGetAsyncError) api_->CommGetAsyncError(static_cast<ncclComm_t>(comm_), &async);
+    const bool failed = async != ncclSuccess && async != ncclInProgress;
+    if (failed || (timeout_ms_ > 0 && ms > timeout_ms_)) {
+      aborted_ = true;
+      if (api_->CommAbort) api_->CommAbort(static_cast<ncclComm_t>(comm_));
+      comm_ = nullptr;
+      throw std::runtime_error(
+          failed ? std::string("lockstep: RCCL reported an asynchronous error (") + api_->GetErrorString(async) +
+                       "): a peer rank failed"
+                 : "lockstep: no answer from the other ranks within " + std::to_string(timeout_ms_) +
+                       " ms (a peer rank died or hung); RCCL communicator aborted");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
 int RcclLockstep::issue(int64_t a, int64_t b, int64_t c) {
   const int s = int(issued_ % uint64_t(slots_));
+  if (aborted_) throw std::runtime_error("lockstep: the RCCL communicator was aborted after a failure");
   // the slot's previous round trip must be complete before its buffers are reused
-  TKH_HIP(hipEventSynchronize(ev_[size_t(s)]));
+  wait_event(s, "lockstep slot reuse");
   int64_t* hin = h_in_ + 3 * s;
   int64_t* hout = h_out_ + 3 * s;
   int64_t* din = d_ + 6 * s;
@@ -114,7 +154,7 @@ int RcclLockstep::issue(int64_t a, int64_t b, int64_t c) {
 bool RcclLockstep::ready(int t) { return hipEventQuery(ev_.at(size_t(t))) == hipSuccess; }
 
 void RcclLockstep::wait(int t, int64_t out[3]) {
-  TKH_HIP(hipEventSynchronize(ev_.at(size_t(t))));
+  wait_event(t, "lockstep wait");
   const int64_t* hout = h_out_ + 3 * t;
   out[0] = hout[0];
   out[1] = hout[1];

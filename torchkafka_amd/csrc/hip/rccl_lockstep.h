@@ -45,6 +45,11 @@ class RcclLockstep : public LockstepTransport {
   // Waits for a ticket's result.
   void wait(int ticket, int64_t out[3]) override;
   bool ready(int ticket);
+  // Failure detection: a round trip not complete after `ms` (a peer rank died or hung) aborts
+  // the communicator and raises instead of blocking forever; <= 0 waits indefinitely.
+  void set_timeout_ms(int64_t ms) { timeout_ms_ = ms; }
+  int64_t timeout_ms() const { return timeout_ms_; }
+  bool aborted() const { return aborted_; }
   int world() const { return world_; }
   int rank() const { return rank_; }
   uint64_t issued() const { return issued_; }
@@ -59,6 +64,9 @@ class RcclLockstep : public LockstepTransport {
   int64_t* h_out_ = nullptr;   // pinned [slots][3]
   std::vector<hipEvent_t> ev_;
   uint64_t issued_ = 0;
+  int64_t timeout_ms_ = 600000;  // like torch.distributed's default NCCL timeout
+  bool aborted_ = false;
+  void wait_event(int t, const char* what);  // bounded wait with async-error checks
 };
 
 }  // namespace tkh

@@ -268,6 +268,8 @@ class DeviceLoader:
         coalesce: fixed-width batches that are already staged when the next one is requested are
             collated together, up to this many per kernel launch (one allocation, one launch, one
             completion event); the following requests return them without a HIP call.  1 disables.
+        lockstep_timeout: seconds the native RCCL lockstep waits for the other ranks before it
+            aborts its communicator and raises (a peer died or hung); <= 0 waits forever.
         numa_bind: before forking the workers, restrict this process (and so the workers) to the CPUs
             of the socket the target GPU is attached to (no-op on single-socket hosts or when
             ``TORCHKAFKA_NUMA=0``); see ``utils/topology.py``.
@@ -282,7 +284,8 @@ class DeviceLoader:
                  rank: int | None = None, world_size: int | None = None, timeout: float = 0,
                  group_id: str | None = None, bootstrap_servers=None, base_seed: int | None = None,
                  lockstep_depth: int = 2, h2d: str = "auto", copy_streams: int = 4,
-                 event_every: int | None = None, numa_bind: bool = True, coalesce: int = 4):
+                 event_every: int | None = None, numa_bind: bool = True, coalesce: int = 4,
+                 lockstep_timeout: float = 600.0):
         if batch_size < 1:
             raise ValueError("batch_size must be >= 1")
         if num_workers < 1:
@@ -326,6 +329,7 @@ class DeviceLoader:
         self.event_every = None if event_every is None else max(1, int(event_every))
         self.numa_bind = bool(numa_bind)
         self.coalesce = max(1, min(8, int(coalesce)))
+        self.lockstep_timeout = float(lockstep_timeout)
         r, w = dist_rank_world()
         self.rank = r if rank is None else int(rank)
         self.world_size = w if world_size is None else int(world_size)
@@ -518,7 +522,9 @@ class DeviceLoader:
         via = self.device if dist.get_backend(process_group) == "nccl" else torch.device("cpu")
         dist.broadcast_object_list(uid, src=src, group=process_group, device=via)
         dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
-        return hip().RcclLockstep(lib, uid[0], rank, world, dev, self.lockstep_depth + 2)
+        ls = hip().RcclLockstep(lib, uid[0], rank, world, dev, self.lockstep_depth + 2)
+        ls.set_timeout_ms(int(self.lockstep_timeout * 1000))
+        return ls
 
     def _iterate_driver(self, run: _Run, auto_commit: bool):
         """GPU iteration through the native step driver (one native call per fixed-width batch)."""
