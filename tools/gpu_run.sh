@@ -38,6 +38,12 @@ for s in $STEPS; do
     benchdirectw8) step bench_direct_w8 600 python bench.py --stats --steps 4000 --warmup 100 --h2d direct --workers 8 ;;
     pytestdirect) step pytest_direct 300 python -u -m pytest tests/test_gpu_loader.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread -k "direct" ;;
     benchnospin) TORCHKAFKA_WORKER_SPIN_US=0 step bench_nospin 600 python bench.py --stats --steps 4000 --warmup 100 ;;
+    benchpf0) TORCHKAFKA_CRC_PREFETCH=0 step bench_pf0 600 python bench.py --stats --steps 4000 --warmup 100 ;;
+    benchpf2k) TORCHKAFKA_CRC_PREFETCH=2048 step bench_pf2k 600 python bench.py --stats --steps 4000 --warmup 100 ;;
+    benchpf4k) TORCHKAFKA_CRC_PREFETCH=4096 step bench_pf4k 600 python bench.py --stats --steps 4000 --warmup 100 ;;
+    benchs8) step bench_s8 600 python bench.py --stats --steps 4000 --warmup 100 --slots-per-worker 8 ;;
+    benchs8nocrc) step bench_s8nocrc 600 python bench.py --stats --steps 4000 --warmup 100 --slots-per-worker 8 --no-crc ;;
+    benchs16) step bench_s16 600 python bench.py --stats --steps 4000 --warmup 100 --slots-per-worker 16 ;;
     benchnocrc) step bench_nocrc 600 python bench.py --stats --steps 4000 --warmup 100 --no-crc ;;
     benchzc) step bench_zc 600 python bench.py --stats --steps 4000 --warmup 100 --h2d zerocopy ;;
     benchs1) step bench_s1 600 python bench.py --stats --steps 4000 --warmup 100 --copy-streams 1 ;;
@@ -58,6 +64,8 @@ for s in $STEPS; do
     pmc)    (cd /tmp && export TMPDIR=/tmp && step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 "$OLDPWD/tools/kernel_bench.py" --quick) || exit $?
             (cd /tmp && export TMPDIR=/tmp && step pmc_write 300 rocprofv3 --pmc WRITE_SIZE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_INSTS_VMEM_WR --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$OLDPWD/tools/kernel_bench.py" --quick) || exit $? ;;
     profcopy) (cd /tmp && export TMPDIR=/tmp && step profcopy 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profcopy" -o run -- python3 "$OLDPWD/bench.py" --steps 1000) || exit $? ;;
+    profnocrc) (cd /tmp && export TMPDIR=/tmp && step profnocrc 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profnocrc" -o run -- python3 "$OLDPWD/bench.py" --steps 2000 --no-crc --stats) || exit $? ;;
+    proflong) (cd /tmp && export TMPDIR=/tmp && step proflong 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/proflong" -o run -- python3 "$OLDPWD/bench.py" --steps 2000 --stats) || exit $? ;;
     prof)   (cd /tmp && export TMPDIR=/tmp && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$OLDPWD/bench.py" --steps 200) || exit $? ;;
   esac
 done

@@ -253,6 +253,10 @@ PYBIND11_MODULE(_tkhip, m) {
              s["phase_steps"] = d.ph_steps_;
              s["events"] = d.events_;
              s["groups"] = d.groups();
+             s["release_ns"] = d.rel_ns_;
+             s["released"] = d.released_;
+             s["polled"] = d.polled_;
+             s["poll_ns"] = d.poll_ns_;
              s["log_bytes_registered"] = d.log_bytes_registered();
              s["log_register_ns"] = d.log_register_ns();
              return s;

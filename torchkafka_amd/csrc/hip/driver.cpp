@@ -66,12 +66,18 @@ MainDriver::~MainDriver() {
 // With batched events only some slots carry one; a completed event also completes
 // every slot launched before it on that stream (note_handed keeps one stream per run).
 void MainDriver::release_completed() {
+  const int64_t t0 = tk::now_ns();
+  release_completed_impl();
+  rel_ns_ += tk::now_ns() - t0;
+}
+
+void MainDriver::release_completed_impl() {
   size_t k = 0;
   while (k < handed_.size()) {
     size_t e = k;
     while (e < handed_.size() && !handed_[e].ev) ++e;  // next slot with an event
     if (e == handed_.size() || !eng_->slot_done(int(handed_[e].g))) break;
-    for (; k <= e; ++k) ring_->main_release(uint32_t(handed_[k].g));
+    for (; k <= e; ++k, ++released_) ring_->main_release(uint32_t(handed_[k].g));
   }
   if (k) handed_.erase(handed_.begin(), handed_.begin() + long(k));
 }
@@ -105,20 +111,44 @@ void MainDriver::note_handed(int64_t g, hipStream_t stream, bool* record) {
 int MainDriver::poll_blocking(int64_t timeout_ms) {
   // Workers may be waiting for slots the GPU still reads: cover them with an event and keep
   // releasing while waiting, so a full ring drains without a round trip through the caller.
+  // While slots are in flight on the GPU this must not sleep on the ring futex: the next READY
+  // slot may depend on a release only this thread can do (worker waits for a FREE slot, the
+  // slot waits for its kernel, nobody would wake us before the futex timeout).  So: poll the
+  // ring and the completion events together, spinning first (a kernel or a worker is usually
+  // microseconds away), then in short sleeps; block on the futex only with nothing in flight.
   cover_handed();
-  const int64_t deadline = timeout_ms < 0 ? INT64_MAX : tk::now_ns() + timeout_ms * 1000000LL;
+  const int64_t start = tk::now_ns();
+  const int64_t deadline = timeout_ms < 0 ? INT64_MAX : start + timeout_ms * 1000000LL;
   for (;;) {
-    const int64_t now = tk::now_ns();
-    const int64_t left_ms = deadline == INT64_MAX ? -1 : std::max<int64_t>(0, (deadline - now) / 1000000LL);
-    const int64_t slice = handed_.empty() ? left_ms : (left_ms < 0 ? 1 : std::min<int64_t>(left_ms, 1));
-    const int r = poll_one(true, slice);
+    const int r = poll_one(false, 0);
     if (r != -1) return r;
+    const int64_t now = tk::now_ns();
+    if (now >= deadline) return -1;
+    if (handed_.empty()) {
+      const int64_t left_ms = deadline == INT64_MAX ? 20 : std::max<int64_t>(0, (deadline - now) / 1000000LL);
+      const int r2 = poll_one(true, std::min<int64_t>(left_ms, 20));
+      if (r2 != -1) return r2;
+      continue;
+    }
     release_completed();
-    if (tk::now_ns() >= deadline) return -1;
+    if (now - start < 200000) {
+      for (int k = 0; k < 32; ++k) tk::cpu_relax();
+    } else {
+      timespec ts{0, 20000};
+      nanosleep(&ts, nullptr);
+    }
   }
 }
 
 int MainDriver::poll_one(bool block, int64_t timeout_ms) {
+  const int64_t t0 = block ? 0 : tk::now_ns();
+  const int r = poll_one_impl(block, timeout_ms);
+  if (!block) poll_ns_ += tk::now_ns() - t0;
+  if (r == 1) ++polled_;
+  return r;
+}
+
+int MainDriver::poll_one_impl(bool block, int64_t timeout_ms) {
   for (;;) {
     const int64_t g = ring_->main_acquire(cursor_.data(), &rr_, done_.data(), in_order_, block ? timeout_ms : 0);
     if (g == -2) return -2;
@@ -646,6 +676,7 @@ void MainDriver::reset_stats() {
   ph_commit_ns_ = ph_next_ns_ = ph_launch_ns_ = ph_steps_ = events_ = groups_ = 0;
   reg_ns_ = 0;
   reg_total_ = 0;
+  rel_ns_ = released_ = polled_ = poll_ns_ = 0;
   commit_ns_.clear();
 }
 

@@ -124,7 +124,9 @@ class MainDriver {
 
  private:
   int poll_one(bool block, int64_t timeout_ms);
+  int poll_one_impl(bool block, int64_t timeout_ms);
   void release_completed();
+  void release_completed_impl();
   void note_handed(int64_t g, hipStream_t stream, bool* record);  // decides whether slot g records its event
   void cover_handed();  // records an event for the newest handed slot without one
   int poll_blocking(int64_t timeout_ms);  // blocks for a slot, releasing completed ones meanwhile
@@ -185,6 +187,8 @@ class MainDriver {
   int64_t fill_ns_ = 0, fills_ = 0, blocked_ns_ = 0, blocked_calls_ = 0, ready_age_ns_ = 0;
   // step_fixed phases (ns): finish+commit of the previous batch, slot acquisition/release, collate launch
   int64_t ph_commit_ns_ = 0, ph_next_ns_ = 0, ph_launch_ns_ = 0, ph_steps_ = 0, events_ = 0;
+  // inside the next phase: slot releases (event queries + ring hand-back) and stagings of READY slots
+  int64_t rel_ns_ = 0, released_ = 0, polled_ = 0, poll_ns_ = 0;
  private:
   std::vector<int64_t> commit_ns_;
   int coalesce_ = 1;

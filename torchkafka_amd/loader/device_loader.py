@@ -630,6 +630,9 @@ class DeviceLoader:
         self.stats.phase_steps += st["phase_steps"]
         self.stats.events += st["events"]
         self.stats.groups += st.get("groups", 0)
+        self.stats.release_ns += st.get("release_ns", 0)
+        self.stats.poll_ns += st.get("poll_ns", 0)
+        self.stats.polled += st.get("polled", 0)
         self.stats.log_bytes_registered = st.get("log_bytes_registered", 0)
         self.stats.log_register_ns = st.get("log_register_ns", 0)
         self.stats.commits += st["commits"]

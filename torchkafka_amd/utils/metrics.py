@@ -39,6 +39,9 @@ class LoaderStats:
     phase_steps: int = 0
     events: int = 0            # completion events recorded (batched: fewer than batches)
     groups: int = 0            # coalesced launches (several batches collated by one kernel)
+    release_ns: int = 0        # native next phase: slot releases (event queries + ring hand-back)
+    poll_ns: int = 0           # native next phase: non-blocking stagings of READY slots
+    polled: int = 0
     log_bytes_registered: int = 0  # h2d="direct": broker log bytes pinned in place so far
     log_register_ns: int = 0
     started: float = field(default_factory=time.perf_counter)
@@ -77,6 +80,9 @@ class LoaderStats:
             "native_launch_us_per_step": self.phase_launch_ns / 1e3 / max(self.phase_steps, 1),
             "events_per_batch": self.events / max(self.batches, 1),
             "group_launches_per_batch": self.groups / max(self.batches, 1),
+            "native_release_us_per_step": self.release_ns / 1e3 / max(self.phase_steps, 1),
+            "native_poll_us_per_step": self.poll_ns / 1e3 / max(self.phase_steps, 1),
+            "native_poll_us_per_slot": self.poll_ns / 1e3 / max(self.polled, 1),
             "log_mib_pinned": self.log_bytes_registered / 2**20,
             "log_pin_ms": self.log_register_ns / 1e6,
             "commits": self.commits,
