@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--dim", type=int, default=256, help="float32 elements per record")
     ap.add_argument("--workers", type=int, default=4)
     ap.add_argument("--partitions-per-gpu", type=int, default=8)
-    ap.add_argument("--slots-per-worker", type=int, default=4)
+    ap.add_argument("--slots-per-worker", type=int, default=None, help="ring depth (default: loader's auto)")
     ap.add_argument("--prefetch", type=int, default=2)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "f16", "f32"])
     ap.add_argument("--records-per-batch", type=int, default=64, help="Kafka RecordBatch size in the log")
@@ -99,7 +99,7 @@ def main() -> int:
     # backlog per owned partition: every batch the timed loop and the warm-up consume, plus what the
     # workers prefetch into their ring slots, with headroom
     mine = shard_partitions(n_parts, rank, world)
-    batches = args.warmup + args.steps + args.workers * (args.slots_per_worker + 2)
+    batches = args.warmup + args.steps + args.workers * ((args.slots_per_worker or 8) + 2)
     per_part = int(math.ceil(batches * B * 1.25 / max(1, len(mine)))) + B
     t_fill = time.perf_counter()
     broker.fill("bench", per_part, "fixed_f32", size=args.dim, partitions=mine,

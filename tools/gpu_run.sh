@@ -44,6 +44,9 @@ for s in $STEPS; do
     benchs8) step bench_s8 600 python bench.py --stats --steps 4000 --warmup 100 --slots-per-worker 8 ;;
     benchs8nocrc) step bench_s8nocrc 600 python bench.py --stats --steps 4000 --warmup 100 --slots-per-worker 8 --no-crc ;;
     benchs16) step bench_s16 600 python bench.py --stats --steps 4000 --warmup 100 --slots-per-worker 16 ;;
+    benchdmas8) step bench_dma_s8 600 python bench.py --stats --steps 4000 --warmup 100 --slots-per-worker 8 --h2d dma ;;
+    benchdmas8c1) step bench_dma_s8c1 600 python bench.py --stats --steps 4000 --warmup 100 --slots-per-worker 8 --h2d dma --coalesce 1 ;;
+    profs8) (cd /tmp && export TMPDIR=/tmp && step profs8 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profs8" -o run -- python3 "$OLDPWD/bench.py" --steps 2000 --stats --slots-per-worker 8) || exit $? ;;
     benchnocrc) step bench_nocrc 600 python bench.py --stats --steps 4000 --warmup 100 --no-crc ;;
     benchzc) step bench_zc 600 python bench.py --stats --steps 4000 --warmup 100 --h2d zerocopy ;;
     benchs1) step bench_s1 600 python bench.py --stats --steps 4000 --warmup 100 --copy-streams 1 ;;

@@ -254,6 +254,9 @@ PYBIND11_MODULE(_tkhip, m) {
              s["events"] = d.events_;
              s["groups"] = d.groups();
              s["release_ns"] = d.rel_ns_;
+             s["fast_batches"] = d.fast_batches_;
+             s["fast_records"] = d.fast_records_;
+             s["fast_ns"] = d.fast_ns_;
              s["released"] = d.released_;
              s["polled"] = d.polled_;
              s["poll_ns"] = d.poll_ns_;

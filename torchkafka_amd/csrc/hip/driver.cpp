@@ -677,6 +677,7 @@ void MainDriver::reset_stats() {
   reg_ns_ = 0;
   reg_total_ = 0;
   rel_ns_ = released_ = polled_ = poll_ns_ = 0;
+  fast_batches_ = fast_records_ = fast_ns_ = 0;
   commit_ns_.clear();
 }
 

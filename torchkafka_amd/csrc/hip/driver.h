@@ -189,6 +189,21 @@ class MainDriver {
   int64_t ph_commit_ns_ = 0, ph_next_ns_ = 0, ph_launch_ns_ = 0, ph_steps_ = 0, events_ = 0;
   // inside the next phase: slot releases (event queries + ring hand-back) and stagings of READY slots
   int64_t rel_ns_ = 0, released_ = 0, polled_ = 0, poll_ns_ = 0;
+
+  // Per-iteration constants of the fixed-width fast path (set once by torch_step.cpp's
+  // configure_fast; fast_next() then takes no arguments) and its own counters.
+  struct FastConfig {
+    int device = 0;
+    std::vector<int64_t> shape;
+    int dst_dt = 0;
+    int64_t row = 0;
+    const float* shift = nullptr;
+    const float* scale = nullptr;
+    bool auto_commit = true;
+    int64_t timeout_ms = 100;
+    bool grouped = true;
+  } fast;
+  int64_t fast_batches_ = 0, fast_records_ = 0, fast_ns_ = 0;
  private:
   std::vector<int64_t> commit_ns_;
   int coalesce_ = 1;

@@ -35,9 +35,98 @@ at::ScalarType scalar_type_of(int code) {
     default: throw std::invalid_argument("step_fixed_tensor: unsupported dtype code");
   }
 }
+// One fixed-width step: finish + commit the previous batch, take the next one, collate it
+// (coalesced with staged ones when cfg.grouped) into a tensor on the current stream.
+py::tuple step_once(MainDriver& d, const MainDriver::FastConfig& cfg) {
+  const auto dev = c10::DeviceIndex(cfg.device);
+  hipStream_t stream = c10::hip::getCurrentHIPStream(dev).stream();
+  const auto opts = at::TensorOptions().dtype(scalar_type_of(cfg.dst_dt)).device(at::kCUDA, dev);
+  int cs = 0;
+  int64_t r;
+  if (!cfg.grouped) {
+    at::Tensor out = at::empty(cfg.shape, opts);
+    {
+      py::gil_scoped_release nogil;
+      r = d.step_fixed(stream, cfg.dst_dt, out.data_ptr(), cfg.row, cfg.shift, cfg.scale, cfg.auto_commit,
+                       cfg.timeout_ms, &cs, &d.last);
+    }
+    if (r <= 0) return py::make_tuple(r, cs, py::none());
+    if (r < cfg.shape[0]) out = out.narrow(0, 0, r);
+    return py::make_tuple(r, cs, py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(out))));
+  }
+  std::vector<int64_t> rows;
+  std::shared_ptr<void> pre;
+  {
+    py::gil_scoped_release nogil;
+    r = d.step_group_begin(stream, cfg.auto_commit, cfg.timeout_ms, &cs, &rows, &pre);
+  }
+  if (r <= 0) return py::make_tuple(r, cs, py::none());
+  at::Tensor out;
+  if (pre) {
+    out = *static_cast<at::Tensor*>(pre.get());
+  } else {
+    int64_t total = 0;
+    for (auto x : rows) total += x;
+    std::vector<int64_t> all_shape(cfg.shape);
+    all_shape[0] = total;
+    at::Tensor all = at::empty(all_shape, opts);
+    void* dsts[kMaxGroup];
+    std::vector<std::shared_ptr<void>> handles;
+    handles.reserve(rows.size());
+    int64_t off = 0;
+    for (size_t k = 0; k < rows.size(); ++k) {
+      at::Tensor t = rows.size() == 1 ? all : all.narrow(0, off, rows[k]);
+      dsts[k] = t.data_ptr();
+      if (k == 0)
+        out = t;
+      else
+        handles.emplace_back(new at::Tensor(std::move(t)), [](void* p) { delete static_cast<at::Tensor*>(p); });
+      off += rows[k];
+    }
+    py::gil_scoped_release nogil;
+    d.step_group_launch(stream, cfg.dst_dt, dsts, cfg.row, cfg.shift, cfg.scale, std::move(handles));
+  }
+  return py::make_tuple(r, cs, py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(out))));
+}
+
 }  // namespace
 
 void register_torch_step(py::module_& m) {
+  // Argument-free fast path: the iteration's constants are set once, and each step is one
+  // method call on the driver that also keeps the loader's batch/record/time counters, so the
+  // per-batch Python work is a bound-method call and a tuple unpack.
+  auto cls = py::reinterpret_borrow<py::class_<MainDriver>>(m.attr("MainDriver"));
+  cls.def(
+      "configure_fast",
+      [](MainDriver& d, int device, std::vector<int64_t> shape, int dst_dt, int64_t row, uintptr_t shift,
+         uintptr_t scale, bool auto_commit, int64_t timeout_ms, bool grouped) {
+        if (shape.empty()) throw std::invalid_argument("configure_fast: empty shape");
+        scalar_type_of(dst_dt);  // validates
+        auto& c = d.fast;
+        c.device = device;
+        c.shape = std::move(shape);
+        c.dst_dt = dst_dt;
+        c.row = row;
+        c.shift = reinterpret_cast<const float*>(shift);
+        c.scale = reinterpret_cast<const float*>(scale);
+        c.auto_commit = auto_commit;
+        c.timeout_ms = timeout_ms;
+        c.grouped = grouped;
+      },
+      py::arg("device"), py::arg("shape"), py::arg("dst_dt"), py::arg("row"), py::arg("shift"), py::arg("scale"),
+      py::arg("auto_commit"), py::arg("timeout_ms"), py::arg("grouped"));
+  cls.def("fast_next", [](MainDriver& d) -> py::tuple {
+    const int64_t t0 = tk::now_ns();
+    py::tuple res = step_once(d, d.fast);
+    const int64_t r = res[0].cast<int64_t>();
+    if (r > 0) {
+      ++d.fast_batches_;
+      d.fast_records_ += r;
+      d.fast_ns_ += tk::now_ns() - t0;
+    }
+    return res;
+  });
+
   m.def(
       "step_fixed_tensor",
       [](MainDriver& d, int device, std::vector<int64_t> shape, int dst_dt, int64_t row, uintptr_t shift,

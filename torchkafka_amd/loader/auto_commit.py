@@ -56,13 +56,18 @@ def auto_commit(dataloader, *, final_commit_timeout: float = 5.0, process_group=
 
     ``dataloader`` is a ``torch.utils.data.DataLoader`` (any dataset) or a
     :class:`~torchkafka_amd.loader.DeviceLoader`.  ``process_group`` (DeviceLoader
-    only) overrides the group used for cross-rank lockstep.
+    only) overrides the group used for cross-rank lockstep.  Returns a generator; for a
+    DeviceLoader it is the loader's own (one generator level less per batch).
     """
     from .device_loader import DeviceLoader
 
     if isinstance(dataloader, DeviceLoader):
-        yield from dataloader._iterate(auto_commit=True, process_group=process_group)
-        return
+        return dataloader._iterate(auto_commit=True, process_group=process_group)
+    return _auto_commit(dataloader, final_commit_timeout)
+
+
+def _auto_commit(dataloader, final_commit_timeout: float):
+    # a generator function: a non-DataLoader raises on the first next(), as in the reference (B18)
     if not isinstance(dataloader, DataLoader):
         raise TypeError("A DataLoader must be provided.")
 
