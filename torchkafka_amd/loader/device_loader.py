@@ -39,7 +39,7 @@ from typing import NamedTuple
 import torch
 
 from ..client.errors import COMMIT_FAILED_ERRORS
-from ..ops.collate import CODE_DTYPE, DTYPE_CODE, FLOAT_DTYPES, normalize_params
+from ..ops.collate import CODE_DTYPE, DTYPE_CODE, FLOAT_DTYPES, _stream_ptr, normalize_params
 from ..ops.native import core, hip
 from ..parallel.sharding import dist_rank_world
 from ..utils import topology
@@ -552,7 +552,7 @@ class DeviceLoader:
             else:
                 while True:
                     # asking for the next batch finishes the previous one
-                    drv.finish_delivered(torch.cuda.current_stream(self.device).cuda_stream)
+                    drv.finish_delivered(_stream_ptr(self.device))
                     if auto_commit:
                         self._log_commit(drv.commit_pending(), debug)
                     item = self._next_item_driver(run)
@@ -562,7 +562,7 @@ class DeviceLoader:
                     yield item[0]
             completed = True
         finally:
-            drv.finish_delivered(torch.cuda.current_stream(self.device).cuda_stream)
+            drv.finish_delivered(_stream_ptr(self.device))
             if completed:
                 drv.finish_lockstep()
             drv.drain_fenced(True)
@@ -616,7 +616,7 @@ class DeviceLoader:
                     run._wait_since = None
             completed = True
         finally:
-            drv.finish_delivered(torch.cuda.current_stream(self.device).cuda_stream)
+            drv.finish_delivered(_stream_ptr(self.device))
             if completed:
                 drv.finish_lockstep()
             drv.drain_fenced(True)
@@ -775,7 +775,7 @@ class DeviceLoader:
         if (dst_dt in FLOAT_DTYPES) != (src_dt in FLOAT_DTYPES) and src_dt in FLOAT_DTYPES:
             raise TypeError(f"cannot collate {src_dt} records to {dst_dt}")
         dev = self.device
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = _stream_ptr(dev)
         lengths = mask = None
         fixed = kind == core().PACK_FIXED
         if fixed:
@@ -825,7 +825,7 @@ class DeviceLoader:
             prm = self._norm_params(row)
             if run.engine is not None:
                 shift, scale = (prm[0].data_ptr(), prm[1].data_ptr()) if prm is not None else (0, 0)
-                run.engine.collate_fixed(g, torch.cuda.current_stream(dev).cuda_stream, voff, DTYPE_CODE[src_dt],
+                run.engine.collate_fixed(g, _stream_ptr(dev), voff, DTYPE_CODE[src_dt],
                                          out.data_ptr(), DTYPE_CODE[dst_dt], n_rows, row, shift, scale)
             else:
                 view = run.ring.payload_view(g)
@@ -843,7 +843,7 @@ class DeviceLoader:
             lengths = torch.empty(n_rows, dtype=torch.int64, device=dev)
             mask = torch.empty((n_rows, L), dtype=torch.bool, device=dev) if self.return_mask else None
             if run.engine is not None:
-                run.engine.collate_varlen(g, torch.cuda.current_stream(dev).cuda_stream, voff, DTYPE_CODE[src_dt],
+                run.engine.collate_varlen(g, _stream_ptr(dev), voff, DTYPE_CODE[src_dt],
                                           out.data_ptr(), DTYPE_CODE[dst_dt], n_rows, L, float(self.pad_value),
                                           lengths.data_ptr(), mask.data_ptr() if mask is not None else 0)
             else:
@@ -921,7 +921,7 @@ class DeviceLoader:
         """Commits every batch yielded so far (manual mode)."""
         run = self._run
         if run is not None and run.driver is not None and not run.closed:
-            run.driver.finish_delivered(torch.cuda.current_stream(self.device).cuda_stream)
+            run.driver.finish_delivered(_stream_ptr(self.device))
             run.driver.drain_fenced(True)
             self._log_commit(run.driver.commit_pending(), _ds_logger.isEnabledFor(logging.DEBUG))
             self._absorb_driver_stats(run.driver)

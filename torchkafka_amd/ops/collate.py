@@ -26,7 +26,10 @@ def _code(dt: torch.dtype) -> int:
 
 
 def _stream_ptr(device: torch.device) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
+    # the raw handle: ~0.08 µs, against ~1.9 µs for torch.cuda.current_stream(device).cuda_stream
+    # (host_overhead.log), which builds a Stream object per call
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    return torch._C._cuda_getCurrentRawStream(idx)
 
 
 def normalize_params(normalize, row: int, device) -> tuple[torch.Tensor, torch.Tensor] | None:
