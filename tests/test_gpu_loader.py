@@ -343,3 +343,20 @@ def test_direct_log_gather_values(broker):
             seen.add((p, o))
     assert len(seen) == 1800
     assert broker.committed_offsets("g", "t") == {p: 300 for p in range(6)}
+
+
+def test_state_dict_is_live_during_iteration(broker):
+    """state_dict() mid-iteration reflects the native driver's commits (checkpoint every k steps)."""
+    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
+
+    broker.create_topic("t", 1)
+    broker.fill("t", 200, "fixed_f32", size=16, records_per_batch=10)
+    DS = _dataset(FixedWidth(torch.float32, (16,)))
+    dl = DeviceLoader(DS.placeholder(), 20, num_workers=1, device="cuda:0",
+                      worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    snaps = []
+    for i, _ in enumerate(auto_commit(dl)):
+        if i in (3, 6):
+            snaps.append(dl.state_dict()["offsets"]["t"][0])
+    assert snaps == [60, 120]  # batches 0..2 and 0..5 finished and committed when batch 3 / 6 arrived

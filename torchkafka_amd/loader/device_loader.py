@@ -942,6 +942,11 @@ class DeviceLoader:
         return self.stats.summary()
 
     def committed_offsets(self) -> dict[int, int]:
+        """{partition index: committed offset} of every partition this loader committed (live during
+        iteration: the native driver's commits are included)."""
+        run = self._run
+        if run is not None and run.driver is not None and not run.closed:
+            self._committed.update(dict(run.driver.committed()))
         return dict(self._committed)
 
     # ------------------------------------------------------------------ checkpoint / resume
