@@ -57,7 +57,8 @@ def parse():
     ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy", "direct"])
     ap.add_argument("--copy-streams", type=int, default=4)
     ap.add_argument("--lockstep-depth", type=int, default=2)
-    ap.add_argument("--coalesce", type=int, default=4, help="staged batches collated per kernel launch")
+    ap.add_argument("--coalesce", type=int, default=8, help="staged batches collated per kernel launch")
+    ap.add_argument("--coalesce-wait-us", type=int, default=50, help="adaptive coalescing wait while the GPU is busy")
     ap.add_argument("--no-numa", action="store_true", help="do not bind ranks to their GPU's NUMA node")
     return ap.parse_args()
 
@@ -115,6 +116,7 @@ def main() -> int:
         slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
         in_order=args.in_order, h2d=args.h2d, copy_streams=args.copy_streams, lockstep_depth=args.lockstep_depth,
         event_every=args.event_every, numa_bind=not args.no_numa, coalesce=args.coalesce,
+        coalesce_wait_us=args.coalesce_wait_us,
         worker_init_fn=Records.init_worker("bench", bootstrap_servers=url, group_id="bench",
                                            auto_offset_reset="earliest", check_crcs=not args.no_crc),
     )

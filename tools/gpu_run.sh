@@ -47,6 +47,9 @@ for s in $STEPS; do
     benchdmas8) step bench_dma_s8 600 python bench.py --stats --steps 4000 --warmup 100 --slots-per-worker 8 --h2d dma ;;
     benchdmas8c1) step bench_dma_s8c1 600 python bench.py --stats --steps 4000 --warmup 100 --slots-per-worker 8 --h2d dma --coalesce 1 ;;
     profs8) (cd /tmp && export TMPDIR=/tmp && step profs8 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profs8" -o run -- python3 "$OLDPWD/bench.py" --steps 2000 --stats --slots-per-worker 8) || exit $? ;;
+    benchw0) step bench_w0 600 python bench.py --stats --steps 4000 --warmup 100 --coalesce-wait-us 0 ;;
+    benchc8w) step bench_c8w 600 python bench.py --stats --steps 4000 --warmup 100 --coalesce 8 ;;
+    benchc8w200) step bench_c8w200 600 python bench.py --stats --steps 4000 --warmup 100 --coalesce 8 --coalesce-wait-us 200 ;;
     benchnocrc) step bench_nocrc 600 python bench.py --stats --steps 4000 --warmup 100 --no-crc ;;
     benchzc) step bench_zc 600 python bench.py --stats --steps 4000 --warmup 100 --h2d zerocopy ;;
     benchs1) step bench_s1 600 python bench.py --stats --steps 4000 --warmup 100 --copy-streams 1 ;;

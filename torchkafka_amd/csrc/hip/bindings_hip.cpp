@@ -268,6 +268,7 @@ PYBIND11_MODULE(_tkhip, m) {
       .def("set_event_every", &MainDriver::set_event_every, py::arg("n"))
       .def_property_readonly("event_every", &MainDriver::event_every)
       .def("set_coalesce", &MainDriver::set_coalesce, py::arg("n"))
+      .def("set_coalesce_wait_us", &MainDriver::set_coalesce_wait_us, py::arg("us"))
       .def("enable_direct", &MainDriver::enable_direct)
       .def_property_readonly("direct", &MainDriver::direct)
       .def_property_readonly("coalesce", &MainDriver::coalesce)

@@ -21,8 +21,9 @@ void launch_varlen(const int32_t* offs, const void* vals, int src_dt, void* out,
 
 // Up to kMaxGroup dense casts (consecutive batches, same dtypes and row width) in one launch.
 constexpr int kMaxGroup = 8;
+// host_src: the sources are pinned host memory read over PCIe (zero-copy), which sizes the grid.
 void launch_fixed_group(const void* const* srcs, int src_dt, void* const* dsts, int dst_dt, const int64_t* rows, int n,
-                        int64_t row, const float* shift, const float* scale, hipStream_t stream);
+                        int64_t row, const float* shift, const float* scale, hipStream_t stream, bool host_src);
 
 // Fixed-width rows gathered from pinned broker logs: ents[k][i] = (pidx << 44) | byte offset,
 // bases[pidx] = device address of partition pidx's log.  Rows of `row_bytes` at any alignment.

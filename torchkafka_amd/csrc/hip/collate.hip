@@ -290,7 +290,7 @@ __global__ __launch_bounds__(kThreads) void fixed_group_kernel(FixedGroupArgs a,
 
 template <typename S, typename D>
 void launch_fixed_group_t(const void* const* srcs, void* const* dsts, const int64_t* rows, int n, int64_t row,
-                          const float* shift, const float* scale, hipStream_t stream) {
+                          const float* shift, const float* scale, hipStream_t stream, bool host_src) {
   const bool affine = shift != nullptr;
   bool vec = (row % kEPT == 0) &&
              (!affine || (reinterpret_cast<uintptr_t>(shift) % 16 == 0 && reinterpret_cast<uintptr_t>(scale) % 16 == 0));
@@ -301,6 +301,7 @@ void launch_fixed_group_t(const void* const* srcs, void* const* dsts, const int6
   }
   if (!vec || max_groups == 0) {  // unaligned or odd rows: one ordinary launch per slot
     for (int k = 0; k < n; ++k) launch_fixed_t<S, D>(srcs[k], dsts[k], rows[k], row, shift, scale, stream);
+    (void)host_src;
     return;
   }
   FixedGroupArgs a{};
@@ -310,8 +311,12 @@ void launch_fixed_group_t(const void* const* srcs, void* const* dsts, const int6
     a.dst[k] = dsts[k];
     a.groups[k] = rows[k] * row / kEPT;
   }
-  // every lane's load in flight at once up to ~2048 blocks in total
-  a.bps = int(std::max<int64_t>(1, std::min<int64_t>((max_groups + kThreads - 1) / kThreads, 2048 / n)));
+  // A zero-copy read is PCIe-latency-bound: ~16 blocks in total keep enough bytes in flight per
+  // wave, more blocks only add request overhead (probe over k x 256 KiB slots, group_probe.log:
+  // 4 slots 20.9 us at 4 blocks/slot vs 24.7 us at 32; 8 slots 39.4 vs 50.2 us).  HBM sources
+  // (DMA staging) are not latency-bound and get one block per 256 groups.
+  const int64_t full = std::max<int64_t>(1, std::min<int64_t>((max_groups + kThreads - 1) / kThreads, 2048 / n));
+  a.bps = int(host_src ? std::min<int64_t>(full, std::max(4, 16 / n)) : full);
   const dim3 grid(unsigned(a.bps * n));
   if (affine)
     hipLaunchKernelGGL((fixed_group_kernel<S, D, true>), grid, dim3(kThreads), 0, stream, a, row, shift, scale);
@@ -556,12 +561,12 @@ void launch_varlen(const int32_t* offs, const void* vals, int src_dt, void* out,
 }
 
 void launch_fixed_group(const void* const* srcs, int src_dt, void* const* dsts, int dst_dt, const int64_t* rows, int n,
-                        int64_t row, const float* shift, const float* scale, hipStream_t stream) {
+                        int64_t row, const float* shift, const float* scale, hipStream_t stream, bool host_src) {
   if (n < 1 || n > kMaxGroup) throw std::invalid_argument("collate: group size out of range");
   if (!is_float_dt(dst_dt) && is_float_dt(src_dt))
     throw std::invalid_argument("collate: float records cannot be cast to an integer dtype");
   if (shift && !is_float_dt(dst_dt)) throw std::invalid_argument("collate: normalisation needs a float dtype");
-  TK_DISPATCH_SRC(launch_fixed_group_t, srcs, dsts, rows, n, row, shift, scale, stream)
+  TK_DISPATCH_SRC(launch_fixed_group_t, srcs, dsts, rows, n, row, shift, scale, stream, host_src)
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("fixed group collate launch: ") + hipGetErrorString(e));
 }

@@ -448,6 +448,14 @@ void MainDriver::collate_fixed(const SlotView& v, hipStream_t stream, int dst_dt
                                const float* shift, const float* scale) {
   bool record;
   note_handed(v.g, stream, &record);
+  if (!record && coalesce_wait_ns_ > 0 && coalesce_ > 1) {
+    // adaptive coalescing decides from the latest launch's completion: give this one its event
+    handed_.back().ev = true;
+    unevented_ = 0;
+    ++events_;
+    record = true;
+  }
+  if (record) last_ev_slot_ = v.g;
   if (v.kind == uint32_t(tk::kPackGatherFixed)) {
     const int slot = int(v.g);
     const int64_t rows = v.n_rows;
@@ -599,17 +607,46 @@ int64_t MainDriver::step_group_begin(hipStream_t stream, bool auto_commit, int64
   }
   group_rows->push_back(last.n_rows);
   if (last.kind == uint32_t(tk::kPackFixed) || last.kind == uint32_t(tk::kPackGatherFixed)) {
-    for (size_t i = 0; i < staged_.size() && int(group_rows->size()) < coalesce_; ++i) {
-      const SlotView& v = staged_[i];
-      if (v.g < 0) continue;  // watermark-only slot: rides on the next delivered batch
-      if (v.pre || v.kind != last.kind || v.src_dtype != last.src_dtype || v.max_row_len != last.max_row_len ||
-          v.row_bytes != last.row_bytes || v.shape != last.shape || v.n_rows == 0)
-        break;
-      group_idx_.push_back(i);
-      group_rows->push_back(v.n_rows);
+    extend_group();
+    if (coalesce_wait_ns_ > 0 && int(1 + group_idx_.size()) < coalesce_) {
+      const int64_t until = tk::now_ns() + coalesce_wait_ns_;
+      while (int(1 + group_idx_.size()) < coalesce_ && gpu_busy() && tk::now_ns() < until) {
+        const int r2 = poll_one(false, 0);
+        if (r2 == -3) break;  // reported by the next call
+        if (r2 == 1) {
+          extend_group();
+          continue;
+        }
+        release_completed();
+        for (int k = 0; k < 16; ++k) tk::cpu_relax();
+      }
     }
+    for (size_t i : group_idx_) group_rows->push_back(staged_[i].n_rows);
   }
   return last.n_rows;
+}
+
+// Appends to group_idx_ the staged batches right behind `last` that one kernel can collate with it.
+void MainDriver::extend_group() {
+  size_t i = group_idx_.empty() ? 0 : group_idx_.back() + 1;
+  for (; i < staged_.size() && int(1 + group_idx_.size()) < coalesce_; ++i) {
+    const SlotView& v = staged_[i];
+    if (v.g < 0) continue;  // watermark-only slot: rides on the next delivered batch
+    if (v.pre || v.kind != last.kind || v.src_dtype != last.src_dtype || v.max_row_len != last.max_row_len ||
+        v.row_bytes != last.row_bytes || v.shape != last.shape || v.n_rows == 0)
+      return;
+    group_idx_.push_back(i);
+  }
+}
+
+// True while the latest launch that recorded a completion event has not finished on the GPU.
+bool MainDriver::gpu_busy() {
+  if (last_ev_slot_ < 0) return false;
+  if (eng_->slot_done(int(last_ev_slot_))) {
+    last_ev_slot_ = -1;
+    return false;
+  }
+  return true;
 }
 
 void MainDriver::step_group_launch(hipStream_t stream, int dst_dt, void* const* dsts, int64_t row,
@@ -640,6 +677,7 @@ void MainDriver::step_group_launch(hipStream_t stream, int dst_dt, void* const* 
     launch_group(slots, rows, voffs, n, last, stream, dst_dt, dsts, row, shift, scale);
     // one completion event (after the group kernel, on the last slot) releases every slot of the group
     for (int k = 0; k < n; ++k) handed_.push_back(Handed{slots[k], k == n - 1});
+    last_ev_slot_ = slots[n - 1];
     unevented_ = 0;
     ++events_;
     ++groups_;

@@ -151,7 +151,7 @@ void Engine::collate_fixed_group(const int* slots, int n, hipStream_t user, cons
     begin(slots[k], user);
     srcs[k] = src_base(slots[k]) + values_offsets[k];
   }
-  launch_fixed_group(srcs, src_dt, dsts, dst_dt, rows, n, row, shift, scale, user);
+  launch_fixed_group(srcs, src_dt, dsts, dst_dt, rows, n, row, shift, scale, user, mode_ == kH2DZeroCopy);
   finish(slots[n - 1], user);
 }
 

@@ -129,6 +129,7 @@ class _Run:
                 self.driver.set_commit_on_device(L.commit_on == "device")
                 self.driver.set_event_every(L._event_every(self.ring.n_slots))
                 self.driver.set_coalesce(L.coalesce)
+                self.driver.set_coalesce_wait_us(L.coalesce_wait_us if L.coalesce > 1 else 0)
                 if L._direct():
                     self.driver.enable_direct()
         except BaseException:
@@ -271,6 +272,9 @@ class DeviceLoader:
         coalesce: fixed-width batches that are already staged when the next one is requested are
             collated together, up to this many per kernel launch (one allocation, one launch, one
             completion event); the following requests return them without a HIP call.  1 disables.
+        coalesce_wait_us: while the GPU is still busy with an earlier launch, wait up to this long
+            for enough staged batches to fill a group (costs no GPU time; a zero-copy batch takes
+            7.1 us alone and 5.2 us in a group of 4).  0 launches whatever is staged at once.
         lockstep_timeout: seconds the native RCCL lockstep waits for the other ranks before it
             aborts its communicator and raises (a peer died or hung); <= 0 waits forever.
         numa_bind: before forking the workers, restrict this process (and so the workers) to the CPUs
@@ -288,7 +292,8 @@ class DeviceLoader:
                  rank: int | None = None, world_size: int | None = None, timeout: float = 0,
                  group_id: str | None = None, bootstrap_servers=None, base_seed: int | None = None,
                  lockstep_depth: int = 2, h2d: str = "auto", copy_streams: int = 4,
-                 event_every: int | None = None, numa_bind: bool = True, coalesce: int = 4,
+                 event_every: int | None = None, numa_bind: bool = True, coalesce: int = 8,
+                 coalesce_wait_us: int = 50,
                  lockstep_timeout: float = 600.0):
         if batch_size < 1:
             raise ValueError("batch_size must be >= 1")
@@ -333,6 +338,7 @@ class DeviceLoader:
         self.event_every = None if event_every is None else max(1, int(event_every))
         self.numa_bind = bool(numa_bind)
         self.coalesce = max(1, min(8, int(coalesce)))
+        self.coalesce_wait_us = max(0, int(coalesce_wait_us))
         self.lockstep_timeout = float(lockstep_timeout)
         r, w = dist_rank_world()
         self.rank = r if rank is None else int(rank)
