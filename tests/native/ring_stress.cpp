@@ -39,7 +39,7 @@ static void ring_protocol(uint32_t nw, uint32_t spw, uint32_t per_worker) {
     ws.emplace_back([&, w] {
       for (uint32_t i = 0; i < per_worker; ++i) {
         const uint32_t slot_i = i % spw;
-        CHECK(ring->worker_acquire(w, slot_i, 10000));
+        CHECK(ring->worker_acquire(w, slot_i, 60000));
         const uint32_t g = ring->gslot(w, slot_i);
         SlotHeader* h = ring->slot(g);
         uint32_t* pay = reinterpret_cast<uint32_t*>(ring->payload(g));
@@ -58,7 +58,7 @@ static void ring_protocol(uint32_t nw, uint32_t spw, uint32_t per_worker) {
   uint32_t rr = 0;
   uint64_t got = 0;
   for (;;) {
-    const int64_t g = ring->main_acquire(cursor.data(), &rr, done.data(), false, 10000);
+    const int64_t g = ring->main_acquire(cursor.data(), &rr, done.data(), false, 60000);
     if (g == -2) break;
     CHECK(g >= 0);
     SlotHeader* h = ring->slot(uint32_t(g));
@@ -125,7 +125,7 @@ static void broker_pipeline(uint32_t nw, uint32_t per_part) {
       uint32_t i = 0;
       uint64_t rows = 0;
       while (rows < 2ull * per_part) {
-        CHECK(ring->worker_acquire(w, i % 3, 20000));
+        CHECK(ring->worker_acquire(w, i % 3, 60000));
         const uint32_t g = ring->gslot(w, i % 3);
         FillOutcome o = fill_slot(f, *ring, g, spec, 64, 50, &rr);
         rows += uint64_t(o.rows);
@@ -142,7 +142,7 @@ static void broker_pipeline(uint32_t nw, uint32_t per_part) {
   const uint32_t grp = b->group_index("stress", true);
   std::vector<int64_t> expect(np, 0);
   for (;;) {
-    const int64_t g = ring->main_acquire(cursor.data(), &rr, done.data(), false, 20000);
+    const int64_t g = ring->main_acquire(cursor.data(), &rr, done.data(), false, 60000);
     if (g == -2) break;
     CHECK(g >= 0);
     SlotHeader* h = ring->slot(uint32_t(g));
