@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--min-len", type=int, default=16)
     ap.add_argument("--max-len", type=int, default=256)
     ap.add_argument("--device", default="cuda:0")
+    ap.add_argument("--json-parse", default="auto", choices=["auto", "device", "host"])
+    ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy"])
     args = ap.parse_args()
 
     import torch
@@ -49,6 +51,7 @@ def main():
         b.fill("json", per_part, "json_f32", size=args.min_len, max_size=args.max_len, threads=args.partitions)
         fill_s = time.perf_counter() - t
         dl = DeviceLoader(Json.placeholder(), B, num_workers=args.workers, device=args.device, dtype=torch.bfloat16,
+                          json_parse=args.json_parse, h2d=args.h2d,
                           worker_init_fn=Json.init_worker("json", bootstrap_servers=url, group_id="cfg4",
                                                           auto_offset_reset="earliest"))
         it = iter(auto_commit(dl))
@@ -71,7 +74,7 @@ def main():
         text_bytes = b.partition_stats("json", 0)["log_bytes"] / max(1, b.end_offset("json", 0))
         print(json.dumps({"config": 4, "metric": "JSON records/s to GPU (bf16 padded), per-batch commit",
                           "value": round(rows / el), "ms_per_step": round(el / args.steps * 1e3, 4),
-                          "batch_size": B, "avg_record_bytes": round(text_bytes), "last_batch_shape": list(x.shape),
+                          "batch_size": B, "json_parse": args.json_parse, "h2d": args.h2d, "avg_record_bytes": round(text_bytes), "last_batch_shape": list(x.shape),
                           "device": args.device, "fill_s": round(fill_s, 2), "loader": st}))
     finally:
         b.destroy()

@@ -100,7 +100,8 @@ def test_fixed_cast_on_device_matches_cpu_path(broker, dtype):
     assert torch.equal(a.nan_to_num(), b.nan_to_num())
 
 
-def test_json_varlen_on_device(broker):
+@pytest.mark.parametrize("json_parse", ["device", "host"])
+def test_json_varlen_on_device(broker, json_parse):
     from torchkafka_amd import DeviceLoader, JsonArray, auto_commit
     from torchkafka_amd.client import KafkaConsumer
 
@@ -108,7 +109,7 @@ def test_json_varlen_on_device(broker):
     broker.fill("j", 200, "json_f32", size=1, max_size=40)
     DS = _dataset(JsonArray(min_len=5))
     dl = DeviceLoader(DS.placeholder(), 32, num_workers=2, device="cuda:0", dtype=torch.float32, return_mask=True,
-                      return_info=True,
+                      return_info=True, json_parse=json_parse,
                       worker_init_fn=DS.init_worker("j", bootstrap_servers=broker.url, group_id="g",
                                                     auto_offset_reset="earliest", consumer_timeout_ms=300))
     got = {}
@@ -360,3 +361,78 @@ def test_state_dict_is_live_during_iteration(broker):
         if i in (3, 6):
             snaps.append(dl.state_dict()["offsets"]["t"][0])
     assert snaps == [60, 120]  # batches 0..2 and 0..5 finished and committed when batch 3 / 6 arrived
+
+
+def _produce_json(broker, topic, rows_per_part):
+    from torchkafka_amd.client.producer import KafkaProducer
+
+    p = KafkaProducer(bootstrap_servers=broker.url)
+    for part, rows in rows_per_part.items():
+        for r in rows:
+            p.send(topic, value=r, key=b"k", partition=part)
+    p.flush()
+
+
+@pytest.mark.parametrize("h2d", ["dma", "zerocopy"])
+def test_json_device_parse_mixed_rows_match_python(broker, h2d):
+    """Simple rows parsed by the kernel, exponent/NaN/long rows parsed by the workers, None skipped."""
+    import json
+    import math
+    import random
+
+    from torchkafka_amd import DeviceLoader, JsonArray, auto_commit
+
+    rnd = random.Random(5)
+    rows = {0: [], 1: []}
+    for part in rows:
+        for i in range(150):
+            k = rnd.random()
+            if k < 0.05:
+                rows[part].append(None)
+                continue
+            n = rnd.randint(0, 120)
+            if k < 0.2:
+                vals = [repr(rnd.uniform(-1e20, 1e20)) for _ in range(n)] + ["1e-7", "NaN", "-Infinity"]
+            else:
+                vals = ["%.*f" % (rnd.randint(0, 5), rnd.uniform(-1e4, 1e4)) for _ in range(n)] + ["-0"]
+            rows[part].append(("[" + ", ".join(vals) + "]").encode())
+    broker.create_topic("m", 2)
+    _produce_json(broker, "m", rows)
+    DS = _dataset(JsonArray())
+    dl = DeviceLoader(DS.placeholder(), 40, num_workers=2, device="cuda:0", dtype=torch.float32, return_info=True,
+                      json_parse="device", h2d=h2d,
+                      worker_init_fn=DS.init_worker("m", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    got = []
+    for b in auto_commit(dl):
+        for i in range(b.data.shape[0]):
+            got.append(b.data[i, : int(b.lengths[i])].cpu())
+    ref = [torch.tensor([float(x) for x in json.loads(r)], dtype=torch.float64).to(torch.float32)
+           for part in rows for r in rows[part] if r is not None]
+    key = lambda t: (t.numel(), tuple(0.0 if math.isnan(x) else x for x in t.tolist()))  # noqa: E731
+    assert len(got) == len(ref)
+    for a, b in zip(sorted(got, key=key), sorted(ref, key=key)):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))  # bit-exact, including -0.0 vs +0.0
+    assert broker.committed_offsets("g", "m") == {0: 150, 1: 150}
+
+
+def test_json_device_parse_error_raises_before_commit(broker):
+    from torchkafka_amd import DeviceLoader, JsonArray, auto_commit
+    from torchkafka_amd.client.errors import CorruptRecordException
+
+    good = [b"[1, 2, 3]"] * 40
+    rows = {0: good + [b"[1,,2]"] + good}
+    broker.create_topic("e", 1)
+    _produce_json(broker, "e", rows)
+    DS = _dataset(JsonArray())
+    dl = DeviceLoader(DS.placeholder(), 10, num_workers=1, device="cuda:0", json_parse="device",
+                      worker_init_fn=DS.init_worker("e", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    seen = 0
+    with pytest.raises(CorruptRecordException, match="not a flat numeric JSON array"):
+        for x, _lens in auto_commit(dl):
+            seen += x.shape[0]
+            torch.cuda.synchronize()
+    # batches 0-3 (offsets 0..39) were clean and committed; the batch holding offset 40 never is
+    assert seen >= 50
+    assert broker.committed_offsets("g", "e") == {0: 40}

@@ -20,6 +20,9 @@ for s in $STEPS; do
     build)  step build 600 python -c "import __graft_entry__ as g; g.build()" ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     pytestloader) step pytest_loader 300 python -u -m pytest tests/test_gpu_loader.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    pytestjson) step pytest_json 300 python -u -m pytest tests/test_gpu_json_parse.py tests/test_gpu_loader.py -k json -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    config4zc) step config4_zc 300 python benchmarks/config4_json_varlen.py --h2d zerocopy ;;
+    config4host) step config4_host 300 python benchmarks/config4_json_varlen.py --json-parse host ;;
     pytest) step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     nccl)   step nccl_probe 120 python tools/nccl_probe.py ;;
     overhead) step host_overhead 120 python tools/host_overhead.py ;;
@@ -73,6 +76,7 @@ for s in $STEPS; do
     profcopy) (cd /tmp && export TMPDIR=/tmp && step profcopy 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profcopy" -o run -- python3 "$OLDPWD/bench.py" --steps 1000) || exit $? ;;
     profnocrc) (cd /tmp && export TMPDIR=/tmp && step profnocrc 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profnocrc" -o run -- python3 "$OLDPWD/bench.py" --steps 2000 --no-crc --stats) || exit $? ;;
     proflong) (cd /tmp && export TMPDIR=/tmp && step proflong 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/proflong" -o run -- python3 "$OLDPWD/bench.py" --steps 2000 --stats) || exit $? ;;
+    profc4) (cd /tmp && export TMPDIR=/tmp && step profc4 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profc4" -o run -- python3 "$OLDPWD/benchmarks/config4_json_varlen.py" --steps 300) || exit $? ;;
     prof)   (cd /tmp && export TMPDIR=/tmp && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$OLDPWD/bench.py" --steps 200) || exit $? ;;
   esac
 done

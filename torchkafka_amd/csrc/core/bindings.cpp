@@ -164,6 +164,25 @@ PYBIND11_MODULE(_tkcore, m) {
     v.resize(size_t(n));
     return v;
   });
+  m.def(
+      "json_scan_simple",
+      [](py::bytes b, bool simd) {
+        std::string s = b;
+        return json_scan_simple(s.data(), s.size(), simd);
+      },
+      py::arg("data"), py::arg("simd") = true);
+  m.def("json_scan_copy", [](py::bytes b) {
+    std::string s = b;
+    const size_t nr = (s.size() + 31) / 32 * 32 + 64;
+    std::vector<char> src(nr, 'x');  // read-ahead bytes are garbage on purpose
+    std::memcpy(src.data(), s.data(), s.size());
+    void* dst = nullptr;
+    if (posix_memalign(&dst, 64, nr) != 0) throw std::bad_alloc();
+    const int64_t cnt = json_scan_copy(src.data(), s.size(), static_cast<uint8_t*>(dst));
+    const bool same = std::memcmp(dst, s.data(), s.size()) == 0;
+    std::free(dst);
+    return py::make_tuple(cnt, same);
+  });
   m.def("json_array_len", [](py::bytes b) {
     std::string s = b;
     return json_array_len(s.data(), s.size());
@@ -575,5 +594,6 @@ PYBIND11_MODULE(_tkcore, m) {
   m.attr("PACK_VARLEN") = int(kPackVarlen);
   m.attr("PACK_JSON_F32") = int(kPackJsonF32);
   m.attr("PACK_GATHER_FIXED") = int(kPackGatherFixed);
+  m.attr("PACK_JSON_TEXT") = int(kPackJsonText);
   m.attr("SLOT_HEADER_BYTES") = kSlotHeaderBytes;
 }

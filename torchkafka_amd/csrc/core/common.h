@@ -70,4 +70,18 @@ inline uint64_t get_be64(const uint8_t* p) { uint64_t v; std::memcpy(&v, p, 8); 
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// ---------------------------------------------------------------- slot layouts
+// kPackJsonText rows (device JSON parse): one descriptor per row at the start of the
+// slot payload; `off` is relative to the slot's values area.  tlen >= 0: `tlen` bytes
+// of raw JSON text at `off` (32-byte aligned) holding `count` numbers; tlen == -1: the
+// row was parsed on the host, `n_out` float32 at `off`.  n_out = count after max_len
+// truncation -- the row's output length.
+struct alignas(16) JsonRowDesc {
+  uint32_t off;
+  int32_t tlen;
+  int32_t count;
+  int32_t n_out;
+};
+static_assert(sizeof(JsonRowDesc) == 16, "JsonRowDesc is read with one 16-byte load");
+
 }  // namespace tk

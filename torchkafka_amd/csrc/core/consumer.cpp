@@ -145,6 +145,7 @@ const char* parse_number(const char* p, const char* e, double* out) {
     if (mant == 0 && d == 0) continue;
     if (nd < 19) { mant = mant * 10 + uint64_t(d); ++nd; } else { ++exp10; truncated = true; }
   }
+  const bool is_int_so_far = !(p < e && (*p == '.' || *p == 'e' || *p == 'E'));
   if (p < e && *p == '.') {
     ++p;
     bool frac = false;
@@ -167,6 +168,8 @@ const char* parse_number(const char* p, const char* e, double* out) {
     while (p < e && is_digit(*p)) { if (ev < 100000) ev = ev * 10 + (*p - '0'); ++p; }
     exp10 += eneg ? -ev : ev;
   }
+  // "-0" is the JSON integer 0 for Python (json.loads gives int 0, float() +0.0); "-0.0" stays -0.0
+  if (neg && mant == 0 && is_int_so_far) neg = false;
   double v;
   if (!truncated && mant <= (1ull << 53) && exp10 >= -22 && exp10 <= 22) {
     // Clinger's fast path: both operands exact, one correctly rounded op.
@@ -230,6 +233,176 @@ int64_t json_array_len(const char* s, size_t n) {
   return -1;
 }
 
+// ------------------------------------------------------------ JSON pre-scan (device parse)
+// A row is "simple" -- parsed on the GPU (json_parse.hip) -- when, after trimming
+// whitespace, it is '[' ... ']' whose interior holds only digits, '.', '-', ',' and
+// whitespace, and no run of number characters is longer than 16.  Such numbers have at
+// most 16 digits and no exponent, so Clinger's fast path (or an exact u64 -> f64
+// conversion for integers) gives Python's float() on the device too.  Returns the
+// element count (commas + 1, or 0 for an empty array), or -1 when the row is not simple
+// (the host parser then decides: a valid row is parsed, a malformed one is bad()).
+namespace {
+
+constexpr int kMaxSimpleToken = 16;
+
+inline bool scan_tok(uint8_t c) { return uint8_t(c - '0') <= 9 || c == '.' || c == '-'; }
+inline bool scan_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
+// interior scan state carried across blocks
+struct ScanState {
+  int64_t commas = 0;
+  int run = 0;       // length of the token-character run ending at the previous byte
+  bool any_tok = false;
+};
+
+bool scan_interior_scalar(const uint8_t* p, size_t n, ScanState& st) {
+  for (size_t i = 0; i < n; ++i) {
+    const uint8_t c = p[i];
+    if (scan_tok(c)) {
+      st.any_tok = true;
+      if (++st.run > kMaxSimpleToken) return false;
+    } else {
+      st.run = 0;
+      if (c == ',') ++st.commas;
+      else if (!scan_ws(c)) return false;
+    }
+  }
+  return true;
+}
+
+#if defined(__x86_64__)
+// 64 bytes per iteration, branch-free: the character-class and long-run verdicts are
+// OR-ed into `bad` and checked once.  A run of > 16 token characters ending in this block
+// either lies inside the 80 bits (previous block's top 16 + this block's 64) or was already
+// caught in the previous block, so one 128-bit AND-of-shifts per block finds every run.
+// 32 bytes -> token-character and comma masks; returns the mask of bytes outside the row alphabet
+__attribute__((target("avx2"), always_inline)) inline uint32_t scan_classify32(const uint8_t* q, uint32_t* tokm,
+                                                                               uint32_t* comm) {
+  const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(q));
+  const __m256i c9 = _mm256_set1_epi8(9);
+  const __m256i dv = _mm256_sub_epi8(v, _mm256_set1_epi8('0'));
+  const __m256i dig = _mm256_cmpeq_epi8(_mm256_min_epu8(dv, c9), dv);
+  const __m256i tok = _mm256_or_si256(dig, _mm256_or_si256(_mm256_cmpeq_epi8(v, _mm256_set1_epi8('.')),
+                                                            _mm256_cmpeq_epi8(v, _mm256_set1_epi8('-'))));
+  const __m256i com = _mm256_cmpeq_epi8(v, _mm256_set1_epi8(','));
+  const __m256i ws = _mm256_or_si256(
+      _mm256_or_si256(_mm256_cmpeq_epi8(v, _mm256_set1_epi8(' ')), _mm256_cmpeq_epi8(v, _mm256_set1_epi8('\t'))),
+      _mm256_or_si256(_mm256_cmpeq_epi8(v, _mm256_set1_epi8('\n')), _mm256_cmpeq_epi8(v, _mm256_set1_epi8('\r'))));
+  *tokm = uint32_t(_mm256_movemask_epi8(tok));
+  *comm = uint32_t(_mm256_movemask_epi8(com));
+  return ~uint32_t(_mm256_movemask_epi8(_mm256_or_si256(tok, _mm256_or_si256(com, ws))));
+}
+
+__attribute__((target("avx2,bmi,popcnt"))) bool scan_interior_avx2(const uint8_t* p, size_t n, ScanState& st) {
+  // carry the previous run as the top bits of a virtual previous mask
+  uint64_t prev = st.run >= 16 ? ~uint64_t(0) : (st.run ? ~uint64_t(0) << (64 - st.run) : 0);
+  uint64_t bad = st.run > kMaxSimpleToken ? 1 : 0, anyt = 0;
+  int64_t commas = 0;
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64) {
+    uint32_t t0, t1, c0m, c1m;
+    bad |= scan_classify32(p + i, &t0, &c0m);
+    bad |= scan_classify32(p + i + 32, &t1, &c1m);
+    const uint64_t m = uint64_t(t0) | (uint64_t(t1) << 32);
+    commas += __builtin_popcountll(uint64_t(c0m) | (uint64_t(c1m) << 32));
+    anyt |= m;
+    const unsigned __int128 y = (static_cast<unsigned __int128>(m) << 16) | (prev >> 48);
+    unsigned __int128 r = y & (y >> 1);  // runs >= 2
+    r &= r >> 2;                          // >= 4
+    r &= r >> 4;                          // >= 8
+    r &= r >> 8;                          // >= 16
+    r &= y >> 16;                         // >= 17
+    bad |= uint64_t(r) | uint64_t(r >> 64);
+    prev = m;
+  }
+  if (bad) return false;
+  st.commas += commas;
+  st.any_tok = st.any_tok || anyt != 0;
+  if (i) st.run = prev == ~uint64_t(0) ? std::max(st.run, 0) + 64 : __builtin_clzll(~prev);
+  if (i && prev == ~uint64_t(0)) return false;  // a 64-character token
+  return scan_interior_scalar(p + i, n - i, st);
+}
+const bool g_scan_avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("bmi") &&
+                         __builtin_cpu_supports("popcnt");
+#endif
+
+int64_t json_scan_impl(const char* s, size_t n, bool simd) {
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(s);
+  size_t a = 0, b = n;
+  while (a < b && scan_ws(p[a])) ++a;
+  while (b > a && scan_ws(p[b - 1])) --b;
+  if (b - a < 2 || p[a] != '[' || p[b - 1] != ']') return -1;
+  ScanState st;
+  bool ok;
+#if defined(__x86_64__)
+  if (simd && g_scan_avx2)
+    ok = scan_interior_avx2(p + a + 1, b - a - 2, st);
+  else
+#endif
+    ok = scan_interior_scalar(p + a + 1, b - a - 2, st);
+  (void)simd;
+  if (!ok) return -1;
+  if (!st.any_tok) return st.commas == 0 ? 0 : -1;
+  return st.commas + 1;
+}
+
+}  // namespace
+
+int64_t json_scan_simple(const char* s, size_t n, bool simd) { return json_scan_impl(s, n, simd); }
+
+// Fused pre-scan + copy for the worker's hot path: every 32-byte chunk of the row is loaded
+// once, classified (json_scan_simple's rules) and streamed to the slot.  Bytes outside the
+// array's interior -- leading/trailing whitespace, the brackets, the read-ahead past `n` --
+// are masked out of the verdicts.  Needs: dst 32-byte aligned, src readable and dst writable
+// up to align_up(n, 32).  Returns what json_scan_simple returns; the text is copied either way.
+#if defined(__x86_64__)
+__attribute__((target("avx2,bmi,popcnt"))) int64_t json_scan_copy_avx2(const uint8_t* src, size_t n, uint8_t* dst) {
+  size_t a = 0, b = n;
+  while (a < b && scan_ws(src[a])) ++a;
+  while (b > a && scan_ws(src[b - 1])) --b;
+  const bool framed = b - a >= 2 && src[a] == '[' && src[b - 1] == ']';
+  const size_t lo = a + 1, hi = framed ? b - 1 : lo;  // interior [lo, hi)
+  uint64_t bad = 0, anyt = 0, prev = 0;
+  int64_t commas = 0;
+  const size_t nr = (n + 31) & ~size_t(31);
+  for (size_t i = 0; i < nr; i += 32) {
+    const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i));
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i), v);
+    uint32_t tokm, comm;
+    uint32_t badm = scan_classify32(src + i, &tokm, &comm);
+    // interior bits of this chunk
+    uint32_t in = 0xFFFFFFFFu;
+    if (i < lo) in = lo - i >= 32 ? 0u : in << (lo - i);
+    if (i + 32 > hi) in &= hi <= i ? 0u : (0xFFFFFFFFu >> (32 - (hi - i)));
+    tokm &= in;
+    bad |= badm & in;
+    commas += __builtin_popcount(comm & in);
+    anyt |= tokm;
+    // runs of > 16 number characters: this chunk plus the previous chunk's top 16 bits
+    const uint64_t y = (uint64_t(tokm) << 16) | (prev >> 16);
+    uint64_t q = y & (y >> 1);
+    q &= q >> 2;
+    q &= q >> 4;
+    q &= q >> 8;
+    q &= y >> 16;
+    bad |= q;
+    prev = tokm;
+  }
+  if (!framed || bad) return -1;
+  if (!anyt) return commas == 0 ? 0 : -1;
+  return commas + 1;
+}
+#endif
+
+int64_t json_scan_copy(const char* s, size_t n, uint8_t* dst) {
+#if defined(__x86_64__)
+  if (g_scan_avx2 && g_avx2 && (reinterpret_cast<uintptr_t>(dst) & 31) == 0)
+    return json_scan_copy_avx2(reinterpret_cast<const uint8_t*>(s), n, dst);
+#endif
+  std::memcpy(dst, s, n);
+  return json_scan_impl(s, n, false);
+}
+
 // ------------------------------------------------------------ fill
 FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, int64_t B, int64_t timeout_ms,
                       size_t* rr) {
@@ -253,11 +426,14 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   if (B <= 0) throw std::invalid_argument("batch size must be positive");
 
   const bool fixed = spec.kind == kPackFixed;
+  const bool json_text = spec.kind == kPackJsonText;
+  JsonRowDesc* jrows = nullptr;
   const uint64_t row_bytes = fixed ? uint64_t(spec.row_elems) * uint64_t(spec.elem_size) : 0;
   uint64_t values_off = 0;
   int32_t* offs = nullptr;
   uint64_t* gat = nullptr;
   std::vector<const uint8_t*> log_of;
+  std::vector<uint64_t> log_cap;
   if (gather) {
     if (uint64_t(B) * 8 > cap) throw std::invalid_argument("ring slot too small for the batch's gather table");
     gat = reinterpret_cast<uint64_t*>(pay);
@@ -265,6 +441,14 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
     for (const auto& fp : parts) log_of.push_back(f.broker().log_base(fp.pidx));
   } else if (fixed) {
     if (uint64_t(B) * row_bytes > cap) throw std::invalid_argument("ring slot too small for the batch");
+  } else if (json_text) {
+    for (const auto& fp : parts) {
+      log_of.push_back(f.broker().log_base(fp.pidx));
+      log_cap.push_back(f.broker().part(fp.pidx).log_capacity);
+    }
+    values_off = align_up(uint64_t(B) * sizeof(JsonRowDesc), 256);
+    if (values_off >= cap) throw std::invalid_argument("ring slot too small for the batch's row table");
+    jrows = reinterpret_cast<JsonRowDesc*>(pay);
   } else {
     values_off = align_up(uint64_t(B + 1) * 4, 256);
     if (values_off >= cap) throw std::invalid_argument("ring slot too small for the batch offsets");
@@ -321,6 +505,59 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
     }
     int64_t len;
     uint64_t nbytes;
+    if (json_text) {
+      // device parse: frame the row (count + simple check), copy its text; rows that are not
+      // simple are parsed here and travel as float32 (JsonRowDesc::tlen == -1)
+      const char* txt = reinterpret_cast<const char*>(r.value);
+      const size_t tn = size_t(r.value_len);
+      const uint64_t at = align_up(vused, 32);
+      JsonRowDesc dsc;
+      if (at + tn + 32 > vcap) {
+        if (rows == 0) throw std::runtime_error("a single record exceeds the ring slot capacity");
+        slot_full = true;
+        return kStopBefore;
+      }
+      // one pass: classify + stream the text into the slot (the 32-byte read-ahead must stay
+      // inside the partition log's mapping); else scan, and copy below
+      const bool fused = uint64_t(r.value - log_of[cur_part]) + tn + 32 <= log_cap[cur_part];
+      int64_t cnt = fused ? json_scan_copy(txt, tn, vals + at) : json_scan_simple(txt, tn);
+      if (cnt >= 0) {
+        dsc.tlen = int32_t(tn);
+        nbytes = tn;
+      } else {
+        const int64_t room = at + 32 < vcap ? int64_t((vcap - at - 32) / 4) : 0;
+        cnt = parse_json_f32(txt, tn, reinterpret_cast<float*>(vals + at), room);
+        if (cnt == -2) {
+          if (rows == 0) throw std::runtime_error("a single record exceeds the ring slot capacity");
+          slot_full = true;
+          return kStopBefore;
+        }
+        if (cnt < 0) return bad(r, "value is not a flat numeric JSON array");
+        dsc.tlen = -1;
+        nbytes = 0;
+      }
+      if (cnt < spec.min_len) { touch(r); return kTake; }
+      len = cnt;
+      if (spec.max_len >= 0 && len > spec.max_len) {
+        if (!spec.truncate) { touch(r); return kTake; }
+        len = spec.max_len;
+      }
+      if (dsc.tlen < 0)
+        nbytes = uint64_t(len) * 4;
+      else if (!fused)
+        copy_to_slot(vals + at, r.value, tn);
+      if (cnt > INT32_MAX || at > UINT32_MAX) throw std::runtime_error("JSON row too large for the device parser");
+      dsc.off = uint32_t(at);
+      dsc.count = int32_t(cnt);
+      dsc.n_out = int32_t(len);
+      jrows[rows] = dsc;
+      vused = at + nbytes;
+      elems += len;
+      max_len = std::max(max_len, len);
+      touch(r);
+      ++rows;
+      return rows == B ? kTakeStop : kTake;
+    }
     if (spec.kind == kPackVarlen) {
       if (r.value_len % spec.elem_size) return bad(r, "value size is not a multiple of the element size");
       len = r.value_len / spec.elem_size;
@@ -406,6 +643,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   h->row_bytes = uint32_t(row_bytes);
   h->values_offset = values_off;
   h->values_bytes = gather ? uint64_t(rows) * 8 : (fixed ? uint64_t(rows) * row_bytes : vused);
+  if (json_text) h->values_bytes = align_up(vused, 16);  // the kernel reads whole 16-byte chunks
   h->payload_bytes = values_off + h->values_bytes;
   h->max_row_len = fixed ? spec.row_elems : max_len;
   h->total_elems = fixed ? rows * spec.row_elems : elems;

@@ -62,7 +62,11 @@ class Fetcher {
 };
 
 // ------------------------------------------------------------ packers
-enum PackKind : int { kPackFixed = 0, kPackVarlen = 1, kPackJsonF32 = 2, kPackGatherFixed = 3 };
+enum PackKind : int { kPackFixed = 0, kPackVarlen = 1, kPackJsonF32 = 2, kPackGatherFixed = 3, kPackJsonText = 4 };
+
+// kPackJsonText: JsonArray rows for the device parser (json_parse.hip).  The payload starts
+// with one JsonRowDesc per row (common.h); the values area (at values_offset) holds each
+// simple row's raw text, or the host-parsed float32 values of a row that is not simple.
 
 // kPackGatherFixed: the slot holds no values, only one uint64 per row locating the row's value
 // inside the broker log it was fetched from, (pidx << kGatherShift) | byte offset.  The main
@@ -98,6 +102,14 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t gslot, const PackSpec& sp
 // Numeric JSON array -> float32 (correctly rounded as Python float()+float32 cast).
 // Returns elements parsed, or -1 when the text is not a flat numeric array.
 int64_t parse_json_f32(const char* s, size_t n, float* out, int64_t cap);
+
+// Device-parse pre-scan: element count of a "simple" JSON number array (digits, '.', '-'
+// only, tokens <= 16 characters), or -1 if the row must be parsed on the host.
+// simd=false forces the scalar reference implementation (tests compare the two).
+int64_t json_scan_simple(const char* s, size_t n, bool simd = true);
+// The same verdict, fused with a streaming copy of the text to `dst` (32-byte aligned; src
+// readable and dst writable up to align_up(n, 32)).
+int64_t json_scan_copy(const char* s, size_t n, uint8_t* dst);
 // Element count of a flat numeric JSON array without converting (-1 if malformed).
 int64_t json_array_len(const char* s, size_t n);
 

@@ -93,6 +93,16 @@ PYBIND11_MODULE(_tkhip, m) {
       py::arg("rows"), py::arg("L"), py::arg("pad") = 0.0, py::arg("lengths") = 0, py::arg("mask") = 0,
       py::arg("stream") = 0);
 
+  m.def(
+      "launch_json_rows",
+      [](uintptr_t rows, uintptr_t vals, uintptr_t out, int dst_dt, int64_t n_rows, int64_t L, double pad,
+         uintptr_t lengths, uintptr_t mask, uintptr_t err, uintptr_t stream) {
+        launch_json_rows(ptr<const JsonRowDesc>(rows), ptr<const void>(vals), ptr<void>(out), dst_dt, n_rows, L, pad,
+                         ptr<int64_t>(lengths), ptr<uint8_t>(mask), ptr<int32_t>(err), stream_of(stream));
+      },
+      py::arg("rows"), py::arg("values"), py::arg("out"), py::arg("dst_dtype"), py::arg("n_rows"), py::arg("L"),
+      py::arg("pad") = 0.0, py::arg("lengths") = 0, py::arg("mask") = 0, py::arg("err") = 0, py::arg("stream") = 0);
+
   py::class_<Engine>(m, "Engine")
       .def(py::init<int, int, size_t, int, int>(), py::arg("device"), py::arg("n_slots"), py::arg("staging_bytes"),
            py::arg("n_streams") = 4, py::arg("mode") = int(kH2DDma))
@@ -212,6 +222,7 @@ PYBIND11_MODULE(_tkhip, m) {
              return l;
            })
       .def("deliver_last", [](MainDriver& d) { d.deliver(d.last); })
+      .def("parse_error", [](MainDriver& d) { return d.parse_error(); })
       .def("discard_last",
            [](MainDriver& d) {
              py::gil_scoped_release nogil;

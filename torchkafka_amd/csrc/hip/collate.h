@@ -8,6 +8,8 @@
 #include <utility>
 #include <vector>
 
+#include "common.h"
+
 namespace tkh {
 
 // Dense [rows, row] -> [rows, row] cast with optional fused (x - shift) * scale.
@@ -30,6 +32,13 @@ void launch_fixed_group(const void* const* srcs, int src_dt, void* const* dsts, 
 void launch_gather_group(const uint64_t* const* ents, int src_dt, void* const* dsts, int dst_dt, const int64_t* rows,
                          int n, const uint64_t* bases, int64_t row_bytes, const float* shift, const float* scale,
                          hipStream_t stream);
+
+// JSON text rows (tk::JsonRowDesc[n_rows] + values area, kPackJsonText) parsed on the
+// device -> padded [n_rows, L] float dtype; a row with a grammar error stores its index
+// into *err (host-mapped, may be null) and gets NaN for the bad numbers.
+using tk::JsonRowDesc;
+void launch_json_rows(const JsonRowDesc* rows, const void* vals, void* out, int dst_dt, int64_t n_rows, int64_t L,
+                      double pad, int64_t* lengths, uint8_t* mask, int32_t* err, hipStream_t stream);
 
 std::vector<std::pair<std::string, double>> api_bench(int device, int iters);
 

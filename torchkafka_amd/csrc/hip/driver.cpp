@@ -57,6 +57,10 @@ MainDriver::~MainDriver() {
     }
   }
   for (auto& f : fenced_) hipEventDestroy(std::get<0>(f));
+  if (perr_host_) {
+    hipDeviceSynchronize();  // no kernel may still write an error word
+    hipHostFree(perr_host_);
+  }
   for (auto e : event_pool_) hipEventDestroy(e);
 }
 
@@ -357,6 +361,7 @@ void MainDriver::finish_lockstep() {
 int MainDriver::next_slot(int64_t timeout_ms, SlotView* out) {
   release_completed();
   if (!fenced_.empty()) drain_fenced(false);
+  if (!parse_error_.empty()) return -4;
   if (ls_) return next_slot_lockstep(timeout_ms, out);
   for (;;) {
     // keep `prefetch` batches beyond the one handed out in flight to the device
@@ -471,12 +476,49 @@ void MainDriver::collate_fixed(const SlotView& v, hipStream_t stream, int dst_dt
 void MainDriver::collate_varlen(const SlotView& v, hipStream_t stream, int dst_dt, void* out, int64_t L, double pad,
                                 int64_t* lengths, uint8_t* mask) {
   bool record;
+  if (v.kind == tk::kPackJsonText) {
+    if (!perr_host_) {
+      void* h = nullptr;
+      if (hipHostMalloc(&h, kErrWords * sizeof(int32_t), hipHostMallocMapped) != hipSuccess)
+        throw std::runtime_error("driver: hipHostMalloc of the parse error words failed");
+      perr_host_ = static_cast<int32_t*>(h);
+      void* d = nullptr;
+      if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess)
+        throw std::runtime_error("driver: hipHostGetDevicePointer failed");
+      perr_dev_ = static_cast<int32_t*>(d);
+    }
+    // an error word is reused after kErrWords launches; its batch was checked long before
+    // (fenced batches are checked in order and the ring holds far fewer slots)
+    const int64_t idx = int64_t(perr_seq_++ % uint64_t(kErrWords));
+    perr_host_[idx] = -1;
+    note_handed(v.g, stream, &record);
+    eng_->collate_json(int(v.g), stream, v.values_offset, out, dst_dt, v.n_rows, L, pad, lengths, mask,
+                       perr_dev_ + idx, record);
+    last_perr_ = idx;
+    return;
+  }
   note_handed(v.g, stream, &record);
   eng_->collate_varlen(int(v.g), stream, v.values_offset, v.src_dtype, out, dst_dt, v.n_rows, L, pad, lengths, mask,
                        record);
 }
 
-void MainDriver::deliver(const SlotView& v) { delivered_ = v.wms; }
+void MainDriver::deliver(const SlotView& v) {
+  delivered_ = v.wms;
+  delivered_perr_ = v.kind == tk::kPackJsonText ? last_perr_ : -1;
+}
+
+bool MainDriver::check_parse_error(int64_t idx, const std::vector<tk::Watermark>& wms) {
+  if (idx < 0) return true;
+  const int32_t row = __atomic_load_n(perr_host_ + idx, __ATOMIC_ACQUIRE);
+  if (row < 0) return true;
+  std::string where;
+  for (const auto& w : wms)
+    where += (where.empty() ? "" : ", ") + std::string("partition index ") + std::to_string(w.pidx) + " offsets [" +
+             std::to_string(w.first_offset) + ", " + std::to_string(w.next_offset) + ")";
+  parse_error_ = "batch row " + std::to_string(row) + " is not a flat numeric JSON array (device parse; batch: " +
+                 where + ")";
+  return false;
+}
 
 void MainDriver::discard(const SlotView& v) {
   if (v.g < 0) return;
@@ -500,7 +542,9 @@ void MainDriver::stage_finished(int64_t index, std::vector<tk::Watermark>&& wms)
 
 void MainDriver::finish_delivered(hipStream_t fence) {
   if (delivered_.empty()) return;
-  if (commit_on_device_) {
+  const int64_t perr = delivered_perr_;
+  delivered_perr_ = -1;
+  if (commit_on_device_ || perr >= 0) {  // a device-parsed batch commits only once its kernel ran clean
     hipEvent_t ev;
     if (event_pool_.empty()) {
       if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
@@ -510,7 +554,7 @@ void MainDriver::finish_delivered(hipStream_t fence) {
       event_pool_.pop_back();
     }
     if (hipEventRecord(ev, fence) != hipSuccess) throw std::runtime_error("driver: hipEventRecord failed");
-    fenced_.emplace_back(ev, delivered_index_, std::move(delivered_));
+    fenced_.emplace_back(ev, delivered_index_, std::move(delivered_), perr);
   } else {
     stage_finished(delivered_index_, std::move(delivered_));
   }
@@ -518,7 +562,7 @@ void MainDriver::finish_delivered(hipStream_t fence) {
 }
 
 void MainDriver::drain_fenced(bool wait) {
-  while (!fenced_.empty()) {
+  while (!fenced_.empty() && parse_error_.empty()) {
     auto& f = fenced_.front();
     hipEvent_t ev = std::get<0>(f);
     if (wait) {
@@ -526,6 +570,7 @@ void MainDriver::drain_fenced(bool wait) {
     } else if (hipEventQuery(ev) != hipSuccess) {
       break;  // in order: a later batch is never committed before an earlier one
     }
+    if (!check_parse_error(std::get<3>(f), std::get<2>(f))) break;  // never committed
     stage_finished(std::get<1>(f), std::move(std::get<2>(f)));
     event_pool_.push_back(ev);
     fenced_.pop_front();
@@ -534,7 +579,7 @@ void MainDriver::drain_fenced(bool wait) {
 
 int MainDriver::commit_pending() {
   drain_fenced(false);
-  if (pending_.empty()) return 0;
+  if (pending_.empty()) return parse_error_.empty() ? 0 : -2;
   if (!broker_) throw std::runtime_error("DeviceLoader cannot commit: no group_id / broker");
   const int64_t t0 = tk::now_ns();
   entries_.clear();
@@ -550,6 +595,7 @@ int MainDriver::commit_pending() {
   }
   pending_.clear();
   if (commit_ns_.size() < (1u << 20)) commit_ns_.push_back(tk::now_ns() - t0);
+  if (!parse_error_.empty()) return -2;  // the batches before the bad one were committed
   return status;
 }
 

@@ -46,7 +46,8 @@ class MainDriver {
              int prefetch, bool in_order, int default_src_dt);
   ~MainDriver();
 
-  // Next batch slot (H2D issued).  Returns 1 (out filled), -1 timeout, -2 end of stream, -3 worker error.
+  // Next batch slot (H2D issued).  Returns 1 (out filled), -1 timeout, -2 end of stream, -3 worker error,
+  // -4 an earlier device-parsed batch was malformed (parse_error()).
   int next_slot(int64_t timeout_ms, SlotView* out);
   const std::string& error() const { return error_; }
 
@@ -54,6 +55,12 @@ class MainDriver {
                      const float* scale);
   void collate_varlen(const SlotView& v, hipStream_t stream, int dst_dt, void* out, int64_t L, double pad,
                       int64_t* lengths, uint8_t* mask);
+
+  // Device JSON parse (kPackJsonText): grammar errors found by the kernel.  A batch's error
+  // word is checked once its GPU work completed, before the batch can be committed; a bad
+  // batch stops the commits (commit_pending() returns -2, next_slot() -4) and parse_error()
+  // describes it.
+  const std::string& parse_error() const { return parse_error_; }
 
   void deliver(const SlotView& v);   // batch handed to the user
   void discard(const SlotView& v);   // consumed but not handed out (drop_last): free its slot
@@ -143,7 +150,15 @@ class MainDriver {
 
   void stage_finished(int64_t index, std::vector<tk::Watermark>&& wms);
   bool commit_on_device_ = false;
-  std::deque<std::tuple<hipEvent_t, int64_t, std::vector<tk::Watermark>>> fenced_;
+  // (event, batch index, watermarks, parse-error word index or -1)
+  std::deque<std::tuple<hipEvent_t, int64_t, std::vector<tk::Watermark>, int64_t>> fenced_;
+  static constexpr int64_t kErrWords = 4096;
+  int32_t* perr_host_ = nullptr;  // hipHostMalloc'ed, device-mapped error words (one per JSON launch)
+  int32_t* perr_dev_ = nullptr;
+  uint64_t perr_seq_ = 0;
+  int64_t last_perr_ = -1, delivered_perr_ = -1;
+  std::string parse_error_;
+  bool check_parse_error(int64_t idx, const std::vector<tk::Watermark>& wms);
   std::vector<hipEvent_t> event_pool_;
 
   struct Ticket {

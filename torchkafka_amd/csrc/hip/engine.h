@@ -45,6 +45,10 @@ class Engine {
                      int64_t row, const float* shift, const float* scale, bool record = true);
   void collate_varlen(int s, hipStream_t user, size_t values_offset, int src_dt, void* out, int dst_dt, int64_t rows,
                       int64_t L, double pad, int64_t* lengths, uint8_t* mask, bool record = true);
+  // kPackJsonText slot: rows parsed from JSON text on the device (json_parse.hip); a grammar
+  // error stores the row index into *err (host-mapped).
+  void collate_json(int s, hipStream_t user, size_t values_offset, void* out, int dst_dt, int64_t rows, int64_t L,
+                    double pad, int64_t* lengths, uint8_t* mask, int32_t* err, bool record = true);
   // Consecutive fixed-width slots collated by one kernel (collate.h launch_fixed_group);
   // the completion event of the last slot is recorded (it stands for all of them).
   void collate_fixed_group(const int* slots, int n, hipStream_t user, const size_t* values_offsets, int src_dt,

@@ -184,6 +184,16 @@ void Engine::collate_varlen(int s, hipStream_t user, size_t values_offset, int s
   if (record) finish(s, user);
 }
 
+void Engine::collate_json(int s, hipStream_t user, size_t values_offset, void* out, int dst_dt, int64_t rows,
+                          int64_t L, double pad, int64_t* lengths, uint8_t* mask, int32_t* err, bool record) {
+  check_slot(s);
+  const uint8_t* base = src_base(s);
+  begin(s, user);
+  launch_json_rows(reinterpret_cast<const JsonRowDesc*>(base), base + values_offset, out, dst_dt, rows, L, pad,
+                   lengths, mask, err, user);
+  if (record) finish(s, user);
+}
+
 void Engine::copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes) {
   check_slot(s);
   begin(s, user);

@@ -1,0 +1,297 @@
+// gfx950 JSON-array parse + pad/stack + cast: the device half of the JsonArray
+// schema's "device parse" mode (the reference's README decodes
+// each record with `json.loads(record.value)` in Python, README.md:54,74).
+//
+// The worker no longer parses numbers.  It only frames each record
+// (Fetcher::fill_slot, kPackJsonText): an AVX2 pre-scan counts the elements
+// and checks the row is "simple" (numbers made of [0-9.-] only, every token at
+// most 16 characters), then copies the raw text into the pinned slot.  Rows
+// that are not simple (exponents, NaN/Infinity, long tokens, anything odd) are
+// parsed on the host as before and ride in the same slot as float32.
+//
+// One 256-thread block (4 waves) owns one row.  The row's text goes through
+// LDS in 2 KiB windows (one 16-byte load per thread), then:
+//   1. token starts: thread t classifies its 8 contiguous bytes in registers
+//      -> an 8-bit start mask; a block-wide exclusive scan of the popcounts
+//      (wave shuffles + per-wave totals) gives every token its index, and its
+//      window-relative start goes to an LDS table;
+//   2. parse: thread t parses tokens t, t+256, ... (one per thread for a
+//      typical window) from registers loaded off LDS with the host
+//      parser's grammar and arithmetic (Clinger's fast path in fp64: both
+//      operands exact, one correctly rounded IEEE op; u64 -> f64 for plain
+//      integers), then f64 -> f32 -> destination dtype, bit-exact with
+//      Python float() + torch's casts; consecutive lanes store consecutive
+//      columns (coalesced);
+//   3. a token cut by the window end restarts the next window (16-byte
+//      aligned at or below its start).
+// Grammar errors (e.g. "1..2", "[1,,2]": they pass the worker's character
+// scan) write the row index into a host-mapped error word; the step driver
+// checks it before the batch is committed and raises CorruptRecordException.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+#include "collate.h"
+#include "dtypes.h"
+
+namespace tkh {
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kThreads = 256;                 // one block (4 waves) per row
+constexpr int kWaves = kThreads / kWave;
+constexpr int kWin = 2048;                    // bytes of text per window (one 8-byte slice per thread)
+constexpr int kLaneBytes = kWin / kThreads;   // 8 contiguous bytes classified per thread
+constexpr int kMaxTok = kWin / 2 + 1;         // a token needs >= 1 char and 1 separator
+
+__device__ __forceinline__ bool is_sep(uint32_t c) {
+  return c == ',' || c == ' ' || c == '[' || c == ']' || c == '\n' || c == '\t' || c == '\r';
+}
+
+__device__ __constant__ double kP10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                           1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+template <typename D>
+__device__ __forceinline__ D pad_value(float p) { return Store<D>::cvt(p); }
+
+// The token starting at window byte s, parsed from registers: the 32 LDS bytes from
+// s & ~15 (two ds_read_b128) are funnel-shifted so that t[0..4] hold bytes s .. s+19, and a
+// fully unrolled walk over at most 17 bytes (a simple row's number has <= 16 characters,
+// then a separator) runs the host parser's grammar with no dependent memory access.
+// `avail` = bytes of the window from s on.  Returns 1 ok, 0 grammar error, 2 cut by the
+// window end (parsed again in the next window).
+__device__ __forceinline__ int parse_token_regs(const uint8_t* buf, int s, int avail, bool last_window, float* out) {
+  const int A = s & ~15;
+  const uint4 lo = *reinterpret_cast<const uint4*>(buf + A);
+  const uint4 hi = *reinterpret_cast<const uint4*>(buf + A + 16);
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  const int o = s - A, q = o >> 2;
+  const uint32_t sh = uint32_t(o & 3) * 8u;
+  uint32_t t[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    // dwords q+k and q+k+1 (q <= 3, so at most w[7] and a dummy)
+    const uint32_t a0 = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
+    const uint32_t a1 = q == 0 ? w[k + 1] : q == 1 ? w[k + 2] : q == 2 ? w[k + 3] : (k + 4 < 8 ? w[k + 4] : 0u);
+    t[k] = sh ? (a0 >> sh) | (a1 << (32u - sh)) : a0;
+  }
+  bool neg = false, dot = false, frac = false, any = false, ended = false, bad = false, truncated = false;
+  uint32_t endc = 0;
+  int endj = 17;
+  uint64_t mant = 0;
+  int nd = 0, exp10 = 0;
+#pragma unroll
+  for (int j = 0; j < 17; ++j) {
+    const uint32_t c = (t[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
+    if (!ended) {
+      if (j >= avail) {
+        ended = true;
+        endj = j;
+        endc = 0x100u;  // window end
+      } else if (j == 0 && c == '-') {
+        neg = true;
+      } else if (c - '0' <= 9u) {
+        const uint32_t dd = c - '0';
+        any = true;
+        if (dot) frac = true;
+        if (mant == 0 && dd == 0) {
+          if (dot) --exp10;
+        } else if (nd < 19) {
+          mant = mant * 10 + dd;
+          ++nd;
+          if (dot) --exp10;
+        } else {
+          truncated = true;
+          if (!dot) ++exp10;
+        }
+      } else if (c == '.' && !dot) {
+        dot = true;
+      } else {
+        ended = true;
+        endj = j;
+        endc = c;
+      }
+    }
+  }
+  if (!ended) return 0;  // longer than a simple number
+  if (endc == 0x100u) {
+    if (!last_window) return 2;
+    return 0;  // text ended inside a number
+  }
+  (void)endj;
+  bad = !any || (dot && !frac) || !is_sep(endc);
+  if (bad) return 0;
+  if (mant == 0 && !dot) neg = false;  // "-0" is the JSON integer 0: +0.0 after Python's float()
+  double v;
+  if (!truncated && mant <= (uint64_t(1) << 53) && exp10 >= -22 && exp10 <= 22) {
+    v = exp10 < 0 ? double(mant) / kP10[-exp10] : double(mant) * kP10[exp10];
+  } else if (!truncated && exp10 == 0) {
+    v = double(mant);  // one rounding: the hi/lo u32 halves convert exactly, the add rounds
+  } else {
+    return 0;  // the worker's pre-scan never sends such tokens
+  }
+  *out = float(neg ? -v : v);
+  return 1;
+}
+
+template <typename D>
+__global__ __launch_bounds__(kThreads) void json_rows_kernel(const JsonRowDesc* __restrict__ rows,
+                                                             const uint8_t* __restrict__ vals, D* __restrict__ out,
+                                                             int64_t L, float pad, int64_t* __restrict__ lengths,
+                                                             uint8_t* __restrict__ mask, int32_t* __restrict__ err) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kWin + 32];  // + the 32-byte token reads
+  __shared__ uint16_t starts[kMaxTok];
+  __shared__ int s_wsum[kWaves];
+  __shared__ int s_cut, s_bad;
+
+  const int64_t r = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  const JsonRowDesc d = rows[r];
+  const int64_t n_out = d.n_out < L ? d.n_out : L;
+  D* orow = out + r * L;
+  bool bad = false;  // block-uniform: only read after a barrier
+
+  if (d.tlen < 0) {
+    // parsed on the host (not a simple row): float32 values
+    const float* f = reinterpret_cast<const float*>(vals + d.off);
+    for (int64_t k = tid; k < n_out; k += kThreads) orow[k] = Store<D>::cvt(f[k]);
+  } else {
+    const uint8_t* text = vals + d.off;  // 32-byte aligned (worker)
+    const int T = d.tlen;
+    int pend = 0;    // tokens starting before pend are done; text[pend-1] is a separator or pend starts a token
+    int64_t k0 = 0;  // index of the first token of this window
+    if (tid == 0) s_bad = 0;
+    while (pend < T) {
+      const int base = pend & ~15;
+      const int wlen = T - base < kWin ? T - base : kWin;
+      const bool last = base + wlen >= T;
+      // stage the window: one 16-byte load per thread for the first 128 threads
+      if (tid * 16 < wlen)
+        *reinterpret_cast<uint4*>(buf + tid * 16) = *reinterpret_cast<const uint4*>(text + base + tid * 16);
+      if (tid == 0) s_cut = kMaxTok;
+      __syncthreads();
+      // 1. token starts in this thread's 8 bytes, classified in registers.  A byte is a number
+      // character iff it lies in '-'..'9' (0x2D-0x39); simple rows hold nothing else but
+      // separators, and anything odd fails the parse below.
+      const int b0 = tid * kLaneBytes;
+      const uint2 cw = *reinterpret_cast<const uint2*>(buf + b0);
+      uint32_t tokm = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t c = ((j < 4 ? cw.x : cw.y) >> ((j & 3) * 8)) & 0xFFu;
+        tokm |= uint32_t(c - 0x2Du <= 0x0Cu) << j;
+      }
+      const int lim = wlen - b0;  // valid bytes of this thread (may be <= 0 or > 8)
+      if (lim < 8) tokm &= lim <= 0 ? 0u : ((1u << lim) - 1u);
+      const uint32_t pc = b0 > 0 && b0 <= wlen ? buf[b0 - 1] : uint32_t(',');
+      const uint32_t prev_tok = uint32_t(pc - 0x2Du <= 0x0Cu);
+      uint32_t m = tokm & ~((tokm << 1) | prev_tok);
+      // only tokens at or after pend (pend itself starts a token when it is a number character)
+      const int rel = pend - base - b0;  // pend relative to this thread's first byte
+      if (rel > 0) {
+        m &= rel >= 8 ? 0u : ~((1u << rel) - 1u);
+        if (rel < 8) m |= tokm & (1u << rel);
+      } else if (rel == 0) {
+        m |= tokm & 1u;
+      }
+      // block-wide exclusive scan of the start counts: wave scan + per-wave totals
+      const int cnt = __popc(m);
+      int incl = cnt;
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const int t = __shfl_up(incl, o, kWave);
+        if (lane >= o) incl += t;
+      }
+      if (lane == kWave - 1) s_wsum[wid] = incl;
+      __syncthreads();
+      int woff = 0, total = 0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) {
+        const int ws = s_wsum[w];
+        woff += w < wid ? ws : 0;
+        total += ws;
+      }
+      int idx = woff + incl - cnt;
+      while (m) {
+        const int j = __ffs(m) - 1;
+        m &= m - 1;
+        starts[idx++] = uint16_t(b0 + j);
+      }
+      __syncthreads();
+      // 2. parse; only the window's last token can be cut
+      bool lbad = false;
+      for (int t = tid; t < total; t += kThreads) {
+        float v;
+        const int st0 = starts[t];
+        const int rc = parse_token_regs(buf, st0, wlen - st0, last, &v);
+        if (rc == 2) {
+          s_cut = t;
+        } else {
+          if (rc == 0) {
+            lbad = true;
+            v = __builtin_nanf("");
+          }
+          const int64_t k = k0 + t;
+          if (k < n_out) orow[k] = Store<D>::cvt(v);
+        }
+      }
+      if (lbad) s_bad = 1;
+      __syncthreads();
+      const int cut = s_cut;
+      if (cut < total) {
+        if (base + int(starts[cut]) == pend) {  // one token longer than a window: no progress possible
+          bad = true;
+          break;
+        }
+        k0 += cut;
+        pend = base + starts[cut];
+      } else {
+        k0 += total;
+        pend = base + wlen;
+      }
+      __syncthreads();  // buf/starts/s_wsum are rewritten by the next window
+    }
+    bad = bad || s_bad != 0 || k0 != d.count;
+  }
+  // padding, lengths, mask
+  for (int64_t k = n_out + tid; k < L; k += kThreads) orow[k] = pad_value<D>(pad);
+  if (mask) {
+    uint8_t* mrow = mask + r * L;
+    for (int64_t k = tid; k < L; k += kThreads) mrow[k] = uint8_t(k < n_out);
+  }
+  if (lengths && tid == 0) lengths[r] = n_out;
+  if (err && bad && tid == 0) *err = int32_t(r);
+}
+
+template <typename D>
+void launch_json_t(const JsonRowDesc* rows, const uint8_t* vals, void* out, int64_t n_rows, int64_t L, float pad,
+                   int64_t* lengths, uint8_t* mask, int32_t* err, hipStream_t stream) {
+  hipLaunchKernelGGL((json_rows_kernel<D>), dim3(unsigned(n_rows)), dim3(kThreads), 0, stream, rows, vals,
+                     static_cast<D*>(out), L, pad, lengths, mask, err);
+}
+
+}  // namespace
+
+void launch_json_rows(const JsonRowDesc* rows, const void* vals, void* out, int dst_dt, int64_t n_rows, int64_t L,
+                      double pad, int64_t* lengths, uint8_t* mask, int32_t* err, hipStream_t stream) {
+  if (n_rows == 0) return;
+  if (n_rows > INT32_MAX) throw std::invalid_argument("json collate: too many rows");
+  if (reinterpret_cast<uintptr_t>(vals) % 16 || reinterpret_cast<uintptr_t>(rows) % 16)
+    throw std::invalid_argument("json collate: slot regions must be 16-byte aligned");
+  const auto* v = static_cast<const uint8_t*>(vals);
+  const float p = float(pad);
+  switch (dst_dt) {
+    case kF32: launch_json_t<float>(rows, v, out, n_rows, L, p, lengths, mask, err, stream); break;
+    case kF16: launch_json_t<_Float16>(rows, v, out, n_rows, L, p, lengths, mask, err, stream); break;
+    case kBF16: launch_json_t<__bf16>(rows, v, out, n_rows, L, p, lengths, mask, err, stream); break;
+    case kFP8E4M3: launch_json_t<fp8e4m3>(rows, v, out, n_rows, L, p, lengths, mask, err, stream); break;
+    default: throw std::invalid_argument("json collate: destination must be a float dtype");
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("json collate launch: ") + hipGetErrorString(e));
+}
+
+}  // namespace tkh

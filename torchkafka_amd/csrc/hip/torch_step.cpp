@@ -127,6 +127,57 @@ void register_torch_step(py::module_& m) {
     return res;
   });
 
+  // Var-len / JSON fast path: one call per batch -- finish + commit the previous batch, take
+  // the next slot, allocate [rows, L] + lengths (+ mask) on the current stream, launch the
+  // pad/stack (or JSON parse) kernel and mark the batch delivered.
+  // -> (r, commit_status, out | None, lengths | None, mask | None); r as next_slot().
+  cls.def(
+      "varlen_next",
+      [](MainDriver& d, int device, int dst_dt, int64_t pad_to, int64_t pad_multiple, double pad, bool want_mask,
+         bool auto_commit, int64_t timeout_ms) -> py::tuple {
+        const int64_t t0 = tk::now_ns();
+        const auto dev = c10::DeviceIndex(device);
+        hipStream_t stream = c10::hip::getCurrentHIPStream(dev).stream();
+        int cs = 0;
+        int r;
+        int64_t t1, t2;
+        {
+          py::gil_scoped_release nogil;
+          d.finish_delivered(stream);
+          if (auto_commit) cs = d.commit_pending();
+          t1 = tk::now_ns();
+          r = d.next_slot(timeout_ms, &d.last);
+          t2 = tk::now_ns();
+        }
+        d.ph_commit_ns_ += t1 - t0;
+        d.ph_next_ns_ += t2 - t1;
+        if (r != 1) return py::make_tuple(r, cs, py::none(), py::none(), py::none());
+        const SlotView& v = d.last;
+        int64_t L = pad_to >= 0 ? pad_to : v.max_row_len;
+        if (pad_to < 0 && pad_multiple > 1) L = (L + pad_multiple - 1) / pad_multiple * pad_multiple;
+        const int64_t n = int64_t(v.n_rows);
+        at::Tensor out = at::empty({n, L}, at::TensorOptions().dtype(scalar_type_of(dst_dt)).device(at::kCUDA, dev));
+        at::Tensor lengths = at::empty({n}, at::TensorOptions().dtype(at::kLong).device(at::kCUDA, dev));
+        at::Tensor mask;
+        if (want_mask) mask = at::empty({n, L}, at::TensorOptions().dtype(at::kBool).device(at::kCUDA, dev));
+        {
+          py::gil_scoped_release nogil;
+          d.collate_varlen(v, stream, dst_dt, out.data_ptr(), L, pad, lengths.data_ptr<int64_t>(),
+                           want_mask ? static_cast<uint8_t*>(mask.data_ptr()) : nullptr);
+          d.deliver(v);
+        }
+        d.ph_launch_ns_ += tk::now_ns() - t2;
+        ++d.ph_steps_;
+        ++d.fast_batches_;
+        d.fast_records_ += n;
+        d.fast_ns_ += tk::now_ns() - t0;
+        py::object m = want_mask ? py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(mask))) : py::none();
+        return py::make_tuple(r, cs, py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(out))),
+                              py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(lengths))), m);
+      },
+      py::arg("device"), py::arg("dst_dt"), py::arg("pad_to"), py::arg("pad_multiple"), py::arg("pad"),
+      py::arg("want_mask"), py::arg("auto_commit"), py::arg("timeout_ms"));
+
   m.def(
       "step_fixed_tensor",
       [](MainDriver& d, int device, std::vector<int64_t> shape, int dst_dt, int64_t row, uintptr_t shift,

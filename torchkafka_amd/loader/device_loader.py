@@ -38,7 +38,7 @@ from typing import NamedTuple
 
 import torch
 
-from ..client.errors import COMMIT_FAILED_ERRORS
+from ..client.errors import COMMIT_FAILED_ERRORS, CorruptRecordException
 from ..ops.collate import CODE_DTYPE, DTYPE_CODE, FLOAT_DTYPES, _stream_ptr, normalize_params
 from ..ops.native import core, hip
 from ..parallel.sharding import dist_rank_world
@@ -293,7 +293,7 @@ class DeviceLoader:
                  group_id: str | None = None, bootstrap_servers=None, base_seed: int | None = None,
                  lockstep_depth: int = 2, h2d: str = "auto", copy_streams: int = 4,
                  event_every: int | None = None, numa_bind: bool = True, coalesce: int = 8,
-                 coalesce_wait_us: int = 50,
+                 coalesce_wait_us: int = 50, json_parse: str = "auto",
                  lockstep_timeout: float = 600.0):
         if batch_size < 1:
             raise ValueError("batch_size must be >= 1")
@@ -334,6 +334,9 @@ class DeviceLoader:
         if h2d not in ("auto", "dma", "zerocopy", "direct"):
             raise ValueError("h2d must be 'auto', 'dma' (hipMemcpyAsync on side streams), 'zerocopy' or 'direct'")
         self.h2d = h2d
+        if json_parse not in ("auto", "device", "host"):
+            raise ValueError("json_parse must be 'auto', 'device' (gfx950 parse kernel) or 'host' (worker parse)")
+        self.json_parse = json_parse
         self.copy_streams = max(1, int(copy_streams))
         self.event_every = None if event_every is None else max(1, int(event_every))
         self.numa_bind = bool(numa_bind)
@@ -391,6 +394,11 @@ class DeviceLoader:
     def _resolve_h2d(self, slot_payload_bytes: int) -> str:
         if self.h2d != "auto":
             return self.h2d
+        if self._json_device():
+            # JSON text batches are a few hundred KiB whatever the slot capacity; the parse kernel
+            # reads each row once, so zero-copy beats a DMA + HBM re-read (14.3 vs 12.6 M rec/s,
+            # BASELINE config 4, profiles/r01_s5)
+            return "zerocopy"
         return "zerocopy" if slot_payload_bytes <= self.ZERO_COPY_MAX_BYTES else "dma"
 
     def _default_src_code(self) -> int:
@@ -420,7 +428,25 @@ class DeviceLoader:
     def _worker_cfg(self) -> dict:
         return {"batch_size": self.batch_size, "sharding": self.sharding, "rank": self.rank,
                 "world_size": self.world_size, "native": self.native, "base_seed": self.base_seed,
-                "gather": self._direct()}
+                "gather": self._direct(), "json_device": self._json_device()}
+
+    def _json_device(self) -> bool:
+        """JsonArray records parsed by the gfx950 kernel (json_parse.hip) instead of the workers.
+
+        The workers then only frame each record (AVX2 element count + copy of the text).  A
+        malformed row that passes their character scan (e.g. ``[1,,2]``) is found by the
+        kernel: the batch is never committed and ``CorruptRecordException`` is raised one
+        step later, when the batch's GPU work has completed.  ``skip_bad=True`` needs the
+        row dropped from its batch, which only the host parser can do, so 'auto' picks
+        the host parser there.
+        """
+        s = self.schema
+        if getattr(s, "kind", None) != 2 or self.json_parse == "host":
+            return False
+        ok = self.device.type == "cuda" and self.native and not getattr(s, "skip_bad", False)
+        if self.json_parse == "device" and not ok:
+            raise ValueError("json_parse='device' needs a CUDA device, native=True and skip_bad=False")
+        return ok
 
     def _direct(self) -> bool:
         """h2d='direct': fixed-width rows gathered by the kernel straight from the pinned broker logs."""
@@ -475,6 +501,8 @@ class DeviceLoader:
         if run.driver is not None:
             if self._fast_path_ok() and not _roctx_enabled():
                 yield from self._iterate_fast(run, auto_commit)
+            elif self._varlen_fast_ok():
+                yield from self._iterate_varlen_fast(run, auto_commit)
             else:
                 yield from self._iterate_driver(run, auto_commit)
             return
@@ -568,19 +596,80 @@ class DeviceLoader:
                     yield item[0]
             completed = True
         finally:
-            drv.finish_delivered(_stream_ptr(self.device))
-            if completed:
-                drv.finish_lockstep()
-            drv.drain_fenced(True)
-            if completed and auto_commit:
-                self._log_commit(drv.commit_pending(), debug)
-            elif not auto_commit:
-                # manual mode: keep every yielded batch committable by DeviceLoader.commit()
-                pend = drv.take_pending()
-                if pend:
-                    self._pending_wms.append(([(p, 0, o, 0) for p, o in pend], None))
-            self._absorb_driver_stats(drv)
-            run.close()
+            try:
+                drv.finish_delivered(_stream_ptr(self.device))
+                if completed:
+                    drv.finish_lockstep()
+                drv.drain_fenced(True)
+                if completed and auto_commit:
+                    self._log_commit(drv.commit_pending(), debug)
+                elif not auto_commit:
+                    # manual mode: keep every yielded batch committable by DeviceLoader.commit()
+                    pend = drv.take_pending()
+                    if pend:
+                        self._pending_wms.append(([(p, 0, o, 0) for p, o in pend], None))
+            finally:
+                self._absorb_driver_stats(drv)
+                run.close()
+
+    def _varlen_fast_ok(self) -> bool:
+        s = self.schema
+        return (s is not None and getattr(s, "kind", None) in (1, 2) and self.native and not self.return_info
+                and not self.drop_last and not _roctx_enabled())
+
+    def _iterate_varlen_fast(self, run: _Run, auto_commit: bool):
+        """Var-len / JSON GPU iteration, one native call per batch (MainDriver.varlen_next): finish +
+        commit the previous batch, take the next slot, allocate the padded batch on the current
+        stream and launch its pad/stack (or JSON parse) kernel."""
+        drv = run.driver
+        debug = _ds_logger.isEnabledFor(logging.DEBUG)
+        src = CODE_DTYPE[self._default_src_code()]
+        dst_dt = self._out_dtype(src)
+        if (dst_dt in FLOAT_DTYPES) != (src in FLOAT_DTYPES) and src in FLOAT_DTYPES:
+            raise TypeError(f"cannot collate {src} records to {dst_dt}")
+        args = (self.device.index, DTYPE_CODE[dst_dt], -1 if self.pad_to is None else int(self.pad_to),
+                self.pad_multiple, float(self.pad_value), bool(self.return_mask), auto_commit, 100)
+        step = drv.varlen_next
+        want_mask = self.return_mask
+        completed = False
+        try:
+            wait_since = None
+            while True:
+                r, cs, out, lengths, mask = step(*args)
+                if cs:
+                    self._log_commit(cs, debug)
+                if r == 1:
+                    wait_since = None
+                    yield (out, lengths, mask) if want_mask else (out, lengths)
+                elif r == -2:
+                    break
+                elif r == -3:
+                    raise WorkerError(drv.error())
+                elif r == -4:
+                    raise CorruptRecordException(drv.parse_error())
+                else:  # -1: nothing within the poll slice
+                    run._check_workers_native()
+                    if self.timeout > 0:
+                        now = time.monotonic()
+                        wait_since = now if wait_since is None else wait_since
+                        if now - wait_since > self.timeout:
+                            raise TimeoutError(f"DeviceLoader timed out after {self.timeout}s waiting for a batch")
+            completed = True
+        finally:
+            try:
+                drv.finish_delivered(_stream_ptr(self.device))
+                if completed:
+                    drv.finish_lockstep()
+                drv.drain_fenced(True)
+                if completed and auto_commit:
+                    self._log_commit(drv.commit_pending(), debug)
+                elif not auto_commit:
+                    pend = drv.take_pending()
+                    if pend:
+                        self._pending_wms.append(([(p, 0, o, 0) for p, o in pend], None))
+            finally:
+                self._absorb_driver_stats(drv)
+                run.close()
 
     def _iterate_fast(self, run: _Run, auto_commit: bool):
         """Fixed-width GPU iteration: each batch is ONE argument-free native call (finish + commit
@@ -687,6 +776,8 @@ class DeviceLoader:
                     raise TimeoutError(f"DeviceLoader timed out after {self.timeout}s waiting for a batch")
 
     def _log_commit(self, status: int, debug: bool) -> None:
+        if status == -2:  # a device-parsed batch was malformed: it (and what follows) stays uncommitted
+            raise CorruptRecordException(self._run.driver.parse_error())
         if status == -1:
             _ds_logger.error("Commit failed.")
         elif status == 1 and debug:
@@ -762,6 +853,8 @@ class DeviceLoader:
                 return None
             if r == -3:
                 raise WorkerError(drv.error())
+            if r == -4:
+                raise CorruptRecordException(drv.parse_error())
             if r == -1:
                 run._check_workers_native()
                 if self.timeout > 0 and time.perf_counter_ns() - t0 > self.timeout * 1e9:

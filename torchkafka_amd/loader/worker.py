@@ -112,6 +112,8 @@ def _native_loop(ring, worker_id, spw, consumer, schema, cfg, state) -> None:
     from ..client.errors import OffsetOutOfRangeError
 
     kind, elem, row_elems, min_len, max_len, trunc, skip_bad = schema.native_spec()
+    if kind == core().PACK_JSON_F32 and cfg.get("json_device"):
+        kind = core().PACK_JSON_TEXT  # frame + copy the text; the gfx950 kernel parses it
     bs = int(cfg["batch_size"])
     timeout = _consumer_timeout_ms(consumer)
     fetcher = consumer._fetcher
