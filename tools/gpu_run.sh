@@ -22,6 +22,9 @@ for s in $STEPS; do
     pytestloader) step pytest_loader 300 python -u -m pytest tests/test_gpu_loader.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     pytestjson) step pytest_json 300 python -u -m pytest tests/test_gpu_json_parse.py tests/test_gpu_loader.py -k json -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     config4zc) step config4_zc 300 python benchmarks/config4_json_varlen.py --h2d zerocopy ;;
+    config4w8) step config4_w8 300 python benchmarks/config4_json_varlen.py --workers 8 ;;
+    config4w6) step config4_w6 300 python benchmarks/config4_json_varlen.py --workers 6 ;;
+    pmcjson) (cd /tmp && export TMPDIR=/tmp && step pmc_json 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_json" -o run -- python3 "$OLDPWD/benchmarks/config4_json_varlen.py" --steps 100 --warmup 10) || exit $? ;;
     config4host) step config4_host 300 python benchmarks/config4_json_varlen.py --json-parse host ;;
     pytest) step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     nccl)   step nccl_probe 120 python tools/nccl_probe.py ;;
