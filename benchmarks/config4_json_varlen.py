@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--json-parse", default="auto", choices=["auto", "device", "host"])
     ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy"])
+    ap.add_argument("--slots-per-worker", type=int, default=None)
+    ap.add_argument("--event-every", type=int, default=None)
+    ap.add_argument("--prefetch", type=int, default=2)
     args = ap.parse_args()
 
     import torch
@@ -51,7 +54,8 @@ def main():
         b.fill("json", per_part, "json_f32", size=args.min_len, max_size=args.max_len, threads=args.partitions)
         fill_s = time.perf_counter() - t
         dl = DeviceLoader(Json.placeholder(), B, num_workers=args.workers, device=args.device, dtype=torch.bfloat16,
-                          json_parse=args.json_parse, h2d=args.h2d,
+                          json_parse=args.json_parse, h2d=args.h2d, slots_per_worker=args.slots_per_worker,
+                          event_every=args.event_every, prefetch=args.prefetch,
                           worker_init_fn=Json.init_worker("json", bootstrap_servers=url, group_id="cfg4",
                                                           auto_offset_reset="earliest"))
         it = iter(auto_commit(dl))

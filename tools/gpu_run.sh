@@ -25,6 +25,11 @@ for s in $STEPS; do
     config4w8) step config4_w8 300 python benchmarks/config4_json_varlen.py --workers 8 ;;
     config4w6) step config4_w6 300 python benchmarks/config4_json_varlen.py --workers 6 ;;
     pmcjson) (cd /tmp && export TMPDIR=/tmp && step pmc_json 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_json" -o run -- python3 "$OLDPWD/benchmarks/config4_json_varlen.py" --steps 100 --warmup 10) || exit $? ;;
+    config4s8) step config4_s8 300 python benchmarks/config4_json_varlen.py --slots-per-worker 8 ;;
+    config4e1) step config4_e1 300 python benchmarks/config4_json_varlen.py --event-every 1 ;;
+    config4s8e1) step config4_s8e1 300 python benchmarks/config4_json_varlen.py --slots-per-worker 8 --event-every 1 ;;
+    config4p0) step config4_p0 300 python benchmarks/config4_json_varlen.py --prefetch 0 --event-every 1 ;;
+    config4nofence) TORCHKAFKA_EXP_NO_PARSE_FENCE=1 step config4_nofence 300 python benchmarks/config4_json_varlen.py ;;
     config4host) step config4_host 300 python benchmarks/config4_json_varlen.py --json-parse host ;;
     pytest) step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     nccl)   step nccl_probe 120 python tools/nccl_probe.py ;;
@@ -79,6 +84,7 @@ for s in $STEPS; do
     profcopy) (cd /tmp && export TMPDIR=/tmp && step profcopy 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profcopy" -o run -- python3 "$OLDPWD/bench.py" --steps 1000) || exit $? ;;
     profnocrc) (cd /tmp && export TMPDIR=/tmp && step profnocrc 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profnocrc" -o run -- python3 "$OLDPWD/bench.py" --steps 2000 --no-crc --stats) || exit $? ;;
     proflong) (cd /tmp && export TMPDIR=/tmp && step proflong 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/proflong" -o run -- python3 "$OLDPWD/bench.py" --steps 2000 --stats) || exit $? ;;
+    profc4t) (cd /tmp && export TMPDIR=/tmp && step profc4t 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/profc4t" -o run -- python3 "$OLDPWD/benchmarks/config4_json_varlen.py" --steps 300) || exit $? ;;
     profc4) (cd /tmp && export TMPDIR=/tmp && step profc4 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profc4" -o run -- python3 "$OLDPWD/benchmarks/config4_json_varlen.py" --steps 300) || exit $? ;;
     prof)   (cd /tmp && export TMPDIR=/tmp && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$OLDPWD/bench.py" --steps 200) || exit $? ;;
   esac

@@ -121,6 +121,7 @@ bool Ring::worker_acquire(uint32_t worker, uint32_t i, int64_t timeout_ms) {
     uint32_t st = s->state.load(std::memory_order_acquire);
     if (st == kSlotFree) {
       s->state.store(kSlotFilling, std::memory_order_relaxed);
+      s->t_acquire_wait_ns = now_ns() - start;
       return true;
     }
     const int64_t now = now_ns();

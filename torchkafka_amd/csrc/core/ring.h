@@ -52,6 +52,7 @@ struct alignas(64) SlotHeader {
   int64_t n_scanned;       // records consumed incl. skipped ones
   int64_t t_fill_start_ns;
   int64_t t_ready_ns;
+  int64_t t_acquire_wait_ns;  // how long the worker waited for this slot to come back FREE
   uint32_t err_len;
   uint32_t row_bytes;      // fixed-width: bytes per row
   int32_t src_dtype;       // element dtype code of the payload (-1: decided by the loader's schema)

@@ -258,6 +258,8 @@ PYBIND11_MODULE(_tkhip, m) {
              s["blocked_ns"] = d.blocked_ns_;
              s["blocked_calls"] = d.blocked_calls_;
              s["ready_age_ns"] = d.ready_age_ns_;
+             s["worker_idle_ns"] = d.worker_idle_ns_;
+             s["worker_slot_wait_ns"] = d.worker_slot_wait_ns_;
              s["phase_commit_ns"] = d.ph_commit_ns_;
              s["phase_next_ns"] = d.ph_next_ns_;
              s["phase_launch_ns"] = d.ph_launch_ns_;

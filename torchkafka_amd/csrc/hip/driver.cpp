@@ -56,7 +56,8 @@ MainDriver::~MainDriver() {
     } catch (...) {
     }
   }
-  for (auto& f : fenced_) hipEventDestroy(std::get<0>(f));
+  for (auto& f : fenced_)
+    if (std::get<0>(f)) hipEventDestroy(std::get<0>(f));
   if (perr_host_) {
     hipDeviceSynchronize();  // no kernel may still write an error word
     hipHostFree(perr_host_);
@@ -81,7 +82,11 @@ void MainDriver::release_completed_impl() {
     size_t e = k;
     while (e < handed_.size() && !handed_[e].ev) ++e;  // next slot with an event
     if (e == handed_.size() || !eng_->slot_done(int(handed_[e].g))) break;
-    for (; k <= e; ++k, ++released_) ring_->main_release(uint32_t(handed_[k].g));
+    for (; k <= e; ++k, ++released_) {
+      const int64_t pe = handed_[k].perr;
+      if (pe >= 0) perr_state_[size_t(pe)] = __atomic_load_n(perr_host_ + pe, __ATOMIC_ACQUIRE) < 0 ? 1 : 2;
+      ring_->main_release(uint32_t(handed_[k].g));
+    }
   }
   if (k) handed_.erase(handed_.begin(), handed_.begin() + long(k));
 }
@@ -169,6 +174,15 @@ int MainDriver::poll_one_impl(bool block, int64_t timeout_ms) {
     }
     fill_ns_ += h->t_ready_ns - h->t_fill_start_ns;
     ready_age_ns_ += tk::now_ns() - h->t_ready_ns;
+    {
+      // worker idle: from its previous publish to the start of this fill (waiting for a FREE
+      // slot, plus its per-batch Python work)
+      if (last_ready_.size() <= h->worker) last_ready_.resize(h->worker + 1, 0);
+      int64_t& lr = last_ready_[h->worker];
+      if (lr > 0 && h->t_fill_start_ns > lr) worker_idle_ns_ += h->t_fill_start_ns - lr;
+      worker_slot_wait_ns_ += h->t_acquire_wait_ns;
+      lr = h->t_ready_ns;
+    }
     ++fills_;
     SlotView v;
     v.g = g;
@@ -490,8 +504,13 @@ void MainDriver::collate_varlen(const SlotView& v, hipStream_t stream, int dst_d
     // an error word is reused after kErrWords launches; its batch was checked long before
     // (fenced batches are checked in order and the ring holds far fewer slots)
     const int64_t idx = int64_t(perr_seq_++ % uint64_t(kErrWords));
+    if (perr_state_.empty()) perr_state_.assign(size_t(kErrWords), 1);
+    if (perr_state_[size_t(idx)] == 0)
+      throw std::runtime_error("driver: more than 4096 device-parsed batches awaiting their kernels");
     perr_host_[idx] = -1;
+    perr_state_[size_t(idx)] = 0;
     note_handed(v.g, stream, &record);
+    handed_.back().perr = idx;
     eng_->collate_json(int(v.g), stream, v.values_offset, out, dst_dt, v.n_rows, L, pad, lengths, mask,
                        perr_dev_ + idx, record);
     last_perr_ = idx;
@@ -507,18 +526,6 @@ void MainDriver::deliver(const SlotView& v) {
   delivered_perr_ = v.kind == tk::kPackJsonText ? last_perr_ : -1;
 }
 
-bool MainDriver::check_parse_error(int64_t idx, const std::vector<tk::Watermark>& wms) {
-  if (idx < 0) return true;
-  const int32_t row = __atomic_load_n(perr_host_ + idx, __ATOMIC_ACQUIRE);
-  if (row < 0) return true;
-  std::string where;
-  for (const auto& w : wms)
-    where += (where.empty() ? "" : ", ") + std::string("partition index ") + std::to_string(w.pidx) + " offsets [" +
-             std::to_string(w.first_offset) + ", " + std::to_string(w.next_offset) + ")";
-  parse_error_ = "batch row " + std::to_string(row) + " is not a flat numeric JSON array (device parse; batch: " +
-                 where + ")";
-  return false;
-}
 
 void MainDriver::discard(const SlotView& v) {
   if (v.g < 0) return;
@@ -544,7 +551,10 @@ void MainDriver::finish_delivered(hipStream_t fence) {
   if (delivered_.empty()) return;
   const int64_t perr = delivered_perr_;
   delivered_perr_ = -1;
-  if (commit_on_device_ || perr >= 0) {  // a device-parsed batch commits only once its kernel ran clean
+  if (perr >= 0 && !commit_on_device_) {
+    // a device-parsed batch commits only once its kernel ran clean (read at slot release)
+    fenced_.emplace_back(nullptr, delivered_index_, std::move(delivered_), perr);
+  } else if (commit_on_device_) {
     hipEvent_t ev;
     if (event_pool_.empty()) {
       if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
@@ -561,18 +571,53 @@ void MainDriver::finish_delivered(hipStream_t fence) {
   delivered_.clear();
 }
 
+// Waits (wait=true) until every launched device-parse kernel completed and its slot was
+// released, so each pending error word has been read.
+void MainDriver::settle_parse_errors(bool wait) {
+  if (!wait) {
+    release_completed();
+    return;
+  }
+  cover_handed();
+  while (!handed_.empty()) {
+    for (const auto& h : handed_)
+      if (h.ev) eng_->wait_slot(int(h.g));
+    release_completed();
+  }
+}
+
 void MainDriver::drain_fenced(bool wait) {
+  bool settled = false;
   while (!fenced_.empty() && parse_error_.empty()) {
     auto& f = fenced_.front();
     hipEvent_t ev = std::get<0>(f);
-    if (wait) {
-      if (hipEventSynchronize(ev) != hipSuccess) throw std::runtime_error("driver: hipEventSynchronize failed");
-    } else if (hipEventQuery(ev) != hipSuccess) {
-      break;  // in order: a later batch is never committed before an earlier one
+    const int64_t pe = std::get<3>(f);
+    if (ev) {
+      if (wait) {
+        if (hipEventSynchronize(ev) != hipSuccess) throw std::runtime_error("driver: hipEventSynchronize failed");
+      } else if (hipEventQuery(ev) != hipSuccess) {
+        break;  // in order: a later batch is never committed before an earlier one
+      }
     }
-    if (!check_parse_error(std::get<3>(f), std::get<2>(f))) break;  // never committed
+    if (pe >= 0 && perr_state_[size_t(pe)] == 0) {
+      if (!settled) {
+        settle_parse_errors(wait);
+        settled = true;
+      }
+      if (perr_state_[size_t(pe)] == 0) break;  // its kernel has not completed yet
+    }
+    if (pe >= 0 && perr_state_[size_t(pe)] == 2) {
+      const int32_t row = __atomic_load_n(perr_host_ + pe, __ATOMIC_ACQUIRE);
+      std::string where;
+      for (const auto& w : std::get<2>(f))
+        where += (where.empty() ? "" : ", ") + std::string("partition index ") + std::to_string(w.pidx) +
+                 " offsets [" + std::to_string(w.first_offset) + ", " + std::to_string(w.next_offset) + ")";
+      parse_error_ = "batch row " + std::to_string(row) +
+                     " is not a flat numeric JSON array (device parse; batch: " + where + ")";
+      break;  // never committed
+    }
     stage_finished(std::get<1>(f), std::move(std::get<2>(f)));
-    event_pool_.push_back(ev);
+    if (ev) event_pool_.push_back(ev);
     fenced_.pop_front();
   }
 }
@@ -756,7 +801,7 @@ std::vector<std::pair<uint32_t, int64_t>> MainDriver::take_pending() {
 
 void MainDriver::reset_stats() {
   commits_ = commit_failures_ = 0;
-  fill_ns_ = fills_ = blocked_ns_ = blocked_calls_ = ready_age_ns_ = 0;
+  fill_ns_ = fills_ = blocked_ns_ = blocked_calls_ = ready_age_ns_ = worker_idle_ns_ = worker_slot_wait_ns_ = 0;
   ph_commit_ns_ = ph_next_ns_ = ph_launch_ns_ = ph_steps_ = events_ = groups_ = 0;
   reg_ns_ = 0;
   reg_total_ = 0;

@@ -150,15 +150,18 @@ class MainDriver {
 
   void stage_finished(int64_t index, std::vector<tk::Watermark>&& wms);
   bool commit_on_device_ = false;
-  // (event, batch index, watermarks, parse-error word index or -1)
+  // (event or null, batch index, watermarks, parse-error word index or -1).  A device-parsed
+  // batch needs no event of its own: it becomes committable once its slot was released (its
+  // kernel completed) and its error word read clean (perr_state_).
   std::deque<std::tuple<hipEvent_t, int64_t, std::vector<tk::Watermark>, int64_t>> fenced_;
+  std::vector<uint8_t> perr_state_;  // per error word: 0 kernel pending, 1 clean, 2 malformed row
+  void settle_parse_errors(bool wait);
   static constexpr int64_t kErrWords = 4096;
   int32_t* perr_host_ = nullptr;  // hipHostMalloc'ed, device-mapped error words (one per JSON launch)
   int32_t* perr_dev_ = nullptr;
   uint64_t perr_seq_ = 0;
   int64_t last_perr_ = -1, delivered_perr_ = -1;
   std::string parse_error_;
-  bool check_parse_error(int64_t idx, const std::vector<tk::Watermark>& wms);
   std::vector<hipEvent_t> event_pool_;
 
   struct Ticket {
@@ -190,7 +193,8 @@ class MainDriver {
   std::deque<SlotView> staged_;
   struct Handed {
     int64_t g;
-    bool ev;  // its own completion event was recorded
+    bool ev;            // its own completion event was recorded
+    int64_t perr = -1;  // device JSON parse: its error word, checked when the slot is released
   };
   std::deque<Handed> handed_;  // slots whose collate was launched, in launch order
   hipStream_t last_stream_ = nullptr;
@@ -204,7 +208,9 @@ class MainDriver {
   uint64_t commits_ = 0, commit_failures_ = 0;
  public:
   // profiling counters (ns): worker fill time of delivered slots, main time blocked on the ring
-  int64_t fill_ns_ = 0, fills_ = 0, blocked_ns_ = 0, blocked_calls_ = 0, ready_age_ns_ = 0;
+  int64_t fill_ns_ = 0, fills_ = 0, blocked_ns_ = 0, blocked_calls_ = 0, ready_age_ns_ = 0, worker_idle_ns_ = 0,
+          worker_slot_wait_ns_ = 0;
+  std::vector<int64_t> last_ready_;
   // step_fixed phases (ns): finish+commit of the previous batch, slot acquisition/release, collate launch
   int64_t ph_commit_ns_ = 0, ph_next_ns_ = 0, ph_launch_ns_ = 0, ph_steps_ = 0, events_ = 0;
   // inside the next phase: slot releases (event queries + ring hand-back) and stagings of READY slots

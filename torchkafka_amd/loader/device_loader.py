@@ -789,6 +789,8 @@ class DeviceLoader:
         self.stats.worker_fills += st["fills"]
         self.stats.wait_ns += st["blocked_ns"]
         self.stats.ready_age_ns += st["ready_age_ns"]
+        self.stats.worker_idle_ns += st.get("worker_idle_ns", 0)
+        self.stats.worker_slot_wait_ns += st.get("worker_slot_wait_ns", 0)
         self.stats.phase_commit_ns += st["phase_commit_ns"]
         self.stats.phase_next_ns += st["phase_next_ns"]
         self.stats.phase_launch_ns += st["phase_launch_ns"]

@@ -33,6 +33,8 @@ class LoaderStats:
     worker_fill_ns: int = 0
     worker_fills: int = 0
     ready_age_ns: int = 0
+    worker_idle_ns: int = 0
+    worker_slot_wait_ns: int = 0
     phase_commit_ns: int = 0   # native step driver: finish + commit of the previous batch
     phase_next_ns: int = 0     # native step driver: slot release/acquire (+H2D issue)
     phase_launch_ns: int = 0   # native step driver: collate launch (+event)
@@ -75,6 +77,8 @@ class LoaderStats:
             "host_issue_us_per_batch": self.issue_ns / 1e3 / max(self.batches, 1),
             "worker_fill_us_per_batch": self.worker_fill_ns / 1e3 / max(self.worker_fills, 1),
             "ready_age_us_per_batch": self.ready_age_ns / 1e3 / max(self.worker_fills, 1),
+            "worker_idle_us_per_batch": self.worker_idle_ns / 1e3 / max(self.worker_fills, 1),
+            "worker_slot_wait_us_per_batch": self.worker_slot_wait_ns / 1e3 / max(self.worker_fills, 1),
             "native_commit_us_per_step": self.phase_commit_ns / 1e3 / max(self.phase_steps, 1),
             "native_next_us_per_step": self.phase_next_ns / 1e3 / max(self.phase_steps, 1),
             "native_launch_us_per_step": self.phase_launch_ns / 1e3 / max(self.phase_steps, 1),
