@@ -373,8 +373,8 @@ def _produce_json(broker, topic, rows_per_part):
     p.flush()
 
 
-@pytest.mark.parametrize("h2d", ["dma", "zerocopy"])
-def test_json_device_parse_mixed_rows_match_python(broker, h2d):
+@pytest.mark.parametrize("h2d,coalesce", [("dma", 8), ("zerocopy", 8), ("zerocopy", 1)])
+def test_json_device_parse_mixed_rows_match_python(broker, h2d, coalesce):
     """Simple rows parsed by the kernel, exponent/NaN/long rows parsed by the workers, None skipped."""
     import json
     import math
@@ -400,7 +400,7 @@ def test_json_device_parse_mixed_rows_match_python(broker, h2d):
     _produce_json(broker, "m", rows)
     DS = _dataset(JsonArray())
     dl = DeviceLoader(DS.placeholder(), 40, num_workers=2, device="cuda:0", dtype=torch.float32, return_info=True,
-                      json_parse="device", h2d=h2d,
+                      json_parse="device", h2d=h2d, coalesce=coalesce,
                       worker_init_fn=DS.init_worker("m", bootstrap_servers=broker.url, group_id="g",
                                                     auto_offset_reset="earliest", consumer_timeout_ms=300))
     got = []

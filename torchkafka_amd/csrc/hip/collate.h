@@ -40,6 +40,22 @@ using tk::JsonRowDesc;
 void launch_json_rows(const JsonRowDesc* rows, const void* vals, void* out, int dst_dt, int64_t n_rows, int64_t L,
                       double pad, int64_t* lengths, uint8_t* mask, int32_t* err, hipStream_t stream);
 
+// Up to kMaxGroup JSON batches in one launch; row_base[k] = first global row of batch k,
+// row_base[n] = total rows.  Entries k >= n are ignored.
+struct JsonGroupArgs {
+  int n;
+  float pad;
+  int64_t row_base[kMaxGroup + 1];
+  const JsonRowDesc* rows[kMaxGroup];
+  const uint8_t* vals[kMaxGroup];
+  void* out[kMaxGroup];
+  int64_t L[kMaxGroup];
+  int64_t* lengths[kMaxGroup];
+  uint8_t* mask[kMaxGroup];
+  int32_t* err[kMaxGroup];
+};
+void launch_json_group(JsonGroupArgs& a, int dst_dt, hipStream_t stream);
+
 std::vector<std::pair<std::string, double>> api_bench(int device, int iters);
 
 }  // namespace tkh

@@ -523,7 +523,81 @@ void MainDriver::collate_varlen(const SlotView& v, hipStream_t stream, int dst_d
 
 void MainDriver::deliver(const SlotView& v) {
   delivered_ = v.wms;
-  delivered_perr_ = v.kind == tk::kPackJsonText ? last_perr_ : -1;
+  delivered_perr_ = v.kind == tk::kPackJsonText ? (v.perr >= 0 ? v.perr : last_perr_) : -1;
+}
+
+void MainDriver::stage_ready(int extra) {
+  if (ls_) return;
+  while (int(staged_.size()) < prefetch_ + extra) {
+    const int r = poll_one(false, 0);
+    if (r <= 0) break;  // -3 is reported by next_slot
+  }
+}
+
+size_t MainDriver::json_group_extend() {
+  group_idx_.clear();
+  if (coalesce_ <= 1 || last.kind != uint32_t(tk::kPackJsonText)) return 0;
+  for (size_t i = 0; i < staged_.size() && int(1 + group_idx_.size()) < coalesce_; ++i) {
+    const SlotView& v = staged_[i];
+    if (v.g < 0) continue;  // watermark-only slot: rides on the next delivered batch
+    if (v.pre || v.kind != last.kind || v.n_rows == 0) break;
+    group_idx_.push_back(i);
+  }
+  return group_idx_.size();
+}
+
+void MainDriver::json_group_launch(hipStream_t stream, int dst_dt, double pad, void* const* outs, const int64_t* Ls,
+                                   int64_t* const* lengths, uint8_t* const* masks,
+                                   std::vector<std::shared_ptr<void>>&& handles) {
+  const int n = 1 + int(group_idx_.size());
+  if (int(handles.size()) != n - 1) throw std::invalid_argument("driver: group handles do not match the group");
+  if (!perr_host_) {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, kErrWords * sizeof(int32_t), hipHostMallocMapped) != hipSuccess)
+      throw std::runtime_error("driver: hipHostMalloc of the parse error words failed");
+    perr_host_ = static_cast<int32_t*>(h);
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) throw std::runtime_error("driver: hipHostGetDevicePointer failed");
+    perr_dev_ = static_cast<int32_t*>(d);
+    perr_state_.assign(size_t(kErrWords), 1);
+  }
+  int slots[kMaxGroup];
+  size_t voffs[kMaxGroup];
+  int64_t rows[kMaxGroup], perr[kMaxGroup];
+  int32_t* errs[kMaxGroup];
+  for (int k = 0; k < n; ++k) {
+    SlotView& v = k == 0 ? last : staged_[group_idx_[size_t(k - 1)]];
+    slots[k] = int(v.g);
+    voffs[k] = v.values_offset;
+    rows[k] = v.n_rows;
+    const int64_t idx = int64_t(perr_seq_++ % uint64_t(kErrWords));
+    if (perr_state_[size_t(idx)] == 0)
+      throw std::runtime_error("driver: more than 4096 device-parsed batches awaiting their kernels");
+    perr_host_[idx] = -1;
+    perr_state_[size_t(idx)] = 0;
+    perr[k] = idx;
+    errs[k] = perr_dev_ + idx;
+    v.perr = idx;
+  }
+  if (stream != last_stream_) {
+    cover_handed();
+    last_stream_ = stream;
+  }
+  eng_->collate_json_group(slots, n, stream, voffs, rows, outs, Ls, lengths, masks, errs, pad, dst_dt);
+  // one completion event (after the group kernel, on the last slot) releases every slot of the group
+  for (int k = 0; k < n; ++k) handed_.push_back(Handed{slots[k], k == n - 1, perr[k]});
+  last_ev_slot_ = slots[n - 1];
+  unevented_ = 0;
+  ++events_;
+  if (n > 1) ++groups_;
+  for (int k = 1; k < n; ++k) {
+    SlotView& v = staged_[group_idx_[size_t(k - 1)]];
+    v.pre = true;
+    v.pre_stream = stream;
+    v.pre_event_slot = slots[n - 1];
+    v.pre_out = std::move(handles[size_t(k - 1)]);
+  }
+  group_idx_.clear();
 }
 
 

@@ -38,6 +38,7 @@ struct SlotView {
   hipStream_t pre_stream = nullptr;
   int64_t pre_event_slot = -1;        // slot whose completion event follows the group kernel
   std::shared_ptr<void> pre_out;      // the output tensor (opaque here: libtorch stays in torch_step.cpp)
+  int64_t perr = -1;                  // device JSON parse: its error word (set at launch)
 };
 
 class MainDriver {
@@ -93,6 +94,20 @@ class MainDriver {
                            std::vector<int64_t>* group_rows, std::shared_ptr<void>* pre_out);
   void step_group_launch(hipStream_t stream, int dst_dt, void* const* dsts, int64_t row, const float* shift,
                          const float* scale, std::vector<std::shared_ptr<void>>&& handles);
+  // Coalesced device JSON parse (kPackJsonText), two phases around the caller's allocations:
+  //   json_group_extend: after next_slot() returned a JSON batch in `last`, lists the staged
+  //                      JSON batches right behind it that one launch can parse too (<= coalesce-1);
+  //   json_group_launch: one kernel for last + those; outs/Ls/... hold 1 + n entries, handles
+  //                      (the staged batches' outputs) ride with them until they are delivered.
+  size_t json_group_extend();
+  // Stages READY slots until `extra` beyond prefetch are staged (never blocks).
+  void stage_ready(int extra);
+  // A batch parsed by a group launch on another stream: `stream` waits for that kernel.
+  void wait_group(const SlotView& v, hipStream_t stream) { eng_->stream_wait_done(int(v.pre_event_slot), stream); }
+  const SlotView& group_member(size_t k) const { return staged_[group_idx_[k]]; }
+  void json_group_launch(hipStream_t stream, int dst_dt, double pad, void* const* outs, const int64_t* Ls,
+                         int64_t* const* lengths, uint8_t* const* masks,
+                         std::vector<std::shared_ptr<void>>&& handles);
   void set_coalesce(int n) { coalesce_ = n < 1 ? 1 : (n > kMaxGroup ? kMaxGroup : n); }
   // Adaptive coalescing: while the GPU is still running an earlier launch, wait up to `us` for
   // more staged batches so the next launch carries a full group (0 disables).  Waiting costs no

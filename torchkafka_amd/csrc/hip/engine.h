@@ -49,6 +49,11 @@ class Engine {
   // error stores the row index into *err (host-mapped).
   void collate_json(int s, hipStream_t user, size_t values_offset, void* out, int dst_dt, int64_t rows, int64_t L,
                     double pad, int64_t* lengths, uint8_t* mask, int32_t* err, bool record = true);
+  // Up to kMaxGroup kPackJsonText slots parsed by one kernel; the completion event of the last
+  // slot is recorded (it stands for all of them).
+  void collate_json_group(const int* slots, int n, hipStream_t user, const size_t* values_offsets, const int64_t* rows,
+                          void* const* outs, const int64_t* Ls, int64_t* const* lengths, uint8_t* const* masks,
+                          int32_t* const* errs, double pad, int dst_dt);
   // Consecutive fixed-width slots collated by one kernel (collate.h launch_fixed_group);
   // the completion event of the last slot is recorded (it stands for all of them).
   void collate_fixed_group(const int* slots, int n, hipStream_t user, const size_t* values_offsets, int src_dt,

@@ -194,6 +194,31 @@ void Engine::collate_json(int s, hipStream_t user, size_t values_offset, void* o
   if (record) finish(s, user);
 }
 
+void Engine::collate_json_group(const int* slots, int n, hipStream_t user, const size_t* values_offsets,
+                                const int64_t* rows, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
+                                uint8_t* const* masks, int32_t* const* errs, double pad, int dst_dt) {
+  if (n < 1 || n > kMaxGroup) throw std::invalid_argument("engine: bad group size");
+  JsonGroupArgs a{};
+  a.n = n;
+  a.pad = float(pad);
+  a.row_base[0] = 0;
+  for (int k = 0; k < n; ++k) {
+    check_slot(slots[k]);
+    begin(slots[k], user);
+    const uint8_t* base = src_base(slots[k]);
+    a.rows[k] = reinterpret_cast<const JsonRowDesc*>(base);
+    a.vals[k] = base + values_offsets[k];
+    a.out[k] = outs[k];
+    a.L[k] = Ls[k];
+    a.lengths[k] = lengths[k];
+    a.mask[k] = masks[k];
+    a.err[k] = errs[k];
+    a.row_base[k + 1] = a.row_base[k] + rows[k];
+  }
+  launch_json_group(a, dst_dt, user);
+  finish(slots[n - 1], user);
+}
+
 void Engine::copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes) {
   check_slot(s);
   begin(s, user);

@@ -137,17 +137,27 @@ __device__ __forceinline__ int parse_token_regs(const uint8_t* buf, int s, int a
   return 1;
 }
 
+// Blocks [row_base[k], row_base[k+1]) parse batch k: one launch serves up to kMaxGroup
+// staged batches (the driver's coalesced launches), each with its own slot, output and L.
 template <typename D>
-__global__ __launch_bounds__(kThreads) void json_rows_kernel(const JsonRowDesc* __restrict__ rows,
-                                                             const uint8_t* __restrict__ vals, D* __restrict__ out,
-                                                             int64_t L, float pad, int64_t* __restrict__ lengths,
-                                                             uint8_t* __restrict__ mask, int32_t* __restrict__ err) {
+__global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kWin + 32];  // + the 32-byte token reads
   __shared__ uint16_t starts[kMaxTok];
   __shared__ int s_wsum[kWaves];
   __shared__ int s_cut, s_bad;
 
-  const int64_t r = blockIdx.x;
+  int bk = 0;
+#pragma unroll
+  for (int k = 1; k < kMaxGroup; ++k) bk += (k < a.n && int64_t(blockIdx.x) >= a.row_base[k]) ? 1 : 0;
+  const int64_t r = int64_t(blockIdx.x) - a.row_base[bk];
+  const JsonRowDesc* __restrict__ rows = a.rows[bk];
+  const uint8_t* __restrict__ vals = a.vals[bk];
+  D* __restrict__ out = static_cast<D*>(a.out[bk]);
+  const int64_t L = a.L[bk];
+  const float pad = a.pad;
+  int64_t* __restrict__ lengths = a.lengths[bk];
+  uint8_t* __restrict__ mask = a.mask[bk];
+  int32_t* __restrict__ err = a.err[bk];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
   const JsonRowDesc d = rows[r];
   const int64_t n_out = d.n_out < L ? d.n_out : L;
@@ -267,31 +277,47 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(const JsonRowDesc* 
 }
 
 template <typename D>
-void launch_json_t(const JsonRowDesc* rows, const uint8_t* vals, void* out, int64_t n_rows, int64_t L, float pad,
-                   int64_t* lengths, uint8_t* mask, int32_t* err, hipStream_t stream) {
-  hipLaunchKernelGGL((json_rows_kernel<D>), dim3(unsigned(n_rows)), dim3(kThreads), 0, stream, rows, vals,
-                     static_cast<D*>(out), L, pad, lengths, mask, err);
+void launch_json_t(const JsonGroupArgs& a, int64_t total_rows, hipStream_t stream) {
+  hipLaunchKernelGGL((json_rows_kernel<D>), dim3(unsigned(total_rows)), dim3(kThreads), 0, stream, a);
+}
+
+void launch_json_args(JsonGroupArgs& a, int dst_dt, hipStream_t stream) {
+  if (a.n < 1 || a.n > kMaxGroup) throw std::invalid_argument("json collate: group size out of range");
+  const int64_t total = a.row_base[a.n];
+  if (total == 0) return;
+  if (total > INT32_MAX) throw std::invalid_argument("json collate: too many rows");
+  for (int k = 0; k < a.n; ++k)
+    if (reinterpret_cast<uintptr_t>(a.vals[k]) % 16 || reinterpret_cast<uintptr_t>(a.rows[k]) % 16)
+      throw std::invalid_argument("json collate: slot regions must be 16-byte aligned");
+  switch (dst_dt) {
+    case kF32: launch_json_t<float>(a, total, stream); break;
+    case kF16: launch_json_t<_Float16>(a, total, stream); break;
+    case kBF16: launch_json_t<__bf16>(a, total, stream); break;
+    case kFP8E4M3: launch_json_t<fp8e4m3>(a, total, stream); break;
+    default: throw std::invalid_argument("json collate: destination must be a float dtype");
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("json collate launch: ") + hipGetErrorString(e));
 }
 
 }  // namespace
 
 void launch_json_rows(const JsonRowDesc* rows, const void* vals, void* out, int dst_dt, int64_t n_rows, int64_t L,
                       double pad, int64_t* lengths, uint8_t* mask, int32_t* err, hipStream_t stream) {
-  if (n_rows == 0) return;
-  if (n_rows > INT32_MAX) throw std::invalid_argument("json collate: too many rows");
-  if (reinterpret_cast<uintptr_t>(vals) % 16 || reinterpret_cast<uintptr_t>(rows) % 16)
-    throw std::invalid_argument("json collate: slot regions must be 16-byte aligned");
-  const auto* v = static_cast<const uint8_t*>(vals);
-  const float p = float(pad);
-  switch (dst_dt) {
-    case kF32: launch_json_t<float>(rows, v, out, n_rows, L, p, lengths, mask, err, stream); break;
-    case kF16: launch_json_t<_Float16>(rows, v, out, n_rows, L, p, lengths, mask, err, stream); break;
-    case kBF16: launch_json_t<__bf16>(rows, v, out, n_rows, L, p, lengths, mask, err, stream); break;
-    case kFP8E4M3: launch_json_t<fp8e4m3>(rows, v, out, n_rows, L, p, lengths, mask, err, stream); break;
-    default: throw std::invalid_argument("json collate: destination must be a float dtype");
-  }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) throw std::runtime_error(std::string("json collate launch: ") + hipGetErrorString(e));
+  JsonGroupArgs a{};
+  a.n = 1;
+  a.row_base[1] = n_rows;
+  a.rows[0] = rows;
+  a.vals[0] = static_cast<const uint8_t*>(vals);
+  a.out[0] = out;
+  a.L[0] = L;
+  a.lengths[0] = lengths;
+  a.mask[0] = mask;
+  a.err[0] = err;
+  a.pad = float(pad);
+  launch_json_args(a, dst_dt, stream);
 }
+
+void launch_json_group(JsonGroupArgs& a, int dst_dt, hipStream_t stream) { launch_json_args(a, dst_dt, stream); }
 
 }  // namespace tkh

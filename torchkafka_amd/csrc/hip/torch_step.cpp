@@ -13,6 +13,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "consumer.h"
 #include "driver.h"
 #include "collate.h"
 #include "dtypes.h"
@@ -35,6 +36,11 @@ at::ScalarType scalar_type_of(int code) {
     default: throw std::invalid_argument("step_fixed_tensor: unsupported dtype code");
   }
 }
+// Outputs of a var-len batch parsed ahead of its delivery by a coalesced launch.
+struct VarlenOut {
+  at::Tensor out, lengths, mask;
+};
+
 // One fixed-width step: finish + commit the previous batch, take the next one, collate it
 // (coalesced with staged ones when cfg.grouped) into a tensor on the current stream.
 py::tuple step_once(MainDriver& d, const MainDriver::FastConfig& cfg) {
@@ -141,30 +147,79 @@ void register_torch_step(py::module_& m) {
         int cs = 0;
         int r;
         int64_t t1, t2;
+        size_t extra = 0;
         {
           py::gil_scoped_release nogil;
           d.finish_delivered(stream);
           if (auto_commit) cs = d.commit_pending();
           t1 = tk::now_ns();
+          if (d.coalesce() > 1) d.stage_ready(d.coalesce());  // let a group form (never blocks)
           r = d.next_slot(timeout_ms, &d.last);
+          if (r == 1 && !d.last.pre) extra = d.json_group_extend();
           t2 = tk::now_ns();
         }
         d.ph_commit_ns_ += t1 - t0;
         d.ph_next_ns_ += t2 - t1;
         if (r != 1) return py::make_tuple(r, cs, py::none(), py::none(), py::none());
-        const SlotView& v = d.last;
-        int64_t L = pad_to >= 0 ? pad_to : v.max_row_len;
-        if (pad_to < 0 && pad_multiple > 1) L = (L + pad_multiple - 1) / pad_multiple * pad_multiple;
+        SlotView& v = d.last;
         const int64_t n = int64_t(v.n_rows);
-        at::Tensor out = at::empty({n, L}, at::TensorOptions().dtype(scalar_type_of(dst_dt)).device(at::kCUDA, dev));
-        at::Tensor lengths = at::empty({n}, at::TensorOptions().dtype(at::kLong).device(at::kCUDA, dev));
-        at::Tensor mask;
-        if (want_mask) mask = at::empty({n, L}, at::TensorOptions().dtype(at::kBool).device(at::kCUDA, dev));
-        {
+        at::Tensor out, lengths, mask;
+        if (v.pre) {
+          // parsed by an earlier group launch; a consumer on another stream waits for that kernel
+          auto* o = static_cast<VarlenOut*>(v.pre_out.get());
+          out = o->out;
+          lengths = o->lengths;
+          mask = o->mask;
           py::gil_scoped_release nogil;
-          d.collate_varlen(v, stream, dst_dt, out.data_ptr(), L, pad, lengths.data_ptr<int64_t>(),
-                           want_mask ? static_cast<uint8_t*>(mask.data_ptr()) : nullptr);
+          if (v.pre_stream != stream) d.wait_group(v, stream);
           d.deliver(v);
+        } else {
+          auto alloc = [&](const SlotView& s, VarlenOut* o, int64_t* Lout) {
+            int64_t L = pad_to >= 0 ? pad_to : s.max_row_len;
+            if (pad_to < 0 && pad_multiple > 1) L = (L + pad_multiple - 1) / pad_multiple * pad_multiple;
+            const int64_t m = int64_t(s.n_rows);
+            o->out = at::empty({m, L}, at::TensorOptions().dtype(scalar_type_of(dst_dt)).device(at::kCUDA, dev));
+            o->lengths = at::empty({m}, at::TensorOptions().dtype(at::kLong).device(at::kCUDA, dev));
+            if (want_mask) o->mask = at::empty({m, L}, at::TensorOptions().dtype(at::kBool).device(at::kCUDA, dev));
+            *Lout = L;
+          };
+          if (extra == 0 || v.kind != uint32_t(tk::kPackJsonText)) {
+            VarlenOut o;
+            int64_t L;
+            alloc(v, &o, &L);
+            out = o.out;
+            lengths = o.lengths;
+            mask = o.mask;
+            py::gil_scoped_release nogil;
+            d.collate_varlen(v, stream, dst_dt, out.data_ptr(), L, pad, lengths.data_ptr<int64_t>(),
+                             want_mask ? static_cast<uint8_t*>(mask.data_ptr()) : nullptr);
+            d.deliver(v);
+          } else {
+            // one launch parses `last` and the staged JSON batches behind it
+            void* outs[kMaxGroup];
+            int64_t Ls[kMaxGroup];
+            int64_t* lens[kMaxGroup];
+            uint8_t* masks[kMaxGroup];
+            std::vector<std::shared_ptr<void>> handles;
+            handles.reserve(extra);
+            for (size_t k = 0; k <= extra; ++k) {
+              auto o = std::make_shared<VarlenOut>();
+              alloc(k == 0 ? v : d.group_member(k - 1), o.get(), &Ls[k]);
+              outs[k] = o->out.data_ptr();
+              lens[k] = o->lengths.data_ptr<int64_t>();
+              masks[k] = want_mask ? static_cast<uint8_t*>(o->mask.data_ptr()) : nullptr;
+              if (k == 0) {
+                out = o->out;
+                lengths = o->lengths;
+                mask = o->mask;
+              } else {
+                handles.emplace_back(std::move(o));
+              }
+            }
+            py::gil_scoped_release nogil;
+            d.json_group_launch(stream, dst_dt, pad, outs, Ls, lens, masks, std::move(handles));
+            d.deliver(v);
+          }
         }
         d.ph_launch_ns_ += tk::now_ns() - t2;
         ++d.ph_steps_;

@@ -410,11 +410,17 @@ class DeviceLoader:
         return DTYPE_CODE[s.dtype]
 
     RING_AUTO_BYTES = 64 << 20
+    RING_AUTO_BYTES_VARLEN = 512 << 20
 
     def _slots_per_worker(self) -> int:
         if self.slots_per_worker is not None:
             return self.slots_per_worker
-        fit = self.RING_AUTO_BYTES // max(1, self.num_workers * self._slot_capacity())
+        budget = self.RING_AUTO_BYTES
+        if getattr(self.schema, "kind", None) in (1, 2) and self.device.type == "cuda":
+            # var-len / JSON slots are sized for the worst row (16 MiB) but hold a few hundred KiB:
+            # 8 per worker keeps the workers off the slot-release wait (config 4: +4 %)
+            budget = self.RING_AUTO_BYTES_VARLEN
+        fit = budget // max(1, self.num_workers * self._slot_capacity())
         return int(max(4, min(8, fit)))
 
     def _slot_capacity(self) -> int:
