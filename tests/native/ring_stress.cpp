@@ -104,6 +104,7 @@ static void broker_pipeline(uint32_t nw, uint32_t per_part) {
           const uint32_t k = std::min<uint32_t>(7, per_part - n);
           for (uint32_t i = 0; i < k; ++i) {
             for (int j = 0; j < 16; ++j) v[j] = float(n + i);
+            v[1] = float(pidx);
             recs[i] = RecordIn{0, nullptr, -1, reinterpret_cast<const uint8_t*>(v.data()), 64, nullptr, 0};
             b->append(pidx, recs.data(), 1);
           }
@@ -148,15 +149,29 @@ static void broker_pipeline(uint32_t nw, uint32_t per_part) {
     SlotHeader* h = ring->slot(uint32_t(g));
     const float* vals = reinterpret_cast<const float*>(ring->payload(uint32_t(g)));
     std::vector<CommitEntry> ce;
-    uint32_t r = 0;
+    // rows of different partitions may interleave (a packer revisits a partition that grew
+    // while it read another); per partition they are contiguous offsets from first_offset
+    std::vector<int64_t> next_row(np, -1);
+    uint32_t total = 0;
     for (uint32_t k = 0; k < h->n_parts; ++k) {
       const Watermark& wm = h->wm[k];
       CHECK(wm.first_offset == expect[wm.pidx - t.first_pidx]);  // contiguous, exact offsets
-      for (uint32_t c = 0; c < wm.count; ++c, ++r) CHECK(vals[r * 16] == float(wm.first_offset + c));
+      next_row[wm.pidx - t.first_pidx] = wm.first_offset;
+      total += wm.count;
+    }
+    CHECK(total == h->n_rows);
+    for (uint32_t r = 0; r < h->n_rows; ++r) {
+      const uint32_t p = uint32_t(vals[r * 16 + 1]) - t.first_pidx;
+      CHECK(p < np && next_row[p] >= 0);
+      CHECK(vals[r * 16] == float(next_row[p]));
+      ++next_row[p];
+    }
+    for (uint32_t k = 0; k < h->n_parts; ++k) {
+      const Watermark& wm = h->wm[k];
+      CHECK(next_row[wm.pidx - t.first_pidx] == wm.next_offset);
       expect[wm.pidx - t.first_pidx] = wm.next_offset;
       ce.push_back(CommitEntry{wm.pidx, wm.next_offset, std::string()});
     }
-    CHECK(r == h->n_rows);
     rows += h->n_rows;
     b->commit(grp, -1, 0, 0, ce);
     if (h->flags & kSlotEOS) done[h->worker] = 1;
