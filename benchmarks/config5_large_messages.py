@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch-size", type=int, default=8)
-    ap.add_argument("--workers", type=int, default=4)
+    ap.add_argument("--workers", type=int, default=8)
     ap.add_argument("--partitions", type=int, default=128)
     ap.add_argument("--slots-per-worker", type=int, default=2)
     ap.add_argument("--device", default="cuda:0")
