@@ -141,3 +141,19 @@ def test_json_parser_random_numbers():
 def test_json_parser_rejects(bad):
     with pytest.raises(ValueError):
         core().parse_json_f32(bad.encode())
+
+
+def test_crc32c_methods_agree():
+    """Table, 3-stream crc32 instruction and AVX-512 VPCLMULQDQ folding give the same CRC32C."""
+    import random
+
+    c = core()
+    rnd = random.Random(11)
+    methods = [0] + ([1] if c.crc32c_hw() else []) + ([2] if c.crc32c_fold() else [])
+    for n in [256, 257, 300, 511, 512, 513, 1024 + 3, 4096, 65536 + 17, 200_003]:
+        for _ in range(3):
+            d = rnd.randbytes(n)
+            want = py_crc32c(d) if n <= 4096 else c.crc32c_method(0, d)
+            got = {m: c.crc32c_method(m, d) for m in methods}
+            assert set(got.values()) == {want}, (n, got, want)
+            assert c.crc32c(d) == want

@@ -62,6 +62,9 @@ for s in $STEPS; do
     benchw0) step bench_w0 600 python bench.py --stats --steps 4000 --warmup 100 --coalesce-wait-us 0 ;;
     benchc8w) step bench_c8w 600 python bench.py --stats --steps 4000 --warmup 100 --coalesce 8 ;;
     benchc8w200) step bench_c8w200 600 python bench.py --stats --steps 4000 --warmup 100 --coalesce 8 --coalesce-wait-us 200 ;;
+    benchnofold) TORCHKAFKA_CRC_FOLD=0 step bench_nofold 600 python bench.py --stats --steps 4000 --warmup 100 ;;
+    fillbench) step fill_bench 300 python tools/fill_bench.py ;;
+    fillbenchnofold) TORCHKAFKA_CRC_FOLD=0 step fill_bench_nofold 300 python tools/fill_bench.py ;;
     benchnocrc) step bench_nocrc 600 python bench.py --stats --steps 4000 --warmup 100 --no-crc ;;
     benchzc) step bench_zc 600 python bench.py --stats --steps 4000 --warmup 100 --h2d zerocopy ;;
     benchs1) step bench_s1 600 python bench.py --stats --steps 4000 --warmup 100 --copy-streams 1 ;;

@@ -123,6 +123,11 @@ PYBIND11_MODULE(_tkcore, m) {
     return crc32c(s.data(), s.size());
   });
   m.def("crc32c_hw", &crc32c_hw);
+  m.def("crc32c_fold", &crc32c_fold);
+  m.def("crc32c_method", [](int method, py::bytes b) {
+    std::string s = b;
+    return crc32c_method(method, s.data(), s.size());
+  });
   m.def(
       "encode_batch",
       [](int64_t base_offset, std::vector<py::object> values, std::vector<py::object> keys,

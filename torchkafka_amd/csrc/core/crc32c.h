@@ -14,5 +14,9 @@ uint32_t crc32c(const void* data, size_t n);
 uint32_t crc32c_extend(uint32_t crc, const void* data, size_t n);
 // True if the hardware (SSE4.2) path is in use.
 bool crc32c_hw();
+// True when the AVX-512 VPCLMULQDQ folding path is used for buffers >= 512 bytes.
+bool crc32c_fold();
+// One implementation explicitly (tests): 0 table, 1 crc32 instruction (3 streams), 2 folding.
+uint32_t crc32c_method(int method, const void* data, size_t n);
 
 }  // namespace tk
