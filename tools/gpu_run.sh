@@ -65,6 +65,9 @@ for s in $STEPS; do
     benchnofold) TORCHKAFKA_CRC_FOLD=0 step bench_nofold 600 python bench.py --stats --steps 4000 --warmup 100 ;;
     fillbench) step fill_bench 300 python tools/fill_bench.py ;;
     fillbenchnofold) TORCHKAFKA_CRC_FOLD=0 step fill_bench_nofold 300 python tools/fill_bench.py ;;
+    benchfp2k) TORCHKAFKA_CRC_FOLD_PREFETCH=2048 step bench_fp2k 600 python bench.py --stats --steps 4000 --warmup 100 ;;
+    benchfp4k) TORCHKAFKA_CRC_FOLD_PREFETCH=4096 step bench_fp4k 600 python bench.py --stats --steps 4000 --warmup 100 ;;
+    benchfp512) TORCHKAFKA_CRC_FOLD_PREFETCH=512 step bench_fp512 600 python bench.py --stats --steps 4000 --warmup 100 ;;
     benchnocrc) step bench_nocrc 600 python bench.py --stats --steps 4000 --warmup 100 --no-crc ;;
     benchzc) step bench_zc 600 python bench.py --stats --steps 4000 --warmup 100 --h2d zerocopy ;;
     benchs1) step bench_s1 600 python bench.py --stats --steps 4000 --warmup 100 --copy-streams 1 ;;

@@ -173,6 +173,11 @@ bool detect_hw() { return __builtin_cpu_supports("sse4.2"); }
 // << 1 in the reflected representation (derived and checked against the bitwise CRC; tests).
 // The lanes are then folded into one 128-bit remainder whose raw CRC (two crc32 instructions
 // from state 0) is the CRC of everything folded.
+const size_t kFoldPrefetch = [] {
+  const char* e = std::getenv("TORCHKAFKA_CRC_FOLD_PREFETCH");  // 512/1K/2K/4K: 45.3/45.3/45.4/45.9 M rec/s
+  return e ? size_t(std::strtoul(e, nullptr, 10)) : size_t(4096);
+}();
+
 struct FoldConsts {
   __m128i k2048, k512, k384, k256, k128;
   FoldConsts() {
@@ -212,8 +217,11 @@ __attribute__((target("avx512f,avx512dq,vpclmulqdq,pclmul,sse4.2"))) uint32_t ra
   n -= 256;
   const __m512i k = _mm512_broadcast_i32x4(C.k2048);
   while (n >= 256) {
-    _mm_prefetch(reinterpret_cast<const char*>(p + 1024), _MM_HINT_T0);
-    _mm_prefetch(reinterpret_cast<const char*>(p + 1024 + 128), _MM_HINT_T0);
+    // the log is usually read cold from DRAM: keep kFoldPrefetch bytes requested ahead
+    _mm_prefetch(reinterpret_cast<const char*>(p + kFoldPrefetch), _MM_HINT_T0);
+    _mm_prefetch(reinterpret_cast<const char*>(p + kFoldPrefetch + 64), _MM_HINT_T0);
+    _mm_prefetch(reinterpret_cast<const char*>(p + kFoldPrefetch + 128), _MM_HINT_T0);
+    _mm_prefetch(reinterpret_cast<const char*>(p + kFoldPrefetch + 192), _MM_HINT_T0);
     a0 = fold512(a0, k, _mm512_loadu_si512(p));
     a1 = fold512(a1, k, _mm512_loadu_si512(p + 64));
     a2 = fold512(a2, k, _mm512_loadu_si512(p + 128));
