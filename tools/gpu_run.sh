@@ -68,6 +68,10 @@ for s in $STEPS; do
     benchfp2k) TORCHKAFKA_CRC_FOLD_PREFETCH=2048 step bench_fp2k 600 python bench.py --stats --steps 4000 --warmup 100 ;;
     benchfp4k) TORCHKAFKA_CRC_FOLD_PREFETCH=4096 step bench_fp4k 600 python bench.py --stats --steps 4000 --warmup 100 ;;
     benchfp512) TORCHKAFKA_CRC_FOLD_PREFETCH=512 step bench_fp512 600 python bench.py --stats --steps 4000 --warmup 100 ;;
+    benchfp8k) TORCHKAFKA_CRC_FOLD_PREFETCH=8192 step bench_fp8k 600 python bench.py --stats --steps 4000 --warmup 100 ;;
+    benchfp16k) TORCHKAFKA_CRC_FOLD_PREFETCH=16384 step bench_fp16k 600 python bench.py --stats --steps 4000 --warmup 100 ;;
+    benchw100) step bench_w100 600 python bench.py --stats --steps 4000 --warmup 100 --coalesce-wait-us 100 ;;
+    benchpf4) step bench_pf4 600 python bench.py --stats --steps 4000 --warmup 100 --prefetch 4 ;;
     benchnocrc) step bench_nocrc 600 python bench.py --stats --steps 4000 --warmup 100 --no-crc ;;
     benchzc) step bench_zc 600 python bench.py --stats --steps 4000 --warmup 100 --h2d zerocopy ;;
     benchs1) step bench_s1 600 python bench.py --stats --steps 4000 --warmup 100 --copy-streams 1 ;;
