@@ -145,6 +145,59 @@ def main():
                     "torch_gpu_us": round(g_torch, 2), "torch_GBps": round(nbytes / g_torch / 1e3, 1),
                     "eager_us": round(t_ours, 2), "torch_eager_us": round(t_torch, 2)})
 
+    # device JSON parse (json_parse.hip) from HBM: text bytes parsed per second, against the
+    # workers' native host parser on the same rows (no PyTorch GPU equivalent exists)
+    import random
+    import time
+
+    import numpy as np
+
+    from torchkafka_amd.ops.native import core
+
+    rnd = random.Random(0)
+    for name, rows in (("config4 256 rows JSON -> bf16", 256), ("4096 rows JSON -> bf16", 4096)):
+        texts = []
+        for _ in range(rows):
+            n = rnd.randint(16, 256)
+            texts.append(("[" + ", ".join("%.2f" % rnd.uniform(-50, 51) for _ in range(n)) + "]").encode())
+        desc = np.zeros((rows, 4), dtype=np.int32)
+        blob = bytearray()
+        for i, t in enumerate(texts):
+            at = (len(blob) + 31) // 32 * 32
+            blob.extend(b"\0" * (at - len(blob)))
+            cnt = core().json_scan_simple(t)
+            desc[i] = (at, len(t), cnt, cnt)
+            blob.extend(t)
+        blob.extend(b"\0" * 64)
+        L = int(desc[:, 3].max())
+        d_desc = torch.from_numpy(desc).to(dev)
+        d_vals = torch.frombuffer(blob, dtype=torch.uint8).to(dev)
+        o = torch.empty((rows, L), dtype=torch.bfloat16, device=dev)
+        ln = torch.empty(rows, dtype=torch.int64, device=dev)
+        mod = hip()
+
+        def jparse():
+            mod.launch_json_rows(d_desc.data_ptr(), d_vals.data_ptr(), o.data_ptr(), 2, rows, L, 0.0, ln.data_ptr(), 0,
+                                 0, torch.cuda.current_stream(dev).cuda_stream)
+
+        jparse()
+        ref = torch.zeros((rows, L), dtype=torch.float32)
+        for i, t in enumerate(texts):
+            v = json.loads(t)
+            ref[i, : len(v)] = torch.tensor(v, dtype=torch.float64).float()
+        assert torch.equal(o.cpu().view(torch.int16), ref.to(torch.bfloat16).view(torch.int16))
+        g_ours = timeit_graph(jparse, iters)
+        t0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            for t in texts:
+                core().parse_json_f32(t)
+        host_us = (time.perf_counter() - t0) / reps * 1e6
+        text_bytes = sum(len(t) for t in texts)
+        out.append({"kernel": "json_parse", "case": name, "gpu_us": round(g_ours, 2),
+                    "text_GBps": round(text_bytes / g_ours / 1e3, 1), "numbers": int(desc[:, 2].sum()),
+                    "host_parser_us_one_core": round(host_us, 1)})
+
     for r in out:
         print(json.dumps(r))
 
