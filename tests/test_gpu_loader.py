@@ -436,3 +436,36 @@ def test_json_device_parse_error_raises_before_commit(broker):
     # batches 0-3 (offsets 0..39) were clean and committed; the batch holding offset 40 never is
     assert seen >= 50
     assert broker.committed_offsets("g", "e") == {0: 40}
+
+
+def test_json_device_parse_coalesced_batches_on_another_stream(broker):
+    """Batches parsed ahead by a group launch and consumed on a different stream wait for that kernel."""
+    import json
+
+    from torchkafka_amd import DeviceLoader, JsonArray, auto_commit
+
+    rows = {0: [("[" + ", ".join(str(i * 10 + j) for j in range(1 + i % 7)) + "]").encode() for i in range(400)]}
+    broker.create_topic("s", 1)
+    _produce_json(broker, "s", rows)
+    DS = _dataset(JsonArray())
+    dl = DeviceLoader(DS.placeholder(), 16, num_workers=1, device="cuda:0", dtype=torch.float32, coalesce=8,
+                      slots_per_worker=8, json_parse="device",
+                      worker_init_fn=DS.init_worker("s", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    side = [torch.cuda.Stream(), torch.cuda.Stream()]
+    got = []
+    it = iter(auto_commit(dl))
+    k = 0
+    while True:
+        with torch.cuda.stream(side[k % 2]):
+            try:
+                x, lens = next(it)
+            except StopIteration:
+                break
+            y = x * 1.0  # consume on this stream
+            got += [y[i, : int(lens[i])].tolist() for i in range(y.shape[0])]
+        k += 1
+    torch.cuda.synchronize()
+    ref = [[float(v) for v in json.loads(r)] for r in rows[0]]
+    assert got == ref
+    assert broker.committed_offsets("g", "s") == {0: 400}
