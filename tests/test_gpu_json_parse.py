@@ -167,3 +167,45 @@ def test_json_rows_grammar_errors_flag_the_row(bad):
     out, _lengths, _mask, err, _ = _run(texts, torch.float32)
     assert err == 1
     assert out[0, :2].tolist() == [1.0, 2.0] and out[2, 0].item() == 3.0
+
+
+def test_json_rows_fuzz_matches_host_parser_verdicts():
+    """Random character-clean rows (what the worker sends to the device): the kernel accepts exactly
+    the rows the host parser accepts, with identical float32 values, and flags the others."""
+    from torchkafka_amd.ops.native import core
+
+    c = core()
+    rnd = random.Random(99)
+    alphabet = "0123456789.-, "
+    good, bad = [], []
+    while len(good) < 300 or len(bad) < 60:
+        k = rnd.random()
+        if k < 0.5:
+            body = "".join(rnd.choice(alphabet) for _ in range(rnd.randint(0, 60)))
+        else:
+            toks = []
+            for _ in range(rnd.randint(1, 40)):
+                t = "".join(rnd.choice("0123456789.-") for _ in range(rnd.randint(1, 16)))
+                toks.append(t)
+            body = rnd.choice([",", ", ", " , "]).join(toks)
+        row = ("[" + body + "]").encode()
+        if c.json_scan_simple(row) < 0:
+            continue  # the worker parses it on the host
+        try:
+            c.parse_json_f32(row)
+            ok = True
+        except ValueError:
+            ok = False
+        (good if ok else bad).append(row)
+    good, bad = good[:300], bad[:60]
+    # valid rows: one launch, identical values
+    out, lengths, _m, err, desc = _run(good, torch.float32)
+    assert err == -1
+    for i, row in enumerate(good):
+        want = torch.tensor(c.parse_json_f32(row), dtype=torch.float32)
+        got = out[i, : int(lengths[i])]
+        assert torch.equal(got.view(torch.int32), want.view(torch.int32)), row
+    # each malformed row is flagged (one launch per row, so the flagged index is unambiguous)
+    for row in bad:
+        _o, _l, _m, err, _d = _run([b"[1]", row], torch.float32)
+        assert err == 1, row
