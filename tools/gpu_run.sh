@@ -87,6 +87,7 @@ for s in $STEPS; do
     config5direct) step config5_direct 300 python benchmarks/config5_large_messages.py --h2d direct ;;
     config5w8) step config5_w8 300 python benchmarks/config5_large_messages.py --workers 8 ;;
     example3) step example3 300 python examples/03_device_loader_training.py ;;
+    example4) step example4 300 python examples/04_json_device_parse.py ;;
     kbench) step kernel_bench 300 python tools/kernel_bench.py ;;
     kprof)  (cd /tmp && export TMPDIR=/tmp && step kprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kprof" -o run -- python3 "$OLDPWD/tools/kernel_bench.py" --quick) || exit $? ;;
     # TCC has 4 slots per pass: FETCH_SIZE costs 3, WRITE_SIZE 2 (MI355X_MICROARCH.md) -> two passes
