@@ -237,3 +237,19 @@ def test_producer_partitioning_and_futures(broker):
     assert set(rr) == {0, 1, 2, 3}
     p.close()
     assert sum(broker.end_offsets("t").values()) == 38
+
+
+def test_poll_without_update_offsets_peeks(broker):
+    broker.create_topic("t", 1)
+    broker.produce("t", [b"a", b"b", b"c"], partition=0)
+    c = consumer(broker, "t")
+    tp = TopicPartition("t", 0)
+    peek = {}
+    deadline = time.time() + 2
+    while not peek and time.time() < deadline:
+        peek = c.poll(timeout_ms=50, max_records=2, update_offsets=False)
+    assert [r.offset for r in peek[tp]] == [0, 1]
+    assert c.position(tp) == 0
+    got = c.poll(timeout_ms=500, max_records=2)
+    assert [r.offset for r in got[tp]] == [0, 1]
+    assert c.position(tp) == 2

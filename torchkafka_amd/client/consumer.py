@@ -423,10 +423,12 @@ class KafkaConsumer:
 
     # ------------------------------------------------------------------ fetching
     def poll(self, timeout_ms: int = 0, max_records: int | None = None, update_offsets: bool = True) -> dict:
-        """Returns ``{TopicPartition: [ConsumerRecord]}``; waits up to ``timeout_ms`` for data."""
+        """Returns ``{TopicPartition: [ConsumerRecord]}``; waits up to ``timeout_ms`` for data.
+
+        ``update_offsets=False`` peeks: the records stay buffered and positions do not move, so the next
+        ``poll``/``next`` returns them again (kafka-python's semantics).
+        """
         self._check_open()
-        if not update_offsets:
-            raise NotImplementedError("update_offsets=False is not supported")
         max_records = max_records or self.config["max_poll_records"]
         deadline = time.monotonic() + timeout_ms / 1000.0
         backoff = 0.0002
@@ -437,6 +439,11 @@ class KafkaConsumer:
                 self._fetch_into_buffer(max_records)
             if self._buffer:
                 out: dict = {}
+                if not update_offsets:
+                    for i in range(min(max_records, len(self._buffer))):
+                        r = self._buffer[i][1]
+                        out.setdefault(TopicPartition(r.topic, r.partition), []).append(r)
+                    return out
                 for _ in range(min(max_records, len(self._buffer))):
                     pidx, r = self._buffer.popleft()
                     rec = self._make_record(pidx, r)
