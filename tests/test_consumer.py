@@ -253,3 +253,23 @@ def test_poll_without_update_offsets_peeks(broker):
     got = c.poll(timeout_ms=500, max_records=2)
     assert [r.offset for r in got[tp]] == [0, 1]
     assert c.position(tp) == 2
+
+
+def test_offsets_for_times(broker):
+    broker.create_topic("t", 2)
+    broker.produce("t", [b"a", b"b", b"c"], partition=0, timestamps=[100, 200, 300])
+    broker.produce("t", [b"d", b"e"], partition=0, timestamps=[250, 400])
+    broker.produce("t", [b"x"], partition=1, timestamps=[50])
+    c = consumer(broker, "t")
+    tp0, tp1 = TopicPartition("t", 0), TopicPartition("t", 1)
+    got = c.offsets_for_times({tp0: 150, tp1: 10})
+    assert (got[tp0].offset, got[tp0].timestamp) == (1, 200)
+    assert (got[tp1].offset, got[tp1].timestamp) == (0, 50)
+    # first record at or after the time, not the first batch whose max covers it
+    assert c.offsets_for_times({tp0: 240})[tp0] == (2, 300)
+    assert c.offsets_for_times({tp0: 350})[tp0] == (4, 400)
+    assert c.offsets_for_times({tp0: 401, tp1: 51}) == {tp0: None, tp1: None}
+    broker.delete_records("t", 0, 2)
+    assert c.offsets_for_times({tp0: 0})[tp0] == (2, 300)
+    with pytest.raises(ValueError):
+        c.offsets_for_times({tp0: -1})

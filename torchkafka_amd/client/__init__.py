@@ -5,8 +5,8 @@ from .errors import (
     OffsetOutOfRangeError,
 )
 from .producer import KafkaProducer
-from .records import ConsumerRecord, OffsetAndMetadata, RecordMetadata, TopicPartition
+from .records import ConsumerRecord, OffsetAndMetadata, OffsetAndTimestamp, RecordMetadata, TopicPartition
 
-__all__ = ["KafkaConsumer", "KafkaProducer", "ConsumerRecord", "TopicPartition", "OffsetAndMetadata",
+__all__ = ["KafkaConsumer", "KafkaProducer", "ConsumerRecord", "TopicPartition", "OffsetAndMetadata", "OffsetAndTimestamp",
            "RecordMetadata", "KafkaError", "CommitFailedError", "CorruptRecordException", "NoBrokersAvailable",
            "OffsetOutOfRangeError", "KafkaConfigurationError"]

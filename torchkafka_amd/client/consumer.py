@@ -33,7 +33,7 @@ from .errors import (
     CommitFailedError, IllegalStateError, KafkaConfigurationError, NoOffsetForPartitionError,
     OffsetOutOfRangeError,
 )
-from .records import ConsumerRecord, OffsetAndMetadata, TopicPartition
+from .records import ConsumerRecord, OffsetAndMetadata, OffsetAndTimestamp, TopicPartition
 
 _getpid = os.getpid
 log = logging.getLogger(__name__)
@@ -394,6 +394,16 @@ class KafkaConsumer:
 
     def end_offsets(self, partitions) -> dict:
         return {tp: self._b.high_watermark(self._pidx(tp)) for tp in partitions}
+
+    def offsets_for_times(self, timestamps: dict) -> dict:
+        """``{tp: ts_ms}`` -> ``{tp: OffsetAndTimestamp | None}``: earliest offset whose timestamp is >= ts."""
+        out = {}
+        for tp, ts in timestamps.items():
+            if int(ts) < 0:
+                raise ValueError(f"The target time for partition {tp} is {ts}. It should be non-negative.")
+            off, rts = self._b.offset_for_time(self._pidx(tp), int(ts))
+            out[tp] = OffsetAndTimestamp(off, rts) if off >= 0 else None
+        return out
 
     def highwater(self, partition: TopicPartition) -> int:
         return self._b.high_watermark(self._pidx(partition))

@@ -16,6 +16,7 @@ ConsumerRecord = namedtuple(
 TopicPartition = namedtuple("TopicPartition", ["topic", "partition"])
 
 OffsetAndMetadata = namedtuple("OffsetAndMetadata", ["offset", "metadata"])
+OffsetAndTimestamp = namedtuple("OffsetAndTimestamp", ["offset", "timestamp"])
 
 RecordMetadata = namedtuple(
     "RecordMetadata",

@@ -245,6 +245,7 @@ PYBIND11_MODULE(_tkcore, m) {
              return py::bytes(reinterpret_cast<const char*>(b.log_base(p)) + off, n);
            },
            py::arg("pidx"), py::arg("offset"), py::arg("n"), "raw bytes of a partition log (tests, tools)")
+      .def("offset_for_time", &Broker::offset_for_time, py::arg("pidx"), py::arg("timestamp"))
       .def("partition_stats",
            [](Broker& b, uint32_t p) {
              auto& P = b.part(p);

@@ -322,6 +322,24 @@ int64_t Broker::find_batch(uint32_t pidx, int64_t offset, int64_t hint) {
   return i;
 }
 
+std::pair<int64_t, int64_t> Broker::offset_for_time(uint32_t pidx, int64_t ts) {
+  const PartitionEntry& P = part(pidx);
+  const Mapped& m = mapped(pidx);
+  const int64_t nb = int64_t(P.n_batches.load(std::memory_order_acquire));
+  const int64_t start = P.log_start_offset.load(std::memory_order_acquire);
+  for (int64_t i = 0; i < nb; ++i) {
+    const IndexEntry& e = m.idx[i];
+    if (e.base_offset + e.last_offset_delta < start || e.max_timestamp < ts) continue;
+    const uint8_t* bp = m.log + e.pos;
+    BatchHeader h = parse_batch_header(bp, e.size);
+    RecordIter it(bp, h);
+    RecordView r;
+    while (it.next(&r))
+      if (r.offset >= start && r.timestamp >= ts) return {r.offset, r.timestamp};
+  }
+  return {-1, -1};
+}
+
 // ------------------------------------------------------------ produce
 int64_t Broker::append(uint32_t pidx, const RecordIn* recs, size_t n) {
   if (n == 0) throw std::invalid_argument("empty batch");

@@ -22,6 +22,7 @@
 #include <pthread.h>
 
 #include <atomic>
+#include <utility>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -166,6 +167,9 @@ class Broker {
   const IndexEntry* index_base(uint32_t pidx);
   // Index of the batch containing `offset` (requires log_start <= offset < hw), hint = last result.
   int64_t find_batch(uint32_t pidx, int64_t offset, int64_t hint) ;
+  // ListOffsets-by-timestamp: earliest retained record with timestamp >= ts, as {offset, timestamp};
+  // {-1, -1} when none.  Skips whole batches by the index's max_timestamp.
+  std::pair<int64_t, int64_t> offset_for_time(uint32_t pidx, int64_t ts);
 
   // ---- produce: appends one batch, returns its base offset.
   int64_t append(uint32_t pidx, const RecordIn* recs, size_t n);
