@@ -273,3 +273,23 @@ def test_offsets_for_times(broker):
     assert c.offsets_for_times({tp0: 0})[tp0] == (2, 300)
     with pytest.raises(ValueError):
         c.offsets_for_times({tp0: -1})
+
+
+def test_producer_future_callbacks_and_errbacks(broker):
+    broker.create_topic("t", 1)
+    p = KafkaProducer(bootstrap_servers=broker.url)
+    seen, errs = [], []
+    fut = p.send("t", b"v0").add_callback(seen.append).add_errback(errs.append)
+    assert not fut.is_done and not fut.succeeded() and fut.value is None
+    p.flush()
+    assert fut.is_done and fut.succeeded() and not fut.failed()
+    assert [m.offset for m in seen] == [0] and fut.value.offset == 0 and not errs
+    late = []
+    fut.add_callback(lambda tag, md: late.append((tag, md.offset)), "x")  # already resolved: runs at once
+    assert late == [("x", 0)]
+    bad = p.send("t", b"v1", partition=7).add_errback(errs.append)  # no partition 7: fails at flush
+    p.flush()
+    assert bad.failed() and bad.is_done and len(errs) == 1 and bad.exception is errs[0]
+    with pytest.raises(type(errs[0])):
+        bad.get()
+    p.close()

@@ -10,6 +10,7 @@ partitioner is Kafka's: murmur2(key) for keyed records, round-robin otherwise.
 from __future__ import annotations
 
 import copy
+import functools
 import itertools
 import threading
 import time
@@ -56,22 +57,68 @@ def default_partition(key: bytes | None, n_partitions: int, counter) -> int:
 
 
 class FutureRecordMetadata:
+    """kafka-python's send() future: ``get``, ``is_done``, ``succeeded()``/``failed()``, ``value``/``exception``
+    and ``add_callback``/``add_errback`` (run at flush time, or at once when already resolved)."""
+
     def __init__(self, producer: "KafkaProducer", tp: TopicPartition, idx: int, ts: int, ksize: int, vsize: int):
         self._producer, self._tp, self._idx, self._ts = producer, tp, idx, ts
         self._ksize, self._vsize = ksize, vsize
         self._offset = None
+        self.exception = None
+        self._callbacks: list = []
+        self._errbacks: list = []
 
-    def _resolve(self, base: int) -> None:
-        self._offset = base + self._idx
-
-    def get(self, timeout=None) -> RecordMetadata:
-        if self._offset is None:
-            self._producer.flush()
+    def _metadata(self) -> RecordMetadata:
         return RecordMetadata(self._tp.topic, self._tp.partition, self._tp, self._offset, self._ts, None,
                               self._ksize, self._vsize, -1)
 
+    def _resolve(self, base: int) -> None:
+        self._offset = base + self._idx
+        md = self._metadata()
+        for f in self._callbacks:
+            f(md)
+
+    def _fail(self, exc: BaseException) -> None:
+        self.exception = exc
+        for f in self._errbacks:
+            f(exc)
+
+    @property
     def is_done(self) -> bool:
+        return self._offset is not None or self.exception is not None
+
+    @property
+    def value(self):
+        return self._metadata() if self._offset is not None else None
+
+    def succeeded(self) -> bool:
         return self._offset is not None
+
+    def failed(self) -> bool:
+        return self.exception is not None
+
+    def add_callback(self, fn, *args, **kwargs) -> "FutureRecordMetadata":
+        f = functools.partial(fn, *args, **kwargs)
+        if self._offset is not None:
+            f(self._metadata())
+        else:
+            self._callbacks.append(f)
+        return self
+
+    def add_errback(self, fn, *args, **kwargs) -> "FutureRecordMetadata":
+        f = functools.partial(fn, *args, **kwargs)
+        if self.exception is not None:
+            f(self.exception)
+        else:
+            self._errbacks.append(f)
+        return self
+
+    def get(self, timeout=None) -> RecordMetadata:
+        if not self.is_done:
+            self._producer.flush()
+        if self.exception is not None:
+            raise self.exception
+        return self._metadata()
 
 
 class KafkaProducer:
@@ -145,9 +192,14 @@ class KafkaProducer:
             self._pending_bytes.pop(tp, None)
         if not recs:
             return
-        base = self._broker.produce(tp.topic, [r[0] for r in recs], partition=tp.partition,
-                                    keys=[r[1] for r in recs], timestamps=[r[2] for r in recs],
-                                    headers=[r[3] for r in recs])
+        try:
+            base = self._broker.produce(tp.topic, [r[0] for r in recs], partition=tp.partition,
+                                        keys=[r[1] for r in recs], timestamps=[r[2] for r in recs],
+                                        headers=[r[3] for r in recs])
+        except Exception as exc:  # noqa: BLE001 - handed to the futures, as kafka-python does
+            for r in recs:
+                r[4]._fail(exc)
+            return
         for r in recs:
             r[4]._resolve(base)
 
