@@ -19,6 +19,7 @@ Additions for the framework (not in kafka-python):
 from __future__ import annotations
 
 import copy
+import itertools
 import logging
 import os
 import time
@@ -450,8 +451,7 @@ class KafkaConsumer:
             if self._buffer:
                 out: dict = {}
                 if not update_offsets:
-                    for i in range(min(max_records, len(self._buffer))):
-                        r = self._buffer[i][1]
+                    for _, r in itertools.islice(self._buffer, max_records):
                         out.setdefault(TopicPartition(r.topic, r.partition), []).append(r)
                     return out
                 for _ in range(min(max_records, len(self._buffer))):
