@@ -293,3 +293,20 @@ def test_producer_future_callbacks_and_errbacks(broker):
     with pytest.raises(type(errs[0])):
         bad.get()
     p.close()
+
+
+def test_commit_async_future(broker):
+    broker.create_topic("t", 1)
+    broker.produce("t", [b"a", b"b"], partition=0)
+    c = consumer(broker, "t", group_id="ga")
+    assert len(list(c)) == 2
+    seen = []
+    fut = c.commit_async(callback=lambda offs, exc: seen.append(exc))
+    assert fut.is_done and fut.succeeded() and seen == [None]
+    assert broker.committed("ga", "t", 0) == 2
+    broker.inject_commit_failures("ga", 1)
+    errs = []
+    fut = c.commit_async().add_errback(errs.append)
+    assert fut.failed() and isinstance(errs[0], CommitFailedError)
+    with pytest.raises(CommitFailedError):
+        fut.get()

@@ -42,6 +42,37 @@ log = logging.getLogger(__name__)
 _GROUP_STABLE = 2
 
 
+class CommitFuture:
+    """Resolved future returned by ``commit_async`` (kafka-python ``Future`` subset)."""
+
+    is_done = True
+
+    def __init__(self):
+        self.exception = None
+        self.value = None
+
+    def succeeded(self) -> bool:
+        return self.exception is None
+
+    def failed(self) -> bool:
+        return self.exception is not None
+
+    def add_callback(self, fn, *args, **kwargs) -> "CommitFuture":
+        if self.exception is None:
+            fn(*args, self.value, **kwargs)
+        return self
+
+    def add_errback(self, fn, *args, **kwargs) -> "CommitFuture":
+        if self.exception is not None:
+            fn(*args, self.exception, **kwargs)
+        return self
+
+    def get(self, timeout=None):
+        if self.exception is not None:
+            raise self.exception
+        return self.value
+
+
 class KafkaConsumer:
     """Consume records from the synthetic broker with kafka-python's API."""
 
@@ -532,16 +563,17 @@ class KafkaConsumer:
                 raise CommitFailedError("CommitFailedError: consumer is not part of an active group")
             self._b.commit(self._g, self._member_slot, self._member_id, self._generation, entries)
 
-    def commit_async(self, offsets=None, callback=None):
-        """Commit without a future API: performed synchronously, ``callback(offsets, exc_or_none)`` after."""
-        exc = None
+    def commit_async(self, offsets=None, callback=None) -> "CommitFuture":
+        """kafka-python's async commit.  The shared-memory commit takes well under a microsecond, so it runs
+        inline; ``callback(offsets, exc_or_none)`` follows and the returned future is already resolved."""
+        fut = CommitFuture()
         try:
             self.commit(offsets)
         except CommitFailedError as e:
-            exc = e
+            fut.exception = e
         if callback is not None:
-            callback(offsets, exc)
-        return exc
+            callback(offsets, fut.exception)
+        return fut
 
     # ------------------------------------------------------------------ lifecycle
     def close(self, autocommit: bool = True) -> None:
