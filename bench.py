@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--coalesce", type=int, default=8, help="staged batches collated per kernel launch")
     ap.add_argument("--coalesce-wait-us", type=int, default=50, help="adaptive coalescing wait while the GPU is busy")
     ap.add_argument("--no-numa", action="store_true", help="do not bind ranks to their GPU's NUMA node")
+    ap.add_argument("--steady-steps", type=int, default=None,
+                    help="steps of the steady-state block timed after the headline (default: max(50 x ring "
+                         "slots, 4000); 0 skips it)")
     return ap.parse_args()
 
 
@@ -100,7 +103,9 @@ def main() -> int:
     # backlog per owned partition: every batch the timed loop and the warm-up consume, plus what the
     # workers prefetch into their ring slots, with headroom
     mine = shard_partitions(n_parts, rank, world)
-    batches = args.warmup + args.steps + args.workers * ((args.slots_per_worker or 8) + 2)
+    ring_guess = args.workers * (args.slots_per_worker or 8)
+    steady = args.steady_steps if args.steady_steps is not None else max(50 * ring_guess, 4000)
+    batches = args.warmup + args.steps + steady + args.workers * ((args.slots_per_worker or 8) + 2)
     per_part = int(math.ceil(batches * B * 1.25 / max(1, len(mine)))) + B
     t_fill = time.perf_counter()
     broker.fill("bench", per_part, "fixed_f32", size=args.dim, partitions=mine,
@@ -137,6 +142,8 @@ def main() -> int:
         x = next(it)
     sync()
     loader.reset_stats()
+    # what the workers filled ahead of the consumer: a short timed region may only drain these
+    occ = loader.ring_occupancy()
     t0 = time.perf_counter()
     rows = 0
     for _ in range(args.steps):
@@ -146,17 +153,51 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     stats = loader.stats_summary()
 
-    # whole-job aggregate: records of every rank over the slowest rank's time
-    if world > 1:
-        t = torch.tensor([elapsed, float(rows)], dtype=torch.float64,
-                         device=device if device.type == "cuda" else "cpu")
+    def job_rate(el: float, nrows: int) -> tuple[float, float]:
+        """whole-job aggregate: records of every rank over the slowest rank's time"""
+        if world == 1:
+            return el, float(nrows)
+        t = torch.tensor([el, float(nrows)], dtype=torch.float64, device=device if device.type == "cuda" else "cpu")
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        elapsed, total_rows = float(tmax[0]), float(t[1])
-    else:
-        total_rows = float(rows)
+        return float(tmax[0]), float(t[1])
+
+    elapsed, total_rows = job_rate(elapsed, rows)
     value = total_rows / elapsed
+
+    # Steady state, same process, right after the headline: many times the ring depth, so the
+    # batches the workers had prefilled before t0 are a small part of it and the producer side
+    # (fetch, pack, publish) is inside the timed region.
+    steady_out = None
+    if steady > 0:
+        n_slots = occ["n_slots"] or ring_guess
+        s_steps = steady
+        loader.reset_stats()
+        sync()
+        occ_s = loader.ring_occupancy()
+        t1 = time.perf_counter()
+        srows = 0
+        for _ in range(s_steps):
+            x = next(it)
+            srows += x.shape[0]
+        sync()
+        s_el, s_total = job_rate(time.perf_counter() - t1, srows)
+        s_stats = loader.stats_summary()
+        steady_out = {
+            "steps": s_steps,
+            "timed_s": round(s_el, 6),
+            "records_per_s": round(s_total / s_el, 1),
+            "ms_per_step": round(s_el / s_steps * 1000, 4),
+            "gb_per_s": round(s_total / s_el * args.dim * 4 / 1e9, 3),
+            "ring_slots": n_slots,
+            "prefilled_slots_at_t0": occ_s["prefilled"],
+            "steps_per_ring": round(s_steps / max(1, n_slots), 1),
+            "vs_baseline": round(s_total / s_el / BASELINE_VALUE, 3),
+            "commit_p50_us": round(s_stats["commit_p50_us"], 2),
+            "commit_p99_us": round(s_stats["commit_p99_us"], 2),
+            "worker_fill_us_per_batch": round(s_stats.get("worker_fill_us_per_batch", 0.0), 2),
+        }
 
     # check what landed on the device: the last batch's records must be this rank's partitions
     xf = x.float()
@@ -197,6 +238,10 @@ def main() -> int:
                 "gb_per_s": round(value * args.dim * 4 / 1e9, 3),
                 "commit_p99_us": round(stats["commit_p99_us"], 2),
             },
+            "timed_region_s": round(elapsed, 6),
+            "prefilled_slots_at_t0": occ["prefilled"],
+            "ring_slots": occ["n_slots"],
+            "steady_state": steady_out,
         }
         print(json.dumps(out))
     loader.close()

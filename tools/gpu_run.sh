@@ -39,6 +39,9 @@ for s in $STEPS; do
     lockjson) LOCKCHECK_SCHEMA=json LOCKCHECK_DEPTHS=0,3 step lockstep_json 150 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29634 tools/lockstep_check.py ;;
     lockcheck) step lockstep_check 150 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29631 tools/lockstep_check.py ;;
     bench)  step bench 600 python bench.py --stats ;;
+    benchdrv) step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    benchf32) step bench_f32 600 python bench.py --stats --dtype f32 ;;
+    benchdma2) step bench_dma 600 python bench.py --stats --h2d dma ;;
     bench8) step bench_fp8 600 python bench.py --stats --dtype fp8 ;;
     benchlong) step bench_long 600 python bench.py --stats --steps 4000 --warmup 100 ;;
     benchnonuma) step bench_nonuma 600 python bench.py --stats --steps 4000 --warmup 100 --no-numa ;;

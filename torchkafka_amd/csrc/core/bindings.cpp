@@ -562,6 +562,17 @@ PYBIND11_MODULE(_tkcore, m) {
              std::vector<int64_t> shape(h->shape, h->shape + h->ndim);
              return py::make_tuple(h->src_dtype, shape);
            })
+      .def("slot_states",
+           [](PyRing& r) {
+             // FREE / FILLING / READY / INFLIGHT counts: how much of the ring the workers have
+             // filled ahead of the consumer (bench.py's prefilled_slots_at_t0)
+             std::vector<uint32_t> n(4, 0);
+             for (uint32_t g = 0; g < r.r->n_slots(); ++g) {
+               const uint32_t s = r.r->slot(g)->state.load(std::memory_order_acquire);
+               if (s < 4) ++n[s];
+             }
+             return n;
+           })
       .def("set_flags", [](PyRing& r, uint32_t g, uint32_t flags) { r.r->slot(g)->flags |= flags; })
       .def("set_error",
            [](PyRing& r, uint32_t g, const std::string& msg) {

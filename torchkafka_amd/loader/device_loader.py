@@ -1034,6 +1034,18 @@ class DeviceLoader:
             self._absorb_driver_stats(run.driver)
         self._commit_finished(wait=True)
 
+    def ring_occupancy(self) -> dict:
+        """Slots of the live iteration's ring by state: ``ready`` (published by a worker, not yet
+        taken), ``inflight`` (taken by the main process: staged, collated ahead or still read by
+        the GPU), ``filling`` and ``free``; ``prefilled`` = ready + inflight, the batches a timed
+        region starting now would not have to wait for."""
+        run = self._run
+        if run is None or run.closed:
+            return {"free": 0, "filling": 0, "ready": 0, "inflight": 0, "prefilled": 0, "n_slots": 0}
+        free, filling, ready, inflight = run.ring.slot_states()
+        return {"free": free, "filling": filling, "ready": ready, "inflight": inflight,
+                "prefilled": ready + inflight, "n_slots": run.ring.n_slots}
+
     def reset_stats(self) -> None:
         """Zeroes the loader's counters (and the native driver's) -- e.g. after warm-up."""
         self.stats.reset()
