@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--coalesce", type=int, default=8, help="staged batches collated per kernel launch")
     ap.add_argument("--coalesce-wait-us", type=int, default=50, help="adaptive coalescing wait while the GPU is busy")
     ap.add_argument("--no-numa", action="store_true", help="do not bind ranks to their GPU's NUMA node")
+    ap.add_argument("--decode", default="auto", choices=["auto", "device", "host"],
+                    help="device: gfx950 RecordBatch decode + CRC from the pinned logs; host: workers CRC-check + pack")
     ap.add_argument("--steady-steps", type=int, default=None,
                     help="steps of the steady-state block timed after the headline (default: max(50 x ring "
                          "slots, 4000); 0 skips it)")
@@ -121,7 +123,7 @@ def main() -> int:
         slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
         in_order=args.in_order, h2d=args.h2d, copy_streams=args.copy_streams, lockstep_depth=args.lockstep_depth,
         event_every=args.event_every, numa_bind=not args.no_numa, coalesce=args.coalesce,
-        coalesce_wait_us=args.coalesce_wait_us,
+        coalesce_wait_us=args.coalesce_wait_us, decode=args.decode,
         worker_init_fn=Records.init_worker("bench", bootstrap_servers=url, group_id="bench",
                                            auto_offset_reset="earliest", check_crcs=not args.no_crc),
     )
@@ -234,6 +236,7 @@ def main() -> int:
                 "num_workers": args.workers,
                 "commit": "auto_commit per batch" + (", RCCL lockstep" if world > 1 else ""),
                 "h2d": loader._resolve_h2d(loader._slot_capacity()) if device.type == "cuda" else "n/a (cpu)",
+                "decode": "device (gfx950 CRC32C + decode from pinned logs)" if loader._span() else "host workers",
                 "bytes_per_step_per_gpu": B * args.dim * 4,
                 "gb_per_s": round(value * args.dim * 4 / 1e9, 3),
                 "commit_p99_us": round(stats["commit_p99_us"], 2),

@@ -1,0 +1,209 @@
+"""gfx950 RecordBatch decode (DeviceLoader decode='device', csrc/hip/span_decode.hip) on the GPU.
+
+The kernel reads record values straight out of the pinned broker logs, verifies the CRC32C of
+every RecordBatch (kafka-python's check_crcs, reference kafka_dataset.py:156 loop) and casts the
+values; every case is compared bit for bit with the host path (decode='host': workers CRC-check
+and pack, the collate kernel casts), which tests/test_gpu_kernels.py pins to Tensor.to.
+"""
+import os
+import random
+
+import pytest
+import torch
+
+from conftest import synth_f32
+
+pytestmark = pytest.mark.gpu
+
+
+def _dataset(schema):
+    from torchkafka_amd import KafkaDataset
+
+    class DS(KafkaDataset):
+        pass
+
+    DS.schema = schema
+    return DS
+
+
+def _bits(t: torch.Tensor) -> torch.Tensor:
+    return t.view({1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[t.element_size()])
+
+
+def _run(broker, topic, DS, decode, bs, group, **kw):
+    from torchkafka_amd import DeviceLoader, auto_commit
+
+    dl = DeviceLoader(DS.placeholder(), bs, device="cuda:0", decode=decode,
+                      worker_init_fn=DS.init_worker(topic, bootstrap_servers=broker.url, group_id=group,
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300), **kw)
+    assert dl._span() == (decode == "device")
+    xs = [x.clone() for x in auto_commit(dl)]
+    torch.cuda.synchronize()
+    return torch.cat(xs) if xs else None, dl
+
+
+def _produce_random(broker, topic, n_parts, n_per_part, nbytes, rpb=16, seed=0, nulls=False):
+    rng = random.Random(seed)
+    for p in range(n_parts):
+        vals, keys = [], []
+        for o in range(n_per_part):
+            vals.append(None if nulls and o % 5 == 2 else bytes(rng.getrandbits(8) for _ in range(nbytes)))
+            keys.append(b"k" * rng.randrange(0, 9))  # shifts every value's alignment in the log
+        for i in range(0, n_per_part, rpb):
+            broker.produce(topic, vals[i:i + rpb], partition=p, keys=keys[i:i + rpb])
+
+
+@pytest.mark.parametrize("shape,src,dst,norm,bs,rpb,workers", [
+    ((256,), torch.float32, torch.bfloat16, False, 64, 64, 2),   # config 2's record shape
+    ((256,), torch.float32, torch.float32, False, 50, 16, 1),    # batch boundaries inside RecordBatches
+    ((13,), torch.float32, torch.float32, False, 33, 7, 2),      # 52-byte rows: partial 16-byte groups
+    ((40,), torch.bfloat16, torch.float32, False, 32, 5, 1),     # 2-byte source elements
+    ((48,), torch.uint8, torch.float16, False, 32, 9, 1),        # 1-byte source elements
+    ((64,), torch.float32, torch.float8_e4m3fn, False, 40, 8, 2),
+    ((64,), torch.float32, torch.bfloat16, True, 32, 16, 1),     # fused normalisation
+    ((12000,), torch.float32, torch.bfloat16, False, 8, 4, 1),   # 192 KB RecordBatches: CRC chained over segments
+    ((3,), torch.int32, torch.int64, False, 1000, 400, 1),       # tiny rows, many rows per segment
+])
+def test_device_decode_matches_host_path(broker, shape, src, dst, norm, bs, rpb, workers):
+    numel = 1
+    for d in shape:
+        numel *= d
+    esize = torch.empty((), dtype=src).element_size()
+    n = 120 if numel < 1000 else 24
+    broker.create_topic("t", 3)
+    _produce_random(broker, "t", 3, n, numel * esize, rpb=rpb)
+    from torchkafka_amd import FixedWidth
+
+    DS = _dataset(FixedWidth(src, shape))
+    normalize = (0.5, 2.0) if norm else None
+    outs = {}
+    for decode in ("host", "device"):
+        outs[decode], _dl = _run(broker, "t", DS, decode, bs, f"g-{decode}", num_workers=workers, dtype=dst,
+                                 normalize=normalize, in_order=True, coalesce=4)
+        assert broker.committed_offsets(f"g-{decode}", "t") == {0: n, 1: n, 2: n}
+    a, b = outs["host"], outs["device"]
+    assert a.shape == b.shape == (3 * n, *shape)
+    assert torch.equal(_bits(a), _bits(b))
+
+
+def test_device_decode_values_and_commits(broker):
+    """Known record contents (the synthetic f32 generator), several workers, exactly-once delivery."""
+    from torchkafka_amd import FixedWidth
+
+    broker.create_topic("t", 6)
+    broker.fill("t", 300, "fixed_f32", size=32, records_per_batch=50)
+    DS = _dataset(FixedWidth(torch.float32, (32,)))
+    x, dl = _run(broker, "t", DS, "device", 64, "g", num_workers=3)
+    seen = set()
+    for row in x.cpu():
+        o, p = int(row[0]), int(row[1])
+        assert torch.equal(row, torch.tensor([synth_f32(p, o, j) for j in range(32)]))
+        assert (p, o) not in seen
+        seen.add((p, o))
+    assert len(seen) == 1800
+    assert broker.committed_offsets("g", "t") == {p: 300 for p in range(6)}
+    assert dl.stats.log_bytes_registered > 0
+
+
+def test_device_decode_skips_null_values_like_host(broker):
+    from torchkafka_amd import FixedWidth
+
+    broker.create_topic("t", 2)
+    _produce_random(broker, "t", 2, 200, 64, rpb=11, nulls=True)
+    DS = _dataset(FixedWidth(torch.float32, (16,)))
+    a, _ = _run(broker, "t", DS, "host", 30, "gh", num_workers=1, in_order=True)
+    b, _ = _run(broker, "t", DS, "device", 30, "gd", num_workers=1, in_order=True)
+    assert a.shape == b.shape == (2 * 160, 16)
+    assert torch.equal(_bits(a), _bits(b))
+    assert broker.committed_offsets("gd", "t") == {0: 200, 1: 200}
+
+
+def _corrupt(broker, pidx, pos):
+    path = os.path.join(broker.native.dir, f"p{pidx:05d}.log")
+    with open(path, "r+b") as f:
+        f.seek(pos)
+        b = f.read(1)
+        f.seek(pos)
+        f.write(bytes([b[0] ^ 0x5A]))
+
+
+@pytest.mark.parametrize("size,rpb", [(64, 10), (12000, 4)])
+def test_device_decode_crc_failure_raises_before_commit(broker, size, rpb):
+    """A flipped value byte (the worker never reads values) is caught by the device CRC: the
+    batch holding it is never committed and CorruptRecordException names its RecordBatch.
+    size 12000 floats: the RecordBatch is split over segments, its CRC chained on the host."""
+    from torchkafka_amd import FixedWidth
+    from torchkafka_amd.client.errors import CorruptRecordException
+
+    broker.create_topic("c", 1)
+    n = 100 if size < 1000 else 24
+    broker.fill("c", n, "fixed_f32", size=size, records_per_batch=rpb)
+    pidx = broker.pidx("c", 0)
+    # corrupt a value byte of the record at offset 4 * rpb + 1 (RecordBatch 4)
+    row_bytes = size * 4
+    bad_rb = 4
+    log = broker.native.read_log(pidx, 0, broker.native.log_bytes(pidx))
+    pos, k = 0, 0
+    while k < bad_rb:
+        pos += 12 + int.from_bytes(log[pos + 8:pos + 12], "big")
+        k += 1
+    _corrupt(broker, pidx, pos + 61 + 30 + row_bytes // 2)
+    DS = _dataset(FixedWidth(torch.float32, (size,)))
+    from torchkafka_amd import DeviceLoader, auto_commit
+
+    bs = rpb
+    dl = DeviceLoader(DS.placeholder(), bs, num_workers=1, device="cuda:0", decode="device", coalesce=1,
+                      worker_init_fn=DS.init_worker("c", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    with pytest.raises(CorruptRecordException, match=f"offset {bad_rb * rpb} .*failed CRC check"):
+        for _x in auto_commit(dl):
+            torch.cuda.synchronize()
+    committed = broker.committed_offsets("g", "c").get(0)
+    assert committed is not None and committed <= bad_rb * rpb
+
+
+def test_device_decode_without_crc_checks(broker):
+    """check_crcs=False: no verification anywhere (kafka-python semantics), only values are read."""
+    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
+
+    broker.create_topic("t", 2)
+    broker.fill("t", 200, "fixed_f32", size=32, records_per_batch=20)
+    DS = _dataset(FixedWidth(torch.float32, (32,)))
+    dl = DeviceLoader(DS.placeholder(), 64, num_workers=1, device="cuda:0", decode="device",
+                      worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300,
+                                                    check_crcs=False))
+    n = 0
+    for x in auto_commit(dl):
+        n += x.shape[0]
+    assert n == 400 and broker.committed_offsets("g", "t") == {0: 200, 1: 200}
+
+
+def test_device_decode_coalesced_batch_on_another_stream(broker):
+    """Batches decoded ahead by a group launch, consumed on other streams, stay correct."""
+    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
+
+    broker.create_topic("t", 4)
+    broker.fill("t", 256, "fixed_f32", size=64, records_per_batch=32)
+    DS = _dataset(FixedWidth(torch.float32, (64,)))
+    dl = DeviceLoader(DS.placeholder(), 32, num_workers=2, device="cuda:0", decode="device", coalesce=8,
+                      worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    side = [torch.cuda.Stream(), torch.cuda.Stream()]
+    copies = []
+    it = iter(auto_commit(dl))
+    k = 0
+    while True:
+        with torch.cuda.stream(side[k % 2]):
+            try:
+                x = next(it)
+            except StopIteration:
+                break
+            copies.append(x.clone())
+        k += 1
+    torch.cuda.synchronize()
+    rows = torch.cat(copies).cpu()
+    assert rows.shape[0] == 1024
+    for row in rows[::37]:
+        o, p = int(row[0]), int(row[1])
+        assert torch.equal(row, torch.tensor([synth_f32(p, o, j) for j in range(64)]))

@@ -39,6 +39,10 @@ for s in $STEPS; do
     lockjson) LOCKCHECK_SCHEMA=json LOCKCHECK_DEPTHS=0,3 step lockstep_json 150 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29634 tools/lockstep_check.py ;;
     lockcheck) step lockstep_check 150 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29631 tools/lockstep_check.py ;;
     bench)  step bench 600 python bench.py --stats ;;
+    pytestspan) step pytest_span 300 python -u -m pytest tests/test_gpu_span.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    spannocrc) step bench_span_nocrc 300 python bench.py --steps 1000 --steady-steps 4000 --no-crc --stats ;;
+    spanburst) for b in 1 2 4 8; do TORCHKAFKA_SPAN_BURST=$b step bench_burst$b 300 python bench.py --steps 1000 --steady-steps 4000; done ;;
+    benchhost) step bench_host 600 python bench.py --stats --decode host ;;
     benchdrv) step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     benchf32) step bench_f32 600 python bench.py --stats --dtype f32 ;;
     benchdma2) step bench_dma 600 python bench.py --stats --h2d dma ;;
@@ -101,6 +105,7 @@ for s in $STEPS; do
     proflong) (cd /tmp && export TMPDIR=/tmp && step proflong 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/proflong" -o run -- python3 "$OLDPWD/bench.py" --steps 2000 --stats) || exit $? ;;
     profc4t) (cd /tmp && export TMPDIR=/tmp && step profc4t 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/profc4t" -o run -- python3 "$OLDPWD/benchmarks/config4_json_varlen.py" --steps 300) || exit $? ;;
     profc4) (cd /tmp && export TMPDIR=/tmp && step profc4 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profc4" -o run -- python3 "$OLDPWD/benchmarks/config4_json_varlen.py" --steps 300) || exit $? ;;
+    profspan) (cd /tmp && export TMPDIR=/tmp && step profspan 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profspan" -o run -- python3 "$OLDPWD/bench.py" --steps 500 --steady-steps 1000 --stats) || exit $? ;;
     prof)   (cd /tmp && export TMPDIR=/tmp && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$OLDPWD/bench.py" --steps 200) || exit $? ;;
   esac
 done

@@ -124,6 +124,21 @@ PYBIND11_MODULE(_tkcore, m) {
   });
   m.def("crc32c_hw", &crc32c_hw);
   m.def("crc32c_fold", &crc32c_fold);
+  m.def("crc32c_shift_raw", &crc32c_shift_raw, py::arg("raw"), py::arg("n_bytes"));
+  m.def(
+      "crc32c_span_emulate",
+      [](py::bytes b, uint32_t c0, uint32_t c1, bool first) {
+        std::string s = b;
+        if (c0 > c1 || c1 > s.size() || c1 - c0 > kSpanLaneBytes * kSpanLanes)
+          throw std::invalid_argument("crc32c_span_emulate: bad range");
+        return crc32c_span_emulate(reinterpret_cast<const uint8_t*>(s.data()), c0, c1, first);
+      },
+      py::arg("data"), py::arg("c0"), py::arg("c1"), py::arg("first"));
+  m.def("span_tables", []() {
+    std::vector<uint32_t> t(kSpanTabWords);
+    crc32c_span_tables(t.data());
+    return t;
+  });
   m.def("crc32c_method", [](int method, py::bytes b) {
     std::string s = b;
     return crc32c_method(method, s.data(), s.size());
@@ -448,10 +463,11 @@ PYBIND11_MODULE(_tkcore, m) {
           "fill_slot",
           [](PyFetcher& f, py::object ring_obj, uint32_t gslot, int kind, int elem_size, int64_t row_elems,
              int64_t min_len, int64_t max_len, bool truncate, bool skip_bad, int64_t batch_rows, int64_t timeout_ms,
-             bool gather) {
+             bool gather, bool span) {
             PyRing& ring = ring_obj.cast<PyRing&>();
             PackSpec s;
             s.gather = gather;
+            s.span = span;
             s.kind = kind;
             s.elem_size = elem_size;
             s.row_elems = row_elems;
@@ -468,7 +484,7 @@ PYBIND11_MODULE(_tkcore, m) {
           },
           py::arg("ring"), py::arg("gslot"), py::arg("kind"), py::arg("elem_size"), py::arg("row_elems"),
           py::arg("min_len"), py::arg("max_len"), py::arg("truncate"), py::arg("skip_bad"), py::arg("batch_rows"),
-          py::arg("timeout_ms"), py::arg("gather") = false);
+          py::arg("timeout_ms"), py::arg("gather") = false, py::arg("span") = false);
 
   // ---- ring
   py::class_<PyRing>(m, "Ring")
@@ -517,7 +533,20 @@ PYBIND11_MODULE(_tkcore, m) {
              d["t_ready_ns"] = h->t_ready_ns;
              d["error"] = std::string(h->err, h->err_len);
              d["log_end"] = std::vector<uint64_t>(h->log_end, h->log_end + h->n_parts);
+             d["n_segs"] = h->n_segs;
              return d;
+           })
+      .def("span_segments",
+           [](PyRing& r, uint32_t g) {
+             // kPackRecordSpan slots: [(log_pos, len, pidx, flags, crc, row_begin, row_end)]
+             SlotHeader* h = r.r->slot(g);
+             py::list l;
+             if (h->kind != uint32_t(kPackRecordSpan)) return l;
+             const auto* sg = reinterpret_cast<const SpanSeg*>(r.r->payload(g) + h->values_offset);
+             for (uint32_t i = 0; i < h->n_segs; ++i)
+               l.append(py::make_tuple(sg[i].log_pos, sg[i].len, sg[i].pidx, sg[i].flags, sg[i].crc, sg[i].row_begin,
+                                       sg[i].row_end));
+             return l;
            })
       .def("watermarks",
            [](PyRing& r, uint32_t g) {
@@ -612,5 +641,8 @@ PYBIND11_MODULE(_tkcore, m) {
   m.attr("PACK_JSON_F32") = int(kPackJsonF32);
   m.attr("PACK_GATHER_FIXED") = int(kPackGatherFixed);
   m.attr("PACK_JSON_TEXT") = int(kPackJsonText);
+  m.attr("PACK_RECORD_SPAN") = int(kPackRecordSpan);
+  m.attr("SPAN_SEG_MAX") = kSpanSegMax;
+  m.attr("SPAN_MAX_SEG_ROWS") = kSpanMaxSegRows;
   m.attr("SLOT_HEADER_BYTES") = kSlotHeaderBytes;
 }

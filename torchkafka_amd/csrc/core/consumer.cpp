@@ -403,6 +403,75 @@ int64_t json_scan_copy(const char* s, size_t n, uint8_t* dst) {
   return json_scan_impl(s, n, false);
 }
 
+// ------------------------------------------------------------ device-decode segments (span.h)
+namespace {
+
+// A RecordBatch a span fill walked into, and the slot rows [row_first, row_last) taken from it.
+struct SpanRB {
+  uint32_t pidx;
+  uint32_t size;
+  uint64_t pos;
+  uint32_t crc;
+  bool verify;  // first visit with check_crcs: the device verifies its CRC
+  int64_t row_first, row_last;
+};
+
+// Cuts the log ranges the device must read into SpanSeg entries (<= kSpanSegMax bytes and
+// <= kSpanMaxSegRows rows each, cuts never inside an element).  Returns the count.
+uint32_t build_span_segments(const SpanRB* rbs, size_t n_rbs, const uint64_t* row_pos, uint64_t row_bytes,
+                             uint32_t esz, SpanSeg* out, uint64_t cap) {
+  uint32_t n = 0;
+  for (size_t i = 0; i < n_rbs; ++i) {
+    const SpanRB& rb = rbs[i];
+    uint64_t lo, hi;
+    if (rb.verify) {
+      lo = rb.pos;  // the whole batch: its CRC covers [pos + 21, pos + size)
+      hi = rb.pos + rb.size;
+    } else if (rb.row_last > rb.row_first) {
+      lo = row_pos[rb.row_first];  // CRC already checked: only the values taken from it
+      hi = row_pos[rb.row_last - 1] + row_bytes;
+    } else {
+      continue;  // nothing taken and nothing to verify (skipped records only)
+    }
+    int64_t r = rb.row_first;  // first row that may intersect [cur, ...)
+    uint64_t cur = lo;
+    bool first = true;
+    while (cur < hi) {
+      while (r < rb.row_last && row_pos[r] + row_bytes <= cur) ++r;
+      uint64_t cut = std::min<uint64_t>(cur + kSpanSegMax, hi);
+      // at most kSpanMaxSegRows rows: end before the value of row r + kSpanMaxSegRows
+      if (rb.row_last - r > int64_t(kSpanMaxSegRows) && row_pos[r + kSpanMaxSegRows] < cut)
+        cut = std::max<uint64_t>(row_pos[r + kSpanMaxSegRows], cur + 1);
+      if (cut < hi) {
+        // never split an element: move the cut back to an element boundary of the row it hits
+        int64_t q = r;
+        while (q < rb.row_last && row_pos[q] + row_bytes <= cut) ++q;
+        if (q < rb.row_last && row_pos[q] < cut) {
+          const uint64_t in = (cut - row_pos[q]) / esz * esz;
+          cut = row_pos[q] + in;
+          if (cut <= cur) cut = row_pos[q] + esz;  // cur sits inside this element's row start
+        }
+      }
+      int64_t re = r;
+      while (re < rb.row_last && row_pos[re] < cut) ++re;
+      if (n >= cap) throw std::runtime_error("ring slot too small for the batch's device-decode segments");
+      SpanSeg& sg = out[n++];
+      sg.log_pos = cur;
+      sg.len = uint32_t(cut - cur);
+      sg.pidx = rb.pidx;
+      sg.flags = rb.verify ? (kSegCrc | (first ? kSegCrcFirst : 0u) | (cut == hi ? kSegCrcLast : 0u)) : 0u;
+      sg.crc = rb.crc;
+      sg.row_begin = uint32_t(r);
+      sg.row_end = uint32_t(re);
+      first = false;
+      cur = cut;
+    }
+  }
+  return n;
+}
+
+}  // namespace
+
 // ------------------------------------------------------------ fill
 FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, int64_t B, int64_t timeout_ms,
                       size_t* rr) {
@@ -412,10 +481,12 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   auto& parts = f.parts();
   FillOutcome out;
   const bool gather = spec.kind == kPackFixed && spec.gather;
+  const bool span = spec.kind == kPackFixed && spec.span && !gather;
   h->n_rows = 0;
   h->n_parts = 0;
+  h->n_segs = 0;
   h->flags = 0;
-  h->kind = uint32_t(gather ? kPackGatherFixed : spec.kind);
+  h->kind = uint32_t(gather ? kPackGatherFixed : span ? kPackRecordSpan : spec.kind);
   h->err_len = 0;
   h->max_row_len = 0;
   h->total_elems = 0;
@@ -434,8 +505,9 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   uint64_t* gat = nullptr;
   std::vector<const uint8_t*> log_of;
   std::vector<uint64_t> log_cap;
-  if (gather) {
-    if (uint64_t(B) * 8 > cap) throw std::invalid_argument("ring slot too small for the batch's gather table");
+  if (gather || span) {
+    // gather: one (pidx << 44 | log offset) per row; span: one log position per row (span.h)
+    if (uint64_t(B) * 8 > cap) throw std::invalid_argument("ring slot too small for the batch's row table");
     gat = reinterpret_cast<uint64_t*>(pay);
     log_of.reserve(parts.size());
     for (const auto& fp : parts) log_of.push_back(f.broker().log_base(fp.pidx));
@@ -485,10 +557,27 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
     return kTake;
   };
 
+  // span: the RecordBatches the walk entered, in slot order (segments are cut from them below)
+  thread_local std::vector<SpanRB> rbs;
+  rbs.clear();
+  auto on_batch = [&](const IndexEntry& e, const BatchHeader& bh, bool unverified) -> bool {
+    if (!span) return true;
+    const uint32_t pidx = parts[cur_part].pidx;
+    if (rbs.empty() || rbs.back().pidx != pidx || rbs.back().pos != e.pos)
+      rbs.push_back(SpanRB{pidx, e.size, e.pos, bh.crc, unverified, rows, rows});
+    return false;  // no host CRC pass: the walk never reads the values
+  };
+
   auto visit = [&](const RecordView& r) -> int {
     if (r.value == nullptr) { touch(r); return kTake; }  // null value == `_process` returned None
     if (fixed) {
       if (uint64_t(r.value_len) != row_bytes) return bad(r, "value size does not match the fixed-width schema");
+      if (span) {
+        gat[rows] = uint64_t(r.value - log_of[cur_part]);
+        touch(r);
+        rbs.back().row_last = ++rows;
+        return rows == B ? kTakeStop : kTake;
+      }
       if (gather) {
         const uint64_t off = uint64_t(r.value - log_of[cur_part]);
         gat[rows] = (uint64_t(parts[cur_part].pidx) << kGatherShift) | off;
@@ -612,7 +701,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
       if (fp.paused) continue;
       size_t n;
       try {
-        n = f.scan(fp, 1u << 20, visit);
+        n = f.scan(fp, 1u << 20, visit, on_batch);
       } catch (const OffsetOutOfRange&) {
         if (rows == 0 && scanned == 0) throw;  // nothing packed yet: let the caller reset positions
         stop = true;                           // keep what is packed; the reset happens on the next fill
@@ -641,6 +730,22 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   }
   h->n_rows = uint32_t(rows);
   h->row_bytes = uint32_t(row_bytes);
+  if (span) {
+    values_off = align_up(uint64_t(B) * 8, 256);
+    const uint32_t n = build_span_segments(rbs.data(), rbs.size(), gat, row_bytes, uint32_t(spec.elem_size),
+                                           reinterpret_cast<SpanSeg*>(pay + values_off),
+                                           cap > values_off ? (cap - values_off) / sizeof(SpanSeg) : 0);
+    h->n_segs = n;
+    h->values_offset = values_off;
+    h->values_bytes = uint64_t(n) * sizeof(SpanSeg);
+    h->payload_bytes = values_off + h->values_bytes;
+    h->max_row_len = spec.row_elems;
+    h->total_elems = rows * spec.row_elems;
+    h->n_scanned = scanned;
+    out.rows = rows;
+    out.scanned = scanned;
+    return out;
+  }
   h->values_offset = values_off;
   h->values_bytes = gather ? uint64_t(rows) * 8 : (fixed ? uint64_t(rows) * row_bytes : vused);
   if (json_text) h->values_bytes = align_up(vused, 16);  // the kernel reads whole 16-byte chunks

@@ -14,6 +14,7 @@
 #include "broker.h"
 #include "record_batch.h"
 #include "ring.h"
+#include "span.h"
 
 namespace tk {
 
@@ -41,7 +42,14 @@ class Fetcher {
   // Visits up to `max_records` records of one partition at/after its position
   // without blocking.  Applies fetch fault injection.  Returns records taken.
   template <class F>
-  size_t scan(FetchPart& fp, size_t max_records, F&& visit);
+  size_t scan(FetchPart& fp, size_t max_records, F&& visit) {
+    return scan(fp, max_records, visit, [](const IndexEntry&, const BatchHeader&, bool) { return true; });
+  }
+  // The same, calling on_batch(index entry, header, unverified) when the walk enters a
+  // RecordBatch; `unverified`: CRC checks are on and this batch's CRC was not checked yet.
+  // on_batch returns whether the host checks it now (false: the device will, kPackRecordSpan).
+  template <class F, class G>
+  size_t scan(FetchPart& fp, size_t max_records, F&& visit, G&& on_batch);
 
   // Throws OffsetOutOfRange when position is outside [log_start, hw].
   bool has_data(const FetchPart& fp);
@@ -62,7 +70,14 @@ class Fetcher {
 };
 
 // ------------------------------------------------------------ packers
-enum PackKind : int { kPackFixed = 0, kPackVarlen = 1, kPackJsonF32 = 2, kPackGatherFixed = 3, kPackJsonText = 4 };
+enum PackKind : int {
+  kPackFixed = 0,
+  kPackVarlen = 1,
+  kPackJsonF32 = 2,
+  kPackGatherFixed = 3,
+  kPackJsonText = 4,
+  kPackRecordSpan = 5,  // fixed-width rows decoded on the device from the pinned logs (span.h)
+};
 
 // kPackJsonText: JsonArray rows for the device parser (json_parse.hip).  The payload starts
 // with one JsonRowDesc per row (common.h); the values area (at values_offset) holds each
@@ -84,6 +99,7 @@ struct PackSpec {
   int truncate = 1;
   int skip_bad = 0;         // malformed rows: 1 = skip, 0 = raise
   int gather = 0;           // fixed-width: emit log locations (kPackGatherFixed) instead of values
+  int span = 0;             // fixed-width: emit log ranges + row positions (kPackRecordSpan), CRC on device
 };
 
 struct FillOutcome {
@@ -114,8 +130,8 @@ int64_t json_scan_copy(const char* s, size_t n, uint8_t* dst);
 int64_t json_array_len(const char* s, size_t n);
 
 // ------------------------------------------------------------ template impl
-template <class F>
-size_t Fetcher::scan(FetchPart& fp, size_t max_records, F&& visit) {
+template <class F, class G>
+size_t Fetcher::scan(FetchPart& fp, size_t max_records, F&& visit, G&& on_batch) {
   Broker& b = *b_;
   PartitionEntry& P = b.part(fp.pidx);
   const int64_t delay = P.fetch_delay_ns.load(std::memory_order_relaxed);
@@ -142,11 +158,12 @@ size_t Fetcher::scan(FetchPart& fp, size_t max_records, F&& visit) {
     if (e.pos + e.size > fp.populated_end) prefault(fp, log, e.pos, P.log_end_pos.load(std::memory_order_acquire));
     const uint8_t* bp = log + e.pos;
     const BatchHeader h = parse_batch_header(bp, e.size);
-    if (check_crcs_ && fp.verified_base != h.base_offset) {
+    const bool unverified = check_crcs_ && fp.verified_base != h.base_offset;
+    if (on_batch(e, h, unverified) && unverified) {
       if (!verify_batch_crc(bp, h))
         throw CorruptRecord("Record batch at offset " + std::to_string(h.base_offset) + " failed CRC check");
-      fp.verified_base = h.base_offset;
     }
+    if (unverified) fp.verified_base = h.base_offset;  // checked here, or by the device before any commit
     bytes += e.size;
     RecordIter it(bp, h);
     RecordView r;

@@ -19,4 +19,13 @@ bool crc32c_fold();
 // One implementation explicitly (tests): 0 table, 1 crc32 instruction (3 streams), 2 folding.
 uint32_t crc32c_method(int method, const void* data, size_t n);
 
+// Raw (zero-initialised, no final xor) CRC state `raw` advanced over n_bytes zero bytes:
+// raw CRC of (A || B) = crc32c_shift_raw(raw(A), |B|) ^ raw(B).
+uint32_t crc32c_shift_raw(uint32_t raw, uint64_t n_bytes);
+// Tables of the device CRC stage (span.h: kSpanTabWords uint32).
+void crc32c_span_tables(uint32_t* out);
+// Host emulation of the device CRC stage over buf[c0, c1): raw CRC, with the RecordBatch's
+// initial-value xor applied to its first 4 bytes when `first` (tests compare it with crc32c).
+uint32_t crc32c_span_emulate(const uint8_t* buf, uint32_t c0, uint32_t c1, bool first);
+
 }  // namespace tk

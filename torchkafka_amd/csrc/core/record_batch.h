@@ -94,6 +94,7 @@ struct RecordView {
 // Iterates the records of one batch in order.  `next` returns false at the end.
 class RecordIter {
  public:
+  static constexpr int kPrefetchAhead = 8;
   RecordIter(const uint8_t* batch, const BatchHeader& h);
   bool next(RecordView* out);
   int remaining() const { return remaining_; }

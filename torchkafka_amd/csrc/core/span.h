@@ -1,0 +1,67 @@
+// Device-decode slots (kPackRecordSpan): what a worker hands the GPU instead of packed values.
+//
+// The reference's hot loop is kafka-python's per-record iterator: CRC-check every fetched
+// RecordBatch (check_crcs), decode each record, call `_process` (kafka_dataset.py:156-162).
+// On the device path of this framework the worker only WALKS the record headers of the
+// batches it consumes (a chain of small reads, one or two cache lines per record: it never
+// touches the values) to fix the exact batch boundary -- which records are taken, which are
+// skipped (null values, the schema's `_process -> None`) -- and writes:
+//   * SpanSeg[n_segs] at payload offset 0: byte ranges of the partition logs to read.  A
+//     RecordBatch the worker has not seen before is covered whole, so the GPU can verify its
+//     CRC32C; one it already had verified (a batch boundary falls inside it) only over the
+//     values taken from it.  Ranges longer than kSpanSegMax are split at element boundaries.
+//   * uint64 row_pos[n_rows] at values_offset: log byte position of every taken value.
+// The gfx950 kernel (csrc/hip/span_decode.hip) then reads the ranges straight out of the
+// pinned broker logs (zero-copy over PCIe, one workgroup per segment staged in LDS),
+// verifies the CRC32C of every whole RecordBatch, extracts + casts the values into the
+// batch tensor and reports a bad CRC through an error word that blocks the batch's commit.
+// Host DRAM sees each payload byte once (the GPU's read) instead of three times (worker
+// read, worker slot write, GPU read).
+#pragma once
+#include <cstdint>
+
+namespace tk {
+
+// Largest log range one workgroup stages in LDS (plus 32 bytes of 16-byte alignment slack),
+// and most rows whose values may intersect one range (their positions are staged in LDS too).
+constexpr uint32_t kSpanSegMax = 128u << 10;
+constexpr uint32_t kSpanMaxSegRows = 2048;
+
+// A segment holds a whole RecordBatch of up to 128 KiB, so producer batches of the usual sizes
+// (Kafka's batch.size default is 16 KiB; config 2's 64 x 1 KiB records are 66 KB) are verified
+// on the device alone; longer ones are split and their partial CRCs chained by the driver.
+//
+// CRC32C on the device: a segment's CRC range [c0, c1) is cut into kSpanLanes chunks of
+// kSpanLaneBytes ENDING at c1 (the first chunk is front-padded with zeros, which leave a
+// zero-initialised CRC unchanged); each lane folds its chunk with slice-by-4 tables and a
+// log2(kSpanLanes)-level tree merges neighbours with "shift by 2^j chunks" operators.  A
+// 516-byte chunk (129 dwords, odd) puts the 32 lanes of a ds_read_b32 group on 32 different
+// LDS banks.
+constexpr uint32_t kSpanLaneBytes = 516;
+constexpr uint32_t kSpanLanes = 256;
+constexpr uint32_t kSpanLevels = 8;
+static_assert(kSpanLaneBytes * kSpanLanes >= kSpanSegMax, "lanes must cover a whole segment");
+// Device table layout (uint32 words): slice-by-4 byte tables T0..T3, then for level j and
+// byte k of the value: shift-by-(kSpanLaneBytes << j)-bytes of (b << 8k).
+constexpr uint32_t kSpanTabSlice = 0;
+constexpr uint32_t kSpanTabShift = 4 * 256;
+constexpr uint32_t kSpanTabWords = kSpanTabShift + kSpanLevels * 4 * 256;
+
+enum SpanSegFlags : uint32_t {
+  kSegCrcFirst = 1,   // the segment holds the first CRC'd byte of its RecordBatch (offset 21)
+  kSegCrcLast = 2,    // ... and/or the last byte of its RecordBatch
+  kSegCrc = 4,        // the segment is part of a RecordBatch whose CRC is verified
+};
+
+struct SpanSeg {
+  uint64_t log_pos;    // byte position of the range in partition `pidx`'s log
+  uint32_t len;        // bytes (<= kSpanSegMax)
+  uint32_t pidx;
+  uint32_t flags;      // SpanSegFlags
+  uint32_t crc;        // kSegCrc: the header CRC of the RecordBatch (every piece of it carries it)
+  uint32_t row_begin;  // rows of the slot whose values intersect this range: [row_begin, row_end)
+  uint32_t row_end;
+};
+static_assert(sizeof(SpanSeg) == 32, "SpanSeg layout");
+
+}  // namespace tk

@@ -1,6 +1,8 @@
 #include "driver.h"
 
 #include "consumer.h"
+#include "crc32c.h"
+#include "dtypes.h"
 
 #include <unistd.h>
 
@@ -41,6 +43,7 @@ MainDriver::MainDriver(Engine* engine, const std::string& ring_name, const std::
   if (!broker_url.empty() && !group.empty()) {
     broker_ = std::make_shared<tk::Broker>(broker_url, false, tk::BrokerConfig{});
     group_ = broker_->group_index(group, true);
+    reg_end_.assign(broker_->meta().max_partitions, 0);  // log ranges pinned for direct / span reads
   }
   commit_ns_.reserve(1 << 16);
 }
@@ -58,10 +61,9 @@ MainDriver::~MainDriver() {
   }
   for (auto& f : fenced_)
     if (std::get<0>(f)) hipEventDestroy(std::get<0>(f));
-  if (perr_host_) {
-    hipDeviceSynchronize();  // no kernel may still write an error word
-    hipHostFree(perr_host_);
-  }
+  if (perr_host_ || part_host_) hipDeviceSynchronize();  // no kernel may still write a status word
+  if (perr_host_) hipHostFree(perr_host_);
+  if (part_host_) hipHostFree(part_host_);
   for (auto e : event_pool_) hipEventDestroy(e);
 }
 
@@ -84,7 +86,10 @@ void MainDriver::release_completed_impl() {
     if (e == handed_.size() || !eng_->slot_done(int(handed_[e].g))) break;
     for (; k <= e; ++k, ++released_) {
       const int64_t pe = handed_[k].perr;
-      if (pe >= 0) perr_state_[size_t(pe)] = __atomic_load_n(perr_host_ + pe, __ATOMIC_ACQUIRE) < 0 ? 1 : 2;
+      if (pe >= 0) {
+        if (handed_[k].span) check_span(handed_[k].g, pe);  // reads the slot: before its release
+        perr_state_[size_t(pe)] = __atomic_load_n(perr_host_ + pe, __ATOMIC_ACQUIRE) < 0 ? 1 : 2;
+      }
       ring_->main_release(uint32_t(handed_[k].g));
     }
   }
@@ -209,6 +214,20 @@ int MainDriver::poll_one_impl(bool block, int64_t timeout_ms) {
       }
       if (!block) return 0;
       continue;
+    }
+    if (v.kind == uint32_t(tk::kPackRecordSpan)) {
+      if (!broker_) {
+        error_ = "DeviceLoader: device decode needs the synthetic broker (group_id + bootstrap_servers)";
+        return -3;
+      }
+      // pin every log range the segments cover (plus the 16-byte tail the kernel's aligned loads
+      // may touch) before any kernel may read them
+      v.n_segs = h->n_segs;
+      const auto* sg = reinterpret_cast<const tk::SpanSeg*>(ring_->payload(uint32_t(g)) + h->values_offset);
+      for (uint32_t i = 0; i < h->n_segs; ++i) {
+        const uint64_t cap = broker_->part(sg[i].pidx).log_capacity;
+        ensure_log(sg[i].pidx, std::min<uint64_t>(sg[i].log_pos + sg[i].len + 16, cap));
+      }
     }
     if (v.kind == uint32_t(tk::kPackGatherFixed)) {
       if (!direct_) {
@@ -442,7 +461,7 @@ void MainDriver::ensure_log(uint32_t pidx, uint64_t end) {
   if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess || dp != p)
     throw std::runtime_error("driver: h2d='direct' needs device addresses of pinned host memory to equal host "
                              "addresses (unified addressing)");
-  if (lo == 0) {
+  if (lo == 0 && bases_dev_) {
     const uint64_t b = reinterpret_cast<uint64_t>(base);
     if (hipMemcpy(bases_dev_ + pidx, &b, sizeof(b), hipMemcpyHostToDevice) != hipSuccess)
       throw std::runtime_error("driver: log base table update failed");
@@ -475,6 +494,17 @@ void MainDriver::collate_fixed(const SlotView& v, hipStream_t stream, int dst_dt
     record = true;
   }
   if (record) last_ev_slot_ = v.g;
+  if (v.kind == uint32_t(tk::kPackRecordSpan)) {
+    const int slot = int(v.g);
+    const SlotView* vs[1] = {&v};
+    void* d = dst;
+    int64_t pe;
+    launch_span(&slot, vs, 1, stream, dst_dt, &d, shift, scale, record, &pe);
+    handed_.back().perr = pe;
+    handed_.back().span = true;
+    last_perr_ = pe;
+    return;
+  }
   if (v.kind == uint32_t(tk::kPackGatherFixed)) {
     const int slot = int(v.g);
     const int64_t rows = v.n_rows;
@@ -491,24 +521,7 @@ void MainDriver::collate_varlen(const SlotView& v, hipStream_t stream, int dst_d
                                 int64_t* lengths, uint8_t* mask) {
   bool record;
   if (v.kind == tk::kPackJsonText) {
-    if (!perr_host_) {
-      void* h = nullptr;
-      if (hipHostMalloc(&h, kErrWords * sizeof(int32_t), hipHostMallocMapped) != hipSuccess)
-        throw std::runtime_error("driver: hipHostMalloc of the parse error words failed");
-      perr_host_ = static_cast<int32_t*>(h);
-      void* d = nullptr;
-      if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess)
-        throw std::runtime_error("driver: hipHostGetDevicePointer failed");
-      perr_dev_ = static_cast<int32_t*>(d);
-    }
-    // an error word is reused after kErrWords launches; its batch was checked long before
-    // (fenced batches are checked in order and the ring holds far fewer slots)
-    const int64_t idx = int64_t(perr_seq_++ % uint64_t(kErrWords));
-    if (perr_state_.empty()) perr_state_.assign(size_t(kErrWords), 1);
-    if (perr_state_[size_t(idx)] == 0)
-      throw std::runtime_error("driver: more than 4096 device-parsed batches awaiting their kernels");
-    perr_host_[idx] = -1;
-    perr_state_[size_t(idx)] = 0;
+    const int64_t idx = next_err_word();
     note_handed(v.g, stream, &record);
     handed_.back().perr = idx;
     eng_->collate_json(int(v.g), stream, v.values_offset, out, dst_dt, v.n_rows, L, pad, lengths, mask,
@@ -521,9 +534,126 @@ void MainDriver::collate_varlen(const SlotView& v, hipStream_t stream, int dst_d
                        record);
 }
 
-void MainDriver::deliver(const SlotView& v) {
+void MainDriver::deliver(const SlotView& v) { set_delivered(v); }
+
+void MainDriver::set_delivered(const SlotView& v) {
   delivered_ = v.wms;
-  delivered_perr_ = v.kind == tk::kPackJsonText ? (v.perr >= 0 ? v.perr : last_perr_) : -1;
+  const bool checked = v.kind == tk::kPackJsonText || v.kind == tk::kPackRecordSpan;
+  delivered_perr_ = checked ? (v.perr >= 0 ? v.perr : last_perr_) : -1;
+}
+
+void MainDriver::ensure_status() {
+  if (perr_host_) return;
+  void* h = nullptr;
+  if (hipHostMalloc(&h, kErrWords * sizeof(int32_t), hipHostMallocMapped) != hipSuccess)
+    throw std::runtime_error("driver: hipHostMalloc of the status words failed");
+  perr_host_ = static_cast<int32_t*>(h);
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) throw std::runtime_error("driver: hipHostGetDevicePointer failed");
+  perr_dev_ = static_cast<int32_t*>(d);
+  if (perr_state_.empty()) perr_state_.assign(size_t(kErrWords), 1);
+}
+
+int64_t MainDriver::next_err_word() {
+  ensure_status();
+  // an error word is reused after kErrWords launches; its batch was checked long before
+  // (fenced batches are checked in order and the ring holds far fewer slots)
+  const int64_t idx = int64_t(perr_seq_++ % uint64_t(kErrWords));
+  if (perr_state_[size_t(idx)] == 0)
+    throw std::runtime_error("driver: more than 4096 device-checked batches awaiting their kernels");
+  perr_host_[idx] = -1;
+  perr_state_[size_t(idx)] = 0;
+  if (!perr_msg_.empty()) perr_msg_[size_t(idx)].clear();
+  return idx;
+}
+
+void MainDriver::launch_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
+                             void* const* dsts, const float* shift, const float* scale, bool record_last,
+                             int64_t* perrs) {
+  if (!broker_) throw std::runtime_error("driver: device decode needs the synthetic broker");
+  if (!part_host_) {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, size_t(kErrWords * kPartials) * sizeof(uint32_t), hipHostMallocMapped) != hipSuccess)
+      throw std::runtime_error("driver: hipHostMalloc of the partial CRC words failed");
+    part_host_ = static_cast<uint32_t*>(h);
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) throw std::runtime_error("driver: hipHostGetDevicePointer failed");
+    part_dev_ = static_cast<uint32_t*>(d);
+    perr_msg_.assign(size_t(kErrWords), std::string());
+  }
+  const SlotView& v0 = *views[0];
+  SpanLaunch a{};
+  a.row_elems = v0.max_row_len;
+  const int ssz = dtype_size(v0.src_dtype), dsz = dtype_size(dst_dt);
+  const int per = ssz > 0 ? 16 / ssz : 1;
+  bool vec = ssz > 0 && a.row_elems % per == 0 && (a.row_elems * dsz) % 16 == 0;
+  for (int k = 0; k < n; ++k) {
+    vec = vec && reinterpret_cast<uintptr_t>(dsts[k]) % 16 == 0;
+    perrs[k] = next_err_word();
+    a.b[k].out = dsts[k];
+    a.b[k].err = perr_dev_ + perrs[k];
+    a.b[k].partials = part_dev_ + perrs[k] * kPartials;
+  }
+  a.vec_store = vec ? 1 : 0;
+  static const int burst = [] {
+    const char* e = std::getenv("TORCHKAFKA_SPAN_BURST");
+    return e ? std::atoi(e) : 0;
+  }();
+  a.burst = burst;
+  int launches = 0;
+  for (int k = 0; k < n; ++k) {
+    const SlotView& v = *views[k];
+    const auto* sg = reinterpret_cast<const tk::SpanSeg*>(ring_->payload(uint32_t(v.g)) + v.values_offset);
+    for (uint32_t i = 0; i < v.n_segs; ++i) {
+      constexpr uint32_t kWhole = tk::kSegCrcFirst | tk::kSegCrcLast;
+      if ((sg[i].flags & tk::kSegCrc) && (sg[i].flags & kWhole) != kWhole && i >= uint32_t(kPartials))
+        throw std::runtime_error("driver: a batch splits RecordBatches into more than 512 device segments");
+      if (a.n_seg == kMaxLaunchSegs) {
+        eng_->collate_span(slots, n, stream, a, v0.src_dtype, dst_dt, shift, scale, false);
+        ++launches;
+        a.n_seg = 0;
+      }
+      SpanDevSeg& d = a.s[a.n_seg++];
+      d.src = broker_->log_base(sg[i].pidx) + sg[i].log_pos;  // pinned: device address == host address
+      d.log_pos = sg[i].log_pos;
+      d.len = sg[i].len;
+      d.flags = sg[i].flags;
+      d.crc = sg[i].crc;
+      d.row_begin = sg[i].row_begin;
+      d.row_end = sg[i].row_end;
+      d.batch = uint16_t(k);
+      d.seg = uint16_t(i);
+    }
+  }
+  eng_->collate_span(slots, n, stream, a, v0.src_dtype, dst_dt, shift, scale, record_last);
+  (void)launches;
+}
+
+void MainDriver::check_span(int64_t g, int64_t pe) {
+  const tk::SlotHeader* h = ring_->slot(uint32_t(g));
+  const auto* sg = reinterpret_cast<const tk::SpanSeg*>(ring_->payload(uint32_t(g)) + h->values_offset);
+  int32_t bad = __atomic_load_n(perr_host_ + pe, __ATOMIC_ACQUIRE);  // a whole RecordBatch failed on the device
+  const uint32_t* part = part_host_ + pe * kPartials;
+  uint32_t acc = 0;
+  for (uint32_t i = 0; i < h->n_segs && bad < 0; ++i) {
+    const uint32_t f = sg[i].flags;
+    constexpr uint32_t kWhole = tk::kSegCrcFirst | tk::kSegCrcLast;
+    if (!(f & tk::kSegCrc) || (f & kWhole) == kWhole) continue;
+    const uint32_t crc_len = sg[i].len - ((f & tk::kSegCrcFirst) ? 21u : 0u);
+    if (f & tk::kSegCrcFirst) acc = 0;
+    acc = tk::crc32c_shift_raw(acc, crc_len) ^ __atomic_load_n(part + i, __ATOMIC_ACQUIRE);
+    if ((f & tk::kSegCrcLast) && (acc ^ 0xFFFFFFFFu) != sg[i].crc) bad = int32_t(i);
+  }
+  if (bad < 0) return;
+  // the RecordBatch of segment `bad`: walk back to its first segment for its base offset
+  uint32_t i = uint32_t(bad);
+  while (i > 0 && !(sg[i].flags & tk::kSegCrcFirst)) --i;
+  const uint8_t* rb = broker_->log_base(sg[i].pidx) + sg[i].log_pos;
+  int64_t base = 0;
+  for (int b = 0; b < 8; ++b) base = (base << 8) | int64_t(rb[b]);
+  perr_msg_[size_t(pe)] = "Record batch at offset " + std::to_string(base) + " of partition index " +
+                          std::to_string(sg[i].pidx) + " failed CRC check (verified on the device)";
+  __atomic_store_n(perr_host_ + pe, bad, __ATOMIC_RELEASE);
 }
 
 void MainDriver::stage_ready(int extra) {
@@ -551,16 +681,6 @@ void MainDriver::json_group_launch(hipStream_t stream, int dst_dt, double pad, v
                                    std::vector<std::shared_ptr<void>>&& handles) {
   const int n = 1 + int(group_idx_.size());
   if (int(handles.size()) != n - 1) throw std::invalid_argument("driver: group handles do not match the group");
-  if (!perr_host_) {
-    void* h = nullptr;
-    if (hipHostMalloc(&h, kErrWords * sizeof(int32_t), hipHostMallocMapped) != hipSuccess)
-      throw std::runtime_error("driver: hipHostMalloc of the parse error words failed");
-    perr_host_ = static_cast<int32_t*>(h);
-    void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) throw std::runtime_error("driver: hipHostGetDevicePointer failed");
-    perr_dev_ = static_cast<int32_t*>(d);
-    perr_state_.assign(size_t(kErrWords), 1);
-  }
   int slots[kMaxGroup];
   size_t voffs[kMaxGroup];
   int64_t rows[kMaxGroup], perr[kMaxGroup];
@@ -570,11 +690,7 @@ void MainDriver::json_group_launch(hipStream_t stream, int dst_dt, double pad, v
     slots[k] = int(v.g);
     voffs[k] = v.values_offset;
     rows[k] = v.n_rows;
-    const int64_t idx = int64_t(perr_seq_++ % uint64_t(kErrWords));
-    if (perr_state_[size_t(idx)] == 0)
-      throw std::runtime_error("driver: more than 4096 device-parsed batches awaiting their kernels");
-    perr_host_[idx] = -1;
-    perr_state_[size_t(idx)] = 0;
+    const int64_t idx = next_err_word();
     perr[k] = idx;
     errs[k] = perr_dev_ + idx;
     v.perr = idx;
@@ -686,8 +802,11 @@ void MainDriver::drain_fenced(bool wait) {
       for (const auto& w : std::get<2>(f))
         where += (where.empty() ? "" : ", ") + std::string("partition index ") + std::to_string(w.pidx) +
                  " offsets [" + std::to_string(w.first_offset) + ", " + std::to_string(w.next_offset) + ")";
-      parse_error_ = "batch row " + std::to_string(row) +
-                     " is not a flat numeric JSON array (device parse; batch: " + where + ")";
+      if (pe < int64_t(perr_msg_.size()) && !perr_msg_[size_t(pe)].empty())
+        parse_error_ = perr_msg_[size_t(pe)] + " (batch: " + where + ")";
+      else
+        parse_error_ = "batch row " + std::to_string(row) +
+                       " is not a flat numeric JSON array (device parse; batch: " + where + ")";
       break;  // never committed
     }
     stage_finished(std::get<1>(f), std::move(std::get<2>(f)));
@@ -732,7 +851,7 @@ int64_t MainDriver::step_fixed(hipStream_t stream, int dst_dt, void* dst, int64_
   ph_next_ns_ += t2 - t1;
   if (r < 0) return r;
   collate_fixed(*out, stream, dst_dt, dst, row, shift, scale);
-  delivered_ = out->wms;
+  set_delivered(*out);
   prefetch_ready();
   ph_launch_ns_ += tk::now_ns() - t2;
   ++ph_steps_;
@@ -765,13 +884,14 @@ int64_t MainDriver::step_group_begin(hipStream_t stream, bool auto_commit, int64
     // collated by an earlier group launch; a consumer on another stream waits for that kernel
     if (last.pre_stream != stream) eng_->stream_wait_done(int(last.pre_event_slot), stream);
     *pre_out = std::move(last.pre_out);
-    delivered_ = last.wms;
+    set_delivered(last);
     prefetch_ready();
     ++ph_steps_;
     return last.n_rows;
   }
   group_rows->push_back(last.n_rows);
-  if (last.kind == uint32_t(tk::kPackFixed) || last.kind == uint32_t(tk::kPackGatherFixed)) {
+  if (last.kind == uint32_t(tk::kPackFixed) || last.kind == uint32_t(tk::kPackGatherFixed) ||
+      last.kind == uint32_t(tk::kPackRecordSpan)) {
     extend_group();
     if (coalesce_wait_ns_ > 0 && int(1 + group_idx_.size()) < coalesce_) {
       const int64_t until = tk::now_ns() + coalesce_wait_ns_;
@@ -839,9 +959,20 @@ void MainDriver::step_group_launch(hipStream_t stream, int dst_dt, void* const* 
       cover_handed();
       last_stream_ = stream;
     }
-    launch_group(slots, rows, voffs, n, last, stream, dst_dt, dsts, row, shift, scale);
+    int64_t perrs[kMaxGroup];
+    const bool span = last.kind == uint32_t(tk::kPackRecordSpan);
+    if (span) {
+      const SlotView* vs[kMaxGroup];
+      vs[0] = &last;
+      for (int k = 1; k < n; ++k) vs[k] = &staged_[group_idx_[size_t(k - 1)]];
+      launch_span(slots, vs, n, stream, dst_dt, dsts, shift, scale, true, perrs);
+      last.perr = perrs[0];
+      for (int k = 1; k < n; ++k) staged_[group_idx_[size_t(k - 1)]].perr = perrs[k];
+    } else {
+      launch_group(slots, rows, voffs, n, last, stream, dst_dt, dsts, row, shift, scale);
+    }
     // one completion event (after the group kernel, on the last slot) releases every slot of the group
-    for (int k = 0; k < n; ++k) handed_.push_back(Handed{slots[k], k == n - 1});
+    for (int k = 0; k < n; ++k) handed_.push_back(Handed{slots[k], k == n - 1, span ? perrs[k] : -1, span});
     last_ev_slot_ = slots[n - 1];
     unevented_ = 0;
     ++events_;
@@ -855,7 +986,7 @@ void MainDriver::step_group_launch(hipStream_t stream, int dst_dt, void* const* 
     }
   }
   group_idx_.clear();
-  delivered_ = last.wms;
+  set_delivered(last);
   prefetch_ready();
   ph_launch_ns_ += tk::now_ns() - t0;
   ++ph_steps_;

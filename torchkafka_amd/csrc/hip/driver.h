@@ -21,6 +21,7 @@
 #include "engine.h"
 #include "rccl_lockstep.h"
 #include "ring.h"
+#include "span_decode.h"
 
 namespace tkh {
 
@@ -31,6 +32,7 @@ struct SlotView {
   uint32_t row_bytes = 0;
   int64_t max_row_len = 0, total_elems = 0, n_scanned = 0;
   int32_t src_dtype = -1;
+  uint32_t n_segs = 0;                // kPackRecordSpan: SpanSeg entries at values_offset
   std::vector<int64_t> shape;
   std::vector<tk::Watermark> wms;
   // coalesced fast path: collated ahead of delivery by a group launch
@@ -64,6 +66,7 @@ class MainDriver {
   const std::string& parse_error() const { return parse_error_; }
 
   void deliver(const SlotView& v);   // batch handed to the user
+  void set_delivered(const SlotView& v);
   void discard(const SlotView& v);   // consumed but not handed out (drop_last): free its slot
   // The user is done with every delivered batch.  With commit-on-device, `fence`
   // (the user's stream) gets an event and the batch only becomes committable
@@ -171,7 +174,17 @@ class MainDriver {
   std::deque<std::tuple<hipEvent_t, int64_t, std::vector<tk::Watermark>, int64_t>> fenced_;
   std::vector<uint8_t> perr_state_;  // per error word: 0 kernel pending, 1 clean, 2 malformed row
   void settle_parse_errors(bool wait);
+  void ensure_status();
+  int64_t next_err_word();
+  // Span decode: CRC chains of RecordBatches split over segments, verdict and message (at release).
+  void check_span(int64_t g, int64_t pe);
+  void launch_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
+                   void* const* dsts, const float* shift, const float* scale, bool record_last, int64_t* perrs);
   static constexpr int64_t kErrWords = 4096;
+  static constexpr int64_t kPartials = 512;  // raw CRC words per error word (segments of one slot)
+  uint32_t* part_host_ = nullptr;          // hipHostMalloc'ed, device-mapped partial CRCs
+  uint32_t* part_dev_ = nullptr;
+  std::vector<std::string> perr_msg_;      // span decode: the message of a bad batch, by error word
   int32_t* perr_host_ = nullptr;  // hipHostMalloc'ed, device-mapped error words (one per JSON launch)
   int32_t* perr_dev_ = nullptr;
   uint64_t perr_seq_ = 0;
@@ -209,7 +222,8 @@ class MainDriver {
   struct Handed {
     int64_t g;
     bool ev;            // its own completion event was recorded
-    int64_t perr = -1;  // device JSON parse: its error word, checked when the slot is released
+    int64_t perr = -1;  // device JSON parse / span decode: its error word, checked at slot release
+    bool span = false;  // kPackRecordSpan: chain the partial CRCs of split RecordBatches at release
   };
   std::deque<Handed> handed_;  // slots whose collate was launched, in launch order
   hipStream_t last_stream_ = nullptr;

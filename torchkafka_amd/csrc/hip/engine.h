@@ -7,6 +7,8 @@
 
 namespace tkh {
 
+struct SpanLaunch;  // span_decode.h
+
 // How a ring slot's bytes reach the collate kernel.
 enum H2DMode : int {
   kH2DDma = 0,       // hipMemcpyAsync (SDMA engine) into a device staging buffer, then the kernel
@@ -64,6 +66,13 @@ class Engine {
   void collate_gather_group(const int* slots, int n, hipStream_t user, int src_dt, void* const* dsts, int dst_dt,
                             const int64_t* rows, int64_t row_bytes, const uint64_t* bases, const float* shift,
                             const float* scale, bool record = true);
+  // Device decode (kPackRecordSpan, span_decode.hip): `a` lists the segments of up to kMaxGroup
+  // slots (a.b[k].row_pos is filled in here from slots[k]); records the completion event of
+  // slots[n - 1] when `record`.  The log bytes are read from the pinned broker logs.
+  void collate_span(const int* slots, int n, hipStream_t user, SpanLaunch& a, int src_dt, int dst_dt,
+                    const float* shift, const float* scale, bool record = true);
+  // Device copy of the CRC tables of the span kernel (uploaded on first use).
+  const uint32_t* span_tables();
   // `user` waits for slot s's completion event (a batch collated on another stream).
   void stream_wait_done(int s, hipStream_t user);
   void record_done(int s, hipStream_t user) { finish(s, user); }
@@ -92,6 +101,7 @@ class Engine {
   void* host_ptr_ = nullptr;
   uint8_t* host_dev_ = nullptr;           // device view of the registered host region (zero-copy)
   size_t host_len_ = 0;
+  uint32_t* span_tabs_ = nullptr;
 };
 
 }  // namespace tkh

@@ -24,7 +24,9 @@
 #include <vector>
 
 #include "collate.h"
+#include "crc32c.h"
 #include "engine.h"
+#include "span_decode.h"
 
 namespace tkh {
 
@@ -59,6 +61,7 @@ Engine::~Engine() {
   for (auto e : done_) hipEventDestroy(e);
   for (auto e : copied_) hipEventDestroy(e);
   if (staging_) hipFree(staging_);
+  if (span_tabs_) hipFree(span_tabs_);
   for (auto st : streams_) hipStreamDestroy(st);
 }
 
@@ -217,6 +220,30 @@ void Engine::collate_json_group(const int* slots, int n, hipStream_t user, const
   }
   launch_json_group(a, dst_dt, user);
   finish(slots[n - 1], user);
+}
+
+const uint32_t* Engine::span_tables() {
+  if (!span_tabs_) {
+    std::vector<uint32_t> t(tk::kSpanTabWords);
+    tk::crc32c_span_tables(t.data());
+    TKH_CHECK(hipSetDevice(device_));
+    TKH_CHECK(hipMalloc(reinterpret_cast<void**>(&span_tabs_), t.size() * sizeof(uint32_t)));
+    TKH_CHECK(hipMemcpy(span_tabs_, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  }
+  return span_tabs_;
+}
+
+void Engine::collate_span(const int* slots, int n, hipStream_t user, SpanLaunch& a, int src_dt, int dst_dt,
+                          const float* shift, const float* scale, bool record) {
+  if (n < 1 || n > kMaxGroup) throw std::invalid_argument("engine: bad group size");
+  for (int k = 0; k < n; ++k) {
+    check_slot(slots[k]);
+    begin(slots[k], user);  // DMA mode: the row table was copied with the slot payload
+    a.b[k].row_pos = reinterpret_cast<const uint64_t*>(src_base(slots[k]));
+  }
+  a.tabs = span_tables();
+  launch_span_decode(a, src_dt, dst_dt, shift, scale, user);
+  if (record) finish(slots[n - 1], user);
 }
 
 void Engine::copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes) {

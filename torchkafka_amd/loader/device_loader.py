@@ -294,7 +294,7 @@ class DeviceLoader:
                  lockstep_depth: int = 2, h2d: str = "auto", copy_streams: int = 4,
                  event_every: int | None = None, numa_bind: bool = True, coalesce: int = 8,
                  coalesce_wait_us: int = 50, json_parse: str = "auto",
-                 lockstep_timeout: float = 600.0):
+                 lockstep_timeout: float = 600.0, decode: str = "auto"):
         if batch_size < 1:
             raise ValueError("batch_size must be >= 1")
         if num_workers < 1:
@@ -337,6 +337,9 @@ class DeviceLoader:
         if json_parse not in ("auto", "device", "host"):
             raise ValueError("json_parse must be 'auto', 'device' (gfx950 parse kernel) or 'host' (worker parse)")
         self.json_parse = json_parse
+        if decode not in ("auto", "device", "host"):
+            raise ValueError("decode must be 'auto', 'device' (gfx950 RecordBatch decode) or 'host' (worker pack)")
+        self.decode = decode
         self.copy_streams = max(1, int(copy_streams))
         self.event_every = None if event_every is None else max(1, int(event_every))
         self.numa_bind = bool(numa_bind)
@@ -415,6 +418,10 @@ class DeviceLoader:
     def _slots_per_worker(self) -> int:
         if self.slots_per_worker is not None:
             return self.slots_per_worker
+        if self._span():
+            # device-decode slots hold row positions only (a few KiB): a deep ring costs no pinned
+            # memory and lets the workers run ahead while slots wait for their kernels
+            return 16
         budget = self.RING_AUTO_BYTES
         if getattr(self.schema, "kind", None) in (1, 2) and self.device.type == "cuda":
             # var-len / JSON slots are sized for the worst row (16 MiB) but hold a few hundred KiB:
@@ -427,6 +434,12 @@ class DeviceLoader:
         if self.slot_bytes is not None:
             return int(self.slot_bytes)
         s = self.schema
+        if self._span():
+            # row table (8 B per row) + SpanSeg entries: one per RecordBatch touched, plus one per
+            # 32 KiB of values (kSpanSegMax cuts), with headroom
+            B = self.batch_size
+            segs = 2 * B + 128 + (B * s.row_bytes) // (32 << 10)
+            return (B * 8 + 255) // 256 * 256 + 32 * segs
         if s is not None and getattr(s, "kind", None) == 0:
             return self.batch_size * s.row_bytes
         return 16 << 20
@@ -434,7 +447,28 @@ class DeviceLoader:
     def _worker_cfg(self) -> dict:
         return {"batch_size": self.batch_size, "sharding": self.sharding, "rank": self.rank,
                 "world_size": self.world_size, "native": self.native, "base_seed": self.base_seed,
-                "gather": self._direct(), "json_device": self._json_device()}
+                "gather": self._direct(), "json_device": self._json_device(), "span": self._span()}
+
+    def _span(self) -> bool:
+        """decode='device': fixed-width records decoded by the gfx950 kernel (span_decode.hip).
+
+        The workers only walk the record headers of the batches they consume (exact batch
+        boundaries, null values skipped like ``_process -> None``) and hand over log ranges +
+        row positions; the kernel reads the ranges straight out of the pinned broker logs,
+        verifies every RecordBatch's CRC32C (kafka-python's ``check_crcs``), extracts and casts
+        the values.  A corrupted batch raises ``CorruptRecordException`` before its offsets are
+        committed.  'auto' takes it whenever it applies: CUDA device, FixedWidth schema, the
+        native path, the synthetic broker (shm:// or file://) with a group_id, h2d != 'direct'.
+        """
+        if self.decode == "host":
+            return False
+        s = self.schema
+        ok = (self.device.type == "cuda" and self.native and getattr(s, "kind", None) == 0
+              and self.h2d != "direct" and self._commit_target_url()[0] != "")
+        if self.decode == "device" and not ok:
+            raise ValueError("decode='device' needs a CUDA device, a FixedWidth schema, native=True, h2d != 'direct' "
+                             "and the synthetic broker (bootstrap_servers shm:// or file://) with a group_id")
+        return ok
 
     def _json_device(self) -> bool:
         """JsonArray records parsed by the gfx950 kernel (json_parse.hip) instead of the workers.
@@ -701,6 +735,8 @@ class DeviceLoader:
                     break
                 elif r == -3:
                     raise WorkerError(drv.error())
+                elif r == -4:  # an earlier device-checked batch was corrupt (manual-commit mode)
+                    raise CorruptRecordException(drv.parse_error())
                 else:  # -1: nothing within the poll slice
                     if cs:
                         self._log_commit(cs, debug)
@@ -776,6 +812,8 @@ class DeviceLoader:
                 return
             elif r == -3:
                 raise WorkerError(drv.error())
+            elif r == -4:
+                raise CorruptRecordException(drv.parse_error())
             else:
                 run._check_workers_native()
                 if self.timeout > 0 and time.perf_counter_ns() - t0 > self.timeout * 1e9:

@@ -118,6 +118,7 @@ def _native_loop(ring, worker_id, spw, consumer, schema, cfg, state) -> None:
     timeout = _consumer_timeout_ms(consumer)
     fetcher = consumer._fetcher
     gather = bool(cfg.get("gather")) and kind == core().PACK_FIXED
+    span = bool(cfg.get("span")) and kind == core().PACK_FIXED and not gather
     if not fetcher.assigned() and cfg["sharding"] == "static":
         g = _acquire(ring, worker_id, state)  # nothing to read, ever: end of stream right away
         ring.set_slot(g, 0, core().SLOT_EOS, kind, 0, 0, 0, 0, 0, [])
@@ -130,7 +131,7 @@ def _native_loop(ring, worker_id, spw, consumer, schema, cfg, state) -> None:
             try:
                 rows, _scanned, timed_out, shut = fetcher.fill_slot(ring, g, kind, elem, row_elems, min_len,
                                                                     max_len, trunc, skip_bad, bs, timeout,
-                                                                    gather)
+                                                                    gather, span)
                 break
             except OffsetOutOfRangeError:
                 # retention moved past a position: reset it like the consumer would and refill this slot
