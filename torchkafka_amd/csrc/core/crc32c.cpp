@@ -305,44 +305,61 @@ uint32_t crc32c_shift_raw(uint32_t raw, uint64_t n_bytes) {
 
 void crc32c_span_tables(uint32_t* out) {
   const Tables& T = tables();
-  for (int k = 0; k < 4; ++k)
+  for (int k = 0; k < 8; ++k)
     for (int b = 0; b < 256; ++b) out[kSpanTabSlice + k * 256 + b] = T.t[k][b];
-  for (uint32_t j = 0; j < kSpanLevels; ++j) {
-    const uint32_t op = T.x2nmodp(uint64_t(kSpanLaneBytes) << j, 3);  // x^(8 * 260 * 2^j)
-    for (int k = 0; k < 4; ++k)
-      for (uint32_t b = 0; b < 256; ++b)
-        out[kSpanTabShift + (j * 4 + uint32_t(k)) * 256 + b] = Tables::multmodp(op, b << (8 * k));
+  const uint32_t lanes[2] = {kSpanLaneSmall, kSpanLaneLarge};
+  for (int set = 0; set < 2; ++set) {
+    for (uint32_t j = 0; j < kSpanLevels; ++j) {
+      const uint32_t op = T.x2nmodp(uint64_t(lanes[set]) << j, 3);  // x^(8 * L * 2^j)
+      for (int k = 0; k < 4; ++k)
+        for (uint32_t b = 0; b < 256; ++b)
+          out[kSpanTabShift + uint32_t(set) * kSpanTabShiftSet + (j * 4 + uint32_t(k)) * 256 + b] =
+              Tables::multmodp(op, b << (8 * k));
+    }
   }
 }
 
 uint32_t crc32c_span_emulate(const uint8_t* buf, uint32_t c0, uint32_t c1, bool first) {
-  // Host mirror of span_decode.hip's CRC stage, step for step: end-aligned 260-byte lane chunks,
-  // slice-by-4 over dword windows, bytes below c0 masked to zero, the first 4 CRC'd bytes of a
-  // RecordBatch xor 0xFF (the 0xFFFFFFFF initial value), then the 8-level shift tree.
+  // Host mirror of span_decode.hip's CRC stage, step for step: end-aligned lane chunks (260 or
+  // 516 bytes), a slice-by-4 step for a chunk's first 4 bytes then slice-by-8 steps, bytes below
+  // c0 masked to zero (groups wholly below c0 skipped), the first 4 CRC'd bytes of a RecordBatch
+  // xor 0xFF (the 0xFFFFFFFF initial value), then the 8-level shift tree.
   static uint32_t tab[kSpanTabWords];
   static const bool init = (crc32c_span_tables(tab), true);
   (void)init;
+  const uint32_t L = span_lane_bytes(c1 - c0);
+  const uint32_t* S0 = tab + kSpanTabShift + (L == kSpanLaneSmall ? 0u : kSpanTabShiftSet);
+  auto byte_at = [&](int64_t ab) -> uint32_t {
+    uint32_t b = ab >= int64_t(c0) ? buf[ab] : 0u;
+    if (first && ab >= int64_t(c0) && ab < int64_t(c0) + 4) b ^= 0xFFu;
+    return b;
+  };
+  auto word_at = [&](int64_t a) -> uint32_t {
+    uint32_t w = 0;
+    for (int k = 0; k < 4; ++k) w |= byte_at(a + k) << (8 * k);
+    return w;
+  };
+  const uint32_t* T = tab + kSpanTabSlice;
   uint32_t lane[kSpanLanes];
   for (uint32_t t = 0; t < kSpanLanes; ++t) {
-    const int64_t start = int64_t(c1) - int64_t(kSpanLanes - t) * kSpanLaneBytes;
+    const int64_t start = int64_t(c1) - int64_t(kSpanLanes - t) * L;
     uint32_t crc = 0;
-    for (uint32_t j = 0; j < kSpanLaneBytes / 4; ++j) {
-      const int64_t a = start + 4 * int64_t(j);
-      if (a + 4 <= int64_t(c0)) continue;
-      uint32_t w = 0;
-      for (int k = 0; k < 4; ++k) {
-        const int64_t ab = a + k;
-        uint32_t byte = ab >= int64_t(c0) ? buf[ab] : 0u;
-        if (first && ab >= int64_t(c0) && ab < int64_t(c0) + 4) byte ^= 0xFFu;
-        w |= byte << (8 * k);
-      }
-      const uint32_t x = crc ^ w;
-      crc = tab[3 * 256 + (x & 255)] ^ tab[2 * 256 + ((x >> 8) & 255)] ^ tab[256 + ((x >> 16) & 255)] ^ tab[x >> 24];
+    if (start + 4 > int64_t(c0)) {
+      const uint32_t x = crc ^ word_at(start);
+      crc = T[3 * 256 + (x & 255)] ^ T[2 * 256 + ((x >> 8) & 255)] ^ T[256 + ((x >> 16) & 255)] ^ T[x >> 24];
+    }
+    for (uint32_t j = 0; j < (L - 4) / 8; ++j) {
+      const int64_t a = start + 4 + 8 * int64_t(j);
+      if (a + 8 <= int64_t(c0)) continue;
+      const uint32_t x = crc ^ word_at(a), y = word_at(a + 4);
+      crc = T[7 * 256 + (x & 255)] ^ T[6 * 256 + ((x >> 8) & 255)] ^ T[5 * 256 + ((x >> 16) & 255)] ^
+            T[4 * 256 + (x >> 24)] ^ T[3 * 256 + (y & 255)] ^ T[2 * 256 + ((y >> 8) & 255)] ^
+            T[256 + ((y >> 16) & 255)] ^ T[y >> 24];
     }
     lane[t] = crc;
   }
   for (uint32_t j = 0; j < kSpanLevels; ++j) {
-    const uint32_t* S = tab + kSpanTabShift + j * 4 * 256;
+    const uint32_t* S = S0 + j * 4 * 256;
     for (uint32_t t = 0; t < kSpanLanes; t += 2u << j) {
       const uint32_t c = lane[t];
       lane[t] = S[c & 255] ^ S[256 + ((c >> 8) & 255)] ^ S[512 + ((c >> 16) & 255)] ^ S[768 + (c >> 24)] ^

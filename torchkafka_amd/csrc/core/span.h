@@ -31,21 +31,27 @@ constexpr uint32_t kSpanMaxSegRows = 2048;
 // (Kafka's batch.size default is 16 KiB; config 2's 64 x 1 KiB records are 66 KB) are verified
 // on the device alone; longer ones are split and their partial CRCs chained by the driver.
 //
-// CRC32C on the device: a segment's CRC range [c0, c1) is cut into kSpanLanes chunks of
-// kSpanLaneBytes ENDING at c1 (the first chunk is front-padded with zeros, which leave a
-// zero-initialised CRC unchanged); each lane folds its chunk with slice-by-4 tables and a
-// log2(kSpanLanes)-level tree merges neighbours with "shift by 2^j chunks" operators.  A
-// 516-byte chunk (129 dwords, odd) puts the 32 lanes of a ds_read_b32 group on 32 different
-// LDS banks.
-constexpr uint32_t kSpanLaneBytes = 516;
+// CRC32C on the device: a segment's CRC range [c0, c1) is cut into kSpanLanes chunks of L bytes
+// ENDING at c1 (the first chunk is front-padded with zeros, which leave a zero-initialised CRC
+// unchanged).  Each lane folds its chunk -- one slice-by-4 step for its first 4 bytes, then
+// slice-by-8 steps -- and a log2(kSpanLanes)-level tree merges neighbours with "shift by 2^j
+// chunks" operators.  L is 260 bytes (65 dwords) for ranges up to 66,560 bytes, so a config-2
+// RecordBatch (64 x 1 KiB records, 66 KB) keeps all 256 lanes busy, else 516 (129 dwords): an
+// odd dword count puts the 32 lanes of a ds_read_b32 group on 32 different LDS banks.
+constexpr uint32_t kSpanLaneSmall = 260;
+constexpr uint32_t kSpanLaneLarge = 516;
 constexpr uint32_t kSpanLanes = 256;
 constexpr uint32_t kSpanLevels = 8;
-static_assert(kSpanLaneBytes * kSpanLanes >= kSpanSegMax, "lanes must cover a whole segment");
-// Device table layout (uint32 words): slice-by-4 byte tables T0..T3, then for level j and
-// byte k of the value: shift-by-(kSpanLaneBytes << j)-bytes of (b << 8k).
+static_assert(kSpanLaneLarge * kSpanLanes >= kSpanSegMax, "lanes must cover a whole segment");
+inline constexpr uint32_t span_lane_bytes(uint32_t crc_len) {
+  return crc_len <= kSpanLaneSmall * kSpanLanes ? kSpanLaneSmall : kSpanLaneLarge;
+}
+// Device table layout (uint32 words): slice-by-8 byte tables T0..T7, then for each lane size
+// (small, large), level j and byte k of the value: shift-by-(L << j)-bytes of (b << 8k).
 constexpr uint32_t kSpanTabSlice = 0;
-constexpr uint32_t kSpanTabShift = 4 * 256;
-constexpr uint32_t kSpanTabWords = kSpanTabShift + kSpanLevels * 4 * 256;
+constexpr uint32_t kSpanTabShift = 8 * 256;
+constexpr uint32_t kSpanTabShiftSet = kSpanLevels * 4 * 256;
+constexpr uint32_t kSpanTabWords = kSpanTabShift + 2 * kSpanTabShiftSet;
 
 enum SpanSegFlags : uint32_t {
   kSegCrcFirst = 1,   // the segment holds the first CRC'd byte of its RecordBatch (offset 21)

@@ -74,6 +74,9 @@ MainDriver::~MainDriver() {
 // every slot launched before it on that stream (note_handed keeps one stream per run).
 void MainDriver::release_completed() {
   const int64_t t0 = tk::now_ns();
+  // hipEventQuery costs ~0.5-1 us of host time; a group's kernel runs for tens of us, so an
+  // event found pending is not asked again for kReleaseRequeryNs (a step calls this 2-3 times)
+  if (t0 - pending_query_ns_ < kReleaseRequeryNs) return;
   release_completed_impl();
   rel_ns_ += tk::now_ns() - t0;
 }
@@ -83,7 +86,11 @@ void MainDriver::release_completed_impl() {
   while (k < handed_.size()) {
     size_t e = k;
     while (e < handed_.size() && !handed_[e].ev) ++e;  // next slot with an event
-    if (e == handed_.size() || !eng_->slot_done(int(handed_[e].g))) break;
+    if (e == handed_.size()) break;
+    if (!eng_->slot_done(int(handed_[e].g))) {
+      pending_query_ns_ = tk::now_ns();
+      break;
+    }
     for (; k <= e; ++k, ++released_) {
       const int64_t pe = handed_[k].perr;
       if (pe >= 0) {
@@ -772,6 +779,7 @@ void MainDriver::settle_parse_errors(bool wait) {
   while (!handed_.empty()) {
     for (const auto& h : handed_)
       if (h.ev) eng_->wait_slot(int(h.g));
+    pending_query_ns_ = 0;
     release_completed();
   }
 }
@@ -882,7 +890,11 @@ int64_t MainDriver::step_group_begin(hipStream_t stream, bool auto_commit, int64
   if (r < 0) return r;
   if (last.pre) {
     // collated by an earlier group launch; a consumer on another stream waits for that kernel
-    if (last.pre_stream != stream) eng_->stream_wait_done(int(last.pre_event_slot), stream);
+    if (last.pre_stream != stream && !(waited_ev_slot_ == last.pre_event_slot && waited_stream_ == stream)) {
+      eng_->stream_wait_done(int(last.pre_event_slot), stream);
+      waited_ev_slot_ = last.pre_event_slot;
+      waited_stream_ = stream;
+    }
     *pre_out = std::move(last.pre_out);
     set_delivered(last);
     prefetch_ready();
@@ -927,10 +939,13 @@ void MainDriver::extend_group() {
 // True while the latest launch that recorded a completion event has not finished on the GPU.
 bool MainDriver::gpu_busy() {
   if (last_ev_slot_ < 0) return false;
+  const int64_t now = tk::now_ns();
+  if (now - busy_query_ns_ < kReleaseRequeryNs) return true;  // found busy a moment ago
   if (eng_->slot_done(int(last_ev_slot_))) {
     last_ev_slot_ = -1;
     return false;
   }
+  busy_query_ns_ = now;
   return true;
 }
 
@@ -952,27 +967,47 @@ void MainDriver::step_group_launch(hipStream_t stream, int dst_dt, void* const* 
     voffs[k] = v.values_offset;
     rows[k] = v.n_rows;
   }
-  if (n == 1) {
+  if (last.kind == uint32_t(tk::kPackRecordSpan)) {
+    // Device decode runs on two decode streams in turn: a group's kernel is PCIe-bound while it
+    // loads and compute-bound in its CRC/extract tail, so the next group's loads overlap that
+    // tail.  The outputs were allocated on the decode stream (torch_step.cpp: the caching
+    // allocator orders their reuse against it, and knows the user's stream uses them); the
+    // user's stream waits for the group's completion before it touches a batch of it.
+    cover_handed();
+    hipStream_t ks = eng_->decode_stream(int(span_launches_++ & 1));
+    last_stream_ = ks;
+    int64_t perrs[kMaxGroup];
+    const SlotView* vs[kMaxGroup];
+    vs[0] = &last;
+    for (int k = 1; k < n; ++k) vs[k] = &staged_[group_idx_[size_t(k - 1)]];
+    launch_span(slots, vs, n, ks, dst_dt, dsts, shift, scale, true, perrs);
+    last.perr = perrs[0];
+    for (int k = 0; k < n; ++k) handed_.push_back(Handed{slots[k], k == n - 1, perrs[k], true});
+    last_ev_slot_ = slots[n - 1];
+    unevented_ = 0;
+    ++events_;
+    if (n > 1) ++groups_;
+    for (int k = 1; k < n; ++k) {
+      SlotView& v = staged_[group_idx_[size_t(k - 1)]];
+      v.perr = perrs[k];
+      v.pre = true;
+      v.pre_stream = ks;
+      v.pre_event_slot = slots[n - 1];
+      v.pre_out = std::move(handles[size_t(k - 1)]);
+    }
+    eng_->stream_wait_done(slots[n - 1], stream);
+    waited_ev_slot_ = slots[n - 1];
+    waited_stream_ = stream;
+  } else if (n == 1) {
     collate_fixed(last, stream, dst_dt, dsts[0], row, shift, scale);
   } else {
     if (stream != last_stream_) {
       cover_handed();
       last_stream_ = stream;
     }
-    int64_t perrs[kMaxGroup];
-    const bool span = last.kind == uint32_t(tk::kPackRecordSpan);
-    if (span) {
-      const SlotView* vs[kMaxGroup];
-      vs[0] = &last;
-      for (int k = 1; k < n; ++k) vs[k] = &staged_[group_idx_[size_t(k - 1)]];
-      launch_span(slots, vs, n, stream, dst_dt, dsts, shift, scale, true, perrs);
-      last.perr = perrs[0];
-      for (int k = 1; k < n; ++k) staged_[group_idx_[size_t(k - 1)]].perr = perrs[k];
-    } else {
-      launch_group(slots, rows, voffs, n, last, stream, dst_dt, dsts, row, shift, scale);
-    }
+    launch_group(slots, rows, voffs, n, last, stream, dst_dt, dsts, row, shift, scale);
     // one completion event (after the group kernel, on the last slot) releases every slot of the group
-    for (int k = 0; k < n; ++k) handed_.push_back(Handed{slots[k], k == n - 1, span ? perrs[k] : -1, span});
+    for (int k = 0; k < n; ++k) handed_.push_back(Handed{slots[k], k == n - 1});
     last_ev_slot_ = slots[n - 1];
     unevented_ = 0;
     ++events_;

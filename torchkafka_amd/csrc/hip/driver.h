@@ -111,6 +111,8 @@ class MainDriver {
   void json_group_launch(hipStream_t stream, int dst_dt, double pad, void* const* outs, const int64_t* Ls,
                          int64_t* const* lengths, uint8_t* const* masks,
                          std::vector<std::shared_ptr<void>>&& handles);
+  // The stream the next device-decode group launch runs on (its outputs are allocated there).
+  hipStream_t next_decode_stream() { return eng_->decode_stream(int(span_launches_ & 1)); }
   void set_coalesce(int n) { coalesce_ = n < 1 ? 1 : (n > kMaxGroup ? kMaxGroup : n); }
   // Adaptive coalescing: while the GPU is still running an earlier launch, wait up to `us` for
   // more staged batches so the next launch carries a full group (0 disables).  Waiting costs no
@@ -157,6 +159,9 @@ class MainDriver {
   int poll_one_impl(bool block, int64_t timeout_ms);
   void release_completed();
   void release_completed_impl();
+  static constexpr int64_t kReleaseRequeryNs = 3000;
+  int64_t pending_query_ns_ = 0;  // when an event was last found pending (release_completed)
+  int64_t busy_query_ns_ = 0;     // when gpu_busy() last found the latest launch running
   void note_handed(int64_t g, hipStream_t stream, bool* record);  // decides whether slot g records its event
   void cover_handed();  // records an event for the newest handed slot without one
   int poll_blocking(int64_t timeout_ms);  // blocks for a slot, releasing completed ones meanwhile
@@ -265,6 +270,9 @@ class MainDriver {
   int64_t groups_ = 0;
   int64_t coalesce_wait_ns_ = 0;
   int64_t last_ev_slot_ = -1;  // slot whose completion event was recorded by the latest launch
+  uint64_t span_launches_ = 0;  // device-decode group launches (they alternate between two streams)
+  int64_t waited_ev_slot_ = -1;       // the user's stream already waits for this slot's event ...
+  hipStream_t waited_stream_ = nullptr;  // ... (skips repeated waits for one group's batches)
   bool gpu_busy();
   void extend_group();
   void ensure_log(uint32_t pidx, uint64_t end);

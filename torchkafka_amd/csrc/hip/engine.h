@@ -73,6 +73,10 @@ class Engine {
                     const float* shift, const float* scale, bool record = true);
   // Device copy of the CRC tables of the span kernel (uploaded on first use).
   const uint32_t* span_tables();
+  // The two streams device-decode groups alternate on (created on first use).
+  hipStream_t decode_stream(int k);
+  // `later` runs after everything queued on `earlier` so far (an event on `earlier`).
+  void stream_after(hipStream_t later, hipStream_t earlier);
   // `user` waits for slot s's completion event (a batch collated on another stream).
   void stream_wait_done(int s, hipStream_t user);
   void record_done(int s, hipStream_t user) { finish(s, user); }
@@ -82,7 +86,7 @@ class Engine {
   // legacy names used by tests
   bool h2d_complete(int s) { return slot_done(s); }
   void wait_h2d(int s) { wait_slot(s); }
-  hipStream_t copy_stream() const { return streams_[0]; }
+  hipStream_t copy_stream() const { return streams_.empty() ? nullptr : streams_[0]; }
 
  private:
   void check_slot(int s) const;
@@ -102,6 +106,9 @@ class Engine {
   uint8_t* host_dev_ = nullptr;           // device view of the registered host region (zero-copy)
   size_t host_len_ = 0;
   uint32_t* span_tabs_ = nullptr;
+  hipStream_t decode_streams_[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> order_events_;  // stream_after: a small pool used round-robin
+  size_t order_next_ = 0;
 };
 
 }  // namespace tkh

@@ -42,6 +42,10 @@ Engine::Engine(int device, int n_slots, size_t staging_bytes, int n_streams, int
   if (mode != kH2DDma && mode != kH2DZeroCopy) throw std::invalid_argument("engine: bad h2d mode");
   if (n_streams < 1) n_streams = 1;
   if (n_streams > n_slots) n_streams = n_slots;
+  // Zero-copy mode issues no copies: no copy streams.  Every stream takes one of the process's
+  // few hardware queues (GPU_MAX_HW_QUEUES, 4 by default) round-robin, and idle ones would push
+  // the decode streams onto a shared queue, serialising the launches they exist to overlap.
+  if (mode == kH2DZeroCopy) n_streams = 0;
   TKH_CHECK(hipSetDevice(device_));
   streams_.resize(size_t(n_streams));
   for (auto& st : streams_) TKH_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -62,6 +66,12 @@ Engine::~Engine() {
   for (auto e : copied_) hipEventDestroy(e);
   if (staging_) hipFree(staging_);
   if (span_tabs_) hipFree(span_tabs_);
+  for (auto st : decode_streams_)
+    if (st) {
+      hipStreamSynchronize(st);
+      hipStreamDestroy(st);
+    }
+  for (auto e : order_events_) hipEventDestroy(e);
   for (auto st : streams_) hipStreamDestroy(st);
 }
 
@@ -233,6 +243,27 @@ const uint32_t* Engine::span_tables() {
   return span_tabs_;
 }
 
+hipStream_t Engine::decode_stream(int k) {
+  hipStream_t& st = decode_streams_[k & 1];
+  if (!st) {
+    TKH_CHECK(hipSetDevice(device_));
+    TKH_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  }
+  return st;
+}
+
+void Engine::stream_after(hipStream_t later, hipStream_t earlier) {
+  if (later == earlier) return;
+  if (order_events_.empty()) {
+    order_events_.resize(16);
+    for (auto& e : order_events_) TKH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  // an event may be re-recorded once the wait that used it was enqueued (the wait captured it)
+  hipEvent_t e = order_events_[order_next_++ % order_events_.size()];
+  TKH_CHECK(hipEventRecord(e, earlier));
+  TKH_CHECK(hipStreamWaitEvent(later, e, 0));
+}
+
 void Engine::collate_span(const int* slots, int n, hipStream_t user, SpanLaunch& a, int src_dt, int dst_dt,
                           const float* shift, const float* scale, bool record) {
   if (n < 1 || n > kMaxGroup) throw std::invalid_argument("engine: bad group size");
@@ -255,6 +286,8 @@ void Engine::copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t 
 
 void Engine::synchronize() {
   for (auto st : streams_) TKH_CHECK(hipStreamSynchronize(st));
+  for (auto st : decode_streams_)
+    if (st) TKH_CHECK(hipStreamSynchronize(st));
 }
 
 }  // namespace tkh

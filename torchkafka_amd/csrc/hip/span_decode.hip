@@ -11,14 +11,16 @@
 //      all in flight: a zero-copy read over PCIe is latency-bound, so the whole segment is
 //      requested before the first one is waited on) into a contiguous LDS image at a 16-byte
 //      front offset, plus the slot's row positions and the CRC slice tables;
-//   2. CRC32C of a RecordBatch's bytes [21, end): 256 lanes x 516-byte chunks ending at the
-//      range end (129 dwords per chunk: the 32 lanes of a ds_read_b32 group hit 32 different
-//      banks), slice-by-4 tables in LDS fed by a sliding dword window (one ds_read_b32 +
-//      v_alignbyte per 4 bytes), then 6 shuffle levels and 2 LDS levels of "shift by 2^j
-//      chunks" (4 table lookups each, csrc/core/crc32c.cpp crc32c_span_tables);
-//   3. values: (row, 16-byte group) pairs strided over the block, each group read as a
-//      5-dword window + v_alignbyte (values sit at arbitrary byte offsets behind their varint
-//      headers), converted (dtypes.h: bit-exact with Tensor.to) and stored 8-16 B per lane;
+//   2. CRC32C of a RecordBatch's bytes [21, end): 256 lanes x 260- or 516-byte chunks ending at
+//      the range end (an odd dword count per chunk: the 32 lanes of a ds_read_b32 group hit 32
+//      different banks), slice-by-8 tables in LDS fed by a sliding dword window (two
+//      ds_read_b32 + two v_alignbyte per 8 bytes), then 6 shuffle levels and 2 LDS levels of
+//      "shift by 2^j chunks" (4 table lookups each, csrc/core/crc32c.cpp crc32c_span_tables);
+//   3. values: a wave per row for rows of >= 32 16-byte groups (lanes over the row's groups
+//      held by this segment), else (row, group) pairs strided over the block; each group is
+//      read as a 5-dword window + v_alignbyte (values sit at arbitrary byte offsets behind
+//      their varint headers), converted (dtypes.h: bit-exact with Tensor.to), stored 8-16 B
+//      per lane;
 //   4. lane 0: a RecordBatch held whole by the segment is compared with its header CRC; a
 //      mismatch stores the segment index into the batch's host-mapped error word (the driver
 //      reads it when the slot is released and never commits the batch); a RecordBatch cut
@@ -47,8 +49,8 @@ __device__ __forceinline__ uint32_t keep_from(int32_t a, int32_t c) {
   return d <= 0 ? 0xFFFFFFFFu : d >= 4 ? 0u : (0xFFFFFFFFu << (8 * d));
 }
 
-__device__ __forceinline__ uint32_t shift_op(const uint32_t* __restrict__ tabs, uint32_t level, uint32_t c) {
-  const uint32_t* S = tabs + tk::kSpanTabShift + level * 1024u;
+__device__ __forceinline__ uint32_t shift_op(const uint32_t* __restrict__ set, uint32_t level, uint32_t c) {
+  const uint32_t* S = set + level * 1024u;
   return S[c & 255u] ^ S[256u + ((c >> 8) & 255u)] ^ S[512u + ((c >> 16) & 255u)] ^ S[768u + (c >> 24)];
 }
 
@@ -77,7 +79,7 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
   constexpr int kPer = 16 / int(sizeof(S));  // source elements per 16-byte group
   __shared__ __attribute__((aligned(16))) uint8_t buf[kBufBytes];
   __shared__ int32_t rel[tk::kSpanMaxSegRows];
-  __shared__ uint32_t tab[1024];
+  __shared__ uint32_t tab[2048];
   __shared__ uint32_t wcrc[kThreads / 64];
 
   const int t = int(threadIdx.x);
@@ -110,43 +112,65 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
     for (uint32_t r = uint32_t(t); r < nrows; r += kThreads)
       rel[r] = int32_t(int64_t(bo.row_pos[row_begin + r]) - base);
     if (do_crc)
-      for (int i = t; i < 1024; i += kThreads) tab[i] = a.tabs[tk::kSpanTabSlice + i];
+      for (int i = t; i < 2048; i += kThreads) tab[i] = a.tabs[tk::kSpanTabSlice + i];
   }
   __syncthreads();
   const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
   const int32_t lo_b = kFront + head, hi_b = kFront + head + int32_t(len);  // valid LDS bytes
 
-  // ---- 2. CRC32C lanes (span.h: end-aligned 260-byte chunks)
+  // ---- 2. CRC32C lanes (span.h: end-aligned chunks of L bytes: one slice-by-4 step, then
+  // slice-by-8 steps over a sliding dword window)
   uint32_t crc = 0;
+  const uint32_t* shift_set = a.tabs + tk::kSpanTabShift;
   if (do_crc) {
     const bool first = (flags & tk::kSegCrcFirst) != 0;
     const int32_t c0 = lo_b + (first ? 21 : 0), c1 = hi_b;
-    const int32_t start = c1 - (int32_t(tk::kSpanLanes) - t) * int32_t(tk::kSpanLaneBytes);
-    constexpr int32_t kGroups = int32_t(tk::kSpanLaneBytes / 4);
-    const int32_t j0 = start >= c0 ? 0 : (c0 - start) >> 2;
-    if (j0 < kGroups) {
-      int32_t ad = start + 4 * j0;  // >= c0 - 3 >= kFront - 3
+    const int32_t L = int32_t(tk::span_lane_bytes(uint32_t(c1 - c0)));
+    if (L != int32_t(tk::kSpanLaneSmall)) shift_set += tk::kSpanTabShiftSet;
+    const int32_t start = c1 - (int32_t(tk::kSpanLanes) - t) * L;
+    const int32_t nsteps = (L - 4) >> 3;
+    if (start + 4 > c0) {  // the chunk's first 4 bytes (>= kFront - 3 whenever start + 4 > c0)
+      const int32_t w = start >> 2, sh = start & 3;
+      uint32_t x = __builtin_amdgcn_alignbyte(b32[w + 1], b32[w], sh);
+      if (start < c0 + 4) {
+        const uint32_t keep = keep_from(start, c0);
+        x &= keep;
+        if (first) x ^= keep & ~keep_from(start, c0 + 4);  // the 0xFFFFFFFF initial value
+      }
+      crc = tab[768 + (x & 255u)] ^ tab[512 + ((x >> 8) & 255u)] ^ tab[256 + ((x >> 16) & 255u)] ^ tab[x >> 24];
+    }
+    const int32_t a1 = start + 4;
+    const int32_t j0 = a1 >= c0 ? 0 : (c0 - a1) >> 3;  // 8-byte groups wholly below c0 are skipped
+    if (j0 < nsteps) {
+      int32_t ad = a1 + 8 * j0;
       int32_t w = ad >> 2;
       const int32_t sh = ad & 3;
       uint32_t lo = b32[w];
-      for (int32_t j = j0; j < kGroups; ++j, ad += 4) {
-        const uint32_t hi = b32[++w];
-        uint32_t x = __builtin_amdgcn_alignbyte(hi, lo, sh);
-        lo = hi;
+      for (int32_t j = j0; j < nsteps; ++j, ad += 8) {
+        const uint32_t m1 = b32[w + 1], m2 = b32[w + 2];
+        w += 2;
+        uint32_t x = __builtin_amdgcn_alignbyte(m1, lo, sh), y = __builtin_amdgcn_alignbyte(m2, m1, sh);
+        lo = m2;
         if (ad < c0 + 4) {
-          const uint32_t keep = keep_from(ad, c0);
-          x &= keep;
-          if (first) x ^= keep & ~keep_from(ad, c0 + 4);  // the 0xFFFFFFFF initial value
+          const uint32_t kx = keep_from(ad, c0), ky = keep_from(ad + 4, c0);
+          x &= kx;
+          y &= ky;
+          if (first) {
+            x ^= kx & ~keep_from(ad, c0 + 4);
+            y ^= ky & ~keep_from(ad + 4, c0 + 4);
+          }
         }
         x ^= crc;
-        crc = tab[768 + (x & 255u)] ^ tab[512 + ((x >> 8) & 255u)] ^ tab[256 + ((x >> 16) & 255u)] ^ tab[x >> 24];
+        crc = tab[1792 + (x & 255u)] ^ tab[1536 + ((x >> 8) & 255u)] ^ tab[1280 + ((x >> 16) & 255u)] ^
+              tab[1024 + (x >> 24)] ^ tab[768 + (y & 255u)] ^ tab[512 + ((y >> 8) & 255u)] ^
+              tab[256 + ((y >> 16) & 255u)] ^ tab[y >> 24];
       }
     }
     const int lane = t & 63;
 #pragma unroll
     for (uint32_t j = 0; j < 6; ++j) {
       const uint32_t other = __shfl_down(crc, 1u << j, 64);
-      if ((lane & ((2 << j) - 1)) == 0) crc = shift_op(a.tabs, j, crc) ^ other;
+      if ((lane & ((2 << j) - 1)) == 0) crc = shift_op(shift_set, j, crc) ^ other;
     }
     if (lane == 0) wcrc[t >> 6] = crc;
   }
@@ -156,14 +180,12 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
     const int64_t RE = a.row_elems;
     const uint32_t G = uint32_t((RE + kPer - 1) / kPer);  // 16-byte groups per row
     D* __restrict__ out = static_cast<D*>(bo.out);
-    const uint32_t total = nrows * G;
-    for (uint32_t p = uint32_t(t); p < total; p += kThreads) {
-      const uint32_t rr = p / G, gi = p - rr * G;
+    auto group = [&](uint32_t rr, uint32_t gi) {
       const int32_t e0 = int32_t(gi) * kPer;
       const int32_t b0 = rel[rr] + e0 * int32_t(sizeof(S));
       const int64_t rem = RE - e0;
       const int nel = rem < kPer ? int(rem) : kPer;
-      if (b0 + nel * int32_t(sizeof(S)) <= lo_b || b0 >= hi_b) continue;  // group held by another segment
+      if (b0 + nel * int32_t(sizeof(S)) <= lo_b || b0 >= hi_b) return;  // group held by another segment
       D* __restrict__ orow = out + int64_t(row_begin + rr) * RE;
       if (nel == kPer && b0 >= lo_b && b0 + 16 <= hi_b) {
         const int32_t w = b0 >> 2, sh = b0 & 3;
@@ -198,6 +220,23 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
             orow[e0 + k] = C::apply(sv, 0.f, 1.f, false);
         }
       }
+    };
+    if (G >= 32) {
+      // wide rows: a wave per row, its lanes over the groups of the row held by this segment
+      const int lane = t & 63;
+      for (uint32_t rr = uint32_t(t >> 6); rr < nrows; rr += kThreads / 64) {
+        const int32_t r0 = rel[rr];
+        const int32_t glo = r0 >= lo_b ? 0 : (lo_b - r0) / 16;
+        const int64_t ghi64 = (int64_t(hi_b) - r0 + 15) / 16;
+        const uint32_t ghi = uint32_t(ghi64 < 0 ? 0 : ghi64 < int64_t(G) ? ghi64 : int64_t(G));
+        for (uint32_t gi = uint32_t(glo) + uint32_t(lane); gi < ghi; gi += 64) group(rr, gi);
+      }
+    } else {
+      const uint32_t total = nrows * G;
+      for (uint32_t p = uint32_t(t); p < total; p += kThreads) {
+        const uint32_t rr = p / G;
+        group(rr, p - rr * G);
+      }
     }
   }
 
@@ -205,8 +244,8 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
   if (do_crc) {
     __syncthreads();
     if (t == 0) {
-      uint32_t c = shift_op(a.tabs, 6, wcrc[0]) ^ wcrc[1];
-      c = shift_op(a.tabs, 7, c) ^ (shift_op(a.tabs, 6, wcrc[2]) ^ wcrc[3]);
+      uint32_t c = shift_op(shift_set, 6, wcrc[0]) ^ wcrc[1];
+      c = shift_op(shift_set, 7, c) ^ (shift_op(shift_set, 6, wcrc[2]) ^ wcrc[3]);
       constexpr uint32_t kWhole = tk::kSegCrcFirst | tk::kSegCrcLast;
       if ((flags & kWhole) == kWhole) {
         if ((c ^ 0xFFFFFFFFu) != sg.crc) *bo.err = int32_t(sg.seg);

@@ -8,6 +8,8 @@
 // they were allocated on).  This is the only translation unit that sees libtorch
 // headers.
 #include <ATen/ATen.h>
+#include <c10/hip/HIPCachingAllocator.h>
+#include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/csrc/autograd/python_variable.h>
 #include <pybind11/pybind11.h>
@@ -40,6 +42,23 @@ at::ScalarType scalar_type_of(int code) {
 struct VarlenOut {
   at::Tensor out, lengths, mask;
 };
+
+// Output block of a coalesced fixed-width launch.  Device decode runs on the driver's decode
+// stream: allocate there, so the caching allocator orders the memory's reuse against that stream
+// (no wait on the user's stream, which already waits for the previous group), and record the
+// user's stream on it (the batches are used there).
+at::Tensor alloc_group(MainDriver& d, const std::vector<int64_t>& shape, const at::TensorOptions& opts,
+                       c10::DeviceIndex dev) {
+  if (d.last.kind != uint32_t(tk::kPackRecordSpan)) return at::empty(shape, opts);
+  const auto ks = c10::hip::getStreamFromExternal(d.next_decode_stream(), dev);
+  at::Tensor all;
+  {
+    c10::hip::HIPStreamGuard guard(ks);
+    all = at::empty(shape, opts);
+  }
+  c10::hip::HIPCachingAllocator::recordStream(all.storage().data_ptr(), c10::hip::getCurrentHIPStream(dev));
+  return all;
+}
 
 // One fixed-width step: finish + commit the previous batch, take the next one, collate it
 // (coalesced with staged ones when cfg.grouped) into a tensor on the current stream.
@@ -75,7 +94,7 @@ py::tuple step_once(MainDriver& d, const MainDriver::FastConfig& cfg) {
     for (auto x : rows) total += x;
     std::vector<int64_t> all_shape(cfg.shape);
     all_shape[0] = total;
-    at::Tensor all = at::empty(all_shape, opts);
+    at::Tensor all = alloc_group(d, all_shape, opts, dev);
     void* dsts[kMaxGroup];
     std::vector<std::shared_ptr<void>> handles;
     handles.reserve(rows.size());
@@ -283,7 +302,7 @@ void register_torch_step(py::module_& m) {
           std::vector<int64_t> all_shape(shape);
           all_shape[0] = total;
           at::Tensor all =
-              at::empty(all_shape, at::TensorOptions().dtype(scalar_type_of(dst_dt)).device(at::kCUDA, dev));
+              alloc_group(d, all_shape, at::TensorOptions().dtype(scalar_type_of(dst_dt)).device(at::kCUDA, dev), dev);
           void* dsts[kMaxGroup];
           std::vector<std::shared_ptr<void>> handles;
           handles.reserve(rows.size());
