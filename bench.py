@@ -178,6 +178,8 @@ def main() -> int:
         loader.reset_stats()
         sync()
         occ_s = loader.ring_occupancy()
+        if args.stats:
+            print(json.dumps({"ring_at_steady_t0": occ_s}), file=sys.stderr)
         t1 = time.perf_counter()
         srows = 0
         for _ in range(s_steps):

@@ -41,7 +41,21 @@ for s in $STEPS; do
     bench)  step bench 600 python bench.py --stats ;;
     pytestspan) step pytest_span 300 python -u -m pytest tests/test_gpu_span.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     spannocrc) step bench_span_nocrc 300 python bench.py --steps 1000 --steady-steps 4000 --no-crc --stats ;;
+    spanb1) for n in 2 3 4; do TORCHKAFKA_SPAN_BURST=1 TORCHKAFKA_DECODE_STREAMS=$n step bench_b1s$n 300 python bench.py --steps 1000 --stats; done
+            TORCHKAFKA_SPAN_BURST=2 step bench_b2s2 300 python bench.py --steps 1000 --stats
+            TORCHKAFKA_SPAN_BURST=1 step bench_b1s2c16 300 python bench.py --steps 1000 --stats --slots-per-worker 32 ;;
     spanburst) for b in 1 2 4 8; do TORCHKAFKA_SPAN_BURST=$b step bench_burst$b 300 python bench.py --steps 1000 --steady-steps 4000; done ;;
+    tlbprobe) step tlb_probe 300 tools/probes/bin/tlb_probe ;;
+    spanstreams) for n in 1 3 4; do TORCHKAFKA_DECODE_STREAMS=$n step bench_ds$n 300 python bench.py --steps 1000 --stats; done ;;
+    ahead) for n in 0 3 4 6; do TORCHKAFKA_AHEAD_DEPTH=$n step bench_ahead$n 300 python bench.py --steps 1000 --stats; done
+           TORCHKAFKA_AHEAD_DEPTH=4 step bench_drv_ahead4 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    spanreg) TORCHKAFKA_SPAN_BURST=-1 step bench_spanreg 300 python bench.py --steps 1000 --stats ;;
+    spansweep) step sw_s32 300 python bench.py --steps 1000 --slots-per-worker 32 --stats
+               step sw_c4 300 python bench.py --steps 1000 --coalesce 4 --stats
+               step sw_w6 300 python bench.py --steps 1000 --workers 6 --stats
+               step sw_cw0 300 python bench.py --steps 1000 --coalesce-wait-us 0 --stats
+               step sw_cw200 300 python bench.py --steps 1000 --coalesce-wait-us 200 --stats
+               step sw_pf8 300 python bench.py --steps 1000 --prefetch 8 --stats ;;
     benchhost) step bench_host 600 python bench.py --stats --decode host ;;
     benchdrv) step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     benchf32) step bench_f32 600 python bench.py --stats --dtype f32 ;;

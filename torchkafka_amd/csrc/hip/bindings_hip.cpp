@@ -266,6 +266,11 @@ PYBIND11_MODULE(_tkhip, m) {
              s["phase_steps"] = d.ph_steps_;
              s["events"] = d.events_;
              s["groups"] = d.groups();
+             s["coalesce_wait_ns"] = d.cwait_ns_;
+             s["ahead_groups"] = d.ahead_groups_;
+             s["occ_handed"] = d.occ_handed_;
+             s["occ_staged"] = d.occ_staged_;
+             s["occ_samples"] = d.occ_samples_;
              s["release_ns"] = d.rel_ns_;
              s["fast_batches"] = d.fast_batches_;
              s["fast_records"] = d.fast_records_;
@@ -283,6 +288,14 @@ PYBIND11_MODULE(_tkhip, m) {
       .def("set_coalesce", &MainDriver::set_coalesce, py::arg("n"))
       .def("set_coalesce_wait_us", &MainDriver::set_coalesce_wait_us, py::arg("us"))
       .def("enable_direct", &MainDriver::enable_direct)
+      .def("set_ahead_depth", &MainDriver::set_ahead_depth)
+      .def(
+          "pin_logs",
+          [](MainDriver& d, std::vector<uint32_t> pidxs) {
+            py::gil_scoped_release nogil;
+            d.pin_logs(pidxs);
+          },
+          py::arg("pidxs"), "pin (and device-map) what the partition logs hold now, before the first batch")
       .def_property_readonly("direct", &MainDriver::direct)
       .def_property_readonly("coalesce", &MainDriver::coalesce)
       .def("enable_lockstep", &MainDriver::enable_lockstep, py::keep_alive<1, 2>())

@@ -445,6 +445,16 @@ void MainDriver::enable_direct() {
   direct_ = true;
 }
 
+void MainDriver::pin_logs(const std::vector<uint32_t>& pidxs) {
+  if (!broker_) return;
+  eng_->prepare_decode();
+  for (uint32_t p : pidxs) {
+    if (p >= reg_end_.size()) continue;
+    const uint64_t written = broker_->part(p).log_end_pos.load(std::memory_order_acquire);
+    if (written) ensure_log(p, written);
+  }
+}
+
 void MainDriver::ensure_log(uint32_t pidx, uint64_t end) {
   if (pidx >= reg_end_.size()) throw std::out_of_range("driver: partition index beyond the broker's table");
   if (end <= reg_end_[pidx]) return;
@@ -602,9 +612,9 @@ void MainDriver::launch_span(const int* slots, const SlotView* const* views, int
     a.b[k].partials = part_dev_ + perrs[k] * kPartials;
   }
   a.vec_store = vec ? 1 : 0;
-  static const int burst = [] {
+  static const int burst = [] {  // loads a wave keeps in flight (span_decode.hip stage 1)
     const char* e = std::getenv("TORCHKAFKA_SPAN_BURST");
-    return e ? std::atoi(e) : 0;
+    return e ? std::atoi(e) : 1;
   }();
   a.burst = burst;
   int launches = 0;
@@ -883,6 +893,9 @@ int64_t MainDriver::step_group_begin(hipStream_t stream, bool auto_commit, int64
       if (r <= 0) break;
     }
   }
+  occ_handed_ += int64_t(handed_.size());
+  occ_staged_ += int64_t(staged_.size());
+  ++occ_samples_;
   const int r = next_slot(timeout_ms, &last);
   const int64_t t2 = tk::now_ns();
   ph_commit_ns_ += t1 - t0;
@@ -906,7 +919,8 @@ int64_t MainDriver::step_group_begin(hipStream_t stream, bool auto_commit, int64
       last.kind == uint32_t(tk::kPackRecordSpan)) {
     extend_group();
     if (coalesce_wait_ns_ > 0 && int(1 + group_idx_.size()) < coalesce_) {
-      const int64_t until = tk::now_ns() + coalesce_wait_ns_;
+      const int64_t cw0 = tk::now_ns();
+      const int64_t until = cw0 + coalesce_wait_ns_;
       while (int(1 + group_idx_.size()) < coalesce_ && gpu_busy() && tk::now_ns() < until) {
         const int r2 = poll_one(false, 0);
         if (r2 == -3) break;  // reported by the next call
@@ -917,10 +931,83 @@ int64_t MainDriver::step_group_begin(hipStream_t stream, bool auto_commit, int64
         release_completed();
         for (int k = 0; k < 16; ++k) tk::cpu_relax();
       }
+      cwait_ns_ += tk::now_ns() - cw0;
     }
     for (size_t i : group_idx_) group_rows->push_back(staged_[i].n_rows);
   }
   return last.n_rows;
+}
+
+void MainDriver::ahead_begin(std::vector<int64_t>* rows) {
+  rows->clear();
+  group_idx_.clear();
+  if (ahead_depth_ <= 0 || coalesce_ <= 1) return;
+  const size_t want = size_t(prefetch_ + (ahead_depth_ + 1) * coalesce_);
+  while (staged_.size() < want) {
+    if (poll_one(false, 0) <= 0) break;  // nothing ready (an error is reported by next_slot)
+  }
+  int pre = 0;
+  size_t i0 = staged_.size();
+  for (size_t i = 0; i < staged_.size(); ++i) {
+    const SlotView& v = staged_[i];
+    if (v.g < 0) continue;
+    if (v.pre)
+      ++pre;
+    else if (i0 == staged_.size())
+      i0 = i;
+  }
+  if (pre >= ahead_depth_ * coalesce_ || i0 == staged_.size()) return;
+  const SlotView& f = staged_[i0];
+  if (f.kind != uint32_t(tk::kPackRecordSpan) || f.n_rows == 0) return;
+  for (size_t i = i0; i < staged_.size() && int(group_idx_.size()) < coalesce_; ++i) {
+    const SlotView& v = staged_[i];
+    if (v.g < 0) continue;  // watermark-only slot: rides on the next delivered batch
+    if (v.pre || v.kind != f.kind || v.src_dtype != f.src_dtype || v.max_row_len != f.max_row_len ||
+        v.row_bytes != f.row_bytes || v.shape != f.shape || v.n_rows == 0)
+      break;
+    group_idx_.push_back(i);
+  }
+  if (int(group_idx_.size()) < coalesce_) {  // only full groups go ahead; the rest waits for the user
+    group_idx_.clear();
+    return;
+  }
+  for (size_t i : group_idx_) rows->push_back(staged_[i].n_rows);
+}
+
+void MainDriver::ahead_launch(int dst_dt, void* const* dsts, const float* shift, const float* scale,
+                              std::vector<std::shared_ptr<void>>&& handles) {
+  const int n = int(group_idx_.size());
+  if (n < 1 || int(handles.size()) != n) throw std::invalid_argument("driver: ahead group does not match");
+  const int64_t t0 = tk::now_ns();
+  int slots[kMaxGroup];
+  const SlotView* vs[kMaxGroup];
+  for (int k = 0; k < n; ++k) {
+    const SlotView& v = staged_[group_idx_[size_t(k)]];
+    slots[k] = int(v.g);
+    vs[k] = &v;
+  }
+  cover_handed();
+  hipStream_t ks = next_decode_stream();
+  ++span_launches_;
+  last_stream_ = ks;
+  int64_t perrs[kMaxGroup];
+  launch_span(slots, vs, n, ks, dst_dt, dsts, shift, scale, true, perrs);
+  for (int k = 0; k < n; ++k) handed_.push_back(Handed{slots[k], k == n - 1, perrs[k], true});
+  last_ev_slot_ = slots[n - 1];
+  unevented_ = 0;
+  ++events_;
+  ++groups_;
+  ++ahead_groups_;
+  for (int k = 0; k < n; ++k) {
+    SlotView& v = staged_[group_idx_[size_t(k)]];
+    v.perr = perrs[k];
+    v.pre = true;
+    v.pre_stream = ks;
+    v.pre_event_slot = slots[n - 1];
+    v.pre_out = std::move(handles[size_t(k)]);
+  }
+  group_idx_.clear();
+  ph_launch_ns_ += tk::now_ns() - t0;
 }
 
 // Appends to group_idx_ the staged batches right behind `last` that one kernel can collate with it.
@@ -974,7 +1061,8 @@ void MainDriver::step_group_launch(hipStream_t stream, int dst_dt, void* const* 
     // allocator orders their reuse against it, and knows the user's stream uses them); the
     // user's stream waits for the group's completion before it touches a batch of it.
     cover_handed();
-    hipStream_t ks = eng_->decode_stream(int(span_launches_++ & 1));
+    hipStream_t ks = next_decode_stream();
+    ++span_launches_;
     last_stream_ = ks;
     int64_t perrs[kMaxGroup];
     const SlotView* vs[kMaxGroup];
@@ -1045,7 +1133,9 @@ void MainDriver::reset_stats() {
   ph_commit_ns_ = ph_next_ns_ = ph_launch_ns_ = ph_steps_ = events_ = groups_ = 0;
   reg_ns_ = 0;
   reg_total_ = 0;
-  rel_ns_ = released_ = polled_ = poll_ns_ = 0;
+  rel_ns_ = released_ = polled_ = poll_ns_ = cwait_ns_ = 0;
+  occ_handed_ = occ_staged_ = occ_samples_ = 0;
+  ahead_groups_ = 0;
   fast_batches_ = fast_records_ = fast_ns_ = 0;
   commit_ns_.clear();
 }

@@ -111,8 +111,20 @@ class MainDriver {
   void json_group_launch(hipStream_t stream, int dst_dt, double pad, void* const* outs, const int64_t* Ls,
                          int64_t* const* lengths, uint8_t* const* masks,
                          std::vector<std::shared_ptr<void>>&& handles);
+  // Device decode AHEAD of delivery: once the user has taken a batch, the driver forms the next
+  // group from staged batches nobody has asked for yet and launches it at once, so its kernel
+  // (tens of us: PCIe-bound, sharing the link with the groups before it) runs while the user
+  // works through the batches already decoded.  ahead_begin stages what the workers published
+  // (never blocks) and lists the rows of a full group of not-yet-decoded device-decode batches
+  // (empty: nothing to launch, or ahead_depth groups are already decoded ahead); ahead_launch
+  // decodes them into dsts[k] (handles[k] keep each output alive until its batch is delivered).
+  void ahead_begin(std::vector<int64_t>* rows);
+  void ahead_launch(int dst_dt, void* const* dsts, const float* shift, const float* scale,
+                    std::vector<std::shared_ptr<void>>&& handles);
+  void set_ahead_depth(int n) { ahead_depth_ = n < 0 ? 0 : n; }
+  int ahead_depth_ = 4;  // config 2: depth 0 52.2 M, 3-6 52.3-52.7 M steady, and 54 M over 2000 steps
   // The stream the next device-decode group launch runs on (its outputs are allocated there).
-  hipStream_t next_decode_stream() { return eng_->decode_stream(int(span_launches_ & 1)); }
+  hipStream_t next_decode_stream() { return eng_->decode_stream(int(span_launches_ % 4096)); }
   void set_coalesce(int n) { coalesce_ = n < 1 ? 1 : (n > kMaxGroup ? kMaxGroup : n); }
   // Adaptive coalescing: while the GPU is still running an earlier launch, wait up to `us` for
   // more staged batches so the next launch carries a full group (0 disables).  Waiting costs no
@@ -125,6 +137,10 @@ class MainDriver {
   // references) and keeps a device table of their addresses for the gather kernel.
   static constexpr uint64_t kLogChunk = uint64_t(64) << 20;
   void enable_direct();
+  // Device decode / direct: pin the logs of these partitions as far as they are written now (the
+  // retained backlog), so their registration (~13 GB/s of fresh pages on the MI355X host) is paid
+  // when the iteration starts instead of by the first batches that reach each partition.
+  void pin_logs(const std::vector<uint32_t>& pidxs);
   bool direct() const { return direct_; }
   uint64_t log_bytes_registered() const { return reg_total_; }
   int64_t log_register_ns() const { return reg_ns_; }
@@ -249,6 +265,9 @@ class MainDriver {
   int64_t ph_commit_ns_ = 0, ph_next_ns_ = 0, ph_launch_ns_ = 0, ph_steps_ = 0, events_ = 0;
   // inside the next phase: slot releases (event queries + ring hand-back) and stagings of READY slots
   int64_t rel_ns_ = 0, released_ = 0, polled_ = 0, poll_ns_ = 0;
+  int64_t cwait_ns_ = 0;  // time spent waiting for a full group while the GPU was busy
+  int64_t ahead_groups_ = 0;  // device-decode groups launched ahead of delivery
+  int64_t occ_handed_ = 0, occ_staged_ = 0, occ_samples_ = 0;  // slots launched / staged, summed per step
 
   // Per-iteration constants of the fixed-width fast path (set once by torch_step.cpp's
   // configure_fast; fast_next() then takes no arguments) and its own counters.

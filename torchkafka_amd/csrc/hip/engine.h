@@ -73,8 +73,13 @@ class Engine {
                     const float* shift, const float* scale, bool record = true);
   // Device copy of the CRC tables of the span kernel (uploaded on first use).
   const uint32_t* span_tables();
-  // The two streams device-decode groups alternate on (created on first use).
+  // The streams device-decode groups rotate over (created on first use; kDecodeStreams).
   hipStream_t decode_stream(int k);
+  int decode_streams() const;
+  // Creates the decode streams, uploads the CRC tables and runs an empty kernel on every decode
+  // stream (the runtime binds a stream to a hardware queue at its first launch), so none of that
+  // lands on the first batches of an iteration.
+  void prepare_decode();
   // `later` runs after everything queued on `earlier` so far (an event on `earlier`).
   void stream_after(hipStream_t later, hipStream_t earlier);
   // `user` waits for slot s's completion event (a batch collated on another stream).
@@ -106,7 +111,7 @@ class Engine {
   uint8_t* host_dev_ = nullptr;           // device view of the registered host region (zero-copy)
   size_t host_len_ = 0;
   uint32_t* span_tabs_ = nullptr;
-  hipStream_t decode_streams_[2] = {nullptr, nullptr};
+  hipStream_t decode_streams_[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> order_events_;  // stream_after: a small pool used round-robin
   size_t order_next_ = 0;
 };

@@ -41,6 +41,10 @@ struct SpanLaunch {
   SpanDevSeg s[kMaxLaunchSegs];
 };
 
+// Queries the attributes of the span kernel instantiations (loads their code object), so the
+// first real launch does not pay for it.
+void prewarm_span_kernels(int device);
+
 void launch_span_decode(const SpanLaunch& a, int src_dt, int dst_dt, const float* shift, const float* scale,
                         hipStream_t stream);
 

@@ -7,10 +7,10 @@
 // framework's host path, the worker's CRC pass and value copy into the ring slot.
 //
 // One 256-thread workgroup per segment (<= 128 KiB of one partition log; 1 workgroup per CU):
-//   1. every thread issues its 16-byte LDS-DMA loads of the segment (33 x global_load_lds_dwordx4,
-//      all in flight: a zero-copy read over PCIe is latency-bound, so the whole segment is
-//      requested before the first one is waited on) into a contiguous LDS image at a 16-byte
-//      front offset, plus the slot's row positions and the CRC slice tables;
+//   1. the segment is copied into a contiguous LDS image (16-byte front offset) by LDS-DMA,
+//      global_load_lds_dwordx4, one 1 KiB load in flight per wave (fewer outstanding PCIe reads
+//      move more bytes; the launches of two or three decode streams keep the link busy), plus
+//      the slot's row positions and the CRC slice tables;
 //   2. CRC32C of a RecordBatch's bytes [21, end): 256 lanes x 260- or 516-byte chunks ending at
 //      the range end (an odd dword count per chunk: the 32 lanes of a ds_read_b32 group hit 32
 //      different banks), slice-by-8 tables in LDS fed by a sliding dword window (two
@@ -93,26 +93,37 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
   const uint32_t nrows = sg.row_end - row_begin;
   const bool do_crc = (flags & tk::kSegCrc) != 0;
 
-  // ---- 1. stage: every load in flight before the first wait.  LDS-DMA (global_load_lds_dwordx4):
-  // wave w's i-th load writes chunks [i * 256 + 64 w, +64) -- one contiguous KiB of the image,
-  // which is exactly the instruction's wave-uniform-base + 16 * lane layout -- with no VGPR staging.
+  // ---- 1. stage: LDS-DMA (global_load_lds_dwordx4).  Wave w's i-th load writes chunks
+  // [i * 256 + 64 w, +64) -- one contiguous KiB of the image, exactly the instruction's
+  // wave-uniform-base + 16 * lane layout -- with no VGPR staging.  Each wave keeps ONE load in
+  // flight: zero-copy PCIe reads lose bandwidth with many outstanding requests (tools/probes/
+  // tlb_probe.hip: 53 GB/s at 32 reading blocks, 40 at 512), and with two or three decode
+  // kernels running at once the link stays full (config 2: 53 M rec/s with one load in flight
+  // per wave, 41-44 M with 2-8, 46 M with all 17 issued up front).
   {
     const uint8_t* gsrc = reinterpret_cast<const uint8_t*>(su - uint32_t(head));
     const int wv = t >> 6;
-#pragma unroll
-    for (int i = 0; i < kLoads; ++i) {
+    auto dma = [&](int i) {
       const uint32_t c = uint32_t(t + i * kThreads);
       if (c < nchunk)
         __builtin_amdgcn_global_load_lds(
             gsrc + 16u * c,
             (__attribute__((address_space(3))) void*)(buf + kFront + 16 * (i * kThreads + wv * 64)), 16, 0, 0);
-      if (a.burst > 0 && (i + 1) % a.burst == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    };
+    const int burst = a.burst;  // 0: all in flight; k > 0: wait after every k (default 1)
+    dma(0);
+    // the row positions and CRC tables load behind the first chunk (waiting for them waits for it)
     const int64_t base = int64_t(sg.log_pos) - int64_t(head) - kFront;  // log position of LDS byte 0
     for (uint32_t r = uint32_t(t); r < nrows; r += kThreads)
       rel[r] = int32_t(int64_t(bo.row_pos[row_begin + r]) - base);
     if (do_crc)
       for (int i = t; i < 2048; i += kThreads) tab[i] = a.tabs[tk::kSpanTabSlice + i];
+#pragma unroll
+    for (int i = 1; i < kLoads; ++i) {
+      if (16u * uint32_t(i * kThreads) >= 16u * nchunk) break;  // block-uniform: no wave has chunk i
+      dma(i);
+      if (burst > 0 && (i % burst) == burst - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   __syncthreads();
   const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
@@ -268,6 +279,16 @@ void launch_span_t(const SpanLaunch& a, const float* shift, const float* scale, 
 }
 
 }  // namespace
+
+void prewarm_span_kernels(int device) {
+  (void)device;
+  hipFuncAttributes attr;
+  // the common instantiations (f32 records -> bf16 / f32 / f16 / fp8, no normalisation)
+  (void)hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&span_decode_kernel<float, __bf16, false>));
+  (void)hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&span_decode_kernel<float, float, false>));
+  (void)hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&span_decode_kernel<float, _Float16, false>));
+  (void)hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&span_decode_kernel<float, fp8e4m3, false>));
+}
 
 void launch_span_decode(const SpanLaunch& a, int src_dt, int dst_dt, const float* shift, const float* scale,
                         hipStream_t stream) {

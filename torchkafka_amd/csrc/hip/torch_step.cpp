@@ -48,8 +48,8 @@ struct VarlenOut {
 // (no wait on the user's stream, which already waits for the previous group), and record the
 // user's stream on it (the batches are used there).
 at::Tensor alloc_group(MainDriver& d, const std::vector<int64_t>& shape, const at::TensorOptions& opts,
-                       c10::DeviceIndex dev) {
-  if (d.last.kind != uint32_t(tk::kPackRecordSpan)) return at::empty(shape, opts);
+                       c10::DeviceIndex dev, bool span) {
+  if (!span) return at::empty(shape, opts);
   const auto ks = c10::hip::getStreamFromExternal(d.next_decode_stream(), dev);
   at::Tensor all;
   {
@@ -58,6 +58,37 @@ at::Tensor alloc_group(MainDriver& d, const std::vector<int64_t>& shape, const a
   }
   c10::hip::HIPCachingAllocator::recordStream(all.storage().data_ptr(), c10::hip::getCurrentHIPStream(dev));
   return all;
+}
+
+// Device decode ahead of delivery (MainDriver::ahead_begin): up to two full groups of staged
+// batches are decoded while the user still works on earlier ones.
+void launch_ahead(MainDriver& d, const std::vector<int64_t>& row_shape, const at::TensorOptions& opts,
+                  c10::DeviceIndex dev, int dst_dt, const float* shift, const float* scale) {
+  std::vector<int64_t> rows;
+  for (int q = 0; q < 3; ++q) {
+    {
+      py::gil_scoped_release nogil;
+      d.ahead_begin(&rows);
+    }
+    if (rows.empty()) return;
+    int64_t total = 0;
+    for (auto x : rows) total += x;
+    std::vector<int64_t> all_shape(row_shape);
+    all_shape[0] = total;
+    at::Tensor all = alloc_group(d, all_shape, opts, dev, true);
+    void* dsts[kMaxGroup];
+    std::vector<std::shared_ptr<void>> handles;
+    handles.reserve(rows.size());
+    int64_t off = 0;
+    for (size_t k = 0; k < rows.size(); ++k) {
+      at::Tensor t = rows.size() == 1 ? all : all.narrow(0, off, rows[k]);
+      dsts[k] = t.data_ptr();
+      handles.emplace_back(new at::Tensor(std::move(t)), [](void* p) { delete static_cast<at::Tensor*>(p); });
+      off += rows[k];
+    }
+    py::gil_scoped_release nogil;
+    d.ahead_launch(dst_dt, dsts, shift, scale, std::move(handles));
+  }
 }
 
 // One fixed-width step: finish + commit the previous batch, take the next one, collate it
@@ -94,7 +125,7 @@ py::tuple step_once(MainDriver& d, const MainDriver::FastConfig& cfg) {
     for (auto x : rows) total += x;
     std::vector<int64_t> all_shape(cfg.shape);
     all_shape[0] = total;
-    at::Tensor all = alloc_group(d, all_shape, opts, dev);
+    at::Tensor all = alloc_group(d, all_shape, opts, dev, d.last.kind == uint32_t(tk::kPackRecordSpan));
     void* dsts[kMaxGroup];
     std::vector<std::shared_ptr<void>> handles;
     handles.reserve(rows.size());
@@ -111,6 +142,8 @@ py::tuple step_once(MainDriver& d, const MainDriver::FastConfig& cfg) {
     py::gil_scoped_release nogil;
     d.step_group_launch(stream, cfg.dst_dt, dsts, cfg.row, cfg.shift, cfg.scale, std::move(handles));
   }
+  if (d.last.kind == uint32_t(tk::kPackRecordSpan))
+    launch_ahead(d, cfg.shape, opts, dev, cfg.dst_dt, cfg.shift, cfg.scale);
   return py::make_tuple(r, cs, py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(out))));
 }
 
@@ -302,7 +335,8 @@ void register_torch_step(py::module_& m) {
           std::vector<int64_t> all_shape(shape);
           all_shape[0] = total;
           at::Tensor all =
-              alloc_group(d, all_shape, at::TensorOptions().dtype(scalar_type_of(dst_dt)).device(at::kCUDA, dev), dev);
+              alloc_group(d, all_shape, at::TensorOptions().dtype(scalar_type_of(dst_dt)).device(at::kCUDA, dev), dev,
+                          d.last.kind == uint32_t(tk::kPackRecordSpan));
           void* dsts[kMaxGroup];
           std::vector<std::shared_ptr<void>> handles;
           handles.reserve(rows.size());

@@ -132,6 +132,10 @@ class _Run:
                 self.driver.set_coalesce_wait_us(L.coalesce_wait_us if L.coalesce > 1 else 0)
                 if L._direct():
                     self.driver.enable_direct()
+                if L._direct() or L._span():
+                    self.driver.pin_logs(L._rank_partitions())
+                if "TORCHKAFKA_AHEAD_DEPTH" in os.environ:
+                    self.driver.set_ahead_depth(int(os.environ["TORCHKAFKA_AHEAD_DEPTH"]))
         except BaseException:
             self.close()
             raise
@@ -448,6 +452,26 @@ class DeviceLoader:
         return {"batch_size": self.batch_size, "sharding": self.sharding, "rank": self.rank,
                 "world_size": self.world_size, "native": self.native, "base_seed": self.base_seed,
                 "gather": self._direct(), "json_device": self._json_device(), "span": self._span()}
+
+    def _rank_partitions(self) -> list[int]:
+        """Broker partition indices this rank's workers will read (static sharding of the topics
+        given to ``init_worker``); empty when not known up front (group sharding, custom init)."""
+        from ..models.kafka_dataset import _WorkerInit
+        from ..parallel.sharding import shard_partitions
+
+        wi = self.worker_init_fn
+        if self.sharding != "static" or not isinstance(wi, _WorkerInit) or not wi.args:
+            return []
+        try:
+            b = self._broker()
+            out = []
+            for topic in wi.args:
+                if isinstance(topic, str) and b.has_topic(topic):
+                    _, n, first = b.topic(topic)
+                    out += [first + p for p in shard_partitions(n, self.rank, self.world_size)]
+            return out
+        except Exception:  # noqa: BLE001 - not a synthetic broker: pinned lazily, batch by batch
+            return []
 
     def _span(self) -> bool:
         """decode='device': fixed-width records decoded by the gfx950 kernel (span_decode.hip).
@@ -844,6 +868,10 @@ class DeviceLoader:
         self.stats.records += st.get("fast_records", 0)
         self.stats.issue_ns += st.get("fast_ns", 0)
         self.stats.groups += st.get("groups", 0)
+        self.stats.coalesce_wait_ns += st.get("coalesce_wait_ns", 0)
+        self.stats.occ_handed += st.get("occ_handed", 0)
+        self.stats.occ_staged += st.get("occ_staged", 0)
+        self.stats.occ_samples += st.get("occ_samples", 0)
         self.stats.release_ns += st.get("release_ns", 0)
         self.stats.poll_ns += st.get("poll_ns", 0)
         self.stats.polled += st.get("polled", 0)

@@ -41,6 +41,10 @@ class LoaderStats:
     phase_steps: int = 0
     events: int = 0            # completion events recorded (batched: fewer than batches)
     groups: int = 0            # coalesced launches (several batches collated by one kernel)
+    coalesce_wait_ns: int = 0  # main thread waiting for a full group while the GPU was busy
+    occ_handed: int = 0        # slots launched on the GPU and not yet released, summed per step
+    occ_staged: int = 0        # slots taken from the ring and not yet launched, summed per step
+    occ_samples: int = 0
     release_ns: int = 0        # native next phase: slot releases (event queries + ring hand-back)
     poll_ns: int = 0           # native next phase: non-blocking stagings of READY slots
     polled: int = 0
@@ -84,6 +88,9 @@ class LoaderStats:
             "native_launch_us_per_step": self.phase_launch_ns / 1e3 / max(self.phase_steps, 1),
             "events_per_batch": self.events / max(self.batches, 1),
             "group_launches_per_batch": self.groups / max(self.batches, 1),
+            "coalesce_wait_us_per_batch": self.coalesce_wait_ns / 1e3 / max(self.batches, 1),
+            "slots_on_gpu_avg": self.occ_handed / max(self.occ_samples, 1),
+            "slots_staged_avg": self.occ_staged / max(self.occ_samples, 1),
             "native_release_us_per_step": self.release_ns / 1e3 / max(self.phase_steps, 1),
             "native_poll_us_per_step": self.poll_ns / 1e3 / max(self.phase_steps, 1),
             "native_poll_us_per_slot": self.poll_ns / 1e3 / max(self.polled, 1),
