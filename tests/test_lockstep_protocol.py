@@ -1,0 +1,166 @@
+"""The native cross-rank lockstep (csrc/core/lockstep.h, the credit protocol the GPU step driver
+runs) at world 2/4/8 over gloo, with scripted per-rank data paths.
+
+Each rank owns a fake producer with its own record count, arrival pace and ring capacity; the
+loop is the driver's: ask the protocol, deliver the oldest staged batch, mark the previous one
+finished.  Checked on every rank:
+  * all ranks deliver exactly min(batches per rank) steps and stop together (a rank with no
+    partitions stops everybody at step 0 instead of hanging them);
+  * a rank is never granted a batch it does not hold;
+  * a batch becomes committable only after an agreement proves every rank got past it, in
+    delivery order, and every delivered batch is committable after finish();
+  * a peer that dies makes the others fail within the process-group timeout, not hang.
+The reference has no cross-rank notion at all; its per-batch commit orchestration
+is auto_commit.py:59-72.
+"""
+import datetime
+import json
+import multiprocessing as mp
+import os
+import random
+import socket
+
+import pytest
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+class _Producer:
+    """A rank's data path: `total` batches arriving in random bursts, at most `cap` held."""
+
+    def __init__(self, total, cap, seed, slow):
+        self.total, self.cap, self.rng, self.slow = total, cap, random.Random(seed), slow
+        self.produced = self.delivered = 0
+
+    def _arrive(self, burst):
+        room = min(self.cap - (self.produced - self.delivered), self.total - self.produced)
+        if room > 0:
+            self.produced += min(room, burst)
+
+    def staged(self):
+        if not self.slow and self.rng.random() < 0.5:
+            self._arrive(self.rng.randrange(1, 4))
+        return self.produced - self.delivered
+
+    def all_done(self):
+        return self.produced == self.total
+
+    def wait_data(self, timeout_ms):
+        if self.slow:
+            import time
+
+            time.sleep(0.0005)
+        before = self.produced
+        self._arrive(self.rng.randrange(1, 3))
+        return 1 if self.produced > before else 0
+
+
+def _rank_main(rank, world, port, outdir, totals, cap, depth, slow_rank, die_rank):
+    import torch
+    import torch.distributed as dist
+
+    from torchkafka_amd.ops.native import core
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=8))
+    buf = torch.zeros(3, dtype=torch.int64)
+
+    def allreduce_min(a, b, c):
+        buf[0], buf[1], buf[2] = a, b, c
+        dist.all_reduce(buf, op=dist.ReduceOp.MIN)
+        return int(buf[0]), int(buf[1]), int(buf[2])
+
+    c = core()
+    lock = c.CreditLockstep(c.PyLockstepTransport(allreduce_min), depth)
+    committed = []
+    lock.set_on_committable(lambda wms: committed.extend(w[1] for w in wms))
+    src = _Producer(totals[rank], cap, seed=1000 * rank + depth, slow=(rank == slow_rank))
+    out = {"rank": rank, "error": None}
+    steps, prev, committed_at_deliver = 0, None, []
+    try:
+        while True:
+            r = lock.next(src, 20)
+            if r == -1:
+                continue
+            if r == -2:
+                break
+            assert r == 1, r
+            assert src.produced - src.delivered > 0, "granted a batch this rank does not hold"
+            idx = lock.delivered()
+            assert idx == steps
+            src.delivered += 1
+            if prev is not None:
+                lock.finished(prev, [(rank, prev, prev + 1, 1)])
+            prev = idx
+            committed_at_deliver.append(len(committed))
+            steps += 1
+            if rank == die_rank and steps == 5:
+                os._exit(3)  # a crashed peer
+        if prev is not None:
+            lock.finished(prev, [(rank, prev, prev + 1, 1)])
+        lock.finish()
+    except Exception as e:  # noqa: BLE001 - reported to the parent
+        out["error"] = f"{type(e).__name__}: {e}"
+    out.update(steps=steps, committed=committed, committed_at_deliver=committed_at_deliver,
+               agreements=lock.agreements)
+    with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
+        json.dump(out, f)
+    if out["error"] is None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _run(tmp_path, world, totals, cap=8, depth=2, slow_rank=-1, die_rank=-1):
+    # plain processes (not torch's spawn helper, which kills the others when one rank dies)
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_rank_main,
+                         args=(r, world, port, str(tmp_path), totals, cap, depth, slow_rank, die_rank))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=90)
+        if p.is_alive():
+            p.kill()
+            p.join()
+    return [json.load(open(tmp_path / f"r{r}.json")) for r in range(world) if (tmp_path / f"r{r}.json").exists()]
+
+
+@pytest.mark.parametrize("world,totals,cap,depth", [
+    (2, [40, 25], 4, 0),
+    (2, [60, 60], 2, 2),
+    (4, [30, 50, 10, 70], 8, 2),
+    (4, [20, 0, 35, 40], 8, 5),        # a rank with no partitions stops everyone at once
+    (8, [25, 40, 33, 18, 50, 29, 45, 37], 16, 2),
+    (8, [64] * 8, 3, 5),               # tiny ring, deep pipeline
+])
+def test_credit_lockstep_stops_together_and_commits_only_finished(tmp_path, world, totals, cap, depth):
+    res = _run(tmp_path, world, totals, cap=cap, depth=depth, slow_rank=world - 1)
+    assert len(res) == world
+    want = min(totals)
+    for r in res:
+        assert r["error"] is None, r["error"]
+        assert r["steps"] == want, (r["rank"], r["steps"], want)
+        # after finish(): every delivered batch is committable, in delivery order
+        assert r["committed"] == list(range(want))
+        # while iterating, batch k was never committable before the protocol let k+1 through
+        for k, n_committed in enumerate(r["committed_at_deliver"]):
+            assert n_committed <= k
+        # one agreement grants as many batches as the slowest rank staged: amortised below 1/step
+        assert r["agreements"] <= want + 2 + world
+
+
+def test_credit_lockstep_peer_death_fails_instead_of_hanging(tmp_path):
+    res = _run(tmp_path, 4, [200] * 4, cap=8, depth=2, die_rank=2)
+    survivors = [r for r in res if r["rank"] != 2]
+    assert len(survivors) == 3
+    for r in survivors:
+        assert r["error"] is not None, r

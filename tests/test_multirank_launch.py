@@ -1,0 +1,56 @@
+"""Launch-level multi-rank checks with torch.distributed.run (127.0.0.1 rendezvous).
+
+* bench.py at N=2 on the CPU (gloo): the driver's multi-GPU command line, rehearsed without GPUs
+  -- one JSON line from rank 0 with the whole-job aggregate and dp2.
+* tools/lockstep_check.py at N=2 on ONE GPU (marked gpu): the native step driver's credit
+  lockstep (csrc/core/lockstep.h) over the gloo transport, both ranks on cuda:0 (RCCL refuses two
+  ranks on one device), at pipeline depths 0/2/5: every rank stops at the same step and commits
+  only what every rank finished.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _torchrun(nproc, script, *args, timeout=240, env=None):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), script, *args]
+    e = dict(os.environ)
+    e.update(env or {})
+    e["PYTHONPATH"] = ROOT + os.pathsep + e.get("PYTHONPATH", "")
+    return subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                          timeout=timeout, env=e)
+
+
+def test_bench_two_ranks_gloo_cpu():
+    r = _torchrun(2, "bench.py", "--gpus", "2", "--steps", "30", "--warmup", "5", "--device", "cpu",
+                  "--steady-steps", "60", "--workers", "2", "--partitions-per-gpu", "4")
+    assert r.returncode == 0, r.stdout[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["steps"] == 30 and out["config"]["parallelism"] == "dp2"
+    assert out["config"]["partitions"] == 8 and out["config"]["global_batch"] == 512
+    assert out["value"] > 0 and out["steady_state"]["records_per_s"] > 0
+
+
+@pytest.mark.gpu
+def test_native_lockstep_two_ranks_one_gpu():
+    r = _torchrun(2, "tools/lockstep_check.py", timeout=200)
+    assert r.returncode == 0, r.stdout[-4000:]
+    oks = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"rank"')]
+    assert len(oks) == 2 and all(o["ok"] for o in oks), r.stdout[-4000:]

@@ -8,6 +8,7 @@
 #include "broker.h"
 #include "consumer.h"
 #include "crc32c.h"
+#include "lockstep.h"
 #include "record_batch.h"
 #include "ring.h"
 
@@ -89,6 +90,44 @@ std::vector<RecordIn> to_records(const std::vector<py::object>& values, const st
     }
   }
   return recs;
+}
+
+// Lockstep transport over a Python all-reduce(MIN) of three ints (gloo in the CPU tests).
+class PyLockstepTransport : public LockstepTransport {
+ public:
+  explicit PyLockstepTransport(py::function fn) : fn_(std::move(fn)) {}
+  int issue(int64_t a, int64_t b, int64_t c) override {
+    py::tuple r = fn_(a, b, c);
+    const int t = int(next_++ % 64);
+    for (int k = 0; k < 3; ++k) res_[t][k] = r[size_t(k)].cast<int64_t>();
+    return t;
+  }
+  void wait(int t, int64_t out[3]) override {
+    for (int k = 0; k < 3; ++k) out[k] = res_[t][k];
+  }
+
+ private:
+  py::function fn_;
+  uint64_t next_ = 0;
+  int64_t res_[64][3];
+};
+
+// A rank's data path scripted in Python: an object with staged(), all_done(), wait_data(ms).
+class PyLockstepSource : public LockstepSource {
+ public:
+  explicit PyLockstepSource(py::object o) : o_(std::move(o)) {}
+  int64_t staged() override { return o_.attr("staged")().cast<int64_t>(); }
+  bool all_done() override { return o_.attr("all_done")().cast<bool>(); }
+  int wait_data(int64_t timeout_ms) override { return o_.attr("wait_data")(timeout_ms).cast<int>(); }
+
+ private:
+  py::object o_;
+};
+
+py::list wms_to_list(const std::vector<Watermark>& w) {
+  py::list l;
+  for (const auto& x : w) l.append(py::make_tuple(x.pidx, x.first_offset, x.next_offset, x.count));
+  return l;
 }
 
 }  // namespace
@@ -633,6 +672,43 @@ PYBIND11_MODULE(_tkcore, m) {
       .def("shutdown", [](PyRing& r) { r.r->shutdown(); })
       .def("is_shutdown", [](PyRing& r) { return bool(r.r->header()->shutdown.load()); })
       .def("unlink", [](PyRing& r) { r.r->unlink(); });
+
+  // ---- lockstep credit protocol (the device driver's, csrc/core/lockstep.h)
+  py::register_exception<LockstepError>(m, "LockstepError", PyExc_RuntimeError);
+  py::class_<LockstepTransport>(m, "LockstepTransport", py::module_local());
+  py::class_<PyLockstepTransport, LockstepTransport>(m, "PyLockstepTransport", py::module_local())
+      .def(py::init<py::function>(), py::arg("allreduce_min"));
+  py::class_<CreditLockstep>(m, "CreditLockstep")
+      .def(py::init<LockstepTransport*, int>(), py::arg("transport"), py::arg("depth"), py::keep_alive<1, 2>())
+      .def(
+          "next",
+          [](CreditLockstep& l, py::object src, int64_t timeout_ms) {
+            PyLockstepSource s(std::move(src));
+            return l.next(s, timeout_ms);
+          },
+          py::arg("source"), py::arg("timeout_ms") = 100,
+          "1: deliver the next batch (then call delivered()), -1 starved for now, -2 every rank stops here, "
+          "-3 producer error")
+      .def("delivered", &CreditLockstep::delivered)
+      .def(
+          "finished",
+          [](CreditLockstep& l, int64_t index, std::vector<std::tuple<uint32_t, int64_t, int64_t, uint32_t>> wms) {
+            std::vector<Watermark> w;
+            for (auto& t : wms) w.push_back(Watermark{std::get<0>(t), std::get<3>(t), std::get<1>(t), std::get<2>(t)});
+            l.finished(index, std::move(w));
+          },
+          py::arg("index"), py::arg("watermarks"))
+      .def("finish", &CreditLockstep::finish)
+      .def(
+          "set_on_committable",
+          [](CreditLockstep& l, py::function f) {
+            l.set_on_committable([f](std::vector<Watermark>&& w) { f(wms_to_list(w)); });
+          },
+          py::arg("callback"))
+      .def_property_readonly("step", &CreditLockstep::step)
+      .def_property_readonly("granted", &CreditLockstep::granted)
+      .def_property_readonly("stopped", &CreditLockstep::stopped)
+      .def_property_readonly("agreements", &CreditLockstep::agreements);
 
   m.attr("SLOT_EOS") = int(kSlotEOS);
   m.attr("SLOT_ERROR") = int(kSlotError);

@@ -1,0 +1,72 @@
+#include "lockstep.h"
+
+#include <string>
+
+namespace tk {
+
+int64_t CreditLockstep::credit(LockstepSource& src) const {
+  const int64_t beyond = src.staged() - (granted_ - step_);
+  if (beyond > 0) return beyond;
+  return src.all_done() ? -1 : 0;
+}
+
+void CreditLockstep::issue(LockstepSource& src) {
+  const int64_t v = credit(src);
+  tickets_.push_back(Ticket{step_, granted_, t_->issue(v, step_, -step_)});
+  ++agreements_;
+}
+
+void CreditLockstep::settle() {
+  const Ticket t = tickets_.front();
+  tickets_.pop_front();
+  int64_t res[3];
+  t_->wait(t.ticket, res);
+  if (res[1] != -res[2])
+    throw LockstepError("lockstep: ranks are out of step (min " + std::to_string(res[1]) + ", max " +
+                        std::to_string(-res[2]) + ")");
+  while (!finished_q_.empty() && finished_q_.front().first < t.step) {
+    emit(std::move(finished_q_.front().second));
+    finished_q_.pop_front();
+  }
+  if (res[0] < 0)
+    no_more_credit_ = true;
+  else if (t.base + res[0] > granted_)
+    granted_ = t.base + res[0];
+}
+
+int CreditLockstep::next(LockstepSource& src, int64_t timeout_ms) {
+  if (stopped_) return -2;
+  // issue ahead while credits remain, so the round trip overlaps the delivery of granted batches
+  if (tickets_.empty() && !no_more_credit_ && granted_ - step_ <= depth_ && step_ < granted_) issue(src);
+  while (step_ >= granted_) {
+    if (no_more_credit_) {
+      stopped_ = true;
+      return -2;
+    }
+    bool starved = false;
+    if (tickets_.empty()) {
+      if (src.staged() == 0 && !src.all_done()) {
+        // nothing to offer yet: give the producers a moment before spending a collective round
+        const int r = src.wait_data(timeout_ms);
+        if (r == -3) return -3;
+        starved = r <= 0;
+      }
+      issue(src);  // credit 0 when still starved: the other ranks wait with us, nobody hangs
+    }
+    settle();
+    if (starved && step_ >= granted_) return -1;
+  }
+  return 1;
+}
+
+void CreditLockstep::finish() {
+  while (!tickets_.empty()) settle();  // every rank issued the same agreements
+  int64_t res[3];
+  t_->wait(t_->issue(0, 0, 0), res);   // every rank has stopped at the same step
+  ++agreements_;
+  for (auto& f : finished_q_) emit(std::move(f.second));
+  finished_q_.clear();
+  stopped_ = true;
+}
+
+}  // namespace tk

@@ -1,0 +1,104 @@
+// Cross-rank lockstep of the loader as a credit protocol -- HIP-free, so the
+// exact protocol the device driver runs is also driven by CPU tests over gloo at world 2..8.
+//
+// The reference has no notion of ranks: under torchrun every rank's consumers would run at their
+// own pace, so one rank running dry leaves the others hanging in the next gradient all-reduce,
+// and offsets committed by a fast rank describe steps the job never finished.
+//
+// Ranks deliver batch indices in the same order; `granted` is the index below which every rank
+// is known to hold a batch.  An agreement carries each rank's CREDIT -- how many batches it holds
+// beyond `granted` (what is staged now: never a wait on data a worker cannot publish while its
+// ring slots are all staged here), or -1 once its stream ended and it holds none -- as an
+// all-reduce(MIN); the minimum extends `granted` for every rank, -1 means no credit will ever
+// come again, so all ranks stop at the same index.  A new agreement is issued while `depth`
+// credits remain, so its round trip overlaps the delivery of those batches.  Every decision
+// depends only on (step, granted) and agreement results, identical on all ranks, so the
+// collective sequences stay aligned.  Completion of an agreement issued at step s proves every
+// rank reached s: batches < s are finished everywhere and become committable.  Two more words
+// ride along as a consistency check: step and -step (MIN of both = min and -max).
+#pragma once
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <stdexcept>
+#include <utility>
+#include <vector>
+
+#include "ring.h"
+
+namespace tk {
+
+// A pipelined all-reduce(MIN) of three int64: issue() returns a ticket, wait() its result.
+// Implemented over RCCL (csrc/hip/rccl_lockstep.*) and over any Python all-reduce (gloo).
+class LockstepTransport {
+ public:
+  virtual ~LockstepTransport() = default;
+  virtual int issue(int64_t a, int64_t b, int64_t c) = 0;
+  virtual void wait(int ticket, int64_t out[3]) = 0;
+};
+
+class LockstepError : public std::runtime_error {
+ public:
+  using std::runtime_error::runtime_error;
+};
+
+// What the protocol needs from the rank's data path.
+class LockstepSource {
+ public:
+  virtual ~LockstepSource() = default;
+  virtual int64_t staged() = 0;   // data batches held now and not yet delivered
+  virtual bool all_done() = 0;    // every producer of this rank has ended its stream
+  // Blocks up to timeout_ms for more data: 1 got some, 0/-1 nothing, -3 producer error.
+  virtual int wait_data(int64_t timeout_ms) = 0;
+};
+
+class CreditLockstep {
+ public:
+  CreditLockstep(LockstepTransport* t, int depth) : t_(t), depth_(depth < 0 ? 0 : depth) {
+    if (!t_) throw std::invalid_argument("lockstep: no transport");
+  }
+  // May the next batch be delivered?  1: yes (the caller delivers its oldest staged batch, then
+  // calls delivered()), -1: starved for now (let the caller check worker health, call again),
+  // -2: every rank stops here, -3: the source reported a producer error.
+  int next(LockstepSource& src, int64_t timeout_ms);
+  // The batch next() allowed was handed out; returns its index.
+  int64_t delivered() { return step_++; }
+  // A delivered batch is finished (the user asked for the next one): it becomes committable
+  // once an agreement proves every rank got past it (settle).
+  void finished(int64_t index, std::vector<Watermark>&& wms) { finished_q_.emplace_back(index, std::move(wms)); }
+  // End of the iteration: settle every agreement in flight, then one more round (a barrier:
+  // every rank stopped at the same step); everything finished becomes committable.
+  void finish();
+  // Committable batches are handed to this callback (settle / finish order = delivery order).
+  void set_on_committable(std::function<void(std::vector<Watermark>&&)> f) { on_commit_ = std::move(f); }
+
+  int64_t step() const { return step_; }
+  int64_t granted() const { return granted_; }
+  bool stopped() const { return stopped_; }
+  uint64_t agreements() const { return agreements_; }
+  int depth() const { return depth_; }
+
+ private:
+  struct Ticket {
+    int64_t step;  // step at which it was issued
+    int64_t base;  // granted at issue time
+    int ticket;
+  };
+  int64_t credit(LockstepSource& src) const;
+  void issue(LockstepSource& src);
+  void settle();
+  void emit(std::vector<Watermark>&& wms) {
+    if (on_commit_) on_commit_(std::move(wms));
+  }
+
+  LockstepTransport* t_;
+  int depth_;
+  int64_t step_ = 0, granted_ = 0;
+  bool stopped_ = false, no_more_credit_ = false;
+  uint64_t agreements_ = 0;
+  std::deque<Ticket> tickets_;
+  std::deque<std::pair<int64_t, std::vector<Watermark>>> finished_q_;
+  std::function<void(std::vector<Watermark>&&)> on_commit_;
+};
+
+}  // namespace tk

@@ -148,9 +148,10 @@ PYBIND11_MODULE(_tkhip, m) {
         e.synchronize();
       });
 
-  py::class_<LockstepTransport>(m, "LockstepTransport");
-  py::class_<PyLockstep, LockstepTransport>(m, "PyLockstep").def(py::init<py::function>(), py::arg("allreduce_min"));
-  py::class_<RcclLockstep, LockstepTransport>(m, "RcclLockstep")
+  py::class_<LockstepTransport>(m, "LockstepTransport", py::module_local());
+  py::class_<PyLockstep, LockstepTransport>(m, "PyLockstep", py::module_local())
+      .def(py::init<py::function>(), py::arg("allreduce_min"));
+  py::class_<RcclLockstep, LockstepTransport>(m, "RcclLockstep", py::module_local())
       .def(py::init([](const std::string& lib, py::bytes id, int rank, int world, int device, int slots) {
              return new RcclLockstep(lib, std::string(id), rank, world, device, slots);
            }),

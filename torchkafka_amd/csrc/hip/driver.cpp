@@ -297,105 +297,51 @@ bool MainDriver::pop_data(SlotView* out) {
   return false;
 }
 
-void MainDriver::enable_lockstep(LockstepTransport* ls, int depth) {
-  ls_ = ls;
-  depth_ = std::max(0, depth);
-  step_ = granted_ = 0;
-  delivered_index_ = -1;
-  stopped_ = no_more_credit_ = false;
-  tickets_.clear();
-  finished_q_.clear();
-}
-
-// Cross-rank lockstep as a credit protocol.  Ranks deliver batch indices in
-// the same order; `granted_` is the index below which every rank is known to
-// hold a batch.  An agreement carries each rank's count of batches it holds
-// beyond `granted_` (what is staged now -- never a wait on data that a worker
-// cannot publish while its ring slots are all staged here), or -1 if its
-// stream has ended and it holds none.  MIN over ranks extends `granted_`; -1
-// means no further credit will ever come, so all ranks stop at the same
-// index.  A new agreement is issued while `depth` credits remain, so its
-// round trip overlaps the delivery of those batches.  Every decision depends
-// only on (step_, granted_) and agreement results, which are identical on all
-// ranks, so the collective sequences stay aligned.  Completion of an
-// agreement issued at step s proves every rank reached s: batches < s are
-// finished everywhere and become committable.
-int64_t MainDriver::credit_value() const {
-  const int64_t beyond = int64_t(data_staged()) - (granted_ - step_);
-  if (beyond > 0) return beyond;
-  return all_done() ? -1 : 0;
-}
-
-void MainDriver::issue_agreement() {
-  const int64_t v = credit_value();
-  DTRACE("step %ld issue agreement base=%ld value=%ld staged=%d", long(step_), long(granted_), long(v),
-         data_staged());
-  tickets_.push_back(Ticket{step_, granted_, ls_->issue(v, step_, -step_)});
-}
-
-void MainDriver::settle_agreement() {
-  const Ticket t = tickets_.front();
-  tickets_.pop_front();
-  int64_t res[3];
-  ls_->wait(t.ticket, res);
-  if (res[1] != -res[2])
-    throw std::runtime_error("lockstep: ranks are out of step (min " + std::to_string(res[1]) + ", max " +
-                             std::to_string(-res[2]) + ")");
-  while (!finished_q_.empty() && finished_q_.front().first < t.step) {
-    add_finished(finished_q_.front().second);
-    finished_q_.pop_front();
+// The rank's data path as the lockstep protocol sees it (csrc/core/lockstep.h).
+class MainDriver::Source : public tk::LockstepSource {
+ public:
+  explicit Source(MainDriver& d) : d_(d) {}
+  int64_t staged() override { return d_.data_staged(); }
+  bool all_done() override { return d_.all_done(); }
+  int wait_data(int64_t timeout_ms) override {
+    const int64_t t0 = tk::now_ns();
+    const int r = d_.poll_blocking(timeout_ms);
+    d_.blocked_ns_ += tk::now_ns() - t0;
+    ++d_.blocked_calls_;
+    return r == -3 ? -3 : r == 1 ? 1 : 0;
   }
-  if (res[0] < 0)
-    no_more_credit_ = true;
-  else
-    granted_ = std::max(granted_, t.base + res[0]);
-  DTRACE("step %ld settled agreement from step %ld: min=%ld granted=%ld", long(step_), long(t.step), long(res[0]),
-         long(granted_));
+
+ private:
+  MainDriver& d_;
+};
+
+void MainDriver::enable_lockstep(LockstepTransport* ls, int depth) {
+  ls_ = std::make_unique<tk::CreditLockstep>(ls, depth);
+  ls_->set_on_committable([this](std::vector<tk::Watermark>&& wms) { add_finished(wms); });
+  delivered_index_ = -1;
 }
 
 int MainDriver::next_slot_lockstep(int64_t timeout_ms, SlotView* out) {
-  if (stopped_) return -2;
+  if (ls_->stopped()) return -2;
   // stage everything already published (non-blocking): these are the credits this rank can offer
   for (;;) {
     int r = poll_one(false, 0);
     if (r == -3) return -3;
     if (r <= 0) break;
   }
-  if (tickets_.empty() && !no_more_credit_ && granted_ - step_ <= depth_ && step_ < granted_) issue_agreement();
-  while (step_ >= granted_) {
-    if (no_more_credit_) {
-      stopped_ = true;
-      return -2;
-    }
-    bool starved = false;
-    if (tickets_.empty()) {
-      if (data_staged() == 0 && !all_done()) {
-        // nothing to offer yet: give this rank's workers a moment before spending a collective round
-        const int64_t t0 = tk::now_ns();
-        int r = poll_blocking(timeout_ms);
-        blocked_ns_ += tk::now_ns() - t0;
-        ++blocked_calls_;
-        if (r == -3) return -3;
-        starved = (r == -1 || r == 0);
-      }
-      issue_agreement();  // value 0 when still starved: the other ranks wait with us, nobody hangs
-    }
-    settle_agreement();
-    if (starved && step_ >= granted_) return -1;  // let the caller check worker health, then call again
-  }
+  Source src(*this);
+  const int r = ls_->next(src, timeout_ms);
+  DTRACE("lockstep next=%d step %ld granted %ld staged %d", r, long(ls_->step()), long(ls_->granted()),
+         data_staged());
+  if (r != 1) return r;
   if (!pop_data(out)) throw std::logic_error("lockstep: granted a batch that is not staged");
-  delivered_index_ = step_++;
+  delivered_index_ = ls_->delivered();
   return 1;
 }
 
 void MainDriver::finish_lockstep() {
   drain_fenced(true);
-  if (!ls_) return;
-  while (!tickets_.empty()) settle_agreement();  // every rank issued the same agreements
-  int64_t res[3];
-  ls_->wait(ls_->issue(0, 0, 0), res);  // every rank has stopped at the same step
-  for (auto& f : finished_q_) add_finished(f.second);
-  finished_q_.clear();
+  if (ls_) ls_->finish();
 }
 
 int MainDriver::next_slot(int64_t timeout_ms, SlotView* out) {
@@ -749,7 +695,7 @@ void MainDriver::add_finished(const std::vector<tk::Watermark>& wms) {
 
 void MainDriver::stage_finished(int64_t index, std::vector<tk::Watermark>&& wms) {
   if (ls_)
-    finished_q_.emplace_back(index, std::move(wms));
+    ls_->finished(index, std::move(wms));
   else
     add_finished(wms);
 }

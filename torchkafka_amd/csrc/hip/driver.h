@@ -160,7 +160,8 @@ class MainDriver {
   void enable_lockstep(LockstepTransport* ls, int depth);
   // End of a lock-stepped iteration: barrier, then every finished batch becomes committable.
   void finish_lockstep();
-  bool lockstep_enabled() const { return ls_ != nullptr; }
+  bool lockstep_enabled() const { return bool(ls_); }
+  uint64_t lockstep_agreements() const { return ls_ ? ls_->agreements() : 0; }
 
   SlotView last;  // the slot most recently returned by next_slot / step_fixed
 
@@ -213,20 +214,10 @@ class MainDriver {
   std::string parse_error_;
   std::vector<hipEvent_t> event_pool_;
 
-  struct Ticket {
-    int64_t step;   // step at which it was issued
-    int64_t base;   // granted_ at issue time
-    int ticket;
-  };
-  int64_t credit_value() const;
-  void issue_agreement();
-  void settle_agreement();
-  LockstepTransport* ls_ = nullptr;
-  int depth_ = 2;
-  int64_t step_ = 0, granted_ = 0, delivered_index_ = -1;
-  bool stopped_ = false, no_more_credit_ = false;
-  std::deque<Ticket> tickets_;
-  std::deque<std::pair<int64_t, std::vector<tk::Watermark>>> finished_q_;
+  // Cross-rank lockstep: the credit protocol (csrc/core/lockstep.h) over the caller's transport.
+  class Source;
+  std::unique_ptr<tk::CreditLockstep> ls_;
+  int64_t delivered_index_ = -1;
 
   Engine* eng_;
   bool registered_ = false;

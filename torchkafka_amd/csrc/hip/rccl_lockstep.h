@@ -19,17 +19,15 @@
 #include <string>
 #include <vector>
 
+#include "lockstep.h"
+
 namespace tkh {
 
 struct RcclApi;
 
-// A pipelined all-reduce(MIN) of three int64 per step: issue() returns a ticket, wait() its result.
-class LockstepTransport {
- public:
-  virtual ~LockstepTransport() = default;
-  virtual int issue(int64_t a, int64_t b, int64_t c) = 0;
-  virtual void wait(int ticket, int64_t out[3]) = 0;
-};
+// The transport interface lives in the HIP-free core (csrc/core/lockstep.h), next to the credit
+// protocol that drives it.
+using LockstepTransport = tk::LockstepTransport;
 
 class RcclLockstep : public LockstepTransport {
  public:
