@@ -469,3 +469,25 @@ def test_json_device_parse_coalesced_batches_on_another_stream(broker):
     ref = [[float(v) for v in json.loads(r)] for r in rows[0]]
     assert got == ref
     assert broker.committed_offsets("g", "s") == {0: 400}
+
+
+@pytest.mark.parametrize("decode,sharding", [("device", "static"), ("host", "static"), ("device", "group")])
+def test_worker_commit_sink_native_driver(broker, decode, sharding):
+    """commit_sink='worker' through the native step driver: finished offsets reach the workers'
+    consumers (group members under sharding='group'), which commit exactly what was delivered."""
+    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
+
+    broker.create_topic("t", 4)
+    broker.fill("t", 200, "fixed_f32", size=32, records_per_batch=25)
+    DS = _dataset(FixedWidth(torch.float32, (32,)))
+    dl = DeviceLoader(DS.placeholder(), 40, num_workers=2, device="cuda:0", decode=decode, sharding=sharding,
+                      commit_sink="worker",
+                      worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=700))
+    assert dl._sink == "worker"
+    n = 0
+    for x in auto_commit(dl):
+        _expected_rows(x[:4])
+        n += x.shape[0]
+    assert n == 800
+    assert broker.committed_offsets("g", "t") == {p: 200 for p in range(4)}

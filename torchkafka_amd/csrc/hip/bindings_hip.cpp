@@ -290,6 +290,8 @@ PYBIND11_MODULE(_tkhip, m) {
       .def("set_coalesce_wait_us", &MainDriver::set_coalesce_wait_us, py::arg("us"))
       .def("enable_direct", &MainDriver::enable_direct)
       .def("set_ahead_depth", &MainDriver::set_ahead_depth)
+      .def("set_worker_sink", &MainDriver::set_worker_sink, py::arg("table"), py::arg("n_workers"),
+           py::arg("capacity"))
       .def(
           "pin_logs",
           [](MainDriver& d, std::vector<uint32_t> pidxs) {

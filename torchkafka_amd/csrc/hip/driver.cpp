@@ -211,6 +211,8 @@ int MainDriver::poll_one_impl(bool block, int64_t timeout_ms) {
     v.src_dtype = h->src_dtype >= 0 ? h->src_dtype : default_src_dt_;
     if (h->src_dtype >= 0) v.shape.assign(h->shape, h->shape + h->ndim);
     v.wms.assign(h->wm, h->wm + h->n_parts);
+    if (sink_table_)
+      for (uint32_t k = 0; k < h->n_parts; ++k) pidx_worker_[h->wm[k].pidx] = h->worker;
     if (v.n_rows == 0) {
       // empty (end-of-stream) slot: keep its watermarks in delivery order
       ring_->main_release(uint32_t(g));
@@ -779,9 +781,54 @@ void MainDriver::drain_fenced(bool wait) {
   }
 }
 
+void MainDriver::set_worker_sink(uintptr_t table, int n_workers, int capacity) {
+  if (!table || n_workers < 1 || capacity < 1) throw std::invalid_argument("driver: bad worker commit table");
+  sink_table_ = reinterpret_cast<int64_t*>(table);
+  sink_workers_ = n_workers;
+  sink_cap_ = capacity;
+  sink_index_.assign(size_t(n_workers), {});
+}
+
+void MainDriver::publish_to_workers() {
+  std::vector<uint8_t> touched(size_t(sink_workers_), 0);
+  const int64_t block = 1 + 2 * int64_t(sink_cap_);
+  for (const auto& kv : pending_) {
+    auto it = pidx_worker_.find(kv.first);
+    if (it == pidx_worker_.end()) throw std::logic_error("driver: finished offsets of a partition no worker delivered");
+    const uint32_t w = it->second;
+    if (int(w) >= sink_workers_) throw std::logic_error("driver: worker index beyond the commit table");
+    int64_t* b = sink_table_ + 2 * int64_t(sink_workers_) + int64_t(w) * block;
+    auto& idx = sink_index_[w];
+    auto e = idx.find(kv.first);
+    if (e == idx.end()) {
+      const int64_t k = __atomic_load_n(b, __ATOMIC_RELAXED);
+      if (k >= sink_cap_) throw std::runtime_error("driver: worker commit table full");
+      __atomic_store_n(b + 1 + 2 * k, int64_t(kv.first), __ATOMIC_RELAXED);
+      __atomic_store_n(b + 2 + 2 * k, kv.second, __ATOMIC_RELAXED);
+      __atomic_store_n(b, k + 1, __ATOMIC_RELEASE);  // the entry is complete before n covers it
+      idx.emplace(kv.first, int(k));
+    } else if (kv.second > __atomic_load_n(b + 2 + 2 * e->second, __ATOMIC_RELAXED)) {
+      __atomic_store_n(b + 2 + 2 * e->second, kv.second, __ATOMIC_RELAXED);
+    }
+    touched[w] = 1;
+  }
+  for (int w = 0; w < sink_workers_; ++w)
+    if (touched[size_t(w)]) __atomic_fetch_add(sink_table_ + 2 * w, int64_t(1), __ATOMIC_RELEASE);
+}
+
 int MainDriver::commit_pending() {
   drain_fenced(false);
   if (pending_.empty()) return parse_error_.empty() ? 0 : -2;
+  if (sink_table_) {
+    // the workers' consumers commit (and log, and swallow CommitFailedError) asynchronously
+    const int64_t t0 = tk::now_ns();
+    publish_to_workers();
+    for (const auto& kv : pending_) committed_[kv.first] = kv.second;
+    pending_.clear();
+    ++commits_;
+    if (commit_ns_.size() < (1u << 20)) commit_ns_.push_back(tk::now_ns() - t0);
+    return parse_error_.empty() ? 1 : -2;
+  }
   if (!broker_) throw std::runtime_error("DeviceLoader cannot commit: no group_id / broker");
   const int64_t t0 = tk::now_ns();
   entries_.clear();

@@ -78,7 +78,11 @@ class MainDriver {
   void add_finished(const std::vector<tk::Watermark>& wms);
   // Commits every finished batch.  Returns 0 nothing to do, 1 committed, -1 CommitFailedError.
   int commit_pending();
-  bool can_commit() const { return broker_ != nullptr; }
+  bool can_commit() const { return broker_ != nullptr || sink_table_ != nullptr; }
+  // commit_sink='worker' (loader/commit_channel.py WatermarkTable): finished offsets are
+  // published to the worker that delivered each partition, whose own consumer commits them as a
+  // group member, instead of being stored into the synthetic broker from this process.
+  void set_worker_sink(uintptr_t table, int n_workers, int capacity);
 
   // Fused fast path: [finish+commit previous] -> next slot -> fixed-width collate into dst.
   // Returns n_rows (>0), or -1 timeout, -2 end, -3 error; *commit_status as commit_pending().
@@ -244,6 +248,11 @@ class MainDriver {
   std::vector<tk::Watermark> delivered_;
   std::unordered_map<uint32_t, int64_t> pending_;
   std::unordered_map<uint32_t, int64_t> committed_;
+  int64_t* sink_table_ = nullptr;  // WatermarkTable layout, see set_worker_sink
+  int sink_workers_ = 0, sink_cap_ = 0;
+  std::vector<std::unordered_map<uint32_t, int>> sink_index_;  // per worker: pidx -> entry
+  std::unordered_map<uint32_t, uint32_t> pidx_worker_;         // partition -> worker that delivers it
+  void publish_to_workers();
   std::vector<tk::CommitEntry> entries_;
   std::string error_;
   uint64_t commits_ = 0, commit_failures_ = 0;

@@ -92,3 +92,115 @@ class CommitChannel:
                 self._shm.unlink()
         except Exception:  # noqa: BLE001
             pass
+
+
+class WatermarkTable:
+    """Main -> worker commit requests carrying exact offsets (DeviceLoader ``commit_sink='worker'``).
+
+    The device loader knows exactly which records the user finished (slot watermarks), but only
+    the consumer that read a partition may commit it as a group member (Kafka rejects a commit
+    from a non-member once the group has members; a kafka-python consumer lives in its worker).
+    So the main process publishes, per worker, the finished offset of every partition that
+    worker delivered, and the worker's consumer commits them (kafka_dataset.py:124-143 messages,
+    CommitFailedError logged and swallowed as B14).
+
+    Layout (int64): per worker [seq_req, seq_ack], then per worker a block
+    [n, pidx_0, off_0, ..., pidx_{cap-1}, off_{cap-1}].  An entry's pidx is written once, before
+    ``n`` covers it; offsets only grow and are single aligned 64-bit stores, so a worker reading
+    while the main process writes sees each offset old or new, never torn.  ``seq_req`` is bumped
+    after every publish; the worker acknowledges the sequence it committed.  The native step
+    driver (csrc/hip/driver.cpp) writes the same layout through :attr:`address`.
+    """
+
+    def __init__(self, num_workers: int, capacity: int = 4096):
+        if num_workers < 1 or capacity < 1:
+            raise ValueError("watermark table needs num_workers >= 1 and capacity >= 1")
+        self.num_workers = num_workers
+        self.capacity = capacity
+        self._block = 1 + 2 * capacity
+        n = 2 * num_workers + num_workers * self._block
+        self._shm = shared_memory.SharedMemory(create=True, size=8 * n)
+        self._owner = True
+        self._arr = np.ndarray((n,), dtype=np.int64, buffer=self._shm.buf)
+        self._arr[:] = 0
+        self._index = [dict() for _ in range(num_workers)]
+
+    def __getstate__(self):
+        return {"name": self._shm.name, "num_workers": self.num_workers, "capacity": self.capacity}
+
+    def __setstate__(self, st):
+        self.num_workers, self.capacity = st["num_workers"], st["capacity"]
+        self._block = 1 + 2 * self.capacity
+        self._shm = shared_memory.SharedMemory(name=st["name"])
+        try:
+            from multiprocessing import resource_tracker
+
+            resource_tracker.unregister(self._shm._name, "shared_memory")  # type: ignore[attr-defined]
+        except Exception:  # noqa: BLE001
+            pass
+        self._owner = False
+        n = 2 * self.num_workers + self.num_workers * self._block
+        self._arr = np.ndarray((n,), dtype=np.int64, buffer=self._shm.buf)
+        self._index = [dict() for _ in range(self.num_workers)]
+
+    @property
+    def address(self) -> int:
+        """Address of the table in this process (the native driver writes through it)."""
+        return self._arr.ctypes.data
+
+    def _base(self, w: int) -> int:
+        return 2 * self.num_workers + w * self._block
+
+    # ---- main process
+    def publish(self, worker: int, offsets: dict) -> None:
+        """Offsets (pidx -> next offset) the user finished on ``worker``'s partitions."""
+        b = self._base(worker)
+        idx = self._index[worker]
+        for pidx, off in offsets.items():
+            k = idx.get(pidx)
+            if k is None:
+                k = int(self._arr[b])
+                if k >= self.capacity:
+                    raise RuntimeError("watermark table full: more partitions per worker than its capacity")
+                self._arr[b + 1 + 2 * k] = pidx
+                self._arr[b + 2 + 2 * k] = off
+                self._arr[b] = k + 1
+                idx[pidx] = k
+            elif off > self._arr[b + 2 + 2 * k]:
+                self._arr[b + 2 + 2 * k] = off
+        self._arr[2 * worker] += 1
+
+    def requested(self, worker: int) -> int:
+        return int(self._arr[2 * worker])
+
+    def acked(self, worker: int) -> int:
+        return int(self._arr[2 * worker + 1])
+
+    def wait_acks(self, timeout: float = 5.0, alive=None) -> bool:
+        deadline = time.monotonic() + timeout
+        while True:
+            pending = [w for w in range(self.num_workers) if self.acked(w) < self.requested(w)
+                       and (alive is None or alive(w))]
+            if not pending:
+                return True
+            if time.monotonic() >= deadline:
+                return False
+            time.sleep(0.001)
+
+    # ---- worker
+    def entries(self, worker: int) -> list:
+        b = self._base(worker)
+        n = int(self._arr[b])
+        return [(int(self._arr[b + 1 + 2 * k]), int(self._arr[b + 2 + 2 * k])) for k in range(n)]
+
+    def ack(self, worker: int, seq: int) -> None:
+        self._arr[2 * worker + 1] = seq
+
+    def close(self) -> None:
+        try:
+            self._arr = None
+            self._shm.close()
+            if self._owner:
+                self._shm.unlink()
+        except Exception:  # noqa: BLE001
+            pass

@@ -106,6 +106,13 @@ class _Run:
             topology.bind_to_gpu_numa(L.device.index)
         ctx = mp.get_context(L.multiprocessing_context)
         cfg = L._worker_cfg()
+        self.table = None          # commit_sink='worker': finished offsets published to the workers
+        self.pidx_worker: dict = {}
+        if L._sink == "worker":
+            from .commit_channel import WatermarkTable
+
+            self.table = WatermarkTable(L.num_workers)
+            cfg["commit_table"] = self.table
         pass_ring = L.multiprocessing_context == "fork"
         try:
             for w in range(L.num_workers):
@@ -127,6 +134,8 @@ class _Run:
                 self.driver = hip().MainDriver(self.engine, self.name, url, group, L.prefetch, L.in_order,
                                                L._default_src_code())
                 self.driver.set_commit_on_device(L.commit_on == "device")
+                if self.table is not None:
+                    self.driver.set_worker_sink(self.table.address, L.num_workers, self.table.capacity)
                 self.driver.set_event_every(L._event_every(self.ring.n_slots))
                 self.driver.set_coalesce(L.coalesce)
                 self.driver.set_coalesce_wait_us(L.coalesce_wait_us if L.coalesce > 1 else 0)
@@ -180,6 +189,9 @@ class _Run:
                 self.done[w] = True
                 ring.mark_done(w)
             wms = ring.watermarks(g)
+            if self.table is not None:
+                for w in wms:
+                    self.pidx_worker[w[0]] = summ[6]
             if n_rows == 0:
                 # empty (end-of-stream) slot: no data, but its watermarks may cover skipped records;
                 # it stays in delivery order so they are committed after the worker's earlier batches
@@ -207,6 +219,10 @@ class _Run:
         if self.closed:
             return
         self.closed = True
+        if self.table is not None:
+            # the workers' consumers commit what the user finished before they are stopped
+            self.table.wait_acks(timeout=10.0, alive=lambda w: self.procs[w].is_alive() if w < len(self.procs)
+                                 else False)
         try:
             self.ring.shutdown()
         except Exception:  # noqa: BLE001
@@ -224,6 +240,8 @@ class _Run:
         self.driver = None  # unregisters its pinned ring mapping
         self.rccl = None
         self.engine = None
+        if self.table is not None:
+            self.table.close()
         try:
             self.ring.unlink()
         except Exception:  # noqa: BLE001
@@ -298,7 +316,7 @@ class DeviceLoader:
                  lockstep_depth: int = 2, h2d: str = "auto", copy_streams: int = 4,
                  event_every: int | None = None, numa_bind: bool = True, coalesce: int = 8,
                  coalesce_wait_us: int = 50, json_parse: str = "auto",
-                 lockstep_timeout: float = 600.0, decode: str = "auto"):
+                 lockstep_timeout: float = 600.0, decode: str = "auto", commit_sink: str = "auto"):
         if batch_size < 1:
             raise ValueError("batch_size must be >= 1")
         if num_workers < 1:
@@ -344,6 +362,10 @@ class DeviceLoader:
         if decode not in ("auto", "device", "host"):
             raise ValueError("decode must be 'auto', 'device' (gfx950 RecordBatch decode) or 'host' (worker pack)")
         self.decode = decode
+        if commit_sink not in ("auto", "broker", "worker"):
+            raise ValueError("commit_sink must be 'auto', 'broker' (the main process stores offsets into the "
+                             "synthetic broker) or 'worker' (each worker's consumer commits its partitions)")
+        self.commit_sink = commit_sink
         self.copy_streams = max(1, int(copy_streams))
         self.event_every = None if event_every is None else max(1, int(event_every))
         self.numa_bind = bool(numa_bind)
@@ -356,6 +378,7 @@ class DeviceLoader:
         self.timeout = timeout
         self.base_seed = int(torch.empty((), dtype=torch.int64).random_().item()) if base_seed is None else base_seed
         self._group_id, self._servers = self._resolve_commit_target(group_id, bootstrap_servers)
+        self._sink = self._resolve_sink()
         self._pending_wms: list = []   # finished-but-uncommitted watermark lists
         self._committed: dict[int, int] = {}
         self._norm = None
@@ -376,6 +399,29 @@ class DeviceLoader:
                 group_id = group_id if group_id is not None else cons.config.get("group_id")
                 servers = servers if servers is not None else cons.config.get("bootstrap_servers")
         return group_id, servers
+
+    def _resolve_sink(self) -> str:
+        """Where finished offsets are committed.  'broker': this process stores them straight into
+        the synthetic broker's offset table (one native store per batch) -- only valid when the
+        workers are simple (manually assigned) consumers of a synthetic broker.  'worker': each
+        worker's own consumer commits them: required with sharding='group' (a member's commit is
+        tied to its generation) and with any other consumer (kafka-python)."""
+        synthetic = self._commit_target_url()[0] != ""
+        if self.commit_sink == "broker":
+            if not synthetic or self.sharding != "static":
+                raise ValueError("commit_sink='broker' needs the synthetic broker, a group_id and sharding='static'")
+            return "broker"
+        if self.commit_sink == "worker" or self.sharding == "group" or not synthetic:
+            return "worker"
+        return "broker"
+
+    def _process_overridden(self) -> bool:
+        """The dataset maps records with a ``_process`` of its own (reference kafka_dataset.py:159):
+        the native schema packers and the device decode would bypass it, so the workers run the
+        per-record loop and the batches take the generic path."""
+        from ..models.kafka_dataset import KafkaDataset
+
+        return type(self.dataset)._process is not KafkaDataset._process
 
     def _commit_target_url(self) -> tuple[str, str]:
         if self._group_id is None or self._servers is None:
@@ -444,14 +490,15 @@ class DeviceLoader:
             B = self.batch_size
             segs = 2 * B + 128 + (B * s.row_bytes) // (32 << 10)
             return (B * 8 + 255) // 256 * 256 + 32 * segs
-        if s is not None and getattr(s, "kind", None) == 0:
+        if s is not None and getattr(s, "kind", None) == 0 and not self._process_overridden():
             return self.batch_size * s.row_bytes
         return 16 << 20
 
     def _worker_cfg(self) -> dict:
         return {"batch_size": self.batch_size, "sharding": self.sharding, "rank": self.rank,
                 "world_size": self.world_size, "native": self.native, "base_seed": self.base_seed,
-                "gather": self._direct(), "json_device": self._json_device(), "span": self._span()}
+                "gather": self._direct(), "json_device": self._json_device(), "span": self._span(),
+                "process_overridden": self._process_overridden(), "commit_table": None}
 
     def _rank_partitions(self) -> list[int]:
         """Broker partition indices this rank's workers will read (static sharding of the topics
@@ -488,7 +535,7 @@ class DeviceLoader:
             return False
         s = self.schema
         ok = (self.device.type == "cuda" and self.native and getattr(s, "kind", None) == 0
-              and self.h2d != "direct" and self._commit_target_url()[0] != "")
+              and self.h2d != "direct" and self._commit_target_url()[0] != "" and not self._process_overridden())
         if self.decode == "device" and not ok:
             raise ValueError("decode='device' needs a CUDA device, a FixedWidth schema, native=True, h2d != 'direct' "
                              "and the synthetic broker (bootstrap_servers shm:// or file://) with a group_id")
@@ -505,7 +552,7 @@ class DeviceLoader:
         the host parser there.
         """
         s = self.schema
-        if getattr(s, "kind", None) != 2 or self.json_parse == "host":
+        if getattr(s, "kind", None) != 2 or self.json_parse == "host" or self._process_overridden():
             return False
         ok = self.device.type == "cuda" and self.native and not getattr(s, "skip_bad", False)
         if self.json_parse == "device" and not ok:
@@ -621,7 +668,7 @@ class DeviceLoader:
     def _fast_path_ok(self) -> bool:
         s = self.schema
         return (s is not None and getattr(s, "kind", None) == 0 and self.native and not self.return_info
-                and not self.drop_last)
+                and not self.drop_last and not self._process_overridden())
 
     def _make_rccl_lockstep(self, process_group):
         """Native RCCL communicator for the per-step lockstep (id broadcast through torch.distributed)."""
@@ -679,7 +726,7 @@ class DeviceLoader:
     def _varlen_fast_ok(self) -> bool:
         s = self.schema
         return (s is not None and getattr(s, "kind", None) in (1, 2) and self.native and not self.return_info
-                and not self.drop_last and not _roctx_enabled())
+                and not self.drop_last and not _roctx_enabled() and not self._process_overridden())
 
     def _iterate_varlen_fast(self, run: _Run, auto_commit: bool):
         """Var-len / JSON GPU iteration, one native call per batch (MainDriver.varlen_next): finish +
@@ -1059,11 +1106,13 @@ class DeviceLoader:
             return
         offsets: dict[int, int] = {}
         keep = []
-        for entry in pending:
+        for i, entry in enumerate(pending):
             wms, ev = entry if isinstance(entry, tuple) else (entry, None)
             if ev is not None and not wait and not ev.query():
-                keep.append(entry)
-                continue
+                # in order: a later batch is never committed before an earlier one (the committed
+                # offset must not go backwards when the earlier one completes)
+                keep.extend(pending[i:])
+                break
             if ev is not None and wait:
                 ev.synchronize()
             for pidx, _first, nxt, _cnt in wms:
@@ -1074,6 +1123,19 @@ class DeviceLoader:
             self._commit(offsets)
 
     def _commit(self, offsets: dict[int, int]) -> None:
+        if self._sink == "worker":
+            run = self._run
+            if run is None or run.table is None or run.closed:
+                raise RuntimeError("DeviceLoader commit_sink='worker': commit() must be called while iterating")
+            t0 = time.perf_counter_ns()
+            by_worker: dict[int, dict[int, int]] = {}
+            for p, o in offsets.items():
+                by_worker.setdefault(run.pidx_worker[p], {})[p] = o
+            for w, offs in by_worker.items():
+                run.table.publish(w, offs)  # that worker's consumer commits (and logs) them
+            self._committed.update(offsets)
+            self.stats.record_commit(time.perf_counter_ns() - t0)
+            return
         if self._group_id is None:
             raise RuntimeError("DeviceLoader cannot commit: no group_id (pass it to init_worker or DeviceLoader)")
         t0 = time.perf_counter_ns()

@@ -67,12 +67,25 @@ def worker_main(ring, ring_name: str, worker_id: int, num_workers: int, dataset,
             topics = sorted(consumer.subscription() or [])
             if not topics:
                 raise RuntimeError("static sharding needs the consumer to be created with its topics")
+            if not hasattr(consumer, "assign_shard"):
+                raise RuntimeError("static sharding needs the synthetic-broker consumer; use sharding='group' "
+                                   "with a kafka-python consumer (Kafka's group assignment shards partitions)")
             consumer.assign_shard(topics, cfg["rank"], cfg["world_size"], worker_id, num_workers)
-        if cfg["native"] and getattr(consumer, "_fetcher", None) is not None and dataset.schema is not None:
+        sink = _WorkerSink(cfg.get("commit_table"), worker_id, dataset, consumer)
+        state["sink"] = sink
+        if (cfg["native"] and getattr(consumer, "_fetcher", None) is not None and dataset.schema is not None
+                and not cfg.get("process_overridden", False)):
+            sink.start_thread()
             _native_loop(ring, worker_id, spw, consumer, dataset.schema, cfg, state)
         else:
+            # a `_process` of its own (or a consumer without the native fetcher): the reference's
+            # per-record loop, kafka_dataset.py:156-162
             _generic_loop(ring, worker_id, spw, consumer, dataset, cfg, state)
+        sink.serve_until_shutdown(ring)
     except _StopWorker:
+        sink = state.get("sink")
+        if sink is not None:
+            sink.serve_once()  # the final commit request may have come with the shutdown
         return
     except BaseException:  # noqa: BLE001 - everything goes to the main process
         msg = f"Caught exception in DeviceLoader worker {worker_id} (pid {os.getpid()}):\n{traceback.format_exc()}"
@@ -87,6 +100,81 @@ def worker_main(ring, ring_name: str, worker_id: int, num_workers: int, dataset,
             ring.worker_publish(g)
         except Exception:  # noqa: BLE001
             pass
+
+
+class _WorkerSink:
+    """commit_sink='worker': this worker's consumer commits the offsets the main process
+    published for its partitions (loader/commit_channel.py WatermarkTable) -- as a group member
+    when the consumer joined a group, through kafka-python when that is the consumer -- with the
+    reference's worker log messages and CommitFailedError handling (kafka_dataset.py:124-143)."""
+
+    def __init__(self, table, worker_id, dataset, consumer):
+        import threading
+
+        self.table, self.w, self.ds, self.consumer = table, worker_id, dataset, consumer
+        self.seen = 0
+        self.committed: dict = {}
+        self.lock = threading.Lock()   # the consumer is used by one thread at a time
+        self.local_tps: list = []      # generic loop without a broker: local id -> TopicPartition
+        self._thread = None
+
+    def tp_of(self, pidx: int):
+        broker = getattr(self.consumer, "_broker", None)
+        if broker is not None:
+            return broker.tp_of(pidx)
+        return self.local_tps[pidx & 0xFFFF]
+
+    def serve_once(self) -> None:
+        t = self.table
+        if t is None:
+            return
+        seq = t.requested(self.w)
+        if seq <= self.seen:
+            return
+        from ..client.records import OffsetAndMetadata
+
+        offsets = {}
+        for pidx, off in t.entries(self.w):
+            if off > self.committed.get(pidx, -1):
+                offsets[pidx] = off
+        if offsets:
+            with self.lock:
+                self.ds._do_commit({self.tp_of(p): OffsetAndMetadata(o, "") for p, o in offsets.items()})
+            # a failed commit (rebalance) is logged and not retried, as in the reference (B14)
+            self.committed.update(offsets)
+        self.seen = seq
+        t.ack(self.w, seq)
+
+    def start_thread(self) -> None:
+        """Native loop: the fill runs in C++ without the GIL; commits are served beside it."""
+        if self.table is None or self._thread is not None:
+            return
+        import threading
+        import time
+
+        def run():
+            while True:
+                time.sleep(0.001)
+                try:
+                    self.serve_once()
+                except Exception:  # noqa: BLE001 - logged; the next request retries
+                    import logging
+
+                    logging.getLogger(__name__).exception("commit on worker %d failed", self.w)
+
+        self._thread = threading.Thread(target=run, name="torchkafka-worker-commit", daemon=True)
+        self._thread.start()
+
+    def serve_until_shutdown(self, ring) -> None:
+        """After end of stream: keep committing what the user finishes until the loader closes."""
+        if self.table is None:
+            return
+        import time
+
+        while not ring.is_shutdown():
+            self.serve_once()
+            time.sleep(0.001)
+        self.serve_once()
 
 
 def _acquire(ring, worker_id: int, state: dict) -> int:
@@ -150,17 +238,37 @@ def _native_loop(ring, worker_id, spw, consumer, schema, cfg, state) -> None:
 
 
 def _generic_loop(ring, worker_id, spw, consumer, dataset, cfg, state) -> None:
+    """The reference's per-record loop (kafka_dataset.py:156-162) around ``dataset._process``,
+    over ``consumer.poll`` so commit requests are served between polls (kafka-python consumers
+    are not thread-safe) and an idle partition never blocks them (D8).  Watermarks carry the
+    synthetic broker's partition index, or -- for any other consumer (kafka-python) -- a
+    worker-local id of the (topic, partition) that only this worker's commit sink resolves."""
+    import time
+
     bs = int(cfg["batch_size"])
     broker = getattr(consumer, "_broker", None)
+    sink = state.get("sink")
     cap = ring.payload_capacity
     samples: list = []
     wm: dict = {}  # pidx -> [first, next, count]
     first_pos: dict = {}
+    local: dict = {}
+    timeout_ms = _consumer_timeout_ms(consumer)
 
     def pidx_of(rec):
-        if broker is None:
-            raise RuntimeError("DeviceLoader's generic path needs the synthetic-broker consumer")
-        return broker.pidx(rec.topic, rec.partition)
+        if broker is not None:
+            return broker.pidx(rec.topic, rec.partition)
+        if sink is None or sink.table is None:
+            raise RuntimeError("DeviceLoader needs commit_sink='worker' for a consumer other than the synthetic "
+                               "broker's")
+        key = (rec.topic, rec.partition)
+        k = local.get(key)
+        if k is None:
+            from ..client.records import TopicPartition
+
+            k = local[key] = (worker_id << 16) | len(sink.local_tps)
+            sink.local_tps.append(TopicPartition(rec.topic, rec.partition))
+        return k
 
     def flush(eos: bool) -> None:
         g = _acquire(ring, worker_id, state)
@@ -209,18 +317,43 @@ def _generic_loop(ring, worker_id, spw, consumer, dataset, cfg, state) -> None:
         samples.clear()
         wm.clear()
 
-    for record in consumer:
-        p = pidx_of(record)
-        ent = wm.get(p)
-        if ent is None:
-            ent = wm[p] = [first_pos.get(p, record.offset), record.offset + 1, 0]
-        ent[1] = record.offset + 1
-        ent[2] += 1
-        first_pos[p] = record.offset + 1
-        data = dataset._process(record)
-        if data is None:
+    last_data = time.monotonic()
+    while True:
+        if sink is not None:
+            sink.serve_once()
+        if ring.is_shutdown():
+            raise _StopWorker
+        with (sink.lock if sink is not None else _nolock):
+            polled = consumer.poll(timeout_ms=20, max_records=max(1, bs - len(samples)))
+        if not polled:
+            if timeout_ms >= 0 and (time.monotonic() - last_data) * 1000.0 >= timeout_ms:
+                break  # consumer_timeout_ms without records: end of stream, as the consumer iterator does
             continue
-        samples.append(data)
-        if len(samples) == bs:
-            flush(False)
+        last_data = time.monotonic()
+        for _tp, records in polled.items():
+            for record in records:
+                p = pidx_of(record)
+                ent = wm.get(p)
+                if ent is None:
+                    ent = wm[p] = [first_pos.get(p, record.offset), record.offset + 1, 0]
+                ent[1] = record.offset + 1
+                ent[2] += 1
+                first_pos[p] = record.offset + 1
+                data = dataset._process(record)
+                if data is None:
+                    continue
+                samples.append(data)
+                if len(samples) == bs:
+                    flush(False)
     flush(True)
+
+
+class _NoLock:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+_nolock = _NoLock()
