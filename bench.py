@@ -214,7 +214,8 @@ def main() -> int:
     committed = broker.committed_offsets("bench", "bench")
     if rank == 0:
         if args.stats:
-            print(json.dumps({"loader_stats": stats, "fill_s": t_fill, "committed_sample": dict(list(committed.items())[:4])}),
+            print(json.dumps({"loader_stats": stats, "fill_s": t_fill,
+                              "committed_sample": dict(list(committed.items())[:4])}),
                   file=sys.stderr)
         out = {
             "metric": BASELINE_METRIC,
@@ -228,9 +229,11 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_VALUE, 3),
             "dtype": args.dtype,
-            "data": "synthetic (Kafka RecordBatch v2 records in the shared-memory broker, random-free deterministic f32)",
+            "data": ("synthetic (Kafka RecordBatch v2 records in the shared-memory broker, "
+                     "random-free deterministic f32)"),
             "config": {
-                "model": f"KafkaDataset FixedWidth f32[{args.dim}] ({args.dim * 4} B records) -> {args.dtype} via gfx950 collate",
+                "model": (f"KafkaDataset FixedWidth f32[{args.dim}] ({args.dim * 4} B records) -> {args.dtype} "
+                          "via gfx950 collate"),
                 "global_batch": B * world,
                 "seq_len": args.dim,
                 "parallelism": f"dp{world}",

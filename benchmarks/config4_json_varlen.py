@@ -78,7 +78,9 @@ def main():
         text_bytes = b.partition_stats("json", 0)["log_bytes"] / max(1, b.end_offset("json", 0))
         print(json.dumps({"config": 4, "metric": "JSON records/s to GPU (bf16 padded), per-batch commit",
                           "value": round(rows / el), "ms_per_step": round(el / args.steps * 1e3, 4),
-                          "batch_size": B, "json_parse": args.json_parse, "h2d": args.h2d, "avg_record_bytes": round(text_bytes), "last_batch_shape": list(x.shape),
+                          "batch_size": B, "json_parse": args.json_parse, "h2d": args.h2d,
+                          "avg_record_bytes": round(text_bytes),
+                          "last_batch_shape": list(x.shape),
                           "device": args.device, "fill_s": round(fill_s, 2), "loader": st}))
     finally:
         b.destroy()

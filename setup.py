@@ -20,6 +20,7 @@ setup(
     package_data={"torchkafka_amd": ["csrc/core/*", "csrc/hip/*", "*.so"]},
     python_requires=">=3.8",
     install_requires=["torch>=1.6.0", "numpy", "pybind11"],
-    extras_require={"kafka": ["kafka-python>=2.0.2"], "dev": ["pytest", "pytest-timeout"]},
+    extras_require={"kafka": ["kafka-python>=2.0.2"],
+                    "dev": ["pytest", "pytest-timeout", "hypothesis", "pylint", "ruff"]},
     cmdclass={"build_py": BuildNative},
 )

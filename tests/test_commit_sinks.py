@@ -18,7 +18,6 @@ import sys
 import types
 from collections import namedtuple
 
-import pytest
 import torch
 
 from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit

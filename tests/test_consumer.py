@@ -1,6 +1,5 @@
 """KafkaConsumer / KafkaProducer: kafka-python compatible behaviour over the synthetic broker."""
 import json
-import os
 import time
 
 import pytest

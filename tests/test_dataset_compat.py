@@ -2,7 +2,6 @@
 and the deliberate fixes of its defects (§2.7, D1-D8).  CPU only, torch DataLoader paths."""
 import json
 import logging
-import os
 import signal
 import threading
 import time
@@ -12,7 +11,7 @@ import torch
 from torch.utils.data import DataLoader
 
 from torchkafka_amd import KafkaDataset, auto_commit
-from torchkafka_amd.client.errors import CommitFailedError, IllegalStateError, NoBrokersAvailable
+from torchkafka_amd.client.errors import IllegalStateError, NoBrokersAvailable
 
 
 class Rand8(KafkaDataset):

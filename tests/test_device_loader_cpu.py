@@ -225,7 +225,8 @@ def test_static_sharding_across_ranks(broker):
 def test_group_sharding_mode(broker):
     broker.create_topic("t", 4)
     broker.fill("t", 25, "fixed_f32", size=16)
-    xs = torch.cat(list(loader(Vec16, broker, 10, workers=2, sharding="group", consumer_kw={"consumer_timeout_ms": 600})))
+    xs = torch.cat(list(loader(Vec16, broker, 10, workers=2, sharding="group",
+                               consumer_kw={"consumer_timeout_ms": 600})))
     assert sorted(map(tuple, xs[:, :2].long().tolist())) == sorted((o, p) for p in range(4) for o in range(25))
 
 

@@ -6,7 +6,6 @@ proves the protocol at world sizes 2 and 4 without GPUs.
 import json
 import os
 import socket
-import uuid
 
 import pytest
 import torch

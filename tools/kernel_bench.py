@@ -92,7 +92,8 @@ def main():
         g_ours = timeit_graph(lambda: collate_fixed(src, dt), iters)
         g_torch = timeit_graph(lambda: src.to(dt), iters)
         nbytes = src.numel() * 4 + src.numel() * torch.empty((), dtype=dt).element_size()
-        out.append({"kernel": "fixed", "case": name, "gpu_us": round(g_ours, 2), "GBps": round(nbytes / g_ours / 1e3, 1),
+        out.append({"kernel": "fixed", "case": name, "gpu_us": round(g_ours, 2),
+                    "GBps": round(nbytes / g_ours / 1e3, 1),
                     "torch_gpu_us": round(g_torch, 2), "torch_GBps": round(nbytes / g_torch / 1e3, 1),
                     "eager_us": round(t_ours, 2), "torch_eager_us": round(t_torch, 2)})
 
@@ -141,7 +142,8 @@ def main():
                                                           2, rows, L, 0.0, ln.data_ptr(), 0,
                                                           torch.cuda.current_stream(dev).cuda_stream), iters)
         g_torch = timeit_graph(torch_pad, iters)
-        out.append({"kernel": "varlen", "case": name, "gpu_us": round(g_ours, 2), "GBps": round(nbytes / g_ours / 1e3, 1),
+        out.append({"kernel": "varlen", "case": name, "gpu_us": round(g_ours, 2),
+                    "GBps": round(nbytes / g_ours / 1e3, 1),
                     "torch_gpu_us": round(g_torch, 2), "torch_GBps": round(nbytes / g_torch / 1e3, 1),
                     "eager_us": round(t_ours, 2), "torch_eager_us": round(t_torch, 2)})
 

@@ -7,6 +7,7 @@ from .errors import (
 from .producer import KafkaProducer
 from .records import ConsumerRecord, OffsetAndMetadata, OffsetAndTimestamp, RecordMetadata, TopicPartition
 
-__all__ = ["KafkaConsumer", "KafkaProducer", "ConsumerRecord", "TopicPartition", "OffsetAndMetadata", "OffsetAndTimestamp",
+__all__ = ["KafkaConsumer", "KafkaProducer", "ConsumerRecord", "TopicPartition", "OffsetAndMetadata",
+           "OffsetAndTimestamp",
            "RecordMetadata", "KafkaError", "CommitFailedError", "CorruptRecordException", "NoBrokersAvailable",
            "OffsetOutOfRangeError", "KafkaConfigurationError"]

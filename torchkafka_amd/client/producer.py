@@ -30,7 +30,8 @@ def murmur2(data: bytes) -> int:
     length4 = length // 4
     for i in range(length4):
         i4 = i * 4
-        k = (data[i4] & 0xFF) + ((data[i4 + 1] & 0xFF) << 8) + ((data[i4 + 2] & 0xFF) << 16) + ((data[i4 + 3] & 0xFF) << 24)
+        k = ((data[i4] & 0xFF) + ((data[i4 + 1] & 0xFF) << 8) + ((data[i4 + 2] & 0xFF) << 16)
+             + ((data[i4 + 3] & 0xFF) << 24))
         k = (k * m) & 0xFFFFFFFF
         k ^= (k % 0x100000000) >> r
         k = (k * m) & 0xFFFFFFFF
