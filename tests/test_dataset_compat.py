@@ -264,6 +264,49 @@ def test_d3_exact_commit_with_prefetch(broker):
     assert broker.committed_offsets("group_1", "topic") == {0: 24, 1: 24}
 
 
+def _pairs_collate(samples):
+    """A collate_fn that changes the leading dimension (pairs of samples per row)."""
+    x = torch.stack(samples)
+    return x.reshape(-1, 2 * x.shape[1]) if x.shape[0] % 2 == 0 else x.reshape(1, -1)
+
+
+def test_exact_commit_with_reshaping_collate_fn(broker):
+    """The main process counts finished *batches* per worker; the worker maps them to samples, so
+    a collate_fn that reshapes the batch cannot skew the committed offsets."""
+    produce_offsets(broker, n=21, partitions=2)
+    ds = PartOffset.placeholder()
+    dl = DataLoader(ds, batch_size=4, num_workers=2, prefetch_factor=2, collate_fn=_pairs_collate,
+                    worker_init_fn=PartOffset.init_worker("topic", **kw(broker, consumer_timeout_ms=600)))
+    gen = auto_commit(dl)
+    first = next(gen)
+    assert first.shape == (2, 4)  # 4 samples in 2 rows
+    p = int(first[0, 0])
+    second = next(gen)
+    deadline = time.time() + 5
+    while broker.committed("group_1", "topic", p) is None and time.time() < deadline:
+        time.sleep(0.005)
+    assert broker.committed("group_1", "topic", p) == int(first[-1, 3]) + 1 == 4
+    rest = [second] + list(gen)
+    rows = torch.cat([b.reshape(-1, 2) for b in [first] + rest]).tolist()
+    assert sorted(map(tuple, rows)) == [(q, o) for q in range(2) for o in range(21)]
+    assert broker.committed_offsets("group_1", "topic") == {0: 21, 1: 21}
+
+
+def test_manual_break_commits_only_finished_batches(broker):
+    """Breaking out commits exactly the batches finished before the break (B8 + D3)."""
+    produce_offsets(broker, n=40, partitions=1)
+    ds = PartOffset.placeholder()
+    dl = DataLoader(ds, batch_size=5, num_workers=1, prefetch_factor=4,
+                    worker_init_fn=PartOffset.init_worker("topic", **kw(broker, consumer_timeout_ms=600)))
+    for i, _ in enumerate(auto_commit(dl)):
+        if i == 3:
+            break
+    deadline = time.time() + 5
+    while broker.committed("group_1", "topic", 0) != 15 and time.time() < deadline:
+        time.sleep(0.005)
+    assert broker.committed("group_1", "topic", 0) == 15  # batches 0..2 finished; batch 3 was not
+
+
 def test_d4_d5_uneven_workers_no_signal_death(broker):
     """Worker 0 runs dry early: attribution stays right and no worker is killed (reference D4/D5)."""
     broker.create_topic("topic", 2)

@@ -491,3 +491,30 @@ def test_worker_commit_sink_native_driver(broker, decode, sharding):
         n += x.shape[0]
     assert n == 800
     assert broker.committed_offsets("g", "t") == {p: 200 for p in range(4)}
+
+
+@pytest.mark.parametrize("decode,coalesce", [("device", 8), ("host", 1), ("host", 8)])
+def test_native_path_logs_commits_like_reference(broker, caplog, decode, coalesce):
+    """DEBUG 'Committing offsets.' before and 'Committed offsets.' after every native commit
+    (reference kafka_dataset.py:124-143); one commit per delivered batch under auto_commit."""
+    import logging
+
+    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
+
+    broker.create_topic("t", 2)
+    broker.fill("t", 100, "fixed_f32", size=32, records_per_batch=25)
+    DS = _dataset(FixedWidth(torch.float32, (32,)))
+    dl = DeviceLoader(DS.placeholder(), 20, num_workers=2, device="cuda:0", decode=decode, coalesce=coalesce,
+                      worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    with caplog.at_level(logging.DEBUG, logger="torchkafka.kafka_dataset"):
+        n = sum(1 for _ in auto_commit(dl))
+    msgs = [r.getMessage() for r in caplog.records if r.name == "torchkafka.kafka_dataset"]
+    seq = [m for m in msgs if m in ("Committing offsets.", "Committed offsets.")]
+    assert n == 10
+    assert seq.count("Committing offsets.") == n
+    assert 1 <= seq.count("Committed offsets.") <= n
+    for a, b in zip(seq, seq[1:]):  # every 'Committed' directly follows its 'Committing'
+        if b == "Committed offsets.":
+            assert a == "Committing offsets."
+    assert broker.committed_offsets("g", "t") == {0: 100, 1: 100}

@@ -23,7 +23,6 @@ from __future__ import annotations
 import itertools as it
 import logging
 
-import torch
 from torch.utils.data import DataLoader
 
 from .commit_channel import CommitChannel
@@ -35,20 +34,6 @@ def _is_kafka_dataset(ds) -> bool:
     from ..models.kafka_dataset import KafkaDataset
 
     return isinstance(ds, KafkaDataset) or bool(getattr(type(ds), "_torchkafka_dataset", False))
-
-
-def _batch_len(batch, default: int) -> int:
-    if isinstance(batch, torch.Tensor):
-        return int(batch.shape[0]) if batch.dim() else default
-    if isinstance(batch, (list, tuple)) and batch:
-        first = batch[0]
-        if isinstance(first, torch.Tensor) and len(batch) and all(isinstance(b, torch.Tensor) for b in batch):
-            # default_collate of equal-length lists yields a *transposed* list of tensors (B25)
-            return int(first.shape[0]) if first.dim() else default
-        return _batch_len(first, default) if isinstance(first, (list, tuple, dict)) else len(batch)
-    if isinstance(batch, dict) and batch:
-        return _batch_len(next(iter(batch.values())), default)
-    return default
 
 
 def auto_commit(dataloader, *, final_commit_timeout: float = 5.0, process_group=None):
@@ -111,7 +96,9 @@ def _multi_worker(dataloader: DataLoader, final_commit_timeout: float):
         for batch in batches:
             w = last_worker[0] if attribution is None else next(attribution)
             yield batch
-            consumed[w] += _batch_len(batch, bs)
+            # batches, not samples: the worker maps its k-th batch to the consumer positions after
+            # its samples, whatever shape the collate_fn gave the batch
+            consumed[w] += 1
             channel.request(w, consumed[w])
         # normal end: make sure every worker committed its final batch before shutdown
         channel.close_requests()

@@ -4,9 +4,10 @@ The reference asks a worker to commit with SIGUSR1 (kafka_dataset.py:235-239)
 and the worker commits its consumer *position*, which already includes every
 prefetched batch (B10/D3); after the stream ends the default action of the
 signal kills the worker (D4).  Here the main process publishes, per worker,
-the cumulative number of that worker's samples the user has finished with;
-the worker maps the count to the consumer positions it recorded when it
-produced that sample and commits exactly those.  Workers acknowledge, so the
+the cumulative number of that worker's *batches* the user has finished with
+(counted by the main process, so a collate_fn that reshapes batches cannot
+skew it); the worker maps batch k to the consumer positions it recorded after
+its sample min(k * batch_size, produced) and commits exactly those.  Workers acknowledge, so the
 main process can wait for the final commit before tearing workers down.
 """
 from __future__ import annotations
@@ -53,14 +54,14 @@ class CommitChannel:
     def _i(self, w: int, which: int) -> int:
         return _HDR + 2 * w + which
 
-    def request(self, worker: int, samples: int) -> None:
-        self._arr[self._i(worker, _REQ)] = samples
+    def request(self, worker: int, batches: int) -> None:
+        self._arr[self._i(worker, _REQ)] = batches
 
     def requested(self, worker: int) -> int:
         return int(self._arr[self._i(worker, _REQ)])
 
-    def ack(self, worker: int, samples: int) -> None:
-        self._arr[self._i(worker, _ACK)] = samples
+    def ack(self, worker: int, batches: int) -> None:
+        self._arr[self._i(worker, _ACK)] = batches
 
     def acked(self, worker: int) -> int:
         return int(self._arr[self._i(worker, _ACK)])

@@ -691,6 +691,7 @@ class DeviceLoader:
         drv = run.driver
         debug = _ds_logger.isEnabledFor(logging.DEBUG)
         completed = False
+        delivered = False
         try:
             if self._fast_path_ok():
                 yield from self._fast_loop(run, auto_commit, debug)
@@ -698,12 +699,13 @@ class DeviceLoader:
                 while True:
                     # asking for the next batch finishes the previous one
                     drv.finish_delivered(_stream_ptr(self.device))
-                    if auto_commit:
-                        self._log_commit(drv.commit_pending(), debug)
+                    if auto_commit and delivered:
+                        self._commit_native(drv, debug)
                     item = self._next_item_driver(run)
                     if item is None:
                         break
                     drv.deliver_last()
+                    delivered = True
                     yield item[0]
             completed = True
         finally:
@@ -713,7 +715,7 @@ class DeviceLoader:
                     drv.finish_lockstep()
                 drv.drain_fenced(True)
                 if completed and auto_commit:
-                    self._log_commit(drv.commit_pending(), debug)
+                    self._commit_native(drv, debug)
                 elif not auto_commit:
                     # manual mode: keep every yielded batch committable by DeviceLoader.commit()
                     pend = drv.take_pending()
@@ -738,18 +740,24 @@ class DeviceLoader:
         dst_dt = self._out_dtype(src)
         if (dst_dt in FLOAT_DTYPES) != (src in FLOAT_DTYPES) and src in FLOAT_DTYPES:
             raise TypeError(f"cannot collate {src} records to {dst_dt}")
+        log_commits = debug and auto_commit
         args = (self.device.index, DTYPE_CODE[dst_dt], -1 if self.pad_to is None else int(self.pad_to),
-                self.pad_multiple, float(self.pad_value), bool(self.return_mask), auto_commit, 100)
+                self.pad_multiple, float(self.pad_value), bool(self.return_mask), auto_commit and not log_commits,
+                100)
         step = drv.varlen_next
         want_mask = self.return_mask
         completed = False
         try:
             wait_since = None
+            delivered = False
             while True:
                 r, cs, out, lengths, mask = step(*args)
                 if cs:
                     self._log_commit(cs, debug)
                 if r == 1:
+                    if log_commits and delivered:
+                        self._commit_logged(drv)
+                    delivered = True
                     wait_since = None
                     yield (out, lengths, mask) if want_mask else (out, lengths)
                 elif r == -2:
@@ -773,7 +781,7 @@ class DeviceLoader:
                     drv.finish_lockstep()
                 drv.drain_fenced(True)
                 if completed and auto_commit:
-                    self._log_commit(drv.commit_pending(), debug)
+                    self._commit_native(drv, debug)
                 elif not auto_commit:
                     pend = drv.take_pending()
                     if pend:
@@ -791,16 +799,21 @@ class DeviceLoader:
         s = self.schema
         prm = self._norm_params(s.row_elems)
         shift, scale = (prm[0].data_ptr(), prm[1].data_ptr()) if prm is not None else (0, 0)
+        log_commits = debug and auto_commit
         drv.configure_fast(self.device.index, [self.batch_size, *s.shape], DTYPE_CODE[self._out_dtype(s.dtype)],
-                           s.row_elems, shift, scale, auto_commit, 100, self.coalesce > 1)
+                           s.row_elems, shift, scale, auto_commit and not log_commits, 100, self.coalesce > 1)
         step = drv.fast_next
         completed = False
+        delivered = False
         try:
             while True:
                 r, cs, out = step()
                 if r > 0:
                     if cs:
                         self._log_commit(cs, debug)
+                    elif log_commits and delivered:
+                        self._commit_logged(drv)
+                    delivered = True
                     yield out
                 elif r == -2:
                     break
@@ -829,7 +842,7 @@ class DeviceLoader:
                 drv.finish_lockstep()
             drv.drain_fenced(True)
             if completed and auto_commit:
-                self._log_commit(drv.commit_pending(), debug)
+                self._commit_native(drv, debug)
             elif not auto_commit:
                 pend = drv.take_pending()
                 if pend:
@@ -869,12 +882,18 @@ class DeviceLoader:
         # one native call per batch: allocate (torch caching allocator, current stream),
         # finish + commit the previous batch, take the next slot, launch the collate
         step = hip().step_fixed_group_tensor if self.coalesce > 1 else hip().step_fixed_tensor
+        log_commits = debug and auto_commit
+        native_ac = auto_commit and not log_commits
+        delivered = False
         while True:
             t0 = time.perf_counter_ns()
-            r, cs, out = step(drv, dev_index, out_shape, dst_code, row, shift, scale, auto_commit, 100)
+            r, cs, out = step(drv, dev_index, out_shape, dst_code, row, shift, scale, native_ac, 100)
             if cs:
                 self._log_commit(cs, debug)
             if r > 0:
+                if log_commits and delivered:
+                    self._commit_logged(drv)
+                delivered = True
                 stats.batches += 1
                 stats.records += r
                 stats.issue_ns += time.perf_counter_ns() - t0
@@ -889,6 +908,26 @@ class DeviceLoader:
                 run._check_workers_native()
                 if self.timeout > 0 and time.perf_counter_ns() - t0 > self.timeout * 1e9:
                     raise TimeoutError(f"DeviceLoader timed out after {self.timeout}s waiting for a batch")
+
+    def _commit_logged(self, drv) -> None:
+        """One native commit bracketed by the reference's DEBUG messages (kafka_dataset.py:124-143).
+
+        With DEBUG enabled the native loops hand the commit back to Python (the step call is made
+        with its inline commit off), so "Committing offsets." precedes the store as it does in the
+        reference; without DEBUG the commit stays inside the one native step call.  With
+        ``commit_sink='worker'`` the workers commit and log ("Committing offsets on worker %d."), as
+        the reference's workers do, and the main process stays silent."""
+        if self._sink == "worker":
+            self._log_commit(drv.commit_pending(), False)
+            return
+        _ds_logger.debug("Committing offsets.")
+        self._log_commit(drv.commit_pending(), True)
+
+    def _commit_native(self, drv, debug: bool) -> None:
+        if debug:
+            self._commit_logged(drv)
+        else:
+            self._log_commit(drv.commit_pending(), False)
 
     def _log_commit(self, status: int, debug: bool) -> None:
         if status == -2:  # a device-parsed batch was malformed: it (and what follows) stays uncommitted
@@ -1158,7 +1197,7 @@ class DeviceLoader:
         if run is not None and run.driver is not None and not run.closed:
             run.driver.finish_delivered(_stream_ptr(self.device))
             run.driver.drain_fenced(True)
-            self._log_commit(run.driver.commit_pending(), _ds_logger.isEnabledFor(logging.DEBUG))
+            self._commit_logged(run.driver)
             self._absorb_driver_stats(run.driver)
         self._commit_finished(wait=True)
 

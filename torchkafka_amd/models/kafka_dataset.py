@@ -154,18 +154,22 @@ class KafkaDataset(IterableDataset):
         if ch is None or self._worker_id is None:
             return
         with self._channel_lock:
+            # the request counts this worker's *batches* the user finished; the DataLoader's
+            # fetcher cuts a worker's stream into batch_size samples per batch (only the last one
+            # of the stream is short), so batch k ends at sample min(k * batch_size, yielded)
             req = ch.requested(self._worker_id)
             if req <= self._channel_done:
                 return
+            limit = req * ch.batch_size
             snap = None
-            while self._snapshots and self._snapshots[0][0] <= req:
+            while self._snapshots and self._snapshots[0][0] <= limit:
                 snap = self._snapshots.popleft()
             if snap is not None:
                 offsets = {TopicPartition(t, p): OffsetAndMetadata(o, "") for (t, p), o in snap[1].items()}
                 if offsets:
                     self._do_commit(offsets)
                 # a failed commit is logged and not retried, as in the reference (B14)
-                self._channel_done = snap[0]
+            self._channel_done = req
             ch.ack(self._worker_id, req)
 
     def _start_committer(self) -> None:
@@ -181,8 +185,12 @@ class KafkaDataset(IterableDataset):
             return
 
         def run():
-            while True:
-                time.sleep(0.002)
+            # 2 ms while requests keep coming, backing off to 50 ms once the main process has
+            # been quiet for a while; ends once the main process announced its last request
+            nap, ch = 0.002, self._commit_channel
+            while ch is not None and not ch.closing():
+                time.sleep(nap)
+                seen = self._channel_done
                 if self._consumer_lock.acquire(blocking=False):
                     try:
                         self._service_channel()
@@ -190,6 +198,7 @@ class KafkaDataset(IterableDataset):
                         _logger.exception("commit request failed on worker %s", self._worker_id)
                     finally:
                         self._consumer_lock.release()
+                nap = 0.002 if self._channel_done != seen else min(0.05, nap * 1.25)
 
         self._committer = threading.Thread(target=run, name="torchkafka-committer", daemon=True)
         self._committer.start()
@@ -201,7 +210,7 @@ class KafkaDataset(IterableDataset):
         self._channel_finalizer = mpu.Finalize(self, KafkaDataset._final_service, args=(self,), exitpriority=100)
 
     @staticmethod
-    def _final_service(ds, max_wait: float = 60.0) -> None:
+    def _final_service(ds, max_wait: float = 15.0) -> None:
         """Worker exit hook: serve the commit of this worker's last batch.
 
         The DataLoader may shut a worker down as soon as its end of stream is
@@ -217,7 +226,7 @@ class KafkaDataset(IterableDataset):
                 with ds._consumer_lock:
                     ds._service_channel()
                 total = getattr(ds, "_final_yielded", None)
-                if ch is None or total is None or ch.acked(ds._worker_id) >= total or ch.closing():
+                if ch is None or total is None or ch.acked(ds._worker_id) * ch.batch_size >= total or ch.closing():
                     break
                 if os.getppid() != parent or time.monotonic() > deadline:
                     break
