@@ -288,3 +288,63 @@ def test_state_dict_round_trip_resumes_exactly(broker):
     assert firsts == {p: o for p, o in snap.items() if o < 200}
     with pytest.raises(ValueError):
         dl2.load_state_dict({"version": 2, "offsets": {}})
+
+
+def _direct(ds_cls, broker, topic="t", group="g", **kw):
+    """The reference's single-process construction: the dataset owns its consumer."""
+    d = dict(bootstrap_servers=broker.url, group_id=group, auto_offset_reset="earliest", consumer_timeout_ms=250)
+    d.update(kw)
+    return ds_cls(topic, **d)
+
+
+def test_single_process_mode_exact_commits(broker):
+    """num_workers=0 (reference auto_commit.py:49-58): no worker processes; a thread of this process
+    packs the ring with the dataset's own consumer; every batch is committed once finished."""
+    import multiprocessing as mp
+
+    broker.create_topic("t", 3)
+    broker.fill("t", 50, "fixed_f32", size=16, records_per_batch=20)
+    dl = DeviceLoader(_direct(Vec16, broker), 16, num_workers=0, device="cpu")
+    children = len(mp.active_children())
+    seen = set()
+    gen = auto_commit(dl)
+    first = next(gen)
+    assert len(mp.active_children()) == children  # nothing was forked
+    for x in [first, *gen]:
+        check_rows(x)
+        seen |= {tuple(r) for r in x[:, :2].long().tolist()}
+    assert len(seen) == 150
+    assert broker.committed_offsets("g", "t") == {0: 50, 1: 50, 2: 50}
+
+
+def test_single_process_mode_break_and_resume(broker):
+    broker.create_topic("t", 1)
+    broker.fill("t", 60, "fixed_f32", size=16)
+    ds = _direct(Vec16, broker)
+    for i, _x in enumerate(auto_commit(DeviceLoader(ds, 10, num_workers=0, device="cpu"))):
+        if i == 2:
+            break
+    assert broker.committed("g", "t", 0) == 20  # batches 0 and 1 finished; the break skips batch 2
+    ds.close()
+    rest = torch.cat(list(auto_commit(DeviceLoader(_direct(Vec16, broker), 10, num_workers=0, device="cpu"))))
+    assert sorted(rest[:, 0].long().tolist()) == list(range(20, 60))
+    assert broker.committed("g", "t", 0) == 60
+
+
+def test_single_process_mode_generic_process(broker):
+    broker.create_topic("t", 2)
+    broker.fill("t", 40, "fixed_f32", size=16)
+    xs = torch.cat(list(auto_commit(DeviceLoader(_direct(Doubled, broker), 7, num_workers=0, device="cpu"))))
+    offs = sorted((xs[:, 0] / 2).long().tolist())
+    assert len(offs) == 60 and all(o % 4 for o in offs)
+    assert broker.committed_offsets("g", "t") == {0: 40, 1: 40}
+
+
+def test_single_process_mode_argument_errors(broker):
+    broker.create_topic("t", 1)
+    with pytest.raises(ValueError, match=r"num_workers=0\) needs a dataset with its consumer"):
+        DeviceLoader(Vec16.placeholder(), 8, num_workers=0, device="cpu")
+    with pytest.raises(ValueError, match="worker_init_fn is not used"):
+        DeviceLoader(_direct(Vec16, broker), 8, num_workers=0, device="cpu", worker_init_fn=init(Vec16, broker))
+    with pytest.raises(ValueError, match="num_workers must be >= 0"):
+        DeviceLoader(Vec16.placeholder(), 8, num_workers=-1, device="cpu")

@@ -518,3 +518,42 @@ def test_native_path_logs_commits_like_reference(broker, caplog, decode, coalesc
         if b == "Committed offsets.":
             assert a == "Committing offsets."
     assert broker.committed_offsets("g", "t") == {0: 100, 1: 100}
+
+
+@pytest.mark.parametrize("decode", ["device", "host"])
+def test_single_process_mode_on_gpu(broker, decode):
+    """num_workers=0: the dataset's own consumer, packed by a thread of this process, through the
+    same native step driver and kernels (reference auto_commit.py:49-58)."""
+    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
+
+    broker.create_topic("t", 2)
+    broker.fill("t", 128, "fixed_f32", size=32, records_per_batch=32)
+    DS = _dataset(FixedWidth(torch.float32, (32,)))
+    ds = DS("t", bootstrap_servers=broker.url, group_id="g", auto_offset_reset="earliest", consumer_timeout_ms=300)
+    dl = DeviceLoader(ds, 32, num_workers=0, device="cuda:0", decode=decode)
+    rows = set()
+    for x in auto_commit(dl):
+        assert x.is_cuda
+        _expected_rows(x[:3])
+        rows |= {tuple(r) for r in x[:, :2].long().tolist()}
+    assert len(rows) == 256
+    assert broker.committed_offsets("g", "t") == {0: 128, 1: 128}
+
+
+@pytest.mark.parametrize("tuning", [dict(decode_streams=1, span_burst=0, ahead_depth=0),
+                                    dict(decode_streams=2, span_burst=4, ahead_depth=8, coalesce=2)])
+def test_tuning_knobs_do_not_change_results(broker, tuning):
+    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
+
+    broker.create_topic("t", 4)
+    broker.fill("t", 300, "fixed_f32", size=64, records_per_batch=40)
+    DS = _dataset(FixedWidth(torch.float32, (64,)))
+    dl = DeviceLoader(DS.placeholder(), 48, num_workers=2, device="cuda:0", decode="device", **tuning,
+                      worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    rows = []
+    for x in auto_commit(dl):
+        _expected_rows(x[:2])
+        rows += [tuple(r) for r in x[:, :2].long().tolist()]
+    assert len(rows) == len(set(rows)) == 1200
+    assert broker.committed_offsets("g", "t") == {p: 300 for p in range(4)}

@@ -7,13 +7,14 @@ is an alias of this package.
 """
 import numpy.random  # noqa: F401  -- import eagerly: a lazy import racing a DataLoader fork deadlocks/crashes workers
 
+from .config import LoaderConfig, Tuning
 from .loader import DeviceLoader, KafkaBatch, auto_commit
 from .models import FixedWidth, JsonArray, KafkaDataset, VarLen
 
 __version__ = "1.2.0+mi355x.1"
 
-__all__ = ["KafkaDataset", "auto_commit", "DeviceLoader", "KafkaBatch", "FixedWidth", "VarLen", "JsonArray",
-           "SyntheticBroker", "KafkaConsumer", "KafkaProducer"]
+__all__ = ["KafkaDataset", "auto_commit", "DeviceLoader", "KafkaBatch", "LoaderConfig", "Tuning", "FixedWidth",
+           "VarLen", "JsonArray", "SyntheticBroker", "KafkaConsumer", "KafkaProducer"]
 
 
 def __getattr__(name):

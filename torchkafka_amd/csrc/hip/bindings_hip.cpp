@@ -143,6 +143,8 @@ PYBIND11_MODULE(_tkhip, m) {
            [](Engine& e, int s, uintptr_t stream, size_t off, uintptr_t dst, size_t n) {
              e.copy_raw(s, stream_of(stream), off, ptr<void>(dst), n);
            })
+      .def("set_decode_streams", &Engine::set_decode_streams, py::arg("n"))
+      .def("decode_streams", &Engine::decode_streams)
       .def("synchronize", [](Engine& e) {
         py::gil_scoped_release nogil;
         e.synchronize();
@@ -290,6 +292,7 @@ PYBIND11_MODULE(_tkhip, m) {
       .def("set_coalesce_wait_us", &MainDriver::set_coalesce_wait_us, py::arg("us"))
       .def("enable_direct", &MainDriver::enable_direct)
       .def("set_ahead_depth", &MainDriver::set_ahead_depth)
+      .def("set_span_burst", &MainDriver::set_span_burst)
       .def("set_worker_sink", &MainDriver::set_worker_sink, py::arg("table"), py::arg("n_workers"),
            py::arg("capacity"))
       .def(

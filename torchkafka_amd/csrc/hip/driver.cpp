@@ -560,11 +560,7 @@ void MainDriver::launch_span(const int* slots, const SlotView* const* views, int
     a.b[k].partials = part_dev_ + perrs[k] * kPartials;
   }
   a.vec_store = vec ? 1 : 0;
-  static const int burst = [] {  // loads a wave keeps in flight (span_decode.hip stage 1)
-    const char* e = std::getenv("TORCHKAFKA_SPAN_BURST");
-    return e ? std::atoi(e) : 1;
-  }();
-  a.burst = burst;
+  a.burst = span_burst_;  // loads a wave keeps in flight (span_decode.hip stage 1)
   int launches = 0;
   for (int k = 0; k < n; ++k) {
     const SlotView& v = *views[k];

@@ -8,6 +8,8 @@
 // the finished-but-uncommitted offsets, and commits straight into the
 // broker's shared-memory offset table.
 #pragma once
+
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <deque>
@@ -126,6 +128,14 @@ class MainDriver {
   void ahead_launch(int dst_dt, void* const* dsts, const float* shift, const float* scale,
                     std::vector<std::shared_ptr<void>>&& handles);
   void set_ahead_depth(int n) { ahead_depth_ = n < 0 ? 0 : n; }
+  // LDS-DMA loads a wave of the span decode kernel keeps in flight before it waits (0 = all;
+  // default 1; TORCHKAFKA_SPAN_BURST)
+  void set_span_burst(int n) { span_burst_ = n < 0 ? 0 : n > 8 ? 8 : n; }
+  int span_burst_ = [] {
+    const char* e = std::getenv("TORCHKAFKA_SPAN_BURST");
+    const int v = e ? std::atoi(e) : 1;
+    return v < 0 ? 0 : v > 8 ? 8 : v;
+  }();
   int ahead_depth_ = 4;  // config 2: depth 0 52.2 M, 3-6 52.3-52.7 M steady, and 54 M over 2000 steps
   // The stream the next device-decode group launch runs on (its outputs are allocated there).
   hipStream_t next_decode_stream() { return eng_->decode_stream(int(span_launches_ % 4096)); }

@@ -75,7 +75,9 @@ class Engine {
   const uint32_t* span_tables();
   // The streams device-decode groups rotate over (created on first use; kDecodeStreams).
   hipStream_t decode_stream(int k);
-  int decode_streams() const;
+  int decode_streams() const { return n_decode_; }
+  // number of decode streams (1..4); only before the first decode stream is created
+  void set_decode_streams(int n);
   // Creates the decode streams, uploads the CRC tables and runs an empty kernel on every decode
   // stream (the runtime binds a stream to a hardware queue at its first launch), so none of that
   // lands on the first batches of an iteration.
@@ -112,6 +114,8 @@ class Engine {
   size_t host_len_ = 0;
   uint32_t* span_tabs_ = nullptr;
   hipStream_t decode_streams_[4] = {nullptr, nullptr, nullptr, nullptr};
+  int n_decode_ = default_decode_streams();
+  static int default_decode_streams();
   std::vector<hipEvent_t> order_events_;  // stream_after: a small pool used round-robin
   size_t order_next_ = 0;
 };

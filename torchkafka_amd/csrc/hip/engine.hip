@@ -244,16 +244,19 @@ const uint32_t* Engine::span_tables() {
   return span_tabs_;
 }
 
-int Engine::decode_streams() const {
-  static const int n = [] {
-    const char* e = std::getenv("TORCHKAFKA_DECODE_STREAMS");
-    // three decode streams + the user's stream fill the 4 hardware queues HIP gives a process by
-    // default (config 2: 2 streams 52.9 M rec/s, 3 streams 54.0 M, 4 streams 45.0 M -- the fourth
-    // shares a queue)
-    const int v = e ? std::atoi(e) : 3;
-    return v < 1 ? 1 : v > 4 ? 4 : v;
-  }();
-  return n;
+int Engine::default_decode_streams() {
+  // three decode streams + the user's stream fill the 4 hardware queues HIP gives a process by
+  // default (config 2: 2 streams 52.9 M rec/s, 3 streams 54.0 M, 4 streams 45.0 M -- the fourth
+  // shares a queue).  TORCHKAFKA_DECODE_STREAMS / Tuning.decode_streams override it.
+  const char* e = std::getenv("TORCHKAFKA_DECODE_STREAMS");
+  const int v = e ? std::atoi(e) : 3;
+  return v < 1 ? 1 : v > 4 ? 4 : v;
+}
+
+void Engine::set_decode_streams(int n) {
+  for (auto st : decode_streams_)
+    if (st != nullptr) throw std::runtime_error("set_decode_streams: decode streams already created");
+  n_decode_ = n < 1 ? 1 : n > 4 ? 4 : n;
 }
 
 __global__ void decode_warm_kernel() {}

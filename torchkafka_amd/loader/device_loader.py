@@ -31,6 +31,7 @@ from __future__ import annotations
 import logging
 import multiprocessing as mp
 import os
+import threading
 import time
 import uuid
 from collections import deque
@@ -39,6 +40,7 @@ from typing import NamedTuple
 import torch
 
 from ..client.errors import COMMIT_FAILED_ERRORS, CorruptRecordException
+from ..config import LoaderConfig
 from ..ops.collate import CODE_DTYPE, DTYPE_CODE, FLOAT_DTYPES, _stream_ptr, normalize_params
 from ..ops.native import core, hip
 from ..parallel.sharding import dist_rank_world
@@ -82,6 +84,23 @@ class WorkerError(RuntimeError):
     pass
 
 
+class _PackerThread(threading.Thread):
+    """num_workers=0: the ring producer as a thread of the main process (looks like a worker
+    process to the liveness checks)."""
+
+    def __init__(self, ring, name, dataset, cfg):
+        super().__init__(target=worker_main, args=(ring, name, 0, 1, dataset, None, cfg), daemon=True,
+                         name="torchkafka-packer")
+        self.pid = os.getpid()
+
+    @property
+    def exitcode(self):
+        return None if self.is_alive() else 0
+
+    def terminate(self):  # stops at ring.shutdown(); nothing to signal
+        pass
+
+
 class _Run:
     """Resources of one iteration: ring, worker processes, H2D engine."""
 
@@ -89,7 +108,7 @@ class _Run:
         self.loader = loader
         L = loader
         self.name = f"/tkring-{os.getpid()}-{uuid.uuid4().hex[:10]}"
-        self.ring = core().Ring.create(self.name, L.num_workers, L._slots_per_worker(), L._slot_capacity())
+        self.ring = core().Ring.create(self.name, L.n_producers, L._slots_per_worker(), L._slot_capacity())
         self.procs: list = []
         self.engine = None
         self.driver = None
@@ -97,7 +116,7 @@ class _Run:
         self.payload_addr = [self.ring.payload_address(g) for g in range(self.ring.n_slots)]
         self.staged: deque = deque()       # (g, summary, wms) with H2D issued (or CPU: just acquired)
         self.inflight: list = []           # slots whose H2D may still be reading host memory
-        self.done = [False] * L.num_workers
+        self.done = [False] * L.n_producers
         self.carry: list = []              # watermarks of consumed-but-undelivered records
         self.closed = False
         if L.numa_bind and L.device.type == "cuda" and L.device.index is not None:
@@ -111,10 +130,17 @@ class _Run:
         if L._sink == "worker":
             from .commit_channel import WatermarkTable
 
-            self.table = WatermarkTable(L.num_workers)
+            self.table = WatermarkTable(L.n_producers)
             cfg["commit_table"] = self.table
         pass_ring = L.multiprocessing_context == "fork"
         try:
+            if L.num_workers == 0:
+                # single-process mode: the packer runs in a thread of this process (the native fill
+                # releases the GIL), on the dataset's own consumer
+                cfg["in_process"] = True
+                t = _PackerThread(self.ring, self.name, L.dataset, cfg)
+                t.start()
+                self.procs.append(t)
             for w in range(L.num_workers):
                 p = ctx.Process(target=worker_main,
                                 args=(self.ring if pass_ring else None, self.name, w, L.num_workers, L.dataset,
@@ -135,7 +161,7 @@ class _Run:
                                                L._default_src_code())
                 self.driver.set_commit_on_device(L.commit_on == "device")
                 if self.table is not None:
-                    self.driver.set_worker_sink(self.table.address, L.num_workers, self.table.capacity)
+                    self.driver.set_worker_sink(self.table.address, L.n_producers, self.table.capacity)
                 self.driver.set_event_every(L._event_every(self.ring.n_slots))
                 self.driver.set_coalesce(L.coalesce)
                 self.driver.set_coalesce_wait_us(L.coalesce_wait_us if L.coalesce > 1 else 0)
@@ -143,8 +169,13 @@ class _Run:
                     self.driver.enable_direct()
                 if L._direct() or L._span():
                     self.driver.pin_logs(L._rank_partitions())
-                if "TORCHKAFKA_AHEAD_DEPTH" in os.environ:
-                    self.driver.set_ahead_depth(int(os.environ["TORCHKAFKA_AHEAD_DEPTH"]))
+                tun = L.tuning
+                if tun.ahead_depth is not None:
+                    self.driver.set_ahead_depth(int(tun.ahead_depth))
+                if tun.span_burst is not None:
+                    self.driver.set_span_burst(int(tun.span_burst))
+                if tun.decode_streams is not None:
+                    self.engine.set_decode_streams(int(tun.decode_streams))
         except BaseException:
             self.close()
             raise
@@ -257,12 +288,21 @@ class DeviceLoader:
     :func:`~torchkafka_amd.auto_commit` (commit after every batch).
 
     Args:
-        dataset: a ``KafkaDataset`` placeholder (workers build consumers via ``worker_init_fn``).
+        dataset: a ``KafkaDataset`` placeholder (workers build consumers via ``worker_init_fn``), or
+            -- with ``num_workers=0`` -- a dataset built with its consumer (``YourDataset(topic, ...)``).
         batch_size: records per batch (per rank).
-        num_workers: consumer/packer processes (>= 1).
+        num_workers: consumer/packer processes; 0 = the reference's single-process mode
+            (auto_commit.py:49-58): a thread of this process consumes and packs the pinned ring
+            slots with the dataset's own consumer, and the device path is unchanged.
         worker_init_fn: usually ``YourDataset.init_worker(topic, group_id=..., bootstrap_servers=...)``.
         device: target device (default: current CUDA device, else CPU).
         dtype: output dtype (default: the schema's); floats may go to bf16/f16/fp8 (OCP e4m3fn).
+        config: a :class:`~torchkafka_amd.config.LoaderConfig` (or its dict form).  Every field below
+            can also be passed as a keyword argument, which overrides the config; the performance
+            knobs (``slots_per_worker``, ``slot_bytes``, ``prefetch``, ``copy_streams``,
+            ``event_every``, ``coalesce``, ``coalesce_wait_us``, ``lockstep_depth``, ``numa_bind``,
+            ``ahead_depth``, ``decode_streams``, ``span_burst``, ``worker_spin_us``) form its
+            :class:`~torchkafka_amd.config.Tuning` (docs/CONFIG.md).  Options:
         normalize: optional ``(mean, std)`` fused into the collate kernel.
         sharding: ``"static"`` rank/worker partition map (default) or ``"group"`` (Kafka group assignment).
         slots_per_worker: ring depth per worker (prefetched batches in pinned memory).  Default: as
@@ -305,30 +345,26 @@ class DeviceLoader:
     """
 
     def __init__(self, dataset, batch_size: int = 256, *, num_workers: int = 4, worker_init_fn=None,
-                 device=None, dtype: torch.dtype | None = None, normalize=None, sharding: str = "static",
-                 slots_per_worker: int | None = None, prefetch: int = 2, in_order: bool = False,
-                 drop_last: bool = False,
-                 pad_to: int | None = None, pad_multiple: int = 8, pad_value: float = 0, return_mask: bool = False,
-                 return_info: bool = False, slot_bytes: int | None = None, native: bool = True,
-                 multiprocessing_context: str = "fork", commit_on: str = "host", lockstep: bool = True,
-                 rank: int | None = None, world_size: int | None = None, timeout: float = 0,
-                 group_id: str | None = None, bootstrap_servers=None, base_seed: int | None = None,
-                 lockstep_depth: int = 2, h2d: str = "auto", copy_streams: int = 4,
-                 event_every: int | None = None, numa_bind: bool = True, coalesce: int = 8,
-                 coalesce_wait_us: int = 50, json_parse: str = "auto",
-                 lockstep_timeout: float = 600.0, decode: str = "auto", commit_sink: str = "auto"):
+                 device=None, dtype: torch.dtype | None = None, config: LoaderConfig | dict | None = None,
+                 **options):
         if batch_size < 1:
             raise ValueError("batch_size must be >= 1")
-        if num_workers < 1:
-            raise ValueError("DeviceLoader needs num_workers >= 1 (records are consumed in worker processes)")
-        if sharding not in ("static", "group"):
-            raise ValueError("sharding must be 'static' or 'group'")
-        if commit_on not in ("host", "device"):
-            raise ValueError("commit_on must be 'host' or 'device'")
+        if num_workers < 0:
+            raise ValueError("num_workers must be >= 0")
+        cfg = self.config = LoaderConfig.build(config, **options)
+        tun = cfg.tuning
         self.dataset = dataset
         self.batch_size = int(batch_size)
         self.num_workers = int(num_workers)
         self.worker_init_fn = worker_init_fn
+        if self.num_workers == 0:
+            # the reference's single-process mode (auto_commit.py:49-58): the dataset was built with
+            # its consumer in this process; a thread of this process packs the ring slots
+            if getattr(dataset, "_consumer", None) is None:
+                raise ValueError("DeviceLoader(num_workers=0) needs a dataset with its consumer, e.g. "
+                                 "YourDataset('topic', bootstrap_servers=..., group_id=...), not a placeholder")
+            if worker_init_fn is not None:
+                raise ValueError("worker_init_fn is not used with num_workers=0 (there are no workers)")
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
@@ -336,54 +372,54 @@ class DeviceLoader:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.schema = getattr(dataset, "schema", None)
         self.dtype = dtype
-        self.normalize = normalize
-        self.sharding = sharding
-        self.slots_per_worker = None if slots_per_worker is None else max(2, int(slots_per_worker))
-        self.prefetch = max(0, int(prefetch))
-        self.in_order = in_order
-        self.drop_last = drop_last
-        self.pad_to = pad_to
-        self.pad_multiple = max(1, int(pad_multiple))
-        self.pad_value = pad_value
-        self.return_mask = return_mask
-        self.return_info = return_info
-        self.slot_bytes = slot_bytes
-        self.native = native
-        self.multiprocessing_context = multiprocessing_context
-        self.commit_on = commit_on
-        self.lockstep = lockstep
-        self.lockstep_depth = max(0, int(lockstep_depth))
-        if h2d not in ("auto", "dma", "zerocopy", "direct"):
-            raise ValueError("h2d must be 'auto', 'dma' (hipMemcpyAsync on side streams), 'zerocopy' or 'direct'")
-        self.h2d = h2d
-        if json_parse not in ("auto", "device", "host"):
-            raise ValueError("json_parse must be 'auto', 'device' (gfx950 parse kernel) or 'host' (worker parse)")
-        self.json_parse = json_parse
-        if decode not in ("auto", "device", "host"):
-            raise ValueError("decode must be 'auto', 'device' (gfx950 RecordBatch decode) or 'host' (worker pack)")
-        self.decode = decode
-        if commit_sink not in ("auto", "broker", "worker"):
-            raise ValueError("commit_sink must be 'auto', 'broker' (the main process stores offsets into the "
-                             "synthetic broker) or 'worker' (each worker's consumer commits its partitions)")
-        self.commit_sink = commit_sink
-        self.copy_streams = max(1, int(copy_streams))
-        self.event_every = None if event_every is None else max(1, int(event_every))
-        self.numa_bind = bool(numa_bind)
-        self.coalesce = max(1, min(8, int(coalesce)))
-        self.coalesce_wait_us = max(0, int(coalesce_wait_us))
-        self.lockstep_timeout = float(lockstep_timeout)
+        # behaviour (config.LoaderConfig)
+        self.normalize = cfg.normalize
+        self.sharding = cfg.sharding
+        self.in_order = cfg.in_order
+        self.drop_last = cfg.drop_last
+        self.pad_to = cfg.pad_to
+        self.pad_multiple = int(cfg.pad_multiple)
+        self.pad_value = cfg.pad_value
+        self.return_mask = cfg.return_mask
+        self.return_info = cfg.return_info
+        self.native = cfg.native
+        self.multiprocessing_context = cfg.multiprocessing_context
+        self.commit_on = cfg.commit_on
+        self.commit_sink = cfg.commit_sink
+        self.lockstep = cfg.lockstep
+        self.lockstep_timeout = float(cfg.lockstep_timeout)
+        self.h2d = cfg.h2d
+        self.json_parse = cfg.json_parse
+        self.decode = cfg.decode
+        self.timeout = cfg.timeout
         r, w = dist_rank_world()
-        self.rank = r if rank is None else int(rank)
-        self.world_size = w if world_size is None else int(world_size)
-        self.timeout = timeout
-        self.base_seed = int(torch.empty((), dtype=torch.int64).random_().item()) if base_seed is None else base_seed
-        self._group_id, self._servers = self._resolve_commit_target(group_id, bootstrap_servers)
+        self.rank = r if cfg.rank is None else int(cfg.rank)
+        self.world_size = w if cfg.world_size is None else int(cfg.world_size)
+        self.base_seed = (int(torch.empty((), dtype=torch.int64).random_().item()) if cfg.base_seed is None
+                          else cfg.base_seed)
+        # performance (config.Tuning)
+        self.tuning = tun
+        self.slots_per_worker = None if tun.slots_per_worker is None else int(tun.slots_per_worker)
+        self.slot_bytes = tun.slot_bytes
+        self.prefetch = int(tun.prefetch)
+        self.copy_streams = int(tun.copy_streams)
+        self.event_every = None if tun.event_every is None else int(tun.event_every)
+        self.coalesce = int(tun.coalesce)
+        self.coalesce_wait_us = int(tun.coalesce_wait_us)
+        self.lockstep_depth = int(tun.lockstep_depth)
+        self.numa_bind = bool(tun.numa_bind)
+        self._group_id, self._servers = self._resolve_commit_target(cfg.group_id, cfg.bootstrap_servers)
         self._sink = self._resolve_sink()
         self._pending_wms: list = []   # finished-but-uncommitted watermark lists
         self._committed: dict[int, int] = {}
         self._norm = None
         self.stats = LoaderStats()
         self._run: _Run | None = None
+
+    @property
+    def n_producers(self) -> int:
+        """Ring producers: the worker processes, or the in-process packer thread (num_workers=0)."""
+        return max(1, self.num_workers)
 
     # ------------------------------------------------------------------ configuration helpers
     def _resolve_commit_target(self, group_id, servers):
@@ -477,7 +513,7 @@ class DeviceLoader:
             # var-len / JSON slots are sized for the worst row (16 MiB) but hold a few hundred KiB:
             # 8 per worker keeps the workers off the slot-release wait (config 4: +4 %)
             budget = self.RING_AUTO_BYTES_VARLEN
-        fit = budget // max(1, self.num_workers * self._slot_capacity())
+        fit = budget // max(1, self.n_producers * self._slot_capacity())
         return int(max(4, min(8, fit)))
 
     def _slot_capacity(self) -> int:
@@ -498,7 +534,8 @@ class DeviceLoader:
         return {"batch_size": self.batch_size, "sharding": self.sharding, "rank": self.rank,
                 "world_size": self.world_size, "native": self.native, "base_seed": self.base_seed,
                 "gather": self._direct(), "json_device": self._json_device(), "span": self._span(),
-                "process_overridden": self._process_overridden(), "commit_table": None}
+                "process_overridden": self._process_overridden(), "commit_table": None,
+                "worker_spin_us": int(self.tuning.worker_spin_us), "in_process": False}
 
     def _rank_partitions(self) -> list[int]:
         """Broker partition indices this rank's workers will read (static sharding of the topics
@@ -507,12 +544,17 @@ class DeviceLoader:
         from ..parallel.sharding import shard_partitions
 
         wi = self.worker_init_fn
-        if self.sharding != "static" or not isinstance(wi, _WorkerInit) or not wi.args:
+        if self.num_workers == 0:
+            cons = getattr(self.dataset, "_consumer", None)
+            topics = sorted(cons.subscription() or []) if cons is not None and hasattr(cons, "subscription") else []
+        else:
+            topics = list(wi.args) if isinstance(wi, _WorkerInit) else []
+        if self.sharding != "static" or not topics:
             return []
         try:
             b = self._broker()
             out = []
-            for topic in wi.args:
+            for topic in topics:
                 if isinstance(topic, str) and b.has_topic(topic):
                     _, n, first = b.topic(topic)
                     out += [first + p for p in shard_partitions(n, self.rank, self.world_size)]

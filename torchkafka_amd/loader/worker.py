@@ -43,26 +43,29 @@ def worker_main(ring, ring_name: str, worker_id: int, num_workers: int, dataset,
     """Entry point of a DeviceLoader worker process."""
     if ring is None:
         ring = core().Ring.open(ring_name)
+    in_process = bool(cfg.get("in_process", False))  # num_workers=0: a thread of the main process
     ring.set_worker_pid(worker_id, os.getpid())
     # spin (µs) on a full sub-ring before sleeping: keeps futex wakes off the main thread's path
-    ring.set_worker_spin_ns(int(os.environ.get("TORCHKAFKA_WORKER_SPIN_US", "200")) * 1000)
+    ring.set_worker_spin_ns(int(cfg.get("worker_spin_us", 200)) * 1000)
     spw = ring.slots_per_worker
     state = {"i": 0, "g": None}
     try:
-        torch.set_num_threads(1)
-        seed = int(cfg.get("base_seed", 0)) + worker_id
-        random.seed(seed)
-        torch.manual_seed(seed)
-        np.random.seed(seed % (2**32))
-        _set_worker_info(worker_id, num_workers, seed, dataset)
-        if worker_init_fn is not None:
-            worker_init_fn(worker_id)
+        if not in_process:  # process-wide state belongs to the user in single-process mode
+            torch.set_num_threads(1)
+            seed = int(cfg.get("base_seed", 0)) + worker_id
+            random.seed(seed)
+            torch.manual_seed(seed)
+            np.random.seed(seed % (2**32))
+            _set_worker_info(worker_id, num_workers, seed, dataset)
+            if worker_init_fn is not None:
+                worker_init_fn(worker_id)
         consumer = getattr(dataset, "_consumer", None)
         if consumer is None:
             raise RuntimeError(
                 "DeviceLoader worker has no consumer: build the dataset with placeholder() and pass "
                 "worker_init_fn=YourDataset.init_worker(topic, ...)")
-        dataset._worker_id = worker_id
+        if not in_process:
+            dataset._worker_id = worker_id
         if cfg["sharding"] == "static":
             topics = sorted(consumer.subscription() or [])
             if not topics:
