@@ -62,6 +62,11 @@ def parse():
     ap.add_argument("--no-numa", action="store_true", help="do not bind ranks to their GPU's NUMA node")
     ap.add_argument("--decode", default="auto", choices=["auto", "device", "host"],
                     help="device: gfx950 RecordBatch decode + CRC from the pinned logs; host: workers CRC-check + pack")
+    ap.add_argument("--lockstep", default="auto", choices=["auto", "off", "rccl", "host"],
+                    help="cross-rank step/commit agreement: auto = RCCL at N > 1, none at N = 1; rccl/host force "
+                         "it (also at N = 1) over the native RCCL communicator / the process group's all-reduce")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on cuda:0 with a gloo group (rehearse N > 1 ranks on a one-GPU box)")
     ap.add_argument("--steady-steps", type=int, default=None,
                     help="steps of the steady-state block timed after the headline (default: max(50 x ring "
                          "slots, 4000); 0 skips it)")
@@ -90,7 +95,16 @@ def main() -> int:
         bind_to_gpu_numa(local_rank)
 
     dtype = {"bf16": torch.bfloat16, "fp8": torch.float8_e4m3fn, "f16": torch.float16, "f32": torch.float32}[args.dtype]
-    device = torch.device(args.device) if args.device else torch.device("cuda", local_rank)
+    device = torch.device(args.device) if args.device else torch.device("cuda", 0 if args.same_device else local_rank)
+    # lockstep: the agreement every step runs before a batch is delivered and committed
+    if args.lockstep == "off":
+        lockstep = False
+    elif args.lockstep == "auto":
+        lockstep = "host" if args.same_device else True
+    elif world == 1:
+        lockstep = "always"  # agree every step even alone: RCCL on an nccl group, all-reduce on gloo
+    else:
+        lockstep = args.lockstep
 
     class Records(KafkaDataset):
         schema = FixedWidth(torch.float32, (args.dim,))
@@ -114,16 +128,19 @@ def main() -> int:
                 records_per_batch=args.records_per_batch, threads=min(16, len(mine)))
     t_fill = time.perf_counter() - t_fill
 
-    if world > 1:
+    use_gloo = device.type != "cuda" or args.same_device or args.lockstep == "host"
+    if world > 1 or args.lockstep in ("rccl", "host"):
         # no CUDA touched yet: the loader forks its workers before HIP is initialised
-        dist.init_process_group("nccl" if device.type == "cuda" else "gloo")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+        dist.init_process_group("gloo" if use_gloo else "nccl", rank=rank, world_size=world)
 
     loader = DeviceLoader(
         Records.placeholder(), B, num_workers=args.workers, device=device, dtype=dtype,
         slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
         in_order=args.in_order, h2d=args.h2d, copy_streams=args.copy_streams, lockstep_depth=args.lockstep_depth,
         event_every=args.event_every, numa_bind=not args.no_numa, coalesce=args.coalesce,
-        coalesce_wait_us=args.coalesce_wait_us, decode=args.decode,
+        coalesce_wait_us=args.coalesce_wait_us, decode=args.decode, lockstep=lockstep,
         worker_init_fn=Records.init_worker("bench", bootstrap_servers=url, group_id="bench",
                                            auto_offset_reset="earliest", check_crcs=not args.no_crc),
     )
@@ -132,11 +149,14 @@ def main() -> int:
     if device.type == "cuda":
         torch.cuda.set_device(device)
 
+    def barrier():
+        dist.barrier(device_ids=[local_rank] if device.type == "cuda" and not use_gloo else None)
+
     def sync():
         if device.type == "cuda":
             torch.cuda.synchronize(device)
         if world > 1:
-            dist.barrier(device_ids=[local_rank] if device.type == "cuda" else None)
+            barrier()
             if device.type == "cuda":
                 torch.cuda.synchronize(device)
 
@@ -159,7 +179,7 @@ def main() -> int:
         """whole-job aggregate: records of every rank over the slowest rank's time"""
         if world == 1:
             return el, float(nrows)
-        t = torch.tensor([el, float(nrows)], dtype=torch.float64, device=device if device.type == "cuda" else "cpu")
+        t = torch.tensor([el, float(nrows)], dtype=torch.float64, device="cpu" if use_gloo else device)
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
@@ -200,6 +220,8 @@ def main() -> int:
             "vs_baseline": round(s_total / s_el / BASELINE_VALUE, 3),
             "commit_p50_us": round(s_stats["commit_p50_us"], 2),
             "commit_p99_us": round(s_stats["commit_p99_us"], 2),
+            "commit_latency_p50_us": round(s_stats["commit_latency_p50_us"], 2),
+            "commit_latency_p99_us": round(s_stats["commit_latency_p99_us"], 2),
             "worker_fill_us_per_batch": round(s_stats.get("worker_fill_us_per_batch", 0.0), 2),
         }
 
@@ -210,7 +232,7 @@ def main() -> int:
 
     it.close()  # normal end of the auto_commit generator: final commit + worker shutdown
     if world > 1:
-        dist.barrier(device_ids=[local_rank] if device.type == "cuda" else None)
+        barrier()
     committed = broker.committed_offsets("bench", "bench")
     if rank == 0:
         if args.stats:
@@ -239,13 +261,19 @@ def main() -> int:
                 "parallelism": f"dp{world}",
                 "partitions": n_parts,
                 "num_workers": args.workers,
-                "commit": "auto_commit per batch" + (", RCCL lockstep" if world > 1 else ""),
+                "commit": "auto_commit per batch" + (
+                    "" if not lockstep or (lockstep is True and world == 1)
+                    else ", lockstep (gloo all-reduce)" if use_gloo else ", RCCL lockstep"),
                 "h2d": loader._resolve_h2d(loader._slot_capacity()) if device.type == "cuda" else "n/a (cpu)",
                 "decode": "device (gfx950 CRC32C + decode from pinned logs)" if loader._span() else "host workers",
                 "bytes_per_step_per_gpu": B * args.dim * 4,
                 "gb_per_s": round(value * args.dim * 4 / 1e9, 3),
                 "commit_p99_us": round(stats["commit_p99_us"], 2),
             },
+            # request of batch k+1 -> batch k's offsets stored, incl. the lockstep agreement and the
+            # wait for batch k's on-device CRC verdict (steady-state block when it ran)
+            "commit_latency_p50_us": round((s_stats if steady_out else stats)["commit_latency_p50_us"], 2),
+            "commit_latency_p99_us": round((s_stats if steady_out else stats)["commit_latency_p99_us"], 2),
             "timed_region_s": round(elapsed, 6),
             "prefilled_slots_at_t0": occ["prefilled"],
             "ring_slots": occ["n_slots"],
@@ -254,7 +282,7 @@ def main() -> int:
         print(json.dumps(out))
     loader.close()
     if world > 1:
-        dist.barrier(device_ids=[local_rank] if device.type == "cuda" else None)
+        barrier()
         dist.destroy_process_group()
     if rank == 0:
         broker.destroy()

@@ -348,3 +348,14 @@ def test_single_process_mode_argument_errors(broker):
         DeviceLoader(_direct(Vec16, broker), 8, num_workers=0, device="cpu", worker_init_fn=init(Vec16, broker))
     with pytest.raises(ValueError, match="num_workers must be >= 0"):
         DeviceLoader(Vec16.placeholder(), 8, num_workers=-1, device="cpu")
+
+
+def test_commit_latency_is_measured_per_batch(broker):
+    """commit latency = the user's request of batch k+1 -> batch k's offsets stored."""
+    broker.create_topic("t", 2)
+    broker.fill("t", 100, "fixed_f32", size=16)
+    dl = loader(Vec16, broker, 20, workers=2)
+    n = sum(1 for _ in auto_commit(dl))
+    s = dl.stats_summary()
+    assert n == 10 and s["commit_latency_samples"] == n
+    assert 0 < s["commit_latency_p50_us"] <= s["commit_latency_p99_us"] <= s["commit_latency_max_us"]

@@ -39,6 +39,10 @@ for s in $STEPS; do
     lockjson) LOCKCHECK_SCHEMA=json LOCKCHECK_DEPTHS=0,3 step lockstep_json 150 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29634 tools/lockstep_check.py ;;
     lockcheck) step lockstep_check 150 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29631 tools/lockstep_check.py ;;
     bench)  step bench 600 python bench.py --stats ;;
+    benchlockr) step bench_lock_rccl 600 python bench.py --lockstep rccl --stats ;;
+    benchlockoff) step bench_lock_off 600 python bench.py --lockstep off --stats ;;
+    bench2r) step bench_2rank_gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29641 bench.py --gpus 2 --same-device --steps 2000 --warmup 200 --stats ;;
+    benchdriver) step bench_driver 300 python bench.py --steps 20 --warmup 5 ;;
     pytestspan) step pytest_span 300 python -u -m pytest tests/test_gpu_span.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     spannocrc) step bench_span_nocrc 300 python bench.py --steps 1000 --steady-steps 4000 --no-crc --stats ;;
     spanb1) for n in 2 3 4; do TORCHKAFKA_SPAN_BURST=1 TORCHKAFKA_DECODE_STREAMS=$n step bench_b1s$n 300 python bench.py --steps 1000 --stats; done

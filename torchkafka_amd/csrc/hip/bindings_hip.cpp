@@ -256,6 +256,7 @@ PYBIND11_MODULE(_tkhip, m) {
              s["commits"] = d.commits();
              s["commit_failures"] = d.commit_failures();
              s["commit_ns"] = d.commit_ns();
+             s["commit_latency_ns"] = d.commit_latency_ns();
              s["fill_ns"] = d.fill_ns_;
              s["fills"] = d.fills_;
              s["blocked_ns"] = d.blocked_ns_;

@@ -319,7 +319,7 @@ class MainDriver::Source : public tk::LockstepSource {
 
 void MainDriver::enable_lockstep(LockstepTransport* ls, int depth) {
   ls_ = std::make_unique<tk::CreditLockstep>(ls, depth);
-  ls_->set_on_committable([this](std::vector<tk::Watermark>&& wms) { add_finished(wms); });
+  ls_->set_on_committable([this](std::vector<tk::Watermark>&& wms) { batch_committable(wms); });
   delivered_index_ = -1;
 }
 
@@ -695,11 +695,32 @@ void MainDriver::stage_finished(int64_t index, std::vector<tk::Watermark>&& wms)
   if (ls_)
     ls_->finished(index, std::move(wms));
   else
-    add_finished(wms);
+    batch_committable(wms);
+}
+
+void MainDriver::batch_committable(const std::vector<tk::Watermark>& wms) {
+  add_finished(wms);
+  ++committable_batches_;
+}
+
+// Batches become committable in delivery order, so the first committable_batches_ finish times
+// belong to the batches whose offsets the commit that just ran stored (durable) or dropped.
+void MainDriver::settle_commit_latency(bool durable) {
+  const int64_t now = tk::now_ns();
+  for (; committable_batches_ > 0 && !finish_t_.empty(); --committable_batches_) {
+    if (durable && commit_lat_ns_.size() < (1u << 20)) commit_lat_ns_.push_back(now - finish_t_.front());
+    finish_t_.pop_front();
+  }
+  committable_batches_ = 0;
 }
 
 void MainDriver::finish_delivered(hipStream_t fence) {
   if (delivered_.empty()) return;
+  finish_t_.push_back(tk::now_ns());
+  if (finish_t_.size() > (1u << 20)) {  // manual mode that never commits: keep the queue bounded
+    finish_t_.pop_front();
+    if (committable_batches_ > 0) --committable_batches_;
+  }
   const int64_t perr = delivered_perr_;
   delivered_perr_ = -1;
   if (perr >= 0 && !commit_on_device_) {
@@ -823,6 +844,7 @@ int MainDriver::commit_pending() {
     pending_.clear();
     ++commits_;
     if (commit_ns_.size() < (1u << 20)) commit_ns_.push_back(tk::now_ns() - t0);
+    settle_commit_latency(true);
     return parse_error_.empty() ? 1 : -2;
   }
   if (!broker_) throw std::runtime_error("DeviceLoader cannot commit: no group_id / broker");
@@ -840,6 +862,7 @@ int MainDriver::commit_pending() {
   }
   pending_.clear();
   if (commit_ns_.size() < (1u << 20)) commit_ns_.push_back(tk::now_ns() - t0);
+  settle_commit_latency(status == 1);
   if (!parse_error_.empty()) return -2;  // the batches before the bad one were committed
   return status;
 }
@@ -1113,6 +1136,7 @@ std::vector<std::pair<uint32_t, int64_t>> MainDriver::committed() const {
 std::vector<std::pair<uint32_t, int64_t>> MainDriver::take_pending() {
   std::vector<std::pair<uint32_t, int64_t>> v(pending_.begin(), pending_.end());
   pending_.clear();
+  settle_commit_latency(false);  // handed to Python (manual commit): not timed here
   return v;
 }
 
@@ -1127,6 +1151,7 @@ void MainDriver::reset_stats() {
   ahead_groups_ = 0;
   fast_batches_ = fast_records_ = fast_ns_ = 0;
   commit_ns_.clear();
+  commit_lat_ns_.clear();
 }
 
 }  // namespace tkh

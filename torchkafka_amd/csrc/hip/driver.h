@@ -168,6 +168,11 @@ class MainDriver {
   uint64_t commits() const { return commits_; }
   uint64_t commit_failures() const { return commit_failures_; }
   const std::vector<int64_t>& commit_ns() const { return commit_ns_; }
+  // Commit latency per batch: from the request that finished batch k (the user asking for k+1)
+  // to k's offsets being stored -- including the wait for its decode kernel's CRC verdict, the
+  // user's GPU work (commit_on='device') and the cross-rank lockstep agreement.  With the worker
+  // commit sink it ends when the offsets are handed to the workers.
+  const std::vector<int64_t>& commit_latency_ns() const { return commit_lat_ns_; }
   void reset_stats();
 
   // Cross-rank lockstep over RCCL, pipelined `depth` steps ahead (ls is owned by the caller).
@@ -203,6 +208,8 @@ class MainDriver {
   bool pop_data(SlotView* out);
 
   void stage_finished(int64_t index, std::vector<tk::Watermark>&& wms);
+  void batch_committable(const std::vector<tk::Watermark>& wms);
+  void settle_commit_latency(bool durable);
   bool commit_on_device_ = false;
   // (event or null, batch index, watermarks, parse-error word index or -1).  A device-parsed
   // batch needs no event of its own: it becomes committable once its slot was released (its
@@ -295,6 +302,9 @@ class MainDriver {
   int64_t fast_batches_ = 0, fast_records_ = 0, fast_ns_ = 0;
  private:
   std::vector<int64_t> commit_ns_;
+  std::vector<int64_t> commit_lat_ns_;
+  std::deque<int64_t> finish_t_;       // finish time of each delivered batch not yet committed
+  int64_t committable_batches_ = 0;    // of those, batches whose offsets are in pending_
   int coalesce_ = 1;
   int64_t groups_ = 0;
   int64_t coalesce_wait_ns_ = 0;

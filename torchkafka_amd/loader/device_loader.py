@@ -154,6 +154,8 @@ class _Run:
                 mode = hip().H2D_ZERO_COPY if L._resolve_h2d(self.ring.payload_capacity) in ("zerocopy", "direct") \
                     else hip().H2D_DMA
                 self.engine = hip().Engine(dev, self.ring.n_slots, self.ring.payload_capacity, L.copy_streams, mode)
+                if L.tuning.decode_streams is not None:  # before anything creates a decode stream
+                    self.engine.set_decode_streams(int(L.tuning.decode_streams))
                 if L.numa_bind:
                     topology.check_device(dev)
                 url, group = L._commit_target_url()
@@ -174,8 +176,6 @@ class _Run:
                     self.driver.set_ahead_depth(int(tun.ahead_depth))
                 if tun.span_burst is not None:
                     self.driver.set_span_burst(int(tun.span_burst))
-                if tun.decode_streams is not None:
-                    self.engine.set_decode_streams(int(tun.decode_streams))
         except BaseException:
             self.close()
             raise
@@ -668,6 +668,7 @@ class DeviceLoader:
                 item = self._next_item(run)
                 if prev is not None and auto_commit:
                     finished.append(self._finish_marker(prev))  # the user is done with the previous batch
+                    prev = None
                 if lock is not None:
                     ok = lock.agree(item is not None, step)
                     if auto_commit:
@@ -701,11 +702,12 @@ class DeviceLoader:
 
     def _finish_marker(self, wms):
         """Marks a batch finished; in ``commit_on='device'`` mode fenced by the user's queued GPU work."""
+        t = time.perf_counter_ns()  # the user asked for the next batch: commit latency starts
         if self.commit_on == "device" and self.device.type == "cuda":
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.device))
-            return (wms, ev)
-        return (wms, None)
+            return (wms, ev, t)
+        return (wms, None, t)
 
     def _fast_path_ok(self) -> bool:
         s = self.schema
@@ -1008,6 +1010,7 @@ class DeviceLoader:
         self.stats.commits += st["commits"]
         self.stats.commit_failures += st["commit_failures"]
         self.stats.commit_ns.extend(st["commit_ns"])
+        self.stats.commit_latency_ns.extend(st.get("commit_latency_ns", ()))
         self._committed.update(dict(drv.committed()))
         drv.reset_stats()
 
@@ -1187,8 +1190,9 @@ class DeviceLoader:
             return
         offsets: dict[int, int] = {}
         keep = []
+        started = []
         for i, entry in enumerate(pending):
-            wms, ev = entry if isinstance(entry, tuple) else (entry, None)
+            wms, ev = (entry[0], entry[1]) if isinstance(entry, tuple) else (entry, None)
             if ev is not None and not wait and not ev.query():
                 # in order: a later batch is never committed before an earlier one (the committed
                 # offset must not go backwards when the earlier one completes)
@@ -1196,14 +1200,19 @@ class DeviceLoader:
                 break
             if ev is not None and wait:
                 ev.synchronize()
+            if isinstance(entry, tuple) and len(entry) > 2:
+                started.append(entry[2])
             for pidx, _first, nxt, _cnt in wms:
                 if nxt > offsets.get(pidx, -1):
                     offsets[pidx] = nxt
         self._pending_wms[:] = keep
         if offsets:
-            self._commit(offsets)
+            if self._commit(offsets):
+                now = time.perf_counter_ns()
+                for t in started:
+                    self.stats.record_commit_latency(now - t)
 
-    def _commit(self, offsets: dict[int, int]) -> None:
+    def _commit(self, offsets: dict[int, int]) -> bool:
         if self._sink == "worker":
             run = self._run
             if run is None or run.table is None or run.closed:
@@ -1216,13 +1225,14 @@ class DeviceLoader:
                 run.table.publish(w, offs)  # that worker's consumer commits (and logs) them
             self._committed.update(offsets)
             self.stats.record_commit(time.perf_counter_ns() - t0)
-            return
+            return True
         if self._group_id is None:
             raise RuntimeError("DeviceLoader cannot commit: no group_id (pass it to init_worker or DeviceLoader)")
         t0 = time.perf_counter_ns()
         b = self._broker().native
         g = b.group_index(self._group_id, True)
         _ds_logger.debug("Committing offsets.")
+        ok = False
         try:
             b.commit(g, -1, 0, 0, [(p, int(o), "") for p, o in offsets.items()])
         except COMMIT_FAILED_ERRORS:
@@ -1231,7 +1241,9 @@ class DeviceLoader:
         else:
             _ds_logger.debug("Committed offsets.")
             self._committed.update(offsets)
+            ok = True
         self.stats.record_commit(time.perf_counter_ns() - t0)
+        return ok
 
     def commit(self) -> None:
         """Commits every batch yielded so far (manual mode)."""

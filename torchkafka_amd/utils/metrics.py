@@ -30,6 +30,8 @@ class LoaderStats:
     commits: int = 0
     commit_failures: int = 0
     commit_ns: list = field(default_factory=list)
+    # request of batch k+1 -> batch k's offsets stored (incl. lockstep / decode verdict / fence waits)
+    commit_latency_ns: list = field(default_factory=list)
     worker_fill_ns: int = 0
     worker_fills: int = 0
     ready_age_ns: int = 0
@@ -65,12 +67,17 @@ class LoaderStats:
         if len(self.commit_ns) < self.max_commit_samples:
             self.commit_ns.append(ns)
 
+    def record_commit_latency(self, ns: int) -> None:
+        if len(self.commit_latency_ns) < self.max_commit_samples:
+            self.commit_latency_ns.append(ns)
+
     def reset(self) -> None:
         self.__init__()
 
     def summary(self) -> dict:
         el = time.perf_counter() - self.started
         c_us = [x / 1e3 for x in self.commit_ns]
+        lat_us = [x / 1e3 for x in self.commit_latency_ns]
         return {
             "batches": self.batches,
             "records": self.records,
@@ -100,6 +107,10 @@ class LoaderStats:
             "commit_failures": self.commit_failures,
             "commit_p50_us": percentile(c_us, 50),
             "commit_p99_us": percentile(c_us, 99),
+            "commit_latency_p50_us": percentile(lat_us, 50),
+            "commit_latency_p99_us": percentile(lat_us, 99),
+            "commit_latency_max_us": max(lat_us) if lat_us else float("nan"),
+            "commit_latency_samples": len(lat_us),
         }
 
 
