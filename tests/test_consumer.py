@@ -309,3 +309,23 @@ def test_commit_async_future(broker):
     assert fut.failed() and isinstance(errs[0], CommitFailedError)
     with pytest.raises(CommitFailedError):
         fut.get()
+
+
+def test_commit_async_callback_gets_committed_offsets(broker):
+    broker.create_topic("t", 2)
+    broker.produce("t", [b"a", b"b", b"c"], partition=0)
+    broker.produce("t", [b"d"], partition=1)
+    seen = []
+    c = consumer(broker, "t", group_id="gb", default_offset_commit_callback=lambda o, e: seen.append((o, e)))
+    assert len(list(c)) == 4
+    fut = c.commit_async()  # no callback: kafka-python's default_offset_commit_callback runs
+    want = {TopicPartition("t", 0): OffsetAndMetadata(3, ""), TopicPartition("t", 1): OffsetAndMetadata(1, "")}
+    assert seen == [(want, None)] and fut.value == want
+    got = []
+    tp = TopicPartition("t", 0)
+    c.commit_async({tp: 2}, callback=lambda o, e: got.append((o, e)))
+    assert got == [({tp: OffsetAndMetadata(2, "")}, None)]
+    assert broker.committed("gb", "t", 0) == 2
+    broker.inject_commit_failures("gb", 1)
+    fut = c.commit_async(callback=lambda o, e: got.append((o, e)))
+    assert fut.failed() and isinstance(got[-1][1], CommitFailedError) and got[-1][0] == want

@@ -31,7 +31,7 @@ from ..broker.synthetic import open_broker, resolve_url
 from ..ops.native import core
 from ..parallel.sharding import shard_partitions
 from .errors import (
-    CommitFailedError, IllegalStateError, KafkaConfigurationError, NoOffsetForPartitionError,
+    CommitFailedError, IllegalStateError, KafkaConfigurationError, KafkaError, NoOffsetForPartitionError,
     OffsetOutOfRangeError,
 )
 from .records import ConsumerRecord, OffsetAndMetadata, OffsetAndTimestamp, TopicPartition
@@ -565,14 +565,26 @@ class KafkaConsumer:
 
     def commit_async(self, offsets=None, callback=None) -> "CommitFuture":
         """kafka-python's async commit.  The shared-memory commit takes well under a microsecond, so it runs
-        inline; ``callback(offsets, exc_or_none)`` follows and the returned future is already resolved."""
+        inline; ``callback(offsets, exc_or_none)`` follows and the returned future is already resolved.
+
+        As in kafka-python, the callback receives the ``{TopicPartition: OffsetAndMetadata}`` that was
+        committed (the consumed positions when ``offsets`` is None), ``default_offset_commit_callback``
+        stands in when no callback is given, and a KafkaError lands in the future instead of raising."""
         fut = CommitFuture()
+        if offsets is None:
+            self._check_open()
+            committed = {self._tp(p): OffsetAndMetadata(o, "") for p, o in self._consumed_offsets().items()}
+        else:
+            committed = {tp: om if isinstance(om, OffsetAndMetadata) else OffsetAndMetadata(int(om), "")
+                         for tp, om in offsets.items()}
         try:
             self.commit(offsets)
-        except CommitFailedError as e:
+        except KafkaError as e:
             fut.exception = e
-        if callback is not None:
-            callback(offsets, fut.exception)
+        else:
+            fut.value = committed
+        cb = callback if callback is not None else self.config["default_offset_commit_callback"]
+        cb(committed, fut.exception)
         return fut
 
     # ------------------------------------------------------------------ lifecycle
