@@ -2,10 +2,13 @@
 """BASELINE config 4: variable-length JSON records, on-device pad/stack -> bf16 (HIP collate), batch 256.
 
 Records are JSON arrays of 16..256 numbers ("[-12.34, 5.06, ...]", ~1 KiB of text on
-average), as in the reference README's ``json.loads(record.value)`` example.  Workers
-parse them natively (C++ JSON -> CSR float32 in the pinned ring) and the gfx950
-var-len kernel pads/stacks/casts on the GPU.  The reference cannot collate this at
-all (variable-length lists fail default_collate).
+average), as in the reference README's ``json.loads(record.value)`` example.  By default
+(decode='device') the workers only walk the record headers and pre-scan each text in place,
+and the gfx950 kernel (json_span.hip) reads the texts straight from the pinned broker logs,
+verifies the RecordBatch CRCs, parses, pads, stacks and casts.  --decode host: the workers
+frame + copy the text into the ring (json_parse.hip parses it); --json-parse host: the
+workers parse every number.  The reference cannot collate this at all (variable-length lists
+fail default_collate).
 
 Usage: python benchmarks/config4_json_varlen.py [--steps K] [--device cuda:0]
 """
@@ -21,7 +24,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--steps", type=int, default=4000)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--batch-size", type=int, default=256)
     ap.add_argument("--workers", type=int, default=4)
@@ -31,6 +34,7 @@ def main():
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--json-parse", default="auto", choices=["auto", "device", "host"])
     ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy"])
+    ap.add_argument("--decode", default="auto", choices=["auto", "device", "host"])
     ap.add_argument("--slots-per-worker", type=int, default=None)
     ap.add_argument("--event-every", type=int, default=None)
     ap.add_argument("--prefetch", type=int, default=2)
@@ -54,7 +58,7 @@ def main():
         b.fill("json", per_part, "json_f32", size=args.min_len, max_size=args.max_len, threads=args.partitions)
         fill_s = time.perf_counter() - t
         dl = DeviceLoader(Json.placeholder(), B, num_workers=args.workers, device=args.device, dtype=torch.bfloat16,
-                          json_parse=args.json_parse, h2d=args.h2d, slots_per_worker=args.slots_per_worker,
+                          json_parse=args.json_parse, h2d=args.h2d, decode=args.decode, slots_per_worker=args.slots_per_worker,
                           event_every=args.event_every, prefetch=args.prefetch,
                           worker_init_fn=Json.init_worker("json", bootstrap_servers=url, group_id="cfg4",
                                                           auto_offset_reset="earliest"))
@@ -79,6 +83,8 @@ def main():
         print(json.dumps({"config": 4, "metric": "JSON records/s to GPU (bf16 padded), per-batch commit",
                           "value": round(rows / el), "ms_per_step": round(el / args.steps * 1e3, 4),
                           "batch_size": B, "json_parse": args.json_parse, "h2d": args.h2d,
+                          "decode": "device (json_span.hip from the pinned logs)" if dl._json_span() else args.decode,
+                          "timed_s": round(el, 4), "steps": args.steps,
                           "avg_record_bytes": round(text_bytes),
                           "last_batch_shape": list(x.shape),
                           "device": args.device, "fill_s": round(fill_s, 2), "loader": st}))

@@ -207,3 +207,23 @@ def test_device_decode_coalesced_batch_on_another_stream(broker):
     for row in rows[::37]:
         o, p = int(row[0]), int(row[1])
         assert torch.equal(row, torch.tensor([synth_f32(p, o, j) for j in range(64)]))
+
+
+@pytest.mark.parametrize("chunk_mib,chunks,rpb,size", [(1, 2, 16, 256), (1, 3, 4, 12000), (8, 4, 64, 256)])
+def test_device_decode_through_hbm_mirror(broker, chunk_mib, chunks, rpb, size):
+    """h2d='dma': the copy engines mirror the logs into HBM (log_mirror.h) and the kernel reads
+    there; bit-exact with the host path, every byte mirrored once, buffers recycled safely."""
+    from torchkafka_amd import FixedWidth, Tuning
+
+    n = 600 if size < 1000 else 60
+    broker.create_topic("t", 3)
+    _produce_random(broker, "t", 3, n, size * 4, rpb=rpb)
+    DS = _dataset(FixedWidth(torch.float32, (size,)))
+    a, _ = _run(broker, "t", DS, "host", 32, "gh", num_workers=2, in_order=True)
+    b, dl = _run(broker, "t", DS, "device", 32, "gm", num_workers=2, in_order=True, h2d="dma",
+                 tuning=Tuning(mirror_chunk_mib=chunk_mib, mirror_chunks=chunks))
+    assert dl._mirror()
+    assert torch.equal(_bits(a), _bits(b))
+    assert broker.committed_offsets("gm", "t") == {0: n, 1: n, 2: n}
+    st = dl.stats_summary()
+    assert st["mirror_copies"] > 0 and st["mirror_mib_copied"] > 0

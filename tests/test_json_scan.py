@@ -80,3 +80,30 @@ def test_fused_scan_copy_matches_scan(body, ws, tokens):
         cnt, same = c.json_scan_copy(s)
         assert same
         assert cnt == scan(s, False), s
+
+
+@settings(max_examples=3000, deadline=None)
+@given(st.binary(max_size=400), st.sampled_from([b"", b" ", b"\n\t  "]),
+       st.lists(st.text(alphabet="0123456789.-", min_size=1, max_size=20), max_size=60))
+def test_inplace_scan_matches_scan(body, ws, tokens):
+    # the device-parse-from-the-log worker scan (64-byte blocks, garbage past the row) == the reference scan
+    c = core()
+    for s in (ws + b"[" + body + b"]" + ws, body, ws + ("[" + ", ".join(tokens) + "]").encode() + ws):
+        for variant in (0, 1, 2, 3):
+            assert c.json_scan_inplace(s, variant)[0] == scan(s, False), (variant, s)
+
+
+def test_inplace_scan_long_rows_and_block_edges():
+    c = core()
+    rnd = random.Random(8)
+    for n in list(range(0, 200)) + [1000, 5000]:
+        nums = ["%.*f" % (rnd.randint(0, 4), rnd.uniform(-1e5, 1e5)) for _ in range(n)]
+        s = ("[" + ",".join(nums) + "]").encode()
+        for variant in (0, 1):
+            assert c.json_scan_inplace(s, variant)[0] == scan(s, False) == \
+                (len(nums) if all(len(x) <= 16 for x in nums) else -1)
+    # a 17-character run straddling a 64-byte block boundary
+    for pad in range(40, 70):
+        s = b"[" + b"1," * (pad // 2) + b"12345678901234567" + b"]"
+        for variant in (0, 1):
+            assert c.json_scan_inplace(s, variant)[0] == -1 == scan(s, False)

@@ -1,0 +1,30 @@
+#!/bin/bash
+# Ad-hoc GPU session: each step under its own time limit; the first failure ends the script.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+run() {  # run <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  tail -n 15 "gpurun_out/$name.log"
+  echo "=== $name rc=$rc"
+  [ $rc -ne 0 ] && exit $rc
+  return 0
+}
+for s in ${STEPS:-pytest_new}; do
+  case $s in
+    pytest_new) run pytest_new 400 python -u -m pytest tests/test_gpu_json_span.py tests/test_gpu_span.py tests/test_gpu_json_parse.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    pytest_all) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    config4) run config4 300 python benchmarks/config4_json_varlen.py ;;
+    config4host) run config4_hostdecode 300 python benchmarks/config4_json_varlen.py --decode host ;;
+    config4dma) run config4_dma 300 python benchmarks/config4_json_varlen.py --h2d dma ;;
+    bench) run bench 300 python bench.py --stats ;;
+    benchdma) run bench_dma 300 python bench.py --stats --h2d dma ;;
+    benchdrv) run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    profc4) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/profc4" -o run -- python3 "$OLDPWD/benchmarks/config4_json_varlen.py" --steps 300 > "$OLDPWD/gpurun_out/profc4.log" 2>&1) || exit $?
+            tail -5 gpurun_out/profc4.log ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+  esac
+done
+echo "=== done"

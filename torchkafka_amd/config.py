@@ -79,6 +79,9 @@ class Tuning:
         decode_streams: HIP streams for the device decode kernels (1..4); None = 3.
         span_burst: LDS-DMA loads a decode wave keeps in flight (0 = all, 1..8); None = 1.
         worker_spin_us: worker spin on a full sub-ring before sleeping (0..100000 us).
+        mirror_chunk_mib: h2d='dma' with device decode: log bytes per hipMemcpyAsync into the HBM
+            mirror of a partition log (1..1024 MiB).
+        mirror_chunks: HBM mirror buffers per partition (2..64).
     """
 
     slots_per_worker: Optional[int] = None
@@ -94,6 +97,8 @@ class Tuning:
     decode_streams: Optional[int] = None
     span_burst: Optional[int] = None
     worker_spin_us: Optional[int] = None
+    mirror_chunk_mib: int = 8
+    mirror_chunks: int = 4
 
     def __post_init__(self):
         # environment defaults for fields left at None
@@ -120,6 +125,8 @@ class Tuning:
         _check(self.decode_streams is None or 1 <= int(self.decode_streams) <= 4, "decode_streams must be in [1, 4]")
         _check(self.span_burst is None or 0 <= int(self.span_burst) <= 8, "span_burst must be in [0, 8]")
         _check(0 <= int(self.worker_spin_us) <= 100_000, "worker_spin_us must be in [0, 100000]")
+        _check(1 <= int(self.mirror_chunk_mib) <= 1024, "mirror_chunk_mib must be in [1, 1024]")
+        _check(2 <= int(self.mirror_chunks) <= 64, "mirror_chunks must be in [2, 64]")
 
 
 _CHOICES = {

@@ -230,6 +230,19 @@ PYBIND11_MODULE(_tkcore, m) {
         return json_scan_simple(s.data(), s.size(), simd);
       },
       py::arg("data"), py::arg("simd") = true);
+  m.def(
+      "json_scan_inplace",
+      [](py::bytes b, int variant, int iters) {
+        std::string s = b;
+        std::vector<char> src((s.size() + 63) / 64 * 64 + 128, 'x');  // bytes past the row are garbage on purpose
+        std::memcpy(src.data(), s.data(), s.size());
+        int64_t r = json_scan_inplace(src.data(), s.size(), src.size(), variant);
+        if (iters <= 1) return py::make_tuple(r, 0.0);
+        const int64_t t0 = now_ns();
+        for (int i = 0; i < iters; ++i) r += json_scan_inplace(src.data(), s.size(), src.size(), variant) - r;
+        return py::make_tuple(r, double(now_ns() - t0) / iters);  // (verdict, ns per scan)
+      },
+      py::arg("data"), py::arg("variant") = 0, py::arg("iters") = 1);
   m.def("json_scan_copy", [](py::bytes b) {
     std::string s = b;
     const size_t nr = (s.size() + 31) / 32 * 32 + 64;
@@ -573,14 +586,15 @@ PYBIND11_MODULE(_tkcore, m) {
              d["error"] = std::string(h->err, h->err_len);
              d["log_end"] = std::vector<uint64_t>(h->log_end, h->log_end + h->n_parts);
              d["n_segs"] = h->n_segs;
+             d["trunc_len"] = h->trunc_len;
              return d;
            })
       .def("span_segments",
            [](PyRing& r, uint32_t g) {
-             // kPackRecordSpan slots: [(log_pos, len, pidx, flags, crc, row_begin, row_end)]
+             // kPackRecordSpan / kPackJsonSpan slots: [(log_pos, len, pidx, flags, crc, row_begin, row_end)]
              SlotHeader* h = r.r->slot(g);
              py::list l;
-             if (h->kind != uint32_t(kPackRecordSpan)) return l;
+             if (h->kind != uint32_t(kPackRecordSpan) && h->kind != uint32_t(kPackJsonSpan)) return l;
              const auto* sg = reinterpret_cast<const SpanSeg*>(r.r->payload(g) + h->values_offset);
              for (uint32_t i = 0; i < h->n_segs; ++i)
                l.append(py::make_tuple(sg[i].log_pos, sg[i].len, sg[i].pidx, sg[i].flags, sg[i].crc, sg[i].row_begin,
@@ -720,5 +734,9 @@ PYBIND11_MODULE(_tkcore, m) {
   m.attr("PACK_RECORD_SPAN") = int(kPackRecordSpan);
   m.attr("SPAN_SEG_MAX") = kSpanSegMax;
   m.attr("SPAN_MAX_SEG_ROWS") = kSpanMaxSegRows;
+  m.attr("PACK_JSON_SPAN") = int(kPackJsonSpan);
+  m.attr("JSON_SPAN_MAX_SEG_ROWS") = kJsonSpanMaxSegRows;
+  m.attr("JSON_SPAN_ROW_MAX") = kJsonSpanRowMax;
+  m.attr("SEG_HOST_ROWS") = int(kSegHostRows);
   m.attr("SLOT_HEADER_BYTES") = kSlotHeaderBytes;
 }

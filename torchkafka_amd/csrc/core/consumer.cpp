@@ -394,6 +394,126 @@ __attribute__((target("avx2,bmi,popcnt"))) int64_t json_scan_copy_avx2(const uin
 }
 #endif
 
+// In-place pre-scan for the device parse from the log (kPackJsonSpan): json_scan_simple's verdict
+// without a per-row scalar tail -- whole 64-byte blocks, bytes outside the array interior masked
+// out of the verdicts (AVX-512BW: one compare per character class per 64 bytes).  Needs the text
+// readable up to align_up(n, 64) bytes from s.
+#if defined(__x86_64__)
+__attribute__((target("avx512f,avx512bw,bmi,popcnt"))) int64_t json_scan_inplace_avx512(const uint8_t* src,
+                                                                                         size_t n) {
+  size_t a = 0, b = n;
+  while (a < b && scan_ws(src[a])) ++a;
+  while (b > a && scan_ws(src[b - 1])) --b;
+  if (b - a < 2 || src[a] != '[' || src[b - 1] != ']') return -1;
+  const size_t lo = a + 1, hi = b - 1;  // interior [lo, hi)
+  const __m512i c0 = _mm512_set1_epi8('0'), c9 = _mm512_set1_epi8(9), dot = _mm512_set1_epi8('.'),
+                mi = _mm512_set1_epi8('-'), co = _mm512_set1_epi8(','), sp = _mm512_set1_epi8(' '),
+                tb = _mm512_set1_epi8('\t'), nl = _mm512_set1_epi8('\n'), cr = _mm512_set1_epi8('\r');
+  uint64_t bad = 0, anyt = 0, prev = 0;
+  int64_t commas = 0;
+  for (size_t i = lo & ~size_t(63); i < hi; i += 64) {
+    const __m512i v = _mm512_loadu_si512(reinterpret_cast<const void*>(src + i));
+    uint64_t in = ~uint64_t(0);
+    if (i < lo) in <<= (lo - i);
+    if (i + 64 > hi) in &= ~uint64_t(0) >> (64 - (hi - i));
+    const uint64_t tok = (_mm512_cmple_epu8_mask(_mm512_sub_epi8(v, c0), c9) | _mm512_cmpeq_epi8_mask(v, dot) |
+                          _mm512_cmpeq_epi8_mask(v, mi)) & in;
+    const uint64_t com = _mm512_cmpeq_epi8_mask(v, co) & in;
+    const uint64_t ws = _mm512_cmpeq_epi8_mask(v, sp) | _mm512_cmpeq_epi8_mask(v, tb) |
+                        _mm512_cmpeq_epi8_mask(v, nl) | _mm512_cmpeq_epi8_mask(v, cr);
+    bad |= in & ~(tok | com | ws);
+    commas += __builtin_popcountll(com);
+    anyt |= tok;
+    // runs of > 16 number characters ending in this block: this block plus the previous one's top 16 bits
+    const unsigned __int128 y = (static_cast<unsigned __int128>(tok) << 16) | (prev >> 48);
+    unsigned __int128 r = y & (y >> 1);
+    r &= r >> 2;
+    r &= r >> 4;
+    r &= r >> 8;
+    r &= y >> 16;
+    bad |= uint64_t(r) | uint64_t(r >> 64);
+    prev = tok;
+  }
+  if (bad) return -1;
+  if (!anyt) return commas == 0 ? 0 : -1;
+  return commas + 1;
+}
+const bool g_scan_avx512 = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+                           __builtin_cpu_supports("bmi") && __builtin_cpu_supports("popcnt");
+
+// The same scan with one byte-class lookup per 64 bytes (AVX-512 VBMI vpermt2b over a 128-entry
+// table: bit 0 number character [0-9.-], bit 1 ',', bit 2 JSON whitespace) instead of nine
+// compares, and the long-run check in plain 64-bit words: runs of >= 17 inside the block by
+// shift-and, runs across the block boundary from the previous block's top run + this one's bottom
+// run.  ~3x the compare version on the worker's hot path.
+constexpr uint8_t scan_class(int c) {
+  return uint8_t(((c >= '0' && c <= '9') || c == '.' || c == '-') ? 1
+                 : c == ','                                        ? 2
+                 : (c == ' ' || c == '\t' || c == '\n' || c == '\r') ? 4
+                                                                   : 0);
+}
+struct ScanTable {
+  alignas(64) uint8_t t[128];
+  constexpr ScanTable() : t{} {
+    for (int i = 0; i < 128; ++i) t[i] = scan_class(i);
+  }
+};
+constexpr ScanTable kScanTable{};
+
+__attribute__((target("avx512f,avx512bw,avx512vbmi,bmi,lzcnt,popcnt"))) int64_t json_scan_inplace_vbmi(
+    const uint8_t* src, size_t n) {
+  size_t a = 0, b = n;
+  while (a < b && scan_ws(src[a])) ++a;
+  while (b > a && scan_ws(src[b - 1])) --b;
+  if (b - a < 2 || src[a] != '[' || src[b - 1] != ']') return -1;
+  const size_t lo = a + 1, hi = b - 1;  // interior [lo, hi)
+  const __m512i tlo = _mm512_load_si512(reinterpret_cast<const void*>(kScanTable.t));
+  const __m512i thi = _mm512_load_si512(reinterpret_cast<const void*>(kScanTable.t + 64));
+  const __m512i b_tok = _mm512_set1_epi8(1), b_com = _mm512_set1_epi8(2), b_any = _mm512_set1_epi8(7);
+  uint64_t bad = 0, anyt = 0;
+  int64_t commas = 0;
+  int prev_run = 0;  // number characters ending at the previous block's top
+  for (size_t i = lo & ~size_t(63); i < hi; i += 64) {
+    const __m512i v = _mm512_loadu_si512(reinterpret_cast<const void*>(src + i));
+    uint64_t in = ~uint64_t(0);
+    if (i < lo) in <<= (lo - i);
+    if (i + 64 > hi) in &= ~uint64_t(0) >> (64 - (hi - i));
+    const __m512i cls = _mm512_permutex2var_epi8(tlo, v, thi);  // index: the low 7 bits
+    const uint64_t tok = _mm512_test_epi8_mask(cls, b_tok) & in;
+    const uint64_t com = _mm512_test_epi8_mask(cls, b_com) & in;
+    const uint64_t ok = _mm512_test_epi8_mask(cls, b_any) & ~_mm512_movepi8_mask(v);  // ASCII, in the alphabet
+    bad |= in & ~ok;
+    commas += __builtin_popcountll(com);
+    anyt |= tok;
+    uint64_t r = tok & (tok >> 1);
+    r &= r >> 2;
+    r &= r >> 4;
+    r &= r >> 8;
+    r &= tok >> 16;  // bit j: 17 number characters at j .. j + 16
+    bad |= r;
+    const int lead = tok == ~uint64_t(0) ? 64 : int(__builtin_ctzll(~tok));
+    bad |= uint64_t(prev_run + lead > kMaxSimpleToken);
+    prev_run = tok == ~uint64_t(0) ? prev_run + 64 : int(__builtin_clzll(~tok));
+  }
+  if (bad) return -1;
+  if (!anyt) return commas == 0 ? 0 : -1;
+  return commas + 1;
+}
+const bool g_scan_vbmi = g_scan_avx512 && __builtin_cpu_supports("avx512vbmi") && __builtin_cpu_supports("lzcnt");
+#endif
+
+int64_t json_scan_inplace(const char* s, size_t n, size_t readable, int variant) {
+#if defined(__x86_64__)
+  if (readable >= ((n + 63) & ~size_t(63)) + 64) {
+    if (g_scan_vbmi && variant <= 0) return json_scan_inplace_vbmi(reinterpret_cast<const uint8_t*>(s), n);
+    if (g_scan_avx512 && variant <= 1) return json_scan_inplace_avx512(reinterpret_cast<const uint8_t*>(s), n);
+  }
+#endif
+  (void)readable;
+  (void)variant;
+  return json_scan_impl(s, n, variant <= 2);
+}
+
 int64_t json_scan_copy(const char* s, size_t n, uint8_t* dst) {
 #if defined(__x86_64__)
   if (g_scan_avx2 && g_avx2 && (reinterpret_cast<uintptr_t>(dst) & 31) == 0)
@@ -470,6 +590,77 @@ uint32_t build_span_segments(const SpanRB* rbs, size_t n_rbs, const uint64_t* ro
   return n;
 }
 
+// kPackJsonSpan: the same log ranges, but cut only between row texts (a row's text lies whole in
+// one segment, so one wave parses it from LDS), at most kJsonSpanMaxSegRows rows per segment;
+// then kSegHostRows pseudo-segments over the rows the worker parsed itself.
+uint32_t build_json_segments(const SpanRB* rbs, size_t n_rbs, const JsonSpanRow* rows, int64_t n_rows, SpanSeg* out,
+                             uint64_t cap) {
+  uint32_t n = 0;
+  auto emit = [&](uint64_t pos, uint32_t len, uint32_t pidx, uint32_t flags, uint32_t crc, int64_t r0, int64_t r1) {
+    if (n >= cap) throw std::runtime_error("ring slot too small for the batch's device-parse segments");
+    SpanSeg& sg = out[n++];
+    sg.log_pos = pos;
+    sg.len = len;
+    sg.pidx = pidx;
+    sg.flags = flags;
+    sg.crc = crc;
+    sg.row_begin = uint32_t(r0);
+    sg.row_end = uint32_t(r1);
+  };
+  for (size_t i = 0; i < n_rbs; ++i) {
+    const SpanRB& rb = rbs[i];
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (int64_t r = rb.row_first; r < rb.row_last; ++r) {
+      if (rows[r].tlen < 0) continue;
+      lo = std::min<uint64_t>(lo, rows[r].pos);
+      hi = std::max<uint64_t>(hi, rows[r].pos + uint64_t(rows[r].tlen));
+    }
+    if (rb.verify) {
+      lo = rb.pos;  // the whole batch: its CRC covers [pos + 21, pos + size)
+      hi = rb.pos + rb.size;
+    } else if (lo >= hi) {
+      continue;  // nothing for the device: skipped records or worker-parsed rows only
+    }
+    int64_t r = rb.row_first;
+    uint64_t cur = lo;
+    bool first = true;
+    while (cur < hi) {
+      while (r < rb.row_last && (rows[r].tlen < 0 || rows[r].pos < cur)) ++r;  // rows of earlier segments
+      uint64_t cut = std::min<uint64_t>(cur + kSpanSegMax, hi);
+      int64_t re = r;
+      for (; re < rb.row_last && re - r < int64_t(kJsonSpanMaxSegRows); ++re) {
+        if (rows[re].tlen < 0) continue;
+        if (rows[re].pos >= cut) break;
+        if (rows[re].pos + uint64_t(rows[re].tlen) > cut) {  // the text would straddle the cut: cut before it
+          cut = rows[re].pos;
+          break;
+        }
+      }
+      if (re - r == int64_t(kJsonSpanMaxSegRows)) {
+        // row limit: end the segment at the next device row's text
+        int64_t q = re;
+        while (q < rb.row_last && rows[q].tlen < 0) ++q;
+        if (q < rb.row_last && rows[q].pos < cut) cut = rows[q].pos;
+      }
+      if (cut <= cur) throw std::logic_error("json span: empty segment");
+      emit(cur, uint32_t(cut - cur), rb.pidx,
+           rb.verify ? (kSegCrc | (first ? kSegCrcFirst : 0u) | (cut == hi ? kSegCrcLast : 0u)) : 0u, rb.crc, r, re);
+      first = false;
+      cur = cut;
+    }
+  }
+  int64_t h0 = -1;
+  for (int64_t r = 0; r <= n_rows; ++r) {
+    const bool host = r < n_rows && rows[r].tlen < 0;
+    if (h0 >= 0 && (!host || r - h0 == int64_t(kJsonSpanMaxSegRows))) {
+      emit(0, 0, UINT32_MAX, kSegHostRows, 0, h0, r);
+      h0 = -1;
+    }
+    if (host && h0 < 0) h0 = r;
+  }
+  return n;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------ fill
@@ -482,11 +673,13 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   FillOutcome out;
   const bool gather = spec.kind == kPackFixed && spec.gather;
   const bool span = spec.kind == kPackFixed && spec.span && !gather;
+  const bool jspan = spec.kind == kPackJsonText && spec.span;  // JSON text parsed on the device from the logs
   h->n_rows = 0;
   h->n_parts = 0;
   h->n_segs = 0;
   h->flags = 0;
-  h->kind = uint32_t(gather ? kPackGatherFixed : span ? kPackRecordSpan : spec.kind);
+  h->kind = uint32_t(gather ? kPackGatherFixed : span ? kPackRecordSpan : jspan ? kPackJsonSpan : spec.kind);
+  h->trunc_len = -1;
   h->err_len = 0;
   h->max_row_len = 0;
   h->total_elems = 0;
@@ -499,6 +692,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   const bool fixed = spec.kind == kPackFixed;
   const bool json_text = spec.kind == kPackJsonText;
   JsonRowDesc* jrows = nullptr;
+  JsonSpanRow* srows = nullptr;
   const uint64_t row_bytes = fixed ? uint64_t(spec.row_elems) * uint64_t(spec.elem_size) : 0;
   uint64_t values_off = 0;
   int32_t* offs = nullptr;
@@ -513,6 +707,14 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
     for (const auto& fp : parts) log_of.push_back(f.broker().log_base(fp.pidx));
   } else if (fixed) {
     if (uint64_t(B) * row_bytes > cap) throw std::invalid_argument("ring slot too small for the batch");
+  } else if (jspan) {
+    for (const auto& fp : parts) {
+      log_of.push_back(f.broker().log_base(fp.pidx));
+      log_cap.push_back(f.broker().part(fp.pidx).log_capacity);
+    }
+    values_off = align_up(uint64_t(B) * sizeof(JsonSpanRow), 256);  // worker-parsed rows' f32 values follow
+    if (values_off >= cap) throw std::invalid_argument("ring slot too small for the batch's row table");
+    srows = reinterpret_cast<JsonSpanRow*>(pay);
   } else if (json_text) {
     for (const auto& fp : parts) {
       log_of.push_back(f.broker().log_base(fp.pidx));
@@ -561,7 +763,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   thread_local std::vector<SpanRB> rbs;
   rbs.clear();
   auto on_batch = [&](const IndexEntry& e, const BatchHeader& bh, bool unverified) -> bool {
-    if (!span) return true;
+    if (!span && !jspan) return true;
     const uint32_t pidx = parts[cur_part].pidx;
     if (rbs.empty() || rbs.back().pidx != pidx || rbs.back().pos != e.pos)
       rbs.push_back(SpanRB{pidx, e.size, e.pos, bh.crc, unverified, rows, rows});
@@ -594,6 +796,50 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
     }
     int64_t len;
     uint64_t nbytes;
+    if (jspan) {
+      // device parse from the log: count + simple check of the text where it lies (no copy, no
+      // CRC pass); rows that are not simple are parsed here, their float32 values ride in the slot
+      const char* txt = reinterpret_cast<const char*>(r.value);
+      const size_t tn = size_t(r.value_len);
+      JsonSpanRow d;
+      const uint64_t at_log = uint64_t(r.value - log_of[cur_part]);
+      int64_t cnt = tn <= kJsonSpanRowMax ? json_scan_inplace(txt, tn, size_t(log_cap[cur_part] - at_log)) : -1;
+      uint64_t at = vused;
+      if (cnt >= 0) {
+        d.pos = at_log;
+        d.tlen = int32_t(tn);
+        nbytes = 0;
+      } else {
+        at = align_up(vused, 16);
+        const int64_t room = at < vcap ? int64_t((vcap - at) / 4) : 0;
+        cnt = parse_json_f32(txt, tn, reinterpret_cast<float*>(vals + at), room);
+        if (cnt == -2) {
+          if (rows == 0) throw std::runtime_error("a single record exceeds the ring slot capacity");
+          slot_full = true;
+          return kStopBefore;
+        }
+        if (cnt < 0) return bad(r, "value is not a flat numeric JSON array");
+        d.pos = values_off + at;
+        d.tlen = -1;
+        nbytes = 0;
+      }
+      if (cnt < spec.min_len) { touch(r); return kTake; }
+      len = cnt;
+      if (spec.max_len >= 0 && len > spec.max_len) {
+        if (!spec.truncate) { touch(r); return kTake; }
+        len = spec.max_len;
+      }
+      if (d.tlen < 0) nbytes = uint64_t(len) * 4;
+      if (cnt > INT32_MAX) throw std::runtime_error("JSON row too large for the device parser");
+      d.count = int32_t(cnt);
+      srows[rows] = d;
+      if (d.tlen < 0) vused = at + nbytes;
+      elems += len;
+      max_len = std::max(max_len, len);
+      touch(r);
+      rbs.back().row_last = ++rows;
+      return rows == B ? kTakeStop : kTake;
+    }
     if (json_text) {
       // device parse: frame the row (count + simple check), copy its text; rows that are not
       // simple are parsed here and travel as float32 (JsonRowDesc::tlen == -1)
@@ -741,6 +987,23 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
     h->payload_bytes = values_off + h->values_bytes;
     h->max_row_len = spec.row_elems;
     h->total_elems = rows * spec.row_elems;
+    h->n_scanned = scanned;
+    out.rows = rows;
+    out.scanned = scanned;
+    return out;
+  }
+  if (jspan) {
+    const uint64_t seg_off = align_up(values_off + vused, 256);
+    const uint32_t n = build_json_segments(rbs.data(), rbs.size(), srows, rows,
+                                           reinterpret_cast<SpanSeg*>(pay + seg_off),
+                                           cap > seg_off ? (cap - seg_off) / sizeof(SpanSeg) : 0);
+    h->n_segs = n;
+    h->values_offset = seg_off;
+    h->values_bytes = uint64_t(n) * sizeof(SpanSeg);
+    h->payload_bytes = seg_off + h->values_bytes;
+    h->max_row_len = max_len;
+    h->total_elems = elems;
+    h->trunc_len = spec.max_len >= 0 && spec.max_len < INT32_MAX ? int32_t(spec.max_len) : -1;
     h->n_scanned = scanned;
     out.rows = rows;
     out.scanned = scanned;

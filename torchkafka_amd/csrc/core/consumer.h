@@ -77,6 +77,7 @@ enum PackKind : int {
   kPackGatherFixed = 3,
   kPackJsonText = 4,
   kPackRecordSpan = 5,  // fixed-width rows decoded on the device from the pinned logs (span.h)
+  kPackJsonSpan = 6,    // JsonArray rows parsed on the device straight from the pinned logs (span.h)
 };
 
 // kPackJsonText: JsonArray rows for the device parser (json_parse.hip).  The payload starts
@@ -99,7 +100,8 @@ struct PackSpec {
   int truncate = 1;
   int skip_bad = 0;         // malformed rows: 1 = skip, 0 = raise
   int gather = 0;           // fixed-width: emit log locations (kPackGatherFixed) instead of values
-  int span = 0;             // fixed-width: emit log ranges + row positions (kPackRecordSpan), CRC on device
+  int span = 0;             // fixed-width / JSON text: emit log ranges + row positions (kPackRecordSpan /
+                            // kPackJsonSpan) instead of values; CRC and decode on the device
 };
 
 struct FillOutcome {
@@ -123,6 +125,9 @@ int64_t parse_json_f32(const char* s, size_t n, float* out, int64_t cap);
 // only, tokens <= 16 characters), or -1 if the row must be parsed on the host.
 // simd=false forces the scalar reference implementation (tests compare the two).
 int64_t json_scan_simple(const char* s, size_t n, bool simd = true);
+// The same verdict, scanning whole 64-byte blocks in place (`readable`: bytes readable from s).
+// variant (tests/benchmarks): 0 best available, 1 AVX-512BW compares, 2 AVX2 rows, 3 scalar.
+int64_t json_scan_inplace(const char* s, size_t n, size_t readable, int variant = 0);
 // The same verdict, fused with a streaming copy of the text to `dst` (32-byte aligned; src
 // readable and dst writable up to align_up(n, 32)).
 int64_t json_scan_copy(const char* s, size_t n, uint8_t* dst);

@@ -57,8 +57,8 @@ struct alignas(64) SlotHeader {
   uint32_t row_bytes;      // fixed-width: bytes per row
   int32_t src_dtype;       // element dtype code of the payload (-1: decided by the loader's schema)
   int32_t ndim;            // sample rank for fixed-width payloads written by the generic path
-  uint32_t n_segs;         // kPackRecordSpan: SpanSeg entries at values_offset
-  uint32_t pad_;
+  uint32_t n_segs;         // kPackRecordSpan / kPackJsonSpan: SpanSeg entries at values_offset
+  int32_t trunc_len;       // kPackJsonSpan: rows longer than this are truncated to it (-1: no limit)
   int64_t shape[8];
   char err[2048];
   Watermark wm[kMaxSlotParts];

@@ -57,7 +57,31 @@ enum SpanSegFlags : uint32_t {
   kSegCrcFirst = 1,   // the segment holds the first CRC'd byte of its RecordBatch (offset 21)
   kSegCrcLast = 2,    // ... and/or the last byte of its RecordBatch
   kSegCrc = 4,        // the segment is part of a RecordBatch whose CRC is verified
+  kSegHostRows = 8,   // kPackJsonSpan: no log bytes; rows [row_begin, row_end) parsed by the worker
 };
+
+// ---- kPackJsonSpan: JsonArray rows parsed on the device from the pinned logs.
+// The reference decodes each record with json.loads in `_process` (README.md:54,74).  Here the
+// worker walks the record headers and pre-scans each value's text once (element count and the
+// "simple row" check of json_scan_simple, no copy, no CRC); the slot then holds
+//   * JsonSpanRow[n_rows] at payload offset 0;
+//   * the float32 values of the rare rows that are not simple (exponents, NaN, long tokens),
+//     parsed by the worker, right after the row table;
+//   * SpanSeg[n_segs] at values_offset: log ranges as for kPackRecordSpan, cut only between row
+//     texts (a row's text always lies whole in one segment), plus kSegHostRows pseudo-segments
+//     for the worker-parsed rows.
+// The gfx950 kernel (csrc/hip/json_span.hip) stages each segment in LDS, verifies the
+// RecordBatch CRC32C like span_decode.hip, and parses every row with one wave.
+struct JsonSpanRow {
+  uint64_t pos;    // tlen >= 0: log byte position of the row's text; tlen < 0: payload offset of its f32 values
+  int32_t tlen;    // bytes of text (parsed on the device), or -1 (parsed by the worker)
+  int32_t count;   // elements of the row (the device checks its own token count against it)
+};
+static_assert(sizeof(JsonSpanRow) == 16, "JsonSpanRow layout");
+// Rows whose values one JSON segment may hold (their tables are staged in LDS next to the text),
+// and the longest text parsed on the device (a longer row is parsed by the worker).
+constexpr uint32_t kJsonSpanMaxSegRows = 1024;
+constexpr uint32_t kJsonSpanRowMax = 64u << 10;
 
 struct SpanSeg {
   uint64_t log_pos;    // byte position of the range in partition `pidx`'s log
@@ -69,5 +93,9 @@ struct SpanSeg {
   uint32_t row_end;
 };
 static_assert(sizeof(SpanSeg) == 32, "SpanSeg layout");
+
+// Parse-error words of the device JSON parse carry this bit over the slot row index (a CRC
+// failure stores the segment index, below it).
+constexpr int32_t kSpanParseErrBit = 1 << 30;
 
 }  // namespace tk

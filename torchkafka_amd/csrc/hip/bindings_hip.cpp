@@ -283,6 +283,12 @@ PYBIND11_MODULE(_tkhip, m) {
              s["polled"] = d.polled_;
              s["poll_ns"] = d.poll_ns_;
              s["log_bytes_registered"] = d.log_bytes_registered();
+             if (const LogMirror* m = d.mirror()) {
+               s["mirror_bytes_copied"] = m->bytes_copied();
+               s["mirror_copies"] = m->copies();
+               s["mirror_fallbacks"] = m->fallbacks();
+               s["mirror_device_bytes"] = m->device_bytes();
+             }
              s["log_register_ns"] = d.log_register_ns();
              return s;
            })
@@ -292,6 +298,7 @@ PYBIND11_MODULE(_tkhip, m) {
       .def("set_coalesce", &MainDriver::set_coalesce, py::arg("n"))
       .def("set_coalesce_wait_us", &MainDriver::set_coalesce_wait_us, py::arg("us"))
       .def("enable_direct", &MainDriver::enable_direct)
+      .def("enable_mirror", &MainDriver::enable_mirror, py::arg("chunk_bytes"), py::arg("chunks_per_partition"))
       .def("set_ahead_depth", &MainDriver::set_ahead_depth)
       .def("set_span_burst", &MainDriver::set_span_burst)
       .def("set_worker_sink", &MainDriver::set_worker_sink, py::arg("table"), py::arg("n_workers"),

@@ -53,6 +53,11 @@ struct JsonGroupArgs {
   int64_t* lengths[kMaxGroup];
   uint8_t* mask[kMaxGroup];
   int32_t* err[kMaxGroup];
+  // kPackJsonSpan: bytes of each batch's staging area (a descriptor reaching beyond it is a bad
+  // row, never read), and the tag OR-ed into a parse error's row index (tk::kSpanParseErrBit); a
+  // parse error then never overwrites an earlier verdict (the stage kernel's CRC failure).
+  uint64_t vals_cap[kMaxGroup];
+  int32_t err_tag;
 };
 void launch_json_group(JsonGroupArgs& a, int dst_dt, hipStream_t stream);
 

@@ -49,10 +49,15 @@ MainDriver::MainDriver(Engine* engine, const std::string& ring_name, const std::
 }
 
 MainDriver::~MainDriver() {
+  mirror_.reset();  // its copies read the pinned logs: before they are unregistered
   // pinned log ranges first: the kernels that read them completed (slots drained by the caller)
   if (!reg_ptrs_.empty()) hipDeviceSynchronize();
   for (void* p : reg_ptrs_) hipHostUnregister(p);
   if (bases_dev_) hipFree(bases_dev_);
+  if (stage_dev_) {
+    hipDeviceSynchronize();
+    hipFree(stage_dev_);
+  }
   if (registered_) {
     try {
       eng_->unregister_host();  // before ring_'s mapping goes away
@@ -97,6 +102,7 @@ void MainDriver::release_completed_impl() {
         if (handed_[k].span) check_span(handed_[k].g, pe);  // reads the slot: before its release
         perr_state_[size_t(pe)] = __atomic_load_n(perr_host_ + pe, __ATOMIC_ACQUIRE) < 0 ? 1 : 2;
       }
+      if (handed_[k].stage_end) stage_tail_ = handed_[k].stage_end;  // its group's kernels completed
       ring_->main_release(uint32_t(handed_[k].g));
     }
   }
@@ -224,7 +230,7 @@ int MainDriver::poll_one_impl(bool block, int64_t timeout_ms) {
       if (!block) return 0;
       continue;
     }
-    if (v.kind == uint32_t(tk::kPackRecordSpan)) {
+    if (v.kind == uint32_t(tk::kPackRecordSpan) || v.kind == uint32_t(tk::kPackJsonSpan)) {
       if (!broker_) {
         error_ = "DeviceLoader: device decode needs the synthetic broker (group_id + bootstrap_servers)";
         return -3;
@@ -232,8 +238,10 @@ int MainDriver::poll_one_impl(bool block, int64_t timeout_ms) {
       // pin every log range the segments cover (plus the 16-byte tail the kernel's aligned loads
       // may touch) before any kernel may read them
       v.n_segs = h->n_segs;
+      v.trunc_len = h->trunc_len;
       const auto* sg = reinterpret_cast<const tk::SpanSeg*>(ring_->payload(uint32_t(g)) + h->values_offset);
       for (uint32_t i = 0; i < h->n_segs; ++i) {
+        if (sg[i].flags & tk::kSegHostRows) continue;  // worker-parsed rows: no log bytes
         const uint64_t cap = broker_->part(sg[i].pidx).log_capacity;
         ensure_log(sg[i].pidx, std::min<uint64_t>(sg[i].log_pos + sg[i].len + 16, cap));
       }
@@ -503,7 +511,7 @@ void MainDriver::deliver(const SlotView& v) { set_delivered(v); }
 
 void MainDriver::set_delivered(const SlotView& v) {
   delivered_ = v.wms;
-  const bool checked = v.kind == tk::kPackJsonText || v.kind == tk::kPackRecordSpan;
+  const bool checked = v.kind == tk::kPackJsonText || v.kind == tk::kPackRecordSpan || v.kind == tk::kPackJsonSpan;
   delivered_perr_ = checked ? (v.perr >= 0 ? v.perr : last_perr_) : -1;
 }
 
@@ -532,20 +540,23 @@ int64_t MainDriver::next_err_word() {
   return idx;
 }
 
+void MainDriver::ensure_partials() {
+  if (part_host_) return;
+  void* h = nullptr;
+  if (hipHostMalloc(&h, size_t(kErrWords * kPartials) * sizeof(uint32_t), hipHostMallocMapped) != hipSuccess)
+    throw std::runtime_error("driver: hipHostMalloc of the partial CRC words failed");
+  part_host_ = static_cast<uint32_t*>(h);
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) throw std::runtime_error("driver: hipHostGetDevicePointer failed");
+  part_dev_ = static_cast<uint32_t*>(d);
+  perr_msg_.assign(size_t(kErrWords), std::string());
+}
+
 void MainDriver::launch_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
                              void* const* dsts, const float* shift, const float* scale, bool record_last,
                              int64_t* perrs) {
   if (!broker_) throw std::runtime_error("driver: device decode needs the synthetic broker");
-  if (!part_host_) {
-    void* h = nullptr;
-    if (hipHostMalloc(&h, size_t(kErrWords * kPartials) * sizeof(uint32_t), hipHostMallocMapped) != hipSuccess)
-      throw std::runtime_error("driver: hipHostMalloc of the partial CRC words failed");
-    part_host_ = static_cast<uint32_t*>(h);
-    void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) throw std::runtime_error("driver: hipHostGetDevicePointer failed");
-    part_dev_ = static_cast<uint32_t*>(d);
-    perr_msg_.assign(size_t(kErrWords), std::string());
-  }
+  ensure_partials();
   const SlotView& v0 = *views[0];
   SpanLaunch a{};
   a.row_elems = v0.max_row_len;
@@ -570,12 +581,14 @@ void MainDriver::launch_span(const int* slots, const SlotView* const* views, int
       if ((sg[i].flags & tk::kSegCrc) && (sg[i].flags & kWhole) != kWhole && i >= uint32_t(kPartials))
         throw std::runtime_error("driver: a batch splits RecordBatches into more than 512 device segments");
       if (a.n_seg == kMaxLaunchSegs) {
+        if (mirror_) mirror_->before(stream);
         eng_->collate_span(slots, n, stream, a, v0.src_dtype, dst_dt, shift, scale, false);
+        if (mirror_) mirror_->after(stream);
         ++launches;
         a.n_seg = 0;
       }
       SpanDevSeg& d = a.s[a.n_seg++];
-      d.src = broker_->log_base(sg[i].pidx) + sg[i].log_pos;  // pinned: device address == host address
+      d.src = seg_src(sg[i]);
       d.log_pos = sg[i].log_pos;
       d.len = sg[i].len;
       d.flags = sg[i].flags;
@@ -586,14 +599,192 @@ void MainDriver::launch_span(const int* slots, const SlotView* const* views, int
       d.seg = uint16_t(i);
     }
   }
+  if (mirror_) mirror_->before(stream);
   eng_->collate_span(slots, n, stream, a, v0.src_dtype, dst_dt, shift, scale, record_last);
+  if (mirror_) mirror_->after(stream);
   (void)launches;
+}
+
+uint64_t MainDriver::stage_alloc(uint64_t bytes) {
+  bytes = (bytes + 255) & ~uint64_t(255);
+  if (bytes > kStageBytes) throw std::runtime_error("driver: a device JSON group exceeds the staging ring");
+  if (!stage_dev_ && hipMalloc(reinterpret_cast<void**>(&stage_dev_), kStageBytes) != hipSuccess)
+    throw std::runtime_error("driver: hipMalloc of the JSON staging ring failed");
+  uint64_t pos = stage_head_;
+  const uint64_t in = pos % kStageBytes;
+  if (in + bytes > kStageBytes) pos += kStageBytes - in;  // never split a region: restart at the front
+  while (pos + bytes - stage_tail_ > kStageBytes) {
+    // the oldest groups still read their regions: wait for the first one with an event
+    cover_handed();
+    bool waited = false;
+    for (const auto& h : handed_) {
+      if (!h.ev) continue;
+      eng_->wait_slot(int(h.g));
+      waited = true;
+      break;
+    }
+    if (!waited) throw std::logic_error("driver: JSON staging ring full with nothing in flight");
+    pending_query_ns_ = 0;
+    release_completed_impl();
+  }
+  stage_head_ = pos + bytes;
+  stage_last_end_ = stage_head_;
+  return pos % kStageBytes;
+}
+
+void MainDriver::launch_json_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream,
+                                  int dst_dt, double pad, void* const* outs, const int64_t* Ls,
+                                  int64_t* const* lengths, uint8_t* const* masks, bool record_last, int64_t* perrs) {
+  if (!broker_) throw std::runtime_error("driver: device JSON parse needs the synthetic broker");
+  ensure_partials();
+  // staging per batch: the row descriptors, then one region per segment (row texts rounded up to
+  // 16 bytes, or the float32 values of the rows the worker parsed)
+  constexpr uint64_t kA = 256;
+  auto up = [](uint64_t x, uint64_t a) { return (x + a - 1) / a * a; };
+  uint64_t batch_bytes[kMaxGroup], total = 0;
+  for (int k = 0; k < n; ++k) {
+    const SlotView& v = *views[k];
+    const uint8_t* pay = ring_->payload(uint32_t(v.g));
+    const auto* sg = reinterpret_cast<const tk::SpanSeg*>(pay + v.values_offset);
+    const auto* rows = reinterpret_cast<const tk::JsonSpanRow*>(pay);
+    uint64_t b = up(uint64_t(v.n_rows) * sizeof(JsonRowDesc), kA);
+    for (uint32_t i = 0; i < v.n_segs; ++i) {
+      const uint64_t nr = sg[i].row_end - sg[i].row_begin;
+      if (sg[i].flags & tk::kSegHostRows) {
+        for (uint32_t r = sg[i].row_begin; r < sg[i].row_end; ++r) {
+          int64_t c = rows[r].count;
+          if (v.trunc_len >= 0 && c > v.trunc_len) c = v.trunc_len;
+          b += up(uint64_t(c < 0 ? 0 : c) * 4, 16);
+        }
+        b = up(b, kA);
+      } else {
+        b += up(up(sg[i].len, 16) + 16 * nr, kA);
+      }
+    }
+    batch_bytes[k] = b;
+    total += b;
+  }
+  const uint64_t base = stage_alloc(total);
+  JsonStageLaunch a{};
+  a.burst = span_burst_;
+  JsonGroupArgs ga{};
+  ga.n = n;
+  ga.pad = float(pad);
+  ga.err_tag = tk::kSpanParseErrBit;
+  uint64_t off = base;
+  for (int k = 0; k < n; ++k) {
+    const SlotView& v = *views[k];
+    perrs[k] = next_err_word();
+    JsonStageBatch& b = a.b[k];
+    b.desc = reinterpret_cast<JsonRowDesc*>(stage_dev_ + off);
+    const uint64_t dbytes = up(uint64_t(v.n_rows) * sizeof(JsonRowDesc), kA);
+    b.stage = stage_dev_ + off + dbytes;
+    b.err = perr_dev_ + perrs[k];
+    b.partials = part_dev_ + perrs[k] * kPartials;
+    b.trunc_len = v.trunc_len;
+    ga.rows[k] = b.desc;
+    ga.vals[k] = b.stage;
+    ga.vals_cap[k] = batch_bytes[k] - dbytes;
+    ga.out[k] = outs[k];
+    ga.L[k] = Ls[k];
+    ga.lengths[k] = lengths[k];
+    ga.mask[k] = masks[k];
+    ga.err[k] = b.err;
+    ga.row_base[k + 1] = ga.row_base[k] + int64_t(v.n_rows);
+    off += batch_bytes[k];
+  }
+  for (int k = 0; k < n; ++k) {
+    const SlotView& v = *views[k];
+    const uint8_t* pay = ring_->payload(uint32_t(v.g));
+    const auto* sg = reinterpret_cast<const tk::SpanSeg*>(pay + v.values_offset);
+    const auto* rows = reinterpret_cast<const tk::JsonSpanRow*>(pay);
+    uint64_t soff = 0;  // offset in the batch's staging area (after its descriptors)
+    for (uint32_t i = 0; i < v.n_segs; ++i) {
+      constexpr uint32_t kWhole = tk::kSegCrcFirst | tk::kSegCrcLast;
+      if ((sg[i].flags & tk::kSegCrc) && (sg[i].flags & kWhole) != kWhole && i >= uint32_t(kPartials))
+        throw std::runtime_error("driver: a batch splits RecordBatches into more than 512 device segments");
+      if (a.n_seg == kMaxLaunchSegs) {
+        if (mirror_) mirror_->before(stream);
+        eng_->collate_json_stage(slots, n, stream, a);
+        if (mirror_) mirror_->after(stream);
+        a.n_seg = 0;
+      }
+      SpanDevSeg& d = a.s[a.n_seg++];
+      const bool host = (sg[i].flags & tk::kSegHostRows) != 0;
+      d.src = host ? nullptr : seg_src(sg[i]);
+      d.log_pos = sg[i].log_pos;
+      d.len = sg[i].len;
+      d.flags = sg[i].flags;
+      d.crc = sg[i].crc;
+      d.row_begin = sg[i].row_begin;
+      d.row_end = sg[i].row_end;
+      d.batch = uint16_t(k);
+      d.seg = uint16_t(i);
+      d.stage_off = uint32_t(soff);
+      const uint64_t nr = sg[i].row_end - sg[i].row_begin;
+      if (host) {
+        for (uint32_t r = sg[i].row_begin; r < sg[i].row_end; ++r) {
+          int64_t c = rows[r].count;
+          if (v.trunc_len >= 0 && c > v.trunc_len) c = v.trunc_len;
+          soff += up(uint64_t(c < 0 ? 0 : c) * 4, 16);
+        }
+        soff = up(soff, kA);
+      } else {
+        soff += up(up(sg[i].len, 16) + 16 * nr, kA);
+      }
+    }
+  }
+  if (mirror_) mirror_->before(stream);
+  eng_->collate_json_stage(slots, n, stream, a);
+  if (mirror_) mirror_->after(stream);
+  // the parse: a block per row over the staged texts, on the same stream
+  launch_json_group(ga, dst_dt, stream);
+  if (record_last) eng_->record_done(slots[n - 1], stream);
+}
+
+const uint8_t* MainDriver::seg_src(const tk::SpanSeg& sg) {
+  const uint8_t* log = broker_->log_base(sg.pidx);  // pinned: device address == host address
+  if (mirror_) {
+    // pin ahead of the segment so the mirror can copy (and prefetch) whole chunks
+    const auto& part = broker_->part(sg.pidx);
+    ensure_log(sg.pidx, std::min<uint64_t>(part.log_capacity, sg.log_pos + 2 * mirror_->chunk_bytes()));
+    const uint64_t written = part.log_end_pos.load(std::memory_order_acquire);
+    const uint8_t* m = mirror_->map(sg.pidx, sg.log_pos, sg.len, log, std::min<uint64_t>(reg_end_[sg.pidx], written));
+    if (m) return m;
+  }
+  return log + sg.log_pos;
+}
+
+void MainDriver::enable_mirror(uint64_t chunk_bytes, int chunks_per_partition) {
+  if (!broker_) throw std::runtime_error("DeviceLoader h2d='dma' device decode needs the synthetic broker");
+  mirror_ = std::make_unique<LogMirror>(eng_->device(), chunk_bytes, chunks_per_partition);
+}
+
+void MainDriver::span_group_handed(const int* slots, int n, hipStream_t ks, const int64_t* perrs,
+                                   std::vector<std::shared_ptr<void>>&& handles, size_t first) {
+  for (int k = 0; k < n; ++k) handed_.push_back(Handed{slots[k], k == n - 1, perrs[k], true});
+  handed_.back().stage_end = stage_last_end_;  // 0 unless a JSON group just took a staging region
+  stage_last_end_ = 0;
+  last_ev_slot_ = slots[n - 1];
+  unevented_ = 0;
+  ++events_;
+  if (n > 1) ++groups_;
+  for (size_t k = first; k < size_t(n); ++k) {
+    SlotView& v = staged_[group_idx_[k - first]];
+    v.perr = perrs[k];
+    v.pre = true;
+    v.pre_stream = ks;
+    v.pre_event_slot = slots[n - 1];
+    v.pre_out = std::move(handles[k - first]);
+  }
 }
 
 void MainDriver::check_span(int64_t g, int64_t pe) {
   const tk::SlotHeader* h = ring_->slot(uint32_t(g));
   const auto* sg = reinterpret_cast<const tk::SpanSeg*>(ring_->payload(uint32_t(g)) + h->values_offset);
-  int32_t bad = __atomic_load_n(perr_host_ + pe, __ATOMIC_ACQUIRE);  // a whole RecordBatch failed on the device
+  // a whole RecordBatch failed its CRC on the device (segment index), or a JSON row its parse
+  const int32_t dev = __atomic_load_n(perr_host_ + pe, __ATOMIC_ACQUIRE);
+  int32_t bad = dev >= tk::kSpanParseErrBit ? -1 : dev;
   const uint32_t* part = part_host_ + pe * kPartials;
   uint32_t acc = 0;
   for (uint32_t i = 0; i < h->n_segs && bad < 0; ++i) {
@@ -605,7 +796,12 @@ void MainDriver::check_span(int64_t g, int64_t pe) {
     acc = tk::crc32c_shift_raw(acc, crc_len) ^ __atomic_load_n(part + i, __ATOMIC_ACQUIRE);
     if ((f & tk::kSegCrcLast) && (acc ^ 0xFFFFFFFFu) != sg[i].crc) bad = int32_t(i);
   }
-  if (bad < 0) return;
+  if (bad < 0) {
+    if (dev >= tk::kSpanParseErrBit)
+      perr_msg_[size_t(pe)] = "batch row " + std::to_string(dev & ~tk::kSpanParseErrBit) +
+                              " is not a flat numeric JSON array (device parse from the log)";
+    return;
+  }
   // the RecordBatch of segment `bad`: walk back to its first segment for its base offset
   uint32_t i = uint32_t(bad);
   while (i > 0 && !(sg[i].flags & tk::kSegCrcFirst)) --i;
@@ -627,7 +823,8 @@ void MainDriver::stage_ready(int extra) {
 
 size_t MainDriver::json_group_extend() {
   group_idx_.clear();
-  if (coalesce_ <= 1 || last.kind != uint32_t(tk::kPackJsonText)) return 0;
+  if (coalesce_ <= 1 || (last.kind != uint32_t(tk::kPackJsonText) && last.kind != uint32_t(tk::kPackJsonSpan)))
+    return 0;
   for (size_t i = 0; i < staged_.size() && int(1 + group_idx_.size()) < coalesce_; ++i) {
     const SlotView& v = staged_[i];
     if (v.g < 0) continue;  // watermark-only slot: rides on the next delivered batch
@@ -642,6 +839,29 @@ void MainDriver::json_group_launch(hipStream_t stream, int dst_dt, double pad, v
                                    std::vector<std::shared_ptr<void>>&& handles) {
   const int n = 1 + int(group_idx_.size());
   if (int(handles.size()) != n - 1) throw std::invalid_argument("driver: group handles do not match the group");
+  if (last.kind == uint32_t(tk::kPackJsonSpan)) {
+    // parsed on the next decode stream (outputs allocated there, torch_step.cpp); the user's
+    // stream waits for the group's completion
+    int slots[kMaxGroup];
+    const SlotView* vs[kMaxGroup];
+    for (int k = 0; k < n; ++k) {
+      vs[k] = k == 0 ? &last : &staged_[group_idx_[size_t(k - 1)]];
+      slots[k] = int(vs[k]->g);
+    }
+    cover_handed();
+    hipStream_t ks = next_decode_stream();
+    ++span_launches_;
+    last_stream_ = ks;
+    int64_t perrs[kMaxGroup];
+    launch_json_span(slots, vs, n, ks, dst_dt, pad, outs, Ls, lengths, masks, true, perrs);
+    last.perr = perrs[0];
+    span_group_handed(slots, n, ks, perrs, std::move(handles), 1);
+    eng_->stream_wait_done(slots[n - 1], stream);
+    waited_ev_slot_ = slots[n - 1];
+    waited_stream_ = stream;
+    group_idx_.clear();
+    return;
+  }
   int slots[kMaxGroup];
   size_t voffs[kMaxGroup];
   int64_t rows[kMaxGroup], perr[kMaxGroup];
@@ -970,12 +1190,14 @@ void MainDriver::ahead_begin(std::vector<int64_t>* rows) {
   }
   if (pre >= ahead_depth_ * coalesce_ || i0 == staged_.size()) return;
   const SlotView& f = staged_[i0];
-  if (f.kind != uint32_t(tk::kPackRecordSpan) || f.n_rows == 0) return;
+  const bool json = f.kind == uint32_t(tk::kPackJsonSpan);  // outputs sized per batch: no shape match needed
+  if ((f.kind != uint32_t(tk::kPackRecordSpan) && !json) || f.n_rows == 0) return;
   for (size_t i = i0; i < staged_.size() && int(group_idx_.size()) < coalesce_; ++i) {
     const SlotView& v = staged_[i];
     if (v.g < 0) continue;  // watermark-only slot: rides on the next delivered batch
-    if (v.pre || v.kind != f.kind || v.src_dtype != f.src_dtype || v.max_row_len != f.max_row_len ||
-        v.row_bytes != f.row_bytes || v.shape != f.shape || v.n_rows == 0)
+    if (v.pre || v.kind != f.kind || v.n_rows == 0) break;
+    if (!json && (v.src_dtype != f.src_dtype || v.max_row_len != f.max_row_len || v.row_bytes != f.row_bytes ||
+                  v.shape != f.shape))
       break;
     group_idx_.push_back(i);
   }
@@ -1018,6 +1240,30 @@ void MainDriver::ahead_launch(int dst_dt, void* const* dsts, const float* shift,
     v.pre_event_slot = slots[n - 1];
     v.pre_out = std::move(handles[size_t(k)]);
   }
+  group_idx_.clear();
+  ph_launch_ns_ += tk::now_ns() - t0;
+}
+
+void MainDriver::ahead_launch_json(int dst_dt, double pad, void* const* outs, const int64_t* Ls,
+                                   int64_t* const* lengths, uint8_t* const* masks,
+                                   std::vector<std::shared_ptr<void>>&& handles) {
+  const int n = int(group_idx_.size());
+  if (n < 1 || int(handles.size()) != n) throw std::invalid_argument("driver: ahead group does not match");
+  const int64_t t0 = tk::now_ns();
+  int slots[kMaxGroup];
+  const SlotView* vs[kMaxGroup];
+  for (int k = 0; k < n; ++k) {
+    vs[k] = &staged_[group_idx_[size_t(k)]];
+    slots[k] = int(vs[k]->g);
+  }
+  cover_handed();
+  hipStream_t ks = next_decode_stream();
+  ++span_launches_;
+  last_stream_ = ks;
+  int64_t perrs[kMaxGroup];
+  launch_json_span(slots, vs, n, ks, dst_dt, pad, outs, Ls, lengths, masks, true, perrs);
+  span_group_handed(slots, n, ks, perrs, std::move(handles), 0);
+  ++ahead_groups_;
   group_idx_.clear();
   ph_launch_ns_ += tk::now_ns() - t0;
 }

@@ -21,6 +21,7 @@
 #include "broker.h"
 #include "collate.h"
 #include "engine.h"
+#include "log_mirror.h"
 #include "rccl_lockstep.h"
 #include "ring.h"
 #include "span_decode.h"
@@ -34,7 +35,8 @@ struct SlotView {
   uint32_t row_bytes = 0;
   int64_t max_row_len = 0, total_elems = 0, n_scanned = 0;
   int32_t src_dtype = -1;
-  uint32_t n_segs = 0;                // kPackRecordSpan: SpanSeg entries at values_offset
+  uint32_t n_segs = 0;                // kPackRecordSpan / kPackJsonSpan: SpanSeg entries at values_offset
+  int32_t trunc_len = -1;             // kPackJsonSpan: rows keep at most this many elements (-1: all)
   std::vector<int64_t> shape;
   std::vector<tk::Watermark> wms;
   // coalesced fast path: collated ahead of delivery by a group launch
@@ -112,7 +114,12 @@ class MainDriver {
   // Stages READY slots until `extra` beyond prefetch are staged (never blocks).
   void stage_ready(int extra);
   // A batch parsed by a group launch on another stream: `stream` waits for that kernel.
-  void wait_group(const SlotView& v, hipStream_t stream) { eng_->stream_wait_done(int(v.pre_event_slot), stream); }
+  void wait_group(const SlotView& v, hipStream_t stream) {
+    if (waited_ev_slot_ == v.pre_event_slot && waited_stream_ == stream) return;  // one wait per group
+    eng_->stream_wait_done(int(v.pre_event_slot), stream);
+    waited_ev_slot_ = v.pre_event_slot;
+    waited_stream_ = stream;
+  }
   const SlotView& group_member(size_t k) const { return staged_[group_idx_[k]]; }
   void json_group_launch(hipStream_t stream, int dst_dt, double pad, void* const* outs, const int64_t* Ls,
                          int64_t* const* lengths, uint8_t* const* masks,
@@ -127,6 +134,11 @@ class MainDriver {
   void ahead_begin(std::vector<int64_t>* rows);
   void ahead_launch(int dst_dt, void* const* dsts, const float* shift, const float* scale,
                     std::vector<std::shared_ptr<void>>&& handles);
+  // The batches of the group ahead_begin formed (JSON: their row counts and max row lengths size
+  // the outputs), and the JSON-span variant of ahead_launch (outputs as json_group_launch).
+  const SlotView& ahead_member(size_t k) const { return staged_[group_idx_[k]]; }
+  void ahead_launch_json(int dst_dt, double pad, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
+                         uint8_t* const* masks, std::vector<std::shared_ptr<void>>&& handles);
   void set_ahead_depth(int n) { ahead_depth_ = n < 0 ? 0 : n; }
   // LDS-DMA loads a wave of the span decode kernel keeps in flight before it waits (0 = all;
   // default 1; TORCHKAFKA_SPAN_BURST)
@@ -156,6 +168,10 @@ class MainDriver {
   // when the iteration starts instead of by the first batches that reach each partition.
   void pin_logs(const std::vector<uint32_t>& pidxs);
   bool direct() const { return direct_; }
+  // h2d='dma' with device decode: the decode kernels read the logs from an HBM mirror that the copy
+  // engines fill chunk by chunk (log_mirror.h) instead of over PCIe from the pinned logs.
+  void enable_mirror(uint64_t chunk_bytes, int chunks_per_partition);
+  const LogMirror* mirror() const { return mirror_.get(); }
   uint64_t log_bytes_registered() const { return reg_total_; }
   int64_t log_register_ns() const { return reg_ns_; }
   int coalesce() const { return coalesce_; }
@@ -223,6 +239,20 @@ class MainDriver {
   void check_span(int64_t g, int64_t pe);
   void launch_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
                    void* const* dsts, const float* shift, const float* scale, bool record_last, int64_t* perrs);
+  void launch_json_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
+                        double pad, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
+                        uint8_t* const* masks, bool record_last, int64_t* perrs);
+  void ensure_partials();
+  // HBM staging ring of the device JSON parse (row texts between the two kernels, json_span.hip):
+  // positions are monotonic, regions are freed in launch order as their groups' slots are released.
+  static constexpr uint64_t kStageBytes = uint64_t(128) << 20;
+  uint8_t* stage_dev_ = nullptr;
+  uint64_t stage_head_ = 0, stage_tail_ = 0, stage_last_end_ = 0;
+  uint64_t stage_alloc(uint64_t bytes);
+  // One device-decode group launched on the next decode stream: slots handed out, the staged
+  // members marked pre-decoded (outputs in handles, offset by `first`: 1 when views[0] is `last`).
+  void span_group_handed(const int* slots, int n, hipStream_t ks, const int64_t* perrs,
+                         std::vector<std::shared_ptr<void>>&& handles, size_t first);
   static constexpr int64_t kErrWords = 4096;
   static constexpr int64_t kPartials = 512;  // raw CRC words per error word (segments of one slot)
   uint32_t* part_host_ = nullptr;          // hipHostMalloc'ed, device-mapped partial CRCs
@@ -257,6 +287,7 @@ class MainDriver {
     bool ev;            // its own completion event was recorded
     int64_t perr = -1;  // device JSON parse / span decode: its error word, checked at slot release
     bool span = false;  // kPackRecordSpan: chain the partial CRCs of split RecordBatches at release
+    uint64_t stage_end = 0;  // kPackJsonSpan group: staging ring position freed when this slot is released
   };
   std::deque<Handed> handed_;  // slots whose collate was launched, in launch order
   hipStream_t last_stream_ = nullptr;
@@ -319,6 +350,8 @@ class MainDriver {
                     hipStream_t stream, int dst_dt, void* const* dsts, int64_t row, const float* shift,
                     const float* scale);
   bool direct_ = false;
+  std::unique_ptr<LogMirror> mirror_;
+  const uint8_t* seg_src(const tk::SpanSeg& sg);  // the address a decode kernel reads a segment from
   uint64_t* bases_dev_ = nullptr;
   std::vector<uint64_t> reg_end_;        // per pidx: bytes of its log pinned (and device-mapped)
   std::vector<void*> reg_ptrs_;          // registered ranges, unregistered at teardown

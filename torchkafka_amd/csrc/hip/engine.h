@@ -7,7 +7,8 @@
 
 namespace tkh {
 
-struct SpanLaunch;  // span_decode.h
+struct SpanLaunch;      // span_decode.h
+struct JsonStageLaunch;
 
 // How a ring slot's bytes reach the collate kernel.
 enum H2DMode : int {
@@ -71,6 +72,10 @@ class Engine {
   // slots[n - 1] when `record`.  The log bytes are read from the pinned broker logs.
   void collate_span(const int* slots, int n, hipStream_t user, SpanLaunch& a, int src_dt, int dst_dt,
                     const float* shift, const float* scale, bool record = true);
+  // Device JSON parse from the logs (kPackJsonSpan, json_span.hip), first kernel: stage + CRC +
+  // row texts into HBM (a.b[k].rows / .slot are filled in here from slots[k]); the driver then
+  // launches json_rows_kernel over the descriptors and records the completion event.
+  void collate_json_stage(const int* slots, int n, hipStream_t user, JsonStageLaunch& a);
   // Device copy of the CRC tables of the span kernel (uploaded on first use).
   const uint32_t* span_tables();
   // The streams device-decode groups rotate over (created on first use; kDecodeStreams).

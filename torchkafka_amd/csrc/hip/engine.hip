@@ -270,6 +270,7 @@ void Engine::prepare_decode() {
     TKH_CHECK(hipStreamSynchronize(st));
   }
   prewarm_span_kernels(device_);
+  prewarm_json_span_kernels();
 }
 
 hipStream_t Engine::decode_stream(int k) {
@@ -304,6 +305,18 @@ void Engine::collate_span(const int* slots, int n, hipStream_t user, SpanLaunch&
   a.tabs = span_tables();
   launch_span_decode(a, src_dt, dst_dt, shift, scale, user);
   if (record) finish(slots[n - 1], user);
+}
+
+void Engine::collate_json_stage(const int* slots, int n, hipStream_t user, JsonStageLaunch& a) {
+  if (n < 1 || n > kMaxGroup) throw std::invalid_argument("engine: bad group size");
+  for (int k = 0; k < n; ++k) {
+    check_slot(slots[k]);
+    begin(slots[k], user);  // DMA mode: the row table and host-parsed values were copied with the slot
+    a.b[k].slot = src_base(slots[k]);
+    a.b[k].rows = reinterpret_cast<const tk::JsonSpanRow*>(a.b[k].slot);
+  }
+  a.tabs = span_tables();
+  launch_json_stage(a, user);
 }
 
 void Engine::copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes) {

@@ -35,6 +35,7 @@
 
 #include "collate.h"
 #include "dtypes.h"
+#include "json_token.h"
 
 namespace tkh {
 
@@ -47,95 +48,8 @@ constexpr int kWin = 2048;                    // bytes of text per window (one 8
 constexpr int kLaneBytes = kWin / kThreads;   // 8 contiguous bytes classified per thread
 constexpr int kMaxTok = kWin / 2 + 1;         // a token needs >= 1 char and 1 separator
 
-__device__ __forceinline__ bool is_sep(uint32_t c) {
-  return c == ',' || c == ' ' || c == '[' || c == ']' || c == '\n' || c == '\t' || c == '\r';
-}
-
-__device__ __constant__ double kP10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
-                                           1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
-
 template <typename D>
 __device__ __forceinline__ D pad_value(float p) { return Store<D>::cvt(p); }
-
-// The token starting at window byte s, parsed from registers: the 32 LDS bytes from
-// s & ~15 (two ds_read_b128) are funnel-shifted so that t[0..4] hold bytes s .. s+19, and a
-// fully unrolled walk over at most 17 bytes (a simple row's number has <= 16 characters,
-// then a separator) runs the host parser's grammar with no dependent memory access.
-// `avail` = bytes of the window from s on.  Returns 1 ok, 0 grammar error, 2 cut by the
-// window end (parsed again in the next window).
-__device__ __forceinline__ int parse_token_regs(const uint8_t* buf, int s, int avail, bool last_window, float* out) {
-  const int A = s & ~15;
-  const uint4 lo = *reinterpret_cast<const uint4*>(buf + A);
-  const uint4 hi = *reinterpret_cast<const uint4*>(buf + A + 16);
-  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-  const int o = s - A, q = o >> 2;
-  const uint32_t sh = uint32_t(o & 3) * 8u;
-  uint32_t t[5];
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    // dwords q+k and q+k+1 (q <= 3, so at most w[7] and a dummy)
-    const uint32_t a0 = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
-    const uint32_t a1 = q == 0 ? w[k + 1] : q == 1 ? w[k + 2] : q == 2 ? w[k + 3] : (k + 4 < 8 ? w[k + 4] : 0u);
-    t[k] = sh ? (a0 >> sh) | (a1 << (32u - sh)) : a0;
-  }
-  bool neg = false, dot = false, frac = false, any = false, ended = false, bad = false, truncated = false;
-  uint32_t endc = 0;
-  int endj = 17;
-  uint64_t mant = 0;
-  int nd = 0, exp10 = 0;
-#pragma unroll
-  for (int j = 0; j < 17; ++j) {
-    const uint32_t c = (t[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
-    if (!ended) {
-      if (j >= avail) {
-        ended = true;
-        endj = j;
-        endc = 0x100u;  // window end
-      } else if (j == 0 && c == '-') {
-        neg = true;
-      } else if (c - '0' <= 9u) {
-        const uint32_t dd = c - '0';
-        any = true;
-        if (dot) frac = true;
-        if (mant == 0 && dd == 0) {
-          if (dot) --exp10;
-        } else if (nd < 19) {
-          mant = mant * 10 + dd;
-          ++nd;
-          if (dot) --exp10;
-        } else {
-          truncated = true;
-          if (!dot) ++exp10;
-        }
-      } else if (c == '.' && !dot) {
-        dot = true;
-      } else {
-        ended = true;
-        endj = j;
-        endc = c;
-      }
-    }
-  }
-  if (!ended) return 0;  // longer than a simple number
-  if (endc == 0x100u) {
-    if (!last_window) return 2;
-    return 0;  // text ended inside a number
-  }
-  (void)endj;
-  bad = !any || (dot && !frac) || !is_sep(endc);
-  if (bad) return 0;
-  if (mant == 0 && !dot) neg = false;  // "-0" is the JSON integer 0: +0.0 after Python's float()
-  double v;
-  if (!truncated && mant <= (uint64_t(1) << 53) && exp10 >= -22 && exp10 <= 22) {
-    v = exp10 < 0 ? double(mant) / kP10[-exp10] : double(mant) * kP10[exp10];
-  } else if (!truncated && exp10 == 0) {
-    v = double(mant);  // one rounding: the hi/lo u32 halves convert exactly, the add rounds
-  } else {
-    return 0;  // the worker's pre-scan never sends such tokens
-  }
-  *out = float(neg ? -v : v);
-  return 1;
-}
 
 // Blocks [row_base[k], row_base[k+1]) parse batch k: one launch serves up to kMaxGroup
 // staged batches (the driver's coalesced launches), each with its own slot, output and L.
@@ -159,10 +73,18 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
   uint8_t* __restrict__ mask = a.mask[bk];
   int32_t* __restrict__ err = a.err[bk];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-  const JsonRowDesc d = rows[r];
+  JsonRowDesc d = rows[r];
+  bool bad = false;  // block-uniform: only read after a barrier
+  if (a.vals_cap[bk] > 0) {
+    // staged by json_stage_kernel: a descriptor must stay inside the batch's staging area
+    const uint64_t need = d.tlen >= 0 ? uint64_t(d.tlen) : uint64_t(d.n_out < 0 ? 0 : d.n_out) * 4u;
+    if (d.count < 0 || d.n_out < 0 || d.n_out > d.count || uint64_t(d.off) + ((need + 15u) & ~uint64_t(15)) > a.vals_cap[bk]) {
+      bad = true;
+      d = JsonRowDesc{0, 0, 0, 0};
+    }
+  }
   const int64_t n_out = d.n_out < L ? d.n_out : L;
   D* orow = out + r * L;
-  bool bad = false;  // block-uniform: only read after a barrier
 
   if (d.tlen < 0) {
     // parsed on the host (not a simple row): float32 values
@@ -273,7 +195,7 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
     for (int64_t k = tid; k < L; k += kThreads) mrow[k] = uint8_t(k < n_out);
   }
   if (lengths && tid == 0) lengths[r] = n_out;
-  if (err && bad && tid == 0) *err = int32_t(r);
+  if (err && bad && tid == 0 && (a.err_tag == 0 || *err < 0)) *err = a.err_tag | int32_t(r);
 }
 
 template <typename D>

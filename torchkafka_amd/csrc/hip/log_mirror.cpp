@@ -1,0 +1,169 @@
+#include "log_mirror.h"
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+
+#include "span.h"
+
+namespace tkh {
+
+#define TKM_CHECK(expr)                                                                                \
+  do {                                                                                                 \
+    hipError_t _e = (expr);                                                                            \
+    if (_e != hipSuccess) throw std::runtime_error(std::string("log mirror: ") + #expr + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+LogMirror::LogMirror(int device, uint64_t chunk_bytes, int chunks_per_partition)
+    : device_(device), chunk_(chunk_bytes), K_(chunks_per_partition) {
+  if (chunk_ < (uint64_t(1) << 20) || chunk_ % 4096 != 0) throw std::invalid_argument("log mirror: chunk must be >= 1 MiB, 4 KiB aligned");
+  if (K_ < 2) throw std::invalid_argument("log mirror: at least 2 chunks per partition");
+  stride_ = (chunk_ + tk::kSpanSegMax + 256 + 4095) / 4096 * 4096;
+  TKM_CHECK(hipSetDevice(device_));
+  TKM_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+  TKM_CHECK(hipEventCreateWithFlags(&copied_, hipEventDisableTiming));
+  pool_.resize(256);
+  for (auto& e : pool_) TKM_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  pool_seq_.assign(pool_.size(), 0);
+  pool_refs_.assign(pool_.size(), 0);
+}
+
+LogMirror::~LogMirror() {
+  hipSetDevice(device_);
+  if (copy_) hipStreamSynchronize(copy_);
+  hipDeviceSynchronize();  // no decode kernel may still read a buffer
+  for (auto& P : parts_)
+    if (P.dev) hipFree(P.dev);
+  for (auto e : pool_) hipEventDestroy(e);
+  if (copied_) hipEventDestroy(copied_);
+  if (copy_) hipStreamDestroy(copy_);
+}
+
+LogMirror::Part& LogMirror::part(uint32_t pidx) {
+  if (pidx >= parts_.size()) parts_.resize(size_t(pidx) + 1);
+  Part& P = parts_[pidx];
+  if (!P.dev) {
+    TKM_CHECK(hipSetDevice(device_));
+    TKM_CHECK(hipMalloc(reinterpret_cast<void**>(&P.dev), stride_ * size_t(K_)));
+    P.bufs.assign(size_t(K_), Buf{});
+    dev_bytes_ += stride_ * size_t(K_);
+  }
+  return P;
+}
+
+void LogMirror::retarget(Buf& b, int64_t c) {
+  // the copy stream overwrites the buffer only after every reader of its previous chunk
+  for (auto& r : b.readers) {
+    if (r.ev >= 0 && pool_seq_[size_t(r.ev)] == r.seq) {
+      TKM_CHECK(hipStreamWaitEvent(copy_, pool_[size_t(r.ev)], 0));
+      --pool_refs_[size_t(r.ev)];
+    }
+    r = Reader{};
+  }
+  b.chunk = c;
+  b.end = uint64_t(c) * chunk_;
+  b.copy_seq = 0;
+}
+
+LogMirror::Buf* LogMirror::ensure(Part& P, uint32_t pidx, int64_t c, uint64_t want_end, const uint8_t* log,
+                                  uint64_t pinned, bool prefetch) {
+  (void)pidx;
+  const size_t j = size_t(c % K_);
+  Buf& b = P.bufs[j];
+  if (b.chunk != c) {
+    if (b.pending) return nullptr;  // read by the launch being formed
+    retarget(b, c);
+  }
+  const uint64_t lo_c = uint64_t(c) * chunk_;
+  const uint64_t target = std::min<uint64_t>(pinned, lo_c + chunk_ + tk::kSpanSegMax);
+  if (want_end > b.end) {
+    if (target < want_end) return nullptr;  // not pinned/written that far (the caller pins first)
+  } else if (!prefetch || target <= b.end || (target - b.end < chunk_ / 4 && target < lo_c + chunk_ + tk::kSpanSegMax)) {
+    return &b;  // resident (a prefetch tops up only in sizeable pieces)
+  }
+  if (target > b.end) {
+    TKM_CHECK(hipMemcpyAsync(P.dev + j * stride_ + (b.end - lo_c), log + b.end, size_t(target - b.end),
+                             hipMemcpyHostToDevice, copy_));
+    bytes_ += target - b.end;
+    ++copies_;
+    b.end = target;
+    b.copy_seq = ++copy_seq_;
+  }
+  return &b;
+}
+
+const uint8_t* LogMirror::map(uint32_t pidx, uint64_t pos, uint32_t len, const uint8_t* log, uint64_t pinned) {
+  if (len > tk::kSpanSegMax) throw std::invalid_argument("log mirror: segment longer than kSpanSegMax");
+  Part& P = part(pidx);
+  const int64_t c = int64_t(pos / chunk_);
+  Buf* b = ensure(P, pidx, c, pos + len, log, pinned, false);
+  if (!b) {
+    ++fallbacks_;
+    return nullptr;
+  }
+  if (!b->pending) {
+    b->pending = true;
+    pending_.emplace_back(pidx, int(c % K_));
+  }
+  // the next chunk streams in behind this one while the decode catches up with it
+  if (pinned > uint64_t(c + 1) * chunk_) ensure(P, pidx, c + 1, 0, log, pinned, true);
+  return P.dev + size_t(c % K_) * stride_ + (pos - uint64_t(c) * chunk_);
+}
+
+void LogMirror::before(hipStream_t stream) {
+  uint64_t need = 0;
+  for (const auto& pb : pending_) need = std::max(need, parts_[pb.first].bufs[size_t(pb.second)].copy_seq);
+  if (need == 0 || need <= done_seq_) return;
+  if (recorded_seq_ < need) {
+    TKM_CHECK(hipEventRecord(copied_, copy_));
+    recorded_seq_ = copy_seq_;
+  }
+  // a copy found complete need not be waited for again
+  if (hipEventQuery(copied_) == hipSuccess) {
+    done_seq_ = recorded_seq_;
+    return;
+  }
+  TKM_CHECK(hipStreamWaitEvent(stream, copied_, 0));
+}
+
+int LogMirror::next_event() {
+  const int e = int(pool_next_++ % pool_.size());
+  if (pool_refs_[size_t(e)] > 0) {
+    // still named by a buffer: that reader is 256 launches old; make sure it completed, then
+    // every reference to its old recording counts as completed (the sequence moves on)
+    TKM_CHECK(hipEventSynchronize(pool_[size_t(e)]));
+    pool_refs_[size_t(e)] = 0;
+  }
+  ++pool_seq_[size_t(e)];
+  return e;
+}
+
+void LogMirror::after(hipStream_t stream) {
+  if (pending_.empty()) return;
+  const int e = next_event();
+  TKM_CHECK(hipEventRecord(pool_[size_t(e)], stream));
+  for (const auto& pb : pending_) {
+    Buf& b = parts_[pb.first].bufs[size_t(pb.second)];
+    b.pending = false;
+    Reader* slot = nullptr;
+    for (auto& r : b.readers) {
+      if (r.ev >= 0 && pool_seq_[size_t(r.ev)] != r.seq) r = Reader{};  // completed long ago
+      if (r.ev >= 0 && r.stream == stream) {
+        --pool_refs_[size_t(r.ev)];  // superseded: the new event follows it on the same stream
+        r = Reader{};
+      }
+      if (r.ev < 0 && !slot) slot = &r;
+    }
+    if (!slot) {
+      // more reader streams than remembered: retire the first one on the host
+      slot = &b.readers[0];
+      TKM_CHECK(hipEventSynchronize(pool_[size_t(slot->ev)]));
+      --pool_refs_[size_t(slot->ev)];
+    }
+    *slot = Reader{stream, e, pool_seq_[size_t(e)]};
+    ++pool_refs_[size_t(e)];
+  }
+  pending_.clear();
+}
+
+}  // namespace tkh

@@ -1,0 +1,85 @@
+// HBM mirror of the pinned partition logs for the device-decode kernels (DeviceLoader h2d='dma'
+// with decode='device'; BASELINE config 2's "pinned hipMemcpyAsync H2D overlap").
+//
+// Zero-copy decode (the default) reads each segment over PCIe from inside the kernel: the
+// workgroup holds its CU for the whole transfer.  With the mirror, the copy engines (SDMA) move
+// the log bytes into HBM in large chunks ahead of use, on a copy stream of their own, and the
+// decode kernels read HBM: the CUs are busy only for the CRC and the decode, which leaves them to
+// the model that trains on the batches.  A partition log is mirrored chunk by chunk: chunk c holds
+// log bytes [c * C, (c + 1) * C + kSpanSegMax) -- the overlap keeps every segment (<= kSpanSegMax)
+// that starts in chunk c whole in one buffer -- in one of K buffers per partition (c % K), copied
+// as one hipMemcpyAsync of what is written (plus the next chunk as a prefetch), topped up when the
+// log grows.  Ordering is all on the GPU: a decode stream waits for the copy stream's event before
+// its kernel, and a buffer is overwritten only after the copy stream waited for the events of
+// every decode stream that read its previous chunk.  A segment whose buffer is still in use by the
+// group being formed is served from the pinned log instead (map() returns nullptr).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+namespace tkh {
+
+class LogMirror {
+ public:
+  LogMirror(int device, uint64_t chunk_bytes, int chunks_per_partition);
+  ~LogMirror();
+  LogMirror(const LogMirror&) = delete;
+  LogMirror& operator=(const LogMirror&) = delete;
+
+  // Device address of log bytes [pos, pos + len) of partition `pidx` (`log`: its pinned host base;
+  // bytes [0, pinned) are pinned and written), copying their chunk first when needed.  nullptr:
+  // not mirrored for this launch -- read the pinned log.
+  const uint8_t* map(uint32_t pidx, uint64_t pos, uint32_t len, const uint8_t* log, uint64_t pinned);
+  // Before the launch that reads what map() returned on `stream`: `stream` waits for the copies.
+  void before(hipStream_t stream);
+  // After that launch: the buffers it reads are released once `stream` passes this point.
+  void after(hipStream_t stream);
+
+  uint64_t chunk_bytes() const { return chunk_; }
+  uint64_t bytes_copied() const { return bytes_; }
+  uint64_t copies() const { return copies_; }
+  uint64_t fallbacks() const { return fallbacks_; }
+  uint64_t device_bytes() const { return dev_bytes_; }
+
+ private:
+  static constexpr int kStreams = 8;  // distinct reader streams remembered per buffer
+  struct Reader {
+    hipStream_t stream = nullptr;
+    int ev = -1;        // pool index
+    uint64_t seq = 0;   // pool_seq_[ev] when recorded; a newer value means it completed
+  };
+  struct Buf {
+    int64_t chunk = -1;
+    uint64_t end = 0;        // log position up to which the buffer holds the chunk's bytes
+    uint64_t copy_seq = 0;   // copy that brought in its latest bytes
+    bool pending = false;    // mapped for the launch being formed
+    Reader readers[kStreams];
+  };
+  struct Part {
+    uint8_t* dev = nullptr;
+    std::vector<Buf> bufs;
+  };
+  Part& part(uint32_t pidx);
+  Buf* ensure(Part& P, uint32_t pidx, int64_t c, uint64_t want_end, const uint8_t* log, uint64_t pinned,
+              bool prefetch);
+  void retarget(Buf& b, int64_t c);
+  int next_event();
+
+  int device_;
+  uint64_t chunk_, stride_;
+  int K_;
+  hipStream_t copy_ = nullptr;
+  hipEvent_t copied_ = nullptr;      // recorded on copy_ after the latest copy (when a launch needs it)
+  uint64_t copy_seq_ = 0, recorded_seq_ = 0, done_seq_ = 0;
+  std::vector<Part> parts_;
+  std::vector<std::pair<uint32_t, int>> pending_;
+  std::vector<hipEvent_t> pool_;
+  std::vector<uint64_t> pool_seq_;
+  std::vector<int> pool_refs_;
+  size_t pool_next_ = 0;
+  uint64_t bytes_ = 0, copies_ = 0, fallbacks_ = 0, dev_bytes_ = 0;
+};
+
+}  // namespace tkh

@@ -22,6 +22,8 @@ struct SpanDevSeg {
   uint32_t row_end;
   uint16_t batch;       // index into SpanLaunch::b
   uint16_t seg;         // index of the segment in its slot (partials[seg], *err = seg)
+  uint32_t stage_off;   // kPackJsonSpan: the segment's region in its batch's HBM staging area
+  uint32_t reserved;
 };
 
 struct SpanBatchOut {
@@ -40,6 +42,32 @@ struct SpanLaunch {
   SpanBatchOut b[kMaxGroup];
   SpanDevSeg s[kMaxLaunchSegs];
 };
+
+// kPackJsonSpan (json_span.hip): JSON text parsed straight from the pinned logs, in two kernels on
+// one stream: json_stage_kernel (a workgroup per segment: LDS-DMA stage, RecordBatch CRC, each row's
+// text copied 16-byte aligned into an HBM staging area + its JsonRowDesc) and json_parse.hip's
+// json_rows_kernel over those descriptors (a 256-thread block per row: the whole GPU parses).
+struct JsonStageBatch {
+  const tk::JsonSpanRow* rows;  // device view of the slot's row table
+  const uint8_t* slot;          // device view of the slot payload (the worker-parsed rows' float32 values)
+  JsonRowDesc* desc;            // [rows] descriptors for json_rows_kernel (HBM)
+  uint8_t* stage;               // the batch's staging area (HBM): texts / float32 values at desc[r].off
+  int32_t* err;                 // host-mapped status word: -1 clean, else the first bad segment (CRC)
+  uint32_t* partials;           // host-mapped raw CRC per segment (RecordBatches spanning segments)
+  int32_t trunc_len;            // rows with more elements keep this many (-1: no limit)
+  int32_t reserved;
+};
+
+struct JsonStageLaunch {
+  int n_seg;
+  int burst;                    // as SpanLaunch::burst
+  const uint32_t* tabs;         // device CRC tables (tk::kSpanTabWords)
+  JsonStageBatch b[kMaxGroup];
+  SpanDevSeg s[kMaxLaunchSegs];
+};
+
+void launch_json_stage(const JsonStageLaunch& a, hipStream_t stream);
+void prewarm_json_span_kernels();
 
 // Queries the attributes of the span kernel instantiations (loads their code object), so the
 // first real launch does not pay for it.

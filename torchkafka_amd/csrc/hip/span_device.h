@@ -1,0 +1,155 @@
+// Device code shared by the span kernels (span_decode.hip: fixed-width values, json_span.hip: JSON
+// text): one 256-thread workgroup per log segment (<= 128 KiB of one pinned partition log, so one
+// workgroup per CU),
+//   1. stage: the segment is copied into a contiguous LDS image (16-byte front offset) by LDS-DMA,
+//      global_load_lds_dwordx4, one 1 KiB load in flight per wave (fewer outstanding PCIe reads
+//      move more bytes; the launches of two or three decode streams keep the link busy);
+//   2. crc_lanes: CRC32C of a RecordBatch's bytes [21, end): 256 lanes x 260- or 516-byte chunks
+//      ending at the range end (an odd dword count per chunk: the 32 lanes of a ds_read_b32
+//      group hit 32 different banks), slice-by-8 tables in LDS fed by a sliding dword window
+//      (two ds_read_b32 + two v_alignbyte per 8 bytes), then 6 shuffle levels of "shift by 2^j
+//      chunks" (4 table lookups each, csrc/core/crc32c.cpp crc32c_span_tables);
+//   3. crc_verdict (thread 0, after a barrier): 2 LDS levels merge the 4 wave CRCs; a RecordBatch
+//      held whole by the segment is compared with its header CRC -- a mismatch stores the segment
+//      index into the batch's host-mapped error word (the driver reads it when the slot is
+//      released and never commits the batch) -- and a RecordBatch cut into several segments
+//      stores the raw partial CRC for the driver to chain.
+// Replaces kafka-python's check_crcs pass over every fetched RecordBatch.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "span.h"
+
+namespace tkh {
+namespace span {
+
+constexpr int kThreads = 256;
+constexpr int kFront = 16;  // LDS image offset: boundary reads may start up to 3 bytes before it
+constexpr int kLoads = int((tk::kSpanSegMax + 32) / 16 / kThreads) + 1;
+constexpr int kBufBytes = kFront + int(tk::kSpanSegMax) + 64;
+
+__device__ __forceinline__ uint32_t keep_from(int32_t a, int32_t c) {
+  // bytes of the dword at address a whose address is >= c
+  const int32_t d = c - a;
+  return d <= 0 ? 0xFFFFFFFFu : d >= 4 ? 0u : (0xFFFFFFFFu << (8 * d));
+}
+
+__device__ __forceinline__ uint32_t shift_op(const uint32_t* __restrict__ set, uint32_t level, uint32_t c) {
+  const uint32_t* S = set + level * 1024u;
+  return S[c & 255u] ^ S[256u + ((c >> 8) & 255u)] ^ S[512u + ((c >> 16) & 255u)] ^ S[768u + (c >> 24)];
+}
+
+// Stage 1.  Wave w's i-th load writes chunks [i * 256 + 64 w, +64) -- one contiguous KiB of the
+// image, exactly the instruction's wave-uniform-base + 16 * lane layout -- with no VGPR staging.
+// Each wave keeps `burst` loads in flight (0: all): zero-copy PCIe reads lose bandwidth with many
+// outstanding requests (tools/probes/tlb_probe.hip: 53 GB/s at 32 reading blocks, 40 at 512), and
+// with two or three decode kernels running at once the link stays full (config 2: 53 M rec/s with
+// one load in flight per wave, 41-44 M with 2-8, 46 M with all 17 issued up front).
+// `behind_first()` runs once the first load is issued (the row tables and CRC tables load behind
+// it: waiting for them waits for it).  The caller's __syncthreads() completes the image.
+template <class F>
+__device__ __forceinline__ void stage(const uint8_t* src, uint32_t len, uint8_t* buf, int burst, F&& behind_first) {
+  const int t = int(threadIdx.x);
+  const uintptr_t su = reinterpret_cast<uintptr_t>(src);
+  const uint32_t head = uint32_t(su & 15u);
+  const uint32_t nchunk = (head + len + 15u) >> 4;
+  const uint8_t* gsrc = reinterpret_cast<const uint8_t*>(su - head);
+  const int wv = t >> 6;
+  auto dma = [&](int i) {
+    const uint32_t c = uint32_t(t + i * kThreads);
+    if (c < nchunk)
+      __builtin_amdgcn_global_load_lds(
+          gsrc + 16u * c, (__attribute__((address_space(3))) void*)(buf + kFront + 16 * (i * kThreads + wv * 64)), 16,
+          0, 0);
+  };
+  dma(0);
+  behind_first();
+#pragma unroll
+  for (int i = 1; i < kLoads; ++i) {
+    if (16u * uint32_t(i * kThreads) >= 16u * nchunk) break;  // block-uniform: no wave has chunk i
+    dma(i);
+    if (burst > 0 && (i % burst) == burst - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// Stage 2 (every thread, after the barrier that completed the image).  The CRC range is
+// [c0, c1) in LDS bytes: [lo_b + 21, hi_b) for the segment holding a RecordBatch's start, else
+// [lo_b, hi_b).  Each wave's lane 0 leaves the wave's CRC in wcrc[wave]; returns the shift-table
+// set of the lane size used (for crc_verdict).
+__device__ __forceinline__ const uint32_t* crc_lanes(const uint32_t* __restrict__ b32, const uint32_t* __restrict__ tab,
+                                                     const uint32_t* __restrict__ tabs, int32_t lo_b, int32_t hi_b,
+                                                     uint32_t flags, uint32_t* wcrc) {
+  const int t = int(threadIdx.x);
+  const uint32_t* shift_set = tabs + tk::kSpanTabShift;
+  uint32_t crc = 0;
+  const bool first = (flags & tk::kSegCrcFirst) != 0;
+  const int32_t c0 = lo_b + (first ? 21 : 0), c1 = hi_b;
+  const int32_t L = int32_t(tk::span_lane_bytes(uint32_t(c1 - c0)));
+  if (L != int32_t(tk::kSpanLaneSmall)) shift_set += tk::kSpanTabShiftSet;
+  const int32_t start = c1 - (int32_t(tk::kSpanLanes) - t) * L;
+  const int32_t nsteps = (L - 4) >> 3;
+  if (start + 4 > c0) {  // the chunk's first 4 bytes (>= kFront - 3 whenever start + 4 > c0)
+    const int32_t w = start >> 2, sh = start & 3;
+    uint32_t x = __builtin_amdgcn_alignbyte(b32[w + 1], b32[w], sh);
+    if (start < c0 + 4) {
+      const uint32_t keep = keep_from(start, c0);
+      x &= keep;
+      if (first) x ^= keep & ~keep_from(start, c0 + 4);  // the 0xFFFFFFFF initial value
+    }
+    crc = tab[768 + (x & 255u)] ^ tab[512 + ((x >> 8) & 255u)] ^ tab[256 + ((x >> 16) & 255u)] ^ tab[x >> 24];
+  }
+  const int32_t a1 = start + 4;
+  const int32_t j0 = a1 >= c0 ? 0 : (c0 - a1) >> 3;  // 8-byte groups wholly below c0 are skipped
+  if (j0 < nsteps) {
+    int32_t ad = a1 + 8 * j0;
+    int32_t w = ad >> 2;
+    const int32_t sh = ad & 3;
+    uint32_t lo = b32[w];
+    for (int32_t j = j0; j < nsteps; ++j, ad += 8) {
+      const uint32_t m1 = b32[w + 1], m2 = b32[w + 2];
+      w += 2;
+      uint32_t x = __builtin_amdgcn_alignbyte(m1, lo, sh), y = __builtin_amdgcn_alignbyte(m2, m1, sh);
+      lo = m2;
+      if (ad < c0 + 4) {
+        const uint32_t kx = keep_from(ad, c0), ky = keep_from(ad + 4, c0);
+        x &= kx;
+        y &= ky;
+        if (first) {
+          x ^= kx & ~keep_from(ad, c0 + 4);
+          y ^= ky & ~keep_from(ad + 4, c0 + 4);
+        }
+      }
+      x ^= crc;
+      crc = tab[1792 + (x & 255u)] ^ tab[1536 + ((x >> 8) & 255u)] ^ tab[1280 + ((x >> 16) & 255u)] ^
+            tab[1024 + (x >> 24)] ^ tab[768 + (y & 255u)] ^ tab[512 + ((y >> 8) & 255u)] ^
+            tab[256 + ((y >> 16) & 255u)] ^ tab[y >> 24];
+    }
+  }
+  const int lane = t & 63;
+#pragma unroll
+  for (uint32_t j = 0; j < 6; ++j) {
+    const uint32_t other = __shfl_down(crc, 1u << j, 64);
+    if ((lane & ((2 << j) - 1)) == 0) crc = shift_op(shift_set, j, crc) ^ other;
+  }
+  if (lane == 0) wcrc[t >> 6] = crc;
+  return shift_set;
+}
+
+// Stage 3 (thread 0 only, after a barrier that follows crc_lanes).
+__device__ __forceinline__ void crc_verdict(const uint32_t* __restrict__ shift_set, const uint32_t* wcrc,
+                                            uint32_t flags, uint32_t want, uint32_t seg, int32_t* err,
+                                            uint32_t* partials) {
+  uint32_t c = shift_op(shift_set, 6, wcrc[0]) ^ wcrc[1];
+  c = shift_op(shift_set, 7, c) ^ (shift_op(shift_set, 6, wcrc[2]) ^ wcrc[3]);
+  constexpr uint32_t kWhole = tk::kSegCrcFirst | tk::kSegCrcLast;
+  if ((flags & kWhole) == kWhole) {
+    if ((c ^ 0xFFFFFFFFu) != want) *err = int32_t(seg);
+  } else {
+    partials[seg] = c;
+  }
+}
+
+}  // namespace span
+}  // namespace tkh

@@ -91,6 +91,80 @@ void launch_ahead(MainDriver& d, const std::vector<int64_t>& row_shape, const at
   }
 }
 
+// Padded width of a var-len batch: pad_to, else its longest row (rounded up to pad_multiple).
+int64_t padded_len(const SlotView& s, int64_t pad_to, int64_t pad_multiple) {
+  int64_t L = pad_to >= 0 ? pad_to : s.max_row_len;
+  if (pad_to < 0 && pad_multiple > 1) L = (L + pad_multiple - 1) / pad_multiple * pad_multiple;
+  return L;
+}
+
+// Outputs of a group of device-parsed JSON batches (kPackJsonSpan): one allocation for the values
+// of all of them, one for the lengths (and one for the masks), made on the decode stream the group
+// runs on and recorded on the user's stream (as alloc_group), then viewed per batch.
+void alloc_json_group(MainDriver& d, const int64_t* ms, const int64_t* Ls, int n, int dst_dt, bool want_mask,
+                      c10::DeviceIndex dev, std::shared_ptr<VarlenOut>* outs) {
+  int64_t tot = 0, rows = 0;
+  for (int k = 0; k < n; ++k) {
+    tot += ms[k] * Ls[k];
+    rows += ms[k];
+  }
+  const auto ks = c10::hip::getStreamFromExternal(d.next_decode_stream(), dev);
+  at::Tensor vals, lens, masks;
+  {
+    c10::hip::HIPStreamGuard guard(ks);
+    vals = at::empty({tot}, at::TensorOptions().dtype(scalar_type_of(dst_dt)).device(at::kCUDA, dev));
+    lens = at::empty({rows}, at::TensorOptions().dtype(at::kLong).device(at::kCUDA, dev));
+    if (want_mask) masks = at::empty({tot}, at::TensorOptions().dtype(at::kBool).device(at::kCUDA, dev));
+  }
+  const auto user = c10::hip::getCurrentHIPStream(dev);
+  for (const at::Tensor* t : {&vals, &lens, &masks})
+    if (t->defined() && t->numel() > 0) c10::hip::HIPCachingAllocator::recordStream(t->storage().data_ptr(), user);
+  int64_t vo = 0, ro = 0;
+  for (int k = 0; k < n; ++k) {
+    auto o = std::make_shared<VarlenOut>();
+    o->out = vals.narrow(0, vo, ms[k] * Ls[k]).view({ms[k], Ls[k]});
+    o->lengths = lens.narrow(0, ro, ms[k]);
+    if (want_mask) o->mask = masks.narrow(0, vo, ms[k] * Ls[k]).view({ms[k], Ls[k]});
+    vo += ms[k] * Ls[k];
+    ro += ms[k];
+    outs[k] = std::move(o);
+  }
+}
+
+// Device JSON parse ahead of delivery (MainDriver::ahead_begin, as launch_ahead).
+void launch_ahead_json(MainDriver& d, int dst_dt, double pad, int64_t pad_to, int64_t pad_multiple, bool want_mask,
+                       c10::DeviceIndex dev) {
+  std::vector<int64_t> rows;
+  for (int q = 0; q < 3; ++q) {
+    {
+      py::gil_scoped_release nogil;
+      d.ahead_begin(&rows);
+    }
+    if (rows.empty()) return;
+    const int n = int(rows.size());
+    int64_t ms[kMaxGroup], Ls[kMaxGroup];
+    for (int k = 0; k < n; ++k) {
+      ms[k] = rows[size_t(k)];
+      Ls[k] = padded_len(d.ahead_member(size_t(k)), pad_to, pad_multiple);
+    }
+    std::shared_ptr<VarlenOut> o[kMaxGroup];
+    alloc_json_group(d, ms, Ls, n, dst_dt, want_mask, dev, o);
+    void* outs[kMaxGroup];
+    int64_t* lens[kMaxGroup];
+    uint8_t* masks[kMaxGroup];
+    std::vector<std::shared_ptr<void>> handles;
+    handles.reserve(size_t(n));
+    for (int k = 0; k < n; ++k) {
+      outs[k] = o[k]->out.data_ptr();
+      lens[k] = o[k]->lengths.data_ptr<int64_t>();
+      masks[k] = want_mask ? static_cast<uint8_t*>(o[k]->mask.data_ptr()) : nullptr;
+      handles.emplace_back(std::move(o[k]));
+    }
+    py::gil_scoped_release nogil;
+    d.ahead_launch_json(dst_dt, pad, outs, Ls, lens, masks, std::move(handles));
+  }
+}
+
 // One fixed-width step: finish + commit the previous batch, take the next one, collate it
 // (coalesced with staged ones when cfg.grouped) into a tensor on the current stream.
 py::tuple step_once(MainDriver& d, const MainDriver::FastConfig& cfg) {
@@ -225,10 +299,37 @@ void register_torch_step(py::module_& m) {
           py::gil_scoped_release nogil;
           if (v.pre_stream != stream) d.wait_group(v, stream);
           d.deliver(v);
+        } else if (v.kind == uint32_t(tk::kPackJsonSpan)) {
+          // parsed from the logs by one launch with the staged JSON batches behind it
+          const int ng = 1 + int(extra);
+          int64_t ms[kMaxGroup], Ls[kMaxGroup];
+          for (int k = 0; k < ng; ++k) {
+            const SlotView& s = k == 0 ? v : d.group_member(size_t(k - 1));
+            ms[k] = int64_t(s.n_rows);
+            Ls[k] = padded_len(s, pad_to, pad_multiple);
+          }
+          std::shared_ptr<VarlenOut> o[kMaxGroup];
+          alloc_json_group(d, ms, Ls, ng, dst_dt, want_mask, dev, o);
+          void* outs[kMaxGroup];
+          int64_t* lens[kMaxGroup];
+          uint8_t* masks[kMaxGroup];
+          std::vector<std::shared_ptr<void>> handles;
+          handles.reserve(extra);
+          for (int k = 0; k < ng; ++k) {
+            outs[k] = o[k]->out.data_ptr();
+            lens[k] = o[k]->lengths.data_ptr<int64_t>();
+            masks[k] = want_mask ? static_cast<uint8_t*>(o[k]->mask.data_ptr()) : nullptr;
+          }
+          out = o[0]->out;
+          lengths = o[0]->lengths;
+          mask = o[0]->mask;
+          for (int k = 1; k < ng; ++k) handles.emplace_back(std::move(o[k]));
+          py::gil_scoped_release nogil;
+          d.json_group_launch(stream, dst_dt, pad, outs, Ls, lens, masks, std::move(handles));
+          d.deliver(v);
         } else {
           auto alloc = [&](const SlotView& s, VarlenOut* o, int64_t* Lout) {
-            int64_t L = pad_to >= 0 ? pad_to : s.max_row_len;
-            if (pad_to < 0 && pad_multiple > 1) L = (L + pad_multiple - 1) / pad_multiple * pad_multiple;
+            const int64_t L = padded_len(s, pad_to, pad_multiple);
             const int64_t m = int64_t(s.n_rows);
             o->out = at::empty({m, L}, at::TensorOptions().dtype(scalar_type_of(dst_dt)).device(at::kCUDA, dev));
             o->lengths = at::empty({m}, at::TensorOptions().dtype(at::kLong).device(at::kCUDA, dev));
@@ -273,6 +374,8 @@ void register_torch_step(py::module_& m) {
             d.deliver(v);
           }
         }
+        if (v.kind == uint32_t(tk::kPackJsonSpan))
+          launch_ahead_json(d, dst_dt, pad, pad_to, pad_multiple, want_mask, dev);
         d.ph_launch_ns_ += tk::now_ns() - t2;
         ++d.ph_steps_;
         ++d.fast_batches_;

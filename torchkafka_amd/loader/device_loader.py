@@ -151,8 +151,10 @@ class _Run:
             if L.device.type == "cuda":
                 # only after the fork: workers never inherit an initialised HIP runtime state they would use
                 dev = L.device.index if L.device.index is not None else torch.cuda.current_device()
-                mode = hip().H2D_ZERO_COPY if L._resolve_h2d(self.ring.payload_capacity) in ("zerocopy", "direct") \
-                    else hip().H2D_DMA
+                # device decode with h2d='dma': the slots (row tables) are read zero-copy and the copy
+                # engines move the log bytes into an HBM mirror (enable_mirror below)
+                mode = hip().H2D_ZERO_COPY if (L._resolve_h2d(self.ring.payload_capacity) in ("zerocopy", "direct")
+                                               or L._mirror()) else hip().H2D_DMA
                 self.engine = hip().Engine(dev, self.ring.n_slots, self.ring.payload_capacity, L.copy_streams, mode)
                 if L.tuning.decode_streams is not None:  # before anything creates a decode stream
                     self.engine.set_decode_streams(int(L.tuning.decode_streams))
@@ -169,8 +171,10 @@ class _Run:
                 self.driver.set_coalesce_wait_us(L.coalesce_wait_us if L.coalesce > 1 else 0)
                 if L._direct():
                     self.driver.enable_direct()
-                if L._direct() or L._span():
+                if L._direct() or L._span() or L._json_span():
                     self.driver.pin_logs(L._rank_partitions())
+                if L._mirror():
+                    self.driver.enable_mirror(int(L.tuning.mirror_chunk_mib) << 20, int(L.tuning.mirror_chunks))
                 tun = L.tuning
                 if tun.ahead_depth is not None:
                     self.driver.set_ahead_depth(int(tun.ahead_depth))
@@ -504,7 +508,7 @@ class DeviceLoader:
     def _slots_per_worker(self) -> int:
         if self.slots_per_worker is not None:
             return self.slots_per_worker
-        if self._span():
+        if self._span() or self._json_span():
             # device-decode slots hold row positions only (a few KiB): a deep ring costs no pinned
             # memory and lets the workers run ahead while slots wait for their kernels
             return 16
@@ -526,6 +530,12 @@ class DeviceLoader:
             B = self.batch_size
             segs = 2 * B + 128 + (B * s.row_bytes) // (32 << 10)
             return (B * 8 + 255) // 256 * 256 + 32 * segs
+        if self._json_span():
+            # row table (16 B per row) + the float32 values of rows the workers parse themselves (not
+            # "simple": exponents, NaN, long tokens; a batch closes early if they do not fit) + the
+            # segments (one per RecordBatch touched, one per 128 KiB or 1024 rows, host-row groups)
+            B = self.batch_size
+            return (B * 16 + 255) // 256 * 256 + self.JSON_SPAN_HOST_VALUES_BYTES + 32 * (3 * B + 128)
         if s is not None and getattr(s, "kind", None) == 0 and not self._process_overridden():
             return self.batch_size * s.row_bytes
         return 16 << 20
@@ -533,7 +543,8 @@ class DeviceLoader:
     def _worker_cfg(self) -> dict:
         return {"batch_size": self.batch_size, "sharding": self.sharding, "rank": self.rank,
                 "world_size": self.world_size, "native": self.native, "base_seed": self.base_seed,
-                "gather": self._direct(), "json_device": self._json_device(), "span": self._span(),
+                "gather": self._direct(), "json_device": self._json_device(),
+                "span": self._span() or self._json_span(),
                 "process_overridden": self._process_overridden(), "commit_table": None,
                 "worker_spin_us": int(self.tuning.worker_spin_us), "in_process": False}
 
@@ -578,9 +589,27 @@ class DeviceLoader:
         s = self.schema
         ok = (self.device.type == "cuda" and self.native and getattr(s, "kind", None) == 0
               and self.h2d != "direct" and self._commit_target_url()[0] != "" and not self._process_overridden())
-        if self.decode == "device" and not ok:
+        if self.decode == "device" and not ok and getattr(s, "kind", None) != 2:  # JSON: _json_span()
             raise ValueError("decode='device' needs a CUDA device, a FixedWidth schema, native=True, h2d != 'direct' "
                              "and the synthetic broker (bootstrap_servers shm:// or file://) with a group_id")
+        return ok
+
+    #: slot room of a device-parsed JSON batch (decode='device') for the rows its worker parses itself
+    JSON_SPAN_HOST_VALUES_BYTES = 2 << 20
+
+    def _json_span(self) -> bool:
+        """decode='device' for JsonArray records parsed on the GPU (json_span.hip): the workers walk the
+        record headers and pre-scan each text where it lies (element count, "simple row" check) but
+        neither copy it nor CRC the batch; the kernel reads the texts straight out of the pinned
+        broker logs, verifies each RecordBatch's CRC32C and parses the rows.  'auto' takes it
+        whenever the device JSON parse applies and the synthetic broker is the source (shm:// or
+        file:// with a group_id); decode='host' keeps the workers framing + copying the text."""
+        if self.decode == "host" or not self._json_device():
+            return False
+        ok = self.h2d != "direct" and self._commit_target_url()[0] != ""
+        if self.decode == "device" and not ok:
+            raise ValueError("decode='device' needs the synthetic broker (bootstrap_servers shm:// or file://) "
+                             "with a group_id and h2d != 'direct'")
         return ok
 
     def _json_device(self) -> bool:
@@ -600,6 +629,12 @@ class DeviceLoader:
         if self.json_parse == "device" and not ok:
             raise ValueError("json_parse='device' needs a CUDA device, native=True and skip_bad=False")
         return ok
+
+    def _mirror(self) -> bool:
+        """h2d='dma' with device decode: log bytes reach HBM by hipMemcpyAsync (SDMA copy engines, in
+        mirror chunks of ``tuning.mirror_chunk_mib``) and the decode kernels read them there, instead
+        of reading the pinned logs over PCIe themselves (csrc/hip/log_mirror.h)."""
+        return self.h2d == "dma" and (self._span() or self._json_span())
 
     def _direct(self) -> bool:
         """h2d='direct': fixed-width rows gathered by the kernel straight from the pinned broker logs."""
@@ -1007,6 +1042,9 @@ class DeviceLoader:
         self.stats.polled += st.get("polled", 0)
         self.stats.log_bytes_registered = st.get("log_bytes_registered", 0)
         self.stats.log_register_ns = st.get("log_register_ns", 0)
+        self.stats.mirror_bytes += st.get("mirror_bytes_copied", 0)
+        self.stats.mirror_copies += st.get("mirror_copies", 0)
+        self.stats.mirror_fallbacks += st.get("mirror_fallbacks", 0)
         self.stats.commits += st["commits"]
         self.stats.commit_failures += st["commit_failures"]
         self.stats.commit_ns.extend(st["commit_ns"])

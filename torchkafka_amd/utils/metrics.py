@@ -52,6 +52,9 @@ class LoaderStats:
     polled: int = 0
     log_bytes_registered: int = 0  # h2d="direct": broker log bytes pinned in place so far
     log_register_ns: int = 0
+    mirror_bytes: int = 0     # h2d="dma" device decode: log bytes copied into the HBM mirror (SDMA)
+    mirror_copies: int = 0
+    mirror_fallbacks: int = 0  # segments read from the pinned log instead (buffer busy)
     started: float = field(default_factory=time.perf_counter)
     max_commit_samples: int = 100000
 
@@ -103,6 +106,9 @@ class LoaderStats:
             "native_poll_us_per_slot": self.poll_ns / 1e3 / max(self.polled, 1),
             "log_mib_pinned": self.log_bytes_registered / 2**20,
             "log_pin_ms": self.log_register_ns / 1e6,
+            "mirror_mib_copied": self.mirror_bytes / 2**20,
+            "mirror_copies": self.mirror_copies,
+            "mirror_fallbacks": self.mirror_fallbacks,
             "commits": self.commits,
             "commit_failures": self.commit_failures,
             "commit_p50_us": percentile(c_us, 50),
