@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--event-every", type=int, default=None)
     ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy", "direct"])
     ap.add_argument("--copy-streams", type=int, default=4)
+    ap.add_argument("--mirror-chunk-mib", type=int, default=8,
+                    help="--h2d dma with device decode: MiB per hipMemcpyAsync into the HBM log mirror")
     ap.add_argument("--lockstep-depth", type=int, default=2)
     ap.add_argument("--coalesce", type=int, default=8, help="staged batches collated per kernel launch")
     ap.add_argument("--coalesce-wait-us", type=int, default=50, help="adaptive coalescing wait while the GPU is busy")
@@ -141,6 +143,7 @@ def main() -> int:
         in_order=args.in_order, h2d=args.h2d, copy_streams=args.copy_streams, lockstep_depth=args.lockstep_depth,
         event_every=args.event_every, numa_bind=not args.no_numa, coalesce=args.coalesce,
         coalesce_wait_us=args.coalesce_wait_us, decode=args.decode, lockstep=lockstep,
+        mirror_chunk_mib=args.mirror_chunk_mib,
         worker_init_fn=Records.init_worker("bench", bootstrap_servers=url, group_id="bench",
                                            auto_offset_reset="earliest", check_crcs=not args.no_crc),
     )
@@ -265,7 +268,9 @@ def main() -> int:
                     "" if not lockstep or (lockstep is True and world == 1)
                     else ", lockstep (gloo all-reduce)" if use_gloo else ", RCCL lockstep"),
                 "h2d": loader._resolve_h2d(loader._slot_capacity()) if device.type == "cuda" else "n/a (cpu)",
-                "decode": "device (gfx950 CRC32C + decode from pinned logs)" if loader._span() else "host workers",
+                "decode": ("host workers" if not loader._span() else
+                           "device (gfx950 CRC32C + decode from an HBM mirror filled by SDMA copies)"
+                           if loader._mirror() else "device (gfx950 CRC32C + decode from pinned logs)"),
                 "bytes_per_step_per_gpu": B * args.dim * 4,
                 "gb_per_s": round(value * args.dim * 4 / 1e9, 3),
                 "commit_p99_us": round(stats["commit_p99_us"], 2),

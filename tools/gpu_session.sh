@@ -24,6 +24,9 @@ for s in ${STEPS:-pytest_new}; do
     benchdrv) run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     profc4) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/profc4" -o run -- python3 "$OLDPWD/benchmarks/config4_json_varlen.py" --steps 300 > "$OLDPWD/gpurun_out/profc4.log" 2>&1) || exit $?
             tail -5 gpurun_out/profc4.log ;;
+    dmasweep) for c in 2 4 16 32; do run bench_dma_c$c 300 python bench.py --stats --h2d dma --mirror-chunk-mib $c --steps 1000; done ;;
+    profdma) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/profdma" -o run -- python3 "$OLDPWD/bench.py" --h2d dma --steps 1000 --steady-steps 1000 > "$OLDPWD/gpurun_out/profdma.log" 2>&1) || exit $?
+            tail -3 gpurun_out/profdma.log ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   esac
 done

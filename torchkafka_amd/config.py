@@ -81,7 +81,7 @@ class Tuning:
         worker_spin_us: worker spin on a full sub-ring before sleeping (0..100000 us).
         mirror_chunk_mib: h2d='dma' with device decode: log bytes per hipMemcpyAsync into the HBM
             mirror of a partition log (1..1024 MiB).
-        mirror_chunks: HBM mirror buffers per partition (2..64).
+        mirror_chunks: HBM mirror buffers per partition (2..64); K - 2 of them are prefetched ahead.
     """
 
     slots_per_worker: Optional[int] = None
@@ -98,7 +98,7 @@ class Tuning:
     span_burst: Optional[int] = None
     worker_spin_us: Optional[int] = None
     mirror_chunk_mib: int = 8
-    mirror_chunks: int = 4
+    mirror_chunks: int = 6
 
     def __post_init__(self):
         # environment defaults for fields left at None

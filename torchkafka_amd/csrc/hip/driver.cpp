@@ -747,7 +747,7 @@ const uint8_t* MainDriver::seg_src(const tk::SpanSeg& sg) {
   if (mirror_) {
     // pin ahead of the segment so the mirror can copy (and prefetch) whole chunks
     const auto& part = broker_->part(sg.pidx);
-    ensure_log(sg.pidx, std::min<uint64_t>(part.log_capacity, sg.log_pos + 2 * mirror_->chunk_bytes()));
+    ensure_log(sg.pidx, std::min<uint64_t>(part.log_capacity, sg.log_pos + mirror_->span_bytes()));
     const uint64_t written = part.log_end_pos.load(std::memory_order_acquire);
     const uint8_t* m = mirror_->map(sg.pidx, sg.log_pos, sg.len, log, std::min<uint64_t>(reg_end_[sg.pidx], written));
     if (m) return m;

@@ -8,10 +8,11 @@
 // the model that trains on the batches.  A partition log is mirrored chunk by chunk: chunk c holds
 // log bytes [c * C, (c + 1) * C + kSpanSegMax) -- the overlap keeps every segment (<= kSpanSegMax)
 // that starts in chunk c whole in one buffer -- in one of K buffers per partition (c % K), copied
-// as one hipMemcpyAsync of what is written (plus the next chunk as a prefetch), topped up when the
-// log grows.  Ordering is all on the GPU: a decode stream waits for the copy stream's event before
-// its kernel, and a buffer is overwritten only after the copy stream waited for the events of
-// every decode stream that read its previous chunk.  A segment whose buffer is still in use by the
+// as one hipMemcpyAsync of what is written (plus the next K - 2 chunks as a prefetch, so the copy
+// engine always has work queued), topped up when the log grows.  Ordering is all on the GPU: a
+// decode stream waits for the copy stream's event before its kernel, and a buffer is
+// overwritten only after the copy stream waited for the events of every decode stream that read
+// its previous chunk.  A segment whose buffer is still in use by the
 // group being formed is served from the pinned log instead (map() returns nullptr).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -19,7 +20,11 @@
 #include <cstdint>
 #include <vector>
 
+#include "span.h"
+
 namespace tkh {
+
+inline constexpr uint64_t tk_seg_max() { return tk::kSpanSegMax; }
 
 class LogMirror {
  public:
@@ -38,6 +43,8 @@ class LogMirror {
   void after(hipStream_t stream);
 
   uint64_t chunk_bytes() const { return chunk_; }
+  // log bytes from a mapped position that the mirror may copy (the chunk and its prefetches)
+  uint64_t span_bytes() const { return chunk_ * uint64_t(prefetch_ + 1) + tk_seg_max(); }
   uint64_t bytes_copied() const { return bytes_; }
   uint64_t copies() const { return copies_; }
   uint64_t fallbacks() const { return fallbacks_; }
@@ -70,6 +77,7 @@ class LogMirror {
   int device_;
   uint64_t chunk_, stride_;
   int K_;
+  int prefetch_ = 1;  // chunks copied ahead of the one being read
   hipStream_t copy_ = nullptr;
   hipEvent_t copied_ = nullptr;      // recorded on copy_ after the latest copy (when a launch needs it)
   uint64_t copy_seq_ = 0, recorded_seq_ = 0, done_seq_ = 0;

@@ -158,6 +158,11 @@ class _Run:
                 self.engine = hip().Engine(dev, self.ring.n_slots, self.ring.payload_capacity, L.copy_streams, mode)
                 if L.tuning.decode_streams is not None:  # before anything creates a decode stream
                     self.engine.set_decode_streams(int(L.tuning.decode_streams))
+                elif L._lockstep_transport() == "rccl":
+                    # HIP gives a process 4 hardware queues: the user's stream, two decode streams and
+                    # the lockstep's RCCL stream each keep one, so a collective waiting for the other
+                    # ranks never sits in front of a decode kernel those ranks' progress depends on
+                    self.engine.set_decode_streams(2)
                 if L.numa_bind:
                     topology.check_device(dev)
                 url, group = L._commit_target_url()
@@ -667,14 +672,13 @@ class DeviceLoader:
         run = self._run = _Run(self)
         lock = None
         try:
-            want = self.lockstep and (self.world_size > 1 or self.lockstep == "always")
-            if want:
+            transport = self._lockstep_transport(process_group)
+            if transport is not None:
                 import torch.distributed as dist
 
                 if dist.is_available() and dist.is_initialized():
                     if run.driver is not None:
-                        backend = dist.get_backend(process_group)
-                        if self.lockstep == "rccl" or (backend == "nccl" and self.lockstep != "host"):
+                        if transport == "rccl":
                             run.rccl = self._make_rccl_lockstep(process_group)
                         else:
                             run.rccl = hip().PyLockstep(_host_allreduce_min(process_group))
@@ -748,6 +752,20 @@ class DeviceLoader:
         s = self.schema
         return (s is not None and getattr(s, "kind", None) == 0 and self.native and not self.return_info
                 and not self.drop_last and not self._process_overridden())
+
+    def _lockstep_transport(self, process_group=None):
+        """How ranks agree on every step: 'rccl' (native communicator, an nccl process group or
+        lockstep='rccl'), 'host' (the process group's all-reduce), or None (no lockstep)."""
+        if not (self.lockstep and (self.world_size > 1 or self.lockstep == "always")):
+            return None
+        import torch.distributed as dist
+
+        if not (dist.is_available() and dist.is_initialized()):
+            return None
+        if self.device.type != "cuda" or not self.native:
+            return "host"
+        backend = dist.get_backend(process_group)
+        return "rccl" if self.lockstep == "rccl" or (backend == "nccl" and self.lockstep != "host") else "host"
 
     def _make_rccl_lockstep(self, process_group):
         """Native RCCL communicator for the per-step lockstep (id broadcast through torch.distributed)."""
