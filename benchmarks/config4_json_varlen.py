@@ -58,8 +58,8 @@ def main():
         b.fill("json", per_part, "json_f32", size=args.min_len, max_size=args.max_len, threads=args.partitions)
         fill_s = time.perf_counter() - t
         dl = DeviceLoader(Json.placeholder(), B, num_workers=args.workers, device=args.device, dtype=torch.bfloat16,
-                          json_parse=args.json_parse, h2d=args.h2d, decode=args.decode, slots_per_worker=args.slots_per_worker,
-                          event_every=args.event_every, prefetch=args.prefetch,
+                          json_parse=args.json_parse, h2d=args.h2d, decode=args.decode,
+                          slots_per_worker=args.slots_per_worker, event_every=args.event_every, prefetch=args.prefetch,
                           worker_init_fn=Json.init_worker("json", bootstrap_servers=url, group_id="cfg4",
                                                           auto_offset_reset="earliest"))
         it = iter(auto_commit(dl))
@@ -83,7 +83,8 @@ def main():
         print(json.dumps({"config": 4, "metric": "JSON records/s to GPU (bf16 padded), per-batch commit",
                           "value": round(rows / el), "ms_per_step": round(el / args.steps * 1e3, 4),
                           "batch_size": B, "json_parse": args.json_parse, "h2d": args.h2d,
-                          "decode": "device (json_span.hip from the pinned logs)" if dl._json_span() else args.decode,
+                          "decode": ("device (json_span.hip from the pinned logs)" if dl._json_span()
+                                     else args.decode),
                           "timed_s": round(el, 4), "steps": args.steps,
                           "avg_record_bytes": round(text_bytes),
                           "last_batch_shape": list(x.shape),

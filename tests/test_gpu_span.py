@@ -227,3 +227,26 @@ def test_device_decode_through_hbm_mirror(broker, chunk_mib, chunks, rpb, size):
     assert broker.committed_offsets("gm", "t") == {0: n, 1: n, 2: n}
     st = dl.stats_summary()
     assert st["mirror_copies"] > 0 and st["mirror_mib_copied"] > 0
+
+
+def test_device_decode_generic_driver_path(broker):
+    """return_info=True takes the driver's generic per-batch path: device-decoded batches arrive
+    there too (KafkaBatch with watermarks), bit-exact with the host path."""
+    from torchkafka_amd import FixedWidth
+
+    broker.create_topic("t", 2)
+    _produce_random(broker, "t", 2, 150, 64 * 4, rpb=10)
+    DS = _dataset(FixedWidth(torch.float32, (64,)))
+    from torchkafka_amd import DeviceLoader, auto_commit
+
+    outs = {}
+    for decode in ("host", "device"):
+        dl = DeviceLoader(DS.placeholder(), 32, num_workers=1, device="cuda:0", decode=decode, return_info=True,
+                          in_order=True, dtype=torch.bfloat16,
+                          worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id=f"g{decode}",
+                                                        auto_offset_reset="earliest", consumer_timeout_ms=300))
+        bs = [b for b in auto_commit(dl)]
+        assert all(b.watermarks for b in bs)
+        outs[decode] = torch.cat([b.data.clone() for b in bs])
+        assert broker.committed_offsets(f"g{decode}", "t") == {0: 150, 1: 150}
+    assert torch.equal(_bits(outs["host"]), _bits(outs["device"]))

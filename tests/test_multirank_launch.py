@@ -48,9 +48,20 @@ def test_bench_two_ranks_gloo_cpu():
     assert out["value"] > 0 and out["steady_state"]["records_per_s"] > 0
 
 
+def _rank_lines(out: str) -> list:
+    """Every '{"rank": ...}' object the ranks printed (their lines may interleave on one line)."""
+    dec = json.JSONDecoder()
+    found, i = [], out.find('{"rank"')
+    while i >= 0:
+        obj, end = dec.raw_decode(out, i)
+        found.append(obj)
+        i = out.find('{"rank"', end)
+    return found
+
+
 @pytest.mark.gpu
 def test_native_lockstep_two_ranks_one_gpu():
     r = _torchrun(2, "tools/lockstep_check.py", timeout=200)
     assert r.returncode == 0, r.stdout[-4000:]
-    oks = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"rank"')]
+    oks = _rank_lines(r.stdout)
     assert len(oks) == 2 and all(o["ok"] for o in oks), r.stdout[-4000:]

@@ -27,6 +27,13 @@ for s in ${STEPS:-pytest_new}; do
     dmasweep) for c in 2 4 16 32; do run bench_dma_c$c 300 python bench.py --stats --h2d dma --mirror-chunk-mib $c --steps 1000; done ;;
     profdma) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/profdma" -o run -- python3 "$OLDPWD/bench.py" --h2d dma --steps 1000 --steady-steps 1000 > "$OLDPWD/gpurun_out/profdma.log" 2>&1) || exit $?
             tail -3 gpurun_out/profdma.log ;;
+    config5) run config5 300 python benchmarks/config5_large_messages.py ;;
+    bench2r) run bench_2rank_gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29641 bench.py --gpus 2 --same-device --steps 2000 --warmup 200 --stats ;;
+    benchf32) run bench_f32 300 python bench.py --stats --dtype f32 ;;
+    benchhost) run bench_host 300 python bench.py --stats --decode host ;;
+    benchlockr) run bench_lock_rccl 300 python bench.py --lockstep rccl --stats ;;
+    profbench) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/profbench" -o run -- python3 "$OLDPWD/bench.py" --steps 1000 --steady-steps 2000 > "$OLDPWD/gpurun_out/profbench.log" 2>&1) || exit $?
+            tail -2 gpurun_out/profbench.log ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   esac
 done

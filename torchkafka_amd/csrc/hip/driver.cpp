@@ -493,6 +493,24 @@ void MainDriver::collate_fixed(const SlotView& v, hipStream_t stream, int dst_dt
 void MainDriver::collate_varlen(const SlotView& v, hipStream_t stream, int dst_dt, void* out, int64_t L, double pad,
                                 int64_t* lengths, uint8_t* mask) {
   bool record;
+  if (v.kind == tk::kPackJsonSpan) {
+    // parsed from the logs (stage + parse kernels) on the user's stream, its own completion event
+    if (stream != last_stream_) {
+      cover_handed();
+      last_stream_ = stream;
+    }
+    const int slot = int(v.g);
+    const SlotView* vs[1] = {&v};
+    void* outs[1] = {out};
+    const int64_t Ls[1] = {L};
+    int64_t* lens[1] = {lengths};
+    uint8_t* masks[1] = {mask};
+    int64_t pe;
+    launch_json_span(&slot, vs, 1, stream, dst_dt, pad, outs, Ls, lens, masks, true, &pe);
+    span_group_handed(&slot, 1, stream, &pe, {}, 1);
+    last_perr_ = pe;
+    return;
+  }
   if (v.kind == tk::kPackJsonText) {
     const int64_t idx = next_err_word();
     note_handed(v.g, stream, &record);

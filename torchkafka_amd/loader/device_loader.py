@@ -28,6 +28,7 @@ whatever the prefetch depth and whichever worker produced the batch (D5).
 """
 from __future__ import annotations
 
+import gc
 import logging
 import multiprocessing as mp
 import os
@@ -141,13 +142,25 @@ class _Run:
                 t = _PackerThread(self.ring, self.name, L.dataset, cfg)
                 t.start()
                 self.procs.append(t)
-            for w in range(L.num_workers):
-                p = ctx.Process(target=worker_main,
-                                args=(self.ring if pass_ring else None, self.name, w, L.num_workers, L.dataset,
-                                      L.worker_init_fn, cfg),
-                                daemon=True, name=f"torchkafka-worker-{w}")
-                p.start()
-                self.procs.append(p)
+            # A forked child must never run the finalizers of the parent's objects: when this process
+            # already initialised HIP (a second epoch, a test session), a garbage CUDA tensor
+            # collected in the child calls into a runtime that does not exist there (SIGSEGV right
+            # after the fork, measured).  Collect now and freeze what is left out of the child's GC.
+            frozen = pass_ring and L.num_workers > 0
+            if frozen:
+                gc.collect()
+                gc.freeze()
+            try:
+                for w in range(L.num_workers):
+                    p = ctx.Process(target=worker_main,
+                                    args=(self.ring if pass_ring else None, self.name, w, L.num_workers,
+                                          L.dataset, L.worker_init_fn, cfg),
+                                    daemon=True, name=f"torchkafka-worker-{w}")
+                    p.start()
+                    self.procs.append(p)
+            finally:
+                if frozen:
+                    gc.unfreeze()
             if L.device.type == "cuda":
                 # only after the fork: workers never inherit an initialised HIP runtime state they would use
                 dev = L.device.index if L.device.index is not None else torch.cuda.current_device()
@@ -1137,7 +1150,8 @@ class DeviceLoader:
         dev = self.device
         stream = _stream_ptr(dev)
         lengths = mask = None
-        fixed = kind == core().PACK_FIXED
+        # device-decode and log-gather slots are fixed-width batches too (MainDriver.collate_fixed)
+        fixed = kind in (core().PACK_FIXED, core().PACK_RECORD_SPAN, core().PACK_GATHER_FIXED)
         if fixed:
             if not shape:
                 shape = tuple(self.schema.shape)
