@@ -18,6 +18,7 @@ for s in ${STEPS:-pytest_new}; do
     pytest_all) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     config4) run config4 300 python benchmarks/config4_json_varlen.py ;;
     config4host) run config4_hostdecode 300 python benchmarks/config4_json_varlen.py --decode host ;;
+    config4w) for w in 6 8; do run config4_w$w 300 python benchmarks/config4_json_varlen.py --workers $w; done ;;
     config4dma) run config4_dma 300 python benchmarks/config4_json_varlen.py --h2d dma ;;
     bench) run bench 300 python bench.py --stats ;;
     benchdma) run bench_dma 300 python bench.py --stats --h2d dma ;;
