@@ -41,6 +41,7 @@ for s in ${STEPS:-pytest_new}; do
              tail -2 gpurun_out/pmc_jspan.log ;;
     pmcfetch) (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE WRITE_SIZE SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d "$OLDPWD/gpurun_out/pmc_fetch_span" -o run -- python3 "$OLDPWD/bench.py" --steps 200 --warmup 20 --steady-steps 0 --h2d dma > "$OLDPWD/gpurun_out/pmc_fetch_span.log" 2>&1) || exit $?
              tail -2 gpurun_out/pmc_fetch_span.log ;;
+    aheaddrv) for a in 1 2 3 4 6; do TORCHKAFKA_AHEAD_DEPTH=$a run bench_drv_ahead$a 300 python bench.py --gpus 1 --steps 20 --warmup 5; done ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   esac
 done

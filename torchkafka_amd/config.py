@@ -82,6 +82,8 @@ class Tuning:
         mirror_chunk_mib: h2d='dma' with device decode: log bytes per hipMemcpyAsync into the HBM
             mirror of a partition log (1..1024 MiB).
         mirror_chunks: HBM mirror buffers per partition (2..64); K - 2 of them are prefetched ahead.
+        group_mib: device-decode groups stop growing at this many MiB of log bytes (1..1024): a
+            group's batches become committable together, so large batches form small groups.
     """
 
     slots_per_worker: Optional[int] = None
@@ -99,6 +101,7 @@ class Tuning:
     worker_spin_us: Optional[int] = None
     mirror_chunk_mib: int = 8
     mirror_chunks: int = 6
+    group_mib: int = 16
 
     def __post_init__(self):
         # environment defaults for fields left at None
@@ -127,6 +130,7 @@ class Tuning:
         _check(0 <= int(self.worker_spin_us) <= 100_000, "worker_spin_us must be in [0, 100000]")
         _check(1 <= int(self.mirror_chunk_mib) <= 1024, "mirror_chunk_mib must be in [1, 1024]")
         _check(2 <= int(self.mirror_chunks) <= 64, "mirror_chunks must be in [2, 64]")
+        _check(1 <= int(self.group_mib) <= 1024, "group_mib must be in [1, 1024]")
 
 
 _CHOICES = {

@@ -691,6 +691,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
 
   const bool fixed = spec.kind == kPackFixed;
   const bool json_text = spec.kind == kPackJsonText;
+  f.set_sparse_touch(span && uint64_t(spec.row_elems) * uint64_t(spec.elem_size) >= (16u << 10));
   JsonRowDesc* jrows = nullptr;
   JsonSpanRow* srows = nullptr;
   const uint64_t row_bytes = fixed ? uint64_t(spec.row_elems) * uint64_t(spec.elem_size) : 0;

@@ -301,6 +301,7 @@ PYBIND11_MODULE(_tkhip, m) {
       .def("enable_mirror", &MainDriver::enable_mirror, py::arg("chunk_bytes"), py::arg("chunks_per_partition"))
       .def("set_ahead_depth", &MainDriver::set_ahead_depth)
       .def("set_span_burst", &MainDriver::set_span_burst)
+      .def("set_group_bytes", &MainDriver::set_group_bytes)
       .def("set_worker_sink", &MainDriver::set_worker_sink, py::arg("table"), py::arg("n_workers"),
            py::arg("capacity"))
       .def(

@@ -242,6 +242,7 @@ int MainDriver::poll_one_impl(bool block, int64_t timeout_ms) {
       const auto* sg = reinterpret_cast<const tk::SpanSeg*>(ring_->payload(uint32_t(g)) + h->values_offset);
       for (uint32_t i = 0; i < h->n_segs; ++i) {
         if (sg[i].flags & tk::kSegHostRows) continue;  // worker-parsed rows: no log bytes
+        v.span_bytes += sg[i].len;
         const uint64_t cap = broker_->part(sg[i].pidx).log_capacity;
         ensure_log(sg[i].pidx, std::min<uint64_t>(sg[i].log_pos + sg[i].len + 16, cap));
       }
@@ -843,10 +844,12 @@ size_t MainDriver::json_group_extend() {
   group_idx_.clear();
   if (coalesce_ <= 1 || (last.kind != uint32_t(tk::kPackJsonText) && last.kind != uint32_t(tk::kPackJsonSpan)))
     return 0;
+  uint64_t bytes = last.span_bytes;
   for (size_t i = 0; i < staged_.size() && int(1 + group_idx_.size()) < coalesce_; ++i) {
     const SlotView& v = staged_[i];
     if (v.g < 0) continue;  // watermark-only slot: rides on the next delivered batch
-    if (v.pre || v.kind != last.kind || v.n_rows == 0) break;
+    if (v.pre || v.kind != last.kind || v.n_rows == 0 || group_full(bytes, v)) break;
+    bytes += v.span_bytes;
     group_idx_.push_back(i);
   }
   return group_idx_.size();
@@ -1167,11 +1170,12 @@ int64_t MainDriver::step_group_begin(hipStream_t stream, bool auto_commit, int64
   group_rows->push_back(last.n_rows);
   if (last.kind == uint32_t(tk::kPackFixed) || last.kind == uint32_t(tk::kPackGatherFixed) ||
       last.kind == uint32_t(tk::kPackRecordSpan)) {
+    group_capped_ = false;
     extend_group();
-    if (coalesce_wait_ns_ > 0 && int(1 + group_idx_.size()) < coalesce_) {
+    if (coalesce_wait_ns_ > 0 && int(1 + group_idx_.size()) < coalesce_ && !group_capped_) {
       const int64_t cw0 = tk::now_ns();
       const int64_t until = cw0 + coalesce_wait_ns_;
-      while (int(1 + group_idx_.size()) < coalesce_ && gpu_busy() && tk::now_ns() < until) {
+      while (int(1 + group_idx_.size()) < coalesce_ && !group_capped_ && gpu_busy() && tk::now_ns() < until) {
         const int r2 = poll_one(false, 0);
         if (r2 == -3) break;  // reported by the next call
         if (r2 == 1) {
@@ -1210,16 +1214,23 @@ void MainDriver::ahead_begin(std::vector<int64_t>* rows) {
   const SlotView& f = staged_[i0];
   const bool json = f.kind == uint32_t(tk::kPackJsonSpan);  // outputs sized per batch: no shape match needed
   if ((f.kind != uint32_t(tk::kPackRecordSpan) && !json) || f.n_rows == 0) return;
+  uint64_t bytes = 0;
+  bool capped = false;
   for (size_t i = i0; i < staged_.size() && int(group_idx_.size()) < coalesce_; ++i) {
     const SlotView& v = staged_[i];
     if (v.g < 0) continue;  // watermark-only slot: rides on the next delivered batch
     if (v.pre || v.kind != f.kind || v.n_rows == 0) break;
+    if (group_full(bytes, v)) {
+      capped = true;  // a full group by bytes
+      break;
+    }
+    bytes += v.span_bytes;
     if (!json && (v.src_dtype != f.src_dtype || v.max_row_len != f.max_row_len || v.row_bytes != f.row_bytes ||
                   v.shape != f.shape))
       break;
     group_idx_.push_back(i);
   }
-  if (int(group_idx_.size()) < coalesce_) {  // only full groups go ahead; the rest waits for the user
+  if (int(group_idx_.size()) < coalesce_ && !capped) {  // only full groups go ahead; the rest waits for the user
     group_idx_.clear();
     return;
   }
@@ -1289,12 +1300,16 @@ void MainDriver::ahead_launch_json(int dst_dt, double pad, void* const* outs, co
 // Appends to group_idx_ the staged batches right behind `last` that one kernel can collate with it.
 void MainDriver::extend_group() {
   size_t i = group_idx_.empty() ? 0 : group_idx_.back() + 1;
+  uint64_t bytes = last.span_bytes;
+  for (size_t k : group_idx_) bytes += staged_[k].span_bytes;
   for (; i < staged_.size() && int(1 + group_idx_.size()) < coalesce_; ++i) {
     const SlotView& v = staged_[i];
     if (v.g < 0) continue;  // watermark-only slot: rides on the next delivered batch
+    if (group_full(bytes, v)) group_capped_ = true;
     if (v.pre || v.kind != last.kind || v.src_dtype != last.src_dtype || v.max_row_len != last.max_row_len ||
-        v.row_bytes != last.row_bytes || v.shape != last.shape || v.n_rows == 0)
+        v.row_bytes != last.row_bytes || v.shape != last.shape || v.n_rows == 0 || group_capped_)
       return;
+    bytes += v.span_bytes;
     group_idx_.push_back(i);
   }
 }

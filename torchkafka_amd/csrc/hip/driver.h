@@ -37,6 +37,7 @@ struct SlotView {
   int32_t src_dtype = -1;
   uint32_t n_segs = 0;                // kPackRecordSpan / kPackJsonSpan: SpanSeg entries at values_offset
   int32_t trunc_len = -1;             // kPackJsonSpan: rows keep at most this many elements (-1: all)
+  uint64_t span_bytes = 0;            // device decode: log bytes its segments read
   std::vector<int64_t> shape;
   std::vector<tk::Watermark> wms;
   // coalesced fast path: collated ahead of delivery by a group launch
@@ -152,6 +153,15 @@ class MainDriver {
   // The stream the next device-decode group launch runs on (its outputs are allocated there).
   hipStream_t next_decode_stream() { return eng_->decode_stream(int(span_launches_ % 4096)); }
   void set_coalesce(int n) { coalesce_ = n < 1 ? 1 : (n > kMaxGroup ? kMaxGroup : n); }
+  // Device-decode groups stop growing at this many log bytes: a group's batches become committable
+  // together when its kernel completes, so 8 x 8 MiB batches (config 5) would hold every commit for
+  // a 64 MiB transfer (~1.3 ms); small batches still group 8 at a time.
+  void set_group_bytes(uint64_t b) { group_bytes_max_ = b < (1u << 20) ? (1u << 20) : b; }
+  uint64_t group_bytes_max_ = uint64_t(16) << 20;
+  bool group_capped_ = false;  // extend_group stopped at group_bytes_max_
+  bool group_full(uint64_t bytes, const SlotView& next) const {
+    return next.span_bytes > 0 && bytes > 0 && bytes + next.span_bytes > group_bytes_max_;
+  }
   // Adaptive coalescing: while the GPU is still running an earlier launch, wait up to `us` for
   // more staged batches so the next launch carries a full group (0 disables).  Waiting costs no
   // GPU time -- the GPU is busy anyway -- and a zero-copy batch costs 7.1 us alone but 5.2 us

@@ -198,6 +198,7 @@ class _Run:
                     self.driver.set_ahead_depth(int(tun.ahead_depth))
                 if tun.span_burst is not None:
                     self.driver.set_span_burst(int(tun.span_burst))
+                self.driver.set_group_bytes(int(tun.group_mib) << 20)
         except BaseException:
             self.close()
             raise
