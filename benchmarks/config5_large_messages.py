@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """BASELINE config 5 (stress): 1 MiB messages, 128 partitions, pinned ring, p99 commit latency.
 
-Each record is 262,144 float32 (1 MiB); batches of ``--batch-size`` records are packed by
-the workers into pinned ring slots (``slots_per_worker`` deep: 2 = double-buffered),
-copied by hipMemcpyAsync on side streams, cast to bf16 on device, and committed after
-use.  Reports records/s, GB/s and the commit latency distribution (p50/p99) measured
+Each record is 262,144 float32 (1 MiB); batches of ``--batch-size`` records are described by
+the workers in pinned ring slots (``slots_per_worker`` deep: 2 = double-buffered) and decoded
+on the device straight from the pinned logs (CRC32C + cast to bf16, span_decode.hip), then
+committed after use.  Reports records/s, GB/s and the commit latency distribution (p50/p99) measured
 around every commit.  Reference yardstick: 3,481 records/s (3.40 GiB/s)
 at batch 8 with 4 workers, CPU only.
 
@@ -27,7 +27,11 @@ def main():
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch-size", type=int, default=8)
-    ap.add_argument("--workers", type=int, default=8)
+    # Device decode leaves the workers only the record headers (~25-33 us per 8 MiB batch), so the ring
+    # depth sets the commit latency (Little's law: in-flight bytes / link rate): 2 workers x 2 slots
+    # 51.3 k rec/s, latency p99 0.78 ms; 4 workers 45.4 k, 1.6 ms; 8 workers 45.8 k, 3.0 ms
+    # (profiles/r02_s3_final/config5_w*.log)
+    ap.add_argument("--workers", type=int, default=2)
     ap.add_argument("--partitions", type=int, default=128)
     ap.add_argument("--slots-per-worker", type=int, default=2)
     ap.add_argument("--device", default="cuda:0")

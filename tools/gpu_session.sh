@@ -29,6 +29,7 @@ for s in ${STEPS:-pytest_new}; do
     profdma) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/profdma" -o run -- python3 "$OLDPWD/bench.py" --h2d dma --steps 1000 --steady-steps 1000 > "$OLDPWD/gpurun_out/profdma.log" 2>&1) || exit $?
             tail -3 gpurun_out/profdma.log ;;
     config5) run config5 300 python benchmarks/config5_large_messages.py ;;
+    config5w) for w in 2 4; do run config5_w$w 300 python benchmarks/config5_large_messages.py --workers $w; done ;;
     bench2r) run bench_2rank_gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29641 bench.py --gpus 2 --same-device --steps 2000 --warmup 200 --stats ;;
     benchf32) run bench_f32 300 python bench.py --stats --dtype f32 ;;
     benchhost) run bench_host 300 python bench.py --stats --decode host ;;
