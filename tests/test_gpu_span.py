@@ -250,3 +250,54 @@ def test_device_decode_generic_driver_path(broker):
         outs[decode] = torch.cat([b.data.clone() for b in bs])
         assert broker.committed_offsets(f"g{decode}", "t") == {0: 150, 1: 150}
     assert torch.equal(_bits(outs["host"]), _bits(outs["device"]))
+
+
+@pytest.mark.parametrize("src,dst,lens,nulls,long_every,opts", [
+    (torch.int32, torch.int64, (0, 300), 0, 0, {}),                                   # token ids
+    (torch.int32, torch.int32, (1, 60), 7, 11, {"return_mask": True, "pad_value": -1}),  # worker-copied long rows
+    (torch.uint8, torch.float16, (0, 90), 0, 0, {"pad_to": 128}),
+    (torch.float16, torch.bfloat16, (0, 40), 5, 0, {"pad_multiple": 16}),  # 2-byte elements, any bits
+])
+def test_var_span_matches_host_path(broker, src, dst, lens, nulls, long_every, opts):
+    """VarLen records decoded on the device from the logs (varlen_span_kernel) == the host CSR
+    pack + varlen collate kernel, bit for bit (lengths, padding and masks included)."""
+    import struct
+
+    from torchkafka_amd import DeviceLoader, VarLen, auto_commit
+    from torchkafka_amd.ops.native import core
+
+    esize = torch.empty((), dtype=src).element_size()
+    fmt = {1: "B", 2: "H", 4: "i"}[esize]
+    rng = random.Random(esize * 7 + lens[1])
+    broker.create_topic("v", 2)
+    for p in range(2):
+        vals = []
+        for i in range(180):
+            if nulls and i % nulls == 3:
+                vals.append(None)
+                continue
+            k = rng.randint(*lens)
+            if long_every and i % long_every == 2:
+                k = core().VAR_SPAN_ROW_MAX // esize + rng.randint(1, 300)
+            lo, hi = (0, (1 << (8 * esize)) - 1) if fmt in "BH" else (-(1 << 31), (1 << 31) - 1)
+            vals.append(struct.pack(f"<{k}{fmt}", *[rng.randint(lo, hi) for _ in range(k)]))
+        for i in range(0, len(vals), 13):
+            broker.produce("v", vals[i:i + 13], partition=p)
+    DS = _dataset(VarLen(src))
+    outs = {}
+    for decode in ("host", "device"):
+        dl = DeviceLoader(DS.placeholder(), 32, num_workers=2, device="cuda:0", decode=decode, dtype=dst,
+                          in_order=True, coalesce=4,
+                          worker_init_fn=DS.init_worker("v", bootstrap_servers=broker.url, group_id=f"g{decode}",
+                                                        auto_offset_reset="earliest", consumer_timeout_ms=300),
+                          **opts)
+        assert dl._var_span() == (decode == "device")
+        outs[decode] = [tuple(t.clone() for t in b) for b in auto_commit(dl)]
+        assert broker.committed_offsets(f"g{decode}", "v") == {0: 180, 1: 180}
+    a, b = outs["host"], outs["device"]
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        assert len(x) == len(y)
+        for u, v in zip(x, y):
+            assert u.shape == v.shape and u.dtype == v.dtype
+            assert torch.equal(_bits(u) if u.is_floating_point() else u, _bits(v) if v.is_floating_point() else v)

@@ -1,4 +1,4 @@
-"""Device JSON-parse slots (kPackJsonSpan, csrc/core/span.h) on the CPU.
+"""Device JSON-parse and var-len slots (kPackJsonSpan / kPackVarSpan, csrc/core/span.h) on the CPU.
 
 The gfx950 kernel is checked on the GPU (tests/test_gpu_json_span.py).  Here a worker's JSON span
 fill must describe exactly the rows the host packer (PACK_JSON_F32: the worker parses every
@@ -6,6 +6,8 @@ number) takes -- same watermarks, same row count, same element counts, texts at 
 positions that ``json.loads`` to the host-parsed values, worker-parsed rows for the texts that
 are not "simple" -- and its segments must keep every row text whole, cover every CRC-verified
 RecordBatch to its end, and chain to the header CRC.
+The same holds for VarLen rows (token ids etc.): the span fill must describe exactly the rows of
+the host CSR packer, values at the recorded positions, long values copied by the worker.
 Reference: ``json.loads(record.value)`` in ``_process`` (README.md:54,74), kafka_dataset.py:156-162.
 """
 import json
@@ -174,3 +176,108 @@ def test_json_span_without_crc_checks_covers_only_texts(broker):
     for sr, si, _sw, sp, segs in span:
         assert sr and all(s[3] == 0 for s in segs)
         _decode_jspan(broker, si, sp, segs, -1)
+
+
+# ------------------------------------------------------------------ kPackVarSpan (VarLen)
+def _var_values(rnd, n, lo, hi, esize=4, nulls_every=0, long_every=0):
+    import struct
+    out = []
+    for i in range(n):
+        if nulls_every and i % nulls_every == 3:
+            out.append(None)
+            continue
+        k = rnd.randint(lo, hi)
+        if long_every and i % long_every == 2:
+            k = (core().VAR_SPAN_ROW_MAX // esize) + rnd.randint(1, 500)  # longer than a segment: worker copy
+        fmt = {1: "B", 2: "h", 4: "i", 8: "q"}[esize]
+        lim = (1 << (8 * esize - 1)) - 1 if esize > 1 else 255
+        out.append(struct.pack(f"<{k}{fmt}", *[rnd.randint(0 if esize == 1 else -lim, lim) for _ in range(k)]))
+    return out
+
+
+def _fill_var(broker, vspan, bs, values, rpb, esize, *, min_len=0, max_len=-1, truncate=True, slots=8):
+    c = core()
+    topic = f"v{random.randrange(1 << 30)}"
+    broker.create_topic(topic, len(values))
+    for p, vals in enumerate(values):
+        for i in range(0, len(vals), rpb):
+            broker.produce(topic, vals[i:i + rpb], partition=p)
+    t0 = broker.topic(topic)[2]
+    ring = c.Ring.create(f"/tkvspan-{os.getpid()}-{random.randrange(1 << 30)}", 1, 2, 32 << 20)
+    f = c.Fetcher(broker.native, True)
+    f.assign(list(range(t0, t0 + len(values))), [0] * len(values))
+    out = []
+    try:
+        for i in range(slots):
+            g = i % 2
+            assert ring.worker_acquire(0, g, 1000)
+            rows, _sc, timed_out, _sh = f.fill_slot(ring, g, c.PACK_VARLEN, esize, 0, min_len, max_len, truncate,
+                                                    False, bs, 50, False, vspan)
+            info = ring.slot_info(g)
+            pay = bytes(ring.payload_view(g)[:info["payload_bytes"]])
+            out.append((rows, info, [(p - t0, a, b, n) for p, a, b, n in ring.watermarks(g)], pay,
+                        ring.span_segments(g)))
+            ring.worker_publish(g)
+            assert ring.main_acquire(100) == g
+            ring.main_release(g)
+            if timed_out:
+                break
+    finally:
+        ring.shutdown()
+        ring.unlink()
+    return out
+
+
+def _decode_var(broker, info, pay, segs, esize, trunc):
+    c = core()
+    dt = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[esize]
+    n = info["n_rows"]
+    tab = np.frombuffer(pay[:16 * n], dtype=np.dtype([("pos", "<u8"), ("tlen", "<i4"), ("count", "<i4")]))
+    got = [None] * n
+    for pos, ln, pidx, flags, _crc, r0, r1 in segs:
+        if flags & c.SEG_HOST_ROWS:
+            for r in range(r0, r1):
+                assert tab[r]["tlen"] < 0
+                k = int(tab[r]["count"]) if trunc < 0 else min(int(tab[r]["count"]), trunc)
+                got[r] = np.frombuffer(pay[int(tab[r]["pos"]):int(tab[r]["pos"]) + k * esize], dtype=dt)
+            continue
+        data = broker.native.read_log(pidx, pos, ln)
+        for r in range(r0, r1):
+            if tab[r]["tlen"] < 0:
+                continue
+            p0, tl = int(tab[r]["pos"]), int(tab[r]["tlen"])
+            assert pos <= p0 and p0 + tl <= pos + ln and tl == int(tab[r]["count"]) * esize
+            k = int(tab[r]["count"]) if trunc < 0 else min(int(tab[r]["count"]), trunc)
+            assert got[r] is None
+            got[r] = np.frombuffer(data[p0 - pos:p0 - pos + k * esize], dtype=dt)
+    assert all(g is not None for g in got)
+    return got
+
+
+@pytest.mark.parametrize("esize,bs,rpb,lens,nulls,long_every,filt", [
+    (4, 64, 16, (0, 300), 0, 0, (0, -1, True)),        # token ids, batch boundaries inside RecordBatches
+    (4, 32, 64, (1, 50), 7, 13, (0, -1, True)),        # tombstones + values longer than a segment
+    (2, 100, 5, (0, 40), 0, 0, (3, 20, True)),         # min_len / truncation
+    (1, 50, 9, (0, 70), 5, 0, (2, 30, False)),         # max_len without truncation: skipped
+    (8, 2000, 3000, (1, 2), 0, 0, (0, -1, True)),      # > 1024 rows per RecordBatch
+])
+def test_var_span_fill_matches_host_pack(broker, esize, bs, rpb, lens, nulls, long_every, filt):
+    rnd = random.Random(esize * 100 + bs)
+    n = max(3 * bs, 400)
+    vals = [_var_values(rnd, n, *lens, esize=esize, nulls_every=nulls, long_every=long_every) for _ in range(2)]
+    min_len, max_len, trunc = filt
+    host = _fill_var(broker, False, bs, vals, rpb, esize, min_len=min_len, max_len=max_len, truncate=trunc)
+    span = _fill_var(broker, True, bs, vals, rpb, esize, min_len=min_len, max_len=max_len, truncate=trunc)
+    assert len(host) == len(span)
+    dt = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[esize]
+    for (hr, hi, hw, hp, _), (sr, si, sw, sp, segs) in zip(host, span):
+        assert hr == sr and hw == sw
+        if sr == 0:
+            continue
+        assert si["kind"] == core().PACK_VAR_SPAN
+        assert si["max_row_len"] == hi["max_row_len"] and si["total_elems"] == hi["total_elems"]
+        offs = np.frombuffer(hp[:4 * (hr + 1)], dtype=np.int32)
+        hv = np.frombuffer(hp[hi["values_offset"]:hi["values_offset"] + esize * int(offs[-1])], dtype=dt)
+        got = _decode_var(broker, si, sp, segs, esize, si["trunc_len"])
+        for r in range(hr):
+            np.testing.assert_array_equal(got[r], hv[offs[r]:offs[r + 1]])

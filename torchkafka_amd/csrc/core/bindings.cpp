@@ -594,7 +594,9 @@ PYBIND11_MODULE(_tkcore, m) {
              // kPackRecordSpan / kPackJsonSpan slots: [(log_pos, len, pidx, flags, crc, row_begin, row_end)]
              SlotHeader* h = r.r->slot(g);
              py::list l;
-             if (h->kind != uint32_t(kPackRecordSpan) && h->kind != uint32_t(kPackJsonSpan)) return l;
+             if (h->kind != uint32_t(kPackRecordSpan) && h->kind != uint32_t(kPackJsonSpan) &&
+                 h->kind != uint32_t(kPackVarSpan))
+               return l;
              const auto* sg = reinterpret_cast<const SpanSeg*>(r.r->payload(g) + h->values_offset);
              for (uint32_t i = 0; i < h->n_segs; ++i)
                l.append(py::make_tuple(sg[i].log_pos, sg[i].len, sg[i].pidx, sg[i].flags, sg[i].crc, sg[i].row_begin,
@@ -735,6 +737,8 @@ PYBIND11_MODULE(_tkcore, m) {
   m.attr("SPAN_SEG_MAX") = kSpanSegMax;
   m.attr("SPAN_MAX_SEG_ROWS") = kSpanMaxSegRows;
   m.attr("PACK_JSON_SPAN") = int(kPackJsonSpan);
+  m.attr("PACK_VAR_SPAN") = int(kPackVarSpan);
+  m.attr("VAR_SPAN_ROW_MAX") = kVarSpanRowMax;
   m.attr("JSON_SPAN_MAX_SEG_ROWS") = kJsonSpanMaxSegRows;
   m.attr("JSON_SPAN_ROW_MAX") = kJsonSpanRowMax;
   m.attr("SEG_HOST_ROWS") = int(kSegHostRows);

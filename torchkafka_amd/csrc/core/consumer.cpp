@@ -674,11 +674,14 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   const bool gather = spec.kind == kPackFixed && spec.gather;
   const bool span = spec.kind == kPackFixed && spec.span && !gather;
   const bool jspan = spec.kind == kPackJsonText && spec.span;  // JSON text parsed on the device from the logs
+  const bool vspan = spec.kind == kPackVarlen && spec.span;    // var-len values decoded on the device from the logs
+  const bool rspan = jspan || vspan;                           // rows + segments slot layout (span.h)
   h->n_rows = 0;
   h->n_parts = 0;
   h->n_segs = 0;
   h->flags = 0;
-  h->kind = uint32_t(gather ? kPackGatherFixed : span ? kPackRecordSpan : jspan ? kPackJsonSpan : spec.kind);
+  h->kind = uint32_t(gather ? kPackGatherFixed : span ? kPackRecordSpan : jspan ? kPackJsonSpan
+                    : vspan ? kPackVarSpan : spec.kind);
   h->trunc_len = -1;
   h->err_len = 0;
   h->max_row_len = 0;
@@ -708,7 +711,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
     for (const auto& fp : parts) log_of.push_back(f.broker().log_base(fp.pidx));
   } else if (fixed) {
     if (uint64_t(B) * row_bytes > cap) throw std::invalid_argument("ring slot too small for the batch");
-  } else if (jspan) {
+  } else if (rspan) {
     for (const auto& fp : parts) {
       log_of.push_back(f.broker().log_base(fp.pidx));
       log_cap.push_back(f.broker().part(fp.pidx).log_capacity);
@@ -764,7 +767,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   thread_local std::vector<SpanRB> rbs;
   rbs.clear();
   auto on_batch = [&](const IndexEntry& e, const BatchHeader& bh, bool unverified) -> bool {
-    if (!span && !jspan) return true;
+    if (!span && !rspan) return true;
     const uint32_t pidx = parts[cur_part].pidx;
     if (rbs.empty() || rbs.back().pidx != pidx || rbs.back().pos != e.pos)
       rbs.push_back(SpanRB{pidx, e.size, e.pos, bh.crc, unverified, rows, rows});
@@ -797,6 +800,43 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
     }
     int64_t len;
     uint64_t nbytes;
+    if (vspan) {
+      // device decode from the log: the header gave the value's length; nothing else is read.  A
+      // value too long for one segment is copied into the slot here (rare)
+      if (r.value_len % spec.elem_size) return bad(r, "value size is not a multiple of the element size");
+      const int64_t cnt = r.value_len / spec.elem_size;
+      if (cnt < spec.min_len) { touch(r); return kTake; }
+      len = cnt;
+      if (spec.max_len >= 0 && len > spec.max_len) {
+        if (!spec.truncate) { touch(r); return kTake; }
+        len = spec.max_len;
+      }
+      if (cnt > INT32_MAX) throw std::runtime_error("var-len row too large for the device decode");
+      JsonSpanRow d;
+      d.count = int32_t(cnt);
+      if (uint64_t(r.value_len) <= kVarSpanRowMax) {
+        d.pos = uint64_t(r.value - log_of[cur_part]);
+        d.tlen = int32_t(r.value_len);
+      } else {
+        nbytes = uint64_t(len) * uint64_t(spec.elem_size);
+        const uint64_t at = align_up(vused, 16);
+        if (at + nbytes > vcap) {
+          if (rows == 0) throw std::runtime_error("a single record exceeds the ring slot capacity");
+          slot_full = true;
+          return kStopBefore;
+        }
+        copy_to_slot(vals + at, r.value, nbytes);
+        d.pos = values_off + at;
+        d.tlen = -1;
+        vused = at + nbytes;
+      }
+      srows[rows] = d;
+      elems += len;
+      max_len = std::max(max_len, len);
+      touch(r);
+      rbs.back().row_last = ++rows;
+      return rows == B ? kTakeStop : kTake;
+    }
     if (jspan) {
       // device parse from the log: count + simple check of the text where it lies (no copy, no
       // CRC pass); rows that are not simple are parsed here, their float32 values ride in the slot
@@ -993,7 +1033,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
     out.scanned = scanned;
     return out;
   }
-  if (jspan) {
+  if (rspan) {
     const uint64_t seg_off = align_up(values_off + vused, 256);
     const uint32_t n = build_json_segments(rbs.data(), rbs.size(), srows, rows,
                                            reinterpret_cast<SpanSeg*>(pay + seg_off),

@@ -85,6 +85,7 @@ enum PackKind : int {
   kPackJsonText = 4,
   kPackRecordSpan = 5,  // fixed-width rows decoded on the device from the pinned logs (span.h)
   kPackJsonSpan = 6,    // JsonArray rows parsed on the device straight from the pinned logs (span.h)
+  kPackVarSpan = 7,     // VarLen rows padded/cast on the device straight from the pinned logs (span.h)
 };
 
 // kPackJsonText: JsonArray rows for the device parser (json_parse.hip).  The payload starts

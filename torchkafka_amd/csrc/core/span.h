@@ -83,6 +83,13 @@ static_assert(sizeof(JsonSpanRow) == 16, "JsonSpanRow layout");
 constexpr uint32_t kJsonSpanMaxSegRows = 1024;
 constexpr uint32_t kJsonSpanRowMax = 64u << 10;
 
+// ---- kPackVarSpan: VarLen rows (raw little-endian elements, e.g. int32 token ids) decoded on the
+// device from the logs.  The same slot layout as kPackJsonSpan, with JsonSpanRow::tlen the value's
+// bytes and ::count its elements (no scan: the worker reads only the record headers); a value of
+// more than kVarSpanRowMax bytes is copied into the slot by the worker (tlen = -1).  The kernel
+// (span_decode.hip varlen_span_kernel) pads, casts, and writes lengths/mask straight into the batch.
+constexpr uint32_t kVarSpanRowMax = kSpanSegMax - 1024;
+
 struct SpanSeg {
   uint64_t log_pos;    // byte position of the range in partition `pidx`'s log
   uint32_t len;        // bytes (<= kSpanSegMax)

@@ -230,7 +230,7 @@ int MainDriver::poll_one_impl(bool block, int64_t timeout_ms) {
       if (!block) return 0;
       continue;
     }
-    if (v.kind == uint32_t(tk::kPackRecordSpan) || v.kind == uint32_t(tk::kPackJsonSpan)) {
+    if (v.kind == uint32_t(tk::kPackRecordSpan) || row_span_kind(v.kind)) {
       if (!broker_) {
         error_ = "DeviceLoader: device decode needs the synthetic broker (group_id + bootstrap_servers)";
         return -3;
@@ -494,8 +494,8 @@ void MainDriver::collate_fixed(const SlotView& v, hipStream_t stream, int dst_dt
 void MainDriver::collate_varlen(const SlotView& v, hipStream_t stream, int dst_dt, void* out, int64_t L, double pad,
                                 int64_t* lengths, uint8_t* mask) {
   bool record;
-  if (v.kind == tk::kPackJsonSpan) {
-    // parsed from the logs (stage + parse kernels) on the user's stream, its own completion event
+  if (row_span_kind(v.kind)) {
+    // decoded from the logs on the user's stream, its own completion event
     if (stream != last_stream_) {
       cover_handed();
       last_stream_ = stream;
@@ -507,7 +507,7 @@ void MainDriver::collate_varlen(const SlotView& v, hipStream_t stream, int dst_d
     int64_t* lens[1] = {lengths};
     uint8_t* masks[1] = {mask};
     int64_t pe;
-    launch_json_span(&slot, vs, 1, stream, dst_dt, pad, outs, Ls, lens, masks, true, &pe);
+    launch_row_span(&slot, vs, 1, stream, dst_dt, pad, outs, Ls, lens, masks, true, &pe);
     span_group_handed(&slot, 1, stream, &pe, {}, 1);
     last_perr_ = pe;
     return;
@@ -530,7 +530,7 @@ void MainDriver::deliver(const SlotView& v) { set_delivered(v); }
 
 void MainDriver::set_delivered(const SlotView& v) {
   delivered_ = v.wms;
-  const bool checked = v.kind == tk::kPackJsonText || v.kind == tk::kPackRecordSpan || v.kind == tk::kPackJsonSpan;
+  const bool checked = v.kind == tk::kPackJsonText || v.kind == tk::kPackRecordSpan || row_span_kind(v.kind);
   delivered_perr_ = checked ? (v.perr >= 0 ? v.perr : last_perr_) : -1;
 }
 
@@ -761,6 +761,64 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
   if (record_last) eng_->record_done(slots[n - 1], stream);
 }
 
+void MainDriver::launch_var_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream,
+                                 int dst_dt, double pad, void* const* outs, const int64_t* Ls,
+                                 int64_t* const* lengths, uint8_t* const* masks, bool record_last, int64_t* perrs) {
+  if (!broker_) throw std::runtime_error("driver: device decode needs the synthetic broker");
+  ensure_partials();
+  VarSpanLaunch a{};
+  a.burst = span_burst_;
+  for (int k = 0; k < n; ++k) {
+    perrs[k] = next_err_word();
+    VarSpanBatch& b = a.b[k];
+    b.out = outs[k];
+    b.L = Ls[k];
+    b.lengths = lengths[k];
+    b.mask = masks[k];
+    b.err = perr_dev_ + perrs[k];
+    b.partials = part_dev_ + perrs[k] * kPartials;
+    b.trunc_len = views[k]->trunc_len;
+  }
+  const int src_dt = views[0]->src_dtype;
+  auto flush = [&](bool record) {
+    for (int k = 0; k < n; ++k) {
+      a.b[k].slot = eng_->slot_src(slots[k], stream);  // DMA mode: after the slot's copy
+      a.b[k].rows = reinterpret_cast<const tk::JsonSpanRow*>(a.b[k].slot);
+    }
+    a.tabs = eng_->span_tables();
+    if (mirror_) mirror_->before(stream);
+    tkh::launch_var_span(a, src_dt, dst_dt, pad, stream);
+    if (mirror_) mirror_->after(stream);
+    if (record) eng_->record_done(slots[n - 1], stream);
+  };
+  for (int k = 0; k < n; ++k) {
+    const SlotView& v = *views[k];
+    if (v.src_dtype != src_dt) throw std::invalid_argument("driver: a var-len group mixes element dtypes");
+    const auto* sg = reinterpret_cast<const tk::SpanSeg*>(ring_->payload(uint32_t(v.g)) + v.values_offset);
+    for (uint32_t i = 0; i < v.n_segs; ++i) {
+      constexpr uint32_t kWhole = tk::kSegCrcFirst | tk::kSegCrcLast;
+      if ((sg[i].flags & tk::kSegCrc) && (sg[i].flags & kWhole) != kWhole && i >= uint32_t(kPartials))
+        throw std::runtime_error("driver: a batch splits RecordBatches into more than 512 device segments");
+      if (a.n_seg == kMaxLaunchSegs) {
+        flush(false);
+        a.n_seg = 0;
+      }
+      SpanDevSeg& d = a.s[a.n_seg++];
+      d = SpanDevSeg{};
+      d.src = (sg[i].flags & tk::kSegHostRows) ? nullptr : seg_src(sg[i]);
+      d.log_pos = sg[i].log_pos;
+      d.len = sg[i].len;
+      d.flags = sg[i].flags;
+      d.crc = sg[i].crc;
+      d.row_begin = sg[i].row_begin;
+      d.row_end = sg[i].row_end;
+      d.batch = uint16_t(k);
+      d.seg = uint16_t(i);
+    }
+  }
+  flush(record_last);
+}
+
 const uint8_t* MainDriver::seg_src(const tk::SpanSeg& sg) {
   const uint8_t* log = broker_->log_base(sg.pidx);  // pinned: device address == host address
   if (mirror_) {
@@ -842,7 +900,7 @@ void MainDriver::stage_ready(int extra) {
 
 size_t MainDriver::json_group_extend() {
   group_idx_.clear();
-  if (coalesce_ <= 1 || (last.kind != uint32_t(tk::kPackJsonText) && last.kind != uint32_t(tk::kPackJsonSpan)))
+  if (coalesce_ <= 1 || (last.kind != uint32_t(tk::kPackJsonText) && !row_span_kind(last.kind)))
     return 0;
   uint64_t bytes = last.span_bytes;
   for (size_t i = 0; i < staged_.size() && int(1 + group_idx_.size()) < coalesce_; ++i) {
@@ -860,8 +918,8 @@ void MainDriver::json_group_launch(hipStream_t stream, int dst_dt, double pad, v
                                    std::vector<std::shared_ptr<void>>&& handles) {
   const int n = 1 + int(group_idx_.size());
   if (int(handles.size()) != n - 1) throw std::invalid_argument("driver: group handles do not match the group");
-  if (last.kind == uint32_t(tk::kPackJsonSpan)) {
-    // parsed on the next decode stream (outputs allocated there, torch_step.cpp); the user's
+  if (row_span_kind(last.kind)) {
+    // decoded on the next decode stream (outputs allocated there, torch_step.cpp); the user's
     // stream waits for the group's completion
     int slots[kMaxGroup];
     const SlotView* vs[kMaxGroup];
@@ -874,7 +932,7 @@ void MainDriver::json_group_launch(hipStream_t stream, int dst_dt, double pad, v
     ++span_launches_;
     last_stream_ = ks;
     int64_t perrs[kMaxGroup];
-    launch_json_span(slots, vs, n, ks, dst_dt, pad, outs, Ls, lengths, masks, true, perrs);
+    launch_row_span(slots, vs, n, ks, dst_dt, pad, outs, Ls, lengths, masks, true, perrs);
     last.perr = perrs[0];
     span_group_handed(slots, n, ks, perrs, std::move(handles), 1);
     eng_->stream_wait_done(slots[n - 1], stream);
@@ -1212,7 +1270,7 @@ void MainDriver::ahead_begin(std::vector<int64_t>* rows) {
   }
   if (pre >= ahead_depth_ * coalesce_ || i0 == staged_.size()) return;
   const SlotView& f = staged_[i0];
-  const bool json = f.kind == uint32_t(tk::kPackJsonSpan);  // outputs sized per batch: no shape match needed
+  const bool json = row_span_kind(f.kind);  // outputs sized per batch: no shape match needed
   if ((f.kind != uint32_t(tk::kPackRecordSpan) && !json) || f.n_rows == 0) return;
   uint64_t bytes = 0;
   bool capped = false;
@@ -1290,7 +1348,7 @@ void MainDriver::ahead_launch_json(int dst_dt, double pad, void* const* outs, co
   ++span_launches_;
   last_stream_ = ks;
   int64_t perrs[kMaxGroup];
-  launch_json_span(slots, vs, n, ks, dst_dt, pad, outs, Ls, lengths, masks, true, perrs);
+  launch_row_span(slots, vs, n, ks, dst_dt, pad, outs, Ls, lengths, masks, true, perrs);
   span_group_handed(slots, n, ks, perrs, std::move(handles), 0);
   ++ahead_groups_;
   group_idx_.clear();

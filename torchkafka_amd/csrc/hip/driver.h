@@ -20,6 +20,7 @@
 
 #include "broker.h"
 #include "collate.h"
+#include "consumer.h"
 #include "engine.h"
 #include "log_mirror.h"
 #include "rccl_lockstep.h"
@@ -27,6 +28,9 @@
 #include "span_decode.h"
 
 namespace tkh {
+
+// Slots whose rows are decoded on the device from the logs into a padded batch (span.h).
+inline bool row_span_kind(uint32_t k) { return k == uint32_t(tk::kPackJsonSpan) || k == uint32_t(tk::kPackVarSpan); }
 
 struct SlotView {
   int64_t g = -1;
@@ -252,6 +256,18 @@ class MainDriver {
   void launch_json_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
                         double pad, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
                         uint8_t* const* masks, bool record_last, int64_t* perrs);
+  void launch_var_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
+                       double pad, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
+                       uint8_t* const* masks, bool record_last, int64_t* perrs);
+  // kPackJsonSpan or kPackVarSpan by the views' kind
+  void launch_row_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
+                       double pad, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
+                       uint8_t* const* masks, bool record_last, int64_t* perrs) {
+    if (views[0]->kind == uint32_t(tk::kPackVarSpan))
+      launch_var_span(slots, views, n, stream, dst_dt, pad, outs, Ls, lengths, masks, record_last, perrs);
+    else
+      launch_json_span(slots, views, n, stream, dst_dt, pad, outs, Ls, lengths, masks, record_last, perrs);
+  }
   void ensure_partials();
   // HBM staging ring of the device JSON parse (row texts between the two kernels, json_span.hip):
   // positions are monotonic, regions are freed in launch order as their groups' slots are released.

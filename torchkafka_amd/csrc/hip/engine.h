@@ -76,6 +76,13 @@ class Engine {
   // row texts into HBM (a.b[k].rows / .slot are filled in here from slots[k]); the driver then
   // launches json_rows_kernel over the descriptors and records the completion event.
   void collate_json_stage(const int* slots, int n, hipStream_t user, JsonStageLaunch& a);
+  // Where a kernel launched on `user` reads slot s's payload (DMA mode: after its copy; the
+  // stream waits for it).
+  const uint8_t* slot_src(int s, hipStream_t user) {
+    check_slot(s);
+    begin(s, user);
+    return src_base(s);
+  }
   // Device copy of the CRC tables of the span kernel (uploaded on first use).
   const uint32_t* span_tables();
   // The streams device-decode groups rotate over (created on first use; kDecodeStreams).

@@ -67,6 +67,31 @@ struct JsonStageLaunch {
 };
 
 void launch_json_stage(const JsonStageLaunch& a, hipStream_t stream);
+
+// kPackVarSpan (span_decode.hip varlen_span_kernel): VarLen rows padded + cast straight from the
+// logs into the batch (one kernel: stage, CRC, a wave per row).
+struct VarSpanBatch {
+  void* out;                    // [rows, L] padded output
+  const tk::JsonSpanRow* rows;  // device view of the slot's row table
+  const uint8_t* slot;          // device view of the slot payload (rows the worker copied)
+  int64_t* lengths;             // [rows] elements per row (may be null)
+  uint8_t* mask;                // [rows, L] (may be null)
+  int32_t* err;                 // host-mapped status word (-1 clean, else the first bad segment)
+  uint32_t* partials;           // host-mapped raw CRC per segment
+  int64_t L;
+  int32_t trunc_len;            // rows with more elements keep this many (-1: no limit)
+  int32_t reserved;
+};
+
+struct VarSpanLaunch {
+  int n_seg;
+  int burst;
+  const uint32_t* tabs;
+  VarSpanBatch b[kMaxGroup];
+  SpanDevSeg s[kMaxLaunchSegs];
+};
+
+void launch_var_span(const VarSpanLaunch& a, int src_dt, int dst_dt, double pad, hipStream_t stream);
 void prewarm_json_span_kernels();
 
 // Queries the attributes of the span kernel instantiations (loads their code object), so the

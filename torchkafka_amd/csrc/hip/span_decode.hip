@@ -156,6 +156,106 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
   }
 }
 
+// VarLen rows (kPackVarSpan): stage + CRC as above, then a wave per row converts its elements
+// (any byte alignment: two dwords + v_alignbyte per element) and pads the row to L.
+template <typename S, typename D>
+__global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, D pad) {
+  using C = Conv<S, D, IsIntDst<D>::value>;
+  constexpr int kWaves = kThreads / 64;
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kBufBytes];
+  __shared__ int32_t rel[tk::kJsonSpanMaxSegRows];
+  __shared__ int32_t tln[tk::kJsonSpanMaxSegRows];
+  __shared__ int32_t cnt[tk::kJsonSpanMaxSegRows];
+  __shared__ uint32_t tab[2048];
+  __shared__ uint32_t wcrc[kWaves];
+
+  const int t = int(threadIdx.x), lane = t & 63, wv = t >> 6;
+  const SpanDevSeg& sg = a.s[blockIdx.x];
+  const VarSpanBatch& bo = a.b[sg.batch];
+  const uint32_t row_begin = sg.row_begin;
+  const uint32_t nrows = sg.row_end - row_begin;
+  const uint32_t flags = sg.flags;
+  const int64_t L = bo.L;
+  const int32_t trunc = bo.trunc_len;
+  D* __restrict__ out = static_cast<D*>(bo.out);
+  auto finish = [&](D* orow, int64_t row, int64_t n_out) {
+    for (int64_t k = n_out + lane; k < L; k += 64) orow[k] = pad;
+    if (bo.mask) {
+      uint8_t* mrow = bo.mask + row * L;
+      for (int64_t k = lane; k < L; k += 64) mrow[k] = uint8_t(k < n_out);
+    }
+    if (bo.lengths && lane == 0) bo.lengths[row] = n_out;
+  };
+
+  if (flags & tk::kSegHostRows) {
+    // rows the worker copied into the slot (longer than one segment): a wave per row
+    for (uint32_t rr = uint32_t(wv); rr < nrows; rr += kWaves) {
+      const int64_t row = int64_t(row_begin + rr);
+      const tk::JsonSpanRow d = bo.rows[row];
+      if (d.tlen >= 0) continue;
+      int64_t n_out = trunc >= 0 && d.count > trunc ? trunc : d.count;
+      n_out = n_out < L ? n_out : L;
+      const S* __restrict__ v = reinterpret_cast<const S*>(bo.slot + d.pos);
+      D* orow = out + row * L;
+      for (int64_t k = lane; k < n_out; k += 64) orow[k] = C::apply(v[k], 0.f, 1.f, false);
+      finish(orow, row, n_out);
+    }
+    return;
+  }
+
+  const uint32_t len = sg.len;
+  const int32_t head = int32_t(reinterpret_cast<uintptr_t>(sg.src) & 15u);
+  const bool do_crc = (flags & tk::kSegCrc) != 0;
+  span::stage(sg.src, len, buf, a.burst, [&] {
+    const int64_t base = int64_t(sg.log_pos) - int64_t(head) - kFront;  // log position of LDS byte 0
+    for (uint32_t r = uint32_t(t); r < nrows; r += kThreads) {
+      const tk::JsonSpanRow d = bo.rows[row_begin + r];
+      rel[r] = d.tlen >= 0 ? int32_t(int64_t(d.pos) - base) : 0;
+      tln[r] = d.tlen;
+      cnt[r] = d.count;
+    }
+    if (do_crc)
+      for (int i = t; i < 2048; i += kThreads) tab[i] = a.tabs[tk::kSpanTabSlice + i];
+  });
+  __syncthreads();
+  const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
+  const int32_t lo_b = kFront + head, hi_b = kFront + head + int32_t(len);
+  const uint32_t* shift_set = nullptr;
+  if (do_crc) shift_set = span::crc_lanes(b32, tab, a.tabs, lo_b, hi_b, flags, wcrc);
+
+  bool off_seg = false;
+  for (uint32_t rr = uint32_t(wv); rr < nrows; rr += kWaves) {
+    const int32_t T = tln[rr];
+    if (T < 0) continue;  // copied by the worker (its kSegHostRows block writes it)
+    const int32_t r0 = rel[rr];
+    const int64_t row = int64_t(row_begin + rr);
+    D* orow = out + row * L;
+    const int32_t count = cnt[rr];
+    int64_t n_out = trunc >= 0 && count > trunc ? trunc : count;
+    n_out = n_out < L ? n_out : L;
+    if (r0 < lo_b || r0 + T > hi_b || int64_t(count) * int64_t(sizeof(S)) != T) {
+      off_seg = true;  // the row table disagrees with the segment: read nothing, never commit
+      n_out = 0;
+    }
+    for (int64_t k = lane; k < n_out; k += 64)
+      orow[k] = C::apply(lds_elem<S>(b32, r0 + int32_t(k) * int32_t(sizeof(S))), 0.f, 1.f, false);
+    finish(orow, row, n_out);
+  }
+  if (off_seg && lane == 0) *bo.err = int32_t(sg.seg);
+
+  if (do_crc) {
+    __syncthreads();
+    if (t == 0) span::crc_verdict(shift_set, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials);
+  }
+}
+
+template <typename S, typename D>
+void launch_var_span_t(const VarSpanLaunch& a, double pad, hipStream_t stream) {
+  D padv;
+  if constexpr (IsIntDst<D>::value) padv = D(int64_t(pad)); else padv = Store<D>::cvt(float(pad));
+  hipLaunchKernelGGL((varlen_span_kernel<S, D>), dim3(unsigned(a.n_seg)), dim3(kThreads), 0, stream, a, padv);
+}
+
 template <typename S, typename D>
 void launch_span_t(const SpanLaunch& a, const float* shift, const float* scale, hipStream_t stream) {
   if (a.n_seg <= 0) return;
@@ -177,6 +277,24 @@ void prewarm_span_kernels(int device) {
   (void)hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&span_decode_kernel<float, float, false>));
   (void)hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&span_decode_kernel<float, _Float16, false>));
   (void)hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&span_decode_kernel<float, fp8e4m3, false>));
+}
+
+void launch_var_span(const VarSpanLaunch& a, int src_dt, int dst_dt, double pad, hipStream_t stream) {
+  if (a.n_seg < 0 || a.n_seg > kMaxLaunchSegs) throw std::invalid_argument("var span: bad segment count");
+  if (a.n_seg == 0) return;
+  if (!is_float_dt(dst_dt) && is_float_dt(src_dt))
+    throw std::invalid_argument("collate: float records cannot be cast to an integer dtype");
+  for (int i = 0; i < a.n_seg; ++i) {
+    const SpanDevSeg& s = a.s[i];
+    const bool host = (s.flags & tk::kSegHostRows) != 0;
+    if ((!host && (s.len == 0 || s.len > tk::kSpanSegMax || s.src == nullptr)) || s.row_end < s.row_begin ||
+        s.row_end - s.row_begin > tk::kJsonSpanMaxSegRows || s.batch >= kMaxGroup ||
+        (a.b[s.batch].L > 0 && a.b[s.batch].out == nullptr))
+      throw std::invalid_argument("var span: malformed segment");
+  }
+  TK_DISPATCH_SRC(launch_var_span_t, a, pad, stream)
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("var span launch: ") + hipGetErrorString(e));
 }
 
 void launch_span_decode(const SpanLaunch& a, int src_dt, int dst_dt, const float* shift, const float* scale,

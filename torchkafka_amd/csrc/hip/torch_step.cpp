@@ -299,7 +299,7 @@ void register_torch_step(py::module_& m) {
           py::gil_scoped_release nogil;
           if (v.pre_stream != stream) d.wait_group(v, stream);
           d.deliver(v);
-        } else if (v.kind == uint32_t(tk::kPackJsonSpan)) {
+        } else if (row_span_kind(v.kind)) {
           // parsed from the logs by one launch with the staged JSON batches behind it
           const int ng = 1 + int(extra);
           int64_t ms[kMaxGroup], Ls[kMaxGroup];
@@ -374,8 +374,7 @@ void register_torch_step(py::module_& m) {
             d.deliver(v);
           }
         }
-        if (v.kind == uint32_t(tk::kPackJsonSpan))
-          launch_ahead_json(d, dst_dt, pad, pad_to, pad_multiple, want_mask, dev);
+        if (row_span_kind(v.kind)) launch_ahead_json(d, dst_dt, pad, pad_to, pad_multiple, want_mask, dev);
         d.ph_launch_ns_ += tk::now_ns() - t2;
         ++d.ph_steps_;
         ++d.fast_batches_;

@@ -189,7 +189,7 @@ class _Run:
                 self.driver.set_coalesce_wait_us(L.coalesce_wait_us if L.coalesce > 1 else 0)
                 if L._direct():
                     self.driver.enable_direct()
-                if L._direct() or L._span() or L._json_span():
+                if L._direct() or L._device_decode():
                     self.driver.pin_logs(L._rank_partitions())
                 if L._mirror():
                     self.driver.enable_mirror(int(L.tuning.mirror_chunk_mib) << 20, int(L.tuning.mirror_chunks))
@@ -527,7 +527,7 @@ class DeviceLoader:
     def _slots_per_worker(self) -> int:
         if self.slots_per_worker is not None:
             return self.slots_per_worker
-        if self._span() or self._json_span():
+        if self._device_decode():
             # device-decode slots hold row positions only (a few KiB): a deep ring costs no pinned
             # memory and lets the workers run ahead while slots wait for their kernels
             return 16
@@ -549,12 +549,14 @@ class DeviceLoader:
             B = self.batch_size
             segs = 2 * B + 128 + (B * s.row_bytes) // (32 << 10)
             return (B * 8 + 255) // 256 * 256 + 32 * segs
-        if self._json_span():
-            # row table (16 B per row) + the float32 values of rows the workers parse themselves (not
-            # "simple": exponents, NaN, long tokens; a batch closes early if they do not fit) + the
-            # segments (one per RecordBatch touched, one per 128 KiB or 1024 rows, host-row groups)
+        if self._json_span() or self._var_span():
+            # row table (16 B per row) + the values of rows the workers handle themselves (JSON rows
+            # that are not "simple": exponents, NaN, long tokens; var-len values longer than a
+            # segment; a batch closes early if they do not fit) + the segments (one per RecordBatch
+            # touched, one per 128 KiB or 1024 rows, host-row groups)
             B = self.batch_size
-            return (B * 16 + 255) // 256 * 256 + self.JSON_SPAN_HOST_VALUES_BYTES + 32 * (3 * B + 128)
+            host = self.JSON_SPAN_HOST_VALUES_BYTES if self._json_span() else self.VAR_SPAN_HOST_VALUES_BYTES
+            return (B * 16 + 255) // 256 * 256 + host + 32 * (3 * B + 128)
         if s is not None and getattr(s, "kind", None) == 0 and not self._process_overridden():
             return self.batch_size * s.row_bytes
         return 16 << 20
@@ -563,7 +565,7 @@ class DeviceLoader:
         return {"batch_size": self.batch_size, "sharding": self.sharding, "rank": self.rank,
                 "world_size": self.world_size, "native": self.native, "base_seed": self.base_seed,
                 "gather": self._direct(), "json_device": self._json_device(),
-                "span": self._span() or self._json_span(),
+                "span": self._device_decode(),
                 "process_overridden": self._process_overridden(), "commit_table": None,
                 "worker_spin_us": int(self.tuning.worker_spin_us), "in_process": False}
 
@@ -608,13 +610,33 @@ class DeviceLoader:
         s = self.schema
         ok = (self.device.type == "cuda" and self.native and getattr(s, "kind", None) == 0
               and self.h2d != "direct" and self._commit_target_url()[0] != "" and not self._process_overridden())
-        if self.decode == "device" and not ok and getattr(s, "kind", None) != 2:  # JSON: _json_span()
+        if self.decode == "device" and not ok and getattr(s, "kind", None) not in (1, 2):  # _var_span/_json_span
             raise ValueError("decode='device' needs a CUDA device, a FixedWidth schema, native=True, h2d != 'direct' "
                              "and the synthetic broker (bootstrap_servers shm:// or file://) with a group_id")
         return ok
 
     #: slot room of a device-parsed JSON batch (decode='device') for the rows its worker parses itself
     JSON_SPAN_HOST_VALUES_BYTES = 2 << 20
+    #: slot room of a device-decoded var-len batch for the values its worker copies (longer than a segment)
+    VAR_SPAN_HOST_VALUES_BYTES = 4 << 20
+
+    def _device_decode(self) -> bool:
+        """Any schema decoded on the device straight from the pinned logs (decode='auto'/'device')."""
+        return self._span() or self._json_span() or self._var_span()
+
+    def _var_span(self) -> bool:
+        """decode='device' for VarLen records (e.g. int32 token ids): the workers only walk the record
+        headers (the value length is in the header); span_decode.hip's varlen_span_kernel stages the
+        log segments, verifies each RecordBatch's CRC32C and pads/casts every row into the batch."""
+        if self.decode == "host":
+            return False
+        s = self.schema
+        ok = (self.device.type == "cuda" and self.native and getattr(s, "kind", None) == 1
+              and self.h2d != "direct" and self._commit_target_url()[0] != "" and not self._process_overridden())
+        if self.decode == "device" and not ok and getattr(s, "kind", None) == 1:
+            raise ValueError("decode='device' for VarLen needs a CUDA device, native=True, h2d != 'direct' and the "
+                             "synthetic broker (bootstrap_servers shm:// or file://) with a group_id")
+        return ok
 
     def _json_span(self) -> bool:
         """decode='device' for JsonArray records parsed on the GPU (json_span.hip): the workers walk the
@@ -653,7 +675,7 @@ class DeviceLoader:
         """h2d='dma' with device decode: log bytes reach HBM by hipMemcpyAsync (SDMA copy engines, in
         mirror chunks of ``tuning.mirror_chunk_mib``) and the decode kernels read them there, instead
         of reading the pinned logs over PCIe themselves (csrc/hip/log_mirror.h)."""
-        return self.h2d == "dma" and (self._span() or self._json_span())
+        return self.h2d == "dma" and self._device_decode()
 
     def _direct(self) -> bool:
         """h2d='direct': fixed-width rows gathered by the kernel straight from the pinned broker logs."""

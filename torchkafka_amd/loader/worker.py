@@ -209,7 +209,8 @@ def _native_loop(ring, worker_id, spw, consumer, schema, cfg, state) -> None:
     timeout = _consumer_timeout_ms(consumer)
     fetcher = consumer._fetcher
     gather = bool(cfg.get("gather")) and kind == core().PACK_FIXED
-    span = bool(cfg.get("span")) and kind in (core().PACK_FIXED, core().PACK_JSON_TEXT) and not gather
+    span = (bool(cfg.get("span")) and kind in (core().PACK_FIXED, core().PACK_JSON_TEXT, core().PACK_VARLEN)
+            and not gather)
     if not fetcher.assigned() and cfg["sharding"] == "static":
         g = _acquire(ring, worker_id, state)  # nothing to read, ever: end of stream right away
         ring.set_slot(g, 0, core().SLOT_EOS, kind, 0, 0, 0, 0, 0, [])
