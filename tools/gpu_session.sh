@@ -43,6 +43,12 @@ for s in ${STEPS:-pytest_new}; do
     pmcfetch) (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE WRITE_SIZE SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d "$OLDPWD/gpurun_out/pmc_fetch_span" -o run -- python3 "$OLDPWD/bench.py" --steps 200 --warmup 20 --steady-steps 0 --h2d dma > "$OLDPWD/gpurun_out/pmc_fetch_span.log" 2>&1) || exit $?
              tail -2 gpurun_out/pmc_fetch_span.log ;;
     aheaddrv) for a in 1 2 3 4 6; do TORCHKAFKA_AHEAD_DEPTH=$a run bench_drv_ahead$a 300 python bench.py --gpus 1 --steps 20 --warmup 5; done ;;
+    tokens) run tokens_device 300 python benchmarks/varlen_tokens.py
+            run tokens_host 300 python benchmarks/varlen_tokens.py --decode host ;;
+    tokenslong) run tokens_long_device 300 python benchmarks/varlen_tokens.py --min-len 2048 --max-len 8192 --batch-size 32 --steps 2000
+            run tokens_long_host 300 python benchmarks/varlen_tokens.py --min-len 2048 --max-len 8192 --batch-size 32 --steps 2000 --decode host ;;
+    proftok) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/proftok" -o run -- python3 "$OLDPWD/benchmarks/varlen_tokens.py" --steps 500 > "$OLDPWD/gpurun_out/proftok.log" 2>&1) || exit $?
+             tail -1 gpurun_out/proftok.log | cut -c1-200 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   esac
 done

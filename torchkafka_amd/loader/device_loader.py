@@ -506,6 +506,10 @@ class DeviceLoader:
     def _resolve_h2d(self, slot_payload_bytes: int) -> str:
         if self.h2d != "auto":
             return self.h2d
+        if self._device_decode():
+            # device decode: the slots hold row tables (a few KiB read once by the kernel), the values
+            # stay in the pinned logs -- a DMA of the slot would only add a copy and an event per batch
+            return "zerocopy"
         if self._json_device():
             # JSON text batches are a few hundred KiB whatever the slot capacity; the parse kernel
             # reads each row once, so zero-copy beats a DMA + HBM re-read (14.3 vs 12.6 M rec/s,
