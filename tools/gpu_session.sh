@@ -14,6 +14,7 @@ run() {  # run <name> <timeout> <cmd...>
 }
 for s in ${STEPS:-pytest_new}; do
   case $s in
+    pytest_var) run pytest_var 300 python -u -m pytest tests/test_gpu_span.py -k "var_span" -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     pytest_new) run pytest_new 400 python -u -m pytest tests/test_gpu_json_span.py tests/test_gpu_span.py tests/test_gpu_json_parse.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     pytest_all) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     config4) run config4 300 python benchmarks/config4_json_varlen.py ;;

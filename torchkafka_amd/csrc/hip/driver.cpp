@@ -778,6 +778,11 @@ void MainDriver::launch_var_span(const int* slots, const SlotView* const* views,
     b.err = perr_dev_ + perrs[k];
     b.partials = part_dev_ + perrs[k] * kPartials;
     b.trunc_len = views[k]->trunc_len;
+    // vector stores of a 16-byte source group (16 / ssz elements of dsz bytes): rows and groups aligned
+    const int ssz = dtype_size(views[0]->src_dtype), dsz = dtype_size(dst_dt);
+    const int64_t gbytes = ssz > 0 ? int64_t(16 / ssz) * dsz : 0;
+    b.reserved = (gbytes >= 16 && gbytes % 16 == 0 && reinterpret_cast<uintptr_t>(outs[k]) % 16 == 0 &&
+                  (Ls[k] * dsz) % 16 == 0) ? 1 : 0;
   }
   const int src_dt = views[0]->src_dtype;
   auto flush = [&](bool record) {

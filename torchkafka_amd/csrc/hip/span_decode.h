@@ -80,7 +80,7 @@ struct VarSpanBatch {
   uint32_t* partials;           // host-mapped raw CRC per segment
   int64_t L;
   int32_t trunc_len;            // rows with more elements keep this many (-1: no limit)
-  int32_t reserved;
+  int32_t reserved;             // 1: every row starts 16-byte aligned (vector stores of 16 source bytes)
 };
 
 struct VarSpanLaunch {

@@ -237,7 +237,24 @@ __global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, 
       off_seg = true;  // the row table disagrees with the segment: read nothing, never commit
       n_out = 0;
     }
-    for (int64_t k = lane; k < n_out; k += 64)
+    // 16 source bytes per lane per step (a 5-dword window + v_alignbyte: values sit at any byte
+    // offset behind their headers), vector stores when the row is aligned; then the tail
+    constexpr int kPer = 16 / int(sizeof(S));
+    const int64_t full = bo.reserved ? n_out / kPer * kPer : 0;
+    for (int64_t e0 = int64_t(lane) * kPer; e0 < full; e0 += 64 * kPer) {
+      const int32_t b0 = r0 + int32_t(e0) * int32_t(sizeof(S));
+      const int32_t w = b0 >> 2, sh = b0 & 3;
+      const uint32_t x0 = b32[w], x1 = b32[w + 1], x2 = b32[w + 2], x3 = b32[w + 3], x4 = b32[w + 4];
+      const uint32_t o[4] = {__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                             __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
+      S sv[kPer];
+      __builtin_memcpy(sv, o, 16);
+      Vec<D, kPer> ov;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) ov.v[k] = C::apply(sv[k], 0.f, 1.f, false);
+      *reinterpret_cast<Vec<D, kPer>*>(orow + e0) = ov;
+    }
+    for (int64_t k = full + lane; k < n_out; k += 64)
       orow[k] = C::apply(lds_elem<S>(b32, r0 + int32_t(k) * int32_t(sizeof(S))), 0.f, 1.f, false);
     finish(orow, row, n_out);
   }
