@@ -1,0 +1,63 @@
+"""A Kafka cluster feeding the gfx950 decode path (KafkaBridge -> replica logs -> span_decode).
+
+The native replicator receives Fetch responses into the tails of local partition logs while the
+loader pins those logs and decodes batches from them on the device (CRC32C + cast,
+csrc/hip/span_decode.hip).  The cluster is `KafkaWireServer` over a synthetic broker (no Kafka
+cluster exists on the box); results are compared bit for bit with the host decode path, and the
+cluster's committed offsets are checked after close().
+"""
+import os
+import time
+import uuid
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _loader(DS, url, decode, bs=64):
+    from torchkafka_amd import DeviceLoader
+
+    return DeviceLoader(DS.placeholder(), bs, num_workers=2, device="cuda:0", decode=decode, dtype=torch.float32,
+                        worker_init_fn=DS.init_worker("t", bootstrap_servers=url, group_id=f"trainer-{decode}",
+                                                      auto_offset_reset="earliest", consumer_timeout_ms=400))
+
+
+@pytest.mark.parametrize("live", [False, True])
+def test_device_decode_from_a_replicated_cluster(broker, live):
+    from torchkafka_amd import FixedWidth, KafkaDataset, auto_commit
+    from torchkafka_amd.broker import KafkaBridge, KafkaWireServer
+
+    class Rows(KafkaDataset):
+        schema = FixedWidth(torch.float32, (256,))
+
+    broker.create_topic("t", 4)
+    broker.fill("t", 600 if live else 1200, "fixed_f32", size=256, records_per_batch=64)
+    out = {}
+    with KafkaWireServer(broker) as srv:
+        for decode in ("device", "host"):
+            br = KafkaBridge(srv.address, "t", group_id=f"trainer-{decode}",
+                             url=f"shm://tkgbr-{os.getpid()}-{uuid.uuid4().hex[:6]}", log_capacity=256 << 20)
+            try:
+                if not live:
+                    assert br.wait_caught_up(20)
+                dl = _loader(Rows, br.url, decode)
+                assert dl._span() == (decode == "device")
+                xs = []
+                for i, x in enumerate(auto_commit(dl)):
+                    xs.append(x.clone())
+                    if live and decode == "device" and i == 3:
+                        # the cluster keeps producing while the replica is being decoded from
+                        broker.fill("t", 600, "fixed_f32", size=256, records_per_batch=64)
+                    if live and decode == "device" and i == 4:
+                        time.sleep(0.2)
+                torch.cuda.synchronize()
+                out[decode] = torch.cat(xs)
+            finally:
+                br.close()
+            assert broker.committed_offsets(f"trainer-{decode}", "t") == {p: 1200 for p in range(4)}
+    d, h = out["device"], out["host"]
+    assert d.shape == h.shape == (4800, 256)
+    key = lambda t: (t[:, 1].float() * 1e6 + t[:, 0].float()).argsort()  # noqa: E731 -- (partition, offset) order
+    assert torch.equal(d[key(d)].view(torch.int32), h[key(h)].view(torch.int32))

@@ -1,4 +1,7 @@
-"""Synthetic shared-memory Kafka broker (stands in for a cluster; kafka-python is not installed)."""
+"""Brokers: the synthetic shared-memory broker, its Kafka-protocol front end, and the bridge that
+mirrors a real Kafka cluster into a local broker for the device path."""
+from .bridge import KafkaBridge
 from .synthetic import SyntheticBroker, is_synthetic_url, open_broker, resolve_url
+from .wire_server import KafkaWireServer
 
-__all__ = ["SyntheticBroker", "open_broker", "resolve_url", "is_synthetic_url"]
+__all__ = ["SyntheticBroker", "KafkaBridge", "KafkaWireServer", "open_broker", "resolve_url", "is_synthetic_url"]

@@ -1,0 +1,136 @@
+"""KafkaBridge: a real Kafka cluster feeding the device path.
+
+The reference reads its cluster through kafka-python (``/root/reference/src/kafka_dataset.py:21-22,
+206``): every worker's consumer parses Fetch responses and CRC-checks record batches in Python.
+Here a native replicator (``csrc/core/replicator.cpp``, the Kafka wire protocol in
+``csrc/core/kafka_wire.cpp``) fetches a rank's partitions with C++ threads and receives every
+record set straight into the tail of a local partition log in shared memory -- the logs the
+synthetic broker keeps.  The loader then runs unchanged on that local broker: workers walk record
+headers, the main process pins the logs, gfx950 kernels verify CRC32C and decode the values.
+Offsets are the cluster's own; every commit the loader makes into the local offset table is
+forwarded to the group coordinator (OffsetCommit) by a committer thread, and ``close()`` flushes
+the last one::
+
+    bridge = KafkaBridge("broker1:9092,broker2:9092", "events", group_id="trainer",
+                         partitions=shard_partitions(n_parts, rank, world))
+    ds_init = Events.init_worker("events", bootstrap_servers=bridge.url, group_id="trainer")
+    loader = DeviceLoader(Events.placeholder(), 256, num_workers=4, worker_init_fn=ds_init, ...)
+    for batch in auto_commit(loader):
+        ...
+    bridge.close()          # forwards the final commit
+
+Semantics: at-least-once, like the reference's commit-after-batch.  A commit lands in the local
+table synchronously and reaches the cluster within ``commit_interval_ms`` (5 ms); a crash in
+between replays at most that window's batches.  Records are fetched read_uncommitted, control
+batches (transaction markers) are dropped, compressed batches stop their partition with an
+``UnsupportedCodecError`` (the device decoders read raw records).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import threading
+import uuid
+from typing import Iterable
+
+from ..ops.native import core
+from .synthetic import SyntheticBroker
+
+log = logging.getLogger("torchkafka.bridge")
+
+
+class KafkaBridge:
+    """Mirrors ``topic`` (all or ``partitions``) of a Kafka cluster into a local broker at :attr:`url`."""
+
+    def __init__(self, bootstrap_servers: str | Iterable[str], topic: str, *, group_id: str | None = None,
+                 partitions: Iterable[int] | None = None, url: str | None = None,
+                 auto_offset_reset: str = "earliest", max_lag_bytes: int = 1 << 30,
+                 log_capacity: int = 64 << 30, index_capacity: int = 1 << 22, fetch_max_wait_ms: int = 100,
+                 fetch_max_bytes: int = 64 << 20, max_partition_fetch_bytes: int = 8 << 20,
+                 request_timeout_ms: int = 30000, commit_interval_ms: int = 5, fetchers: int = 0,
+                 client_id: str = "torchkafka-bridge", start: bool = True):
+        if not isinstance(bootstrap_servers, str):
+            bootstrap_servers = ",".join(bootstrap_servers)
+        self.bootstrap_servers = bootstrap_servers
+        self.topic = topic
+        self.group_id = group_id
+        self.url = url or f"shm://tkbridge-{os.getpid()}-{uuid.uuid4().hex[:8]}"
+        self._own = url is None
+        # a fresh local broker (or an existing persistent replica: file:// URLs resume their logs)
+        self.local = SyntheticBroker(self.url, create=True, log_capacity=log_capacity,
+                                     index_capacity=index_capacity)
+        self._r = core().Replicator(
+            self.local.native, bootstrap_servers, topic, group=group_id or "",
+            partitions=sorted(int(p) for p in partitions) if partitions is not None else [],
+            auto_offset_reset=auto_offset_reset, max_wait_ms=int(fetch_max_wait_ms), max_bytes=int(fetch_max_bytes),
+            partition_max_bytes=int(max_partition_fetch_bytes), timeout_ms=int(request_timeout_ms),
+            max_lag_bytes=int(max_lag_bytes), commit_interval_ms=int(commit_interval_ms), fetchers=int(fetchers),
+            log_capacity=int(log_capacity), index_capacity=int(index_capacity), client_id=client_id)
+        self._closed = False
+        self._lock = threading.Lock()
+        self._reported = 0
+        if start:
+            self.start()
+
+    # ------------------------------------------------------------ lifecycle
+    def start(self) -> "KafkaBridge":
+        self._r.start()
+        log.debug("Bridge %s -> %s started (%d partitions).", self.bootstrap_servers, self.url,
+                  len(self._r.stats()))
+        return self
+
+    def close(self, *, flush: bool = True, destroy: bool | None = None) -> None:
+        """Stops fetching and forwards the latest commits (``flush``); removes an owned local broker."""
+        with self._lock:
+            if self._closed:
+                return
+            self._closed = True
+        self._r.stop(flush)
+        self._report_errors()
+        if destroy if destroy is not None else self._own:
+            self.local.destroy()
+
+    def __enter__(self) -> "KafkaBridge":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
+    def __del__(self):
+        try:
+            if not self._closed:
+                self._r.stop(True)
+        except Exception:  # noqa: BLE001 -- interpreter teardown
+            pass
+
+    # ------------------------------------------------------------ state
+    @property
+    def running(self) -> bool:
+        return bool(self._r.running)
+
+    def flush(self) -> int:
+        """Forwards every changed local commit to the cluster now; returns partitions committed."""
+        n = self._r.flush_commits()
+        self._report_errors()
+        return n
+
+    def wait_caught_up(self, timeout: float = 30.0) -> bool:
+        """Blocks until every mirrored partition reached the cluster's current end offset."""
+        return bool(self._r.wait_caught_up(int(timeout * 1000)))
+
+    def stats(self) -> list[dict]:
+        return list(self._r.stats())
+
+    @property
+    def errors(self) -> int:
+        return int(self._r.errors)
+
+    def last_error(self) -> str:
+        return str(self._r.last_error())
+
+    def _report_errors(self) -> None:
+        n = self.errors
+        if n > self._reported:
+            log.warning("Bridge %s: %d error(s), last: %s", self.bootstrap_servers, n - self._reported,
+                        self.last_error())
+            self._reported = n

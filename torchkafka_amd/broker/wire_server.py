@@ -1,0 +1,452 @@
+"""The synthetic broker served over the Kafka wire protocol.
+
+A small Kafka-protocol front end for :class:`SyntheticBroker`: it answers the requests a
+consumer makes (ApiVersions, Metadata, ListOffsets, Fetch, FindCoordinator, OffsetCommit,
+OffsetFetch -- the non-flexible versions every Kafka client speaks) from the broker's
+RecordBatch v2 logs and its committed-offset table.  It is what the native replicator
+(:class:`~torchkafka_amd.broker.KafkaBridge`, ``csrc/core/replicator.cpp``) is tested
+against here, where no Kafka cluster exists, and it lets any Kafka client (kafka-python,
+where installed) read a synthetic topic over TCP.
+
+Fault injection mirrors what a real cluster does to a consumer: NOT_LEADER /
+OFFSET_OUT_OF_RANGE / arbitrary error codes on fetches, failed commits, record sets cut
+inside a batch (a broker's ``partition_max_bytes`` cut), control batches (transaction
+markers) between data batches.
+
+Reference: the reference consumes through kafka-python's KafkaConsumer
+(``/root/reference/src/kafka_dataset.py:21-22, 206``); this server plays the cluster.
+"""
+from __future__ import annotations
+
+import socket
+import socketserver
+import struct
+import threading
+import time
+
+from .synthetic import SyntheticBroker
+
+API_FETCH, API_LIST_OFFSETS, API_METADATA = 1, 2, 3
+API_OFFSET_COMMIT, API_OFFSET_FETCH, API_FIND_COORDINATOR, API_API_VERSIONS = 8, 9, 10, 18
+# api key -> (min, max) version served
+SUPPORTED = {API_FETCH: (4, 4), API_LIST_OFFSETS: (0, 1), API_METADATA: (0, 1), API_OFFSET_COMMIT: (2, 2),
+             API_OFFSET_FETCH: (1, 1), API_FIND_COORDINATOR: (0, 0), API_API_VERSIONS: (0, 0)}
+
+NONE, OFFSET_OUT_OF_RANGE, UNKNOWN_TOPIC, NOT_LEADER, UNSUPPORTED_VERSION = 0, 1, 3, 6, 35
+ILLEGAL_GENERATION = 22
+
+
+class _R:
+    """Big-endian reader over one request body."""
+
+    def __init__(self, b: bytes):
+        self.b, self.o = b, 0
+
+    def _u(self, fmt: str, n: int):
+        v = struct.unpack_from(fmt, self.b, self.o)[0]
+        self.o += n
+        return v
+
+    def i8(self):
+        return self._u(">b", 1)
+
+    def i16(self):
+        return self._u(">h", 2)
+
+    def i32(self):
+        return self._u(">i", 4)
+
+    def i64(self):
+        return self._u(">q", 8)
+
+    def str(self):
+        n = self.i16()
+        if n < 0:
+            return None
+        s = self.b[self.o:self.o + n].decode()
+        self.o += n
+        return s
+
+
+class _W:
+    def __init__(self):
+        self.parts: list[bytes] = []
+
+    def i8(self, v):
+        self.parts.append(struct.pack(">b", v))
+
+    def i16(self, v):
+        self.parts.append(struct.pack(">h", v))
+
+    def i32(self, v):
+        self.parts.append(struct.pack(">i", v))
+
+    def i64(self, v):
+        self.parts.append(struct.pack(">q", v))
+
+    def str(self, s):
+        if s is None:
+            self.i16(-1)
+        else:
+            b = s.encode()
+            self.i16(len(b))
+            self.parts.append(b)
+
+    def bytes(self, b):
+        if b is None:
+            self.i32(-1)
+        else:
+            self.i32(len(b))
+            self.parts.append(b)
+
+    def data(self) -> bytes:
+        return b"".join(self.parts)
+
+
+def control_batch(base_offset: int, timestamp_ms: int = 0, commit: bool = True) -> bytes:
+    """A transaction-marker RecordBatch (control bit set), as a transactional producer leaves in a log."""
+    from ..ops.native import core
+
+    key = struct.pack(">hh", 0, 1 if commit else 0)  # version, type (COMMIT / ABORT)
+    val = struct.pack(">hi", 0, 0)
+    body = bytearray()
+    rec = bytearray()
+    rec += b"\x00"                     # attributes
+    rec += _varint(0)                  # timestamp delta
+    rec += _varint(0)                  # offset delta
+    rec += _varint(len(key)) + key
+    rec += _varint(len(val)) + val
+    rec += _varint(0)                  # headers
+    body += _varint(len(rec)) + rec
+    attrs = 0x20 | 0x10                # control + transactional
+    after_crc = struct.pack(">hiqqqhii", attrs, 0, timestamp_ms, timestamp_ms, 7, 0, -1, 1) + bytes(body)
+    crc = core().crc32c(after_crc)
+    blen = 4 + 1 + 4 + len(after_crc)
+    return struct.pack(">qiibI", base_offset, blen, 0, 2, crc) + after_crc
+
+
+def _varint(v: int) -> bytes:
+    z = (v << 1) ^ (v >> 63)
+    out = bytearray()
+    while z >= 0x80:
+        out.append((z & 0x7F) | 0x80)
+        z >>= 7
+    out.append(z)
+    return bytes(out)
+
+
+class KafkaWireServer:
+    """Serves a :class:`SyntheticBroker` over the Kafka protocol on ``host:port`` (0: a free port)."""
+
+    def __init__(self, broker: SyntheticBroker, host: str = "127.0.0.1", port: int = 0, node_id: int = 0):
+        self.broker = broker
+        self.node_id = node_id
+        self._lock = threading.Lock()
+        self._fetch_faults: dict[tuple[str, int], list[int]] = {}
+        self._commit_faults: list[int] = []
+        self.partial_tail = False          # cut every record set inside its last batch
+        self.requests: dict[int, int] = {}  # api key -> count
+        srv = self
+
+        class Handler(socketserver.BaseRequestHandler):
+            def handle(self):
+                self.request.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                try:
+                    while True:
+                        head = _recv_exact(self.request, 4)
+                        if head is None:
+                            return
+                        (n,) = struct.unpack(">i", head)
+                        req = _recv_exact(self.request, n)
+                        if req is None:
+                            return
+                        resp = srv._dispatch(req)
+                        if resp is None:
+                            return
+                        self.request.sendall(struct.pack(">i", len(resp)) + resp)
+                except (ConnectionError, OSError):
+                    return
+
+        class Server(socketserver.ThreadingTCPServer):
+            daemon_threads = True
+            allow_reuse_address = True
+
+        self._srv = Server((host, port), Handler)
+        self.host, self.port = self._srv.server_address[:2]
+        self._thread = threading.Thread(target=self._srv.serve_forever, daemon=True, name="kafka-wire-server")
+
+    # ------------------------------------------------------------ lifecycle
+    @property
+    def address(self) -> str:
+        return f"{self.host}:{self.port}"
+
+    def start(self) -> "KafkaWireServer":
+        self._thread.start()
+        return self
+
+    def close(self) -> None:
+        self._srv.shutdown()
+        self._srv.server_close()
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ------------------------------------------------------------ fault injection
+    def inject_fetch_errors(self, topic: str, partition: int, code: int = NOT_LEADER, n: int = 1) -> None:
+        """The next ``n`` fetches of a partition answer ``code`` (NOT_LEADER by default)."""
+        with self._lock:
+            self._fetch_faults.setdefault((topic, partition), []).extend([code] * n)
+
+    def inject_commit_errors(self, code: int = ILLEGAL_GENERATION, n: int = 1) -> None:
+        with self._lock:
+            self._commit_faults.extend([code] * n)
+
+    # ------------------------------------------------------------ protocol
+    def _dispatch(self, req: bytes) -> bytes | None:
+        r = _R(req)
+        key, ver, corr = r.i16(), r.i16(), r.i32()
+        r.str()  # client id
+        with self._lock:
+            self.requests[key] = self.requests.get(key, 0) + 1
+        w = _W()
+        w.i32(corr)
+        lo_hi = SUPPORTED.get(key)
+        if key == API_API_VERSIONS:
+            w.i16(NONE)
+            w.i32(len(SUPPORTED))
+            for k, (lo, hi) in sorted(SUPPORTED.items()):
+                w.i16(k)
+                w.i16(lo)
+                w.i16(hi)
+            return w.data()
+        if lo_hi is None or not lo_hi[0] <= ver <= lo_hi[1]:
+            return None  # a real broker closes the connection on an unsupported version
+        getattr(self, f"_api_{key}")(r, ver, w)
+        return w.data()
+
+    def _topic_names(self, r: _R, ver: int):
+        n = r.i32()
+        if n < 0 or (n == 0 and ver == 0):
+            return self.broker.topics()
+        return [r.str() for _ in range(n)]
+
+    def _api_3(self, r: _R, ver: int, w: _W) -> None:  # Metadata v0/v1
+        names = self._topic_names(r, ver)
+        w.i32(1)
+        w.i32(self.node_id)
+        w.str(self.host)
+        w.i32(self.port)
+        if ver >= 1:
+            w.str(None)  # rack
+            w.i32(self.node_id)  # controller
+        w.i32(len(names))
+        for name in names:
+            if not self.broker.has_topic(name):
+                w.i16(UNKNOWN_TOPIC)
+                w.str(name)
+                if ver >= 1:
+                    w.i8(0)
+                w.i32(0)
+                continue
+            n = self.broker.topic(name)[1]
+            w.i16(NONE)
+            w.str(name)
+            if ver >= 1:
+                w.i8(0)
+            w.i32(n)
+            for p in range(n):
+                w.i16(NONE)
+                w.i32(p)
+                w.i32(self.node_id)
+                w.i32(1)
+                w.i32(self.node_id)
+                w.i32(1)
+                w.i32(self.node_id)
+
+    def _api_2(self, r: _R, ver: int, w: _W) -> None:  # ListOffsets v0/v1
+        r.i32()  # replica
+        nt = r.i32()
+        w.i32(nt)
+        for _ in range(nt):
+            name = r.str()
+            np_ = r.i32()
+            w.str(name)
+            w.i32(np_)
+            for _ in range(np_):
+                p, ts = r.i32(), r.i64()
+                if ver == 0:
+                    r.i32()  # max offsets
+                err, off = NONE, -1
+                try:
+                    pidx = self.broker.pidx(name, p)
+                    nat = self.broker.native
+                    if ts == -1:
+                        off = nat.high_watermark(pidx)
+                    elif ts == -2:
+                        off = nat.log_start_offset(pidx)
+                    else:
+                        off = nat.offset_for_time(pidx, ts)[0]
+                except Exception:  # noqa: BLE001 -- any lookup failure is an unknown partition
+                    err = UNKNOWN_TOPIC
+                w.i32(p)
+                w.i16(err)
+                if ver == 0:
+                    w.i32(1 if off >= 0 else 0)
+                    if off >= 0:
+                        w.i64(off)
+                else:
+                    w.i64(-1)
+                    w.i64(off)
+
+    def _api_1(self, r: _R, ver: int, w: _W) -> None:  # Fetch v4
+        r.i32()  # replica
+        max_wait, min_bytes, max_bytes = r.i32(), r.i32(), r.i32()
+        r.i8()  # isolation level
+        reqs = []
+        for _ in range(r.i32()):
+            name = r.str()
+            reqs.append((name, [(r.i32(), r.i64(), r.i32()) for _ in range(r.i32())]))
+        faults = {}
+        with self._lock:  # one injected error per partition per request
+            for name, parts in reqs:
+                for p, _off, _pmax in parts:
+                    q = self._fetch_faults.get((name, p))
+                    if q:
+                        faults[(name, p)] = q.pop(0)
+        deadline = time.monotonic() + max_wait / 1000.0
+        while True:
+            out, total = self._fetch_once(reqs, max_bytes, faults)
+            if total >= max(1, min_bytes) or time.monotonic() >= deadline:
+                break
+            time.sleep(0.002)
+        w.i32(0)  # throttle
+        w.i32(len(out))
+        for name, parts in out:
+            w.str(name)
+            w.i32(len(parts))
+            for p, err, hw, data in parts:
+                w.i32(p)
+                w.i16(err)
+                w.i64(hw)
+                w.i64(hw)   # last stable offset
+                w.i32(-1)   # aborted transactions: null
+                w.bytes(data)
+
+    def _fetch_once(self, reqs, max_bytes: int, faults: dict):
+        out, total = [], 0
+        nat = self.broker.native
+        for name, parts in reqs:
+            po = []
+            for p, off, pmax in parts:
+                fault = faults.get((name, p))
+                if fault is not None:
+                    po.append((p, fault, -1, None))
+                    continue
+                try:
+                    pidx = self.broker.pidx(name, p)
+                except Exception:  # noqa: BLE001
+                    po.append((p, UNKNOWN_TOPIC, -1, None))
+                    continue
+                try:
+                    budget = max(0, min(pmax, max_bytes - total))
+                    data, hw, _start = nat.read_batches(pidx, off, max(budget, 1))
+                except Exception:  # noqa: BLE001 -- OffsetOutOfRange
+                    po.append((p, OFFSET_OUT_OF_RANGE, nat.high_watermark(pidx), None))
+                    continue
+                if data and self.partial_tail:
+                    # add the front half of the next batch, as a broker cutting at partition_max_bytes does
+                    try:
+                        more, _, _ = nat.read_batches(pidx, _next_offset(data), 1)
+                        data = data + more[:max(12, len(more) // 2)]
+                    except Exception:  # noqa: BLE001 -- nothing after it
+                        pass
+                total += len(data)
+                po.append((p, NONE, hw, data))
+            out.append((name, po))
+        return out, total
+
+    def _api_10(self, r: _R, ver: int, w: _W) -> None:  # FindCoordinator v0
+        r.str()
+        w.i16(NONE)
+        w.i32(self.node_id)
+        w.str(self.host)
+        w.i32(self.port)
+
+    def _api_8(self, r: _R, ver: int, w: _W) -> None:  # OffsetCommit v2
+        group = r.str()
+        r.i32()   # generation
+        r.str()   # member
+        r.i64()   # retention
+        nat = self.broker.native
+        g = nat.group_index(group, True)
+        nt = r.i32()
+        w.i32(nt)
+        for _ in range(nt):
+            name = r.str()
+            np_ = r.i32()
+            w.str(name)
+            w.i32(np_)
+            for _ in range(np_):
+                p, off = r.i32(), r.i64()
+                meta = r.str() or ""
+                with self._lock:
+                    err = self._commit_faults.pop(0) if self._commit_faults else NONE
+                if err == NONE:
+                    try:
+                        nat.commit(g, -1, 0, 0, [(self.broker.pidx(name, p), int(off), meta)])
+                    except Exception:  # noqa: BLE001 -- a group with live members refuses a simple commit
+                        err = ILLEGAL_GENERATION
+                w.i32(p)
+                w.i16(err)
+
+    def _api_9(self, r: _R, ver: int, w: _W) -> None:  # OffsetFetch v1
+        group = r.str()
+        nat = self.broker.native
+        g = nat.group_index(group, True)
+        nt = r.i32()
+        w.i32(nt)
+        for _ in range(nt):
+            name = r.str()
+            np_ = r.i32()
+            w.str(name)
+            w.i32(np_)
+            for _ in range(np_):
+                p = r.i32()
+                try:
+                    off, meta = nat.committed(g, self.broker.pidx(name, p))
+                    err = NONE
+                except Exception:  # noqa: BLE001
+                    off, meta, err = -1, "", UNKNOWN_TOPIC
+                w.i32(p)
+                w.i64(off)
+                w.str(meta)
+                w.i16(err)
+
+
+def _last_batch_start(data: bytes) -> int:
+    o = 0
+    while True:
+        (blen,) = struct.unpack_from(">i", data, o + 8)
+        if o + 12 + blen >= len(data):
+            return o
+        o += 12 + blen
+
+
+def _next_offset(data: bytes) -> int:
+    o = _last_batch_start(data)
+    base = struct.unpack_from(">q", data, o)[0]
+    (delta,) = struct.unpack_from(">i", data, o + 23)
+    return base + delta + 1
+
+
+def _recv_exact(sock, n: int) -> bytes | None:
+    buf = bytearray()
+    while len(buf) < n:
+        chunk = sock.recv(n - len(buf))
+        if not chunk:
+            return None
+        buf += chunk
+    return bytes(buf)

@@ -9,7 +9,9 @@
 #include "consumer.h"
 #include "crc32c.h"
 #include "lockstep.h"
+#include "kafka_wire.h"
 #include "record_batch.h"
+#include "replicator.h"
 #include "ring.h"
 
 namespace py = pybind11;
@@ -345,6 +347,44 @@ PYBIND11_MODULE(_tkcore, m) {
           py::arg("pidxs"), py::arg("n_records"), py::arg("kind"), py::arg("size_a"), py::arg("size_b") = 0,
           py::arg("records_per_batch") = 64, py::arg("seed") = 0, py::arg("threads") = 1)
       .def("delete_records", &Broker::delete_records)
+      .def("read_batches",
+           [](Broker& b, uint32_t p, int64_t offset, uint64_t max_bytes) {
+             // Whole RecordBatches from the one holding `offset` (or the next after a gap), at most
+             // max_bytes but at least one batch (a Kafka Fetch response's record set, KIP-74).
+             PartitionEntry& P = b.part(p);
+             const int64_t hw = P.high_watermark.load(std::memory_order_acquire);
+             const int64_t start = P.log_start_offset.load(std::memory_order_acquire);
+             if (offset < start || offset > hw) throw OffsetOutOfRange("offset " + std::to_string(offset) + " out of range");
+             if (offset == hw) return py::make_tuple(py::bytes(), hw, start);
+             const IndexEntry* idx = b.index_base(p);
+             const uint64_t nb = P.n_batches.load(std::memory_order_acquire);
+             int64_t i = b.find_batch(p, offset, -1);
+             const uint64_t pos0 = idx[i].pos;
+             uint64_t end = pos0 + idx[i].size;
+             for (uint64_t j = uint64_t(i) + 1; j < nb && idx[j].pos + idx[j].size - pos0 <= max_bytes; ++j)
+               end = idx[j].pos + idx[j].size;
+             return py::make_tuple(py::bytes(reinterpret_cast<const char*>(b.log_base(p)) + pos0, end - pos0), hw, start);
+           },
+           py::arg("pidx"), py::arg("offset"), py::arg("max_bytes"))
+      .def("reset_empty", &Broker::reset_empty)
+      .def("ingest_bytes",
+           [](Broker& b, uint32_t p, py::bytes data, int64_t from_offset, bool keep_control) {
+             std::string s = data;
+             uint64_t avail = 0;
+             uint8_t* tail = b.log_tail(p, &avail);
+             if (s.size() > avail) throw KafkaError("ingest_bytes: log full");
+             std::memcpy(tail, s.data(), s.size());
+             Broker::Ingested in = b.ingest(p, s.size(), from_offset, keep_control);
+             py::dict d;
+             d["consumed"] = in.consumed;
+             d["kept"] = in.kept;
+             d["kept_bytes"] = in.kept_bytes;
+             d["control"] = in.control;
+             d["next_offset"] = in.next_offset;
+             return d;
+           },
+           py::arg("pidx"), py::arg("data"), py::arg("from_offset") = -1, py::arg("keep_control") = false)
+      .def("position_of", &Broker::position_of)
       .def("group_index", &Broker::group_index, py::arg("group"), py::arg("create") = true)
       .def("group_name", &Broker::group_name)
       .def("join_group", &Broker::join_group)
@@ -389,6 +429,92 @@ PYBIND11_MODULE(_tkcore, m) {
       .def("reset_group_offsets", &Broker::reset_group_offsets)
       .def("set_fetch_delay", &Broker::set_fetch_delay)
       .def("inject_fetch_errors", &Broker::inject_fetch_errors);
+
+  // ---- Kafka wire protocol (kafka_wire.h) and the cluster -> local log replicator (replicator.h)
+  py::class_<wire::Client>(m, "WireClient")
+      .def(py::init<const std::string&, const std::string&, int>(), py::arg("bootstrap"),
+           py::arg("client_id") = "torchkafka", py::arg("timeout_ms") = 30000)
+      .def("metadata",
+           [](wire::Client& c, const std::string& topic) {
+             wire::TopicMeta t;
+             {
+               py::gil_scoped_release nogil;
+               t = c.metadata(topic);
+             }
+             py::list parts;
+             for (auto& p : t.partitions) parts.append(py::make_tuple(p.partition, p.leader, p.error));
+             return py::make_tuple(t.error, parts);
+           })
+      .def("brokers",
+           [](wire::Client& c) {
+             py::list l;
+             for (auto& b : c.brokers()) l.append(py::make_tuple(b.node_id, b.host, b.port));
+             return l;
+           })
+      .def("list_offsets", &wire::Client::list_offsets, py::call_guard<py::gil_scoped_release>())
+      .def("offset_fetch", &wire::Client::offset_fetch, py::call_guard<py::gil_scoped_release>())
+      .def("offset_commit", &wire::Client::offset_commit, py::arg("group"), py::arg("topic"), py::arg("offsets"),
+           py::arg("metadata") = "", py::call_guard<py::gil_scoped_release>())
+      .def_static("parse_bootstrap", &wire::Client::parse_bootstrap);
+
+  py::class_<Replicator>(m, "Replicator")
+      .def(py::init([](std::shared_ptr<Broker> local, const std::string& bootstrap, const std::string& topic,
+                       const std::string& group, std::vector<int32_t> partitions, const std::string& reset,
+                       int32_t max_wait_ms, int32_t max_bytes, int32_t partition_max_bytes, int32_t timeout_ms,
+                       int64_t max_lag_bytes, int32_t commit_interval_ms, int32_t fetchers, uint64_t log_capacity,
+                       uint64_t index_capacity, const std::string& client_id) {
+             ReplicaConfig c;
+             c.bootstrap = bootstrap;
+             c.topic = topic;
+             c.group = group;
+             c.partitions = std::move(partitions);
+             c.auto_offset_reset = reset;
+             c.max_wait_ms = max_wait_ms;
+             c.max_bytes = max_bytes;
+             c.partition_max_bytes = partition_max_bytes;
+             c.timeout_ms = timeout_ms;
+             c.max_lag_bytes = max_lag_bytes;
+             c.commit_interval_ms = commit_interval_ms;
+             c.fetchers = fetchers;
+             c.log_capacity = log_capacity;
+             c.index_capacity = index_capacity;
+             c.client_id = client_id;
+             return std::make_unique<Replicator>(std::move(local), c);
+           }),
+           py::arg("local"), py::arg("bootstrap"), py::arg("topic"), py::arg("group") = "",
+           py::arg("partitions") = std::vector<int32_t>(), py::arg("auto_offset_reset") = "earliest",
+           py::arg("max_wait_ms") = 100, py::arg("max_bytes") = 64 << 20, py::arg("partition_max_bytes") = 8 << 20,
+           py::arg("timeout_ms") = 30000, py::arg("max_lag_bytes") = int64_t(1) << 30,
+           py::arg("commit_interval_ms") = 5, py::arg("fetchers") = 0, py::arg("log_capacity") = 0,
+           py::arg("index_capacity") = 0, py::arg("client_id") = "torchkafka-replicator")
+      .def("start", &Replicator::start, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &Replicator::stop, py::arg("flush") = true, py::call_guard<py::gil_scoped_release>())
+      .def("flush_commits", &Replicator::flush_commits, py::call_guard<py::gil_scoped_release>())
+      .def("wait_caught_up", &Replicator::wait_caught_up, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("running", &Replicator::running)
+      .def_property_readonly("errors", &Replicator::errors)
+      .def_property_readonly("first_pidx", &Replicator::first_pidx)
+      .def_property_readonly("n_partitions", &Replicator::n_partitions)
+      .def("last_error", &Replicator::last_error)
+      .def("stats", [](Replicator& r) {
+        py::list l;
+        for (auto& s : r.stats()) {
+          py::dict d;
+          d["partition"] = s.partition;
+          d["pidx"] = s.pidx;
+          d["start_offset"] = s.start_offset;
+          d["fetch_offset"] = s.fetch_offset;
+          d["remote_hw"] = s.remote_hw;
+          d["forwarded"] = s.forwarded;
+          d["bytes"] = s.bytes;
+          d["batches"] = s.batches;
+          d["control_batches"] = s.control_batches;
+          d["fetches"] = s.fetches;
+          d["throttled"] = s.throttled;
+          l.append(d);
+        }
+        return l;
+      });
 
   // ---- fetcher
   py::class_<PyFetcher>(m, "Fetcher")

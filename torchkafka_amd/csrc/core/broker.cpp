@@ -318,8 +318,11 @@ int64_t Broker::find_batch(uint32_t pidx, int64_t offset, int64_t hint) {
     if (idx[mid].base_offset <= offset) lo = mid + 1; else hi = mid;
   }
   int64_t i = lo - 1;
-  if (!contains(i)) throw OffsetOutOfRange("offset " + std::to_string(offset) + " not in log");
-  return i;
+  if (contains(i)) return i;
+  // an offset in a gap (compacted away, or a dropped transaction marker of a replica) reads
+  // from the next batch; the record walk skips offsets below the position
+  if (lo < nb && offset >= P.log_start_offset.load(std::memory_order_acquire)) return lo;
+  throw OffsetOutOfRange("offset " + std::to_string(offset) + " not in log");
 }
 
 std::pair<int64_t, int64_t> Broker::offset_for_time(uint32_t pidx, int64_t ts) {
@@ -364,6 +367,83 @@ int64_t Broker::append(uint32_t pidx, const RecordIn* recs, size_t n) {
   P.records_produced.fetch_add(n, std::memory_order_relaxed);
   P.high_watermark.store(base + int64_t(n), std::memory_order_release);
   return base;
+}
+
+uint8_t* Broker::log_tail(uint32_t pidx, uint64_t* avail) {
+  PartitionEntry& P = part(pidx);
+  Mapped& m = mapped(pidx);
+  const uint64_t pos = P.log_end_pos.load(std::memory_order_acquire);
+  *avail = P.log_capacity - pos;
+  return m.log + pos;
+}
+
+void Broker::reset_empty(uint32_t pidx, int64_t offset) {
+  PartitionEntry& P = part(pidx);
+  RobustLock l(&P.lock);
+  if (P.n_batches.load() != 0) throw KafkaError("reset_empty: partition already holds batches");
+  P.log_start_offset.store(offset, std::memory_order_release);
+  P.high_watermark.store(offset, std::memory_order_release);
+}
+
+Broker::Ingested Broker::ingest(uint32_t pidx, uint64_t len, int64_t from_offset, bool keep_control) {
+  PartitionEntry& P = part(pidx);
+  Mapped& m = mapped(pidx);
+  RobustLock l(&P.lock);
+  const uint64_t pos0 = P.log_end_pos.load(std::memory_order_relaxed);
+  if (pos0 + len > P.log_capacity) throw KafkaError("ingest beyond the partition log capacity");
+  uint8_t* base = m.log + pos0;
+  uint64_t nb = P.n_batches.load(std::memory_order_relaxed);
+  int64_t hw = P.high_watermark.load(std::memory_order_relaxed);
+  Ingested out;
+  uint64_t r = 0, w = 0;
+  while (len - r >= kBatchHeaderBytes) {
+    int32_t blen;
+    std::memcpy(&blen, base + r + kBatchLengthOffset, 4);
+    blen = int32_t(__builtin_bswap32(uint32_t(blen)));
+    if (blen < int32_t(kBatchHeaderBytes - 12)) throw CorruptRecord("replica: bad RecordBatch length");
+    const uint64_t total = uint64_t(blen) + 12;
+    if (len - r < total) break;  // partial trailing batch: the next fetch brings it whole
+    const BatchHeader h = parse_batch_header(base + r, total);
+    if (h.magic != 2)
+      throw CorruptRecord("replica: message format v" + std::to_string(h.magic) +
+                          " (only RecordBatch v2 is supported; upgrade the topic's message.format.version)");
+    out.consumed = r + total;
+    out.next_offset = h.next_offset();
+    const bool control = (h.attributes >> 5) & 1;
+    if (control) ++out.control;
+    if ((!control || keep_control) && h.next_offset() > from_offset && h.next_offset() > hw) {
+      if ((h.attributes & 7) && !keep_control)
+        throw KafkaError("UnsupportedCodecError: compressed RecordBatch (codec " + std::to_string(h.attributes & 7) +
+                         ") on a device-decoded replica; produce with compression_type=None");
+      if (nb >= P.index_capacity) throw KafkaError("partition index full");
+      if (w != r) std::memmove(base + w, base + r, total);
+      m.idx[nb++] = IndexEntry{h.base_offset, pos0 + w, uint32_t(total), h.last_offset_delta, h.max_timestamp};
+      w += total;
+      hw = h.next_offset();
+      ++out.kept;
+    }
+    r += total;
+  }
+  out.kept_bytes = w;
+  if (out.kept) {
+    P.log_end_pos.store(pos0 + w, std::memory_order_release);
+    P.n_batches.store(nb, std::memory_order_release);
+    P.records_produced.fetch_add(uint64_t(out.kept), std::memory_order_relaxed);
+    P.high_watermark.store(hw, std::memory_order_release);
+  }
+  return out;
+}
+
+uint64_t Broker::position_of(uint32_t pidx, int64_t offset) {
+  const PartitionEntry& P = part(pidx);
+  const IndexEntry* idx = mapped(pidx).idx;
+  const int64_t nb = int64_t(P.n_batches.load(std::memory_order_acquire));
+  int64_t lo = 0, hi = nb;  // first batch whose last offset >= offset
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) / 2;
+    if (idx[mid].base_offset + idx[mid].last_offset_delta < offset) lo = mid + 1; else hi = mid;
+  }
+  return lo < nb ? idx[lo].pos : P.log_end_pos.load(std::memory_order_acquire);
 }
 
 void Broker::delete_records(uint32_t pidx, int64_t before_offset) {

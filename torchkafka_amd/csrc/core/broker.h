@@ -178,6 +178,27 @@ class Broker {
                       int64_t size_b, uint32_t records_per_batch, uint64_t seed, int n_threads);
   void delete_records(uint32_t pidx, int64_t before_offset);
 
+  // ---- replica ingest (replicator.h: a Kafka cluster mirrored into this broker's logs)
+  // Writable tail of a partition log: bytes [log_end_pos, capacity) -- a Fetch response's record
+  // set is received straight into it, then ingest() indexes the whole batches it holds.
+  uint8_t* log_tail(uint32_t pidx, uint64_t* avail);
+  // An empty partition starts at `offset` (log start = high watermark = offset).
+  void reset_empty(uint32_t pidx, int64_t offset);
+  struct Ingested {
+    uint64_t consumed = 0;     // bytes of whole batches walked (kept or dropped)
+    uint64_t kept_bytes = 0;
+    uint32_t kept = 0, control = 0;
+    int64_t next_offset = -1;  // next offset to fetch (-1: no whole batch in the data)
+  };
+  // Walks the RecordBatches received at log_tail(): keeps (indexes, publishes) whole data
+  // batches at or beyond `from_offset`, drops control batches (transaction markers) and
+  // batches already held, compacting in place; a trailing partial batch is left for the next
+  // fetch to overwrite.  Compressed batches raise (the device path decodes raw records only).
+  // keep_control: store control batches too (a broker's own log, e.g. the wire server's tests).
+  Ingested ingest(uint32_t pidx, uint64_t len, int64_t from_offset, bool keep_control = false);
+  // Log byte position of the first batch holding an offset >= `offset` (log end if none).
+  uint64_t position_of(uint32_t pidx, int64_t offset);
+
   // ---- groups / offsets
   uint32_t group_index(const std::string& group, bool create = true);
   std::string group_name(uint32_t g) const;

@@ -172,6 +172,10 @@ size_t Fetcher::scan(FetchPart& fp, size_t max_records, F&& visit, G&& on_batch)
       prefault(fp, log, e.pos, P.log_end_pos.load(std::memory_order_acquire));
     const uint8_t* bp = log + e.pos;
     const BatchHeader h = parse_batch_header(bp, e.size);
+    if ((h.attributes >> 5) & 1) {  // control batch (a transaction marker): never delivered, as in Kafka clients
+      if (fp.position < h.next_offset()) fp.position = h.next_offset();
+      continue;
+    }
     const bool unverified = check_crcs_ && fp.verified_base != h.base_offset;
     if (on_batch(e, h, unverified) && unverified) {
       if (!verify_batch_crc(bp, h))

@@ -1,0 +1,559 @@
+// Native Kafka wire-protocol client: see kafka_wire.h.
+#include "kafka_wire.h"
+
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstring>
+
+namespace tk::wire {
+
+const char* error_name(int16_t code) {
+  switch (code) {
+    case kNone: return "NoError";
+    case kOffsetOutOfRange: return "OffsetOutOfRangeError";
+    case kCorruptMessage: return "CorruptRecordException";
+    case kUnknownTopicOrPartition: return "UnknownTopicOrPartitionError";
+    case kLeaderNotAvailable: return "LeaderNotAvailableError";
+    case kNotLeaderForPartition: return "NotLeaderForPartitionError";
+    case kRequestTimedOut: return "RequestTimedOutError";
+    case kCoordinatorLoadInProgress: return "CoordinatorLoadInProgressError";
+    case kCoordinatorNotAvailable: return "CoordinatorNotAvailableError";
+    case kNotCoordinator: return "NotCoordinatorError";
+    case kIllegalGeneration: return "IllegalGenerationError";
+    case kUnknownMemberId: return "UnknownMemberIdError";
+    case kRebalanceInProgress: return "RebalanceInProgressError";
+    default: return "KafkaError";
+  }
+}
+
+// ------------------------------------------------------------ Writer / Reader
+void Writer::i16(int16_t v) {
+  const uint16_t b = htons(uint16_t(v));
+  buf_.append(reinterpret_cast<const char*>(&b), 2);
+}
+void Writer::i32(int32_t v) {
+  const uint32_t b = htonl(uint32_t(v));
+  buf_.append(reinterpret_cast<const char*>(&b), 4);
+}
+void Writer::i64(int64_t v) {
+  i32(int32_t(uint64_t(v) >> 32));
+  i32(int32_t(uint64_t(v) & 0xffffffffu));
+}
+void Writer::str(const std::string& s) {
+  if (s.size() > 32767) throw KafkaError("wire: string too long");
+  i16(int16_t(s.size()));
+  buf_.append(s);
+}
+
+void Reader::need(size_t n) const {
+  if (size_t(end_ - p_) < n) throw KafkaError("wire: truncated response");
+}
+int8_t Reader::i8() { need(1); return int8_t(*p_++); }
+int16_t Reader::i16() {
+  need(2);
+  uint16_t v;
+  std::memcpy(&v, p_, 2);
+  p_ += 2;
+  return int16_t(ntohs(v));
+}
+int32_t Reader::i32() {
+  need(4);
+  uint32_t v;
+  std::memcpy(&v, p_, 4);
+  p_ += 4;
+  return int32_t(ntohl(v));
+}
+int64_t Reader::i64() {
+  const uint64_t hi = uint32_t(i32());
+  const uint64_t lo = uint32_t(i32());
+  return int64_t((hi << 32) | lo);
+}
+std::string Reader::str() {
+  const int16_t n = i16();
+  if (n < 0) return std::string();
+  need(size_t(n));
+  std::string s(reinterpret_cast<const char*>(p_), size_t(n));
+  p_ += n;
+  return s;
+}
+const uint8_t* Reader::bytes(int32_t* len) {
+  const int32_t n = i32();
+  *len = n;
+  if (n < 0) return nullptr;
+  need(size_t(n));
+  const uint8_t* p = p_;
+  p_ += n;
+  return p;
+}
+
+// ------------------------------------------------------------ Conn
+namespace {
+int64_t mono_ms() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return int64_t(ts.tv_sec) * 1000 + ts.tv_nsec / 1000000;
+}
+}  // namespace
+
+Conn::Conn(const std::string& host, int port, int timeout_ms)
+    : host_(host), port_(port), timeout_ms_(timeout_ms), buf_(size_t(1) << 16) {
+  addrinfo hints{};
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  addrinfo* res = nullptr;
+  const std::string ps = std::to_string(port);
+  if (getaddrinfo(host.c_str(), ps.c_str(), &hints, &res) != 0 || !res)
+    throw KafkaError("NoBrokersAvailable: cannot resolve " + host + ":" + ps);
+  std::string why = "no address";
+  for (addrinfo* a = res; a; a = a->ai_next) {
+    int fd = ::socket(a->ai_family, a->ai_socktype | SOCK_CLOEXEC, a->ai_protocol);
+    if (fd < 0) continue;
+    // non-blocking connect bounded by the timeout
+    int fl = 1;
+    ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &fl, sizeof(fl));
+    int rcv = 8 << 20;
+    ::setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &rcv, sizeof(rcv));
+    timeval tv{timeout_ms / 1000, (timeout_ms % 1000) * 1000};
+    ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+    if (::connect(fd, a->ai_addr, a->ai_addrlen) == 0) {
+      fd_ = fd;
+      break;
+    }
+    why = std::strerror(errno);
+    ::close(fd);
+  }
+  freeaddrinfo(res);
+  if (fd_ < 0) throw KafkaError("NoBrokersAvailable: cannot connect to " + host + ":" + ps + " (" + why + ")");
+}
+
+Conn::~Conn() { close(); }
+
+void Conn::close() {
+  if (fd_ >= 0) ::close(fd_);
+  fd_ = -1;
+}
+
+void Conn::send_all(const std::string& frame) {
+  size_t off = 0;
+  while (off < frame.size()) {
+    const ssize_t n = ::send(fd_, frame.data() + off, frame.size() - off, MSG_NOSIGNAL);
+    if (n < 0) {
+      if (errno == EINTR) continue;
+      const std::string e = std::strerror(errno);
+      close();
+      throw KafkaError("KafkaConnectionError: send to " + host_ + " failed: " + e);
+    }
+    off += size_t(n);
+  }
+}
+
+void Conn::send(int16_t api_key, int16_t api_version, const std::string& client_id, const std::string& body) {
+  if (fd_ < 0) throw KafkaError("KafkaConnectionError: connection to " + host_ + " is closed");
+  if (remaining_) finish();
+  Writer h;
+  h.i32(0);  // size, patched below
+  h.i16(api_key);
+  h.i16(api_version);
+  expect_corr_ = ++corr_;
+  h.i32(expect_corr_);
+  h.str(client_id);
+  std::string& f = h.data();
+  f.append(body);
+  const uint32_t sz = htonl(uint32_t(f.size() - 4));
+  std::memcpy(&f[0], &sz, 4);
+  send_all(f);
+}
+
+void Conn::fill(size_t want) {
+  // compact, then read until `want` bytes are buffered (never past the current response)
+  if (b0_ == b1_) b0_ = b1_ = 0;
+  if (b0_ > 0 && buf_.size() - b1_ < want) {
+    std::memmove(buf_.data(), buf_.data() + b0_, b1_ - b0_);
+    b1_ -= b0_;
+    b0_ = 0;
+  }
+  if (buf_.size() < want) buf_.resize(want);
+  while (b1_ - b0_ < want) {
+    const int64_t left = deadline_ms_ - mono_ms();
+    if (left <= 0) {
+      close();
+      throw KafkaError("KafkaTimeoutError: no response from " + host_ + ":" + std::to_string(port_));
+    }
+    pollfd p{fd_, POLLIN, 0};
+    const int r = ::poll(&p, 1, int(std::min<int64_t>(left, 1000)));
+    if (r < 0 && errno != EINTR) {
+      close();
+      throw KafkaError("KafkaConnectionError: poll failed");
+    }
+    if (r <= 0) continue;
+    const ssize_t n = ::recv(fd_, buf_.data() + b1_, buf_.size() - b1_, 0);
+    if (n == 0 || (n < 0 && errno != EINTR && errno != EAGAIN)) {
+      close();
+      throw KafkaError("KafkaConnectionError: connection to " + host_ + " closed by the broker");
+    }
+    if (n > 0) b1_ += size_t(n);
+  }
+}
+
+size_t Conn::begin_response(int timeout_ms) {
+  remaining_ = 0;
+  deadline_ms_ = mono_ms() + timeout_ms;
+  fill(8);
+  uint32_t sz, corr;
+  std::memcpy(&sz, buf_.data() + b0_, 4);
+  std::memcpy(&corr, buf_.data() + b0_ + 4, 4);
+  b0_ += 8;
+  sz = ntohl(sz);
+  corr = ntohl(corr);
+  if (sz < 4 || int32_t(corr) != expect_corr_) {
+    close();
+    throw KafkaError("wire: response correlation mismatch from " + host_);
+  }
+  remaining_ = sz - 4;
+  return remaining_;
+}
+
+void Conn::read(void* dst, size_t n) {
+  if (n > remaining_) throw KafkaError("wire: read past the end of a response");
+  if (b1_ - b0_ < n && n <= 4096) fill(n);  // small fields: one recv fills the buffer for many of them
+  auto* d = static_cast<uint8_t*>(dst);
+  const size_t have = std::min(n, b1_ - b0_);
+  std::memcpy(d, buf_.data() + b0_, have);
+  b0_ += have;
+  size_t off = have;
+  // large reads go straight from the socket into the destination (record sets into the log)
+  while (off < n) {
+    const int64_t left = deadline_ms_ - mono_ms();
+    if (left <= 0) {
+      close();
+      throw KafkaError("KafkaTimeoutError: response from " + host_ + " stalled");
+    }
+    pollfd p{fd_, POLLIN, 0};
+    const int r = ::poll(&p, 1, int(std::min<int64_t>(left, 1000)));
+    if (r <= 0) continue;
+    const ssize_t got = ::recv(fd_, d + off, n - off, 0);
+    if (got == 0 || (got < 0 && errno != EINTR && errno != EAGAIN)) {
+      close();
+      throw KafkaError("KafkaConnectionError: connection to " + host_ + " closed mid-response");
+    }
+    if (got > 0) off += size_t(got);
+  }
+  remaining_ -= n;
+}
+
+int8_t Conn::r8() { int8_t v; read(&v, 1); return v; }
+int16_t Conn::r16() { uint16_t v; read(&v, 2); return int16_t(ntohs(v)); }
+int32_t Conn::r32() { uint32_t v; read(&v, 4); return int32_t(ntohl(v)); }
+int64_t Conn::r64() {
+  const uint64_t hi = uint32_t(r32());
+  const uint64_t lo = uint32_t(r32());
+  return int64_t((hi << 32) | lo);
+}
+std::string Conn::rstr() {
+  const int16_t n = r16();
+  if (n <= 0) return std::string();
+  std::string s(size_t(n), '\0');
+  read(&s[0], size_t(n));
+  return s;
+}
+void Conn::skip(size_t n) {
+  uint8_t tmp[4096];
+  while (n) {
+    const size_t k = std::min(n, sizeof(tmp));
+    read(tmp, k);
+    n -= k;
+  }
+}
+void Conn::finish() { skip(remaining_); }
+
+std::vector<uint8_t> Conn::roundtrip(int16_t api_key, int16_t api_version, const std::string& client_id,
+                                     const std::string& body, int timeout_ms) {
+  send(api_key, api_version, client_id, body);
+  const size_t n = begin_response(timeout_ms);
+  std::vector<uint8_t> out(n);
+  read(out.data(), n);
+  return out;
+}
+
+// ------------------------------------------------------------ Client
+std::vector<std::pair<std::string, int>> Client::parse_bootstrap(const std::string& s0) {
+  std::vector<std::pair<std::string, int>> out;
+  std::string s = s0;
+  size_t start = 0;
+  while (start <= s.size()) {
+    size_t comma = s.find(',', start);
+    std::string item = s.substr(start, comma == std::string::npos ? std::string::npos : comma - start);
+    start = comma == std::string::npos ? s.size() + 1 : comma + 1;
+    item.erase(0, item.find_first_not_of(" \t"));
+    item.erase(item.find_last_not_of(" \t") + 1);
+    if (item.rfind("kafka://", 0) == 0) item = item.substr(8);
+    if (item.empty()) continue;
+    int port = 9092;
+    std::string host = item;
+    const size_t close_br = item.find(']');
+    const size_t colon = item.rfind(':');
+    if (colon != std::string::npos && (close_br == std::string::npos ? item.find(':') == colon : colon > close_br)) {
+      host = item.substr(0, colon);
+      port = std::stoi(item.substr(colon + 1));
+    }
+    if (!host.empty() && host.front() == '[' && host.back() == ']') host = host.substr(1, host.size() - 2);
+    out.emplace_back(host, port);
+  }
+  if (out.empty()) throw KafkaError("NoBrokersAvailable: empty bootstrap_servers");
+  return out;
+}
+
+Client::Client(const std::string& bootstrap, const std::string& client_id, int timeout_ms)
+    : bootstrap_(parse_bootstrap(bootstrap)), client_id_(client_id), timeout_ms_(timeout_ms) {}
+
+Conn& Client::bootstrap_conn() {
+  auto it = conns_.find(-1);
+  if (it != conns_.end() && it->second->ok()) return *it->second;
+  std::string why;
+  for (auto& [h, p] : bootstrap_) {
+    try {
+      conns_[-1] = std::make_unique<Conn>(h, p, timeout_ms_);
+      return *conns_[-1];
+    } catch (const KafkaError& e) {
+      why = e.what();
+    }
+  }
+  throw KafkaError("NoBrokersAvailable: " + why);
+}
+
+Conn& Client::conn(int32_t node_id) {
+  if (node_id < 0) return bootstrap_conn();
+  auto it = conns_.find(node_id);
+  if (it != conns_.end() && it->second->ok()) return *it->second;
+  auto nd = nodes_.find(node_id);
+  if (nd == nodes_.end()) throw WireError(kLeaderNotAvailable, "wire: unknown broker node " + std::to_string(node_id));
+  conns_[node_id] = std::make_unique<Conn>(nd->second.host, nd->second.port, timeout_ms_);
+  return *conns_[node_id];
+}
+
+void Client::drop(int32_t node_id) { conns_.erase(node_id); }
+
+std::vector<BrokerAddr> Client::brokers() {
+  std::vector<BrokerAddr> v;
+  for (auto& [id, b] : nodes_) v.push_back(b);
+  return v;
+}
+
+TopicMeta Client::metadata(const std::string& topic) {
+  Writer w;
+  w.array(1);
+  w.str(topic);
+  std::vector<uint8_t> resp;
+  try {
+    resp = bootstrap_conn().roundtrip(kMetadata, 1, client_id_, w.data(), timeout_ms_);
+  } catch (const KafkaError&) {
+    drop(-1);
+    resp = bootstrap_conn().roundtrip(kMetadata, 1, client_id_, w.data(), timeout_ms_);
+  }
+  Reader r(resp.data(), resp.size());
+  const int32_t nb = r.i32();
+  for (int32_t i = 0; i < nb; ++i) {
+    BrokerAddr b;
+    b.node_id = r.i32();
+    b.host = r.str();
+    b.port = r.i32();
+    r.str();  // rack
+    auto old = nodes_.find(b.node_id);
+    if (old != nodes_.end() && (old->second.host != b.host || old->second.port != b.port)) drop(b.node_id);
+    nodes_[b.node_id] = b;
+  }
+  r.i32();  // controller
+  const int32_t nt = r.i32();
+  TopicMeta out;
+  out.name = topic;
+  out.error = kUnknownTopicOrPartition;
+  for (int32_t i = 0; i < nt; ++i) {
+    TopicMeta t;
+    t.error = r.i16();
+    t.name = r.str();
+    r.i8();  // is_internal
+    const int32_t np = r.i32();
+    for (int32_t j = 0; j < np; ++j) {
+      PartitionMeta p;
+      p.error = r.i16();
+      p.partition = r.i32();
+      p.leader = r.i32();
+      const int32_t nrep = r.i32();
+      for (int32_t k = 0; k < nrep; ++k) r.i32();
+      const int32_t nisr = r.i32();
+      for (int32_t k = 0; k < nisr; ++k) r.i32();
+      t.partitions.push_back(p);
+    }
+    std::sort(t.partitions.begin(), t.partitions.end(),
+              [](const PartitionMeta& a, const PartitionMeta& b) { return a.partition < b.partition; });
+    if (t.name == topic) out = t;
+    topics_[t.name] = t;
+  }
+  return out;
+}
+
+int32_t Client::leader(const std::string& topic, int32_t partition) {
+  auto it = topics_.find(topic);
+  if (it == topics_.end()) return -1;
+  for (auto& p : it->second.partitions)
+    if (p.partition == partition) return p.error == kNone || p.error == kLeaderNotAvailable ? p.leader : -1;
+  return -1;
+}
+
+std::map<int32_t, int64_t> Client::list_offsets(const std::string& topic, const std::vector<int32_t>& parts,
+                                                int64_t timestamp) {
+  if (topics_.find(topic) == topics_.end()) metadata(topic);
+  std::map<int32_t, std::vector<int32_t>> by_leader;
+  for (int32_t p : parts) by_leader[leader(topic, p)].push_back(p);
+  std::map<int32_t, int64_t> out;
+  for (auto& [node, ps] : by_leader) {
+    if (node < 0) throw WireError(kLeaderNotAvailable, "LeaderNotAvailableError: " + topic);
+    Writer w;
+    w.i32(-1);  // replica id
+    w.array(1);
+    w.str(topic);
+    w.array(int32_t(ps.size()));
+    for (int32_t p : ps) {
+      w.i32(p);
+      w.i64(timestamp);
+    }
+    auto resp = conn(node).roundtrip(kListOffsets, 1, client_id_, w.data(), timeout_ms_);
+    Reader r(resp.data(), resp.size());
+    const int32_t nt = r.i32();
+    for (int32_t i = 0; i < nt; ++i) {
+      r.str();
+      const int32_t np = r.i32();
+      for (int32_t j = 0; j < np; ++j) {
+        const int32_t p = r.i32();
+        const int16_t e = r.i16();
+        r.i64();  // timestamp
+        const int64_t off = r.i64();
+        if (e != kNone)
+          throw WireError(e, std::string(error_name(e)) + ": ListOffsets " + topic + "-" + std::to_string(p));
+        out[p] = off;
+      }
+    }
+  }
+  return out;
+}
+
+int32_t Client::coordinator(const std::string& group) {
+  if (coordinator_ >= 0 && coordinator_group_ == group) return coordinator_;
+  Writer w;
+  w.str(group);
+  auto resp = bootstrap_conn().roundtrip(kFindCoordinator, 0, client_id_, w.data(), timeout_ms_);
+  Reader r(resp.data(), resp.size());
+  const int16_t e = r.i16();
+  BrokerAddr b;
+  b.node_id = r.i32();
+  b.host = r.str();
+  b.port = r.i32();
+  if (e != kNone) throw WireError(e, std::string(error_name(e)) + ": FindCoordinator " + group);
+  auto old = nodes_.find(b.node_id);
+  if (old != nodes_.end() && (old->second.host != b.host || old->second.port != b.port)) drop(b.node_id);
+  nodes_[b.node_id] = b;
+  coordinator_ = b.node_id;
+  coordinator_group_ = group;
+  return coordinator_;
+}
+
+std::map<int32_t, int64_t> Client::offset_fetch(const std::string& group, const std::string& topic,
+                                                const std::vector<int32_t>& parts) {
+  Writer w;
+  w.str(group);
+  w.array(1);
+  w.str(topic);
+  w.array(int32_t(parts.size()));
+  for (int32_t p : parts) w.i32(p);
+  const int32_t node = coordinator(group);
+  auto resp = conn(node).roundtrip(kOffsetFetch, 1, client_id_, w.data(), timeout_ms_);
+  Reader r(resp.data(), resp.size());
+  std::map<int32_t, int64_t> out;
+  const int32_t nt = r.i32();
+  for (int32_t i = 0; i < nt; ++i) {
+    r.str();
+    const int32_t np = r.i32();
+    for (int32_t j = 0; j < np; ++j) {
+      const int32_t p = r.i32();
+      const int64_t off = r.i64();
+      r.str();  // metadata
+      const int16_t e = r.i16();
+      if (e != kNone) {
+        if (needs_metadata(e)) invalidate_coordinator();
+        throw WireError(e, std::string(error_name(e)) + ": OffsetFetch " + topic + "-" + std::to_string(p));
+      }
+      out[p] = off;
+    }
+  }
+  return out;
+}
+
+std::map<int32_t, int16_t> Client::offset_commit(const std::string& group, const std::string& topic,
+                                                 const std::map<int32_t, int64_t>& offsets,
+                                                 const std::string& metadata) {
+  Writer w;
+  w.str(group);
+  w.i32(-1);      // generation: a manually assigned ("simple") consumer
+  w.str("");      // member id
+  w.i64(-1);      // retention: the broker's default
+  w.array(1);
+  w.str(topic);
+  w.array(int32_t(offsets.size()));
+  for (auto& [p, o] : offsets) {
+    w.i32(p);
+    w.i64(o);
+    w.str(metadata);
+  }
+  const int32_t node = coordinator(group);
+  std::vector<uint8_t> resp;
+  try {
+    resp = conn(node).roundtrip(kOffsetCommit, 2, client_id_, w.data(), timeout_ms_);
+  } catch (const KafkaError&) {
+    drop(node);
+    invalidate_coordinator();
+    throw;
+  }
+  Reader r(resp.data(), resp.size());
+  std::map<int32_t, int16_t> out;
+  const int32_t nt = r.i32();
+  for (int32_t i = 0; i < nt; ++i) {
+    r.str();
+    const int32_t np = r.i32();
+    for (int32_t j = 0; j < np; ++j) {
+      const int32_t p = r.i32();
+      const int16_t e = r.i16();
+      if (needs_metadata(e)) invalidate_coordinator();
+      out[p] = e;
+    }
+  }
+  return out;
+}
+
+std::string fetch_request(const std::string& topic, const std::vector<FetchPartReq>& parts, int32_t max_wait_ms,
+                          int32_t min_bytes, int32_t max_bytes) {
+  Writer w;
+  w.i32(-1);  // replica id: a consumer
+  w.i32(max_wait_ms);
+  w.i32(min_bytes);
+  w.i32(max_bytes);
+  w.i8(0);    // isolation level: read_uncommitted (kafka-python's default)
+  w.array(1);
+  w.str(topic);
+  w.array(int32_t(parts.size()));
+  for (auto& p : parts) {
+    w.i32(p.partition);
+    w.i64(p.offset);
+    w.i32(p.max_bytes);
+  }
+  return std::move(w.data());
+}
+
+}  // namespace tk::wire

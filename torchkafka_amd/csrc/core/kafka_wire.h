@@ -1,0 +1,200 @@
+// Native Kafka wire-protocol client (the part of a consumer this framework needs).
+//
+// The reference reaches its cluster through kafka-python's KafkaConsumer
+// (kafka_dataset.py:21-22, 206): a Python client that parses every Fetch response, checks
+// every RecordBatch CRC on the CPU and hands out Python records one by one.  Here the
+// cluster is read by a native replicator (replicator.h) that speaks the protocol directly:
+// Fetch responses are received straight into the local partition logs (the same mapped
+// RecordBatch v2 logs the synthetic broker keeps), so workers walk headers and the gfx950
+// decode kernels verify CRCs and decode values from those bytes exactly as they do for the
+// synthetic broker -- no Python, no per-record objects, no second host copy.
+//
+// Protocol subset (non-flexible request versions, understood by Kafka 0.11 .. 3.x brokers):
+//   ApiVersions v0, Metadata v1, ListOffsets v1, Fetch v4 (RecordBatch v2, read_uncommitted),
+//   FindCoordinator v0, OffsetCommit v2, OffsetFetch v1.
+// Group membership (JoinGroup/SyncGroup) is not used: partitions are assigned statically by
+// (rank, worker) as in the rest of the framework, and offsets are committed like kafka-python's
+// manually-assigned consumer with a group_id (generation -1, empty member id).
+#pragma once
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "common.h"
+
+namespace tk::wire {
+
+enum ApiKey : int16_t {
+  kFetch = 1, kListOffsets = 2, kMetadata = 3, kOffsetCommit = 8, kOffsetFetch = 9,
+  kFindCoordinator = 10, kApiVersions = 18,
+};
+
+// Kafka error codes the client acts on.
+enum ErrorCode : int16_t {
+  kNone = 0, kOffsetOutOfRange = 1, kCorruptMessage = 2, kUnknownTopicOrPartition = 3,
+  kLeaderNotAvailable = 5, kNotLeaderForPartition = 6, kRequestTimedOut = 7,
+  kCoordinatorLoadInProgress = 14, kCoordinatorNotAvailable = 15, kNotCoordinator = 16,
+  kIllegalGeneration = 22, kUnknownMemberId = 25, kRebalanceInProgress = 27,
+};
+const char* error_name(int16_t code);
+// Errors after which the partition's leader (or the group's coordinator) must be looked up again.
+inline bool needs_metadata(int16_t e) {
+  return e == kUnknownTopicOrPartition || e == kLeaderNotAvailable || e == kNotLeaderForPartition ||
+         e == kCoordinatorNotAvailable || e == kNotCoordinator || e == kCoordinatorLoadInProgress ||
+         e == kRequestTimedOut;
+}
+
+struct WireError : KafkaError {
+  int16_t code;
+  WireError(int16_t c, const std::string& what) : KafkaError(what), code(c) {}
+};
+
+// ------------------------------------------------------------ encoding (big-endian)
+class Writer {
+ public:
+  void i8(int8_t v) { buf_.push_back(char(v)); }
+  void i16(int16_t v);
+  void i32(int32_t v);
+  void i64(int64_t v);
+  void str(const std::string& s);   // int16 length + bytes
+  void nullable_str_null() { i16(-1); }
+  void array(int32_t n) { i32(n); }
+  std::string& data() { return buf_; }
+
+ private:
+  std::string buf_;
+};
+
+class Reader {
+ public:
+  Reader(const uint8_t* p, size_t n) : p_(p), end_(p + n) {}
+  int8_t i8();
+  int16_t i16();
+  int32_t i32();
+  int64_t i64();
+  std::string str();          // nullable: null -> ""
+  const uint8_t* bytes(int32_t* len);  // nullable bytes (int32 length; null -> len -1)
+  size_t left() const { return size_t(end_ - p_); }
+
+ private:
+  void need(size_t n) const;
+  const uint8_t* p_;
+  const uint8_t* end_;
+};
+
+// ------------------------------------------------------------ one TCP connection
+class Conn {
+ public:
+  Conn(const std::string& host, int port, int timeout_ms);
+  ~Conn();
+  Conn(const Conn&) = delete;
+  Conn& operator=(const Conn&) = delete;
+  const std::string& host() const { return host_; }
+  int port() const { return port_; }
+  bool ok() const { return fd_ >= 0; }
+
+  // Request/response with the whole response body in memory (small responses).
+  std::vector<uint8_t> roundtrip(int16_t api_key, int16_t api_version, const std::string& client_id,
+                                 const std::string& body, int timeout_ms);
+
+  // Streaming responses (Fetch): send, then read the body field by field; record sets are
+  // received straight into the caller's memory.
+  void send(int16_t api_key, int16_t api_version, const std::string& client_id, const std::string& body);
+  size_t begin_response(int timeout_ms);  // reads size + correlation id; returns body bytes
+  void read(void* dst, size_t n);
+  int8_t r8();
+  int16_t r16();
+  int32_t r32();
+  int64_t r64();
+  std::string rstr();
+  void skip(size_t n);
+  void finish();  // drains the rest of the current response
+  size_t remaining() const { return remaining_; }
+  void close();
+
+ private:
+  void send_all(const std::string& frame);
+  void fill(size_t want);  // at least min(want, remaining) bytes buffered
+  std::string host_;
+  int port_;
+  int fd_ = -1;
+  int timeout_ms_;
+  int64_t deadline_ms_ = 0;
+  int32_t corr_ = 0;
+  int32_t expect_corr_ = -1;
+  size_t remaining_ = 0;
+  std::vector<uint8_t> buf_;
+  size_t b0_ = 0, b1_ = 0;
+};
+
+// ------------------------------------------------------------ cluster view
+struct BrokerAddr {
+  int32_t node_id;
+  std::string host;
+  int32_t port;
+};
+struct PartitionMeta {
+  int32_t partition;
+  int32_t leader;  // -1 when none
+  int16_t error;
+};
+struct TopicMeta {
+  std::string name;
+  int16_t error = 0;
+  std::vector<PartitionMeta> partitions;  // sorted by partition id
+};
+
+struct FetchPartReq {
+  int32_t partition;
+  int64_t offset;
+  int32_t max_bytes;
+};
+
+class Client {
+ public:
+  // bootstrap: "host:port[,host:port...]" (an optional "kafka://" prefix is accepted).
+  Client(const std::string& bootstrap, const std::string& client_id, int timeout_ms);
+  static std::vector<std::pair<std::string, int>> parse_bootstrap(const std::string& s);
+
+  TopicMeta metadata(const std::string& topic);          // refreshes the broker table too
+  std::vector<BrokerAddr> brokers();
+  // ListOffsets: timestamp -2 = earliest, -1 = latest, else first offset with ts >= timestamp.
+  std::map<int32_t, int64_t> list_offsets(const std::string& topic, const std::vector<int32_t>& parts,
+                                          int64_t timestamp);
+  std::map<int32_t, int64_t> offset_fetch(const std::string& group, const std::string& topic,
+                                          const std::vector<int32_t>& parts);
+  // Returns per-partition error codes (0 = committed).
+  std::map<int32_t, int16_t> offset_commit(const std::string& group, const std::string& topic,
+                                           const std::map<int32_t, int64_t>& offsets,
+                                           const std::string& metadata = "");
+  void invalidate_coordinator() { coordinator_ = -1; }
+
+  // Connection to a node (-1: any bootstrap server).  Owned by the client; one per node.
+  Conn& conn(int32_t node_id);
+  void drop(int32_t node_id);
+  const std::string& client_id() const { return client_id_; }
+  int timeout_ms() const { return timeout_ms_; }
+  int32_t leader(const std::string& topic, int32_t partition);  // cached, -1 unknown
+
+ private:
+  Conn& bootstrap_conn();
+  int32_t coordinator(const std::string& group);
+  std::vector<std::pair<std::string, int>> bootstrap_;
+  std::string client_id_;
+  int timeout_ms_;
+  std::map<int32_t, BrokerAddr> nodes_;
+  std::map<int32_t, std::unique_ptr<Conn>> conns_;  // node -> connection (-1: bootstrap)
+  std::map<std::string, TopicMeta> topics_;
+  int32_t coordinator_ = -1;
+  std::string coordinator_group_;
+};
+
+// Encodes a Fetch v4 request body (tests and the replicator share it).
+std::string fetch_request(const std::string& topic, const std::vector<FetchPartReq>& parts, int32_t max_wait_ms,
+                          int32_t min_bytes, int32_t max_bytes);
+
+}  // namespace tk::wire

@@ -1,0 +1,360 @@
+// Kafka cluster -> local partition logs: see replicator.h.
+#include "replicator.h"
+
+#include <algorithm>
+#include <chrono>
+#include <set>
+
+namespace tk {
+
+namespace {
+void sleep_ms(int ms) { std::this_thread::sleep_for(std::chrono::milliseconds(ms)); }
+}  // namespace
+
+Replicator::Replicator(std::shared_ptr<Broker> local, ReplicaConfig cfg) : local_(std::move(local)), cfg_(std::move(cfg)) {
+  if (cfg_.topic.empty()) throw std::invalid_argument("replicator: a topic is required");
+  if (cfg_.auto_offset_reset != "earliest" && cfg_.auto_offset_reset != "latest" &&
+      cfg_.auto_offset_reset != "smallest" && cfg_.auto_offset_reset != "largest")
+    throw std::invalid_argument("replicator: auto_offset_reset must be 'earliest' or 'latest'");
+  if (cfg_.partition_max_bytes < 4096 || cfg_.max_bytes < cfg_.partition_max_bytes)
+    throw std::invalid_argument("replicator: need 4096 <= partition_max_bytes <= max_bytes");
+}
+
+Replicator::~Replicator() {
+  try {
+    stop(false);
+  } catch (...) {
+  }
+}
+
+void Replicator::set_error(const std::string& e) {
+  errors_.fetch_add(1);
+  std::lock_guard<std::mutex> g(err_mu_);
+  last_error_ = e;
+}
+
+std::string Replicator::last_error() {
+  std::lock_guard<std::mutex> g(err_mu_);
+  return last_error_;
+}
+
+void Replicator::start() {
+  if (running_.load()) return;
+  wire::Client c(cfg_.bootstrap, cfg_.client_id, cfg_.timeout_ms);
+  wire::TopicMeta t = c.metadata(cfg_.topic);
+  if (t.error != wire::kNone || t.partitions.empty())
+    throw wire::WireError(t.error ? t.error : int16_t(wire::kUnknownTopicOrPartition),
+                          std::string(wire::error_name(t.error)) + ": topic '" + cfg_.topic + "'");
+  n_remote_parts_ = int32_t(t.partitions.size());
+  TopicInfo ti;
+  if (!local_->find_topic(cfg_.topic, &ti)) ti = local_->create_topic(cfg_.topic, uint32_t(n_remote_parts_),
+                                                                     cfg_.log_capacity, cfg_.index_capacity);
+  if (int32_t(ti.n_partitions) != n_remote_parts_)
+    throw KafkaError("replicator: local topic '" + cfg_.topic + "' has " + std::to_string(ti.n_partitions) +
+                     " partitions, the cluster " + std::to_string(n_remote_parts_));
+  first_pidx_ = ti.first_pidx;
+  std::vector<int32_t> ids = cfg_.partitions;
+  if (ids.empty())
+    for (auto& p : t.partitions) ids.push_back(p.partition);
+  std::sort(ids.begin(), ids.end());
+  ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+  for (int32_t id : ids)
+    if (id < 0 || id >= n_remote_parts_)
+      throw KafkaError("UnknownTopicOrPartitionError: " + cfg_.topic + "-" + std::to_string(id));
+
+  std::map<int32_t, int64_t> committed;
+  if (!cfg_.group.empty()) {
+    group_ = local_->group_index(cfg_.group, true);
+    committed = c.offset_fetch(cfg_.group, cfg_.topic, ids);
+  }
+  std::vector<int32_t> need_reset;
+  for (int32_t id : ids) {
+    auto it = committed.find(id);
+    if (it == committed.end() || it->second < 0) need_reset.push_back(id);
+  }
+  const bool latest = cfg_.auto_offset_reset == "latest" || cfg_.auto_offset_reset == "largest";
+  std::map<int32_t, int64_t> reset;
+  if (!need_reset.empty()) reset = c.list_offsets(cfg_.topic, need_reset, latest ? -1 : -2);
+
+  parts_.clear();
+  for (int32_t id : ids) {
+    auto p = std::make_unique<Part>();
+    p->partition = id;
+    p->pidx = first_pidx_ + uint32_t(id);
+    auto ci = committed.find(id);
+    const int64_t remote_committed = ci != committed.end() ? ci->second : -1;
+    const int64_t start = remote_committed >= 0 ? remote_committed : reset.at(id);
+    PartitionEntry& P = local_->part(p->pidx);
+    if (P.n_batches.load() == 0) {
+      local_->reset_empty(p->pidx, start);
+      p->fetch_offset = start;
+    } else {
+      p->fetch_offset = P.high_watermark.load();  // a persistent (file://) replica resumes its log
+    }
+    p->start_offset = start;
+    p->forwarded = remote_committed;
+    if (remote_committed >= 0 && !cfg_.group.empty() && local_->committed(group_, p->pidx) < remote_committed) {
+      try {
+        local_->commit(group_, -1, 0, 0, {CommitEntry{p->pidx, remote_committed, std::string()}});
+      } catch (const KafkaError& e) {
+        set_error(std::string("replicator: seeding the local committed offset failed: ") + e.what());
+      }
+    }
+    parts_.push_back(std::move(p));
+  }
+
+  // fetch threads: partitions grouped by leader, leaders spread over the threads
+  std::map<int32_t, std::vector<Part*>> by_leader;
+  for (auto& p : parts_) by_leader[c.leader(cfg_.topic, p->partition)].push_back(p.get());
+  int n_threads = cfg_.fetchers > 0 ? cfg_.fetchers : std::min<int>(8, int(by_leader.size()));
+  n_threads = std::max(1, std::min<int>(n_threads, int(parts_.size())));
+  std::vector<std::vector<Part*>> per(static_cast<size_t>(n_threads));
+  size_t k = 0;
+  for (auto& [leader, ps] : by_leader)
+    for (Part* p : ps) per[(k++) % per.size()].push_back(p);
+  stop_ = false;
+  running_ = true;
+  for (auto& v : per)
+    if (!v.empty()) threads_.emplace_back([this, v]() { fetch_loop(v); });
+  if (!cfg_.group.empty()) {
+    commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", cfg_.timeout_ms);
+    threads_.emplace_back([this]() { commit_loop(); });
+  }
+}
+
+void Replicator::stop(bool flush) {
+  if (!running_.load() && threads_.empty()) return;
+  stop_ = true;
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  threads_.clear();
+  running_ = false;
+  if (flush && !cfg_.group.empty()) {
+    for (int attempt = 0; attempt < 3; ++attempt) {
+      try {
+        if (!commit_client_)
+          commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", cfg_.timeout_ms);
+        forward(*commit_client_);
+        break;
+      } catch (const KafkaError& e) {
+        set_error(std::string("replicator: final commit: ") + e.what());
+        commit_client_.reset();
+        sleep_ms(50 << attempt);
+      }
+    }
+  }
+}
+
+bool Replicator::throttled(Part& p) {
+  const PartitionEntry& P = local_->part(p.pidx);
+  const uint64_t end = P.log_end_pos.load(std::memory_order_acquire);
+  if (end == 0) return false;
+  int64_t c = cfg_.group.empty() ? -1 : local_->committed(group_, p.pidx);
+  if (c < 0) c = p.start_offset;
+  const uint64_t pos = local_->position_of(p.pidx, c);
+  return end > pos && int64_t(end - pos) > cfg_.max_lag_bytes;
+}
+
+void Replicator::reset_offset(wire::Client& c, Part& p) {
+  const bool latest = cfg_.auto_offset_reset == "latest" || cfg_.auto_offset_reset == "largest";
+  auto r = c.list_offsets(cfg_.topic, {p.partition}, latest ? -1 : -2);
+  p.fetch_offset = r.at(p.partition);
+  set_error("OffsetOutOfRangeError: " + cfg_.topic + "-" + std::to_string(p.partition) + " reset to offset " +
+            std::to_string(p.fetch_offset.load()));
+}
+
+void Replicator::fetch_loop(std::vector<Part*> mine) {
+  std::unique_ptr<wire::Client> c;
+  std::set<Part*> failed;
+  int backoff_ms = 0;
+  while (!stop_.load()) {
+    try {
+      if (!c) {
+        c = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id, cfg_.timeout_ms);
+        c->metadata(cfg_.topic);
+      }
+      std::map<int32_t, std::vector<Part*>> by;
+      bool unknown_leader = false;
+      for (Part* p : mine) {
+        if (failed.count(p)) continue;
+        if (throttled(*p)) {
+          p->throttled.fetch_add(1, std::memory_order_relaxed);
+          continue;
+        }
+        const int32_t node = c->leader(cfg_.topic, p->partition);
+        if (node < 0) unknown_leader = true; else by[node].push_back(p);
+      }
+      if (unknown_leader) c->metadata(cfg_.topic);
+      if (by.empty()) {
+        sleep_ms(unknown_leader ? 50 : 1);
+        continue;
+      }
+      const int32_t wait = by.size() > 1 ? std::min<int32_t>(cfg_.max_wait_ms, 10) : cfg_.max_wait_ms;
+      bool refresh = false;
+      for (auto& [node, ps] : by) {
+        std::vector<wire::FetchPartReq> req;
+        std::map<int32_t, Part*> lookup;
+        for (Part* p : ps) {
+          uint64_t avail = 0;
+          local_->log_tail(p->pidx, &avail);
+          if (avail < 4096) {
+            if (!failed.count(p))
+              set_error("replicator: local log of " + cfg_.topic + "-" + std::to_string(p->partition) +
+                        " is full (raise log_capacity)");
+            failed.insert(p);
+            continue;
+          }
+          req.push_back({p->partition, p->fetch_offset.load(),
+                         int32_t(std::min<uint64_t>(uint64_t(cfg_.partition_max_bytes), avail))});
+          lookup[p->partition] = p;
+        }
+        if (req.empty()) continue;
+        wire::Conn& k = c->conn(node);
+        k.send(wire::kFetch, 4, c->client_id(),
+               wire::fetch_request(cfg_.topic, req, wait, cfg_.min_bytes, cfg_.max_bytes));
+        k.begin_response(cfg_.timeout_ms + wait);
+        k.r32();  // throttle_time_ms
+        const int32_t nt = k.r32();
+        for (int32_t i = 0; i < nt; ++i) {
+          k.rstr();
+          const int32_t np = k.r32();
+          for (int32_t j = 0; j < np; ++j) {
+            const int32_t pid = k.r32();
+            const int16_t err = k.r16();
+            const int64_t hw = k.r64();
+            k.r64();  // last stable offset
+            const int32_t n_aborted = k.r32();
+            if (n_aborted > 0) k.skip(size_t(n_aborted) * 16);
+            const int32_t len = k.r32();
+            auto it = lookup.find(pid);
+            Part* p = it == lookup.end() ? nullptr : it->second;
+            if (!p || err != wire::kNone) {
+              if (len > 0) k.skip(size_t(len));
+              if (!p) continue;
+              if (err == wire::kOffsetOutOfRange) {
+                reset_offset(*c, *p);
+              } else {
+                set_error(std::string(wire::error_name(err)) + ": fetch " + cfg_.topic + "-" + std::to_string(pid));
+                if (wire::needs_metadata(err)) refresh = true;
+              }
+              continue;
+            }
+            p->remote_hw.store(hw, std::memory_order_relaxed);
+            p->fetches.fetch_add(1, std::memory_order_relaxed);
+            if (len <= 0) continue;
+            uint64_t avail = 0;
+            uint8_t* tail = local_->log_tail(p->pidx, &avail);
+            if (uint64_t(len) > avail) {  // an oversized first batch (KIP-74) the log cannot hold
+              k.skip(size_t(len));
+              set_error("replicator: local log of " + cfg_.topic + "-" + std::to_string(pid) + " is full");
+              failed.insert(p);
+              continue;
+            }
+            k.read(tail, size_t(len));  // the record set lands in the log tail: no second copy
+            try {
+              const Broker::Ingested in = local_->ingest(p->pidx, uint64_t(len), p->fetch_offset.load());
+              if (in.next_offset > p->fetch_offset.load()) p->fetch_offset.store(in.next_offset);
+              p->bytes.fetch_add(in.kept_bytes, std::memory_order_relaxed);
+              p->batches.fetch_add(in.kept, std::memory_order_relaxed);
+              p->control.fetch_add(in.control, std::memory_order_relaxed);
+            } catch (const KafkaError& e) {  // compressed / corrupt / old-format data: this partition stops
+              set_error(std::string("replicator: ") + cfg_.topic + "-" + std::to_string(pid) + ": " + e.what());
+              failed.insert(p);
+            }
+          }
+        }
+        k.finish();
+      }
+      if (refresh) {
+        c->metadata(cfg_.topic);
+        sleep_ms(10);
+      }
+      backoff_ms = 0;
+    } catch (const std::exception& e) {
+      set_error(std::string("replicator: ") + e.what());
+      c.reset();  // reconnect + fresh metadata
+      backoff_ms = std::min(1000, std::max(10, backoff_ms * 2));
+      for (int s = 0; s < backoff_ms && !stop_.load(); s += 10) sleep_ms(10);
+    }
+  }
+}
+
+int Replicator::forward(wire::Client& c) {
+  std::lock_guard<std::mutex> g(commit_mu_);
+  std::map<int32_t, int64_t> offs;
+  std::map<int32_t, Part*> by;
+  for (auto& p : parts_) {
+    const int64_t off = local_->committed(group_, p->pidx);
+    if (off >= 0 && off != p->forwarded.load()) {
+      offs[p->partition] = off;
+      by[p->partition] = p.get();
+    }
+  }
+  if (offs.empty()) return 0;
+  int n = 0;
+  auto errs = c.offset_commit(cfg_.group, cfg_.topic, offs);
+  for (auto& [pid, e] : errs) {
+    auto it = by.find(pid);
+    if (it == by.end()) continue;
+    if (e == wire::kNone) {
+      it->second->forwarded.store(offs[pid]);
+      ++n;
+    } else {
+      set_error(std::string("CommitFailedError: ") + wire::error_name(e) + " committing " + cfg_.topic + "-" +
+                std::to_string(pid));
+    }
+  }
+  return n;
+}
+
+int Replicator::flush_commits() {
+  if (cfg_.group.empty()) return 0;
+  wire::Client c(cfg_.bootstrap, cfg_.client_id + "-flush", cfg_.timeout_ms);
+  return forward(c);
+}
+
+void Replicator::commit_loop() {
+  int backoff_ms = cfg_.commit_interval_ms;
+  while (!stop_.load()) {
+    for (int s = 0; s < backoff_ms && !stop_.load(); s += 1) sleep_ms(1);
+    if (stop_.load()) break;
+    try {
+      if (!commit_client_)
+        commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", cfg_.timeout_ms);
+      forward(*commit_client_);
+      backoff_ms = cfg_.commit_interval_ms;
+    } catch (const std::exception& e) {
+      set_error(std::string("replicator: commit: ") + e.what());
+      commit_client_.reset();
+      backoff_ms = std::min(1000, std::max(10, backoff_ms * 2));
+    }
+  }
+}
+
+std::vector<ReplicaPartStats> Replicator::stats() {
+  std::vector<ReplicaPartStats> v;
+  for (auto& p : parts_)
+    v.push_back(ReplicaPartStats{p->partition, p->pidx, p->start_offset, p->fetch_offset.load(), p->remote_hw.load(),
+                                 p->forwarded.load(), p->bytes.load(), p->batches.load(), p->control.load(),
+                                 p->fetches.load(), p->throttled.load()});
+  return v;
+}
+
+bool Replicator::wait_caught_up(int timeout_ms) {
+  std::vector<int32_t> ids;
+  for (auto& p : parts_) ids.push_back(p->partition);
+  if (ids.empty()) return true;
+  wire::Client c(cfg_.bootstrap, cfg_.client_id + "-lag", cfg_.timeout_ms);
+  auto hw = c.list_offsets(cfg_.topic, ids, -1);
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  while (std::chrono::steady_clock::now() < deadline) {
+    bool all = true;
+    for (auto& p : parts_)
+      if (p->fetch_offset.load() < hw[p->partition]) all = false;
+    if (all) return true;
+    sleep_ms(2);
+  }
+  return false;
+}
+
+}  // namespace tk

@@ -1,0 +1,123 @@
+// Kafka cluster -> local partition logs: the native bridge between a real cluster and the
+// device path.
+//
+// The reference consumes through kafka-python (kafka_dataset.py:21-22, 206-210): every worker
+// owns a KafkaConsumer whose fetcher parses each response in Python and CRC-checks every batch
+// on the CPU before `_process` sees a record.  Here one native replicator per rank (threads,
+// no GIL) fetches the rank's partitions over the Kafka protocol (kafka_wire.h) and receives
+// each response's record set directly into the tail of a local partition log -- the same
+// mapped RecordBatch v2 logs the synthetic broker serves.  Everything downstream is unchanged:
+// workers walk record headers in those logs, the main process pins them, and the gfx950
+// kernels verify CRC32C and decode values from them (span_decode.hip / json_span.hip).
+// Offsets are preserved, so what the loader commits into the local offset table is exactly the
+// cluster's offset; a committer thread forwards those commits to the group coordinator
+// (OffsetCommit), and close() flushes the last one.
+//
+// Flow control: a partition is not fetched while its replicated-but-uncommitted bytes exceed
+// `max_lag_bytes` (the loader commits every batch, so this bounds host memory per partition).
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "broker.h"
+#include "kafka_wire.h"
+
+namespace tk {
+
+struct ReplicaConfig {
+  std::string bootstrap;               // "host:port[,host:port]" (kafka:// accepted)
+  std::string topic;
+  std::string group;                   // committed offsets: read at start, forwarded on commit
+  std::string client_id = "torchkafka-replicator";
+  std::vector<int32_t> partitions;     // empty: every partition of the topic
+  std::string auto_offset_reset = "earliest";  // without a committed offset: earliest | latest
+  int32_t max_wait_ms = 100;
+  int32_t min_bytes = 1;
+  int32_t max_bytes = 64 << 20;        // per Fetch response
+  int32_t partition_max_bytes = 8 << 20;
+  int32_t timeout_ms = 30000;
+  int64_t max_lag_bytes = int64_t(1) << 30;
+  int32_t commit_interval_ms = 5;
+  int32_t fetchers = 0;                // fetch threads (0: one per partition leader, at most 8)
+  uint64_t log_capacity = 0;           // local topic creation (0: the broker default)
+  uint64_t index_capacity = 0;
+};
+
+struct ReplicaPartStats {
+  int32_t partition;
+  uint32_t pidx;
+  int64_t start_offset;
+  int64_t fetch_offset;
+  int64_t remote_hw;
+  int64_t forwarded;        // last offset committed to the cluster (-1 none)
+  uint64_t bytes;
+  uint64_t batches;
+  uint64_t control_batches;
+  uint64_t fetches;
+  uint64_t throttled;       // fetch rounds skipped by flow control
+};
+
+class Replicator {
+ public:
+  Replicator(std::shared_ptr<Broker> local, ReplicaConfig cfg);
+  ~Replicator();
+  Replicator(const Replicator&) = delete;
+  Replicator& operator=(const Replicator&) = delete;
+
+  // Metadata, local topic, start positions (committed offset, else auto_offset_reset), threads.
+  void start();
+  // Stops fetching; forwards the latest local commits first when `flush`.
+  void stop(bool flush = true);
+  // Forwards every changed local commit to the coordinator now; returns partitions committed.
+  int flush_commits();
+  bool running() const { return running_.load(); }
+  std::string last_error();
+  int64_t errors() const { return errors_.load(); }
+  std::vector<ReplicaPartStats> stats();
+  uint32_t first_pidx() const { return first_pidx_; }
+  int32_t n_partitions() const { return n_remote_parts_; }
+  // Blocks until every replicated partition has fetched up to the cluster's high watermark as
+  // seen at call time (tests, tools); false on timeout.
+  bool wait_caught_up(int timeout_ms);
+
+ private:
+  struct Part {
+    int32_t partition;
+    uint32_t pidx;
+    int64_t start_offset = 0;
+    std::atomic<int64_t> fetch_offset{0};
+    std::atomic<int64_t> remote_hw{-1};
+    std::atomic<int64_t> forwarded{-1};
+    std::atomic<uint64_t> bytes{0}, batches{0}, control{0}, fetches{0}, throttled{0};
+    int64_t scratch_len = 0;  // record-set bytes that did not fit the tail (dropped, refetched)
+  };
+  void fetch_loop(std::vector<Part*> mine);
+  void commit_loop();
+  bool throttled(Part& p);
+  void reset_offset(wire::Client& c, Part& p);
+  void set_error(const std::string& e);
+  int forward(wire::Client& c);
+
+  std::shared_ptr<Broker> local_;
+  ReplicaConfig cfg_;
+  uint32_t group_ = 0;
+  uint32_t first_pidx_ = 0;
+  int32_t n_remote_parts_ = 0;
+  std::vector<std::unique_ptr<Part>> parts_;
+  std::vector<std::thread> threads_;
+  std::atomic<bool> running_{false};
+  std::atomic<bool> stop_{false};
+  std::atomic<int64_t> errors_{0};
+  std::mutex err_mu_;
+  std::string last_error_;
+  std::mutex commit_mu_;  // serialises forward() between the committer thread and flush_commits()
+  std::unique_ptr<wire::Client> commit_client_;
+};
+
+}  // namespace tk
