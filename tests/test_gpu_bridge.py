@@ -61,3 +61,43 @@ def test_device_decode_from_a_replicated_cluster(broker, live):
     assert d.shape == h.shape == (4800, 256)
     key = lambda t: (t[:, 1].float() * 1e6 + t[:, 0].float()).argsort()  # noqa: E731 -- (partition, offset) order
     assert torch.equal(d[key(d)].view(torch.int32), h[key(h)].view(torch.int32))
+
+
+def test_long_stream_unpins_and_releases_consumed_log(broker):
+    """A replica stream longer than the driver's 64 MiB pin chunks: committed ranges are unpinned
+    by the driver and punched out of the replica files by the replicator, and decoding goes on."""
+    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
+    from torchkafka_amd.broker import KafkaBridge, KafkaWireServer, SyntheticBroker
+
+    class Rows(KafkaDataset):
+        schema = FixedWidth(torch.float32, (256,))
+
+    src = SyntheticBroker.create(f"shm://tkgsrc-{os.getpid()}-{uuid.uuid4().hex[:6]}", log_capacity=512 << 20)
+    try:
+        src.create_topic("t", 1)
+        src.fill("t", 160_000, "fixed_f32", size=256, records_per_batch=64)  # ~165 MB
+        with KafkaWireServer(src) as srv:
+            br = KafkaBridge(srv.address, "t", group_id="g", url=f"shm://tkgbr-{os.getpid()}-{uuid.uuid4().hex[:6]}",
+                             log_capacity=512 << 20, max_lag_bytes=96 << 20, release_bytes=16 << 20)
+            try:
+                dl = DeviceLoader(Rows.placeholder(), 256, num_workers=1, device="cuda:0", dtype=torch.float32,
+                                  worker_init_fn=Rows.init_worker("t", bootstrap_servers=br.url, group_id="g",
+                                                                  auto_offset_reset="earliest",
+                                                                  consumer_timeout_ms=1000))
+                assert dl._span()
+                n, last = 0, -1
+                for x in auto_commit(dl):
+                    offs = x[:, 0]
+                    assert int(offs[0].item()) == last + 1  # one partition, in order
+                    last = int(offs[-1].item())
+                    n += x.shape[0]
+                torch.cuda.synchronize()
+                assert n == 160_000 and last == 159_999
+                assert dl.stats.log_bytes_unpinned >= 64 << 20
+                released = br.stats()[0]["released"]
+                assert released >= 64 << 20, br.stats()
+            finally:
+                br.close()
+        assert src.committed("g", "t", 0) == 160_000
+    finally:
+        src.destroy()

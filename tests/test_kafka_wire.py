@@ -220,3 +220,29 @@ def test_bridge_partition_subset_per_rank(broker, server):
 def test_unreachable_cluster_raises():
     with pytest.raises(Exception, match="NoBrokersAvailable"):
         KafkaBridge("127.0.0.1:1", "t", url=f"shm://tkbr-none-{os.getpid()}", request_timeout_ms=500)
+
+
+def test_committed_log_bytes_are_released(broker, server):
+    """A replica frees what its group committed: log start moves up, the bytes below are punched
+    out of the shm file (st_blocks drops), consumers carry on from the committed offset."""
+    broker.create_topic("t", 1)
+    broker.fill("t", 10000, "fixed_f32", size=256, records_per_batch=64)  # ~10.3 MB
+    with bridge(server, group_id="g", release_bytes=2 << 20, log_capacity=64 << 20) as br:
+        assert br.wait_caught_up(10)
+        pidx = br.local.pidx("t", 0)
+        path = os.path.join(br.local.dir, f"p{pidx:05d}.log")
+        before = os.stat(path).st_blocks * 512
+        assert before >= 9 << 20
+        dl = DeviceLoader(Vec256.placeholder(), 256, device="cpu", num_workers=1,
+                          worker_init_fn=Vec256.init_worker("t", bootstrap_servers=br.url, group_id="g",
+                                                            auto_offset_reset="earliest", consumer_timeout_ms=300))
+        n = sum(x.shape[0] for x in auto_commit(dl))
+        assert n == 10000
+        assert wait_for(lambda: br.stats()[0]["released"] >= 6 << 20)
+        assert os.stat(path).st_blocks * 512 <= before - (6 << 20)
+        assert br.local.beginning_offset("t", 0) > 0
+    assert broker.committed("g", "t", 0) == 10000
+
+
+class Vec256(KafkaDataset):
+    schema = FixedWidth(torch.float32, (256,))

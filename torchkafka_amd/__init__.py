@@ -11,17 +11,22 @@ from .config import LoaderConfig, Tuning
 from .loader import DeviceLoader, KafkaBatch, auto_commit
 from .models import FixedWidth, JsonArray, KafkaDataset, VarLen
 
-__version__ = "1.2.0+mi355x.1"
+__version__ = "1.2.0+mi355x.4"
 
 __all__ = ["KafkaDataset", "auto_commit", "DeviceLoader", "KafkaBatch", "LoaderConfig", "Tuning", "FixedWidth",
-           "VarLen", "JsonArray", "SyntheticBroker", "KafkaConsumer", "KafkaProducer"]
+           "VarLen", "JsonArray", "SyntheticBroker", "KafkaBridge", "KafkaWireServer", "KafkaConsumer",
+           "KafkaProducer", "TopicPartition"]
 
 
 def __getattr__(name):
-    if name == "SyntheticBroker":
-        from .broker import SyntheticBroker
+    if name in ("SyntheticBroker", "KafkaBridge", "KafkaWireServer"):
+        from . import broker
 
-        return SyntheticBroker
+        return getattr(broker, name)
+    if name == "TopicPartition":
+        from .client.records import TopicPartition
+
+        return TopicPartition
     if name in ("KafkaConsumer", "KafkaProducer"):
         from . import client
 

@@ -19,6 +19,12 @@ the last one::
         ...
     bridge.close()          # forwards the final commit
 
+Memory: with a ``group_id`` the committed part of every replica log is released (the log start
+moves up to the committed offset, the bytes below it are punched out of the shm files and the
+device loader unpins them), so a long stream holds about ``max_lag_bytes`` per partition in host
+memory, not the whole stream; ``log_capacity`` (sparse) bounds the bytes one replica partition
+can take in over its lifetime.
+
 Semantics: at-least-once, like the reference's commit-after-batch.  A commit lands in the local
 table synchronously and reaches the cluster within ``commit_interval_ms`` (5 ms); a crash in
 between replays at most that window's batches.  Records are fetched read_uncommitted, control
@@ -48,7 +54,8 @@ class KafkaBridge:
                  log_capacity: int = 64 << 30, index_capacity: int = 1 << 22, fetch_max_wait_ms: int = 100,
                  fetch_max_bytes: int = 64 << 20, max_partition_fetch_bytes: int = 8 << 20,
                  request_timeout_ms: int = 30000, commit_interval_ms: int = 5, fetchers: int = 0,
-                 client_id: str = "torchkafka-bridge", start: bool = True):
+                 client_id: str = "torchkafka-bridge", release_consumed: bool = True,
+                 release_bytes: int = 64 << 20, start: bool = True):
         if not isinstance(bootstrap_servers, str):
             bootstrap_servers = ",".join(bootstrap_servers)
         self.bootstrap_servers = bootstrap_servers
@@ -65,7 +72,8 @@ class KafkaBridge:
             auto_offset_reset=auto_offset_reset, max_wait_ms=int(fetch_max_wait_ms), max_bytes=int(fetch_max_bytes),
             partition_max_bytes=int(max_partition_fetch_bytes), timeout_ms=int(request_timeout_ms),
             max_lag_bytes=int(max_lag_bytes), commit_interval_ms=int(commit_interval_ms), fetchers=int(fetchers),
-            log_capacity=int(log_capacity), index_capacity=int(index_capacity), client_id=client_id)
+            log_capacity=int(log_capacity), index_capacity=int(index_capacity), client_id=client_id,
+            release_consumed=bool(release_consumed), release_bytes=int(release_bytes))
         self._closed = False
         self._lock = threading.Lock()
         self._reported = 0

@@ -462,7 +462,8 @@ PYBIND11_MODULE(_tkcore, m) {
                        const std::string& group, std::vector<int32_t> partitions, const std::string& reset,
                        int32_t max_wait_ms, int32_t max_bytes, int32_t partition_max_bytes, int32_t timeout_ms,
                        int64_t max_lag_bytes, int32_t commit_interval_ms, int32_t fetchers, uint64_t log_capacity,
-                       uint64_t index_capacity, const std::string& client_id) {
+                       uint64_t index_capacity, const std::string& client_id, bool release_consumed,
+                       uint64_t release_bytes) {
              ReplicaConfig c;
              c.bootstrap = bootstrap;
              c.topic = topic;
@@ -479,6 +480,8 @@ PYBIND11_MODULE(_tkcore, m) {
              c.log_capacity = log_capacity;
              c.index_capacity = index_capacity;
              c.client_id = client_id;
+             c.release_consumed = release_consumed;
+             c.release_bytes = release_bytes;
              return std::make_unique<Replicator>(std::move(local), c);
            }),
            py::arg("local"), py::arg("bootstrap"), py::arg("topic"), py::arg("group") = "",
@@ -486,7 +489,8 @@ PYBIND11_MODULE(_tkcore, m) {
            py::arg("max_wait_ms") = 100, py::arg("max_bytes") = 64 << 20, py::arg("partition_max_bytes") = 8 << 20,
            py::arg("timeout_ms") = 30000, py::arg("max_lag_bytes") = int64_t(1) << 30,
            py::arg("commit_interval_ms") = 5, py::arg("fetchers") = 0, py::arg("log_capacity") = 0,
-           py::arg("index_capacity") = 0, py::arg("client_id") = "torchkafka-replicator")
+           py::arg("index_capacity") = 0, py::arg("client_id") = "torchkafka-replicator",
+           py::arg("release_consumed") = true, py::arg("release_bytes") = uint64_t(64) << 20)
       .def("start", &Replicator::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Replicator::stop, py::arg("flush") = true, py::call_guard<py::gil_scoped_release>())
       .def("flush_commits", &Replicator::flush_commits, py::call_guard<py::gil_scoped_release>())
@@ -511,6 +515,7 @@ PYBIND11_MODULE(_tkcore, m) {
           d["control_batches"] = s.control_batches;
           d["fetches"] = s.fetches;
           d["throttled"] = s.throttled;
+          d["released"] = s.released;
           l.append(d);
         }
         return l;

@@ -1,6 +1,7 @@
 #include "broker.h"
 
 #include <fcntl.h>
+#include <linux/falloc.h>
 #include <signal.h>
 #include <sys/file.h>
 #include <sys/mman.h>
@@ -444,6 +445,24 @@ uint64_t Broker::position_of(uint32_t pidx, int64_t offset) {
     if (idx[mid].base_offset + idx[mid].last_offset_delta < offset) lo = mid + 1; else hi = mid;
   }
   return lo < nb ? idx[lo].pos : P.log_end_pos.load(std::memory_order_acquire);
+}
+
+uint64_t Broker::release_log(uint32_t pidx, uint64_t from, uint64_t to) {
+  const uint64_t page = 4096;
+  from = (from + page - 1) / page * page;
+  to = to / page * page;
+  if (to <= from) return 0;
+  const std::string path = part_path(dir_, pidx, "log");
+  const int fd = open(path.c_str(), O_RDWR);
+  if (fd < 0) throw_errno("open " + path);
+  const int rc = fallocate(fd, FALLOC_FL_PUNCH_HOLE | FALLOC_FL_KEEP_SIZE, off_t(from), off_t(to - from));
+  const int err = errno;
+  close(fd);
+  if (rc != 0) {
+    errno = err;
+    throw_errno("fallocate(PUNCH_HOLE) " + path);
+  }
+  return to - from;
 }
 
 void Broker::delete_records(uint32_t pidx, int64_t before_offset) {

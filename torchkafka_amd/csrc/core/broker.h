@@ -48,13 +48,20 @@ struct BrokerConfig {
   uint32_t group_initial_rebalance_delay_ms = 100;
 };
 
+enum BrokerFlags : uint32_t {
+  // Log bytes below a partition's committed position may be released (a replica: KafkaBridge owns
+  // the broker and one group consumes it).  The replicator punches them out of the log files, the
+  // device driver unpins them; the log start offset moves up to the committed offset.
+  kReleaseConsumed = 1,
+};
+
 struct alignas(64) MetaHeader {
   uint64_t magic;
   uint32_t version;
   std::atomic<uint32_t> ready;
   uint32_t max_topics, max_partitions, max_groups, group_initial_rebalance_delay_ms;
   uint64_t default_log_capacity, default_index_capacity;
-  std::atomic<uint32_t> n_topics, n_partitions, n_groups, pad0;
+  std::atomic<uint32_t> n_topics, n_partitions, n_groups, flags;  // flags: BrokerFlags
   pthread_mutex_t lock;  // topic/group creation, membership changes
 };
 
@@ -198,6 +205,11 @@ class Broker {
   Ingested ingest(uint32_t pidx, uint64_t len, int64_t from_offset, bool keep_control = false);
   // Log byte position of the first batch holding an offset >= `offset` (log end if none).
   uint64_t position_of(uint32_t pidx, int64_t offset);
+  uint32_t flags() const { return meta_->flags.load(std::memory_order_acquire); }
+  void set_flags(uint32_t f) { meta_->flags.fetch_or(f, std::memory_order_acq_rel); }
+  // Frees log bytes [from, to) (page-aligned inwards) of a partition: FALLOC_FL_PUNCH_HOLE on its
+  // log file, so every process's mapping of them drops to the zero page.  Returns bytes released.
+  uint64_t release_log(uint32_t pidx, uint64_t from, uint64_t to);
 
   // ---- groups / offsets
   uint32_t group_index(const std::string& group, bool create = true);

@@ -53,6 +53,7 @@ void Replicator::start() {
     throw KafkaError("replicator: local topic '" + cfg_.topic + "' has " + std::to_string(ti.n_partitions) +
                      " partitions, the cluster " + std::to_string(n_remote_parts_));
   first_pidx_ = ti.first_pidx;
+  if (cfg_.release_consumed && !cfg_.group.empty()) local_->set_flags(kReleaseConsumed);
   std::vector<int32_t> ids = cfg_.partitions;
   if (ids.empty())
     for (auto& p : t.partitions) ids.push_back(p.partition);
@@ -322,6 +323,7 @@ void Replicator::commit_loop() {
       if (!commit_client_)
         commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", cfg_.timeout_ms);
       forward(*commit_client_);
+      if (cfg_.release_consumed) release_consumed();
       backoff_ms = cfg_.commit_interval_ms;
     } catch (const std::exception& e) {
       set_error(std::string("replicator: commit: ") + e.what());
@@ -331,12 +333,30 @@ void Replicator::commit_loop() {
   }
 }
 
+// Committed log bytes are never read again (the bridge's broker has one consuming group): move
+// the log start up to the committed offset, then punch the bytes below its batch out of the log
+// file.  Host memory then holds the uncommitted window (max_lag_bytes) instead of the whole stream.
+// A device loader unpins its registered ranges below the same position (MainDriver).
+void Replicator::release_consumed() {
+  for (auto& p : parts_) {
+    const int64_t c = local_->committed(group_, p->pidx);
+    if (c < 0) continue;
+    const uint64_t pos = local_->position_of(p->pidx, c);
+    const uint64_t to = pos / (2u << 20) * (2u << 20);
+    const uint64_t from = p->released.load();
+    if (to < from + cfg_.release_bytes) continue;
+    local_->delete_records(p->pidx, c);  // readers below c now see OffsetOutOfRange, as after retention
+    local_->release_log(p->pidx, from, to);
+    p->released.store(to);
+  }
+}
+
 std::vector<ReplicaPartStats> Replicator::stats() {
   std::vector<ReplicaPartStats> v;
   for (auto& p : parts_)
     v.push_back(ReplicaPartStats{p->partition, p->pidx, p->start_offset, p->fetch_offset.load(), p->remote_hw.load(),
                                  p->forwarded.load(), p->bytes.load(), p->batches.load(), p->control.load(),
-                                 p->fetches.load(), p->throttled.load()});
+                                 p->fetches.load(), p->throttled.load(), p->released.load()});
   return v;
 }
 

@@ -45,6 +45,8 @@ struct ReplicaConfig {
   int64_t max_lag_bytes = int64_t(1) << 30;
   int32_t commit_interval_ms = 5;
   int32_t fetchers = 0;                // fetch threads (0: one per partition leader, at most 8)
+  bool release_consumed = true;        // free committed log bytes (punch holes; kReleaseConsumed)
+  uint64_t release_bytes = 64u << 20;  // ... in steps of at least this many bytes
   uint64_t log_capacity = 0;           // local topic creation (0: the broker default)
   uint64_t index_capacity = 0;
 };
@@ -61,6 +63,7 @@ struct ReplicaPartStats {
   uint64_t control_batches;
   uint64_t fetches;
   uint64_t throttled;       // fetch rounds skipped by flow control
+  uint64_t released;        // log bytes released below the committed position
 };
 
 class Replicator {
@@ -95,8 +98,9 @@ class Replicator {
     std::atomic<int64_t> remote_hw{-1};
     std::atomic<int64_t> forwarded{-1};
     std::atomic<uint64_t> bytes{0}, batches{0}, control{0}, fetches{0}, throttled{0};
-    int64_t scratch_len = 0;  // record-set bytes that did not fit the tail (dropped, refetched)
+    std::atomic<uint64_t> released{0};  // log bytes [0, released) freed (committed past)
   };
+  void release_consumed();
   void fetch_loop(std::vector<Part*> mine);
   void commit_loop();
   bool throttled(Part& p);

@@ -283,6 +283,7 @@ PYBIND11_MODULE(_tkhip, m) {
              s["polled"] = d.polled_;
              s["poll_ns"] = d.poll_ns_;
              s["log_bytes_registered"] = d.log_bytes_registered();
+             s["log_bytes_unpinned"] = d.log_bytes_unpinned();
              if (const LogMirror* m = d.mirror()) {
                s["mirror_bytes_copied"] = m->bytes_copied();
                s["mirror_copies"] = m->copies();

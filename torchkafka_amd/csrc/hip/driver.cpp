@@ -44,6 +44,8 @@ MainDriver::MainDriver(Engine* engine, const std::string& ring_name, const std::
     broker_ = std::make_shared<tk::Broker>(broker_url, false, tk::BrokerConfig{});
     group_ = broker_->group_index(group, true);
     reg_end_.assign(broker_->meta().max_partitions, 0);  // log ranges pinned for direct / span reads
+    reg_ranges_.resize(broker_->meta().max_partitions);
+    release_consumed_ = (broker_->flags() & tk::kReleaseConsumed) != 0;
   }
   commit_ns_.reserve(1 << 16);
 }
@@ -51,8 +53,11 @@ MainDriver::MainDriver(Engine* engine, const std::string& ring_name, const std::
 MainDriver::~MainDriver() {
   mirror_.reset();  // its copies read the pinned logs: before they are unregistered
   // pinned log ranges first: the kernels that read them completed (slots drained by the caller)
-  if (!reg_ptrs_.empty()) hipDeviceSynchronize();
-  for (void* p : reg_ptrs_) hipHostUnregister(p);
+  bool any = false;
+  for (auto& q : reg_ranges_) any = any || !q.empty();
+  if (any) hipDeviceSynchronize();
+  for (auto& q : reg_ranges_)
+    for (auto& r : q) hipHostUnregister(r.first);
   if (bases_dev_) hipFree(bases_dev_);
   if (stage_dev_) {
     hipDeviceSynchronize();
@@ -430,7 +435,8 @@ void MainDriver::ensure_log(uint32_t pidx, uint64_t end) {
   void* p = const_cast<uint8_t*>(base) + lo;
   if (hipHostRegister(p, hi - lo, hipHostRegisterMapped) != hipSuccess)
     throw std::runtime_error("driver: hipHostRegister of a partition log failed");
-  reg_ptrs_.push_back(p);
+  if (reg_ranges_.size() <= pidx) reg_ranges_.resize(size_t(pidx) + 1);
+  reg_ranges_[pidx].emplace_back(p, hi);
   void* dp = nullptr;
   if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess || dp != p)
     throw std::runtime_error("driver: h2d='direct' needs device addresses of pinned host memory to equal host "
@@ -1137,6 +1143,27 @@ void MainDriver::publish_to_workers() {
     if (touched[size_t(w)]) __atomic_fetch_add(sink_table_ + 2 * w, int64_t(1), __ATOMIC_RELEASE);
 }
 
+// A replica's log bytes below the committed position are never read again (one group consumes
+// it; the replicator punches them out of the files): unpin whole registered ranges below it, so
+// the pages are freed and a long stream holds only its in-flight window pinned.  Every kernel that
+// read them completed: a batch is committed only after its decode verdict.
+void MainDriver::release_consumed() {
+  commits_since_release_ = 0;
+  for (const auto& kv : committed_) {
+    const uint32_t pidx = kv.first;
+    if (pidx >= reg_ranges_.size() || reg_ranges_[pidx].size() < 2) continue;  // keep the range being read
+    auto& q = reg_ranges_[pidx];
+    const uint64_t pos = broker_->position_of(pidx, kv.second);
+    while (q.size() > 1 && q.front().second <= pos) {
+      if (hipHostUnregister(q.front().first) != hipSuccess)
+        throw std::runtime_error("driver: hipHostUnregister of a consumed log range failed");
+      unpinned_bytes_ += q.front().second -
+                         uint64_t(static_cast<const uint8_t*>(q.front().first) - broker_->log_base(pidx));
+      q.pop_front();
+    }
+  }
+}
+
 int MainDriver::commit_pending() {
   drain_fenced(false);
   if (pending_.empty()) return parse_error_.empty() ? 0 : -2;
@@ -1160,6 +1187,7 @@ int MainDriver::commit_pending() {
     broker_->commit(group_, -1, 0, 0, entries_);
     for (const auto& kv : pending_) committed_[kv.first] = kv.second;
     ++commits_;
+    if (release_consumed_ && ++commits_since_release_ >= 32) release_consumed();
   } catch (const tk::CommitFailed&) {
     ++commit_failures_;
     status = -1;

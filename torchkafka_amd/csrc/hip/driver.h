@@ -187,6 +187,7 @@ class MainDriver {
   void enable_mirror(uint64_t chunk_bytes, int chunks_per_partition);
   const LogMirror* mirror() const { return mirror_.get(); }
   uint64_t log_bytes_registered() const { return reg_total_; }
+  uint64_t log_bytes_unpinned() const { return unpinned_bytes_; }
   int64_t log_register_ns() const { return reg_ns_; }
   int coalesce() const { return coalesce_; }
   int64_t groups() const { return groups_; }
@@ -380,7 +381,13 @@ class MainDriver {
   const uint8_t* seg_src(const tk::SpanSeg& sg);  // the address a decode kernel reads a segment from
   uint64_t* bases_dev_ = nullptr;
   std::vector<uint64_t> reg_end_;        // per pidx: bytes of its log pinned (and device-mapped)
-  std::vector<void*> reg_ptrs_;          // registered ranges, unregistered at teardown
+  // per pidx: pinned ranges (address, end position), unpinned once committed past (a replica
+  // broker, tk::kReleaseConsumed) or at teardown
+  std::vector<std::deque<std::pair<void*, uint64_t>>> reg_ranges_;
+  bool release_consumed_ = false;
+  uint64_t unpinned_bytes_ = 0;
+  uint64_t commits_since_release_ = 0;
+  void release_consumed();
   uint64_t reg_total_ = 0;
   int64_t reg_ns_ = 0;
   std::vector<size_t> group_idx_;  // staged_ indices of the batches behind `last` in the pending group

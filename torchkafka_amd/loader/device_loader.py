@@ -1099,6 +1099,7 @@ class DeviceLoader:
         self.stats.poll_ns += st.get("poll_ns", 0)
         self.stats.polled += st.get("polled", 0)
         self.stats.log_bytes_registered = st.get("log_bytes_registered", 0)
+        self.stats.log_bytes_unpinned = st.get("log_bytes_unpinned", 0)
         self.stats.log_register_ns = st.get("log_register_ns", 0)
         self.stats.mirror_bytes += st.get("mirror_bytes_copied", 0)
         self.stats.mirror_copies += st.get("mirror_copies", 0)

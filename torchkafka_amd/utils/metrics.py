@@ -51,6 +51,7 @@ class LoaderStats:
     poll_ns: int = 0           # native next phase: non-blocking stagings of READY slots
     polled: int = 0
     log_bytes_registered: int = 0  # h2d="direct": broker log bytes pinned in place so far
+    log_bytes_unpinned: int = 0    # replica logs: consumed ranges unpinned again (kReleaseConsumed)
     log_register_ns: int = 0
     mirror_bytes: int = 0     # h2d="dma" device decode: log bytes copied into the HBM mirror (SDMA)
     mirror_copies: int = 0
@@ -105,6 +106,7 @@ class LoaderStats:
             "native_poll_us_per_step": self.poll_ns / 1e3 / max(self.phase_steps, 1),
             "native_poll_us_per_slot": self.poll_ns / 1e3 / max(self.polled, 1),
             "log_mib_pinned": self.log_bytes_registered / 2**20,
+            "log_mib_unpinned": self.log_bytes_unpinned / 2**20,
             "log_pin_ms": self.log_register_ns / 1e6,
             "mirror_mib_copied": self.mirror_bytes / 2**20,
             "mirror_copies": self.mirror_copies,
