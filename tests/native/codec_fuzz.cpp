@@ -8,6 +8,7 @@
 #include <random>
 #include <vector>
 
+#include "codecs.h"
 #include "consumer.h"
 #include "crc32c.h"
 #include "record_batch.h"
@@ -100,7 +101,36 @@ int main(int argc, char** argv) {
     CHECK(n2 >= -1);
     std::free(s);
   }
-  std::printf("codec fuzz: %d batches, %llu corrupted decodes survived, %llu rejected; JSON fuzz ok\n", iters,
-              (unsigned long long)decoded, (unsigned long long)rejected);
+  // decompressors (replica ingest of compressed record sets): random and mutated inputs must
+  // either decode or throw CorruptRecord, never read or write outside their buffers
+  uint64_t inflated = 0, refused = 0;
+  for (int it = 0; it < iters * 4; ++it) {
+    std::vector<uint8_t> in(rng() % 512);
+    for (auto& c : in) c = uint8_t(rng() % 4 == 0 ? rng() : (rng() % 8));
+    if (it % 3 == 1 && in.size() >= 7) {  // an LZ4 frame header in front
+      const uint8_t hdr[7] = {0x04, 0x22, 0x4D, 0x18, 0x60, 0x40, 0x82};
+      std::memcpy(in.data(), hdr, 7);
+    }
+    const int codec = it % 3 == 0 ? kCodecSnappy : it % 3 == 1 ? kCodecLz4 : -1;
+    std::vector<uint8_t> out;
+    try {
+      if (codec < 0) snappy_raw_decompress(in.data(), in.size(), out);
+      else decompress(codec, in.data(), in.size(), out);
+      ++inflated;
+    } catch (const CorruptRecord&) {
+      ++refused;
+    }
+    std::vector<uint8_t> out2;
+    try {
+      lz4_block_decompress(in.data(), in.size(), out2);
+      ++inflated;
+    } catch (const CorruptRecord&) {
+      ++refused;
+    }
+  }
+  std::printf("codec fuzz: %d batches, %llu corrupted decodes survived, %llu rejected; JSON fuzz ok; "
+              "decompressors: %llu decoded, %llu refused\n", iters,
+              (unsigned long long)decoded, (unsigned long long)rejected, (unsigned long long)inflated,
+              (unsigned long long)refused);
   return 0;
 }

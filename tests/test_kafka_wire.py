@@ -246,3 +246,204 @@ def test_committed_log_bytes_are_released(broker, server):
 
 class Vec256(KafkaDataset):
     schema = FixedWidth(torch.float32, (256,))
+
+
+# ---------------------------------------------------------------- compressed record sets
+# Minimal encoders (the image has no snappy/lz4 packages): greedy 4-byte matches, enough to
+# exercise every element type of the native decoders (literals of every length class, copies
+# with overlapping matches).
+
+def _snappy_raw(data: bytes) -> bytes:
+    out = bytearray()
+    n = len(data)
+    v = n
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    table, i, lit = {}, 0, 0
+
+    def emit_literal(a, b):
+        while a < b:
+            k = min(b - a, 65536)
+            if k <= 60:
+                out.append((k - 1) << 2)
+            elif k <= 256:
+                out.extend(bytes([60 << 2, k - 1]))
+            else:
+                out.extend(bytes([61 << 2]) + (k - 1).to_bytes(2, "little"))
+            out.extend(data[a:a + k])
+            a += k
+
+    while i + 4 <= n:
+        key = data[i:i + 4]
+        j = table.get(key)
+        table[key] = i
+        if j is not None and i - j < 65536:
+            m = 4
+            while i + m < n and data[j + m] == data[i + m] and m < 64:
+                m += 1
+            emit_literal(lit, i)
+            off = i - j
+            if m <= 11 and off < 2048:
+                out += bytes([1 | ((m - 4) << 2) | ((off >> 8) << 5), off & 0xFF])
+            else:
+                out += bytes([2 | ((m - 1) << 2)]) + off.to_bytes(2, "little")
+            i += m
+            lit = i
+        else:
+            i += 1
+    emit_literal(lit, n)
+    return bytes(out)
+
+
+def _xerial(data: bytes, block=32 << 10) -> bytes:
+    out = bytearray(b"\x82SNAPPY\x00" + (1).to_bytes(4, "big") + (1).to_bytes(4, "big"))
+    for a in range(0, len(data), block):
+        c = _snappy_raw(data[a:a + block])
+        out += len(c).to_bytes(4, "big") + c
+    return bytes(out)
+
+
+def _lz4_block(data: bytes) -> bytes:
+    out = bytearray()
+    n, i, lit, table = len(data), 0, 0, {}
+
+    def lenbytes(v):
+        b = bytearray()
+        while v >= 255:
+            b.append(255)
+            v -= 255
+        b.append(v)
+        return b
+
+    while i + 12 <= n:
+        key = data[i:i + 4]
+        j = table.get(key)
+        table[key] = i
+        if j is not None and i - j < 65536:
+            m = 4
+            while i + m < n - 5 and data[j + m] == data[i + m]:
+                m += 1
+            ll, ml = i - lit, m - 4
+            out.append((min(ll, 15) << 4) | min(ml, 15))
+            if ll >= 15:
+                out += lenbytes(ll - 15)
+            out += data[lit:i]
+            out += (i - j).to_bytes(2, "little")
+            if ml >= 15:
+                out += lenbytes(ml - 15)
+            i += m
+            lit = i
+        else:
+            i += 1
+    ll = n - lit
+    out.append(min(ll, 15) << 4)
+    if ll >= 15:
+        out += lenbytes(ll - 15)
+    out += data[lit:]
+    return bytes(out)
+
+
+def _lz4_frame(data: bytes, block=64 << 10) -> bytes:
+    out = bytearray((0x184D2204).to_bytes(4, "little") + bytes([0x60, 0x40, 0x82]))  # FLG, BD, HC
+    for a in range(0, len(data), block):
+        chunk = data[a:a + block]
+        c = _lz4_block(chunk)
+        if len(c) >= len(chunk):
+            out += (len(chunk) | 0x80000000).to_bytes(4, "little") + chunk
+        else:
+            out += len(c).to_bytes(4, "little") + c
+    out += (0).to_bytes(4, "little")
+    return bytes(out)
+
+
+def _compress_batch(batch: bytes, codec: int) -> bytes:
+    import gzip
+    import struct
+
+    records = batch[61:]
+    comp = {1: gzip.compress, 2: _xerial, 3: _lz4_frame}[codec](records)
+    hdr = bytearray(batch[:61])
+    attrs = struct.unpack_from(">h", hdr, 21)[0] | codec
+    struct.pack_into(">h", hdr, 21, attrs)
+    struct.pack_into(">i", hdr, 8, 61 - 12 + len(comp))
+    body = bytes(hdr[21:]) + comp
+    struct.pack_into(">I", hdr, 17, core().crc32c(body))
+    return bytes(hdr[:21]) + body
+
+
+@pytest.mark.parametrize("codec", [1, 2, 3])
+def test_native_decompressors(codec):
+    import gzip
+
+    data = (b"abcabcabcabc" * 300 + bytes(range(256)) * 40 + b"x" * 5000 + os.urandom(3000)) * 3
+    comp = {1: gzip.compress, 2: _xerial, 3: _lz4_frame}[codec](data)
+    assert core().decompress(codec, comp) == data
+    assert core().decompress(2, _snappy_raw(data)) == data  # raw snappy (no xerial framing)
+    with pytest.raises(Exception, match="corrupt compressed|CRC|Corrupt"):
+        core().decompress(codec, comp[: len(comp) // 2])
+
+
+def test_zstd_is_reported_unsupported():
+    with pytest.raises(Exception, match="UnsupportedCodecError: zstd"):
+        core().decompress(4, b"\x28\xb5\x2f\xfd")
+
+
+@pytest.mark.parametrize("codec", [1, 2, 3])
+def test_compressed_batches_are_inflated_on_ingest(broker, server, codec):
+    """A producer's compressed batches reach the replica as plain RecordBatch v2 (fresh CRC), so
+    the loader and the device decoders read them like any other batch."""
+    ref = SyntheticBroker.create(f"shm://tkref-{os.getpid()}-{uuid.uuid4().hex[:6]}", log_capacity=64 << 20)
+    try:
+        ref.create_topic("t", 1)
+        ref.fill("t", 600, "fixed_f32", size=64, records_per_batch=40)
+        raw = log_bytes(ref, "t", 0)
+        broker.create_topic("t", 1)
+        pidx = broker.pidx("t", 0)
+        o = 0
+        while o < len(raw):
+            blen = int.from_bytes(raw[o + 8:o + 12], "big") + 12
+            broker.native.ingest_bytes(pidx, _compress_batch(raw[o:o + blen], codec), keep_control=True)
+            o += blen
+        assert broker.end_offset("t", 0) == 600
+        assert len(log_bytes(broker, "t", 0)) < len(raw)  # stored compressed at the source
+        with bridge(server, group_id="g") as br:
+            assert br.wait_caught_up(10)
+            assert log_bytes(br.local, "t", 0) == raw       # inflated replica == uncompressed log
+            dl = DeviceLoader(Vec64.placeholder(), 50, device="cpu", num_workers=1,
+                              worker_init_fn=Vec64.init_worker("t", bootstrap_servers=br.url, group_id="g",
+                                                               auto_offset_reset="earliest",
+                                                               consumer_timeout_ms=300))
+            rows = torch.cat(list(auto_commit(dl)))
+            assert rows.shape == (600, 64)
+            assert rows[:, 0].tolist() == [float(i) for i in range(600)]
+            assert rows[7, 2:].tolist() == [synth_f32(0, 7, j) for j in range(2, 64)]
+    finally:
+        ref.destroy()
+
+
+def test_corrupt_compressed_batch_stops_the_partition(broker, server):
+    ref = SyntheticBroker.create(f"shm://tkref-{os.getpid()}-{uuid.uuid4().hex[:6]}", log_capacity=64 << 20)
+    try:
+        ref.create_topic("t", 1)
+        ref.fill("t", 40, "fixed_f32", size=16, records_per_batch=20)
+        raw = log_bytes(ref, "t", 0)
+        blen = int.from_bytes(raw[8:12], "big") + 12
+        good = _compress_batch(raw[:blen], 1)
+        bad = bytearray(_compress_batch(raw[blen:], 1))
+        bad[-3] ^= 0xFF  # flips a compressed byte: the producer CRC no longer matches
+        broker.create_topic("t", 1)
+        pidx = broker.pidx("t", 0)
+        broker.native.ingest_bytes(pidx, good, keep_control=True)
+        broker.native.ingest_bytes(pidx, bytes(bad), keep_control=True)
+        with bridge(server) as br:
+            assert wait_for(lambda: br.errors > 0)
+            assert "CRC" in br.last_error()
+            assert br.local.end_offset("t", 0) == 20  # the good batch only
+    finally:
+        ref.destroy()
+
+
+class Vec64(KafkaDataset):
+    schema = FixedWidth(torch.float32, (64,))

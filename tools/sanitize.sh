@@ -8,14 +8,14 @@ cd "$(dirname "$0")/.."
 OUT=${1:-build/sanitize}
 mkdir -p "$OUT"
 CORE=torchkafka_amd/csrc/core
-SRCS="$CORE/ring.cpp $CORE/broker.cpp $CORE/consumer.cpp $CORE/record_batch.cpp $CORE/crc32c.cpp"
+SRCS="$CORE/ring.cpp $CORE/broker.cpp $CORE/consumer.cpp $CORE/record_batch.cpp $CORE/crc32c.cpp $CORE/codecs.cpp"
 CXX=${CXX:-g++}
 COMMON="-std=c++17 -O1 -g -fno-omit-frame-pointer -I$CORE -pthread"
-$CXX $COMMON -fsanitize=thread tests/native/ring_stress.cpp $SRCS -o "$OUT/ring_stress_tsan" -lrt
+$CXX $COMMON -fsanitize=thread tests/native/ring_stress.cpp $SRCS -o "$OUT/ring_stress_tsan" -lrt -lz
 $CXX $COMMON -fsanitize=address,undefined -fno-sanitize-recover=undefined tests/native/ring_stress.cpp $SRCS \
-    -o "$OUT/ring_stress_asan" -lrt
+    -o "$OUT/ring_stress_asan" -lrt -lz
 $CXX $COMMON -fsanitize=address,undefined -fno-sanitize-recover=undefined tests/native/codec_fuzz.cpp $SRCS \
-    -o "$OUT/codec_fuzz_asan" -lrt
+    -o "$OUT/codec_fuzz_asan" -lrt -lz
 export TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1"
 export ASAN_OPTIONS="halt_on_error=1 detect_leaks=1"
 export UBSAN_OPTIONS="halt_on_error=1 print_stacktrace=1"

@@ -67,7 +67,8 @@ def resolve_url(servers) -> str:
         return env
     raise NoBrokersAvailable(
         f"NoBrokersAvailable: cannot reach {servers!r}: kafka-python is not installed and "
-        "no synthetic broker is configured (use bootstrap_servers='shm://<name>' or set TORCHKAFKA_BROKER)"
+        "no synthetic broker is configured (use bootstrap_servers='shm://<name>', set TORCHKAFKA_BROKER, or "
+        "mirror the cluster with torchkafka.KafkaBridge(servers, topic, group_id=...) and pass bridge.url)"
     )
 
 

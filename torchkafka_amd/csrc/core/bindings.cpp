@@ -6,6 +6,7 @@
 #include <deque>
 
 #include "broker.h"
+#include "codecs.h"
 #include "consumer.h"
 #include "crc32c.h"
 #include "lockstep.h"
@@ -164,6 +165,12 @@ PYBIND11_MODULE(_tkcore, m) {
     return crc32c(s.data(), s.size());
   });
   m.def("crc32c_hw", &crc32c_hw);
+  m.def("decompress", [](int codec, py::bytes b) {
+    std::string s = b;
+    std::vector<uint8_t> out;
+    decompress(codec, reinterpret_cast<const uint8_t*>(s.data()), s.size(), out);
+    return py::bytes(reinterpret_cast<const char*>(out.data()), out.size());
+  });
   m.def("crc32c_fold", &crc32c_fold);
   m.def("crc32c_shift_raw", &crc32c_shift_raw, py::arg("raw"), py::arg("n_bytes"));
   m.def(
@@ -380,6 +387,7 @@ PYBIND11_MODULE(_tkcore, m) {
              d["kept"] = in.kept;
              d["kept_bytes"] = in.kept_bytes;
              d["control"] = in.control;
+             d["inflated"] = in.inflated;
              d["next_offset"] = in.next_offset;
              return d;
            },

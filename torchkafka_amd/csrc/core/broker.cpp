@@ -1,5 +1,8 @@
 #include "broker.h"
 
+#include "codecs.h"
+#include "crc32c.h"
+
 #include <fcntl.h>
 #include <linux/falloc.h>
 #include <signal.h>
@@ -396,34 +399,74 @@ Broker::Ingested Broker::ingest(uint32_t pidx, uint64_t len, int64_t from_offset
   uint64_t nb = P.n_batches.load(std::memory_order_relaxed);
   int64_t hw = P.high_watermark.load(std::memory_order_relaxed);
   Ingested out;
-  uint64_t r = 0, w = 0;
-  while (len - r >= kBatchHeaderBytes) {
+  // Input starts in place (the record set was received into the log tail) and output compacts
+  // it towards its start; an inflated batch grows, so from the first compressed batch on the
+  // unread input moves to `spill` and the output may run past it.
+  const uint8_t* in = base;
+  uint64_t in_len = len, r = 0, w = 0, consumed_base = 0;
+  std::vector<uint8_t> spill, plain;
+  auto publish = [&](const uint8_t* src, uint64_t total, const BatchHeader& h) {
+    if (pos0 + w + total > P.log_capacity) throw KafkaError("partition log full (raise log_capacity)");
+    if (nb >= P.index_capacity) throw KafkaError("partition index full");
+    if (base + w != src) std::memmove(base + w, src, total);
+    m.idx[nb++] = IndexEntry{h.base_offset, pos0 + w, uint32_t(total), h.last_offset_delta, h.max_timestamp};
+    w += total;
+    hw = h.next_offset();
+    ++out.kept;
+  };
+  std::exception_ptr failure;  // the batches before a bad one are still published
+  try {
+  while (in_len - r >= kBatchHeaderBytes) {
     int32_t blen;
-    std::memcpy(&blen, base + r + kBatchLengthOffset, 4);
+    std::memcpy(&blen, in + r + kBatchLengthOffset, 4);
     blen = int32_t(__builtin_bswap32(uint32_t(blen)));
     if (blen < int32_t(kBatchHeaderBytes - 12)) throw CorruptRecord("replica: bad RecordBatch length");
     const uint64_t total = uint64_t(blen) + 12;
-    if (len - r < total) break;  // partial trailing batch: the next fetch brings it whole
-    const BatchHeader h = parse_batch_header(base + r, total);
+    if (in_len - r < total) break;  // partial trailing batch: the next fetch brings it whole
+    if (in[r + 16] != 2)
+      throw CorruptRecord("replica: message format v" + std::to_string(int(in[r + 16])) +
+                          " (only RecordBatch v2 is supported; upgrade the topic's message.format.version)");
+    const BatchHeader h = parse_batch_header(in + r, total, true);
     if (h.magic != 2)
       throw CorruptRecord("replica: message format v" + std::to_string(h.magic) +
                           " (only RecordBatch v2 is supported; upgrade the topic's message.format.version)");
-    out.consumed = r + total;
+    out.consumed = consumed_base + r + total;
     out.next_offset = h.next_offset();
     const bool control = (h.attributes >> 5) & 1;
     if (control) ++out.control;
     if ((!control || keep_control) && h.next_offset() > from_offset && h.next_offset() > hw) {
-      if ((h.attributes & 7) && !keep_control)
-        throw KafkaError("UnsupportedCodecError: compressed RecordBatch (codec " + std::to_string(h.attributes & 7) +
-                         ") on a device-decoded replica; produce with compression_type=None");
-      if (nb >= P.index_capacity) throw KafkaError("partition index full");
-      if (w != r) std::memmove(base + w, base + r, total);
-      m.idx[nb++] = IndexEntry{h.base_offset, pos0 + w, uint32_t(total), h.last_offset_delta, h.max_timestamp};
-      w += total;
-      hw = h.next_offset();
-      ++out.kept;
+      const int codec = h.attributes & 7;
+      if (codec == kCodecNone || keep_control) {
+        publish(in + r, total, h);
+      } else {
+        // inflate once on arrival: the producer's CRC is checked over the compressed bytes, the
+        // stored batch is plain RecordBatch v2 with its own CRC, so the device path verifies it
+        if (!verify_batch_crc(in + r, h))
+          throw CorruptRecord("Record batch at offset " + std::to_string(h.base_offset) + " failed CRC check");
+        if (in == base) {
+          spill.assign(in + r, in + in_len);
+          consumed_base += r;
+          in = spill.data();
+          in_len = spill.size();
+          r = 0;
+        }
+        plain.assign(in + r, in + r + kBatchHeaderBytes);
+        decompress(codec, in + r + kBatchHeaderBytes, total - kBatchHeaderBytes, plain);
+        const uint32_t new_len = uint32_t(plain.size() - 12);
+        const uint32_t be_len = __builtin_bswap32(new_len);
+        std::memcpy(plain.data() + kBatchLengthOffset, &be_len, 4);
+        plain[kBatchAttrOffset + 1] = uint8_t(plain[kBatchAttrOffset + 1] & ~7);  // attributes: no codec
+        const uint32_t be_crc = __builtin_bswap32(crc32c(plain.data() + kBatchAttrOffset, plain.size() - kBatchAttrOffset));
+        std::memcpy(plain.data() + kBatchCrcOffset, &be_crc, 4);
+        BatchHeader ph = parse_batch_header(plain.data(), plain.size());
+        publish(plain.data(), plain.size(), ph);
+        ++out.inflated;
+      }
     }
     r += total;
+  }
+  } catch (...) {
+    failure = std::current_exception();
   }
   out.kept_bytes = w;
   if (out.kept) {
@@ -432,6 +475,7 @@ Broker::Ingested Broker::ingest(uint32_t pidx, uint64_t len, int64_t from_offset
     P.records_produced.fetch_add(uint64_t(out.kept), std::memory_order_relaxed);
     P.high_watermark.store(hw, std::memory_order_release);
   }
+  if (failure) std::rethrow_exception(failure);
   return out;
 }
 

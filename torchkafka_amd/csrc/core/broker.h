@@ -194,13 +194,14 @@ class Broker {
   struct Ingested {
     uint64_t consumed = 0;     // bytes of whole batches walked (kept or dropped)
     uint64_t kept_bytes = 0;
-    uint32_t kept = 0, control = 0;
+    uint32_t kept = 0, control = 0, inflated = 0;  // inflated: compressed batches stored decompressed
     int64_t next_offset = -1;  // next offset to fetch (-1: no whole batch in the data)
   };
   // Walks the RecordBatches received at log_tail(): keeps (indexes, publishes) whole data
   // batches at or beyond `from_offset`, drops control batches (transaction markers) and
   // batches already held, compacting in place; a trailing partial batch is left for the next
-  // fetch to overwrite.  Compressed batches raise (the device path decodes raw records only).
+  // fetch to overwrite.  Compressed batches (gzip/snappy/lz4, codecs.h) are CRC-checked and stored
+  // inflated, as plain RecordBatch v2 with a fresh CRC: the device path decodes raw records.
   // keep_control: store control batches too (a broker's own log, e.g. the wire server's tests).
   Ingested ingest(uint32_t pidx, uint64_t len, int64_t from_offset, bool keep_control = false);
   // Log byte position of the first batch holding an offset >= `offset` (log end if none).

@@ -1,0 +1,210 @@
+// Kafka record-set decompression: see codecs.h.
+#include "codecs.h"
+
+#include <zlib.h>
+
+#include <cstring>
+#include <string>
+
+#include "common.h"
+
+namespace tk {
+
+const char* codec_name(int codec) {
+  switch (codec) {
+    case kCodecNone: return "none";
+    case kCodecGzip: return "gzip";
+    case kCodecSnappy: return "snappy";
+    case kCodecLz4: return "lz4";
+    case kCodecZstd: return "zstd";
+    default: return "unknown";
+  }
+}
+
+namespace {
+
+[[noreturn]] void bad(const char* what) { throw CorruptRecord(std::string("corrupt compressed record set: ") + what); }
+
+uint32_t be32(const uint8_t* p) { return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | p[3]; }
+uint32_t le32(const uint8_t* p) { return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24); }
+
+// Back-reference copy; may overlap its own output (offset < length repeats a pattern).
+void copy_match(std::vector<uint8_t>& out, size_t base, size_t offset, size_t len) {
+  if (offset == 0 || offset > out.size() - base) bad("match offset");
+  size_t from = out.size() - offset;
+  out.reserve(out.size() + len);
+  for (size_t i = 0; i < len; ++i) out.push_back(out[from + i]);
+}
+
+void gunzip(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
+  z_stream z{};
+  if (inflateInit2(&z, 16 + MAX_WBITS) != Z_OK) bad("zlib init");
+  z.next_in = const_cast<Bytef*>(src);
+  z.avail_in = uInt(n);
+  int rc = Z_OK;
+  while (rc != Z_STREAM_END) {
+    const size_t old = out.size();
+    out.resize(old + std::max<size_t>(n * 2, 64 << 10));
+    z.next_out = out.data() + old;
+    z.avail_out = uInt(out.size() - old);
+    rc = inflate(&z, Z_NO_FLUSH);
+    out.resize(out.size() - z.avail_out);
+    if (rc == Z_STREAM_END) {
+      // concatenated gzip members (some producers flush per message set)
+      if (z.avail_in == 0) break;
+      if (inflateReset(&z) != Z_OK) break;
+      rc = Z_OK;
+      continue;
+    }
+    if (rc != Z_OK && !(rc == Z_BUF_ERROR && z.avail_in)) {
+      inflateEnd(&z);
+      bad("gzip stream");
+    }
+  }
+  inflateEnd(&z);
+}
+
+}  // namespace
+
+void snappy_raw_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
+  const uint8_t* p = src;
+  const uint8_t* end = src + n;
+  uint64_t want = 0;
+  for (int shift = 0;; shift += 7) {
+    if (p >= end || shift > 35) bad("snappy length");
+    const uint8_t b = *p++;
+    want |= uint64_t(b & 0x7f) << shift;
+    if (!(b & 0x80)) break;
+  }
+  const size_t base = out.size();
+  out.reserve(base + want);
+  while (p < end) {
+    const uint8_t tag = *p++;
+    const int type = tag & 3;
+    if (type == 0) {  // literal
+      size_t len = tag >> 2;
+      if (len >= 60) {
+        const int nb = int(len) - 59;
+        if (end - p < nb) bad("snappy literal length");
+        len = 0;
+        for (int i = 0; i < nb; ++i) len |= size_t(p[i]) << (8 * i);
+        p += nb;
+      }
+      len += 1;
+      if (size_t(end - p) < len) bad("snappy literal");
+      out.insert(out.end(), p, p + len);
+      p += len;
+    } else {
+      size_t len, off;
+      if (type == 1) {
+        if (p >= end) bad("snappy copy1");
+        len = 4 + ((tag >> 2) & 7);
+        off = (size_t(tag >> 5) << 8) | *p++;
+      } else if (type == 2) {
+        if (end - p < 2) bad("snappy copy2");
+        len = 1 + (tag >> 2);
+        off = size_t(p[0]) | (size_t(p[1]) << 8);
+        p += 2;
+      } else {
+        if (end - p < 4) bad("snappy copy4");
+        len = 1 + (tag >> 2);
+        off = le32(p);
+        p += 4;
+      }
+      copy_match(out, base, off, len);
+    }
+  }
+  if (out.size() - base != want) bad("snappy size");
+}
+
+void lz4_block_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
+  const uint8_t* p = src;
+  const uint8_t* end = src + n;
+  const size_t base = out.size();
+  while (p < end) {
+    const uint8_t token = *p++;
+    size_t lit = token >> 4;
+    if (lit == 15) {
+      uint8_t b;
+      do {
+        if (p >= end) bad("lz4 literal length");
+        b = *p++;
+        lit += b;
+      } while (b == 255);
+    }
+    if (size_t(end - p) < lit) bad("lz4 literals");
+    out.insert(out.end(), p, p + lit);
+    p += lit;
+    if (p == end) break;  // the last sequence has literals only
+    if (end - p < 2) bad("lz4 offset");
+    const size_t off = size_t(p[0]) | (size_t(p[1]) << 8);
+    p += 2;
+    size_t len = token & 15;
+    if (len == 15) {
+      uint8_t b;
+      do {
+        if (p >= end) bad("lz4 match length");
+        b = *p++;
+        len += b;
+      } while (b == 255);
+    }
+    copy_match(out, base, off, len + 4);
+  }
+}
+
+namespace {
+
+void unsnappy(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
+  static const uint8_t kXerial[8] = {0x82, 'S', 'N', 'A', 'P', 'P', 'Y', 0};
+  if (n >= 16 && std::memcmp(src, kXerial, 8) == 0) {  // xerial framing: header, then [BE len][block]...
+    size_t o = 16;
+    while (o < n) {
+      if (n - o < 4) bad("xerial block header");
+      const uint32_t len = be32(src + o);
+      o += 4;
+      if (n - o < len) bad("xerial block");
+      snappy_raw_decompress(src + o, len, out);
+      o += len;
+    }
+    return;
+  }
+  snappy_raw_decompress(src, n, out);
+}
+
+void unlz4_frame(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
+  if (n < 7 || le32(src) != 0x184D2204u) bad("lz4 frame magic");
+  const uint8_t flg = src[4];
+  if ((flg >> 6) != 1) bad("lz4 frame version");
+  size_t o = 6;                     // magic, FLG, BD
+  if (flg & 0x08) o += 8;           // content size
+  if (flg & 0x01) o += 4;           // dictionary id
+  o += 1;                           // header checksum
+  const bool block_sum = flg & 0x10;
+  while (true) {
+    if (n - o < 4) bad("lz4 block size");
+    const uint32_t word = le32(src + o);
+    o += 4;
+    if (word == 0) break;           // end mark
+    const uint32_t len = word & 0x7fffffffu;
+    if (n - o < len) bad("lz4 block");
+    if (word & 0x80000000u) out.insert(out.end(), src + o, src + o + len);  // stored uncompressed
+    else lz4_block_decompress(src + o, len, out);
+    o += len + (block_sum ? 4 : 0);
+    if (o > n) bad("lz4 block checksum");
+  }
+}
+
+}  // namespace
+
+void decompress(int codec, const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
+  switch (codec) {
+    case kCodecGzip: gunzip(src, n, out); return;
+    case kCodecSnappy: unsnappy(src, n, out); return;
+    case kCodecLz4: unlz4_frame(src, n, out); return;
+    default:
+      throw KafkaError(std::string("UnsupportedCodecError: ") + codec_name(codec) +
+                       " record batches cannot be decoded by this build (gzip, snappy and lz4 can)");
+  }
+}
+
+}  // namespace tk

@@ -1,0 +1,29 @@
+// Kafka record-set decompression (RecordBatch attributes bits 0-2) for the replica bridge.
+//
+// kafka-python decompresses a compressed RecordBatch in its fetcher (gzip, snappy, lz4, zstd via
+// optional Python packages) before `_process` sees a record (kafka_dataset.py:156-162).  The
+// device decoders read raw records straight out of the logs, so the replicator
+// (replicator.cpp -> Broker::ingest) inflates a compressed batch once, on arrival, into an
+// uncompressed RecordBatch v2 with a fresh CRC32C (after checking the producer's CRC over the
+// compressed bytes).  gzip goes through zlib; snappy (raw or xerial-framed, as the Java client
+// writes it) and LZ4 (frame format) are decoded here; zstd is not available in this image and
+// raises UnsupportedCodecError.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace tk {
+
+enum Codec : int { kCodecNone = 0, kCodecGzip = 1, kCodecSnappy = 2, kCodecLz4 = 3, kCodecZstd = 4 };
+const char* codec_name(int codec);
+
+// Appends the decompressed bytes of `src` to `out`.  Throws CorruptRecord on malformed input,
+// KafkaError("UnsupportedCodecError ...") for codecs this build cannot decode.
+void decompress(int codec, const uint8_t* src, size_t n, std::vector<uint8_t>& out);
+
+// The raw block formats (tests encode with their own minimal compressors).
+void snappy_raw_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& out);
+void lz4_block_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& out);
+
+}  // namespace tk

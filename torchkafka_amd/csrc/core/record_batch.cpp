@@ -4,7 +4,7 @@
 
 namespace tk {
 
-BatchHeader parse_batch_header(const uint8_t* p, size_t avail) {
+BatchHeader parse_batch_header(const uint8_t* p, size_t avail, bool allow_compressed) {
   if (avail < kBatchHeaderBytes) throw CorruptRecord("truncated record batch header");
   BatchHeader h;
   h.base_offset = int64_t(get_be64(p));
@@ -23,7 +23,8 @@ BatchHeader parse_batch_header(const uint8_t* p, size_t avail) {
   if (h.magic != 2) throw CorruptRecord("unsupported record batch magic " + std::to_string(int(h.magic)));
   if (h.batch_length < int32_t(kBatchHeaderBytes - 12) || h.total_size() > avail)
     throw CorruptRecord("record batch length out of range");
-  if (h.attributes & 0x7) throw CorruptRecord("compressed record batches are not supported");
+  if ((h.attributes & 0x7) && !allow_compressed)
+    throw CorruptRecord("compressed record batches are not supported (a KafkaBridge replica stores them inflated)");
   if (h.record_count < 0) throw CorruptRecord("negative record count");
   return h;
 }

@@ -74,8 +74,9 @@ struct BatchHeader {
   int timestamp_type() const { return (attributes >> 3) & 1; }
 };
 
-// Parses the fixed 61-byte header.  Throws CorruptRecord when malformed.
-BatchHeader parse_batch_header(const uint8_t* p, size_t avail);
+// Parses the fixed 61-byte header.  Throws CorruptRecord when malformed (or compressed, unless
+// `allow_compressed`: the replica ingest inflates those, codecs.h).
+BatchHeader parse_batch_header(const uint8_t* p, size_t avail, bool allow_compressed = false);
 // Verifies the CRC of a complete batch starting at p.
 bool verify_batch_crc(const uint8_t* p, const BatchHeader& h);
 
