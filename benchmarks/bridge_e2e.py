@@ -1,0 +1,143 @@
+#!/usr/bin/env python3
+"""A Kafka cluster over TCP -> KafkaBridge replica -> DeviceLoader (device decode) -> commits back.
+
+Not a BASELINE config: it measures the production route of `KafkaBridge` on the config-2 record
+shape (f32[256], 1 KiB records, batch 256, commit after every batch).  The cluster is
+`KafkaWireServer` over a synthetic broker, one server process per node (partition p led by node
+p % nodes) on the loopback interface, so the numbers include the Kafka protocol, TCP, the
+replicator's fetch threads (one per leader) and its commit forwarding; they do not include a real
+broker's disk or a NIC.
+
+Phases: (1) replication alone: a backlog mirrored from the cluster into the replica (GB/s);
+(2) end to end: a fresh group replicates and consumes concurrently, every batch's offsets
+committed locally and forwarded to the cluster (records/s), and the cluster's committed offsets are
+checked at the end.
+
+Usage: python benchmarks/bridge_e2e.py [--nodes 4 --partitions 8 --records 200000]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import socket
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _free_ports(n):
+    socks, ports = [], []
+    for _ in range(n):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        socks.append(s)
+        ports.append(s.getsockname()[1])
+    for s in socks:
+        s.close()
+    return ports
+
+
+def _serve(url, node_id, cluster, ready):
+    from torchkafka_amd.broker import KafkaWireServer, open_broker
+
+    srv = KafkaWireServer(open_broker(url), port=cluster[node_id][2], node_id=node_id, cluster=cluster).start()
+    ready.set()
+    while True:
+        time.sleep(3600)
+    srv.close()
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=4)
+    ap.add_argument("--partitions", type=int, default=8)
+    ap.add_argument("--records", type=int, default=200_000, help="records per partition")
+    ap.add_argument("--dim", type=int, default=256)
+    ap.add_argument("--batch-size", type=int, default=256)
+    ap.add_argument("--workers", type=int, default=4)
+    ap.add_argument("--device", default="cuda:0")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--partition-fetch-mib", type=int, default=8)
+    args = ap.parse_args()
+
+    from torchkafka_amd.broker import KafkaBridge, SyntheticBroker
+
+    url = f"shm://tkbe2e-{os.getpid()}"
+    src = SyntheticBroker.create(url, log_capacity=1 << 34, index_capacity=1 << 22)
+    src.create_topic("t", args.partitions)
+    t0 = time.perf_counter()
+    src.fill("t", args.records, "fixed_f32", size=args.dim, records_per_batch=64, threads=min(16, args.partitions))
+    fill_s = time.perf_counter() - t0
+    total_bytes = sum(src.native.log_bytes(src.pidx("t", p)) for p in range(args.partitions))
+    ports = _free_ports(args.nodes)
+    cluster = [(i, "127.0.0.1", ports[i]) for i in range(args.nodes)]
+    ctx = mp.get_context("fork")  # before any HIP call in this process
+    procs = []
+    for i in range(args.nodes):
+        ev = ctx.Event()
+        pr = ctx.Process(target=_serve, args=(url, i, cluster, ev), daemon=True)
+        pr.start()
+        ev.wait(30)
+        procs.append(pr)
+    boot = f"127.0.0.1:{ports[0]}"
+    out = {"nodes": args.nodes, "partitions": args.partitions, "records_per_partition": args.records,
+           "cluster_gb": round(total_bytes / 1e9, 3), "fill_s": round(fill_s, 2)}
+    try:
+        # (1) replication alone
+        t0 = time.perf_counter()
+        br = KafkaBridge(boot, "t", url=f"shm://tkbe2e-r-{os.getpid()}", log_capacity=1 << 34,
+                         index_capacity=1 << 22, max_partition_fetch_bytes=args.partition_fetch_mib << 20,
+                         max_lag_bytes=1 << 40)
+        ok = br.wait_caught_up(300)
+        rep_s = time.perf_counter() - t0
+        out["replication"] = {"caught_up": ok, "s": round(rep_s, 3), "gb_per_s": round(total_bytes / rep_s / 1e9, 2),
+                              "fetch_threads": len({s["partition"] % args.nodes for s in br.stats()}),
+                              "errors": br.errors}
+        br.close()
+
+        # (2) end to end: replicate + decode + commit concurrently
+        import torch
+
+        from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
+
+        class Rows(KafkaDataset):
+            schema = FixedWidth(torch.float32, (args.dim,))
+
+        dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+        br = KafkaBridge(boot, "t", group_id="trainer", url=f"shm://tkbe2e-e-{os.getpid()}", log_capacity=1 << 34,
+                         index_capacity=1 << 22, max_partition_fetch_bytes=args.partition_fetch_mib << 20,
+                         max_lag_bytes=512 << 20)
+        dl = DeviceLoader(Rows.placeholder(), args.batch_size, num_workers=args.workers, device=args.device,
+                          dtype=dtype, worker_init_fn=Rows.init_worker("t", bootstrap_servers=br.url,
+                                                                       group_id="trainer",
+                                                                       auto_offset_reset="earliest",
+                                                                       consumer_timeout_ms=2000))
+        n = 0
+        t0 = time.perf_counter()
+        for x in auto_commit(dl):
+            n += x.shape[0]
+        if args.device.startswith("cuda"):
+            torch.cuda.synchronize()
+        el = time.perf_counter() - t0 - 2.0  # the consumers' end-of-stream timeout
+        br.close()
+        committed = src.committed_offsets("trainer", "t")
+        out["end_to_end"] = {"records": n, "s": round(el, 3), "records_per_s": round(n / el, 1),
+                             "gb_per_s": round(n * args.dim * 4 / el / 1e9, 2),
+                             "decode": "device" if dl._span() else "host",
+                             "cluster_committed_ok": all(v == args.records for v in committed.values()),
+                             "loader": {k: v for k, v in dl.stats_summary().items()
+                                        if k in ("worker_fill_us_per_batch", "commit_latency_p99_us",
+                                                 "log_mib_unpinned")}}
+    finally:
+        for pr in procs:
+            pr.terminate()
+        src.destroy()
+    print(json.dumps(out))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

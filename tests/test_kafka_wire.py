@@ -447,3 +447,37 @@ def test_corrupt_compressed_batch_stops_the_partition(broker, server):
 
 class Vec64(KafkaDataset):
     schema = FixedWidth(torch.float32, (64,))
+
+
+def test_multi_node_cluster_fetches_from_each_leader(broker):
+    """Three nodes, partition p led by node p % 3: the replicator opens one fetch thread per
+    leader; a node asked for a partition it does not lead answers NOT_LEADER."""
+    import socket as _s
+
+    broker.create_topic("t", 6)
+    broker.fill("t", 300, "fixed_f32", size=16, records_per_batch=30)
+    socks = [_s.socket() for _ in range(3)]
+    for s in socks:
+        s.bind(("127.0.0.1", 0))
+    ports = [s.getsockname()[1] for s in socks]
+    for s in socks:
+        s.close()
+    cluster = [(i, "127.0.0.1", ports[i]) for i in range(3)]
+    nodes = [KafkaWireServer(broker, port=ports[i], node_id=i, cluster=cluster).start() for i in range(3)]
+    try:
+        c = core().WireClient(nodes[0].address)
+        assert [p[1] for p in c.metadata("t")[1]] == [0, 1, 2, 0, 1, 2]
+        assert sorted(b[0] for b in c.brokers()) == [0, 1, 2]
+        with bridge(nodes[2], group_id="g") as br:  # bootstrap through any node
+            assert br.wait_caught_up(10)
+            for p in range(6):
+                assert log_bytes(br.local, "t", p) == log_bytes(broker, "t", p)
+            assert br.errors == 0
+            br.local.commit("g", {TopicPartition("t", p): 100 + p for p in range(6)})
+            br.flush()
+        assert broker.committed_offsets("g", "t") == {p: 100 + p for p in range(6)}
+        fetched = [n.requests.get(1, 0) for n in nodes]
+        assert all(f > 0 for f in fetched), fetched
+    finally:
+        for n in nodes:
+            n.close()

@@ -99,8 +99,9 @@ class _W:
             self.i32(len(b))
             self.parts.append(b)
 
-    def data(self) -> bytes:
-        return b"".join(self.parts)
+    def data(self) -> list:
+        """The response as a buffer list: record sets stay views of the mapped logs (no copy)."""
+        return self.parts
 
 
 def control_batch(base_offset: int, timestamp_ms: int = 0, commit: bool = True) -> bytes:
@@ -138,14 +139,20 @@ def _varint(v: int) -> bytes:
 class KafkaWireServer:
     """Serves a :class:`SyntheticBroker` over the Kafka protocol on ``host:port`` (0: a free port)."""
 
-    def __init__(self, broker: SyntheticBroker, host: str = "127.0.0.1", port: int = 0, node_id: int = 0):
+    def __init__(self, broker: SyntheticBroker, host: str = "127.0.0.1", port: int = 0, node_id: int = 0,
+                 cluster: list[tuple[int, str, int]] | None = None):
+        """``cluster``: every node of a multi-node test cluster as (node_id, host, port), this one
+        included; partition p is led by ``cluster[p % len(cluster)]`` and fetches sent to another
+        node answer NOT_LEADER.  None: a single-node cluster (this server leads everything)."""
         self.broker = broker
         self.node_id = node_id
+        self.cluster = cluster
         self._lock = threading.Lock()
         self._fetch_faults: dict[tuple[str, int], list[int]] = {}
         self._commit_faults: list[int] = []
         self.partial_tail = False          # cut every record set inside its last batch
         self.requests: dict[int, int] = {}  # api key -> count
+        self._views: dict[int, memoryview] = {}
         srv = self
 
         class Handler(socketserver.BaseRequestHandler):
@@ -160,10 +167,11 @@ class KafkaWireServer:
                         req = _recv_exact(self.request, n)
                         if req is None:
                             return
-                        resp = srv._dispatch(req)
-                        if resp is None:
+                        parts = srv._dispatch(req)
+                        if parts is None:
                             return
-                        self.request.sendall(struct.pack(">i", len(resp)) + resp)
+                        n = sum(len(b) for b in parts)
+                        _sendall_vec(self.request, [struct.pack(">i", n)] + parts)
                 except (ConnectionError, OSError):
                     return
 
@@ -173,6 +181,8 @@ class KafkaWireServer:
 
         self._srv = Server((host, port), Handler)
         self.host, self.port = self._srv.server_address[:2]
+        if self.cluster is None:
+            self.cluster = [(node_id, self.host, self.port)]
         self._thread = threading.Thread(target=self._srv.serve_forever, daemon=True, name="kafka-wire-server")
 
     # ------------------------------------------------------------ lifecycle
@@ -205,7 +215,13 @@ class KafkaWireServer:
             self._commit_faults.extend([code] * n)
 
     # ------------------------------------------------------------ protocol
-    def _dispatch(self, req: bytes) -> bytes | None:
+    def _log(self, pidx: int) -> memoryview:
+        v = self._views.get(pidx)
+        if v is None:
+            v = self._views[pidx] = self.broker.native.log_view(pidx)
+        return v
+
+    def _dispatch(self, req: bytes) -> list | None:
         r = _R(req)
         key, ver, corr = r.i16(), r.i16(), r.i32()
         r.str()  # client id
@@ -235,13 +251,15 @@ class KafkaWireServer:
 
     def _api_3(self, r: _R, ver: int, w: _W) -> None:  # Metadata v0/v1
         names = self._topic_names(r, ver)
-        w.i32(1)
-        w.i32(self.node_id)
-        w.str(self.host)
-        w.i32(self.port)
+        w.i32(len(self.cluster))
+        for nid, host, port in self.cluster:
+            w.i32(nid)
+            w.str(host)
+            w.i32(port)
+            if ver >= 1:
+                w.str(None)  # rack
         if ver >= 1:
-            w.str(None)  # rack
-            w.i32(self.node_id)  # controller
+            w.i32(self.cluster[0][0])  # controller
         w.i32(len(names))
         for name in names:
             if not self.broker.has_topic(name):
@@ -258,13 +276,17 @@ class KafkaWireServer:
                 w.i8(0)
             w.i32(n)
             for p in range(n):
+                leader = self.leader(p)
                 w.i16(NONE)
                 w.i32(p)
-                w.i32(self.node_id)
+                w.i32(leader)
                 w.i32(1)
-                w.i32(self.node_id)
+                w.i32(leader)
                 w.i32(1)
-                w.i32(self.node_id)
+                w.i32(leader)
+
+    def leader(self, partition: int) -> int:
+        return self.cluster[partition % len(self.cluster)][0]
 
     def _api_2(self, r: _R, ver: int, w: _W) -> None:  # ListOffsets v0/v1
         r.i32()  # replica
@@ -342,6 +364,8 @@ class KafkaWireServer:
             po = []
             for p, off, pmax in parts:
                 fault = faults.get((name, p))
+                if fault is None and self.leader(p) != self.node_id:
+                    fault = NOT_LEADER
                 if fault is not None:
                     po.append((p, fault, -1, None))
                     continue
@@ -352,12 +376,14 @@ class KafkaWireServer:
                     continue
                 try:
                     budget = max(0, min(pmax, max_bytes - total))
-                    data, hw, _start = nat.read_batches(pidx, off, max(budget, 1))
+                    pos, nbytes, hw, _start = nat.batch_range(pidx, off, max(budget, 1))
                 except Exception:  # noqa: BLE001 -- OffsetOutOfRange
                     po.append((p, OFFSET_OUT_OF_RANGE, nat.high_watermark(pidx), None))
                     continue
-                if data and self.partial_tail:
+                data = self._log(pidx)[pos:pos + nbytes]  # a view: the record set is sent from the log
+                if nbytes and self.partial_tail:
                     # add the front half of the next batch, as a broker cutting at partition_max_bytes does
+                    data = bytes(data)
                     try:
                         more, _, _ = nat.read_batches(pidx, _next_offset(data), 1)
                         data = data + more[:max(12, len(more) // 2)]
@@ -440,6 +466,20 @@ def _next_offset(data: bytes) -> int:
     base = struct.unpack_from(">q", data, o)[0]
     (delta,) = struct.unpack_from(">i", data, o + 23)
     return base + delta + 1
+
+
+def _sendall_vec(sock, bufs: list) -> None:
+    """sendall over a buffer list (scatter-gather; partial sends resumed)."""
+    views = [memoryview(b) for b in bufs if len(b)]
+    while views:
+        sent = sock.sendmsg(views[:512])
+        while sent:
+            if sent >= len(views[0]):
+                sent -= len(views[0])
+                views.pop(0)
+            else:
+                views[0] = views[0][sent:]
+                sent = 0
 
 
 def _recv_exact(sock, n: int) -> bytes | None:

@@ -373,6 +373,31 @@ PYBIND11_MODULE(_tkcore, m) {
              return py::make_tuple(py::bytes(reinterpret_cast<const char*>(b.log_base(p)) + pos0, end - pos0), hw, start);
            },
            py::arg("pidx"), py::arg("offset"), py::arg("max_bytes"))
+      .def("batch_range",
+           [](Broker& b, uint32_t p, int64_t offset, uint64_t max_bytes) -> py::tuple {
+             // read_batches without the copy: (log byte position, bytes, high watermark, log start)
+             PartitionEntry& P = b.part(p);
+             const int64_t hw = P.high_watermark.load(std::memory_order_acquire);
+             const int64_t start = P.log_start_offset.load(std::memory_order_acquire);
+             if (offset < start || offset > hw) throw OffsetOutOfRange("offset " + std::to_string(offset) + " out of range");
+             if (offset == hw) return py::make_tuple(uint64_t(0), uint64_t(0), hw, start);
+             const IndexEntry* idx = b.index_base(p);
+             const uint64_t nb = P.n_batches.load(std::memory_order_acquire);
+             const int64_t i = b.find_batch(p, offset, -1);
+             const uint64_t pos0 = idx[i].pos;
+             uint64_t end = pos0 + idx[i].size;
+             for (uint64_t j = uint64_t(i) + 1; j < nb && idx[j].pos + idx[j].size - pos0 <= max_bytes; ++j)
+               end = idx[j].pos + idx[j].size;
+             return py::make_tuple(pos0, end - pos0, hw, start);
+           },
+           py::arg("pidx"), py::arg("offset"), py::arg("max_bytes"))
+      .def("log_view",
+           [](Broker& b, uint32_t p) {
+             // the whole mapped log of a partition, read-only (the wire server sends from it)
+             return py::memoryview::from_memory(reinterpret_cast<const void*>(b.log_base(p)),
+                                                py::ssize_t(b.part(p).log_capacity));
+           },
+           py::keep_alive<0, 1>())
       .def("reset_empty", &Broker::reset_empty)
       .def("ingest_bytes",
            [](Broker& b, uint32_t p, py::bytes data, int64_t from_offset, bool keep_control) {
