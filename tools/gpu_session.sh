@@ -51,7 +51,7 @@ for s in ${STEPS:-pytest_new}; do
     proftok) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/proftok" -o run -- python3 "$OLDPWD/benchmarks/varlen_tokens.py" --steps 500 > "$OLDPWD/gpurun_out/proftok.log" 2>&1) || exit $?
              tail -1 gpurun_out/proftok.log | cut -c1-200 ;;
     bridge) run bridge_e2e 600 python benchmarks/bridge_e2e.py
-            run bridge_e2e_1node 600 python benchmarks/bridge_e2e.py --nodes 1 ;;
+            run bridge_e2e_1node 600 python benchmarks/bridge_e2e.py --nodes 1
             run bridge_e2e_8node 600 python benchmarks/bridge_e2e.py --nodes 8 --workers 8 ;;
     pytest_bridge) run pytest_bridge 400 python -u -m pytest tests/test_gpu_bridge.py -x -v -p no:cacheprovider --timeout 240 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
