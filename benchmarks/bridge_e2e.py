@@ -61,6 +61,9 @@ def main() -> int:
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--partition-fetch-mib", type=int, default=8)
+    ap.add_argument("--max-lag-mib", type=int, default=512)
+    ap.add_argument("--no-release", action="store_true", help="keep committed replica bytes (no unpin/punch)")
+    ap.add_argument("--stats", action="store_true")
     args = ap.parse_args()
 
     from torchkafka_amd.broker import KafkaBridge, SyntheticBroker
@@ -109,7 +112,7 @@ def main() -> int:
         dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
         br = KafkaBridge(boot, "t", group_id="trainer", url=f"shm://tkbe2e-e-{os.getpid()}", log_capacity=1 << 34,
                          index_capacity=1 << 22, max_partition_fetch_bytes=args.partition_fetch_mib << 20,
-                         max_lag_bytes=512 << 20)
+                         max_lag_bytes=args.max_lag_mib << 20, release_consumed=not args.no_release)
         dl = DeviceLoader(Rows.placeholder(), args.batch_size, num_workers=args.workers, device=args.device,
                           dtype=dtype, worker_init_fn=Rows.init_worker("t", bootstrap_servers=br.url,
                                                                        group_id="trainer",
@@ -127,6 +130,8 @@ def main() -> int:
             torch.cuda.synchronize()
         el = t_last - t_first
         out["startup_to_first_batch_s"] = round(t_first - t0, 3)
+        if args.stats:
+            print(json.dumps({"loader": dl.stats_summary(), "bridge": br.stats()}), file=sys.stderr)
         n_timed = n - n_first
         br.close()
         committed = src.committed_offsets("trainer", "t")
