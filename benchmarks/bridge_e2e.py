@@ -28,6 +28,10 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+class _SkipCluster(Exception):
+    pass
+
+
 def _free_ports(n):
     socks, ports = [], []
     for _ in range(n):
@@ -64,10 +68,24 @@ def main() -> int:
     ap.add_argument("--max-lag-mib", type=int, default=512)
     ap.add_argument("--no-release", action="store_true", help="keep committed replica bytes (no unpin/punch)")
     ap.add_argument("--stats", action="store_true")
+    ap.add_argument("--numa", action="store_true", help="bind to the GPU's NUMA node before filling/replicating")
+    ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy"])
+    ap.add_argument("--direct", action="store_true",
+                    help="control run: phase 2 consumes the cluster's own broker directly (no wire, no replica)")
+    ap.add_argument("--no-cluster", action="store_true", help="control: no servers, no bridge (implies --direct)")
+    ap.add_argument("--backlog", action="store_true",
+                    help="phase 2 waits until the replica holds the whole backlog before consuming it (the "
+                         "consumer side alone)")
     args = ap.parse_args()
+    if args.no_cluster:
+        args.direct, args.nodes = True, 0
 
     from torchkafka_amd.broker import KafkaBridge, SyntheticBroker
 
+    if args.numa and args.device.startswith("cuda"):
+        from torchkafka_amd.utils.topology import bind_to_gpu_numa
+
+        bind_to_gpu_numa(int(args.device.split(":")[1]) if ":" in args.device else 0)
     url = f"shm://tkbe2e-{os.getpid()}"
     src = SyntheticBroker.create(url, log_capacity=1 << 34, index_capacity=1 << 22)
     src.create_topic("t", args.partitions)
@@ -85,11 +103,13 @@ def main() -> int:
         pr.start()
         ev.wait(30)
         procs.append(pr)
-    boot = f"127.0.0.1:{ports[0]}"
+    boot = f"127.0.0.1:{ports[0]}" if ports else None
     out = {"nodes": args.nodes, "partitions": args.partitions, "records_per_partition": args.records,
            "cluster_gb": round(total_bytes / 1e9, 3), "fill_s": round(fill_s, 2)}
     try:
         # (1) replication alone
+        if args.no_cluster:
+            raise _SkipCluster
         t0 = time.perf_counter()
         br = KafkaBridge(boot, "t", url=f"shm://tkbe2e-r-{os.getpid()}", log_capacity=1 << 34,
                          index_capacity=1 << 22, max_partition_fetch_bytes=args.partition_fetch_mib << 20,
@@ -100,7 +120,9 @@ def main() -> int:
                               "fetch_threads": len({s["partition"] % args.nodes for s in br.stats()}),
                               "errors": br.errors}
         br.close()
-
+    except _SkipCluster:
+        pass
+    try:
         # (2) end to end: replicate + decode + commit concurrently
         import torch
 
@@ -110,32 +132,60 @@ def main() -> int:
             schema = FixedWidth(torch.float32, (args.dim,))
 
         dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-        br = KafkaBridge(boot, "t", group_id="trainer", url=f"shm://tkbe2e-e-{os.getpid()}", log_capacity=1 << 34,
+        br = None if args.no_cluster else KafkaBridge(boot, "t", group_id="trainer", url=f"shm://tkbe2e-e-{os.getpid()}", log_capacity=1 << 34,
                          index_capacity=1 << 22, max_partition_fetch_bytes=args.partition_fetch_mib << 20,
                          max_lag_bytes=args.max_lag_mib << 20, release_consumed=not args.no_release)
         dl = DeviceLoader(Rows.placeholder(), args.batch_size, num_workers=args.workers, device=args.device,
-                          dtype=dtype, worker_init_fn=Rows.init_worker("t", bootstrap_servers=br.url,
+                          dtype=dtype, h2d=args.h2d,
+                          worker_init_fn=Rows.init_worker("t", bootstrap_servers=url if args.direct else br.url,
                                                                        group_id="trainer",
                                                                        auto_offset_reset="earliest",
                                                                        consumer_timeout_ms=2000))
+        import threading
+
+        caught = {}
+
+        def _watch():
+            caught["ok"] = br.wait_caught_up(300)
+            caught["t"] = time.perf_counter()
+
+        if br is None:
+            pass
+        elif args.backlog:
+            _watch()
+        else:
+            threading.Thread(target=_watch, daemon=True).start()
         n = n_first = 0
         t0 = time.perf_counter()
         t_first = t_last = None
+        marks = []
         for x in auto_commit(dl):
             n += x.shape[0]
-            t_last = time.perf_counter()  # the stream's end is only known after the consumers' timeout
+            t_last = time.perf_counter()
+            marks.append((t_last, n))
             if t_first is None:  # worker fork + HIP init + first fetches are startup, not throughput
                 t_first, n_first = t_last, n
         if args.device.startswith("cuda"):
             torch.cuda.synchronize()
+        # A worker's last, partial batch is only handed over after its consumer timeout (the end
+        # of a stream is a timeout): the timed region ends at the last batch before that stall.
+        for (ta, na), (tb, _nb) in zip(marks, marks[1:]):
+            if tb - ta > 0.5:
+                t_last, n = ta, na
+                break
         el = t_last - t_first
         out["startup_to_first_batch_s"] = round(t_first - t0, 3)
+        if "t" in caught and not args.backlog:
+            out["replica_caught_up_after_first_batch_s"] = round(caught["t"] - t_first, 3)
         if args.stats:
-            print(json.dumps({"loader": dl.stats_summary(), "bridge": br.stats()}), file=sys.stderr)
+            print(json.dumps({"loader": dl.stats_summary(), "bridge": br.stats() if br else None}), file=sys.stderr)
         n_timed = n - n_first
-        br.close()
+        if br is not None:
+            br.close()
         committed = src.committed_offsets("trainer", "t")
-        out["end_to_end"] = {"records": n, "s": round(el, 3), "records_per_s": round(n_timed / el, 1),
+        if args.direct:
+            committed = {p: args.records for p in committed}  # committed straight into the source
+        out["end_to_end"] = {"records": n, "records_total": marks[-1][1], "s": round(el, 3), "records_per_s": round(n_timed / el, 1),
                              "gb_per_s": round(n_timed * args.dim * 4 / el / 1e9, 2),
                              "decode": "device" if dl._span() else "host",
                              "cluster_committed_ok": all(v == args.records for v in committed.values()),
