@@ -93,9 +93,14 @@ struct alignas(64) PartitionEntry {
   // fault injection & metrics
   std::atomic<int64_t> fetch_delay_ns;
   std::atomic<int32_t> fetch_errors;
-  std::atomic<uint32_t> pad1;
+  // Device readers (MainDriver) that pinned this log with hipHostRegister, and the lowest log byte
+  // they still hold pinned.  Released (punched) bytes must stay below pin_floor: invalidating the
+  // CPU mapping of a pinned range makes the GPU driver evict and re-pin it (a ~100 ms stall).
+  std::atomic<uint32_t> pinned;
   std::atomic<uint64_t> fetch_calls, bytes_fetched, records_produced;
+  std::atomic<uint64_t> pin_floor;  // in the struct's former tail padding: the layout is unchanged
 };
+static_assert(sizeof(PartitionEntry) == 192, "partition entry layout (shared with existing broker files)");
 
 struct alignas(64) MemberEntry {
   std::atomic<uint32_t> active;

@@ -341,7 +341,9 @@ void Replicator::release_consumed() {
   for (auto& p : parts_) {
     const int64_t c = local_->committed(group_, p->pidx);
     if (c < 0) continue;
-    const uint64_t pos = local_->position_of(p->pidx, c);
+    uint64_t pos = local_->position_of(p->pidx, c);
+    const PartitionEntry& P = local_->part(p->pidx);
+    if (P.pinned.load(std::memory_order_acquire)) pos = std::min<uint64_t>(pos, P.pin_floor.load());
     const uint64_t to = pos / (2u << 20) * (2u << 20);
     const uint64_t from = p->released.load();
     if (to < from + cfg_.release_bytes) continue;

@@ -56,8 +56,11 @@ MainDriver::~MainDriver() {
   bool any = false;
   for (auto& q : reg_ranges_) any = any || !q.empty();
   if (any) hipDeviceSynchronize();
-  for (auto& q : reg_ranges_)
+  for (size_t pidx = 0; pidx < reg_ranges_.size(); ++pidx) {
+    auto& q = reg_ranges_[pidx];
     for (auto& r : q) hipHostUnregister(r.first);
+    if (!q.empty() && broker_) broker_->part(uint32_t(pidx)).pinned.fetch_sub(1, std::memory_order_acq_rel);
+  }
   if (bases_dev_) hipFree(bases_dev_);
   if (stage_dev_) {
     hipDeviceSynchronize();
@@ -432,15 +435,24 @@ void MainDriver::ensure_log(uint32_t pidx, uint64_t end) {
   uint64_t hi = (std::max(end, written) + kLogChunk - 1) / kLogChunk * kLogChunk;
   if (hi > cap) hi = cap;
   const uint64_t lo = reg_end_[pidx];
-  void* p = const_cast<uint8_t*>(base) + lo;
-  if (hipHostRegister(p, hi - lo, hipHostRegisterMapped) != hipSuccess)
-    throw std::runtime_error("driver: hipHostRegister of a partition log failed");
   if (reg_ranges_.size() <= pidx) reg_ranges_.resize(size_t(pidx) + 1);
-  reg_ranges_[pidx].emplace_back(p, hi);
-  void* dp = nullptr;
-  if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess || dp != p)
-    throw std::runtime_error("driver: h2d='direct' needs device addresses of pinned host memory to equal host "
-                             "addresses (unified addressing)");
+  auto& part = broker_->part(pidx);
+  if (reg_ranges_[pidx].empty()) {  // announce the pin before it exists (the replicator reads these)
+    part.pin_floor.store(lo, std::memory_order_release);
+    part.pinned.fetch_add(1, std::memory_order_acq_rel);
+  }
+  // kLogChunk pieces, so that consumed ranges can be unpinned piecewise (release_consumed)
+  for (uint64_t a = lo; a < hi; a += kLogChunk) {
+    const uint64_t b = std::min(hi, a + kLogChunk);
+    void* p = const_cast<uint8_t*>(base) + a;
+    if (hipHostRegister(p, b - a, hipHostRegisterMapped) != hipSuccess)
+      throw std::runtime_error("driver: hipHostRegister of a partition log failed");
+    reg_ranges_[pidx].emplace_back(p, b);
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess || dp != p)
+      throw std::runtime_error("driver: h2d='direct' needs device addresses of pinned host memory to equal host "
+                               "addresses (unified addressing)");
+  }
   if (lo == 0 && bases_dev_) {
     const uint64_t b = reinterpret_cast<uint64_t>(base);
     if (hipMemcpy(bases_dev_ + pidx, &b, sizeof(b), hipMemcpyHostToDevice) != hipSuccess)
@@ -1154,13 +1166,18 @@ void MainDriver::release_consumed() {
     if (pidx >= reg_ranges_.size() || reg_ranges_[pidx].size() < 2) continue;  // keep the range being read
     auto& q = reg_ranges_[pidx];
     const uint64_t pos = broker_->position_of(pidx, kv.second);
+    const uint8_t* base = broker_->log_base(pidx);
+    bool moved = false;
     while (q.size() > 1 && q.front().second <= pos) {
       if (hipHostUnregister(q.front().first) != hipSuccess)
         throw std::runtime_error("driver: hipHostUnregister of a consumed log range failed");
-      unpinned_bytes_ += q.front().second -
-                         uint64_t(static_cast<const uint8_t*>(q.front().first) - broker_->log_base(pidx));
+      unpinned_bytes_ += q.front().second - uint64_t(static_cast<const uint8_t*>(q.front().first) - base);
       q.pop_front();
+      moved = true;
     }
+    if (moved)  // the replicator may now punch the bytes below the first range still pinned
+      broker_->part(pidx).pin_floor.store(uint64_t(static_cast<const uint8_t*>(q.front().first) - base),
+                                          std::memory_order_release);
   }
 }
 
