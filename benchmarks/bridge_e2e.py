@@ -66,8 +66,11 @@ def main() -> int:
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--partition-fetch-mib", type=int, default=8)
     ap.add_argument("--max-lag-mib", type=int, default=512)
+    ap.add_argument("--release-mib", type=int, default=1024, help="consumed bytes kept resident per partition")
     ap.add_argument("--no-release", action="store_true", help="keep committed replica bytes (no unpin/punch)")
     ap.add_argument("--stats", action="store_true")
+    ap.add_argument("--unpin-only", action="store_true",
+                    help="experiment: the device driver unpins consumed ranges, the replicator frees nothing")
     ap.add_argument("--numa", action="store_true", help="bind to the GPU's NUMA node before filling/replicating")
     ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy"])
     ap.add_argument("--direct", action="store_true",
@@ -134,7 +137,11 @@ def main() -> int:
         dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
         br = None if args.no_cluster else KafkaBridge(boot, "t", group_id="trainer", url=f"shm://tkbe2e-e-{os.getpid()}", log_capacity=1 << 34,
                          index_capacity=1 << 22, max_partition_fetch_bytes=args.partition_fetch_mib << 20,
-                         max_lag_bytes=args.max_lag_mib << 20, release_consumed=not args.no_release)
+                         max_lag_bytes=args.max_lag_mib << 20,
+                         release_consumed=not (args.no_release or args.unpin_only),
+                         release_bytes=args.release_mib << 20)
+        if br is not None and args.unpin_only:
+            br.local.native.flags = 1  # kReleaseConsumed: the driver unpins, nobody punches
         dl = DeviceLoader(Rows.placeholder(), args.batch_size, num_workers=args.workers, device=args.device,
                           dtype=dtype, h2d=args.h2d,
                           worker_init_fn=Rows.init_worker("t", bootstrap_servers=url if args.direct else br.url,

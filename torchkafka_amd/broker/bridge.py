@@ -19,11 +19,12 @@ the last one::
         ...
     bridge.close()          # forwards the final commit
 
-Memory: with a ``group_id`` the committed part of every replica log is released (the log start
-moves up to the committed offset, the bytes below it are punched out of the shm files and the
-device loader unpins them), so a long stream holds about ``max_lag_bytes`` per partition in host
-memory, not the whole stream; ``log_capacity`` (sparse) bounds the bytes one replica partition
-can take in over its lifetime.
+Memory: with a ``group_id`` the committed part of every replica log is released (the device
+loader unpins it, the log start moves up to the committed offset and a background thread punches
+the bytes below it out of the shm files, keeping the last ``release_bytes`` of consumed log), so a
+long stream holds about ``max_lag_bytes + release_bytes`` per partition in host memory, not the
+whole stream; ``log_capacity`` (sparse) bounds the bytes one replica partition can take in over
+its lifetime.
 
 Semantics: at-least-once, like the reference's commit-after-batch.  A commit lands in the local
 table synchronously and reaches the cluster within ``commit_interval_ms`` (5 ms); a crash in
@@ -56,7 +57,7 @@ class KafkaBridge:
                  fetch_max_bytes: int = 64 << 20, max_partition_fetch_bytes: int = 8 << 20,
                  request_timeout_ms: int = 30000, commit_interval_ms: int = 5, fetchers: int = 0,
                  client_id: str = "torchkafka-bridge", release_consumed: bool = True,
-                 release_bytes: int = 64 << 20, start: bool = True):
+                 release_bytes: int = 1 << 30, start: bool = True):
         if not isinstance(bootstrap_servers, str):
             bootstrap_servers = ",".join(bootstrap_servers)
         self.bootstrap_servers = bootstrap_servers

@@ -399,6 +399,7 @@ PYBIND11_MODULE(_tkcore, m) {
            },
            py::keep_alive<0, 1>())
       .def("reset_empty", &Broker::reset_empty)
+      .def_property("flags", &Broker::flags, &Broker::set_flags)
       .def("ingest_bytes",
            [](Broker& b, uint32_t p, py::bytes data, int64_t from_offset, bool keep_control) {
              std::string s = data;
@@ -523,7 +524,7 @@ PYBIND11_MODULE(_tkcore, m) {
            py::arg("timeout_ms") = 30000, py::arg("max_lag_bytes") = int64_t(1) << 30,
            py::arg("commit_interval_ms") = 5, py::arg("fetchers") = 0, py::arg("log_capacity") = 0,
            py::arg("index_capacity") = 0, py::arg("client_id") = "torchkafka-replicator",
-           py::arg("release_consumed") = true, py::arg("release_bytes") = uint64_t(64) << 20)
+           py::arg("release_consumed") = true, py::arg("release_bytes") = uint64_t(1) << 30)
       .def("start", &Replicator::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Replicator::stop, py::arg("flush") = true, py::call_guard<py::gil_scoped_release>())
       .def("flush_commits", &Replicator::flush_commits, py::call_guard<py::gil_scoped_release>())

@@ -120,6 +120,7 @@ void Replicator::start() {
   if (!cfg_.group.empty()) {
     commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", cfg_.timeout_ms);
     threads_.emplace_back([this]() { commit_loop(); });
+    if (cfg_.release_consumed) threads_.emplace_back([this]() { release_loop(); });
   }
 }
 
@@ -323,7 +324,6 @@ void Replicator::commit_loop() {
       if (!commit_client_)
         commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", cfg_.timeout_ms);
       forward(*commit_client_);
-      if (cfg_.release_consumed) release_consumed();
       backoff_ms = cfg_.commit_interval_ms;
     } catch (const std::exception& e) {
       set_error(std::string("replicator: commit: ") + e.what());
@@ -334,22 +334,41 @@ void Replicator::commit_loop() {
 }
 
 // Committed log bytes are never read again (the bridge's broker has one consuming group): move
-// the log start up to the committed offset, then punch the bytes below its batch out of the log
-// file.  Host memory then holds the uncommitted window (max_lag_bytes) instead of the whole stream.
-// A device loader unpins its registered ranges below the same position (MainDriver).
-void Replicator::release_consumed() {
-  for (auto& p : parts_) {
-    const int64_t c = local_->committed(group_, p->pidx);
-    if (c < 0) continue;
-    uint64_t pos = local_->position_of(p->pidx, c);
-    const PartitionEntry& P = local_->part(p->pidx);
-    if (P.pinned.load(std::memory_order_acquire)) pos = std::min<uint64_t>(pos, P.pin_floor.load());
-    const uint64_t to = pos / (2u << 20) * (2u << 20);
-    const uint64_t from = p->released.load();
-    if (to < from + cfg_.release_bytes) continue;
-    local_->delete_records(p->pidx, c);  // readers below c now see OffsetOutOfRange, as after retention
-    local_->release_log(p->pidx, from, to);
-    p->released.store(to);
+// the log start up to the committed offset, then punch the bytes below it out of the log file, so
+// host memory holds the uncommitted window (max_lag_bytes) plus `release_bytes` of consumed log,
+// not the whole stream.  Bytes a device loader still holds pinned are never punched (pin_floor):
+// invalidating a pinned range makes the GPU driver evict and re-pin it.  Punching frees pages at
+// ~7 GB/s and holds the file's invalidate lock (which page faults on the same file wait for), so
+// it runs on its own thread in 2 MiB steps with a pause between them: workers and the fetch
+// threads fault pages in between, and a fast consumer is never stalled by it (measured:
+// benchmarks/bridge_e2e.py; 64 MiB punches in the commit thread cost ~160 ms commit stalls).
+void Replicator::release_loop() {
+  constexpr uint64_t kStep = 2u << 20;
+  while (!stop_.load()) {
+    bool worked = false;
+    for (auto& p : parts_) {
+      if (stop_.load()) break;
+      const int64_t c = local_->committed(group_, p->pidx);
+      if (c < 0) continue;
+      uint64_t pos = local_->position_of(p->pidx, c);
+      const PartitionEntry& P = local_->part(p->pidx);
+      if (P.pinned.load(std::memory_order_acquire)) pos = std::min<uint64_t>(pos, P.pin_floor.load());
+      if (pos <= cfg_.release_bytes) continue;
+      const uint64_t target = (pos - cfg_.release_bytes) / kStep * kStep;
+      uint64_t from = p->released.load();
+      if (target <= from) continue;
+      local_->delete_records(p->pidx, c);  // readers below c now see OffsetOutOfRange, as after retention
+      const uint64_t until = std::min(target, from + 16 * kStep);  // then the next partition
+      while (from < until && !stop_.load()) {
+        const uint64_t to = std::min(until, (from / kStep + 1) * kStep);
+        local_->release_log(p->pidx, from, to);
+        from = to;
+        p->released.store(from);
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+      }
+      worked = true;
+    }
+    if (!worked) sleep_ms(10);
   }
 }
 

@@ -46,7 +46,7 @@ struct ReplicaConfig {
   int32_t commit_interval_ms = 5;
   int32_t fetchers = 0;                // fetch threads (0: one per partition leader, at most 8)
   bool release_consumed = true;        // free committed log bytes (punch holes; kReleaseConsumed)
-  uint64_t release_bytes = 64u << 20;  // ... in steps of at least this many bytes
+  uint64_t release_bytes = 1u << 30;   // ... keeping this many consumed bytes per partition resident
   uint64_t log_capacity = 0;           // local topic creation (0: the broker default)
   uint64_t index_capacity = 0;
 };
@@ -100,7 +100,7 @@ class Replicator {
     std::atomic<uint64_t> bytes{0}, batches{0}, control{0}, fetches{0}, throttled{0};
     std::atomic<uint64_t> released{0};  // log bytes [0, released) freed (committed past)
   };
-  void release_consumed();
+  void release_loop();
   void fetch_loop(std::vector<Part*> mine);
   void commit_loop();
   bool throttled(Part& p);
