@@ -227,7 +227,7 @@ def test_committed_log_bytes_are_released(broker, server):
     out of the shm file (st_blocks drops), consumers carry on from the committed offset."""
     broker.create_topic("t", 1)
     broker.fill("t", 10000, "fixed_f32", size=256, records_per_batch=64)  # ~10.3 MB
-    with bridge(server, group_id="g", release_bytes=2 << 20, log_capacity=64 << 20) as br:
+    with bridge(server, group_id="g", release_bytes=2 << 20, release_step=2 << 20, log_capacity=64 << 20) as br:
         assert br.wait_caught_up(10)
         pidx = br.local.pidx("t", 0)
         path = os.path.join(br.local.dir, f"p{pidx:05d}.log")
@@ -238,7 +238,7 @@ def test_committed_log_bytes_are_released(broker, server):
                                                             auto_offset_reset="earliest", consumer_timeout_ms=300))
         n = sum(x.shape[0] for x in auto_commit(dl))
         assert n == 10000
-        assert wait_for(lambda: br.stats()[0]["released"] >= 6 << 20)
+        assert wait_for(lambda: br.stats()[0]["released"] >= 6 << 20), br.stats()
         assert os.stat(path).st_blocks * 512 <= before - (6 << 20)
         assert br.local.beginning_offset("t", 0) > 0
     assert broker.committed("g", "t", 0) == 10000

@@ -21,9 +21,10 @@ the last one::
 
 Memory: with a ``group_id`` the committed part of every replica log is released (the device
 loader unpins it, the log start moves up to the committed offset and a background thread punches
-the bytes below it out of the shm files, keeping the last ``release_bytes`` of consumed log), so a
-long stream holds about ``max_lag_bytes + release_bytes`` per partition in host memory, not the
-whole stream; ``log_capacity`` (sparse) bounds the bytes one replica partition can take in over
+the bytes below it out of the shm files in bursts of ``release_step``, keeping the last
+``release_bytes`` of consumed log), so a long stream holds about ``max_lag_bytes + release_bytes +
+release_step`` per partition in host memory, not the whole stream (each burst costs the GPU of a
+device loader a ~25 ms stall: punching once-pinned pages makes the GPU driver revalidate); ``log_capacity`` (sparse) bounds the bytes one replica partition can take in over
 its lifetime.
 
 Semantics: at-least-once, like the reference's commit-after-batch.  A commit lands in the local
@@ -57,7 +58,7 @@ class KafkaBridge:
                  fetch_max_bytes: int = 64 << 20, max_partition_fetch_bytes: int = 8 << 20,
                  request_timeout_ms: int = 30000, commit_interval_ms: int = 5, fetchers: int = 0,
                  client_id: str = "torchkafka-bridge", release_consumed: bool = True,
-                 release_bytes: int = 1 << 30, start: bool = True):
+                 release_bytes: int = 256 << 20, release_step: int = 1 << 30, start: bool = True):
         if not isinstance(bootstrap_servers, str):
             bootstrap_servers = ",".join(bootstrap_servers)
         self.bootstrap_servers = bootstrap_servers
@@ -75,7 +76,8 @@ class KafkaBridge:
             partition_max_bytes=int(max_partition_fetch_bytes), timeout_ms=int(request_timeout_ms),
             max_lag_bytes=int(max_lag_bytes), commit_interval_ms=int(commit_interval_ms), fetchers=int(fetchers),
             log_capacity=int(log_capacity), index_capacity=int(index_capacity), client_id=client_id,
-            release_consumed=bool(release_consumed), release_bytes=int(release_bytes))
+            release_consumed=bool(release_consumed), release_bytes=int(release_bytes),
+            release_step=int(release_step))
         self._closed = False
         self._lock = threading.Lock()
         self._reported = 0

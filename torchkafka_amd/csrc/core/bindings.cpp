@@ -497,7 +497,7 @@ PYBIND11_MODULE(_tkcore, m) {
                        int32_t max_wait_ms, int32_t max_bytes, int32_t partition_max_bytes, int32_t timeout_ms,
                        int64_t max_lag_bytes, int32_t commit_interval_ms, int32_t fetchers, uint64_t log_capacity,
                        uint64_t index_capacity, const std::string& client_id, bool release_consumed,
-                       uint64_t release_bytes) {
+                       uint64_t release_bytes, uint64_t release_step) {
              ReplicaConfig c;
              c.bootstrap = bootstrap;
              c.topic = topic;
@@ -516,6 +516,7 @@ PYBIND11_MODULE(_tkcore, m) {
              c.client_id = client_id;
              c.release_consumed = release_consumed;
              c.release_bytes = release_bytes;
+             c.release_step = release_step;
              return std::make_unique<Replicator>(std::move(local), c);
            }),
            py::arg("local"), py::arg("bootstrap"), py::arg("topic"), py::arg("group") = "",
@@ -524,7 +525,8 @@ PYBIND11_MODULE(_tkcore, m) {
            py::arg("timeout_ms") = 30000, py::arg("max_lag_bytes") = int64_t(1) << 30,
            py::arg("commit_interval_ms") = 5, py::arg("fetchers") = 0, py::arg("log_capacity") = 0,
            py::arg("index_capacity") = 0, py::arg("client_id") = "torchkafka-replicator",
-           py::arg("release_consumed") = true, py::arg("release_bytes") = uint64_t(1) << 30)
+           py::arg("release_consumed") = true, py::arg("release_bytes") = uint64_t(256) << 20,
+           py::arg("release_step") = uint64_t(1) << 30)
       .def("start", &Replicator::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Replicator::stop, py::arg("flush") = true, py::call_guard<py::gil_scoped_release>())
       .def("flush_commits", &Replicator::flush_commits, py::call_guard<py::gil_scoped_release>())

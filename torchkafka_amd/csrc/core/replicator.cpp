@@ -335,40 +335,40 @@ void Replicator::commit_loop() {
 
 // Committed log bytes are never read again (the bridge's broker has one consuming group): move
 // the log start up to the committed offset, then punch the bytes below it out of the log file, so
-// host memory holds the uncommitted window (max_lag_bytes) plus `release_bytes` of consumed log,
-// not the whole stream.  Bytes a device loader still holds pinned are never punched (pin_floor):
-// invalidating a pinned range makes the GPU driver evict and re-pin it.  Punching frees pages at
-// ~7 GB/s and holds the file's invalidate lock (which page faults on the same file wait for), so
-// it runs on its own thread in 2 MiB steps with a pause between them: workers and the fetch
-// threads fault pages in between, and a fast consumer is never stalled by it (measured:
-// benchmarks/bridge_e2e.py; 64 MiB punches in the commit thread cost ~160 ms commit stalls).
+// host memory holds the uncommitted window (max_lag_bytes) plus up to release_bytes + release_step
+// of consumed log per partition, not the whole stream.  Bytes a device loader still holds pinned
+// are never punched (pin_floor).  Punching a range that was pinned once (even after
+// hipHostUnregister) stalls the GPU of the loader's process for ~20-30 ms per punch, about
+// independent of its size (tools/probes/punch_probe.py, profiles/r02_s5_bridge/punch_probe.log),
+// so releases come in rare bursts: once some partition has release_step (1 GiB) releasable bytes,
+// every partition releases what it can in one punch each, back to back.
 void Replicator::release_loop() {
-  constexpr uint64_t kStep = 2u << 20;
+  constexpr uint64_t kAlign = 2u << 20;
   while (!stop_.load()) {
-    bool worked = false;
+    sleep_ms(10);
+    std::vector<std::pair<Part*, uint64_t>> todo;
+    uint64_t most = 0;
     for (auto& p : parts_) {
-      if (stop_.load()) break;
       const int64_t c = local_->committed(group_, p->pidx);
       if (c < 0) continue;
       uint64_t pos = local_->position_of(p->pidx, c);
       const PartitionEntry& P = local_->part(p->pidx);
       if (P.pinned.load(std::memory_order_acquire)) pos = std::min<uint64_t>(pos, P.pin_floor.load());
       if (pos <= cfg_.release_bytes) continue;
-      const uint64_t target = (pos - cfg_.release_bytes) / kStep * kStep;
-      uint64_t from = p->released.load();
+      const uint64_t target = (pos - cfg_.release_bytes) / kAlign * kAlign;
+      const uint64_t from = p->released.load();
       if (target <= from) continue;
-      local_->delete_records(p->pidx, c);  // readers below c now see OffsetOutOfRange, as after retention
-      const uint64_t until = std::min(target, from + 16 * kStep);  // then the next partition
-      while (from < until && !stop_.load()) {
-        const uint64_t to = std::min(until, (from / kStep + 1) * kStep);
-        local_->release_log(p->pidx, from, to);
-        from = to;
-        p->released.store(from);
-        std::this_thread::sleep_for(std::chrono::microseconds(200));
-      }
-      worked = true;
+      todo.emplace_back(p.get(), target);
+      most = std::max(most, target - from);
     }
-    if (!worked) sleep_ms(10);
+    if (most < cfg_.release_step) continue;
+    for (auto& [p, target] : todo) {
+      const uint64_t from = p->released.load();
+      if (target - from < std::min<uint64_t>(64u << 20, cfg_.release_step)) continue;
+      local_->delete_records(p->pidx, local_->committed(group_, p->pidx));  // readers below see OffsetOutOfRange
+      local_->release_log(p->pidx, from, target);
+      p->released.store(target);
+    }
   }
 }
 

@@ -46,7 +46,8 @@ struct ReplicaConfig {
   int32_t commit_interval_ms = 5;
   int32_t fetchers = 0;                // fetch threads (0: one per partition leader, at most 8)
   bool release_consumed = true;        // free committed log bytes (punch holes; kReleaseConsumed)
-  uint64_t release_bytes = 1u << 30;   // ... keeping this many consumed bytes per partition resident
+  uint64_t release_bytes = 256u << 20; // ... keeping this many consumed bytes per partition resident
+  uint64_t release_step = 1u << 30;    // ... in bursts, once a partition has this many releasable bytes
   uint64_t log_capacity = 0;           // local topic creation (0: the broker default)
   uint64_t index_capacity = 0;
 };
