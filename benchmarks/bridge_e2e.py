@@ -136,7 +136,8 @@ def main() -> int:
             schema = FixedWidth(torch.float32, (args.dim,))
 
         dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-        br = None if args.no_cluster else KafkaBridge(boot, "t", group_id="trainer", url=f"shm://tkbe2e-e-{os.getpid()}", log_capacity=1 << 34,
+        br = None if args.no_cluster else KafkaBridge(
+                         boot, "t", group_id="trainer", url=f"shm://tkbe2e-e-{os.getpid()}", log_capacity=1 << 34,
                          index_capacity=1 << 22, max_partition_fetch_bytes=args.partition_fetch_mib << 20,
                          max_lag_bytes=args.max_lag_mib << 20,
                          release_consumed=not (args.no_release or args.unpin_only),
@@ -193,7 +194,8 @@ def main() -> int:
         committed = src.committed_offsets("trainer", "t")
         if args.direct:
             committed = {p: args.records for p in committed}  # committed straight into the source
-        out["end_to_end"] = {"records": n, "records_total": marks[-1][1], "s": round(el, 3), "records_per_s": round(n_timed / el, 1),
+        out["end_to_end"] = {"records": n, "records_total": marks[-1][1], "s": round(el, 3),
+                             "records_per_s": round(n_timed / el, 1),
                              "gb_per_s": round(n_timed * args.dim * 4 / el / 1e9, 2),
                              "decode": "device" if dl._span() else "host",
                              "cluster_committed_ok": all(v == args.records for v in committed.values()),

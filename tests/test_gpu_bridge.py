@@ -78,7 +78,8 @@ def test_long_stream_unpins_and_releases_consumed_log(broker):
         src.fill("t", 160_000, "fixed_f32", size=256, records_per_batch=64)  # ~165 MB
         with KafkaWireServer(src) as srv:
             br = KafkaBridge(srv.address, "t", group_id="g", url=f"shm://tkgbr-{os.getpid()}-{uuid.uuid4().hex[:6]}",
-                             log_capacity=512 << 20, max_lag_bytes=96 << 20, release_bytes=16 << 20, release_step=64 << 20)
+                             log_capacity=512 << 20, max_lag_bytes=96 << 20, release_bytes=16 << 20,
+                             release_step=64 << 20)
             try:
                 dl = DeviceLoader(Rows.placeholder(), 256, num_workers=1, device="cuda:0", dtype=torch.float32,
                                   worker_init_fn=Rows.init_worker("t", bootstrap_servers=br.url, group_id="g",

@@ -481,3 +481,28 @@ def test_multi_node_cluster_fetches_from_each_leader(broker):
     finally:
         for n in nodes:
             n.close()
+
+
+def test_device_loader_bridges_a_cluster_named_like_the_reference(broker, server):
+    """`init_worker('t', bootstrap_servers='host:port', group_id=...)` -- the reference's usage --
+    works unchanged: the loader mirrors this rank's partitions through a KafkaBridge (bridge='auto')
+    and its commits land in the cluster."""
+    broker.create_topic("t", 4)
+    broker.fill("t", 60, "fixed_f32", size=8, records_per_batch=12)
+    dl = DeviceLoader(Vec8.placeholder(), 16, device="cpu", num_workers=2,
+                      worker_init_fn=Vec8.init_worker("t", bootstrap_servers=[server.address], group_id="ref",
+                                                      auto_offset_reset="earliest", consumer_timeout_ms=400))
+    assert len(dl._bridges) == 1 and dl._servers.startswith("shm://")
+    seen = set()
+    for x in auto_commit(dl):
+        seen |= {(int(p), int(o)) for o, p in x[:, :2].tolist()}
+    dl.close()
+    assert seen == {(p, o) for p in range(4) for o in range(60)}
+    assert broker.committed_offsets("ref", "t") == {p: 60 for p in range(4)}
+
+
+def test_bridge_off_keeps_the_kafka_python_route(server):
+    with pytest.raises(Exception, match="NoBrokersAvailable"):
+        dl = DeviceLoader(Vec8.placeholder(), 16, device="cpu", num_workers=1, bridge=False,
+                          worker_init_fn=Vec8.init_worker("t", bootstrap_servers=server.address, group_id="g"))
+        list(dl)

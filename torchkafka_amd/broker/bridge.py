@@ -24,7 +24,8 @@ loader unpins it, the log start moves up to the committed offset and a backgroun
 the bytes below it out of the shm files in bursts of ``release_step``, keeping the last
 ``release_bytes`` of consumed log), so a long stream holds about ``max_lag_bytes + release_bytes +
 release_step`` per partition in host memory, not the whole stream (each burst costs the GPU of a
-device loader a ~25 ms stall: punching once-pinned pages makes the GPU driver revalidate); ``log_capacity`` (sparse) bounds the bytes one replica partition can take in over
+device loader a ~25 ms stall: punching once-pinned pages makes the GPU driver revalidate);
+``log_capacity`` (sparse) bounds the bytes one replica partition can take in over
 its lifetime.
 
 Semantics: at-least-once, like the reference's commit-after-batch.  A commit lands in the local

@@ -179,6 +179,7 @@ class LoaderConfig:
     h2d: str = "auto"
     decode: str = "auto"
     json_parse: str = "auto"
+    bridge: Any = "auto"
     tuning: Tuning = field(default_factory=Tuning)
 
     def __post_init__(self):
@@ -191,6 +192,7 @@ class LoaderConfig:
             v = getattr(self, name)
             if v not in choices:
                 raise ValueError(f"{name} must be {_CHOICE_HELP.get(name, ' or '.join(map(repr, choices)))}")
+        _check(self.bridge in ("auto", True, False), "bridge must be 'auto', True or False")
         _check(self.lockstep in (True, False, "host", "rccl", "always"),
                "lockstep must be True, False, 'host', 'rccl' or 'always'")
         _check(self.pad_to is None or int(self.pad_to) >= 1, "pad_to must be >= 1 (or None)")

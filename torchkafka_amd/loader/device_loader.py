@@ -40,7 +40,7 @@ from typing import NamedTuple
 
 import torch
 
-from ..client.errors import COMMIT_FAILED_ERRORS, CorruptRecordException
+from ..client.errors import COMMIT_FAILED_ERRORS, CorruptRecordException, KafkaError
 from ..config import LoaderConfig
 from ..ops.collate import CODE_DTYPE, DTYPE_CODE, FLOAT_DTYPES, _stream_ptr, normalize_params
 from ..ops.native import core, hip
@@ -431,6 +431,9 @@ class DeviceLoader:
         self.coalesce_wait_us = int(tun.coalesce_wait_us)
         self.lockstep_depth = int(tun.lockstep_depth)
         self.numa_bind = bool(tun.numa_bind)
+        self._bridges: list = []
+        if self.num_workers > 0 and cfg.bridge is not False:
+            self.worker_init_fn = self._bridge_cluster(self.worker_init_fn, forced=cfg.bridge is True)
         self._group_id, self._servers = self._resolve_commit_target(cfg.group_id, cfg.bootstrap_servers)
         self._sink = self._resolve_sink()
         self._pending_wms: list = []   # finished-but-uncommitted watermark lists
@@ -445,6 +448,57 @@ class DeviceLoader:
         return max(1, self.num_workers)
 
     # ------------------------------------------------------------------ configuration helpers
+    def _bridge_cluster(self, wi, forced: bool):
+        """``bridge='auto'``: workers told to read a real Kafka cluster (``init_worker(topic,
+        bootstrap_servers='host:9092', ...)``, the reference's usage) read a local replica instead,
+        which a native :class:`~torchkafka_amd.broker.KafkaBridge` per topic fills with this rank's
+        partitions; the device path (header walk, gfx950 CRC + decode) then runs unchanged and the
+        commits reach the cluster's group coordinator.  Static sharding only (the bridge assigns
+        partitions by rank; ``sharding='group'`` keeps kafka-python's group membership)."""
+        from ..broker.synthetic import is_synthetic_url
+        from ..models.kafka_dataset import _WorkerInit
+
+        if not isinstance(wi, _WorkerInit) or self.sharding != "static":
+            if forced:
+                raise ValueError("bridge=True needs static sharding and a worker_init_fn from init_worker()")
+            return wi
+        servers = wi.kwargs.get("bootstrap_servers", "localhost:9092")  # kafka-python's default
+        if is_synthetic_url(servers) or (not forced and os.environ.get("TORCHKAFKA_BROKER")):
+            return wi
+        topics = list(wi.args)
+        if not topics or not all(isinstance(t, str) for t in topics):
+            if forced:
+                raise ValueError("bridge=True needs the topics named in init_worker()")
+            return wi
+        from ..broker.bridge import KafkaBridge
+        from ..ops.native import core
+        from ..parallel.sharding import shard_partitions
+
+        if not isinstance(servers, str):
+            servers = ",".join(servers)
+        group = wi.kwargs.get("group_id")
+        reset = wi.kwargs.get("auto_offset_reset", "latest")  # kafka-python's default
+        client = core().WireClient(servers, "torchkafka-bridge", int(wi.kwargs.get("request_timeout_ms", 30000)))
+        url = None
+        try:
+            for t in topics:
+                err, parts = client.metadata(t)
+                if err:
+                    raise KafkaError(f"UnknownTopicOrPartitionError: topic {t!r} on {servers}")
+                mine = shard_partitions(len(parts), self.rank, self.world_size)
+                br = KafkaBridge(servers, t, group_id=group, partitions=mine, url=url, auto_offset_reset=reset)
+                br._own = url is None  # the first bridge owns the shared replica broker
+                url = br.url
+                self._bridges.append(br)
+        except BaseException:
+            for br in self._bridges:
+                br.close(flush=False)
+            self._bridges.clear()
+            raise
+        log.info("DeviceLoader: %s mirrored into %s by %d KafkaBridge(s) (rank %d/%d).", servers, url,
+                  len(self._bridges), self.rank, self.world_size)
+        return _WorkerInit(wi.cls, wi.args, {**wi.kwargs, "bootstrap_servers": url})
+
     def _resolve_commit_target(self, group_id, servers):
         from ..models.kafka_dataset import _WorkerInit
 
@@ -1423,6 +1477,9 @@ class DeviceLoader:
         if self._run is not None:
             self._run.close()
             self._run = None
+        for br in reversed(getattr(self, "_bridges", [])):  # forwards the last commits, then drops replicas
+            br.close()
+        self._bridges = []
 
     def __del__(self):
         try:
