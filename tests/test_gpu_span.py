@@ -301,3 +301,27 @@ def test_var_span_matches_host_path(broker, src, dst, lens, nulls, long_every, o
         for u, v in zip(x, y):
             assert u.shape == v.shape and u.dtype == v.dtype
             assert torch.equal(_bits(u) if u.is_floating_point() else u, _bits(v) if v.is_floating_point() else v)
+
+
+def test_hbm_mirror_copies_across_pin_pieces(broker):
+    """A log longer than the driver's 64 MiB pin pieces: the mirror splits its copies at the piece
+    boundaries (a DMA source must lie in one registration); values intact across them."""
+    import os
+    import uuid
+
+    from torchkafka_amd import FixedWidth, Tuning
+    from torchkafka_amd.broker import SyntheticBroker
+
+    big = SyntheticBroker.create(f"shm://tkbig-{os.getpid()}-{uuid.uuid4().hex[:6]}", log_capacity=256 << 20)
+    try:
+        big.create_topic("t", 1)
+        big.fill("t", 90_000, "fixed_f32", size=256, records_per_batch=64)  # ~93 MB: two pin pieces
+        DS = _dataset(FixedWidth(torch.float32, (256,)))
+        b, dl = _run(big, "t", DS, "device", 256, "gm", num_workers=1, in_order=True, h2d="dma",
+                     tuning=Tuning(mirror_chunk_mib=8, mirror_chunks=4))
+        assert dl._mirror() and b.shape == (90_000, 256)
+        assert torch.equal(b[:, 0], torch.arange(90_000, dtype=torch.float32, device=b.device))
+        for o in (0, 65_000, 89_999):
+            assert torch.equal(b[o].cpu(), torch.tensor([synth_f32(0, o, j) for j in range(256)]))
+    finally:
+        big.destroy()

@@ -420,6 +420,8 @@ void MainDriver::pin_logs(const std::vector<uint32_t>& pidxs) {
   }
 }
 
+static_assert(MainDriver::kLogChunk == LogMirror::kRegAlign, "mirror copies split at the pin pieces");
+
 void MainDriver::ensure_log(uint32_t pidx, uint64_t end) {
   if (pidx >= reg_end_.size()) throw std::out_of_range("driver: partition index beyond the broker's table");
   if (end <= reg_end_[pidx]) return;

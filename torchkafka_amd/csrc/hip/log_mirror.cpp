@@ -83,10 +83,16 @@ LogMirror::Buf* LogMirror::ensure(Part& P, uint32_t pidx, int64_t c, uint64_t wa
     return &b;  // resident (a prefetch tops up only in sizeable pieces)
   }
   if (target > b.end) {
-    TKM_CHECK(hipMemcpyAsync(P.dev + j * stride_ + (b.end - lo_c), log + b.end, size_t(target - b.end),
-                             hipMemcpyHostToDevice, copy_));
+    // one copy per pinned registration: a DMA source must lie inside one registered range, and the
+    // driver pins the logs in kRegAlign pieces (so that consumed pieces can be unpinned)
+    for (uint64_t a = b.end; a < target;) {
+      const uint64_t e = std::min<uint64_t>(target, (a / kRegAlign + 1) * kRegAlign);
+      TKM_CHECK(hipMemcpyAsync(P.dev + j * stride_ + (a - lo_c), log + a, size_t(e - a), hipMemcpyHostToDevice,
+                               copy_));
+      ++copies_;
+      a = e;
+    }
     bytes_ += target - b.end;
-    ++copies_;
     b.end = target;
     b.copy_seq = ++copy_seq_;
   }

@@ -28,6 +28,9 @@ inline constexpr uint64_t tk_seg_max() { return tk::kSpanSegMax; }
 
 class LogMirror {
  public:
+  // The driver registers (pins) partition logs in pieces of this many bytes, at multiples of it
+  // (MainDriver::kLogChunk): one copy never spans two registrations.
+  static constexpr uint64_t kRegAlign = uint64_t(64) << 20;
   LogMirror(int device, uint64_t chunk_bytes, int chunks_per_partition);
   ~LogMirror();
   LogMirror(const LogMirror&) = delete;
