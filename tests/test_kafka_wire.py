@@ -501,8 +501,56 @@ def test_device_loader_bridges_a_cluster_named_like_the_reference(broker, server
     assert broker.committed_offsets("ref", "t") == {p: 60 for p in range(4)}
 
 
-def test_bridge_off_keeps_the_kafka_python_route(server):
-    with pytest.raises(Exception, match="NoBrokersAvailable"):
-        dl = DeviceLoader(Vec8.placeholder(), 16, device="cpu", num_workers=1, bridge=False,
-                          worker_init_fn=Vec8.init_worker("t", bootstrap_servers=server.address, group_id="g"))
-        list(dl)
+def test_bridge_off_gives_each_worker_its_own_consumer(broker, server):
+    """bridge=False: no loader-level replica; every worker builds its consumer as the reference does
+    (kafka-python when installed, else the native wire route with its own replica of the worker's
+    partitions), and the workers' consumers commit."""
+    broker.create_topic("t", 4)
+    broker.fill("t", 30, "fixed_f32", size=8, records_per_batch=10)
+    dl = DeviceLoader(Vec8.placeholder(), 10, device="cpu", num_workers=2, bridge=False,
+                      worker_init_fn=Vec8.init_worker("t", bootstrap_servers=server.address, group_id="pw",
+                                                      auto_offset_reset="earliest", consumer_timeout_ms=400))
+    assert dl._bridges == [] and dl._sink == "worker"
+    n = sum(x.shape[0] for x in auto_commit(dl))
+    dl.close()
+    assert n == 120
+    assert wait_for(lambda: broker.committed_offsets("pw", "t") == {p: 30 for p in range(4)}), \
+        broker.committed_offsets("pw", "t")
+
+
+class Doubled(KafkaDataset):
+    def _process(self, record):  # the reference's README example shape: bytes -> tensor
+        v = torch.frombuffer(bytearray(record.value), dtype=torch.float32)
+        return None if int(v[0]) % 5 == 4 else v[:2] * 2
+
+
+@pytest.mark.parametrize("workers", [0, 2])
+def test_reference_api_reads_a_cluster_without_kafka_python(broker, server, workers):
+    """The reference's own usage -- KafkaDataset + torch DataLoader + auto_commit, pointed at
+    'host:port' -- works without kafka-python: the native wire route mirrors each worker's share of
+    the partitions and the commits reach the cluster (None-skipped records committed too, B6)."""
+    from torch.utils.data import DataLoader
+
+    broker.create_topic("t", 4)
+    broker.fill("t", 40, "fixed_f32", size=8, records_per_batch=8)
+    kw = dict(bootstrap_servers=[server.address], group_id="refgrp", auto_offset_reset="earliest",
+              consumer_timeout_ms=500)
+    if workers == 0:
+        dl = DataLoader(Doubled("t", **kw), batch_size=4)
+    else:
+        dl = DataLoader(Doubled.placeholder(), batch_size=4, num_workers=workers,
+                        worker_init_fn=Doubled.init_worker("t", **kw))
+    rows = torch.cat(list(auto_commit(dl)))
+    assert rows.shape == (4 * 32, 2)
+    got = sorted((int(o) // 2, int(p) // 2) for o, p in rows.tolist())
+    assert got == sorted((o, p) for p in range(4) for o in range(40) if o % 5 != 4)
+    if workers == 0:
+        dl.dataset.close()  # the reference's close() does not commit (R4): what auto_commit committed stays
+    last = {p: max(o for o, q in got if q == p) for p in range(4)}
+
+    def covered():
+        c = broker.committed_offsets("refgrp", "t")
+        return all(c[p] is not None and c[p] >= last[p] + 1 for p in range(4))
+    # every delivered record is committed in the cluster (a trailing None-skipped record may wait for
+    # the next commit, B6)
+    assert wait_for(covered), (broker.committed_offsets("refgrp", "t"), last)

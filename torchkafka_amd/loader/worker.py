@@ -60,13 +60,16 @@ def worker_main(ring, ring_name: str, worker_id: int, num_workers: int, dataset,
             if worker_init_fn is not None:
                 worker_init_fn(worker_id)
         consumer = getattr(dataset, "_consumer", None)
+        state["consumer"] = consumer
         if consumer is None:
             raise RuntimeError(
                 "DeviceLoader worker has no consumer: build the dataset with placeholder() and pass "
                 "worker_init_fn=YourDataset.init_worker(topic, ...)")
         if not in_process:
             dataset._worker_id = worker_id
-        if cfg["sharding"] == "static":
+        if cfg["sharding"] == "static" and getattr(consumer, "_bridged_shard", False):
+            pass  # a native wire-route consumer: its bridge already mirrors exactly this worker's shard
+        elif cfg["sharding"] == "static":
             topics = sorted(consumer.subscription() or [])
             if not topics:
                 raise RuntimeError("static sharding needs the consumer to be created with its topics")
@@ -103,6 +106,14 @@ def worker_main(ring, ring_name: str, worker_id: int, num_workers: int, dataset,
             ring.worker_publish(g)
         except Exception:  # noqa: BLE001
             pass
+    finally:
+        # a native wire-route consumer: forward what it committed before this process ends (its
+        # bridge's committer thread runs every few ms; the last commit must not be lost)
+        for br in reversed(getattr(state.get("consumer"), "_bridges", None) or []):
+            try:
+                br.close()
+            except Exception:  # noqa: BLE001 - logged by the bridge
+                pass
 
 
 class _WorkerSink:

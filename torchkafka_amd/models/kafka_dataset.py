@@ -30,7 +30,8 @@ from collections import deque
 
 from torch.utils.data import IterableDataset, get_worker_info
 
-from ..client.errors import COMMIT_FAILED_ERRORS
+from ..client.consumer import KafkaConsumer
+from ..client.errors import COMMIT_FAILED_ERRORS, KafkaError, NoBrokersAvailable
 from ..client.records import OffsetAndMetadata, TopicPartition
 
 _logger = logging.getLogger("torchkafka.kafka_dataset")
@@ -337,17 +338,90 @@ class KafkaDataset(IterableDataset):
 
 
 def _make_consumer(*topics, **kwargs):
-    """Synthetic-broker consumer, or kafka-python's when installed and pointed at a real cluster."""
+    """Synthetic-broker consumer; for a real cluster kafka-python's when installed, else the native
+    wire route (:func:`_bridged_consumer`)."""
     from ..broker.synthetic import is_synthetic_url
 
-    servers = kwargs.get("bootstrap_servers")
+    servers = kwargs.get("bootstrap_servers", "localhost:9092")
     if not is_synthetic_url(servers) and not os.environ.get("TORCHKAFKA_BROKER"):
         try:  # pragma: no cover - kafka-python is not installed in this image
             from kafka import KafkaConsumer as _KP  # type: ignore
 
             return _KP(*topics, **kwargs)
         except ImportError:
-            pass
-    from ..client.consumer import KafkaConsumer
-
+            return _bridged_consumer(topics, kwargs)
     return KafkaConsumer(*topics, **kwargs)
+
+
+def _bridged_consumer(topics, kwargs):
+    """A consumer of a real cluster without kafka-python: a native KafkaBridge per topic mirrors
+    this process's share of the partitions into a local replica, and the built-in consumer reads
+    it; its commits reach the cluster's group coordinator (forwarded within 5 ms, flushed by
+    ``close()``).  The share is static -- partition p goes to rank ``p % world`` and, there, to
+    DataLoader worker ``(p // world) % num_workers`` -- where kafka-python's group membership would
+    rebalance them among the group's consumers (reference kafka_dataset.py:206)."""
+    from ..broker.bridge import KafkaBridge
+    from ..ops.native import core
+    from ..parallel.sharding import dist_rank_world, shard_partitions
+
+    if not topics or not all(isinstance(t, str) for t in topics):
+        raise NoBrokersAvailable("NoBrokersAvailable: kafka-python is not installed; the native Kafka "
+                                 "client needs the topics named up front")
+    servers = kwargs.get("bootstrap_servers", "localhost:9092")
+    if not isinstance(servers, str):
+        servers = ",".join(servers)
+    rank, world = dist_rank_world()
+    wi = get_worker_info()
+    wid, nw = (wi.id, wi.num_workers) if wi is not None else (0, 1)
+    timeout = int(kwargs.get("request_timeout_ms", 30000))
+    client = core().WireClient(servers, str(kwargs.get("client_id", "torchkafka")), timeout)
+    bridges, tps, url = [], [], None
+    try:
+        for t in topics:
+            err, parts = client.metadata(t)
+            if err:
+                raise KafkaError(f"UnknownTopicOrPartitionError: topic {t!r} on {servers}")
+            mine = shard_partitions(len(parts), rank, world, wid, nw)
+            br = KafkaBridge(servers, t, group_id=kwargs.get("group_id"), partitions=mine, url=url,
+                             auto_offset_reset=kwargs.get("auto_offset_reset", "latest"), request_timeout_ms=timeout)
+            br._own = url is None
+            url = br.url
+            bridges.append(br)
+            tps += [TopicPartition(t, p) for p in mine]
+        cons = _BridgedConsumer(**{**kwargs, "bootstrap_servers": url})
+        cons._bridges = bridges
+        cons.assign(tps)
+        # a DataLoader worker ends through multiprocessing's exit hooks, not close(): forward the
+        # last commits there, after the dataset's own final commit service (exitpriority 100)
+        import multiprocessing.util as mpu
+
+        mpu.Finalize(cons, _flush_bridges, args=(bridges,), exitpriority=10)
+        return cons
+    except BaseException:
+        for br in bridges:
+            br.close(flush=False)
+        raise
+
+
+def _flush_bridges(bridges) -> None:
+    for br in reversed(bridges):
+        try:
+            br.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown; the bridge logs its errors
+            pass
+
+
+class _BridgedConsumer(KafkaConsumer):
+    """The built-in consumer over a KafkaBridge replica; closing it flushes the bridge's commits."""
+
+    _bridges: list = []
+    _bridged_shard = True  # assigned this process's static share of the partitions already
+
+    def close(self, autocommit: bool = True) -> None:
+        try:
+            super().close(autocommit)
+        finally:
+            if os.getpid() == self._pid:
+                for br in reversed(self._bridges):
+                    br.close()
+            self._bridges = []
