@@ -81,3 +81,48 @@ def test_lockstep_stops_all_ranks_together(broker, tmp_path, world):
     committed = broker.committed_offsets("g", "t")
     for r in range(world):
         assert committed[r] + committed[r + world] == 80  # exactly the 8 batches every rank finished
+
+
+def _bridge_rank_main(rank, world, servers, port, outdir):
+    import torch.distributed as dist
+
+    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class Vec(KafkaDataset):
+        schema = FixedWidth(torch.float32, (8,))
+
+    # the reference's worker_init_fn, pointed at a Kafka cluster: each rank mirrors its partitions
+    dl = DeviceLoader(Vec.placeholder(), 10, num_workers=2, device="cpu",
+                      worker_init_fn=Vec.init_worker("t", bootstrap_servers=servers, group_id="gb",
+                                                     auto_offset_reset="earliest", consumer_timeout_ms=400))
+    mirrored = sorted(s["partition"] for br in dl._bridges for s in br.stats())
+    steps, parts = 0, set()
+    for x in auto_commit(dl):
+        steps += 1
+        parts |= set(x[:, 1].long().tolist())
+    dl.close()
+    with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
+        json.dump({"steps": steps, "parts": sorted(parts), "mirrored": mirrored}, f)
+    dist.destroy_process_group()
+
+
+def test_ranks_mirror_their_partitions_of_a_cluster(broker, tmp_path):
+    """World 2 over gloo against a Kafka-protocol cluster: every rank's loader bridges only its own
+    partitions, the ranks stop together (lockstep), and the cluster holds every rank's commits."""
+    from torchkafka_amd.broker import KafkaWireServer
+
+    world = 2
+    broker.create_topic("t", 4)
+    broker.fill("t", 50, "fixed_f32", size=8, records_per_batch=10)
+    with KafkaWireServer(broker) as srv:
+        tmp.spawn(_bridge_rank_main, args=(world, srv.address, _free_port(), str(tmp_path)), nprocs=world,
+                  join=True)
+    res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
+    for r in range(world):
+        assert res[r]["mirrored"] == [r, r + world] and res[r]["parts"] == [r, r + world]
+        assert res[r]["steps"] == 10
+    assert broker.committed_offsets("gb", "t") == {p: 50 for p in range(4)}
