@@ -554,3 +554,28 @@ def test_reference_api_reads_a_cluster_without_kafka_python(broker, server, work
     # every delivered record is committed in the cluster (a trailing None-skipped record may wait for
     # the next commit, B6)
     assert wait_for(covered), (broker.committed_offsets("refgrp", "t"), last)
+
+
+def test_replicator_reconnects_after_the_broker_restarts(broker):
+    """The cluster goes away mid-stream and comes back on the same address: the fetch threads
+    back off, reconnect, refresh metadata and carry on from where the replica ends."""
+    broker.create_topic("t", 2)
+    broker.fill("t", 100, "fixed_f32", size=8, records_per_batch=10)
+    srv = KafkaWireServer(broker).start()
+    port = srv.port
+    br = bridge(srv, group_id="g")
+    try:
+        assert br.wait_caught_up(10)
+        srv.close()
+        broker.fill("t", 100, "fixed_f32", size=8, records_per_batch=10)  # produced while it is down
+        time.sleep(0.3)
+        assert br.errors > 0 and br.running
+        srv = KafkaWireServer(broker, port=port).start()
+        assert wait_for(lambda: all(s["fetch_offset"] == 200 for s in br.stats()))
+        for p in range(2):
+            assert log_bytes(br.local, "t", p) == log_bytes(broker, "t", p)
+        br.local.commit("g", {TopicPartition("t", 0): 150})
+        assert wait_for(lambda: broker.committed("g", "t", 0) == 150)
+    finally:
+        br.close()
+        srv.close()

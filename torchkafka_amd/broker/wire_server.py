@@ -153,11 +153,14 @@ class KafkaWireServer:
         self.partial_tail = False          # cut every record set inside its last batch
         self.requests: dict[int, int] = {}  # api key -> count
         self._views: dict[int, memoryview] = {}
+        self._conns: set = set()
         srv = self
 
         class Handler(socketserver.BaseRequestHandler):
             def handle(self):
                 self.request.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                with srv._lock:
+                    srv._conns.add(self.request)
                 try:
                     while True:
                         head = _recv_exact(self.request, 4)
@@ -174,6 +177,9 @@ class KafkaWireServer:
                         _sendall_vec(self.request, [struct.pack(">i", n)] + parts)
                 except (ConnectionError, OSError):
                     return
+                finally:
+                    with srv._lock:
+                        srv._conns.discard(self.request)
 
         class Server(socketserver.ThreadingTCPServer):
             daemon_threads = True
@@ -195,8 +201,17 @@ class KafkaWireServer:
         return self
 
     def close(self) -> None:
+        """Stops listening and drops every client connection (a broker going down)."""
         self._srv.shutdown()
         self._srv.server_close()
+        with self._lock:
+            conns = list(self._conns)
+        for c in conns:
+            try:
+                c.shutdown(socket.SHUT_RDWR)
+                c.close()
+            except OSError:
+                pass
 
     def __enter__(self):
         return self.start()
