@@ -579,3 +579,16 @@ def test_replicator_reconnects_after_the_broker_restarts(broker):
     finally:
         br.close()
         srv.close()
+
+
+def test_stopping_a_bridge_does_not_wait_out_a_hung_broker(broker, server):
+    broker.create_topic("t", 1)
+    broker.fill("t", 10, "fixed_f32", size=8)
+    br = bridge(server, request_timeout_ms=30000)
+    assert br.wait_caught_up(10)
+    server.stall_s = 20.0  # every fetch now hangs in the broker
+    time.sleep(0.3)
+    t0 = time.monotonic()
+    br.close(flush=False)
+    assert time.monotonic() - t0 < 3.0
+    server.stall_s = 0.0

@@ -151,6 +151,7 @@ class KafkaWireServer:
         self._fetch_faults: dict[tuple[str, int], list[int]] = {}
         self._commit_faults: list[int] = []
         self.partial_tail = False          # cut every record set inside its last batch
+        self.stall_s = 0.0                 # fault injection: hold every Fetch this long (a hung broker)
         self.requests: dict[int, int] = {}  # api key -> count
         self._views: dict[int, memoryview] = {}
         self._conns: set = set()
@@ -339,6 +340,8 @@ class KafkaWireServer:
                     w.i64(off)
 
     def _api_1(self, r: _R, ver: int, w: _W) -> None:  # Fetch v4
+        if self.stall_s:
+            time.sleep(self.stall_s)
         r.i32()  # replica
         max_wait, min_bytes, max_bytes = r.i32(), r.i32(), r.i32()
         r.i8()  # isolation level

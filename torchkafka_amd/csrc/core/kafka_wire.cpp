@@ -172,6 +172,13 @@ void Conn::send(int16_t api_key, int16_t api_version, const std::string& client_
   send_all(f);
 }
 
+void Conn::check_cancel() {
+  if (cancel_ && cancel_->load(std::memory_order_relaxed)) {
+    close();
+    throw KafkaError("KafkaError: request cancelled (client stopping)");
+  }
+}
+
 void Conn::fill(size_t want) {
   // compact, then read until `want` bytes are buffered (never past the current response)
   if (b0_ == b1_) b0_ = b1_ = 0;
@@ -187,8 +194,9 @@ void Conn::fill(size_t want) {
       close();
       throw KafkaError("KafkaTimeoutError: no response from " + host_ + ":" + std::to_string(port_));
     }
+    check_cancel();
     pollfd p{fd_, POLLIN, 0};
-    const int r = ::poll(&p, 1, int(std::min<int64_t>(left, 1000)));
+    const int r = ::poll(&p, 1, int(std::min<int64_t>(left, 100)));
     if (r < 0 && errno != EINTR) {
       close();
       throw KafkaError("KafkaConnectionError: poll failed");
@@ -236,8 +244,9 @@ void Conn::read(void* dst, size_t n) {
       close();
       throw KafkaError("KafkaTimeoutError: response from " + host_ + " stalled");
     }
+    check_cancel();
     pollfd p{fd_, POLLIN, 0};
-    const int r = ::poll(&p, 1, int(std::min<int64_t>(left, 1000)));
+    const int r = ::poll(&p, 1, int(std::min<int64_t>(left, 100)));
     if (r <= 0) continue;
     const ssize_t got = ::recv(fd_, d + off, n - off, 0);
     if (got == 0 || (got < 0 && errno != EINTR && errno != EAGAIN)) {
@@ -321,6 +330,7 @@ Conn& Client::bootstrap_conn() {
   for (auto& [h, p] : bootstrap_) {
     try {
       conns_[-1] = std::make_unique<Conn>(h, p, timeout_ms_);
+      conns_[-1]->set_cancel(cancel_);
       return *conns_[-1];
     } catch (const KafkaError& e) {
       why = e.what();
@@ -336,6 +346,7 @@ Conn& Client::conn(int32_t node_id) {
   auto nd = nodes_.find(node_id);
   if (nd == nodes_.end()) throw WireError(kLeaderNotAvailable, "wire: unknown broker node " + std::to_string(node_id));
   conns_[node_id] = std::make_unique<Conn>(nd->second.host, nd->second.port, timeout_ms_);
+  conns_[node_id]->set_cancel(cancel_);
   return *conns_[node_id];
 }
 

@@ -16,6 +16,7 @@
 // (rank, worker) as in the rest of the framework, and offsets are committed like kafka-python's
 // manually-assigned consumer with a group_id (generation -1, empty member id).
 #pragma once
+#include <atomic>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -115,6 +116,9 @@ class Conn {
   void finish();  // drains the rest of the current response
   size_t remaining() const { return remaining_; }
   void close();
+  // Waits for the socket end early (KafkaError "cancelled") once *flag is true: a stopping
+  // replicator does not sit out a request timeout on an unresponsive broker.
+  void set_cancel(const std::atomic<bool>* flag) { cancel_ = flag; }
 
  private:
   void send_all(const std::string& frame);
@@ -129,6 +133,8 @@ class Conn {
   size_t remaining_ = 0;
   std::vector<uint8_t> buf_;
   size_t b0_ = 0, b1_ = 0;
+  const std::atomic<bool>* cancel_ = nullptr;
+  void check_cancel();
 };
 
 // ------------------------------------------------------------ cluster view
@@ -172,6 +178,7 @@ class Client {
                                            const std::map<int32_t, int64_t>& offsets,
                                            const std::string& metadata = "");
   void invalidate_coordinator() { coordinator_ = -1; }
+  void set_cancel(const std::atomic<bool>* flag) { cancel_ = flag; }  // every connection of this client
 
   // Connection to a node (-1: any bootstrap server).  Owned by the client; one per node.
   Conn& conn(int32_t node_id);
@@ -191,6 +198,7 @@ class Client {
   std::map<std::string, TopicMeta> topics_;
   int32_t coordinator_ = -1;
   std::string coordinator_group_;
+  const std::atomic<bool>* cancel_ = nullptr;
 };
 
 // Encodes a Fetch v4 request body (tests and the replicator share it).

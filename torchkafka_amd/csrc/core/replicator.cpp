@@ -132,6 +132,7 @@ void Replicator::stop(bool flush) {
   threads_.clear();
   running_ = false;
   if (flush && !cfg_.group.empty()) {
+    commit_client_.reset();  // its connections may carry the stop flag: flush on fresh ones
     for (int attempt = 0; attempt < 3; ++attempt) {
       try {
         if (!commit_client_)
@@ -173,6 +174,7 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
     try {
       if (!c) {
         c = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id, cfg_.timeout_ms);
+        c->set_cancel(&stop_);
         c->metadata(cfg_.topic);
       }
       std::map<int32_t, std::vector<Part*>> by;
@@ -321,8 +323,10 @@ void Replicator::commit_loop() {
     for (int s = 0; s < backoff_ms && !stop_.load(); s += 1) sleep_ms(1);
     if (stop_.load()) break;
     try {
-      if (!commit_client_)
+      if (!commit_client_) {
         commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", cfg_.timeout_ms);
+        commit_client_->set_cancel(&stop_);
+      }
       forward(*commit_client_);
       backoff_ms = cfg_.commit_interval_ms;
     } catch (const std::exception& e) {
