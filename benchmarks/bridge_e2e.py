@@ -3,7 +3,8 @@
 
 Not a BASELINE config: it measures the production route of `KafkaBridge` on the config-2 record
 shape (f32[256], 1 KiB records, batch 256, commit after every batch).  The cluster is
-`KafkaWireServer` over a synthetic broker, one server process per node (partition p led by node
+`NativeWireServer` (C++, record sets sent from the mapped logs; `--python-server`: the Python
+`KafkaWireServer`) over a synthetic broker, one server process per node (partition p led by node
 p % nodes) on the loopback interface, so the numbers include the Kafka protocol, TCP, the
 replicator's fetch threads (one per leader) and its commit forwarding; they do not include a real
 broker's disk or a NIC.
@@ -44,10 +45,11 @@ def _free_ports(n):
     return ports
 
 
-def _serve(url, node_id, cluster, ready):
-    from torchkafka_amd.broker import KafkaWireServer, open_broker
+def _serve(url, node_id, cluster, ready, python_server):
+    from torchkafka_amd.broker import KafkaWireServer, NativeWireServer, open_broker
 
-    srv = KafkaWireServer(open_broker(url), port=cluster[node_id][2], node_id=node_id, cluster=cluster).start()
+    cls = KafkaWireServer if python_server else NativeWireServer
+    srv = cls(open_broker(url), port=cluster[node_id][2], node_id=node_id, cluster=cluster).start()
     ready.set()
     while True:
         time.sleep(3600)
@@ -76,6 +78,8 @@ def main() -> int:
     ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy"])
     ap.add_argument("--direct", action="store_true",
                     help="control run: phase 2 consumes the cluster's own broker directly (no wire, no replica)")
+    ap.add_argument("--python-server", action="store_true",
+                    help="serve the cluster with the Python KafkaWireServer instead of the native one")
     ap.add_argument("--no-cluster", action="store_true", help="control: no servers, no bridge (implies --direct)")
     ap.add_argument("--backlog", action="store_true",
                     help="phase 2 waits until the replica holds the whole backlog before consuming it (the "
@@ -103,12 +107,12 @@ def main() -> int:
     procs = []
     for i in range(args.nodes):
         ev = ctx.Event()
-        pr = ctx.Process(target=_serve, args=(url, i, cluster, ev), daemon=True)
+        pr = ctx.Process(target=_serve, args=(url, i, cluster, ev, args.python_server), daemon=True)
         pr.start()
         ev.wait(30)
         procs.append(pr)
     boot = f"127.0.0.1:{ports[0]}" if ports else None
-    out = {"nodes": args.nodes, "partitions": args.partitions, "records_per_partition": args.records,
+    out = {"server": "python" if args.python_server else "native", "nodes": args.nodes, "partitions": args.partitions, "records_per_partition": args.records,
            "cluster_gb": round(total_bytes / 1e9, 3), "fill_s": round(fill_s, 2)}
     try:
         # (1) replication alone

@@ -592,3 +592,58 @@ def test_stopping_a_bridge_does_not_wait_out_a_hung_broker(broker, server):
     br.close(flush=False)
     assert time.monotonic() - t0 < 3.0
     server.stall_s = 0.0
+
+
+# ---------------------------------------------------------------- the native (C++) wire server
+
+def test_native_server_protocol_and_byte_identical_replica(broker):
+    from torchkafka_amd.broker import NativeWireServer
+
+    broker.create_topic("t", 3)
+    broker.fill("t", 500, "fixed_f32", size=32, records_per_batch=50)
+    with NativeWireServer(broker) as srv:
+        c = core().WireClient(srv.address)
+        assert c.metadata("t")[0] == 0 and c.metadata("nope")[0] == 3
+        assert c.list_offsets("t", [0, 1, 2], -1) == {0: 500, 1: 500, 2: 500}
+        assert c.offset_commit("g", "t", {1: 42}) == {1: 0}
+        assert c.offset_fetch("g", "t", [0, 1]) == {0: -1, 1: 42}
+        with bridge(srv, group_id="g", max_partition_fetch_bytes=8192, fetch_max_bytes=16384) as br:
+            assert br.wait_caught_up(10)
+            for p in range(3):
+                assert log_bytes(br.local, "t", p) == log_bytes(broker, "t", p)
+            assert {s["start_offset"] for s in br.stats()} == {0, 42}
+            broker.fill("t", 100, "fixed_f32", size=32, records_per_batch=50)  # long-poll wakes up
+            assert br.wait_caught_up(10)
+            assert br.errors == 0
+        assert srv.requests > 10 and srv.bytes_sent > 3 * 500 * 128
+
+
+def test_native_server_cluster_and_device_loader(broker):
+    import socket as _s
+
+    from torchkafka_amd.broker import NativeWireServer
+
+    broker.create_topic("t", 4)
+    broker.fill("t", 90, "fixed_f32", size=8, records_per_batch=15)
+    socks = [_s.socket() for _ in range(2)]
+    for s in socks:
+        s.bind(("127.0.0.1", 0))
+    ports = [s.getsockname()[1] for s in socks]
+    for s in socks:
+        s.close()
+    cluster = [(i, "127.0.0.1", ports[i]) for i in range(2)]
+    nodes = [NativeWireServer(broker, port=ports[i], node_id=i, cluster=cluster).start() for i in range(2)]
+    try:
+        dl = DeviceLoader(Vec8.placeholder(), 12, device="cpu", num_workers=2,
+                          worker_init_fn=Vec8.init_worker("t", bootstrap_servers=nodes[1].address, group_id="nat",
+                                                          auto_offset_reset="earliest", consumer_timeout_ms=400))
+        seen = set()
+        for x in auto_commit(dl):
+            seen |= {(int(p), int(o)) for o, p in x[:, :2].tolist()}
+        dl.close()
+        assert seen == {(p, o) for p in range(4) for o in range(90)}
+        assert broker.committed_offsets("nat", "t") == {p: 90 for p in range(4)}
+        assert all(n.requests > 0 for n in nodes)
+    finally:
+        for n in nodes:
+            n.close()

@@ -508,3 +508,44 @@ def _recv_exact(sock, n: int) -> bytes | None:
             return None
         buf += chunk
     return bytes(buf)
+
+
+class NativeWireServer:
+    """The same protocol served by C++ threads (``csrc/core/wire_server.cpp``): record sets go out
+    of the mapped logs by ``sendmsg`` without a copy, so a cluster of these feeds a replicator at
+    memory / NIC speed (the Python server above is bound by its interpreter).  No fault injection.
+    ``cluster``: every node as (node_id, host, port); partition p is led by node p % len(cluster)."""
+
+    def __init__(self, broker: SyntheticBroker, host: str = "127.0.0.1", port: int = 0, node_id: int = 0,
+                 cluster: list[tuple[int, str, int]] | None = None):
+        from ..ops.native import core
+
+        self.broker = broker
+        self.host = host
+        self._s = core().WireServer(broker.native, host, int(port), int(node_id), list(cluster or []))
+        self.port = self._s.port
+
+    @property
+    def address(self) -> str:
+        return f"{self.host}:{self.port}"
+
+    @property
+    def requests(self) -> int:
+        return int(self._s.requests)
+
+    @property
+    def bytes_sent(self) -> int:
+        return int(self._s.bytes_sent)
+
+    def start(self) -> "NativeWireServer":
+        self._s.start()
+        return self
+
+    def close(self) -> None:
+        self._s.stop()
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.close()

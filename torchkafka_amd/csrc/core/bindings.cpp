@@ -14,6 +14,7 @@
 #include "record_batch.h"
 #include "replicator.h"
 #include "ring.h"
+#include "wire_server.h"
 
 namespace py = pybind11;
 using namespace tk;
@@ -490,6 +491,21 @@ PYBIND11_MODULE(_tkcore, m) {
       .def("offset_commit", &wire::Client::offset_commit, py::arg("group"), py::arg("topic"), py::arg("offsets"),
            py::arg("metadata") = "", py::call_guard<py::gil_scoped_release>())
       .def_static("parse_bootstrap", &wire::Client::parse_bootstrap);
+
+  py::class_<WireServer>(m, "WireServer")
+      .def(py::init([](std::shared_ptr<Broker> b, const std::string& host, int port, int32_t node_id,
+                       std::vector<std::tuple<int32_t, std::string, int32_t>> cluster) {
+             std::vector<WireNode> nodes;
+             for (auto& [id, h, p] : cluster) nodes.push_back(WireNode{id, h, p});
+             return std::make_unique<WireServer>(std::move(b), host, port, node_id, std::move(nodes));
+           }),
+           py::arg("broker"), py::arg("host") = "127.0.0.1", py::arg("port") = 0, py::arg("node_id") = 0,
+           py::arg("cluster") = std::vector<std::tuple<int32_t, std::string, int32_t>>())
+      .def("start", &WireServer::start)
+      .def("stop", &WireServer::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("port", &WireServer::port)
+      .def_property_readonly("requests", &WireServer::requests)
+      .def_property_readonly("bytes_sent", &WireServer::bytes_sent);
 
   py::class_<Replicator>(m, "Replicator")
       .def(py::init([](std::shared_ptr<Broker> local, const std::string& bootstrap, const std::string& topic,
