@@ -13,6 +13,8 @@ import uuid
 import pytest
 import torch
 
+from conftest import synth_f32
+
 pytestmark = pytest.mark.gpu
 
 
@@ -79,7 +81,7 @@ def test_long_stream_unpins_and_releases_consumed_log(broker):
         with KafkaWireServer(src) as srv:
             br = KafkaBridge(srv.address, "t", group_id="g", url=f"shm://tkgbr-{os.getpid()}-{uuid.uuid4().hex[:6]}",
                              log_capacity=512 << 20, max_lag_bytes=96 << 20, release_bytes=16 << 20,
-                             release_step=64 << 20)
+                             release_step=64 << 20, ring_bytes=0)  # a linear replica with release
             try:
                 dl = DeviceLoader(Rows.placeholder(), 256, num_workers=1, device="cuda:0", dtype=torch.float32,
                                   worker_init_fn=Rows.init_worker("t", bootstrap_servers=br.url, group_id="g",
@@ -97,6 +99,48 @@ def test_long_stream_unpins_and_releases_consumed_log(broker):
                 assert dl.stats.log_bytes_unpinned >= 64 << 20
                 released = br.stats()[0]["released"]
                 assert released >= 64 << 20, br.stats()
+            finally:
+                br.close()
+        assert src.committed("g", "t", 0) == 160_000
+    finally:
+        src.destroy()
+
+
+def test_ring_replica_long_stream_device_decode(broker):
+    """The default replica: a 32 MiB ring per partition carries a ~165 MB stream.  Segments are read
+    zero-copy from the pinned ring while the replicator writes over committed batches; values and
+    order exact, every offset committed to the cluster."""
+    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
+    from torchkafka_amd.broker import KafkaBridge, NativeWireServer, SyntheticBroker
+
+    class Rows(KafkaDataset):
+        schema = FixedWidth(torch.float32, (256,))
+
+    src = SyntheticBroker.create(f"shm://tkgsrc-{os.getpid()}-{uuid.uuid4().hex[:6]}", log_capacity=512 << 20)
+    try:
+        src.create_topic("t", 1)
+        src.fill("t", 160_000, "fixed_f32", size=256, records_per_batch=64)
+        with NativeWireServer(src) as srv:
+            br = KafkaBridge(srv.address, "t", group_id="g", url=f"shm://tkgbr-{os.getpid()}-{uuid.uuid4().hex[:6]}",
+                             ring_bytes=32 << 20, log_capacity=64 << 20, max_partition_fetch_bytes=4 << 20)
+            try:
+                dl = DeviceLoader(Rows.placeholder(), 256, num_workers=1, device="cuda:0", dtype=torch.float32,
+                                  worker_init_fn=Rows.init_worker("t", bootstrap_servers=br.url, group_id="g",
+                                                                  auto_offset_reset="earliest",
+                                                                  consumer_timeout_ms=1500))
+                assert dl._span()
+                n, last = 0, -1
+                for x in auto_commit(dl):
+                    assert int(x[0, 0].item()) == last + 1
+                    if n % 64000 == 0:
+                        o = int(x[7, 0].item())
+                        assert torch.equal(x[7].cpu(), torch.tensor([synth_f32(0, o, j) for j in range(256)]))
+                    last = int(x[-1, 0].item())
+                    n += x.shape[0]
+                torch.cuda.synchronize()
+                dl.close()
+                assert n == 160_000 and last == 159_999
+                assert br.local.native.first_batch(br.local.pidx("t", 0)) > 0
             finally:
                 br.close()
         assert src.committed("g", "t", 0) == 160_000

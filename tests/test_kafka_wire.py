@@ -170,7 +170,7 @@ def test_flow_control_bounds_uncommitted_bytes(broker, server):
     broker.create_topic("t", 1)
     broker.fill("t", 2000, "fixed_f32", size=64, records_per_batch=20)  # ~550 KB
     with bridge(server, group_id="g", max_lag_bytes=64 << 10, max_partition_fetch_bytes=16 << 10,
-                fetch_max_bytes=16 << 10) as br:
+                fetch_max_bytes=16 << 10, ring_bytes=0) as br:  # a linear log: max_lag_bytes bounds it
         assert wait_for(lambda: br.stats()[0]["throttled"] > 0)
         held = br.local.native.log_bytes(br.local.pidx("t", 0))
         assert held < (64 << 10) + (16 << 10) + 8192
@@ -227,7 +227,8 @@ def test_committed_log_bytes_are_released(broker, server):
     out of the shm file (st_blocks drops), consumers carry on from the committed offset."""
     broker.create_topic("t", 1)
     broker.fill("t", 10000, "fixed_f32", size=256, records_per_batch=64)  # ~10.3 MB
-    with bridge(server, group_id="g", release_bytes=2 << 20, release_step=2 << 20, log_capacity=64 << 20) as br:
+    with bridge(server, group_id="g", release_bytes=2 << 20, release_step=2 << 20, log_capacity=64 << 20,
+                ring_bytes=0) as br:
         assert br.wait_caught_up(10)
         pidx = br.local.pidx("t", 0)
         path = os.path.join(br.local.dir, f"p{pidx:05d}.log")
@@ -647,3 +648,52 @@ def test_native_server_cluster_and_device_loader(broker):
     finally:
         for n in nodes:
             n.close()
+
+
+
+# ---------------------------------------------------------------- ring replicas
+
+def test_ring_replica_streams_more_than_its_size(broker, server):
+    """A 1 MiB ring carries a ~4 MB stream: the replicator writes over committed batches, wraps, and
+    waits while the consumer holds the ring (flow control); every record arrives once, in order."""
+    broker.create_topic("t", 1)
+    broker.fill("t", 4000, "fixed_f32", size=256, records_per_batch=16)  # ~4.2 MB, 16.6 KB batches
+    with bridge(server, group_id="g", ring_bytes=1 << 20, max_partition_fetch_bytes=128 << 10,
+                fetch_max_bytes=128 << 10, fetch_max_wait_ms=5) as br:
+        pidx = br.local.pidx("t", 0)
+        assert br.local.native.ring_bytes(pidx) == 1 << 20
+        assert wait_for(lambda: br.stats()[0]["throttled"] > 0)  # nothing committed yet: the ring fills
+        assert br.stats()[0]["fetch_offset"] < 4000
+        c = KafkaConsumer("t", bootstrap_servers=br.url, group_id="g", auto_offset_reset="earliest",
+                          enable_auto_commit=False, consumer_timeout_ms=1000)
+        got = []
+        for r in c:
+            v = torch.frombuffer(bytearray(r.value), dtype=torch.float32)
+            assert int(v[0]) == r.offset and v[2:6].tolist() == [synth_f32(0, r.offset, j) for j in range(2, 6)]
+            got.append(r.offset)
+            if r.offset % 100 == 99:
+                c.commit()  # frees ring space for the replicator
+        c.commit()
+        c.close()
+        assert got == list(range(4000))
+        assert br.local.native.first_batch(pidx) > 0  # batches were retired and written over
+        assert br.local.beginning_offset("t", 0) > 0
+        br.flush()
+    assert broker.committed("g", "t", 0) == 4000
+
+
+def test_ring_replica_feeds_a_device_loader(broker, server):
+    broker.create_topic("t", 2)
+    broker.fill("t", 3000, "fixed_f32", size=64, records_per_batch=20)  # ~800 KB per partition
+    with bridge(server, group_id="gr", ring_bytes=256 << 10, max_partition_fetch_bytes=32 << 10,
+                fetch_max_bytes=64 << 10, fetch_max_wait_ms=5) as br:
+        dl = DeviceLoader(Vec64.placeholder(), 50, device="cpu", num_workers=2,
+                          worker_init_fn=Vec64.init_worker("t", bootstrap_servers=br.url, group_id="gr",
+                                                           auto_offset_reset="earliest", consumer_timeout_ms=1500))
+        seen = []
+        for x in auto_commit(dl):
+            seen += [(int(p), int(o)) for o, p in x[:, :2].tolist()]
+        dl.close()
+        assert sorted(seen) == [(p, o) for p in range(2) for o in range(3000)]
+        assert all(br.local.native.first_batch(br.local.pidx("t", p)) > 0 for p in range(2))
+    assert broker.committed_offsets("gr", "t") == {0: 3000, 1: 3000}

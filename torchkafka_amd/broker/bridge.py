@@ -19,7 +19,11 @@ the last one::
         ...
     bridge.close()          # forwards the final commit
 
-Memory: with a ``group_id`` the committed part of every replica log is released (the device
+Memory: by default each replica partition is a **ring** of ``ring_bytes`` (512 MiB): the
+replicator writes over batches the group has committed, so the pages are allocated, and pinned by
+a device loader, once -- a stream of any length needs no page freeing, unpinning or re-pinning,
+and a full ring is the flow control (consumers behind by ``ring_bytes`` hold the fetches).  With
+``ring_bytes=0`` the logs are linear and, with a ``group_id``, the committed part is released (the device
 loader unpins it, the log start moves up to the committed offset and a background thread punches
 the bytes below it out of the shm files in bursts of ``release_step``, keeping the last
 ``release_bytes`` of consumed log), so a long stream holds about ``max_lag_bytes + release_bytes +
@@ -59,7 +63,8 @@ class KafkaBridge:
                  fetch_max_bytes: int = 64 << 20, max_partition_fetch_bytes: int = 8 << 20,
                  request_timeout_ms: int = 30000, commit_interval_ms: int = 5, fetchers: int = 0,
                  client_id: str = "torchkafka-bridge", release_consumed: bool = True,
-                 release_bytes: int = 256 << 20, release_step: int = 1 << 30, start: bool = True):
+                 release_bytes: int = 256 << 20, release_step: int = 1 << 30, ring_bytes: int = 512 << 20,
+                 start: bool = True):
         if not isinstance(bootstrap_servers, str):
             bootstrap_servers = ",".join(bootstrap_servers)
         self.bootstrap_servers = bootstrap_servers
@@ -78,7 +83,7 @@ class KafkaBridge:
             max_lag_bytes=int(max_lag_bytes), commit_interval_ms=int(commit_interval_ms), fetchers=int(fetchers),
             log_capacity=int(log_capacity), index_capacity=int(index_capacity), client_id=client_id,
             release_consumed=bool(release_consumed), release_bytes=int(release_bytes),
-            release_step=int(release_step))
+            release_step=int(release_step), ring_bytes=int(ring_bytes))
         self._closed = False
         self._lock = threading.Lock()
         self._reported = 0

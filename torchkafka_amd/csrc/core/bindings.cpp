@@ -367,10 +367,11 @@ PYBIND11_MODULE(_tkcore, m) {
              const IndexEntry* idx = b.index_base(p);
              const uint64_t nb = P.n_batches.load(std::memory_order_acquire);
              int64_t i = b.find_batch(p, offset, -1);
-             const uint64_t pos0 = idx[i].pos;
-             uint64_t end = pos0 + idx[i].size;
-             for (uint64_t j = uint64_t(i) + 1; j < nb && idx[j].pos + idx[j].size - pos0 <= max_bytes; ++j)
-               end = idx[j].pos + idx[j].size;
+             const uint64_t icap = P.index_capacity;
+             const uint64_t pos0 = idx[uint64_t(i) % icap].pos;
+             uint64_t end = pos0 + idx[uint64_t(i) % icap].size;
+             for (uint64_t j = uint64_t(i) + 1; j < nb && idx[j % icap].pos + idx[j % icap].size - pos0 <= max_bytes; ++j)
+               end = idx[j % icap].pos + idx[j % icap].size;
              return py::make_tuple(py::bytes(reinterpret_cast<const char*>(b.log_base(p)) + pos0, end - pos0), hw, start);
            },
            py::arg("pidx"), py::arg("offset"), py::arg("max_bytes"))
@@ -385,10 +386,11 @@ PYBIND11_MODULE(_tkcore, m) {
              const IndexEntry* idx = b.index_base(p);
              const uint64_t nb = P.n_batches.load(std::memory_order_acquire);
              const int64_t i = b.find_batch(p, offset, -1);
-             const uint64_t pos0 = idx[i].pos;
-             uint64_t end = pos0 + idx[i].size;
-             for (uint64_t j = uint64_t(i) + 1; j < nb && idx[j].pos + idx[j].size - pos0 <= max_bytes; ++j)
-               end = idx[j].pos + idx[j].size;
+             const uint64_t icap = P.index_capacity;
+             const uint64_t pos0 = idx[uint64_t(i) % icap].pos;
+             uint64_t end = pos0 + idx[uint64_t(i) % icap].size;
+             for (uint64_t j = uint64_t(i) + 1; j < nb && idx[j % icap].pos + idx[j % icap].size - pos0 <= max_bytes; ++j)
+               end = idx[j % icap].pos + idx[j % icap].size;
              return py::make_tuple(pos0, end - pos0, hw, start);
            },
            py::arg("pidx"), py::arg("offset"), py::arg("max_bytes"))
@@ -420,6 +422,8 @@ PYBIND11_MODULE(_tkcore, m) {
            },
            py::arg("pidx"), py::arg("data"), py::arg("from_offset") = -1, py::arg("keep_control") = false)
       .def("position_of", &Broker::position_of)
+      .def("ring_bytes", [](Broker& b, uint32_t p) { return b.part(p).ring_bytes.load(); })
+      .def("first_batch", [](Broker& b, uint32_t p) { return b.part(p).first_batch.load(); })
       .def("group_index", &Broker::group_index, py::arg("group"), py::arg("create") = true)
       .def("group_name", &Broker::group_name)
       .def("join_group", &Broker::join_group)
@@ -513,7 +517,7 @@ PYBIND11_MODULE(_tkcore, m) {
                        int32_t max_wait_ms, int32_t max_bytes, int32_t partition_max_bytes, int32_t timeout_ms,
                        int64_t max_lag_bytes, int32_t commit_interval_ms, int32_t fetchers, uint64_t log_capacity,
                        uint64_t index_capacity, const std::string& client_id, bool release_consumed,
-                       uint64_t release_bytes, uint64_t release_step) {
+                       uint64_t release_bytes, uint64_t release_step, uint64_t ring_bytes) {
              ReplicaConfig c;
              c.bootstrap = bootstrap;
              c.topic = topic;
@@ -533,6 +537,7 @@ PYBIND11_MODULE(_tkcore, m) {
              c.release_consumed = release_consumed;
              c.release_bytes = release_bytes;
              c.release_step = release_step;
+             c.ring_bytes = ring_bytes;
              return std::make_unique<Replicator>(std::move(local), c);
            }),
            py::arg("local"), py::arg("bootstrap"), py::arg("topic"), py::arg("group") = "",
@@ -542,7 +547,7 @@ PYBIND11_MODULE(_tkcore, m) {
            py::arg("commit_interval_ms") = 5, py::arg("fetchers") = 0, py::arg("log_capacity") = 0,
            py::arg("index_capacity") = 0, py::arg("client_id") = "torchkafka-replicator",
            py::arg("release_consumed") = true, py::arg("release_bytes") = uint64_t(256) << 20,
-           py::arg("release_step") = uint64_t(1) << 30)
+           py::arg("release_step") = uint64_t(1) << 30, py::arg("ring_bytes") = uint64_t(0))
       .def("start", &Replicator::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Replicator::stop, py::arg("flush") = true, py::call_guard<py::gil_scoped_release>())
       .def("flush_commits", &Replicator::flush_commits, py::call_guard<py::gil_scoped_release>())

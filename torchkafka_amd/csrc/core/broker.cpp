@@ -235,6 +235,8 @@ TopicInfo Broker::create_topic(const std::string& name, uint32_t n_partitions, u
       P.partition = i;
       P.fetch_delay_ns.store(0);
       P.fetch_errors.store(0);
+      P.ring_bytes.store(0);
+      P.first_batch.store(0);
       // Create (sparse) backing files now so readers can map them.
       void* a = map_file(part_path(dir_, pidx, "log"), log_capacity, true);
       munmap(a, log_capacity);
@@ -310,16 +312,19 @@ const IndexEntry* Broker::index_base(uint32_t pidx) { return mapped(pidx).idx; }
 int64_t Broker::find_batch(uint32_t pidx, int64_t offset, int64_t hint) {
   const PartitionEntry& P = part(pidx);
   const IndexEntry* idx = mapped(pidx).idx;
+  const uint64_t icap = P.index_capacity;
   const int64_t nb = int64_t(P.n_batches.load(std::memory_order_acquire));
+  const int64_t first = int64_t(P.first_batch.load(std::memory_order_acquire));
+  auto at = [&](int64_t i) -> const IndexEntry& { return idx[uint64_t(i) % icap]; };
   auto contains = [&](int64_t i) {
-    return i >= 0 && i < nb && idx[i].base_offset <= offset && offset <= idx[i].base_offset + idx[i].last_offset_delta;
+    return i >= first && i < nb && at(i).base_offset <= offset && offset <= at(i).base_offset + at(i).last_offset_delta;
   };
   if (contains(hint)) return hint;
   if (contains(hint + 1)) return hint + 1;
-  int64_t lo = 0, hi = nb;  // first entry with base_offset > offset
+  int64_t lo = first, hi = nb;  // first entry with base_offset > offset
   while (lo < hi) {
-    int64_t mid = (lo + hi) / 2;
-    if (idx[mid].base_offset <= offset) lo = mid + 1; else hi = mid;
+    int64_t mid = lo + (hi - lo) / 2;
+    if (at(mid).base_offset <= offset) lo = mid + 1; else hi = mid;
   }
   int64_t i = lo - 1;
   if (contains(i)) return i;
@@ -334,8 +339,8 @@ std::pair<int64_t, int64_t> Broker::offset_for_time(uint32_t pidx, int64_t ts) {
   const Mapped& m = mapped(pidx);
   const int64_t nb = int64_t(P.n_batches.load(std::memory_order_acquire));
   const int64_t start = P.log_start_offset.load(std::memory_order_acquire);
-  for (int64_t i = 0; i < nb; ++i) {
-    const IndexEntry& e = m.idx[i];
+  for (int64_t i = int64_t(P.first_batch.load(std::memory_order_acquire)); i < nb; ++i) {
+    const IndexEntry& e = m.idx[uint64_t(i) % P.index_capacity];
     if (e.base_offset + e.last_offset_delta < start || e.max_timestamp < ts) continue;
     const uint8_t* bp = m.log + e.pos;
     BatchHeader h = parse_batch_header(bp, e.size);
@@ -365,7 +370,7 @@ int64_t Broker::append(uint32_t pidx, const RecordIn* recs, size_t n) {
   const size_t wrote = encode_batch(m.log + pos, base, recs, n);
   int64_t max_ts = recs[0].timestamp;
   for (size_t i = 1; i < n; ++i) max_ts = std::max(max_ts, recs[i].timestamp);
-  m.idx[nb] = IndexEntry{base, pos, uint32_t(wrote), int32_t(n - 1), max_ts};
+  m.idx[nb % P.index_capacity] = IndexEntry{base, pos, uint32_t(wrote), int32_t(n - 1), max_ts};
   P.log_end_pos.store(pos + wrote, std::memory_order_release);
   P.n_batches.store(nb + 1, std::memory_order_release);
   P.records_produced.fetch_add(n, std::memory_order_relaxed);
@@ -389,12 +394,14 @@ void Broker::reset_empty(uint32_t pidx, int64_t offset) {
   P.high_watermark.store(offset, std::memory_order_release);
 }
 
-Broker::Ingested Broker::ingest(uint32_t pidx, uint64_t len, int64_t from_offset, bool keep_control) {
+Broker::Ingested Broker::ingest(uint32_t pidx, uint64_t len, int64_t from_offset, bool keep_control,
+                                uint64_t limit) {
   PartitionEntry& P = part(pidx);
   Mapped& m = mapped(pidx);
   RobustLock l(&P.lock);
   const uint64_t pos0 = P.log_end_pos.load(std::memory_order_relaxed);
   if (pos0 + len > P.log_capacity) throw KafkaError("ingest beyond the partition log capacity");
+  const uint64_t room = limit ? std::min<uint64_t>(limit, P.log_capacity - pos0) : P.log_capacity - pos0;
   uint8_t* base = m.log + pos0;
   uint64_t nb = P.n_batches.load(std::memory_order_relaxed);
   int64_t hw = P.high_watermark.load(std::memory_order_relaxed);
@@ -405,11 +412,16 @@ Broker::Ingested Broker::ingest(uint32_t pidx, uint64_t len, int64_t from_offset
   const uint8_t* in = base;
   uint64_t in_len = len, r = 0, w = 0, consumed_base = 0;
   std::vector<uint8_t> spill, plain;
+  const bool ring = P.ring_bytes.load(std::memory_order_relaxed) != 0;
+  auto fits = [&](uint64_t total) {
+    return w + total <= room && (ring ? nb - P.first_batch.load(std::memory_order_relaxed) < P.index_capacity
+                                      : nb < P.index_capacity);
+  };
   auto publish = [&](const uint8_t* src, uint64_t total, const BatchHeader& h) {
-    if (pos0 + w + total > P.log_capacity) throw KafkaError("partition log full (raise log_capacity)");
-    if (nb >= P.index_capacity) throw KafkaError("partition index full");
     if (base + w != src) std::memmove(base + w, src, total);
-    m.idx[nb++] = IndexEntry{h.base_offset, pos0 + w, uint32_t(total), h.last_offset_delta, h.max_timestamp};
+    m.idx[nb % P.index_capacity] = IndexEntry{h.base_offset, pos0 + w, uint32_t(total), h.last_offset_delta,
+                                              h.max_timestamp};
+    ++nb;
     w += total;
     hw = h.next_offset();
     ++out.kept;
@@ -430,12 +442,17 @@ Broker::Ingested Broker::ingest(uint32_t pidx, uint64_t len, int64_t from_offset
     if (h.magic != 2)
       throw CorruptRecord("replica: message format v" + std::to_string(h.magic) +
                           " (only RecordBatch v2 is supported; upgrade the topic's message.format.version)");
+    const bool control = (h.attributes >> 5) & 1;
+    const bool keep = (!control || keep_control) && h.next_offset() > from_offset && h.next_offset() > hw;
+    const int codec = h.attributes & 7;
+    if (keep && (codec == kCodecNone || keep_control) && !fits(total)) {
+      out.full = true;  // refetched once committed batches free space
+      break;
+    }
     out.consumed = consumed_base + r + total;
     out.next_offset = h.next_offset();
-    const bool control = (h.attributes >> 5) & 1;
     if (control) ++out.control;
-    if ((!control || keep_control) && h.next_offset() > from_offset && h.next_offset() > hw) {
-      const int codec = h.attributes & 7;
+    if (keep) {
       if (codec == kCodecNone || keep_control) {
         publish(in + r, total, h);
       } else {
@@ -459,6 +476,12 @@ Broker::Ingested Broker::ingest(uint32_t pidx, uint64_t len, int64_t from_offset
         const uint32_t be_crc = __builtin_bswap32(crc32c(plain.data() + kBatchAttrOffset, plain.size() - kBatchAttrOffset));
         std::memcpy(plain.data() + kBatchCrcOffset, &be_crc, 4);
         BatchHeader ph = parse_batch_header(plain.data(), plain.size());
+        if (!fits(plain.size())) {
+          out.consumed = consumed_base + r;
+          out.next_offset = h.base_offset;  // not taken: fetched again
+          out.full = true;
+          break;
+        }
         publish(plain.data(), plain.size(), ph);
         ++out.inflated;
       }
@@ -482,13 +505,68 @@ Broker::Ingested Broker::ingest(uint32_t pidx, uint64_t len, int64_t from_offset
 uint64_t Broker::position_of(uint32_t pidx, int64_t offset) {
   const PartitionEntry& P = part(pidx);
   const IndexEntry* idx = mapped(pidx).idx;
+  const uint64_t icap = P.index_capacity;
   const int64_t nb = int64_t(P.n_batches.load(std::memory_order_acquire));
-  int64_t lo = 0, hi = nb;  // first batch whose last offset >= offset
+  int64_t lo = int64_t(P.first_batch.load(std::memory_order_acquire)), hi = nb;  // first batch ending >= offset
   while (lo < hi) {
-    const int64_t mid = (lo + hi) / 2;
-    if (idx[mid].base_offset + idx[mid].last_offset_delta < offset) lo = mid + 1; else hi = mid;
+    const int64_t mid = lo + (hi - lo) / 2;
+    const IndexEntry& e = idx[uint64_t(mid) % icap];
+    if (e.base_offset + e.last_offset_delta < offset) lo = mid + 1; else hi = mid;
   }
-  return lo < nb ? idx[lo].pos : P.log_end_pos.load(std::memory_order_acquire);
+  return lo < nb ? idx[uint64_t(lo) % icap].pos : P.log_end_pos.load(std::memory_order_acquire);
+}
+
+void Broker::make_ring(uint32_t pidx, uint64_t bytes) {
+  PartitionEntry& P = part(pidx);
+  RobustLock l(&P.lock);
+  if (P.n_batches.load() != 0) throw KafkaError("make_ring: partition already holds batches");
+  if (bytes == 0 || bytes > P.log_capacity) throw std::invalid_argument("make_ring: 0 < bytes <= log capacity");
+  P.ring_bytes.store(bytes, std::memory_order_release);
+  P.first_batch.store(0, std::memory_order_release);
+}
+
+uint8_t* Broker::ring_reserve(uint32_t pidx, uint64_t want, int64_t keep_offset, uint64_t* avail) {
+  PartitionEntry& P = part(pidx);
+  Mapped& m = mapped(pidx);
+  RobustLock l(&P.lock);
+  const uint64_t C = P.ring_bytes.load(std::memory_order_relaxed);
+  if (!C) throw KafkaError("ring_reserve on a linear log");
+  const uint64_t icap = P.index_capacity;
+  const uint64_t nb = P.n_batches.load(std::memory_order_relaxed);
+  uint64_t first = P.first_batch.load(std::memory_order_relaxed);
+  // retire batches every reader is done with (committed past): their bytes may be written over
+  bool moved = false;
+  while (first < nb) {
+    const IndexEntry& e = m.idx[first % icap];
+    if (e.base_offset + e.last_offset_delta >= keep_offset) break;
+    ++first;
+    moved = true;
+  }
+  if (moved) {
+    const int64_t start = first < nb ? m.idx[first % icap].base_offset : P.high_watermark.load();
+    if (start > P.log_start_offset.load()) P.log_start_offset.store(start, std::memory_order_release);
+    P.first_batch.store(first, std::memory_order_release);
+  }
+  uint64_t w = P.log_end_pos.load(std::memory_order_relaxed);
+  uint64_t free_bytes;
+  if (first == nb) {  // nothing live: anywhere
+    if (C - w < want) w = 0;
+    free_bytes = C - w;
+  } else {
+    const uint64_t oldest = m.idx[first % icap].pos;
+    if (oldest < w) {  // live bytes lie behind the writer: the tail, or the head before them
+      free_bytes = C - w;
+      if (free_bytes < want && oldest > free_bytes) {
+        w = 0;
+        free_bytes = oldest;
+      }
+    } else {  // the writer wrapped and sits behind the oldest live batch
+      free_bytes = oldest - w;
+    }
+  }
+  if (w != P.log_end_pos.load(std::memory_order_relaxed)) P.log_end_pos.store(w, std::memory_order_release);
+  *avail = std::min(free_bytes, want);
+  return m.log + w;
 }
 
 uint64_t Broker::release_log(uint32_t pidx, uint64_t from, uint64_t to) {

@@ -99,6 +99,12 @@ struct alignas(64) PartitionEntry {
   std::atomic<uint32_t> pinned;
   std::atomic<uint64_t> fetch_calls, bytes_fetched, records_produced;
   std::atomic<uint64_t> pin_floor;  // in the struct's former tail padding: the layout is unchanged
+  // Ring logs (KafkaBridge replicas): the log is a ring of ring_bytes whose pages are written over
+  // once their batches are committed -- the pages stay allocated and pinned, so a long stream
+  // needs no page freeing, unpinning or re-pinning.  Index entries are a ring too: logical batch
+  // i lives in slot i % index_capacity; [first_batch, n_batches) are live.  Linear logs: 0, 0.
+  std::atomic<uint64_t> ring_bytes;
+  std::atomic<uint64_t> first_batch;
 };
 static_assert(sizeof(PartitionEntry) == 192, "partition entry layout (shared with existing broker files)");
 
@@ -200,6 +206,7 @@ class Broker {
     uint64_t consumed = 0;     // bytes of whole batches walked (kept or dropped)
     uint64_t kept_bytes = 0;
     uint32_t kept = 0, control = 0, inflated = 0;  // inflated: compressed batches stored decompressed
+    bool full = false;         // stopped at a batch the space left could not hold
     int64_t next_offset = -1;  // next offset to fetch (-1: no whole batch in the data)
   };
   // Walks the RecordBatches received at log_tail(): keeps (indexes, publishes) whole data
@@ -208,9 +215,19 @@ class Broker {
   // fetch to overwrite.  Compressed batches (gzip/snappy/lz4, codecs.h) are CRC-checked and stored
   // inflated, as plain RecordBatch v2 with a fresh CRC: the device path decodes raw records.
   // keep_control: store control batches too (a broker's own log, e.g. the wire server's tests).
-  Ingested ingest(uint32_t pidx, uint64_t len, int64_t from_offset, bool keep_control = false);
+  // `limit`: bytes from the write position the batches may occupy (0: up to the capacity); a batch
+  // that does not fit ends the walk (Ingested::full) and is fetched again later.
+  Ingested ingest(uint32_t pidx, uint64_t len, int64_t from_offset, bool keep_control = false, uint64_t limit = 0);
   // Log byte position of the first batch holding an offset >= `offset` (log end if none).
   uint64_t position_of(uint32_t pidx, int64_t offset);
+  // Index entry of logical batch i (ring-indexed: slot i % index_capacity).
+  IndexEntry entry(uint32_t pidx, int64_t i) { return mapped(pidx).idx[uint64_t(i) % part(pidx).index_capacity]; }
+  // Turns an empty partition into a ring log of `bytes` (<= its capacity).
+  void make_ring(uint32_t pidx, uint64_t bytes);
+  // Ring logs: retires live batches that end at or below `keep_offset` (log start moves up), then
+  // returns the write position with up to `want` contiguous bytes that overwrite no live batch
+  // (wrapping to the ring's start when the tail is too short); *avail = those bytes (may be < want).
+  uint8_t* ring_reserve(uint32_t pidx, uint64_t want, int64_t keep_offset, uint64_t* avail);
   uint32_t flags() const { return meta_->flags.load(std::memory_order_acquire); }
   void set_flags(uint32_t f) { meta_->flags.fetch_or(f, std::memory_order_acq_rel); }
   // Frees log bytes [from, to) (page-aligned inwards) of a partition: FALLOC_FL_PUNCH_HOLE on its

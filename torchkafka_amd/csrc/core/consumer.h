@@ -167,7 +167,7 @@ size_t Fetcher::scan(FetchPart& fp, size_t max_records, F&& visit, G&& on_batch)
   while (taken < max_records && fp.position < hw) {
     const int64_t bi = b.find_batch(fp.pidx, fp.position, fp.batch_hint);
     fp.batch_hint = bi;
-    const IndexEntry e = idx[bi];
+    const IndexEntry e = idx[uint64_t(bi) % P.index_capacity];  // ring-indexed (replica ring logs)
     if (!sparse_touch_ && e.pos + e.size > fp.populated_end)
       prefault(fp, log, e.pos, P.log_end_pos.load(std::memory_order_acquire));
     const uint8_t* bp = log + e.pos;

@@ -53,6 +53,9 @@ void Replicator::start() {
     throw KafkaError("replicator: local topic '" + cfg_.topic + "' has " + std::to_string(ti.n_partitions) +
                      " partitions, the cluster " + std::to_string(n_remote_parts_));
   first_pidx_ = ti.first_pidx;
+  if (cfg_.ring_bytes && cfg_.ring_bytes < (uint64_t(cfg_.partition_max_bytes) * 4))
+    throw std::invalid_argument("replicator: ring_bytes must hold at least 4 x partition_max_bytes");
+  if (cfg_.ring_bytes) cfg_.release_consumed = false;  // a ring reuses its pages: nothing to free
   if (cfg_.release_consumed && !cfg_.group.empty()) local_->set_flags(kReleaseConsumed);
   std::vector<int32_t> ids = cfg_.partitions;
   if (ids.empty())
@@ -88,6 +91,7 @@ void Replicator::start() {
     PartitionEntry& P = local_->part(p->pidx);
     if (P.n_batches.load() == 0) {
       local_->reset_empty(p->pidx, start);
+      if (cfg_.ring_bytes) local_->make_ring(p->pidx, std::min<uint64_t>(cfg_.ring_bytes, P.log_capacity));
       p->fetch_offset = start;
     } else {
       p->fetch_offset = P.high_watermark.load();  // a persistent (file://) replica resumes its log
@@ -148,7 +152,24 @@ void Replicator::stop(bool flush) {
   }
 }
 
+int64_t Replicator::keep_offset(Part& p) {
+  int64_t c = cfg_.group.empty() ? -1 : local_->committed(group_, p.pidx);
+  return c < 0 ? p.start_offset : c;
+}
+
+// Write room for the next record set: a ring log reuses the bytes of committed batches, a linear
+// log has its tail up to the capacity.
+uint8_t* Replicator::room(Part& p, uint64_t* avail) {
+  if (cfg_.ring_bytes) return local_->ring_reserve(p.pidx, uint64_t(cfg_.partition_max_bytes), keep_offset(p), avail);
+  return local_->log_tail(p.pidx, avail);
+}
+
 bool Replicator::throttled(Part& p) {
+  if (cfg_.ring_bytes) {  // a ring is full while the consumers hold it: flow control by itself
+    uint64_t avail = 0;
+    local_->ring_reserve(p.pidx, uint64_t(cfg_.partition_max_bytes), keep_offset(p), &avail);
+    return avail < std::min<uint64_t>(uint64_t(cfg_.partition_max_bytes), 256u << 10);
+  }
   const PartitionEntry& P = local_->part(p.pidx);
   const uint64_t end = P.log_end_pos.load(std::memory_order_acquire);
   if (end == 0) return false;
@@ -200,7 +221,8 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
         std::map<int32_t, Part*> lookup;
         for (Part* p : ps) {
           uint64_t avail = 0;
-          local_->log_tail(p->pidx, &avail);
+          room(*p, &avail);
+          if (avail < 4096 && cfg_.ring_bytes) continue;  // waits for the consumers to commit
           if (avail < 4096) {
             if (!failed.count(p))
               set_error("replicator: local log of " + cfg_.topic + "-" + std::to_string(p->partition) +
@@ -247,16 +269,18 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
             p->fetches.fetch_add(1, std::memory_order_relaxed);
             if (len <= 0) continue;
             uint64_t avail = 0;
-            uint8_t* tail = local_->log_tail(p->pidx, &avail);
-            if (uint64_t(len) > avail) {  // an oversized first batch (KIP-74) the log cannot hold
+            uint8_t* tail = room(*p, &avail);
+            if (uint64_t(len) > avail) {  // an oversized first batch (KIP-74) the log cannot hold now
               k.skip(size_t(len));
+              if (cfg_.ring_bytes && uint64_t(len) < cfg_.ring_bytes / 2) continue;  // refetched when room frees
               set_error("replicator: local log of " + cfg_.topic + "-" + std::to_string(pid) + " is full");
               failed.insert(p);
               continue;
             }
             k.read(tail, size_t(len));  // the record set lands in the log tail: no second copy
             try {
-              const Broker::Ingested in = local_->ingest(p->pidx, uint64_t(len), p->fetch_offset.load());
+              const Broker::Ingested in = local_->ingest(p->pidx, uint64_t(len), p->fetch_offset.load(), false,
+                                                         cfg_.ring_bytes ? avail : 0);
               if (in.next_offset > p->fetch_offset.load()) p->fetch_offset.store(in.next_offset);
               p->bytes.fetch_add(in.kept_bytes, std::memory_order_relaxed);
               p->batches.fetch_add(in.kept, std::memory_order_relaxed);

@@ -48,6 +48,10 @@ struct ReplicaConfig {
   bool release_consumed = true;        // free committed log bytes (punch holes; kReleaseConsumed)
   uint64_t release_bytes = 256u << 20; // ... keeping this many consumed bytes per partition resident
   uint64_t release_step = 1u << 30;    // ... in bursts, once a partition has this many releasable bytes
+  // Ring replica (the default for device loaders): each partition log is a ring of this many bytes
+  // whose committed batches are written over -- pages allocated and pinned once, no release.
+  // 0: a linear log (grows; committed bytes released per release_consumed).
+  uint64_t ring_bytes = 0;
   uint64_t log_capacity = 0;           // local topic creation (0: the broker default)
   uint64_t index_capacity = 0;
 };
@@ -105,6 +109,8 @@ class Replicator {
   void fetch_loop(std::vector<Part*> mine);
   void commit_loop();
   bool throttled(Part& p);
+  int64_t keep_offset(Part& p);
+  uint8_t* room(Part& p, uint64_t* avail);
   void reset_offset(wire::Client& c, Part& p);
   void set_error(const std::string& e);
   int forward(wire::Client& c);

@@ -348,11 +348,12 @@ bool WireServer::handle(int fd, const std::vector<uint8_t>& req) {
             const IndexEntry* idx = b_->index_base(pidx);
             const uint64_t nb = P.n_batches.load(std::memory_order_acquire);
             const int64_t i = b_->find_batch(pidx, off, -1);
-            const uint64_t pos0 = idx[i].pos;
+            const uint64_t icap = P.index_capacity;
+            const uint64_t pos0 = idx[uint64_t(i) % icap].pos;
             const uint64_t cap = uint64_t(std::max<int64_t>(1, std::min<int64_t>(pmax, budget)));
-            uint64_t end = pos0 + idx[i].size;  // at least one batch (KIP-74)
-            for (uint64_t k = uint64_t(i) + 1; k < nb && idx[k].pos + idx[k].size - pos0 <= cap; ++k)
-              end = idx[k].pos + idx[k].size;
+            uint64_t end = pos0 + idx[uint64_t(i) % icap].size;  // at least one batch (KIP-74)
+            for (uint64_t k = uint64_t(i) + 1; k < nb && idx[k % icap].pos + idx[k % icap].size - pos0 <= cap; ++k)
+              end = idx[k % icap].pos + idx[k % icap].size;
             data = b_->log_base(pidx) + pos0;
             n = size_t(end - pos0);
             budget -= int64_t(n);

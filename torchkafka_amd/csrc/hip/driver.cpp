@@ -846,7 +846,9 @@ void MainDriver::launch_var_span(const int* slots, const SlotView* const* views,
 
 const uint8_t* MainDriver::seg_src(const tk::SpanSeg& sg) {
   const uint8_t* log = broker_->log_base(sg.pidx);  // pinned: device address == host address
-  if (mirror_) {
+  // a ring log (KafkaBridge replica) writes over its chunks: an HBM mirror of them would go stale,
+  // so its segments are read zero-copy
+  if (mirror_ && broker_->part(sg.pidx).ring_bytes.load(std::memory_order_relaxed) == 0) {
     // pin ahead of the segment so the mirror can copy (and prefetch) whole chunks
     const auto& part = broker_->part(sg.pidx);
     ensure_log(sg.pidx, std::min<uint64_t>(part.log_capacity, sg.log_pos + mirror_->span_bytes()));
