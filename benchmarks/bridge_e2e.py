@@ -69,6 +69,7 @@ def main() -> int:
     ap.add_argument("--partition-fetch-mib", type=int, default=8)
     ap.add_argument("--max-lag-mib", type=int, default=512)
     ap.add_argument("--release-mib", type=int, default=256, help="consumed bytes kept resident per partition")
+    ap.add_argument("--ring-mib", type=int, default=512, help="replica ring per partition (0: linear + release)")
     ap.add_argument("--release-step-mib", type=int, default=1024, help="release burst threshold per partition")
     ap.add_argument("--no-release", action="store_true", help="keep committed replica bytes (no unpin/punch)")
     ap.add_argument("--stats", action="store_true")
@@ -112,7 +113,8 @@ def main() -> int:
         ev.wait(30)
         procs.append(pr)
     boot = f"127.0.0.1:{ports[0]}" if ports else None
-    out = {"server": "python" if args.python_server else "native", "nodes": args.nodes, "partitions": args.partitions, "records_per_partition": args.records,
+    out = {"server": "python" if args.python_server else "native", "nodes": args.nodes,
+           "partitions": args.partitions, "records_per_partition": args.records,
            "cluster_gb": round(total_bytes / 1e9, 3), "fill_s": round(fill_s, 2)}
     try:
         # (1) replication alone
@@ -145,7 +147,8 @@ def main() -> int:
                          index_capacity=1 << 22, max_partition_fetch_bytes=args.partition_fetch_mib << 20,
                          max_lag_bytes=args.max_lag_mib << 20,
                          release_consumed=not (args.no_release or args.unpin_only),
-                         release_bytes=args.release_mib << 20, release_step=args.release_step_mib << 20)
+                         release_bytes=args.release_mib << 20, release_step=args.release_step_mib << 20,
+                         ring_bytes=args.ring_mib << 20)
         if br is not None and args.unpin_only:
             br.local.native.flags = 1  # kReleaseConsumed: the driver unpins, nobody punches
         dl = DeviceLoader(Rows.placeholder(), args.batch_size, num_workers=args.workers, device=args.device,

@@ -53,9 +53,9 @@ for s in ${STEPS:-pytest_new}; do
     bridge) run bridge_e2e 600 python benchmarks/bridge_e2e.py
             run bridge_e2e_1node 600 python benchmarks/bridge_e2e.py --nodes 1
             run bridge_e2e_8node 600 python benchmarks/bridge_e2e.py --nodes 8 --workers 8 ;;
-    bridgex) run bridge_native_long 900 python benchmarks/bridge_e2e.py --records 2000000 --stats
-             run bridge_native_long_norel 900 python benchmarks/bridge_e2e.py --records 2000000 --no-release --stats
-             run bridge_native_long_8n 900 python benchmarks/bridge_e2e.py --records 2000000 --nodes 8 --workers 8 --stats ;;
+    bridgex) run bridge_ring_long 900 python benchmarks/bridge_e2e.py --records 2000000 --stats
+             run bridge_ring_long_8n 900 python benchmarks/bridge_e2e.py --records 2000000 --nodes 8 --workers 8 --stats
+             run bridge_linear_long 900 python benchmarks/bridge_e2e.py --records 2000000 --ring-mib 0 --stats ;;
     pytest_bridge) run pytest_bridge 400 python -u -m pytest tests/test_gpu_bridge.py -x -v -p no:cacheprovider --timeout 240 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   esac

@@ -4,4 +4,5 @@ from .bridge import KafkaBridge
 from .synthetic import SyntheticBroker, is_synthetic_url, open_broker, resolve_url
 from .wire_server import KafkaWireServer, NativeWireServer
 
-__all__ = ["SyntheticBroker", "KafkaBridge", "KafkaWireServer", "NativeWireServer", "open_broker", "resolve_url", "is_synthetic_url"]
+__all__ = ["SyntheticBroker", "KafkaBridge", "KafkaWireServer", "NativeWireServer", "open_broker", "resolve_url",
+           "is_synthetic_url"]

@@ -19,7 +19,8 @@ the last one::
         ...
     bridge.close()          # forwards the final commit
 
-Memory: by default each replica partition is a **ring** of ``ring_bytes`` (512 MiB): the
+Memory: by default (with a ``group_id``) each replica partition is a **ring** of ``ring_bytes``
+(512 MiB): the
 replicator writes over batches the group has committed, so the pages are allocated, and pinned by
 a device loader, once -- a stream of any length needs no page freeing, unpinning or re-pinning,
 and a full ring is the flow control (consumers behind by ``ring_bytes`` hold the fetches).  With
@@ -63,7 +64,7 @@ class KafkaBridge:
                  fetch_max_bytes: int = 64 << 20, max_partition_fetch_bytes: int = 8 << 20,
                  request_timeout_ms: int = 30000, commit_interval_ms: int = 5, fetchers: int = 0,
                  client_id: str = "torchkafka-bridge", release_consumed: bool = True,
-                 release_bytes: int = 256 << 20, release_step: int = 1 << 30, ring_bytes: int = 512 << 20,
+                 release_bytes: int = 256 << 20, release_step: int = 1 << 30, ring_bytes: int | None = None,
                  start: bool = True):
         if not isinstance(bootstrap_servers, str):
             bootstrap_servers = ",".join(bootstrap_servers)
@@ -71,6 +72,8 @@ class KafkaBridge:
         self.topic = topic
         self.group_id = group_id
         self.url = url or f"shm://tkbridge-{os.getpid()}-{uuid.uuid4().hex[:8]}"
+        if ring_bytes is None:  # a ring frees space as the group commits: without a group, a linear log
+            ring_bytes = min(512 << 20, int(log_capacity)) if group_id else 0
         self._own = url is None
         # a fresh local broker (or an existing persistent replica: file:// URLs resume their logs)
         self.local = SyntheticBroker(self.url, create=True, log_capacity=log_capacity,
