@@ -299,6 +299,7 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
       }
       backoff_ms = 0;
     } catch (const std::exception& e) {
+      if (stop_.load()) break;  // a wait cancelled by stop(): not an error
       set_error(std::string("replicator: ") + e.what());
       c.reset();  // reconnect + fresh metadata
       backoff_ms = std::min(1000, std::max(10, backoff_ms * 2));
@@ -354,6 +355,7 @@ void Replicator::commit_loop() {
       forward(*commit_client_);
       backoff_ms = cfg_.commit_interval_ms;
     } catch (const std::exception& e) {
+      if (stop_.load()) break;
       set_error(std::string("replicator: commit: ") + e.what());
       commit_client_.reset();
       backoff_ms = std::min(1000, std::max(10, backoff_ms * 2));
