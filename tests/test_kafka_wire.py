@@ -697,3 +697,23 @@ def test_ring_replica_feeds_a_device_loader(broker, server):
         assert sorted(seen) == [(p, o) for p in range(2) for o in range(3000)]
         assert all(br.local.native.first_batch(br.local.pidx("t", p)) > 0 for p in range(2))
     assert broker.committed_offsets("gr", "t") == {0: 3000, 1: 3000}
+
+
+def test_load_state_dict_rewinds_a_bridged_cluster(broker, server):
+    """A checkpoint's offsets are the cluster's: load_state_dict commits them there and mirrors
+    afresh from them, even where the replica no longer holds those records (ring written over)."""
+    broker.create_topic("t", 2)
+    broker.fill("t", 400, "fixed_f32", size=8, records_per_batch=20)
+    kw = dict(bootstrap_servers=server.address, group_id="ck", auto_offset_reset="earliest", consumer_timeout_ms=400)
+    dl = DeviceLoader(Vec8.placeholder(), 20, device="cpu", num_workers=1, worker_init_fn=Vec8.init_worker("t", **kw))
+    n = sum(x.shape[0] for x in auto_commit(dl))
+    dl.close()
+    assert n == 800 and broker.committed_offsets("ck", "t") == {0: 400, 1: 400}
+    # resume from a checkpoint taken earlier in the stream
+    dl2 = DeviceLoader(Vec8.placeholder(), 20, device="cpu", num_workers=1, worker_init_fn=Vec8.init_worker("t", **kw))
+    dl2.load_state_dict({"version": 1, "group_id": "ck", "offsets": {"t": {0: 100, 1: 300}}})
+    assert broker.committed_offsets("ck", "t") == {0: 100, 1: 300}
+    got = sorted((int(p), int(o)) for x in auto_commit(dl2) for o, p in x[:, :2].tolist())
+    dl2.close()
+    assert got == sorted([(0, o) for o in range(100, 400)] + [(1, o) for o in range(300, 400)])
+    assert broker.committed_offsets("ck", "t") == {0: 400, 1: 400}

@@ -480,15 +480,30 @@ class DeviceLoader:
         group = wi.kwargs.get("group_id")
         reset = wi.kwargs.get("auto_offset_reset", "latest")  # kafka-python's default
         client = core().WireClient(servers, "torchkafka-bridge", int(wi.kwargs.get("request_timeout_ms", 30000)))
-        url = None
+        shares = {}
+        for t in topics:
+            err, parts = client.metadata(t)
+            if err:
+                raise KafkaError(f"UnknownTopicOrPartitionError: topic {t!r} on {servers}")
+            shares[t] = shard_partitions(len(parts), self.rank, self.world_size)
+        self._bridge_spec = (servers, group, reset, shares)
+        url = self._start_bridges(None)
+        log.info("DeviceLoader: %s mirrored into %s by %d KafkaBridge(s) (rank %d/%d).", servers, url,
+                  len(self._bridges), self.rank, self.world_size)
+        return _WorkerInit(wi.cls, wi.args, {**wi.kwargs, "bootstrap_servers": url})
+
+    def _start_bridges(self, url):
+        """One KafkaBridge per topic of ``self._bridge_spec`` into one replica broker (``url``: reuse
+        that name); returns the replica's URL."""
+        from ..broker.bridge import KafkaBridge
+
+        servers, group, reset, shares = self._bridge_spec
+        first = True
         try:
-            for t in topics:
-                err, parts = client.metadata(t)
-                if err:
-                    raise KafkaError(f"UnknownTopicOrPartitionError: topic {t!r} on {servers}")
-                mine = shard_partitions(len(parts), self.rank, self.world_size)
+            for t, mine in shares.items():
                 br = KafkaBridge(servers, t, group_id=group, partitions=mine, url=url, auto_offset_reset=reset)
-                br._own = url is None  # the first bridge owns the shared replica broker
+                br._own = first  # the first bridge owns the shared replica broker
+                first = False
                 url = br.url
                 self._bridges.append(br)
         except BaseException:
@@ -496,9 +511,7 @@ class DeviceLoader:
                 br.close(flush=False)
             self._bridges.clear()
             raise
-        log.info("DeviceLoader: %s mirrored into %s by %d KafkaBridge(s) (rank %d/%d).", servers, url,
-                  len(self._bridges), self.rank, self.world_size)
-        return _WorkerInit(wi.cls, wi.args, {**wi.kwargs, "bootstrap_servers": url})
+        return url
 
     def _resolve_commit_target(self, group_id, servers):
         from ..models.kafka_dataset import _WorkerInit
@@ -1472,8 +1485,25 @@ class DeviceLoader:
         group = state.get("group_id") or self._group_id
         if group is None:
             raise RuntimeError("load_state_dict needs a group_id (in the state or the loader)")
-        b = self._broker()
         offs = {TopicPartition(t, int(p)): int(o) for t, parts in state["offsets"].items() for p, o in parts.items()}
+        if self._bridges and offs:
+            # a replica of a Kafka cluster: the offsets are the cluster's -- commit them there, then
+            # mirror afresh from them (the replica may not hold those records any more)
+            from ..ops.native import core
+
+            servers = self._bridge_spec[0]
+            client = core().WireClient(servers, "torchkafka-bridge", 30000)
+            for t in sorted({tp.topic for tp in offs}):
+                errs = client.offset_commit(group, t, {tp.partition: o for tp, o in offs.items() if tp.topic == t})
+                bad = {p: e for p, e in errs.items() if e}
+                if bad:
+                    raise KafkaError(f"CommitFailedError: load_state_dict could not commit {t} {bad} on {servers}")
+            url = self._bridges[0].url
+            for br in reversed(self._bridges):
+                br.close(flush=False)
+            self._bridges = []
+            self._start_bridges(url)
+        b = self._broker()
         if offs:
             b.commit(group, offs)
         self._committed.update({b.pidx(tp.topic, tp.partition): o for tp, o in offs.items()})
