@@ -137,10 +137,11 @@ void Replicator::stop(bool flush) {
   running_ = false;
   if (flush && !cfg_.group.empty()) {
     commit_client_.reset();  // its connections may carry the stop flag: flush on fresh ones
+    const int flush_timeout = std::min(cfg_.timeout_ms, 5000);  // close() must not hang on a dead cluster
     for (int attempt = 0; attempt < 3; ++attempt) {
       try {
         if (!commit_client_)
-          commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", cfg_.timeout_ms);
+          commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", flush_timeout);
         forward(*commit_client_);
         break;
       } catch (const KafkaError& e) {
