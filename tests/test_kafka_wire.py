@@ -717,3 +717,21 @@ def test_load_state_dict_rewinds_a_bridged_cluster(broker, server):
     dl2.close()
     assert got == sorted([(0, o) for o in range(100, 400)] + [(1, o) for o in range(300, 400)])
     assert broker.committed_offsets("ck", "t") == {0: 400, 1: 400}
+
+
+def test_serve_cli(broker):
+    import subprocess
+    import sys
+
+    broker.create_topic("t", 2)
+    broker.fill("t", 10, "fixed_f32", size=8)
+    p = subprocess.Popen([sys.executable, "-m", "torchkafka_amd.broker.serve", broker.url, "--port", "0"],
+                         stdout=subprocess.PIPE, text=True,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        line = p.stdout.readline().strip()
+        assert line.startswith("serving ")
+        assert core().WireClient(line.rsplit(" ", 1)[1]).list_offsets("t", [0, 1], -1) == {0: 10, 1: 10}
+    finally:
+        p.terminate()
+        p.wait(10)

@@ -549,3 +549,4 @@ class NativeWireServer:
 
     def __exit__(self, *exc):
         self.close()
+
