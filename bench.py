@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--copy-streams", type=int, default=4)
     ap.add_argument("--mirror-chunk-mib", type=int, default=8,
                     help="--h2d dma with device decode: MiB per hipMemcpyAsync into the HBM log mirror")
+    ap.add_argument("--mirror-chunks", type=int, default=None, help="--h2d dma: HBM mirror buffers per partition")
     ap.add_argument("--lockstep-depth", type=int, default=2)
     ap.add_argument("--coalesce", type=int, default=8, help="staged batches collated per kernel launch")
     ap.add_argument("--coalesce-wait-us", type=int, default=50, help="adaptive coalescing wait while the GPU is busy")
@@ -144,6 +145,7 @@ def main() -> int:
         event_every=args.event_every, numa_bind=not args.no_numa, coalesce=args.coalesce,
         coalesce_wait_us=args.coalesce_wait_us, decode=args.decode, lockstep=lockstep,
         mirror_chunk_mib=args.mirror_chunk_mib,
+        **({"mirror_chunks": args.mirror_chunks} if args.mirror_chunks else {}),
         worker_init_fn=Records.init_worker("bench", bootstrap_servers=url, group_id="bench",
                                            auto_offset_reset="earliest", check_crcs=not args.no_crc),
     )
