@@ -82,9 +82,10 @@ class Tuning:
         mirror_chunk_mib: h2d='dma' with device decode: log bytes per hipMemcpyAsync into the HBM
             mirror of a partition log (1..1024 MiB).
         mirror_chunks: HBM mirror buffers per partition (2..64); K - 2 of them are prefetched ahead.
-            4 by default: deeper prefetch queues more SDMA work in front of each launch's copy event and
-            intermittently collapsed the steady state (8 MiB x 6: 13-47 M rec/s, x 8: 11 M; x 4: 43-46 M;
-            tools/mirror_probe.sh, tools/dma_steps_probe.sh).
+            6 by default.  Each launch's prefetches are queued after its copy event (a launch never
+            waits for them): 8 MiB x 6 then runs 48-49 M rec/s steady (13-47 M before, when a launch's
+            event also covered its own prefetches); 8 buffers still collapse (8-11 M; avoid).
+            tools/mirror_probe.sh, tools/mirror_probe2.sh.
         group_mib: device-decode groups stop growing at this many MiB of log bytes (1..1024): a
             group's batches become committable together, so large batches form small groups.
     """
@@ -103,7 +104,7 @@ class Tuning:
     span_burst: Optional[int] = None
     worker_spin_us: Optional[int] = None
     mirror_chunk_mib: int = 8
-    mirror_chunks: int = 4
+    mirror_chunks: int = 6
     group_mib: int = 16
 
     def __post_init__(self):

@@ -113,16 +113,28 @@ const uint8_t* LogMirror::map(uint32_t pidx, uint64_t pos, uint32_t len, const u
     pending_.emplace_back(pidx, int(c % K_));
   }
   // the next chunks stream in behind this one while the decode catches up with it: K - 2 ahead (one
-  // buffer for the chunk being read, one for the chunk its readers may still finish)
-  for (int64_t d = 1; d <= prefetch_ && pinned > uint64_t(c + d) * chunk_; ++d)
-    if (!ensure(P, pidx, c + d, 0, log, pinned, true)) break;
+  // buffer for the chunk being read, one for the chunk its readers may still finish).  Queued after
+  // before() has recorded this launch's copy event, so the launch never waits for its prefetches.
+  deferred_.push_back(Deferred{pidx, c, log, pinned});
   return P.dev + size_t(c % K_) * stride_ + (pos - uint64_t(c) * chunk_);
+}
+
+void LogMirror::issue_prefetches() {
+  for (const auto& d : deferred_) {
+    Part& P = parts_[d.pidx];
+    for (int64_t k = 1; k <= prefetch_ && d.pinned > uint64_t(d.chunk + k) * chunk_; ++k)
+      if (!ensure(P, d.pidx, d.chunk + k, 0, d.log, d.pinned, true)) break;
+  }
+  deferred_.clear();
 }
 
 void LogMirror::before(hipStream_t stream) {
   uint64_t need = 0;
   for (const auto& pb : pending_) need = std::max(need, parts_[pb.first].bufs[size_t(pb.second)].copy_seq);
-  if (need == 0 || need <= done_seq_) return;
+  if (need == 0 || need <= done_seq_) {
+    issue_prefetches();
+    return;
+  }
   // One event, recorded only when a launch needs a copy not known complete: it also covers the
   // prefetches queued behind that copy (a longer wait), but events between SDMA copies cost more
   // than they save (measured, config 2 --h2d dma: 46.5 M rec/s this way, 32-34 M with an event
@@ -133,9 +145,10 @@ void LogMirror::before(hipStream_t stream) {
   }
   if (hipEventQuery(copied_) == hipSuccess) {  // found complete: no wait, and remembered
     done_seq_ = recorded_seq_;
-    return;
+  } else {
+    TKM_CHECK(hipStreamWaitEvent(stream, copied_, 0));
   }
-  TKM_CHECK(hipStreamWaitEvent(stream, copied_, 0));
+  issue_prefetches();
 }
 
 int LogMirror::next_event() {

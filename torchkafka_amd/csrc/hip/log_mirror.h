@@ -76,6 +76,14 @@ class LogMirror {
               bool prefetch);
   void retarget(Buf& b, int64_t c);
   int next_event();
+  void issue_prefetches();
+  struct Deferred {
+    uint32_t pidx;
+    int64_t chunk;
+    const uint8_t* log;
+    uint64_t pinned;
+  };
+  std::vector<Deferred> deferred_;  // prefetches of the launch being formed, queued after its copy event
 
   int device_;
   uint64_t chunk_, stride_;
