@@ -735,3 +735,92 @@ def test_serve_cli(broker):
     finally:
         p.terminate()
         p.wait(10)
+
+
+# ---- TLS and SASL/PLAIN (kafka-python's security_protocol / ssl_* / sasl_* settings)
+
+@pytest.fixture(scope="module")
+def tls_cert(tmp_path_factory):
+    """A self-signed certificate for 127.0.0.1 (openssl CLI; the test is skipped without it)."""
+    import shutil
+    import subprocess
+    if shutil.which("openssl") is None:
+        pytest.skip("openssl CLI not available")
+    d = tmp_path_factory.mktemp("tls")
+    cert, key = str(d / "cert.pem"), str(d / "key.pem")
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", key, "-out", cert,
+                    "-days", "1", "-subj", "/CN=127.0.0.1", "-addext", "subjectAltName=IP:127.0.0.1"],
+                   check=True, capture_output=True)
+    return cert, key
+
+
+def secure_server(broker, tls_cert=None, users=None):
+    import ssl
+    ctx = None
+    if tls_cert is not None:
+        ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+        ctx.load_cert_chain(*tls_cert)
+    return KafkaWireServer(broker, ssl_context=ctx, sasl_users=users).start()
+
+
+def test_tls_replica_is_byte_identical(broker, tls_cert):
+    broker.create_topic("t", 2)
+    broker.fill("t", 300, "fixed_f32", size=16, records_per_batch=25)
+    srv = secure_server(broker, tls_cert)
+    try:
+        with bridge(srv, group_id="g", security_protocol="SSL", ssl_cafile=tls_cert[0]) as br:
+            assert br.wait_caught_up(10)
+            for p in range(2):
+                assert log_bytes(br.local, "t", p) == log_bytes(broker, "t", p)
+            br.local.commit("g", {TopicPartition("t", 0): 123})
+            assert wait_for(lambda: broker.committed_offsets("g", "t").get(0) == 123)
+        # an untrusted certificate (no cafile -> system roots) fails the handshake
+        with pytest.raises(Exception, match="(?i)ssl|certificate|NoBrokersAvailable"):
+            core().WireClient(srv.address, timeout_ms=2000, security={"security_protocol": "SSL"}).metadata("t")
+        # a plaintext client on a TLS listener gets nowhere
+        with pytest.raises(Exception):
+            core().WireClient(srv.address, timeout_ms=1000).metadata("t")
+    finally:
+        srv.close()
+
+
+def test_sasl_plain_authenticates(broker):
+    broker.create_topic("t", 1)
+    broker.fill("t", 50, "fixed_f32", size=8)
+    srv = secure_server(broker, users={"alice": "s3cret"})
+    try:
+        sec = {"security_protocol": "SASL_PLAINTEXT", "sasl_mechanism": "PLAIN", "sasl_plain_username": "alice"}
+        c = core().WireClient(srv.address, timeout_ms=2000, security=dict(sec, sasl_plain_password="s3cret"))
+        assert c.list_offsets("t", [0], -1) == {0: 50}
+        with pytest.raises(Exception, match="(?i)auth"):
+            core().WireClient(srv.address, timeout_ms=2000,
+                              security=dict(sec, sasl_plain_password="wrong")).metadata("t")
+        # no credentials: the listener drops the unauthenticated request
+        with pytest.raises(Exception):
+            core().WireClient(srv.address, timeout_ms=1000).metadata("t")
+        with bridge(srv, group_id="g", security_protocol="SASL_PLAINTEXT", sasl_mechanism="PLAIN",
+                    sasl_plain_username="alice", sasl_plain_password="s3cret") as br:
+            assert br.wait_caught_up(10) and br.local.end_offset("t", 0) == 50
+    finally:
+        srv.close()
+
+
+def test_sasl_ssl_combined(broker, tls_cert):
+    broker.create_topic("t", 2)
+    broker.fill("t", 120, "fixed_f32", size=8, records_per_batch=10)
+    srv = secure_server(broker, tls_cert, users={"bob": "pw"})
+    try:
+        with bridge(srv, group_id="g", security_protocol="SASL_SSL", ssl_cafile=tls_cert[0],
+                    sasl_plain_username="bob", sasl_plain_password="pw") as br:
+            assert br.wait_caught_up(10)
+            assert all(log_bytes(br.local, "t", p) == log_bytes(broker, "t", p) for p in range(2))
+    finally:
+        srv.close()
+
+
+def test_security_config_validates_the_mechanism():
+    from torchkafka_amd.broker.bridge import security_config
+    assert security_config(security_protocol="SSL", ssl_cafile=None, bootstrap_servers="x") == \
+        {"security_protocol": "SSL"}
+    with pytest.raises(ValueError, match="PLAIN"):
+        security_config(security_protocol="SASL_SSL", sasl_mechanism="SCRAM-SHA-256")

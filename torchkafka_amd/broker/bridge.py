@@ -53,6 +53,19 @@ from .synthetic import SyntheticBroker
 
 log = logging.getLogger("torchkafka.bridge")
 
+#: kafka-python configuration keys the native client understands for TLS / SASL
+SECURITY_KEYS = ("security_protocol", "ssl_cafile", "ssl_check_hostname", "ssl_certfile", "ssl_keyfile",
+                 "sasl_mechanism", "sasl_plain_username", "sasl_plain_password")
+
+
+def security_config(**kw) -> dict:
+    """The TLS / SASL subset of a kafka-python configuration, for the native wire client
+    (security_protocol PLAINTEXT | SSL | SASL_PLAINTEXT | SASL_SSL; SASL mechanism PLAIN)."""
+    out = {k: v for k, v in kw.items() if k in SECURITY_KEYS and v is not None}
+    if out.get("security_protocol", "PLAINTEXT").startswith("SASL_") and out.get("sasl_mechanism", "PLAIN") != "PLAIN":
+        raise ValueError(f"sasl_mechanism {out['sasl_mechanism']!r}: the native client speaks PLAIN")
+    return out
+
 
 class KafkaBridge:
     """Mirrors ``topic`` (all or ``partitions``) of a Kafka cluster into a local broker at :attr:`url`."""
@@ -65,6 +78,9 @@ class KafkaBridge:
                  request_timeout_ms: int = 30000, commit_interval_ms: int = 5, fetchers: int = 0,
                  client_id: str = "torchkafka-bridge", release_consumed: bool = True,
                  release_bytes: int = 256 << 20, release_step: int = 1 << 30, ring_bytes: int | None = None,
+                 security_protocol: str = "PLAINTEXT", ssl_cafile: str | None = None, ssl_check_hostname: bool = True,
+                 ssl_certfile: str | None = None, ssl_keyfile: str | None = None, sasl_mechanism: str | None = None,
+                 sasl_plain_username: str | None = None, sasl_plain_password: str | None = None,
                  start: bool = True):
         if not isinstance(bootstrap_servers, str):
             bootstrap_servers = ",".join(bootstrap_servers)
@@ -86,7 +102,12 @@ class KafkaBridge:
             max_lag_bytes=int(max_lag_bytes), commit_interval_ms=int(commit_interval_ms), fetchers=int(fetchers),
             log_capacity=int(log_capacity), index_capacity=int(index_capacity), client_id=client_id,
             release_consumed=bool(release_consumed), release_bytes=int(release_bytes),
-            release_step=int(release_step), ring_bytes=int(ring_bytes))
+            release_step=int(release_step), ring_bytes=int(ring_bytes),
+            security=security_config(security_protocol=security_protocol, ssl_cafile=ssl_cafile,
+                                     ssl_check_hostname=ssl_check_hostname, ssl_certfile=ssl_certfile,
+                                     ssl_keyfile=ssl_keyfile, sasl_mechanism=sasl_mechanism,
+                                     sasl_plain_username=sasl_plain_username,
+                                     sasl_plain_password=sasl_plain_password))
         self._closed = False
         self._lock = threading.Lock()
         self._reported = 0

@@ -33,7 +33,8 @@ SUPPORTED = {API_FETCH: (4, 4), API_LIST_OFFSETS: (0, 1), API_METADATA: (0, 1), 
              API_OFFSET_FETCH: (1, 1), API_FIND_COORDINATOR: (0, 0), API_API_VERSIONS: (0, 0)}
 
 NONE, OFFSET_OUT_OF_RANGE, UNKNOWN_TOPIC, NOT_LEADER, UNSUPPORTED_VERSION = 0, 1, 3, 6, 35
-ILLEGAL_GENERATION = 22
+ILLEGAL_GENERATION, UNSUPPORTED_SASL_MECHANISM, SASL_AUTHENTICATION_FAILED = 22, 33, 58
+API_SASL_HANDSHAKE, API_SASL_AUTHENTICATE = 17, 36
 
 
 class _R:
@@ -140,10 +141,16 @@ class KafkaWireServer:
     """Serves a :class:`SyntheticBroker` over the Kafka protocol on ``host:port`` (0: a free port)."""
 
     def __init__(self, broker: SyntheticBroker, host: str = "127.0.0.1", port: int = 0, node_id: int = 0,
-                 cluster: list[tuple[int, str, int]] | None = None):
+                 cluster: list[tuple[int, str, int]] | None = None, ssl_context=None,
+                 sasl_users: dict[str, str] | None = None):
         """``cluster``: every node of a multi-node test cluster as (node_id, host, port), this one
         included; partition p is led by ``cluster[p % len(cluster)]`` and fetches sent to another
-        node answer NOT_LEADER.  None: a single-node cluster (this server leads everything)."""
+        node answer NOT_LEADER.  None: a single-node cluster (this server leads everything).
+        ``ssl_context``: a server-side ``ssl.SSLContext`` (listeners SSL / SASL_SSL).  ``sasl_users``:
+        {user: password} accepted by SASL/PLAIN; every request but ApiVersions and the SASL exchange
+        closes the connection until it authenticated."""
+        self.ssl_context = ssl_context
+        self.sasl_users = sasl_users
         self.broker = broker
         self.node_id = node_id
         self.cluster = cluster
@@ -159,28 +166,38 @@ class KafkaWireServer:
 
         class Handler(socketserver.BaseRequestHandler):
             def handle(self):
-                self.request.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                sock = self.request
+                sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                if srv.ssl_context is not None:
+                    try:
+                        sock = srv.ssl_context.wrap_socket(sock, server_side=True)
+                    except (OSError, ValueError):
+                        return  # failed TLS handshake (untrusted client / plaintext probe)
                 with srv._lock:
-                    srv._conns.add(self.request)
+                    srv._conns.add(sock)
+                state = {"authed": srv.sasl_users is None}
                 try:
                     while True:
-                        head = _recv_exact(self.request, 4)
+                        head = _recv_exact(sock, 4)
                         if head is None:
                             return
                         (n,) = struct.unpack(">i", head)
-                        req = _recv_exact(self.request, n)
+                        req = _recv_exact(sock, n)
                         if req is None:
                             return
-                        parts = srv._dispatch(req)
+                        parts = srv._dispatch(req, state)
                         if parts is None:
                             return
                         n = sum(len(b) for b in parts)
-                        _sendall_vec(self.request, [struct.pack(">i", n)] + parts)
+                        if srv.ssl_context is not None:
+                            sock.sendall(struct.pack(">i", n) + b"".join(bytes(b) for b in parts))
+                        else:
+                            _sendall_vec(sock, [struct.pack(">i", n)] + parts)
                 except (ConnectionError, OSError):
                     return
                 finally:
                     with srv._lock:
-                        srv._conns.discard(self.request)
+                        srv._conns.discard(sock)
 
         class Server(socketserver.ThreadingTCPServer):
             daemon_threads = True
@@ -237,7 +254,7 @@ class KafkaWireServer:
             v = self._views[pidx] = self.broker.native.log_view(pidx)
         return v
 
-    def _dispatch(self, req: bytes) -> list | None:
+    def _dispatch(self, req: bytes, state: dict | None = None) -> list | None:
         r = _R(req)
         key, ver, corr = r.i16(), r.i16(), r.i32()
         r.str()  # client id
@@ -245,6 +262,28 @@ class KafkaWireServer:
             self.requests[key] = self.requests.get(key, 0) + 1
         w = _W()
         w.i32(corr)
+        state = {"authed": True} if state is None else state
+        if key == API_SASL_HANDSHAKE:
+            mech = r.str()
+            ok = self.sasl_users is not None and mech == "PLAIN"
+            w.i16(NONE if ok else UNSUPPORTED_SASL_MECHANISM)
+            w.i32(1)
+            w.str("PLAIN")
+            state["mech"] = ok
+            return w.data()
+        if key == API_SASL_AUTHENTICATE:
+            n = r.i32()
+            token = r.b[r.o:r.o + n]
+            parts = token.split(b"\0")
+            user, pw = (parts[1].decode(), parts[2].decode()) if len(parts) == 3 else ("", None)
+            ok = bool(state.get("mech")) and self.sasl_users.get(user) == pw
+            state["authed"] = ok
+            w.i16(NONE if ok else SASL_AUTHENTICATION_FAILED)
+            w.str(None if ok else "Authentication failed: invalid username or password")
+            w.bytes(b"")
+            return w.data()
+        if not state["authed"] and key != API_API_VERSIONS:
+            return None  # a SASL listener drops unauthenticated requests
         lo_hi = SUPPORTED.get(key)
         if key == API_API_VERSIONS:
             w.i16(NONE)

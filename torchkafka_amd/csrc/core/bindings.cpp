@@ -128,6 +128,24 @@ class PyLockstepSource : public LockstepSource {
   py::object o_;
 };
 
+// kafka-python-named security settings -> wire::Security
+wire::Security to_security(const py::dict& d) {
+  wire::Security s;
+  auto get = [&](const char* k, std::string* out) {
+    if (d.contains(k) && !d[k].is_none()) *out = d[k].cast<std::string>();
+  };
+  get("security_protocol", &s.protocol);
+  get("ssl_cafile", &s.cafile);
+  get("ssl_certfile", &s.certfile);
+  get("ssl_keyfile", &s.keyfile);
+  get("sasl_mechanism", &s.sasl_mechanism);
+  get("sasl_plain_username", &s.username);
+  get("sasl_plain_password", &s.password);
+  if (d.contains("ssl_check_hostname") && !d["ssl_check_hostname"].is_none())
+    s.check_hostname = d["ssl_check_hostname"].cast<bool>();
+  return s;
+}
+
 py::list wms_to_list(const std::vector<Watermark>& w) {
   py::list l;
   for (const auto& x : w) l.append(py::make_tuple(x.pidx, x.first_offset, x.next_offset, x.count));
@@ -471,8 +489,11 @@ PYBIND11_MODULE(_tkcore, m) {
 
   // ---- Kafka wire protocol (kafka_wire.h) and the cluster -> local log replicator (replicator.h)
   py::class_<wire::Client>(m, "WireClient")
-      .def(py::init<const std::string&, const std::string&, int>(), py::arg("bootstrap"),
-           py::arg("client_id") = "torchkafka", py::arg("timeout_ms") = 30000)
+      .def(py::init([](const std::string& bootstrap, const std::string& client_id, int timeout_ms, py::dict security) {
+             return std::make_unique<wire::Client>(bootstrap, client_id, timeout_ms, to_security(security));
+           }),
+           py::arg("bootstrap"), py::arg("client_id") = "torchkafka", py::arg("timeout_ms") = 30000,
+           py::arg("security") = py::dict())
       .def("metadata",
            [](wire::Client& c, const std::string& topic) {
              wire::TopicMeta t;
@@ -517,7 +538,7 @@ PYBIND11_MODULE(_tkcore, m) {
                        int32_t max_wait_ms, int32_t max_bytes, int32_t partition_max_bytes, int32_t timeout_ms,
                        int64_t max_lag_bytes, int32_t commit_interval_ms, int32_t fetchers, uint64_t log_capacity,
                        uint64_t index_capacity, const std::string& client_id, bool release_consumed,
-                       uint64_t release_bytes, uint64_t release_step, uint64_t ring_bytes) {
+                       uint64_t release_bytes, uint64_t release_step, uint64_t ring_bytes, py::dict security) {
              ReplicaConfig c;
              c.bootstrap = bootstrap;
              c.topic = topic;
@@ -538,6 +559,7 @@ PYBIND11_MODULE(_tkcore, m) {
              c.release_bytes = release_bytes;
              c.release_step = release_step;
              c.ring_bytes = ring_bytes;
+             c.security = to_security(security);
              return std::make_unique<Replicator>(std::move(local), c);
            }),
            py::arg("local"), py::arg("bootstrap"), py::arg("topic"), py::arg("group") = "",
@@ -547,7 +569,8 @@ PYBIND11_MODULE(_tkcore, m) {
            py::arg("commit_interval_ms") = 5, py::arg("fetchers") = 0, py::arg("log_capacity") = 0,
            py::arg("index_capacity") = 0, py::arg("client_id") = "torchkafka-replicator",
            py::arg("release_consumed") = true, py::arg("release_bytes") = uint64_t(256) << 20,
-           py::arg("release_step") = uint64_t(1) << 30, py::arg("ring_bytes") = uint64_t(0))
+           py::arg("release_step") = uint64_t(1) << 30, py::arg("ring_bytes") = uint64_t(0),
+           py::arg("security") = py::dict())
       .def("start", &Replicator::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Replicator::stop, py::arg("flush") = true, py::call_guard<py::gil_scoped_release>())
       .def("flush_commits", &Replicator::flush_commits, py::call_guard<py::gil_scoped_release>())

@@ -7,6 +7,9 @@
 #include <netinet/tcp.h>
 #include <poll.h>
 #include <sys/socket.h>
+#include <openssl/err.h>
+#include <openssl/ssl.h>
+#include <openssl/x509v3.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -103,7 +106,16 @@ int64_t mono_ms() {
 }
 }  // namespace
 
-Conn::Conn(const std::string& host, int port, int timeout_ms)
+namespace {
+std::string ssl_error(const std::string& what) {
+  char buf[256];
+  const unsigned long e = ERR_get_error();
+  ERR_error_string_n(e, buf, sizeof(buf));
+  return what + ": " + (e ? std::string(buf) : std::string("TLS failure"));
+}
+}  // namespace
+
+Conn::Conn(const std::string& host, int port, int timeout_ms, const Security* sec, SSL_CTX* ctx)
     : host_(host), port_(port), timeout_ms_(timeout_ms), buf_(size_t(1) << 16) {
   addrinfo hints{};
   hints.ai_family = AF_UNSPEC;
@@ -132,11 +144,89 @@ Conn::Conn(const std::string& host, int port, int timeout_ms)
   }
   freeaddrinfo(res);
   if (fd_ < 0) throw KafkaError("NoBrokersAvailable: cannot connect to " + host + ":" + ps + " (" + why + ")");
+  if (sec && sec->tls()) {
+    if (!ctx) throw KafkaError("wire: TLS requested without a TLS context");
+    timeval tv{timeout_ms / 1000, (timeout_ms % 1000) * 1000};
+    ::setsockopt(fd_, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));  // bounds the handshake
+    ssl_ = SSL_new(ctx);
+    SSL_set_fd(ssl_, fd_);
+    SSL_set_tlsext_host_name(ssl_, host.c_str());
+    if (sec->check_hostname) {
+      X509_VERIFY_PARAM* vp = SSL_get0_param(ssl_);
+      X509_VERIFY_PARAM_set_hostflags(vp, X509_CHECK_FLAG_NO_PARTIAL_WILDCARDS);
+      X509_VERIFY_PARAM_set1_host(vp, host.c_str(), 0);
+    }
+    if (SSL_connect(ssl_) != 1) {
+      const std::string e = ssl_error("KafkaConnectionError: TLS handshake with " + host + ":" + ps);
+      close();
+      throw KafkaError(e);
+    }
+    timeval none{0, 0};
+    ::setsockopt(fd_, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));
+  }
+  if (sec && sec->sasl()) authenticate(*sec);
+}
+
+void Conn::authenticate(const Security& sec) {
+  if (sec.sasl_mechanism != "PLAIN")
+    throw KafkaError("UnsupportedSaslMechanismError: " + sec.sasl_mechanism + " (this client speaks PLAIN)");
+  Writer hs;
+  hs.str(sec.sasl_mechanism);
+  auto r1 = roundtrip(kSaslHandshake, 1, "torchkafka", hs.data(), timeout_ms_);
+  Reader a(r1.data(), r1.size());
+  const int16_t e1 = a.i16();
+  if (e1 != kNone) {
+    close();
+    throw KafkaError(std::string(error_name(e1)) + ": SaslHandshake " + sec.sasl_mechanism + " refused by " + host_);
+  }
+  std::string token;
+  token.push_back('\0');
+  token += sec.username;
+  token.push_back('\0');
+  token += sec.password;
+  Writer au;
+  au.i32(int32_t(token.size()));
+  au.data().append(token);
+  auto r2 = roundtrip(kSaslAuthenticate, 0, "torchkafka", au.data(), timeout_ms_);
+  Reader b(r2.data(), r2.size());
+  const int16_t e2 = b.i16();
+  const std::string msg = b.str();
+  if (e2 != kNone) {
+    close();
+    throw KafkaError("SaslAuthenticationFailedError: " + (msg.empty() ? std::string(error_name(e2)) : msg));
+  }
+}
+
+ssize_t Conn::io_recv(void* dst, size_t n) {
+  if (!ssl_) return ::recv(fd_, dst, n, 0);
+  const int k = SSL_read(ssl_, dst, int(std::min<size_t>(n, INT32_MAX)));
+  if (k > 0) return k;
+  const int err = SSL_get_error(ssl_, k);
+  if (err == SSL_ERROR_WANT_READ || err == SSL_ERROR_WANT_WRITE) {
+    errno = EAGAIN;
+    return -1;
+  }
+  return k == 0 ? 0 : -1;
+}
+
+bool Conn::wait_readable(int ms) {
+  if (ssl_ && SSL_pending(ssl_) > 0) return true;  // decrypted bytes already buffered
+  pollfd p{fd_, POLLIN, 0};
+  const int r = ::poll(&p, 1, ms);
+  if (r < 0 && errno != EINTR) {
+    close();
+    throw KafkaError("KafkaConnectionError: poll failed");
+  }
+  return r > 0;
 }
 
 Conn::~Conn() { close(); }
 
 void Conn::close() {
+  if (ssl_) {
+    SSL_free(ssl_);
+    ssl_ = nullptr;
+  }
   if (fd_ >= 0) ::close(fd_);
   fd_ = -1;
 }
@@ -144,7 +234,13 @@ void Conn::close() {
 void Conn::send_all(const std::string& frame) {
   size_t off = 0;
   while (off < frame.size()) {
-    const ssize_t n = ::send(fd_, frame.data() + off, frame.size() - off, MSG_NOSIGNAL);
+    const ssize_t n = ssl_ ? ssize_t(SSL_write(ssl_, frame.data() + off, int(frame.size() - off)))
+                           : ::send(fd_, frame.data() + off, frame.size() - off, MSG_NOSIGNAL);
+    if (ssl_ && n <= 0) {
+      const std::string e = ssl_error("KafkaConnectionError: TLS send");
+      close();
+      throw KafkaError(e);
+    }
     if (n < 0) {
       if (errno == EINTR) continue;
       const std::string e = std::strerror(errno);
@@ -195,14 +291,8 @@ void Conn::fill(size_t want) {
       throw KafkaError("KafkaTimeoutError: no response from " + host_ + ":" + std::to_string(port_));
     }
     check_cancel();
-    pollfd p{fd_, POLLIN, 0};
-    const int r = ::poll(&p, 1, int(std::min<int64_t>(left, 100)));
-    if (r < 0 && errno != EINTR) {
-      close();
-      throw KafkaError("KafkaConnectionError: poll failed");
-    }
-    if (r <= 0) continue;
-    const ssize_t n = ::recv(fd_, buf_.data() + b1_, buf_.size() - b1_, 0);
+    if (!wait_readable(int(std::min<int64_t>(left, 100)))) continue;
+    const ssize_t n = io_recv(buf_.data() + b1_, buf_.size() - b1_);
     if (n == 0 || (n < 0 && errno != EINTR && errno != EAGAIN)) {
       close();
       throw KafkaError("KafkaConnectionError: connection to " + host_ + " closed by the broker");
@@ -245,10 +335,8 @@ void Conn::read(void* dst, size_t n) {
       throw KafkaError("KafkaTimeoutError: response from " + host_ + " stalled");
     }
     check_cancel();
-    pollfd p{fd_, POLLIN, 0};
-    const int r = ::poll(&p, 1, int(std::min<int64_t>(left, 100)));
-    if (r <= 0) continue;
-    const ssize_t got = ::recv(fd_, d + off, n - off, 0);
+    if (!wait_readable(int(std::min<int64_t>(left, 100)))) continue;
+    const ssize_t got = io_recv(d + off, n - off);
     if (got == 0 || (got < 0 && errno != EINTR && errno != EAGAIN)) {
       close();
       throw KafkaError("KafkaConnectionError: connection to " + host_ + " closed mid-response");
@@ -320,8 +408,38 @@ std::vector<std::pair<std::string, int>> Client::parse_bootstrap(const std::stri
   return out;
 }
 
-Client::Client(const std::string& bootstrap, const std::string& client_id, int timeout_ms)
-    : bootstrap_(parse_bootstrap(bootstrap)), client_id_(client_id), timeout_ms_(timeout_ms) {}
+Client::Client(const std::string& bootstrap, const std::string& client_id, int timeout_ms, const Security& security)
+    : bootstrap_(parse_bootstrap(bootstrap)), client_id_(client_id), timeout_ms_(timeout_ms), sec_(security) {
+  if (sec_.protocol != "PLAINTEXT" && sec_.protocol != "SSL" && sec_.protocol != "SASL_PLAINTEXT" &&
+      sec_.protocol != "SASL_SSL")
+    throw std::invalid_argument("security_protocol must be PLAINTEXT, SSL, SASL_PLAINTEXT or SASL_SSL");
+  if (!sec_.tls()) return;
+  ctx_ = SSL_CTX_new(TLS_client_method());
+  if (!ctx_) throw KafkaError(ssl_error("wire: SSL_CTX_new"));
+  SSL_CTX_set_min_proto_version(ctx_, TLS1_2_VERSION);
+  SSL_CTX_set_verify(ctx_, SSL_VERIFY_PEER, nullptr);
+  const bool ok = sec_.cafile.empty() ? SSL_CTX_set_default_verify_paths(ctx_) == 1
+                                      : SSL_CTX_load_verify_locations(ctx_, sec_.cafile.c_str(), nullptr) == 1;
+  if (!ok) {
+    SSL_CTX_free(ctx_);
+    ctx_ = nullptr;
+    throw KafkaError(ssl_error("wire: loading ssl_cafile"));
+  }
+  if (!sec_.certfile.empty()) {  // client certificate (mutual TLS)
+    if (SSL_CTX_use_certificate_chain_file(ctx_, sec_.certfile.c_str()) != 1 ||
+        SSL_CTX_use_PrivateKey_file(ctx_, (sec_.keyfile.empty() ? sec_.certfile : sec_.keyfile).c_str(),
+                                    SSL_FILETYPE_PEM) != 1) {
+      SSL_CTX_free(ctx_);
+      ctx_ = nullptr;
+      throw KafkaError(ssl_error("wire: loading ssl_certfile/ssl_keyfile"));
+    }
+  }
+}
+
+Client::~Client() {
+  conns_.clear();  // TLS sessions before their context
+  if (ctx_) SSL_CTX_free(ctx_);
+}
 
 Conn& Client::bootstrap_conn() {
   auto it = conns_.find(-1);
@@ -329,7 +447,7 @@ Conn& Client::bootstrap_conn() {
   std::string why;
   for (auto& [h, p] : bootstrap_) {
     try {
-      conns_[-1] = std::make_unique<Conn>(h, p, timeout_ms_);
+      conns_[-1] = std::make_unique<Conn>(h, p, timeout_ms_, &sec_, ctx_);
       conns_[-1]->set_cancel(cancel_);
       return *conns_[-1];
     } catch (const KafkaError& e) {
@@ -345,7 +463,7 @@ Conn& Client::conn(int32_t node_id) {
   if (it != conns_.end() && it->second->ok()) return *it->second;
   auto nd = nodes_.find(node_id);
   if (nd == nodes_.end()) throw WireError(kLeaderNotAvailable, "wire: unknown broker node " + std::to_string(node_id));
-  conns_[node_id] = std::make_unique<Conn>(nd->second.host, nd->second.port, timeout_ms_);
+  conns_[node_id] = std::make_unique<Conn>(nd->second.host, nd->second.port, timeout_ms_, &sec_, ctx_);
   conns_[node_id]->set_cancel(cancel_);
   return *conns_[node_id];
 }

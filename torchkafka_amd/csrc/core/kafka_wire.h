@@ -16,6 +16,8 @@
 // (rank, worker) as in the rest of the framework, and offsets are committed like kafka-python's
 // manually-assigned consumer with a group_id (generation -1, empty member id).
 #pragma once
+#include <sys/types.h>
+
 #include <atomic>
 #include <cstdint>
 #include <map>
@@ -27,11 +29,27 @@
 
 #include "common.h"
 
+typedef struct ssl_st SSL;
+typedef struct ssl_ctx_st SSL_CTX;
+
 namespace tk::wire {
+
+// Connection security, named as kafka-python's configuration: security_protocol PLAINTEXT | SSL |
+// SASL_PLAINTEXT | SASL_SSL; TLS through OpenSSL (server verified against ssl_cafile, or the
+// system store); SASL mechanism PLAIN (SaslHandshake v1 + SaslAuthenticate v0).
+struct Security {
+  std::string protocol = "PLAINTEXT";
+  std::string cafile, certfile, keyfile;
+  bool check_hostname = true;
+  std::string sasl_mechanism = "PLAIN";
+  std::string username, password;
+  bool tls() const { return protocol == "SSL" || protocol == "SASL_SSL"; }
+  bool sasl() const { return protocol == "SASL_PLAINTEXT" || protocol == "SASL_SSL"; }
+};
 
 enum ApiKey : int16_t {
   kFetch = 1, kListOffsets = 2, kMetadata = 3, kOffsetCommit = 8, kOffsetFetch = 9,
-  kFindCoordinator = 10, kApiVersions = 18,
+  kFindCoordinator = 10, kSaslHandshake = 17, kApiVersions = 18, kSaslAuthenticate = 36,
 };
 
 // Kafka error codes the client acts on.
@@ -40,6 +58,7 @@ enum ErrorCode : int16_t {
   kLeaderNotAvailable = 5, kNotLeaderForPartition = 6, kRequestTimedOut = 7,
   kCoordinatorLoadInProgress = 14, kCoordinatorNotAvailable = 15, kNotCoordinator = 16,
   kIllegalGeneration = 22, kUnknownMemberId = 25, kRebalanceInProgress = 27,
+  kUnsupportedSaslMechanism = 33, kIllegalSaslState = 34, kSaslAuthenticationFailed = 58,
 };
 const char* error_name(int16_t code);
 // Errors after which the partition's leader (or the group's coordinator) must be looked up again.
@@ -90,7 +109,8 @@ class Reader {
 // ------------------------------------------------------------ one TCP connection
 class Conn {
  public:
-  Conn(const std::string& host, int port, int timeout_ms);
+  // sec/ctx: TLS handshake and SASL authentication right after the TCP connect (nullptr: plaintext).
+  Conn(const std::string& host, int port, int timeout_ms, const Security* sec = nullptr, SSL_CTX* ctx = nullptr);
   ~Conn();
   Conn(const Conn&) = delete;
   Conn& operator=(const Conn&) = delete;
@@ -123,6 +143,10 @@ class Conn {
  private:
   void send_all(const std::string& frame);
   void fill(size_t want);  // at least min(want, remaining) bytes buffered
+  ssize_t io_recv(void* dst, size_t n);
+  bool wait_readable(int ms);
+  void authenticate(const Security& sec);
+  SSL* ssl_ = nullptr;
   std::string host_;
   int port_;
   int fd_ = -1;
@@ -163,7 +187,9 @@ struct FetchPartReq {
 class Client {
  public:
   // bootstrap: "host:port[,host:port...]" (an optional "kafka://" prefix is accepted).
-  Client(const std::string& bootstrap, const std::string& client_id, int timeout_ms);
+  Client(const std::string& bootstrap, const std::string& client_id, int timeout_ms,
+         const Security& security = Security());
+  ~Client();
   static std::vector<std::pair<std::string, int>> parse_bootstrap(const std::string& s);
 
   TopicMeta metadata(const std::string& topic);          // refreshes the broker table too
@@ -199,6 +225,8 @@ class Client {
   int32_t coordinator_ = -1;
   std::string coordinator_group_;
   const std::atomic<bool>* cancel_ = nullptr;
+  Security sec_;
+  SSL_CTX* ctx_ = nullptr;
 };
 
 // Encodes a Fetch v4 request body (tests and the replicator share it).

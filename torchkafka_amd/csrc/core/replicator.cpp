@@ -40,7 +40,7 @@ std::string Replicator::last_error() {
 
 void Replicator::start() {
   if (running_.load()) return;
-  wire::Client c(cfg_.bootstrap, cfg_.client_id, cfg_.timeout_ms);
+  wire::Client c(cfg_.bootstrap, cfg_.client_id, cfg_.timeout_ms, cfg_.security);
   wire::TopicMeta t = c.metadata(cfg_.topic);
   if (t.error != wire::kNone || t.partitions.empty())
     throw wire::WireError(t.error ? t.error : int16_t(wire::kUnknownTopicOrPartition),
@@ -122,7 +122,7 @@ void Replicator::start() {
   for (auto& v : per)
     if (!v.empty()) threads_.emplace_back([this, v]() { fetch_loop(v); });
   if (!cfg_.group.empty()) {
-    commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", cfg_.timeout_ms);
+    commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", cfg_.timeout_ms, cfg_.security);
     threads_.emplace_back([this]() { commit_loop(); });
     if (cfg_.release_consumed) threads_.emplace_back([this]() { release_loop(); });
   }
@@ -141,7 +141,7 @@ void Replicator::stop(bool flush) {
     for (int attempt = 0; attempt < 3; ++attempt) {
       try {
         if (!commit_client_)
-          commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", flush_timeout);
+          commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", flush_timeout, cfg_.security);
         forward(*commit_client_);
         break;
       } catch (const KafkaError& e) {
@@ -195,7 +195,7 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
   while (!stop_.load()) {
     try {
       if (!c) {
-        c = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id, cfg_.timeout_ms);
+        c = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id, cfg_.timeout_ms, cfg_.security);
         c->set_cancel(&stop_);
         c->metadata(cfg_.topic);
       }
@@ -339,7 +339,7 @@ int Replicator::forward(wire::Client& c) {
 
 int Replicator::flush_commits() {
   if (cfg_.group.empty()) return 0;
-  wire::Client c(cfg_.bootstrap, cfg_.client_id + "-flush", cfg_.timeout_ms);
+  wire::Client c(cfg_.bootstrap, cfg_.client_id + "-flush", cfg_.timeout_ms, cfg_.security);
   return forward(c);
 }
 
@@ -350,7 +350,7 @@ void Replicator::commit_loop() {
     if (stop_.load()) break;
     try {
       if (!commit_client_) {
-        commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", cfg_.timeout_ms);
+        commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", cfg_.timeout_ms, cfg_.security);
         commit_client_->set_cancel(&stop_);
       }
       forward(*commit_client_);
@@ -416,7 +416,7 @@ bool Replicator::wait_caught_up(int timeout_ms) {
   std::vector<int32_t> ids;
   for (auto& p : parts_) ids.push_back(p->partition);
   if (ids.empty()) return true;
-  wire::Client c(cfg_.bootstrap, cfg_.client_id + "-lag", cfg_.timeout_ms);
+  wire::Client c(cfg_.bootstrap, cfg_.client_id + "-lag", cfg_.timeout_ms, cfg_.security);
   auto hw = c.list_offsets(cfg_.topic, ids, -1);
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
   while (std::chrono::steady_clock::now() < deadline) {

@@ -35,6 +35,7 @@ struct ReplicaConfig {
   std::string topic;
   std::string group;                   // committed offsets: read at start, forwarded on commit
   std::string client_id = "torchkafka-replicator";
+  wire::Security security;             // TLS / SASL (kafka-python's security_protocol, ssl_*, sasl_*)
   std::vector<int32_t> partitions;     // empty: every partition of the topic
   std::string auto_offset_reset = "earliest";  // without a committed offset: earliest | latest
   int32_t max_wait_ms = 100;

@@ -479,14 +479,18 @@ class DeviceLoader:
             servers = ",".join(servers)
         group = wi.kwargs.get("group_id")
         reset = wi.kwargs.get("auto_offset_reset", "latest")  # kafka-python's default
-        client = core().WireClient(servers, "torchkafka-bridge", int(wi.kwargs.get("request_timeout_ms", 30000)))
+        from ..broker.bridge import SECURITY_KEYS, security_config
+
+        security = security_config(**{k: v for k, v in wi.kwargs.items() if k in SECURITY_KEYS})
+        client = core().WireClient(servers, "torchkafka-bridge", int(wi.kwargs.get("request_timeout_ms", 30000)),
+                                   security)
         shares = {}
         for t in topics:
             err, parts = client.metadata(t)
             if err:
                 raise KafkaError(f"UnknownTopicOrPartitionError: topic {t!r} on {servers}")
             shares[t] = shard_partitions(len(parts), self.rank, self.world_size)
-        self._bridge_spec = (servers, group, reset, shares)
+        self._bridge_spec = (servers, group, reset, shares, security)
         url = self._start_bridges(None)
         log.info("DeviceLoader: %s mirrored into %s by %d KafkaBridge(s) (rank %d/%d).", servers, url,
                   len(self._bridges), self.rank, self.world_size)
@@ -497,11 +501,12 @@ class DeviceLoader:
         that name); returns the replica's URL."""
         from ..broker.bridge import KafkaBridge
 
-        servers, group, reset, shares = self._bridge_spec
+        servers, group, reset, shares, security = self._bridge_spec
         first = True
         try:
             for t, mine in shares.items():
-                br = KafkaBridge(servers, t, group_id=group, partitions=mine, url=url, auto_offset_reset=reset)
+                br = KafkaBridge(servers, t, group_id=group, partitions=mine, url=url, auto_offset_reset=reset,
+                                 **security)
                 br._own = first  # the first bridge owns the shared replica broker
                 first = False
                 url = br.url
@@ -1491,8 +1496,8 @@ class DeviceLoader:
             # mirror afresh from them (the replica may not hold those records any more)
             from ..ops.native import core
 
-            servers = self._bridge_spec[0]
-            client = core().WireClient(servers, "torchkafka-bridge", 30000)
+            servers, security = self._bridge_spec[0], self._bridge_spec[4]
+            client = core().WireClient(servers, "torchkafka-bridge", 30000, security)
             for t in sorted({tp.topic for tp in offs}):
                 errs = client.offset_commit(group, t, {tp.partition: o for tp, o in offs.items() if tp.topic == t})
                 bad = {p: e for p, e in errs.items() if e}

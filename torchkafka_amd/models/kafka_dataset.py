@@ -374,7 +374,10 @@ def _bridged_consumer(topics, kwargs):
     wi = get_worker_info()
     wid, nw = (wi.id, wi.num_workers) if wi is not None else (0, 1)
     timeout = int(kwargs.get("request_timeout_ms", 30000))
-    client = core().WireClient(servers, str(kwargs.get("client_id", "torchkafka")), timeout)
+    from ..broker.bridge import SECURITY_KEYS, security_config
+
+    security = security_config(**{k: v for k, v in kwargs.items() if k in SECURITY_KEYS})
+    client = core().WireClient(servers, str(kwargs.get("client_id", "torchkafka")), timeout, security)
     bridges, tps, url = [], [], None
     try:
         for t in topics:
@@ -383,12 +386,14 @@ def _bridged_consumer(topics, kwargs):
                 raise KafkaError(f"UnknownTopicOrPartitionError: topic {t!r} on {servers}")
             mine = shard_partitions(len(parts), rank, world, wid, nw)
             br = KafkaBridge(servers, t, group_id=kwargs.get("group_id"), partitions=mine, url=url,
-                             auto_offset_reset=kwargs.get("auto_offset_reset", "latest"), request_timeout_ms=timeout)
+                             auto_offset_reset=kwargs.get("auto_offset_reset", "latest"), request_timeout_ms=timeout,
+                             **security)
             br._own = url is None
             url = br.url
             bridges.append(br)
             tps += [TopicPartition(t, p) for p in mine]
-        cons = _BridgedConsumer(**{**kwargs, "bootstrap_servers": url})
+        cons = _BridgedConsumer(**{**{k: v for k, v in kwargs.items() if k not in SECURITY_KEYS},
+                                   "bootstrap_servers": url})  # the replica is local: plaintext
         cons._bridges = bridges
         cons.assign(tps)
         # a DataLoader worker ends through multiprocessing's exit hooks, not close(): forward the
