@@ -359,12 +359,40 @@ def _lz4_frame(data: bytes, block=64 << 10) -> bytes:
     return bytes(out)
 
 
-def _compress_batch(batch: bytes, codec: int) -> bytes:
+def _zstd(data: bytes) -> bytes:
+    """zstd frames from the system libzstd (ctypes): two concatenated frames, as a streaming
+    producer that flushes mid-batch leaves them."""
+    import ctypes
+    try:
+        z = ctypes.CDLL("libzstd.so.1")
+    except OSError:
+        pytest.skip("libzstd.so.1 not loadable")
+    z.ZSTD_compressBound.restype = ctypes.c_size_t
+    z.ZSTD_compress.restype = ctypes.c_size_t
+    z.ZSTD_compress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]
+    out = b""
+    for part in (data[:len(data) // 3], data[len(data) // 3:]):
+        cap = z.ZSTD_compressBound(ctypes.c_size_t(len(part)))
+        buf = ctypes.create_string_buffer(cap)
+        n = z.ZSTD_compress(buf, cap, part, len(part), 3)
+        assert n < cap
+        out += buf.raw[:n]
+    return out
+
+
+CODECS = {1: None, 2: _xerial, 3: _lz4_frame, 4: _zstd}
+
+
+def _codec(codec):
     import gzip
+    return gzip.compress if codec == 1 else CODECS[codec]
+
+
+def _compress_batch(batch: bytes, codec: int) -> bytes:
     import struct
 
     records = batch[61:]
-    comp = {1: gzip.compress, 2: _xerial, 3: _lz4_frame}[codec](records)
+    comp = _codec(codec)(records)
     hdr = bytearray(batch[:61])
     attrs = struct.unpack_from(">h", hdr, 21)[0] | codec
     struct.pack_into(">h", hdr, 21, attrs)
@@ -374,24 +402,25 @@ def _compress_batch(batch: bytes, codec: int) -> bytes:
     return bytes(hdr[:21]) + body
 
 
-@pytest.mark.parametrize("codec", [1, 2, 3])
+@pytest.mark.parametrize("codec", [1, 2, 3, 4])
 def test_native_decompressors(codec):
-    import gzip
-
     data = (b"abcabcabcabc" * 300 + bytes(range(256)) * 40 + b"x" * 5000 + os.urandom(3000)) * 3
-    comp = {1: gzip.compress, 2: _xerial, 3: _lz4_frame}[codec](data)
+    comp = _codec(codec)(data)
     assert core().decompress(codec, comp) == data
     assert core().decompress(2, _snappy_raw(data)) == data  # raw snappy (no xerial framing)
     with pytest.raises(Exception, match="corrupt compressed|CRC|Corrupt"):
         core().decompress(codec, comp[: len(comp) // 2])
 
 
-def test_zstd_is_reported_unsupported():
-    with pytest.raises(Exception, match="UnsupportedCodecError: zstd"):
-        core().decompress(4, b"\x28\xb5\x2f\xfd")
+def test_zstd_goes_through_the_system_library():
+    assert core().zstd_available()  # libzstd.so.1 ships with the image
+    with pytest.raises(Exception, match="corrupt compressed"):
+        core().decompress(4, b"\x28\xb5\x2f\xfd")  # bare magic: a truncated frame
+    with pytest.raises(Exception, match="UnsupportedCodecError"):
+        core().decompress(5, b"xyz")
 
 
-@pytest.mark.parametrize("codec", [1, 2, 3])
+@pytest.mark.parametrize("codec", [1, 2, 3, 4])
 def test_compressed_batches_are_inflated_on_ingest(broker, server, codec):
     """A producer's compressed batches reach the replica as plain RecordBatch v2 (fresh CRC), so
     the loader and the device decoders read them like any other batch."""

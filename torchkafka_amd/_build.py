@@ -92,7 +92,7 @@ def build_core(force: bool = False, verbose: bool = False) -> Path:
         jobs.append([cxx, *flags, "-c", str(s), "-o", str(o)])
     _compile_all(jobs)
     tmp = out.with_suffix(".tmp.so")
-    _run([cxx, "-shared", "-o", str(tmp), *map(str, objs), "-lpthread", "-lrt", "-lz", "-lssl", "-lcrypto",
+    _run([cxx, "-shared", "-o", str(tmp), *map(str, objs), "-lpthread", "-lrt", "-lz", "-lssl", "-lcrypto", "-ldl",
           *os.environ.get("TORCHKAFKA_LDFLAGS", "").split()])
     os.replace(tmp, out)
     if verbose:
@@ -138,7 +138,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> Path:
     tmp = out.with_suffix(".tmp.so")
     _run([cc, "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs), f"-L{ROCM}/lib", "-lamdhip64",
           f"-L{t_lib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch", "-ltorch_python",
-          f"-Wl,-rpath,{t_lib}", "-lpthread", "-lrt", "-lz", "-lssl", "-lcrypto"])
+          f"-Wl,-rpath,{t_lib}", "-lpthread", "-lrt", "-lz", "-lssl", "-lcrypto", "-ldl"])
     os.replace(tmp, out)
     if verbose:
         print(f"[torchkafka_amd] built {out.name} for {ARCH}")

@@ -36,9 +36,9 @@ its lifetime.
 Semantics: at-least-once, like the reference's commit-after-batch.  A commit lands in the local
 table synchronously and reaches the cluster within ``commit_interval_ms`` (5 ms); a crash in
 between replays at most that window's batches.  Records are fetched read_uncommitted, control
-batches (transaction markers) are dropped, compressed batches (gzip, snappy, lz4) are CRC-checked
-and stored inflated (the device decoders read raw records); zstd stops its partition with an
-``UnsupportedCodecError``.
+batches (transaction markers) are dropped, compressed batches (gzip, snappy, lz4, zstd) are
+CRC-checked and stored inflated (the device decoders read raw records); zstd needs the system's
+libzstd.so.1 (without it such a batch stops its partition with an ``UnsupportedCodecError``).
 """
 from __future__ import annotations
 

@@ -190,6 +190,7 @@ PYBIND11_MODULE(_tkcore, m) {
     decompress(codec, reinterpret_cast<const uint8_t*>(s.data()), s.size(), out);
     return py::bytes(reinterpret_cast<const char*>(out.data()), out.size());
   });
+  m.def("zstd_available", &zstd_available);
   m.def("crc32c_fold", &crc32c_fold);
   m.def("crc32c_shift_raw", &crc32c_shift_raw, py::arg("raw"), py::arg("n_bytes"));
   m.def(

@@ -1,9 +1,12 @@
 // Kafka record-set decompression: see codecs.h.
 #include "codecs.h"
 
+#include <dlfcn.h>
 #include <zlib.h>
 
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <string>
 
 #include "common.h"
@@ -194,16 +197,71 @@ void unlz4_frame(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
   }
 }
 
+// zstd: the image ships the system's libzstd.so.1 but no header, so the streaming decoder's stable
+// ABI (zstd.h, v1.3+) is declared here and resolved once with dlopen.  Streaming, because producers
+// (librdkafka, the Java client's ZstdOutputStream) may leave the frame content size out.
+struct ZstdIn { const void* src; size_t size; size_t pos; };
+struct ZstdOut { void* dst; size_t size; size_t pos; };
+struct ZstdApi {
+  void* (*create)() = nullptr;
+  size_t (*free_ds)(void*) = nullptr;
+  size_t (*init)(void*) = nullptr;
+  size_t (*stream)(void*, ZstdOut*, ZstdIn*) = nullptr;
+  unsigned (*is_error)(size_t) = nullptr;
+  const char* (*error_name)(size_t) = nullptr;
+  bool ok = false;
+};
+
+const ZstdApi& zstd_api() {
+  static ZstdApi api;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    api.create = reinterpret_cast<void* (*)()>(dlsym(h, "ZSTD_createDStream"));
+    api.free_ds = reinterpret_cast<size_t (*)(void*)>(dlsym(h, "ZSTD_freeDStream"));
+    api.init = reinterpret_cast<size_t (*)(void*)>(dlsym(h, "ZSTD_initDStream"));
+    api.stream = reinterpret_cast<size_t (*)(void*, ZstdOut*, ZstdIn*)>(dlsym(h, "ZSTD_decompressStream"));
+    api.is_error = reinterpret_cast<unsigned (*)(size_t)>(dlsym(h, "ZSTD_isError"));
+    api.error_name = reinterpret_cast<const char* (*)(size_t)>(dlsym(h, "ZSTD_getErrorName"));
+    api.ok = api.create && api.free_ds && api.init && api.stream && api.is_error && api.error_name;
+  });
+  return api;
+}
+
+void unzstd(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
+  const ZstdApi& z = zstd_api();
+  if (!z.ok) throw KafkaError("UnsupportedCodecError: zstd record batches need libzstd.so.1, which is not loadable");
+  std::unique_ptr<void, size_t (*)(void*)> ds(z.create(), z.free_ds);
+  if (!ds || z.is_error(z.init(ds.get()))) bad("zstd init");
+  ZstdIn in{src, n, 0};
+  size_t rc = 1;
+  while (in.pos < in.size || rc != 0) {
+    const size_t old = out.size();
+    out.resize(old + std::max<size_t>(n * 4, 128 << 10));
+    ZstdOut o{out.data() + old, out.size() - old, 0};
+    const size_t in_before = in.pos;
+    rc = z.stream(ds.get(), &o, &in);
+    out.resize(old + o.pos);
+    if (z.is_error(rc)) bad((std::string("zstd: ") + z.error_name(rc)).c_str());
+    // input exhausted mid-frame with no progress: the frame is truncated
+    if (rc != 0 && in.pos == in.size && o.pos == 0 && in.pos == in_before) bad("zstd frame truncated");
+  }
+}
+
 }  // namespace
+
+bool zstd_available() { return zstd_api().ok; }
 
 void decompress(int codec, const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
   switch (codec) {
     case kCodecGzip: gunzip(src, n, out); return;
     case kCodecSnappy: unsnappy(src, n, out); return;
     case kCodecLz4: unlz4_frame(src, n, out); return;
+    case kCodecZstd: unzstd(src, n, out); return;
     default:
       throw KafkaError(std::string("UnsupportedCodecError: ") + codec_name(codec) +
-                       " record batches cannot be decoded by this build (gzip, snappy and lz4 can)");
+                       " record batches cannot be decoded (gzip, snappy, lz4 and zstd can)");
   }
 }
 

@@ -6,8 +6,8 @@
 // (replicator.cpp -> Broker::ingest) inflates a compressed batch once, on arrival, into an
 // uncompressed RecordBatch v2 with a fresh CRC32C (after checking the producer's CRC over the
 // compressed bytes).  gzip goes through zlib; snappy (raw or xerial-framed, as the Java client
-// writes it) and LZ4 (frame format) are decoded here; zstd is not available in this image and
-// raises UnsupportedCodecError.
+// writes it) and LZ4 (frame format) are decoded here; zstd goes through the system libzstd.so.1
+// (dlopen'd; UnsupportedCodecError when it cannot be loaded).
 #pragma once
 #include <cstddef>
 #include <cstdint>
@@ -21,6 +21,7 @@ const char* codec_name(int codec);
 // Appends the decompressed bytes of `src` to `out`.  Throws CorruptRecord on malformed input,
 // KafkaError("UnsupportedCodecError ...") for codecs this build cannot decode.
 void decompress(int codec, const uint8_t* src, size_t n, std::vector<uint8_t>& out);
+bool zstd_available();
 
 // The raw block formats (tests encode with their own minimal compressors).
 void snappy_raw_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& out);
