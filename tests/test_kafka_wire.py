@@ -853,3 +853,83 @@ def test_security_config_validates_the_mechanism():
         {"security_protocol": "SSL"}
     with pytest.raises(ValueError, match="PLAIN"):
         security_config(security_protocol="SASL_SSL", sasl_mechanism="SCRAM-SHA-256")
+
+
+# ---- group membership: subscribe mode (JoinGroup / SyncGroup / Heartbeat / LeaveGroup)
+
+def test_range_assignor_matches_kafkas():
+    got = core().range_assign([("c", ["t"]), ("a", ["t", "u"]), ("b", ["t"])], {"t": 8, "u": 3})
+    assert got == {"a": {"t": [0, 1, 2], "u": [0, 1, 2]}, "b": {"t": [3, 4, 5]}, "c": {"t": [6, 7]}}
+    assert core().range_assign([("a", ["t"]), ("b", ["t"]), ("c", ["t"])], {"t": 2})["c"] == {"t": []}
+
+
+def _start_all(bridges):
+    import threading
+    errs = []
+
+    def go(b):
+        try:
+            b.start()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append(e)
+    ts = [threading.Thread(target=go, args=(b,)) for b in bridges]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(30)
+    assert not errs, errs
+
+
+def test_subscribe_splits_partitions_across_members(broker, server):
+    broker.create_topic("t", 6)
+    broker.fill("t", 200, "fixed_f32", size=8, records_per_batch=20)
+    kw = dict(group_id="g", subscribe=True, heartbeat_interval_ms=100, start=False)
+    bs = [bridge(server, **kw) for _ in range(2)]
+    try:
+        _start_all(bs)
+        a, b = (sorted(x.assignment) for x in bs)
+        assert sorted(a + b) == list(range(6)) and len(a) == len(b) == 3
+        assert bs[0].generation == bs[1].generation >= 1 and bs[0].member_id != bs[1].member_id
+        for x in bs:
+            assert x.wait_caught_up(10)
+            for p in x.assignment:
+                assert log_bytes(x.local, "t", p) == log_bytes(broker, "t", p)
+            others = set(range(6)) - set(x.assignment)
+            assert all(x.local.end_offset("t", p) == 0 for p in others)
+            x.local.commit("g", {TopicPartition("t", p): 150 for p in x.assignment})
+        # commits carry the member's generation and reach the cluster
+        assert wait_for(lambda: broker.committed_offsets("g", "t") == {p: 150 for p in range(6)})
+        stale = core().WireClient(server.address).offset_commit("g", "t", {0: 1}, "", bs[0].generation - 1,
+                                                               bs[0].member_id)
+        assert stale == {0: 22}  # IllegalGeneration: a zombie member is fenced
+        assert len(server.group_members("g")) == 2
+    finally:
+        for x in bs:
+            x.close()
+    assert server.group_members("g") == {}  # both left the group on close
+
+
+def test_a_rebalance_fences_the_old_members(broker, server):
+    broker.create_topic("t", 4)
+    broker.fill("t", 40, "fixed_f32", size=8)
+    kw = dict(group_id="g", subscribe=True, heartbeat_interval_ms=50, session_timeout_ms=1500)
+    first = bridge(server, **kw)
+    try:
+        assert sorted(first.assignment) == [0, 1, 2, 3] and not first.fenced
+        second = bridge(server, **kw)  # its join round waits out the session timeout of `first`
+        try:
+            assert wait_for(lambda: first.fenced, 5)
+            assert "RebalanceInProgress" in first.last_error()
+            assert sorted(second.assignment) == [0, 1, 2, 3] and second.generation == first.generation + 1
+            assert second.wait_caught_up(10)
+        finally:
+            second.close()
+    finally:
+        first.close()
+
+
+def test_subscribe_needs_a_group(broker, server):
+    with pytest.raises(ValueError, match="group_id"):
+        KafkaBridge(server.address, "t", subscribe=True)
+    with pytest.raises(ValueError, match="no partitions"):
+        KafkaBridge(server.address, "t", group_id="g", subscribe=True, partitions=[0])

@@ -81,7 +81,18 @@ class KafkaBridge:
                  security_protocol: str = "PLAINTEXT", ssl_cafile: str | None = None, ssl_check_hostname: bool = True,
                  ssl_certfile: str | None = None, ssl_keyfile: str | None = None, sasl_mechanism: str | None = None,
                  sasl_plain_username: str | None = None, sasl_plain_password: str | None = None,
+                 subscribe: bool = False, session_timeout_ms: int = 10000, heartbeat_interval_ms: int = 3000,
                  start: bool = True):
+        """``subscribe=True`` (needs ``group_id``, excludes ``partitions``): join the consumer group
+        like kafka-python's ``subscribe()`` -- JoinGroup/SyncGroup with the range assignor -- and
+        mirror the partitions the coordinator assigns (:attr:`assignment`).  Membership is fixed
+        for the bridge's lifetime: when the group rebalances the bridge stops fetching and
+        forwarding (:attr:`fenced`, RebalanceInProgressError in :meth:`last_error`) and the job
+        re-shards by restarting.  Default: the static ``partitions`` (kafka-python's ``assign()``)."""
+        if subscribe and not group_id:
+            raise ValueError("subscribe=True needs a group_id")
+        if subscribe and partitions is not None:
+            raise ValueError("subscribe=True assigns partitions through the group: pass no partitions")
         if not isinstance(bootstrap_servers, str):
             bootstrap_servers = ",".join(bootstrap_servers)
         self.bootstrap_servers = bootstrap_servers
@@ -107,7 +118,9 @@ class KafkaBridge:
                                      ssl_check_hostname=ssl_check_hostname, ssl_certfile=ssl_certfile,
                                      ssl_keyfile=ssl_keyfile, sasl_mechanism=sasl_mechanism,
                                      sasl_plain_username=sasl_plain_username,
-                                     sasl_plain_password=sasl_plain_password))
+                                     sasl_plain_password=sasl_plain_password),
+            subscribe=bool(subscribe), session_timeout_ms=int(session_timeout_ms),
+            heartbeat_interval_ms=int(heartbeat_interval_ms))
         self._closed = False
         self._lock = threading.Lock()
         self._reported = 0
@@ -162,6 +175,24 @@ class KafkaBridge:
 
     def stats(self) -> list[dict]:
         return list(self._r.stats())
+
+    @property
+    def assignment(self) -> list[int]:
+        """The partitions this bridge mirrors (subscribe mode: what the coordinator assigned)."""
+        return list(self._r.assignment) if self._r.member_id else [s["partition"] for s in self.stats()]
+
+    @property
+    def member_id(self) -> str:
+        return str(self._r.member_id)
+
+    @property
+    def generation(self) -> int:
+        return int(self._r.generation)
+
+    @property
+    def fenced(self) -> bool:
+        """Subscribe mode: the group rebalanced under this bridge (it stopped fetching and committing)."""
+        return bool(self._r.fenced)
 
     @property
     def errors(self) -> int:

@@ -23,17 +23,21 @@ import socketserver
 import struct
 import threading
 import time
+import uuid
 
 from .synthetic import SyntheticBroker
 
 API_FETCH, API_LIST_OFFSETS, API_METADATA = 1, 2, 3
 API_OFFSET_COMMIT, API_OFFSET_FETCH, API_FIND_COORDINATOR, API_API_VERSIONS = 8, 9, 10, 18
 # api key -> (min, max) version served
+API_JOIN_GROUP, API_HEARTBEAT, API_LEAVE_GROUP, API_SYNC_GROUP = 11, 12, 13, 14
 SUPPORTED = {API_FETCH: (4, 4), API_LIST_OFFSETS: (0, 1), API_METADATA: (0, 1), API_OFFSET_COMMIT: (2, 2),
-             API_OFFSET_FETCH: (1, 1), API_FIND_COORDINATOR: (0, 0), API_API_VERSIONS: (0, 0)}
+             API_OFFSET_FETCH: (1, 1), API_FIND_COORDINATOR: (0, 0), API_API_VERSIONS: (0, 0),
+             API_JOIN_GROUP: (0, 0), API_HEARTBEAT: (0, 0), API_LEAVE_GROUP: (0, 0), API_SYNC_GROUP: (0, 0)}
 
 NONE, OFFSET_OUT_OF_RANGE, UNKNOWN_TOPIC, NOT_LEADER, UNSUPPORTED_VERSION = 0, 1, 3, 6, 35
 ILLEGAL_GENERATION, UNSUPPORTED_SASL_MECHANISM, SASL_AUTHENTICATION_FAILED = 22, 33, 58
+UNKNOWN_MEMBER_ID, REBALANCE_IN_PROGRESS = 25, 27
 API_SASL_HANDSHAKE, API_SASL_AUTHENTICATE = 17, 36
 
 
@@ -137,6 +141,20 @@ def _varint(v: int) -> bytes:
     return bytes(out)
 
 
+class _Group:
+    """A consumer group's membership as the coordinator sees it."""
+
+    def __init__(self):
+        self.state = "empty"   # empty | joining | syncing | stable
+        self.generation = 0
+        self.members: dict[str, bytes] = {}   # member id -> subscription metadata (this generation)
+        self.joining: dict[str, bytes] = {}   # the round in progress
+        self.leader = ""
+        self.protocol = ""
+        self.assignments: dict[str, bytes] = {}
+        self.min_end = self.deadline = 0.0
+
+
 class KafkaWireServer:
     """Serves a :class:`SyntheticBroker` over the Kafka protocol on ``host:port`` (0: a free port)."""
 
@@ -162,6 +180,9 @@ class KafkaWireServer:
         self.requests: dict[int, int] = {}  # api key -> count
         self._views: dict[int, memoryview] = {}
         self._conns: set = set()
+        self._groups: dict[str, _Group] = {}
+        self._gcond = threading.Condition()
+        self.join_delay_s = 0.3            # group.initial.rebalance.delay.ms of a fresh group
         srv = self
 
         class Handler(socketserver.BaseRequestHandler):
@@ -458,11 +479,138 @@ class KafkaWireServer:
         w.str(self.host)
         w.i32(self.port)
 
+    # ------------------------------------------------------------ group membership (coordinator)
+    # JoinGroup / SyncGroup / Heartbeat / LeaveGroup v0 with Kafka's state machine, reduced to what
+    # a test needs: a join round ends once every member of the last generation rejoined (a fresh
+    # group waits ``join_delay_s`` for more joiners) or after the rebalance timeout, which drops
+    # the absentees; the first joiner leads and sends the assignment through SyncGroup.
+    def _group(self, name: str) -> "_Group":
+        g = self._groups.get(name)
+        if g is None:
+            g = self._groups[name] = _Group()
+        return g
+
+    def _begin_round(self, g: "_Group", timeout_s: float) -> None:
+        if g.state != "joining":
+            g.state, g.joining = "joining", {}
+            now = time.monotonic()
+            g.min_end = now + (self.join_delay_s if not g.members else 0.0)
+            g.deadline = now + max(timeout_s, self.join_delay_s)
+
+    def _api_11(self, r: _R, ver: int, w: _W) -> None:  # JoinGroup v0 (blocks until the round ends)
+        group, session_ms, member, _ptype = r.str(), r.i32(), r.str() or "", r.str()
+        protos: list[tuple[str, bytes]] = []
+        for _ in range(r.i32()):
+            name = r.str()
+            n = r.i32()
+            protos.append((name, bytes(r.b[r.o:r.o + n])))
+            r.o += n
+        with self._gcond:
+            g = self._group(group)
+            if member and member not in g.members and member not in g.joining:
+                self._join_reply(w, UNKNOWN_MEMBER_ID, -1, "", "", member, {})
+                return
+            member = member or f"member-{uuid.uuid4().hex[:12]}"
+            self._begin_round(g, session_ms / 1000.0)
+            g.joining[member] = protos[0][1] if protos else b""
+            g.protocol = protos[0][0] if protos else ""
+            gen0 = g.generation
+            self._gcond.notify_all()
+            while g.generation == gen0:
+                now = time.monotonic()
+                done = set(g.members) <= set(g.joining) and now >= g.min_end
+                if done or now >= g.deadline:
+                    g.generation += 1
+                    g.members = dict(g.joining)
+                    g.leader = next(iter(g.joining))
+                    g.state, g.assignments = "syncing", {}
+                    self._gcond.notify_all()
+                    break
+                self._gcond.wait(0.01)
+            if member not in g.members:  # joined after the round closed: rejoin
+                self._join_reply(w, REBALANCE_IN_PROGRESS, -1, "", "", member, {})
+                return
+            self._join_reply(w, NONE, g.generation, g.protocol, g.leader, member,
+                             g.members if member == g.leader else {})
+
+    @staticmethod
+    def _join_reply(w: _W, err, gen, proto, leader, member, members) -> None:
+        w.i16(err)
+        w.i32(gen)
+        w.str(proto)
+        w.str(leader)
+        w.str(member)
+        w.i32(len(members))
+        for m, meta in members.items():
+            w.str(m)
+            w.bytes(meta)
+
+    def _member_error(self, g: "_Group | None", gen: int, member: str) -> int:
+        if g is None or member not in g.members:
+            return UNKNOWN_MEMBER_ID
+        if gen != g.generation:
+            return ILLEGAL_GENERATION
+        return NONE
+
+    def _api_14(self, r: _R, ver: int, w: _W) -> None:  # SyncGroup v0
+        group, gen, member = r.str(), r.i32(), r.str() or ""
+        assign = {}
+        for _ in range(r.i32()):
+            m = r.str()
+            n = r.i32()
+            assign[m] = bytes(r.b[r.o:r.o + n])
+            r.o += n
+        with self._gcond:
+            g = self._groups.get(group)
+            err = self._member_error(g, gen, member)
+            if err == NONE and member == g.leader:
+                g.assignments, g.state = assign, "stable"
+                self._gcond.notify_all()
+            deadline = time.monotonic() + 30
+            while err == NONE and g.state == "syncing" and g.generation == gen and time.monotonic() < deadline:
+                self._gcond.wait(0.01)
+            if err == NONE and (g.generation != gen or g.state != "stable"):
+                err = REBALANCE_IN_PROGRESS
+            w.i16(err)
+            w.bytes(g.assignments.get(member, b"") if err == NONE else b"")
+
+    def _api_12(self, r: _R, ver: int, w: _W) -> None:  # Heartbeat v0
+        group, gen, member = r.str(), r.i32(), r.str() or ""
+        with self._gcond:
+            g = self._groups.get(group)
+            err = self._member_error(g, gen, member)
+            if err == NONE and g.state == "joining":
+                err = REBALANCE_IN_PROGRESS
+            w.i16(err)
+
+    def _api_13(self, r: _R, ver: int, w: _W) -> None:  # LeaveGroup v0
+        group, member = r.str(), r.str() or ""
+        with self._gcond:
+            g = self._groups.get(group)
+            if g is None or member not in g.members:
+                w.i16(UNKNOWN_MEMBER_ID)
+                return
+            del g.members[member]
+            if g.members:
+                self._begin_round(g, 10.0)  # the others learn it from their next heartbeat
+            else:
+                g.state = "empty"
+            self._gcond.notify_all()
+            w.i16(NONE)
+
+    def group_members(self, group: str) -> dict[str, bytes]:
+        """{member id: assignment} of a group's current generation (tests)."""
+        with self._gcond:
+            g = self._groups.get(group)
+            return {} if g is None else {m: g.assignments.get(m, b"") for m in g.members}
+
     def _api_8(self, r: _R, ver: int, w: _W) -> None:  # OffsetCommit v2
         group = r.str()
-        r.i32()   # generation
-        r.str()   # member
+        gen = r.i32()
+        member = r.str() or ""
         r.i64()   # retention
+        with self._gcond:
+            fenced = NONE if gen == -1 else self._member_error(self._groups.get(group), gen, member)
         nat = self.broker.native
         g = nat.group_index(group, True)
         nt = r.i32()
@@ -476,7 +624,7 @@ class KafkaWireServer:
                 p, off = r.i32(), r.i64()
                 meta = r.str() or ""
                 with self._lock:
-                    err = self._commit_faults.pop(0) if self._commit_faults else NONE
+                    err = self._commit_faults.pop(0) if self._commit_faults else fenced
                 if err == NONE:
                     try:
                         nat.commit(g, -1, 0, 0, [(self.broker.pidx(name, p), int(off), meta)])

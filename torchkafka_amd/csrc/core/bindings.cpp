@@ -191,6 +191,16 @@ PYBIND11_MODULE(_tkcore, m) {
     return py::bytes(reinterpret_cast<const char*>(out.data()), out.size());
   });
   m.def("zstd_available", &zstd_available);
+  // Kafka's range assignor over (member id, subscribed topics): {member: {topic: [partitions]}}
+  m.def("range_assign", [](const std::vector<std::pair<std::string, std::vector<std::string>>>& members,
+                           const std::map<std::string, int32_t>& counts) {
+    std::vector<std::pair<std::string, std::string>> ms;
+    for (auto& [m, topics] : members) ms.emplace_back(m, wire::encode_subscription(topics));
+    auto out = wire::range_assign(ms, counts);
+    std::map<std::string, wire::Assignment> back;
+    for (auto& [m, a] : out) back[m] = wire::decode_assignment(wire::encode_assignment(a));
+    return back;
+  });
   m.def("crc32c_fold", &crc32c_fold);
   m.def("crc32c_shift_raw", &crc32c_shift_raw, py::arg("raw"), py::arg("n_bytes"));
   m.def(
@@ -515,7 +525,10 @@ PYBIND11_MODULE(_tkcore, m) {
       .def("list_offsets", &wire::Client::list_offsets, py::call_guard<py::gil_scoped_release>())
       .def("offset_fetch", &wire::Client::offset_fetch, py::call_guard<py::gil_scoped_release>())
       .def("offset_commit", &wire::Client::offset_commit, py::arg("group"), py::arg("topic"), py::arg("offsets"),
-           py::arg("metadata") = "", py::call_guard<py::gil_scoped_release>())
+           py::arg("metadata") = "", py::arg("generation") = -1, py::arg("member_id") = "",
+           py::call_guard<py::gil_scoped_release>())
+      .def("heartbeat", &wire::Client::heartbeat, py::call_guard<py::gil_scoped_release>())
+      .def("leave_group", &wire::Client::leave_group, py::call_guard<py::gil_scoped_release>())
       .def_static("parse_bootstrap", &wire::Client::parse_bootstrap);
 
   py::class_<WireServer>(m, "WireServer")
@@ -539,8 +552,12 @@ PYBIND11_MODULE(_tkcore, m) {
                        int32_t max_wait_ms, int32_t max_bytes, int32_t partition_max_bytes, int32_t timeout_ms,
                        int64_t max_lag_bytes, int32_t commit_interval_ms, int32_t fetchers, uint64_t log_capacity,
                        uint64_t index_capacity, const std::string& client_id, bool release_consumed,
-                       uint64_t release_bytes, uint64_t release_step, uint64_t ring_bytes, py::dict security) {
+                       uint64_t release_bytes, uint64_t release_step, uint64_t ring_bytes, py::dict security,
+                       bool subscribe, int32_t session_timeout_ms, int32_t heartbeat_interval_ms) {
              ReplicaConfig c;
+             c.subscribe = subscribe;
+             c.session_timeout_ms = session_timeout_ms;
+             c.heartbeat_interval_ms = heartbeat_interval_ms;
              c.bootstrap = bootstrap;
              c.topic = topic;
              c.group = group;
@@ -571,7 +588,8 @@ PYBIND11_MODULE(_tkcore, m) {
            py::arg("index_capacity") = 0, py::arg("client_id") = "torchkafka-replicator",
            py::arg("release_consumed") = true, py::arg("release_bytes") = uint64_t(256) << 20,
            py::arg("release_step") = uint64_t(1) << 30, py::arg("ring_bytes") = uint64_t(0),
-           py::arg("security") = py::dict())
+           py::arg("security") = py::dict(), py::arg("subscribe") = false, py::arg("session_timeout_ms") = 10000,
+           py::arg("heartbeat_interval_ms") = 3000)
       .def("start", &Replicator::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Replicator::stop, py::arg("flush") = true, py::call_guard<py::gil_scoped_release>())
       .def("flush_commits", &Replicator::flush_commits, py::call_guard<py::gil_scoped_release>())
@@ -580,6 +598,10 @@ PYBIND11_MODULE(_tkcore, m) {
       .def_property_readonly("errors", &Replicator::errors)
       .def_property_readonly("first_pidx", &Replicator::first_pidx)
       .def_property_readonly("n_partitions", &Replicator::n_partitions)
+      .def_property_readonly("member_id", &Replicator::member_id)
+      .def_property_readonly("generation", &Replicator::generation)
+      .def_property_readonly("assignment", &Replicator::assignment)
+      .def_property_readonly("fenced", &Replicator::fenced)
       .def("last_error", &Replicator::last_error)
       .def("stats", [](Replicator& r) {
         py::list l;

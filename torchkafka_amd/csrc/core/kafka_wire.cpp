@@ -625,13 +625,169 @@ std::map<int32_t, int64_t> Client::offset_fetch(const std::string& group, const 
   return out;
 }
 
-std::map<int32_t, int16_t> Client::offset_commit(const std::string& group, const std::string& topic,
-                                                 const std::map<int32_t, int64_t>& offsets,
-                                                 const std::string& metadata) {
+std::vector<uint8_t> Client::coordinator_roundtrip(const std::string& group, int16_t key, int16_t version,
+                                                  const std::string& body, int timeout_ms) {
+  const int32_t node = coordinator(group);
+  try {
+    return conn(node).roundtrip(key, version, client_id_, body, timeout_ms);
+  } catch (const KafkaError&) {
+    drop(node);
+    invalidate_coordinator();
+    throw;
+  }
+}
+
+JoinResult Client::join_group(const std::string& group, int32_t session_timeout_ms, const std::string& member_id,
+                              const std::string& subscription) {
   Writer w;
   w.str(group);
-  w.i32(-1);      // generation: a manually assigned ("simple") consumer
-  w.str("");      // member id
+  w.i32(session_timeout_ms);
+  w.str(member_id);
+  w.str("consumer");
+  w.array(1);
+  w.str("range");
+  w.i32(int32_t(subscription.size()));
+  w.data() += subscription;
+  // the coordinator holds the request until the join round ends
+  auto resp = coordinator_roundtrip(group, kJoinGroup, 0, w.data(), timeout_ms_ + session_timeout_ms);
+  Reader r(resp.data(), resp.size());
+  JoinResult j;
+  j.error = r.i16();
+  j.generation = r.i32();
+  j.protocol = r.str();
+  j.leader = r.str();
+  j.member_id = r.str();
+  const int32_t n = r.i32();
+  for (int32_t i = 0; i < n; ++i) {
+    std::string m = r.str();
+    int32_t len = 0;
+    const uint8_t* p = r.bytes(&len);
+    j.members.emplace_back(std::move(m), len > 0 ? std::string(reinterpret_cast<const char*>(p), size_t(len)) : "");
+  }
+  if (needs_metadata(j.error)) invalidate_coordinator();
+  return j;
+}
+
+std::pair<int16_t, std::string> Client::sync_group(const std::string& group, int32_t generation,
+                                                   const std::string& member_id,
+                                                   const std::map<std::string, std::string>& assignments) {
+  Writer w;
+  w.str(group);
+  w.i32(generation);
+  w.str(member_id);
+  w.array(int32_t(assignments.size()));
+  for (auto& [m, a] : assignments) {
+    w.str(m);
+    w.i32(int32_t(a.size()));
+    w.data() += a;
+  }
+  auto resp = coordinator_roundtrip(group, kSyncGroup, 0, w.data(), timeout_ms_ * 2);
+  Reader r(resp.data(), resp.size());
+  const int16_t e = r.i16();
+  int32_t len = 0;
+  const uint8_t* p = r.bytes(&len);
+  if (needs_metadata(e)) invalidate_coordinator();
+  return {e, len > 0 ? std::string(reinterpret_cast<const char*>(p), size_t(len)) : std::string()};
+}
+
+int16_t Client::heartbeat(const std::string& group, int32_t generation, const std::string& member_id) {
+  Writer w;
+  w.str(group);
+  w.i32(generation);
+  w.str(member_id);
+  auto resp = coordinator_roundtrip(group, kHeartbeat, 0, w.data(), timeout_ms_);
+  Reader r(resp.data(), resp.size());
+  const int16_t e = r.i16();
+  if (needs_metadata(e)) invalidate_coordinator();
+  return e;
+}
+
+int16_t Client::leave_group(const std::string& group, const std::string& member_id) {
+  Writer w;
+  w.str(group);
+  w.str(member_id);
+  auto resp = coordinator_roundtrip(group, kLeaveGroup, 0, w.data(), timeout_ms_);
+  Reader r(resp.data(), resp.size());
+  return r.i16();
+}
+
+std::string encode_subscription(const std::vector<std::string>& topics) {
+  Writer w;
+  w.i16(0);  // version
+  w.array(int32_t(topics.size()));
+  for (auto& t : topics) w.str(t);
+  w.i32(-1);  // user data: null
+  return w.data();
+}
+
+std::vector<std::string> decode_subscription(const std::string& metadata) {
+  Reader r(reinterpret_cast<const uint8_t*>(metadata.data()), metadata.size());
+  r.i16();
+  std::vector<std::string> out(size_t(std::max(0, r.i32())));
+  for (auto& t : out) t = r.str();
+  return out;
+}
+
+std::string encode_assignment(const Assignment& a) {
+  Writer w;
+  w.i16(0);
+  w.array(int32_t(a.size()));
+  for (auto& [t, ps] : a) {
+    w.str(t);
+    w.array(int32_t(ps.size()));
+    for (int32_t p : ps) w.i32(p);
+  }
+  w.i32(-1);
+  return w.data();
+}
+
+Assignment decode_assignment(const std::string& bytes) {
+  Assignment a;
+  if (bytes.size() < 2) return a;  // an empty assignment
+  Reader r(reinterpret_cast<const uint8_t*>(bytes.data()), bytes.size());
+  r.i16();
+  const int32_t nt = r.i32();
+  for (int32_t i = 0; i < nt; ++i) {
+    std::string t = r.str();
+    auto& ps = a[t];
+    const int32_t np = r.i32();
+    for (int32_t j = 0; j < np; ++j) ps.push_back(r.i32());
+  }
+  return a;
+}
+
+std::map<std::string, Assignment> range_assign(const std::vector<std::pair<std::string, std::string>>& members,
+                                               const std::map<std::string, int32_t>& partitions_per_topic) {
+  std::map<std::string, Assignment> out;
+  std::map<std::string, std::vector<std::string>> subscribers;  // topic -> member ids (sorted: std::map order)
+  std::map<std::string, std::vector<std::string>> subs;
+  for (auto& [m, meta] : members) {
+    out[m];
+    subs[m] = decode_subscription(meta);
+  }
+  for (auto& [m, topics] : subs)
+    for (auto& t : topics) subscribers[t].push_back(m);
+  for (auto& [t, ms] : subscribers) {
+    auto it = partitions_per_topic.find(t);
+    if (it == partitions_per_topic.end() || ms.empty()) continue;
+    const int32_t P = it->second, C = int32_t(ms.size()), per = P / C, extra = P % C;
+    for (int32_t i = 0; i < C; ++i) {
+      const int32_t start = per * i + std::min(i, extra), len = per + (i < extra ? 1 : 0);
+      auto& ps = out[ms[size_t(i)]][t];
+      for (int32_t p = start; p < start + len; ++p) ps.push_back(p);
+    }
+  }
+  return out;
+}
+
+std::map<int32_t, int16_t> Client::offset_commit(const std::string& group, const std::string& topic,
+                                                 const std::map<int32_t, int64_t>& offsets,
+                                                 const std::string& metadata, int32_t generation,
+                                                 const std::string& member_id) {
+  Writer w;
+  w.str(group);
+  w.i32(generation);  // -1 with an empty member id: a manually assigned ("simple") consumer
+  w.str(member_id);
   w.i64(-1);      // retention: the broker's default
   w.array(1);
   w.str(topic);

@@ -11,10 +11,12 @@
 //
 // Protocol subset (non-flexible request versions, understood by Kafka 0.11 .. 3.x brokers):
 //   ApiVersions v0, Metadata v1, ListOffsets v1, Fetch v4 (RecordBatch v2, read_uncommitted),
-//   FindCoordinator v0, OffsetCommit v2, OffsetFetch v1.
-// Group membership (JoinGroup/SyncGroup) is not used: partitions are assigned statically by
-// (rank, worker) as in the rest of the framework, and offsets are committed like kafka-python's
-// manually-assigned consumer with a group_id (generation -1, empty member id).
+//   FindCoordinator v0, OffsetCommit v2, OffsetFetch v1; group membership (subscribe mode):
+//   JoinGroup v0, SyncGroup v0, Heartbeat v0, LeaveGroup v0 with the "consumer" protocol and
+//   Kafka's range assignor.
+// By default partitions are assigned statically by (rank, worker) as in the rest of the
+// framework, and offsets are committed like kafka-python's manually-assigned consumer with a
+// group_id (generation -1, empty member id).
 #pragma once
 #include <sys/types.h>
 
@@ -49,7 +51,7 @@ struct Security {
 
 enum ApiKey : int16_t {
   kFetch = 1, kListOffsets = 2, kMetadata = 3, kOffsetCommit = 8, kOffsetFetch = 9,
-  kFindCoordinator = 10, kSaslHandshake = 17, kApiVersions = 18, kSaslAuthenticate = 36,
+  kFindCoordinator = 10, kJoinGroup = 11, kHeartbeat = 12, kLeaveGroup = 13, kSyncGroup = 14, kSaslHandshake = 17, kApiVersions = 18, kSaslAuthenticate = 36,
 };
 
 // Kafka error codes the client acts on.
@@ -178,6 +180,25 @@ struct TopicMeta {
   std::vector<PartitionMeta> partitions;  // sorted by partition id
 };
 
+// JoinGroup v0 response; `members` (member id, subscription metadata) is filled for the leader only.
+struct JoinResult {
+  int16_t error = 0;
+  int32_t generation = -1;
+  std::string protocol, leader, member_id;
+  std::vector<std::pair<std::string, std::string>> members;
+};
+using Assignment = std::map<std::string, std::vector<int32_t>>;  // topic -> partitions
+
+// Consumer protocol v0 (ConsumerProtocolSubscription / ConsumerProtocolAssignment).
+std::string encode_subscription(const std::vector<std::string>& topics);
+std::vector<std::string> decode_subscription(const std::string& metadata);
+std::string encode_assignment(const Assignment& a);
+Assignment decode_assignment(const std::string& bytes);
+// Kafka's RangeAssignor: per topic, the subscribed members sorted by id take contiguous ranges,
+// the first (P % members) one partition more.  members: (id, subscription metadata).
+std::map<std::string, Assignment> range_assign(const std::vector<std::pair<std::string, std::string>>& members,
+                                               const std::map<std::string, int32_t>& partitions_per_topic);
+
 struct FetchPartReq {
   int32_t partition;
   int64_t offset;
@@ -202,7 +223,17 @@ class Client {
   // Returns per-partition error codes (0 = committed).
   std::map<int32_t, int16_t> offset_commit(const std::string& group, const std::string& topic,
                                            const std::map<int32_t, int64_t>& offsets,
-                                           const std::string& metadata = "");
+                                           const std::string& metadata = "", int32_t generation = -1,
+                                           const std::string& member_id = "");
+  // Group membership against the group's coordinator.  join_group blocks at the coordinator
+  // until the join round ends (up to the session timeout).
+  JoinResult join_group(const std::string& group, int32_t session_timeout_ms, const std::string& member_id,
+                        const std::string& subscription);
+  std::pair<int16_t, std::string> sync_group(const std::string& group, int32_t generation,
+                                             const std::string& member_id,
+                                             const std::map<std::string, std::string>& assignments);
+  int16_t heartbeat(const std::string& group, int32_t generation, const std::string& member_id);
+  int16_t leave_group(const std::string& group, const std::string& member_id);
   void invalidate_coordinator() { coordinator_ = -1; }
   void set_cancel(const std::atomic<bool>* flag) { cancel_ = flag; }  // every connection of this client
 
@@ -216,6 +247,8 @@ class Client {
  private:
   Conn& bootstrap_conn();
   int32_t coordinator(const std::string& group);
+  std::vector<uint8_t> coordinator_roundtrip(const std::string& group, int16_t key, int16_t version,
+                                             const std::string& body, int timeout_ms);
   std::vector<std::pair<std::string, int>> bootstrap_;
   std::string client_id_;
   int timeout_ms_;

@@ -9,6 +9,9 @@ namespace tk {
 
 namespace {
 void sleep_ms(int ms) { std::this_thread::sleep_for(std::chrono::milliseconds(ms)); }
+int64_t now_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 }  // namespace
 
 Replicator::Replicator(std::shared_ptr<Broker> local, ReplicaConfig cfg) : local_(std::move(local)), cfg_(std::move(cfg)) {
@@ -57,8 +60,12 @@ void Replicator::start() {
     throw std::invalid_argument("replicator: ring_bytes must hold at least 4 x partition_max_bytes");
   if (cfg_.ring_bytes) cfg_.release_consumed = false;  // a ring reuses its pages: nothing to free
   if (cfg_.release_consumed && !cfg_.group.empty()) local_->set_flags(kReleaseConsumed);
-  std::vector<int32_t> ids = cfg_.partitions;
-  if (ids.empty())
+  if (cfg_.subscribe) {
+    if (cfg_.group.empty()) throw std::invalid_argument("replicator: subscribe mode needs a group");
+    join_group(c);
+  }
+  std::vector<int32_t> ids = cfg_.subscribe ? assigned_ : cfg_.partitions;
+  if (ids.empty() && !cfg_.subscribe)
     for (auto& p : t.partitions) ids.push_back(p.partition);
   std::sort(ids.begin(), ids.end());
   ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
@@ -128,6 +135,64 @@ void Replicator::start() {
   }
 }
 
+void Replicator::join_group(wire::Client& c) {
+  const std::string sub = wire::encode_subscription({cfg_.topic});
+  for (int attempt = 0; attempt < 8; ++attempt) {
+    wire::JoinResult j = c.join_group(cfg_.group, cfg_.session_timeout_ms, member_id_, sub);
+    if (j.error == wire::kUnknownMemberId) {
+      member_id_.clear();
+      continue;
+    }
+    if (j.error == wire::kRebalanceInProgress || wire::needs_metadata(j.error)) {
+      sleep_ms(20 << std::min(attempt, 5));
+      continue;
+    }
+    if (j.error != wire::kNone)
+      throw wire::WireError(j.error, std::string(wire::error_name(j.error)) + ": JoinGroup '" + cfg_.group + "'");
+    member_id_ = j.member_id;
+    std::map<std::string, std::string> plan;
+    if (j.leader == j.member_id) {  // the leader assigns every member's subscription
+      std::map<std::string, int32_t> counts;
+      for (auto& [m, meta] : j.members)
+        for (auto& topic : wire::decode_subscription(meta))
+          if (!counts.count(topic)) {
+            wire::TopicMeta tm = c.metadata(topic);
+            counts[topic] = tm.error ? 0 : int32_t(tm.partitions.size());
+          }
+      for (auto& [m, a] : wire::range_assign(j.members, counts)) plan[m] = wire::encode_assignment(a);
+    }
+    auto [e, bytes] = c.sync_group(cfg_.group, j.generation, member_id_, plan);
+    if (e == wire::kRebalanceInProgress || e == wire::kIllegalGeneration || wire::needs_metadata(e)) {
+      sleep_ms(20 << std::min(attempt, 5));
+      continue;
+    }
+    if (e != wire::kNone)
+      throw wire::WireError(e, std::string(wire::error_name(e)) + ": SyncGroup '" + cfg_.group + "'");
+    generation_ = j.generation;
+    assigned_ = wire::decode_assignment(bytes)[cfg_.topic];
+    last_heartbeat_ms_ = now_ms();
+    return;
+  }
+  throw KafkaError("replicator: group '" + cfg_.group + "' did not settle (JoinGroup/SyncGroup kept rebalancing)");
+}
+
+void Replicator::heartbeat(wire::Client& c) {
+  if (!cfg_.subscribe || fenced_.load() || now_ms() - last_heartbeat_ms_ < cfg_.heartbeat_interval_ms) return;
+  last_heartbeat_ms_ = now_ms();
+  const int16_t e = c.heartbeat(cfg_.group, generation_, member_id_);
+  if (e == wire::kRebalanceInProgress || e == wire::kIllegalGeneration || e == wire::kUnknownMemberId) {
+    try {
+      forward(c);  // the current generation may still commit what was consumed
+    } catch (const KafkaError&) {
+    }
+    fenced_ = true;
+    set_error(std::string(wire::error_name(e)) + ": group '" + cfg_.group + "' rebalanced (generation " +
+              std::to_string(generation_) + "); this replica stopped fetching and committing -- restart to re-shard");
+  } else if (e != wire::kNone) {
+    throw wire::WireError(e, std::string(wire::error_name(e)) + ": Heartbeat");
+  }
+}
+
 void Replicator::stop(bool flush) {
   if (!running_.load() && threads_.empty()) return;
   stop_ = true;
@@ -143,6 +208,7 @@ void Replicator::stop(bool flush) {
         if (!commit_client_)
           commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", flush_timeout, cfg_.security);
         forward(*commit_client_);
+        if (cfg_.subscribe && !fenced_.load() && !member_id_.empty()) commit_client_->leave_group(cfg_.group, member_id_);
         break;
       } catch (const KafkaError& e) {
         set_error(std::string("replicator: final commit: ") + e.what());
@@ -192,7 +258,7 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
   std::unique_ptr<wire::Client> c;
   std::set<Part*> failed;
   int backoff_ms = 0;
-  while (!stop_.load()) {
+  while (!stop_.load() && !fenced_.load()) {
     try {
       if (!c) {
         c = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id, cfg_.timeout_ms, cfg_.security);
@@ -311,6 +377,7 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
 
 int Replicator::forward(wire::Client& c) {
   std::lock_guard<std::mutex> g(commit_mu_);
+  if (fenced_.load()) return 0;  // the group moved on: these partitions may belong to another member
   std::map<int32_t, int64_t> offs;
   std::map<int32_t, Part*> by;
   for (auto& p : parts_) {
@@ -322,7 +389,7 @@ int Replicator::forward(wire::Client& c) {
   }
   if (offs.empty()) return 0;
   int n = 0;
-  auto errs = c.offset_commit(cfg_.group, cfg_.topic, offs);
+  auto errs = c.offset_commit(cfg_.group, cfg_.topic, offs, "", generation_, member_id_);
   for (auto& [pid, e] : errs) {
     auto it = by.find(pid);
     if (it == by.end()) continue;
@@ -354,6 +421,7 @@ void Replicator::commit_loop() {
         commit_client_->set_cancel(&stop_);
       }
       forward(*commit_client_);
+      heartbeat(*commit_client_);
       backoff_ms = cfg_.commit_interval_ms;
     } catch (const std::exception& e) {
       if (stop_.load()) break;

@@ -37,6 +37,14 @@ struct ReplicaConfig {
   std::string client_id = "torchkafka-replicator";
   wire::Security security;             // TLS / SASL (kafka-python's security_protocol, ssl_*, sasl_*)
   std::vector<int32_t> partitions;     // empty: every partition of the topic
+  // Subscribe mode: join `group` (JoinGroup/SyncGroup, range assignor) and mirror the partitions
+  // the coordinator assigns, as kafka-python's subscribe() does.  Membership is fixed for the
+  // replica's lifetime: when the group rebalances (a member joins or leaves) the replica stops
+  // fetching and forwarding ("fenced"), reports RebalanceInProgressError, and the job re-shards
+  // by restarting -- the elastic-restart model of a DDP job.  Heartbeats ride the commit thread.
+  bool subscribe = false;
+  int32_t session_timeout_ms = 10000;
+  int32_t heartbeat_interval_ms = 3000;
   std::string auto_offset_reset = "earliest";  // without a committed offset: earliest | latest
   int32_t max_wait_ms = 100;
   int32_t min_bytes = 1;
@@ -91,6 +99,12 @@ class Replicator {
   std::vector<ReplicaPartStats> stats();
   uint32_t first_pidx() const { return first_pidx_; }
   int32_t n_partitions() const { return n_remote_parts_; }
+  // subscribe mode: this member's id / generation / assigned partitions; fenced once the group
+  // rebalanced under it
+  std::string member_id() const { return member_id_; }
+  int32_t generation() const { return generation_; }
+  std::vector<int32_t> assignment() const { return assigned_; }
+  bool fenced() const { return fenced_.load(); }
   // Blocks until every replicated partition has fetched up to the cluster's high watermark as
   // seen at call time (tests, tools); false on timeout.
   bool wait_caught_up(int timeout_ms);
@@ -130,6 +144,13 @@ class Replicator {
   std::string last_error_;
   std::mutex commit_mu_;  // serialises forward() between the committer thread and flush_commits()
   std::unique_ptr<wire::Client> commit_client_;
+  void join_group(wire::Client& c);
+  void heartbeat(wire::Client& c);
+  std::string member_id_;
+  int32_t generation_ = -1;
+  std::vector<int32_t> assigned_;
+  std::atomic<bool> fenced_{false};
+  int64_t last_heartbeat_ms_ = 0;
 };
 
 }  // namespace tk
