@@ -127,7 +127,7 @@ def main() -> int:
         ok = br.wait_caught_up(300)
         rep_s = time.perf_counter() - t0
         out["replication"] = {"caught_up": ok, "s": round(rep_s, 3), "gb_per_s": round(total_bytes / rep_s / 1e9, 2),
-                              "fetch_threads": len({s["partition"] % args.nodes for s in br.stats()}),
+                              "fetch_threads": br._r.fetch_threads,
                               "errors": br.errors}
         br.close()
     except _SkipCluster:

@@ -602,6 +602,7 @@ PYBIND11_MODULE(_tkcore, m) {
       .def_property_readonly("generation", &Replicator::generation)
       .def_property_readonly("assignment", &Replicator::assignment)
       .def_property_readonly("fenced", &Replicator::fenced)
+      .def_property_readonly("fetch_threads", &Replicator::fetch_threads)
       .def("last_error", &Replicator::last_error)
       .def("stats", [](Replicator& r) {
         py::list l;

@@ -118,7 +118,9 @@ void Replicator::start() {
   // fetch threads: partitions grouped by leader, leaders spread over the threads
   std::map<int32_t, std::vector<Part*>> by_leader;
   for (auto& p : parts_) by_leader[c.leader(cfg_.topic, p->partition)].push_back(p.get());
-  int n_threads = cfg_.fetchers > 0 ? cfg_.fetchers : std::min<int>(8, int(by_leader.size()));
+  // default: one thread per leader, and at least 4 when there are fewer leaders than that -- one
+  // connection per thread, so a small cluster is not held to one socket's receive rate
+  int n_threads = cfg_.fetchers > 0 ? cfg_.fetchers : std::min<int>(8, std::max<int>(int(by_leader.size()), 4));
   n_threads = std::max(1, std::min<int>(n_threads, int(parts_.size())));
   std::vector<std::vector<Part*>> per(static_cast<size_t>(n_threads));
   size_t k = 0;
@@ -126,8 +128,12 @@ void Replicator::start() {
     for (Part* p : ps) per[(k++) % per.size()].push_back(p);
   stop_ = false;
   running_ = true;
+  n_fetch_threads_ = 0;
   for (auto& v : per)
-    if (!v.empty()) threads_.emplace_back([this, v]() { fetch_loop(v); });
+    if (!v.empty()) {
+      threads_.emplace_back([this, v]() { fetch_loop(v); });
+      ++n_fetch_threads_;
+    }
   if (!cfg_.group.empty()) {
     commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", cfg_.timeout_ms, cfg_.security);
     threads_.emplace_back([this]() { commit_loop(); });

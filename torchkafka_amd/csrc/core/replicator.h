@@ -105,6 +105,7 @@ class Replicator {
   int32_t generation() const { return generation_; }
   std::vector<int32_t> assignment() const { return assigned_; }
   bool fenced() const { return fenced_.load(); }
+  int fetch_threads() const { return n_fetch_threads_; }
   // Blocks until every replicated partition has fetched up to the cluster's high watermark as
   // seen at call time (tests, tools); false on timeout.
   bool wait_caught_up(int timeout_ms);
@@ -151,6 +152,7 @@ class Replicator {
   std::vector<int32_t> assigned_;
   std::atomic<bool> fenced_{false};
   int64_t last_heartbeat_ms_ = 0;
+  int n_fetch_threads_ = 0;
 };
 
 }  // namespace tk
