@@ -13,3 +13,17 @@ def test_example_05_kafka_cluster_bridge_on_cpu():
     assert r.returncode == 0, r.stderr[-3000:]
     assert "20000 records on cpu" in r.stdout
     assert "{0: 5000, 1: 5000, 2: 5000, 3: 5000}" in r.stdout
+
+
+def test_example_06_group_subscribe_tls():
+    import shutil
+
+    import pytest
+    if shutil.which("openssl") is None:
+        pytest.skip("openssl CLI not available")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "examples", "06_group_subscribe_tls.py")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "partitions [0, 1, 2], generation 1, 3000 records" in r.stdout
+    assert "partitions [3, 4, 5], generation 1, 3000 records" in r.stdout
+    assert "{0: 1000, 1: 1000, 2: 1000, 3: 1000, 4: 1000, 5: 1000}" in r.stdout
