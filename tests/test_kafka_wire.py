@@ -852,7 +852,26 @@ def test_security_config_validates_the_mechanism():
     assert security_config(security_protocol="SSL", ssl_cafile=None, bootstrap_servers="x") == \
         {"security_protocol": "SSL"}
     with pytest.raises(ValueError, match="PLAIN"):
-        security_config(security_protocol="SASL_SSL", sasl_mechanism="SCRAM-SHA-256")
+        security_config(security_protocol="SASL_SSL", sasl_mechanism="GSSAPI")
+
+
+@pytest.mark.parametrize("mech", ["SCRAM-SHA-256", "SCRAM-SHA-512"])
+def test_sasl_scram_authenticates(broker, tls_cert, mech):
+    broker.create_topic("t", 2)
+    broker.fill("t", 30, "fixed_f32", size=8)
+    srv = secure_server(broker, tls_cert, users={"carol": "p,w=d"})
+    try:
+        sec = {"security_protocol": "SASL_SSL", "ssl_cafile": tls_cert[0], "sasl_mechanism": mech,
+               "sasl_plain_username": "carol"}
+        c = core().WireClient(srv.address, timeout_ms=2000, security=dict(sec, sasl_plain_password="p,w=d"))
+        assert c.list_offsets("t", [0, 1], -1) == {0: 30, 1: 30}
+        with pytest.raises(Exception, match="SaslAuthenticationFailed"):
+            core().WireClient(srv.address, timeout_ms=2000, security=dict(sec, sasl_plain_password="nope")).metadata("t")
+        with bridge(srv, group_id="g", security_protocol="SASL_SSL", ssl_cafile=tls_cert[0], sasl_mechanism=mech,
+                    sasl_plain_username="carol", sasl_plain_password="p,w=d") as br:
+            assert br.wait_caught_up(10) and br.local.end_offset("t", 1) == 30
+    finally:
+        srv.close()
 
 
 # ---- group membership: subscribe mode (JoinGroup / SyncGroup / Heartbeat / LeaveGroup)

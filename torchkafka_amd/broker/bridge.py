@@ -58,12 +58,17 @@ SECURITY_KEYS = ("security_protocol", "ssl_cafile", "ssl_check_hostname", "ssl_c
                  "sasl_mechanism", "sasl_plain_username", "sasl_plain_password")
 
 
+SASL_MECHANISMS = ("PLAIN", "SCRAM-SHA-256", "SCRAM-SHA-512")
+
+
 def security_config(**kw) -> dict:
     """The TLS / SASL subset of a kafka-python configuration, for the native wire client
-    (security_protocol PLAINTEXT | SSL | SASL_PLAINTEXT | SASL_SSL; SASL mechanism PLAIN)."""
+    (security_protocol PLAINTEXT | SSL | SASL_PLAINTEXT | SASL_SSL; SASL mechanism PLAIN,
+    SCRAM-SHA-256 or SCRAM-SHA-512)."""
     out = {k: v for k, v in kw.items() if k in SECURITY_KEYS and v is not None}
-    if out.get("security_protocol", "PLAINTEXT").startswith("SASL_") and out.get("sasl_mechanism", "PLAIN") != "PLAIN":
-        raise ValueError(f"sasl_mechanism {out['sasl_mechanism']!r}: the native client speaks PLAIN")
+    mech = out.get("sasl_mechanism", "PLAIN")
+    if out.get("security_protocol", "PLAINTEXT").startswith("SASL_") and mech not in SASL_MECHANISMS:
+        raise ValueError(f"sasl_mechanism {mech!r}: the native client speaks {', '.join(SASL_MECHANISMS)}")
     return out
 
 

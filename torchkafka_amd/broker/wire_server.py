@@ -18,6 +18,10 @@ Reference: the reference consumes through kafka-python's KafkaConsumer
 """
 from __future__ import annotations
 
+import base64
+import hashlib
+import hmac
+import os
 import socket
 import socketserver
 import struct
@@ -39,6 +43,7 @@ NONE, OFFSET_OUT_OF_RANGE, UNKNOWN_TOPIC, NOT_LEADER, UNSUPPORTED_VERSION = 0, 1
 ILLEGAL_GENERATION, UNSUPPORTED_SASL_MECHANISM, SASL_AUTHENTICATION_FAILED = 22, 33, 58
 UNKNOWN_MEMBER_ID, REBALANCE_IN_PROGRESS = 25, 27
 API_SASL_HANDSHAKE, API_SASL_AUTHENTICATE = 17, 36
+SASL_MECHANISMS = ("PLAIN", "SCRAM-SHA-256", "SCRAM-SHA-512")
 
 
 class _R:
@@ -286,22 +291,20 @@ class KafkaWireServer:
         state = {"authed": True} if state is None else state
         if key == API_SASL_HANDSHAKE:
             mech = r.str()
-            ok = self.sasl_users is not None and mech == "PLAIN"
+            ok = self.sasl_users is not None and mech in SASL_MECHANISMS
             w.i16(NONE if ok else UNSUPPORTED_SASL_MECHANISM)
-            w.i32(1)
-            w.str("PLAIN")
-            state["mech"] = ok
+            w.i32(len(SASL_MECHANISMS))
+            for m in SASL_MECHANISMS:
+                w.str(m)
+            state["mech"] = mech if ok else None
             return w.data()
         if key == API_SASL_AUTHENTICATE:
             n = r.i32()
-            token = r.b[r.o:r.o + n]
-            parts = token.split(b"\0")
-            user, pw = (parts[1].decode(), parts[2].decode()) if len(parts) == 3 else ("", None)
-            ok = bool(state.get("mech")) and self.sasl_users.get(user) == pw
-            state["authed"] = ok
+            token = bytes(r.b[r.o:r.o + n])
+            reply, ok = self._sasl_step(state, token)
             w.i16(NONE if ok else SASL_AUTHENTICATION_FAILED)
             w.str(None if ok else "Authentication failed: invalid username or password")
-            w.bytes(b"")
+            w.bytes(reply if ok else b"")
             return w.data()
         if not state["authed"] and key != API_API_VERSIONS:
             return None  # a SASL listener drops unauthenticated requests
@@ -318,6 +321,46 @@ class KafkaWireServer:
             return None  # a real broker closes the connection on an unsupported version
         getattr(self, f"_api_{key}")(r, ver, w)
         return w.data()
+
+    def _sasl_step(self, state: dict, token: bytes) -> tuple[bytes, bool]:
+        """One SaslAuthenticate round of the mechanism the handshake chose: PLAIN in one round,
+        SCRAM-SHA-256/512 (RFC 5802) in two -- client-first, then client-final with the proof."""
+        mech = state.get("mech")
+        if mech == "PLAIN":
+            parts = token.split(b"\0")
+            user, pw = (parts[1].decode(), parts[2].decode()) if len(parts) == 3 else ("", None)
+            state["authed"] = ok = self.sasl_users.get(user) == pw
+            return b"", ok
+        if mech not in ("SCRAM-SHA-256", "SCRAM-SHA-512"):
+            return b"", False
+        h = hashlib.sha512 if mech.endswith("512") else hashlib.sha256
+        msg = token.decode()
+        attrs = lambda m: dict(kv.split("=", 1) for kv in m.split(",") if "=" in kv)  # noqa: E731
+        if "scram" not in state:  # client-first: "n,,n=user,r=cnonce"
+            bare = msg[3:] if msg.startswith("n,,") else ""
+            a = attrs(bare)
+            user = a.get("n", "").replace("=2C", ",").replace("=3D", "=")
+            if user not in self.sasl_users or "r" not in a:
+                return b"", False
+            salt, iters = os.urandom(16), 4096
+            first = f"r={a['r']}{base64.b64encode(os.urandom(18)).decode()},s={base64.b64encode(salt).decode()},i={iters}"
+            salted = hashlib.pbkdf2_hmac(h().name, self.sasl_users[user].encode(), salt, iters)
+            state["scram"] = (bare, first, salted)
+            return first.encode(), True
+        bare, first, salted = state.pop("scram")
+        a = attrs(msg)
+        without_proof = msg[:msg.rfind(",p=")]
+        if a.get("r") != attrs(first)["r"]:
+            return b"", False
+        auth = f"{bare},{first},{without_proof}".encode()
+        client_key = hmac.new(salted, b"Client Key", h).digest()
+        signature = hmac.new(h(client_key).digest(), auth, h).digest()
+        proof = base64.b64decode(a.get("p", ""))
+        if len(proof) != len(signature) or bytes(x ^ y for x, y in zip(proof, signature)) != client_key:
+            return b"", False
+        state["authed"] = True
+        server_sig = hmac.new(hmac.new(salted, b"Server Key", h).digest(), auth, h).digest()
+        return ("v=" + base64.b64encode(server_sig).decode()).encode(), True
 
     def _topic_names(self, r: _R, ver: int):
         n = r.i32()

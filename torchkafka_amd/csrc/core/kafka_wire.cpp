@@ -8,6 +8,9 @@
 #include <poll.h>
 #include <sys/socket.h>
 #include <openssl/err.h>
+#include <openssl/evp.h>
+#include <openssl/hmac.h>
+#include <openssl/rand.h>
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
 #include <unistd.h>
@@ -167,9 +170,114 @@ Conn::Conn(const std::string& host, int port, int timeout_ms, const Security* se
   if (sec && sec->sasl()) authenticate(*sec);
 }
 
+namespace {
+
+std::string b64(const std::string& s) {
+  std::string out(4 * ((s.size() + 2) / 3) + 1, '\0');
+  const int n = EVP_EncodeBlock(reinterpret_cast<unsigned char*>(&out[0]),
+                                reinterpret_cast<const unsigned char*>(s.data()), int(s.size()));
+  out.resize(size_t(n));
+  return out;
+}
+
+std::string unb64(const std::string& s) {
+  if (s.size() % 4) throw KafkaError("SaslAuthenticationFailedError: bad base64 from the server");
+  std::string out(s.size() / 4 * 3 + 1, '\0');
+  const int n = EVP_DecodeBlock(reinterpret_cast<unsigned char*>(&out[0]),
+                                reinterpret_cast<const unsigned char*>(s.data()), int(s.size()));
+  if (n < 0) throw KafkaError("SaslAuthenticationFailedError: bad base64 from the server");
+  size_t pad = 0;
+  for (size_t i = s.size(); i > 0 && s[i - 1] == '='; --i) ++pad;
+  out.resize(size_t(n) - pad);
+  return out;
+}
+
+std::string hmac(const EVP_MD* md, const std::string& key, const std::string& msg) {
+  unsigned char out[EVP_MAX_MD_SIZE];
+  unsigned len = 0;
+  HMAC(md, key.data(), int(key.size()), reinterpret_cast<const unsigned char*>(msg.data()), msg.size(), out, &len);
+  return std::string(reinterpret_cast<char*>(out), len);
+}
+
+std::string digest(const EVP_MD* md, const std::string& msg) {
+  unsigned char out[EVP_MAX_MD_SIZE];
+  unsigned len = 0;
+  EVP_Digest(msg.data(), msg.size(), out, &len, md, nullptr);
+  return std::string(reinterpret_cast<char*>(out), len);
+}
+
+// "a=1,b=2" -> value of `key`
+std::string scram_attr(const std::string& msg, char key) {
+  size_t i = 0;
+  while (i < msg.size()) {
+    size_t j = msg.find(',', i);
+    if (j == std::string::npos) j = msg.size();
+    if (j - i >= 2 && msg[i] == key && msg[i + 1] == '=') return msg.substr(i + 2, j - i - 2);
+    i = j + 1;
+  }
+  return "";
+}
+
+}  // namespace
+
+// One SaslAuthenticate v0 round: sends `token`, returns the server's bytes (throws on an error).
+std::string Conn::sasl_round(const std::string& token) {
+  Writer au;
+  au.i32(int32_t(token.size()));
+  au.data().append(token);
+  auto r = roundtrip(kSaslAuthenticate, 0, "torchkafka", au.data(), timeout_ms_);
+  Reader b(r.data(), r.size());
+  const int16_t e = b.i16();
+  const std::string msg = b.str();
+  int32_t len = 0;
+  const uint8_t* p = b.bytes(&len);
+  if (e != kNone) {
+    close();
+    throw KafkaError("SaslAuthenticationFailedError: " + (msg.empty() ? std::string(error_name(e)) : msg));
+  }
+  return len > 0 ? std::string(reinterpret_cast<const char*>(p), size_t(len)) : std::string();
+}
+
+// SCRAM-SHA-256 / SCRAM-SHA-512 (RFC 5802 / 7677): two SaslAuthenticate rounds; the server's
+// signature is checked too, so a man in the middle without the password is detected.
+void Conn::scram(const Security& sec) {
+  const EVP_MD* md = sec.sasl_mechanism == "SCRAM-SHA-512" ? EVP_sha512() : EVP_sha256();
+  unsigned char rnd[24];
+  if (RAND_bytes(rnd, sizeof(rnd)) != 1) throw KafkaError("SASL: no random bytes for the SCRAM nonce");
+  const std::string cnonce = b64(std::string(reinterpret_cast<char*>(rnd), sizeof(rnd)));
+  std::string user;
+  for (char ch : sec.username) user += ch == '=' ? "=3D" : ch == ',' ? "=2C" : std::string(1, ch);
+  const std::string first_bare = "n=" + user + ",r=" + cnonce;
+  const std::string server_first = sasl_round("n,," + first_bare);
+  const std::string nonce = scram_attr(server_first, 'r'), salt = unb64(scram_attr(server_first, 's'));
+  const int iters = std::atoi(scram_attr(server_first, 'i').c_str());
+  if (nonce.compare(0, cnonce.size(), cnonce) != 0 || iters < 1) {
+    close();
+    throw KafkaError("SaslAuthenticationFailedError: malformed SCRAM server-first message");
+  }
+  const int hlen = EVP_MD_get_size(md);
+  std::string salted(size_t(hlen), '\0');
+  PKCS5_PBKDF2_HMAC(sec.password.data(), int(sec.password.size()), reinterpret_cast<const unsigned char*>(salt.data()),
+                    int(salt.size()), iters, md, hlen, reinterpret_cast<unsigned char*>(&salted[0]));
+  const std::string client_key = hmac(md, salted, "Client Key");
+  const std::string stored_key = digest(md, client_key);
+  const std::string final_wo_proof = "c=biws,r=" + nonce;  // biws = base64("n,,")
+  const std::string auth_msg = first_bare + "," + server_first + "," + final_wo_proof;
+  std::string proof = hmac(md, stored_key, auth_msg);
+  for (size_t i = 0; i < proof.size(); ++i) proof[i] = char(proof[i] ^ client_key[i]);
+  const std::string server_final = sasl_round(final_wo_proof + ",p=" + b64(proof));
+  const std::string expect = b64(hmac(md, hmac(md, salted, "Server Key"), auth_msg));
+  if (scram_attr(server_final, 'v') != expect) {
+    close();
+    throw KafkaError("SaslAuthenticationFailedError: the server's SCRAM signature does not match");
+  }
+}
+
 void Conn::authenticate(const Security& sec) {
-  if (sec.sasl_mechanism != "PLAIN")
-    throw KafkaError("UnsupportedSaslMechanismError: " + sec.sasl_mechanism + " (this client speaks PLAIN)");
+  const bool is_scram = sec.sasl_mechanism == "SCRAM-SHA-256" || sec.sasl_mechanism == "SCRAM-SHA-512";
+  if (sec.sasl_mechanism != "PLAIN" && !is_scram)
+    throw KafkaError("UnsupportedSaslMechanismError: " + sec.sasl_mechanism +
+                     " (this client speaks PLAIN, SCRAM-SHA-256 and SCRAM-SHA-512)");
   Writer hs;
   hs.str(sec.sasl_mechanism);
   auto r1 = roundtrip(kSaslHandshake, 1, "torchkafka", hs.data(), timeout_ms_);
@@ -179,22 +287,16 @@ void Conn::authenticate(const Security& sec) {
     close();
     throw KafkaError(std::string(error_name(e1)) + ": SaslHandshake " + sec.sasl_mechanism + " refused by " + host_);
   }
+  if (is_scram) {
+    scram(sec);
+    return;
+  }
   std::string token;
   token.push_back('\0');
   token += sec.username;
   token.push_back('\0');
   token += sec.password;
-  Writer au;
-  au.i32(int32_t(token.size()));
-  au.data().append(token);
-  auto r2 = roundtrip(kSaslAuthenticate, 0, "torchkafka", au.data(), timeout_ms_);
-  Reader b(r2.data(), r2.size());
-  const int16_t e2 = b.i16();
-  const std::string msg = b.str();
-  if (e2 != kNone) {
-    close();
-    throw KafkaError("SaslAuthenticationFailedError: " + (msg.empty() ? std::string(error_name(e2)) : msg));
-  }
+  sasl_round(token);
 }
 
 ssize_t Conn::io_recv(void* dst, size_t n) {

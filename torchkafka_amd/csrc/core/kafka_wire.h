@@ -38,7 +38,8 @@ namespace tk::wire {
 
 // Connection security, named as kafka-python's configuration: security_protocol PLAINTEXT | SSL |
 // SASL_PLAINTEXT | SASL_SSL; TLS through OpenSSL (server verified against ssl_cafile, or the
-// system store); SASL mechanism PLAIN (SaslHandshake v1 + SaslAuthenticate v0).
+// system store); SASL mechanisms PLAIN, SCRAM-SHA-256 and SCRAM-SHA-512 (SaslHandshake v1 +
+// SaslAuthenticate v0).
 struct Security {
   std::string protocol = "PLAINTEXT";
   std::string cafile, certfile, keyfile;
@@ -148,6 +149,8 @@ class Conn {
   ssize_t io_recv(void* dst, size_t n);
   bool wait_readable(int ms);
   void authenticate(const Security& sec);
+  void scram(const Security& sec);
+  std::string sasl_round(const std::string& token);
   SSL* ssl_ = nullptr;
   std::string host_;
   int port_;
