@@ -866,7 +866,8 @@ def test_sasl_scram_authenticates(broker, tls_cert, mech):
         c = core().WireClient(srv.address, timeout_ms=2000, security=dict(sec, sasl_plain_password="p,w=d"))
         assert c.list_offsets("t", [0, 1], -1) == {0: 30, 1: 30}
         with pytest.raises(Exception, match="SaslAuthenticationFailed"):
-            core().WireClient(srv.address, timeout_ms=2000, security=dict(sec, sasl_plain_password="nope")).metadata("t")
+            bad = dict(sec, sasl_plain_password="nope")
+            core().WireClient(srv.address, timeout_ms=2000, security=bad).metadata("t")
         with bridge(srv, group_id="g", security_protocol="SASL_SSL", ssl_cafile=tls_cert[0], sasl_mechanism=mech,
                     sasl_plain_username="carol", sasl_plain_password="p,w=d") as br:
             assert br.wait_caught_up(10) and br.local.end_offset("t", 1) == 30

@@ -343,7 +343,8 @@ class KafkaWireServer:
             if user not in self.sasl_users or "r" not in a:
                 return b"", False
             salt, iters = os.urandom(16), 4096
-            first = f"r={a['r']}{base64.b64encode(os.urandom(18)).decode()},s={base64.b64encode(salt).decode()},i={iters}"
+            snonce, s64 = base64.b64encode(os.urandom(18)).decode(), base64.b64encode(salt).decode()
+            first = f"r={a['r']}{snonce},s={s64},i={iters}"
             salted = hashlib.pbkdf2_hmac(h().name, self.sasl_users[user].encode(), salt, iters)
             state["scram"] = (bare, first, salted)
             return first.encode(), True
