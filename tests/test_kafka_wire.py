@@ -929,23 +929,43 @@ def test_subscribe_splits_partitions_across_members(broker, server):
     assert server.group_members("g") == {}  # both left the group on close
 
 
-def test_a_rebalance_fences_the_old_members(broker, server):
+def test_a_rebalance_that_moves_partitions_fences_the_old_member(broker, server):
     broker.create_topic("t", 4)
     broker.fill("t", 40, "fixed_f32", size=8)
-    kw = dict(group_id="g", subscribe=True, heartbeat_interval_ms=50, session_timeout_ms=1500)
+    kw = dict(group_id="g", subscribe=True, heartbeat_interval_ms=50, session_timeout_ms=3000)
     first = bridge(server, **kw)
     try:
         assert sorted(first.assignment) == [0, 1, 2, 3] and not first.fenced
-        second = bridge(server, **kw)  # its join round waits out the session timeout of `first`
+        second = bridge(server, **kw)  # `first` rejoins on its next heartbeat; the range assignor halves t
         try:
             assert wait_for(lambda: first.fenced, 5)
             assert "RebalanceInProgress" in first.last_error()
-            assert sorted(second.assignment) == [0, 1, 2, 3] and second.generation == first.generation + 1
+            assert len(second.assignment) == 2 and second.generation == first.generation == 2
             assert second.wait_caught_up(10)
         finally:
             second.close()
     finally:
         first.close()
+
+
+def test_a_rebalance_that_keeps_the_partitions_carries_on(broker, server):
+    broker.create_topic("t", 2)
+    broker.create_topic("u", 2)
+    broker.fill("t", 30, "fixed_f32", size=8)
+    broker.fill("u", 30, "fixed_f32", size=8)
+    kw = dict(group_id="g", subscribe=True, heartbeat_interval_ms=50, session_timeout_ms=3000)
+    a = bridge(server, "t", **kw)
+    try:
+        b = bridge(server, "u", **kw)  # another topic in the same group: a keeps all of t
+        try:
+            assert wait_for(lambda: a.generation == 2, 5) and not a.fenced
+            assert sorted(a.assignment) == [0, 1] and sorted(b.assignment) == [0, 1]
+            a.local.commit("g", {TopicPartition("t", 0): 30})
+            assert wait_for(lambda: broker.committed_offsets("g", "t").get(0) == 30)  # generation 2 commit
+        finally:
+            b.close()
+    finally:
+        a.close()
 
 
 def test_subscribe_needs_a_group(broker, server):

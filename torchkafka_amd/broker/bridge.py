@@ -90,10 +90,10 @@ class KafkaBridge:
                  start: bool = True):
         """``subscribe=True`` (needs ``group_id``, excludes ``partitions``): join the consumer group
         like kafka-python's ``subscribe()`` -- JoinGroup/SyncGroup with the range assignor -- and
-        mirror the partitions the coordinator assigns (:attr:`assignment`).  Membership is fixed
-        for the bridge's lifetime: when the group rebalances the bridge stops fetching and
-        forwarding (:attr:`fenced`, RebalanceInProgressError in :meth:`last_error`) and the job
-        re-shards by restarting.  Default: the static ``partitions`` (kafka-python's ``assign()``)."""
+        mirror the partitions the coordinator assigns (:attr:`assignment`).  On a rebalance the
+        bridge commits and rejoins; with the same partitions back it carries on, otherwise it
+        stops fetching and forwarding (:attr:`fenced`, RebalanceInProgressError in
+        :meth:`last_error`) and the job re-shards by restarting.  Default: the static ``partitions`` (kafka-python's ``assign()``)."""
         if subscribe and not group_id:
             raise ValueError("subscribe=True needs a group_id")
         if subscribe and partitions is not None:

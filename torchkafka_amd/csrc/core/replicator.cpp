@@ -62,7 +62,7 @@ void Replicator::start() {
   if (cfg_.release_consumed && !cfg_.group.empty()) local_->set_flags(kReleaseConsumed);
   if (cfg_.subscribe) {
     if (cfg_.group.empty()) throw std::invalid_argument("replicator: subscribe mode needs a group");
-    join_group(c);
+    assigned_ = join_group(c);
   }
   std::vector<int32_t> ids = cfg_.subscribe ? assigned_ : cfg_.partitions;
   if (ids.empty() && !cfg_.subscribe)
@@ -141,7 +141,7 @@ void Replicator::start() {
   }
 }
 
-void Replicator::join_group(wire::Client& c) {
+std::vector<int32_t> Replicator::join_group(wire::Client& c) {
   const std::string sub = wire::encode_subscription({cfg_.topic});
   for (int attempt = 0; attempt < 8; ++attempt) {
     wire::JoinResult j = c.join_group(cfg_.group, cfg_.session_timeout_ms, member_id_, sub);
@@ -175,9 +175,10 @@ void Replicator::join_group(wire::Client& c) {
     if (e != wire::kNone)
       throw wire::WireError(e, std::string(wire::error_name(e)) + ": SyncGroup '" + cfg_.group + "'");
     generation_ = j.generation;
-    assigned_ = wire::decode_assignment(bytes)[cfg_.topic];
     last_heartbeat_ms_ = now_ms();
-    return;
+    std::vector<int32_t> mine = wire::decode_assignment(bytes)[cfg_.topic];
+    std::sort(mine.begin(), mine.end());
+    return mine;
   }
   throw KafkaError("replicator: group '" + cfg_.group + "' did not settle (JoinGroup/SyncGroup kept rebalancing)");
 }
@@ -191,7 +192,16 @@ void Replicator::heartbeat(wire::Client& c) {
       forward(c);  // the current generation may still commit what was consumed
     } catch (const KafkaError&) {
     }
-    fenced_ = true;
+    {
+      std::lock_guard<std::mutex> g(commit_mu_);  // forward() reads generation_ / member_id_
+      try {
+        if (e == wire::kUnknownMemberId) member_id_.clear();
+        if (join_group(c) == assigned_) return;  // same partitions: carry on in the new generation
+      } catch (const KafkaError&) {
+        if (stop_.load()) return;
+      }
+      fenced_ = true;
+    }
     set_error(std::string(wire::error_name(e)) + ": group '" + cfg_.group + "' rebalanced (generation " +
               std::to_string(generation_) + "); this replica stopped fetching and committing -- restart to re-shard");
   } else if (e != wire::kNone) {

@@ -38,10 +38,11 @@ struct ReplicaConfig {
   wire::Security security;             // TLS / SASL (kafka-python's security_protocol, ssl_*, sasl_*)
   std::vector<int32_t> partitions;     // empty: every partition of the topic
   // Subscribe mode: join `group` (JoinGroup/SyncGroup, range assignor) and mirror the partitions
-  // the coordinator assigns, as kafka-python's subscribe() does.  Membership is fixed for the
-  // replica's lifetime: when the group rebalances (a member joins or leaves) the replica stops
-  // fetching and forwarding ("fenced"), reports RebalanceInProgressError, and the job re-shards
-  // by restarting -- the elastic-restart model of a DDP job.  Heartbeats ride the commit thread.
+  // the coordinator assigns, as kafka-python's subscribe() does.  The partition set is fixed for
+  // the replica's lifetime: when the group rebalances the replica commits, rejoins, and carries on
+  // if it got the same partitions back; otherwise it stops fetching and forwarding ("fenced"),
+  // reports RebalanceInProgressError, and the job re-shards by restarting -- the elastic-restart
+  // model of a DDP job.  Heartbeats ride the commit thread.
   bool subscribe = false;
   int32_t session_timeout_ms = 10000;
   int32_t heartbeat_interval_ms = 3000;
@@ -145,7 +146,7 @@ class Replicator {
   std::string last_error_;
   std::mutex commit_mu_;  // serialises forward() between the committer thread and flush_commits()
   std::unique_ptr<wire::Client> commit_client_;
-  void join_group(wire::Client& c);
+  std::vector<int32_t> join_group(wire::Client& c);  // sets member_id_ / generation_
   void heartbeat(wire::Client& c);
   std::string member_id_;
   int32_t generation_ = -1;
