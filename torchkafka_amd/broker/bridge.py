@@ -93,7 +93,8 @@ class KafkaBridge:
         mirror the partitions the coordinator assigns (:attr:`assignment`).  On a rebalance the
         bridge commits and rejoins; with the same partitions back it carries on, otherwise it
         stops fetching and forwarding (:attr:`fenced`, RebalanceInProgressError in
-        :meth:`last_error`) and the job re-shards by restarting.  Default: the static ``partitions`` (kafka-python's ``assign()``)."""
+        :meth:`last_error`) and the job re-shards by restarting.  Default: the static
+        ``partitions`` (kafka-python's ``assign()``)."""
         if subscribe and not group_id:
             raise ValueError("subscribe=True needs a group_id")
         if subscribe and partitions is not None:
