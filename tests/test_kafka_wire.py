@@ -881,6 +881,23 @@ def test_range_assignor_matches_kafkas():
     got = core().range_assign([("c", ["t"]), ("a", ["t", "u"]), ("b", ["t"])], {"t": 8, "u": 3})
     assert got == {"a": {"t": [0, 1, 2], "u": [0, 1, 2]}, "b": {"t": [3, 4, 5]}, "c": {"t": [6, 7]}}
     assert core().range_assign([("a", ["t"]), ("b", ["t"]), ("c", ["t"])], {"t": 2})["c"] == {"t": []}
+    rr = core().range_assign([("b", ["t", "u"]), ("a", ["t"])], {"t": 5, "u": 2}, roundrobin=True)
+    assert rr == {"a": {"t": [0, 2, 4]}, "b": {"t": [1, 3], "u": [0, 1]}}
+
+
+def test_roundrobin_strategy_through_the_coordinator(broker, server):
+    broker.create_topic("t", 5)
+    broker.fill("t", 20, "fixed_f32", size=8)
+    kw = dict(group_id="g", subscribe=True, partition_assignment_strategy=["roundrobin", "range"], start=False)
+    bs = [bridge(server, **kw) for _ in range(2)]
+    try:
+        _start_all(bs)
+        assert sorted(sorted(b.assignment) for b in bs) == [[0, 2, 4], [1, 3]]
+    finally:
+        for b in bs:
+            b.close()
+    with pytest.raises(Exception, match="range . roundrobin"):
+        bridge(server, group_id="g", subscribe=True, partition_assignment_strategy=["sticky"])
 
 
 def _start_all(bridges):

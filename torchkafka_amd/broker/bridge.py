@@ -87,13 +87,15 @@ class KafkaBridge:
                  ssl_certfile: str | None = None, ssl_keyfile: str | None = None, sasl_mechanism: str | None = None,
                  sasl_plain_username: str | None = None, sasl_plain_password: str | None = None,
                  subscribe: bool = False, session_timeout_ms: int = 10000, heartbeat_interval_ms: int = 3000,
-                 start: bool = True):
+                 partition_assignment_strategy: Iterable[str] = ("range",), start: bool = True):
         """``subscribe=True`` (needs ``group_id``, excludes ``partitions``): join the consumer group
         like kafka-python's ``subscribe()`` -- JoinGroup/SyncGroup with the range assignor -- and
         mirror the partitions the coordinator assigns (:attr:`assignment`).  On a rebalance the
         bridge commits and rejoins; with the same partitions back it carries on, otherwise it
         stops fetching and forwarding (:attr:`fenced`, RebalanceInProgressError in
-        :meth:`last_error`) and the job re-shards by restarting.  Default: the static
+        :meth:`last_error`) and the job re-shards by restarting.  ``partition_assignment_strategy``:
+        assignor names in preference order, "range" and/or "roundrobin" (kafka-python's two).
+        Default: the static
         ``partitions`` (kafka-python's ``assign()``)."""
         if subscribe and not group_id:
             raise ValueError("subscribe=True needs a group_id")
@@ -126,7 +128,8 @@ class KafkaBridge:
                                      sasl_plain_username=sasl_plain_username,
                                      sasl_plain_password=sasl_plain_password),
             subscribe=bool(subscribe), session_timeout_ms=int(session_timeout_ms),
-            heartbeat_interval_ms=int(heartbeat_interval_ms))
+            heartbeat_interval_ms=int(heartbeat_interval_ms),
+            assignors=[str(a) for a in partition_assignment_strategy])
         self._closed = False
         self._lock = threading.Lock()
         self._reported = 0

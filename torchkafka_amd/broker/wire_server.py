@@ -153,7 +153,7 @@ class _Group:
         self.state = "empty"   # empty | joining | syncing | stable
         self.generation = 0
         self.members: dict[str, bytes] = {}   # member id -> subscription metadata (this generation)
-        self.joining: dict[str, bytes] = {}   # the round in progress
+        self.joining: dict[str, dict] = {}    # the round in progress: member -> {assignor: metadata}
         self.leader = ""
         self.protocol = ""
         self.assignments: dict[str, bytes] = {}
@@ -556,8 +556,7 @@ class KafkaWireServer:
                 return
             member = member or f"member-{uuid.uuid4().hex[:12]}"
             self._begin_round(g, session_ms / 1000.0)
-            g.joining[member] = protos[0][1] if protos else b""
-            g.protocol = protos[0][0] if protos else ""
+            g.joining[member] = dict(protos)  # assignor name -> subscription metadata
             gen0 = g.generation
             self._gcond.notify_all()
             while g.generation == gen0:
@@ -565,8 +564,10 @@ class KafkaWireServer:
                 done = set(g.members) <= set(g.joining) and now >= g.min_end
                 if done or now >= g.deadline:
                     g.generation += 1
-                    g.members = dict(g.joining)
                     g.leader = next(iter(g.joining))
+                    common = [n for n in g.joining[g.leader] if all(n in ps for ps in g.joining.values())]
+                    g.protocol = common[0] if common else ""
+                    g.members = {m: ps.get(g.protocol, b"") for m, ps in g.joining.items()}
                     g.state, g.assignments = "syncing", {}
                     self._gcond.notify_all()
                     break

@@ -193,14 +193,14 @@ PYBIND11_MODULE(_tkcore, m) {
   m.def("zstd_available", &zstd_available);
   // Kafka's range assignor over (member id, subscribed topics): {member: {topic: [partitions]}}
   m.def("range_assign", [](const std::vector<std::pair<std::string, std::vector<std::string>>>& members,
-                           const std::map<std::string, int32_t>& counts) {
+                           const std::map<std::string, int32_t>& counts, bool rr) {
     std::vector<std::pair<std::string, std::string>> ms;
     for (auto& [m, topics] : members) ms.emplace_back(m, wire::encode_subscription(topics));
-    auto out = wire::range_assign(ms, counts);
+    auto out = rr ? wire::roundrobin_assign(ms, counts) : wire::range_assign(ms, counts);
     std::map<std::string, wire::Assignment> back;
     for (auto& [m, a] : out) back[m] = wire::decode_assignment(wire::encode_assignment(a));
     return back;
-  });
+  }, py::arg("members"), py::arg("counts"), py::arg("roundrobin") = false);
   m.def("crc32c_fold", &crc32c_fold);
   m.def("crc32c_shift_raw", &crc32c_shift_raw, py::arg("raw"), py::arg("n_bytes"));
   m.def(
@@ -553,8 +553,13 @@ PYBIND11_MODULE(_tkcore, m) {
                        int64_t max_lag_bytes, int32_t commit_interval_ms, int32_t fetchers, uint64_t log_capacity,
                        uint64_t index_capacity, const std::string& client_id, bool release_consumed,
                        uint64_t release_bytes, uint64_t release_step, uint64_t ring_bytes, py::dict security,
-                       bool subscribe, int32_t session_timeout_ms, int32_t heartbeat_interval_ms) {
+                       bool subscribe, int32_t session_timeout_ms, int32_t heartbeat_interval_ms,
+                       std::vector<std::string> assignors) {
              ReplicaConfig c;
+             for (auto& a : assignors)
+               if (a != "range" && a != "roundrobin")
+                 throw std::invalid_argument("partition_assignment_strategy: '" + a + "' (range | roundrobin)");
+             if (!assignors.empty()) c.assignors = std::move(assignors);
              c.subscribe = subscribe;
              c.session_timeout_ms = session_timeout_ms;
              c.heartbeat_interval_ms = heartbeat_interval_ms;
@@ -589,7 +594,7 @@ PYBIND11_MODULE(_tkcore, m) {
            py::arg("release_consumed") = true, py::arg("release_bytes") = uint64_t(256) << 20,
            py::arg("release_step") = uint64_t(1) << 30, py::arg("ring_bytes") = uint64_t(0),
            py::arg("security") = py::dict(), py::arg("subscribe") = false, py::arg("session_timeout_ms") = 10000,
-           py::arg("heartbeat_interval_ms") = 3000)
+           py::arg("heartbeat_interval_ms") = 3000, py::arg("assignors") = std::vector<std::string>{"range"})
       .def("start", &Replicator::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Replicator::stop, py::arg("flush") = true, py::call_guard<py::gil_scoped_release>())
       .def("flush_commits", &Replicator::flush_commits, py::call_guard<py::gil_scoped_release>())

@@ -740,16 +740,18 @@ std::vector<uint8_t> Client::coordinator_roundtrip(const std::string& group, int
 }
 
 JoinResult Client::join_group(const std::string& group, int32_t session_timeout_ms, const std::string& member_id,
-                              const std::string& subscription) {
+                              const std::string& subscription, const std::vector<std::string>& protocols) {
   Writer w;
   w.str(group);
   w.i32(session_timeout_ms);
   w.str(member_id);
   w.str("consumer");
-  w.array(1);
-  w.str("range");
-  w.i32(int32_t(subscription.size()));
-  w.data() += subscription;
+  w.array(int32_t(protocols.size()));
+  for (auto& name : protocols) {
+    w.str(name);
+    w.i32(int32_t(subscription.size()));
+    w.data() += subscription;
+  }
   // the coordinator holds the request until the join round ends
   auto resp = coordinator_roundtrip(group, kJoinGroup, 0, w.data(), timeout_ms_ + session_timeout_ms);
   Reader r(resp.data(), resp.size());
@@ -879,6 +881,30 @@ std::map<std::string, Assignment> range_assign(const std::vector<std::pair<std::
       for (int32_t p = start; p < start + len; ++p) ps.push_back(p);
     }
   }
+  return out;
+}
+
+std::map<std::string, Assignment> roundrobin_assign(const std::vector<std::pair<std::string, std::string>>& members,
+                                                    const std::map<std::string, int32_t>& partitions_per_topic) {
+  std::map<std::string, Assignment> out;
+  std::map<std::string, std::vector<std::string>> subs;  // member -> topics (sorted by member id)
+  for (auto& [m, meta] : members) {
+    out[m];
+    subs[m] = decode_subscription(meta);
+  }
+  std::vector<std::string> ids;
+  for (auto& [m, t] : subs) ids.push_back(m);
+  size_t next = 0;
+  for (auto& [topic, n] : partitions_per_topic)
+    for (int32_t p = 0; p < n && !ids.empty(); ++p)
+      for (size_t k = 0; k < ids.size(); ++k) {  // next member (cyclically) subscribed to `topic`
+        const std::string& m = ids[(next + k) % ids.size()];
+        const auto& ts = subs[m];
+        if (std::find(ts.begin(), ts.end(), topic) == ts.end()) continue;
+        out[m][topic].push_back(p);
+        next = (next + k + 1) % ids.size();
+        break;
+      }
   return out;
 }
 

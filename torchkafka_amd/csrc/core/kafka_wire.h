@@ -201,6 +201,10 @@ Assignment decode_assignment(const std::string& bytes);
 // the first (P % members) one partition more.  members: (id, subscription metadata).
 std::map<std::string, Assignment> range_assign(const std::vector<std::pair<std::string, std::string>>& members,
                                                const std::map<std::string, int32_t>& partitions_per_topic);
+// Kafka's RoundRobinAssignor: every (topic, partition) in order, dealt to the members sorted by id
+// (skipping members not subscribed to that topic).
+std::map<std::string, Assignment> roundrobin_assign(const std::vector<std::pair<std::string, std::string>>& members,
+                                                    const std::map<std::string, int32_t>& partitions_per_topic);
 
 struct FetchPartReq {
   int32_t partition;
@@ -230,8 +234,10 @@ class Client {
                                            const std::string& member_id = "");
   // Group membership against the group's coordinator.  join_group blocks at the coordinator
   // until the join round ends (up to the session timeout).
+  // protocols: assignor names in preference order ("range", "roundrobin")
   JoinResult join_group(const std::string& group, int32_t session_timeout_ms, const std::string& member_id,
-                        const std::string& subscription);
+                        const std::string& subscription,
+                        const std::vector<std::string>& protocols = std::vector<std::string>{"range"});
   std::pair<int16_t, std::string> sync_group(const std::string& group, int32_t generation,
                                              const std::string& member_id,
                                              const std::map<std::string, std::string>& assignments);

@@ -144,7 +144,7 @@ void Replicator::start() {
 std::vector<int32_t> Replicator::join_group(wire::Client& c) {
   const std::string sub = wire::encode_subscription({cfg_.topic});
   for (int attempt = 0; attempt < 8; ++attempt) {
-    wire::JoinResult j = c.join_group(cfg_.group, cfg_.session_timeout_ms, member_id_, sub);
+    wire::JoinResult j = c.join_group(cfg_.group, cfg_.session_timeout_ms, member_id_, sub, cfg_.assignors);
     if (j.error == wire::kUnknownMemberId) {
       member_id_.clear();
       continue;
@@ -165,7 +165,9 @@ std::vector<int32_t> Replicator::join_group(wire::Client& c) {
             wire::TopicMeta tm = c.metadata(topic);
             counts[topic] = tm.error ? 0 : int32_t(tm.partitions.size());
           }
-      for (auto& [m, a] : wire::range_assign(j.members, counts)) plan[m] = wire::encode_assignment(a);
+      auto plan_of = j.protocol == "roundrobin" ? wire::roundrobin_assign(j.members, counts)
+                                                : wire::range_assign(j.members, counts);
+      for (auto& [m, a] : plan_of) plan[m] = wire::encode_assignment(a);
     }
     auto [e, bytes] = c.sync_group(cfg_.group, j.generation, member_id_, plan);
     if (e == wire::kRebalanceInProgress || e == wire::kIllegalGeneration || wire::needs_metadata(e)) {

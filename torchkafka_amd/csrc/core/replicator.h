@@ -44,6 +44,7 @@ struct ReplicaConfig {
   // reports RebalanceInProgressError, and the job re-shards by restarting -- the elastic-restart
   // model of a DDP job.  Heartbeats ride the commit thread.
   bool subscribe = false;
+  std::vector<std::string> assignors{"range"};  // partition_assignment_strategy, in preference order
   int32_t session_timeout_ms = 10000;
   int32_t heartbeat_interval_ms = 3000;
   std::string auto_offset_reset = "earliest";  // without a committed offset: earliest | latest
