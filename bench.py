@@ -7,20 +7,36 @@ BASELINE.json metric "Kafka records/sec to GPU with per-batch commit, at
   * N = 1 : config 2 -- 1x MI355X, num_workers=4, 8-partition topic,
             fixed-width float32 records (256 x f32 = 1 KiB), pinned ring +
             hipMemcpyAsync on a side stream, gfx950 collate kernel -> bf16;
-  * N > 1 : config 3 -- one process per GPU (torchrun), 8 partitions per rank
+  * N > 1 : config 3 -- one process per GPU, 8 partitions per rank
             (64 at N = 8), static rank sharding, auto_commit lock-stepped by an
             RCCL all-reduce over xGMI every step.
 
 A step = one batch of ``--batch-size`` records per rank consumed from the
-synthetic broker, packed in pinned memory, copied to the GPU, collated to
-bf16 by the HIP kernel, handed to the user, and its offsets committed (the
-commit of batch k happens when batch k+1 is requested, as in the reference's
-auto_commit).  Records are synthetic Kafka RecordBatch v2 records produced
-into the shared-memory broker before timing (a retained backlog).
-Weak scaling: per-rank work is fixed as N grows.
+synthetic broker, decoded on the GPU (CRC32C + values cast to bf16 by the
+gfx950 kernels), handed to the user, and its offsets committed (the commit of
+batch k happens when batch k+1 is requested, as in the reference's
+auto_commit, /root/reference/src/auto_commit.py:55-58).  Records are synthetic
+Kafka RecordBatch v2 records produced into the shared-memory broker before
+timing (a retained backlog).  Weak scaling: per-rank work is fixed as N grows.
 
-Usage: python bench.py [--gpus N --steps K --warmup W]
-  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+Launch: ``python bench.py --gpus N --steps K --warmup W``.  Under torchrun
+(``WORLD_SIZE`` set) this process is one rank.  Without it and N > 1, this
+process starts N rank processes itself -- before any GPU call, as fresh
+children with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 set --
+relays rank 0's single JSON line and exits with the first failing rank's code.
+It refuses to run (exit 2) when fewer than N GPUs are visible.
+
+Blocks in the one JSON line (all timed between a barrier + synchronize on both
+sides, max over ranks, whole-job records):
+  * ``value``: the driver's K steps (after W warm-up steps);
+  * ``steady_state``: ``--steady-steps`` more steps of the same loader (default
+    50 000: >= 0.25 s at the measured rate; the workers' prefilled slots are a
+    fraction of a percent of it), with per-rank rates and the lockstep's cost;
+  * ``steady_dma``: a second loader (own consumer group, same topic from the
+    earliest offset) with ``h2d="dma"``: the partition logs are copied into HBM
+    by hipMemcpyAsync on a side stream (SDMA) and decoded there -- the config-2
+    mechanism;
+  * ``steady_f32``: a third loader delivering float32 (the reference's dtype).
 """
 from __future__ import annotations
 
@@ -28,7 +44,10 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 BASELINE_METRIC = "Kafka records/sec to GPU with per-batch commit, at 1/2/4/8 MI355X"
@@ -72,33 +91,226 @@ def parse():
                     help="every rank on cuda:0 with a gloo group (rehearse N > 1 ranks on a one-GPU box)")
     ap.add_argument("--steady-steps", type=int, default=None,
                     help="steps of the steady-state block timed after the headline (default: max(50 x ring "
-                         "slots, 4000); 0 skips it)")
+                         "slots, 50000) on a GPU, 2000 on the CPU; 0 skips it)")
+    ap.add_argument("--extra-blocks", default="dma,f32",
+                    help="comma list of secondary steady blocks, each a fresh loader: dma (h2d='dma', HBM "
+                         "mirror filled by SDMA), f32 (float32 output); '' for none")
+    ap.add_argument("--extra-steps", type=int, default=None,
+                    help="timed steps of each secondary block (default: the steady-state steps)")
     return ap.parse_args()
 
 
-def main() -> int:
-    args = parse()
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local_rank = int(os.environ.get("LOCAL_RANK", 0))
-    if world != args.gpus:
-        print(f"[bench] warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+# ---------------------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
-    import torch
-    import torch.distributed as dist
 
+def launch_ranks(args) -> int:
+    """N > 1 without torchrun: start N rank processes (this process never touches the GPU --
+    ``torch.cuda.device_count()`` does not initialise HIP on this image) and relay rank 0's line."""
+    n = args.gpus
+    if not args.device and not args.same_device:
+        import torch
+
+        visible = torch.cuda.device_count()
+        if visible < n:
+            print(f"[bench] --gpus {n} but only {visible} GPU(s) are visible: refusing to run fewer ranks",
+                  file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   TK_BENCH_LAUNCHER=f"bench.py self-launch ({n} child ranks)")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    lines: list[str] = []
+
+    def relay():
+        for line in procs[0].stdout:
+            lines.append(line)
+            if not line.startswith('{"metric"'):
+                sys.stderr.write(line)
+
+    t = threading.Thread(target=relay, daemon=True)
+    t.start()
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(i, c) for i, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                rc = bad[0][1]
+                print(f"[bench] rank {bad[0][0]} exited with {rc}: stopping the other ranks", file=sys.stderr)
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(0.1)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    t.join(timeout=10)
+    out = [x for x in lines if x.startswith('{"metric"')]
+    if rc == 0:
+        if len(out) != 1:
+            print(f"[bench] rank 0 printed {len(out)} result lines", file=sys.stderr)
+            return 1
+        res = json.loads(out[0])
+        if res.get("n_gpus") != n:
+            print(f"[bench] rank 0 reported n_gpus={res.get('n_gpus')}, launched {n}", file=sys.stderr)
+            return 1
+        sys.stdout.write(out[0])
+        sys.stdout.flush()
+    return rc if rc >= 0 else 128 - rc
+
+
+# ---------------------------------------------------------------------------------------- one rank
+class Rank:
+    """One rank's side of the job: process group, device, the shared broker, timing helpers."""
+
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist, self.args = torch, dist, args
+        self.rank = int(os.environ.get("RANK", 0))
+        self.world = int(os.environ.get("WORLD_SIZE", 1))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", 0))
+        if self.world != args.gpus:
+            raise SystemExit(f"[bench] WORLD_SIZE={self.world} but --gpus={args.gpus}")
+        dev = args.device
+        if not dev:
+            if not args.same_device and self.local_rank >= torch.cuda.device_count():
+                raise SystemExit(f"[bench] rank {self.rank}: LOCAL_RANK {self.local_rank} but only "
+                                 f"{torch.cuda.device_count()} GPU(s) visible")
+            dev = f"cuda:{0 if args.same_device else self.local_rank}"
+        self.device = torch.device(dev)
+        self.use_gloo = self.device.type != "cuda" or args.same_device or args.lockstep == "host"
+
+    def init_group(self) -> None:
+        dist = self.dist
+        if self.world > 1 or self.args.lockstep in ("rccl", "host"):
+            # no GPU touched yet: the loader forks its workers before HIP is initialised
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+            dist.init_process_group("gloo" if self.use_gloo else "nccl", rank=self.rank, world_size=self.world)
+
+    def _t(self, vals):
+        torch = self.torch
+        return torch.tensor(vals, dtype=torch.float64, device="cpu" if self.use_gloo else self.device)
+
+    def barrier(self) -> None:
+        if self.dist.is_initialized():
+            self.dist.barrier(device_ids=[self.device.index] if not self.use_gloo else None)
+
+    def sync(self) -> None:
+        torch = self.torch
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        if self.world > 1:
+            self.barrier()
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+
+    def gather(self, vals: list[float]) -> list[list[float]]:
+        """Every rank's ``vals`` (rank order)."""
+        if self.world == 1:
+            return [list(vals)]
+        t = self._t(vals)
+        out = [self.torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [[float(v) for v in x.tolist()] for x in out]
+
+    def check_ranks(self) -> dict:
+        """Start-up proof that the process group spans the job: one all-reduce of the rank ids."""
+        if self.world == 1:
+            return {"process_group": None, "world_size": 1}
+        t = self._t([float(self.rank)])
+        self.dist.all_reduce(t)
+        s = int(t.item())
+        want = self.world * (self.world - 1) // 2
+        if s != want:
+            raise RuntimeError(f"rank-id all-reduce gave {s}, expected {want} for {self.world} ranks")
+        return {"process_group": self.dist.get_backend(), "world_size": self.dist.get_world_size(),
+                "rank_id_sum": s}
+
+
+def time_steps(R: Rank, it, steps: int, loader) -> dict:
+    """Times ``steps`` batches: barrier + synchronize on both sides, max time over ranks."""
+    loader.reset_stats()
+    R.sync()
+    occ = loader.ring_occupancy()
+    t0 = time.perf_counter()
+    rows = 0
+    x = None
+    for _ in range(steps):
+        x = next(it)
+        rows += x.shape[0]
+    R.sync()
+    el = time.perf_counter() - t0
+    per_rank = R.gather([el, float(rows)])
+    tmax = max(p[0] for p in per_rank)
+    total = sum(p[1] for p in per_rank)
+    st = loader.stats_summary()
+    return {"el": tmax, "rows": total, "per_rank": per_rank, "stats": st, "occ": occ, "last": x}
+
+
+def steady_block(R: Rank, res: dict, steps: int, dim: int) -> dict:
+    st = res["stats"]
+    el, total = res["el"], res["rows"]
+    out = {
+        "steps": steps,
+        "timed_s": round(el, 6),
+        "records_per_s": round(total / el, 1),
+        "ms_per_step": round(el / steps * 1000, 4),
+        "gb_per_s": round(total / el * dim * 4 / 1e9, 3),
+        "ring_slots": res["occ"]["n_slots"],
+        "prefilled_slots_at_t0": res["occ"]["prefilled"],
+        "steps_per_ring": round(steps / max(1, res["occ"]["n_slots"]), 1),
+        "vs_baseline": round(total / el / BASELINE_VALUE, 3),
+        "commit_p50_us": round(st["commit_p50_us"], 2),
+        "commit_p99_us": round(st["commit_p99_us"], 2),
+        "commit_latency_p50_us": round(st["commit_latency_p50_us"], 2),
+        "commit_latency_p99_us": round(st["commit_latency_p99_us"], 2),
+        "commits": st["commits"],
+        "worker_fill_us_per_batch": round(st.get("worker_fill_us_per_batch", 0.0), 2),
+    }
+    if R.world > 1:
+        out["per_rank_records_per_s"] = [round(r / e, 1) for e, r in res["per_rank"]]
+        out["lockstep_agreements"] = st.get("lockstep_agreements", 0)
+        out["lockstep_wait_us_per_step"] = round(st.get("lockstep_wait_us_per_batch", 0.0), 2)
+        out["lockstep_step_wait_max_us"] = round(st.get("lockstep_step_wait_max_us", 0.0), 1)
+    return out
+
+
+def run_rank(args) -> int:
+    R = Rank(args)
+    torch, dist = R.torch, R.dist
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
     from torchkafka_amd.broker import SyntheticBroker
     from torchkafka_amd.parallel import shard_partitions
     from torchkafka_amd.utils.topology import bind_to_gpu_numa
 
+    rank, world = R.rank, R.world
     if not args.device and not args.no_numa:
         # the broker log this rank fills, its ring and its workers all live on its GPU's socket
-        bind_to_gpu_numa(local_rank)
-
-    dtype = {"bf16": torch.bfloat16, "fp8": torch.float8_e4m3fn, "f16": torch.float16, "f32": torch.float32}[args.dtype]
-    device = torch.device(args.device) if args.device else torch.device("cuda", 0 if args.same_device else local_rank)
+        bind_to_gpu_numa(R.local_rank)
+    dtypes = {"bf16": torch.bfloat16, "fp8": torch.float8_e4m3fn, "f16": torch.float16, "f32": torch.float32}
+    device = R.device
     # lockstep: the agreement every step runs before a batch is delivered and committed
     if args.lockstep == "off":
         lockstep = False
@@ -112,7 +324,7 @@ def main() -> int:
     class Records(KafkaDataset):
         schema = FixedWidth(torch.float32, (args.dim,))
 
-    # --- broker: one per job (all ranks of a torchrun share the agent's pid and port)
+    # --- broker: one per job (every rank of the job shares its launcher's pid and port)
     tag = f"{os.getppid()}-{os.environ.get('MASTER_PORT', '0')}" if world > 1 else f"{os.getpid()}"
     url = f"shm://tkbench-{tag}"
     n_parts = args.partitions_per_gpu * world
@@ -120,125 +332,102 @@ def main() -> int:
     broker = SyntheticBroker.create(url, log_capacity=1 << 34, index_capacity=1 << 22)
     broker.create_topic("bench", n_parts)
     # backlog per owned partition: every batch the timed loop and the warm-up consume, plus what the
-    # workers prefetch into their ring slots, with headroom
+    # workers prefetch into their ring slots, with headroom (the secondary blocks re-read it from the
+    # earliest offset under consumer groups of their own)
     mine = shard_partitions(n_parts, rank, world)
     ring_guess = args.workers * (args.slots_per_worker or 8)
-    steady = args.steady_steps if args.steady_steps is not None else max(50 * ring_guess, 4000)
-    batches = args.warmup + args.steps + steady + args.workers * ((args.slots_per_worker or 8) + 2)
+    # >= 0.25 s on the GPU; a CPU dry run keeps its backlog (host memory) small
+    steady = (args.steady_steps if args.steady_steps is not None
+              else max(50 * ring_guess, 50000) if device.type == "cuda" else 2000)
+    extra = [b for b in args.extra_blocks.split(",") if b]
+    if device.type != "cuda":
+        extra = [b for b in extra if b != "dma"]
+    extra_steps = args.extra_steps if args.extra_steps is not None else steady
+    extra_warm = max(50, args.warmup)
+    consumed = max(args.warmup + args.steps + steady, (extra_warm + extra_steps) if extra else 0)
+    batches = consumed + args.workers * ((args.slots_per_worker or 8) + 2)
     per_part = int(math.ceil(batches * B * 1.25 / max(1, len(mine)))) + B
     t_fill = time.perf_counter()
     broker.fill("bench", per_part, "fixed_f32", size=args.dim, partitions=mine,
                 records_per_batch=args.records_per_batch, threads=min(16, len(mine)))
     t_fill = time.perf_counter() - t_fill
 
-    use_gloo = device.type != "cuda" or args.same_device or args.lockstep == "host"
-    if world > 1 or args.lockstep in ("rccl", "host"):
-        # no CUDA touched yet: the loader forks its workers before HIP is initialised
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
-        dist.init_process_group("gloo" if use_gloo else "nccl", rank=rank, world_size=world)
+    R.init_group()
 
-    loader = DeviceLoader(
-        Records.placeholder(), B, num_workers=args.workers, device=device, dtype=dtype,
-        slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
-        in_order=args.in_order, h2d=args.h2d, copy_streams=args.copy_streams, lockstep_depth=args.lockstep_depth,
-        event_every=args.event_every, numa_bind=not args.no_numa, coalesce=args.coalesce,
-        coalesce_wait_us=args.coalesce_wait_us, decode=args.decode, lockstep=lockstep,
-        mirror_chunk_mib=args.mirror_chunk_mib,
-        **({"mirror_chunks": args.mirror_chunks} if args.mirror_chunks else {}),
-        worker_init_fn=Records.init_worker("bench", bootstrap_servers=url, group_id="bench",
-                                           auto_offset_reset="earliest", check_crcs=not args.no_crc),
-    )
+    def make_loader(group: str, dtype, h2d: str):
+        return DeviceLoader(
+            Records.placeholder(), B, num_workers=args.workers, device=device, dtype=dtype,
+            slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
+            in_order=args.in_order, h2d=h2d, copy_streams=args.copy_streams, lockstep_depth=args.lockstep_depth,
+            event_every=args.event_every, numa_bind=not args.no_numa, coalesce=args.coalesce,
+            coalesce_wait_us=args.coalesce_wait_us, decode=args.decode, lockstep=lockstep,
+            mirror_chunk_mib=args.mirror_chunk_mib,
+            **({"mirror_chunks": args.mirror_chunks} if args.mirror_chunks else {}),
+            worker_init_fn=Records.init_worker("bench", bootstrap_servers=url, group_id=group,
+                                               auto_offset_reset="earliest", check_crcs=not args.no_crc),
+        )
+
+    def describe(loader) -> tuple[str, str]:
+        h2d = loader._resolve_h2d(loader._slot_capacity()) if device.type == "cuda" else "n/a (cpu)"
+        decode = ("host workers" if not loader._span() else
+                  "device (gfx950 CRC32C + decode from an HBM mirror filled by SDMA copies)"
+                  if loader._mirror() else "device (gfx950 CRC32C + decode from pinned logs)")
+        return h2d, decode
+
+    loader = make_loader("bench", dtypes[args.dtype], args.h2d)
     it = iter(auto_commit(loader))
-    x = next(it)  # forks workers, initialises HIP/RCCL
+    x = next(it)  # forks workers, initialises HIP / the RCCL lockstep
     if device.type == "cuda":
         torch.cuda.set_device(device)
-
-    def barrier():
-        dist.barrier(device_ids=[local_rank] if device.type == "cuda" and not use_gloo else None)
-
-    def sync():
-        if device.type == "cuda":
-            torch.cuda.synchronize(device)
-        if world > 1:
-            barrier()
-            if device.type == "cuda":
-                torch.cuda.synchronize(device)
+    ranks_check = R.check_ranks()
+    lock_info = dict(loader.lockstep_info)
 
     for _ in range(max(0, args.warmup - 1)):
         x = next(it)
-    sync()
-    loader.reset_stats()
-    # what the workers filled ahead of the consumer: a short timed region may only drain these
-    occ = loader.ring_occupancy()
-    t0 = time.perf_counter()
-    rows = 0
-    for _ in range(args.steps):
-        x = next(it)
-        rows += x.shape[0]
-    sync()
-    elapsed = time.perf_counter() - t0
-    stats = loader.stats_summary()
-
-    def job_rate(el: float, nrows: int) -> tuple[float, float]:
-        """whole-job aggregate: records of every rank over the slowest rank's time"""
-        if world == 1:
-            return el, float(nrows)
-        t = torch.tensor([el, float(nrows)], dtype=torch.float64, device="cpu" if use_gloo else device)
-        tmax = t.clone()
-        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        return float(tmax[0]), float(t[1])
-
-    elapsed, total_rows = job_rate(elapsed, rows)
+    head = time_steps(R, it, args.steps, loader)
+    elapsed, total_rows, stats = head["el"], head["rows"], head["stats"]
     value = total_rows / elapsed
+    h2d_desc, decode_desc = describe(loader)
 
-    # Steady state, same process, right after the headline: many times the ring depth, so the
-    # batches the workers had prefilled before t0 are a small part of it and the producer side
-    # (fetch, pack, publish) is inside the timed region.
-    steady_out = None
+    # Steady state, same loader, right after the headline: many times the ring depth, so the batches
+    # the workers had prefilled before t0 are a small part of it and the producer side (fetch, pack,
+    # publish) is inside the timed region.
+    steady_out = s_stats = None
     if steady > 0:
-        n_slots = occ["n_slots"] or ring_guess
-        s_steps = steady
-        loader.reset_stats()
-        sync()
-        occ_s = loader.ring_occupancy()
-        if args.stats:
-            print(json.dumps({"ring_at_steady_t0": occ_s}), file=sys.stderr)
-        t1 = time.perf_counter()
-        srows = 0
-        for _ in range(s_steps):
-            x = next(it)
-            srows += x.shape[0]
-        sync()
-        s_el, s_total = job_rate(time.perf_counter() - t1, srows)
-        s_stats = loader.stats_summary()
-        steady_out = {
-            "steps": s_steps,
-            "timed_s": round(s_el, 6),
-            "records_per_s": round(s_total / s_el, 1),
-            "ms_per_step": round(s_el / s_steps * 1000, 4),
-            "gb_per_s": round(s_total / s_el * args.dim * 4 / 1e9, 3),
-            "ring_slots": n_slots,
-            "prefilled_slots_at_t0": occ_s["prefilled"],
-            "steps_per_ring": round(s_steps / max(1, n_slots), 1),
-            "vs_baseline": round(s_total / s_el / BASELINE_VALUE, 3),
-            "commit_p50_us": round(s_stats["commit_p50_us"], 2),
-            "commit_p99_us": round(s_stats["commit_p99_us"], 2),
-            "commit_latency_p50_us": round(s_stats["commit_latency_p50_us"], 2),
-            "commit_latency_p99_us": round(s_stats["commit_latency_p99_us"], 2),
-            "worker_fill_us_per_batch": round(s_stats.get("worker_fill_us_per_batch", 0.0), 2),
-        }
+        sres = time_steps(R, it, steady, loader)
+        s_stats = sres["stats"]
+        steady_out = steady_block(R, sres, steady, args.dim)
+        if args.stats and rank == 0:
+            print(json.dumps({"ring_at_steady_t0": sres["occ"]}), file=sys.stderr)
+        x = sres["last"]
 
     # check what landed on the device: the last batch's records must be this rank's partitions
-    xf = x.float()
-    parts = set(int(p) for p in xf[:, 1].tolist())
+    parts = set(int(p) for p in x.float()[:, 1].tolist())
     assert parts <= set(mine), f"rank {rank} received foreign partitions {parts - set(mine)}"
-
     it.close()  # normal end of the auto_commit generator: final commit + worker shutdown
+    loader.close()
     if world > 1:
-        barrier()
+        R.barrier()
     committed = broker.committed_offsets("bench", "bench")
+
+    # secondary blocks: fresh loaders (own consumer groups) over the same retained topic
+    extra_out = {}
+    for name in extra:
+        dt = torch.float32 if name == "f32" else dtypes[args.dtype]
+        ld = make_loader(f"bench-{name}", dt, "dma" if name == "dma" else args.h2d)
+        eit = iter(auto_commit(ld))
+        for _ in range(extra_warm):
+            next(eit)
+        eres = time_steps(R, eit, extra_steps, ld)
+        blk = steady_block(R, eres, extra_steps, args.dim)
+        blk["dtype"] = "f32" if name == "f32" else args.dtype
+        blk["h2d"], blk["decode"] = describe(ld)
+        extra_out[f"steady_{name}"] = blk
+        eit.close()
+        ld.close()
+        if world > 1:
+            R.barrier()
+
     if rank == 0:
         if args.stats:
             print(json.dumps({"loader_stats": stats, "fill_s": t_fill,
@@ -267,33 +456,45 @@ def main() -> int:
                 "partitions": n_parts,
                 "num_workers": args.workers,
                 "commit": "auto_commit per batch" + (
-                    "" if not lockstep or (lockstep is True and world == 1)
-                    else ", lockstep (gloo all-reduce)" if use_gloo else ", RCCL lockstep"),
-                "h2d": loader._resolve_h2d(loader._slot_capacity()) if device.type == "cuda" else "n/a (cpu)",
-                "decode": ("host workers" if not loader._span() else
-                           "device (gfx950 CRC32C + decode from an HBM mirror filled by SDMA copies)"
-                           if loader._mirror() else "device (gfx950 CRC32C + decode from pinned logs)"),
+                    "" if not lock_info else ", RCCL lockstep" if lock_info.get("transport") == "rccl"
+                    else f", lockstep ({lock_info.get('backend', 'host')} all-reduce)"),
+                "h2d": h2d_desc,
+                "decode": decode_desc,
                 "bytes_per_step_per_gpu": B * args.dim * 4,
                 "gb_per_s": round(value * args.dim * 4 / 1e9, 3),
                 "commit_p99_us": round(stats["commit_p99_us"], 2),
             },
+            "launcher": os.environ.get("TK_BENCH_LAUNCHER", "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ
+                                       else "single process"),
+            "ranks": ranks_check,
+            "lockstep": lock_info or None,
+            "rccl_nranks": lock_info.get("rccl_nranks"),
+            "per_rank_records_per_s": [round(r / e, 1) for e, r in head["per_rank"]],
             # request of batch k+1 -> batch k's offsets stored, incl. the lockstep agreement and the
             # wait for batch k's on-device CRC verdict (steady-state block when it ran)
-            "commit_latency_p50_us": round((s_stats if steady_out else stats)["commit_latency_p50_us"], 2),
-            "commit_latency_p99_us": round((s_stats if steady_out else stats)["commit_latency_p99_us"], 2),
+            "commit_latency_p50_us": round((s_stats or stats)["commit_latency_p50_us"], 2),
+            "commit_latency_p99_us": round((s_stats or stats)["commit_latency_p99_us"], 2),
             "timed_region_s": round(elapsed, 6),
-            "prefilled_slots_at_t0": occ["prefilled"],
-            "ring_slots": occ["n_slots"],
+            "prefilled_slots_at_t0": head["occ"]["prefilled"],
+            "ring_slots": head["occ"]["n_slots"],
+            "fill_s": round(t_fill, 2),
             "steady_state": steady_out,
+            **extra_out,
         }
-        print(json.dumps(out))
-    loader.close()
+        print(json.dumps(out), flush=True)
     if world > 1:
-        barrier()
+        R.barrier()
         dist.destroy_process_group()
     if rank == 0:
         broker.destroy()
     return 0
+
+
+def main() -> int:
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args)
+    return run_rank(args)
 
 
 if __name__ == "__main__":

@@ -27,6 +27,21 @@ def pytest_collection_modifyitems(config, items):
             item.add_marker(skip)
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _remove_leftover_shm():
+    """Removes the shared-memory brokers / replicas this test process created and did not destroy
+    (a test that failed half-way, a bridge whose cluster was unreachable)."""
+    yield
+    import glob
+    import re
+    import shutil
+
+    pid = re.compile(rf"-{os.getpid()}(-|$)")
+    for d in glob.glob("/dev/shm/torchkafka/*"):
+        if pid.search(os.path.basename(d)):
+            shutil.rmtree(d, ignore_errors=True)
+
+
 @pytest.fixture
 def broker():
     """A fresh shared-memory broker, destroyed after the test."""

@@ -128,6 +128,57 @@ int main(int argc, char** argv) {
       ++refused;
     }
   }
+  // LZ4 frames whose FLG announces a content size (0x08) and/or a dictionary id (0x01) or block
+  // checksums (0x10), cut short anywhere in the header: the parser must refuse them, never read
+  // past the (exact-size, heap) input
+  const uint8_t flgs[] = {0x68, 0x61, 0x69, 0x70, 0x78, 0x79};
+  for (uint8_t flg : flgs) {
+    for (size_t n = 7; n <= 32; ++n) {
+      uint8_t* in = static_cast<uint8_t*>(std::malloc(n));
+      const uint8_t hdr[6] = {0x04, 0x22, 0x4D, 0x18, flg, 0x40};
+      std::memcpy(in, hdr, 6);
+      for (size_t i = 6; i < n; ++i) in[i] = uint8_t(rng() % 3 == 0 ? 0 : rng());
+      std::vector<uint8_t> out;
+      try {
+        decompress(kCodecLz4, in, n, out);
+        ++inflated;
+      } catch (const CorruptRecord&) {
+        ++refused;
+      }
+      std::free(in);
+    }
+  }
+  // output bounds: a snappy stream declaring 2^40 bytes, and real output past a small bound,
+  // are CorruptRecord -- not bad_alloc / length_error, which the replica would retry forever
+  {
+    const uint8_t huge[] = {0x80, 0x80, 0x80, 0x80, 0x80, 0x20, 0x00};
+    std::vector<uint8_t> out;
+    bool threw = false;
+    try {
+      decompress(kCodecSnappy, huge, sizeof(huge), out);
+    } catch (const CorruptRecord&) {
+      threw = true;
+    }
+    CHECK(threw);
+    // literal run of 200 bytes then a 4 KiB repeat: over a 1 KiB bound
+    std::vector<uint8_t> blk;
+    blk.push_back(uint8_t(0xFF));  // 15 literals (+ext), match length 15 (+ext)
+    blk.push_back(uint8_t(200 - 15));
+    for (int i = 0; i < 200; ++i) blk.push_back(uint8_t(i));
+    blk.push_back(1);
+    blk.push_back(0);                      // offset 1
+    for (int i = 0; i < 16; ++i) blk.push_back(255);
+    blk.push_back(0);
+    blk.push_back(0x00);                   // final sequence: no literals
+    std::vector<uint8_t> o2;
+    threw = false;
+    try {
+      lz4_block_decompress(blk.data(), blk.size(), o2, 1024);
+    } catch (const CorruptRecord&) {
+      threw = true;
+    }
+    CHECK(threw && o2.size() <= 1024);
+  }
   std::printf("codec fuzz: %d batches, %llu corrupted decodes survived, %llu rejected; JSON fuzz ok; "
               "decompressors: %llu decoded, %llu refused\n", iters,
               (unsigned long long)decoded, (unsigned long long)rejected, (unsigned long long)inflated,

@@ -48,6 +48,42 @@ def test_bench_two_ranks_gloo_cpu():
     assert out["value"] > 0 and out["steady_state"]["records_per_s"] > 0
 
 
+def _bench(*args, timeout=240):
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e["PYTHONPATH"] = ROOT + os.pathsep + e.get("PYTHONPATH", "")
+    return subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, stdout=subprocess.PIPE,
+                          stderr=subprocess.PIPE, text=True, timeout=timeout, env=e)
+
+
+def test_bench_self_launches_n_ranks_without_torchrun():
+    """The driver's plain `python bench.py --gpus N` runs N ranks (never one rank silently)."""
+    r = _bench("--gpus", "2", "--device", "cpu", "--steps", "30", "--warmup", "5", "--steady-steps", "60",
+               "--extra-blocks", "f32", "--extra-steps", "40", "--workers", "2")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["partitions"] == 16
+    assert out["launcher"].startswith("bench.py self-launch")
+    assert out["ranks"]["world_size"] == 2 and out["ranks"]["rank_id_sum"] == 1
+    assert out["lockstep"]["world_size"] == 2
+    assert len(out["per_rank_records_per_s"]) == 2
+    ss = out["steady_state"]
+    assert len(ss["per_rank_records_per_s"]) == 2 and ss["lockstep_agreements"] >= 60
+    assert out["steady_f32"]["dtype"] == "f32" and out["steady_f32"]["steps"] == 40
+
+
+def test_bench_refuses_more_ranks_than_visible_gpus():
+    import torch
+
+    if torch.cuda.device_count() >= 64:
+        pytest.skip("64 GPUs visible")
+    r = _bench("--gpus", "64", "--steps", "5", "--warmup", "1", timeout=120)
+    assert r.returncode == 2 and "refusing" in r.stderr, (r.returncode, r.stderr[-2000:])
+    assert '{"metric"' not in r.stdout
+
+
 def _rank_lines(out: str) -> list:
     """Every '{"rank": ...}' object the ranks printed (their lines may interleave on one line)."""
     dec = json.JSONDecoder()

@@ -113,23 +113,28 @@ class KafkaBridge:
         # a fresh local broker (or an existing persistent replica: file:// URLs resume their logs)
         self.local = SyntheticBroker(self.url, create=True, log_capacity=log_capacity,
                                      index_capacity=index_capacity)
-        self._r = core().Replicator(
-            self.local.native, bootstrap_servers, topic, group=group_id or "",
-            partitions=sorted(int(p) for p in partitions) if partitions is not None else [],
-            auto_offset_reset=auto_offset_reset, max_wait_ms=int(fetch_max_wait_ms), max_bytes=int(fetch_max_bytes),
-            partition_max_bytes=int(max_partition_fetch_bytes), timeout_ms=int(request_timeout_ms),
-            max_lag_bytes=int(max_lag_bytes), commit_interval_ms=int(commit_interval_ms), fetchers=int(fetchers),
-            log_capacity=int(log_capacity), index_capacity=int(index_capacity), client_id=client_id,
-            release_consumed=bool(release_consumed), release_bytes=int(release_bytes),
-            release_step=int(release_step), ring_bytes=int(ring_bytes),
-            security=security_config(security_protocol=security_protocol, ssl_cafile=ssl_cafile,
-                                     ssl_check_hostname=ssl_check_hostname, ssl_certfile=ssl_certfile,
-                                     ssl_keyfile=ssl_keyfile, sasl_mechanism=sasl_mechanism,
-                                     sasl_plain_username=sasl_plain_username,
-                                     sasl_plain_password=sasl_plain_password),
-            subscribe=bool(subscribe), session_timeout_ms=int(session_timeout_ms),
-            heartbeat_interval_ms=int(heartbeat_interval_ms),
-            assignors=[str(a) for a in partition_assignment_strategy])
+        try:
+            self._r = core().Replicator(
+                self.local.native, bootstrap_servers, topic, group=group_id or "",
+                partitions=sorted(int(p) for p in partitions) if partitions is not None else [],
+                auto_offset_reset=auto_offset_reset, max_wait_ms=int(fetch_max_wait_ms), max_bytes=int(fetch_max_bytes),
+                partition_max_bytes=int(max_partition_fetch_bytes), timeout_ms=int(request_timeout_ms),
+                max_lag_bytes=int(max_lag_bytes), commit_interval_ms=int(commit_interval_ms), fetchers=int(fetchers),
+                log_capacity=int(log_capacity), index_capacity=int(index_capacity), client_id=client_id,
+                release_consumed=bool(release_consumed), release_bytes=int(release_bytes),
+                release_step=int(release_step), ring_bytes=int(ring_bytes),
+                security=security_config(security_protocol=security_protocol, ssl_cafile=ssl_cafile,
+                                         ssl_check_hostname=ssl_check_hostname, ssl_certfile=ssl_certfile,
+                                         ssl_keyfile=ssl_keyfile, sasl_mechanism=sasl_mechanism,
+                                         sasl_plain_username=sasl_plain_username,
+                                         sasl_plain_password=sasl_plain_password),
+                subscribe=bool(subscribe), session_timeout_ms=int(session_timeout_ms),
+                heartbeat_interval_ms=int(heartbeat_interval_ms),
+                assignors=[str(a) for a in partition_assignment_strategy])
+        except BaseException:
+            if not self.url.startswith("file://"):  # a fresh shm replica nobody else can use
+                self.local.destroy()
+            raise
         self._closed = False
         self._lock = threading.Lock()
         self._reported = 0

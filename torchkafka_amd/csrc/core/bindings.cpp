@@ -964,7 +964,9 @@ PYBIND11_MODULE(_tkcore, m) {
       .def_property_readonly("step", &CreditLockstep::step)
       .def_property_readonly("granted", &CreditLockstep::granted)
       .def_property_readonly("stopped", &CreditLockstep::stopped)
-      .def_property_readonly("agreements", &CreditLockstep::agreements);
+      .def_property_readonly("agreements", &CreditLockstep::agreements)
+      .def_property_readonly("wait_ns", &CreditLockstep::wait_ns)
+      .def_property_readonly("step_wait_max_ns", &CreditLockstep::step_wait_max_ns);
 
   m.attr("SLOT_EOS") = int(kSlotEOS);
   m.attr("SLOT_ERROR") = int(kSlotError);

@@ -468,7 +468,10 @@ Broker::Ingested Broker::ingest(uint32_t pidx, uint64_t len, int64_t from_offset
           r = 0;
         }
         plain.assign(in + r, in + r + kBatchHeaderBytes);
-        decompress(codec, in + r + kBatchHeaderBytes, total - kBatchHeaderBytes, plain);
+        // an inflated batch larger than the log (or its ring) could never be stored
+        const uint64_t cap = ring ? P.ring_bytes.load(std::memory_order_relaxed) : P.log_capacity;
+        decompress(codec, in + r + kBatchHeaderBytes, total - kBatchHeaderBytes, plain,
+                   size_t(std::min<uint64_t>(cap, kMaxInflatedBytes)));
         const uint32_t new_len = uint32_t(plain.size() - 12);
         const uint32_t be_len = __builtin_bswap32(new_len);
         std::memcpy(plain.data() + kBatchLengthOffset, &be_len, 4);

@@ -6,6 +6,8 @@
 
 #include <cstring>
 #include <memory>
+#include <new>
+#include <stdexcept>
 #include <mutex>
 #include <string>
 
@@ -31,15 +33,21 @@ namespace {
 uint32_t be32(const uint8_t* p) { return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | p[3]; }
 uint32_t le32(const uint8_t* p) { return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24); }
 
+// Output would exceed the caller's bound.
+void room(const std::vector<uint8_t>& out, size_t add, size_t max_out) {
+  if (add > max_out || out.size() > max_out - add) bad("inflated size exceeds the bound");
+}
+
 // Back-reference copy; may overlap its own output (offset < length repeats a pattern).
-void copy_match(std::vector<uint8_t>& out, size_t base, size_t offset, size_t len) {
+void copy_match(std::vector<uint8_t>& out, size_t base, size_t offset, size_t len, size_t max_out) {
   if (offset == 0 || offset > out.size() - base) bad("match offset");
+  room(out, len, max_out);
   size_t from = out.size() - offset;
   out.reserve(out.size() + len);
   for (size_t i = 0; i < len; ++i) out.push_back(out[from + i]);
 }
 
-void gunzip(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
+void gunzip(const uint8_t* src, size_t n, std::vector<uint8_t>& out, size_t max_out) {
   z_stream z{};
   if (inflateInit2(&z, 16 + MAX_WBITS) != Z_OK) bad("zlib init");
   z.next_in = const_cast<Bytef*>(src);
@@ -47,7 +55,11 @@ void gunzip(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
   int rc = Z_OK;
   while (rc != Z_STREAM_END) {
     const size_t old = out.size();
-    out.resize(old + std::max<size_t>(n * 2, 64 << 10));
+    if (old >= max_out) {
+      inflateEnd(&z);
+      bad("inflated size exceeds the bound");
+    }
+    out.resize(old + std::min<size_t>(std::max<size_t>(n * 2, 64 << 10), max_out - old));
     z.next_out = out.data() + old;
     z.avail_out = uInt(out.size() - old);
     rc = inflate(&z, Z_NO_FLUSH);
@@ -69,7 +81,7 @@ void gunzip(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
 
 }  // namespace
 
-void snappy_raw_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
+void snappy_raw_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& out, size_t max_out) {
   const uint8_t* p = src;
   const uint8_t* end = src + n;
   uint64_t want = 0;
@@ -80,6 +92,7 @@ void snappy_raw_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& o
     if (!(b & 0x80)) break;
   }
   const size_t base = out.size();
+  room(out, want, max_out);  // the declared size is checked before anything is reserved for it
   out.reserve(base + want);
   while (p < end) {
     const uint8_t tag = *p++;
@@ -95,6 +108,7 @@ void snappy_raw_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& o
       }
       len += 1;
       if (size_t(end - p) < len) bad("snappy literal");
+      room(out, len, max_out);
       out.insert(out.end(), p, p + len);
       p += len;
     } else {
@@ -114,13 +128,13 @@ void snappy_raw_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& o
         off = le32(p);
         p += 4;
       }
-      copy_match(out, base, off, len);
+      copy_match(out, base, off, len, max_out);
     }
   }
   if (out.size() - base != want) bad("snappy size");
 }
 
-void lz4_block_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
+void lz4_block_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& out, size_t max_out) {
   const uint8_t* p = src;
   const uint8_t* end = src + n;
   const size_t base = out.size();
@@ -136,6 +150,7 @@ void lz4_block_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& ou
       } while (b == 255);
     }
     if (size_t(end - p) < lit) bad("lz4 literals");
+    room(out, lit, max_out);
     out.insert(out.end(), p, p + lit);
     p += lit;
     if (p == end) break;  // the last sequence has literals only
@@ -151,13 +166,13 @@ void lz4_block_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& ou
         len += b;
       } while (b == 255);
     }
-    copy_match(out, base, off, len + 4);
+    copy_match(out, base, off, len + 4, max_out);
   }
 }
 
 namespace {
 
-void unsnappy(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
+void unsnappy(const uint8_t* src, size_t n, std::vector<uint8_t>& out, size_t max_out) {
   static const uint8_t kXerial[8] = {0x82, 'S', 'N', 'A', 'P', 'P', 'Y', 0};
   if (n >= 16 && std::memcmp(src, kXerial, 8) == 0) {  // xerial framing: header, then [BE len][block]...
     size_t o = 16;
@@ -166,15 +181,15 @@ void unsnappy(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
       const uint32_t len = be32(src + o);
       o += 4;
       if (n - o < len) bad("xerial block");
-      snappy_raw_decompress(src + o, len, out);
+      snappy_raw_decompress(src + o, len, out, max_out);
       o += len;
     }
     return;
   }
-  snappy_raw_decompress(src, n, out);
+  snappy_raw_decompress(src, n, out, max_out);
 }
 
-void unlz4_frame(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
+void unlz4_frame(const uint8_t* src, size_t n, std::vector<uint8_t>& out, size_t max_out) {
   if (n < 7 || le32(src) != 0x184D2204u) bad("lz4 frame magic");
   const uint8_t flg = src[4];
   if ((flg >> 6) != 1) bad("lz4 frame version");
@@ -182,6 +197,7 @@ void unlz4_frame(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
   if (flg & 0x08) o += 8;           // content size
   if (flg & 0x01) o += 4;           // dictionary id
   o += 1;                           // header checksum
+  if (o > n) bad("lz4 frame header");  // invariant from here on: o <= n, so n - o never wraps
   const bool block_sum = flg & 0x10;
   while (true) {
     if (n - o < 4) bad("lz4 block size");
@@ -190,10 +206,17 @@ void unlz4_frame(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
     if (word == 0) break;           // end mark
     const uint32_t len = word & 0x7fffffffu;
     if (n - o < len) bad("lz4 block");
-    if (word & 0x80000000u) out.insert(out.end(), src + o, src + o + len);  // stored uncompressed
-    else lz4_block_decompress(src + o, len, out);
-    o += len + (block_sum ? 4 : 0);
-    if (o > n) bad("lz4 block checksum");
+    if (word & 0x80000000u) {       // stored uncompressed
+      room(out, len, max_out);
+      out.insert(out.end(), src + o, src + o + len);
+    } else {
+      lz4_block_decompress(src + o, len, out, max_out);
+    }
+    o += len;
+    if (block_sum) {
+      if (n - o < 4) bad("lz4 block checksum");
+      o += 4;
+    }
   }
 }
 
@@ -229,7 +252,7 @@ const ZstdApi& zstd_api() {
   return api;
 }
 
-void unzstd(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
+void unzstd(const uint8_t* src, size_t n, std::vector<uint8_t>& out, size_t max_out) {
   const ZstdApi& z = zstd_api();
   if (!z.ok) throw KafkaError("UnsupportedCodecError: zstd record batches need libzstd.so.1, which is not loadable");
   std::unique_ptr<void, size_t (*)(void*)> ds(z.create(), z.free_ds);
@@ -238,7 +261,8 @@ void unzstd(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
   size_t rc = 1;
   while (in.pos < in.size || rc != 0) {
     const size_t old = out.size();
-    out.resize(old + std::max<size_t>(n * 4, 128 << 10));
+    if (old >= max_out) bad("inflated size exceeds the bound");
+    out.resize(old + std::min<size_t>(std::max<size_t>(n * 4, 128 << 10), max_out - old));
     ZstdOut o{out.data() + old, out.size() - old, 0};
     const size_t in_before = in.pos;
     rc = z.stream(ds.get(), &o, &in);
@@ -253,15 +277,21 @@ void unzstd(const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
 
 bool zstd_available() { return zstd_api().ok; }
 
-void decompress(int codec, const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
-  switch (codec) {
-    case kCodecGzip: gunzip(src, n, out); return;
-    case kCodecSnappy: unsnappy(src, n, out); return;
-    case kCodecLz4: unlz4_frame(src, n, out); return;
-    case kCodecZstd: unzstd(src, n, out); return;
-    default:
-      throw KafkaError(std::string("UnsupportedCodecError: ") + codec_name(codec) +
-                       " record batches cannot be decoded (gzip, snappy, lz4 and zstd can)");
+void decompress(int codec, const uint8_t* src, size_t n, std::vector<uint8_t>& out, size_t max_out) {
+  try {
+    switch (codec) {
+      case kCodecGzip: gunzip(src, n, out, max_out); return;
+      case kCodecSnappy: unsnappy(src, n, out, max_out); return;
+      case kCodecLz4: unlz4_frame(src, n, out, max_out); return;
+      case kCodecZstd: unzstd(src, n, out, max_out); return;
+      default:
+        throw KafkaError(std::string("UnsupportedCodecError: ") + codec_name(codec) +
+                         " record batches cannot be decoded (gzip, snappy, lz4 and zstd can)");
+    }
+  } catch (const std::bad_alloc&) {
+    bad("out of memory while inflating");
+  } catch (const std::length_error&) {
+    bad("inflated size exceeds the bound");
   }
 }
 

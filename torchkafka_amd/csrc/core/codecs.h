@@ -18,13 +18,22 @@ namespace tk {
 enum Codec : int { kCodecNone = 0, kCodecGzip = 1, kCodecSnappy = 2, kCodecLz4 = 3, kCodecZstd = 4 };
 const char* codec_name(int codec);
 
-// Appends the decompressed bytes of `src` to `out`.  Throws CorruptRecord on malformed input,
-// KafkaError("UnsupportedCodecError ...") for codecs this build cannot decode.
-void decompress(int codec, const uint8_t* src, size_t n, std::vector<uint8_t>& out);
+// A RecordBatch's length field is an int32: no inflated batch can be larger.
+constexpr size_t kMaxInflatedBytes = size_t(0x7fffffff);
+
+// Appends the decompressed bytes of `src` to `out`, which may grow to at most `max_out` bytes in
+// total (the caller passes what a batch could ever occupy, e.g. its log's capacity): a small
+// compressed record set from the network cannot claim unbounded memory.  Throws CorruptRecord on
+// malformed or oversized input (allocation failures included), KafkaError("UnsupportedCodecError
+// ...") for codecs this build cannot decode.
+void decompress(int codec, const uint8_t* src, size_t n, std::vector<uint8_t>& out,
+                size_t max_out = kMaxInflatedBytes);
 bool zstd_available();
 
 // The raw block formats (tests encode with their own minimal compressors).
-void snappy_raw_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& out);
-void lz4_block_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& out);
+void snappy_raw_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& out,
+                           size_t max_out = kMaxInflatedBytes);
+void lz4_block_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>& out,
+                          size_t max_out = kMaxInflatedBytes);
 
 }  // namespace tk

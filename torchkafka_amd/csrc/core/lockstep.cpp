@@ -20,7 +20,12 @@ void CreditLockstep::settle() {
   const Ticket t = tickets_.front();
   tickets_.pop_front();
   int64_t res[3];
+  const auto w0 = std::chrono::steady_clock::now();
   t_->wait(t.ticket, res);
+  const int64_t waited =
+      std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
+  wait_ns_ += waited;
+  step_wait_ns_ += waited;
   if (res[1] != -res[2])
     throw LockstepError("lockstep: ranks are out of step (min " + std::to_string(res[1]) + ", max " +
                         std::to_string(-res[2]) + ")");
@@ -36,6 +41,13 @@ void CreditLockstep::settle() {
 
 int CreditLockstep::next(LockstepSource& src, int64_t timeout_ms) {
   if (stopped_) return -2;
+  step_wait_ns_ = 0;
+  const int r = next_impl(src, timeout_ms);
+  if (step_wait_ns_ > step_wait_max_ns_) step_wait_max_ns_ = step_wait_ns_;
+  return r;
+}
+
+int CreditLockstep::next_impl(LockstepSource& src, int64_t timeout_ms) {
   // issue ahead while credits remain, so the round trip overlaps the delivery of granted batches
   if (tickets_.empty() && !no_more_credit_ && granted_ - step_ <= depth_ && step_ < granted_) issue(src);
   while (step_ >= granted_) {

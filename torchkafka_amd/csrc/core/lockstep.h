@@ -17,6 +17,7 @@
 // rank reached s: batches < s are finished everywhere and become committable.  Two more words
 // ride along as a consistency check: step and -step (MIN of both = min and -max).
 #pragma once
+#include <chrono>
 #include <cstdint>
 #include <deque>
 #include <functional>
@@ -77,6 +78,15 @@ class CreditLockstep {
   bool stopped() const { return stopped_; }
   uint64_t agreements() const { return agreements_; }
   int depth() const { return depth_; }
+  // Host time spent waiting for agreement results: in total, and the most one delivered step
+  // (one next() call) waited -- what the collective's round trip cost the critical path.
+  int64_t wait_ns() const { return wait_ns_; }
+  int64_t step_wait_max_ns() const { return step_wait_max_ns_; }
+  uint64_t agreements_since_reset() const { return agreements_ - agreements_at_reset_; }
+  void reset_stats() {
+    wait_ns_ = step_wait_max_ns_ = 0;
+    agreements_at_reset_ = agreements_;
+  }
 
  private:
   struct Ticket {
@@ -84,6 +94,7 @@ class CreditLockstep {
     int64_t base;  // granted at issue time
     int ticket;
   };
+  int next_impl(LockstepSource& src, int64_t timeout_ms);
   int64_t credit(LockstepSource& src) const;
   void issue(LockstepSource& src);
   void settle();
@@ -95,7 +106,8 @@ class CreditLockstep {
   int depth_;
   int64_t step_ = 0, granted_ = 0;
   bool stopped_ = false, no_more_credit_ = false;
-  uint64_t agreements_ = 0;
+  uint64_t agreements_ = 0, agreements_at_reset_ = 0;
+  int64_t wait_ns_ = 0, step_wait_max_ns_ = 0, step_wait_ns_ = 0;
   std::deque<Ticket> tickets_;
   std::deque<std::pair<int64_t, std::vector<Watermark>>> finished_q_;
   std::function<void(std::vector<Watermark>&&)> on_commit_;

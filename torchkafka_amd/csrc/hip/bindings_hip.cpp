@@ -170,6 +170,15 @@ PYBIND11_MODULE(_tkhip, m) {
              return py::make_tuple(r[0], r[1], r[2]);
            })
       .def_property_readonly("issued", &RcclLockstep::issued)
+      .def_property_readonly("nranks", &RcclLockstep::comm_count,
+                             "ranks in the private communicator, as RCCL reports them (ncclCommCount)")
+      .def(
+          "allreduce_sum",
+          [](RcclLockstep& l, int64_t v) {
+            py::gil_scoped_release nogil;
+            return l.allreduce_sum(v);
+          },
+          py::arg("value"), "blocking all-reduce(SUM) of one int64 over the private communicator")
       .def("set_timeout_ms", &RcclLockstep::set_timeout_ms, py::arg("ms"))
       .def_property_readonly("timeout_ms", &RcclLockstep::timeout_ms)
       .def_property_readonly("aborted", &RcclLockstep::aborted);
@@ -291,6 +300,9 @@ PYBIND11_MODULE(_tkhip, m) {
                s["mirror_device_bytes"] = m->device_bytes();
              }
              s["log_register_ns"] = d.log_register_ns();
+             s["lockstep_agreements"] = d.lockstep_agreements();
+             s["lockstep_wait_ns"] = d.lockstep_wait_ns();
+             s["lockstep_step_wait_max_ns"] = d.lockstep_step_wait_max_ns();
              return s;
            })
       .def("reset_stats", &MainDriver::reset_stats)

@@ -1543,6 +1543,7 @@ void MainDriver::reset_stats() {
   fast_batches_ = fast_records_ = fast_ns_ = 0;
   commit_ns_.clear();
   commit_lat_ns_.clear();
+  if (ls_) ls_->reset_stats();
 }
 
 }  // namespace tkh

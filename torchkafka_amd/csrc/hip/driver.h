@@ -211,7 +211,9 @@ class MainDriver {
   // End of a lock-stepped iteration: barrier, then every finished batch becomes committable.
   void finish_lockstep();
   bool lockstep_enabled() const { return bool(ls_); }
-  uint64_t lockstep_agreements() const { return ls_ ? ls_->agreements() : 0; }
+  uint64_t lockstep_agreements() const { return ls_ ? ls_->agreements_since_reset() : 0; }
+  int64_t lockstep_wait_ns() const { return ls_ ? ls_->wait_ns() : 0; }
+  int64_t lockstep_step_wait_max_ns() const { return ls_ ? ls_->step_wait_max_ns() : 0; }
 
   SlotView last;  // the slot most recently returned by next_slot / step_fixed
 

@@ -16,6 +16,7 @@ struct RcclApi {
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommCount)(const ncclComm_t, int*) = nullptr;
   ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;                         // optional
   ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;  // optional
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
@@ -46,6 +47,7 @@ RcclApi* load_api(const std::string& path) {
   api->CommInitRank = reinterpret_cast<decltype(api->CommInitRank)>(sym("ncclCommInitRank"));
   api->AllReduce = reinterpret_cast<decltype(api->AllReduce)>(sym("ncclAllReduce"));
   api->CommDestroy = reinterpret_cast<decltype(api->CommDestroy)>(sym("ncclCommDestroy"));
+  api->CommCount = reinterpret_cast<decltype(api->CommCount)>(sym("ncclCommCount"));
   api->GetErrorString = reinterpret_cast<decltype(api->GetErrorString)>(sym("ncclGetErrorString"));
   api->CommAbort = reinterpret_cast<decltype(api->CommAbort)>(dlsym(lib, "ncclCommAbort"));
   api->CommGetAsyncError = reinterpret_cast<decltype(api->CommGetAsyncError)>(dlsym(lib, "ncclCommGetAsyncError"));
@@ -149,6 +151,32 @@ int RcclLockstep::issue(int64_t a, int64_t b, int64_t c) {
   TKH_HIP(hipEventRecord(ev_[size_t(s)], stream_));
   ++issued_;
   return s;
+}
+
+int RcclLockstep::comm_count() const {
+  if (!comm_) throw std::runtime_error("lockstep: the RCCL communicator was aborted after a failure");
+  int n = 0;
+  check(api_, api_->CommCount(static_cast<ncclComm_t>(comm_), &n), "ncclCommCount");
+  return n;
+}
+
+int64_t RcclLockstep::allreduce_sum(int64_t v) {
+  if (aborted_) throw std::runtime_error("lockstep: the RCCL communicator was aborted after a failure");
+  // every pipelined agreement is settled first: the slots' buffers are shared with issue()
+  for (int s = 0; s < slots_; ++s) wait_event(s, "lockstep drain");
+  const int s = int(issued_ % uint64_t(slots_));
+  int64_t* hin = h_in_ + 3 * s;
+  int64_t* hout = h_out_ + 3 * s;
+  int64_t* din = d_ + 6 * s;
+  hin[0] = v;
+  TKH_HIP(hipMemcpyAsync(din, hin, sizeof(int64_t), hipMemcpyHostToDevice, stream_));
+  check(api_, api_->AllReduce(din, din + 3, 1, ncclInt64, ncclSum, static_cast<ncclComm_t>(comm_), stream_),
+        "ncclAllReduce");
+  TKH_HIP(hipMemcpyAsync(hout, din + 3, sizeof(int64_t), hipMemcpyDeviceToHost, stream_));
+  TKH_HIP(hipEventRecord(ev_[size_t(s)], stream_));
+  ++issued_;
+  wait_event(s, "lockstep allreduce_sum");
+  return hout[0];
 }
 
 bool RcclLockstep::ready(int t) { return hipEventQuery(ev_.at(size_t(t))) == hipSuccess; }

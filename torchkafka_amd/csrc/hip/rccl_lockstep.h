@@ -51,6 +51,11 @@ class RcclLockstep : public LockstepTransport {
   int world() const { return world_; }
   int rank() const { return rank_; }
   uint64_t issued() const { return issued_; }
+  // What RCCL itself reports for the communicator: its size (ncclCommCount) -- the proof that
+  // the lockstep spans `world` ranks -- and a blocking all-reduce(SUM) for start-up checks
+  // (sum of rank ids == world * (world - 1) / 2).
+  int comm_count() const;
+  int64_t allreduce_sum(int64_t v);
 
  private:
   RcclApi* api_ = nullptr;

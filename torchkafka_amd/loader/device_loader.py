@@ -412,6 +412,7 @@ class DeviceLoader:
         self.commit_sink = cfg.commit_sink
         self.lockstep = cfg.lockstep
         self.lockstep_timeout = float(cfg.lockstep_timeout)
+        self.lockstep_info: dict = {}  # how the last iteration agreed across ranks (bench / logs)
         self.h2d = cfg.h2d
         self.json_parse = cfg.json_parse
         self.decode = cfg.decode
@@ -795,11 +796,15 @@ class DeviceLoader:
                             run.rccl = self._make_rccl_lockstep(process_group)
                         else:
                             run.rccl = hip().PyLockstep(_host_allreduce_min(process_group))
+                            self.lockstep_info = {"transport": "host", "backend": dist.get_backend(process_group),
+                                                  "world_size": dist.get_world_size(process_group)}
                         run.driver.enable_lockstep(run.rccl, self.lockstep_depth)
                     else:
                         from ..parallel.lockstep import Lockstep
 
                         lock = Lockstep(process_group, None)
+                        self.lockstep_info = {"transport": "host", "backend": dist.get_backend(process_group),
+                                              "world_size": lock.world_size}
         except BaseException:
             run.close()
             raise
@@ -822,7 +827,13 @@ class DeviceLoader:
                     finished.append(self._finish_marker(prev))  # the user is done with the previous batch
                     prev = None
                 if lock is not None:
+                    t_agree = time.perf_counter_ns()
                     ok = lock.agree(item is not None, step)
+                    t_agree = time.perf_counter_ns() - t_agree
+                    st = self.stats
+                    st.lockstep_agreements += 1
+                    st.lockstep_wait_ns += t_agree
+                    st.lockstep_step_wait_max_ns = max(st.lockstep_step_wait_max_ns, t_agree)
                     if auto_commit:
                         self._commit_finished()
                     if not ok:
@@ -894,6 +905,15 @@ class DeviceLoader:
         dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
         ls = hip().RcclLockstep(lib, uid[0], rank, world, dev, self.lockstep_depth + 2)
         ls.set_timeout_ms(int(self.lockstep_timeout * 1000))
+        # start-up proof that the communicator spans the whole job: RCCL's own count of its ranks,
+        # and one all-reduce of the rank ids over it
+        nranks = int(ls.nranks)
+        rank_sum = int(ls.allreduce_sum(rank))
+        if nranks != world or rank_sum != world * (world - 1) // 2:
+            raise RuntimeError(f"lockstep: RCCL communicator has {nranks} ranks (rank-id sum {rank_sum}), "
+                               f"the process group {world}")
+        self.lockstep_info = {"transport": "rccl", "rccl_nranks": nranks, "rank_id_sum": rank_sum,
+                              "world_size": world}
         return ls
 
     def _iterate_driver(self, run: _Run, auto_commit: bool):
@@ -1177,6 +1197,10 @@ class DeviceLoader:
         self.stats.mirror_bytes += st.get("mirror_bytes_copied", 0)
         self.stats.mirror_copies += st.get("mirror_copies", 0)
         self.stats.mirror_fallbacks += st.get("mirror_fallbacks", 0)
+        self.stats.lockstep_agreements += st.get("lockstep_agreements", 0)
+        self.stats.lockstep_wait_ns += st.get("lockstep_wait_ns", 0)
+        self.stats.lockstep_step_wait_max_ns = max(self.stats.lockstep_step_wait_max_ns,
+                                                   st.get("lockstep_step_wait_max_ns", 0))
         self.stats.commits += st["commits"]
         self.stats.commit_failures += st["commit_failures"]
         self.stats.commit_ns.extend(st["commit_ns"])

@@ -56,6 +56,9 @@ class LoaderStats:
     mirror_bytes: int = 0     # h2d="dma" device decode: log bytes copied into the HBM mirror (SDMA)
     mirror_copies: int = 0
     mirror_fallbacks: int = 0  # segments read from the pinned log instead (buffer busy)
+    lockstep_agreements: int = 0      # cross-rank agreements (collectives) issued
+    lockstep_wait_ns: int = 0         # host time waiting for agreement results
+    lockstep_step_wait_max_ns: int = 0  # the most one delivered step waited for them
     started: float = field(default_factory=time.perf_counter)
     max_commit_samples: int = 100000
 
@@ -111,6 +114,9 @@ class LoaderStats:
             "mirror_mib_copied": self.mirror_bytes / 2**20,
             "mirror_copies": self.mirror_copies,
             "mirror_fallbacks": self.mirror_fallbacks,
+            "lockstep_agreements": self.lockstep_agreements,
+            "lockstep_wait_us_per_batch": self.lockstep_wait_ns / 1e3 / max(self.batches, 1),
+            "lockstep_step_wait_max_us": self.lockstep_step_wait_max_ns / 1e3,
             "commits": self.commits,
             "commit_failures": self.commit_failures,
             "commit_p50_us": percentile(c_us, 50),
