@@ -2,8 +2,9 @@
 
 The reference consumes a real cluster through kafka-python (/root/reference/src/kafka_dataset.py:
 21-22, 206).  No cluster exists here, so `KafkaWireServer` serves a synthetic broker over the
-Kafka protocol (ApiVersions, Metadata, ListOffsets, Fetch v4, FindCoordinator, OffsetCommit v2,
-OffsetFetch v1) and the native replicator (csrc/core/replicator.cpp) mirrors it into a local
+Kafka protocol (ApiVersions, Metadata, ListOffsets, Fetch, FindCoordinator, OffsetCommit,
+OffsetFetch, the group APIs, SASL) at a "legacy" (pre-2.x) and a "kafka4" (KIP-896) version
+profile, and the native replicator (csrc/core/replicator.cpp) mirrors it into a local
 broker that the loader reads.  Parity with a real Kafka broker is unpinned (none is reachable);
 the server follows the protocol's published request/response layouts.
 """
@@ -17,14 +18,16 @@ import torch
 from conftest import synth_f32
 from torchkafka_amd import DeviceLoader, FixedWidth, KafkaConsumer, KafkaDataset, auto_commit
 from torchkafka_amd.broker import KafkaBridge, KafkaWireServer, SyntheticBroker
-from torchkafka_amd.broker.wire_server import NOT_LEADER, control_batch
+from torchkafka_amd.broker.wire_server import NOT_LEADER, PROFILES as KW_PROFILES, control_batch
 from torchkafka_amd.client.records import TopicPartition
 from torchkafka_amd.ops.native import core
 
 
-@pytest.fixture
-def server(broker):
-    srv = KafkaWireServer(broker).start()
+@pytest.fixture(params=["legacy", "kafka4"])
+def server(broker, request):
+    """The test cluster at both protocol profiles: a pre-2.x broker (the versions the client used
+    to hard-code) and Kafka 4.x after KIP-896 (the pre-2.1 request versions removed)."""
+    srv = KafkaWireServer(broker, profile=request.param).start()
     try:
         yield srv
     finally:
@@ -946,21 +949,51 @@ def test_subscribe_splits_partitions_across_members(broker, server):
     assert server.group_members("g") == {}  # both left the group on close
 
 
-def test_a_rebalance_that_moves_partitions_fences_the_old_member(broker, server):
+def test_a_rebalance_moves_partitions_in_process(broker, server):
+    """A second member joins: the first one gives up half of the topic without stopping -- the
+    partitions it keeps carry on, the revoked ones stop fetching, and when the second member leaves
+    the first one gets every partition back in the next rebalance (no session-timeout wait)."""
     broker.create_topic("t", 4)
     broker.fill("t", 40, "fixed_f32", size=8)
     kw = dict(group_id="g", subscribe=True, heartbeat_interval_ms=50, session_timeout_ms=3000)
     first = bridge(server, **kw)
     try:
-        assert sorted(first.assignment) == [0, 1, 2, 3] and not first.fenced
+        assert sorted(first.assignment) == [0, 1, 2, 3] and first.wait_caught_up(10)
+        e0 = first.assignment_epoch
+        first.local.commit("g", {TopicPartition("t", p): 10 for p in range(4)})
         second = bridge(server, **kw)  # `first` rejoins on its next heartbeat; the range assignor halves t
         try:
-            assert wait_for(lambda: first.fenced, 5)
-            assert "RebalanceInProgress" in first.last_error()
-            assert len(second.assignment) == 2 and second.generation == first.generation == 2
+            assert wait_for(lambda: len(first.assignment) == 2, 5)
+            a, b = sorted(first.assignment), sorted(second.assignment)
+            assert sorted(a + b) == [0, 1, 2, 3] and second.generation == first.generation == 2
+            assert first.assignment_epoch > e0 and first.rebalances == 1 and not first.fenced
+            # what first consumed before the rebalance reached the cluster; second starts there
+            assert broker.committed_offsets("g", "t") == {p: 10 for p in range(4)}
+            assert {s["partition"]: s["start_offset"] for s in second.stats() if s["owned"]} == {p: 10 for p in b}
             assert second.wait_caught_up(10)
+            # new records reach each partition's new owner only
+            broker.fill("t", 5, "fixed_f32", size=8)
+            assert first.wait_caught_up(10) and second.wait_caught_up(10)
+            for p in a:
+                assert first.local.end_offset("t", p) == 45
+            for p in b:
+                assert second.local.end_offset("t", p) == 45 and first.local.end_offset("t", p) == 40
+            second.local.commit("g", {TopicPartition("t", p): 45 for p in b})
+            assert wait_for(lambda: all(broker.committed_offsets("g", "t")[p] == 45 for p in b))
         finally:
             second.close()
+        # the survivor takes every partition back within one rebalance; those it gets back restart
+        # at the group's committed offset (45), not where its own replica stopped (40)
+        assert wait_for(lambda: sorted(first.assignment) == [0, 1, 2, 3], 5)
+        assert first.generation == 3 and first.errors == 0
+        starts = {s["partition"]: s["start_offset"] for s in first.stats()}
+        assert all(starts[p] == 45 for p in b)
+        epochs = dict(first.assignment_epochs())
+        assert all(epochs[p] > epochs[q] for p in b for q in a)
+        assert first.wait_caught_up(10)
+        for p in b:
+            assert first.local.end_offset("t", p) == 45
+            assert first.local.committed_offsets("g", "t")[p] == 45
     finally:
         first.close()
 
@@ -975,7 +1008,7 @@ def test_a_rebalance_that_keeps_the_partitions_carries_on(broker, server):
     try:
         b = bridge(server, "u", **kw)  # another topic in the same group: a keeps all of t
         try:
-            assert wait_for(lambda: a.generation == 2, 5) and not a.fenced
+            assert wait_for(lambda: a.generation == 2, 5) and a.rebalances == 1
             assert sorted(a.assignment) == [0, 1] and sorted(b.assignment) == [0, 1]
             a.local.commit("g", {TopicPartition("t", 0): 30})
             assert wait_for(lambda: broker.committed_offsets("g", "t").get(0) == 30)  # generation 2 commit
@@ -983,6 +1016,68 @@ def test_a_rebalance_that_keeps_the_partitions_carries_on(broker, server):
             b.close()
     finally:
         a.close()
+
+
+# ---- protocol version negotiation (ApiVersions)
+
+def test_client_negotiates_the_highest_common_version(broker, server):
+    broker.create_topic("t", 2)
+    broker.fill("t", 30, "fixed_f32", size=8)
+    kw = dict(group_id="g", subscribe=True, heartbeat_interval_ms=50, session_timeout_ms=3000)
+    with bridge(server, **kw) as br:
+        assert br.wait_caught_up(10)
+        br.local.commit("g", {TopicPartition("t", 0): 30})
+        assert wait_for(lambda: broker.committed_offsets("g", "t").get(0) == 30)
+    seen = {k: max(v) for k, v in server.request_versions.items()}
+    cv = core().client_versions()
+    for key, (lo, hi) in server.versions.items():
+        if key in seen and key in cv:
+            assert seen[key] == min(hi, cv[key][1]), (key, seen[key])
+    if server.profile == "kafka4":
+        assert (seen[3], seen[1], seen[11], seen[14], seen[8], seen[9], seen[2], seen[10]) == (8, 11, 5, 3, 7, 5, 5, 2)
+    else:  # the versions the client hard-coded before it negotiated
+        assert (seen[3], seen[1], seen[11], seen[14], seen[8], seen[9], seen[2], seen[10]) == (1, 4, 0, 0, 2, 1, 1, 0)
+
+
+def test_ancient_broker_without_api_versions(broker):
+    """A broker that predates ApiVersions closes the connection on it: the client reconnects and
+    uses the fixed pre-negotiation versions."""
+    broker.create_topic("t", 2)
+    broker.fill("t", 30, "fixed_f32", size=8, records_per_batch=10)
+    with KafkaWireServer(broker, profile="ancient") as srv:
+        c = core().WireClient(srv.address)
+        assert c.list_offsets("t", [0, 1], -1) == {0: 30, 1: 30}
+        assert c.offset_commit("g", "t", {1: 7}) == {1: 0} and c.offset_fetch("g", "t", [1]) == {1: 7}
+        with bridge(srv, group_id="g") as br:
+            assert br.wait_caught_up(10)
+            assert log_bytes(br.local, "t", 0) == log_bytes(broker, "t", 0)
+        assert 18 not in srv.request_versions or srv.requests[18] >= 1
+
+
+def test_no_common_version_is_unsupported_version(broker):
+    broker.create_topic("t", 1)
+    future = dict(KW_PROFILES["kafka4"])
+    future[3] = (12, 13)  # a broker that only speaks Metadata v12+ (flexible versions)
+    with KafkaWireServer(broker, profile=future) as srv:
+        c = core().WireClient(srv.address)
+        with pytest.raises(Exception, match="UnsupportedVersionError"):
+            c.metadata("t")
+
+
+@pytest.mark.parametrize("profile", ["legacy", "kafka4", "ancient"])
+def test_native_server_profiles(broker, profile):
+    from torchkafka_amd.broker import NativeWireServer
+
+    broker.create_topic("t", 2)
+    broker.fill("t", 300, "fixed_f32", size=16, records_per_batch=30)
+    with NativeWireServer(broker, profile=profile) as srv:
+        c = core().WireClient(srv.address)
+        assert c.list_offsets("t", [0, 1], -2) == {0: 0, 1: 0}
+        assert c.offset_commit("g", "t", {0: 5}) == {0: 0} and c.offset_fetch("g", "t", [0, 1]) == {0: 5, 1: -1}
+        with bridge(srv, group_id="g", max_partition_fetch_bytes=8192) as br:
+            assert br.wait_caught_up(10) and br.errors == 0
+            for p in range(2):  # partition 0 starts at the committed 5, inside the first batch
+                assert log_bytes(br.local, "t", p) == log_bytes(broker, "t", p)
 
 
 def test_subscribe_needs_a_group(broker, server):

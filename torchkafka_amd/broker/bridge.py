@@ -87,16 +87,18 @@ class KafkaBridge:
                  ssl_certfile: str | None = None, ssl_keyfile: str | None = None, sasl_mechanism: str | None = None,
                  sasl_plain_username: str | None = None, sasl_plain_password: str | None = None,
                  subscribe: bool = False, session_timeout_ms: int = 10000, heartbeat_interval_ms: int = 3000,
-                 partition_assignment_strategy: Iterable[str] = ("range",), start: bool = True):
+                 partition_assignment_strategy: Iterable[str] = ("range",), rebalance_timeout_ms: int = 0,
+                 start: bool = True):
         """``subscribe=True`` (needs ``group_id``, excludes ``partitions``): join the consumer group
-        like kafka-python's ``subscribe()`` -- JoinGroup/SyncGroup with the range assignor -- and
-        mirror the partitions the coordinator assigns (:attr:`assignment`).  On a rebalance the
-        bridge commits and rejoins; with the same partitions back it carries on, otherwise it
-        stops fetching and forwarding (:attr:`fenced`, RebalanceInProgressError in
-        :meth:`last_error`) and the job re-shards by restarting.  ``partition_assignment_strategy``:
-        assignor names in preference order, "range" and/or "roundrobin" (kafka-python's two).
-        Default: the static
-        ``partitions`` (kafka-python's ``assign()``)."""
+        like kafka-python's ``subscribe()`` -- JoinGroup/SyncGroup with the range or round-robin
+        assignor -- and mirror the partitions the coordinator assigns (:attr:`assignment`).
+        Rebalances are followed in process, as kafka-python does: the bridge forwards what was
+        consumed, rejoins, stops fetching revoked partitions and starts newly assigned ones at the
+        group's committed offset; :attr:`assignment_epoch` tells the replica's consumers which
+        partitions (re)started.  ``partition_assignment_strategy``: assignor names in preference
+        order, "range" and/or "roundrobin" (kafka-python's two).  ``rebalance_timeout_ms``: how
+        long the coordinator waits for members to rejoin (JoinGroup v1+; 0: the session timeout).
+        Default: the static ``partitions`` (kafka-python's ``assign()``)."""
         if subscribe and not group_id:
             raise ValueError("subscribe=True needs a group_id")
         if subscribe and partitions is not None:
@@ -110,6 +112,7 @@ class KafkaBridge:
         if ring_bytes is None:  # a ring frees space as the group commits: without a group, a linear log
             ring_bytes = min(512 << 20, int(log_capacity)) if group_id else 0
         self._own = url is None
+        self._subscribe = bool(subscribe)
         # a fresh local broker (or an existing persistent replica: file:// URLs resume their logs)
         self.local = SyntheticBroker(self.url, create=True, log_capacity=log_capacity,
                                      index_capacity=index_capacity)
@@ -130,7 +133,8 @@ class KafkaBridge:
                                          sasl_plain_password=sasl_plain_password),
                 subscribe=bool(subscribe), session_timeout_ms=int(session_timeout_ms),
                 heartbeat_interval_ms=int(heartbeat_interval_ms),
-                assignors=[str(a) for a in partition_assignment_strategy])
+                assignors=[str(a) for a in partition_assignment_strategy],
+                rebalance_timeout_ms=int(rebalance_timeout_ms))
         except BaseException:
             if not self.url.startswith("file://"):  # a fresh shm replica nobody else can use
                 self.local.destroy()
@@ -191,9 +195,32 @@ class KafkaBridge:
         return list(self._r.stats())
 
     @property
+    def subscribed(self) -> bool:
+        """Group-managed (subscribe mode): the assignment follows the group's rebalances."""
+        return bool(self._subscribe)
+
+    @property
     def assignment(self) -> list[int]:
         """The partitions this bridge mirrors (subscribe mode: what the coordinator assigned)."""
-        return list(self._r.assignment) if self._r.member_id else [s["partition"] for s in self.stats()]
+        if self._subscribe:
+            return sorted(self._r.assignment)
+        return [s["partition"] for s in self.stats()]
+
+    @property
+    def assignment_epoch(self) -> int:
+        """Bumped by every assignment change (subscribe mode)."""
+        return int(self._r.assignment_epoch)
+
+    def assignment_epochs(self) -> list[tuple[int, int]]:
+        """``[(partition, epoch at which it was (re)assigned)]`` of the partitions owned now: a
+        consumer that holds state of a partition from an older epoch must drop it (the partition
+        was revoked and handed back, and restarted at the group's committed offset)."""
+        return [(int(p), int(e)) for p, e in self._r.assignment_epochs()]
+
+    @property
+    def rebalances(self) -> int:
+        """Rebalances this member went through since it started."""
+        return int(self._r.rebalances)
 
     @property
     def member_id(self) -> str:
@@ -205,8 +232,8 @@ class KafkaBridge:
 
     @property
     def fenced(self) -> bool:
-        """Subscribe mode: the group rebalanced under this bridge (it stopped fetching and committing)."""
-        return bool(self._r.fenced)
+        """Always False: rebalances are followed in process (kept for API compatibility)."""
+        return False
 
     @property
     def errors(self) -> int:

@@ -33,16 +33,32 @@ from .synthetic import SyntheticBroker
 
 API_FETCH, API_LIST_OFFSETS, API_METADATA = 1, 2, 3
 API_OFFSET_COMMIT, API_OFFSET_FETCH, API_FIND_COORDINATOR, API_API_VERSIONS = 8, 9, 10, 18
-# api key -> (min, max) version served
 API_JOIN_GROUP, API_HEARTBEAT, API_LEAVE_GROUP, API_SYNC_GROUP = 11, 12, 13, 14
-SUPPORTED = {API_FETCH: (4, 4), API_LIST_OFFSETS: (0, 1), API_METADATA: (0, 1), API_OFFSET_COMMIT: (2, 2),
-             API_OFFSET_FETCH: (1, 1), API_FIND_COORDINATOR: (0, 0), API_API_VERSIONS: (0, 0),
-             API_JOIN_GROUP: (0, 0), API_HEARTBEAT: (0, 0), API_LEAVE_GROUP: (0, 0), API_SYNC_GROUP: (0, 0)}
+API_SASL_HANDSHAKE, API_SASL_AUTHENTICATE = 17, 36
+
+# Version profiles: api key -> (min, max) served.  Requests outside a range close the connection,
+# as a Kafka broker does; ApiVersions above its range answers UNSUPPORTED_VERSION in the v0 format.
+#   legacy  -- a pre-2.x broker: exactly the versions the native client used before it negotiated;
+#   kafka4  -- Kafka 4.x after KIP-896 dropped the pre-2.1 request versions (modelled strictly: the
+#              minimums below are at or above the real broker's), up to what this server implements;
+#   ancient -- a broker that predates ApiVersions (0.9): the legacy set, and ApiVersions closes the
+#              connection (clients must fall back to fixed versions).
+PROFILES = {
+    "legacy": {API_FETCH: (4, 4), API_LIST_OFFSETS: (0, 1), API_METADATA: (0, 1), API_OFFSET_COMMIT: (2, 2),
+               API_OFFSET_FETCH: (1, 1), API_FIND_COORDINATOR: (0, 0), API_API_VERSIONS: (0, 0),
+               API_JOIN_GROUP: (0, 0), API_HEARTBEAT: (0, 0), API_LEAVE_GROUP: (0, 0), API_SYNC_GROUP: (0, 0),
+               API_SASL_HANDSHAKE: (0, 1), API_SASL_AUTHENTICATE: (0, 0)},
+    "kafka4": {API_FETCH: (4, 11), API_LIST_OFFSETS: (1, 5), API_METADATA: (4, 8), API_OFFSET_COMMIT: (2, 7),
+               API_OFFSET_FETCH: (1, 5), API_FIND_COORDINATOR: (0, 2), API_API_VERSIONS: (0, 2),
+               API_JOIN_GROUP: (2, 5), API_HEARTBEAT: (0, 3), API_LEAVE_GROUP: (0, 2), API_SYNC_GROUP: (0, 3),
+               API_SASL_HANDSHAKE: (1, 1), API_SASL_AUTHENTICATE: (0, 1)},
+}
+PROFILES["ancient"] = {k: v for k, v in PROFILES["legacy"].items() if k != API_API_VERSIONS}
+SUPPORTED = PROFILES["legacy"]  # the default profile
 
 NONE, OFFSET_OUT_OF_RANGE, UNKNOWN_TOPIC, NOT_LEADER, UNSUPPORTED_VERSION = 0, 1, 3, 6, 35
 ILLEGAL_GENERATION, UNSUPPORTED_SASL_MECHANISM, SASL_AUTHENTICATION_FAILED = 22, 33, 58
-UNKNOWN_MEMBER_ID, REBALANCE_IN_PROGRESS = 25, 27
-API_SASL_HANDSHAKE, API_SASL_AUTHENTICATE = 17, 36
+UNKNOWN_MEMBER_ID, REBALANCE_IN_PROGRESS, MEMBER_ID_REQUIRED = 25, 27, 79
 SASL_MECHANISMS = ("PLAIN", "SCRAM-SHA-256", "SCRAM-SHA-512")
 
 
@@ -157,6 +173,7 @@ class _Group:
         self.leader = ""
         self.protocol = ""
         self.assignments: dict[str, bytes] = {}
+        self.pending: set[str] = set()       # ids handed out with MEMBER_ID_REQUIRED, not joined yet
         self.min_end = self.deadline = 0.0
 
 
@@ -165,13 +182,20 @@ class KafkaWireServer:
 
     def __init__(self, broker: SyntheticBroker, host: str = "127.0.0.1", port: int = 0, node_id: int = 0,
                  cluster: list[tuple[int, str, int]] | None = None, ssl_context=None,
-                 sasl_users: dict[str, str] | None = None):
+                 sasl_users: dict[str, str] | None = None, profile: "str | dict" = "legacy"):
         """``cluster``: every node of a multi-node test cluster as (node_id, host, port), this one
         included; partition p is led by ``cluster[p % len(cluster)]`` and fetches sent to another
         node answer NOT_LEADER.  None: a single-node cluster (this server leads everything).
         ``ssl_context``: a server-side ``ssl.SSLContext`` (listeners SSL / SASL_SSL).  ``sasl_users``:
         {user: password} accepted by SASL/PLAIN; every request but ApiVersions and the SASL exchange
-        closes the connection until it authenticated."""
+        closes the connection until it authenticated.  ``profile``: the request versions served
+        (:data:`PROFILES`: "legacy", "kafka4", "ancient"; or an ``{api key: (min, max)}`` dict)."""
+        if isinstance(profile, dict):
+            self.profile, self.versions = "custom", dict(profile)
+        elif profile in PROFILES:
+            self.profile, self.versions = profile, PROFILES[profile]
+        else:
+            raise ValueError(f"profile {profile!r}: one of {sorted(PROFILES)} or an {{api: (min, max)}} dict")
         self.ssl_context = ssl_context
         self.sasl_users = sasl_users
         self.broker = broker
@@ -183,6 +207,8 @@ class KafkaWireServer:
         self.partial_tail = False          # cut every record set inside its last batch
         self.stall_s = 0.0                 # fault injection: hold every Fetch this long (a hung broker)
         self.requests: dict[int, int] = {}  # api key -> count
+        self.request_versions: dict[int, set] = {}  # api key -> versions seen (tests)
+        self.commit_log: list = []          # (group, topic, partition, offset) of every accepted commit
         self._views: dict[int, memoryview] = {}
         self._conns: set = set()
         self._groups: dict[str, _Group] = {}
@@ -286,9 +312,26 @@ class KafkaWireServer:
         r.str()  # client id
         with self._lock:
             self.requests[key] = self.requests.get(key, 0) + 1
+            self.request_versions.setdefault(key, set()).add(ver)
         w = _W()
         w.i32(corr)
         state = {"authed": True} if state is None else state
+        lo_hi = self.versions.get(key)
+        if key == API_API_VERSIONS:
+            if lo_hi is None:
+                return None  # predates ApiVersions: the connection just closes
+            err = NONE if lo_hi[0] <= ver <= lo_hi[1] else UNSUPPORTED_VERSION
+            w.i16(err)
+            w.i32(len(self.versions))
+            for k, (lo, hi) in sorted(self.versions.items()):
+                w.i16(k)
+                w.i16(lo)
+                w.i16(hi)
+            if err == NONE and ver >= 1:
+                w.i32(0)  # throttle
+            return w.data()
+        if lo_hi is None or not lo_hi[0] <= ver <= lo_hi[1]:
+            return None  # a real broker closes the connection on an unsupported version
         if key == API_SASL_HANDSHAKE:
             mech = r.str()
             ok = self.sasl_users is not None and mech in SASL_MECHANISMS
@@ -305,20 +348,11 @@ class KafkaWireServer:
             w.i16(NONE if ok else SASL_AUTHENTICATION_FAILED)
             w.str(None if ok else "Authentication failed: invalid username or password")
             w.bytes(reply if ok else b"")
+            if ver >= 1:
+                w.i64(0)  # session lifetime: no re-authentication required
             return w.data()
-        if not state["authed"] and key != API_API_VERSIONS:
+        if not state["authed"]:
             return None  # a SASL listener drops unauthenticated requests
-        lo_hi = SUPPORTED.get(key)
-        if key == API_API_VERSIONS:
-            w.i16(NONE)
-            w.i32(len(SUPPORTED))
-            for k, (lo, hi) in sorted(SUPPORTED.items()):
-                w.i16(k)
-                w.i16(lo)
-                w.i16(hi)
-            return w.data()
-        if lo_hi is None or not lo_hi[0] <= ver <= lo_hi[1]:
-            return None  # a real broker closes the connection on an unsupported version
         getattr(self, f"_api_{key}")(r, ver, w)
         return w.data()
 
@@ -369,8 +403,15 @@ class KafkaWireServer:
             return self.broker.topics()
         return [r.str() for _ in range(n)]
 
-    def _api_3(self, r: _R, ver: int, w: _W) -> None:  # Metadata v0/v1
+    def _api_3(self, r: _R, ver: int, w: _W) -> None:  # Metadata v0-v8
         names = self._topic_names(r, ver)
+        if ver >= 4:
+            r.i8()  # allow_auto_topic_creation (topics are never created here)
+        if ver >= 8:
+            r.i8()
+            r.i8()  # include cluster / topic authorized operations
+        if ver >= 3:
+            w.i32(0)  # throttle
         w.i32(len(self.cluster))
         for nid, host, port in self.cluster:
             w.i32(nid)
@@ -378,6 +419,8 @@ class KafkaWireServer:
             w.i32(port)
             if ver >= 1:
                 w.str(None)  # rack
+        if ver >= 2:
+            w.str("torchkafka-synthetic")  # cluster id
         if ver >= 1:
             w.i32(self.cluster[0][0])  # controller
         w.i32(len(names))
@@ -388,6 +431,8 @@ class KafkaWireServer:
                 if ver >= 1:
                     w.i8(0)
                 w.i32(0)
+                if ver >= 8:
+                    w.i32(-2147483648)  # authorized operations: not requested
                 continue
             n = self.broker.topic(name)[1]
             w.i16(NONE)
@@ -400,16 +445,27 @@ class KafkaWireServer:
                 w.i16(NONE)
                 w.i32(p)
                 w.i32(leader)
+                if ver >= 7:
+                    w.i32(0)  # leader epoch
                 w.i32(1)
                 w.i32(leader)
                 w.i32(1)
                 w.i32(leader)
+                if ver >= 5:
+                    w.i32(0)  # offline replicas
+            if ver >= 8:
+                w.i32(-2147483648)
+        if ver >= 8:
+            w.i32(-2147483648)
 
     def leader(self, partition: int) -> int:
         return self.cluster[partition % len(self.cluster)][0]
 
-    def _api_2(self, r: _R, ver: int, w: _W) -> None:  # ListOffsets v0/v1
+    def _api_2(self, r: _R, ver: int, w: _W) -> None:  # ListOffsets v0-v5
         r.i32()  # replica
+        if ver >= 2:
+            r.i8()  # isolation level
+            w.i32(0)  # throttle
         nt = r.i32()
         w.i32(nt)
         for _ in range(nt):
@@ -418,7 +474,10 @@ class KafkaWireServer:
             w.str(name)
             w.i32(np_)
             for _ in range(np_):
-                p, ts = r.i32(), r.i64()
+                p = r.i32()
+                if ver >= 4:
+                    r.i32()  # current leader epoch
+                ts = r.i64()
                 if ver == 0:
                     r.i32()  # max offsets
                 err, off = NONE, -1
@@ -442,17 +501,31 @@ class KafkaWireServer:
                 else:
                     w.i64(-1)
                     w.i64(off)
+                    if ver >= 4:
+                        w.i32(0)  # leader epoch
 
-    def _api_1(self, r: _R, ver: int, w: _W) -> None:  # Fetch v4
+    def _api_1(self, r: _R, ver: int, w: _W) -> None:  # Fetch v4-v11 (sessionless)
         if self.stall_s:
             time.sleep(self.stall_s)
         r.i32()  # replica
         max_wait, min_bytes, max_bytes = r.i32(), r.i32(), r.i32()
         r.i8()  # isolation level
+        if ver >= 7:
+            r.i32()
+            r.i32()  # session id / epoch: every fetch is answered in full (no incremental sessions)
         reqs = []
         for _ in range(r.i32()):
             name = r.str()
-            reqs.append((name, [(r.i32(), r.i64(), r.i32()) for _ in range(r.i32())]))
+            parts = []
+            for _ in range(r.i32()):
+                p = r.i32()
+                if ver >= 9:
+                    r.i32()  # current leader epoch
+                off = r.i64()
+                if ver >= 5:
+                    r.i64()  # log start offset (a follower's)
+                parts.append((p, off, r.i32()))
+            reqs.append((name, parts))
         faults = {}
         with self._lock:  # one injected error per partition per request
             for name, parts in reqs:
@@ -467,7 +540,11 @@ class KafkaWireServer:
                 break
             time.sleep(0.002)
         w.i32(0)  # throttle
+        if ver >= 7:
+            w.i16(NONE)
+            w.i32(0)  # session id: none
         w.i32(len(out))
+        nat = self.broker.native
         for name, parts in out:
             w.str(name)
             w.i32(len(parts))
@@ -476,7 +553,14 @@ class KafkaWireServer:
                 w.i16(err)
                 w.i64(hw)
                 w.i64(hw)   # last stable offset
+                if ver >= 5:
+                    try:
+                        w.i64(nat.log_start_offset(self.broker.pidx(name, p)))
+                    except Exception:  # noqa: BLE001
+                        w.i64(-1)
                 w.i32(-1)   # aborted transactions: null
+                if ver >= 11:
+                    w.i32(-1)  # preferred read replica: none
                 w.bytes(data)
 
     def _fetch_once(self, reqs, max_bytes: int, faults: dict):
@@ -516,18 +600,25 @@ class KafkaWireServer:
             out.append((name, po))
         return out, total
 
-    def _api_10(self, r: _R, ver: int, w: _W) -> None:  # FindCoordinator v0
+    def _api_10(self, r: _R, ver: int, w: _W) -> None:  # FindCoordinator v0-v2
         r.str()
+        if ver >= 1:
+            r.i8()  # key type
+            w.i32(0)  # throttle
         w.i16(NONE)
+        if ver >= 1:
+            w.str(None)  # error message
         w.i32(self.node_id)
         w.str(self.host)
         w.i32(self.port)
 
     # ------------------------------------------------------------ group membership (coordinator)
-    # JoinGroup / SyncGroup / Heartbeat / LeaveGroup v0 with Kafka's state machine, reduced to what
-    # a test needs: a join round ends once every member of the last generation rejoined (a fresh
-    # group waits ``join_delay_s`` for more joiners) or after the rebalance timeout, which drops
-    # the absentees; the first joiner leads and sends the assignment through SyncGroup.
+    # JoinGroup v0-v5 / SyncGroup v0-v3 / Heartbeat v0-v3 / LeaveGroup v0-v2 with Kafka's state
+    # machine, reduced to what a test needs: a join round ends once every member of the last
+    # generation rejoined (a fresh group waits ``join_delay_s`` for more joiners) or after the
+    # rebalance timeout (v1+; the session timeout at v0), which drops the absentees; the first
+    # joiner leads and sends the assignment through SyncGroup.  From JoinGroup v4 a member joining
+    # without an id gets MEMBER_ID_REQUIRED and an id to join again with (KIP-394).
     def _group(self, name: str) -> "_Group":
         g = self._groups.get(name)
         if g is None:
@@ -541,8 +632,13 @@ class KafkaWireServer:
             g.min_end = now + (self.join_delay_s if not g.members else 0.0)
             g.deadline = now + max(timeout_s, self.join_delay_s)
 
-    def _api_11(self, r: _R, ver: int, w: _W) -> None:  # JoinGroup v0 (blocks until the round ends)
-        group, session_ms, member, _ptype = r.str(), r.i32(), r.str() or "", r.str()
+    def _api_11(self, r: _R, ver: int, w: _W) -> None:  # JoinGroup v0-v5 (blocks until the round ends)
+        group, session_ms = r.str(), r.i32()
+        rebalance_ms = r.i32() if ver >= 1 else session_ms
+        member = r.str() or ""
+        if ver >= 5:
+            r.str()  # group instance id (static membership is not modelled)
+        r.str()  # protocol type
         protos: list[tuple[str, bytes]] = []
         for _ in range(r.i32()):
             name = r.str()
@@ -551,11 +647,17 @@ class KafkaWireServer:
             r.o += n
         with self._gcond:
             g = self._group(group)
-            if member and member not in g.members and member not in g.joining:
-                self._join_reply(w, UNKNOWN_MEMBER_ID, -1, "", "", member, {})
+            if not member and ver >= 4:
+                member = f"member-{uuid.uuid4().hex[:12]}"
+                g.pending.add(member)
+                self._join_reply(w, ver, MEMBER_ID_REQUIRED, -1, "", "", member, {})
                 return
+            if member and member not in g.members and member not in g.joining and member not in g.pending:
+                self._join_reply(w, ver, UNKNOWN_MEMBER_ID, -1, "", "", member, {})
+                return
+            g.pending.discard(member)
             member = member or f"member-{uuid.uuid4().hex[:12]}"
-            self._begin_round(g, session_ms / 1000.0)
+            self._begin_round(g, rebalance_ms / 1000.0)
             g.joining[member] = dict(protos)  # assignor name -> subscription metadata
             gen0 = g.generation
             self._gcond.notify_all()
@@ -573,13 +675,15 @@ class KafkaWireServer:
                     break
                 self._gcond.wait(0.01)
             if member not in g.members:  # joined after the round closed: rejoin
-                self._join_reply(w, REBALANCE_IN_PROGRESS, -1, "", "", member, {})
+                self._join_reply(w, ver, REBALANCE_IN_PROGRESS, -1, "", "", member, {})
                 return
-            self._join_reply(w, NONE, g.generation, g.protocol, g.leader, member,
+            self._join_reply(w, ver, NONE, g.generation, g.protocol, g.leader, member,
                              g.members if member == g.leader else {})
 
     @staticmethod
-    def _join_reply(w: _W, err, gen, proto, leader, member, members) -> None:
+    def _join_reply(w: _W, ver, err, gen, proto, leader, member, members) -> None:
+        if ver >= 2:
+            w.i32(0)  # throttle
         w.i16(err)
         w.i32(gen)
         w.str(proto)
@@ -588,6 +692,8 @@ class KafkaWireServer:
         w.i32(len(members))
         for m, meta in members.items():
             w.str(m)
+            if ver >= 5:
+                w.str(None)  # group instance id
             w.bytes(meta)
 
     def _member_error(self, g: "_Group | None", gen: int, member: str) -> int:
@@ -597,8 +703,10 @@ class KafkaWireServer:
             return ILLEGAL_GENERATION
         return NONE
 
-    def _api_14(self, r: _R, ver: int, w: _W) -> None:  # SyncGroup v0
+    def _api_14(self, r: _R, ver: int, w: _W) -> None:  # SyncGroup v0-v3
         group, gen, member = r.str(), r.i32(), r.str() or ""
+        if ver >= 3:
+            r.str()  # group instance id
         assign = {}
         for _ in range(r.i32()):
             m = r.str()
@@ -616,20 +724,28 @@ class KafkaWireServer:
                 self._gcond.wait(0.01)
             if err == NONE and (g.generation != gen or g.state != "stable"):
                 err = REBALANCE_IN_PROGRESS
+            if ver >= 1:
+                w.i32(0)  # throttle
             w.i16(err)
             w.bytes(g.assignments.get(member, b"") if err == NONE else b"")
 
-    def _api_12(self, r: _R, ver: int, w: _W) -> None:  # Heartbeat v0
+    def _api_12(self, r: _R, ver: int, w: _W) -> None:  # Heartbeat v0-v3
         group, gen, member = r.str(), r.i32(), r.str() or ""
+        if ver >= 3:
+            r.str()  # group instance id
         with self._gcond:
             g = self._groups.get(group)
             err = self._member_error(g, gen, member)
             if err == NONE and g.state == "joining":
                 err = REBALANCE_IN_PROGRESS
+            if ver >= 1:
+                w.i32(0)  # throttle
             w.i16(err)
 
-    def _api_13(self, r: _R, ver: int, w: _W) -> None:  # LeaveGroup v0
+    def _api_13(self, r: _R, ver: int, w: _W) -> None:  # LeaveGroup v0-v2
         group, member = r.str(), r.str() or ""
+        if ver >= 1:
+            w.i32(0)  # throttle
         with self._gcond:
             g = self._groups.get(group)
             if g is None or member not in g.members:
@@ -649,15 +765,25 @@ class KafkaWireServer:
             g = self._groups.get(group)
             return {} if g is None else {m: g.assignments.get(m, b"") for m in g.members}
 
-    def _api_8(self, r: _R, ver: int, w: _W) -> None:  # OffsetCommit v2
+    def committed(self, group: str, topic: str, partition: int) -> int:
+        """The group's committed offset of a partition (-1: none) -- what the cluster holds (tests)."""
+        nat = self.broker.native
+        return nat.committed(nat.group_index(group, True), self.broker.pidx(topic, partition))[0]
+
+    def _api_8(self, r: _R, ver: int, w: _W) -> None:  # OffsetCommit v2-v7
         group = r.str()
         gen = r.i32()
         member = r.str() or ""
-        r.i64()   # retention
+        if ver >= 7:
+            r.str()  # group instance id
+        if ver <= 4:
+            r.i64()   # retention
         with self._gcond:
             fenced = NONE if gen == -1 else self._member_error(self._groups.get(group), gen, member)
         nat = self.broker.native
         g = nat.group_index(group, True)
+        if ver >= 3:
+            w.i32(0)  # throttle
         nt = r.i32()
         w.i32(nt)
         for _ in range(nt):
@@ -667,30 +793,40 @@ class KafkaWireServer:
             w.i32(np_)
             for _ in range(np_):
                 p, off = r.i32(), r.i64()
+                if ver >= 6:
+                    r.i32()  # committed leader epoch
                 meta = r.str() or ""
                 with self._lock:
                     err = self._commit_faults.pop(0) if self._commit_faults else fenced
                 if err == NONE:
                     try:
                         nat.commit(g, -1, 0, 0, [(self.broker.pidx(name, p), int(off), meta)])
+                        with self._lock:
+                            self.commit_log.append((group, name, p, int(off)))
                     except Exception:  # noqa: BLE001 -- a group with live members refuses a simple commit
                         err = ILLEGAL_GENERATION
                 w.i32(p)
                 w.i16(err)
 
-    def _api_9(self, r: _R, ver: int, w: _W) -> None:  # OffsetFetch v1
+    def _api_9(self, r: _R, ver: int, w: _W) -> None:  # OffsetFetch v1-v5
         group = r.str()
         nat = self.broker.native
         g = nat.group_index(group, True)
+        if ver >= 3:
+            w.i32(0)  # throttle
         nt = r.i32()
-        w.i32(nt)
-        for _ in range(nt):
-            name = r.str()
-            np_ = r.i32()
+        if nt < 0:  # v2+: every topic of the group
+            reqs = [(t, list(range(self.broker.topic(t)[1]))) for t in self.broker.topics()]
+        else:
+            reqs = []
+            for _ in range(nt):
+                name = r.str()
+                reqs.append((name, [r.i32() for _ in range(r.i32())]))
+        w.i32(len(reqs))
+        for name, parts in reqs:
             w.str(name)
-            w.i32(np_)
-            for _ in range(np_):
-                p = r.i32()
+            w.i32(len(parts))
+            for p in parts:
                 try:
                     off, meta = nat.committed(g, self.broker.pidx(name, p))
                     err = NONE
@@ -698,8 +834,12 @@ class KafkaWireServer:
                     off, meta, err = -1, "", UNKNOWN_TOPIC
                 w.i32(p)
                 w.i64(off)
+                if ver >= 5:
+                    w.i32(-1)  # committed leader epoch
                 w.str(meta)
                 w.i16(err)
+        if ver >= 2:
+            w.i16(NONE)
 
 
 def _last_batch_start(data: bytes) -> int:
@@ -749,12 +889,13 @@ class NativeWireServer:
     ``cluster``: every node as (node_id, host, port); partition p is led by node p % len(cluster)."""
 
     def __init__(self, broker: SyntheticBroker, host: str = "127.0.0.1", port: int = 0, node_id: int = 0,
-                 cluster: list[tuple[int, str, int]] | None = None):
+                 cluster: list[tuple[int, str, int]] | None = None, profile: str = "legacy"):
         from ..ops.native import core
 
         self.broker = broker
         self.host = host
-        self._s = core().WireServer(broker.native, host, int(port), int(node_id), list(cluster or []))
+        self.profile = profile
+        self._s = core().WireServer(broker.native, host, int(port), int(node_id), list(cluster or []), profile)
         self.port = self._s.port
 
     @property

@@ -191,6 +191,11 @@ PYBIND11_MODULE(_tkcore, m) {
     return py::bytes(reinterpret_cast<const char*>(out.data()), out.size());
   });
   m.def("zstd_available", &zstd_available);
+  m.def("client_versions", []() {
+    std::map<int16_t, std::pair<int16_t, int16_t>> out;
+    for (auto& [k, r] : wire::client_versions()) out[k] = {r.min, r.max};
+    return out;
+  }, "{api key: (min, max)} request versions the native Kafka client implements");
   // Kafka's range assignor over (member id, subscribed topics): {member: {topic: [partitions]}}
   m.def("range_assign", [](const std::vector<std::pair<std::string, std::vector<std::string>>>& members,
                            const std::map<std::string, int32_t>& counts, bool rr) {
@@ -533,13 +538,14 @@ PYBIND11_MODULE(_tkcore, m) {
 
   py::class_<WireServer>(m, "WireServer")
       .def(py::init([](std::shared_ptr<Broker> b, const std::string& host, int port, int32_t node_id,
-                       std::vector<std::tuple<int32_t, std::string, int32_t>> cluster) {
+                       std::vector<std::tuple<int32_t, std::string, int32_t>> cluster, const std::string& profile) {
              std::vector<WireNode> nodes;
              for (auto& [id, h, p] : cluster) nodes.push_back(WireNode{id, h, p});
-             return std::make_unique<WireServer>(std::move(b), host, port, node_id, std::move(nodes));
+             return std::make_unique<WireServer>(std::move(b), host, port, node_id, std::move(nodes), profile);
            }),
            py::arg("broker"), py::arg("host") = "127.0.0.1", py::arg("port") = 0, py::arg("node_id") = 0,
-           py::arg("cluster") = std::vector<std::tuple<int32_t, std::string, int32_t>>())
+           py::arg("cluster") = std::vector<std::tuple<int32_t, std::string, int32_t>>(),
+           py::arg("profile") = "legacy")
       .def("start", &WireServer::start)
       .def("stop", &WireServer::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("port", &WireServer::port)
@@ -554,7 +560,7 @@ PYBIND11_MODULE(_tkcore, m) {
                        uint64_t index_capacity, const std::string& client_id, bool release_consumed,
                        uint64_t release_bytes, uint64_t release_step, uint64_t ring_bytes, py::dict security,
                        bool subscribe, int32_t session_timeout_ms, int32_t heartbeat_interval_ms,
-                       std::vector<std::string> assignors) {
+                       std::vector<std::string> assignors, int32_t rebalance_timeout_ms) {
              ReplicaConfig c;
              for (auto& a : assignors)
                if (a != "range" && a != "roundrobin")
@@ -563,6 +569,7 @@ PYBIND11_MODULE(_tkcore, m) {
              c.subscribe = subscribe;
              c.session_timeout_ms = session_timeout_ms;
              c.heartbeat_interval_ms = heartbeat_interval_ms;
+             c.rebalance_timeout_ms = rebalance_timeout_ms;
              c.bootstrap = bootstrap;
              c.topic = topic;
              c.group = group;
@@ -594,7 +601,8 @@ PYBIND11_MODULE(_tkcore, m) {
            py::arg("release_consumed") = true, py::arg("release_bytes") = uint64_t(256) << 20,
            py::arg("release_step") = uint64_t(1) << 30, py::arg("ring_bytes") = uint64_t(0),
            py::arg("security") = py::dict(), py::arg("subscribe") = false, py::arg("session_timeout_ms") = 10000,
-           py::arg("heartbeat_interval_ms") = 3000, py::arg("assignors") = std::vector<std::string>{"range"})
+           py::arg("heartbeat_interval_ms") = 3000, py::arg("assignors") = std::vector<std::string>{"range"},
+           py::arg("rebalance_timeout_ms") = 0)
       .def("start", &Replicator::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Replicator::stop, py::arg("flush") = true, py::call_guard<py::gil_scoped_release>())
       .def("flush_commits", &Replicator::flush_commits, py::call_guard<py::gil_scoped_release>())
@@ -607,6 +615,10 @@ PYBIND11_MODULE(_tkcore, m) {
       .def_property_readonly("generation", &Replicator::generation)
       .def_property_readonly("assignment", &Replicator::assignment)
       .def_property_readonly("fenced", &Replicator::fenced)
+      .def_property_readonly("assignment_epoch", &Replicator::assignment_epoch)
+      .def_property_readonly("rebalances", &Replicator::rebalances)
+      .def("assignment_epochs", &Replicator::assignment_epochs,
+           "[(partition, epoch at which it was (re)assigned)] of the partitions owned now")
       .def_property_readonly("fetch_threads", &Replicator::fetch_threads)
       .def("last_error", &Replicator::last_error)
       .def("stats", [](Replicator& r) {
@@ -625,6 +637,7 @@ PYBIND11_MODULE(_tkcore, m) {
           d["fetches"] = s.fetches;
           d["throttled"] = s.throttled;
           d["released"] = s.released;
+          d["owned"] = s.owned;
           l.append(d);
         }
         return l;

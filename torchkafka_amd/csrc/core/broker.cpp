@@ -394,6 +394,16 @@ void Broker::reset_empty(uint32_t pidx, int64_t offset) {
   P.high_watermark.store(offset, std::memory_order_release);
 }
 
+void Broker::reset_partition(uint32_t pidx, int64_t offset) {
+  PartitionEntry& P = part(pidx);
+  RobustLock l(&P.lock);
+  P.n_batches.store(0, std::memory_order_release);
+  P.first_batch.store(0, std::memory_order_release);
+  P.log_end_pos.store(0, std::memory_order_release);
+  P.log_start_offset.store(offset, std::memory_order_release);
+  P.high_watermark.store(offset, std::memory_order_release);
+}
+
 Broker::Ingested Broker::ingest(uint32_t pidx, uint64_t len, int64_t from_offset, bool keep_control,
                                 uint64_t limit) {
   PartitionEntry& P = part(pidx);

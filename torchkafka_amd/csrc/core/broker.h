@@ -202,6 +202,11 @@ class Broker {
   uint8_t* log_tail(uint32_t pidx, uint64_t* avail);
   // An empty partition starts at `offset` (log start = high watermark = offset).
   void reset_empty(uint32_t pidx, int64_t offset);
+  // Drops everything a replica partition holds and restarts it, empty, at `offset` (the log is
+  // rewritten from byte 0; a ring stays a ring).  For a partition a group rebalance gives back to
+  // this replica: its cluster-committed offset may lie outside what the local log still holds.
+  // Nobody may be reading the partition (the replica's consumers dropped it when it was revoked).
+  void reset_partition(uint32_t pidx, int64_t offset);
   struct Ingested {
     uint64_t consumed = 0;     // bytes of whole batches walked (kept or dropped)
     uint64_t kept_bytes = 0;

@@ -36,7 +36,34 @@ const char* error_name(int16_t code) {
     case kIllegalGeneration: return "IllegalGenerationError";
     case kUnknownMemberId: return "UnknownMemberIdError";
     case kRebalanceInProgress: return "RebalanceInProgressError";
+    case kUnsupportedVersion: return "UnsupportedVersionError";
+    case kMemberIdRequired: return "MemberIdRequiredError";
+    case kUnsupportedSaslMechanism: return "UnsupportedSaslMechanismError";
+    case kSaslAuthenticationFailed: return "SaslAuthenticationFailedError";
     default: return "KafkaError";
+  }
+}
+
+const std::map<int16_t, ApiRange>& client_versions() {
+  static const std::map<int16_t, ApiRange> v = {
+      {kFetch, {4, 11}},         {kListOffsets, {1, 5}},     {kMetadata, {1, 8}},
+      {kOffsetCommit, {2, 7}},   {kOffsetFetch, {1, 5}},     {kFindCoordinator, {0, 2}},
+      {kJoinGroup, {0, 5}},      {kHeartbeat, {0, 3}},       {kLeaveGroup, {0, 2}},
+      {kSyncGroup, {0, 3}},      {kSaslHandshake, {1, 1}},   {kApiVersions, {0, 0}},
+      {kSaslAuthenticate, {0, 1}},
+  };
+  return v;
+}
+
+int16_t legacy_version(int16_t api_key) {
+  switch (api_key) {
+    case kFetch: return 4;
+    case kListOffsets: return 1;
+    case kMetadata: return 1;
+    case kOffsetCommit: return 2;
+    case kOffsetFetch: return 1;
+    case kSaslHandshake: return 1;
+    default: return 0;
   }
 }
 
@@ -120,6 +147,15 @@ std::string ssl_error(const std::string& what) {
 
 Conn::Conn(const std::string& host, int port, int timeout_ms, const Security* sec, SSL_CTX* ctx)
     : host_(host), port_(port), timeout_ms_(timeout_ms), buf_(size_t(1) << 16) {
+  open_socket(sec, ctx);
+  negotiate(sec, ctx);
+  if (sec && sec->sasl()) authenticate(*sec);
+}
+
+void Conn::open_socket(const Security* sec, SSL_CTX* ctx) {
+  const std::string& host = host_;
+  const int port = port_;
+  const int timeout_ms = timeout_ms_;
   addrinfo hints{};
   hints.ai_family = AF_UNSPEC;
   hints.ai_socktype = SOCK_STREAM;
@@ -167,7 +203,55 @@ Conn::Conn(const std::string& host, int port, int timeout_ms, const Security* se
     timeval none{0, 0};
     ::setsockopt(fd_, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));
   }
-  if (sec && sec->sasl()) authenticate(*sec);
+}
+
+// ApiVersions v0 (every broker since 0.10 answers it, before authentication too).  A broker
+// that predates it closes the connection: reconnect and use the fixed legacy versions.
+void Conn::negotiate(const Security* sec, SSL_CTX* ctx) {
+  std::vector<uint8_t> resp;
+  try {
+    resp = roundtrip(kApiVersions, 0, "torchkafka", std::string(), timeout_ms_);
+  } catch (const KafkaError&) {
+    close();
+    b0_ = b1_ = 0;
+    remaining_ = 0;
+    open_socket(sec, ctx);
+    broker_.clear();
+    return;
+  }
+  Reader r(resp.data(), resp.size());
+  const int16_t e = r.i16();
+  const int32_t n = r.i32();
+  std::map<int16_t, ApiRange> m;
+  for (int32_t i = 0; i < n; ++i) {
+    const int16_t key = r.i16();
+    const int16_t lo = r.i16();
+    const int16_t hi = r.i16();
+    m[key] = ApiRange{lo, hi};
+  }
+  if (e != kNone && m.empty()) {
+    close();
+    throw WireError(e, std::string(error_name(e)) + ": ApiVersions refused by " + host_);
+  }
+  broker_ = std::move(m);
+}
+
+int16_t Conn::version(int16_t api_key) const {
+  if (broker_.empty()) return legacy_version(api_key);
+  const auto& cv = client_versions();
+  auto c = cv.find(api_key);
+  auto b = broker_.find(api_key);
+  if (c == cv.end() || b == broker_.end())
+    throw WireError(kUnsupportedVersion, "UnsupportedVersionError: " + host_ + " does not serve API " +
+                                             std::to_string(api_key));
+  const int16_t hi = std::min(c->second.max, b->second.max);
+  const int16_t lo = std::max(c->second.min, b->second.min);
+  if (hi < lo)
+    throw WireError(kUnsupportedVersion,
+                    "UnsupportedVersionError: API " + std::to_string(api_key) + ": " + host_ + " serves v" +
+                        std::to_string(b->second.min) + "-" + std::to_string(b->second.max) + ", this client v" +
+                        std::to_string(c->second.min) + "-" + std::to_string(c->second.max));
+  return hi;
 }
 
 namespace {
@@ -225,12 +309,14 @@ std::string Conn::sasl_round(const std::string& token) {
   Writer au;
   au.i32(int32_t(token.size()));
   au.data().append(token);
-  auto r = roundtrip(kSaslAuthenticate, 0, "torchkafka", au.data(), timeout_ms_);
+  const int16_t v = version(kSaslAuthenticate);
+  auto r = roundtrip(kSaslAuthenticate, v, "torchkafka", au.data(), timeout_ms_);
   Reader b(r.data(), r.size());
   const int16_t e = b.i16();
   const std::string msg = b.str();
   int32_t len = 0;
   const uint8_t* p = b.bytes(&len);
+  if (v >= 1) b.i64();  // session lifetime (KIP-368): re-authentication is not needed here
   if (e != kNone) {
     close();
     throw KafkaError("SaslAuthenticationFailedError: " + (msg.empty() ? std::string(error_name(e)) : msg));
@@ -280,7 +366,7 @@ void Conn::authenticate(const Security& sec) {
                      " (this client speaks PLAIN, SCRAM-SHA-256 and SCRAM-SHA-512)");
   Writer hs;
   hs.str(sec.sasl_mechanism);
-  auto r1 = roundtrip(kSaslHandshake, 1, "torchkafka", hs.data(), timeout_ms_);
+  auto r1 = roundtrip(kSaslHandshake, version(kSaslHandshake), "torchkafka", hs.data(), timeout_ms_);
   Reader a(r1.data(), r1.size());
   const int16_t e1 = a.i16();
   if (e1 != kNone) {
@@ -579,29 +665,44 @@ std::vector<BrokerAddr> Client::brokers() {
 }
 
 TopicMeta Client::metadata(const std::string& topic) {
-  Writer w;
-  w.array(1);
-  w.str(topic);
   std::vector<uint8_t> resp;
+  int16_t v = 1;
+  auto ask = [&]() {
+    Conn& k = bootstrap_conn();
+    v = k.version(kMetadata);
+    Writer w;
+    w.array(1);
+    w.str(topic);
+    if (v >= 4) w.i8(0);  // allow_auto_topic_creation: false (a consumer never creates topics)
+    if (v >= 8) {
+      w.i8(0);  // include_cluster_authorized_operations
+      w.i8(0);  // include_topic_authorized_operations
+    }
+    resp = k.roundtrip(kMetadata, v, client_id_, w.data(), timeout_ms_);
+  };
   try {
-    resp = bootstrap_conn().roundtrip(kMetadata, 1, client_id_, w.data(), timeout_ms_);
+    ask();
+  } catch (const WireError&) {
+    throw;
   } catch (const KafkaError&) {
     drop(-1);
-    resp = bootstrap_conn().roundtrip(kMetadata, 1, client_id_, w.data(), timeout_ms_);
+    ask();
   }
   Reader r(resp.data(), resp.size());
+  if (v >= 3) r.i32();  // throttle_time_ms
   const int32_t nb = r.i32();
   for (int32_t i = 0; i < nb; ++i) {
     BrokerAddr b;
     b.node_id = r.i32();
     b.host = r.str();
     b.port = r.i32();
-    r.str();  // rack
+    if (v >= 1) r.str();  // rack
     auto old = nodes_.find(b.node_id);
     if (old != nodes_.end() && (old->second.host != b.host || old->second.port != b.port)) drop(b.node_id);
     nodes_[b.node_id] = b;
   }
-  r.i32();  // controller
+  if (v >= 2) r.str();  // cluster id
+  r.i32();              // controller
   const int32_t nt = r.i32();
   TopicMeta out;
   out.name = topic;
@@ -617,12 +718,18 @@ TopicMeta Client::metadata(const std::string& topic) {
       p.error = r.i16();
       p.partition = r.i32();
       p.leader = r.i32();
+      if (v >= 7) r.i32();  // leader epoch
       const int32_t nrep = r.i32();
       for (int32_t k = 0; k < nrep; ++k) r.i32();
       const int32_t nisr = r.i32();
       for (int32_t k = 0; k < nisr; ++k) r.i32();
+      if (v >= 5) {
+        const int32_t noff = r.i32();  // offline replicas
+        for (int32_t k = 0; k < noff; ++k) r.i32();
+      }
       t.partitions.push_back(p);
     }
+    if (v >= 8) r.i32();  // topic authorized operations
     std::sort(t.partitions.begin(), t.partitions.end(),
               [](const PartitionMeta& a, const PartitionMeta& b) { return a.partition < b.partition; });
     if (t.name == topic) out = t;
@@ -647,17 +754,22 @@ std::map<int32_t, int64_t> Client::list_offsets(const std::string& topic, const 
   std::map<int32_t, int64_t> out;
   for (auto& [node, ps] : by_leader) {
     if (node < 0) throw WireError(kLeaderNotAvailable, "LeaderNotAvailableError: " + topic);
+    Conn& k = conn(node);
+    const int16_t v = k.version(kListOffsets);
     Writer w;
-    w.i32(-1);  // replica id
+    w.i32(-1);           // replica id
+    if (v >= 2) w.i8(0);  // isolation level: read_uncommitted
     w.array(1);
     w.str(topic);
     w.array(int32_t(ps.size()));
     for (int32_t p : ps) {
       w.i32(p);
+      if (v >= 4) w.i32(-1);  // current leader epoch: unknown
       w.i64(timestamp);
     }
-    auto resp = conn(node).roundtrip(kListOffsets, 1, client_id_, w.data(), timeout_ms_);
+    auto resp = k.roundtrip(kListOffsets, v, client_id_, w.data(), timeout_ms_);
     Reader r(resp.data(), resp.size());
+    if (v >= 2) r.i32();  // throttle
     const int32_t nt = r.i32();
     for (int32_t i = 0; i < nt; ++i) {
       r.str();
@@ -667,6 +779,7 @@ std::map<int32_t, int64_t> Client::list_offsets(const std::string& topic, const 
         const int16_t e = r.i16();
         r.i64();  // timestamp
         const int64_t off = r.i64();
+        if (v >= 4) r.i32();  // leader epoch
         if (e != kNone)
           throw WireError(e, std::string(error_name(e)) + ": ListOffsets " + topic + "-" + std::to_string(p));
         out[p] = off;
@@ -678,16 +791,23 @@ std::map<int32_t, int64_t> Client::list_offsets(const std::string& topic, const 
 
 int32_t Client::coordinator(const std::string& group) {
   if (coordinator_ >= 0 && coordinator_group_ == group) return coordinator_;
+  Conn& k = bootstrap_conn();
+  const int16_t v = k.version(kFindCoordinator);
   Writer w;
   w.str(group);
-  auto resp = bootstrap_conn().roundtrip(kFindCoordinator, 0, client_id_, w.data(), timeout_ms_);
+  if (v >= 1) w.i8(0);  // key type: group
+  auto resp = k.roundtrip(kFindCoordinator, v, client_id_, w.data(), timeout_ms_);
   Reader r(resp.data(), resp.size());
+  if (v >= 1) r.i32();  // throttle
   const int16_t e = r.i16();
+  std::string msg;
+  if (v >= 1) msg = r.str();
   BrokerAddr b;
   b.node_id = r.i32();
   b.host = r.str();
   b.port = r.i32();
-  if (e != kNone) throw WireError(e, std::string(error_name(e)) + ": FindCoordinator " + group);
+  if (e != kNone)
+    throw WireError(e, std::string(error_name(e)) + ": FindCoordinator " + group + (msg.empty() ? "" : " (" + msg + ")"));
   auto old = nodes_.find(b.node_id);
   if (old != nodes_.end() && (old->second.host != b.host || old->second.port != b.port)) drop(b.node_id);
   nodes_[b.node_id] = b;
@@ -704,34 +824,54 @@ std::map<int32_t, int64_t> Client::offset_fetch(const std::string& group, const 
   w.str(topic);
   w.array(int32_t(parts.size()));
   for (int32_t p : parts) w.i32(p);
-  const int32_t node = coordinator(group);
-  auto resp = conn(node).roundtrip(kOffsetFetch, 1, client_id_, w.data(), timeout_ms_);
+  int16_t v = 1;
+  auto resp = coordinator_roundtrip(group, kOffsetFetch, -1, w.data(), timeout_ms_, &v);
   Reader r(resp.data(), resp.size());
+  if (v >= 3) r.i32();  // throttle
   std::map<int32_t, int64_t> out;
   const int32_t nt = r.i32();
+  int16_t first_err = kNone;
+  int32_t err_part = -1;
   for (int32_t i = 0; i < nt; ++i) {
     r.str();
     const int32_t np = r.i32();
     for (int32_t j = 0; j < np; ++j) {
       const int32_t p = r.i32();
       const int64_t off = r.i64();
-      r.str();  // metadata
+      if (v >= 5) r.i32();  // committed leader epoch
+      r.str();              // metadata
       const int16_t e = r.i16();
-      if (e != kNone) {
-        if (needs_metadata(e)) invalidate_coordinator();
-        throw WireError(e, std::string(error_name(e)) + ": OffsetFetch " + topic + "-" + std::to_string(p));
+      if (e != kNone && first_err == kNone) {
+        first_err = e;
+        err_part = p;
       }
       out[p] = off;
     }
+  }
+  const int16_t top = v >= 2 ? r.i16() : int16_t(kNone);
+  const int16_t e = top != kNone ? top : first_err;
+  if (e != kNone) {
+    if (needs_metadata(e)) invalidate_coordinator();
+    throw WireError(e, std::string(error_name(e)) + ": OffsetFetch " + topic +
+                           (top == kNone ? "-" + std::to_string(err_part) : std::string()));
   }
   return out;
 }
 
 std::vector<uint8_t> Client::coordinator_roundtrip(const std::string& group, int16_t key, int16_t version,
-                                                  const std::string& body, int timeout_ms) {
+                                                  const std::string& body, int timeout_ms, int16_t* used) {
   const int32_t node = coordinator(group);
   try {
-    return conn(node).roundtrip(key, version, client_id_, body, timeout_ms);
+    Conn& k = conn(node);
+    const int16_t v = version >= 0 ? version : k.version(key);
+    if (used) *used = v;
+    return k.roundtrip(key, v, client_id_, body, timeout_ms);
+  } catch (const WireError& e) {
+    if (e.code != kUnsupportedVersion) {
+      drop(node);
+      invalidate_coordinator();
+    }
+    throw;
   } catch (const KafkaError&) {
     drop(node);
     invalidate_coordinator();
@@ -739,12 +879,21 @@ std::vector<uint8_t> Client::coordinator_roundtrip(const std::string& group, int
   }
 }
 
+int16_t Client::coordinator_version(const std::string& group, int16_t key) {
+  return conn(coordinator(group)).version(key);
+}
+
 JoinResult Client::join_group(const std::string& group, int32_t session_timeout_ms, const std::string& member_id,
-                              const std::string& subscription, const std::vector<std::string>& protocols) {
+                              const std::string& subscription, const std::vector<std::string>& protocols,
+                              int32_t rebalance_timeout_ms) {
+  const int16_t v = coordinator_version(group, kJoinGroup);
+  const int32_t rebalance = rebalance_timeout_ms > 0 ? rebalance_timeout_ms : session_timeout_ms;
   Writer w;
   w.str(group);
   w.i32(session_timeout_ms);
+  if (v >= 1) w.i32(rebalance);
   w.str(member_id);
+  if (v >= 5) w.nullable_str_null();  // group instance id: dynamic membership
   w.str("consumer");
   w.array(int32_t(protocols.size()));
   for (auto& name : protocols) {
@@ -753,9 +902,11 @@ JoinResult Client::join_group(const std::string& group, int32_t session_timeout_
     w.data() += subscription;
   }
   // the coordinator holds the request until the join round ends
-  auto resp = coordinator_roundtrip(group, kJoinGroup, 0, w.data(), timeout_ms_ + session_timeout_ms);
+  auto resp = coordinator_roundtrip(group, kJoinGroup, v, w.data(),
+                                    timeout_ms_ + std::max(session_timeout_ms, v >= 1 ? rebalance : 0));
   Reader r(resp.data(), resp.size());
   JoinResult j;
+  if (v >= 2) r.i32();  // throttle
   j.error = r.i16();
   j.generation = r.i32();
   j.protocol = r.str();
@@ -764,6 +915,7 @@ JoinResult Client::join_group(const std::string& group, int32_t session_timeout_
   const int32_t n = r.i32();
   for (int32_t i = 0; i < n; ++i) {
     std::string m = r.str();
+    if (v >= 5) r.str();  // group instance id
     int32_t len = 0;
     const uint8_t* p = r.bytes(&len);
     j.members.emplace_back(std::move(m), len > 0 ? std::string(reinterpret_cast<const char*>(p), size_t(len)) : "");
@@ -775,18 +927,21 @@ JoinResult Client::join_group(const std::string& group, int32_t session_timeout_
 std::pair<int16_t, std::string> Client::sync_group(const std::string& group, int32_t generation,
                                                    const std::string& member_id,
                                                    const std::map<std::string, std::string>& assignments) {
+  const int16_t v = coordinator_version(group, kSyncGroup);
   Writer w;
   w.str(group);
   w.i32(generation);
   w.str(member_id);
+  if (v >= 3) w.nullable_str_null();  // group instance id
   w.array(int32_t(assignments.size()));
   for (auto& [m, a] : assignments) {
     w.str(m);
     w.i32(int32_t(a.size()));
     w.data() += a;
   }
-  auto resp = coordinator_roundtrip(group, kSyncGroup, 0, w.data(), timeout_ms_ * 2);
+  auto resp = coordinator_roundtrip(group, kSyncGroup, v, w.data(), timeout_ms_ * 2);
   Reader r(resp.data(), resp.size());
+  if (v >= 1) r.i32();  // throttle
   const int16_t e = r.i16();
   int32_t len = 0;
   const uint8_t* p = r.bytes(&len);
@@ -795,23 +950,28 @@ std::pair<int16_t, std::string> Client::sync_group(const std::string& group, int
 }
 
 int16_t Client::heartbeat(const std::string& group, int32_t generation, const std::string& member_id) {
+  const int16_t v = coordinator_version(group, kHeartbeat);
   Writer w;
   w.str(group);
   w.i32(generation);
   w.str(member_id);
-  auto resp = coordinator_roundtrip(group, kHeartbeat, 0, w.data(), timeout_ms_);
+  if (v >= 3) w.nullable_str_null();  // group instance id
+  auto resp = coordinator_roundtrip(group, kHeartbeat, v, w.data(), timeout_ms_);
   Reader r(resp.data(), resp.size());
+  if (v >= 1) r.i32();  // throttle
   const int16_t e = r.i16();
   if (needs_metadata(e)) invalidate_coordinator();
   return e;
 }
 
 int16_t Client::leave_group(const std::string& group, const std::string& member_id) {
+  const int16_t v = coordinator_version(group, kLeaveGroup);
   Writer w;
   w.str(group);
   w.str(member_id);
-  auto resp = coordinator_roundtrip(group, kLeaveGroup, 0, w.data(), timeout_ms_);
+  auto resp = coordinator_roundtrip(group, kLeaveGroup, v, w.data(), timeout_ms_);
   Reader r(resp.data(), resp.size());
+  if (v >= 1) r.i32();  // throttle
   return r.i16();
 }
 
@@ -912,29 +1072,25 @@ std::map<int32_t, int16_t> Client::offset_commit(const std::string& group, const
                                                  const std::map<int32_t, int64_t>& offsets,
                                                  const std::string& metadata, int32_t generation,
                                                  const std::string& member_id) {
+  const int16_t v = coordinator_version(group, kOffsetCommit);
   Writer w;
   w.str(group);
   w.i32(generation);  // -1 with an empty member id: a manually assigned ("simple") consumer
   w.str(member_id);
-  w.i64(-1);      // retention: the broker's default
+  if (v >= 7) w.nullable_str_null();  // group instance id
+  if (v <= 4) w.i64(-1);              // retention: the broker's default (dropped in v5)
   w.array(1);
   w.str(topic);
   w.array(int32_t(offsets.size()));
   for (auto& [p, o] : offsets) {
     w.i32(p);
     w.i64(o);
+    if (v >= 6) w.i32(-1);  // committed leader epoch: unknown
     w.str(metadata);
   }
-  const int32_t node = coordinator(group);
-  std::vector<uint8_t> resp;
-  try {
-    resp = conn(node).roundtrip(kOffsetCommit, 2, client_id_, w.data(), timeout_ms_);
-  } catch (const KafkaError&) {
-    drop(node);
-    invalidate_coordinator();
-    throw;
-  }
+  auto resp = coordinator_roundtrip(group, kOffsetCommit, v, w.data(), timeout_ms_);
   Reader r(resp.data(), resp.size());
+  if (v >= 3) r.i32();  // throttle
   std::map<int32_t, int16_t> out;
   const int32_t nt = r.i32();
   for (int32_t i = 0; i < nt; ++i) {
@@ -950,23 +1106,54 @@ std::map<int32_t, int16_t> Client::offset_commit(const std::string& group, const
   return out;
 }
 
-std::string fetch_request(const std::string& topic, const std::vector<FetchPartReq>& parts, int32_t max_wait_ms,
-                          int32_t min_bytes, int32_t max_bytes) {
+std::string fetch_request(int16_t v, const std::string& topic, const std::vector<FetchPartReq>& parts,
+                          int32_t max_wait_ms, int32_t min_bytes, int32_t max_bytes) {
   Writer w;
   w.i32(-1);  // replica id: a consumer
   w.i32(max_wait_ms);
   w.i32(min_bytes);
   w.i32(max_bytes);
   w.i8(0);    // isolation level: read_uncommitted (kafka-python's default)
+  if (v >= 7) {
+    w.i32(0);   // session id 0 + epoch -1: a sessionless (full) fetch (KIP-227)
+    w.i32(-1);
+  }
   w.array(1);
   w.str(topic);
   w.array(int32_t(parts.size()));
   for (auto& p : parts) {
     w.i32(p.partition);
+    if (v >= 9) w.i32(-1);  // current leader epoch: unknown
     w.i64(p.offset);
+    if (v >= 5) w.i64(-1);  // log start offset: a consumer sends -1
     w.i32(p.max_bytes);
   }
+  if (v >= 7) w.array(0);  // forgotten topics
+  if (v >= 11) w.str("");  // rack id
   return std::move(w.data());
+}
+
+void fetch_response_header(Conn& k, int16_t v) {
+  k.r32();  // throttle_time_ms
+  if (v >= 7) {
+    const int16_t e = k.r16();
+    k.r32();  // session id
+    if (e != kNone) throw WireError(e, std::string(error_name(e)) + ": Fetch");
+  }
+}
+
+FetchPartHeader fetch_partition_header(Conn& k, int16_t v) {
+  FetchPartHeader h;
+  h.partition = k.r32();
+  h.error = k.r16();
+  h.high_watermark = k.r64();
+  k.r64();              // last stable offset
+  if (v >= 5) k.r64();  // log start offset
+  const int32_t n_aborted = k.r32();
+  if (n_aborted > 0) k.skip(size_t(n_aborted) * 16);
+  if (v >= 11) k.r32();  // preferred read replica
+  h.records_len = k.r32();
+  return h;
 }
 
 }  // namespace tk::wire

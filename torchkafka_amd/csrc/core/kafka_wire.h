@@ -9,11 +9,18 @@
 // decode kernels verify CRCs and decode values from those bytes exactly as they do for the
 // synthetic broker -- no Python, no per-record objects, no second host copy.
 //
-// Protocol subset (non-flexible request versions, understood by Kafka 0.11 .. 3.x brokers):
-//   ApiVersions v0, Metadata v1, ListOffsets v1, Fetch v4 (RecordBatch v2, read_uncommitted),
-//   FindCoordinator v0, OffsetCommit v2, OffsetFetch v1; group membership (subscribe mode):
-//   JoinGroup v0, SyncGroup v0, Heartbeat v0, LeaveGroup v0 with the "consumer" protocol and
-//   Kafka's range assignor.
+// Protocol subset: the non-flexible request versions, negotiated per connection.  Every new
+// connection first sends ApiVersions v0 and each request then goes out at the highest version
+// both sides implement (client ranges in client_versions(); the broker's from its answer), as
+// kafka-python and the Java client do.  A broker that predates ApiVersions (it closes the
+// connection) gets the fixed pre-negotiation set: Metadata v1, ListOffsets v1, Fetch v4,
+// FindCoordinator v0, OffsetCommit v2, OffsetFetch v1, JoinGroup / SyncGroup / Heartbeat /
+// LeaveGroup v0.  Client ranges: Metadata 1-8, ListOffsets 1-5, Fetch 4-11 (sessionless),
+// FindCoordinator 0-2, OffsetCommit 2-7, OffsetFetch 1-5, JoinGroup 0-5 (v4+: the
+// MEMBER_ID_REQUIRED round trip), SyncGroup 0-3, Heartbeat 0-3, LeaveGroup 0-2 -- which covers
+// brokers from 0.11 through Kafka 4.x, whose KIP-896 dropped the pre-2.1 versions (e.g. JoinGroup
+// v0-1, Fetch v0-3).  Group membership uses the "consumer" protocol with Kafka's range and
+// round-robin assignors.
 // By default partitions are assigned statically by (rank, worker) as in the rest of the
 // framework, and offsets are committed like kafka-python's manually-assigned consumer with a
 // group_id (generation -1, empty member id).
@@ -61,8 +68,18 @@ enum ErrorCode : int16_t {
   kLeaderNotAvailable = 5, kNotLeaderForPartition = 6, kRequestTimedOut = 7,
   kCoordinatorLoadInProgress = 14, kCoordinatorNotAvailable = 15, kNotCoordinator = 16,
   kIllegalGeneration = 22, kUnknownMemberId = 25, kRebalanceInProgress = 27,
-  kUnsupportedSaslMechanism = 33, kIllegalSaslState = 34, kSaslAuthenticationFailed = 58,
+  kUnsupportedSaslMechanism = 33, kIllegalSaslState = 34, kUnsupportedVersion = 35,
+  kSaslAuthenticationFailed = 58, kMemberIdRequired = 79,
 };
+
+// Version range of one API.
+struct ApiRange {
+  int16_t min, max;
+};
+// What this client implements, per API key.
+const std::map<int16_t, ApiRange>& client_versions();
+// What it sends to a broker that does not answer ApiVersions.
+int16_t legacy_version(int16_t api_key);
 const char* error_name(int16_t code);
 // Errors after which the partition's leader (or the group's coordinator) must be looked up again.
 inline bool needs_metadata(int16_t e) {
@@ -121,6 +138,12 @@ class Conn {
   int port() const { return port_; }
   bool ok() const { return fd_ >= 0; }
 
+  // The version to send `api_key` at on this connection: the highest one both this client and the
+  // broker implement (WireError UNSUPPORTED_VERSION when the ranges do not meet).
+  int16_t version(int16_t api_key) const;
+  // The broker's ApiVersions answer (empty: it predates ApiVersions, legacy_version() is used).
+  const std::map<int16_t, ApiRange>& broker_versions() const { return broker_; }
+
   // Request/response with the whole response body in memory (small responses).
   std::vector<uint8_t> roundtrip(int16_t api_key, int16_t api_version, const std::string& client_id,
                                  const std::string& body, int timeout_ms);
@@ -148,6 +171,9 @@ class Conn {
   void fill(size_t want);  // at least min(want, remaining) bytes buffered
   ssize_t io_recv(void* dst, size_t n);
   bool wait_readable(int ms);
+  void open_socket(const Security* sec, SSL_CTX* ctx);  // TCP connect (+ TLS handshake)
+  void negotiate(const Security* sec, SSL_CTX* ctx);    // ApiVersions
+  std::map<int16_t, ApiRange> broker_;
   void authenticate(const Security& sec);
   void scram(const Security& sec);
   std::string sasl_round(const std::string& token);
@@ -183,7 +209,7 @@ struct TopicMeta {
   std::vector<PartitionMeta> partitions;  // sorted by partition id
 };
 
-// JoinGroup v0 response; `members` (member id, subscription metadata) is filled for the leader only.
+// JoinGroup response; `members` (member id, subscription metadata) is filled for the leader only.
 struct JoinResult {
   int16_t error = 0;
   int32_t generation = -1;
@@ -235,9 +261,12 @@ class Client {
   // Group membership against the group's coordinator.  join_group blocks at the coordinator
   // until the join round ends (up to the session timeout).
   // protocols: assignor names in preference order ("range", "roundrobin")
+  // rebalance_timeout_ms (JoinGroup v1+): how long the coordinator waits for every member to
+  // rejoin during a rebalance (kafka-python: max_poll_interval_ms); <= 0: the session timeout.
   JoinResult join_group(const std::string& group, int32_t session_timeout_ms, const std::string& member_id,
                         const std::string& subscription,
-                        const std::vector<std::string>& protocols = std::vector<std::string>{"range"});
+                        const std::vector<std::string>& protocols = std::vector<std::string>{"range"},
+                        int32_t rebalance_timeout_ms = -1);
   std::pair<int16_t, std::string> sync_group(const std::string& group, int32_t generation,
                                              const std::string& member_id,
                                              const std::map<std::string, std::string>& assignments);
@@ -256,8 +285,10 @@ class Client {
  private:
   Conn& bootstrap_conn();
   int32_t coordinator(const std::string& group);
+  // version < 0: negotiated on the coordinator's connection (reported through *used)
   std::vector<uint8_t> coordinator_roundtrip(const std::string& group, int16_t key, int16_t version,
-                                             const std::string& body, int timeout_ms);
+                                             const std::string& body, int timeout_ms, int16_t* used = nullptr);
+  int16_t coordinator_version(const std::string& group, int16_t key);
   std::vector<std::pair<std::string, int>> bootstrap_;
   std::string client_id_;
   int timeout_ms_;
@@ -271,8 +302,17 @@ class Client {
   SSL_CTX* ctx_ = nullptr;
 };
 
-// Encodes a Fetch v4 request body (tests and the replicator share it).
-std::string fetch_request(const std::string& topic, const std::vector<FetchPartReq>& parts, int32_t max_wait_ms,
-                          int32_t min_bytes, int32_t max_bytes);
+// Encodes a sessionless Fetch request body of `version` (4..11).
+std::string fetch_request(int16_t version, const std::string& topic, const std::vector<FetchPartReq>& parts,
+                          int32_t max_wait_ms, int32_t min_bytes, int32_t max_bytes);
+// Streaming Fetch response parts that vary with the version (the replicator reads the rest).
+void fetch_response_header(Conn& k, int16_t version);  // throttle / error / session, up to the topic array
+struct FetchPartHeader {
+  int32_t partition;
+  int16_t error;
+  int64_t high_watermark;
+  int32_t records_len;  // -1: null
+};
+FetchPartHeader fetch_partition_header(Conn& k, int16_t version);  // up to (and including) the records length
 
 }  // namespace tk::wire

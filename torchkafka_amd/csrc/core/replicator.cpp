@@ -60,59 +60,41 @@ void Replicator::start() {
     throw std::invalid_argument("replicator: ring_bytes must hold at least 4 x partition_max_bytes");
   if (cfg_.ring_bytes) cfg_.release_consumed = false;  // a ring reuses its pages: nothing to free
   if (cfg_.release_consumed && !cfg_.group.empty()) local_->set_flags(kReleaseConsumed);
+  std::vector<int32_t> mine;
   if (cfg_.subscribe) {
     if (cfg_.group.empty()) throw std::invalid_argument("replicator: subscribe mode needs a group");
-    assigned_ = join_group(c);
+    mine = join_group(c);
   }
-  std::vector<int32_t> ids = cfg_.subscribe ? assigned_ : cfg_.partitions;
-  if (ids.empty() && !cfg_.subscribe)
+  // subscribe mode keeps a Part for every partition of the topic (the assignment moves between
+  // them); static mode only for the partitions it mirrors
+  std::vector<int32_t> ids = cfg_.subscribe ? std::vector<int32_t>() : cfg_.partitions;
+  if (ids.empty())
     for (auto& p : t.partitions) ids.push_back(p.partition);
   std::sort(ids.begin(), ids.end());
   ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
   for (int32_t id : ids)
     if (id < 0 || id >= n_remote_parts_)
       throw KafkaError("UnknownTopicOrPartitionError: " + cfg_.topic + "-" + std::to_string(id));
-
-  std::map<int32_t, int64_t> committed;
-  if (!cfg_.group.empty()) {
-    group_ = local_->group_index(cfg_.group, true);
-    committed = c.offset_fetch(cfg_.group, cfg_.topic, ids);
-  }
-  std::vector<int32_t> need_reset;
-  for (int32_t id : ids) {
-    auto it = committed.find(id);
-    if (it == committed.end() || it->second < 0) need_reset.push_back(id);
-  }
-  const bool latest = cfg_.auto_offset_reset == "latest" || cfg_.auto_offset_reset == "largest";
-  std::map<int32_t, int64_t> reset;
-  if (!need_reset.empty()) reset = c.list_offsets(cfg_.topic, need_reset, latest ? -1 : -2);
+  if (!cfg_.group.empty()) group_ = local_->group_index(cfg_.group, true);
 
   parts_.clear();
+  std::vector<Part*> owned;
+  const std::set<int32_t> assigned(mine.begin(), mine.end());
   for (int32_t id : ids) {
     auto p = std::make_unique<Part>();
     p->partition = id;
     p->pidx = first_pidx_ + uint32_t(id);
-    auto ci = committed.find(id);
-    const int64_t remote_committed = ci != committed.end() ? ci->second : -1;
-    const int64_t start = remote_committed >= 0 ? remote_committed : reset.at(id);
-    PartitionEntry& P = local_->part(p->pidx);
-    if (P.n_batches.load() == 0) {
-      local_->reset_empty(p->pidx, start);
-      if (cfg_.ring_bytes) local_->make_ring(p->pidx, std::min<uint64_t>(cfg_.ring_bytes, P.log_capacity));
-      p->fetch_offset = start;
-    } else {
-      p->fetch_offset = P.high_watermark.load();  // a persistent (file://) replica resumes its log
-    }
-    p->start_offset = start;
-    p->forwarded = remote_committed;
-    if (remote_committed >= 0 && !cfg_.group.empty() && local_->committed(group_, p->pidx) < remote_committed) {
-      try {
-        local_->commit(group_, -1, 0, 0, {CommitEntry{p->pidx, remote_committed, std::string()}});
-      } catch (const KafkaError& e) {
-        set_error(std::string("replicator: seeding the local committed offset failed: ") + e.what());
-      }
-    }
+    p->owned = !cfg_.subscribe || assigned.count(id) > 0;
+    p->fetch_offset = -1;
+    if (p->owned) owned.push_back(p.get());
     parts_.push_back(std::move(p));
+  }
+  start_parts(c, owned, true);
+  {
+    std::lock_guard<std::mutex> g(assign_mu_);
+    for (Part* p : owned) p->since = 1;
+    assigned_ = mine;
+    epoch_.store(1, std::memory_order_release);
   }
 
   // fetch threads: partitions grouped by leader, leaders spread over the threads
@@ -141,12 +123,72 @@ void Replicator::start() {
   }
 }
 
+// Positions of partitions this replica starts owning: the group's committed offset, else
+// auto_offset_reset.  `fresh` (start()): a persistent replica's log that can serve that offset is
+// resumed; otherwise -- and always for a partition a rebalance handed over -- the local partition
+// restarts, empty, at that offset (the log may hold a stale or overwritten range of it).
+void Replicator::start_parts(wire::Client& c, const std::vector<Part*>& ps, bool fresh) {
+  if (ps.empty()) return;
+  std::vector<int32_t> ids;
+  for (Part* p : ps) ids.push_back(p->partition);
+  std::map<int32_t, int64_t> committed;
+  if (!cfg_.group.empty()) committed = c.offset_fetch(cfg_.group, cfg_.topic, ids);
+  std::vector<int32_t> need_reset;
+  for (int32_t id : ids) {
+    auto it = committed.find(id);
+    if (it == committed.end() || it->second < 0) need_reset.push_back(id);
+  }
+  const bool latest = cfg_.auto_offset_reset == "latest" || cfg_.auto_offset_reset == "largest";
+  std::map<int32_t, int64_t> reset;
+  if (!need_reset.empty()) reset = c.list_offsets(cfg_.topic, need_reset, latest ? -1 : -2);
+  for (Part* p : ps) {
+    auto ci = committed.find(p->partition);
+    const int64_t remote_committed = ci != committed.end() ? ci->second : -1;
+    const int64_t start = remote_committed >= 0 ? remote_committed : reset.at(p->partition);
+    std::lock_guard<std::mutex> pg(p->mu);
+    PartitionEntry& P = local_->part(p->pidx);
+    const bool resume = fresh && P.n_batches.load() != 0 && P.ring_bytes.load() == 0 &&
+                        start >= P.log_start_offset.load() && start <= P.high_watermark.load();
+    if (resume) {
+      p->fetch_offset = P.high_watermark.load();  // a persistent (file://) replica resumes its log
+    } else {
+      if (P.n_batches.load() != 0 || P.high_watermark.load() != start) local_->reset_partition(p->pidx, start);
+      if (cfg_.ring_bytes && P.ring_bytes.load() == 0)
+        local_->make_ring(p->pidx, std::min<uint64_t>(cfg_.ring_bytes, P.log_capacity));
+      p->fetch_offset = start;
+      p->released = 0;
+    }
+    p->start_offset = start;
+    p->forwarded = remote_committed;
+    if (!cfg_.group.empty() && (!fresh || (remote_committed >= 0 && local_->committed(group_, p->pidx) < remote_committed))) {
+      // the local table is where the replica's consumers resume: the group's offset (a partition
+      // handed over by a rebalance starts where its last owner committed, not where we left it)
+      try {
+        local_->commit(group_, -1, 0, 0, {CommitEntry{p->pidx, start, std::string()}});
+      } catch (const KafkaError& e) {
+        set_error(std::string("replicator: seeding the local committed offset failed: ") + e.what());
+      }
+    }
+  }
+}
+
 std::vector<int32_t> Replicator::join_group(wire::Client& c) {
   const std::string sub = wire::encode_subscription({cfg_.topic});
+  std::string mid;
+  {
+    std::lock_guard<std::mutex> g(assign_mu_);
+    mid = member_id_;
+  }
   for (int attempt = 0; attempt < 8; ++attempt) {
-    wire::JoinResult j = c.join_group(cfg_.group, cfg_.session_timeout_ms, member_id_, sub, cfg_.assignors);
+    wire::JoinResult j = c.join_group(cfg_.group, cfg_.session_timeout_ms, mid, sub, cfg_.assignors,
+                                      cfg_.rebalance_timeout_ms);
+    if (j.error == wire::kMemberIdRequired) {  // JoinGroup v4+: join again with the id the coordinator chose
+      mid = j.member_id;
+      --attempt;
+      continue;
+    }
     if (j.error == wire::kUnknownMemberId) {
-      member_id_.clear();
+      mid.clear();
       continue;
     }
     if (j.error == wire::kRebalanceInProgress || wire::needs_metadata(j.error)) {
@@ -155,7 +197,7 @@ std::vector<int32_t> Replicator::join_group(wire::Client& c) {
     }
     if (j.error != wire::kNone)
       throw wire::WireError(j.error, std::string(wire::error_name(j.error)) + ": JoinGroup '" + cfg_.group + "'");
-    member_id_ = j.member_id;
+    mid = j.member_id;
     std::map<std::string, std::string> plan;
     if (j.leader == j.member_id) {  // the leader assigns every member's subscription
       std::map<std::string, int32_t> counts;
@@ -169,14 +211,22 @@ std::vector<int32_t> Replicator::join_group(wire::Client& c) {
                                                 : wire::range_assign(j.members, counts);
       for (auto& [m, a] : plan_of) plan[m] = wire::encode_assignment(a);
     }
-    auto [e, bytes] = c.sync_group(cfg_.group, j.generation, member_id_, plan);
+    auto [e, bytes] = c.sync_group(cfg_.group, j.generation, mid, plan);
     if (e == wire::kRebalanceInProgress || e == wire::kIllegalGeneration || wire::needs_metadata(e)) {
       sleep_ms(20 << std::min(attempt, 5));
       continue;
     }
+    if (e == wire::kUnknownMemberId) {
+      mid.clear();
+      continue;
+    }
     if (e != wire::kNone)
       throw wire::WireError(e, std::string(wire::error_name(e)) + ": SyncGroup '" + cfg_.group + "'");
-    generation_ = j.generation;
+    {
+      std::lock_guard<std::mutex> g(assign_mu_);
+      member_id_ = mid;
+      generation_ = j.generation;
+    }
     last_heartbeat_ms_ = now_ms();
     std::vector<int32_t> mine = wire::decode_assignment(bytes)[cfg_.topic];
     std::sort(mine.begin(), mine.end());
@@ -185,30 +235,80 @@ std::vector<int32_t> Replicator::join_group(wire::Client& c) {
   throw KafkaError("replicator: group '" + cfg_.group + "' did not settle (JoinGroup/SyncGroup kept rebalancing)");
 }
 
+// A new assignment, in process: revoked partitions stop (fetching, forwarding) at once, newly
+// assigned ones start at the group's committed offset; consumers of the local replica learn both
+// from assignment_epoch().  Runs on the commit thread under commit_mu_.
+void Replicator::apply_assignment(wire::Client& c, const std::vector<int32_t>& mine) {
+  const std::set<int32_t> now(mine.begin(), mine.end());
+  std::vector<Part*> added;
+  bool revoked = false;
+  {
+    std::lock_guard<std::mutex> g(assign_mu_);
+    for (auto& p : parts_) {
+      const bool want = now.count(p->partition) > 0;
+      if (p->owned.load() && !want) {
+        p->owned = false;
+        revoked = true;
+      } else if (!p->owned.load() && want) {
+        added.push_back(p.get());
+      }
+    }
+    if (revoked) epoch_.fetch_add(1, std::memory_order_acq_rel);
+  }
+  start_parts(c, added, false);  // network: outside the lock
+  std::lock_guard<std::mutex> g(assign_mu_);
+  const uint64_t e = epoch_.load() + (added.empty() ? 0 : 1);
+  for (Part* p : added) {
+    p->since = e;
+    p->owned = true;
+  }
+  assigned_ = mine;
+  epoch_.store(e, std::memory_order_release);
+}
+
 void Replicator::heartbeat(wire::Client& c) {
-  if (!cfg_.subscribe || fenced_.load() || now_ms() - last_heartbeat_ms_ < cfg_.heartbeat_interval_ms) return;
+  if (!cfg_.subscribe || now_ms() - last_heartbeat_ms_ < cfg_.heartbeat_interval_ms) return;
   last_heartbeat_ms_ = now_ms();
-  const int16_t e = c.heartbeat(cfg_.group, generation_, member_id_);
+  const int16_t e = c.heartbeat(cfg_.group, generation(), member_id());
   if (e == wire::kRebalanceInProgress || e == wire::kIllegalGeneration || e == wire::kUnknownMemberId) {
     try {
       forward(c);  // the current generation may still commit what was consumed
     } catch (const KafkaError&) {
     }
-    {
-      std::lock_guard<std::mutex> g(commit_mu_);  // forward() reads generation_ / member_id_
-      try {
-        if (e == wire::kUnknownMemberId) member_id_.clear();
-        if (join_group(c) == assigned_) return;  // same partitions: carry on in the new generation
-      } catch (const KafkaError&) {
-        if (stop_.load()) return;
-      }
-      fenced_ = true;
+    std::lock_guard<std::mutex> g(commit_mu_);  // forward() reads generation_ / member_id_
+    if (e == wire::kUnknownMemberId) {
+      std::lock_guard<std::mutex> a(assign_mu_);
+      member_id_.clear();
     }
-    set_error(std::string(wire::error_name(e)) + ": group '" + cfg_.group + "' rebalanced (generation " +
-              std::to_string(generation_) + "); this replica stopped fetching and committing -- restart to re-shard");
+    const std::vector<int32_t> mine = join_group(c);
+    rebalances_.fetch_add(1);
+    apply_assignment(c, mine);
   } else if (e != wire::kNone) {
     throw wire::WireError(e, std::string(wire::error_name(e)) + ": Heartbeat");
   }
+}
+
+std::string Replicator::member_id() const {
+  std::lock_guard<std::mutex> g(assign_mu_);
+  return member_id_;
+}
+
+int32_t Replicator::generation() const {
+  std::lock_guard<std::mutex> g(assign_mu_);
+  return generation_;
+}
+
+std::vector<int32_t> Replicator::assignment() const {
+  std::lock_guard<std::mutex> g(assign_mu_);
+  return assigned_;
+}
+
+std::vector<std::pair<int32_t, uint64_t>> Replicator::assignment_epochs() const {
+  std::lock_guard<std::mutex> g(assign_mu_);
+  std::vector<std::pair<int32_t, uint64_t>> v;
+  for (auto& p : parts_)
+    if (p->owned.load()) v.emplace_back(p->partition, p->since.load());
+  return v;
 }
 
 void Replicator::stop(bool flush) {
@@ -226,7 +326,8 @@ void Replicator::stop(bool flush) {
         if (!commit_client_)
           commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", flush_timeout, cfg_.security);
         forward(*commit_client_);
-        if (cfg_.subscribe && !fenced_.load() && !member_id_.empty()) commit_client_->leave_group(cfg_.group, member_id_);
+        const std::string mid = member_id();
+        if (cfg_.subscribe && !mid.empty()) commit_client_->leave_group(cfg_.group, mid);
         break;
       } catch (const KafkaError& e) {
         set_error(std::string("replicator: final commit: ") + e.what());
@@ -274,9 +375,9 @@ void Replicator::reset_offset(wire::Client& c, Part& p) {
 
 void Replicator::fetch_loop(std::vector<Part*> mine) {
   std::unique_ptr<wire::Client> c;
-  std::set<Part*> failed;
+  std::map<Part*, uint64_t> failed;  // -> assignment epoch at the failure
   int backoff_ms = 0;
-  while (!stop_.load() && !fenced_.load()) {
+  while (!stop_.load()) {
     try {
       if (!c) {
         c = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id, cfg_.timeout_ms, cfg_.security);
@@ -286,7 +387,12 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
       std::map<int32_t, std::vector<Part*>> by;
       bool unknown_leader = false;
       for (Part* p : mine) {
-        if (failed.count(p)) continue;
+        if (!p->owned.load(std::memory_order_acquire)) continue;
+        auto f = failed.find(p);
+        if (f != failed.end()) {
+          if (f->second == p->since.load()) continue;
+          failed.erase(f);  // restarted by a rebalance since it failed
+        }
         if (throttled(*p)) {
           p->throttled.fetch_add(1, std::memory_order_relaxed);
           continue;
@@ -304,6 +410,7 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
       for (auto& [node, ps] : by) {
         std::vector<wire::FetchPartReq> req;
         std::map<int32_t, Part*> lookup;
+        std::map<Part*, uint64_t> since;  // a partition restarted while its fetch was in flight drops the data
         for (Part* p : ps) {
           uint64_t avail = 0;
           room(*p, &avail);
@@ -312,54 +419,60 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
             if (!failed.count(p))
               set_error("replicator: local log of " + cfg_.topic + "-" + std::to_string(p->partition) +
                         " is full (raise log_capacity)");
-            failed.insert(p);
+            failed[p] = p->since.load();
             continue;
           }
           req.push_back({p->partition, p->fetch_offset.load(),
                          int32_t(std::min<uint64_t>(uint64_t(cfg_.partition_max_bytes), avail))});
           lookup[p->partition] = p;
+          since[p] = p->since.load();
         }
         if (req.empty()) continue;
         wire::Conn& k = c->conn(node);
-        k.send(wire::kFetch, 4, c->client_id(),
-               wire::fetch_request(cfg_.topic, req, wait, cfg_.min_bytes, cfg_.max_bytes));
+        const int16_t fv = k.version(wire::kFetch);
+        k.send(wire::kFetch, fv, c->client_id(),
+               wire::fetch_request(fv, cfg_.topic, req, wait, cfg_.min_bytes, cfg_.max_bytes));
         k.begin_response(cfg_.timeout_ms + wait);
-        k.r32();  // throttle_time_ms
+        wire::fetch_response_header(k, fv);
+        std::vector<Part*> out_of_range;  // reset once the response is read: ListOffsets reuses the connection
         const int32_t nt = k.r32();
         for (int32_t i = 0; i < nt; ++i) {
           k.rstr();
           const int32_t np = k.r32();
           for (int32_t j = 0; j < np; ++j) {
-            const int32_t pid = k.r32();
-            const int16_t err = k.r16();
-            const int64_t hw = k.r64();
-            k.r64();  // last stable offset
-            const int32_t n_aborted = k.r32();
-            if (n_aborted > 0) k.skip(size_t(n_aborted) * 16);
-            const int32_t len = k.r32();
+            const wire::FetchPartHeader ph = wire::fetch_partition_header(k, fv);
+            const int32_t pid = ph.partition, len = ph.records_len;
+            const int16_t err = ph.error;
             auto it = lookup.find(pid);
             Part* p = it == lookup.end() ? nullptr : it->second;
             if (!p || err != wire::kNone) {
               if (len > 0) k.skip(size_t(len));
               if (!p) continue;
               if (err == wire::kOffsetOutOfRange) {
-                reset_offset(*c, *p);
+                out_of_range.push_back(p);
               } else {
                 set_error(std::string(wire::error_name(err)) + ": fetch " + cfg_.topic + "-" + std::to_string(pid));
                 if (wire::needs_metadata(err)) refresh = true;
               }
               continue;
             }
-            p->remote_hw.store(hw, std::memory_order_relaxed);
+            std::unique_lock<std::mutex> pg(p->mu);
+            if (!p->owned.load() || p->since.load() != since[p]) {  // revoked / restarted meanwhile
+              pg.unlock();
+              if (len > 0) k.skip(size_t(len));
+              continue;
+            }
+            p->remote_hw.store(ph.high_watermark, std::memory_order_relaxed);
             p->fetches.fetch_add(1, std::memory_order_relaxed);
             if (len <= 0) continue;
             uint64_t avail = 0;
             uint8_t* tail = room(*p, &avail);
             if (uint64_t(len) > avail) {  // an oversized first batch (KIP-74) the log cannot hold now
+              pg.unlock();
               k.skip(size_t(len));
               if (cfg_.ring_bytes && uint64_t(len) < cfg_.ring_bytes / 2) continue;  // refetched when room frees
               set_error("replicator: local log of " + cfg_.topic + "-" + std::to_string(pid) + " is full");
-              failed.insert(p);
+              failed[p] = since[p];
               continue;
             }
             k.read(tail, size_t(len));  // the record set lands in the log tail: no second copy
@@ -372,11 +485,12 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
               p->control.fetch_add(in.control, std::memory_order_relaxed);
             } catch (const KafkaError& e) {  // compressed / corrupt / old-format data: this partition stops
               set_error(std::string("replicator: ") + cfg_.topic + "-" + std::to_string(pid) + ": " + e.what());
-              failed.insert(p);
+              failed[p] = since[p];
             }
           }
         }
         k.finish();
+        for (Part* p : out_of_range) reset_offset(*c, *p);
       }
       if (refresh) {
         c->metadata(cfg_.topic);
@@ -395,10 +509,10 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
 
 int Replicator::forward(wire::Client& c) {
   std::lock_guard<std::mutex> g(commit_mu_);
-  if (fenced_.load()) return 0;  // the group moved on: these partitions may belong to another member
   std::map<int32_t, int64_t> offs;
   std::map<int32_t, Part*> by;
   for (auto& p : parts_) {
+    if (!p->owned.load()) continue;  // revoked: another member's commits now
     const int64_t off = local_->committed(group_, p->pidx);
     if (off >= 0 && off != p->forwarded.load()) {
       offs[p->partition] = off;
@@ -407,7 +521,14 @@ int Replicator::forward(wire::Client& c) {
   }
   if (offs.empty()) return 0;
   int n = 0;
-  auto errs = c.offset_commit(cfg_.group, cfg_.topic, offs, "", generation_, member_id_);
+  std::string mid;
+  int32_t gen;
+  {
+    std::lock_guard<std::mutex> a(assign_mu_);
+    mid = member_id_;
+    gen = generation_;
+  }
+  auto errs = c.offset_commit(cfg_.group, cfg_.topic, offs, "", gen, mid);
   for (auto& [pid, e] : errs) {
     auto it = by.find(pid);
     if (it == by.end()) continue;
@@ -466,6 +587,7 @@ void Replicator::release_loop() {
     std::vector<std::pair<Part*, uint64_t>> todo;
     uint64_t most = 0;
     for (auto& p : parts_) {
+      if (!p->owned.load()) continue;
       const int64_t c = local_->committed(group_, p->pidx);
       if (c < 0) continue;
       uint64_t pos = local_->position_of(p->pidx, c);
@@ -494,13 +616,14 @@ std::vector<ReplicaPartStats> Replicator::stats() {
   for (auto& p : parts_)
     v.push_back(ReplicaPartStats{p->partition, p->pidx, p->start_offset, p->fetch_offset.load(), p->remote_hw.load(),
                                  p->forwarded.load(), p->bytes.load(), p->batches.load(), p->control.load(),
-                                 p->fetches.load(), p->throttled.load(), p->released.load()});
+                                 p->fetches.load(), p->throttled.load(), p->released.load(), p->owned.load()});
   return v;
 }
 
 bool Replicator::wait_caught_up(int timeout_ms) {
   std::vector<int32_t> ids;
-  for (auto& p : parts_) ids.push_back(p->partition);
+  for (auto& p : parts_)
+    if (p->owned.load()) ids.push_back(p->partition);
   if (ids.empty()) return true;
   wire::Client c(cfg_.bootstrap, cfg_.client_id + "-lag", cfg_.timeout_ms, cfg_.security);
   auto hw = c.list_offsets(cfg_.topic, ids, -1);
@@ -508,7 +631,7 @@ bool Replicator::wait_caught_up(int timeout_ms) {
   while (std::chrono::steady_clock::now() < deadline) {
     bool all = true;
     for (auto& p : parts_)
-      if (p->fetch_offset.load() < hw[p->partition]) all = false;
+      if (p->owned.load() && p->fetch_offset.load() < hw[p->partition]) all = false;
     if (all) return true;
     sleep_ms(2);
   }

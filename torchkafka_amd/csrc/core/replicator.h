@@ -37,16 +37,17 @@ struct ReplicaConfig {
   std::string client_id = "torchkafka-replicator";
   wire::Security security;             // TLS / SASL (kafka-python's security_protocol, ssl_*, sasl_*)
   std::vector<int32_t> partitions;     // empty: every partition of the topic
-  // Subscribe mode: join `group` (JoinGroup/SyncGroup, range assignor) and mirror the partitions
-  // the coordinator assigns, as kafka-python's subscribe() does.  The partition set is fixed for
-  // the replica's lifetime: when the group rebalances the replica commits, rejoins, and carries on
-  // if it got the same partitions back; otherwise it stops fetching and forwarding ("fenced"),
-  // reports RebalanceInProgressError, and the job re-shards by restarting -- the elastic-restart
-  // model of a DDP job.  Heartbeats ride the commit thread.
+  // Subscribe mode: join `group` (JoinGroup/SyncGroup, range or round-robin assignor) and mirror
+  // the partitions the coordinator assigns, as kafka-python's subscribe() does.  Rebalances are
+  // followed in process: heartbeats (on the commit thread) notice a rebalance, the replica forwards
+  // what was consumed, rejoins, stops fetching revoked partitions and starts the newly assigned
+  // ones at the group's committed offset.  assignment_epoch() / partition_epoch() tell consumers
+  // of the local replica which partitions (re)started, so they drop what they buffered of them.
   bool subscribe = false;
   std::vector<std::string> assignors{"range"};  // partition_assignment_strategy, in preference order
   int32_t session_timeout_ms = 10000;
   int32_t heartbeat_interval_ms = 3000;
+  int32_t rebalance_timeout_ms = 0;    // JoinGroup v1+ (kafka-python: max_poll_interval_ms); 0: session timeout
   std::string auto_offset_reset = "earliest";  // without a committed offset: earliest | latest
   int32_t max_wait_ms = 100;
   int32_t min_bytes = 1;
@@ -80,6 +81,7 @@ struct ReplicaPartStats {
   uint64_t fetches;
   uint64_t throttled;       // fetch rounds skipped by flow control
   uint64_t released;        // log bytes released below the committed position
+  bool owned;               // subscribe mode: assigned to this member now
 };
 
 class Replicator {
@@ -101,12 +103,18 @@ class Replicator {
   std::vector<ReplicaPartStats> stats();
   uint32_t first_pidx() const { return first_pidx_; }
   int32_t n_partitions() const { return n_remote_parts_; }
-  // subscribe mode: this member's id / generation / assigned partitions; fenced once the group
-  // rebalanced under it
-  std::string member_id() const { return member_id_; }
-  int32_t generation() const { return generation_; }
-  std::vector<int32_t> assignment() const { return assigned_; }
-  bool fenced() const { return fenced_.load(); }
+  // subscribe mode: this member's id / generation / assigned partitions (snapshots: the commit
+  // thread rewrites them during a rebalance)
+  std::string member_id() const;
+  int32_t generation() const;
+  std::vector<int32_t> assignment() const;
+  // Bumped whenever the assignment changes; partition_epoch(p) is the epoch at which partition p
+  // was last (re)assigned to this replica -- a consumer holding older state of p must drop it.
+  uint64_t assignment_epoch() const { return epoch_.load(std::memory_order_acquire); }
+  std::vector<std::pair<int32_t, uint64_t>> assignment_epochs() const;
+  uint64_t rebalances() const { return rebalances_.load(); }
+  // Never set any more (rebalances are followed in process); kept for API compatibility.
+  bool fenced() const { return false; }
   int fetch_threads() const { return n_fetch_threads_; }
   // Blocks until every replicated partition has fetched up to the cluster's high watermark as
   // seen at call time (tests, tools); false on timeout.
@@ -122,6 +130,9 @@ class Replicator {
     std::atomic<int64_t> forwarded{-1};
     std::atomic<uint64_t> bytes{0}, batches{0}, control{0}, fetches{0}, throttled{0};
     std::atomic<uint64_t> released{0};  // log bytes [0, released) freed (committed past)
+    std::atomic<bool> owned{true};       // subscribe mode: assigned to this member now
+    std::atomic<uint64_t> since{0};      // assignment epoch at which it was (re)assigned
+    std::mutex mu;                       // a fetch's write into the log vs. a restart of the partition
   };
   void release_loop();
   void fetch_loop(std::vector<Part*> mine);
@@ -149,10 +160,14 @@ class Replicator {
   std::unique_ptr<wire::Client> commit_client_;
   std::vector<int32_t> join_group(wire::Client& c);  // sets member_id_ / generation_
   void heartbeat(wire::Client& c);
+  // Starts owned partitions at the group's committed offset (else auto_offset_reset).
+  void start_parts(wire::Client& c, const std::vector<Part*>& ps, bool fresh);
+  void apply_assignment(wire::Client& c, const std::vector<int32_t>& mine);
+  mutable std::mutex assign_mu_;  // member_id_ / generation_ / assigned_ snapshots for readers
   std::string member_id_;
   int32_t generation_ = -1;
   std::vector<int32_t> assigned_;
-  std::atomic<bool> fenced_{false};
+  std::atomic<uint64_t> epoch_{0}, rebalances_{0};
   int64_t last_heartbeat_ms_ = 0;
   int n_fetch_threads_ = 0;
 };

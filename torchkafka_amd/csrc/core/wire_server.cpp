@@ -99,8 +99,17 @@ struct Response {
 }  // namespace
 
 WireServer::WireServer(std::shared_ptr<Broker> broker, const std::string& host, int port, int32_t node_id,
-                       std::vector<WireNode> cluster)
+                       std::vector<WireNode> cluster, const std::string& profile)
     : b_(std::move(broker)), host_(host), port_(port), node_(node_id), cluster_(std::move(cluster)) {
+  // the Python server's PROFILES (broker/wire_server.py) for the APIs served here
+  if (profile == "legacy" || profile == "ancient") {
+    versions_ = {{1, 4, 4}, {2, 0, 1}, {3, 0, 1}, {8, 2, 2}, {9, 1, 1}, {10, 0, 0}, {18, 0, 0}};
+    api_versions_ = profile == "legacy";
+  } else if (profile == "kafka4") {
+    versions_ = {{1, 4, 11}, {2, 1, 5}, {3, 4, 8}, {8, 2, 7}, {9, 1, 5}, {10, 0, 2}, {18, 0, 2}};
+  } else {
+    throw std::invalid_argument("wire server profile '" + profile + "': legacy | kafka4 | ancient");
+  }
   listen_fd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
   if (listen_fd_ < 0) throw_errno("wire server socket");
   int one = 1;
@@ -179,6 +188,12 @@ void WireServer::serve(int fd) {
   ::close(fd);
 }
 
+bool WireServer::serves(int16_t key, int16_t ver) const {
+  for (auto& v : versions_)
+    if (v[0] == key) return ver >= v[1] && ver <= v[2] && (key != wire::kApiVersions || api_versions_);
+  return false;
+}
+
 int32_t WireServer::leader(int32_t partition) const {
   return cluster_[size_t(partition) % cluster_.size()].node_id;
 }
@@ -192,20 +207,22 @@ bool WireServer::handle(int fd, const std::vector<uint8_t>& req) {
   requests_.fetch_add(1, std::memory_order_relaxed);
   Response out;
   wire::Writer& w = out.w;
-  switch (key) {
-    case wire::kApiVersions: {
-      const int16_t apis[][3] = {{1, 4, 4}, {2, 0, 1}, {3, 0, 1}, {8, 2, 2}, {9, 1, 1}, {10, 0, 0}, {18, 0, 0}};
-      w.i16(0);
-      w.array(int32_t(sizeof(apis) / sizeof(apis[0])));
-      for (auto& a : apis) {
-        w.i16(a[0]);
-        w.i16(a[1]);
-        w.i16(a[2]);
-      }
-      break;
+  if (key == wire::kApiVersions) {
+    if (!api_versions_) return false;  // predates ApiVersions: close
+    const bool ok = serves(key, ver);
+    w.i16(ok ? int16_t(0) : int16_t(wire::kUnsupportedVersion));  // v0 layout on a version error
+    w.array(int32_t(versions_.size()));
+    for (auto& a : versions_) {
+      w.i16(a[0]);
+      w.i16(a[1]);
+      w.i16(a[2]);
     }
+    if (ok && ver >= 1) w.i32(0);  // throttle
+    return out.send(fd, corr, &bytes_);
+  }
+  if (!serves(key, ver)) return false;  // an unsupported version / API closes the connection, as Kafka does
+  switch (key) {
     case wire::kMetadata: {
-      if (ver > 1) return false;
       std::vector<std::string> names;
       const int32_t nt = r.i32();
       if (nt < 0 || (nt == 0 && ver == 0)) {
@@ -213,6 +230,7 @@ bool WireServer::handle(int fd, const std::vector<uint8_t>& req) {
       } else {
         for (int32_t i = 0; i < nt; ++i) names.push_back(r.str());
       }
+      if (ver >= 3) w.i32(0);  // throttle
       w.array(int32_t(cluster_.size()));
       for (auto& n : cluster_) {
         w.i32(n.node_id);
@@ -220,6 +238,7 @@ bool WireServer::handle(int fd, const std::vector<uint8_t>& req) {
         w.i32(n.port);
         if (ver >= 1) w.nullable_str_null();
       }
+      if (ver >= 2) w.str("torchkafka-synthetic");  // cluster id
       if (ver >= 1) w.i32(cluster_[0].node_id);
       w.array(int32_t(names.size()));
       for (auto& name : names) {
@@ -234,17 +253,24 @@ bool WireServer::handle(int fd, const std::vector<uint8_t>& req) {
           w.i16(0);
           w.i32(int32_t(p));
           w.i32(l);
+          if (ver >= 7) w.i32(0);  // leader epoch
           w.array(1);
           w.i32(l);
           w.array(1);
           w.i32(l);
+          if (ver >= 5) w.array(0);  // offline replicas
         }
+        if (ver >= 8) w.i32(INT32_MIN);  // topic authorized operations: not requested
       }
+      if (ver >= 8) w.i32(INT32_MIN);
       break;
     }
     case wire::kListOffsets: {
-      if (ver > 1) return false;
       r.i32();  // replica
+      if (ver >= 2) {
+        r.i8();    // isolation level
+        w.i32(0);  // throttle
+      }
       const int32_t nt = r.i32();
       w.array(nt);
       for (int32_t i = 0; i < nt; ++i) {
@@ -256,6 +282,7 @@ bool WireServer::handle(int fd, const std::vector<uint8_t>& req) {
         w.array(np);
         for (int32_t j = 0; j < np; ++j) {
           const int32_t p = r.i32();
+          if (ver >= 4) r.i32();  // current leader epoch
           const int64_t ts = r.i64();
           if (ver == 0) r.i32();
           int16_t err = 0;
@@ -276,18 +303,22 @@ bool WireServer::handle(int fd, const std::vector<uint8_t>& req) {
           } else {
             w.i64(-1);
             w.i64(off);
+            if (ver >= 4) w.i32(0);  // leader epoch
           }
         }
       }
       break;
     }
     case wire::kFetch: {
-      if (ver != 4) return false;
       r.i32();  // replica
       const int32_t max_wait = r.i32();
       const int32_t min_bytes = r.i32();
       const int32_t max_bytes = r.i32();
       r.i8();   // isolation level
+      if (ver >= 7) {
+        r.i32();  // session id / epoch: every fetch is answered in full
+        r.i32();
+      }
       struct Req { std::string topic; TopicInfo t; bool ok; std::vector<std::tuple<int32_t, int64_t, int32_t>> parts; };
       std::vector<Req> reqs(size_t(std::max(0, r.i32())));
       for (auto& q : reqs) {
@@ -296,7 +327,9 @@ bool WireServer::handle(int fd, const std::vector<uint8_t>& req) {
         const int32_t np = r.i32();
         for (int32_t j = 0; j < np; ++j) {
           const int32_t p = r.i32();
+          if (ver >= 9) r.i32();  // current leader epoch
           const int64_t off = r.i64();
+          if (ver >= 5) r.i64();  // log start offset (a follower's)
           const int32_t pmax = r.i32();
           q.parts.emplace_back(p, off, pmax);
         }
@@ -314,8 +347,17 @@ bool WireServer::handle(int fd, const std::vector<uint8_t>& req) {
         std::this_thread::sleep_for(std::chrono::microseconds(500));
       }
       w.i32(0);  // throttle
+      if (ver >= 7) {
+        w.i16(0);  // error
+        w.i32(0);  // session id: none
+      }
       w.array(int32_t(reqs.size()));
       int64_t budget = max_bytes;
+      auto part_tail = [&](int64_t log_start) {  // the fields between last_stable_offset and the records
+        if (ver >= 5) w.i64(log_start);
+        w.i32(-1);                 // aborted transactions: null
+        if (ver >= 11) w.i32(-1);  // preferred read replica
+      };
       for (auto& q : reqs) {
         w.str(q.topic);
         w.array(int32_t(q.parts.size()));
@@ -326,7 +368,7 @@ bool WireServer::handle(int fd, const std::vector<uint8_t>& req) {
                                                                     : int16_t(wire::kUnknownTopicOrPartition));
             w.i64(-1);
             w.i64(-1);
-            w.i32(-1);
+            part_tail(-1);
             w.i32(-1);
             continue;
           }
@@ -338,7 +380,7 @@ bool WireServer::handle(int fd, const std::vector<uint8_t>& req) {
             w.i16(wire::kOffsetOutOfRange);
             w.i64(hw);
             w.i64(hw);
-            w.i32(-1);
+            part_tail(start);
             w.i32(-1);
             continue;
           }
@@ -361,7 +403,7 @@ bool WireServer::handle(int fd, const std::vector<uint8_t>& req) {
           w.i16(0);
           w.i64(hw);
           w.i64(hw);
-          w.i32(-1);  // aborted transactions: null
+          part_tail(start);
           w.i32(int32_t(n));
           if (n) out.slice(data, n);  // sent from the mapped log
         }
@@ -370,18 +412,24 @@ bool WireServer::handle(int fd, const std::vector<uint8_t>& req) {
     }
     case wire::kFindCoordinator: {
       r.str();
+      if (ver >= 1) {
+        r.i8();    // key type
+        w.i32(0);  // throttle
+      }
       w.i16(0);
+      if (ver >= 1) w.nullable_str_null();  // error message
       w.i32(cluster_[0].node_id);
       w.str(cluster_[0].host);
       w.i32(cluster_[0].port);
       break;
     }
     case wire::kOffsetCommit: {
-      if (ver != 2) return false;
       const std::string group = r.str();
       r.i32();
       r.str();
-      r.i64();
+      if (ver >= 7) r.str();  // group instance id
+      if (ver <= 4) r.i64();  // retention
+      if (ver >= 3) w.i32(0);  // throttle
       const uint32_t g = b_->group_index(group, true);
       const int32_t nt = r.i32();
       w.array(nt);
@@ -395,6 +443,7 @@ bool WireServer::handle(int fd, const std::vector<uint8_t>& req) {
         for (int32_t j = 0; j < np; ++j) {
           const int32_t p = r.i32();
           const int64_t off = r.i64();
+          if (ver >= 6) r.i32();  // committed leader epoch
           const std::string meta = r.str();
           int16_t err = 0;
           if (!ok || p < 0 || uint32_t(p) >= t.n_partitions) {
@@ -413,19 +462,31 @@ bool WireServer::handle(int fd, const std::vector<uint8_t>& req) {
       break;
     }
     case wire::kOffsetFetch: {
-      if (ver != 1) return false;
       const uint32_t g = b_->group_index(r.str(), true);
+      if (ver >= 3) w.i32(0);  // throttle
       const int32_t nt = r.i32();
-      w.array(nt);
-      for (int32_t i = 0; i < nt; ++i) {
-        const std::string name = r.str();
+      std::vector<std::pair<std::string, std::vector<int32_t>>> reqs;
+      if (nt < 0) {  // v2+: every topic
+        for (auto& t : b_->topics()) {
+          std::vector<int32_t> ps;
+          for (uint32_t p = 0; p < t.n_partitions; ++p) ps.push_back(int32_t(p));
+          reqs.emplace_back(t.name, ps);
+        }
+      } else {
+        for (int32_t i = 0; i < nt; ++i) {
+          std::string name = r.str();
+          std::vector<int32_t> ps(size_t(std::max(0, r.i32())));
+          for (auto& p : ps) p = r.i32();
+          reqs.emplace_back(std::move(name), std::move(ps));
+        }
+      }
+      w.array(int32_t(reqs.size()));
+      for (auto& [name, ps] : reqs) {
         TopicInfo t;
         const bool ok = b_->find_topic(name, &t);
-        const int32_t np = r.i32();
         w.str(name);
-        w.array(np);
-        for (int32_t j = 0; j < np; ++j) {
-          const int32_t p = r.i32();
+        w.array(int32_t(ps.size()));
+        for (int32_t p : ps) {
           std::string meta;
           int64_t off = -1;
           int16_t err = 0;
@@ -433,10 +494,12 @@ bool WireServer::handle(int fd, const std::vector<uint8_t>& req) {
           else off = b_->committed(g, t.first_pidx + uint32_t(p), &meta);
           w.i32(p);
           w.i64(off);
+          if (ver >= 5) w.i32(-1);  // committed leader epoch
           w.str(meta);
           w.i16(err);
         }
       }
+      if (ver >= 2) w.i16(0);  // top-level error
       break;
     }
     default:
