@@ -42,6 +42,8 @@ py::tuple record_tuple(const RecordView& r, int ts_type) {
 struct PyFetcher {
   Fetcher f;
   size_t rr = 0;
+  bool last_reassigned = false;  // the last fill_slot returned early: the watched assignment changed
+  py::list watched;              // the Replicators whose epochs f watches (kept alive here)
   PyFetcher(std::shared_ptr<Broker> b, bool crc) : f(std::move(b), crc) {}
 };
 
@@ -647,6 +649,18 @@ PYBIND11_MODULE(_tkcore, m) {
   py::class_<PyFetcher>(m, "Fetcher")
       .def(py::init<std::shared_ptr<Broker>, bool>(), py::arg("broker"), py::arg("check_crcs") = true)
       .def("assign", [](PyFetcher& f, std::vector<uint32_t> p, std::vector<int64_t> pos) { f.f.assign(p, pos); })
+      .def(
+          "watch",
+          [](PyFetcher& f, py::list replicators) {
+            std::vector<const std::atomic<uint64_t>*> eps;
+            for (auto h : replicators) eps.push_back(h.cast<Replicator&>().epoch_ptr());
+            f.watched = replicators;
+            f.f.set_watch(std::move(eps));
+          },
+          py::arg("replicators"),
+          "group-managed: fills return early (last_reassigned) when these replicas' assignment changes")
+      .def("set_watch_base", [](PyFetcher& f, uint64_t base) { f.f.set_watch_base(base); }, py::arg("epoch_sum"))
+      .def_property_readonly("last_reassigned", [](PyFetcher& f) { return f.last_reassigned; })
       .def("assigned", [](PyFetcher& f) {
         py::list l;
         for (auto& p : f.f.parts()) l.append(p.pidx);
@@ -785,6 +799,7 @@ PYBIND11_MODULE(_tkcore, m) {
               py::gil_scoped_release nogil;
               o = fill_slot(f.f, *ring.r, gslot, s, batch_rows, timeout_ms, &f.rr);
             }
+            f.last_reassigned = o.reassigned;
             return py::make_tuple(o.rows, o.scanned, o.timed_out, o.shutdown);
           },
           py::arg("ring"), py::arg("gslot"), py::arg("kind"), py::arg("elem_size"), py::arg("row_elems"),

@@ -992,7 +992,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   int64_t last_progress = now_ns();
   int64_t backoff_ns = 20000;
   bool stop = false;
-  while (rows < B && !stop && !parts.empty()) {
+  while (rows < B && !stop && (!parts.empty() || f.watching())) {
     bool progress = false;
     for (size_t k = 0; k < parts.size() && rows < B; ++k) {
       cur_part = (*rr + k) % parts.size();
@@ -1012,7 +1012,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
         break;
       }
     }
-    *rr = (*rr + 1) % std::max<size_t>(parts.size(), 1);
+    *rr = (*rr + 1) % std::max<size_t>(parts.size(), 1);  // (no partitions: a group member waits for some)
     if (rows >= B || stop) break;
     if (progress) {
       last_progress = now_ns();
@@ -1020,6 +1020,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
       continue;
     }
     if (ring.header()->shutdown.load(std::memory_order_acquire)) { out.shutdown = true; break; }
+    if (f.watching() && f.watch_changed()) { out.reassigned = true; break; }
     const int64_t now = now_ns();
     if (now - last_progress >= idle_ns) { out.timed_out = true; break; }
     const int64_t sl = std::min<int64_t>(backoff_ns, idle_ns - (now - last_progress));

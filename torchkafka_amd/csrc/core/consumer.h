@@ -8,6 +8,7 @@
 // pack values into a pinned ring slot as either a dense [rows, D] block or a
 // CSR (int32 row offsets + values) for variable-length rows.
 #pragma once
+#include <atomic>
 #include <memory>
 #include <vector>
 
@@ -62,6 +63,19 @@ class Fetcher {
   static constexpr uint64_t kPrefaultBytes = 4u << 20;
   void prefault(FetchPart& fp, const uint8_t* log, uint64_t pos, uint64_t log_end);
 
+  // Group-managed consumers: the assignment epochs of the replicas whose group assigns this
+  // fetcher's partitions (replicator.h).  While a fill waits for data it returns early
+  // (FillOutcome::reassigned) once their sum leaves `base`, so the caller can take the new
+  // assignment instead of waiting on partitions that moved to another member.
+  void set_watch(std::vector<const std::atomic<uint64_t>*> epochs) { watch_ = std::move(epochs); }
+  void set_watch_base(uint64_t base) { watch_base_ = base; }
+  bool watching() const { return !watch_.empty(); }
+  bool watch_changed() const {
+    uint64_t sum = 0;
+    for (auto* e : watch_) sum += e->load(std::memory_order_acquire);
+    return sum != watch_base_;
+  }
+
  private:
   std::shared_ptr<Broker> b_;
   bool check_crcs_;
@@ -74,6 +88,8 @@ class Fetcher {
  private:
   bool sparse_touch_ = false;
   std::vector<FetchPart> parts_;
+  std::vector<const std::atomic<uint64_t>*> watch_;
+  uint64_t watch_base_ = 0;
 };
 
 // ------------------------------------------------------------ packers
@@ -117,6 +133,7 @@ struct FillOutcome {
   int64_t scanned = 0;
   bool timed_out = false;
   bool shutdown = false;
+  bool reassigned = false;  // a watched group assignment changed while waiting (Fetcher::set_watch)
 };
 
 // Fills one ring slot with up to `batch_rows` rows, blocking until the batch

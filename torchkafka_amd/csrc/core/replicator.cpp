@@ -378,6 +378,12 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
   std::map<Part*, uint64_t> failed;  // -> assignment epoch at the failure
   int backoff_ms = 0;
   while (!stop_.load()) {
+    // subscribe mode: a thread whose partitions are all assigned elsewhere holds no connection
+    if (cfg_.subscribe && std::none_of(mine.begin(), mine.end(), [](Part* p) { return p->owned.load(); })) {
+      c.reset();
+      sleep_ms(5);
+      continue;
+    }
     try {
       if (!c) {
         c = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id, cfg_.timeout_ms, cfg_.security);
@@ -514,6 +520,9 @@ int Replicator::forward(wire::Client& c) {
   for (auto& p : parts_) {
     if (!p->owned.load()) continue;  // revoked: another member's commits now
     const int64_t off = local_->committed(group_, p->pidx);
+    // subscribe mode: an offset below where this ownership started (the group's committed offset
+    // then) comes from a batch consumed in an earlier ownership -- never move the group back
+    if (cfg_.subscribe && off < p->start_offset) continue;
     if (off >= 0 && off != p->forwarded.load()) {
       offs[p->partition] = off;
       by[p->partition] = p.get();

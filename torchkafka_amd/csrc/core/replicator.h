@@ -111,6 +111,7 @@ class Replicator {
   // Bumped whenever the assignment changes; partition_epoch(p) is the epoch at which partition p
   // was last (re)assigned to this replica -- a consumer holding older state of p must drop it.
   uint64_t assignment_epoch() const { return epoch_.load(std::memory_order_acquire); }
+  const std::atomic<uint64_t>* epoch_ptr() const { return &epoch_; }
   std::vector<std::pair<int32_t, uint64_t>> assignment_epochs() const;
   uint64_t rebalances() const { return rebalances_.load(); }
   // Never set any more (rebalances are followed in process); kept for API compatibility.

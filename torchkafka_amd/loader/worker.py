@@ -222,7 +222,12 @@ def _native_loop(ring, worker_id, spw, consumer, schema, cfg, state) -> None:
     gather = bool(cfg.get("gather")) and kind == core().PACK_FIXED
     span = (bool(cfg.get("span")) and kind in (core().PACK_FIXED, core().PACK_JSON_TEXT, core().PACK_VARLEN)
             and not gather)
-    if not fetcher.assigned() and cfg["sharding"] == "static":
+    # a member of a Kafka group over KafkaBridge replicas: the partitions move with rebalances, and
+    # a fill waiting for data returns early when they do
+    group_managed = bool(getattr(consumer, "_group_managed", False))
+    if group_managed:
+        fetcher.watch([br._r for br in consumer._bridges])
+    if not fetcher.assigned() and cfg["sharding"] == "static" and not group_managed:
         g = _acquire(ring, worker_id, state)  # nothing to read, ever: end of stream right away
         ring.set_slot(g, 0, core().SLOT_EOS, kind, 0, 0, 0, 0, 0, [])
         _publish(ring, worker_id, spw, state)
@@ -231,10 +236,16 @@ def _native_loop(ring, worker_id, spw, consumer, schema, cfg, state) -> None:
         g = _acquire(ring, worker_id, state)
         consumer._ensure_group()
         while True:
+            if group_managed:
+                fetcher.set_watch_base(consumer._seen_epoch)
             try:
                 rows, _scanned, timed_out, shut = fetcher.fill_slot(ring, g, kind, elem, row_elems, min_len,
                                                                     max_len, trunc, skip_bad, bs, timeout,
                                                                     gather, span)
+                if group_managed and fetcher.last_reassigned:
+                    consumer._ensure_group()  # the next fill reads the new assignment
+                    if rows == 0:
+                        continue  # nothing packed yet: fill this slot from the new partitions
                 break
             except OffsetOutOfRangeError:
                 # retention moved past a position: reset it like the consumer would and refill this slot

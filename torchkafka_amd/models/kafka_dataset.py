@@ -347,19 +347,65 @@ def _make_consumer(*topics, **kwargs):
         try:  # pragma: no cover - kafka-python is not installed in this image
             from kafka import KafkaConsumer as _KP  # type: ignore
 
+            kwargs.pop(ASSIGNMENT_KEY, None)  # kafka-python's subscribe() is group-managed
             return _KP(*topics, **kwargs)
         except ImportError:
             return _bridged_consumer(topics, kwargs)
+    # the synthetic broker runs its own group coordinator: subscribing consumers are group-managed
+    kwargs.pop(ASSIGNMENT_KEY, None)
     return KafkaConsumer(*topics, **kwargs)
+
+
+#: consumer kwargs naming how a real cluster's partitions are split (not a kafka-python key)
+ASSIGNMENT_KEY = "assignment"
+_ASSIGNORS = {"range": "range", "roundrobin": "roundrobin", "rangepartitionassignor": "range",
+              "roundrobinpartitionassignor": "roundrobin"}
+
+
+def _assignor_names(strategy) -> list[str]:
+    """kafka-python's partition_assignment_strategy (assignor classes or names) -> native names."""
+    if not strategy:
+        return ["range"]
+    out = []
+    for a in strategy:
+        name = getattr(a, "name", None) or getattr(a, "__name__", None) or str(a)
+        key = str(name).lower()
+        if key not in _ASSIGNORS:
+            raise KafkaError(f"partition_assignment_strategy {name!r}: the native client implements the range "
+                             "and round-robin assignors")
+        out.append(_ASSIGNORS[key])
+    return out
+
+
+def _assignment_mode(kwargs) -> str:
+    """'group' (the group coordinator assigns partitions, rebalancing as members come and go -- the
+    reference's kafka-python behaviour, B21) or 'static' (partition p to rank p % world, worker
+    (p // world) % num_workers).  Default: group with a group_id outside torch.distributed; static
+    under DDP, whose lockstep needs every rank's share fixed."""
+    from ..parallel.sharding import dist_rank_world
+
+    mode = kwargs.pop(ASSIGNMENT_KEY, None) or os.environ.get("TORCHKAFKA_ASSIGNMENT", "auto")
+    if mode not in ("auto", "group", "static"):
+        raise ValueError(f"assignment={mode!r}: 'auto', 'group' or 'static'")
+    if mode == "group" and not kwargs.get("group_id"):
+        raise ValueError("assignment='group' needs a group_id")
+    if mode == "auto":
+        mode = "group" if kwargs.get("group_id") and dist_rank_world()[1] == 1 else "static"
+    return mode
 
 
 def _bridged_consumer(topics, kwargs):
     """A consumer of a real cluster without kafka-python: a native KafkaBridge per topic mirrors
-    this process's share of the partitions into a local replica, and the built-in consumer reads
-    it; its commits reach the cluster's group coordinator (forwarded within 5 ms, flushed by
-    ``close()``).  The share is static -- partition p goes to rank ``p % world`` and, there, to
-    DataLoader worker ``(p // world) % num_workers`` -- where kafka-python's group membership would
-    rebalance them among the group's consumers (reference kafka_dataset.py:206)."""
+    this consumer's partitions into a local replica, and the built-in consumer reads it; its
+    commits reach the cluster's group coordinator (forwarded within 5 ms, flushed by ``close()``).
+
+    Which partitions (:func:`_assignment_mode`): with a ``group_id`` outside torch.distributed,
+    each consumer -- every DataLoader worker's, as in the reference (kafka_dataset.py:206,
+    219-231) -- is a member of the group: the coordinator's assignor splits the partitions among
+    all members of all processes, and rebalances move them while the loader runs (the bridge
+    follows in process; the consumer drops what it buffered of revoked partitions and restarts
+    newly assigned ones at the group's committed offset).  Under DDP (or ``assignment="static"``)
+    partition p goes to rank ``p % world`` and, there, to worker ``(p // world) % num_workers``."""
     from ..broker.bridge import KafkaBridge
     from ..ops.native import core
     from ..parallel.sharding import dist_rank_world, shard_partitions
@@ -367,6 +413,8 @@ def _bridged_consumer(topics, kwargs):
     if not topics or not all(isinstance(t, str) for t in topics):
         raise NoBrokersAvailable("NoBrokersAvailable: kafka-python is not installed; the native Kafka "
                                  "client needs the topics named up front")
+    kwargs = dict(kwargs)
+    mode = _assignment_mode(kwargs)
     servers = kwargs.get("bootstrap_servers", "localhost:9092")
     if not isinstance(servers, str):
         servers = ",".join(servers)
@@ -379,23 +427,34 @@ def _bridged_consumer(topics, kwargs):
     security = security_config(**{k: v for k, v in kwargs.items() if k in SECURITY_KEYS})
     client = core().WireClient(servers, str(kwargs.get("client_id", "torchkafka")), timeout, security)
     bridges, tps, url = [], [], None
+    group = dict(subscribe=True, session_timeout_ms=int(kwargs.get("session_timeout_ms", 10000)),
+                 heartbeat_interval_ms=int(kwargs.get("heartbeat_interval_ms", 3000)),
+                 partition_assignment_strategy=_assignor_names(kwargs.get("partition_assignment_strategy")),
+                 rebalance_timeout_ms=int(kwargs.get("max_poll_interval_ms", 0) or 0)) if mode == "group" else {}
     try:
         for t in topics:
             err, parts = client.metadata(t)
             if err:
                 raise KafkaError(f"UnknownTopicOrPartitionError: topic {t!r} on {servers}")
-            mine = shard_partitions(len(parts), rank, world, wid, nw)
+            mine = None if mode == "group" else shard_partitions(len(parts), rank, world, wid, nw)
             br = KafkaBridge(servers, t, group_id=kwargs.get("group_id"), partitions=mine, url=url,
                              auto_offset_reset=kwargs.get("auto_offset_reset", "latest"), request_timeout_ms=timeout,
-                             **security)
+                             **group, **security)
             br._own = url is None
             url = br.url
             bridges.append(br)
-            tps += [TopicPartition(t, p) for p in mine]
-        cons = _BridgedConsumer(**{**{k: v for k, v in kwargs.items() if k not in SECURITY_KEYS},
-                                   "bootstrap_servers": url})  # the replica is local: plaintext
+            if mine is not None:
+                tps += [TopicPartition(t, p) for p in mine]
+        local = {k: v for k, v in kwargs.items() if k not in SECURITY_KEYS}
+        local["bootstrap_servers"] = url  # the replica is local: plaintext
+        for k in ("partition_assignment_strategy",):
+            local.pop(k, None)
+        cons = _BridgedConsumer(**local)
         cons._bridges = bridges
+        cons._group_managed = mode == "group"
         cons.assign(tps)
+        if cons._group_managed:
+            cons._follow_bridges()
         # a DataLoader worker ends through multiprocessing's exit hooks, not close(): forward the
         # last commits there, after the dataset's own final commit service (exitpriority 100)
         import multiprocessing.util as mpu
@@ -417,10 +476,91 @@ def _flush_bridges(bridges) -> None:
 
 
 class _BridgedConsumer(KafkaConsumer):
-    """The built-in consumer over a KafkaBridge replica; closing it flushes the bridge's commits."""
+    """The built-in consumer over KafkaBridge replicas; closing it flushes the bridges' commits.
+
+    Group-managed (``_group_managed``): the assignment follows the bridges' -- i.e. the group
+    coordinator's.  Before fetching, returning a record or committing, the consumer checks the
+    bridges' assignment epoch; on a change it drops buffered records of revoked and restarted
+    partitions, starts (re)assigned ones at the committed offset the bridge seeded, and ignores
+    commits below that offset from before the restart (a batch consumed in an older ownership can
+    never move the group's offset backwards)."""
 
     _bridges: list = []
-    _bridged_shard = True  # assigned this process's static share of the partitions already
+    _bridged_shard = True  # assigned this process's share of the partitions already
+    _group_managed = False
+
+    def _bridges_epoch(self) -> int:
+        return sum(br.assignment_epoch for br in self._bridges)
+
+    def _follow_bridges(self) -> None:
+        epoch = self._bridges_epoch()
+        if epoch == getattr(self, "_seen_epoch", None):
+            return
+        epochs = {}
+        for br in self._bridges:
+            for p, e in br.assignment_epochs():
+                epochs[self._broker.pidx(br.topic, p)] = e
+        old_epochs = getattr(self, "_part_epochs", {})
+        floors = getattr(self, "_floors", {})
+        kept = {p for p, e in epochs.items() if old_epochs.get(p) == e}
+        pidxs = sorted(epochs)
+        old = self._fetcher.positions()
+        positions = [old[p] if p in kept and p in old else self._initial_position(p) for p in pidxs]
+        self._fetcher.assign(pidxs, positions)
+        for p in pidxs:
+            if p in self._paused:
+                self._fetcher.pause(p, True)
+        if self._buffer:
+            self._buffer = deque(r for r in self._buffer if r[0] in kept)
+        for p, pos in zip(pidxs, positions):
+            if p not in kept:
+                self._position[p] = pos
+                floors[p] = pos
+        self._position = {p: v for p, v in self._position.items() if p in epochs}
+        self._assignment = pidxs
+        self._part_epochs, self._floors, self._seen_epoch = epochs, floors, epoch
+        self._sync_positions()
+        if set(pidxs) != set(old):
+            _logger.debug("Group %s assignment now %s.", self.config["group_id"], [self._tp(p) for p in pidxs])
+
+    def _ensure_group(self, block: bool = True) -> None:
+        if self._group_managed:
+            self._follow_bridges()
+            return
+        super()._ensure_group(block)
+
+    def __next__(self):
+        if self._group_managed and self._buffer and self._bridges_epoch() != self._seen_epoch:
+            self._follow_bridges()  # never hand out a buffered record of a revoked partition
+        return super().__next__()
+
+    def commit(self, offsets=None) -> None:
+        if self._group_managed:
+            if offsets is None:
+                self._follow_bridges()  # commits the positions of what is owned now
+            else:
+                offsets = self._owned_offsets(offsets)
+                if not offsets:
+                    return
+        super().commit(offsets)
+
+    def _owned_offsets(self, offsets: dict) -> dict:
+        """The entries of ``offsets`` this consumer may still commit: partitions it owns in the
+        same assignment epoch it consumed them in, at or past where that ownership started.  Reads
+        the bridges' epochs without touching the fetcher (a DeviceLoader worker commits from a
+        thread beside the fill)."""
+        live = {}
+        for br in self._bridges:
+            for p, e in br.assignment_epochs():
+                live[self._broker.pidx(br.topic, p)] = e
+        seen, floors = getattr(self, "_part_epochs", {}), getattr(self, "_floors", {})
+        keep = {}
+        for tp, om in offsets.items():
+            p = self._pidx(tp)
+            off = om.offset if isinstance(om, OffsetAndMetadata) else int(om)
+            if p in live and live[p] == seen.get(p) and off >= floors.get(p, -1):
+                keep[tp] = om
+        return keep
 
     def close(self, autocommit: bool = True) -> None:
         try:
