@@ -36,7 +36,12 @@ sides, max over ranks, whole-job records):
     earliest offset) with ``h2d="dma"``: the partition logs are copied into HBM
     by hipMemcpyAsync on a side stream (SDMA) and decoded there -- the config-2
     mechanism;
-  * ``steady_f32``: a third loader delivering float32 (the reference's dtype).
+  * ``steady_f32``: a third loader delivering float32 (the reference's dtype);
+  * ``bridge``: the same records served over the Kafka protocol (a native C++ wire server on the
+    loopback interface, Kafka 4.x version profile) to a DeviceLoader whose KafkaBridge mirrors this
+    rank's partitions into a local ring replica and forwards every commit to the group
+    coordinator -- ``async`` (the default commit mode; coordinator round trips reported) and
+    ``sync`` (``commit="sync"``: batch k's OffsetCommit answered before batch k+1 is handed out).
 """
 from __future__ import annotations
 
@@ -97,6 +102,9 @@ def parse():
                          "mirror filled by SDMA), f32 (float32 output); '' for none")
     ap.add_argument("--extra-steps", type=int, default=None,
                     help="timed steps of each secondary block (default: the steady-state steps)")
+    ap.add_argument("--bridge-steps", type=int, default=None,
+                    help="timed steps of the Kafka-protocol bridge blocks (async; sync runs a quarter): "
+                         "default 8000 on a GPU, 200 on the CPU; 0 skips them")
     return ap.parse_args()
 
 
@@ -354,16 +362,16 @@ def run_rank(args) -> int:
 
     R.init_group()
 
-    def make_loader(group: str, dtype, h2d: str):
+    def make_loader(group: str, dtype, h2d: str, servers: str = url, commit: str = "async"):
         return DeviceLoader(
             Records.placeholder(), B, num_workers=args.workers, device=device, dtype=dtype,
             slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
             in_order=args.in_order, h2d=h2d, copy_streams=args.copy_streams, lockstep_depth=args.lockstep_depth,
             event_every=args.event_every, numa_bind=not args.no_numa, coalesce=args.coalesce,
             coalesce_wait_us=args.coalesce_wait_us, decode=args.decode, lockstep=lockstep,
-            mirror_chunk_mib=args.mirror_chunk_mib,
+            mirror_chunk_mib=args.mirror_chunk_mib, commit=commit,
             **({"mirror_chunks": args.mirror_chunks} if args.mirror_chunks else {}),
-            worker_init_fn=Records.init_worker("bench", bootstrap_servers=url, group_id=group,
+            worker_init_fn=Records.init_worker("bench", bootstrap_servers=servers, group_id=group,
                                                auto_offset_reset="earliest", check_crcs=not args.no_crc),
         )
 
@@ -428,6 +436,49 @@ def run_rank(args) -> int:
         if world > 1:
             R.barrier()
 
+    # the Kafka-protocol route: this rank's partitions over a loopback wire server -> bridge replica
+    bridge_out = None
+    bsteps = args.bridge_steps if args.bridge_steps is not None else (8000 if device.type == "cuda" else 200)
+    if bsteps > 0:
+        from torchkafka_amd.broker import NativeWireServer
+
+        srv = NativeWireServer(broker, profile="kafka4").start()
+        bridge_out = {"server": "NativeWireServer (C++), loopback TCP, Kafka 4.x protocol profile",
+                      "replica": "KafkaBridge ring replica of this rank's partitions (static shard)"}
+        try:
+            for mode, steps in (("async", bsteps), ("sync", max(1, bsteps // 4))):
+                ld = make_loader(f"bench-bridge-{mode}", dtypes[args.dtype], args.h2d, servers=srv.address,
+                                 commit=mode)
+                bit = iter(auto_commit(ld))
+                for _ in range(extra_warm):
+                    next(bit)
+                for br in ld._bridges:
+                    br.take_forward_ns()
+                bres = time_steps(R, bit, steps, ld)
+                blk = steady_block(R, bres, steps, args.dim)
+                rtt = sorted(x / 1e3 for br in ld._bridges for x in br.take_forward_ns())
+                if mode == "async":
+                    blk["commit_latency_means"] = "request of batch k+1 -> batch k stored in the replica's table"
+                    blk["coordinator_rtt_p50_us"] = round(rtt[len(rtt) // 2], 1) if rtt else None
+                    blk["coordinator_rtt_p99_us"] = round(rtt[min(len(rtt) - 1, len(rtt) * 99 // 100)], 1) if rtt else None
+                    blk["coordinator_commits"] = len(rtt)
+                    blk["forward_interval_ms"] = 5
+                else:
+                    st = bres["stats"]
+                    blk["commit_latency_means"] = ("request of batch k+1 -> batch k's OffsetCommit answered by "
+                                                   "the coordinator (sync_commit_*)")
+                    blk["sync_commit_p50_us"] = round(st["sync_commit_p50_us"], 1)
+                    blk["sync_commit_p99_us"] = round(st["sync_commit_p99_us"], 1)
+                    blk["sync_commits"] = st["sync_commits"]
+                blk["bridge_errors"] = sum(br.errors for br in ld._bridges)
+                bridge_out[mode] = blk
+                bit.close()
+                ld.close()
+                if world > 1:
+                    R.barrier()
+        finally:
+            srv.close()
+
     if rank == 0:
         if args.stats:
             print(json.dumps({"loader_stats": stats, "fill_s": t_fill,
@@ -480,6 +531,7 @@ def run_rank(args) -> int:
             "fill_s": round(t_fill, 2),
             "steady_state": steady_out,
             **extra_out,
+            "bridge": bridge_out,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

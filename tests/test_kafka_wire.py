@@ -1085,3 +1085,30 @@ def test_subscribe_needs_a_group(broker, server):
         KafkaBridge(server.address, "t", subscribe=True)
     with pytest.raises(ValueError, match="no partitions"):
         KafkaBridge(server.address, "t", group_id="g", subscribe=True, partitions=[0])
+
+
+# ---- commit="sync": batch k's OffsetCommit answered before batch k+1 is handed out
+
+@pytest.mark.parametrize("workers,bridge_mode", [(0, "auto"), (2, "auto"), (2, False)])
+def test_sync_commit_reaches_the_coordinator_before_the_next_batch(broker, server, workers, bridge_mode):
+    broker.create_topic("t", 4)
+    broker.fill("t", 60, "fixed_f32", size=8, records_per_batch=10)
+    dl = DeviceLoader(Vec8.placeholder() if workers else Vec8("t", bootstrap_servers=server.address, group_id="s",
+                                                               auto_offset_reset="earliest", consumer_timeout_ms=500,
+                                                               assignment="static"),
+                      12, device="cpu", num_workers=workers, bridge=bridge_mode, commit="sync",
+                      worker_init_fn=Vec8.init_worker("t", bootstrap_servers=server.address, group_id="s",
+                                                      auto_offset_reset="earliest", consumer_timeout_ms=500,
+                                                      assignment="static") if workers else None)
+    prev, n = None, 0
+    for x in auto_commit(dl):
+        if prev is not None:  # every record of the previous batch is committed at the cluster
+            got = broker.committed_offsets("s", "t")
+            for o, p in prev:
+                assert got.get(p) is not None and got[p] >= o + 1, (p, o, got)
+        prev = [(int(o), int(p)) for o, p in x[:, :2].tolist()]
+        n += x.shape[0]
+    st = dl.stats_summary()
+    dl.close()
+    assert n == 240 and broker.committed_offsets("s", "t") == {p: 60 for p in range(4)}
+    assert st["sync_commits"] >= 240 // 12 - 1 and st["commit_failures"] == 0

@@ -187,6 +187,20 @@ class KafkaBridge:
         self._report_errors()
         return n
 
+    def commit_sync(self, timeout: float = 30.0) -> bool:
+        """Forwards the latest local commits now and waits for the coordinator's answer (the
+        reference's synchronous ``consumer.commit()``, kafka_dataset.py:130).  True when every
+        partition committed; False on a commit error (CommitFailedError in :meth:`last_error`) or
+        timeout."""
+        ok = bool(self._r.commit_sync(int(timeout * 1000)))
+        if not ok:
+            self._report_errors()
+        return ok
+
+    def take_forward_ns(self) -> list[int]:
+        """OffsetCommit round-trip times (ns) of the forwards made since the last call."""
+        return list(self._r.take_forward_ns())
+
     def wait_caught_up(self, timeout: float = 30.0) -> bool:
         """Blocks until every mirrored partition reached the cluster's current end offset."""
         return bool(self._r.wait_caught_up(int(timeout * 1000)))

@@ -140,6 +140,7 @@ class Tuning:
 _CHOICES = {
     "sharding": ("static", "group"),
     "commit_on": ("host", "device"),
+    "commit": ("async", "sync"),
     "commit_sink": ("auto", "broker", "worker"),
     "h2d": ("auto", "dma", "zerocopy", "direct"),
     "decode": ("auto", "device", "host"),
@@ -152,6 +153,9 @@ _CHOICE_HELP = {
     "json_parse": "'auto', 'device' (gfx950 parse kernel) or 'host' (worker parse)",
     "commit_sink": ("'auto', 'broker' (the main process stores offsets into the synthetic broker) or "
                     "'worker' (each worker's consumer commits its partitions)"),
+    "commit": ("'async' (batch k's offsets are stored when batch k+1 is requested; a KafkaBridge forwards "
+               "them to the coordinator within commit_interval_ms) or 'sync' (batch k+1 is handed out only "
+               "once the coordinator answered batch k's OffsetCommit)"),
 }
 
 
@@ -171,6 +175,7 @@ class LoaderConfig:
     native: bool = True
     multiprocessing_context: str = "fork"
     commit_on: str = "host"
+    commit: str = "async"
     commit_sink: str = "auto"
     lockstep: Any = True
     lockstep_timeout: float = 600.0

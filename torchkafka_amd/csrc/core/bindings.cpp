@@ -608,6 +608,8 @@ PYBIND11_MODULE(_tkcore, m) {
       .def("start", &Replicator::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Replicator::stop, py::arg("flush") = true, py::call_guard<py::gil_scoped_release>())
       .def("flush_commits", &Replicator::flush_commits, py::call_guard<py::gil_scoped_release>())
+      .def("commit_sync", &Replicator::commit_sync, py::arg("timeout_ms"), py::call_guard<py::gil_scoped_release>())
+      .def("take_forward_ns", &Replicator::take_forward_ns)
       .def("wait_caught_up", &Replicator::wait_caught_up, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("running", &Replicator::running)
       .def_property_readonly("errors", &Replicator::errors)

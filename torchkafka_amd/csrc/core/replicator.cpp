@@ -313,7 +313,11 @@ std::vector<std::pair<int32_t, uint64_t>> Replicator::assignment_epochs() const 
 
 void Replicator::stop(bool flush) {
   if (!running_.load() && threads_.empty()) return;
-  stop_ = true;
+  {
+    std::lock_guard<std::mutex> l(sync_mu_);
+    stop_ = true;
+  }
+  sync_cv_.notify_all();
   for (auto& t : threads_)
     if (t.joinable()) t.join();
   threads_.clear();
@@ -561,14 +565,29 @@ int Replicator::flush_commits() {
 void Replicator::commit_loop() {
   int backoff_ms = cfg_.commit_interval_ms;
   while (!stop_.load()) {
-    for (int s = 0; s < backoff_ms && !stop_.load(); s += 1) sleep_ms(1);
+    uint64_t serving;
+    {
+      // every commit_interval_ms, or at once when commit_sync() asks
+      std::unique_lock<std::mutex> l(sync_mu_);
+      sync_cv_.wait_for(l, std::chrono::milliseconds(backoff_ms),
+                        [&] { return stop_.load() || sync_req_ > sync_done_; });
+      serving = sync_req_;
+    }
     if (stop_.load()) break;
+    bool ok = false;
     try {
       if (!commit_client_) {
         commit_client_ = std::make_unique<wire::Client>(cfg_.bootstrap, cfg_.client_id + "-commit", cfg_.timeout_ms, cfg_.security);
         commit_client_->set_cancel(&stop_);
       }
-      forward(*commit_client_);
+      const int64_t errs0 = errors_.load();
+      const int64_t t0 = now_ns();
+      const int n = forward(*commit_client_);
+      if (n > 0) {
+        std::lock_guard<std::mutex> g(stats_mu_);
+        if (forward_ns_.size() < (1u << 16)) forward_ns_.push_back(now_ns() - t0);
+      }
+      ok = errors_.load() == errs0;
       heartbeat(*commit_client_);
       backoff_ms = cfg_.commit_interval_ms;
     } catch (const std::exception& e) {
@@ -577,7 +596,33 @@ void Replicator::commit_loop() {
       commit_client_.reset();
       backoff_ms = std::min(1000, std::max(10, backoff_ms * 2));
     }
+    {
+      std::lock_guard<std::mutex> l(sync_mu_);
+      if (serving > sync_done_) {
+        sync_done_ = serving;
+        sync_ok_ = ok;
+      }
+    }
+    sync_cv_.notify_all();
   }
+  sync_cv_.notify_all();
+}
+
+bool Replicator::commit_sync(int timeout_ms) {
+  if (cfg_.group.empty() || !running_.load()) return false;
+  std::unique_lock<std::mutex> l(sync_mu_);
+  const uint64_t want = ++sync_req_;
+  sync_cv_.notify_all();
+  const bool done = sync_cv_.wait_for(l, std::chrono::milliseconds(timeout_ms),
+                                      [&] { return sync_done_ >= want || stop_.load(); });
+  return done && sync_done_ >= want && sync_ok_;
+}
+
+std::vector<int64_t> Replicator::take_forward_ns() {
+  std::lock_guard<std::mutex> g(stats_mu_);
+  std::vector<int64_t> v;
+  v.swap(forward_ns_);
+  return v;
 }
 
 // Committed log bytes are never read again (the bridge's broker has one consuming group): move

@@ -97,6 +97,12 @@ class Replicator {
   void stop(bool flush = true);
   // Forwards every changed local commit to the coordinator now; returns partitions committed.
   int flush_commits();
+  // Synchronous commit (DeviceLoader commit="sync"): wakes the commit thread, which forwards every
+  // changed local commit on its coordinator connection; returns once that OffsetCommit was answered
+  // -- true when every partition committed cleanly, false on an error or after timeout_ms.
+  bool commit_sync(int timeout_ms);
+  // Durations of the OffsetCommit round trips the commit thread made since the last call.
+  std::vector<int64_t> take_forward_ns();
   bool running() const { return running_.load(); }
   std::string last_error();
   int64_t errors() const { return errors_.load(); }
@@ -158,6 +164,12 @@ class Replicator {
   std::mutex err_mu_;
   std::string last_error_;
   std::mutex commit_mu_;  // serialises forward() between the committer thread and flush_commits()
+  std::mutex sync_mu_;    // commit_sync() requests / the commit thread's answers
+  std::condition_variable sync_cv_;
+  uint64_t sync_req_ = 0, sync_done_ = 0;
+  bool sync_ok_ = true;
+  std::mutex stats_mu_;
+  std::vector<int64_t> forward_ns_;
   std::unique_ptr<wire::Client> commit_client_;
   std::vector<int32_t> join_group(wire::Client& c);  // sets member_id_ / generation_
   void heartbeat(wire::Client& c);

@@ -56,6 +56,14 @@ log = logging.getLogger(__name__)
 _ds_logger = logging.getLogger("torchkafka.kafka_dataset")
 
 
+def _traced_step(step):
+    """A native iteration step inside one roctx range (``TORCHKAFKA_ROCTX=1``)."""
+    def traced():
+        with trace_range("torchkafka.next_batch"):
+            return step()
+    return traced
+
+
 def _host_allreduce_min(group):
     """all-reduce(MIN) of three int64 over a CPU (gloo) group, for the driver's PyLockstep transport."""
     import torch.distributed as dist
@@ -270,14 +278,18 @@ class _Run:
                 keep.append(g)
         self.inflight = keep
 
+    def wait_worker_commits(self, timeout: float) -> bool:
+        """commit_sink='worker': waits until every live worker acknowledged its latest request."""
+        return self.table.wait_acks(timeout=timeout, alive=lambda w: self.procs[w].is_alive()
+                                    if w < len(self.procs) else False)
+
     def close(self) -> None:
         if self.closed:
             return
         self.closed = True
         if self.table is not None:
             # the workers' consumers commit what the user finished before they are stopped
-            self.table.wait_acks(timeout=10.0, alive=lambda w: self.procs[w].is_alive() if w < len(self.procs)
-                                 else False)
+            self.wait_worker_commits(10.0)
         try:
             self.ring.shutdown()
         except Exception:  # noqa: BLE001
@@ -338,6 +350,11 @@ class DeviceLoader:
         pad_to / pad_multiple / pad_value / return_mask: variable-length padding controls.
         commit_on: ``"host"`` (commit when the next batch is requested, as the reference) or
             ``"device"`` (additionally wait until the GPU finished the user's work on the batch).
+        commit: ``"async"`` (default: batch k's offsets are stored -- in the synthetic broker, or in a
+            KafkaBridge replica that forwards them to the group coordinator within a few ms -- when
+            batch k+1 is requested) or ``"sync"`` (the reference's semantics, kafka_dataset.py:130:
+            batch k+1 is handed out only after batch k's device verdict landed, its offsets were
+            stored and, through a bridge, the coordinator answered its OffsetCommit).
         lockstep: synchronise steps and commits across ranks when torch.distributed is initialised
             (``True``: native RCCL on GPUs with an nccl group, the group's own all-reduce otherwise;
             ``"host"``: the group's all-reduce (e.g. gloo) even on GPUs; ``"rccl"``: the native RCCL
@@ -409,6 +426,7 @@ class DeviceLoader:
         self.native = cfg.native
         self.multiprocessing_context = cfg.multiprocessing_context
         self.commit_on = cfg.commit_on
+        self.commit_mode = cfg.commit
         self.commit_sink = cfg.commit_sink
         self.lockstep = cfg.lockstep
         self.lockstep_timeout = float(cfg.lockstep_timeout)
@@ -645,7 +663,8 @@ class DeviceLoader:
                 "gather": self._direct(), "json_device": self._json_device(),
                 "span": self._device_decode(),
                 "process_overridden": self._process_overridden(), "commit_table": None,
-                "worker_spin_us": int(self.tuning.worker_spin_us), "in_process": False}
+                "worker_spin_us": int(self.tuning.worker_spin_us), "in_process": False,
+                "commit_mode": self.commit_mode}
 
     def _rank_partitions(self) -> list[int]:
         """Broker partition indices this rank's workers will read (static sharding of the topics
@@ -809,23 +828,21 @@ class DeviceLoader:
             run.close()
             raise
         if run.driver is not None:
-            if self._fast_path_ok() and not _roctx_enabled():
-                yield from self._iterate_fast(run, auto_commit)
-            elif self._varlen_fast_ok():
-                yield from self._iterate_varlen_fast(run, auto_commit)
-            else:
-                yield from self._iterate_driver(run, auto_commit)
+            yield from self._iterate_native(run, auto_commit)
             return
         finished = self._pending_wms
         prev = None
         step = 0
         completed = False
         try:
+            sync = auto_commit and self.commit_mode == "sync"
             while True:
                 item = self._next_item(run)
                 if prev is not None and auto_commit:
                     finished.append(self._finish_marker(prev))  # the user is done with the previous batch
                     prev = None
+                    if sync and lock is None:
+                        self._sync_commit_py()
                 if lock is not None:
                     t_agree = time.perf_counter_ns()
                     ok = lock.agree(item is not None, step)
@@ -834,7 +851,9 @@ class DeviceLoader:
                     st.lockstep_agreements += 1
                     st.lockstep_wait_ns += t_agree
                     st.lockstep_step_wait_max_ns = max(st.lockstep_step_wait_max_ns, t_agree)
-                    if auto_commit:
+                    if sync:
+                        self._sync_commit_py()
+                    elif auto_commit:
                         self._commit_finished()
                     if not ok:
                         break
@@ -861,6 +880,8 @@ class DeviceLoader:
                 if lock is not None:
                     lock.barrier()
                 self._commit_finished(wait=True)
+                if self.commit_mode == "sync":
+                    self._sync_commit_py()
             run.close()
 
     def _finish_marker(self, wms):
@@ -916,85 +937,54 @@ class DeviceLoader:
                               "world_size": world}
         return ls
 
-    def _iterate_driver(self, run: _Run, auto_commit: bool):
-        """GPU iteration through the native step driver (one native call per fixed-width batch)."""
+    # ------------------------------------------------------------------ native iteration
+    def _iterate_native(self, run: _Run, auto_commit: bool):
+        """GPU iteration through the native step driver: one loop for every schema.  A *stage*
+        makes one batch per call -- ``(status, commit status, item)`` -- and the loop around it
+        owns what they share: result codes, commit logging, ``commit='sync'``, the wait timeout and
+        the end of the iteration (final commit, stats, ring teardown).  Stages:
+
+        * fixed-width (``FixedWidth`` schemas): ONE argument-free native call per batch (finish +
+          commit the previous batch, take the next slot, allocate on the current stream, decode --
+          coalesced with staged batches);
+        * var-len / JSON (``VarLen`` / ``JsonArray``): the same with the pad/stack or JSON parse;
+        * slot (everything else: ``return_info``, ``drop_last``, a ``_process`` of its own): the
+          driver hands out slots and Python collates them.
+        """
         drv = run.driver
         debug = _ds_logger.isEnabledFor(logging.DEBUG)
-        completed = False
-        delivered = False
-        try:
-            if self._fast_path_ok():
-                yield from self._fast_loop(run, auto_commit, debug)
-            else:
-                while True:
-                    # asking for the next batch finishes the previous one
-                    drv.finish_delivered(_stream_ptr(self.device))
-                    if auto_commit and delivered:
-                        self._commit_native(drv, debug)
-                    item = self._next_item_driver(run)
-                    if item is None:
-                        break
-                    drv.deliver_last()
-                    delivered = True
-                    yield item[0]
-            completed = True
-        finally:
-            try:
-                drv.finish_delivered(_stream_ptr(self.device))
-                if completed:
-                    drv.finish_lockstep()
-                drv.drain_fenced(True)
-                if completed and auto_commit:
-                    self._commit_native(drv, debug)
-                elif not auto_commit:
-                    # manual mode: keep every yielded batch committable by DeviceLoader.commit()
-                    pend = drv.take_pending()
-                    if pend:
-                        self._pending_wms.append(([(p, 0, o, 0) for p, o in pend], None))
-            finally:
-                self._absorb_driver_stats(drv)
-                run.close()
-
-    def _varlen_fast_ok(self) -> bool:
-        s = self.schema
-        return (s is not None and getattr(s, "kind", None) in (1, 2) and self.native and not self.return_info
-                and not self.drop_last and not _roctx_enabled() and not self._process_overridden())
-
-    def _iterate_varlen_fast(self, run: _Run, auto_commit: bool):
-        """Var-len / JSON GPU iteration, one native call per batch (MainDriver.varlen_next): finish +
-        commit the previous batch, take the next slot, allocate the padded batch on the current
-        stream and launch its pad/stack (or JSON parse) kernel."""
-        drv = run.driver
-        debug = _ds_logger.isEnabledFor(logging.DEBUG)
-        src = CODE_DTYPE[self._default_src_code()]
-        dst_dt = self._out_dtype(src)
-        if (dst_dt in FLOAT_DTYPES) != (src in FLOAT_DTYPES) and src in FLOAT_DTYPES:
-            raise TypeError(f"cannot collate {src} records to {dst_dt}")
         log_commits = debug and auto_commit
-        args = (self.device.index, DTYPE_CODE[dst_dt], -1 if self.pad_to is None else int(self.pad_to),
-                self.pad_multiple, float(self.pad_value), bool(self.return_mask), auto_commit and not log_commits,
-                100)
-        step = drv.varlen_next
-        want_mask = self.return_mask
-        completed = False
+        native_ac = auto_commit and not log_commits  # with DEBUG the commit comes back to Python to be logged
+        if self._fast_path_ok():
+            step, py_commits = self._fixed_stage(drv, native_ac), False
+        elif self._varlen_fast_ok():
+            step, py_commits = self._varlen_stage(drv, native_ac), False
+        else:
+            step, py_commits = self._slot_stage(run, auto_commit, debug), True
+        if _roctx_enabled():
+            step = _traced_step(step)
+        sync = auto_commit and self.commit_mode == "sync"
+        completed = delivered = False
+        wait_since = None
         try:
-            wait_since = None
-            delivered = False
             while True:
-                r, cs, out, lengths, mask = step(*args)
+                r, cs, item = step()
                 if cs:
                     self._log_commit(cs, debug)
-                if r == 1:
-                    if log_commits and delivered:
-                        self._commit_logged(drv)
+                if r > 0:
+                    if delivered:
+                        if log_commits and not py_commits:
+                            self._commit_logged(drv)
+                        if sync:
+                            self._sync_commit(drv, debug)  # batch k durable before k+1 is handed out
                     delivered = True
                     wait_since = None
-                    yield (out, lengths, mask) if want_mask else (out, lengths)
+                    yield item
                 elif r == -2:
                     break
                 elif r == -3:
                     raise WorkerError(drv.error())
-                elif r == -4:
+                elif r == -4:  # an earlier device-checked batch was corrupt (manual-commit mode)
                     raise CorruptRecordException(drv.parse_error())
                 else:  # -1: nothing within the poll slice
                     run._check_workers_native()
@@ -1012,7 +1002,10 @@ class DeviceLoader:
                 drv.drain_fenced(True)
                 if completed and auto_commit:
                     self._commit_native(drv, debug)
+                    if sync:
+                        self._sync_commit(drv, debug)
                 elif not auto_commit:
+                    # manual mode: keep every yielded batch committable by DeviceLoader.commit()
                     pend = drv.take_pending()
                     if pend:
                         self._pending_wms.append(([(p, 0, o, 0) for p, o in pend], None))
@@ -1020,124 +1013,55 @@ class DeviceLoader:
                 self._absorb_driver_stats(drv)
                 run.close()
 
-    def _iterate_fast(self, run: _Run, auto_commit: bool):
-        """Fixed-width GPU iteration: each batch is ONE argument-free native call (finish + commit
-        the previous batch, take the next slot, allocate on the current stream, collate -- coalesced
-        with staged batches -- and count), so the per-batch Python work is a bound-method call."""
-        drv = run.driver
-        debug = _ds_logger.isEnabledFor(logging.DEBUG)
+    def _fixed_stage(self, drv, native_ac: bool):
         s = self.schema
         prm = self._norm_params(s.row_elems)
         shift, scale = (prm[0].data_ptr(), prm[1].data_ptr()) if prm is not None else (0, 0)
-        log_commits = debug and auto_commit
         drv.configure_fast(self.device.index, [self.batch_size, *s.shape], DTYPE_CODE[self._out_dtype(s.dtype)],
-                           s.row_elems, shift, scale, auto_commit and not log_commits, 100, self.coalesce > 1)
-        step = drv.fast_next
-        completed = False
-        delivered = False
-        try:
-            while True:
-                r, cs, out = step()
-                if r > 0:
-                    if cs:
-                        self._log_commit(cs, debug)
-                    elif log_commits and delivered:
-                        self._commit_logged(drv)
-                    delivered = True
-                    yield out
-                elif r == -2:
-                    break
-                elif r == -3:
-                    raise WorkerError(drv.error())
-                elif r == -4:  # an earlier device-checked batch was corrupt (manual-commit mode)
-                    raise CorruptRecordException(drv.parse_error())
-                else:  # -1: nothing within the poll slice
-                    if cs:
-                        self._log_commit(cs, debug)
-                    run._check_workers_native()
-                    if self.timeout > 0:
-                        t0 = getattr(run, "_wait_since", None)
-                        now = time.monotonic()
-                        if t0 is None:
-                            run._wait_since = now
-                        elif now - t0 > self.timeout:
-                            raise TimeoutError(f"DeviceLoader timed out after {self.timeout}s waiting for a batch")
-                        continue
-                if self.timeout > 0:
-                    run._wait_since = None
-            completed = True
-        finally:
-            drv.finish_delivered(_stream_ptr(self.device))
-            if completed:
-                drv.finish_lockstep()
-            drv.drain_fenced(True)
-            if completed and auto_commit:
-                self._commit_native(drv, debug)
-            elif not auto_commit:
-                pend = drv.take_pending()
-                if pend:
-                    self._pending_wms.append(([(p, 0, o, 0) for p, o in pend], None))
-            self._absorb_driver_stats(drv)
-            run.close()
+                           s.row_elems, shift, scale, native_ac, 100, self.coalesce > 1)
+        return drv.fast_next
 
-    def _fast_loop(self, run: _Run, auto_commit: bool, debug: bool):
-        if _roctx_enabled():
-            yield from self._fast_loop_traced(run, auto_commit, debug)
-            return
-        yield from self._fast_loop_plain(run, auto_commit, debug)
+    def _varlen_stage(self, drv, native_ac: bool):
+        src = CODE_DTYPE[self._default_src_code()]
+        dst_dt = self._out_dtype(src)
+        if (dst_dt in FLOAT_DTYPES) != (src in FLOAT_DTYPES) and src in FLOAT_DTYPES:
+            raise TypeError(f"cannot collate {src} records to {dst_dt}")
+        args = (self.device.index, DTYPE_CODE[dst_dt], -1 if self.pad_to is None else int(self.pad_to),
+                self.pad_multiple, float(self.pad_value), bool(self.return_mask), native_ac, 100)
+        native = drv.varlen_next
+        want_mask = self.return_mask
 
-    def _fast_loop_traced(self, run: _Run, auto_commit: bool, debug: bool):
-        """The fast loop with one roctx range per step (``TORCHKAFKA_ROCTX=1``)."""
-        gen = self._fast_loop_plain(run, auto_commit, debug)
-        while True:
-            with trace_range("torchkafka.next_batch"):
-                try:
-                    x = next(gen)
-                except StopIteration:
-                    return
-            yield x
+        def step():
+            r, cs, out, lengths, mask = native(*args)
+            return r, cs, ((out, lengths, mask) if want_mask else (out, lengths)) if r == 1 else None
+        return step
 
-    def _fast_loop_plain(self, run: _Run, auto_commit: bool, debug: bool):
+    def _slot_stage(self, run: _Run, auto_commit: bool, debug: bool):
         drv = run.driver
-        s = self.schema
-        B, shape, row = self.batch_size, tuple(s.shape), s.row_elems
-        dst_dt = self._out_dtype(s.dtype)
-        dst_code = DTYPE_CODE[dst_dt]
-        prm = self._norm_params(row)
-        shift, scale = (prm[0].data_ptr(), prm[1].data_ptr()) if prm is not None else (0, 0)
-        dev = self.device
-        stats = self.stats
-        dev_index = dev.index
-        out_shape = [B, *shape]
-        # one native call per batch: allocate (torch caching allocator, current stream),
-        # finish + commit the previous batch, take the next slot, launch the collate
-        step = hip().step_fixed_group_tensor if self.coalesce > 1 else hip().step_fixed_tensor
-        log_commits = debug and auto_commit
-        native_ac = auto_commit and not log_commits
-        delivered = False
-        while True:
-            t0 = time.perf_counter_ns()
-            r, cs, out = step(drv, dev_index, out_shape, dst_code, row, shift, scale, native_ac, 100)
-            if cs:
-                self._log_commit(cs, debug)
-            if r > 0:
-                if log_commits and delivered:
-                    self._commit_logged(drv)
-                delivered = True
-                stats.batches += 1
-                stats.records += r
-                stats.issue_ns += time.perf_counter_ns() - t0
-                yield out
-            elif r == -2:
-                return
-            elif r == -3:
-                raise WorkerError(drv.error())
-            elif r == -4:
-                raise CorruptRecordException(drv.parse_error())
-            else:
-                run._check_workers_native()
-                if self.timeout > 0 and time.perf_counter_ns() - t0 > self.timeout * 1e9:
-                    raise TimeoutError(f"DeviceLoader timed out after {self.timeout}s waiting for a batch")
+        state = {"delivered": False}
+
+        def step():
+            drv.finish_delivered(_stream_ptr(self.device))  # asking for the next batch finishes the previous one
+            if auto_commit and state["delivered"]:
+                self._commit_native(drv, debug)
+            item = self._next_item_driver(run)
+            if item is None:
+                return -2, 0, None
+            drv.deliver_last()
+            state["delivered"] = True
+            return 1, 0, item[0]
+        return step
+
+    def _sync_commit(self, drv, debug: bool) -> None:
+        """``commit='sync'``: every finished batch's verdict, local store and -- through the
+        bridges -- the coordinator's OffsetCommit answer, before the next batch is handed out."""
+        t0 = time.perf_counter_ns()
+        drv.drain_fenced(True)
+        self._commit_native(drv, debug)
+        run = self._run
+        if run is not None and run.table is not None:
+            run.wait_worker_commits(30.0)  # each worker's consumer committed (and, bridged, forwarded)
+        self._sync_bridges(t0)
 
     def _commit_logged(self, drv) -> None:
         """One native commit bracketed by the reference's DEBUG messages (kafka_dataset.py:124-143).
@@ -1381,6 +1305,32 @@ class DeviceLoader:
         from ..broker.synthetic import open_broker, resolve_url
 
         return open_broker(resolve_url(self._servers))
+
+    def _sync_bridges(self, t0: int) -> None:
+        """commit='sync': waits for the coordinator's answer through every bridge this process
+        commits into -- the loader's own (bridge='auto') or, single-process, the dataset
+        consumer's (``KafkaDataset(topic, bootstrap_servers=cluster)``)."""
+        bridges = list(self._bridges)
+        if self.num_workers == 0:
+            bridges += getattr(getattr(self.dataset, "_consumer", None), "_bridges", None) or []
+        ok = True
+        for br in bridges:
+            if not br._closed:
+                ok = br.commit_sync() and ok
+        if not ok:
+            _ds_logger.error("Commit failed.")
+            self.stats.commit_failures += 1
+        self.stats.record_sync_commit(time.perf_counter_ns() - t0)
+
+    def _sync_commit_py(self) -> None:
+        """commit='sync' on the Python path: every finished batch stored (fences waited for) and,
+        through the bridges / the workers' consumers, answered by the coordinator."""
+        t0 = time.perf_counter_ns()
+        self._commit_finished(wait=True)
+        run = self._run
+        if run is not None and run.table is not None:
+            run.wait_worker_commits(30.0)
+        self._sync_bridges(t0)
 
     def _commit_finished(self, wait: bool = False) -> None:
         """Commits the watermarks of every batch the user finished (exactly those)."""

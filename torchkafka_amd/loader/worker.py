@@ -77,7 +77,7 @@ def worker_main(ring, ring_name: str, worker_id: int, num_workers: int, dataset,
                 raise RuntimeError("static sharding needs the synthetic-broker consumer; use sharding='group' "
                                    "with a kafka-python consumer (Kafka's group assignment shards partitions)")
             consumer.assign_shard(topics, cfg["rank"], cfg["world_size"], worker_id, num_workers)
-        sink = _WorkerSink(cfg.get("commit_table"), worker_id, dataset, consumer)
+        sink = _WorkerSink(cfg.get("commit_table"), worker_id, dataset, consumer, cfg.get("commit_mode") == "sync")
         state["sink"] = sink
         if (cfg["native"] and getattr(consumer, "_fetcher", None) is not None and dataset.schema is not None
                 and not cfg.get("process_overridden", False)):
@@ -108,8 +108,9 @@ def worker_main(ring, ring_name: str, worker_id: int, num_workers: int, dataset,
             pass
     finally:
         # a native wire-route consumer: forward what it committed before this process ends (its
-        # bridge's committer thread runs every few ms; the last commit must not be lost)
-        for br in reversed(getattr(state.get("consumer"), "_bridges", None) or []):
+        # bridge's committer thread runs every few ms; the last commit must not be lost).  In
+        # single-process mode the consumer is the dataset's: it lives on with the dataset.
+        for br in [] if in_process else reversed(getattr(state.get("consumer"), "_bridges", None) or []):
             try:
                 br.close()
             except Exception:  # noqa: BLE001 - logged by the bridge
@@ -122,10 +123,11 @@ class _WorkerSink:
     when the consumer joined a group, through kafka-python when that is the consumer -- with the
     reference's worker log messages and CommitFailedError handling (kafka_dataset.py:124-143)."""
 
-    def __init__(self, table, worker_id, dataset, consumer):
+    def __init__(self, table, worker_id, dataset, consumer, sync: bool = False):
         import threading
 
         self.table, self.w, self.ds, self.consumer = table, worker_id, dataset, consumer
+        self.sync = sync
         self.seen = 0
         self.committed: dict = {}
         self.lock = threading.Lock()   # the consumer is used by one thread at a time
@@ -154,6 +156,9 @@ class _WorkerSink:
         if offsets:
             with self.lock:
                 self.ds._do_commit({self.tp_of(p): OffsetAndMetadata(o, "") for p, o in offsets.items()})
+                if self.sync:  # commit='sync': the coordinator answered before the request is acked
+                    for br in getattr(self.consumer, "_bridges", None) or []:
+                        br.commit_sync()
             # a failed commit (rebalance) is logged and not retried, as in the reference (B14)
             self.committed.update(offsets)
         self.seen = seq

@@ -32,6 +32,8 @@ class LoaderStats:
     commit_ns: list = field(default_factory=list)
     # request of batch k+1 -> batch k's offsets stored (incl. lockstep / decode verdict / fence waits)
     commit_latency_ns: list = field(default_factory=list)
+    # commit='sync': the wait for batch k's verdict + store + coordinator answer before batch k+1
+    sync_commit_ns: list = field(default_factory=list)
     worker_fill_ns: int = 0
     worker_fills: int = 0
     ready_age_ns: int = 0
@@ -73,6 +75,10 @@ class LoaderStats:
         self.commits += 1
         if len(self.commit_ns) < self.max_commit_samples:
             self.commit_ns.append(ns)
+
+    def record_sync_commit(self, ns: int) -> None:
+        if len(self.sync_commit_ns) < self.max_commit_samples:
+            self.sync_commit_ns.append(ns)
 
     def record_commit_latency(self, ns: int) -> None:
         if len(self.commit_latency_ns) < self.max_commit_samples:
@@ -125,6 +131,9 @@ class LoaderStats:
             "commit_latency_p99_us": percentile(lat_us, 99),
             "commit_latency_max_us": max(lat_us) if lat_us else float("nan"),
             "commit_latency_samples": len(lat_us),
+            "sync_commit_p50_us": percentile([x / 1e3 for x in self.sync_commit_ns], 50),
+            "sync_commit_p99_us": percentile([x / 1e3 for x in self.sync_commit_ns], 99),
+            "sync_commits": len(self.sync_commit_ns),
         }
 
 
