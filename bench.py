@@ -104,7 +104,7 @@ def parse():
                     help="timed steps of each secondary block (default: the steady-state steps)")
     ap.add_argument("--bridge-steps", type=int, default=None,
                     help="timed steps of the Kafka-protocol bridge blocks (async; sync runs a quarter): "
-                         "default 8000 on a GPU, 200 on the CPU; 0 skips them")
+                         "default 8000 on a GPU, 20 on the CPU; 0 skips them")
     return ap.parse_args()
 
 
@@ -438,7 +438,7 @@ def run_rank(args) -> int:
 
     # the Kafka-protocol route: this rank's partitions over a loopback wire server -> bridge replica
     bridge_out = None
-    bsteps = args.bridge_steps if args.bridge_steps is not None else (8000 if device.type == "cuda" else 200)
+    bsteps = args.bridge_steps if args.bridge_steps is not None else (8000 if device.type == "cuda" else 20)
     if bsteps > 0:
         from torchkafka_amd.broker import NativeWireServer
 
@@ -460,7 +460,8 @@ def run_rank(args) -> int:
                 if mode == "async":
                     blk["commit_latency_means"] = "request of batch k+1 -> batch k stored in the replica's table"
                     blk["coordinator_rtt_p50_us"] = round(rtt[len(rtt) // 2], 1) if rtt else None
-                    blk["coordinator_rtt_p99_us"] = round(rtt[min(len(rtt) - 1, len(rtt) * 99 // 100)], 1) if rtt else None
+                    p99 = rtt[min(len(rtt) - 1, len(rtt) * 99 // 100)] if rtt else None
+                    blk["coordinator_rtt_p99_us"] = round(p99, 1) if rtt else None
                     blk["coordinator_commits"] = len(rtt)
                     blk["forward_interval_ms"] = 5
                 else:

@@ -38,7 +38,7 @@ def _torchrun(nproc, script, *args, timeout=240, env=None):
 
 def test_bench_two_ranks_gloo_cpu():
     r = _torchrun(2, "bench.py", "--gpus", "2", "--steps", "30", "--warmup", "5", "--device", "cpu",
-                  "--steady-steps", "60", "--workers", "2", "--partitions-per-gpu", "4")
+                  "--steady-steps", "60", "--workers", "2", "--partitions-per-gpu", "4", "--bridge-steps", "8")
     assert r.returncode == 0, r.stdout[-3000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')]
     assert len(lines) == 1, r.stdout[-3000:]
@@ -59,7 +59,7 @@ def _bench(*args, timeout=240):
 def test_bench_self_launches_n_ranks_without_torchrun():
     """The driver's plain `python bench.py --gpus N` runs N ranks (never one rank silently)."""
     r = _bench("--gpus", "2", "--device", "cpu", "--steps", "30", "--warmup", "5", "--steady-steps", "60",
-               "--extra-blocks", "f32", "--extra-steps", "40", "--workers", "2")
+               "--extra-blocks", "f32", "--extra-steps", "40", "--workers", "2", "--bridge-steps", "8")
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')]
     assert len(lines) == 1, r.stdout[-3000:]
@@ -72,6 +72,9 @@ def test_bench_self_launches_n_ranks_without_torchrun():
     ss = out["steady_state"]
     assert len(ss["per_rank_records_per_s"]) == 2 and ss["lockstep_agreements"] >= 60
     assert out["steady_f32"]["dtype"] == "f32" and out["steady_f32"]["steps"] == 40
+    br = out["bridge"]
+    assert br["async"]["steps"] == 8 and br["sync"]["steps"] == 2 and len(br["sync"]["per_rank_records_per_s"]) == 2
+    assert br["async"]["bridge_errors"] == 0 and br["sync"]["sync_commits"] >= 1
 
 
 def test_bench_refuses_more_ranks_than_visible_gpus():
