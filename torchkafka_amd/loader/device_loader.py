@@ -1013,6 +1013,11 @@ class DeviceLoader:
                 self._absorb_driver_stats(drv)
                 run.close()
 
+    def _varlen_fast_ok(self) -> bool:
+        s = self.schema
+        return (s is not None and getattr(s, "kind", None) in (1, 2) and self.native and not self.return_info
+                and not self.drop_last and not self._process_overridden())
+
     def _fixed_stage(self, drv, native_ac: bool):
         s = self.schema
         prm = self._norm_params(s.row_elems)
