@@ -359,3 +359,75 @@ def test_commit_latency_is_measured_per_batch(broker):
     s = dl.stats_summary()
     assert n == 10 and s["commit_latency_samples"] == n
     assert 0 < s["commit_latency_p50_us"] <= s["commit_latency_p99_us"] <= s["commit_latency_max_us"]
+
+
+# ---- structured samples: (features, label), dicts, lists -- as default_collate builds them
+
+class Pair(KafkaDataset):
+    """The reference README's shape: a feature tensor and a label."""
+
+    def _process(self, record):
+        v = torch.frombuffer(bytearray(record.value), dtype=torch.float32)
+        return v[2:8].clone(), int(v[0]) % 3  # (features, python int label)
+
+
+class Nested(KafkaDataset):
+    def _process(self, record):
+        v = torch.frombuffer(bytearray(record.value), dtype=torch.float32)
+        if int(v[0]) % 5 == 4:
+            return None  # skipped, still committed (B6)
+        return {"x": v[2:6].view(2, 2).clone(), "meta": [torch.tensor([record.partition, record.offset]),
+                                                        float(v[2])],
+                "key": f"p{record.partition}o{record.offset}", "ok": True}
+
+
+def _reference_batches(ds_cls, broker, bs, group):
+    """What the reference's DataLoader + default_collate deliver for the same records."""
+    from torch.utils.data import DataLoader
+
+    ds = ds_cls("t", bootstrap_servers=broker.url, group_id=group, auto_offset_reset="earliest",
+                consumer_timeout_ms=250)
+    return list(DataLoader(ds, batch_size=bs))
+
+
+@pytest.mark.parametrize("workers", [0, 1])
+def test_structured_samples_match_default_collate(broker, workers):
+    broker.create_topic("t", 1)
+    broker.fill("t", 50, "fixed_f32", size=8)
+    for cls in (Pair, Nested):
+        ref = _reference_batches(cls, broker, 8, f"ref-{cls.__name__}")
+        if workers:
+            dl = loader(cls, broker, 8, workers=1, group=f"dl-{cls.__name__}")
+        else:
+            dl = DeviceLoader(cls("t", bootstrap_servers=broker.url, group_id=f"dl-{cls.__name__}",
+                                  auto_offset_reset="earliest", consumer_timeout_ms=250), 8, num_workers=0,
+                              device="cpu")
+        got = list(auto_commit(dl))
+        assert len(got) == len(ref)
+        for a, b in zip(got, ref):
+            fa, fb = torch.utils._pytree.tree_flatten(a), torch.utils._pytree.tree_flatten(b)
+            assert fa[1] == fb[1]  # same structure (tuple / dict / list nesting, keys)
+            for x, y in zip(fa[0], fb[0]):
+                if isinstance(y, torch.Tensor):
+                    assert x.dtype == y.dtype and torch.equal(x, y)
+                else:
+                    assert x == y
+        committed = broker.committed_offsets(f"dl-{cls.__name__}", "t")
+        assert committed == {0: 50}
+
+
+def test_structured_samples_errors(broker):
+    class Mixed(KafkaDataset):
+        def _process(self, record):
+            return (torch.zeros(2),) if record.offset % 2 else (torch.zeros(2), 1)
+
+    class Ragged2(KafkaDataset):
+        def _process(self, record):
+            return {"x": torch.zeros(1 + record.offset % 2)}
+
+    broker.create_topic("t", 1)
+    broker.fill("t", 10, "fixed_f32", size=8)
+    with pytest.raises(WorkerError, match="share their structure"):
+        list(auto_commit(loader(Mixed, broker, 4, workers=1)))
+    with pytest.raises(WorkerError, match="equal size"):
+        list(auto_commit(loader(Ragged2, broker, 4, workers=1, group="g2")))

@@ -146,3 +146,37 @@ def test_ring_replica_long_stream_device_decode(broker):
         assert src.committed("g", "t", 0) == 160_000
     finally:
         src.destroy()
+
+
+@pytest.mark.parametrize("schema_kind", ["fixed", "varlen"])
+def test_sync_commit_on_the_device_path(broker, schema_kind):
+    """commit='sync' through the native step driver: before batch k+1 is handed out, batch k's
+    device verdict landed and the coordinator answered its OffsetCommit (bridge='auto')."""
+    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, VarLen, auto_commit
+    from torchkafka_amd.broker import NativeWireServer
+
+    class Rows(KafkaDataset):
+        schema = FixedWidth(torch.float32, (64,)) if schema_kind == "fixed" else VarLen(torch.float32, max_len=64)
+
+    broker.create_topic("t", 4)
+    if schema_kind == "fixed":
+        broker.fill("t", 400, "fixed_f32", size=64, records_per_batch=20)
+    else:
+        broker.fill("t", 400, "varlen_f32", size=8, max_size=64, records_per_batch=20)
+    with NativeWireServer(broker, profile="kafka4") as srv:
+        dl = DeviceLoader(Rows.placeholder(), 32, num_workers=2, device="cuda:0", commit="sync", dtype=torch.float32,
+                          worker_init_fn=Rows.init_worker("t", bootstrap_servers=srv.address, group_id="sync",
+                                                          auto_offset_reset="earliest", consumer_timeout_ms=500))
+        assert dl._bridges, "bridge='auto' mirrors the cluster"
+        n, batches = 0, 0
+        for x in auto_commit(dl):
+            got = broker.committed_offsets("sync", "t")
+            if batches >= 1:  # what the previous batches covered is at the coordinator already
+                assert sum(v or 0 for v in got.values()) >= n, (got, n)
+            rows = x[0] if isinstance(x, tuple) else x
+            n += rows.shape[0]
+            batches += 1
+        st = dl.stats_summary()
+        dl.close()
+    assert n == 1600 and broker.committed_offsets("sync", "t") == {p: 400 for p in range(4)}
+    assert st["sync_commits"] >= batches - 1 and st["commit_failures"] == 0

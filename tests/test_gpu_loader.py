@@ -557,3 +557,40 @@ def test_tuning_knobs_do_not_change_results(broker, tuning):
         rows += [tuple(r) for r in x[:, :2].long().tolist()]
     assert len(rows) == len(set(rows)) == 1200
     assert broker.committed_offsets("g", "t") == {p: 300 for p in range(4)}
+
+
+def _labelled_cls():
+    from torchkafka_amd import KafkaDataset
+
+    class Labelled(KafkaDataset):
+        def _process(self, record):
+            t = torch.frombuffer(bytearray(record.value), dtype=torch.float32)
+            return {"x": t[2:], "y": int(t[0]) % 7, "pos": (record.partition, record.offset), "k": str(record.offset)}
+    return Labelled
+
+
+@pytest.mark.parametrize("h2d", ["zerocopy", "dma"])
+def test_structured_samples_on_device(broker, h2d):
+    """`_process` returning a dict of tensors / ints / tuples / strings: one copy of the slot to the
+    device, every tensor leaf a view of it, values as default_collate stacks them (bit-exact)."""
+    from torchkafka_amd import DeviceLoader, auto_commit
+
+    DS = _labelled_cls()
+    broker.create_topic("t", 2)
+    broker.fill("t", 64, "fixed_f32", size=16)
+    dl = DeviceLoader(DS.placeholder(), 16, num_workers=2, device="cuda:0", h2d=h2d,
+                      worker_init_fn=DS.init_worker("t", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    n = 0
+    for b in auto_commit(dl):
+        assert set(b) == {"x", "y", "pos", "k"} and b["x"].is_cuda and b["x"].shape == (16, 14)
+        assert b["y"].dtype == torch.int64 and b["y"].is_cuda
+        p, o = b["pos"]  # a tuple comes back as a list, as default_collate does
+        assert p.is_cuda and o.dtype == torch.int64
+        assert b["k"] == [str(int(v)) for v in o.cpu()]
+        for i in range(16):
+            exp = torch.tensor([synth_f32(int(p[i]), int(o[i]), j) for j in range(2, 16)])
+            assert torch.equal(b["x"][i].cpu(), exp)
+            assert int(b["y"][i]) == int(o[i]) % 7
+        n += 16
+    assert n == 128 and broker.committed_offsets("g", "t") == {0: 64, 1: 64}

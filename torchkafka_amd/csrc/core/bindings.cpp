@@ -1010,6 +1010,7 @@ PYBIND11_MODULE(_tkcore, m) {
   m.attr("SPAN_MAX_SEG_ROWS") = kSpanMaxSegRows;
   m.attr("PACK_JSON_SPAN") = int(kPackJsonSpan);
   m.attr("PACK_VAR_SPAN") = int(kPackVarSpan);
+  m.attr("PACK_TREE") = int(kPackTree);
   m.attr("VAR_SPAN_ROW_MAX") = kVarSpanRowMax;
   m.attr("JSON_SPAN_MAX_SEG_ROWS") = kJsonSpanMaxSegRows;
   m.attr("JSON_SPAN_ROW_MAX") = kJsonSpanRowMax;

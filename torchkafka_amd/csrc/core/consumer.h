@@ -102,6 +102,8 @@ enum PackKind : int {
   kPackRecordSpan = 5,  // fixed-width rows decoded on the device from the pinned logs (span.h)
   kPackJsonSpan = 6,    // JsonArray rows parsed on the device straight from the pinned logs (span.h)
   kPackVarSpan = 7,     // VarLen rows padded/cast on the device straight from the pinned logs (span.h)
+  kPackTree = 8,        // structured `_process` samples (tuple / list / dict of tensors): a descriptor
+                        // plus one stacked region per leaf; copied to the device as one block
 };
 
 // kPackJsonText: JsonArray rows for the device parser (json_parse.hip).  The payload starts

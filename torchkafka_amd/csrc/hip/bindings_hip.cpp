@@ -227,6 +227,9 @@ PYBIND11_MODULE(_tkhip, m) {
              d.collate_varlen(d.last, stream_of(stream), dst_dt, ptr<void>(out), L, pad, ptr<int64_t>(lengths),
                               ptr<uint8_t>(mask));
            })
+      .def("copy_payload_last",
+           [](MainDriver& d, uintptr_t stream, uintptr_t dst) { d.copy_payload(d.last, stream_of(stream), ptr<void>(dst)); })
+      .def_property_readonly("last_slot", [](MainDriver& d) { return int64_t(d.last.g); })
       .def("last_watermarks",
            [](MainDriver& d) {
              py::list l;

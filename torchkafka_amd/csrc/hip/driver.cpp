@@ -546,6 +546,17 @@ void MainDriver::collate_varlen(const SlotView& v, hipStream_t stream, int dst_d
                        record);
 }
 
+void MainDriver::copy_payload(const SlotView& v, hipStream_t stream, void* dst) {
+  bool record;
+  note_handed(v.g, stream, &record);
+  if (!record) {  // copy_raw always records the slot's completion event
+    handed_.back().ev = true;
+    unevented_ = 0;
+    ++events_;
+  }
+  eng_->copy_raw(int(v.g), stream, 0, dst, size_t(v.payload_bytes));
+}
+
 void MainDriver::deliver(const SlotView& v) { set_delivered(v); }
 
 void MainDriver::set_delivered(const SlotView& v) {

@@ -65,6 +65,9 @@ class MainDriver {
 
   void collate_fixed(const SlotView& v, hipStream_t stream, int dst_dt, void* dst, int64_t row, const float* shift,
                      const float* scale);
+  // The slot's whole payload copied to `dst` (device memory) on `stream` (kPackTree slots: the
+  // fields are views of that block); the slot is released once the copy completed.
+  void copy_payload(const SlotView& v, hipStream_t stream, void* dst);
   void collate_varlen(const SlotView& v, hipStream_t stream, int dst_dt, void* out, int64_t L, double pad,
                       int64_t* lengths, uint8_t* mask);
 

@@ -1197,6 +1197,13 @@ class DeviceLoader:
                 continue
             break
         t1 = time.perf_counter_ns()
+        if kind == core().PACK_TREE:  # structured samples: one copy of the slot, leaves are views
+            out = self._collate_tree(run, drv.last_slot, payload_bytes,
+                                     lambda block: drv.copy_payload_last(_stream_ptr(self.device), block.data_ptr()))
+            self.stats.record_batch(n_rows, payload_bytes, t1 - t0, time.perf_counter_ns() - t1)
+            if self.return_info:
+                return KafkaBatch(out, None, None, wms, sum(w[3] for w in wms)), wms
+            return out, wms
         src_dt = CODE_DTYPE[src_code]
         dst_dt = self._out_dtype(src_dt)
         if (dst_dt in FLOAT_DTYPES) != (src_dt in FLOAT_DTYPES) and src_dt in FLOAT_DTYPES:
@@ -1232,8 +1239,30 @@ class DeviceLoader:
         return ((out, lengths, mask) if self.return_mask else (out, lengths)), wms
 
     # ------------------------------------------------------------------ collate
+    def _collate_tree(self, run: _Run, g: int, payload_bytes: int, copy):
+        """A PACK_TREE slot (loader/tree.py) -> the sample structure, leaves on the device."""
+        from . import tree
+
+        desc, data = tree.descriptor(run.ring.payload_view(g))
+        fdt = self.dtype if self.dtype is not None and self.dtype.is_floating_point else None
+        if self.device.type == "cuda":
+            block = torch.empty(payload_bytes, dtype=torch.uint8, device=self.device)
+            copy(block)
+        else:
+            block = torch.frombuffer(run.ring.payload_view(g), dtype=torch.uint8, count=payload_bytes).clone()
+        return tree.unpack(desc, data, block, fdt)
+
     def _collate(self, run: _Run, g: int, summ, wms):
         n_rows, _flags, payload_bytes, voff, max_len, total, _w, kind, src_code = summ
+        if kind == core().PACK_TREE:
+            def copy(block):
+                run.engine.copy_raw(g, _stream_ptr(self.device), 0, block.data_ptr(), payload_bytes)
+            out = self._collate_tree(run, g, payload_bytes, copy)
+            if run.engine is None:
+                run.ring.main_release(g)
+            if self.return_info:
+                return KafkaBatch(out, None, None, wms, sum(w[3] for w in wms))
+            return out
         fixed = kind == core().PACK_FIXED
         if src_code >= 0:
             src_dt = CODE_DTYPE[src_code]

@@ -305,10 +305,16 @@ def _generic_loop(ring, worker_id, spw, consumer, dataset, cfg, state) -> None:
         g = _acquire(ring, worker_id, state)
         view = ring.payload_view(g)
         wms = [(p, v[0], v[1], v[2]) for p, v in wm.items()]
-        if samples:
+        if samples and not isinstance(samples[0], torch.Tensor):
+            # (features, label), {"x": ..., "y": ...}: one stacked region per leaf (loader/tree.py)
+            from . import tree
+
+            nbytes = tree.pack(samples, view, cap)
+            ring.set_slot(g, len(samples), core().SLOT_EOS if eos else 0, core().PACK_TREE, nbytes, 0, 0, 0,
+                          len(samples), wms)
+            ring.set_slot_sample(g, -1, [])
+        elif samples:
             s0 = samples[0]
-            if not isinstance(s0, torch.Tensor):
-                raise TypeError(f"DeviceLoader samples must be tensors, got {type(s0).__name__}")
             dt = s0.dtype
             code = _DT_CODE.get(dt)
             if code is None:
