@@ -16,8 +16,9 @@ synthetic broker, decoded on the GPU (CRC32C + values cast to bf16 by the
 gfx950 kernels), handed to the user, and its offsets committed (the commit of
 batch k happens when batch k+1 is requested, as in the reference's
 auto_commit, /root/reference/src/auto_commit.py:55-58).  Records are synthetic
-Kafka RecordBatch v2 records produced into the shared-memory broker before
-timing (a retained backlog).  Weak scaling: per-rank work is fixed as N grows.
+Kafka RecordBatch v2 records (an 8-byte key, the offset % 1000, and 1 KiB of
+float32 values each) produced into the shared-memory broker before timing (a
+retained backlog).  Weak scaling: per-rank work is fixed as N grows.
 
 Launch: ``python bench.py --gpus N --steps K --warmup W``.  Under torchrun
 (``WORLD_SIZE`` set) this process is one rank.  Without it and N > 1, this
@@ -37,6 +38,9 @@ sides, max over ranks, whole-job records):
     by hipMemcpyAsync on a side stream (SDMA) and decoded there -- the config-2
     mechanism;
   * ``steady_f32``: a third loader delivering float32 (the reference's dtype);
+  * ``steady_label``: values plus the record key as an int64 label column per batch
+    (``FixedWidth(...) + Key()``: the worker reads each key while it walks the headers, the decode
+    kernel copies the labels beside the values) -- ``(features, label)`` batches;
   * ``bridge``: the same records served over the Kafka protocol (a native C++ wire server on the
     loopback interface, Kafka 4.x version profile) to a DeviceLoader whose KafkaBridge mirrors this
     rank's partitions into a local ring replica and forwards every commit to the group
@@ -97,9 +101,10 @@ def parse():
     ap.add_argument("--steady-steps", type=int, default=None,
                     help="steps of the steady-state block timed after the headline (default: max(50 x ring "
                          "slots, 50000) on a GPU, 2000 on the CPU; 0 skips it)")
-    ap.add_argument("--extra-blocks", default="dma,f32",
+    ap.add_argument("--extra-blocks", default="dma,f32,label",
                     help="comma list of secondary steady blocks, each a fresh loader: dma (h2d='dma', HBM "
-                         "mirror filled by SDMA), f32 (float32 output); '' for none")
+                         "mirror filled by SDMA), f32 (float32 output), label (the record key as an int64 "
+                         "label beside the values: FixedWidth + Key()); '' for none")
     ap.add_argument("--extra-steps", type=int, default=None,
                     help="timed steps of each secondary block (default: the steady-state steps)")
     ap.add_argument("--bridge-steps", type=int, default=None,
@@ -266,7 +271,7 @@ def time_steps(R: Rank, it, steps: int, loader) -> dict:
     x = None
     for _ in range(steps):
         x = next(it)
-        rows += x.shape[0]
+        rows += (x[0] if isinstance(x, (tuple, list)) else x).shape[0]
     R.sync()
     el = time.perf_counter() - t0
     per_rank = R.gather([el, float(rows)])
@@ -308,7 +313,7 @@ def run_rank(args) -> int:
     R = Rank(args)
     torch, dist = R.torch, R.dist
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
+    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, Key, auto_commit
     from torchkafka_amd.broker import SyntheticBroker
     from torchkafka_amd.parallel import shard_partitions
     from torchkafka_amd.utils.topology import bind_to_gpu_numa
@@ -331,6 +336,9 @@ def run_rank(args) -> int:
 
     class Records(KafkaDataset):
         schema = FixedWidth(torch.float32, (args.dim,))
+
+    class Labelled(KafkaDataset):
+        schema = FixedWidth(torch.float32, (args.dim,)) + Key()
 
     # --- broker: one per job (every rank of the job shares its launcher's pid and port)
     tag = f"{os.getppid()}-{os.environ.get('MASTER_PORT', '0')}" if world > 1 else f"{os.getpid()}"
@@ -357,22 +365,22 @@ def run_rank(args) -> int:
     per_part = int(math.ceil(batches * B * 1.25 / max(1, len(mine)))) + B
     t_fill = time.perf_counter()
     broker.fill("bench", per_part, "fixed_f32", size=args.dim, partitions=mine,
-                records_per_batch=args.records_per_batch, threads=min(16, len(mine)))
+                records_per_batch=args.records_per_batch, threads=min(16, len(mine)), keyed=True)
     t_fill = time.perf_counter() - t_fill
 
     R.init_group()
 
-    def make_loader(group: str, dtype, h2d: str, servers: str = url, commit: str = "async"):
+    def make_loader(group: str, dtype, h2d: str, servers: str = url, commit: str = "async", ds=Records):
         return DeviceLoader(
-            Records.placeholder(), B, num_workers=args.workers, device=device, dtype=dtype,
+            ds.placeholder(), B, num_workers=args.workers, device=device, dtype=dtype,
             slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
             in_order=args.in_order, h2d=h2d, copy_streams=args.copy_streams, lockstep_depth=args.lockstep_depth,
             event_every=args.event_every, numa_bind=not args.no_numa, coalesce=args.coalesce,
             coalesce_wait_us=args.coalesce_wait_us, decode=args.decode, lockstep=lockstep,
             mirror_chunk_mib=args.mirror_chunk_mib, commit=commit,
             **({"mirror_chunks": args.mirror_chunks} if args.mirror_chunks else {}),
-            worker_init_fn=Records.init_worker("bench", bootstrap_servers=servers, group_id=group,
-                                               auto_offset_reset="earliest", check_crcs=not args.no_crc),
+            worker_init_fn=ds.init_worker("bench", bootstrap_servers=servers, group_id=group,
+                                          auto_offset_reset="earliest", check_crcs=not args.no_crc),
         )
 
     def describe(loader) -> tuple[str, str]:
@@ -422,11 +430,16 @@ def run_rank(args) -> int:
     extra_out = {}
     for name in extra:
         dt = torch.float32 if name == "f32" else dtypes[args.dtype]
-        ld = make_loader(f"bench-{name}", dt, "dma" if name == "dma" else args.h2d)
+        ld = make_loader(f"bench-{name}", dt, "dma" if name == "dma" else args.h2d,
+                         ds=Labelled if name == "label" else Records)
         eit = iter(auto_commit(ld))
         for _ in range(extra_warm):
             next(eit)
         eres = time_steps(R, eit, extra_steps, ld)
+        if name == "label":  # (features, label): the label is the key the broker wrote, offset % 1000
+            xv, lab = eres["last"]
+            if lab.dtype != torch.int64 or lab.shape != (xv.shape[0],) or not bool(((lab >= 0) & (lab < 1000)).all()):
+                raise RuntimeError(f"label column mismatch: {lab.dtype} {tuple(lab.shape)}")
         blk = steady_block(R, eres, extra_steps, args.dim)
         blk["dtype"] = "f32" if name == "f32" else args.dtype
         blk["h2d"], blk["decode"] = describe(ld)

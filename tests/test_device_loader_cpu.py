@@ -431,3 +431,63 @@ def test_structured_samples_errors(broker):
         list(auto_commit(loader(Mixed, broker, 4, workers=1)))
     with pytest.raises(WorkerError, match="equal size"):
         list(auto_commit(loader(Ragged2, broker, 4, workers=1, group="g2")))
+
+
+# ---- record fields beside the value: FixedWidth(...) + Key() + Timestamp()
+
+def _produce_keyed(broker, n=60, parts=2, key_kind="be"):
+    import struct
+
+    from torchkafka_amd import KafkaProducer
+
+    prod = KafkaProducer(bootstrap_servers=broker.url, linger_ms=0, batch_size=4096)
+    for i in range(n):
+        p = i % parts
+        v = torch.arange(8, dtype=torch.float32) + i
+        key = (struct.pack(">q", 1000 + i) if key_kind == "be" else str(1000 + i).encode()) if i % 7 else None
+        prod.send("t", value=v.numpy().tobytes(), key=key, partition=p, timestamp_ms=1_700_000_000_000 + i)
+    prod.flush()
+
+
+@pytest.mark.parametrize("workers", [0, 2])
+def test_key_and_timestamp_fields_ride_with_the_values(broker, workers):
+    from torchkafka_amd import Key, Timestamp
+
+    class Labelled(KafkaDataset):
+        schema = FixedWidth(torch.float32, (8,)) + Timestamp() + Key("be", default=-7)
+
+    broker.create_topic("t", 2)
+    _produce_keyed(broker)
+    kw = dict(bootstrap_servers=broker.url, group_id="g", auto_offset_reset="earliest", consumer_timeout_ms=250)
+    if workers:
+        dl = DeviceLoader(Labelled.placeholder(), 8, num_workers=workers, device="cpu",
+                          worker_init_fn=Labelled.init_worker("t", **kw))
+    else:
+        dl = DeviceLoader(Labelled("t", **kw), 8, num_workers=0, device="cpu")
+    seen = 0
+    for x, ts, key in auto_commit(dl):
+        assert ts.dtype == key.dtype == torch.int64 and ts.shape == key.shape == (x.shape[0],)
+        for row, t, k in zip(x, ts.tolist(), key.tolist()):
+            i = int(row[0])
+            assert t == 1_700_000_000_000 + i
+            assert k == (1000 + i if i % 7 else -7)
+        seen += x.shape[0]
+    assert seen == 60 and broker.committed_offsets("g", "t") == {0: 30, 1: 30}
+    # the per-record path (torch DataLoader compat) gives the same fields
+    rec = Labelled.schema.process(type("R", (), {"value": torch.zeros(8).numpy().tobytes(), "key": b"\0" * 8,
+                                                   "timestamp": 5, "offset": 0})())
+    assert rec[1].item() == 5 and rec[2].item() == 0
+
+
+def test_ascii_keys_and_schema_validation():
+    from torchkafka_amd import Key, Timestamp, VarLen
+    from torchkafka_amd.ops.native import core
+
+    assert core().key_int64(b"-42", 2, -1) == -42 and core().key_int64(b"4x", 2, -1) == -1
+    assert core().key_int64(None, 0, 9) == 9 and core().key_int64(b"\0" * 7 + b"\x05", 0, -1) == 5
+    with pytest.raises(ValueError):
+        Key("utf16")
+    with pytest.raises(ValueError):
+        _ = FixedWidth() + Key() + Key()
+    with pytest.raises(TypeError):
+        _ = VarLen() + Timestamp()

@@ -594,3 +594,30 @@ def test_structured_samples_on_device(broker, h2d):
             assert int(b["y"][i]) == int(o[i]) % 7
         n += 16
     assert n == 128 and broker.committed_offsets("g", "t") == {0: 64, 1: 64}
+
+
+@pytest.mark.parametrize("decode,h2d,workers", [("device", "zerocopy", 2), ("device", "dma", 2),
+                                                ("host", "zerocopy", 2), ("device", "zerocopy", 0)])
+def test_key_and_timestamp_fields_on_device(broker, decode, h2d, workers):
+    """FixedWidth + Timestamp() + Key(): the worker reads each record's key / timestamp while it walks
+    the headers, the span kernel (or the host collate) lands them as int64 columns beside the values."""
+    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, Key, Timestamp, auto_commit
+
+    class Labelled(KafkaDataset):
+        schema = FixedWidth(torch.float32, (16,)) + Timestamp() + Key()
+
+    broker.create_topic("t", 2)
+    broker.fill("t", 96, "fixed_f32", size=16, keyed=True)  # key = offset % 1000, ts = 1.7e12 + offset
+    kw = dict(bootstrap_servers=broker.url, group_id="g", auto_offset_reset="earliest", consumer_timeout_ms=300)
+    if workers:
+        dl = DeviceLoader(Labelled.placeholder(), 24, num_workers=workers, device="cuda:0", decode=decode, h2d=h2d,
+                          dtype=torch.float32, worker_init_fn=Labelled.init_worker("t", **kw))
+    else:
+        dl = DeviceLoader(Labelled("t", **kw), 24, num_workers=0, device="cuda:0", decode=decode, dtype=torch.float32)
+    n = 0
+    for x, ts, key in auto_commit(dl):
+        assert x.is_cuda and ts.is_cuda and key.is_cuda and ts.dtype == key.dtype == torch.int64
+        o = x[:, 0].to(torch.int64)
+        assert torch.equal(key, o % 1000) and torch.equal(ts, o + 1_700_000_000_000)
+        n += x.shape[0]
+    assert n == 192 and broker.committed_offsets("g", "t") == {0: 96, 1: 96}

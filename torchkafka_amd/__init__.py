@@ -9,13 +9,13 @@ import numpy.random  # noqa: F401  -- import eagerly: a lazy import racing a Dat
 
 from .config import LoaderConfig, Tuning
 from .loader import DeviceLoader, KafkaBatch, auto_commit
-from .models import FixedWidth, JsonArray, KafkaDataset, VarLen
+from .models import FixedWidth, JsonArray, KafkaDataset, Key, Timestamp, VarLen, WithFields
 
 __version__ = "1.2.0+mi355x.4"
 
 __all__ = ["KafkaDataset", "auto_commit", "DeviceLoader", "KafkaBatch", "LoaderConfig", "Tuning", "FixedWidth",
-           "VarLen", "JsonArray", "SyntheticBroker", "KafkaBridge", "KafkaWireServer", "KafkaConsumer",
-           "KafkaProducer", "TopicPartition"]
+           "VarLen", "JsonArray", "Key", "Timestamp", "WithFields", "SyntheticBroker", "KafkaBridge", "KafkaWireServer",
+           "KafkaConsumer", "KafkaProducer", "TopicPartition"]
 
 
 def __getattr__(name):

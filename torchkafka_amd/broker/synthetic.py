@@ -194,11 +194,12 @@ class SyntheticBroker:
 
     def fill(self, topic: str, n_per_partition: int, kind: str = "fixed_f32", *, size: int = 256,
              max_size: int | None = None, partitions: Iterable[int] | None = None, records_per_batch: int = 64,
-             seed: int = 0, threads: int | None = None) -> None:
+             seed: int = 0, threads: int | None = None, keyed: bool = False) -> None:
         """Appends ``n_per_partition`` deterministic synthetic records to each partition.
 
         kinds: ``fixed_f32`` (``size`` floats: v[0]=offset, v[1]=partition), ``json_f32`` (JSON arrays of
         ``size..max_size`` numbers), ``bytes`` (``size..max_size`` bytes), ``tokens_i32``, ``varlen_f32``.
+        ``keyed``: every record carries an 8-byte big-endian key, ``offset % 1000`` (a label).
         """
         k = _KINDS[kind]
         _, n, first = self.topic(topic)
@@ -207,7 +208,7 @@ class SyntheticBroker:
         threads = threads or min(len(pidxs), max(1, min(16, (os.cpu_count() or 4))))
         self._b.fill_synthetic(pidxs, int(n_per_partition), k, int(size),
                                int(max_size if max_size is not None else size), int(records_per_batch), int(seed),
-                               int(threads))
+                               int(threads), bool(keyed))
 
     def delete_records(self, topic: str, partition: int, before_offset: int) -> None:
         self._b.delete_records(self.pidx(topic, partition), int(before_offset))

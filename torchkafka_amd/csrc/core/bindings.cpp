@@ -384,12 +384,12 @@ PYBIND11_MODULE(_tkcore, m) {
       .def(
           "fill_synthetic",
           [](Broker& b, std::vector<uint32_t> pidxs, int64_t n, int kind, int64_t a, int64_t bb, uint32_t rpb,
-             uint64_t seed, int threads) {
+             uint64_t seed, int threads, bool keyed) {
             py::gil_scoped_release nogil;
-            b.fill_synthetic(pidxs, n, kind, a, bb, rpb, seed, threads);
+            b.fill_synthetic(pidxs, n, kind, a, bb, rpb, seed, threads, keyed);
           },
           py::arg("pidxs"), py::arg("n_records"), py::arg("kind"), py::arg("size_a"), py::arg("size_b") = 0,
-          py::arg("records_per_batch") = 64, py::arg("seed") = 0, py::arg("threads") = 1)
+          py::arg("records_per_batch") = 64, py::arg("seed") = 0, py::arg("threads") = 1, py::arg("keyed") = false)
       .def("delete_records", &Broker::delete_records)
       .def("read_batches",
            [](Broker& b, uint32_t p, int64_t offset, uint64_t max_bytes) {
@@ -784,11 +784,14 @@ PYBIND11_MODULE(_tkcore, m) {
           "fill_slot",
           [](PyFetcher& f, py::object ring_obj, uint32_t gslot, int kind, int elem_size, int64_t row_elems,
              int64_t min_len, int64_t max_len, bool truncate, bool skip_bad, int64_t batch_rows, int64_t timeout_ms,
-             bool gather, bool span) {
+             bool gather, bool span, int extras, int key_enc, int64_t key_default) {
             PyRing& ring = ring_obj.cast<PyRing&>();
             PackSpec s;
             s.gather = gather;
             s.span = span;
+            s.extras = extras;
+            s.key_enc = key_enc;
+            s.key_default = key_default;
             s.kind = kind;
             s.elem_size = elem_size;
             s.row_elems = row_elems;
@@ -806,7 +809,16 @@ PYBIND11_MODULE(_tkcore, m) {
           },
           py::arg("ring"), py::arg("gslot"), py::arg("kind"), py::arg("elem_size"), py::arg("row_elems"),
           py::arg("min_len"), py::arg("max_len"), py::arg("truncate"), py::arg("skip_bad"), py::arg("batch_rows"),
-          py::arg("timeout_ms"), py::arg("gather") = false, py::arg("span") = false);
+          py::arg("timeout_ms"), py::arg("gather") = false, py::arg("span") = false, py::arg("extras") = 0,
+          py::arg("key_enc") = 0, py::arg("key_default") = -1);
+  m.def("key_int64", [](py::object key, int enc, int64_t dflt) {
+    if (key.is_none()) return key_int64(nullptr, -1, enc, dflt);
+    std::string k = key.cast<py::bytes>();
+    return key_int64(reinterpret_cast<const uint8_t*>(k.data()), int32_t(k.size()), enc, dflt);
+  }, py::arg("key"), py::arg("encoding"), py::arg("default"),
+     "the integer a record key carries (the native packer's rule, for the per-record path)");
+  m.attr("EXTRA_KEY") = int(kExtraKey);
+  m.attr("EXTRA_TIMESTAMP") = int(kExtraTimestamp);
 
   // ---- ring
   py::class_<PyRing>(m, "Ring")
@@ -893,6 +905,8 @@ PYBIND11_MODULE(_tkcore, m) {
              h->err_len = 0;
              h->kind = kind;
              h->payload_bytes = payload_bytes;
+             h->extras_offset = 0;
+             h->extras_n = 0;
              h->values_offset = values_offset;
              h->values_bytes = payload_bytes - values_offset;
              h->max_row_len = max_row_len;
@@ -902,6 +916,11 @@ PYBIND11_MODULE(_tkcore, m) {
              for (size_t i = 0; i < wms.size(); ++i)
                h->wm[i] = Watermark{std::get<0>(wms[i]), std::get<3>(wms[i]), std::get<1>(wms[i]), std::get<2>(wms[i])};
            })
+      .def("slot_extras",
+           [](PyRing& r, uint32_t g) {
+             SlotHeader* h = r.r->slot(g);
+             return py::make_tuple(h->extras_offset, h->extras_n);
+           }, "(payload offset, int64 columns) of the record fields beside the values")
       .def("set_slot_sample",
            [](PyRing& r, uint32_t g, int32_t dtype, std::vector<int64_t> shape) {
              SlotHeader* h = r.r->slot(g);

@@ -4,6 +4,8 @@
 #include "crc32c.h"
 
 #include <fcntl.h>
+
+#include <array>
 #include <linux/falloc.h>
 #include <signal.h>
 #include <sys/file.h>
@@ -690,7 +692,7 @@ size_t gen_value(std::vector<uint8_t>& buf, int kind, uint32_t p, int64_t o, int
 }  // namespace
 
 void Broker::fill_synthetic(const std::vector<uint32_t>& pidxs, int64_t n_records, int kind, int64_t size_a,
-                            int64_t size_b, uint32_t records_per_batch, uint64_t seed, int n_threads) {
+                            int64_t size_b, uint32_t records_per_batch, uint64_t seed, int n_threads, bool keyed) {
   if (records_per_batch == 0) records_per_batch = 1;
   for (uint32_t pidx : pidxs) { part(pidx); mapped(pidx); }
   std::atomic<size_t> next{0};
@@ -698,6 +700,7 @@ void Broker::fill_synthetic(const std::vector<uint32_t>& pidxs, int64_t n_record
   std::mutex err_mu;
   auto work = [&]() {
     std::vector<std::vector<uint8_t>> vals(records_per_batch);
+    std::vector<std::array<uint8_t, 8>> keys(records_per_batch);
     std::vector<RecordIn> recs(records_per_batch);
     try {
       for (;;) {
@@ -713,6 +716,12 @@ void Broker::fill_synthetic(const std::vector<uint32_t>& pidxs, int64_t n_record
             const int64_t o = base + int64_t(i);
             size_t len = gen_value(vals[i], kind, p, o, size_a, size_b, seed);
             recs[i] = RecordIn{1700000000000LL + o, nullptr, -1, vals[i].data(), int32_t(len), nullptr, 0};
+            if (keyed) {  // a class label: offset % 1000 as 8 bytes big-endian (Kafka's LongSerializer)
+              const uint64_t key = __builtin_bswap64(uint64_t(o % 1000));
+              std::memcpy(keys[i].data(), &key, 8);
+              recs[i].key = keys[i].data();
+              recs[i].key_len = 8;
+            }
           }
           append(pidx, recs.data(), n);
           done += int64_t(n);

@@ -192,8 +192,9 @@ class Broker {
   // ---- produce: appends one batch, returns its base offset.
   int64_t append(uint32_t pidx, const RecordIn* recs, size_t n);
   // Synthetic generator (see SyntheticSpec in broker.cpp): fills n records per partition.
+  // keyed: every record carries an 8-byte big-endian key, its offset % 1000 (a label).
   void fill_synthetic(const std::vector<uint32_t>& pidxs, int64_t n_records, int kind, int64_t size_a,
-                      int64_t size_b, uint32_t records_per_batch, uint64_t seed, int n_threads);
+                      int64_t size_b, uint32_t records_per_batch, uint64_t seed, int n_threads, bool keyed = false);
   void delete_records(uint32_t pidx, int64_t before_offset);
 
   // ---- replica ingest (replicator.h: a Kafka cluster mirrored into this broker's logs)

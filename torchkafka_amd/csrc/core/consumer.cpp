@@ -663,6 +663,27 @@ uint32_t build_json_segments(const SpanRB* rbs, size_t n_rbs, const JsonSpanRow*
 
 }  // namespace
 
+int64_t key_int64(const uint8_t* key, int32_t len, int enc, int64_t dflt) {
+  if (!key || len < 0) return dflt;
+  if (enc == kKeyAscii) {
+    int32_t i = 0;
+    bool neg = false;
+    if (i < len && (key[i] == '-' || key[i] == '+')) neg = key[i++] == '-';
+    if (i == len || len - i > 19) return dflt;
+    int64_t v = 0;
+    for (; i < len; ++i) {
+      if (key[i] < '0' || key[i] > '9') return dflt;
+      v = v * 10 + (key[i] - '0');
+    }
+    return neg ? -v : v;
+  }
+  if (len != 8) return dflt;
+  uint64_t v;
+  std::memcpy(&v, key, 8);
+  if (enc == kKeyBigEndian) v = __builtin_bswap64(v);
+  return int64_t(v);
+}
+
 // ------------------------------------------------------------ fill
 FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, int64_t B, int64_t timeout_ms,
                       size_t* rr) {
@@ -689,6 +710,8 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   h->n_scanned = 0;
   h->src_dtype = -1;
   h->ndim = 0;
+  h->extras_offset = 0;
+  h->extras_n = 0;
   h->t_fill_start_ns = now_ns();
   if (B <= 0) throw std::invalid_argument("batch size must be positive");
 
@@ -988,6 +1011,36 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
     return rows == B ? kTakeStop : kTake;
   };
 
+  // record fields beside the value: captured for every row the visit takes, stored after the layout
+  const int n_extras = ((spec.extras & kExtraKey) ? 1 : 0) + ((spec.extras & kExtraTimestamp) ? 1 : 0);
+  thread_local std::vector<int64_t> xkey, xts;
+  xkey.clear();
+  xts.clear();
+  auto visit_x = [&](const RecordView& r) -> int {
+    const int64_t before = rows;
+    const int res = visit(r);
+    if (rows > before) {
+      if (spec.extras & kExtraKey) xkey.push_back(key_int64(r.key, r.key_len, spec.key_enc, spec.key_default));
+      if (spec.extras & kExtraTimestamp) xts.push_back(r.timestamp);
+    }
+    return res;
+  };
+  auto put_extras = [&]() {
+    if (!n_extras) return;
+    const uint64_t off = align_up(h->payload_bytes, 256);
+    const uint64_t need = uint64_t(rows) * 8u * uint64_t(n_extras);
+    if (off + need > cap) throw std::invalid_argument("ring slot too small for the batch's record fields");
+    int64_t* dst = reinterpret_cast<int64_t*>(pay + off);
+    if (spec.extras & kExtraKey) {
+      std::memcpy(dst, xkey.data(), size_t(rows) * 8);
+      dst += rows;
+    }
+    if (spec.extras & kExtraTimestamp) std::memcpy(dst, xts.data(), size_t(rows) * 8);
+    h->extras_offset = off;
+    h->extras_n = uint32_t(n_extras);
+    h->payload_bytes = off + need;
+  };
+
   const int64_t idle_ns = timeout_ms < 0 ? INT64_MAX : timeout_ms * 1000000LL;
   int64_t last_progress = now_ns();
   int64_t backoff_ns = 20000;
@@ -1000,7 +1053,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
       if (fp.paused) continue;
       size_t n;
       try {
-        n = f.scan(fp, 1u << 20, visit, on_batch);
+        n = n_extras ? f.scan(fp, 1u << 20, visit_x, on_batch) : f.scan(fp, 1u << 20, visit, on_batch);
       } catch (const OffsetOutOfRange&) {
         if (rows == 0 && scanned == 0) throw;  // nothing packed yet: let the caller reset positions
         stop = true;                           // keep what is packed; the reset happens on the next fill
@@ -1042,6 +1095,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
     h->max_row_len = spec.row_elems;
     h->total_elems = rows * spec.row_elems;
     h->n_scanned = scanned;
+    put_extras();
     out.rows = rows;
     out.scanned = scanned;
     return out;
@@ -1059,6 +1113,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
     h->total_elems = elems;
     h->trunc_len = spec.max_len >= 0 && spec.max_len < INT32_MAX ? int32_t(spec.max_len) : -1;
     h->n_scanned = scanned;
+    put_extras();
     out.rows = rows;
     out.scanned = scanned;
     return out;
@@ -1070,6 +1125,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   h->max_row_len = fixed ? spec.row_elems : max_len;
   h->total_elems = fixed ? rows * spec.row_elems : elems;
   h->n_scanned = scanned;
+  put_extras();
   out.rows = rows;
   out.scanned = scanned;
   return out;

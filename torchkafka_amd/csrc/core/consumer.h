@@ -128,7 +128,17 @@ struct PackSpec {
   int gather = 0;           // fixed-width: emit log locations (kPackGatherFixed) instead of values
   int span = 0;             // fixed-width / JSON text: emit log ranges + row positions (kPackRecordSpan /
                             // kPackJsonSpan) instead of values; CRC and decode on the device
+  // Record fields delivered beside the value, one int64 per row each (SlotHeader::extras_*):
+  // kExtraKey = the record key as an integer (key_enc), kExtraTimestamp = its timestamp (ms).
+  int extras = 0;
+  int key_enc = 0;           // kKeyBigEndian (Kafka's LongSerializer) | kKeyLittleEndian | kKeyAscii
+  int64_t key_default = -1;  // a null key, or one the encoding cannot read
 };
+
+enum ExtraField : int { kExtraKey = 1, kExtraTimestamp = 2 };
+enum KeyEncoding : int { kKeyBigEndian = 0, kKeyLittleEndian = 1, kKeyAscii = 2 };
+// The integer of a record key (KeyEncoding); `dflt` when null or unreadable.
+int64_t key_int64(const uint8_t* key, int32_t len, int enc, int64_t dflt);
 
 struct FillOutcome {
   int64_t rows = 0;

@@ -64,6 +64,12 @@ struct alignas(64) SlotHeader {
   Watermark wm[kMaxSlotParts];
   // direct (log-gather) slots: bytes of wm[k]'s partition log referenced by this slot, [0, log_end[k])
   uint64_t log_end[kMaxSlotParts];
+  // Per-row record fields a schema asked for beside the value (PackSpec::extras): extras_n int64
+  // columns of n_rows each (key, then timestamp), at extras_offset in the payload (inside
+  // payload_bytes); 0 columns: none.
+  uint64_t extras_offset;
+  uint32_t extras_n;
+  uint32_t extras_pad;
 };
 static_assert(sizeof(SlotHeader) <= kSlotHeaderBytes, "slot header too large");
 

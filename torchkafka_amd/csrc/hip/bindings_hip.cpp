@@ -217,10 +217,17 @@ PYBIND11_MODULE(_tkhip, m) {
            })
       .def("collate_fixed_last",
            [](MainDriver& d, uintptr_t stream, int dst_dt, uintptr_t dst, int64_t row, uintptr_t shift,
-              uintptr_t scale) {
+              uintptr_t scale, uintptr_t ext_dst) {
+             if (ext_dst) {
+               int64_t* e = ptr<int64_t>(ext_dst);
+               d.set_extra_outputs(&e, 1);
+             }
              d.collate_fixed(d.last, stream_of(stream), dst_dt, ptr<void>(dst), row, ptr<const float>(shift),
                              ptr<const float>(scale));
-           })
+           },
+           py::arg("stream"), py::arg("dst_dt"), py::arg("dst"), py::arg("row"), py::arg("shift"), py::arg("scale"),
+           py::arg("ext_dst") = 0)
+      .def_property_readonly("last_extras", [](MainDriver& d) { return int(d.last.extras_n); })
       .def("collate_varlen_last",
            [](MainDriver& d, uintptr_t stream, int dst_dt, uintptr_t out, int64_t L, double pad, uintptr_t lengths,
               uintptr_t mask) {

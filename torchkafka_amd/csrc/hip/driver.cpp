@@ -218,6 +218,8 @@ int MainDriver::poll_one_impl(bool block, int64_t timeout_ms) {
     v.worker = h->worker;
     v.payload_bytes = h->payload_bytes;
     v.values_offset = h->values_offset;
+    v.extras_offset = h->extras_offset;
+    v.extras_n = h->extras_n;
     v.row_bytes = h->row_bytes;
     v.max_row_len = h->max_row_len;
     v.total_elems = h->total_elems;
@@ -476,8 +478,22 @@ void MainDriver::launch_group(const int* slots, const int64_t* rows, const size_
     eng_->collate_fixed_group(slots, n, stream, voffs, v.src_dtype, dsts, dst_dt, rows, row, shift, scale);
 }
 
+void MainDriver::copy_extras(const int* slots, const SlotView* const* views, int n, hipStream_t stream) {
+  for (int k = 0; k < n && k < ext_n_; ++k) {
+    const SlotView& v = *views[k];
+    if (v.extras_n && ext_dsts_[k])
+      eng_->copy_bytes(slots[k], stream, size_t(v.extras_offset), ext_dsts_[k], size_t(v.n_rows) * v.extras_n * 8u);
+  }
+  ext_n_ = 0;
+}
+
 void MainDriver::collate_fixed(const SlotView& v, hipStream_t stream, int dst_dt, void* dst, int64_t row,
                                const float* shift, const float* scale) {
+  if (v.kind != uint32_t(tk::kPackRecordSpan) && ext_n_) {  // before the collate: its event covers the copy
+    const int slot = int(v.g);
+    const SlotView* vs[1] = {&v};
+    copy_extras(&slot, vs, 1, stream);
+  }
   bool record;
   note_handed(v.g, stream, &record);
   if (!record && coalesce_wait_ns_ > 0 && coalesce_ > 1) {
@@ -619,7 +635,14 @@ void MainDriver::launch_span(const int* slots, const SlotView* const* views, int
     a.b[k].out = dsts[k];
     a.b[k].err = perr_dev_ + perrs[k];
     a.b[k].partials = part_dev_ + perrs[k] * kPartials;
+    const SlotView& v = *views[k];
+    if (v.extras_n && k < ext_n_ && ext_dsts_[k]) {  // key / timestamp columns ride in the same kernel
+      a.b[k].ext_out = ext_dsts_[k];
+      a.b[k].ext_off = v.extras_offset;
+      a.b[k].ext_words = v.n_rows * v.extras_n;
+    }
   }
+  ext_n_ = 0;
   a.vec_store = vec ? 1 : 0;
   a.burst = span_burst_;  // loads a wave keeps in flight (span_decode.hip stage 1)
   int launches = 0;
@@ -1506,6 +1529,12 @@ void MainDriver::step_group_launch(hipStream_t stream, int dst_dt, void* const* 
     if (stream != last_stream_) {
       cover_handed();
       last_stream_ = stream;
+    }
+    if (ext_n_) {
+      const SlotView* vs[kMaxGroup];
+      vs[0] = &last;
+      for (int k = 1; k < n; ++k) vs[k] = &staged_[group_idx_[size_t(k - 1)]];
+      copy_extras(slots, vs, n, stream);
     }
     launch_group(slots, rows, voffs, n, last, stream, dst_dt, dsts, row, shift, scale);
     // one completion event (after the group kernel, on the last slot) releases every slot of the group

@@ -42,6 +42,8 @@ struct SlotView {
   uint32_t n_segs = 0;                // kPackRecordSpan / kPackJsonSpan: SpanSeg entries at values_offset
   int32_t trunc_len = -1;             // kPackJsonSpan: rows keep at most this many elements (-1: all)
   uint64_t span_bytes = 0;            // device decode: log bytes its segments read
+  uint64_t extras_offset = 0;         // record fields beside the values (SlotHeader::extras_*)
+  uint32_t extras_n = 0;
   std::vector<int64_t> shape;
   std::vector<tk::Watermark> wms;
   // coalesced fast path: collated ahead of delivery by a group launch
@@ -65,6 +67,13 @@ class MainDriver {
 
   void collate_fixed(const SlotView& v, hipStream_t stream, int dst_dt, void* dst, int64_t row, const float* shift,
                      const float* scale);
+  // Record fields beside the values (SlotView::extras_*): the next fixed-width launch (single,
+  // group or ahead) writes batch k's [extras_n, rows] int64 columns to dsts[k].  Consumed by that
+  // launch; torch_step.cpp allocates them with the value tensors.
+  void set_extra_outputs(int64_t* const* dsts, int n) {
+    ext_n_ = n;
+    for (int k = 0; k < n && k < kMaxGroup; ++k) ext_dsts_[k] = dsts[k];
+  }
   // The slot's whole payload copied to `dst` (device memory) on `stream` (kPackTree slots: the
   // fields are views of that block); the slot is released once the copy completed.
   void copy_payload(const SlotView& v, hipStream_t stream, void* dst);
@@ -257,6 +266,10 @@ class MainDriver {
   int64_t next_err_word();
   // Span decode: CRC chains of RecordBatches split over segments, verdict and message (at release).
   void check_span(int64_t g, int64_t pe);
+  int ext_n_ = 0;                  // set_extra_outputs(): destinations of the next launch
+  int64_t* ext_dsts_[kMaxGroup] = {};
+  // host-decoded fixed-width batches: their record fields copied beside the collate (same stream)
+  void copy_extras(const int* slots, const SlotView* const* views, int n, hipStream_t stream);
   void launch_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
                    void* const* dsts, const float* shift, const float* scale, bool record_last, int64_t* perrs);
   void launch_json_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
@@ -361,6 +374,7 @@ class MainDriver {
     bool auto_commit = true;
     int64_t timeout_ms = 100;
     bool grouped = true;
+    int extras = 0;  // record-field columns per batch (key / timestamp), 0: values only
   } fast;
   int64_t fast_batches_ = 0, fast_records_ = 0, fast_ns_ = 0;
  private:

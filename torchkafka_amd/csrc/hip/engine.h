@@ -100,6 +100,8 @@ class Engine {
   void stream_wait_done(int s, hipStream_t user);
   void record_done(int s, hipStream_t user) { finish(s, user); }
   void copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes);
+  // The same without the slot's completion event: a kernel queued after it on `user` records it.
+  void copy_bytes(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes);
   void synchronize();
 
   // legacy names used by tests

@@ -301,6 +301,7 @@ void Engine::collate_span(const int* slots, int n, hipStream_t user, SpanLaunch&
     check_slot(slots[k]);
     begin(slots[k], user);  // DMA mode: the row table was copied with the slot payload
     a.b[k].row_pos = reinterpret_cast<const uint64_t*>(src_base(slots[k]));
+    if (a.b[k].ext_words) a.b[k].ext_src = reinterpret_cast<const int64_t*>(src_base(slots[k]) + a.b[k].ext_off);
   }
   a.tabs = span_tables();
   launch_span_decode(a, src_dt, dst_dt, shift, scale, user);
@@ -317,6 +318,12 @@ void Engine::collate_json_stage(const int* slots, int n, hipStream_t user, JsonS
   }
   a.tabs = span_tables();
   launch_json_stage(a, user);
+}
+
+void Engine::copy_bytes(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes) {
+  check_slot(s);
+  begin(s, user);
+  if (nbytes) TKH_CHECK(hipMemcpyAsync(dst, src_base(s) + offset, nbytes, hipMemcpyDefault, user));
 }
 
 void Engine::copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes) {

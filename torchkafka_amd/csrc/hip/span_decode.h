@@ -31,6 +31,14 @@ struct SpanBatchOut {
   const uint64_t* row_pos;   // device view of the slot's row table (log positions of the values)
   int32_t* err;              // host-mapped status word: -1 clean, else the first bad segment
   uint32_t* partials;        // host-mapped raw CRC per segment (RecordBatches spanning segments)
+  // Record fields beside the values (key / timestamp, one int64 per row each): the workgroup of
+  // the batch's first segment copies ext_words of them from the slot (ext_src; the driver gives
+  // the payload offset in ext_off, the engine turns it into the slot's device address) to ext_out.
+  int64_t* ext_out;
+  const int64_t* ext_src;
+  uint64_t ext_off;
+  uint32_t ext_words;
+  uint32_t ext_pad;
 };
 
 struct SpanLaunch {

@@ -149,7 +149,11 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
     }
   }
 
-  // ---- 4. verdict
+  // ---- 4. record fields beside the values (key / timestamp): the batch's first segment copies them
+  if (sg.seg == 0 && bo.ext_words)
+    for (uint32_t i = uint32_t(t); i < bo.ext_words; i += kThreads) bo.ext_out[i] = bo.ext_src[i];
+
+  // ---- 5. verdict
   if (do_crc) {
     __syncthreads();
     if (t == 0) span::crc_verdict(shift_set, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials);

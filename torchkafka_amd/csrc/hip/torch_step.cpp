@@ -38,10 +38,56 @@ at::ScalarType scalar_type_of(int code) {
     default: throw std::invalid_argument("step_fixed_tensor: unsupported dtype code");
   }
 }
+at::Tensor alloc_group(MainDriver& d, const std::vector<int64_t>& shape, const at::TensorOptions& opts,
+                       c10::DeviceIndex dev, bool span);
+
 // Outputs of a var-len batch parsed ahead of its delivery by a coalesced launch.
 struct VarlenOut {
   at::Tensor out, lengths, mask;
 };
+
+// Outputs of a fixed-width batch: the values, and -- when the schema asks for record fields --
+// its [extras, rows] int64 key / timestamp columns (decoded by the same launch).
+struct FixedOut {
+  at::Tensor out, ext;
+};
+
+std::shared_ptr<void> fixed_handle(at::Tensor out, at::Tensor ext) {
+  auto h = std::make_shared<FixedOut>();
+  h->out = std::move(out);
+  h->ext = std::move(ext);
+  return h;
+}
+
+// [sum(rows) * extras] int64, viewed [extras, rows_k] per batch, allocated like its values block
+// (on the decode stream for a device-decode group) and handed to the driver's next launch.
+std::vector<at::Tensor> alloc_extras(MainDriver& d, const std::vector<int64_t>& rows, int extras,
+                                     c10::DeviceIndex dev, bool span) {
+  std::vector<at::Tensor> out;
+  if (extras <= 0) return out;
+  int64_t total = 0;
+  for (auto x : rows) total += x;
+  const auto opts = at::TensorOptions().dtype(at::kLong).device(at::kCUDA, dev);
+  at::Tensor all = alloc_group(d, {total * extras}, opts, dev, span);
+  int64_t* dsts[kMaxGroup];
+  int64_t off = 0;
+  for (size_t k = 0; k < rows.size(); ++k) {
+    out.push_back(all.narrow(0, off, rows[k] * extras).view({extras, rows[k]}));
+    dsts[k] = out.back().data_ptr<int64_t>();
+    off += rows[k] * extras;
+  }
+  d.set_extra_outputs(dsts, int(rows.size()));
+  return out;
+}
+
+// The item a fixed-width step hands out: the values, or (values, column 0, column 1, ...).
+py::object fixed_item(const at::Tensor& out, const at::Tensor& ext) {
+  if (!ext.defined()) return py::reinterpret_steal<py::object>(THPVariable_Wrap(out));
+  py::list items;
+  items.append(py::reinterpret_steal<py::object>(THPVariable_Wrap(out)));
+  for (int64_t i = 0; i < ext.size(0); ++i) items.append(py::reinterpret_steal<py::object>(THPVariable_Wrap(ext[i])));
+  return py::tuple(items);
+}
 
 // Output block of a coalesced fixed-width launch.  Device decode runs on the driver's decode
 // stream: allocate there, so the caching allocator orders the memory's reuse against that stream
@@ -63,7 +109,7 @@ at::Tensor alloc_group(MainDriver& d, const std::vector<int64_t>& shape, const a
 // Device decode ahead of delivery (MainDriver::ahead_begin): up to two full groups of staged
 // batches are decoded while the user still works on earlier ones.
 void launch_ahead(MainDriver& d, const std::vector<int64_t>& row_shape, const at::TensorOptions& opts,
-                  c10::DeviceIndex dev, int dst_dt, const float* shift, const float* scale) {
+                  c10::DeviceIndex dev, int dst_dt, const float* shift, const float* scale, int extras) {
   std::vector<int64_t> rows;
   for (int q = 0; q < 3; ++q) {
     {
@@ -76,6 +122,7 @@ void launch_ahead(MainDriver& d, const std::vector<int64_t>& row_shape, const at
     std::vector<int64_t> all_shape(row_shape);
     all_shape[0] = total;
     at::Tensor all = alloc_group(d, all_shape, opts, dev, true);
+    std::vector<at::Tensor> ext = alloc_extras(d, rows, extras, dev, true);
     void* dsts[kMaxGroup];
     std::vector<std::shared_ptr<void>> handles;
     handles.reserve(rows.size());
@@ -83,7 +130,7 @@ void launch_ahead(MainDriver& d, const std::vector<int64_t>& row_shape, const at
     for (size_t k = 0; k < rows.size(); ++k) {
       at::Tensor t = rows.size() == 1 ? all : all.narrow(0, off, rows[k]);
       dsts[k] = t.data_ptr();
-      handles.emplace_back(new at::Tensor(std::move(t)), [](void* p) { delete static_cast<at::Tensor*>(p); });
+      handles.emplace_back(fixed_handle(std::move(t), ext.empty() ? at::Tensor() : ext[k]));
       off += rows[k];
     }
     py::gil_scoped_release nogil;
@@ -175,14 +222,20 @@ py::tuple step_once(MainDriver& d, const MainDriver::FastConfig& cfg) {
   int64_t r;
   if (!cfg.grouped) {
     at::Tensor out = at::empty(cfg.shape, opts);
+    std::vector<at::Tensor> ext = alloc_extras(d, {cfg.shape[0]}, cfg.extras, dev, false);
     {
       py::gil_scoped_release nogil;
       r = d.step_fixed(stream, cfg.dst_dt, out.data_ptr(), cfg.row, cfg.shift, cfg.scale, cfg.auto_commit,
                        cfg.timeout_ms, &cs, &d.last);
     }
     if (r <= 0) return py::make_tuple(r, cs, py::none());
-    if (r < cfg.shape[0]) out = out.narrow(0, 0, r);
-    return py::make_tuple(r, cs, py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(out))));
+    at::Tensor e = ext.empty() ? at::Tensor() : ext[0];
+    if (r < cfg.shape[0]) {
+      out = out.narrow(0, 0, r);
+      // a short batch's columns were written back to back: [extras, r] from the block's start
+      if (e.defined()) e = e.reshape({-1}).narrow(0, 0, e.size(0) * r).view({e.size(0), r});
+    }
+    return py::make_tuple(r, cs, fixed_item(out, e));
   }
   std::vector<int64_t> rows;
   std::shared_ptr<void> pre;
@@ -191,15 +244,19 @@ py::tuple step_once(MainDriver& d, const MainDriver::FastConfig& cfg) {
     r = d.step_group_begin(stream, cfg.auto_commit, cfg.timeout_ms, &cs, &rows, &pre);
   }
   if (r <= 0) return py::make_tuple(r, cs, py::none());
-  at::Tensor out;
+  at::Tensor out, ext;
   if (pre) {
-    out = *static_cast<at::Tensor*>(pre.get());
+    const auto* o = static_cast<FixedOut*>(pre.get());
+    out = o->out;
+    ext = o->ext;
   } else {
     int64_t total = 0;
     for (auto x : rows) total += x;
     std::vector<int64_t> all_shape(cfg.shape);
     all_shape[0] = total;
-    at::Tensor all = alloc_group(d, all_shape, opts, dev, d.last.kind == uint32_t(tk::kPackRecordSpan));
+    const bool span = d.last.kind == uint32_t(tk::kPackRecordSpan);
+    at::Tensor all = alloc_group(d, all_shape, opts, dev, span);
+    std::vector<at::Tensor> exts = alloc_extras(d, rows, cfg.extras, dev, span);
     void* dsts[kMaxGroup];
     std::vector<std::shared_ptr<void>> handles;
     handles.reserve(rows.size());
@@ -207,18 +264,20 @@ py::tuple step_once(MainDriver& d, const MainDriver::FastConfig& cfg) {
     for (size_t k = 0; k < rows.size(); ++k) {
       at::Tensor t = rows.size() == 1 ? all : all.narrow(0, off, rows[k]);
       dsts[k] = t.data_ptr();
-      if (k == 0)
+      if (k == 0) {
         out = t;
-      else
-        handles.emplace_back(new at::Tensor(std::move(t)), [](void* p) { delete static_cast<at::Tensor*>(p); });
+        if (!exts.empty()) ext = exts[0];
+      } else {
+        handles.emplace_back(fixed_handle(std::move(t), exts.empty() ? at::Tensor() : exts[k]));
+      }
       off += rows[k];
     }
     py::gil_scoped_release nogil;
     d.step_group_launch(stream, cfg.dst_dt, dsts, cfg.row, cfg.shift, cfg.scale, std::move(handles));
   }
   if (d.last.kind == uint32_t(tk::kPackRecordSpan))
-    launch_ahead(d, cfg.shape, opts, dev, cfg.dst_dt, cfg.shift, cfg.scale);
-  return py::make_tuple(r, cs, py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(out))));
+    launch_ahead(d, cfg.shape, opts, dev, cfg.dst_dt, cfg.shift, cfg.scale, cfg.extras);
+  return py::make_tuple(r, cs, fixed_item(out, ext));
 }
 
 }  // namespace
@@ -231,7 +290,7 @@ void register_torch_step(py::module_& m) {
   cls.def(
       "configure_fast",
       [](MainDriver& d, int device, std::vector<int64_t> shape, int dst_dt, int64_t row, uintptr_t shift,
-         uintptr_t scale, bool auto_commit, int64_t timeout_ms, bool grouped) {
+         uintptr_t scale, bool auto_commit, int64_t timeout_ms, bool grouped, int extras) {
         if (shape.empty()) throw std::invalid_argument("configure_fast: empty shape");
         scalar_type_of(dst_dt);  // validates
         auto& c = d.fast;
@@ -244,9 +303,10 @@ void register_torch_step(py::module_& m) {
         c.auto_commit = auto_commit;
         c.timeout_ms = timeout_ms;
         c.grouped = grouped;
+        c.extras = extras;
       },
       py::arg("device"), py::arg("shape"), py::arg("dst_dt"), py::arg("row"), py::arg("shift"), py::arg("scale"),
-      py::arg("auto_commit"), py::arg("timeout_ms"), py::arg("grouped"));
+      py::arg("auto_commit"), py::arg("timeout_ms"), py::arg("grouped"), py::arg("extras") = 0);
   cls.def("fast_next", [](MainDriver& d) -> py::tuple {
     const int64_t t0 = tk::now_ns();
     py::tuple res = step_once(d, d.fast);
@@ -430,7 +490,7 @@ void register_torch_step(py::module_& m) {
         if (r <= 0) return py::make_tuple(r, cs, py::none());
         at::Tensor out;
         if (pre) {
-          out = *static_cast<at::Tensor*>(pre.get());
+          out = static_cast<FixedOut*>(pre.get())->out;
         } else {
           int64_t total = 0;
           for (auto x : rows) total += x;
@@ -449,7 +509,7 @@ void register_torch_step(py::module_& m) {
             if (k == 0)
               out = t;
             else
-              handles.emplace_back(new at::Tensor(std::move(t)), [](void* p) { delete static_cast<at::Tensor*>(p); });
+              handles.emplace_back(fixed_handle(std::move(t), at::Tensor()));
             off += rows[k];
           }
           py::gil_scoped_release nogil;

@@ -635,9 +635,17 @@ class DeviceLoader:
         fit = budget // max(1, self.n_producers * self._slot_capacity())
         return int(max(4, min(8, fit)))
 
+    def _n_extras(self) -> int:
+        """Record-field columns (Key / Timestamp) the schema adds beside the value."""
+        return len(getattr(self.schema, "fields", ()) or ())
+
     def _slot_capacity(self) -> int:
         if self.slot_bytes is not None:
             return int(self.slot_bytes)
+        # record fields ride after the layout: one int64 per row each (+ alignment)
+        return self._layout_capacity() + (self.batch_size * 8 * self._n_extras() + 256 if self._n_extras() else 0)
+
+    def _layout_capacity(self) -> int:
         s = self.schema
         if self._span():
             # row table (8 B per row) + SpanSeg entries: one per RecordBatch touched, plus one per
@@ -1022,9 +1030,20 @@ class DeviceLoader:
         s = self.schema
         prm = self._norm_params(s.row_elems)
         shift, scale = (prm[0].data_ptr(), prm[1].data_ptr()) if prm is not None else (0, 0)
+        nx = self._n_extras()
         drv.configure_fast(self.device.index, [self.batch_size, *s.shape], DTYPE_CODE[self._out_dtype(s.dtype)],
-                           s.row_elems, shift, scale, native_ac, 100, self.coalesce > 1)
-        return drv.fast_next
+                           s.row_elems, shift, scale, native_ac, 100, self.coalesce > 1, nx)
+        if nx < 2 or s.column_order() == list(range(nx)):
+            return drv.fast_next
+        order = s.column_order()  # fields added timestamp first: the native columns are key-first
+        native = drv.fast_next
+
+        def step():
+            r, cs, item = native()
+            if item is not None:
+                item = (item[0], *(item[1 + i] for i in order))
+            return r, cs, item
+        return step
 
     def _varlen_stage(self, drv, native_ac: bool):
         src = CODE_DTYPE[self._default_src_code()]
@@ -1220,7 +1239,12 @@ class DeviceLoader:
             out = torch.empty((n_rows, *shape), dtype=dst_dt, device=dev)
             prm = self._norm_params(row)
             shift, scale = (prm[0].data_ptr(), prm[1].data_ptr()) if prm is not None else (0, 0)
-            drv.collate_fixed_last(stream, DTYPE_CODE[dst_dt], out.data_ptr(), row, shift, scale)
+            nx = drv.last_extras
+            ext = torch.empty((nx, n_rows), dtype=torch.int64, device=dev) if nx else None
+            drv.collate_fixed_last(stream, DTYPE_CODE[dst_dt], out.data_ptr(), row, shift, scale,
+                                   ext.data_ptr() if ext is not None else 0)
+            if ext is not None and not self.return_info:
+                out = self._with_fields(out, ext)
         else:
             L = self.pad_to if self.pad_to is not None else int(max_len)
             if self.pad_to is None and self.pad_multiple > 1:
@@ -1275,8 +1299,16 @@ class DeviceLoader:
         if (dst_dt in FLOAT_DTYPES) != (src_dt in FLOAT_DTYPES) and src_dt in FLOAT_DTYPES:
             raise TypeError(f"cannot collate {src_dt} records to {dst_dt}")
         dev = self.device
-        lengths = mask = None
+        lengths = mask = ext = None
         if fixed:
+            x_off, nx = run.ring.slot_extras(g)
+            if nx:  # record fields beside the values: [nx, rows] int64 at x_off (read before the slot is released)
+                ext = torch.empty((nx, n_rows), dtype=torch.int64, device=dev)
+                if run.engine is not None:
+                    run.engine.copy_raw(g, _stream_ptr(dev), int(x_off), ext.data_ptr(), nx * n_rows * 8)
+                else:
+                    ext.copy_(torch.frombuffer(run.ring.payload_view(g), dtype=torch.int64, count=nx * n_rows,
+                                               offset=int(x_off)).view(nx, n_rows))
             row = int(max_len) if max_len else 1
             out = torch.empty((n_rows, *shape), dtype=dst_dt, device=dev)
             prm = self._norm_params(row)
@@ -1324,8 +1356,13 @@ class DeviceLoader:
         if self.return_info:
             return KafkaBatch(out, lengths, mask, wms, n_rec)
         if fixed:
-            return out
+            return out if ext is None else self._with_fields(out, ext)
         return (out, lengths, mask) if self.return_mask else (out, lengths)
+
+    def _with_fields(self, out, ext):
+        """(values, fields...) in the order the schema added them (native columns: key first)."""
+        order = self.schema.column_order()
+        return (out, *(ext[i] for i in order))
 
     def _norm_params(self, row: int):
         if self.normalize is None:

@@ -219,6 +219,7 @@ def _native_loop(ring, worker_id, spw, consumer, schema, cfg, state) -> None:
     from ..client.errors import OffsetOutOfRangeError
 
     kind, elem, row_elems, min_len, max_len, trunc, skip_bad = schema.native_spec()
+    extras, key_enc, key_default = schema.extras_spec() if hasattr(schema, "extras_spec") else (0, 0, -1)
     if kind == core().PACK_JSON_F32 and cfg.get("json_device"):
         kind = core().PACK_JSON_TEXT  # frame + copy the text; the gfx950 kernel parses it
     bs = int(cfg["batch_size"])
@@ -246,7 +247,7 @@ def _native_loop(ring, worker_id, spw, consumer, schema, cfg, state) -> None:
             try:
                 rows, _scanned, timed_out, shut = fetcher.fill_slot(ring, g, kind, elem, row_elems, min_len,
                                                                     max_len, trunc, skip_bad, bs, timeout,
-                                                                    gather, span)
+                                                                    gather, span, extras, key_enc, key_default)
                 if group_managed and fetcher.last_reassigned:
                     consumer._ensure_group()  # the next fill reads the new assignment
                     if rows == 0:

@@ -71,6 +71,12 @@ class FixedWidth:
     def native_spec(self) -> tuple:
         return (core().PACK_FIXED, self.elem_size, self.row_elems, 0, -1, True, self.skip_bad)
 
+    def __add__(self, field):
+        return WithFields(self, (field,))
+
+    # record fields beside the value (see WithFields): none
+    fields: tuple = ()
+
 
 @dataclass(frozen=True)
 class VarLen:
@@ -144,3 +150,112 @@ class JsonArray(VarLen):
     def native_spec(self) -> tuple:
         return (core().PACK_JSON_F32, 4, 0, self.min_len, -1 if self.max_len is None else self.max_len,
                 self.truncate, self.skip_bad)
+
+
+# ---------------------------------------------------------------- record fields beside the value
+
+_KEY_ENCODINGS = {"be": 0, "le": 1, "ascii": 2}
+
+
+@dataclass(frozen=True)
+class Key:
+    """The record key as an int64 label beside the value: ``encoding`` "be" (8 bytes big-endian,
+    Kafka's LongSerializer -- the default), "le" (8 bytes little-endian) or "ascii" (decimal
+    digits).  A null key, or one the encoding cannot read, gives ``default``."""
+
+    encoding: str = "be"
+    default: int = -1
+
+    bit = 1  # csrc/core/consumer.h kExtraKey
+
+    def __post_init__(self):
+        if self.encoding not in _KEY_ENCODINGS:
+            raise ValueError(f"Key encoding {self.encoding!r}: one of {sorted(_KEY_ENCODINGS)}")
+
+    def value_of(self, record) -> int:
+        return int(core().key_int64(record.key, _KEY_ENCODINGS[self.encoding], int(self.default)))
+
+
+@dataclass(frozen=True)
+class Timestamp:
+    """The record timestamp (ms, int64) beside the value."""
+
+    bit = 2  # csrc/core/consumer.h kExtraTimestamp
+
+    def value_of(self, record) -> int:
+        return int(record.timestamp)
+
+
+@dataclass(frozen=True)
+class WithFields:
+    """A fixed-width value plus per-record fields, e.g. ``FixedWidth(torch.float32, (256,)) +
+    Key()`` -- a label riding with the features (the reference README's ``(features, label)``
+    samples, README.md:40-44).  Batches are ``(values, key, timestamp)`` in the order the fields
+    were added, each field an int64 tensor of one element per row.  On the device path the worker
+    reads the fields while it walks the record headers and the gfx950 decode kernel copies them
+    into the batch beside the values (no extra launch)."""
+
+    value: FixedWidth
+    fields: tuple = ()
+
+    def __post_init__(self):
+        if not isinstance(self.value, FixedWidth):
+            raise TypeError("record fields ride with a FixedWidth value schema")
+        bits = [f.bit for f in self.fields]
+        if len(set(bits)) != len(bits):
+            raise ValueError("each record field can be added once")
+        if any(not isinstance(f, (Key, Timestamp)) for f in self.fields):
+            raise TypeError("fields: Key() and/or Timestamp()")
+
+    def __add__(self, field):
+        return WithFields(self.value, self.fields + (field,))
+
+    # the value schema's interface
+    kind = 0
+
+    @property
+    def dtype(self):
+        return self.value.dtype
+
+    @property
+    def shape(self):
+        return self.value.shape
+
+    @property
+    def skip_bad(self):
+        return self.value.skip_bad
+
+    @property
+    def row_elems(self) -> int:
+        return self.value.row_elems
+
+    @property
+    def elem_size(self) -> int:
+        return self.value.elem_size
+
+    @property
+    def row_bytes(self) -> int:
+        return self.value.row_bytes
+
+    def native_spec(self) -> tuple:
+        return self.value.native_spec()
+
+    def extras_spec(self) -> tuple:
+        """(field bits, key encoding, key default) for the native packer; the columns are stored
+        key first, then timestamp -- :meth:`column_order` maps them back to the order added."""
+        key = next((f for f in self.fields if isinstance(f, Key)), None)
+        bits = 0
+        for f in self.fields:
+            bits |= f.bit
+        return bits, _KEY_ENCODINGS[key.encoding] if key else 0, int(key.default) if key else -1
+
+    def column_order(self) -> list[int]:
+        """Index of each added field among the native columns (key, timestamp)."""
+        native = sorted(self.fields, key=lambda f: f.bit)
+        return [native.index(f) for f in self.fields]
+
+    def process(self, record):
+        v = self.value.process(record)
+        if v is None:
+            return None
+        return (v, *(torch.tensor(f.value_of(record), dtype=torch.int64) for f in self.fields))
