@@ -25,6 +25,16 @@ prof() {  # prof <name> <timeout> <rocprofv3 args...> -- <program...>   (kernel 
   [ $rc -ne 0 ] && exit $rc
   return 0
 }
+pmc() {  # pmc <name> <seconds> <counters...> -- <program...>   (counters only, SIGKILL at the limit)
+  local name=$1 t=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  (cd /tmp && export TMPDIR=/tmp && timeout -s KILL "$t" rocprofv3 --pmc "$@" > "$OUT/$name.log" 2>&1)
+  local rc=$?
+  tail -n 3 "$OUT/$name.log" | cut -c1-1500
+  echo "=== $name rc=$rc"
+  [ $rc -ne 0 ] && exit $rc
+  return 0
+}
 R=$PWD
 for s in ${STEPS:-smoke benchdrv}; do
   case $s in
@@ -39,10 +49,10 @@ for s in ${STEPS:-smoke benchdrv}; do
     config4w8) run config4_w8 300 python benchmarks/config4_json_varlen.py --workers 8 ;;
     config5) run config5 300 python benchmarks/config5_large_messages.py ;;
     bridge) run bridge_e2e 600 python benchmarks/bridge_e2e.py ;;
-    profbench) prof profbench 300 --kernel-trace --stats --output-format csv -d "$OUT/profbench" -o run -- python3 "$R/bench.py" --steps 1000 --steady-steps 4000 --extra-blocks "" ;;
-    profdma) prof profdma 300 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profdma" -o run -- python3 "$R/bench.py" --h2d dma --steps 1000 --steady-steps 4000 --extra-blocks "" ;;
-    pmcspan) prof pmc_span 120 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_span" -o run -- python3 "$R/bench.py" --steps 200 --warmup 20 --steady-steps 0 --extra-blocks "" ;;
-    pmcdma) prof pmc_dma 120 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_dma" -o run -- python3 "$R/bench.py" --steps 200 --warmup 20 --steady-steps 0 --extra-blocks "" --h2d dma ;;
+    profbench) prof profbench 300 --kernel-trace --stats --output-format csv -d "$OUT/profbench" -o run -- python3 "$R/bench.py" --steps 1000 --steady-steps 4000 --extra-blocks "" --bridge-steps 0 ;;
+    profdma) prof profdma 300 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profdma" -o run -- python3 "$R/bench.py" --h2d dma --steps 1000 --steady-steps 4000 --extra-blocks "" --bridge-steps 0 ;;
+    pmcspan) pmc pmc_span 120 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_span" -o run -- python3 "$R/bench.py" --steps 200 --warmup 20 --steady-steps 0 --extra-blocks "" --bridge-steps 0 ;;
+    pmcdma) pmc pmc_dma 120 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_dma" -o run -- python3 "$R/bench.py" --steps 200 --warmup 20 --steady-steps 0 --extra-blocks "" --bridge-steps 0 --h2d dma ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

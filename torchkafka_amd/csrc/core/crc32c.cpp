@@ -307,6 +307,11 @@ void crc32c_span_tables(uint32_t* out) {
   const Tables& T = tables();
   for (int k = 0; k < 8; ++k)
     for (int b = 0; b < 256; ++b) out[kSpanTabSlice + k * 256 + b] = T.t[k][b];
+  for (int k = 0; k < 8; ++k)
+    for (int n = 0; n < 16; ++n) {
+      out[kSpanTabNib + (2 * k) * 16 + n] = T.t[k][n];
+      out[kSpanTabNib + (2 * k + 1) * 16 + n] = T.t[k][n << 4];
+    }
   const uint32_t lanes[2] = {kSpanLaneSmall, kSpanLaneLarge};
   for (int set = 0; set < 2; ++set) {
     for (uint32_t j = 0; j < kSpanLevels; ++j) {
@@ -321,7 +326,7 @@ void crc32c_span_tables(uint32_t* out) {
 
 uint32_t crc32c_span_emulate(const uint8_t* buf, uint32_t c0, uint32_t c1, bool first) {
   // Host mirror of span_decode.hip's CRC stage, step for step: end-aligned lane chunks (260 or
-  // 516 bytes), a slice-by-4 step for a chunk's first 4 bytes then slice-by-8 steps, bytes below
+  // 516 bytes) looked up in the same nibble rows, a slice-by-4 step for a chunk's first 4 bytes then slice-by-8 steps, bytes below
   // c0 masked to zero (groups wholly below c0 skipped), the first 4 CRC'd bytes of a RecordBatch
   // xor 0xFF (the 0xFFFFFFFF initial value), then the 8-level shift tree.
   static uint32_t tab[kSpanTabWords];
@@ -339,22 +344,29 @@ uint32_t crc32c_span_emulate(const uint8_t* buf, uint32_t c0, uint32_t c1, bool 
     for (int k = 0; k < 4; ++k) w |= byte_at(a + k) << (8 * k);
     return w;
   };
-  const uint32_t* T = tab + kSpanTabSlice;
+  // byte table k through its two nibble rows, as the kernel looks it up (span_device.h nib_dword)
+  const uint32_t* N = tab + kSpanTabNib;
+  auto nib = [&](uint32_t w, int b) {
+    uint32_t r = 0;
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t v = (w >> (8 * i)) & 255u;
+      r ^= N[(2 * (b - i)) * 16 + (v & 15u)] ^ N[(2 * (b - i) + 1) * 16 + (v >> 4)];
+    }
+    return r;
+  };
   uint32_t lane[kSpanLanes];
   for (uint32_t t = 0; t < kSpanLanes; ++t) {
     const int64_t start = int64_t(c1) - int64_t(kSpanLanes - t) * L;
     uint32_t crc = 0;
     if (start + 4 > int64_t(c0)) {
       const uint32_t x = crc ^ word_at(start);
-      crc = T[3 * 256 + (x & 255)] ^ T[2 * 256 + ((x >> 8) & 255)] ^ T[256 + ((x >> 16) & 255)] ^ T[x >> 24];
+      crc = nib(x, 3);
     }
     for (uint32_t j = 0; j < (L - 4) / 8; ++j) {
       const int64_t a = start + 4 + 8 * int64_t(j);
       if (a + 8 <= int64_t(c0)) continue;
       const uint32_t x = crc ^ word_at(a), y = word_at(a + 4);
-      crc = T[7 * 256 + (x & 255)] ^ T[6 * 256 + ((x >> 8) & 255)] ^ T[5 * 256 + ((x >> 16) & 255)] ^
-            T[4 * 256 + (x >> 24)] ^ T[3 * 256 + (y & 255)] ^ T[2 * 256 + ((y >> 8) & 255)] ^
-            T[256 + ((y >> 16) & 255)] ^ T[y >> 24];
+      crc = nib(x, 7) ^ nib(y, 3);
     }
     lane[t] = crc;
   }

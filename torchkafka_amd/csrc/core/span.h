@@ -47,11 +47,18 @@ inline constexpr uint32_t span_lane_bytes(uint32_t crc_len) {
   return crc_len <= kSpanLaneSmall * kSpanLanes ? kSpanLaneSmall : kSpanLaneLarge;
 }
 // Device table layout (uint32 words): slice-by-8 byte tables T0..T7, then for each lane size
-// (small, large), level j and byte k of the value: shift-by-(L << j)-bytes of (b << 8k).
+// (small, large), level j and byte k of the value: shift-by-(L << j)-bytes of (b << 8k), then the
+// nibble split of T0..T7 the kernels keep in LDS: row 2k + h holds T_k[n << 4h] for n < 16.  A
+// byte table is linear over GF(2), so T_k[b] = row(2k)[b & 15] ^ row(2k + 1)[b >> 4]; a 16-entry
+// row spans 16 LDS banks, so a ds_read_b32 of one row by any 32 lanes is conflict-free (distinct
+// nibbles hit distinct banks, equal ones broadcast), where a data-dependent 256-entry lookup put
+// ~3 lanes on a bank.
 constexpr uint32_t kSpanTabSlice = 0;
 constexpr uint32_t kSpanTabShift = 8 * 256;
 constexpr uint32_t kSpanTabShiftSet = kSpanLevels * 4 * 256;
-constexpr uint32_t kSpanTabWords = kSpanTabShift + 2 * kSpanTabShiftSet;
+constexpr uint32_t kSpanTabNib = kSpanTabShift + 2 * kSpanTabShiftSet;
+constexpr uint32_t kSpanTabNibWords = 16 * 16;
+constexpr uint32_t kSpanTabWords = kSpanTabNib + kSpanTabNibWords;
 
 enum SpanSegFlags : uint32_t {
   kSegCrcFirst = 1,   // the segment holds the first CRC'd byte of its RecordBatch (offset 21)

@@ -43,7 +43,7 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
   __shared__ int32_t tln[kMaxRows];
   __shared__ int32_t cnt[kMaxRows];
   __shared__ uint32_t dst[kMaxRows];
-  __shared__ uint32_t tab[2048];
+  __shared__ __attribute__((aligned(256))) uint32_t tab[span::kNibLdsWords];
   __shared__ uint32_t wcrc[kWaves];
   __shared__ uint32_t wsum[kWaves];
 
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
       cnt[r] = d.count;
     }
     if (do_crc)
-      for (int i = t; i < 2048; i += kThreads) tab[i] = a.tabs[tk::kSpanTabSlice + i];
+      span::load_nib_rows(tab, a.tabs);
   });
   __syncthreads();
   const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
   constexpr int kPer = 16 / int(sizeof(S));  // source elements per 16-byte group
   __shared__ __attribute__((aligned(16))) uint8_t buf[kBufBytes];
   __shared__ int32_t rel[tk::kSpanMaxSegRows];
-  __shared__ uint32_t tab[2048];
+  __shared__ __attribute__((aligned(256))) uint32_t tab[span::kNibLdsWords];
   __shared__ uint32_t wcrc[kThreads / 64];
 
   const int t = int(threadIdx.x);
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
     for (uint32_t r = uint32_t(t); r < nrows; r += kThreads)
       rel[r] = int32_t(int64_t(bo.row_pos[row_begin + r]) - base);
     if (do_crc)
-      for (int i = t; i < 2048; i += kThreads) tab[i] = a.tabs[tk::kSpanTabSlice + i];
+      span::load_nib_rows(tab, a.tabs);
   });
   __syncthreads();
   const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, 
   __shared__ int32_t rel[tk::kJsonSpanMaxSegRows];
   __shared__ int32_t tln[tk::kJsonSpanMaxSegRows];
   __shared__ int32_t cnt[tk::kJsonSpanMaxSegRows];
-  __shared__ uint32_t tab[2048];
+  __shared__ __attribute__((aligned(256))) uint32_t tab[span::kNibLdsWords];
   __shared__ uint32_t wcrc[kWaves];
 
   const int t = int(threadIdx.x), lane = t & 63, wv = t >> 6;
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, 
       cnt[r] = d.count;
     }
     if (do_crc)
-      for (int i = t; i < 2048; i += kThreads) tab[i] = a.tabs[tk::kSpanTabSlice + i];
+      span::load_nib_rows(tab, a.tabs);
   });
   __syncthreads();
   const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);

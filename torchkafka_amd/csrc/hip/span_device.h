@@ -6,9 +6,11 @@
 //      move more bytes; the launches of two or three decode streams keep the link busy);
 //   2. crc_lanes: CRC32C of a RecordBatch's bytes [21, end): 256 lanes x 260- or 516-byte chunks
 //      ending at the range end (an odd dword count per chunk: the 32 lanes of a ds_read_b32
-//      group hit 32 different banks), slice-by-8 tables in LDS fed by a sliding dword window
-//      (two ds_read_b32 + two v_alignbyte per 8 bytes), then 6 shuffle levels of "shift by 2^j
-//      chunks" (4 table lookups each, csrc/core/crc32c.cpp crc32c_span_tables);
+//      group hit 32 different banks), slice-by-8 fed by a sliding dword window (two ds_read_b32 +
+//      two v_alignbyte per 8 bytes) and looked up per NIBBLE in 16-entry LDS rows (span.h
+//      kSpanTabNib: 16 conflict-free reads per 8 bytes instead of 8 byte-table reads at ~3-way
+//      conflicts), then 6 shuffle levels of "shift by 2^j chunks" (4 table lookups each,
+//      csrc/core/crc32c.cpp crc32c_span_tables);
 //   3. crc_verdict (thread 0, after a barrier): 2 LDS levels merge the 4 wave CRCs; a RecordBatch
 //      held whole by the segment is compared with its header CRC -- a mismatch stores the segment
 //      index into the batch's host-mapped error word (the driver reads it when the slot is
@@ -74,9 +76,39 @@ __device__ __forceinline__ void stage(const uint8_t* src, uint32_t len, uint8_t*
   }
 }
 
+// The nibble rows in LDS: row r (16 words) at byte r * 256 of a 256-byte aligned 4 KiB array, so a
+// lookup's LDS address is (row base) | (nibble * 4) with the nibble in the address's low byte.
+constexpr int kNibRowWords = 64;
+constexpr int kNibLdsWords = 16 * kNibRowWords;
+using lds_u32 = __attribute__((address_space(3))) const uint32_t;
+
+__device__ __forceinline__ void load_nib_rows(uint32_t* tab, const uint32_t* __restrict__ tabs) {
+  for (int i = int(threadIdx.x); i < int(tk::kSpanTabNibWords); i += kThreads)
+    tab[(i >> 4) * kNibRowWords + (i & 15)] = tabs[tk::kSpanTabNib + i];
+}
+
+// Slice-by-4 of one dword through the nibble rows: byte i of w goes through byte table B - i,
+// i.e. rows 2 (B - i) (low nibble) and 2 (B - i) + 1 (high nibble).  The nibbles of all four
+// bytes are pre-scaled to byte offsets (x4) at once; each lookup is then ONE v_perm_b32 (byte i of
+// the scaled nibbles into the address's low byte, the row base's upper bytes above it) and a
+// ds_read_b32.
+template <int B>
+__device__ __forceinline__ uint32_t nib_dword(uint32_t nbase, uint32_t w) {
+  const uint32_t lo = (w << 2) & 0x3C3C3C3Cu, hi = (w >> 2) & 0x3C3C3C3Cu;
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t sel = 0x07060500u | uint32_t(i);  // byte 0 <- byte i of src1, bytes 1-3 <- src0
+    const uint32_t a0 = __builtin_amdgcn_perm(nbase + uint32_t(2 * (B - i)) * 256u, lo, sel);
+    const uint32_t a1 = __builtin_amdgcn_perm(nbase + uint32_t(2 * (B - i) + 1) * 256u, hi, sel);
+    r ^= *(lds_u32*)uintptr_t(a0) ^ *(lds_u32*)uintptr_t(a1);
+  }
+  return r;
+}
+
 // Stage 2 (every thread, after the barrier that completed the image).  The CRC range is
 // [c0, c1) in LDS bytes: [lo_b + 21, hi_b) for the segment holding a RecordBatch's start, else
-// [lo_b, hi_b).  Each wave's lane 0 leaves the wave's CRC in wcrc[wave]; returns the shift-table
+// [lo_b, hi_b); `tab` is the LDS copy of the nibble rows (load_nib_rows).  Each wave's lane 0 leaves the wave's CRC in wcrc[wave]; returns the shift-table
 // set of the lane size used (for crc_verdict).
 __device__ __forceinline__ const uint32_t* crc_lanes(const uint32_t* __restrict__ b32, const uint32_t* __restrict__ tab,
                                                      const uint32_t* __restrict__ tabs, int32_t lo_b, int32_t hi_b,
@@ -84,6 +116,7 @@ __device__ __forceinline__ const uint32_t* crc_lanes(const uint32_t* __restrict_
   const int t = int(threadIdx.x);
   const uint32_t* shift_set = tabs + tk::kSpanTabShift;
   uint32_t crc = 0;
+  const uint32_t nbase = uint32_t(uintptr_t((lds_u32*)tab));  // the LDS byte address
   const bool first = (flags & tk::kSegCrcFirst) != 0;
   const int32_t c0 = lo_b + (first ? 21 : 0), c1 = hi_b;
   const int32_t L = int32_t(tk::span_lane_bytes(uint32_t(c1 - c0)));
@@ -98,7 +131,7 @@ __device__ __forceinline__ const uint32_t* crc_lanes(const uint32_t* __restrict_
       x &= keep;
       if (first) x ^= keep & ~keep_from(start, c0 + 4);  // the 0xFFFFFFFF initial value
     }
-    crc = tab[768 + (x & 255u)] ^ tab[512 + ((x >> 8) & 255u)] ^ tab[256 + ((x >> 16) & 255u)] ^ tab[x >> 24];
+    crc = nib_dword<3>(nbase, x);
   }
   const int32_t a1 = start + 4;
   const int32_t j0 = a1 >= c0 ? 0 : (c0 - a1) >> 3;  // 8-byte groups wholly below c0 are skipped
@@ -122,9 +155,7 @@ __device__ __forceinline__ const uint32_t* crc_lanes(const uint32_t* __restrict_
         }
       }
       x ^= crc;
-      crc = tab[1792 + (x & 255u)] ^ tab[1536 + ((x >> 8) & 255u)] ^ tab[1280 + ((x >> 16) & 255u)] ^
-            tab[1024 + (x >> 24)] ^ tab[768 + (y & 255u)] ^ tab[512 + ((y >> 8) & 255u)] ^
-            tab[256 + ((y >> 16) & 255u)] ^ tab[y >> 24];
+      crc = nib_dword<7>(nbase, x) ^ nib_dword<3>(nbase, y);
     }
   }
   const int lane = t & 63;
