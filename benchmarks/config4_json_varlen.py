@@ -27,9 +27,8 @@ def main():
     ap.add_argument("--steps", type=int, default=4000)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--batch-size", type=int, default=256)
-    # the config fixes no worker count; the workers' header walk + pre-scan read every text byte once
-    # (27-36 us per 256-record batch): 4 workers 30-36 M rec/s, 8 workers 44.5 M (profiles/r02_s3_final)
-    ap.add_argument("--workers", type=int, default=8)
+    # config 2's worker count; the result line records it (round 2 quoted an 8-worker run as 4)
+    ap.add_argument("--workers", type=int, default=4)
     ap.add_argument("--partitions", type=int, default=8)
     ap.add_argument("--min-len", type=int, default=16)
     ap.add_argument("--max-len", type=int, default=256)
@@ -84,7 +83,7 @@ def main():
         text_bytes = b.partition_stats("json", 0)["log_bytes"] / max(1, b.end_offset("json", 0))
         print(json.dumps({"config": 4, "metric": "JSON records/s to GPU (bf16 padded), per-batch commit",
                           "value": round(rows / el), "ms_per_step": round(el / args.steps * 1e3, 4),
-                          "batch_size": B, "json_parse": args.json_parse, "h2d": args.h2d,
+                          "batch_size": B, "workers": args.workers, "json_parse": args.json_parse, "h2d": args.h2d,
                           "decode": ("device (json_span.hip from the pinned logs)" if dl._json_span()
                                      else args.decode),
                           "timed_s": round(el, 4), "steps": args.steps,
