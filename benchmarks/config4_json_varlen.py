@@ -3,7 +3,8 @@
 
 Records are JSON arrays of 16..256 numbers ("[-12.34, 5.06, ...]", ~1 KiB of text on
 average), as in the reference README's ``json.loads(record.value)`` example.  By default
-(decode='device') the workers only walk the record headers and pre-scan each text in place,
+(decode='device') the workers only walk the record headers (the stage kernel counts each row's
+elements and checks it is "simple"; --json-count host: the workers pre-scan each text in place),
 and the gfx950 kernel (json_span.hip) reads the texts straight from the pinned broker logs,
 verifies the RecordBatch CRCs, parses, pads, stacks and casts.  --decode host: the workers
 frame + copy the text into the ring (json_parse.hip parses it); --json-parse host: the
@@ -36,6 +37,8 @@ def main():
     ap.add_argument("--json-parse", default="auto", choices=["auto", "device", "host"])
     ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy"])
     ap.add_argument("--decode", default="auto", choices=["auto", "device", "host"])
+    ap.add_argument("--json-count", default="auto", choices=["auto", "device", "host"],
+                    help="who counts the elements of device-parsed rows: the stage kernel, or the workers")
     ap.add_argument("--slots-per-worker", type=int, default=None)
     ap.add_argument("--event-every", type=int, default=None)
     ap.add_argument("--prefetch", type=int, default=2)
@@ -59,7 +62,7 @@ def main():
         b.fill("json", per_part, "json_f32", size=args.min_len, max_size=args.max_len, threads=args.partitions)
         fill_s = time.perf_counter() - t
         dl = DeviceLoader(Json.placeholder(), B, num_workers=args.workers, device=args.device, dtype=torch.bfloat16,
-                          json_parse=args.json_parse, h2d=args.h2d, decode=args.decode,
+                          json_parse=args.json_parse, h2d=args.h2d, decode=args.decode, json_count=args.json_count,
                           slots_per_worker=args.slots_per_worker, event_every=args.event_every, prefetch=args.prefetch,
                           worker_init_fn=Json.init_worker("json", bootstrap_servers=url, group_id="cfg4",
                                                           auto_offset_reset="earliest"))
@@ -86,6 +89,7 @@ def main():
                           "batch_size": B, "workers": args.workers, "json_parse": args.json_parse, "h2d": args.h2d,
                           "decode": ("device (json_span.hip from the pinned logs)" if dl._json_span()
                                      else args.decode),
+                          "json_count": "device" if dl._json_count() else "workers",
                           "timed_s": round(el, 4), "steps": args.steps,
                           "avg_record_bytes": round(text_bytes),
                           "last_batch_shape": list(x.shape),

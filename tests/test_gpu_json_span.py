@@ -106,20 +106,75 @@ def test_json_span_matches_json_loads(broker, dtype, bs, rpb, lens, odd, nulls, 
 
     DS = _dataset(JsonArray())
     got, dl = _run(broker, "t", DS, bs, "g-dev", dtype=dtype, num_workers=workers, coalesce=4)
-    assert dl._json_span()
+    assert dl._json_span() and dl._json_count()  # the workers read headers only; the device counts
     exp = _expected(texts, bs, dtype)
     assert len(got) == len(exp)
     for (x, ln), (ex, el) in zip(got, exp):
         assert x.shape == ex.shape and x.dtype == dtype
         assert torch.equal(_bits(x.cpu()), _bits(ex)) and torch.equal(ln.cpu(), el)
     assert broker.committed_offsets("g-dev", "t") == {0: n}
-    # the other two JSON paths deliver the same bits
-    for decode, jp in (("host", "auto"), ("auto", "host")):
-        other, dl2 = _run(broker, "t", DS, bs, f"g-{decode}-{jp}", dtype=dtype, num_workers=workers,
-                          decode=decode, json_parse=jp)
-        assert not dl2._json_span()
+    # the other JSON paths deliver the same bits: workers counting for the device parse, workers
+    # framing + copying the text, workers parsing
+    for decode, jp, jc in (("auto", "auto", "host"), ("host", "auto", "auto"), ("auto", "host", "auto")):
+        other, dl2 = _run(broker, "t", DS, bs, f"g-{decode}-{jp}-{jc}", dtype=dtype, num_workers=workers,
+                          decode=decode, json_parse=jp, json_count=jc)
+        assert dl2._json_span() == (jc == "host") and not dl2._json_count()
+        assert len(other) == len(got)
         for (x, ln), (y, lm) in zip(got, other):
             assert torch.equal(_bits(x), _bits(y)) and torch.equal(ln, lm)
+
+
+_EDGE_TEXTS = [b"[1,2,3]", b"  [4, 5]  ", b"[]", b"[ ]", b"\n[7]\t", b"[1.5e3, 2]", b"[NaN, 1, Infinity]",
+               b"[12345678901234567, 1]", b"[1234567890123456]", b"[-0.0, 0.5, -12.25]", b" [ 3 , 4 ] ",
+               b"[1e-7]", b"[" + b",".join(b"%d" % i for i in range(300)) + b"]", b"[0.1,0.2,0.30000000000000004]"]
+
+
+@pytest.mark.parametrize("pad_to,pad_multiple,dtype,bs", [(None, 8, torch.float32, 16), (None, 1, torch.bfloat16, 7),
+                                                          (320, 8, torch.float32, 16)])
+def test_json_device_count_edge_rows(broker, pad_to, pad_multiple, dtype, bs):
+    """Device-counted rows (tuning.json_count): trimmed whitespace, empty arrays, exponents / NaN /
+    Infinity / 17-digit tokens (not simple: parsed on the host at delivery), a 16-digit token (simple),
+    widths from the device max (or a fixed pad_to) -- bit for bit json.loads + torch casts."""
+    from torchkafka_amd import JsonArray
+
+    rng = random.Random(bs)
+    texts = [_EDGE_TEXTS[rng.randrange(len(_EDGE_TEXTS))] for _ in range(300)]
+    _produce(broker, "e", 1, lambda p: texts, 11)
+    DS = _dataset(JsonArray())
+    kw = dict(pad_multiple=pad_multiple, return_mask=True, pad_value=-3.0)
+    if pad_to is not None:
+        kw["pad_to"] = pad_to
+    got, dl = _run(broker, "e", DS, bs, "g", dtype=dtype, num_workers=1, **kw)
+    assert dl._json_count()
+    ref, _ = _run(broker, "e", DS, bs, "g-host", dtype=dtype, num_workers=1, json_count="host", **kw)
+    exp = _expected(texts, bs, dtype, pad=-3.0, pad_multiple=pad_multiple)
+    assert len(got) == len(exp) == len(ref)
+    for (x, ln, m), (ex, el), (y, lm, my) in zip(got, exp, ref):
+        if pad_to is not None:
+            ex = torch.nn.functional.pad(ex.float(), (0, pad_to - ex.shape[1]), value=-3.0).to(dtype)
+        assert x.shape == ex.shape and torch.equal(_bits(x.cpu()), _bits(ex)) and torch.equal(ln.cpu(), el)
+        assert torch.equal(_bits(x), _bits(y)) and torch.equal(m, my) and torch.equal(ln, lm)
+        assert torch.equal(m.cpu(), torch.arange(x.shape[1])[None, :] < el[:, None])
+    assert broker.committed_offsets("g", "e") == {0: 300}
+
+
+@pytest.mark.parametrize("bad", [b"[1,,2]", b"5", b"[1, \"a\"]", b"[,]", b"{}"])
+def test_json_device_count_malformed_row_raises_before_commit(broker, bad):
+    from torchkafka_amd import DeviceLoader, JsonArray, auto_commit
+    from torchkafka_amd.client.errors import CorruptRecordException
+
+    texts = [b"[1, 2]"] * 100 + [bad] + [b"[3]"] * 60
+    _produce(broker, "m", 1, lambda p: texts, 16)
+    DS = _dataset(JsonArray())
+    dl = DeviceLoader(DS.placeholder(), 32, num_workers=1, device="cuda:0",
+                      worker_init_fn=DS.init_worker("m", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    assert dl._json_count()
+    with pytest.raises(CorruptRecordException, match="not a flat numeric JSON array"):
+        for _x in auto_commit(dl):
+            torch.cuda.synchronize()
+    committed = broker.committed_offsets("g", "m").get(0)
+    assert committed is None or committed <= 96
 
 
 def test_json_span_filters_pad_and_mask(broker):

@@ -107,7 +107,7 @@ def _decode_jspan(broker, info, pay, segs, trunc):
             p0, tl = int(tab[r]["pos"]), int(tab[r]["tlen"])
             assert pos <= p0 and p0 + tl <= pos + ln, "a row text is cut by its segment"
             vals = json.loads(data[p0 - pos:p0 + tl - pos])
-            assert len(vals) == tab[r]["count"]
+            assert len(vals) == tab[r]["count"] or tab[r]["count"] == c.JSON_COUNT_ON_DEVICE
             k = len(vals) if trunc < 0 else min(len(vals), trunc)
             assert got[r] is None, "a row is listed by two segments"
             got[r] = np.array([float(v) for v in vals[:k]], dtype=np.float32)
@@ -167,6 +167,46 @@ def test_json_span_filters_like_host(broker):
             got = _decode_jspan(broker, si, sp, segs, si["trunc_len"])
             for a, b in zip(got, _host_rows(hi, hp)):
                 np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("bs,rpb,odd,nulls,lens,max_len", [
+    (100, 64, 5, 0, (1, 40), -1),
+    (256, 7, 0, 9, (0, 30), 12),      # tombstones, empty arrays, truncation
+    (32, 512, 3, 0, (200, 600), -1),  # RecordBatches > 128 KiB
+])
+def test_json_span_device_count_walks_headers_only(broker, bs, rpb, odd, nulls, lens, max_len):
+    """tuning.json_count (span mode SPAN_JSON_DEV_COUNT): the worker reads no text -- every row is
+    left to the device (count JSON_COUNT_ON_DEVICE, its text in the log), the slot is flagged
+    SLOT_DEV_COUNT and max_row_len is the text-length bound -- over exactly the rows and
+    watermarks of the host packer, whose values the texts still decode to."""
+    c = core()
+    rnd = random.Random(bs * 13 + rpb)
+    n = max(4 * bs, 600)
+    vals = [_rows(rnd, n, *lens, odd_every=odd, nulls_every=nulls) for _ in range(2)]
+    host = _fill(broker, False, bs, vals, rpb, max_len=max_len)
+    dev = _fill(broker, c.SPAN_JSON_DEV_COUNT, bs, vals, rpb, max_len=max_len)
+    assert len(host) == len(dev)
+    for (hr, hi, hw, hp, _), (sr, si, sw, sp, segs) in zip(host, dev):
+        assert hr == sr and hw == sw
+        if sr == 0:
+            continue
+        assert si["flags"] & c.SLOT_DEV_COUNT and si["kind"] == c.PACK_JSON_SPAN
+        tab = np.frombuffer(sp[:16 * sr], dtype=np.dtype([("pos", "<u8"), ("tlen", "<i4"), ("count", "<i4")]))
+        assert (tab["count"] == c.JSON_COUNT_ON_DEVICE).all() and (tab["tlen"] >= 0).all()
+        bound = tab["tlen"] // 2 if max_len < 0 else np.minimum(tab["tlen"] // 2, max_len)
+        assert si["max_row_len"] == int(bound.max()) >= hi["max_row_len"]
+        got = _decode_jspan(broker, si, sp, segs, si["trunc_len"])
+        for a, b in zip(got, _host_rows(hi, hp)):
+            np.testing.assert_array_equal(a, b)
+
+
+def test_json_span_device_count_refuses_dropping_filters(broker):
+    c = core()
+    vals = [[b"[1,2,3]"] * 50]
+    for min_len, max_len, trunc in [(2, -1, True), (0, 2, False)]:
+        with pytest.raises(ValueError, match="cannot drop rows"):
+            _fill(broker, c.SPAN_JSON_DEV_COUNT, 16, vals, 8, min_len=min_len, max_len=max_len, truncate=trunc,
+                  slots=1)
 
 
 def test_json_span_without_crc_checks_covers_only_texts(broker):

@@ -47,6 +47,8 @@ for s in ${STEPS:-smoke benchdrv}; do
     benchlockr) run bench_lock_rccl 600 python bench.py --lockstep rccl --steps 200 --warmup 50 --steady-steps 8000 --extra-blocks "" ;;
     config4) run config4_w4 300 python benchmarks/config4_json_varlen.py --workers 4 ;;
     config4w8) run config4_w8 300 python benchmarks/config4_json_varlen.py --workers 8 ;;
+    config4host) run config4_w4_hostcount 300 python benchmarks/config4_json_varlen.py --workers 4 --json-count host ;;
+    config4dma) run config4_w4_dma 300 python benchmarks/config4_json_varlen.py --workers 4 --h2d dma ;;
     config5) run config5 300 python benchmarks/config5_large_messages.py ;;
     bridge) run bridge_e2e 600 python benchmarks/bridge_e2e.py ;;
     profbench) prof profbench 300 --kernel-trace --stats --output-format csv -d "$OUT/profbench" -o run -- python3 "$R/bench.py" --steps 1000 --steady-steps 4000 --extra-blocks "" --bridge-steps 0 ;;

@@ -88,6 +88,11 @@ class Tuning:
             tools/mirror_probe.sh, tools/mirror_probe2.sh.
         group_mib: device-decode groups stop growing at this many MiB of log bytes (1..1024): a
             group's batches become committable together, so large batches form small groups.
+        json_count: JsonArray rows parsed on the device from the logs: who counts their elements.
+            'auto' / 'device': the gfx950 stage kernel, while it stages the text (the workers read
+            only record headers; the batch width is a device max); 'host': the workers pre-scan
+            every text.  Filters that drop rows (min_len > 0, max_len without truncate) need the
+            workers to count, so 'auto' leaves those to them.
     """
 
     slots_per_worker: Optional[int] = None
@@ -106,6 +111,7 @@ class Tuning:
     mirror_chunk_mib: int = 8
     mirror_chunks: int = 6
     group_mib: int = 16
+    json_count: str = "auto"
 
     def __post_init__(self):
         # environment defaults for fields left at None
@@ -135,6 +141,7 @@ class Tuning:
         _check(1 <= int(self.mirror_chunk_mib) <= 1024, "mirror_chunk_mib must be in [1, 1024]")
         _check(2 <= int(self.mirror_chunks) <= 64, "mirror_chunks must be in [2, 64]")
         _check(1 <= int(self.group_mib) <= 1024, "group_mib must be in [1, 1024]")
+        _check(self.json_count in ("auto", "device", "host"), "json_count must be 'auto', 'device' or 'host'")
 
 
 _CHOICES = {

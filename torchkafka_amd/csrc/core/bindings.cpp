@@ -784,7 +784,7 @@ PYBIND11_MODULE(_tkcore, m) {
           "fill_slot",
           [](PyFetcher& f, py::object ring_obj, uint32_t gslot, int kind, int elem_size, int64_t row_elems,
              int64_t min_len, int64_t max_len, bool truncate, bool skip_bad, int64_t batch_rows, int64_t timeout_ms,
-             bool gather, bool span, int extras, int key_enc, int64_t key_default) {
+             bool gather, int span, int extras, int key_enc, int64_t key_default) {
             PyRing& ring = ring_obj.cast<PyRing&>();
             PackSpec s;
             s.gather = gather;
@@ -809,7 +809,7 @@ PYBIND11_MODULE(_tkcore, m) {
           },
           py::arg("ring"), py::arg("gslot"), py::arg("kind"), py::arg("elem_size"), py::arg("row_elems"),
           py::arg("min_len"), py::arg("max_len"), py::arg("truncate"), py::arg("skip_bad"), py::arg("batch_rows"),
-          py::arg("timeout_ms"), py::arg("gather") = false, py::arg("span") = false, py::arg("extras") = 0,
+          py::arg("timeout_ms"), py::arg("gather") = false, py::arg("span") = 0, py::arg("extras") = 0,
           py::arg("key_enc") = 0, py::arg("key_default") = -1);
   m.def("key_int64", [](py::object key, int enc, int64_t dflt) {
     if (key.is_none()) return key_int64(nullptr, -1, enc, dflt);
@@ -1034,5 +1034,8 @@ PYBIND11_MODULE(_tkcore, m) {
   m.attr("JSON_SPAN_MAX_SEG_ROWS") = kJsonSpanMaxSegRows;
   m.attr("JSON_SPAN_ROW_MAX") = kJsonSpanRowMax;
   m.attr("SEG_HOST_ROWS") = int(kSegHostRows);
+  m.attr("SPAN_JSON_DEV_COUNT") = kSpanJsonDevCount;
+  m.attr("JSON_COUNT_ON_DEVICE") = kJsonCountOnDevice;
+  m.attr("SLOT_DEV_COUNT") = int(kSlotDevCount);
   m.attr("SLOT_HEADER_BYTES") = kSlotHeaderBytes;
 }

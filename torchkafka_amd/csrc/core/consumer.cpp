@@ -695,6 +695,11 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
   const bool gather = spec.kind == kPackFixed && spec.gather;
   const bool span = spec.kind == kPackFixed && spec.span && !gather;
   const bool jspan = spec.kind == kPackJsonText && spec.span;  // JSON text parsed on the device from the logs
+  // ... and counted there: the walk reads headers only (span.h kJsonCountOnDevice)
+  const bool jcount = jspan && spec.span == kSpanJsonDevCount;
+  if (jcount && (spec.min_len > 0 || (spec.max_len >= 0 && !spec.truncate) || spec.skip_bad))
+    throw std::invalid_argument("device element counting cannot drop rows (min_len, max_len without truncate, "
+                                "skip_bad): the worker must count them");
   const bool vspan = spec.kind == kPackVarlen && spec.span;    // var-len values decoded on the device from the logs
   const bool rspan = jspan || vspan;                           // rows + segments slot layout (span.h)
   h->n_rows = 0;
@@ -879,6 +884,25 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
       const size_t tn = size_t(r.value_len);
       JsonSpanRow d;
       const uint64_t at_log = uint64_t(r.value - log_of[cur_part]);
+      if (jcount && tn <= kJsonSpanRowMax) {
+        // the header gave the text's place and length; the device counts its elements
+        if (uint64_t(r.value_len) < kWalkStreamMax) {  // the var-len walk's software prefetch stream
+          const uint8_t* want = r.value + r.value_len + kWalkAhead;
+          if (pf_frontier < r.value || pf_frontier > want + kWalkAhead) pf_frontier = r.value;
+          for (; pf_frontier < want; pf_frontier += 64) __builtin_prefetch(pf_frontier);
+        }
+        d.pos = at_log;
+        d.tlen = int32_t(tn);
+        d.count = kJsonCountOnDevice;
+        srows[rows] = d;
+        int64_t bound = json_count_bound(tn);
+        if (spec.max_len >= 0 && bound > spec.max_len) bound = spec.max_len;
+        elems += bound;
+        max_len = std::max(max_len, bound);
+        touch(r);
+        rbs.back().row_last = ++rows;
+        return rows == B ? kTakeStop : kTake;
+      }
       int64_t cnt = tn <= kJsonSpanRowMax ? json_scan_inplace(txt, tn, size_t(log_cap[cur_part] - at_log)) : -1;
       uint64_t at = vused;
       if (cnt >= 0) {
@@ -1112,6 +1136,7 @@ FillOutcome fill_slot(Fetcher& f, Ring& ring, uint32_t g, const PackSpec& spec, 
     h->max_row_len = max_len;
     h->total_elems = elems;
     h->trunc_len = spec.max_len >= 0 && spec.max_len < INT32_MAX ? int32_t(spec.max_len) : -1;
+    if (jcount) h->flags |= kSlotDevCount;
     h->n_scanned = scanned;
     put_extras();
     out.rows = rows;

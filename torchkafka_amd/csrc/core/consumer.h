@@ -127,7 +127,8 @@ struct PackSpec {
   int skip_bad = 0;         // malformed rows: 1 = skip, 0 = raise
   int gather = 0;           // fixed-width: emit log locations (kPackGatherFixed) instead of values
   int span = 0;             // fixed-width / JSON text: emit log ranges + row positions (kPackRecordSpan /
-                            // kPackJsonSpan) instead of values; CRC and decode on the device
+                            // kPackJsonSpan) instead of values; CRC and decode on the device;
+                            // kSpanJsonDevCount: JSON elements counted on the device too (span.h)
   // Record fields delivered beside the value, one int64 per row each (SlotHeader::extras_*):
   // kExtraKey = the record key as an integer (key_enc), kExtraTimestamp = its timestamp (ms).
   int extras = 0;

@@ -27,7 +27,9 @@ constexpr int kMaxSlotParts = 256;
 constexpr size_t kSlotHeaderBytes = 16384;
 
 enum SlotState : uint32_t { kSlotFree = 0, kSlotFilling = 1, kSlotReady = 2, kSlotInflight = 3 };
-enum SlotFlags : uint32_t { kSlotEOS = 1, kSlotError = 2 };
+// kSlotDevCount (kPackJsonSpan): the worker walked only the headers; the device counts the elements
+// of the rows whose JsonSpanRow::count is kJsonCountOnDevice, and max_row_len is an upper bound.
+enum SlotFlags : uint32_t { kSlotEOS = 1, kSlotError = 2, kSlotDevCount = 4 };
 
 struct Watermark {
   uint32_t pidx;

@@ -89,6 +89,16 @@ static_assert(sizeof(JsonSpanRow) == 16, "JsonSpanRow layout");
 // and the longest text parsed on the device (a longer row is parsed by the worker).
 constexpr uint32_t kJsonSpanMaxSegRows = 1024;
 constexpr uint32_t kJsonSpanRowMax = 64u << 10;
+// Device counting (PackSpec::span == kSpanJsonDevCount, the slot flagged kSlotDevCount): the worker
+// reads only the record headers -- no byte of text -- and leaves JsonSpanRow::count at
+// kJsonCountOnDevice.  json_span.hip then runs json_scan_simple's rules on the staged text (trim,
+// '[' ... ']' framing, interior alphabet, token runs <= 16, element count), the batch's padded width
+// comes from a device max over its rows (json_parse.hip), and a row that is not simple is parsed on
+// the host when its batch is delivered (MainDriver::json_host_rows).  Until then the slot's
+// max_row_len is only a bound: json_count_bound(text bytes) elements per row.
+constexpr int32_t kJsonCountOnDevice = -2;
+constexpr int kSpanJsonDevCount = 2;
+inline constexpr int64_t json_count_bound(uint64_t text_bytes) { return int64_t(text_bytes / 2); }
 
 // ---- kPackVarSpan: VarLen rows (raw little-endian elements, e.g. int32 token ids) decoded on the
 // device from the logs.  The same slot layout as kPackJsonSpan, with JsonSpanRow::tlen the value's

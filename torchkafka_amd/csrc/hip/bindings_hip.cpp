@@ -230,10 +230,25 @@ PYBIND11_MODULE(_tkhip, m) {
       .def_property_readonly("last_extras", [](MainDriver& d) { return int(d.last.extras_n); })
       .def("collate_varlen_last",
            [](MainDriver& d, uintptr_t stream, int dst_dt, uintptr_t out, int64_t L, double pad, uintptr_t lengths,
-              uintptr_t mask) {
+              uintptr_t mask, int64_t mult) -> int64_t {
+             // -> the batch's width: L, or for a device-counted JSON batch (kSlotDevCount, L its
+             // capacity) the width the parse kernel chose; its first rows * width elements hold the batch
+             py::gil_scoped_release nogil;
+             d.set_json_mult(mult);
              d.collate_varlen(d.last, stream_of(stream), dst_dt, ptr<void>(out), L, pad, ptr<int64_t>(lengths),
                               ptr<uint8_t>(mask));
-           })
+             if (!(d.last.flags & tk::kSlotDevCount) || d.last.n_rows == 0) return L;
+             SlotView v = d.last;
+             v.perr = d.last_perr();
+             int64_t n_host = 0;
+             const int64_t w = d.json_width(v, &n_host);
+             if (n_host > 0)
+               d.json_host_rows(v, ptr<void>(out), w, dst_dt, pad, ptr<int64_t>(lengths), ptr<uint8_t>(mask),
+                                stream_of(stream));
+             return w;
+           },
+           py::arg("stream"), py::arg("dst_dt"), py::arg("out"), py::arg("L"), py::arg("pad"), py::arg("lengths"),
+           py::arg("mask"), py::arg("mult") = 1)
       .def("copy_payload_last",
            [](MainDriver& d, uintptr_t stream, uintptr_t dst) { d.copy_payload(d.last, stream_of(stream), ptr<void>(dst)); })
       .def_property_readonly("last_slot", [](MainDriver& d) { return int64_t(d.last.g); })

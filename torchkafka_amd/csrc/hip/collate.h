@@ -58,6 +58,12 @@ struct JsonGroupArgs {
   // parse error then never overwrites an earlier verdict (the stage kernel's CRC failure).
   uint64_t vals_cap[kMaxGroup];
   int32_t err_tag;
+  // Device-counted batches (kSlotDevCount): L[k] is only the capacity of out/mask; the width is
+  // min(L[k], ctr[k][0] rounded up to `mult`) (mult 0: L[k], a fixed pad_to width), and the batch's first block stores {width, rows
+  // left to the host, 1} into the host-mapped info[k] (MainDriver::json_width).  nullptr: L[k].
+  const int32_t* ctr[kMaxGroup];
+  int32_t* info[kMaxGroup];
+  int32_t mult;
 };
 void launch_json_group(JsonGroupArgs& a, int dst_dt, hipStream_t stream);
 

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 namespace {
 const bool g_trace = [] {
@@ -76,6 +77,8 @@ MainDriver::~MainDriver() {
     if (std::get<0>(f)) hipEventDestroy(std::get<0>(f));
   if (perr_host_ || part_host_) hipDeviceSynchronize();  // no kernel may still write a status word
   if (perr_host_) hipHostFree(perr_host_);
+  if (jinfo_host_) hipHostFree(jinfo_host_);
+  if (patch_dev_) hipFree(patch_dev_);
   if (part_host_) hipHostFree(part_host_);
   for (auto e : event_pool_) hipEventDestroy(e);
 }
@@ -107,6 +110,10 @@ void MainDriver::release_completed_impl() {
     for (; k <= e; ++k, ++released_) {
       const int64_t pe = handed_[k].perr;
       if (pe >= 0) {
+        // a device-counted JSON batch with rows left to the host: parse them while the slot (their
+        // row table) is still held, in case the batch is delivered after this release
+        if (handed_[k].span && __atomic_load_n(jinfo_host_ + pe * 4 + 1, __ATOMIC_ACQUIRE) > 0)
+          json_parse_host_rows(handed_[k].g, pe);
         if (handed_[k].span) check_span(handed_[k].g, pe);  // reads the slot: before its release
         perr_state_[size_t(pe)] = __atomic_load_n(perr_host_ + pe, __ATOMIC_ACQUIRE) < 0 ? 1 : 2;
       }
@@ -591,6 +598,14 @@ void MainDriver::ensure_status() {
   if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) throw std::runtime_error("driver: hipHostGetDevicePointer failed");
   perr_dev_ = static_cast<int32_t*>(d);
   if (perr_state_.empty()) perr_state_.assign(size_t(kErrWords), 1);
+  if (hipHostMalloc(&h, kErrWords * 4 * sizeof(int32_t), hipHostMallocMapped) != hipSuccess)
+    throw std::runtime_error("driver: hipHostMalloc of the JSON width words failed");
+  jinfo_host_ = static_cast<int32_t*>(h);
+  std::memset(jinfo_host_, 0, kErrWords * 4 * sizeof(int32_t));
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) throw std::runtime_error("driver: hipHostGetDevicePointer failed");
+  jinfo_dev_ = static_cast<int32_t*>(d);
+  jrows_.assign(size_t(kErrWords), {});
+  jparsed_.assign(size_t(kErrWords), 0);
 }
 
 int64_t MainDriver::next_err_word() {
@@ -601,6 +616,10 @@ int64_t MainDriver::next_err_word() {
   if (perr_state_[size_t(idx)] == 0)
     throw std::runtime_error("driver: more than 4096 device-checked batches awaiting their kernels");
   perr_host_[idx] = -1;
+  jinfo_host_[idx * 4 + 1] = 0;
+  __atomic_store_n(jinfo_host_ + idx * 4 + 2, 0, __ATOMIC_RELEASE);
+  jrows_[size_t(idx)].clear();
+  jparsed_[size_t(idx)] = 0;
   perr_state_[size_t(idx)] = 0;
   if (!perr_msg_.empty()) perr_msg_[size_t(idx)].clear();
   return idx;
@@ -737,18 +756,30 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
     batch_bytes[k] = b;
     total += b;
   }
-  const uint64_t base = stage_alloc(total);
+  // device-counted batches: two zeroed counter words each at the front of the group's region
+  bool devc = false;
+  for (int k = 0; k < n; ++k) devc = devc || (views[k]->flags & tk::kSlotDevCount) != 0;
+  const uint64_t ctr_bytes = devc ? kA : 0;
+  const uint64_t base = stage_alloc(total + ctr_bytes);
+  if (devc && hipMemsetAsync(stage_dev_ + base, 0, ctr_bytes, stream) != hipSuccess)
+    throw std::runtime_error("driver: hipMemsetAsync of the JSON counters failed");
   JsonStageLaunch a{};
   a.burst = span_burst_;
   JsonGroupArgs ga{};
   ga.n = n;
   ga.pad = float(pad);
   ga.err_tag = tk::kSpanParseErrBit;
-  uint64_t off = base;
+  ga.mult = json_mult_;
+  uint64_t off = base + ctr_bytes;
   for (int k = 0; k < n; ++k) {
     const SlotView& v = *views[k];
     perrs[k] = next_err_word();
     JsonStageBatch& b = a.b[k];
+    if (v.flags & tk::kSlotDevCount) {
+      b.ctr = reinterpret_cast<int32_t*>(stage_dev_ + base) + 4 * k;
+      ga.ctr[k] = b.ctr;
+      ga.info[k] = jinfo_dev_ + perrs[k] * 4;
+    }
     b.desc = reinterpret_cast<JsonRowDesc*>(stage_dev_ + off);
     const uint64_t dbytes = up(uint64_t(v.n_rows) * sizeof(JsonRowDesc), kA);
     b.stage = stage_dev_ + off + dbytes;
@@ -896,6 +927,103 @@ const uint8_t* MainDriver::seg_src(const tk::SpanSeg& sg) {
 void MainDriver::enable_mirror(uint64_t chunk_bytes, int chunks_per_partition) {
   if (!broker_) throw std::runtime_error("DeviceLoader h2d='dma' device decode needs the synthetic broker");
   mirror_ = std::make_unique<LogMirror>(eng_->device(), chunk_bytes, chunks_per_partition);
+}
+
+int64_t MainDriver::json_width(const SlotView& v, int64_t* n_host) {
+  *n_host = 0;
+  if (v.perr < 0 || !jinfo_host_) throw std::logic_error("driver: json_width of a batch without a parse launch");
+  const int32_t* info = jinfo_host_ + v.perr * 4;
+  // the parse kernel's first block of the batch reports the width: usually long done (the batch was
+  // parsed ahead), else within one kernel's latency
+  const int64_t t0 = tk::now_ns();
+  for (int spin = 0; __atomic_load_n(info + 2, __ATOMIC_ACQUIRE) == 0; ++spin) {
+    if (spin < 4096) {
+      tk::cpu_relax();
+      continue;
+    }
+    if (tk::now_ns() - t0 > 60'000'000'000LL)
+      throw std::runtime_error("driver: the JSON parse kernel did not report a batch width within 60 s");
+    timespec ts{0, 20000};
+    nanosleep(&ts, nullptr);
+  }
+  *n_host = __atomic_load_n(info + 1, __ATOMIC_ACQUIRE);
+  return __atomic_load_n(info, __ATOMIC_ACQUIRE);
+}
+
+void MainDriver::json_parse_host_rows(int64_t g, int64_t pe) {
+  if (jparsed_[size_t(pe)]) return;
+  jparsed_[size_t(pe)] = 1;
+  // the rows the device found not simple are the device-counted rows json_scan_simple rejects;
+  // parse them as the worker would have (parse_json_f32: Python's float() of each number)
+  const tk::SlotHeader* h = ring_->slot(uint32_t(g));
+  const uint8_t* pay = ring_->payload(uint32_t(g));
+  const auto* rows = reinterpret_cast<const tk::JsonSpanRow*>(pay);
+  const auto* sg = reinterpret_cast<const tk::SpanSeg*>(pay + h->values_offset);
+  auto& out = jrows_[size_t(pe)];
+  for (uint32_t i = 0; i < h->n_segs; ++i) {
+    if (sg[i].flags & tk::kSegHostRows) continue;
+    const uint8_t* log = broker_->log_base(sg[i].pidx);
+    for (uint32_t r = sg[i].row_begin; r < sg[i].row_end && r < h->n_rows; ++r) {
+      const tk::JsonSpanRow& d = rows[r];
+      if (d.count != tk::kJsonCountOnDevice || d.tlen < 0) continue;
+      const char* txt = reinterpret_cast<const char*>(log + d.pos);
+      if (tk::json_scan_simple(txt, size_t(d.tlen)) >= 0) continue;  // parsed on the device
+      HostRow hr;
+      hr.row = int64_t(r);
+      hr.vals.resize(size_t(tk::json_count_bound(uint64_t(d.tlen))) + 1);
+      const int64_t c = tk::parse_json_f32(txt, size_t(d.tlen), hr.vals.data(), int64_t(hr.vals.size()));
+      if (c < 0) {
+        // not a flat numeric JSON array: the batch is never committed (as a device parse error)
+        int32_t expect = -1;
+        __atomic_compare_exchange_n(perr_host_ + pe, &expect, tk::kSpanParseErrBit | int32_t(r), false,
+                                    __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
+        if (perr_state_[size_t(pe)] == 1) perr_state_[size_t(pe)] = 2;
+        if (pe < int64_t(perr_msg_.size()) && perr_msg_[size_t(pe)].empty())
+          perr_msg_[size_t(pe)] = "batch row " + std::to_string(r) + " is not a flat numeric JSON array";
+        continue;
+      }
+      hr.count = int32_t(c);
+      hr.vals.resize(size_t(c));
+      out.push_back(std::move(hr));
+    }
+  }
+}
+
+void MainDriver::json_host_rows(const SlotView& v, void* out, int64_t L, int dst_dt, double pad, int64_t* lengths,
+                                uint8_t* mask, hipStream_t stream) {
+  if (v.perr < 0) return;
+  if (!jparsed_[size_t(v.perr)]) json_parse_host_rows(v.g, v.perr);  // the slot is still held
+  const int dsz = dtype_size(dst_dt);
+  constexpr size_t kVals = 256;  // the values start 256 bytes after the row descriptor
+  for (const HostRow& hr : jrows_[size_t(v.perr)]) {
+    int64_t n_out = hr.count;
+    if (v.trunc_len >= 0 && n_out > v.trunc_len) n_out = v.trunc_len;
+    if (n_out > L) {
+      // wider than the device count made the batch: cannot happen for a flat numeric array
+      int32_t expect = -1;
+      __atomic_compare_exchange_n(perr_host_ + v.perr, &expect, tk::kSpanParseErrBit | int32_t(hr.row), false,
+                                  __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
+      if (perr_state_[size_t(v.perr)] == 1) perr_state_[size_t(v.perr)] = 2;
+      continue;
+    }
+    const size_t need = kVals + hr.vals.size() * sizeof(float) + 16;
+    if (need > patch_cap_) {
+      if (patch_dev_ && hipFree(patch_dev_) != hipSuccess) throw std::runtime_error("driver: hipFree failed");
+      patch_dev_ = nullptr;
+      patch_cap_ = std::max<size_t>(need, size_t(1) << 20);
+      if (hipMalloc(&patch_dev_, patch_cap_) != hipSuccess) throw std::runtime_error("driver: hipMalloc failed");
+    }
+    const tk::JsonRowDesc d{0, -1, hr.count, int32_t(n_out)};
+    if (hipMemcpyAsync(patch_dev_, &d, sizeof(d), hipMemcpyHostToDevice, stream) != hipSuccess ||
+        (!hr.vals.empty() && hipMemcpyAsync(patch_dev_ + kVals, hr.vals.data(), hr.vals.size() * sizeof(float),
+                                            hipMemcpyHostToDevice, stream) != hipSuccess))
+      throw std::runtime_error("driver: hipMemcpyAsync of a host-parsed JSON row failed");
+    launch_json_rows(reinterpret_cast<const tk::JsonRowDesc*>(patch_dev_), patch_dev_ + kVals,
+                     static_cast<uint8_t*>(out) + hr.row * L * dsz, dst_dt, 1, L, pad, lengths ? lengths + hr.row : nullptr,
+                     mask ? mask + hr.row * L : nullptr, nullptr, stream);
+    // the descriptor and values are read before the next row's copies overwrite them
+    if (hipStreamSynchronize(stream) != hipSuccess) throw std::runtime_error("driver: hipStreamSynchronize failed");
+  }
 }
 
 void MainDriver::span_group_handed(const int* slots, int n, hipStream_t ks, const int64_t* perrs,

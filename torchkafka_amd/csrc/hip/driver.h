@@ -157,6 +157,19 @@ class MainDriver {
   void ahead_launch_json(int dst_dt, double pad, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
                          uint8_t* const* masks, std::vector<std::shared_ptr<void>>&& handles);
   void set_ahead_depth(int n) { ahead_depth_ = n < 0 ? 0 : n; }
+  // Device-counted JSON batches (kSlotDevCount, span.h kJsonCountOnDevice).  Their outputs are
+  // allocated at the worker's bound (max_row_len); the parse kernel picks the real width from the
+  // device count of the longest row, rounded up to `mult` (0: the allocated width stays, pad_to).
+  void set_json_mult(int64_t mult) { json_mult_ = mult < 0 ? 0 : int32_t(mult); }
+  // json_width: the width of delivered batch v (waits for its parse kernel to report it) and, in
+  // *n_host, the rows that were not simple.  json_host_rows: parses those rows on the host (from the
+  // pinned logs, when the batch is delivered or its slot released, whichever comes first) and
+  // writes them into the batch's outputs on `stream`, which it then synchronizes.
+  int64_t json_width(const SlotView& v, int64_t* n_host);
+  void json_host_rows(const SlotView& v, void* out, int64_t L, int dst_dt, double pad, int64_t* lengths,
+                      uint8_t* mask, hipStream_t stream);
+  hipStream_t last_stream() const { return last_stream_; }
+  int64_t last_perr() const { return last_perr_; }
   // LDS-DMA loads a wave of the span decode kernel keeps in flight before it waits (0 = all;
   // default 1; TORCHKAFKA_SPAN_BURST)
   void set_span_burst(int n) { span_burst_ = n < 0 ? 0 : n > 8 ? 8 : n; }
@@ -305,6 +318,21 @@ class MainDriver {
   std::vector<std::string> perr_msg_;      // span decode: the message of a bad batch, by error word
   int32_t* perr_host_ = nullptr;  // hipHostMalloc'ed, device-mapped error words (one per JSON launch)
   int32_t* perr_dev_ = nullptr;
+  // Device-counted JSON: per error word {width, rows left to the host, done} (host-mapped, written
+  // by the parse kernel), and the host-parsed values of those rows (json_host_rows).
+  struct HostRow {
+    int64_t row;
+    int32_t count;
+    std::vector<float> vals;
+  };
+  int32_t* jinfo_host_ = nullptr;
+  int32_t* jinfo_dev_ = nullptr;
+  int32_t json_mult_ = 1;
+  std::vector<std::vector<HostRow>> jrows_;
+  std::vector<uint8_t> jparsed_;  // per error word: its host rows were parsed (jrows_)
+  void json_parse_host_rows(int64_t g, int64_t pe);
+  uint8_t* patch_dev_ = nullptr;
+  size_t patch_cap_ = 0;
   uint64_t perr_seq_ = 0;
   int64_t last_perr_ = -1, delivered_perr_ = -1;
   std::string parse_error_;

@@ -36,6 +36,7 @@
 #include "collate.h"
 #include "dtypes.h"
 #include "json_token.h"
+#include "span.h"
 
 namespace tkh {
 
@@ -67,7 +68,24 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
   const JsonRowDesc* __restrict__ rows = a.rows[bk];
   const uint8_t* __restrict__ vals = a.vals[bk];
   D* __restrict__ out = static_cast<D*>(a.out[bk]);
-  const int64_t L = a.L[bk];
+  int64_t L = a.L[bk];
+  if (a.ctr[bk]) {
+    // device-counted batch: its width is the longest kept row (rounded up to the pad multiple),
+    // within the capacity the host allocated; the first block reports it (and the rows left to
+    // the host) through the host-mapped info words
+    if (a.mult > 0) {  // 0: the allocated width stays (pad_to)
+      int64_t w = a.ctr[bk][0] < 0 ? 0 : a.ctr[bk][0];
+      if (a.mult > 1) w = (w + a.mult - 1) / a.mult * a.mult;
+      if (w < L) L = w;
+    }
+    if (int64_t(blockIdx.x) == a.row_base[bk] && threadIdx.x == 0 && a.info[bk]) {
+      volatile int32_t* info = a.info[bk];
+      info[0] = int32_t(L);
+      info[1] = a.ctr[bk][1];
+      __threadfence_system();
+      info[2] = 1;
+    }
+  }
   const float pad = a.pad;
   int64_t* __restrict__ lengths = a.lengths[bk];
   uint8_t* __restrict__ mask = a.mask[bk];
@@ -77,7 +95,9 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
   bool bad = false;  // block-uniform: only read after a barrier
   if (a.vals_cap[bk] > 0) {
     // staged by json_stage_kernel: a descriptor must stay inside the batch's staging area
-    const uint64_t need = d.tlen >= 0 ? uint64_t(d.tlen) : uint64_t(d.n_out < 0 ? 0 : d.n_out) * 4u;
+    const uint64_t need = d.tlen >= 0                     ? uint64_t(d.tlen)
+                          : d.tlen == tk::kJsonCountOnDevice ? 0u
+                                                             : uint64_t(d.n_out < 0 ? 0 : d.n_out) * 4u;
     if (d.count < 0 || d.n_out < 0 || d.n_out > d.count || uint64_t(d.off) + ((need + 15u) & ~uint64_t(15)) > a.vals_cap[bk]) {
       bad = true;
       d = JsonRowDesc{0, 0, 0, 0};
@@ -85,8 +105,11 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
   }
   const int64_t n_out = d.n_out < L ? d.n_out : L;
   D* orow = out + r * L;
+  int64_t pad_from = n_out;
 
-  if (d.tlen < 0) {
+  if (d.tlen == tk::kJsonCountOnDevice) {
+    pad_from = 0;  // not a simple row: the host writes its values when the batch is delivered
+  } else if (d.tlen < 0) {
     // parsed on the host (not a simple row): float32 values
     const float* f = reinterpret_cast<const float*>(vals + d.off);
     for (int64_t k = tid; k < n_out; k += kThreads) orow[k] = Store<D>::cvt(f[k]);
@@ -189,7 +212,7 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
     bad = bad || s_bad != 0 || k0 != d.count;
   }
   // padding, lengths, mask
-  for (int64_t k = n_out + tid; k < L; k += kThreads) orow[k] = pad_value<D>(pad);
+  for (int64_t k = pad_from + tid; k < L; k += kThreads) orow[k] = pad_value<D>(pad);
   if (mask) {
     uint8_t* mrow = mask + r * L;
     for (int64_t k = tid; k < L; k += kThreads) mrow[k] = uint8_t(k < n_out);

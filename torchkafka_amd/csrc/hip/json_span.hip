@@ -36,6 +36,101 @@ constexpr int kMaxRows = int(tk::kJsonSpanMaxSegRows);
 constexpr int kRowsPerThread = kMaxRows / kThreads;
 
 __device__ __forceinline__ uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
+__device__ __forceinline__ bool is_ws(uint32_t c) { return c == 32u || c == 9u || c == 10u || c == 13u; }
+
+// 16 bytes of a row's text from the LDS image (any alignment: 5-dword window + v_alignbyte).
+__device__ __forceinline__ uint4 load16(const uint32_t* b32, int32_t b0) {
+  const int32_t w = b0 >> 2, sh = b0 & 3;
+  const uint32_t x0 = b32[w], x1 = b32[w + 1], x2 = b32[w + 2], x3 = b32[w + 3], x4 = b32[w + 4];
+  uint4 v;
+  v.x = __builtin_amdgcn_alignbyte(x1, x0, sh);
+  v.y = __builtin_amdgcn_alignbyte(x2, x1, sh);
+  v.z = __builtin_amdgcn_alignbyte(x3, x2, sh);
+  v.w = __builtin_amdgcn_alignbyte(x4, x3, sh);
+  return v;
+}
+
+// One wave copies a row's T bytes (LDS byte r0) to `o` and, for a device-counted row
+// (kJsonCountOnDevice), runs json_scan_simple's rules on them on the way (csrc/core/consumer.cpp
+// json_scan_impl, bit for bit): whitespace trimmed, '[' ... ']' framing, an interior of number
+// characters [0-9.-], commas and whitespace only, no run of more than 16 number characters.
+// Returns the element count (commas + 1; 0 for an empty interior), or -1 when the row is not
+// simple; *guess is then the element count a flat array of that text has (commas + 1, 0 when the
+// interior is empty or the text is not framed) -- the width its host parse will fill.
+__device__ int32_t copy_scan_row(const uint32_t* b32, const uint8_t* buf, int32_t r0, int32_t T, uint8_t* o,
+                                 int lane, int32_t* guess) {
+  int32_t lo, hi;
+  bool framed;
+  if (T >= 2 && buf[r0] == '[' && buf[r0 + T - 1] == ']') {
+    lo = 1;
+    hi = T - 1;
+    framed = true;
+  } else {
+    int32_t fa = T, lb = -1;  // first and last byte that is not whitespace
+    for (int32_t i = lane; i < T; i += 64)
+      if (!is_ws(buf[r0 + i])) {
+        fa = min(fa, i);
+        lb = max(lb, i);
+      }
+#pragma unroll
+    for (int off = 32; off; off >>= 1) {
+      fa = min(fa, __shfl_xor(fa, off, 64));
+      lb = max(lb, __shfl_xor(lb, off, 64));
+    }
+    framed = lb - fa + 1 >= 2 && buf[r0 + fa] == '[' && buf[r0 + lb] == ']';
+    lo = framed ? fa + 1 : 0;
+    hi = framed ? lb : 0;
+  }
+  int32_t commas = 0;
+  bool bad = !framed, anyt = false, anyc = false;
+  uint32_t carry = 0;  // number characters ending the previous 1 KiB pass (its lane 63)
+  for (int32_t base = 0; base < T; base += 64 * 16) {
+    const int32_t c = base + 16 * lane;
+    uint32_t tokm = 0;
+    if (c < T) {
+      const uint4 v = load16(b32, r0 + c);
+      *reinterpret_cast<uint4*>(o + c) = v;
+      const int32_t l0 = lo - c, h0 = hi - c;
+      uint32_t in = h0 <= 0 ? 0u : h0 >= 16 ? 0xFFFFu : (1u << h0) - 1u;
+      if (l0 > 0) in &= l0 >= 16 ? 0u : ~((1u << l0) - 1u);
+      if (in) {
+        const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+        uint32_t com = 0, oth = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const uint32_t ch = (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+          const bool tk = ch - 48u <= 9u || ch == 46u || ch == 45u;
+          tokm |= uint32_t(tk) << j;
+          com |= uint32_t(ch == 44u) << j;
+          oth |= uint32_t(!tk && ch != 44u && !is_ws(ch)) << j;
+        }
+        tokm &= in;
+        com &= in;
+        oth &= in;
+        commas += __popc(com);
+        bad = bad || oth != 0;
+        anyt = anyt || tokm != 0;
+        anyc = anyc || (tokm | com | oth) != 0;
+      }
+    }
+    // a run of > 16 number characters crosses a chunk boundary (inside 16 bytes it cannot)
+    const uint32_t lead = uint32_t(__builtin_ctz(~tokm));
+    const uint32_t trail = uint32_t(__builtin_clz(~(tokm << 16)));
+    uint32_t prev = __shfl_up(trail, 1, 64);
+    if (lane == 0) prev = carry;
+    if (prev + lead > 16u) bad = true;
+    carry = __shfl(trail, 63, 64);
+  }
+#pragma unroll
+  for (int off = 32; off; off >>= 1) commas += __shfl_xor(commas, off, 64);
+  bad = __ballot(bad) != 0;
+  anyt = __ballot(anyt) != 0;
+  anyc = __ballot(anyc) != 0;
+  *guess = framed && anyc ? commas + 1 : 0;
+  if (bad) return -1;
+  if (!anyt) return commas == 0 ? 0 : -1;
+  return commas + 1;
+}
 
 __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kBufBytes];
@@ -67,7 +162,10 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
       const float* __restrict__ src = reinterpret_cast<const float*>(bo.slot + d.pos);
       float* __restrict__ o = reinterpret_cast<float*>(bo.stage + off);
       for (int32_t k = lane; k < n_out; k += 64) o[k] = src[k];
-      if (lane == 0) bo.desc[row] = JsonRowDesc{off, -1, d.count, n_out};
+      if (lane == 0) {
+        bo.desc[row] = JsonRowDesc{off, -1, d.count, n_out};
+        if (bo.ctr) atomicMax(bo.ctr, n_out);
+      }
       off += align16(uint32_t(n_out) * 4u);
     }
     return;
@@ -139,19 +237,23 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
       continue;
     }
     uint8_t* __restrict__ o = bo.stage + dst[rr];
-    for (int32_t c = 16 * lane; c < T; c += 64 * 16) {
-      const int32_t b0 = r0 + c, w = b0 >> 2, sh = b0 & 3;
-      const uint32_t x0 = b32[w], x1 = b32[w + 1], x2 = b32[w + 2], x3 = b32[w + 3], x4 = b32[w + 4];
-      uint4 v;
-      v.x = __builtin_amdgcn_alignbyte(x1, x0, sh);
-      v.y = __builtin_amdgcn_alignbyte(x2, x1, sh);
-      v.z = __builtin_amdgcn_alignbyte(x3, x2, sh);
-      v.w = __builtin_amdgcn_alignbyte(x4, x3, sh);
-      *reinterpret_cast<uint4*>(o + c) = v;
+    int32_t count = cnt[rr], guess = 0;
+    if (count == tk::kJsonCountOnDevice) {
+      count = copy_scan_row(b32, buf, r0, T, o, lane, &guess);
+    } else {
+      for (int32_t c = 16 * lane; c < T; c += 64 * 16) *reinterpret_cast<uint4*>(o + c) = load16(b32, r0 + c);
     }
     if (lane == 0) {
-      const int32_t count = cnt[rr];
-      bo.desc[row_begin + rr] = JsonRowDesc{dst[rr], T, count, trunc >= 0 && count > trunc ? trunc : count};
+      // a device-counted row that is not simple: the host parses it when the batch is delivered
+      // (tlen kJsonCountOnDevice: json_rows_kernel writes its padding, lengths and mask only)
+      const bool host = count < 0;
+      const int32_t c = host ? guess : count;
+      const int32_t n_out = trunc >= 0 && c > trunc ? trunc : c;
+      bo.desc[row_begin + rr] = JsonRowDesc{dst[rr], host ? tk::kJsonCountOnDevice : T, c, n_out};
+      if (bo.ctr) {
+        atomicMax(bo.ctr, n_out);
+        if (host) atomicAdd(bo.ctr + 1, 1);
+      }
     }
   }
   if (off_seg && lane == 0) *bo.err = int32_t(sg.seg);  // never committed (reported as this segment)

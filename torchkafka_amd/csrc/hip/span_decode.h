@@ -64,6 +64,10 @@ struct JsonStageBatch {
   uint32_t* partials;           // host-mapped raw CRC per segment (RecordBatches spanning segments)
   int32_t trunc_len;            // rows with more elements keep this many (-1: no limit)
   int32_t reserved;
+  // kSlotDevCount batches: zeroed device words [0] = max elements kept by a row, [1] = rows left
+  // to the host (not simple); the kernel counts rows whose JsonSpanRow::count is
+  // kJsonCountOnDevice.  nullptr: every count came from the worker.
+  int32_t* ctr;
 };
 
 struct JsonStageLaunch {

@@ -44,7 +44,34 @@ at::Tensor alloc_group(MainDriver& d, const std::vector<int64_t>& shape, const a
 // Outputs of a var-len batch parsed ahead of its delivery by a coalesced launch.
 struct VarlenOut {
   at::Tensor out, lengths, mask;
+  // device-counted JSON batch (kSlotDevCount): out/mask are [m, capacity] until finish_json views
+  // the first m * width elements as [m, width]
+  at::Tensor flat_out, flat_mask;
+  int64_t m = 0;
+  bool devc = false;
 };
+
+// A device-counted JSON batch at delivery: its width as the parse kernel reported it (the kernel
+// wrote the rows with that stride), and the rows it left to the host parsed and written on `ks`.
+void finish_json(MainDriver& d, const SlotView& v, VarlenOut* o, int dst_dt, double pad, hipStream_t ks) {
+  if (!o->devc) return;
+  o->devc = false;
+  const int64_t m = o->m;
+  int64_t n_host = 0, L = 0;
+  if (m > 0) {
+    py::gil_scoped_release nogil;
+    L = d.json_width(v, &n_host);
+  }
+  o->out = o->flat_out.narrow(0, 0, m * L).view({m, L});
+  if (o->flat_mask.defined()) o->mask = o->flat_mask.narrow(0, 0, m * L).view({m, L});
+  if (n_host > 0) {
+    uint8_t* mk = o->mask.defined() ? static_cast<uint8_t*>(o->mask.data_ptr()) : nullptr;
+    void* out = o->out.data_ptr();
+    int64_t* lens = o->lengths.data_ptr<int64_t>();
+    py::gil_scoped_release nogil;
+    d.json_host_rows(v, out, L, dst_dt, pad, lens, mk, ks);
+  }
+}
 
 // Outputs of a fixed-width batch: the values, and -- when the schema asks for record fields --
 // its [extras, rows] int64 key / timestamp columns (decoded by the same launch).
@@ -148,8 +175,8 @@ int64_t padded_len(const SlotView& s, int64_t pad_to, int64_t pad_multiple) {
 // Outputs of a group of device-parsed JSON batches (kPackJsonSpan): one allocation for the values
 // of all of them, one for the lengths (and one for the masks), made on the decode stream the group
 // runs on and recorded on the user's stream (as alloc_group), then viewed per batch.
-void alloc_json_group(MainDriver& d, const int64_t* ms, const int64_t* Ls, int n, int dst_dt, bool want_mask,
-                      c10::DeviceIndex dev, std::shared_ptr<VarlenOut>* outs) {
+void alloc_json_group(MainDriver& d, const int64_t* ms, const int64_t* Ls, const bool* devc, int n, int dst_dt,
+                      bool want_mask, c10::DeviceIndex dev, std::shared_ptr<VarlenOut>* outs) {
   int64_t tot = 0, rows = 0;
   for (int k = 0; k < n; ++k) {
     tot += ms[k] * Ls[k];
@@ -172,6 +199,12 @@ void alloc_json_group(MainDriver& d, const int64_t* ms, const int64_t* Ls, int n
     o->out = vals.narrow(0, vo, ms[k] * Ls[k]).view({ms[k], Ls[k]});
     o->lengths = lens.narrow(0, ro, ms[k]);
     if (want_mask) o->mask = masks.narrow(0, vo, ms[k] * Ls[k]).view({ms[k], Ls[k]});
+    if (devc[k]) {
+      o->devc = true;
+      o->m = ms[k];
+      o->flat_out = vals.narrow(0, vo, ms[k] * Ls[k]);
+      if (want_mask) o->flat_mask = masks.narrow(0, vo, ms[k] * Ls[k]);
+    }
     vo += ms[k] * Ls[k];
     ro += ms[k];
     outs[k] = std::move(o);
@@ -190,12 +223,14 @@ void launch_ahead_json(MainDriver& d, int dst_dt, double pad, int64_t pad_to, in
     if (rows.empty()) return;
     const int n = int(rows.size());
     int64_t ms[kMaxGroup], Ls[kMaxGroup];
+    bool devc[kMaxGroup];
     for (int k = 0; k < n; ++k) {
       ms[k] = rows[size_t(k)];
       Ls[k] = padded_len(d.ahead_member(size_t(k)), pad_to, pad_multiple);
+      devc[k] = (d.ahead_member(size_t(k)).flags & tk::kSlotDevCount) != 0;
     }
     std::shared_ptr<VarlenOut> o[kMaxGroup];
-    alloc_json_group(d, ms, Ls, n, dst_dt, want_mask, dev, o);
+    alloc_json_group(d, ms, Ls, devc, n, dst_dt, want_mask, dev, o);
     void* outs[kMaxGroup];
     int64_t* lens[kMaxGroup];
     uint8_t* masks[kMaxGroup];
@@ -334,6 +369,7 @@ void register_torch_step(py::module_& m) {
         int r;
         int64_t t1, t2;
         size_t extra = 0;
+        d.set_json_mult(pad_to >= 0 ? 0 : std::max<int64_t>(1, pad_multiple));
         {
           py::gil_scoped_release nogil;
           d.finish_delivered(stream);
@@ -353,6 +389,7 @@ void register_torch_step(py::module_& m) {
         if (v.pre) {
           // parsed by an earlier group launch; a consumer on another stream waits for that kernel
           auto* o = static_cast<VarlenOut*>(v.pre_out.get());
+          finish_json(d, v, o, dst_dt, pad, v.pre_stream);
           out = o->out;
           lengths = o->lengths;
           mask = o->mask;
@@ -363,13 +400,15 @@ void register_torch_step(py::module_& m) {
           // parsed from the logs by one launch with the staged JSON batches behind it
           const int ng = 1 + int(extra);
           int64_t ms[kMaxGroup], Ls[kMaxGroup];
+          bool devc[kMaxGroup];
           for (int k = 0; k < ng; ++k) {
             const SlotView& s = k == 0 ? v : d.group_member(size_t(k - 1));
             ms[k] = int64_t(s.n_rows);
             Ls[k] = padded_len(s, pad_to, pad_multiple);
+            devc[k] = (s.flags & tk::kSlotDevCount) != 0;
           }
           std::shared_ptr<VarlenOut> o[kMaxGroup];
-          alloc_json_group(d, ms, Ls, ng, dst_dt, want_mask, dev, o);
+          alloc_json_group(d, ms, Ls, devc, ng, dst_dt, want_mask, dev, o);
           void* outs[kMaxGroup];
           int64_t* lens[kMaxGroup];
           uint8_t* masks[kMaxGroup];
@@ -380,12 +419,16 @@ void register_torch_step(py::module_& m) {
             lens[k] = o[k]->lengths.data_ptr<int64_t>();
             masks[k] = want_mask ? static_cast<uint8_t*>(o[k]->mask.data_ptr()) : nullptr;
           }
+          for (int k = 1; k < ng; ++k) handles.emplace_back(std::move(o[k]));
+          {
+            py::gil_scoped_release nogil;
+            d.json_group_launch(stream, dst_dt, pad, outs, Ls, lens, masks, std::move(handles));
+          }
+          finish_json(d, v, o[0].get(), dst_dt, pad, d.last_stream());
           out = o[0]->out;
           lengths = o[0]->lengths;
           mask = o[0]->mask;
-          for (int k = 1; k < ng; ++k) handles.emplace_back(std::move(o[k]));
           py::gil_scoped_release nogil;
-          d.json_group_launch(stream, dst_dt, pad, outs, Ls, lens, masks, std::move(handles));
           d.deliver(v);
         } else {
           auto alloc = [&](const SlotView& s, VarlenOut* o, int64_t* Lout) {

@@ -337,7 +337,7 @@ class DeviceLoader:
             can also be passed as a keyword argument, which overrides the config; the performance
             knobs (``slots_per_worker``, ``slot_bytes``, ``prefetch``, ``copy_streams``,
             ``event_every``, ``coalesce``, ``coalesce_wait_us``, ``lockstep_depth``, ``numa_bind``,
-            ``ahead_depth``, ``decode_streams``, ``span_burst``, ``worker_spin_us``) form its
+            ``ahead_depth``, ``decode_streams``, ``span_burst``, ``worker_spin_us``, ``json_count``, ...) form its
             :class:`~torchkafka_amd.config.Tuning` (docs/CONFIG.md).  Options:
         normalize: optional ``(mean, std)`` fused into the collate kernel.
         sharding: ``"static"`` rank/worker partition map (default) or ``"group"`` (Kafka group assignment).
@@ -668,7 +668,7 @@ class DeviceLoader:
     def _worker_cfg(self) -> dict:
         return {"batch_size": self.batch_size, "sharding": self.sharding, "rank": self.rank,
                 "world_size": self.world_size, "native": self.native, "base_seed": self.base_seed,
-                "gather": self._direct(), "json_device": self._json_device(),
+                "gather": self._direct(), "json_device": self._json_device(), "json_count": self._json_count(),
                 "span": self._device_decode(),
                 "process_overridden": self._process_overridden(), "commit_table": None,
                 "worker_spin_us": int(self.tuning.worker_spin_us), "in_process": False,
@@ -757,6 +757,22 @@ class DeviceLoader:
             raise ValueError("decode='device' needs the synthetic broker (bootstrap_servers shm:// or file://) "
                              "with a group_id and h2d != 'direct'")
         return ok
+
+    def _json_count(self) -> bool:
+        """Device-parsed JsonArray rows counted on the device too (``tuning.json_count``): the workers
+        then read only the record headers, as for fixed-width records, and json_span.hip runs the
+        "simple row" check and the element count while it stages each text; the batch's width is the
+        longest row's count, reduced on the device (a row that is not simple -- exponents, NaN -- is
+        parsed on the host when its batch is delivered).  Filters that drop rows need the counts
+        before the batch is packed, so those keep the workers counting."""
+        if not self._json_span():
+            return False
+        s = self.schema
+        mode = getattr(self.tuning, "json_count", "auto")
+        ok = int(getattr(s, "min_len", 0)) == 0 and (getattr(s, "max_len", None) is None or bool(s.truncate))
+        if mode == "device" and not ok:
+            raise ValueError("tuning.json_count='device' cannot drop rows: needs min_len=0 and truncate=True")
+        return ok and mode != "host"
 
     def _json_device(self) -> bool:
         """JsonArray records parsed by the gfx950 kernel (json_parse.hip) instead of the workers.
@@ -1252,8 +1268,13 @@ class DeviceLoader:
             out = torch.empty((n_rows, L), dtype=dst_dt, device=dev)
             lengths = torch.empty(n_rows, dtype=torch.int64, device=dev)
             mask = torch.empty((n_rows, L), dtype=torch.bool, device=dev) if self.return_mask else None
-            drv.collate_varlen_last(stream, DTYPE_CODE[dst_dt], out.data_ptr(), L, float(self.pad_value),
-                                    lengths.data_ptr(), mask.data_ptr() if mask is not None else 0)
+            W = drv.collate_varlen_last(stream, DTYPE_CODE[dst_dt], out.data_ptr(), L, float(self.pad_value),
+                                        lengths.data_ptr(), mask.data_ptr() if mask is not None else 0,
+                                        0 if self.pad_to is not None else max(1, self.pad_multiple))
+            if W != L:  # device-counted JSON: L was the workers' bound, W the width the kernel chose
+                out = out.view(-1)[:n_rows * W].view(n_rows, W)
+                if mask is not None:
+                    mask = mask.view(-1)[:n_rows * W].view(n_rows, W)
         self.stats.record_batch(n_rows, payload_bytes, t1 - t0, time.perf_counter_ns() - t1)
         n_rec = sum(w[3] for w in wms)
         if self.return_info:

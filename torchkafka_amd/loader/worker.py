@@ -226,8 +226,10 @@ def _native_loop(ring, worker_id, spw, consumer, schema, cfg, state) -> None:
     timeout = _consumer_timeout_ms(consumer)
     fetcher = consumer._fetcher
     gather = bool(cfg.get("gather")) and kind == core().PACK_FIXED
-    span = (bool(cfg.get("span")) and kind in (core().PACK_FIXED, core().PACK_JSON_TEXT, core().PACK_VARLEN)
-            and not gather)
+    span = int(bool(cfg.get("span")) and kind in (core().PACK_FIXED, core().PACK_JSON_TEXT, core().PACK_VARLEN)
+               and not gather)
+    if span and kind == core().PACK_JSON_TEXT and cfg.get("json_count"):
+        span = core().SPAN_JSON_DEV_COUNT  # headers only: the device counts the elements
     # a member of a Kafka group over KafkaBridge replicas: the partitions move with rebalances, and
     # a fill waiting for data returns early when they do
     group_managed = bool(getattr(consumer, "_group_managed", False))
