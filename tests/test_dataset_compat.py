@@ -320,6 +320,25 @@ def test_d4_d5_uneven_workers_no_signal_death(broker):
     assert broker.committed_offsets("group_1", "topic") == {0: 4, 1: 40}
 
 
+def test_batches_carry_their_worker_and_collate_fn_is_restored(broker):
+    """Attribution comes from a stamp the workers put on each batch (no hook into the private
+    _MultiProcessingDataLoaderIter); the user's DataLoader keeps its own collate_fn, and a loader
+    whose persistent workers were started outside auto_commit is refused rather than guessed."""
+    produce_offsets(broker, n=12, partitions=2)
+    ds = PartOffset.placeholder()
+    dl = DataLoader(ds, batch_size=4, num_workers=2, collate_fn=_pairs_collate,
+                    worker_init_fn=PartOffset.init_worker("topic", **kw(broker, consumer_timeout_ms=600)))
+    out = list(auto_commit(dl))
+    assert dl.collate_fn is _pairs_collate and all(isinstance(b, torch.Tensor) for b in out)
+    assert broker.committed_offsets("group_1", "topic") == {0: 12, 1: 12}
+    dl2 = DataLoader(PartOffset.placeholder(), batch_size=4, num_workers=1, persistent_workers=True,
+                     worker_init_fn=PartOffset.init_worker("topic", **kw(broker, group_id="group_2",
+                                                                          consumer_timeout_ms=300)))
+    iter(dl2)  # workers start with the plain collate_fn
+    with pytest.raises(RuntimeError, match="persistent_workers"):
+        next(auto_commit(dl2))
+
+
 def test_d4_commit_worker_signal_after_stream_end_is_harmless(broker):
     broker.create_topic("topic", 2)
     broker.produce("topic", [b"x"] * 4, partition=0)

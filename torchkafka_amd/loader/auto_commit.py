@@ -11,23 +11,40 @@ Changed on purpose:
   * the dataset check is by class *or* marker, so two import paths of the
     package can no longer silently disable commits (D1/D2);
   * workers are told how many of their samples the user finished through a
-    shared-memory channel and commit exactly those positions (D3), the
-    producing worker of each batch is read from the iterator instead of
-    assumed by ``itertools.cycle`` (D5), and the final batch of every worker
-    is committed and acknowledged before the loader shuts down (D4);
+    shared-memory channel and commit exactly those positions (D3), each batch
+    carries the id of the worker that collated it (a wrapper around the
+    loader's ``collate_fn`` stamps it, ``get_worker_info()``) instead of the
+    producer being assumed by ``itertools.cycle`` (D5), and the final batch of
+    every worker is committed and acknowledged before the loader shuts down (D4);
   * :class:`DeviceLoader` inputs get the device-resident path with exact
     watermark commits, optionally lock-stepped across ranks over RCCL.
 """
 from __future__ import annotations
 
-import itertools as it
+import collections
 import logging
 
-from torch.utils.data import DataLoader
+from torch.utils.data import DataLoader, get_worker_info
 
 from .commit_channel import CommitChannel
 
 log = logging.getLogger(__name__)
+
+# A batch as the workers hand it over: the user's collated batch and the id of the worker that
+# collated it.  A namedtuple, so pin_memory=True pins the batch field and leaves the id alone.
+_Stamped = collections.namedtuple("_Stamped", ["batch", "worker"])
+
+
+class _StampingCollate:
+    """The loader's ``collate_fn``, run in the workers, with each batch stamped by its worker id
+    (picklable for spawn / forkserver workers whenever the wrapped function is)."""
+
+    def __init__(self, inner):
+        self.inner = inner
+
+    def __call__(self, data):
+        info = get_worker_info()
+        return _Stamped(self.inner(data), info.id if info is not None else 0)
 
 
 def _is_kafka_dataset(ds) -> bool:
@@ -71,21 +88,14 @@ def _multi_worker(dataloader: DataLoader, final_commit_timeout: float):
     bs = dataloader.batch_size or 1
     channel = CommitChannel(dataloader.num_workers, bs)
     previous = getattr(ds, "_commit_channel", None)
+    collate = dataloader.collate_fn
     ds._commit_channel = channel  # inherited (fork) / pickled (spawn) into the workers created by iter()
-    batches = iter(dataloader)
-    ds._commit_channel = previous
-    last_worker = [None]
-    process_data = getattr(batches, "_process_data", None)
-    if process_data is not None:
-        def _tap(data, worker_idx, _orig=process_data):
-            last_worker[0] = worker_idx
-            return _orig(data, worker_idx)
-
-        batches._process_data = _tap
-        attribution = None
-    else:  # pragma: no cover - torch without _process_data: reference's round-robin assumption
-        attribution = it.cycle(range(dataloader.num_workers))
-        log.warning("DataLoader iterator has no _process_data; assuming round-robin batch order")
+    dataloader.collate_fn = _StampingCollate(collate)  # handed to the workers by iter() as well
+    try:
+        batches = iter(dataloader)
+    finally:
+        ds._commit_channel = previous
+        dataloader.collate_fn = collate
     consumed = [0] * dataloader.num_workers
     workers = getattr(batches, "_workers", [])
 
@@ -93,8 +103,13 @@ def _multi_worker(dataloader: DataLoader, final_commit_timeout: float):
         return w < len(workers) and workers[w].is_alive()
 
     try:
-        for batch in batches:
-            w = last_worker[0] if attribution is None else next(attribution)
+        for stamped in batches:
+            if not isinstance(stamped, _Stamped):
+                # persistent workers started by an earlier iter() without the stamp: which worker
+                # made a batch is unknown, and a wrong guess would commit unread records
+                raise RuntimeError("auto_commit: the DataLoader's workers were started outside auto_commit "
+                                   "(persistent_workers=True); iterate it through auto_commit from the start")
+            batch, w = stamped
             yield batch
             # batches, not samples: the worker maps its k-th batch to the consumer positions after
             # its samples, whatever shape the collate_fn gave the batch
