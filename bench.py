@@ -546,6 +546,8 @@ def run_rank(args) -> int:
             "steady_state": steady_out,
             **extra_out,
             "bridge": bridge_out,
+            # the native binaries that ran, with the source sha compiled into each (ops.build_info)
+            "native_build": _native_build(),
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -554,6 +556,13 @@ def run_rank(args) -> int:
     if rank == 0:
         broker.destroy()
     return 0
+
+
+def _native_build() -> dict:
+    from torchkafka_amd.ops import build_info
+
+    return {name: {"sha16": b["built_from"][:16] if b["built_from"] else None, "matches_tree": b["matches_tree"]}
+            for name, b in build_info().items()}
 
 
 def main() -> int:

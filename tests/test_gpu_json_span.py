@@ -26,7 +26,14 @@ def _dataset(schema):
 
 
 def _bits(t: torch.Tensor) -> torch.Tensor:
-    return t.view({1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[t.element_size()])
+    """Bit patterns, with every NaN as one pattern: torch's own CPU casts do not agree on NaN bits
+    (the vectorised f32 -> bf16 cast gives 0xFFFF, the scalar one 0x7FC0), so only NaN-ness is pinned."""
+    bits = t.view({1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[t.element_size()])
+    if t.is_floating_point():
+        nan = torch.isnan(t.float())
+        if bool(nan.any()):
+            bits = torch.where(nan, torch.full_like(bits, 0x7F), bits)
+    return bits
 
 
 def _texts(rng, n, lo, hi, odd_every=0, nulls_every=0, bad_at=None):

@@ -14,7 +14,9 @@ snapshot to the GPU box.  Run ``python -m torchkafka_amd._build`` (or
 from __future__ import annotations
 
 import concurrent.futures as cf
+import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -55,8 +57,40 @@ def hip_target() -> Path:
     return PKG / f"_tkhip{EXT_SUFFIX}"
 
 
-def _newest(paths) -> float:
-    return max((p.stat().st_mtime for p in paths), default=0.0)
+def sources(builder: str) -> list[Path]:
+    """Every file an extension is built from (its sources and the headers they may include)."""
+    core_dir, hip_dir = CSRC / "core", CSRC / "hip"
+    core = sorted(core_dir.glob("*.cpp")) + sorted(core_dir.glob("*.h"))
+    if builder == "core":
+        return core
+    return sorted(hip_dir.glob("*.hip")) + sorted(hip_dir.glob("*.cpp")) + sorted(hip_dir.glob("*.h")) + core
+
+
+def sources_sha(builder: str) -> str:
+    """sha256 over the relative paths and bytes of sources(builder) (plus the target arch for hip):
+    compiled into the extension, so a binary names the exact tree it was built from."""
+    h = hashlib.sha256(f"{builder}:{ARCH if builder == 'hip' else 'host'}\n".encode())
+    for p in sources(builder):
+        h.update(str(p.relative_to(CSRC)).encode() + b"\0")
+        h.update(p.read_bytes())
+    return h.hexdigest()
+
+
+_SHA_RE = re.compile(rb"TKSRCSHA:([0-9a-f]{64})")
+
+
+def embedded_sha(path: Path) -> str | None:
+    """The sources_sha a built extension carries (read from the file, nothing is loaded)."""
+    try:
+        m = _SHA_RE.search(path.read_bytes())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
+
+
+def up_to_date(builder: str) -> bool:
+    target = core_target() if builder == "core" else hip_target()
+    return target.exists() and embedded_sha(target) == sources_sha(builder)
 
 
 def _run(cmd: list[str]) -> None:
@@ -75,9 +109,8 @@ def _compile_all(jobs: list[list[str]]) -> None:
 def build_core(force: bool = False, verbose: bool = False) -> Path:
     src_dir = CSRC / "core"
     srcs = sorted(src_dir.glob("*.cpp"))
-    deps = srcs + sorted(src_dir.glob("*.h"))
     out = core_target()
-    if not force and out.exists() and out.stat().st_mtime >= _newest(deps):
+    if not force and up_to_date("core"):
         return out
     obj_dir = BUILD / "core"
     obj_dir.mkdir(parents=True, exist_ok=True)
@@ -85,6 +118,7 @@ def build_core(force: bool = False, verbose: bool = False) -> Path:
     flags = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
              "-DNDEBUG", *_py_includes(), f"-I{src_dir}"]
     flags += os.environ.get("TORCHKAFKA_CXXFLAGS", "").split()
+    flags.append(f'-DTK_SOURCES_SHA="{sources_sha("core")}"')
     objs, jobs = [], []
     for s in srcs:
         o = obj_dir / (s.stem + ".o")
@@ -113,9 +147,8 @@ def build_hip(force: bool = False, verbose: bool = False) -> Path:
     # the main-process step driver embeds the host core (ring, broker) to commit natively
     core_srcs = [p for p in sorted(core_dir.glob("*.cpp")) if p.name != "bindings.cpp"]
     srcs = sorted(src_dir.glob("*.hip")) + sorted(src_dir.glob("*.cpp")) + core_srcs
-    deps = srcs + sorted(src_dir.glob("*.h")) + sorted(core_dir.glob("*.h"))
     out = hip_target()
-    if not force and out.exists() and out.stat().st_mtime >= _newest(deps):
+    if not force and up_to_date("hip"):
         return out
     obj_dir = BUILD / f"hip-{ARCH}"
     obj_dir.mkdir(parents=True, exist_ok=True)
@@ -124,7 +157,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> Path:
     # torch's include dir first: its bundled pybind11 is the one every binding in this module uses
     flags = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}", "-DNDEBUG",
              "-Wno-unused-result", f"-I{t_inc}", f"-I{sysconfig.get_paths()['include']}", f"-I{src_dir}",
-             f"-I{core_dir}"]
+             f"-I{core_dir}", f'-DTK_SOURCES_SHA="{sources_sha("hip")}"']
     torch_flags = [f"-I{t_inc / 'torch' / 'csrc' / 'api' / 'include'}", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1",
                    "-DTORCH_API_INCLUDE_EXTENSION_H", "-D_GLIBCXX_USE_CXX11_ABI=1", "-Wno-deprecated-declarations"]
     objs, jobs = [], []

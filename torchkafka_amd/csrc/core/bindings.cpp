@@ -156,7 +156,15 @@ py::list wms_to_list(const std::vector<Watermark>& w) {
 
 }  // namespace
 
+#ifndef TK_SOURCES_SHA
+#define TK_SOURCES_SHA "unversioned"  // built outside _build.py
+#endif
+// The sha of the sources this binary was built from (_build.sources_sha): _build.embedded_sha finds it
+// in the file, ops.build_info() compares it with the tree.
+__attribute__((used)) static const char kSourcesSha[] = "TKSRCSHA:" TK_SOURCES_SHA;
+
 PYBIND11_MODULE(_tkcore, m) {
+  m.attr("SOURCES_SHA") = std::string(kSourcesSha + 9);
   m.doc() = "torchkafka_amd host native core: RecordBatch codec, shm broker, fetcher, packers, slot ring";
 
   static py::exception<KafkaError> kafka_error(m, "KafkaError", PyExc_RuntimeError);

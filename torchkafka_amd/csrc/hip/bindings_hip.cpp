@@ -53,7 +53,15 @@ T* ptr(uintptr_t p) { return reinterpret_cast<T*>(p); }
 hipStream_t stream_of(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 }  // namespace
 
+#ifndef TK_SOURCES_SHA
+#define TK_SOURCES_SHA "unversioned"  // built outside _build.py
+#endif
+// The sha of the sources this binary was built from (_build.sources_sha): _build.embedded_sha finds it
+// in the file, ops.build_info() compares it with the tree.
+__attribute__((used)) static const char kSourcesSha[] = "TKSRCSHA:" TK_SOURCES_SHA;
+
 PYBIND11_MODULE(_tkhip, m) {
+  m.attr("SOURCES_SHA") = std::string(kSourcesSha + 9);
   m.doc() = "torchkafka_amd gfx950 device path: H2D engine + collate kernels";
 
   m.def("device_info", [](int dev) {
@@ -291,13 +299,13 @@ PYBIND11_MODULE(_tkhip, m) {
              s["commit_failures"] = d.commit_failures();
              s["commit_ns"] = d.commit_ns();
              s["commit_latency_ns"] = d.commit_latency_ns();
-             s["fill_ns"] = d.fill_ns_;
-             s["fills"] = d.fills_;
+             s["fill_ns"] = d.poll_stats().fill_ns;
+             s["fills"] = d.poll_stats().fills;
              s["blocked_ns"] = d.blocked_ns_;
              s["blocked_calls"] = d.blocked_calls_;
-             s["ready_age_ns"] = d.ready_age_ns_;
-             s["worker_idle_ns"] = d.worker_idle_ns_;
-             s["worker_slot_wait_ns"] = d.worker_slot_wait_ns_;
+             s["ready_age_ns"] = d.poll_stats().ready_age_ns;
+             s["worker_idle_ns"] = d.poll_stats().worker_idle_ns;
+             s["worker_slot_wait_ns"] = d.poll_stats().worker_slot_wait_ns;
              s["phase_commit_ns"] = d.ph_commit_ns_;
              s["phase_next_ns"] = d.ph_next_ns_;
              s["phase_launch_ns"] = d.ph_launch_ns_;
@@ -314,8 +322,8 @@ PYBIND11_MODULE(_tkhip, m) {
              s["fast_records"] = d.fast_records_;
              s["fast_ns"] = d.fast_ns_;
              s["released"] = d.released_;
-             s["polled"] = d.polled_;
-             s["poll_ns"] = d.poll_ns_;
+             s["polled"] = d.poll_stats().polled;
+             s["poll_ns"] = d.poll_stats().poll_ns;
              s["log_bytes_registered"] = d.log_bytes_registered();
              s["log_bytes_unpinned"] = d.log_bytes_unpinned();
              if (const LogMirror* m = d.mirror()) {

@@ -1,12 +1,16 @@
 // Main-process step driver: the per-batch host path of DeviceLoader in one native call.
 //
-// Python-level per-batch work (ring polling, summary/watermark reads, H2D
-// issue, event bookkeeping, commit) cost ~20 us per batch; at 256 x 1 KiB
-// records per batch that capped one MI355X at ~11 M records/s.  The driver
-// keeps all of it native: it owns the ring cursors, the staged (H2D-issued)
-// queue, the in-flight host slots, the carried watermarks of empty slots and
-// the finished-but-uncommitted offsets, and commits straight into the
-// broker's shared-memory offset table.
+// Python-level per-batch work (ring polling, summary/watermark reads, H2D issue, event
+// bookkeeping, commit) cost ~20 us per batch; at 256 x 1 KiB records per batch that capped one
+// MI355X at ~11 M records/s.  The driver keeps all of it native.  It is the LAUNCHER: it forms
+// groups of staged batches, launches their collate / decode kernels on the user's or the decode
+// streams, tracks the launched slots' completion events and releases the slots, and decides when
+// a delivered batch is finished and committable.  The parts around it are their own classes:
+//   RingPoller    (ring_poller.h)    READY ring slots -> staged batches (H2D issued)
+//   LogPins       (log_pins.h)       partition logs pinned / mirrored for device decode
+//   BatchVerdicts (batch_verdicts.h) device CRC / parse status words of launched batches
+//   CommitLedger  (commit_ledger.h)  finished offsets -> durable commits, commit latency
+//   CreditLockstep (core/lockstep.h) cross-rank agreement on the step count (DDP)
 #pragma once
 
 #include <cstdlib>
@@ -15,44 +19,24 @@
 #include <deque>
 #include <memory>
 #include <string>
-#include <unordered_map>
+#include <tuple>
 #include <vector>
 
+#include "batch_verdicts.h"
 #include "broker.h"
 #include "collate.h"
+#include "commit_ledger.h"
 #include "consumer.h"
 #include "engine.h"
+#include "lockstep.h"
 #include "log_mirror.h"
+#include "log_pins.h"
 #include "rccl_lockstep.h"
 #include "ring.h"
+#include "ring_poller.h"
 #include "span_decode.h"
 
 namespace tkh {
-
-// Slots whose rows are decoded on the device from the logs into a padded batch (span.h).
-inline bool row_span_kind(uint32_t k) { return k == uint32_t(tk::kPackJsonSpan) || k == uint32_t(tk::kPackVarSpan); }
-
-struct SlotView {
-  int64_t g = -1;
-  uint32_t n_rows = 0, flags = 0, kind = 0, worker = 0;
-  uint64_t payload_bytes = 0, values_offset = 0;
-  uint32_t row_bytes = 0;
-  int64_t max_row_len = 0, total_elems = 0, n_scanned = 0;
-  int32_t src_dtype = -1;
-  uint32_t n_segs = 0;                // kPackRecordSpan / kPackJsonSpan: SpanSeg entries at values_offset
-  int32_t trunc_len = -1;             // kPackJsonSpan: rows keep at most this many elements (-1: all)
-  uint64_t span_bytes = 0;            // device decode: log bytes its segments read
-  uint64_t extras_offset = 0;         // record fields beside the values (SlotHeader::extras_*)
-  uint32_t extras_n = 0;
-  std::vector<int64_t> shape;
-  std::vector<tk::Watermark> wms;
-  // coalesced fast path: collated ahead of delivery by a group launch
-  bool pre = false;
-  hipStream_t pre_stream = nullptr;
-  int64_t pre_event_slot = -1;        // slot whose completion event follows the group kernel
-  std::shared_ptr<void> pre_out;      // the output tensor (opaque here: libtorch stays in torch_step.cpp)
-  int64_t perr = -1;                  // device JSON parse: its error word (set at launch)
-};
 
 class MainDriver {
  public:
@@ -63,7 +47,7 @@ class MainDriver {
   // Next batch slot (H2D issued).  Returns 1 (out filled), -1 timeout, -2 end of stream, -3 worker error,
   // -4 an earlier device-parsed batch was malformed (parse_error()).
   int next_slot(int64_t timeout_ms, SlotView* out);
-  const std::string& error() const { return error_; }
+  const std::string& error() const { return poller_->error(); }
 
   void collate_fixed(const SlotView& v, hipStream_t stream, int dst_dt, void* dst, int64_t row, const float* shift,
                      const float* scale);
@@ -80,10 +64,9 @@ class MainDriver {
   void collate_varlen(const SlotView& v, hipStream_t stream, int dst_dt, void* out, int64_t L, double pad,
                       int64_t* lengths, uint8_t* mask);
 
-  // Device JSON parse (kPackJsonText): grammar errors found by the kernel.  A batch's error
-  // word is checked once its GPU work completed, before the batch can be committed; a bad
-  // batch stops the commits (commit_pending() returns -2, next_slot() -4) and parse_error()
-  // describes it.
+  // Device JSON parse / span decode: a batch's status word is checked once its GPU work completed,
+  // before the batch can be committed; a bad batch stops the commits (commit_pending() returns -2,
+  // next_slot() -4) and parse_error() describes it.
   const std::string& parse_error() const { return parse_error_; }
 
   void deliver(const SlotView& v);   // batch handed to the user
@@ -96,14 +79,14 @@ class MainDriver {
   void set_commit_on_device(bool on) { commit_on_device_ = on; }
   // Moves fenced batches whose GPU work completed to the committable stage.
   void drain_fenced(bool wait);
-  void add_finished(const std::vector<tk::Watermark>& wms);
-  // Commits every finished batch.  Returns 0 nothing to do, 1 committed, -1 CommitFailedError.
+  void add_finished(const std::vector<tk::Watermark>& wms) { ledger_->add_finished(wms); }
+  // Commits every finished batch.  Returns 0 nothing to do, 1 committed, -1 CommitFailedError,
+  // -2 a device-checked batch failed (the batches before it were committed).
   int commit_pending();
-  bool can_commit() const { return broker_ != nullptr || sink_table_ != nullptr; }
-  // commit_sink='worker' (loader/commit_channel.py WatermarkTable): finished offsets are
-  // published to the worker that delivered each partition, whose own consumer commits them as a
-  // group member, instead of being stored into the synthetic broker from this process.
-  void set_worker_sink(uintptr_t table, int n_workers, int capacity);
+  bool can_commit() const { return ledger_->can_commit(); }
+  void set_worker_sink(uintptr_t table, int n_workers, int capacity) {
+    ledger_->set_worker_sink(table, n_workers, capacity);
+  }
 
   // Fused fast path: [finish+commit previous] -> next slot -> fixed-width collate into dst.
   // Returns n_rows (>0), or -1 timeout, -2 end, -3 error; *commit_status as commit_pending().
@@ -131,13 +114,8 @@ class MainDriver {
   // Stages READY slots until `extra` beyond prefetch are staged (never blocks).
   void stage_ready(int extra);
   // A batch parsed by a group launch on another stream: `stream` waits for that kernel.
-  void wait_group(const SlotView& v, hipStream_t stream) {
-    if (waited_ev_slot_ == v.pre_event_slot && waited_stream_ == stream) return;  // one wait per group
-    eng_->stream_wait_done(int(v.pre_event_slot), stream);
-    waited_ev_slot_ = v.pre_event_slot;
-    waited_stream_ = stream;
-  }
-  const SlotView& group_member(size_t k) const { return staged_[group_idx_[k]]; }
+  void wait_group(const SlotView& v, hipStream_t stream) { wait_event_slot(v.pre_event_slot, stream); }
+  const SlotView& group_member(size_t k) const { return poller_->staged()[group_idx_[k]]; }
   void json_group_launch(hipStream_t stream, int dst_dt, double pad, void* const* outs, const int64_t* Ls,
                          int64_t* const* lengths, uint8_t* const* masks,
                          std::vector<std::shared_ptr<void>>&& handles);
@@ -153,7 +131,7 @@ class MainDriver {
                     std::vector<std::shared_ptr<void>>&& handles);
   // The batches of the group ahead_begin formed (JSON: their row counts and max row lengths size
   // the outputs), and the JSON-span variant of ahead_launch (outputs as json_group_launch).
-  const SlotView& ahead_member(size_t k) const { return staged_[group_idx_[k]]; }
+  const SlotView& ahead_member(size_t k) const { return poller_->staged()[group_idx_[k]]; }
   void ahead_launch_json(int dst_dt, double pad, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
                          uint8_t* const* masks, std::vector<std::shared_ptr<void>>&& handles);
   void set_ahead_depth(int n) { ahead_depth_ = n < 0 ? 0 : n; }
@@ -165,20 +143,16 @@ class MainDriver {
   // *n_host, the rows that were not simple.  json_host_rows: parses those rows on the host (from the
   // pinned logs, when the batch is delivered or its slot released, whichever comes first) and
   // writes them into the batch's outputs on `stream`, which it then synchronizes.
-  int64_t json_width(const SlotView& v, int64_t* n_host);
+  int64_t json_width(const SlotView& v, int64_t* n_host) { return verdicts_->json_width(v.perr, n_host); }
   void json_host_rows(const SlotView& v, void* out, int64_t L, int dst_dt, double pad, int64_t* lengths,
-                      uint8_t* mask, hipStream_t stream);
+                      uint8_t* mask, hipStream_t stream) {
+    verdicts_->json_host_rows(v.g, v.perr, v.trunc_len, out, L, dst_dt, pad, lengths, mask, stream);
+  }
   hipStream_t last_stream() const { return last_stream_; }
   int64_t last_perr() const { return last_perr_; }
   // LDS-DMA loads a wave of the span decode kernel keeps in flight before it waits (0 = all;
   // default 1; TORCHKAFKA_SPAN_BURST)
   void set_span_burst(int n) { span_burst_ = n < 0 ? 0 : n > 8 ? 8 : n; }
-  int span_burst_ = [] {
-    const char* e = std::getenv("TORCHKAFKA_SPAN_BURST");
-    const int v = e ? std::atoi(e) : 1;
-    return v < 0 ? 0 : v > 8 ? 8 : v;
-  }();
-  int ahead_depth_ = 4;  // config 2: depth 0 52.2 M, 3-6 52.3-52.7 M steady, and 54 M over 2000 steps
   // The stream the next device-decode group launch runs on (its outputs are allocated there).
   hipStream_t next_decode_stream() { return eng_->decode_stream(int(span_launches_ % 4096)); }
   void set_coalesce(int n) { coalesce_ = n < 1 ? 1 : (n > kMaxGroup ? kMaxGroup : n); }
@@ -186,49 +160,46 @@ class MainDriver {
   // together when its kernel completes, so 8 x 8 MiB batches (config 5) would hold every commit for
   // a 64 MiB transfer (~1.3 ms); small batches still group 8 at a time.
   void set_group_bytes(uint64_t b) { group_bytes_max_ = b < (1u << 20) ? (1u << 20) : b; }
-  uint64_t group_bytes_max_ = uint64_t(16) << 20;
-  bool group_capped_ = false;  // extend_group stopped at group_bytes_max_
-  bool group_full(uint64_t bytes, const SlotView& next) const {
-    return next.span_bytes > 0 && bytes > 0 && bytes + next.span_bytes > group_bytes_max_;
-  }
   // Adaptive coalescing: while the GPU is still running an earlier launch, wait up to `us` for
   // more staged batches so the next launch carries a full group (0 disables).  Waiting costs no
   // GPU time -- the GPU is busy anyway -- and a zero-copy batch costs 7.1 us alone but 5.2 us
   // in a group of 4 (PCIe latency amortised).
   void set_coalesce_wait_us(int64_t us) { coalesce_wait_ns_ = us < 0 ? 0 : us * 1000; }
 
-  // h2d="direct": the workers' slots hold log locations (kPackGatherFixed); the driver pins each
-  // partition log in place (hipHostRegister, kLogChunk at a time, just ahead of what a slot
-  // references) and keeps a device table of their addresses for the gather kernel.
-  static constexpr uint64_t kLogChunk = uint64_t(64) << 20;
-  void enable_direct();
+  // h2d="direct": the workers' slots hold log locations (kPackGatherFixed); the logs are pinned in
+  // place just ahead of what a slot references, with a device table of their addresses.
+  static constexpr uint64_t kLogChunk = LogPins::kChunk;
+  void enable_direct() { pins_->enable_direct(); }
   // Device decode / direct: pin the logs of these partitions as far as they are written now (the
   // retained backlog), so their registration (~13 GB/s of fresh pages on the MI355X host) is paid
   // when the iteration starts instead of by the first batches that reach each partition.
-  void pin_logs(const std::vector<uint32_t>& pidxs);
-  bool direct() const { return direct_; }
+  void pin_logs(const std::vector<uint32_t>& pidxs) { pins_->pin_written(pidxs); }
+  bool direct() const { return pins_->direct(); }
   // h2d='dma' with device decode: the decode kernels read the logs from an HBM mirror that the copy
   // engines fill chunk by chunk (log_mirror.h) instead of over PCIe from the pinned logs.
-  void enable_mirror(uint64_t chunk_bytes, int chunks_per_partition);
-  const LogMirror* mirror() const { return mirror_.get(); }
-  uint64_t log_bytes_registered() const { return reg_total_; }
-  uint64_t log_bytes_unpinned() const { return unpinned_bytes_; }
-  int64_t log_register_ns() const { return reg_ns_; }
+  void enable_mirror(uint64_t chunk_bytes, int chunks_per_partition) {
+    pins_->enable_mirror(chunk_bytes, chunks_per_partition);
+  }
+  const LogMirror* mirror() const { return pins_->mirror(); }
+  uint64_t log_bytes_registered() const { return pins_->bytes_registered(); }
+  uint64_t log_bytes_unpinned() const { return pins_->bytes_unpinned(); }
+  int64_t log_register_ns() const { return pins_->register_ns(); }
   int coalesce() const { return coalesce_; }
   int64_t groups() const { return groups_; }
 
   const std::vector<tk::Watermark>& delivered() const { return delivered_; }
-  std::vector<std::pair<uint32_t, int64_t>> committed() const;
-  std::vector<std::pair<uint32_t, int64_t>> take_pending();
-  bool worker_done(uint32_t w) const { return done_.at(w) != 0; }
-  uint64_t commits() const { return commits_; }
-  uint64_t commit_failures() const { return commit_failures_; }
-  const std::vector<int64_t>& commit_ns() const { return commit_ns_; }
+  std::vector<std::pair<uint32_t, int64_t>> committed() const { return ledger_->committed(); }
+  std::vector<std::pair<uint32_t, int64_t>> take_pending() { return ledger_->take_pending(); }
+  bool worker_done(uint32_t w) const { return poller_->worker_done(w); }
+  uint64_t commits() const { return ledger_->commits(); }
+  uint64_t commit_failures() const { return ledger_->commit_failures(); }
+  const std::vector<int64_t>& commit_ns() const { return ledger_->commit_ns(); }
   // Commit latency per batch: from the request that finished batch k (the user asking for k+1)
   // to k's offsets being stored -- including the wait for its decode kernel's CRC verdict, the
   // user's GPU work (commit_on='device') and the cross-rank lockstep agreement.  With the worker
   // commit sink it ends when the offsets are handed to the workers.
-  const std::vector<int64_t>& commit_latency_ns() const { return commit_lat_ns_; }
+  const std::vector<int64_t>& commit_latency_ns() const { return ledger_->commit_latency_ns(); }
+  const RingPoller::Stats& poll_stats() const { return poller_->stats; }
   void reset_stats();
 
   // Cross-rank lockstep over RCCL, pipelined `depth` steps ahead (ls is owned by the caller).
@@ -248,144 +219,12 @@ class MainDriver {
   void set_event_every(int n) { event_every_ = n < 1 ? 1 : n; }
   int event_every() const { return event_every_; }
 
- private:
-  int poll_one(bool block, int64_t timeout_ms);
-  int poll_one_impl(bool block, int64_t timeout_ms);
-  void release_completed();
-  void release_completed_impl();
-  static constexpr int64_t kReleaseRequeryNs = 3000;
-  int64_t pending_query_ns_ = 0;  // when an event was last found pending (release_completed)
-  int64_t busy_query_ns_ = 0;     // when gpu_busy() last found the latest launch running
-  void note_handed(int64_t g, hipStream_t stream, bool* record);  // decides whether slot g records its event
-  void cover_handed();  // records an event for the newest handed slot without one
-  int poll_blocking(int64_t timeout_ms);  // blocks for a slot, releasing completed ones meanwhile
-  int next_slot_lockstep(int64_t timeout_ms, SlotView* out);
-  int data_staged() const;
-  void prefetch_ready() const;
-  bool all_done() const;
-  bool pop_data(SlotView* out);
-
-  void stage_finished(int64_t index, std::vector<tk::Watermark>&& wms);
-  void batch_committable(const std::vector<tk::Watermark>& wms);
-  void settle_commit_latency(bool durable);
-  bool commit_on_device_ = false;
-  // (event or null, batch index, watermarks, parse-error word index or -1).  A device-parsed
-  // batch needs no event of its own: it becomes committable once its slot was released (its
-  // kernel completed) and its error word read clean (perr_state_).
-  std::deque<std::tuple<hipEvent_t, int64_t, std::vector<tk::Watermark>, int64_t>> fenced_;
-  std::vector<uint8_t> perr_state_;  // per error word: 0 kernel pending, 1 clean, 2 malformed row
-  void settle_parse_errors(bool wait);
-  void ensure_status();
-  int64_t next_err_word();
-  // Span decode: CRC chains of RecordBatches split over segments, verdict and message (at release).
-  void check_span(int64_t g, int64_t pe);
-  int ext_n_ = 0;                  // set_extra_outputs(): destinations of the next launch
-  int64_t* ext_dsts_[kMaxGroup] = {};
-  // host-decoded fixed-width batches: their record fields copied beside the collate (same stream)
-  void copy_extras(const int* slots, const SlotView* const* views, int n, hipStream_t stream);
-  void launch_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
-                   void* const* dsts, const float* shift, const float* scale, bool record_last, int64_t* perrs);
-  void launch_json_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
-                        double pad, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
-                        uint8_t* const* masks, bool record_last, int64_t* perrs);
-  void launch_var_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
-                       double pad, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
-                       uint8_t* const* masks, bool record_last, int64_t* perrs);
-  // kPackJsonSpan or kPackVarSpan by the views' kind
-  void launch_row_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
-                       double pad, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
-                       uint8_t* const* masks, bool record_last, int64_t* perrs) {
-    if (views[0]->kind == uint32_t(tk::kPackVarSpan))
-      launch_var_span(slots, views, n, stream, dst_dt, pad, outs, Ls, lengths, masks, record_last, perrs);
-    else
-      launch_json_span(slots, views, n, stream, dst_dt, pad, outs, Ls, lengths, masks, record_last, perrs);
-  }
-  void ensure_partials();
-  // HBM staging ring of the device JSON parse (row texts between the two kernels, json_span.hip):
-  // positions are monotonic, regions are freed in launch order as their groups' slots are released.
-  static constexpr uint64_t kStageBytes = uint64_t(128) << 20;
-  uint8_t* stage_dev_ = nullptr;
-  uint64_t stage_head_ = 0, stage_tail_ = 0, stage_last_end_ = 0;
-  uint64_t stage_alloc(uint64_t bytes);
-  // One device-decode group launched on the next decode stream: slots handed out, the staged
-  // members marked pre-decoded (outputs in handles, offset by `first`: 1 when views[0] is `last`).
-  void span_group_handed(const int* slots, int n, hipStream_t ks, const int64_t* perrs,
-                         std::vector<std::shared_ptr<void>>&& handles, size_t first);
-  static constexpr int64_t kErrWords = 4096;
-  static constexpr int64_t kPartials = 512;  // raw CRC words per error word (segments of one slot)
-  uint32_t* part_host_ = nullptr;          // hipHostMalloc'ed, device-mapped partial CRCs
-  uint32_t* part_dev_ = nullptr;
-  std::vector<std::string> perr_msg_;      // span decode: the message of a bad batch, by error word
-  int32_t* perr_host_ = nullptr;  // hipHostMalloc'ed, device-mapped error words (one per JSON launch)
-  int32_t* perr_dev_ = nullptr;
-  // Device-counted JSON: per error word {width, rows left to the host, done} (host-mapped, written
-  // by the parse kernel), and the host-parsed values of those rows (json_host_rows).
-  struct HostRow {
-    int64_t row;
-    int32_t count;
-    std::vector<float> vals;
-  };
-  int32_t* jinfo_host_ = nullptr;
-  int32_t* jinfo_dev_ = nullptr;
-  int32_t json_mult_ = 1;
-  std::vector<std::vector<HostRow>> jrows_;
-  std::vector<uint8_t> jparsed_;  // per error word: its host rows were parsed (jrows_)
-  void json_parse_host_rows(int64_t g, int64_t pe);
-  uint8_t* patch_dev_ = nullptr;
-  size_t patch_cap_ = 0;
-  uint64_t perr_seq_ = 0;
-  int64_t last_perr_ = -1, delivered_perr_ = -1;
-  std::string parse_error_;
-  std::vector<hipEvent_t> event_pool_;
-
-  // Cross-rank lockstep: the credit protocol (csrc/core/lockstep.h) over the caller's transport.
-  class Source;
-  std::unique_ptr<tk::CreditLockstep> ls_;
-  int64_t delivered_index_ = -1;
-
-  Engine* eng_;
-  bool registered_ = false;
-  std::unique_ptr<tk::Ring> ring_;
-  std::shared_ptr<tk::Broker> broker_;
-  uint32_t group_ = 0;
-  int prefetch_;
-  bool in_order_;
-  int default_src_dt_;
-  std::vector<uint32_t> cursor_;
-  std::vector<uint8_t> done_;
-  uint32_t rr_ = 0;
-  std::deque<SlotView> staged_;
-  struct Handed {
-    int64_t g;
-    bool ev;            // its own completion event was recorded
-    int64_t perr = -1;  // device JSON parse / span decode: its error word, checked at slot release
-    bool span = false;  // kPackRecordSpan: chain the partial CRCs of split RecordBatches at release
-    uint64_t stage_end = 0;  // kPackJsonSpan group: staging ring position freed when this slot is released
-  };
-  std::deque<Handed> handed_;  // slots whose collate was launched, in launch order
-  hipStream_t last_stream_ = nullptr;
-  int event_every_ = 1, unevented_ = 0;
-  std::vector<tk::Watermark> carry_;
-  std::vector<tk::Watermark> delivered_;
-  std::unordered_map<uint32_t, int64_t> pending_;
-  std::unordered_map<uint32_t, int64_t> committed_;
-  int64_t* sink_table_ = nullptr;  // WatermarkTable layout, see set_worker_sink
-  int sink_workers_ = 0, sink_cap_ = 0;
-  std::vector<std::unordered_map<uint32_t, int>> sink_index_;  // per worker: pidx -> entry
-  std::unordered_map<uint32_t, uint32_t> pidx_worker_;         // partition -> worker that delivers it
-  void publish_to_workers();
-  std::vector<tk::CommitEntry> entries_;
-  std::string error_;
-  uint64_t commits_ = 0, commit_failures_ = 0;
- public:
-  // profiling counters (ns): worker fill time of delivered slots, main time blocked on the ring
-  int64_t fill_ns_ = 0, fills_ = 0, blocked_ns_ = 0, blocked_calls_ = 0, ready_age_ns_ = 0, worker_idle_ns_ = 0,
-          worker_slot_wait_ns_ = 0;
-  std::vector<int64_t> last_ready_;
+  // profiling counters (ns): main time blocked on the ring
+  int64_t blocked_ns_ = 0, blocked_calls_ = 0;
   // step_fixed phases (ns): finish+commit of the previous batch, slot acquisition/release, collate launch
   int64_t ph_commit_ns_ = 0, ph_next_ns_ = 0, ph_launch_ns_ = 0, ph_steps_ = 0, events_ = 0;
-  // inside the next phase: slot releases (event queries + ring hand-back) and stagings of READY slots
-  int64_t rel_ns_ = 0, released_ = 0, polled_ = 0, poll_ns_ = 0;
+  // inside the next phase: slot releases (event queries + ring hand-back)
+  int64_t rel_ns_ = 0, released_ = 0;
   int64_t cwait_ns_ = 0;  // time spent waiting for a full group while the GPU was busy
   int64_t ahead_groups_ = 0;  // device-decode groups launched ahead of delivery
   int64_t occ_handed_ = 0, occ_staged_ = 0, occ_samples_ = 0;  // slots launched / staged, summed per step
@@ -405,39 +244,123 @@ class MainDriver {
     int extras = 0;  // record-field columns per batch (key / timestamp), 0: values only
   } fast;
   int64_t fast_batches_ = 0, fast_records_ = 0, fast_ns_ = 0;
+
  private:
-  std::vector<int64_t> commit_ns_;
-  std::vector<int64_t> commit_lat_ns_;
-  std::deque<int64_t> finish_t_;       // finish time of each delivered batch not yet committed
-  int64_t committable_batches_ = 0;    // of those, batches whose offsets are in pending_
-  int coalesce_ = 1;
-  int64_t groups_ = 0;
-  int64_t coalesce_wait_ns_ = 0;
-  int64_t last_ev_slot_ = -1;  // slot whose completion event was recorded by the latest launch
-  uint64_t span_launches_ = 0;  // device-decode group launches (they alternate between two streams)
-  int64_t waited_ev_slot_ = -1;       // the user's stream already waits for this slot's event ...
-  hipStream_t waited_stream_ = nullptr;  // ... (skips repeated waits for one group's batches)
+  // --- launched slots and their completion events
+  struct Handed {
+    int64_t g;
+    bool ev;            // its own completion event was recorded
+    int64_t perr = -1;  // device-checked batch: its status word, read at slot release
+    bool span = false;  // decoded from the logs: chain split RecordBatch CRCs at release
+    uint64_t stage_end = 0;  // kPackJsonSpan group: staging ring position freed when this slot is released
+  };
+  void release_completed();
+  void release_completed_impl();
+  static constexpr int64_t kReleaseRequeryNs = 3000;
+  int64_t pending_query_ns_ = 0;  // when an event was last found pending (release_completed)
+  int64_t busy_query_ns_ = 0;     // when gpu_busy() last found the latest launch running
+  void note_handed(int64_t g, hipStream_t stream, bool* record);  // decides whether slot g records its event
+  void force_event();   // the slot just handed records its event after all
+  void cover_handed();  // records an event for the newest handed slot without one
+  void switch_stream(hipStream_t stream);  // later launches run on `stream`
+  // One group launch on `stream` handed out slots[0..n): the last slot's event (after the kernel)
+  // releases them all.  Members from slots[first] on are staged batches (group_idx_) that are now
+  // collated ahead of delivery; handles keep their outputs alive.  perrs: status words or null.
+  void group_handed(const int* slots, int n, hipStream_t stream, const int64_t* perrs, bool span,
+                    std::vector<std::shared_ptr<void>>&& handles, size_t first);
+  void wait_event_slot(int64_t slot, hipStream_t stream);
+  int poll_blocking(int64_t timeout_ms);  // blocks for a slot, releasing completed ones meanwhile
   bool gpu_busy();
+  std::deque<Handed> handed_;  // slots whose collate was launched, in launch order
+  hipStream_t last_stream_ = nullptr;
+  int event_every_ = 1, unevented_ = 0;
+  int64_t last_ev_slot_ = -1;  // slot whose completion event was recorded by the latest launch
+  int64_t waited_ev_slot_ = -1;          // the user's stream already waits for this slot's event ...
+  hipStream_t waited_stream_ = nullptr;  // ... (skips repeated waits for one group's batches)
+
+  // --- group formation
   void extend_group();
-  void ensure_log(uint32_t pidx, uint64_t end);
+  bool group_full(uint64_t bytes, const SlotView& next) const {
+    return next.span_bytes > 0 && bytes > 0 && bytes + next.span_bytes > group_bytes_max_;
+  }
+  std::vector<size_t> group_idx_;  // staged indices of the batches behind `last` in the pending group
+  int coalesce_ = 1;
+  int64_t coalesce_wait_ns_ = 0;
+  uint64_t group_bytes_max_ = uint64_t(16) << 20;
+  bool group_capped_ = false;  // extend_group stopped at group_bytes_max_
+  int ahead_depth_ = 4;  // config 2: depth 0 52.2 M, 3-6 52.3-52.7 M steady, and 54 M over 2000 steps
+  int64_t groups_ = 0;
+  uint64_t span_launches_ = 0;  // device-decode group launches (they rotate over the decode streams)
+
+  // --- kernel launches
+  void copy_extras(const int* slots, const SlotView* const* views, int n, hipStream_t stream);
   void launch_group(const int* slots, const int64_t* rows, const size_t* voffs, int n, const SlotView& v,
                     hipStream_t stream, int dst_dt, void* const* dsts, int64_t row, const float* shift,
                     const float* scale);
-  bool direct_ = false;
-  std::unique_ptr<LogMirror> mirror_;
-  const uint8_t* seg_src(const tk::SpanSeg& sg);  // the address a decode kernel reads a segment from
-  uint64_t* bases_dev_ = nullptr;
-  std::vector<uint64_t> reg_end_;        // per pidx: bytes of its log pinned (and device-mapped)
-  // per pidx: pinned ranges (address, end position), unpinned once committed past (a replica
-  // broker, tk::kReleaseConsumed) or at teardown
-  std::vector<std::deque<std::pair<void*, uint64_t>>> reg_ranges_;
-  bool release_consumed_ = false;
-  uint64_t unpinned_bytes_ = 0;
-  uint64_t commits_since_release_ = 0;
-  void release_consumed();
-  uint64_t reg_total_ = 0;
-  int64_t reg_ns_ = 0;
-  std::vector<size_t> group_idx_;  // staged_ indices of the batches behind `last` in the pending group
+  void launch_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
+                   void* const* dsts, const float* shift, const float* scale, bool record_last, int64_t* perrs);
+  void launch_json_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
+                        double pad, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
+                        uint8_t* const* masks, bool record_last, int64_t* perrs);
+  void launch_var_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
+                       double pad, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
+                       uint8_t* const* masks, bool record_last, int64_t* perrs);
+  // kPackJsonSpan or kPackVarSpan by the views' kind
+  void launch_row_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
+                       double pad, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
+                       uint8_t* const* masks, bool record_last, int64_t* perrs) {
+    if (views[0]->kind == uint32_t(tk::kPackVarSpan))
+      launch_var_span(slots, views, n, stream, dst_dt, pad, outs, Ls, lengths, masks, record_last, perrs);
+    else
+      launch_json_span(slots, views, n, stream, dst_dt, pad, outs, Ls, lengths, masks, record_last, perrs);
+  }
+  const tk::SpanSeg* segs(const SlotView& v) {
+    return reinterpret_cast<const tk::SpanSeg*>(poller_->ring().payload(uint32_t(v.g)) + v.values_offset);
+  }
+  void check_seg_count(const tk::SpanSeg& sg, uint32_t i) const;
+  static void fill_seg(SpanDevSeg& d, const tk::SpanSeg& sg, const uint8_t* src, int k, uint32_t i);
+  int ext_n_ = 0;  // set_extra_outputs(): destinations of the next launch
+  int64_t* ext_dsts_[kMaxGroup] = {};
+  int span_burst_ = [] {
+    const char* e = std::getenv("TORCHKAFKA_SPAN_BURST");
+    const int v = e ? std::atoi(e) : 1;
+    return v < 0 ? 0 : v > 8 ? 8 : v;
+  }();
+  int32_t json_mult_ = 1;
+  // HBM staging ring of the device JSON parse (row texts between the two kernels, json_span.hip):
+  // positions are monotonic, regions are freed in launch order as their groups' slots are released.
+  static constexpr uint64_t kStageBytes = uint64_t(128) << 20;
+  uint8_t* stage_dev_ = nullptr;
+  uint64_t stage_head_ = 0, stage_tail_ = 0, stage_last_end_ = 0;
+  uint64_t stage_alloc(uint64_t bytes);
+
+  // --- delivery, fencing and the commit decision
+  void stage_finished(int64_t index, std::vector<tk::Watermark>&& wms);
+  void settle_parse_errors(bool wait);
+  int next_slot_lockstep(int64_t timeout_ms, SlotView* out);
+  bool commit_on_device_ = false;
+  // (event or null, batch index, watermarks, status word or -1).  A device-checked batch needs no
+  // event of its own: it becomes committable once its slot was released (its kernel completed)
+  // and its status word read clean.
+  std::deque<std::tuple<hipEvent_t, int64_t, std::vector<tk::Watermark>, int64_t>> fenced_;
+  std::vector<hipEvent_t> event_pool_;
+  std::vector<tk::Watermark> delivered_;
+  int64_t delivered_index_ = -1;
+  int64_t last_perr_ = -1, delivered_perr_ = -1;
+  std::string parse_error_;
+
+  // Cross-rank lockstep: the credit protocol (csrc/core/lockstep.h) over the caller's transport.
+  class Source;
+  std::unique_ptr<tk::CreditLockstep> ls_;
+
+  Engine* eng_;
+  bool registered_ = false;
+  int prefetch_;
+  std::shared_ptr<tk::Broker> broker_;
+  std::unique_ptr<CommitLedger> ledger_;
+  std::unique_ptr<LogPins> pins_;
+  std::unique_ptr<RingPoller> poller_;  // owns the ring mapping: destroyed after the members above use it
+  std::unique_ptr<BatchVerdicts> verdicts_;
 };
 
 }  // namespace tkh

@@ -1,7 +1,7 @@
 """Native ops: host core (_tkcore) and gfx950 collate kernels (_tkhip)."""
-from .native import core, hip, loaded_extensions
+from .native import build_info, core, hip, loaded_extensions
 
-__all__ = ["core", "hip", "loaded_extensions", "collate_fixed", "collate_varlen"]
+__all__ = ["build_info", "core", "hip", "loaded_extensions", "collate_fixed", "collate_varlen"]
 
 
 def __getattr__(name):

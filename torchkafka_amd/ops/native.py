@@ -32,9 +32,8 @@ def _load(name: str, builder: str):
         target = getattr(_build, f"{builder}_target")()
         stale = not target.exists()
         if not stale and os.environ.get("TORCHKAFKA_NO_REBUILD") != "1":
-            # rebuild when sources are newer than the binary (dev checkouts)
-            srcs = list((_build.CSRC / builder).glob("*"))
-            stale = any(p.stat().st_mtime > target.stat().st_mtime for p in srcs)
+            # rebuild when the binary was built from other sources than the tree's (its embedded sha)
+            stale = not _build.up_to_date(builder)
         if stale:
             lock_path = _PKG.parent / "build" / f".{builder}.lock"
             lock_path.parent.mkdir(parents=True, exist_ok=True)
@@ -68,3 +67,20 @@ def hip():
 
 def loaded_extensions() -> list[str]:
     return sorted(_mods)
+
+
+def build_info() -> dict:
+    """Provenance of the loaded extensions: the source sha each binary was built from (compiled
+    in), the sha of the sources in this tree, whether they match, and the file it was loaded from."""
+    from .. import _build
+
+    out = {}
+    for name, builder in (("_tkcore", "core"), ("_tkhip", "hip")):
+        mod = _mods.get(name)
+        if mod is None:
+            continue
+        tree = _build.sources_sha(builder)
+        built = getattr(mod, "SOURCES_SHA", None)
+        out[name] = {"built_from": built, "tree": tree, "matches_tree": built == tree,
+                     "file": os.path.relpath(mod.__file__, _PKG.parent)}
+    return out
