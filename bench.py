@@ -359,6 +359,8 @@ def run_rank(args) -> int:
     if device.type != "cuda":
         extra = [b for b in extra if b != "dma"]
     extra_steps = args.extra_steps if args.extra_steps is not None else steady
+    if extra_steps <= 0:
+        extra = []
     extra_warm = max(50, args.warmup)
     consumed = max(args.warmup + args.steps + steady, (extra_warm + extra_steps) if extra else 0)
     batches = consumed + args.workers * ((args.slots_per_worker or 8) + 2)

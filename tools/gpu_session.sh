@@ -37,11 +37,11 @@ for s in ${STEPS:-pytest_new}; do
     benchlockr) run bench_lock_rccl 300 python bench.py --lockstep rccl --stats ;;
     profbench) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/profbench" -o run -- python3 "$OLDPWD/bench.py" --steps 1000 --steady-steps 2000 > "$OLDPWD/gpurun_out/profbench.log" 2>&1) || exit $?
             tail -2 gpurun_out/profbench.log ;;
-    pmcspan) (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OLDPWD/gpurun_out/pmc_span" -o run -- python3 "$OLDPWD/bench.py" --steps 200 --warmup 20 --steady-steps 0 > "$OLDPWD/gpurun_out/pmc_span.log" 2>&1) || exit $?
+    pmcspan) (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OLDPWD/gpurun_out/pmc_span" -o run -- python3 "$OLDPWD/bench.py" --steps 200 --warmup 20 --steady-steps 0 --extra-blocks "" --bridge-steps 0 > "$OLDPWD/gpurun_out/pmc_span.log" 2>&1) || exit $?
              tail -2 gpurun_out/pmc_span.log ;;
     pmcjspan) (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OLDPWD/gpurun_out/pmc_jspan" -o run -- python3 "$OLDPWD/benchmarks/config4_json_varlen.py" --steps 200 --warmup 10 > "$OLDPWD/gpurun_out/pmc_jspan.log" 2>&1) || exit $?
              tail -2 gpurun_out/pmc_jspan.log ;;
-    pmcfetch) (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE WRITE_SIZE SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d "$OLDPWD/gpurun_out/pmc_fetch_span" -o run -- python3 "$OLDPWD/bench.py" --steps 200 --warmup 20 --steady-steps 0 --h2d dma > "$OLDPWD/gpurun_out/pmc_fetch_span.log" 2>&1) || exit $?
+    pmcfetch) (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE WRITE_SIZE SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d "$OLDPWD/gpurun_out/pmc_fetch_span" -o run -- python3 "$OLDPWD/bench.py" --steps 200 --warmup 20 --steady-steps 0 --extra-blocks "" --bridge-steps 0 --h2d dma > "$OLDPWD/gpurun_out/pmc_fetch_span.log" 2>&1) || exit $?
              tail -2 gpurun_out/pmc_fetch_span.log ;;
     aheaddrv) for a in 1 2 3 4 6; do TORCHKAFKA_AHEAD_DEPTH=$a run bench_drv_ahead$a 300 python bench.py --gpus 1 --steps 20 --warmup 5; done ;;
     tokens) run tokens_device 300 python benchmarks/varlen_tokens.py

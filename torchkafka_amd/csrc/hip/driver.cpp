@@ -141,8 +141,9 @@ void MainDriver::force_event() {
   ++events_;
 }
 
-void MainDriver::group_handed(const int* slots, int n, hipStream_t stream, const int64_t* perrs, bool span,
-                              std::vector<std::shared_ptr<void>>&& handles, size_t first) {
+int64_t MainDriver::group_handed(const int* slots, int n, hipStream_t stream, const int64_t* perrs, bool span,
+                                 std::vector<std::shared_ptr<void>>&& handles, size_t first) {
+  const int64_t gid = ++group_seq_;
   for (int k = 0; k < n; ++k) handed_.push_back(Handed{slots[k], k == n - 1, perrs ? perrs[k] : -1, span});
   handed_.back().stage_end = stage_last_end_;  // 0 unless a JSON group just took a staging region
   stage_last_end_ = 0;
@@ -157,14 +158,16 @@ void MainDriver::group_handed(const int* slots, int n, hipStream_t stream, const
     v.pre = true;
     v.pre_stream = stream;
     v.pre_event_slot = slots[n - 1];
+    v.pre_group = gid;
     v.pre_out = std::move(handles[k - first]);
   }
+  return gid;
 }
 
-void MainDriver::wait_event_slot(int64_t slot, hipStream_t stream) {
-  if (waited_ev_slot_ == slot && waited_stream_ == stream) return;  // one wait per group
+void MainDriver::wait_launch(int64_t slot, int64_t group, hipStream_t stream) {
+  if (waited_group_ == group && waited_stream_ == stream) return;  // one wait per group
   eng_->stream_wait_done(int(slot), stream);
-  waited_ev_slot_ = slot;
+  waited_group_ = group;
   waited_stream_ = stream;
 }
 
@@ -674,8 +677,8 @@ void MainDriver::json_group_launch(hipStream_t stream, int dst_dt, double pad, v
     last_stream_ = ks;
     launch_row_span(slots, vs, n, ks, dst_dt, pad, outs, Ls, lengths, masks, true, perrs);
     last.perr = perrs[0];
-    group_handed(slots, n, ks, perrs, true, std::move(handles), 1);
-    wait_event_slot(slots[n - 1], stream);
+    const int64_t gid = group_handed(slots, n, ks, perrs, true, std::move(handles), 1);
+    wait_launch(slots[n - 1], gid, stream);
     group_idx_.clear();
     return;
   }
@@ -744,7 +747,7 @@ int64_t MainDriver::step_group_begin(hipStream_t stream, bool auto_commit, int64
   if (r < 0) return r;
   if (last.pre) {
     // collated by an earlier group launch; a consumer on another stream waits for that kernel
-    if (last.pre_stream != stream) wait_event_slot(last.pre_event_slot, stream);
+    if (last.pre_stream != stream) wait_launch(last.pre_event_slot, last.pre_group, stream);
     *pre_out = std::move(last.pre_out);
     set_delivered(last);
     poller_->prefetch_ready();
@@ -824,8 +827,8 @@ void MainDriver::step_group_launch(hipStream_t stream, int dst_dt, void* const* 
     int64_t perrs[kMaxGroup];
     launch_span(slots, vs, n, ks, dst_dt, dsts, shift, scale, true, perrs);
     last.perr = perrs[0];
-    group_handed(slots, n, ks, perrs, true, std::move(handles), 1);
-    wait_event_slot(slots[n - 1], stream);
+    const int64_t gid = group_handed(slots, n, ks, perrs, true, std::move(handles), 1);
+    wait_launch(slots[n - 1], gid, stream);
   } else if (n == 1) {
     collate_fixed(last, stream, dst_dt, dsts[0], row, shift, scale);
   } else {

@@ -114,7 +114,7 @@ class MainDriver {
   // Stages READY slots until `extra` beyond prefetch are staged (never blocks).
   void stage_ready(int extra);
   // A batch parsed by a group launch on another stream: `stream` waits for that kernel.
-  void wait_group(const SlotView& v, hipStream_t stream) { wait_event_slot(v.pre_event_slot, stream); }
+  void wait_group(const SlotView& v, hipStream_t stream) { wait_launch(v.pre_event_slot, v.pre_group, stream); }
   const SlotView& group_member(size_t k) const { return poller_->staged()[group_idx_[k]]; }
   void json_group_launch(hipStream_t stream, int dst_dt, double pad, void* const* outs, const int64_t* Ls,
                          int64_t* const* lengths, uint8_t* const* masks,
@@ -266,16 +266,19 @@ class MainDriver {
   // One group launch on `stream` handed out slots[0..n): the last slot's event (after the kernel)
   // releases them all.  Members from slots[first] on are staged batches (group_idx_) that are now
   // collated ahead of delivery; handles keep their outputs alive.  perrs: status words or null.
-  void group_handed(const int* slots, int n, hipStream_t stream, const int64_t* perrs, bool span,
-                    std::vector<std::shared_ptr<void>>&& handles, size_t first);
-  void wait_event_slot(int64_t slot, hipStream_t stream);
+  // Returns the launch's sequence number.
+  int64_t group_handed(const int* slots, int n, hipStream_t stream, const int64_t* perrs, bool span,
+                       std::vector<std::shared_ptr<void>>&& handles, size_t first);
+  // `stream` waits for group launch `group` (its last slot's completion event), once per stream.
+  void wait_launch(int64_t slot, int64_t group, hipStream_t stream);
   int poll_blocking(int64_t timeout_ms);  // blocks for a slot, releasing completed ones meanwhile
   bool gpu_busy();
   std::deque<Handed> handed_;  // slots whose collate was launched, in launch order
   hipStream_t last_stream_ = nullptr;
   int event_every_ = 1, unevented_ = 0;
   int64_t last_ev_slot_ = -1;  // slot whose completion event was recorded by the latest launch
-  int64_t waited_ev_slot_ = -1;          // the user's stream already waits for this slot's event ...
+  int64_t group_seq_ = 0;                // group launches so far
+  int64_t waited_group_ = -1;            // the user's stream already waits for this launch ...
   hipStream_t waited_stream_ = nullptr;  // ... (skips repeated waits for one group's batches)
 
   // --- group formation

@@ -45,6 +45,7 @@ struct SlotView {
   bool pre = false;
   hipStream_t pre_stream = nullptr;
   int64_t pre_event_slot = -1;        // slot whose completion event follows the group kernel
+  int64_t pre_group = -1;             // that group launch's sequence number (slot numbers recur)
   std::shared_ptr<void> pre_out;      // the output tensor (opaque here: libtorch stays in torch_step.cpp)
   int64_t perr = -1;                  // device-checked batch: its status word (set at launch)
 };

@@ -39,6 +39,20 @@ def _set_worker_info(worker_id: int, num_workers: int, seed: int, dataset) -> No
     _w._worker_info = _w.WorkerInfo(id=worker_id, num_workers=num_workers, seed=seed, dataset=dataset)
 
 
+def _die_with_parent() -> None:
+    """A worker never outlives the process that forked it (PR_SET_PDEATHSIG): a main process that
+    dies or is killed without closing its loader leaves no worker holding the ring or the broker."""
+    try:
+        import ctypes
+        import signal
+
+        ctypes.CDLL(None, use_errno=True).prctl(1, int(signal.SIGKILL), 0, 0, 0)  # PR_SET_PDEATHSIG
+    except (OSError, AttributeError):
+        return
+    if os.getppid() == 1:  # the parent died before the call
+        os._exit(1)
+
+
 def worker_main(ring, ring_name: str, worker_id: int, num_workers: int, dataset, worker_init_fn, cfg: dict) -> None:
     """Entry point of a DeviceLoader worker process."""
     if ring is None:
@@ -51,6 +65,7 @@ def worker_main(ring, ring_name: str, worker_id: int, num_workers: int, dataset,
     state = {"i": 0, "g": None}
     try:
         if not in_process:  # process-wide state belongs to the user in single-process mode
+            _die_with_parent()
             torch.set_num_threads(1)
             seed = int(cfg.get("base_seed", 0)) + worker_id
             random.seed(seed)
