@@ -27,6 +27,10 @@ for s in ${STEPS:-pytest_new}; do
     profc4) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/profc4" -o run -- python3 "$OLDPWD/benchmarks/config4_json_varlen.py" --steps 300 > "$OLDPWD/gpurun_out/profc4.log" 2>&1) || exit $?
             tail -5 gpurun_out/profc4.log ;;
     dmasweep) for c in 2 4 16 32; do run bench_dma_c$c 300 python bench.py --stats --h2d dma --mirror-chunk-mib $c --steps 1000; done ;;
+    profc4api) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --runtime-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/profc4api" -o run -- python3 "$OLDPWD/benchmarks/config4_json_varlen.py" --steps 2000 > "$OLDPWD/gpurun_out/profc4api.log" 2>&1) || exit $?
+            tail -2 gpurun_out/profc4api.log ;;
+    profbenchapi) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --runtime-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/profbenchapi" -o run -- python3 "$OLDPWD/bench.py" --steps 2000 --steady-steps 4000 --extra-blocks "" --bridge-steps 0 > "$OLDPWD/gpurun_out/profbenchapi.log" 2>&1) || exit $?
+            tail -2 gpurun_out/profbenchapi.log ;;
     profdma) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/profdma" -o run -- python3 "$OLDPWD/bench.py" --h2d dma --steps 1000 --steady-steps 1000 > "$OLDPWD/gpurun_out/profdma.log" 2>&1) || exit $?
             tail -3 gpurun_out/profdma.log ;;
     config5) run config5 300 python benchmarks/config5_large_messages.py ;;
@@ -35,7 +39,7 @@ for s in ${STEPS:-pytest_new}; do
     benchf32) run bench_f32 300 python bench.py --stats --dtype f32 ;;
     benchhost) run bench_host 300 python bench.py --stats --decode host ;;
     benchlockr) run bench_lock_rccl 300 python bench.py --lockstep rccl --stats ;;
-    profbench) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/profbench" -o run -- python3 "$OLDPWD/bench.py" --steps 1000 --steady-steps 2000 > "$OLDPWD/gpurun_out/profbench.log" 2>&1) || exit $?
+    profbench) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/profbench" -o run -- python3 "$OLDPWD/bench.py" --steps 1000 --steady-steps 2000 --extra-blocks "" --bridge-steps 0 > "$OLDPWD/gpurun_out/profbench.log" 2>&1) || exit $?
             tail -2 gpurun_out/profbench.log ;;
     pmcspan) (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OLDPWD/gpurun_out/pmc_span" -o run -- python3 "$OLDPWD/bench.py" --steps 200 --warmup 20 --steady-steps 0 --extra-blocks "" --bridge-steps 0 > "$OLDPWD/gpurun_out/pmc_span.log" 2>&1) || exit $?
              tail -2 gpurun_out/pmc_span.log ;;
@@ -43,7 +47,7 @@ for s in ${STEPS:-pytest_new}; do
              tail -2 gpurun_out/pmc_jspan.log ;;
     pmcfetch) (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE WRITE_SIZE SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d "$OLDPWD/gpurun_out/pmc_fetch_span" -o run -- python3 "$OLDPWD/bench.py" --steps 200 --warmup 20 --steady-steps 0 --extra-blocks "" --bridge-steps 0 --h2d dma > "$OLDPWD/gpurun_out/pmc_fetch_span.log" 2>&1) || exit $?
              tail -2 gpurun_out/pmc_fetch_span.log ;;
-    aheaddrv) for a in 1 2 3 4 6; do TORCHKAFKA_AHEAD_DEPTH=$a run bench_drv_ahead$a 300 python bench.py --gpus 1 --steps 20 --warmup 5; done ;;
+    aheaddrv) for a in 0 1 2 4; do for rep in 1 2; do TORCHKAFKA_AHEAD_DEPTH=$a run bench_drv_ahead${a}_$rep 300 python bench.py --gpus 1 --steps 20 --warmup 5 --steady-steps 0 --extra-blocks "" --bridge-steps 0; done; done ;;
     tokens) run tokens_device 300 python benchmarks/varlen_tokens.py
             run tokens_host 300 python benchmarks/varlen_tokens.py --decode host ;;
     tokenslong) run tokens_long_device 300 python benchmarks/varlen_tokens.py --min-len 2048 --max-len 8192 --batch-size 32 --steps 2000

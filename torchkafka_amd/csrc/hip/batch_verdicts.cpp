@@ -32,6 +32,7 @@ BatchVerdicts::~BatchVerdicts() {
   if (jinfo_host_) hipHostFree(jinfo_host_);
   if (patch_dev_) hipFree(patch_dev_);
   if (part_host_) hipHostFree(part_host_);
+  if (ctr_dev_) hipFree(ctr_dev_);
 }
 
 void BatchVerdicts::ensure_status() {
@@ -42,6 +43,10 @@ void BatchVerdicts::ensure_status() {
   std::memset(jinfo_host_, 0, size_t(kWords) * 4 * sizeof(int32_t));
   jrows_.assign(size_t(kWords), {});
   jparsed_.assign(size_t(kWords), 0);
+  if (hipMalloc(reinterpret_cast<void**>(&ctr_dev_), size_t(kWords) * 2 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(ctr_dev_, 0, size_t(kWords) * 2 * sizeof(unsigned long long)) != hipSuccess)
+    throw std::runtime_error("driver: allocating the JSON count words failed");
+  tag_.assign(size_t(kWords), 0);
 }
 
 void BatchVerdicts::ensure_partials() {
@@ -52,7 +57,9 @@ void BatchVerdicts::ensure_partials() {
 
 int64_t BatchVerdicts::next_word() {
   ensure_status();
-  const int64_t w = int64_t(seq_++ % uint64_t(kWords));
+  const int64_t w = int64_t(seq_ % uint64_t(kWords));
+  tag_[size_t(w)] = uint32_t(seq_ / uint64_t(kWords)) + 1;  // 0 is the zeroed words' tag
+  ++seq_;
   if (state_[size_t(w)] == 0) throw std::runtime_error("driver: more than 4096 device-checked batches awaiting their kernels");
   perr_host_[w] = -1;
   jinfo_host_[w * 4 + 1] = 0;
@@ -121,7 +128,7 @@ std::string BatchVerdicts::failure(int64_t w, const std::vector<tk::Watermark>& 
   return "batch row " + std::to_string(row) + " is not a flat numeric JSON array (device parse; batch: " + where + ")";
 }
 
-int64_t BatchVerdicts::json_width(int64_t w, int64_t* n_host) const {
+int64_t BatchVerdicts::json_width(int64_t w, int64_t* n_host) {
   *n_host = 0;
   if (w < 0 || !jinfo_host_) throw std::logic_error("driver: json_width of a batch without a parse launch");
   const int32_t* info = jinfo_host_ + w * 4;
@@ -138,6 +145,7 @@ int64_t BatchVerdicts::json_width(int64_t w, int64_t* n_host) const {
     timespec ts{0, 20000};
     nanosleep(&ts, nullptr);
   }
+  width_wait_ns += tk::now_ns() - t0;
   *n_host = __atomic_load_n(info + 1, __ATOMIC_ACQUIRE);
   return __atomic_load_n(info, __ATOMIC_ACQUIRE);
 }

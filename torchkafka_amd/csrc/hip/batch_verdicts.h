@@ -36,6 +36,10 @@ class BatchVerdicts {
   int32_t* err_dev(int64_t w) const { return perr_dev_ + w; }
   uint32_t* partials_dev(int64_t w) const { return part_dev_ + w * kPartials; }
   int32_t* json_info_dev(int64_t w) const { return jinfo_dev_ + w * 4; }
+  // Device-counted JSON: word w's two count words in HBM (zeroed once) and the tag of its current
+  // launch (the number of times w was taken: higher than every earlier tag of these words).
+  unsigned long long* json_ctr_dev(int64_t w) const { return ctr_dev_ + w * 2; }
+  uint32_t ctr_tag(int64_t w) const { return tag_[size_t(w)]; }
 
   // 0 kernel pending, 1 clean, 2 malformed (read when the slot was released)
   uint8_t state(int64_t w) const { return state_[size_t(w)]; }
@@ -48,7 +52,8 @@ class BatchVerdicts {
 
   // Device-counted JSON (kSlotDevCount): the width the parse kernel chose for the batch (waits for
   // its first block), rows it left to the host in *n_host, and those rows written on `stream`.
-  int64_t json_width(int64_t w, int64_t* n_host) const;
+  int64_t json_width(int64_t w, int64_t* n_host);
+  int64_t width_wait_ns = 0;  // host time json_width spent waiting for a parse kernel's report
   void json_host_rows(int64_t g, int64_t w, int32_t trunc_len, void* out, int64_t L, int dst_dt, double pad,
                       int64_t* lengths, uint8_t* mask, hipStream_t stream);
 
@@ -71,6 +76,8 @@ class BatchVerdicts {
   uint32_t* part_dev_ = nullptr;
   int32_t* jinfo_host_ = nullptr;  // device-counted JSON: {width, rows left to the host, done} per word
   int32_t* jinfo_dev_ = nullptr;
+  unsigned long long* ctr_dev_ = nullptr;  // [kWords][2] tagged count words (device memory)
+  std::vector<uint32_t> tag_;
   std::vector<uint8_t> state_;
   std::vector<std::string> msg_;  // span decode: the message of a bad batch, by word
   std::vector<std::vector<HostRow>> jrows_;

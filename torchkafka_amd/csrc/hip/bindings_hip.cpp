@@ -314,6 +314,8 @@ PYBIND11_MODULE(_tkhip, m) {
              s["groups"] = d.groups();
              s["coalesce_wait_ns"] = d.cwait_ns_;
              s["ahead_groups"] = d.ahead_groups_;
+             s["ahead_ns"] = d.ahead_ns_;
+             s["json_width_wait_ns"] = d.json_width_wait_ns();
              s["occ_handed"] = d.occ_handed_;
              s["occ_staged"] = d.occ_staged_;
              s["occ_samples"] = d.occ_samples_;

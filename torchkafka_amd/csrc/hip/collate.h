@@ -59,9 +59,12 @@ struct JsonGroupArgs {
   uint64_t vals_cap[kMaxGroup];
   int32_t err_tag;
   // Device-counted batches (kSlotDevCount): L[k] is only the capacity of out/mask; the width is
-  // min(L[k], ctr[k][0] rounded up to `mult`) (mult 0: L[k], a fixed pad_to width), and the batch's first block stores {width, rows
-  // left to the host, 1} into the host-mapped info[k] (MainDriver::json_width).  nullptr: L[k].
-  const int32_t* ctr[kMaxGroup];
+  // min(L[k], the stage kernel's count rounded up to `mult`) (mult 0: L[k], a fixed pad_to width),
+  // and the batch's first block stores {width, rows left to the host (0/1), 1} into the
+  // host-mapped info[k] (MainDriver::json_width).  ctr[k]: the tagged count words
+  // (JsonStageBatch::ctr), valid where their high half equals ctr_tag[k]; nullptr: L[k].
+  const unsigned long long* ctr[kMaxGroup];
+  uint32_t ctr_tag[kMaxGroup];
   int32_t* info[kMaxGroup];
   int32_t mult;
 };

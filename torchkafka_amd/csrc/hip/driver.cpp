@@ -517,13 +517,7 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
     batch_bytes[k] = b;
     total += b;
   }
-  // device-counted batches: two zeroed counter words each at the front of the group's region
-  bool devc = false;
-  for (int k = 0; k < n; ++k) devc = devc || (views[k]->flags & tk::kSlotDevCount) != 0;
-  const uint64_t ctr_bytes = devc ? kA : 0;
-  const uint64_t base = stage_alloc(total + ctr_bytes);
-  if (devc && hipMemsetAsync(stage_dev_ + base, 0, ctr_bytes, stream) != hipSuccess)
-    throw std::runtime_error("driver: hipMemsetAsync of the JSON counters failed");
+  const uint64_t base = stage_alloc(total);
   JsonStageLaunch a{};
   a.burst = span_burst_;
   JsonGroupArgs ga{};
@@ -531,14 +525,16 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
   ga.pad = float(pad);
   ga.err_tag = tk::kSpanParseErrBit;
   ga.mult = json_mult_;
-  uint64_t off = base + ctr_bytes;
+  uint64_t off = base;
   for (int k = 0; k < n; ++k) {
     const SlotView& v = *views[k];
     perrs[k] = verdicts_->next_word();
     JsonStageBatch& b = a.b[k];
-    if (v.flags & tk::kSlotDevCount) {
-      b.ctr = reinterpret_cast<int32_t*>(stage_dev_ + base) + 4 * k;
+    if (v.flags & tk::kSlotDevCount) {  // tagged count words: nothing to zero per launch
+      b.ctr = verdicts_->json_ctr_dev(perrs[k]);
+      b.ctr_tag = verdicts_->ctr_tag(perrs[k]);
       ga.ctr[k] = b.ctr;
+      ga.ctr_tag[k] = b.ctr_tag;
       ga.info[k] = verdicts_->json_info_dev(perrs[k]);
     }
     b.desc = reinterpret_cast<JsonRowDesc*>(stage_dev_ + off);
@@ -1050,7 +1046,8 @@ void MainDriver::reset_stats() {
   ph_commit_ns_ = ph_next_ns_ = ph_launch_ns_ = ph_steps_ = events_ = groups_ = 0;
   rel_ns_ = released_ = cwait_ns_ = 0;
   occ_handed_ = occ_staged_ = occ_samples_ = 0;
-  ahead_groups_ = 0;
+  ahead_groups_ = ahead_ns_ = 0;
+  verdicts_->width_wait_ns = 0;
   fast_batches_ = fast_records_ = fast_ns_ = 0;
   if (ls_) ls_->reset_stats();
 }

@@ -200,6 +200,7 @@ class MainDriver {
   // commit sink it ends when the offsets are handed to the workers.
   const std::vector<int64_t>& commit_latency_ns() const { return ledger_->commit_latency_ns(); }
   const RingPoller::Stats& poll_stats() const { return poller_->stats; }
+  int64_t json_width_wait_ns() const { return verdicts_->width_wait_ns; }
   void reset_stats();
 
   // Cross-rank lockstep over RCCL, pipelined `depth` steps ahead (ls is owned by the caller).
@@ -227,6 +228,7 @@ class MainDriver {
   int64_t rel_ns_ = 0, released_ = 0;
   int64_t cwait_ns_ = 0;  // time spent waiting for a full group while the GPU was busy
   int64_t ahead_groups_ = 0;  // device-decode groups launched ahead of delivery
+  int64_t ahead_ns_ = 0;      // host time forming, allocating and launching them (torch_step.cpp)
   int64_t occ_handed_ = 0, occ_staged_ = 0, occ_samples_ = 0;  // slots launched / staged, summed per step
 
   // Per-iteration constants of the fixed-width fast path (set once by torch_step.cpp's

@@ -73,15 +73,17 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
     // device-counted batch: its width is the longest kept row (rounded up to the pad multiple),
     // within the capacity the host allocated; the first block reports it (and the rows left to
     // the host) through the host-mapped info words
+    const unsigned long long c0 = a.ctr[bk][0], c1 = a.ctr[bk][1];
+    const uint32_t tag = a.ctr_tag[bk];
     if (a.mult > 0) {  // 0: the allocated width stays (pad_to)
-      int64_t w = a.ctr[bk][0] < 0 ? 0 : a.ctr[bk][0];
+      int64_t w = uint32_t(c0 >> 32) == tag ? int64_t(uint32_t(c0)) : 0;  // no row counted: 0
       if (a.mult > 1) w = (w + a.mult - 1) / a.mult * a.mult;
       if (w < L) L = w;
     }
     if (int64_t(blockIdx.x) == a.row_base[bk] && threadIdx.x == 0 && a.info[bk]) {
       volatile int32_t* info = a.info[bk];
       info[0] = int32_t(L);
-      info[1] = a.ctr[bk][1];
+      info[1] = uint32_t(c1 >> 32) == tag ? 1 : 0;
       __threadfence_system();
       info[2] = 1;
     }

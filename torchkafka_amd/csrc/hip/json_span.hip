@@ -164,7 +164,7 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
       for (int32_t k = lane; k < n_out; k += 64) o[k] = src[k];
       if (lane == 0) {
         bo.desc[row] = JsonRowDesc{off, -1, d.count, n_out};
-        if (bo.ctr) atomicMax(bo.ctr, n_out);
+        if (bo.ctr) atomicMax(bo.ctr, (static_cast<unsigned long long>(bo.ctr_tag) << 32) | uint32_t(max(n_out, 0)));
       }
       off += align16(uint32_t(n_out) * 4u);
     }
@@ -251,8 +251,9 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
       const int32_t n_out = trunc >= 0 && c > trunc ? trunc : c;
       bo.desc[row_begin + rr] = JsonRowDesc{dst[rr], host ? tk::kJsonCountOnDevice : T, c, n_out};
       if (bo.ctr) {
-        atomicMax(bo.ctr, n_out);
-        if (host) atomicAdd(bo.ctr + 1, 1);
+        const unsigned long long tag = static_cast<unsigned long long>(bo.ctr_tag) << 32;
+        atomicMax(bo.ctr, tag | uint32_t(max(n_out, 0)));
+        if (host) atomicMax(bo.ctr + 1, tag | 1u);
       }
     }
   }

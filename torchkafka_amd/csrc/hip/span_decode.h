@@ -63,11 +63,13 @@ struct JsonStageBatch {
   int32_t* err;                 // host-mapped status word: -1 clean, else the first bad segment (CRC)
   uint32_t* partials;           // host-mapped raw CRC per segment (RecordBatches spanning segments)
   int32_t trunc_len;            // rows with more elements keep this many (-1: no limit)
-  int32_t reserved;
-  // kSlotDevCount batches: zeroed device words [0] = max elements kept by a row, [1] = rows left
-  // to the host (not simple); the kernel counts rows whose JsonSpanRow::count is
-  // kJsonCountOnDevice.  nullptr: every count came from the worker.
-  int32_t* ctr;
+  uint32_t ctr_tag;             // this launch's tag of the ctr words
+  // kSlotDevCount batches: device words tagged with ctr_tag in their high 32 bits (never zeroed:
+  // a launch's tag is higher than any earlier tag of the same words, BatchVerdicts::ctr_tag) --
+  // [0] atomicMax of the elements kept by a row, [1] set when a row is left to the host (not
+  // simple); the kernel counts rows whose JsonSpanRow::count is kJsonCountOnDevice.  nullptr:
+  // every count came from the worker.
+  unsigned long long* ctr;
 };
 
 struct JsonStageLaunch {

@@ -41,29 +41,34 @@ at::ScalarType scalar_type_of(int code) {
 at::Tensor alloc_group(MainDriver& d, const std::vector<int64_t>& shape, const at::TensorOptions& opts,
                        c10::DeviceIndex dev, bool span);
 
-// Outputs of a var-len batch parsed ahead of its delivery by a coalesced launch.
+// Outputs of a var-len batch.  A batch of a device-decode group owns a region of the group's blocks
+// (vals / lens / masks, one allocation each for the whole group) and gets its tensors -- views of
+// that region -- only at delivery (finish_json), so forming a group costs three allocations
+// instead of three tensors per batch.
 struct VarlenOut {
-  at::Tensor out, lengths, mask;
-  // device-counted JSON batch (kSlotDevCount): out/mask are [m, capacity] until finish_json views
-  // the first m * width elements as [m, width]
-  at::Tensor flat_out, flat_mask;
-  int64_t m = 0;
+  at::Tensor out, lengths, mask;  // the delivered tensors
+  at::Tensor vals, lens, masks;   // group blocks (device-decode groups)
+  int64_t vo = 0, ro = 0;         // this batch's first element / row in them
+  int64_t m = 0, L = 0;           // rows, allocated width
+  // device-counted JSON batch (kSlotDevCount): L is a capacity; the batch is [m, width] with the
+  // width the parse kernel reported, at the start of its region
   bool devc = false;
 };
 
-// A device-counted JSON batch at delivery: its width as the parse kernel reported it (the kernel
-// wrote the rows with that stride), and the rows it left to the host parsed and written on `ks`.
+// A group batch at delivery: its views -- for a device-counted JSON batch with the width the parse
+// kernel reported (the kernel wrote the rows with that stride), and the rows it left to the host
+// parsed and written on `ks`.
 void finish_json(MainDriver& d, const SlotView& v, VarlenOut* o, int dst_dt, double pad, hipStream_t ks) {
-  if (!o->devc) return;
-  o->devc = false;
+  if (o->out.defined()) return;
   const int64_t m = o->m;
-  int64_t n_host = 0, L = 0;
-  if (m > 0) {
+  int64_t n_host = 0, L = o->devc ? 0 : o->L;
+  if (o->devc && m > 0) {
     py::gil_scoped_release nogil;
     L = d.json_width(v, &n_host);
   }
-  o->out = o->flat_out.narrow(0, 0, m * L).view({m, L});
-  if (o->flat_mask.defined()) o->mask = o->flat_mask.narrow(0, 0, m * L).view({m, L});
+  o->out = o->vals.as_strided({m, L}, {L, 1}, o->vo);
+  o->lengths = o->lens.as_strided({m}, {1}, o->ro);
+  if (o->masks.defined()) o->mask = o->masks.as_strided({m, L}, {L, 1}, o->vo);
   if (n_host > 0) {
     uint8_t* mk = o->mask.defined() ? static_cast<uint8_t*>(o->mask.data_ptr()) : nullptr;
     void* out = o->out.data_ptr();
@@ -196,19 +201,27 @@ void alloc_json_group(MainDriver& d, const int64_t* ms, const int64_t* Ls, const
   int64_t vo = 0, ro = 0;
   for (int k = 0; k < n; ++k) {
     auto o = std::make_shared<VarlenOut>();
-    o->out = vals.narrow(0, vo, ms[k] * Ls[k]).view({ms[k], Ls[k]});
-    o->lengths = lens.narrow(0, ro, ms[k]);
-    if (want_mask) o->mask = masks.narrow(0, vo, ms[k] * Ls[k]).view({ms[k], Ls[k]});
-    if (devc[k]) {
-      o->devc = true;
-      o->m = ms[k];
-      o->flat_out = vals.narrow(0, vo, ms[k] * Ls[k]);
-      if (want_mask) o->flat_mask = masks.narrow(0, vo, ms[k] * Ls[k]);
-    }
+    o->vals = vals;
+    o->lens = lens;
+    o->masks = masks;
+    o->vo = vo;
+    o->ro = ro;
+    o->m = ms[k];
+    o->L = Ls[k];
+    o->devc = devc[k];
     vo += ms[k] * Ls[k];
     ro += ms[k];
     outs[k] = std::move(o);
   }
+}
+
+// Device pointers of a group batch's region (the launch writes them before any view exists).
+void* vals_ptr(const VarlenOut& o) {
+  return static_cast<uint8_t*>(o.vals.data_ptr()) + o.vo * int64_t(o.vals.element_size());
+}
+int64_t* lens_ptr(const VarlenOut& o) { return o.lens.data_ptr<int64_t>() + o.ro; }
+uint8_t* mask_ptr(const VarlenOut& o) {
+  return o.masks.defined() ? static_cast<uint8_t*>(o.masks.data_ptr()) + o.vo : nullptr;
 }
 
 // Device JSON parse ahead of delivery (MainDriver::ahead_begin, as launch_ahead).
@@ -237,9 +250,9 @@ void launch_ahead_json(MainDriver& d, int dst_dt, double pad, int64_t pad_to, in
     std::vector<std::shared_ptr<void>> handles;
     handles.reserve(size_t(n));
     for (int k = 0; k < n; ++k) {
-      outs[k] = o[k]->out.data_ptr();
-      lens[k] = o[k]->lengths.data_ptr<int64_t>();
-      masks[k] = want_mask ? static_cast<uint8_t*>(o[k]->mask.data_ptr()) : nullptr;
+      outs[k] = vals_ptr(*o[k]);
+      lens[k] = lens_ptr(*o[k]);
+      masks[k] = mask_ptr(*o[k]);
       handles.emplace_back(std::move(o[k]));
     }
     py::gil_scoped_release nogil;
@@ -310,8 +323,11 @@ py::tuple step_once(MainDriver& d, const MainDriver::FastConfig& cfg) {
     py::gil_scoped_release nogil;
     d.step_group_launch(stream, cfg.dst_dt, dsts, cfg.row, cfg.shift, cfg.scale, std::move(handles));
   }
-  if (d.last.kind == uint32_t(tk::kPackRecordSpan))
+  if (d.last.kind == uint32_t(tk::kPackRecordSpan)) {
+    const int64_t ta = tk::now_ns();
     launch_ahead(d, cfg.shape, opts, dev, cfg.dst_dt, cfg.shift, cfg.scale, cfg.extras);
+    d.ahead_ns_ += tk::now_ns() - ta;
+  }
   return py::make_tuple(r, cs, fixed_item(out, ext));
 }
 
@@ -415,9 +431,9 @@ void register_torch_step(py::module_& m) {
           std::vector<std::shared_ptr<void>> handles;
           handles.reserve(extra);
           for (int k = 0; k < ng; ++k) {
-            outs[k] = o[k]->out.data_ptr();
-            lens[k] = o[k]->lengths.data_ptr<int64_t>();
-            masks[k] = want_mask ? static_cast<uint8_t*>(o[k]->mask.data_ptr()) : nullptr;
+            outs[k] = vals_ptr(*o[k]);
+            lens[k] = lens_ptr(*o[k]);
+            masks[k] = mask_ptr(*o[k]);
           }
           for (int k = 1; k < ng; ++k) handles.emplace_back(std::move(o[k]));
           {
@@ -477,7 +493,11 @@ void register_torch_step(py::module_& m) {
             d.deliver(v);
           }
         }
-        if (row_span_kind(v.kind)) launch_ahead_json(d, dst_dt, pad, pad_to, pad_multiple, want_mask, dev);
+        if (row_span_kind(v.kind)) {
+          const int64_t ta = tk::now_ns();
+          launch_ahead_json(d, dst_dt, pad, pad_to, pad_multiple, want_mask, dev);
+          d.ahead_ns_ += tk::now_ns() - ta;
+        }
         d.ph_launch_ns_ += tk::now_ns() - t2;
         ++d.ph_steps_;
         ++d.fast_batches_;

@@ -1149,6 +1149,8 @@ class DeviceLoader:
         self.stats.issue_ns += st.get("fast_ns", 0)
         self.stats.groups += st.get("groups", 0)
         self.stats.coalesce_wait_ns += st.get("coalesce_wait_ns", 0)
+        self.stats.ahead_ns += st.get("ahead_ns", 0)
+        self.stats.json_width_wait_ns += st.get("json_width_wait_ns", 0)
         self.stats.occ_handed += st.get("occ_handed", 0)
         self.stats.occ_staged += st.get("occ_staged", 0)
         self.stats.occ_samples += st.get("occ_samples", 0)

@@ -46,6 +46,8 @@ class LoaderStats:
     events: int = 0            # completion events recorded (batched: fewer than batches)
     groups: int = 0            # coalesced launches (several batches collated by one kernel)
     coalesce_wait_ns: int = 0  # main thread waiting for a full group while the GPU was busy
+    ahead_ns: int = 0  # main thread forming and launching device-decode groups ahead of delivery
+    json_width_wait_ns: int = 0  # main thread waiting for a parse kernel to report a batch width
     occ_handed: int = 0        # slots launched on the GPU and not yet released, summed per step
     occ_staged: int = 0        # slots taken from the ring and not yet launched, summed per step
     occ_samples: int = 0
@@ -109,6 +111,8 @@ class LoaderStats:
             "events_per_batch": self.events / max(self.batches, 1),
             "group_launches_per_batch": self.groups / max(self.batches, 1),
             "coalesce_wait_us_per_batch": self.coalesce_wait_ns / 1e3 / max(self.batches, 1),
+            "ahead_launch_us_per_batch": self.ahead_ns / 1e3 / max(self.batches, 1),
+            "json_width_wait_us_per_batch": self.json_width_wait_ns / 1e3 / max(self.batches, 1),
             "slots_on_gpu_avg": self.occ_handed / max(self.occ_samples, 1),
             "slots_staged_avg": self.occ_staged / max(self.occ_samples, 1),
             "native_release_us_per_step": self.release_ns / 1e3 / max(self.phase_steps, 1),
