@@ -65,10 +65,13 @@ struct JsonGroupArgs {
   // (JsonStageBatch::ctr), valid where their high half equals ctr_tag[k]; nullptr: L[k].
   const unsigned long long* ctr[kMaxGroup];
   uint32_t ctr_tag[kMaxGroup];
+  int32_t trunc[kMaxGroup];  // json_count_kernel: rows keep at most this many elements (-1: all)
   int32_t* info[kMaxGroup];
   int32_t mult;
 };
 void launch_json_group(JsonGroupArgs& a, int dst_dt, hipStream_t stream);
+// Device counting of a staged group (json_span.hip): before launch_json_group on the same stream.
+void launch_json_count(const JsonGroupArgs& a, hipStream_t stream);
 
 std::vector<std::pair<std::string, double>> api_bench(int device, int iters);
 

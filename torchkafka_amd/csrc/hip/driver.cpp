@@ -552,6 +552,7 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
     ga.mask[k] = masks[k];
     ga.err[k] = b.err;
     ga.row_base[k + 1] = ga.row_base[k] + int64_t(v.n_rows);
+    ga.trunc[k] = v.trunc_len;
     off += batch_bytes[k];
   }
   auto flush = [&]() {
@@ -576,6 +577,9 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
     }
   }
   flush();
+  bool devc = false;
+  for (int k = 0; k < n; ++k) devc = devc || ga.ctr[k] != nullptr;
+  if (devc) launch_json_count(ga, stream);  // a wave per row: counts, simple check, the width words
   // the parse: a block per row over the staged texts, on the same stream
   launch_json_group(ga, dst_dt, stream);
   if (record_last) eng_->record_done(slots[n - 1], stream);

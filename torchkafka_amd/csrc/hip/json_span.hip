@@ -10,6 +10,8 @@
 //     -- PCIe-bound, like span_decode.hip -- then copy each row's text 16-byte aligned into the
 //     batch's HBM staging area (a block-wide scan of the rounded lengths places them) and write
 //     its JsonRowDesc;
+//   json_count_kernel (device counting, kSlotDevCount): a wave per row scans the staged text --
+//     json_scan_simple's rules -- and completes the row's descriptor and the batch's width word;
 //   json_parse.hip's json_rows_kernel over those descriptors: a 256-thread block per row, one
 //     token per thread (bit-exact with json.loads).  Parsing is ~100x the work of the copy, so it
 //     gets the whole GPU (a block per row) instead of the few workgroups the segments give.
@@ -50,25 +52,25 @@ __device__ __forceinline__ uint4 load16(const uint32_t* b32, int32_t b0) {
   return v;
 }
 
-// One wave copies a row's T bytes (LDS byte r0) to `o` and, for a device-counted row
-// (kJsonCountOnDevice), runs json_scan_simple's rules on them on the way (csrc/core/consumer.cpp
+// One wave runs json_scan_simple's rules on a device-counted row's T bytes (csrc/core/consumer.cpp
 // json_scan_impl, bit for bit): whitespace trimmed, '[' ... ']' framing, an interior of number
 // characters [0-9.-], commas and whitespace only, no run of more than 16 number characters.
-// Returns the element count (commas + 1; 0 for an empty interior), or -1 when the row is not
-// simple; *guess is then the element count a flat array of that text has (commas + 1, 0 when the
-// interior is empty or the text is not framed) -- the width its host parse will fill.
-__device__ int32_t copy_scan_row(const uint32_t* b32, const uint8_t* buf, int32_t r0, int32_t T, uint8_t* o,
-                                 int lane, int32_t* guess) {
+// load(c) gives the text's 16 bytes at c (c a multiple of 16; bytes past T are ignored), byte(i)
+// its byte i.  Returns the element count (commas + 1; 0 for an empty interior), or -1 when the row
+// is not simple; *guess is then the element count a flat array of that text has (commas + 1, 0
+// when the interior is empty or the text is not framed) -- the width its host parse will fill.
+template <class Load, class Byte>
+__device__ int32_t scan_row(Load&& load, Byte&& byte, int32_t T, int lane, int32_t* guess) {
   int32_t lo, hi;
   bool framed;
-  if (T >= 2 && buf[r0] == '[' && buf[r0 + T - 1] == ']') {
+  if (T >= 2 && byte(0) == '[' && byte(T - 1) == ']') {
     lo = 1;
     hi = T - 1;
     framed = true;
   } else {
     int32_t fa = T, lb = -1;  // first and last byte that is not whitespace
     for (int32_t i = lane; i < T; i += 64)
-      if (!is_ws(buf[r0 + i])) {
+      if (!is_ws(byte(i))) {
         fa = min(fa, i);
         lb = max(lb, i);
       }
@@ -77,7 +79,7 @@ __device__ int32_t copy_scan_row(const uint32_t* b32, const uint8_t* buf, int32_
       fa = min(fa, __shfl_xor(fa, off, 64));
       lb = max(lb, __shfl_xor(lb, off, 64));
     }
-    framed = lb - fa + 1 >= 2 && buf[r0 + fa] == '[' && buf[r0 + lb] == ']';
+    framed = lb - fa + 1 >= 2 && byte(fa) == '[' && byte(lb) == ']';
     lo = framed ? fa + 1 : 0;
     hi = framed ? lb : 0;
   }
@@ -88,8 +90,7 @@ __device__ int32_t copy_scan_row(const uint32_t* b32, const uint8_t* buf, int32_
     const int32_t c = base + 16 * lane;
     uint32_t tokm = 0;
     if (c < T) {
-      const uint4 v = load16(b32, r0 + c);
-      *reinterpret_cast<uint4*>(o + c) = v;
+      const uint4 v = load(c);
       const int32_t l0 = lo - c, h0 = hi - c;
       uint32_t in = h0 <= 0 ? 0u : h0 >= 16 ? 0xFFFFu : (1u << h0) - 1u;
       if (l0 > 0) in &= l0 >= 16 ? 0u : ~((1u << l0) - 1u);
@@ -237,24 +238,13 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
       continue;
     }
     uint8_t* __restrict__ o = bo.stage + dst[rr];
-    int32_t count = cnt[rr], guess = 0;
-    if (count == tk::kJsonCountOnDevice) {
-      count = copy_scan_row(b32, buf, r0, T, o, lane, &guess);
-    } else {
-      for (int32_t c = 16 * lane; c < T; c += 64 * 16) *reinterpret_cast<uint4*>(o + c) = load16(b32, r0 + c);
-    }
+    for (int32_t c = 16 * lane; c < T; c += 64 * 16) *reinterpret_cast<uint4*>(o + c) = load16(b32, r0 + c);
     if (lane == 0) {
-      // a device-counted row that is not simple: the host parses it when the batch is delivered
-      // (tlen kJsonCountOnDevice: json_rows_kernel writes its padding, lengths and mask only)
-      const bool host = count < 0;
-      const int32_t c = host ? guess : count;
-      const int32_t n_out = trunc >= 0 && c > trunc ? trunc : c;
-      bo.desc[row_begin + rr] = JsonRowDesc{dst[rr], host ? tk::kJsonCountOnDevice : T, c, n_out};
-      if (bo.ctr) {
-        const unsigned long long tag = static_cast<unsigned long long>(bo.ctr_tag) << 32;
-        atomicMax(bo.ctr, tag | uint32_t(max(n_out, 0)));
-        if (host) atomicMax(bo.ctr + 1, tag | 1u);
-      }
+      // a device-counted row (count kJsonCountOnDevice) keeps that count here: json_count_kernel
+      // scans its staged text and completes the descriptor before json_rows_kernel reads it
+      const int32_t c = cnt[rr];
+      const int32_t n_out = c < 0 ? 0 : trunc >= 0 && c > trunc ? trunc : c;
+      bo.desc[row_begin + rr] = JsonRowDesc{dst[rr], T, c, n_out};
     }
   }
   if (off_seg && lane == 0) *bo.err = int32_t(sg.seg);  // never committed (reported as this segment)
@@ -266,7 +256,52 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
   }
 }
 
+// Device counting, between the stage and the parse: a wave per device-counted row (a block of four
+// rows; blocks [row_base[k] / 4 ..) of batch k) scans the row's staged, 16-byte aligned HBM text,
+// completes its descriptor and raises the batch's tagged width word.  Kept out of the stage kernel,
+// whose few workgroups (one per segment) are busy with PCIe loads: here every row gets a wave.
+__global__ __launch_bounds__(256) void json_count_kernel(JsonGroupArgs a) {
+  const int lane = int(threadIdx.x) & 63;
+  const int64_t g = int64_t(blockIdx.x) * 4 + int64_t(threadIdx.x >> 6);  // this wave's global row
+  if (g >= a.row_base[a.n]) return;
+  int bk = 0;
+#pragma unroll
+  for (int k = 1; k < kMaxGroup; ++k) bk += (k < a.n && g >= a.row_base[k]) ? 1 : 0;
+  if (!a.ctr[bk]) return;
+  const int64_t r = g - a.row_base[bk];
+  JsonRowDesc* desc = const_cast<JsonRowDesc*>(a.rows[bk]) + r;
+  const JsonRowDesc d = *desc;
+  if (d.count != tk::kJsonCountOnDevice || d.tlen < 0) return;
+  const int32_t T = d.tlen;
+  if (uint64_t(d.off) + ((uint64_t(T) + 15u) & ~uint64_t(15)) > a.vals_cap[bk]) return;  // json_rows_kernel flags it
+  const uint8_t* __restrict__ text = a.vals[bk] + d.off;
+  int32_t guess = 0;
+  const int32_t count = scan_row([&](int32_t c) { return *reinterpret_cast<const uint4*>(text + c); },
+                                 [&](int32_t i) { return uint32_t(text[i]); }, T, lane, &guess);
+  if (lane == 0) {
+    // a row that is not simple: the host parses it when the batch is delivered (tlen
+    // kJsonCountOnDevice: json_rows_kernel writes its padding, lengths and mask only)
+    const bool host = count < 0;
+    const int32_t c = host ? guess : count;
+    const int32_t trunc = a.trunc[bk];
+    const int32_t n_out = trunc >= 0 && c > trunc ? trunc : c;
+    *desc = JsonRowDesc{d.off, host ? tk::kJsonCountOnDevice : T, c, n_out};
+    const unsigned long long tag = static_cast<unsigned long long>(a.ctr_tag[bk]) << 32;
+    atomicMax(const_cast<unsigned long long*>(a.ctr[bk]), tag | uint32_t(max(n_out, 0)));
+    if (host) atomicMax(const_cast<unsigned long long*>(a.ctr[bk]) + 1, tag | 1u);
+  }
+}
+
 }  // namespace
+
+void launch_json_count(const JsonGroupArgs& a, hipStream_t stream) {
+  if (a.n < 1 || a.n > kMaxGroup) throw std::invalid_argument("json count: group size out of range");
+  const int64_t total = a.row_base[a.n];
+  if (total <= 0) return;
+  hipLaunchKernelGGL(json_count_kernel, dim3(unsigned((total + 3) / 4)), dim3(256), 0, stream, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("json count launch: ") + hipGetErrorString(e));
+}
 
 void launch_json_stage(const JsonStageLaunch& a, hipStream_t stream) {
   if (a.n_seg < 0 || a.n_seg > kMaxLaunchSegs) throw std::invalid_argument("json stage: bad segment count");
@@ -288,6 +323,7 @@ void launch_json_stage(const JsonStageLaunch& a, hipStream_t stream) {
 void prewarm_json_span_kernels() {
   hipFuncAttributes attr;
   (void)hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&json_stage_kernel));
+  (void)hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&json_count_kernel));
 }
 
 }  // namespace tkh
