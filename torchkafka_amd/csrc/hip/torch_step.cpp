@@ -121,6 +121,17 @@ py::object fixed_item(const at::Tensor& out, const at::Tensor& ext) {
   return py::tuple(items);
 }
 
+// Makes `ks` the current stream of its device for the scope's allocations: the caching allocator
+// then takes the blocks from (and orders their reuse against) that stream.  The device is already
+// the current one, so unlike HIPStreamGuard this makes no hipGetDevice / hipSetDevice calls.
+struct StreamScope {
+  c10::hip::HIPStream prev;
+  StreamScope(const c10::hip::HIPStream& ks, c10::DeviceIndex dev) : prev(c10::hip::getCurrentHIPStream(dev)) {
+    c10::hip::setCurrentHIPStream(ks);
+  }
+  ~StreamScope() { c10::hip::setCurrentHIPStream(prev); }
+};
+
 // Output block of a coalesced fixed-width launch.  Device decode runs on the driver's decode
 // stream: allocate there, so the caching allocator orders the memory's reuse against that stream
 // (no wait on the user's stream, which already waits for the previous group), and record the
@@ -131,7 +142,7 @@ at::Tensor alloc_group(MainDriver& d, const std::vector<int64_t>& shape, const a
   const auto ks = c10::hip::getStreamFromExternal(d.next_decode_stream(), dev);
   at::Tensor all;
   {
-    c10::hip::HIPStreamGuard guard(ks);
+    StreamScope scope(ks, dev);
     all = at::empty(shape, opts);
   }
   c10::hip::HIPCachingAllocator::recordStream(all.storage().data_ptr(), c10::hip::getCurrentHIPStream(dev));
@@ -190,7 +201,7 @@ void alloc_json_group(MainDriver& d, const int64_t* ms, const int64_t* Ls, const
   const auto ks = c10::hip::getStreamFromExternal(d.next_decode_stream(), dev);
   at::Tensor vals, lens, masks;
   {
-    c10::hip::HIPStreamGuard guard(ks);
+    StreamScope scope(ks, dev);
     vals = at::empty({tot}, at::TensorOptions().dtype(scalar_type_of(dst_dt)).device(at::kCUDA, dev));
     lens = at::empty({rows}, at::TensorOptions().dtype(at::kLong).device(at::kCUDA, dev));
     if (want_mask) masks = at::empty({tot}, at::TensorOptions().dtype(at::kBool).device(at::kCUDA, dev));
