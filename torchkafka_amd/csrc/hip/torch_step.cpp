@@ -66,9 +66,10 @@ void finish_json(MainDriver& d, const SlotView& v, VarlenOut* o, int dst_dt, dou
     py::gil_scoped_release nogil;
     L = d.json_width(v, &n_host);
   }
-  o->out = o->vals.as_strided({m, L}, {L, 1}, o->vo);
-  o->lengths = o->lens.as_strided({m}, {1}, o->ro);
-  if (o->masks.defined()) o->mask = o->masks.as_strided({m, L}, {L, 1}, o->vo);
+  // (as_strided's offset is absolute in the storage the three blocks share)
+  o->out = o->vals.as_strided({m, L}, {L, 1}, o->vals.storage_offset() + o->vo);
+  o->lengths = o->lens.as_strided({m}, {1}, o->lens.storage_offset() + o->ro);
+  if (o->masks.defined()) o->mask = o->masks.as_strided({m, L}, {L, 1}, o->masks.storage_offset() + o->vo);
   if (n_host > 0) {
     uint8_t* mk = o->mask.defined() ? static_cast<uint8_t*>(o->mask.data_ptr()) : nullptr;
     void* out = o->out.data_ptr();
@@ -188,9 +189,10 @@ int64_t padded_len(const SlotView& s, int64_t pad_to, int64_t pad_multiple) {
   return L;
 }
 
-// Outputs of a group of device-parsed JSON batches (kPackJsonSpan): one allocation for the values
-// of all of them, one for the lengths (and one for the masks), made on the decode stream the group
-// runs on and recorded on the user's stream (as alloc_group), then viewed per batch.
+// Outputs of a group of device-parsed JSON batches (kPackJsonSpan): ONE allocation holds the values
+// of all of them, their lengths and their masks (256-byte aligned sub-blocks viewed with their
+// dtypes), made on the decode stream the group runs on and recorded on the user's stream (as
+// alloc_group): one allocator round trip and one free-time event per group.
 void alloc_json_group(MainDriver& d, const int64_t* ms, const int64_t* Ls, const bool* devc, int n, int dst_dt,
                       bool want_mask, c10::DeviceIndex dev, std::shared_ptr<VarlenOut>* outs) {
   int64_t tot = 0, rows = 0;
@@ -199,16 +201,20 @@ void alloc_json_group(MainDriver& d, const int64_t* ms, const int64_t* Ls, const
     rows += ms[k];
   }
   const auto ks = c10::hip::getStreamFromExternal(d.next_decode_stream(), dev);
-  at::Tensor vals, lens, masks;
+  auto up = [](int64_t x) { return (x + 255) / 256 * 256; };
+  const at::ScalarType vt = scalar_type_of(dst_dt);
+  const int64_t vbytes = up(tot * int64_t(c10::elementSize(vt))), lbytes = up(rows * 8);
+  const int64_t mbytes = want_mask ? up(tot) : 0;
+  at::Tensor all;
   {
     StreamScope scope(ks, dev);
-    vals = at::empty({tot}, at::TensorOptions().dtype(scalar_type_of(dst_dt)).device(at::kCUDA, dev));
-    lens = at::empty({rows}, at::TensorOptions().dtype(at::kLong).device(at::kCUDA, dev));
-    if (want_mask) masks = at::empty({tot}, at::TensorOptions().dtype(at::kBool).device(at::kCUDA, dev));
+    all = at::empty({vbytes + lbytes + mbytes}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, dev));
   }
-  const auto user = c10::hip::getCurrentHIPStream(dev);
-  for (const at::Tensor* t : {&vals, &lens, &masks})
-    if (t->defined() && t->numel() > 0) c10::hip::HIPCachingAllocator::recordStream(t->storage().data_ptr(), user);
+  if (all.numel() > 0)
+    c10::hip::HIPCachingAllocator::recordStream(all.storage().data_ptr(), c10::hip::getCurrentHIPStream(dev));
+  const at::Tensor vals = all.narrow(0, 0, tot * int64_t(c10::elementSize(vt))).view(vt);
+  const at::Tensor lens = all.narrow(0, vbytes, rows * 8).view(at::kLong);
+  const at::Tensor masks = want_mask ? all.narrow(0, vbytes + lbytes, tot).view(at::kBool) : at::Tensor();
   int64_t vo = 0, ro = 0;
   for (int k = 0; k < n; ++k) {
     auto o = std::make_shared<VarlenOut>();
