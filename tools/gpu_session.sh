@@ -31,7 +31,7 @@ for s in ${STEPS:-pytest_new}; do
             tail -2 gpurun_out/profc4api.log ;;
     profbenchapi) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --runtime-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/profbenchapi" -o run -- python3 "$OLDPWD/bench.py" --steps 2000 --steady-steps 4000 --extra-blocks "" --bridge-steps 0 > "$OLDPWD/gpurun_out/profbenchapi.log" 2>&1) || exit $?
             tail -2 gpurun_out/profbenchapi.log ;;
-    profdma) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/profdma" -o run -- python3 "$OLDPWD/bench.py" --h2d dma --steps 1000 --steady-steps 1000 > "$OLDPWD/gpurun_out/profdma.log" 2>&1) || exit $?
+    profdma) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/profdma" -o run -- python3 "$OLDPWD/bench.py" --h2d dma --steps 1000 --steady-steps 4000 --extra-blocks "" --bridge-steps 0 > "$OLDPWD/gpurun_out/profdma.log" 2>&1) || exit $?
             tail -3 gpurun_out/profdma.log ;;
     config5) run config5 300 python benchmarks/config5_large_messages.py ;;
     config5w) for w in 2 4; do run config5_w$w 300 python benchmarks/config5_large_messages.py --workers $w; done ;;
