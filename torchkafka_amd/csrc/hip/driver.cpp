@@ -438,8 +438,10 @@ void MainDriver::launch_span(const int* slots, const SlotView* const* views, int
   }
   ext_n_ = 0;
   a.vec_store = vec ? 1 : 0;
-  a.burst = span_burst_;  // loads a wave keeps in flight (span_decode.hip stage 1)
+  bool pcie = false;  // a segment of this launch is read over PCIe (not from the HBM mirror)
   auto flush = [&](bool record) {
+    a.burst = pcie ? span_burst_ : mirror_burst_;  // loads a wave keeps in flight (span_decode.hip stage 1)
+    pcie = false;
     if (mirror) mirror->before(stream);
     eng_->collate_span(slots, n, stream, a, v0.src_dtype, dst_dt, shift, scale, record);
     if (mirror) mirror->after(stream);
@@ -452,7 +454,7 @@ void MainDriver::launch_span(const int* slots, const SlotView* const* views, int
         flush(false);
         a.n_seg = 0;
       }
-      fill_seg(a.s[a.n_seg++], sg[i], pins_->seg_src(sg[i]), k, i);
+      fill_seg(a.s[a.n_seg++], sg[i], seg_src(sg[i], &pcie), k, i);
     }
   }
   flush(record_last);
@@ -519,7 +521,7 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
   }
   const uint64_t base = stage_alloc(total);
   JsonStageLaunch a{};
-  a.burst = span_burst_;
+  bool pcie = false;
   JsonGroupArgs ga{};
   ga.n = n;
   ga.pad = float(pad);
@@ -556,6 +558,8 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
     off += batch_bytes[k];
   }
   auto flush = [&]() {
+    a.burst = pcie ? span_burst_ : mirror_burst_;
+    pcie = false;
     if (mirror) mirror->before(stream);
     eng_->collate_json_stage(slots, n, stream, a);
     if (mirror) mirror->after(stream);
@@ -571,7 +575,7 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
         a.n_seg = 0;
       }
       SpanDevSeg& d = a.s[a.n_seg++];
-      fill_seg(d, sg[i], (sg[i].flags & tk::kSegHostRows) ? nullptr : pins_->seg_src(sg[i]), k, i);
+      fill_seg(d, sg[i], (sg[i].flags & tk::kSegHostRows) ? nullptr : seg_src(sg[i], &pcie), k, i);
       d.stage_off = uint32_t(soff);
       soff += seg_bytes(v, sg[i]);
     }
@@ -592,7 +596,7 @@ void MainDriver::launch_var_span(const int* slots, const SlotView* const* views,
   verdicts_->ensure_partials();
   LogMirror* mirror = pins_->mirror();
   VarSpanLaunch a{};
-  a.burst = span_burst_;
+  bool pcie = false;
   const int src_dt = views[0]->src_dtype;
   for (int k = 0; k < n; ++k) {
     perrs[k] = verdicts_->next_word();
@@ -616,6 +620,8 @@ void MainDriver::launch_var_span(const int* slots, const SlotView* const* views,
       a.b[k].rows = reinterpret_cast<const tk::JsonSpanRow*>(a.b[k].slot);
     }
     a.tabs = eng_->span_tables();
+    a.burst = pcie ? span_burst_ : mirror_burst_;
+    pcie = false;
     if (mirror) mirror->before(stream);
     tkh::launch_var_span(a, src_dt, dst_dt, pad, stream);
     if (mirror) mirror->after(stream);
@@ -631,7 +637,7 @@ void MainDriver::launch_var_span(const int* slots, const SlotView* const* views,
         flush(false);
         a.n_seg = 0;
       }
-      fill_seg(a.s[a.n_seg++], sg[i], (sg[i].flags & tk::kSegHostRows) ? nullptr : pins_->seg_src(sg[i]), k, i);
+      fill_seg(a.s[a.n_seg++], sg[i], (sg[i].flags & tk::kSegHostRows) ? nullptr : seg_src(sg[i], &pcie), k, i);
     }
   }
   flush(record_last);

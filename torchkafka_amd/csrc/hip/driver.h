@@ -331,6 +331,21 @@ class MainDriver {
     const int v = e ? std::atoi(e) : 1;
     return v < 0 ? 0 : v > 8 ? 8 : v;
   }();
+  // ... for a launch whose segments all come from the HBM mirror: HBM takes every load of a wave at
+  // once (0), where PCIe reads lose bandwidth with many in flight (mirror decode: 34.1 us per group
+  // at 1, 27.8 us at 0, 29.9 us at 4; profiles/r03_s3/burst/); TORCHKAFKA_MIRROR_BURST
+  int mirror_burst_ = [] {
+    const char* e = std::getenv("TORCHKAFKA_MIRROR_BURST");
+    const int v = e ? std::atoi(e) : 0;
+    return v < 0 ? 0 : v > 8 ? 8 : v;
+  }();
+  // the segment source of a decode launch; *pcie is set when it is not the HBM mirror
+  const uint8_t* seg_src(const tk::SpanSeg& sg, bool* pcie) {
+    bool hbm = false;
+    const uint8_t* s = pins_->seg_src(sg, &hbm);
+    *pcie = *pcie || !hbm;
+    return s;
+  }
   int32_t json_mult_ = 1;
   // HBM staging ring of the device JSON parse (row texts between the two kernels, json_span.hip):
   // positions are monotonic, regions are freed in launch order as their groups' slots are released.

@@ -98,7 +98,8 @@ void LogPins::ensure(uint32_t pidx, uint64_t end) {
   reg_ns_ += tk::now_ns() - t0;
 }
 
-const uint8_t* LogPins::seg_src(const tk::SpanSeg& sg) {
+const uint8_t* LogPins::seg_src(const tk::SpanSeg& sg, bool* hbm) {
+  *hbm = false;
   const uint8_t* log = broker_->log_base(sg.pidx);  // pinned: device address == host address
   // a ring log (KafkaBridge replica) writes over its chunks: an HBM mirror of them would go stale,
   // so its segments are read zero-copy
@@ -108,7 +109,10 @@ const uint8_t* LogPins::seg_src(const tk::SpanSeg& sg) {
     ensure(sg.pidx, std::min<uint64_t>(part.log_capacity, sg.log_pos + mirror_->span_bytes()));
     const uint64_t written = part.log_end_pos.load(std::memory_order_acquire);
     const uint8_t* m = mirror_->map(sg.pidx, sg.log_pos, sg.len, log, std::min<uint64_t>(reg_end_[sg.pidx], written));
-    if (m) return m;
+    if (m) {
+      *hbm = true;
+      return m;
+    }
   }
   return log + sg.log_pos;
 }

@@ -44,8 +44,8 @@ class LogPins {
   void enable_mirror(uint64_t chunk_bytes, int chunks_per_partition);
   LogMirror* mirror() { return mirror_.get(); }
   const LogMirror* mirror() const { return mirror_.get(); }
-  // The address a decode kernel reads a segment from (mirror, else the pinned log).
-  const uint8_t* seg_src(const tk::SpanSeg& sg);
+  // The address a decode kernel reads a segment from (mirror, else the pinned log); *hbm tells which.
+  const uint8_t* seg_src(const tk::SpanSeg& sg, bool* hbm);
 
   // A commit stored these offsets: every 32 commits, unpin replica ranges wholly below them.
   void committed(const std::unordered_map<uint32_t, int64_t>& committed);
