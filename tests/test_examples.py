@@ -27,3 +27,12 @@ def test_example_06_group_subscribe_tls():
     assert "partitions [0, 1, 2], generation 1, 3000 records" in r.stdout
     assert "partitions [3, 4, 5], generation 1, 3000 records" in r.stdout
     assert "{0: 1000, 1: 1000, 2: 1000, 3: 1000, 4: 1000, 5: 1000}" in r.stdout
+
+
+def test_example_07_labels_and_sync_commits_on_cpu():
+    env = {**os.environ, "CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "examples", "07_labels_and_sync_commits.py")],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "4000 labelled records on cpu, 0 label mismatches" in r.stdout
+    assert "{0: 2000, 1: 2000}" in r.stdout
