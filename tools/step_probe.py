@@ -1,4 +1,9 @@
-import os, sys, time, json
+"""Host time of each step in 20-step windows after a synchronize, and the final drain (fixed-width, 1 GPU)."""
+import json
+import os
+import sys
+import time
+
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
 import torch
 from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
@@ -21,5 +26,6 @@ for rep in range(5):
     t1 = time.perf_counter()
     torch.cuda.synchronize()
     t2 = time.perf_counter()
-    print(json.dumps({"steps_us": [round(x, 1) for x in ts], "loop_us": round((t1 - t0) * 1e6, 1), "sync_us": round((t2 - t1) * 1e6, 1)}), flush=True)
+    print(json.dumps({"steps_us": [round(x, 1) for x in ts], "loop_us": round((t1 - t0) * 1e6, 1),
+                      "sync_us": round((t2 - t1) * 1e6, 1)}), flush=True)
 it.close(); dl.close(); b.destroy()
