@@ -298,6 +298,13 @@ void launch_json_count(const JsonGroupArgs& a, hipStream_t stream) {
   if (a.n < 1 || a.n > kMaxGroup) throw std::invalid_argument("json count: group size out of range");
   const int64_t total = a.row_base[a.n];
   if (total <= 0) return;
+  if (total > INT32_MAX) throw std::invalid_argument("json count: too many rows");
+  for (int k = 0; k < a.n; ++k) {
+    // the kernel reads each row's staged text as 16-byte vectors from its 16-byte aligned region
+    if (a.ctr[k] && (reinterpret_cast<uintptr_t>(a.vals[k]) % 16 || reinterpret_cast<uintptr_t>(a.rows[k]) % 16 ||
+                     a.row_base[k + 1] < a.row_base[k]))
+      throw std::invalid_argument("json count: malformed group");
+  }
   hipLaunchKernelGGL(json_count_kernel, dim3(unsigned((total + 3) / 4)), dim3(256), 0, stream, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("json count launch: ") + hipGetErrorString(e));
