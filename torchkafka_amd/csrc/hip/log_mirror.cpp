@@ -1,6 +1,7 @@
 #include "log_mirror.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -21,8 +22,13 @@ LogMirror::LogMirror(int device, uint64_t chunk_bytes, int chunks_per_partition)
   prefetch_ = K_ > 3 ? K_ - 2 : 1;
   stride_ = (chunk_ + tk::kSpanSegMax + 256 + 4095) / 4096 * 4096;
   TKM_CHECK(hipSetDevice(device_));
-  TKM_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
-  TKM_CHECK(hipEventCreateWithFlags(&copied_, hipEventDisableTiming));
+  const char* e = std::getenv("TORCHKAFKA_MIRROR_COPY_STREAMS");
+  const int n = e ? std::atoi(e) : 2;
+  cs_.resize(size_t(n < 1 ? 1 : n > 4 ? 4 : n));
+  for (auto& c : cs_) {
+    TKM_CHECK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    TKM_CHECK(hipEventCreateWithFlags(&c.copied, hipEventDisableTiming));
+  }
   pool_.resize(256);
   for (auto& e : pool_) TKM_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   pool_seq_.assign(pool_.size(), 0);
@@ -31,13 +37,16 @@ LogMirror::LogMirror(int device, uint64_t chunk_bytes, int chunks_per_partition)
 
 LogMirror::~LogMirror() {
   hipSetDevice(device_);
-  if (copy_) hipStreamSynchronize(copy_);
+  for (auto& c : cs_)
+    if (c.stream) hipStreamSynchronize(c.stream);
   hipDeviceSynchronize();  // no decode kernel may still read a buffer
   for (auto& P : parts_)
     if (P.dev) hipFree(P.dev);
   for (auto e : pool_) hipEventDestroy(e);
-  if (copied_) hipEventDestroy(copied_);
-  if (copy_) hipStreamDestroy(copy_);
+  for (auto& c : cs_) {
+    if (c.copied) hipEventDestroy(c.copied);
+    if (c.stream) hipStreamDestroy(c.stream);
+  }
 }
 
 LogMirror::Part& LogMirror::part(uint32_t pidx) {
@@ -47,6 +56,7 @@ LogMirror::Part& LogMirror::part(uint32_t pidx) {
     TKM_CHECK(hipSetDevice(device_));
     TKM_CHECK(hipMalloc(reinterpret_cast<void**>(&P.dev), stride_ * size_t(K_)));
     P.bufs.assign(size_t(K_), Buf{});
+    for (auto& b : P.bufs) b.s = int(pidx % cs_.size());
     dev_bytes_ += stride_ * size_t(K_);
   }
   return P;
@@ -54,9 +64,10 @@ LogMirror::Part& LogMirror::part(uint32_t pidx) {
 
 void LogMirror::retarget(Buf& b, int64_t c) {
   // the copy stream overwrites the buffer only after every reader of its previous chunk
+  hipStream_t copy = cs_[size_t(b.s)].stream;
   for (auto& r : b.readers) {
     if (r.ev >= 0 && pool_seq_[size_t(r.ev)] == r.seq) {
-      TKM_CHECK(hipStreamWaitEvent(copy_, pool_[size_t(r.ev)], 0));
+      TKM_CHECK(hipStreamWaitEvent(copy, pool_[size_t(r.ev)], 0));
       --pool_refs_[size_t(r.ev)];
     }
     r = Reader{};
@@ -88,13 +99,13 @@ LogMirror::Buf* LogMirror::ensure(Part& P, uint32_t pidx, int64_t c, uint64_t wa
     for (uint64_t a = b.end; a < target;) {
       const uint64_t e = std::min<uint64_t>(target, (a / kRegAlign + 1) * kRegAlign);
       TKM_CHECK(hipMemcpyAsync(P.dev + j * stride_ + (a - lo_c), log + a, size_t(e - a), hipMemcpyHostToDevice,
-                               copy_));
+                               cs_[size_t(b.s)].stream));
       ++copies_;
       a = e;
     }
     bytes_ += target - b.end;
     b.end = target;
-    b.copy_seq = ++copy_seq_;
+    b.copy_seq = ++cs_[size_t(b.s)].seq;
   }
   return &b;
 }
@@ -129,24 +140,27 @@ void LogMirror::issue_prefetches() {
 }
 
 void LogMirror::before(hipStream_t stream) {
-  uint64_t need = 0;
-  for (const auto& pb : pending_) need = std::max(need, parts_[pb.first].bufs[size_t(pb.second)].copy_seq);
-  if (need == 0 || need <= done_seq_) {
-    issue_prefetches();
-    return;
+  uint64_t need[4] = {0, 0, 0, 0};
+  for (const auto& pb : pending_) {
+    const Buf& b = parts_[pb.first].bufs[size_t(pb.second)];
+    need[b.s] = std::max(need[b.s], b.copy_seq);
   }
-  // One event, recorded only when a launch needs a copy not known complete: it also covers the
-  // prefetches queued behind that copy (a longer wait), but events between SDMA copies cost more
-  // than they save (measured, config 2 --h2d dma: 46.5 M rec/s this way, 32-34 M with an event
-  // after every copy).
-  if (recorded_seq_ < need) {
-    TKM_CHECK(hipEventRecord(copied_, copy_));
-    recorded_seq_ = copy_seq_;
-  }
-  if (hipEventQuery(copied_) == hipSuccess) {  // found complete: no wait, and remembered
-    done_seq_ = recorded_seq_;
-  } else {
-    TKM_CHECK(hipStreamWaitEvent(stream, copied_, 0));
+  for (size_t s = 0; s < cs_.size(); ++s) {
+    CopyStream& c = cs_[s];
+    if (need[s] == 0 || need[s] <= c.done) continue;
+    // One event per copy stream, recorded only when a launch needs a copy not known complete: it
+    // also covers the prefetches queued behind that copy (a longer wait), but events between SDMA
+    // copies cost more than they save (measured, config 2 --h2d dma: 46.5 M rec/s this way,
+    // 32-34 M with an event after every copy).
+    if (c.recorded < need[s]) {
+      TKM_CHECK(hipEventRecord(c.copied, c.stream));
+      c.recorded = c.seq;
+    }
+    if (hipEventQuery(c.copied) == hipSuccess) {  // found complete: no wait, and remembered
+      c.done = c.recorded;
+    } else {
+      TKM_CHECK(hipStreamWaitEvent(stream, c.copied, 0));
+    }
   }
   issue_prefetches();
 }

@@ -62,6 +62,7 @@ class LogMirror {
   };
   struct Buf {
     int64_t chunk = -1;
+    int s = 0;               // the copy stream that fills it (its partition's)
     uint64_t end = 0;        // log position up to which the buffer holds the chunk's bytes
     uint64_t copy_seq = 0;   // copy that brought in its latest bytes
     bool pending = false;    // mapped for the launch being formed
@@ -89,9 +90,17 @@ class LogMirror {
   uint64_t chunk_, stride_;
   int K_;
   int prefetch_ = 1;  // chunks copied ahead of the one being read
-  hipStream_t copy_ = nullptr;
-  hipEvent_t copied_ = nullptr;      // recorded on copy_ after the latest copy (when a launch needs it)
-  uint64_t copy_seq_ = 0, recorded_seq_ = 0, done_seq_ = 0;
+  // Copy streams: partition p is copied on stream p % S.  A buffer is refilled only after the
+  // copy stream waited for the readers of its previous chunk; with one stream that wait holds up
+  // every partition's copies behind it, with S it holds up only its own partitions'.
+  // TORCHKAFKA_MIRROR_COPY_STREAMS (1..4, default 2).
+  struct CopyStream {
+    hipStream_t stream = nullptr;
+    hipEvent_t copied = nullptr;  // recorded after the latest copy (when a launch needs it)
+    uint64_t seq = 0, recorded = 0, done = 0;
+  };
+  std::vector<CopyStream> cs_;
+  CopyStream& cs_of(uint32_t pidx) { return cs_[pidx % cs_.size()]; }
   std::vector<Part> parts_;
   std::vector<std::pair<uint32_t, int>> pending_;
   std::vector<hipEvent_t> pool_;
