@@ -87,8 +87,9 @@ def main():
         print(json.dumps({"config": 4, "metric": "JSON records/s to GPU (bf16 padded), per-batch commit",
                           "value": round(rows / el), "ms_per_step": round(el / args.steps * 1e3, 4),
                           "batch_size": B, "workers": args.workers, "json_parse": args.json_parse, "h2d": args.h2d,
-                          "decode": ("device (json_span.hip from the pinned logs)" if dl._json_span()
-                                     else args.decode),
+                          "decode": (("device (json_span.hip from an HBM mirror filled by SDMA copies)"
+                                      if dl._mirror() else "device (json_span.hip from the pinned logs)")
+                                     if dl._json_span() else args.decode),
                           "json_count": "device" if dl._json_count() else "workers",
                           "timed_s": round(el, 4), "steps": args.steps,
                           "avg_record_bytes": round(text_bytes),

@@ -795,8 +795,15 @@ class DeviceLoader:
     def _mirror(self) -> bool:
         """h2d='dma' with device decode: log bytes reach HBM by hipMemcpyAsync (SDMA copy engines, in
         mirror chunks of ``tuning.mirror_chunk_mib``) and the decode kernels read them there, instead
-        of reading the pinned logs over PCIe themselves (csrc/hip/log_mirror.h)."""
-        return self.h2d == "dma" and self._device_decode()
+        of reading the pinned logs over PCIe themselves (csrc/hip/log_mirror.h).
+
+        ``h2d='auto'`` takes the mirror for JSON parsed from the logs: its stage kernel then reads
+        HBM and the GPU stops being a bound (config 4, 4 workers: 42.9-43.6 M rec/s against
+        39.8-40.1 M zero-copy, profiles/r03_s3/c4_h2d/).  Fixed-width decode stays zero-copy: the
+        two are at parity there, zero-copy with the smaller spread (profiles/r03_s3/h2d_ab/)."""
+        if not self._device_decode():
+            return False
+        return self.h2d == "dma" or (self.h2d == "auto" and self._json_span())
 
     def _direct(self) -> bool:
         """h2d='direct': fixed-width rows gathered by the kernel straight from the pinned broker logs."""
