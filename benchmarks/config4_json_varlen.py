@@ -25,7 +25,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=4000)
+    ap.add_argument("--steps", type=int, default=20000)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--batch-size", type=int, default=256)
     # config 2's worker count; the result line records it (round 2 quoted an 8-worker run as 4)
