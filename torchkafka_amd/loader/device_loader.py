@@ -797,13 +797,11 @@ class DeviceLoader:
         mirror chunks of ``tuning.mirror_chunk_mib``) and the decode kernels read them there, instead
         of reading the pinned logs over PCIe themselves (csrc/hip/log_mirror.h).
 
-        ``h2d='auto'`` takes the mirror for JSON parsed from the logs: its stage kernel then reads
-        HBM and the GPU stops being a bound (config 4, 4 workers: 42.9-43.6 M rec/s against
-        39.8-40.1 M zero-copy, profiles/r03_s3/c4_h2d/).  Fixed-width decode stays zero-copy: the
-        two are at parity there, zero-copy with the smaller spread (profiles/r03_s3/h2d_ab/)."""
-        if not self._device_decode():
-            return False
-        return self.h2d == "dma" or (self.h2d == "auto" and self._json_span())
+        Opt-in (``h2d='auto'`` stays zero-copy): the mirror matches zero-copy on fixed-width decode
+        and beats it on JSON on most runs (config 4: 41-52 M rec/s against 36-40 M), but some runs
+        collapse (config 4 29.7 M, VarLen tokens 17-25 M: profiles/r03_s3/mirror_stability/) when
+        a needed chunk's copy waits behind queued prefetches on its copy stream."""
+        return self.h2d == "dma" and self._device_decode()
 
     def _direct(self) -> bool:
         """h2d='direct': fixed-width rows gathered by the kernel straight from the pinned broker logs."""
