@@ -42,6 +42,9 @@ PROCESS_ENV = {
     "TORCHKAFKA_NT_COPY": "0: plain (cached) stores when workers pack slots",
     "TORCHKAFKA_DRIVER_TRACE": "1: step-driver trace lines on stderr (debugging)",
     "TORCHKAFKA_NO_REBUILD": "1: never rebuild stale in-tree extensions at import",
+    "TORCHKAFKA_MIRROR_BURST": "LDS-DMA loads a decode wave keeps in flight when its launch reads only the HBM "
+                               "mirror (0 = all, the default; csrc/hip/driver.h)",
+    "TORCHKAFKA_MIRROR_COPY_STREAMS": "copy streams of the HBM mirror, partitions split p % n (1..4, default 2)",
 }
 
 
