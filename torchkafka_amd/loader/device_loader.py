@@ -798,9 +798,11 @@ class DeviceLoader:
         of reading the pinned logs over PCIe themselves (csrc/hip/log_mirror.h).
 
         Opt-in (``h2d='auto'`` stays zero-copy): the mirror matches zero-copy on fixed-width decode
-        and beats it on JSON on most runs (config 4: 41-52 M rec/s against 36-40 M), but some runs
-        collapse (config 4 29.7 M, VarLen tokens 17-25 M: profiles/r03_s3/mirror_stability/) when
-        a needed chunk's copy waits behind queued prefetches on its copy stream."""
+        and beats it on JSON on most runs (config 4: median 44.7 M rec/s against 39.7 M, and it won
+        12 of 12 alternated pairs: profiles/r03_final/c4_mirror_ab/).  But 2 config-4 runs of 33
+        collapsed (29.7 M and 27.3 M: profiles/r03_s3/mirror_stability/,
+        profiles/r03_final/c4_auto_mirror_trial/), and VarLen tokens run 17-25 M through it.  The
+        likely cause is a needed chunk's copy waiting behind queued prefetches on its copy stream."""
         return self.h2d == "dma" and self._device_decode()
 
     def _direct(self) -> bool:
