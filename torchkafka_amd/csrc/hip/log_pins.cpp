@@ -104,10 +104,14 @@ const uint8_t* LogPins::seg_src(const tk::SpanSeg& sg, bool* hbm) {
   // a ring log (KafkaBridge replica) writes over its chunks: an HBM mirror of them would go stale,
   // so its segments are read zero-copy
   if (mirror_ && broker_->part(sg.pidx).ring_bytes.load(std::memory_order_relaxed) == 0) {
-    // pin ahead of the segment so the mirror can copy (and prefetch) whole chunks
+    // pin ahead of the segment so the mirror can copy (and prefetch) whole chunks -- of what is
+    // written only: the mirror never copies past it, and registering fresh pages of the log beyond
+    // it stalled this thread for 20-28 ms (128 MiB) in the only two config-4 runs that collapsed
+    // (profiles/r03_final/c4_auto_mirror_trial/c4_6.log, profiles/r03_s3/mirror_stability/)
     const auto& part = broker_->part(sg.pidx);
-    ensure(sg.pidx, std::min<uint64_t>(part.log_capacity, sg.log_pos + mirror_->span_bytes()));
     const uint64_t written = part.log_end_pos.load(std::memory_order_acquire);
+    ensure(sg.pidx, std::min<uint64_t>(std::max<uint64_t>(written, sg.log_pos + sg.len),
+                                       sg.log_pos + mirror_->span_bytes()));
     const uint8_t* m = mirror_->map(sg.pidx, sg.log_pos, sg.len, log, std::min<uint64_t>(reg_end_[sg.pidx], written));
     if (m) {
       *hbm = true;
