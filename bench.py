@@ -88,6 +88,9 @@ def parse():
                     help="--h2d dma with device decode: MiB per hipMemcpyAsync into the HBM log mirror")
     ap.add_argument("--mirror-chunks", type=int, default=None, help="--h2d dma: HBM mirror buffers per partition")
     ap.add_argument("--lockstep-depth", type=int, default=2)
+    ap.add_argument("--verify", default="deliver", choices=["deliver", "commit"],
+                    help="deliver: a batch is handed out after its device CRC verdict landed (default); commit: "
+                         "the verdict gates only its commit")
     ap.add_argument("--coalesce", type=int, default=8, help="staged batches collated per kernel launch")
     ap.add_argument("--coalesce-wait-us", type=int, default=50, help="adaptive coalescing wait while the GPU is busy")
     ap.add_argument("--no-numa", action="store_true", help="do not bind ranks to their GPU's NUMA node")
@@ -107,6 +110,16 @@ def parse():
                          "label beside the values: FixedWidth + Key()); '' for none")
     ap.add_argument("--extra-steps", type=int, default=None,
                     help="timed steps of each secondary block (default: the steady-state steps)")
+    ap.add_argument("--self-launch", action="store_true",
+                    help="start the rank processes from this process even at --gpus 1 / --same-device (the "
+                         "launcher path the N > 1 runs take without torchrun)")
+    ap.add_argument("--config-blocks", default="config4,config5,config1,rccl",
+                    help="comma list of BASELINE-config blocks run at N = 1: config4 (JSON -> bf16), config5 "
+                         "(1 MiB records, 128 partitions), config1 (CPU plumbing), rccl (steady state with the "
+                         "native RCCL lockstep forced at world 1); '' for none")
+    ap.add_argument("--config4-steps", type=int, default=20000)
+    ap.add_argument("--config5-steps", type=int, default=1000)
+    ap.add_argument("--config1-records", type=int, default=100000)
     ap.add_argument("--bridge-steps", type=int, default=None,
                     help="timed steps of the Kafka-protocol bridge blocks (async; sync runs a quarter): "
                          "default 8000 on a GPU, 20 on the CPU; 0 skips them")
@@ -126,14 +139,29 @@ def launch_ranks(args) -> int:
     """N > 1 without torchrun: start N rank processes (this process never touches the GPU --
     ``torch.cuda.device_count()`` does not initialise HIP on this image) and relay rank 0's line."""
     n = args.gpus
-    if not args.device and not args.same_device:
-        import torch
+    parent = {}
+    if not args.device:
+        # counted without any HIP call (sysfs KFD topology + amdsmi): the parent must never initialise HIP
+        from torchkafka_amd.utils.topology import count_gpus_without_hip, hip_touched
 
-        visible = torch.cuda.device_count()
-        if visible < n:
-            print(f"[bench] --gpus {n} but only {visible} GPU(s) are visible: refusing to run fewer ranks",
+        try:
+            gpus = count_gpus_without_hip()
+        except RuntimeError as e:
+            print(f"[bench] {e}: refusing to launch", file=sys.stderr)
+            return 2
+        parent = {"gpus_visible": gpus, **hip_touched()}
+        if not args.same_device and gpus["count"] < n:
+            print(f"[bench] --gpus {n} but only {gpus['count']} GPU(s) are visible ({gpus}): refusing to run "
+                  "fewer ranks", file=sys.stderr)
+            return 2
+        if parent["torch_cuda_initialized"] or parent["kfd_fds"]:
+            print(f"[bench] the launcher initialised HIP before starting its ranks ({parent}): refusing",
                   file=sys.stderr)
             return 2
+    rep = os.environ.get("TK_BENCH_PARENT_REPORT")
+    if rep:
+        with open(rep, "w") as f:
+            json.dump(parent, f)
     port = _free_port()
     procs = []
     for r in range(n):
@@ -309,6 +337,129 @@ def steady_block(R: Rank, res: dict, steps: int, dim: int) -> dict:
     return out
 
 
+def record_bytes(args) -> int:
+    """Log bytes of one synthetic record: the f32 values, the 8-byte key and the record framing
+    (~20 B of varints), plus its share of the 61-byte RecordBatch header."""
+    return args.dim * 4 + 8 + 24 + (61 + args.records_per_batch - 1) // args.records_per_batch
+
+
+def memory_preflight(R: "Rank", need_per_rank: int) -> dict:
+    """The backlog every local rank writes into /dev/shm (and later pins) against what the host has:
+    free space of /dev/shm and MemAvailable, shared by the local ranks.  ``scale`` < 1 tells the
+    caller how far to shorten the timed blocks so that 1.25x the need fits."""
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", R.world))
+    out = {"bytes_per_rank": need_per_rank, "local_ranks": local}
+    room = []
+    try:
+        st = os.statvfs("/dev/shm")
+        out["shm_free"] = st.f_bavail * st.f_frsize
+        room.append(out["shm_free"])
+    except OSError:
+        pass
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                if line.startswith("MemAvailable:"):
+                    out["mem_available"] = int(line.split()[1]) * 1024
+                    room.append(out["mem_available"])
+    except OSError:
+        pass
+    budget = min(room) / max(1, local) if room else float("inf")
+    out["scale"] = 1.0 if need_per_rank * 1.25 <= budget else budget / (need_per_rank * 1.25)
+    return out
+
+
+def run_config_blocks(R: "Rank", args) -> dict:
+    """BASELINE configs 4, 5 and 1 and the RCCL-lockstep steady state, each on a broker of its own
+    (N = 1 only: these are single-GPU configurations)."""
+    import importlib
+
+    torch = R.torch
+    names = [b for b in args.config_blocks.split(",") if b]
+    out: dict = {}
+    if R.world != 1 or not names:
+        return out
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "benchmarks")
+    if here not in sys.path:
+        sys.path.insert(0, here)
+    dev = str(R.device)
+    on_gpu = R.device.type == "cuda"
+    for name in names:
+        t0 = time.perf_counter()
+        if name == "config4" and on_gpu:
+            m = importlib.import_module("config4_json_varlen")
+            a = m.parse(["--steps", str(args.config4_steps), "--device", dev, "--verify", args.verify])
+            res = m.run(a, sync=R.sync)
+            res.pop("loader", None)
+        elif name == "config5" and on_gpu:
+            m = importlib.import_module("config5_large_messages")
+            a = m.parse(["--steps", str(args.config5_steps), "--device", dev, "--verify", args.verify])
+            res = m.run(a, sync=R.sync)
+            res.pop("loader", None)
+        elif name == "config1":
+            m = importlib.import_module("config1_cpu_plumbing")
+            res = m.run(m.parse(["--records", str(args.config1_records)]))
+        elif name == "rccl" and on_gpu:
+            res = rccl_steady_block(R, args)
+        else:
+            continue
+        res["block_wall_s"] = round(time.perf_counter() - t0, 2)
+        out[name if name != "rccl" else "steady_rccl"] = res
+    return out
+
+
+def rccl_steady_block(R: "Rank", args) -> dict:
+    """config 2's loader with the native RCCL lockstep forced at world 1 (lockstep='always' on a
+    world-1 nccl group): one all-reduce(MIN) agreement over the private RCCL communicator every
+    ``lockstep_depth`` steps -- the RCCL cost a one-GPU box can show."""
+    torch, dist = R.torch, R.dist
+    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
+    from torchkafka_amd.broker import SyntheticBroker
+
+    class Records(KafkaDataset):
+        schema = FixedWidth(torch.float32, (args.dim,))
+
+    url = f"shm://tkbench-rccl-{os.getpid()}"
+    B, steps, warm = args.batch_size, 50000, 200
+    n_parts = args.partitions_per_gpu
+    per_part = int(math.ceil((steps + warm + args.workers * 18) * B * 1.25 / n_parts)) + B
+    broker = SyntheticBroker.create(url, log_capacity=1 << 34, index_capacity=1 << 22)
+    own_group = not dist.is_initialized()
+    try:
+        broker.create_topic("bench", n_parts)
+        broker.fill("bench", per_part, "fixed_f32", size=args.dim, records_per_batch=args.records_per_batch,
+                    threads=min(16, n_parts), keyed=True)
+        if own_group:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ["MASTER_PORT"] = str(_free_port())
+            dist.init_process_group("nccl", rank=0, world_size=1)  # lazy: no torch RCCL comm (streams) is made
+        dtypes = {"bf16": torch.bfloat16, "fp8": torch.float8_e4m3fn, "f16": torch.float16, "f32": torch.float32}
+        ld = DeviceLoader(Records.placeholder(), B, num_workers=args.workers, device=R.device,
+                          dtype=dtypes[args.dtype], prefetch=args.prefetch, lockstep="always",
+                          lockstep_depth=args.lockstep_depth, coalesce=args.coalesce,
+                          coalesce_wait_us=args.coalesce_wait_us, numa_bind=not args.no_numa, verify=args.verify,
+                          worker_init_fn=Records.init_worker("bench", bootstrap_servers=url, group_id="bench-rccl",
+                                                             auto_offset_reset="earliest"))
+        it = iter(auto_commit(ld))
+        for _ in range(warm):
+            next(it)
+        res = time_steps(R, it, steps, ld)
+        blk = steady_block(R, res, steps, args.dim)
+        st = res["stats"]
+        blk["lockstep"] = dict(ld.lockstep_info)
+        blk["lockstep_agreements"] = st.get("lockstep_agreements", 0)
+        blk["lockstep_wait_us_per_step"] = round(st.get("lockstep_wait_us_per_batch", 0.0), 3)
+        blk["lockstep_step_wait_max_us"] = round(st.get("lockstep_step_wait_max_us", 0.0), 1)
+        blk["streams"] = ld.stream_plan()
+        it.close()
+        ld.close()
+        return blk
+    finally:
+        if own_group and dist.is_initialized():
+            dist.destroy_process_group()
+        broker.destroy()
+
+
 def run_rank(args) -> int:
     R = Rank(args)
     torch, dist = R.torch, R.dist
@@ -362,9 +513,24 @@ def run_rank(args) -> int:
     if extra_steps <= 0:
         extra = []
     extra_warm = max(50, args.warmup)
-    consumed = max(args.warmup + args.steps + steady, (extra_warm + extra_steps) if extra else 0)
-    batches = consumed + args.workers * ((args.slots_per_worker or 8) + 2)
-    per_part = int(math.ceil(batches * B * 1.25 / max(1, len(mine)))) + B
+
+    def backlog(steady_n, extra_n):
+        consumed = max(args.warmup + args.steps + steady_n, (extra_warm + extra_n) if extra else 0)
+        batches = consumed + args.workers * ((args.slots_per_worker or 8) + 2)
+        return int(math.ceil(batches * B * 1.25 / max(1, len(mine)))) + B
+
+    per_part = backlog(steady, extra_steps)
+    preflight = memory_preflight(R, per_part * len(mine) * record_bytes(args))
+    if preflight["scale"] < 1.0:
+        # not enough shared memory / RAM for every local rank's backlog: shorten the steady blocks
+        steady = int(steady * preflight["scale"])
+        extra_steps = int(extra_steps * preflight["scale"])
+        per_part = backlog(steady, extra_steps)
+        preflight["shrunk_to"] = {"steady_steps": steady, "extra_steps": extra_steps,
+                                  "bytes_per_rank": per_part * len(mine) * record_bytes(args)}
+        if steady < 2000:
+            print(f"[bench] rank {rank}: not enough memory for the backlog ({preflight}): refusing", file=sys.stderr)
+            return 2
     t_fill = time.perf_counter()
     broker.fill("bench", per_part, "fixed_f32", size=args.dim, partitions=mine,
                 records_per_batch=args.records_per_batch, threads=min(16, len(mine)), keyed=True)
@@ -379,7 +545,7 @@ def run_rank(args) -> int:
             in_order=args.in_order, h2d=h2d, copy_streams=args.copy_streams, lockstep_depth=args.lockstep_depth,
             event_every=args.event_every, numa_bind=not args.no_numa, coalesce=args.coalesce,
             coalesce_wait_us=args.coalesce_wait_us, decode=args.decode, lockstep=lockstep,
-            mirror_chunk_mib=args.mirror_chunk_mib, commit=commit,
+            mirror_chunk_mib=args.mirror_chunk_mib, commit=commit, verify=args.verify,
             **({"mirror_chunks": args.mirror_chunks} if args.mirror_chunks else {}),
             worker_init_fn=ds.init_worker("bench", bootstrap_servers=servers, group_id=group,
                                           auto_offset_reset="earliest", check_crcs=not args.no_crc),
@@ -495,6 +661,8 @@ def run_rank(args) -> int:
         finally:
             srv.close()
 
+    config_out = run_config_blocks(R, args)
+
     if rank == 0:
         if args.stats:
             print(json.dumps({"loader_stats": stats, "fill_s": t_fill,
@@ -548,6 +716,8 @@ def run_rank(args) -> int:
             "steady_state": steady_out,
             **extra_out,
             "bridge": bridge_out,
+            **config_out,
+            "memory_preflight": preflight,
             # the native binaries that ran, with the source sha compiled into each (ops.build_info)
             "native_build": _native_build(),
         }
@@ -569,7 +739,7 @@ def _native_build() -> dict:
 
 def main() -> int:
     args = parse()
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.self_launch):
         return launch_ranks(args)
     return run_rank(args)
 

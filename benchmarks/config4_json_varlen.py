@@ -23,7 +23,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20000)
     ap.add_argument("--warmup", type=int, default=30)
@@ -42,8 +42,13 @@ def main():
     ap.add_argument("--slots-per-worker", type=int, default=None)
     ap.add_argument("--event-every", type=int, default=None)
     ap.add_argument("--prefetch", type=int, default=2)
-    args = ap.parse_args()
+    ap.add_argument("--verify", default="deliver", choices=["deliver", "commit"])
+    return ap.parse_args(argv)
 
+
+def run(args, sync=None) -> dict:
+    """One config-4 measurement; ``sync`` (optional) is called before and after the timed steps
+    (bench.py passes its barrier + synchronize)."""
     import torch
 
     from torchkafka_amd import DeviceLoader, JsonArray, KafkaDataset, auto_commit
@@ -64,6 +69,7 @@ def main():
         dl = DeviceLoader(Json.placeholder(), B, num_workers=args.workers, device=args.device, dtype=torch.bfloat16,
                           json_parse=args.json_parse, h2d=args.h2d, decode=args.decode, json_count=args.json_count,
                           slots_per_worker=args.slots_per_worker, event_every=args.event_every, prefetch=args.prefetch,
+                          verify=args.verify,
                           worker_init_fn=Json.init_worker("json", bootstrap_servers=url, group_id="cfg4",
                                                           auto_offset_reset="earliest"))
         it = iter(auto_commit(dl))
@@ -71,32 +77,44 @@ def main():
             x, lens = next(it)
         if x.is_cuda:
             torch.cuda.synchronize()
+        if sync is not None:
+            sync()
         dl.reset_stats()
         t0 = time.perf_counter()
         rows = 0
-        elems = 0
         for _ in range(args.steps):
             x, lens = next(it)
             rows += x.shape[0]
         if x.is_cuda:
             torch.cuda.synchronize()
+        if sync is not None:
+            sync()
         el = time.perf_counter() - t0
         st = dl.stats_summary()
         it.close()
+        dl.close()
         text_bytes = b.partition_stats("json", 0)["log_bytes"] / max(1, b.end_offset("json", 0))
-        print(json.dumps({"config": 4, "metric": "JSON records/s to GPU (bf16 padded), per-batch commit",
-                          "value": round(rows / el), "ms_per_step": round(el / args.steps * 1e3, 4),
-                          "batch_size": B, "workers": args.workers, "json_parse": args.json_parse, "h2d": args.h2d,
-                          "decode": (("device (json_span.hip from an HBM mirror filled by SDMA copies)"
-                                      if dl._mirror() else "device (json_span.hip from the pinned logs)")
-                                     if dl._json_span() else args.decode),
-                          "json_count": "device" if dl._json_count() else "workers",
-                          "timed_s": round(el, 4), "steps": args.steps,
-                          "avg_record_bytes": round(text_bytes),
-                          "last_batch_shape": list(x.shape),
-                          "device": args.device, "fill_s": round(fill_s, 2), "loader": st}))
+        return {"config": 4, "metric": "JSON records/s to GPU (bf16 padded), per-batch commit",
+                "value": round(rows / el), "ms_per_step": round(el / args.steps * 1e3, 4),
+                "gb_per_s_text": round(rows / el * text_bytes / 1e9, 2),
+                "batch_size": B, "workers": args.workers, "partitions": args.partitions,
+                "json_parse": args.json_parse, "h2d": args.h2d, "verify": dl.verify,
+                "decode": (("device (json_span.hip from an HBM mirror filled by SDMA copies)"
+                            if dl._mirror() else "device (json_span.hip from the pinned logs)")
+                           if dl._json_span() else args.decode),
+                "json_count": "device" if dl._json_count() else "workers",
+                "timed_s": round(el, 4), "steps": args.steps,
+                "avg_record_bytes": round(text_bytes),
+                "last_batch_shape": list(x.shape),
+                "commits": st["commits"], "commit_latency_p50_us": round(st["commit_latency_p50_us"], 2),
+                "commit_latency_p99_us": round(st["commit_latency_p99_us"], 2),
+                "device": args.device, "fill_s": round(fill_s, 2), "loader": st}
     finally:
         b.destroy()
+
+
+def main():
+    print(json.dumps(run(parse())))
 
 
 if __name__ == "__main__":

@@ -22,9 +22,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 YARDSTICK = 3481.0
 
 
-def main():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch-size", type=int, default=8)
     # Device decode leaves the workers only the record headers (~25-33 us per 8 MiB batch), so the ring
@@ -37,8 +37,12 @@ def main():
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy", "direct"])
-    args = ap.parse_args()
+    ap.add_argument("--verify", default="deliver", choices=["deliver", "commit"])
+    return ap.parse_args(argv)
 
+
+def run(args, sync=None) -> dict:
+    """One config-5 measurement; ``sync`` (optional) brackets the timed steps (bench.py's barrier)."""
     import torch
 
     from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
@@ -61,7 +65,7 @@ def main():
         fill_s = time.perf_counter() - t
         dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
         dl = DeviceLoader(Big.placeholder(), B, num_workers=args.workers, device=args.device, dtype=dtype,
-                          slots_per_worker=args.slots_per_worker, prefetch=1, h2d=args.h2d,
+                          slots_per_worker=args.slots_per_worker, prefetch=1, h2d=args.h2d, verify=args.verify,
                           worker_init_fn=Big.init_worker("big", bootstrap_servers=url, group_id="cfg5",
                                                          auto_offset_reset="earliest"))
         it = iter(auto_commit(dl))
@@ -69,6 +73,8 @@ def main():
             x = next(it)
         if x.is_cuda:
             torch.cuda.synchronize()
+        if sync is not None:
+            sync()
         dl.reset_stats()
         t0 = time.perf_counter()
         rows = 0
@@ -77,18 +83,29 @@ def main():
             rows += x.shape[0]
         if x.is_cuda:
             torch.cuda.synchronize()
+        if sync is not None:
+            sync()
         el = time.perf_counter() - t0
         st = dl.stats_summary()
         it.close()
+        dl.close()
         v = rows / el
-        print(json.dumps({"config": 5, "metric": "1 MiB records/s to GPU, per-batch commit", "value": round(v, 1),
-                          "gb_per_s": round(v * D * 4 / 1e9, 2), "vs_yardstick": round(v / YARDSTICK, 2),
-                          "commit_p50_us": st["commit_p50_us"], "commit_p99_us": st["commit_p99_us"],
-                          "batch_size": B, "partitions": args.partitions, "workers": args.workers,
-                          "slots_per_worker": args.slots_per_worker, "device": args.device, "fill_s": round(fill_s, 1),
-                          "loader": st}))
+        return {"config": 5, "metric": "1 MiB records/s to GPU, per-batch commit", "value": round(v, 1),
+                "gb_per_s": round(v * D * 4 / 1e9, 2), "vs_yardstick": round(v / YARDSTICK, 2),
+                "steps": args.steps, "timed_s": round(el, 4), "commits": st["commits"],
+                "commit_p50_us": round(st["commit_p50_us"], 2), "commit_p99_us": round(st["commit_p99_us"], 2),
+                "commit_latency_means": "request of batch k+1 -> batch k's offsets stored (incl. its CRC verdict)",
+                "commit_latency_p50_us": round(st["commit_latency_p50_us"], 2),
+                "commit_latency_p99_us": round(st["commit_latency_p99_us"], 2),
+                "batch_size": B, "partitions": args.partitions, "workers": args.workers,
+                "slots_per_worker": args.slots_per_worker, "verify": dl.verify, "device": args.device,
+                "fill_s": round(fill_s, 1), "loader": st}
     finally:
         b.destroy()
+
+
+def main():
+    print(json.dumps(run(parse())))
 
 
 if __name__ == "__main__":

@@ -334,9 +334,8 @@ def test_batches_carry_their_worker_and_collate_fn_is_restored(broker):
     dl2 = DataLoader(PartOffset.placeholder(), batch_size=4, num_workers=1, persistent_workers=True,
                      worker_init_fn=PartOffset.init_worker("topic", **kw(broker, group_id="group_2",
                                                                           consumer_timeout_ms=300)))
-    iter(dl2)  # workers start with the plain collate_fn
     with pytest.raises(RuntimeError, match="persistent_workers"):
-        next(auto_commit(dl2))
+        next(auto_commit(dl2))  # refused before any worker starts: they would keep this iteration's channel
 
 
 def test_d4_commit_worker_signal_after_stream_end_is_harmless(broker):
@@ -490,3 +489,47 @@ def test_readme_rand8_multiprocess(broker):
     n = sum(b.shape[0] for b in auto_commit(dataloader))
     assert n == 20
     assert broker.committed_offsets("group_1", "topic") == {0: 10, 1: 10}
+
+
+def test_persistent_workers_are_refused_and_the_loader_stays_plain(broker):
+    """auto_commit cannot serve persistent workers (they would keep the first iteration's stamping
+    collate_fn and commit channel); it refuses before any worker starts, so the same DataLoader
+    still yields plain batches for two epochs when iterated directly."""
+    produce_offsets(broker, n=8, partitions=1)
+    dl = DataLoader(PartOffset.placeholder(), batch_size=4, num_workers=1, persistent_workers=True,
+                    worker_init_fn=PartOffset.init_worker("topic", **kw(broker, group_id="gp",
+                                                                         consumer_timeout_ms=300)))
+    with pytest.raises(RuntimeError, match="persistent_workers"):
+        next(auto_commit(dl))
+    assert getattr(dl, "_iterator", None) is None and dl.collate_fn is not None
+    first = list(dl)
+    assert len(first) == 2 and all(isinstance(b, torch.Tensor) for b in first)
+    # the persistent worker's consumer resumes at its position: the stream has ended, no stamps
+    assert all(isinstance(b, torch.Tensor) for b in list(dl))
+
+
+def test_channel_liveness_comes_from_registered_pids():
+    """auto_commit no longer reads the DataLoader's private worker list: workers register their
+    pid in the commit channel, and a dead (or never started) worker is not waited for."""
+    import multiprocessing as mp
+    import os
+    import time as _t
+
+    from torchkafka_amd.loader.commit_channel import CommitChannel
+
+    ch = CommitChannel(2, 4)
+    try:
+        assert not ch.alive(0)
+        ch.register(0, os.getpid())
+        assert ch.alive(0)
+        p = mp.get_context("fork").Process(target=_t.sleep, args=(0.01,))
+        p.start()
+        ch.register(1, p.pid)
+        p.join()  # reaped: the pid is gone
+        assert not ch.alive(1)
+        ch.request(1, 3)  # a request the dead worker will never acknowledge
+        t0 = _t.monotonic()
+        assert ch.wait_acks(2.0)
+        assert _t.monotonic() - t0 < 0.5
+    finally:
+        ch.close()

@@ -485,6 +485,12 @@ def test_ascii_keys_and_schema_validation():
 
     assert core().key_int64(b"-42", 2, -1) == -42 and core().key_int64(b"4x", 2, -1) == -1
     assert core().key_int64(None, 0, 9) == 9 and core().key_int64(b"\0" * 7 + b"\x05", 0, -1) == 5
+    # 19-digit keys: the int64 range is exact at both ends, one past it is the default (no overflow)
+    k = core().key_int64
+    assert k(b"9223372036854775807", 2, -1) == 2**63 - 1
+    assert k(b"-9223372036854775808", 2, -1) == -2**63
+    assert k(b"9223372036854775808", 2, -1) == -1 and k(b"-9223372036854775809", 2, -1) == -1
+    assert k(b"9999999999999999999", 2, 7) == 7 and k(b"+1234567890123456789", 2, -1) == 1234567890123456789
     with pytest.raises(ValueError):
         Key("utf16")
     with pytest.raises(ValueError):

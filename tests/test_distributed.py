@@ -126,3 +126,59 @@ def test_ranks_mirror_their_partitions_of_a_cluster(broker, tmp_path):
         assert res[r]["mirrored"] == [r, r + world] and res[r]["parts"] == [r, r + world]
         assert res[r]["steps"] == 10
     assert broker.committed_offsets("gb", "t") == {p: 50 for p in range(4)}
+
+
+def _sync_rank_main(rank, world, url, port, outdir):
+    import torch.distributed as dist
+
+    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
+    from torchkafka_amd.broker.synthetic import open_broker
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class Vec(KafkaDataset):
+        schema = FixedWidth(torch.float32, (8,))
+
+    b = open_broker(url)
+    dl = DeviceLoader(Vec.placeholder(), 10, num_workers=2, device="cpu", commit="sync", return_info=True,
+                      worker_init_fn=Vec.init_worker("t", bootstrap_servers=url, group_id="gs",
+                                                     auto_offset_reset="earliest", consumer_timeout_ms=400))
+    want: dict[int, int] = {}   # end of every batch this rank finished, per partition
+    checks, mismatches, steps = 0, [], 0
+    for batch in auto_commit(dl):
+        if steps:
+            got = {p: o for p, o in b.committed_offsets("gs", "t").items() if p in want}
+            checks += 1
+            if got != want:
+                mismatches.append((steps, got, dict(want)))
+        for pidx, _first, nxt, _n in batch.watermarks:
+            want[pidx] = max(want.get(pidx, 0), nxt)
+        steps += 1
+    with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
+        json.dump({"steps": steps, "checks": checks, "mismatches": mismatches[:3],
+                   "commits": dl.stats.commits, "sync_commits": len(dl.stats.sync_commit_ns)}, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sync_commit_is_a_per_batch_barrier_across_ranks(broker, tmp_path, world):
+    """commit='sync' at world > 1 (the reference's contract, auto_commit.py:55-58 /
+    kafka_dataset.py:130, made a cross-rank barrier): on every rank, at the moment batch k+1 is
+    yielded, the group's committed offsets for that rank's partitions are exactly the end of
+    batch k -- including the steps before the rank with the least data runs dry."""
+    n_parts = 2 * world
+    broker.create_topic("t", n_parts)
+    per_rank = {r: 100 - 40 * (r == 0) for r in range(world)}  # rank 0 runs dry after 6 batches
+    for p in range(n_parts):
+        broker.fill("t", per_rank[p % world] // 2, "fixed_f32", size=8, partitions=[p], records_per_batch=5)
+    tmp.spawn(_sync_rank_main, args=(world, broker.url, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
+    for r in res:
+        assert r["steps"] == 6, r
+        assert r["checks"] == 5 and r["mismatches"] == [], r
+        assert r["sync_commits"] >= r["steps"], r
+    committed = broker.committed_offsets("gs", "t")
+    for r in range(world):
+        assert committed[r] + committed[r + world] == 60

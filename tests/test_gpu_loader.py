@@ -416,7 +416,8 @@ def test_json_device_parse_mixed_rows_match_python(broker, h2d, coalesce):
     assert broker.committed_offsets("g", "m") == {0: 150, 1: 150}
 
 
-def test_json_device_parse_error_raises_before_commit(broker):
+@pytest.mark.parametrize("verify", ["commit", "deliver"])
+def test_json_device_parse_error_raises_before_commit(broker, verify):
     from torchkafka_amd import DeviceLoader, JsonArray, auto_commit
     from torchkafka_amd.client.errors import CorruptRecordException
 
@@ -425,7 +426,7 @@ def test_json_device_parse_error_raises_before_commit(broker):
     broker.create_topic("e", 1)
     _produce_json(broker, "e", rows)
     DS = _dataset(JsonArray())
-    dl = DeviceLoader(DS.placeholder(), 10, num_workers=1, device="cuda:0", json_parse="device",
+    dl = DeviceLoader(DS.placeholder(), 10, num_workers=1, device="cuda:0", json_parse="device", verify=verify,
                       worker_init_fn=DS.init_worker("e", bootstrap_servers=broker.url, group_id="g",
                                                     auto_offset_reset="earliest", consumer_timeout_ms=300))
     seen = 0
@@ -434,7 +435,10 @@ def test_json_device_parse_error_raises_before_commit(broker):
             seen += x.shape[0]
             torch.cuda.synchronize()
     # batches 0-3 (offsets 0..39) were clean and committed; the batch holding offset 40 never is
-    assert seen >= 50
+    if verify == "deliver":
+        assert seen == 40  # the loop body never saw the malformed batch
+    else:
+        assert seen >= 50  # the verdict gates only the commit: the raise comes steps later
     assert broker.committed_offsets("g", "e") == {0: 40}
 
 

@@ -162,6 +162,39 @@ def test_device_decode_crc_failure_raises_before_commit(broker, size, rpb):
     assert committed is not None and committed <= bad_rb * rpb
 
 
+@pytest.mark.parametrize("coalesce", [1, 8])
+def test_verify_deliver_never_yields_a_corrupt_batch(broker, coalesce):
+    """verify='deliver' (the default): a batch is handed out only after its device CRC verdict
+    landed, so the loop body never sees the corrupt RecordBatch's records -- as kafka-python's
+    check_crcs iterator raises before _process sees them (reference kafka_dataset.py:156-162).
+    The batches before it are committed, it never is."""
+    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
+    from torchkafka_amd.client.errors import CorruptRecordException
+
+    rpb, size, bad_rb = 16, 64, 9
+    broker.create_topic("c", 1)
+    broker.fill("c", 400, "fixed_f32", size=size, records_per_batch=rpb)
+    pidx = broker.pidx("c", 0)
+    log = broker.native.read_log(pidx, 0, broker.native.log_bytes(pidx))
+    pos, k = 0, 0
+    while k < bad_rb:
+        pos += 12 + int.from_bytes(log[pos + 8:pos + 12], "big")
+        k += 1
+    _corrupt(broker, pidx, pos + 61 + 30 + size * 2)
+    DS = _dataset(FixedWidth(torch.float32, (size,)))
+    dl = DeviceLoader(DS.placeholder(), rpb, num_workers=1, device="cuda:0", decode="device", coalesce=coalesce,
+                      dtype=torch.float32,
+                      worker_init_fn=DS.init_worker("c", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    assert dl.verify == "deliver"
+    seen = []
+    with pytest.raises(CorruptRecordException, match=f"offset {bad_rb * rpb} .*failed CRC check"):
+        for x in auto_commit(dl):
+            seen += x[:, 0].long().tolist()  # the user's step: reads every record of the batch
+    assert seen == list(range(bad_rb * rpb)), (len(seen), seen[-3:])
+    assert broker.committed_offsets("g", "c").get(0) == bad_rb * rpb
+
+
 def test_device_decode_without_crc_checks(broker):
     """check_crcs=False: no verification anywhere (kafka-python semantics), only values are read."""
     from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit

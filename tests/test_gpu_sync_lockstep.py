@@ -1,0 +1,102 @@
+"""commit='sync' under the cross-rank lockstep on the native (GPU) step driver: two ranks on one
+MI355X over a gloo group (the driver's CreditLockstep in sync mode; RCCL refuses two ranks on one
+device, so the RCCL transport is covered at world 1 in test_zz_gpu_rccl.py).
+
+The reference's contract (auto_commit.py:55-58, kafka_dataset.py:130): batch k's commit completes
+before batch k+1 is handed out.  Under DDP that commit is a barrier: at the moment batch k+1 is
+yielded on any rank, every rank's part of batch k is committed.
+"""
+import json
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def batch_ends(x) -> dict:
+    """{partition: offset after the batch's last record} from the fixed_f32 rows (col 0 offset, col 1 partition)."""
+    v = x.float().cpu()
+    out = {}
+    for p in v[:, 1].long().unique().tolist():
+        out[p] = int(v[v[:, 1] == p][:, 0].max().item()) + 1
+    return out
+
+
+def _rank_main(rank, world, url, port, outdir, verify):
+    import torch.distributed as dist
+
+    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
+    from torchkafka_amd.broker.synthetic import open_broker
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class Vec(KafkaDataset):
+        schema = FixedWidth(torch.float32, (16,))
+
+    b = open_broker(url)
+    dl = DeviceLoader(Vec.placeholder(), 32, num_workers=2, device="cuda:0", dtype=torch.float32, commit="sync",
+                      lockstep="host", verify=verify,
+                      worker_init_fn=Vec.init_worker("t", bootstrap_servers=url, group_id="gs",
+                                                     auto_offset_reset="earliest", consumer_timeout_ms=500))
+    want: dict = {}
+    steps, mismatches = 0, []
+    for x in auto_commit(dl):
+        if steps:
+            got = {p: o for p, o in b.committed_offsets("gs", "t").items() if p in want}
+            if got != want:
+                mismatches.append((steps, got, dict(want)))
+        for p, e in batch_ends(x).items():
+            want[p] = max(want.get(p, 0), e)
+        steps += 1
+    st = dl.stats_summary()
+    dl.close()
+    with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
+        json.dump({"steps": steps, "mismatches": mismatches[:3], "commits": st["commits"],
+                   "agreements": st["lockstep_agreements"], "lat_p99_us": st["commit_latency_p99_us"]}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("verify", ["deliver", "commit"])
+def test_sync_commit_barrier_two_ranks_one_gpu(broker, tmp_path, verify):
+    import torch.multiprocessing as tmp
+
+    world = 2
+    broker.create_topic("t", 4)
+    # rank 0 (partitions 0, 2) has 3 batches of 32 less than rank 1: it runs dry first
+    for p in range(4):
+        broker.fill("t", 240 - 48 * (p % 2 == 0), "fixed_f32", size=16, partitions=[p], records_per_batch=16)
+    ctx = tmp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, broker.url, port, str(tmp_path), verify))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=100)
+        if p.is_alive():
+            p.kill()
+            p.join()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
+    want_steps = (2 * 192) // 32
+    for r in res:
+        assert r["steps"] == want_steps, r
+        assert r["mismatches"] == [], r
+        # every batch committed on its own (one commit per step, the last at the end)
+        assert r["commits"] >= want_steps - 1, r
+    committed = broker.committed_offsets("gs", "t")
+    assert committed[0] + committed[2] == 384 and committed[1] + committed[3] == 384, committed

@@ -61,7 +61,7 @@ class _Producer:
         return 1 if self.produced > before else 0
 
 
-def _rank_main(rank, world, port, outdir, totals, cap, depth, slow_rank, die_rank):
+def _rank_main(rank, world, port, outdir, totals, cap, depth, slow_rank, die_rank, sync=False):
     import torch
     import torch.distributed as dist
 
@@ -79,6 +79,7 @@ def _rank_main(rank, world, port, outdir, totals, cap, depth, slow_rank, die_ran
 
     c = core()
     lock = c.CreditLockstep(c.PyLockstepTransport(allreduce_min), depth)
+    lock.set_sync(sync)
     committed = []
     lock.set_on_committable(lambda wms: committed.extend(w[1] for w in wms))
     src = _Producer(totals[rank], cap, seed=1000 * rank + depth, slow=(rank == slow_rank))
@@ -86,6 +87,10 @@ def _rank_main(rank, world, port, outdir, totals, cap, depth, slow_rank, die_ran
     steps, prev, committed_at_deliver = 0, None, []
     try:
         while True:
+            # the driver's order: asking for the next batch finishes the previous one first
+            if prev is not None:
+                lock.finished(prev, [(rank, prev, prev + 1, 1)])
+                prev = None
             r = lock.next(src, 20)
             if r == -1:
                 continue
@@ -96,8 +101,6 @@ def _rank_main(rank, world, port, outdir, totals, cap, depth, slow_rank, die_ran
             idx = lock.delivered()
             assert idx == steps
             src.delivered += 1
-            if prev is not None:
-                lock.finished(prev, [(rank, prev, prev + 1, 1)])
             prev = idx
             committed_at_deliver.append(len(committed))
             steps += 1
@@ -117,12 +120,12 @@ def _rank_main(rank, world, port, outdir, totals, cap, depth, slow_rank, die_ran
         dist.destroy_process_group()
 
 
-def _run(tmp_path, world, totals, cap=8, depth=2, slow_rank=-1, die_rank=-1):
+def _run(tmp_path, world, totals, cap=8, depth=2, slow_rank=-1, die_rank=-1, sync=False):
     # plain processes (not torch's spawn helper, which kills the others when one rank dies)
     port = _free_port()
     ctx = mp.get_context("spawn")
     procs = [ctx.Process(target=_rank_main,
-                         args=(r, world, port, str(tmp_path), totals, cap, depth, slow_rank, die_rank))
+                         args=(r, world, port, str(tmp_path), totals, cap, depth, slow_rank, die_rank, sync))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -156,6 +159,30 @@ def test_credit_lockstep_stops_together_and_commits_only_finished(tmp_path, worl
             assert n_committed <= k
         # one agreement grants as many batches as the slowest rank staged: amortised below 1/step
         assert r["agreements"] <= want + 2 + world
+
+
+@pytest.mark.parametrize("world,totals,cap", [
+    (2, [40, 25], 4),
+    (2, [30, 30], 2),
+    (4, [30, 50, 10, 70], 8),
+    (4, [20, 0, 35, 40], 8),           # a rank with no partitions: everyone stops at step 0
+    (4, [12, 40, 40, 40], 3),          # one rank runs dry early
+])
+def test_sync_mode_commits_every_batch_before_the_next_is_delivered(tmp_path, world, totals, cap):
+    """commit='sync' under the lockstep (the reference's per-batch commit, auto_commit.py:55-58,
+    as an RCCL barrier): when batch k+1 is handed out on any rank, batch k is committable on
+    every rank -- an agreement at step k+1 proved every rank finished it."""
+    res = _run(tmp_path, world, totals, cap=cap, depth=2, slow_rank=world - 1, sync=True)
+    assert len(res) == world
+    want = min(totals)
+    for r in res:
+        assert r["error"] is None, r["error"]
+        assert r["steps"] == want, (r["rank"], r["steps"], want)
+        assert r["committed"] == list(range(want))
+        # exactly batches 0..k-1 committable at the moment batch k is delivered
+        assert r["committed_at_deliver"] == list(range(want)), r["committed_at_deliver"]
+        # one agreement per delivered step (plus starved rounds, the stop and the final barrier)
+        assert r["agreements"] >= want
 
 
 def test_credit_lockstep_peer_death_fails_instead_of_hanging(tmp_path):

@@ -104,3 +104,42 @@ def test_native_lockstep_two_ranks_one_gpu():
     assert r.returncode == 0, r.stdout[-4000:]
     oks = _rank_lines(r.stdout)
     assert len(oks) == 2 and all(o["ok"] for o in oks), r.stdout[-4000:]
+
+
+def test_bench_eight_ranks_on_cpu_without_torchrun():
+    """The driver's N = 8 command line (`python bench.py --gpus 8`, no torchrun) rehearsed on the CPU
+    over gloo: 8 self-launched ranks, 64 partitions, every rank's rate reported, one JSON line."""
+    r = _bench("--gpus", "8", "--device", "cpu", "--workers", "1", "--steps", "20", "--warmup", "5",
+               "--steady-steps", "200", "--extra-blocks", "", "--bridge-steps", "0", "--config-blocks", "",
+               timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = lines[0]
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8" and out["config"]["partitions"] == 64
+    assert out["launcher"].startswith("bench.py self-launch")
+    assert out["ranks"]["world_size"] == 8 and out["ranks"]["rank_id_sum"] == 28
+    assert len(out["per_rank_records_per_s"]) == 8 and all(v > 0 for v in out["per_rank_records_per_s"])
+    assert len(out["steady_state"]["per_rank_records_per_s"]) == 8
+    assert out["memory_preflight"]["local_ranks"] == 8 and out["memory_preflight"]["scale"] == 1.0
+
+
+@pytest.mark.gpu
+def test_bench_launcher_parent_never_initialises_hip(tmp_path):
+    """The launcher path the driver's N > 1 runs take, exercised at --gpus 1 (--self-launch): the
+    parent counts GPUs without a HIP call (KFD sysfs + amdsmi) and starts its rank with Popen
+    having neither initialised torch's HIP state nor opened /dev/kfd."""
+    rep = tmp_path / "parent.json"
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e["TK_BENCH_PARENT_REPORT"] = str(rep)
+    e["PYTHONPATH"] = ROOT + os.pathsep + e.get("PYTHONPATH", "")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--self-launch", "--steps", "20", "--warmup", "5",
+                        "--steady-steps", "500", "--extra-blocks", "", "--bridge-steps", "0", "--config-blocks", ""],
+                       cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240, env=e)
+    assert r.returncode == 0, r.stderr[-3000:]
+    parent = json.load(open(rep))
+    assert parent["torch_cuda_initialized"] is False and parent["kfd_fds"] == 0, parent
+    assert parent["gpus_visible"]["count"] >= 1, parent
+    out = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')][0]
+    assert out["launcher"].startswith("bench.py self-launch") and out["n_gpus"] == 1

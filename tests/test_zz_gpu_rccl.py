@@ -64,3 +64,47 @@ def test_rccl_lockstep_transport_failure_detection_plumbing():
         assert ls.allreduce_min(i, -i, 7) == (i, -i, 7)
     assert not ls.aborted
     del ls
+
+
+def test_native_rccl_lockstep_sync_commit_world1(broker):
+    """commit='sync' through the RCCL lockstep (world 1, lockstep='always'): one agreement per step
+    makes batch k committable before batch k+1 is handed out, and k's offsets are stored then."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
+    from test_gpu_sync_lockstep import batch_ends
+
+    class Vec(KafkaDataset):
+        schema = FixedWidth(torch.float32, (8,))
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = "29543"
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        broker.create_topic("t", 2)
+        broker.fill("t", 200, "fixed_f32", size=8, records_per_batch=10)
+        dl = DeviceLoader(Vec.placeholder(), 20, num_workers=2, device="cuda:0", lockstep="always", commit="sync",
+                          dtype=torch.float32,
+                          worker_init_fn=Vec.init_worker("t", bootstrap_servers=broker.url, group_id="gsync",
+                                                         auto_offset_reset="earliest", consumer_timeout_ms=300))
+        want, steps, bad = {}, 0, []
+        for x in auto_commit(dl):
+            if steps:
+                got = {p: o for p, o in broker.committed_offsets("gsync", "t").items() if p in want}
+                if got != want:
+                    bad.append((steps, got, dict(want)))
+            for p, e in batch_ends(x).items():
+                want[p] = max(want.get(p, 0), e)
+            steps += 1
+        st = dl.stats_summary()
+        info = dict(dl.lockstep_info)
+        dl.close()
+        assert info.get("transport") == "rccl"
+        assert steps == 20 and bad == []
+        assert st["commits"] >= steps - 1
+        assert broker.committed_offsets("gsync", "t") == {0: 200, 1: 200}
+    finally:
+        dist.destroy_process_group()

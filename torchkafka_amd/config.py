@@ -151,6 +151,7 @@ _CHOICES = {
     "sharding": ("static", "group"),
     "commit_on": ("host", "device"),
     "commit": ("async", "sync"),
+    "verify": ("commit", "deliver"),
     "commit_sink": ("auto", "broker", "worker"),
     "h2d": ("auto", "dma", "zerocopy", "direct"),
     "decode": ("auto", "device", "host"),
@@ -163,6 +164,9 @@ _CHOICE_HELP = {
     "json_parse": "'auto', 'device' (gfx950 parse kernel) or 'host' (worker parse)",
     "commit_sink": ("'auto', 'broker' (the main process stores offsets into the synthetic broker) or "
                     "'worker' (each worker's consumer commits its partitions)"),
+    "verify": ("'commit' (a device-checked batch's CRC32C / parse verdict gates its commit: it is handed out "
+               "while its kernel may still run) or 'deliver' (the verdict gates delivery: a corrupt batch raises "
+               "CorruptRecordException before it is yielded, as kafka-python's check_crcs iterator does)"),
     "commit": ("'async' (batch k's offsets are stored when batch k+1 is requested; a KafkaBridge forwards "
                "them to the coordinator within commit_interval_ms) or 'sync' (batch k+1 is handed out only "
                "once the coordinator answered batch k's OffsetCommit)"),
@@ -186,6 +190,7 @@ class LoaderConfig:
     multiprocessing_context: str = "fork"
     commit_on: str = "host"
     commit: str = "async"
+    verify: str = "deliver"
     commit_sink: str = "auto"
     lockstep: Any = True
     lockstep_timeout: float = 600.0

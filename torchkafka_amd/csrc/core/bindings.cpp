@@ -1012,6 +1012,7 @@ PYBIND11_MODULE(_tkcore, m) {
           },
           py::arg("index"), py::arg("watermarks"))
       .def("finish", &CreditLockstep::finish)
+      .def("set_sync", &CreditLockstep::set_sync, py::arg("sync"))
       .def(
           "set_on_committable",
           [](CreditLockstep& l, py::function f) {

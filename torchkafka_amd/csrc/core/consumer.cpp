@@ -670,12 +670,17 @@ int64_t key_int64(const uint8_t* key, int32_t len, int enc, int64_t dflt) {
     bool neg = false;
     if (i < len && (key[i] == '-' || key[i] == '+')) neg = key[i++] == '-';
     if (i == len || len - i > 19) return dflt;
-    int64_t v = 0;
+    // accumulate unsigned and bound before each step: 19 digits reach 9999999999999999999, past
+    // INT64_MAX; the most a key may hold is INT64_MAX, or INT64_MAX + 1 when negative
+    const uint64_t lim = neg ? uint64_t(INT64_MAX) + 1 : uint64_t(INT64_MAX);
+    uint64_t v = 0;
     for (; i < len; ++i) {
       if (key[i] < '0' || key[i] > '9') return dflt;
-      v = v * 10 + (key[i] - '0');
+      const uint64_t d = uint64_t(key[i] - '0');
+      if (v > (lim - d) / 10) return dflt;  // v * 10 + d would exceed lim
+      v = v * 10 + d;
     }
-    return neg ? -v : v;
+    return neg ? int64_t(0 - v) : int64_t(v);
   }
   if (len != 8) return dflt;
   uint64_t v;

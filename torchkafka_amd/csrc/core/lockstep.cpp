@@ -26,6 +26,7 @@ void CreditLockstep::settle() {
       std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
   wait_ns_ += waited;
   step_wait_ns_ += waited;
+  if (t.step > settled_step_) settled_step_ = t.step;
   if (res[1] != -res[2])
     throw LockstepError("lockstep: ranks are out of step (min " + std::to_string(res[1]) + ", max " +
                         std::to_string(-res[2]) + ")");
@@ -48,8 +49,18 @@ int CreditLockstep::next(LockstepSource& src, int64_t timeout_ms) {
 }
 
 int CreditLockstep::next_impl(LockstepSource& src, int64_t timeout_ms) {
-  // issue ahead while credits remain, so the round trip overlaps the delivery of granted batches
-  if (tickets_.empty() && !no_more_credit_ && granted_ - step_ <= depth_ && step_ < granted_) issue(src);
+  if (sync_) {
+    // every rank is at this step with the same tickets in flight (none, in sync mode): one
+    // agreement at step_ proves batches < step_ finished everywhere and settles them now
+    while (!tickets_.empty()) settle();
+    if (settled_step_ < step_) {
+      issue(src);
+      settle();
+    }
+  } else if (tickets_.empty() && !no_more_credit_ && granted_ - step_ <= depth_ && step_ < granted_) {
+    // issue ahead while credits remain, so the round trip overlaps the delivery of granted batches
+    issue(src);
+  }
   while (step_ >= granted_) {
     if (no_more_credit_) {
       stopped_ = true;

@@ -16,6 +16,12 @@
 // collective sequences stay aligned.  Completion of an agreement issued at step s proves every
 // rank reached s: batches < s are finished everywhere and become committable.  Two more words
 // ride along as a consistency check: step and -step (MIN of both = min and -max).
+//
+// Sync mode (commit='sync', the reference's per-batch commit contract, auto_commit.py:55-58 /
+// kafka_dataset.py:130): before batch k+1 may be handed out, an agreement issued at step k+1 must
+// have completed -- it proves every rank finished batch k, so k becomes committable on every rank
+// at that moment and the caller commits it before delivering.  One collective per step: the
+// issue-ahead pipelining is off, the agreement's credit still grants the following batches.
 #pragma once
 #include <chrono>
 #include <cstdint>
@@ -72,6 +78,9 @@ class CreditLockstep {
   void finish();
   // Committable batches are handed to this callback (settle / finish order = delivery order).
   void set_on_committable(std::function<void(std::vector<Watermark>&&)> f) { on_commit_ = std::move(f); }
+  // Sync mode (see above).  Every rank must use the same mode: it decides which collectives run.
+  void set_sync(bool s) { sync_ = s; }
+  bool sync() const { return sync_; }
 
   int64_t step() const { return step_; }
   int64_t granted() const { return granted_; }
@@ -105,7 +114,8 @@ class CreditLockstep {
   LockstepTransport* t_;
   int depth_;
   int64_t step_ = 0, granted_ = 0;
-  bool stopped_ = false, no_more_credit_ = false;
+  bool stopped_ = false, no_more_credit_ = false, sync_ = false;
+  int64_t settled_step_ = -1;  // highest step an agreement was issued at and has completed
   uint64_t agreements_ = 0, agreements_at_reset_ = 0;
   int64_t wait_ns_ = 0, step_wait_max_ns_ = 0, step_wait_ns_ = 0;
   std::deque<Ticket> tickets_;

@@ -153,6 +153,7 @@ PYBIND11_MODULE(_tkhip, m) {
            })
       .def("set_decode_streams", &Engine::set_decode_streams, py::arg("n"))
       .def("decode_streams", &Engine::decode_streams)
+      .def("copy_streams", &Engine::copy_streams)
       .def("synchronize", [](Engine& e) {
         py::gil_scoped_release nogil;
         e.synchronize();
@@ -338,6 +339,7 @@ PYBIND11_MODULE(_tkhip, m) {
              s["lockstep_agreements"] = d.lockstep_agreements();
              s["lockstep_wait_ns"] = d.lockstep_wait_ns();
              s["lockstep_step_wait_max_ns"] = d.lockstep_step_wait_max_ns();
+             s["verify_wait_ns"] = d.verify_wait_ns_;
              return s;
            })
       .def("reset_stats", &MainDriver::reset_stats)
@@ -346,7 +348,10 @@ PYBIND11_MODULE(_tkhip, m) {
       .def("set_coalesce", &MainDriver::set_coalesce, py::arg("n"))
       .def("set_coalesce_wait_us", &MainDriver::set_coalesce_wait_us, py::arg("us"))
       .def("enable_direct", &MainDriver::enable_direct)
-      .def("enable_mirror", &MainDriver::enable_mirror, py::arg("chunk_bytes"), py::arg("chunks_per_partition"))
+      .def("enable_mirror", &MainDriver::enable_mirror, py::arg("chunk_bytes"), py::arg("chunks_per_partition"),
+           py::arg("copy_streams") = 0)
+      .def_property_readonly("mirror_copy_streams",
+                             [](MainDriver& d) { return d.mirror_copy_streams(); })
       .def("set_ahead_depth", &MainDriver::set_ahead_depth)
       .def("set_span_burst", &MainDriver::set_span_burst)
       .def("set_group_bytes", &MainDriver::set_group_bytes)
@@ -362,6 +367,12 @@ PYBIND11_MODULE(_tkhip, m) {
       .def_property_readonly("direct", &MainDriver::direct)
       .def_property_readonly("coalesce", &MainDriver::coalesce)
       .def("enable_lockstep", &MainDriver::enable_lockstep, py::keep_alive<1, 2>())
+      .def("set_sync_commit", &MainDriver::set_sync_commit, py::arg("sync"))
+      .def("verify_delivered",
+           [](MainDriver& d) {
+             py::gil_scoped_release nogil;
+             return d.verify_delivered();
+           })
       .def("finish_lockstep",
            [](MainDriver& d) {
              py::gil_scoped_release nogil;

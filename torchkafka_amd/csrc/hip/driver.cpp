@@ -240,6 +240,7 @@ class MainDriver::Source : public tk::LockstepSource {
 void MainDriver::enable_lockstep(LockstepTransport* ls, int depth) {
   ls_ = std::make_unique<tk::CreditLockstep>(ls, depth);
   ls_->set_on_committable([this](std::vector<tk::Watermark>&& wms) { ledger_->batch_committable(wms); });
+  ls_->set_sync(sync_commit_);
   delivered_index_ = -1;
 }
 
@@ -268,7 +269,9 @@ void MainDriver::finish_lockstep() {
 
 int MainDriver::next_slot(int64_t timeout_ms, SlotView* out) {
   release_completed();
-  if (!fenced_.empty()) drain_fenced(false);
+  // sync commits under a lockstep: the previous batch enters the protocol's finished queue (its
+  // verdict landed) before the agreement that makes it committable on every rank is issued
+  if (!fenced_.empty()) drain_fenced(ls_ && sync_commit_);
   if (!parse_error_.empty()) return -4;
   if (ls_) return next_slot_lockstep(timeout_ms, out);
   auto& staged = poller_->staged();
@@ -1040,6 +1043,39 @@ void MainDriver::drain_fenced(bool wait) {
   }
 }
 
+int MainDriver::verify_delivered() {
+  const int64_t pe = delivered_perr_;
+  if (!parse_error_.empty()) return -4;
+  if (pe < 0) return 0;  // not device-checked: the worker verified it before publishing
+  if (verdicts_->state(pe) == 0) {
+    const int64_t t0 = tk::now_ns();
+    cover_handed();
+    for (;;) {
+      size_t i = 0;
+      while (i < handed_.size() && handed_[i].perr != pe) ++i;
+      if (i == handed_.size()) break;  // released: its verdict was read
+      size_t e = i;
+      while (e < handed_.size() && !handed_[e].ev) ++e;
+      if (e == handed_.size()) throw std::logic_error("driver: a delivered batch has no completion event");
+      // release is in hand-out order: every earlier launch (other decode streams too) must be done
+      for (size_t k = 0; k <= e; ++k)
+        if (handed_[k].ev) eng_->wait_slot(int(handed_[k].g));
+      pending_query_ns_ = 0;
+      release_completed_impl();
+    }
+    verify_wait_ns_ += tk::now_ns() - t0;
+  }
+  if (verdicts_->state(pe) == 2) {
+    drain_fenced(true);  // batches finished before this one stay committable (the reference commits
+                         // batch k-1 before the fetch of batch k fails its CRC check)
+    if (parse_error_.empty()) parse_error_ = verdicts_->failure(pe, delivered_);
+    delivered_.clear();  // never finished, never committed
+    delivered_perr_ = -1;
+    return -4;
+  }
+  return 0;
+}
+
 int MainDriver::commit_pending() {
   drain_fenced(false);
   const int status = ledger_->commit();
@@ -1059,6 +1095,7 @@ void MainDriver::reset_stats() {
   ahead_groups_ = ahead_ns_ = 0;
   verdicts_->width_wait_ns = 0;
   fast_batches_ = fast_records_ = fast_ns_ = 0;
+  verify_wait_ns_ = 0;
   if (ls_) ls_->reset_stats();
 }
 

@@ -177,8 +177,9 @@ class MainDriver {
   bool direct() const { return pins_->direct(); }
   // h2d='dma' with device decode: the decode kernels read the logs from an HBM mirror that the copy
   // engines fill chunk by chunk (log_mirror.h) instead of over PCIe from the pinned logs.
-  void enable_mirror(uint64_t chunk_bytes, int chunks_per_partition) {
-    pins_->enable_mirror(chunk_bytes, chunks_per_partition);
+  int mirror_copy_streams() const { return pins_->mirror() ? pins_->mirror()->copy_streams() : 0; }
+  void enable_mirror(uint64_t chunk_bytes, int chunks_per_partition, int copy_streams = 0) {
+    pins_->enable_mirror(chunk_bytes, chunks_per_partition, copy_streams);
   }
   const LogMirror* mirror() const { return pins_->mirror(); }
   uint64_t log_bytes_registered() const { return pins_->bytes_registered(); }
@@ -205,6 +206,17 @@ class MainDriver {
 
   // Cross-rank lockstep over RCCL, pipelined `depth` steps ahead (ls is owned by the caller).
   void enable_lockstep(LockstepTransport* ls, int depth);
+  // commit='sync': batch k+1 is taken only after batch k's verdict landed and (under a lockstep)
+  // an agreement at step k+1 made k committable on every rank (CreditLockstep sync mode).
+  void set_sync_commit(bool s) {
+    sync_commit_ = s;
+    if (ls_) ls_->set_sync(s);
+  }
+  // verify='deliver': waits for the device verdict (CRC32C / JSON grammar) of the batch just
+  // delivered.  0 clean or not device-checked; -4 corrupt (parse_error() says why: the batches
+  // finished before it were made committable first, it and what follows never are).
+  int verify_delivered();
+  int64_t verify_wait_ns_ = 0;  // host time verify_delivered() spent waiting for kernels
   // End of a lock-stepped iteration: barrier, then every finished batch becomes committable.
   void finish_lockstep();
   bool lockstep_enabled() const { return bool(ls_); }
@@ -372,6 +384,7 @@ class MainDriver {
   // Cross-rank lockstep: the credit protocol (csrc/core/lockstep.h) over the caller's transport.
   class Source;
   std::unique_ptr<tk::CreditLockstep> ls_;
+  bool sync_commit_ = false;
 
   Engine* eng_;
   bool registered_ = false;

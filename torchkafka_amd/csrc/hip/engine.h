@@ -88,6 +88,7 @@ class Engine {
   // The streams device-decode groups rotate over (created on first use; kDecodeStreams).
   hipStream_t decode_stream(int k);
   int decode_streams() const { return n_decode_; }
+  int copy_streams() const { return int(streams_.size()); }  // 0 in zero-copy mode
   // number of decode streams (1..4); only before the first decode stream is created
   void set_decode_streams(int n);
   // Creates the decode streams, uploads the CRC tables and runs an empty kernel on every decode

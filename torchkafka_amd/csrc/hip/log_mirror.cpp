@@ -15,7 +15,7 @@ namespace tkh {
     if (_e != hipSuccess) throw std::runtime_error(std::string("log mirror: ") + #expr + ": " + hipGetErrorString(_e)); \
   } while (0)
 
-LogMirror::LogMirror(int device, uint64_t chunk_bytes, int chunks_per_partition)
+LogMirror::LogMirror(int device, uint64_t chunk_bytes, int chunks_per_partition, int copy_streams)
     : device_(device), chunk_(chunk_bytes), K_(chunks_per_partition) {
   if (chunk_ < (uint64_t(1) << 20) || chunk_ % 4096 != 0) throw std::invalid_argument("log mirror: chunk must be >= 1 MiB, 4 KiB aligned");
   if (K_ < 2) throw std::invalid_argument("log mirror: at least 2 chunks per partition");
@@ -23,7 +23,7 @@ LogMirror::LogMirror(int device, uint64_t chunk_bytes, int chunks_per_partition)
   stride_ = (chunk_ + tk::kSpanSegMax + 256 + 4095) / 4096 * 4096;
   TKM_CHECK(hipSetDevice(device_));
   const char* e = std::getenv("TORCHKAFKA_MIRROR_COPY_STREAMS");
-  const int n = e ? std::atoi(e) : 2;
+  const int n = copy_streams > 0 ? copy_streams : e ? std::atoi(e) : 2;
   cs_.resize(size_t(n < 1 ? 1 : n > 4 ? 4 : n));
   for (auto& c : cs_) {
     TKM_CHECK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));

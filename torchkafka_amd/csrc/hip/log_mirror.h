@@ -31,8 +31,11 @@ class LogMirror {
   // The driver registers (pins) partition logs in pieces of this many bytes, at multiples of it
   // (MainDriver::kLogChunk): one copy never spans two registrations.
   static constexpr uint64_t kRegAlign = uint64_t(64) << 20;
-  LogMirror(int device, uint64_t chunk_bytes, int chunks_per_partition);
+  // copy_streams: SDMA copy streams (partitions split p % n); <= 0 takes
+  // TORCHKAFKA_MIRROR_COPY_STREAMS, else 2.  Each takes one of the process's hardware queues.
+  LogMirror(int device, uint64_t chunk_bytes, int chunks_per_partition, int copy_streams = 0);
   ~LogMirror();
+  int copy_streams() const { return int(cs_.size()); }
   LogMirror(const LogMirror&) = delete;
   LogMirror& operator=(const LogMirror&) = delete;
 

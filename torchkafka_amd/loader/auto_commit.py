@@ -84,6 +84,12 @@ def _auto_commit(dataloader, final_commit_timeout: float):
 
 
 def _multi_worker(dataloader: DataLoader, final_commit_timeout: float):
+    if dataloader.persistent_workers:
+        # persistent workers outlive this generator with the stamping collate_fn and this
+        # iteration's commit channel pickled into them: a later plain `for b in dataloader` would
+        # get stamped batches, and which worker made a batch would be unknowable for a new channel
+        raise RuntimeError("auto_commit does not support persistent_workers=True: its workers keep the "
+                           "commit channel of the iteration that started them")
     ds = dataloader.dataset
     bs = dataloader.batch_size or 1
     channel = CommitChannel(dataloader.num_workers, bs)
@@ -97,19 +103,8 @@ def _multi_worker(dataloader: DataLoader, final_commit_timeout: float):
         ds._commit_channel = previous
         dataloader.collate_fn = collate
     consumed = [0] * dataloader.num_workers
-    workers = getattr(batches, "_workers", [])
-
-    def alive(w):
-        return w < len(workers) and workers[w].is_alive()
-
     try:
-        for stamped in batches:
-            if not isinstance(stamped, _Stamped):
-                # persistent workers started by an earlier iter() without the stamp: which worker
-                # made a batch is unknown, and a wrong guess would commit unread records
-                raise RuntimeError("auto_commit: the DataLoader's workers were started outside auto_commit "
-                                   "(persistent_workers=True); iterate it through auto_commit from the start")
-            batch, w = stamped
+        for batch, w in batches:
             yield batch
             # batches, not samples: the worker maps its k-th batch to the consumer positions after
             # its samples, whatever shape the collate_fn gave the batch
@@ -117,12 +112,11 @@ def _multi_worker(dataloader: DataLoader, final_commit_timeout: float):
             channel.request(w, consumed[w])
         # normal end: make sure every worker committed its final batch before shutdown
         channel.close_requests()
-        if not channel.wait_acks(final_commit_timeout, alive):
+        if not channel.wait_acks(final_commit_timeout):  # liveness: the pids the workers registered
             log.warning("auto_commit: some workers did not acknowledge their final commit")
     finally:
         channel.close_requests()  # a worker waiting to serve a last request may exit now
-        try:
-            batches._shutdown_workers()  # type: ignore[attr-defined]
-        except Exception:  # noqa: BLE001
-            pass
+        # the last reference to the iterator: its finaliser joins (and if needed terminates) the
+        # workers -- the public teardown, the same as a user's loop ending
+        del batches
         channel.close()

@@ -17,7 +17,8 @@ from multiprocessing import shared_memory
 
 import numpy as np
 
-_REQ, _ACK, _HDR = 0, 1, 3
+_REQ, _ACK, _PID, _HDR = 0, 1, 2, 3
+_W = 3  # words per worker: request, acknowledgement, pid
 _CLOSING = 2  # header word: the main process will send no further requests
 
 
@@ -27,9 +28,9 @@ class CommitChannel:
             raise ValueError("commit channel needs num_workers >= 1 and batch_size >= 1")
         self.num_workers = num_workers
         self.batch_size = batch_size
-        self._shm = shared_memory.SharedMemory(create=True, size=8 * (_HDR + 2 * num_workers))
+        self._shm = shared_memory.SharedMemory(create=True, size=8 * (_HDR + _W * num_workers))
         self._owner = True
-        self._arr = np.ndarray((_HDR + 2 * num_workers,), dtype=np.int64, buffer=self._shm.buf)
+        self._arr = np.ndarray((_HDR + _W * num_workers,), dtype=np.int64, buffer=self._shm.buf)
         self._arr[:] = 0
         self._arr[0] = num_workers
         self._arr[1] = batch_size
@@ -49,10 +50,10 @@ class CommitChannel:
         except Exception:  # noqa: BLE001
             pass
         self._owner = False
-        self._arr = np.ndarray((_HDR + 2 * self.num_workers,), dtype=np.int64, buffer=self._shm.buf)
+        self._arr = np.ndarray((_HDR + _W * self.num_workers,), dtype=np.int64, buffer=self._shm.buf)
 
     def _i(self, w: int, which: int) -> int:
-        return _HDR + 2 * w + which
+        return _HDR + _W * w + which
 
     def request(self, worker: int, batches: int) -> None:
         self._arr[self._i(worker, _REQ)] = batches
@@ -66,6 +67,23 @@ class CommitChannel:
     def acked(self, worker: int) -> int:
         return int(self._arr[self._i(worker, _ACK)])
 
+    def register(self, worker: int, pid: int) -> None:
+        """A worker announces its process (liveness is read from here, not from the DataLoader)."""
+        self._arr[self._i(worker, _PID)] = pid
+
+    def alive(self, worker: int) -> bool:
+        """The worker registered and its process still runs (a zombie -- exited, not yet reaped by
+        the DataLoader -- counts as dead)."""
+        pid = int(self._arr[self._i(worker, _PID)])
+        if pid <= 0:
+            return False
+        try:
+            with open(f"/proc/{pid}/stat") as f:
+                state = f.read().rsplit(")", 1)[1].split()[0]
+        except (OSError, IndexError):
+            return False
+        return state not in ("Z", "X")
+
     def close_requests(self) -> None:
         """No more requests will come (end of iteration or the user broke out of the loop)."""
         self._arr[_CLOSING] = 1
@@ -74,7 +92,10 @@ class CommitChannel:
         return bool(self._arr[_CLOSING])
 
     def wait_acks(self, timeout: float = 5.0, alive=None) -> bool:
-        """Waits until every worker acknowledged its latest request; ``alive(w)`` can cut a dead worker short."""
+        """Waits until every worker acknowledged its latest request; a dead worker (``alive(w)``,
+        by default the channel's own pid registry) is not waited for."""
+        if alive is None:
+            alive = self.alive
         deadline = time.monotonic() + timeout
         while True:
             pending = [w for w in range(self.num_workers) if self.acked(w) < self.requested(w)

@@ -201,7 +201,10 @@ class _Run:
                 if L._direct() or L._device_decode():
                     self.driver.pin_logs(L._rank_partitions())
                 if L._mirror():
-                    self.driver.enable_mirror(int(L.tuning.mirror_chunk_mib) << 20, int(L.tuning.mirror_chunks))
+                    # under the RCCL lockstep one SDMA copy stream: the process's 4 hardware queues
+                    # go to the user's stream, two decode streams and the lockstep's RCCL stream
+                    mcs = 1 if L._lockstep_transport() == "rccl" else 0
+                    self.driver.enable_mirror(int(L.tuning.mirror_chunk_mib) << 20, int(L.tuning.mirror_chunks), mcs)
                 tun = L.tuning
                 if tun.ahead_depth is not None:
                     self.driver.set_ahead_depth(int(tun.ahead_depth))
@@ -354,7 +357,17 @@ class DeviceLoader:
             KafkaBridge replica that forwards them to the group coordinator within a few ms -- when
             batch k+1 is requested) or ``"sync"`` (the reference's semantics, kafka_dataset.py:130:
             batch k+1 is handed out only after batch k's device verdict landed, its offsets were
-            stored and, through a bridge, the coordinator answered its OffsetCommit).
+            stored and, through a bridge, the coordinator answered its OffsetCommit).  Under a
+            cross-rank lockstep the same holds on every rank: before batch k+1 is taken, one
+            agreement issued at step k+1 proves every rank finished batch k, and each rank commits
+            its own part of batch k before it hands out k+1 (one collective per step).
+        verify: ``"deliver"`` (a batch decoded or parsed on the GPU is handed out only once its
+            kernel's verdict -- every RecordBatch's CRC32C, every JSON row's grammar -- landed; a
+            corrupt batch raises ``CorruptRecordException`` before it is yielded, as kafka-python's
+            ``check_crcs`` iterator raises before ``_process`` sees a record) or ``"commit"`` (the
+            verdict gates only the commit: the batch may be yielded while its kernel still runs and
+            the exception comes one or more steps later).  Host-decoded batches are verified by the
+            workers before they are published, in both modes.
         lockstep: synchronise steps and commits across ranks when torch.distributed is initialised
             (``True``: native RCCL on GPUs with an nccl group, the group's own all-reduce otherwise;
             ``"host"``: the group's all-reduce (e.g. gloo) even on GPUs; ``"rccl"``: the native RCCL
@@ -427,6 +440,7 @@ class DeviceLoader:
         self.multiprocessing_context = cfg.multiprocessing_context
         self.commit_on = cfg.commit_on
         self.commit_mode = cfg.commit
+        self.verify = cfg.verify
         self.commit_sink = cfg.commit_sink
         self.lockstep = cfg.lockstep
         self.lockstep_timeout = float(cfg.lockstep_timeout)
@@ -859,6 +873,13 @@ class DeviceLoader:
             run.close()
             raise
         if run.driver is not None:
+            plan = self.stream_plan()
+            if self.lockstep_info:
+                self.lockstep_info["streams"] = plan
+            if plan["shared"]:
+                lvl = logging.WARNING if plan["rccl_lockstep"] else logging.DEBUG
+                log.log(lvl, "DeviceLoader: %d HIP streams on %d hardware queues (%s): some share a queue",
+                        plan["total"], plan["hw_queues"], plan)
             yield from self._iterate_native(run, auto_commit)
             return
         finished = self._pending_wms
@@ -952,8 +973,14 @@ class DeviceLoader:
         world = dist.get_world_size(process_group)
         uid = [hip().RcclLockstep.unique_id(lib) if rank == 0 else None]
         src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
-        via = self.device if dist.get_backend(process_group) == "nccl" else torch.device("cpu")
-        dist.broadcast_object_list(uid, src=src, group=process_group, device=via)
+        # the id travels over a CPU (gloo) group: broadcasting it over an nccl group would create
+        # torch's own RCCL communicator -- and its streams, which take hardware queues -- for one
+        # 128-byte message
+        via_group = process_group
+        if dist.get_backend(process_group) != "gloo":
+            ranks = None if process_group is None else dist.get_process_group_ranks(process_group)
+            via_group = dist.new_group(ranks=ranks, backend="gloo")  # collective: every rank gets here
+        dist.broadcast_object_list(uid, src=src, group=via_group, device=torch.device("cpu"))
         dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
         ls = hip().RcclLockstep(lib, uid[0], rank, world, dev, self.lockstep_depth + 2)
         ls.set_timeout_ms(int(self.lockstep_timeout * 1000))
@@ -967,6 +994,32 @@ class DeviceLoader:
         self.lockstep_info = {"transport": "rccl", "rccl_nranks": nranks, "rank_id_sum": rank_sum,
                               "world_size": world}
         return ls
+
+    def stream_plan(self) -> dict:
+        """The HIP streams the live iteration uses, against the process's hardware queues
+        (``GPU_MAX_HW_QUEUES``, 4 by default).  HIP binds streams to queues round-robin in creation
+        order, so past that count two streams share a queue and a launch on one can wait behind
+        the other's (e.g. a decode kernel behind a collective waiting for the other ranks)."""
+        run = self._run
+        plan = {"user": 1, "decode": 0, "copy": 0, "mirror_copy": 0, "rccl_lockstep": 0, "torch_nccl": 0}
+        if run is not None and run.engine is not None:
+            plan["decode"] = int(run.engine.decode_streams()) if self._device_decode() else 0
+            plan["copy"] = int(run.engine.copy_streams())
+            if run.driver is not None:
+                plan["mirror_copy"] = int(run.driver.mirror_copy_streams)
+        if run is not None and run.rccl is not None and self.lockstep_info.get("transport") == "rccl":
+            plan["rccl_lockstep"] = 1
+        try:
+            import torch.distributed as dist
+
+            if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+                plan["torch_nccl"] = 1
+        except Exception:  # noqa: BLE001
+            pass
+        total = sum(plan.values())
+        hw = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+        plan.update(total=total, hw_queues=hw, shared=total > hw)
+        return plan
 
     # ------------------------------------------------------------------ native iteration
     def _iterate_native(self, run: _Run, auto_commit: bool):
@@ -995,6 +1048,8 @@ class DeviceLoader:
         if _roctx_enabled():
             step = _traced_step(step)
         sync = auto_commit and self.commit_mode == "sync"
+        drv.set_sync_commit(sync)
+        verify = self.verify == "deliver"
         completed = delivered = False
         wait_since = None
         try:
@@ -1003,6 +1058,13 @@ class DeviceLoader:
                 if cs:
                     self._log_commit(cs, debug)
                 if r > 0:
+                    if verify and drv.verify_delivered() < 0:
+                        # the batch's CRC32C / grammar verdict is bad: it never reaches the user (the
+                        # reference's records pass kafka-python's check_crcs before _process sees them,
+                        # kafka_dataset.py:156-162); the batches finished before it are committed first
+                        if auto_commit and delivered:
+                            self._commit_native(drv, debug)
+                        raise CorruptRecordException(drv.parse_error())
                     if delivered:
                         if log_commits and not py_commits:
                             self._commit_logged(drv)
@@ -1170,6 +1232,7 @@ class DeviceLoader:
         self.stats.mirror_bytes += st.get("mirror_bytes_copied", 0)
         self.stats.mirror_copies += st.get("mirror_copies", 0)
         self.stats.mirror_fallbacks += st.get("mirror_fallbacks", 0)
+        self.stats.verify_wait_ns += st.get("verify_wait_ns", 0)
         self.stats.lockstep_agreements += st.get("lockstep_agreements", 0)
         self.stats.lockstep_wait_ns += st.get("lockstep_wait_ns", 0)
         self.stats.lockstep_step_wait_max_ns = max(self.stats.lockstep_step_wait_max_ns,

@@ -254,6 +254,7 @@ class KafkaDataset(IterableDataset):
         if ch is None:
             yield from self._records(in_worker)
             return
+        ch.register(self._worker_id, os.getpid())  # auto_commit reads the workers' liveness here
         if getattr(self, "_consumer_lock", None) is None:
             self._consumer_lock = threading.Lock()
             self._channel_lock = threading.Lock()

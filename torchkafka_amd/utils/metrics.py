@@ -62,6 +62,7 @@ class LoaderStats:
     mirror_fallbacks: int = 0  # segments read from the pinned log instead (buffer busy)
     lockstep_agreements: int = 0      # cross-rank agreements (collectives) issued
     lockstep_wait_ns: int = 0         # host time waiting for agreement results
+    verify_wait_ns: int = 0           # verify='deliver': host time waiting for a batch's device verdict
     lockstep_step_wait_max_ns: int = 0  # the most one delivered step waited for them
     started: float = field(default_factory=time.perf_counter)
     max_commit_samples: int = 100000
@@ -126,6 +127,7 @@ class LoaderStats:
             "mirror_fallbacks": self.mirror_fallbacks,
             "lockstep_agreements": self.lockstep_agreements,
             "lockstep_wait_us_per_batch": self.lockstep_wait_ns / 1e3 / max(self.batches, 1),
+            "verify_wait_us_per_batch": self.verify_wait_ns / 1e3 / max(self.batches, 1),
             "lockstep_step_wait_max_us": self.lockstep_step_wait_max_ns / 1e3,
             "commits": self.commits,
             "commit_failures": self.commit_failures,

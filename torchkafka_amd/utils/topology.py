@@ -90,6 +90,56 @@ def visible_gpus() -> list[dict]:
     return _apply_visible(devs, hip, False)
 
 
+def count_gpus_without_hip() -> dict:
+    """How many GPUs this process could use, found without any HIP call (a launcher must not
+    initialise HIP before it starts its rank processes): the KFD topology filtered by the
+    visibility variables (:func:`visible_gpus`), cross-checked against amdsmi when torch can reach
+    it (``torch.cuda._device_count_amdsmi`` -- it never falls back to ``hipGetDeviceCount``).
+    ``{"count": n, "sysfs": n_sysfs, "amdsmi": n_smi or None}``; raises RuntimeError when neither
+    source answers (the caller refuses to launch rather than guess)."""
+    n_sys = len(visible_gpus())
+    n_smi = None
+    try:
+        import torch
+
+        fn = getattr(torch.cuda, "_device_count_amdsmi", None)
+        if fn is not None and torch.version.hip:
+            v = int(fn())
+            n_smi = v if v >= 0 else None
+    except Exception:  # noqa: BLE001 - amdsmi absent or broken: sysfs decides
+        n_smi = None
+    if n_sys > 0:
+        count = n_sys if n_smi is None else min(n_sys, n_smi)
+    elif n_smi is not None:
+        count = n_smi
+    else:
+        raise RuntimeError("cannot count GPUs without initialising HIP: no KFD GPU nodes in sysfs and amdsmi "
+                           "is unavailable")
+    return {"count": count, "sysfs": n_sys, "amdsmi": n_smi}
+
+
+def hip_touched() -> dict:
+    """Whether this process has initialised HIP (torch's lazy init) or holds an open /dev/kfd."""
+    kfd = 0
+    try:
+        for fd in os.listdir("/proc/self/fd"):
+            try:
+                if os.readlink(f"/proc/self/fd/{fd}") == "/dev/kfd":
+                    kfd += 1
+            except OSError:
+                continue
+    except OSError:
+        pass
+    init = False
+    try:
+        import torch
+
+        init = bool(torch.cuda.is_initialized())
+    except Exception:  # noqa: BLE001
+        pass
+    return {"torch_cuda_initialized": init, "kfd_fds": kfd}
+
+
 def _bdf(props: dict) -> str | None:
     try:
         loc, dom = int(props["location_id"]), int(props.get("domain", "0") or 0)
