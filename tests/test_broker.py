@@ -110,6 +110,13 @@ def test_group_range_assignment_and_rebalance(broker):
     assert active and state == 2 and asg == [0, 1, 2, 3, 4]
     s2 = b.join_group(g, [ti], 10000, 300000)
     m2 = b.member_id(g, s2)
+    # Kafka's PreparingRebalance: the first member must rejoin before anything is reassigned, and
+    # may still commit with its current generation until it does
+    g_prep, st_prep, active, asg_prep = b.poll_group(g, s1, m1)
+    assert (g_prep, st_prep, active, asg_prep) == (gen1, 1, True, [])
+    b.commit(g, s1, m1, gen1, [(4, 3, "")])
+    assert b.committed(g, 4) == (3, "")
+    b.rejoin_group(g, s1, m1)
     gen2, _, _, asg1 = b.poll_group(g, s1, m1)
     _, _, _, asg2 = b.poll_group(g, s2, m2)
     assert gen2 == gen1 + 1
@@ -122,7 +129,9 @@ def test_group_range_assignment_and_rebalance(broker):
     # a non-member commit is rejected while the group has members
     with pytest.raises(CommitFailedError):
         b.commit(g, -1, 0, 0, [(0, 2, "")])
-    b.leave_group(g, s2, m2)
+    b.leave_group(g, s2, m2)  # a member leaves: the one left rejoins, then takes everything
+    assert b.poll_group(g, s1, m1)[1] == 1
+    b.rejoin_group(g, s1, m1)
     gen3, _, _, asg1 = b.poll_group(g, s1, m1)
     assert gen3 == gen2 + 1 and asg1 == [0, 1, 2, 3, 4]
 

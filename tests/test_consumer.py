@@ -157,17 +157,27 @@ def test_group_members_split_partitions(broker):
 
 
 def test_stale_generation_commit_fails(broker):
+    """Kafka's rebalance round: a joining member waits for the others to rejoin; until c1 does, its
+    current-generation commit is accepted; once the round completed without it (its rebalance
+    timeout, max_poll_interval_ms, expired) its commit is rejected and it rejoins as a new member."""
+    import threading
+
     broker.create_topic("t", 2)
-    c1 = consumer(broker, "t", group_id="g", enable_auto_commit=False)
+    c1 = consumer(broker, "t", group_id="g", enable_auto_commit=False, max_poll_interval_ms=400)
     c1.assignment()
     time.sleep(0.35)
-    c1.assignment()
+    assert len(c1.assignment()) == 2
     c2 = consumer(broker, "t", group_id="g")
-    c2.assignment()  # joins: rebalance, c1's generation is now stale
+    done = threading.Event()
+    th = threading.Thread(target=lambda: (c2.assignment(), done.set()))
+    th.start()  # joins: blocks until every member rejoined (or c1's rebalance timeout)
+    time.sleep(0.05)
+    assert not done.is_set()
+    c1.commit()  # the group is preparing a rebalance: c1's generation is still current
+    th.join(timeout=10)  # c1 never rejoined: dropped at its rebalance timeout, c2 gets everything
+    assert done.is_set() and len(c2.assignment()) == 2
     with pytest.raises(CommitFailedError):
         c1.commit()
-    c1.assignment()  # c1 follows the new generation
-    c1.commit()
 
 
 def test_max_poll_interval_exceeded(broker):

@@ -15,7 +15,7 @@ __version__ = "1.2.0+mi355x.5"
 
 __all__ = ["KafkaDataset", "auto_commit", "DeviceLoader", "KafkaBatch", "LoaderConfig", "Tuning", "FixedWidth",
            "VarLen", "JsonArray", "Key", "Timestamp", "WithFields", "SyntheticBroker", "KafkaBridge", "KafkaWireServer",
-           "KafkaConsumer", "KafkaProducer", "TopicPartition"]
+           "KafkaConsumer", "KafkaProducer", "TopicPartition", "ConsumerRebalanceListener"]
 
 
 def __getattr__(name):
@@ -27,7 +27,7 @@ def __getattr__(name):
         from .client.records import TopicPartition
 
         return TopicPartition
-    if name in ("KafkaConsumer", "KafkaProducer"):
+    if name in ("KafkaConsumer", "KafkaProducer", "ConsumerRebalanceListener"):
         from . import client
 
         return getattr(client, name)

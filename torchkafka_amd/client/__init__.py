@@ -1,5 +1,5 @@
 """kafka-python compatible client over the synthetic broker."""
-from .consumer import KafkaConsumer
+from .consumer import ConsumerRebalanceListener, KafkaConsumer
 from .errors import (
     CommitFailedError, CorruptRecordException, KafkaConfigurationError, KafkaError, NoBrokersAvailable,
     OffsetOutOfRangeError,
@@ -7,7 +7,8 @@ from .errors import (
 from .producer import KafkaProducer
 from .records import ConsumerRecord, OffsetAndMetadata, OffsetAndTimestamp, RecordMetadata, TopicPartition
 
-__all__ = ["KafkaConsumer", "KafkaProducer", "ConsumerRecord", "TopicPartition", "OffsetAndMetadata",
+__all__ = ["KafkaConsumer", "ConsumerRebalanceListener",
+           "KafkaProducer", "ConsumerRecord", "TopicPartition", "OffsetAndMetadata",
            "OffsetAndTimestamp",
            "RecordMetadata", "KafkaError", "CommitFailedError", "CorruptRecordException", "NoBrokersAvailable",
            "OffsetOutOfRangeError", "KafkaConfigurationError"]

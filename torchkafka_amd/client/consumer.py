@@ -12,12 +12,16 @@ Additions for the framework (not in kafka-python):
   * ``_fetcher``: the native fetch/decode core used by the loader fast path;
   * ``_idle_hooks``: callbacks run while iteration waits for records, so a
     worker can apply commit requests on idle partitions (fixes reference D8);
+  * ``_revoke_hooks``: callbacks run when the group takes this member's partitions away, before
+    the user's ``ConsumerRebalanceListener.on_partitions_revoked`` -- the loaders commit what the
+    user finished there, so the listener sees those offsets committed;
   * ``assign_shard``: deterministic rank/worker partition sharding (N3);
   * fork detection: using a consumer in a process other than the one that
     created it raises instead of silently sharing state (reference D7).
 """
 from __future__ import annotations
 
+import abc
 import copy
 import itertools
 import logging
@@ -38,6 +42,23 @@ from .records import ConsumerRecord, OffsetAndMetadata, OffsetAndTimestamp, Topi
 
 _getpid = os.getpid
 log = logging.getLogger(__name__)
+
+
+class ConsumerRebalanceListener(abc.ABC):
+    """kafka-python's rebalance callback interface (``kafka.ConsumerRebalanceListener``), passed to
+    :meth:`KafkaConsumer.subscribe`.  Eager semantics, as kafka-python 2.0.2: before every
+    (re)join the member gives up its whole assignment -- ``on_partitions_revoked`` with it (an
+    empty set before the first join) -- and ``on_partitions_assigned`` receives the complete new
+    assignment once the group is stable again.  Both run in the thread that polls the consumer;
+    an exception they raise is logged, not propagated (kafka-python's coordinator does the same)."""
+
+    @abc.abstractmethod
+    def on_partitions_revoked(self, revoked):
+        """``revoked``: set of TopicPartition this member owned until now."""
+
+    @abc.abstractmethod
+    def on_partitions_assigned(self, assigned):
+        """``assigned``: set of TopicPartition this member owns from now on."""
 
 _GROUP_STABLE = 2
 
@@ -155,6 +176,10 @@ class KafkaConsumer:
         self._tp_cache: dict[int, TopicPartition] = {}
         self._position: dict[int, int] = {}
         self._idle_hooks: list[Callable[[], None]] = []
+        self._revoke_hooks: list[Callable[[], None]] = []
+        self._listener: ConsumerRebalanceListener | None = None
+        self._revoked = False  # the current assignment was already given up (revoke callbacks ran)
+        self._rejoining = False  # rejoined a rebalance round: hand nothing out until it completes
         self._iter_deadline = None
         self._last_auto_commit = time.monotonic()
         # group membership (subscription mode)
@@ -211,6 +236,46 @@ class KafkaConsumer:
                     return off
         return self._reset_position(pidx)
 
+    def _call_listener(self, which: str, pidxs) -> None:
+        if self._listener is None:
+            return
+        tps = {self._tp(p) for p in pidxs}
+        try:
+            getattr(self._listener, which)(tps)
+        except Exception:  # noqa: BLE001 - kafka-python logs a failing user listener and carries on
+            what = "revocation" if which == "on_partitions_revoked" else "assignment"
+            log.exception("User provided listener %s for group %s failed on partition %s", self._listener,
+                          self.config["group_id"], what)
+
+    def _revoke(self, owned=None) -> None:
+        """This member is about to (re)join: what the user finished is committed (the loaders'
+        ``_revoke_hooks``), then the listener is told the whole assignment is gone (eager
+        protocol, kafka-python's ``_on_join_prepare``).  Once per rebalance."""
+        if self._revoked:
+            return
+        self._revoked = True
+        owned = self._assignment if owned is None else owned
+        for hook in list(self._revoke_hooks):
+            try:
+                hook()
+            except Exception:  # noqa: BLE001 - a failed commit is logged, as any other (B14)
+                log.exception("commit before partition revocation failed")
+        self._call_listener("on_partitions_revoked", owned)
+
+    def _assigned(self, pidxs) -> None:
+        self._revoked = False
+        self._call_listener("on_partitions_assigned", pidxs)
+
+    def _group_tick(self) -> None:
+        """Group maintenance without waiting (a loader's background thread, while the consumer is
+        otherwise idle): answers a rebalance round -- commit hooks, revoke callback, rejoin -- and
+        takes the new assignment once the group is stable.  kafka-python leaves this to poll();
+        a DataLoader worker parked on its index queue would then stall the whole group until the
+        rebalance timeout."""
+        if self._closed or self._manual or not self._subscription or self._g is None or self._pid != _getpid():
+            return
+        self._ensure_group(block=False)
+
     def _set_assignment(self, pidxs: Iterable[int]) -> None:
         pidxs = sorted(set(pidxs))
         old = self._fetcher.positions()
@@ -240,6 +305,7 @@ class KafkaConsumer:
                 self._set_assignment(pidxs)
             return
         if self._member_slot < 0:
+            self._revoke()  # kafka-python calls it before every join, the first one included
             topics = [self._broker.topic(t)[0] for t in sorted(self._subscription)]
             self._member_slot = self._b.join_group(self._g, topics, int(self.config["session_timeout_ms"]),
                                                    int(self.config["max_poll_interval_ms"]))
@@ -247,6 +313,7 @@ class KafkaConsumer:
         gen, state, active, assignment = self._b.poll_group(self._g, self._member_slot, self._member_id)
         if not active:
             # evicted (max_poll_interval exceeded or broker decided): rejoin
+            self._revoke()
             self._member_slot = -1
             self._assignment = []
             self._fetcher.assign([], [])
@@ -254,8 +321,13 @@ class KafkaConsumer:
             self._position = {}
             return self._ensure_group()
         if state != _GROUP_STABLE:
-            if self._assignment:
-                self._set_assignment([])
+            self._revoke()  # a rebalance is under way: give the partitions up (commits first)
+            # rejoin: the coordinator reassigns once every member did (or at the rebalance timeout).
+            # Nothing more is handed out until then (_rejoining); the fetch positions stay, so a
+            # partition the next generation gives back to this member resumes where it was -- it
+            # had no other owner in between -- and others start at the group's committed offset.
+            self._b.rejoin_group(self._g, self._member_slot, self._member_id)
+            self._rejoining = True
             # kafka-python joins the group synchronously (ensure_active_group blocks):
             # wait out the initial rebalance delay instead of returning an empty assignment
             if not block:
@@ -263,16 +335,21 @@ class KafkaConsumer:
             deadline = time.monotonic() + 60.0
             while state != _GROUP_STABLE and time.monotonic() < deadline:
                 time.sleep(0.005)
+                # idempotent; also answers a round that started while this member waited
+                self._b.rejoin_group(self._g, self._member_slot, self._member_id)
                 gen, state, active, assignment = self._b.poll_group(self._g, self._member_slot, self._member_id)
                 if not active:
                     return self._ensure_group()
             if state != _GROUP_STABLE:
                 return
         if gen != self._generation:
-            self._generation = gen
+            self._revoke()  # the rebalance completed between two polls: revoke before the new assignment
+            prev, self._generation = self._generation, gen
             old = set(self._assignment)
-            # revoked partitions restart from committed offsets when re-acquired
-            keep_positions = {p: pos for p, pos in self._fetcher.positions().items() if p in assignment}
+            # revoked partitions restart from committed offsets when re-acquired; one this member
+            # keeps into the very next generation had no other owner: it resumes where it was
+            keep_positions = ({p: pos for p, pos in self._fetcher.positions().items() if p in assignment}
+                              if gen == prev + 1 else {})
             pidxs = sorted(assignment)
             positions = [keep_positions[p] if p in keep_positions else self._initial_position(p) for p in pidxs]
             self._fetcher.assign(pidxs, positions)
@@ -284,6 +361,8 @@ class KafkaConsumer:
             if set(pidxs) != old:
                 log.debug("group %s generation %d assignment %s", self.config["group_id"], gen,
                           [self._tp(p) for p in pidxs])
+            self._rejoining = False
+            self._assigned(pidxs)
 
     def _fetch_into_buffer(self, max_records: int) -> int:
         tps = self._tp_cache
@@ -328,6 +407,9 @@ class KafkaConsumer:
         self._check_open()
         if self._manual:
             raise IllegalStateError("Subscription to topics, partitions and pattern are mutually exclusive")
+        if listener is not None and not isinstance(listener, ConsumerRebalanceListener):
+            raise TypeError("listener must be a ConsumerRebalanceListener")
+        self._listener = listener
         if pattern is not None:
             import re
 
@@ -504,7 +586,7 @@ class KafkaConsumer:
     def __next__(self) -> ConsumerRecord:
         """Blocks for the next record; StopIteration after ``consumer_timeout_ms`` without one."""
         buf = self._buffer
-        if buf and not self._closed and self._pid == _getpid():
+        if buf and not self._rejoining and not self._closed and self._pid == _getpid():
             pidx, r = buf.popleft()  # hot path: one record from the fetched buffer
             self._position[pidx] = r[2] + 1
             return r
@@ -513,7 +595,9 @@ class KafkaConsumer:
         deadline = None if timeout == float("inf") else time.monotonic() + timeout / 1000.0
         backoff = 0.0002
         while True:
-            if self._buffer:
+            if self._rejoining:
+                self._ensure_group()  # a rebalance round this member rejoined from a background tick
+            if self._buffer and not self._rejoining:
                 pidx, r = self._buffer.popleft()
                 return self._make_record(pidx, r)
             self._ensure_group()

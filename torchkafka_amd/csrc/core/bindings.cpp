@@ -472,6 +472,7 @@ PYBIND11_MODULE(_tkcore, m) {
       .def("group_name", &Broker::group_name)
       .def("join_group", &Broker::join_group)
       .def("leave_group", &Broker::leave_group)
+      .def("rejoin_group", &Broker::rejoin_group)
       .def("member_id", &Broker::member_id)
       .def("poll_group",
            [](Broker& b, uint32_t g, int slot, uint64_t mid) {

@@ -775,6 +775,7 @@ uint32_t Broker::group_index(const std::string& name, bool create) {
   G.generation.store(0);
   G.state.store(kGroupEmpty);
   G.next_member_id = 0;
+  G.awaiting.store(0);
   for (auto& m : G.members) m.active.store(0);
   meta_->n_groups.store(n + 1, std::memory_order_release);
   return n;
@@ -833,6 +834,7 @@ void Broker::rebalance_locked(GroupEntry& G, uint32_t g, int64_t now, bool immed
     std::fill(own, own + meta_->max_partitions, int16_t(-1));
     G.generation.fetch_add(1);
     G.state.store(kGroupEmpty);
+    G.awaiting.store(0);
     return;
   }
   const uint32_t st = G.state.load();
@@ -843,8 +845,60 @@ void Broker::rebalance_locked(GroupEntry& G, uint32_t g, int64_t now, bool immed
   }
   if (st == kGroupPreparing && !immediate && now < G.prepare_deadline_ns) return;
   assign_locked(G, g);
+  G.awaiting.store(0);
   G.generation.fetch_add(1);
   G.state.store(kGroupStable, std::memory_order_release);
+}
+
+void Broker::membership_changed_locked(GroupEntry& G, uint32_t g, int64_t now) {
+  int active = 0;
+  int64_t timeout = 0;
+  for (auto& M : G.members)
+    if (M.active.load()) {
+      ++active;
+      timeout = std::max(timeout, M.max_poll_interval_ns);
+    }
+  const uint32_t st = G.state.load();
+  if (active == 0 || st == kGroupEmpty || (st == kGroupPreparing && !G.awaiting.load())) {
+    // nobody left, or a group forming: the initial rebalance delay lets its first members join
+    // one round together (group.initial.rebalance.delay.ms)
+    rebalance_locked(G, g, now, active == 0);
+    return;
+  }
+  if (st == kGroupStable) {
+    // Kafka's PreparingRebalance: the members keep their partitions (and may commit them) until
+    // they rejoin; the rebalance timeout is the members' largest max.poll.interval.ms
+    for (auto& M : G.members) M.rejoined.store(0);
+    G.prepare_deadline_ns = now + timeout;
+    G.awaiting.store(1);
+    G.state.store(kGroupPreparing, std::memory_order_release);
+  }
+  try_complete_round_locked(G, g, now);
+}
+
+void Broker::try_complete_round_locked(GroupEntry& G, uint32_t g, int64_t now) {
+  if (G.state.load() != kGroupPreparing || !G.awaiting.load()) return;
+  bool all = true;
+  for (auto& M : G.members)
+    if (M.active.load() && !M.rejoined.load()) all = false;
+  if (!all) {
+    if (now < G.prepare_deadline_ns) return;
+    for (auto& M : G.members)  // the absentees are dropped from the group, as Kafka does
+      if (M.active.load() && !M.rejoined.load()) M.active.store(0);
+  }
+  rebalance_locked(G, g, now, true);
+}
+
+void Broker::rejoin_group(uint32_t g, int slot, uint64_t mid) {
+  GroupEntry& G = group(g);
+  RobustLock l(&meta_->lock);
+  MemberEntry& M = G.members[slot];
+  if (!M.active.load() || M.member_id != mid) return;
+  const int64_t now = now_ns();
+  M.last_poll_ns.store(now);
+  if (G.state.load() != kGroupPreparing || !G.awaiting.load()) return;
+  M.rejoined.store(1);
+  try_complete_round_locked(G, g, now);
 }
 
 int Broker::join_group(uint32_t g, const std::vector<uint32_t>& topic_indices, int64_t session_timeout_ms,
@@ -867,7 +921,9 @@ int Broker::join_group(uint32_t g, const std::vector<uint32_t>& topic_indices, i
   M.n_topics = uint32_t(topic_indices.size());
   for (size_t i = 0; i < topic_indices.size(); ++i) M.topics[i] = topic_indices[i];
   M.active.store(1, std::memory_order_release);
-  rebalance_locked(G, g, now, false);
+  membership_changed_locked(G, g, now);
+  M.rejoined.store(1);  // a new member is part of the round its join started
+  try_complete_round_locked(G, g, now);
   return slot;
 }
 
@@ -877,7 +933,7 @@ void Broker::leave_group(uint32_t g, int slot, uint64_t mid) {
   MemberEntry& M = G.members[slot];
   if (!M.active.load() || M.member_id != mid) return;
   M.active.store(0);
-  rebalance_locked(G, g, now_ns(), true);
+  membership_changed_locked(G, g, now_ns());
 }
 
 GroupView Broker::poll_group(uint32_t g, int slot, uint64_t mid) {
@@ -888,8 +944,13 @@ GroupView Broker::poll_group(uint32_t g, int slot, uint64_t mid) {
   if (M.active.load() && M.member_id == mid) M.last_poll_ns.store(now);
   RobustLock l(&meta_->lock);
   if (now - G.last_expiry_check_ns.load() > 50000000LL && expire_members_locked(G, now))
-    rebalance_locked(G, g, now, true);
-  if (G.state.load() == kGroupPreparing && now >= G.prepare_deadline_ns) rebalance_locked(G, g, now, false);
+    membership_changed_locked(G, g, now);
+  if (G.state.load() == kGroupPreparing && now >= G.prepare_deadline_ns) {
+    if (G.awaiting.load())
+      try_complete_round_locked(G, g, now);
+    else
+      rebalance_locked(G, g, now, false);
+  }
   v.member_active = M.active.load() && M.member_id == mid;
   v.generation = G.generation.load();
   v.state = G.state.load();
@@ -917,10 +978,14 @@ void Broker::commit(uint32_t g, int slot, uint64_t mid, uint32_t generation, con
     const int64_t now = now_ns();
     if (now - M.last_poll_ns.load() > M.max_poll_interval_ns) {
       M.active.store(0);
-      rebalance_locked(G, g, now, true);
+      membership_changed_locked(G, g, now);
       throw CommitFailed("CommitFailedError: time between polls exceeded max_poll_interval_ms");
     }
-    if (G.state.load() != kGroupStable || G.generation.load() != generation)
+    // Kafka accepts a current-generation commit during PreparingRebalance (a member commits what
+    // it finished before it rejoins -- kafka-python's _on_join_prepare), not once reassigned
+    const uint32_t st = G.state.load();
+    const bool open = st == kGroupStable || (st == kGroupPreparing && G.awaiting.load());
+    if (!open || G.generation.load() != generation)
       throw CommitFailed("CommitFailedError: the group has rebalanced (generation " +
                          std::to_string(G.generation.load()) + ", member had " + std::to_string(generation) + ")");
   } else if (G.state.load(std::memory_order_acquire) != kGroupEmpty) {

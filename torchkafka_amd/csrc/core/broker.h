@@ -117,6 +117,9 @@ struct alignas(64) MemberEntry {
   uint64_t member_id;
   uint32_t n_topics;
   uint32_t topics[kMaxSubscribedTopics];
+  // a rebalance round of a group that had members (GroupEntry::awaiting): this member rejoined
+  // (committed what it finished and gave its partitions up) -- in the struct's tail padding
+  std::atomic<uint32_t> rejoined;
 };
 
 enum GroupState : uint32_t { kGroupEmpty = 0, kGroupPreparing = 1, kGroupStable = 2 };
@@ -128,7 +131,11 @@ struct alignas(64) GroupEntry {
   int64_t prepare_deadline_ns;
   uint64_t next_member_id;
   std::atomic<int32_t> inject_commit_failures;
-  std::atomic<int32_t> pad;
+  // Preparing because the membership of a group with members changed: every member must rejoin
+  // (Kafka's PreparingRebalance; commits of the current generation are still accepted) before the
+  // partitions are reassigned, or be dropped at prepare_deadline_ns (the rebalance timeout).
+  // 0: Preparing is the initial delay of an empty group.
+  std::atomic<int32_t> awaiting;
   std::atomic<uint64_t> n_commits;
   std::atomic<int64_t> last_expiry_check_ns;
   MemberEntry members[kMaxMembers];
@@ -247,6 +254,9 @@ class Broker {
   int join_group(uint32_t g, const std::vector<uint32_t>& topic_indices, int64_t session_timeout_ms,
                  int64_t max_poll_interval_ms);
   void leave_group(uint32_t g, int member_slot, uint64_t member_id);
+  // During a rejoin round (poll_group reports Preparing): this member committed what it finished
+  // and gave its partitions up.  No-op outside a round.
+  void rejoin_group(uint32_t g, int member_slot, uint64_t member_id);
   uint64_t member_id(uint32_t g, int slot) const;
   GroupView poll_group(uint32_t g, int member_slot, uint64_t member_id);
   // member_slot < 0: manual-assignment ("simple") consumer.
@@ -273,6 +283,11 @@ class Broker {
   int16_t* owners(uint32_t g) const;
   OffsetEntry& offset_entry(uint32_t g, uint32_t pidx) const;
   void rebalance_locked(GroupEntry& G, uint32_t g, int64_t now, bool immediate);
+  // The membership of a group with members changed: start a rejoin round (or, with nobody left
+  // to wait for, reassign now).
+  void membership_changed_locked(GroupEntry& G, uint32_t g, int64_t now);
+  // A rejoin round ends once every active member rejoined, or at its deadline (absentees dropped).
+  void try_complete_round_locked(GroupEntry& G, uint32_t g, int64_t now);
   void assign_locked(GroupEntry& G, uint32_t g);
   bool expire_members_locked(GroupEntry& G, int64_t now);
 

@@ -94,6 +94,11 @@ def worker_main(ring, ring_name: str, worker_id: int, num_workers: int, dataset,
             consumer.assign_shard(topics, cfg["rank"], cfg["world_size"], worker_id, num_workers)
         sink = _WorkerSink(cfg.get("commit_table"), worker_id, dataset, consumer, cfg.get("commit_mode") == "sync")
         state["sink"] = sink
+        hooks = getattr(consumer, "_revoke_hooks", None)
+        if hooks is not None and sink.table is not None:
+            # a rebalance takes partitions away: what the user finished is committed first, then the
+            # user's ConsumerRebalanceListener hears of the revocation
+            hooks.append(sink.serve_once)
         if (cfg["native"] and getattr(consumer, "_fetcher", None) is not None and dataset.schema is not None
                 and not cfg.get("process_overridden", False)):
             sink.start_thread()

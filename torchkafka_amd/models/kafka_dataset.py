@@ -31,7 +31,7 @@ from collections import deque
 from torch.utils.data import IterableDataset, get_worker_info
 
 from ..client.consumer import KafkaConsumer
-from ..client.errors import COMMIT_FAILED_ERRORS, KafkaError, NoBrokersAvailable
+from ..client.errors import COMMIT_FAILED_ERRORS, IllegalStateError, KafkaError, NoBrokersAvailable
 from ..client.records import OffsetAndMetadata, TopicPartition
 
 _logger = logging.getLogger("torchkafka.kafka_dataset")
@@ -195,6 +195,9 @@ class KafkaDataset(IterableDataset):
                 if self._consumer_lock.acquire(blocking=False):
                     try:
                         self._service_channel()
+                        tick = getattr(self._consumer, "_group_tick", None)
+                        if tick is not None:
+                            tick()  # the generator is suspended: keep the group moving for it
                     except Exception:  # noqa: BLE001 - keep serving; the error is logged
                         _logger.exception("commit request failed on worker %s", self._worker_id)
                     finally:
@@ -265,6 +268,9 @@ class KafkaDataset(IterableDataset):
         hooks = getattr(self._consumer, "_idle_hooks", None)
         if hooks is not None and self._service_channel not in hooks:
             hooks.append(self._service_channel)
+        hooks = getattr(self._consumer, "_revoke_hooks", None)
+        if hooks is not None and self._service_channel not in hooks:
+            hooks.append(self._service_channel)  # commit the user's finished batches before a revocation
         self._start_committer()
         cl = self._consumer_lock
         bs = ch.batch_size
@@ -493,10 +499,33 @@ class _BridgedConsumer(KafkaConsumer):
     def _bridges_epoch(self) -> int:
         return sum(br.assignment_epoch for br in self._bridges)
 
+    def subscribe(self, topics=(), pattern=None, listener=None) -> None:
+        """Group-managed: the bridges hold the membership for the topics this consumer was built
+        with; re-subscribing to them attaches a ``ConsumerRebalanceListener`` (the next poll tells
+        it the current assignment, as after a first join)."""
+        if not self._group_managed:
+            return super().subscribe(topics, pattern, listener)
+        from ..client.consumer import ConsumerRebalanceListener
+
+        if isinstance(topics, str):
+            topics = [topics]
+        mine = {br.topic for br in self._bridges}
+        if pattern is not None or not set(topics) <= mine:
+            raise IllegalStateError(f"this consumer's group membership covers {sorted(mine)} (its KafkaBridges); "
+                                    "subscribe to those topics, or build a new consumer")
+        if listener is not None and not isinstance(listener, ConsumerRebalanceListener):
+            raise TypeError("listener must be a ConsumerRebalanceListener")
+        self._listener = listener
+        self._listener_view = []
+        self._seen_epoch = None  # re-follow: the listener hears revoked(set()) then the assignment
+
     def _follow_bridges(self) -> None:
         epoch = self._bridges_epoch()
         if epoch == getattr(self, "_seen_epoch", None):
             return
+        # eager protocol (kafka-python): the whole previous assignment is revoked -- after the
+        # revoke hooks commit what the user finished -- before buffered records are dropped
+        self._revoke(getattr(self, "_listener_view", self._assignment))
         epochs = {}
         for br in self._bridges:
             for p, e in br.assignment_epochs():
@@ -523,6 +552,8 @@ class _BridgedConsumer(KafkaConsumer):
         self._sync_positions()
         if set(pidxs) != set(old):
             _logger.debug("Group %s assignment now %s.", self.config["group_id"], [self._tp(p) for p in pidxs])
+        self._listener_view = list(pidxs)
+        self._assigned(pidxs)
 
     def _ensure_group(self, block: bool = True) -> None:
         if self._group_managed:
