@@ -878,6 +878,55 @@ def test_sasl_scram_authenticates(broker, tls_cert, mech):
         srv.close()
 
 
+class _Tokens:
+    """kafka-python's AbstractTokenProvider shape: token() (rotating) and extensions()."""
+
+    def __init__(self, tokens, extensions=None):
+        self.tokens, self.ext, self.calls = list(tokens), extensions, 0
+
+    def token(self):
+        self.calls += 1
+        return self.tokens[min(self.calls - 1, len(self.tokens) - 1)]
+
+    def extensions(self):
+        return self.ext or {}
+
+
+@pytest.mark.parametrize("profile", ["legacy", "kafka4"])
+def test_sasl_oauthbearer_authenticates(broker, profile):
+    """SASL/OAUTHBEARER (RFC 7628): the token comes from kafka-python's sasl_oauth_token_provider,
+    extensions ride in the client message, a bad token fails the exchange, and a KafkaBridge
+    refreshes the token for the connections it makes later."""
+    from torchkafka_amd.broker.bridge import security_config
+
+    broker.create_topic("t", 2)
+    broker.fill("t", 40, "fixed_f32", size=8)
+    srv = KafkaWireServer(broker, profile=profile, sasl_oauth_tokens={"tok-1": "svc", "tok-2": "svc"}).start()
+    try:
+        base = {"security_protocol": "SASL_PLAINTEXT", "sasl_mechanism": "OAUTHBEARER"}
+        sec = security_config(**base, sasl_oauth_token_provider=_Tokens(["tok-1"], {"traceId": "abc"}))
+        assert sec["sasl_oauth_token"] == "tok-1" and sec["sasl_oauth_extensions"] == "traceId=abc"
+        c = core().WireClient(srv.address, timeout_ms=2000, security=sec)
+        assert c.list_offsets("t", [0, 1], -1) == {0: 40, 1: 40}
+        assert srv.oauth_log[-1] == ("tok-1", {"traceId": "abc"}, True)
+        with pytest.raises(Exception, match="SaslAuthenticationFailed"):
+            bad = security_config(**base, sasl_oauth_token_provider=_Tokens(["forged"]))
+            core().WireClient(srv.address, timeout_ms=2000, security=bad).metadata("t")
+        assert srv.oauth_log[-1][2] is False
+        with pytest.raises(ValueError, match="sasl_oauth_token_provider"):
+            security_config(**base)
+        prov = _Tokens(["tok-1", "tok-2"])
+        with bridge(srv, group_id="g", security_protocol="SASL_PLAINTEXT", sasl_mechanism="OAUTHBEARER",
+                    sasl_oauth_token_provider=prov, oauth_refresh_s=0.05) as br:
+            assert br.wait_caught_up(10) and br.local.end_offset("t", 1) == 40
+            assert wait_for(lambda: prov.calls >= 2)  # refreshed from the bridge's Python thread
+            br.local.commit("g", {TopicPartition("t", 0): 7})  # the commit client connects later
+            assert wait_for(lambda: broker.committed_offsets("g", "t").get(0) == 7)
+        assert {tok for tok, _, ok in srv.oauth_log if ok} >= {"tok-1"}
+    finally:
+        srv.close()
+
+
 # ---- group membership: subscribe mode (JoinGroup / SyncGroup / Heartbeat / LeaveGroup)
 
 def test_range_assignor_matches_kafkas():

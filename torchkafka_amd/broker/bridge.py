@@ -55,20 +55,43 @@ log = logging.getLogger("torchkafka.bridge")
 
 #: kafka-python configuration keys the native client understands for TLS / SASL
 SECURITY_KEYS = ("security_protocol", "ssl_cafile", "ssl_check_hostname", "ssl_certfile", "ssl_keyfile",
-                 "sasl_mechanism", "sasl_plain_username", "sasl_plain_password")
+                 "sasl_mechanism", "sasl_plain_username", "sasl_plain_password", "sasl_oauth_token_provider")
 
 
-SASL_MECHANISMS = ("PLAIN", "SCRAM-SHA-256", "SCRAM-SHA-512")
+SASL_MECHANISMS = ("PLAIN", "SCRAM-SHA-256", "SCRAM-SHA-512", "OAUTHBEARER")
+
+
+def oauth_token(provider) -> tuple[str, str]:
+    """kafka-python's ``AbstractTokenProvider``: ``token()`` and, optionally, ``extensions()`` (a
+    dict) -> (token, the extensions as RFC 7628 ``key=value`` pairs joined by 0x01)."""
+    tok = provider.token()
+    if not isinstance(tok, str) or not tok:
+        raise ValueError("sasl_oauth_token_provider.token() must return a non-empty str")
+    ext = {}
+    if hasattr(provider, "extensions"):
+        ext = provider.extensions() or {}
+    bad = [k for k in ext if k == "auth" or not str(k).isalpha()]
+    if bad:
+        raise ValueError(f"SASL/OAUTHBEARER extension names must be alphabetic and not 'auth': {bad}")
+    return tok, "\x01".join(f"{k}={v}" for k, v in ext.items())
 
 
 def security_config(**kw) -> dict:
     """The TLS / SASL subset of a kafka-python configuration, for the native wire client
     (security_protocol PLAINTEXT | SSL | SASL_PLAINTEXT | SASL_SSL; SASL mechanism PLAIN,
-    SCRAM-SHA-256 or SCRAM-SHA-512)."""
+    SCRAM-SHA-256, SCRAM-SHA-512 or OAUTHBEARER).  OAUTHBEARER's token is taken from
+    ``sasl_oauth_token_provider`` here, in Python; a :class:`KafkaBridge` refreshes it."""
     out = {k: v for k, v in kw.items() if k in SECURITY_KEYS and v is not None}
+    provider = out.pop("sasl_oauth_token_provider", None)
     mech = out.get("sasl_mechanism", "PLAIN")
-    if out.get("security_protocol", "PLAINTEXT").startswith("SASL_") and mech not in SASL_MECHANISMS:
-        raise ValueError(f"sasl_mechanism {mech!r}: the native client speaks {', '.join(SASL_MECHANISMS)}")
+    if out.get("security_protocol", "PLAINTEXT").startswith("SASL_"):
+        if mech not in SASL_MECHANISMS:
+            raise ValueError(f"sasl_mechanism {mech!r}: the native client speaks {', '.join(SASL_MECHANISMS)}")
+        if mech == "OAUTHBEARER":
+            if provider is None:
+                raise ValueError("sasl_mechanism OAUTHBEARER needs sasl_oauth_token_provider (kafka-python's "
+                                 "AbstractTokenProvider: token() and optionally extensions())")
+            out["sasl_oauth_token"], out["sasl_oauth_extensions"] = oauth_token(provider)
     return out
 
 
@@ -86,7 +109,7 @@ class KafkaBridge:
                  security_protocol: str = "PLAINTEXT", ssl_cafile: str | None = None, ssl_check_hostname: bool = True,
                  ssl_certfile: str | None = None, ssl_keyfile: str | None = None, sasl_mechanism: str | None = None,
                  sasl_plain_username: str | None = None, sasl_plain_password: str | None = None,
-                 subscribe: bool = False, session_timeout_ms: int = 10000, heartbeat_interval_ms: int = 3000,
+                 sasl_oauth_token_provider=None, oauth_refresh_s: float = 60.0, subscribe: bool = False, session_timeout_ms: int = 10000, heartbeat_interval_ms: int = 3000,
                  partition_assignment_strategy: Iterable[str] = ("range",), rebalance_timeout_ms: int = 0,
                  start: bool = True):
         """``subscribe=True`` (needs ``group_id``, excludes ``partitions``): join the consumer group
@@ -130,7 +153,8 @@ class KafkaBridge:
                                          ssl_check_hostname=ssl_check_hostname, ssl_certfile=ssl_certfile,
                                          ssl_keyfile=ssl_keyfile, sasl_mechanism=sasl_mechanism,
                                          sasl_plain_username=sasl_plain_username,
-                                         sasl_plain_password=sasl_plain_password),
+                                         sasl_plain_password=sasl_plain_password,
+                                         sasl_oauth_token_provider=sasl_oauth_token_provider),
                 subscribe=bool(subscribe), session_timeout_ms=int(session_timeout_ms),
                 heartbeat_interval_ms=int(heartbeat_interval_ms),
                 assignors=[str(a) for a in partition_assignment_strategy],
@@ -142,8 +166,21 @@ class KafkaBridge:
         self._closed = False
         self._lock = threading.Lock()
         self._reported = 0
+        self._oauth_stop = threading.Event()
+        if sasl_oauth_token_provider is not None and sasl_mechanism == "OAUTHBEARER":
+            # connections made later (reconnects, the commit client, rebalance rejoins) present a
+            # fresh token: the provider is asked again every oauth_refresh_s, from this Python thread
+            threading.Thread(target=self._refresh_oauth, args=(sasl_oauth_token_provider, float(oauth_refresh_s)),
+                             name="torchkafka-oauth", daemon=True).start()
         if start:
             self.start()
+
+    def _refresh_oauth(self, provider, every: float) -> None:
+        while not self._oauth_stop.wait(every):
+            try:
+                self._r.set_oauth_token(*oauth_token(provider))
+            except Exception:  # noqa: BLE001 - the previous token stays; the next round retries
+                log.exception("Bridge %s: sasl_oauth_token_provider failed", self.bootstrap_servers)
 
     # ------------------------------------------------------------ lifecycle
     def start(self) -> "KafkaBridge":
@@ -158,6 +195,7 @@ class KafkaBridge:
             if self._closed:
                 return
             self._closed = True
+        self._oauth_stop.set()
         self._r.stop(flush)
         self._report_errors()
         if destroy if destroy is not None else self._own:

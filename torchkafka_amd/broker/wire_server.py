@@ -59,7 +59,7 @@ SUPPORTED = PROFILES["legacy"]  # the default profile
 NONE, OFFSET_OUT_OF_RANGE, UNKNOWN_TOPIC, NOT_LEADER, UNSUPPORTED_VERSION = 0, 1, 3, 6, 35
 ILLEGAL_GENERATION, UNSUPPORTED_SASL_MECHANISM, SASL_AUTHENTICATION_FAILED = 22, 33, 58
 UNKNOWN_MEMBER_ID, REBALANCE_IN_PROGRESS, MEMBER_ID_REQUIRED = 25, 27, 79
-SASL_MECHANISMS = ("PLAIN", "SCRAM-SHA-256", "SCRAM-SHA-512")
+SASL_MECHANISMS = ("PLAIN", "SCRAM-SHA-256", "SCRAM-SHA-512", "OAUTHBEARER")
 
 
 class _R:
@@ -182,13 +182,16 @@ class KafkaWireServer:
 
     def __init__(self, broker: SyntheticBroker, host: str = "127.0.0.1", port: int = 0, node_id: int = 0,
                  cluster: list[tuple[int, str, int]] | None = None, ssl_context=None,
-                 sasl_users: dict[str, str] | None = None, profile: "str | dict" = "legacy"):
+                 sasl_users: dict[str, str] | None = None, profile: "str | dict" = "legacy",
+                 sasl_oauth_tokens: dict[str, str] | None = None):
         """``cluster``: every node of a multi-node test cluster as (node_id, host, port), this one
         included; partition p is led by ``cluster[p % len(cluster)]`` and fetches sent to another
         node answer NOT_LEADER.  None: a single-node cluster (this server leads everything).
         ``ssl_context``: a server-side ``ssl.SSLContext`` (listeners SSL / SASL_SSL).  ``sasl_users``:
         {user: password} accepted by SASL/PLAIN; every request but ApiVersions and the SASL exchange
-        closes the connection until it authenticated.  ``profile``: the request versions served
+        closes the connection until it authenticated.  ``sasl_oauth_tokens``: {bearer token: principal}
+        accepted by SASL/OAUTHBEARER (RFC 7628; every exchange is kept in :attr:`oauth_log` as
+        (token, extensions dict, accepted)).  ``profile``: the request versions served
         (:data:`PROFILES`: "legacy", "kafka4", "ancient"; or an ``{api key: (min, max)}`` dict)."""
         if isinstance(profile, dict):
             self.profile, self.versions = "custom", dict(profile)
@@ -198,6 +201,8 @@ class KafkaWireServer:
             raise ValueError(f"profile {profile!r}: one of {sorted(PROFILES)} or an {{api: (min, max)}} dict")
         self.ssl_context = ssl_context
         self.sasl_users = sasl_users
+        self.sasl_oauth_tokens = sasl_oauth_tokens
+        self.oauth_log: list = []
         self.broker = broker
         self.node_id = node_id
         self.cluster = cluster
@@ -227,7 +232,7 @@ class KafkaWireServer:
                         return  # failed TLS handshake (untrusted client / plaintext probe)
                 with srv._lock:
                     srv._conns.add(sock)
-                state = {"authed": srv.sasl_users is None}
+                state = {"authed": srv.sasl_users is None and srv.sasl_oauth_tokens is None}
                 try:
                     while True:
                         head = _recv_exact(sock, 4)
@@ -334,7 +339,8 @@ class KafkaWireServer:
             return None  # a real broker closes the connection on an unsupported version
         if key == API_SASL_HANDSHAKE:
             mech = r.str()
-            ok = self.sasl_users is not None and mech in SASL_MECHANISMS
+            ok = (self.sasl_oauth_tokens is not None if mech == "OAUTHBEARER"
+                  else self.sasl_users is not None and mech in SASL_MECHANISMS)
             w.i16(NONE if ok else UNSUPPORTED_SASL_MECHANISM)
             w.i32(len(SASL_MECHANISMS))
             for m in SASL_MECHANISMS:
@@ -360,6 +366,8 @@ class KafkaWireServer:
         """One SaslAuthenticate round of the mechanism the handshake chose: PLAIN in one round,
         SCRAM-SHA-256/512 (RFC 5802) in two -- client-first, then client-final with the proof."""
         mech = state.get("mech")
+        if mech == "OAUTHBEARER":
+            return self._oauth_step(state, token)
         if mech == "PLAIN":
             parts = token.split(b"\0")
             user, pw = (parts[1].decode(), parts[2].decode()) if len(parts) == 3 else ("", None)
@@ -396,6 +404,29 @@ class KafkaWireServer:
         state["authed"] = True
         server_sig = hmac.new(hmac.new(salted, b"Server Key", h).digest(), auth, h).digest()
         return ("v=" + base64.b64encode(server_sig).decode()).encode(), True
+
+    def _oauth_step(self, state: dict, token: bytes) -> tuple[bytes, bool]:
+        """RFC 7628: the client's first message is "n,[a=authzid],", then 0x01-separated key=value
+        pairs -- auth=Bearer <token> and the extensions -- and 0x01 0x01.  A bad token gets an error
+        challenge (JSON, error code NONE); the client's lone 0x01 that follows fails the exchange."""
+        if state.pop("oauth_failed", False):
+            return b"", False  # the client acknowledged the error challenge
+        try:
+            gs2, rest = token.decode().split(",", 2)[:2], token.decode().split(",", 2)[2]
+        except (UnicodeDecodeError, IndexError):
+            return b"", False
+        if gs2[0] not in ("n", "y") or not rest.startswith("\x01") or not rest.endswith("\x01\x01"):
+            return b"", False
+        pairs = dict(kv.split("=", 1) for kv in rest.strip("\x01").split("\x01") if "=" in kv)
+        auth = pairs.pop("auth", "")
+        bearer = auth[7:] if auth.startswith("Bearer ") else None
+        ok = bearer is not None and bearer in self.sasl_oauth_tokens
+        self.oauth_log.append((bearer, pairs, ok))
+        if ok:
+            state["authed"] = True
+            return b"", True
+        state["oauth_failed"] = True
+        return b'{"status":"invalid_token"}', True
 
     def _topic_names(self, r: _R, ver: int):
         n = r.i32()

@@ -145,6 +145,14 @@ wire::Security to_security(const py::dict& d) {
   get("sasl_plain_password", &s.password);
   if (d.contains("ssl_check_hostname") && !d["ssl_check_hostname"].is_none())
     s.check_hostname = d["ssl_check_hostname"].cast<bool>();
+  if (d.contains("sasl_oauth_token") && !d["sasl_oauth_token"].is_none()) {
+    // resolved from sasl_oauth_token_provider in Python (broker/bridge.py security_config): no
+    // native thread ever calls back into the interpreter
+    s.oauth = std::make_shared<wire::OAuthToken>();
+    s.oauth->token = d["sasl_oauth_token"].cast<std::string>();
+    if (d.contains("sasl_oauth_extensions") && !d["sasl_oauth_extensions"].is_none())
+      s.oauth->extensions = d["sasl_oauth_extensions"].cast<std::string>();
+  }
   return s;
 }
 
@@ -618,6 +626,7 @@ PYBIND11_MODULE(_tkcore, m) {
       .def("stop", &Replicator::stop, py::arg("flush") = true, py::call_guard<py::gil_scoped_release>())
       .def("flush_commits", &Replicator::flush_commits, py::call_guard<py::gil_scoped_release>())
       .def("commit_sync", &Replicator::commit_sync, py::arg("timeout_ms"), py::call_guard<py::gil_scoped_release>())
+      .def("set_oauth_token", &Replicator::set_oauth_token, py::arg("token"), py::arg("extensions") = "")
       .def("take_forward_ns", &Replicator::take_forward_ns)
       .def("wait_caught_up", &Replicator::wait_caught_up, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("running", &Replicator::running)

@@ -359,11 +359,41 @@ void Conn::scram(const Security& sec) {
   }
 }
 
+// OAUTHBEARER (RFC 7628 section 3.1): one client message -- the GS2 header "n,," then
+// 0x01-separated "auth=Bearer <token>" and the extensions, closed by 0x01 0x01.  A server that
+// rejects the token answers with an error challenge (JSON); the client acknowledges it with a
+// lone 0x01 (section 3.2.3) and the exchange fails.
+void Conn::oauthbearer(const Security& sec) {
+  std::string token, ext;
+  if (sec.oauth) {
+    std::lock_guard<std::mutex> l(sec.oauth->m);
+    token = sec.oauth->token;
+    ext = sec.oauth->extensions;
+  }
+  if (token.empty()) {
+    close();
+    throw KafkaError("SaslAuthenticationFailedError: OAUTHBEARER needs a token (sasl_oauth_token_provider)");
+  }
+  std::string msg = std::string("n,,\x01") + "auth=Bearer " + token;  // (a hex escape would eat the 'a')
+  if (!ext.empty()) msg += "\x01" + ext;
+  msg += "\x01\x01";
+  const std::string challenge = sasl_round(msg);
+  if (!challenge.empty()) {
+    try {
+      sasl_round(std::string(1, '\x01'));
+    } catch (const KafkaError&) {
+    }
+    close();
+    throw KafkaError("SaslAuthenticationFailedError: OAUTHBEARER token rejected: " + challenge);
+  }
+}
+
 void Conn::authenticate(const Security& sec) {
   const bool is_scram = sec.sasl_mechanism == "SCRAM-SHA-256" || sec.sasl_mechanism == "SCRAM-SHA-512";
-  if (sec.sasl_mechanism != "PLAIN" && !is_scram)
+  const bool is_oauth = sec.sasl_mechanism == "OAUTHBEARER";
+  if (sec.sasl_mechanism != "PLAIN" && !is_scram && !is_oauth)
     throw KafkaError("UnsupportedSaslMechanismError: " + sec.sasl_mechanism +
-                     " (this client speaks PLAIN, SCRAM-SHA-256 and SCRAM-SHA-512)");
+                     " (this client speaks PLAIN, SCRAM-SHA-256, SCRAM-SHA-512 and OAUTHBEARER)");
   Writer hs;
   hs.str(sec.sasl_mechanism);
   auto r1 = roundtrip(kSaslHandshake, version(kSaslHandshake), "torchkafka", hs.data(), timeout_ms_);
@@ -375,6 +405,10 @@ void Conn::authenticate(const Security& sec) {
   }
   if (is_scram) {
     scram(sec);
+    return;
+  }
+  if (is_oauth) {
+    oauthbearer(sec);
     return;
   }
   std::string token;

@@ -47,12 +47,21 @@ namespace tk::wire {
 // SASL_PLAINTEXT | SASL_SSL; TLS through OpenSSL (server verified against ssl_cafile, or the
 // system store); SASL mechanisms PLAIN, SCRAM-SHA-256 and SCRAM-SHA-512 (SaslHandshake v1 +
 // SaslAuthenticate v0).
+// SASL/OAUTHBEARER (RFC 7628): the bearer token (and "key=value" extensions joined by 0x01) a
+// connection authenticates with.  Shared by every copy of the Security it belongs to, so a token
+// refreshed through one handle (Replicator::set_oauth_token) reaches the connections made later.
+struct OAuthToken {
+  std::mutex m;
+  std::string token, extensions;
+};
+
 struct Security {
   std::string protocol = "PLAINTEXT";
   std::string cafile, certfile, keyfile;
   bool check_hostname = true;
   std::string sasl_mechanism = "PLAIN";
   std::string username, password;
+  std::shared_ptr<OAuthToken> oauth;  // sasl_mechanism OAUTHBEARER
   bool tls() const { return protocol == "SSL" || protocol == "SASL_SSL"; }
   bool sasl() const { return protocol == "SASL_PLAINTEXT" || protocol == "SASL_SSL"; }
 };
@@ -176,6 +185,7 @@ class Conn {
   std::map<int16_t, ApiRange> broker_;
   void authenticate(const Security& sec);
   void scram(const Security& sec);
+  void oauthbearer(const Security& sec);
   std::string sasl_round(const std::string& token);
   SSL* ssl_ = nullptr;
   std::string host_;

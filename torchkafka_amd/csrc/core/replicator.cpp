@@ -311,6 +311,13 @@ std::vector<std::pair<int32_t, uint64_t>> Replicator::assignment_epochs() const 
   return v;
 }
 
+void Replicator::set_oauth_token(const std::string& token, const std::string& extensions) {
+  if (!cfg_.security.oauth) throw std::invalid_argument("replicator: not configured for SASL/OAUTHBEARER");
+  std::lock_guard<std::mutex> l(cfg_.security.oauth->m);
+  cfg_.security.oauth->token = token;
+  cfg_.security.oauth->extensions = extensions;
+}
+
 void Replicator::stop(bool flush) {
   if (!running_.load() && threads_.empty()) return;
   {

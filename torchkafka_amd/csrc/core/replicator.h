@@ -95,6 +95,9 @@ class Replicator {
   void start();
   // Stops fetching; forwards the latest local commits first when `flush`.
   void stop(bool flush = true);
+  // SASL/OAUTHBEARER: the token (and extensions) the connections made from now on present
+  // (KafkaBridge refreshes it from the sasl_oauth_token_provider).
+  void set_oauth_token(const std::string& token, const std::string& extensions);
   // Forwards every changed local commit to the coordinator now; returns partitions committed.
   int flush_commits();
   // Synchronous commit (DeviceLoader commit="sync"): wakes the commit thread, which forwards every
