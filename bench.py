@@ -552,10 +552,10 @@ def run_rank(args) -> int:
         )
 
     def describe(loader) -> tuple[str, str]:
-        h2d = loader._resolve_h2d(loader._slot_capacity()) if device.type == "cuda" else "n/a (cpu)"
-        decode = ("host workers" if not loader._span() else
+        h2d = loader.plan.resolve_h2d(loader._slot_capacity()) if device.type == "cuda" else "n/a (cpu)"
+        decode = ("host workers" if not loader.plan.span else
                   "device (gfx950 CRC32C + decode from an HBM mirror filled by SDMA copies)"
-                  if loader._mirror() else "device (gfx950 CRC32C + decode from pinned logs)")
+                  if loader.plan.mirror else "device (gfx950 CRC32C + decode from pinned logs)")
         return h2d, decode
 
     loader = make_loader("bench", dtypes[args.dtype], args.h2d)

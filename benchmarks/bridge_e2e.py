@@ -204,7 +204,7 @@ def main() -> int:
         out["end_to_end"] = {"records": n, "records_total": marks[-1][1], "s": round(el, 3),
                              "records_per_s": round(n_timed / el, 1),
                              "gb_per_s": round(n_timed * args.dim * 4 / el / 1e9, 2),
-                             "decode": "device" if dl._span() else "host",
+                             "decode": "device" if dl.plan.span else "host",
                              "cluster_committed_ok": all(v == args.records for v in committed.values()),
                              "loader": {k: v for k, v in dl.stats_summary().items()
                                         if k in ("worker_fill_us_per_batch", "commit_latency_p99_us",

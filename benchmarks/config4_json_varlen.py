@@ -100,9 +100,9 @@ def run(args, sync=None) -> dict:
                 "batch_size": B, "workers": args.workers, "partitions": args.partitions,
                 "json_parse": args.json_parse, "h2d": args.h2d, "verify": dl.verify,
                 "decode": (("device (json_span.hip from an HBM mirror filled by SDMA copies)"
-                            if dl._mirror() else "device (json_span.hip from the pinned logs)")
-                           if dl._json_span() else args.decode),
-                "json_count": "device" if dl._json_count() else "workers",
+                            if dl.plan.mirror else "device (json_span.hip from the pinned logs)")
+                           if dl.plan.json_span else args.decode),
+                "json_count": "device" if dl.plan.json_count else "workers",
                 "timed_s": round(el, 4), "steps": args.steps,
                 "avg_record_bytes": round(text_bytes),
                 "last_batch_shape": list(x.shape),

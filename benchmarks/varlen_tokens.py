@@ -69,8 +69,8 @@ def main():
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         st = dl.stats_summary()
-        decode = (("device (varlen_span_kernel from an HBM mirror filled by SDMA copies)" if dl._mirror()
-                   else "device (varlen_span_kernel from the pinned logs)") if dl._var_span() else "host workers")
+        decode = (("device (varlen_span_kernel from an HBM mirror filled by SDMA copies)" if dl.plan.mirror
+                   else "device (varlen_span_kernel from the pinned logs)") if dl.plan.var_span else "host workers")
         it.close()
         rec_bytes = b.partition_stats("tok", 0)["log_bytes"] / max(1, b.end_offset("tok", 0))
         print(json.dumps({"metric": "int32 token records/s to GPU (int64 padded), per-batch commit",

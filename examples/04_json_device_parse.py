@@ -47,7 +47,7 @@ def main():
         for x, lengths, mask in auto_commit(loader):  # x: [128, L] bf16, L = the batch's longest row
             rows += x.shape[0]
             assert bool((mask.sum(1) == lengths).all())
-        print(f"{rows} rows on {device} (device parse: {loader._json_device()}); "
+        print(f"{rows} rows on {device} (device parse: {loader.plan.json_device}); "
               f"committed {broker.committed_offsets('ex4', 'seq')}")
     finally:
         broker.destroy()

@@ -82,7 +82,7 @@ def test_overridden_process_is_honoured_with_a_schema(broker):
     broker.create_topic("t", 2)
     broker.fill("t", 30, "fixed_f32", size=8)
     dl = _loader(EvenOnly, broker, 5)
-    assert dl._process_overridden() and not dl._fast_path_ok()
+    assert dl.plan.process_overridden and not dl.plan.fast_path
     xs = torch.cat(list(auto_commit(dl)))
     offsets = sorted((xs[:, 0] / 2).long().tolist())
     assert len(offsets) == 30 and all(o % 2 == 0 for o in offsets)
@@ -164,7 +164,7 @@ def test_kafka_python_consumer_commits_through_its_worker(tmp_path, monkeypatch)
     dl = DeviceLoader(Vec8.placeholder(), 10, device="cpu", num_workers=2, sharding="group",
                       worker_init_fn=Vec8.init_worker("t", bootstrap_servers="kafka-1:9092", group_id="g",
                                                       consumer_timeout_ms=300))
-    assert dl._sink == "worker" and not dl._span()
+    assert dl._sink == "worker" and not dl.plan.span
     xs = torch.cat(list(auto_commit(dl)))
     assert sorted(map(tuple, xs[:, :2].long().tolist())) == sorted((o, p) for p in range(3) for o in range(25))
     final = {}

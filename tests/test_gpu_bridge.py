@@ -45,7 +45,7 @@ def test_device_decode_from_a_replicated_cluster(broker, live):
                 if not live:
                     assert br.wait_caught_up(20)
                 dl = _loader(Rows, br.url, decode)
-                assert dl._span() == (decode == "device")
+                assert dl.plan.span == (decode == "device")
                 xs = []
                 for i, x in enumerate(auto_commit(dl)):
                     xs.append(x.clone())
@@ -87,7 +87,7 @@ def test_long_stream_unpins_and_releases_consumed_log(broker):
                                   worker_init_fn=Rows.init_worker("t", bootstrap_servers=br.url, group_id="g",
                                                                   auto_offset_reset="earliest",
                                                                   consumer_timeout_ms=1000))
-                assert dl._span()
+                assert dl.plan.span
                 n, last = 0, -1
                 for x in auto_commit(dl):
                     offs = x[:, 0]
@@ -128,7 +128,7 @@ def test_ring_replica_long_stream_device_decode(broker):
                                   worker_init_fn=Rows.init_worker("t", bootstrap_servers=br.url, group_id="g",
                                                                   auto_offset_reset="earliest",
                                                                   consumer_timeout_ms=1500))
-                assert dl._span()
+                assert dl.plan.span
                 n, last = 0, -1
                 for x in auto_commit(dl):
                     assert int(x[0, 0].item()) == last + 1

@@ -113,7 +113,7 @@ def test_json_span_matches_json_loads(broker, dtype, bs, rpb, lens, odd, nulls, 
 
     DS = _dataset(JsonArray())
     got, dl = _run(broker, "t", DS, bs, "g-dev", dtype=dtype, num_workers=workers, coalesce=4)
-    assert dl._json_span() and dl._json_count()  # the workers read headers only; the device counts
+    assert dl.plan.json_span and dl.plan.json_count  # the workers read headers only; the device counts
     exp = _expected(texts, bs, dtype)
     assert len(got) == len(exp)
     for (x, ln), (ex, el) in zip(got, exp):
@@ -125,7 +125,7 @@ def test_json_span_matches_json_loads(broker, dtype, bs, rpb, lens, odd, nulls, 
     for decode, jp, jc in (("auto", "auto", "host"), ("host", "auto", "auto"), ("auto", "host", "auto")):
         other, dl2 = _run(broker, "t", DS, bs, f"g-{decode}-{jp}-{jc}", dtype=dtype, num_workers=workers,
                           decode=decode, json_parse=jp, json_count=jc)
-        assert dl2._json_span() == (jc == "host") and not dl2._json_count()
+        assert dl2.plan.json_span == (jc == "host") and not dl2.plan.json_count
         assert len(other) == len(got)
         for (x, ln), (y, lm) in zip(got, other):
             assert torch.equal(_bits(x), _bits(y)) and torch.equal(ln, lm)
@@ -152,7 +152,7 @@ def test_json_device_count_edge_rows(broker, pad_to, pad_multiple, dtype, bs):
     if pad_to is not None:
         kw["pad_to"] = pad_to
     got, dl = _run(broker, "e", DS, bs, "g", dtype=dtype, num_workers=1, **kw)
-    assert dl._json_count()
+    assert dl.plan.json_count
     ref, _ = _run(broker, "e", DS, bs, "g-host", dtype=dtype, num_workers=1, json_count="host", **kw)
     exp = _expected(texts, bs, dtype, pad=-3.0, pad_multiple=pad_multiple)
     assert len(got) == len(exp) == len(ref)
@@ -176,7 +176,7 @@ def test_json_device_count_malformed_row_raises_before_commit(broker, bad):
     dl = DeviceLoader(DS.placeholder(), 32, num_workers=1, device="cuda:0",
                       worker_init_fn=DS.init_worker("m", bootstrap_servers=broker.url, group_id="g",
                                                     auto_offset_reset="earliest", consumer_timeout_ms=300))
-    assert dl._json_count()
+    assert dl.plan.json_count
     with pytest.raises(CorruptRecordException, match="not a flat numeric JSON array"):
         for _x in auto_commit(dl):
             torch.cuda.synchronize()
@@ -193,7 +193,7 @@ def test_json_span_filters_pad_and_mask(broker):
     DS = _dataset(JsonArray(min_len=4, max_len=25))
     got, dl = _run(broker, "t", DS, 100, "g", dtype=torch.float32, num_workers=2, pad_value=-7.0, return_mask=True,
                    pad_multiple=8)
-    assert dl._json_span()
+    assert dl.plan.json_span
     n = 0
     for x, ln, m in got:
         assert x.shape[1] % 8 == 0 and x.shape[1] <= 32
@@ -236,7 +236,7 @@ def test_json_span_crc_failure_raises_before_commit(broker):
     dl = DeviceLoader(DS.placeholder(), 10, num_workers=1, device="cuda:0", coalesce=1,
                       worker_init_fn=DS.init_worker("c", bootstrap_servers=broker.url, group_id="g",
                                                     auto_offset_reset="earliest", consumer_timeout_ms=300))
-    assert dl._json_span()
+    assert dl.plan.json_span
     with pytest.raises(CorruptRecordException, match="offset 60 .*failed CRC check"):
         for _x in auto_commit(dl):
             torch.cuda.synchronize()
@@ -303,7 +303,7 @@ def test_json_span_through_hbm_mirror(broker):
     a, _ = _run(broker, "t", DS, 128, "gz", dtype=torch.bfloat16, num_workers=2)
     b, dl = _run(broker, "t", DS, 128, "gm", dtype=torch.bfloat16, num_workers=2, h2d="dma",
                  tuning=Tuning(mirror_chunk_mib=1, mirror_chunks=2))
-    assert dl._json_span() and dl._mirror()
+    assert dl.plan.json_span and dl.plan.mirror
     assert len(a) == len(b)
     for (x, ln), (y, lm) in zip(a, b):
         assert torch.equal(_bits(x), _bits(y)) and torch.equal(ln, lm)

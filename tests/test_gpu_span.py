@@ -36,7 +36,7 @@ def _run(broker, topic, DS, decode, bs, group, **kw):
     dl = DeviceLoader(DS.placeholder(), bs, device="cuda:0", decode=decode,
                       worker_init_fn=DS.init_worker(topic, bootstrap_servers=broker.url, group_id=group,
                                                     auto_offset_reset="earliest", consumer_timeout_ms=300), **kw)
-    assert dl._span() == (decode == "device")
+    assert dl.plan.span == (decode == "device")
     xs = [x.clone() for x in auto_commit(dl)]
     torch.cuda.synchronize()
     return torch.cat(xs) if xs else None, dl
@@ -255,7 +255,7 @@ def test_device_decode_through_hbm_mirror(broker, chunk_mib, chunks, rpb, size):
     a, _ = _run(broker, "t", DS, "host", 32, "gh", num_workers=2, in_order=True)
     b, dl = _run(broker, "t", DS, "device", 32, "gm", num_workers=2, in_order=True, h2d="dma",
                  tuning=Tuning(mirror_chunk_mib=chunk_mib, mirror_chunks=chunks))
-    assert dl._mirror()
+    assert dl.plan.mirror
     assert torch.equal(_bits(a), _bits(b))
     assert broker.committed_offsets("gm", "t") == {0: n, 1: n, 2: n}
     st = dl.stats_summary()
@@ -324,7 +324,7 @@ def test_var_span_matches_host_path(broker, src, dst, lens, nulls, long_every, o
                           worker_init_fn=DS.init_worker("v", bootstrap_servers=broker.url, group_id=f"g{decode}",
                                                         auto_offset_reset="earliest", consumer_timeout_ms=300),
                           **opts)
-        assert dl._var_span() == (decode == "device")
+        assert dl.plan.var_span == (decode == "device")
         outs[decode] = [tuple(t.clone() for t in b) for b in auto_commit(dl)]
         assert broker.committed_offsets(f"g{decode}", "v") == {0: 180, 1: 180}
     a, b = outs["host"], outs["device"]
@@ -352,7 +352,7 @@ def test_hbm_mirror_copies_across_pin_pieces(broker):
         DS = _dataset(FixedWidth(torch.float32, (256,)))
         b, dl = _run(big, "t", DS, "device", 256, "gm", num_workers=1, in_order=True, h2d="dma",
                      tuning=Tuning(mirror_chunk_mib=8, mirror_chunks=4))
-        assert dl._mirror() and b.shape == (90_000, 256)
+        assert dl.plan.mirror and b.shape == (90_000, 256)
         assert torch.equal(b[:, 0], torch.arange(90_000, dtype=torch.float32, device=b.device))
         for o in (0, 65_000, 89_999):
             assert torch.equal(b[o].cpu(), torch.tensor([synth_f32(0, o, j) for j in range(256)]))

@@ -109,7 +109,8 @@ class KafkaBridge:
                  security_protocol: str = "PLAINTEXT", ssl_cafile: str | None = None, ssl_check_hostname: bool = True,
                  ssl_certfile: str | None = None, ssl_keyfile: str | None = None, sasl_mechanism: str | None = None,
                  sasl_plain_username: str | None = None, sasl_plain_password: str | None = None,
-                 sasl_oauth_token_provider=None, oauth_refresh_s: float = 60.0, subscribe: bool = False, session_timeout_ms: int = 10000, heartbeat_interval_ms: int = 3000,
+                 sasl_oauth_token_provider=None, oauth_refresh_s: float = 60.0, subscribe: bool = False,
+                 session_timeout_ms: int = 10000, heartbeat_interval_ms: int = 3000,
                  partition_assignment_strategy: Iterable[str] = ("range",), rebalance_timeout_ms: int = 0,
                  start: bool = True):
         """``subscribe=True`` (needs ``group_id``, excludes ``partitions``): join the consumer group

@@ -41,7 +41,7 @@ from typing import NamedTuple
 
 import torch
 
-from ..client.errors import COMMIT_FAILED_ERRORS, CorruptRecordException, KafkaError
+from ..client.errors import CorruptRecordException
 from ..config import LoaderConfig
 from ..ops.collate import CODE_DTYPE, DTYPE_CODE, FLOAT_DTYPES, _stream_ptr, normalize_params
 from ..ops.native import core, hip
@@ -50,6 +50,9 @@ from ..utils import topology
 from ..utils.metrics import LoaderStats
 from ..utils.tracing import enabled as _roctx_enabled
 from ..utils.tracing import trace_range
+from .bridging import LoaderBridges
+from .commits import LoaderCommits
+from .path_plan import PathPlan
 from .worker import worker_main
 
 log = logging.getLogger(__name__)
@@ -175,8 +178,8 @@ class _Run:
                 dev = L.device.index if L.device.index is not None else torch.cuda.current_device()
                 # device decode with h2d='dma': the slots (row tables) are read zero-copy and the copy
                 # engines move the log bytes into an HBM mirror (enable_mirror below)
-                mode = hip().H2D_ZERO_COPY if (L._resolve_h2d(self.ring.payload_capacity) in ("zerocopy", "direct")
-                                               or L._mirror()) else hip().H2D_DMA
+                mode = hip().H2D_ZERO_COPY if (L.plan.resolve_h2d(self.ring.payload_capacity) in ("zerocopy", "direct")
+                                               or L.plan.mirror) else hip().H2D_DMA
                 self.engine = hip().Engine(dev, self.ring.n_slots, self.ring.payload_capacity, L.copy_streams, mode)
                 if L.tuning.decode_streams is not None:  # before anything creates a decode stream
                     self.engine.set_decode_streams(int(L.tuning.decode_streams))
@@ -196,11 +199,11 @@ class _Run:
                 self.driver.set_event_every(L._event_every(self.ring.n_slots))
                 self.driver.set_coalesce(L.coalesce)
                 self.driver.set_coalesce_wait_us(L.coalesce_wait_us if L.coalesce > 1 else 0)
-                if L._direct():
+                if L.plan.direct:
                     self.driver.enable_direct()
-                if L._direct() or L._device_decode():
+                if L.plan.direct or L.plan.device_decode:
                     self.driver.pin_logs(L._rank_partitions())
-                if L._mirror():
+                if L.plan.mirror:
                     # under the RCCL lockstep one SDMA copy stream: the process's 4 hardware queues
                     # go to the user's stream, two decode streams and the lockstep's RCCL stream
                     mcs = 1 if L._lockstep_transport() == "rccl" else 0
@@ -318,7 +321,7 @@ class _Run:
             pass
 
 
-class DeviceLoader:
+class DeviceLoader(LoaderBridges, LoaderCommits):
     """Streams a :class:`KafkaDataset` to device tensors.
 
     Mirrors ``DataLoader(dataset, batch_size, num_workers, worker_init_fn)``
@@ -470,6 +473,11 @@ class DeviceLoader:
             self.worker_init_fn = self._bridge_cluster(self.worker_init_fn, forced=cfg.bridge is True)
         self._group_id, self._servers = self._resolve_commit_target(cfg.group_id, cfg.bootstrap_servers)
         self._sink = self._resolve_sink()
+        self.plan = PathPlan.build(
+            device_type=self.device.type, schema=self.schema, native=self.native, decode=self.decode, h2d=self.h2d,
+            json_parse=self.json_parse, synthetic_commits=self._commit_target_url()[0] != "",
+            process_overridden=self._process_overridden(), return_info=self.return_info,
+            drop_last=self.drop_last, json_count_mode=getattr(tun, "json_count", "auto"))
         self._pending_wms: list = []   # finished-but-uncommitted watermark lists
         self._committed: dict[int, int] = {}
         self._norm = None
@@ -482,88 +490,6 @@ class DeviceLoader:
         return max(1, self.num_workers)
 
     # ------------------------------------------------------------------ configuration helpers
-    def _bridge_cluster(self, wi, forced: bool):
-        """``bridge='auto'``: workers told to read a real Kafka cluster (``init_worker(topic,
-        bootstrap_servers='host:9092', ...)``, the reference's usage) read a local replica instead,
-        which a native :class:`~torchkafka_amd.broker.KafkaBridge` per topic fills with this rank's
-        partitions; the device path (header walk, gfx950 CRC + decode) then runs unchanged and the
-        commits reach the cluster's group coordinator.  Static sharding only (the bridge assigns
-        partitions by rank; ``sharding='group'`` keeps kafka-python's group membership)."""
-        from ..broker.synthetic import is_synthetic_url
-        from ..models.kafka_dataset import _WorkerInit
-
-        if not isinstance(wi, _WorkerInit) or self.sharding != "static":
-            if forced:
-                raise ValueError("bridge=True needs static sharding and a worker_init_fn from init_worker()")
-            return wi
-        servers = wi.kwargs.get("bootstrap_servers", "localhost:9092")  # kafka-python's default
-        if is_synthetic_url(servers) or (not forced and os.environ.get("TORCHKAFKA_BROKER")):
-            return wi
-        topics = list(wi.args)
-        if not topics or not all(isinstance(t, str) for t in topics):
-            if forced:
-                raise ValueError("bridge=True needs the topics named in init_worker()")
-            return wi
-        from ..broker.bridge import KafkaBridge
-        from ..ops.native import core
-        from ..parallel.sharding import shard_partitions
-
-        if not isinstance(servers, str):
-            servers = ",".join(servers)
-        group = wi.kwargs.get("group_id")
-        reset = wi.kwargs.get("auto_offset_reset", "latest")  # kafka-python's default
-        from ..broker.bridge import SECURITY_KEYS, security_config
-
-        security = security_config(**{k: v for k, v in wi.kwargs.items() if k in SECURITY_KEYS})
-        client = core().WireClient(servers, "torchkafka-bridge", int(wi.kwargs.get("request_timeout_ms", 30000)),
-                                   security)
-        shares = {}
-        for t in topics:
-            err, parts = client.metadata(t)
-            if err:
-                raise KafkaError(f"UnknownTopicOrPartitionError: topic {t!r} on {servers}")
-            shares[t] = shard_partitions(len(parts), self.rank, self.world_size)
-        self._bridge_spec = (servers, group, reset, shares, security)
-        url = self._start_bridges(None)
-        log.info("DeviceLoader: %s mirrored into %s by %d KafkaBridge(s) (rank %d/%d).", servers, url,
-                  len(self._bridges), self.rank, self.world_size)
-        return _WorkerInit(wi.cls, wi.args, {**wi.kwargs, "bootstrap_servers": url})
-
-    def _start_bridges(self, url):
-        """One KafkaBridge per topic of ``self._bridge_spec`` into one replica broker (``url``: reuse
-        that name); returns the replica's URL."""
-        from ..broker.bridge import KafkaBridge
-
-        servers, group, reset, shares, security = self._bridge_spec
-        first = True
-        try:
-            for t, mine in shares.items():
-                br = KafkaBridge(servers, t, group_id=group, partitions=mine, url=url, auto_offset_reset=reset,
-                                 **security)
-                br._own = first  # the first bridge owns the shared replica broker
-                first = False
-                url = br.url
-                self._bridges.append(br)
-        except BaseException:
-            for br in self._bridges:
-                br.close(flush=False)
-            self._bridges.clear()
-            raise
-        return url
-
-    def _resolve_commit_target(self, group_id, servers):
-        from ..models.kafka_dataset import _WorkerInit
-
-        if group_id is None or servers is None:
-            wi = self.worker_init_fn
-            if isinstance(wi, _WorkerInit):
-                group_id = group_id if group_id is not None else wi.kwargs.get("group_id")
-                servers = servers if servers is not None else wi.kwargs.get("bootstrap_servers")
-            cons = getattr(self.dataset, "_consumer", None)
-            if cons is not None and hasattr(cons, "config"):
-                group_id = group_id if group_id is not None else cons.config.get("group_id")
-                servers = servers if servers is not None else cons.config.get("bootstrap_servers")
-        return group_id, servers
 
     def _resolve_sink(self) -> str:
         """Where finished offsets are committed.  'broker': this process stores them straight into
@@ -588,19 +514,6 @@ class DeviceLoader:
 
         return type(self.dataset)._process is not KafkaDataset._process
 
-    def _commit_target_url(self) -> tuple[str, str]:
-        if self._group_id is None or self._servers is None:
-            return "", ""
-        from ..broker.synthetic import resolve_url
-
-        try:
-            return resolve_url(self._servers), str(self._group_id)
-        except Exception:  # noqa: BLE001 - not a synthetic broker: commits go through Python
-            return "", ""
-
-    #: largest slot payload that ``h2d="auto"`` moves with zero-copy reads (above: DMA on side streams)
-    ZERO_COPY_MAX_BYTES = 1 << 20
-
     def _event_every(self, n_slots: int) -> int:
         """Slots per completion event: one ``hipEventRecord`` per batch costs ~1.3 µs of host time,
         so with a deep ring only every k-th batch records one (k <= n_slots / 4 keeps workers fed;
@@ -608,20 +521,6 @@ class DeviceLoader:
         if self.event_every is not None:
             return self.event_every
         return max(1, min(4, n_slots // 4))
-
-    def _resolve_h2d(self, slot_payload_bytes: int) -> str:
-        if self.h2d != "auto":
-            return self.h2d
-        if self._device_decode():
-            # device decode: the slots hold row tables (a few KiB read once by the kernel), the values
-            # stay in the pinned logs -- a DMA of the slot would only add a copy and an event per batch
-            return "zerocopy"
-        if self._json_device():
-            # JSON text batches are a few hundred KiB whatever the slot capacity; the parse kernel
-            # reads each row once, so zero-copy beats a DMA + HBM re-read (14.3 vs 12.6 M rec/s,
-            # BASELINE config 4, profiles/r01_s5)
-            return "zerocopy"
-        return "zerocopy" if slot_payload_bytes <= self.ZERO_COPY_MAX_BYTES else "dma"
 
     def _default_src_code(self) -> int:
         s = self.schema
@@ -631,23 +530,10 @@ class DeviceLoader:
             return DTYPE_CODE[torch.float32]
         return DTYPE_CODE[s.dtype]
 
-    RING_AUTO_BYTES = 64 << 20
-    RING_AUTO_BYTES_VARLEN = 512 << 20
-
     def _slots_per_worker(self) -> int:
         if self.slots_per_worker is not None:
             return self.slots_per_worker
-        if self._device_decode():
-            # device-decode slots hold row positions only (a few KiB): a deep ring costs no pinned
-            # memory and lets the workers run ahead while slots wait for their kernels
-            return 16
-        budget = self.RING_AUTO_BYTES
-        if getattr(self.schema, "kind", None) in (1, 2) and self.device.type == "cuda":
-            # var-len / JSON slots are sized for the worst row (16 MiB) but hold a few hundred KiB:
-            # 8 per worker keeps the workers off the slot-release wait (config 4: +4 %)
-            budget = self.RING_AUTO_BYTES_VARLEN
-        fit = budget // max(1, self.n_producers * self._slot_capacity())
-        return int(max(4, min(8, fit)))
+        return self.plan.slots_per_worker(self._slot_capacity(), self.n_producers)
 
     def _n_extras(self) -> int:
         """Record-field columns (Key / Timestamp) the schema adds beside the value."""
@@ -657,34 +543,15 @@ class DeviceLoader:
         if self.slot_bytes is not None:
             return int(self.slot_bytes)
         # record fields ride after the layout: one int64 per row each (+ alignment)
-        return self._layout_capacity() + (self.batch_size * 8 * self._n_extras() + 256 if self._n_extras() else 0)
-
-    def _layout_capacity(self) -> int:
-        s = self.schema
-        if self._span():
-            # row table (8 B per row) + SpanSeg entries: one per RecordBatch touched, plus one per
-            # 32 KiB of values (kSpanSegMax cuts), with headroom
-            B = self.batch_size
-            segs = 2 * B + 128 + (B * s.row_bytes) // (32 << 10)
-            return (B * 8 + 255) // 256 * 256 + 32 * segs
-        if self._json_span() or self._var_span():
-            # row table (16 B per row) + the values of rows the workers handle themselves (JSON rows
-            # that are not "simple": exponents, NaN, long tokens; var-len values longer than a
-            # segment; a batch closes early if they do not fit) + the segments (one per RecordBatch
-            # touched, one per 128 KiB or 1024 rows, host-row groups)
-            B = self.batch_size
-            host = self.JSON_SPAN_HOST_VALUES_BYTES if self._json_span() else self.VAR_SPAN_HOST_VALUES_BYTES
-            return (B * 16 + 255) // 256 * 256 + host + 32 * (3 * B + 128)
-        if s is not None and getattr(s, "kind", None) == 0 and not self._process_overridden():
-            return self.batch_size * s.row_bytes
-        return 16 << 20
+        nx = self._n_extras()
+        return self.plan.layout_capacity(self.batch_size, self.schema) + (self.batch_size * 8 * nx + 256 if nx else 0)
 
     def _worker_cfg(self) -> dict:
         return {"batch_size": self.batch_size, "sharding": self.sharding, "rank": self.rank,
                 "world_size": self.world_size, "native": self.native, "base_seed": self.base_seed,
-                "gather": self._direct(), "json_device": self._json_device(), "json_count": self._json_count(),
-                "span": self._device_decode(),
-                "process_overridden": self._process_overridden(), "commit_table": None,
+                "gather": self.plan.direct, "json_device": self.plan.json_device, "json_count": self.plan.json_count,
+                "span": self.plan.device_decode,
+                "process_overridden": self.plan.process_overridden, "commit_table": None,
                 "worker_spin_us": int(self.tuning.worker_spin_us), "in_process": False,
                 "commit_mode": self.commit_mode}
 
@@ -712,124 +579,6 @@ class DeviceLoader:
             return out
         except Exception:  # noqa: BLE001 - not a synthetic broker: pinned lazily, batch by batch
             return []
-
-    def _span(self) -> bool:
-        """decode='device': fixed-width records decoded by the gfx950 kernel (span_decode.hip).
-
-        The workers only walk the record headers of the batches they consume (exact batch
-        boundaries, null values skipped like ``_process -> None``) and hand over log ranges +
-        row positions; the kernel reads the ranges straight out of the pinned broker logs,
-        verifies every RecordBatch's CRC32C (kafka-python's ``check_crcs``), extracts and casts
-        the values.  A corrupted batch raises ``CorruptRecordException`` before its offsets are
-        committed.  'auto' takes it whenever it applies: CUDA device, FixedWidth schema, the
-        native path, the synthetic broker (shm:// or file://) with a group_id, h2d != 'direct'.
-        """
-        if self.decode == "host":
-            return False
-        s = self.schema
-        ok = (self.device.type == "cuda" and self.native and getattr(s, "kind", None) == 0
-              and self.h2d != "direct" and self._commit_target_url()[0] != "" and not self._process_overridden())
-        if self.decode == "device" and not ok and getattr(s, "kind", None) not in (1, 2):  # _var_span/_json_span
-            raise ValueError("decode='device' needs a CUDA device, a FixedWidth schema, native=True, h2d != 'direct' "
-                             "and the synthetic broker (bootstrap_servers shm:// or file://) with a group_id")
-        return ok
-
-    #: slot room of a device-parsed JSON batch (decode='device') for the rows its worker parses itself
-    JSON_SPAN_HOST_VALUES_BYTES = 2 << 20
-    #: slot room of a device-decoded var-len batch for the values its worker copies (longer than a segment)
-    VAR_SPAN_HOST_VALUES_BYTES = 4 << 20
-
-    def _device_decode(self) -> bool:
-        """Any schema decoded on the device straight from the pinned logs (decode='auto'/'device')."""
-        return self._span() or self._json_span() or self._var_span()
-
-    def _var_span(self) -> bool:
-        """decode='device' for VarLen records (e.g. int32 token ids): the workers only walk the record
-        headers (the value length is in the header); span_decode.hip's varlen_span_kernel stages the
-        log segments, verifies each RecordBatch's CRC32C and pads/casts every row into the batch."""
-        if self.decode == "host":
-            return False
-        s = self.schema
-        ok = (self.device.type == "cuda" and self.native and getattr(s, "kind", None) == 1
-              and self.h2d != "direct" and self._commit_target_url()[0] != "" and not self._process_overridden())
-        if self.decode == "device" and not ok and getattr(s, "kind", None) == 1:
-            raise ValueError("decode='device' for VarLen needs a CUDA device, native=True, h2d != 'direct' and the "
-                             "synthetic broker (bootstrap_servers shm:// or file://) with a group_id")
-        return ok
-
-    def _json_span(self) -> bool:
-        """decode='device' for JsonArray records parsed on the GPU (json_span.hip): the workers walk the
-        record headers and pre-scan each text where it lies (element count, "simple row" check) but
-        neither copy it nor CRC the batch; the kernel reads the texts straight out of the pinned
-        broker logs, verifies each RecordBatch's CRC32C and parses the rows.  'auto' takes it
-        whenever the device JSON parse applies and the synthetic broker is the source (shm:// or
-        file:// with a group_id); decode='host' keeps the workers framing + copying the text."""
-        if self.decode == "host" or not self._json_device():
-            return False
-        ok = self.h2d != "direct" and self._commit_target_url()[0] != ""
-        if self.decode == "device" and not ok:
-            raise ValueError("decode='device' needs the synthetic broker (bootstrap_servers shm:// or file://) "
-                             "with a group_id and h2d != 'direct'")
-        return ok
-
-    def _json_count(self) -> bool:
-        """Device-parsed JsonArray rows counted on the device too (``tuning.json_count``): the workers
-        then read only the record headers, as for fixed-width records, and json_span.hip runs the
-        "simple row" check and the element count while it stages each text; the batch's width is the
-        longest row's count, reduced on the device (a row that is not simple -- exponents, NaN -- is
-        parsed on the host when its batch is delivered).  Filters that drop rows need the counts
-        before the batch is packed, so those keep the workers counting."""
-        if not self._json_span():
-            return False
-        s = self.schema
-        mode = getattr(self.tuning, "json_count", "auto")
-        ok = int(getattr(s, "min_len", 0)) == 0 and (getattr(s, "max_len", None) is None or bool(s.truncate))
-        if mode == "device" and not ok:
-            raise ValueError("tuning.json_count='device' cannot drop rows: needs min_len=0 and truncate=True")
-        return ok and mode != "host"
-
-    def _json_device(self) -> bool:
-        """JsonArray records parsed by the gfx950 kernel (json_parse.hip) instead of the workers.
-
-        The workers then only frame each record (AVX2 element count + copy of the text).  A
-        malformed row that passes their character scan (e.g. ``[1,,2]``) is found by the
-        kernel: the batch is never committed and ``CorruptRecordException`` is raised one
-        step later, when the batch's GPU work has completed.  ``skip_bad=True`` needs the
-        row dropped from its batch, which only the host parser can do, so 'auto' picks
-        the host parser there.
-        """
-        s = self.schema
-        if getattr(s, "kind", None) != 2 or self.json_parse == "host" or self._process_overridden():
-            return False
-        ok = self.device.type == "cuda" and self.native and not getattr(s, "skip_bad", False)
-        if self.json_parse == "device" and not ok:
-            raise ValueError("json_parse='device' needs a CUDA device, native=True and skip_bad=False")
-        return ok
-
-    def _mirror(self) -> bool:
-        """h2d='dma' with device decode: log bytes reach HBM by hipMemcpyAsync (SDMA copy engines, in
-        mirror chunks of ``tuning.mirror_chunk_mib``) and the decode kernels read them there, instead
-        of reading the pinned logs over PCIe themselves (csrc/hip/log_mirror.h).
-
-        Opt-in (``h2d='auto'`` stays zero-copy): the mirror matches zero-copy on fixed-width decode
-        and beats it on JSON on most runs (config 4: median 44.7 M rec/s against 39.7 M, and it won
-        12 of 12 alternated pairs: profiles/r03_final/c4_mirror_ab/).  But 2 config-4 runs of 33
-        collapsed (29.7 M and 27.3 M: profiles/r03_s3/mirror_stability/,
-        profiles/r03_final/c4_auto_mirror_trial/), and VarLen tokens run 17-25 M through it.  The
-        likely cause is a needed chunk's copy waiting behind queued prefetches on its copy stream."""
-        return self.h2d == "dma" and self._device_decode()
-
-    def _direct(self) -> bool:
-        """h2d='direct': fixed-width rows gathered by the kernel straight from the pinned broker logs."""
-        if self.h2d != "direct":
-            return False
-        if self.device.type != "cuda" or not self._fast_path_ok():
-            raise ValueError("h2d='direct' needs a CUDA device, a FixedWidth schema, native=True, "
-                             "return_info=False and drop_last=False")
-        if self._commit_target_url()[0] == "":
-            raise ValueError("h2d='direct' needs the synthetic broker (bootstrap_servers shm:// or file://) "
-                             "and a group_id")
-        return True
 
     def _out_dtype(self, src: torch.dtype) -> torch.dtype:
         if self.dtype is not None:
@@ -936,20 +685,6 @@ class DeviceLoader:
                     self._sync_commit_py()
             run.close()
 
-    def _finish_marker(self, wms):
-        """Marks a batch finished; in ``commit_on='device'`` mode fenced by the user's queued GPU work."""
-        t = time.perf_counter_ns()  # the user asked for the next batch: commit latency starts
-        if self.commit_on == "device" and self.device.type == "cuda":
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.device))
-            return (wms, ev, t)
-        return (wms, None, t)
-
-    def _fast_path_ok(self) -> bool:
-        s = self.schema
-        return (s is not None and getattr(s, "kind", None) == 0 and self.native and not self.return_info
-                and not self.drop_last and not self._process_overridden())
-
     def _lockstep_transport(self, process_group=None):
         """How ranks agree on every step: 'rccl' (native communicator, an nccl process group or
         lockstep='rccl'), 'host' (the process group's all-reduce), or None (no lockstep)."""
@@ -1003,7 +738,7 @@ class DeviceLoader:
         run = self._run
         plan = {"user": 1, "decode": 0, "copy": 0, "mirror_copy": 0, "rccl_lockstep": 0, "torch_nccl": 0}
         if run is not None and run.engine is not None:
-            plan["decode"] = int(run.engine.decode_streams()) if self._device_decode() else 0
+            plan["decode"] = int(run.engine.decode_streams()) if self.plan.device_decode else 0
             plan["copy"] = int(run.engine.copy_streams())
             if run.driver is not None:
                 plan["mirror_copy"] = int(run.driver.mirror_copy_streams)
@@ -1039,9 +774,9 @@ class DeviceLoader:
         debug = _ds_logger.isEnabledFor(logging.DEBUG)
         log_commits = debug and auto_commit
         native_ac = auto_commit and not log_commits  # with DEBUG the commit comes back to Python to be logged
-        if self._fast_path_ok():
+        if self.plan.fast_path:
             step, py_commits = self._fixed_stage(drv, native_ac), False
-        elif self._varlen_fast_ok():
+        elif self.plan.varlen_fast:
             step, py_commits = self._varlen_stage(drv, native_ac), False
         else:
             step, py_commits = self._slot_stage(run, auto_commit, debug), True
@@ -1106,11 +841,6 @@ class DeviceLoader:
                 self._absorb_driver_stats(drv)
                 run.close()
 
-    def _varlen_fast_ok(self) -> bool:
-        s = self.schema
-        return (s is not None and getattr(s, "kind", None) in (1, 2) and self.native and not self.return_info
-                and not self.drop_last and not self._process_overridden())
-
     def _fixed_stage(self, drv, native_ac: bool):
         s = self.schema
         prm = self._norm_params(s.row_elems)
@@ -1160,89 +890,6 @@ class DeviceLoader:
             state["delivered"] = True
             return 1, 0, item[0]
         return step
-
-    def _sync_commit(self, drv, debug: bool) -> None:
-        """``commit='sync'``: every finished batch's verdict, local store and -- through the
-        bridges -- the coordinator's OffsetCommit answer, before the next batch is handed out."""
-        t0 = time.perf_counter_ns()
-        drv.drain_fenced(True)
-        self._commit_native(drv, debug)
-        run = self._run
-        if run is not None and run.table is not None:
-            run.wait_worker_commits(30.0)  # each worker's consumer committed (and, bridged, forwarded)
-        self._sync_bridges(t0)
-
-    def _commit_logged(self, drv) -> None:
-        """One native commit bracketed by the reference's DEBUG messages (kafka_dataset.py:124-143).
-
-        With DEBUG enabled the native loops hand the commit back to Python (the step call is made
-        with its inline commit off), so "Committing offsets." precedes the store as it does in the
-        reference; without DEBUG the commit stays inside the one native step call.  With
-        ``commit_sink='worker'`` the workers commit and log ("Committing offsets on worker %d."), as
-        the reference's workers do, and the main process stays silent."""
-        if self._sink == "worker":
-            self._log_commit(drv.commit_pending(), False)
-            return
-        _ds_logger.debug("Committing offsets.")
-        self._log_commit(drv.commit_pending(), True)
-
-    def _commit_native(self, drv, debug: bool) -> None:
-        if debug:
-            self._commit_logged(drv)
-        else:
-            self._log_commit(drv.commit_pending(), False)
-
-    def _log_commit(self, status: int, debug: bool) -> None:
-        if status == -2:  # a device-parsed batch was malformed: it (and what follows) stays uncommitted
-            raise CorruptRecordException(self._run.driver.parse_error())
-        if status == -1:
-            _ds_logger.error("Commit failed.")
-        elif status == 1 and debug:
-            _ds_logger.debug("Committed offsets.")
-
-    def _absorb_driver_stats(self, drv) -> None:
-        st = drv.stats()
-        self.stats.worker_fill_ns += st["fill_ns"]
-        self.stats.worker_fills += st["fills"]
-        self.stats.wait_ns += st["blocked_ns"]
-        self.stats.ready_age_ns += st["ready_age_ns"]
-        self.stats.worker_idle_ns += st.get("worker_idle_ns", 0)
-        self.stats.worker_slot_wait_ns += st.get("worker_slot_wait_ns", 0)
-        self.stats.phase_commit_ns += st["phase_commit_ns"]
-        self.stats.phase_next_ns += st["phase_next_ns"]
-        self.stats.phase_launch_ns += st["phase_launch_ns"]
-        self.stats.phase_steps += st["phase_steps"]
-        self.stats.events += st["events"]
-        self.stats.batches += st.get("fast_batches", 0)
-        self.stats.records += st.get("fast_records", 0)
-        self.stats.issue_ns += st.get("fast_ns", 0)
-        self.stats.groups += st.get("groups", 0)
-        self.stats.coalesce_wait_ns += st.get("coalesce_wait_ns", 0)
-        self.stats.ahead_ns += st.get("ahead_ns", 0)
-        self.stats.json_width_wait_ns += st.get("json_width_wait_ns", 0)
-        self.stats.occ_handed += st.get("occ_handed", 0)
-        self.stats.occ_staged += st.get("occ_staged", 0)
-        self.stats.occ_samples += st.get("occ_samples", 0)
-        self.stats.release_ns += st.get("release_ns", 0)
-        self.stats.poll_ns += st.get("poll_ns", 0)
-        self.stats.polled += st.get("polled", 0)
-        self.stats.log_bytes_registered = st.get("log_bytes_registered", 0)
-        self.stats.log_bytes_unpinned = st.get("log_bytes_unpinned", 0)
-        self.stats.log_register_ns = st.get("log_register_ns", 0)
-        self.stats.mirror_bytes += st.get("mirror_bytes_copied", 0)
-        self.stats.mirror_copies += st.get("mirror_copies", 0)
-        self.stats.mirror_fallbacks += st.get("mirror_fallbacks", 0)
-        self.stats.verify_wait_ns += st.get("verify_wait_ns", 0)
-        self.stats.lockstep_agreements += st.get("lockstep_agreements", 0)
-        self.stats.lockstep_wait_ns += st.get("lockstep_wait_ns", 0)
-        self.stats.lockstep_step_wait_max_ns = max(self.stats.lockstep_step_wait_max_ns,
-                                                   st.get("lockstep_step_wait_max_ns", 0))
-        self.stats.commits += st["commits"]
-        self.stats.commit_failures += st["commit_failures"]
-        self.stats.commit_ns.extend(st["commit_ns"])
-        self.stats.commit_latency_ns.extend(st.get("commit_latency_ns", ()))
-        self._committed.update(dict(drv.committed()))
-        drv.reset_stats()
 
     def _next_item(self, run: _Run):
         """Returns (batch, watermarks) or None at end of stream."""
@@ -1464,110 +1111,7 @@ class DeviceLoader:
             self._norm = normalize_params(self.normalize, row, self.device)
         return self._norm
 
-    # ------------------------------------------------------------------ commits
-    def _broker(self):
-        from ..broker.synthetic import open_broker, resolve_url
-
-        return open_broker(resolve_url(self._servers))
-
-    def _sync_bridges(self, t0: int) -> None:
-        """commit='sync': waits for the coordinator's answer through every bridge this process
-        commits into -- the loader's own (bridge='auto') or, single-process, the dataset
-        consumer's (``KafkaDataset(topic, bootstrap_servers=cluster)``)."""
-        bridges = list(self._bridges)
-        if self.num_workers == 0:
-            bridges += getattr(getattr(self.dataset, "_consumer", None), "_bridges", None) or []
-        ok = True
-        for br in bridges:
-            if not br._closed:
-                ok = br.commit_sync() and ok
-        if not ok:
-            _ds_logger.error("Commit failed.")
-            self.stats.commit_failures += 1
-        self.stats.record_sync_commit(time.perf_counter_ns() - t0)
-
-    def _sync_commit_py(self) -> None:
-        """commit='sync' on the Python path: every finished batch stored (fences waited for) and,
-        through the bridges / the workers' consumers, answered by the coordinator."""
-        t0 = time.perf_counter_ns()
-        self._commit_finished(wait=True)
-        run = self._run
-        if run is not None and run.table is not None:
-            run.wait_worker_commits(30.0)
-        self._sync_bridges(t0)
-
-    def _commit_finished(self, wait: bool = False) -> None:
-        """Commits the watermarks of every batch the user finished (exactly those)."""
-        pending = self._pending_wms
-        if not pending:
-            return
-        offsets: dict[int, int] = {}
-        keep = []
-        started = []
-        for i, entry in enumerate(pending):
-            wms, ev = (entry[0], entry[1]) if isinstance(entry, tuple) else (entry, None)
-            if ev is not None and not wait and not ev.query():
-                # in order: a later batch is never committed before an earlier one (the committed
-                # offset must not go backwards when the earlier one completes)
-                keep.extend(pending[i:])
-                break
-            if ev is not None and wait:
-                ev.synchronize()
-            if isinstance(entry, tuple) and len(entry) > 2:
-                started.append(entry[2])
-            for pidx, _first, nxt, _cnt in wms:
-                if nxt > offsets.get(pidx, -1):
-                    offsets[pidx] = nxt
-        self._pending_wms[:] = keep
-        if offsets:
-            if self._commit(offsets):
-                now = time.perf_counter_ns()
-                for t in started:
-                    self.stats.record_commit_latency(now - t)
-
-    def _commit(self, offsets: dict[int, int]) -> bool:
-        if self._sink == "worker":
-            run = self._run
-            if run is None or run.table is None or run.closed:
-                raise RuntimeError("DeviceLoader commit_sink='worker': commit() must be called while iterating")
-            t0 = time.perf_counter_ns()
-            by_worker: dict[int, dict[int, int]] = {}
-            for p, o in offsets.items():
-                by_worker.setdefault(run.pidx_worker[p], {})[p] = o
-            for w, offs in by_worker.items():
-                run.table.publish(w, offs)  # that worker's consumer commits (and logs) them
-            self._committed.update(offsets)
-            self.stats.record_commit(time.perf_counter_ns() - t0)
-            return True
-        if self._group_id is None:
-            raise RuntimeError("DeviceLoader cannot commit: no group_id (pass it to init_worker or DeviceLoader)")
-        t0 = time.perf_counter_ns()
-        b = self._broker().native
-        g = b.group_index(self._group_id, True)
-        _ds_logger.debug("Committing offsets.")
-        ok = False
-        try:
-            b.commit(g, -1, 0, 0, [(p, int(o), "") for p, o in offsets.items()])
-        except COMMIT_FAILED_ERRORS:
-            _ds_logger.error("Commit failed.")
-            self.stats.commit_failures += 1
-        else:
-            _ds_logger.debug("Committed offsets.")
-            self._committed.update(offsets)
-            ok = True
-        self.stats.record_commit(time.perf_counter_ns() - t0)
-        return ok
-
-    def commit(self) -> None:
-        """Commits every batch yielded so far (manual mode)."""
-        run = self._run
-        if run is not None and run.driver is not None and not run.closed:
-            run.driver.finish_delivered(_stream_ptr(self.device))
-            run.driver.drain_fenced(True)
-            self._commit_logged(run.driver)
-            self._absorb_driver_stats(run.driver)
-        self._commit_finished(wait=True)
-
+    # ------------------------------------------------------------------ observability
     def ring_occupancy(self) -> dict:
         """Slots of the live iteration's ring by state: ``ready`` (published by a worker, not yet
         taken), ``inflight`` (taken by the main process: staged, collated ahead or still read by
@@ -1593,63 +1137,6 @@ class DeviceLoader:
         if run is not None and run.driver is not None and not run.closed:
             self._absorb_driver_stats(run.driver)
         return self.stats.summary()
-
-    def committed_offsets(self) -> dict[int, int]:
-        """{partition index: committed offset} of every partition this loader committed (live during
-        iteration: the native driver's commits are included)."""
-        run = self._run
-        if run is not None and run.driver is not None and not run.closed:
-            self._committed.update(dict(run.driver.committed()))
-        return dict(self._committed)
-
-    # ------------------------------------------------------------------ checkpoint / resume
-    def state_dict(self) -> dict:
-        """Committed positions for a model checkpoint (the committed offsets ARE the
-        checkpoint).  ``{"version": 1, "group_id": g, "offsets": {topic: {partition: offset}}}``
-        -- JSON-serialisable.  Under DDP each rank reports the partitions it consumed and committed;
-        save one per rank or all-gather them."""
-        b = self._broker()
-        offsets: dict[str, dict[int, int]] = {}
-        for pidx, off in sorted(self.committed_offsets().items()):
-            tp = b.tp_of(pidx)
-            offsets.setdefault(tp.topic, {})[tp.partition] = int(off)
-        return {"version": 1, "group_id": self._group_id, "offsets": offsets}
-
-    def load_state_dict(self, state: dict) -> None:
-        """Resumes from a checkpoint's offsets: they are committed for the group (an administrative
-        commit, as ``kafka-consumer-groups --reset-offsets`` does), so the next iteration's workers
-        start exactly there, like consumers restarting after a crash.  Call before iterating."""
-        from ..client.records import TopicPartition
-
-        if self._run is not None and not self._run.closed:
-            raise RuntimeError("load_state_dict() must be called before iterating the loader")
-        if int(state.get("version", 1)) != 1:
-            raise ValueError(f"unsupported DeviceLoader state version {state.get('version')}")
-        group = state.get("group_id") or self._group_id
-        if group is None:
-            raise RuntimeError("load_state_dict needs a group_id (in the state or the loader)")
-        offs = {TopicPartition(t, int(p)): int(o) for t, parts in state["offsets"].items() for p, o in parts.items()}
-        if self._bridges and offs:
-            # a replica of a Kafka cluster: the offsets are the cluster's -- commit them there, then
-            # mirror afresh from them (the replica may not hold those records any more)
-            from ..ops.native import core
-
-            servers, security = self._bridge_spec[0], self._bridge_spec[4]
-            client = core().WireClient(servers, "torchkafka-bridge", 30000, security)
-            for t in sorted({tp.topic for tp in offs}):
-                errs = client.offset_commit(group, t, {tp.partition: o for tp, o in offs.items() if tp.topic == t})
-                bad = {p: e for p, e in errs.items() if e}
-                if bad:
-                    raise KafkaError(f"CommitFailedError: load_state_dict could not commit {t} {bad} on {servers}")
-            url = self._bridges[0].url
-            for br in reversed(self._bridges):
-                br.close(flush=False)
-            self._bridges = []
-            self._start_bridges(url)
-        b = self._broker()
-        if offs:
-            b.commit(group, offs)
-        self._committed.update({b.pidx(tp.topic, tp.partition): o for tp, o in offs.items()})
 
     def close(self) -> None:
         if self._run is not None:
