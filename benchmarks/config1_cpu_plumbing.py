@@ -27,6 +27,32 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+def reference_loop_same_host(records: int = 40000, batch_size: int = 4) -> float:
+    """The reference's config-1 loop as SURVEY §6 measured it, on this host: an in-memory fake
+    consumer (zero broker cost) under the reference's KafkaDataset.__iter__ shape (process,
+    None-skip), torch's DataLoader (num_workers=0) and a no-op commit per batch.  The yardstick
+    above (108,521 rec/s) was measured on another host; this is the same loop here."""
+    import torch
+    from torch.utils.data import DataLoader, IterableDataset
+
+    class Fake(IterableDataset):
+        def __iter__(self):
+            for _ in range(records):
+                data = torch.rand(8)  # the README's _process
+                if data is not None:
+                    yield data
+
+        def commit(self):
+            pass
+
+    dl = DataLoader(Fake(), batch_size=batch_size)
+    n, t0 = 0, time.perf_counter()
+    for batch in dl:
+        n += batch.shape[0]
+        dl.dataset.commit()
+    return n / (time.perf_counter() - t0)
+
+
 def run(args) -> dict:
     import torch
     from torch.utils.data import DataLoader
@@ -64,9 +90,13 @@ def run(args) -> dict:
         assert b.committed("group_1", "topic", 0) == args.records
         ds.close()
         v = n / el
+        ref_here = reference_loop_same_host(batch_size=args.batch_size)
         return {"config": 1, "metric": "records/s (CPU plumbing, per-batch commit)", "value": round(v),
+                "reference_loop_same_host": round(ref_here), "vs_reference_loop_same_host": round(v / ref_here, 3),
                 "batch_size": args.batch_size, "records": n, "commits": commits, "timed_s": round(el, 4),
-                "path": "KafkaConsumer -> KafkaDataset._process -> torch DataLoader (num_workers=0) -> auto_commit",
+                "path": ("KafkaConsumer -> KafkaDataset._process -> auto_commit over a torch DataLoader "
+                         "(num_workers=0: its batch_size / collate_fn / drop_last, without the per-batch "
+                         "iterator overhead)"),
                 "vs_yardstick": round(v / YARDSTICK, 3)}
     finally:
         torch.set_num_threads(threads)
