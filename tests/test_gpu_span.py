@@ -358,3 +358,81 @@ def test_hbm_mirror_copies_across_pin_pieces(broker):
             assert torch.equal(b[o].cpu(), torch.tensor([synth_f32(0, o, j) for j in range(256)]))
     finally:
         big.destroy()
+
+
+@pytest.fixture
+def big_broker():
+    """A broker whose partition logs hold a few hundred MiB (the shared fixture's hold 64 MiB)."""
+    import uuid
+
+    from torchkafka_amd.broker import SyntheticBroker
+
+    b = SyntheticBroker.create(f"shm://tkbig-{os.getpid()}-{uuid.uuid4().hex[:8]}", log_capacity=1 << 30,
+                               index_capacity=1 << 18)
+    try:
+        yield b
+    finally:
+        b.destroy()
+
+
+def test_mirror_pins_only_up_to_the_chunk_holding_the_written_end(big_broker):
+    """h2d='dma' over a pre-filled log: the mirror's reads never make LogPins register past the
+    64 MiB piece that holds each partition's written end (the round-3 look-ahead registered up to
+    128 MiB of unwritten log on the launch thread)."""
+    from torchkafka_amd import FixedWidth
+
+    chunk = 64 << 20
+    big_broker.create_topic("t", 2)
+    big_broker.fill("t", 20000, "fixed_f32", size=1024, records_per_batch=32)  # ~82 MB per partition
+    DS = _dataset(FixedWidth(torch.float32, (1024,)))
+    written = [big_broker.native.log_bytes(big_broker.pidx("t", p)) for p in range(2)]
+    x, dl = _run(big_broker, "t", DS, "device", 256, "gp", num_workers=2, h2d="dma")
+    assert dl.plan.mirror and x.shape == (40000, 1024)
+    want = sum((w + chunk - 1) // chunk * chunk for w in written)
+    assert dl.stats.log_bytes_registered <= want, (dl.stats.log_bytes_registered, want, written)
+
+
+def test_growing_log_is_pinned_off_the_launch_thread(big_broker):
+    """A live tail: records keep arriving while the loader decodes them from the pinned logs.  The
+    pin thread registers each new 64 MiB piece as the written end reaches it; every record arrives
+    exactly once and the launch thread's wait for pinning stays a small part of the run."""
+    import threading
+    import time
+
+    from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
+
+    big_broker.create_topic("t", 2)
+    big_broker.fill("t", 2000, "fixed_f32", size=1024, records_per_batch=50)
+    DS = _dataset(FixedWidth(torch.float32, (1024,)))
+    stop = threading.Event()
+    rounds = 60
+
+    def produce():  # ~8 MB per partition per round: the logs cross several 64 MiB pieces
+        for _ in range(rounds):
+            big_broker.fill("t", 2000, "fixed_f32", size=1024, records_per_batch=50)
+            time.sleep(0.01)
+        stop.set()
+
+    th = threading.Thread(target=produce)
+    th.start()
+    dl = DeviceLoader(DS.placeholder(), 256, num_workers=2, device="cuda:0", dtype=torch.float32,
+                      worker_init_fn=DS.init_worker("t", bootstrap_servers=big_broker.url, group_id="gl",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=1500))
+    t0 = time.perf_counter()
+    seen = 0
+    last = {}
+    for x in auto_commit(dl):
+        rows = x[:, :2].long().cpu()
+        seen += rows.shape[0]
+        for p in (0, 1):
+            o = rows[rows[:, 1] == p][:, 0]
+            if o.numel():
+                assert int(o[0]) == last.get(p, -1) + 1  # in order, nothing skipped or repeated
+                last[p] = int(o[-1])
+    el = time.perf_counter() - t0
+    th.join()
+    st = dl.stats_summary()
+    total = 2000 * (rounds + 1)
+    assert seen == 2 * total and last == {0: total - 1, 1: total - 1}
+    assert st["log_pin_ms"] > 0 and dl.stats.log_bytes_registered >= 2 * (total * 4096 // (64 << 20)) * (64 << 20)
+    assert st["log_pin_wait_ms"] < 0.25 * el * 1e3, (st["log_pin_wait_ms"], el)

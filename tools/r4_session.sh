@@ -61,6 +61,10 @@ for s in ${STEPS:-smoke benchdrv}; do
     pytestnew) run pytest_new 600 python -u -m pytest tests/test_gpu_sync_lockstep.py tests/test_gpu_span.py tests/test_gpu_loader.py tests/test_multirank_launch.py -k "sync or verify or parse_error or launcher" -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     pytestrccl) run pytest_rccl 300 python -u -m pytest tests/test_zz_gpu_rccl.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     benchverify) run bench_verify_commit 600 python bench.py --verify commit --steps 200 --warmup 50 --steady-steps 50000 --extra-blocks "" --bridge-steps 0 ;;
+    pytestpin) run pytest_pin 600 python -u -m pytest tests/test_gpu_span.py -k "pins_only or growing_log or mirror" -x -v -p no:cacheprovider --timeout 180 --timeout-method thread ;;
+    c4mirror) for rep in $(seq 1 "${REPS:-12}"); do run c4_dma_$rep 200 python benchmarks/config4_json_varlen.py --h2d dma; grep -o '"value": [0-9]*' "$OUT/c4_dma_$rep.log"; grep -o '"log_pin_ms": [0-9.]*\|"log_pin_wait_ms": [0-9.]*\|"log_mib_pinned": [0-9.]*' "$OUT/c4_dma_$rep.log" | tr '\n' ' '; echo; done ;;
+    c4zc) for rep in $(seq 1 "${REPS:-12}"); do run c4_zc_$rep 200 python benchmarks/config4_json_varlen.py; grep -o '"value": [0-9]*' "$OUT/c4_zc_$rep.log"; done ;;
+    tokens) run tokens_zc 300 python benchmarks/varlen_tokens.py && run tokens_dma 300 python benchmarks/varlen_tokens.py --h2d dma ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

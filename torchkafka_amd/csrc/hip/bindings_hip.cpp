@@ -336,6 +336,7 @@ PYBIND11_MODULE(_tkhip, m) {
                s["mirror_device_bytes"] = m->device_bytes();
              }
              s["log_register_ns"] = d.log_register_ns();
+             s["log_register_wait_ns"] = d.log_register_wait_ns();
              s["lockstep_agreements"] = d.lockstep_agreements();
              s["lockstep_wait_ns"] = d.lockstep_wait_ns();
              s["lockstep_step_wait_max_ns"] = d.lockstep_step_wait_max_ns();

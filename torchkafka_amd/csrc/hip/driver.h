@@ -185,6 +185,7 @@ class MainDriver {
   uint64_t log_bytes_registered() const { return pins_->bytes_registered(); }
   uint64_t log_bytes_unpinned() const { return pins_->bytes_unpinned(); }
   int64_t log_register_ns() const { return pins_->register_ns(); }
+  int64_t log_register_wait_ns() const { return pins_->register_wait_ns(); }
   int coalesce() const { return coalesce_; }
   int64_t groups() const { return groups_; }
 

@@ -1,6 +1,7 @@
 #include "log_pins.h"
 
 #include <algorithm>
+#include <chrono>
 #include <stdexcept>
 
 namespace tkh {
@@ -9,13 +10,21 @@ static_assert(LogPins::kChunk == LogMirror::kRegAlign, "mirror copies split at t
 
 LogPins::LogPins(Engine* engine, std::shared_ptr<tk::Broker> broker) : eng_(engine), broker_(std::move(broker)) {
   if (broker_) {
-    reg_end_.assign(broker_->meta().max_partitions, 0);
-    reg_ranges_.resize(broker_->meta().max_partitions);
+    n_parts_ = broker_->meta().max_partitions;
+    reg_end_ = std::make_unique<std::atomic<uint64_t>[]>(n_parts_);
+    for (uint32_t i = 0; i < n_parts_; ++i) reg_end_[i].store(0, std::memory_order_relaxed);
+    reg_ranges_.resize(n_parts_);
     release_consumed_ = (broker_->flags() & tk::kReleaseConsumed) != 0;
   }
 }
 
 LogPins::~LogPins() {
+  {
+    std::lock_guard<std::mutex> l(pm_);
+    stop_ = true;
+  }
+  pcv_.notify_all();
+  if (pin_thread_.joinable()) pin_thread_.join();
   mirror_.reset();  // its copies read the pinned logs: before they are unregistered
   // the kernels that read the ranges completed (slots drained by the caller)
   bool any = false;
@@ -30,10 +39,9 @@ LogPins::~LogPins() {
 }
 
 void LogPins::enable_direct() {
-  if (!broker_) throw std::runtime_error("DeviceLoader h2d='direct' needs the synthetic broker (group_id + URL)");
+  if (!broker_) throw std::runtime_error("DeviceLoader h2d='dma' direct needs the synthetic broker (group_id + URL)");
   if (bases_dev_) return;
-  const uint32_t np = broker_->meta().max_partitions;
-  reg_end_.assign(np, 0);
+  const uint32_t np = n_parts_;
   if (hipMalloc(reinterpret_cast<void**>(&bases_dev_), size_t(np) * sizeof(uint64_t)) != hipSuccess)
     throw std::runtime_error("driver: hipMalloc(log base table) failed");
   if (hipMemset(bases_dev_, 0, size_t(np) * sizeof(uint64_t)) != hipSuccess)
@@ -49,29 +57,28 @@ void LogPins::pin_written(const std::vector<uint32_t>& pidxs) {
   if (!broker_) return;
   eng_->prepare_decode();
   for (uint32_t p : pidxs) {
-    if (p >= reg_end_.size()) continue;
+    if (p >= n_parts_) continue;
     const uint64_t written = broker_->part(p).log_end_pos.load(std::memory_order_acquire);
     if (written) ensure(p, written);
   }
 }
 
-void LogPins::ensure(uint32_t pidx, uint64_t end) {
-  if (pidx >= reg_end_.size()) throw std::out_of_range("driver: partition index beyond the broker's table");
-  if (end <= reg_end_[pidx]) return;
-  const int64_t t0 = tk::now_ns();
-  const uint8_t* base = broker_->log_base(pidx);
+bool LogPins::pin_some(uint32_t pidx, uint64_t end, bool one_piece) {
+  std::lock_guard<std::mutex> l(reg_m_);
+  const uint64_t lo = reg_end_[pidx].load(std::memory_order_relaxed);
   auto& part = broker_->part(pidx);
   const uint64_t cap = part.log_capacity;
   if (end > cap) throw std::runtime_error("driver: slot references bytes beyond the partition log");
-  // Everything already written (a retained backlog is pinned once, at its first use), then whole
-  // chunks, so a growing log pays one registration per 64 MiB.  Pinning costs ~13 GB/s of fresh
-  // shm pages on the MI355X host (profiles/*/register_probe2.log): it is what bounds this mode
-  // on a log that grows faster than that.
+  // Everything already written, then whole chunks, so a growing log pays one registration per
+  // 64 MiB (and a mirror never copies across two registrations).  What is pinned past the written
+  // end is at most the rest of the chunk the end falls in -- fresh pages of the sparse file.
   const uint64_t written = part.log_end_pos.load(std::memory_order_acquire);
   uint64_t hi = (std::max(end, written) + kChunk - 1) / kChunk * kChunk;
   if (hi > cap) hi = cap;
-  const uint64_t lo = reg_end_[pidx];
-  if (reg_ranges_.size() <= pidx) reg_ranges_.resize(size_t(pidx) + 1);
+  if (one_piece) hi = std::min(hi, lo + kChunk);
+  if (hi <= lo) return false;
+  const int64_t t0 = tk::now_ns();
+  const uint8_t* base = broker_->log_base(pidx);
   if (reg_ranges_[pidx].empty()) {  // announce the pin before it exists (the replicator reads these)
     part.pin_floor.store(lo, std::memory_order_release);
     part.pinned.fetch_add(1, std::memory_order_acq_rel);
@@ -85,7 +92,7 @@ void LogPins::ensure(uint32_t pidx, uint64_t end) {
     reg_ranges_[pidx].emplace_back(p, b);
     void* dp = nullptr;
     if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess || dp != p)
-      throw std::runtime_error("driver: h2d='direct' needs device addresses of pinned host memory to equal host "
+      throw std::runtime_error("driver: device decode needs device addresses of pinned host memory to equal host "
                                "addresses (unified addressing)");
   }
   if (lo == 0 && bases_dev_) {
@@ -93,9 +100,83 @@ void LogPins::ensure(uint32_t pidx, uint64_t end) {
     if (hipMemcpy(bases_dev_ + pidx, &b, sizeof(b), hipMemcpyHostToDevice) != hipSuccess)
       throw std::runtime_error("driver: log base table update failed");
   }
-  reg_end_[pidx] = hi;
+  reg_end_[pidx].store(hi, std::memory_order_release);
   reg_total_ += hi - lo;
   reg_ns_ += tk::now_ns() - t0;
+  return true;
+}
+
+void LogPins::ensure(uint32_t pidx, uint64_t end) {
+  if (pidx >= n_parts_) throw std::out_of_range("driver: partition index beyond the broker's table");
+  if (end <= reg_end_[pidx].load(std::memory_order_acquire)) return;
+  if (end > broker_->part(pidx).log_capacity)
+    throw std::runtime_error("driver: slot references bytes beyond the partition log");
+  if (bases_dev_ || reg_end_[pidx].load(std::memory_order_acquire) == 0) {
+    // the first pin of a log (its retained backlog, before any batch of it) and h2d='direct'
+    // (experimental) register here; afterwards the pin thread follows the log as it grows
+    pin_some(pidx, end, false);
+    if (!bases_dev_) {
+      std::lock_guard<std::mutex> l(pm_);
+      tracked_.insert(pidx);
+      if (!pin_thread_.joinable()) pin_thread_ = std::thread([this] { pin_loop(); });
+    }
+    return;
+  }
+  const int64_t t0 = tk::now_ns();
+  std::unique_lock<std::mutex> l(pm_);
+  uint64_t& d = demand_[pidx];
+  d = std::max(d, end);
+  pcv_.notify_one();
+  done_cv_.wait(l, [&] { return reg_end_[pidx].load(std::memory_order_acquire) >= end || !err_.empty(); });
+  wait_ns_ += tk::now_ns() - t0;
+  if (reg_end_[pidx].load(std::memory_order_acquire) < end) throw std::runtime_error(err_);
+}
+
+// The pin thread: demands first (the launch thread is waiting), then one chunk for any tracked
+// partition whose written end has passed its pinned end; otherwise a 1 ms nap.
+void LogPins::pin_loop() {
+  std::unique_lock<std::mutex> l(pm_);
+  while (!stop_) {
+    uint32_t pidx = UINT32_MAX;
+    uint64_t want = 0;
+    for (auto it = demand_.begin(); it != demand_.end();) {
+      if (reg_end_[it->first].load(std::memory_order_acquire) >= it->second) {
+        it = demand_.erase(it);
+      } else {
+        pidx = it->first;
+        want = it->second;
+        break;
+      }
+    }
+    if (pidx == UINT32_MAX) {
+      for (uint32_t p : tracked_) {
+        const uint64_t w = broker_->part(p).log_end_pos.load(std::memory_order_acquire);
+        if (w > reg_end_[p].load(std::memory_order_acquire)) {
+          pidx = p;
+          want = w;
+          break;
+        }
+      }
+    }
+    if (pidx == UINT32_MAX) {
+      pcv_.wait_for(l, std::chrono::milliseconds(1));
+      continue;
+    }
+    l.unlock();
+    std::string err;
+    try {
+      pin_some(pidx, want, true);
+    } catch (const std::exception& e) {
+      err = e.what();
+    }
+    l.lock();
+    if (!err.empty()) {
+      err_ = err;
+      done_cv_.notify_all();
+      return;
+    }
+    done_cv_.notify_all();
+  }
 }
 
 const uint8_t* LogPins::seg_src(const tk::SpanSeg& sg, bool* hbm) {
@@ -104,15 +185,18 @@ const uint8_t* LogPins::seg_src(const tk::SpanSeg& sg, bool* hbm) {
   // a ring log (KafkaBridge replica) writes over its chunks: an HBM mirror of them would go stale,
   // so its segments are read zero-copy
   if (mirror_ && broker_->part(sg.pidx).ring_bytes.load(std::memory_order_relaxed) == 0) {
-    // pin ahead of the segment so the mirror can copy (and prefetch) whole chunks -- of what is
-    // written only: the mirror never copies past it, and registering fresh pages of the log beyond
-    // it stalled this thread for 20-28 ms (128 MiB) in the only two config-4 runs that collapsed
-    // (profiles/r03_final/c4_auto_mirror_trial/c4_6.log, profiles/r03_s3/mirror_stability/)
+    // pin ahead of the segment so the mirror can copy (and prefetch) whole chunks.  No look-ahead
+    // past the written end: the mirror never copies past it.  (A growing log still gets whole
+    // chunks registered -- up to the next 64 MiB boundary -- but by the pin thread, not here.)
+    // The look-ahead this replaced registered up to 128 MiB of unwritten log on the launch thread
+    // (20-28 ms) in the two config-4 mirror runs that collapsed in round 3 (profiles/r03_final/
+    // c4_auto_mirror_trial/c4_6.log, profiles/r03_s3/mirror_stability/); whether that was the
+    // cause is for the re-measurement in profiles/r04_* to show.
     const auto& part = broker_->part(sg.pidx);
     const uint64_t written = part.log_end_pos.load(std::memory_order_acquire);
     ensure(sg.pidx, std::min<uint64_t>(std::max<uint64_t>(written, sg.log_pos + sg.len),
                                        sg.log_pos + mirror_->span_bytes()));
-    const uint8_t* m = mirror_->map(sg.pidx, sg.log_pos, sg.len, log, std::min<uint64_t>(reg_end_[sg.pidx], written));
+    const uint8_t* m = mirror_->map(sg.pidx, sg.log_pos, sg.len, log, std::min<uint64_t>(pinned_end(sg.pidx), written));
     if (m) {
       *hbm = true;
       return m;
@@ -131,6 +215,7 @@ void LogPins::committed(const std::unordered_map<uint32_t, int64_t>& committed) 
 // its decode verdict.
 void LogPins::release_consumed(const std::unordered_map<uint32_t, int64_t>& committed) {
   commits_since_release_ = 0;
+  std::lock_guard<std::mutex> l(reg_m_);
   for (const auto& kv : committed) {
     const uint32_t pidx = kv.first;
     if (pidx >= reg_ranges_.size() || reg_ranges_[pidx].size() < 2) continue;  // keep the range being read

@@ -103,6 +103,7 @@ class LoaderCommits:
         self.stats.log_bytes_registered = st.get("log_bytes_registered", 0)
         self.stats.log_bytes_unpinned = st.get("log_bytes_unpinned", 0)
         self.stats.log_register_ns = st.get("log_register_ns", 0)
+        self.stats.log_register_wait_ns = st.get("log_register_wait_ns", 0)
         self.stats.mirror_bytes += st.get("mirror_bytes_copied", 0)
         self.stats.mirror_copies += st.get("mirror_copies", 0)
         self.stats.mirror_fallbacks += st.get("mirror_fallbacks", 0)

@@ -57,6 +57,7 @@ class LoaderStats:
     log_bytes_registered: int = 0  # h2d="direct": broker log bytes pinned in place so far
     log_bytes_unpinned: int = 0    # replica logs: consumed ranges unpinned again (kReleaseConsumed)
     log_register_ns: int = 0
+    log_register_wait_ns: int = 0     # the launch thread waiting for the pin thread (growing logs)
     mirror_bytes: int = 0     # h2d="dma" device decode: log bytes copied into the HBM mirror (SDMA)
     mirror_copies: int = 0
     mirror_fallbacks: int = 0  # segments read from the pinned log instead (buffer busy)
@@ -122,6 +123,7 @@ class LoaderStats:
             "log_mib_pinned": self.log_bytes_registered / 2**20,
             "log_mib_unpinned": self.log_bytes_unpinned / 2**20,
             "log_pin_ms": self.log_register_ns / 1e6,
+            "log_pin_wait_ms": self.log_register_wait_ns / 1e6,
             "mirror_mib_copied": self.mirror_bytes / 2**20,
             "mirror_copies": self.mirror_copies,
             "mirror_fallbacks": self.mirror_fallbacks,
