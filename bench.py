@@ -104,19 +104,20 @@ def parse():
     ap.add_argument("--steady-steps", type=int, default=None,
                     help="steps of the steady-state block timed after the headline (default: max(50 x ring "
                          "slots, 50000) on a GPU, 2000 on the CPU; 0 skips it)")
-    ap.add_argument("--extra-blocks", default="dma,f32,label",
-                    help="comma list of secondary steady blocks, each a fresh loader: dma (h2d='dma', HBM "
-                         "mirror filled by SDMA), f32 (float32 output), label (the record key as an int64 "
-                         "label beside the values: FixedWidth + Key()); '' for none")
+    ap.add_argument("--extra-blocks", default="dma,f32,label,rccl,verify",
+                    help="comma list of secondary steady blocks, each a fresh loader over the same topic: dma "
+                         "(h2d='dma', HBM mirror filled by SDMA), f32 (float32 output), label (the record key as "
+                         "an int64 label beside the values: FixedWidth + Key()), rccl (the native RCCL lockstep "
+                         "forced at N = 1: the RCCL cost a one-GPU box shows), verify (the other --verify mode: "
+                         "steady_unverified or steady_verified); '' for none")
     ap.add_argument("--extra-steps", type=int, default=None,
                     help="timed steps of each secondary block (default: the steady-state steps)")
     ap.add_argument("--self-launch", action="store_true",
                     help="start the rank processes from this process even at --gpus 1 / --same-device (the "
                          "launcher path the N > 1 runs take without torchrun)")
-    ap.add_argument("--config-blocks", default="config4,config5,config1,rccl",
-                    help="comma list of BASELINE-config blocks run at N = 1: config4 (JSON -> bf16), config5 "
-                         "(1 MiB records, 128 partitions), config1 (CPU plumbing), rccl (steady state with the "
-                         "native RCCL lockstep forced at world 1); '' for none")
+    ap.add_argument("--config-blocks", default="config4,config5,config1",
+                    help="comma list of BASELINE-config blocks run at N = 1, each on a broker of its own: config4 "
+                         "(JSON -> bf16), config5 (1 MiB records, 128 partitions), config1 (CPU plumbing); '' for none")
     ap.add_argument("--config4-steps", type=int, default=20000)
     ap.add_argument("--config5-steps", type=int, default=1000)
     ap.add_argument("--config1-records", type=int, default=100000)
@@ -328,6 +329,7 @@ def steady_block(R: Rank, res: dict, steps: int, dim: int) -> dict:
         "commit_latency_p99_us": round(st["commit_latency_p99_us"], 2),
         "commits": st["commits"],
         "worker_fill_us_per_batch": round(st.get("worker_fill_us_per_batch", 0.0), 2),
+        "verify_wait_us_per_batch": round(st.get("verify_wait_us_per_batch", 0.0), 3),
     }
     if R.world > 1:
         out["per_rank_records_per_s"] = [round(r / e, 1) for e, r in res["per_rank"]]
@@ -399,65 +401,11 @@ def run_config_blocks(R: "Rank", args) -> dict:
         elif name == "config1":
             m = importlib.import_module("config1_cpu_plumbing")
             res = m.run(m.parse(["--records", str(args.config1_records)]))
-        elif name == "rccl" and on_gpu:
-            res = rccl_steady_block(R, args)
         else:
             continue
         res["block_wall_s"] = round(time.perf_counter() - t0, 2)
-        out[name if name != "rccl" else "steady_rccl"] = res
+        out[name] = res
     return out
-
-
-def rccl_steady_block(R: "Rank", args) -> dict:
-    """config 2's loader with the native RCCL lockstep forced at world 1 (lockstep='always' on a
-    world-1 nccl group): one all-reduce(MIN) agreement over the private RCCL communicator every
-    ``lockstep_depth`` steps -- the RCCL cost a one-GPU box can show."""
-    torch, dist = R.torch, R.dist
-    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
-    from torchkafka_amd.broker import SyntheticBroker
-
-    class Records(KafkaDataset):
-        schema = FixedWidth(torch.float32, (args.dim,))
-
-    url = f"shm://tkbench-rccl-{os.getpid()}"
-    B, steps, warm = args.batch_size, 50000, 200
-    n_parts = args.partitions_per_gpu
-    per_part = int(math.ceil((steps + warm + args.workers * 18) * B * 1.25 / n_parts)) + B
-    broker = SyntheticBroker.create(url, log_capacity=1 << 34, index_capacity=1 << 22)
-    own_group = not dist.is_initialized()
-    try:
-        broker.create_topic("bench", n_parts)
-        broker.fill("bench", per_part, "fixed_f32", size=args.dim, records_per_batch=args.records_per_batch,
-                    threads=min(16, n_parts), keyed=True)
-        if own_group:
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ["MASTER_PORT"] = str(_free_port())
-            dist.init_process_group("nccl", rank=0, world_size=1)  # lazy: no torch RCCL comm (streams) is made
-        dtypes = {"bf16": torch.bfloat16, "fp8": torch.float8_e4m3fn, "f16": torch.float16, "f32": torch.float32}
-        ld = DeviceLoader(Records.placeholder(), B, num_workers=args.workers, device=R.device,
-                          dtype=dtypes[args.dtype], prefetch=args.prefetch, lockstep="always",
-                          lockstep_depth=args.lockstep_depth, coalesce=args.coalesce,
-                          coalesce_wait_us=args.coalesce_wait_us, numa_bind=not args.no_numa, verify=args.verify,
-                          worker_init_fn=Records.init_worker("bench", bootstrap_servers=url, group_id="bench-rccl",
-                                                             auto_offset_reset="earliest"))
-        it = iter(auto_commit(ld))
-        for _ in range(warm):
-            next(it)
-        res = time_steps(R, it, steps, ld)
-        blk = steady_block(R, res, steps, args.dim)
-        st = res["stats"]
-        blk["lockstep"] = dict(ld.lockstep_info)
-        blk["lockstep_agreements"] = st.get("lockstep_agreements", 0)
-        blk["lockstep_wait_us_per_step"] = round(st.get("lockstep_wait_us_per_batch", 0.0), 3)
-        blk["lockstep_step_wait_max_us"] = round(st.get("lockstep_step_wait_max_us", 0.0), 1)
-        blk["streams"] = ld.stream_plan()
-        it.close()
-        ld.close()
-        return blk
-    finally:
-        if own_group and dist.is_initialized():
-            dist.destroy_process_group()
-        broker.destroy()
 
 
 def run_rank(args) -> int:
@@ -508,7 +456,9 @@ def run_rank(args) -> int:
               else max(50 * ring_guess, 50000) if device.type == "cuda" else 2000)
     extra = [b for b in args.extra_blocks.split(",") if b]
     if device.type != "cuda":
-        extra = [b for b in extra if b != "dma"]
+        extra = [b for b in extra if b not in ("dma", "rccl", "verify")]
+    if world > 1:  # the main blocks run the lockstep already (RCCL on GPUs)
+        extra = [b for b in extra if b != "rccl"]
     extra_steps = args.extra_steps if args.extra_steps is not None else steady
     if extra_steps <= 0:
         extra = []
@@ -538,14 +488,16 @@ def run_rank(args) -> int:
 
     R.init_group()
 
-    def make_loader(group: str, dtype, h2d: str, servers: str = url, commit: str = "async", ds=Records):
+    def make_loader(group: str, dtype, h2d: str, servers: str = url, commit: str = "async", ds=Records,
+                    verify: str | None = None, lockstep_mode=None):
         return DeviceLoader(
             ds.placeholder(), B, num_workers=args.workers, device=device, dtype=dtype,
             slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
             in_order=args.in_order, h2d=h2d, copy_streams=args.copy_streams, lockstep_depth=args.lockstep_depth,
             event_every=args.event_every, numa_bind=not args.no_numa, coalesce=args.coalesce,
-            coalesce_wait_us=args.coalesce_wait_us, decode=args.decode, lockstep=lockstep,
-            mirror_chunk_mib=args.mirror_chunk_mib, commit=commit, verify=args.verify,
+            coalesce_wait_us=args.coalesce_wait_us, decode=args.decode,
+            lockstep=lockstep if lockstep_mode is None else lockstep_mode,
+            mirror_chunk_mib=args.mirror_chunk_mib, commit=commit, verify=verify or args.verify,
             **({"mirror_chunks": args.mirror_chunks} if args.mirror_chunks else {}),
             worker_init_fn=ds.init_worker("bench", bootstrap_servers=servers, group_id=group,
                                           auto_offset_reset="earliest", check_crcs=not args.no_crc),
@@ -596,10 +548,21 @@ def run_rank(args) -> int:
 
     # secondary blocks: fresh loaders (own consumer groups) over the same retained topic
     extra_out = {}
+    other_verify = "commit" if args.verify == "deliver" else "deliver"
     for name in extra:
         dt = torch.float32 if name == "f32" else dtypes[args.dtype]
+        own_group = False
+        if name == "rccl" and not dist.is_initialized():
+            # a world-1 nccl group, lazily initialised: torch creates no RCCL communicator of its own;
+            # the loader's private one carries every agreement
+            os.environ["MASTER_ADDR"] = "127.0.0.1"
+            os.environ["MASTER_PORT"] = str(_free_port())
+            dist.init_process_group("nccl", rank=0, world_size=1)
+            own_group = True
         ld = make_loader(f"bench-{name}", dt, "dma" if name == "dma" else args.h2d,
-                         ds=Labelled if name == "label" else Records)
+                         ds=Labelled if name == "label" else Records,
+                         verify=other_verify if name == "verify" else None,
+                         lockstep_mode="always" if name == "rccl" else None)
         eit = iter(auto_commit(ld))
         for _ in range(extra_warm):
             next(eit)
@@ -611,9 +574,22 @@ def run_rank(args) -> int:
         blk = steady_block(R, eres, extra_steps, args.dim)
         blk["dtype"] = "f32" if name == "f32" else args.dtype
         blk["h2d"], blk["decode"] = describe(ld)
-        extra_out[f"steady_{name}"] = blk
+        blk["verify"] = ld.verify
+        key = f"steady_{name}"
+        if name == "rccl":
+            st = eres["stats"]
+            blk["lockstep"] = dict(ld.lockstep_info)
+            blk["lockstep_agreements"] = st.get("lockstep_agreements", 0)
+            blk["lockstep_wait_us_per_step"] = round(st.get("lockstep_wait_us_per_batch", 0.0), 3)
+            blk["lockstep_step_wait_max_us"] = round(st.get("lockstep_step_wait_max_us", 0.0), 1)
+        if name == "verify":
+            key = "steady_unverified" if ld.verify == "commit" else "steady_verified"
+            blk["verify_wait_us_per_batch"] = round(eres["stats"].get("verify_wait_us_per_batch", 0.0), 3)
+        extra_out[key] = blk
         eit.close()
         ld.close()
+        if own_group:
+            dist.destroy_process_group()
         if world > 1:
             R.barrier()
 
@@ -690,6 +666,8 @@ def run_rank(args) -> int:
                 "parallelism": f"dp{world}",
                 "partitions": n_parts,
                 "num_workers": args.workers,
+                "verify": ("deliver (a batch is handed out after its device CRC32C verdict)" if args.verify == "deliver"
+                           else "commit (the CRC32C verdict gates the commit only)"),
                 "commit": "auto_commit per batch" + (
                     "" if not lock_info else ", RCCL lockstep" if lock_info.get("transport") == "rccl"
                     else f", lockstep ({lock_info.get('backend', 'host')} all-reduce)"),
