@@ -36,3 +36,12 @@ def test_example_07_labels_and_sync_commits_on_cpu():
     assert r.returncode == 0, r.stderr[-3000:]
     assert "4000 labelled records on cpu, 0 label mismatches" in r.stdout
     assert "{0: 2000, 1: 2000}" in r.stdout
+
+
+def test_example_08_rebalance_listener():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "examples", "08_rebalance_listener.py")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = r.stdout.splitlines()
+    assert "worker 0: revoked []" in lines and "main: assigned [3]" in lines  # the visitor took a partition
+    assert lines[-1] == "12000 records delivered; committed {0: 3000, 1: 3000, 2: 3000, 3: 3000}"
