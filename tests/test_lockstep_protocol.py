@@ -69,7 +69,10 @@ def _rank_main(rank, world, port, outdir, totals, cap, depth, slow_rank, die_ran
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=8))
+    # a short timeout only where a peer dies on purpose (the survivors must fail, not hang); elsewhere
+    # room for slow rank start-up under a loaded test machine (the store waits for rank 0)
+    secs = 8 if die_rank >= 0 else 60
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=secs))
     buf = torch.zeros(3, dtype=torch.int64)
 
     def allreduce_min(a, b, c):

@@ -12,7 +12,9 @@ run() {  # run <name> <timeout> <cmd...>
   local rc=$?
   tail -n 12 "$OUT/$name.log" | cut -c1-1500
   echo "=== $name rc=$rc"
-  [ $rc -ne 0 ] && exit $rc
+  # a failed test or bench is recorded and the session goes on; a crash, abort or time limit
+  # (124/134/137/139) ends it: nothing more touches the GPU after a fault
+  case $rc in 0) ;; 124|134|137|139) exit $rc ;; *) FAILED="$FAILED $name" ;; esac
   return 0
 }
 prof() {  # prof <name> <timeout> <rocprofv3 args...> -- <program...>   (kernel trace + stats only)
@@ -36,6 +38,8 @@ pmc() {  # pmc <name> <seconds> <counters...> -- <program...>   (counters only, 
   return 0
 }
 R=$PWD
+FAILED=""
+trap 'echo "=== failed steps:${FAILED:- none}"' EXIT
 for s in ${STEPS:-smoke benchdrv}; do
   case $s in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;

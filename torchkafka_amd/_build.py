@@ -145,7 +145,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> Path:
     src_dir = CSRC / "hip"
     core_dir = CSRC / "core"
     # the main-process step driver embeds the host core (ring, broker) to commit natively
-    core_srcs = [p for p in sorted(core_dir.glob("*.cpp")) if p.name != "bindings.cpp"]
+    core_srcs = [p for p in sorted(core_dir.glob("*.cpp")) if not p.name.startswith("bindings")]
     srcs = sorted(src_dir.glob("*.hip")) + sorted(src_dir.glob("*.cpp")) + core_srcs
     out = hip_target()
     if not force and up_to_date("hip"):
