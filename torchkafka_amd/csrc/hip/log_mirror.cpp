@@ -22,6 +22,8 @@ LogMirror::LogMirror(int device, uint64_t chunk_bytes, int chunks_per_partition,
   prefetch_ = K_ > 3 ? K_ - 2 : 1;
   stride_ = (chunk_ + tk::kSpanSegMax + 256 + 4095) / 4096 * 4096;
   TKM_CHECK(hipSetDevice(device_));
+  const char* w = std::getenv("TORCHKAFKA_MIRROR_WAIT");
+  wait_ = w && w[0] == '1';
   const char* e = std::getenv("TORCHKAFKA_MIRROR_COPY_STREAMS");
   const int n = copy_streams > 0 ? copy_streams : e ? std::atoi(e) : 2;
   cs_.resize(size_t(n < 1 ? 1 : n > 4 ? 4 : n));
@@ -119,6 +121,17 @@ const uint8_t* LogMirror::map(uint32_t pidx, uint64_t pos, uint32_t len, const u
     ++fallbacks_;
     return nullptr;
   }
+  if (!wait_ && b->copy_seq > cs_[size_t(b->s)].done) {
+    CopyStream& cs = cs_[size_t(b->s)];
+    if (!cs.queried) learn(cs);
+    if (b->copy_seq > cs.done) {
+      // its copy is still in flight: read the pinned log this time (the prefetches keep going)
+      ++fallbacks_;
+      ++pending_fallbacks_;
+      deferred_.push_back(Deferred{pidx, c, log, pinned});
+      return nullptr;
+    }
+  }
   if (!b->pending) {
     b->pending = true;
     pending_.emplace_back(pidx, int(c % K_));
@@ -139,7 +152,29 @@ void LogMirror::issue_prefetches() {
   deferred_.clear();
 }
 
+void LogMirror::learn(CopyStream& c) {
+  c.queried = true;
+  if (c.recorded > c.done && hipEventQuery(c.copied) == hipSuccess) c.done = c.recorded;
+  if (c.seq > c.recorded && c.recorded == c.done) {
+    TKM_CHECK(hipEventRecord(c.copied, c.stream));
+    c.recorded = c.seq;
+  }
+}
+
 void LogMirror::before(hipStream_t stream) {
+  if (!wait_) {
+    // every buffer this launch maps was found complete: nothing to wait for; queue the
+    // prefetches, then mark the copy streams' tails so their completion can be learned
+    issue_prefetches();
+    for (auto& c : cs_) {
+      if (c.seq > c.recorded && c.recorded == c.done) {
+        TKM_CHECK(hipEventRecord(c.copied, c.stream));
+        c.recorded = c.seq;
+      }
+      c.queried = false;
+    }
+    return;
+  }
   uint64_t need[4] = {0, 0, 0, 0};
   for (const auto& pb : pending_) {
     const Buf& b = parts_[pb.first].bufs[size_t(pb.second)];

@@ -14,6 +14,14 @@
 // overwritten only after the copy stream waited for the events of every decode stream that read
 // its previous chunk.  A segment whose buffer is still in use by the
 // group being formed is served from the pinned log instead (map() returns nullptr).
+//
+// A launch never waits for a copy (the default; TORCHKAFKA_MIRROR_WAIT=1 restores the waits): a
+// segment is served from HBM only once its chunk's copy is known complete, else from the pinned
+// log over PCIe while the copy engines catch up.  A copy stream's completion is learned from one
+// event at a time, re-recorded at its tail once the previous one completed.  Waiting instead made
+// a launch that caught up with the copies wait for the copy stream's whole queue -- the needed
+// chunk and every prefetch queued behind it (up to (K - 2) chunks per partition of that stream):
+// config-4 mirror runs then ranged 38-50 M rec/s on one box (profiles/r04_s1/c4_dma_*.log).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -54,6 +62,8 @@ class LogMirror {
   uint64_t bytes_copied() const { return bytes_; }
   uint64_t copies() const { return copies_; }
   uint64_t fallbacks() const { return fallbacks_; }
+  uint64_t pending_fallbacks() const { return pending_fallbacks_; }  // served from the log: copy in flight
+  void reset_stats() { bytes_ = copies_ = fallbacks_ = pending_fallbacks_ = 0; }
   uint64_t device_bytes() const { return dev_bytes_; }
 
  private:
@@ -101,7 +111,13 @@ class LogMirror {
     hipStream_t stream = nullptr;
     hipEvent_t copied = nullptr;  // recorded after the latest copy (when a launch needs it)
     uint64_t seq = 0, recorded = 0, done = 0;
+    bool queried = false;  // its event was queried for the launch being formed
   };
+  // no-wait mode: what the copy stream has completed (one query per launch), and a fresh event
+  // at its tail once the last one completed
+  void learn(CopyStream& c);
+  bool wait_ = false;
+  uint64_t pending_fallbacks_ = 0;
   std::vector<CopyStream> cs_;
   CopyStream& cs_of(uint32_t pidx) { return cs_[pidx % cs_.size()]; }
   std::vector<Part> parts_;

@@ -75,6 +75,7 @@ class LogPins {
     reg_total_ = 0;
     reg_ns_ = 0;
     wait_ns_ = 0;
+    if (mirror_) mirror_->reset_stats();
   }
 
  private:

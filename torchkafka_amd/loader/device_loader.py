@@ -747,7 +747,10 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
         try:
             import torch.distributed as dist
 
-            if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+            # torch makes its RCCL communicator (and streams) at a group's first collective: the
+            # lockstep never runs one on it, a DDP job's gradient all-reduce does (world > 1)
+            if (dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"
+                    and dist.get_world_size() > 1):
                 plan["torch_nccl"] = 1
         except Exception:  # noqa: BLE001
             pass
