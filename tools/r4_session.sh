@@ -72,7 +72,6 @@ for s in ${STEPS:-smoke benchdrv}; do
     c4wait) for rep in $(seq 1 "${REPS:-4}"); do TORCHKAFKA_MIRROR_WAIT=1 run c4_wait_$rep 200 python benchmarks/config4_json_varlen.py --h2d dma; grep -o '"value": [0-9]*' "$OUT/c4_wait_$rep.log"; done ;;
     c5ab) for rep in 1 2; do run c5_deliver_$rep 200 python benchmarks/config5_large_messages.py && run c5_commit_$rep 200 python benchmarks/config5_large_messages.py --verify commit; done ;;
     pytestgpu) run pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 180 --timeout-method thread ;;
-    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
