@@ -90,6 +90,8 @@ const std::map<int16_t, ApiRange>& client_versions();
 // What it sends to a broker that does not answer ApiVersions.
 int16_t legacy_version(int16_t api_key);
 const char* error_name(int16_t code);
+// OpenSSL's latest error appended to `what` (kafka_wire_conn.cpp)
+std::string ssl_error(const std::string& what);
 // Errors after which the partition's leader (or the group's coordinator) must be looked up again.
 inline bool needs_metadata(int16_t e) {
   return e == kUnknownTopicOrPartition || e == kLeaderNotAvailable || e == kNotLeaderForPartition ||
