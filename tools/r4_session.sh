@@ -71,6 +71,8 @@ for s in ${STEPS:-smoke benchdrv}; do
     tokens) run tokens_zc 300 python benchmarks/varlen_tokens.py && run tokens_dma 300 python benchmarks/varlen_tokens.py --h2d dma ;;
     c4wait) for rep in $(seq 1 "${REPS:-4}"); do TORCHKAFKA_MIRROR_WAIT=1 run c4_wait_$rep 200 python benchmarks/config4_json_varlen.py --h2d dma; grep -o '"value": [0-9]*' "$OUT/c4_wait_$rep.log"; done ;;
     c5ab) for rep in 1 2; do run c5_deliver_$rep 200 python benchmarks/config5_large_messages.py && run c5_commit_$rep 200 python benchmarks/config5_large_messages.py --verify commit; done ;;
+    prof4) prof prof4 300 --kernel-trace --hip-trace --stats --output-format csv -d "$OUT/prof4" -o run -- python3 "$R/benchmarks/config4_json_varlen.py" --h2d dma ;;
+    prof4zc) prof prof4zc 300 --kernel-trace --hip-trace --stats --output-format csv -d "$OUT/prof4zc" -o run -- python3 "$R/benchmarks/config4_json_varlen.py" ;;
     pytestgpu) run pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 180 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -1043,6 +1043,15 @@ void MainDriver::drain_fenced(bool wait) {
   }
 }
 
+bool MainDriver::delivered_verdict_known() {
+  const int64_t pe = delivered_perr_;
+  if (pe < 0 || !parse_error_.empty() || verdicts_->state(pe) != 0) return true;
+  cover_handed();
+  pending_query_ns_ = 0;
+  release_completed_impl();
+  return verdicts_->state(pe) != 0;
+}
+
 int MainDriver::verify_delivered() {
   const int64_t pe = delivered_perr_;
   if (!parse_error_.empty()) return -4;

@@ -217,6 +217,11 @@ class MainDriver {
   // delivered.  0 clean or not device-checked; -4 corrupt (parse_error() says why: the batches
   // finished before it were made committable first, it and what follows never are).
   int verify_delivered();
+  // The non-blocking half of verify_delivered: true once the delivered batch's verdict is known
+  // (its kernel completed and its slot was released) or it carries none.  The fast paths poll it
+  // while launching the groups the workers finish meanwhile (torch_step.cpp verify_ahead), so the
+  // GPU is not left idle between the verdict and the next request.
+  bool delivered_verdict_known();
   int64_t verify_wait_ns_ = 0;  // host time verify_delivered() spent waiting for kernels
   // End of a lock-stepped iteration: barrier, then every finished batch becomes committable.
   void finish_lockstep();
@@ -257,6 +262,7 @@ class MainDriver {
     int64_t timeout_ms = 100;
     bool grouped = true;
     int extras = 0;  // record-field columns per batch (key / timestamp), 0: values only
+    bool verify = false;  // verify='deliver': the step returns once the batch's verdict is known
   } fast;
   int64_t fast_batches_ = 0, fast_records_ = 0, fast_ns_ = 0;
 

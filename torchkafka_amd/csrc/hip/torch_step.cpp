@@ -15,6 +15,8 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <ctime>
+
 #include "consumer.h"
 #include "driver.h"
 #include "collate.h"
@@ -182,6 +184,33 @@ void launch_ahead(MainDriver& d, const std::vector<int64_t>& row_shape, const at
   }
 }
 
+// verify='deliver' on a device-decode path: waits for the delivered batch's verdict while
+// launching, behind its kernel, the groups the workers finish meanwhile (`ahead`).  Waiting in
+// MainDriver::verify_delivered instead leaves them staged until the next request, so with a
+// shallow ring (config 5: 4 slots of 8 MiB) the GPU idled between each verdict and the next
+// launch.  The caller's verify_delivered() then only reads the known verdict.
+template <class Ahead>
+void verify_ahead(MainDriver& d, Ahead&& ahead) {
+  const int64_t t0 = tk::now_ns();
+  for (;;) {
+    bool known;
+    {
+      py::gil_scoped_release nogil;
+      known = d.delivered_verdict_known();
+    }
+    if (known) break;
+    ahead();
+    py::gil_scoped_release nogil;
+    if (tk::now_ns() - t0 < 200000) {
+      for (int k = 0; k < 64; ++k) tk::cpu_relax();
+    } else {
+      timespec ts{0, 20000};
+      nanosleep(&ts, nullptr);
+    }
+  }
+  d.verify_wait_ns_ += tk::now_ns() - t0;
+}
+
 // Padded width of a var-len batch: pad_to, else its longest row (rounded up to pad_multiple).
 int64_t padded_len(const SlotView& s, int64_t pad_to, int64_t pad_multiple) {
   int64_t L = pad_to >= 0 ? pad_to : s.max_row_len;
@@ -344,6 +373,8 @@ py::tuple step_once(MainDriver& d, const MainDriver::FastConfig& cfg) {
     const int64_t ta = tk::now_ns();
     launch_ahead(d, cfg.shape, opts, dev, cfg.dst_dt, cfg.shift, cfg.scale, cfg.extras);
     d.ahead_ns_ += tk::now_ns() - ta;
+    if (cfg.verify)
+      verify_ahead(d, [&] { launch_ahead(d, cfg.shape, opts, dev, cfg.dst_dt, cfg.shift, cfg.scale, cfg.extras); });
   }
   return py::make_tuple(r, cs, fixed_item(out, ext));
 }
@@ -358,7 +389,7 @@ void register_torch_step(py::module_& m) {
   cls.def(
       "configure_fast",
       [](MainDriver& d, int device, std::vector<int64_t> shape, int dst_dt, int64_t row, uintptr_t shift,
-         uintptr_t scale, bool auto_commit, int64_t timeout_ms, bool grouped, int extras) {
+         uintptr_t scale, bool auto_commit, int64_t timeout_ms, bool grouped, int extras, bool verify) {
         if (shape.empty()) throw std::invalid_argument("configure_fast: empty shape");
         scalar_type_of(dst_dt);  // validates
         auto& c = d.fast;
@@ -372,9 +403,11 @@ void register_torch_step(py::module_& m) {
         c.timeout_ms = timeout_ms;
         c.grouped = grouped;
         c.extras = extras;
+        c.verify = verify;
       },
       py::arg("device"), py::arg("shape"), py::arg("dst_dt"), py::arg("row"), py::arg("shift"), py::arg("scale"),
-      py::arg("auto_commit"), py::arg("timeout_ms"), py::arg("grouped"), py::arg("extras") = 0);
+      py::arg("auto_commit"), py::arg("timeout_ms"), py::arg("grouped"), py::arg("extras") = 0,
+      py::arg("verify") = false);
   cls.def("fast_next", [](MainDriver& d) -> py::tuple {
     const int64_t t0 = tk::now_ns();
     py::tuple res = step_once(d, d.fast);
@@ -394,7 +427,7 @@ void register_torch_step(py::module_& m) {
   cls.def(
       "varlen_next",
       [](MainDriver& d, int device, int dst_dt, int64_t pad_to, int64_t pad_multiple, double pad, bool want_mask,
-         bool auto_commit, int64_t timeout_ms) -> py::tuple {
+         bool auto_commit, int64_t timeout_ms, bool verify) -> py::tuple {
         const int64_t t0 = tk::now_ns();
         const auto dev = c10::DeviceIndex(device);
         hipStream_t stream = c10::hip::getCurrentHIPStream(dev).stream();
@@ -514,6 +547,8 @@ void register_torch_step(py::module_& m) {
           const int64_t ta = tk::now_ns();
           launch_ahead_json(d, dst_dt, pad, pad_to, pad_multiple, want_mask, dev);
           d.ahead_ns_ += tk::now_ns() - ta;
+          if (verify)
+            verify_ahead(d, [&] { launch_ahead_json(d, dst_dt, pad, pad_to, pad_multiple, want_mask, dev); });
         }
         d.ph_launch_ns_ += tk::now_ns() - t2;
         ++d.ph_steps_;
@@ -525,7 +560,7 @@ void register_torch_step(py::module_& m) {
                               py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(lengths))), m);
       },
       py::arg("device"), py::arg("dst_dt"), py::arg("pad_to"), py::arg("pad_multiple"), py::arg("pad"),
-      py::arg("want_mask"), py::arg("auto_commit"), py::arg("timeout_ms"));
+      py::arg("want_mask"), py::arg("auto_commit"), py::arg("timeout_ms"), py::arg("verify") = false);
 
   m.def(
       "step_fixed_tensor",

@@ -850,7 +850,8 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
         shift, scale = (prm[0].data_ptr(), prm[1].data_ptr()) if prm is not None else (0, 0)
         nx = self._n_extras()
         drv.configure_fast(self.device.index, [self.batch_size, *s.shape], DTYPE_CODE[self._out_dtype(s.dtype)],
-                           s.row_elems, shift, scale, native_ac, 100, self.coalesce > 1, nx)
+                           s.row_elems, shift, scale, native_ac, 100, self.coalesce > 1, nx,
+                           self.verify == "deliver")
         if nx < 2 or s.column_order() == list(range(nx)):
             return drv.fast_next
         order = s.column_order()  # fields added timestamp first: the native columns are key-first
@@ -869,7 +870,8 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
         if (dst_dt in FLOAT_DTYPES) != (src in FLOAT_DTYPES) and src in FLOAT_DTYPES:
             raise TypeError(f"cannot collate {src} records to {dst_dt}")
         args = (self.device.index, DTYPE_CODE[dst_dt], -1 if self.pad_to is None else int(self.pad_to),
-                self.pad_multiple, float(self.pad_value), bool(self.return_mask), native_ac, 100)
+                self.pad_multiple, float(self.pad_value), bool(self.return_mask), native_ac, 100,
+                self.verify == "deliver")
         native = drv.varlen_next
         want_mask = self.return_mask
 
