@@ -73,6 +73,10 @@ for s in ${STEPS:-smoke benchdrv}; do
     c5ab) for rep in 1 2; do run c5_deliver_$rep 200 python benchmarks/config5_large_messages.py && run c5_commit_$rep 200 python benchmarks/config5_large_messages.py --verify commit; done ;;
     prof4) prof prof4 300 --kernel-trace --hip-trace --stats --output-format csv -d "$OUT/prof4" -o run -- python3 "$R/benchmarks/config4_json_varlen.py" --h2d dma ;;
     prof4zc) prof prof4zc 300 --kernel-trace --hip-trace --stats --output-format csv -d "$OUT/prof4zc" -o run -- python3 "$R/benchmarks/config4_json_varlen.py" ;;
+    c4split) for rep in $(seq 1 "${REPS:-4}"); do TORCHKAFKA_JSON_COUNT_SPLIT=1 run c4_split_$rep 200 python benchmarks/config4_json_varlen.py; grep -o '"value": [0-9]*' "$OUT/c4_split_$rep.log"; done ;;
+    c5) for rep in 1 2 3; do run c5_deliver_$rep 200 python benchmarks/config5_large_messages.py; grep -o '"value": [0-9.]*' "$OUT/c5_deliver_$rep.log"; done ;;
+    pytestjson) run pytest_json 600 python -u -m pytest tests/test_gpu_json_span.py tests/test_gpu_json_parse.py tests/test_gpu_span.py tests/test_gpu_loader.py -k "json or verify or count or span" -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    benchahead) for d in 0 1 2 4 0 1 2 4; do TORCHKAFKA_AHEAD_DEPTH=$d run bench_ahead${d}_$RANDOM 300 python bench.py --steps 20 --warmup 5 --steady-steps 20000 --extra-blocks "" --bridge-steps 0 --config-blocks ""; done; grep -o '"value": [0-9.]*\|"records_per_s": [0-9.]*' "$OUT"/bench_ahead*.log ;;
     pytestgpu) run pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 180 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -524,6 +524,7 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
   }
   const uint64_t base = stage_alloc(total);
   JsonStageLaunch a{};
+  a.fuse_count = json_count_split_ ? 0 : 1;
   bool pcie = false;
   JsonGroupArgs ga{};
   ga.n = n;
@@ -586,7 +587,7 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
   flush();
   bool devc = false;
   for (int k = 0; k < n; ++k) devc = devc || ga.ctr[k] != nullptr;
-  if (devc) launch_json_count(ga, stream);  // a wave per row: counts, simple check, the width words
+  if (devc && !a.fuse_count) launch_json_count(ga, stream);  // a wave per row: counts, simple check, width words
   // the parse: a block per row over the staged texts, on the same stream
   launch_json_group(ga, dst_dt, stream);
   if (record_last) eng_->record_done(slots[n - 1], stream);
@@ -892,6 +893,11 @@ void MainDriver::ahead_begin(std::vector<int64_t>* rows) {
       break;
     group_idx_.push_back(i);
   }
+  // a group that could not take one more batch of its last one's size is full without waiting to
+  // see that batch: config 5 (8 MiB batches, 16 MiB groups, a 4-slot ring) never has a third
+  // batch staged while two are in flight, so its groups would otherwise never go ahead
+  if (!capped && !group_idx_.empty() && bytes + staged[group_idx_.back()].span_bytes > group_bytes_max_)
+    capped = true;
   if (int(group_idx_.size()) < coalesce_ && !capped) {  // only full groups go ahead; the rest waits for the user
     group_idx_.clear();
     return;

@@ -264,6 +264,18 @@ class MainDriver {
     int extras = 0;  // record-field columns per batch (key / timestamp), 0: values only
     bool verify = false;  // verify='deliver': the step returns once the batch's verdict is known
   } fast;
+  // The var-len / JSON fast path's constants (torch_step.cpp varlen_fast_next).
+  struct VarlenConfig {
+    int device = 0;
+    int dst_dt = 0;
+    int64_t pad_to = -1;  // -1: each batch's longest row (rounded up to pad_multiple)
+    int64_t pad_multiple = 1;
+    double pad = 0.0;
+    bool want_mask = false;
+    bool auto_commit = true;
+    int64_t timeout_ms = 100;
+    bool verify = false;
+  } varlen;
   int64_t fast_batches_ = 0, fast_records_ = 0, fast_ns_ = 0;
 
  private:
@@ -366,6 +378,11 @@ class MainDriver {
     return s;
   }
   int32_t json_mult_ = 1;
+  // device JSON counting in its own kernel instead of json_stage_kernel (A/B: TORCHKAFKA_JSON_COUNT_SPLIT=1)
+  const bool json_count_split_ = [] {
+    const char* e = std::getenv("TORCHKAFKA_JSON_COUNT_SPLIT");
+    return e && e[0] == '1';
+  }();
   // HBM staging ring of the device JSON parse (row texts between the two kernels, json_span.hip):
   // positions are monotonic, regions are freed in launch order as their groups' slots are released.
   static constexpr uint64_t kStageBytes = uint64_t(128) << 20;

@@ -211,6 +211,13 @@ void verify_ahead(MainDriver& d, Ahead&& ahead) {
   d.verify_wait_ns_ += tk::now_ns() - t0;
 }
 
+// verify='deliver': true when the delivered batch's device verdict is bad (the batches finished
+// before it were made committable; parse_error() says why).
+bool verdict_bad(MainDriver& d) {
+  py::gil_scoped_release nogil;
+  return d.verify_delivered() < 0;
+}
+
 // Padded width of a var-len batch: pad_to, else its longest row (rounded up to pad_multiple).
 int64_t padded_len(const SlotView& s, int64_t pad_to, int64_t pad_multiple) {
   int64_t L = pad_to >= 0 ? pad_to : s.max_row_len;
@@ -323,6 +330,7 @@ py::tuple step_once(MainDriver& d, const MainDriver::FastConfig& cfg) {
                        cfg.timeout_ms, &cs, &d.last);
     }
     if (r <= 0) return py::make_tuple(r, cs, py::none());
+    if (cfg.verify && verdict_bad(d)) return py::make_tuple(-5, cs, py::none());
     at::Tensor e = ext.empty() ? at::Tensor() : ext[0];
     if (r < cfg.shape[0]) {
       out = out.narrow(0, 0, r);
@@ -376,7 +384,153 @@ py::tuple step_once(MainDriver& d, const MainDriver::FastConfig& cfg) {
     if (cfg.verify)
       verify_ahead(d, [&] { launch_ahead(d, cfg.shape, opts, dev, cfg.dst_dt, cfg.shift, cfg.scale, cfg.extras); });
   }
+  if (cfg.verify && verdict_bad(d)) return py::make_tuple(-5, cs, py::none());
   return py::make_tuple(r, cs, fixed_item(out, ext));
+}
+
+// Var-len / JSON fast path: one call per batch -- finish + commit the previous batch, take the
+// next slot, allocate [rows, L] + lengths (+ mask) on the current stream, launch the pad/stack (or
+// JSON parse) kernel and mark the batch delivered; with verify='deliver' return once its verdict
+// is known.  -> (r, commit_status, (out, lengths[, mask]) | None); r as next_slot(), or -5 when
+// the batch's device verdict is bad (it is not handed out; parse_error() says why).
+py::tuple varlen_step(MainDriver& d, const MainDriver::VarlenConfig& c) {
+  const int device = c.device, dst_dt = c.dst_dt;
+  const int64_t pad_to = c.pad_to, pad_multiple = c.pad_multiple, timeout_ms = c.timeout_ms;
+  const double pad = c.pad;
+  const bool want_mask = c.want_mask, auto_commit = c.auto_commit, verify = c.verify;
+  const int64_t t0 = tk::now_ns();
+  const auto dev = c10::DeviceIndex(device);
+  hipStream_t stream = c10::hip::getCurrentHIPStream(dev).stream();
+  int cs = 0;
+  int r;
+  int64_t t1, t2;
+  size_t extra = 0;
+  d.set_json_mult(pad_to >= 0 ? 0 : std::max<int64_t>(1, pad_multiple));
+  {
+    py::gil_scoped_release nogil;
+    d.finish_delivered(stream);
+    if (auto_commit) cs = d.commit_pending();
+    t1 = tk::now_ns();
+    if (d.coalesce() > 1) d.stage_ready(d.coalesce());  // let a group form (never blocks)
+    r = d.next_slot(timeout_ms, &d.last);
+    if (r == 1 && !d.last.pre) extra = d.json_group_extend();
+    t2 = tk::now_ns();
+  }
+  d.ph_commit_ns_ += t1 - t0;
+  d.ph_next_ns_ += t2 - t1;
+  if (r != 1) return py::make_tuple(r, cs, py::none());
+  SlotView& v = d.last;
+  const int64_t n = int64_t(v.n_rows);
+  at::Tensor out, lengths, mask;
+  if (v.pre) {
+    // parsed by an earlier group launch; a consumer on another stream waits for that kernel
+    auto* o = static_cast<VarlenOut*>(v.pre_out.get());
+    finish_json(d, v, o, dst_dt, pad, v.pre_stream);
+    out = o->out;
+    lengths = o->lengths;
+    mask = o->mask;
+    py::gil_scoped_release nogil;
+    if (v.pre_stream != stream) d.wait_group(v, stream);
+    d.deliver(v);
+  } else if (row_span_kind(v.kind)) {
+    // parsed from the logs by one launch with the staged JSON batches behind it
+    const int ng = 1 + int(extra);
+    int64_t ms[kMaxGroup], Ls[kMaxGroup];
+    bool devc[kMaxGroup];
+    for (int k = 0; k < ng; ++k) {
+      const SlotView& s = k == 0 ? v : d.group_member(size_t(k - 1));
+      ms[k] = int64_t(s.n_rows);
+      Ls[k] = padded_len(s, pad_to, pad_multiple);
+      devc[k] = (s.flags & tk::kSlotDevCount) != 0;
+    }
+    std::shared_ptr<VarlenOut> o[kMaxGroup];
+    alloc_json_group(d, ms, Ls, devc, ng, dst_dt, want_mask, dev, o);
+    void* outs[kMaxGroup];
+    int64_t* lens[kMaxGroup];
+    uint8_t* masks[kMaxGroup];
+    std::vector<std::shared_ptr<void>> handles;
+    handles.reserve(extra);
+    for (int k = 0; k < ng; ++k) {
+      outs[k] = vals_ptr(*o[k]);
+      lens[k] = lens_ptr(*o[k]);
+      masks[k] = mask_ptr(*o[k]);
+    }
+    for (int k = 1; k < ng; ++k) handles.emplace_back(std::move(o[k]));
+    {
+      py::gil_scoped_release nogil;
+      d.json_group_launch(stream, dst_dt, pad, outs, Ls, lens, masks, std::move(handles));
+    }
+    finish_json(d, v, o[0].get(), dst_dt, pad, d.last_stream());
+    out = o[0]->out;
+    lengths = o[0]->lengths;
+    mask = o[0]->mask;
+    py::gil_scoped_release nogil;
+    d.deliver(v);
+  } else {
+    auto alloc = [&](const SlotView& s, VarlenOut* o, int64_t* Lout) {
+      const int64_t L = padded_len(s, pad_to, pad_multiple);
+      const int64_t m = int64_t(s.n_rows);
+      o->out = at::empty({m, L}, at::TensorOptions().dtype(scalar_type_of(dst_dt)).device(at::kCUDA, dev));
+      o->lengths = at::empty({m}, at::TensorOptions().dtype(at::kLong).device(at::kCUDA, dev));
+      if (want_mask) o->mask = at::empty({m, L}, at::TensorOptions().dtype(at::kBool).device(at::kCUDA, dev));
+      *Lout = L;
+    };
+    if (extra == 0 || v.kind != uint32_t(tk::kPackJsonText)) {
+      VarlenOut o;
+      int64_t L;
+      alloc(v, &o, &L);
+      out = o.out;
+      lengths = o.lengths;
+      mask = o.mask;
+      py::gil_scoped_release nogil;
+      d.collate_varlen(v, stream, dst_dt, out.data_ptr(), L, pad, lengths.data_ptr<int64_t>(),
+                       want_mask ? static_cast<uint8_t*>(mask.data_ptr()) : nullptr);
+      d.deliver(v);
+    } else {
+      // one launch parses `last` and the staged JSON batches behind it
+      void* outs[kMaxGroup];
+      int64_t Ls[kMaxGroup];
+      int64_t* lens[kMaxGroup];
+      uint8_t* masks[kMaxGroup];
+      std::vector<std::shared_ptr<void>> handles;
+      handles.reserve(extra);
+      for (size_t k = 0; k <= extra; ++k) {
+        auto o = std::make_shared<VarlenOut>();
+        alloc(k == 0 ? v : d.group_member(k - 1), o.get(), &Ls[k]);
+        outs[k] = o->out.data_ptr();
+        lens[k] = o->lengths.data_ptr<int64_t>();
+        masks[k] = want_mask ? static_cast<uint8_t*>(o->mask.data_ptr()) : nullptr;
+        if (k == 0) {
+          out = o->out;
+          lengths = o->lengths;
+          mask = o->mask;
+        } else {
+          handles.emplace_back(std::move(o));
+        }
+      }
+      py::gil_scoped_release nogil;
+      d.json_group_launch(stream, dst_dt, pad, outs, Ls, lens, masks, std::move(handles));
+      d.deliver(v);
+    }
+  }
+  if (row_span_kind(v.kind)) {
+    const int64_t ta = tk::now_ns();
+    launch_ahead_json(d, dst_dt, pad, pad_to, pad_multiple, want_mask, dev);
+    d.ahead_ns_ += tk::now_ns() - ta;
+    if (verify)
+      verify_ahead(d, [&] { launch_ahead_json(d, dst_dt, pad, pad_to, pad_multiple, want_mask, dev); });
+  }
+  d.ph_launch_ns_ += tk::now_ns() - t2;
+  ++d.ph_steps_;
+  if (verify && verdict_bad(d)) return py::make_tuple(-5, cs, py::none());
+  ++d.fast_batches_;
+  d.fast_records_ += n;
+  d.fast_ns_ += tk::now_ns() - t0;
+  py::object o = py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(out)));
+  py::object l = py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(lengths)));
+  py::tuple item = want_mask ? py::make_tuple(o, l, py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(mask))))
+                             : py::make_tuple(o, l);
+  return py::make_tuple(r, cs, item);
 }
 
 }  // namespace
@@ -420,147 +574,18 @@ void register_torch_step(py::module_& m) {
     return res;
   });
 
-  // Var-len / JSON fast path: one call per batch -- finish + commit the previous batch, take
-  // the next slot, allocate [rows, L] + lengths (+ mask) on the current stream, launch the
-  // pad/stack (or JSON parse) kernel and mark the batch delivered.
-  // -> (r, commit_status, out | None, lengths | None, mask | None); r as next_slot().
+  // Var-len / JSON fast path: configured once per iteration, then one argument-free call per batch.
   cls.def(
-      "varlen_next",
+      "configure_varlen",
       [](MainDriver& d, int device, int dst_dt, int64_t pad_to, int64_t pad_multiple, double pad, bool want_mask,
-         bool auto_commit, int64_t timeout_ms, bool verify) -> py::tuple {
-        const int64_t t0 = tk::now_ns();
-        const auto dev = c10::DeviceIndex(device);
-        hipStream_t stream = c10::hip::getCurrentHIPStream(dev).stream();
-        int cs = 0;
-        int r;
-        int64_t t1, t2;
-        size_t extra = 0;
-        d.set_json_mult(pad_to >= 0 ? 0 : std::max<int64_t>(1, pad_multiple));
-        {
-          py::gil_scoped_release nogil;
-          d.finish_delivered(stream);
-          if (auto_commit) cs = d.commit_pending();
-          t1 = tk::now_ns();
-          if (d.coalesce() > 1) d.stage_ready(d.coalesce());  // let a group form (never blocks)
-          r = d.next_slot(timeout_ms, &d.last);
-          if (r == 1 && !d.last.pre) extra = d.json_group_extend();
-          t2 = tk::now_ns();
-        }
-        d.ph_commit_ns_ += t1 - t0;
-        d.ph_next_ns_ += t2 - t1;
-        if (r != 1) return py::make_tuple(r, cs, py::none(), py::none(), py::none());
-        SlotView& v = d.last;
-        const int64_t n = int64_t(v.n_rows);
-        at::Tensor out, lengths, mask;
-        if (v.pre) {
-          // parsed by an earlier group launch; a consumer on another stream waits for that kernel
-          auto* o = static_cast<VarlenOut*>(v.pre_out.get());
-          finish_json(d, v, o, dst_dt, pad, v.pre_stream);
-          out = o->out;
-          lengths = o->lengths;
-          mask = o->mask;
-          py::gil_scoped_release nogil;
-          if (v.pre_stream != stream) d.wait_group(v, stream);
-          d.deliver(v);
-        } else if (row_span_kind(v.kind)) {
-          // parsed from the logs by one launch with the staged JSON batches behind it
-          const int ng = 1 + int(extra);
-          int64_t ms[kMaxGroup], Ls[kMaxGroup];
-          bool devc[kMaxGroup];
-          for (int k = 0; k < ng; ++k) {
-            const SlotView& s = k == 0 ? v : d.group_member(size_t(k - 1));
-            ms[k] = int64_t(s.n_rows);
-            Ls[k] = padded_len(s, pad_to, pad_multiple);
-            devc[k] = (s.flags & tk::kSlotDevCount) != 0;
-          }
-          std::shared_ptr<VarlenOut> o[kMaxGroup];
-          alloc_json_group(d, ms, Ls, devc, ng, dst_dt, want_mask, dev, o);
-          void* outs[kMaxGroup];
-          int64_t* lens[kMaxGroup];
-          uint8_t* masks[kMaxGroup];
-          std::vector<std::shared_ptr<void>> handles;
-          handles.reserve(extra);
-          for (int k = 0; k < ng; ++k) {
-            outs[k] = vals_ptr(*o[k]);
-            lens[k] = lens_ptr(*o[k]);
-            masks[k] = mask_ptr(*o[k]);
-          }
-          for (int k = 1; k < ng; ++k) handles.emplace_back(std::move(o[k]));
-          {
-            py::gil_scoped_release nogil;
-            d.json_group_launch(stream, dst_dt, pad, outs, Ls, lens, masks, std::move(handles));
-          }
-          finish_json(d, v, o[0].get(), dst_dt, pad, d.last_stream());
-          out = o[0]->out;
-          lengths = o[0]->lengths;
-          mask = o[0]->mask;
-          py::gil_scoped_release nogil;
-          d.deliver(v);
-        } else {
-          auto alloc = [&](const SlotView& s, VarlenOut* o, int64_t* Lout) {
-            const int64_t L = padded_len(s, pad_to, pad_multiple);
-            const int64_t m = int64_t(s.n_rows);
-            o->out = at::empty({m, L}, at::TensorOptions().dtype(scalar_type_of(dst_dt)).device(at::kCUDA, dev));
-            o->lengths = at::empty({m}, at::TensorOptions().dtype(at::kLong).device(at::kCUDA, dev));
-            if (want_mask) o->mask = at::empty({m, L}, at::TensorOptions().dtype(at::kBool).device(at::kCUDA, dev));
-            *Lout = L;
-          };
-          if (extra == 0 || v.kind != uint32_t(tk::kPackJsonText)) {
-            VarlenOut o;
-            int64_t L;
-            alloc(v, &o, &L);
-            out = o.out;
-            lengths = o.lengths;
-            mask = o.mask;
-            py::gil_scoped_release nogil;
-            d.collate_varlen(v, stream, dst_dt, out.data_ptr(), L, pad, lengths.data_ptr<int64_t>(),
-                             want_mask ? static_cast<uint8_t*>(mask.data_ptr()) : nullptr);
-            d.deliver(v);
-          } else {
-            // one launch parses `last` and the staged JSON batches behind it
-            void* outs[kMaxGroup];
-            int64_t Ls[kMaxGroup];
-            int64_t* lens[kMaxGroup];
-            uint8_t* masks[kMaxGroup];
-            std::vector<std::shared_ptr<void>> handles;
-            handles.reserve(extra);
-            for (size_t k = 0; k <= extra; ++k) {
-              auto o = std::make_shared<VarlenOut>();
-              alloc(k == 0 ? v : d.group_member(k - 1), o.get(), &Ls[k]);
-              outs[k] = o->out.data_ptr();
-              lens[k] = o->lengths.data_ptr<int64_t>();
-              masks[k] = want_mask ? static_cast<uint8_t*>(o->mask.data_ptr()) : nullptr;
-              if (k == 0) {
-                out = o->out;
-                lengths = o->lengths;
-                mask = o->mask;
-              } else {
-                handles.emplace_back(std::move(o));
-              }
-            }
-            py::gil_scoped_release nogil;
-            d.json_group_launch(stream, dst_dt, pad, outs, Ls, lens, masks, std::move(handles));
-            d.deliver(v);
-          }
-        }
-        if (row_span_kind(v.kind)) {
-          const int64_t ta = tk::now_ns();
-          launch_ahead_json(d, dst_dt, pad, pad_to, pad_multiple, want_mask, dev);
-          d.ahead_ns_ += tk::now_ns() - ta;
-          if (verify)
-            verify_ahead(d, [&] { launch_ahead_json(d, dst_dt, pad, pad_to, pad_multiple, want_mask, dev); });
-        }
-        d.ph_launch_ns_ += tk::now_ns() - t2;
-        ++d.ph_steps_;
-        ++d.fast_batches_;
-        d.fast_records_ += n;
-        d.fast_ns_ += tk::now_ns() - t0;
-        py::object m = want_mask ? py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(mask))) : py::none();
-        return py::make_tuple(r, cs, py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(out))),
-                              py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(lengths))), m);
+         bool auto_commit, int64_t timeout_ms, bool verify) {
+        scalar_type_of(dst_dt);  // validates
+        d.varlen = MainDriver::VarlenConfig{device, dst_dt, pad_to, pad_multiple, pad, want_mask, auto_commit,
+                                            timeout_ms, verify};
       },
       py::arg("device"), py::arg("dst_dt"), py::arg("pad_to"), py::arg("pad_multiple"), py::arg("pad"),
       py::arg("want_mask"), py::arg("auto_commit"), py::arg("timeout_ms"), py::arg("verify") = false);
+  cls.def("varlen_fast_next", [](MainDriver& d) { return varlen_step(d, d.varlen); });
 
   m.def(
       "step_fixed_tensor",

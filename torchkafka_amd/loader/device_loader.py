@@ -795,14 +795,16 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
                 r, cs, item = step()
                 if cs:
                     self._log_commit(cs, debug)
+                if r > 0 and verify and py_commits and drv.verify_delivered() < 0:
+                    r = -5  # the fast stages wait for the verdict natively and return -5 themselves
+                if r == -5:
+                    # the batch's CRC32C / grammar verdict is bad: it never reaches the user (the
+                    # reference's records pass kafka-python's check_crcs before _process sees them,
+                    # kafka_dataset.py:156-162); the batches finished before it are committed first
+                    if auto_commit and delivered:
+                        self._commit_native(drv, debug)
+                    raise CorruptRecordException(drv.parse_error())
                 if r > 0:
-                    if verify and drv.verify_delivered() < 0:
-                        # the batch's CRC32C / grammar verdict is bad: it never reaches the user (the
-                        # reference's records pass kafka-python's check_crcs before _process sees them,
-                        # kafka_dataset.py:156-162); the batches finished before it are committed first
-                        if auto_commit and delivered:
-                            self._commit_native(drv, debug)
-                        raise CorruptRecordException(drv.parse_error())
                     if delivered:
                         if log_commits and not py_commits:
                             self._commit_logged(drv)
@@ -869,16 +871,10 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
         dst_dt = self._out_dtype(src)
         if (dst_dt in FLOAT_DTYPES) != (src in FLOAT_DTYPES) and src in FLOAT_DTYPES:
             raise TypeError(f"cannot collate {src} records to {dst_dt}")
-        args = (self.device.index, DTYPE_CODE[dst_dt], -1 if self.pad_to is None else int(self.pad_to),
-                self.pad_multiple, float(self.pad_value), bool(self.return_mask), native_ac, 100,
-                self.verify == "deliver")
-        native = drv.varlen_next
-        want_mask = self.return_mask
-
-        def step():
-            r, cs, out, lengths, mask = native(*args)
-            return r, cs, ((out, lengths, mask) if want_mask else (out, lengths)) if r == 1 else None
-        return step
+        drv.configure_varlen(self.device.index, DTYPE_CODE[dst_dt], -1 if self.pad_to is None else int(self.pad_to),
+                             self.pad_multiple, float(self.pad_value), bool(self.return_mask), native_ac, 100,
+                             self.verify == "deliver")
+        return drv.varlen_fast_next
 
     def _slot_stage(self, run: _Run, auto_commit: bool, debug: bool):
         drv = run.driver

@@ -57,8 +57,8 @@ class LoaderStats:
     log_bytes_registered: int = 0  # h2d="direct": broker log bytes pinned in place so far
     log_bytes_unpinned: int = 0    # replica logs: consumed ranges unpinned again (kReleaseConsumed)
     log_register_ns: int = 0
-    log_register_wait_ns: int = 0
-    mirror_pending_fallbacks: int = 0  # mirror segments read from the pinned log: their copy was in flight     # the launch thread waiting for the pin thread (growing logs)
+    log_register_wait_ns: int = 0  # the launch thread waiting for the pin thread (growing logs)
+    mirror_pending_fallbacks: int = 0  # mirror segments read from the pinned log: their copy was in flight
     mirror_bytes: int = 0     # h2d="dma" device decode: log bytes copied into the HBM mirror (SDMA)
     mirror_copies: int = 0
     mirror_fallbacks: int = 0  # segments read from the pinned log instead (buffer busy)
