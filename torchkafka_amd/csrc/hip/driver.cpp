@@ -524,7 +524,6 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
   }
   const uint64_t base = stage_alloc(total);
   JsonStageLaunch a{};
-  a.fuse_count = json_count_split_ ? 0 : 1;
   bool pcie = false;
   JsonGroupArgs ga{};
   ga.n = n;
@@ -587,7 +586,10 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
   flush();
   bool devc = false;
   for (int k = 0; k < n; ++k) devc = devc || ga.ctr[k] != nullptr;
-  if (devc && !a.fuse_count) launch_json_count(ga, stream);  // a wave per row: counts, simple check, width words
+  // a wave per row: counts, simple check, the width words.  Not fused into json_stage_kernel: its
+  // few workgroups (one per segment) took 149 us per group doing it instead of 71 us, and config 4
+  // fell from 40.5 M to 35.5 M rec/s (profiles/r04_s4)
+  if (devc) launch_json_count(ga, stream);
   // the parse: a block per row over the staged texts, on the same stream
   launch_json_group(ga, dst_dt, stream);
   if (record_last) eng_->record_done(slots[n - 1], stream);

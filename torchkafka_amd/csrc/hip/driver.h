@@ -378,11 +378,6 @@ class MainDriver {
     return s;
   }
   int32_t json_mult_ = 1;
-  // device JSON counting in its own kernel instead of json_stage_kernel (A/B: TORCHKAFKA_JSON_COUNT_SPLIT=1)
-  const bool json_count_split_ = [] {
-    const char* e = std::getenv("TORCHKAFKA_JSON_COUNT_SPLIT");
-    return e && e[0] == '1';
-  }();
   // HBM staging ring of the device JSON parse (row texts between the two kernels, json_span.hip):
   // positions are monotonic, regions are freed in launch order as their groups' slots are released.
   static constexpr uint64_t kStageBytes = uint64_t(128) << 20;

@@ -9,10 +9,9 @@
 //     cut): stage the segment in LDS by LDS-DMA and verify the RecordBatch CRC32C (span_device.h)
 //     -- PCIe-bound, like span_decode.hip -- then copy each row's text 16-byte aligned into the
 //     batch's HBM staging area (a block-wide scan of the rounded lengths places them) and write
-//     its JsonRowDesc.  A device-counted row (kSlotDevCount) is scanned by the same wave as it is copied --
-//     json_scan_simple's rules on the chunks it loads from LDS -- which completes the row's
-//     descriptor and raises the batch's width word (json_count_kernel, a wave per row over the
-//     staged HBM text, is the unfused variant: TORCHKAFKA_JSON_COUNT_SPLIT=1);
+//     its JsonRowDesc;
+//   json_count_kernel (device counting, kSlotDevCount): a wave per row scans the staged text --
+//     json_scan_simple's rules -- and completes the row's descriptor and the batch's width word;
 //   json_parse.hip's json_rows_kernel over those descriptors: a 256-thread block per row, one
 //     token per thread (bit-exact with json.loads).  Parsing is ~100x the work of the copy, so it
 //     gets the whole GPU (a block per row) instead of the few workgroups the segments give.
@@ -239,32 +238,10 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
       continue;
     }
     uint8_t* __restrict__ o = bo.stage + dst[rr];
-    if (a.fuse_count && cnt[rr] == tk::kJsonCountOnDevice && bo.ctr) {
-      // device counting fused with the copy: scan_row reads each 16-byte chunk once (from LDS) and
-      // the same load is stored to HBM -- no second pass over the staged text, no extra launch
-      int32_t guess = 0;
-      const int32_t count = scan_row(
-          [&](int32_t c) {
-            const uint4 v = load16(b32, r0 + c);
-            *reinterpret_cast<uint4*>(o + c) = v;
-            return v;
-          },
-          [&](int32_t i) { return uint32_t(buf[r0 + i]); }, T, lane, &guess);
-      if (lane == 0) {
-        // a row that is not simple: the host parses it when the batch is delivered (tlen
-        // kJsonCountOnDevice: json_rows_kernel writes its padding, lengths and mask only)
-        const bool host = count < 0;
-        const int32_t c = host ? guess : count;
-        const int32_t n_out = trunc >= 0 && c > trunc ? trunc : c;
-        bo.desc[row_begin + rr] = JsonRowDesc{dst[rr], host ? tk::kJsonCountOnDevice : T, c, n_out};
-        const unsigned long long tag = static_cast<unsigned long long>(bo.ctr_tag) << 32;
-        atomicMax(bo.ctr, tag | uint32_t(max(n_out, 0)));
-        if (host) atomicMax(bo.ctr + 1, tag | 1u);
-      }
-      continue;
-    }
     for (int32_t c = 16 * lane; c < T; c += 64 * 16) *reinterpret_cast<uint4*>(o + c) = load16(b32, r0 + c);
     if (lane == 0) {
+      // a device-counted row (count kJsonCountOnDevice) keeps that count here: json_count_kernel
+      // scans its staged text and completes the descriptor before json_rows_kernel reads it
       const int32_t c = cnt[rr];
       const int32_t n_out = c < 0 ? 0 : trunc >= 0 && c > trunc ? trunc : c;
       bo.desc[row_begin + rr] = JsonRowDesc{dst[rr], T, c, n_out};
@@ -279,11 +256,10 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
   }
 }
 
-// Device counting as a kernel of its own, between the stage and the parse (TORCHKAFKA_JSON_COUNT_SPLIT=1):
-// a wave per device-counted row (a block of four rows; blocks [row_base[k] / 4 ..) of batch k) scans
-// the row's staged, 16-byte aligned HBM text, completes its descriptor and raises the batch's tagged
-// width word.  The default counts in json_stage_kernel instead: one launch less per group, and the
-// text is classified from the LDS chunks the copy loads anyway instead of being read back from HBM.
+// Device counting, between the stage and the parse: a wave per device-counted row (a block of four
+// rows; blocks [row_base[k] / 4 ..) of batch k) scans the row's staged, 16-byte aligned HBM text,
+// completes its descriptor and raises the batch's tagged width word.  Kept out of the stage kernel,
+// whose few workgroups (one per segment) are busy with PCIe loads: here every row gets a wave.
 __global__ __launch_bounds__(256) void json_count_kernel(JsonGroupArgs a) {
   const int lane = int(threadIdx.x) & 63;
   const int64_t g = int64_t(blockIdx.x) * 4 + int64_t(threadIdx.x >> 6);  // this wave's global row

@@ -75,7 +75,6 @@ struct JsonStageBatch {
 struct JsonStageLaunch {
   int n_seg;
   int burst;                    // as SpanLaunch::burst
-  int fuse_count;               // 1: the copy also counts device-counted rows (no json_count_kernel)
   const uint32_t* tabs;         // device CRC tables (tk::kSpanTabWords)
   JsonStageBatch b[kMaxGroup];
   SpanDevSeg s[kMaxLaunchSegs];
