@@ -1,4 +1,6 @@
 """LoaderConfig / Tuning: one validated configuration for DeviceLoader."""
+import os
+
 import pytest
 import torch
 
@@ -35,7 +37,8 @@ def test_invalid_behaviour_rejected(kw, msg):
 
 
 @pytest.mark.parametrize("kw,msg", [
-    ({"coalesce": 9}, "coalesce"), ({"copy_streams": 0}, "copy_streams"), ({"decode_streams": 5}, "decode_streams"),
+    ({"coalesce": 17}, "coalesce"), ({"varlen_coalesce": 0}, "varlen_coalesce"), ({"copy_streams": 0}, "copy_streams"),
+    ({"decode_streams": 5}, "decode_streams"),
     ({"slots_per_worker": 1}, "slots_per_worker"), ({"span_burst": -1}, "span_burst"),
     ({"ahead_depth": 99}, "ahead_depth"), ({"coalesce_wait_us": -5}, "coalesce_wait_us"),
 ])
@@ -77,3 +80,16 @@ def test_device_loader_takes_config_and_keyword_overrides(broker):
         DeviceLoader(Vec4.placeholder(), 8, device="cpu", not_an_option=1)
     with pytest.raises(ValueError, match="coalesce"):
         DeviceLoader(Vec4.placeholder(), 8, device="cpu", coalesce=0)
+
+
+def test_config_doc_is_generated_from_the_code():
+    """docs/CONFIG.md lists every LoaderConfig / Tuning field with a description (tools/gen_config_doc.py)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "gen_config_doc.py"), "--check"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    text = open(os.path.join(root, "docs", "CONFIG.md")).read()
+    assert not [ln for ln in text.splitlines() if ln.startswith("| `") and ln.rstrip().endswith("|  |")]

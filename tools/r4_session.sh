@@ -77,6 +77,9 @@ for s in ${STEPS:-smoke benchdrv}; do
     c5) for rep in 1 2 3; do run c5_deliver_$rep 200 python benchmarks/config5_large_messages.py; grep -o '"value": [0-9.]*' "$OUT/c5_deliver_$rep.log"; done ;;
     pytestjson) run pytest_json 600 python -u -m pytest tests/test_gpu_json_span.py tests/test_gpu_json_parse.py tests/test_gpu_span.py tests/test_gpu_loader.py -k "json or verify or count or span" -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     benchahead) for d in 0 1 2 4 0 1 2 4; do TORCHKAFKA_AHEAD_DEPTH=$d run bench_ahead${d}_$RANDOM 300 python bench.py --steps 20 --warmup 5 --steady-steps 20000 --extra-blocks "" --bridge-steps 0 --config-blocks ""; done; grep -o '"value": [0-9.]*\|"records_per_s": [0-9.]*' "$OUT"/bench_ahead*.log ;;
+    c4g8) for rep in $(seq 1 "${REPS:-4}"); do run c4_g8_$rep 200 python benchmarks/config4_json_varlen.py --varlen-coalesce 8; grep -o '"value": [0-9]*' "$OUT/c4_g8_$rep.log"; done ;;
+    c4g8dma) for rep in $(seq 1 "${REPS:-4}"); do run c4_g8dma_$rep 200 python benchmarks/config4_json_varlen.py --varlen-coalesce 8 --h2d dma; grep -o '"value": [0-9]*' "$OUT/c4_g8dma_$rep.log"; done ;;
+    kernarg) run kernarg 60 tools/probes/kernarg_probe ;;
     pytestgpu) run pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 180 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

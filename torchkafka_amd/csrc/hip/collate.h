@@ -22,7 +22,10 @@ void launch_varlen(const int32_t* offs, const void* vals, int src_dt, void* out,
                    double pad, int64_t* lengths, uint8_t* mask, hipStream_t stream);
 
 // Up to kMaxGroup dense casts (consecutive batches, same dtypes and row width) in one launch.
-constexpr int kMaxGroup = 8;
+// 16: device-parsed JSON / var-len batches group 16 at a time (Tuning.varlen_coalesce), which
+// halves the per-batch launch cost that bounds config 4; fixed-width groups stay at 8 by default.
+// The largest by-value launch struct (VarSpanLaunch) stays under 4 KiB.
+constexpr int kMaxGroup = 16;
 // host_src: the sources are pinned host memory read over PCIe (zero-copy), which sizes the grid.
 void launch_fixed_group(const void* const* srcs, int src_dt, void* const* dsts, int dst_dt, const int64_t* rows, int n,
                         int64_t row, const float* shift, const float* scale, hipStream_t stream, bool host_src);

@@ -197,7 +197,8 @@ class _Run:
                 if self.table is not None:
                     self.driver.set_worker_sink(self.table.address, L.n_producers, self.table.capacity)
                 self.driver.set_event_every(L._event_every(self.ring.n_slots))
-                self.driver.set_coalesce(L.coalesce)
+                self.driver.set_coalesce(int(L.tuning.varlen_coalesce) if L.plan.json_span or L.plan.var_span
+                                         else L.coalesce)
                 self.driver.set_coalesce_wait_us(L.coalesce_wait_us if L.coalesce > 1 else 0)
                 if L.plan.direct:
                     self.driver.enable_direct()
@@ -353,7 +354,33 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
             the workers (config 2 on MI355X: 4 slots 29-31 M rec/s, 8 slots 30-33 M).
         prefetch: batches whose H2D copy is issued ahead of the user (overlap with compute).
         in_order: strict worker round-robin (reference order) instead of first-ready.
-        pad_to / pad_multiple / pad_value / return_mask: variable-length padding controls.
+        pad_to: var-len / JSON batches are padded to this fixed width (use the schema's ``max_len`` /
+            ``truncate`` to bound the rows); None pads each batch to its longest row.
+        pad_multiple: with ``pad_to=None``, the batch width is rounded up to a multiple of this.
+        pad_value: the value written into the padding.
+        return_mask: var-len / JSON batches also yield a bool ``[rows, width]`` mask of real elements.
+        drop_last: drop a final batch shorter than ``batch_size`` (DataLoader's meaning).
+        return_info: yield ``(batch, BatchInfo)`` with each batch's partitions and offset ranges.
+        native: use the native step driver (``False``: the Python loop, for debugging).
+        multiprocessing_context: start method of the worker processes (``"fork"``, ``"spawn"``,
+            ``"forkserver"``).
+        commit_sink: ``"broker"`` (this process stores finished offsets into the synthetic broker),
+            ``"worker"`` (each worker's consumer commits its own partitions, as the reference) or
+            ``"auto"`` (broker when the workers read the synthetic broker with static sharding).
+        rank: this process's rank for static sharding (default: torch.distributed's, else 0).
+        world_size: ranks sharing the topic (default: torch.distributed's, else 1).
+        timeout: seconds to wait for a batch before ``TimeoutError`` (0 waits forever).
+        group_id: consumer group the commits go to (default: the one given to ``init_worker``).
+        bootstrap_servers: where the group lives (default: the one given to ``init_worker``).
+        base_seed: seed of the workers' RNGs (worker k gets ``base_seed + k``); None draws one from torch.
+        decode: ``"device"`` (fixed-width / var-len records decoded by the gfx950 kernels straight from
+            the pinned broker logs, CRC32C included; the workers only walk record headers),
+            ``"host"`` (the workers CRC-check and pack the values) or ``"auto"`` (device when possible).
+        json_parse: ``JsonArray`` records parsed by the gfx950 kernel (``"device"``), by the workers
+            (``"host"``), or ``"auto"`` (device unless ``skip_bad=True`` needs rows dropped).
+        bridge: ``"auto"``: workers pointed at a real Kafka cluster read a local replica that a native
+            ``KafkaBridge`` fills with this rank's partitions (commits reach the cluster's coordinator);
+            ``True`` requires it, ``False`` lets the workers' consumers read the cluster themselves.
         commit_on: ``"host"`` (commit when the next batch is requested, as the reference) or
             ``"device"`` (additionally wait until the GPU finished the user's work on the batch).
         commit: ``"async"`` (default: batch k's offsets are stored -- in the synthetic broker, or in a
@@ -391,6 +418,7 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
         coalesce: fixed-width batches that are already staged when the next one is requested are
             collated together, up to this many per kernel launch (one allocation, one launch, one
             completion event); the following requests return them without a HIP call.  1 disables.
+            Var-len and JSON batches decoded on the device group by ``varlen_coalesce`` instead (16).
         coalesce_wait_us: while the GPU is still busy with an earlier launch, wait up to this long
             for enough staged batches to fill a group (costs no GPU time; a zero-copy batch takes
             7.1 us alone and 5.2 us in a group of 4).  0 launches whatever is staged at once.
