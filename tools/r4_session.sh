@@ -79,6 +79,11 @@ for s in ${STEPS:-smoke benchdrv}; do
     benchahead) for d in 0 1 2 4 0 1 2 4; do TORCHKAFKA_AHEAD_DEPTH=$d run bench_ahead${d}_$RANDOM 300 python bench.py --steps 20 --warmup 5 --steady-steps 20000 --extra-blocks "" --bridge-steps 0 --config-blocks ""; done; grep -o '"value": [0-9.]*\|"records_per_s": [0-9.]*' "$OUT"/bench_ahead*.log ;;
     c4g8) for rep in $(seq 1 "${REPS:-4}"); do run c4_g8_$rep 200 python benchmarks/config4_json_varlen.py --varlen-coalesce 8; grep -o '"value": [0-9]*' "$OUT/c4_g8_$rep.log"; done ;;
     c4g8dma) for rep in $(seq 1 "${REPS:-4}"); do run c4_g8dma_$rep 200 python benchmarks/config4_json_varlen.py --varlen-coalesce 8 --h2d dma; grep -o '"value": [0-9]*' "$OUT/c4_g8dma_$rep.log"; done ;;
+    c4ab) for rep in $(seq 1 "${REPS:-3}"); do
+            run c4_g8_$rep 200 python benchmarks/config4_json_varlen.py --varlen-coalesce 8 &&
+            run c4_g16s32_$rep 200 python benchmarks/config4_json_varlen.py --varlen-coalesce 16 --slots-per-worker 32 &&
+            run c4_g8s32_$rep 200 python benchmarks/config4_json_varlen.py --varlen-coalesce 8 --slots-per-worker 32
+          done; grep -o '"value": [0-9]*' "$OUT"/c4_g*.log ;;
     kernarg) run kernarg 60 tools/probes/kernarg_probe ;;
     pytestgpu) run pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 180 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
