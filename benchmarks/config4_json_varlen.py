@@ -43,7 +43,6 @@ def parse(argv=None):
     ap.add_argument("--event-every", type=int, default=None)
     ap.add_argument("--prefetch", type=int, default=2)
     ap.add_argument("--verify", default="deliver", choices=["deliver", "commit"])
-    ap.add_argument("--varlen-coalesce", type=int, default=16, help="JSON batches per device launch (1..16)")
     return ap.parse_args(argv)
 
 
@@ -70,7 +69,7 @@ def run(args, sync=None) -> dict:
         dl = DeviceLoader(Json.placeholder(), B, num_workers=args.workers, device=args.device, dtype=torch.bfloat16,
                           json_parse=args.json_parse, h2d=args.h2d, decode=args.decode, json_count=args.json_count,
                           slots_per_worker=args.slots_per_worker, event_every=args.event_every, prefetch=args.prefetch,
-                          verify=args.verify, varlen_coalesce=args.varlen_coalesce,
+                          verify=args.verify,
                           worker_init_fn=Json.init_worker("json", bootstrap_servers=url, group_id="cfg4",
                                                           auto_offset_reset="earliest"))
         it = iter(auto_commit(dl))

@@ -37,8 +37,7 @@ def test_invalid_behaviour_rejected(kw, msg):
 
 
 @pytest.mark.parametrize("kw,msg", [
-    ({"coalesce": 17}, "coalesce"), ({"varlen_coalesce": 0}, "varlen_coalesce"), ({"copy_streams": 0}, "copy_streams"),
-    ({"decode_streams": 5}, "decode_streams"),
+    ({"coalesce": 9}, "coalesce"), ({"copy_streams": 0}, "copy_streams"), ({"decode_streams": 5}, "decode_streams"),
     ({"slots_per_worker": 1}, "slots_per_worker"), ({"span_burst": -1}, "span_burst"),
     ({"ahead_depth": 99}, "ahead_depth"), ({"coalesce_wait_us": -5}, "coalesce_wait_us"),
 ])

@@ -117,7 +117,8 @@ def test_device_loader_workers_follow_a_rebalance(broker, cluster):
     broker.create_topic("t", 4)
     broker.fill("t", 200, "fixed_f32", size=8, records_per_batch=10)
     cluster.join_delay_s = 5.0
-    a = _spawn(cluster.address, nw=2, slow=0.01, idle=8000, mode="device")
+    # a long idle: under a loaded host the joiner can take longer to start than the feed lasts
+    a = _spawn(cluster.address, nw=2, slow=0.01, idle=30000, mode="device")
     t0 = time.monotonic()
     while len(cluster.commit_log) < 4 and time.monotonic() - t0 < 60:
         time.sleep(0.05)

@@ -76,10 +76,7 @@ class Tuning:
         prefetch: batches whose H2D is issued ahead of the user (DMA mode).
         copy_streams: HIP side streams for DMA copies (1..8).
         event_every: record a completion event every k slots; None = ring slots / 4, at most 4.
-        coalesce: staged fixed-width batches collated per kernel launch (1..16; 1 disables).
-        varlen_coalesce: the same for var-len and JSON batches decoded on the device from the logs
-            (1..16).  16 by default: their launches (stage, count, parse) cost the main thread more
-            than a fixed-width decode, so larger groups amortise them.
+        coalesce: staged batches collated per kernel launch (1..8; 1 disables).
         coalesce_wait_us: how long to wait for a fuller group while the GPU is busy (0..10000).
         lockstep_depth: cross-rank agreements issued ahead of use (0..64).
         numa_bind: bind the loader (and its workers) to the target GPU's socket.
@@ -109,7 +106,6 @@ class Tuning:
     copy_streams: int = 4
     event_every: Optional[int] = None
     coalesce: int = 8
-    varlen_coalesce: int = 16
     coalesce_wait_us: int = 50
     lockstep_depth: int = 2
     numa_bind: Optional[bool] = None
@@ -140,8 +136,7 @@ class Tuning:
         _check(0 <= int(self.prefetch) <= 64, "prefetch must be in [0, 64]")
         _check(1 <= int(self.copy_streams) <= 8, "copy_streams must be in [1, 8]")
         _check(self.event_every is None or 1 <= int(self.event_every) <= 4096, "event_every must be >= 1 (or None)")
-        _check(1 <= int(self.coalesce) <= 16, "coalesce must be in [1, 16]")
-        _check(1 <= int(self.varlen_coalesce) <= 16, "varlen_coalesce must be in [1, 16]")
+        _check(1 <= int(self.coalesce) <= 8, "coalesce must be in [1, 8]")
         _check(0 <= int(self.coalesce_wait_us) <= 10_000, "coalesce_wait_us must be in [0, 10000]")
         _check(0 <= int(self.lockstep_depth) <= 64, "lockstep_depth must be in [0, 64]")
         _check(self.ahead_depth is None or 0 <= int(self.ahead_depth) <= 16, "ahead_depth must be in [0, 16]")

@@ -22,10 +22,9 @@ void launch_varlen(const int32_t* offs, const void* vals, int src_dt, void* out,
                    double pad, int64_t* lengths, uint8_t* mask, hipStream_t stream);
 
 // Up to kMaxGroup dense casts (consecutive batches, same dtypes and row width) in one launch.
-// 16: device-parsed JSON / var-len batches group 16 at a time (Tuning.varlen_coalesce), which
-// halves the per-batch launch cost that bounds config 4; fixed-width groups stay at 8 by default.
-// The largest by-value launch struct (VarSpanLaunch) stays under 4 KiB.
-constexpr int kMaxGroup = 16;
+// 8: JSON groups of 16 were tried (config 4: 35-36.6 M rec/s against 38.6-39.1 M for 8, even with
+// a 32-deep ring: the first batch of a group waits longer for its parse kernel; profiles/r04_s6).
+constexpr int kMaxGroup = 8;
 // host_src: the sources are pinned host memory read over PCIe (zero-copy), which sizes the grid.
 void launch_fixed_group(const void* const* srcs, int src_dt, void* const* dsts, int dst_dt, const int64_t* rows, int n,
                         int64_t row, const float* shift, const float* scale, hipStream_t stream, bool host_src);

@@ -188,10 +188,10 @@ const uint8_t* LogPins::seg_src(const tk::SpanSeg& sg, bool* hbm) {
     // pin ahead of the segment so the mirror can copy (and prefetch) whole chunks.  No look-ahead
     // past the written end: the mirror never copies past it.  (A growing log still gets whole
     // chunks registered -- up to the next 64 MiB boundary -- but by the pin thread, not here.)
-    // The look-ahead this replaced registered up to 128 MiB of unwritten log on the launch thread
-    // (20-28 ms) in the two config-4 mirror runs that collapsed in round 3 (profiles/r03_final/
-    // c4_auto_mirror_trial/c4_6.log, profiles/r03_s3/mirror_stability/); whether that was the
-    // cause is for the re-measurement in profiles/r04_* to show.
+    // The look-ahead this replaced registered up to 128 MiB of unwritten log on the launch thread.
+    // It was not what made round 3's config-4 mirror runs collapse: round 4's slow runs registered
+    // nothing in their timed windows (profiles/r04_s1/c4); their launches waited for the copy
+    // stream's whole queue, which LogMirror's no-wait policy removed (profiles/r04_s2, r04_s3).
     const auto& part = broker_->part(sg.pidx);
     const uint64_t written = part.log_end_pos.load(std::memory_order_acquire);
     ensure(sg.pidx, std::min<uint64_t>(std::max<uint64_t>(written, sg.log_pos + sg.len),

@@ -197,8 +197,7 @@ class _Run:
                 if self.table is not None:
                     self.driver.set_worker_sink(self.table.address, L.n_producers, self.table.capacity)
                 self.driver.set_event_every(L._event_every(self.ring.n_slots))
-                self.driver.set_coalesce(int(L.tuning.varlen_coalesce) if L.plan.json_span or L.plan.var_span
-                                         else L.coalesce)
+                self.driver.set_coalesce(L.coalesce)
                 self.driver.set_coalesce_wait_us(L.coalesce_wait_us if L.coalesce > 1 else 0)
                 if L.plan.direct:
                     self.driver.enable_direct()
@@ -407,7 +406,9 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
             ``prefetch`` batches ahead), ``"zerocopy"`` (the collate kernel reads pinned host memory over
             PCIe: two HIP calls per batch instead of five, but the read runs on the compute stream) or
             ``"auto"`` (default: zero-copy for slots up to ``ZERO_COPY_MAX_BYTES``, where a batch is
-            latency-bound; DMA above, where copy/compute overlap matters) or ``"direct"`` (experimental;
+            latency-bound; DMA above, where copy/compute overlap matters; var-len / JSON rows decoded
+            on the device read an HBM mirror of the logs that the copy engines fill, fixed-width rows
+            read the pinned logs in place -- loader/path_plan.py) or ``"direct"`` (experimental;
             fixed-width schemas on the synthetic broker: workers only locate each row in the broker log,
             the main process pins the logs in place and the collate kernel gathers rows straight out of
             them over PCIe, so no worker copies the payload.  Measured slower than "zerocopy" on MI355X
@@ -418,7 +419,6 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
         coalesce: fixed-width batches that are already staged when the next one is requested are
             collated together, up to this many per kernel launch (one allocation, one launch, one
             completion event); the following requests return them without a HIP call.  1 disables.
-            Var-len and JSON batches decoded on the device group by ``varlen_coalesce`` instead (16).
         coalesce_wait_us: while the GPU is still busy with an earlier launch, wait up to this long
             for enough staged batches to fill a group (costs no GPU time; a zero-copy batch takes
             7.1 us alone and 5.2 us in a group of 4).  0 launches whatever is staged at once.

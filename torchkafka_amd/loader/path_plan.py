@@ -110,10 +110,13 @@ class PathPlan:
                 raise ValueError("h2d='direct' needs the synthetic broker (bootstrap_servers shm:// or file://) "
                                  "and a group_id")
             direct = True
-        # Opt-in: h2d='auto' stays zero-copy.  The mirror matches zero-copy on fixed-width decode and
-        # beats it on JSON on most runs (config 4: median 44.7 M rec/s against 39.7 M,
-        # profiles/r03_final/c4_mirror_ab/), but 2 config-4 runs of 33 collapsed (29.7 M and 27.3 M)
-        mirror = h2d == "dma" and (span or json_span or var_span)
+        # The HBM mirror: always with h2d='dma'; with h2d='auto' for JSON and var-len rows.  Since its
+        # launches never wait for a copy (round 4) it beats zero-copy there on every box measured --
+        # config 4: 40.8-45.9 M rec/s over 20 runs (none below 40 M) against 38.8-41.3 M zero-copy,
+        # VarLen tokens 43.3 / 46.2 M against 42.2 / 44.2 M (profiles/r04_s1..s4).  Fixed-width decode
+        # stays zero-copy under 'auto': both run at the PCIe roof (52.5 against 51.5 M), and zero-copy
+        # needs no HBM and no copy engine.
+        mirror = (span or json_span or var_span) if h2d == "dma" else (h2d == "auto" and (json_span or var_span))
         return cls(cuda=cuda, kind=kind, process_overridden=process_overridden, span=span, var_span=var_span,
                    json_span=json_span, json_device=json_device, json_count=json_count, mirror=mirror,
                    direct=direct, fast_path=fast_path, varlen_fast=fast_common and kind in (1, 2), h2d=h2d)
