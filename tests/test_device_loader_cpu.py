@@ -497,3 +497,82 @@ def test_ascii_keys_and_schema_validation():
         _ = FixedWidth() + Key() + Key()
     with pytest.raises(TypeError):
         _ = VarLen() + Timestamp()
+
+
+def test_native_loop_bad_verdict_commits_the_batches_before_and_never_yields(monkeypatch):
+    """The fast stages return status -5 when the delivered batch's device verdict is bad
+    (verify='deliver', torch_step.cpp verdict_bad): the loop commits what the user finished, then
+    raises CorruptRecordException without yielding that batch.  A fake driver scripts the stage."""
+    from collections import defaultdict
+
+    import torchkafka_amd.loader.device_loader as dlm
+    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset
+    from torchkafka_amd.client.errors import CorruptRecordException
+
+    class DS(KafkaDataset):
+        schema = FixedWidth(torch.float32, (4,))
+
+    dl = DeviceLoader(DS.placeholder(), 4, num_workers=1, device="cpu")
+    assert dl.plan.fast_path and dl.verify == "deliver"
+
+    class Drv:
+        def __init__(self):
+            self.calls = []
+
+        def set_sync_commit(self, s):
+            self.calls.append(("sync", s))
+
+        def verify_delivered(self):
+            raise AssertionError("the fast stages verify natively")
+
+        def parse_error(self):
+            return "RecordBatch CRC32C mismatch"
+
+        def commit_pending(self):
+            self.calls.append("commit")
+            return 1
+
+        def finish_delivered(self, stream):
+            self.calls.append("finish")
+
+        def finish_lockstep(self):
+            self.calls.append("finish_lockstep")
+
+        def drain_fenced(self, wait):
+            pass
+
+        def take_pending(self):
+            return []
+
+        def stats(self):
+            st = defaultdict(int)
+            st["commit_ns"] = []
+            return st
+
+        def committed(self):
+            return []
+
+        def reset_stats(self):
+            pass
+
+    class Run:
+        driver = Drv()
+        closed = False
+
+        def _check_workers_native(self):
+            pass
+
+        def close(self):
+            Run.closed = True
+
+    script = iter([(1, 0, "b0"), (1, 0, "b1"), (-5, 0, None), (1, 0, "never")])
+    monkeypatch.setattr(dlm, "_stream_ptr", lambda device: 0)
+    monkeypatch.setattr(DeviceLoader, "_fixed_stage", lambda self, drv, native_ac: (lambda: next(script)))
+    got = []
+    with pytest.raises(CorruptRecordException, match="CRC32C"):
+        for b in dl._iterate_native(Run(), auto_commit=True):
+            got.append(b)
+    assert got == ["b0", "b1"]
+    calls = Run.driver.calls
+    assert calls.count("commit") == 1 and "finish_lockstep" not in calls  # b0/b1 committed, no clean end
+    assert Run.closed
