@@ -72,6 +72,7 @@ def test_launcher_fixed_width_same_batches_values_and_commits(broker):
         assert dl.plan.span
         assert broker.committed_offsets(f"g{int(lt)}", "t") == {p: 2000 for p in range(4)}
         assert dl.stats.batches == 125
+        assert dl.stats.ahead_ns > 0  # groups were decoded ahead (by the launcher thread when lt)
     _same(runs[False], runs[True])
     x = torch.cat(runs[True]).cpu()
     seen = {(int(r[1]), int(r[0])) for r in x}
@@ -91,6 +92,7 @@ def test_launcher_json_same_batches_and_commits(broker):
         runs[lt], dl = _run(broker, "j", DS, 256, f"g{int(lt)}", lt, num_workers=1, in_order=True,
                             dtype=torch.bfloat16)
         assert dl.plan.json_span and dl.plan.mirror  # the default JSON path: HBM mirror
+        assert dl.stats.ahead_ns > 0
         assert broker.committed_offsets(f"g{int(lt)}", "j") == {0: 1500, 1: 1500}
     _same(runs[False], runs[True])
 

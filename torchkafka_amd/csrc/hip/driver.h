@@ -299,7 +299,8 @@ class MainDriver {
   } step_lock;
   std::shared_ptr<void> launcher;      // the launcher thread while it runs (joined when reset)
   std::atomic<bool> launcher_on{false};
-  hipStream_t user_stream = nullptr;  // the stream the user takes batches on (published by each step)
+  hipStream_t user_stream = nullptr;  // the stream the user takes batches on (published by each step;
+  bool user_stream_known = false;     // null is the default stream, hence the flag)
 
  private:
   // --- launched slots and their completion events

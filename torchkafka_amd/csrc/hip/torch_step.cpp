@@ -573,15 +573,18 @@ struct Launcher {
       const auto& v = d.varlen;
       const auto opts = at::TensorOptions().dtype(scalar_type_of(json ? v.dst_dt : f.dst_dt)).device(at::kCUDA, dev);
       hipStream_t cur = nullptr;
+      bool have = false;
       int idle = 0;
       while (!stop.load(std::memory_order_relaxed)) {
         int n = 0;
         {
           std::lock_guard<MainDriver::StepLock> g(d.step_lock);
-          if (d.user_stream) {
-            if (d.user_stream != cur) {  // allocations below are recorded on the user's stream
+          if (d.user_stream_known) {
+            if (!have || d.user_stream != cur) {  // allocations below are recorded on the user's stream
               cur = d.user_stream;
-              c10::hip::setCurrentHIPStream(c10::hip::getStreamFromExternal(cur, dev));
+              have = true;
+              c10::hip::setCurrentHIPStream(cur ? c10::hip::getStreamFromExternal(cur, dev)
+                                                : c10::hip::getDefaultHIPStream(dev));
             }
             const int64_t t0 = tk::now_ns();
             n = json ? launch_ahead_json(d, v.dst_dt, v.pad, v.pad_to, v.pad_multiple, v.want_mask, dev)
@@ -623,6 +626,7 @@ struct StepTurn {
     }
     held = true;
     d.user_stream = us;
+    d.user_stream_known = true;
   }
   ~StepTurn() {
     if (held) d.step_lock.unlock();
@@ -692,6 +696,7 @@ void register_torch_step(py::module_& m) {
       [](MainDriver& d, bool row_span) {
         if (d.launcher) throw std::logic_error("start_launcher: already running");
         d.user_stream = nullptr;
+        d.user_stream_known = false;
         d.launcher = std::make_shared<Launcher>(d, row_span);
         d.launcher_on.store(true, std::memory_order_release);
       },
