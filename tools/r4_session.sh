@@ -84,18 +84,6 @@ for s in ${STEPS:-smoke benchdrv}; do
             run c4_g16s32_$rep 200 python benchmarks/config4_json_varlen.py --varlen-coalesce 16 --slots-per-worker 32 &&
             run c4_g8s32_$rep 200 python benchmarks/config4_json_varlen.py --varlen-coalesce 8 --slots-per-worker 32
           done; grep -o '"value": [0-9]*' "$OUT"/c4_g*.log ;;
-    pytestlaunch) run pytest_launch 300 python -u -m pytest tests/test_gpu_launcher.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
-    ablaunch) for rep in 1 2 3; do
-            run c4_base_$rep 200 python benchmarks/config4_json_varlen.py &&
-            TORCHKAFKA_LAUNCH_THREAD=1 run c4_lt_$rep 200 python benchmarks/config4_json_varlen.py
-          done
-          for rep in 1 2; do
-            run bench_base_$rep 300 python bench.py --steps 20 --warmup 5 --steady-steps 20000 --extra-blocks "" --bridge-steps 0 --config-blocks "" &&
-            TORCHKAFKA_LAUNCH_THREAD=1 run bench_lt_$rep 300 python bench.py --steps 20 --warmup 5 --steady-steps 20000 --extra-blocks "" --bridge-steps 0 --config-blocks ""
-          done
-          run tokens_base 300 python benchmarks/varlen_tokens.py && TORCHKAFKA_LAUNCH_THREAD=1 run tokens_lt 300 python benchmarks/varlen_tokens.py
-          run c5_base 200 python benchmarks/config5_large_messages.py && TORCHKAFKA_LAUNCH_THREAD=1 run c5_lt 200 python benchmarks/config5_large_messages.py
-          grep -o '"value": [0-9.]*' "$OUT"/c4_base_*.log "$OUT"/c4_lt_*.log "$OUT"/bench_*.log "$OUT"/tokens_*.log "$OUT"/c5_*.log ;;
     kernarg) run kernarg 60 tools/probes/kernarg_probe ;;
     pytestgpu) run pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 180 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -30,7 +30,6 @@ TUNING_ENV = {
     "decode_streams": "TORCHKAFKA_DECODE_STREAMS",
     "span_burst": "TORCHKAFKA_SPAN_BURST",
     "worker_spin_us": "TORCHKAFKA_WORKER_SPIN_US",
-    "launch_thread": "TORCHKAFKA_LAUNCH_THREAD",  # "1" enables it
 }
 
 #: process-wide switches read once by the native libraries or at import (not per loader)
@@ -94,9 +93,6 @@ class Tuning:
             tools/mirror_probe.sh, tools/mirror_probe2.sh.
         group_mib: device-decode groups stop growing at this many MiB of log bytes (1..1024): a
             group's batches become committable together, so large batches form small groups.
-        launch_thread: device-decode fast paths (no lockstep, ``commit="async"``): a native thread
-            forms, allocates and launches the groups decoded ahead of delivery, beside the thread
-            that hands the batches out (csrc/hip/torch_step.cpp ``Launcher``).  Off by default.
         json_count: JsonArray rows parsed on the device from the logs: who counts their elements.
             'auto' / 'device': the gfx950 stage kernel, while it stages the text (the workers read
             only record headers; the batch width is a device max); 'host': the workers pre-scan
@@ -121,7 +117,6 @@ class Tuning:
     mirror_chunks: int = 6
     group_mib: int = 16
     json_count: str = "auto"
-    launch_thread: Optional[bool] = None
 
     def __post_init__(self):
         # environment defaults for fields left at None
@@ -132,8 +127,7 @@ class Tuning:
                 setattr(self, name, _env_int(TUNING_ENV[name], None))
         if self.worker_spin_us is None:
             self.worker_spin_us = 200
-        if self.launch_thread is None:
-            self.launch_thread = os.environ.get(TUNING_ENV["launch_thread"], "0") == "1"
+
         self.validate()
 
     def validate(self) -> None:
@@ -154,7 +148,6 @@ class Tuning:
         _check(2 <= int(self.mirror_chunks) <= 64, "mirror_chunks must be in [2, 64]")
         _check(1 <= int(self.group_mib) <= 1024, "group_mib must be in [1, 1024]")
         _check(self.json_count in ("auto", "device", "host"), "json_count must be 'auto', 'device' or 'host'")
-        _check(isinstance(self.launch_thread, bool), "launch_thread must be True or False")
 
 
 _CHOICES = {

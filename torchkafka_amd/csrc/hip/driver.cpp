@@ -50,7 +50,6 @@ MainDriver::MainDriver(Engine* engine, const std::string& ring_name, const std::
 }
 
 MainDriver::~MainDriver() {
-  launcher.reset();  // its thread uses everything below
   pins_.reset();  // pinned log ranges first: the kernels that read them completed (slots drained by the caller)
   if (stage_dev_) {
     hipDeviceSynchronize();

@@ -14,9 +14,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
-#include <sched.h>
 
-#include <atomic>
 #include <cstdlib>
 
 #include <deque>
@@ -280,27 +278,6 @@ class MainDriver {
     bool verify = false;
   } varlen;
   int64_t fast_batches_ = 0, fast_records_ = 0, fast_ns_ = 0;
-
-  // Ahead launches on a thread of their own (torch_step.cpp Launcher, Tuning.launch_thread):
-  // while it runs, the fast-path steps and that thread take turns on the driver under step_lock
-  // (a test-and-test-and-set lock: a turn lasts microseconds, a futex round trip would cost more).
-  struct StepLock {
-    std::atomic<bool> held{false};
-    void lock() {
-      for (int i = 0;; ++i) {
-        if (!held.load(std::memory_order_relaxed) && !held.exchange(true, std::memory_order_acquire)) return;
-        if (i < 4096)
-          tk::cpu_relax();
-        else
-          sched_yield();
-      }
-    }
-    void unlock() { held.store(false, std::memory_order_release); }
-  } step_lock;
-  std::shared_ptr<void> launcher;      // the launcher thread while it runs (joined when reset)
-  std::atomic<bool> launcher_on{false};
-  hipStream_t user_stream = nullptr;  // the stream the user takes batches on (published by each step;
-  bool user_stream_known = false;     // null is the default stream, hence the flag)
 
  private:
   // --- launched slots and their completion events

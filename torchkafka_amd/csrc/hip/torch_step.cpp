@@ -15,11 +15,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
-#include <atomic>
 #include <ctime>
-#include <mutex>
-#include <string>
-#include <thread>
 
 #include "consumer.h"
 #include "driver.h"
@@ -158,8 +154,8 @@ at::Tensor alloc_group(MainDriver& d, const std::vector<int64_t>& shape, const a
 
 // Device decode ahead of delivery (MainDriver::ahead_begin): up to three full groups of staged
 // batches are decoded while the user still works on earlier ones.  Pure C++ (ATen allocations,
-// driver calls): the caller does not hold the GIL -- the step functions release it around the
-// call, and the launcher thread never has it.  Returns the groups launched.
+// driver calls): the step functions release the GIL once around the call.  Returns the groups
+// launched.
 int launch_ahead(MainDriver& d, const std::vector<int64_t>& row_shape, const at::TensorOptions& opts,
                  c10::DeviceIndex dev, int dst_dt, const float* shift, const float* scale, int extras) {
   std::vector<int64_t> rows;
@@ -193,23 +189,19 @@ int launch_ahead(MainDriver& d, const std::vector<int64_t>& row_shape, const at:
 // launching, behind its kernel, the groups the workers finish meanwhile (`ahead`).  Waiting in
 // MainDriver::verify_delivered instead leaves them staged until the next request, so with a
 // shallow ring (config 5: 4 slots of 8 MiB) the GPU idled between each verdict and the next
-// launch.  With the launcher thread running, the wait leaves the driver to it instead (the step
-// lock is released while pausing).  The caller's verify_delivered() then only reads the verdict.
-// Called without the GIL.
+// launch.  The caller's verify_delivered() then only reads the known verdict.  Called without
+// the GIL.
 template <class Ahead>
 void verify_ahead(MainDriver& d, Ahead&& ahead) {
   const int64_t t0 = tk::now_ns();
-  const bool launcher = d.launcher_on.load(std::memory_order_relaxed);
   while (!d.delivered_verdict_known()) {
-    if (launcher) d.step_lock.unlock();
-    else ahead();
+    ahead();
     if (tk::now_ns() - t0 < 200000) {
       for (int k = 0; k < 64; ++k) tk::cpu_relax();
     } else {
       timespec ts{0, 20000};
       nanosleep(&ts, nullptr);
     }
-    if (launcher) d.step_lock.lock();
   }
   d.verify_wait_ns_ += tk::now_ns() - t0;
 }
@@ -381,11 +373,9 @@ py::tuple step_once(MainDriver& d, const MainDriver::FastConfig& cfg) {
   }
   if (d.last.kind == uint32_t(tk::kPackRecordSpan)) {
     py::gil_scoped_release nogil;
-    if (!d.launcher_on.load(std::memory_order_relaxed)) {  // else the launcher thread does it
-      const int64_t ta = tk::now_ns();
-      launch_ahead(d, cfg.shape, opts, dev, cfg.dst_dt, cfg.shift, cfg.scale, cfg.extras);
-      d.ahead_ns_ += tk::now_ns() - ta;
-    }
+    const int64_t ta = tk::now_ns();
+    launch_ahead(d, cfg.shape, opts, dev, cfg.dst_dt, cfg.shift, cfg.scale, cfg.extras);
+    d.ahead_ns_ += tk::now_ns() - ta;
     if (cfg.verify)
       verify_ahead(d, [&] { launch_ahead(d, cfg.shape, opts, dev, cfg.dst_dt, cfg.shift, cfg.scale, cfg.extras); });
   }
@@ -520,11 +510,9 @@ py::tuple varlen_step(MainDriver& d, const MainDriver::VarlenConfig& c) {
   }
   if (row_span_kind(v.kind)) {
     py::gil_scoped_release nogil;
-    if (!d.launcher_on.load(std::memory_order_relaxed)) {  // else the launcher thread does it
-      const int64_t ta = tk::now_ns();
-      launch_ahead_json(d, dst_dt, pad, pad_to, pad_multiple, want_mask, dev);
-      d.ahead_ns_ += tk::now_ns() - ta;
-    }
+    const int64_t ta = tk::now_ns();
+    launch_ahead_json(d, dst_dt, pad, pad_to, pad_multiple, want_mask, dev);
+    d.ahead_ns_ += tk::now_ns() - ta;
     if (verify)
       verify_ahead(d, [&] { launch_ahead_json(d, dst_dt, pad, pad_to, pad_multiple, want_mask, dev); });
   }
@@ -540,98 +528,6 @@ py::tuple varlen_step(MainDriver& d, const MainDriver::VarlenConfig& c) {
                              : py::make_tuple(o, l);
   return py::make_tuple(r, cs, item);
 }
-
-// Ahead launches on a thread of their own (Tuning.launch_thread).  On the device-decode fast
-// paths the main thread spends about half of each step forming, allocating and launching the
-// groups of batches it will hand out later (config 4: 2.7 of 6.3 us per step).  The launcher thread
-// does that instead: it and the step functions take turns on the driver under
-// MainDriver::step_lock (every driver call of a step, and each launch_ahead call, runs under it),
-// so the main thread's steps shrink to taking decoded batches, committing and waking the GPU work
-// the user queues, while the next groups are launched beside them.  All HIP calls of both threads
-// still happen under the lock, one thread at a time.  The thread allocates the groups' outputs as
-// the main thread would (on a decode stream, recorded on the user's stream, which each step
-// publishes in MainDriver::user_stream).  Started and stopped by DeviceLoader around a fast-path
-// iteration without lockstep, synchronous commits or commit logging.
-struct Launcher {
-  MainDriver& d;
-  const bool json;  // row-span batches (JSON / var-len) rather than fixed-width
-  std::atomic<bool> stop{false}, failed{false};
-  std::string error;
-  std::thread th;
-
-  Launcher(MainDriver& drv, bool row_span) : d(drv), json(row_span) { th = std::thread([this] { run(); }); }
-  ~Launcher() {
-    stop.store(true, std::memory_order_relaxed);
-    if (th.joinable()) th.join();
-  }
-
-  void run() {
-    try {
-      const auto dev = c10::DeviceIndex(json ? d.varlen.device : d.fast.device);
-      if (hipSetDevice(dev) != hipSuccess) throw std::runtime_error("hipSetDevice failed");
-      const auto& f = d.fast;
-      const auto& v = d.varlen;
-      const auto opts = at::TensorOptions().dtype(scalar_type_of(json ? v.dst_dt : f.dst_dt)).device(at::kCUDA, dev);
-      hipStream_t cur = nullptr;
-      bool have = false;
-      int idle = 0;
-      while (!stop.load(std::memory_order_relaxed)) {
-        int n = 0;
-        {
-          std::lock_guard<MainDriver::StepLock> g(d.step_lock);
-          if (d.user_stream_known) {
-            if (!have || d.user_stream != cur) {  // allocations below are recorded on the user's stream
-              cur = d.user_stream;
-              have = true;
-              c10::hip::setCurrentHIPStream(cur ? c10::hip::getStreamFromExternal(cur, dev)
-                                                : c10::hip::getDefaultHIPStream(dev));
-            }
-            const int64_t t0 = tk::now_ns();
-            n = json ? launch_ahead_json(d, v.dst_dt, v.pad, v.pad_to, v.pad_multiple, v.want_mask, dev)
-                     : launch_ahead(d, f.shape, opts, dev, f.dst_dt, f.shift, f.scale, f.extras);
-            if (n) d.ahead_ns_ += tk::now_ns() - t0;
-          }
-        }
-        if (n) {
-          idle = 0;
-          continue;
-        }
-        if (++idle < 64) {
-          for (int k = 0; k < 64; ++k) tk::cpu_relax();
-        } else {
-          timespec ts{0, 20000};
-          nanosleep(&ts, nullptr);
-        }
-      }
-    } catch (const std::exception& e) {
-      error = e.what();
-      failed.store(true, std::memory_order_release);
-    }
-  }
-};
-
-// A fast-path step with the launcher running: publishes the user's stream and holds the step lock
-// (taken without the GIL) for the step's duration; reports a launcher failure.
-struct StepTurn {
-  MainDriver& d;
-  bool held = false;
-  explicit StepTurn(MainDriver& drv, int device) : d(drv) {
-    if (!d.launcher_on.load(std::memory_order_relaxed)) return;
-    const auto* L = static_cast<const Launcher*>(d.launcher.get());
-    if (L && L->failed.load(std::memory_order_acquire)) throw std::runtime_error("ahead launcher: " + L->error);
-    hipStream_t us = c10::hip::getCurrentHIPStream(c10::DeviceIndex(device)).stream();
-    {
-      py::gil_scoped_release nogil;
-      d.step_lock.lock();
-    }
-    held = true;
-    d.user_stream = us;
-    d.user_stream_known = true;
-  }
-  ~StepTurn() {
-    if (held) d.step_lock.unlock();
-  }
-};
 
 }  // namespace
 
@@ -664,7 +560,6 @@ void register_torch_step(py::module_& m) {
       py::arg("verify") = false);
   cls.def("fast_next", [](MainDriver& d) -> py::tuple {
     const int64_t t0 = tk::now_ns();
-    StepTurn turn(d, d.fast.device);
     py::tuple res = step_once(d, d.fast);
     const int64_t r = res[0].cast<int64_t>();
     if (r > 0) {
@@ -686,27 +581,7 @@ void register_torch_step(py::module_& m) {
       },
       py::arg("device"), py::arg("dst_dt"), py::arg("pad_to"), py::arg("pad_multiple"), py::arg("pad"),
       py::arg("want_mask"), py::arg("auto_commit"), py::arg("timeout_ms"), py::arg("verify") = false);
-  cls.def("varlen_fast_next", [](MainDriver& d) {
-    StepTurn turn(d, d.varlen.device);
-    return varlen_step(d, d.varlen);
-  });
-  // Ahead launches on their own thread for the configured fast path (see Launcher).
-  cls.def(
-      "start_launcher",
-      [](MainDriver& d, bool row_span) {
-        if (d.launcher) throw std::logic_error("start_launcher: already running");
-        d.user_stream = nullptr;
-        d.user_stream_known = false;
-        d.launcher = std::make_shared<Launcher>(d, row_span);
-        d.launcher_on.store(true, std::memory_order_release);
-      },
-      py::arg("row_span"));
-  cls.def("stop_launcher", [](MainDriver& d) {
-    py::gil_scoped_release nogil;
-    d.launcher.reset();  // joins the thread (it finishes the launch it is in)
-    d.launcher_on.store(false, std::memory_order_release);
-  });
-
+  cls.def("varlen_fast_next", [](MainDriver& d) { return varlen_step(d, d.varlen); });
   m.def(
       "step_fixed_tensor",
       [](MainDriver& d, int device, std::vector<int64_t> shape, int dst_dt, int64_t row, uintptr_t shift,

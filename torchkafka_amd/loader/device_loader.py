@@ -816,12 +816,6 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
         sync = auto_commit and self.commit_mode == "sync"
         drv.set_sync_commit(sync)
         verify = self.verify == "deliver"
-        # ahead launches on their own native thread (Tuning.launch_thread): only where every driver
-        # call of the loop is the fast stage's own (no lockstep, no per-step commits from Python)
-        launcher = (self.tuning.launch_thread and self.plan.device_decode and not py_commits and not sync
-                    and not log_commits and not drv.lockstep_enabled)
-        if launcher:
-            drv.start_launcher(not self.plan.fast_path)
         completed = delivered = False
         wait_since = None
         try:
@@ -863,8 +857,6 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
             completed = True
         finally:
             try:
-                if launcher:
-                    drv.stop_launcher()
                 drv.finish_delivered(_stream_ptr(self.device))
                 if completed:
                     drv.finish_lockstep()
