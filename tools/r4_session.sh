@@ -86,6 +86,7 @@ for s in ${STEPS:-smoke benchdrv}; do
           done; grep -o '"value": [0-9]*' "$OUT"/c4_g*.log ;;
     pmcjson) pmc pmc_json 120 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_json" -o run -- python3 "$R/benchmarks/config4_json_varlen.py" --steps 3000 ;;
     profjson) prof profjson 300 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profjson" -o run -- python3 "$R/benchmarks/config4_json_varlen.py" ;;
+    launchcost) run launch_cost 60 tools/probes/launch_cost_probe ;;
     kernarg) run kernarg 60 tools/probes/kernarg_probe ;;
     pytestgpu) run pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 180 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
