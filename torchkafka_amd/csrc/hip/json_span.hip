@@ -40,18 +40,6 @@ constexpr int kRowsPerThread = kMaxRows / kThreads;
 __device__ __forceinline__ uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
 __device__ __forceinline__ bool is_ws(uint32_t c) { return c == 32u || c == 9u || c == 10u || c == 13u; }
 
-// 16 bytes of a row's text from the LDS image (any alignment: 5-dword window + v_alignbyte).
-__device__ __forceinline__ uint4 load16(const uint32_t* b32, int32_t b0) {
-  const int32_t w = b0 >> 2, sh = b0 & 3;
-  const uint32_t x0 = b32[w], x1 = b32[w + 1], x2 = b32[w + 2], x3 = b32[w + 3], x4 = b32[w + 4];
-  uint4 v;
-  v.x = __builtin_amdgcn_alignbyte(x1, x0, sh);
-  v.y = __builtin_amdgcn_alignbyte(x2, x1, sh);
-  v.z = __builtin_amdgcn_alignbyte(x3, x2, sh);
-  v.w = __builtin_amdgcn_alignbyte(x4, x3, sh);
-  return v;
-}
-
 // One wave runs json_scan_simple's rules on a device-counted row's T bytes (csrc/core/consumer.cpp
 // json_scan_impl, bit for bit): whitespace trimmed, '[' ... ']' framing, an interior of number
 // characters [0-9.-], commas and whitespace only, no run of more than 16 number characters.
@@ -238,7 +226,7 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
       continue;
     }
     uint8_t* __restrict__ o = bo.stage + dst[rr];
-    for (int32_t c = 16 * lane; c < T; c += 64 * 16) *reinterpret_cast<uint4*>(o + c) = load16(b32, r0 + c);
+    for (int32_t c = 16 * lane; c < T; c += 64 * 16) *reinterpret_cast<uint4*>(o + c) = span::lds16(b32, r0 + c);
     if (lane == 0) {
       // a device-counted row (count kJsonCountOnDevice) keeps that count here: json_count_kernel
       // scans its staged text and completes the descriptor before json_rows_kernel reads it

@@ -10,9 +10,9 @@
 // (span_device.h), then
 //   values: a wave per row for rows of >= 32 16-byte groups (lanes over the row's groups
 //   held by this segment), else (row, group) pairs strided over the block; each group is
-//   read as a 5-dword window + v_alignbyte (values sit at arbitrary byte offsets behind
-//   their varint headers), converted (dtypes.h: bit-exact with Tensor.to), stored 8-16 B
-//   per lane.
+//   read as two aligned 16-byte LDS reads cut to the group's bytes (span::lds16: values sit
+//   at arbitrary byte offsets behind their varint headers), converted (dtypes.h: bit-exact
+//   with Tensor.to), stored 8-16 B per lane.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -97,12 +97,9 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
       if (b0 + nel * int32_t(sizeof(S)) <= lo_b || b0 >= hi_b) return;  // group held by another segment
       D* __restrict__ orow = out + int64_t(row_begin + rr) * RE;
       if (nel == kPer && b0 >= lo_b && b0 + 16 <= hi_b) {
-        const int32_t w = b0 >> 2, sh = b0 & 3;
-        const uint32_t x0 = b32[w], x1 = b32[w + 1], x2 = b32[w + 2], x3 = b32[w + 3], x4 = b32[w + 4];
-        const uint32_t o[4] = {__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
-                               __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
+        const uint4 o = span::lds16(b32, b0);
         S sv[kPer];
-        __builtin_memcpy(sv, o, 16);
+        __builtin_memcpy(sv, &o, 16);
         Vec<D, kPer> ov;
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
@@ -241,18 +238,14 @@ __global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, 
       off_seg = true;  // the row table disagrees with the segment: read nothing, never commit
       n_out = 0;
     }
-    // 16 source bytes per lane per step (a 5-dword window + v_alignbyte: values sit at any byte
-    // offset behind their headers), vector stores when the row is aligned; then the tail
+    // 16 source bytes per lane per step (span::lds16: values sit at any byte offset behind their
+    // headers), vector stores when the row is aligned; then the tail
     constexpr int kPer = 16 / int(sizeof(S));
     const int64_t full = bo.reserved ? n_out / kPer * kPer : 0;
     for (int64_t e0 = int64_t(lane) * kPer; e0 < full; e0 += 64 * kPer) {
-      const int32_t b0 = r0 + int32_t(e0) * int32_t(sizeof(S));
-      const int32_t w = b0 >> 2, sh = b0 & 3;
-      const uint32_t x0 = b32[w], x1 = b32[w + 1], x2 = b32[w + 2], x3 = b32[w + 3], x4 = b32[w + 4];
-      const uint32_t o[4] = {__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
-                             __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
+      const uint4 o = span::lds16(b32, r0 + int32_t(e0) * int32_t(sizeof(S)));
       S sv[kPer];
-      __builtin_memcpy(sv, o, 16);
+      __builtin_memcpy(sv, &o, 16);
       Vec<D, kPer> ov;
 #pragma unroll
       for (int k = 0; k < kPer; ++k) ov.v[k] = C::apply(sv[k], 0.f, 1.f, false);

@@ -32,6 +32,30 @@ constexpr int kFront = 16;  // LDS image offset: boundary reads may start up to 
 constexpr int kLoads = int((tk::kSpanSegMax + 32) / 16 / kThreads) + 1;
 constexpr int kBufBytes = kFront + int(tk::kSpanSegMax) + 64;
 
+// 16 bytes at LDS byte b0 of a 16-byte aligned image (any alignment of b0), for loops whose
+// lanes read consecutive 16-byte pieces: two 16-byte-aligned ds_read_b128 per lane -- consecutive
+// slots across the wave, conflict-free -- and the unaligned 16 bytes cut out of those 32 in
+// registers.  Five ds_read_b32 at a 16-byte lane stride (the 5-dword window used before) cost a
+// 4-way bank conflict each: banks (a/4) mod 32 in 32-lane groups (MI355X_MICROARCH.md §LDS).
+// Reads up to the 16-byte boundary at or below b0 + 31: the image keeps 64 spare bytes at its end.
+__device__ __forceinline__ uint4 lds16(const uint32_t* b32, int32_t b0) {
+  const int32_t a = b0 & ~15, q = (b0 >> 2) & 3, sh = b0 & 3;
+  const uint4 lo = *reinterpret_cast<const uint4*>(b32 + (a >> 2));
+  const uint4 hi = *reinterpret_cast<const uint4*>(b32 + (a >> 2) + 4);
+  // dwords q .. q + 4 of lo:hi
+  const uint32_t d0 = q == 0 ? lo.x : q == 1 ? lo.y : q == 2 ? lo.z : lo.w;
+  const uint32_t d1 = q == 0 ? lo.y : q == 1 ? lo.z : q == 2 ? lo.w : hi.x;
+  const uint32_t d2 = q == 0 ? lo.z : q == 1 ? lo.w : q == 2 ? hi.x : hi.y;
+  const uint32_t d3 = q == 0 ? lo.w : q == 1 ? hi.x : q == 2 ? hi.y : hi.z;
+  const uint32_t d4 = q == 0 ? hi.x : q == 1 ? hi.y : q == 2 ? hi.z : hi.w;
+  uint4 v;
+  v.x = __builtin_amdgcn_alignbyte(d1, d0, sh);
+  v.y = __builtin_amdgcn_alignbyte(d2, d1, sh);
+  v.z = __builtin_amdgcn_alignbyte(d3, d2, sh);
+  v.w = __builtin_amdgcn_alignbyte(d4, d3, sh);
+  return v;
+}
+
 __device__ __forceinline__ uint32_t keep_from(int32_t a, int32_t c) {
   // bytes of the dword at address a whose address is >= c
   const int32_t d = c - a;
