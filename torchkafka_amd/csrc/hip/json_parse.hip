@@ -57,7 +57,9 @@ __device__ __forceinline__ D pad_value(float p) { return Store<D>::cvt(p); }
 template <typename D>
 __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kWin + 32];  // + the 32-byte token reads
-  __shared__ uint16_t starts[kMaxTok];
+  // one dword per token start: 16-bit entries put two lanes' stores on one dword, which the LDS
+  // serialises (46 % of this kernel's LDS cycles were bank conflicts with uint16_t, r04_s10)
+  __shared__ uint32_t starts[kMaxTok];
   __shared__ int s_wsum[kWaves];
   __shared__ int s_cut, s_bad;
 
@@ -143,7 +145,10 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
       }
       const int lim = wlen - b0;  // valid bytes of this thread (may be <= 0 or > 8)
       if (lim < 8) tokm &= lim <= 0 ? 0u : ((1u << lim) - 1u);
-      const uint32_t pc = b0 > 0 && b0 <= wlen ? buf[b0 - 1] : uint32_t(',');
+      // the byte before this thread's 8: the last byte of the previous lane's (a shuffle, not a
+      // byte read at an 8-byte lane stride, which is a 2-way bank conflict); lane 0 reads it
+      const uint32_t pw = __shfl_up(cw.y, 1, kWave) >> 24;
+      const uint32_t pc = b0 > 0 && b0 <= wlen ? (lane == 0 ? uint32_t(buf[b0 - 1]) : pw) : uint32_t(',');
       const uint32_t prev_tok = uint32_t(pc - 0x2Du <= 0x0Cu);
       uint32_t m = tokm & ~((tokm << 1) | prev_tok);
       // only tokens at or after pend (pend itself starts a token when it is a number character)
@@ -175,7 +180,7 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
       while (m) {
         const int j = __ffs(m) - 1;
         m &= m - 1;
-        starts[idx++] = uint16_t(b0 + j);
+        starts[idx++] = uint32_t(b0 + j);
       }
       __syncthreads();
       // 2. parse; only the window's last token can be cut
