@@ -178,6 +178,7 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
   });
   __syncthreads();
   const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
+  const uint4* b128 = reinterpret_cast<const uint4*>(buf);  // 16-byte slots (span::lds16)
   const int32_t lo_b = kFront + head, hi_b = kFront + head + int32_t(len);
 
   // ---- 2. CRC32C lanes (the verdict comes last)
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
       continue;
     }
     uint8_t* __restrict__ o = bo.stage + dst[rr];
-    for (int32_t c = 16 * lane; c < T; c += 64 * 16) *reinterpret_cast<uint4*>(o + c) = span::lds16(b32, r0 + c);
+    for (int32_t c = 16 * lane; c < T; c += 64 * 16) *reinterpret_cast<uint4*>(o + c) = span::lds16(b128, r0 + c);
     if (lane == 0) {
       // a device-counted row (count kJsonCountOnDevice) keeps that count here: json_count_kernel
       // scans its staged text and completes the descriptor before json_rows_kernel reads it

@@ -26,8 +26,12 @@ __device__ __constant__ double kP10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1
 // window end (parsed again in the next window).
 __device__ __forceinline__ int parse_token_regs(const uint8_t* buf, int s, int avail, bool last_window, float* out) {
   const int A = s & ~15;
-  const uint4 lo = *reinterpret_cast<const uint4*>(buf + A);
-  const uint4 hi = *reinterpret_cast<const uint4*>(buf + A + 16);
+  // two whole ds_read_b128 (nontemporal: a no-op hint for LDS that keeps the compiler from
+  // narrowing them to the dwords it can prove are used, as ds_read2_b32 pairs)
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const v4u lv = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(buf + A));
+  const v4u hv = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(buf + A + 16));
+  const uint4 lo = make_uint4(lv.x, lv.y, lv.z, lv.w), hi = make_uint4(hv.x, hv.y, hv.z, hv.w);
   const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
   const int o = s - A, q = o >> 2;
   const uint32_t sh = uint32_t(o & 3) * 8u;

@@ -78,6 +78,7 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
   });
   __syncthreads();
   const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
+  const uint4* b128 = reinterpret_cast<const uint4*>(buf);  // 16-byte slots (span::lds16)
   const int32_t lo_b = kFront + head, hi_b = kFront + head + int32_t(len);  // valid LDS bytes
 
   // ---- 2. CRC32C lanes
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
       if (b0 + nel * int32_t(sizeof(S)) <= lo_b || b0 >= hi_b) return;  // group held by another segment
       D* __restrict__ orow = out + int64_t(row_begin + rr) * RE;
       if (nel == kPer && b0 >= lo_b && b0 + 16 <= hi_b) {
-        const uint4 o = span::lds16(b32, b0);
+        const uint4 o = span::lds16(b128, b0);
         S sv[kPer];
         __builtin_memcpy(sv, &o, 16);
         Vec<D, kPer> ov;
@@ -220,6 +221,7 @@ __global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, 
   });
   __syncthreads();
   const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
+  const uint4* b128 = reinterpret_cast<const uint4*>(buf);  // 16-byte slots (span::lds16)
   const int32_t lo_b = kFront + head, hi_b = kFront + head + int32_t(len);
   const uint32_t* shift_set = nullptr;
   if (do_crc) shift_set = span::crc_lanes(b32, tab, a.tabs, lo_b, hi_b, flags, wcrc);
@@ -243,7 +245,7 @@ __global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, 
     constexpr int kPer = 16 / int(sizeof(S));
     const int64_t full = bo.reserved ? n_out / kPer * kPer : 0;
     for (int64_t e0 = int64_t(lane) * kPer; e0 < full; e0 += 64 * kPer) {
-      const uint4 o = span::lds16(b32, r0 + int32_t(e0) * int32_t(sizeof(S)));
+      const uint4 o = span::lds16(b128, r0 + int32_t(e0) * int32_t(sizeof(S)));
       S sv[kPer];
       __builtin_memcpy(sv, &o, 16);
       Vec<D, kPer> ov;

@@ -38,10 +38,16 @@ constexpr int kBufBytes = kFront + int(tk::kSpanSegMax) + 64;
 // registers.  Five ds_read_b32 at a 16-byte lane stride (the 5-dword window used before) cost a
 // 4-way bank conflict each: banks (a/4) mod 32 in 32-lane groups (MI355X_MICROARCH.md §LDS).
 // Reads up to the 16-byte boundary at or below b0 + 31: the image keeps 64 spare bytes at its end.
-__device__ __forceinline__ uint4 lds16(const uint32_t* b32, int32_t b0) {
-  const int32_t a = b0 & ~15, q = (b0 >> 2) & 3, sh = b0 & 3;
-  const uint4 lo = *reinterpret_cast<const uint4*>(b32 + (a >> 2));
-  const uint4 hi = *reinterpret_cast<const uint4*>(b32 + (a >> 2) + 4);
+// `img` is the image as 16-byte slots.  The reads are nontemporal loads (a no-op hint for LDS)
+// because the compiler otherwise narrows them to the dwords the selects below can pick --
+// ds_read2_b32 pairs at a 16-byte lane stride, the conflicting pattern this replaces.
+typedef uint32_t lds_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 lds16(const uint4* img16, int32_t b0) {
+  const lds_v4u* img = reinterpret_cast<const lds_v4u*>(img16);
+  const int32_t q = (b0 >> 2) & 3, sh = b0 & 3;
+  const lds_v4u lv = __builtin_nontemporal_load(img + (b0 >> 4));
+  const lds_v4u hv = __builtin_nontemporal_load(img + (b0 >> 4) + 1);
+  const uint4 lo = make_uint4(lv.x, lv.y, lv.z, lv.w), hi = make_uint4(hv.x, hv.y, hv.z, hv.w);
   // dwords q .. q + 4 of lo:hi
   const uint32_t d0 = q == 0 ? lo.x : q == 1 ? lo.y : q == 2 ? lo.z : lo.w;
   const uint32_t d1 = q == 0 ? lo.y : q == 1 ? lo.z : q == 2 ? lo.w : hi.x;
