@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round-4 GPU session: STEPS="smoke benchdrv ..." SESSION=name tools/r4_session.sh
+# (steps of one-off A/Bs that were reverted were removed; their logs are under profiles/r04_*)
 # Each GPU step runs under its own time limit; the first failure (or a crash / time limit) ends the
 # script, so nothing more touches the GPU after a fault.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -73,17 +74,9 @@ for s in ${STEPS:-smoke benchdrv}; do
     c5ab) for rep in 1 2; do run c5_deliver_$rep 200 python benchmarks/config5_large_messages.py && run c5_commit_$rep 200 python benchmarks/config5_large_messages.py --verify commit; done ;;
     prof4) prof prof4 300 --kernel-trace --hip-trace --stats --output-format csv -d "$OUT/prof4" -o run -- python3 "$R/benchmarks/config4_json_varlen.py" --h2d dma ;;
     prof4zc) prof prof4zc 300 --kernel-trace --hip-trace --stats --output-format csv -d "$OUT/prof4zc" -o run -- python3 "$R/benchmarks/config4_json_varlen.py" ;;
-    c4split) for rep in $(seq 1 "${REPS:-4}"); do TORCHKAFKA_JSON_COUNT_SPLIT=1 run c4_split_$rep 200 python benchmarks/config4_json_varlen.py; grep -o '"value": [0-9]*' "$OUT/c4_split_$rep.log"; done ;;
     c5) for rep in 1 2 3; do run c5_deliver_$rep 200 python benchmarks/config5_large_messages.py; grep -o '"value": [0-9.]*' "$OUT/c5_deliver_$rep.log"; done ;;
     pytestjson) run pytest_json 600 python -u -m pytest tests/test_gpu_json_span.py tests/test_gpu_json_parse.py tests/test_gpu_span.py tests/test_gpu_loader.py -k "json or verify or count or span" -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     benchahead) for d in 0 1 2 4 0 1 2 4; do TORCHKAFKA_AHEAD_DEPTH=$d run bench_ahead${d}_$RANDOM 300 python bench.py --steps 20 --warmup 5 --steady-steps 20000 --extra-blocks "" --bridge-steps 0 --config-blocks ""; done; grep -o '"value": [0-9.]*\|"records_per_s": [0-9.]*' "$OUT"/bench_ahead*.log ;;
-    c4g8) for rep in $(seq 1 "${REPS:-4}"); do run c4_g8_$rep 200 python benchmarks/config4_json_varlen.py --varlen-coalesce 8; grep -o '"value": [0-9]*' "$OUT/c4_g8_$rep.log"; done ;;
-    c4g8dma) for rep in $(seq 1 "${REPS:-4}"); do run c4_g8dma_$rep 200 python benchmarks/config4_json_varlen.py --varlen-coalesce 8 --h2d dma; grep -o '"value": [0-9]*' "$OUT/c4_g8dma_$rep.log"; done ;;
-    c4ab) for rep in $(seq 1 "${REPS:-3}"); do
-            run c4_g8_$rep 200 python benchmarks/config4_json_varlen.py --varlen-coalesce 8 &&
-            run c4_g16s32_$rep 200 python benchmarks/config4_json_varlen.py --varlen-coalesce 16 --slots-per-worker 32 &&
-            run c4_g8s32_$rep 200 python benchmarks/config4_json_varlen.py --varlen-coalesce 8 --slots-per-worker 32
-          done; grep -o '"value": [0-9]*' "$OUT"/c4_g*.log ;;
     pmcjson) pmc pmc_json 120 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_json" -o run -- python3 "$R/benchmarks/config4_json_varlen.py" --steps 3000 ;;
     profjson) prof profjson 300 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profjson" -o run -- python3 "$R/benchmarks/config4_json_varlen.py" ;;
     launchcost) run launch_cost 60 tools/probes/launch_cost_probe ;;
