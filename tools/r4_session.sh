@@ -80,6 +80,18 @@ for s in ${STEPS:-smoke benchdrv}; do
     pmcjson) pmc pmc_json 120 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_json" -o run -- python3 "$R/benchmarks/config4_json_varlen.py" --steps 3000 ;;
     profjson) prof profjson 300 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/profjson" -o run -- python3 "$R/benchmarks/config4_json_varlen.py" ;;
     launchcost) run launch_cost 60 tools/probes/launch_cost_probe ;;
+    pytestq) TORCHKAFKA_HIP_QUEUE=1 run pytest_queue 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 180 --timeout-method thread ;;
+    abqueue) for rep in 1 2 3; do
+            run c4_base_$rep 200 python benchmarks/config4_json_varlen.py &&
+            TORCHKAFKA_HIP_QUEUE=1 run c4_q_$rep 200 python benchmarks/config4_json_varlen.py
+          done
+          for rep in 1 2; do
+            run bench_base_$rep 300 python bench.py --steps 20 --warmup 5 --steady-steps 20000 --extra-blocks "" --bridge-steps 0 --config-blocks "" &&
+            TORCHKAFKA_HIP_QUEUE=1 run bench_q_$rep 300 python bench.py --steps 20 --warmup 5 --steady-steps 20000 --extra-blocks "" --bridge-steps 0 --config-blocks ""
+          done
+          run tokens_base 300 python benchmarks/varlen_tokens.py && TORCHKAFKA_HIP_QUEUE=1 run tokens_q 300 python benchmarks/varlen_tokens.py
+          run c5_base 200 python benchmarks/config5_large_messages.py && TORCHKAFKA_HIP_QUEUE=1 run c5_q 200 python benchmarks/config5_large_messages.py
+          grep -o '"value": [0-9.]*' "$OUT"/c4_*.log "$OUT"/bench_*.log "$OUT"/tokens_*.log "$OUT"/c5_*.log ;;
     kernarg) run kernarg 60 tools/probes/kernarg_probe ;;
     pytestgpu) run pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 180 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;

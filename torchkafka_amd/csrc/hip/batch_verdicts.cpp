@@ -9,6 +9,7 @@
 #include "consumer.h"
 #include "crc32c.h"
 #include "dtypes.h"
+#include "hip_queue.h"
 #include "span.h"
 
 namespace tkh {
@@ -189,6 +190,7 @@ void BatchVerdicts::parse_host_rows(int64_t g, int64_t w) {
 void BatchVerdicts::json_host_rows(int64_t g, int64_t w, int32_t trunc_len, void* out, int64_t L, int dst_dt,
                                    double pad, int64_t* lengths, uint8_t* mask, hipStream_t stream) {
   if (w < 0) return;
+  HipQueue::get().drain();  // the copies below go on `stream` after its queued parse kernel
   if (!jparsed_[size_t(w)]) parse_host_rows(g, w);  // the slot is still held
   const int dsz = dtype_size(dst_dt);
   constexpr size_t kVals = 256;  // the values start 256 bytes after the row descriptor

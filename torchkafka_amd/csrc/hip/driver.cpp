@@ -1,6 +1,7 @@
 #include "driver.h"
 
 #include "dtypes.h"
+#include "hip_queue.h"
 
 #include <unistd.h>
 
@@ -50,6 +51,10 @@ MainDriver::MainDriver(Engine* engine, const std::string& ring_name, const std::
 }
 
 MainDriver::~MainDriver() {
+  try {
+    HipQueue::get().drain();  // queued launches read the slots, logs and staging freed below
+  } catch (...) {
+  }
   pins_.reset();  // pinned log ranges first: the kernels that read them completed (slots drained by the caller)
   if (stage_dev_) {
     hipDeviceSynchronize();
@@ -589,9 +594,9 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
   // a wave per row: counts, simple check, the width words.  Not fused into json_stage_kernel: its
   // few workgroups (one per segment) took 149 us per group doing it instead of 71 us, and config 4
   // fell from 40.5 M to 35.5 M rec/s (profiles/r04_s4)
-  if (devc) launch_json_count(ga, stream);
+  if (devc) eng_->run_on(stream, [ga, stream] { launch_json_count(ga, stream); });
   // the parse: a block per row over the staged texts, on the same stream
-  launch_json_group(ga, dst_dt, stream);
+  eng_->run_on(stream, [ga, dst_dt, stream]() mutable { launch_json_group(ga, dst_dt, stream); });
   if (record_last) eng_->record_done(slots[n - 1], stream);
 }
 
@@ -629,7 +634,7 @@ void MainDriver::launch_var_span(const int* slots, const SlotView* const* views,
     a.burst = pcie ? span_burst_ : mirror_burst_;
     pcie = false;
     if (mirror) mirror->before(stream);
-    tkh::launch_var_span(a, src_dt, dst_dt, pad, stream);
+    eng_->run_on(stream, [a, src_dt, dst_dt, pad, stream] { tkh::launch_var_span(a, src_dt, dst_dt, pad, stream); });
     if (mirror) mirror->after(stream);
     if (record) eng_->record_done(slots[n - 1], stream);
   };

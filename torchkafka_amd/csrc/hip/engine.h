@@ -3,6 +3,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 namespace tkh {
@@ -100,6 +101,10 @@ class Engine {
   // `user` waits for slot s's completion event (a batch collated on another stream).
   void stream_wait_done(int s, hipStream_t user);
   void record_done(int s, hipStream_t user) { finish(s, user); }
+  // Runs f -- HIP calls on `stream` -- now, or through the HIP command queue when `stream` is a
+  // decode stream and the queue is on (hip_queue.h).
+  void run_on(hipStream_t stream, std::function<void()>&& f);
+  bool queued(hipStream_t stream) const;  // calls on `stream` go through the command queue
   void copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes);
   // The same without the slot's completion event: a kernel queued after it on `user` records it.
   void copy_bytes(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes);
@@ -123,6 +128,7 @@ class Engine {
   void* staging_ = nullptr;
   std::vector<hipStream_t> streams_;
   std::vector<hipEvent_t> done_, copied_;
+  std::vector<uint64_t> done_seq_;  // command-queue number of each done_ record (0: recorded directly)
   std::vector<const uint8_t*> host_src_;  // per slot: host payload pointer given at h2d()
   void* host_ptr_ = nullptr;
   uint8_t* host_dev_ = nullptr;           // device view of the registered host region (zero-copy)

@@ -27,6 +27,7 @@
 #include "collate.h"
 #include "crc32c.h"
 #include "engine.h"
+#include "hip_queue.h"
 #include "span_decode.h"
 
 namespace tkh {
@@ -54,12 +55,17 @@ Engine::Engine(int device, int n_slots, size_t staging_bytes, int n_streams, int
   if (mode_ == kH2DDma) TKH_CHECK(hipMalloc(&staging_, stride_ * size_t(n_slots)));
   done_.resize(size_t(n_slots));
   for (auto& e : done_) TKH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  done_seq_.assign(size_t(n_slots), 0);
   copied_.resize(size_t(n_slots));
   for (auto& e : copied_) TKH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   host_src_.assign(size_t(n_slots), nullptr);
 }
 
 Engine::~Engine() {
+  try {
+    HipQueue::get().drain();  // queued calls use the streams and events below
+  } catch (...) {
+  }
   hipSetDevice(device_);
   for (auto st : streams_) hipStreamSynchronize(st);
   if (host_ptr_) hipHostUnregister(host_ptr_);
@@ -123,8 +129,23 @@ const uint8_t* Engine::src_base(int s) const {
   return host_dev_ + (h - static_cast<const uint8_t*>(host_ptr_));
 }
 
+bool Engine::queued(hipStream_t stream) const {
+  if (!HipQueue::get().on() || !stream) return false;
+  for (auto st : decode_streams_)
+    if (st == stream) return true;
+  return false;
+}
+
+void Engine::run_on(hipStream_t stream, std::function<void()>&& f) {
+  if (queued(stream))
+    HipQueue::get().submit(std::move(f));
+  else
+    f();
+}
+
 bool Engine::slot_done(int s) {
   check_slot(s);
+  if (!HipQueue::get().ran(done_seq_[size_t(s)])) return false;  // its record has not even run yet
   hipError_t e = hipEventQuery(done_[size_t(s)]);
   if (e == hipSuccess) return true;
   if (e == hipErrorNotReady) return false;
@@ -133,6 +154,7 @@ bool Engine::slot_done(int s) {
 
 void Engine::wait_slot(int s) {
   check_slot(s);
+  HipQueue::get().wait(done_seq_[size_t(s)]);
   TKH_CHECK(hipEventSynchronize(done_[size_t(s)]));
 }
 
@@ -145,10 +167,19 @@ void Engine::begin(int s, hipStream_t user) {
   if (mode_ == kH2DDma) TKH_CHECK(hipStreamWaitEvent(user, copied_[size_t(s)], 0));
 }
 
-void Engine::finish(int s, hipStream_t user) { TKH_CHECK(hipEventRecord(done_[size_t(s)], user)); }
+void Engine::finish(int s, hipStream_t user) {
+  hipEvent_t e = done_[size_t(s)];
+  if (queued(user)) {
+    done_seq_[size_t(s)] = HipQueue::get().submit([e, user] { TKH_CHECK(hipEventRecord(e, user)); });
+  } else {
+    TKH_CHECK(hipEventRecord(e, user));
+    done_seq_[size_t(s)] = 0;
+  }
+}
 
 void Engine::collate_fixed(int s, hipStream_t user, size_t values_offset, int src_dt, void* dst, int dst_dt,
                            int64_t rows, int64_t row, const float* shift, const float* scale, bool record) {
+  if (queued(user)) HipQueue::get().drain();  // a direct launch on a queued stream: after the queue
   check_slot(s);
   begin(s, user);
   launch_fixed(src_base(s) + values_offset, src_dt, dst, dst_dt, rows, row, shift, scale, user);
@@ -158,6 +189,7 @@ void Engine::collate_fixed(int s, hipStream_t user, size_t values_offset, int sr
 void Engine::collate_fixed_group(const int* slots, int n, hipStream_t user, const size_t* values_offsets, int src_dt,
                                  void* const* dsts, int dst_dt, const int64_t* rows, int64_t row, const float* shift,
                                  const float* scale) {
+  if (queued(user)) HipQueue::get().drain();  // a direct launch on a queued stream: after the queue
   if (n < 1 || n > kMaxGroup) throw std::invalid_argument("engine: bad group size");
   const void* srcs[kMaxGroup];
   for (int k = 0; k < n; ++k) {
@@ -172,6 +204,7 @@ void Engine::collate_fixed_group(const int* slots, int n, hipStream_t user, cons
 void Engine::collate_gather_group(const int* slots, int n, hipStream_t user, int src_dt, void* const* dsts, int dst_dt,
                                   const int64_t* rows, int64_t row_bytes, const uint64_t* bases, const float* shift,
                                   const float* scale, bool record) {
+  if (queued(user)) HipQueue::get().drain();  // a direct launch on a queued stream: after the queue
   if (n < 1 || n > kMaxGroup) throw std::invalid_argument("engine: bad group size");
   const uint64_t* ents[kMaxGroup];
   for (int k = 0; k < n; ++k) {
@@ -185,11 +218,18 @@ void Engine::collate_gather_group(const int* slots, int n, hipStream_t user, int
 
 void Engine::stream_wait_done(int s, hipStream_t user) {
   check_slot(s);
-  TKH_CHECK(hipStreamWaitEvent(user, done_[size_t(s)], 0));
+  hipEvent_t e = done_[size_t(s)];
+  if (queued(user)) {
+    HipQueue::get().submit([e, user] { TKH_CHECK(hipStreamWaitEvent(user, e, 0)); });
+  } else {
+    HipQueue::get().wait(done_seq_[size_t(s)]);  // the record the wait refers to has run
+    TKH_CHECK(hipStreamWaitEvent(user, e, 0));
+  }
 }
 
 void Engine::collate_varlen(int s, hipStream_t user, size_t values_offset, int src_dt, void* out, int dst_dt,
                             int64_t rows, int64_t L, double pad, int64_t* lengths, uint8_t* mask, bool record) {
+  if (queued(user)) HipQueue::get().drain();  // a direct launch on a queued stream: after the queue
   check_slot(s);
   const uint8_t* base = src_base(s);
   begin(s, user);
@@ -200,6 +240,7 @@ void Engine::collate_varlen(int s, hipStream_t user, size_t values_offset, int s
 
 void Engine::collate_json(int s, hipStream_t user, size_t values_offset, void* out, int dst_dt, int64_t rows,
                           int64_t L, double pad, int64_t* lengths, uint8_t* mask, int32_t* err, bool record) {
+  if (queued(user)) HipQueue::get().drain();  // a direct launch on a queued stream: after the queue
   check_slot(s);
   const uint8_t* base = src_base(s);
   begin(s, user);
@@ -211,6 +252,7 @@ void Engine::collate_json(int s, hipStream_t user, size_t values_offset, void* o
 void Engine::collate_json_group(const int* slots, int n, hipStream_t user, const size_t* values_offsets,
                                 const int64_t* rows, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
                                 uint8_t* const* masks, int32_t* const* errs, double pad, int dst_dt) {
+  if (queued(user)) HipQueue::get().drain();  // a direct launch on a queued stream: after the queue
   if (n < 1 || n > kMaxGroup) throw std::invalid_argument("engine: bad group size");
   JsonGroupArgs a{};
   a.n = n;
@@ -262,6 +304,7 @@ void Engine::set_decode_streams(int n) {
 __global__ void decode_warm_kernel() {}
 
 void Engine::prepare_decode() {
+  HipQueue::get().drain();
   span_tables();
   for (int k = 0; k < decode_streams(); ++k) {
     hipStream_t st = decode_stream(k);
@@ -284,6 +327,7 @@ hipStream_t Engine::decode_stream(int k) {
 
 void Engine::stream_after(hipStream_t later, hipStream_t earlier) {
   if (later == earlier) return;
+  if (queued(later) || queued(earlier)) HipQueue::get().drain();  // rare: keep both in order
   if (order_events_.empty()) {
     order_events_.resize(16);
     for (auto& e : order_events_) TKH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -304,7 +348,13 @@ void Engine::collate_span(const int* slots, int n, hipStream_t user, SpanLaunch&
     if (a.b[k].ext_words) a.b[k].ext_src = reinterpret_cast<const int64_t*>(src_base(slots[k]) + a.b[k].ext_off);
   }
   a.tabs = span_tables();
-  launch_span_decode(a, src_dt, dst_dt, shift, scale, user);
+  if (queued(user)) {
+    HipQueue::get().submit([a, src_dt, dst_dt, shift, scale, user] {
+      launch_span_decode(a, src_dt, dst_dt, shift, scale, user);
+    });
+  } else {
+    launch_span_decode(a, src_dt, dst_dt, shift, scale, user);
+  }
   if (record) finish(slots[n - 1], user);
 }
 
@@ -317,16 +367,21 @@ void Engine::collate_json_stage(const int* slots, int n, hipStream_t user, JsonS
     a.b[k].rows = reinterpret_cast<const tk::JsonSpanRow*>(a.b[k].slot);
   }
   a.tabs = span_tables();
-  launch_json_stage(a, user);
+  if (queued(user))
+    HipQueue::get().submit([a, user] { launch_json_stage(a, user); });
+  else
+    launch_json_stage(a, user);
 }
 
 void Engine::copy_bytes(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes) {
+  if (queued(user)) HipQueue::get().drain();  // a direct launch on a queued stream: after the queue
   check_slot(s);
   begin(s, user);
   if (nbytes) TKH_CHECK(hipMemcpyAsync(dst, src_base(s) + offset, nbytes, hipMemcpyDefault, user));
 }
 
 void Engine::copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes) {
+  if (queued(user)) HipQueue::get().drain();  // a direct launch on a queued stream: after the queue
   check_slot(s);
   begin(s, user);
   if (nbytes) TKH_CHECK(hipMemcpyAsync(dst, src_base(s) + offset, nbytes, hipMemcpyDefault, user));
@@ -334,6 +389,7 @@ void Engine::copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t 
 }
 
 void Engine::synchronize() {
+  HipQueue::get().drain();
   for (auto st : streams_) TKH_CHECK(hipStreamSynchronize(st));
   for (auto st : decode_streams_)
     if (st) TKH_CHECK(hipStreamSynchronize(st));

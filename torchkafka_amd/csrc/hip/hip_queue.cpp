@@ -1,0 +1,103 @@
+#include "hip_queue.h"
+
+#include <chrono>
+#include <cstdlib>
+#include <ctime>
+#include <stdexcept>
+
+#include "common.h"
+
+namespace tkh {
+
+HipQueue& HipQueue::get() {
+  static HipQueue* q = new HipQueue();  // leaked on purpose: no teardown race with the HIP runtime
+  return *q;
+}
+
+HipQueue::HipQueue() {
+  const char* e = std::getenv("TORCHKAFKA_HIP_QUEUE");
+  on_ = e && e[0] == '1';
+  if (on_) ring_.resize(kCap);
+}
+
+void HipQueue::start() {
+  if (hipGetDevice(&device_) != hipSuccess) device_ = 0;
+  th_ = std::thread([this] { run(); });
+  th_.detach();
+  started_ = true;
+}
+
+uint64_t HipQueue::submit(std::function<void()>&& f) {
+  if (!on_) {
+    f();
+    return 0;
+  }
+  check();
+  uint64_t seq;
+  {
+    std::lock_guard<std::mutex> g(push_m_);
+    if (!started_) start();
+    seq = submitted_.load(std::memory_order_relaxed) + 1;
+    while (seq - done_.load(std::memory_order_acquire) > kCap) tk::cpu_relax();  // full: the thread catches up
+    ring_[seq % kCap] = std::move(f);
+    submitted_.store(seq, std::memory_order_seq_cst);
+  }
+  // seq_cst on both sides (here and in run()): the thread either sees this submission before it
+  // sleeps or is seen asleep here and woken
+  if (sleeping_.load(std::memory_order_seq_cst)) {
+    std::lock_guard<std::mutex> g(sleep_m_);
+    wake_.notify_one();
+  }
+  return seq;
+}
+
+void HipQueue::check() const {
+  if (failed_.load(std::memory_order_acquire)) throw std::runtime_error("HIP command queue: " + error_);
+}
+
+void HipQueue::wait(uint64_t seq) {
+  if (seq == 0) return;
+  for (int i = 0; done_.load(std::memory_order_acquire) < seq; ++i) {
+    check();
+    if (i < 20000)
+      tk::cpu_relax();
+    else
+      std::this_thread::yield();
+  }
+  check();
+}
+
+void HipQueue::run() {
+  hipSetDevice(device_);
+  uint64_t next = 1;
+  int idle = 0;
+  for (;;) {
+    if (submitted_.load(std::memory_order_acquire) >= next) {
+      std::function<void()> f = std::move(ring_[next % kCap]);
+      ring_[next % kCap] = nullptr;
+      if (!failed_.load(std::memory_order_relaxed)) {
+        try {
+          f();
+        } catch (const std::exception& ex) {
+          error_ = ex.what();
+          failed_.store(true, std::memory_order_release);
+        }
+      }
+      done_.store(next, std::memory_order_release);
+      ++next;
+      idle = 0;
+      continue;
+    }
+    if (++idle < 4000) {  // a few hundred microseconds of spinning: steps come every few microseconds
+      tk::cpu_relax();
+      continue;
+    }
+    std::unique_lock<std::mutex> lk(sleep_m_);
+    sleeping_.store(true, std::memory_order_seq_cst);
+    if (submitted_.load(std::memory_order_seq_cst) < next) wake_.wait_for(lk, std::chrono::milliseconds(5));
+    sleeping_.store(false, std::memory_order_release);
+    idle = 0;
+  }
+}
+
+}  // namespace tkh

@@ -1,0 +1,65 @@
+// Ordered HIP command queue executed by a thread of its own (TORCHKAFKA_HIP_QUEUE=1).
+//
+// On the device-decode paths the stepping thread spends about a third of each step in HIP calls
+// for groups it will hand out later (config 4: three kernel launches and two or three events per
+// group of 8 batches, 12-15 us; tools/probes/launch_cost_probe.hip: 3.0-4.8 us per launch).  With
+// the queue on, every HIP call the loader makes on the streams only it uses -- the decode streams
+// and the HBM mirror's copy streams -- is queued as a closure and run, in submission order, by
+// this thread.  The stepping thread keeps everything else: the decisions, the allocations and the
+// calls on the user's stream.
+//
+// Each queued call gets a sequence number.  An event whose record is queued carries the number of
+// that record (Engine::done_seq_, LogMirror tags); until the thread has run it, the event counts
+// as not complete (no HIP call), and a blocking wait first waits for it to run.  Before the user's
+// stream is made to wait for a decoded batch, the batch's record has run -- groups decoded ahead
+// were queued long before, so that wait is nearly always free.  Off by default.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace tkh {
+
+class HipQueue {
+ public:
+  static HipQueue& get();  // one per process (never destroyed: its thread may outlive main)
+  bool on() const { return on_; }
+  // Queues f (on) or runs it now (off: returns 0).  Returns f's sequence number.
+  uint64_t submit(std::function<void()>&& f);
+  // Every call up to `seq` ran (0: nothing to wait for).  Rethrows the thread's failure.
+  void wait(uint64_t seq);
+  void drain() { wait(submitted_.load(std::memory_order_acquire)); }
+  bool ran(uint64_t seq) const { return seq <= done_.load(std::memory_order_acquire); }
+  void check() const;  // throws the thread's failure, if any
+  uint64_t calls() const { return done_.load(std::memory_order_relaxed); }
+
+ private:
+  HipQueue();
+  void start();
+  void run();
+
+  static constexpr uint64_t kCap = 8192;
+  bool on_ = false;
+  bool started_ = false;
+  int device_ = 0;
+  std::vector<std::function<void()>> ring_;
+  std::mutex push_m_;                      // producers (the stepping thread; the pin thread never queues)
+  std::atomic<uint64_t> submitted_{0};     // last sequence number handed out (and published)
+  std::atomic<uint64_t> done_{0};          // last sequence number that ran
+  std::atomic<bool> failed_{false};
+  std::atomic<bool> sleeping_{false};
+  std::mutex sleep_m_;
+  std::condition_variable wake_;
+  std::string error_;
+  std::thread th_;
+};
+
+}  // namespace tkh

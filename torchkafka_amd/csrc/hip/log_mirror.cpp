@@ -5,6 +5,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "hip_queue.h"
 #include "span.h"
 
 namespace tkh {
@@ -34,10 +35,15 @@ LogMirror::LogMirror(int device, uint64_t chunk_bytes, int chunks_per_partition,
   pool_.resize(256);
   for (auto& e : pool_) TKM_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   pool_seq_.assign(pool_.size(), 0);
+  pool_rec_q_.assign(pool_.size(), 0);
   pool_refs_.assign(pool_.size(), 0);
 }
 
 LogMirror::~LogMirror() {
+  try {
+    HipQueue::get().drain();  // queued copies and records use the streams and events below
+  } catch (...) {
+  }
   hipSetDevice(device_);
   for (auto& c : cs_)
     if (c.stream) hipStreamSynchronize(c.stream);
@@ -69,7 +75,8 @@ void LogMirror::retarget(Buf& b, int64_t c) {
   hipStream_t copy = cs_[size_t(b.s)].stream;
   for (auto& r : b.readers) {
     if (r.ev >= 0 && pool_seq_[size_t(r.ev)] == r.seq) {
-      TKM_CHECK(hipStreamWaitEvent(copy, pool_[size_t(r.ev)], 0));
+      hipEvent_t ev = pool_[size_t(r.ev)];
+      HipQueue::get().submit([copy, ev] { TKM_CHECK(hipStreamWaitEvent(copy, ev, 0)); });
       --pool_refs_[size_t(r.ev)];
     }
     r = Reader{};
@@ -100,8 +107,11 @@ LogMirror::Buf* LogMirror::ensure(Part& P, uint32_t pidx, int64_t c, uint64_t wa
     // driver pins the logs in kRegAlign pieces (so that consumed pieces can be unpinned)
     for (uint64_t a = b.end; a < target;) {
       const uint64_t e = std::min<uint64_t>(target, (a / kRegAlign + 1) * kRegAlign);
-      TKM_CHECK(hipMemcpyAsync(P.dev + j * stride_ + (a - lo_c), log + a, size_t(e - a), hipMemcpyHostToDevice,
-                               cs_[size_t(b.s)].stream));
+      uint8_t* dst = P.dev + j * stride_ + (a - lo_c);
+      const uint8_t* src = log + a;
+      const size_t n = size_t(e - a);
+      hipStream_t st = cs_[size_t(b.s)].stream;
+      HipQueue::get().submit([dst, src, n, st] { TKM_CHECK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st)); });
       ++copies_;
       a = e;
     }
@@ -152,13 +162,23 @@ void LogMirror::issue_prefetches() {
   deferred_.clear();
 }
 
+// The copy stream's event is recorded through the HIP command queue when it is on: until that
+// record has run, the copies it covers count as in flight (no HIP call).
+bool LogMirror::copied_done(CopyStream& c) {
+  return HipQueue::get().ran(c.rec_q) && hipEventQuery(c.copied) == hipSuccess;
+}
+
+void LogMirror::record_copied(CopyStream& c) {
+  hipEvent_t ev = c.copied;
+  hipStream_t st = c.stream;
+  c.rec_q = HipQueue::get().submit([ev, st] { TKM_CHECK(hipEventRecord(ev, st)); });
+  c.recorded = c.seq;
+}
+
 void LogMirror::learn(CopyStream& c) {
   c.queried = true;
-  if (c.recorded > c.done && hipEventQuery(c.copied) == hipSuccess) c.done = c.recorded;
-  if (c.seq > c.recorded && c.recorded == c.done) {
-    TKM_CHECK(hipEventRecord(c.copied, c.stream));
-    c.recorded = c.seq;
-  }
+  if (c.recorded > c.done && copied_done(c)) c.done = c.recorded;
+  if (c.seq > c.recorded && c.recorded == c.done) record_copied(c);
 }
 
 void LogMirror::before(hipStream_t stream) {
@@ -167,10 +187,7 @@ void LogMirror::before(hipStream_t stream) {
     // prefetches, then mark the copy streams' tails so their completion can be learned
     issue_prefetches();
     for (auto& c : cs_) {
-      if (c.seq > c.recorded && c.recorded == c.done) {
-        TKM_CHECK(hipEventRecord(c.copied, c.stream));
-        c.recorded = c.seq;
-      }
+      if (c.seq > c.recorded && c.recorded == c.done) record_copied(c);
       c.queried = false;
     }
     return;
@@ -187,14 +204,12 @@ void LogMirror::before(hipStream_t stream) {
     // also covers the prefetches queued behind that copy (a longer wait), but events between SDMA
     // copies cost more than they save (measured, config 2 --h2d dma: 46.5 M rec/s this way,
     // 32-34 M with an event after every copy).
-    if (c.recorded < need[s]) {
-      TKM_CHECK(hipEventRecord(c.copied, c.stream));
-      c.recorded = c.seq;
-    }
-    if (hipEventQuery(c.copied) == hipSuccess) {  // found complete: no wait, and remembered
+    if (c.recorded < need[s]) record_copied(c);
+    if (copied_done(c)) {  // found complete: no wait, and remembered
       c.done = c.recorded;
     } else {
-      TKM_CHECK(hipStreamWaitEvent(stream, c.copied, 0));
+      hipEvent_t ev = c.copied;
+      HipQueue::get().submit([stream, ev] { TKM_CHECK(hipStreamWaitEvent(stream, ev, 0)); });
     }
   }
   issue_prefetches();
@@ -205,6 +220,7 @@ int LogMirror::next_event() {
   if (pool_refs_[size_t(e)] > 0) {
     // still named by a buffer: that reader is 256 launches old; make sure it completed, then
     // every reference to its old recording counts as completed (the sequence moves on)
+    HipQueue::get().wait(pool_rec_q_[size_t(e)]);
     TKM_CHECK(hipEventSynchronize(pool_[size_t(e)]));
     pool_refs_[size_t(e)] = 0;
   }
@@ -215,7 +231,10 @@ int LogMirror::next_event() {
 void LogMirror::after(hipStream_t stream) {
   if (pending_.empty()) return;
   const int e = next_event();
-  TKM_CHECK(hipEventRecord(pool_[size_t(e)], stream));
+  {
+    hipEvent_t ev = pool_[size_t(e)];
+    pool_rec_q_[size_t(e)] = HipQueue::get().submit([ev, stream] { TKM_CHECK(hipEventRecord(ev, stream)); });
+  }
   for (const auto& pb : pending_) {
     Buf& b = parts_[pb.first].bufs[size_t(pb.second)];
     b.pending = false;
@@ -231,6 +250,7 @@ void LogMirror::after(hipStream_t stream) {
     if (!slot) {
       // more reader streams than remembered: retire the first one on the host
       slot = &b.readers[0];
+      HipQueue::get().wait(pool_rec_q_[size_t(slot->ev)]);
       TKM_CHECK(hipEventSynchronize(pool_[size_t(slot->ev)]));
       --pool_refs_[size_t(slot->ev)];
     }

@@ -112,10 +112,13 @@ class LogMirror {
     hipEvent_t copied = nullptr;  // recorded after the latest copy (when a launch needs it)
     uint64_t seq = 0, recorded = 0, done = 0;
     bool queried = false;  // its event was queried for the launch being formed
+    uint64_t rec_q = 0;    // HIP command-queue number of the latest record of `copied` (hip_queue.h)
   };
   // no-wait mode: what the copy stream has completed (one query per launch), and a fresh event
   // at its tail once the last one completed
   void learn(CopyStream& c);
+  bool copied_done(CopyStream& c);   // its latest record ran and completed
+  void record_copied(CopyStream& c);  // records `copied` at the stream's tail (queued when the queue is on)
   bool wait_ = false;
   uint64_t pending_fallbacks_ = 0;
   std::vector<CopyStream> cs_;
@@ -124,6 +127,7 @@ class LogMirror {
   std::vector<std::pair<uint32_t, int>> pending_;
   std::vector<hipEvent_t> pool_;
   std::vector<uint64_t> pool_seq_;
+  std::vector<uint64_t> pool_rec_q_;  // HIP command-queue number of each pool event's latest record
   std::vector<int> pool_refs_;
   size_t pool_next_ = 0;
   uint64_t bytes_ = 0, copies_ = 0, fallbacks_ = 0, dev_bytes_ = 0;
