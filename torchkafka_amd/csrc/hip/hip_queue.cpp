@@ -15,8 +15,8 @@ HipQueue& HipQueue::get() {
 }
 
 HipQueue::HipQueue() {
-  const char* e = std::getenv("TORCHKAFKA_HIP_QUEUE");
-  on_ = e && e[0] == '1';
+  const char* e = std::getenv("TORCHKAFKA_HIP_QUEUE");  // on unless "0"
+  on_ = !(e && e[0] == '0');
   if (on_) ring_.resize(kCap);
 }
 
