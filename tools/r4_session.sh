@@ -92,6 +92,14 @@ for s in ${STEPS:-smoke benchdrv}; do
           run tokens_base 300 python benchmarks/varlen_tokens.py && TORCHKAFKA_HIP_QUEUE=1 run tokens_q 300 python benchmarks/varlen_tokens.py
           run c5_base 200 python benchmarks/config5_large_messages.py && TORCHKAFKA_HIP_QUEUE=1 run c5_q 200 python benchmarks/config5_large_messages.py
           grep -o '"value": [0-9.]*' "$OUT"/c4_*.log "$OUT"/bench_*.log "$OUT"/tokens_*.log "$OUT"/c5_*.log ;;
+    abvalue) for rep in 1 2 3 4; do
+            run bv_q_$rep 300 python bench.py --steps 20 --warmup 5 --steady-steps 8000 --extra-blocks "" --bridge-steps 0 --config-blocks "" &&
+            TORCHKAFKA_HIP_QUEUE=0 run bv_base_$rep 300 python bench.py --steps 20 --warmup 5 --steady-steps 8000 --extra-blocks "" --bridge-steps 0 --config-blocks ""
+          done
+          for rep in 1 2 3; do
+            run c4_q_$rep 200 python benchmarks/config4_json_varlen.py && TORCHKAFKA_HIP_QUEUE=0 run c4_base_$rep 200 python benchmarks/config4_json_varlen.py
+          done
+          grep -o '"value": [0-9.]*\|"timed_region_s": [0-9.]*' "$OUT"/bv_*.log "$OUT"/c4_*.log ;;
     kernarg) run kernarg 60 tools/probes/kernarg_probe ;;
     pytestgpu) run pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 180 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;

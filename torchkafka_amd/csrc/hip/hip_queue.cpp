@@ -37,7 +37,17 @@ uint64_t HipQueue::submit(std::function<void()>&& f) {
   {
     std::lock_guard<std::mutex> g(push_m_);
     if (!started_) start();
-    seq = submitted_.load(std::memory_order_relaxed) + 1;
+    const uint64_t last = submitted_.load(std::memory_order_relaxed);
+    if (sleeping_.load(std::memory_order_seq_cst) && done_.load(std::memory_order_acquire) == last) {
+      // the thread is asleep with nothing queued (a pause between iterations, a synchronize): run
+      // f here -- waiting for the thread to wake would delay it by tens of microseconds -- and wake
+      // the thread for the calls that follow
+      f();
+      std::lock_guard<std::mutex> w(sleep_m_);
+      wake_.notify_one();
+      return 0;
+    }
+    seq = last + 1;
     while (seq - done_.load(std::memory_order_acquire) > kCap) tk::cpu_relax();  // full: the thread catches up
     ring_[seq % kCap] = std::move(f);
     submitted_.store(seq, std::memory_order_seq_cst);
