@@ -45,9 +45,8 @@ PROCESS_ENV = {
     "TORCHKAFKA_MIRROR_BURST": "LDS-DMA loads a decode wave keeps in flight when its launch reads only the HBM "
                                "mirror (0 = all, the default; csrc/hip/driver.h)",
     "TORCHKAFKA_MIRROR_COPY_STREAMS": "copy streams of the HBM mirror, partitions split p % n (1..4, default 2)",
-    "TORCHKAFKA_HIP_QUEUE": "0: the loader's HIP calls on its decode and mirror-copy streams are made by the stepping "
-                            "thread itself instead of, in order, by a thread of their own (csrc/hip/hip_queue.h, "
-                            "the default)",
+    "TORCHKAFKA_HIP_QUEUE": "0: var-len / JSON device decode makes its decode- and mirror-copy-stream HIP calls on "
+                            "the stepping thread instead of, in order, on a thread of their own (csrc/hip/hip_queue.h)",
     "TORCHKAFKA_MIRROR_WAIT": "1: a mirror launch waits for the copy of a chunk still in flight instead of reading "
                               "that segment from the pinned log (round-3 behaviour; A/B only)",
 }

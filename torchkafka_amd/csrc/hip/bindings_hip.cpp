@@ -370,6 +370,7 @@ PYBIND11_MODULE(_tkhip, m) {
       .def_property_readonly("coalesce", &MainDriver::coalesce)
       .def("enable_lockstep", &MainDriver::enable_lockstep, py::keep_alive<1, 2>())
       .def("set_sync_commit", &MainDriver::set_sync_commit, py::arg("sync"))
+      .def("set_command_queue", &MainDriver::set_command_queue, py::arg("on"))
       .def("verify_delivered",
            [](MainDriver& d) {
              py::gil_scoped_release nogil;

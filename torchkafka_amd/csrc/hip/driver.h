@@ -183,6 +183,12 @@ class MainDriver {
     pins_->enable_mirror(chunk_bytes, chunks_per_partition, copy_streams);
   }
   const LogMirror* mirror() const { return pins_->mirror(); }
+  // The decode-stream and mirror HIP calls of this driver go through the HIP command queue
+  // (hip_queue.h): DeviceLoader turns it on for var-len / JSON device decode.
+  void set_command_queue(bool on) {
+    eng_->set_command_queue(on);
+    if (pins_->mirror()) pins_->mirror()->set_command_queue(on);
+  }
   uint64_t log_bytes_registered() const { return pins_->bytes_registered(); }
   uint64_t log_bytes_unpinned() const { return pins_->bytes_unpinned(); }
   int64_t log_register_ns() const { return pins_->register_ns(); }

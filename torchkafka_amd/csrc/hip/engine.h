@@ -105,6 +105,9 @@ class Engine {
   // decode stream and the queue is on (hip_queue.h).
   void run_on(hipStream_t stream, std::function<void()>&& f);
   bool queued(hipStream_t stream) const;  // calls on `stream` go through the command queue
+  // Whether this engine's decode-stream calls use the command queue (set per loader: var-len and
+  // JSON device decode; fixed-width decode keeps its calls on the stepping thread).
+  void set_command_queue(bool on);
   void copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes);
   // The same without the slot's completion event: a kernel queued after it on `user` records it.
   void copy_bytes(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes);
@@ -129,6 +132,7 @@ class Engine {
   std::vector<hipStream_t> streams_;
   std::vector<hipEvent_t> done_, copied_;
   std::vector<uint64_t> done_seq_;  // command-queue number of each done_ record (0: recorded directly)
+  bool cq_ = false;                 // set_command_queue
   std::vector<const uint8_t*> host_src_;  // per slot: host payload pointer given at h2d()
   void* host_ptr_ = nullptr;
   uint8_t* host_dev_ = nullptr;           // device view of the registered host region (zero-copy)

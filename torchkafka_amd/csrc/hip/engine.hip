@@ -129,8 +129,13 @@ const uint8_t* Engine::src_base(int s) const {
   return host_dev_ + (h - static_cast<const uint8_t*>(host_ptr_));
 }
 
+void Engine::set_command_queue(bool on) {
+  if (!on && cq_) HipQueue::get().drain();  // calls queued so far stay ahead of the direct ones
+  cq_ = on && HipQueue::get().on();
+}
+
 bool Engine::queued(hipStream_t stream) const {
-  if (!HipQueue::get().on() || !stream) return false;
+  if (!cq_ || !stream) return false;
   for (auto st : decode_streams_)
     if (st == stream) return true;
   return false;

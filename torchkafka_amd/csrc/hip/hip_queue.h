@@ -13,9 +13,12 @@
 // that record (Engine::done_seq_, LogMirror tags); until the thread has run it, the event counts
 // as not complete (no HIP call), and a blocking wait first waits for it to run.  Before the user's
 // stream is made to wait for a decoded batch, the batch's record has run -- groups decoded ahead
-// were queued long before, so that wait is nearly always free.  Config 4 on one box: 45.8-49.2 M
-// rec/s against 44.2-44.8 M without the queue; VarLen tokens 43.2 against 41.8 M; fixed-width
-// steady state and config 5 unchanged; the GPU suite passes either way (profiles/r04_s14).
+// were queued long before, so that wait is nearly always free.  Used per loader
+// (Engine::set_command_queue): var-len and JSON device decode -- config 4 45.3-50.3 M rec/s against
+// 42.7-44.9 M without it on one box, VarLen tokens 43.2 against 41.8 M; fixed-width decode does not
+// use it -- its 20-step headline fell 12 % with it (the window's ahead groups are handed to the
+// thread and drained after it), its steady state did not move (profiles/r04_s14, r04_s16).  The
+// GPU suite passes with every loader on the queue (r04_s14).
 #pragma once
 
 #include <hip/hip_runtime.h>

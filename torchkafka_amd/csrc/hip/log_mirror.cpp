@@ -57,6 +57,17 @@ LogMirror::~LogMirror() {
   }
 }
 
+void LogMirror::set_command_queue(bool on) {
+  if (!on && cq_) HipQueue::get().drain();
+  cq_ = on && HipQueue::get().on();
+}
+
+uint64_t LogMirror::issue(std::function<void()>&& f) {
+  if (cq_) return HipQueue::get().submit(std::move(f));
+  f();
+  return 0;
+}
+
 LogMirror::Part& LogMirror::part(uint32_t pidx) {
   if (pidx >= parts_.size()) parts_.resize(size_t(pidx) + 1);
   Part& P = parts_[pidx];
@@ -76,7 +87,7 @@ void LogMirror::retarget(Buf& b, int64_t c) {
   for (auto& r : b.readers) {
     if (r.ev >= 0 && pool_seq_[size_t(r.ev)] == r.seq) {
       hipEvent_t ev = pool_[size_t(r.ev)];
-      HipQueue::get().submit([copy, ev] { TKM_CHECK(hipStreamWaitEvent(copy, ev, 0)); });
+      issue([copy, ev] { TKM_CHECK(hipStreamWaitEvent(copy, ev, 0)); });
       --pool_refs_[size_t(r.ev)];
     }
     r = Reader{};
@@ -111,7 +122,7 @@ LogMirror::Buf* LogMirror::ensure(Part& P, uint32_t pidx, int64_t c, uint64_t wa
       const uint8_t* src = log + a;
       const size_t n = size_t(e - a);
       hipStream_t st = cs_[size_t(b.s)].stream;
-      HipQueue::get().submit([dst, src, n, st] { TKM_CHECK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st)); });
+      issue([dst, src, n, st] { TKM_CHECK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st)); });
       ++copies_;
       a = e;
     }
@@ -171,7 +182,7 @@ bool LogMirror::copied_done(CopyStream& c) {
 void LogMirror::record_copied(CopyStream& c) {
   hipEvent_t ev = c.copied;
   hipStream_t st = c.stream;
-  c.rec_q = HipQueue::get().submit([ev, st] { TKM_CHECK(hipEventRecord(ev, st)); });
+  c.rec_q = issue([ev, st] { TKM_CHECK(hipEventRecord(ev, st)); });
   c.recorded = c.seq;
 }
 
@@ -209,7 +220,7 @@ void LogMirror::before(hipStream_t stream) {
       c.done = c.recorded;
     } else {
       hipEvent_t ev = c.copied;
-      HipQueue::get().submit([stream, ev] { TKM_CHECK(hipStreamWaitEvent(stream, ev, 0)); });
+      issue([stream, ev] { TKM_CHECK(hipStreamWaitEvent(stream, ev, 0)); });
     }
   }
   issue_prefetches();
@@ -233,7 +244,7 @@ void LogMirror::after(hipStream_t stream) {
   const int e = next_event();
   {
     hipEvent_t ev = pool_[size_t(e)];
-    pool_rec_q_[size_t(e)] = HipQueue::get().submit([ev, stream] { TKM_CHECK(hipEventRecord(ev, stream)); });
+    pool_rec_q_[size_t(e)] = issue([ev, stream] { TKM_CHECK(hipEventRecord(ev, stream)); });
   }
   for (const auto& pb : pending_) {
     Buf& b = parts_[pb.first].bufs[size_t(pb.second)];

@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "span.h"
@@ -43,6 +44,8 @@ class LogMirror {
   // TORCHKAFKA_MIRROR_COPY_STREAMS, else 2.  Each takes one of the process's hardware queues.
   LogMirror(int device, uint64_t chunk_bytes, int chunks_per_partition, int copy_streams = 0);
   ~LogMirror();
+  // The mirror's HIP calls go through the HIP command queue (hip_queue.h) when on.
+  void set_command_queue(bool on);
   int copy_streams() const { return int(cs_.size()); }
   LogMirror(const LogMirror&) = delete;
   LogMirror& operator=(const LogMirror&) = delete;
@@ -118,6 +121,10 @@ class LogMirror {
   // at its tail once the last one completed
   void learn(CopyStream& c);
   bool copied_done(CopyStream& c);   // its latest record ran and completed
+  // f (HIP calls on the copy or decode streams) through the command queue when set_command_queue
+  // turned it on, else now; returns its queue number (0: ran now)
+  uint64_t issue(std::function<void()>&& f);
+  bool cq_ = false;
   void record_copied(CopyStream& c);  // records `copied` at the stream's tail (queued when the queue is on)
   bool wait_ = false;
   uint64_t pending_fallbacks_ = 0;

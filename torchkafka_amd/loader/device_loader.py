@@ -214,6 +214,10 @@ class _Run:
                 if tun.span_burst is not None:
                     self.driver.set_span_burst(int(tun.span_burst))
                 self.driver.set_group_bytes(int(tun.group_mib) << 20)
+                # var-len / JSON device decode: the launches of the groups decoded ahead go through the
+                # HIP command queue (csrc/hip/hip_queue.h; config 4 +9 %); fixed-width decode keeps
+                # them on this thread (the 20-step headline lost 12 % to the queue's hand-off)
+                self.driver.set_command_queue(bool(L.plan.json_span or L.plan.var_span))
         except BaseException:
             self.close()
             raise
