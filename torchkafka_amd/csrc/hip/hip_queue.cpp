@@ -5,6 +5,8 @@
 #include <ctime>
 #include <stdexcept>
 
+#include <pthread.h>
+
 #include "common.h"
 
 namespace tkh {
@@ -18,6 +20,13 @@ HipQueue::HipQueue() {
   const char* e = std::getenv("TORCHKAFKA_HIP_QUEUE");  // on unless "0"
   on_ = !(e && e[0] == '0');
   if (on_) ring_.resize(kCap);
+  // DataLoader workers are forked from the loader's process: the thread does not survive a fork,
+  // so in the child every call runs inline (the workers make no HIP calls; this is a guard)
+  pthread_atfork(nullptr, nullptr, [] {
+    HipQueue& q = get();
+    q.on_ = false;
+    q.child_ = true;
+  });
 }
 
 void HipQueue::start() {
@@ -25,6 +34,21 @@ void HipQueue::start() {
   th_ = std::thread([this] { run(); });
   th_.detach();
   started_ = true;
+  std::atexit([] { get().shutdown(); });
+}
+
+void HipQueue::shutdown() {
+  if (child_ || !started_) return;
+  try {
+    drain();
+  } catch (...) {
+  }
+  stop_.store(true, std::memory_order_seq_cst);
+  {
+    std::lock_guard<std::mutex> g(sleep_m_);
+    wake_.notify_one();
+  }
+  for (int i = 0; i < 100000 && !exited_.load(std::memory_order_acquire); ++i) std::this_thread::yield();
 }
 
 uint64_t HipQueue::submit(std::function<void()>&& f) {
@@ -81,7 +105,7 @@ void HipQueue::run() {
   hipSetDevice(device_);
   uint64_t next = 1;
   int idle = 0;
-  for (;;) {
+  while (!stop_.load(std::memory_order_acquire)) {
     if (submitted_.load(std::memory_order_acquire) >= next) {
       std::function<void()> f = std::move(ring_[next % kCap]);
       ring_[next % kCap] = nullptr;
@@ -108,6 +132,7 @@ void HipQueue::run() {
     sleeping_.store(false, std::memory_order_release);
     idle = 0;
   }
+  exited_.store(true, std::memory_order_release);
 }
 
 }  // namespace tkh

@@ -46,6 +46,9 @@ class HipQueue {
   bool ran(uint64_t seq) const { return seq <= done_.load(std::memory_order_acquire); }
   void check() const;  // throws the thread's failure, if any
   uint64_t calls() const { return done_.load(std::memory_order_relaxed); }
+  // At process exit (atexit, registered when the thread starts): everything queued runs, then the
+  // thread stops -- before the HIP runtime's own teardown, registered earlier, runs.
+  void shutdown();
 
  private:
   HipQueue();
@@ -61,6 +64,8 @@ class HipQueue {
   std::atomic<uint64_t> submitted_{0};     // last sequence number handed out (and published)
   std::atomic<uint64_t> done_{0};          // last sequence number that ran
   std::atomic<bool> failed_{false};
+  std::atomic<bool> stop_{false}, exited_{false};
+  bool child_ = false;  // a forked child: the thread did not survive the fork
   std::atomic<bool> sleeping_{false};
   std::mutex sleep_m_;
   std::condition_variable wake_;
