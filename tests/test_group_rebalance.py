@@ -80,7 +80,8 @@ def test_a_third_process_joining_rebalances_at_least_once(broker, cluster):
     broker.create_topic("t", 6)
     broker.fill("t", 400, "fixed_f32", size=8, records_per_batch=10)
     cluster.join_delay_s = 6.0
-    a, b = _spawn(cluster.address, slow=0.01, idle=8000), _spawn(cluster.address, slow=0.01, idle=8000)
+    # a long idle: under a loaded host the joiner can take longer to start than the feed lasts
+    a, b = _spawn(cluster.address, slow=0.01, idle=30000), _spawn(cluster.address, slow=0.01, idle=30000)
     t0 = time.monotonic()
     while len(cluster.commit_log) < 6 and time.monotonic() - t0 < 60:
         time.sleep(0.05)
