@@ -16,10 +16,16 @@ $CXX $COMMON -fsanitize=address,undefined -fno-sanitize-recover=undefined tests/
     -o "$OUT/ring_stress_asan" -lrt -lz
 $CXX $COMMON -fsanitize=address,undefined -fno-sanitize-recover=undefined tests/native/codec_fuzz.cpp $SRCS \
     -o "$OUT/codec_fuzz_asan" -lrt -lz
+# the HIP command queue (csrc/hip/hip_queue.*) with its two device calls stubbed (no GPU)
+HQ="-D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Itorchkafka_amd/csrc/hip tests/native/hip_queue_test.cpp torchkafka_amd/csrc/hip/hip_queue.cpp"
+$CXX $COMMON -fsanitize=thread $HQ -o "$OUT/hip_queue_tsan"
+$CXX $COMMON -fsanitize=address,undefined -fno-sanitize-recover=undefined $HQ -o "$OUT/hip_queue_asan"
 export TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1"
 export ASAN_OPTIONS="halt_on_error=1 detect_leaks=1"
 export UBSAN_OPTIONS="halt_on_error=1 print_stacktrace=1"
 echo "== tsan ring_stress"; "$OUT/ring_stress_tsan" 4 3 ${TK_SAN_BATCHES:-2000}
 echo "== asan ring_stress"; "$OUT/ring_stress_asan" 4 3 ${TK_SAN_BATCHES:-2000}
 echo "== asan codec_fuzz"; "$OUT/codec_fuzz_asan" ${TK_SAN_FUZZ:-3000}
+echo "== tsan hip_queue"; "$OUT/hip_queue_tsan" ${TK_SAN_QUEUE:-50000}
+echo "== asan hip_queue"; "$OUT/hip_queue_asan" ${TK_SAN_QUEUE:-50000}
 echo "sanitizers: all clean"

@@ -1,5 +1,7 @@
 #include "hip_queue.h"
 
+#include <hip/hip_runtime_api.h>
+
 #include <chrono>
 #include <cstdlib>
 #include <ctime>
@@ -128,7 +130,12 @@ void HipQueue::run() {
     }
     std::unique_lock<std::mutex> lk(sleep_m_);
     sleeping_.store(true, std::memory_order_seq_cst);
-    if (submitted_.load(std::memory_order_seq_cst) < next) wake_.wait_for(lk, std::chrono::milliseconds(5));
+    // the timeout is a safety net only (the seq_cst hand-off above loses no wake-up); it is taken
+    // against the system clock -- pthread_cond_timedwait, which ThreadSanitizer follows (the
+    // steady-clock wait_for calls pthread_cond_clockwait, which GCC 11's TSan does not intercept:
+    // it then reports the sleeping thread as still holding sleep_m_)
+    if (submitted_.load(std::memory_order_seq_cst) < next)
+      wake_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(5));
     sleeping_.store(false, std::memory_order_release);
     idle = 0;
   }

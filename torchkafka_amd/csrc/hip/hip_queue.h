@@ -21,8 +21,6 @@
 // GPU suite passes with every loader on the queue (r04_s14).
 #pragma once
 
-#include <hip/hip_runtime.h>
-
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
