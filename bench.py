@@ -80,6 +80,9 @@ def parse():
     ap.add_argument("--no-crc", action="store_true", help="skip CRC32C verification (kafka-python check_crcs)")
     ap.add_argument("--device", default=None, help="override device (e.g. cpu for a dry run)")
     ap.add_argument("--stats", action="store_true", help="print loader stats to stderr")
+    ap.add_argument("--window-trace", type=int, default=0,
+                    help="diagnostic: after the headline, time this many more headline-sized windows step by "
+                         "step and print where their time goes to stderr")
     ap.add_argument("--in-order", action="store_true", help="strict worker round-robin delivery")
     ap.add_argument("--event-every", type=int, default=None)
     ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy", "direct"])
@@ -290,8 +293,9 @@ class Rank:
                 "rank_id_sum": s}
 
 
-def time_steps(R: Rank, it, steps: int, loader) -> dict:
-    """Times ``steps`` batches: barrier + synchronize on both sides, max time over ranks."""
+def time_steps(R: Rank, it, steps: int, loader, trace: list | None = None) -> dict:
+    """Times ``steps`` batches: barrier + synchronize on both sides, max time over ranks.
+    ``trace`` (diagnostic): receives each step's end time and the closing sync's, from t0, in ns."""
     loader.reset_stats()
     R.sync()
     occ = loader.ring_occupancy()
@@ -301,13 +305,55 @@ def time_steps(R: Rank, it, steps: int, loader) -> dict:
     for _ in range(steps):
         x = next(it)
         rows += (x[0] if isinstance(x, (tuple, list)) else x).shape[0]
+        if trace is not None:
+            trace.append(time.perf_counter() - t0)
     R.sync()
     el = time.perf_counter() - t0
+    if trace is not None:
+        trace.append(el)
     per_rank = R.gather([el, float(rows)])
     tmax = max(p[0] for p in per_rank)
     total = sum(p[1] for p in per_rank)
     st = loader.stats_summary()
     return {"el": tmax, "rows": total, "per_rank": per_rank, "stats": st, "occ": occ, "last": x}
+
+
+def window_trace(R: Rank, it, steps: int, n: int, loader) -> dict:
+    """Diagnostic (--window-trace): ``n`` windows shaped like the headline's, each step's host time
+    and the closing synchronize timed apart, and the native driver's counters over each window.
+    Medians over the windows, in microseconds (counters: per window)."""
+    per_step, tails, totals = [[] for _ in range(steps)], [], []
+    keys = ("groups", "ahead_groups", "ahead_ns", "phase_launch_ns", "phase_next_ns", "phase_commit_ns",
+            "fast_ns", "poll_ns", "blocked_ns", "verify_wait_ns", "events", "released")
+    ctr = {k: [] for k in keys}
+    run = getattr(loader, "_run", None)
+    drv = run.driver if run is not None else None
+    for _ in range(n):
+        if drv is not None:
+            drv.reset_stats()
+        R.sync()
+        t0 = t = time.perf_counter_ns()
+        for k in range(steps):
+            next(it)
+            u = time.perf_counter_ns()
+            per_step[k].append(u - t)
+            t = u
+        R.sync()
+        u = time.perf_counter_ns()
+        tails.append(u - t)
+        totals.append(u - t0)
+        if drv is not None:
+            st = drv.stats()
+            for k in keys:
+                if isinstance(st.get(k, 0), (int, float)):
+                    ctr[k].append(st.get(k, 0))
+
+    def med(xs):
+        return round(sorted(xs)[len(xs) // 2] / 1e3, 2)
+
+    return {"windows": n, "steps": steps, "window_us": med(totals), "steps_us": [med(x) for x in per_step],
+            "host_us": round(sum(med(x) for x in per_step), 1), "sync_tail_us": med(tails),
+            "counters": {k: (med(v) if k.endswith("_ns") else sorted(v)[len(v) // 2]) for k, v in ctr.items() if v}}
 
 
 def steady_block(R: Rank, res: dict, steps: int, dim: int) -> dict:
@@ -465,7 +511,8 @@ def run_rank(args) -> int:
     extra_warm = max(50, args.warmup)
 
     def backlog(steady_n, extra_n):
-        consumed = max(args.warmup + args.steps + steady_n, (extra_warm + extra_n) if extra else 0)
+        consumed = max(args.warmup + args.steps * (1 + args.window_trace) + steady_n,
+                       (extra_warm + extra_n) if extra else 0)
         batches = consumed + args.workers * ((args.slots_per_worker or 8) + 2)
         return int(math.ceil(batches * B * 1.25 / max(1, len(mine)))) + B
 
@@ -520,10 +567,16 @@ def run_rank(args) -> int:
 
     for _ in range(max(0, args.warmup - 1)):
         x = next(it)
-    head = time_steps(R, it, args.steps, loader)
+    head_trace = [] if args.window_trace > 0 else None
+    head = time_steps(R, it, args.steps, loader, head_trace)
+    if head_trace and rank == 0:
+        print(json.dumps({"headline_trace_us": [round(x * 1e6, 1) for x in head_trace]}), file=sys.stderr)
     elapsed, total_rows, stats = head["el"], head["rows"], head["stats"]
     value = total_rows / elapsed
     h2d_desc, decode_desc = describe(loader)
+
+    if args.window_trace > 0 and rank == 0:
+        print(json.dumps({"window_trace": window_trace(R, it, args.steps, args.window_trace, loader)}), file=sys.stderr)
 
     # Steady state, same loader, right after the headline: many times the ring depth, so the batches
     # the workers had prefilled before t0 are a small part of it and the producer side (fetch, pack,

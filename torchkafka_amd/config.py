@@ -49,6 +49,9 @@ PROCESS_ENV = {
                             "the stepping thread instead of, in order, on a thread of their own (csrc/hip/hip_queue.h)",
     "TORCHKAFKA_MIRROR_WAIT": "1: a mirror launch waits for the copy of a chunk still in flight instead of reading "
                               "that segment from the pinned log (round-3 behaviour; A/B only)",
+    "TORCHKAFKA_SPAN_SPLIT": "workgroups per log segment of the fixed-width decode kernel reading over PCIe (1, 2 "
+                             "or 4; default 1 -- 2 and 4 measured slower; span_decode.hip step 0)",
+    "TORCHKAFKA_MIRROR_SPLIT": "the same for launches reading the HBM mirror (default 1)",
 }
 
 

@@ -344,6 +344,8 @@ PYBIND11_MODULE(_tkhip, m) {
              s["verify_wait_ns"] = d.verify_wait_ns_;
              return s;
            })
+      .def_property_readonly("span_split", &MainDriver::span_split)
+      .def_property_readonly("mirror_split", &MainDriver::mirror_split)
       .def("reset_stats", &MainDriver::reset_stats)
       .def("set_event_every", &MainDriver::set_event_every, py::arg("n"))
       .def_property_readonly("event_every", &MainDriver::event_every)

@@ -449,6 +449,7 @@ void MainDriver::launch_span(const int* slots, const SlotView* const* views, int
   bool pcie = false;  // a segment of this launch is read over PCIe (not from the HBM mirror)
   auto flush = [&](bool record) {
     a.burst = pcie ? span_burst_ : mirror_burst_;  // loads a wave keeps in flight (span_decode.hip stage 1)
+    a.split = pcie ? span_split_ : mirror_split_;
     pcie = false;
     if (mirror) mirror->before(stream);
     eng_->collate_span(slots, n, stream, a, v0.src_dtype, dst_dt, shift, scale, record);

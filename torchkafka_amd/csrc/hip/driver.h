@@ -136,6 +136,10 @@ class MainDriver {
   void ahead_launch_json(int dst_dt, double pad, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
                          uint8_t* const* masks, std::vector<std::shared_ptr<void>>&& handles);
   void set_ahead_depth(int n) { ahead_depth_ = n < 0 ? 0 : n; }
+  int ahead_depth() const { return ahead_depth_; }
+  // (stream, bytes) of the output blocks already cached on a decode stream (torch_step.cpp
+  // warm_group_blocks)
+  std::vector<std::pair<hipStream_t, int64_t>> warm_blocks_;
   // Device-counted JSON batches (kSlotDevCount, span.h kJsonCountOnDevice).  Their outputs are
   // allocated at the worker's bound (max_row_len); the parse kernel picks the real width from the
   // device count of the longest row, rounded up to `mult` (0: the allocated width stays, pad_to).
@@ -154,6 +158,9 @@ class MainDriver {
   // LDS-DMA loads a wave of the span decode kernel keeps in flight before it waits (0 = all;
   // default 1; TORCHKAFKA_SPAN_BURST)
   void set_span_burst(int n) { span_burst_ = n < 0 ? 0 : n > 8 ? 8 : n; }
+  // Workgroups per segment of the fixed-width decode kernel over PCIe / from the HBM mirror
+  int span_split() const { return span_split_; }
+  int mirror_split() const { return mirror_split_; }
   // The stream the next device-decode group launch runs on (its outputs are allocated there).
   hipStream_t next_decode_stream() { return eng_->decode_stream(int(span_launches_ % 4096)); }
   void set_coalesce(int n) { coalesce_ = n < 1 ? 1 : (n > kMaxGroup ? kMaxGroup : n); }
@@ -369,6 +376,15 @@ class MainDriver {
     const int v = e ? std::atoi(e) : 1;
     return v < 0 ? 0 : v > 8 ? 8 : v;
   }();
+  // Workgroups per segment of the fixed-width decode kernel (1, 2 or 4; span_decode.hip step 0),
+  // for launches read over PCIe and from the HBM mirror; TORCHKAFKA_SPAN_SPLIT / _MIRROR_SPLIT
+  static int split_env(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    const int v = e ? std::atoi(e) : dflt;
+    return v >= 4 ? 4 : v >= 2 ? 2 : 1;
+  }
+  int span_split_ = split_env("TORCHKAFKA_SPAN_SPLIT", 1);
+  int mirror_split_ = split_env("TORCHKAFKA_MIRROR_SPLIT", 1);
   // ... for a launch whose segments all come from the HBM mirror: HBM takes every load of a wave at
   // once (0), where PCIe reads lose bandwidth with many in flight (mirror decode: 34.1 us per group
   // at 1, 27.8 us at 0, 29.9 us at 4; profiles/r03_s3/burst/); TORCHKAFKA_MIRROR_BURST

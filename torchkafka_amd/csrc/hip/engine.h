@@ -86,6 +86,9 @@ class Engine {
   }
   // Device copy of the CRC tables of the span kernel (uploaded on first use).
   const uint32_t* span_tables();
+  // The part-CRC words of span decode launches split over workgroups on `stream` (a decode stream:
+  // its launches run in order, and each leaves the words zeroed); nullptr for any other stream.
+  uint32_t* part_crc(hipStream_t stream);
   // The streams device-decode groups rotate over (created on first use; kDecodeStreams).
   hipStream_t decode_stream(int k);
   int decode_streams() const { return n_decode_; }
@@ -139,6 +142,7 @@ class Engine {
   size_t host_len_ = 0;
   uint32_t* span_tabs_ = nullptr;
   hipStream_t decode_streams_[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint32_t* part_crc_ = nullptr;  // [4 decode streams][kMaxLaunchSegs][kPartCrcWords]
   int n_decode_ = default_decode_streams();
   static int default_decode_streams();
   std::vector<hipEvent_t> order_events_;  // stream_after: a small pool used round-robin

@@ -73,6 +73,7 @@ Engine::~Engine() {
   for (auto e : copied_) hipEventDestroy(e);
   if (staging_) hipFree(staging_);
   if (span_tabs_) hipFree(span_tabs_);
+  if (part_crc_) hipFree(part_crc_);
   for (auto st : decode_streams_)
     if (st) {
       hipStreamSynchronize(st);
@@ -291,6 +292,21 @@ const uint32_t* Engine::span_tables() {
   return span_tabs_;
 }
 
+uint32_t* Engine::part_crc(hipStream_t stream) {
+  int k = -1;
+  for (int i = 0; i < 4; ++i)
+    if (decode_streams_[i] && decode_streams_[i] == stream) k = i;
+  if (k < 0) return nullptr;
+  constexpr size_t per = size_t(kMaxLaunchSegs) * kPartCrcWords;
+  if (!part_crc_) {
+    TKH_CHECK(hipSetDevice(device_));
+    TKH_CHECK(hipMalloc(reinterpret_cast<void**>(&part_crc_), 4 * per * sizeof(uint32_t)));
+    TKH_CHECK(hipMemset(part_crc_, 0, 4 * per * sizeof(uint32_t)));
+    TKH_CHECK(hipDeviceSynchronize());  // zeroed before any launch reads it
+  }
+  return part_crc_ + size_t(k) * per;
+}
+
 int Engine::default_decode_streams() {
   // three decode streams + the user's stream fill the 4 hardware queues HIP gives a process by
   // default (config 2: 2 streams 52.9 M rec/s, 3 streams 54.0 M, 4 streams 45.0 M -- the fourth
@@ -353,6 +369,8 @@ void Engine::collate_span(const int* slots, int n, hipStream_t user, SpanLaunch&
     if (a.b[k].ext_words) a.b[k].ext_src = reinterpret_cast<const int64_t*>(src_base(slots[k]) + a.b[k].ext_off);
   }
   a.tabs = span_tables();
+  if (a.split < 1) a.split = 1;
+  if (a.split > 1 && !(a.part_crc = part_crc(user))) a.split = 1;  // not a decode stream: one workgroup
   if (queued(user)) {
     HipQueue::get().submit([a, src_dt, dst_dt, shift, scale, user] {
       launch_span_decode(a, src_dt, dst_dt, shift, scale, user);

@@ -6,8 +6,9 @@
 // then `_process` and torch.stack (kafka_dataset.py:156-162) -- and, in this
 // framework's host path, the worker's CRC pass and value copy into the ring slot.
 //
-// One 256-thread workgroup per segment: stage it in LDS and verify its RecordBatch CRC32C
-// (span_device.h), then
+// One 256-thread workgroup per segment (or `split` of them, each with a share of its CRC lanes and
+// bytes -- opt-in, slower over PCIe: profiles/r04_s21_window): stage it in LDS and verify its
+// RecordBatch CRC32C (span_device.h), then
 //   values: a wave per row for rows of >= 32 16-byte groups (lanes over the row's groups
 //   held by this segment), else (row, group) pairs strided over the block; each group is
 //   read as two aligned 16-byte LDS reads cut to the group's bytes (span::lds16: values sit
@@ -60,7 +61,9 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
   __shared__ uint32_t wcrc[kThreads / 64];
 
   const int t = int(threadIdx.x);
-  const SpanDevSeg& sg = a.s[blockIdx.x];
+  const int P = a.split, part = int(blockIdx.x) % P;
+  const int nl = int(tk::kSpanLanes) / P;  // CRC lanes of the whole segment's layout per part
+  const SpanDevSeg& sg = a.s[blockIdx.x / P];
   const SpanBatchOut& bo = a.b[sg.batch];
   const uint32_t len = sg.len, flags = sg.flags;
   const int32_t head = int32_t(reinterpret_cast<uintptr_t>(sg.src) & 15u);
@@ -68,9 +71,36 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
   const uint32_t nrows = sg.row_end - row_begin;
   const bool do_crc = (flags & tk::kSegCrc) != 0;
 
+  // ---- 0. split: P workgroups share the segment.  Part j runs CRC lanes [j nl, (j+1) nl) of the
+  // whole segment's layout (chunks of L bytes ending at its last byte), owns the values whose
+  // 16-byte group starts in those lanes' bytes, and stages them with a margin.  Coordinates below
+  // are LDS bytes of this part's image: the whole-segment image's shifted down by `sh` (a multiple
+  // of 16, so 16-byte slots stay aligned).
+  const int32_t w_lo = kFront + head, w_hi = w_lo + int32_t(len);  // the segment, whole image
+  int32_t o_lo = w_lo, o_hi = w_hi, sh = 0;
+  const uint8_t* src = sg.src;
+  uint32_t slen = len;
+  if (P > 1) {
+    const int32_t c0 = w_lo + ((flags & tk::kSegCrcFirst) ? 21 : 0);
+    const int32_t L = int32_t(tk::span_lane_bytes(uint32_t(w_hi - c0)));
+    auto cut = [&](int q) {
+      const int32_t x = w_hi - (int32_t(tk::kSpanLanes) - q * nl) * L;
+      return x < w_lo ? w_lo : x;
+    };
+    if (part > 0) o_lo = cut(part);
+    if (part < P - 1) o_hi = cut(part + 1);
+    const int32_t s_lo = o_lo - 16 > w_lo ? o_lo - 16 : w_lo;
+    const int32_t s_hi = o_hi + 32 < w_hi ? o_hi + 32 : w_hi;
+    src = sg.src + (s_lo - w_lo);
+    slen = s_hi > s_lo ? uint32_t(s_hi - s_lo) : 0u;
+    sh = head + (s_lo - w_lo) - int32_t(reinterpret_cast<uintptr_t>(src) & 15u);
+  }
+  const int32_t lo_b = w_lo - sh, hi_b = w_hi - sh;  // the segment's bytes (valid where staged)
+  const int32_t own_lo = o_lo - sh, own_hi = o_hi - sh;
+
   // ---- 1. stage the segment (span_device.h); the row positions and CRC tables load behind it
-  span::stage(sg.src, len, buf, a.burst, [&] {
-    const int64_t base = int64_t(sg.log_pos) - int64_t(head) - kFront;  // log position of LDS byte 0
+  span::stage(src, slen, buf, a.burst, [&] {
+    const int64_t base = int64_t(sg.log_pos) - int64_t(head) - kFront + sh;  // log position of LDS byte 0
     for (uint32_t r = uint32_t(t); r < nrows; r += kThreads)
       rel[r] = int32_t(int64_t(bo.row_pos[row_begin + r]) - base);
     if (do_crc)
@@ -79,11 +109,10 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
   __syncthreads();
   const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
   const uint4* b128 = reinterpret_cast<const uint4*>(buf);  // 16-byte slots (span::lds16)
-  const int32_t lo_b = kFront + head, hi_b = kFront + head + int32_t(len);  // valid LDS bytes
 
-  // ---- 2. CRC32C lanes
+  // ---- 2. CRC32C lanes (a part: its lanes on its first nl threads, whole waves)
   const uint32_t* shift_set = nullptr;
-  if (do_crc) shift_set = span::crc_lanes(b32, tab, a.tabs, lo_b, hi_b, flags, wcrc);
+  if (do_crc && t < nl) shift_set = span::crc_lanes(b32, tab, a.tabs, lo_b, hi_b, flags, wcrc, part * nl);
 
   // ---- 3. values -> out[row, :]
   {
@@ -96,6 +125,8 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
       const int64_t rem = RE - e0;
       const int nel = rem < kPer ? int(rem) : kPer;
       if (b0 + nel * int32_t(sizeof(S)) <= lo_b || b0 >= hi_b) return;  // group held by another segment
+      const int32_t key = b0 > lo_b ? b0 : lo_b;
+      if (key < own_lo || key >= own_hi) return;  // held by another part of this segment
       D* __restrict__ orow = out + int64_t(row_begin + rr) * RE;
       if (nel == kPer && b0 >= lo_b && b0 + 16 <= hi_b) {
         const uint4 o = span::lds16(b128, b0);
@@ -148,13 +179,30 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
   }
 
   // ---- 4. record fields beside the values (key / timestamp): the batch's first segment copies them
-  if (sg.seg == 0 && bo.ext_words)
+  if (sg.seg == 0 && part == 0 && bo.ext_words)
     for (uint32_t i = uint32_t(t); i < bo.ext_words; i += kThreads) bo.ext_out[i] = bo.ext_src[i];
 
-  // ---- 5. verdict
+  // ---- 5. verdict; split: each part leaves its wave CRCs in part_crc and the last to arrive
+  // (agent-scope acq_rel count) combines all four, then zeroes the count for the stream's next launch
   if (do_crc) {
     __syncthreads();
-    if (t == 0) span::crc_verdict(shift_set, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials);
+    if (t == 0) {
+      if (P == 1) {
+        span::crc_verdict(shift_set, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials);
+      } else {
+        uint32_t* pc = a.part_crc + (blockIdx.x / P) * kPartCrcWords;
+        const int nw = nl / 64;
+        for (int w = part * nw; w < (part + 1) * nw; ++w)
+          __hip_atomic_store(pc + w, wcrc[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t prev = __hip_atomic_fetch_add(pc + 4, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == uint32_t(P - 1)) {
+          uint32_t all[4];
+          for (int w = 0; w < 4; ++w) all[w] = __hip_atomic_load(pc + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(pc + 4, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          span::crc_verdict(shift_set, all, flags, sg.crc, sg.seg, bo.err, bo.partials);
+        }
+      }
+    }
   }
 }
 
@@ -275,12 +323,11 @@ void launch_var_span_t(const VarSpanLaunch& a, double pad, hipStream_t stream) {
 template <typename S, typename D>
 void launch_span_t(const SpanLaunch& a, const float* shift, const float* scale, hipStream_t stream) {
   if (a.n_seg <= 0) return;
+  const dim3 grid(unsigned(a.n_seg * a.split));
   if (shift)
-    hipLaunchKernelGGL((span_decode_kernel<S, D, true>), dim3(unsigned(a.n_seg)), dim3(kThreads), 0, stream, a, shift,
-                       scale);
+    hipLaunchKernelGGL((span_decode_kernel<S, D, true>), grid, dim3(kThreads), 0, stream, a, shift, scale);
   else
-    hipLaunchKernelGGL((span_decode_kernel<S, D, false>), dim3(unsigned(a.n_seg)), dim3(kThreads), 0, stream, a,
-                       shift, scale);
+    hipLaunchKernelGGL((span_decode_kernel<S, D, false>), grid, dim3(kThreads), 0, stream, a, shift, scale);
 }
 
 }  // namespace
@@ -316,6 +363,8 @@ void launch_var_span(const VarSpanLaunch& a, int src_dt, int dst_dt, double pad,
 void launch_span_decode(const SpanLaunch& a, int src_dt, int dst_dt, const float* shift, const float* scale,
                         hipStream_t stream) {
   if (a.n_seg < 0 || a.n_seg > kMaxLaunchSegs) throw std::invalid_argument("span decode: bad segment count");
+  if ((a.split != 1 && a.split != 2 && a.split != 4) || (a.split > 1 && a.part_crc == nullptr))
+    throw std::invalid_argument("span decode: bad split");
   if (!is_float_dt(dst_dt) && is_float_dt(src_dt))
     throw std::invalid_argument("collate: float records cannot be cast to an integer dtype");
   if (shift && !is_float_dt(dst_dt)) throw std::invalid_argument("collate: normalisation needs a float dtype");

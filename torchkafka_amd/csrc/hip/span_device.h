@@ -140,10 +140,12 @@ __device__ __forceinline__ uint32_t nib_dword(uint32_t nbase, uint32_t w) {
 // [c0, c1) in LDS bytes: [lo_b + 21, hi_b) for the segment holding a RecordBatch's start, else
 // [lo_b, hi_b); `tab` is the LDS copy of the nibble rows (load_nib_rows).  Each wave's lane 0 leaves the wave's CRC in wcrc[wave]; returns the shift-table
 // set of the lane size used (for crc_verdict).
+// `lane_base`: a workgroup that holds only part of the range (span_decode_kernel's split) runs
+// lanes lane_base.. of the whole range's layout on its first threads (whole waves).
 __device__ __forceinline__ const uint32_t* crc_lanes(const uint32_t* __restrict__ b32, const uint32_t* __restrict__ tab,
                                                      const uint32_t* __restrict__ tabs, int32_t lo_b, int32_t hi_b,
-                                                     uint32_t flags, uint32_t* wcrc) {
-  const int t = int(threadIdx.x);
+                                                     uint32_t flags, uint32_t* wcrc, int lane_base = 0) {
+  const int t = int(threadIdx.x) + lane_base;
   const uint32_t* shift_set = tabs + tk::kSpanTabShift;
   uint32_t crc = 0;
   const uint32_t nbase = uint32_t(uintptr_t((lds_u32*)tab));  // the LDS byte address

@@ -135,6 +135,24 @@ struct StreamScope {
   ~StreamScope() { c10::hip::setCurrentHIPStream(prev); }
 };
 
+// The first group of a size on a decode stream: the caching allocator has no block of it there
+// yet, so each of the first few launches per stream paid a hipMalloc -- 40-80 us on the stepping
+// thread, against 11 us for a warm launch, in the first 20-step window after warm-up
+// (bench.py --window-trace; profiles/r04_s25).  Allocating and dropping as many blocks as a stream
+// holds at once (the decode-ahead depth, the delivered batch, one spare) caches them on that
+// stream up front.  Groups above 64 MiB are left alone (config 5's are 16 MiB).
+void warm_group_blocks(MainDriver& d, hipStream_t ks, const std::vector<int64_t>& shape,
+                       const at::TensorOptions& opts) {
+  int64_t bytes = int64_t(c10::elementSize(c10::typeMetaToScalarType(opts.dtype())));
+  for (auto x : shape) bytes *= x;
+  if (bytes <= 0 || bytes > (int64_t(64) << 20)) return;
+  for (const auto& w : d.warm_blocks_)
+    if (w.first == ks && w.second == bytes) return;
+  d.warm_blocks_.emplace_back(ks, bytes);
+  std::vector<at::Tensor> hold;
+  for (int i = 0; i < d.ahead_depth() + 2; ++i) hold.push_back(at::empty(shape, opts));
+}
+
 // Output block of a coalesced fixed-width launch.  Device decode runs on the driver's decode
 // stream: allocate there, so the caching allocator orders the memory's reuse against that stream
 // (no wait on the user's stream, which already waits for the previous group), and record the
@@ -146,6 +164,7 @@ at::Tensor alloc_group(MainDriver& d, const std::vector<int64_t>& shape, const a
   at::Tensor all;
   {
     StreamScope scope(ks, dev);
+    warm_group_blocks(d, ks.stream(), shape, opts);
     all = at::empty(shape, opts);
   }
   c10::hip::HIPCachingAllocator::recordStream(all.storage().data_ptr(), c10::hip::getCurrentHIPStream(dev));
