@@ -46,6 +46,32 @@ static_assert(kSpanLaneLarge * kSpanLanes >= kSpanSegMax, "lanes must cover a wh
 inline constexpr uint32_t span_lane_bytes(uint32_t crc_len) {
   return crc_len <= kSpanLaneSmall * kSpanLanes ? kSpanLaneSmall : kSpanLaneLarge;
 }
+
+// A segment decoded by `parts` workgroups (span_decode.hip step 0; parts = 1, 2 or 4).  Part j runs
+// CRC lanes [j n, (j+1) n) (n = kSpanLanes / parts) of the whole segment's lane layout, owns the
+// bytes those lanes cover (the first part also the bytes before the CRC range, the last part up to
+// the end) -- a value's 16-byte group belongs to the part owning its first byte in the segment --
+// and stages its bytes with 16 before and 32 after (a group starting at the end of its range, and
+// the lanes' dword reads).  Offsets from the segment's first byte, `len` its length, `crc_first`:
+// the segment holds its RecordBatch's start (CRC from byte 21).  Tested by
+// tests/native/span_split_test.cpp.
+struct SpanPart {
+  int32_t own_lo, own_hi;      // the bytes this part checks and decodes
+  int32_t stage_lo, stage_hi;  // the bytes it stages
+};
+inline constexpr int32_t span_part_cut(uint32_t len, bool crc_first, int parts, int q) {
+  const int32_t n = int32_t(len), c0 = crc_first ? 21 : 0;
+  const int32_t L = int32_t(span_lane_bytes(uint32_t(n - c0)));
+  const int32_t x = n - (int32_t(kSpanLanes) - q * (int32_t(kSpanLanes) / parts)) * L;
+  return x < 0 ? 0 : x;
+}
+inline constexpr SpanPart span_part(uint32_t len, bool crc_first, int parts, int part) {
+  const int32_t n = int32_t(len);
+  if (parts <= 1) return SpanPart{0, n, 0, n};
+  const int32_t lo = part > 0 ? span_part_cut(len, crc_first, parts, part) : 0;
+  const int32_t hi = part < parts - 1 ? span_part_cut(len, crc_first, parts, part + 1) : n;
+  return SpanPart{lo, hi, lo - 16 > 0 ? lo - 16 : 0, hi + 32 < n ? hi + 32 : n};
+}
 // Device table layout (uint32 words): slice-by-8 byte tables T0..T7, then for each lane size
 // (small, large), level j and byte k of the value: shift-by-(L << j)-bytes of (b << 8k), then the
 // nibble split of T0..T7 the kernels keep in LDS: row 2k + h holds T_k[n << 4h] for n < 16.  A

@@ -104,7 +104,7 @@ void HipQueue::wait(uint64_t seq) {
 }
 
 void HipQueue::run() {
-  hipSetDevice(device_);
+  (void)hipSetDevice(device_);  // a failure shows in the first queued call
   uint64_t next = 1;
   int idle = 0;
   while (!stop_.load(std::memory_order_acquire)) {

@@ -81,19 +81,12 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
   const uint8_t* src = sg.src;
   uint32_t slen = len;
   if (P > 1) {
-    const int32_t c0 = w_lo + ((flags & tk::kSegCrcFirst) ? 21 : 0);
-    const int32_t L = int32_t(tk::span_lane_bytes(uint32_t(w_hi - c0)));
-    auto cut = [&](int q) {
-      const int32_t x = w_hi - (int32_t(tk::kSpanLanes) - q * nl) * L;
-      return x < w_lo ? w_lo : x;
-    };
-    if (part > 0) o_lo = cut(part);
-    if (part < P - 1) o_hi = cut(part + 1);
-    const int32_t s_lo = o_lo - 16 > w_lo ? o_lo - 16 : w_lo;
-    const int32_t s_hi = o_hi + 32 < w_hi ? o_hi + 32 : w_hi;
-    src = sg.src + (s_lo - w_lo);
-    slen = s_hi > s_lo ? uint32_t(s_hi - s_lo) : 0u;
-    sh = head + (s_lo - w_lo) - int32_t(reinterpret_cast<uintptr_t>(src) & 15u);
+    const tk::SpanPart pr = tk::span_part(len, (flags & tk::kSegCrcFirst) != 0, P, part);  // span.h
+    o_lo = w_lo + pr.own_lo;
+    o_hi = w_lo + pr.own_hi;
+    src = sg.src + pr.stage_lo;
+    slen = uint32_t(pr.stage_hi - pr.stage_lo);
+    sh = head + pr.stage_lo - int32_t(reinterpret_cast<uintptr_t>(src) & 15u);
   }
   const int32_t lo_b = w_lo - sh, hi_b = w_hi - sh;  // the segment's bytes (valid where staged)
   const int32_t own_lo = o_lo - sh, own_hi = o_hi - sh;
