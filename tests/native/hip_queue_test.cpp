@@ -3,7 +3,9 @@
 // thread makes are stubbed below, so no GPU is needed.  Checks: calls run in submission order;
 // wait(seq) returns once call seq ran; a call made while the thread sleeps with nothing queued runs
 // inline on the caller, and the calls after it run on the thread again; a failing call is reported
-// to the caller.
+// to the caller -- and every later ran() / wait() / submit() of that queue throws (a slot whose
+// launch was skipped is never reported done), while another loader's queue keeps working; a
+// queue's destructor stops its thread.
 #include <hip/hip_runtime_api.h>
 
 #include <atomic>
@@ -32,7 +34,7 @@ extern "C" hipError_t hipSetDevice(int) { return hipSuccess; }
 
 int main(int argc, char** argv) {
   const int n = argc > 1 ? std::atoi(argv[1]) : 200000;
-  tkh::HipQueue& q = tkh::HipQueue::get();
+  tkh::HipQueue q(0);
   CHECK(q.on());
 
   // 1. order: every call sees exactly its predecessors' effects; waits at random points
@@ -80,6 +82,44 @@ int main(int argc, char** argv) {
     reported = std::string(e.what()).find("boom") != std::string::npos;
   }
   CHECK(reported);
-  std::printf("hip_queue_test: ok (%d ordered calls, inline path, failure report)\n", n);
+
+  // 4. after the failure the queue answers nothing: a later call was skipped, and ran() of it (or of
+  // any number) throws instead of reporting it done; so do wait() and submit()
+  tkh::HipQueue f(0);
+  std::atomic<bool> skipped_ran{false};
+  uint64_t s_bad = 0, s_after = 0;
+  for (int tries = 0; tries < 100 && s_bad == 0; ++tries) {
+    // queue behind a slow call, so the failing call and the one after it run on the thread
+    f.submit([] { std::this_thread::sleep_for(std::chrono::milliseconds(5)); });
+    s_bad = f.submit([] { throw std::runtime_error("launch failed"); });
+  }
+  CHECK(s_bad != 0);
+  s_after = f.submit([&skipped_ran] { skipped_ran.store(true); });
+  auto throws = [](auto&& fn) {
+    try {
+      fn();
+    } catch (const std::runtime_error& e) {
+      return std::string(e.what()).find("launch failed") != std::string::npos;
+    }
+    return false;
+  };
+  CHECK(throws([&] { f.wait(s_after); }));
+  CHECK(!skipped_ran.load());
+  CHECK(throws([&] { (void)f.ran(s_after); }));
+  CHECK(throws([&] { (void)f.ran(1); }));
+  CHECK(throws([&] { f.submit([] {}); }));
+  CHECK(throws([&] { f.drain(); }));
+
+  // 5. another loader's queue is not affected, and a destroyed queue stops its thread
+  {
+    tkh::HipQueue g(0);
+    std::atomic<int> ok{0};
+    for (int i = 0; i < 100; ++i) g.submit([&ok] { ok.fetch_add(1); });
+    g.drain();
+    CHECK(ok.load() == 100);
+    CHECK(g.ran(1));
+  }
+  std::printf("hip_queue_test: ok (%d ordered calls, inline path, failure report, failed-queue answers, "
+              "per-loader queues)\n", n);
   return 0;
 }

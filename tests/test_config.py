@@ -38,7 +38,7 @@ def test_invalid_behaviour_rejected(kw, msg):
 
 @pytest.mark.parametrize("kw,msg", [
     ({"coalesce": 9}, "coalesce"), ({"copy_streams": 0}, "copy_streams"), ({"decode_streams": 5}, "decode_streams"),
-    ({"slots_per_worker": 1}, "slots_per_worker"), ({"span_burst": -1}, "span_burst"),
+    ({"slots_per_worker": 1}, "slots_per_worker"), ({"worker_spin_us": -1}, "worker_spin_us"),
     ({"ahead_depth": 99}, "ahead_depth"), ({"coalesce_wait_us": -5}, "coalesce_wait_us"),
 ])
 def test_invalid_tuning_rejected(kw, msg):
@@ -54,8 +54,8 @@ def test_environment_sets_tuning_defaults_explicit_wins(monkeypatch):
     t = Tuning()
     assert (t.ahead_depth, t.decode_streams, t.numa_bind, t.worker_spin_us) == (2, 2, False, 50)
     assert Tuning(ahead_depth=6).ahead_depth == 6
-    monkeypatch.setenv(TUNING_ENV["span_burst"], "lots")
-    with pytest.raises(ValueError, match="TORCHKAFKA_SPAN_BURST"):
+    monkeypatch.setenv(TUNING_ENV["ahead_depth"], "lots")
+    with pytest.raises(ValueError, match="TORCHKAFKA_AHEAD_DEPTH"):
         Tuning()
 
 

@@ -544,8 +544,8 @@ def test_single_process_mode_on_gpu(broker, decode):
     assert broker.committed_offsets("g", "t") == {0: 128, 1: 128}
 
 
-@pytest.mark.parametrize("tuning", [dict(decode_streams=1, span_burst=0, ahead_depth=0),
-                                    dict(decode_streams=2, span_burst=4, ahead_depth=8, coalesce=2)])
+@pytest.mark.parametrize("tuning", [dict(decode_streams=1, ahead_depth=0),
+                                    dict(decode_streams=2, ahead_depth=8, coalesce=2)])
 def test_tuning_knobs_do_not_change_results(broker, tuning):
     from torchkafka_amd import DeviceLoader, FixedWidth, auto_commit
 

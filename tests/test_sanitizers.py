@@ -1,6 +1,6 @@
 """Host sanitizers over the native core: ThreadSanitizer on the slot-ring protocol
 and the broker -> fetcher -> packer -> commit pipeline (threads standing in for worker processes),
-the HIP command queue (its device calls stubbed), the split-decode byte ranges (span.h span_part),
+the HIP command queue (its device calls stubbed), the span kernels' window geometry (span.h SpanWindows),
 AddressSanitizer + UBSan on the same stress test and on a RecordBatch/CRC32C/JSON fuzz test.
 The sources are tests/native/*.cpp; tools/sanitize.sh builds and runs them."""
 import os

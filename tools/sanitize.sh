@@ -21,7 +21,7 @@ HQ="-D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Itorchkafka_amd/csrc/hip tests/n
 $CXX $COMMON -fsanitize=thread $HQ -o "$OUT/hip_queue_tsan"
 $CXX $COMMON -fsanitize=address,undefined -fno-sanitize-recover=undefined $HQ -o "$OUT/hip_queue_asan"
 $CXX $COMMON -fsanitize=address,undefined -fno-sanitize-recover=undefined -Itorchkafka_amd/csrc/core \
-  tests/native/span_split_test.cpp -o "$OUT/span_split_asan"
+  tests/native/span_window_test.cpp -o "$OUT/span_window_asan"
 export TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1"
 export ASAN_OPTIONS="halt_on_error=1 detect_leaks=1"
 export UBSAN_OPTIONS="halt_on_error=1 print_stacktrace=1"
@@ -30,5 +30,5 @@ echo "== asan ring_stress"; "$OUT/ring_stress_asan" 4 3 ${TK_SAN_BATCHES:-2000}
 echo "== asan codec_fuzz"; "$OUT/codec_fuzz_asan" ${TK_SAN_FUZZ:-3000}
 echo "== tsan hip_queue"; "$OUT/hip_queue_tsan" ${TK_SAN_QUEUE:-50000}
 echo "== asan hip_queue"; "$OUT/hip_queue_asan" ${TK_SAN_QUEUE:-50000}
-echo "== asan span_split"; "$OUT/span_split_asan"
+echo "== asan span_window"; "$OUT/span_window_asan"
 echo "sanitizers: all clean"

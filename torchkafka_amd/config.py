@@ -28,7 +28,6 @@ TUNING_ENV = {
     "numa_bind": "TORCHKAFKA_NUMA",              # "0" disables the NUMA bind
     "ahead_depth": "TORCHKAFKA_AHEAD_DEPTH",
     "decode_streams": "TORCHKAFKA_DECODE_STREAMS",
-    "span_burst": "TORCHKAFKA_SPAN_BURST",
     "worker_spin_us": "TORCHKAFKA_WORKER_SPIN_US",
 }
 
@@ -42,16 +41,13 @@ PROCESS_ENV = {
     "TORCHKAFKA_NT_COPY": "0: plain (cached) stores when workers pack slots",
     "TORCHKAFKA_DRIVER_TRACE": "1: step-driver trace lines on stderr (debugging)",
     "TORCHKAFKA_NO_REBUILD": "1: never rebuild stale in-tree extensions at import",
-    "TORCHKAFKA_MIRROR_BURST": "LDS-DMA loads a decode wave keeps in flight when its launch reads only the HBM "
-                               "mirror (0 = all, the default; csrc/hip/driver.h)",
+    "TORCHKAFKA_DECODE_PRIORITY": "high / normal (default) / low: HIP stream priority of the decode streams "
+                                  "(csrc/hip/engine.hip; no measured effect beside a GEMM, profiles/r05_s2)",
     "TORCHKAFKA_MIRROR_COPY_STREAMS": "copy streams of the HBM mirror, partitions split p % n (1..4, default 2)",
     "TORCHKAFKA_HIP_QUEUE": "0: var-len / JSON device decode makes its decode- and mirror-copy-stream HIP calls on "
                             "the stepping thread instead of, in order, on a thread of their own (csrc/hip/hip_queue.h)",
     "TORCHKAFKA_MIRROR_WAIT": "1: a mirror launch waits for the copy of a chunk still in flight instead of reading "
                               "that segment from the pinned log (round-3 behaviour; A/B only)",
-    "TORCHKAFKA_SPAN_SPLIT": "workgroups per log segment of the fixed-width decode kernel reading over PCIe (1, 2 "
-                             "or 4; default 1 -- 2 and 4 measured slower; span_decode.hip step 0)",
-    "TORCHKAFKA_MIRROR_SPLIT": "the same for launches reading the HBM mirror (default 1)",
 }
 
 
@@ -87,7 +83,6 @@ class Tuning:
         numa_bind: bind the loader (and its workers) to the target GPU's socket.
         ahead_depth: device-decode groups launched ahead of the user's request (0..16); None = 4.
         decode_streams: HIP streams for the device decode kernels (1..4); None = 3.
-        span_burst: LDS-DMA loads a decode wave keeps in flight (0 = all, 1..8); None = 1.
         worker_spin_us: worker spin on a full sub-ring before sleeping (0..100000 us).
         mirror_chunk_mib: h2d='dma' with device decode: log bytes per hipMemcpyAsync into the HBM
             mirror of a partition log (1..1024 MiB).
@@ -116,7 +111,6 @@ class Tuning:
     numa_bind: Optional[bool] = None
     ahead_depth: Optional[int] = None
     decode_streams: Optional[int] = None
-    span_burst: Optional[int] = None
     worker_spin_us: Optional[int] = None
     mirror_chunk_mib: int = 8
     mirror_chunks: int = 6
@@ -127,7 +121,7 @@ class Tuning:
         # environment defaults for fields left at None
         if self.numa_bind is None:
             self.numa_bind = os.environ.get(TUNING_ENV["numa_bind"], "1") != "0"
-        for name in ("ahead_depth", "decode_streams", "span_burst", "worker_spin_us"):
+        for name in ("ahead_depth", "decode_streams", "worker_spin_us"):
             if getattr(self, name) is None:
                 setattr(self, name, _env_int(TUNING_ENV[name], None))
         if self.worker_spin_us is None:
@@ -147,7 +141,6 @@ class Tuning:
         _check(0 <= int(self.lockstep_depth) <= 64, "lockstep_depth must be in [0, 64]")
         _check(self.ahead_depth is None or 0 <= int(self.ahead_depth) <= 16, "ahead_depth must be in [0, 16]")
         _check(self.decode_streams is None or 1 <= int(self.decode_streams) <= 4, "decode_streams must be in [1, 4]")
-        _check(self.span_burst is None or 0 <= int(self.span_burst) <= 8, "span_burst must be in [0, 8]")
         _check(0 <= int(self.worker_spin_us) <= 100_000, "worker_spin_us must be in [0, 100000]")
         _check(1 <= int(self.mirror_chunk_mib) <= 1024, "mirror_chunk_mib must be in [1, 1024]")
         _check(2 <= int(self.mirror_chunks) <= 64, "mirror_chunks must be in [2, 64]")

@@ -312,28 +312,28 @@ void crc32c_span_tables(uint32_t* out) {
       out[kSpanTabNib + (2 * k) * 16 + n] = T.t[k][n];
       out[kSpanTabNib + (2 * k + 1) * 16 + n] = T.t[k][n << 4];
     }
-  const uint32_t lanes[2] = {kSpanLaneSmall, kSpanLaneLarge};
-  for (int set = 0; set < 2; ++set) {
-    for (uint32_t j = 0; j < kSpanLevels; ++j) {
-      const uint32_t op = T.x2nmodp(uint64_t(lanes[set]) << j, 3);  // x^(8 * L * 2^j)
-      for (int k = 0; k < 4; ++k)
-        for (uint32_t b = 0; b < 256; ++b)
-          out[kSpanTabShift + uint32_t(set) * kSpanTabShiftSet + (j * 4 + uint32_t(k)) * 256 + b] =
-              Tables::multmodp(op, b << (8 * k));
-    }
+  for (uint32_t j = 0; j < kSpanLevels; ++j) {
+    const uint32_t op = T.x2nmodp(uint64_t(kSpanPiece) << j, 3);  // x^(8 * P * 2^j)
+    for (int k = 0; k < 4; ++k)
+      for (uint32_t b = 0; b < 256; ++b)
+        out[kSpanTabShift + (j * 4 + uint32_t(k)) * 256 + b] = Tables::multmodp(op, b << (8 * k));
   }
+  const uint32_t gap = T.x2nmodp(uint64_t(kSpanWin - kSpanPiece), 3);
+  for (uint32_t i = 0; i < 8; ++i)
+    for (uint32_t n = 0; n < 16; ++n) out[kSpanTabGap + i * 16 + n] = Tables::multmodp(gap, n << (4 * i));
 }
 
 uint32_t crc32c_span_emulate(const uint8_t* buf, uint32_t c0, uint32_t c1, bool first) {
-  // Host mirror of span_decode.hip's CRC stage, step for step: end-aligned lane chunks (260 or
-  // 516 bytes) looked up in the same nibble rows, a slice-by-4 step for a chunk's first 4 bytes then slice-by-8 steps, bytes below
-  // c0 masked to zero (groups wholly below c0 skipped), the first 4 CRC'd bytes of a RecordBatch
-  // xor 0xFF (the 0xFFFFFFFF initial value), then the 8-level shift tree.
+  // Host mirror of the device CRC stage (span_device.h), step for step: windows of kSpanWin bytes
+  // ending at c1, lane t folding its kSpanPiece bytes of every window into a running state (the
+  // window gap operator between windows), looked up in the same nibble rows; a slice-by-4 step for
+  // a piece's first 4 bytes then slice-by-8 steps; bytes below c0 masked to zero (8-byte groups
+  // wholly below c0 skipped); the first 4 CRC'd bytes of a RecordBatch xor 0xFF (the 0xFFFFFFFF
+  // initial value); then the 8-level shift tree.  The range is the segment [0, c1) with c0 < 22.
   static uint32_t tab[kSpanTabWords];
   static const bool init = (crc32c_span_tables(tab), true);
   (void)init;
-  const uint32_t L = span_lane_bytes(c1 - c0);
-  const uint32_t* S0 = tab + kSpanTabShift + (L == kSpanLaneSmall ? 0u : kSpanTabShiftSet);
+  const uint32_t* S0 = tab + kSpanTabShift;
   auto byte_at = [&](int64_t ab) -> uint32_t {
     uint32_t b = ab >= int64_t(c0) ? buf[ab] : 0u;
     if (first && ab >= int64_t(c0) && ab < int64_t(c0) + 4) b ^= 0xFFu;
@@ -354,21 +354,27 @@ uint32_t crc32c_span_emulate(const uint8_t* buf, uint32_t c0, uint32_t c1, bool 
     }
     return r;
   };
-  uint32_t lane[kSpanLanes];
-  for (uint32_t t = 0; t < kSpanLanes; ++t) {
-    const int64_t start = int64_t(c1) - int64_t(kSpanLanes - t) * L;
-    uint32_t crc = 0;
-    if (start + 4 > int64_t(c0)) {
-      const uint32_t x = crc ^ word_at(start);
-      crc = nib(x, 3);
+  auto gap = [&](uint32_t c) {
+    uint32_t r = 0;
+    for (int i = 0; i < 8; ++i) r ^= tab[kSpanTabGap + i * 16 + ((c >> (4 * i)) & 15u)];
+    return r;
+  };
+  const int64_t nw = int64_t(span_windows(c1));
+  const int64_t w0 = int64_t(c1) - nw * int64_t(kSpanWin);
+  uint32_t lane[kSpanLanes] = {};
+  for (int64_t k = 0; k < nw; ++k) {
+    for (uint32_t t = 0; t < kSpanLanes; ++t) {
+      const int64_t start = w0 + k * int64_t(kSpanWin) + int64_t(t) * kSpanPiece;
+      uint32_t crc = gap(lane[t]);
+      if (start + 4 > int64_t(c0)) crc = nib(crc ^ word_at(start), 3);
+      for (uint32_t j = 0; j < (kSpanPiece - 4) / 8; ++j) {
+        const int64_t a = start + 4 + 8 * int64_t(j);
+        if (a + 8 <= int64_t(c0)) continue;
+        const uint32_t x = crc ^ word_at(a), y = word_at(a + 4);
+        crc = nib(x, 7) ^ nib(y, 3);
+      }
+      lane[t] = crc;
     }
-    for (uint32_t j = 0; j < (L - 4) / 8; ++j) {
-      const int64_t a = start + 4 + 8 * int64_t(j);
-      if (a + 8 <= int64_t(c0)) continue;
-      const uint32_t x = crc ^ word_at(a), y = word_at(a + 4);
-      crc = nib(x, 7) ^ nib(y, 3);
-    }
-    lane[t] = crc;
   }
   for (uint32_t j = 0; j < kSpanLevels; ++j) {
     const uint32_t* S = S0 + j * 4 * 256;

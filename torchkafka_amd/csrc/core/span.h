@@ -22,8 +22,8 @@
 
 namespace tk {
 
-// Largest log range one workgroup stages in LDS (plus 32 bytes of 16-byte alignment slack),
-// and most rows whose values may intersect one range (their positions are staged in LDS too).
+// Largest log range one workgroup decodes, and most rows whose values may intersect one range
+// (their positions are staged in LDS).
 constexpr uint32_t kSpanSegMax = 128u << 10;
 constexpr uint32_t kSpanMaxSegRows = 2048;
 
@@ -31,60 +31,77 @@ constexpr uint32_t kSpanMaxSegRows = 2048;
 // (Kafka's batch.size default is 16 KiB; config 2's 64 x 1 KiB records are 66 KB) are verified
 // on the device alone; longer ones are split and their partial CRCs chained by the driver.
 //
-// CRC32C on the device: a segment's CRC range [c0, c1) is cut into kSpanLanes chunks of L bytes
-// ENDING at c1 (the first chunk is front-padded with zeros, which leave a zero-initialised CRC
-// unchanged).  Each lane folds its chunk -- one slice-by-4 step for its first 4 bytes, then
-// slice-by-8 steps -- and a log2(kSpanLanes)-level tree merges neighbours with "shift by 2^j
-// chunks" operators.  L is 260 bytes (65 dwords) for ranges up to 66,560 bytes, so a config-2
-// RecordBatch (64 x 1 KiB records, 66 KB) keeps all 256 lanes busy, else 516 (129 dwords): an
-// odd dword count puts the 32 lanes of a ds_read_b32 group on 32 different LDS banks.
-constexpr uint32_t kSpanLaneSmall = 260;
-constexpr uint32_t kSpanLaneLarge = 516;
+// The kernels never hold a whole segment: they stream it through two LDS windows of kSpanWin bytes
+// (span_device.h), staging window k+1 while they check and decode window k, so a workgroup needs
+// ~45 KiB of LDS and fits on a CU beside a training job's GEMM tiles (benchmarks/compute_overlap.py).
+//
+// CRC32C on the device: a segment's CRC range [c0, c1) is cut into windows of kSpanWin bytes
+// ENDING at c1 (the first window reaches below the segment; bytes below c0 count as zeros, which
+// leave a zero CRC state unchanged).  In every window lane t folds its kSpanPiece bytes
+// [w + t P, w + (t+1) P) into a running state -- one slice-by-4 step for the piece's first 4 bytes,
+// then slice-by-8 steps -- and between windows the state crosses the other lanes' bytes with one
+// "shift by kSpanWin - kSpanPiece zero bytes" operator (kSpanTabGap).  After the last window lane t
+// holds the CRC of its bytes followed by zeros up to the end of its last piece, and a
+// log2(kSpanLanes)-level tree merges neighbours with "shift by 2^j pieces" operators.  kSpanPiece is
+// 60 bytes (15 dwords): an odd dword count puts the 32 lanes of a ds_read_b32 group on 32 different
+// LDS banks.  Host mirror: crc32c_span_emulate (csrc/core/crc32c.cpp).
+constexpr uint32_t kSpanPiece = 60;
 constexpr uint32_t kSpanLanes = 256;
+constexpr uint32_t kSpanWin = kSpanPiece * kSpanLanes;  // 15,360 bytes
 constexpr uint32_t kSpanLevels = 8;
-static_assert(kSpanLaneLarge * kSpanLanes >= kSpanSegMax, "lanes must cover a whole segment");
-inline constexpr uint32_t span_lane_bytes(uint32_t crc_len) {
-  return crc_len <= kSpanLaneSmall * kSpanLanes ? kSpanLaneSmall : kSpanLaneLarge;
-}
+constexpr uint32_t kSpanMaxWins = (kSpanSegMax + kSpanWin - 1) / kSpanWin;
+static_assert(kSpanMaxWins <= 16, "window tables hold 16 entries");
+// Windows of a segment of `len` bytes (>= 1).
+inline constexpr uint32_t span_windows(uint32_t len) { return len == 0 ? 1u : (len + kSpanWin - 1) / kSpanWin; }
 
-// A segment decoded by `parts` workgroups (span_decode.hip step 0; parts = 1, 2 or 4).  Part j runs
-// CRC lanes [j n, (j+1) n) (n = kSpanLanes / parts) of the whole segment's lane layout, owns the
-// bytes those lanes cover (the first part also the bytes before the CRC range, the last part up to
-// the end) -- a value's 16-byte group belongs to the part owning its first byte in the segment --
-// and stages its bytes with 16 before and 32 after (a group starting at the end of its range, and
-// the lanes' dword reads).  Offsets from the segment's first byte, `len` its length, `crc_first`:
-// the segment holds its RecordBatch's start (CRC from byte 21).  Tested by
-// tests/native/span_split_test.cpp.
-struct SpanPart {
-  int32_t own_lo, own_hi;      // the bytes this part checks and decodes
-  int32_t stage_lo, stage_hi;  // the bytes it stages
+// Window geometry of one segment (span_device.h), in the kernels' image coordinates: segment byte
+// i is image byte 16 + (address & 15) + i, so image byte 16 is the segment's first byte rounded
+// down to 16 bytes and [lo, hi) are its bytes.  Window k owns [own_lo(k), own_hi(k)) -- a partition
+// of [lo, hi): a value group, a text piece or a CRC byte belongs to the window owning its first
+// byte -- and stages [stage_lo(k), stage_hi(k)), 16-byte aligned, from 16 bytes before its bytes to
+// 48 after them (a 16-byte group starting in the window is whole in LDS).  Tested on the host by
+// tests/native/span_window_test.cpp.
+struct SpanWindows {
+  int32_t lo, hi, w0;
+  int32_t nw;
+  constexpr SpanWindows(int32_t lo_b, int32_t hi_b)
+      : lo(lo_b), hi(hi_b), w0(hi_b - int32_t(span_windows(uint32_t(hi_b - lo_b)) * kSpanWin)),
+        nw(int32_t(span_windows(uint32_t(hi_b - lo_b)))) {}
+  constexpr int32_t own_lo(int32_t k) const { return k == 0 ? lo : w0 + k * int32_t(kSpanWin); }
+  constexpr int32_t own_hi(int32_t k) const { return k == nw - 1 ? hi : w0 + (k + 1) * int32_t(kSpanWin); }
+  constexpr int32_t stage_lo(int32_t k) const {
+    const int32_t a = (own_lo(k) - 16) & ~15;
+    return a > 16 ? a : 16;
+  }
+  constexpr int32_t stage_hi(int32_t k) const {
+    const int32_t e = (hi + 15) & ~15, b = (own_hi(k) + 48 + 15) & ~15;
+    return e < b ? e : b;
+  }
+  // the window owning image byte x (clamped into the segment's windows)
+  constexpr int32_t win_of(int32_t x) const {
+    const int32_t k = (x - w0) / int32_t(kSpanWin);
+    return k < 0 ? 0 : k >= nw ? nw - 1 : k;
+  }
 };
-inline constexpr int32_t span_part_cut(uint32_t len, bool crc_first, int parts, int q) {
-  const int32_t n = int32_t(len), c0 = crc_first ? 21 : 0;
-  const int32_t L = int32_t(span_lane_bytes(uint32_t(n - c0)));
-  const int32_t x = n - (int32_t(kSpanLanes) - q * (int32_t(kSpanLanes) / parts)) * L;
-  return x < 0 ? 0 : x;
-}
-inline constexpr SpanPart span_part(uint32_t len, bool crc_first, int parts, int part) {
-  const int32_t n = int32_t(len);
-  if (parts <= 1) return SpanPart{0, n, 0, n};
-  const int32_t lo = part > 0 ? span_part_cut(len, crc_first, parts, part) : 0;
-  const int32_t hi = part < parts - 1 ? span_part_cut(len, crc_first, parts, part + 1) : n;
-  return SpanPart{lo, hi, lo - 16 > 0 ? lo - 16 : 0, hi + 32 < n ? hi + 32 : n};
-}
-// Device table layout (uint32 words): slice-by-8 byte tables T0..T7, then for each lane size
-// (small, large), level j and byte k of the value: shift-by-(L << j)-bytes of (b << 8k), then the
-// nibble split of T0..T7 the kernels keep in LDS: row 2k + h holds T_k[n << 4h] for n < 16.  A
-// byte table is linear over GF(2), so T_k[b] = row(2k)[b & 15] ^ row(2k + 1)[b >> 4]; a 16-entry
-// row spans 16 LDS banks, so a ds_read_b32 of one row by any 32 lanes is conflict-free (distinct
-// nibbles hit distinct banks, equal ones broadcast), where a data-dependent 256-entry lookup put
-// ~3 lanes on a bank.
+// LDS bytes of one window buffer: 16 before the staged bytes (reads start at most 10 below them),
+// at most kSpanWin + 96 staged, 32 after (a 16-byte read of the slot past the last one).
+constexpr int32_t kSpanWinPad = 16;
+constexpr int32_t kSpanWinBytes = kSpanWinPad + int32_t(kSpanWin) + 96 + 32;
+
+// Device table layout (uint32 words): slice-by-8 byte tables T0..T7; for level j and byte k of the
+// value, shift-by-(kSpanPiece << j)-bytes of (b << 8k); the nibble split of T0..T7 the kernels keep
+// in LDS: row 2k + h holds T_k[n << 4h] for n < 16 (a byte table is linear over GF(2), so
+// T_k[b] = row(2k)[b & 15] ^ row(2k + 1)[b >> 4]; a 16-entry row spans 16 LDS banks, so a
+// ds_read_b32 of one row by any 32 lanes is conflict-free); and the window gap operator, nibble
+// split too: row i holds shift-by-(kSpanWin - kSpanPiece)-bytes of (n << 4i).
 constexpr uint32_t kSpanTabSlice = 0;
 constexpr uint32_t kSpanTabShift = 8 * 256;
 constexpr uint32_t kSpanTabShiftSet = kSpanLevels * 4 * 256;
-constexpr uint32_t kSpanTabNib = kSpanTabShift + 2 * kSpanTabShiftSet;
+constexpr uint32_t kSpanTabNib = kSpanTabShift + kSpanTabShiftSet;
 constexpr uint32_t kSpanTabNibWords = 16 * 16;
-constexpr uint32_t kSpanTabWords = kSpanTabNib + kSpanTabNibWords;
+constexpr uint32_t kSpanTabGap = kSpanTabNib + kSpanTabNibWords;
+constexpr uint32_t kSpanTabGapWords = 8 * 16;
+constexpr uint32_t kSpanTabWords = kSpanTabGap + kSpanTabGapWords;
 
 enum SpanSegFlags : uint32_t {
   kSegCrcFirst = 1,   // the segment holds the first CRC'd byte of its RecordBatch (offset 21)

@@ -28,7 +28,7 @@ void host_mapped(size_t n, T** host, T** dev, const char* what) {
 }  // namespace
 
 BatchVerdicts::~BatchVerdicts() {
-  if (perr_host_ || part_host_) hipDeviceSynchronize();  // no kernel may still write a status word
+  // no kernel still writes a status word: the driver waited for every handed slot (quiesce)
   if (perr_host_) hipHostFree(perr_host_);
   if (jinfo_host_) hipHostFree(jinfo_host_);
   if (patch_dev_) hipFree(patch_dev_);
@@ -141,6 +141,7 @@ int64_t BatchVerdicts::json_width(int64_t w, int64_t* n_host) {
       tk::cpu_relax();
       continue;
     }
+    q_->check();  // a failed queue never ran the parse: report its failure, not a timeout
     if (tk::now_ns() - t0 > 60'000'000'000LL)
       throw std::runtime_error("driver: the JSON parse kernel did not report a batch width within 60 s");
     timespec ts{0, 20000};
@@ -190,7 +191,7 @@ void BatchVerdicts::parse_host_rows(int64_t g, int64_t w) {
 void BatchVerdicts::json_host_rows(int64_t g, int64_t w, int32_t trunc_len, void* out, int64_t L, int dst_dt,
                                    double pad, int64_t* lengths, uint8_t* mask, hipStream_t stream) {
   if (w < 0) return;
-  HipQueue::get().drain();  // the copies below go on `stream` after its queued parse kernel
+  q_->drain();  // the copies below go on `stream` after its queued parse kernel
   if (!jparsed_[size_t(w)]) parse_host_rows(g, w);  // the slot is still held
   const int dsz = dtype_size(dst_dt);
   constexpr size_t kVals = 256;  // the values start 256 bytes after the row descriptor

@@ -24,7 +24,8 @@ class BatchVerdicts {
   static constexpr int64_t kWords = 4096;
   static constexpr int64_t kPartials = 512;  // raw CRC words per status word (segments of one slot)
 
-  BatchVerdicts(tk::Ring* ring, tk::Broker* broker) : ring_(ring), broker_(broker) {}
+  // `queue`: the loader's HIP command queue (its parse launches are queued there)
+  BatchVerdicts(tk::Ring* ring, tk::Broker* broker, HipQueue* queue) : ring_(ring), broker_(broker), q_(queue) {}
   ~BatchVerdicts();
   BatchVerdicts(const BatchVerdicts&) = delete;
   BatchVerdicts& operator=(const BatchVerdicts&) = delete;
@@ -85,6 +86,7 @@ class BatchVerdicts {
   uint8_t* patch_dev_ = nullptr;  // one host-parsed row at a time
   size_t patch_cap_ = 0;
   uint64_t seq_ = 0;
+  HipQueue* q_ = nullptr;  // the loader's command queue
 };
 
 }  // namespace tkh

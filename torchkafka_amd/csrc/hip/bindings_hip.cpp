@@ -344,8 +344,6 @@ PYBIND11_MODULE(_tkhip, m) {
              s["verify_wait_ns"] = d.verify_wait_ns_;
              return s;
            })
-      .def_property_readonly("span_split", &MainDriver::span_split)
-      .def_property_readonly("mirror_split", &MainDriver::mirror_split)
       .def("reset_stats", &MainDriver::reset_stats)
       .def("set_event_every", &MainDriver::set_event_every, py::arg("n"))
       .def_property_readonly("event_every", &MainDriver::event_every)
@@ -357,7 +355,6 @@ PYBIND11_MODULE(_tkhip, m) {
       .def_property_readonly("mirror_copy_streams",
                              [](MainDriver& d) { return d.mirror_copy_streams(); })
       .def("set_ahead_depth", &MainDriver::set_ahead_depth)
-      .def("set_span_burst", &MainDriver::set_span_burst)
       .def("set_group_bytes", &MainDriver::set_group_bytes)
       .def("set_worker_sink", &MainDriver::set_worker_sink, py::arg("table"), py::arg("n_workers"),
            py::arg("capacity"))

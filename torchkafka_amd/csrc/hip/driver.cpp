@@ -45,21 +45,17 @@ MainDriver::MainDriver(Engine* engine, const std::string& ring_name, const std::
   }
   ledger_ = std::make_unique<CommitLedger>(broker_, gidx);
   pins_ = std::make_unique<LogPins>(eng_, broker_);
-  verdicts_ = std::make_unique<BatchVerdicts>(ring.get(), broker_.get());
+  verdicts_ = std::make_unique<BatchVerdicts>(ring.get(), broker_.get(), &eng_->queue());
   poller_ = std::make_unique<RingPoller>(std::move(ring), eng_, pins_.get(), ledger_.get(), broker_.get(), in_order,
                                          default_src_dt);
 }
 
 MainDriver::~MainDriver() {
-  try {
-    HipQueue::get().drain();  // queued launches read the slots, logs and staging freed below
-  } catch (...) {
-  }
-  pins_.reset();  // pinned log ranges first: the kernels that read them completed (slots drained by the caller)
-  if (stage_dev_) {
-    hipDeviceSynchronize();
-    hipFree(stage_dev_);
-  }
+  // Quiesce this loader only -- never the device: the user's stream may hold a training step's
+  // work for milliseconds, and a device-wide synchronize here would block the host on it.
+  quiesce();
+  pins_.reset();  // pinned log ranges: every kernel that read them completed (quiesce)
+  if (stage_dev_) hipFree(stage_dev_);
   if (registered_) {
     try {
       eng_->unregister_host();  // before the ring's mapping goes away (poller_)
@@ -68,8 +64,28 @@ MainDriver::~MainDriver() {
   }
   for (auto& f : fenced_)
     if (std::get<0>(f)) hipEventDestroy(std::get<0>(f));
-  verdicts_.reset();  // waits for any kernel that may still write a status word
+  verdicts_.reset();  // no kernel still writes a status word (quiesce)
   for (auto e : event_pool_) hipEventDestroy(e);
+}
+
+void MainDriver::quiesce() noexcept {
+  try {
+    eng_->queue().drain();  // queued launches read the slots, logs and staging freed by the caller
+  } catch (...) {
+  }
+  // every slot handed out: its completion event follows its kernel, on whichever stream (a decode
+  // stream, or the user's for the host-decode collates) -- not the user's later work
+  for (const Handed& h : handed_) {
+    if (!h.ev) continue;
+    try {
+      eng_->wait_slot(int(h.g));
+    } catch (...) {
+    }
+  }
+  try {
+    eng_->synchronize();  // the decode and copy streams (ahead groups nobody was handed yet)
+  } catch (...) {
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -448,8 +464,6 @@ void MainDriver::launch_span(const int* slots, const SlotView* const* views, int
   a.vec_store = vec ? 1 : 0;
   bool pcie = false;  // a segment of this launch is read over PCIe (not from the HBM mirror)
   auto flush = [&](bool record) {
-    a.burst = pcie ? span_burst_ : mirror_burst_;  // loads a wave keeps in flight (span_decode.hip stage 1)
-    a.split = pcie ? span_split_ : mirror_split_;
     pcie = false;
     if (mirror) mirror->before(stream);
     eng_->collate_span(slots, n, stream, a, v0.src_dtype, dst_dt, shift, scale, record);
@@ -567,7 +581,6 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
     off += batch_bytes[k];
   }
   auto flush = [&]() {
-    a.burst = pcie ? span_burst_ : mirror_burst_;
     pcie = false;
     if (mirror) mirror->before(stream);
     eng_->collate_json_stage(slots, n, stream, a);
@@ -632,7 +645,6 @@ void MainDriver::launch_var_span(const int* slots, const SlotView* const* views,
       a.b[k].rows = reinterpret_cast<const tk::JsonSpanRow*>(a.b[k].slot);
     }
     a.tabs = eng_->span_tables();
-    a.burst = pcie ? span_burst_ : mirror_burst_;
     pcie = false;
     if (mirror) mirror->before(stream);
     eng_->run_on(stream, [a, src_dt, dst_dt, pad, stream] { tkh::launch_var_span(a, src_dt, dst_dt, pad, stream); });

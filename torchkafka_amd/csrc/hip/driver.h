@@ -155,12 +155,6 @@ class MainDriver {
   }
   hipStream_t last_stream() const { return last_stream_; }
   int64_t last_perr() const { return last_perr_; }
-  // LDS-DMA loads a wave of the span decode kernel keeps in flight before it waits (0 = all;
-  // default 1; TORCHKAFKA_SPAN_BURST)
-  void set_span_burst(int n) { span_burst_ = n < 0 ? 0 : n > 8 ? 8 : n; }
-  // Workgroups per segment of the fixed-width decode kernel over PCIe / from the HBM mirror
-  int span_split() const { return span_split_; }
-  int mirror_split() const { return mirror_split_; }
   // The stream the next device-decode group launch runs on (its outputs are allocated there).
   hipStream_t next_decode_stream() { return eng_->decode_stream(int(span_launches_ % 4096)); }
   void set_coalesce(int n) { coalesce_ = n < 1 ? 1 : (n > kMaxGroup ? kMaxGroup : n); }
@@ -303,6 +297,9 @@ class MainDriver {
   };
   void release_completed();
   void release_completed_impl();
+  // Teardown: waits for this loader's own work (queued calls, handed slots' events, its decode and
+  // copy streams) -- never the device.
+  void quiesce() noexcept;
   static constexpr int64_t kReleaseRequeryNs = 3000;
   int64_t pending_query_ns_ = 0;  // when an event was last found pending (release_completed)
   int64_t busy_query_ns_ = 0;     // when gpu_busy() last found the latest launch running
@@ -371,28 +368,6 @@ class MainDriver {
   static void fill_seg(SpanDevSeg& d, const tk::SpanSeg& sg, const uint8_t* src, int k, uint32_t i);
   int ext_n_ = 0;  // set_extra_outputs(): destinations of the next launch
   int64_t* ext_dsts_[kMaxGroup] = {};
-  int span_burst_ = [] {
-    const char* e = std::getenv("TORCHKAFKA_SPAN_BURST");
-    const int v = e ? std::atoi(e) : 1;
-    return v < 0 ? 0 : v > 8 ? 8 : v;
-  }();
-  // Workgroups per segment of the fixed-width decode kernel (1, 2 or 4; span_decode.hip step 0),
-  // for launches read over PCIe and from the HBM mirror; TORCHKAFKA_SPAN_SPLIT / _MIRROR_SPLIT
-  static int split_env(const char* name, int dflt) {
-    const char* e = std::getenv(name);
-    const int v = e ? std::atoi(e) : dflt;
-    return v >= 4 ? 4 : v >= 2 ? 2 : 1;
-  }
-  int span_split_ = split_env("TORCHKAFKA_SPAN_SPLIT", 1);
-  int mirror_split_ = split_env("TORCHKAFKA_MIRROR_SPLIT", 1);
-  // ... for a launch whose segments all come from the HBM mirror: HBM takes every load of a wave at
-  // once (0), where PCIe reads lose bandwidth with many in flight (mirror decode: 34.1 us per group
-  // at 1, 27.8 us at 0, 29.9 us at 4; profiles/r03_s3/burst/); TORCHKAFKA_MIRROR_BURST
-  int mirror_burst_ = [] {
-    const char* e = std::getenv("TORCHKAFKA_MIRROR_BURST");
-    const int v = e ? std::atoi(e) : 0;
-    return v < 0 ? 0 : v > 8 ? 8 : v;
-  }();
   // the segment source of a decode launch; *pcie is set when it is not the HBM mirror
   const uint8_t* seg_src(const tk::SpanSeg& sg, bool* pcie) {
     bool hbm = false;

@@ -4,7 +4,10 @@
 #include <cstddef>
 #include <cstdint>
 #include <functional>
+#include <memory>
 #include <vector>
+
+#include "hip_queue.h"
 
 namespace tkh {
 
@@ -86,9 +89,6 @@ class Engine {
   }
   // Device copy of the CRC tables of the span kernel (uploaded on first use).
   const uint32_t* span_tables();
-  // The part-CRC words of span decode launches split over workgroups on `stream` (a decode stream:
-  // its launches run in order, and each leaves the words zeroed); nullptr for any other stream.
-  uint32_t* part_crc(hipStream_t stream);
   // The streams device-decode groups rotate over (created on first use; kDecodeStreams).
   hipStream_t decode_stream(int k);
   int decode_streams() const { return n_decode_; }
@@ -111,6 +111,8 @@ class Engine {
   // Whether this engine's decode-stream calls use the command queue (set per loader: var-len and
   // JSON device decode; fixed-width decode keeps its calls on the stepping thread).
   void set_command_queue(bool on);
+  // This engine's (this loader's) HIP command queue (hip_queue.h).
+  HipQueue& queue() { return *q_; }
   void copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes);
   // The same without the slot's completion event: a kernel queued after it on `user` records it.
   void copy_bytes(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes);
@@ -136,15 +138,22 @@ class Engine {
   std::vector<hipEvent_t> done_, copied_;
   std::vector<uint64_t> done_seq_;  // command-queue number of each done_ record (0: recorded directly)
   bool cq_ = false;                 // set_command_queue
+  std::unique_ptr<HipQueue> q_;     // made with the engine; its thread starts at the first queued call
   std::vector<const uint8_t*> host_src_;  // per slot: host payload pointer given at h2d()
   void* host_ptr_ = nullptr;
   uint8_t* host_dev_ = nullptr;           // device view of the registered host region (zero-copy)
   size_t host_len_ = 0;
   uint32_t* span_tabs_ = nullptr;
   hipStream_t decode_streams_[4] = {nullptr, nullptr, nullptr, nullptr};
-  uint32_t* part_crc_ = nullptr;  // [4 decode streams][kMaxLaunchSegs][kPartCrcWords]
   int n_decode_ = default_decode_streams();
   static int default_decode_streams();
+
+ public:
+  // 1: decode streams at the device's greatest stream priority, 0: HIP's default, -1: the least
+  static int decode_priority();
+  static constexpr int kDefaultDecodePriority = 0;
+
+ private:
   std::vector<hipEvent_t> order_events_;  // stream_after: a small pool used round-robin
   size_t order_next_ = 0;
 };

@@ -39,7 +39,7 @@ namespace tkh {
   } while (0)
 
 Engine::Engine(int device, int n_slots, size_t staging_bytes, int n_streams, int mode)
-    : device_(device), n_slots_(n_slots), mode_(mode) {
+    : device_(device), n_slots_(n_slots), mode_(mode), q_(std::make_unique<HipQueue>(device)) {
   if (n_slots <= 0) throw std::invalid_argument("engine: n_slots must be positive");
   if (mode != kH2DDma && mode != kH2DZeroCopy) throw std::invalid_argument("engine: bad h2d mode");
   if (n_streams < 1) n_streams = 1;
@@ -63,7 +63,7 @@ Engine::Engine(int device, int n_slots, size_t staging_bytes, int n_streams, int
 
 Engine::~Engine() {
   try {
-    HipQueue::get().drain();  // queued calls use the streams and events below
+    queue().drain();  // queued calls use the streams and events below
   } catch (...) {
   }
   hipSetDevice(device_);
@@ -73,7 +73,6 @@ Engine::~Engine() {
   for (auto e : copied_) hipEventDestroy(e);
   if (staging_) hipFree(staging_);
   if (span_tabs_) hipFree(span_tabs_);
-  if (part_crc_) hipFree(part_crc_);
   for (auto st : decode_streams_)
     if (st) {
       hipStreamSynchronize(st);
@@ -131,8 +130,8 @@ const uint8_t* Engine::src_base(int s) const {
 }
 
 void Engine::set_command_queue(bool on) {
-  if (!on && cq_) HipQueue::get().drain();  // calls queued so far stay ahead of the direct ones
-  cq_ = on && HipQueue::get().on();
+  if (!on && cq_) queue().drain();  // calls queued so far stay ahead of the direct ones
+  cq_ = on && queue().on();
 }
 
 bool Engine::queued(hipStream_t stream) const {
@@ -144,14 +143,14 @@ bool Engine::queued(hipStream_t stream) const {
 
 void Engine::run_on(hipStream_t stream, std::function<void()>&& f) {
   if (queued(stream))
-    HipQueue::get().submit(std::move(f));
+    queue().submit(std::move(f));
   else
     f();
 }
 
 bool Engine::slot_done(int s) {
   check_slot(s);
-  if (!HipQueue::get().ran(done_seq_[size_t(s)])) return false;  // its record has not even run yet
+  if (!queue().ran(done_seq_[size_t(s)])) return false;  // its record has not even run yet
   hipError_t e = hipEventQuery(done_[size_t(s)]);
   if (e == hipSuccess) return true;
   if (e == hipErrorNotReady) return false;
@@ -160,7 +159,7 @@ bool Engine::slot_done(int s) {
 
 void Engine::wait_slot(int s) {
   check_slot(s);
-  HipQueue::get().wait(done_seq_[size_t(s)]);
+  queue().wait(done_seq_[size_t(s)]);
   TKH_CHECK(hipEventSynchronize(done_[size_t(s)]));
 }
 
@@ -176,7 +175,7 @@ void Engine::begin(int s, hipStream_t user) {
 void Engine::finish(int s, hipStream_t user) {
   hipEvent_t e = done_[size_t(s)];
   if (queued(user)) {
-    done_seq_[size_t(s)] = HipQueue::get().submit([e, user] { TKH_CHECK(hipEventRecord(e, user)); });
+    done_seq_[size_t(s)] = queue().submit([e, user] { TKH_CHECK(hipEventRecord(e, user)); });
   } else {
     TKH_CHECK(hipEventRecord(e, user));
     done_seq_[size_t(s)] = 0;
@@ -185,7 +184,7 @@ void Engine::finish(int s, hipStream_t user) {
 
 void Engine::collate_fixed(int s, hipStream_t user, size_t values_offset, int src_dt, void* dst, int dst_dt,
                            int64_t rows, int64_t row, const float* shift, const float* scale, bool record) {
-  if (queued(user)) HipQueue::get().drain();  // a direct launch on a queued stream: after the queue
+  if (queued(user)) queue().drain();  // a direct launch on a queued stream: after the queue
   check_slot(s);
   begin(s, user);
   launch_fixed(src_base(s) + values_offset, src_dt, dst, dst_dt, rows, row, shift, scale, user);
@@ -195,7 +194,7 @@ void Engine::collate_fixed(int s, hipStream_t user, size_t values_offset, int sr
 void Engine::collate_fixed_group(const int* slots, int n, hipStream_t user, const size_t* values_offsets, int src_dt,
                                  void* const* dsts, int dst_dt, const int64_t* rows, int64_t row, const float* shift,
                                  const float* scale) {
-  if (queued(user)) HipQueue::get().drain();  // a direct launch on a queued stream: after the queue
+  if (queued(user)) queue().drain();  // a direct launch on a queued stream: after the queue
   if (n < 1 || n > kMaxGroup) throw std::invalid_argument("engine: bad group size");
   const void* srcs[kMaxGroup];
   for (int k = 0; k < n; ++k) {
@@ -210,7 +209,7 @@ void Engine::collate_fixed_group(const int* slots, int n, hipStream_t user, cons
 void Engine::collate_gather_group(const int* slots, int n, hipStream_t user, int src_dt, void* const* dsts, int dst_dt,
                                   const int64_t* rows, int64_t row_bytes, const uint64_t* bases, const float* shift,
                                   const float* scale, bool record) {
-  if (queued(user)) HipQueue::get().drain();  // a direct launch on a queued stream: after the queue
+  if (queued(user)) queue().drain();  // a direct launch on a queued stream: after the queue
   if (n < 1 || n > kMaxGroup) throw std::invalid_argument("engine: bad group size");
   const uint64_t* ents[kMaxGroup];
   for (int k = 0; k < n; ++k) {
@@ -226,16 +225,16 @@ void Engine::stream_wait_done(int s, hipStream_t user) {
   check_slot(s);
   hipEvent_t e = done_[size_t(s)];
   if (queued(user)) {
-    HipQueue::get().submit([e, user] { TKH_CHECK(hipStreamWaitEvent(user, e, 0)); });
+    queue().submit([e, user] { TKH_CHECK(hipStreamWaitEvent(user, e, 0)); });
   } else {
-    HipQueue::get().wait(done_seq_[size_t(s)]);  // the record the wait refers to has run
+    queue().wait(done_seq_[size_t(s)]);  // the record the wait refers to has run
     TKH_CHECK(hipStreamWaitEvent(user, e, 0));
   }
 }
 
 void Engine::collate_varlen(int s, hipStream_t user, size_t values_offset, int src_dt, void* out, int dst_dt,
                             int64_t rows, int64_t L, double pad, int64_t* lengths, uint8_t* mask, bool record) {
-  if (queued(user)) HipQueue::get().drain();  // a direct launch on a queued stream: after the queue
+  if (queued(user)) queue().drain();  // a direct launch on a queued stream: after the queue
   check_slot(s);
   const uint8_t* base = src_base(s);
   begin(s, user);
@@ -246,7 +245,7 @@ void Engine::collate_varlen(int s, hipStream_t user, size_t values_offset, int s
 
 void Engine::collate_json(int s, hipStream_t user, size_t values_offset, void* out, int dst_dt, int64_t rows,
                           int64_t L, double pad, int64_t* lengths, uint8_t* mask, int32_t* err, bool record) {
-  if (queued(user)) HipQueue::get().drain();  // a direct launch on a queued stream: after the queue
+  if (queued(user)) queue().drain();  // a direct launch on a queued stream: after the queue
   check_slot(s);
   const uint8_t* base = src_base(s);
   begin(s, user);
@@ -258,7 +257,7 @@ void Engine::collate_json(int s, hipStream_t user, size_t values_offset, void* o
 void Engine::collate_json_group(const int* slots, int n, hipStream_t user, const size_t* values_offsets,
                                 const int64_t* rows, void* const* outs, const int64_t* Ls, int64_t* const* lengths,
                                 uint8_t* const* masks, int32_t* const* errs, double pad, int dst_dt) {
-  if (queued(user)) HipQueue::get().drain();  // a direct launch on a queued stream: after the queue
+  if (queued(user)) queue().drain();  // a direct launch on a queued stream: after the queue
   if (n < 1 || n > kMaxGroup) throw std::invalid_argument("engine: bad group size");
   JsonGroupArgs a{};
   a.n = n;
@@ -292,21 +291,6 @@ const uint32_t* Engine::span_tables() {
   return span_tabs_;
 }
 
-uint32_t* Engine::part_crc(hipStream_t stream) {
-  int k = -1;
-  for (int i = 0; i < 4; ++i)
-    if (decode_streams_[i] && decode_streams_[i] == stream) k = i;
-  if (k < 0) return nullptr;
-  constexpr size_t per = size_t(kMaxLaunchSegs) * kPartCrcWords;
-  if (!part_crc_) {
-    TKH_CHECK(hipSetDevice(device_));
-    TKH_CHECK(hipMalloc(reinterpret_cast<void**>(&part_crc_), 4 * per * sizeof(uint32_t)));
-    TKH_CHECK(hipMemset(part_crc_, 0, 4 * per * sizeof(uint32_t)));
-    TKH_CHECK(hipDeviceSynchronize());  // zeroed before any launch reads it
-  }
-  return part_crc_ + size_t(k) * per;
-}
-
 int Engine::default_decode_streams() {
   // three decode streams + the user's stream fill the 4 hardware queues HIP gives a process by
   // default (config 2: 2 streams 52.9 M rec/s, 3 streams 54.0 M, 4 streams 45.0 M -- the fourth
@@ -325,7 +309,7 @@ void Engine::set_decode_streams(int n) {
 __global__ void decode_warm_kernel() {}
 
 void Engine::prepare_decode() {
-  HipQueue::get().drain();
+  queue().drain();
   span_tables();
   for (int k = 0; k < decode_streams(); ++k) {
     hipStream_t st = decode_stream(k);
@@ -341,14 +325,31 @@ hipStream_t Engine::decode_stream(int k) {
   hipStream_t& st = decode_streams_[k % decode_streams()];
   if (!st) {
     TKH_CHECK(hipSetDevice(device_));
-    TKH_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    const int prio = decode_priority();
+    if (prio == 0) {
+      TKH_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    } else {
+      int least = 0, greatest = 0;
+      TKH_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      TKH_CHECK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio > 0 ? greatest : least));
+    }
   }
   return st;
 }
 
+int Engine::decode_priority() {
+  // the HSA queue priority of the decode streams: "high" lets the dispatcher hand freed CUs to the
+  // decode workgroups before a co-running training job's next tiles (benchmarks/compute_overlap.py);
+  // "normal" is HIP's default, "low" the opposite.  TORCHKAFKA_DECODE_PRIORITY overrides.
+  const char* e = std::getenv("TORCHKAFKA_DECODE_PRIORITY");
+  if (!e) return kDefaultDecodePriority;
+  const std::string v(e);
+  return v == "high" ? 1 : v == "low" ? -1 : 0;
+}
+
 void Engine::stream_after(hipStream_t later, hipStream_t earlier) {
   if (later == earlier) return;
-  if (queued(later) || queued(earlier)) HipQueue::get().drain();  // rare: keep both in order
+  if (queued(later) || queued(earlier)) queue().drain();  // rare: keep both in order
   if (order_events_.empty()) {
     order_events_.resize(16);
     for (auto& e : order_events_) TKH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -369,10 +370,8 @@ void Engine::collate_span(const int* slots, int n, hipStream_t user, SpanLaunch&
     if (a.b[k].ext_words) a.b[k].ext_src = reinterpret_cast<const int64_t*>(src_base(slots[k]) + a.b[k].ext_off);
   }
   a.tabs = span_tables();
-  if (a.split < 1) a.split = 1;
-  if (a.split > 1 && !(a.part_crc = part_crc(user))) a.split = 1;  // not a decode stream: one workgroup
   if (queued(user)) {
-    HipQueue::get().submit([a, src_dt, dst_dt, shift, scale, user] {
+    queue().submit([a, src_dt, dst_dt, shift, scale, user] {
       launch_span_decode(a, src_dt, dst_dt, shift, scale, user);
     });
   } else {
@@ -391,20 +390,20 @@ void Engine::collate_json_stage(const int* slots, int n, hipStream_t user, JsonS
   }
   a.tabs = span_tables();
   if (queued(user))
-    HipQueue::get().submit([a, user] { launch_json_stage(a, user); });
+    queue().submit([a, user] { launch_json_stage(a, user); });
   else
     launch_json_stage(a, user);
 }
 
 void Engine::copy_bytes(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes) {
-  if (queued(user)) HipQueue::get().drain();  // a direct launch on a queued stream: after the queue
+  if (queued(user)) queue().drain();  // a direct launch on a queued stream: after the queue
   check_slot(s);
   begin(s, user);
   if (nbytes) TKH_CHECK(hipMemcpyAsync(dst, src_base(s) + offset, nbytes, hipMemcpyDefault, user));
 }
 
 void Engine::copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t nbytes) {
-  if (queued(user)) HipQueue::get().drain();  // a direct launch on a queued stream: after the queue
+  if (queued(user)) queue().drain();  // a direct launch on a queued stream: after the queue
   check_slot(s);
   begin(s, user);
   if (nbytes) TKH_CHECK(hipMemcpyAsync(dst, src_base(s) + offset, nbytes, hipMemcpyDefault, user));
@@ -412,7 +411,7 @@ void Engine::copy_raw(int s, hipStream_t user, size_t offset, void* dst, size_t 
 }
 
 void Engine::synchronize() {
-  HipQueue::get().drain();
+  queue().drain();
   for (auto st : streams_) TKH_CHECK(hipStreamSynchronize(st));
   for (auto st : decode_streams_)
     if (st) TKH_CHECK(hipStreamSynchronize(st));

@@ -2,7 +2,9 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <ctime>
 #include <stdexcept>
@@ -13,34 +15,72 @@
 
 namespace tkh {
 
-HipQueue& HipQueue::get() {
-  static HipQueue* q = new HipQueue();  // leaked on purpose: no teardown race with the HIP runtime
-  return *q;
+namespace {
+
+// Forks seen by this process image: a queue made before a fork belongs to the parent (its thread
+// did not survive into the child).  DataLoader workers are forked from the loader's process; they
+// make no HIP calls, so in a child every call runs inline and waits return at once (a guard).
+std::atomic<uint64_t> g_fork_gen{0};
+
+// Live queues, shut down at process exit before the HIP runtime tears down.
+std::mutex g_live_m;
+std::vector<HipQueue*>* g_live = nullptr;  // leaked on purpose: atexit may run after static teardown
+bool g_atexit = false;
+
+void register_live(HipQueue* q) {
+  std::lock_guard<std::mutex> g(g_live_m);
+  if (!g_live) g_live = new std::vector<HipQueue*>();
+  g_live->push_back(q);
+  if (!g_atexit) {
+    g_atexit = true;
+    std::atexit([] {
+      std::vector<HipQueue*> qs;
+      {
+        std::lock_guard<std::mutex> g(g_live_m);
+        if (g_live) qs = *g_live;
+      }
+      for (HipQueue* q : qs) q->shutdown();
+    });
+  }
 }
 
-HipQueue::HipQueue() {
-  const char* e = std::getenv("TORCHKAFKA_HIP_QUEUE");  // on unless "0"
-  on_ = !(e && e[0] == '0');
-  if (on_) ring_.resize(kCap);
-  // DataLoader workers are forked from the loader's process: the thread does not survive a fork,
-  // so in the child every call runs inline (the workers make no HIP calls; this is a guard)
-  pthread_atfork(nullptr, nullptr, [] {
-    HipQueue& q = get();
-    q.on_ = false;
-    q.child_ = true;
-  });
+void unregister_live(HipQueue* q) {
+  std::lock_guard<std::mutex> g(g_live_m);
+  if (g_live) g_live->erase(std::remove(g_live->begin(), g_live->end(), q), g_live->end());
 }
+
+}  // namespace
+
+bool HipQueue::enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("TORCHKAFKA_HIP_QUEUE");  // on unless "0"
+    pthread_atfork(nullptr, nullptr, [] { g_fork_gen.fetch_add(1, std::memory_order_relaxed); });
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+HipQueue::HipQueue(int device) : on_(enabled()), device_(device), fork_gen_(g_fork_gen.load()) {
+  if (on_) ring_.resize(kCap);
+}
+
+HipQueue::~HipQueue() {
+  if (started_ && !child()) {
+    shutdown();
+    unregister_live(this);
+  }
+}
+
+bool HipQueue::child() const { return g_fork_gen.load(std::memory_order_relaxed) != fork_gen_; }
 
 void HipQueue::start() {
-  if (hipGetDevice(&device_) != hipSuccess) device_ = 0;
   th_ = std::thread([this] { run(); });
-  th_.detach();
   started_ = true;
-  std::atexit([] { get().shutdown(); });
+  register_live(this);
 }
 
-void HipQueue::shutdown() {
-  if (child_ || !started_) return;
+void HipQueue::shutdown(int timeout_ms) {
+  if (child() || !started_ || !th_.joinable()) return;
   try {
     drain();
   } catch (...) {
@@ -50,11 +90,22 @@ void HipQueue::shutdown() {
     std::lock_guard<std::mutex> g(sleep_m_);
     wake_.notify_one();
   }
-  for (int i = 0; i < 100000 && !exited_.load(std::memory_order_acquire); ++i) std::this_thread::yield();
+  std::unique_lock<std::mutex> lk(exit_m_);
+  // system clock: pthread_cond_timedwait, which ThreadSanitizer follows (see run())
+  const bool stopped = exit_cv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms),
+                                           [this] { return exited_.load(std::memory_order_acquire); });
+  lk.unlock();
+  if (stopped) {
+    th_.join();
+  } else {
+    // still inside a HIP call: leave it running rather than hang the process
+    std::fprintf(stderr, "[torchkafka] HIP command queue thread did not stop within %d ms; detached\n", timeout_ms);
+    th_.detach();
+  }
 }
 
 uint64_t HipQueue::submit(std::function<void()>&& f) {
-  if (!on_) {
+  if (!on_ || child()) {
     f();
     return 0;
   }
@@ -92,7 +143,7 @@ void HipQueue::check() const {
 }
 
 void HipQueue::wait(uint64_t seq) {
-  if (seq == 0) return;
+  if (seq == 0 || child()) return;
   for (int i = 0; done_.load(std::memory_order_acquire) < seq; ++i) {
     check();
     if (i < 20000)
@@ -134,12 +185,16 @@ void HipQueue::run() {
     // against the system clock -- pthread_cond_timedwait, which ThreadSanitizer follows (the
     // steady-clock wait_for calls pthread_cond_clockwait, which GCC 11's TSan does not intercept:
     // it then reports the sleeping thread as still holding sleep_m_)
-    if (submitted_.load(std::memory_order_seq_cst) < next)
+    if (submitted_.load(std::memory_order_seq_cst) < next && !stop_.load(std::memory_order_acquire))
       wake_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(5));
     sleeping_.store(false, std::memory_order_release);
     idle = 0;
   }
-  exited_.store(true, std::memory_order_release);
+  {
+    std::lock_guard<std::mutex> g(exit_m_);
+    exited_.store(true, std::memory_order_release);
+  }
+  exit_cv_.notify_all();
 }
 
 }  // namespace tkh

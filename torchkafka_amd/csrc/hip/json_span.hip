@@ -6,10 +6,11 @@
 // each text in place (element count + "simple row" check); it neither copies the text nor CRCs
 // the batch.  Two kernels on one decode stream:
 //   json_stage_kernel, one 256-thread workgroup per log segment (<= 128 KiB, a row's text never
-//     cut): stage the segment in LDS by LDS-DMA and verify the RecordBatch CRC32C (span_device.h)
-//     -- PCIe-bound, like span_decode.hip -- then copy each row's text 16-byte aligned into the
-//     batch's HBM staging area (a block-wide scan of the rounded lengths places them) and write
-//     its JsonRowDesc;
+//     cut): a block-wide scan of the rounded text lengths places each row in the batch's HBM
+//     staging area and writes its JsonRowDesc, then the segment streams through two 15 KiB LDS
+//     windows (span_device.h: LDS-DMA staging of window k+1 behind the work on window k) -- each
+//     window verifies its share of the RecordBatch CRC32C and copies the 16-byte text pieces that
+//     start in it to their 16-byte aligned place;
 //   json_count_kernel (device counting, kSlotDevCount): a wave per row scans the staged text --
 //     json_scan_simple's rules -- and completes the row's descriptor and the batch's width word;
 //   json_parse.hip's json_rows_kernel over those descriptors: a 256-thread block per row, one
@@ -30,9 +31,9 @@ namespace tkh {
 
 namespace {
 
-using span::kBufBytes;
 using span::kFront;
 using span::kThreads;
+using span::kWinBytes;
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxRows = int(tk::kJsonSpanMaxSegRows);
 constexpr int kRowsPerThread = kMaxRows / kThreads;
@@ -122,20 +123,21 @@ __device__ int32_t scan_row(Load&& load, Byte&& byte, int32_t T, int lane, int32
 }
 
 __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[kBufBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t bufs[2][kWinBytes];
   __shared__ int32_t rel[kMaxRows];
   __shared__ int32_t tln[kMaxRows];
-  __shared__ int32_t cnt[kMaxRows];
   __shared__ uint32_t dst[kMaxRows];
   __shared__ __attribute__((aligned(256))) uint32_t tab[span::kNibLdsWords];
+  __shared__ span::RowWins rw;
   __shared__ uint32_t wcrc[kWaves];
   __shared__ uint32_t wsum[kWaves];
+  __shared__ int32_t bad;
 
   const int t = int(threadIdx.x), lane = t & 63, wv = t >> 6;
   const SpanDevSeg& sg = a.s[blockIdx.x];
   const JsonStageBatch& bo = a.b[sg.batch];
   const uint32_t row_begin = sg.row_begin;
-  const uint32_t nrows = sg.row_end - row_begin;
+  const int32_t nrows = int32_t(sg.row_end - row_begin);
   const uint32_t flags = sg.flags;
   const int32_t trunc = bo.trunc_len;
 
@@ -143,8 +145,8 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
     // rows the worker parsed (rare): one wave copies their float32 values, row after row
     if (wv != 0) return;
     uint32_t off = sg.stage_off;
-    for (uint32_t rr = 0; rr < nrows; ++rr) {
-      const int64_t row = int64_t(row_begin + rr);
+    for (int32_t rr = 0; rr < nrows; ++rr) {
+      const int64_t row = int64_t(row_begin) + rr;
       const tk::JsonSpanRow d = bo.rows[row];
       if (d.tlen >= 0) continue;
       const int32_t n_out = trunc >= 0 && d.count > trunc ? trunc : d.count;
@@ -163,86 +165,91 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
   const uint32_t len = sg.len;
   const int32_t head = int32_t(reinterpret_cast<uintptr_t>(sg.src) & 15u);
   const bool do_crc = (flags & tk::kSegCrc) != 0;
+  const int32_t lo_b = kFront + head, hi_b = lo_b + int32_t(len);
+  const span::Windows W(lo_b, hi_b);
 
-  // ---- 1. stage the segment; the row table and CRC tables load behind its first chunk
-  span::stage(sg.src, len, buf, a.burst, [&] {
-    const int64_t base = int64_t(sg.log_pos) - int64_t(head) - kFront;  // log position of LDS byte 0
-    for (uint32_t r = uint32_t(t); r < nrows; r += kThreads) {
-      const tk::JsonSpanRow d = bo.rows[row_begin + r];
-      rel[r] = d.tlen >= 0 ? int32_t(int64_t(d.pos) - base) : 0;
-      tln[r] = d.tlen;
-      cnt[r] = d.count;
-    }
-    if (do_crc)
-      span::load_nib_rows(tab, a.tabs);
-  });
-  __syncthreads();
-  const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
-  const uint4* b128 = reinterpret_cast<const uint4*>(buf);  // 16-byte slots (span::lds16)
-  const int32_t lo_b = kFront + head, hi_b = kFront + head + int32_t(len);
-
-  // ---- 2. CRC32C lanes (the verdict comes last)
-  const uint32_t* shift_set = nullptr;
-  if (do_crc) shift_set = span::crc_lanes(b32, tab, a.tabs, lo_b, hi_b, flags, wcrc);
-
-  // ---- 3. place the rows: exclusive scan of the 16-byte-rounded text lengths (thread t holds
-  // rows t * kRowsPerThread ..)
-  {
-    uint32_t sz[kRowsPerThread], local = 0;
+  const uint32_t crc = span::pipeline(
+      sg.src, W, bufs, tab, a.tabs, lo_b + ((flags & tk::kSegCrcFirst) ? 21 : 0), do_crc,
+      (flags & tk::kSegCrcFirst) != 0,
+      [&] {  // setup: the row table (image bytes, text lengths; -2: the row disagrees with the segment)
+        const int64_t base = int64_t(sg.log_pos) - int64_t(head) - kFront;  // log position of image byte 0
+        for (int32_t r = t; r < nrows; r += kThreads) {
+          const tk::JsonSpanRow d = bo.rows[row_begin + uint32_t(r)];
+          const int32_t r0 = d.tlen >= 0 ? int32_t(int64_t(d.pos) - base) : 0;
+          rel[r] = r0;
+          tln[r] = d.tlen < 0 ? -1 : (r0 < lo_b || r0 + d.tlen > hi_b) ? -2 : d.tlen;
+        }
+        span::row_wins_init(rw, W.nw);
+        if (t == 0) bad = 0;
+      },
+      [&] {  // prepare: place the rows (exclusive scan of the 16-byte-rounded text lengths, thread t
+             // holding rows t * kRowsPerThread ..), write their descriptors, find their windows
+        uint32_t sz[kRowsPerThread], local = 0;
 #pragma unroll
-    for (int i = 0; i < kRowsPerThread; ++i) {
-      const uint32_t r = uint32_t(t * kRowsPerThread + i);
-      sz[i] = r < nrows && tln[r] >= 0 ? align16(uint32_t(tln[r])) : 0u;
-      local += sz[i];
-    }
-    uint32_t incl = local;
+        for (int i = 0; i < kRowsPerThread; ++i) {
+          const int32_t r = t * kRowsPerThread + i;
+          sz[i] = r < nrows && tln[r] >= 0 ? align16(uint32_t(tln[r])) : 0u;
+          local += sz[i];
+        }
+        uint32_t incl = local;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += u;
-    }
-    if (lane == 63) wsum[wv] = incl;
-    __syncthreads();
-    uint32_t off = sg.stage_off + incl - local;
-    for (int w = 0; w < wv; ++w) off += wsum[w];
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t u = __shfl_up(incl, o, 64);
+          if (lane >= o) incl += u;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        uint32_t off = sg.stage_off + incl - local;
+        for (int w = 0; w < wv; ++w) off += wsum[w];
 #pragma unroll
-    for (int i = 0; i < kRowsPerThread; ++i) {
-      const uint32_t r = uint32_t(t * kRowsPerThread + i);
-      if (r < nrows) dst[r] = off;
-      off += sz[i];
-    }
-  }
-  __syncthreads();
+        for (int i = 0; i < kRowsPerThread; ++i) {
+          const int32_t r = t * kRowsPerThread + i;
+          if (r < nrows) {
+            dst[r] = off;
+            const int32_t T = tln[r];
+            if (T == -2) {  // the row table disagrees with the segment: read nothing, never commit
+              bo.desc[row_begin + uint32_t(r)] = JsonRowDesc{off, 0, 0, 0};
+              bad = 1;
+            } else if (T >= 0) {
+              // a device-counted row (count kJsonCountOnDevice) keeps that count here: json_count_kernel
+              // scans its staged text and completes the descriptor before json_rows_kernel reads it
+              const int32_t c = bo.rows[row_begin + uint32_t(r)].count;
+              const int32_t n_out = c < 0 ? 0 : trunc >= 0 && c > trunc ? trunc : c;
+              bo.desc[row_begin + uint32_t(r)] = JsonRowDesc{off, T, c, n_out};
+            }
+          }
+          off += sz[i];
+        }
+        for (int32_t r0w = 0; r0w < nrows; r0w += kThreads) {
+          const int32_t r = r0w + t;
+          const int32_t T = r < nrows ? tln[r] : -1;
+          const int32_t r0 = r < nrows ? rel[r] : 0;
+          span::row_wins_add(rw, W.nw, r0w + (t & ~63), T > 0, W.win_of(r0), W.win_of(r0 + ((T - 1) & ~15)));
+        }
+      },
+      [&](int k, const uint8_t* buf, int32_t off) {  // body: copy the 16-byte pieces window k owns
+        const int32_t ra = rw.lo[k], rb = rw.hi[k];
+        if (ra >= rb) return;
+        const int32_t own_lo = W.own_lo(k), own_hi = W.own_hi(k);
+        span::for_window_units(
+            ra, rb,
+            [&](int32_t rr, int32_t* ulo, int32_t* uhi) {
+              const int32_t T = tln[rr], r0 = rel[rr];
+              *ulo = span::unit_from(r0, own_lo);
+              *uhi = min(T > 0 ? (T + 15) >> 4 : 0, span::unit_from(r0, own_hi));
+            },
+            [&](int32_t rr, int32_t u) {
+              *reinterpret_cast<uint4*>(bo.stage + dst[rr] + 16u * uint32_t(u)) =
+                  span::lds16(reinterpret_cast<const uint4*>(buf), rel[rr] + 16 * u + off);
+            });
+      });
 
-  // ---- 4. copy: a wave per row, 16 bytes per lane (any LDS alignment: 5-dword window +
-  // v_alignbyte), aligned 16-byte stores into HBM; then the row's descriptor
-  bool off_seg = false;
-  for (uint32_t rr = uint32_t(wv); rr < nrows; rr += kWaves) {
-    const int32_t T = tln[rr];
-    if (T < 0) continue;  // parsed by the worker (its kSegHostRows block writes it)
-    const int32_t r0 = rel[rr];
-    if (r0 < lo_b || r0 + T > hi_b) {  // the row table disagrees with the segment: read nothing
-      off_seg = true;
-      if (lane == 0) bo.desc[row_begin + rr] = JsonRowDesc{dst[rr], 0, 0, 0};
-      continue;
-    }
-    uint8_t* __restrict__ o = bo.stage + dst[rr];
-    for (int32_t c = 16 * lane; c < T; c += 64 * 16) *reinterpret_cast<uint4*>(o + c) = span::lds16(b128, r0 + c);
-    if (lane == 0) {
-      // a device-counted row (count kJsonCountOnDevice) keeps that count here: json_count_kernel
-      // scans its staged text and completes the descriptor before json_rows_kernel reads it
-      const int32_t c = cnt[rr];
-      const int32_t n_out = c < 0 ? 0 : trunc >= 0 && c > trunc ? trunc : c;
-      bo.desc[row_begin + rr] = JsonRowDesc{dst[rr], T, c, n_out};
-    }
-  }
-  if (off_seg && lane == 0) *bo.err = int32_t(sg.seg);  // never committed (reported as this segment)
-
-  // ---- 5. CRC verdict
   if (do_crc) {
+    const uint32_t* shift_set = span::crc_merge(a.tabs, crc, wcrc);
     __syncthreads();
     if (t == 0) span::crc_verdict(shift_set, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials);
   }
+  if (t == 0 && bad) *bo.err = int32_t(sg.seg);  // never committed (reported as this segment)
 }
 
 // Device counting, between the stage and the parse: a wave per device-counted row (a block of four
@@ -303,7 +310,7 @@ void launch_json_stage(const JsonStageLaunch& a, hipStream_t stream) {
   if (a.n_seg < 0 || a.n_seg > kMaxLaunchSegs) throw std::invalid_argument("json stage: bad segment count");
   if (a.n_seg == 0) return;
   for (int i = 0; i < a.n_seg; ++i) {
-    // the kernel stages a segment whole in LDS and its row table next to it
+    // the kernel streams a segment of <= kSpanSegMax bytes and keeps its row table in LDS
     const SpanDevSeg& s = a.s[i];
     const bool host = (s.flags & tk::kSegHostRows) != 0;
     if ((!host && (s.len == 0 || s.len > tk::kSpanSegMax || s.src == nullptr)) || s.row_end < s.row_begin ||

@@ -16,8 +16,9 @@ namespace tkh {
     if (_e != hipSuccess) throw std::runtime_error(std::string("log mirror: ") + #expr + ": " + hipGetErrorString(_e)); \
   } while (0)
 
-LogMirror::LogMirror(int device, uint64_t chunk_bytes, int chunks_per_partition, int copy_streams)
-    : device_(device), chunk_(chunk_bytes), K_(chunks_per_partition) {
+LogMirror::LogMirror(int device, HipQueue* queue, uint64_t chunk_bytes, int chunks_per_partition, int copy_streams)
+    : device_(device), chunk_(chunk_bytes), K_(chunks_per_partition), q_(queue) {
+  if (!q_) throw std::invalid_argument("log mirror: no command queue");
   if (chunk_ < (uint64_t(1) << 20) || chunk_ % 4096 != 0) throw std::invalid_argument("log mirror: chunk must be >= 1 MiB, 4 KiB aligned");
   if (K_ < 2) throw std::invalid_argument("log mirror: at least 2 chunks per partition");
   prefetch_ = K_ > 3 ? K_ - 2 : 1;
@@ -41,13 +42,13 @@ LogMirror::LogMirror(int device, uint64_t chunk_bytes, int chunks_per_partition,
 
 LogMirror::~LogMirror() {
   try {
-    HipQueue::get().drain();  // queued copies and records use the streams and events below
+    q_->drain();  // queued copies and records use the streams and events below
   } catch (...) {
   }
   hipSetDevice(device_);
   for (auto& c : cs_)
     if (c.stream) hipStreamSynchronize(c.stream);
-  hipDeviceSynchronize();  // no decode kernel may still read a buffer
+  // no decode kernel still reads a buffer: the owner (LogPins) synchronized the decode streams
   for (auto& P : parts_)
     if (P.dev) hipFree(P.dev);
   for (auto e : pool_) hipEventDestroy(e);
@@ -58,12 +59,12 @@ LogMirror::~LogMirror() {
 }
 
 void LogMirror::set_command_queue(bool on) {
-  if (!on && cq_) HipQueue::get().drain();
-  cq_ = on && HipQueue::get().on();
+  if (!on && cq_) q_->drain();
+  cq_ = on && q_->on();
 }
 
 uint64_t LogMirror::issue(std::function<void()>&& f) {
-  if (cq_) return HipQueue::get().submit(std::move(f));
+  if (cq_) return q_->submit(std::move(f));
   f();
   return 0;
 }
@@ -176,7 +177,7 @@ void LogMirror::issue_prefetches() {
 // The copy stream's event is recorded through the HIP command queue when it is on: until that
 // record has run, the copies it covers count as in flight (no HIP call).
 bool LogMirror::copied_done(CopyStream& c) {
-  return HipQueue::get().ran(c.rec_q) && hipEventQuery(c.copied) == hipSuccess;
+  return q_->ran(c.rec_q) && hipEventQuery(c.copied) == hipSuccess;
 }
 
 void LogMirror::record_copied(CopyStream& c) {
@@ -231,7 +232,7 @@ int LogMirror::next_event() {
   if (pool_refs_[size_t(e)] > 0) {
     // still named by a buffer: that reader is 256 launches old; make sure it completed, then
     // every reference to its old recording counts as completed (the sequence moves on)
-    HipQueue::get().wait(pool_rec_q_[size_t(e)]);
+    q_->wait(pool_rec_q_[size_t(e)]);
     TKM_CHECK(hipEventSynchronize(pool_[size_t(e)]));
     pool_refs_[size_t(e)] = 0;
   }
@@ -261,7 +262,7 @@ void LogMirror::after(hipStream_t stream) {
     if (!slot) {
       // more reader streams than remembered: retire the first one on the host
       slot = &b.readers[0];
-      HipQueue::get().wait(pool_rec_q_[size_t(slot->ev)]);
+      q_->wait(pool_rec_q_[size_t(slot->ev)]);
       TKM_CHECK(hipEventSynchronize(pool_[size_t(slot->ev)]));
       --pool_refs_[size_t(slot->ev)];
     }

@@ -29,6 +29,7 @@
 #include <functional>
 #include <vector>
 
+#include "hip_queue.h"
 #include "span.h"
 
 namespace tkh {
@@ -42,7 +43,8 @@ class LogMirror {
   static constexpr uint64_t kRegAlign = uint64_t(64) << 20;
   // copy_streams: SDMA copy streams (partitions split p % n); <= 0 takes
   // TORCHKAFKA_MIRROR_COPY_STREAMS, else 2.  Each takes one of the process's hardware queues.
-  LogMirror(int device, uint64_t chunk_bytes, int chunks_per_partition, int copy_streams = 0);
+  // `queue`: the loader's HIP command queue (Engine::queue), used once set_command_queue(true)
+  LogMirror(int device, HipQueue* queue, uint64_t chunk_bytes, int chunks_per_partition, int copy_streams = 0);
   ~LogMirror();
   // The mirror's HIP calls go through the HIP command queue (hip_queue.h) when on.
   void set_command_queue(bool on);
@@ -125,6 +127,7 @@ class LogMirror {
   // turned it on, else now; returns its queue number (0: ran now)
   uint64_t issue(std::function<void()>&& f);
   bool cq_ = false;
+  HipQueue* q_ = nullptr;  // the loader's command queue
   void record_copied(CopyStream& c);  // records `copied` at the stream's tail (queued when the queue is on)
   bool wait_ = false;
   uint64_t pending_fallbacks_ = 0;

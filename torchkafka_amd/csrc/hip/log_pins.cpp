@@ -25,11 +25,11 @@ LogPins::~LogPins() {
   }
   pcv_.notify_all();
   if (pin_thread_.joinable()) pin_thread_.join();
+  try {
+    eng_->synchronize();  // the decode streams that read the mirror and the ranges (the driver quiesced)
+  } catch (...) {
+  }
   mirror_.reset();  // its copies read the pinned logs: before they are unregistered
-  // the kernels that read the ranges completed (slots drained by the caller)
-  bool any = false;
-  for (auto& q : reg_ranges_) any = any || !q.empty();
-  if (any) hipDeviceSynchronize();
   for (size_t pidx = 0; pidx < reg_ranges_.size(); ++pidx) {
     auto& q = reg_ranges_[pidx];
     for (auto& r : q) hipHostUnregister(r.first);
@@ -50,7 +50,7 @@ void LogPins::enable_direct() {
 
 void LogPins::enable_mirror(uint64_t chunk_bytes, int chunks_per_partition, int copy_streams) {
   if (!broker_) throw std::runtime_error("DeviceLoader h2d='dma' device decode needs the synthetic broker");
-  mirror_ = std::make_unique<LogMirror>(eng_->device(), chunk_bytes, chunks_per_partition, copy_streams);
+  mirror_ = std::make_unique<LogMirror>(eng_->device(), &eng_->queue(), chunk_bytes, chunks_per_partition, copy_streams);
 }
 
 void LogPins::pin_written(const std::vector<uint32_t>& pidxs) {

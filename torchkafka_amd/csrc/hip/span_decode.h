@@ -9,9 +9,8 @@
 
 namespace tkh {
 
-// Segments one launch can carry in its kernel arguments (one workgroup each, or `split`).
+// Segments one launch can carry in its kernel arguments (one workgroup each).
 constexpr int kMaxLaunchSegs = 48;
-constexpr int kPartCrcWords = 8;  // SpanLaunch::part_crc words per segment: 4 wave CRCs, a count
 
 struct SpanDevSeg {
   const uint8_t* src;   // device address of log byte `log_pos` (pinned broker log, zero-copy)
@@ -45,12 +44,8 @@ struct SpanBatchOut {
 struct SpanLaunch {
   int n_seg;
   int vec_store;             // every batch's rows start 16-byte aligned for vector stores
-  int burst;                 // > 0: each wave waits for its loads after every `burst` of them
-  int split;                 // workgroups per segment: 1, 2 or 4 (span_decode_kernel)
   int64_t row_elems;
   const uint32_t* tabs;      // device CRC tables (tk::kSpanTabWords)
-  uint32_t* part_crc;        // split > 1: kPartCrcWords per segment (wave CRCs + arrival count; zero
-                             // between launches), owned by the launch's stream (Engine::part_crc)
   SpanBatchOut b[kMaxGroup];
   SpanDevSeg s[kMaxLaunchSegs];
 };
@@ -78,7 +73,6 @@ struct JsonStageBatch {
 
 struct JsonStageLaunch {
   int n_seg;
-  int burst;                    // as SpanLaunch::burst
   const uint32_t* tabs;         // device CRC tables (tk::kSpanTabWords)
   JsonStageBatch b[kMaxGroup];
   SpanDevSeg s[kMaxLaunchSegs];
@@ -103,7 +97,6 @@ struct VarSpanBatch {
 
 struct VarSpanLaunch {
   int n_seg;
-  int burst;
   const uint32_t* tabs;
   VarSpanBatch b[kMaxGroup];
   SpanDevSeg s[kMaxLaunchSegs];

@@ -1,19 +1,20 @@
-// gfx950 decode of Kafka RecordBatches straight out of the pinned broker logs
-// (kPackRecordSpan, csrc/core/span.h).
+// gfx950 decode of Kafka RecordBatches straight out of the pinned broker logs (kPackRecordSpan,
+// csrc/core/span.h) or their HBM mirror.
 //
 // Replaces, for schema-declared fixed-width records, the work the reference does per record on
 // the CPU -- kafka-python's CRC check of every fetched batch (check_crcs) and value decode,
 // then `_process` and torch.stack (kafka_dataset.py:156-162) -- and, in this
 // framework's host path, the worker's CRC pass and value copy into the ring slot.
 //
-// One 256-thread workgroup per segment (or `split` of them, each with a share of its CRC lanes and
-// bytes -- opt-in, slower over PCIe: profiles/r04_s21_window): stage it in LDS and verify its
-// RecordBatch CRC32C (span_device.h), then
-//   values: a wave per row for rows of >= 32 16-byte groups (lanes over the row's groups
-//   held by this segment), else (row, group) pairs strided over the block; each group is
-//   read as two aligned 16-byte LDS reads cut to the group's bytes (span::lds16: values sit
-//   at arbitrary byte offsets behind their varint headers), converted (dtypes.h: bit-exact
-//   with Tensor.to), stored 8-16 B per lane.
+// One 256-thread workgroup per segment, streamed through two 15 KiB LDS windows (span_device.h:
+// window k+1 is staged while window k is checked and decoded; ~45 KiB of LDS, so a decode
+// workgroup fits on a CU beside a training job's GEMM tiles).  In each window
+//   values: the 16-byte groups that START in the window's bytes -- a chunk of 64 groups of a row
+//   per wave, or (row, group) pairs strided over the block for rows of < 32 groups; each group is
+//   read as two aligned 16-byte LDS reads cut to the group's bytes (span::lds16: values sit at
+//   arbitrary byte offsets behind their varint headers), converted (dtypes.h: bit-exact with
+//   Tensor.to), stored 8-16 B per lane;
+//   CRC32C: every lane folds its 60-byte piece into its running state (span::crc_piece).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -28,9 +29,9 @@ namespace tkh {
 
 namespace {
 
-using span::kBufBytes;
 using span::kFront;
 using span::kThreads;
+using span::kWinBytes;
 
 template <typename S>
 __device__ __forceinline__ S lds_elem(const uint32_t* b32, int32_t b) {
@@ -55,168 +56,141 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
                                                                const float* __restrict__ scale) {
   using C = Conv<S, D, IsIntDst<D>::value>;
   constexpr int kPer = 16 / int(sizeof(S));  // source elements per 16-byte group
-  __shared__ __attribute__((aligned(16))) uint8_t buf[kBufBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t bufs[2][kWinBytes];
   __shared__ int32_t rel[tk::kSpanMaxSegRows];
   __shared__ __attribute__((aligned(256))) uint32_t tab[span::kNibLdsWords];
+  __shared__ span::RowWins rw;
   __shared__ uint32_t wcrc[kThreads / 64];
 
   const int t = int(threadIdx.x);
-  const int P = a.split, part = int(blockIdx.x) % P;
-  const int nl = int(tk::kSpanLanes) / P;  // CRC lanes of the whole segment's layout per part
-  const SpanDevSeg& sg = a.s[blockIdx.x / P];
+  const SpanDevSeg& sg = a.s[blockIdx.x];
   const SpanBatchOut& bo = a.b[sg.batch];
   const uint32_t len = sg.len, flags = sg.flags;
   const int32_t head = int32_t(reinterpret_cast<uintptr_t>(sg.src) & 15u);
   const uint32_t row_begin = sg.row_begin;
-  const uint32_t nrows = sg.row_end - row_begin;
+  const int32_t nrows = int32_t(sg.row_end - row_begin);
   const bool do_crc = (flags & tk::kSegCrc) != 0;
+  const int32_t lo_b = kFront + head, hi_b = lo_b + int32_t(len);  // the segment's image bytes
+  const span::Windows W(lo_b, hi_b);
+  const int64_t RE = a.row_elems;
+  const int32_t G = int32_t((RE + kPer - 1) / kPer);  // 16-byte groups per row
+  const int32_t row_bytes = int32_t(RE * int64_t(sizeof(S)));
+  D* __restrict__ out = static_cast<D*>(bo.out);
 
-  // ---- 0. split: P workgroups share the segment.  Part j runs CRC lanes [j nl, (j+1) nl) of the
-  // whole segment's layout (chunks of L bytes ending at its last byte), owns the values whose
-  // 16-byte group starts in those lanes' bytes, and stages them with a margin.  Coordinates below
-  // are LDS bytes of this part's image: the whole-segment image's shifted down by `sh` (a multiple
-  // of 16, so 16-byte slots stay aligned).
-  const int32_t w_lo = kFront + head, w_hi = w_lo + int32_t(len);  // the segment, whole image
-  int32_t o_lo = w_lo, o_hi = w_hi, sh = 0;
-  const uint8_t* src = sg.src;
-  uint32_t slen = len;
-  if (P > 1) {
-    const tk::SpanPart pr = tk::span_part(len, (flags & tk::kSegCrcFirst) != 0, P, part);  // span.h
-    o_lo = w_lo + pr.own_lo;
-    o_hi = w_lo + pr.own_hi;
-    src = sg.src + pr.stage_lo;
-    slen = uint32_t(pr.stage_hi - pr.stage_lo);
-    sh = head + pr.stage_lo - int32_t(reinterpret_cast<uintptr_t>(src) & 15u);
-  }
-  const int32_t lo_b = w_lo - sh, hi_b = w_hi - sh;  // the segment's bytes (valid where staged)
-  const int32_t own_lo = o_lo - sh, own_hi = o_hi - sh;
-
-  // ---- 1. stage the segment (span_device.h); the row positions and CRC tables load behind it
-  span::stage(src, slen, buf, a.burst, [&] {
-    const int64_t base = int64_t(sg.log_pos) - int64_t(head) - kFront + sh;  // log position of LDS byte 0
-    for (uint32_t r = uint32_t(t); r < nrows; r += kThreads)
-      rel[r] = int32_t(int64_t(bo.row_pos[row_begin + r]) - base);
-    if (do_crc)
-      span::load_nib_rows(tab, a.tabs);
-  });
-  __syncthreads();
-  const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
-  const uint4* b128 = reinterpret_cast<const uint4*>(buf);  // 16-byte slots (span::lds16)
-
-  // ---- 2. CRC32C lanes (a part: its lanes on its first nl threads, whole waves)
-  const uint32_t* shift_set = nullptr;
-  if (do_crc && t < nl) shift_set = span::crc_lanes(b32, tab, a.tabs, lo_b, hi_b, flags, wcrc, part * nl);
-
-  // ---- 3. values -> out[row, :]
-  {
-    const int64_t RE = a.row_elems;
-    const uint32_t G = uint32_t((RE + kPer - 1) / kPer);  // 16-byte groups per row
-    D* __restrict__ out = static_cast<D*>(bo.out);
-    auto group = [&](uint32_t rr, uint32_t gi) {
-      const int32_t e0 = int32_t(gi) * kPer;
-      const int32_t b0 = rel[rr] + e0 * int32_t(sizeof(S));
-      const int64_t rem = RE - e0;
-      const int nel = rem < kPer ? int(rem) : kPer;
-      if (b0 + nel * int32_t(sizeof(S)) <= lo_b || b0 >= hi_b) return;  // group held by another segment
-      const int32_t key = b0 > lo_b ? b0 : lo_b;
-      if (key < own_lo || key >= own_hi) return;  // held by another part of this segment
-      D* __restrict__ orow = out + int64_t(row_begin + rr) * RE;
-      if (nel == kPer && b0 >= lo_b && b0 + 16 <= hi_b) {
-        const uint4 o = span::lds16(b128, b0);
-        S sv[kPer];
-        __builtin_memcpy(sv, &o, 16);
-        Vec<D, kPer> ov;
+  // group gi of row rr, when its key (first byte in the segment) lies in [own_lo, own_hi)
+  auto group = [&](const uint8_t* buf, int32_t off, int32_t own_lo, int32_t own_hi, int32_t rr, int32_t gi) {
+    const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
+    const int32_t e0 = gi * kPer;
+    const int32_t b0 = rel[rr] + e0 * int32_t(sizeof(S));
+    const int64_t rem = RE - e0;
+    const int nel = rem < kPer ? int(rem) : kPer;
+    if (b0 + nel * int32_t(sizeof(S)) <= lo_b || b0 >= hi_b) return;  // held by another segment
+    const int32_t key = b0 > lo_b ? b0 : lo_b;
+    if (key < own_lo || key >= own_hi) return;  // another window's
+    D* __restrict__ orow = out + int64_t(row_begin + uint32_t(rr)) * RE;
+    if (nel == kPer && b0 >= lo_b && b0 + 16 <= hi_b) {
+      const uint4 o = span::lds16(reinterpret_cast<const uint4*>(buf), b0 + off);
+      S sv[kPer];
+      __builtin_memcpy(sv, &o, 16);
+      Vec<D, kPer> ov;
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-          if constexpr (AFFINE)
-            ov.v[k] = C::apply(sv[k], shift[e0 + k], scale[e0 + k], true);
-          else
-            ov.v[k] = C::apply(sv[k], 0.f, 1.f, false);
-        }
-        if (a.vec_store) {
-          *reinterpret_cast<Vec<D, kPer>*>(orow + e0) = ov;
-        } else {
-#pragma unroll
-          for (int k = 0; k < kPer; ++k) orow[e0 + k] = ov.v[k];
-        }
-      } else {
-        // a group cut by the segment's edge (large rows) or a short row tail
-        for (int k = 0; k < nel; ++k) {
-          const int32_t be = b0 + k * int32_t(sizeof(S));
-          if (be < lo_b || be + int32_t(sizeof(S)) > hi_b) continue;
-          const S sv = lds_elem<S>(b32, be);
-          if constexpr (AFFINE)
-            orow[e0 + k] = C::apply(sv, shift[e0 + k], scale[e0 + k], true);
-          else
-            orow[e0 + k] = C::apply(sv, 0.f, 1.f, false);
-        }
+      for (int k = 0; k < kPer; ++k) {
+        if constexpr (AFFINE)
+          ov.v[k] = C::apply(sv[k], shift[e0 + k], scale[e0 + k], true);
+        else
+          ov.v[k] = C::apply(sv[k], 0.f, 1.f, false);
       }
-    };
-    if (G >= 32) {
-      // wide rows: a wave per row, its lanes over the groups of the row held by this segment
-      const int lane = t & 63;
-      for (uint32_t rr = uint32_t(t >> 6); rr < nrows; rr += kThreads / 64) {
-        const int32_t r0 = rel[rr];
-        const int32_t glo = r0 >= lo_b ? 0 : (lo_b - r0) / 16;
-        const int64_t ghi64 = (int64_t(hi_b) - r0 + 15) / 16;
-        const uint32_t ghi = uint32_t(ghi64 < 0 ? 0 : ghi64 < int64_t(G) ? ghi64 : int64_t(G));
-        for (uint32_t gi = uint32_t(glo) + uint32_t(lane); gi < ghi; gi += 64) group(rr, gi);
+      if (a.vec_store) {
+        *reinterpret_cast<Vec<D, kPer>*>(orow + e0) = ov;
+      } else {
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) orow[e0 + k] = ov.v[k];
       }
     } else {
-      const uint32_t total = nrows * G;
-      for (uint32_t p = uint32_t(t); p < total; p += kThreads) {
-        const uint32_t rr = p / G;
-        group(rr, p - rr * G);
+      // a group cut by the segment's edge (large rows) or a short row tail
+      for (int k = 0; k < nel; ++k) {
+        const int32_t be = b0 + k * int32_t(sizeof(S));
+        if (be < lo_b || be + int32_t(sizeof(S)) > hi_b) continue;
+        const S sv = lds_elem<S>(b32, be + off);
+        if constexpr (AFFINE)
+          orow[e0 + k] = C::apply(sv, shift[e0 + k], scale[e0 + k], true);
+        else
+          orow[e0 + k] = C::apply(sv, 0.f, 1.f, false);
       }
     }
-  }
+  };
 
-  // ---- 4. record fields beside the values (key / timestamp): the batch's first segment copies them
-  if (sg.seg == 0 && part == 0 && bo.ext_words)
-    for (uint32_t i = uint32_t(t); i < bo.ext_words; i += kThreads) bo.ext_out[i] = bo.ext_src[i];
-
-  // ---- 5. verdict; split: each part leaves its wave CRCs in part_crc and the last to arrive
-  // (agent-scope acq_rel count) combines all four, then zeroes the count for the stream's next launch
-  if (do_crc) {
-    __syncthreads();
-    if (t == 0) {
-      if (P == 1) {
-        span::crc_verdict(shift_set, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials);
-      } else {
-        uint32_t* pc = a.part_crc + (blockIdx.x / P) * kPartCrcWords;
-        const int nw = nl / 64;
-        for (int w = part * nw; w < (part + 1) * nw; ++w)
-          __hip_atomic_store(pc + w, wcrc[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t prev = __hip_atomic_fetch_add(pc + 4, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == uint32_t(P - 1)) {
-          uint32_t all[4];
-          for (int w = 0; w < 4; ++w) all[w] = __hip_atomic_load(pc + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(pc + 4, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          span::crc_verdict(shift_set, all, flags, sg.crc, sg.seg, bo.err, bo.partials);
+  const uint32_t crc = span::pipeline(
+      sg.src, W, bufs, tab, a.tabs, lo_b + ((flags & tk::kSegCrcFirst) ? 21 : 0), do_crc,
+      (flags & tk::kSegCrcFirst) != 0,
+      [&] {  // setup: row positions (image bytes) and the window table, behind window 0's loads
+        const int64_t base = int64_t(sg.log_pos) - int64_t(head) - kFront;  // log position of image byte 0
+        for (int32_t r = t; r < nrows; r += kThreads) rel[r] = int32_t(int64_t(bo.row_pos[row_begin + uint32_t(r)]) - base);
+        span::row_wins_init(rw, W.nw);
+      },
+      [&] {  // prepare: the windows each row's groups start in; the record fields beside the values
+        for (int32_t r0w = 0; r0w < nrows; r0w += kThreads) {
+          const int32_t r = r0w + t;
+          const int32_t r0 = r < nrows ? rel[r] : 0;
+          const bool in = r < nrows && r0 + row_bytes > lo_b && r0 < hi_b;
+          const int32_t kf = r0 > lo_b ? r0 : lo_b, kl = min(r0 + (G - 1) * 16, hi_b - 1);
+          span::row_wins_add(rw, W.nw, r0w + (t & ~63), in, W.win_of(kf), W.win_of(kl));
         }
-      }
-    }
+        if (sg.seg == 0 && bo.ext_words)
+          for (uint32_t i = uint32_t(t); i < bo.ext_words; i += kThreads) bo.ext_out[i] = bo.ext_src[i];
+      },
+      [&](int k, const uint8_t* buf, int32_t off) {  // body: the groups window k owns
+        const int32_t ra = rw.lo[k], rb = rw.hi[k];
+        if (ra >= rb) return;
+        const int32_t own_lo = W.own_lo(k), own_hi = W.own_hi(k);
+        if (G >= 32) {
+          span::for_window_units(
+              ra, rb,
+              [&](int32_t rr, int32_t* ulo, int32_t* uhi) {
+                const int32_t r0 = rel[rr];
+                // k == 0 also owns the group cut by the segment's start (its key is lo_b)
+                *ulo = k == 0 ? (r0 >= lo_b ? 0 : (lo_b - r0) >> 4) : span::unit_from(r0, own_lo);
+                *uhi = min(G, span::unit_from(r0, own_hi));
+              },
+              [&](int32_t rr, int32_t gi) { group(buf, off, own_lo, own_hi, rr, gi); });
+        } else {
+          const int32_t total = (rb - ra) * G;
+          for (int32_t p = t; p < total; p += kThreads) {
+            const int32_t q = p / G;
+            group(buf, off, own_lo, own_hi, ra + q, p - q * G);
+          }
+        }
+      });
+
+  // ---- verdict: merge the lanes; thread 0 compares (or leaves the partial for the driver)
+  if (do_crc) {
+    const uint32_t* shift_set = span::crc_merge(a.tabs, crc, wcrc);
+    __syncthreads();
+    if (t == 0) span::crc_verdict(shift_set, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials);
   }
 }
 
-// VarLen rows (kPackVarSpan): stage + CRC as above, then a wave per row converts its elements
-// (any byte alignment: two dwords + v_alignbyte per element) and pads the row to L.
+// VarLen rows (kPackVarSpan): staged and checked as above; each row's elements (any byte alignment)
+// converted in 16-byte units by the window its unit starts in; padding, mask and lengths written
+// before the windows (they need only the row table).
 template <typename S, typename D>
 __global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, D pad) {
   using C = Conv<S, D, IsIntDst<D>::value>;
   constexpr int kWaves = kThreads / 64;
-  __shared__ __attribute__((aligned(16))) uint8_t buf[kBufBytes];
+  constexpr int kPer = 16 / int(sizeof(S));
+  __shared__ __attribute__((aligned(16))) uint8_t bufs[2][kWinBytes];
   __shared__ int32_t rel[tk::kJsonSpanMaxSegRows];
-  __shared__ int32_t tln[tk::kJsonSpanMaxSegRows];
-  __shared__ int32_t cnt[tk::kJsonSpanMaxSegRows];
+  __shared__ int32_t nout[tk::kJsonSpanMaxSegRows];  // elements to convert (-1: a worker-copied row)
   __shared__ __attribute__((aligned(256))) uint32_t tab[span::kNibLdsWords];
+  __shared__ span::RowWins rw;
   __shared__ uint32_t wcrc[kWaves];
+  __shared__ int32_t bad;
 
   const int t = int(threadIdx.x), lane = t & 63, wv = t >> 6;
   const SpanDevSeg& sg = a.s[blockIdx.x];
   const VarSpanBatch& bo = a.b[sg.batch];
   const uint32_t row_begin = sg.row_begin;
-  const uint32_t nrows = sg.row_end - row_begin;
+  const int32_t nrows = int32_t(sg.row_end - row_begin);
   const uint32_t flags = sg.flags;
   const int64_t L = bo.L;
   const int32_t trunc = bo.trunc_len;
@@ -232,8 +206,8 @@ __global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, 
 
   if (flags & tk::kSegHostRows) {
     // rows the worker copied into the slot (longer than one segment): a wave per row
-    for (uint32_t rr = uint32_t(wv); rr < nrows; rr += kWaves) {
-      const int64_t row = int64_t(row_begin + rr);
+    for (int32_t rr = wv; rr < nrows; rr += kWaves) {
+      const int64_t row = int64_t(row_begin) + rr;
       const tk::JsonSpanRow d = bo.rows[row];
       if (d.tlen >= 0) continue;
       int64_t n_out = trunc >= 0 && d.count > trunc ? trunc : d.count;
@@ -249,61 +223,86 @@ __global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, 
   const uint32_t len = sg.len;
   const int32_t head = int32_t(reinterpret_cast<uintptr_t>(sg.src) & 15u);
   const bool do_crc = (flags & tk::kSegCrc) != 0;
-  span::stage(sg.src, len, buf, a.burst, [&] {
-    const int64_t base = int64_t(sg.log_pos) - int64_t(head) - kFront;  // log position of LDS byte 0
-    for (uint32_t r = uint32_t(t); r < nrows; r += kThreads) {
-      const tk::JsonSpanRow d = bo.rows[row_begin + r];
-      rel[r] = d.tlen >= 0 ? int32_t(int64_t(d.pos) - base) : 0;
-      tln[r] = d.tlen;
-      cnt[r] = d.count;
-    }
-    if (do_crc)
-      span::load_nib_rows(tab, a.tabs);
-  });
-  __syncthreads();
-  const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
-  const uint4* b128 = reinterpret_cast<const uint4*>(buf);  // 16-byte slots (span::lds16)
-  const int32_t lo_b = kFront + head, hi_b = kFront + head + int32_t(len);
-  const uint32_t* shift_set = nullptr;
-  if (do_crc) shift_set = span::crc_lanes(b32, tab, a.tabs, lo_b, hi_b, flags, wcrc);
+  const int32_t lo_b = kFront + head, hi_b = lo_b + int32_t(len);
+  const span::Windows W(lo_b, hi_b);
 
-  bool off_seg = false;
-  for (uint32_t rr = uint32_t(wv); rr < nrows; rr += kWaves) {
-    const int32_t T = tln[rr];
-    if (T < 0) continue;  // copied by the worker (its kSegHostRows block writes it)
-    const int32_t r0 = rel[rr];
-    const int64_t row = int64_t(row_begin + rr);
-    D* orow = out + row * L;
-    const int32_t count = cnt[rr];
-    int64_t n_out = trunc >= 0 && count > trunc ? trunc : count;
-    n_out = n_out < L ? n_out : L;
-    if (r0 < lo_b || r0 + T > hi_b || int64_t(count) * int64_t(sizeof(S)) != T) {
-      off_seg = true;  // the row table disagrees with the segment: read nothing, never commit
-      n_out = 0;
-    }
-    // 16 source bytes per lane per step (span::lds16: values sit at any byte offset behind their
-    // headers), vector stores when the row is aligned; then the tail
-    constexpr int kPer = 16 / int(sizeof(S));
-    const int64_t full = bo.reserved ? n_out / kPer * kPer : 0;
-    for (int64_t e0 = int64_t(lane) * kPer; e0 < full; e0 += 64 * kPer) {
-      const uint4 o = span::lds16(b128, r0 + int32_t(e0) * int32_t(sizeof(S)));
-      S sv[kPer];
-      __builtin_memcpy(sv, &o, 16);
-      Vec<D, kPer> ov;
+  const uint32_t crc = span::pipeline(
+      sg.src, W, bufs, tab, a.tabs, lo_b + ((flags & tk::kSegCrcFirst) ? 21 : 0), do_crc,
+      (flags & tk::kSegCrcFirst) != 0,
+      [&] {  // setup: the row table (image bytes, elements to convert)
+        const int64_t base = int64_t(sg.log_pos) - int64_t(head) - kFront;  // log position of image byte 0
+        for (int32_t r = t; r < nrows; r += kThreads) {
+          const tk::JsonSpanRow d = bo.rows[row_begin + uint32_t(r)];
+          rel[r] = d.tlen >= 0 ? int32_t(int64_t(d.pos) - base) : 0;
+          int32_t n = -1;
+          if (d.tlen >= 0) {
+            int64_t n_out = trunc >= 0 && d.count > trunc ? trunc : d.count;
+            n_out = n_out < L ? n_out : L;
+            // the row table must agree with the segment: else read nothing and never commit
+            const bool ok = rel[r] >= lo_b && rel[r] + d.tlen <= hi_b && int64_t(d.count) * int64_t(sizeof(S)) == d.tlen;
+            n = ok ? int32_t(n_out) : -2;
+          }
+          nout[r] = n;
+        }
+        span::row_wins_init(rw, W.nw);
+        if (t == 0) bad = 0;
+      },
+      [&] {  // prepare: padding, mask and lengths of every row; the windows its units start in
+        for (int32_t rr = wv; rr < nrows; rr += kWaves) {
+          const int32_t n = nout[rr];
+          if (n == -1) continue;  // copied by the worker (its kSegHostRows block writes it)
+          if (n == -2 && lane == 0) bad = 1;
+          const int64_t row = int64_t(row_begin) + rr;
+          finish(out + row * L, row, n < 0 ? 0 : n);
+        }
+        for (int32_t r0w = 0; r0w < nrows; r0w += kThreads) {
+          const int32_t r = r0w + t;
+          const int32_t n = r < nrows ? nout[r] : 0;
+          const int32_t r0 = r < nrows ? rel[r] : 0;
+          const int32_t units = n > 0 ? (n + kPer - 1) / kPer : 0;
+          span::row_wins_add(rw, W.nw, r0w + (t & ~63), units > 0, W.win_of(r0), W.win_of(r0 + 16 * (units - 1)));
+        }
+      },
+      [&](int k, const uint8_t* buf, int32_t off) {  // body: the 16-byte units window k owns
+        const int32_t ra = rw.lo[k], rb = rw.hi[k];
+        if (ra >= rb) return;
+        const int32_t own_lo = W.own_lo(k), own_hi = W.own_hi(k);
+        const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
+        span::for_window_units(
+            ra, rb,
+            [&](int32_t rr, int32_t* ulo, int32_t* uhi) {
+              const int32_t n = nout[rr], r0 = rel[rr];
+              const int32_t units = n > 0 ? (n + kPer - 1) / kPer : 0;
+              *ulo = span::unit_from(r0, own_lo);
+              *uhi = min(units, span::unit_from(r0, own_hi));
+            },
+            [&](int32_t rr, int32_t u) {
+              const int32_t n = nout[rr], r0 = rel[rr];
+              D* orow = out + (int64_t(row_begin) + rr) * L;
+              const int32_t e0 = u * kPer, b0 = r0 + 16 * u + off;
+              if (bo.reserved && e0 + kPer <= n) {
+                // 16 source bytes (span::lds16: values sit at any byte offset behind their headers),
+                // a vector store (the row starts 16-byte aligned)
+                const uint4 o = span::lds16(reinterpret_cast<const uint4*>(buf), b0);
+                S sv[kPer];
+                __builtin_memcpy(sv, &o, 16);
+                Vec<D, kPer> ov;
 #pragma unroll
-      for (int k = 0; k < kPer; ++k) ov.v[k] = C::apply(sv[k], 0.f, 1.f, false);
-      *reinterpret_cast<Vec<D, kPer>*>(orow + e0) = ov;
-    }
-    for (int64_t k = full + lane; k < n_out; k += 64)
-      orow[k] = C::apply(lds_elem<S>(b32, r0 + int32_t(k) * int32_t(sizeof(S))), 0.f, 1.f, false);
-    finish(orow, row, n_out);
-  }
-  if (off_seg && lane == 0) *bo.err = int32_t(sg.seg);
+                for (int q = 0; q < kPer; ++q) ov.v[q] = C::apply(sv[q], 0.f, 1.f, false);
+                *reinterpret_cast<Vec<D, kPer>*>(orow + e0) = ov;
+              } else {
+                for (int q = 0; q < kPer && e0 + q < n; ++q)
+                  orow[e0 + q] = C::apply(lds_elem<S>(b32, b0 + q * int32_t(sizeof(S))), 0.f, 1.f, false);
+              }
+            });
+      });
 
   if (do_crc) {
+    const uint32_t* shift_set = span::crc_merge(a.tabs, crc, wcrc);
     __syncthreads();
     if (t == 0) span::crc_verdict(shift_set, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials);
   }
+  if (t == 0 && bad) *bo.err = int32_t(sg.seg);
 }
 
 template <typename S, typename D>
@@ -316,7 +315,7 @@ void launch_var_span_t(const VarSpanLaunch& a, double pad, hipStream_t stream) {
 template <typename S, typename D>
 void launch_span_t(const SpanLaunch& a, const float* shift, const float* scale, hipStream_t stream) {
   if (a.n_seg <= 0) return;
-  const dim3 grid(unsigned(a.n_seg * a.split));
+  const dim3 grid(unsigned(a.n_seg));
   if (shift)
     hipLaunchKernelGGL((span_decode_kernel<S, D, true>), grid, dim3(kThreads), 0, stream, a, shift, scale);
   else
@@ -356,13 +355,11 @@ void launch_var_span(const VarSpanLaunch& a, int src_dt, int dst_dt, double pad,
 void launch_span_decode(const SpanLaunch& a, int src_dt, int dst_dt, const float* shift, const float* scale,
                         hipStream_t stream) {
   if (a.n_seg < 0 || a.n_seg > kMaxLaunchSegs) throw std::invalid_argument("span decode: bad segment count");
-  if ((a.split != 1 && a.split != 2 && a.split != 4) || (a.split > 1 && a.part_crc == nullptr))
-    throw std::invalid_argument("span decode: bad split");
   if (!is_float_dt(dst_dt) && is_float_dt(src_dt))
     throw std::invalid_argument("collate: float records cannot be cast to an integer dtype");
   if (shift && !is_float_dt(dst_dt)) throw std::invalid_argument("collate: normalisation needs a float dtype");
   for (int i = 0; i < a.n_seg; ++i) {
-    // the kernel stages a segment whole in LDS and its row positions next to it
+    // the kernel streams a segment of <= kSpanSegMax bytes and keeps its row positions in LDS
     if (a.s[i].len == 0 || a.s[i].len > tk::kSpanSegMax || a.s[i].row_end < a.s[i].row_begin ||
         a.s[i].row_end - a.s[i].row_begin > tk::kSpanMaxSegRows || a.s[i].batch >= kMaxGroup)
       throw std::invalid_argument("span decode: malformed segment");

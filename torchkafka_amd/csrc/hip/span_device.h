@@ -1,22 +1,28 @@
-// Device code shared by the span kernels (span_decode.hip: fixed-width values, json_span.hip: JSON
-// text): one 256-thread workgroup per log segment (<= 128 KiB of one pinned partition log, so one
-// workgroup per CU),
-//   1. stage: the segment is copied into a contiguous LDS image (16-byte front offset) by LDS-DMA,
-//      global_load_lds_dwordx4, one 1 KiB load in flight per wave (fewer outstanding PCIe reads
-//      move more bytes; the launches of two or three decode streams keep the link busy);
-//   2. crc_lanes: CRC32C of a RecordBatch's bytes [21, end): 256 lanes x 260- or 516-byte chunks
-//      ending at the range end (an odd dword count per chunk: the 32 lanes of a ds_read_b32
-//      group hit 32 different banks), slice-by-8 fed by a sliding dword window (two ds_read_b32 +
-//      two v_alignbyte per 8 bytes) and looked up per NIBBLE in 16-entry LDS rows (span.h
-//      kSpanTabNib: 16 conflict-free reads per 8 bytes instead of 8 byte-table reads at ~3-way
-//      conflicts), then 6 shuffle levels of "shift by 2^j chunks" (4 table lookups each,
-//      csrc/core/crc32c.cpp crc32c_span_tables);
-//   3. crc_verdict (thread 0, after a barrier): 2 LDS levels merge the 4 wave CRCs; a RecordBatch
-//      held whole by the segment is compared with its header CRC -- a mismatch stores the segment
-//      index into the batch's host-mapped error word (the driver reads it when the slot is
-//      released and never commits the batch) -- and a RecordBatch cut into several segments
-//      stores the raw partial CRC for the driver to chain.
-// Replaces kafka-python's check_crcs pass over every fetched RecordBatch (SURVEY E5).
+// Device code shared by the span kernels (span_decode.hip: fixed-width and var-len values,
+// json_span.hip: JSON text): one 256-thread workgroup per log segment (<= 128 KiB of one partition
+// log, pinned host memory or its HBM mirror), streamed through TWO LDS windows:
+//
+//   window k = segment bytes [w0 + k W, w0 + (k+1) W), W = kSpanWin (15,360), the windows ending at
+//   the segment's end (span.h).  Window k+1 is staged by LDS-DMA (global_load_lds_dwordx4, every
+//   lane of a wave one 16-byte chunk of a contiguous KiB) while the workgroup checks and decodes
+//   window k out of the other buffer:
+//     * CRC32C: lane t folds its 60-byte piece of the window into a running state (slice-by-8 fed by
+//       a sliding dword window, looked up per NIBBLE in 16-entry LDS rows: conflict-free), the state
+//       crossing the other lanes' bytes with one gap operator between windows; after the last
+//       window 6 shuffle levels and 2 LDS levels of "shift by 2^j pieces" merge the lanes
+//       (span.h, host mirror csrc/core/crc32c.cpp crc32c_span_emulate);
+//     * the values / texts whose 16-byte group (or piece) STARTS in the window's bytes of the
+//       segment (staged with 16 bytes before and 48 after, so a group reaching past the window is
+//       whole in LDS).
+//   A workgroup needs ~45 KiB of LDS instead of the whole segment's 143 KiB: it lands on a CU beside
+//   a training job's GEMM tiles (a hipBLASLt 256x256 tile holds 65 KiB) instead of waiting for the
+//   GEMM to end, and its staging overlaps its compute.
+//
+// A RecordBatch held whole by the segment is compared with its header CRC -- a mismatch stores the
+// segment index into the batch's host-mapped error word (the driver reads it when the slot is
+// released and never commits the batch) -- and one cut into several segments stores the raw
+// partial CRC for the driver to chain.
+// Replaces kafka-python's check_crcs pass over every fetched RecordBatch (SURVEY E5/E8).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -28,19 +34,21 @@ namespace tkh {
 namespace span {
 
 constexpr int kThreads = 256;
-constexpr int kFront = 16;  // LDS image offset: boundary reads may start up to 3 bytes before it
-constexpr int kLoads = int((tk::kSpanSegMax + 32) / 16 / kThreads) + 1;
-constexpr int kBufBytes = kFront + int(tk::kSpanSegMax) + 64;
+constexpr int kFront = 16;     // image coordinates: segment byte i is image byte kFront + (src & 15) + i
+constexpr int32_t kWin = int32_t(tk::kSpanWin);
+constexpr int kPad = tk::kSpanWinPad;          // LDS bytes before a window's first staged byte
+constexpr int kWinBytes = tk::kSpanWinBytes;    // one window buffer (span.h)
+constexpr int kWinLoads = (kWin + 96 + 16 * kThreads - 1) / (16 * kThreads);  // LDS-DMA rounds per window
+static_assert(kWinBytes % 16 == 0, "window buffers stay 16-byte aligned");
 
 // 16 bytes at LDS byte b0 of a 16-byte aligned image (any alignment of b0), for loops whose
 // lanes read consecutive 16-byte pieces: two 16-byte-aligned ds_read_b128 per lane -- consecutive
 // slots across the wave, conflict-free -- and the unaligned 16 bytes cut out of those 32 in
-// registers.  Five ds_read_b32 at a 16-byte lane stride (the 5-dword window used before) cost a
-// 4-way bank conflict each: banks (a/4) mod 32 in 32-lane groups (MI355X_MICROARCH.md §LDS).
-// Reads up to the 16-byte boundary at or below b0 + 31: the image keeps 64 spare bytes at its end.
-// `img` is the image as 16-byte slots.  The reads are nontemporal loads (a no-op hint for LDS)
-// because the compiler otherwise narrows them to the dwords the selects below can pick --
-// ds_read2_b32 pairs at a 16-byte lane stride, the conflicting pattern this replaces.
+// registers.  Five ds_read_b32 at a 16-byte lane stride cost a 4-way bank conflict each: banks
+// (a/4) mod 32 in 32-lane groups (MI355X_MICROARCH.md §LDS).  Reads up to the 16-byte boundary at
+// or below b0 + 31.  The reads are nontemporal loads (a no-op hint for LDS) because the compiler
+// otherwise narrows them to the dwords the selects below can pick -- ds_read2_b32 pairs at a
+// 16-byte lane stride, the conflicting pattern this replaces.
 typedef uint32_t lds_v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 lds16(const uint4* img16, int32_t b0) {
   const lds_v4u* img = reinterpret_cast<const lds_v4u*>(img16);
@@ -73,41 +81,78 @@ __device__ __forceinline__ uint32_t shift_op(const uint32_t* __restrict__ set, u
   return S[c & 255u] ^ S[256u + ((c >> 8) & 255u)] ^ S[512u + ((c >> 16) & 255u)] ^ S[768u + (c >> 24)];
 }
 
-// Stage 1.  Wave w's i-th load writes chunks [i * 256 + 64 w, +64) -- one contiguous KiB of the
-// image, exactly the instruction's wave-uniform-base + 16 * lane layout -- with no VGPR staging.
-// Each wave keeps `burst` loads in flight (0: all): zero-copy PCIe reads lose bandwidth with many
-// outstanding requests (tools/probes/tlb_probe.hip: 53 GB/s at 32 reading blocks, 40 at 512), and
-// with two or three decode kernels running at once the link stays full (config 2: 53 M rec/s with
-// one load in flight per wave, 41-44 M with 2-8, 46 M with all 17 issued up front).
-// `behind_first()` runs once the first load is issued (the row tables and CRC tables load behind
-// it: waiting for them waits for it).  The caller's __syncthreads() completes the image.
-template <class F>
-__device__ __forceinline__ void stage(const uint8_t* src, uint32_t len, uint8_t* buf, int burst, F&& behind_first) {
-  const int t = int(threadIdx.x);
-  const uintptr_t su = reinterpret_cast<uintptr_t>(src);
-  const uint32_t head = uint32_t(su & 15u);
-  const uint32_t nchunk = (head + len + 15u) >> 4;
-  const uint8_t* gsrc = reinterpret_cast<const uint8_t*>(su - head);
-  const int wv = t >> 6;
-  auto dma = [&](int i) {
-    const uint32_t c = uint32_t(t + i * kThreads);
-    if (c < nchunk)
-      __builtin_amdgcn_global_load_lds(
-          gsrc + 16u * c, (__attribute__((address_space(3))) void*)(buf + kFront + 16 * (i * kThreads + wv * 64)), 16,
-          0, 0);
-  };
-  dma(0);
-  behind_first();
+using Windows = tk::SpanWindows;  // span.h
+
+// Issues window k's LDS-DMA loads into `buf` (kWinBytes); `gbase` is the global address of image
+// byte kFront (the segment's first byte rounded down to 16).  LDS byte of image byte x:
+// kPad + x - stage_lo(k).  Round r of wave w writes chunks [r * 256 + 64 w, +64) -- one contiguous
+// KiB, the instruction's wave-uniform-base + 16 * lane layout -- with no VGPR staging.  The caller
+// completes them with s_waitcnt vmcnt(0) + a barrier.
+__device__ __forceinline__ void stage_window(const uint8_t* gbase, const Windows& W, int k, uint8_t* buf) {
+  const int t = int(threadIdx.x), wv = t >> 6;
+  const int32_t a = W.stage_lo(k);
+  const uint32_t nchunk = uint32_t(W.stage_hi(k) - a) >> 4;
+  const uint8_t* g = gbase + (a - kFront);
 #pragma unroll
-  for (int i = 1; i < kLoads; ++i) {
-    if (16u * uint32_t(i * kThreads) >= 16u * nchunk) break;  // block-uniform: no wave has chunk i
-    dma(i);
-    if (burst > 0 && (i % burst) == burst - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int r = 0; r < kWinLoads; ++r) {
+    if (uint32_t(r * kThreads) >= nchunk) break;  // block-uniform
+    const uint32_t c = uint32_t(t + r * kThreads);
+    if (c < nchunk)
+      __builtin_amdgcn_global_load_lds(g + 16u * c,
+                                       (__attribute__((address_space(3))) void*)(buf + kPad + 16 * (r * kThreads + wv * 64)),
+                                       16, 0, 0);
   }
 }
 
+__device__ __forceinline__ void wait_window() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// Row ranges per window: rows [lo[k], hi[k]) hold every group a window owns (rows in any order;
+// a row outside the range owns nothing there).  Each thread reports its row's first and last
+// owned key window (kf > kl: the row owns nothing); wave ballots keep one LDS atomic per window.
+struct RowWins {
+  int32_t lo[16], hi[16];
+};
+__device__ __forceinline__ void row_wins_init(RowWins& rw, int nw) {
+  const int t = int(threadIdx.x);
+  if (t < nw) {
+    rw.lo[t] = 0x7FFFFFFF;
+    rw.hi[t] = 0;
+  }
+}
+__device__ __forceinline__ void row_wins_add(RowWins& rw, int nw, int32_t row_base, bool valid, int kf, int kl) {
+  const int lane = int(threadIdx.x) & 63;
+  for (int k = 0; k < nw; ++k) {
+    const unsigned long long m = __ballot(valid && kf <= k && k <= kl);
+    if (m && lane == 0) {
+      atomicMin(&rw.lo[k], row_base + int32_t(__builtin_ctzll(m)));
+      atomicMax(&rw.hi[k], row_base + 64 - int32_t(__builtin_clzll(m)));
+    }
+  }
+}
+
+// The 16-byte units a window owns, spread over the workgroup: rows [ra, rb) in order, each row's
+// owned units [ulo, uhi) (range(rr, &ulo, &uhi)) cut into chunks of 64 lanes, the chunks dealt to
+// the 4 waves round robin -- a wave per row for rows of up to 64 units, all four on a wide row.
+template <class Range, class Fn>
+__device__ __forceinline__ void for_window_units(int32_t ra, int32_t rb, Range&& range, Fn&& fn) {
+  const int t = int(threadIdx.x), lane = t & 63, wv = t >> 6;
+  int ci = 0;
+  for (int32_t rr = ra; rr < rb; ++rr) {
+    int32_t ulo = 0, uhi = 0;
+    range(rr, &ulo, &uhi);
+    for (int32_t u = ulo; u < uhi; u += 64, ++ci)
+      if ((ci & 3) == wv && u + lane < uhi) fn(rr, u + lane);
+  }
+}
+// First unit of a row whose key (key0 + 16 u) is >= x.
+__device__ __forceinline__ int32_t unit_from(int32_t key0, int32_t x) { return key0 >= x ? 0 : (x - key0 + 15) >> 4; }
+
 // The nibble rows in LDS: row r (16 words) at byte r * 256 of a 256-byte aligned 4 KiB array, so a
-// lookup's LDS address is (row base) | (nibble * 4) with the nibble in the address's low byte.
+// lookup's LDS address is (row base) | (nibble * 4) with the nibble in the address's low byte; the
+// gap operator's row i sits in words 16..31 of row i.
 constexpr int kNibRowWords = 64;
 constexpr int kNibLdsWords = 16 * kNibRowWords;
 using lds_u32 = __attribute__((address_space(3))) const uint32_t;
@@ -115,6 +160,8 @@ using lds_u32 = __attribute__((address_space(3))) const uint32_t;
 __device__ __forceinline__ void load_nib_rows(uint32_t* tab, const uint32_t* __restrict__ tabs) {
   for (int i = int(threadIdx.x); i < int(tk::kSpanTabNibWords); i += kThreads)
     tab[(i >> 4) * kNibRowWords + (i & 15)] = tabs[tk::kSpanTabNib + i];
+  for (int i = int(threadIdx.x); i < int(tk::kSpanTabGapWords); i += kThreads)
+    tab[(i >> 4) * kNibRowWords + 16 + (i & 15)] = tabs[tk::kSpanTabGap + i];
 }
 
 // Slice-by-4 of one dword through the nibble rows: byte i of w goes through byte table B - i,
@@ -136,61 +183,70 @@ __device__ __forceinline__ uint32_t nib_dword(uint32_t nbase, uint32_t w) {
   return r;
 }
 
-// Stage 2 (every thread, after the barrier that completed the image).  The CRC range is
-// [c0, c1) in LDS bytes: [lo_b + 21, hi_b) for the segment holding a RecordBatch's start, else
-// [lo_b, hi_b); `tab` is the LDS copy of the nibble rows (load_nib_rows).  Each wave's lane 0 leaves the wave's CRC in wcrc[wave]; returns the shift-table
-// set of the lane size used (for crc_verdict).
-// `lane_base`: a workgroup that holds only part of the range (span_decode_kernel's split) runs
-// lanes lane_base.. of the whole range's layout on its first threads (whole waves).
-__device__ __forceinline__ const uint32_t* crc_lanes(const uint32_t* __restrict__ b32, const uint32_t* __restrict__ tab,
-                                                     const uint32_t* __restrict__ tabs, int32_t lo_b, int32_t hi_b,
-                                                     uint32_t flags, uint32_t* wcrc, int lane_base = 0) {
-  const int t = int(threadIdx.x) + lane_base;
-  const uint32_t* shift_set = tabs + tk::kSpanTabShift;
-  uint32_t crc = 0;
-  const uint32_t nbase = uint32_t(uintptr_t((lds_u32*)tab));  // the LDS byte address
-  const bool first = (flags & tk::kSegCrcFirst) != 0;
-  const int32_t c0 = lo_b + (first ? 21 : 0), c1 = hi_b;
-  const int32_t L = int32_t(tk::span_lane_bytes(uint32_t(c1 - c0)));
-  if (L != int32_t(tk::kSpanLaneSmall)) shift_set += tk::kSpanTabShiftSet;
-  const int32_t start = c1 - (int32_t(tk::kSpanLanes) - t) * L;
-  const int32_t nsteps = (L - 4) >> 3;
-  if (start + 4 > c0) {  // the chunk's first 4 bytes (>= kFront - 3 whenever start + 4 > c0)
+// The window gap: the state after kSpanWin - kSpanPiece zero bytes (8 nibble lookups).
+__device__ __forceinline__ uint32_t gap_op(uint32_t nbase, uint32_t c) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r ^= *(lds_u32*)uintptr_t(nbase + uint32_t(i) * 256u + 64u + ((c >> (4 * i)) & 15u) * 4u);
+  return r;
+}
+
+// One lane's piece of window k folded into its running state `crc` (every thread, every window).
+// b32: the window's LDS bytes as dwords; `off` = LDS byte of image byte 0 (kPad - stage_lo(k));
+// c0: image byte of the first CRC'd byte ([lo + 21, hi) for the segment holding a RecordBatch's
+// start, else [lo, hi)); `first`: inject the 0xFFFFFFFF initial value into its first 4 bytes.
+__device__ __forceinline__ uint32_t crc_piece(const uint32_t* __restrict__ b32, uint32_t nbase, const Windows& W,
+                                              int k, int32_t off, int32_t c0, bool first, uint32_t crc) {
+  const int t = int(threadIdx.x);
+  constexpr int32_t P = int32_t(tk::kSpanPiece);
+  constexpr int32_t nsteps = (P - 4) >> 3;
+  if (k > 0) crc = gap_op(nbase, crc);  // still zero before the first CRC'd byte
+  const int32_t start = W.w0 + k * kWin + t * P + off;  // LDS byte of the piece
+  const int32_t cl = c0 + off;                          // LDS byte of c0
+  if (start + 4 > cl) {
     const int32_t w = start >> 2, sh = start & 3;
     uint32_t x = __builtin_amdgcn_alignbyte(b32[w + 1], b32[w], sh);
-    if (start < c0 + 4) {
-      const uint32_t keep = keep_from(start, c0);
+    if (start < cl + 4) {
+      const uint32_t keep = keep_from(start, cl);
       x &= keep;
-      if (first) x ^= keep & ~keep_from(start, c0 + 4);  // the 0xFFFFFFFF initial value
+      if (first) x ^= keep & ~keep_from(start, cl + 4);  // the 0xFFFFFFFF initial value
     }
-    crc = nib_dword<3>(nbase, x);
+    crc = nib_dword<3>(nbase, x ^ crc);
   }
   const int32_t a1 = start + 4;
-  const int32_t j0 = a1 >= c0 ? 0 : (c0 - a1) >> 3;  // 8-byte groups wholly below c0 are skipped
+  const int32_t j0 = a1 >= cl ? 0 : (cl - a1) >> 3;  // 8-byte groups wholly below c0 are skipped
   if (j0 < nsteps) {
     int32_t ad = a1 + 8 * j0;
     int32_t w = ad >> 2;
     const int32_t sh = ad & 3;
     uint32_t lo = b32[w];
+#pragma unroll 7
     for (int32_t j = j0; j < nsteps; ++j, ad += 8) {
       const uint32_t m1 = b32[w + 1], m2 = b32[w + 2];
       w += 2;
       uint32_t x = __builtin_amdgcn_alignbyte(m1, lo, sh), y = __builtin_amdgcn_alignbyte(m2, m1, sh);
       lo = m2;
-      if (ad < c0 + 4) {
-        const uint32_t kx = keep_from(ad, c0), ky = keep_from(ad + 4, c0);
+      if (ad < cl + 4) {
+        const uint32_t kx = keep_from(ad, cl), ky = keep_from(ad + 4, cl);
         x &= kx;
         y &= ky;
         if (first) {
-          x ^= kx & ~keep_from(ad, c0 + 4);
-          y ^= ky & ~keep_from(ad + 4, c0 + 4);
+          x ^= kx & ~keep_from(ad, cl + 4);
+          y ^= ky & ~keep_from(ad + 4, cl + 4);
         }
       }
       x ^= crc;
       crc = nib_dword<7>(nbase, x) ^ nib_dword<3>(nbase, y);
     }
   }
-  const int lane = t & 63;
+  return crc;
+}
+
+// After the last window (every thread): 6 shuffle levels merge each wave's 64 lane states; lane 0
+// leaves the wave's CRC in wcrc[wave].  Returns the shift-table set (for crc_verdict).
+__device__ __forceinline__ const uint32_t* crc_merge(const uint32_t* __restrict__ tabs, uint32_t crc, uint32_t* wcrc) {
+  const uint32_t* shift_set = tabs + tk::kSpanTabShift;
+  const int t = int(threadIdx.x), lane = t & 63;
 #pragma unroll
   for (uint32_t j = 0; j < 6; ++j) {
     const uint32_t other = __shfl_down(crc, 1u << j, 64);
@@ -200,7 +256,7 @@ __device__ __forceinline__ const uint32_t* crc_lanes(const uint32_t* __restrict_
   return shift_set;
 }
 
-// Stage 3 (thread 0 only, after a barrier that follows crc_lanes).
+// Thread 0 only, after a barrier that follows crc_merge.
 __device__ __forceinline__ void crc_verdict(const uint32_t* __restrict__ shift_set, const uint32_t* wcrc,
                                             uint32_t flags, uint32_t want, uint32_t seg, int32_t* err,
                                             uint32_t* partials) {
@@ -212,6 +268,36 @@ __device__ __forceinline__ void crc_verdict(const uint32_t* __restrict__ shift_s
   } else {
     partials[seg] = c;
   }
+}
+
+// The pipeline every span kernel runs: stage window 0, run `setup` (row tables into LDS -- their
+// loads overlap window 0's), wait, run `prepare` (per-row work that needs the tables: row window
+// ranges, scans, descriptors), then for every window k: stage k+1 into the other buffer, `body(k,
+// buf, off)` (the window's values; off = LDS byte of image byte 0) and its CRC pieces.  Returns the
+// lane's CRC state (0 when the segment carries no CRC).
+template <class Setup, class Prepare, class Body>
+__device__ __forceinline__ uint32_t pipeline(const uint8_t* src, const Windows& W, uint8_t (*bufs)[kWinBytes],
+                                             uint32_t* tab, const uint32_t* __restrict__ tabs, int32_t c0,
+                                             bool do_crc, bool first, Setup&& setup, Prepare&& prepare,
+                                             Body&& body) {
+  const uint8_t* gbase = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(src) & ~uintptr_t(15));
+  stage_window(gbase, W, 0, bufs[0]);
+  if (do_crc) load_nib_rows(tab, tabs);
+  setup();
+  wait_window();
+  prepare();
+  __syncthreads();
+  const uint32_t nbase = uint32_t(uintptr_t((lds_u32*)tab));  // the LDS byte address
+  uint32_t crc = 0;
+  for (int k = 0; k < W.nw; ++k) {
+    if (k > 0) wait_window();  // window k landed; every thread is done with window k - 1's buffer
+    if (k + 1 < W.nw) stage_window(gbase, W, k + 1, bufs[(k + 1) & 1]);
+    uint8_t* buf = bufs[k & 1];
+    const int32_t off = kPad - W.stage_lo(k);
+    body(k, buf, off);  // stores first: they drain while the CRC runs
+    if (do_crc) crc = crc_piece(reinterpret_cast<const uint32_t*>(buf), nbase, W, k, off, c0, first, crc);
+  }
+  return crc;
 }
 
 }  // namespace span

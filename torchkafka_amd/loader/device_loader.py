@@ -211,8 +211,6 @@ class _Run:
                 tun = L.tuning
                 if tun.ahead_depth is not None:
                     self.driver.set_ahead_depth(int(tun.ahead_depth))
-                if tun.span_burst is not None:
-                    self.driver.set_span_burst(int(tun.span_burst))
                 self.driver.set_group_bytes(int(tun.group_mib) << 20)
                 # var-len / JSON device decode: the launches of the groups decoded ahead go through the
                 # HIP command queue (csrc/hip/hip_queue.h; config 4 +9 %); fixed-width decode keeps
@@ -347,7 +345,7 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
             can also be passed as a keyword argument, which overrides the config; the performance
             knobs (``slots_per_worker``, ``slot_bytes``, ``prefetch``, ``copy_streams``,
             ``event_every``, ``coalesce``, ``coalesce_wait_us``, ``lockstep_depth``, ``numa_bind``,
-            ``ahead_depth``, ``decode_streams``, ``span_burst``, ``worker_spin_us``, ``json_count``, ...) form its
+            ``ahead_depth``, ``decode_streams``, ``worker_spin_us``, ``json_count``, ...) form its
             :class:`~torchkafka_amd.config.Tuning` (docs/CONFIG.md).  Options:
         normalize: optional ``(mean, std)`` fused into the collate kernel.
         sharding: ``"static"`` rank/worker partition map (default) or ``"group"`` (Kafka group assignment).
