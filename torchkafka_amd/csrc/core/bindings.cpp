@@ -88,7 +88,7 @@ PYBIND11_MODULE(_tkcore, m) {
       "crc32c_span_emulate",
       [](py::bytes b, uint32_t c0, uint32_t c1, bool first) {
         std::string s = b;
-        if (c0 > c1 || c1 > s.size() || span_windows(c1) > 16)
+        if (c0 > c1 || c1 > s.size() || span_windows(c1) > 32)
           throw std::invalid_argument("crc32c_span_emulate: bad range");
         return crc32c_span_emulate(reinterpret_cast<const uint8_t*>(s.data()), c0, c1, first);
       },

@@ -31,9 +31,9 @@ constexpr uint32_t kSpanMaxSegRows = 2048;
 // (Kafka's batch.size default is 16 KiB; config 2's 64 x 1 KiB records are 66 KB) are verified
 // on the device alone; longer ones are split and their partial CRCs chained by the driver.
 //
-// The kernels never hold a whole segment: they stream it through two LDS windows of kSpanWin bytes
-// (span_device.h), staging window k+1 while they check and decode window k, so a workgroup needs
-// ~45 KiB of LDS and fits on a CU beside a training job's GEMM tiles (benchmarks/compute_overlap.py).
+// The kernels never hold a whole segment: they stream it through a ring of 2-3 LDS windows of
+// kSpanWin bytes (span_device.h) -- a loader wave keeps the next windows in flight while eight
+// compute waves check and decode the current one -- so a workgroup needs 39-47 KiB of LDS.
 //
 // CRC32C on the device: a segment's CRC range [c0, c1) is cut into windows of kSpanWin bytes
 // ENDING at c1 (the first window reaches below the segment; bytes below c0 count as zeros, which
@@ -43,14 +43,15 @@ constexpr uint32_t kSpanMaxSegRows = 2048;
 // "shift by kSpanWin - kSpanPiece zero bytes" operator (kSpanTabGap).  After the last window lane t
 // holds the CRC of its bytes followed by zeros up to the end of its last piece, and a
 // log2(kSpanLanes)-level tree merges neighbours with "shift by 2^j pieces" operators.  kSpanPiece is
-// 60 bytes (15 dwords): an odd dword count puts the 32 lanes of a ds_read_b32 group on 32 different
-// LDS banks.  Host mirror: crc32c_span_emulate (csrc/core/crc32c.cpp).
-constexpr uint32_t kSpanPiece = 60;
-constexpr uint32_t kSpanLanes = 256;
-constexpr uint32_t kSpanWin = kSpanPiece * kSpanLanes;  // 15,360 bytes
-constexpr uint32_t kSpanLevels = 8;
+// 20 bytes (5 dwords): an odd dword count puts the 32 lanes of a ds_read_b32 group on 32 different
+// LDS banks; 4 + 2 x 8 bytes per lane per window, 512 lanes (8 compute waves, two per SIMD: one
+// hides the other's LDS latency).  Host mirror: crc32c_span_emulate (csrc/core/crc32c.cpp).
+constexpr uint32_t kSpanPiece = 20;
+constexpr uint32_t kSpanLanes = 512;
+constexpr uint32_t kSpanWin = kSpanPiece * kSpanLanes;  // 10,240 bytes
+constexpr uint32_t kSpanLevels = 9;
 constexpr uint32_t kSpanMaxWins = (kSpanSegMax + kSpanWin - 1) / kSpanWin;
-static_assert(kSpanMaxWins <= 16, "window tables hold 16 entries");
+static_assert(kSpanMaxWins <= 32, "window tables hold 32 entries");
 // Windows of a segment of `len` bytes (>= 1).
 inline constexpr uint32_t span_windows(uint32_t len) { return len == 0 ? 1u : (len + kSpanWin - 1) / kSpanWin; }
 
@@ -84,9 +85,13 @@ struct SpanWindows {
   }
 };
 // LDS bytes of one window buffer: 16 before the staged bytes (reads start at most 10 below them),
-// at most kSpanWin + 96 staged, 32 after (a 16-byte read of the slot past the last one).
+// the loader wave's kSpanWinLoads KiB-wide LDS-DMA instructions (at most kSpanWin + 96 bytes of them
+// staged; the lanes past the end repeat the last chunk into their own slot: every window costs the
+// same instruction count, so the loader can wait with a counted vmcnt), 32 after (a 16-byte read
+// of the slot past the last one).
 constexpr int32_t kSpanWinPad = 16;
-constexpr int32_t kSpanWinBytes = kSpanWinPad + int32_t(kSpanWin) + 96 + 32;
+constexpr int32_t kSpanWinLoads = (int32_t(kSpanWin) + 96 + 1023) / 1024;
+constexpr int32_t kSpanWinBytes = kSpanWinPad + 1024 * kSpanWinLoads + 32;
 
 // Device table layout (uint32 words): slice-by-8 byte tables T0..T7; for level j and byte k of the
 // value, shift-by-(kSpanPiece << j)-bytes of (b << 8k); the nibble split of T0..T7 the kernels keep

@@ -31,9 +31,11 @@ namespace tkh {
 
 namespace {
 
+using span::kBlock;
 using span::kFront;
 using span::kThreads;
 using span::kWinBytes;
+constexpr int kBufs = 2;  // LDS windows per workgroup (1 in flight; the row tables take the rest)
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxRows = int(tk::kJsonSpanMaxSegRows);
 constexpr int kRowsPerThread = kMaxRows / kThreads;
@@ -122,8 +124,8 @@ __device__ int32_t scan_row(Load&& load, Byte&& byte, int32_t T, int lane, int32
   return commas + 1;
 }
 
-__global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a) {
-  __shared__ __attribute__((aligned(16))) uint8_t bufs[2][kWinBytes];
+__global__ __launch_bounds__(kBlock) void json_stage_kernel(JsonStageLaunch a) {
+  __shared__ __attribute__((aligned(16))) uint8_t bufs[kBufs][kWinBytes];
   __shared__ int32_t rel[kMaxRows];
   __shared__ int32_t tln[kMaxRows];
   __shared__ uint32_t dst[kMaxRows];
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
   const int32_t lo_b = kFront + head, hi_b = lo_b + int32_t(len);
   const span::Windows W(lo_b, hi_b);
 
-  const uint32_t crc = span::pipeline(
+  const uint32_t crc = span::pipeline<kBufs>(
       sg.src, W, bufs, tab, a.tabs, lo_b + ((flags & tk::kSegCrcFirst) ? 21 : 0), do_crc,
       (flags & tk::kSegCrcFirst) != 0,
       [&] {  // setup: the row table (image bytes, text lengths; -2: the row disagrees with the segment)
@@ -183,12 +185,14 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
         if (t == 0) bad = 0;
       },
       [&] {  // prepare: place the rows (exclusive scan of the 16-byte-rounded text lengths, thread t
-             // holding rows t * kRowsPerThread ..), write their descriptors, find their windows
+             // holding rows t * kRowsPerThread ..), write their descriptors, find their windows.  The
+             // loader wave's threads only meet the barrier.
+        const bool cw = t < kThreads;
         uint32_t sz[kRowsPerThread], local = 0;
 #pragma unroll
         for (int i = 0; i < kRowsPerThread; ++i) {
           const int32_t r = t * kRowsPerThread + i;
-          sz[i] = r < nrows && tln[r] >= 0 ? align16(uint32_t(tln[r])) : 0u;
+          sz[i] = cw && r < nrows && tln[r] >= 0 ? align16(uint32_t(tln[r])) : 0u;
           local += sz[i];
         }
         uint32_t incl = local;
@@ -197,8 +201,9 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
           const uint32_t u = __shfl_up(incl, o, 64);
           if (lane >= o) incl += u;
         }
-        if (lane == 63) wsum[wv] = incl;
+        if (cw && lane == 63) wsum[wv] = incl;
         __syncthreads();
+        if (!cw) return;
         uint32_t off = sg.stage_off + incl - local;
         for (int w = 0; w < wv; ++w) off += wsum[w];
 #pragma unroll
@@ -231,8 +236,8 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
         const int32_t ra = rw.lo[k], rb = rw.hi[k];
         if (ra >= rb) return;
         const int32_t own_lo = W.own_lo(k), own_hi = W.own_hi(k);
-        span::for_window_units(
-            ra, rb,
+        span::for_rows(
+            ra, rb, false,
             [&](int32_t rr, int32_t* ulo, int32_t* uhi) {
               const int32_t T = tln[rr], r0 = rel[rr];
               *ulo = span::unit_from(r0, own_lo);
@@ -240,12 +245,12 @@ __global__ __launch_bounds__(kThreads) void json_stage_kernel(JsonStageLaunch a)
             },
             [&](int32_t rr, int32_t u) {
               *reinterpret_cast<uint4*>(bo.stage + dst[rr] + 16u * uint32_t(u)) =
-                  span::lds16(reinterpret_cast<const uint4*>(buf), rel[rr] + 16 * u + off);
+                  span::lds16_row(reinterpret_cast<const uint4*>(buf), rel[rr] + 16 * u + off);
             });
       });
 
   if (do_crc) {
-    const uint32_t* shift_set = span::crc_merge(a.tabs, crc, wcrc);
+    const uint32_t* shift_set = t < kThreads ? span::crc_merge(a.tabs, crc, wcrc) : nullptr;
     __syncthreads();
     if (t == 0) span::crc_verdict(shift_set, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials);
   }
@@ -318,7 +323,7 @@ void launch_json_stage(const JsonStageLaunch& a, hipStream_t stream) {
         a.b[s.batch].desc == nullptr || (s.stage_off & 15u) != 0)
       throw std::invalid_argument("json stage: malformed segment");
   }
-  hipLaunchKernelGGL(json_stage_kernel, dim3(unsigned(a.n_seg)), dim3(kThreads), 0, stream, a);
+  hipLaunchKernelGGL(json_stage_kernel, dim3(unsigned(a.n_seg)), dim3(kBlock), 0, stream, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("json stage launch: ") + hipGetErrorString(e));
 }

@@ -6,15 +6,15 @@
 // then `_process` and torch.stack (kafka_dataset.py:156-162) -- and, in this
 // framework's host path, the worker's CRC pass and value copy into the ring slot.
 //
-// One 256-thread workgroup per segment, streamed through two 15 KiB LDS windows (span_device.h:
-// window k+1 is staged while window k is checked and decoded; ~45 KiB of LDS, so a decode
-// workgroup fits on a CU beside a training job's GEMM tiles).  In each window
-//   values: the 16-byte groups that START in the window's bytes -- a chunk of 64 groups of a row
-//   per wave, or (row, group) pairs strided over the block for rows of < 32 groups; each group is
-//   read as two aligned 16-byte LDS reads cut to the group's bytes (span::lds16: values sit at
-//   arbitrary byte offsets behind their varint headers), converted (dtypes.h: bit-exact with
-//   Tensor.to), stored 8-16 B per lane;
-//   CRC32C: every lane folds its 60-byte piece into its running state (span::crc_piece).
+// One workgroup per segment -- 8 compute waves and a loader wave -- streamed through a ring of 3
+// LDS windows of 10 KiB (span_device.h: the loader wave keeps 2 windows in flight while the compute
+// waves check and decode one; 46 KiB of LDS).  In each window
+//   values: the 16-byte groups that START in the window's bytes -- a wave per row, its lanes over
+//   the row's groups (all waves on rows of > 128 groups), or (row, group) pairs strided over
+//   the block for rows of < 32 groups; each group is read as two aligned 16-byte LDS reads cut to
+//   the group's bytes (span::lds16_row: values sit at arbitrary byte offsets behind their varint
+//   headers), converted (dtypes.h: bit-exact with Tensor.to), stored 8-16 B per lane;
+//   CRC32C: every lane folds its 20-byte piece into its running state (span::crc_piece).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -29,9 +29,11 @@ namespace tkh {
 
 namespace {
 
+using span::kBlock;
 using span::kFront;
 using span::kThreads;
 using span::kWinBytes;
+constexpr int kBufs = 3;  // LDS windows per workgroup (2 in flight)
 
 template <typename S>
 __device__ __forceinline__ S lds_elem(const uint32_t* b32, int32_t b) {
@@ -52,11 +54,11 @@ __device__ __forceinline__ S lds_elem(const uint32_t* b32, int32_t b) {
 }
 
 template <typename S, typename D, bool AFFINE>
-__global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, const float* __restrict__ shift,
+__global__ __launch_bounds__(kBlock) void span_decode_kernel(SpanLaunch a, const float* __restrict__ shift,
                                                                const float* __restrict__ scale) {
   using C = Conv<S, D, IsIntDst<D>::value>;
   constexpr int kPer = 16 / int(sizeof(S));  // source elements per 16-byte group
-  __shared__ __attribute__((aligned(16))) uint8_t bufs[2][kWinBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t bufs[kBufs][kWinBytes];
   __shared__ int32_t rel[tk::kSpanMaxSegRows];
   __shared__ __attribute__((aligned(256))) uint32_t tab[span::kNibLdsWords];
   __shared__ span::RowWins rw;
@@ -78,7 +80,9 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
   D* __restrict__ out = static_cast<D*>(bo.out);
 
   // group gi of row rr, when its key (first byte in the segment) lies in [own_lo, own_hi)
-  auto group = [&](const uint8_t* buf, int32_t off, int32_t own_lo, int32_t own_hi, int32_t rr, int32_t gi) {
+  // row_wave: every lane of the wave is on row rr (lds16_row's uniform alignment)
+  auto group = [&](const uint8_t* buf, int32_t off, int32_t own_lo, int32_t own_hi, int32_t rr, int32_t gi,
+                   bool row_wave) {
     const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
     const int32_t e0 = gi * kPer;
     const int32_t b0 = rel[rr] + e0 * int32_t(sizeof(S));
@@ -89,7 +93,8 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
     if (key < own_lo || key >= own_hi) return;  // another window's
     D* __restrict__ orow = out + int64_t(row_begin + uint32_t(rr)) * RE;
     if (nel == kPer && b0 >= lo_b && b0 + 16 <= hi_b) {
-      const uint4 o = span::lds16(reinterpret_cast<const uint4*>(buf), b0 + off);
+      const uint4 o = row_wave ? span::lds16_row(reinterpret_cast<const uint4*>(buf), b0 + off)
+                               : span::lds16(reinterpret_cast<const uint4*>(buf), b0 + off);
       S sv[kPer];
       __builtin_memcpy(sv, &o, 16);
       Vec<D, kPer> ov;
@@ -120,15 +125,16 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
     }
   };
 
-  const uint32_t crc = span::pipeline(
+  const uint32_t crc = span::pipeline<kBufs>(
       sg.src, W, bufs, tab, a.tabs, lo_b + ((flags & tk::kSegCrcFirst) ? 21 : 0), do_crc,
       (flags & tk::kSegCrcFirst) != 0,
-      [&] {  // setup: row positions (image bytes) and the window table, behind window 0's loads
+      [&] {  // setup: row positions (image bytes) and the window table, behind the first windows' loads
         const int64_t base = int64_t(sg.log_pos) - int64_t(head) - kFront;  // log position of image byte 0
         for (int32_t r = t; r < nrows; r += kThreads) rel[r] = int32_t(int64_t(bo.row_pos[row_begin + uint32_t(r)]) - base);
         span::row_wins_init(rw, W.nw);
       },
       [&] {  // prepare: the windows each row's groups start in; the record fields beside the values
+        if (t >= kThreads) return;
         for (int32_t r0w = 0; r0w < nrows; r0w += kThreads) {
           const int32_t r = r0w + t;
           const int32_t r0 = r < nrows ? rel[r] : 0;
@@ -144,27 +150,27 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
         if (ra >= rb) return;
         const int32_t own_lo = W.own_lo(k), own_hi = W.own_hi(k);
         if (G >= 32) {
-          span::for_window_units(
-              ra, rb,
+          span::for_rows(
+              ra, rb, G > 128,
               [&](int32_t rr, int32_t* ulo, int32_t* uhi) {
                 const int32_t r0 = rel[rr];
                 // k == 0 also owns the group cut by the segment's start (its key is lo_b)
                 *ulo = k == 0 ? (r0 >= lo_b ? 0 : (lo_b - r0) >> 4) : span::unit_from(r0, own_lo);
                 *uhi = min(G, span::unit_from(r0, own_hi));
               },
-              [&](int32_t rr, int32_t gi) { group(buf, off, own_lo, own_hi, rr, gi); });
+              [&](int32_t rr, int32_t gi) { group(buf, off, own_lo, own_hi, rr, gi, true); });
         } else {
           const int32_t total = (rb - ra) * G;
           for (int32_t p = t; p < total; p += kThreads) {
             const int32_t q = p / G;
-            group(buf, off, own_lo, own_hi, ra + q, p - q * G);
+            group(buf, off, own_lo, own_hi, ra + q, p - q * G, false);
           }
         }
       });
 
   // ---- verdict: merge the lanes; thread 0 compares (or leaves the partial for the driver)
   if (do_crc) {
-    const uint32_t* shift_set = span::crc_merge(a.tabs, crc, wcrc);
+    const uint32_t* shift_set = t < kThreads ? span::crc_merge(a.tabs, crc, wcrc) : nullptr;
     __syncthreads();
     if (t == 0) span::crc_verdict(shift_set, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials);
   }
@@ -174,11 +180,11 @@ __global__ __launch_bounds__(kThreads) void span_decode_kernel(SpanLaunch a, con
 // converted in 16-byte units by the window its unit starts in; padding, mask and lengths written
 // before the windows (they need only the row table).
 template <typename S, typename D>
-__global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, D pad) {
+__global__ __launch_bounds__(kBlock) void varlen_span_kernel(VarSpanLaunch a, D pad) {
   using C = Conv<S, D, IsIntDst<D>::value>;
   constexpr int kWaves = kThreads / 64;
   constexpr int kPer = 16 / int(sizeof(S));
-  __shared__ __attribute__((aligned(16))) uint8_t bufs[2][kWinBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t bufs[kBufs][kWinBytes];
   __shared__ int32_t rel[tk::kJsonSpanMaxSegRows];
   __shared__ int32_t nout[tk::kJsonSpanMaxSegRows];  // elements to convert (-1: a worker-copied row)
   __shared__ __attribute__((aligned(256))) uint32_t tab[span::kNibLdsWords];
@@ -206,6 +212,7 @@ __global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, 
 
   if (flags & tk::kSegHostRows) {
     // rows the worker copied into the slot (longer than one segment): a wave per row
+    if (wv >= kWaves) return;  // the loader wave has nothing to stage here
     for (int32_t rr = wv; rr < nrows; rr += kWaves) {
       const int64_t row = int64_t(row_begin) + rr;
       const tk::JsonSpanRow d = bo.rows[row];
@@ -226,7 +233,7 @@ __global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, 
   const int32_t lo_b = kFront + head, hi_b = lo_b + int32_t(len);
   const span::Windows W(lo_b, hi_b);
 
-  const uint32_t crc = span::pipeline(
+  const uint32_t crc = span::pipeline<kBufs>(
       sg.src, W, bufs, tab, a.tabs, lo_b + ((flags & tk::kSegCrcFirst) ? 21 : 0), do_crc,
       (flags & tk::kSegCrcFirst) != 0,
       [&] {  // setup: the row table (image bytes, elements to convert)
@@ -248,6 +255,7 @@ __global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, 
         if (t == 0) bad = 0;
       },
       [&] {  // prepare: padding, mask and lengths of every row; the windows its units start in
+        if (t >= kThreads) return;
         for (int32_t rr = wv; rr < nrows; rr += kWaves) {
           const int32_t n = nout[rr];
           if (n == -1) continue;  // copied by the worker (its kSegHostRows block writes it)
@@ -268,8 +276,8 @@ __global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, 
         if (ra >= rb) return;
         const int32_t own_lo = W.own_lo(k), own_hi = W.own_hi(k);
         const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
-        span::for_window_units(
-            ra, rb,
+        span::for_rows(
+            ra, rb, false,
             [&](int32_t rr, int32_t* ulo, int32_t* uhi) {
               const int32_t n = nout[rr], r0 = rel[rr];
               const int32_t units = n > 0 ? (n + kPer - 1) / kPer : 0;
@@ -283,7 +291,7 @@ __global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, 
               if (bo.reserved && e0 + kPer <= n) {
                 // 16 source bytes (span::lds16: values sit at any byte offset behind their headers),
                 // a vector store (the row starts 16-byte aligned)
-                const uint4 o = span::lds16(reinterpret_cast<const uint4*>(buf), b0);
+                const uint4 o = span::lds16_row(reinterpret_cast<const uint4*>(buf), b0);
                 S sv[kPer];
                 __builtin_memcpy(sv, &o, 16);
                 Vec<D, kPer> ov;
@@ -298,7 +306,7 @@ __global__ __launch_bounds__(kThreads) void varlen_span_kernel(VarSpanLaunch a, 
       });
 
   if (do_crc) {
-    const uint32_t* shift_set = span::crc_merge(a.tabs, crc, wcrc);
+    const uint32_t* shift_set = t < kThreads ? span::crc_merge(a.tabs, crc, wcrc) : nullptr;
     __syncthreads();
     if (t == 0) span::crc_verdict(shift_set, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials);
   }
@@ -309,7 +317,7 @@ template <typename S, typename D>
 void launch_var_span_t(const VarSpanLaunch& a, double pad, hipStream_t stream) {
   D padv;
   if constexpr (IsIntDst<D>::value) padv = D(int64_t(pad)); else padv = Store<D>::cvt(float(pad));
-  hipLaunchKernelGGL((varlen_span_kernel<S, D>), dim3(unsigned(a.n_seg)), dim3(kThreads), 0, stream, a, padv);
+  hipLaunchKernelGGL((varlen_span_kernel<S, D>), dim3(unsigned(a.n_seg)), dim3(kBlock), 0, stream, a, padv);
 }
 
 template <typename S, typename D>
@@ -317,9 +325,9 @@ void launch_span_t(const SpanLaunch& a, const float* shift, const float* scale, 
   if (a.n_seg <= 0) return;
   const dim3 grid(unsigned(a.n_seg));
   if (shift)
-    hipLaunchKernelGGL((span_decode_kernel<S, D, true>), grid, dim3(kThreads), 0, stream, a, shift, scale);
+    hipLaunchKernelGGL((span_decode_kernel<S, D, true>), grid, dim3(kBlock), 0, stream, a, shift, scale);
   else
-    hipLaunchKernelGGL((span_decode_kernel<S, D, false>), grid, dim3(kThreads), 0, stream, a, shift, scale);
+    hipLaunchKernelGGL((span_decode_kernel<S, D, false>), grid, dim3(kBlock), 0, stream, a, shift, scale);
 }
 
 }  // namespace

@@ -1,22 +1,26 @@
 // Device code shared by the span kernels (span_decode.hip: fixed-width and var-len values,
-// json_span.hip: JSON text): one 256-thread workgroup per log segment (<= 128 KiB of one partition
-// log, pinned host memory or its HBM mirror), streamed through TWO LDS windows:
+// json_span.hip: JSON text): one workgroup per log segment (<= 128 KiB of one partition log, pinned
+// host memory or its HBM mirror), streamed through a ring of NB LDS windows of 10 KiB:
 //
-//   window k = segment bytes [w0 + k W, w0 + (k+1) W), W = kSpanWin (15,360), the windows ending at
-//   the segment's end (span.h).  Window k+1 is staged by LDS-DMA (global_load_lds_dwordx4, every
-//   lane of a wave one 16-byte chunk of a contiguous KiB) while the workgroup checks and decodes
-//   window k out of the other buffer:
-//     * CRC32C: lane t folds its 60-byte piece of the window into a running state (slice-by-8 fed by
+//   window k = segment bytes [w0 + k W, w0 + (k+1) W), W = kSpanWin (10,240), the windows ending at
+//   the segment's end (span.h SpanWindows).  The workgroup is 8 compute waves (512 threads: the CRC
+//   lanes; two waves per SIMD, so one hides the other's LDS latency) and ONE loader wave.  The loader wave only issues LDS-DMA loads (global_load_lds_dwordx4, a
+//   contiguous KiB per instruction, kSpanWinLoads of them per window) and keeps NB - 1 windows in
+//   flight; since nothing else is on its vector-memory counter it waits for the oldest window with a
+//   counted s_waitcnt vmcnt (the compute waves' stores would make a count meaningless, and a
+//   vmcnt(0) would drain the windows behind it).  One raw s_barrier per window hands window k to the
+//   compute waves and hands them window k-1's buffer back.  The compute waves, per window:
+//     * the values / texts whose 16-byte group (or piece) STARTS in the window's bytes (staged with
+//       16 bytes before and 48 after, so a group reaching past the window is whole in LDS): a wave
+//       per row, its lanes over the row's groups (a row's groups share one alignment, so the 16
+//       bytes of a group are cut out of two aligned ds_read_b128 with wave-uniform selects);
+//     * CRC32C: lane t folds its 20-byte piece of the window into a running state (slice-by-8 fed by
 //       a sliding dword window, looked up per NIBBLE in 16-entry LDS rows: conflict-free), the state
 //       crossing the other lanes' bytes with one gap operator between windows; after the last
-//       window 6 shuffle levels and 2 LDS levels of "shift by 2^j pieces" merge the lanes
-//       (span.h, host mirror csrc/core/crc32c.cpp crc32c_span_emulate);
-//     * the values / texts whose 16-byte group (or piece) STARTS in the window's bytes of the
-//       segment (staged with 16 bytes before and 48 after, so a group reaching past the window is
-//       whole in LDS).
-//   A workgroup needs ~45 KiB of LDS instead of the whole segment's 143 KiB: it lands on a CU beside
-//   a training job's GEMM tiles (a hipBLASLt 256x256 tile holds 65 KiB) instead of waiting for the
-//   GEMM to end, and its staging overlaps its compute.
+//       window 6 shuffle levels and 3 LDS levels of "shift by 2^j pieces" merge the lanes
+//       (span.h, host mirror csrc/core/crc32c.cpp crc32c_span_emulate).
+//   A workgroup needs 39-47 KiB of LDS (round 4: the whole 143 KiB segment) and its loads are always
+//   NB - 1 windows ahead of its compute, so it holds a CU for a fraction of the time it used to.
 //
 // A RecordBatch held whole by the segment is compared with its header CRC -- a mismatch stores the
 // segment index into the batch's host-mapped error word (the driver reads it when the slot is
@@ -33,13 +37,18 @@
 namespace tkh {
 namespace span {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = int(tk::kSpanLanes);  // compute threads: 8 waves, one CRC lane each
+constexpr int kBlock = kThreads + 64;      // + the loader wave
 constexpr int kFront = 16;     // image coordinates: segment byte i is image byte kFront + (src & 15) + i
 constexpr int32_t kWin = int32_t(tk::kSpanWin);
 constexpr int kPad = tk::kSpanWinPad;          // LDS bytes before a window's first staged byte
 constexpr int kWinBytes = tk::kSpanWinBytes;    // one window buffer (span.h)
-constexpr int kWinLoads = (kWin + 96 + 16 * kThreads - 1) / (16 * kThreads);  // LDS-DMA rounds per window
+constexpr int kWinLoads = tk::kSpanWinLoads;    // the loader wave's LDS-DMA instructions per window
 static_assert(kWinBytes % 16 == 0, "window buffers stay 16-byte aligned");
+static_assert(kWinLoads <= 21, "counted waits: at most 3 windows of loads in flight (vmcnt <= 63)");
+static_assert(kThreads == 512, "crc_merge / crc_verdict: 8 compute waves");
+
+__device__ __forceinline__ bool loader_wave() { return threadIdx.x >= kThreads; }
 
 // 16 bytes at LDS byte b0 of a 16-byte aligned image (any alignment of b0), for loops whose
 // lanes read consecutive 16-byte pieces: two 16-byte-aligned ds_read_b128 per lane -- consecutive
@@ -70,6 +79,31 @@ __device__ __forceinline__ uint4 lds16(const uint4* img16, int32_t b0) {
   return v;
 }
 
+// span::lds16 for a whole wave reading the same row: the lanes' groups share one alignment
+// (b0 mod 16), so the dword selects are one wave-uniform branch instead of 15 v_cndmask per lane.
+__device__ __forceinline__ uint4 lds16_row(const uint4* img16, int32_t b0) {
+  const lds_v4u* img = reinterpret_cast<const lds_v4u*>(img16);
+  const int32_t a = __builtin_amdgcn_readfirstlane(b0 & 15), q = a >> 2, sh = a & 3;
+  const lds_v4u lv = __builtin_nontemporal_load(img + (b0 >> 4));
+  const lds_v4u hv = __builtin_nontemporal_load(img + (b0 >> 4) + 1);
+  uint32_t d[5];
+  if (q == 0) {
+    d[0] = lv.x, d[1] = lv.y, d[2] = lv.z, d[3] = lv.w, d[4] = hv.x;
+  } else if (q == 1) {
+    d[0] = lv.y, d[1] = lv.z, d[2] = lv.w, d[3] = hv.x, d[4] = hv.y;
+  } else if (q == 2) {
+    d[0] = lv.z, d[1] = lv.w, d[2] = hv.x, d[3] = hv.y, d[4] = hv.z;
+  } else {
+    d[0] = lv.w, d[1] = hv.x, d[2] = hv.y, d[3] = hv.z, d[4] = hv.w;
+  }
+  uint4 v;
+  v.x = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
+  v.y = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
+  v.z = __builtin_amdgcn_alignbyte(d[3], d[2], sh);
+  v.w = __builtin_amdgcn_alignbyte(d[4], d[3], sh);
+  return v;
+}
+
 __device__ __forceinline__ uint32_t keep_from(int32_t a, int32_t c) {
   // bytes of the dword at address a whose address is >= c
   const int32_t d = c - a;
@@ -83,37 +117,48 @@ __device__ __forceinline__ uint32_t shift_op(const uint32_t* __restrict__ set, u
 
 using Windows = tk::SpanWindows;  // span.h
 
-// Issues window k's LDS-DMA loads into `buf` (kWinBytes); `gbase` is the global address of image
-// byte kFront (the segment's first byte rounded down to 16).  LDS byte of image byte x:
-// kPad + x - stage_lo(k).  Round r of wave w writes chunks [r * 256 + 64 w, +64) -- one contiguous
-// KiB, the instruction's wave-uniform-base + 16 * lane layout -- with no VGPR staging.  The caller
-// completes them with s_waitcnt vmcnt(0) + a barrier.
-__device__ __forceinline__ void stage_window(const uint8_t* gbase, const Windows& W, int k, uint8_t* buf) {
-  const int t = int(threadIdx.x), wv = t >> 6;
+// The loader wave issues window k's LDS-DMA loads into `buf` (kWinBytes); `gbase` is the global
+// address of image byte kFront (the segment's first byte rounded down to 16).  LDS byte of image
+// byte x: kPad + x - stage_lo(k).  Instruction r writes chunks [64 r, 64 r + 64) -- one contiguous
+// KiB, the instruction's wave-uniform-base + 16 * lane layout -- with no VGPR staging; lanes past
+// the window's chunks reload its last chunk into their own slot (past the staged bytes), so every
+// window is exactly kWinLoads instructions.
+__device__ __forceinline__ void issue_window(const uint8_t* gbase, const Windows& W, int k, uint8_t* buf) {
+  const int lane = int(threadIdx.x) & 63;
   const int32_t a = W.stage_lo(k);
-  const uint32_t nchunk = uint32_t(W.stage_hi(k) - a) >> 4;
+  const int32_t last = ((W.stage_hi(k) - a) >> 4) - 1;
   const uint8_t* g = gbase + (a - kFront);
 #pragma unroll
   for (int r = 0; r < kWinLoads; ++r) {
-    if (uint32_t(r * kThreads) >= nchunk) break;  // block-uniform
-    const uint32_t c = uint32_t(t + r * kThreads);
-    if (c < nchunk)
-      __builtin_amdgcn_global_load_lds(g + 16u * c,
-                                       (__attribute__((address_space(3))) void*)(buf + kPad + 16 * (r * kThreads + wv * 64)),
-                                       16, 0, 0);
+    const int32_t c = min(r * 64 + lane, last);
+    __builtin_amdgcn_global_load_lds(g + 16 * c, (__attribute__((address_space(3))) void*)(buf + kPad + 1024 * r), 16,
+                                     0, 0);
   }
 }
 
-__device__ __forceinline__ void wait_window() {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+// The loader wave: every load older than the youngest `n` windows it issued has landed.
+__device__ __forceinline__ void loader_wait(int n) {
+  if (n <= 0)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (n == 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWinLoads) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kWinLoads) : "memory");
+}
+
+// A workgroup barrier that leaves the loader wave's loads in flight (a __syncthreads() fence waits
+// for every vector-memory operation): LDS operations completed, then s_barrier.
+__device__ __forceinline__ void window_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 // Row ranges per window: rows [lo[k], hi[k]) hold every group a window owns (rows in any order;
 // a row outside the range owns nothing there).  Each thread reports its row's first and last
 // owned key window (kf > kl: the row owns nothing); wave ballots keep one LDS atomic per window.
 struct RowWins {
-  int32_t lo[16], hi[16];
+  int32_t lo[32], hi[32];
 };
 __device__ __forceinline__ void row_wins_init(RowWins& rw, int nw) {
   const int t = int(threadIdx.x);
@@ -133,18 +178,19 @@ __device__ __forceinline__ void row_wins_add(RowWins& rw, int nw, int32_t row_ba
   }
 }
 
-// The 16-byte units a window owns, spread over the workgroup: rows [ra, rb) in order, each row's
-// owned units [ulo, uhi) (range(rr, &ulo, &uhi)) cut into chunks of 64 lanes, the chunks dealt to
-// the 4 waves round robin -- a wave per row for rows of up to 64 units, all four on a wide row.
+// The 16-byte units a window owns, spread over the compute waves: rows [ra, rb), each row's owned
+// units [ulo, uhi) (range(rr, &ulo, &uhi)) in chunks of 64 lanes.  A wave per row (rows strided
+// over the compute waves), or with `wide` all of them on every row (its chunks strided over them) --
+// for rows so long that a window holds only a few of them.  fn(rr, u, row_key0) runs with every lane
+// of the wave on the same row.
 template <class Range, class Fn>
-__device__ __forceinline__ void for_window_units(int32_t ra, int32_t rb, Range&& range, Fn&& fn) {
+__device__ __forceinline__ void for_rows(int32_t ra, int32_t rb, bool wide, Range&& range, Fn&& fn) {
   const int t = int(threadIdx.x), lane = t & 63, wv = t >> 6;
-  int ci = 0;
-  for (int32_t rr = ra; rr < rb; ++rr) {
+  const int32_t r_step = wide ? 1 : kThreads / 64, c_off = wide ? 64 * wv : 0, c_step = wide ? kThreads : 64;
+  for (int32_t rr = ra + (wide ? 0 : wv); rr < rb; rr += r_step) {
     int32_t ulo = 0, uhi = 0;
     range(rr, &ulo, &uhi);
-    for (int32_t u = ulo; u < uhi; u += 64, ++ci)
-      if ((ci & 3) == wv && u + lane < uhi) fn(rr, u + lane);
+    for (int32_t u = ulo + c_off + lane; u < uhi; u += c_step) fn(rr, u);
   }
 }
 // First unit of a row whose key (key0 + 16 u) is >= x.
@@ -157,7 +203,7 @@ constexpr int kNibRowWords = 64;
 constexpr int kNibLdsWords = 16 * kNibRowWords;
 using lds_u32 = __attribute__((address_space(3))) const uint32_t;
 
-__device__ __forceinline__ void load_nib_rows(uint32_t* tab, const uint32_t* __restrict__ tabs) {
+__device__ __forceinline__ void load_nib_rows(uint32_t* tab, const uint32_t* __restrict__ tabs) {  // compute threads
   for (int i = int(threadIdx.x); i < int(tk::kSpanTabNibWords); i += kThreads)
     tab[(i >> 4) * kNibRowWords + (i & 15)] = tabs[tk::kSpanTabNib + i];
   for (int i = int(threadIdx.x); i < int(tk::kSpanTabGapWords); i += kThreads)
@@ -191,10 +237,12 @@ __device__ __forceinline__ uint32_t gap_op(uint32_t nbase, uint32_t c) {
   return r;
 }
 
-// One lane's piece of window k folded into its running state `crc` (every thread, every window).
-// b32: the window's LDS bytes as dwords; `off` = LDS byte of image byte 0 (kPad - stage_lo(k));
-// c0: image byte of the first CRC'd byte ([lo + 21, hi) for the segment holding a RecordBatch's
-// start, else [lo, hi)); `first`: inject the 0xFFFFFFFF initial value into its first 4 bytes.
+// One lane's piece of window k folded into its running state `crc` (every compute thread, every
+// window).  b32: the window's LDS bytes as dwords; `off` = LDS byte of image byte 0 (kPad -
+// stage_lo(k)); c0: image byte of the first CRC'd byte ([lo + 21, hi) for the segment holding a
+// RecordBatch's start, else [lo, hi)); `first`: inject the 0xFFFFFFFF initial value into its first
+// 4 bytes.  A piece wholly past c0 + 4 takes the straight-line path (no masks); the few around c0
+// take the masked loop.
 __device__ __forceinline__ uint32_t crc_piece(const uint32_t* __restrict__ b32, uint32_t nbase, const Windows& W,
                                               int k, int32_t off, int32_t c0, bool first, uint32_t crc) {
   const int t = int(threadIdx.x);
@@ -203,24 +251,33 @@ __device__ __forceinline__ uint32_t crc_piece(const uint32_t* __restrict__ b32, 
   if (k > 0) crc = gap_op(nbase, crc);  // still zero before the first CRC'd byte
   const int32_t start = W.w0 + k * kWin + t * P + off;  // LDS byte of the piece
   const int32_t cl = c0 + off;                          // LDS byte of c0
-  if (start + 4 > cl) {
-    const int32_t w = start >> 2, sh = start & 3;
-    uint32_t x = __builtin_amdgcn_alignbyte(b32[w + 1], b32[w], sh);
-    if (start < cl + 4) {
-      const uint32_t keep = keep_from(start, cl);
-      x &= keep;
-      if (first) x ^= keep & ~keep_from(start, cl + 4);  // the 0xFFFFFFFF initial value
+  const int32_t sh = start & 3;                         // the same for every lane and window
+  int32_t w = start >> 2;
+  if (start >= cl + 4) {
+    uint32_t lo = b32[w + 1];
+    crc = nib_dword<3>(nbase, __builtin_amdgcn_alignbyte(lo, b32[w], sh) ^ crc);
+#pragma unroll
+    for (int32_t j = 0; j < nsteps; ++j) {
+      const uint32_t m1 = b32[w + 2 + 2 * j], m2 = b32[w + 3 + 2 * j];
+      const uint32_t x = __builtin_amdgcn_alignbyte(m1, lo, sh) ^ crc, y = __builtin_amdgcn_alignbyte(m2, m1, sh);
+      lo = m2;
+      crc = nib_dword<7>(nbase, x) ^ nib_dword<3>(nbase, y);
     }
+    return crc;
+  }
+  if (start + 4 > cl) {
+    uint32_t x = __builtin_amdgcn_alignbyte(b32[w + 1], b32[w], sh);
+    const uint32_t keep = keep_from(start, cl);
+    x &= keep;
+    if (first) x ^= keep & ~keep_from(start, cl + 4);  // the 0xFFFFFFFF initial value
     crc = nib_dword<3>(nbase, x ^ crc);
   }
   const int32_t a1 = start + 4;
   const int32_t j0 = a1 >= cl ? 0 : (cl - a1) >> 3;  // 8-byte groups wholly below c0 are skipped
   if (j0 < nsteps) {
     int32_t ad = a1 + 8 * j0;
-    int32_t w = ad >> 2;
-    const int32_t sh = ad & 3;
+    w = ad >> 2;
     uint32_t lo = b32[w];
-#pragma unroll 7
     for (int32_t j = j0; j < nsteps; ++j, ad += 8) {
       const uint32_t m1 = b32[w + 1], m2 = b32[w + 2];
       w += 2;
@@ -256,12 +313,15 @@ __device__ __forceinline__ const uint32_t* crc_merge(const uint32_t* __restrict_
   return shift_set;
 }
 
-// Thread 0 only, after a barrier that follows crc_merge.
+// Thread 0 only, after a barrier that follows crc_merge: 3 levels merge the 8 wave CRCs.
 __device__ __forceinline__ void crc_verdict(const uint32_t* __restrict__ shift_set, const uint32_t* wcrc,
                                             uint32_t flags, uint32_t want, uint32_t seg, int32_t* err,
                                             uint32_t* partials) {
-  uint32_t c = shift_op(shift_set, 6, wcrc[0]) ^ wcrc[1];
-  c = shift_op(shift_set, 7, c) ^ (shift_op(shift_set, 6, wcrc[2]) ^ wcrc[3]);
+  uint32_t c4[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c4[i] = shift_op(shift_set, 6, wcrc[2 * i]) ^ wcrc[2 * i + 1];
+  const uint32_t lo = shift_op(shift_set, 7, c4[0]) ^ c4[1], hi = shift_op(shift_set, 7, c4[2]) ^ c4[3];
+  const uint32_t c = shift_op(shift_set, 8, lo) ^ hi;
   constexpr uint32_t kWhole = tk::kSegCrcFirst | tk::kSegCrcLast;
   if ((flags & kWhole) == kWhole) {
     if ((c ^ 0xFFFFFFFFu) != want) *err = int32_t(seg);
@@ -270,32 +330,52 @@ __device__ __forceinline__ void crc_verdict(const uint32_t* __restrict__ shift_s
   }
 }
 
-// The pipeline every span kernel runs: stage window 0, run `setup` (row tables into LDS -- their
-// loads overlap window 0's), wait, run `prepare` (per-row work that needs the tables: row window
-// ranges, scans, descriptors), then for every window k: stage k+1 into the other buffer, `body(k,
-// buf, off)` (the window's values; off = LDS byte of image byte 0) and its CRC pieces.  Returns the
-// lane's CRC state (0 when the segment carries no CRC).
-template <class Setup, class Prepare, class Body>
+// The pipeline every span kernel runs (all kBlock threads call it).  The loader wave issues the
+// first NB - 1 windows; the compute threads meanwhile run `setup` (row tables into LDS); after a
+// barrier every thread runs `prepare` (per-row work that needs the tables: row window ranges,
+// scans, descriptors -- it may contain __syncthreads(); the loader wave's threads must do no work
+// in it), then for every window k:
+//   loader: wait until window k landed (counted vmcnt) -- barrier -- issue window k + NB - 1 into
+//           the buffer window k - 1 used;
+//   compute: barrier -- `body(k, buf, off)` (the window's values; off = LDS byte of image byte 0) --
+//           its CRC pieces.
+// Returns the lane's CRC state (0 when the segment carries no CRC, and on the loader wave).
+template <int NB, class Setup, class Prepare, class Body>
 __device__ __forceinline__ uint32_t pipeline(const uint8_t* src, const Windows& W, uint8_t (*bufs)[kWinBytes],
                                              uint32_t* tab, const uint32_t* __restrict__ tabs, int32_t c0,
                                              bool do_crc, bool first, Setup&& setup, Prepare&& prepare,
                                              Body&& body) {
+  static_assert(NB >= 2 && NB <= 4, "2..4 window buffers");
   const uint8_t* gbase = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(src) & ~uintptr_t(15));
-  stage_window(gbase, W, 0, bufs[0]);
-  if (do_crc) load_nib_rows(tab, tabs);
-  setup();
-  wait_window();
+  const bool loader = loader_wave();
+  if (loader) {
+    for (int k = 0; k < NB - 1 && k < W.nw; ++k) issue_window(gbase, W, k, bufs[k]);
+  } else {
+    if (do_crc) load_nib_rows(tab, tabs);
+    setup();
+  }
+  window_barrier();  // the row tables (the compute waves' LDS writes)
   prepare();
-  __syncthreads();
+  __syncthreads();  // (drains the loader's first windows: they were needed first anyway)
   const uint32_t nbase = uint32_t(uintptr_t((lds_u32*)tab));  // the LDS byte address
   uint32_t crc = 0;
   for (int k = 0; k < W.nw; ++k) {
-    if (k > 0) wait_window();  // window k landed; every thread is done with window k - 1's buffer
-    if (k + 1 < W.nw) stage_window(gbase, W, k + 1, bufs[(k + 1) & 1]);
-    uint8_t* buf = bufs[k & 1];
-    const int32_t off = kPad - W.stage_lo(k);
-    body(k, buf, off);  // stores first: they drain while the CRC runs
-    if (do_crc) crc = crc_piece(reinterpret_cast<const uint32_t*>(buf), nbase, W, k, off, c0, first, crc);
+    if (loader) {
+      // windows issued so far: up to min(k + NB - 2, nw - 1); all but those after k must have landed
+      loader_wait(min(k + NB - 2, W.nw - 1) - k);
+      window_barrier();
+      if (k + NB - 1 < W.nw) issue_window(gbase, W, k + NB - 1, bufs[(k + NB - 1) % NB]);
+    } else {
+      window_barrier();  // window k landed; every compute wave is done with window k - 1's buffer
+      uint8_t* buf = bufs[k % NB];
+      const int32_t off = kPad - W.stage_lo(k);
+#ifndef TKH_SPAN_PROBE_NO_BODY  // tools/probes/span_bench.hip builds variants without one stage
+      body(k, buf, off);  // stores first: they drain while the CRC runs
+#endif
+#ifndef TKH_SPAN_PROBE_NO_CRC
+      if (do_crc) crc = crc_piece(reinterpret_cast<const uint32_t*>(buf), nbase, W, k, off, c0, first, crc);
+#endif
+    }
   }
   return crc;
 }
