@@ -107,12 +107,13 @@ def parse():
     ap.add_argument("--steady-steps", type=int, default=None,
                     help="steps of the steady-state block timed after the headline (default: max(50 x ring "
                          "slots, 50000) on a GPU, 2000 on the CPU; 0 skips it)")
-    ap.add_argument("--extra-blocks", default="dma,f32,label,rccl,verify",
+    ap.add_argument("--extra-blocks", default="dma,f32,label,rccl,rccl_sync,verify",
                     help="comma list of secondary steady blocks, each a fresh loader over the same topic: dma "
                          "(h2d='dma', HBM mirror filled by SDMA), f32 (float32 output), label (the record key as "
                          "an int64 label beside the values: FixedWidth + Key()), rccl (the native RCCL lockstep "
-                         "forced at N = 1: the RCCL cost a one-GPU box shows), verify (the other --verify mode: "
-                         "steady_unverified or steady_verified); '' for none")
+                         "forced at N = 1: the RCCL cost a one-GPU box shows), rccl_sync (the same with "
+                         "commit='sync': one agreement per step after every commit -- the cross-rank barrier), "
+                         "verify (the other --verify mode: steady_unverified or steady_verified); '' for none")
     ap.add_argument("--extra-steps", type=int, default=None,
                     help="timed steps of each secondary block (default: the steady-state steps)")
     ap.add_argument("--self-launch", action="store_true",
@@ -513,7 +514,7 @@ def run_rank(args) -> int:
               else max(50 * ring_guess, 50000) if device.type == "cuda" else 2000)
     extra = [b for b in args.extra_blocks.split(",") if b]
     if device.type != "cuda":
-        extra = [b for b in extra if b not in ("dma", "rccl", "verify")]
+        extra = [b for b in extra if b not in ("dma", "rccl", "rccl_sync", "verify")]
     if world > 1:  # the main blocks run the lockstep already (RCCL on GPUs)
         extra = [b for b in extra if b != "rccl"]
     extra_steps = args.extra_steps if args.extra_steps is not None else steady
@@ -616,17 +617,23 @@ def run_rank(args) -> int:
     for name in extra:
         dt = torch.float32 if name == "f32" else dtypes[args.dtype]
         own_group = False
-        if name == "rccl" and not dist.is_initialized():
-            # a world-1 nccl group, lazily initialised: torch creates no RCCL communicator of its own;
-            # the loader's private one carries every agreement
+        rccl_block = name in ("rccl", "rccl_sync")
+        if rccl_block and not dist.is_initialized():
+            # a world-1 nccl group; one all-reduce on it makes torch's own RCCL communicator and its
+            # streams, as a DDP job's gradient all-reduce does at N > 1 -- the N = 8 queue layout,
+            # rehearsed on one GPU (the loader's private communicator carries every agreement)
             os.environ["MASTER_ADDR"] = "127.0.0.1"
             os.environ["MASTER_PORT"] = str(_free_port())
             dist.init_process_group("nccl", rank=0, world_size=1)
+            dist.all_reduce(torch.ones(1, device=device))
+            torch.cuda.synchronize(device)
+            os.environ["TORCHKAFKA_TORCH_NCCL_ACTIVE"] = "1"
             own_group = True
         ld = make_loader(f"bench-{name}", dt, "dma" if name == "dma" else args.h2d,
                          ds=Labelled if name == "label" else Records,
                          verify=other_verify if name == "verify" else None,
-                         lockstep_mode="always" if name == "rccl" else None)
+                         commit="sync" if name == "rccl_sync" else "async",
+                         lockstep_mode="always" if rccl_block and world == 1 else None)
         eit = iter(auto_commit(ld))
         for _ in range(extra_warm):
             next(eit)
@@ -640,11 +647,15 @@ def run_rank(args) -> int:
         blk["h2d"], blk["decode"] = describe(ld)
         blk["verify"] = ld.verify
         key = f"steady_{name}"
-        if name == "rccl":
+        if rccl_block:
             st = eres["stats"]
+            blk["commit"] = "sync (commit, then the agreement: a cross-rank barrier per step)" if name == "rccl_sync" \
+                else "async (commits land at agreements)"
+            blk["batches_per_commit"] = round(extra_steps / max(1, st["commits"]), 2)
             blk["lockstep"] = dict(ld.lockstep_info)
             blk["lockstep_agreements"] = st.get("lockstep_agreements", 0)
             blk["lockstep_wait_us_per_step"] = round(st.get("lockstep_wait_us_per_batch", 0.0), 3)
+            blk["lockstep_issue_us_per_step"] = round(st.get("lockstep_issue_us_per_batch", 0.0), 3)
             blk["lockstep_step_wait_max_us"] = round(st.get("lockstep_step_wait_max_us", 0.0), 1)
         if name == "verify":
             key = "steady_unverified" if ld.verify == "commit" else "steady_verified"
@@ -654,6 +665,7 @@ def run_rank(args) -> int:
         ld.close()
         if own_group:
             dist.destroy_process_group()
+            os.environ.pop("TORCHKAFKA_TORCH_NCCL_ACTIVE", None)
         if world > 1:
             R.barrier()
 
@@ -732,7 +744,10 @@ def run_rank(args) -> int:
                 "num_workers": args.workers,
                 "verify": ("deliver (a batch is handed out after its device CRC32C verdict)" if args.verify == "deliver"
                            else "commit (the CRC32C verdict gates the commit only)"),
-                "commit": "auto_commit per batch" + (
+                "commit": (f"auto_commit: {(s_stats or stats)['commits']} commits in "
+                           f"{steady if s_stats else args.steps} steps "
+                           f"({(steady if s_stats else args.steps) / max(1, (s_stats or stats)['commits']):.2f} "
+                           "batches per commit)") + (
                     "" if not lock_info else ", RCCL lockstep" if lock_info.get("transport") == "rccl"
                     else f", lockstep ({lock_info.get('backend', 'host')} all-reduce)"),
                 "h2d": h2d_desc,

@@ -147,18 +147,22 @@ def _sync_rank_main(rank, world, url, port, outdir):
                                                      auto_offset_reset="earliest", consumer_timeout_ms=400))
     want: dict[int, int] = {}   # end of every batch this rank finished, per partition
     checks, mismatches, steps = 0, [], 0
+    snapshots, wants = [], []   # every partition's committed offset when batch k+1 was yielded; want after k
     for batch in auto_commit(dl):
         if steps:
-            got = {p: o for p, o in b.committed_offsets("gs", "t").items() if p in want}
+            allc = b.committed_offsets("gs", "t")
+            snapshots.append({str(p): o for p, o in allc.items()})
+            got = {p: o for p, o in allc.items() if p in want}
             checks += 1
             if got != want:
                 mismatches.append((steps, got, dict(want)))
         for pidx, _first, nxt, _n in batch.watermarks:
             want[pidx] = max(want.get(pidx, 0), nxt)
+        wants.append({str(p): o for p, o in want.items()})
         steps += 1
     with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
-        json.dump({"steps": steps, "checks": checks, "mismatches": mismatches[:3],
-                   "commits": dl.stats.commits, "sync_commits": len(dl.stats.sync_commit_ns)}, f)
+        json.dump({"steps": steps, "checks": checks, "mismatches": mismatches[:3], "snapshots": snapshots,
+                   "wants": wants, "commits": dl.stats.commits, "sync_commits": len(dl.stats.sync_commit_ns)}, f)
     dist.destroy_process_group()
 
 
@@ -166,8 +170,8 @@ def _sync_rank_main(rank, world, url, port, outdir):
 def test_sync_commit_is_a_per_batch_barrier_across_ranks(broker, tmp_path, world):
     """commit='sync' at world > 1 (the reference's contract, auto_commit.py:55-58 /
     kafka_dataset.py:130, made a cross-rank barrier): on every rank, at the moment batch k+1 is
-    yielded, the group's committed offsets for that rank's partitions are exactly the end of
-    batch k -- including the steps before the rank with the least data runs dry."""
+    yielded, the group's committed offsets of EVERY rank's partitions are exactly the end of each
+    rank's batch k -- including the steps before the rank with the least data runs dry."""
     n_parts = 2 * world
     broker.create_topic("t", n_parts)
     per_rank = {r: 100 - 40 * (r == 0) for r in range(world)}  # rank 0 runs dry after 6 batches
@@ -176,9 +180,20 @@ def test_sync_commit_is_a_per_batch_barrier_across_ranks(broker, tmp_path, world
     tmp.spawn(_sync_rank_main, args=(world, broker.url, _free_port(), str(tmp_path)), nprocs=world, join=True)
     res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
     for r in res:
-        assert r["steps"] == 6, r
-        assert r["checks"] == 5 and r["mismatches"] == [], r
-        assert r["sync_commits"] >= r["steps"], r
+        assert r["steps"] == 6, {k: v for k, v in r.items() if k not in ("snapshots", "wants")}
+        assert r["checks"] == 5 and r["mismatches"] == [], r["mismatches"]
+        assert r["sync_commits"] >= r["steps"], r["sync_commits"]
+    # the cross-rank barrier: when rank r yielded batch k+1, every rank q had committed its batch k
+    # (at least: q may already have committed k+1 too -- never k+2, which needs r's next agreement)
+    bad = []
+    for r in res:
+        for k, snap in enumerate(r["snapshots"]):
+            for q in res:
+                for p, o in q["wants"][k].items():
+                    hi = q["wants"][k + 1][p] if k + 1 < len(q["wants"]) else o
+                    if snap.get(p) is None or not o <= snap[p] <= hi:
+                        bad.append((k + 1, p, snap.get(p), o, hi))
+    assert bad == [], bad[:5]
     committed = broker.committed_offsets("gs", "t")
     for r in range(world):
         assert committed[r] + committed[r + world] == 60

@@ -3,8 +3,9 @@ MI355X over a gloo group (the driver's CreditLockstep in sync mode; RCCL refuses
 device, so the RCCL transport is covered at world 1 in test_zz_gpu_rccl.py).
 
 The reference's contract (auto_commit.py:55-58, kafka_dataset.py:130): batch k's commit completes
-before batch k+1 is handed out.  Under DDP that commit is a barrier: at the moment batch k+1 is
-yielded on any rank, every rank's part of batch k is committed.
+before batch k+1 is handed out.  Under DDP that commit is a barrier: each rank commits k, then the
+agreement at step k+1 -- so at the moment batch k+1 is yielded on any rank, EVERY rank's part of
+batch k is committed (checked across the two ranks' records).
 """
 import json
 import os
@@ -52,19 +53,23 @@ def _rank_main(rank, world, url, port, outdir, verify):
                       worker_init_fn=Vec.init_worker("t", bootstrap_servers=url, group_id="gs",
                                                      auto_offset_reset="earliest", consumer_timeout_ms=500))
     want: dict = {}
-    steps, mismatches = 0, []
+    steps, mismatches, snapshots, wants = 0, [], [], []
     for x in auto_commit(dl):
         if steps:
-            got = {p: o for p, o in b.committed_offsets("gs", "t").items() if p in want}
+            allc = b.committed_offsets("gs", "t")
+            snapshots.append({str(p): o for p, o in allc.items()})
+            got = {p: o for p, o in allc.items() if p in want}
             if got != want:
                 mismatches.append((steps, got, dict(want)))
         for p, e in batch_ends(x).items():
             want[p] = max(want.get(p, 0), e)
+        wants.append({str(p): o for p, o in want.items()})
         steps += 1
     st = dl.stats_summary()
     dl.close()
     with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
-        json.dump({"steps": steps, "mismatches": mismatches[:3], "commits": st["commits"],
+        json.dump({"steps": steps, "mismatches": mismatches[:3], "snapshots": snapshots, "wants": wants,
+                   "commits": st["commits"],
                    "agreements": st["lockstep_agreements"], "lat_p99_us": st["commit_latency_p99_us"]}, f)
     dist.barrier()
     dist.destroy_process_group()
@@ -94,9 +99,20 @@ def test_sync_commit_barrier_two_ranks_one_gpu(broker, tmp_path, verify):
     res = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
     want_steps = (2 * 192) // 32
     for r in res:
-        assert r["steps"] == want_steps, r
-        assert r["mismatches"] == [], r
+        assert r["steps"] == want_steps, r["steps"]
+        assert r["mismatches"] == [], r["mismatches"]
         # every batch committed on its own (one commit per step, the last at the end)
-        assert r["commits"] >= want_steps - 1, r
+        assert r["commits"] >= want_steps - 1, r["commits"]
+    # the cross-rank barrier: when a rank yielded batch k+1, the OTHER rank had committed its batch k
+    # too (and possibly k+1, never k+2)
+    bad = []
+    for r in res:
+        for k, snap in enumerate(r["snapshots"]):
+            for q in res:
+                for p, o in q["wants"][k].items():
+                    hi = q["wants"][k + 1][p] if k + 1 < len(q["wants"]) else o
+                    if snap.get(p) is None or not o <= snap[p] <= hi:
+                        bad.append((k + 1, p, snap.get(p), o, hi))
+    assert bad == [], bad[:5]
     committed = broker.committed_offsets("gs", "t")
     assert committed[0] + committed[2] == 384 and committed[1] + committed[3] == 384, committed

@@ -61,7 +61,8 @@ class _Producer:
         return 1 if self.produced > before else 0
 
 
-def _rank_main(rank, world, port, outdir, totals, cap, depth, slow_rank, die_rank, sync=False):
+def _rank_main(rank, world, port, outdir, totals, cap, depth, slow_rank, die_rank, sync=False, shared=None,
+               fail_at=None):
     import torch
     import torch.distributed as dist
 
@@ -73,12 +74,12 @@ def _rank_main(rank, world, port, outdir, totals, cap, depth, slow_rank, die_ran
     # room for slow rank start-up under a loaded test machine (the store waits for rank 0)
     secs = 8 if die_rank >= 0 else 60
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=secs))
-    buf = torch.zeros(3, dtype=torch.int64)
+    buf = torch.zeros(4, dtype=torch.int64)
 
-    def allreduce_min(a, b, c):
-        buf[0], buf[1], buf[2] = a, b, c
+    def allreduce_min(a, b, c, d):
+        buf[0], buf[1], buf[2], buf[3] = a, b, c, d
         dist.all_reduce(buf, op=dist.ReduceOp.MIN)
-        return int(buf[0]), int(buf[1]), int(buf[2])
+        return tuple(int(v) for v in buf.tolist())
 
     c = core()
     lock = c.CreditLockstep(c.PyLockstepTransport(allreduce_min), depth)
@@ -87,12 +88,19 @@ def _rank_main(rank, world, port, outdir, totals, cap, depth, slow_rank, die_ran
     lock.set_on_committable(lambda wms: committed.extend(w[1] for w in wms))
     src = _Producer(totals[rank], cap, seed=1000 * rank + depth, slow=(rank == slow_rank))
     out = {"rank": rank, "error": None}
-    steps, prev, committed_at_deliver = 0, None, []
+    steps, prev, committed_at_deliver, group_at_deliver = 0, None, [], []
     try:
         while True:
             # the driver's order: asking for the next batch finishes the previous one first
             if prev is not None:
                 lock.finished(prev, [(rank, prev, prev + 1, 1)])
+                if sync:
+                    # the commit of `prev` (what the driver's _sync_commit does), published for the
+                    # other ranks to check, and its status for the agreement
+                    if shared is not None:
+                        shared[rank] = len(committed)
+                    if fail_at is not None and fail_at[0] == rank and prev == fail_at[1]:
+                        lock.set_commit_status(fail_at[2])
                 prev = None
             r = lock.next(src, 20)
             if r == -1:
@@ -106,6 +114,8 @@ def _rank_main(rank, world, port, outdir, totals, cap, depth, slow_rank, die_ran
             src.delivered += 1
             prev = idx
             committed_at_deliver.append(len(committed))
+            if shared is not None:
+                group_at_deliver.append(min(shared[:]))  # batches every rank committed when idx was handed out
             steps += 1
             if rank == die_rank and steps == 5:
                 os._exit(3)  # a crashed peer
@@ -115,7 +125,8 @@ def _rank_main(rank, world, port, outdir, totals, cap, depth, slow_rank, die_ran
     except Exception as e:  # noqa: BLE001 - reported to the parent
         out["error"] = f"{type(e).__name__}: {e}"
     out.update(steps=steps, committed=committed, committed_at_deliver=committed_at_deliver,
-               agreements=lock.agreements)
+               group_at_deliver=group_at_deliver, agreements=lock.agreements,
+               group_commit_failures=lock.group_commit_failures)
     with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
         json.dump(out, f)
     if out["error"] is None:
@@ -123,12 +134,14 @@ def _rank_main(rank, world, port, outdir, totals, cap, depth, slow_rank, die_ran
         dist.destroy_process_group()
 
 
-def _run(tmp_path, world, totals, cap=8, depth=2, slow_rank=-1, die_rank=-1, sync=False):
+def _run(tmp_path, world, totals, cap=8, depth=2, slow_rank=-1, die_rank=-1, sync=False, fail_at=None):
     # plain processes (not torch's spawn helper, which kills the others when one rank dies)
     port = _free_port()
     ctx = mp.get_context("spawn")
+    shared = ctx.Array("q", world, lock=False) if sync else None  # batches each rank committed
     procs = [ctx.Process(target=_rank_main,
-                         args=(r, world, port, str(tmp_path), totals, cap, depth, slow_rank, die_rank, sync))
+                         args=(r, world, port, str(tmp_path), totals, cap, depth, slow_rank, die_rank, sync,
+                               shared, fail_at))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -173,8 +186,9 @@ def test_credit_lockstep_stops_together_and_commits_only_finished(tmp_path, worl
 ])
 def test_sync_mode_commits_every_batch_before_the_next_is_delivered(tmp_path, world, totals, cap):
     """commit='sync' under the lockstep (the reference's per-batch commit, auto_commit.py:55-58,
-    as an RCCL barrier): when batch k+1 is handed out on any rank, batch k is committable on
-    every rank -- an agreement at step k+1 proved every rank finished it."""
+    as an RCCL barrier): each rank commits batch k, then the agreement at step k+1 -- so when batch
+    k+1 is handed out on ANY rank, EVERY rank has committed batches 0..k (checked against the
+    other ranks' published commit counts, not this rank's)."""
     res = _run(tmp_path, world, totals, cap=cap, depth=2, slow_rank=world - 1, sync=True)
     assert len(res) == world
     want = min(totals)
@@ -182,10 +196,30 @@ def test_sync_mode_commits_every_batch_before_the_next_is_delivered(tmp_path, wo
         assert r["error"] is None, r["error"]
         assert r["steps"] == want, (r["rank"], r["steps"], want)
         assert r["committed"] == list(range(want))
-        # exactly batches 0..k-1 committable at the moment batch k is delivered
+        # exactly batches 0..k-1 committed here at the moment batch k is delivered ...
         assert r["committed_at_deliver"] == list(range(want)), r["committed_at_deliver"]
+        # ... and on every other rank too
+        assert r["group_at_deliver"] == list(range(want)), r["group_at_deliver"]
         # one agreement per delivered step (plus starved rounds, the stop and the final barrier)
         assert r["agreements"] >= want
+        assert r["group_commit_failures"] == 0
+
+
+@pytest.mark.parametrize("status,world", [(0, 2), (0, 4), (1, 4)])
+def test_sync_mode_a_failed_commit_reaches_every_rank(tmp_path, status, world):
+    """A rank whose commit of batch 5 raised (status 0) makes EVERY rank stop with an error at the
+    agreement that would hand out batch 6; a swallowed CommitFailedError (status 1, the reference
+    logs it and continues, kafka_dataset.py:131-135) lets every rank continue, counted once."""
+    res = _run(tmp_path, world, [20] * world, cap=4, depth=2, sync=True, fail_at=(1, 5, status))
+    assert len(res) == world
+    for r in res:
+        if status == 0:
+            assert r["error"] is not None and "commit" in r["error"], r
+            assert r["steps"] == 6, r  # batches 0..5 handed out, 6 never
+        else:
+            assert r["error"] is None, r["error"]
+            assert r["steps"] == 20
+            assert r["group_commit_failures"] == 1
 
 
 def test_credit_lockstep_peer_death_fails_instead_of_hanging(tmp_path):

@@ -55,15 +55,23 @@ def test_rccl_lockstep_transport_failure_detection_plumbing():
     from torchkafka_amd.ops.native import hip
 
     lib = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
-    uid = hip().RcclLockstep.unique_id(lib)
-    ls = hip().RcclLockstep(lib, uid, 0, 1, 0, 3)
-    assert ls.timeout_ms == 600000
-    ls.set_timeout_ms(2000)
-    assert ls.timeout_ms == 2000
-    for i in range(10):
-        assert ls.allreduce_min(i, -i, 7) == (i, -i, 7)
-    assert not ls.aborted
-    del ls
+    # the agreement's four words reach RCCL through tiny copy kernels (default), as host-mapped
+    # buffers handed to RCCL itself, or by hipMemcpyAsync (A/B)
+    for mode in ("kernel", "host", "copy"):
+        os.environ["TORCHKAFKA_RCCL_WORDS"] = mode
+        try:
+            uid = hip().RcclLockstep.unique_id(lib)
+            ls = hip().RcclLockstep(lib, uid, 0, 1, 0, 3)
+        finally:
+            del os.environ["TORCHKAFKA_RCCL_WORDS"]
+        assert ls.words_mode == mode
+        assert ls.timeout_ms == 600000
+        ls.set_timeout_ms(2000)
+        assert ls.timeout_ms == 2000
+        for i in range(10):
+            assert ls.allreduce_min(i, -i, 7, 2 - i % 3) == (i, -i, 7, 2 - i % 3)
+        assert not ls.aborted
+        del ls
 
 
 def test_native_rccl_lockstep_sync_commit_world1(broker):

@@ -105,20 +105,20 @@ inline std::vector<RecordIn> to_records(const std::vector<py::object>& values, c
 class PyLockstepTransport : public LockstepTransport {
  public:
   explicit PyLockstepTransport(py::function fn) : fn_(std::move(fn)) {}
-  int issue(int64_t a, int64_t b, int64_t c) override {
-    py::tuple r = fn_(a, b, c);
+  int issue(const int64_t in[kLockstepWords]) override {
+    py::tuple r = fn_(in[0], in[1], in[2], in[3]);
     const int t = int(next_++ % 64);
-    for (int k = 0; k < 3; ++k) res_[t][k] = r[size_t(k)].cast<int64_t>();
+    for (int k = 0; k < kLockstepWords; ++k) res_[t][k] = r[size_t(k)].cast<int64_t>();
     return t;
   }
-  void wait(int t, int64_t out[3]) override {
-    for (int k = 0; k < 3; ++k) out[k] = res_[t][k];
+  void wait(int t, int64_t out[kLockstepWords]) override {
+    for (int k = 0; k < kLockstepWords; ++k) out[k] = res_[t][k];
   }
 
  private:
   py::function fn_;
   uint64_t next_ = 0;
-  int64_t res_[64][3];
+  int64_t res_[64][kLockstepWords];
 };
 
 // A rank's data path scripted in Python: an object with staged(), all_done(), wait_data(ms).

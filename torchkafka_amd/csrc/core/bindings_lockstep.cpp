@@ -8,7 +8,12 @@ void bind_lockstep(py::module_& m) {
   py::register_exception<LockstepError>(m, "LockstepError", PyExc_RuntimeError);
   py::class_<LockstepTransport>(m, "LockstepTransport", py::module_local());
   py::class_<PyLockstepTransport, LockstepTransport>(m, "PyLockstepTransport", py::module_local())
-      .def(py::init<py::function>(), py::arg("allreduce_min"));
+      .def(py::init<py::function>(), py::arg("allreduce_min"),
+           "allreduce_min(credit, step, -step, commit_status) -> the 4 words' MIN over the ranks");
+  m.attr("LOCKSTEP_WORDS") = kLockstepWords;
+  m.attr("COMMIT_OK") = kCommitOk;
+  m.attr("COMMIT_FAILED") = kCommitFailed;
+  m.attr("COMMIT_FATAL") = kCommitFatal;
   py::class_<CreditLockstep>(m, "CreditLockstep")
       .def(py::init<LockstepTransport*, int>(), py::arg("transport"), py::arg("depth"), py::keep_alive<1, 2>())
       .def(
@@ -31,6 +36,10 @@ void bind_lockstep(py::module_& m) {
           py::arg("index"), py::arg("watermarks"))
       .def("finish", &CreditLockstep::finish)
       .def("set_sync", &CreditLockstep::set_sync, py::arg("sync"))
+      .def("set_commit_status", &CreditLockstep::set_commit_status, py::arg("status"),
+           "sync mode: 2 committed, 1 CommitFailedError swallowed, 0 the commit raised")
+      .def_property_readonly("group_commit_status", &CreditLockstep::group_commit_status)
+      .def_property_readonly("group_commit_failures", &CreditLockstep::group_commit_failures)
       .def(
           "set_on_committable",
           [](CreditLockstep& l, py::function f) {

@@ -11,15 +11,18 @@ int64_t CreditLockstep::credit(LockstepSource& src) const {
 }
 
 void CreditLockstep::issue(LockstepSource& src) {
-  const int64_t v = credit(src);
-  tickets_.push_back(Ticket{step_, granted_, t_->issue(v, step_, -step_)});
+  const int64_t w[kLockstepWords] = {credit(src), step_, -step_, commit_status_};
+  commit_status_ = kCommitOk;
+  const auto t0 = std::chrono::steady_clock::now();
+  tickets_.push_back(Ticket{step_, granted_, t_->issue(w)});
+  issue_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
   ++agreements_;
 }
 
 void CreditLockstep::settle() {
   const Ticket t = tickets_.front();
   tickets_.pop_front();
-  int64_t res[3];
+  int64_t res[kLockstepWords];
   const auto w0 = std::chrono::steady_clock::now();
   t_->wait(t.ticket, res);
   const int64_t waited =
@@ -30,6 +33,11 @@ void CreditLockstep::settle() {
   if (res[1] != -res[2])
     throw LockstepError("lockstep: ranks are out of step (min " + std::to_string(res[1]) + ", max " +
                         std::to_string(-res[2]) + ")");
+  group_status_ = res[3];
+  if (res[3] == kCommitFailed) ++group_failures_;
+  if (res[3] <= kCommitFatal)
+    throw LockstepError("lockstep: a rank's commit before step " + std::to_string(t.step) +
+                        " failed; every rank stops at this step");
   while (!finished_q_.empty() && finished_q_.front().first < t.step) {
     emit(std::move(finished_q_.front().second));
     finished_q_.pop_front();
@@ -84,9 +92,16 @@ int CreditLockstep::next_impl(LockstepSource& src, int64_t timeout_ms) {
 
 void CreditLockstep::finish() {
   while (!tickets_.empty()) settle();  // every rank issued the same agreements
-  int64_t res[3];
-  t_->wait(t_->issue(0, 0, 0), res);   // every rank has stopped at the same step
+  const int64_t w[kLockstepWords] = {0, 0, 0, commit_status_};
+  commit_status_ = kCommitOk;
+  int64_t res[kLockstepWords];
+  t_->wait(t_->issue(w), res);   // every rank has stopped at the same step
   ++agreements_;
+  group_status_ = res[3];
+  if (res[3] <= kCommitFatal) {
+    stopped_ = true;
+    throw LockstepError("lockstep: a rank's last commit failed");
+  }
   for (auto& f : finished_q_) emit(std::move(f.second));
   finished_q_.clear();
   stopped_ = true;

@@ -18,10 +18,15 @@
 // ride along as a consistency check: step and -step (MIN of both = min and -max).
 //
 // Sync mode (commit='sync', the reference's per-batch commit contract, auto_commit.py:55-58 /
-// kafka_dataset.py:130): before batch k+1 may be handed out, an agreement issued at step k+1 must
-// have completed -- it proves every rank finished batch k, so k becomes committable on every rank
-// at that moment and the caller commits it before delivering.  One collective per step: the
-// issue-ahead pipelining is off, the agreement's credit still grants the following batches.
+// kafka_dataset.py:130, made a cross-rank barrier): a finished batch is committable at once on
+// its own rank; the caller commits it (its store, the coordinator's answer through a bridge) and
+// reports how that went (set_commit_status); then, before batch k+1 may be handed out, an
+// agreement issued at step k+1 must complete.  So when any rank hands out k+1, EVERY rank has
+// committed k.  The agreement's fourth word is the MIN of the ranks' commit statuses: a rank whose
+// commit failed fatally makes every rank raise at the same step (kCommitFatal), a swallowed
+// CommitFailedError (the reference logs it and continues, kafka_dataset.py:131-135) lets every rank
+// continue (kCommitFailed is counted).  One collective per step: the issue-ahead pipelining is
+// off, the agreement's credit still grants the following batches.
 #pragma once
 #include <chrono>
 #include <cstdint>
@@ -35,13 +40,19 @@
 
 namespace tk {
 
-// A pipelined all-reduce(MIN) of three int64: issue() returns a ticket, wait() its result.
+// The words of one agreement, all-reduced with MIN: [credit, step, -step, commit status].
+constexpr int kLockstepWords = 4;
+// Commit status word (sync mode): every batch committed so far was stored / a CommitFailedError
+// was swallowed on some rank / a commit raised on some rank.
+constexpr int64_t kCommitOk = 2, kCommitFailed = 1, kCommitFatal = 0;
+
+// A pipelined all-reduce(MIN) of kLockstepWords int64: issue() returns a ticket, wait() its result.
 // Implemented over RCCL (csrc/hip/rccl_lockstep.*) and over any Python all-reduce (gloo).
 class LockstepTransport {
  public:
   virtual ~LockstepTransport() = default;
-  virtual int issue(int64_t a, int64_t b, int64_t c) = 0;
-  virtual void wait(int ticket, int64_t out[3]) = 0;
+  virtual int issue(const int64_t in[kLockstepWords]) = 0;
+  virtual void wait(int ticket, int64_t out[kLockstepWords]) = 0;
 };
 
 class LockstepError : public std::runtime_error {
@@ -71,8 +82,20 @@ class CreditLockstep {
   // The batch next() allowed was handed out; returns its index.
   int64_t delivered() { return step_++; }
   // A delivered batch is finished (the user asked for the next one): it becomes committable
-  // once an agreement proves every rank got past it (settle).
-  void finished(int64_t index, std::vector<Watermark>&& wms) { finished_q_.emplace_back(index, std::move(wms)); }
+  // once an agreement proves every rank got past it (settle) -- in sync mode at once (the
+  // agreement after its commit is the barrier).
+  void finished(int64_t index, std::vector<Watermark>&& wms) {
+    if (sync_)
+      emit(std::move(wms));
+    else
+      finished_q_.emplace_back(index, std::move(wms));
+  }
+  // Sync mode: how this rank's commits since the last agreement went (kCommitOk / kCommitFailed /
+  // kCommitFatal); carried by the next agreement, then reset to kCommitOk.
+  void set_commit_status(int64_t s) { commit_status_ = s < commit_status_ ? s : commit_status_; }
+  // The MIN commit status of the last settled agreement, and agreements that carried a failure.
+  int64_t group_commit_status() const { return group_status_; }
+  uint64_t group_commit_failures() const { return group_failures_; }
   // End of the iteration: settle every agreement in flight, then one more round (a barrier:
   // every rank stopped at the same step); everything finished becomes committable.
   void finish();
@@ -90,10 +113,11 @@ class CreditLockstep {
   // Host time spent waiting for agreement results: in total, and the most one delivered step
   // (one next() call) waited -- what the collective's round trip cost the critical path.
   int64_t wait_ns() const { return wait_ns_; }
+  int64_t issue_ns() const { return issue_ns_; }  // host time spent issuing agreements
   int64_t step_wait_max_ns() const { return step_wait_max_ns_; }
   uint64_t agreements_since_reset() const { return agreements_ - agreements_at_reset_; }
   void reset_stats() {
-    wait_ns_ = step_wait_max_ns_ = 0;
+    wait_ns_ = step_wait_max_ns_ = issue_ns_ = 0;
     agreements_at_reset_ = agreements_;
   }
 
@@ -116,8 +140,10 @@ class CreditLockstep {
   int64_t step_ = 0, granted_ = 0;
   bool stopped_ = false, no_more_credit_ = false, sync_ = false;
   int64_t settled_step_ = -1;  // highest step an agreement was issued at and has completed
+  int64_t commit_status_ = kCommitOk, group_status_ = kCommitOk;
+  uint64_t group_failures_ = 0;
   uint64_t agreements_ = 0, agreements_at_reset_ = 0;
-  int64_t wait_ns_ = 0, step_wait_max_ns_ = 0, step_wait_ns_ = 0;
+  int64_t wait_ns_ = 0, step_wait_max_ns_ = 0, step_wait_ns_ = 0, issue_ns_ = 0;
   std::deque<Ticket> tickets_;
   std::deque<std::pair<int64_t, std::vector<Watermark>>> finished_q_;
   std::function<void(std::vector<Watermark>&&)> on_commit_;

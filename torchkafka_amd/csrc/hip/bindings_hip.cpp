@@ -27,25 +27,21 @@ namespace {
 class PyLockstep : public LockstepTransport {
  public:
   explicit PyLockstep(py::function fn) : fn_(std::move(fn)) {}
-  int issue(int64_t a, int64_t b, int64_t c) override {
+  int issue(const int64_t in[tk::kLockstepWords]) override {
     py::gil_scoped_acquire gil;
-    py::tuple r = fn_(a, b, c);
+    py::tuple r = fn_(in[0], in[1], in[2], in[3]);
     const int t = int(next_++ % 64);
-    res_[t][0] = r[0].cast<int64_t>();
-    res_[t][1] = r[1].cast<int64_t>();
-    res_[t][2] = r[2].cast<int64_t>();
+    for (int k = 0; k < tk::kLockstepWords; ++k) res_[t][k] = r[size_t(k)].cast<int64_t>();
     return t;
   }
-  void wait(int t, int64_t out[3]) override {
-    out[0] = res_[t][0];
-    out[1] = res_[t][1];
-    out[2] = res_[t][2];
+  void wait(int t, int64_t out[tk::kLockstepWords]) override {
+    for (int k = 0; k < tk::kLockstepWords; ++k) out[k] = res_[t][k];
   }
 
  private:
   py::function fn_;
   uint64_t next_ = 0;
-  int64_t res_[64][3];
+  int64_t res_[64][tk::kLockstepWords];
 };
 
 template <typename T>
@@ -170,14 +166,21 @@ PYBIND11_MODULE(_tkhip, m) {
            py::arg("slots"))
       .def_static("unique_id", [](const std::string& lib) { return py::bytes(RcclLockstep::unique_id(lib)); })
       .def("allreduce_min",
-           [](RcclLockstep& l, int64_t a, int64_t b, int64_t c) {
-             int64_t r[3];
+           [](RcclLockstep& l, int64_t a, int64_t b, int64_t c, int64_t d) {
+             const int64_t in[tk::kLockstepWords] = {a, b, c, d};
+             int64_t r[tk::kLockstepWords];
              {
                py::gil_scoped_release nogil;
-               l.wait(l.issue(a, b, c), r);
+               l.wait(l.issue(in), r);
              }
-             return py::make_tuple(r[0], r[1], r[2]);
-           })
+             return py::make_tuple(r[0], r[1], r[2], r[3]);
+           },
+           py::arg("a"), py::arg("b"), py::arg("c"), py::arg("d") = tk::kCommitOk)
+      .def_property_readonly("high_priority", &RcclLockstep::high_priority,
+                             "the lockstep stream is at the device's greatest priority (a hardware queue of its own)")
+      .def_property_readonly("words_mode", &RcclLockstep::words_mode,
+                             "how the agreement words reach RCCL: kernel (tiny copy kernels), host (RCCL on "
+                             "host-mapped memory) or copy (hipMemcpyAsync)")
       .def_property_readonly("issued", &RcclLockstep::issued)
       .def_property_readonly("nranks", &RcclLockstep::comm_count,
                              "ranks in the private communicator, as RCCL reports them (ncclCommCount)")
@@ -340,6 +343,7 @@ PYBIND11_MODULE(_tkhip, m) {
              s["log_register_wait_ns"] = d.log_register_wait_ns();
              s["lockstep_agreements"] = d.lockstep_agreements();
              s["lockstep_wait_ns"] = d.lockstep_wait_ns();
+             s["lockstep_issue_ns"] = d.lockstep_issue_ns();
              s["lockstep_step_wait_max_ns"] = d.lockstep_step_wait_max_ns();
              s["verify_wait_ns"] = d.verify_wait_ns_;
              return s;
@@ -369,6 +373,10 @@ PYBIND11_MODULE(_tkhip, m) {
       .def_property_readonly("coalesce", &MainDriver::coalesce)
       .def("enable_lockstep", &MainDriver::enable_lockstep, py::keep_alive<1, 2>())
       .def("set_sync_commit", &MainDriver::set_sync_commit, py::arg("sync"))
+      .def("set_commit_status", &MainDriver::set_commit_status, py::arg("status"),
+           "sync commits under the lockstep: how this rank's commits of the finished batch went (2 stored, 1 "
+           "CommitFailedError swallowed, 0 raised); the next agreement carries it to every rank")
+      .def_property_readonly("group_commit_failures", &MainDriver::group_commit_failures)
       .def("set_command_queue", &MainDriver::set_command_queue, py::arg("on"))
       .def("verify_delivered",
            [](MainDriver& d) {

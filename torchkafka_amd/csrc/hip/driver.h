@@ -221,6 +221,11 @@ class MainDriver {
     sync_commit_ = s;
     if (ls_) ls_->set_sync(s);
   }
+  // Sync mode under a lockstep: this rank's commit status for the next agreement (lockstep.h).
+  void set_commit_status(int64_t s) {
+    if (ls_) ls_->set_commit_status(s);
+  }
+  uint64_t group_commit_failures() const { return ls_ ? ls_->group_commit_failures() : 0; }
   // verify='deliver': waits for the device verdict (CRC32C / JSON grammar) of the batch just
   // delivered.  0 clean or not device-checked; -4 corrupt (parse_error() says why: the batches
   // finished before it were made committable first, it and what follows never are).
@@ -236,6 +241,7 @@ class MainDriver {
   bool lockstep_enabled() const { return bool(ls_); }
   uint64_t lockstep_agreements() const { return ls_ ? ls_->agreements_since_reset() : 0; }
   int64_t lockstep_wait_ns() const { return ls_ ? ls_->wait_ns() : 0; }
+  int64_t lockstep_issue_ns() const { return ls_ ? ls_->issue_ns() : 0; }
   int64_t lockstep_step_wait_max_ns() const { return ls_ ? ls_->step_wait_max_ns() : 0; }
 
   SlotView last;  // the slot most recently returned by next_slot / step_fixed

@@ -1,9 +1,16 @@
 // Native RCCL lockstep collective for multi-GPU streaming.
 //
-// One tiny all-reduce(MIN) of int64 [have_batch, step, -step] per loader step
-// decides, for every rank at once, whether all ranks have a batch for that
-// step (so they continue or stop together) and proves they are on the same
-// step.  Issued from C++ on a private HIP stream -- never behind the user's
+// One tiny all-reduce(MIN) of int64 [credit, step, -step, commit status] per
+// agreement decides, for every rank at once, how far all ranks may go (so they
+// continue or stop together), proves they are on the same step and, under
+// commit='sync', tells every rank whether every rank's commit went through.
+//
+// The words never take a hipMemcpyAsync (two 32-byte copies per
+// agreement, three queue operations): by default a one-wave kernel reads them
+// from pinned host memory into the device buffer RCCL reduces, and another
+// writes the result back to pinned host memory (TORCHKAFKA_RCCL_WORDS=kernel);
+// `host` hands RCCL the host-mapped buffers themselves (one queue operation);
+// `copy` keeps the two hipMemcpyAsync (A/B only).  Issued from C++ on a private HIP stream -- never behind the user's
 // queued compute -- and pipelined `depth` steps ahead, so the host never
 // waits on the ~10-30 us xGMI round trip: the result for step k was issued
 // at step k - depth and is normally complete when it is read.
@@ -38,10 +45,12 @@ class RcclLockstep : public LockstepTransport {
   RcclLockstep(const RcclLockstep&) = delete;
   RcclLockstep& operator=(const RcclLockstep&) = delete;
 
-  // Enqueues all-reduce(MIN) of {a, b, c}; returns a ticket.
-  int issue(int64_t a, int64_t b, int64_t c) override;
+  // Enqueues all-reduce(MIN) of the agreement's words; returns a ticket.
+  int issue(const int64_t in[tk::kLockstepWords]) override;
   // Waits for a ticket's result.
-  void wait(int ticket, int64_t out[3]) override;
+  void wait(int ticket, int64_t out[tk::kLockstepWords]) override;
+  const char* words_mode() const { return mode_ == 0 ? "kernel" : mode_ == 1 ? "host" : "copy"; }
+  bool high_priority() const { return high_prio_; }
   bool ready(int ticket);
   // Failure detection: a round trip not complete after `ms` (a peer rank died or hung) aborts
   // the communicator and raises instead of blocking forever; <= 0 waits indefinitely.
@@ -62,9 +71,13 @@ class RcclLockstep : public LockstepTransport {
   void* comm_ = nullptr;
   int rank_, world_, device_, slots_;
   hipStream_t stream_ = nullptr;
-  int64_t* d_ = nullptr;       // device [slots][2][3]: in, out
-  int64_t* h_in_ = nullptr;    // pinned [slots][3]
-  int64_t* h_out_ = nullptr;   // pinned [slots][3]
+  int64_t* d_ = nullptr;       // device [slots][2][kLockstepWords]: in, out
+  int64_t* h_in_ = nullptr;    // pinned, device-mapped [slots][kLockstepWords]
+  int64_t* h_out_ = nullptr;   // pinned, device-mapped [slots][kLockstepWords]
+  int64_t* h_in_dev_ = nullptr;   // their device addresses
+  int64_t* h_out_dev_ = nullptr;
+  int mode_ = 0;               // 0 kernel, 1 host, 2 copy (TORCHKAFKA_RCCL_WORDS)
+  bool high_prio_ = true;      // stream_ at the greatest priority (its own hardware-queue pool)
   std::vector<hipEvent_t> ev_;
   uint64_t issued_ = 0;
   int64_t timeout_ms_ = 600000;  // like torch.distributed's default NCCL timeout

@@ -4,6 +4,7 @@
 #include <rccl/rccl.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <thread>
@@ -58,6 +59,22 @@ void check(RcclApi* api, ncclResult_t r, const char* what) {
   if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + api->GetErrorString(r));
 }
 
+constexpr int kW = tk::kLockstepWords;
+
+// The agreement's words between pinned host memory and the device buffer RCCL reduces: one wave,
+// one word per lane (system-coherent host-mapped memory, read and written over PCIe).
+__global__ void words_copy_kernel(const int64_t* __restrict__ src, int64_t* __restrict__ dst, int n) {
+  const int i = int(threadIdx.x);
+  if (i < n) dst[i] = src[i];
+}
+
+int words_mode_env() {
+  const char* e = std::getenv("TORCHKAFKA_RCCL_WORDS");
+  if (!e) return 0;
+  const std::string v(e);
+  return v == "host" ? 1 : v == "copy" ? 2 : 0;
+}
+
 }  // namespace
 
 std::string RcclLockstep::unique_id(const std::string& lib_path) {
@@ -74,10 +91,25 @@ RcclLockstep::RcclLockstep(const std::string& lib_path, const std::string& id, i
   if (id.size() != NCCL_UNIQUE_ID_BYTES) throw std::invalid_argument("RCCL unique id must be 128 bytes");
   api_ = load_api(lib_path);
   TKH_HIP(hipSetDevice(device_));
-  TKH_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  TKH_HIP(hipMalloc(reinterpret_cast<void**>(&d_), sizeof(int64_t) * 6 * size_t(slots_)));
-  TKH_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_in_), sizeof(int64_t) * 3 * size_t(slots_), hipHostMallocDefault));
-  TKH_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_out_), sizeof(int64_t) * 3 * size_t(slots_), hipHostMallocDefault));
+  // the lockstep's stream at the device's greatest priority: HIP keeps a hardware-queue pool per
+  // priority, so it never shares a queue with the decode and copy streams (normal priority) or the
+  // user's -- a decode launch never waits behind a collective that waits for the other ranks
+  // (tools/probes/queue_probe.py); TORCHKAFKA_LOCKSTEP_PRIORITY=normal for the A/B
+  const char* pe = std::getenv("TORCHKAFKA_LOCKSTEP_PRIORITY");
+  high_prio_ = !(pe && std::string(pe) == "normal");
+  if (high_prio_) {
+    int least = 0, greatest = 0;
+    TKH_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    TKH_HIP(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, greatest));
+  } else {
+    TKH_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  }
+  mode_ = words_mode_env();
+  TKH_HIP(hipMalloc(reinterpret_cast<void**>(&d_), sizeof(int64_t) * 2 * kW * size_t(slots_)));
+  TKH_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_in_), sizeof(int64_t) * kW * size_t(slots_), hipHostMallocMapped));
+  TKH_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_out_), sizeof(int64_t) * kW * size_t(slots_), hipHostMallocMapped));
+  TKH_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_in_dev_), h_in_, 0));
+  TKH_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_out_dev_), h_out_, 0));
   ev_.resize(size_t(slots_));
   for (auto& e : ev_) TKH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   ncclUniqueId uid;
@@ -132,22 +164,32 @@ void RcclLockstep::wait_event(int t, const char* what) {
   }
 }
 
-int RcclLockstep::issue(int64_t a, int64_t b, int64_t c) {
+int RcclLockstep::issue(const int64_t in[kW]) {
   const int s = int(issued_ % uint64_t(slots_));
   if (aborted_) throw std::runtime_error("lockstep: the RCCL communicator was aborted after a failure");
   // the slot's previous round trip must be complete before its buffers are reused
   wait_event(s, "lockstep slot reuse");
-  int64_t* hin = h_in_ + 3 * s;
-  int64_t* hout = h_out_ + 3 * s;
-  int64_t* din = d_ + 6 * s;
-  int64_t* dout = din + 3;
-  hin[0] = a;
-  hin[1] = b;
-  hin[2] = c;
-  TKH_HIP(hipMemcpyAsync(din, hin, 3 * sizeof(int64_t), hipMemcpyHostToDevice, stream_));
-  check(api_, api_->AllReduce(din, dout, 3, ncclInt64, ncclMin, static_cast<ncclComm_t>(comm_), stream_),
-        "ncclAllReduce");
-  TKH_HIP(hipMemcpyAsync(hout, dout, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, stream_));
+  int64_t* hin = h_in_ + kW * s;
+  int64_t* hout = h_out_ + kW * s;
+  int64_t* din = d_ + 2 * kW * s;
+  int64_t* dout = din + kW;
+  for (int k = 0; k < kW; ++k) hin[k] = in[k];
+  auto* comm = static_cast<ncclComm_t>(comm_);
+  if (mode_ == 1) {
+    // RCCL reads and writes the host-mapped words itself: one queue operation
+    check(api_, api_->AllReduce(h_in_dev_ + kW * s, h_out_dev_ + kW * s, kW, ncclInt64, ncclMin, comm, stream_),
+          "ncclAllReduce");
+  } else if (mode_ == 2) {
+    TKH_HIP(hipMemcpyAsync(din, hin, kW * sizeof(int64_t), hipMemcpyHostToDevice, stream_));
+    check(api_, api_->AllReduce(din, dout, kW, ncclInt64, ncclMin, comm, stream_), "ncclAllReduce");
+    TKH_HIP(hipMemcpyAsync(hout, dout, kW * sizeof(int64_t), hipMemcpyDeviceToHost, stream_));
+  } else {
+    hipLaunchKernelGGL(words_copy_kernel, dim3(1), dim3(64), 0, stream_, h_in_dev_ + kW * s, din, kW);
+    TKH_HIP(hipGetLastError());
+    check(api_, api_->AllReduce(din, dout, kW, ncclInt64, ncclMin, comm, stream_), "ncclAllReduce");
+    hipLaunchKernelGGL(words_copy_kernel, dim3(1), dim3(64), 0, stream_, dout, h_out_dev_ + kW * s, kW);
+    TKH_HIP(hipGetLastError());
+  }
   TKH_HIP(hipEventRecord(ev_[size_t(s)], stream_));
   ++issued_;
   return s;
@@ -165,14 +207,14 @@ int64_t RcclLockstep::allreduce_sum(int64_t v) {
   // every pipelined agreement is settled first: the slots' buffers are shared with issue()
   for (int s = 0; s < slots_; ++s) wait_event(s, "lockstep drain");
   const int s = int(issued_ % uint64_t(slots_));
-  int64_t* hin = h_in_ + 3 * s;
-  int64_t* hout = h_out_ + 3 * s;
-  int64_t* din = d_ + 6 * s;
+  int64_t* hin = h_in_ + kW * s;
+  int64_t* hout = h_out_ + kW * s;
+  int64_t* din = d_ + 2 * kW * s;
   hin[0] = v;
   TKH_HIP(hipMemcpyAsync(din, hin, sizeof(int64_t), hipMemcpyHostToDevice, stream_));
-  check(api_, api_->AllReduce(din, din + 3, 1, ncclInt64, ncclSum, static_cast<ncclComm_t>(comm_), stream_),
+  check(api_, api_->AllReduce(din, din + kW, 1, ncclInt64, ncclSum, static_cast<ncclComm_t>(comm_), stream_),
         "ncclAllReduce");
-  TKH_HIP(hipMemcpyAsync(hout, din + 3, sizeof(int64_t), hipMemcpyDeviceToHost, stream_));
+  TKH_HIP(hipMemcpyAsync(hout, din + kW, sizeof(int64_t), hipMemcpyDeviceToHost, stream_));
   TKH_HIP(hipEventRecord(ev_[size_t(s)], stream_));
   ++issued_;
   wait_event(s, "lockstep allreduce_sum");
@@ -181,12 +223,10 @@ int64_t RcclLockstep::allreduce_sum(int64_t v) {
 
 bool RcclLockstep::ready(int t) { return hipEventQuery(ev_.at(size_t(t))) == hipSuccess; }
 
-void RcclLockstep::wait(int t, int64_t out[3]) {
+void RcclLockstep::wait(int t, int64_t out[kW]) {
   wait_event(t, "lockstep wait");
-  const int64_t* hout = h_out_ + 3 * t;
-  out[0] = hout[0];
-  out[1] = hout[1];
-  out[2] = hout[2];
+  const volatile int64_t* hout = h_out_ + kW * t;
+  for (int k = 0; k < kW; ++k) out[k] = hout[k];
 }
 
 }  // namespace tkh

@@ -118,10 +118,11 @@ class LoaderBridges:
         except Exception:  # noqa: BLE001 - not a synthetic broker: commits go through Python
             return "", ""
 
-    def _sync_bridges(self, t0: int) -> None:
+    def _sync_bridges(self, t0: int) -> bool:
         """commit='sync': waits for the coordinator's answer through every bridge this process
         commits into -- the loader's own (bridge='auto') or, single-process, the dataset
-        consumer's (``KafkaDataset(topic, bootstrap_servers=cluster)``)."""
+        consumer's (``KafkaDataset(topic, bootstrap_servers=cluster)``).  False: a coordinator
+        refused a commit (logged, as the reference logs CommitFailedError)."""
         bridges = list(self._bridges)
         if self.num_workers == 0:
             bridges += getattr(getattr(self.dataset, "_consumer", None), "_bridges", None) or []
@@ -133,3 +134,4 @@ class LoaderBridges:
             _ds_logger.error("Commit failed.")
             self.stats.commit_failures += 1
         self.stats.record_sync_commit(time.perf_counter_ns() - t0)
+        return ok

@@ -35,16 +35,19 @@ class LoaderCommits:
             return (wms, ev, t)
         return (wms, None, t)
 
-    def _sync_commit(self, drv, debug: bool) -> None:
+    def _sync_commit(self, drv, debug: bool) -> int:
         """``commit='sync'``: every finished batch's verdict, local store and -- through the
-        bridges -- the coordinator's OffsetCommit answer, before the next batch is handed out."""
+        bridges -- the coordinator's OffsetCommit answer, before the next batch is handed out.
+        Returns the commit status the next lockstep agreement carries to every rank: 2 stored,
+        1 a CommitFailedError was logged and swallowed (the reference's kafka_dataset.py:131-135)."""
         t0 = time.perf_counter_ns()
         drv.drain_fenced(True)
-        self._commit_native(drv, debug)
+        ok = self._commit_native(drv, debug)
         run = self._run
         if run is not None and run.table is not None:
             run.wait_worker_commits(30.0)  # each worker's consumer committed (and, bridged, forwarded)
-        self._sync_bridges(t0)
+        ok = self._sync_bridges(t0) and ok
+        return 2 if ok else 1
 
     def _commit_logged(self, drv) -> None:
         """One native commit bracketed by the reference's DEBUG messages (kafka_dataset.py:124-143).
@@ -55,24 +58,25 @@ class LoaderCommits:
         ``commit_sink='worker'`` the workers commit and log ("Committing offsets on worker %d."), as
         the reference's workers do, and the main process stays silent."""
         if self._sink == "worker":
-            self._log_commit(drv.commit_pending(), False)
-            return
+            return self._log_commit(drv.commit_pending(), False)
         _ds_logger.debug("Committing offsets.")
-        self._log_commit(drv.commit_pending(), True)
+        return self._log_commit(drv.commit_pending(), True)
 
-    def _commit_native(self, drv, debug: bool) -> None:
+    def _commit_native(self, drv, debug: bool) -> bool:
         if debug:
-            self._commit_logged(drv)
-        else:
-            self._log_commit(drv.commit_pending(), False)
+            return self._commit_logged(drv)
+        return self._log_commit(drv.commit_pending(), False)
 
-    def _log_commit(self, status: int, debug: bool) -> None:
+    def _log_commit(self, status: int, debug: bool) -> bool:
+        """False when the commit failed (CommitFailedError: logged, swallowed)."""
         if status == -2:  # a device-parsed batch was malformed: it (and what follows) stays uncommitted
             raise CorruptRecordException(self._run.driver.parse_error())
         if status == -1:
             _ds_logger.error("Commit failed.")
-        elif status == 1 and debug:
+            return False
+        if status == 1 and debug:
             _ds_logger.debug("Committed offsets.")
+        return True
 
     def _absorb_driver_stats(self, drv) -> None:
         st = drv.stats()
@@ -111,6 +115,7 @@ class LoaderCommits:
         self.stats.verify_wait_ns += st.get("verify_wait_ns", 0)
         self.stats.lockstep_agreements += st.get("lockstep_agreements", 0)
         self.stats.lockstep_wait_ns += st.get("lockstep_wait_ns", 0)
+        self.stats.lockstep_issue_ns += st.get("lockstep_issue_ns", 0)
         self.stats.lockstep_step_wait_max_ns = max(self.stats.lockstep_step_wait_max_ns,
                                                    st.get("lockstep_step_wait_max_ns", 0))
         self.stats.commits += st["commits"]
@@ -125,15 +130,18 @@ class LoaderCommits:
 
         return open_broker(resolve_url(self._servers))
 
-    def _sync_commit_py(self) -> None:
+    def _sync_commit_py(self) -> int:
         """commit='sync' on the Python path: every finished batch stored (fences waited for) and,
-        through the bridges / the workers' consumers, answered by the coordinator."""
+        through the bridges / the workers' consumers, answered by the coordinator.  Returns the
+        commit status for the lockstep (2 stored, 1 a CommitFailedError logged and swallowed)."""
         t0 = time.perf_counter_ns()
+        failures = self.stats.commit_failures
         self._commit_finished(wait=True)
         run = self._run
         if run is not None and run.table is not None:
             run.wait_worker_commits(30.0)
-        self._sync_bridges(t0)
+        ok = self._sync_bridges(t0) and self.stats.commit_failures == failures
+        return 2 if ok else 1
 
     def _commit_finished(self, wait: bool = False) -> None:
         """Commits the watermarks of every batch the user finished (exactly those)."""

@@ -68,17 +68,18 @@ def _traced_step(step):
 
 
 def _host_allreduce_min(group):
-    """all-reduce(MIN) of three int64 over a CPU (gloo) group, for the driver's PyLockstep transport."""
+    """all-reduce(MIN) of the lockstep's four int64 words (credit, step, -step, commit status) over a
+    CPU (gloo) group, for the driver's PyLockstep transport."""
     import torch.distributed as dist
 
     if dist.get_backend(group) != "gloo":
         group = dist.new_group(backend="gloo")  # collective: every rank builds its loader iterator
-    buf = torch.zeros(3, dtype=torch.int64)
+    buf = torch.zeros(4, dtype=torch.int64)
 
-    def allreduce_min(a: int, b: int, c: int):
-        buf[0], buf[1], buf[2] = a, b, c
+    def allreduce_min(a: int, b: int, c: int, d: int):
+        buf[0], buf[1], buf[2], buf[3] = a, b, c, d
         dist.all_reduce(buf, op=dist.ReduceOp.MIN, group=group)
-        return int(buf[0]), int(buf[1]), int(buf[2])
+        return int(buf[0]), int(buf[1]), int(buf[2]), int(buf[3])
 
     return allreduce_min
 
@@ -669,26 +670,37 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
             sync = auto_commit and self.commit_mode == "sync"
             while True:
                 item = self._next_item(run)
+                status, fatal = 2, None
                 if prev is not None and auto_commit:
                     finished.append(self._finish_marker(prev))  # the user is done with the previous batch
                     prev = None
-                    if sync and lock is None:
-                        self._sync_commit_py()
+                    if sync:
+                        # commit='sync': batch k committed (and answered) BEFORE the agreement that
+                        # hands out k+1, which carries how it went to every rank
+                        try:
+                            status = self._sync_commit_py()
+                        except Exception as e:  # noqa: BLE001 - re-raised after the agreement
+                            fatal, status = e, 0
                 if lock is not None:
                     t_agree = time.perf_counter_ns()
-                    ok = lock.agree(item is not None, step)
+                    try:
+                        ok = lock.agree(item is not None, step, status)
+                    except Exception as e:
+                        if fatal is not None:
+                            raise fatal from e
+                        raise
                     t_agree = time.perf_counter_ns() - t_agree
                     st = self.stats
                     st.lockstep_agreements += 1
                     st.lockstep_wait_ns += t_agree
                     st.lockstep_step_wait_max_ns = max(st.lockstep_step_wait_max_ns, t_agree)
-                    if sync:
-                        self._sync_commit_py()
-                    elif auto_commit:
+                    if auto_commit and not sync:
                         self._commit_finished()
                     if not ok:
                         break
                 else:
+                    if fatal is not None:
+                        raise fatal
                     if auto_commit:
                         self._commit_finished()
                     if item is None:
@@ -757,7 +769,9 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
             raise RuntimeError(f"lockstep: RCCL communicator has {nranks} ranks (rank-id sum {rank_sum}), "
                                f"the process group {world}")
         self.lockstep_info = {"transport": "rccl", "rccl_nranks": nranks, "rank_id_sum": rank_sum,
-                              "world_size": world}
+                              "world_size": world, "words": ls.words_mode,
+                              "stream": ("greatest priority: a hardware-queue pool of its own" if ls.high_priority
+                                         else "normal priority (shares the process's queues)")}
         return ls
 
     def stream_plan(self) -> dict:
@@ -773,18 +787,21 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
             if run.driver is not None:
                 plan["mirror_copy"] = int(run.driver.mirror_copy_streams)
         if run is not None and run.rccl is not None and self.lockstep_info.get("transport") == "rccl":
-            plan["rccl_lockstep"] = 1
+            # a greatest-priority stream takes a queue from the high-priority pool, not these
+            plan["rccl_lockstep"] = 0 if getattr(run.rccl, "high_priority", False) else 1
+            plan["rccl_lockstep_high_priority"] = 1 - plan["rccl_lockstep"]
         try:
             import torch.distributed as dist
 
             # torch makes its RCCL communicator (and streams) at a group's first collective: the
-            # lockstep never runs one on it, a DDP job's gradient all-reduce does (world > 1)
+            # lockstep never runs one on it, a DDP job's gradient all-reduce does (world > 1, or a
+            # world-1 group that ran one: bench.py's rehearsal of the N = 8 queue layout)
             if (dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"
-                    and dist.get_world_size() > 1):
+                    and (dist.get_world_size() > 1 or os.environ.get("TORCHKAFKA_TORCH_NCCL_ACTIVE") == "1")):
                 plan["torch_nccl"] = 1
         except Exception:  # noqa: BLE001
             pass
-        total = sum(plan.values())
+        total = sum(v for k, v in plan.items() if k != "rccl_lockstep_high_priority")
         hw = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
         plan.update(total=total, hw_queues=hw, shared=total > hw)
         return plan
@@ -822,7 +839,27 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
         wait_since = None
         try:
             while True:
-                r, cs, item = step()
+                fatal = None
+                if sync and delivered:
+                    # commit='sync': asking for batch k+1 finishes batch k -- its verdict, its store
+                    # and the coordinator's answer come FIRST, then the lockstep agreement that
+                    # hands out k+1 carries how that went, so no rank sees k+1 before every rank
+                    # committed k (the reference's auto_commit.py:55-58 / kafka_dataset.py:130 as a
+                    # cross-rank barrier)
+                    drv.finish_delivered(_stream_ptr(self.device))
+                    try:
+                        status = self._sync_commit(drv, debug)
+                    except Exception as e:  # noqa: BLE001 - re-raised after the agreement
+                        fatal, status = e, 0
+                    drv.set_commit_status(status)
+                    if fatal is not None and not drv.lockstep_enabled:
+                        raise fatal
+                try:
+                    r, cs, item = step()
+                except Exception as e:
+                    if fatal is not None:
+                        raise fatal from e
+                    raise
                 if cs:
                     self._log_commit(cs, debug)
                 if r > 0 and verify and py_commits and drv.verify_delivered() < 0:
@@ -835,11 +872,8 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
                         self._commit_native(drv, debug)
                     raise CorruptRecordException(drv.parse_error())
                 if r > 0:
-                    if delivered:
-                        if log_commits and not py_commits:
-                            self._commit_logged(drv)
-                        if sync:
-                            self._sync_commit(drv, debug)  # batch k durable before k+1 is handed out
+                    if delivered and log_commits and not py_commits and not sync:
+                        self._commit_logged(drv)
                     delivered = True
                     wait_since = None
                     yield item

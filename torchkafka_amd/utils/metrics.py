@@ -64,6 +64,7 @@ class LoaderStats:
     mirror_fallbacks: int = 0  # segments read from the pinned log instead (buffer busy)
     lockstep_agreements: int = 0      # cross-rank agreements (collectives) issued
     lockstep_wait_ns: int = 0         # host time waiting for agreement results
+    lockstep_issue_ns: int = 0        # host time issuing agreements (the transport's enqueue)
     verify_wait_ns: int = 0           # verify='deliver': host time waiting for a batch's device verdict
     lockstep_step_wait_max_ns: int = 0  # the most one delivered step waited for them
     started: float = field(default_factory=time.perf_counter)
@@ -131,6 +132,7 @@ class LoaderStats:
             "mirror_pending_fallbacks": self.mirror_pending_fallbacks,
             "lockstep_agreements": self.lockstep_agreements,
             "lockstep_wait_us_per_batch": self.lockstep_wait_ns / 1e3 / max(self.batches, 1),
+            "lockstep_issue_us_per_batch": self.lockstep_issue_ns / 1e3 / max(self.batches, 1),
             "verify_wait_us_per_batch": self.verify_wait_ns / 1e3 / max(self.batches, 1),
             "lockstep_step_wait_max_us": self.lockstep_step_wait_max_ns / 1e3,
             "commits": self.commits,
