@@ -377,6 +377,9 @@ PYBIND11_MODULE(_tkhip, m) {
            "sync commits under the lockstep: how this rank's commits of the finished batch went (2 stored, 1 "
            "CommitFailedError swallowed, 0 raised); the next agreement carries it to every rank")
       .def_property_readonly("group_commit_failures", &MainDriver::group_commit_failures)
+      .def("delivered_positions", &MainDriver::delivered_positions,
+           "[(partition index, position after the batches handed out so far)]")
+      .def_property_readonly("delivered_batches", &MainDriver::delivered_batches)
       .def("set_command_queue", &MainDriver::set_command_queue, py::arg("on"))
       .def("verify_delivered",
            [](MainDriver& d) {

@@ -981,6 +981,11 @@ void MainDriver::deliver(const SlotView& v) { set_delivered(v); }
 
 void MainDriver::set_delivered(const SlotView& v) {
   delivered_ = v.wms;
+  for (const tk::Watermark& w : v.wms) {
+    if (w.pidx >= delivered_pos_.size()) delivered_pos_.resize(size_t(w.pidx) + 1, -1);
+    if (w.next_offset > delivered_pos_[w.pidx]) delivered_pos_[w.pidx] = w.next_offset;
+  }
+  ++delivered_batches_;
   const bool checked = v.kind == tk::kPackJsonText || v.kind == tk::kPackRecordSpan || row_span_kind(v.kind);
   delivered_perr_ = checked ? (v.perr >= 0 ? v.perr : last_perr_) : -1;
 }

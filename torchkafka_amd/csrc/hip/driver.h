@@ -198,6 +198,16 @@ class MainDriver {
   int64_t groups() const { return groups_; }
 
   const std::vector<tk::Watermark>& delivered() const { return delivered_; }
+  // Every partition's position after the batches handed out so far (-1: none from it), and how
+  // many batches that is: DeviceLoader.state_dict(global_step=True) -- the end of a global step
+  // on every rank, ahead of the commits (which under the async lockstep land at agreements).
+  std::vector<std::pair<uint32_t, int64_t>> delivered_positions() const {
+    std::vector<std::pair<uint32_t, int64_t>> out;
+    for (size_t p = 0; p < delivered_pos_.size(); ++p)
+      if (delivered_pos_[p] >= 0) out.emplace_back(uint32_t(p), delivered_pos_[p]);
+    return out;
+  }
+  uint64_t delivered_batches() const { return delivered_batches_; }
   std::vector<std::pair<uint32_t, int64_t>> committed() const { return ledger_->committed(); }
   std::vector<std::pair<uint32_t, int64_t>> take_pending() { return ledger_->take_pending(); }
   bool worker_done(uint32_t w) const { return poller_->worker_done(w); }
@@ -400,6 +410,8 @@ class MainDriver {
   std::deque<std::tuple<hipEvent_t, int64_t, std::vector<tk::Watermark>, int64_t>> fenced_;
   std::vector<hipEvent_t> event_pool_;
   std::vector<tk::Watermark> delivered_;
+  std::vector<int64_t> delivered_pos_;  // per partition index: position after the batches handed out
+  uint64_t delivered_batches_ = 0;
   int64_t delivered_index_ = -1;
   int64_t last_perr_ = -1, delivered_perr_ = -1;
   std::string parse_error_;

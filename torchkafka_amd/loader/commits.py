@@ -223,17 +223,79 @@ class LoaderCommits:
             self._committed.update(dict(run.driver.committed()))
         return dict(self._committed)
 
-    def state_dict(self) -> dict:
-        """Committed positions for a model checkpoint (the committed offsets ARE the
-        checkpoint).  ``{"version": 1, "group_id": g, "offsets": {topic: {partition: offset}}}``
-        -- JSON-serialisable.  Under DDP each rank reports the partitions it consumed and committed;
-        save one per rank or all-gather them."""
+    def _absorb_delivered(self, drv) -> None:
+        """The native driver's delivered positions, kept past its iteration."""
+        pos = self._delivered_pos
+        for pidx, nxt in drv.delivered_positions():
+            if nxt > pos.get(pidx, -1):
+                pos[pidx] = nxt
+
+    def delivered_positions(self) -> dict[int, int]:
+        """{partition index: position after every batch handed out so far} -- live during
+        iteration; includes the checkpoint this loader resumed from."""
+        run = self._run
+        if run is not None and run.driver is not None and not run.closed:
+            self._absorb_delivered(run.driver)
+        return dict(self._delivered_pos)
+
+    def state_dict(self, global_step: bool = False, group=None) -> dict:
+        """Positions for a model checkpoint (the committed offsets ARE the checkpoint).
+
+        ``global_step=False``: this rank's committed positions,
+        ``{"version": 1, "group_id": g, "offsets": {topic: {partition: offset}}}``.
+
+        ``global_step=True`` (DDP): every rank's positions at the END OF THE SAME STEP -- call it
+        on every rank at the same step of the training loop (a collective).  Each rank contributes
+        the positions after the batches it has handed out (not its committed table: under the
+        async lockstep commits land at agreements, dozens of steps apart), one all-gather over
+        ``group`` (a gloo group is made from the default group if it is not one) merges them, and
+        the ranks' step counts must agree.  ``{"version": 2, "group_id", "global_step": S,
+        "world_size": W, "offsets": {...every rank's partitions...}}``, identical on every rank;
+        ``load_state_dict`` resumes from it on any number of ranks.  JSON-serialisable."""
         b = self._broker()
-        offsets: dict[str, dict[int, int]] = {}
-        for pidx, off in sorted(self.committed_offsets().items()):
+        if not global_step:
+            offsets: dict[str, dict[int, int]] = {}
+            for pidx, off in sorted(self.committed_offsets().items()):
+                tp = b.tp_of(pidx)
+                offsets.setdefault(tp.topic, {})[tp.partition] = int(off)
+            return {"version": 1, "group_id": self._group_id, "offsets": offsets}
+        import torch.distributed as dist
+
+        pos = self.delivered_positions()
+        step = self._global_step_base + self._steps_delivered
+        world = 1
+        merged = dict(pos)
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            world = dist.get_world_size(group)
+            grp = group if group is not None and dist.get_backend(group) == "gloo" else self._cpu_group(group)
+            gathered: list = [None] * world
+            dist.all_gather_object(gathered, (step, pos), group=grp)
+            steps = sorted({g[0] for g in gathered})
+            if len(steps) != 1:
+                raise RuntimeError(f"state_dict(global_step=True): the ranks stand at different steps {steps}; call "
+                                   "it on every rank at the same step of the loop")
+            for _, p in gathered:
+                for pidx, nxt in p.items():
+                    if nxt > merged.get(pidx, -1):
+                        merged[pidx] = nxt
+        offsets = {}
+        for pidx, off in sorted(merged.items()):
             tp = b.tp_of(pidx)
             offsets.setdefault(tp.topic, {})[tp.partition] = int(off)
-        return {"version": 1, "group_id": self._group_id, "offsets": offsets}
+        return {"version": 2, "group_id": self._group_id, "global_step": int(step), "world_size": world,
+                "offsets": offsets}
+
+    def _cpu_group(self, group=None):
+        """A gloo group over the ranks of ``group`` (made once: a collective every rank reaches)."""
+        import torch.distributed as dist
+
+        if getattr(self, "_gloo_group", None) is None:
+            if dist.get_backend(group) == "gloo":
+                self._gloo_group = group
+            else:
+                ranks = None if group is None else dist.get_process_group_ranks(group)
+                self._gloo_group = dist.new_group(ranks=ranks, backend="gloo")
+        return self._gloo_group
 
     def load_state_dict(self, state: dict) -> None:
         """Resumes from a checkpoint's offsets: they are committed for the group (an administrative
@@ -243,7 +305,7 @@ class LoaderCommits:
 
         if self._run is not None and not self._run.closed:
             raise RuntimeError("load_state_dict() must be called before iterating the loader")
-        if int(state.get("version", 1)) != 1:
+        if int(state.get("version", 1)) not in (1, 2):
             raise ValueError(f"unsupported DeviceLoader state version {state.get('version')}")
         group = state.get("group_id") or self._group_id
         if group is None:
@@ -269,4 +331,13 @@ class LoaderCommits:
         b = self._broker()
         if offs:
             b.commit(group, offs)
-        self._committed.update({b.pidx(tp.topic, tp.partition): o for tp, o in offs.items()})
+        resumed = {b.pidx(tp.topic, tp.partition): o for tp, o in offs.items()}
+        self._committed.update(resumed)
+        if int(state.get("version", 1)) == 2:
+            # a global-step checkpoint: the steps count on from it, its positions are where every
+            # rank stands (each rank's workers start at the committed offsets)
+            self._global_step_base = int(state.get("global_step", 0))
+            self._steps_delivered = 0
+            for pidx, o in resumed.items():
+                if o > self._delivered_pos.get(pidx, -1):
+                    self._delivered_pos[pidx] = o

@@ -511,6 +511,11 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
             drop_last=self.drop_last, json_count_mode=getattr(tun, "json_count", "auto"))
         self._pending_wms: list = []   # finished-but-uncommitted watermark lists
         self._committed: dict[int, int] = {}
+        # state_dict(global_step=True): every partition's position after the batches handed out
+        # (this loader's lifetime, and the checkpoint it resumed from) and how many steps that is
+        self._delivered_pos: dict[int, int] = {}
+        self._steps_delivered = 0
+        self._global_step_base = 0
         self._norm = None
         self.stats = LoaderStats()
         self._run: _Run | None = None
@@ -710,6 +715,11 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
                     prev = wms
                 else:
                     finished.append((wms, None))  # manual mode: commit() covers every yielded batch
+                pos = self._delivered_pos
+                for pidx, _first, nxt, _n in wms:
+                    if nxt > pos.get(pidx, -1):
+                        pos[pidx] = nxt
+                self._steps_delivered += 1
                 step += 1
                 yield batch
             completed = True
@@ -876,6 +886,7 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
                         self._commit_logged(drv)
                     delivered = True
                     wait_since = None
+                    self._steps_delivered += 1
                     yield item
                 elif r == -2:
                     break
@@ -908,6 +919,7 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
                         self._pending_wms.append(([(p, 0, o, 0) for p, o in pend], None))
             finally:
                 self._absorb_driver_stats(drv)
+                self._absorb_delivered(drv)
                 run.close()
 
     def _fixed_stage(self, drv, native_ac: bool):
