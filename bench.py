@@ -119,18 +119,24 @@ def parse():
     ap.add_argument("--self-launch", action="store_true",
                     help="start the rank processes from this process even at --gpus 1 / --same-device (the "
                          "launcher path the N > 1 runs take without torchrun)")
-    ap.add_argument("--config-blocks", default="compute,config4,config5,config1",
+    ap.add_argument("--config-blocks", default="compute,config4,config5,config1,process",
                     help="comma list of blocks run at N = 1, each on a broker of its own: compute (a bf16 GEMM "
                          "stream beside the config-2 and config-4 loaders: what the loader costs a training job), "
-                         "config4 (JSON -> bf16), config5 (1 MiB records, 128 partitions), config1 (CPU plumbing); "
-                         "'' for none")
+                         "config4 (JSON -> bf16), config5 (1 MiB records, 128 partitions), config1 (CPU plumbing), "
+                         "process (the README's json.loads _process: DeviceLoader vs torch DataLoader + "
+                         "pin_memory); '' for none")
     ap.add_argument("--compute-steps", type=int, default=20000)
     ap.add_argument("--config4-steps", type=int, default=20000)
     ap.add_argument("--config5-steps", type=int, default=1000)
     ap.add_argument("--config1-records", type=int, default=100000)
+    ap.add_argument("--process-steps", type=int, default=1500)
     ap.add_argument("--bridge-steps", type=int, default=None,
                     help="timed steps of the Kafka-protocol bridge blocks (async; sync runs a quarter): "
                          "default 8000 on a GPU, 20 on the CPU; 0 skips them")
+    ap.add_argument("--bridge-codecs", default="lz4,zstd",
+                    help="comma list of compressed bridge blocks (bridge_<codec>: the wire server serves the "
+                         "records as compressed RecordBatches, produced while the block runs, and the bridge's "
+                         "fetch threads inflate them): lz4, zstd, gzip; '' for none")
     return ap.parse_args()
 
 
@@ -389,6 +395,91 @@ def steady_block(R: Rank, res: dict, steps: int, dim: int) -> dict:
     return out
 
 
+def _bridge_counters(loader) -> dict:
+    """Where the bridges' fetch threads spent their time, summed over partitions and threads."""
+    keys = ("bytes", "wire_bytes", "recv_ns", "ingest_ns", "inflate_ns", "inflated_batches", "inflated_bytes")
+    out = {k: 0 for k in keys}
+    out["fetch_wait_ns"] = out["fetch_threads"] = 0
+    for br in loader._bridges:
+        for st in br.stats():
+            for k in keys:
+                out[k] += int(st[k])
+        out["fetch_wait_ns"] += int(br._r.fetch_wait_ns)
+        out["fetch_threads"] += int(br._r.fetch_threads)
+    return out
+
+
+def bridge_codec_block(R: "Rank", args, broker, mine, n_parts, codec, steps, warm, make_loader, server, dtype) -> dict:
+    """bridge_<codec> (VERDICT r4 "do this" 6): the same records served as compressed RecordBatches.
+
+    Setup (untimed): this rank's partitions of the topic are compressed batch by batch, as a
+    producer with ``compression_type=codec`` writes them, into a staging topic; the served topic
+    gets the warm-up's share.  The rest is appended to the served topic when the timed steps start
+    (a live topic whose producer runs ahead), so every timed batch was fetched, inflated by a
+    bridge fetch thread straight into the replica log (codecs.h ``decompress_into``) and then
+    CRC-checked and decoded on the device inside the timed region."""
+    B = args.batch_size
+    stage, topic = f"stage_{codec}", f"bench_{codec}"
+    broker.create_topic(stage, n_parts)
+    broker.create_topic(topic, n_parts)
+    per = int(math.ceil((warm + steps) * B * 1.1 / len(mine))) + B
+    warm_per = int(math.ceil(warm * B * 1.5 / len(mine))) + B
+    t = time.perf_counter()
+    packed = broker.copy_compressed("bench", stage, codec, partitions=mine, max_records=per)
+    compress_s = time.perf_counter() - t
+    broker.copy_compressed(stage, topic, None, partitions=mine, max_records=warm_per)
+    ld = make_loader(f"bench-bridge-{codec}", dtype, args.h2d, servers=server, topic=topic)
+    from torchkafka_amd import auto_commit
+
+    bit = iter(auto_commit(ld))
+    for _ in range(warm):
+        next(bit)
+    c0 = _bridge_counters(ld)
+    err = []
+
+    def produce():
+        try:
+            broker.copy_compressed(stage, topic, None, partitions=mine, start_record=warm_per, max_records=per)
+        except Exception as e:  # noqa: BLE001 - reported below
+            err.append(e)
+
+    pub = threading.Thread(target=produce, name=f"bench-produce-{codec}")
+    pub.start()
+    res = time_steps(R, bit, steps, ld)
+    pub.join()
+    c1 = _bridge_counters(ld)
+    if err:
+        raise err[0]
+    blk = steady_block(R, res, steps, args.dim)
+    d = {k: c1[k] - c0[k] for k in c1 if k != "fetch_threads"}
+    el = res["el"]
+    thread_s = c1["fetch_threads"] * el
+    inflate_s, recv_s, wait_s = d["inflate_ns"] / 1e9, d["recv_ns"] / 1e9, d["fetch_wait_ns"] / 1e9
+    other_ingest_s = max(0.0, d["ingest_ns"] / 1e9 - inflate_s)
+    blk.update({
+        "compression": codec,
+        "served_as": f"{codec} RecordBatches ({packed['batches']} batches of {args.records_per_batch} records per "
+                     "rank), produced into the served topic as the timed steps start",
+        "compression_ratio": round(packed["raw_bytes"] / max(1, packed["compressed_bytes"]), 2),
+        "wire_gb_per_s": round(d["wire_bytes"] / el / 1e9, 3),
+        "inflated_gb_per_s": round(d["inflated_bytes"] / el / 1e9, 3),
+        "inflated_batches_in_timed_region": d["inflated_batches"],
+        "fetch_threads": c1["fetch_threads"],
+        "inflate_gb_per_s_per_thread": round(d["inflated_bytes"] / max(1e-9, inflate_s) / 1e9, 3),
+        # a fetch thread's time over the timed region: inflating, reading record sets off the
+        # socket, the rest of the ingest walk (CRC of the compressed batch, index), waiting for
+        # Fetch responses; the remainder is request building, flow control and idle
+        "fetch_thread_time_share": {
+            "inflate": round(inflate_s / thread_s, 3), "recv": round(recv_s / thread_s, 3),
+            "other_ingest": round(other_ingest_s / thread_s, 3), "fetch_wait": round(wait_s / thread_s, 3)},
+        "compress_setup_s": round(compress_s, 2),
+        "bridge_errors": sum(br.errors for br in ld._bridges),
+    })
+    bit.close()
+    ld.close()
+    return blk
+
+
 def record_bytes(args) -> int:
     """Log bytes of one synthetic record: the f32 values, the 8-byte key and the record framing
     (~20 B of varints), plus its share of the 61-byte RecordBatch header."""
@@ -456,12 +547,17 @@ def run_config_blocks(R: "Rank", args) -> dict:
             a = m.parse(["--steps", str(args.config5_steps), "--device", dev, "--verify", args.verify])
             res = m.run(a, sync=R.sync)
             res.pop("loader", None)
+        elif name == "process":
+            m = importlib.import_module("process_override")
+            res = m.run(m.parse(["--steps", str(args.process_steps), "--device", dev]), sync=R.sync)
+            name = "process_override"
         elif name == "config1":
             m = importlib.import_module("config1_cpu_plumbing")
             res = m.run(m.parse(["--records", str(args.config1_records)]))
         else:
             continue
         res["block_wall_s"] = round(time.perf_counter() - t0, 2)
+        _progress(R, f"{name} block done in {res['block_wall_s']} s")
         out[name] = res
     return out
 
@@ -548,7 +644,7 @@ def run_rank(args) -> int:
     R.init_group()
 
     def make_loader(group: str, dtype, h2d: str, servers: str = url, commit: str = "async", ds=Records,
-                    verify: str | None = None, lockstep_mode=None):
+                    verify: str | None = None, lockstep_mode=None, topic: str = "bench"):
         return DeviceLoader(
             ds.placeholder(), B, num_workers=args.workers, device=device, dtype=dtype,
             slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
@@ -558,7 +654,7 @@ def run_rank(args) -> int:
             lockstep=lockstep if lockstep_mode is None else lockstep_mode,
             mirror_chunk_mib=args.mirror_chunk_mib, commit=commit, verify=verify or args.verify,
             **({"mirror_chunks": args.mirror_chunks} if args.mirror_chunks else {}),
-            worker_init_fn=ds.init_worker("bench", bootstrap_servers=servers, group_id=group,
+            worker_init_fn=ds.init_worker(topic, bootstrap_servers=servers, group_id=group,
                                           auto_offset_reset="earliest", check_crcs=not args.no_crc),
         )
 
@@ -598,6 +694,7 @@ def run_rank(args) -> int:
         sres = time_steps(R, it, steady, loader)
         s_stats = sres["stats"]
         steady_out = steady_block(R, sres, steady, args.dim)
+        _progress(R, f"steady_state {steady_out['records_per_s']:.0f} rec/s")
         if args.stats and rank == 0:
             print(json.dumps({"ring_at_steady_t0": sres["occ"]}), file=sys.stderr)
         x = sres["last"]
@@ -661,6 +758,7 @@ def run_rank(args) -> int:
             key = "steady_unverified" if ld.verify == "commit" else "steady_verified"
             blk["verify_wait_us_per_batch"] = round(eres["stats"].get("verify_wait_us_per_batch", 0.0), 3)
         extra_out[key] = blk
+        _progress(R, f"{key} {blk['records_per_s']:.0f} rec/s")
         eit.close()
         ld.close()
         if own_group:
@@ -706,8 +804,15 @@ def run_rank(args) -> int:
                     blk["sync_commits"] = st["sync_commits"]
                 blk["bridge_errors"] = sum(br.errors for br in ld._bridges)
                 bridge_out[mode] = blk
+                _progress(R, f"bridge {mode} {blk['records_per_s']:.0f} rec/s")
                 bit.close()
                 ld.close()
+                if world > 1:
+                    R.barrier()
+            for codec in [c for c in args.bridge_codecs.split(",") if c]:
+                bridge_out[codec] = bridge_codec_block(R, args, broker, mine, n_parts, codec, bsteps, extra_warm,
+                                                       make_loader, srv.address, dtypes[args.dtype])
+                _progress(R, f"bridge {codec} {bridge_out[codec]['records_per_s']:.0f} rec/s")
                 if world > 1:
                     R.barrier()
         finally:
@@ -794,8 +899,19 @@ def _native_build() -> dict:
             for name, b in build_info().items()}
 
 
+def _progress(R, what: str) -> None:
+    """One stderr line per finished block (rank 0): a long run shows where it is."""
+    if R.rank == 0:
+        print(f"[bench] {what} ({time.strftime('%H:%M:%S')})", file=sys.stderr, flush=True)
+
+
 def main() -> int:
     args = parse()
+    if os.environ.get("TK_BENCH_WATCHDOG"):
+        # diagnostic: every N seconds, every thread's Python stack to stderr (a run that stalls)
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["TK_BENCH_WATCHDOG"]), repeat=True)
     if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.self_launch):
         return launch_ranks(args)
     return run_rank(args)

@@ -192,7 +192,8 @@ def run(args, sync=None) -> dict:
         gs.drain()
         beside = gs.report(cut_ms)
         st = dl.stats_summary()
-        decode = (("device, HBM mirror filled by SDMA copies" if dl.plan.mirror else "device, zero-copy from the pinned logs")
+        decode = (("device, HBM mirror filled by SDMA copies" if dl.plan.mirror
+                   else "device, zero-copy from the pinned logs")
                   if (dl.plan.span or getattr(dl.plan, "json_span", False)) else "host workers")
         it.close()
         dl.close()

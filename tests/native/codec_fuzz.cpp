@@ -179,6 +179,50 @@ int main(int argc, char** argv) {
     }
     CHECK(threw && o2.size() <= 1024);
   }
+  // round trips through compress() (gzip, lz4 frame, zstd) into exact-size heap buffers: the
+  // exact size decodes, one byte less is kNoRoom, never a write past the buffer (ASan); mutated
+  // compressed bytes decode, refuse or report kNoRoom within the buffer
+  uint64_t trips = 0;
+  for (int it = 0; it < iters / 4 + 3; ++it) {
+    const size_t n = 1 + size_t(rng() % (it % 7 == 0 ? 300000 : 5000));
+    std::vector<uint8_t> plain(n);
+    const int alpha = 1 + int(rng() % 40);
+    for (size_t i = 0; i < n; ++i)
+      plain[i] = i > 20 && rng() % 3 ? plain[i - 1 - rng() % 20] : uint8_t(rng() % alpha);
+    for (int codec : {kCodecGzip, kCodecLz4, kCodecZstd}) {
+      if (codec == kCodecZstd && !zstd_available()) continue;
+      std::vector<uint8_t> z;
+      try {
+        compress(codec, plain.data(), n, z, it % 5 == 0 ? 9 : 0);
+      } catch (const KafkaError&) {
+        continue;  // the system library is not loadable
+      }
+      for (size_t cap : {n, n - 1, size_t(rng() % n)}) {
+        uint8_t* d = static_cast<uint8_t*>(std::malloc(cap ? cap : 1));
+        const size_t got = decompress_into(codec, z.data(), z.size(), d, cap);
+        if (cap >= n) CHECK(got == n && std::memcmp(d, plain.data(), n) == 0);
+        else CHECK(got == kNoRoom);
+        std::free(d);
+      }
+      std::vector<uint8_t> zb(z);
+      zb[rng() % zb.size()] ^= uint8_t(1 + rng() % 255);
+      uint8_t* zi = static_cast<uint8_t*>(std::malloc(zb.size()));
+      std::memcpy(zi, zb.data(), zb.size());
+      const size_t cap = size_t(rng() % (2 * n + 1));
+      uint8_t* d = static_cast<uint8_t*>(std::malloc(cap ? cap : 1));
+      try {
+        const size_t got = decompress_into(codec, zi, zb.size(), d, cap);
+        CHECK(got == kNoRoom || got <= cap);
+      } catch (const CorruptRecord&) {
+        ++refused;
+      }
+      std::free(d);
+      std::free(zi);
+      ++trips;
+    }
+  }
+  std::printf("codec round trips: %llu (liblz4 decoder %s)\n", (unsigned long long)trips,
+              lz4_library_available() ? "on" : "off");
   std::printf("codec fuzz: %d batches, %llu corrupted decodes survived, %llu rejected; JSON fuzz ok; "
               "decompressors: %llu decoded, %llu refused\n", iters,
               (unsigned long long)decoded, (unsigned long long)rejected, (unsigned long long)inflated,

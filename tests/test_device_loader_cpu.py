@@ -287,7 +287,7 @@ def test_state_dict_round_trip_resumes_exactly(broker):
             firsts.setdefault(p, o)
     assert firsts == {p: o for p, o in snap.items() if o < 200}
     with pytest.raises(ValueError):
-        dl2.load_state_dict({"version": 2, "offsets": {}})
+        dl2.load_state_dict({"version": 99, "offsets": {}})
 
 
 def _direct(ds_cls, broker, topic="t", group="g", **kw):
@@ -551,6 +551,12 @@ def test_native_loop_bad_verdict_commits_the_batches_before_and_never_yields(mon
 
         def committed(self):
             return []
+
+        def delivered_positions(self):
+            return []
+
+        def delivered_batches(self):
+            return 0
 
         def reset_stats(self):
             pass

@@ -20,7 +20,8 @@ import torch
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--normal", type=int, default=5)
-    ap.add_argument("--high-pool", type=int, default=4, help="then: spin on this many high-priority streams, probe one more")
+    ap.add_argument("--high-pool", type=int, default=4,
+                    help="then: spin on this many high-priority streams, probe one more")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)

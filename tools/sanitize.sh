@@ -28,6 +28,7 @@ export UBSAN_OPTIONS="halt_on_error=1 print_stacktrace=1"
 echo "== tsan ring_stress"; "$OUT/ring_stress_tsan" 4 3 ${TK_SAN_BATCHES:-2000}
 echo "== asan ring_stress"; "$OUT/ring_stress_asan" 4 3 ${TK_SAN_BATCHES:-2000}
 echo "== asan codec_fuzz"; "$OUT/codec_fuzz_asan" ${TK_SAN_FUZZ:-3000}
+echo "== asan codec_fuzz, built-in LZ4 decoder"; TORCHKAFKA_LZ4_LIB=0 "$OUT/codec_fuzz_asan" ${TK_SAN_FUZZ:-3000}
 echo "== tsan hip_queue"; "$OUT/hip_queue_tsan" ${TK_SAN_QUEUE:-50000}
 echo "== asan hip_queue"; "$OUT/hip_queue_asan" ${TK_SAN_QUEUE:-50000}
 echo "== asan span_window"; "$OUT/span_window_asan"

@@ -210,6 +210,23 @@ class SyntheticBroker:
                                int(max_size if max_size is not None else size), int(records_per_batch), int(seed),
                                int(threads), bool(keyed))
 
+    def copy_compressed(self, src_topic: str, dst_topic: str, compression: str | None, *,
+                        partitions: Iterable[int] | None = None, level: int = 0, start_record: int = 0,
+                        max_records: int = -1, threads: int | None = None) -> dict:
+        """Appends the batches of ``src_topic``'s partitions holding records ``[start_record,
+        max_records)`` of each (``-1``: to the end) to the same partitions of ``dst_topic``, each
+        batch compressed as a producer with ``compression_type`` = ``compression`` ("gzip", "lz4",
+        "zstd"; None: copied as they are) writes it: what a Kafka cluster's topic holds.  Served
+        over the wire protocol, a KafkaBridge inflates them.  Returns ``{"raw_bytes",
+        "compressed_bytes", "batches"}``."""
+        codec = {None: 0, "none": 0, "gzip": 1, "lz4": 3, "zstd": 4}[compression]
+        _, n, first = self.topic(src_topic)
+        parts = list(range(n)) if partitions is None else list(partitions)
+        dst = [self.pidx(dst_topic, p) for p in parts]
+        threads = threads or min(len(parts), max(1, min(16, (os.cpu_count() or 4))))
+        return dict(self._b.copy_compressed([first + p for p in parts], dst, codec, int(level), int(max_records),
+                                            int(threads), int(start_record)))
+
     def delete_records(self, topic: str, partition: int, before_offset: int) -> None:
         self._b.delete_records(self.pidx(topic, partition), int(before_offset))
 

@@ -41,12 +41,17 @@ PROCESS_ENV = {
     "TORCHKAFKA_NT_COPY": "0: plain (cached) stores when workers pack slots",
     "TORCHKAFKA_DRIVER_TRACE": "1: step-driver trace lines on stderr (debugging)",
     "TORCHKAFKA_NO_REBUILD": "1: never rebuild stale in-tree extensions at import",
-    "TORCHKAFKA_RCCL_WORDS": "kernel (default) / host / copy: how the RCCL lockstep's agreement words reach RCCL -- "
-                             "tiny copy kernels, RCCL on host-mapped memory, or hipMemcpyAsync (csrc/hip/rccl_lockstep.hip)",
+    "TORCHKAFKA_RCCL_WORDS": "kernel (default) / host / copy: how the RCCL lockstep's agreement words reach "
+                             "RCCL -- tiny copy kernels, RCCL on host-mapped memory, or hipMemcpyAsync "
+                             "(csrc/hip/rccl_lockstep.hip)",
     "TORCHKAFKA_LOCKSTEP_PRIORITY": "high (default) / normal: the RCCL lockstep stream's priority; high gives it a "
                                     "hardware queue of its own (tools/probes/queue_probe.py)",
-    "TORCHKAFKA_TORCH_NCCL_ACTIVE": "1: DeviceLoader.stream_plan() counts torch's own NCCL streams at world 1 (a world-1 "
-                                    "nccl group that ran a collective, as bench.py's N = 8 queue rehearsal does)",
+    "TORCHKAFKA_TORCH_NCCL_ACTIVE": "1: DeviceLoader.stream_plan() counts torch's own NCCL streams at world 1 "
+                                    "(a world-1 nccl group that ran a collective, as bench.py's N = 8 queue "
+                                    "rehearsal does)",
+    "TORCHKAFKA_DEFERRED_FREE": "0: a closing loader frees its device / pinned memory inline (hipFree waits for "
+                                "the whole device) instead of on the deferred-release thread (csrc/hip/reaper.h)",
+    "TORCHKAFKA_LZ4_LIB": "0: decode LZ4 blocks with the built-in decoder instead of the system liblz4.so.1",
     "TORCHKAFKA_DECODE_PRIORITY": "high / normal (default) / low: HIP stream priority of the decode streams "
                                   "(csrc/hip/engine.hip; no measured effect beside a GEMM, profiles/r05_s2)",
     "TORCHKAFKA_MIRROR_COPY_STREAMS": "copy streams of the HBM mirror, partitions split p % n (1..4, default 2)",

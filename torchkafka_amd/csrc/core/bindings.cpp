@@ -66,7 +66,17 @@ PYBIND11_MODULE(_tkcore, m) {
     decompress(codec, reinterpret_cast<const uint8_t*>(s.data()), s.size(), out);
     return py::bytes(reinterpret_cast<const char*>(out.data()), out.size());
   });
+  m.def("compress", [](int codec, py::bytes b, int level) {
+    std::string s = b;
+    std::vector<uint8_t> out;
+    {
+      py::gil_scoped_release nogil;
+      compress(codec, reinterpret_cast<const uint8_t*>(s.data()), s.size(), out, level);
+    }
+    return py::bytes(reinterpret_cast<const char*>(out.data()), out.size());
+  }, py::arg("codec"), py::arg("data"), py::arg("level") = 0);
   m.def("zstd_available", &zstd_available);
+  m.def("lz4_library_available", &lz4_library_available);
   m.def("client_versions", []() {
     std::map<int16_t, std::pair<int16_t, int16_t>> out;
     for (auto& [k, r] : wire::client_versions()) out[k] = {r.min, r.max};

@@ -155,6 +155,75 @@ void bind_broker(py::module_& m) {
              return d;
            },
            py::arg("pidx"), py::arg("data"), py::arg("from_offset") = -1, py::arg("keep_control") = false)
+      .def("copy_compressed",
+           [](Broker& b, std::vector<uint32_t> src, std::vector<uint32_t> dst, int codec, int level,
+              int64_t max_records, int threads, int64_t start_record) {
+             // Appends the batches of partitions `src` whose records lie in [start_record,
+             // max_records) of each (-1: to the end), compressed with `codec` batch by batch as a
+             // producer would (attributes, length and CRC rewritten; codec 0: copied as they are),
+             // to the partitions `dst`: the benchmarks' compressed topics.
+             if (src.size() != dst.size()) throw std::invalid_argument("copy_compressed: src and dst differ in length");
+             std::atomic<size_t> next{0};
+             std::atomic<uint64_t> raw{0}, packed{0}, batches{0};
+             std::mutex err_mu;
+             std::exception_ptr err;
+             auto work = [&]() {
+               std::vector<uint8_t> out;
+               try {
+                 for (size_t j; (j = next.fetch_add(1)) < src.size();) {
+                   PartitionEntry& P = b.part(src[j]);
+                   const uint64_t nb = P.n_batches.load(std::memory_order_acquire);
+                   const uint64_t icap = P.index_capacity;
+                   const IndexEntry* idx = b.index_base(src[j]);
+                   const uint8_t* log = b.log_base(src[j]);
+                   const int64_t start = P.log_start_offset.load(std::memory_order_acquire);
+                   for (uint64_t i = P.first_batch.load(std::memory_order_acquire); i < nb; ++i) {
+                     const IndexEntry& e = idx[i % icap];
+                     if (max_records >= 0 && e.base_offset >= start + max_records) break;
+                     if (e.base_offset < start + start_record) continue;
+                     const uint8_t* bt = log + e.pos;
+                     if (codec == kCodecNone) {
+                       out.assign(bt, bt + e.size);
+                     } else {
+                       out.assign(bt, bt + kBatchHeaderBytes);
+                       compress(codec, bt + kBatchHeaderBytes, e.size - kBatchHeaderBytes, out, level);
+                       const uint32_t be_len = __builtin_bswap32(uint32_t(out.size() - 12));
+                       std::memcpy(out.data() + kBatchLengthOffset, &be_len, 4);
+                       out[kBatchAttrOffset + 1] = uint8_t((out[kBatchAttrOffset + 1] & ~7) | (codec & 7));
+                       const uint32_t be_crc =
+                           __builtin_bswap32(crc32c(out.data() + kBatchAttrOffset, out.size() - kBatchAttrOffset));
+                       std::memcpy(out.data() + kBatchCrcOffset, &be_crc, 4);
+                     }
+                     uint64_t avail = 0;
+                     uint8_t* tail = b.log_tail(dst[j], &avail);
+                     if (out.size() > avail) throw KafkaError("copy_compressed: destination log full");
+                     std::memcpy(tail, out.data(), out.size());
+                     b.ingest(dst[j], out.size(), -1, true);
+                     raw += e.size;
+                     packed += out.size();
+                     ++batches;
+                   }
+                 }
+               } catch (...) {
+                 std::lock_guard<std::mutex> g(err_mu);
+                 if (!err) err = std::current_exception();
+               }
+             };
+             {
+               py::gil_scoped_release nogil;
+               std::vector<std::thread> ts;
+               for (int t = 0; t < std::max(1, std::min<int>(threads, int(src.size()))); ++t) ts.emplace_back(work);
+               for (auto& t : ts) t.join();
+             }
+             if (err) std::rethrow_exception(err);
+             py::dict d;
+             d["raw_bytes"] = raw.load();
+             d["compressed_bytes"] = packed.load();
+             d["batches"] = batches.load();
+             return d;
+           },
+           py::arg("src"), py::arg("dst"), py::arg("codec"), py::arg("level") = 0, py::arg("max_records") = -1,
+           py::arg("threads") = 8, py::arg("start_record") = 0)
       .def("position_of", &Broker::position_of)
       .def("ring_bytes", [](Broker& b, uint32_t p) { return b.part(p).ring_bytes.load(); })
       .def("first_batch", [](Broker& b, uint32_t p) { return b.part(p).first_batch.load(); })

@@ -124,6 +124,7 @@ void bind_wire(py::module_& m) {
       .def("assignment_epochs", &Replicator::assignment_epochs,
            "[(partition, epoch at which it was (re)assigned)] of the partitions owned now")
       .def_property_readonly("fetch_threads", &Replicator::fetch_threads)
+      .def_property_readonly("fetch_wait_ns", &Replicator::fetch_wait_ns)
       .def("last_error", &Replicator::last_error)
       .def("stats", [](Replicator& r) {
         py::list l;
@@ -142,6 +143,12 @@ void bind_wire(py::module_& m) {
           d["throttled"] = s.throttled;
           d["released"] = s.released;
           d["owned"] = s.owned;
+          d["wire_bytes"] = s.wire_bytes;
+          d["recv_ns"] = s.recv_ns;
+          d["ingest_ns"] = s.ingest_ns;
+          d["inflate_ns"] = s.inflate_ns;
+          d["inflated_batches"] = s.inflated_batches;
+          d["inflated_bytes"] = s.inflated_bytes;
           l.append(d);
         }
         return l;

@@ -14,6 +14,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <thread>
 
@@ -479,25 +480,40 @@ Broker::Ingested Broker::ingest(uint32_t pidx, uint64_t len, int64_t from_offset
           in_len = spill.size();
           r = 0;
         }
-        plain.assign(in + r, in + r + kBatchHeaderBytes);
         // an inflated batch larger than the log (or its ring) could never be stored
-        const uint64_t cap = ring ? P.ring_bytes.load(std::memory_order_relaxed) : P.log_capacity;
-        decompress(codec, in + r + kBatchHeaderBytes, total - kBatchHeaderBytes, plain,
-                   size_t(std::min<uint64_t>(cap, kMaxInflatedBytes)));
-        const uint32_t new_len = uint32_t(plain.size() - 12);
-        const uint32_t be_len = __builtin_bswap32(new_len);
-        std::memcpy(plain.data() + kBatchLengthOffset, &be_len, 4);
-        plain[kBatchAttrOffset + 1] = uint8_t(plain[kBatchAttrOffset + 1] & ~7);  // attributes: no codec
-        const uint32_t be_crc = __builtin_bswap32(crc32c(plain.data() + kBatchAttrOffset, plain.size() - kBatchAttrOffset));
-        std::memcpy(plain.data() + kBatchCrcOffset, &be_crc, 4);
-        BatchHeader ph = parse_batch_header(plain.data(), plain.size());
-        if (!fits(plain.size())) {
+        const uint64_t cap = std::min<uint64_t>(ring ? P.ring_bytes.load(std::memory_order_relaxed) : P.log_capacity,
+                                                kMaxInflatedBytes);
+        const auto t0 = std::chrono::steady_clock::now();
+        // straight into the log, after what this walk kept: the input now lives in `spill`
+        uint8_t* dst = base + w;
+        const uint64_t space = std::min<uint64_t>(room - w, cap);
+        size_t got = kNoRoom;
+        if (space > kBatchHeaderBytes && fits(kBatchHeaderBytes))
+          got = decompress_into(codec, in + r + kBatchHeaderBytes, total - kBatchHeaderBytes, dst + kBatchHeaderBytes,
+                                size_t(space - kBatchHeaderBytes));
+        if (got == kNoRoom) {
+          // does not fit what is left now: inflate aside, bounded by what the log could ever hold
+          // (corrupt beyond that), and leave it for a later fetch once consumers freed room
+          plain.assign(in + r, in + r + kBatchHeaderBytes);
+          decompress(codec, in + r + kBatchHeaderBytes, total - kBatchHeaderBytes, plain, size_t(cap));
+          out.inflate_ns += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                         std::chrono::steady_clock::now() - t0).count());
           out.consumed = consumed_base + r;
           out.next_offset = h.base_offset;  // not taken: fetched again
           out.full = true;
           break;
         }
-        publish(plain.data(), plain.size(), ph);
+        std::memcpy(dst, in + r, kBatchHeaderBytes);
+        const uint64_t plain_total = kBatchHeaderBytes + got;
+        const uint32_t be_len = __builtin_bswap32(uint32_t(plain_total - 12));
+        std::memcpy(dst + kBatchLengthOffset, &be_len, 4);
+        dst[kBatchAttrOffset + 1] = uint8_t(dst[kBatchAttrOffset + 1] & ~7);  // attributes: no codec
+        const uint32_t be_crc = __builtin_bswap32(crc32c(dst + kBatchAttrOffset, plain_total - kBatchAttrOffset));
+        std::memcpy(dst + kBatchCrcOffset, &be_crc, 4);
+        out.inflate_ns += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                       std::chrono::steady_clock::now() - t0).count());
+        out.inflated_bytes += plain_total;
+        publish(dst, plain_total, parse_batch_header(dst, plain_total));
         ++out.inflated;
       }
     }

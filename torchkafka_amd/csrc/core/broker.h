@@ -219,14 +219,17 @@ class Broker {
     uint64_t consumed = 0;     // bytes of whole batches walked (kept or dropped)
     uint64_t kept_bytes = 0;
     uint32_t kept = 0, control = 0, inflated = 0;  // inflated: compressed batches stored decompressed
+    uint64_t inflated_bytes = 0;  // bytes of those batches as stored
+    uint64_t inflate_ns = 0;      // time spent inflating them (+ their fresh CRC)
     bool full = false;         // stopped at a batch the space left could not hold
     int64_t next_offset = -1;  // next offset to fetch (-1: no whole batch in the data)
   };
   // Walks the RecordBatches received at log_tail(): keeps (indexes, publishes) whole data
   // batches at or beyond `from_offset`, drops control batches (transaction markers) and
   // batches already held, compacting in place; a trailing partial batch is left for the next
-  // fetch to overwrite.  Compressed batches (gzip/snappy/lz4, codecs.h) are CRC-checked and stored
-  // inflated, as plain RecordBatch v2 with a fresh CRC: the device path decodes raw records.
+  // fetch to overwrite.  Compressed batches (gzip/snappy/lz4/zstd, codecs.h) are CRC-checked and
+  // inflated straight into the log, as plain RecordBatch v2 with a fresh CRC: the device path
+  // decodes raw records.  Runs on the calling (fetch) thread.
   // keep_control: store control batches too (a broker's own log, e.g. the wire server's tests).
   // `limit`: bytes from the write position the batches may occupy (0: up to the capacity); a batch
   // that does not fit ends the walk (Ingested::full) and is fetched again later.

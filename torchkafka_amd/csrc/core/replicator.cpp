@@ -100,9 +100,10 @@ void Replicator::start() {
   // fetch threads: partitions grouped by leader, leaders spread over the threads
   std::map<int32_t, std::vector<Part*>> by_leader;
   for (auto& p : parts_) by_leader[c.leader(cfg_.topic, p->partition)].push_back(p.get());
-  // default: one thread per leader, and at least 4 when there are fewer leaders than that -- one
-  // connection per thread, so a small cluster is not held to one socket's receive rate
-  int n_threads = cfg_.fetchers > 0 ? cfg_.fetchers : std::min<int>(8, std::max<int>(int(by_leader.size()), 4));
+  // default: one thread per partition, at most 8 (and at least one per leader): a thread inflates
+  // the compressed batches it receives, so compressed topics spread that work over the threads
+  int n_threads = cfg_.fetchers > 0 ? cfg_.fetchers
+                                    : std::max<int>(int(by_leader.size()), std::min<int>(8, int(parts_.size())));
   n_threads = std::max(1, std::min<int>(n_threads, int(parts_.size())));
   std::vector<std::vector<Part*>> per(static_cast<size_t>(n_threads));
   size_t k = 0;
@@ -449,7 +450,11 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
         const int16_t fv = k.version(wire::kFetch);
         k.send(wire::kFetch, fv, c->client_id(),
                wire::fetch_request(fv, cfg_.topic, req, wait, cfg_.min_bytes, cfg_.max_bytes));
+        const auto t_sent = std::chrono::steady_clock::now();
         k.begin_response(cfg_.timeout_ms + wait);
+        fetch_wait_ns_.fetch_add(uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                              std::chrono::steady_clock::now() - t_sent).count()),
+                                 std::memory_order_relaxed);
         wire::fetch_response_header(k, fv);
         std::vector<Part*> out_of_range;  // reset once the response is read: ListOffsets reuses the connection
         const int32_t nt = k.r32();
@@ -492,10 +497,21 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
               failed[p] = since[p];
               continue;
             }
+            const auto t_recv = std::chrono::steady_clock::now();
             k.read(tail, size_t(len));  // the record set lands in the log tail: no second copy
+            const auto t_ingest = std::chrono::steady_clock::now();
+            p->wire_bytes.fetch_add(uint64_t(len), std::memory_order_relaxed);
+            p->recv_ns.fetch_add(uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(t_ingest - t_recv).count()),
+                                 std::memory_order_relaxed);
             try {
               const Broker::Ingested in = local_->ingest(p->pidx, uint64_t(len), p->fetch_offset.load(), false,
                                                          cfg_.ring_bytes ? avail : 0);
+              p->ingest_ns.fetch_add(uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                                  std::chrono::steady_clock::now() - t_ingest).count()),
+                                     std::memory_order_relaxed);
+              p->inflate_ns.fetch_add(in.inflate_ns, std::memory_order_relaxed);
+              p->inflated.fetch_add(in.inflated, std::memory_order_relaxed);
+              p->inflated_bytes.fetch_add(in.inflated_bytes, std::memory_order_relaxed);
               if (in.next_offset > p->fetch_offset.load()) p->fetch_offset.store(in.next_offset);
               p->bytes.fetch_add(in.kept_bytes, std::memory_order_relaxed);
               p->batches.fetch_add(in.kept, std::memory_order_relaxed);
@@ -677,7 +693,9 @@ std::vector<ReplicaPartStats> Replicator::stats() {
   for (auto& p : parts_)
     v.push_back(ReplicaPartStats{p->partition, p->pidx, p->start_offset, p->fetch_offset.load(), p->remote_hw.load(),
                                  p->forwarded.load(), p->bytes.load(), p->batches.load(), p->control.load(),
-                                 p->fetches.load(), p->throttled.load(), p->released.load(), p->owned.load()});
+                                 p->fetches.load(), p->throttled.load(), p->released.load(), p->owned.load(),
+                                 p->wire_bytes.load(), p->recv_ns.load(), p->ingest_ns.load(), p->inflate_ns.load(),
+                                 p->inflated.load(), p->inflated_bytes.load()});
   return v;
 }
 

@@ -56,7 +56,7 @@ struct ReplicaConfig {
   int32_t timeout_ms = 30000;
   int64_t max_lag_bytes = int64_t(1) << 30;
   int32_t commit_interval_ms = 5;
-  int32_t fetchers = 0;                // fetch threads (0: one per partition leader, at most 8)
+  int32_t fetchers = 0;                // fetch threads (0: one per partition, at most 8; at least one per leader)
   bool release_consumed = true;        // free committed log bytes (punch holes; kReleaseConsumed)
   uint64_t release_bytes = 256u << 20; // ... keeping this many consumed bytes per partition resident
   uint64_t release_step = 1u << 30;    // ... in bursts, once a partition has this many releasable bytes
@@ -82,6 +82,15 @@ struct ReplicaPartStats {
   uint64_t throttled;       // fetch rounds skipped by flow control
   uint64_t released;        // log bytes released below the committed position
   bool owned;               // subscribe mode: assigned to this member now
+  // where a fetch thread's time goes, per partition: the record sets as received (compressed),
+  // the time reading them off the socket into the log, the whole ingest walk, and the part of it
+  // spent inflating compressed batches (decode + fresh CRC), which yielded inflated_bytes
+  uint64_t wire_bytes;
+  uint64_t recv_ns;
+  uint64_t ingest_ns;
+  uint64_t inflate_ns;
+  uint64_t inflated_batches;
+  uint64_t inflated_bytes;
 };
 
 class Replicator {
@@ -126,6 +135,8 @@ class Replicator {
   // Never set any more (rebalances are followed in process); kept for API compatibility.
   bool fenced() const { return false; }
   int fetch_threads() const { return n_fetch_threads_; }
+  // Summed over the fetch threads: time from a Fetch request sent to its response's first bytes.
+  uint64_t fetch_wait_ns() const { return fetch_wait_ns_.load(std::memory_order_relaxed); }
   // Blocks until every replicated partition has fetched up to the cluster's high watermark as
   // seen at call time (tests, tools); false on timeout.
   bool wait_caught_up(int timeout_ms);
@@ -140,6 +151,7 @@ class Replicator {
     std::atomic<int64_t> forwarded{-1};
     std::atomic<uint64_t> bytes{0}, batches{0}, control{0}, fetches{0}, throttled{0};
     std::atomic<uint64_t> released{0};  // log bytes [0, released) freed (committed past)
+    std::atomic<uint64_t> wire_bytes{0}, recv_ns{0}, ingest_ns{0}, inflate_ns{0}, inflated{0}, inflated_bytes{0};
     std::atomic<bool> owned{true};       // subscribe mode: assigned to this member now
     std::atomic<uint64_t> since{0};      // assignment epoch at which it was (re)assigned
     std::mutex mu;                       // a fetch's write into the log vs. a restart of the partition
@@ -186,6 +198,7 @@ class Replicator {
   std::atomic<uint64_t> epoch_{0}, rebalances_{0};
   int64_t last_heartbeat_ms_ = 0;
   int n_fetch_threads_ = 0;
+  std::atomic<uint64_t> fetch_wait_ns_{0};
 };
 
 }  // namespace tk

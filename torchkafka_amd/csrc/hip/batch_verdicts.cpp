@@ -1,5 +1,7 @@
 #include "batch_verdicts.h"
 
+#include "reaper.h"
+
 #include <algorithm>
 #include <cstring>
 #include <ctime>
@@ -29,11 +31,13 @@ void host_mapped(size_t n, T** host, T** dev, const char* what) {
 
 BatchVerdicts::~BatchVerdicts() {
   // no kernel still writes a status word: the driver waited for every handed slot (quiesce)
-  if (perr_host_) hipHostFree(perr_host_);
-  if (jinfo_host_) hipHostFree(jinfo_host_);
-  if (patch_dev_) hipFree(patch_dev_);
-  if (part_host_) hipHostFree(part_host_);
-  if (ctr_dev_) hipFree(ctr_dev_);
+  // hipFree / hipHostFree wait for the whole device: the deferred-release thread runs them (reaper.h)
+  const int dev = q_ ? q_->device() : 0;
+  Reaper::free_host(dev, perr_host_);
+  Reaper::free_host(dev, jinfo_host_);
+  Reaper::free_device(dev, patch_dev_);
+  Reaper::free_host(dev, part_host_);
+  Reaper::free_device(dev, ctr_dev_);
 }
 
 void BatchVerdicts::ensure_status() {

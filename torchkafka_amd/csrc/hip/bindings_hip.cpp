@@ -12,6 +12,7 @@
 #include "engine.h"
 #include "driver.h"
 #include "rccl_lockstep.h"
+#include "reaper.h"
 
 namespace py = pybind11;
 using namespace tkh;
@@ -75,6 +76,17 @@ PYBIND11_MODULE(_tkhip, m) {
   });
 
   m.def("api_bench", &api_bench, py::arg("device") = 0, py::arg("iters") = 10000);
+  m.def("reaper_drain", [](int timeout_ms) {
+    py::gil_scoped_release nogil;
+    return Reaper::drain(timeout_ms);
+  }, py::arg("timeout_ms") = 60000, "waits until every deferred release (loader teardown) ran");
+  m.def("reaper_stats", []() {
+    py::dict d;
+    d["enabled"] = Reaper::enabled();
+    d["posted"] = Reaper::posted();
+    d["released"] = Reaper::released();
+    return d;
+  });
 
   m.def(
       "collate_fixed",

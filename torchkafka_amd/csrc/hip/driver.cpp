@@ -2,6 +2,7 @@
 
 #include "dtypes.h"
 #include "hip_queue.h"
+#include "reaper.h"
 
 #include <unistd.h>
 
@@ -30,7 +31,8 @@ namespace tkh {
 MainDriver::MainDriver(Engine* engine, const std::string& ring_name, const std::string& broker_url,
                        const std::string& group, int prefetch, bool in_order, int default_src_dt)
     : eng_(engine), prefetch_(std::max(0, prefetch)) {
-  auto ring = tk::Ring::open(ring_name);
+  std::shared_ptr<tk::Ring> ring = tk::Ring::open(ring_name);
+  ring_keep_ = ring;
   if (int(ring->n_slots()) > eng_->n_slots()) throw std::invalid_argument("driver: engine has fewer slots than ring");
   // Pin THIS mapping of the ring: it is the one whose addresses the copies use
   // (another mapping of the same shm object has different virtual addresses).
@@ -54,11 +56,14 @@ MainDriver::~MainDriver() {
   // Quiesce this loader only -- never the device: the user's stream may hold a training step's
   // work for milliseconds, and a device-wide synchronize here would block the host on it.
   quiesce();
+  // Memory and registrations go to the deferred-release thread (reaper.h): hipFree and
+  // hipHostUnregister wait for the whole device, and this runs on the training thread.
   pins_.reset();  // pinned log ranges: every kernel that read them completed (quiesce)
-  if (stage_dev_) hipFree(stage_dev_);
+  Reaper::free_device(eng_->device(), stage_dev_);
+  stage_dev_ = nullptr;
   if (registered_) {
     try {
-      eng_->unregister_host();  // before the ring's mapping goes away (poller_)
+      eng_->unregister_host_deferred(ring_keep_);  // the release keeps the ring's mapping alive
     } catch (...) {
     }
   }

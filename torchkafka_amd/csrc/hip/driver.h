@@ -423,6 +423,7 @@ class MainDriver {
 
   Engine* eng_;
   bool registered_ = false;
+  std::shared_ptr<tk::Ring> ring_keep_;  // the mapping the engine registered: kept until the unregistration ran
   int prefetch_;
   std::shared_ptr<tk::Broker> broker_;
   std::unique_ptr<CommitLedger> ledger_;

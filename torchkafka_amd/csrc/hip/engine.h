@@ -36,6 +36,9 @@ class Engine {
 
   void register_host(void* p, size_t len);
   void unregister_host();
+  // Hands the unregistration to the deferred-release thread (reaper.h) after this engine's own
+  // streams drained; `keep` holds the registered mapping until it ran.
+  void unregister_host_deferred(std::shared_ptr<void> keep);
   bool host_registered() const { return host_ptr_ != nullptr; }
 
   // DMA mode: start the slot's copy (its stream runs the slot's kernel after it).

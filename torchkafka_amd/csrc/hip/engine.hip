@@ -28,6 +28,7 @@
 #include "crc32c.h"
 #include "engine.h"
 #include "hip_queue.h"
+#include "reaper.h"
 #include "span_decode.h"
 
 namespace tkh {
@@ -68,11 +69,14 @@ Engine::~Engine() {
   }
   hipSetDevice(device_);
   for (auto st : streams_) hipStreamSynchronize(st);
-  if (host_ptr_) hipHostUnregister(host_ptr_);
+  if (host_ptr_) {  // registered by the user, never released: deferred like the rest (reaper.h)
+    void* p = host_ptr_;
+    Reaper::post(device_, [p] { (void)hipHostUnregister(p); });
+  }
   for (auto e : done_) hipEventDestroy(e);
   for (auto e : copied_) hipEventDestroy(e);
-  if (staging_) hipFree(staging_);
-  if (span_tabs_) hipFree(span_tabs_);
+  Reaper::free_device(device_, staging_);
+  Reaper::free_device(device_, span_tabs_);
   for (auto st : decode_streams_)
     if (st) {
       hipStreamSynchronize(st);
@@ -101,6 +105,16 @@ void Engine::unregister_host() {
   if (!host_ptr_) return;
   synchronize();
   TKH_CHECK(hipHostUnregister(host_ptr_));
+  host_ptr_ = nullptr;
+  host_dev_ = nullptr;
+  host_len_ = 0;
+}
+
+void Engine::unregister_host_deferred(std::shared_ptr<void> keep) {
+  if (!host_ptr_) return;
+  synchronize();  // this engine's streams: the user's are not waited for
+  void* p = host_ptr_;
+  Reaper::post(device_, [p, keep = std::move(keep)] { (void)hipHostUnregister(p); });
   host_ptr_ = nullptr;
   host_dev_ = nullptr;
   host_len_ = 0;

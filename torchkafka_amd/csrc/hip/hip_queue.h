@@ -60,6 +60,7 @@ class HipQueue {
     return seq <= done_.load(std::memory_order_acquire);
   }
   void check() const;  // throws the thread's failure, if any
+  int device() const { return device_; }
   uint64_t calls() const { return done_.load(std::memory_order_relaxed); }
   // Runs everything queued, then stops the thread; gives up waiting after `timeout_ms` (logged).
   // Also run for every live queue at process exit (atexit, registered when the first thread

@@ -1,5 +1,7 @@
 #include "log_mirror.h"
 
+#include "reaper.h"
+
 #include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
@@ -49,8 +51,7 @@ LogMirror::~LogMirror() {
   for (auto& c : cs_)
     if (c.stream) hipStreamSynchronize(c.stream);
   // no decode kernel still reads a buffer: the owner (LogPins) synchronized the decode streams
-  for (auto& P : parts_)
-    if (P.dev) hipFree(P.dev);
+  for (auto& P : parts_) Reaper::free_device(device_, P.dev);  // hipFree waits for the whole device
   for (auto e : pool_) hipEventDestroy(e);
   for (auto& c : cs_) {
     if (c.copied) hipEventDestroy(c.copied);

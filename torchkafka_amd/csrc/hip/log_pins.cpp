@@ -1,5 +1,7 @@
 #include "log_pins.h"
 
+#include "reaper.h"
+
 #include <algorithm>
 #include <chrono>
 #include <stdexcept>
@@ -30,12 +32,24 @@ LogPins::~LogPins() {
   } catch (...) {
   }
   mirror_.reset();  // its copies read the pinned logs: before they are unregistered
+  // the registrations go to the deferred-release thread (reaper.h), which holds the broker's
+  // mapping until they are gone and only then tells the replicator the logs are unpinned
+  std::vector<std::pair<uint32_t, std::vector<void*>>> regs;
   for (size_t pidx = 0; pidx < reg_ranges_.size(); ++pidx) {
     auto& q = reg_ranges_[pidx];
-    for (auto& r : q) hipHostUnregister(r.first);
-    if (!q.empty() && broker_) broker_->part(uint32_t(pidx)).pinned.fetch_sub(1, std::memory_order_acq_rel);
+    if (q.empty()) continue;
+    std::vector<void*> ps;
+    for (auto& r : q) ps.push_back(r.first);
+    regs.emplace_back(uint32_t(pidx), std::move(ps));
   }
-  if (bases_dev_) hipFree(bases_dev_);
+  if (!regs.empty())
+    Reaper::post(eng_->device(), [regs = std::move(regs), broker = broker_] {
+      for (auto& [pidx, ps] : regs) {
+        for (void* p : ps) (void)hipHostUnregister(p);
+        if (broker) broker->part(pidx).pinned.fetch_sub(1, std::memory_order_acq_rel);
+      }
+    });
+  Reaper::free_device(eng_->device(), bases_dev_);
 }
 
 void LogPins::enable_direct() {

@@ -1,5 +1,7 @@
 #include "rccl_lockstep.h"
 
+#include "reaper.h"
+
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
@@ -124,9 +126,9 @@ RcclLockstep::~RcclLockstep() {
   if (!aborted_ && stream_) hipStreamSynchronize(stream_);
   if (comm_) api_->CommDestroy(static_cast<ncclComm_t>(comm_));  // null once aborted
   for (auto e : ev_) hipEventDestroy(e);
-  if (d_) hipFree(d_);
-  if (h_in_) hipHostFree(h_in_);
-  if (h_out_) hipHostFree(h_out_);
+  Reaper::free_device(device_, d_);  // hipFree / hipHostFree wait for the whole device (reaper.h)
+  Reaper::free_host(device_, h_in_);
+  Reaper::free_host(device_, h_out_);
   if (stream_) hipStreamDestroy(stream_);
   delete api_;
 }

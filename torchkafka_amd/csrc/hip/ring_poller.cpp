@@ -4,7 +4,7 @@
 
 namespace tkh {
 
-RingPoller::RingPoller(std::unique_ptr<tk::Ring> ring, Engine* engine, LogPins* pins, CommitLedger* ledger,
+RingPoller::RingPoller(std::shared_ptr<tk::Ring> ring, Engine* engine, LogPins* pins, CommitLedger* ledger,
                        tk::Broker* broker, bool in_order, int default_src_dt)
     : ring_(std::move(ring)),
       eng_(engine),

@@ -52,7 +52,7 @@ struct SlotView {
 
 class RingPoller {
  public:
-  RingPoller(std::unique_ptr<tk::Ring> ring, Engine* engine, LogPins* pins, CommitLedger* ledger,
+  RingPoller(std::shared_ptr<tk::Ring> ring, Engine* engine, LogPins* pins, CommitLedger* ledger,
              tk::Broker* broker, bool in_order, int default_src_dt);
 
   // One ring acquisition: 1 a batch was staged, 0 an empty slot without watermarks was consumed
@@ -82,7 +82,7 @@ class RingPoller {
  private:
   int acquire(bool block, int64_t timeout_ms);
 
-  std::unique_ptr<tk::Ring> ring_;
+  std::shared_ptr<tk::Ring> ring_;
   Engine* eng_;
   LogPins* pins_;
   CommitLedger* ledger_;
