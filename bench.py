@@ -618,9 +618,13 @@ def run_rank(args) -> int:
         extra = []
     extra_warm = max(50, args.warmup)
 
+    bsteps = args.bridge_steps if args.bridge_steps is not None else (8000 if device.type == "cuda" else 20)
+
     def backlog(steady_n, extra_n):
+        # every block re-reads the topic from the earliest offset under a group of its own: the
+        # longest one sets the backlog (a block that outran it would wait for records forever)
         consumed = max(args.warmup + args.steps * (1 + args.window_trace) + steady_n,
-                       (extra_warm + extra_n) if extra else 0)
+                       (extra_warm + extra_n) if extra else 0, (extra_warm + bsteps) if bsteps > 0 else 0)
         batches = consumed + args.workers * ((args.slots_per_worker or 8) + 2)
         return int(math.ceil(batches * B * 1.25 / max(1, len(mine)))) + B
 
@@ -769,7 +773,6 @@ def run_rank(args) -> int:
 
     # the Kafka-protocol route: this rank's partitions over a loopback wire server -> bridge replica
     bridge_out = None
-    bsteps = args.bridge_steps if args.bridge_steps is not None else (8000 if device.type == "cuda" else 20)
     if bsteps > 0:
         from torchkafka_amd.broker import NativeWireServer
 

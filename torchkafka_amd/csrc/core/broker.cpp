@@ -492,10 +492,13 @@ Broker::Ingested Broker::ingest(uint32_t pidx, uint64_t len, int64_t from_offset
           got = decompress_into(codec, in + r + kBatchHeaderBytes, total - kBatchHeaderBytes, dst + kBatchHeaderBytes,
                                 size_t(space - kBatchHeaderBytes));
         if (got == kNoRoom) {
-          // does not fit what is left now: inflate aside, bounded by what the log could ever hold
-          // (corrupt beyond that), and leave it for a later fetch once consumers freed room
-          plain.assign(in + r, in + r + kBatchHeaderBytes);
-          decompress(codec, in + r + kBatchHeaderBytes, total - kBatchHeaderBytes, plain, size_t(cap));
+          // does not fit what is left now: left for a later fetch once consumers freed room.  With
+          // plenty of room free, inflate it aside to tell a batch larger than the log could ever
+          // hold (corrupt: thrown) from one that only needs more room.
+          if (space >= std::min<uint64_t>(cap / 4, uint64_t(32) << 20)) {
+            plain.assign(in + r, in + r + kBatchHeaderBytes);
+            decompress(codec, in + r + kBatchHeaderBytes, total - kBatchHeaderBytes, plain, size_t(cap));
+          }
           out.inflate_ns += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
                                          std::chrono::steady_clock::now() - t0).count());
           out.consumed = consumed_base + r;
@@ -513,6 +516,7 @@ Broker::Ingested Broker::ingest(uint32_t pidx, uint64_t len, int64_t from_offset
         out.inflate_ns += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
                                        std::chrono::steady_clock::now() - t0).count());
         out.inflated_bytes += plain_total;
+        out.inflated_from += total;
         publish(dst, plain_total, parse_batch_header(dst, plain_total));
         ++out.inflated;
       }

@@ -220,6 +220,7 @@ class Broker {
     uint64_t kept_bytes = 0;
     uint32_t kept = 0, control = 0, inflated = 0;  // inflated: compressed batches stored decompressed
     uint64_t inflated_bytes = 0;  // bytes of those batches as stored
+    uint64_t inflated_from = 0;   // ... and as received (compressed)
     uint64_t inflate_ns = 0;      // time spent inflating them (+ their fresh CRC)
     bool full = false;         // stopped at a batch the space left could not hold
     int64_t next_offset = -1;  // next offset to fetch (-1: no whole batch in the data)

@@ -358,7 +358,12 @@ int64_t Replicator::keep_offset(Part& p) {
 // Write room for the next record set: a ring log reuses the bytes of committed batches, a linear
 // log has its tail up to the capacity.
 uint8_t* Replicator::room(Part& p, uint64_t* avail) {
-  if (cfg_.ring_bytes) return local_->ring_reserve(p.pidx, uint64_t(cfg_.partition_max_bytes), keep_offset(p), avail);
+  if (cfg_.ring_bytes) {
+    // a compressed topic inflates: reserve room for what a full Fetch inflates to (<= ring / 4)
+    const uint64_t want = std::min<uint64_t>(uint64_t(cfg_.partition_max_bytes) * p.ratio16.load() / 16,
+                                             std::max<uint64_t>(cfg_.ring_bytes / 4, uint64_t(cfg_.partition_max_bytes)));
+    return local_->ring_reserve(p.pidx, want, keep_offset(p), avail);
+  }
   return local_->log_tail(p.pidx, avail);
 }
 
@@ -440,8 +445,10 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
             failed[p] = p->since.load();
             continue;
           }
+          // compressed data inflates by ratio16 / 16 in the log: ask for what will fit
+          const uint64_t fit = std::max<uint64_t>(avail * 16 / p->ratio16.load(), 4096);
           req.push_back({p->partition, p->fetch_offset.load(),
-                         int32_t(std::min<uint64_t>(uint64_t(cfg_.partition_max_bytes), avail))});
+                         int32_t(std::min<uint64_t>({uint64_t(cfg_.partition_max_bytes), avail, fit}))});
           lookup[p->partition] = p;
           since[p] = p->since.load();
         }
@@ -512,6 +519,9 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
               p->inflate_ns.fetch_add(in.inflate_ns, std::memory_order_relaxed);
               p->inflated.fetch_add(in.inflated, std::memory_order_relaxed);
               p->inflated_bytes.fetch_add(in.inflated_bytes, std::memory_order_relaxed);
+              if (in.inflated_from)
+                p->ratio16.store(uint32_t(std::clamp<uint64_t>(in.inflated_bytes * 16 / in.inflated_from, 16, 16 * 64)),
+                                 std::memory_order_relaxed);
               if (in.next_offset > p->fetch_offset.load()) p->fetch_offset.store(in.next_offset);
               p->bytes.fetch_add(in.kept_bytes, std::memory_order_relaxed);
               p->batches.fetch_add(in.kept, std::memory_order_relaxed);

@@ -152,6 +152,9 @@ class Replicator {
     std::atomic<uint64_t> bytes{0}, batches{0}, control{0}, fetches{0}, throttled{0};
     std::atomic<uint64_t> released{0};  // log bytes [0, released) freed (committed past)
     std::atomic<uint64_t> wire_bytes{0}, recv_ns{0}, ingest_ns{0}, inflate_ns{0}, inflated{0}, inflated_bytes{0};
+    // inflation of the compressed batches last received, x16 (16: uncompressed): a ring replica
+    // reserves that much more room and asks for that much less per Fetch, so what it fetches fits
+    std::atomic<uint32_t> ratio16{16};
     std::atomic<bool> owned{true};       // subscribe mode: assigned to this member now
     std::atomic<uint64_t> since{0};      // assignment epoch at which it was (re)assigned
     std::mutex mu;                       // a fetch's write into the log vs. a restart of the partition
