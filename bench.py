@@ -399,13 +399,14 @@ def _bridge_counters(loader) -> dict:
     """Where the bridges' fetch threads spent their time, summed over partitions and threads."""
     keys = ("bytes", "wire_bytes", "recv_ns", "ingest_ns", "inflate_ns", "inflated_batches", "inflated_bytes")
     out = {k: 0 for k in keys}
-    out["fetch_wait_ns"] = out["fetch_threads"] = 0
+    out["fetch_wait_ns"] = out["fetch_threads"] = out["inflate_threads"] = 0
     for br in loader._bridges:
         for st in br.stats():
             for k in keys:
                 out[k] += int(st[k])
         out["fetch_wait_ns"] += int(br._r.fetch_wait_ns)
         out["fetch_threads"] += int(br._r.fetch_threads)
+        out["inflate_threads"] += int(br._r.inflate_threads)
     return out
 
 
@@ -451,9 +452,12 @@ def bridge_codec_block(R: "Rank", args, broker, mine, n_parts, codec, steps, war
     if err:
         raise err[0]
     blk = steady_block(R, res, steps, args.dim)
-    d = {k: c1[k] - c0[k] for k in c1 if k != "fetch_threads"}
+    d = {k: c1[k] - c0[k] for k in c1 if k not in ("fetch_threads", "inflate_threads")}
     el = res["el"]
     thread_s = c1["fetch_threads"] * el
+    # compressed partitions are inflated by an inflater thread per fetch thread (replicator.cpp),
+    # overlapping the fetch thread's wait for its next Fetch response
+    inflater_s = (c1["inflate_threads"] or c1["fetch_threads"]) * el
     inflate_s, recv_s, wait_s = d["inflate_ns"] / 1e9, d["recv_ns"] / 1e9, d["fetch_wait_ns"] / 1e9
     other_ingest_s = max(0.0, d["ingest_ns"] / 1e9 - inflate_s)
     blk.update({
@@ -465,13 +469,15 @@ def bridge_codec_block(R: "Rank", args, broker, mine, n_parts, codec, steps, war
         "inflated_gb_per_s": round(d["inflated_bytes"] / el / 1e9, 3),
         "inflated_batches_in_timed_region": d["inflated_batches"],
         "fetch_threads": c1["fetch_threads"],
+        "inflate_threads": c1["inflate_threads"],
         "inflate_gb_per_s_per_thread": round(d["inflated_bytes"] / max(1e-9, inflate_s) / 1e9, 3),
-        # a fetch thread's time over the timed region: inflating, reading record sets off the
-        # socket, the rest of the ingest walk (CRC of the compressed batch, index), waiting for
-        # Fetch responses; the remainder is request building, flow control and idle
-        "fetch_thread_time_share": {
-            "inflate": round(inflate_s / thread_s, 3), "recv": round(recv_s / thread_s, 3),
-            "other_ingest": round(other_ingest_s / thread_s, 3), "fetch_wait": round(wait_s / thread_s, 3)},
+        # over the timed region: a fetch thread's share reading record sets off the socket and
+        # waiting for Fetch responses; an inflater's share inflating (decode + fresh CRC) and in
+        # the rest of the ingest walk (CRC of the compressed batch, index) -- the remainder of
+        # each is flow control and idle
+        "fetch_thread_time_share": {"recv": round(recv_s / thread_s, 3), "fetch_wait": round(wait_s / thread_s, 3)},
+        "inflater_time_share": {"inflate": round(inflate_s / inflater_s, 3),
+                                "other_ingest": round(other_ingest_s / inflater_s, 3)},
         "compress_setup_s": round(compress_s, 2),
         "bridge_errors": sum(br.errors for br in ld._bridges),
     })

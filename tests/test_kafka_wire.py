@@ -456,6 +456,40 @@ def test_compressed_batches_are_inflated_on_ingest(broker, server, codec):
         ref.destroy()
 
 
+@pytest.mark.parametrize("compression", ["lz4", "zstd", "gzip"])
+def test_compressed_topic_streams_through_a_ring_replica(broker, server, compression):
+    """A compressed topic larger than the replica's ring, fetched in small record sets: after the
+    first set shows the partition is compressed, each fetch thread hands its sets to an inflater
+    and asks for the next while it inflates (replicator.cpp inflate_one), and the ring waits for
+    the consumer's commits.  Every record arrives once, in order, per partition."""
+    broker.create_topic("src", 2)
+    broker.fill("src", 3000, "fixed_f32", size=64, records_per_batch=40)  # ~840 KiB per partition
+    broker.create_topic("t", 2)
+    info = broker.copy_compressed("src", "t", compression)
+    assert info["compressed_bytes"] < info["raw_bytes"] and info["batches"] == 2 * 75
+    with bridge(server, group_id="g", ring_bytes=256 << 10, max_partition_fetch_bytes=32 << 10) as br:
+        dl = DeviceLoader(Vec64.placeholder(), 50, device="cpu", num_workers=2,
+                          worker_init_fn=Vec64.init_worker("t", bootstrap_servers=br.url, group_id="g",
+                                                           auto_offset_reset="earliest", consumer_timeout_ms=1000))
+        rows = torch.cat(list(auto_commit(dl)))
+        st = br.stats()
+        assert br.errors == 0, br.last_error()
+    assert rows.shape == (6000, 64)
+    for part in (0, 1):
+        offs = rows[rows[:, 1] == part][:, 0].tolist()
+        assert offs == [float(i) for i in range(3000)]
+    assert sum(s["inflated_batches"] for s in st) == 150
+    assert br._r.inflate_threads >= 1  # the pipelined path ran
+
+
+def test_compress_round_trips_through_the_native_decoders():
+    data = bytes(range(256)) * 300 + b"tail" * 1000
+    for codec in (1, 3, 4):
+        assert core().decompress(codec, core().compress(codec, data)) == data
+    with pytest.raises(Exception, match="UnsupportedCodecError"):
+        core().compress(2, data)  # no snappy encoder
+
+
 def test_corrupt_compressed_batch_stops_the_partition(broker, server):
     ref = SyntheticBroker.create(f"shm://tkref-{os.getpid()}-{uuid.uuid4().hex[:6]}", log_capacity=64 << 20)
     try:

@@ -9,9 +9,12 @@ Usage: python tools/probes/rccl_rtt.py [--iters 2000]
 import argparse
 import json
 import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def pct(xs, q):

@@ -125,6 +125,7 @@ void bind_wire(py::module_& m) {
            "[(partition, epoch at which it was (re)assigned)] of the partitions owned now")
       .def_property_readonly("fetch_threads", &Replicator::fetch_threads)
       .def_property_readonly("fetch_wait_ns", &Replicator::fetch_wait_ns)
+      .def_property_readonly("inflate_threads", &Replicator::inflate_threads)
       .def("last_error", &Replicator::last_error)
       .def("stats", [](Replicator& r) {
         py::list l;

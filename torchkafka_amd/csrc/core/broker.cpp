@@ -408,12 +408,12 @@ void Broker::reset_partition(uint32_t pidx, int64_t offset) {
 }
 
 Broker::Ingested Broker::ingest(uint32_t pidx, uint64_t len, int64_t from_offset, bool keep_control,
-                                uint64_t limit) {
+                                uint64_t limit, const uint8_t* src) {
   PartitionEntry& P = part(pidx);
   Mapped& m = mapped(pidx);
   RobustLock l(&P.lock);
   const uint64_t pos0 = P.log_end_pos.load(std::memory_order_relaxed);
-  if (pos0 + len > P.log_capacity) throw KafkaError("ingest beyond the partition log capacity");
+  if (!src && pos0 + len > P.log_capacity) throw KafkaError("ingest beyond the partition log capacity");
   const uint64_t room = limit ? std::min<uint64_t>(limit, P.log_capacity - pos0) : P.log_capacity - pos0;
   uint8_t* base = m.log + pos0;
   uint64_t nb = P.n_batches.load(std::memory_order_relaxed);
@@ -422,7 +422,7 @@ Broker::Ingested Broker::ingest(uint32_t pidx, uint64_t len, int64_t from_offset
   // Input starts in place (the record set was received into the log tail) and output compacts
   // it towards its start; an inflated batch grows, so from the first compressed batch on the
   // unread input moves to `spill` and the output may run past it.
-  const uint8_t* in = base;
+  const uint8_t* in = src ? src : base;
   uint64_t in_len = len, r = 0, w = 0, consumed_base = 0;
   std::vector<uint8_t> spill, plain;
   const bool ring = P.ring_bytes.load(std::memory_order_relaxed) != 0;

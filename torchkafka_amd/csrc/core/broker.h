@@ -234,7 +234,10 @@ class Broker {
   // keep_control: store control batches too (a broker's own log, e.g. the wire server's tests).
   // `limit`: bytes from the write position the batches may occupy (0: up to the capacity); a batch
   // that does not fit ends the walk (Ingested::full) and is fetched again later.
-  Ingested ingest(uint32_t pidx, uint64_t len, int64_t from_offset, bool keep_control = false, uint64_t limit = 0);
+  // `src`: the record set lies in a buffer of the caller's instead of at log_tail() (a fetch
+  // thread handing compressed record sets to an inflater, replicator.cpp).
+  Ingested ingest(uint32_t pidx, uint64_t len, int64_t from_offset, bool keep_control = false, uint64_t limit = 0,
+                  const uint8_t* src = nullptr);
   // Log byte position of the first batch holding an offset >= `offset` (log end if none).
   uint64_t position_of(uint32_t pidx, int64_t offset);
   // Index entry of logical batch i (ring-indexed: slot i % index_capacity).

@@ -394,6 +394,21 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
   std::unique_ptr<wire::Client> c;
   std::map<Part*, uint64_t> failed;  // -> assignment epoch at the failure
   int backoff_ms = 0;
+  // this thread's inflater: started once one of its partitions turns out compressed
+  Inflater inf;
+  std::thread inf_th;
+  struct StopInflater {
+    Inflater& inf;
+    std::thread& th;
+    ~StopInflater() {
+      {
+        std::lock_guard<std::mutex> g(inf.m);
+        inf.stop = true;
+      }
+      inf.cv.notify_all();
+      if (th.joinable()) th.join();
+    }
+  } stop_inflater{inf, inf_th};
   while (!stop_.load()) {
     // subscribe mode: a thread whose partitions are all assigned elsewhere holds no connection
     if (cfg_.subscribe && std::none_of(mine.begin(), mine.end(), [](Part* p) { return p->owned.load(); })) {
@@ -411,11 +426,13 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
       bool unknown_leader = false;
       for (Part* p : mine) {
         if (!p->owned.load(std::memory_order_acquire)) continue;
+        if (p->failed_since.load(std::memory_order_acquire) == p->since.load()) failed[p] = p->since.load();
         auto f = failed.find(p);
         if (f != failed.end()) {
           if (f->second == p->since.load()) continue;
           failed.erase(f);  // restarted by a rebalance since it failed
         }
+        if (p->inflight.load(std::memory_order_acquire) >= kMaxInflight) continue;  // its inflater is behind
         if (throttled(*p)) {
           p->throttled.fetch_add(1, std::memory_order_relaxed);
           continue;
@@ -425,7 +442,12 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
       }
       if (unknown_leader) c->metadata(cfg_.topic);
       if (by.empty()) {
-        sleep_ms(unknown_leader ? 50 : 1);
+        if (inf_th.joinable() && !unknown_leader) {  // woken early when an inflater finishes a set
+          std::unique_lock<std::mutex> lk(inf.m);
+          inf.done_cv.wait_for(lk, std::chrono::milliseconds(1));
+        } else {
+          sleep_ms(unknown_leader ? 50 : 1);
+        }
         continue;
       }
       const int32_t wait = by.size() > 1 ? std::min<int32_t>(cfg_.max_wait_ms, 10) : cfg_.max_wait_ms;
@@ -447,8 +469,9 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
           }
           // compressed data inflates by ratio16 / 16 in the log: ask for what will fit
           const uint64_t fit = std::max<uint64_t>(avail * 16 / p->ratio16.load(), 4096);
-          req.push_back({p->partition, p->fetch_offset.load(),
-                         int32_t(std::min<uint64_t>({uint64_t(cfg_.partition_max_bytes), avail, fit}))});
+          const bool piped = p->inflight.load(std::memory_order_acquire) > 0;
+          req.push_back({p->partition, piped ? p->ask_offset.load() : p->fetch_offset.load(),
+                         int32_t(std::min<uint64_t>({uint64_t(cfg_.partition_max_bytes), piped ? fit : avail, fit}))});
           lookup[p->partition] = p;
           since[p] = p->since.load();
         }
@@ -494,6 +517,58 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
             p->remote_hw.store(ph.high_watermark, std::memory_order_relaxed);
             p->fetches.fetch_add(1, std::memory_order_relaxed);
             if (len <= 0) continue;
+            if (p->ratio16.load(std::memory_order_relaxed) > 16) {
+              // a compressed partition: receive into a buffer, hand it to this thread's inflater,
+              // and ask for the next record set while it inflates
+              pg.unlock();
+              std::vector<uint8_t> buf;
+              {
+                std::lock_guard<std::mutex> g(inf.m);
+                if (!inf.spare.empty()) {
+                  buf = std::move(inf.spare.back());
+                  inf.spare.pop_back();
+                }
+              }
+              buf.resize(size_t(len));
+              const auto t_recv = std::chrono::steady_clock::now();
+              k.read(buf.data(), size_t(len));
+              p->wire_bytes.fetch_add(uint64_t(len), std::memory_order_relaxed);
+              p->recv_ns.fetch_add(uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                                std::chrono::steady_clock::now() - t_recv).count()),
+                                   std::memory_order_relaxed);
+              // the next offset to ask for: past the last whole batch received
+              const int64_t from = p->inflight.load() > 0 ? p->ask_offset.load() : p->fetch_offset.load();
+              int64_t next = from;
+              for (size_t r = 0; size_t(len) - r >= 61;) {
+                const uint8_t* b = buf.data() + r;
+                const uint64_t total = uint64_t((uint32_t(b[8]) << 24) | (uint32_t(b[9]) << 16) |
+                                                (uint32_t(b[10]) << 8) | uint32_t(b[11])) + 12;
+                if (total < 61 || total > size_t(len) - r) break;
+                int64_t base = 0;
+                for (int q = 0; q < 8; ++q) base = (base << 8) | int64_t(b[q]);
+                const int32_t lod = int32_t((uint32_t(b[23]) << 24) | (uint32_t(b[24]) << 16) |
+                                            (uint32_t(b[25]) << 8) | uint32_t(b[26]));
+                next = std::max(next, base + int64_t(lod) + 1);
+                r += size_t(total);
+              }
+              if (next <= from) {  // no whole batch: ask again from the same offset
+                std::lock_guard<std::mutex> g(inf.m);
+                inf.spare.push_back(std::move(buf));
+                continue;
+              }
+              p->ask_offset.store(next, std::memory_order_release);
+              p->inflight.fetch_add(1, std::memory_order_acq_rel);
+              if (!inf_th.joinable()) {
+                inf_th = std::thread([this, &inf] { inflate_loop(&inf); });
+                n_inflaters_.fetch_add(1, std::memory_order_relaxed);
+              }
+              {
+                std::lock_guard<std::mutex> g(inf.m);
+                inf.q.push_back(Pending{p, since[p], std::move(buf)});
+              }
+              inf.cv.notify_one();
+              continue;
+            }
             uint64_t avail = 0;
             uint8_t* tail = room(*p, &avail);
             if (uint64_t(len) > avail) {  // an oversized first batch (KIP-74) the log cannot hold now
@@ -547,6 +622,76 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
       backoff_ms = std::min(1000, std::max(10, backoff_ms * 2));
       for (int s = 0; s < backoff_ms && !stop_.load(); s += 10) sleep_ms(10);
     }
+  }
+}
+
+void Replicator::inflate_loop(Inflater* inf) {
+  std::unique_lock<std::mutex> lk(inf->m);
+  while (true) {
+    inf->cv.wait(lk, [&] { return inf->stop || !inf->q.empty(); });
+    if (inf->stop) break;  // what is still queued is refetched by the next replicator start
+    Pending pd = std::move(inf->q.front());
+    inf->q.pop_front();
+    lk.unlock();
+    inflate_one(pd);
+    pd.p->inflight.fetch_sub(1, std::memory_order_acq_rel);
+    lk.lock();
+    pd.data.clear();
+    if (inf->spare.size() < size_t(kMaxInflight)) inf->spare.push_back(std::move(pd.data));
+    inf->done_cv.notify_all();
+  }
+  inf->q.clear();
+}
+
+// Stores one received record set of a compressed partition: inflated into the log as room allows
+// (a full ring waits for the consumers' commits), in order, never dropped -- the fetch thread has
+// already asked for what follows it.
+void Replicator::inflate_one(Pending& pd) {
+  Part* p = pd.p;
+  size_t off = 0;
+  while (!stop_.load() && off < pd.data.size()) {
+    std::unique_lock<std::mutex> pg(p->mu);
+    if (!p->owned.load() || p->since.load() != pd.since) return;  // revoked / restarted: dropped
+    uint64_t avail = 0;
+    room(*p, &avail);
+    if (avail < 4096) {
+      pg.unlock();
+      if (!cfg_.ring_bytes) {
+        set_error("replicator: local log of " + cfg_.topic + "-" + std::to_string(p->partition) +
+                  " is full (raise log_capacity)");
+        p->failed_since.store(pd.since, std::memory_order_release);
+        return;
+      }
+      sleep_ms(1);  // a ring frees room as the consumers commit
+      continue;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    Broker::Ingested in;
+    try {
+      in = local_->ingest(p->pidx, uint64_t(pd.data.size() - off), p->fetch_offset.load(), false,
+                          cfg_.ring_bytes ? avail : 0, pd.data.data() + off);
+    } catch (const KafkaError& e) {
+      set_error(std::string("replicator: ") + cfg_.topic + "-" + std::to_string(p->partition) + ": " + e.what());
+      p->failed_since.store(pd.since, std::memory_order_release);
+      return;
+    }
+    p->ingest_ns.fetch_add(uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                        std::chrono::steady_clock::now() - t0).count()),
+                           std::memory_order_relaxed);
+    p->inflate_ns.fetch_add(in.inflate_ns, std::memory_order_relaxed);
+    p->inflated.fetch_add(in.inflated, std::memory_order_relaxed);
+    p->inflated_bytes.fetch_add(in.inflated_bytes, std::memory_order_relaxed);
+    if (in.inflated_from)
+      p->ratio16.store(uint32_t(std::clamp<uint64_t>(in.inflated_bytes * 16 / in.inflated_from, 16, 16 * 64)),
+                       std::memory_order_relaxed);
+    if (in.next_offset > p->fetch_offset.load()) p->fetch_offset.store(in.next_offset);
+    p->bytes.fetch_add(in.kept_bytes, std::memory_order_relaxed);
+    p->batches.fetch_add(in.kept, std::memory_order_relaxed);
+    p->control.fetch_add(in.control, std::memory_order_relaxed);
+    off += size_t(in.consumed);
+    if (!in.full) return;  // stored (a trailing partial batch is asked for again by the fetch thread)
+    pg.unlock();
+    sleep_ms(1);
   }
 }
 

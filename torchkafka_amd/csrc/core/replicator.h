@@ -18,6 +18,7 @@
 #pragma once
 #include <atomic>
 #include <condition_variable>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -137,6 +138,8 @@ class Replicator {
   int fetch_threads() const { return n_fetch_threads_; }
   // Summed over the fetch threads: time from a Fetch request sent to its response's first bytes.
   uint64_t fetch_wait_ns() const { return fetch_wait_ns_.load(std::memory_order_relaxed); }
+  // Inflater threads started (one per fetch thread that met a compressed partition).
+  int inflate_threads() const { return n_inflaters_.load(std::memory_order_relaxed); }
   // Blocks until every replicated partition has fetched up to the cluster's high watermark as
   // seen at call time (tests, tools); false on timeout.
   bool wait_caught_up(int timeout_ms);
@@ -155,10 +158,34 @@ class Replicator {
     // inflation of the compressed batches last received, x16 (16: uncompressed): a ring replica
     // reserves that much more room and asks for that much less per Fetch, so what it fetches fits
     std::atomic<uint32_t> ratio16{16};
+    // compressed partitions (ratio16 > 16): record sets handed to the fetch thread's inflater and
+    // not yet stored, the offset to ask for next while any are, and the assignment epoch at which
+    // the inflater failed on this partition (~0: never)
+    std::atomic<int> inflight{0};
+    std::atomic<int64_t> ask_offset{0};
+    std::atomic<uint64_t> failed_since{~uint64_t(0)};
     std::atomic<bool> owned{true};       // subscribe mode: assigned to this member now
     std::atomic<uint64_t> since{0};      // assignment epoch at which it was (re)assigned
     std::mutex mu;                       // a fetch's write into the log vs. a restart of the partition
   };
+  // A compressed partition's record set, received by a fetch thread into a buffer of its own and
+  // inflated into the log by that thread's inflater (one per fetch thread), so the wait for the
+  // next Fetch response overlaps this one's inflation.  At most kMaxInflight per partition.
+  static constexpr int kMaxInflight = 2;
+  struct Pending {
+    Part* p;
+    uint64_t since;
+    std::vector<uint8_t> data;
+  };
+  struct Inflater {
+    std::mutex m;
+    std::condition_variable cv, done_cv;
+    std::deque<Pending> q;
+    std::vector<std::vector<uint8_t>> spare;
+    bool stop = false;
+  };
+  void inflate_loop(Inflater* inf);
+  void inflate_one(Pending& pd);
   void release_loop();
   void fetch_loop(std::vector<Part*> mine);
   void commit_loop();
@@ -202,6 +229,7 @@ class Replicator {
   int64_t last_heartbeat_ms_ = 0;
   int n_fetch_threads_ = 0;
   std::atomic<uint64_t> fetch_wait_ns_{0};
+  std::atomic<int> n_inflaters_{0};
 };
 
 }  // namespace tk
