@@ -395,6 +395,20 @@ def steady_block(R: Rank, res: dict, steps: int, dim: int) -> dict:
     return out
 
 
+def lockstep_trace_summary(recs) -> dict:
+    """TORCHKAFKA_LOCKSTEP_TRACE=1: where an agreement's round trip went, host clock, µs (p50 / p90):
+    issuing it, the steps delivered before it was needed (slack), waiting for it, issue to result."""
+    recs = [r for r in recs if r[3] > 0]
+
+    def q(xs):
+        xs = sorted(xs)
+        return [round(xs[int(len(xs) * f)] / 1e3, 1) for f in (0.5, 0.9)] if xs else None
+
+    return {"agreements": len(recs), "issue_us": q([r[1] - r[0] for r in recs]),
+            "slack_us": q([r[2] - r[1] for r in recs]), "wait_us": q([r[3] - r[2] for r in recs]),
+            "round_trip_us": q([r[3] - r[0] for r in recs])}
+
+
 def _bridge_counters(loader) -> dict:
     """Where the bridges' fetch threads spent their time, summed over partitions and threads."""
     keys = ("bytes", "wire_bytes", "recv_ns", "ingest_ns", "inflate_ns", "inflated_batches", "inflated_bytes")
@@ -764,6 +778,9 @@ def run_rank(args) -> int:
             blk["lockstep_wait_us_per_step"] = round(st.get("lockstep_wait_us_per_batch", 0.0), 3)
             blk["lockstep_issue_us_per_step"] = round(st.get("lockstep_issue_us_per_batch", 0.0), 3)
             blk["lockstep_step_wait_max_us"] = round(st.get("lockstep_step_wait_max_us", 0.0), 1)
+            rc = getattr(getattr(ld, "_run", None), "rccl", None)
+            if rc is not None and os.environ.get("TORCHKAFKA_LOCKSTEP_TRACE") == "1":
+                blk["lockstep_trace"] = lockstep_trace_summary(rc.take_trace())
         if name == "verify":
             key = "steady_unverified" if ld.verify == "commit" else "steady_verified"
             blk["verify_wait_us_per_batch"] = round(eres["stats"].get("verify_wait_us_per_batch", 0.0), 3)

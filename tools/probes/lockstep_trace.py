@@ -43,7 +43,8 @@ def main():
     for a in agreements:
         s0, e0 = a[0][1], a[-1][2]
         busy.append(sum(1 for (s, e) in others if s < e0 and e > s0))
-    print({"agreements": len(agreements), "kernels_per_agreement": round(sum(len(a) for a in agreements) / max(1, len(agreements)), 2),
+    per = round(sum(len(a) for a in agreements) / max(1, len(agreements)), 2)
+    print({"agreements": len(agreements), "kernels_per_agreement": per,
            "span_us_p50": pct(spans, 0.5), "span_us_p90": pct(spans, 0.9), "span_us_p99": pct(spans, 0.99),
            "gap_between_its_kernels_us_p50": pct(gaps, 0.5), "gap_us_p90": pct(gaps, 0.9),
            "other_kernels_overlapping_p50": sorted(busy)[len(busy) // 2] if busy else None})

@@ -194,6 +194,13 @@ PYBIND11_MODULE(_tkhip, m) {
                              "how the agreement words reach RCCL: kernel (tiny copy kernels), host (RCCL on "
                              "host-mapped memory) or copy (hipMemcpyAsync)")
       .def_property_readonly("issued", &RcclLockstep::issued)
+      .def("take_trace",
+           [](RcclLockstep& l) {
+             py::list out;
+             for (const auto& r : l.take_trace()) out.append(py::make_tuple(r.issue0, r.issue1, r.wait0, r.wait1));
+             return out;
+           },
+           "TORCHKAFKA_LOCKSTEP_TRACE=1: [(issue begin, issue end, wait begin, wait end)] host ns per agreement")
       .def_property_readonly("nranks", &RcclLockstep::comm_count,
                              "ranks in the private communicator, as RCCL reports them (ncclCommCount)")
       .def(

@@ -65,6 +65,16 @@ class RcclLockstep : public LockstepTransport {
   // (sum of rank ids == world * (world - 1) / 2).
   int comm_count() const;
   int64_t allreduce_sum(int64_t v);
+  // TORCHKAFKA_LOCKSTEP_TRACE=1: host timestamps (steady clock, ns) of every agreement -- issue
+  // begin / end, wait begin / end (tools/probes: where an agreement's round trip goes).
+  struct TraceRec {
+    int64_t issue0, issue1, wait0, wait1;
+  };
+  std::vector<TraceRec> take_trace() {
+    std::vector<TraceRec> t;
+    t.swap(trace_);
+    return t;
+  }
 
  private:
   RcclApi* api_ = nullptr;
@@ -82,6 +92,9 @@ class RcclLockstep : public LockstepTransport {
   uint64_t issued_ = 0;
   int64_t timeout_ms_ = 600000;  // like torch.distributed's default NCCL timeout
   bool aborted_ = false;
+  bool tracing_ = false;
+  std::vector<TraceRec> trace_;
+  std::vector<int64_t> slot_rec_;  // per slot: its agreement's record in trace_ (-1: none)
   void wait_event(int t, const char* what);  // bounded wait with async-error checks
 };
 

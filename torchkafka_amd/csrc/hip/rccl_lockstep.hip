@@ -91,6 +91,9 @@ RcclLockstep::RcclLockstep(const std::string& lib_path, const std::string& id, i
                            int slots)
     : rank_(rank), world_(world), device_(device), slots_(slots < 2 ? 2 : slots) {
   if (id.size() != NCCL_UNIQUE_ID_BYTES) throw std::invalid_argument("RCCL unique id must be 128 bytes");
+  const char* tr = std::getenv("TORCHKAFKA_LOCKSTEP_TRACE");
+  tracing_ = tr && tr[0] == '1';
+  slot_rec_.assign(size_t(slots_), -1);
   api_ = load_api(lib_path);
   TKH_HIP(hipSetDevice(device_));
   // the lockstep's stream at the device's greatest priority: HIP keeps a hardware-queue pool per
@@ -166,7 +169,15 @@ void RcclLockstep::wait_event(int t, const char* what) {
   }
 }
 
+namespace {
+int64_t steady_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+}  // namespace
+
 int RcclLockstep::issue(const int64_t in[kW]) {
+  const int64_t t_issue = tracing_ ? steady_ns() : 0;
   const int s = int(issued_ % uint64_t(slots_));
   if (aborted_) throw std::runtime_error("lockstep: the RCCL communicator was aborted after a failure");
   // the slot's previous round trip must be complete before its buffers are reused
@@ -194,6 +205,10 @@ int RcclLockstep::issue(const int64_t in[kW]) {
   }
   TKH_HIP(hipEventRecord(ev_[size_t(s)], stream_));
   ++issued_;
+  if (tracing_ && trace_.size() < (size_t(1) << 20)) {
+    slot_rec_[size_t(s)] = int64_t(trace_.size());
+    trace_.push_back(TraceRec{t_issue, steady_ns(), 0, 0});
+  }
   return s;
 }
 
@@ -226,7 +241,14 @@ int64_t RcclLockstep::allreduce_sum(int64_t v) {
 bool RcclLockstep::ready(int t) { return hipEventQuery(ev_.at(size_t(t))) == hipSuccess; }
 
 void RcclLockstep::wait(int t, int64_t out[kW]) {
+  const int64_t w0 = tracing_ ? steady_ns() : 0;
   wait_event(t, "lockstep wait");
+  if (tracing_ && slot_rec_.at(size_t(t)) >= 0 && size_t(slot_rec_[size_t(t)]) < trace_.size()) {
+    TraceRec& r = trace_[size_t(slot_rec_[size_t(t)])];
+    r.wait0 = w0;
+    r.wait1 = steady_ns();
+    slot_rec_[size_t(t)] = -1;
+  }
   const volatile int64_t* hout = h_out_ + kW * t;
   for (int k = 0; k < kW; ++k) out[k] = hout[k];
 }
