@@ -739,7 +739,7 @@ def run_rank(args) -> int:
         dt = torch.float32 if name == "f32" else dtypes[args.dtype]
         own_group = False
         rccl_block = name in ("rccl", "rccl_sync")
-        if rccl_block and not dist.is_initialized():
+        if rccl_block and not dist.is_initialized() and os.environ.get("TK_BENCH_NO_TORCH_NCCL") != "1":
             # a world-1 nccl group; one all-reduce on it makes torch's own RCCL communicator and its
             # streams, as a DDP job's gradient all-reduce does at N > 1 -- the N = 8 queue layout,
             # rehearsed on one GPU (the loader's private communicator carries every agreement)
