@@ -33,6 +33,22 @@ def test_lane_tree_crc_matches_crc32c(n):
     assert raw ^ 0xFFFFFFFF == _crc32c_ref(buf[21:c1])
 
 
+@pytest.mark.parametrize("parts", [2, 3, 4])
+@pytest.mark.parametrize("n", [61, 10_300, 20_500, 66_000, 131_072 + 21])
+def test_segment_parts_combine_to_the_segment_crc(n, parts):
+    """SpanLaunch::parts: P workgroups each fold a contiguous run of the segment's windows from a
+    zero state, shift their merged CRC to the segment's end by whole windows (kSpanTabWinShift) and
+    xor it in (span_device.h crc_finish) -- the same raw CRC as one workgroup.  Parts with no window
+    (segments shorter than P windows) contribute zero."""
+    c = core()
+    rnd = random.Random(n * 10 + parts)
+    buf = bytes(rnd.getrandbits(8) for _ in range(n))
+    c1 = min(n, 21 + c.SPAN_SEG_MAX)
+    whole = c.crc32c_span_emulate(buf, 21, c1, True)
+    assert c.crc32c_span_emulate(buf, 21, c1, True, parts) == whole
+    assert whole ^ 0xFFFFFFFF == _crc32c_ref(buf[21:c1])
+
+
 def test_lane_tree_crc_unaligned_ranges():
     c = core()
     rnd = random.Random(7)

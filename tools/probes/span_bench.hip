@@ -48,6 +48,7 @@ int main(int argc, char** argv) {
   const int segs = argc > 1 ? std::atoi(argv[1]) : 16;
   const uint32_t seg_len = uint32_t(argc > 2 ? std::atoi(argv[2]) : 128) << 10;
   const int reps = argc > 3 ? std::atoi(argv[3]) : 200;
+  const int parts = argc > 4 ? std::atoi(argv[4]) : 1;  // workgroups per segment (SpanLaunch::parts)
   const int dim = 256, rec = 4 * dim + 32;
   if (segs < 1 || segs > tkh::kMaxLaunchSegs || seg_len > tk::kSpanSegMax) {
     std::fprintf(stderr, "bad shape\n");
@@ -116,8 +117,16 @@ int main(int argc, char** argv) {
   CK(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev), err, 0));
   CK(hipHostGetDevicePointer(reinterpret_cast<void**>(&part_dev), partials, 0));
 
-  auto make = [&](const uint8_t* logp) {
+  const int nstreams = 3;
+  uint32_t* acc[nstreams];
+  for (auto& p : acc) {
+    CK(hipMalloc(reinterpret_cast<void**>(&p), tkh::kMaxLaunchSegs * 2 * sizeof(uint32_t)));
+    CK(hipMemset(p, 0, tkh::kMaxLaunchSegs * 2 * sizeof(uint32_t)));
+  }
+  auto make = [&](const uint8_t* logp, int si) {
     tkh::SpanLaunch a{};
+    a.parts = parts;
+    a.part_acc = acc[si];
     a.n_seg = segs;
     a.vec_store = 1;
     a.row_elems = dim;
@@ -132,17 +141,18 @@ int main(int argc, char** argv) {
     }
     return a;
   };
-  const int nstreams = 3;
   hipStream_t st[nstreams];
   for (auto& s : st) CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  std::printf("{\"segments\": %d, \"segment_bytes\": %u, \"group_bytes\": %zu, \"rows\": %lld", segs, seg_len,
-              size_t(segs) * seg_len, static_cast<long long>(rows));
+  std::printf("{\"segments\": %d, \"segment_bytes\": %u, \"group_bytes\": %zu, \"rows\": %lld, \"parts\": %d", segs,
+              seg_len, size_t(segs) * seg_len, static_cast<long long>(rows), parts);
   for (int mode = 0; mode < 2; ++mode) {
     const char* name = mode == 0 ? "pcie_zero_copy" : "hbm";
-    const tkh::SpanLaunch a = make(mode == 0 ? hlog_dev : dlog);
+    const tkh::SpanLaunch a = make(mode == 0 ? hlog_dev : dlog, 0);
+    const tkh::SpanLaunch a1 = make(mode == 0 ? hlog_dev : dlog, 1), a2 = make(mode == 0 ? hlog_dev : dlog, 2);
+    const tkh::SpanLaunch* per_stream[nstreams] = {&a, &a1, &a2};
     *err = -1;
     CK(hipMemset(out, 0, size_t(rows) * dim * 2));
     tkh::launch_span_decode(a, tkh::kF32, tkh::kBF16, nullptr, nullptr, st[0]);
@@ -172,7 +182,8 @@ int main(int argc, char** argv) {
     // back to back on 3 streams
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0, st[0]));
-    for (int i = 0; i < reps; ++i) tkh::launch_span_decode(a, tkh::kF32, tkh::kBF16, nullptr, nullptr, st[i % nstreams]);
+    for (int i = 0; i < reps; ++i)
+      tkh::launch_span_decode(*per_stream[i % nstreams], tkh::kF32, tkh::kBF16, nullptr, nullptr, st[i % nstreams]);
     for (int s = 1; s < nstreams; ++s) {
       hipEvent_t ej;
       CK(hipEventCreateWithFlags(&ej, hipEventDisableTiming));
@@ -190,6 +201,33 @@ int main(int argc, char** argv) {
                 name, *err, static_cast<long long>(bad), ms[ms.size() / 2] * 1e3, ms[ms.size() / 10] * 1e3,
                 ms[ms.size() * 9 / 10] * 1e3, double(size_t(segs) * seg_len) / (ms[ms.size() / 2] * 1e-3) / 1e9, gb,
                 tb * 1e3 / reps, ms[ms.size() / 2] * 1e3 * segs / (double(size_t(segs) * seg_len) / (1 << 20)));
+  }
+  // partial CRCs of RecordBatches cut into several segments (flags First-only / Last-only /
+  // neither, short and long segments), the same accumulator words for two launches in a row on one
+  // stream: every partial must equal the host emulation's
+  {
+    tkh::SpanLaunch pa = make(dlog, 0);
+    std::vector<uint32_t> want(static_cast<size_t>(segs));
+    for (int s = 0; s < segs; ++s) {
+      tkh::SpanDevSeg& d = pa.s[s];
+      const int kind = s % 3;  // 0: first part of a batch, 1: a middle part, 2: the last part
+      d.flags = tk::kSegCrc | (kind == 0 ? tk::kSegCrcFirst : kind == 2 ? tk::kSegCrcLast : 0u);
+      d.len = kind == 2 ? 3600u + 977u * uint32_t(s % 5) : seg_len - 1000u * uint32_t(s % 4);
+      d.row_begin = d.row_end = 0;
+      const uint32_t c0 = kind == 0 ? 21u : 0u;
+      want[size_t(s)] = tk::crc32c_span_emulate(&host[d.log_pos], c0, d.len, kind == 0, 1);
+    }
+    int64_t bad_partials = 0;
+    for (int rep = 0; rep < 2; ++rep) {
+      for (int s = 0; s < segs; ++s) partials[s] = 0xDEADBEEFu;
+      *err = -1;
+      tkh::launch_span_decode(pa, tkh::kF32, tkh::kBF16, nullptr, nullptr, st[0]);
+      tkh::launch_span_decode(pa, tkh::kF32, tkh::kBF16, nullptr, nullptr, st[0]);
+      CK(hipStreamSynchronize(st[0]));
+      for (int s = 0; s < segs; ++s) bad_partials += partials[s] != want[size_t(s)];
+    }
+    std::printf(", \"partials\": {\"segments\": %d, \"mismatches\": %lld, \"verdict\": %d}", segs,
+                static_cast<long long>(bad_partials), *err);
   }
   std::printf("}\n");
   return 0;

@@ -96,13 +96,13 @@ PYBIND11_MODULE(_tkcore, m) {
   m.def("crc32c_shift_raw", &crc32c_shift_raw, py::arg("raw"), py::arg("n_bytes"));
   m.def(
       "crc32c_span_emulate",
-      [](py::bytes b, uint32_t c0, uint32_t c1, bool first) {
+      [](py::bytes b, uint32_t c0, uint32_t c1, bool first, int parts) {
         std::string s = b;
-        if (c0 > c1 || c1 > s.size() || span_windows(c1) > 32)
+        if (c0 > c1 || c1 > s.size() || span_windows(c1) > 32 || parts < 1 || parts > kSpanMaxParts)
           throw std::invalid_argument("crc32c_span_emulate: bad range");
-        return crc32c_span_emulate(reinterpret_cast<const uint8_t*>(s.data()), c0, c1, first);
+        return crc32c_span_emulate(reinterpret_cast<const uint8_t*>(s.data()), c0, c1, first, parts);
       },
-      py::arg("data"), py::arg("c0"), py::arg("c1"), py::arg("first"));
+      py::arg("data"), py::arg("c0"), py::arg("c1"), py::arg("first"), py::arg("parts") = 1);
   m.def("span_tables", []() {
     std::vector<uint32_t> t(kSpanTabWords);
     crc32c_span_tables(t.data());

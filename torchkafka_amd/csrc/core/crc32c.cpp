@@ -321,9 +321,15 @@ void crc32c_span_tables(uint32_t* out) {
   const uint32_t gap = T.x2nmodp(uint64_t(kSpanWin - kSpanPiece), 3);
   for (uint32_t i = 0; i < 8; ++i)
     for (uint32_t n = 0; n < 16; ++n) out[kSpanTabGap + i * 16 + n] = Tables::multmodp(gap, n << (4 * i));
+  for (uint32_t j = 0; j < kSpanWinLevels; ++j) {
+    const uint32_t op = T.x2nmodp(uint64_t(kSpanWin) << j, 3);  // x^(8 * W * 2^j)
+    for (int k = 0; k < 4; ++k)
+      for (uint32_t b = 0; b < 256; ++b)
+        out[kSpanTabWinShift + (j * 4 + uint32_t(k)) * 256 + b] = Tables::multmodp(op, b << (8 * k));
+  }
 }
 
-uint32_t crc32c_span_emulate(const uint8_t* buf, uint32_t c0, uint32_t c1, bool first) {
+uint32_t crc32c_span_emulate(const uint8_t* buf, uint32_t c0, uint32_t c1, bool first, int parts) {
   // Host mirror of the device CRC stage (span_device.h), step for step: windows of kSpanWin bytes
   // ending at c1, lane t folding its kSpanPiece bytes of every window into a running state (the
   // window gap operator between windows), looked up in the same nibble rows; a slice-by-4 step for
@@ -361,8 +367,17 @@ uint32_t crc32c_span_emulate(const uint8_t* buf, uint32_t c0, uint32_t c1, bool 
   };
   const int64_t nw = int64_t(span_windows(c1));
   const int64_t w0 = int64_t(c1) - nw * int64_t(kSpanWin);
+  auto shift = [&](const uint32_t* S, uint32_t c) {
+    return S[c & 255] ^ S[256 + ((c >> 8) & 255)] ^ S[512 + ((c >> 16) & 255)] ^ S[768 + (c >> 24)];
+  };
+  // segment parts (span_device.h crc_finish): each part's windows from a zero state, merged, moved
+  // to the segment's end by whole windows, xored
+  if (parts < 1) parts = 1;
+  uint32_t total = 0;
+  for (int q = 0; q < parts; ++q) {
+  const int64_t k0 = span_part_k0(q, parts, int32_t(nw)), k1 = span_part_k0(q + 1, parts, int32_t(nw));
   uint32_t lane[kSpanLanes] = {};
-  for (int64_t k = 0; k < nw; ++k) {
+  for (int64_t k = k0; k < k1; ++k) {
     for (uint32_t t = 0; t < kSpanLanes; ++t) {
       const int64_t start = w0 + k * int64_t(kSpanWin) + int64_t(t) * kSpanPiece;
       uint32_t crc = gap(lane[t]);
@@ -378,13 +393,14 @@ uint32_t crc32c_span_emulate(const uint8_t* buf, uint32_t c0, uint32_t c1, bool 
   }
   for (uint32_t j = 0; j < kSpanLevels; ++j) {
     const uint32_t* S = S0 + j * 4 * 256;
-    for (uint32_t t = 0; t < kSpanLanes; t += 2u << j) {
-      const uint32_t c = lane[t];
-      lane[t] = S[c & 255] ^ S[256 + ((c >> 8) & 255)] ^ S[512 + ((c >> 16) & 255)] ^ S[768 + (c >> 24)] ^
-                lane[t + (1u << j)];
-    }
+    for (uint32_t t = 0; t < kSpanLanes; t += 2u << j) lane[t] = shift(S, lane[t]) ^ lane[t + (1u << j)];
   }
-  return lane[0];
+  uint32_t c = lane[0];
+  for (uint32_t j = 0; j < kSpanWinLevels; ++j)
+    if (((nw - k1) >> j) & 1) c = shift(tab + kSpanTabWinShift + j * 4 * 256, c);
+  total ^= c;
+  }
+  return total;
 }
 
 }  // namespace tk

@@ -26,6 +26,6 @@ uint32_t crc32c_shift_raw(uint32_t raw, uint64_t n_bytes);
 void crc32c_span_tables(uint32_t* out);
 // Host emulation of the device CRC stage over buf[c0, c1): raw CRC, with the RecordBatch's
 // initial-value xor applied to its first 4 bytes when `first` (tests compare it with crc32c).
-uint32_t crc32c_span_emulate(const uint8_t* buf, uint32_t c0, uint32_t c1, bool first);
+uint32_t crc32c_span_emulate(const uint8_t* buf, uint32_t c0, uint32_t c1, bool first, int parts = 1);
 
 }  // namespace tk

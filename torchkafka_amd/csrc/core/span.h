@@ -106,7 +106,15 @@ constexpr uint32_t kSpanTabNib = kSpanTabShift + kSpanTabShiftSet;
 constexpr uint32_t kSpanTabNibWords = 16 * 16;
 constexpr uint32_t kSpanTabGap = kSpanTabNib + kSpanTabNibWords;
 constexpr uint32_t kSpanTabGapWords = 8 * 16;
-constexpr uint32_t kSpanTabWords = kSpanTabGap + kSpanTabGapWords;
+// Segment parts (SpanLaunch::parts): for level j and byte k, shift-by-(kSpanWin << j)-bytes of
+// (b << 8k) -- a part's CRC moved from the end of its last window to the segment's end.
+constexpr uint32_t kSpanWinLevels = 5;  // up to 31 windows: kSpanMaxWins <= 32
+constexpr uint32_t kSpanTabWinShift = kSpanTabGap + kSpanTabGapWords;
+constexpr uint32_t kSpanTabWords = kSpanTabWinShift + kSpanWinLevels * 4 * 256;
+// Workgroups one segment may be split over (SpanLaunch::parts: 1, 2 or 4).
+constexpr int kSpanMaxParts = 4;
+// Windows [k0, k1) of part q of P over a segment of nw windows.
+inline constexpr int32_t span_part_k0(int32_t q, int32_t P, int32_t nw) { return q * nw / P; }
 
 enum SpanSegFlags : uint32_t {
   kSegCrcFirst = 1,   // the segment holds the first CRC'd byte of its RecordBatch (offset 21)

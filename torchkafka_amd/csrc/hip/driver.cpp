@@ -650,6 +650,8 @@ void MainDriver::launch_var_span(const int* slots, const SlotView* const* views,
       a.b[k].rows = reinterpret_cast<const tk::JsonSpanRow*>(a.b[k].slot);
     }
     a.tabs = eng_->span_tables();
+    a.parts = eng_->span_parts();
+    a.part_acc = a.parts > 1 ? eng_->part_acc(stream) : nullptr;
     pcie = false;
     if (mirror) mirror->before(stream);
     eng_->run_on(stream, [a, src_dt, dst_dt, pad, stream] { tkh::launch_var_span(a, src_dt, dst_dt, pad, stream); });

@@ -92,6 +92,14 @@ class Engine {
   }
   // Device copy of the CRC tables of the span kernel (uploaded on first use).
   const uint32_t* span_tables();
+  // Workgroups per span segment (TORCHKAFKA_SPAN_PARTS: 1, 2 or 4; span_device.h Part) and the
+  // accumulator words the parts of the next launch on `stream` meet in: zeroed once, left zero by
+  // every launch, and handed out in rotation over kPartAccSets sets per stream -- the dispatches of
+  // one stream may overlap (a launch's first workgroups start before the previous launch's last
+  // ones finished), so consecutive launches must not share words.
+  static constexpr int kPartAccSets = 16;
+  int span_parts() const { return span_parts_; }
+  uint32_t* part_acc(hipStream_t stream);
   // The streams device-decode groups rotate over (created on first use; kDecodeStreams).
   hipStream_t decode_stream(int k);
   int decode_streams() const { return n_decode_; }
@@ -147,6 +155,13 @@ class Engine {
   uint8_t* host_dev_ = nullptr;           // device view of the registered host region (zero-copy)
   size_t host_len_ = 0;
   uint32_t* span_tabs_ = nullptr;
+  int span_parts_ = 1;
+  struct PartAcc {
+    hipStream_t stream;
+    uint32_t* words;
+    uint64_t next;
+  };
+  std::vector<PartAcc> part_acc_;
   hipStream_t decode_streams_[4] = {nullptr, nullptr, nullptr, nullptr};
   int n_decode_ = default_decode_streams();
   static int default_decode_streams();

@@ -41,6 +41,10 @@ namespace tkh {
 
 Engine::Engine(int device, int n_slots, size_t staging_bytes, int n_streams, int mode)
     : device_(device), n_slots_(n_slots), mode_(mode), q_(std::make_unique<HipQueue>(device)) {
+  if (const char* e = std::getenv("TORCHKAFKA_SPAN_PARTS")) {
+    const int p = std::atoi(e);
+    span_parts_ = p == 2 || p == tk::kSpanMaxParts ? p : 1;
+  }
   if (n_slots <= 0) throw std::invalid_argument("engine: n_slots must be positive");
   if (mode != kH2DDma && mode != kH2DZeroCopy) throw std::invalid_argument("engine: bad h2d mode");
   if (n_streams < 1) n_streams = 1;
@@ -77,6 +81,7 @@ Engine::~Engine() {
   for (auto e : copied_) hipEventDestroy(e);
   Reaper::free_device(device_, staging_);
   Reaper::free_device(device_, span_tabs_);
+  for (auto& pa : part_acc_) Reaper::free_device(device_, pa.words);
   for (auto st : decode_streams_)
     if (st) {
       hipStreamSynchronize(st);
@@ -294,6 +299,19 @@ void Engine::collate_json_group(const int* slots, int n, hipStream_t user, const
   finish(slots[n - 1], user);
 }
 
+uint32_t* Engine::part_acc(hipStream_t stream) {
+  constexpr size_t kSetWords = size_t(kMaxLaunchSegs) * 2;
+  for (auto& pa : part_acc_)
+    if (pa.stream == stream) return pa.words + (pa.next++ % kPartAccSets) * kSetWords;
+  uint32_t* p = nullptr;
+  const size_t bytes = kSetWords * kPartAccSets * sizeof(uint32_t);
+  TKH_CHECK(hipSetDevice(device_));
+  TKH_CHECK(hipMalloc(reinterpret_cast<void**>(&p), bytes));
+  TKH_CHECK(hipMemset(p, 0, bytes));
+  part_acc_.push_back(PartAcc{stream, p, 1});
+  return p;
+}
+
 const uint32_t* Engine::span_tables() {
   if (!span_tabs_) {
     std::vector<uint32_t> t(tk::kSpanTabWords);
@@ -384,6 +402,8 @@ void Engine::collate_span(const int* slots, int n, hipStream_t user, SpanLaunch&
     if (a.b[k].ext_words) a.b[k].ext_src = reinterpret_cast<const int64_t*>(src_base(slots[k]) + a.b[k].ext_off);
   }
   a.tabs = span_tables();
+  a.parts = span_parts_;
+  a.part_acc = span_parts_ > 1 ? part_acc(user) : nullptr;
   if (queued(user)) {
     queue().submit([a, src_dt, dst_dt, shift, scale, user] {
       launch_span_decode(a, src_dt, dst_dt, shift, scale, user);
@@ -403,6 +423,8 @@ void Engine::collate_json_stage(const int* slots, int n, hipStream_t user, JsonS
     a.b[k].rows = reinterpret_cast<const tk::JsonSpanRow*>(a.b[k].slot);
   }
   a.tabs = span_tables();
+  a.parts = span_parts_;
+  a.part_acc = span_parts_ > 1 ? part_acc(user) : nullptr;
   if (queued(user))
     queue().submit([a, user] { launch_json_stage(a, user); });
   else

@@ -136,7 +136,8 @@ __global__ __launch_bounds__(kBlock) void json_stage_kernel(JsonStageLaunch a) {
   __shared__ int32_t bad;
 
   const int t = int(threadIdx.x), lane = t & 63, wv = t >> 6;
-  const SpanDevSeg& sg = a.s[blockIdx.x];
+  const int P = a.parts;
+  const SpanDevSeg& sg = a.s[int(blockIdx.x) / P];
   const JsonStageBatch& bo = a.b[sg.batch];
   const uint32_t row_begin = sg.row_begin;
   const int32_t nrows = int32_t(sg.row_end - row_begin);
@@ -144,8 +145,8 @@ __global__ __launch_bounds__(kBlock) void json_stage_kernel(JsonStageLaunch a) {
   const int32_t trunc = bo.trunc_len;
 
   if (flags & tk::kSegHostRows) {
-    // rows the worker parsed (rare): one wave copies their float32 values, row after row
-    if (wv != 0) return;
+    // rows the worker parsed (rare): one wave of part 0 copies their float32 values, row after row
+    if (wv != 0 || int(blockIdx.x) % P != 0) return;
     uint32_t off = sg.stage_off;
     for (int32_t rr = 0; rr < nrows; ++rr) {
       const int64_t row = int64_t(row_begin) + rr;
@@ -169,9 +170,10 @@ __global__ __launch_bounds__(kBlock) void json_stage_kernel(JsonStageLaunch a) {
   const bool do_crc = (flags & tk::kSegCrc) != 0;
   const int32_t lo_b = kFront + head, hi_b = lo_b + int32_t(len);
   const span::Windows W(lo_b, hi_b);
+  const span::Part pt = span::part_of(P, W.nw);
 
   const uint32_t crc = span::pipeline<kBufs>(
-      sg.src, W, bufs, tab, a.tabs, lo_b + ((flags & tk::kSegCrcFirst) ? 21 : 0), do_crc,
+      sg.src, W, pt.k0, pt.k1, bufs, tab, a.tabs, lo_b + ((flags & tk::kSegCrcFirst) ? 21 : 0), do_crc,
       (flags & tk::kSegCrcFirst) != 0,
       [&] {  // setup: the row table (image bytes, text lengths; -2: the row disagrees with the segment)
         const int64_t base = int64_t(sg.log_pos) - int64_t(head) - kFront;  // log position of image byte 0
@@ -212,7 +214,9 @@ __global__ __launch_bounds__(kBlock) void json_stage_kernel(JsonStageLaunch a) {
           if (r < nrows) {
             dst[r] = off;
             const int32_t T = tln[r];
-            if (T == -2) {  // the row table disagrees with the segment: read nothing, never commit
+            if (pt.q != 0) {
+              // the descriptors and the verdict on the row table are part 0's
+            } else if (T == -2) {  // the row table disagrees with the segment: read nothing, never commit
               bo.desc[row_begin + uint32_t(r)] = JsonRowDesc{off, 0, 0, 0};
               bad = 1;
             } else if (T >= 0) {
@@ -250,9 +254,11 @@ __global__ __launch_bounds__(kBlock) void json_stage_kernel(JsonStageLaunch a) {
       });
 
   if (do_crc) {
-    const uint32_t* shift_set = t < kThreads ? span::crc_merge(a.tabs, crc, wcrc) : nullptr;
+    if (t < kThreads) span::crc_merge(a.tabs, crc, wcrc);
     __syncthreads();
-    if (t == 0) span::crc_verdict(shift_set, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials);
+    if (t == 0)
+      span::crc_finish(a.tabs, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials, P, W.nw - pt.k1,
+                       a.part_acc + 2 * pt.seg);
   }
   if (t == 0 && bad) *bo.err = int32_t(sg.seg);  // never committed (reported as this segment)
 }
@@ -311,7 +317,9 @@ void launch_json_count(const JsonGroupArgs& a, hipStream_t stream) {
   if (e != hipSuccess) throw std::runtime_error(std::string("json count launch: ") + hipGetErrorString(e));
 }
 
-void launch_json_stage(const JsonStageLaunch& a, hipStream_t stream) {
+void launch_json_stage(const JsonStageLaunch& a0, hipStream_t stream) {
+  JsonStageLaunch a = a0;
+  a.parts = check_parts(a.parts, a.part_acc, "json stage");
   if (a.n_seg < 0 || a.n_seg > kMaxLaunchSegs) throw std::invalid_argument("json stage: bad segment count");
   if (a.n_seg == 0) return;
   for (int i = 0; i < a.n_seg; ++i) {
@@ -323,7 +331,7 @@ void launch_json_stage(const JsonStageLaunch& a, hipStream_t stream) {
         a.b[s.batch].desc == nullptr || (s.stage_off & 15u) != 0)
       throw std::invalid_argument("json stage: malformed segment");
   }
-  hipLaunchKernelGGL(json_stage_kernel, dim3(unsigned(a.n_seg)), dim3(kBlock), 0, stream, a);
+  hipLaunchKernelGGL(json_stage_kernel, dim3(unsigned(a.n_seg * a.parts)), dim3(kBlock), 0, stream, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("json stage launch: ") + hipGetErrorString(e));
 }

@@ -46,6 +46,8 @@ struct SpanLaunch {
   int vec_store;             // every batch's rows start 16-byte aligned for vector stores
   int64_t row_elems;
   const uint32_t* tabs;      // device CRC tables (tk::kSpanTabWords)
+  int parts;                 // workgroups per segment (1, 2, 4; span_device.h Part): grid n_seg * parts
+  uint32_t* part_acc;        // parts > 1: [kMaxLaunchSegs][2] zeroed device words of this launch's stream
   SpanBatchOut b[kMaxGroup];
   SpanDevSeg s[kMaxLaunchSegs];
 };
@@ -74,6 +76,8 @@ struct JsonStageBatch {
 struct JsonStageLaunch {
   int n_seg;
   const uint32_t* tabs;         // device CRC tables (tk::kSpanTabWords)
+  int parts;                    // workgroups per segment (as SpanLaunch)
+  uint32_t* part_acc;
   JsonStageBatch b[kMaxGroup];
   SpanDevSeg s[kMaxLaunchSegs];
 };
@@ -98,6 +102,8 @@ struct VarSpanBatch {
 struct VarSpanLaunch {
   int n_seg;
   const uint32_t* tabs;
+  int parts;                    // workgroups per segment (as SpanLaunch)
+  uint32_t* part_acc;
   VarSpanBatch b[kMaxGroup];
   SpanDevSeg s[kMaxLaunchSegs];
 };
@@ -111,5 +117,8 @@ void prewarm_span_kernels(int device);
 
 void launch_span_decode(const SpanLaunch& a, int src_dt, int dst_dt, const float* shift, const float* scale,
                         hipStream_t stream);
+
+// Validates SpanLaunch::parts (1, 2, 4; accumulator words needed past 1); returns it (0 -> 1).
+int check_parts(int parts, const uint32_t* acc, const char* what);
 
 }  // namespace tkh

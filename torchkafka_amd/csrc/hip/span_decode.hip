@@ -65,7 +65,8 @@ __global__ __launch_bounds__(kBlock) void span_decode_kernel(SpanLaunch a, const
   __shared__ uint32_t wcrc[kThreads / 64];
 
   const int t = int(threadIdx.x);
-  const SpanDevSeg& sg = a.s[blockIdx.x];
+  const int P = a.parts;
+  const SpanDevSeg& sg = a.s[int(blockIdx.x) / P];
   const SpanBatchOut& bo = a.b[sg.batch];
   const uint32_t len = sg.len, flags = sg.flags;
   const int32_t head = int32_t(reinterpret_cast<uintptr_t>(sg.src) & 15u);
@@ -74,6 +75,7 @@ __global__ __launch_bounds__(kBlock) void span_decode_kernel(SpanLaunch a, const
   const bool do_crc = (flags & tk::kSegCrc) != 0;
   const int32_t lo_b = kFront + head, hi_b = lo_b + int32_t(len);  // the segment's image bytes
   const span::Windows W(lo_b, hi_b);
+  const span::Part pt = span::part_of(P, W.nw);
   const int64_t RE = a.row_elems;
   const int32_t G = int32_t((RE + kPer - 1) / kPer);  // 16-byte groups per row
   const int32_t row_bytes = int32_t(RE * int64_t(sizeof(S)));
@@ -126,7 +128,7 @@ __global__ __launch_bounds__(kBlock) void span_decode_kernel(SpanLaunch a, const
   };
 
   const uint32_t crc = span::pipeline<kBufs>(
-      sg.src, W, bufs, tab, a.tabs, lo_b + ((flags & tk::kSegCrcFirst) ? 21 : 0), do_crc,
+      sg.src, W, pt.k0, pt.k1, bufs, tab, a.tabs, lo_b + ((flags & tk::kSegCrcFirst) ? 21 : 0), do_crc,
       (flags & tk::kSegCrcFirst) != 0,
       [&] {  // setup: row positions (image bytes) and the window table, behind the first windows' loads
         const int64_t base = int64_t(sg.log_pos) - int64_t(head) - kFront;  // log position of image byte 0
@@ -142,7 +144,7 @@ __global__ __launch_bounds__(kBlock) void span_decode_kernel(SpanLaunch a, const
           const int32_t kf = r0 > lo_b ? r0 : lo_b, kl = min(r0 + (G - 1) * 16, hi_b - 1);
           span::row_wins_add(rw, W.nw, r0w + (t & ~63), in, W.win_of(kf), W.win_of(kl));
         }
-        if (sg.seg == 0 && bo.ext_words)
+        if (sg.seg == 0 && pt.q == 0 && bo.ext_words)
           for (uint32_t i = uint32_t(t); i < bo.ext_words; i += kThreads) bo.ext_out[i] = bo.ext_src[i];
       },
       [&](int k, const uint8_t* buf, int32_t off) {  // body: the groups window k owns
@@ -170,9 +172,11 @@ __global__ __launch_bounds__(kBlock) void span_decode_kernel(SpanLaunch a, const
 
   // ---- verdict: merge the lanes; thread 0 compares (or leaves the partial for the driver)
   if (do_crc) {
-    const uint32_t* shift_set = t < kThreads ? span::crc_merge(a.tabs, crc, wcrc) : nullptr;
+    if (t < kThreads) span::crc_merge(a.tabs, crc, wcrc);
     __syncthreads();
-    if (t == 0) span::crc_verdict(shift_set, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials);
+    if (t == 0)
+      span::crc_finish(a.tabs, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials, P, W.nw - pt.k1,
+                       a.part_acc + 2 * pt.seg);
   }
 }
 
@@ -193,7 +197,8 @@ __global__ __launch_bounds__(kBlock) void varlen_span_kernel(VarSpanLaunch a, D 
   __shared__ int32_t bad;
 
   const int t = int(threadIdx.x), lane = t & 63, wv = t >> 6;
-  const SpanDevSeg& sg = a.s[blockIdx.x];
+  const int P = a.parts;
+  const SpanDevSeg& sg = a.s[int(blockIdx.x) / P];
   const VarSpanBatch& bo = a.b[sg.batch];
   const uint32_t row_begin = sg.row_begin;
   const int32_t nrows = int32_t(sg.row_end - row_begin);
@@ -211,8 +216,8 @@ __global__ __launch_bounds__(kBlock) void varlen_span_kernel(VarSpanLaunch a, D 
   };
 
   if (flags & tk::kSegHostRows) {
-    // rows the worker copied into the slot (longer than one segment): a wave per row
-    if (wv >= kWaves) return;  // the loader wave has nothing to stage here
+    // rows the worker copied into the slot (longer than one segment): a wave per row, part 0's
+    if (wv >= kWaves || int(blockIdx.x) % P != 0) return;  // the loader wave has nothing to stage here
     for (int32_t rr = wv; rr < nrows; rr += kWaves) {
       const int64_t row = int64_t(row_begin) + rr;
       const tk::JsonSpanRow d = bo.rows[row];
@@ -232,9 +237,10 @@ __global__ __launch_bounds__(kBlock) void varlen_span_kernel(VarSpanLaunch a, D 
   const bool do_crc = (flags & tk::kSegCrc) != 0;
   const int32_t lo_b = kFront + head, hi_b = lo_b + int32_t(len);
   const span::Windows W(lo_b, hi_b);
+  const span::Part pt = span::part_of(P, W.nw);
 
   const uint32_t crc = span::pipeline<kBufs>(
-      sg.src, W, bufs, tab, a.tabs, lo_b + ((flags & tk::kSegCrcFirst) ? 21 : 0), do_crc,
+      sg.src, W, pt.k0, pt.k1, bufs, tab, a.tabs, lo_b + ((flags & tk::kSegCrcFirst) ? 21 : 0), do_crc,
       (flags & tk::kSegCrcFirst) != 0,
       [&] {  // setup: the row table (image bytes, elements to convert)
         const int64_t base = int64_t(sg.log_pos) - int64_t(head) - kFront;  // log position of image byte 0
@@ -254,14 +260,14 @@ __global__ __launch_bounds__(kBlock) void varlen_span_kernel(VarSpanLaunch a, D 
         span::row_wins_init(rw, W.nw);
         if (t == 0) bad = 0;
       },
-      [&] {  // prepare: padding, mask and lengths of every row; the windows its units start in
+      [&] {  // prepare: padding, mask and lengths of every row (part 0); the windows its units start in
         if (t >= kThreads) return;
         for (int32_t rr = wv; rr < nrows; rr += kWaves) {
           const int32_t n = nout[rr];
           if (n == -1) continue;  // copied by the worker (its kSegHostRows block writes it)
           if (n == -2 && lane == 0) bad = 1;
           const int64_t row = int64_t(row_begin) + rr;
-          finish(out + row * L, row, n < 0 ? 0 : n);
+          if (pt.q == 0) finish(out + row * L, row, n < 0 ? 0 : n);
         }
         for (int32_t r0w = 0; r0w < nrows; r0w += kThreads) {
           const int32_t r = r0w + t;
@@ -306,9 +312,11 @@ __global__ __launch_bounds__(kBlock) void varlen_span_kernel(VarSpanLaunch a, D 
       });
 
   if (do_crc) {
-    const uint32_t* shift_set = t < kThreads ? span::crc_merge(a.tabs, crc, wcrc) : nullptr;
+    if (t < kThreads) span::crc_merge(a.tabs, crc, wcrc);
     __syncthreads();
-    if (t == 0) span::crc_verdict(shift_set, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials);
+    if (t == 0)
+      span::crc_finish(a.tabs, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials, P, W.nw - pt.k1,
+                       a.part_acc + 2 * pt.seg);
   }
   if (t == 0 && bad) *bo.err = int32_t(sg.seg);
 }
@@ -317,13 +325,13 @@ template <typename S, typename D>
 void launch_var_span_t(const VarSpanLaunch& a, double pad, hipStream_t stream) {
   D padv;
   if constexpr (IsIntDst<D>::value) padv = D(int64_t(pad)); else padv = Store<D>::cvt(float(pad));
-  hipLaunchKernelGGL((varlen_span_kernel<S, D>), dim3(unsigned(a.n_seg)), dim3(kBlock), 0, stream, a, padv);
+  hipLaunchKernelGGL((varlen_span_kernel<S, D>), dim3(unsigned(a.n_seg * a.parts)), dim3(kBlock), 0, stream, a, padv);
 }
 
 template <typename S, typename D>
 void launch_span_t(const SpanLaunch& a, const float* shift, const float* scale, hipStream_t stream) {
   if (a.n_seg <= 0) return;
-  const dim3 grid(unsigned(a.n_seg));
+  const dim3 grid(unsigned(a.n_seg * a.parts));
   if (shift)
     hipLaunchKernelGGL((span_decode_kernel<S, D, true>), grid, dim3(kBlock), 0, stream, a, shift, scale);
   else
@@ -331,6 +339,13 @@ void launch_span_t(const SpanLaunch& a, const float* shift, const float* scale, 
 }
 
 }  // namespace
+
+int check_parts(int parts, const uint32_t* acc, const char* what) {
+  if (parts <= 1) return 1;
+  if ((parts != 2 && parts != tk::kSpanMaxParts) || acc == nullptr)
+    throw std::invalid_argument(std::string(what) + ": parts must be 1, 2 or 4 (with accumulator words)");
+  return parts;
+}
 
 void prewarm_span_kernels(int device) {
   (void)device;
@@ -342,7 +357,9 @@ void prewarm_span_kernels(int device) {
   (void)hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&span_decode_kernel<float, fp8e4m3, false>));
 }
 
-void launch_var_span(const VarSpanLaunch& a, int src_dt, int dst_dt, double pad, hipStream_t stream) {
+void launch_var_span(const VarSpanLaunch& a0, int src_dt, int dst_dt, double pad, hipStream_t stream) {
+  VarSpanLaunch a = a0;
+  a.parts = check_parts(a.parts, a.part_acc, "var span");
   if (a.n_seg < 0 || a.n_seg > kMaxLaunchSegs) throw std::invalid_argument("var span: bad segment count");
   if (a.n_seg == 0) return;
   if (!is_float_dt(dst_dt) && is_float_dt(src_dt))
@@ -360,8 +377,10 @@ void launch_var_span(const VarSpanLaunch& a, int src_dt, int dst_dt, double pad,
   if (e != hipSuccess) throw std::runtime_error(std::string("var span launch: ") + hipGetErrorString(e));
 }
 
-void launch_span_decode(const SpanLaunch& a, int src_dt, int dst_dt, const float* shift, const float* scale,
+void launch_span_decode(const SpanLaunch& a0, int src_dt, int dst_dt, const float* shift, const float* scale,
                         hipStream_t stream) {
+  SpanLaunch a = a0;
+  a.parts = check_parts(a.parts, a.part_acc, "span decode");
   if (a.n_seg < 0 || a.n_seg > kMaxLaunchSegs) throw std::invalid_argument("span decode: bad segment count");
   if (!is_float_dt(dst_dt) && is_float_dt(src_dt))
     throw std::invalid_argument("collate: float records cannot be cast to an integer dtype");

@@ -313,15 +313,43 @@ __device__ __forceinline__ const uint32_t* crc_merge(const uint32_t* __restrict_
   return shift_set;
 }
 
-// Thread 0 only, after a barrier that follows crc_merge: 3 levels merge the 8 wave CRCs.
-__device__ __forceinline__ void crc_verdict(const uint32_t* __restrict__ shift_set, const uint32_t* wcrc,
-                                            uint32_t flags, uint32_t want, uint32_t seg, int32_t* err,
-                                            uint32_t* partials) {
+// Segment parts (SpanLaunch::parts = P > 1): P workgroups share one segment, part q taking windows
+// [span_part_k0(q), span_part_k0(q + 1)) -- P times the loads in flight for a lone segment.  Each
+// part folds its windows' CRC pieces from a zero state (the gap operator of a zero state is zero),
+// merges its lanes, moves the result from the end of its last window to the segment's end
+// (kSpanTabWinShift, whole windows of zeros) and xors it into the segment's accumulator word; the
+// last part to arrive (an agent-scope counter beside it) takes the sum, gives the verdict and
+// leaves both words zero for the next launch on its stream.  Host mirror: crc32c_span_emulate.
+struct Part {
+  int32_t seg, q, k0, k1;
+};
+__device__ __forceinline__ Part part_of(int parts, int32_t nw) {
+  const int32_t b = int32_t(blockIdx.x), seg = b / parts, q = b - seg * parts;
+  return Part{seg, q, tk::span_part_k0(q, parts, nw), tk::span_part_k0(q + 1, parts, nw)};
+}
+
+// Thread 0 only, after a barrier that follows crc_merge: 3 levels merge the 8 wave CRCs; with
+// parts, the accumulation above; then the verdict (a RecordBatch held whole) or the raw partial.
+__device__ __forceinline__ void crc_finish(const uint32_t* __restrict__ tabs, const uint32_t* wcrc, uint32_t flags,
+                                           uint32_t want, uint32_t seg, int32_t* err, uint32_t* partials,
+                                           int parts, int32_t wins_after, uint32_t* acc) {
+  const uint32_t* shift_set = tabs + tk::kSpanTabShift;
   uint32_t c4[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) c4[i] = shift_op(shift_set, 6, wcrc[2 * i]) ^ wcrc[2 * i + 1];
   const uint32_t lo = shift_op(shift_set, 7, c4[0]) ^ c4[1], hi = shift_op(shift_set, 7, c4[2]) ^ c4[3];
-  const uint32_t c = shift_op(shift_set, 8, lo) ^ hi;
+  uint32_t c = shift_op(shift_set, 8, lo) ^ hi;
+  if (parts > 1) {
+#pragma unroll
+    for (uint32_t j = 0; j < tk::kSpanWinLevels; ++j)
+      if ((wins_after >> j) & 1) c = shift_op(tabs + tk::kSpanTabWinShift, j, c);
+    atomicXor(acc, c);
+    __threadfence();
+    if (atomicAdd(acc + 1, 1u) != uint32_t(parts - 1)) return;  // another part gives the verdict
+    __threadfence();
+    c = atomicExch(acc, 0u);
+    atomicExch(acc + 1, 0u);
+  }
   constexpr uint32_t kWhole = tk::kSegCrcFirst | tk::kSegCrcLast;
   if ((flags & kWhole) == kWhole) {
     if ((c ^ 0xFFFFFFFFu) != want) *err = int32_t(seg);
@@ -330,7 +358,8 @@ __device__ __forceinline__ void crc_verdict(const uint32_t* __restrict__ shift_s
   }
 }
 
-// The pipeline every span kernel runs (all kBlock threads call it).  The loader wave issues the
+// The pipeline every span kernel runs (all kBlock threads call it) over windows [k0, k1) of the
+// segment (all of them, or one part's).  The loader wave issues the
 // first NB - 1 windows; the compute threads meanwhile run `setup` (row tables into LDS); after a
 // barrier every thread runs `prepare` (per-row work that needs the tables: row window ranges,
 // scans, descriptors -- it may contain __syncthreads(); the loader wave's threads must do no work
@@ -341,15 +370,15 @@ __device__ __forceinline__ void crc_verdict(const uint32_t* __restrict__ shift_s
 //           its CRC pieces.
 // Returns the lane's CRC state (0 when the segment carries no CRC, and on the loader wave).
 template <int NB, class Setup, class Prepare, class Body>
-__device__ __forceinline__ uint32_t pipeline(const uint8_t* src, const Windows& W, uint8_t (*bufs)[kWinBytes],
-                                             uint32_t* tab, const uint32_t* __restrict__ tabs, int32_t c0,
-                                             bool do_crc, bool first, Setup&& setup, Prepare&& prepare,
-                                             Body&& body) {
+__device__ __forceinline__ uint32_t pipeline(const uint8_t* src, const Windows& W, int32_t k0, int32_t k1,
+                                             uint8_t (*bufs)[kWinBytes], uint32_t* tab,
+                                             const uint32_t* __restrict__ tabs, int32_t c0, bool do_crc, bool first,
+                                             Setup&& setup, Prepare&& prepare, Body&& body) {
   static_assert(NB >= 2 && NB <= 4, "2..4 window buffers");
   const uint8_t* gbase = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(src) & ~uintptr_t(15));
   const bool loader = loader_wave();
   if (loader) {
-    for (int k = 0; k < NB - 1 && k < W.nw; ++k) issue_window(gbase, W, k, bufs[k]);
+    for (int j = 0; j < NB - 1 && k0 + j < k1; ++j) issue_window(gbase, W, k0 + j, bufs[j]);
   } else {
     if (do_crc) load_nib_rows(tab, tabs);
     setup();
@@ -359,15 +388,16 @@ __device__ __forceinline__ uint32_t pipeline(const uint8_t* src, const Windows& 
   __syncthreads();  // (drains the loader's first windows: they were needed first anyway)
   const uint32_t nbase = uint32_t(uintptr_t((lds_u32*)tab));  // the LDS byte address
   uint32_t crc = 0;
-  for (int k = 0; k < W.nw; ++k) {
+  for (int k = k0; k < k1; ++k) {
+    const int j = k - k0;
     if (loader) {
-      // windows issued so far: up to min(k + NB - 2, nw - 1); all but those after k must have landed
-      loader_wait(min(k + NB - 2, W.nw - 1) - k);
+      // windows issued so far: up to min(k + NB - 2, k1 - 1); all but those after k must have landed
+      loader_wait(min(k + NB - 2, k1 - 1) - k);
       window_barrier();
-      if (k + NB - 1 < W.nw) issue_window(gbase, W, k + NB - 1, bufs[(k + NB - 1) % NB]);
+      if (k + NB - 1 < k1) issue_window(gbase, W, k + NB - 1, bufs[(j + NB - 1) % NB]);
     } else {
       window_barrier();  // window k landed; every compute wave is done with window k - 1's buffer
-      uint8_t* buf = bufs[k % NB];
+      uint8_t* buf = bufs[j % NB];
       const int32_t off = kPad - W.stage_lo(k);
 #ifndef TKH_SPAN_PROBE_NO_BODY  // tools/probes/span_bench.hip builds variants without one stage
       body(k, buf, off);  // stores first: they drain while the CRC runs
