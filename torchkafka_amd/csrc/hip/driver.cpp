@@ -469,6 +469,10 @@ void MainDriver::launch_span(const int* slots, const SlotView* const* views, int
   a.vec_store = vec ? 1 : 0;
   bool pcie = false;  // a segment of this launch is read over PCIe (not from the HBM mirror)
   auto flush = [&](bool record) {
+    // segments split over parts only when every one is read from HBM: parts multiply the loads in
+    // flight of a lone group from the mirror, while over PCIe the link is the limit and more
+    // workgroups only add their fixed costs (profiles/r05_s20)
+    a.parts = pcie ? 1 : eng_->span_parts();
     pcie = false;
     if (mirror) mirror->before(stream);
     eng_->collate_span(slots, n, stream, a, v0.src_dtype, dst_dt, shift, scale, record);
@@ -586,6 +590,7 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
     off += batch_bytes[k];
   }
   auto flush = [&]() {
+    a.parts = pcie ? 1 : eng_->json_span_parts();  // parts only for segments all read from HBM (launch_span)
     pcie = false;
     if (mirror) mirror->before(stream);
     eng_->collate_json_stage(slots, n, stream, a);
@@ -650,7 +655,7 @@ void MainDriver::launch_var_span(const int* slots, const SlotView* const* views,
       a.b[k].rows = reinterpret_cast<const tk::JsonSpanRow*>(a.b[k].slot);
     }
     a.tabs = eng_->span_tables();
-    a.parts = eng_->span_parts();
+    a.parts = pcie ? 1 : eng_->span_parts();  // parts only for segments all read from HBM (launch_span)
     a.part_acc = a.parts > 1 ? eng_->part_acc(stream) : nullptr;
     pcie = false;
     if (mirror) mirror->before(stream);

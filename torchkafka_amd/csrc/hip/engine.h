@@ -99,6 +99,10 @@ class Engine {
   // ones finished), so consecutive launches must not share words.
   static constexpr int kPartAccSets = 16;
   int span_parts() const { return span_parts_; }
+  // The JSON stage kernel keeps one workgroup per segment unless TORCHKAFKA_SPAN_PARTS is set: its
+  // parts each redo the segment's row scan (config 4 through the mirror: 47-50 M with 4 parts
+  // against 51-52 M with 1, profiles/r05_s23).
+  int json_span_parts() const { return json_parts_; }
   uint32_t* part_acc(hipStream_t stream);
   // The streams device-decode groups rotate over (created on first use; kDecodeStreams).
   hipStream_t decode_stream(int k);
@@ -155,7 +159,8 @@ class Engine {
   uint8_t* host_dev_ = nullptr;           // device view of the registered host region (zero-copy)
   size_t host_len_ = 0;
   uint32_t* span_tabs_ = nullptr;
-  int span_parts_ = 1;
+  int span_parts_ = 4;  // HBM-sourced fixed-width / var-len launches (profiles/r05_s20_s22_parts)
+  int json_parts_ = 1;
   struct PartAcc {
     hipStream_t stream;
     uint32_t* words;

@@ -45,6 +45,7 @@ Engine::Engine(int device, int n_slots, size_t staging_bytes, int n_streams, int
     const int p = std::atoi(e);
     span_parts_ = p == 2 || p == tk::kSpanMaxParts ? p : 1;
   }
+  json_parts_ = std::getenv("TORCHKAFKA_SPAN_PARTS") ? span_parts_ : 1;
   if (n_slots <= 0) throw std::invalid_argument("engine: n_slots must be positive");
   if (mode != kH2DDma && mode != kH2DZeroCopy) throw std::invalid_argument("engine: bad h2d mode");
   if (n_streams < 1) n_streams = 1;
@@ -402,8 +403,7 @@ void Engine::collate_span(const int* slots, int n, hipStream_t user, SpanLaunch&
     if (a.b[k].ext_words) a.b[k].ext_src = reinterpret_cast<const int64_t*>(src_base(slots[k]) + a.b[k].ext_off);
   }
   a.tabs = span_tables();
-  a.parts = span_parts_;
-  a.part_acc = span_parts_ > 1 ? part_acc(user) : nullptr;
+  a.part_acc = a.parts > 1 ? part_acc(user) : nullptr;  // the caller chose the parts
   if (queued(user)) {
     queue().submit([a, src_dt, dst_dt, shift, scale, user] {
       launch_span_decode(a, src_dt, dst_dt, shift, scale, user);
@@ -423,8 +423,7 @@ void Engine::collate_json_stage(const int* slots, int n, hipStream_t user, JsonS
     a.b[k].rows = reinterpret_cast<const tk::JsonSpanRow*>(a.b[k].slot);
   }
   a.tabs = span_tables();
-  a.parts = span_parts_;
-  a.part_acc = span_parts_ > 1 ? part_acc(user) : nullptr;
+  a.part_acc = a.parts > 1 ? part_acc(user) : nullptr;  // the caller chose the parts
   if (queued(user))
     queue().submit([a, user] { launch_json_stage(a, user); });
   else
