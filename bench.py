@@ -90,7 +90,7 @@ def parse():
     ap.add_argument("--mirror-chunk-mib", type=int, default=8,
                     help="--h2d dma with device decode: MiB per hipMemcpyAsync into the HBM log mirror")
     ap.add_argument("--mirror-chunks", type=int, default=None, help="--h2d dma: HBM mirror buffers per partition")
-    ap.add_argument("--lockstep-depth", type=int, default=2)
+    ap.add_argument("--lockstep-depth", type=int, default=None, help="default: the loader's auto depth")
     ap.add_argument("--verify", default="deliver", choices=["deliver", "commit"],
                     help="deliver: a batch is handed out after its device CRC verdict landed (default); commit: "
                          "the verdict gates only its commit")
@@ -672,7 +672,8 @@ def run_rank(args) -> int:
         return DeviceLoader(
             ds.placeholder(), B, num_workers=args.workers, device=device, dtype=dtype,
             slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
-            in_order=args.in_order, h2d=h2d, copy_streams=args.copy_streams, lockstep_depth=args.lockstep_depth,
+            in_order=args.in_order, h2d=h2d, copy_streams=args.copy_streams,
+            **({"lockstep_depth": args.lockstep_depth} if args.lockstep_depth is not None else {}),
             event_every=args.event_every, numa_bind=not args.no_numa, coalesce=args.coalesce,
             coalesce_wait_us=args.coalesce_wait_us, decode=args.decode,
             lockstep=lockstep if lockstep_mode is None else lockstep_mode,

@@ -83,6 +83,7 @@ def test_direct_gather_and_ring_sizing():
     p = plan(FIXED, h2d="direct")
     assert p.direct and not p.span and p.resolve_h2d(10) == "direct"
     assert plan(FIXED).slots_per_worker(4096, 4) == 16            # row tables: deep ring
+    assert plan(FIXED).slots_per_worker(4096, 4, deep=True) == 64  # under an RCCL lockstep: deeper
     assert plan(FIXED, decode="host").slots_per_worker(1 << 20, 4) == 8
     assert plan(FIXED, decode="host").slots_per_worker(64 << 20, 4) == 4
     assert plan(FIXED, decode="host").layout_capacity(256, FIXED) == 256 * 64

@@ -44,8 +44,9 @@ PROCESS_ENV = {
     "TORCHKAFKA_RCCL_WORDS": "kernel (default) / host / copy: how the RCCL lockstep's agreement words reach "
                              "RCCL -- tiny copy kernels, RCCL on host-mapped memory, or hipMemcpyAsync "
                              "(csrc/hip/rccl_lockstep.hip)",
-    "TORCHKAFKA_LOCKSTEP_PRIORITY": "high (default) / normal: the RCCL lockstep stream's priority; high gives it a "
-                                    "hardware queue of its own (tools/probes/queue_probe.py)",
+    "TORCHKAFKA_LOCKSTEP_PRIORITY": "normal (default) / high: the RCCL lockstep stream's priority; high gives it a "
+                                    "hardware queue of its own, where its agreements came back slower "
+                                    "(profiles/r05_s19_rccl_matrix)",
     "TORCHKAFKA_TORCH_NCCL_ACTIVE": "1: DeviceLoader.stream_plan() counts torch's own NCCL streams at world 1 "
                                     "(a world-1 nccl group that ran a collective, as bench.py's N = 8 queue "
                                     "rehearsal does)",
@@ -94,7 +95,10 @@ class Tuning:
         event_every: record a completion event every k slots; None = ring slots / 4, at most 4.
         coalesce: staged batches collated per kernel launch (1..8; 1 disables).
         coalesce_wait_us: how long to wait for a fuller group while the GPU is busy (0..10000).
-        lockstep_depth: cross-rank agreements issued ahead of use (0..64).
+        lockstep_depth: steps before its credits run out that the next cross-rank agreement is issued
+            (0..64); None = auto: 32 under the RCCL lockstep with device decode (whose ring is then 64
+            slots per worker deep, so an agreement's ~60-180 µs round trip is covered by the steps
+            its credits still allow: profiles/r05_s24), else 2.
         numa_bind: bind the loader (and its workers) to the target GPU's socket.
         ahead_depth: device-decode groups launched ahead of the user's request (0..16); None = 4.
         decode_streams: HIP streams for the device decode kernels (1..4); None = 3.
@@ -122,7 +126,7 @@ class Tuning:
     event_every: Optional[int] = None
     coalesce: int = 8
     coalesce_wait_us: int = 50
-    lockstep_depth: int = 2
+    lockstep_depth: Optional[int] = None
     numa_bind: Optional[bool] = None
     ahead_depth: Optional[int] = None
     decode_streams: Optional[int] = None
@@ -153,7 +157,7 @@ class Tuning:
         _check(self.event_every is None or 1 <= int(self.event_every) <= 4096, "event_every must be >= 1 (or None)")
         _check(1 <= int(self.coalesce) <= 8, "coalesce must be in [1, 8]")
         _check(0 <= int(self.coalesce_wait_us) <= 10_000, "coalesce_wait_us must be in [0, 10000]")
-        _check(0 <= int(self.lockstep_depth) <= 64, "lockstep_depth must be in [0, 64]")
+        _check(self.lockstep_depth is None or 0 <= int(self.lockstep_depth) <= 64, "lockstep_depth must be in [0, 64]")
         _check(self.ahead_depth is None or 0 <= int(self.ahead_depth) <= 16, "ahead_depth must be in [0, 16]")
         _check(self.decode_streams is None or 1 <= int(self.decode_streams) <= 4, "decode_streams must be in [1, 4]")
         _check(0 <= int(self.worker_spin_us) <= 100_000, "worker_spin_us must be in [0, 100000]")

@@ -87,7 +87,7 @@ class RcclLockstep : public LockstepTransport {
   int64_t* h_in_dev_ = nullptr;   // their device addresses
   int64_t* h_out_dev_ = nullptr;
   int mode_ = 0;               // 0 kernel, 1 host, 2 copy (TORCHKAFKA_RCCL_WORDS)
-  bool high_prio_ = true;      // stream_ at the greatest priority (its own hardware-queue pool)
+  bool high_prio_ = false;     // stream_ at the greatest priority (its own hardware-queue pool)
   std::vector<hipEvent_t> ev_;
   uint64_t issued_ = 0;
   int64_t timeout_ms_ = 600000;  // like torch.distributed's default NCCL timeout

@@ -96,12 +96,13 @@ RcclLockstep::RcclLockstep(const std::string& lib_path, const std::string& id, i
   slot_rec_.assign(size_t(slots_), -1);
   api_ = load_api(lib_path);
   TKH_HIP(hipSetDevice(device_));
-  // the lockstep's stream at the device's greatest priority: HIP keeps a hardware-queue pool per
-  // priority, so it never shares a queue with the decode and copy streams (normal priority) or the
-  // user's -- a decode launch never waits behind a collective that waits for the other ranks
-  // (tools/probes/queue_probe.py); TORCHKAFKA_LOCKSTEP_PRIORITY=normal for the A/B
+  // At the device's greatest priority the lockstep's stream would get a hardware-queue pool of its
+  // own (tools/probes/queue_probe.py), never sharing a queue with the decode streams.
+  // Normal priority by default: on a queue of its own at the greatest priority an agreement took
+  // ~110 µs to come back in the loop against ~60 µs on a normal one (profiles/r05_s19_rccl_matrix,
+  // r05_s24); TORCHKAFKA_LOCKSTEP_PRIORITY=high restores the separate queue
   const char* pe = std::getenv("TORCHKAFKA_LOCKSTEP_PRIORITY");
-  high_prio_ = !(pe && std::string(pe) == "normal");
+  high_prio_ = pe && std::string(pe) == "high";
   if (high_prio_) {
     int least = 0, greatest = 0;
     TKH_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));

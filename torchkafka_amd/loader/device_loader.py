@@ -497,7 +497,7 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
         self.event_every = None if tun.event_every is None else int(tun.event_every)
         self.coalesce = int(tun.coalesce)
         self.coalesce_wait_us = int(tun.coalesce_wait_us)
-        self.lockstep_depth = int(tun.lockstep_depth)
+        self.lockstep_depth = None if tun.lockstep_depth is None else int(tun.lockstep_depth)
         self.numa_bind = bool(tun.numa_bind)
         self._bridges: list = []
         if self.num_workers > 0 and cfg.bridge is not False:
@@ -569,7 +569,20 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
     def _slots_per_worker(self) -> int:
         if self.slots_per_worker is not None:
             return self.slots_per_worker
-        return self.plan.slots_per_worker(self._slot_capacity(), self.n_producers)
+        try:
+            rccl = self._lockstep_transport() == "rccl"
+        except Exception:  # noqa: BLE001 - no process group to ask: no lockstep
+            rccl = False
+        return self.plan.slots_per_worker(self._slot_capacity(), self.n_producers, deep=rccl)
+
+    def _lockstep_depth(self, transport) -> int:
+        """Tuning.lockstep_depth, or its auto value: an RCCL agreement takes ~60-180 µs to come back
+        while device-decoded steps take ~5 µs, so with the 64-deep ring the next one is issued 32
+        steps before the credits run out (profiles/r05_s24: the wait per step 0.4-0.7 µs at depth 2,
+        0.003 µs at 32); the host lockstep keeps 2."""
+        if self.lockstep_depth is not None:
+            return self.lockstep_depth
+        return 32 if transport == "rccl" and self.plan.device_decode else 2
 
     def _n_extras(self) -> int:
         """Record-field columns (Key / Timestamp) the schema adds beside the value."""
@@ -647,7 +660,7 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
                             run.rccl = hip().PyLockstep(_host_allreduce_min(process_group))
                             self.lockstep_info = {"transport": "host", "backend": dist.get_backend(process_group),
                                                   "world_size": dist.get_world_size(process_group)}
-                        run.driver.enable_lockstep(run.rccl, self.lockstep_depth)
+                        run.driver.enable_lockstep(run.rccl, self._lockstep_depth(transport))
                     else:
                         from ..parallel.lockstep import Lockstep
 
@@ -662,9 +675,10 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
             if self.lockstep_info:
                 self.lockstep_info["streams"] = plan
             if plan["shared"]:
-                lvl = logging.WARNING if plan["rccl_lockstep"] else logging.DEBUG
-                log.log(lvl, "DeviceLoader: %d HIP streams on %d hardware queues (%s): some share a queue",
-                        plan["total"], plan["hw_queues"], plan)
+                # measured: the lockstep on a shared normal-priority queue came back in ~60 µs, on a
+                # queue of its own at the greatest priority in ~110 µs (profiles/r05_s19_rccl_matrix)
+                log.debug("DeviceLoader: %d HIP streams on %d hardware queues (%s): some share a queue",
+                          plan["total"], plan["hw_queues"], plan)
             yield from self._iterate_native(run, auto_commit)
             return
         finished = self._pending_wms
@@ -769,7 +783,7 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
             via_group = dist.new_group(ranks=ranks, backend="gloo")  # collective: every rank gets here
         dist.broadcast_object_list(uid, src=src, group=via_group, device=torch.device("cpu"))
         dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
-        ls = hip().RcclLockstep(lib, uid[0], rank, world, dev, self.lockstep_depth + 2)
+        ls = hip().RcclLockstep(lib, uid[0], rank, world, dev, self._lockstep_depth("rccl") + 2)
         ls.set_timeout_ms(int(self.lockstep_timeout * 1000))
         # start-up proof that the communicator spans the whole job: RCCL's own count of its ranks,
         # and one all-reduce of the rank ids over it

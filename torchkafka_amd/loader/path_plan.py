@@ -156,12 +156,14 @@ class PathPlan:
             return B * schema.row_bytes
         return 16 << 20
 
-    def slots_per_worker(self, slot_capacity: int, n_producers: int) -> int:
-        """Ring depth per worker when not configured."""
+    def slots_per_worker(self, slot_capacity: int, n_producers: int, deep: bool = False) -> int:
+        """Ring depth per worker when not configured.  ``deep``: an RCCL lockstep -- its agreements
+        grant the batches staged beyond the last grant, so a deeper ring makes them rarer and gives
+        each one more steps to come back in (DeviceLoader._lockstep_depth)."""
         if self.device_decode:
             # device-decode slots hold row positions only (a few KiB): a deep ring costs no pinned
             # memory and lets the workers run ahead while slots wait for their kernels
-            return 16
+            return 64 if deep else 16
         budget = RING_AUTO_BYTES
         if self.kind in (1, 2) and self.cuda:
             # var-len / JSON slots are sized for the worst row (16 MiB) but hold a few hundred KiB:
