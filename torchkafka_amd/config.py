@@ -109,7 +109,7 @@ class Tuning:
             6 by default.  Each launch's prefetches are queued after its copy event (a launch never
             waits for them): 8 MiB x 6 then runs 48-49 M rec/s steady (13-47 M before, when a launch's
             event also covered its own prefetches); 8 buffers still collapse (8-11 M; avoid).
-            tools/mirror_probe.sh, tools/mirror_probe2.sh.
+            tools/sessions/experiments/mirror_probe.sh, mirror_probe2.sh.
         group_mib: device-decode groups stop growing at this many MiB of log bytes (1..1024): a
             group's batches become committable together, so large batches form small groups.
         json_count: JsonArray rows parsed on the device from the logs: who counts their elements.
