@@ -17,7 +17,8 @@ import sys
 
 
 def short(name: str) -> str:
-    n = re.sub(r"\(.*", "", name)
+    n = name.replace("(anonymous namespace)::", "")  # its parentheses are not the argument list
+    n = re.sub(r"\(.*", "", n)
     n = re.sub(r"^void ", "", n)
     if len(n) > 70:
         n = n[:67] + "..."

@@ -338,6 +338,7 @@ PYBIND11_MODULE(_tkhip, m) {
              s["coalesce_wait_ns"] = d.cwait_ns_;
              s["ahead_groups"] = d.ahead_groups_;
              s["ahead_ns"] = d.ahead_ns_;
+             s["split_launches"] = d.split_launches_;
              s["json_width_wait_ns"] = d.json_width_wait_ns();
              s["occ_handed"] = d.occ_handed_;
              s["occ_staged"] = d.occ_staged_;

@@ -473,6 +473,7 @@ void MainDriver::launch_span(const int* slots, const SlotView* const* views, int
     // flight of a lone group from the mirror, while over PCIe the link is the limit and more
     // workgroups only add their fixed costs (profiles/r05_s20)
     a.parts = pcie ? 1 : eng_->span_parts();
+    split_launches_ += a.parts > 1;
     pcie = false;
     if (mirror) mirror->before(stream);
     eng_->collate_span(slots, n, stream, a, v0.src_dtype, dst_dt, shift, scale, record);
@@ -591,6 +592,7 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
   }
   auto flush = [&]() {
     a.parts = pcie ? 1 : eng_->json_span_parts();  // parts only for segments all read from HBM (launch_span)
+    split_launches_ += a.parts > 1;
     pcie = false;
     if (mirror) mirror->before(stream);
     eng_->collate_json_stage(slots, n, stream, a);
@@ -657,6 +659,7 @@ void MainDriver::launch_var_span(const int* slots, const SlotView* const* views,
     a.tabs = eng_->span_tables();
     a.parts = pcie ? 1 : eng_->span_parts();  // parts only for segments all read from HBM (launch_span)
     a.part_acc = a.parts > 1 ? eng_->part_acc(stream) : nullptr;
+    split_launches_ += a.parts > 1;
     pcie = false;
     if (mirror) mirror->before(stream);
     eng_->run_on(stream, [a, src_dt, dst_dt, pad, stream] { tkh::launch_var_span(a, src_dt, dst_dt, pad, stream); });
@@ -1144,7 +1147,7 @@ void MainDriver::reset_stats() {
   ph_commit_ns_ = ph_next_ns_ = ph_launch_ns_ = ph_steps_ = events_ = groups_ = 0;
   rel_ns_ = released_ = cwait_ns_ = 0;
   occ_handed_ = occ_staged_ = occ_samples_ = 0;
-  ahead_groups_ = ahead_ns_ = 0;
+  ahead_groups_ = ahead_ns_ = split_launches_ = 0;
   verdicts_->width_wait_ns = 0;
   fast_batches_ = fast_records_ = fast_ns_ = 0;
   verify_wait_ns_ = 0;

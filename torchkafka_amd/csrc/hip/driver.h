@@ -271,6 +271,7 @@ class MainDriver {
   int64_t cwait_ns_ = 0;  // time spent waiting for a full group while the GPU was busy
   int64_t ahead_groups_ = 0;  // device-decode groups launched ahead of delivery
   int64_t ahead_ns_ = 0;      // host time forming, allocating and launching them (torch_step.cpp)
+  int64_t split_launches_ = 0;  // decode launches with each segment split over workgroups (parts > 1)
   int64_t occ_handed_ = 0, occ_staged_ = 0, occ_samples_ = 0;  // slots launched / staged, summed per step
 
   // Per-iteration constants of the fixed-width fast path (set once by torch_step.cpp's

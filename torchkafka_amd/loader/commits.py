@@ -110,6 +110,7 @@ class LoaderCommits:
         self.stats.log_register_wait_ns = st.get("log_register_wait_ns", 0)
         self.stats.mirror_bytes += st.get("mirror_bytes_copied", 0)
         self.stats.mirror_copies += st.get("mirror_copies", 0)
+        self.stats.split_launches += st.get("split_launches", 0)
         self.stats.mirror_fallbacks += st.get("mirror_fallbacks", 0)
         self.stats.mirror_pending_fallbacks += st.get("mirror_pending_fallbacks", 0)
         self.stats.verify_wait_ns += st.get("verify_wait_ns", 0)

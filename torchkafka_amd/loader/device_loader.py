@@ -29,14 +29,8 @@ whatever the prefetch depth and whichever worker produced the batch (D5).
 from __future__ import annotations
 
 import ctypes
-import gc
 import logging
-import multiprocessing as mp
-import os
-import threading
 import time
-import uuid
-from collections import deque
 from typing import NamedTuple
 
 import torch
@@ -46,14 +40,14 @@ from ..config import LoaderConfig
 from ..ops.collate import CODE_DTYPE, DTYPE_CODE, FLOAT_DTYPES, _stream_ptr, normalize_params
 from ..ops.native import core, hip
 from ..parallel.sharding import dist_rank_world
-from ..utils import topology
 from ..utils.metrics import LoaderStats
 from ..utils.tracing import enabled as _roctx_enabled
 from ..utils.tracing import trace_range
 from .bridging import LoaderBridges
 from .commits import LoaderCommits
+from .lockstep import LoaderLockstep, _host_allreduce_min
 from .path_plan import PathPlan
-from .worker import worker_main
+from .run import WorkerError, _Run
 
 log = logging.getLogger(__name__)
 _ds_logger = logging.getLogger("torchkafka.kafka_dataset")
@@ -67,23 +61,6 @@ def _traced_step(step):
     return traced
 
 
-def _host_allreduce_min(group):
-    """all-reduce(MIN) of the lockstep's four int64 words (credit, step, -step, commit status) over a
-    CPU (gloo) group, for the driver's PyLockstep transport."""
-    import torch.distributed as dist
-
-    if dist.get_backend(group) != "gloo":
-        group = dist.new_group(backend="gloo")  # collective: every rank builds its loader iterator
-    buf = torch.zeros(4, dtype=torch.int64)
-
-    def allreduce_min(a: int, b: int, c: int, d: int):
-        buf[0], buf[1], buf[2], buf[3] = a, b, c, d
-        dist.all_reduce(buf, op=dist.ReduceOp.MIN, group=group)
-        return int(buf[0]), int(buf[1]), int(buf[2]), int(buf[3])
-
-    return allreduce_min
-
-
 class KafkaBatch(NamedTuple):
     """Batch plus provenance (``return_info=True``)."""
 
@@ -94,237 +71,7 @@ class KafkaBatch(NamedTuple):
     n_records: int        # records consumed incl. skipped ones
 
 
-class WorkerError(RuntimeError):
-    pass
-
-
-class _PackerThread(threading.Thread):
-    """num_workers=0: the ring producer as a thread of the main process (looks like a worker
-    process to the liveness checks)."""
-
-    def __init__(self, ring, name, dataset, cfg):
-        super().__init__(target=worker_main, args=(ring, name, 0, 1, dataset, None, cfg), daemon=True,
-                         name="torchkafka-packer")
-        self.pid = os.getpid()
-
-    @property
-    def exitcode(self):
-        return None if self.is_alive() else 0
-
-    def terminate(self):  # stops at ring.shutdown(); nothing to signal
-        pass
-
-
-class _Run:
-    """Resources of one iteration: ring, worker processes, H2D engine."""
-
-    def __init__(self, loader: "DeviceLoader"):
-        self.loader = loader
-        L = loader
-        self.name = f"/tkring-{os.getpid()}-{uuid.uuid4().hex[:10]}"
-        self.ring = core().Ring.create(self.name, L.n_producers, L._slots_per_worker(), L._slot_capacity())
-        self.procs: list = []
-        self.engine = None
-        self.driver = None
-        self.rccl = None
-        self.payload_addr = [self.ring.payload_address(g) for g in range(self.ring.n_slots)]
-        self.staged: deque = deque()       # (g, summary, wms) with H2D issued (or CPU: just acquired)
-        self.inflight: list = []           # slots whose H2D may still be reading host memory
-        self.done = [False] * L.n_producers
-        self.carry: list = []              # watermarks of consumed-but-undelivered records
-        self.closed = False
-        if L.numa_bind and L.device.type == "cuda" and L.device.index is not None:
-            # before the fork: the workers inherit the mask, and the ring pages they first-touch land on
-            # the GPU's socket (utils/topology.py)
-            topology.bind_to_gpu_numa(L.device.index)
-        ctx = mp.get_context(L.multiprocessing_context)
-        cfg = L._worker_cfg()
-        self.table = None          # commit_sink='worker': finished offsets published to the workers
-        self.pidx_worker: dict = {}
-        if L._sink == "worker":
-            from .commit_channel import WatermarkTable
-
-            self.table = WatermarkTable(L.n_producers)
-            cfg["commit_table"] = self.table
-        pass_ring = L.multiprocessing_context == "fork"
-        try:
-            if L.num_workers == 0:
-                # single-process mode: the packer runs in a thread of this process (the native fill
-                # releases the GIL), on the dataset's own consumer
-                cfg["in_process"] = True
-                t = _PackerThread(self.ring, self.name, L.dataset, cfg)
-                t.start()
-                self.procs.append(t)
-            # A forked child must never run the finalizers of the parent's objects: when this process
-            # already initialised HIP (a second epoch, a test session), a garbage CUDA tensor
-            # collected in the child calls into a runtime that does not exist there (SIGSEGV right
-            # after the fork, measured).  Collect now and freeze what is left out of the child's GC.
-            frozen = pass_ring and L.num_workers > 0
-            if frozen:
-                gc.collect()
-                gc.freeze()
-            try:
-                for w in range(L.num_workers):
-                    p = ctx.Process(target=worker_main,
-                                    args=(self.ring if pass_ring else None, self.name, w, L.num_workers,
-                                          L.dataset, L.worker_init_fn, cfg),
-                                    daemon=True, name=f"torchkafka-worker-{w}")
-                    p.start()
-                    self.procs.append(p)
-            finally:
-                if frozen:
-                    gc.unfreeze()
-            if L.device.type == "cuda":
-                # only after the fork: workers never inherit an initialised HIP runtime state they would use
-                dev = L.device.index if L.device.index is not None else torch.cuda.current_device()
-                # device decode with h2d='dma': the slots (row tables) are read zero-copy and the copy
-                # engines move the log bytes into an HBM mirror (enable_mirror below)
-                mode = hip().H2D_ZERO_COPY if (L.plan.resolve_h2d(self.ring.payload_capacity) in ("zerocopy", "direct")
-                                               or L.plan.mirror) else hip().H2D_DMA
-                self.engine = hip().Engine(dev, self.ring.n_slots, self.ring.payload_capacity, L.copy_streams, mode)
-                if L.tuning.decode_streams is not None:  # before anything creates a decode stream
-                    self.engine.set_decode_streams(int(L.tuning.decode_streams))
-                elif L._lockstep_transport() == "rccl":
-                    # HIP gives a process 4 hardware queues: the user's stream, two decode streams and
-                    # the lockstep's RCCL stream each keep one, so a collective waiting for the other
-                    # ranks never sits in front of a decode kernel those ranks' progress depends on
-                    self.engine.set_decode_streams(2)
-                if L.numa_bind:
-                    topology.check_device(dev)
-                url, group = L._commit_target_url()
-                self.driver = hip().MainDriver(self.engine, self.name, url, group, L.prefetch, L.in_order,
-                                               L._default_src_code())
-                self.driver.set_commit_on_device(L.commit_on == "device")
-                if self.table is not None:
-                    self.driver.set_worker_sink(self.table.address, L.n_producers, self.table.capacity)
-                self.driver.set_event_every(L._event_every(self.ring.n_slots))
-                self.driver.set_coalesce(L.coalesce)
-                self.driver.set_coalesce_wait_us(L.coalesce_wait_us if L.coalesce > 1 else 0)
-                if L.plan.direct:
-                    self.driver.enable_direct()
-                if L.plan.direct or L.plan.device_decode:
-                    self.driver.pin_logs(L._rank_partitions())
-                if L.plan.mirror:
-                    # under the RCCL lockstep one SDMA copy stream: the process's 4 hardware queues
-                    # go to the user's stream, two decode streams and the lockstep's RCCL stream
-                    mcs = 1 if L._lockstep_transport() == "rccl" else 0
-                    self.driver.enable_mirror(int(L.tuning.mirror_chunk_mib) << 20, int(L.tuning.mirror_chunks), mcs)
-                tun = L.tuning
-                if tun.ahead_depth is not None:
-                    self.driver.set_ahead_depth(int(tun.ahead_depth))
-                self.driver.set_group_bytes(int(tun.group_mib) << 20)
-                # var-len / JSON device decode: the launches of the groups decoded ahead go through the
-                # HIP command queue (csrc/hip/hip_queue.h; config 4 +9 %); fixed-width decode keeps
-                # them on this thread (the 20-step headline lost 12 % to the queue's hand-off)
-                self.driver.set_command_queue(bool(L.plan.json_span or L.plan.var_span))
-        except BaseException:
-            self.close()
-            raise
-
-    # ------------------------------------------------------------------ slot acquisition
-    def _check_workers(self) -> None:
-        for w, p in enumerate(self.procs):
-            if not self.done[w] and not p.is_alive():
-                raise WorkerError(f"DeviceLoader worker {w} (pid {p.pid}) exited unexpectedly "
-                                  f"with exit code {p.exitcode}")
-
-    def _check_workers_native(self) -> None:
-        for w, p in enumerate(self.procs):
-            if not p.is_alive() and not self.driver.worker_done(w):
-                raise WorkerError(f"DeviceLoader worker {w} (pid {p.pid}) exited unexpectedly "
-                                  f"with exit code {p.exitcode}")
-
-    def acquire(self, block: bool):
-        """Next READY slot as (g, summary, wms), or None (nothing ready / end of stream)."""
-        ring = self.ring
-        in_order = self.loader.in_order
-        deadline = None if self.loader.timeout <= 0 else time.monotonic() + self.loader.timeout
-        while True:
-            g = ring.main_acquire(100 if block else 0, in_order)
-            if g == -2:
-                return None  # every worker delivered end-of-stream
-            if g < 0:
-                if not block:
-                    return None
-                self._check_workers()
-                if deadline is not None and time.monotonic() > deadline:
-                    raise TimeoutError(f"DeviceLoader timed out after {self.loader.timeout}s waiting for a batch")
-                continue
-            summ = ring.slot_summary(g)
-            n_rows, flags = summ[0], summ[1]
-            if flags & core().SLOT_ERROR:
-                err = ring.slot_info(g)["error"]
-                ring.main_release(g)
-                raise WorkerError(err)
-            if flags & core().SLOT_EOS:
-                w = summ[6]
-                self.done[w] = True
-                ring.mark_done(w)
-            wms = ring.watermarks(g)
-            if self.table is not None:
-                for w in wms:
-                    self.pidx_worker[w[0]] = summ[6]
-            if n_rows == 0:
-                # empty (end-of-stream) slot: no data, but its watermarks may cover skipped records;
-                # it stays in delivery order so they are committed after the worker's earlier batches
-                ring.main_release(g)
-                if not wms:
-                    continue
-                return g, summ, wms
-            if self.engine is not None:
-                self.engine.h2d(g, self.payload_addr[g], summ[2])
-                self.inflight.append(g)
-            return g, summ, wms
-
-    def release_completed(self) -> None:
-        if not self.inflight:
-            return
-        keep = []
-        for g in self.inflight:
-            if self.engine.h2d_complete(g):
-                self.ring.main_release(g)
-            else:
-                keep.append(g)
-        self.inflight = keep
-
-    def wait_worker_commits(self, timeout: float) -> bool:
-        """commit_sink='worker': waits until every live worker acknowledged its latest request."""
-        return self.table.wait_acks(timeout=timeout, alive=lambda w: self.procs[w].is_alive()
-                                    if w < len(self.procs) else False)
-
-    def close(self) -> None:
-        if self.closed:
-            return
-        self.closed = True
-        if self.table is not None:
-            # the workers' consumers commit what the user finished before they are stopped
-            self.wait_worker_commits(10.0)
-        try:
-            self.ring.shutdown()
-        except Exception:  # noqa: BLE001
-            pass
-        for p in self.procs:
-            p.join(timeout=5)
-            if p.is_alive():
-                p.terminate()
-                p.join(timeout=5)
-        if self.engine is not None:
-            try:
-                self.engine.synchronize()
-            except Exception:  # noqa: BLE001
-                log.exception("engine teardown failed")
-        self.driver = None  # unregisters its pinned ring mapping
-        self.rccl = None
-        self.engine = None
-        if self.table is not None:
-            self.table.close()
-        try:
-            self.ring.unlink()
-        except Exception:  # noqa: BLE001
-            pass
-
-
-class DeviceLoader(LoaderBridges, LoaderCommits):
+class DeviceLoader(LoaderBridges, LoaderCommits, LoaderLockstep):
     """Streams a :class:`KafkaDataset` to device tensors.
 
     Mirrors ``DataLoader(dataset, batch_size, num_workers, worker_init_fn)``
@@ -575,15 +322,6 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
             rccl = False
         return self.plan.slots_per_worker(self._slot_capacity(), self.n_producers, deep=rccl)
 
-    def _lockstep_depth(self, transport) -> int:
-        """Tuning.lockstep_depth, or its auto value: an RCCL agreement takes ~60-180 µs to come back
-        while device-decoded steps take ~5 µs, so with the 64-deep ring the next one is issued 32
-        steps before the credits run out (profiles/r05_s24: the wait per step 0.4-0.7 µs at depth 2,
-        0.003 µs at 32); the host lockstep keeps 2."""
-        if self.lockstep_depth is not None:
-            return self.lockstep_depth
-        return 32 if transport == "rccl" and self.plan.device_decode else 2
-
     def _n_extras(self) -> int:
         """Record-field columns (Key / Timestamp) the schema adds beside the value."""
         return len(getattr(self.schema, "fields", ()) or ())
@@ -750,85 +488,6 @@ class DeviceLoader(LoaderBridges, LoaderCommits):
                 if self.commit_mode == "sync":
                     self._sync_commit_py()
             run.close()
-
-    def _lockstep_transport(self, process_group=None):
-        """How ranks agree on every step: 'rccl' (native communicator, an nccl process group or
-        lockstep='rccl'), 'host' (the process group's all-reduce), or None (no lockstep)."""
-        if not (self.lockstep and (self.world_size > 1 or self.lockstep == "always")):
-            return None
-        import torch.distributed as dist
-
-        if not (dist.is_available() and dist.is_initialized()):
-            return None
-        if self.device.type != "cuda" or not self.native:
-            return "host"
-        backend = dist.get_backend(process_group)
-        return "rccl" if self.lockstep == "rccl" or (backend == "nccl" and self.lockstep != "host") else "host"
-
-    def _make_rccl_lockstep(self, process_group):
-        """Native RCCL communicator for the per-step lockstep (id broadcast through torch.distributed)."""
-        import torch.distributed as dist
-
-        lib = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
-        rank = dist.get_rank(process_group)
-        world = dist.get_world_size(process_group)
-        uid = [hip().RcclLockstep.unique_id(lib) if rank == 0 else None]
-        src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
-        # the id travels over a CPU (gloo) group: broadcasting it over an nccl group would create
-        # torch's own RCCL communicator -- and its streams, which take hardware queues -- for one
-        # 128-byte message
-        via_group = process_group
-        if dist.get_backend(process_group) != "gloo":
-            ranks = None if process_group is None else dist.get_process_group_ranks(process_group)
-            via_group = dist.new_group(ranks=ranks, backend="gloo")  # collective: every rank gets here
-        dist.broadcast_object_list(uid, src=src, group=via_group, device=torch.device("cpu"))
-        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
-        ls = hip().RcclLockstep(lib, uid[0], rank, world, dev, self._lockstep_depth("rccl") + 2)
-        ls.set_timeout_ms(int(self.lockstep_timeout * 1000))
-        # start-up proof that the communicator spans the whole job: RCCL's own count of its ranks,
-        # and one all-reduce of the rank ids over it
-        nranks = int(ls.nranks)
-        rank_sum = int(ls.allreduce_sum(rank))
-        if nranks != world or rank_sum != world * (world - 1) // 2:
-            raise RuntimeError(f"lockstep: RCCL communicator has {nranks} ranks (rank-id sum {rank_sum}), "
-                               f"the process group {world}")
-        self.lockstep_info = {"transport": "rccl", "rccl_nranks": nranks, "rank_id_sum": rank_sum,
-                              "world_size": world, "words": ls.words_mode,
-                              "stream": ("greatest priority: a hardware-queue pool of its own" if ls.high_priority
-                                         else "normal priority (shares the process's queues)")}
-        return ls
-
-    def stream_plan(self) -> dict:
-        """The HIP streams the live iteration uses, against the process's hardware queues
-        (``GPU_MAX_HW_QUEUES``, 4 by default).  HIP binds streams to queues round-robin in creation
-        order, so past that count two streams share a queue and a launch on one can wait behind
-        the other's (e.g. a decode kernel behind a collective waiting for the other ranks)."""
-        run = self._run
-        plan = {"user": 1, "decode": 0, "copy": 0, "mirror_copy": 0, "rccl_lockstep": 0, "torch_nccl": 0}
-        if run is not None and run.engine is not None:
-            plan["decode"] = int(run.engine.decode_streams()) if self.plan.device_decode else 0
-            plan["copy"] = int(run.engine.copy_streams())
-            if run.driver is not None:
-                plan["mirror_copy"] = int(run.driver.mirror_copy_streams)
-        if run is not None and run.rccl is not None and self.lockstep_info.get("transport") == "rccl":
-            # a greatest-priority stream takes a queue from the high-priority pool, not these
-            plan["rccl_lockstep"] = 0 if getattr(run.rccl, "high_priority", False) else 1
-            plan["rccl_lockstep_high_priority"] = 1 - plan["rccl_lockstep"]
-        try:
-            import torch.distributed as dist
-
-            # torch makes its RCCL communicator (and streams) at a group's first collective: the
-            # lockstep never runs one on it, a DDP job's gradient all-reduce does (world > 1, or a
-            # world-1 group that ran one: bench.py's rehearsal of the N = 8 queue layout)
-            if (dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"
-                    and (dist.get_world_size() > 1 or os.environ.get("TORCHKAFKA_TORCH_NCCL_ACTIVE") == "1")):
-                plan["torch_nccl"] = 1
-        except Exception:  # noqa: BLE001
-            pass
-        total = sum(v for k, v in plan.items() if k != "rccl_lockstep_high_priority")
-        hw = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
-        plan.update(total=total, hw_queues=hw, shared=total > hw)
-        return plan
 
     # ------------------------------------------------------------------ native iteration
     def _iterate_native(self, run: _Run, auto_commit: bool):

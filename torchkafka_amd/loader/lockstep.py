@@ -1,0 +1,124 @@
+"""DeviceLoader's cross-rank lockstep: which transport agrees on every step, the native RCCL
+communicator, and the stream plan against the process's hardware queues.
+
+The reference commits per batch with no agreement between ranks (/root/reference/src/
+auto_commit.py:55-58); here every rank's step k is agreed before it is delivered and committed
+(``csrc/core/lockstep.h``), over RCCL on GPUs or the process group's all-reduce otherwise.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from ..ops.native import hip
+
+
+def _host_allreduce_min(group):
+    """all-reduce(MIN) of the lockstep's four int64 words (credit, step, -step, commit status) over a
+    CPU (gloo) group, for the driver's PyLockstep transport."""
+    import torch.distributed as dist
+
+    if dist.get_backend(group) != "gloo":
+        group = dist.new_group(backend="gloo")  # collective: every rank builds its loader iterator
+    buf = torch.zeros(4, dtype=torch.int64)
+
+    def allreduce_min(a: int, b: int, c: int, d: int):
+        buf[0], buf[1], buf[2], buf[3] = a, b, c, d
+        dist.all_reduce(buf, op=dist.ReduceOp.MIN, group=group)
+        return int(buf[0]), int(buf[1]), int(buf[2]), int(buf[3])
+
+    return allreduce_min
+
+
+class LoaderLockstep:
+    """Mixin of :class:`~torchkafka_amd.loader.DeviceLoader`: ``lockstep``, ``lockstep_depth``,
+    ``lockstep_timeout``, ``world_size``, ``device``, ``native``, ``plan``, the live ``_run``."""
+
+    def _lockstep_depth(self, transport) -> int:
+        """Tuning.lockstep_depth, or its auto value: an RCCL agreement takes ~60-180 µs to come back
+        while device-decoded steps take ~5 µs, so with the 64-deep ring the next one is issued 32
+        steps before the credits run out (profiles/r05_s24: the wait per step 0.4-0.7 µs at depth 2,
+        0.003 µs at 32); the host lockstep keeps 2."""
+        if self.lockstep_depth is not None:
+            return self.lockstep_depth
+        return 32 if transport == "rccl" and self.plan.device_decode else 2
+
+    def _lockstep_transport(self, process_group=None):
+        """How ranks agree on every step: 'rccl' (native communicator, an nccl process group or
+        lockstep='rccl'), 'host' (the process group's all-reduce), or None (no lockstep)."""
+        if not (self.lockstep and (self.world_size > 1 or self.lockstep == "always")):
+            return None
+        import torch.distributed as dist
+
+        if not (dist.is_available() and dist.is_initialized()):
+            return None
+        if self.device.type != "cuda" or not self.native:
+            return "host"
+        backend = dist.get_backend(process_group)
+        return "rccl" if self.lockstep == "rccl" or (backend == "nccl" and self.lockstep != "host") else "host"
+
+    def _make_rccl_lockstep(self, process_group):
+        """Native RCCL communicator for the per-step lockstep (id broadcast through torch.distributed)."""
+        import torch.distributed as dist
+
+        lib = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+        rank = dist.get_rank(process_group)
+        world = dist.get_world_size(process_group)
+        uid = [hip().RcclLockstep.unique_id(lib) if rank == 0 else None]
+        src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
+        # the id travels over a CPU (gloo) group: broadcasting it over an nccl group would create
+        # torch's own RCCL communicator -- and its streams, which take hardware queues -- for one
+        # 128-byte message
+        via_group = process_group
+        if dist.get_backend(process_group) != "gloo":
+            ranks = None if process_group is None else dist.get_process_group_ranks(process_group)
+            via_group = dist.new_group(ranks=ranks, backend="gloo")  # collective: every rank gets here
+        dist.broadcast_object_list(uid, src=src, group=via_group, device=torch.device("cpu"))
+        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        ls = hip().RcclLockstep(lib, uid[0], rank, world, dev, self._lockstep_depth("rccl") + 2)
+        ls.set_timeout_ms(int(self.lockstep_timeout * 1000))
+        # start-up proof that the communicator spans the whole job: RCCL's own count of its ranks,
+        # and one all-reduce of the rank ids over it
+        nranks = int(ls.nranks)
+        rank_sum = int(ls.allreduce_sum(rank))
+        if nranks != world or rank_sum != world * (world - 1) // 2:
+            raise RuntimeError(f"lockstep: RCCL communicator has {nranks} ranks (rank-id sum {rank_sum}), "
+                               f"the process group {world}")
+        self.lockstep_info = {"transport": "rccl", "rccl_nranks": nranks, "rank_id_sum": rank_sum,
+                              "world_size": world, "words": ls.words_mode,
+                              "stream": ("greatest priority: a hardware-queue pool of its own" if ls.high_priority
+                                         else "normal priority (shares the process's queues)")}
+        return ls
+
+    def stream_plan(self) -> dict:
+        """The HIP streams the live iteration uses, against the process's hardware queues
+        (``GPU_MAX_HW_QUEUES``, 4 by default).  HIP binds streams to queues round-robin in creation
+        order, so past that count two streams share a queue and a launch on one can wait behind
+        the other's (e.g. a decode kernel behind a collective waiting for the other ranks)."""
+        run = self._run
+        plan = {"user": 1, "decode": 0, "copy": 0, "mirror_copy": 0, "rccl_lockstep": 0, "torch_nccl": 0}
+        if run is not None and run.engine is not None:
+            plan["decode"] = int(run.engine.decode_streams()) if self.plan.device_decode else 0
+            plan["copy"] = int(run.engine.copy_streams())
+            if run.driver is not None:
+                plan["mirror_copy"] = int(run.driver.mirror_copy_streams)
+        if run is not None and run.rccl is not None and self.lockstep_info.get("transport") == "rccl":
+            # a greatest-priority stream takes a queue from the high-priority pool, not these
+            plan["rccl_lockstep"] = 0 if getattr(run.rccl, "high_priority", False) else 1
+            plan["rccl_lockstep_high_priority"] = 1 - plan["rccl_lockstep"]
+        try:
+            import torch.distributed as dist
+
+            # torch makes its RCCL communicator (and streams) at a group's first collective: the
+            # lockstep never runs one on it, a DDP job's gradient all-reduce does (world > 1, or a
+            # world-1 group that ran one: bench.py's rehearsal of the N = 8 queue layout)
+            if (dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"
+                    and (dist.get_world_size() > 1 or os.environ.get("TORCHKAFKA_TORCH_NCCL_ACTIVE") == "1")):
+                plan["torch_nccl"] = 1
+        except Exception:  # noqa: BLE001
+            pass
+        total = sum(v for k, v in plan.items() if k != "rccl_lockstep_high_priority")
+        hw = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+        plan.update(total=total, hw_queues=hw, shared=total > hw)
+        return plan

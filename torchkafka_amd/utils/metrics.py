@@ -61,6 +61,7 @@ class LoaderStats:
     mirror_pending_fallbacks: int = 0  # mirror segments read from the pinned log: their copy was in flight
     mirror_bytes: int = 0     # h2d="dma" device decode: log bytes copied into the HBM mirror (SDMA)
     mirror_copies: int = 0
+    split_launches: int = 0    # decode launches with each segment split over workgroups (HBM)
     mirror_fallbacks: int = 0  # segments read from the pinned log instead (buffer busy)
     lockstep_agreements: int = 0      # cross-rank agreements (collectives) issued
     lockstep_wait_ns: int = 0         # host time waiting for agreement results
@@ -128,6 +129,7 @@ class LoaderStats:
             "log_pin_wait_ms": self.log_register_wait_ns / 1e6,
             "mirror_mib_copied": self.mirror_bytes / 2**20,
             "mirror_copies": self.mirror_copies,
+            "split_launches": self.split_launches,
             "mirror_fallbacks": self.mirror_fallbacks,
             "mirror_pending_fallbacks": self.mirror_pending_fallbacks,
             "lockstep_agreements": self.lockstep_agreements,
