@@ -3,8 +3,8 @@
 A launch whose segments are all read from the HBM mirror gives each segment P workgroups, each
 streaming windows [q*nw/P, (q+1)*nw/P) of it; each part shifts its CRC32C to the segment's end and
 XORs it into an accumulator set of the launch, and the last part to arrive gives the verdict
-(TORCHKAFKA_SPAN_PARTS, default 4 for fixed-width / var-len, JSON with the variable set).  Run
-under P = 1, 2 and 4: values bit-exact with the host path through the mirror (rows cut by part
+(TORCHKAFKA_SPAN_PARTS, default 8 for fixed-width / var-len, JSON with the variable set).  Run
+under P = 1, 2, 4 and 8: values bit-exact with the host path through the mirror (rows cut by part
 boundaries, parts with no window, RecordBatches chained over segments), a flipped byte caught in
 every part's range with the batches before it committed, and the split actually in effect.
 The CPU side of the combination is tests/test_span_decode.py (crc32c_span_emulate)."""
@@ -16,7 +16,7 @@ import test_gpu_span as base
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[1, 2, 4])
+@pytest.fixture(params=[1, 2, 4, 8])
 def parts(request, monkeypatch):
     monkeypatch.setenv("TORCHKAFKA_SPAN_PARTS", str(request.param))
     return request.param

@@ -33,11 +33,11 @@ def test_lane_tree_crc_matches_crc32c(n):
     assert raw ^ 0xFFFFFFFF == _crc32c_ref(buf[21:c1])
 
 
-@pytest.mark.parametrize("parts", [2, 3, 4])
+@pytest.mark.parametrize("parts", [2, 3, 4, 8])
 @pytest.mark.parametrize("n", [61, 10_300, 20_500, 66_000, 131_072 + 21])
 def test_segment_parts_combine_to_the_segment_crc(n, parts):
     """SpanLaunch::parts: P workgroups each fold a contiguous run of the segment's windows from a
-    zero state, shift their merged CRC to the segment's end by whole windows (kSpanTabWinShift) and
+    zero state, move every lane to the segment's end (lane constants, kSpanTabLaneMul) and
     xor it in (span_device.h crc_finish) -- the same raw CRC as one workgroup.  Parts with no window
     (segments shorter than P windows) contribute zero."""
     c = core()

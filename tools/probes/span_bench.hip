@@ -37,6 +37,8 @@
     }                                                                                      \
   } while (0)
 
+__global__ void empty_kernel() {}
+
 static uint16_t bf16_rne(float f) {
   uint32_t u;
   std::memcpy(&u, &f, 4);
@@ -229,6 +231,29 @@ int main(int argc, char** argv) {
     std::printf(", \"partials\": {\"segments\": %d, \"mismatches\": %lld, \"verdict\": %d}", segs,
                 static_cast<long long>(bad_partials), *err);
   }
-  std::printf("}\n");
+  // where a lone group's time goes: an empty kernel's lone time (launch + completion), and the
+  // HBM group with no CRC (values only: no lane merge, no part accumulation, no verdict)
+  auto lone = [&](auto&& launch) {
+    std::vector<float> v;
+    for (int i = 0; i < reps; ++i) {
+      CK(hipEventRecord(e0, st[0]));
+      launch();
+      CK(hipEventRecord(e1, st[0]));
+      CK(hipEventSynchronize(e1));
+      float t = 0;
+      CK(hipEventElapsedTime(&t, e0, e1));
+      v.push_back(t);
+    }
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2] * 1e3;
+  };
+  const double empty_us = lone([&] { hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, st[0]); });
+  const double empty_wide_us =
+      lone([&] { hipLaunchKernelGGL(empty_kernel, dim3(segs * parts), dim3(576), 0, st[0]); });
+  tkh::SpanLaunch nc = make(dlog, 0);
+  for (int s = 0; s < segs; ++s) nc.s[s].flags = 0;
+  const double nocrc_us = lone([&] { tkh::launch_span_decode(nc, tkh::kF32, tkh::kBF16, nullptr, nullptr, st[0]); });
+  std::printf(", \"empty_lone_us_p50\": %.1f, \"empty_grid_lone_us_p50\": %.1f, \"hbm_nocrc_lone_us_p50\": %.1f}\n",
+              empty_us, empty_wide_us, nocrc_us);
   return 0;
 }

@@ -54,7 +54,7 @@ PROCESS_ENV = {
                                 "the whole device) instead of on the deferred-release thread (csrc/hip/reaper.h)",
     "TORCHKAFKA_LOCKSTEP_TRACE": "1: the RCCL lockstep keeps host timestamps of every agreement "
                                  "(RcclLockstep.take_trace)",
-    "TORCHKAFKA_SPAN_PARTS": "1 / 2 / 4 (default 4): workgroups per log segment in a device-decode launch whose "
+    "TORCHKAFKA_SPAN_PARTS": "1 / 2 / 4 / 8 (default 8): workgroups per log segment in a device-decode launch whose "
                              "segments are all read from the HBM mirror (JSON: 1 unless set)",
     "TORCHKAFKA_LZ4_LIB": "0: decode LZ4 blocks with the built-in decoder instead of the system liblz4.so.1",
     "TORCHKAFKA_DECODE_PRIORITY": "high / normal (default) / low: HIP stream priority of the decode streams "

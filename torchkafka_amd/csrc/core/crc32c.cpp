@@ -312,21 +312,13 @@ void crc32c_span_tables(uint32_t* out) {
       out[kSpanTabNib + (2 * k) * 16 + n] = T.t[k][n];
       out[kSpanTabNib + (2 * k + 1) * 16 + n] = T.t[k][n << 4];
     }
-  for (uint32_t j = 0; j < kSpanLevels; ++j) {
-    const uint32_t op = T.x2nmodp(uint64_t(kSpanPiece) << j, 3);  // x^(8 * P * 2^j)
-    for (int k = 0; k < 4; ++k)
-      for (uint32_t b = 0; b < 256; ++b)
-        out[kSpanTabShift + (j * 4 + uint32_t(k)) * 256 + b] = Tables::multmodp(op, b << (8 * k));
-  }
   const uint32_t gap = T.x2nmodp(uint64_t(kSpanWin - kSpanPiece), 3);
   for (uint32_t i = 0; i < 8; ++i)
     for (uint32_t n = 0; n < 16; ++n) out[kSpanTabGap + i * 16 + n] = Tables::multmodp(gap, n << (4 * i));
-  for (uint32_t j = 0; j < kSpanWinLevels; ++j) {
-    const uint32_t op = T.x2nmodp(uint64_t(kSpanWin) << j, 3);  // x^(8 * W * 2^j)
-    for (int k = 0; k < 4; ++k)
-      for (uint32_t b = 0; b < 256; ++b)
-        out[kSpanTabWinShift + (j * 4 + uint32_t(k)) * 256 + b] = Tables::multmodp(op, b << (8 * k));
-  }
+  for (uint32_t m = 0; m < 32; ++m)
+    for (uint32_t t = 0; t < kSpanLanes; ++t)
+      out[kSpanTabLaneMul + m * kSpanLanes + t] =
+          T.x2nmodp(uint64_t(kSpanPiece) * (kSpanLanes - 1 - t) + uint64_t(kSpanWin) * m, 3);
 }
 
 uint32_t crc32c_span_emulate(const uint8_t* buf, uint32_t c0, uint32_t c1, bool first, int parts) {
@@ -335,11 +327,11 @@ uint32_t crc32c_span_emulate(const uint8_t* buf, uint32_t c0, uint32_t c1, bool 
   // window gap operator between windows), looked up in the same nibble rows; a slice-by-4 step for
   // a piece's first 4 bytes then slice-by-8 steps; bytes below c0 masked to zero (8-byte groups
   // wholly below c0 skipped); the first 4 CRC'd bytes of a RecordBatch xor 0xFF (the 0xFFFFFFFF
-  // initial value); then the 8-level shift tree.  The range is the segment [0, c1) with c0 < 22.
+  // initial value); then every lane's state times its lane constant, xored.  The range is the
+  // segment [0, c1) with c0 < 22.
   static uint32_t tab[kSpanTabWords];
   static const bool init = (crc32c_span_tables(tab), true);
   (void)init;
-  const uint32_t* S0 = tab + kSpanTabShift;
   auto byte_at = [&](int64_t ab) -> uint32_t {
     uint32_t b = ab >= int64_t(c0) ? buf[ab] : 0u;
     if (first && ab >= int64_t(c0) && ab < int64_t(c0) + 4) b ^= 0xFFu;
@@ -367,11 +359,8 @@ uint32_t crc32c_span_emulate(const uint8_t* buf, uint32_t c0, uint32_t c1, bool 
   };
   const int64_t nw = int64_t(span_windows(c1));
   const int64_t w0 = int64_t(c1) - nw * int64_t(kSpanWin);
-  auto shift = [&](const uint32_t* S, uint32_t c) {
-    return S[c & 255] ^ S[256 + ((c >> 8) & 255)] ^ S[512 + ((c >> 16) & 255)] ^ S[768 + (c >> 24)];
-  };
-  // segment parts (span_device.h crc_finish): each part's windows from a zero state, merged, moved
-  // to the segment's end by whole windows, xored
+  // segment parts (span_device.h crc_finish): each part's windows from a zero state, each lane moved
+  // to the segment's end (past the later lanes' pieces and the windows after the part's last), xored
   if (parts < 1) parts = 1;
   uint32_t total = 0;
   for (int q = 0; q < parts; ++q) {
@@ -391,14 +380,8 @@ uint32_t crc32c_span_emulate(const uint8_t* buf, uint32_t c0, uint32_t c1, bool 
       lane[t] = crc;
     }
   }
-  for (uint32_t j = 0; j < kSpanLevels; ++j) {
-    const uint32_t* S = S0 + j * 4 * 256;
-    for (uint32_t t = 0; t < kSpanLanes; t += 2u << j) lane[t] = shift(S, lane[t]) ^ lane[t + (1u << j)];
-  }
-  uint32_t c = lane[0];
-  for (uint32_t j = 0; j < kSpanWinLevels; ++j)
-    if (((nw - k1) >> j) & 1) c = shift(tab + kSpanTabWinShift + j * 4 * 256, c);
-  total ^= c;
+  const uint32_t* K = tab + kSpanTabLaneMul + uint32_t(nw - k1) * kSpanLanes;
+  for (uint32_t t = 0; t < kSpanLanes; ++t) total ^= Tables::multmodp(K[t], lane[t]);
   }
   return total;
 }

@@ -41,15 +41,15 @@ constexpr uint32_t kSpanMaxSegRows = 2048;
 // [w + t P, w + (t+1) P) into a running state -- one slice-by-4 step for the piece's first 4 bytes,
 // then slice-by-8 steps -- and between windows the state crosses the other lanes' bytes with one
 // "shift by kSpanWin - kSpanPiece zero bytes" operator (kSpanTabGap).  After the last window lane t
-// holds the CRC of its bytes followed by zeros up to the end of its last piece, and a
-// log2(kSpanLanes)-level tree merges neighbours with "shift by 2^j pieces" operators.  kSpanPiece is
+// holds the CRC of its bytes followed by zeros up to the end of its last piece; it is moved to the
+// end of the last window (and, for a segment part, on to the segment's end) by ONE multiplication
+// with a per-lane constant (kSpanTabLaneMul), and the lanes' products are xored.  kSpanPiece is
 // 20 bytes (5 dwords): an odd dword count puts the 32 lanes of a ds_read_b32 group on 32 different
 // LDS banks; 4 + 2 x 8 bytes per lane per window, 512 lanes (8 compute waves, two per SIMD: one
 // hides the other's LDS latency).  Host mirror: crc32c_span_emulate (csrc/core/crc32c.cpp).
 constexpr uint32_t kSpanPiece = 20;
 constexpr uint32_t kSpanLanes = 512;
 constexpr uint32_t kSpanWin = kSpanPiece * kSpanLanes;  // 10,240 bytes
-constexpr uint32_t kSpanLevels = 9;
 constexpr uint32_t kSpanMaxWins = (kSpanSegMax + kSpanWin - 1) / kSpanWin;
 static_assert(kSpanMaxWins <= 32, "window tables hold 32 entries");
 // Windows of a segment of `len` bytes (>= 1).
@@ -93,26 +93,24 @@ constexpr int32_t kSpanWinPad = 16;
 constexpr int32_t kSpanWinLoads = (int32_t(kSpanWin) + 96 + 1023) / 1024;
 constexpr int32_t kSpanWinBytes = kSpanWinPad + 1024 * kSpanWinLoads + 32;
 
-// Device table layout (uint32 words): slice-by-8 byte tables T0..T7; for level j and byte k of the
-// value, shift-by-(kSpanPiece << j)-bytes of (b << 8k); the nibble split of T0..T7 the kernels keep
+// Device table layout (uint32 words): slice-by-8 byte tables T0..T7; the nibble split of T0..T7 the kernels keep
 // in LDS: row 2k + h holds T_k[n << 4h] for n < 16 (a byte table is linear over GF(2), so
 // T_k[b] = row(2k)[b & 15] ^ row(2k + 1)[b >> 4]; a 16-entry row spans 16 LDS banks, so a
 // ds_read_b32 of one row by any 32 lanes is conflict-free); and the window gap operator, nibble
-// split too: row i holds shift-by-(kSpanWin - kSpanPiece)-bytes of (n << 4i).
+// split too: row i holds shift-by-(kSpanWin - kSpanPiece)-bytes of (n << 4i); then the lane
+// constants: entry m * kSpanLanes + t is x^(8 (kSpanPiece (kSpanLanes - 1 - t) + kSpanWin m)) mod P
+// in zlib's reflected representation -- multiplying a raw CRC state by x^(8n) advances it over n zero
+// bytes -- i.e. lane t's state moved past the later lanes' pieces of its last window and m whole
+// windows more (the windows after a segment part's last one, SpanLaunch::parts).
 constexpr uint32_t kSpanTabSlice = 0;
-constexpr uint32_t kSpanTabShift = 8 * 256;
-constexpr uint32_t kSpanTabShiftSet = kSpanLevels * 4 * 256;
-constexpr uint32_t kSpanTabNib = kSpanTabShift + kSpanTabShiftSet;
+constexpr uint32_t kSpanTabNib = 8 * 256;
 constexpr uint32_t kSpanTabNibWords = 16 * 16;
 constexpr uint32_t kSpanTabGap = kSpanTabNib + kSpanTabNibWords;
 constexpr uint32_t kSpanTabGapWords = 8 * 16;
-// Segment parts (SpanLaunch::parts): for level j and byte k, shift-by-(kSpanWin << j)-bytes of
-// (b << 8k) -- a part's CRC moved from the end of its last window to the segment's end.
-constexpr uint32_t kSpanWinLevels = 5;  // up to 31 windows: kSpanMaxWins <= 32
-constexpr uint32_t kSpanTabWinShift = kSpanTabGap + kSpanTabGapWords;
-constexpr uint32_t kSpanTabWords = kSpanTabWinShift + kSpanWinLevels * 4 * 256;
-// Workgroups one segment may be split over (SpanLaunch::parts: 1, 2 or 4).
-constexpr int kSpanMaxParts = 4;
+constexpr uint32_t kSpanTabLaneMul = kSpanTabGap + kSpanTabGapWords;
+constexpr uint32_t kSpanTabWords = kSpanTabLaneMul + 32 * kSpanLanes;
+// Workgroups one segment may be split over (SpanLaunch::parts: 1, 2, 4 or 8).
+constexpr int kSpanMaxParts = 8;
 // Windows [k0, k1) of part q of P over a segment of nw windows.
 inline constexpr int32_t span_part_k0(int32_t q, int32_t P, int32_t nw) { return q * nw / P; }
 

@@ -92,7 +92,7 @@ class Engine {
   }
   // Device copy of the CRC tables of the span kernel (uploaded on first use).
   const uint32_t* span_tables();
-  // Workgroups per span segment (TORCHKAFKA_SPAN_PARTS: 1, 2 or 4; span_device.h Part) and the
+  // Workgroups per span segment (TORCHKAFKA_SPAN_PARTS: 1, 2, 4 or 8; span_device.h Part) and the
   // accumulator words the parts of the next launch on `stream` meet in: zeroed once, left zero by
   // every launch, and handed out in rotation over kPartAccSets sets per stream -- the dispatches of
   // one stream may overlap (a launch's first workgroups start before the previous launch's last
@@ -159,7 +159,7 @@ class Engine {
   uint8_t* host_dev_ = nullptr;           // device view of the registered host region (zero-copy)
   size_t host_len_ = 0;
   uint32_t* span_tabs_ = nullptr;
-  int span_parts_ = 4;  // HBM-sourced fixed-width / var-len launches (profiles/r05_s20_s22_parts)
+  int span_parts_ = 8;  // HBM-sourced fixed-width / var-len launches (profiles/r05_s30_lane_merge)
   int json_parts_ = 1;
   struct PartAcc {
     hipStream_t stream;

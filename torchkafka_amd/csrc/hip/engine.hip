@@ -43,7 +43,7 @@ Engine::Engine(int device, int n_slots, size_t staging_bytes, int n_streams, int
     : device_(device), n_slots_(n_slots), mode_(mode), q_(std::make_unique<HipQueue>(device)) {
   if (const char* e = std::getenv("TORCHKAFKA_SPAN_PARTS")) {
     const int p = std::atoi(e);
-    span_parts_ = p == 2 || p == tk::kSpanMaxParts ? p : 1;
+    span_parts_ = p == 2 || p == 4 || p == tk::kSpanMaxParts ? p : 1;
   }
   json_parts_ = std::getenv("TORCHKAFKA_SPAN_PARTS") ? span_parts_ : 1;
   if (n_slots <= 0) throw std::invalid_argument("engine: n_slots must be positive");

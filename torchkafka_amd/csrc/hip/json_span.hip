@@ -254,10 +254,10 @@ __global__ __launch_bounds__(kBlock) void json_stage_kernel(JsonStageLaunch a) {
       });
 
   if (do_crc) {
-    if (t < kThreads) span::crc_merge(a.tabs, crc, wcrc);
+    if (t < kThreads) span::crc_merge(crc, wcrc);
     __syncthreads();
     if (t == 0)
-      span::crc_finish(a.tabs, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials, P, W.nw - pt.k1,
+      span::crc_finish(wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials, P, pt.q,
                        a.part_acc + 2 * pt.seg);
   }
   if (t == 0 && bad) *bo.err = int32_t(sg.seg);  // never committed (reported as this segment)

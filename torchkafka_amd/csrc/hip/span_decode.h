@@ -46,7 +46,7 @@ struct SpanLaunch {
   int vec_store;             // every batch's rows start 16-byte aligned for vector stores
   int64_t row_elems;
   const uint32_t* tabs;      // device CRC tables (tk::kSpanTabWords)
-  int parts;                 // workgroups per segment (1, 2, 4; span_device.h Part): grid n_seg * parts
+  int parts;                 // workgroups per segment (1, 2, 4, 8; span_device.h Part): grid n_seg * parts
   uint32_t* part_acc;        // parts > 1: [kMaxLaunchSegs][2] zeroed device words of this launch's stream
   SpanBatchOut b[kMaxGroup];
   SpanDevSeg s[kMaxLaunchSegs];
@@ -118,7 +118,7 @@ void prewarm_span_kernels(int device);
 void launch_span_decode(const SpanLaunch& a, int src_dt, int dst_dt, const float* shift, const float* scale,
                         hipStream_t stream);
 
-// Validates SpanLaunch::parts (1, 2, 4; accumulator words needed past 1); returns it (0 -> 1).
+// Validates SpanLaunch::parts (1, 2, 4, 8; accumulator words needed past 1); returns it (0 -> 1).
 int check_parts(int parts, const uint32_t* acc, const char* what);
 
 }  // namespace tkh

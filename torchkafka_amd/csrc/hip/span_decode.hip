@@ -172,10 +172,10 @@ __global__ __launch_bounds__(kBlock) void span_decode_kernel(SpanLaunch a, const
 
   // ---- verdict: merge the lanes; thread 0 compares (or leaves the partial for the driver)
   if (do_crc) {
-    if (t < kThreads) span::crc_merge(a.tabs, crc, wcrc);
+    if (t < kThreads) span::crc_merge(crc, wcrc);
     __syncthreads();
     if (t == 0)
-      span::crc_finish(a.tabs, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials, P, W.nw - pt.k1,
+      span::crc_finish(wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials, P, pt.q,
                        a.part_acc + 2 * pt.seg);
   }
 }
@@ -312,10 +312,10 @@ __global__ __launch_bounds__(kBlock) void varlen_span_kernel(VarSpanLaunch a, D 
       });
 
   if (do_crc) {
-    if (t < kThreads) span::crc_merge(a.tabs, crc, wcrc);
+    if (t < kThreads) span::crc_merge(crc, wcrc);
     __syncthreads();
     if (t == 0)
-      span::crc_finish(a.tabs, wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials, P, W.nw - pt.k1,
+      span::crc_finish(wcrc, flags, sg.crc, sg.seg, bo.err, bo.partials, P, pt.q,
                        a.part_acc + 2 * pt.seg);
   }
   if (t == 0 && bad) *bo.err = int32_t(sg.seg);
@@ -342,8 +342,8 @@ void launch_span_t(const SpanLaunch& a, const float* shift, const float* scale, 
 
 int check_parts(int parts, const uint32_t* acc, const char* what) {
   if (parts <= 1) return 1;
-  if ((parts != 2 && parts != tk::kSpanMaxParts) || acc == nullptr)
-    throw std::invalid_argument(std::string(what) + ": parts must be 1, 2 or 4 (with accumulator words)");
+  if ((parts != 2 && parts != 4 && parts != tk::kSpanMaxParts) || acc == nullptr)
+    throw std::invalid_argument(std::string(what) + ": parts must be 1, 2, 4 or 8 (with accumulator words)");
   return parts;
 }
 

@@ -17,8 +17,9 @@
 //     * CRC32C: lane t folds its 20-byte piece of the window into a running state (slice-by-8 fed by
 //       a sliding dword window, looked up per NIBBLE in 16-entry LDS rows: conflict-free), the state
 //       crossing the other lanes' bytes with one gap operator between windows; after the last
-//       window 6 shuffle levels and 3 LDS levels of "shift by 2^j pieces" merge the lanes
-//       (span.h, host mirror csrc/core/crc32c.cpp crc32c_span_emulate).
+//       window each lane's state is multiplied by its lane constant (span.h kSpanTabLaneMul: the
+//       shift over the later lanes' bytes, loaded before the first window) and the products are
+//       xored over the wave and the 8 waves (span.h, host mirror crc32c.cpp crc32c_span_emulate).
 //   A workgroup needs 39-47 KiB of LDS (round 4: the whole 143 KiB segment) and its loads are always
 //   NB - 1 windows ahead of its compute, so it holds a CU for a fraction of the time it used to.
 //
@@ -110,9 +111,18 @@ __device__ __forceinline__ uint32_t keep_from(int32_t a, int32_t c) {
   return d <= 0 ? 0xFFFFFFFFu : d >= 4 ? 0u : (0xFFFFFFFFu << (8 * d));
 }
 
-__device__ __forceinline__ uint32_t shift_op(const uint32_t* __restrict__ set, uint32_t level, uint32_t c) {
-  const uint32_t* S = set + level * 1024u;
-  return S[c & 255u] ^ S[256u + ((c >> 8) & 255u)] ^ S[512u + ((c >> 16) & 255u)] ^ S[768u + (c >> 24)];
+// c times the constant k modulo the CRC32C polynomial, both in zlib's reflected representation
+// (crc32c.cpp Tables::multmodp), branch-free: 32 steps of a bit-field extract, a masked xor and a
+// multiply-by-x -- about 220 VALU instructions and no memory access, where the shift-table tree it
+// replaces waited for 9 dependent global table reads after the last window (profiles/r05_s29).
+__device__ __forceinline__ uint32_t gf_mul(uint32_t k, uint32_t c) {
+  uint32_t p = 0;
+#pragma unroll
+  for (int i = 31; i >= 0; --i) {
+    p ^= c & uint32_t(int32_t(k << (31 - i)) >> 31);
+    c = (c >> 1) ^ (0x82F63B78u & uint32_t(int32_t(c << 31) >> 31));
+  }
+  return p;
 }
 
 using Windows = tk::SpanWindows;  // span.h
@@ -299,27 +309,23 @@ __device__ __forceinline__ uint32_t crc_piece(const uint32_t* __restrict__ b32, 
   return crc;
 }
 
-// After the last window (every thread): 6 shuffle levels merge each wave's 64 lane states; lane 0
-// leaves the wave's CRC in wcrc[wave].  Returns the shift-table set (for crc_verdict).
-__device__ __forceinline__ const uint32_t* crc_merge(const uint32_t* __restrict__ tabs, uint32_t crc, uint32_t* wcrc) {
-  const uint32_t* shift_set = tabs + tk::kSpanTabShift;
+// After the last window (compute threads, `crc` as pipeline() returns it: already moved to the
+// segment part's end): the xor of the wave's 64 lane states; lane 0 leaves it in wcrc[wave].
+__device__ __forceinline__ void crc_merge(uint32_t crc, uint32_t* wcrc) {
   const int t = int(threadIdx.x), lane = t & 63;
 #pragma unroll
-  for (uint32_t j = 0; j < 6; ++j) {
-    const uint32_t other = __shfl_down(crc, 1u << j, 64);
-    if ((lane & ((2 << j) - 1)) == 0) crc = shift_op(shift_set, j, crc) ^ other;
-  }
+  for (int j = 32; j >= 1; j >>= 1) crc ^= uint32_t(__shfl_xor(int(crc), j, 64));
   if (lane == 0) wcrc[t >> 6] = crc;
-  return shift_set;
 }
 
 // Segment parts (SpanLaunch::parts = P > 1): P workgroups share one segment, part q taking windows
 // [span_part_k0(q), span_part_k0(q + 1)) -- P times the loads in flight for a lone segment.  Each
 // part folds its windows' CRC pieces from a zero state (the gap operator of a zero state is zero),
-// merges its lanes, moves the result from the end of its last window to the segment's end
-// (kSpanTabWinShift, whole windows of zeros) and xors it into the segment's accumulator word; the
-// last part to arrive (an agent-scope counter beside it) takes the sum, gives the verdict and
-// leaves both words zero for the next launch on its stream.  Host mirror: crc32c_span_emulate.
+// its lane constants also carry the whole windows after its last one (so its merged CRC sits at the
+// segment's end), and it xors that CRC and its own bit into the segment's 64-bit accumulator with
+// ONE returning agent-scope atomic: the part whose returned bits complete the set takes the sum,
+// gives the verdict and zeroes the word for the next launch on its stream.  Host mirror:
+// crc32c_span_emulate.
 struct Part {
   int32_t seg, q, k0, k1;
 };
@@ -328,27 +334,21 @@ __device__ __forceinline__ Part part_of(int parts, int32_t nw) {
   return Part{seg, q, tk::span_part_k0(q, parts, nw), tk::span_part_k0(q + 1, parts, nw)};
 }
 
-// Thread 0 only, after a barrier that follows crc_merge: 3 levels merge the 8 wave CRCs; with
-// parts, the accumulation above; then the verdict (a RecordBatch held whole) or the raw partial.
-__device__ __forceinline__ void crc_finish(const uint32_t* __restrict__ tabs, const uint32_t* wcrc, uint32_t flags,
-                                           uint32_t want, uint32_t seg, int32_t* err, uint32_t* partials,
-                                           int parts, int32_t wins_after, uint32_t* acc) {
-  const uint32_t* shift_set = tabs + tk::kSpanTabShift;
-  uint32_t c4[4];
+// Thread 0 only, after a barrier that follows crc_merge: the xor of the 8 wave CRCs; with parts,
+// the accumulation above (`acc`: the segment's two words, 8-byte aligned); then the verdict (a
+// RecordBatch held whole) or the raw partial.
+__device__ __forceinline__ void crc_finish(const uint32_t* wcrc, uint32_t flags, uint32_t want, uint32_t seg,
+                                           int32_t* err, uint32_t* partials, int parts, int q, uint32_t* acc) {
+  uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) c4[i] = shift_op(shift_set, 6, wcrc[2 * i]) ^ wcrc[2 * i + 1];
-  const uint32_t lo = shift_op(shift_set, 7, c4[0]) ^ c4[1], hi = shift_op(shift_set, 7, c4[2]) ^ c4[3];
-  uint32_t c = shift_op(shift_set, 8, lo) ^ hi;
+  for (int i = 0; i < kThreads / 64; ++i) c ^= wcrc[i];
   if (parts > 1) {
-#pragma unroll
-    for (uint32_t j = 0; j < tk::kSpanWinLevels; ++j)
-      if ((wins_after >> j) & 1) c = shift_op(tabs + tk::kSpanTabWinShift, j, c);
-    atomicXor(acc, c);
-    __threadfence();
-    if (atomicAdd(acc + 1, 1u) != uint32_t(parts - 1)) return;  // another part gives the verdict
-    __threadfence();
-    c = atomicExch(acc, 0u);
-    atomicExch(acc + 1, 0u);
+    auto* word = reinterpret_cast<unsigned long long*>(acc);
+    const uint32_t bit = 1u << q;
+    const unsigned long long old = atomicXor(word, (static_cast<unsigned long long>(bit) << 32) | c);
+    if ((uint32_t(old >> 32) | bit) != (1u << parts) - 1u) return;  // another part gives the verdict
+    c ^= uint32_t(old);
+    *word = 0ull;  // every part of this launch has arrived: zero for the next one on this stream
   }
   constexpr uint32_t kWhole = tk::kSegCrcFirst | tk::kSegCrcLast;
   if ((flags & kWhole) == kWhole) {
@@ -368,7 +368,8 @@ __device__ __forceinline__ void crc_finish(const uint32_t* __restrict__ tabs, co
 //           the buffer window k - 1 used;
 //   compute: barrier -- `body(k, buf, off)` (the window's values; off = LDS byte of image byte 0) --
 //           its CRC pieces.
-// Returns the lane's CRC state (0 when the segment carries no CRC, and on the loader wave).
+// Returns the lane's CRC state moved to the segment's end (lane constant, span.h kSpanTabLaneMul: its
+// load is issued before the windows), or 0 when the segment carries no CRC, and on the loader wave.
 template <int NB, class Setup, class Prepare, class Body>
 __device__ __forceinline__ uint32_t pipeline(const uint8_t* src, const Windows& W, int32_t k0, int32_t k1,
                                              uint8_t (*bufs)[kWinBytes], uint32_t* tab,
@@ -387,6 +388,8 @@ __device__ __forceinline__ uint32_t pipeline(const uint8_t* src, const Windows& 
   prepare();
   __syncthreads();  // (drains the loader's first windows: they were needed first anyway)
   const uint32_t nbase = uint32_t(uintptr_t((lds_u32*)tab));  // the LDS byte address
+  const uint32_t lane_k =
+      do_crc && !loader ? tabs[tk::kSpanTabLaneMul + uint32_t(W.nw - k1) * tk::kSpanLanes + threadIdx.x] : 0u;
   uint32_t crc = 0;
   for (int k = k0; k < k1; ++k) {
     const int j = k - k0;
@@ -407,7 +410,7 @@ __device__ __forceinline__ uint32_t pipeline(const uint8_t* src, const Windows& 
 #endif
     }
   }
-  return crc;
+  return do_crc && !loader ? gf_mul(lane_k, crc) : 0u;
 }
 
 }  // namespace span
