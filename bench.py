@@ -387,6 +387,10 @@ def steady_block(R: Rank, res: dict, steps: int, dim: int) -> dict:
         "worker_fill_us_per_batch": round(st.get("worker_fill_us_per_batch", 0.0), 2),
         "verify_wait_us_per_batch": round(st.get("verify_wait_us_per_batch", 0.0), 3),
     }
+    if st.get("mirror_copies"):
+        # HBM mirror: segments read from the pinned log instead (buffer busy / copy still in flight)
+        out["mirror"] = {k: st.get(k, 0) for k in ("mirror_copies", "mirror_fallbacks", "mirror_pending_fallbacks",
+                                                   "mirror_backoffs", "split_launches")}
     if R.world > 1:
         out["per_rank_records_per_s"] = [round(r / e, 1) for e, r in res["per_rank"]]
         out["lockstep_agreements"] = st.get("lockstep_agreements", 0)

@@ -43,6 +43,8 @@ def parse(argv=None):
     ap.add_argument("--event-every", type=int, default=None)
     ap.add_argument("--prefetch", type=int, default=2)
     ap.add_argument("--verify", default="deliver", choices=["deliver", "commit"])
+    ap.add_argument("--lockstep", default="off", choices=["off", "rccl"],
+                    help="rccl: the per-step RCCL agreement at world 1 (a one-rank nccl group), as under DDP")
     return ap.parse_args(argv)
 
 
@@ -66,15 +68,28 @@ def run(args, sync=None) -> dict:
         t = time.perf_counter()
         b.fill("json", per_part, "json_f32", size=args.min_len, max_size=args.max_len, threads=args.partitions)
         fill_s = time.perf_counter() - t
+        own_group = False
+        if args.lockstep == "rccl" and not torch.distributed.is_initialized():
+            import socket
+
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                port = s.getsockname()[1]
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            torch.distributed.init_process_group("nccl", rank=0, world_size=1)
+            torch.distributed.all_reduce(torch.ones(1, device=args.device))  # torch's communicator, as DDP
+            own_group = True
         dl = DeviceLoader(Json.placeholder(), B, num_workers=args.workers, device=args.device, dtype=torch.bfloat16,
                           json_parse=args.json_parse, h2d=args.h2d, decode=args.decode, json_count=args.json_count,
                           slots_per_worker=args.slots_per_worker, event_every=args.event_every, prefetch=args.prefetch,
-                          verify=args.verify,
+                          verify=args.verify, lockstep="always" if args.lockstep == "rccl" else True,
                           worker_init_fn=Json.init_worker("json", bootstrap_servers=url, group_id="cfg4",
                                                           auto_offset_reset="earliest"))
         it = iter(auto_commit(dl))
         for _ in range(args.warmup):
             x, lens = next(it)
+        mirror_on = bool(getattr(dl._run, "mirror", False))
+        transport = dict(dl.lockstep_info).get("transport")
         if x.is_cuda:
             torch.cuda.synchronize()
         if sync is not None:
@@ -93,14 +108,17 @@ def run(args, sync=None) -> dict:
         st = dl.stats_summary()
         it.close()
         dl.close()
+        if own_group:
+            torch.distributed.destroy_process_group()
         text_bytes = b.partition_stats("json", 0)["log_bytes"] / max(1, b.end_offset("json", 0))
         return {"config": 4, "metric": "JSON records/s to GPU (bf16 padded), per-batch commit",
                 "value": round(rows / el), "ms_per_step": round(el / args.steps * 1e3, 4),
                 "gb_per_s_text": round(rows / el * text_bytes / 1e9, 2),
                 "batch_size": B, "workers": args.workers, "partitions": args.partitions,
                 "json_parse": args.json_parse, "h2d": args.h2d, "verify": dl.verify,
+                "lockstep": transport,
                 "decode": (("device (json_span.hip from an HBM mirror filled by SDMA copies)"
-                            if dl.plan.mirror else "device (json_span.hip from the pinned logs)")
+                            if mirror_on else "device (json_span.hip from the pinned logs)")
                            if dl.plan.json_span else args.decode),
                 "json_count": "device" if dl.plan.json_count else "workers",
                 "timed_s": round(el, 4), "steps": args.steps,

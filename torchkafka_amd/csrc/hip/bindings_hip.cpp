@@ -357,6 +357,7 @@ PYBIND11_MODULE(_tkhip, m) {
                s["mirror_copies"] = m->copies();
                s["mirror_fallbacks"] = m->fallbacks();
                s["mirror_pending_fallbacks"] = m->pending_fallbacks();
+               s["mirror_backoffs"] = m->backoffs();
                s["mirror_device_bytes"] = m->device_bytes();
              }
              s["log_register_ns"] = d.log_register_ns();

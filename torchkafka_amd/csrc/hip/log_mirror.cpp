@@ -29,7 +29,7 @@ LogMirror::LogMirror(int device, HipQueue* queue, uint64_t chunk_bytes, int chun
   const char* w = std::getenv("TORCHKAFKA_MIRROR_WAIT");
   wait_ = w && w[0] == '1';
   const char* e = std::getenv("TORCHKAFKA_MIRROR_COPY_STREAMS");
-  const int n = copy_streams > 0 ? copy_streams : e ? std::atoi(e) : 2;
+  const int n = e ? std::atoi(e) : copy_streams > 0 ? copy_streams : 2;  // the variable wins (A/B runs)
   cs_.resize(size_t(n < 1 ? 1 : n > 4 ? 4 : n));
   for (auto& c : cs_) {
     TKM_CHECK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
@@ -137,6 +137,18 @@ LogMirror::Buf* LogMirror::ensure(Part& P, uint32_t pidx, int64_t c, uint64_t wa
 
 const uint8_t* LogMirror::map(uint32_t pidx, uint64_t pos, uint32_t len, const uint8_t* log, uint64_t pinned) {
   if (len > tk::kSpanSegMax) throw std::invalid_argument("log mirror: segment longer than kSpanSegMax");
+  if (backoff_left_ > 0) {  // copies fell behind the decode (header): the pinned log, no copy
+    --backoff_left_;
+    ++fallbacks_;
+    return nullptr;
+  }
+  if (!wait_ && ++eval_maps_ == kEvalMaps) {
+    if (eval_pending_ * 2 > kEvalMaps) {
+      backoff_left_ = kBackoffMaps;
+      ++backoffs_;
+    }
+    eval_maps_ = eval_pending_ = 0;
+  }
   Part& P = part(pidx);
   const int64_t c = int64_t(pos / chunk_);
   Buf* b = ensure(P, pidx, c, pos + len, log, pinned, false);
@@ -151,6 +163,7 @@ const uint8_t* LogMirror::map(uint32_t pidx, uint64_t pos, uint32_t len, const u
       // its copy is still in flight: read the pinned log this time (the prefetches keep going)
       ++fallbacks_;
       ++pending_fallbacks_;
+      ++eval_pending_;
       deferred_.push_back(Deferred{pidx, c, log, pinned});
       return nullptr;
     }

@@ -22,6 +22,14 @@
 // a launch that caught up with the copies wait for the copy stream's whole queue -- the needed
 // chunk and every prefetch queued behind it (up to (K - 2) chunks per partition of that stream):
 // config-4 mirror runs then ranged 38-50 M rec/s on one box (profiles/r04_s1/c4_dma_*.log).
+//
+// Back-off: when the copy engines fall behind the decode (more than half of a window of kEvalMaps
+// segments found their copy in flight), every byte crosses PCIe twice -- once copied, once read by
+// the kernel that could not wait for it -- and the loader ran at half the zero-copy rate (27 M
+// against 50 M rec/s, fixed-width under the RCCL lockstep with one copy stream: 188 000 of 188 000
+// segments fell back, profiles/r05_s35).  The mirror then stops copying for kBackoffMaps segments
+// (served from the pinned log, as zero-copy), the copy queue drains, and it starts again ahead of
+// the read position.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -41,8 +49,8 @@ class LogMirror {
   // The driver registers (pins) partition logs in pieces of this many bytes, at multiples of it
   // (MainDriver::kLogChunk): one copy never spans two registrations.
   static constexpr uint64_t kRegAlign = uint64_t(64) << 20;
-  // copy_streams: SDMA copy streams (partitions split p % n); <= 0 takes
-  // TORCHKAFKA_MIRROR_COPY_STREAMS, else 2.  Each takes one of the process's hardware queues.
+  // copy_streams: SDMA copy streams (partitions split p % n); TORCHKAFKA_MIRROR_COPY_STREAMS when
+  // set, else copy_streams when > 0, else 2.  Each takes one of the process's hardware queues.
   // `queue`: the loader's HIP command queue (Engine::queue), used once set_command_queue(true)
   LogMirror(int device, HipQueue* queue, uint64_t chunk_bytes, int chunks_per_partition, int copy_streams = 0);
   ~LogMirror();
@@ -68,7 +76,8 @@ class LogMirror {
   uint64_t copies() const { return copies_; }
   uint64_t fallbacks() const { return fallbacks_; }
   uint64_t pending_fallbacks() const { return pending_fallbacks_; }  // served from the log: copy in flight
-  void reset_stats() { bytes_ = copies_ = fallbacks_ = pending_fallbacks_ = 0; }
+  uint64_t backoffs() const { return backoffs_; }  // times the mirror stopped copying (header)
+  void reset_stats() { bytes_ = copies_ = fallbacks_ = pending_fallbacks_ = backoffs_ = 0; }
   uint64_t device_bytes() const { return dev_bytes_; }
 
  private:
@@ -131,6 +140,11 @@ class LogMirror {
   void record_copied(CopyStream& c);  // records `copied` at the stream's tail (queued when the queue is on)
   bool wait_ = false;
   uint64_t pending_fallbacks_ = 0;
+  // back-off (header): segments mapped / found in flight in the current window, segments left to
+  // serve from the pinned log
+  static constexpr uint32_t kEvalMaps = 512, kBackoffMaps = 8192;
+  uint32_t eval_maps_ = 0, eval_pending_ = 0, backoff_left_ = 0;
+  uint64_t backoffs_ = 0;
   std::vector<CopyStream> cs_;
   CopyStream& cs_of(uint32_t pidx) { return cs_[pidx % cs_.size()]; }
   std::vector<Part> parts_;

@@ -113,6 +113,7 @@ class LoaderCommits:
         self.stats.split_launches += st.get("split_launches", 0)
         self.stats.mirror_fallbacks += st.get("mirror_fallbacks", 0)
         self.stats.mirror_pending_fallbacks += st.get("mirror_pending_fallbacks", 0)
+        self.stats.mirror_backoffs += st.get("mirror_backoffs", 0)
         self.stats.verify_wait_ns += st.get("verify_wait_ns", 0)
         self.stats.lockstep_agreements += st.get("lockstep_agreements", 0)
         self.stats.lockstep_wait_ns += st.get("lockstep_wait_ns", 0)

@@ -64,6 +64,7 @@ class _Run:
         self.engine = None
         self.driver = None
         self.rccl = None
+        self.mirror = False  # the HBM mirror is on for this iteration (PathPlan.mirror, RCCL aside)
         self.payload_addr = [self.ring.payload_address(g) for g in range(self.ring.n_slots)]
         self.staged: deque = deque()       # (g, summary, wms) with H2D issued (or CPU: just acquired)
         self.inflight: list = []           # slots whose H2D may still be reading host memory
@@ -141,11 +142,14 @@ class _Run:
                     self.driver.enable_direct()
                 if L.plan.direct or L.plan.device_decode:
                     self.driver.pin_logs(L._rank_partitions())
-                if L.plan.mirror:
-                    # under the RCCL lockstep one SDMA copy stream: the process's 4 hardware queues
-                    # go to the user's stream, two decode streams and the lockstep's RCCL stream
-                    mcs = 1 if L._lockstep_transport() == "rccl" else 0
-                    self.driver.enable_mirror(int(L.tuning.mirror_chunk_mib) << 20, int(L.tuning.mirror_chunks), mcs)
+                # The mirror keeps its two copy streams under the RCCL lockstep too (round 4 gave it
+                # one there, to leave the hardware queues to the decode and RCCL streams): one SDMA
+                # stream cannot keep ahead of the decode -- fixed-width 25 M rec/s even without the
+                # lockstep, against 48-50 M with two; JSON under the lockstep 48.5-51.6 M with two,
+                # 32.8 M from the pinned logs (profiles/r05_s35_mirror_rccl).
+                self.mirror = L.plan.mirror
+                if self.mirror:
+                    self.driver.enable_mirror(int(L.tuning.mirror_chunk_mib) << 20, int(L.tuning.mirror_chunks), 0)
                 tun = L.tuning
                 if tun.ahead_depth is not None:
                     self.driver.set_ahead_depth(int(tun.ahead_depth))

@@ -63,6 +63,7 @@ class LoaderStats:
     mirror_copies: int = 0
     split_launches: int = 0    # decode launches with each segment split over workgroups (HBM)
     mirror_fallbacks: int = 0  # segments read from the pinned log instead (buffer busy)
+    mirror_backoffs: int = 0   # times the mirror stopped copying: its copies fell behind (log_mirror.h)
     lockstep_agreements: int = 0      # cross-rank agreements (collectives) issued
     lockstep_wait_ns: int = 0         # host time waiting for agreement results
     lockstep_issue_ns: int = 0        # host time issuing agreements (the transport's enqueue)
@@ -132,6 +133,7 @@ class LoaderStats:
             "split_launches": self.split_launches,
             "mirror_fallbacks": self.mirror_fallbacks,
             "mirror_pending_fallbacks": self.mirror_pending_fallbacks,
+            "mirror_backoffs": self.mirror_backoffs,
             "lockstep_agreements": self.lockstep_agreements,
             "lockstep_wait_us_per_batch": self.lockstep_wait_ns / 1e3 / max(self.batches, 1),
             "lockstep_issue_us_per_batch": self.lockstep_issue_ns / 1e3 / max(self.batches, 1),
