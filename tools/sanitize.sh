@@ -8,7 +8,7 @@ cd "$(dirname "$0")/.."
 OUT=${1:-build/sanitize}
 mkdir -p "$OUT"
 CORE=torchkafka_amd/csrc/core
-SRCS="$CORE/ring.cpp $CORE/broker.cpp $CORE/consumer.cpp $CORE/json_text.cpp $CORE/record_batch.cpp $CORE/crc32c.cpp $CORE/codecs.cpp"
+SRCS="$CORE/ring.cpp $CORE/broker.cpp $CORE/broker_groups.cpp $CORE/consumer.cpp $CORE/json_text.cpp $CORE/record_batch.cpp $CORE/crc32c.cpp $CORE/codecs.cpp"
 CXX=${CXX:-g++}
 COMMON="-std=c++17 -O1 -g -fno-omit-frame-pointer -I$CORE -pthread"
 $CXX $COMMON -fsanitize=thread tests/native/ring_stress.cpp $SRCS -o "$OUT/ring_stress_tsan" -lrt -lz

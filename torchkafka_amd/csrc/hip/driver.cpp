@@ -329,667 +329,6 @@ void MainDriver::stage_ready(int extra) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Kernel launches
-
-void MainDriver::launch_group(const int* slots, const int64_t* rows, const size_t* voffs, int n, const SlotView& v,
-                              hipStream_t stream, int dst_dt, void* const* dsts, int64_t row, const float* shift,
-                              const float* scale) {
-  if (v.kind == uint32_t(tk::kPackGatherFixed))
-    eng_->collate_gather_group(slots, n, stream, v.src_dtype, dsts, dst_dt, rows, int64_t(v.row_bytes),
-                               pins_->bases_dev(), shift, scale);
-  else
-    eng_->collate_fixed_group(slots, n, stream, voffs, v.src_dtype, dsts, dst_dt, rows, row, shift, scale);
-}
-
-void MainDriver::copy_extras(const int* slots, const SlotView* const* views, int n, hipStream_t stream) {
-  for (int k = 0; k < n && k < ext_n_; ++k) {
-    const SlotView& v = *views[k];
-    if (v.extras_n && ext_dsts_[k])
-      eng_->copy_bytes(slots[k], stream, size_t(v.extras_offset), ext_dsts_[k], size_t(v.n_rows) * v.extras_n * 8u);
-  }
-  ext_n_ = 0;
-}
-
-void MainDriver::collate_fixed(const SlotView& v, hipStream_t stream, int dst_dt, void* dst, int64_t row,
-                               const float* shift, const float* scale) {
-  const int slot = int(v.g);
-  const SlotView* vs[1] = {&v};
-  if (v.kind != uint32_t(tk::kPackRecordSpan) && ext_n_) copy_extras(&slot, vs, 1, stream);  // its event covers the copy
-  bool record;
-  note_handed(v.g, stream, &record);
-  if (!record && coalesce_wait_ns_ > 0 && coalesce_ > 1) {
-    // adaptive coalescing decides from the latest launch's completion: give this one its event
-    force_event();
-    record = true;
-  }
-  if (record) last_ev_slot_ = v.g;
-  if (v.kind == uint32_t(tk::kPackRecordSpan)) {
-    void* d = dst;
-    int64_t pe;
-    launch_span(&slot, vs, 1, stream, dst_dt, &d, shift, scale, record, &pe);
-    handed_.back().perr = pe;
-    handed_.back().span = true;
-    last_perr_ = pe;
-    return;
-  }
-  if (v.kind == uint32_t(tk::kPackGatherFixed)) {
-    const int64_t rows = v.n_rows;
-    void* d = dst;
-    eng_->collate_gather_group(&slot, 1, stream, v.src_dtype, &d, dst_dt, &rows, int64_t(v.row_bytes),
-                               pins_->bases_dev(), shift, scale, record);
-    return;
-  }
-  eng_->collate_fixed(slot, stream, v.values_offset, v.src_dtype, dst, dst_dt, v.n_rows, row, shift, scale, record);
-}
-
-void MainDriver::collate_varlen(const SlotView& v, hipStream_t stream, int dst_dt, void* out, int64_t L, double pad,
-                                int64_t* lengths, uint8_t* mask) {
-  bool record;
-  if (row_span_kind(v.kind)) {
-    // decoded from the logs on the user's stream, its own completion event
-    switch_stream(stream);
-    const int slot = int(v.g);
-    const SlotView* vs[1] = {&v};
-    void* outs[1] = {out};
-    const int64_t Ls[1] = {L};
-    int64_t* lens[1] = {lengths};
-    uint8_t* masks[1] = {mask};
-    int64_t pe;
-    launch_row_span(&slot, vs, 1, stream, dst_dt, pad, outs, Ls, lens, masks, true, &pe);
-    group_handed(&slot, 1, stream, &pe, true, {}, 1);
-    last_perr_ = pe;
-    return;
-  }
-  if (v.kind == tk::kPackJsonText) {
-    const int64_t idx = verdicts_->next_word();
-    note_handed(v.g, stream, &record);
-    handed_.back().perr = idx;
-    eng_->collate_json(int(v.g), stream, v.values_offset, out, dst_dt, v.n_rows, L, pad, lengths, mask,
-                       verdicts_->err_dev(idx), record);
-    last_perr_ = idx;
-    return;
-  }
-  note_handed(v.g, stream, &record);
-  eng_->collate_varlen(int(v.g), stream, v.values_offset, v.src_dtype, out, dst_dt, v.n_rows, L, pad, lengths, mask,
-                       record);
-}
-
-void MainDriver::copy_payload(const SlotView& v, hipStream_t stream, void* dst) {
-  bool record;
-  note_handed(v.g, stream, &record);
-  force_event();  // copy_raw always records the slot's completion event
-  eng_->copy_raw(int(v.g), stream, 0, dst, size_t(v.payload_bytes));
-}
-
-void MainDriver::check_seg_count(const tk::SpanSeg& sg, uint32_t i) const {
-  constexpr uint32_t kWhole = tk::kSegCrcFirst | tk::kSegCrcLast;
-  if ((sg.flags & tk::kSegCrc) && (sg.flags & kWhole) != kWhole && i >= uint32_t(BatchVerdicts::kPartials))
-    throw std::runtime_error("driver: a batch splits RecordBatches into more than 512 device segments");
-}
-
-void MainDriver::fill_seg(SpanDevSeg& d, const tk::SpanSeg& sg, const uint8_t* src, int k, uint32_t i) {
-  d = SpanDevSeg{};
-  d.src = src;
-  d.log_pos = sg.log_pos;
-  d.len = sg.len;
-  d.flags = sg.flags;
-  d.crc = sg.crc;
-  d.row_begin = sg.row_begin;
-  d.row_end = sg.row_end;
-  d.batch = uint16_t(k);
-  d.seg = uint16_t(i);
-}
-
-void MainDriver::launch_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream, int dst_dt,
-                             void* const* dsts, const float* shift, const float* scale, bool record_last,
-                             int64_t* perrs) {
-  if (!broker_) throw std::runtime_error("driver: device decode needs the synthetic broker");
-  verdicts_->ensure_partials();
-  LogMirror* mirror = pins_->mirror();
-  const SlotView& v0 = *views[0];
-  SpanLaunch a{};
-  a.row_elems = v0.max_row_len;
-  const int ssz = dtype_size(v0.src_dtype), dsz = dtype_size(dst_dt);
-  const int per = ssz > 0 ? 16 / ssz : 1;
-  bool vec = ssz > 0 && a.row_elems % per == 0 && (a.row_elems * dsz) % 16 == 0;
-  for (int k = 0; k < n; ++k) {
-    vec = vec && reinterpret_cast<uintptr_t>(dsts[k]) % 16 == 0;
-    perrs[k] = verdicts_->next_word();
-    a.b[k].out = dsts[k];
-    a.b[k].err = verdicts_->err_dev(perrs[k]);
-    a.b[k].partials = verdicts_->partials_dev(perrs[k]);
-    const SlotView& v = *views[k];
-    if (v.extras_n && k < ext_n_ && ext_dsts_[k]) {  // key / timestamp columns ride in the same kernel
-      a.b[k].ext_out = ext_dsts_[k];
-      a.b[k].ext_off = v.extras_offset;
-      a.b[k].ext_words = v.n_rows * v.extras_n;
-    }
-  }
-  ext_n_ = 0;
-  a.vec_store = vec ? 1 : 0;
-  bool pcie = false;  // a segment of this launch is read over PCIe (not from the HBM mirror)
-  auto flush = [&](bool record) {
-    // segments split over parts only when every one is read from HBM: parts multiply the loads in
-    // flight of a lone group from the mirror (2 MiB: 30.6 -> 12.6 us with 8), while over PCIe the
-    // link is the limit and more workgroups only add their fixed costs (profiles/r05_s30_lane_merge)
-    a.parts = pcie ? 1 : eng_->span_parts();
-    split_launches_ += a.parts > 1;
-    pcie = false;
-    if (mirror) mirror->before(stream);
-    eng_->collate_span(slots, n, stream, a, v0.src_dtype, dst_dt, shift, scale, record);
-    if (mirror) mirror->after(stream);
-  };
-  for (int k = 0; k < n; ++k) {
-    const tk::SpanSeg* sg = segs(*views[k]);
-    for (uint32_t i = 0; i < views[k]->n_segs; ++i) {
-      check_seg_count(sg[i], i);
-      if (a.n_seg == kMaxLaunchSegs) {
-        flush(false);
-        a.n_seg = 0;
-      }
-      fill_seg(a.s[a.n_seg++], sg[i], seg_src(sg[i], &pcie), k, i);
-    }
-  }
-  flush(record_last);
-}
-
-uint64_t MainDriver::stage_alloc(uint64_t bytes) {
-  bytes = (bytes + 255) & ~uint64_t(255);
-  if (bytes > kStageBytes) throw std::runtime_error("driver: a device JSON group exceeds the staging ring");
-  if (!stage_dev_ && hipMalloc(reinterpret_cast<void**>(&stage_dev_), kStageBytes) != hipSuccess)
-    throw std::runtime_error("driver: hipMalloc of the JSON staging ring failed");
-  uint64_t pos = stage_head_;
-  const uint64_t in = pos % kStageBytes;
-  if (in + bytes > kStageBytes) pos += kStageBytes - in;  // never split a region: restart at the front
-  while (pos + bytes - stage_tail_ > kStageBytes) {
-    // the oldest groups still read their regions: wait for the first one with an event
-    cover_handed();
-    bool waited = false;
-    for (const auto& h : handed_) {
-      if (!h.ev) continue;
-      eng_->wait_slot(int(h.g));
-      waited = true;
-      break;
-    }
-    if (!waited) throw std::logic_error("driver: JSON staging ring full with nothing in flight");
-    pending_query_ns_ = 0;
-    release_completed_impl();
-  }
-  stage_head_ = pos + bytes;
-  stage_last_end_ = stage_head_;
-  return pos % kStageBytes;
-}
-
-void MainDriver::launch_json_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream,
-                                  int dst_dt, double pad, void* const* outs, const int64_t* Ls,
-                                  int64_t* const* lengths, uint8_t* const* masks, bool record_last, int64_t* perrs) {
-  if (!broker_) throw std::runtime_error("driver: device JSON parse needs the synthetic broker");
-  verdicts_->ensure_partials();
-  LogMirror* mirror = pins_->mirror();
-  tk::Ring& ring = poller_->ring();
-  // staging per batch: the row descriptors, then one region per segment (row texts rounded up to
-  // 16 bytes, or the float32 values of the rows the worker parsed)
-  constexpr uint64_t kA = 256;
-  auto up = [](uint64_t x, uint64_t a) { return (x + a - 1) / a * a; };
-  // bytes of segment i's region in its batch's staging area
-  auto seg_bytes = [&](const SlotView& v, const tk::SpanSeg& sg) {
-    if (!(sg.flags & tk::kSegHostRows)) return up(up(sg.len, 16) + 16 * uint64_t(sg.row_end - sg.row_begin), kA);
-    const auto* rows = reinterpret_cast<const tk::JsonSpanRow*>(ring.payload(uint32_t(v.g)));
-    uint64_t b = 0;
-    for (uint32_t r = sg.row_begin; r < sg.row_end; ++r) {
-      int64_t c = rows[r].count;
-      if (v.trunc_len >= 0 && c > v.trunc_len) c = v.trunc_len;
-      b += up(uint64_t(c < 0 ? 0 : c) * 4, 16);
-    }
-    return up(b, kA);
-  };
-  uint64_t batch_bytes[kMaxGroup], total = 0;
-  for (int k = 0; k < n; ++k) {
-    const SlotView& v = *views[k];
-    const tk::SpanSeg* sg = segs(v);
-    uint64_t b = up(uint64_t(v.n_rows) * sizeof(JsonRowDesc), kA);
-    for (uint32_t i = 0; i < v.n_segs; ++i) b += seg_bytes(v, sg[i]);
-    batch_bytes[k] = b;
-    total += b;
-  }
-  const uint64_t base = stage_alloc(total);
-  JsonStageLaunch a{};
-  bool pcie = false;
-  JsonGroupArgs ga{};
-  ga.n = n;
-  ga.pad = float(pad);
-  ga.err_tag = tk::kSpanParseErrBit;
-  ga.mult = json_mult_;
-  uint64_t off = base;
-  for (int k = 0; k < n; ++k) {
-    const SlotView& v = *views[k];
-    perrs[k] = verdicts_->next_word();
-    JsonStageBatch& b = a.b[k];
-    if (v.flags & tk::kSlotDevCount) {  // tagged count words: nothing to zero per launch
-      b.ctr = verdicts_->json_ctr_dev(perrs[k]);
-      b.ctr_tag = verdicts_->ctr_tag(perrs[k]);
-      ga.ctr[k] = b.ctr;
-      ga.ctr_tag[k] = b.ctr_tag;
-      ga.info[k] = verdicts_->json_info_dev(perrs[k]);
-    }
-    b.desc = reinterpret_cast<JsonRowDesc*>(stage_dev_ + off);
-    const uint64_t dbytes = up(uint64_t(v.n_rows) * sizeof(JsonRowDesc), kA);
-    b.stage = stage_dev_ + off + dbytes;
-    b.err = verdicts_->err_dev(perrs[k]);
-    b.partials = verdicts_->partials_dev(perrs[k]);
-    b.trunc_len = v.trunc_len;
-    ga.rows[k] = b.desc;
-    ga.vals[k] = b.stage;
-    ga.vals_cap[k] = batch_bytes[k] - dbytes;
-    ga.out[k] = outs[k];
-    ga.L[k] = Ls[k];
-    ga.lengths[k] = lengths[k];
-    ga.mask[k] = masks[k];
-    ga.err[k] = b.err;
-    ga.row_base[k + 1] = ga.row_base[k] + int64_t(v.n_rows);
-    ga.trunc[k] = v.trunc_len;
-    off += batch_bytes[k];
-  }
-  auto flush = [&]() {
-    a.parts = pcie ? 1 : eng_->json_span_parts();  // parts only for segments all read from HBM (launch_span)
-    split_launches_ += a.parts > 1;
-    pcie = false;
-    if (mirror) mirror->before(stream);
-    eng_->collate_json_stage(slots, n, stream, a);
-    if (mirror) mirror->after(stream);
-  };
-  for (int k = 0; k < n; ++k) {
-    const SlotView& v = *views[k];
-    const tk::SpanSeg* sg = segs(v);
-    uint64_t soff = 0;  // offset in the batch's staging area (after its descriptors)
-    for (uint32_t i = 0; i < v.n_segs; ++i) {
-      check_seg_count(sg[i], i);
-      if (a.n_seg == kMaxLaunchSegs) {
-        flush();
-        a.n_seg = 0;
-      }
-      SpanDevSeg& d = a.s[a.n_seg++];
-      fill_seg(d, sg[i], (sg[i].flags & tk::kSegHostRows) ? nullptr : seg_src(sg[i], &pcie), k, i);
-      d.stage_off = uint32_t(soff);
-      soff += seg_bytes(v, sg[i]);
-    }
-  }
-  flush();
-  bool devc = false;
-  for (int k = 0; k < n; ++k) devc = devc || ga.ctr[k] != nullptr;
-  // a wave per row: counts, simple check, the width words.  Not fused into json_stage_kernel: its
-  // few workgroups (one per segment) took 149 us per group doing it instead of 71 us, and config 4
-  // fell from 40.5 M to 35.5 M rec/s (profiles/r04_s4)
-  if (devc) eng_->run_on(stream, [ga, stream] { launch_json_count(ga, stream); });
-  // the parse: a block per row over the staged texts, on the same stream
-  eng_->run_on(stream, [ga, dst_dt, stream]() mutable { launch_json_group(ga, dst_dt, stream); });
-  if (record_last) eng_->record_done(slots[n - 1], stream);
-}
-
-void MainDriver::launch_var_span(const int* slots, const SlotView* const* views, int n, hipStream_t stream,
-                                 int dst_dt, double pad, void* const* outs, const int64_t* Ls,
-                                 int64_t* const* lengths, uint8_t* const* masks, bool record_last, int64_t* perrs) {
-  if (!broker_) throw std::runtime_error("driver: device decode needs the synthetic broker");
-  verdicts_->ensure_partials();
-  LogMirror* mirror = pins_->mirror();
-  VarSpanLaunch a{};
-  bool pcie = false;
-  const int src_dt = views[0]->src_dtype;
-  for (int k = 0; k < n; ++k) {
-    perrs[k] = verdicts_->next_word();
-    VarSpanBatch& b = a.b[k];
-    b.out = outs[k];
-    b.L = Ls[k];
-    b.lengths = lengths[k];
-    b.mask = masks[k];
-    b.err = verdicts_->err_dev(perrs[k]);
-    b.partials = verdicts_->partials_dev(perrs[k]);
-    b.trunc_len = views[k]->trunc_len;
-    // vector stores of a 16-byte source group (16 / ssz elements of dsz bytes): rows and groups aligned
-    const int ssz = dtype_size(src_dt), dsz = dtype_size(dst_dt);
-    const int64_t gbytes = ssz > 0 ? int64_t(16 / ssz) * dsz : 0;
-    b.reserved = (gbytes >= 16 && gbytes % 16 == 0 && reinterpret_cast<uintptr_t>(outs[k]) % 16 == 0 &&
-                  (Ls[k] * dsz) % 16 == 0) ? 1 : 0;
-  }
-  auto flush = [&](bool record) {
-    for (int k = 0; k < n; ++k) {
-      a.b[k].slot = eng_->slot_src(slots[k], stream);  // DMA mode: after the slot's copy
-      a.b[k].rows = reinterpret_cast<const tk::JsonSpanRow*>(a.b[k].slot);
-    }
-    a.tabs = eng_->span_tables();
-    a.parts = pcie ? 1 : eng_->span_parts();  // parts only for segments all read from HBM (launch_span)
-    a.part_acc = a.parts > 1 ? eng_->part_acc(stream) : nullptr;
-    split_launches_ += a.parts > 1;
-    pcie = false;
-    if (mirror) mirror->before(stream);
-    eng_->run_on(stream, [a, src_dt, dst_dt, pad, stream] { tkh::launch_var_span(a, src_dt, dst_dt, pad, stream); });
-    if (mirror) mirror->after(stream);
-    if (record) eng_->record_done(slots[n - 1], stream);
-  };
-  for (int k = 0; k < n; ++k) {
-    const SlotView& v = *views[k];
-    if (v.src_dtype != src_dt) throw std::invalid_argument("driver: a var-len group mixes element dtypes");
-    const tk::SpanSeg* sg = segs(v);
-    for (uint32_t i = 0; i < v.n_segs; ++i) {
-      check_seg_count(sg[i], i);
-      if (a.n_seg == kMaxLaunchSegs) {
-        flush(false);
-        a.n_seg = 0;
-      }
-      fill_seg(a.s[a.n_seg++], sg[i], (sg[i].flags & tk::kSegHostRows) ? nullptr : seg_src(sg[i], &pcie), k, i);
-    }
-  }
-  flush(record_last);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Group formation and the coalesced steps
-
-size_t MainDriver::json_group_extend() {
-  group_idx_.clear();
-  if (coalesce_ <= 1 || (last.kind != uint32_t(tk::kPackJsonText) && !row_span_kind(last.kind))) return 0;
-  const auto& staged = poller_->staged();
-  uint64_t bytes = last.span_bytes;
-  for (size_t i = 0; i < staged.size() && int(1 + group_idx_.size()) < coalesce_; ++i) {
-    const SlotView& v = staged[i];
-    if (v.g < 0) continue;  // watermark-only slot: rides on the next delivered batch
-    if (v.pre || v.kind != last.kind || v.n_rows == 0 || group_full(bytes, v)) break;
-    bytes += v.span_bytes;
-    group_idx_.push_back(i);
-  }
-  return group_idx_.size();
-}
-
-void MainDriver::json_group_launch(hipStream_t stream, int dst_dt, double pad, void* const* outs, const int64_t* Ls,
-                                   int64_t* const* lengths, uint8_t* const* masks,
-                                   std::vector<std::shared_ptr<void>>&& handles) {
-  const int n = 1 + int(group_idx_.size());
-  if (int(handles.size()) != n - 1) throw std::invalid_argument("driver: group handles do not match the group");
-  auto& staged = poller_->staged();
-  int slots[kMaxGroup];
-  const SlotView* vs[kMaxGroup];
-  for (int k = 0; k < n; ++k) {
-    vs[k] = k == 0 ? &last : &staged[group_idx_[size_t(k - 1)]];
-    slots[k] = int(vs[k]->g);
-  }
-  int64_t perrs[kMaxGroup];
-  if (row_span_kind(last.kind)) {
-    // decoded on the next decode stream (outputs allocated there, torch_step.cpp); the user's
-    // stream waits for the group's completion
-    cover_handed();
-    hipStream_t ks = next_decode_stream();
-    ++span_launches_;
-    last_stream_ = ks;
-    launch_row_span(slots, vs, n, ks, dst_dt, pad, outs, Ls, lengths, masks, true, perrs);
-    last.perr = perrs[0];
-    const int64_t gid = group_handed(slots, n, ks, perrs, true, std::move(handles), 1);
-    wait_launch(slots[n - 1], gid, stream);
-    group_idx_.clear();
-    return;
-  }
-  size_t voffs[kMaxGroup];
-  int64_t rows[kMaxGroup];
-  int32_t* errs[kMaxGroup];
-  for (int k = 0; k < n; ++k) {
-    voffs[k] = vs[k]->values_offset;
-    rows[k] = vs[k]->n_rows;
-    perrs[k] = verdicts_->next_word();
-    errs[k] = verdicts_->err_dev(perrs[k]);
-  }
-  last.perr = perrs[0];
-  switch_stream(stream);
-  eng_->collate_json_group(slots, n, stream, voffs, rows, outs, Ls, lengths, masks, errs, pad, dst_dt);
-  group_handed(slots, n, stream, perrs, false, std::move(handles), 1);
-  group_idx_.clear();
-}
-
-int64_t MainDriver::step_fixed(hipStream_t stream, int dst_dt, void* dst, int64_t row, const float* shift,
-                               const float* scale, bool auto_commit, int64_t timeout_ms, int* commit_status,
-                               SlotView* out) {
-  *commit_status = 0;
-  const int64_t t0 = tk::now_ns();
-  finish_delivered(stream);  // asking for the next batch finishes the previous one
-  if (auto_commit) *commit_status = commit_pending();
-  const int64_t t1 = tk::now_ns();
-  int r = next_slot(timeout_ms, out);
-  const int64_t t2 = tk::now_ns();
-  ph_commit_ns_ += t1 - t0;
-  ph_next_ns_ += t2 - t1;
-  if (r < 0) return r;
-  collate_fixed(*out, stream, dst_dt, dst, row, shift, scale);
-  set_delivered(*out);
-  poller_->prefetch_ready();
-  ph_launch_ns_ += tk::now_ns() - t2;
-  ++ph_steps_;
-  return out->n_rows;
-}
-
-int64_t MainDriver::step_group_begin(hipStream_t stream, bool auto_commit, int64_t timeout_ms, int* commit_status,
-                                     std::vector<int64_t>* group_rows, std::shared_ptr<void>* pre_out) {
-  *commit_status = 0;
-  group_rows->clear();
-  group_idx_.clear();
-  const int64_t t0 = tk::now_ns();
-  finish_delivered(stream);  // asking for the next batch finishes the previous one
-  if (auto_commit) *commit_status = commit_pending();
-  const int64_t t1 = tk::now_ns();
-  auto& staged = poller_->staged();
-  if (!ls_ && coalesce_ > 1) {
-    // stage what the workers already published, so a group can form (never blocks)
-    while (int(staged.size()) < prefetch_ + coalesce_) {
-      const int r = poller_->poll(false, 0);
-      if (r == -3) return -3;
-      if (r <= 0) break;
-    }
-  }
-  occ_handed_ += int64_t(handed_.size());
-  occ_staged_ += int64_t(staged.size());
-  ++occ_samples_;
-  const int r = next_slot(timeout_ms, &last);
-  const int64_t t2 = tk::now_ns();
-  ph_commit_ns_ += t1 - t0;
-  ph_next_ns_ += t2 - t1;
-  if (r < 0) return r;
-  if (last.pre) {
-    // collated by an earlier group launch; a consumer on another stream waits for that kernel
-    if (last.pre_stream != stream) wait_launch(last.pre_event_slot, last.pre_group, stream);
-    *pre_out = std::move(last.pre_out);
-    set_delivered(last);
-    poller_->prefetch_ready();
-    ++ph_steps_;
-    return last.n_rows;
-  }
-  group_rows->push_back(last.n_rows);
-  if (last.kind == uint32_t(tk::kPackFixed) || last.kind == uint32_t(tk::kPackGatherFixed) ||
-      last.kind == uint32_t(tk::kPackRecordSpan)) {
-    group_capped_ = false;
-    extend_group();
-    if (coalesce_wait_ns_ > 0 && int(1 + group_idx_.size()) < coalesce_ && !group_capped_) {
-      const int64_t cw0 = tk::now_ns();
-      const int64_t until = cw0 + coalesce_wait_ns_;
-      while (int(1 + group_idx_.size()) < coalesce_ && !group_capped_ && gpu_busy() && tk::now_ns() < until) {
-        const int r2 = poller_->poll(false, 0);
-        if (r2 == -3) break;  // reported by the next call
-        if (r2 == 1) {
-          extend_group();
-          continue;
-        }
-        release_completed();
-        for (int k = 0; k < 16; ++k) tk::cpu_relax();
-      }
-      cwait_ns_ += tk::now_ns() - cw0;
-    }
-    for (size_t i : group_idx_) group_rows->push_back(staged[i].n_rows);
-  }
-  return last.n_rows;
-}
-
-// Appends to group_idx_ the staged batches right behind `last` that one kernel can collate with it.
-void MainDriver::extend_group() {
-  const auto& staged = poller_->staged();
-  size_t i = group_idx_.empty() ? 0 : group_idx_.back() + 1;
-  uint64_t bytes = last.span_bytes;
-  for (size_t k : group_idx_) bytes += staged[k].span_bytes;
-  for (; i < staged.size() && int(1 + group_idx_.size()) < coalesce_; ++i) {
-    const SlotView& v = staged[i];
-    if (v.g < 0) continue;  // watermark-only slot: rides on the next delivered batch
-    if (group_full(bytes, v)) group_capped_ = true;
-    if (v.pre || v.kind != last.kind || v.src_dtype != last.src_dtype || v.max_row_len != last.max_row_len ||
-        v.row_bytes != last.row_bytes || v.shape != last.shape || v.n_rows == 0 || group_capped_)
-      return;
-    bytes += v.span_bytes;
-    group_idx_.push_back(i);
-  }
-}
-
-void MainDriver::step_group_launch(hipStream_t stream, int dst_dt, void* const* dsts, int64_t row,
-                                   const float* shift, const float* scale,
-                                   std::vector<std::shared_ptr<void>>&& handles) {
-  const int64_t t0 = tk::now_ns();
-  const int n = 1 + int(group_idx_.size());
-  if (int(handles.size()) != n - 1) throw std::invalid_argument("driver: group handles do not match the group");
-  auto& staged = poller_->staged();
-  int slots[kMaxGroup];
-  size_t voffs[kMaxGroup];
-  int64_t rows[kMaxGroup];
-  const SlotView* vs[kMaxGroup];
-  for (int k = 0; k < n; ++k) {
-    vs[k] = k == 0 ? &last : &staged[group_idx_[size_t(k - 1)]];
-    slots[k] = int(vs[k]->g);
-    voffs[k] = vs[k]->values_offset;
-    rows[k] = vs[k]->n_rows;
-  }
-  if (last.kind == uint32_t(tk::kPackRecordSpan)) {
-    // Device decode rotates over the decode streams: a group's kernel is PCIe-bound while it
-    // loads and compute-bound in its CRC/extract tail, so the next group's loads overlap that
-    // tail.  The outputs were allocated on the decode stream (torch_step.cpp: the caching
-    // allocator orders their reuse against it, and knows the user's stream uses them); the
-    // user's stream waits for the group's completion before it touches a batch of it.
-    cover_handed();
-    hipStream_t ks = next_decode_stream();
-    ++span_launches_;
-    last_stream_ = ks;
-    int64_t perrs[kMaxGroup];
-    launch_span(slots, vs, n, ks, dst_dt, dsts, shift, scale, true, perrs);
-    last.perr = perrs[0];
-    const int64_t gid = group_handed(slots, n, ks, perrs, true, std::move(handles), 1);
-    wait_launch(slots[n - 1], gid, stream);
-  } else if (n == 1) {
-    collate_fixed(last, stream, dst_dt, dsts[0], row, shift, scale);
-  } else {
-    switch_stream(stream);
-    if (ext_n_) copy_extras(slots, vs, n, stream);
-    launch_group(slots, rows, voffs, n, last, stream, dst_dt, dsts, row, shift, scale);
-    group_handed(slots, n, stream, nullptr, false, std::move(handles), 1);
-  }
-  group_idx_.clear();
-  set_delivered(last);
-  poller_->prefetch_ready();
-  ph_launch_ns_ += tk::now_ns() - t0;
-  ++ph_steps_;
-}
-
-void MainDriver::ahead_begin(std::vector<int64_t>* rows) {
-  rows->clear();
-  group_idx_.clear();
-  if (ahead_depth_ <= 0 || coalesce_ <= 1) return;
-  const auto& staged = poller_->staged();
-  const size_t want = size_t(prefetch_ + (ahead_depth_ + 1) * coalesce_);
-  while (staged.size() < want) {
-    if (poller_->poll(false, 0) <= 0) break;  // nothing ready (an error is reported by next_slot)
-  }
-  int pre = 0;
-  size_t i0 = staged.size();
-  for (size_t i = 0; i < staged.size(); ++i) {
-    const SlotView& v = staged[i];
-    if (v.g < 0) continue;
-    if (v.pre)
-      ++pre;
-    else if (i0 == staged.size())
-      i0 = i;
-  }
-  if (pre >= ahead_depth_ * coalesce_ || i0 == staged.size()) return;
-  const SlotView& f = staged[i0];
-  const bool json = row_span_kind(f.kind);  // outputs sized per batch: no shape match needed
-  if ((f.kind != uint32_t(tk::kPackRecordSpan) && !json) || f.n_rows == 0) return;
-  uint64_t bytes = 0;
-  bool capped = false;
-  for (size_t i = i0; i < staged.size() && int(group_idx_.size()) < coalesce_; ++i) {
-    const SlotView& v = staged[i];
-    if (v.g < 0) continue;  // watermark-only slot: rides on the next delivered batch
-    if (v.pre || v.kind != f.kind || v.n_rows == 0) break;
-    if (group_full(bytes, v)) {
-      capped = true;  // a full group by bytes
-      break;
-    }
-    bytes += v.span_bytes;
-    if (!json && (v.src_dtype != f.src_dtype || v.max_row_len != f.max_row_len || v.row_bytes != f.row_bytes ||
-                  v.shape != f.shape))
-      break;
-    group_idx_.push_back(i);
-  }
-  // a group that could not take one more batch of its last one's size is full without waiting to
-  // see that batch: config 5 (8 MiB batches, 16 MiB groups, a 4-slot ring) never has a third
-  // batch staged while two are in flight, so its groups would otherwise never go ahead
-  if (!capped && !group_idx_.empty() && bytes + staged[group_idx_.back()].span_bytes > group_bytes_max_)
-    capped = true;
-  if (int(group_idx_.size()) < coalesce_ && !capped) {  // only full groups go ahead; the rest waits for the user
-    group_idx_.clear();
-    return;
-  }
-  for (size_t i : group_idx_) rows->push_back(staged[i].n_rows);
-}
-
-void MainDriver::ahead_launch(int dst_dt, void* const* dsts, const float* shift, const float* scale,
-                              std::vector<std::shared_ptr<void>>&& handles) {
-  const int n = int(group_idx_.size());
-  if (n < 1 || int(handles.size()) != n) throw std::invalid_argument("driver: ahead group does not match");
-  const int64_t t0 = tk::now_ns();
-  auto& staged = poller_->staged();
-  int slots[kMaxGroup];
-  const SlotView* vs[kMaxGroup];
-  for (int k = 0; k < n; ++k) {
-    vs[k] = &staged[group_idx_[size_t(k)]];
-    slots[k] = int(vs[k]->g);
-  }
-  cover_handed();
-  hipStream_t ks = next_decode_stream();
-  ++span_launches_;
-  last_stream_ = ks;
-  int64_t perrs[kMaxGroup];
-  launch_span(slots, vs, n, ks, dst_dt, dsts, shift, scale, true, perrs);
-  group_handed(slots, n, ks, perrs, true, std::move(handles), 0);
-  group_idx_.clear();
-  ++ahead_groups_;
-  ph_launch_ns_ += tk::now_ns() - t0;
-}
-
-void MainDriver::ahead_launch_json(int dst_dt, double pad, void* const* outs, const int64_t* Ls,
-                                   int64_t* const* lengths, uint8_t* const* masks,
-                                   std::vector<std::shared_ptr<void>>&& handles) {
-  const int n = int(group_idx_.size());
-  if (n < 1 || int(handles.size()) != n) throw std::invalid_argument("driver: ahead group does not match");
-  const int64_t t0 = tk::now_ns();
-  auto& staged = poller_->staged();
-  int slots[kMaxGroup];
-  const SlotView* vs[kMaxGroup];
-  for (int k = 0; k < n; ++k) {
-    vs[k] = &staged[group_idx_[size_t(k)]];
-    slots[k] = int(vs[k]->g);
-  }
-  cover_handed();
-  hipStream_t ks = next_decode_stream();
-  ++span_launches_;
-  last_stream_ = ks;
-  int64_t perrs[kMaxGroup];
-  launch_row_span(slots, vs, n, ks, dst_dt, pad, outs, Ls, lengths, masks, true, perrs);
-  group_handed(slots, n, ks, perrs, true, std::move(handles), 0);
-  group_idx_.clear();
-  ++ahead_groups_;
-  ph_launch_ns_ += tk::now_ns() - t0;
-}
-
-// ---------------------------------------------------------------------------------------------
 // Delivery, fencing and commits
 
 void MainDriver::deliver(const SlotView& v) { set_delivered(v); }
