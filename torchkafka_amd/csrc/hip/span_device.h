@@ -47,7 +47,7 @@ constexpr int kWinBytes = tk::kSpanWinBytes;    // one window buffer (span.h)
 constexpr int kWinLoads = tk::kSpanWinLoads;    // the loader wave's LDS-DMA instructions per window
 static_assert(kWinBytes % 16 == 0, "window buffers stay 16-byte aligned");
 static_assert(kWinLoads <= 21, "counted waits: at most 3 windows of loads in flight (vmcnt <= 63)");
-static_assert(kThreads == 512, "crc_merge / crc_verdict: 8 compute waves");
+static_assert(kThreads == 512, "crc_merge / crc_finish: 8 compute waves, one lane constant per thread");
 
 __device__ __forceinline__ bool loader_wave() { return threadIdx.x >= kThreads; }
 
