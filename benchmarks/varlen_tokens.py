@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--decode", default="auto", choices=["auto", "device", "host"])
     ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy"])
+    ap.add_argument("--lockstep", default="off", choices=["off", "rccl"],
+                    help="rccl: the per-step RCCL agreement at world 1 (a one-rank nccl group), as under DDP")
     args = ap.parse_args()
 
     import torch
@@ -52,13 +54,24 @@ def main():
         t = time.perf_counter()
         b.fill("tok", per_part, "tokens_i32", size=args.min_len, max_size=args.max_len, threads=args.partitions)
         fill_s = time.perf_counter() - t
+        if args.lockstep == "rccl":
+            import socket
+
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                port = s.getsockname()[1]
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            torch.distributed.init_process_group("nccl", rank=0, world_size=1)
+            torch.distributed.all_reduce(torch.ones(1, device=args.device))  # torch's communicator, as DDP
         dl = DeviceLoader(Tokens.placeholder(), B, num_workers=args.workers, device=args.device, dtype=torch.int64,
-                          decode=args.decode, h2d=args.h2d,
+                          decode=args.decode, h2d=args.h2d, lockstep="always" if args.lockstep == "rccl" else True,
                           worker_init_fn=Tokens.init_worker("tok", bootstrap_servers=url, group_id="tok",
                                                             auto_offset_reset="earliest"))
         it = iter(auto_commit(dl))
         for _ in range(args.warmup):
             x, lens = next(it)
+        mirror_on = bool(getattr(dl._run, "mirror", False))
+        transport = dict(dl.lockstep_info).get("transport")
         torch.cuda.synchronize()
         dl.reset_stats()
         t0 = time.perf_counter()
@@ -69,14 +82,18 @@ def main():
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         st = dl.stats_summary()
-        decode = (("device (varlen_span_kernel from an HBM mirror filled by SDMA copies)" if dl.plan.mirror
+        decode = (("device (varlen_span_kernel from an HBM mirror filled by SDMA copies)" if mirror_on
                    else "device (varlen_span_kernel from the pinned logs)") if dl.plan.var_span else "host workers")
         it.close()
+        dl.close()
+        if args.lockstep == "rccl":
+            torch.distributed.destroy_process_group()
         rec_bytes = b.partition_stats("tok", 0)["log_bytes"] / max(1, b.end_offset("tok", 0))
         print(json.dumps({"metric": "int32 token records/s to GPU (int64 padded), per-batch commit",
                           "value": round(rows / el), "ms_per_step": round(el / args.steps * 1e3, 4),
                           "timed_s": round(el, 4), "steps": args.steps, "batch_size": B, "workers": args.workers,
-                          "decode": decode, "h2d": args.h2d, "avg_record_bytes": round(rec_bytes),
+                          "decode": decode, "h2d": args.h2d, "lockstep": transport,
+                          "avg_record_bytes": round(rec_bytes),
                           "gb_per_s": round(rows / el * rec_bytes / 1e9, 2), "last_batch_shape": list(x.shape),
                           "fill_s": round(fill_s, 2), "loader": st}))
     finally:
