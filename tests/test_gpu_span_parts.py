@@ -94,5 +94,5 @@ def test_parts_catch_a_flip_in_every_part(broker, parts, frac):
 
 
 def test_parts_var_len_through_mirror(broker, parts):
-    """VarLen token rows (h2d='auto' decodes them from the HBM mirror) under each split."""
-    base.test_var_span_matches_host_path(broker, torch.int32, torch.int64, (0, 300), 0, 0, {})
+    """VarLen token rows decoded from the HBM mirror (h2d='dma') under each split."""
+    base.test_var_span_matches_host_path(broker, torch.int32, torch.int64, (0, 300), 0, 0, {"h2d": "dma"})

@@ -12,7 +12,8 @@ kafka_dataset.py:147-171); everything here is the device side SURVEY §2.6 adds:
 * ``var_span``  VarLen records padded/stacked by the same kernel family (varlen_span_kernel);
 * ``json_span`` JsonArray texts parsed on the GPU straight from the logs (json_span.hip);
 * ``json_device`` JsonArray texts framed by the workers and parsed by json_parse.hip;
-* ``mirror``    h2d='dma' with device decode: log bytes reach HBM on SDMA copy streams first;
+* ``mirror``    h2d='dma' with device decode (and 'auto' for JSON): log bytes reach HBM on SDMA
+                copy streams first;
 * ``direct``    h2d='direct': fixed-width rows gathered from the pinned logs (experimental);
 * ``fast_path`` / ``varlen_fast``: one argument-free native call per batch (torch_step.cpp).
 
@@ -110,13 +111,14 @@ class PathPlan:
                 raise ValueError("h2d='direct' needs the synthetic broker (bootstrap_servers shm:// or file://) "
                                  "and a group_id")
             direct = True
-        # The HBM mirror: always with h2d='dma'; with h2d='auto' for JSON and var-len rows.  Since its
-        # launches never wait for a copy (round 4) it beats zero-copy there on every box measured --
-        # config 4: 40.8-45.9 M rec/s over 20 runs (none below 40 M) against 38.8-41.3 M zero-copy,
-        # VarLen tokens 43.3 / 46.2 M against 42.2 / 44.2 M (profiles/r04_s1..s4).  Fixed-width decode
-        # stays zero-copy under 'auto': both run at the PCIe roof (52.5 against 51.5 M), and zero-copy
-        # needs no HBM and no copy engine.
-        mirror = (span or json_span or var_span) if h2d == "dma" else (h2d == "auto" and (json_span or var_span))
+        # The HBM mirror: always with h2d='dma'; with h2d='auto' for JSON rows, where it beats
+        # zero-copy with and without the RCCL lockstep (config 4: 46-52 M rec/s against 38 M, under
+        # the lockstep 46-52 M against 33 M; profiles/r05_s35_mirror_rccl).  Fixed-width and var-len
+        # decode stay zero-copy under 'auto': fixed-width runs at the PCIe roof either way (and the
+        # mirror loses 40 % under the lockstep), var-len tokens 45-47 M zero-copy against 42-43 M
+        # mirrored (under the lockstep 42-47 M against 31-37 M; round 4 had measured the reverse,
+        # 43.3 / 46.2 M mirrored against 42.2 / 44.2 M) -- and zero-copy needs no HBM and no copy engine.
+        mirror = (span or json_span or var_span) if h2d == "dma" else (h2d == "auto" and json_span)
         return cls(cuda=cuda, kind=kind, process_overridden=process_overridden, span=span, var_span=var_span,
                    json_span=json_span, json_device=json_device, json_count=json_count, mirror=mirror,
                    direct=direct, fast_path=fast_path, varlen_fast=fast_common and kind in (1, 2), h2d=h2d)
