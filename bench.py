@@ -94,7 +94,8 @@ def parse():
     ap.add_argument("--verify", default="deliver", choices=["deliver", "commit"],
                     help="deliver: a batch is handed out after its device CRC verdict landed (default); commit: "
                          "the verdict gates only its commit")
-    ap.add_argument("--coalesce", type=int, default=8, help="staged batches collated per kernel launch")
+    ap.add_argument("--coalesce", type=int, default=None,
+                    help="staged batches collated per kernel launch (default: the loader's, 6 for fixed width)")
     ap.add_argument("--coalesce-wait-us", type=int, default=50, help="adaptive coalescing wait while the GPU is busy")
     ap.add_argument("--no-numa", action="store_true", help="do not bind ranks to their GPU's NUMA node")
     ap.add_argument("--decode", default="auto", choices=["auto", "device", "host"],
@@ -678,7 +679,8 @@ def run_rank(args) -> int:
             slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
             in_order=args.in_order, h2d=h2d, copy_streams=args.copy_streams,
             **({"lockstep_depth": args.lockstep_depth} if args.lockstep_depth is not None else {}),
-            event_every=args.event_every, numa_bind=not args.no_numa, coalesce=args.coalesce,
+            event_every=args.event_every, numa_bind=not args.no_numa,
+            **({"coalesce": args.coalesce} if args.coalesce is not None else {}),
             coalesce_wait_us=args.coalesce_wait_us, decode=args.decode,
             lockstep=lockstep if lockstep_mode is None else lockstep_mode,
             mirror_chunk_mib=args.mirror_chunk_mib, commit=commit, verify=verify or args.verify,

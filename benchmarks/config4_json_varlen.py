@@ -43,6 +43,7 @@ def parse(argv=None):
     ap.add_argument("--event-every", type=int, default=None)
     ap.add_argument("--prefetch", type=int, default=2)
     ap.add_argument("--verify", default="deliver", choices=["deliver", "commit"])
+    ap.add_argument("--coalesce", type=int, default=None, help="batches per launch (default: the loader's)")
     ap.add_argument("--lockstep", default="off", choices=["off", "rccl"],
                     help="rccl: the per-step RCCL agreement at world 1 (a one-rank nccl group), as under DDP")
     return ap.parse_args(argv)
@@ -83,6 +84,7 @@ def run(args, sync=None) -> dict:
                           json_parse=args.json_parse, h2d=args.h2d, decode=args.decode, json_count=args.json_count,
                           slots_per_worker=args.slots_per_worker, event_every=args.event_every, prefetch=args.prefetch,
                           verify=args.verify, lockstep="always" if args.lockstep == "rccl" else True,
+                          **({"coalesce": args.coalesce} if args.coalesce else {}),
                           worker_init_fn=Json.init_worker("json", bootstrap_servers=url, group_id="cfg4",
                                                           auto_offset_reset="earliest"))
         it = iter(auto_commit(dl))

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--decode", default="auto", choices=["auto", "device", "host"])
     ap.add_argument("--h2d", default="auto", choices=["auto", "dma", "zerocopy"])
+    ap.add_argument("--coalesce", type=int, default=None, help="batches per launch (default: the loader's)")
     ap.add_argument("--lockstep", default="off", choices=["off", "rccl"],
                     help="rccl: the per-step RCCL agreement at world 1 (a one-rank nccl group), as under DDP")
     args = ap.parse_args()
@@ -65,6 +66,7 @@ def main():
             torch.distributed.all_reduce(torch.ones(1, device=args.device))  # torch's communicator, as DDP
         dl = DeviceLoader(Tokens.placeholder(), B, num_workers=args.workers, device=args.device, dtype=torch.int64,
                           decode=args.decode, h2d=args.h2d, lockstep="always" if args.lockstep == "rccl" else True,
+                          **({"coalesce": args.coalesce} if args.coalesce else {}),
                           worker_init_fn=Tokens.init_worker("tok", bootstrap_servers=url, group_id="tok",
                                                             auto_offset_reset="earliest"))
         it = iter(auto_commit(dl))

@@ -14,7 +14,7 @@ class Vec4(KafkaDataset):
 
 def test_defaults_are_valid_and_round_trip():
     c = LoaderConfig()
-    assert c.tuning.coalesce == 8 and c.sharding == "static"
+    assert c.tuning.coalesce is None and c.sharding == "static"  # None: 6 fixed-width device decode, else 8
     d = c.to_dict()
     assert LoaderConfig.from_dict(d) == c
     assert set(d) == LoaderConfig.field_names() | {"tuning"}

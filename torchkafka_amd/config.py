@@ -93,7 +93,9 @@ class Tuning:
         prefetch: batches whose H2D is issued ahead of the user (DMA mode).
         copy_streams: HIP side streams for DMA copies (1..8).
         event_every: record a completion event every k slots; None = ring slots / 4, at most 4.
-        coalesce: staged batches collated per kernel launch (1..8; 1 disables).
+        coalesce: staged batches collated per kernel launch (1..8; 1 disables).  None: 6 for fixed-width
+            device decode (steady 51.3-51.8 M rec/s against 49.5-50.3 M with 8, 20-step window +2 %), 8
+            otherwise (JSON 49.1-49.5 M against 44.7-46.6 M with 6; profiles/r05_s45_coalesce).
         coalesce_wait_us: how long to wait for a fuller group while the GPU is busy (0..10000).
         lockstep_depth: steps before its credits run out that the next cross-rank agreement is issued
             (0..64); None = auto: 32 under the RCCL lockstep with device decode (whose ring is then 64
@@ -124,7 +126,7 @@ class Tuning:
     prefetch: int = 2
     copy_streams: int = 4
     event_every: Optional[int] = None
-    coalesce: int = 8
+    coalesce: Optional[int] = None
     coalesce_wait_us: int = 50
     lockstep_depth: Optional[int] = None
     numa_bind: Optional[bool] = None
@@ -155,7 +157,7 @@ class Tuning:
         _check(0 <= int(self.prefetch) <= 64, "prefetch must be in [0, 64]")
         _check(1 <= int(self.copy_streams) <= 8, "copy_streams must be in [1, 8]")
         _check(self.event_every is None or 1 <= int(self.event_every) <= 4096, "event_every must be >= 1 (or None)")
-        _check(1 <= int(self.coalesce) <= 8, "coalesce must be in [1, 8]")
+        _check(self.coalesce is None or 1 <= int(self.coalesce) <= 8, "coalesce must be in [1, 8] (or None)")
         _check(0 <= int(self.coalesce_wait_us) <= 10_000, "coalesce_wait_us must be in [0, 10000]")
         _check(self.lockstep_depth is None or 0 <= int(self.lockstep_depth) <= 64, "lockstep_depth must be in [0, 64]")
         _check(self.ahead_depth is None or 0 <= int(self.ahead_depth) <= 16, "ahead_depth must be in [0, 16]")

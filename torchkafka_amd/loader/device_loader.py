@@ -242,7 +242,6 @@ class DeviceLoader(LoaderBridges, LoaderCommits, LoaderLockstep):
         self.prefetch = int(tun.prefetch)
         self.copy_streams = int(tun.copy_streams)
         self.event_every = None if tun.event_every is None else int(tun.event_every)
-        self.coalesce = int(tun.coalesce)
         self.coalesce_wait_us = int(tun.coalesce_wait_us)
         self.lockstep_depth = None if tun.lockstep_depth is None else int(tun.lockstep_depth)
         self.numa_bind = bool(tun.numa_bind)
@@ -256,6 +255,8 @@ class DeviceLoader(LoaderBridges, LoaderCommits, LoaderLockstep):
             json_parse=self.json_parse, synthetic_commits=self._commit_target_url()[0] != "",
             process_overridden=self._process_overridden(), return_info=self.return_info,
             drop_last=self.drop_last, json_count_mode=getattr(tun, "json_count", "auto"))
+        # fixed-width device decode: 6 batches per launch; JSON / var-len and the host paths: 8
+        self.coalesce = int(tun.coalesce) if tun.coalesce is not None else (6 if self.plan.span else 8)
         self._pending_wms: list = []   # finished-but-uncommitted watermark lists
         self._committed: dict[int, int] = {}
         # state_dict(global_step=True): every partition's position after the batches handed out
