@@ -100,20 +100,22 @@ def parse():
     ap.add_argument("--no-numa", action="store_true", help="do not bind ranks to their GPU's NUMA node")
     ap.add_argument("--decode", default="auto", choices=["auto", "device", "host"],
                     help="device: gfx950 RecordBatch decode + CRC from the pinned logs; host: workers CRC-check + pack")
-    ap.add_argument("--lockstep", default="auto", choices=["auto", "off", "rccl", "host"],
-                    help="cross-rank step/commit agreement: auto = RCCL at N > 1, none at N = 1; rccl/host force "
-                         "it (also at N = 1) over the native RCCL communicator / the process group's all-reduce")
+    ap.add_argument("--lockstep", default="auto", choices=["auto", "off", "rccl", "host", "shm"],
+                    help="cross-rank step/commit agreement: auto = the loader's choice at N > 1 (the node-local "
+                         "shared-memory transport on one host), none at N = 1; shm/rccl/host force it (also at "
+                         "N = 1) over shared memory / the native RCCL communicator / the process group's all-reduce")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on cuda:0 with a gloo group (rehearse N > 1 ranks on a one-GPU box)")
     ap.add_argument("--steady-steps", type=int, default=None,
                     help="steps of the steady-state block timed after the headline (default: max(50 x ring "
                          "slots, 50000) on a GPU, 2000 on the CPU; 0 skips it)")
-    ap.add_argument("--extra-blocks", default="dma,f32,label,rccl,rccl_sync,verify",
+    ap.add_argument("--extra-blocks", default="dma,f32,label,shm,shm_sync,rccl,rccl_sync,verify",
                     help="comma list of secondary steady blocks, each a fresh loader over the same topic: dma "
                          "(h2d='dma', HBM mirror filled by SDMA), f32 (float32 output), label (the record key as "
-                         "an int64 label beside the values: FixedWidth + Key()), rccl (the native RCCL lockstep "
-                         "forced at N = 1: the RCCL cost a one-GPU box shows), rccl_sync (the same with "
-                         "commit='sync': one agreement per step after every commit -- the cross-rank barrier), "
+                         "an int64 label beside the values: FixedWidth + Key()), shm (the node-local shared-memory "
+                         "lockstep, forced also at N = 1), shm_sync (the same with commit='sync': one agreement per "
+                         "step after every commit -- the cross-rank barrier), rccl / rccl_sync (the same over the "
+                         "native RCCL communicator), "
                          "verify (the other --verify mode: steady_unverified or steady_verified); '' for none")
     ap.add_argument("--extra-steps", type=int, default=None,
                     help="timed steps of each secondary block (default: the steady-state steps)")
@@ -258,7 +260,7 @@ class Rank:
 
     def init_group(self) -> None:
         dist = self.dist
-        if self.world > 1 or self.args.lockstep in ("rccl", "host"):
+        if self.world > 1 or self.args.lockstep in ("rccl", "host", "shm"):
             # no GPU touched yet: the loader forks its workers before HIP is initialised
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
@@ -606,11 +608,9 @@ def run_rank(args) -> int:
     if args.lockstep == "off":
         lockstep = False
     elif args.lockstep == "auto":
-        lockstep = "host" if args.same_device else True
-    elif world == 1:
-        lockstep = "always"  # agree every step even alone: RCCL on an nccl group, all-reduce on gloo
+        lockstep = True  # the loader's transport choice: shared memory when every rank is on this host
     else:
-        lockstep = args.lockstep
+        lockstep = args.lockstep  # a forced transport agrees every step, also at N = 1
 
     class Records(KafkaDataset):
         schema = FixedWidth(torch.float32, (args.dim,))
@@ -636,8 +636,8 @@ def run_rank(args) -> int:
     extra = [b for b in args.extra_blocks.split(",") if b]
     if device.type != "cuda":
         extra = [b for b in extra if b not in ("dma", "rccl", "rccl_sync", "verify")]
-    if world > 1:  # the main blocks run the lockstep already (RCCL on GPUs)
-        extra = [b for b in extra if b != "rccl"]
+    if args.same_device:  # several ranks on one GPU: RCCL needs a device per rank
+        extra = [b for b in extra if b not in ("rccl", "rccl_sync")]
     extra_steps = args.extra_steps if args.extra_steps is not None else steady
     if extra_steps <= 0:
         extra = []
@@ -746,22 +746,25 @@ def run_rank(args) -> int:
         dt = torch.float32 if name == "f32" else dtypes[args.dtype]
         own_group = False
         rccl_block = name in ("rccl", "rccl_sync")
-        if rccl_block and not dist.is_initialized() and os.environ.get("TK_BENCH_NO_TORCH_NCCL") != "1":
+        shm_block = name in ("shm", "shm_sync")
+        if (rccl_block or shm_block) and not dist.is_initialized() and os.environ.get("TK_BENCH_NO_TORCH_NCCL") != "1":
             # a world-1 nccl group; one all-reduce on it makes torch's own RCCL communicator and its
             # streams, as a DDP job's gradient all-reduce does at N > 1 -- the N = 8 queue layout,
-            # rehearsed on one GPU (the loader's private communicator carries every agreement)
+            # rehearsed on one GPU (the loader's own transport carries every agreement)
             os.environ["MASTER_ADDR"] = "127.0.0.1"
             os.environ["MASTER_PORT"] = str(_free_port())
-            dist.init_process_group("nccl", rank=0, world_size=1)
+            on_gpu = device.type == "cuda"
+            dist.init_process_group("nccl" if on_gpu else "gloo", rank=0, world_size=1)
             dist.all_reduce(torch.ones(1, device=device))
-            torch.cuda.synchronize(device)
-            os.environ["TORCHKAFKA_TORCH_NCCL_ACTIVE"] = "1"
+            if on_gpu:
+                torch.cuda.synchronize(device)
+                os.environ["TORCHKAFKA_TORCH_NCCL_ACTIVE"] = "1"
             own_group = True
         ld = make_loader(f"bench-{name}", dt, "dma" if name == "dma" else args.h2d,
                          ds=Labelled if name == "label" else Records,
                          verify=other_verify if name == "verify" else None,
-                         commit="sync" if name == "rccl_sync" else "async",
-                         lockstep_mode="always" if rccl_block and world == 1 else None)
+                         commit="sync" if name in ("rccl_sync", "shm_sync") else "async",
+                         lockstep_mode="rccl" if rccl_block else "shm" if shm_block else None)
         eit = iter(auto_commit(ld))
         for _ in range(extra_warm):
             next(eit)
@@ -775,10 +778,11 @@ def run_rank(args) -> int:
         blk["h2d"], blk["decode"] = describe(ld)
         blk["verify"] = ld.verify
         key = f"steady_{name}"
-        if rccl_block:
+        if rccl_block or shm_block:
             st = eres["stats"]
-            blk["commit"] = "sync (commit, then the agreement: a cross-rank barrier per step)" if name == "rccl_sync" \
-                else "async (commits land at agreements)"
+            blk["commit"] = ("sync (commit, then the agreement: a cross-rank barrier per step)"
+                             if name.endswith("_sync") else "async (commits land at agreements)")
+            blk["commits_per_step"] = round(st["commits"] / max(1, extra_steps), 4)
             blk["batches_per_commit"] = round(extra_steps / max(1, st["commits"]), 2)
             blk["lockstep"] = dict(ld.lockstep_info)
             blk["lockstep_agreements"] = st.get("lockstep_agreements", 0)

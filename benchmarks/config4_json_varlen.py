@@ -83,7 +83,7 @@ def run(args, sync=None) -> dict:
         dl = DeviceLoader(Json.placeholder(), B, num_workers=args.workers, device=args.device, dtype=torch.bfloat16,
                           json_parse=args.json_parse, h2d=args.h2d, decode=args.decode, json_count=args.json_count,
                           slots_per_worker=args.slots_per_worker, event_every=args.event_every, prefetch=args.prefetch,
-                          verify=args.verify, lockstep="always" if args.lockstep == "rccl" else True,
+                          verify=args.verify, lockstep="rccl" if args.lockstep == "rccl" else True,
                           **({"coalesce": args.coalesce} if args.coalesce else {}),
                           worker_init_fn=Json.init_worker("json", bootstrap_servers=url, group_id="cfg4",
                                                           auto_offset_reset="earliest"))

@@ -65,7 +65,7 @@ def main():
             torch.distributed.init_process_group("nccl", rank=0, world_size=1)
             torch.distributed.all_reduce(torch.ones(1, device=args.device))  # torch's communicator, as DDP
         dl = DeviceLoader(Tokens.placeholder(), B, num_workers=args.workers, device=args.device, dtype=torch.int64,
-                          decode=args.decode, h2d=args.h2d, lockstep="always" if args.lockstep == "rccl" else True,
+                          decode=args.decode, h2d=args.h2d, lockstep="rccl" if args.lockstep == "rccl" else True,
                           **({"coalesce": args.coalesce} if args.coalesce else {}),
                           worker_init_fn=Tokens.init_worker("tok", bootstrap_servers=url, group_id="tok",
                                                             auto_offset_reset="earliest"))

@@ -120,3 +120,40 @@ def test_global_step_checkpoint_resumes_exactly_once(broker, tmp_path, world, st
     if dry:
         for p in range(0, n_parts, world):
             assert {int(q): o for q, o in st2["offsets"]["t"].items()}[p] == per_part[p]
+
+
+def _groups_main(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    from torchkafka_amd.loader.commits import LoaderCommits
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pair = dist.new_group(ranks=[0, 1])
+    holder = LoaderCommits.__new__(LoaderCommits)
+    real = dist.get_backend
+    dist.get_backend = lambda g=None: "nccl"  # as under an RCCL job: the gloo groups are made aside
+    try:
+        a = holder._cpu_group(None)
+        b = holder._cpu_group(pair)  # new_group: every rank of the job takes part, members or not
+        b = b if rank < 2 else None
+        a2 = holder._cpu_group(None)
+    finally:
+        dist.get_backend = real
+    out = {"a": dist.get_world_size(a), "same": a is a2,
+           "b": dist.get_world_size(b) if b is not None else None, "distinct": b is not a}
+    with open(os.path.join(outdir, f"g{rank}.json"), "w") as f:
+        json.dump(out, f)
+    dist.destroy_process_group()
+
+
+def test_cpu_group_is_keyed_by_the_ranks(tmp_path):
+    """the gloo group used for state_dict(global_step=True) was cached once and
+    returned for any later ``group``; it is now one per rank list."""
+    import torch.multiprocessing as mp
+
+    mp.start_processes(_groups_main, args=(3, _free_port(), str(tmp_path)), nprocs=3, join=True, start_method="fork")
+    res = [json.load(open(tmp_path / f"g{r}.json")) for r in range(3)]
+    assert all(r["a"] == 3 and r["same"] for r in res)
+    assert [r["b"] for r in res] == [2, 2, None] and all(r["distinct"] for r in res)

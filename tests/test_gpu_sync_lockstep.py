@@ -1,6 +1,8 @@
 """commit='sync' under the cross-rank lockstep on the native (GPU) step driver: two ranks on one
-MI355X over a gloo group (the driver's CreditLockstep in sync mode; RCCL refuses two ranks on one
-device, so the RCCL transport is covered at world 1 in test_zz_gpu_rccl.py).
+MI355X over a gloo group (the driver's CreditLockstep in sync mode), agreeing through the group's
+all-reduce ('host') or the node-local shared-memory transport ('shm', csrc/core/shm_lockstep.h).
+RCCL refuses two ranks on one device, so the RCCL transport is covered at world 1 in
+test_zz_gpu_rccl.py.
 
 The reference's contract (auto_commit.py:55-58, kafka_dataset.py:130): batch k's commit completes
 before batch k+1 is handed out.  Under DDP that commit is a barrier: each rank commits k, then the
@@ -34,7 +36,7 @@ def batch_ends(x) -> dict:
     return out
 
 
-def _rank_main(rank, world, url, port, outdir, verify):
+def _rank_main(rank, world, url, port, outdir, verify, transport="host"):
     import torch.distributed as dist
 
     from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
@@ -49,7 +51,7 @@ def _rank_main(rank, world, url, port, outdir, verify):
 
     b = open_broker(url)
     dl = DeviceLoader(Vec.placeholder(), 32, num_workers=2, device="cuda:0", dtype=torch.float32, commit="sync",
-                      lockstep="host", verify=verify,
+                      lockstep=transport, verify=verify,
                       worker_init_fn=Vec.init_worker("t", bootstrap_servers=url, group_id="gs",
                                                      auto_offset_reset="earliest", consumer_timeout_ms=500))
     want: dict = {}
@@ -75,8 +77,9 @@ def _rank_main(rank, world, url, port, outdir, verify):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("verify", ["deliver", "commit"])
-def test_sync_commit_barrier_two_ranks_one_gpu(broker, tmp_path, verify):
+@pytest.mark.parametrize("verify,transport", [("deliver", "host"), ("commit", "host"), ("deliver", "shm"),
+                                               ("commit", "shm")])
+def test_sync_commit_barrier_two_ranks_one_gpu(broker, tmp_path, verify, transport):
     import torch.multiprocessing as tmp
 
     world = 2
@@ -86,7 +89,7 @@ def test_sync_commit_barrier_two_ranks_one_gpu(broker, tmp_path, verify):
         broker.fill("t", 240 - 48 * (p % 2 == 0), "fixed_f32", size=16, partitions=[p], records_per_batch=16)
     ctx = tmp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, broker.url, port, str(tmp_path), verify))
+    procs = [ctx.Process(target=_rank_main, args=(r, world, broker.url, port, str(tmp_path), verify, transport))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -116,3 +119,48 @@ def test_sync_commit_barrier_two_ranks_one_gpu(broker, tmp_path, verify):
     assert bad == [], bad[:5]
     committed = broker.committed_offsets("gs", "t")
     assert committed[0] + committed[2] == 384 and committed[1] + committed[3] == 384, committed
+
+
+def test_shm_lockstep_native_driver_world1_sync_and_async(broker):
+    """The node-local shared-memory transport through the native driver at world size 1 (forced
+    lockstep='shm' over a world-1 gloo group): sync mode commits every batch before the next is
+    handed out; async mode with commit_every=2 commits at least every few batches."""
+    import torch.distributed as dist
+
+    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
+
+    class Vec(KafkaDataset):
+        schema = FixedWidth(torch.float32, (8,))
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        broker.create_topic("t", 2)
+        broker.fill("t", 400, "fixed_f32", size=8, records_per_batch=10)
+        for commit in ("sync", "async"):
+            dl = DeviceLoader(Vec.placeholder(), 20, num_workers=2, device="cuda:0", lockstep="shm", commit=commit,
+                              dtype=torch.float32, lockstep_commit_every=2,
+                              worker_init_fn=Vec.init_worker("t", bootstrap_servers=broker.url, group_id=f"g{commit}",
+                                                             auto_offset_reset="earliest", consumer_timeout_ms=300))
+            want, steps, lag = {}, 0, []
+            for x in auto_commit(dl):
+                if steps:
+                    got = {p: o for p, o in broker.committed_offsets(f"g{commit}", "t").items() if p in want}
+                    lag.append(sum(want[p] - got.get(p, 0) for p in want))
+                for p, e in batch_ends(x).items():
+                    want[p] = max(want.get(p, 0), e)
+                steps += 1
+            info = dict(dl.lockstep_info)
+            st = dl.stats_summary()
+            dl.close()
+            assert info.get("transport") == "shm", info
+            assert steps == 40
+            if commit == "sync":
+                assert lag == [0] * 39, lag  # batch k committed when k+1 is handed out
+            else:
+                assert max(lag) <= 20 * 8, lag  # at most a few batches of 20 records behind
+                assert st["commits"] >= steps // 4, st["commits"]
+            assert broker.committed_offsets(f"g{commit}", "t") == {0: 400, 1: 400}
+    finally:
+        dist.destroy_process_group()

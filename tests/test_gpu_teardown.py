@@ -51,3 +51,69 @@ def test_close_one_loader_while_another_and_a_user_kernel_run(broker):
     assert res["user_kernel_ms_max"] < 2.5 * res["user_kernel_ms_min"] + 5, res
     # the deferred releases all ran once the device was free
     assert res["reaper_drained"] and res["reaper"]["released"] == res["reaper"]["posted"] > 0
+
+
+@pytest.mark.timeout(180)
+def test_reopen_dma_loader_over_the_same_logs_while_user_work_is_queued(broker):
+    """a dma loader closed while the user's stream holds queued kernels hands its log
+    registrations to the deferred-release thread; a loader (and a new iteration of the same loader)
+    over the same topic right after must pin those logs without waiting for them.  Each driver maps
+    the broker afresh (the release keeps the old mapping alive), so the new registrations are of
+    other addresses; a registration that still finds its pages registered drains the releases and
+    retries (csrc/hip/log_pins.cpp pin_some, counted as log_register_retries)."""
+    import torch
+
+    from torchkafka_amd import DeviceLoader, FixedWidth, KafkaDataset, auto_commit
+
+    class Vec(KafkaDataset):
+        schema = FixedWidth(torch.float32, (256,))
+
+    broker.create_topic("t", 4)
+    broker.fill("t", 20000, "fixed_f32", size=256, records_per_batch=64)
+    dev = torch.device("cuda:0")
+
+    def loader(group):
+        return DeviceLoader(Vec.placeholder(), 256, num_workers=2, device=dev, dtype=torch.bfloat16, h2d="dma",
+                            decode="device",
+                            worker_init_fn=Vec.init_worker("t", bootstrap_servers=broker.url, group_id=group,
+                                                           auto_offset_reset="earliest", consumer_timeout_ms=2000))
+
+    user = torch.cuda.Stream(dev)
+    done = torch.cuda.Event()
+
+    def queue_user_work():
+        with torch.cuda.stream(user):
+            for _ in range(20):
+                torch.cuda._sleep(5_000_000)
+            done.record()
+
+    a = loader("a")
+    seen = {}
+    it = iter(auto_commit(a))
+    for _ in range(20):
+        x = next(it)
+    queue_user_work()
+    it.close()  # end of the first iteration: its run's releases are deferred behind the user's work
+    it = iter(auto_commit(a))  # a new iteration of the same loader
+    for _ in range(20):
+        x = next(it)
+        for row in x.float()[:, :2].tolist():
+            seen.setdefault(int(row[1]), []).append(int(row[0]))
+    st_a = dict(a._run.driver.stats())
+    it.close()
+    a.close()
+    b = loader("b")  # a new loader over the same logs, the user's work still queued
+    n = 0
+    for x in auto_commit(b):
+        n += x.shape[0]
+        if n >= 20 * 256:
+            break
+    st_b = dict(b._run.driver.stats())
+    b.close()
+    user_busy = not done.query()
+    done.synchronize()
+    print({"retries": (st_a.get("log_register_retries"), st_b.get("log_register_retries")), "user_busy": user_busy})
+    assert n >= 20 * 256
+    # the second iteration resumed at the first one's committed offsets: contiguous per partition
+    for p, offs in seen.items():
+        assert offs == sorted(offs) and len(set(offs)) == len(offs), p

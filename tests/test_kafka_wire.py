@@ -482,6 +482,114 @@ def test_compressed_topic_streams_through_a_ring_replica(broker, server, compres
     assert br._r.inflate_threads >= 1  # the pipelined path ran
 
 
+def _batch_spans(raw: bytes) -> list[tuple[int, int]]:
+    """(base offset, next offset) of every RecordBatch of a log, in log order."""
+    out, o = [], 0
+    while len(raw) - o >= 61:
+        total = int.from_bytes(raw[o + 8:o + 12], "big") + 12
+        base = int.from_bytes(raw[o:o + 8], "big")
+        out.append((base, base + int.from_bytes(raw[o + 23:o + 27], "big") + 1))
+        o += total
+    return out
+
+
+def _assert_contiguous(b: SyntheticBroker, topic: str, p: int, start: int, end: int) -> None:
+    spans = _batch_spans(log_bytes(b, topic, p))
+    assert spans, f"{topic}-{p}: empty replica"
+    assert spans[0][0] <= start < spans[0][1] or spans[0][0] == start, (p, spans[0], start)
+    for (_, n0), (b1, _) in zip(spans, spans[1:]):
+        assert b1 == n0, f"{topic}-{p}: gap or overlap in the replica log at {n0} -> {b1}"
+    assert spans[-1][1] == end, (p, spans[-1], end)
+
+
+def _mixed_compressibility_topic(broker, topic: str, n_parts: int, n: int, noisy: range, codec: str) -> None:
+    """Records f32[64] = (offset, partition, payload) in batches of 40, the payload zeros (lz4 /
+    zstd shrink it ~10x) except for offsets in ``noisy``, random bytes (they grow when compressed): the
+    inflation ratio the replicator learns crosses 1 and back while record sets are in flight."""
+    import numpy as np
+
+    rng = np.random.default_rng(7)
+    broker.create_topic("src-" + topic, n_parts)
+    for p in range(n_parts):
+        for b0 in range(0, n, 40):
+            rows = np.zeros((min(40, n - b0), 64), np.float32)
+            rows[:, 0] = np.arange(b0, b0 + len(rows))
+            rows[:, 1] = p
+            for i, o in enumerate(range(b0, b0 + len(rows))):
+                if o in noisy:  # random bytes: lz4 / zstd output is larger than its input
+                    rows[i, 2:] = rng.integers(0, 256, 62 * 4, dtype=np.uint8).view(np.float32)
+            broker.produce("src-" + topic, [r.tobytes() for r in rows], partition=p)
+    broker.create_topic(topic, n_parts)
+    broker.copy_compressed("src-" + topic, topic, codec)
+
+
+@pytest.mark.parametrize("compression", ["lz4", "zstd"])
+def test_compression_ratio_crossing_one_keeps_the_replica_in_order(broker, server, compression, monkeypatch):
+    """while compressed record sets wait for the inflater, later sets are asked for
+    from past them; a set that inflates to less than its wire size used to take the synchronous path
+    and be stored first, and the inflater then dropped the earlier sets as already held -- a silent
+    gap.  Every set now queues behind the ones in flight, so each partition's replica stays
+    contiguous and every record arrives once, in order."""
+    noisy = [o for o in range(3000) if (o // 120) % 2]  # the ratio crosses 1 every 3 batches
+    # a slow inflater keeps kMaxInflight sets queued: the case that lost records
+    monkeypatch.setenv("TORCHKAFKA_TEST_INFLATE_DELAY_US", "1500")
+    _mixed_compressibility_topic(broker, "t", 2, 3000, noisy, compression)
+    with bridge(server, group_id="g", ring_bytes=256 << 10, max_partition_fetch_bytes=16 << 10) as br:
+        dl = DeviceLoader(Vec64.placeholder(), 50, device="cpu", num_workers=2,
+                          worker_init_fn=Vec64.init_worker("t", bootstrap_servers=br.url, group_id="g",
+                                                           auto_offset_reset="earliest", consumer_timeout_ms=1000))
+        rows = torch.cat(list(auto_commit(dl)))
+        assert br.errors == 0, br.last_error()
+        assert br.out_of_order == 0
+    assert rows.shape == (6000, 64)
+    for part in (0, 1):
+        offs = rows[rows[:, 1] == part][:, 0].tolist()
+        assert offs == [float(i) for i in range(3000)]
+
+
+def test_rebalance_while_compressed_sets_are_in_flight(broker, server):
+    """a partition restarted by a rebalance while record sets asked for at its old
+    position still wait for the inflater.  Those sets are dropped (assignment epoch and pipeline
+    generation); each member's replica of each partition it owns ends up contiguous from where its
+    ownership started to the end of the topic."""
+    _mixed_compressibility_topic(broker, "t", 4, 6000, range(2000, 3000), "lz4")
+    kw = dict(group_id="g", subscribe=True, heartbeat_interval_ms=20, session_timeout_ms=3000,
+              max_partition_fetch_bytes=8 << 10, ring_bytes=0)  # linear logs: nobody consumes here
+    first = bridge(server, **kw)
+    try:
+        assert sorted(first.assignment) == [0, 1, 2, 3]
+        first.local.commit("g", {TopicPartition("t", p): 100 for p in range(4)})
+        second = bridge(server, **kw)  # joins while first is still fetching the compressed topic
+        try:
+            assert wait_for(lambda: len(first.assignment) == 2, 5)
+            assert first.wait_caught_up(20) and second.wait_caught_up(20)
+            assert first.errors == 0 and second.errors == 0, (first.last_error(), second.last_error())
+            for br in (first, second):
+                for s in br.stats():
+                    if s["owned"]:
+                        _assert_contiguous(br.local, "t", s["partition"], s["start_offset"], 6000)
+        finally:
+            second.close()
+        assert wait_for(lambda: sorted(first.assignment) == [0, 1, 2, 3], 5) and first.wait_caught_up(20)
+        for s in first.stats():
+            _assert_contiguous(first.local, "t", s["partition"], s["start_offset"], 6000)
+        assert first.errors == 0, first.last_error()
+    finally:
+        first.close()
+
+
+def test_ring_replica_grows_its_reservation_for_a_first_batch_that_inflates_past_it(broker, server):
+    """A ring replica reserves room for a Fetch by the inflation ratio learnt so far (none at the
+    start): a first compressed batch that inflates to more than max_partition_fetch_bytes never fit
+    the reservation, and the partition stalled with nothing stored.  The reservation now doubles
+    until the batch fits."""
+    _mixed_compressibility_topic(broker, "t", 1, 400, range(0), "lz4")  # 457 B batches -> 10.7 KiB
+    with bridge(server, group_id="g", ring_bytes=1 << 20, max_partition_fetch_bytes=4096) as br:
+        assert wait_for(lambda: br.local.end_offset("t", 0) == 400, 10), br.stats()[0]
+        assert br.errors == 0, br.last_error()
+        _assert_contiguous(br.local, "t", 0, 0, 400)
+
+
 def test_compress_round_trips_through_the_native_decoders():
     data = bytes(range(256)) * 300 + b"tail" * 1000
     for codec in (1, 3, 4):

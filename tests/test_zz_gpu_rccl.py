@@ -33,7 +33,7 @@ def test_native_rccl_lockstep_driver_world1(broker):
         broker.create_topic("t", 2)
         broker.fill("t", 95, "fixed_f32", size=8)
         for depth in (0, 1, 3):
-            dl = DeviceLoader(Vec.placeholder(), 20, num_workers=2, device="cuda:0", lockstep="always",
+            dl = DeviceLoader(Vec.placeholder(), 20, num_workers=2, device="cuda:0", lockstep="rccl",
                               lockstep_depth=depth,
                               worker_init_fn=Vec.init_worker("t", bootstrap_servers=broker.url, group_id=f"g{depth}",
                                                              auto_offset_reset="earliest", consumer_timeout_ms=300))
@@ -75,7 +75,7 @@ def test_rccl_lockstep_transport_failure_detection_plumbing():
 
 
 def test_native_rccl_lockstep_sync_commit_world1(broker):
-    """commit='sync' through the RCCL lockstep (world 1, lockstep='always'): one agreement per step
+    """commit='sync' through the RCCL lockstep (world 1, lockstep='rccl'): one agreement per step
     makes batch k committable before batch k+1 is handed out, and k's offsets are stored then."""
     import os
 
@@ -94,7 +94,7 @@ def test_native_rccl_lockstep_sync_commit_world1(broker):
     try:
         broker.create_topic("t", 2)
         broker.fill("t", 200, "fixed_f32", size=8, records_per_batch=10)
-        dl = DeviceLoader(Vec.placeholder(), 20, num_workers=2, device="cuda:0", lockstep="always", commit="sync",
+        dl = DeviceLoader(Vec.placeholder(), 20, num_workers=2, device="cuda:0", lockstep="rccl", commit="sync",
                           dtype=torch.float32,
                           worker_init_fn=Vec.init_worker("t", bootstrap_servers=broker.url, group_id="gsync",
                                                          auto_offset_reset="earliest", consumer_timeout_ms=300))

@@ -276,6 +276,11 @@ class KafkaBridge:
         return int(self._r.rebalances)
 
     @property
+    def out_of_order(self) -> int:
+        """Record sets dropped (and refetched) because they did not start at the replica log's end."""
+        return int(self._r.out_of_order)
+
+    @property
     def member_id(self) -> str:
         return str(self._r.member_id)
 

@@ -101,6 +101,11 @@ class Tuning:
             (0..64); None = auto: 32 under the RCCL lockstep with device decode (whose ring is then 64
             slots per worker deep, so an agreement's ~60-180 µs round trip is covered by the steps
             its credits still allow: profiles/r05_s24), else 2.
+        lockstep_commit_every: async lockstep: an agreement grants at most this many batches and a
+            fresh one is issued every half of it (a few in flight), so finished batches become
+            committable at least that often (0..4096; 0: one agreement grants whatever every rank
+            holds).  None = auto: 4 on the node-local shared-memory transport (an agreement costs
+            well under a microsecond), 32 under RCCL, 0 over a process group's all-reduce.
         numa_bind: bind the loader (and its workers) to the target GPU's socket.
         ahead_depth: device-decode groups launched ahead of the user's request (0..16); None = 4.
         decode_streams: HIP streams for the device decode kernels (1..4); None = 3.
@@ -129,6 +134,7 @@ class Tuning:
     coalesce: Optional[int] = None
     coalesce_wait_us: int = 50
     lockstep_depth: Optional[int] = None
+    lockstep_commit_every: Optional[int] = None
     numa_bind: Optional[bool] = None
     ahead_depth: Optional[int] = None
     decode_streams: Optional[int] = None
@@ -160,6 +166,8 @@ class Tuning:
         _check(self.coalesce is None or 1 <= int(self.coalesce) <= 8, "coalesce must be in [1, 8] (or None)")
         _check(0 <= int(self.coalesce_wait_us) <= 10_000, "coalesce_wait_us must be in [0, 10000]")
         _check(self.lockstep_depth is None or 0 <= int(self.lockstep_depth) <= 64, "lockstep_depth must be in [0, 64]")
+        _check(self.lockstep_commit_every is None or 0 <= int(self.lockstep_commit_every) <= 4096,
+               "lockstep_commit_every must be in [0, 4096]")
         _check(self.ahead_depth is None or 0 <= int(self.ahead_depth) <= 16, "ahead_depth must be in [0, 16]")
         _check(self.decode_streams is None or 1 <= int(self.decode_streams) <= 4, "decode_streams must be in [1, 4]")
         _check(0 <= int(self.worker_spin_us) <= 100_000, "worker_spin_us must be in [0, 100000]")
@@ -239,8 +247,8 @@ class LoaderConfig:
             if v not in choices:
                 raise ValueError(f"{name} must be {_CHOICE_HELP.get(name, ' or '.join(map(repr, choices)))}")
         _check(self.bridge in ("auto", True, False), "bridge must be 'auto', True or False")
-        _check(self.lockstep in (True, False, "host", "rccl", "always"),
-               "lockstep must be True, False, 'host', 'rccl' or 'always'")
+        _check(self.lockstep in (True, False, "host", "rccl", "shm", "always"),
+               "lockstep must be True, False, 'host', 'rccl', 'shm' or 'always'")
         _check(self.pad_to is None or int(self.pad_to) >= 1, "pad_to must be >= 1 (or None)")
         _check(int(self.pad_multiple) >= 1, "pad_multiple must be >= 1")
         _check(float(self.timeout) >= 0, "timeout must be >= 0 (0 waits forever)")

@@ -1,5 +1,6 @@
 // `torchkafka_amd._tkcore` bindings: the cross-rank credit lockstep (csrc/core/lockstep.h).
 #include "bindings_common.h"
+#include "bind_shm_lockstep.h"
 
 namespace tkbind {
 
@@ -10,6 +11,7 @@ void bind_lockstep(py::module_& m) {
   py::class_<PyLockstepTransport, LockstepTransport>(m, "PyLockstepTransport", py::module_local())
       .def(py::init<py::function>(), py::arg("allreduce_min"),
            "allreduce_min(credit, step, -step, commit_status) -> the 4 words' MIN over the ranks");
+  tkbind_shm::bind_shm_lockstep<LockstepTransport>(m);
   m.attr("LOCKSTEP_WORDS") = kLockstepWords;
   m.attr("COMMIT_OK") = kCommitOk;
   m.attr("COMMIT_FAILED") = kCommitFailed;
@@ -36,6 +38,8 @@ void bind_lockstep(py::module_& m) {
           py::arg("index"), py::arg("watermarks"))
       .def("finish", &CreditLockstep::finish)
       .def("set_sync", &CreditLockstep::set_sync, py::arg("sync"))
+      .def("set_commit_every", &CreditLockstep::set_commit_every, py::arg("n"),
+           "async mode: an agreement grants at most n batches (0: no cap)")
       .def("set_commit_status", &CreditLockstep::set_commit_status, py::arg("status"),
            "sync mode: 2 committed, 1 CommitFailedError swallowed, 0 the commit raised")
       .def_property_readonly("group_commit_status", &CreditLockstep::group_commit_status)

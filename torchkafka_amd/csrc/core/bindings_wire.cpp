@@ -121,6 +121,7 @@ void bind_wire(py::module_& m) {
       .def_property_readonly("fenced", &Replicator::fenced)
       .def_property_readonly("assignment_epoch", &Replicator::assignment_epoch)
       .def_property_readonly("rebalances", &Replicator::rebalances)
+      .def_property_readonly("out_of_order", &Replicator::out_of_order)
       .def("assignment_epochs", &Replicator::assignment_epochs,
            "[(partition, epoch at which it was (re)assigned)] of the partitions owned now")
       .def_property_readonly("fetch_threads", &Replicator::fetch_threads)

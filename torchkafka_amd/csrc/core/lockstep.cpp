@@ -1,5 +1,6 @@
 #include "lockstep.h"
 
+#include <algorithm>
 #include <string>
 
 namespace tk {
@@ -11,7 +12,12 @@ int64_t CreditLockstep::credit(LockstepSource& src) const {
 }
 
 void CreditLockstep::issue(LockstepSource& src) {
-  const int64_t w[kLockstepWords] = {credit(src), step_, -step_, commit_status_};
+  int64_t c = credit(src);
+  // commit_every: never grant past step + commit_every (granted_ is this ticket's base)
+  if (commit_every_ > 0 && !sync_ && c > step_ + commit_every_ - granted_)
+    c = std::max<int64_t>(0, step_ + commit_every_ - granted_);
+  last_issue_step_ = step_;
+  const int64_t w[kLockstepWords] = {c, step_, -step_, commit_status_};
   commit_status_ = kCommitOk;
   const auto t0 = std::chrono::steady_clock::now();
   tickets_.push_back(Ticket{step_, granted_, t_->issue(w)});
@@ -19,17 +25,16 @@ void CreditLockstep::issue(LockstepSource& src) {
   ++agreements_;
 }
 
-void CreditLockstep::settle() {
-  const Ticket t = tickets_.front();
-  tickets_.pop_front();
-  int64_t res[kLockstepWords];
+void CreditLockstep::observe(Ticket& t) {
+  if (t.observed) return;
   const auto w0 = std::chrono::steady_clock::now();
-  t_->wait(t.ticket, res);
+  t_->wait(t.ticket, t.res);
   const int64_t waited =
       std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
   wait_ns_ += waited;
   step_wait_ns_ += waited;
-  if (t.step > settled_step_) settled_step_ = t.step;
+  t.observed = true;
+  const int64_t* res = t.res;
   if (res[1] != -res[2])
     throw LockstepError("lockstep: ranks are out of step (min " + std::to_string(res[1]) + ", max " +
                         std::to_string(-res[2]) + ")");
@@ -38,10 +43,19 @@ void CreditLockstep::settle() {
   if (res[3] <= kCommitFatal)
     throw LockstepError("lockstep: a rank's commit before step " + std::to_string(t.step) +
                         " failed; every rank stops at this step");
+  // completion proves every rank reached t.step: the batches before it are finished everywhere
   while (!finished_q_.empty() && finished_q_.front().first < t.step) {
     emit(std::move(finished_q_.front().second));
     finished_q_.pop_front();
   }
+}
+
+void CreditLockstep::settle() {
+  observe(tickets_.front());
+  const Ticket t = tickets_.front();
+  tickets_.pop_front();
+  const int64_t* res = t.res;
+  if (t.step > settled_step_) settled_step_ = t.step;
   if (res[0] < 0)
     no_more_credit_ = true;
   else if (t.base + res[0] > granted_)
@@ -65,9 +79,24 @@ int CreditLockstep::next_impl(LockstepSource& src, int64_t timeout_ms) {
       issue(src);
       settle();
     }
-  } else if (tickets_.empty() && !no_more_credit_ && granted_ - step_ <= depth_ && step_ < granted_) {
-    // issue ahead while credits remain, so the round trip overlaps the delivery of granted batches
-    issue(src);
+  } else {
+    // agreements already back: their batches become committable now, in issue order (local: the
+    // grants are applied where every rank applies them, below)
+    for (auto& t : tickets_) {
+      if (t.observed) continue;
+      if (!t_->ready(t.ticket)) break;
+      observe(t);
+    }
+    const bool low = tickets_.empty() && granted_ - step_ <= depth_;
+    // commit_every: a fresh agreement every commit_every / 2 steps, a few in flight, so batches
+    // become committable at that cadence without the host ever waiting for one round trip.  Every
+    // input to this decision (step, applied grant, tickets issued) is the same on every rank.
+    const bool cadence = commit_every_ > 0 && int(tickets_.size()) < kMaxInflight &&
+                         step_ - last_issue_step_ >= std::max(1, commit_every_ / 2);
+    if (!no_more_credit_ && step_ < granted_ && (low || cadence)) {
+      // issue ahead while credits remain, so the round trip overlaps the delivery of granted batches
+      issue(src);
+    }
   }
   while (step_ >= granted_) {
     if (no_more_credit_) {

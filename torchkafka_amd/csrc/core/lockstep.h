@@ -53,6 +53,8 @@ class LockstepTransport {
   virtual ~LockstepTransport() = default;
   virtual int issue(const int64_t in[kLockstepWords]) = 0;
   virtual void wait(int ticket, int64_t out[kLockstepWords]) = 0;
+  // wait(ticket) would return at once (a transport that computes the result in issue(): always)
+  virtual bool ready(int ticket) { return true; }
 };
 
 class LockstepError : public std::runtime_error {
@@ -103,6 +105,11 @@ class CreditLockstep {
   void set_on_committable(std::function<void(std::vector<Watermark>&&)> f) { on_commit_ = std::move(f); }
   // Sync mode (see above).  Every rank must use the same mode: it decides which collectives run.
   void set_sync(bool s) { sync_ = s; }
+  // Async mode: an agreement grants at most `n` batches (0: whatever every rank holds), so one is
+  // issued at least every n steps and finished batches become committable that often.  Every rank
+  // must use the same value.
+  void set_commit_every(int n) { commit_every_ = n < 0 ? 0 : n; }
+  int commit_every() const { return commit_every_; }
   bool sync() const { return sync_; }
 
   int64_t step() const { return step_; }
@@ -126,11 +133,17 @@ class CreditLockstep {
     int64_t step;  // step at which it was issued
     int64_t base;  // granted at issue time
     int ticket;
+    bool observed = false;  // its result was read (committable batches emitted), grant not applied
+    int64_t res[kLockstepWords] = {0, 0, 0, 0};
   };
   int next_impl(LockstepSource& src, int64_t timeout_ms);
   int64_t credit(LockstepSource& src) const;
   void issue(LockstepSource& src);
   void settle();
+  // Reads the front ticket's result (blocking unless the transport says it is ready) and emits the
+  // batches it made committable.  The grant is applied by settle() only, at a step every rank
+  // reaches with the same state -- observing early is local and never changes what is issued.
+  void observe(Ticket& t);
   void emit(std::vector<Watermark>&& wms) {
     if (on_commit_) on_commit_(std::move(wms));
   }
@@ -139,6 +152,9 @@ class CreditLockstep {
   int depth_;
   int64_t step_ = 0, granted_ = 0;
   bool stopped_ = false, no_more_credit_ = false, sync_ = false;
+  int commit_every_ = 0;
+  int64_t last_issue_step_ = -1;
+  static constexpr int kMaxInflight = 3;  // agreements in flight under commit_every (transport slots >= 4)
   int64_t settled_step_ = -1;  // highest step an agreement was issued at and has completed
   int64_t commit_status_ = kCommitOk, group_status_ = kCommitOk;
   uint64_t group_failures_ = 0;

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <set>
 
 namespace tk {
@@ -161,6 +162,9 @@ void Replicator::start_parts(wire::Client& c, const std::vector<Part*>& ps, bool
     }
     p->start_offset = start;
     p->forwarded = remote_committed;
+    // sets still in flight for the old position are dropped (the fetch thread reads gen first)
+    p->ask_offset.store(p->fetch_offset.load(), std::memory_order_relaxed);
+    p->gen.fetch_add(1, std::memory_order_release);
     if (!cfg_.group.empty() && (!fresh || (remote_committed >= 0 && local_->committed(group_, p->pidx) < remote_committed))) {
       // the local table is where the replica's consumers resume: the group's offset (a partition
       // handed over by a rebalance starts where its last owner committed, not where we left it)
@@ -385,7 +389,12 @@ bool Replicator::throttled(Part& p) {
 void Replicator::reset_offset(wire::Client& c, Part& p) {
   const bool latest = cfg_.auto_offset_reset == "latest" || cfg_.auto_offset_reset == "largest";
   auto r = c.list_offsets(cfg_.topic, {p.partition}, latest ? -1 : -2);
-  p.fetch_offset = r.at(p.partition);
+  {
+    std::lock_guard<std::mutex> pg(p.mu);  // vs. the inflater storing a queued set
+    p.fetch_offset = r.at(p.partition);
+    p.ask_offset.store(p.fetch_offset.load(), std::memory_order_relaxed);
+    p.gen.fetch_add(1, std::memory_order_release);  // queued sets of the old position are dropped
+  }
   set_error("OffsetOutOfRangeError: " + cfg_.topic + "-" + std::to_string(p.partition) + " reset to offset " +
             std::to_string(p.fetch_offset.load()));
 }
@@ -456,6 +465,8 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
         std::vector<wire::FetchPartReq> req;
         std::map<int32_t, Part*> lookup;
         std::map<Part*, uint64_t> since;  // a partition restarted while its fetch was in flight drops the data
+        std::map<Part*, uint64_t> gens;   // ... and so does one whose position jumped (Part::gen)
+        std::map<Part*, int64_t> asked;   // the offset each partition was asked from
         for (Part* p : ps) {
           uint64_t avail = 0;
           room(*p, &avail);
@@ -469,11 +480,16 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
           }
           // compressed data inflates by ratio16 / 16 in the log: ask for what will fit
           const uint64_t fit = std::max<uint64_t>(avail * 16 / p->ratio16.load(), 4096);
+          // the generation first: offsets read after it are at least as new (stored before its bump)
+          const uint64_t g = p->gen.load(std::memory_order_acquire);
           const bool piped = p->inflight.load(std::memory_order_acquire) > 0;
-          req.push_back({p->partition, piped ? p->ask_offset.load() : p->fetch_offset.load(),
+          const int64_t from = piped ? p->ask_offset.load() : p->fetch_offset.load();
+          req.push_back({p->partition, from,
                          int32_t(std::min<uint64_t>({uint64_t(cfg_.partition_max_bytes), piped ? fit : avail, fit}))});
           lookup[p->partition] = p;
           since[p] = p->since.load();
+          gens[p] = g;
+          asked[p] = from;
         }
         if (req.empty()) continue;
         wire::Conn& k = c->conn(node);
@@ -509,17 +525,19 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
               continue;
             }
             std::unique_lock<std::mutex> pg(p->mu);
-            if (!p->owned.load() || p->since.load() != since[p]) {  // revoked / restarted meanwhile
-              pg.unlock();
+            if (!p->owned.load() || p->since.load() != since[p] || p->gen.load() != gens[p]) {
+              pg.unlock();  // revoked / restarted / repositioned meanwhile
               if (len > 0) k.skip(size_t(len));
               continue;
             }
             p->remote_hw.store(ph.high_watermark, std::memory_order_relaxed);
             p->fetches.fetch_add(1, std::memory_order_relaxed);
             if (len <= 0) continue;
-            if (p->ratio16.load(std::memory_order_relaxed) > 16) {
+            if (p->ratio16.load(std::memory_order_relaxed) > 16 || p->inflight.load(std::memory_order_acquire) > 0) {
               // a compressed partition: receive into a buffer, hand it to this thread's inflater,
-              // and ask for the next record set while it inflates
+              // and ask for the next record set while it inflates.  While any set is queued every
+              // later one queues behind it (even if the last ratio fell to 1): the inflater stores
+              // them in the order they were asked for
               pg.unlock();
               std::vector<uint8_t> buf;
               {
@@ -537,7 +555,7 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
                                                 std::chrono::steady_clock::now() - t_recv).count()),
                                    std::memory_order_relaxed);
               // the next offset to ask for: past the last whole batch received
-              const int64_t from = p->inflight.load() > 0 ? p->ask_offset.load() : p->fetch_offset.load();
+              const int64_t from = asked[p];
               int64_t next = from;
               for (size_t r = 0; size_t(len) - r >= 61;) {
                 const uint8_t* b = buf.data() + r;
@@ -564,9 +582,15 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
               }
               {
                 std::lock_guard<std::mutex> g(inf.m);
-                inf.q.push_back(Pending{p, since[p], std::move(buf)});
+                inf.q.push_back(Pending{p, since[p], gens[p], from, std::move(buf)});
               }
               inf.cv.notify_one();
+              continue;
+            }
+            if (asked[p] > p->fetch_offset.load()) {  // would leave a gap in the log: ask again
+              pg.unlock();
+              k.skip(size_t(len));
+              resync(*p, "fetch");
               continue;
             }
             uint64_t avail = 0;
@@ -598,6 +622,7 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
                 p->ratio16.store(uint32_t(std::clamp<uint64_t>(in.inflated_bytes * 16 / in.inflated_from, 16, 16 * 64)),
                                  std::memory_order_relaxed);
               if (in.next_offset > p->fetch_offset.load()) p->fetch_offset.store(in.next_offset);
+              if (in.full && in.kept == 0) grow_reserve(*p);
               p->bytes.fetch_add(in.kept_bytes, std::memory_order_relaxed);
               p->batches.fetch_add(in.kept, std::memory_order_relaxed);
               p->control.fetch_add(in.control, std::memory_order_relaxed);
@@ -649,9 +674,22 @@ void Replicator::inflate_loop(Inflater* inf) {
 void Replicator::inflate_one(Pending& pd) {
   Part* p = pd.p;
   size_t off = 0;
+  // fault injection for tests: an inflater this much slower keeps sets queued behind each other
+  const char* delay = std::getenv("TORCHKAFKA_TEST_INFLATE_DELAY_US");
+  const int delay_us = delay ? std::atoi(delay) : 0;
+  if (delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(delay_us));
   while (!stop_.load() && off < pd.data.size()) {
     std::unique_lock<std::mutex> pg(p->mu);
-    if (!p->owned.load() || p->since.load() != pd.since) return;  // revoked / restarted: dropped
+    // revoked / restarted / repositioned: dropped; so are the sets queued behind one that failed
+    // (storing them would publish the batches after the failure with the failed ones missing)
+    if (!p->owned.load() || p->since.load() != pd.since || p->gen.load() != pd.gen ||
+        p->failed_since.load(std::memory_order_acquire) == pd.since)
+      return;
+    if (off == 0 && pd.asked > p->fetch_offset.load()) {  // does not follow the log's end: a gap
+      pg.unlock();
+      resync(*p, "inflater");
+      return;
+    }
     uint64_t avail = 0;
     room(*p, &avail);
     if (avail < 4096) {
@@ -690,9 +728,30 @@ void Replicator::inflate_one(Pending& pd) {
     p->control.fetch_add(in.control, std::memory_order_relaxed);
     off += size_t(in.consumed);
     if (!in.full) return;  // stored (a trailing partial batch is asked for again by the fetch thread)
+    if (in.kept == 0) grow_reserve(*p);
     pg.unlock();
     sleep_ms(1);
   }
+}
+
+// A ring replica reserves room for what a set inflates to by the ratio learnt from the last
+// inflated batches; before any (or when a batch inflates more than those did) the first batch may
+// not fit the reservation at all, and nothing would ever be stored: double the ratio assumed.
+void Replicator::grow_reserve(Part& p) {
+  if (!cfg_.ring_bytes) return;  // a linear log offers its whole tail
+  const uint32_t r = p.ratio16.load(std::memory_order_relaxed);
+  p.ratio16.store(std::min<uint32_t>(r * 2, 16 * 64), std::memory_order_relaxed);
+}
+
+// A record set that does not start where the partition's log ends would leave a silent gap: it
+// is dropped, and so is everything asked for after it; the fetch thread asks again from the end.
+void Replicator::resync(Part& p, const char* where) {
+  std::lock_guard<std::mutex> pg(p.mu);
+  out_of_order_.fetch_add(1, std::memory_order_relaxed);
+  p.ask_offset.store(p.fetch_offset.load(), std::memory_order_relaxed);
+  p.gen.fetch_add(1, std::memory_order_release);
+  set_error(std::string("replicator: ") + where + ": a record set of " + cfg_.topic + "-" + std::to_string(p.partition) +
+            " did not follow the log end (offset " + std::to_string(p.fetch_offset.load()) + "): refetched");
 }
 
 int Replicator::forward(wire::Client& c) {

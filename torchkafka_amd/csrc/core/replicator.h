@@ -133,6 +133,8 @@ class Replicator {
   const std::atomic<uint64_t>* epoch_ptr() const { return &epoch_; }
   std::vector<std::pair<int32_t, uint64_t>> assignment_epochs() const;
   uint64_t rebalances() const { return rebalances_.load(); }
+  // record sets dropped because they did not start at the log's end (then refetched)
+  uint64_t out_of_order() const { return out_of_order_.load(); }
   // Never set any more (rebalances are followed in process); kept for API compatibility.
   bool fenced() const { return false; }
   int fetch_threads() const { return n_fetch_threads_; }
@@ -164,6 +166,9 @@ class Replicator {
     std::atomic<int> inflight{0};
     std::atomic<int64_t> ask_offset{0};
     std::atomic<uint64_t> failed_since{~uint64_t(0)};
+    // pipeline generation: bumped whenever fetch_offset jumps (OffsetOutOfRange reset, a restart by
+    // a rebalance, an out-of-order set): record sets asked for under an older generation are dropped
+    std::atomic<uint64_t> gen{0};
     std::atomic<bool> owned{true};       // subscribe mode: assigned to this member now
     std::atomic<uint64_t> since{0};      // assignment epoch at which it was (re)assigned
     std::mutex mu;                       // a fetch's write into the log vs. a restart of the partition
@@ -175,6 +180,8 @@ class Replicator {
   struct Pending {
     Part* p;
     uint64_t since;
+    uint64_t gen;    // Part::gen when the set was asked for
+    int64_t asked;   // the offset it was asked from: stored only where the log ends (contiguity)
     std::vector<uint8_t> data;
   };
   struct Inflater {
@@ -193,6 +200,8 @@ class Replicator {
   int64_t keep_offset(Part& p);
   uint8_t* room(Part& p, uint64_t* avail);
   void reset_offset(wire::Client& c, Part& p);
+  void resync(Part& p, const char* where);
+  void grow_reserve(Part& p);
   void set_error(const std::string& e);
   int forward(wire::Client& c);
 
@@ -225,7 +234,7 @@ class Replicator {
   std::string member_id_;
   int32_t generation_ = -1;
   std::vector<int32_t> assigned_;
-  std::atomic<uint64_t> epoch_{0}, rebalances_{0};
+  std::atomic<uint64_t> epoch_{0}, rebalances_{0}, out_of_order_{0};
   int64_t last_heartbeat_ms_ = 0;
   int n_fetch_threads_ = 0;
   std::atomic<uint64_t> fetch_wait_ns_{0};

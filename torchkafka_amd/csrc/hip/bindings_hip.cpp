@@ -12,6 +12,7 @@
 #include "engine.h"
 #include "driver.h"
 #include "rccl_lockstep.h"
+#include "bind_shm_lockstep.h"
 #include "reaper.h"
 
 namespace py = pybind11;
@@ -170,6 +171,7 @@ PYBIND11_MODULE(_tkhip, m) {
   py::class_<LockstepTransport>(m, "LockstepTransport", py::module_local());
   py::class_<PyLockstep, LockstepTransport>(m, "PyLockstep", py::module_local())
       .def(py::init<py::function>(), py::arg("allreduce_min"));
+  tkbind_shm::bind_shm_lockstep<LockstepTransport>(m);
   py::class_<RcclLockstep, LockstepTransport>(m, "RcclLockstep", py::module_local())
       .def(py::init([](const std::string& lib, py::bytes id, int rank, int world, int device, int slots) {
              return new RcclLockstep(lib, std::string(id), rank, world, device, slots);
@@ -362,6 +364,7 @@ PYBIND11_MODULE(_tkhip, m) {
              }
              s["log_register_ns"] = d.log_register_ns();
              s["log_register_wait_ns"] = d.log_register_wait_ns();
+             s["log_register_retries"] = d.log_register_retries();
              s["lockstep_agreements"] = d.lockstep_agreements();
              s["lockstep_wait_ns"] = d.lockstep_wait_ns();
              s["lockstep_issue_ns"] = d.lockstep_issue_ns();
@@ -392,7 +395,8 @@ PYBIND11_MODULE(_tkhip, m) {
           py::arg("pidxs"), "pin (and device-map) what the partition logs hold now, before the first batch")
       .def_property_readonly("direct", &MainDriver::direct)
       .def_property_readonly("coalesce", &MainDriver::coalesce)
-      .def("enable_lockstep", &MainDriver::enable_lockstep, py::keep_alive<1, 2>())
+      .def("enable_lockstep", &MainDriver::enable_lockstep, py::arg("transport"), py::arg("depth"),
+           py::arg("commit_every") = 0, py::keep_alive<1, 2>())
       .def("set_sync_commit", &MainDriver::set_sync_commit, py::arg("sync"))
       .def("set_commit_status", &MainDriver::set_commit_status, py::arg("status"),
            "sync commits under the lockstep: how this rank's commits of the finished batch went (2 stored, 1 "

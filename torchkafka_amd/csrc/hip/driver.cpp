@@ -263,8 +263,9 @@ class MainDriver::Source : public tk::LockstepSource {
   MainDriver& d_;
 };
 
-void MainDriver::enable_lockstep(LockstepTransport* ls, int depth) {
+void MainDriver::enable_lockstep(LockstepTransport* ls, int depth, int commit_every) {
   ls_ = std::make_unique<tk::CreditLockstep>(ls, depth);
+  ls_->set_commit_every(commit_every);
   ls_->set_on_committable([this](std::vector<tk::Watermark>&& wms) { ledger_->batch_committable(wms); });
   ls_->set_sync(sync_commit_);
   delivered_index_ = -1;

@@ -194,6 +194,7 @@ class MainDriver {
   uint64_t log_bytes_unpinned() const { return pins_->bytes_unpinned(); }
   int64_t log_register_ns() const { return pins_->register_ns(); }
   int64_t log_register_wait_ns() const { return pins_->register_wait_ns(); }
+  uint64_t log_register_retries() const { return pins_->register_retries(); }
   int coalesce() const { return coalesce_; }
   int64_t groups() const { return groups_; }
 
@@ -224,7 +225,8 @@ class MainDriver {
   void reset_stats();
 
   // Cross-rank lockstep over RCCL, pipelined `depth` steps ahead (ls is owned by the caller).
-  void enable_lockstep(LockstepTransport* ls, int depth);
+  // Async mode: an agreement grants at most commit_every batches (0: no cap), see lockstep.h.
+  void enable_lockstep(LockstepTransport* ls, int depth, int commit_every = 0);
   // commit='sync': batch k+1 is taken only after batch k's verdict landed and (under a lockstep)
   // an agreement at step k+1 made k committable on every rank (CreditLockstep sync mode).
   void set_sync_commit(bool s) {

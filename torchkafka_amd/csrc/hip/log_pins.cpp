@@ -101,8 +101,22 @@ bool LogPins::pin_some(uint32_t pidx, uint64_t end, bool one_piece) {
   for (uint64_t a = lo; a < hi; a += kChunk) {
     const uint64_t b = std::min(hi, a + kChunk);
     void* p = const_cast<uint8_t*>(base) + a;
-    if (hipHostRegister(p, b - a, hipHostRegisterMapped) != hipSuccess)
-      throw std::runtime_error("driver: hipHostRegister of a partition log failed");
+    hipError_t e = hipHostRegister(p, b - a, hipHostRegisterMapped);
+    if (e == hipErrorHostMemoryAlreadyRegistered) {
+      // the previous iteration (or a closed loader) over this same broker mapping handed its
+      // registration of these pages to the deferred-release thread, which has not run it yet
+      // (it waits for the device, e.g. behind the user's queued kernels): wait for it, once
+      (void)hipGetLastError();
+      Reaper::drain(60000);
+      ++register_retries_;
+      e = hipHostRegister(p, b - a, hipHostRegisterMapped);
+    }
+    if (e != hipSuccess)
+      throw std::runtime_error(std::string("driver: hipHostRegister of a partition log failed: ") +
+                               hipGetErrorString(e) +
+                               (e == hipErrorHostMemoryAlreadyRegistered
+                                    ? " (another live loader of this process pins the same broker mapping)"
+                                    : ""));
     reg_ranges_[pidx].emplace_back(p, b);
     void* dp = nullptr;
     if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess || dp != p)

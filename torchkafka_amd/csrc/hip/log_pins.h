@@ -71,6 +71,8 @@ class LogPins {
   uint64_t bytes_unpinned() const { return unpinned_bytes_; }
   int64_t register_ns() const { return reg_ns_.load(); }       // registration time, any thread
   int64_t register_wait_ns() const { return wait_ns_.load(); }  // the launch thread waiting for it
+  // registrations that first found their pages still registered by a pending deferred release
+  uint64_t register_retries() const { return register_retries_.load(); }
   void reset_stats() {
     reg_total_ = 0;
     reg_ns_ = 0;
@@ -107,6 +109,7 @@ class LogPins {
   uint64_t unpinned_bytes_ = 0;
   std::atomic<uint64_t> reg_total_{0};
   std::atomic<int64_t> reg_ns_{0}, wait_ns_{0};
+  std::atomic<uint64_t> register_retries_{0};
 };
 
 }  // namespace tkh

@@ -51,7 +51,7 @@ class RcclLockstep : public LockstepTransport {
   void wait(int ticket, int64_t out[tk::kLockstepWords]) override;
   const char* words_mode() const { return mode_ == 0 ? "kernel" : mode_ == 1 ? "host" : "copy"; }
   bool high_priority() const { return high_prio_; }
-  bool ready(int ticket);
+  bool ready(int ticket) override;
   // Failure detection: a round trip not complete after `ms` (a peer rank died or hung) aborts
   // the communicator and raises instead of blocking forever; <= 0 waits indefinitely.
   void set_timeout_ms(int64_t ms) { timeout_ms_ = ms; }

@@ -288,16 +288,18 @@ class LoaderCommits:
                 "offsets": offsets}
 
     def _cpu_group(self, group=None):
-        """A gloo group over the ranks of ``group`` (made once: a collective every rank reaches)."""
+        """A gloo group over the ranks of ``group``: ``group`` itself when it is gloo, else one made
+        per distinct rank list (torch's new_group: a collective of EVERY rank of the job, members or
+        not) and kept for the next call with the same ranks."""
         import torch.distributed as dist
 
-        if getattr(self, "_gloo_group", None) is None:
-            if dist.get_backend(group) == "gloo":
-                self._gloo_group = group
-            else:
-                ranks = None if group is None else dist.get_process_group_ranks(group)
-                self._gloo_group = dist.new_group(ranks=ranks, backend="gloo")
-        return self._gloo_group
+        if dist.get_backend(group) == "gloo":
+            return group
+        ranks = tuple(range(dist.get_world_size())) if group is None else tuple(dist.get_process_group_ranks(group))
+        cache = self.__dict__.setdefault("_gloo_groups", {})
+        if ranks not in cache:
+            cache[ranks] = dist.new_group(ranks=list(ranks), backend="gloo")
+        return cache[ranks]
 
     def load_state_dict(self, state: dict) -> None:
         """Resumes from a checkpoint's offsets: they are committed for the group (an administrative

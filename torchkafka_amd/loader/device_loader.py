@@ -148,10 +148,15 @@ class DeviceLoader(LoaderBridges, LoaderCommits, LoaderLockstep):
             the exception comes one or more steps later).  Host-decoded batches are verified by the
             workers before they are published, in both modes.
         lockstep: synchronise steps and commits across ranks when torch.distributed is initialised
-            (``True``: native RCCL on GPUs with an nccl group, the group's own all-reduce otherwise;
-            ``"host"``: the group's all-reduce (e.g. gloo) even on GPUs; ``"rccl"``: the native RCCL
-            transport whatever the group's backend; ``"always"``: also at world size 1).
+            (``True``: when every rank of the group runs on this host, the node-local shared-memory
+            transport (``csrc/core/shm_lockstep.h``: each rank writes its words into its own cache
+            line, well under a microsecond per agreement); across hosts native RCCL on GPUs with an
+            nccl group, the group's own all-reduce otherwise; ``"shm"`` / ``"rccl"`` / ``"host"`` (the
+            group's all-reduce, e.g. gloo) force a transport, at any world size; ``"always"``: the
+            automatic choice, also at world size 1).
         lockstep_depth: steps the per-step agreement is issued ahead (hides the collective's latency).
+        lockstep_commit_every: async lockstep: finished batches become committable at least every
+            this many steps (``Tuning.lockstep_commit_every``; None = per transport).
         h2d: ``"dma"`` (hipMemcpyAsync into device staging on ``copy_streams`` side streams, issued
             ``prefetch`` batches ahead), ``"zerocopy"`` (the collate kernel reads pinned host memory over
             PCIe: two HIP calls per batch instead of five, but the read runs on the compute stream) or
@@ -244,6 +249,8 @@ class DeviceLoader(LoaderBridges, LoaderCommits, LoaderLockstep):
         self.event_every = None if tun.event_every is None else int(tun.event_every)
         self.coalesce_wait_us = int(tun.coalesce_wait_us)
         self.lockstep_depth = None if tun.lockstep_depth is None else int(tun.lockstep_depth)
+        self.lockstep_commit_every = (None if tun.lockstep_commit_every is None
+                                      else int(tun.lockstep_commit_every))
         self.numa_bind = bool(tun.numa_bind)
         self._bridges: list = []
         if self.num_workers > 0 and cfg.bridge is not False:
@@ -387,7 +394,7 @@ class DeviceLoader(LoaderBridges, LoaderCommits, LoaderLockstep):
         run = self._run = _Run(self)
         lock = None
         try:
-            transport = self._lockstep_transport(process_group)
+            transport = self._lockstep_transport(process_group, probe=True)
             if transport is not None:
                 import torch.distributed as dist
 
@@ -395,17 +402,24 @@ class DeviceLoader(LoaderBridges, LoaderCommits, LoaderLockstep):
                     if run.driver is not None:
                         if transport == "rccl":
                             run.rccl = self._make_rccl_lockstep(process_group)
+                        elif transport == "shm":
+                            run.rccl = self._make_shm_lockstep(process_group, hip())
                         else:
                             run.rccl = hip().PyLockstep(_host_allreduce_min(process_group))
                             self.lockstep_info = {"transport": "host", "backend": dist.get_backend(process_group),
                                                   "world_size": dist.get_world_size(process_group)}
-                        run.driver.enable_lockstep(run.rccl, self._lockstep_depth(transport))
+                        every = self._lockstep_commit_every(transport)
+                        run.driver.enable_lockstep(run.rccl, self._lockstep_depth(transport), every)
+                        self.lockstep_info["commit_every"] = every
+                        self.lockstep_info["depth"] = self._lockstep_depth(transport)
                     else:
                         from ..parallel.lockstep import Lockstep
 
-                        lock = Lockstep(process_group, None)
-                        self.lockstep_info = {"transport": "host", "backend": dist.get_backend(process_group),
-                                              "world_size": lock.world_size}
+                        shm = self._make_shm_lockstep(process_group, core()) if transport == "shm" else None
+                        lock = Lockstep(process_group, None, transport=shm)
+                        if shm is None:
+                            self.lockstep_info = {"transport": "host", "backend": dist.get_backend(process_group),
+                                                  "world_size": lock.world_size}
         except BaseException:
             run.close()
             raise

@@ -31,32 +31,132 @@ def _host_allreduce_min(group):
     return allreduce_min
 
 
+def _host_key() -> str:
+    """What identifies this host to the other ranks: hostname and the kernel's boot id (two
+    containers of one machine share /dev/shm only if they share the boot and the IPC namespace;
+    the segment's attach check catches the rest)."""
+    import socket
+
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        boot = ""
+    return f"{socket.gethostname()}/{boot}"
+
+
 class LoaderLockstep:
     """Mixin of :class:`~torchkafka_amd.loader.DeviceLoader`: ``lockstep``, ``lockstep_depth``,
-    ``lockstep_timeout``, ``world_size``, ``device``, ``native``, ``plan``, the live ``_run``."""
+    ``lockstep_commit_every``, ``lockstep_timeout``, ``world_size``, ``device``, ``native``, ``plan``,
+    the live ``_run``."""
 
     def _lockstep_depth(self, transport) -> int:
         """Tuning.lockstep_depth, or its auto value: an RCCL agreement takes ~60-180 µs to come back
         while device-decoded steps take ~5 µs, so with the 64-deep ring the next one is issued 32
         steps before the credits run out (profiles/r05_s24: the wait per step 0.4-0.7 µs at depth 2,
-        0.003 µs at 32); the host lockstep keeps 2."""
+        0.003 µs at 32); the shared-memory and host transports keep 2."""
         if self.lockstep_depth is not None:
             return self.lockstep_depth
         return 32 if transport == "rccl" and self.plan.device_decode else 2
 
-    def _lockstep_transport(self, process_group=None):
-        """How ranks agree on every step: 'rccl' (native communicator, an nccl process group or
+    def _lockstep_commit_every(self, transport) -> int:
+        """Tuning.lockstep_commit_every, or its auto value per transport (config.py Tuning)."""
+        if self.lockstep_commit_every is not None:
+            return self.lockstep_commit_every
+        return {"shm": 4, "rccl": 32}.get(transport, 0)
+
+    def _single_host(self, process_group=None, probe: bool = False):
+        """True when every rank of the group runs on this host.  From torchrun's environment
+        (LOCAL_WORLD_SIZE == WORLD_SIZE) when it is there; else, with ``probe``, one all-gather of
+        the ranks' host keys over a CPU group (a collective: only where every rank gets to);
+        None when unknown."""
+        import os
+
+        import torch.distributed as dist
+
+        world = dist.get_world_size(process_group)
+        if world == 1:
+            return True
+        cache = self.__dict__.setdefault("_single_host_cache", {})
+        key = None if process_group is None else tuple(dist.get_process_group_ranks(process_group))
+        if key in cache:
+            return cache[key]
+        lws, ws = os.environ.get("LOCAL_WORLD_SIZE"), os.environ.get("WORLD_SIZE")
+        if process_group is None and lws and ws and int(ws) == world:
+            cache[key] = int(lws) == int(ws)
+            return cache[key]
+        if not probe:
+            return None
+        keys = [None] * world
+        dist.all_gather_object(keys, _host_key(), group=self._gloo_of(process_group))
+        cache[key] = len(set(keys)) == 1
+        return cache[key]
+
+    def _gloo_of(self, process_group):
+        import torch.distributed as dist
+
+        if dist.get_backend(process_group) == "gloo":
+            return process_group
+        cache = self.__dict__.setdefault("_lockstep_gloo", {})
+        key = None if process_group is None else tuple(dist.get_process_group_ranks(process_group))
+        if key not in cache:
+            ranks = None if process_group is None else list(key)
+            cache[key] = dist.new_group(ranks=ranks, backend="gloo")  # collective: every rank gets here
+        return cache[key]
+
+    def _lockstep_transport(self, process_group=None, probe: bool = False):
+        """How ranks agree on every step: 'shm' (every rank on this host: the node-local shared-memory
+        transport), 'rccl' (native communicator: an nccl process group across hosts, or
         lockstep='rccl'), 'host' (the process group's all-reduce), or None (no lockstep)."""
-        if not (self.lockstep and (self.world_size > 1 or self.lockstep == "always")):
+        # True: at world size > 1; "always" and a forced transport: at any world size (world 1
+        # rehearses the per-step agreement on one GPU)
+        if not self.lockstep or (self.lockstep is True and self.world_size <= 1):
             return None
         import torch.distributed as dist
 
         if not (dist.is_available() and dist.is_initialized()):
             return None
+        if self.lockstep in ("rccl", "host", "shm"):
+            forced = self.lockstep
+            if forced == "rccl" and (self.device.type != "cuda" or not self.native):
+                forced = "host"
+            return forced
+        if self._single_host(process_group, probe):
+            return "shm"
         if self.device.type != "cuda" or not self.native:
             return "host"
-        backend = dist.get_backend(process_group)
-        return "rccl" if self.lockstep == "rccl" or (backend == "nccl" and self.lockstep != "host") else "host"
+        return "rccl" if dist.get_backend(process_group) == "nccl" else "host"
+
+    def _make_shm_lockstep(self, process_group, module):
+        """The node-local transport (csrc/core/shm_lockstep.h): rank 0 makes the segment and names it
+        over a CPU group, every rank maps it, then the name is removed (nothing stays in /dev/shm)."""
+        import torch.distributed as dist
+
+        rank = dist.get_rank(process_group)
+        world = dist.get_world_size(process_group)
+        grp = self._gloo_of(process_group)
+        slots = max(8, self._lockstep_depth("shm") + 4)
+        name = [module.ShmLockstep.create(world, slots) if rank == 0 else None]
+        src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
+        dist.broadcast_object_list(name, src=src, group=grp, device=torch.device("cpu"))
+        try:
+            ls = module.ShmLockstep(name[0], rank, world)
+        finally:
+            dist.barrier(group=grp)  # every rank attached (or failed to) before the name goes
+            if rank == 0:
+                try:
+                    os.unlink("/dev/shm/" + name[0].lstrip("/"))
+                except FileNotFoundError:
+                    pass
+        ls.set_timeout_ms(int(self.lockstep_timeout * 1000))
+        # start-up proof that the segment spans the whole group: one sum of the rank ids through it
+        rank_sum = int(ls.allreduce_sum(rank))
+        if int(ls.attached) != world or rank_sum != world * (world - 1) // 2:
+            raise RuntimeError(f"lockstep: shared-memory segment has {ls.attached} ranks (rank-id sum {rank_sum}), "
+                               f"the process group {world}: are the ranks on different hosts?")
+        self.lockstep_info = {"transport": "shm", "world_size": world, "rank_id_sum": rank_sum, "slots": slots,
+                              "what": "node-local shared-memory all-reduce(MIN) of the agreement words"}
+        return ls
 
     def _make_rccl_lockstep(self, process_group):
         """Native RCCL communicator for the per-step lockstep (id broadcast through torch.distributed)."""

@@ -32,14 +32,18 @@ class LockstepError(RuntimeError):
 
 
 class Lockstep:
-    def __init__(self, group=None, device: torch.device | None = None):
+    """``transport``: a node-local shared-memory transport (``_tkcore.ShmLockstep``, see
+    ``csrc/core/shm_lockstep.h``) to agree through instead of the group's all-reduce."""
+
+    def __init__(self, group=None, device: torch.device | None = None, transport=None):
         if not (dist.is_available() and dist.is_initialized()):
             raise RuntimeError("Lockstep needs an initialised torch.distributed process group")
         self.group = group
         self.world_size = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        self.transport = transport
         backend = dist.get_backend(group)
-        self.on_device = backend == "nccl"
+        self.on_device = backend == "nccl" and transport is None
         if self.on_device:
             if device is None or device.type != "cuda":
                 device = torch.device("cuda", torch.cuda.current_device())
@@ -57,6 +61,11 @@ class Lockstep:
 
     def _allreduce_min(self, *w: int) -> tuple[int, ...]:
         self.collectives += 1
+        if self.transport is not None:
+            try:
+                return tuple(self.transport.allreduce_min(*w))
+            except RuntimeError as e:
+                raise LockstepError(str(e)) from e
         if not self.on_device:
             for i, v in enumerate(w):
                 self._buf[i] = v
