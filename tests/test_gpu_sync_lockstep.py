@@ -147,7 +147,7 @@ def test_shm_lockstep_native_driver_world1_sync_and_async(broker):
             for x in auto_commit(dl):
                 if steps:
                     got = {p: o for p, o in broker.committed_offsets(f"g{commit}", "t").items() if p in want}
-                    lag.append(sum(want[p] - got.get(p, 0) for p in want))
+                    lag.append(sum(want[p] - (got.get(p) or 0) for p in want))
                 for p, e in batch_ends(x).items():
                     want[p] = max(want.get(p, 0), e)
                 steps += 1

@@ -38,12 +38,17 @@ _Stamped = collections.namedtuple("_Stamped", ["batch", "worker"])
 
 class _StampingCollate:
     """The loader's ``collate_fn``, run in the workers, with each batch stamped by its worker id
-    (picklable for spawn / forkserver workers whenever the wrapped function is)."""
+    (picklable for spawn / forkserver workers whenever the wrapped function is).  With
+    ``channel`` (persistent workers keep this collate_fn for the loader's lifetime) it stamps only
+    while an auto_commit iteration is running: a plain ``for b in loader`` gets plain batches."""
 
-    def __init__(self, inner):
+    def __init__(self, inner, channel=None):
         self.inner = inner
+        self.channel = channel
 
     def __call__(self, data):
+        if self.channel is not None and not self.channel.active():
+            return self.inner(data)
         info = get_worker_info()
         return _Stamped(self.inner(data), info.id if info is not None else 0)
 
@@ -125,22 +130,43 @@ def _collate_main_process(batch):
     return default_collate(batch)
 
 
+def _persistent_channel(dataloader: DataLoader, bs: int) -> CommitChannel:
+    """The commit channel of a DataLoader with ``persistent_workers=True``: made with its workers
+    (by the first auto_commit iteration) and kept for the loader's lifetime, one epoch per
+    iteration (commit_channel.py).  Workers started by a plain ``iter(loader)`` carry no channel
+    and no stamping collate_fn: their batches cannot be attributed, so that is refused."""
+    import weakref
+
+    channel = getattr(dataloader, "_tk_commit_channel", None)
+    if channel is None:
+        if getattr(dataloader, "_iterator", None) is not None:
+            raise RuntimeError("auto_commit: this DataLoader's persistent workers were started by a plain "
+                               "iteration; start them with auto_commit (its first iteration gives them the "
+                               "commit channel), or use persistent_workers=False")
+        channel = CommitChannel(dataloader.num_workers, bs)
+        dataloader._tk_commit_channel = channel
+        weakref.finalize(dataloader, channel.close)
+    else:
+        channel.begin_epoch()
+    return channel
+
+
 def _multi_worker(dataloader: DataLoader, final_commit_timeout: float):
-    if dataloader.persistent_workers:
-        # persistent workers outlive this generator with the stamping collate_fn and this
-        # iteration's commit channel pickled into them: a later plain `for b in dataloader` would
-        # get stamped batches, and which worker made a batch would be unknowable for a new channel
-        raise RuntimeError("auto_commit does not support persistent_workers=True: its workers keep the "
-                           "commit channel of the iteration that started them")
     ds = dataloader.dataset
     bs = dataloader.batch_size or 1
-    channel = CommitChannel(dataloader.num_workers, bs)
+    persistent = bool(dataloader.persistent_workers)
+    channel = _persistent_channel(dataloader, bs) if persistent else CommitChannel(dataloader.num_workers, bs)
+    channel.set_active(True)
     previous = getattr(ds, "_commit_channel", None)
     collate = dataloader.collate_fn
     ds._commit_channel = channel  # inherited (fork) / pickled (spawn) into the workers created by iter()
-    dataloader.collate_fn = _StampingCollate(collate)  # handed to the workers by iter() as well
+    # handed to the workers by iter() as well (persistent workers: once, at their start)
+    dataloader.collate_fn = _StampingCollate(collate, channel if persistent else None)
     try:
         batches = iter(dataloader)
+    except BaseException:
+        channel.set_active(False)
+        raise
     finally:
         ds._commit_channel = previous
         dataloader.collate_fn = collate
@@ -158,7 +184,10 @@ def _multi_worker(dataloader: DataLoader, final_commit_timeout: float):
             log.warning("auto_commit: some workers did not acknowledge their final commit")
     finally:
         channel.close_requests()  # a worker waiting to serve a last request may exit now
+        channel.set_active(False)  # persistent workers: the next plain iteration is not stamped
         # the last reference to the iterator: its finaliser joins (and if needed terminates) the
-        # workers -- the public teardown, the same as a user's loop ending
+        # workers -- the public teardown, the same as a user's loop ending (persistent workers:
+        # the DataLoader keeps them, and the channel, for its next iteration)
         del batches
-        channel.close()
+        if not persistent:
+            channel.close()

@@ -17,9 +17,16 @@ from multiprocessing import shared_memory
 
 import numpy as np
 
-_REQ, _ACK, _PID, _HDR = 0, 1, 2, 3
+_REQ, _ACK, _PID, _HDR = 0, 1, 2, 5
 _W = 3  # words per worker: request, acknowledgement, pid
 _CLOSING = 2  # header word: the main process will send no further requests
+_EPOCH = 3  # header word: the iteration (auto_commit pass over the loader) requests belong to
+_ACTIVE = 4  # header word: an auto_commit iteration is running (workers stamp their batches)
+# Requests and acknowledgements carry their iteration in the high bits: a persistent worker (one
+# DataLoader's workers serve every iteration) never takes a request or an acknowledgement of an
+# earlier iteration for one of this iteration.
+_EPOCH_SHIFT = 40
+_COUNT_MASK = (1 << _EPOCH_SHIFT) - 1
 
 
 class CommitChannel:
@@ -34,6 +41,27 @@ class CommitChannel:
         self._arr[:] = 0
         self._arr[0] = num_workers
         self._arr[1] = batch_size
+        self._arr[_EPOCH] = 1
+
+    # ---- iterations (persistent workers serve several)
+    def epoch(self) -> int:
+        return int(self._arr[_EPOCH])
+
+    def begin_epoch(self) -> int:
+        """The main process starts another iteration over the same workers: requests restart at 0
+        (tagged with the new epoch), the channel is open and batches are stamped again."""
+        e = self.epoch() + 1
+        for w in range(self.num_workers):
+            self._arr[self._i(w, _REQ)] = e << _EPOCH_SHIFT
+        self._arr[_CLOSING] = 0
+        self._arr[_EPOCH] = e
+        return e
+
+    def set_active(self, on: bool) -> None:
+        self._arr[_ACTIVE] = 1 if on else 0
+
+    def active(self) -> bool:
+        return bool(self._arr[_ACTIVE])
 
     # pickling (spawn workers): re-attach by name, never unlink from a worker
     def __getstate__(self):
@@ -56,16 +84,20 @@ class CommitChannel:
         return _HDR + _W * w + which
 
     def request(self, worker: int, batches: int) -> None:
-        self._arr[self._i(worker, _REQ)] = batches
+        self._arr[self._i(worker, _REQ)] = (self.epoch() << _EPOCH_SHIFT) | batches
 
-    def requested(self, worker: int) -> int:
-        return int(self._arr[self._i(worker, _REQ)])
+    def requested(self, worker: int, epoch: int | None = None) -> int:
+        """Batches of ``epoch`` (default: the current one) requested from ``worker``; 0 while the
+        slot still holds an older iteration's request."""
+        v = int(self._arr[self._i(worker, _REQ)])
+        return v & _COUNT_MASK if (v >> _EPOCH_SHIFT) == (self.epoch() if epoch is None else epoch) else 0
 
-    def ack(self, worker: int, batches: int) -> None:
-        self._arr[self._i(worker, _ACK)] = batches
+    def ack(self, worker: int, batches: int, epoch: int | None = None) -> None:
+        self._arr[self._i(worker, _ACK)] = ((self.epoch() if epoch is None else epoch) << _EPOCH_SHIFT) | batches
 
-    def acked(self, worker: int) -> int:
-        return int(self._arr[self._i(worker, _ACK)])
+    def acked(self, worker: int, epoch: int | None = None) -> int:
+        v = int(self._arr[self._i(worker, _ACK)])
+        return v & _COUNT_MASK if (v >> _EPOCH_SHIFT) == (self.epoch() if epoch is None else epoch) else 0
 
     def register(self, worker: int, pid: int) -> None:
         """A worker announces its process (liveness is read from here, not from the DataLoader)."""

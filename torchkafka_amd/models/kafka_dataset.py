@@ -158,7 +158,8 @@ class KafkaDataset(IterableDataset):
             # the request counts this worker's *batches* the user finished; the DataLoader's
             # fetcher cuts a worker's stream into batch_size samples per batch (only the last one
             # of the stream is short), so batch k ends at sample min(k * batch_size, yielded)
-            req = ch.requested(self._worker_id)
+            epoch = getattr(self, "_channel_epoch", None)
+            req = ch.requested(self._worker_id, epoch)
             if req <= self._channel_done:
                 return
             limit = req * ch.batch_size
@@ -171,7 +172,7 @@ class KafkaDataset(IterableDataset):
                     self._do_commit(offsets)
                 # a failed commit is logged and not retried, as in the reference (B14)
             self._channel_done = req
-            ch.ack(self._worker_id, req)
+            ch.ack(self._worker_id, req, epoch)
 
     def _start_committer(self) -> None:
         """Background servicing of commit requests while the generator is suspended.
@@ -182,8 +183,8 @@ class KafkaDataset(IterableDataset):
         ``_consumer_lock`` whenever it runs, so this thread only touches the
         consumer while the generator is suspended or finished.
         """
-        if getattr(self, "_committer", None) is not None:
-            return
+        if getattr(self, "_committer", None) is not None and self._committer.is_alive():
+            return  # (a persistent worker's thread ends with each iteration's last request)
 
         def run():
             # 2 ms while requests keep coming, backing off to 50 ms once the main process has
@@ -203,6 +204,14 @@ class KafkaDataset(IterableDataset):
                     finally:
                         self._consumer_lock.release()
                 nap = 0.002 if self._channel_done != seen else min(0.05, nap * 1.25)
+            # the main process announced its last request of this iteration, after publishing it: a
+            # persistent worker lives on (no exit hook runs), so serve that request now
+            if ch is not None:
+                try:
+                    with self._consumer_lock:
+                        self._service_channel()
+                except Exception:  # noqa: BLE001
+                    _logger.exception("final commit request failed on worker %s", self._worker_id)
 
         self._committer = threading.Thread(target=run, name="torchkafka-committer", daemon=True)
         self._committer.start()
@@ -211,7 +220,8 @@ class KafkaDataset(IterableDataset):
         # commit of that worker's last batch.  Serve that request on the way out.
         import multiprocessing.util as mpu
 
-        self._channel_finalizer = mpu.Finalize(self, KafkaDataset._final_service, args=(self,), exitpriority=100)
+        if getattr(self, "_channel_finalizer", None) is None:
+            self._channel_finalizer = mpu.Finalize(self, KafkaDataset._final_service, args=(self,), exitpriority=100)
 
     @staticmethod
     def _final_service(ds, max_wait: float = 15.0) -> None:
@@ -230,7 +240,8 @@ class KafkaDataset(IterableDataset):
                 with ds._consumer_lock:
                     ds._service_channel()
                 total = getattr(ds, "_final_yielded", None)
-                if ch is None or total is None or ch.acked(ds._worker_id) * ch.batch_size >= total or ch.closing():
+                acked = ch.acked(ds._worker_id, getattr(ds, "_channel_epoch", None)) if ch is not None else 0
+                if ch is None or total is None or acked * ch.batch_size >= total or ch.closing():
                     break
                 if os.getppid() != parent or time.monotonic() > deadline:
                     break
@@ -265,6 +276,8 @@ class KafkaDataset(IterableDataset):
             self._snapshots = deque()
             self._channel_done = 0
             self._final_yielded = None
+            # a persistent worker starts a generator per iteration: this one serves that iteration
+            self._channel_epoch = ch.epoch()
         hooks = getattr(self._consumer, "_idle_hooks", None)
         if hooks is not None and self._service_channel not in hooks:
             hooks.append(self._service_channel)
