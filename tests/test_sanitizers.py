@@ -1,6 +1,7 @@
 """Host sanitizers over the native core: ThreadSanitizer on the slot-ring protocol
 and the broker -> fetcher -> packer -> commit pipeline (threads standing in for worker processes),
 the HIP command queue (its device calls stubbed), the span kernels' window geometry (span.h SpanWindows),
+the RCCL lockstep transport's timeout / abort / asynchronous-error paths (HIP and RCCL stubbed),
 AddressSanitizer + UBSan on the same stress test and on a RecordBatch/CRC32C/JSON fuzz test.
 The sources are tests/native/*.cpp; tools/sanitize.sh builds and runs them."""
 import os

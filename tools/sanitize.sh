@@ -22,6 +22,13 @@ $CXX $COMMON -fsanitize=thread $HQ -o "$OUT/hip_queue_tsan"
 $CXX $COMMON -fsanitize=address,undefined -fno-sanitize-recover=undefined $HQ -o "$OUT/hip_queue_asan"
 $CXX $COMMON -fsanitize=address,undefined -fno-sanitize-recover=undefined -Itorchkafka_amd/csrc/core \
   tests/native/span_window_test.cpp -o "$OUT/span_window_asan"
+# the RCCL lockstep transport's failure detection (csrc/hip/rccl_lockstep.cpp) with HIP stubbed and a
+# stand-in librccl (tests/native/rccl_stub.cpp) it dlopen()s
+RL="-D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Itorchkafka_amd/csrc/hip -I$CORE"
+$CXX $COMMON -fsanitize=address,undefined -fno-sanitize-recover=undefined $RL -shared -fPIC \
+  tests/native/rccl_stub.cpp -o "$OUT/librccl_stub.so"
+$CXX $COMMON -fsanitize=address,undefined -fno-sanitize-recover=undefined $RL tests/native/rccl_lockstep_test.cpp \
+  torchkafka_amd/csrc/hip/rccl_lockstep.cpp -o "$OUT/rccl_lockstep_asan" -ldl
 export TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1"
 export ASAN_OPTIONS="halt_on_error=1 detect_leaks=1"
 export UBSAN_OPTIONS="halt_on_error=1 print_stacktrace=1"
@@ -32,4 +39,5 @@ echo "== asan codec_fuzz, built-in LZ4 decoder"; TORCHKAFKA_LZ4_LIB=0 "$OUT/code
 echo "== tsan hip_queue"; "$OUT/hip_queue_tsan" ${TK_SAN_QUEUE:-50000}
 echo "== asan hip_queue"; "$OUT/hip_queue_asan" ${TK_SAN_QUEUE:-50000}
 echo "== asan span_window"; "$OUT/span_window_asan"
+echo "== asan rccl_lockstep"; "$OUT/rccl_lockstep_asan" "$OUT/librccl_stub.so"
 echo "sanitizers: all clean"

@@ -43,7 +43,7 @@ PROCESS_ENV = {
     "TORCHKAFKA_NO_REBUILD": "1: never rebuild stale in-tree extensions at import",
     "TORCHKAFKA_RCCL_WORDS": "kernel (default) / host / copy: how the RCCL lockstep's agreement words reach "
                              "RCCL -- tiny copy kernels, RCCL on host-mapped memory, or hipMemcpyAsync "
-                             "(csrc/hip/rccl_lockstep.hip)",
+                             "(csrc/hip/rccl_issue.hip)",
     "TORCHKAFKA_LOCKSTEP_PRIORITY": "normal (default) / high: the RCCL lockstep stream's priority; high gives it a "
                                     "hardware queue of its own, where its agreements came back slower "
                                     "(profiles/r05_s19_rccl_matrix)",

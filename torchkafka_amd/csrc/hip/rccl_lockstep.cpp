@@ -1,5 +1,10 @@
+// Host side of the native RCCL lockstep transport (rccl_lockstep.h): the communicator, the bounded
+// waits with failure detection, the start-up checks.  Plain HIP runtime calls only -- the one
+// device kernel (the agreement words' copy) and issue() are in rccl_issue.hip -- so this file
+// also builds for the host test with the HIP and RCCL symbols stubbed (tests/native/rccl_lockstep_test.cpp).
 #include "rccl_lockstep.h"
 
+#include "rccl_api.h"
 #include "reaper.h"
 
 #include <dlfcn.h>
@@ -13,25 +18,7 @@
 
 namespace tkh {
 
-struct RcclApi {
-  void* lib = nullptr;
-  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
-  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
-  ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
-  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
-  ncclResult_t (*CommCount)(const ncclComm_t, int*) = nullptr;
-  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;                         // optional
-  ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;  // optional
-  const char* (*GetErrorString)(ncclResult_t) = nullptr;
-};
-
 namespace {
-
-#define TKH_HIP(expr)                                                                          \
-  do {                                                                                         \
-    hipError_t _e = (expr);                                                                    \
-    if (_e != hipSuccess) throw std::runtime_error(std::string(#expr) + ": " + hipGetErrorString(_e)); \
-  } while (0)
 
 RcclApi* load_api(const std::string& path) {
   // Prefer the instance already in the process (torch's), then the given path, then the system one.
@@ -55,19 +42,6 @@ RcclApi* load_api(const std::string& path) {
   api->CommAbort = reinterpret_cast<decltype(api->CommAbort)>(dlsym(lib, "ncclCommAbort"));
   api->CommGetAsyncError = reinterpret_cast<decltype(api->CommGetAsyncError)>(dlsym(lib, "ncclCommGetAsyncError"));
   return api;
-}
-
-void check(RcclApi* api, ncclResult_t r, const char* what) {
-  if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + api->GetErrorString(r));
-}
-
-constexpr int kW = tk::kLockstepWords;
-
-// The agreement's words between pinned host memory and the device buffer RCCL reduces: one wave,
-// one word per lane (system-coherent host-mapped memory, read and written over PCIe).
-__global__ void words_copy_kernel(const int64_t* __restrict__ src, int64_t* __restrict__ dst, int n) {
-  const int i = int(threadIdx.x);
-  if (i < n) dst[i] = src[i];
 }
 
 int words_mode_env() {
@@ -126,14 +100,14 @@ RcclLockstep::RcclLockstep(const std::string& lib_path, const std::string& id, i
 }
 
 RcclLockstep::~RcclLockstep() {
-  hipSetDevice(device_);
-  if (!aborted_ && stream_) hipStreamSynchronize(stream_);
+  (void)hipSetDevice(device_);
+  if (!aborted_ && stream_) (void)hipStreamSynchronize(stream_);
   if (comm_) api_->CommDestroy(static_cast<ncclComm_t>(comm_));  // null once aborted
-  for (auto e : ev_) hipEventDestroy(e);
+  for (auto e : ev_) (void)hipEventDestroy(e);
   Reaper::free_device(device_, d_);  // hipFree / hipHostFree wait for the whole device (reaper.h)
   Reaper::free_host(device_, h_in_);
   Reaper::free_host(device_, h_out_);
-  if (stream_) hipStreamDestroy(stream_);
+  if (stream_) (void)hipStreamDestroy(stream_);
   delete api_;
 }
 
@@ -176,42 +150,6 @@ int64_t steady_ns() {
       .count();
 }
 }  // namespace
-
-int RcclLockstep::issue(const int64_t in[kW]) {
-  const int64_t t_issue = tracing_ ? steady_ns() : 0;
-  const int s = int(issued_ % uint64_t(slots_));
-  if (aborted_) throw std::runtime_error("lockstep: the RCCL communicator was aborted after a failure");
-  // the slot's previous round trip must be complete before its buffers are reused
-  wait_event(s, "lockstep slot reuse");
-  int64_t* hin = h_in_ + kW * s;
-  int64_t* hout = h_out_ + kW * s;
-  int64_t* din = d_ + 2 * kW * s;
-  int64_t* dout = din + kW;
-  for (int k = 0; k < kW; ++k) hin[k] = in[k];
-  auto* comm = static_cast<ncclComm_t>(comm_);
-  if (mode_ == 1) {
-    // RCCL reads and writes the host-mapped words itself: one queue operation
-    check(api_, api_->AllReduce(h_in_dev_ + kW * s, h_out_dev_ + kW * s, kW, ncclInt64, ncclMin, comm, stream_),
-          "ncclAllReduce");
-  } else if (mode_ == 2) {
-    TKH_HIP(hipMemcpyAsync(din, hin, kW * sizeof(int64_t), hipMemcpyHostToDevice, stream_));
-    check(api_, api_->AllReduce(din, dout, kW, ncclInt64, ncclMin, comm, stream_), "ncclAllReduce");
-    TKH_HIP(hipMemcpyAsync(hout, dout, kW * sizeof(int64_t), hipMemcpyDeviceToHost, stream_));
-  } else {
-    hipLaunchKernelGGL(words_copy_kernel, dim3(1), dim3(64), 0, stream_, h_in_dev_ + kW * s, din, kW);
-    TKH_HIP(hipGetLastError());
-    check(api_, api_->AllReduce(din, dout, kW, ncclInt64, ncclMin, comm, stream_), "ncclAllReduce");
-    hipLaunchKernelGGL(words_copy_kernel, dim3(1), dim3(64), 0, stream_, dout, h_out_dev_ + kW * s, kW);
-    TKH_HIP(hipGetLastError());
-  }
-  TKH_HIP(hipEventRecord(ev_[size_t(s)], stream_));
-  ++issued_;
-  if (tracing_ && trace_.size() < (size_t(1) << 20)) {
-    slot_rec_[size_t(s)] = int64_t(trace_.size());
-    trace_.push_back(TraceRec{t_issue, steady_ns(), 0, 0});
-  }
-  return s;
-}
 
 int RcclLockstep::comm_count() const {
   if (!comm_) throw std::runtime_error("lockstep: the RCCL communicator was aborted after a failure");

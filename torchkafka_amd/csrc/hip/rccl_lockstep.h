@@ -20,7 +20,7 @@
 // communicator is our own, bootstrapped from a unique id the caller
 // broadcasts through torch.distributed.
 #pragma once
-#include <hip/hip_runtime.h>
+#include <hip/hip_runtime_api.h>
 
 #include <cstdint>
 #include <string>
