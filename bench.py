@@ -122,13 +122,16 @@ def parse():
     ap.add_argument("--self-launch", action="store_true",
                     help="start the rank processes from this process even at --gpus 1 / --same-device (the "
                          "launcher path the N > 1 runs take without torchrun)")
-    ap.add_argument("--config-blocks", default="compute,config4,config5,config1,process",
-                    help="comma list of blocks run at N = 1, each on a broker of its own: compute (a bf16 GEMM "
+    ap.add_argument("--config-blocks", default="train,compute,config4,config5,config1,process",
+                    help="comma list of blocks run at N = 1, each on a broker of its own: train (a bf16 MLP "
+                         "training step fed by auto_commit(loader) against the same step over pre-staged device "
+                         "batches: the loader's cost inside a real step), compute (a bf16 GEMM "
                          "stream beside the config-2 and config-4 loaders: what the loader costs a training job), "
                          "config4 (JSON -> bf16), config5 (1 MiB records, 128 partitions), config1 (CPU plumbing), "
                          "process (the README's json.loads _process: DeviceLoader vs torch DataLoader + "
                          "pin_memory); '' for none")
     ap.add_argument("--compute-steps", type=int, default=20000)
+    ap.add_argument("--train-steps", type=int, default=1500, help="timed steps per loop of the train block")
     ap.add_argument("--config4-steps", type=int, default=20000)
     ap.add_argument("--config5-steps", type=int, default=1000)
     ap.add_argument("--config1-records", type=int, default=100000)
@@ -564,6 +567,14 @@ def run_config_blocks(R: "Rank", args) -> dict:
                              "--verify", args.verify])
                 res[f"{wl}_{h2d}"] = m.run(a, sync=R.sync)
             name = "steady_compute"
+        elif name == "train" and on_gpu:
+            m = importlib.import_module("train_step")
+            res = {}
+            for wl, h2d in (("config2", "zerocopy"), ("config2", "dma"), ("config4", "auto")):
+                a = m.parse(["--workload", wl, "--h2d", h2d, "--steps", str(args.train_steps), "--device", dev,
+                             "--verify", args.verify])
+                res[f"{wl}_{h2d}"] = m.run(a, sync=R.sync)
+            name = "train_step"
         elif name == "config4" and on_gpu:
             m = importlib.import_module("config4_json_varlen")
             a = m.parse(["--steps", str(args.config4_steps), "--device", dev, "--verify", args.verify])

@@ -18,9 +18,11 @@ measures that share directly:
 A GEMM's TFLOP/s is FLOPs over its own event-timed execution (``sum``: the busy time of the
 GEMMs that ran inside the window), so a host that queued late cannot flatter or hurt it; the
 ``span`` rate (first start to last end) is reported next to it with ``dry_gaps_ms``, the time
-the stream ran without a queued GEMM.  ``gemm_slowdown_pct`` = how much slower each GEMM runs
-beside the loader.  The loader's window ends when its last step returned (with
-``verify="deliver"`` that is after the last batch's device verdict).
+the stream ran without a queued GEMM.  ``gemm_slowdown_pct`` = how much longer the stream takes
+per GEMM beside the loader (span-based: a host that stopped feeding the stream counts), with
+``dry_gaps_ms`` beside it; ``gemm_kernel_slowdown_pct`` = the per-GEMM kernel time alone (p50).
+The loader's window ends when its last step returned (with ``verify="deliver"`` that is after the
+last batch's device verdict).
 
 Usage: python benchmarks/compute_overlap.py [--workload config2|config4] [--h2d auto|zerocopy|dma]
 """
@@ -210,7 +212,12 @@ def run(args, sync=None) -> dict:
             "fill_s": round(fill_s, 2),
         }
         if alone and beside:
-            out["gemm_slowdown_pct"] = round((beside["ms_per_gemm_p50"] / alone["ms_per_gemm_p50"] - 1) * 100, 2)
+            # what the training job sees: its stream's span per GEMM (kernel time AND the gaps when
+            # the host, blocked in next(), stopped feeding it) against alone
+            out["gemm_slowdown_pct"] = round((alone["tflops_span"] / beside["tflops_span"] - 1) * 100, 2)
+            out["dry_gaps_ms"] = beside["dry_gaps_ms"]
+            out["gemm_kernel_slowdown_pct"] = round(
+                (beside["ms_per_gemm_p50"] / alone["ms_per_gemm_p50"] - 1) * 100, 2)
             out["gemm_tflops_ratio"] = round(beside["tflops_sum"] / alone["tflops_sum"], 4)
             out["loader_ratio"] = round(out["together"]["records_per_s"] / out["loader_alone_records_per_s"], 4)
         return out

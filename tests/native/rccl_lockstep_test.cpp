@@ -69,6 +69,8 @@ hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipSt
 namespace tkh {
 // the device half (rccl_issue.hip: the words kernel around the all-reduce) is not built here
 int RcclLockstep::issue(const int64_t*) { throw std::logic_error("issue() is device code"); }
+void RcclLockstep::capture_graphs() {}
+void RcclLockstep::release_graphs() { graphs_.clear(); }
 // the deferred-release thread: released at once here
 void Reaper::free_device(int, void* p) {
   ++g_dev_frees;

@@ -73,7 +73,8 @@ def test_reopen_dma_loader_over_the_same_logs_while_user_work_is_queued(broker):
     dev = torch.device("cuda:0")
 
     def loader(group):
-        return DeviceLoader(Vec.placeholder(), 256, num_workers=2, device=dev, dtype=torch.bfloat16, h2d="dma",
+        # float32 out: the offset column stays exact (bf16 holds 8 significant bits)
+        return DeviceLoader(Vec.placeholder(), 256, num_workers=2, device=dev, dtype=torch.float32, h2d="dma",
                             decode="device",
                             worker_init_fn=Vec.init_worker("t", bootstrap_servers=broker.url, group_id=group,
                                                            auto_offset_reset="earliest", consumer_timeout_ms=2000))
@@ -84,7 +85,7 @@ def test_reopen_dma_loader_over_the_same_logs_while_user_work_is_queued(broker):
     def queue_user_work():
         with torch.cuda.stream(user):
             for _ in range(20):
-                torch.cuda._sleep(5_000_000)
+                torch.cuda._sleep(40_000_000)
             done.record()
 
     a = loader("a")
@@ -104,11 +105,12 @@ def test_reopen_dma_loader_over_the_same_logs_while_user_work_is_queued(broker):
     a.close()
     b = loader("b")  # a new loader over the same logs, the user's work still queued
     n = 0
+    st_b = {}
     for x in auto_commit(b):
         n += x.shape[0]
         if n >= 20 * 256:
+            st_b = dict(b._run.driver.stats())  # (the run closes with the loop)
             break
-    st_b = dict(b._run.driver.stats())
     b.close()
     user_busy = not done.query()
     done.synchronize()

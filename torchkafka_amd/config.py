@@ -41,8 +41,9 @@ PROCESS_ENV = {
     "TORCHKAFKA_NT_COPY": "0: plain (cached) stores when workers pack slots",
     "TORCHKAFKA_DRIVER_TRACE": "1: step-driver trace lines on stderr (debugging)",
     "TORCHKAFKA_NO_REBUILD": "1: never rebuild stale in-tree extensions at import",
-    "TORCHKAFKA_RCCL_WORDS": "kernel (default) / host / copy: how the RCCL lockstep's agreement words reach "
-                             "RCCL -- tiny copy kernels, RCCL on host-mapped memory, or hipMemcpyAsync "
+    "TORCHKAFKA_RCCL_WORDS": "kernel (default) / host / copy / graph: how the RCCL lockstep's agreement words reach "
+                             "RCCL -- tiny copy kernels, RCCL on host-mapped memory, hipMemcpyAsync, or the "
+                             "kernels and the all-reduce captured into one HIP graph per slot "
                              "(csrc/hip/rccl_issue.hip)",
     "TORCHKAFKA_LOCKSTEP_PRIORITY": "normal (default) / high: the RCCL lockstep stream's priority; high gives it a "
                                     "hardware queue of its own, where its agreements came back slower "

@@ -51,6 +51,9 @@ int RcclLockstep::issue(const int64_t in[kW]) {
     TKH_HIP(hipMemcpyAsync(din, hin, kW * sizeof(int64_t), hipMemcpyHostToDevice, stream_));
     check(api_, api_->AllReduce(din, dout, kW, ncclInt64, ncclMin, comm, stream_), "ncclAllReduce");
     TKH_HIP(hipMemcpyAsync(hout, dout, kW * sizeof(int64_t), hipMemcpyDeviceToHost, stream_));
+  } else if (mode_ == 3) {
+    // the three dependent operations below, captured once per slot: one submission per agreement
+    TKH_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(graphs_[size_t(s)]), stream_));
   } else {
     hipLaunchKernelGGL(words_copy_kernel, dim3(1), dim3(64), 0, stream_, h_in_dev_ + kW * s, din, kW);
     TKH_HIP(hipGetLastError());
@@ -65,6 +68,45 @@ int RcclLockstep::issue(const int64_t in[kW]) {
     trace_.push_back(TraceRec{t_issue, steady_ns(), 0, 0});
   }
   return s;
+}
+
+// TORCHKAFKA_RCCL_WORDS=graph: words in, RCCL's all-reduce and words out captured into one HIP
+// graph per slot (their buffers are the slot's, fixed), so an agreement is one hipGraphLaunch
+// instead of three launches.  Any capture failure falls back to the three launches.
+void RcclLockstep::capture_graphs() {
+  auto* comm = static_cast<ncclComm_t>(comm_);
+  graphs_.assign(size_t(slots_), nullptr);
+  for (int s = 0; s < slots_; ++s) {
+    int64_t* din = d_ + 2 * kW * s;
+    int64_t* dout = din + kW;
+    hipGraph_t g = nullptr;
+    bool ok = hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal) == hipSuccess;
+    if (ok) {
+      hipLaunchKernelGGL(words_copy_kernel, dim3(1), dim3(64), 0, stream_, h_in_dev_ + kW * s, din, kW);
+      ok = hipGetLastError() == hipSuccess;
+      ok = api_->AllReduce(din, dout, kW, ncclInt64, ncclMin, comm, stream_) == ncclSuccess && ok;
+      hipLaunchKernelGGL(words_copy_kernel, dim3(1), dim3(64), 0, stream_, dout, h_out_dev_ + kW * s, kW);
+      ok = hipGetLastError() == hipSuccess && ok;
+      ok = hipStreamEndCapture(stream_, &g) == hipSuccess && ok && g != nullptr;
+    }
+    hipGraphExec_t ex = nullptr;
+    if (ok) ok = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) == hipSuccess;
+    if (g) (void)hipGraphDestroy(g);
+    if (!ok) {
+      (void)hipGetLastError();
+      release_graphs();
+      graph_fallback_ = true;
+      mode_ = 0;
+      return;
+    }
+    graphs_[size_t(s)] = ex;
+  }
+}
+
+void RcclLockstep::release_graphs() {
+  for (void* g : graphs_)
+    if (g) (void)hipGraphExecDestroy(static_cast<hipGraphExec_t>(g));
+  graphs_.clear();
 }
 
 }  // namespace tkh

@@ -48,7 +48,7 @@ int words_mode_env() {
   const char* e = std::getenv("TORCHKAFKA_RCCL_WORDS");
   if (!e) return 0;
   const std::string v(e);
-  return v == "host" ? 1 : v == "copy" ? 2 : 0;
+  return v == "host" ? 1 : v == "copy" ? 2 : v == "graph" ? 3 : 0;
 }
 
 }  // namespace
@@ -97,11 +97,13 @@ RcclLockstep::RcclLockstep(const std::string& lib_path, const std::string& id, i
   ncclComm_t comm = nullptr;
   check(api_, api_->CommInitRank(&comm, world_, uid, rank_), "ncclCommInitRank");
   comm_ = comm;
+  if (mode_ == 3) capture_graphs();
 }
 
 RcclLockstep::~RcclLockstep() {
   (void)hipSetDevice(device_);
   if (!aborted_ && stream_) (void)hipStreamSynchronize(stream_);
+  release_graphs();
   if (comm_) api_->CommDestroy(static_cast<ncclComm_t>(comm_));  // null once aborted
   for (auto e : ev_) (void)hipEventDestroy(e);
   Reaper::free_device(device_, d_);  // hipFree / hipHostFree wait for the whole device (reaper.h)

@@ -49,7 +49,10 @@ class RcclLockstep : public LockstepTransport {
   int issue(const int64_t in[tk::kLockstepWords]) override;
   // Waits for a ticket's result.
   void wait(int ticket, int64_t out[tk::kLockstepWords]) override;
-  const char* words_mode() const { return mode_ == 0 ? "kernel" : mode_ == 1 ? "host" : "copy"; }
+  const char* words_mode() const {
+    return mode_ == 0 ? (graph_fallback_ ? "kernel (graph capture failed)" : "kernel")
+                      : mode_ == 1 ? "host" : mode_ == 2 ? "copy" : "graph";
+  }
   bool high_priority() const { return high_prio_; }
   bool ready(int ticket) override;
   // Failure detection: a round trip not complete after `ms` (a peer rank died or hung) aborts
@@ -86,7 +89,11 @@ class RcclLockstep : public LockstepTransport {
   int64_t* h_out_ = nullptr;   // pinned, device-mapped [slots][kLockstepWords]
   int64_t* h_in_dev_ = nullptr;   // their device addresses
   int64_t* h_out_dev_ = nullptr;
-  int mode_ = 0;               // 0 kernel, 1 host, 2 copy (TORCHKAFKA_RCCL_WORDS)
+  int mode_ = 0;               // 0 kernel, 1 host, 2 copy, 3 graph (TORCHKAFKA_RCCL_WORDS)
+  bool graph_fallback_ = false;
+  std::vector<void*> graphs_;  // mode 3: a hipGraphExec_t per slot (rccl_issue.hip)
+  void capture_graphs();
+  void release_graphs();
   bool high_prio_ = false;     // stream_ at the greatest priority (its own hardware-queue pool)
   std::vector<hipEvent_t> ev_;
   uint64_t issued_ = 0;

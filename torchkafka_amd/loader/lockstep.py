@@ -191,6 +191,32 @@ class LoaderLockstep:
                                          else "normal priority (shares the process's queues)")}
         return ls
 
+    def _torch_nccl_active(self) -> bool:
+        """torch makes its RCCL communicator (and streams) at a group's first collective: a DDP
+        job's gradient all-reduce does at world > 1 (bench.py's world-1 rehearsal says so)."""
+        try:
+            import torch.distributed as dist
+
+            return bool(dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"
+                        and (dist.get_world_size() > 1 or os.environ.get("TORCHKAFKA_TORCH_NCCL_ACTIVE") == "1"))
+        except Exception:  # noqa: BLE001
+            return False
+
+    def _decode_streams_fitting(self, copy_streams: int) -> int:
+        """Decode streams that fit beside the other streams of the process in its hardware queues,
+        when a collective shares the GPU with the loader (torch's NCCL stream, the RCCL lockstep);
+        otherwise the engine's default (3: the loader's own streams may share a queue)."""
+        try:
+            rccl = self._lockstep_transport() == "rccl" and os.environ.get("TORCHKAFKA_LOCKSTEP_PRIORITY") != "high"
+        except Exception:  # noqa: BLE001 - no process group to ask: no lockstep
+            rccl = False
+        nccl = self._torch_nccl_active()
+        if not (rccl or nccl):
+            return 3
+        hw = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+        reserved = 1 + int(nccl) + int(rccl) + copy_streams + (2 if self.plan.mirror else 0)  # mirror: 2 SDMA streams
+        return max(1, min(3, hw - reserved))
+
     def stream_plan(self) -> dict:
         """The HIP streams the live iteration uses, against the process's hardware queues
         (``GPU_MAX_HW_QUEUES``, 4 by default).  HIP binds streams to queues round-robin in creation
@@ -207,17 +233,8 @@ class LoaderLockstep:
             # a greatest-priority stream takes a queue from the high-priority pool, not these
             plan["rccl_lockstep"] = 0 if getattr(run.rccl, "high_priority", False) else 1
             plan["rccl_lockstep_high_priority"] = 1 - plan["rccl_lockstep"]
-        try:
-            import torch.distributed as dist
-
-            # torch makes its RCCL communicator (and streams) at a group's first collective: the
-            # lockstep never runs one on it, a DDP job's gradient all-reduce does (world > 1, or a
-            # world-1 group that ran one: bench.py's rehearsal of the N = 8 queue layout)
-            if (dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"
-                    and (dist.get_world_size() > 1 or os.environ.get("TORCHKAFKA_TORCH_NCCL_ACTIVE") == "1")):
-                plan["torch_nccl"] = 1
-        except Exception:  # noqa: BLE001
-            pass
+        # the lockstep never runs a collective on torch's group; a DDP job's gradient all-reduce does
+        plan["torch_nccl"] = int(self._torch_nccl_active())
         total = sum(v for k, v in plan.items() if k != "rccl_lockstep_high_priority")
         hw = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
         plan.update(total=total, hw_queues=hw, shared=total > hw)

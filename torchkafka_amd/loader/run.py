@@ -122,11 +122,16 @@ class _Run:
                 self.engine = hip().Engine(dev, self.ring.n_slots, self.ring.payload_capacity, L.copy_streams, mode)
                 if L.tuning.decode_streams is not None:  # before anything creates a decode stream
                     self.engine.set_decode_streams(int(L.tuning.decode_streams))
-                elif L._lockstep_transport() == "rccl":
-                    # HIP gives a process 4 hardware queues: the user's stream, two decode streams and
-                    # the lockstep's RCCL stream each keep one, so a collective waiting for the other
-                    # ranks never sits in front of a decode kernel those ranks' progress depends on
-                    self.engine.set_decode_streams(2)
+                else:
+                    # HIP gives a process GPU_MAX_HW_QUEUES (4) hardware queues and binds streams to
+                    # them round-robin: the user's stream, torch's NCCL stream (a DDP job's gradient
+                    # all-reduce), the RCCL lockstep's stream and the copy streams each keep one, the
+                    # decode streams take what is left (at most 3, at least 1) -- so a collective
+                    # waiting for the other ranks never sits in front of a decode kernel those ranks'
+                    # progress depends on, nor a decode kernel in front of the gradient all-reduce
+                    n = L._decode_streams_fitting(int(self.engine.copy_streams()))
+                    if n != int(self.engine.decode_streams()):
+                        self.engine.set_decode_streams(n)
                 if L.numa_bind:
                     topology.check_device(dev)
                 url, group = L._commit_target_url()
