@@ -97,6 +97,8 @@ def parse():
     ap.add_argument("--coalesce", type=int, default=None,
                     help="staged batches collated per kernel launch (default: the loader's, 6 for fixed width)")
     ap.add_argument("--coalesce-wait-us", type=int, default=50, help="adaptive coalescing wait while the GPU is busy")
+    ap.add_argument("--decode-streams", type=int, default=None,
+                    help="HIP streams for the device decode (default: the loader's, fitted to the hardware queues)")
     ap.add_argument("--no-numa", action="store_true", help="do not bind ranks to their GPU's NUMA node")
     ap.add_argument("--decode", default="auto", choices=["auto", "device", "host"],
                     help="device: gfx950 RecordBatch decode + CRC from the pinned logs; host: workers CRC-check + pack")
@@ -692,6 +694,7 @@ def run_rank(args) -> int:
             **({"lockstep_depth": args.lockstep_depth} if args.lockstep_depth is not None else {}),
             event_every=args.event_every, numa_bind=not args.no_numa,
             **({"coalesce": args.coalesce} if args.coalesce is not None else {}),
+            **({"decode_streams": args.decode_streams} if args.decode_streams is not None else {}),
             coalesce_wait_us=args.coalesce_wait_us, decode=args.decode,
             lockstep=lockstep if lockstep_mode is None else lockstep_mode,
             mirror_chunk_mib=args.mirror_chunk_mib, commit=commit, verify=verify or args.verify,

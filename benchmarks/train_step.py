@@ -17,7 +17,7 @@ loops are timed on the host between a synchronize before the first step and one 
 any wait of ``next()`` on a decode (the CRC verdict with ``verify="deliver"``) is inside.
 
 The model: Linear(256, H) -> GELU -> [Linear(H, H) -> GELU] x 2 -> Linear(H, 16), bf16, AdamW
-(fused); H = 8192 by default, ~0.9 ms per step at batch 256 on one MI355X.
+(fused); H = 8192 by default, 1.21 ms per step at batch 256 on one MI355X (profiles/r06_s3).
 
 Usage: python benchmarks/train_step.py [--workload config2|config4] [--h2d auto|zerocopy|dma]
 """
@@ -96,12 +96,17 @@ def run(args, sync=None) -> dict:
         model, opt = _model(torch, args.hidden, dev)
 
         def step(x):
+            if isinstance(x, (tuple, list)):  # var-len / JSON batches: (values, lengths)
+                x = x[0]
             loss = model(x).float().pow(2).mean()
             loss.backward()
             opt.step()
             opt.zero_grad(set_to_none=True)
 
-        staged = [next(it).clone() for _ in range(64)]
+        def first(x):
+            return x[0] if isinstance(x, (tuple, list)) else x
+
+        staged = [first(next(it)).clone() for _ in range(64)]
         for k in range(args.warmup):  # kernels chosen, optimiser state made, the loader warm
             step(staged[k % 64])
             next(it)

@@ -294,5 +294,5 @@ def test_async_commit_every_bounds_the_commit_lag(tmp_path, transport, commit_ev
         assert r["error"] is None, r["error"]
         assert r["steps"] == total and r["committed"] == list(range(total))
         lag = max(k - n for k, n in enumerate(r["committed_at_deliver"]))
-        assert lag <= 2 * (commit_every + depth) + 2, (lag, r["committed_at_deliver"][:40])
+        assert lag <= 3 * commit_every + depth + 3, (lag, r["committed_at_deliver"][:40])
         assert r["agreements"] >= total // commit_every

@@ -4,9 +4,9 @@ set -o pipefail
 O=gpurun_out/r06_s3
 mkdir -p $O
 ROOT=$PWD
-timeout -k 10 300 python -u -m pytest tests/test_gpu_teardown.py tests/test_gpu_sync_lockstep.py -x -v -p no:cacheprovider --timeout 150 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+timeout -k 10 300 python -u -m pytest tests/test_zz_gpu_rccl.py -x -v -p no:cacheprovider --timeout 150 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
 tail -8 $O/pytest.log; echo "pytest rc=$rc"; [ $rc -eq 0 ] || exit 1
-for wl in "config2 zerocopy" "config2 dma" "config4 auto"; do
+for wl in "config4 auto"; do
   set -- $wl
   timeout -k 10 200 python benchmarks/train_step.py --workload $1 --h2d $2 > $O/train_$1_$2.json 2> $O/train_$1_$2.err; rc=$?
   echo "train $1 $2 rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/train_$1_$2.err; exit 1; }

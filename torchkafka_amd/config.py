@@ -102,10 +102,10 @@ class Tuning:
             (0..64); None = auto: 32 under the RCCL lockstep with device decode (whose ring is then 64
             slots per worker deep, so an agreement's ~60-180 µs round trip is covered by the steps
             its credits still allow: profiles/r05_s24), else 2.
-        lockstep_commit_every: async lockstep: an agreement grants at most this many batches and a
-            fresh one is issued every half of it (a few in flight), so finished batches become
-            committable at least that often (0..4096; 0: one agreement grants whatever every rank
-            holds).  None = auto: 4 on the node-local shared-memory transport (an agreement costs
+        lockstep_commit_every: async lockstep: a fresh agreement every this many steps (a few in
+            flight, each granting at most twice that far ahead), so finished batches become
+            committable about that often (0..4096; 0: one agreement at a time grants whatever every
+            rank holds).  None = auto: 4 on the node-local shared-memory transport (an agreement costs
             well under a microsecond), 32 under RCCL, 0 over a process group's all-reduce.
         numa_bind: bind the loader (and its workers) to the target GPU's socket.
         ahead_depth: device-decode groups launched ahead of the user's request (0..16); None = 4.

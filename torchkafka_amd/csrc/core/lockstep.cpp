@@ -13,9 +13,10 @@ int64_t CreditLockstep::credit(LockstepSource& src) const {
 
 void CreditLockstep::issue(LockstepSource& src) {
   int64_t c = credit(src);
-  // commit_every: never grant past step + commit_every (granted_ is this ticket's base)
-  if (commit_every_ > 0 && !sync_ && c > step_ + commit_every_ - granted_)
-    c = std::max<int64_t>(0, step_ + commit_every_ - granted_);
+  // commit_every: never grant past step + 2 x commit_every (granted_ is this ticket's base): the next
+  // agreement, issued commit_every steps on, has another commit_every steps to come back
+  if (commit_every_ > 0 && !sync_ && c > step_ + 2 * commit_every_ - granted_)
+    c = std::max<int64_t>(0, step_ + 2 * commit_every_ - granted_);
   last_issue_step_ = step_;
   const int64_t w[kLockstepWords] = {c, step_, -step_, commit_status_};
   commit_status_ = kCommitOk;
@@ -88,11 +89,11 @@ int CreditLockstep::next_impl(LockstepSource& src, int64_t timeout_ms) {
       observe(t);
     }
     const bool low = tickets_.empty() && granted_ - step_ <= depth_;
-    // commit_every: a fresh agreement every commit_every / 2 steps, a few in flight, so batches
-    // become committable at that cadence without the host ever waiting for one round trip.  Every
-    // input to this decision (step, applied grant, tickets issued) is the same on every rank.
+    // commit_every: a fresh agreement every commit_every steps, a few in flight, so batches become
+    // committable at that cadence without the host ever waiting for one round trip.  Every input
+    // to this decision (step, applied grant, tickets issued) is the same on every rank.
     const bool cadence = commit_every_ > 0 && int(tickets_.size()) < kMaxInflight &&
-                         step_ - last_issue_step_ >= std::max(1, commit_every_ / 2);
+                         step_ - last_issue_step_ >= commit_every_;
     if (!no_more_credit_ && step_ < granted_ && (low || cadence)) {
       // issue ahead while credits remain, so the round trip overlaps the delivery of granted batches
       issue(src);

@@ -105,9 +105,9 @@ class CreditLockstep {
   void set_on_committable(std::function<void(std::vector<Watermark>&&)> f) { on_commit_ = std::move(f); }
   // Sync mode (see above).  Every rank must use the same mode: it decides which collectives run.
   void set_sync(bool s) { sync_ = s; }
-  // Async mode: an agreement grants at most `n` batches (0: whatever every rank holds), so one is
-  // issued at least every n steps and finished batches become committable that often.  Every rank
-  // must use the same value.
+  // Async mode: an agreement is issued every `n` steps and grants at most up to step + 2n (0: one
+  // agreement at a time, granting whatever every rank holds), so finished batches become
+  // committable about every n steps.  Every rank must use the same value.
   void set_commit_every(int n) { commit_every_ = n < 0 ? 0 : n; }
   int commit_every() const { return commit_every_; }
   bool sync() const { return sync_; }
