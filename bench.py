@@ -698,6 +698,7 @@ def run_rank(args) -> int:
             coalesce_wait_us=args.coalesce_wait_us, decode=args.decode,
             lockstep=lockstep if lockstep_mode is None else lockstep_mode,
             mirror_chunk_mib=args.mirror_chunk_mib, commit=commit, verify=verify or args.verify,
+            **({"lockstep_timeout": 120.0} if lockstep_mode == "rccl" and world > 1 else {}),
             **({"mirror_chunks": args.mirror_chunks} if args.mirror_chunks else {}),
             worker_init_fn=ds.init_worker(topic, bootstrap_servers=servers, group_id=group,
                                           auto_offset_reset="earliest", check_crcs=not args.no_crc),
@@ -756,7 +757,9 @@ def run_rank(args) -> int:
     # secondary blocks: fresh loaders (own consumer groups) over the same retained topic
     extra_out = {}
     other_verify = "commit" if args.verify == "deliver" else "deliver"
-    for name in extra:
+
+    def extra_block(name: str) -> None:
+        """One secondary steady block: a fresh loader (its own consumer group) over the retained topic."""
         dt = torch.float32 if name == "f32" else dtypes[args.dtype]
         own_group = False
         rccl_block = name in ("rccl", "rccl_sync")
@@ -819,6 +822,13 @@ def run_rank(args) -> int:
         if world > 1:
             R.barrier()
 
+    # the RCCL blocks at N > 1 run last (after the bridge blocks): the first multi-GPU runs of the
+    # native RCCL lockstep -- a failure there is reported in the line instead of ending the run
+    late = [b for b in extra if world > 1 and b in ("rccl", "rccl_sync")]
+    for name in extra:
+        if name not in late:
+            extra_block(name)
+
     # the Kafka-protocol route: this rank's partitions over a loopback wire server -> bridge replica
     bridge_out = None
     if bsteps > 0:
@@ -868,6 +878,15 @@ def run_rank(args) -> int:
                     R.barrier()
         finally:
             srv.close()
+
+    for name in late:
+        try:
+            extra_block(name)
+        except Exception as e:  # noqa: BLE001 - reported in the line
+            extra_out[f"steady_{name}"] = {"error": f"{type(e).__name__}: {e}"[:500]}
+            _progress(R, f"steady_{name} failed: {e}")
+            if world > 1:
+                R.barrier()
 
     config_out = run_config_blocks(R, args)
 
