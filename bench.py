@@ -141,10 +141,12 @@ def parse():
     ap.add_argument("--bridge-steps", type=int, default=None,
                     help="timed steps of the Kafka-protocol bridge blocks (async; sync runs a quarter): "
                          "default 8000 on a GPU, 20 on the CPU; 0 skips them")
-    ap.add_argument("--bridge-codecs", default="lz4,zstd",
+    ap.add_argument("--bridge-codecs", default="lz4,zstd,lz4_static",
                     help="comma list of compressed bridge blocks (bridge_<codec>: the wire server serves the "
                          "records as compressed RecordBatches, produced while the block runs, and the bridge's "
-                         "fetch threads inflate them): lz4, zstd, gzip; '' for none")
+                         "fetch threads inflate them): lz4, zstd, gzip, and <codec>_static (the whole topic "
+                         "produced before the timed steps: the bridge and the decode without the producer); "
+                         "'' for none")
     return ap.parse_args()
 
 
@@ -436,7 +438,8 @@ def _bridge_counters(loader) -> dict:
     return out
 
 
-def bridge_codec_block(R: "Rank", args, broker, mine, n_parts, codec, steps, warm, make_loader, server, dtype) -> dict:
+def bridge_codec_block(R: "Rank", args, broker, mine, n_parts, codec, steps, warm, make_loader, server, dtype,
+                       live: bool = True) -> dict:
     """bridge_<codec> (VERDICT r4 "do this" 6): the same records served as compressed RecordBatches.
 
     Setup (untimed): this rank's partitions of the topic are compressed batch by batch, as a
@@ -444,9 +447,13 @@ def bridge_codec_block(R: "Rank", args, broker, mine, n_parts, codec, steps, war
     gets the warm-up's share.  The rest is appended to the served topic when the timed steps start
     (a live topic whose producer runs ahead), so every timed batch was fetched, inflated by a
     bridge fetch thread straight into the replica log (codecs.h ``decompress_into``) and then
-    CRC-checked and decoded on the device inside the timed region."""
+    CRC-checked and decoded on the device inside the timed region.  ``live=False``: the whole topic
+    is produced before the timed steps (the bridge and the decode alone, without the producer).
+    ``producer``: when the producer's appends ended, against the timed region -- a producer still
+    appending at the end of the timed steps is what the bridge waited for (fetch_wait)."""
     B = args.batch_size
-    stage, topic = f"stage_{codec}", f"bench_{codec}"
+    tag = codec if live else f"{codec}_static"
+    stage, topic = f"stage_{tag}", f"bench_{tag}"
     broker.create_topic(stage, n_parts)
     broker.create_topic(topic, n_parts)
     per = int(math.ceil((warm + steps) * B * 1.1 / len(mine))) + B
@@ -454,8 +461,8 @@ def bridge_codec_block(R: "Rank", args, broker, mine, n_parts, codec, steps, war
     t = time.perf_counter()
     packed = broker.copy_compressed("bench", stage, codec, partitions=mine, max_records=per)
     compress_s = time.perf_counter() - t
-    broker.copy_compressed(stage, topic, None, partitions=mine, max_records=warm_per)
-    ld = make_loader(f"bench-bridge-{codec}", dtype, args.h2d, servers=server, topic=topic)
+    broker.copy_compressed(stage, topic, None, partitions=mine, max_records=warm_per if live else per)
+    ld = make_loader(f"bench-bridge-{tag}", dtype, args.h2d, servers=server, topic=topic)
     from torchkafka_amd import auto_commit
 
     bit = iter(auto_commit(ld))
@@ -463,16 +470,24 @@ def bridge_codec_block(R: "Rank", args, broker, mine, n_parts, codec, steps, war
         next(bit)
     c0 = _bridge_counters(ld)
     err = []
+    prod = {}
 
     def produce():
+        t = time.perf_counter()
         try:
-            broker.copy_compressed(stage, topic, None, partitions=mine, start_record=warm_per, max_records=per)
+            if live:
+                info = broker.copy_compressed(stage, topic, None, partitions=mine, start_record=warm_per,
+                                              max_records=per)
+                prod.update(batches=info["batches"], bytes=info["compressed_bytes"])
         except Exception as e:  # noqa: BLE001 - reported below
             err.append(e)
+        prod["start"], prod["end"] = t, time.perf_counter()
 
     pub = threading.Thread(target=produce, name=f"bench-produce-{codec}")
+    t_pub = time.perf_counter()
     pub.start()
     res = time_steps(R, bit, steps, ld)
+    t_end = time.perf_counter()
     pub.join()
     c1 = _bridge_counters(ld)
     if err:
@@ -505,6 +520,10 @@ def bridge_codec_block(R: "Rank", args, broker, mine, n_parts, codec, steps, war
         "inflater_time_share": {"inflate": round(inflate_s / inflater_s, 3),
                                 "other_ingest": round(other_ingest_s / inflater_s, 3)},
         "compress_setup_s": round(compress_s, 2),
+        "producer": ({"appends_s": round(prod["end"] - prod["start"], 4),
+                      "ended_before_timed_end_s": round(t_end - prod["end"], 4),
+                      "gb_per_s": round(prod.get("bytes", 0) / max(1e-9, prod["end"] - prod["start"]) / 1e9, 3)}
+                     if live else "the whole topic produced before the timed steps"),
         "bridge_errors": sum(br.errors for br in ld._bridges),
     })
     bit.close()
@@ -871,8 +890,10 @@ def run_rank(args) -> int:
                 if world > 1:
                     R.barrier()
             for codec in [c for c in args.bridge_codecs.split(",") if c]:
-                bridge_out[codec] = bridge_codec_block(R, args, broker, mine, n_parts, codec, bsteps, extra_warm,
-                                                       make_loader, srv.address, dtypes[args.dtype])
+                static = codec.endswith("_static")
+                name = codec[:-len("_static")] if static else codec
+                bridge_out[codec] = bridge_codec_block(R, args, broker, mine, n_parts, name, bsteps, extra_warm,
+                                                       make_loader, srv.address, dtypes[args.dtype], live=not static)
                 _progress(R, f"bridge {codec} {bridge_out[codec]['records_per_s']:.0f} rec/s")
                 if world > 1:
                     R.barrier()

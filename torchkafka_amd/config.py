@@ -96,7 +96,9 @@ class Tuning:
         event_every: record a completion event every k slots; None = ring slots / 4, at most 4.
         coalesce: staged batches collated per kernel launch (1..8; 1 disables).  None: 6 for fixed-width
             device decode (steady 51.3-51.8 M rec/s against 49.5-50.3 M with 8, 20-step window +2 %), 8
-            otherwise (JSON 49.1-49.5 M against 44.7-46.6 M with 6; profiles/r05_s45_coalesce).
+            when those rows also carry Key / Timestamp columns (label 44.2-48.1 M against 37.8-40.2 M
+            with 6, profiles/r06_s4) and otherwise (JSON 49.1-49.5 M against 44.7-46.6 M with 6;
+            profiles/r05_s45_coalesce).
         coalesce_wait_us: how long to wait for a fuller group while the GPU is busy (0..10000).
         lockstep_depth: steps before its credits run out that the next cross-rank agreement is issued
             (0..64); None = auto: 32 under the RCCL lockstep with device decode (whose ring is then 64

@@ -83,10 +83,13 @@ int CreditLockstep::next_impl(LockstepSource& src, int64_t timeout_ms) {
   } else {
     // agreements already back: their batches become committable now, in issue order (local: the
     // grants are applied where every rank applies them, below)
-    for (auto& t : tickets_) {
-      if (t.observed) continue;
-      if (!t_->ready(t.ticket)) break;
-      observe(t);
+    if (!tickets_.empty() && step_ - last_poll_step_ >= t_->ready_poll_every()) {
+      last_poll_step_ = step_;
+      for (auto& t : tickets_) {
+        if (t.observed) continue;
+        if (!t_->ready(t.ticket)) break;
+        observe(t);
+      }
     }
     const bool low = tickets_.empty() && granted_ - step_ <= depth_;
     // commit_every: a fresh agreement every commit_every steps, a few in flight, so batches become

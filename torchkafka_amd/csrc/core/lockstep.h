@@ -55,6 +55,9 @@ class LockstepTransport {
   virtual void wait(int ticket, int64_t out[kLockstepWords]) = 0;
   // wait(ticket) would return at once (a transport that computes the result in issue(): always)
   virtual bool ready(int ticket) { return true; }
+  // Steps between two ready() polls of an agreement in flight: a poll that costs a runtime call
+  // (hipEventQuery, ~1-2 us) is not made every step.
+  virtual int ready_poll_every() const { return 1; }
 };
 
 class LockstepError : public std::runtime_error {
@@ -154,6 +157,7 @@ class CreditLockstep {
   bool stopped_ = false, no_more_credit_ = false, sync_ = false;
   int commit_every_ = 0;
   int64_t last_issue_step_ = -1;
+  int64_t last_poll_step_ = -1;
   static constexpr int kMaxInflight = 3;  // agreements in flight under commit_every (transport slots >= 4)
   int64_t settled_step_ = -1;  // highest step an agreement was issued at and has completed
   int64_t commit_status_ = kCommitOk, group_status_ = kCommitOk;

@@ -263,7 +263,10 @@ class DeviceLoader(LoaderBridges, LoaderCommits, LoaderLockstep):
             process_overridden=self._process_overridden(), return_info=self.return_info,
             drop_last=self.drop_last, json_count_mode=getattr(tun, "json_count", "auto"))
         # fixed-width device decode: 6 batches per launch; JSON / var-len and the host paths: 8
-        self.coalesce = int(tun.coalesce) if tun.coalesce is not None else (6 if self.plan.span else 8)
+        # 6 for plain fixed-width device decode; 8 when the rows carry record fields (Key / Timestamp
+        # columns: label 44-48 M against 38-40 M with 6, profiles/r06_s4) and for everything else
+        self.coalesce = (int(tun.coalesce) if tun.coalesce is not None
+                         else 6 if self.plan.span and not self._n_extras() else 8)
         self._pending_wms: list = []   # finished-but-uncommitted watermark lists
         self._committed: dict[int, int] = {}
         # state_dict(global_step=True): every partition's position after the batches handed out
