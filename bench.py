@@ -141,7 +141,7 @@ def parse():
     ap.add_argument("--bridge-steps", type=int, default=None,
                     help="timed steps of the Kafka-protocol bridge blocks (async; sync runs a quarter): "
                          "default 8000 on a GPU, 20 on the CPU; 0 skips them")
-    ap.add_argument("--bridge-codecs", default="lz4,zstd,lz4_static",
+    ap.add_argument("--bridge-codecs", default="lz4,zstd",
                     help="comma list of compressed bridge blocks (bridge_<codec>: the wire server serves the "
                          "records as compressed RecordBatches, produced while the block runs, and the bridge's "
                          "fetch threads inflate them): lz4, zstd, gzip, and <codec>_static (the whole topic "

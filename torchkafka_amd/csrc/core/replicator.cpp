@@ -16,6 +16,7 @@ int64_t now_ms() {
 }  // namespace
 
 Replicator::Replicator(std::shared_ptr<Broker> local, ReplicaConfig cfg) : local_(std::move(local)), cfg_(std::move(cfg)) {
+  if (const char* e = std::getenv("TORCHKAFKA_BRIDGE_INFLIGHT")) max_inflight_ = std::max(1, std::min(16, std::atoi(e)));
   if (cfg_.topic.empty()) throw std::invalid_argument("replicator: a topic is required");
   if (cfg_.auto_offset_reset != "earliest" && cfg_.auto_offset_reset != "latest" &&
       cfg_.auto_offset_reset != "smallest" && cfg_.auto_offset_reset != "largest")
@@ -441,7 +442,7 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
           if (f->second == p->since.load()) continue;
           failed.erase(f);  // restarted by a rebalance since it failed
         }
-        if (p->inflight.load(std::memory_order_acquire) >= kMaxInflight) continue;  // its inflater is behind
+        if (p->inflight.load(std::memory_order_acquire) >= max_inflight_) continue;  // its inflater is behind
         if (throttled(*p)) {
           p->throttled.fetch_add(1, std::memory_order_relaxed);
           continue;
@@ -662,7 +663,7 @@ void Replicator::inflate_loop(Inflater* inf) {
     pd.p->inflight.fetch_sub(1, std::memory_order_acq_rel);
     lk.lock();
     pd.data.clear();
-    if (inf->spare.size() < size_t(kMaxInflight)) inf->spare.push_back(std::move(pd.data));
+    if (inf->spare.size() < size_t(max_inflight_)) inf->spare.push_back(std::move(pd.data));
     inf->done_cv.notify_all();
   }
   inf->q.clear();

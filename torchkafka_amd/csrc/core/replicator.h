@@ -175,8 +175,9 @@ class Replicator {
   };
   // A compressed partition's record set, received by a fetch thread into a buffer of its own and
   // inflated into the log by that thread's inflater (one per fetch thread), so the wait for the
-  // next Fetch response overlaps this one's inflation.  At most kMaxInflight per partition.
-  static constexpr int kMaxInflight = 2;
+  // next Fetch response overlaps this one's inflation.  At most max_inflight_ per partition
+  // (TORCHKAFKA_BRIDGE_INFLIGHT, default 2).
+  int max_inflight_ = 2;
   struct Pending {
     Part* p;
     uint64_t since;
