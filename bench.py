@@ -945,6 +945,7 @@ def run_rank(args) -> int:
                            f"({(steady if s_stats else args.steps) / max(1, (s_stats or stats)['commits']):.2f} "
                            "batches per commit)") + (
                     "" if not lock_info else ", RCCL lockstep" if lock_info.get("transport") == "rccl"
+                    else ", node-local shared-memory lockstep" if lock_info.get("transport") == "shm"
                     else f", lockstep ({lock_info.get('backend', 'host')} all-reduce)"),
                 "h2d": h2d_desc,
                 "decode": decode_desc,
