@@ -50,32 +50,11 @@ __device__ __forceinline__ bool is_ws(uint32_t c) { return c == 32u || c == 9u |
 // its byte i.  Returns the element count (commas + 1; 0 for an empty interior), or -1 when the row
 // is not simple; *guess is then the element count a flat array of that text has (commas + 1, 0
 // when the interior is empty or the text is not framed) -- the width its host parse will fill.
-//
-// Latency: the first 1 KiB pass is loaded before anything else, and the 16 bytes holding the last
-// byte with it (lane 0, when past that pass), so the framing check reads its two bytes out of
-// registers instead of two dependent single-byte loads ahead of the text's.
 template <class Load, class Byte>
 __device__ int32_t scan_row(Load&& load, Byte&& byte, int32_t T, int lane, int32_t* guess) {
   int32_t lo, hi;
   bool framed;
-  const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
-  const uint4 first = 16 * lane < T ? load(16 * lane) : zero;  // pass 0
-  const int32_t lastc = T >= 1 ? ((T - 1) & ~15) : 0;       // the 16 bytes holding byte T - 1
-  const uint4 tailv = (lane == 0 && lastc >= 64 * 16) ? load(lastc) : zero;
-  auto byte_of = [](const uint4& v, int32_t j) -> uint32_t {  // byte j (0..15) of a 16-byte vector
-    const uint32_t w = j < 8 ? (j < 4 ? v.x : v.y) : (j < 12 ? v.z : v.w);
-    return (w >> (8 * (j & 3))) & 0xFFu;
-  };
-  uint32_t b_first = 0, b_last = 0;
-  if (T >= 2) {
-    b_first = __shfl(byte_of(first, 0), 0, 64);
-    const int32_t j = (T - 1) & 15;
-    if (lastc < 64 * 16)
-      b_last = __shfl(byte_of(first, j), lastc >> 4, 64);
-    else
-      b_last = __shfl(byte_of(tailv, j), 0, 64);
-  }
-  if (T >= 2 && b_first == '[' && b_last == ']') {
+  if (T >= 2 && byte(0) == '[' && byte(T - 1) == ']') {
     lo = 1;
     hi = T - 1;
     framed = true;
@@ -102,7 +81,7 @@ __device__ int32_t scan_row(Load&& load, Byte&& byte, int32_t T, int lane, int32
     const int32_t c = base + 16 * lane;
     uint32_t tokm = 0;
     if (c < T) {
-      const uint4 v = base == 0 ? first : load(c);
+      const uint4 v = load(c);
       const int32_t l0 = lo - c, h0 = hi - c;
       uint32_t in = h0 <= 0 ? 0u : h0 >= 16 ? 0xFFFFu : (1u << h0) - 1u;
       if (l0 > 0) in &= l0 >= 16 ? 0u : ~((1u << l0) - 1u);
