@@ -91,6 +91,8 @@ def parse():
                     help="--h2d dma with device decode: MiB per hipMemcpyAsync into the HBM log mirror")
     ap.add_argument("--mirror-chunks", type=int, default=None, help="--h2d dma: HBM mirror buffers per partition")
     ap.add_argument("--lockstep-depth", type=int, default=None, help="default: the loader's auto depth")
+    ap.add_argument("--lockstep-commit-every", type=int, default=None,
+                    help="async lockstep: an agreement every n steps (default: the loader's, per transport)")
     ap.add_argument("--verify", default="deliver", choices=["deliver", "commit"],
                     help="deliver: a batch is handed out after its device CRC verdict landed (default); commit: "
                          "the verdict gates only its commit")
@@ -711,6 +713,8 @@ def run_rank(args) -> int:
             slots_per_worker=args.slots_per_worker, prefetch=args.prefetch, rank=rank, world_size=world,
             in_order=args.in_order, h2d=h2d, copy_streams=args.copy_streams,
             **({"lockstep_depth": args.lockstep_depth} if args.lockstep_depth is not None else {}),
+            **({"lockstep_commit_every": args.lockstep_commit_every} if args.lockstep_commit_every is not None
+               else {}),
             event_every=args.event_every, numa_bind=not args.no_numa,
             **({"coalesce": args.coalesce} if args.coalesce is not None else {}),
             **({"decode_streams": args.decode_streams} if args.decode_streams is not None else {}),

@@ -85,6 +85,7 @@ RcclLockstep::RcclLockstep(const std::string& lib_path, const std::string& id, i
     TKH_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   }
   mode_ = words_mode_env();
+  if (const char* pe = std::getenv("TORCHKAFKA_RCCL_POLL_EVERY")) poll_every_ = std::atoi(pe);
   TKH_HIP(hipMalloc(reinterpret_cast<void**>(&d_), sizeof(int64_t) * 2 * kW * size_t(slots_)));
   TKH_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_in_), sizeof(int64_t) * kW * size_t(slots_), hipHostMallocMapped));
   TKH_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_out_), sizeof(int64_t) * kW * size_t(slots_), hipHostMallocMapped));

@@ -55,9 +55,10 @@ class RcclLockstep : public LockstepTransport {
   }
   bool high_priority() const { return high_prio_; }
   bool ready(int ticket) override;
-  // a poll is a hipEventQuery (~1-2 us of host time): every 8th step (profiles/r06_s4: polled every
-  // step, commit_every=32 cost the loader 28 % at world 1)
-  int ready_poll_every() const override { return 8; }
+  // a poll is a hipEventQuery of the agreement's event: every poll_every_ steps
+  // (TORCHKAFKA_RCCL_POLL_EVERY, default 8; 0: never -- agreements are read where their grant
+  // is needed, as before round 6)
+  int ready_poll_every() const override { return poll_every_ > 0 ? poll_every_ : (1 << 30); }
   // Failure detection: a round trip not complete after `ms` (a peer rank died or hung) aborts
   // the communicator and raises instead of blocking forever; <= 0 waits indefinitely.
   void set_timeout_ms(int64_t ms) { timeout_ms_ = ms; }
@@ -93,6 +94,7 @@ class RcclLockstep : public LockstepTransport {
   int64_t* h_in_dev_ = nullptr;   // their device addresses
   int64_t* h_out_dev_ = nullptr;
   int mode_ = 0;               // 0 kernel, 1 host, 2 copy, 3 graph (TORCHKAFKA_RCCL_WORDS)
+  int poll_every_ = 8;
   bool graph_fallback_ = false;
   std::vector<void*> graphs_;  // mode 3: a hipGraphExec_t per slot (rccl_issue.hip)
   void capture_graphs();
