@@ -244,6 +244,8 @@ class Broker {
   IndexEntry entry(uint32_t pidx, int64_t i) { return mapped(pidx).idx[uint64_t(i) % part(pidx).index_capacity]; }
   // Turns an empty partition into a ring log of `bytes` (<= its capacity).
   void make_ring(uint32_t pidx, uint64_t bytes);
+  // Faults in the pages of partition pidx's ring (a replica's first pass through it then pays none).
+  void populate_ring(uint32_t pidx);
   // Ring logs: retires live batches that end at or below `keep_offset` (log start moves up), then
   // returns the write position with up to `want` contiguous bytes that overwrite no live batch
   // (wrapping to the ring's start when the tail is too short); *avail = those bytes (may be < want).

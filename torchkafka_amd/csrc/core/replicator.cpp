@@ -132,6 +132,7 @@ void Replicator::start() {
 // restarts, empty, at that offset (the log may hold a stale or overwritten range of it).
 void Replicator::start_parts(wire::Client& c, const std::vector<Part*>& ps, bool fresh) {
   if (ps.empty()) return;
+  std::vector<uint32_t> fresh_rings;
   std::vector<int32_t> ids;
   for (Part* p : ps) ids.push_back(p->partition);
   std::map<int32_t, int64_t> committed;
@@ -156,8 +157,10 @@ void Replicator::start_parts(wire::Client& c, const std::vector<Part*>& ps, bool
       p->fetch_offset = P.high_watermark.load();  // a persistent (file://) replica resumes its log
     } else {
       if (P.n_batches.load() != 0 || P.high_watermark.load() != start) local_->reset_partition(p->pidx, start);
-      if (cfg_.ring_bytes && P.ring_bytes.load() == 0)
+      if (cfg_.ring_bytes && P.ring_bytes.load() == 0) {
         local_->make_ring(p->pidx, std::min<uint64_t>(cfg_.ring_bytes, P.log_capacity));
+        fresh_rings.push_back(p->pidx);
+      }
       p->fetch_offset = start;
       p->released = 0;
     }
@@ -176,6 +179,10 @@ void Replicator::start_parts(wire::Client& c, const std::vector<Part*>& ps, bool
       }
     }
   }
+  // the new rings' pages, faulted in in parallel before the first fetch writes into them
+  std::vector<std::thread> th;
+  for (uint32_t pidx : fresh_rings) th.emplace_back([this, pidx] { local_->populate_ring(pidx); });
+  for (auto& t : th) t.join();
 }
 
 std::vector<int32_t> Replicator::join_group(wire::Client& c) {
