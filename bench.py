@@ -315,12 +315,53 @@ class Rank:
                 "rank_id_sum": s}
 
 
+def _thread_cpu(pids) -> dict:
+    """{(pid, tid, name): cpu seconds} of every thread of ``pids`` (Linux /proc; diagnostic)."""
+    out = {}
+    tick = os.sysconf("SC_CLK_TCK")
+    for pid in pids:
+        try:
+            tids = os.listdir(f"/proc/{pid}/task")
+        except OSError:
+            continue
+        for tid in tids:
+            try:
+                with open(f"/proc/{pid}/task/{tid}/stat") as f:
+                    s = f.read()
+            except OSError:
+                continue
+            name = s[s.index("(") + 1:s.rindex(")")]
+            f = s[s.rindex(")") + 2:].split()
+            out[(pid, int(tid), name)] = (int(f[11]) + int(f[12])) / tick  # utime + stime
+    return out
+
+
+def cpu_report(before: dict, after: dict, el: float, main_pid: int) -> dict:
+    """TK_BENCH_CPU=1: the threads that used the CPU during a timed block, in cores (CPU s / wall s)."""
+    used = sorted(((after[k] - before.get(k, 0.0), k) for k in after), reverse=True)
+    top = [{"who": "main" if k[0] == main_pid else "worker", "tid": k[1], "name": k[2], "cores": round(u / el, 2)}
+           for u, k in used[:12] if u > 0]
+    per = {}
+    for u, k in used:
+        w = "main" if k[0] == main_pid else "workers"
+        per[w] = per.get(w, 0.0) + u
+    return {"cores": {w: round(u / el, 2) for w, u in per.items()}, "threads": top,
+            "affinity": len(os.sched_getaffinity(0))}
+
+
 def time_steps(R: Rank, it, steps: int, loader, trace: list | None = None) -> dict:
     """Times ``steps`` batches: barrier + synchronize on both sides, max time over ranks.
-    ``trace`` (diagnostic): receives each step's end time and the closing sync's, from t0, in ns."""
+    ``trace`` (diagnostic): receives each step's end time and the closing sync's, from t0, in ns.
+    TK_BENCH_CPU=1 (diagnostic): the CPU time of every thread of this process and the loader's
+    workers over the block, in ``res["cpu"]``."""
     loader.reset_stats()
     R.sync()
     occ = loader.ring_occupancy()
+    cpu_pids = None
+    if os.environ.get("TK_BENCH_CPU") == "1":
+        run = getattr(loader, "_run", None)
+        cpu_pids = [os.getpid()] + [p.pid for p in getattr(run, "procs", []) if getattr(p, "pid", None)]
+        cpu0 = _thread_cpu(cpu_pids)
     t0 = time.perf_counter()
     rows = 0
     x = None
@@ -337,7 +378,10 @@ def time_steps(R: Rank, it, steps: int, loader, trace: list | None = None) -> di
     tmax = max(p[0] for p in per_rank)
     total = sum(p[1] for p in per_rank)
     st = loader.stats_summary()
-    return {"el": tmax, "rows": total, "per_rank": per_rank, "stats": st, "occ": occ, "last": x}
+    res = {"el": tmax, "rows": total, "per_rank": per_rank, "stats": st, "occ": occ, "last": x}
+    if cpu_pids:
+        res["cpu"] = cpu_report(cpu0, _thread_cpu(cpu_pids), el, os.getpid())
+    return res
 
 
 def window_trace(R: Rank, it, steps: int, n: int, loader) -> dict:
@@ -403,6 +447,8 @@ def steady_block(R: Rank, res: dict, steps: int, dim: int) -> dict:
         # HBM mirror: segments read from the pinned log instead (buffer busy / copy still in flight)
         out["mirror"] = {k: st.get(k, 0) for k in ("mirror_copies", "mirror_fallbacks", "mirror_pending_fallbacks",
                                                    "mirror_backoffs", "split_launches")}
+    if "cpu" in res:
+        out["cpu"] = res["cpu"]
     if R.world > 1:
         out["per_rank_records_per_s"] = [round(r / e, 1) for e, r in res["per_rank"]]
         out["lockstep_agreements"] = st.get("lockstep_agreements", 0)
