@@ -44,6 +44,9 @@ def parse(argv=None):
     ap.add_argument("--prefetch", type=int, default=2)
     ap.add_argument("--verify", default="deliver", choices=["deliver", "commit"])
     ap.add_argument("--coalesce", type=int, default=None, help="batches per launch (default: the loader's)")
+    ap.add_argument("--pad-to", type=int, default=None,
+                    help="a fixed width (e.g. --max-len): the parse kernel counts each row itself "
+                         "(no json_count_kernel); default: the batch's longest row, rounded up to pad_multiple")
     ap.add_argument("--lockstep", default="off", choices=["off", "rccl"],
                     help="rccl: the per-step RCCL agreement at world 1 (a one-rank nccl group), as under DDP")
     return ap.parse_args(argv)
@@ -85,6 +88,7 @@ def run(args, sync=None) -> dict:
                           slots_per_worker=args.slots_per_worker, event_every=args.event_every, prefetch=args.prefetch,
                           verify=args.verify, lockstep="rccl" if args.lockstep == "rccl" else True,
                           **({"coalesce": args.coalesce} if args.coalesce else {}),
+                          **({"pad_to": args.pad_to} if args.pad_to else {}),
                           worker_init_fn=Json.init_worker("json", bootstrap_servers=url, group_id="cfg4",
                                                           auto_offset_reset="earliest"))
         it = iter(auto_commit(dl))
@@ -123,6 +127,7 @@ def run(args, sync=None) -> dict:
                             if mirror_on else "device (json_span.hip from the pinned logs)")
                            if dl.plan.json_span else args.decode),
                 "json_count": "device" if dl.plan.json_count else "workers",
+                "pad_to": args.pad_to,
                 "timed_s": round(el, 4), "steps": args.steps,
                 "avg_record_bytes": round(text_bytes),
                 "last_batch_shape": list(x.shape),

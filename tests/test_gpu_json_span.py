@@ -309,3 +309,58 @@ def test_json_span_through_hbm_mirror(broker):
         assert torch.equal(_bits(x), _bits(y)) and torch.equal(ln, lm)
     assert broker.committed_offsets("gm", "t") == {0: 2000, 1: 2000}
     assert dl.stats_summary()["mirror_copies"] > 0
+
+
+@pytest.mark.parametrize("dtype,bs,rpb,lens,odd,nulls,pad_to,trunc", [
+    (torch.bfloat16, 256, 64, (16, 256), 0, 0, 256, False),  # BASELINE config 4's shape
+    (torch.float32, 50, 7, (0, 30), 4, 6, 32, False),         # worker-parsed and host-parsed rows, tombstones
+    (torch.float16, 64, 16, (0, 90), 5, 0, 40, True),         # rows cut to pad_to (max_len + truncate)
+])
+def test_json_fused_count_with_pad_to(broker, monkeypatch, dtype, bs, rpb, lens, odd, nulls, pad_to, trunc):
+    """A fixed width (pad_to): every parse block counts its own row (no json_count_kernel launch) and
+    the batch's last block reports the rows left to the host -- bit for bit json.loads + torch casts,
+    and the same bits as the separate count kernel (TORCHKAFKA_JSON_FUSED_COUNT=0)."""
+    from torchkafka_amd import JsonArray
+
+    rng = random.Random(bs * 7 + pad_to)
+    n = 4 * bs + 9
+    texts = _texts(rng, n, *lens, odd_every=odd, nulls_every=nulls)
+    # device-counted rows that are not simple (exponents: the host parses them at delivery)
+    texts = [t if t is None or i % 11 != 3 else b"[1.5e3, 2, -7.25e-1]" for i, t in enumerate(texts)]
+    _produce(broker, "f", 1, lambda p: texts, rpb)
+    DS = _dataset(JsonArray(max_len=pad_to, truncate=True) if trunc else JsonArray())
+    kw = dict(dtype=dtype, num_workers=1, pad_to=pad_to, return_mask=True, pad_value=-1.0, coalesce=4)
+    monkeypatch.setenv("TORCHKAFKA_JSON_FUSED_COUNT", "1")
+    got, dl = _run(broker, "f", DS, bs, "g-fused", **kw)
+    assert dl.plan.json_span and dl.plan.json_count
+    monkeypatch.setenv("TORCHKAFKA_JSON_FUSED_COUNT", "0")
+    ref, _ = _run(broker, "f", DS, bs, "g-sep", **kw)
+    exp = _expected(texts, bs, dtype, max_len=pad_to if trunc else None, pad=-1.0, pad_multiple=1)
+    assert len(got) == len(exp) == len(ref)
+    for (x, ln, m), (ex, el), (y, lm, my) in zip(got, exp, ref):
+        ex = torch.nn.functional.pad(ex.float(), (0, pad_to - ex.shape[1]), value=-1.0).to(dtype)
+        assert x.shape == ex.shape == (len(el), pad_to) and x.dtype == dtype
+        assert torch.equal(_bits(x.cpu()), _bits(ex)) and torch.equal(ln.cpu(), el)
+        assert torch.equal(_bits(x), _bits(y)) and torch.equal(ln, lm) and torch.equal(m, my)
+    assert broker.committed_offsets("g-fused", "f") == {0: n}
+
+
+@pytest.mark.parametrize("bad", [b"[1,,2]", b"{}"])
+def test_json_fused_count_malformed_row_raises_before_commit(broker, monkeypatch, bad):
+    from torchkafka_amd import DeviceLoader, JsonArray, auto_commit
+    from torchkafka_amd.client.errors import CorruptRecordException
+
+    monkeypatch.setenv("TORCHKAFKA_JSON_FUSED_COUNT", "1")
+
+    texts = [b"[1, 2]"] * 100 + [bad] + [b"[3]"] * 60
+    _produce(broker, "m", 1, lambda p: texts, 16)
+    DS = _dataset(JsonArray())
+    dl = DeviceLoader(DS.placeholder(), 32, num_workers=1, device="cuda:0", pad_to=8,
+                      worker_init_fn=DS.init_worker("m", bootstrap_servers=broker.url, group_id="g",
+                                                    auto_offset_reset="earliest", consumer_timeout_ms=300))
+    assert dl.plan.json_count
+    with pytest.raises(CorruptRecordException, match="not a flat numeric JSON array"):
+        for _x in auto_commit(dl):
+            torch.cuda.synchronize()
+    committed = broker.committed_offsets("g", "m").get(0)
+    assert committed is None or committed <= 96

@@ -48,10 +48,11 @@ void BatchVerdicts::ensure_status() {
   std::memset(jinfo_host_, 0, size_t(kWords) * 4 * sizeof(int32_t));
   jrows_.assign(size_t(kWords), {});
   jparsed_.assign(size_t(kWords), 0);
-  if (hipMalloc(reinterpret_cast<void**>(&ctr_dev_), size_t(kWords) * 2 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMemset(ctr_dev_, 0, size_t(kWords) * 2 * sizeof(unsigned long long)) != hipSuccess)
+  if (hipMalloc(reinterpret_cast<void**>(&ctr_dev_), size_t(kWords) * kCtrWords * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(ctr_dev_, 0, size_t(kWords) * kCtrWords * sizeof(unsigned long long)) != hipSuccess)
     throw std::runtime_error("driver: allocating the JSON count words failed");
   tag_.assign(size_t(kWords), 0);
+  done_.assign(size_t(kWords), 0);
 }
 
 void BatchVerdicts::ensure_partials() {

@@ -16,7 +16,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
-
 #include <deque>
 #include <memory>
 #include <string>
@@ -395,6 +394,12 @@ class MainDriver {
     return s;
   }
   int32_t json_mult_ = 1;
+  // a fixed JSON width (json_mult_ 0): the parse kernel counts each row itself, no json_count_kernel
+  // launch (TORCHKAFKA_JSON_FUSED_COUNT: 1 on, 0 the separate count kernel)
+  bool json_fused_count_ = [] {
+    const char* e = std::getenv("TORCHKAFKA_JSON_FUSED_COUNT");
+    return e && e[0] == '1';
+  }();
   // HBM staging ring of the device JSON parse (row texts between the two kernels, json_span.hip):
   // positions are monotonic, regions are freed in launch order as their groups' slots are released.
   static constexpr uint64_t kStageBytes = uint64_t(128) << 20;

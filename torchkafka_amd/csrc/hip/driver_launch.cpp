@@ -244,6 +244,7 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
   ga.pad = float(pad);
   ga.err_tag = tk::kSpanParseErrBit;
   ga.mult = json_mult_;
+  ga.fused_count = json_mult_ == 0 && json_fused_count_ ? 1 : 0;
   uint64_t off = base;
   for (int k = 0; k < n; ++k) {
     const SlotView& v = *views[k];
@@ -272,6 +273,7 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
     ga.err[k] = b.err;
     ga.row_base[k + 1] = ga.row_base[k] + int64_t(v.n_rows);
     ga.trunc[k] = v.trunc_len;
+    if (ga.ctr[k] && ga.fused_count) ga.done_base[k] = verdicts_->json_done_base(perrs[k], int64_t(v.n_rows));
     off += batch_bytes[k];
   }
   auto flush = [&]() {
@@ -303,8 +305,9 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
   for (int k = 0; k < n; ++k) devc = devc || ga.ctr[k] != nullptr;
   // a wave per row: counts, simple check, the width words.  Not fused into json_stage_kernel: its
   // few workgroups (one per segment) took 149 us per group doing it instead of 71 us, and config 4
-  // fell from 40.5 M to 35.5 M rec/s (profiles/r04_s4)
-  if (devc) eng_->run_on(stream, [ga, stream] { launch_json_count(ga, stream); });
+  // fell from 40.5 M to 35.5 M rec/s (profiles/r04_s4).  With a fixed width (pad_to) no row waits
+  // for another's count: the parse kernel's block of each row counts it (ga.fused_count).
+  if (devc && !ga.fused_count) eng_->run_on(stream, [ga, stream] { launch_json_count(ga, stream); });
   // the parse: a block per row over the staged texts, on the same stream
   eng_->run_on(stream, [ga, dst_dt, stream]() mutable { launch_json_group(ga, dst_dt, stream); });
   if (record_last) eng_->record_done(slots[n - 1], stream);

@@ -35,6 +35,7 @@
 
 #include "collate.h"
 #include "dtypes.h"
+#include "json_scan_dev.h"
 #include "json_token.h"
 #include "span.h"
 
@@ -62,6 +63,7 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
   __shared__ uint32_t starts[kMaxTok];
   __shared__ int s_wsum[kWaves];
   __shared__ int s_cut, s_bad;
+  __shared__ int32_t s_count, s_guess;
 
   int bk = 0;
 #pragma unroll
@@ -71,7 +73,8 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
   const uint8_t* __restrict__ vals = a.vals[bk];
   D* __restrict__ out = static_cast<D*>(a.out[bk]);
   int64_t L = a.L[bk];
-  if (a.ctr[bk]) {
+  const bool fused = a.ctr[bk] && a.fused_count;
+  if (a.ctr[bk] && !fused) {
     // device-counted batch: its width is the longest kept row (rounded up to the pad multiple),
     // within the capacity the host allocated; the first block reports it (and the rows left to
     // the host) through the host-mapped info words
@@ -96,6 +99,31 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
   int32_t* __restrict__ err = a.err[bk];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
   JsonRowDesc d = rows[r];
+  if (fused && d.count == tk::kJsonCountOnDevice && d.tlen >= 0 &&
+      uint64_t(d.off) + ((uint64_t(d.tlen) + 15u) & ~uint64_t(15)) <= a.vals_cap[bk]) {
+    // a fixed width (pad_to): this block counts its own row -- json_count_kernel's work, without its
+    // launch and its pass over the group.  Wave 0 runs json_scan_simple's rules on the staged text
+    // (16-byte aligned in HBM, L2-warm from the stage kernel); the others wait at the barrier.
+    if (wid == 0) {
+      const uint8_t* __restrict__ text = vals + d.off;
+      int32_t guess = 0;
+      const int32_t count = json_scan_row([&](int32_t c) { return *reinterpret_cast<const uint4*>(text + c); },
+                                          [&](int32_t i) { return uint32_t(text[i]); }, d.tlen, lane, &guess);
+      if (lane == 0) {
+        s_count = count;
+        s_guess = guess;
+      }
+    }
+    __syncthreads();
+    // a row that is not simple: the host parses it when the batch is delivered (its padding,
+    // lengths and mask are written below; the batch's "rows left to the host" word is raised)
+    const bool host = s_count < 0;
+    const int32_t c = host ? s_guess : s_count;
+    const int32_t tr = a.trunc[bk];
+    d = JsonRowDesc{d.off, host ? tk::kJsonCountOnDevice : d.tlen, c, tr >= 0 && c > tr ? tr : c};
+    if (host && tid == 0)
+      atomicMax(const_cast<unsigned long long*>(a.ctr[bk]) + 1, (static_cast<unsigned long long>(a.ctr_tag[bk]) << 32) | 1u);
+  }
   bool bad = false;  // block-uniform: only read after a barrier
   if (a.vals_cap[bk] > 0) {
     // staged by json_stage_kernel: a descriptor must stay inside the batch's staging area
@@ -226,6 +254,23 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
   }
   if (lengths && tid == 0) lengths[r] = n_out;
   if (err && bad && tid == 0 && (a.err_tag == 0 || *err < 0)) *err = a.err_tag | int32_t(r);
+  if (fused && tid == 0) {
+    // the batch's last block to get here reports {width, rows left to the host, 1}: ctr[2] counts
+    // the parse blocks of every fused launch of this word (never reset; the host passes the count
+    // before this launch), one atomicAdd per block
+    __threadfence();
+    const unsigned long long n0 = atomicAdd(const_cast<unsigned long long*>(a.ctr[bk]) + 2, 1ull);
+    if (int64_t(n0 + 1 - a.done_base[bk]) == a.row_base[bk + 1] - a.row_base[bk] && a.info[bk]) {
+      const unsigned long long tg = static_cast<unsigned long long>(a.ctr_tag[bk]) << 32;
+      const unsigned long long c1 =
+          __hip_atomic_load(const_cast<unsigned long long*>(a.ctr[bk]) + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      volatile int32_t* info = a.info[bk];
+      info[0] = int32_t(L);
+      info[1] = (c1 & 0xFFFFFFFF00000000ull) == tg ? 1 : 0;
+      __threadfence_system();
+      info[2] = 1;
+    }
+  }
 }
 
 template <typename D>
