@@ -136,14 +136,17 @@ _EDGE_TEXTS = [b"[1,2,3]", b"  [4, 5]  ", b"[]", b"[ ]", b"\n[7]\t", b"[1.5e3, 2
                b"[1e-7]", b"[" + b",".join(b"%d" % i for i in range(300)) + b"]", b"[0.1,0.2,0.30000000000000004]"]
 
 
-@pytest.mark.parametrize("pad_to,pad_multiple,dtype,bs", [(None, 8, torch.float32, 16), (None, 1, torch.bfloat16, 7),
-                                                          (320, 8, torch.float32, 16)])
-def test_json_device_count_edge_rows(broker, pad_to, pad_multiple, dtype, bs):
+@pytest.mark.parametrize("pad_to,pad_multiple,dtype,bs,fused", [
+    (None, 8, torch.float32, 16, "0"), (None, 1, torch.bfloat16, 7, "0"), (320, 8, torch.float32, 16, "0"),
+    (320, 8, torch.float32, 16, "1"), (304, 1, torch.bfloat16, 7, "1")])
+def test_json_device_count_edge_rows(broker, monkeypatch, pad_to, pad_multiple, dtype, bs, fused):
     """Device-counted rows (tuning.json_count): trimmed whitespace, empty arrays, exponents / NaN /
     Infinity / 17-digit tokens (not simple: parsed on the host at delivery), a 16-digit token (simple),
-    widths from the device max (or a fixed pad_to) -- bit for bit json.loads + torch casts."""
+    widths from the device max (or a fixed pad_to, counted by the count kernel or -- fused -- by the
+    parse kernel itself) -- bit for bit json.loads + torch casts."""
     from torchkafka_amd import JsonArray
 
+    monkeypatch.setenv("TORCHKAFKA_JSON_FUSED_COUNT", fused)
     rng = random.Random(bs)
     texts = [_EDGE_TEXTS[rng.randrange(len(_EDGE_TEXTS))] for _ in range(300)]
     _produce(broker, "e", 1, lambda p: texts, 11)
@@ -345,7 +348,8 @@ def test_json_fused_count_with_pad_to(broker, monkeypatch, dtype, bs, rpb, lens,
     assert broker.committed_offsets("g-fused", "f") == {0: n}
 
 
-@pytest.mark.parametrize("bad", [b"[1,,2]", b"{}"])
+@pytest.mark.parametrize("bad", [b"[1,,2]", b"5", b"[1, \"a\"]", b"[,]", b"{}", b"[1 2]", b"[1.2.3]", b" [1,,2] ",
+                                 b"[1234567890123456-7]"])
 def test_json_fused_count_malformed_row_raises_before_commit(broker, monkeypatch, bad):
     from torchkafka_amd import DeviceLoader, JsonArray, auto_commit
     from torchkafka_amd.client.errors import CorruptRecordException

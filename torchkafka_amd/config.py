@@ -65,6 +65,9 @@ PROCESS_ENV = {
                             "the stepping thread instead of, in order, on a thread of their own (csrc/hip/hip_queue.h)",
     "TORCHKAFKA_MIRROR_WAIT": "1: a mirror launch waits for the copy of a chunk still in flight instead of reading "
                               "that segment from the pinned log (round-3 behaviour; A/B only)",
+    "TORCHKAFKA_JSON_FUSED_COUNT": "1: with a fixed JSON width (pad_to) the parse kernel counts each device-counted "
+                                   "row itself instead of json_count_kernel (GPU time per group -12 %, end to end "
+                                   "within noise: profiles/r06_s12)",
 }
 
 

@@ -52,7 +52,6 @@ void BatchVerdicts::ensure_status() {
       hipMemset(ctr_dev_, 0, size_t(kWords) * kCtrWords * sizeof(unsigned long long)) != hipSuccess)
     throw std::runtime_error("driver: allocating the JSON count words failed");
   tag_.assign(size_t(kWords), 0);
-  done_.assign(size_t(kWords), 0);
 }
 
 void BatchVerdicts::ensure_partials() {

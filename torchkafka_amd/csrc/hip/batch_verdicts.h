@@ -38,17 +38,10 @@ class BatchVerdicts {
   uint32_t* partials_dev(int64_t w) const { return part_dev_ + w * kPartials; }
   int32_t* json_info_dev(int64_t w) const { return jinfo_dev_ + w * 4; }
   // Device-counted JSON: word w's count words in HBM (zeroed once: width, rows left to the host,
-  // parse blocks done, spare) and the tag of its current launch (the number of times w was taken:
+  // both tagged; two spare) and the tag of its current launch (the number of times w was taken:
   // higher than every earlier tag of these words).
   static constexpr int64_t kCtrWords = 4;
   unsigned long long* json_ctr_dev(int64_t w) const { return ctr_dev_ + w * kCtrWords; }
-  // Fused-count parse launches (JsonGroupArgs::fused_count): what word w's done counter
-  // (json_ctr_dev(w)[2]) holds before a launch of `rows` blocks, which it then accounts for.
-  uint64_t json_done_base(int64_t w, int64_t rows) {
-    const uint64_t b = done_[size_t(w)];
-    done_[size_t(w)] += uint64_t(rows);
-    return b;
-  }
   uint32_t ctr_tag(int64_t w) const { return tag_[size_t(w)]; }
 
   // 0 kernel pending, 1 clean, 2 malformed (read when the slot was released)
@@ -88,7 +81,6 @@ class BatchVerdicts {
   int32_t* jinfo_dev_ = nullptr;
   unsigned long long* ctr_dev_ = nullptr;  // [kWords][kCtrWords] count words (device memory)
   std::vector<uint32_t> tag_;
-  std::vector<uint64_t> done_;  // per word: parse blocks its fused-count launches added to ctr[2]
   std::vector<uint8_t> state_;
   std::vector<std::string> msg_;  // span decode: the message of a bad batch, by word
   std::vector<std::vector<HostRow>> jrows_;

@@ -71,10 +71,9 @@ struct JsonGroupArgs {
   int32_t* info[kMaxGroup];
   int32_t mult;
   // 1 (mult 0 only): no json_count_kernel ran -- each parse block counts its own device-counted
-  // row, and the batch's last block to finish stores info[k]: ctr[k][2] counts the blocks of every
-  // fused launch of the batch's word, done_base[k] what it held before this launch
+  // row and raises info[k][1] when it leaves the row to the host; json_report_kernel, launched
+  // behind the parse on the same stream, stores the width and the done flag
   int32_t fused_count;
-  uint64_t done_base[kMaxGroup];
 };
 void launch_json_group(JsonGroupArgs& a, int dst_dt, hipStream_t stream);
 // Device counting of a staged group (json_span.hip): before launch_json_group on the same stream.

@@ -273,7 +273,6 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
     ga.err[k] = b.err;
     ga.row_base[k + 1] = ga.row_base[k] + int64_t(v.n_rows);
     ga.trunc[k] = v.trunc_len;
-    if (ga.ctr[k] && ga.fused_count) ga.done_base[k] = verdicts_->json_done_base(perrs[k], int64_t(v.n_rows));
     off += batch_bytes[k];
   }
   auto flush = [&]() {

@@ -49,6 +49,12 @@ constexpr int kWaves = kThreads / kWave;
 constexpr int kWin = 2048;                    // bytes of text per window (one 8-byte slice per thread)
 constexpr int kLaneBytes = kWin / kThreads;   // 8 contiguous bytes classified per thread
 constexpr int kMaxTok = kWin / 2 + 1;         // a token needs >= 1 char and 1 separator
+// fused count: the byte classes of a row (json_scan_simple's rules), OR-ed over its windows
+constexpr int kClsOther = 1;     // a byte that is not [0-9.-], ',' or whitespace
+constexpr int kClsNumber = 2;    // a number character
+constexpr int kClsAny = 4;       // anything but whitespace
+constexpr int kClsLong = 8;      // a token that does not end within 17 bytes
+constexpr int kClsUnframed = 16;  // the text is not '[' ... ']' at its very ends
 
 template <typename D>
 __device__ __forceinline__ D pad_value(float p) { return Store<D>::cvt(p); }
@@ -64,6 +70,8 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
   __shared__ int s_wsum[kWaves];
   __shared__ int s_cut, s_bad;
   __shared__ int32_t s_count, s_guess;
+  __shared__ int32_t s_commas, s_cls;  // fused count: the row's commas and byte classes (kCls*)
+  __shared__ bool s_host;              // fused count: this block's row is left to the host (thread 0's)
 
   int bk = 0;
 #pragma unroll
@@ -98,31 +106,24 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
   uint8_t* __restrict__ mask = a.mask[bk];
   int32_t* __restrict__ err = a.err[bk];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  if (tid == 0) s_host = false;
   JsonRowDesc d = rows[r];
-  if (fused && d.count == tk::kJsonCountOnDevice && d.tlen >= 0 &&
-      uint64_t(d.off) + ((uint64_t(d.tlen) + 15u) & ~uint64_t(15)) <= a.vals_cap[bk]) {
-    // a fixed width (pad_to): this block counts its own row -- json_count_kernel's work, without its
-    // launch and its pass over the group.  Wave 0 runs json_scan_simple's rules on the staged text
-    // (16-byte aligned in HBM, L2-warm from the stage kernel); the others wait at the barrier.
-    if (wid == 0) {
-      const uint8_t* __restrict__ text = vals + d.off;
-      int32_t guess = 0;
-      const int32_t count = json_scan_row([&](int32_t c) { return *reinterpret_cast<const uint4*>(text + c); },
-                                          [&](int32_t i) { return uint32_t(text[i]); }, d.tlen, lane, &guess);
-      if (lane == 0) {
-        s_count = count;
-        s_guess = guess;
-      }
+  // A fixed width (pad_to) and a device-counted row: this block counts the row while it parses it
+  // -- json_count_kernel's work without its launch and its pass over the text.  The windows below
+  // classify every byte by json_scan_simple's rules (commas, bytes outside [0-9.-] / ',' /
+  // whitespace, '[' and ']' at the text's ends, runs of more than 16 number characters: the parse
+  // reports a token that does not end within 17 bytes); values are written up to the width (or
+  // the truncation) and the row's count, verdict and length are settled after its last window.
+  const int32_t tr = a.trunc[bk];
+  const bool intg = fused && d.count == tk::kJsonCountOnDevice && d.tlen >= 0 &&
+                    uint64_t(d.off) + ((uint64_t(d.tlen) + 15u) & ~uint64_t(15)) <= a.vals_cap[bk];
+  if (intg) {
+    const int64_t lim = tr >= 0 && int64_t(tr) < L ? int64_t(tr) : L;
+    d = JsonRowDesc{d.off, d.tlen, INT32_MAX, int32_t(lim)};
+    if (tid == 0) {
+      s_commas = 0;
+      s_cls = d.tlen < 2 ? kClsUnframed : 0;
     }
-    __syncthreads();
-    // a row that is not simple: the host parses it when the batch is delivered (its padding,
-    // lengths and mask are written below; the batch's "rows left to the host" word is raised)
-    const bool host = s_count < 0;
-    const int32_t c = host ? s_guess : s_count;
-    const int32_t tr = a.trunc[bk];
-    d = JsonRowDesc{d.off, host ? tk::kJsonCountOnDevice : d.tlen, c, tr >= 0 && c > tr ? tr : c};
-    if (host && tid == 0)
-      atomicMax(const_cast<unsigned long long*>(a.ctr[bk]) + 1, (static_cast<unsigned long long>(a.ctr_tag[bk]) << 32) | 1u);
   }
   bool bad = false;  // block-uniform: only read after a barrier
   if (a.vals_cap[bk] > 0) {
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
       d = JsonRowDesc{0, 0, 0, 0};
     }
   }
-  const int64_t n_out = d.n_out < L ? d.n_out : L;
+  int64_t n_out = d.n_out < L ? d.n_out : L;
   D* orow = out + r * L;
   int64_t pad_from = n_out;
 
@@ -150,6 +151,8 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
     const int T = d.tlen;
     int pend = 0;    // tokens starting before pend are done; text[pend-1] is a separator or pend starts a token
     int64_t k0 = 0;  // index of the first token of this window
+    int seen = 0;    // intg: bytes before `seen` were classified by an earlier window
+    bool long_tok = false;
     if (tid == 0) s_bad = 0;
     while (pend < T) {
       const int base = pend & ~15;
@@ -173,6 +176,34 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
       }
       const int lim = wlen - b0;  // valid bytes of this thread (may be <= 0 or > 8)
       if (lim < 8) tokm &= lim <= 0 ? 0u : ((1u << lim) - 1u);
+      if (intg) {  // block-uniform: the wave reductions below need every lane
+        // json_scan_simple's classes of the interior bytes this window is the first to see
+        uint32_t com = 0, oth = 0, num = 0;
+        bool unframed = false;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t c = ((j < 4 ? cw.x : cw.y) >> ((j & 3) * 8)) & 0xFFu;
+          const int pos = base + b0 + j;
+          const bool fresh = j < lim && pos >= seen;
+          const bool in = fresh && pos > 0 && pos < T - 1;
+          const bool isnum = c - 48u <= 9u || c == 46u || c == 45u;
+          com |= uint32_t(in && c == 44u) << j;
+          oth |= uint32_t(in && !isnum && c != 44u && !json_is_ws(c)) << j;
+          num |= uint32_t(in && isnum) << j;
+          unframed = unframed || (fresh && ((pos == 0 && c != '[') || (pos == T - 1 && c != ']')));
+        }
+        // one LDS atomic per wave (a per-lane atomic on one address serialises: 38 us per group
+        // against 17 us, profiles/r06_s12)
+        int nc = __popc(com);
+#pragma unroll
+        for (int o = 32; o; o >>= 1) nc += __shfl_xor(nc, o, kWave);
+        const int cls = (__ballot(oth != 0) ? kClsOther : 0) | (__ballot(num != 0) ? kClsNumber : 0) |
+                        (__ballot((com | oth | num) != 0) ? kClsAny : 0) | (__ballot(unframed) ? kClsUnframed : 0);
+        if (lane == 0) {
+          if (nc) atomicAdd(&s_commas, nc);
+          if (cls) atomicOr(&s_cls, cls);
+        }
+      }
       // the byte before this thread's 8: the last byte of the previous lane's (a shuffle, not a
       // byte read at an 8-byte lane stride, which is a 2-way bank conflict); lane 0 reads it
       const uint32_t pw = __shfl_up(cw.y, 1, kWave) >> 24;
@@ -212,7 +243,7 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
       }
       __syncthreads();
       // 2. parse; only the window's last token can be cut
-      bool lbad = false;
+      bool lbad = false, llong = false;
       for (int t = tid; t < total; t += kThreads) {
         float v;
         const int st0 = starts[t];
@@ -220,8 +251,9 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
         if (rc == 2) {
           s_cut = t;
         } else {
-          if (rc == 0) {
+          if (rc != 1) {
             lbad = true;
+            llong = llong || rc == 3;
             v = __builtin_nanf("");
           }
           const int64_t k = k0 + t;
@@ -229,11 +261,14 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
         }
       }
       if (lbad) s_bad = 1;
+      if (intg && llong) atomicOr(&s_cls, kClsLong);
       __syncthreads();
+      seen = base + wlen;
       const int cut = s_cut;
       if (cut < total) {
         if (base + int(starts[cut]) == pend) {  // one token longer than a window: no progress possible
-          bad = true;
+          bad = !intg;  // intg: a run of > 16 number characters, the host's row
+          long_tok = true;
           break;
         }
         k0 += cut;
@@ -244,7 +279,48 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
       }
       __syncthreads();  // buf/starts/s_wsum are rewritten by the next window
     }
-    bad = bad || s_bad != 0 || k0 != d.count;
+    if (intg) {
+      __syncthreads();  // the classes of every window
+      const int cls = s_cls;
+      const int32_t commas = s_commas;
+      bool simple;
+      int32_t count, guess;
+      if (cls & kClsUnframed) {
+        // not '[' ... ']' at the very ends (whitespace around them, or no framing at all): the
+        // wave-0 scan of the staged text decides (json_scan_simple's trimming), as json_count_kernel
+        if (wid == 0) {
+          int32_t g = 0;
+          const int32_t c = json_scan_row([&](int32_t o) { return *reinterpret_cast<const uint4*>(text + o); },
+                                          [&](int32_t i) { return uint32_t(text[i]); }, T, lane, &g);
+          if (lane == 0) {
+            s_count = c;
+            s_guess = g;
+          }
+        }
+        __syncthreads();
+        count = s_count;
+        guess = s_guess;
+        simple = count >= 0;
+      } else {
+        simple = !(cls & (kClsOther | kClsLong)) && !long_tok && ((cls & kClsNumber) || commas == 0);
+        count = (cls & kClsNumber) ? commas + 1 : 0;
+        guess = (cls & kClsAny) ? commas + 1 : 0;
+      }
+      if (simple) {
+        bad = bad || s_bad != 0 || k0 != count;
+        n_out = tr >= 0 && count > tr ? tr : count;
+      } else {
+        // not simple: the host parses the row at delivery; its padding, lengths and mask here
+        bad = false;
+        n_out = tr >= 0 && guess > tr ? tr : guess;
+        pad_from = 0;
+        if (tid == 0) s_host = true;
+      }
+      if (n_out > L) n_out = L;
+      if (simple) pad_from = n_out;
+    } else {
+      bad = bad || s_bad != 0 || k0 != d.count;
+    }
   }
   // padding, lengths, mask
   for (int64_t k = pad_from + tid; k < L; k += kThreads) orow[k] = pad_value<D>(pad);
@@ -254,28 +330,30 @@ __global__ __launch_bounds__(kThreads) void json_rows_kernel(JsonGroupArgs a) {
   }
   if (lengths && tid == 0) lengths[r] = n_out;
   if (err && bad && tid == 0 && (a.err_tag == 0 || *err < 0)) *err = a.err_tag | int32_t(r);
-  if (fused && tid == 0) {
-    // the batch's last block to get here reports {width, rows left to the host, 1}: ctr[2] counts
-    // the parse blocks of every fused launch of this word (never reset; the host passes the count
-    // before this launch), one atomicAdd per block
-    __threadfence();
-    const unsigned long long n0 = atomicAdd(const_cast<unsigned long long*>(a.ctr[bk]) + 2, 1ull);
-    if (int64_t(n0 + 1 - a.done_base[bk]) == a.row_base[bk + 1] - a.row_base[bk] && a.info[bk]) {
-      const unsigned long long tg = static_cast<unsigned long long>(a.ctr_tag[bk]) << 32;
-      const unsigned long long c1 =
-          __hip_atomic_load(const_cast<unsigned long long*>(a.ctr[bk]) + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-      volatile int32_t* info = a.info[bk];
-      info[0] = int32_t(L);
-      info[1] = (c1 & 0xFFFFFFFF00000000ull) == tg ? 1 : 0;
-      __threadfence_system();
-      info[2] = 1;
-    }
+  if (fused && tid == 0 && s_host && a.info[bk]) {
+    // a row left to the host: the batch's "rows left to the host" word (host-mapped; rare).  The
+    // width and the done flag come from json_report_kernel once every block finished -- a done
+    // counter per block was one device-scope atomic on one address per row, serialised at memory:
+    // 28.8 us per group against 17.1 us without it (profiles/r06_s12)
+    a.info[bk][1] = 1;
+    __threadfence_system();
   }
 }
 
 template <typename D>
 void launch_json_t(const JsonGroupArgs& a, int64_t total_rows, hipStream_t stream) {
   hipLaunchKernelGGL((json_rows_kernel<D>), dim3(unsigned(total_rows)), dim3(kThreads), 0, stream, a);
+}
+
+// After a fused-count parse launch, on its stream: each device-counted batch's {width, -, done}
+// (the parse blocks raised "rows left to the host" themselves).  One wave, a lane per batch.
+__global__ void json_report_kernel(JsonGroupArgs a) {
+  const int k = int(threadIdx.x);
+  if (k >= a.n || !a.ctr[k] || !a.info[k]) return;
+  volatile int32_t* info = a.info[k];
+  info[0] = int32_t(a.L[k]);
+  __threadfence_system();
+  info[2] = 1;
 }
 
 void launch_json_args(JsonGroupArgs& a, int dst_dt, hipStream_t stream) {
@@ -293,6 +371,7 @@ void launch_json_args(JsonGroupArgs& a, int dst_dt, hipStream_t stream) {
     case kFP8E4M3: launch_json_t<fp8e4m3>(a, total, stream); break;
     default: throw std::invalid_argument("json collate: destination must be a float dtype");
   }
+  if (a.fused_count) hipLaunchKernelGGL(json_report_kernel, dim3(1), dim3(64), 0, stream, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("json collate launch: ") + hipGetErrorString(e));
 }

@@ -81,7 +81,7 @@ __device__ __forceinline__ int parse_token_regs(const uint8_t* buf, int s, int a
       }
     }
   }
-  if (!ended) return 0;  // longer than a simple number
+  if (!ended) return 3;  // 17 number characters: longer than a simple number (json_scan_simple's run rule)
   if (endc == 0x100u) {
     if (!last_window) return 2;
     return 0;  // text ended inside a number
