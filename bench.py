@@ -333,20 +333,29 @@ def _thread_cpu(pids) -> dict:
             name = s[s.index("(") + 1:s.rindex(")")]
             f = s[s.rindex(")") + 2:].split()
             out[(pid, int(tid), name)] = (int(f[11]) + int(f[12])) / tick  # utime + stime
+            out[("cpu", int(tid), name)] = int(f[36])  # the CPU it last ran on
     return out
 
 
 def cpu_report(before: dict, after: dict, el: float, main_pid: int) -> dict:
     """TK_BENCH_CPU=1: the threads that used the CPU during a timed block, in cores (CPU s / wall s)."""
+    last_cpu = {k[1]: v for k, v in after.items() if k[0] == "cpu"}
+    after = {k: v for k, v in after.items() if k[0] != "cpu"}
     used = sorted(((after[k] - before.get(k, 0.0), k) for k in after), reverse=True)
-    top = [{"who": "main" if k[0] == main_pid else "worker", "tid": k[1], "name": k[2], "cores": round(u / el, 2)}
-           for u, k in used[:12] if u > 0]
+    top = [{"who": "main" if k[0] == main_pid else "worker", "tid": k[1], "name": k[2], "cores": round(u / el, 2),
+            "cpu": last_cpu.get(k[1])} for u, k in used[:12] if u > 0]
     per = {}
     for u, k in used:
         w = "main" if k[0] == main_pid else "workers"
         per[w] = per.get(w, 0.0) + u
+    aff = {}
+    for pid in sorted({k[0] for k in after}):
+        try:
+            aff["main" if pid == main_pid else str(pid)] = len(os.sched_getaffinity(pid))
+        except OSError:
+            pass
     return {"cores": {w: round(u / el, 2) for w, u in per.items()}, "threads": top,
-            "affinity": len(os.sched_getaffinity(0))}
+            "affinity": len(os.sched_getaffinity(0)), "affinity_of": aff}
 
 
 def time_steps(R: Rank, it, steps: int, loader, trace: list | None = None) -> dict:
