@@ -344,10 +344,11 @@ def cpu_report(before: dict, after: dict, el: float, main_pid: int) -> dict:
     used = sorted(((after[k] - before.get(k, 0.0), k) for k in after), reverse=True)
     top = [{"who": "main" if k[0] == main_pid else "worker", "tid": k[1], "name": k[2], "cores": round(u / el, 2),
             "cpu": last_cpu.get(k[1])} for u, k in used[:12] if u > 0]
-    per = {}
+    per, by_name = {}, {}
     for u, k in used:
         w = "main" if k[0] == main_pid else "workers"
         per[w] = per.get(w, 0.0) + u
+        by_name[f"{w}:{k[2]}"] = by_name.get(f"{w}:{k[2]}", 0.0) + u
     aff = {}
     for pid in sorted({k[0] for k in after}):
         try:
@@ -355,6 +356,7 @@ def cpu_report(before: dict, after: dict, el: float, main_pid: int) -> dict:
         except OSError:
             pass
     return {"cores": {w: round(u / el, 2) for w, u in per.items()}, "threads": top,
+            "by_name": {n: round(u / el, 2) for n, u in sorted(by_name.items(), key=lambda x: -x[1]) if u > 0},
             "affinity": len(os.sched_getaffinity(0)), "affinity_of": aff}
 
 

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <pthread.h>
 #include <time.h>
 
 namespace tk {
@@ -51,6 +52,10 @@ inline int64_t wall_ms() {
   clock_gettime(CLOCK_REALTIME, &ts);
   return int64_t(ts.tv_sec) * 1000LL + ts.tv_nsec / 1000000;
 }
+
+// Names the calling thread (<= 15 characters) so a per-thread CPU census (/proc/<pid>/task/*/comm,
+// bench.py TK_BENCH_CPU=1) tells the native threads apart.
+inline void name_thread(const char* name) { pthread_setname_np(pthread_self(), name); }
 
 inline void cpu_relax() {
 #if defined(__x86_64__)

@@ -408,6 +408,7 @@ void Replicator::reset_offset(wire::Client& c, Part& p) {
 }
 
 void Replicator::fetch_loop(std::vector<Part*> mine) {
+  name_thread("tk-bridge-fetch");
   std::unique_ptr<wire::Client> c;
   std::map<Part*, uint64_t> failed;  // -> assignment epoch at the failure
   int backoff_ms = 0;
@@ -659,6 +660,7 @@ void Replicator::fetch_loop(std::vector<Part*> mine) {
 }
 
 void Replicator::inflate_loop(Inflater* inf) {
+  name_thread("tk-inflate");
   std::unique_lock<std::mutex> lk(inf->m);
   while (true) {
     inf->cv.wait(lk, [&] { return inf->stop || !inf->q.empty(); });
@@ -808,6 +810,7 @@ int Replicator::flush_commits() {
 }
 
 void Replicator::commit_loop() {
+  name_thread("tk-bridge-cmt");
   int backoff_ms = cfg_.commit_interval_ms;
   while (!stop_.load()) {
     uint64_t serving;
@@ -880,6 +883,7 @@ std::vector<int64_t> Replicator::take_forward_ns() {
 // so releases come in rare bursts: once some partition has release_step (1 GiB) releasable bytes,
 // every partition releases what it can in one punch each, back to back.
 void Replicator::release_loop() {
+  name_thread("tk-bridge-rel");
   constexpr uint64_t kAlign = 2u << 20;
   while (!stop_.load()) {
     sleep_ms(10);

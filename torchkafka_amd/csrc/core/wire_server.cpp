@@ -151,6 +151,7 @@ void WireServer::stop() {
 }
 
 void WireServer::accept_loop() {
+  name_thread("tk-wire-accept");
   while (!stop_.load()) {
     pollfd p{listen_fd_, POLLIN, 0};
     if (::poll(&p, 1, 100) <= 0) continue;
@@ -167,6 +168,7 @@ void WireServer::accept_loop() {
 }
 
 void WireServer::serve(int fd) {
+  name_thread("tk-wire-serve");
   std::vector<uint8_t> req;
   while (!stop_.load()) {
     uint32_t n;

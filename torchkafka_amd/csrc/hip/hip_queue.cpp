@@ -155,6 +155,7 @@ void HipQueue::wait(uint64_t seq) {
 }
 
 void HipQueue::run() {
+  tk::name_thread("tk-hip-queue");
   (void)hipSetDevice(device_);  // a failure shows in the first queued call
   uint64_t next = 1;
   int idle = 0;

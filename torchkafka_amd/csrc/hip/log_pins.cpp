@@ -163,6 +163,7 @@ void LogPins::ensure(uint32_t pidx, uint64_t end) {
 // The pin thread: demands first (the launch thread is waiting), then one chunk for any tracked
 // partition whose written end has passed its pinned end; otherwise a 1 ms nap.
 void LogPins::pin_loop() {
+  tk::name_thread("tk-log-pins");
   std::unique_lock<std::mutex> l(pm_);
   while (!stop_) {
     uint32_t pidx = UINT32_MAX;
