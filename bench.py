@@ -905,6 +905,8 @@ def run_rank(args) -> int:
     # the RCCL blocks at N > 1 run last (after the bridge blocks): the first multi-GPU runs of the
     # native RCCL lockstep -- a failure there is reported in the line instead of ending the run
     late = [b for b in extra if world > 1 and b in ("rccl", "rccl_sync")]
+    if os.environ.get("TK_BENCH_TEST_LATE_HANG") == "1" and world > 1:
+        late.append("test_hang")  # tests only: a late block that never returns (the watchdog's path)
     for name in extra:
         if name not in late:
             extra_block(name)
@@ -961,23 +963,10 @@ def run_rank(args) -> int:
         finally:
             srv.close()
 
-    for name in late:
-        try:
-            extra_block(name)
-        except Exception as e:  # noqa: BLE001 - reported in the line
-            extra_out[f"steady_{name}"] = {"error": f"{type(e).__name__}: {e}"[:500]}
-            _progress(R, f"steady_{name} failed: {e}")
-            if world > 1:
-                R.barrier()
-
     config_out = run_config_blocks(R, args)
 
-    if rank == 0:
-        if args.stats:
-            print(json.dumps({"loader_stats": stats, "fill_s": t_fill,
-                              "committed_sample": dict(list(committed.items())[:4])}),
-                  file=sys.stderr)
-        out = {
+    def make_out() -> dict:
+        return {
             "metric": BASELINE_METRIC,
             "value": round(value, 1),
             "unit": "records/s",
@@ -1036,10 +1025,57 @@ def run_rank(args) -> int:
             # the native binaries that ran, with the source sha compiled into each (ops.build_info)
             "native_build": _native_build(),
         }
-        print(json.dumps(out), flush=True)
+
+    # The RCCL blocks at N > 1 run last, under a watchdog: the first multi-GPU runs of the native
+    # RCCL lockstep must not cost the job its line.  A block that fails is reported in the line; if
+    # they have not finished by the deadline (a hang in RCCL itself), every rank's watchdog puts the
+    # line out without them (rank 0) and leaves.
+    printed = threading.Lock()
+    emitted = []
+
+    def emit() -> None:
+        with printed:
+            if rank == 0 and not emitted:
+                print(json.dumps(make_out()), flush=True)
+            emitted.append(1)
+
+    late_done = threading.Event()
+    if late:
+        late_s = float(os.environ.get("TK_BENCH_LATE_TIMEOUT", "300"))
+
+        def watchdog() -> None:
+            if late_done.wait(late_s):
+                return
+            for name in late:
+                extra_out.setdefault(f"steady_{name}", {"error": f"did not finish within {late_s:.0f} s (watchdog)"})
+            _progress(R, f"RCCL blocks did not finish within {late_s:.0f} s: the line goes out without them")
+            emit()
+            if rank == 0:
+                broker.destroy()
+            sys.stdout.flush()
+            os._exit(0)
+
+        threading.Thread(target=watchdog, daemon=True, name="bench-late-watchdog").start()
+    for name in late:
+        try:
+            if name == "test_hang":
+                time.sleep(3600)
+            extra_block(name)
+        except Exception as e:  # noqa: BLE001 - reported in the line
+            extra_out[f"steady_{name}"] = {"error": f"{type(e).__name__}: {e}"[:500]}
+            _progress(R, f"steady_{name} failed: {e}")
+            if world > 1:
+                R.barrier()
+
+    if rank == 0 and args.stats:
+        print(json.dumps({"loader_stats": stats, "fill_s": t_fill,
+                          "committed_sample": dict(list(committed.items())[:4])}),
+              file=sys.stderr)
+    emit()
     if world > 1:
-        R.barrier()
+        R.barrier()  # still under the watchdog: a rank stuck in RCCL must not hold the others here
         dist.destroy_process_group()
+    late_done.set()
     if rank == 0:
         broker.destroy()
     return 0

@@ -48,6 +48,20 @@ def test_bench_two_ranks_gloo_cpu():
     assert out["value"] > 0 and out["steady_state"]["records_per_s"] > 0
 
 
+def test_bench_late_block_watchdog_still_prints_the_line():
+    """A late (RCCL) block that hangs on every rank: each rank's watchdog gives up after
+    TK_BENCH_LATE_TIMEOUT, rank 0 prints the one line with the block marked, and the job exits 0."""
+    r = _torchrun(2, "bench.py", "--gpus", "2", "--steps", "20", "--warmup", "5", "--device", "cpu",
+                  "--steady-steps", "40", "--extra-blocks", "", "--workers", "1", "--partitions-per-gpu", "2",
+                  "--bridge-steps", "0", env={"TK_BENCH_TEST_LATE_HANG": "1", "TK_BENCH_LATE_TIMEOUT": "8"})
+    assert r.returncode == 0, r.stdout[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["value"] > 0
+    assert "watchdog" in out["steady_test_hang"]["error"]
+
+
 def _bench(*args, timeout=240):
     e = dict(os.environ)
     e.pop("WORLD_SIZE", None)
