@@ -107,7 +107,9 @@ std::vector<at::Tensor> alloc_extras(MainDriver& d, const std::vector<int64_t>& 
   int64_t* dsts[kMaxGroup];
   int64_t off = 0;
   for (size_t k = 0; k < rows.size(); ++k) {
-    out.push_back(all.narrow(0, off, rows[k] * extras).view({extras, rows[k]}));
+    // one column (a Key): the [rows] column itself, so delivery hands it out without a select
+    // (the label block runs host-bound at ~5 us per step: every view made per batch shows)
+    out.push_back(extras == 1 ? all.narrow(0, off, rows[k]) : all.narrow(0, off, rows[k] * extras).view({extras, rows[k]}));
     dsts[k] = out.back().data_ptr<int64_t>();
     off += rows[k] * extras;
   }
@@ -118,6 +120,9 @@ std::vector<at::Tensor> alloc_extras(MainDriver& d, const std::vector<int64_t>& 
 // The item a fixed-width step hands out: the values, or (values, column 0, column 1, ...).
 py::object fixed_item(const at::Tensor& out, const at::Tensor& ext) {
   if (!ext.defined()) return py::reinterpret_steal<py::object>(THPVariable_Wrap(out));
+  if (ext.dim() == 1)  // one column, already [rows] (alloc_extras)
+    return py::make_tuple(py::reinterpret_steal<py::object>(THPVariable_Wrap(out)),
+                          py::reinterpret_steal<py::object>(THPVariable_Wrap(ext)));
   py::list items;
   items.append(py::reinterpret_steal<py::object>(THPVariable_Wrap(out)));
   for (int64_t i = 0; i < ext.size(0); ++i) items.append(py::reinterpret_steal<py::object>(THPVariable_Wrap(ext[i])));
@@ -348,7 +353,8 @@ py::tuple step_once(MainDriver& d, const MainDriver::FastConfig& cfg) {
     if (r < cfg.shape[0]) {
       out = out.narrow(0, 0, r);
       // a short batch's columns were written back to back: [extras, r] from the block's start
-      if (e.defined()) e = e.reshape({-1}).narrow(0, 0, e.size(0) * r).view({e.size(0), r});
+      if (e.defined())
+        e = e.dim() == 1 ? e.narrow(0, 0, r) : e.reshape({-1}).narrow(0, 0, e.size(0) * r).view({e.size(0), r});
     }
     return py::make_tuple(r, cs, fixed_item(out, e));
   }
