@@ -360,6 +360,42 @@ def cpu_report(before: dict, after: dict, el: float, main_pid: int) -> dict:
             "affinity": len(os.sched_getaffinity(0)), "affinity_of": aff}
 
 
+class BlockGuard:
+    """Iterator wrapper for a secondary block: its first exception is kept instead of raised, and the
+    loader is closed at once (a lockstep transport then leaves, so the other ranks' blocks fail
+    within milliseconds instead of waiting out the lockstep timeout); next() then returns None.
+    time_steps() gathers every rank's flag and raises on every rank at the same point, so the
+    ranks leave a failed block with the same collectives behind them."""
+
+    def __init__(self, it, loader):
+        self.it, self.loader, self.error = it, loader, None
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        if self.error is not None:
+            return None
+        try:
+            return next(self.it)
+        except StopIteration:
+            raise
+        except Exception as e:  # noqa: BLE001 - raised by time_steps on every rank
+            self.fail(e.with_traceback(None))  # (a kept traceback would keep the generator's frame alive)
+            return None
+
+    def fail(self, e: BaseException) -> None:
+        self.error = e
+        for close in (self.it.close, self.loader.close):  # the iteration's lockstep transport, the loader
+            try:
+                close()
+            except Exception:  # noqa: BLE001
+                pass
+
+    def close(self) -> None:
+        self.it.close()
+
+
 def time_steps(R: Rank, it, steps: int, loader, trace: list | None = None) -> dict:
     """Times ``steps`` batches: barrier + synchronize on both sides, max time over ranks.
     ``trace`` (diagnostic): receives each step's end time and the closing sync's, from t0, in ns.
@@ -378,6 +414,8 @@ def time_steps(R: Rank, it, steps: int, loader, trace: list | None = None) -> di
     x = None
     for _ in range(steps):
         x = next(it)
+        if x is None:  # a BlockGuard'ed block failed on this rank
+            break
         rows += (x[0] if isinstance(x, (tuple, list)) else x).shape[0]
         if trace is not None:
             trace.append(time.perf_counter() - t0)
@@ -385,7 +423,13 @@ def time_steps(R: Rank, it, steps: int, loader, trace: list | None = None) -> di
     el = time.perf_counter() - t0
     if trace is not None:
         trace.append(el)
-    per_rank = R.gather([el, float(rows)])
+    err = getattr(it, "error", None)
+    gathered = R.gather([el, float(rows), 0.0 if err is None else 1.0])
+    failed = [r for r, g in enumerate(gathered) if g[2]]
+    if failed:
+        raise RuntimeError(f"block failed on rank(s) {failed}"
+                           + (f": {type(err).__name__}: {err}" if err is not None else ""))
+    per_rank = [g[:2] for g in gathered]
     tmax = max(p[0] for p in per_rank)
     total = sum(p[1] for p in per_rank)
     st = loader.stats_summary()
@@ -524,7 +568,17 @@ def bridge_codec_block(R: "Rank", args, broker, mine, n_parts, codec, steps, war
     ld = make_loader(f"bench-bridge-{tag}", dtype, args.h2d, servers=server, topic=topic)
     from torchkafka_amd import auto_commit
 
-    bit = iter(auto_commit(ld))
+    bit = BlockGuard(iter(auto_commit(ld)), ld)
+    try:
+        return _bridge_codec_timed(R, args, ld, bit, codec, steps, warm, live, broker, stage, topic, mine, per,
+                                   warm_per, packed, compress_s)
+    finally:
+        bit.close()
+        ld.close()  # (also after a failure: a lockstep transport leaves, the other ranks stop at once)
+
+
+def _bridge_codec_timed(R, args, ld, bit, codec, steps, warm, live, broker, stage, topic, mine, per, warm_per,
+                        packed, compress_s) -> dict:
     for _ in range(warm):
         next(bit)
     c0 = _bridge_counters(ld)
@@ -585,8 +639,6 @@ def bridge_codec_block(R: "Rank", args, broker, mine, n_parts, codec, steps, war
                      if live else "the whole topic produced before the timed steps"),
         "bridge_errors": sum(br.errors for br in ld._bridges),
     })
-    bit.close()
-    ld.close()
     return blk
 
 
@@ -627,7 +679,6 @@ def run_config_blocks(R: "Rank", args) -> dict:
     (N = 1 only: these are single-GPU configurations)."""
     import importlib
 
-    torch = R.torch
     names = [b for b in args.config_blocks.split(",") if b]
     out: dict = {}
     if R.world != 1 or not names:
@@ -639,45 +690,59 @@ def run_config_blocks(R: "Rank", args) -> dict:
     on_gpu = R.device.type == "cuda"
     for name in names:
         t0 = time.perf_counter()
-        if name == "compute" and on_gpu:
-            m = importlib.import_module("compute_overlap")
-            res = {}
-            for wl, h2d in (("config2", "zerocopy"), ("config2", "dma"), ("config4", "auto")):
-                a = m.parse(["--workload", wl, "--h2d", h2d, "--steps", str(args.compute_steps), "--device", dev,
-                             "--verify", args.verify])
-                res[f"{wl}_{h2d}"] = m.run(a, sync=R.sync)
-            name = "steady_compute"
-        elif name == "train" and on_gpu:
-            m = importlib.import_module("train_step")
-            res = {}
-            for wl, h2d in (("config2", "zerocopy"), ("config2", "dma"), ("config4", "auto")):
-                a = m.parse(["--workload", wl, "--h2d", h2d, "--steps", str(args.train_steps), "--device", dev,
-                             "--verify", args.verify])
-                res[f"{wl}_{h2d}"] = m.run(a, sync=R.sync)
-            name = "train_step"
-        elif name == "config4" and on_gpu:
-            m = importlib.import_module("config4_json_varlen")
-            a = m.parse(["--steps", str(args.config4_steps), "--device", dev, "--verify", args.verify])
-            res = m.run(a, sync=R.sync)
-            res.pop("loader", None)
-        elif name == "config5" and on_gpu:
-            m = importlib.import_module("config5_large_messages")
-            a = m.parse(["--steps", str(args.config5_steps), "--device", dev, "--verify", args.verify])
-            res = m.run(a, sync=R.sync)
-            res.pop("loader", None)
-        elif name == "process":
-            m = importlib.import_module("process_override")
-            res = m.run(m.parse(["--steps", str(args.process_steps), "--device", dev]), sync=R.sync)
-            name = "process_override"
-        elif name == "config1":
-            m = importlib.import_module("config1_cpu_plumbing")
-            res = m.run(m.parse(["--records", str(args.config1_records)]))
-        else:
+        try:
+            got = _config_block(R, args, m_import=importlib.import_module, name=name, dev=dev, on_gpu=on_gpu)
+        except Exception as e:  # noqa: BLE001 - reported in the line, the run goes on
+            out[name] = {"error": f"{type(e).__name__}: {e}"[:500], "block_wall_s": round(time.perf_counter() - t0, 2)}
+            _progress(R, f"{name} block failed: {e}")
             continue
+        if got is None:
+            continue
+        name, res = got
         res["block_wall_s"] = round(time.perf_counter() - t0, 2)
         _progress(R, f"{name} block done in {res['block_wall_s']} s")
         out[name] = res
     return out
+
+
+def _config_block(R: "Rank", args, m_import, name: str, dev: str, on_gpu: bool):
+    """One of run_config_blocks' blocks: (the name it is reported under, its result), or None."""
+    if name == "compute" and on_gpu:
+        m = m_import("compute_overlap")
+        res = {}
+        for wl, h2d in (("config2", "zerocopy"), ("config2", "dma"), ("config4", "auto")):
+            a = m.parse(["--workload", wl, "--h2d", h2d, "--steps", str(args.compute_steps), "--device", dev,
+                         "--verify", args.verify])
+            res[f"{wl}_{h2d}"] = m.run(a, sync=R.sync)
+        name = "steady_compute"
+    elif name == "train" and on_gpu:
+        m = m_import("train_step")
+        res = {}
+        for wl, h2d in (("config2", "zerocopy"), ("config2", "dma"), ("config4", "auto")):
+            a = m.parse(["--workload", wl, "--h2d", h2d, "--steps", str(args.train_steps), "--device", dev,
+                         "--verify", args.verify])
+            res[f"{wl}_{h2d}"] = m.run(a, sync=R.sync)
+        name = "train_step"
+    elif name == "config4" and on_gpu:
+        m = m_import("config4_json_varlen")
+        a = m.parse(["--steps", str(args.config4_steps), "--device", dev, "--verify", args.verify])
+        res = m.run(a, sync=R.sync)
+        res.pop("loader", None)
+    elif name == "config5" and on_gpu:
+        m = m_import("config5_large_messages")
+        a = m.parse(["--steps", str(args.config5_steps), "--device", dev, "--verify", args.verify])
+        res = m.run(a, sync=R.sync)
+        res.pop("loader", None)
+    elif name == "process":
+        m = m_import("process_override")
+        res = m.run(m.parse(["--steps", str(args.process_steps), "--device", dev]), sync=R.sync)
+        name = "process_override"
+    elif name == "config1":
+        m = m_import("config1_cpu_plumbing")
+        res = m.run(m.parse(["--records", str(args.config1_records)]))
+    else:
+        return None
+    return name, res
 
 
 def run_rank(args) -> int:
@@ -862,9 +927,24 @@ def run_rank(args) -> int:
                          verify=other_verify if name == "verify" else None,
                          commit="sync" if name in ("rccl_sync", "shm_sync") else "async",
                          lockstep_mode="rccl" if rccl_block else "shm" if shm_block else None)
-        eit = iter(auto_commit(ld))
+        eit = BlockGuard(iter(auto_commit(ld)), ld)
+        try:
+            extra_timed(name, ld, eit, rccl_block, shm_block)
+        finally:
+            eit.close()
+            ld.close()  # (a failed block: its lockstep transport leaves, the other ranks stop at once)
+            if own_group:
+                dist.destroy_process_group()
+                os.environ.pop("TORCHKAFKA_TORCH_NCCL_ACTIVE", None)
+        if world > 1:
+            R.barrier()
+
+    def extra_timed(name: str, ld, eit, rccl_block: bool, shm_block: bool) -> None:
         for _ in range(extra_warm):
             next(eit)
+        if os.environ.get("TK_BENCH_TEST_FAIL_BLOCK") == name and rank == world - 1:
+            # tests only: one rank's block fails after its warm-up, as a failing next() would
+            eit.fail(RuntimeError(f"test failure injected into block {name} on rank {rank}"))
         eres = time_steps(R, eit, extra_steps, ld)
         if name == "label":  # (features, label): the label is the key the broker wrote, offset % 1000
             xv, lab = eres["last"]
@@ -894,13 +974,17 @@ def run_rank(args) -> int:
             blk["verify_wait_us_per_batch"] = round(eres["stats"].get("verify_wait_us_per_batch", 0.0), 3)
         extra_out[key] = blk
         _progress(R, f"{key} {blk['records_per_s']:.0f} rec/s")
-        eit.close()
-        ld.close()
-        if own_group:
-            dist.destroy_process_group()
-            os.environ.pop("TORCHKAFKA_TORCH_NCCL_ACTIVE", None)
-        if world > 1:
-            R.barrier()
+
+    def guarded(key: str, out: dict, fn) -> None:
+        """Runs one secondary block; a failure is reported in the line under ``key`` instead of ending
+        the run (every rank of a lockstepped block fails with it: the failing rank's transport leaves)."""
+        try:
+            fn()
+        except Exception as e:  # noqa: BLE001 - reported in the line
+            out[key] = {"error": f"{type(e).__name__}: {e}"[:500]}
+            _progress(R, f"{key} failed: {e}")
+            if world > 1:
+                R.barrier()
 
     # the RCCL blocks at N > 1 run last (after the bridge blocks): the first multi-GPU runs of the
     # native RCCL lockstep -- a failure there is reported in the line instead of ending the run
@@ -909,7 +993,7 @@ def run_rank(args) -> int:
         late.append("test_hang")  # tests only: a late block that never returns (the watchdog's path)
     for name in extra:
         if name not in late:
-            extra_block(name)
+            guarded(f"steady_{name}", extra_out, lambda name=name: extra_block(name))
 
     # the Kafka-protocol route: this rank's partitions over a loopback wire server -> bridge replica
     bridge_out = None
@@ -919,11 +1003,12 @@ def run_rank(args) -> int:
         srv = NativeWireServer(broker, profile="kafka4").start()
         bridge_out = {"server": "NativeWireServer (C++), loopback TCP, Kafka 4.x protocol profile",
                       "replica": "KafkaBridge ring replica of this rank's partitions (static shard)"}
-        try:
-            for mode, steps in (("async", bsteps), ("sync", max(1, bsteps // 4))):
-                ld = make_loader(f"bench-bridge-{mode}", dtypes[args.dtype], args.h2d, servers=srv.address,
-                                 commit=mode)
-                bit = iter(auto_commit(ld))
+
+        def bridge_mode(mode: str, steps: int) -> None:
+            ld = make_loader(f"bench-bridge-{mode}", dtypes[args.dtype], args.h2d, servers=srv.address,
+                             commit=mode)
+            bit = BlockGuard(iter(auto_commit(ld)), ld)
+            try:
                 for _ in range(extra_warm):
                     next(bit)
                 for br in ld._bridges:
@@ -948,18 +1033,26 @@ def run_rank(args) -> int:
                 blk["bridge_errors"] = sum(br.errors for br in ld._bridges)
                 bridge_out[mode] = blk
                 _progress(R, f"bridge {mode} {blk['records_per_s']:.0f} rec/s")
+            finally:
                 bit.close()
                 ld.close()
-                if world > 1:
-                    R.barrier()
+            if world > 1:
+                R.barrier()
+
+        def bridge_codec(codec: str) -> None:
+            static = codec.endswith("_static")
+            name = codec[:-len("_static")] if static else codec
+            bridge_out[codec] = bridge_codec_block(R, args, broker, mine, n_parts, name, bsteps, extra_warm,
+                                                   make_loader, srv.address, dtypes[args.dtype], live=not static)
+            _progress(R, f"bridge {codec} {bridge_out[codec]['records_per_s']:.0f} rec/s")
+            if world > 1:
+                R.barrier()
+
+        try:
+            for mode, steps in (("async", bsteps), ("sync", max(1, bsteps // 4))):
+                guarded(mode, bridge_out, lambda mode=mode, steps=steps: bridge_mode(mode, steps))
             for codec in [c for c in args.bridge_codecs.split(",") if c]:
-                static = codec.endswith("_static")
-                name = codec[:-len("_static")] if static else codec
-                bridge_out[codec] = bridge_codec_block(R, args, broker, mine, n_parts, name, bsteps, extra_warm,
-                                                       make_loader, srv.address, dtypes[args.dtype], live=not static)
-                _progress(R, f"bridge {codec} {bridge_out[codec]['records_per_s']:.0f} rec/s")
-                if world > 1:
-                    R.barrier()
+                guarded(codec, bridge_out, lambda codec=codec: bridge_codec(codec))
         finally:
             srv.close()
 
@@ -1057,15 +1150,9 @@ def run_rank(args) -> int:
 
         threading.Thread(target=watchdog, daemon=True, name="bench-late-watchdog").start()
     for name in late:
-        try:
-            if name == "test_hang":
-                time.sleep(3600)
-            extra_block(name)
-        except Exception as e:  # noqa: BLE001 - reported in the line
-            extra_out[f"steady_{name}"] = {"error": f"{type(e).__name__}: {e}"[:500]}
-            _progress(R, f"steady_{name} failed: {e}")
-            if world > 1:
-                R.barrier()
+        if name == "test_hang":
+            time.sleep(3600)
+        guarded(f"steady_{name}", extra_out, lambda name=name: extra_block(name))
 
     if rank == 0 and args.stats:
         print(json.dumps({"loader_stats": stats, "fill_s": t_fill,

@@ -62,6 +62,22 @@ def test_bench_late_block_watchdog_still_prints_the_line():
     assert "watchdog" in out["steady_test_hang"]["error"]
 
 
+def test_bench_failed_block_is_reported_and_the_run_goes_on():
+    """One rank's secondary block fails (session r06_s18: a device CRC verdict in the four-rank dma
+    block): the others leave the lockstepped block at once, the failure is reported under the
+    block's key, and the later blocks and the line still run."""
+    r = _torchrun(2, "bench.py", "--gpus", "2", "--steps", "20", "--warmup", "5", "--device", "cpu",
+                  "--steady-steps", "40", "--extra-blocks", "label,f32", "--extra-steps", "4000", "--workers", "1",
+                  "--partitions-per-gpu", "2", "--bridge-steps", "8", "--bridge-codecs", "",
+                  env={"TK_BENCH_TEST_FAIL_BLOCK": "label"})
+    assert r.returncode == 0, r.stdout[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = lines[0]
+    assert "injected" in out["steady_label"]["error"] or "lockstep" in out["steady_label"]["error"]
+    assert out["steady_f32"]["records_per_s"] > 0 and out["bridge"]["async"]["records_per_s"] > 0
+
+
 def _bench(*args, timeout=240):
     e = dict(os.environ)
     e.pop("WORLD_SIZE", None)

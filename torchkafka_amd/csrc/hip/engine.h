@@ -96,8 +96,9 @@ class Engine {
   // accumulator words the parts of the next launch on `stream` meet in: zeroed once, left zero by
   // every launch, and handed out in rotation over kPartAccSets sets per stream -- the dispatches of
   // one stream may overlap (a launch's first workgroups start before the previous launch's last
-  // ones finished), so consecutive launches must not share words.
-  static constexpr int kPartAccSets = 16;
+  // ones finished), so consecutive launches must not share words.  64 sets (24 KiB per stream): a
+  // set comes back only after 63 later launches on its stream were handed theirs.
+  static constexpr int kPartAccSets = 64;
   int span_parts() const { return span_parts_; }
   // The JSON stage kernel keeps one workgroup per segment unless TORCHKAFKA_SPAN_PARTS is set: its
   // parts each redo the segment's row scan (config 4 through the mirror: 47-50 M with 4 parts

@@ -345,10 +345,15 @@ __device__ __forceinline__ void crc_finish(const uint32_t* wcrc, uint32_t flags,
   if (parts > 1) {
     auto* word = reinterpret_cast<unsigned long long*>(acc);
     const uint32_t bit = 1u << q;
-    const unsigned long long old = atomicXor(word, (static_cast<unsigned long long>(bit) << 32) | c);
+    const unsigned long long old = __hip_atomic_fetch_xor(word, (static_cast<unsigned long long>(bit) << 32) | c,
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if ((uint32_t(old >> 32) | bit) != (1u << parts) - 1u) return;  // another part gives the verdict
     c ^= uint32_t(old);
-    *word = 0ull;  // every part of this launch has arrived: zero for the next one on this stream
+    // every part of this launch has arrived: zero for the launch that reuses the set.  An atomic,
+    // like the parts' xors: the parts run on all 8 XCDs (blocks b .. b + 7), and a plain store
+    // stays in this XCD's L2, not coherent with the atomics of the next user of the word
+    // (MI355X_MICROARCH.md, inter-workgroup visibility: 8-B agent atomics on both sides)
+    __hip_atomic_exchange(word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   constexpr uint32_t kWhole = tk::kSegCrcFirst | tk::kSegCrcLast;
   if ((flags & kWhole) == kWhole) {
