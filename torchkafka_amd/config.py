@@ -63,8 +63,9 @@ PROCESS_ENV = {
     "TORCHKAFKA_MIRROR_COPY_STREAMS": "copy streams of the HBM mirror, partitions split p % n (1..4, default 2)",
     "TORCHKAFKA_HIP_QUEUE": "0: var-len / JSON device decode makes its decode- and mirror-copy-stream HIP calls on "
                             "the stepping thread instead of, in order, on a thread of their own (csrc/hip/hip_queue.h)",
-    "TORCHKAFKA_MIRROR_WAIT": "1: a mirror launch waits for the copy of a chunk still in flight instead of reading "
-                              "that segment from the pinned log (round-3 behaviour; A/B only)",
+    "TORCHKAFKA_MIRROR_WAIT": "1 / 0: a mirror launch waits for the copy of a chunk still in flight / reads that "
+                              "segment from the pinned log (default: waits for fixed-width decode, whose launches "
+                              "split segments over workgroups only then; not for JSON / var-len; A/B only)",
     "TORCHKAFKA_JSON_FUSED_COUNT": "1: with a fixed JSON width (pad_to) the parse kernel counts each device-counted "
                                    "row itself instead of json_count_kernel (GPU time per group -12 %, end to end "
                                    "within noise: profiles/r06_s12)",

@@ -379,7 +379,9 @@ PYBIND11_MODULE(_tkhip, m) {
       .def("set_coalesce_wait_us", &MainDriver::set_coalesce_wait_us, py::arg("us"))
       .def("enable_direct", &MainDriver::enable_direct)
       .def("enable_mirror", &MainDriver::enable_mirror, py::arg("chunk_bytes"), py::arg("chunks_per_partition"),
-           py::arg("copy_streams") = 0)
+           py::arg("copy_streams") = 0, py::arg("wait") = -1)
+      .def_property_readonly("mirror_waits",
+                             [](MainDriver& d) { return d.mirror_waits(); })
       .def_property_readonly("mirror_copy_streams",
                              [](MainDriver& d) { return d.mirror_copy_streams(); })
       .def("set_ahead_depth", &MainDriver::set_ahead_depth)

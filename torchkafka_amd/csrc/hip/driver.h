@@ -179,8 +179,12 @@ class MainDriver {
   // h2d='dma' with device decode: the decode kernels read the logs from an HBM mirror that the copy
   // engines fill chunk by chunk (log_mirror.h) instead of over PCIe from the pinned logs.
   int mirror_copy_streams() const { return pins_->mirror() ? pins_->mirror()->copy_streams() : 0; }
-  void enable_mirror(uint64_t chunk_bytes, int chunks_per_partition, int copy_streams = 0) {
-    pins_->enable_mirror(chunk_bytes, chunks_per_partition, copy_streams);
+  bool mirror_waits() const { return pins_->mirror() && pins_->mirror()->waits(); }
+  // wait: 1 the mirror's launches wait for copies in flight (fixed-width decode: segments may be
+  // split over workgroups), 0 they read those segments from the pinned log, -1 the default (0);
+  // TORCHKAFKA_MIRROR_WAIT overrides either (log_mirror.h)
+  void enable_mirror(uint64_t chunk_bytes, int chunks_per_partition, int copy_streams = 0, int wait = -1) {
+    pins_->enable_mirror(chunk_bytes, chunks_per_partition, copy_streams, wait);
   }
   const LogMirror* mirror() const { return pins_->mirror(); }
   // The decode-stream and mirror HIP calls of this driver go through the HIP command queue
@@ -273,6 +277,12 @@ class MainDriver {
   int64_t ahead_groups_ = 0;  // device-decode groups launched ahead of delivery
   int64_t ahead_ns_ = 0;      // host time forming, allocating and launching them (torch_step.cpp)
   int64_t split_launches_ = 0;  // decode launches with each segment split over workgroups (parts > 1)
+  // Segments are split over workgroups only under a mirror that waits for its copies: with the
+  // no-wait policy (segments whose copy is in flight read from the pinned log) split launches failed
+  // the device CRC check at four ranks on one GPU in 4 of 5 runs, while either one workgroup per
+  // segment or the waiting mirror passed 6 of 6 each (profiles/r06_s21, r06_s23; the parts merge,
+  // the copy-event protocol and SDMA-rewritten lines probed clean alone: tools/probes/*_stress.hip)
+  static bool mirror_splits(const LogMirror* m) { return m && m->waits(); }
   int64_t occ_handed_ = 0, occ_staged_ = 0, occ_samples_ = 0;  // slots launched / staged, summed per step
 
   // Per-iteration constants of the fixed-width fast path (set once by torch_step.cpp's

@@ -156,7 +156,9 @@ void MainDriver::launch_span(const int* slots, const SlotView* const* views, int
     // segments split over parts only when every one is read from HBM: parts multiply the loads in
     // flight of a lone group from the mirror (2 MiB: 30.6 -> 12.6 us with 8), while over PCIe the
     // link is the limit and more workgroups only add their fixed costs (profiles/r05_s30_lane_merge)
-    a.parts = pcie ? 1 : eng_->span_parts();
+    // ... and only when the mirror waits for its copies (LogMirror::waits): with the no-wait policy,
+    // split segments failed the device CRC check at four ranks on one GPU (profiles/r06_s21, s23)
+    a.parts = pcie || !mirror_splits(mirror) ? 1 : eng_->span_parts();
     split_launches_ += a.parts > 1;
     pcie = false;
     if (mirror) mirror->before(stream);
@@ -276,7 +278,7 @@ void MainDriver::launch_json_span(const int* slots, const SlotView* const* views
     off += batch_bytes[k];
   }
   auto flush = [&]() {
-    a.parts = pcie ? 1 : eng_->json_span_parts();  // parts only for segments all read from HBM (launch_span)
+    a.parts = pcie || !mirror_splits(mirror) ? 1 : eng_->json_span_parts();  // as launch_span
     split_launches_ += a.parts > 1;
     pcie = false;
     if (mirror) mirror->before(stream);
@@ -343,7 +345,7 @@ void MainDriver::launch_var_span(const int* slots, const SlotView* const* views,
       a.b[k].rows = reinterpret_cast<const tk::JsonSpanRow*>(a.b[k].slot);
     }
     a.tabs = eng_->span_tables();
-    a.parts = pcie ? 1 : eng_->span_parts();  // parts only for segments all read from HBM (launch_span)
+    a.parts = pcie || !mirror_splits(mirror) ? 1 : eng_->span_parts();  // as launch_span
     a.part_acc = a.parts > 1 ? eng_->part_acc(stream) : nullptr;
     split_launches_ += a.parts > 1;
     pcie = false;

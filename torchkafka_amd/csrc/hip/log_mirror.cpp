@@ -18,7 +18,8 @@ namespace tkh {
     if (_e != hipSuccess) throw std::runtime_error(std::string("log mirror: ") + #expr + ": " + hipGetErrorString(_e)); \
   } while (0)
 
-LogMirror::LogMirror(int device, HipQueue* queue, uint64_t chunk_bytes, int chunks_per_partition, int copy_streams)
+LogMirror::LogMirror(int device, HipQueue* queue, uint64_t chunk_bytes, int chunks_per_partition, int copy_streams,
+                     int wait)
     : device_(device), chunk_(chunk_bytes), K_(chunks_per_partition), q_(queue) {
   if (!q_) throw std::invalid_argument("log mirror: no command queue");
   if (chunk_ < (uint64_t(1) << 20) || chunk_ % 4096 != 0) throw std::invalid_argument("log mirror: chunk must be >= 1 MiB, 4 KiB aligned");
@@ -27,7 +28,7 @@ LogMirror::LogMirror(int device, HipQueue* queue, uint64_t chunk_bytes, int chun
   stride_ = (chunk_ + tk::kSpanSegMax + 256 + 4095) / 4096 * 4096;
   TKM_CHECK(hipSetDevice(device_));
   const char* w = std::getenv("TORCHKAFKA_MIRROR_WAIT");
-  wait_ = w && w[0] == '1';
+  wait_ = w && (w[0] == '0' || w[0] == '1') ? w[0] == '1' : wait == 1;  // the variable wins (A/B runs)
   const char* e = std::getenv("TORCHKAFKA_MIRROR_COPY_STREAMS");
   const int n = e ? std::atoi(e) : copy_streams > 0 ? copy_streams : 2;  // the variable wins (A/B runs)
   cs_.resize(size_t(n < 1 ? 1 : n > 4 ? 4 : n));

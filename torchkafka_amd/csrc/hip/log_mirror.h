@@ -15,7 +15,7 @@
 // its previous chunk.  A segment whose buffer is still in use by the
 // group being formed is served from the pinned log instead (map() returns nullptr).
 //
-// A launch never waits for a copy (the default; TORCHKAFKA_MIRROR_WAIT=1 restores the waits): a
+// A launch never waits for a copy (the no-wait policy; JSON / var-len decode): a
 // segment is served from HBM only once its chunk's copy is known complete, else from the pinned
 // log over PCIe while the copy engines catch up.  A copy stream's completion is learned from one
 // event at a time, re-recorded at its tail once the previous one completed.  Waiting instead made
@@ -52,7 +52,11 @@ class LogMirror {
   // copy_streams: SDMA copy streams (partitions split p % n); TORCHKAFKA_MIRROR_COPY_STREAMS when
   // set, else copy_streams when > 0, else 2.  Each takes one of the process's hardware queues.
   // `queue`: the loader's HIP command queue (Engine::queue), used once set_command_queue(true)
-  LogMirror(int device, HipQueue* queue, uint64_t chunk_bytes, int chunks_per_partition, int copy_streams = 0);
+  // wait: 1 a launch waits for a copy in flight (the stream waits on the copy stream's event), 0
+  // the no-wait policy below, -1 the default (0); TORCHKAFKA_MIRROR_WAIT=0/1 overrides either.
+  LogMirror(int device, HipQueue* queue, uint64_t chunk_bytes, int chunks_per_partition, int copy_streams = 0,
+            int wait = -1);
+  bool waits() const { return wait_; }
   ~LogMirror();
   // The mirror's HIP calls go through the HIP command queue (hip_queue.h) when on.
   void set_command_queue(bool on);

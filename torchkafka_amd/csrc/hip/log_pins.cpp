@@ -62,9 +62,10 @@ void LogPins::enable_direct() {
     throw std::runtime_error("driver: hipMemset failed");
 }
 
-void LogPins::enable_mirror(uint64_t chunk_bytes, int chunks_per_partition, int copy_streams) {
+void LogPins::enable_mirror(uint64_t chunk_bytes, int chunks_per_partition, int copy_streams, int wait) {
   if (!broker_) throw std::runtime_error("DeviceLoader h2d='dma' device decode needs the synthetic broker");
-  mirror_ = std::make_unique<LogMirror>(eng_->device(), &eng_->queue(), chunk_bytes, chunks_per_partition, copy_streams);
+  mirror_ = std::make_unique<LogMirror>(eng_->device(), &eng_->queue(), chunk_bytes, chunks_per_partition, copy_streams,
+                                        wait);
 }
 
 void LogPins::pin_written(const std::vector<uint32_t>& pidxs) {

@@ -53,7 +53,7 @@ class LogPins {
   bool direct() const { return bases_dev_ != nullptr; }
   const uint64_t* bases_dev() const { return bases_dev_; }
   // h2d='dma' with device decode: segments are read from an HBM mirror.
-  void enable_mirror(uint64_t chunk_bytes, int chunks_per_partition, int copy_streams = 0);
+  void enable_mirror(uint64_t chunk_bytes, int chunks_per_partition, int copy_streams = 0, int wait = -1);
   LogMirror* mirror() { return mirror_.get(); }
   const LogMirror* mirror() const { return mirror_.get(); }
   // The address a decode kernel reads a segment from (mirror, else the pinned log); *hbm tells which.

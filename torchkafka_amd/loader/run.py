@@ -152,9 +152,16 @@ class _Run:
                 # stream cannot keep ahead of the decode -- fixed-width 25 M rec/s even without the
                 # lockstep, against 48-50 M with two; JSON under the lockstep 48.5-51.6 M with two,
                 # 32.8 M from the pinned logs (profiles/r05_s35_mirror_rccl).
+                # Fixed-width decode splits a segment over workgroups from HBM, which is kept to a mirror
+                # whose launches wait for copies in flight: the no-wait policy with split segments failed
+                # the device CRC check at four ranks on one GPU (profiles/r06_s21, r06_s23; N = 1 dma
+                # block 47.7-48.0 M rec/s waiting against 41.1-45.5 M not).  JSON / var-len decode keep
+                # one workgroup per segment and the no-wait policy (round 4: config 4 waits cost it).
                 self.mirror = L.plan.mirror
                 if self.mirror:
-                    self.driver.enable_mirror(int(L.tuning.mirror_chunk_mib) << 20, int(L.tuning.mirror_chunks), 0)
+                    fixed = not (L.plan.json_span or L.plan.var_span)
+                    self.driver.enable_mirror(int(L.tuning.mirror_chunk_mib) << 20, int(L.tuning.mirror_chunks), 0,
+                                              1 if fixed else 0)
                 tun = L.tuning
                 if tun.ahead_depth is not None:
                     self.driver.set_ahead_depth(int(tun.ahead_depth))
