@@ -73,8 +73,14 @@ void LogPins::pin_written(const std::vector<uint32_t>& pidxs) {
   eng_->prepare_decode();
   for (uint32_t p : pidxs) {
     if (p >= n_parts_) continue;
-    const uint64_t written = broker_->part(p).log_end_pos.load(std::memory_order_acquire);
-    if (written) ensure(p, written);
+    // a ring log (KafkaBridge replica) whole: its pages are written over lap after lap and stay
+    // pinned, and its first lap otherwise ran at the pin thread's registration rate (~12 GB/s, one
+    // 64 MiB piece per ~5 ms: the compressed bridge blocks, whose timed steps all fell in the first
+    // lap, profiles/r06_s27)
+    const auto& part = broker_->part(p);
+    const uint64_t ring = part.ring_bytes.load(std::memory_order_relaxed);
+    const uint64_t want = ring ? ring : part.log_end_pos.load(std::memory_order_acquire);
+    if (want) ensure(p, want);
   }
 }
 
