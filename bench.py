@@ -599,9 +599,11 @@ def _bridge_codec_timed(R, args, ld, bit, codec, steps, warm, live, broker, stag
     pub = threading.Thread(target=produce, name=f"bench-produce-{codec}")
     t_pub = time.perf_counter()
     pub.start()
-    res = time_steps(R, bit, steps, ld)
-    t_end = time.perf_counter()
-    pub.join()
+    try:
+        res = time_steps(R, bit, steps, ld)
+        t_end = time.perf_counter()
+    finally:
+        pub.join()  # (also when the block failed: the producer's appends end on their own)
     c1 = _bridge_counters(ld)
     if err:
         raise err[0]
