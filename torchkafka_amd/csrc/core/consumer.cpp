@@ -52,11 +52,12 @@ bool Fetcher::has_data(const FetchPart& fp) {
   return fp.position < hw;
 }
 
-void Fetcher::prefault(FetchPart& fp, const uint8_t* log, uint64_t pos, uint64_t log_end) {
+void Fetcher::prefault(FetchPart& fp, const uint8_t* log, uint64_t pos, uint64_t log_end, uint64_t ring) {
   static const long page = sysconf(_SC_PAGESIZE);
   const uint64_t pg = uint64_t(page > 0 ? page : 4096);
   const uint64_t lo = std::max<uint64_t>(pos, fp.populated_end) & ~(pg - 1);
-  const uint64_t hi = std::min<uint64_t>(pos + kPrefaultBytes, (log_end + pg - 1) & ~(pg - 1));
+  const uint64_t hi = ring ? (ring + pg - 1) & ~(pg - 1)  // the whole ring (its pages exist: populate_ring)
+                           : std::min<uint64_t>(pos + kPrefaultBytes, (log_end + pg - 1) & ~(pg - 1));
   if (hi > lo && prefault_ok_) {
 #ifdef MADV_POPULATE_READ
     if (madvise(const_cast<uint8_t*>(log) + lo, hi - lo, MADV_POPULATE_READ) != 0 && errno == EINVAL)

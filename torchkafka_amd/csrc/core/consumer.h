@@ -59,9 +59,13 @@ class Fetcher {
   // madvise(MADV_POPULATE_READ) per kPrefaultBytes.  A worker maps the broker's
   // log files itself, so every first read of a page is a minor fault (the kernel
   // maps 16 pages per fault): ~6 faults per 256 KiB batch, about a quarter of a
-  // worker's fill time.  One syscall per 4 MiB replaces them.
+  // worker's fill time.  One syscall per 4 MiB replaces them.  A ring log (KafkaBridge replica;
+  // `ring` its bytes) is mapped whole at its first read: its writer keeps only just ahead of the
+  // reader when it inflates compressed batches, so per-read prefaults shrank to a batch each and
+  // the first lap's faults stayed on the workers' path (worker fill 47-50 us per batch against
+  // 22 us uncompressed, profiles/r06_s28, r06_s34).
   static constexpr uint64_t kPrefaultBytes = 4u << 20;
-  void prefault(FetchPart& fp, const uint8_t* log, uint64_t pos, uint64_t log_end);
+  void prefault(FetchPart& fp, const uint8_t* log, uint64_t pos, uint64_t log_end, uint64_t ring = 0);
 
   // Group-managed consumers: the assignment epochs of the replicas whose group assigns this
   // fetcher's partitions (replicator.h).  While a fill waits for data it returns early
@@ -199,7 +203,8 @@ size_t Fetcher::scan(FetchPart& fp, size_t max_records, F&& visit, G&& on_batch)
     fp.batch_hint = bi;
     const IndexEntry e = idx[uint64_t(bi) % P.index_capacity];  // ring-indexed (replica ring logs)
     if (!sparse_touch_ && e.pos + e.size > fp.populated_end)
-      prefault(fp, log, e.pos, P.log_end_pos.load(std::memory_order_acquire));
+      prefault(fp, log, e.pos, P.log_end_pos.load(std::memory_order_acquire),
+               P.ring_bytes.load(std::memory_order_relaxed));
     const uint8_t* bp = log + e.pos;
     const BatchHeader h = parse_batch_header(bp, e.size);
     if ((h.attributes >> 5) & 1) {  // control batch (a transaction marker): never delivered, as in Kafka clients
