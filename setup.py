@@ -13,7 +13,7 @@ class BuildNative(build_py):
 
 setup(
     name="torchkafka-amd",
-    version="1.2.0+mi355x.5",
+    version="1.2.0+mi355x.7",
     description="Kafka -> PyTorch streaming with per-batch commits, native on AMD Instinct MI355X (gfx950)",
     license="GPL-3.0-or-later",
     packages=find_packages(include=["torchkafka_amd", "torchkafka_amd.*", "torchkafka"]),

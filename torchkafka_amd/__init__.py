@@ -11,7 +11,7 @@ from .config import LoaderConfig, Tuning
 from .loader import DeviceLoader, KafkaBatch, auto_commit
 from .models import FixedWidth, JsonArray, KafkaDataset, Key, Timestamp, VarLen, WithFields
 
-__version__ = "1.2.0+mi355x.5"
+__version__ = "1.2.0+mi355x.7"
 
 __all__ = ["KafkaDataset", "auto_commit", "DeviceLoader", "KafkaBatch", "LoaderConfig", "Tuning", "FixedWidth",
            "VarLen", "JsonArray", "Key", "Timestamp", "WithFields", "SyntheticBroker", "KafkaBridge", "KafkaWireServer",
